@@ -1,0 +1,240 @@
+// PyTorch bindings for the netsdb_amd CDNA4 kernels (module netsdb_amd._hip_kernels).
+// Every op checks device/dtype/shape on the host BEFORE launching (a bad shape must never reach
+// the GPU) and launches on the current HIP stream so ops compose with hipGraph capture.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+extern "C" {
+int nsdb_gemm_splits(int M, int N, int K, int batch);
+int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const float* bias, int M, int N, int K,
+                      long long lda, long long ldb, long long ldc, long long sA, long long sB, long long sC,
+                      long long sBias, int batch, int splits, int act, int bias_mode, int out_f32, float alpha,
+                      float dropout, unsigned long long seed, hipStream_t stream);
+int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* out, int N, int C, int H, int W,
+                      int OC, int KH, int KW, int stride, int pad, int dil, int ldw, int act, int nchw_out,
+                      int out_f32, hipStream_t stream);
+int nsdb_im2col(const void* X, void* out, int N, int C, int H, int W, int KH, int KW, int stride, int pad, int dil,
+                int ldk, hipStream_t stream);
+int nsdb_softmax_rows(const void* X, int x_f32, const float* bias, void* Y, int y_f32, int R, int N,
+                      long long ldx, long long ldy, int log_out, hipStream_t st);
+int nsdb_bias_act(const void* X, int x_f32, const float* bias, void* Y, int y_f32, int R, int N, int bias_mode,
+                  int act, float dropout, unsigned long long seed, hipStream_t st);
+int nsdb_lstm_cell(const void* gates, int g_f32, const float* c_prev, void* h_out, int h_f32, float* c_out, int B,
+                   int H, hipStream_t st);
+int nsdb_embedding_bag(const void* table, int t_f32, const long long* idx, const long long* offsets,
+                       const float* weights, float* out, int Bn, int D, int mode, hipStream_t st);
+}
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_rc(int rc, const char* what) {
+  TORCH_CHECK(rc == 0, what, " failed with code ", rc, " (", hipGetErrorString((hipError_t)(rc > 0 ? rc : 0)), ")");
+}
+
+void check_cuda(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+}
+
+bool is_f32(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.scalar_type() == torch::kFloat32 || t.scalar_type() == torch::kBFloat16, name,
+              " must be float32 or bfloat16");
+  return t.scalar_type() == torch::kFloat32;
+}
+
+// C = epi(alpha * A @ B^T); A [b?,M,K] bf16, B [b?,N,K] bf16 (row stride may exceed K), bias f32.
+torch::Tensor gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Tensor> bias, int64_t bias_mode,
+                      int64_t act, bool out_f32, double alpha, double dropout, int64_t seed, int64_t splits,
+                      c10::optional<torch::Tensor> out) {
+  check_cuda(A, "A");
+  check_cuda(B, "B");
+  TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && B.scalar_type() == torch::kBFloat16, "A,B must be bf16");
+  TORCH_CHECK(A.dim() == B.dim() && (A.dim() == 2 || A.dim() == 3), "A,B must both be 2-D or 3-D");
+  TORCH_CHECK(A.stride(-1) == 1 && B.stride(-1) == 1, "A,B must be K-contiguous");
+  const bool batched = A.dim() == 3;
+  const int64_t batch = batched ? A.size(0) : 1;
+  TORCH_CHECK(!batched || B.size(0) == batch, "batch mismatch");
+  const int64_t M = A.size(-2), K = A.size(-1), N = B.size(-2);
+  TORCH_CHECK(B.size(-1) == K, "K mismatch: A[...,", K, "] vs B[...,", B.size(-1), "]");
+  TORCH_CHECK(K % 8 == 0, "K must be a multiple of 8 (pad the block storage)");
+  TORCH_CHECK(A.stride(-2) % 8 == 0 && B.stride(-2) % 8 == 0, "row strides must be multiples of 8");
+  TORCH_CHECK(M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31), "dims too large");
+  const float* bptr = nullptr;
+  int64_t sBias = 0;
+  if (bias.has_value() && bias->defined()) {
+    check_cuda(*bias, "bias");
+    TORCH_CHECK(bias->scalar_type() == torch::kFloat32 && bias->is_contiguous(), "bias must be contiguous f32");
+    TORCH_CHECK(bias_mode == 1 || bias_mode == 2, "bias_mode must be 1 (per row) or 2 (per col)");
+    const int64_t blen = bias->size(-1);
+    TORCH_CHECK(blen == (bias_mode == 1 ? M : N), "bias length mismatch");
+    sBias = (bias->dim() == 2) ? blen : 0;
+    TORCH_CHECK(bias->dim() == 1 || bias->size(0) == batch, "bias batch mismatch");
+    bptr = bias->data_ptr<float>();
+  }
+  auto opts = A.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16);
+  torch::Tensor C;
+  if (out.has_value() && out->defined()) {
+    C = *out;
+    TORCH_CHECK(C.scalar_type() == opts.dtype(), "out dtype mismatch");
+    TORCH_CHECK(C.size(-2) == M && C.size(-1) == N && C.stride(-1) == 1, "out shape mismatch");
+  } else {
+    C = batched ? torch::empty({batch, M, N}, opts) : torch::empty({M, N}, opts);
+  }
+  int s = splits > 0 ? (int)splits : nsdb_gemm_splits((int)M, (int)N, (int)K, (int)batch);
+  torch::Tensor ws;
+  float* wsp = nullptr;
+  if (s > 1) {
+    ws = torch::empty({batch * s * M * N}, A.options().dtype(torch::kFloat32));
+    wsp = ws.data_ptr<float>();
+  }
+  const int rc = nsdb_gemm_nt_bf16(
+      A.data_ptr(), B.data_ptr(), C.data_ptr(), wsp, bptr, (int)M, (int)N, (int)K, A.stride(-2), B.stride(-2),
+      C.stride(-2), batched ? A.stride(0) : 0, batched ? B.stride(0) : 0, batched ? C.stride(0) : 0, sBias,
+      (int)batch, s, (int)act, (int)bias_mode, out_f32 ? 1 : 0, (float)alpha, (float)dropout,
+      (unsigned long long)seed, cur_stream());
+  check_rc(rc, "gemm_nt");
+  return C;
+}
+
+int64_t gemm_splits(int64_t M, int64_t N, int64_t K, int64_t batch) {
+  return nsdb_gemm_splits((int)M, (int)N, (int)K, (int)batch);
+}
+
+torch::Tensor conv2d(torch::Tensor X, torch::Tensor Wt, c10::optional<torch::Tensor> bias, int64_t KH, int64_t KW,
+                     int64_t stride, int64_t pad, int64_t dil, int64_t act, bool nchw_out, bool out_f32) {
+  check_cuda(X, "X");
+  check_cuda(Wt, "W");
+  TORCH_CHECK(X.scalar_type() == torch::kBFloat16 && Wt.scalar_type() == torch::kBFloat16, "X,W must be bf16");
+  TORCH_CHECK(X.dim() == 4 && X.is_contiguous(), "X must be contiguous NCHW");
+  TORCH_CHECK(Wt.dim() == 2 && Wt.is_contiguous(), "W must be [OC, ldw] contiguous (im2col column order)");
+  const int64_t N = X.size(0), C = X.size(1), H = X.size(2), W = X.size(3), OC = Wt.size(0), ldw = Wt.size(1);
+  TORCH_CHECK(ldw >= C * KH * KW && ldw % 8 == 0, "W row length must be >= C*KH*KW and a multiple of 8");
+  TORCH_CHECK(stride >= 1 && dil >= 1 && pad >= 0, "bad conv geometry");
+  const int64_t OH = (H + 2 * pad - dil * (KH - 1) - 1) / stride + 1;
+  const int64_t OW = (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1;
+  TORCH_CHECK(OH > 0 && OW > 0, "empty output");
+  const float* bptr = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->scalar_type() == torch::kFloat32 && bias->numel() == OC && bias->is_contiguous(), "bias f32[OC]");
+    check_cuda(*bias, "bias");
+    bptr = bias->data_ptr<float>();
+  }
+  auto opts = X.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16);
+  torch::Tensor out = nchw_out ? torch::empty({N, OC, OH, OW}, opts) : torch::empty({N * OH * OW, OC}, opts);
+  check_rc(nsdb_conv2d_igemm(X.data_ptr(), Wt.data_ptr(), bptr, out.data_ptr(), (int)N, (int)C, (int)H, (int)W,
+                             (int)OC, (int)KH, (int)KW, (int)stride, (int)pad, (int)dil, (int)ldw, (int)act,
+                             nchw_out ? 1 : 0, out_f32 ? 1 : 0, cur_stream()),
+           "conv2d");
+  return out;
+}
+
+torch::Tensor im2col(torch::Tensor X, int64_t KH, int64_t KW, int64_t stride, int64_t pad, int64_t dil, int64_t ldk) {
+  check_cuda(X, "X");
+  TORCH_CHECK(X.scalar_type() == torch::kBFloat16 && X.dim() == 4 && X.is_contiguous(), "X bf16 NCHW contiguous");
+  const int64_t N = X.size(0), C = X.size(1), H = X.size(2), W = X.size(3);
+  TORCH_CHECK(ldk >= C * KH * KW, "ldk too small");
+  const int64_t OH = (H + 2 * pad - dil * (KH - 1) - 1) / stride + 1;
+  const int64_t OW = (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1;
+  torch::Tensor out = torch::empty({N * OH * OW, ldk}, X.options());
+  check_rc(nsdb_im2col(X.data_ptr(), out.data_ptr(), (int)N, (int)C, (int)H, (int)W, (int)KH, (int)KW, (int)stride,
+                       (int)pad, (int)dil, (int)ldk, cur_stream()),
+           "im2col");
+  return out;
+}
+
+torch::Tensor softmax_rows(torch::Tensor X, c10::optional<torch::Tensor> bias, bool out_f32, bool log_out) {
+  check_cuda(X, "X");
+  TORCH_CHECK(X.dim() == 2 && X.stride(-1) == 1, "X must be 2-D row-contiguous");
+  const bool xf = is_f32(X, "X");
+  const float* bptr = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->scalar_type() == torch::kFloat32 && bias->numel() == X.size(1), "bias f32[N]");
+    bptr = bias->data_ptr<float>();
+  }
+  auto Y = torch::empty({X.size(0), X.size(1)}, X.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16));
+  check_rc(nsdb_softmax_rows(X.data_ptr(), xf, bptr, Y.data_ptr(), out_f32, (int)X.size(0), (int)X.size(1),
+                             X.stride(0), Y.stride(0), log_out ? 1 : 0, cur_stream()),
+           "softmax_rows");
+  return Y;
+}
+
+torch::Tensor bias_act(torch::Tensor X, c10::optional<torch::Tensor> bias, int64_t bias_mode, int64_t act,
+                       double dropout, int64_t seed, bool out_f32) {
+  check_cuda(X, "X");
+  TORCH_CHECK(X.dim() == 2 && X.is_contiguous(), "X must be contiguous 2-D");
+  const bool xf = is_f32(X, "X");
+  const float* bptr = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->scalar_type() == torch::kFloat32, "bias f32");
+    TORCH_CHECK(bias->numel() == (bias_mode == 1 ? X.size(0) : X.size(1)), "bias length mismatch");
+    bptr = bias->data_ptr<float>();
+  }
+  auto Y = torch::empty_like(X, X.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16));
+  check_rc(nsdb_bias_act(X.data_ptr(), xf, bptr, Y.data_ptr(), out_f32, (int)X.size(0), (int)X.size(1),
+                         (int)bias_mode, (int)act, (float)dropout, (unsigned long long)seed, cur_stream()),
+           "bias_act");
+  return Y;
+}
+
+std::vector<torch::Tensor> lstm_cell(torch::Tensor gates, c10::optional<torch::Tensor> c_prev, bool h_f32) {
+  check_cuda(gates, "gates");
+  TORCH_CHECK(gates.dim() == 2 && gates.is_contiguous() && gates.size(1) % 4 == 0, "gates [B,4H] contiguous");
+  const bool gf = is_f32(gates, "gates");
+  const int64_t B = gates.size(0), H = gates.size(1) / 4;
+  const float* cp = nullptr;
+  if (c_prev.has_value() && c_prev->defined()) {
+    TORCH_CHECK(c_prev->scalar_type() == torch::kFloat32 && c_prev->numel() == B * H && c_prev->is_contiguous(),
+                "c_prev f32 [B,H]");
+    cp = c_prev->data_ptr<float>();
+  }
+  auto h = torch::empty({B, H}, gates.options().dtype(h_f32 ? torch::kFloat32 : torch::kBFloat16));
+  auto c = torch::empty({B, H}, gates.options().dtype(torch::kFloat32));
+  check_rc(nsdb_lstm_cell(gates.data_ptr(), gf, cp, h.data_ptr(), h_f32, c.data_ptr<float>(), (int)B, (int)H,
+                          cur_stream()),
+           "lstm_cell");
+  return {h, c};
+}
+
+torch::Tensor embedding_bag(torch::Tensor table, torch::Tensor idx, torch::Tensor offsets,
+                            c10::optional<torch::Tensor> weights, int64_t mode) {
+  check_cuda(table, "table");
+  TORCH_CHECK(table.dim() == 2 && table.is_contiguous(), "table [V,D] contiguous");
+  const bool tf = is_f32(table, "table");
+  TORCH_CHECK(idx.scalar_type() == torch::kInt64 && offsets.scalar_type() == torch::kInt64, "int64 idx/offsets");
+  TORCH_CHECK(idx.is_contiguous() && offsets.is_contiguous() && offsets.dim() == 1 && offsets.numel() >= 1,
+              "idx/offsets contiguous");
+  const float* wp = nullptr;
+  if (weights.has_value() && weights->defined()) {
+    TORCH_CHECK(weights->scalar_type() == torch::kFloat32 && weights->numel() == idx.numel(), "weights f32[nnz]");
+    wp = weights->data_ptr<float>();
+  }
+  const int64_t Bn = offsets.numel() - 1, D = table.size(1);
+  auto out = torch::empty({Bn, D}, table.options().dtype(torch::kFloat32));
+  check_rc(nsdb_embedding_bag(table.data_ptr(), tf, (const long long*)idx.data_ptr<int64_t>(), (const long long*)offsets.data_ptr<int64_t>(), wp,
+                              out.data_ptr<float>(), (int)Bn, (int)D, (int)mode, cur_stream()),
+           "embedding_bag");
+  return out;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "netsdb_amd CDNA4 (gfx950) HIP kernels";
+  m.def("gemm_nt", &gemm_nt, "epi(alpha*A@B^T) on MFMA", py::arg("A"), py::arg("B"), py::arg("bias") = py::none(),
+        py::arg("bias_mode") = 0, py::arg("act") = 0, py::arg("out_f32") = false, py::arg("alpha") = 1.0,
+        py::arg("dropout") = 0.0, py::arg("seed") = 0, py::arg("splits") = 0, py::arg("out") = py::none());
+  m.def("gemm_splits", &gemm_splits);
+  m.def("conv2d", &conv2d, py::arg("X"), py::arg("W"), py::arg("bias") = py::none(), py::arg("KH") = 1,
+        py::arg("KW") = 1, py::arg("stride") = 1, py::arg("pad") = 0, py::arg("dil") = 1, py::arg("act") = 0,
+        py::arg("nchw_out") = false, py::arg("out_f32") = false);
+  m.def("im2col", &im2col);
+  m.def("softmax_rows", &softmax_rows, py::arg("X"), py::arg("bias") = py::none(), py::arg("out_f32") = true,
+        py::arg("log_out") = false);
+  m.def("bias_act", &bias_act, py::arg("X"), py::arg("bias") = py::none(), py::arg("bias_mode") = 2,
+        py::arg("act") = 0, py::arg("dropout") = 0.0, py::arg("seed") = 0, py::arg("out_f32") = false);
+  m.def("lstm_cell", &lstm_cell, py::arg("gates"), py::arg("c_prev") = py::none(), py::arg("h_f32") = true);
+  m.def("embedding_bag", &embedding_bag, py::arg("table"), py::arg("idx"), py::arg("offsets"),
+        py::arg("weights") = py::none(), py::arg("mode") = 0);
+}

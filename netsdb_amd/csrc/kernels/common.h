@@ -1,0 +1,67 @@
+// Shared CDNA4 (gfx950) helpers for the netsdb_amd HIP kernels.
+// Wave = 64 lanes; MFMA operands are bf16x8 fragments, accumulators f32x4.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace nsdb {
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8;   // 4 VGPRs, one MFMA A/B fragment
+typedef __attribute__((ext_vector_type(4))) float f32x4;    // 16x16 accumulator (4 regs)
+typedef __attribute__((address_space(3))) void lds_void;
+
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_SIGMOID = 2, ACT_EXP = 3, ACT_TANH = 4 };
+
+__device__ __forceinline__ float bf16_to_f32(unsigned short h) {
+  return __uint_as_float(((unsigned)h) << 16);
+}
+
+// Round-to-nearest-even f32 -> bf16 (NaN kept NaN: see MI355X_MICROARCH correctness table).
+__device__ __forceinline__ unsigned short f32_to_bf16(float f) {
+  unsigned u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (unsigned short)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (unsigned short)(u >> 16);
+}
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+  switch (act) {
+    case ACT_RELU: return v > 0.f ? v : 0.f;
+    case ACT_SIGMOID: return 1.f / (1.f + __expf(-v));
+    case ACT_EXP: return __expf(v);
+    case ACT_TANH: return tanhf(v);
+    default: return v;
+  }
+}
+
+// Counter-based hash RNG (stateless; identical on every launch for a given seed).
+__device__ __forceinline__ float hash_uniform(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed + idx * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+// Bijective XCD-aware remap of a linear workgroup id (cdna_hip_programming.md §5 T1):
+// blocks b and b+8 share an XCD under round-robin dispatch, so give each XCD a
+// contiguous run of tile ids -> neighbouring tiles share that XCD's L2.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  if (nwg <= 8) return bid;
+  const int xcd = bid & 7, pos = bid >> 3;
+  const int q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
+}
+
+__device__ __forceinline__ float wave_reduce_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_reduce_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+}  // namespace nsdb

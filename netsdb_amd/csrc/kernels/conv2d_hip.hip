@@ -1,0 +1,204 @@
+#include "hip/hip_runtime.h"
+// Fused conv2d (implicit GEMM) on CDNA4 matrix cores — the MI355X realisation of netsDB's
+// conv2d_memory_fusion spatial rewriting (reference: src/conv2d_memory_fusion/*:
+// ImageToChunks -> ImageChunksToBlock -> ImageBlockToMatrix -> FFTransposeMult -> FFAggMatrix, and
+// KernelBiasJoin's "+1 bias column"). The reference materialises the im2col matrix
+// (N*OH*OW x C*KH*KW+1) as FFMatrixBlocks in a set and then runs the block GEMM; here the
+// im2col rows never exist in HBM: every lane gathers its own MFMA A fragment (8 consecutive
+// k of one output pixel) straight from the L2/MALL-resident image, the filter panel sits in
+// LDS, and bias (+ optional relu) is applied in the epilogue.
+//
+//   out[p][oc] = act( sum_k im2col(X)[p][k] * W[oc][k] + bias[oc] ),  p = (n, oh, ow)
+//
+// Block = 256 threads = 4 waves; tile = 128 pixels x 64 output channels; each wave owns
+// 32 pixels x 64 channels = 2 x 4 mfma_f32_16x16x32_bf16 accumulators.
+#include "common.h"
+#include <algorithm>
+
+namespace nsdb {
+
+constexpr int CV_BM = 128, CV_BN = 64, CV_KC = 512;      // K staged in LDS in chunks of 512
+constexpr int CV_WROW = CV_KC * 2 + 16;                   // padded LDS row (bytes) of the filter panel
+
+struct ConvParams {
+  const unsigned short* X;   // bf16 [N][C][H][W]
+  const unsigned short* Wt;  // bf16 [OC][ldw]   (im2col column order: c, kh, kw)
+  const float* bias;         // f32 [OC] or null
+  void* out;                 // bf16/f32, NHWC-matrix [N*OH*OW][OC] or NCHW [N][OC][OH][OW]
+  int N, C, H, W, OC, KH, KW, OH, OW;
+  int stride, pad, dil;
+  int K, ldw;
+  int act, nchw_out, out_f32;
+};
+
+__global__ void __launch_bounds__(256, 2) conv2d_igemm_kernel(ConvParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[CV_BN * CV_WROW + CV_KC * 8];
+  char* wpanel = smem;
+  int* koff = reinterpret_cast<int*>(smem + CV_BN * CV_WROW);          // per-k image offset
+  int* khw = koff + CV_KC;                                             // (kh*dil)<<16 | (kw*dil)
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const long long P = (long long)p.N * p.OH * p.OW;
+  const long long p0 = (long long)blockIdx.x * CV_BM;
+  const int oc0 = blockIdx.y * CV_BN;
+  const int HW = p.H * p.W, KHW = p.KH * p.KW;
+
+  // per-lane pixel coordinates for the wave's two 16-pixel m-tiles
+  int pix_base[2], ih0[2], iw0[2];
+  bool pix_ok[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const long long pp = p0 + wave * 32 + i * 16 + (lane & 15);
+    pix_ok[i] = pp < P;
+    const long long q = pix_ok[i] ? pp : 0;
+    const int n = (int)(q / (p.OH * p.OW));
+    const int rem = (int)(q % (p.OH * p.OW));
+    const int oh = rem / p.OW, ow = rem % p.OW;
+    ih0[i] = oh * p.stride - p.pad;
+    iw0[i] = ow * p.stride - p.pad;
+    pix_base[i] = n * p.C * HW;
+  }
+
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int kc = 0; kc < p.K; kc += CV_KC) {
+    const int klen = min(CV_KC, p.K - kc);
+    const int klen32 = (klen + 31) & ~31;
+    __syncthreads();
+    // filter panel [64][klen32] -> LDS (16-B vector loads; zero past K / OC)
+    const int chunks_per_row = klen32 / 8;
+    for (int e = tid; e < CV_BN * chunks_per_row; e += 256) {
+      const int r = e / chunks_per_row, ch = e % chunks_per_row;
+      const int oc = oc0 + r, k = kc + ch * 8;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (oc < p.OC && k < p.ldw) v = *reinterpret_cast<const uint4*>(p.Wt + (long long)oc * p.ldw + k);
+      *reinterpret_cast<uint4*>(wpanel + r * CV_WROW + ch * 16) = v;
+    }
+    for (int k = tid; k < klen32; k += 256) {
+      const int kg = kc + k;
+      if (kg < p.K) {
+        const int c = kg / KHW, r2 = kg % KHW, kh = r2 / p.KW, kw = r2 % p.KW;
+        koff[k] = c * HW + kh * p.dil * p.W + kw * p.dil;
+        khw[k] = ((kh * p.dil) << 16) | (kw * p.dil);
+      } else {
+        koff[k] = 0;
+        khw[k] = 0x7fff7fff;   // always out of bounds -> contributes 0
+      }
+    }
+    __syncthreads();
+
+    for (int ks = 0; ks < klen32; ks += 32) {
+      const int kb = ks + 8 * (lane >> 4);
+      bf16x8 af[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int hw = khw[kb + j];
+          const int ih = ih0[i] + (hw >> 16), iw = iw0[i] + (hw & 0xffff);
+          unsigned short v = 0;
+          if (pix_ok[i] && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W)
+            v = p.X[(long long)pix_base[i] + koff[kb + j] + ih0[i] * p.W + iw0[i]];
+          af[i][j] = (short)v;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(wpanel + (j * 16 + (lane & 15)) * CV_WROW + kb * 2);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+
+  // epilogue: col (oc) = lane&15, row (pixel) = (lane>>4)*4 + r
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int oc = oc0 + j * 16 + (lane & 15);
+    if (oc >= p.OC) continue;
+    const float b = p.bias ? p.bias[oc] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const long long pp = p0 + wave * 32 + i * 16 + (lane >> 4) * 4 + r;
+        if (pp >= P) continue;
+        const float v = apply_act(acc[i][j][r] + b, p.act);
+        long long off;
+        if (p.nchw_out) {
+          const long long n = pp / (p.OH * p.OW), rem = pp % (p.OH * p.OW);
+          off = (n * p.OC + oc) * (long long)(p.OH * p.OW) + rem;
+        } else {
+          off = pp * p.OC + oc;
+        }
+        if (p.out_f32) reinterpret_cast<float*>(p.out)[off] = v;
+        else reinterpret_cast<unsigned short*>(p.out)[off] = f32_to_bf16(v);
+      }
+  }
+}
+
+// Explicit im2col (the reference's materialised ImageToChunks/ImageBlockToMatrix path, kept for the
+// "materialise" plan and for testing). out[p][k] bf16 with ld = ldk (>= K, zero padded).
+__global__ void im2col_kernel(const unsigned short* X, unsigned short* out, int N, int C, int H, int W,
+                              int KH, int KW, int OH, int OW, int stride, int pad, int dil, int ldk) {
+  const long long P = (long long)N * OH * OW;
+  const int K = C * KH * KW;
+  const long long total = P * ldk;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const long long pp = e / ldk;
+    const int k = (int)(e % ldk);
+    unsigned short v = 0;
+    if (k < K) {
+      const int n = (int)(pp / (OH * OW)), rem = (int)(pp % (OH * OW));
+      const int oh = rem / OW, ow = rem % OW;
+      const int c = k / (KH * KW), r2 = k % (KH * KW), kh = r2 / KW, kw = r2 % KW;
+      const int ih = oh * stride - pad + kh * dil, iw = ow * stride - pad + kw * dil;
+      if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+        v = X[(((long long)n * C + c) * H + ih) * W + iw];
+    }
+    out[e] = v;
+  }
+}
+
+}  // namespace nsdb
+
+extern "C" {
+
+int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* out, int N, int C, int H,
+                      int W, int OC, int KH, int KW, int stride, int pad, int dil, int ldw, int act,
+                      int nchw_out, int out_f32, hipStream_t stream) {
+  nsdb::ConvParams p;
+  p.X = (const unsigned short*)X; p.Wt = (const unsigned short*)Wt; p.bias = bias; p.out = out;
+  p.N = N; p.C = C; p.H = H; p.W = W; p.OC = OC; p.KH = KH; p.KW = KW;
+  p.stride = stride; p.pad = pad; p.dil = dil;
+  p.OH = (H + 2 * pad - dil * (KH - 1) - 1) / stride + 1;
+  p.OW = (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1;
+  p.K = C * KH * KW; p.ldw = ldw;
+  if (ldw % 8 != 0 || ldw < p.K || p.OH <= 0 || p.OW <= 0) return -1;
+  if ((long long)N * C * H * W >= 0x7fffffffLL) return -2;   // 32-bit image offsets
+  p.act = act; p.nchw_out = nchw_out; p.out_f32 = out_f32;
+  const long long P = (long long)N * p.OH * p.OW;
+  dim3 grid((unsigned)((P + nsdb::CV_BM - 1) / nsdb::CV_BM), (OC + nsdb::CV_BN - 1) / nsdb::CV_BN);
+  hipLaunchKernelGGL(nsdb::conv2d_igemm_kernel, grid, dim3(256), 0, stream, p);
+  return (int)hipGetLastError();
+}
+
+int nsdb_im2col(const void* X, void* out, int N, int C, int H, int W, int KH, int KW, int stride, int pad,
+                int dil, int ldk, hipStream_t stream) {
+  const int OH = (H + 2 * pad - dil * (KH - 1) - 1) / stride + 1;
+  const int OW = (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1;
+  const long long total = (long long)N * OH * OW * ldk;
+  const int blocks = (int)std::min<long long>((total + 255) / 256, 8192);
+  hipLaunchKernelGGL(nsdb::im2col_kernel, dim3(blocks), dim3(256), 0, stream, (const unsigned short*)X,
+                     (unsigned short*)out, N, C, H, W, KH, KW, OH, OW, stride, pad, dil, ldk);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,182 @@
+#include "hip/hip_runtime.h"
+// Memory-bound row/elementwise kernels (vectorised, one workgroup per row or grid-stride):
+//  * row softmax          — netsDB FFRowAggregate (row sum of exp) + FFOutputLayer (divide), fused
+//                           (reference: src/FF/headers/FFRowAggregate.h, FFOutputLayer.h)
+//  * bias + activation    — FFReluBiasSum / FFTransposeBiasSum / FFTransposeBiasSumSigmoid as a
+//                           standalone epilogue for tensors not produced by the GEMM kernel
+//  * LSTM cell            — src/LSTM (LSTMThreeWaySum -> LSTMHiddenState gate math), fused
+//  * embedding bag        — src/word2vec EmbeddingLookupSparse / EmbeddingSegment (gather + segment sum)
+#include "common.h"
+#include <algorithm>
+
+namespace nsdb {
+
+template <typename T> __device__ __forceinline__ float ld(const T* p, long long i);
+template <> __device__ __forceinline__ float ld<float>(const float* p, long long i) { return p[i]; }
+template <> __device__ __forceinline__ float ld<unsigned short>(const unsigned short* p, long long i) {
+  return bf16_to_f32(p[i]);
+}
+__device__ __forceinline__ void st(float* p, long long i, float v) { p[i] = v; }
+__device__ __forceinline__ void st(unsigned short* p, long long i, float v) { p[i] = f32_to_bf16(v); }
+
+__device__ __forceinline__ float block_reduce(float v, float* red, bool is_max) {
+  v = is_max ? wave_reduce_max(v) : wave_reduce_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float r = red[0];
+  for (int i = 1; i < nw; ++i) r = is_max ? fmaxf(r, red[i]) : r + red[i];
+  return r;
+}
+
+// softmax over rows of X[R][N] (+ optional per-column bias), online max/sum in one read pass.
+template <typename TI, typename TO>
+__global__ void __launch_bounds__(256) softmax_rows_kernel(const TI* X, const float* bias, TO* Y, int R, int N,
+                                                           long long ldx, long long ldy, int log_out) {
+  __shared__ float red[8];
+  const int row = blockIdx.x;
+  if (row >= R) return;
+  const TI* x = X + (long long)row * ldx;
+  float m = -INFINITY, s = 0.f;
+  for (int j = threadIdx.x; j < N; j += blockDim.x) {
+    const float v = ld(x, j) + (bias ? bias[j] : 0.f);
+    if (v > m) { s = s * __expf(m - v) + 1.f; m = v; }
+    else s += __expf(v - m);
+  }
+  const float gm = block_reduce(m, red, true);
+  s = (m == -INFINITY) ? 0.f : s * __expf(m - gm);
+  const float gs = block_reduce(s, red, false);
+  const float inv = 1.f / gs, lgs = logf(gs);
+  TO* y = Y + (long long)row * ldy;
+  for (int j = threadIdx.x; j < N; j += blockDim.x) {
+    const float v = ld(x, j) + (bias ? bias[j] : 0.f);
+    st(y, j, log_out ? (v - gm - lgs) : __expf(v - gm) * inv);
+  }
+}
+
+// y = dropout(act(x + bias[row|col])) elementwise over [R][N]
+template <typename TI, typename TO>
+__global__ void __launch_bounds__(256) bias_act_kernel(const TI* X, const float* bias, TO* Y, int R, int N,
+                                                       int bias_mode, int act, float dropout,
+                                                       unsigned long long seed) {
+  const long long total = (long long)R * N;
+  const float keep_scale = dropout > 0.f ? 1.f / (1.f - dropout) : 1.f;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    float v = ld(X, e);
+    if (bias) v += bias_mode == 1 ? bias[e / N] : bias[e % N];
+    v = apply_act(v, act);
+    if (dropout > 0.f) v = hash_uniform(seed, e) < dropout ? 0.f : v * keep_scale;
+    st(Y, e, v);
+  }
+}
+
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+
+// gates[B][4H] laid out (i, f, g, o); c_prev f32 [B][H]; outputs h (bf16|f32) and c (f32)
+template <typename TG, typename TH>
+__global__ void __launch_bounds__(256) lstm_cell_kernel(const TG* gates, const float* c_prev, TH* h_out,
+                                                        float* c_out, int B, int H) {
+  const long long total = (long long)B * H;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const long long b = e / H, j = e % H;
+    const TG* g = gates + b * 4 * H;
+    const float ig = sigm(ld(g, j)), fg = sigm(ld(g, H + j)), gg = tanhf(ld(g, 2 * H + j)),
+                og = sigm(ld(g, 3 * H + j));
+    const float c = fg * (c_prev ? c_prev[e] : 0.f) + ig * gg;
+    c_out[e] = c;
+    st(h_out, e, og * tanhf(c));
+  }
+}
+
+// out[b][:] = reduce_{i in [offsets[b], offsets[b+1])} w_i * table[idx[i]][:]   (mode 0 sum, 1 mean)
+template <typename TT>
+__global__ void __launch_bounds__(256) embedding_bag_kernel(const TT* table, const long long* idx,
+                                                            const long long* offsets, const float* weights,
+                                                            float* out, int Bn, int D, int mode) {
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  if (wave >= Bn) return;
+  const long long s = offsets[wave], e = offsets[wave + 1];
+  for (int d0 = 0; d0 < D; d0 += 64 * 4) {
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    for (long long i = s; i < e; ++i) {
+      const long long r = idx[i];
+      const float w = weights ? weights[i] : 1.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int d = d0 + q * 64 + lane;
+        if (d < D) a[q] += w * ld(table, r * D + d);
+      }
+    }
+    const float sc = (mode == 1 && e > s) ? 1.f / (float)(e - s) : 1.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int d = d0 + q * 64 + lane;
+      if (d < D) out[(long long)wave * D + d] = a[q] * sc;
+    }
+  }
+}
+
+}  // namespace nsdb
+
+static int grid_for(long long n) { return (int)std::min<long long>((n + 255) / 256, 8192); }
+
+extern "C" {
+
+int nsdb_softmax_rows(const void* X, int x_f32, const float* bias, void* Y, int y_f32, int R, int N,
+                      long long ldx, long long ldy, int log_out, hipStream_t st) {
+  if (R <= 0) return 0;
+#define NSDB_SM(TI, TO) \
+  hipLaunchKernelGGL((nsdb::softmax_rows_kernel<TI, TO>), dim3(R), dim3(256), 0, st, (const TI*)X, bias, (TO*)Y, R, N, ldx, ldy, log_out)
+  if (x_f32 && y_f32) NSDB_SM(float, float);
+  else if (x_f32) NSDB_SM(float, unsigned short);
+  else if (y_f32) NSDB_SM(unsigned short, float);
+  else NSDB_SM(unsigned short, unsigned short);
+#undef NSDB_SM
+  return (int)hipGetLastError();
+}
+
+int nsdb_bias_act(const void* X, int x_f32, const float* bias, void* Y, int y_f32, int R, int N, int bias_mode,
+                  int act, float dropout, unsigned long long seed, hipStream_t st) {
+  const long long n = (long long)R * N;
+  if (n <= 0) return 0;
+#define NSDB_BA(TI, TO) \
+  hipLaunchKernelGGL((nsdb::bias_act_kernel<TI, TO>), dim3(grid_for(n)), dim3(256), 0, st, (const TI*)X, bias, (TO*)Y, R, N, bias_mode, act, dropout, seed)
+  if (x_f32 && y_f32) NSDB_BA(float, float);
+  else if (x_f32) NSDB_BA(float, unsigned short);
+  else if (y_f32) NSDB_BA(unsigned short, float);
+  else NSDB_BA(unsigned short, unsigned short);
+#undef NSDB_BA
+  return (int)hipGetLastError();
+}
+
+int nsdb_lstm_cell(const void* gates, int g_f32, const float* c_prev, void* h_out, int h_f32, float* c_out, int B,
+                   int H, hipStream_t st) {
+  const long long n = (long long)B * H;
+  if (n <= 0) return 0;
+#define NSDB_LC(TG, TH) \
+  hipLaunchKernelGGL((nsdb::lstm_cell_kernel<TG, TH>), dim3(grid_for(n)), dim3(256), 0, st, (const TG*)gates, c_prev, (TH*)h_out, c_out, B, H)
+  if (g_f32 && h_f32) NSDB_LC(float, float);
+  else if (g_f32) NSDB_LC(float, unsigned short);
+  else if (h_f32) NSDB_LC(unsigned short, float);
+  else NSDB_LC(unsigned short, unsigned short);
+#undef NSDB_LC
+  return (int)hipGetLastError();
+}
+
+int nsdb_embedding_bag(const void* table, int t_f32, const long long* idx, const long long* offsets,
+                       const float* weights, float* out, int Bn, int D, int mode, hipStream_t st) {
+  if (Bn <= 0) return 0;
+  const int blocks = (Bn * 64 + 255) / 256;
+  if (t_f32)
+    hipLaunchKernelGGL((nsdb::embedding_bag_kernel<float>), dim3(blocks), dim3(256), 0, st, (const float*)table,
+                       idx, offsets, weights, out, Bn, D, mode);
+  else
+    hipLaunchKernelGGL((nsdb::embedding_bag_kernel<unsigned short>), dim3(blocks), dim3(256), 0, st,
+                       (const unsigned short*)table, idx, offsets, weights, out, Bn, D, mode);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

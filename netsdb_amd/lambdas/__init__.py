@@ -1,0 +1,387 @@
+"""UDF lambda trees (reference: src/lambdas/headers/Lambda.h, LambdaCreationFunctions.h,
+AttAccessLambda.h, MethodCallLambda.h, CPlusPlusLambda.h, EqualsLambda.h, AndLambda.h,
+SelfLambda.h, DereferenceLambda.h).
+
+A computation's ``get_selection``/``get_projection``/``get_key_projection`` builds a tree from
+placeholders (:class:`Arg`, the analogue of ``Handle<T> in1``).  The tree is (a) compiled into
+TCAP APPLY/FILTER/HASH atoms, one per node, and (b) evaluated column-at-a-time by the executor:
+attribute and method accesses read whole columns (GPU tensors), comparisons/arithmetic are
+vectorised, and opaque native lambdas either take columns (``vectorized=True``) or fall back to
+object-at-a-time over :class:`RecordView` s.
+"""
+from __future__ import annotations
+
+import itertools
+from typing import Any, Callable, List, Optional, Sequence
+
+import torch
+
+from ..objects.record import RecordBatch, RecordView, column_item
+
+
+class Arg:
+    """Placeholder for the i-th input of a computation (a ``Handle<T>`` parameter)."""
+
+    def __init__(self, index: int, type_: Optional[type] = None):
+        self.index = index
+        self.type = type_
+
+    def __getattr__(self, name):
+        if name.startswith("_"):
+            raise AttributeError(name)
+        # in1.field -> attribute access (sugar; the reference uses makeLambdaFromMember)
+        return AttAccess(self, name)
+
+    def __repr__(self):
+        return f"in{self.index}"
+
+
+class Lambda:
+    """Node of a lambda tree."""
+
+    kind = "lambda"
+
+    def __init__(self, children: Sequence["Lambda"] = (), inputs: Sequence[int] = ()):
+        self.children = list(children)
+        self._inputs = list(inputs)
+        self.name: Optional[str] = None
+
+    # -- structure
+    def input_indices(self) -> List[int]:
+        s = set(self._inputs)
+        for c in self.children:
+            s.update(c.input_indices())
+        return sorted(s)
+
+    def nodes_postorder(self) -> List["Lambda"]:
+        out: List[Lambda] = []
+        for c in self.children:
+            out.extend(c.nodes_postorder())
+        out.append(self)
+        return out
+
+    def assign_names(self, counter=None) -> "Lambda":
+        counter = counter if counter is not None else itertools.count()
+        for n in self.nodes_postorder():
+            if n.name is None:
+                n.name = f"{n.kind}_{next(counter)}"
+        return self
+
+    # -- evaluation: `inputs` are row-aligned RecordBatches (index = computation input index)
+    def eval(self, inputs: Sequence[RecordBatch]):
+        vals = [c.eval(inputs) for c in self.children]
+        return self.eval_node(inputs, vals)
+
+    def eval_node(self, inputs, child_vals):
+        raise NotImplementedError
+
+    # -- operators build trees (reference: operator== / operator&& on LambdaTree)
+    def __eq__(self, other):  # type: ignore[override]
+        return Binary("==", self, _lift(other))
+
+    def __ne__(self, other):  # type: ignore[override]
+        return Binary("!=", self, _lift(other))
+
+    def __and__(self, other):
+        return Binary("&&", self, _lift(other))
+
+    def __or__(self, other):
+        return Binary("||", self, _lift(other))
+
+    def __invert__(self):
+        return Unary("!", self)
+
+    def __gt__(self, other):
+        return Binary(">", self, _lift(other))
+
+    def __ge__(self, other):
+        return Binary(">=", self, _lift(other))
+
+    def __lt__(self, other):
+        return Binary("<", self, _lift(other))
+
+    def __le__(self, other):
+        return Binary("<=", self, _lift(other))
+
+    def __add__(self, other):
+        return Binary("+", self, _lift(other))
+
+    def __sub__(self, other):
+        return Binary("-", self, _lift(other))
+
+    def __mul__(self, other):
+        return Binary("*", self, _lift(other))
+
+    def __truediv__(self, other):
+        return Binary("/", self, _lift(other))
+
+    __hash__ = object.__hash__
+
+    def __repr__(self):
+        return f"{self.kind}({', '.join(map(repr, self.children))})"
+
+
+def _lift(x) -> Lambda:
+    if isinstance(x, Lambda):
+        return x
+    if isinstance(x, Arg):
+        return SelfLambda(x)
+    return Literal(x)
+
+
+class Literal(Lambda):
+    kind = "literal"
+
+    def __init__(self, value):
+        super().__init__()
+        self.value = value
+
+    def eval_node(self, inputs, child_vals):
+        return self.value
+
+
+class SelfLambda(Lambda):
+    """makeLambdaFromSelf: the input object itself (the whole row of that input)."""
+
+    kind = "self"
+
+    def __init__(self, arg: Arg):
+        super().__init__(inputs=[arg.index])
+        self.arg = arg
+
+    def eval_node(self, inputs, child_vals):
+        return SelfRef(inputs[self.arg.index])
+
+
+class SelfRef:
+    """Column value meaning 'the objects of this batch' (materialised lazily)."""
+
+    __slots__ = ("batch",)
+
+    def __init__(self, batch: RecordBatch):
+        self.batch = batch
+
+    def __len__(self):
+        return self.batch.n
+
+    def views(self):
+        return [RecordView(self.batch, i) for i in range(self.batch.n)]
+
+
+class AttAccess(Lambda):
+    kind = "attAccess"
+
+    def __init__(self, arg: Arg, field: str):
+        super().__init__(inputs=[arg.index])
+        self.arg = arg
+        self.field = field
+
+    def eval_node(self, inputs, child_vals):
+        b = inputs[self.arg.index]
+        if self.field in b.columns:
+            return b.columns[self.field]
+        # nested access on an object column is done per record
+        return [getattr(v, self.field) for v in SelfRef(b).views()]
+
+    def __repr__(self):
+        return f"{self.arg}.{self.field}"
+
+
+class MethodCall(Lambda):
+    kind = "methodCall"
+
+    def __init__(self, arg: Arg, method: str):
+        super().__init__(inputs=[arg.index])
+        self.arg = arg
+        self.method = method
+
+    def eval_node(self, inputs, child_vals):
+        b = inputs[self.arg.index]
+        t = b.type
+        fn = getattr(t, self.method, None) if t is not None else None
+        if fn is None:
+            raise AttributeError(f"type {t} has no method {self.method}")
+        vec = getattr(fn, "__vectorized__", None)
+        if vec is not None:
+            return vec(b)
+        return [fn(v) for v in SelfRef(b).views()]
+
+    def __repr__(self):
+        return f"{self.arg}.{self.method}()"
+
+
+class Native(Lambda):
+    """makeLambda(in..., fn): an opaque UDF (CPlusPlusLambda).
+
+    ``vectorized=True``: ``fn`` receives whole columns / batches (SelfRef -> RecordBatch) and must
+    return a column of the batch length — this is how tensor UDFs reach the HIP kernels.
+    Otherwise ``fn`` is called per record with :class:`RecordView` arguments.
+    """
+
+    kind = "native_lambda"
+
+    def __init__(self, args: Sequence[Any], fn: Callable, vectorized: bool = False, tag: Optional[str] = None):
+        kids = [_lift(a) for a in args]
+        super().__init__(children=kids)
+        self.fn = fn
+        self.vectorized = vectorized
+        self.tag = tag  # optional semantic tag (e.g. 'block_matmul') the planner may pattern-match
+
+    def eval_node(self, inputs, child_vals):
+        if self.vectorized:
+            args = [v.batch if isinstance(v, SelfRef) else v for v in child_vals]
+            return self.fn(*args)
+        n = None
+        for v in child_vals:
+            if isinstance(v, SelfRef):
+                n = v.batch.n
+                break
+            if isinstance(v, (list, torch.Tensor)):
+                n = len(v)
+                break
+        if n is None:
+            return self.fn(*child_vals)
+        cols = [_row_accessor(v) for v in child_vals]
+        return [self.fn(*[c(i) for c in cols]) for i in range(n)]
+
+
+def _row_accessor(v):
+    if isinstance(v, SelfRef):
+        b = v.batch
+        return lambda i: RecordView(b, i)
+    if isinstance(v, tuple):
+        return lambda i: tuple(column_item(c, i) for c in v)
+    if isinstance(v, (list, torch.Tensor)):
+        return lambda i: column_item(v, i)
+    return lambda i: v
+
+
+_BIN = {
+    "==": lambda a, b: a == b, "!=": lambda a, b: a != b, ">": lambda a, b: a > b, ">=": lambda a, b: a >= b,
+    "<": lambda a, b: a < b, "<=": lambda a, b: a <= b, "+": lambda a, b: a + b, "-": lambda a, b: a - b,
+    "*": lambda a, b: a * b, "/": lambda a, b: a / b,
+}
+
+
+class Binary(Lambda):
+    def __init__(self, op: str, lhs: Lambda, rhs: Lambda):
+        super().__init__(children=[lhs, rhs])
+        self.op = op
+        self.kind = {"==": "==", "&&": "&&", "||": "||"}.get(op, _OPNAME.get(op, op))
+
+    def eval_node(self, inputs, child_vals):
+        a, b = child_vals
+        if self.op in ("&&", "||"):
+            return _logic(self.op, a, b)
+        if self.op == "==" or self.op == "!=":
+            eq = _equals(a, b)
+            return eq if self.op == "==" else _not(eq)
+        return _elementwise(_BIN[self.op], a, b)
+
+
+_OPNAME = {">": "greaterThan", ">=": "greaterEq", "<": "lessThan", "<=": "lessEq", "+": "plus", "-": "minus",
+           "*": "times", "/": "divide", "!=": "notEquals"}
+
+
+class Unary(Lambda):
+    kind = "not"
+
+    def __init__(self, op: str, x: Lambda):
+        super().__init__(children=[x])
+        self.op = op
+
+    def eval_node(self, inputs, child_vals):
+        return _not(child_vals[0])
+
+
+def _to_tensor_col(v):
+    if isinstance(v, torch.Tensor):
+        return v
+    if isinstance(v, list) and v and isinstance(v[0], (bool, int, float)):
+        return torch.tensor(v)
+    return None
+
+
+def _equals(a, b):
+    if isinstance(a, tuple) and isinstance(b, tuple):
+        out = None
+        for x, y in zip(a, b):
+            e = _equals(x, y)
+            out = e if out is None else _logic("&&", out, e)
+        return out
+    ta, tb = _to_tensor_col(a), _to_tensor_col(b)
+    if ta is not None and (tb is not None or not isinstance(b, (list, SelfRef))):
+        other = tb if tb is not None else b
+        if isinstance(other, torch.Tensor):
+            other = other.to(ta.device)
+        r = ta == other
+        return r if r.dim() <= 1 else r.flatten(1).all(1)
+    return _elementwise(lambda x, y: x == y, a, b)
+
+
+def _logic(op, a, b):
+    ta, tb = _to_tensor_col(a), _to_tensor_col(b)
+    if ta is not None and tb is not None:
+        tb = tb.to(ta.device)
+        return (ta.bool() & tb.bool()) if op == "&&" else (ta.bool() | tb.bool())
+    f = (lambda x, y: bool(x) and bool(y)) if op == "&&" else (lambda x, y: bool(x) or bool(y))
+    return _elementwise(f, a, b)
+
+
+def _not(a):
+    t = _to_tensor_col(a)
+    if t is not None:
+        return ~t.bool()
+    return [not x for x in a]
+
+
+def _elementwise(f, a, b):
+    if isinstance(a, torch.Tensor) and isinstance(b, torch.Tensor):
+        return f(a, b.to(a.device))
+    if isinstance(a, torch.Tensor) and not isinstance(b, (list, SelfRef)):
+        return f(a, b)
+    if isinstance(b, torch.Tensor) and not isinstance(a, (list, SelfRef)):
+        return f(a, b)
+    if isinstance(a, (list, torch.Tensor)) or isinstance(b, (list, torch.Tensor)):
+        n = len(a) if isinstance(a, (list, torch.Tensor)) else len(b)
+        ga, gb = _row_accessor(a), _row_accessor(b)
+        return [f(ga(i), gb(i)) for i in range(n)]
+    return f(a, b)
+
+
+# --------------------------------------------------------------------- creation functions
+def make_lambda_from_member(arg: Arg, member: str) -> Lambda:
+    return AttAccess(arg, member)
+
+
+def make_lambda_from_method(arg: Arg, method: str) -> Lambda:
+    return MethodCall(arg, method)
+
+
+def make_lambda_from_self(arg: Arg) -> Lambda:
+    return SelfLambda(arg)
+
+
+def make_lambda(*args, vectorized: bool = False, tag: Optional[str] = None) -> Lambda:
+    """make_lambda(in1, [in2, ...], fn): the last positional argument is the function."""
+    *ins, fn = args
+    if not callable(fn):
+        raise TypeError("make_lambda(..., fn): last argument must be callable")
+    return Native(ins, fn, vectorized=vectorized, tag=tag)
+
+
+def make_batch_lambda(*args, tag: Optional[str] = None) -> Lambda:
+    """Vectorised native lambda: fn gets RecordBatch / column arguments."""
+    return make_lambda(*args, vectorized=True, tag=tag)
+
+
+# reference-style camelCase aliases
+makeLambda = make_lambda
+makeLambdaFromMember = make_lambda_from_member
+makeLambdaFromMethod = make_lambda_from_method
+makeLambdaFromSelf = make_lambda_from_self
+
+__all__ = ["Arg", "Lambda", "Literal", "SelfLambda", "SelfRef", "AttAccess", "MethodCall", "Native", "Binary",
+           "Unary", "make_lambda", "make_batch_lambda", "make_lambda_from_member", "make_lambda_from_method",
+           "make_lambda_from_self", "makeLambda", "makeLambdaFromMember", "makeLambdaFromMethod",
+           "makeLambdaFromSelf"]

@@ -1,0 +1,375 @@
+"""PDB object model, re-designed columnar for MI355X.
+
+The reference stores C++ objects (``pdb::Object`` + ``Handle`` offset pointers, vtable-fixed
+shared-library types; src/objectModel/headers/Object.h, Handle.h, PDBVector.h, PDBMap.h) in
+pages and runs UDFs object-at-a-time.  Here a *type* is a Python class deriving from
+:class:`PDBObject` whose annotated fields form a schema; a page holds a :class:`RecordBatch` —
+one column per field:
+
+* ``int``/``float``/``bool`` -> 1-D torch tensor (int64 / float64 / bool)
+* ``Tensor(shape, dtype)``  -> one stacked tensor ``[n, *shape]`` (lives in HBM when the set is
+  device-resident: the MatrixBlock payloads of the linear-algebra sets)
+* ``str`` / ``object`` / ``Vector`` -> Python list (host)
+
+UDF lambdas operate on whole columns (vectorised, GPU) or, for opaque Python lambdas, on
+:class:`RecordView` objects (the analogue of dereferencing a ``Handle<T>``).
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Any, Dict, Iterable, List, Optional, Sequence
+
+import torch
+
+
+class Tensor:
+    """Field type for fixed-shape tensor payloads (e.g. a MatrixBlock's rawData)."""
+
+    def __init__(self, shape: Optional[Sequence[int]] = None, dtype: torch.dtype = torch.float32):
+        self.shape = tuple(shape) if shape is not None else None
+        self.dtype = dtype
+
+    def __repr__(self):
+        return f"Tensor({self.shape}, {self.dtype})"
+
+
+class Vector:
+    """Variable-length vector field (pdb::Vector<T>); stored as a list column."""
+
+    def __init__(self, elem=float):
+        self.elem = elem
+
+    def __repr__(self):
+        return f"Vector({getattr(self.elem, '__name__', self.elem)})"
+
+
+SCALAR_TYPES = {int: torch.int64, float: torch.float64, bool: torch.bool}
+
+_REGISTRY: Dict[str, type] = {}
+
+
+def register_type(cls: type) -> type:
+    _REGISTRY[cls.type_name()] = cls
+    return cls
+
+
+def lookup_type(name: str) -> type:
+    if name not in _REGISTRY:
+        raise KeyError(f"type '{name}' is not registered (PDBClient.register_type)")
+    return _REGISTRY[name]
+
+
+def registered_types() -> Dict[str, type]:
+    return dict(_REGISTRY)
+
+
+class PDBObject:
+    """Base class of every storable type. Subclasses declare fields via annotations."""
+
+    __fields__: Dict[str, Any] = {}
+
+    def __init_subclass__(cls, **kw):
+        super().__init_subclass__(**kw)
+        fields: Dict[str, Any] = {}
+        for base in reversed(cls.__mro__[1:]):
+            fields.update(getattr(base, "__fields__", {}))
+        for name, ann in cls.__dict__.get("__annotations__", {}).items():
+            if name.startswith("_"):
+                continue
+            fields[name] = cls.__dict__.get(name, None) if isinstance(cls.__dict__.get(name), (Tensor, Vector)) \
+                else ann
+        cls.__fields__ = fields
+        register_type(cls)
+
+    def __init__(self, *args, **kw):
+        names = list(self.__fields__)
+        if len(args) > len(names):
+            raise TypeError(f"{type(self).__name__} takes {len(names)} fields")
+        for n, v in zip(names, args):
+            setattr(self, n, v)
+        for n, v in kw.items():
+            if n not in self.__fields__:
+                raise TypeError(f"unknown field {n} for {type(self).__name__}")
+            setattr(self, n, v)
+        for n in names:
+            if not hasattr(self, n) or isinstance(getattr(self, n), (Tensor, Vector)):
+                setattr(self, n, _default_for(self.__fields__[n]))
+
+    @classmethod
+    def type_name(cls) -> str:
+        return cls.__name__
+
+    @classmethod
+    def fields(cls) -> Dict[str, Any]:
+        return dict(cls.__fields__)
+
+    def to_dict(self) -> Dict[str, Any]:
+        return {n: getattr(self, n) for n in self.__fields__}
+
+    def __eq__(self, other):
+        if type(other) is not type(self):
+            return NotImplemented
+        for n in self.__fields__:
+            a, b = getattr(self, n), getattr(other, n)
+            if isinstance(a, torch.Tensor) or isinstance(b, torch.Tensor):
+                if not (isinstance(a, torch.Tensor) and isinstance(b, torch.Tensor) and torch.equal(a.cpu(), b.cpu())):
+                    return False
+            elif a != b:
+                return False
+        return True
+
+    def __hash__(self):
+        return hash(tuple(getattr(self, n) for n in self.__fields__ if not isinstance(getattr(self, n), torch.Tensor)))
+
+    def __repr__(self):
+        parts = []
+        for n in self.__fields__:
+            v = getattr(self, n)
+            if isinstance(v, torch.Tensor):
+                v = f"tensor{tuple(v.shape)}"
+            parts.append(f"{n}={v!r}")
+        return f"{type(self).__name__}({', '.join(parts)})"
+
+
+def _default_for(ft):
+    if ft is int:
+        return 0
+    if ft is float:
+        return 0.0
+    if ft is bool:
+        return False
+    if ft is str:
+        return ""
+    if isinstance(ft, Vector):
+        return []
+    return None
+
+
+def column_kind(ft) -> str:
+    if ft in SCALAR_TYPES:
+        return "scalar"
+    if isinstance(ft, Tensor) or ft is torch.Tensor:
+        return "tensor"
+    return "object"
+
+
+class RecordBatch:
+    """Columnar batch of records of one type (or an anonymous tuple set when type is None)."""
+
+    __slots__ = ("type", "columns", "n")
+
+    def __init__(self, columns: Dict[str, Any], n: Optional[int] = None, type_: Optional[type] = None):
+        self.columns = columns
+        self.type = type_
+        if n is None:
+            n = 0
+            for c in columns.values():
+                n = len(c)
+                break
+        self.n = n
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, name):
+        return self.columns[name]
+
+    def names(self) -> List[str]:
+        return list(self.columns)
+
+    @property
+    def device(self) -> torch.device:
+        for c in self.columns.values():
+            if isinstance(c, torch.Tensor):
+                return c.device
+        return torch.device("cpu")
+
+    @staticmethod
+    def from_objects(objs: Sequence[PDBObject], type_: Optional[type] = None,
+                     device: Optional[torch.device] = None) -> "RecordBatch":
+        objs = list(objs)
+        if type_ is None:
+            if not objs:
+                raise ValueError("empty object list needs an explicit type")
+            type_ = type(objs[0])
+        cols: Dict[str, Any] = {}
+        for name, ft in type_.__fields__.items():
+            vals = [getattr(o, name) for o in objs]
+            cols[name] = make_column(vals, ft, device)
+        return RecordBatch(cols, len(objs), type_)
+
+    @staticmethod
+    def empty(type_: type, device=None) -> "RecordBatch":
+        return RecordBatch.from_objects([], type_, device)
+
+    def to_objects(self) -> List[PDBObject]:
+        if self.type is None:
+            return [RecordView(self, i).as_tuple() for i in range(self.n)]
+        out = []
+        for i in range(self.n):
+            o = self.type.__new__(self.type)
+            for name in self.type.__fields__:
+                setattr(o, name, column_item(self.columns[name], i))
+            out.append(o)
+        return out
+
+    def take(self, idx) -> "RecordBatch":
+        """Gather rows (idx: int64 tensor or list)."""
+        cols = {}
+        for k, c in self.columns.items():
+            cols[k] = column_take(c, idx)
+        n = len(idx) if not isinstance(idx, torch.Tensor) else int(idx.numel())
+        return RecordBatch(cols, n, self.type)
+
+    def slice(self, s: int, e: int) -> "RecordBatch":
+        cols = {k: c[s:e] for k, c in self.columns.items()}
+        return RecordBatch(cols, max(0, min(e, self.n) - s), self.type)
+
+    def to(self, device) -> "RecordBatch":
+        cols = {k: (c.to(device, non_blocking=True) if isinstance(c, torch.Tensor) else c)
+                for k, c in self.columns.items()}
+        return RecordBatch(cols, self.n, self.type)
+
+    def nbytes(self) -> int:
+        total = 0
+        for c in self.columns.values():
+            if isinstance(c, torch.Tensor):
+                total += c.numel() * c.element_size()
+            else:
+                total += 16 * len(c) + sum(_obj_size(x) for x in c[:64]) * max(1, len(c) // max(1, min(64, len(c))))
+        return total
+
+    @staticmethod
+    def concat(batches: Sequence["RecordBatch"]) -> "RecordBatch":
+        batches = [b for b in batches if b is not None]
+        if not batches:
+            raise ValueError("nothing to concatenate")
+        nonempty = [b for b in batches if b.n > 0] or batches[:1]
+        first = nonempty[0]
+        cols = {}
+        for k in first.columns:
+            parts = [b.columns[k] for b in nonempty]
+            cols[k] = column_concat(parts)
+        return RecordBatch(cols, sum(b.n for b in nonempty), first.type)
+
+    def __repr__(self):
+        t = self.type.type_name() if self.type else "tuple"
+        return f"RecordBatch<{t}>(n={self.n}, cols={list(self.columns)})"
+
+
+def _obj_size(x) -> int:
+    if isinstance(x, (bytes, str)):
+        return len(x)
+    if isinstance(x, torch.Tensor):
+        return x.numel() * x.element_size()
+    if isinstance(x, (list, tuple)):
+        return 8 * len(x)
+    return 16
+
+
+def make_column(vals: List[Any], ft, device=None):
+    kind = column_kind(ft)
+    if kind == "scalar":
+        return torch.tensor(vals, dtype=SCALAR_TYPES[ft], device=device) if vals else \
+            torch.empty(0, dtype=SCALAR_TYPES[ft], device=device)
+    if kind == "tensor":
+        if not vals:
+            shape = ft.shape if isinstance(ft, Tensor) and ft.shape else (0,)
+            dt = ft.dtype if isinstance(ft, Tensor) else torch.float32
+            return torch.empty((0,) + tuple(shape), dtype=dt, device=device)
+        ts = [v if isinstance(v, torch.Tensor) else torch.as_tensor(v) for v in vals]
+        if all(t.shape == ts[0].shape for t in ts):
+            out = torch.stack(ts)
+            if isinstance(ft, Tensor) and ft.dtype is not None:
+                out = out.to(ft.dtype)
+            return out.to(device) if device is not None else out
+        return [t.to(device) if device is not None else t for t in ts]
+    return list(vals)
+
+
+def column_item(c, i):
+    if isinstance(c, torch.Tensor):
+        v = c[i]
+        return v.item() if v.dim() == 0 else v
+    return c[i]
+
+
+def column_take(c, idx):
+    if isinstance(c, torch.Tensor):
+        if not isinstance(idx, torch.Tensor):
+            idx = torch.as_tensor(idx, dtype=torch.long)
+        return c.index_select(0, idx.to(c.device))
+    if isinstance(idx, torch.Tensor):
+        idx = idx.tolist()
+    return [c[i] for i in idx]
+
+
+def column_concat(parts):
+    if all(isinstance(p, torch.Tensor) for p in parts):
+        if len(parts) == 1:
+            return parts[0]
+        if all(p.shape[1:] == parts[0].shape[1:] for p in parts):
+            dev = parts[0].device
+            return torch.cat([p.to(dev) for p in parts])
+        out = []
+        for p in parts:
+            out.extend(list(p))
+        return out
+    out = []
+    for p in parts:
+        out.extend(list(p) if not isinstance(p, torch.Tensor) else list(p))
+    return out
+
+
+class RecordView:
+    """Object-at-a-time view of row ``i`` of a batch (what a ``Handle<T>`` dereference gives)."""
+
+    __slots__ = ("_b", "_i")
+
+    def __init__(self, batch: RecordBatch, i: int):
+        object.__setattr__(self, "_b", batch)
+        object.__setattr__(self, "_i", i)
+
+    def __getattr__(self, name):
+        b = object.__getattribute__(self, "_b")
+        i = object.__getattribute__(self, "_i")
+        if name in b.columns:
+            return column_item(b.columns[name], i)
+        t = b.type
+        if t is not None and hasattr(t, name):
+            attr = getattr(t, name)
+            if callable(attr):
+                return lambda *a, **k: attr(self, *a, **k)
+            return attr
+        raise AttributeError(name)
+
+    def materialize(self):
+        b = object.__getattribute__(self, "_b")
+        i = object.__getattribute__(self, "_i")
+        if b.type is None:
+            return self.as_tuple()
+        o = b.type.__new__(b.type)
+        for name in b.type.__fields__:
+            setattr(o, name, column_item(b.columns[name], i))
+        return o
+
+    def as_tuple(self):
+        b = object.__getattribute__(self, "_b")
+        i = object.__getattribute__(self, "_i")
+        return tuple(column_item(c, i) for c in b.columns.values())
+
+    def __repr__(self):
+        return f"RecordView({self.materialize()!r})"
+
+
+def batch_of(records: Iterable[Any], type_=None, device=None) -> RecordBatch:
+    """Build a batch from PDBObjects or RecordViews."""
+    objs = [r.materialize() if isinstance(r, RecordView) else r for r in records]
+    return RecordBatch.from_objects(objs, type_, device)
+
+
+__all__ = ["PDBObject", "Tensor", "Vector", "RecordBatch", "RecordView", "register_type", "lookup_type",
+           "registered_types", "batch_of", "make_column", "column_item", "column_take", "column_concat",
+           "column_kind"]
+
+_ = dataclasses  # kept for users defining dataclass-style helpers

@@ -1,0 +1,180 @@
+"""Tensor operators used by the netsDB UDF library (block GEMM, conv2d, softmax, ...).
+
+GPU tensors run on the hand-written CDNA4 HIP kernels in ``netsdb_amd/csrc/kernels``; there is
+no silent eager fallback on a GPU (a missing extension raises).  CPU tensors run the plain fp32
+PyTorch reference of the same op — that is the CPU pseudo-cluster path (the reference netsDB is a
+CPU system) and the numerics oracle of the kernel tests.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .. import _ext
+
+ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_EXP, ACT_TANH = 0, 1, 2, 3, 4
+_ACT_NAMES = {"none": 0, None: 0, "relu": 1, "sigmoid": 2, "exp": 3, "tanh": 4}
+
+BIAS_NONE, BIAS_ROW, BIAS_COL = 0, 1, 2
+
+
+def act_code(act) -> int:
+    if isinstance(act, int):
+        return act
+    return _ACT_NAMES[act]
+
+
+def _apply_act(x: torch.Tensor, act: int) -> torch.Tensor:
+    if act == ACT_RELU:
+        return torch.relu(x)
+    if act == ACT_SIGMOID:
+        return torch.sigmoid(x)
+    if act == ACT_EXP:
+        return torch.exp(x)
+    if act == ACT_TANH:
+        return torch.tanh(x)
+    return x
+
+
+def hash_uniform(seed: int, idx: np.ndarray) -> np.ndarray:
+    """Host twin of the kernels' counter-based RNG (common.h hash_uniform)."""
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed & 0xFFFFFFFFFFFFFFFF) + idx.astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return (z >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+
+
+def _dropout_ref(v: torch.Tensor, p: float, seed: int, base: int = 0) -> torch.Tensor:
+    if p <= 0:
+        return v
+    idx = np.arange(v.numel(), dtype=np.uint64) + np.uint64(base)
+    u = torch.from_numpy(hash_uniform(seed, idx)).reshape(v.shape)
+    return torch.where(u < p, torch.zeros_like(v), v / (1.0 - p))
+
+
+def _use_hip(*ts) -> bool:
+    on_gpu = any(t is not None and t.is_cuda for t in ts)
+    if on_gpu:
+        _ext.hip()  # raises loudly when the kernels are missing
+    return on_gpu
+
+
+def gemm_nt(A, B, bias=None, bias_mode=BIAS_NONE, act=ACT_NONE, out_dtype=torch.bfloat16, alpha=1.0,
+            dropout=0.0, seed=0, splits=0, out=None):
+    """epilogue(alpha * A @ B^T): A [..,M,K], B [..,N,K] (K-contiguous), bias f32 per row/col."""
+    act = act_code(act)
+    if _use_hip(A, B):
+        if bias is not None and bias.dtype != torch.float32:
+            bias = bias.float()
+        return _ext.hip().gemm_nt(A, B, bias, int(bias_mode if bias is not None else 0), act,
+                                  out_dtype == torch.float32, float(alpha), float(dropout), int(seed),
+                                  int(splits), out)
+    v = torch.matmul(A.float(), B.float().transpose(-1, -2)) * alpha
+    if bias is not None:
+        b = bias.float()
+        v = v + (b.unsqueeze(-1) if bias_mode == BIAS_ROW else b.unsqueeze(-2))
+    v = _apply_act(v, act)
+    v = _dropout_ref(v, dropout, seed)
+    v = v.to(out_dtype)
+    if out is not None:
+        out.copy_(v)
+        return out
+    return v
+
+
+def gemm_splits(M, N, K, batch=1) -> int:
+    return int(_ext.hip().gemm_splits(M, N, K, batch))
+
+
+def pad_k(t: torch.Tensor, mult: int = 8) -> torch.Tensor:
+    """Zero-pad the last dim to a multiple of ``mult`` (block storage keeps rows 16-B aligned)."""
+    k = t.shape[-1]
+    kp = (k + mult - 1) // mult * mult
+    if kp == k:
+        return t
+    return torch.nn.functional.pad(t, (0, kp - k))
+
+
+def conv2d(X, Wflat, bias=None, KH=1, KW=1, stride=1, pad=0, dil=1, act=ACT_NONE, nchw_out=False,
+           out_dtype=torch.bfloat16):
+    """Fused implicit-GEMM conv. X [N,C,H,W]; Wflat [OC, >=C*KH*KW] in (c,kh,kw) im2col order."""
+    act = act_code(act)
+    if _use_hip(X, Wflat):
+        if bias is not None and bias.dtype != torch.float32:
+            bias = bias.float()
+        return _ext.hip().conv2d(X, Wflat, bias, KH, KW, stride, pad, dil, act, bool(nchw_out),
+                                 out_dtype == torch.float32)
+    N, C = X.shape[0], X.shape[1]
+    OC = Wflat.shape[0]
+    w = Wflat[:, : C * KH * KW].float().reshape(OC, C, KH, KW)
+    y = torch.nn.functional.conv2d(X.float(), w, bias.float() if bias is not None else None, stride, pad, dil)
+    y = _apply_act(y, act)
+    if not nchw_out:
+        y = y.permute(0, 2, 3, 1).reshape(-1, OC)
+    return y.to(out_dtype)
+
+
+def im2col(X, KH, KW, stride=1, pad=0, dil=1, ldk=None):
+    C = X.shape[1]
+    K = C * KH * KW
+    ldk = ldk or (K + 7) // 8 * 8
+    if _use_hip(X):
+        return _ext.hip().im2col(X, KH, KW, stride, pad, dil, ldk)
+    cols = torch.nn.functional.unfold(X.float(), (KH, KW), dilation=dil, padding=pad, stride=stride)
+    cols = cols.transpose(1, 2).reshape(-1, K)
+    return torch.nn.functional.pad(cols, (0, ldk - K)).to(X.dtype)
+
+
+def softmax_rows(X, bias=None, out_dtype=torch.float32, log=False):
+    if _use_hip(X):
+        return _ext.hip().softmax_rows(X, bias, out_dtype == torch.float32, bool(log))
+    v = X.float() + (bias.float() if bias is not None else 0.0)
+    r = torch.log_softmax(v, dim=-1) if log else torch.softmax(v, dim=-1)
+    return r.to(out_dtype)
+
+
+def bias_act(X, bias=None, bias_mode=BIAS_COL, act=ACT_NONE, dropout=0.0, seed=0, out_dtype=torch.bfloat16):
+    act = act_code(act)
+    if _use_hip(X):
+        if bias is not None and bias.dtype != torch.float32:
+            bias = bias.float()
+        return _ext.hip().bias_act(X.contiguous(), bias, int(bias_mode), act, float(dropout), int(seed),
+                                   out_dtype == torch.float32)
+    v = X.float()
+    if bias is not None:
+        v = v + (bias.float().unsqueeze(-1) if bias_mode == BIAS_ROW else bias.float())
+    v = _dropout_ref(_apply_act(v, act), dropout, seed)
+    return v.to(out_dtype)
+
+
+def lstm_cell(gates, c_prev=None, h_dtype=torch.float32):
+    if _use_hip(gates):
+        return tuple(_ext.hip().lstm_cell(gates.contiguous(), c_prev, h_dtype == torch.float32))
+    g = gates.float()
+    H = g.shape[1] // 4
+    i, f, gg, o = torch.sigmoid(g[:, :H]), torch.sigmoid(g[:, H:2 * H]), torch.tanh(g[:, 2 * H:3 * H]), \
+        torch.sigmoid(g[:, 3 * H:])
+    c = f * (c_prev.float() if c_prev is not None else 0.0) + i * gg
+    h = o * torch.tanh(c)
+    return h.to(h_dtype), c
+
+
+def embedding_bag(table, idx, offsets, weights=None, mode="sum"):
+    m = 1 if mode == "mean" else 0
+    if _use_hip(table):
+        return _ext.hip().embedding_bag(table, idx.long().contiguous(), offsets.long().contiguous(), weights, m)
+    out = torch.zeros(offsets.numel() - 1, table.shape[1], dtype=torch.float32)
+    t = table.float()
+    for b in range(offsets.numel() - 1):
+        s, e = int(offsets[b]), int(offsets[b + 1])
+        if e > s:
+            rows = t[idx[s:e].long()]
+            if weights is not None:
+                rows = rows * weights[s:e].float().unsqueeze(-1)
+            out[b] = rows.sum(0) / ((e - s) if m == 1 else 1)
+    return out
+
+
+__all__ = [n for n in dir() if not n.startswith("_")]

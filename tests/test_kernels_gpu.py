@@ -1,0 +1,125 @@
+"""Numerics of the CDNA4 HIP kernels against plain PyTorch fp32 references of the same op."""
+import pytest
+import torch
+
+from netsdb_amd import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _ref_gemm(A, B, bias=None, mode=0, act=0):
+    v = A.float() @ B.float().transpose(-1, -2)
+    if bias is not None:
+        v = v + (bias.unsqueeze(-1) if mode == 1 else bias.unsqueeze(-2))
+    return ops._apply_act(v, act)
+
+
+def _close(x, ref, tol=2e-2):
+    err = (x.float() - ref).abs().max().item()
+    scale = ref.abs().max().item() + 1e-6
+    assert err <= tol * scale, f"max err {err} vs scale {scale}"
+
+
+def test_gemm_identity_asymmetric():
+    # A = I with an asymmetric B catches a transposed C-write (cdna guide §3)
+    n = 256
+    A = torch.eye(n, device=DEV, dtype=torch.bfloat16)
+    B = (torch.arange(n * n, device=DEV, dtype=torch.float32).reshape(n, n) % 97 - 48).to(torch.bfloat16)
+    C = ops.gemm_nt(A, B, out_dtype=torch.float32)
+    torch.testing.assert_close(C, B.float().t().contiguous(), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (1000, 1000, 4096), (77, 300, 520), (513, 129, 8), (2048, 64, 1024)])
+@pytest.mark.parametrize("splits", [0, 1, 3])
+def test_gemm_shapes(M, N, K, splits):
+    torch.manual_seed(0)
+    A = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    B = torch.randn(N, K, device=DEV).to(torch.bfloat16)
+    C = ops.gemm_nt(A, B, out_dtype=torch.float32, splits=splits)
+    _close(C, _ref_gemm(A, B), tol=1e-2)
+
+
+@pytest.mark.parametrize("mode,act", [(1, ops.ACT_RELU), (2, ops.ACT_SIGMOID), (2, ops.ACT_NONE), (1, ops.ACT_EXP)])
+@pytest.mark.parametrize("splits", [1, 4])
+def test_gemm_epilogue(mode, act, splits):
+    torch.manual_seed(1)
+    M, N, K = 300, 200, 640
+    A = (torch.randn(M, K, device=DEV) * 0.05).to(torch.bfloat16)
+    B = (torch.randn(N, K, device=DEV) * 0.05).to(torch.bfloat16)
+    bias = torch.randn(M if mode == 1 else N, device=DEV)
+    C = ops.gemm_nt(A, B, bias=bias, bias_mode=mode, act=act, out_dtype=torch.float32, splits=splits)
+    _close(C, _ref_gemm(A, B, bias, mode, act), tol=1e-2)
+    Cb = ops.gemm_nt(A, B, bias=bias, bias_mode=mode, act=act, out_dtype=torch.bfloat16, splits=splits)
+    _close(Cb, _ref_gemm(A, B, bias, mode, act), tol=2e-2)
+
+
+def test_gemm_batched_strided():
+    torch.manual_seed(2)
+    A = torch.randn(3, 130, 200, device=DEV).to(torch.bfloat16)[:, :, :192]   # row stride 200 > K
+    B = torch.randn(3, 70, 192, device=DEV).to(torch.bfloat16)
+    C = ops.gemm_nt(A, B, out_dtype=torch.float32)
+    _close(C, _ref_gemm(A, B), tol=1e-2)
+
+
+def test_gemm_dropout_matches_host_rng():
+    torch.manual_seed(3)
+    A = torch.randn(64, 64, device=DEV).to(torch.bfloat16)
+    B = torch.randn(32, 64, device=DEV).to(torch.bfloat16)
+    C = ops.gemm_nt(A, B, out_dtype=torch.float32, dropout=0.5, seed=1234, splits=1)
+    ref = ops.gemm_nt(A.cpu(), B.cpu(), out_dtype=torch.float32, dropout=0.5, seed=1234)
+    assert torch.equal(C.cpu() == 0, ref == 0)
+    _close(C.cpu(), ref, tol=1e-2)
+
+
+@pytest.mark.parametrize("cfg", [
+    dict(N=2, C=3, H=20, W=20, OC=8, KH=7, KW=7, stride=1, pad=0),     # the memfuse 7x7x3 shape, small
+    dict(N=1, C=64, H=14, W=14, OC=70, KH=3, KW=3, stride=2, pad=1),   # K=576 > one LDS K chunk, OC edge
+    dict(N=3, C=16, H=9, W=11, OC=64, KH=1, KW=1, stride=1, pad=0),
+])
+@pytest.mark.parametrize("nchw", [False, True])
+def test_conv2d(cfg, nchw):
+    torch.manual_seed(4)
+    X = torch.randn(cfg["N"], cfg["C"], cfg["H"], cfg["W"], device=DEV).to(torch.bfloat16)
+    K = cfg["C"] * cfg["KH"] * cfg["KW"]
+    Wt = ops.pad_k(torch.randn(cfg["OC"], K, device=DEV) * 0.1).to(torch.bfloat16).contiguous()
+    bias = torch.randn(cfg["OC"], device=DEV)
+    y = ops.conv2d(X, Wt, bias, cfg["KH"], cfg["KW"], cfg["stride"], cfg["pad"], act=ops.ACT_RELU, nchw_out=nchw,
+                   out_dtype=torch.float32)
+    ref = ops.conv2d(X.cpu(), Wt.cpu(), bias.cpu(), cfg["KH"], cfg["KW"], cfg["stride"], cfg["pad"],
+                     act=ops.ACT_RELU, nchw_out=nchw, out_dtype=torch.float32)
+    _close(y.cpu(), ref, tol=1e-2)
+
+
+def test_im2col():
+    X = torch.randn(2, 3, 12, 10, device=DEV).to(torch.bfloat16)
+    a = ops.im2col(X, 3, 3, 1, 1)
+    b = ops.im2col(X.cpu(), 3, 3, 1, 1)
+    torch.testing.assert_close(a.cpu().float(), b.float())
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_softmax_rows(dt):
+    X = (torch.randn(37, 14588, device=DEV) * 3).to(dt)
+    bias = torch.randn(14588, device=DEV)
+    y = ops.softmax_rows(X, bias)
+    _close(y, torch.softmax(X.float() + bias, -1), tol=1e-3)
+    assert torch.allclose(y.sum(-1), torch.ones(37, device=DEV), atol=1e-4)
+
+
+def test_bias_act_and_lstm_and_embedding():
+    X = torch.randn(33, 65, device=DEV)
+    b = torch.randn(33, device=DEV)
+    _close(ops.bias_act(X, b, ops.BIAS_ROW, ops.ACT_RELU, out_dtype=torch.float32), torch.relu(X + b[:, None]), 1e-6)
+    g = torch.randn(16, 4 * 40, device=DEV)
+    c0 = torch.randn(16, 40, device=DEV)
+    h, c = ops.lstm_cell(g, c0)
+    hr, cr = ops.lstm_cell(g.cpu(), c0.cpu())
+    _close(h.cpu(), hr, 1e-5)
+    _close(c.cpu(), cr, 1e-5)
+    table = torch.randn(1000, 300, device=DEV)
+    idx = torch.randint(0, 1000, (50,), device=DEV)
+    offs = torch.tensor([0, 5, 5, 20, 50], device=DEV)
+    e = ops.embedding_bag(table, idx, offs, mode="mean")
+    er = ops.embedding_bag(table.cpu(), idx.cpu(), offs.cpu(), mode="mean")
+    _close(e.cpu(), er, 1e-5)
