@@ -1,0 +1,411 @@
+"""Query execution engine (reference: src/serverFunctionalities/source/{QuerySchedulerServer,
+HermesExecutionServer,FrontendQueryTestServer}.cc, src/queryExecution/source/PipelineStage.cc,
+src/lambdas/headers/{Pipeline,ComputePlan,TupleSetMachine,*Executor,*Sink}.h).
+
+``execute(sinks)``: computation graph -> (tensor-pattern fusion) -> TCAP -> native parser ->
+physical stages -> run every stage on every rank (SPMD).  Each stage streams the pages of its
+source through its atoms batch-at-a-time (a batch is a whole page, so each atom is one big
+vectorised/GPU op) and ends in a sink.  Collectives (shuffle, broadcast, aggregation exchange)
+happen exactly once per sink on every rank, so ranks stay in lock-step.
+"""
+from __future__ import annotations
+
+import time
+from typing import Any, Dict, List, Optional
+
+import torch
+
+from .. import _ext
+from ..computations import AggregateComp, Computation, TopKComp
+from ..lambdas import Literal, SelfRef
+from ..logical_plan.tcap import compile_tcap
+from ..objects.record import PDBObject, RecordBatch, RecordView, batch_of, column_concat
+from ..parallel.comm import ClusterContext
+from ..query_planning.planner import Planner
+from ..utils.trace import Tracer
+from . import kernels as K
+
+
+class _One:
+    """inputs[] shim for a leaf lambda that reads one object column."""
+
+    __slots__ = ("b",)
+
+    def __init__(self, b):
+        self.b = b
+
+    def __getitem__(self, i):
+        return self.b
+
+
+def _normalize(val, n: int, device):
+    if isinstance(val, SelfRef):
+        return val.batch
+    if isinstance(val, (RecordBatch, torch.Tensor, tuple)):
+        return val
+    if isinstance(val, list):
+        if val and isinstance(val[0], PDBObject):
+            return RecordBatch.from_objects(val, type(val[0]))
+        if val and isinstance(val[0], RecordView):
+            return batch_of(val)
+        if val and isinstance(val[0], bool):
+            return torch.tensor(val, dtype=torch.bool)
+        if val and isinstance(val[0], int) and not isinstance(val[0], bool):
+            return torch.tensor(val, dtype=torch.int64)
+        if val and isinstance(val[0], float):
+            return torch.tensor(val, dtype=torch.float64)
+        return val
+    # scalar literal -> broadcast column
+    if isinstance(val, bool):
+        return torch.full((n,), val, dtype=torch.bool, device=device)
+    if isinstance(val, int):
+        return torch.full((n,), val, dtype=torch.int64, device=device)
+    if isinstance(val, float):
+        return torch.full((n,), val, dtype=torch.float64, device=device)
+    return [val] * n
+
+
+class BuildTable:
+    def __init__(self, batch: Optional[RecordBatch], hash_col: str):
+        self.batch = batch
+        self.hash_col = hash_col
+        self.h = batch.columns[hash_col] if batch is not None and batch.n else torch.empty(0, dtype=torch.int64)
+
+
+class JobStats(dict):
+    pass
+
+
+class QueryEngine:
+    def __init__(self, storage, ctx: Optional[ClusterContext] = None, catalog=None, tracer: Optional[Tracer] = None,
+                 broadcast_threshold: int = 2 << 30, fusion: bool = True):
+        self.storage = storage
+        self.ctx = ctx or ClusterContext()
+        self.catalog = catalog
+        self.tracer = tracer or Tracer(enabled=False)
+        self.broadcast_threshold = broadcast_threshold
+        self.fusion = fusion
+        self.last_plan = None
+        self.last_tcap = None
+
+    # ------------------------------------------------------------------ entry
+    def execute(self, sinks: List[Computation], job_name: str = "job") -> JobStats:
+        t0 = time.perf_counter()
+        stats = JobStats(job=job_name, stages=[])
+        sinks = list(sinks)
+        if self.fusion:
+            from ..query_planning.fusion import fuse_tensor_patterns
+
+            sinks, fused = fuse_tensor_patterns(sinks, self)
+            stats["fused_ops"] = fused
+            if not sinks:
+                stats["seconds"] = time.perf_counter() - t0
+                return stats
+        plan = compile_tcap(sinks)
+        self.last_tcap = plan.tcap
+        with self.tracer.span("parse_tcap", job=job_name):
+            atoms = _ext.native().parse_tcap(plan.tcap)
+        planner = Planner(self._scan_size, self.ctx.world_size, self.broadcast_threshold)
+        pplan = planner.plan(atoms)
+        self.last_plan = pplan
+        state = _JobState(plan.computations)
+        for st in pplan.stages:
+            ts = time.perf_counter()
+            with self.tracer.span(f"stage{st.id}", job=job_name, sink=st.sink.get("kind")):
+                n = self._run_stage(st, state)
+            stats["stages"].append({"id": st.id, "desc": st.describe(), "rows_in": n,
+                                    "seconds": time.perf_counter() - ts})
+        stats["seconds"] = time.perf_counter() - t0
+        stats["tcap_atoms"] = len(atoms)
+        return stats
+
+    def _scan_size(self, atom) -> int:
+        try:
+            s = self.storage.get_set(atom["db"], atom["set"])
+        except KeyError:
+            return 0
+        return int(self.ctx.all_reduce_scalar(float(s.nbytes()), "sum")) if self.ctx.distributed else s.nbytes()
+
+    # ------------------------------------------------------------------ stages
+    def _source_batches(self, st, state):
+        src = st.source
+        if src["kind"] == "scan":
+            a = src["atom"]
+            s = self.storage.get_set(a["db"], a["set"])
+            col = a["output"]["atts"][0]
+            for b in s.scan():
+                yield RecordBatch({col: b}, b.n)
+        else:
+            for b in state.materialized.get(src["ts"], []):
+                yield b
+
+    def _run_stage(self, st, state) -> int:
+        # split ops at partitioned-join probes: their inputs must be shuffled collectively first
+        segments: List[List[dict]] = [[]]
+        for o in st.ops:
+            if o["type"] == "JOIN" and o.get("_strategy") == "partitioned":
+                segments.append([o])
+            else:
+                segments[-1].append(o)
+        batches = self._source_batches(st, state)
+        rows = 0
+        for si, seg in enumerate(segments):
+            if si > 0:
+                # collective repartition of the probe side by its join hash
+                probe = seg[0]
+                hcol = probe["input"]["atts"][0] if probe["_probe_side"] == "left" else probe["input2"]["atts"][0]
+                collected = [b for b in batches if b.n]
+                batches = iter(self._shuffle_by(collected, hcol))
+            out = []
+            for b in batches:
+                if si == 0:
+                    rows += b.n
+                for o in seg:
+                    if b.n == 0 and o["type"] != "JOIN":
+                        break
+                    b = self._apply_atom(o, b, state)
+                out.append(b)
+            batches = iter(out)
+        self._sink(st, list(batches), state)
+        return rows
+
+    def _shuffle_by(self, batches: List[RecordBatch], hcol: str) -> List[RecordBatch]:
+        ws = self.ctx.world_size
+        if ws == 1:
+            return batches
+        merged = RecordBatch.concat(batches) if batches else None
+        if merged is None:
+            parts = [None] * ws
+        else:
+            dest = K.partition_of(merged.columns[hcol], ws)
+            parts = K.split_by_dest(merged, dest, ws)
+        return [b for b in self.ctx.exchange(parts) if b is not None]
+
+    # ------------------------------------------------------------------ atoms
+    def _apply_atom(self, a: dict, b: RecordBatch, state) -> RecordBatch:
+        t = a["type"]
+        comp = state.comps.get(a["comp"])
+        if t == "APPLY":
+            args = a["input"]["atts"]
+            carry = a["projection"]["atts"]
+            out_col = a["output"]["atts"][-1]
+            lname = a["lambda"]
+            if lname.startswith("self_in"):
+                val = b.columns[args[0]]
+            else:
+                node = comp.extract_lambdas()[lname]
+                if node.children:
+                    val = node.eval_node(None, [b.columns[x] for x in args])
+                elif isinstance(node, Literal):
+                    val = node.value
+                else:
+                    val = node.eval_node(_One(b.columns[args[0]]), [])
+            val = _normalize(val, b.n, b.device)
+            cols = {c: b.columns[c] for c in carry}
+            cols[out_col] = val
+            return RecordBatch(cols, b.n)
+        if t == "FILTER":
+            mask = b.columns[a["input"]["atts"][0]]
+            if not isinstance(mask, torch.Tensor):
+                mask = torch.tensor([bool(x) for x in mask], dtype=torch.bool)
+            idx = torch.nonzero(mask.bool(), as_tuple=False).flatten()
+            keep = RecordBatch({c: b.columns[c] for c in a["projection"]["atts"]}, b.n)
+            return keep.take(idx)
+        if t in ("HASHLEFT", "HASHRIGHT"):
+            keys = [b.columns[c] for c in a["input"]["atts"]]
+            h = K.hash_keys(keys[0] if len(keys) == 1 else tuple(keys), b.device)
+            cols = {c: b.columns[c] for c in a["projection"]["atts"]}
+            cols[a["output"]["atts"][-1]] = h
+            return RecordBatch(cols, b.n)
+        if t == "HASHONE":
+            cols = {c: b.columns[c] for c in a["projection"]["atts"]}
+            cols[a["output"]["atts"][-1]] = torch.zeros(b.n, dtype=torch.int64, device=b.device)
+            return RecordBatch(cols, b.n)
+        if t == "FLATTEN":
+            vcol = b.columns[a["input"]["atts"][0]]
+            carry = a["projection"]["atts"]
+            lens, flat = [], []
+            for v in (vcol if not isinstance(vcol, RecordBatch) else [vcol]):
+                items = list(v) if not isinstance(v, RecordBatch) else [RecordView(v, i) for i in range(v.n)]
+                lens.append(len(items))
+                flat.extend(items)
+            rep = torch.repeat_interleave(torch.arange(len(lens)), torch.tensor(lens, dtype=torch.int64)) \
+                if lens else torch.empty(0, dtype=torch.int64)
+            cols = {c: RecordBatch({c: b.columns[c]}, b.n).take(rep).columns[c] for c in carry}
+            out_col = a["output"]["atts"][-1]
+            cols[out_col] = _normalize(flat, len(flat), b.device) if flat else []
+            return RecordBatch(cols, len(flat))
+        if t == "JOIN":
+            return self._probe(a, b, state)
+        raise ValueError(f"atom {t} is not streaming")
+
+    def _probe(self, a, b: RecordBatch, state) -> RecordBatch:
+        bt: BuildTable = state.builds[a["output"]["name"]]
+        side = a["_probe_side"]
+        lh, rh = a["input"]["atts"][0], a["input2"]["atts"][0]
+        lcols, rcols = a["projection"]["atts"], a["projection2"]["atts"]
+        probe_h = b.columns[lh if side == "left" else rh]
+        if bt.batch is None or bt.batch.n == 0 or b.n == 0:
+            bi = pi = torch.empty(0, dtype=torch.int64, device=b.device)
+        else:
+            bi, pi = K.join_match(bt.h, probe_h)
+        pb = RecordBatch({c: b.columns[c] for c in (lcols if side == "left" else rcols)}, b.n).take(pi)
+        if bt.batch is None:
+            bb_cols = {c: [] for c in (rcols if side == "left" else lcols)}
+            bbat = RecordBatch(bb_cols, 0)
+        else:
+            bbat = RecordBatch({c: bt.batch.columns[c] for c in (rcols if side == "left" else lcols)}, bt.batch.n).take(bi)
+        cols = {}
+        left, right = (pb, bbat) if side == "left" else (bbat, pb)
+        for c in lcols:
+            cols[c] = left.columns[c]
+        for c in rcols:
+            cols[c] = right.columns[c]
+        return RecordBatch(cols, int(pi.numel()))
+
+    # ------------------------------------------------------------------ sinks
+    def _sink(self, st, batches: List[RecordBatch], state):
+        sk = st.sink
+        kind = sk["kind"]
+        batches = [x for x in batches if x is not None]
+        if kind == "discard":
+            return
+        if kind == "materialize":
+            state.materialized[sk["ts"]] = batches
+            return
+        if kind == "output":
+            a = sk["atom"]
+            col = a["input"]["atts"][0]
+            uset = self.storage.get_set(a["db"], a["set"])
+            for x in batches:
+                if x.n == 0:
+                    continue
+                v = x.columns[col]
+                if not isinstance(v, RecordBatch):
+                    v = RecordBatch({"value": v}, x.n)
+                uset.add_batch(v)
+            return
+        if kind == "join_build":
+            a = sk["atom"]
+            side = sk["side"]
+            hcol = a["input"]["atts"][0] if side == "left" else a["input2"]["atts"][0]
+            cols = (a["projection"]["atts"] if side == "left" else a["projection2"]["atts"]) + [hcol]
+            parts = [RecordBatch({c: x.columns[c] for c in cols}, x.n) for x in batches if x.n]
+            local = RecordBatch.concat(parts) if parts else None
+            strat = sk["strategy"]
+            if strat == "broadcast":
+                got = self.ctx.broadcast_batch_all(local)
+                got = [g for g in got if g is not None and g.n]
+                local = RecordBatch.concat(got) if got else None
+            elif strat == "partitioned":
+                got = self._shuffle_by([local] if local is not None else [], hcol)
+                got = [g for g in got if g.n]
+                local = RecordBatch.concat(got) if got else None
+            state.builds[a["output"]["name"]] = BuildTable(local, hcol)
+            return
+        if kind == "aggregate":
+            self._aggregate(sk["atom"], batches, state)
+            return
+        if kind == "partition":
+            self._partition(sk["atom"], batches, state)
+            return
+        raise ValueError(kind)
+
+    def _aggregate(self, a, batches, state):
+        comp: AggregateComp = state.comps[a["comp"]]
+        kcol, vcol = a["input"]["atts"]
+        out_ts, out_col = a["output"]["name"], a["output"]["atts"][0]
+        nonempty = [x for x in batches if x.n]
+        if isinstance(comp, TopKComp):
+            self._topk(comp, nonempty, kcol, vcol, out_ts, out_col, state)
+            return
+        keys = column_concat([x.columns[kcol] for x in nonempty]) if nonempty else None
+        vals = column_concat([x.columns[vcol] for x in nonempty]) if nonempty else None
+        op = getattr(comp, "reduce_op", "sum")
+        combine = comp.combine
+        if keys is not None:
+            inv, reps, g = K.group_ids(keys)
+            agg = K.segment_reduce(vals, inv, g, op if isinstance(vals, torch.Tensor) else None, combine)
+        else:
+            reps, agg = None, None
+        if self.ctx.distributed:
+            # combiner output -> shuffle by key hash -> final merge (netsDB CombinerProcessor/AggregationProcessor)
+            if reps is not None:
+                kc = reps if isinstance(reps, (tuple, torch.Tensor)) else reps
+                local = RecordBatch({"k": kc, "v": _normalize(agg, len(agg), None)}, len(agg))
+                dest = K.partition_of(K.hash_keys(kc, local.device), self.ctx.world_size)
+                parts = K.split_by_dest(local, dest, self.ctx.world_size)
+            else:
+                parts = [None] * self.ctx.world_size
+            got = [x for x in self.ctx.exchange(parts) if x is not None and x.n]
+            if got:
+                merged = RecordBatch.concat(got)
+                inv, reps, g = K.group_ids(merged.columns["k"])
+                vv = merged.columns["v"]
+                agg = K.segment_reduce(vv, inv, g, op if isinstance(vv, torch.Tensor) else None, combine)
+            else:
+                reps, agg = None, None
+        if reps is None:
+            state.materialized[out_ts] = []
+            return
+        out = comp.make_output(reps, agg)
+        state.materialized[out_ts] = [RecordBatch({out_col: out}, out.n)]
+
+    def _topk(self, comp, batches, kcol, vcol, out_ts, out_col, state):
+        objs, scores = [], []
+        for x in batches:
+            o = x.columns[kcol]
+            s = x.columns[vcol]
+            objs.append(o)
+            scores.append(s if isinstance(s, torch.Tensor) else torch.tensor(s, dtype=torch.float64))
+        if objs:
+            ob = column_concat(objs)
+            sc = torch.cat([s.double().cpu() for s in scores])
+            k = min(comp.k, sc.numel())
+            top = torch.topk(sc, k).indices
+            local = RecordBatch({"o": ob.take(top) if isinstance(ob, RecordBatch) else [ob[i] for i in top.tolist()],
+                                 "s": sc[top]}, k)
+        else:
+            local = None
+        if self.ctx.distributed:
+            got = [g for g in self.ctx.broadcast_batch_all(local) if g is not None and g.n]
+            local = RecordBatch.concat(got) if got else None
+            if local is not None:
+                k = min(comp.k, local.n)
+                local = local.take(torch.topk(local.columns["s"], k).indices)
+            if self.ctx.rank != 0:
+                local = None
+        if local is None or local.n == 0:
+            state.materialized[out_ts] = []
+            return
+        state.materialized[out_ts] = [RecordBatch({out_col: local.columns["o"]}, local.n)]
+
+    def _partition(self, a, batches, state):
+        comp = state.comps[a["comp"]]
+        kcol, ocol = a["input"]["atts"]
+        nonempty = [RecordBatch({"k": x.columns[kcol], "o": x.columns[ocol]}, x.n) for x in batches if x.n]
+        local = RecordBatch.concat(nonempty) if nonempty else None
+        ws = self.ctx.world_size
+        if local is not None:
+            dest = K.partition_of(K.hash_keys(local.columns["k"], local.device), ws)
+            parts = K.split_by_dest(local, dest, ws)
+        else:
+            parts = [None] * ws
+        got = [g for g in self.ctx.exchange(parts) if g is not None and g.n]
+        out_ts, out_col = a["output"]["name"], a["output"]["atts"][0]
+        objs = RecordBatch.concat([g for g in got]).columns["o"] if got else None
+        if objs is not None and getattr(comp, "set_name", "") and self.storage.has_set(comp.db, comp.set_name):
+            self.storage.get_set(comp.db, comp.set_name).add_batch(objs)
+        state.materialized[out_ts] = [RecordBatch({out_col: objs}, objs.n)] if objs is not None else []
+
+
+class _JobState:
+    def __init__(self, comps):
+        self.comps = comps
+        self.materialized: Dict[str, List[RecordBatch]] = {}
+        self.builds: Dict[str, BuildTable] = {}
+
+
+__all__ = ["QueryEngine", "JobStats"]
+
+_ = Any

@@ -236,6 +236,9 @@ class Native(Lambda):
             if isinstance(v, SelfRef):
                 n = v.batch.n
                 break
+            if isinstance(v, RecordBatch):
+                n = v.n
+                break
             if isinstance(v, (list, torch.Tensor)):
                 n = len(v)
                 break
@@ -249,6 +252,8 @@ def _row_accessor(v):
     if isinstance(v, SelfRef):
         b = v.batch
         return lambda i: RecordView(b, i)
+    if isinstance(v, RecordBatch):
+        return lambda i: RecordView(v, i)
     if isinstance(v, tuple):
         return lambda i: tuple(column_item(c, i) for c in v)
     if isinstance(v, (list, torch.Tensor)):

@@ -59,8 +59,12 @@ def compile_lambda(ctx: _Ctx, lam: Lambda, comp_name: str, cur: TupleSpec, obj_c
                    keep: Sequence[str], prefix: str) -> Tuple[TupleSpec, str]:
     """Emit APPLYs for every node of ``lam`` (postorder). Returns (tuple set, result column)."""
     result_col: Dict[int, str] = {}
-    carry = list(keep)
-    for node in lam.nodes_postorder():
+    # intermediate tuple sets carry the kept columns, every input object column and the
+    # results computed so far; the root's APPLY keeps only ``keep`` + its result
+    avail = [c for c in cur.atts]
+    carry = list(keep) + [c for c in obj_cols.values() if c not in keep and c in avail]
+    nodes = lam.nodes_postorder()
+    for pos, node in enumerate(nodes):
         if node.children:
             args = [result_col[id(c)] for c in node.children]
         elif isinstance(node, Literal):
@@ -68,9 +72,11 @@ def compile_lambda(ctx: _Ctx, lam: Lambda, comp_name: str, cur: TupleSpec, obj_c
         else:
             args = [obj_cols[i] for i in node.input_indices()]
         col = f"{prefix}{next(ctx.counter)}"
+        last = pos == len(nodes) - 1
+        this_carry = list(keep) if last else carry
         out = TupleSpec(ctx.tset(f"{node.kind.replace('=', 'eq').replace('&', 'and').replace('|', 'or')}"
-                                 f"OutFor_{comp_name}"), carry + [col])
-        ctx.emit(f"{out} <= APPLY ({TupleSpec(cur.name, args)}, {TupleSpec(cur.name, carry)}, "
+                                 f"OutFor_{comp_name}"), this_carry + [col])
+        ctx.emit(f"{out} <= APPLY ({TupleSpec(cur.name, args)}, {TupleSpec(cur.name, this_carry)}, "
                  f"{_q(comp_name)}, {_q(node.name)})")
         result_col[id(node)] = col
         cur = out

@@ -164,7 +164,7 @@ class RecordBatch:
         if n is None:
             n = 0
             for c in columns.values():
-                n = len(c)
+                n = column_len(c)
                 break
         self.n = n
 
@@ -222,12 +222,11 @@ class RecordBatch:
         return RecordBatch(cols, n, self.type)
 
     def slice(self, s: int, e: int) -> "RecordBatch":
-        cols = {k: c[s:e] for k, c in self.columns.items()}
+        cols = {k: column_slice(c, s, e) for k, c in self.columns.items()}
         return RecordBatch(cols, max(0, min(e, self.n) - s), self.type)
 
     def to(self, device) -> "RecordBatch":
-        cols = {k: (c.to(device, non_blocking=True) if isinstance(c, torch.Tensor) else c)
-                for k, c in self.columns.items()}
+        cols = {k: _col_to(c, device) for k, c in self.columns.items()}
         return RecordBatch(cols, self.n, self.type)
 
     def nbytes(self) -> int:
@@ -235,6 +234,10 @@ class RecordBatch:
         for c in self.columns.values():
             if isinstance(c, torch.Tensor):
                 total += c.numel() * c.element_size()
+            elif isinstance(c, RecordBatch):
+                total += c.nbytes()
+            elif isinstance(c, tuple):
+                total += sum(x.numel() * x.element_size() if isinstance(x, torch.Tensor) else 16 * len(x) for x in c)
             else:
                 total += 16 * len(c) + sum(_obj_size(x) for x in c[:64]) * max(1, len(c) // max(1, min(64, len(c))))
         return total
@@ -255,6 +258,16 @@ class RecordBatch:
     def __repr__(self):
         t = self.type.type_name() if self.type else "tuple"
         return f"RecordBatch<{t}>(n={self.n}, cols={list(self.columns)})"
+
+
+def _col_to(c, device):
+    if isinstance(c, torch.Tensor):
+        return c.to(device, non_blocking=True)
+    if isinstance(c, RecordBatch):
+        return c.to(device)
+    if isinstance(c, tuple):
+        return tuple(_col_to(x, device) for x in c)
+    return c
 
 
 def _obj_size(x) -> int:
@@ -287,7 +300,25 @@ def make_column(vals: List[Any], ft, device=None):
     return list(vals)
 
 
+def column_slice(c, s, e):
+    if isinstance(c, RecordBatch):
+        return c.slice(s, e)
+    if isinstance(c, tuple):
+        return tuple(column_slice(x, s, e) for x in c)
+    return c[s:e]
+
+
+def column_len(c) -> int:
+    if isinstance(c, tuple):
+        return column_len(c[0]) if c else 0
+    return len(c)
+
+
 def column_item(c, i):
+    if isinstance(c, RecordBatch):
+        return RecordView(c, i)
+    if isinstance(c, tuple):
+        return tuple(column_item(x, i) for x in c)
     if isinstance(c, torch.Tensor):
         v = c[i]
         return v.item() if v.dim() == 0 else v
@@ -295,6 +326,10 @@ def column_item(c, i):
 
 
 def column_take(c, idx):
+    if isinstance(c, RecordBatch):
+        return c.take(idx)
+    if isinstance(c, tuple):
+        return tuple(column_take(x, idx) for x in c)
     if isinstance(c, torch.Tensor):
         if not isinstance(idx, torch.Tensor):
             idx = torch.as_tensor(idx, dtype=torch.long)
@@ -305,6 +340,10 @@ def column_take(c, idx):
 
 
 def column_concat(parts):
+    if parts and all(isinstance(p, RecordBatch) for p in parts):
+        return RecordBatch.concat(parts)
+    if parts and all(isinstance(p, tuple) for p in parts):
+        return tuple(column_concat([p[i] for p in parts]) for i in range(len(parts[0])))
     if all(isinstance(p, torch.Tensor) for p in parts):
         if len(parts) == 1:
             return parts[0]
@@ -370,6 +409,6 @@ def batch_of(records: Iterable[Any], type_=None, device=None) -> RecordBatch:
 
 __all__ = ["PDBObject", "Tensor", "Vector", "RecordBatch", "RecordView", "register_type", "lookup_type",
            "registered_types", "batch_of", "make_column", "column_item", "column_take", "column_concat",
-           "column_kind"]
+           "column_kind", "column_slice", "column_len"]
 
 _ = dataclasses  # kept for users defining dataclass-style helpers

@@ -1,0 +1,257 @@
+"""Cluster context and collectives: one process per GPU, torch.distributed over RCCL (xGMI).
+
+Reference: the netsDB shuffle/broadcast machinery — src/communication (PDBCommunicator,
+SimpleSendDataRequest), src/serverFunctionalities/source/{DispatcherServer,BroadcastServer,
+HermesExecutionServer}.cc, src/queryExecution (ShuffleSink, CombinedShuffleSink,
+HashPartitionedJoinBuildHTJobStage, BroadcastJoinBuildHTJobStage) which move serialized pages
+between worker nodes over TCP sockets.
+
+MI355X-native design: every worker is a rank; record batches move with collectives —
+``all_to_all_single`` for hash shuffles (tensor columns stay in HBM and go straight through
+RCCL), ``all_gather`` for broadcast joins, ``reduce_scatter`` for distributed aggregation of
+dense blocks.  Object (host) columns are serialised into byte tensors and ride the same
+collective.  ``backend='gloo'`` runs the identical code path on CPU (tests, pseudo-cluster).
+"""
+from __future__ import annotations
+
+import json
+import os
+from typing import Any, Dict, List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+from ..objects.record import RecordBatch, lookup_type
+from ..storage.serde import _enc_obj, _dec_obj  # noqa: F401  (shared object codec)
+
+
+class ClusterContext:
+    """Rank/device information of this process (a netsDB 'worker node')."""
+
+    def __init__(self, rank: int = 0, world_size: int = 1, device: Optional[torch.device] = None,
+                 backend: Optional[str] = None, group=None):
+        self.rank = rank
+        self.world_size = world_size
+        self.device = device if device is not None else torch.device("cpu")
+        self.backend = backend
+        self.group = group
+
+    @property
+    def distributed(self) -> bool:
+        return self.world_size > 1
+
+    @staticmethod
+    def from_env(device: Optional[str] = None, backend: Optional[str] = None) -> "ClusterContext":
+        """torchrun-style init (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_ADDR/MASTER_PORT)."""
+        ws = int(os.environ.get("WORLD_SIZE", "1"))
+        rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if device is None:
+            device = f"cuda:{local}" if torch.cuda.device_count() > 0 else "cpu"
+        dev = torch.device(device)
+        if dev.type == "cuda":
+            torch.cuda.set_device(dev)
+        if ws > 1 and not dist.is_initialized():
+            be = backend or ("nccl" if dev.type == "cuda" else "gloo")
+            kw = {}
+            if dev.type == "cuda":
+                kw["device_id"] = dev
+            dist.init_process_group(be, rank=rank, world_size=ws, **kw)
+        be = dist.get_backend() if dist.is_initialized() else None
+        return ClusterContext(rank, ws, dev, be)
+
+    # -------------------------------------------------------------- primitives
+    def barrier(self):
+        if self.distributed:
+            if self.device.type == "cuda":
+                dist.barrier(device_ids=[self.device.index])
+            else:
+                dist.barrier()
+
+    def _comm_device(self):
+        return self.device if self.backend == "nccl" else torch.device("cpu")
+
+    def all_reduce(self, t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
+        if self.distributed:
+            dist.all_reduce(t, op=op)
+        return t
+
+    def all_reduce_scalar(self, v: float, op="sum") -> float:
+        if not self.distributed:
+            return v
+        t = torch.tensor([float(v)], dtype=torch.float64, device=self._comm_device())
+        dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
+                               "min": dist.ReduceOp.MIN}[op])
+        return float(t.item())
+
+    def all_gather_tensor(self, t: torch.Tensor) -> List[torch.Tensor]:
+        """Variable-first-dim all_gather (rows)."""
+        if not self.distributed:
+            return [t]
+        cd = self._comm_device()
+        n = torch.tensor([t.shape[0]], dtype=torch.int64, device=cd)
+        ns = [torch.zeros_like(n) for _ in range(self.world_size)]
+        dist.all_gather(ns, n)
+        ns = [int(x.item()) for x in ns]
+        mx = max(ns)
+        src = t.to(cd)
+        if src.shape[0] < mx:
+            src = torch.cat([src, src.new_zeros((mx - src.shape[0],) + tuple(src.shape[1:]))])
+        outs = [torch.empty_like(src) for _ in range(self.world_size)]
+        dist.all_gather(outs, src.contiguous())
+        return [o[:k].to(t.device) for o, k in zip(outs, ns)]
+
+    def all_to_all_rows(self, t: torch.Tensor, send_counts: Sequence[int]) -> (torch.Tensor, List[int]):
+        """Rows of ``t`` (already grouped by destination) -> rows received from every rank."""
+        if not self.distributed:
+            return t, list(send_counts)
+        cd = self._comm_device()
+        sc = torch.tensor(list(send_counts), dtype=torch.int64, device=cd)
+        rc = torch.empty_like(sc)
+        dist.all_to_all_single(rc, sc)
+        recv = [int(x) for x in rc.tolist()]
+        src = t.to(cd).contiguous()
+        out = src.new_empty((sum(recv),) + tuple(src.shape[1:]))
+        if src.dtype == torch.bool:
+            s8, o8 = src.view(torch.uint8), out.view(torch.uint8)
+            dist.all_to_all_single(o8, s8, recv, list(send_counts))
+        else:
+            dist.all_to_all_single(out, src, recv, list(send_counts))
+        return out.to(t.device), recv
+
+    def reduce_scatter_rows(self, t: torch.Tensor, counts: Sequence[int]) -> torch.Tensor:
+        """Sum ``t`` over ranks and return this rank's row slice (counts[r] rows per rank)."""
+        if not self.distributed:
+            return t
+        cd = self._comm_device()
+        if self.backend == "nccl" and len(set(counts)) == 1:
+            out = t.new_empty((counts[self.rank],) + tuple(t.shape[1:]))
+            dist.reduce_scatter_tensor(out, t.contiguous(), op=dist.ReduceOp.SUM)
+            return out
+        full = t.to(cd).contiguous().clone()
+        dist.all_reduce(full)
+        s = sum(counts[: self.rank])
+        return full[s: s + counts[self.rank]].to(t.device)
+
+    def broadcast_object(self, obj: Any, src: int = 0) -> Any:
+        if not self.distributed:
+            return obj
+        box = [obj]
+        dist.broadcast_object_list(box, src=src, device=self._comm_device() if self.backend == "nccl" else None)
+        return box[0]
+
+    # -------------------------------------------------------------- record batch shuffles
+    def exchange(self, parts: Sequence[Optional[RecordBatch]], template: Optional[RecordBatch] = None) -> List[RecordBatch]:
+        """Shuffle: ``parts[d]`` goes to rank d; returns the batches received (one per source)."""
+        ws = self.world_size
+        assert len(parts) == ws
+        if not self.distributed:
+            return [parts[0]] if parts[0] is not None else []
+        ref = template or next((p for p in parts if p is not None), None)
+        meta = _batch_meta(ref)
+        metas = [None] * ws
+        dist.all_gather_object(metas, meta)
+        ref_meta = next((m for m in metas if m is not None), None)
+        if ref_meta is None:
+            return []
+        parts = [p if p is not None else _empty_like_meta(ref_meta, self.device) for p in parts]
+        counts = [p.n for p in parts]
+        recv_cols: Dict[str, Any] = {}
+        recv_counts = None
+        for cm in ref_meta["columns"]:
+            name = cm["name"]
+            if cm["kind"] == "tensor":
+                t = torch.cat([_as_tensor(p.columns[name], cm, self.device) for p in parts])
+                out, recv_counts = self.all_to_all_rows(t, counts)
+                recv_cols[name] = out
+            else:
+                payloads = [json.dumps([_enc_plain(v) for v in p.columns[name]]).encode() for p in parts]
+                data = torch.frombuffer(bytearray(b"".join(payloads)) or bytearray(b"\0"), dtype=torch.uint8)
+                lens = [len(x) for x in payloads]
+                if sum(lens) == 0:
+                    data = data[:0]
+                out, rl = self.all_to_all_rows(data, lens)
+                out = out.cpu().numpy().tobytes()
+                vals, off = [], 0
+                for k in rl:
+                    vals.append(json.loads(out[off: off + k].decode()) if k else [])
+                    off += k
+                recv_cols[name] = vals
+        if recv_counts is None:
+            cd = self._comm_device()
+            sc = torch.tensor(counts, dtype=torch.int64, device=cd)
+            rc = torch.empty_like(sc)
+            dist.all_to_all_single(rc, sc)
+            recv_counts = [int(x) for x in rc.tolist()]
+        t = lookup_type(ref_meta["type"]) if ref_meta["type"] else None
+        out_batches = []
+        off = 0
+        for src, k in enumerate(recv_counts):
+            cols = {}
+            for cm in ref_meta["columns"]:
+                name = cm["name"]
+                if cm["kind"] == "tensor":
+                    cols[name] = recv_cols[name][off: off + k]
+                else:
+                    cols[name] = [_dec_plain(v) for v in recv_cols[name][src]]
+            out_batches.append(RecordBatch(cols, k, t))
+            off += k
+        return out_batches
+
+    def broadcast_batch_all(self, b: Optional[RecordBatch]) -> List[RecordBatch]:
+        """All-gather: every rank receives every rank's batch (broadcast join build side)."""
+        if not self.distributed:
+            return [b] if b is not None else []
+        return self.exchange([b] * self.world_size)
+
+
+def _batch_meta(b: Optional[RecordBatch]):
+    if b is None:
+        return None
+    cols = []
+    for k, c in b.columns.items():
+        if isinstance(c, torch.Tensor):
+            cols.append({"name": k, "kind": "tensor", "dtype": str(c.dtype).replace("torch.", ""),
+                         "shape": list(c.shape[1:])})
+        else:
+            cols.append({"name": k, "kind": "object"})
+    return {"type": b.type.type_name() if b.type is not None else None, "columns": cols}
+
+
+def _as_tensor(c, cm, device):
+    if isinstance(c, torch.Tensor):
+        return c.to(device) if c.device != device and device.type == "cuda" else c
+    return torch.empty((0,) + tuple(cm["shape"]), dtype=getattr(torch, cm["dtype"]), device=device)
+
+
+def _empty_like_meta(meta, device):
+    cols = {}
+    for cm in meta["columns"]:
+        if cm["kind"] == "tensor":
+            cols[cm["name"]] = torch.empty((0,) + tuple(cm["shape"]), dtype=getattr(torch, cm["dtype"]), device=device)
+        else:
+            cols[cm["name"]] = []
+    t = lookup_type(meta["type"]) if meta["type"] else None
+    return RecordBatch(cols, 0, t)
+
+
+def _enc_plain(v):
+    blobs: List[bytes] = []
+    if isinstance(v, torch.Tensor):
+        return {"__tt__": [v.detach().cpu().float().tolist(), str(v.dtype).replace("torch.", "")]}
+    enc = _enc_obj(v, blobs)
+    if blobs:
+        raise TypeError("tensors nested in object columns cannot be shuffled; use a tensor column")
+    return enc
+
+
+def _dec_plain(v):
+    if isinstance(v, dict) and "__tt__" in v:
+        data, dt = v["__tt__"]
+        return torch.tensor(data, dtype=getattr(torch, dt))
+    return _dec_obj(v, [])
+
+
+LOCAL = ClusterContext()
+
+__all__ = ["ClusterContext", "LOCAL"]

@@ -1,0 +1,189 @@
+"""Physical planning: TCAP atoms -> pipeline stages (reference: src/queryPlanning/source/
+TCAPAnalyzer.cc, QueryGraphAnalyzer.cc; job stages in src/builtInPDBObjects/headers/
+TupleSetJobStage.h, AggregationJobStage.h, BroadcastJoinBuildHTJobStage.h,
+HashPartitionedJoinBuildHTJobStage.h).
+
+A *stage* is a pipeline: one source (a SCAN, or a tuple set materialised by an earlier stage),
+a chain of streaming atoms (APPLY, FILTER, FLATTEN, HASHLEFT/RIGHT/ONE, JOIN-probe) and one
+sink (OUTPUT, AGGREGATE, PARTITION, JOIN-build, or MATERIALIZE when a tuple set feeds several
+consumers).  The join build side is chosen from set-size statistics (smaller side builds), and
+the distribution strategy — broadcast (all-gather) vs hash-partitioned (all-to-all) — from the
+build side's size against ``broadcast_threshold`` (netsDB's cost-based choice between
+BroadcastJoinBuildHTJobStage and HashPartitionedJoinBuildHTJobStage).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional
+
+STREAMING = {"APPLY", "FILTER", "FLATTEN", "HASHLEFT", "HASHRIGHT", "HASHONE"}
+
+
+@dataclass
+class Stage:
+    id: int
+    source: dict                      # {"kind": "scan", "atom": a} | {"kind": "materialized", "ts": name}
+    ops: List[dict] = field(default_factory=list)
+    sink: dict = field(default_factory=dict)   # {"kind": ..., "atom": a, "ts": name}
+    deps: List[int] = field(default_factory=list)
+
+    def describe(self) -> str:
+        src = self.source["atom"]["comp"] if self.source["kind"] == "scan" else f"mat:{self.source['ts']}"
+        ops = " -> ".join(f"{o['type']}" + (f"[{o['lambda']}]" if o.get("lambda") else "") for o in self.ops)
+        sk = self.sink.get("kind")
+        extra = ""
+        if sk == "join_build":
+            extra = f" ({self.sink['strategy']})"
+        return f"stage {self.id}: {src} -> {ops or '(none)'} => {sk}{extra}"
+
+
+@dataclass
+class PhysicalPlan:
+    stages: List[Stage]
+    atoms: List[dict]
+    join_strategy: Dict[str, dict]
+
+    def explain(self) -> str:
+        return "\n".join(s.describe() for s in self.stages)
+
+
+class Planner:
+    def __init__(self, size_of_scan: Callable[[dict], int], world_size: int = 1,
+                 broadcast_threshold: int = 2 << 30):
+        self.size_of_scan = size_of_scan
+        self.world_size = world_size
+        self.broadcast_threshold = broadcast_threshold
+
+    def plan(self, atoms: List[dict]) -> PhysicalPlan:
+        producer: Dict[str, dict] = {}
+        consumers: Dict[str, List[dict]] = {}
+        for a in atoms:
+            producer[a["output"]["name"]] = a
+            for key in ("input", "input2"):
+                nm = a[key]["name"]
+                if nm:
+                    lst = consumers.setdefault(nm, [])
+                    if not any(x is a for x in lst):
+                        lst.append(a)
+
+        # --- size estimates per tuple set (bytes of the scans feeding it), for join side selection
+        est: Dict[str, int] = {}
+        for a in atoms:
+            nm = a["output"]["name"]
+            if a["type"] == "SCAN":
+                est[nm] = self.size_of_scan(a)
+            elif a["type"] == "JOIN":
+                est[nm] = est.get(a["input"]["name"], 0) + est.get(a["input2"]["name"], 0)
+            elif a["type"] in ("AGGREGATE",):
+                est[nm] = max(1, est.get(a["input"]["name"], 0) // 4)
+            else:
+                est[nm] = est.get(a["input"]["name"], 0)
+
+        join_strategy: Dict[str, dict] = {}
+        for a in atoms:
+            if a["type"] == "JOIN":
+                left_sz, right_sz = est.get(a["input"]["name"], 0), est.get(a["input2"]["name"], 0)
+                build = "right" if right_sz <= left_sz else "left"
+                bsz = right_sz if build == "right" else left_sz
+                if self.world_size == 1:
+                    strat = "local"
+                elif bsz <= self.broadcast_threshold:
+                    strat = "broadcast"
+                else:
+                    strat = "partitioned"
+                join_strategy[a["output"]["name"]] = {"build": build, "strategy": strat, "build_bytes": bsz}
+
+        stages: List[Stage] = []
+        work: List[tuple] = []
+        for a in atoms:
+            if a["type"] == "SCAN":
+                work.append(({"kind": "scan", "atom": a, "ts": a["output"]["name"]}, None))
+        while work:
+            src, first = work.pop(0)
+            stages.append(self._walk(src, first, consumers, join_strategy, work))
+        for st in stages:
+            deps = set()
+            if st.source["kind"] == "materialized":
+                deps.add(("mat", st.source["ts"]))
+            for o in st.ops:
+                if o["type"] == "JOIN":
+                    deps.add(("build", o["output"]["name"]))
+            st.deps = deps  # type: ignore[assignment]
+        order = self._toposort(stages)
+        return PhysicalPlan(order, atoms, join_strategy)
+
+    def _walk(self, src, first, consumers, join_strategy, work) -> Stage:
+        st = Stage(0, src)
+        ts, c = src["ts"], first
+        while True:
+            if c is None:
+                cons = consumers.get(ts, [])
+                if not cons:
+                    st.sink = {"kind": "discard", "ts": ts}
+                    return st
+                if len(cons) > 1:
+                    st.sink = {"kind": "materialize", "ts": ts}
+                    for cc in cons:
+                        work.append(({"kind": "materialized", "ts": ts}, cc))
+                    return st
+                c = cons[0]
+            t = c["type"]
+            if t in STREAMING:
+                st.ops.append(c)
+                ts, c = c["output"]["name"], None
+                continue
+            if t == "JOIN":
+                js = join_strategy[c["output"]["name"]]
+                side = "left" if c["input"]["name"] == ts else "right"
+                if side == js["build"]:
+                    st.sink = {"kind": "join_build", "atom": c, "side": side, "strategy": js["strategy"], "ts": ts}
+                    return st
+                st.ops.append(dict(c, _probe_side=side, _strategy=js["strategy"], _build=js["build"]))
+                ts, c = c["output"]["name"], None
+                continue
+            if t in ("AGGREGATE", "PARTITION"):
+                st.sink = {"kind": t.lower(), "atom": c, "ts": ts}
+                work.append(({"kind": "materialized", "ts": c["output"]["name"]}, None))
+                return st
+            if t == "OUTPUT":
+                st.sink = {"kind": "output", "atom": c, "ts": ts}
+                return st
+            raise ValueError(f"unexpected atom {t}")
+
+    @staticmethod
+    def _toposort(stages: List[Stage]) -> List[Stage]:
+        provides = {}
+        for st in stages:
+            sk = st.sink.get("kind")
+            if sk == "join_build":
+                provides[("build", st.sink["atom"]["output"]["name"])] = st
+            elif sk in ("aggregate", "partition"):
+                provides[("mat", st.sink["atom"]["output"]["name"])] = st
+            elif sk == "materialize":
+                provides[("mat", st.sink["ts"])] = st
+        done, order = set(), []
+        remaining = list(stages)
+        while remaining:
+            progressed = False
+            for st in list(remaining):
+                if all(d in done or d not in provides for d in st.deps):
+                    order.append(st)
+                    remaining.remove(st)
+                    sk = st.sink.get("kind")
+                    if sk == "join_build":
+                        done.add(("build", st.sink["atom"]["output"]["name"]))
+                    elif sk in ("aggregate", "partition"):
+                        done.add(("mat", st.sink["atom"]["output"]["name"]))
+                    elif sk == "materialize":
+                        done.add(("mat", st.sink["ts"]))
+                    progressed = True
+            if not progressed:
+                raise RuntimeError("cyclic stage dependencies: " + "; ".join(s.describe() for s in remaining))
+        for i, st in enumerate(order):
+            st.id = i
+        return order
+
+
+__all__ = ["Planner", "PhysicalPlan", "Stage"]
+
+_ = Optional

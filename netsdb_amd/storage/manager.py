@@ -1,0 +1,141 @@
+"""Per-node storage manager (reference: src/serverFunctionalities/source/PangeaStorageServer.cc,
+src/storage/source/PageCache.cc, PDBEvictWork.cc, src/bufferMgr/*).
+
+Owns the node's sets, the HBM budget (288 GB per MI355X: the default budget is 85 % of device
+memory), the native :class:`BufferManager` page pool (host memory, LRU-spills to disk), and the
+device->host eviction of unpinned pages when the HBM budget is exceeded.
+"""
+from __future__ import annotations
+
+import itertools
+import os
+import tempfile
+import threading
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from .. import _ext
+from .sets import DenseMatrixSet, Page, UserSet
+
+DEFAULT_PAGE_SIZE = 64 << 20
+
+
+class StorageManager:
+    def __init__(self, root: Optional[str] = None, device=None, page_size: int = DEFAULT_PAGE_SIZE,
+                 pool_pages: int = 16, device_budget: Optional[int] = None, rank: int = 0):
+        self.root = root or tempfile.mkdtemp(prefix="netsdb_amd_")
+        os.makedirs(self.root, exist_ok=True)
+        self.device = torch.device(device) if device is not None else None
+        self.page_size = page_size
+        self.rank = rank
+        spill = os.path.join(self.root, f"node{rank}")
+        os.makedirs(spill, exist_ok=True)
+        self.buffer_manager = _ext.native().BufferManager(page_size, pool_pages, spill)
+        if device_budget is None and self.device is not None and self.device.type == "cuda":
+            total = torch.cuda.get_device_properties(self.device).total_memory
+            device_budget = int(total * 0.85)
+        self.device_budget = device_budget or (1 << 62)
+        self.device_bytes = 0
+        self.sets: Dict[Tuple[str, str], UserSet] = {}
+        self._ids = itertools.count(1)
+        self._clock = itertools.count()
+        self.lock = threading.RLock()
+        self.stats = {"evicted_pages": 0, "evicted_bytes": 0}
+
+    # ----------------------------------------------------------- sets
+    def create_set(self, db: str, name: str, type_=None, page_size: Optional[int] = None, device="default",
+                   dense: bool = False, set_id: Optional[int] = None, persistent: bool = True) -> UserSet:
+        with self.lock:
+            key = (db, name)
+            if key in self.sets:
+                return self.sets[key]
+            dev = self.device if device == "default" else device
+            sid = set_id if set_id is not None else next(self._ids)
+            cls = DenseMatrixSet if dense else UserSet
+            s = cls(self, db, name, type_, sid, page_size or self.page_size, dev, persistent)
+            self.sets[key] = s
+            return s
+
+    def get_set(self, db: str, name: str) -> UserSet:
+        try:
+            return self.sets[(db, name)]
+        except KeyError:
+            raise KeyError(f"set {db}.{name} does not exist on node {self.rank}") from None
+
+    def has_set(self, db: str, name: str) -> bool:
+        return (db, name) in self.sets
+
+    def remove_set(self, db: str, name: str):
+        with self.lock:
+            s = self.sets.pop((db, name), None)
+            if s is not None:
+                for p in s.pages:
+                    if p.location == "device" and p.batch is not None:
+                        self.device_bytes -= p.nbytes
+                s.clear()
+
+    def remove_database(self, db: str):
+        for (d, n) in list(self.sets):
+            if d == db:
+                self.remove_set(d, n)
+
+    def clear_set(self, db: str, name: str):
+        s = self.get_set(db, name)
+        for p in s.pages:
+            if p.location == "device" and p.batch is not None:
+                self.device_bytes -= p.nbytes
+        s.clear()
+
+    # ----------------------------------------------------------- memory accounting / eviction
+    def account(self, page: Page):
+        page.last_use = next(self._clock)
+        if page.location == "device":
+            self.account_bytes(page.nbytes, self.device)
+
+    def account_bytes(self, nbytes: int, device=None):
+        if device is None or torch.device(device).type != "cuda":
+            return
+        with self.lock:
+            self.device_bytes += nbytes
+            if self.device_bytes > self.device_budget:
+                self.evict(self.device_bytes - self.device_budget)
+
+    def touch(self, page: Page):
+        page.last_use = next(self._clock)
+
+    def evict(self, need: int) -> int:
+        """Spill least-recently-used unpinned device pages to the host page pool."""
+        cands = [p for s in self.sets.values() for p in s.pages
+                 if p.location == "device" and p.batch is not None and p.pins == 0]
+        cands.sort(key=lambda p: p.last_use)
+        freed = 0
+        for p in cands:
+            if freed >= need:
+                break
+            f = p.spill()
+            freed += f
+            self.stats["evicted_pages"] += 1
+        self.device_bytes -= freed
+        self.stats["evicted_bytes"] += freed
+        return freed
+
+    def flush(self):
+        for s in self.sets.values():
+            if s.persistent:
+                s.flush()
+        self.buffer_manager.flush_all()
+
+    def summary(self) -> dict:
+        return {
+            "sets": {f"{d}.{n}": {"records": s.num_records(), "bytes": s.nbytes(), "pages": len(s.pages)}
+                     for (d, n), s in self.sets.items()},
+            "device_bytes": self.device_bytes,
+            "device_budget": self.device_budget,
+            "pool_resident_pages": self.buffer_manager.resident_pages,
+            "pool_evictions": self.buffer_manager.evictions,
+            **self.stats,
+        }
+
+
+__all__ = ["StorageManager", "DEFAULT_PAGE_SIZE"]

@@ -1,0 +1,296 @@
+"""Sets and pages (reference: src/storage/headers/UserSet.h, LocalitySet.h, TempSet.h, PDBPage.h,
+PageCache.h, PDBFlushProducerWork/ConsumerWork, PDBEvictWork).
+
+A :class:`UserSet` is one node's partition of a stored set: an ordered list of :class:`Page` s,
+each holding a RecordBatch of at most ``page_size`` bytes.  Pages are resident in HBM (device
+sets), in host memory, or spilled: a spilled page's serialised image lives in the native
+:class:`BufferManager` page pool, which itself LRU-evicts to the set's page file on disk.
+
+:class:`DenseMatrixSet` is the MI355X-native physical layout for block-partitioned matrices
+(MatrixBlock / FFMatrixBlock sets): the node's row-slab of the matrix is ONE dense, 16-B-aligned
+row-major HBM panel that the MFMA kernels read directly with buffer loads; the MatrixBlock
+records the UDFs see are slices of it.  This replaces netsDB's per-block heap objects and avoids
+assembling blocks before every block GEMM.
+"""
+from __future__ import annotations
+
+import itertools
+import math
+import threading
+from typing import Iterator, List, Optional, Tuple
+
+import torch
+
+from ..objects.record import RecordBatch
+from .serde import deserialize_batch, serialize_batch
+
+_page_ids = itertools.count()
+
+
+class Page:
+    __slots__ = ("set", "page_no", "batch", "nbytes", "pins", "location", "dirty", "last_use", "n")
+
+    def __init__(self, uset: "UserSet", page_no: int, batch: RecordBatch):
+        self.set = uset
+        self.page_no = page_no
+        self.batch: Optional[RecordBatch] = batch
+        self.nbytes = batch.nbytes()
+        self.n = batch.n
+        self.pins = 0
+        self.location = "device" if batch.device.type == "cuda" else "host"
+        self.dirty = True
+        self.last_use = 0
+
+    def is_resident(self) -> bool:
+        return self.batch is not None
+
+    def spill(self):
+        """Serialise into the native page pool (LRU -> disk) and drop the in-memory batch."""
+        if self.batch is None or self.pins > 0:
+            return 0
+        bm = self.set.manager.buffer_manager
+        data = serialize_batch(self.batch)
+        if len(data) > bm.page_size:
+            raise RuntimeError(f"page image {len(data)} B exceeds pool page size {bm.page_size}")
+        slot = bm.pin(self.set.set_id, self.page_no, True)
+        view = bm.slot_view(slot)
+        view[: len(data)] = data
+        bm.unpin(self.set.set_id, self.page_no, True, len(data))
+        freed = self.nbytes if self.location == "device" else 0
+        self.batch = None
+        self.location = "pool"
+        self.dirty = False
+        return freed
+
+    def load(self, device) -> RecordBatch:
+        if self.batch is not None:
+            return self.batch
+        bm = self.set.manager.buffer_manager
+        slot = bm.pin(self.set.set_id, self.page_no, False)
+        try:
+            n = bm.bytes_used(self.set.set_id, self.page_no)
+            data = bytes(bm.slot_view(slot)[:n])
+        finally:
+            bm.unpin(self.set.set_id, self.page_no, False, 0)
+        b = deserialize_batch(data)
+        if device is not None and torch.device(device).type == "cuda":
+            b = b.to(device)
+        self.batch = b
+        self.location = "device" if b.device.type == "cuda" else "host"
+        self.dirty = False
+        return b
+
+    def persist(self):
+        """Write the page image to the pool (and from there to disk on flush) without dropping it."""
+        if self.batch is None or not self.dirty:
+            return
+        bm = self.set.manager.buffer_manager
+        data = serialize_batch(self.batch)
+        slot = bm.pin(self.set.set_id, self.page_no, True)
+        bm.slot_view(slot)[: len(data)] = data
+        bm.unpin(self.set.set_id, self.page_no, True, len(data))
+        self.dirty = False
+
+
+class UserSet:
+    """One node's partition of a stored set."""
+
+    def __init__(self, manager, db: str, name: str, type_, set_id: int, page_size: int, device=None,
+                 persistent: bool = True):
+        self.manager = manager
+        self.db, self.name = db, name
+        self.type = type_
+        self.set_id = set_id
+        self.page_size = page_size
+        self.device = device
+        self.pages: List[Page] = []
+        self.persistent = persistent
+        self.lock = threading.RLock()
+        self.partition_key = None       # (computation, lambda) describing how the set is partitioned
+        self.stats = {"records": 0, "bytes": 0}
+
+    # -------------------------------------------------------------- writes
+    def add_batch(self, batch: RecordBatch):
+        if batch.n == 0:
+            return
+        if self.device is not None and batch.device != torch.device(self.device):
+            batch = batch.to(self.device)
+        with self.lock:
+            per_row = max(1, batch.nbytes() // max(1, batch.n))
+            rows_per_page = max(1, self.page_size // per_row)
+            for s in range(0, batch.n, rows_per_page):
+                part = batch.slice(s, min(batch.n, s + rows_per_page)) if batch.n > rows_per_page else batch
+                p = Page(self, len(self.pages), part)
+                self.pages.append(p)
+                self.stats["records"] += part.n
+                self.stats["bytes"] += p.nbytes
+                self.manager.account(p)
+
+    def clear(self):
+        with self.lock:
+            self.pages = []
+            self.stats = {"records": 0, "bytes": 0}
+            self.manager.buffer_manager.drop_set(self.set_id)
+
+    # -------------------------------------------------------------- reads
+    def scan(self, device=None) -> Iterator[RecordBatch]:
+        device = device if device is not None else self.device
+        for p in list(self.pages):
+            p.pins += 1
+            try:
+                b = p.load(device)
+                self.manager.touch(p)
+                yield b
+            finally:
+                p.pins -= 1
+
+    def all(self, device=None) -> Optional[RecordBatch]:
+        bs = list(self.scan(device))
+        if not bs:
+            return None
+        return RecordBatch.concat(bs)
+
+    def num_records(self) -> int:
+        return self.stats["records"]
+
+    def nbytes(self) -> int:
+        return self.stats["bytes"]
+
+    def flush(self):
+        for p in self.pages:
+            p.persist()
+        self.manager.buffer_manager.flush_set(self.set_id)
+
+    def __repr__(self):
+        return f"UserSet({self.db}.{self.name}, pages={len(self.pages)}, records={self.num_records()})"
+
+
+class DenseMatrixSet(UserSet):
+    """A block-partitioned matrix stored as one dense row-slab panel per node."""
+
+    def __init__(self, manager, db, name, type_, set_id, page_size, device=None, persistent=True):
+        super().__init__(manager, db, name, type_, set_id, page_size, device, persistent)
+        self.panel: Optional[torch.Tensor] = None     # [local_rows_padded, ld]
+        self.total_rows = 0
+        self.total_cols = 0
+        self.block_rows = 0
+        self.block_cols = 0
+        self.row_offset = 0                           # first global row held by this node
+        self.local_rows = 0
+
+    # geometry -------------------------------------------------------
+    def define(self, total_rows: int, total_cols: int, block_rows: int, block_cols: int, row_offset: int = 0,
+               local_rows: Optional[int] = None, dtype=torch.bfloat16, device=None, ld_align: int = 64,
+               zero: bool = True):
+        self.total_rows, self.total_cols = total_rows, total_cols
+        self.block_rows, self.block_cols = block_rows, block_cols
+        self.row_offset = row_offset
+        self.local_rows = total_rows - row_offset if local_rows is None else local_rows
+        ld = max(8, math.ceil(total_cols / ld_align) * ld_align)
+        dev = device if device is not None else self.device
+        alloc = torch.zeros if zero else torch.empty
+        self.panel = alloc(self.local_rows, ld, dtype=dtype, device=dev)
+        self.stats = {"records": self.num_blocks(), "bytes": self.panel.numel() * self.panel.element_size()}
+        self.manager.account_bytes(self.stats["bytes"], dev)
+        return self
+
+    def set_panel(self, panel: torch.Tensor, total_rows: int, total_cols: int, block_rows: int, block_cols: int,
+                  row_offset: int = 0):
+        self.panel = panel
+        self.total_rows, self.total_cols = total_rows, total_cols
+        self.block_rows, self.block_cols = block_rows, block_cols
+        self.row_offset = row_offset
+        self.local_rows = panel.shape[0]
+        self.stats = {"records": self.num_blocks(), "bytes": panel.numel() * panel.element_size()}
+        return self
+
+    def matrix(self) -> torch.Tensor:
+        """[local_rows, total_cols] view (row stride = padded ld)."""
+        return self.panel[:, : self.total_cols]
+
+    def num_blocks(self) -> int:
+        if self.block_rows == 0:
+            return 0
+        return math.ceil(self.local_rows / self.block_rows) * math.ceil(self.total_cols / self.block_cols)
+
+    def block_grid(self) -> Tuple[int, int]:
+        return math.ceil(self.total_rows / self.block_rows), math.ceil(self.total_cols / self.block_cols)
+
+    # record view ------------------------------------------------------
+    def add_batch(self, batch: RecordBatch):
+        """Scatter MatrixBlock records into the panel."""
+        if batch.n == 0:
+            return
+        if self.panel is None:
+            b0 = batch.columns
+            self.define(int(b0["total_rows"][0]), int(b0["total_cols"][0]), int(b0["row_nums"][0]),
+                        int(b0["col_nums"][0]), dtype=batch.columns["data"].dtype if isinstance(
+                            batch.columns["data"], torch.Tensor) else torch.float32)
+        rows = batch.columns["block_row"].tolist()
+        cols = batch.columns["block_col"].tolist()
+        data = batch.columns["data"]
+        for i, (r, c) in enumerate(zip(rows, cols)):
+            r0 = r * self.block_rows - self.row_offset
+            c0 = c * self.block_cols
+            blk = data[i]
+            h = min(blk.shape[0], self.local_rows - r0)
+            w = min(blk.shape[1], self.total_cols - c0)
+            if h > 0 and w > 0:
+                self.panel[r0:r0 + h, c0:c0 + w] = blk[:h, :w].to(self.panel.device, self.panel.dtype)
+
+    def scan(self, device=None) -> Iterator[RecordBatch]:
+        if self.panel is None:
+            return
+        yield self.to_blocks(device)
+
+    def to_blocks(self, device=None) -> RecordBatch:
+        from ..objects.builtin import MatrixBlock
+
+        br, bc = self.block_rows, self.block_cols
+        nbr = math.ceil(self.local_rows / br)
+        nbc = math.ceil(self.total_cols / bc)
+        m = self.matrix()
+        pr, pc = nbr * br - self.local_rows, nbc * bc - self.total_cols
+        if pr or pc:
+            m = torch.nn.functional.pad(m, (0, pc, 0, pr))
+        blocks = m.reshape(nbr, br, nbc, bc).permute(0, 2, 1, 3).reshape(nbr * nbc, br, bc)
+        if device is not None:
+            blocks = blocks.to(device)
+        dev = blocks.device
+        first_br = self.row_offset // br
+        r_idx = torch.arange(nbr, device=dev).repeat_interleave(nbc) + first_br
+        c_idx = torch.arange(nbc, device=dev).repeat(nbr)
+        n = nbr * nbc
+        full = lambda v: torch.full((n,), v, dtype=torch.int64, device=dev)  # noqa: E731
+        cols = {"block_row": r_idx, "block_col": c_idx, "row_nums": full(br), "col_nums": full(bc),
+                "total_rows": full(self.total_rows), "total_cols": full(self.total_cols), "data": blocks}
+        t = self.type if self.type is not None else MatrixBlock
+        for f in t.__fields__:
+            if f not in cols:
+                cols[f] = torch.zeros(n, dtype=torch.int64, device=dev)
+        return RecordBatch(cols, n, t)
+
+    def clear(self):
+        self.panel = None
+        self.stats = {"records": 0, "bytes": 0}
+
+    def flush(self):
+        if self.panel is None:
+            return
+        b = self.to_blocks("cpu")
+        bm = self.manager.buffer_manager
+        data = serialize_batch(b)
+        page = 0
+        # dense images may exceed one pool page: store in page-size chunks
+        for s in range(0, len(data), bm.page_size):
+            chunk = data[s: s + bm.page_size]
+            slot = bm.pin(self.set_id, page, True)
+            bm.slot_view(slot)[: len(chunk)] = chunk
+            bm.unpin(self.set_id, page, True, len(chunk))
+            page += 1
+        bm.flush_set(self.set_id)
+
+
+__all__ = ["Page", "UserSet", "DenseMatrixSet"]
+
+_ = _page_ids

@@ -1,0 +1,194 @@
+"""End-to-end query tests on the CPU pseudo-cluster path (reference test strategy: src/tests/source
+Test*.cc selection/join/aggregation programs checked against expected outputs)."""
+import torch
+
+from netsdb_amd.client import PDBClient
+from netsdb_amd.computations import AggregateComp, JoinComp, MultiSelectionComp, ScanSet, SelectionComp, TopKComp, WriteSet
+from netsdb_amd.lambdas import make_lambda, make_lambda_from_member, make_lambda_from_method, make_lambda_from_self
+from netsdb_amd.objects import PDBObject, RecordBatch
+from netsdb_amd.objects.builtin import DepartmentTotal, Employee, StringIntPair
+
+
+class Dept(PDBObject):
+    name: str
+    floor: int
+
+
+class EmpDept(PDBObject):
+    emp: str
+    dept: str
+    floor: int
+
+
+class OlderThan(SelectionComp):
+    def __init__(self, age):
+        super().__init__()
+        self.age = age
+
+    def get_selection(self, e):
+        return make_lambda_from_member(e, "age") > self.age
+
+    def get_projection(self, e):
+        return make_lambda_from_self(e)
+
+
+class NameOnly(SelectionComp):
+    def get_selection(self, e):
+        return make_lambda(e, lambda r: r.department == "eng")
+
+    def get_projection(self, e):
+        return make_lambda(e, lambda r: StringIntPair(r.name, r.age))
+
+
+class EmpJoinDept(JoinComp):
+    def get_selection(self, e, d):
+        return make_lambda_from_member(e, "department") == make_lambda_from_member(d, "name")
+
+    def get_projection(self, e, d):
+        return make_lambda(e, d, lambda a, b: EmpDept(a.name, b.name, b.floor))
+
+
+class SalaryByDept(AggregateComp):
+    def get_key_projection(self, e):
+        return make_lambda_from_method(e, "getDepartment")
+
+    def get_value_projection(self, e):
+        return make_lambda_from_method(e, "getSalary")
+
+    def make_output(self, keys, values):
+        return RecordBatch.from_objects([DepartmentTotal(k, float(v)) for k, v in zip(keys, values.tolist())],
+                                        DepartmentTotal)
+
+
+class Explode(MultiSelectionComp):
+    def get_projection(self, e):
+        return make_lambda(e, lambda r: [StringIntPair(r.name, i) for i in range(r.age % 3)])
+
+
+class TopSalary(TopKComp):
+    def get_value_projection(self, e):
+        return make_lambda_from_member(e, "salary")
+
+
+def _emps(n=50):
+    depts = ["eng", "ops", "sales", "hr"]
+    return [Employee(f"e{i}", 20 + (i * 7) % 40, depts[i % 4], 1000.0 + i) for i in range(n)]
+
+
+def _client(tmp_path):
+    c = PDBClient(root=str(tmp_path), page_size=1 << 12)
+    c.create_database("db")
+    c.create_set("db", "emps", Employee)
+    c.send_data("db", "emps", _emps())
+    return c
+
+
+def test_selection(tmp_path):
+    c = _client(tmp_path)
+    c.create_set("db", "old", Employee)
+    s = OlderThan(40)
+    s.set_input(ScanSet("db", "emps", Employee))
+    w = WriteSet("db", "old")
+    w.set_input(s)
+    c.execute_computations(w)
+    got = sorted(o.name for o in c.get_set_iterator("db", "old"))
+    exp = sorted(e.name for e in _emps() if e.age > 40)
+    assert got == exp and got
+
+
+def test_native_lambda_selection(tmp_path):
+    c = _client(tmp_path)
+    c.create_set("db", "names", StringIntPair)
+    s = NameOnly()
+    s.set_input(ScanSet("db", "emps", Employee))
+    w = WriteSet("db", "names").set_input(s)
+    c.execute_computations(w)
+    got = sorted((o.myString, o.myInt) for o in c.get_set_iterator("db", "names"))
+    assert got == sorted((e.name, e.age) for e in _emps() if e.department == "eng")
+
+
+def test_join(tmp_path):
+    c = _client(tmp_path)
+    c.create_set("db", "depts", Dept)
+    c.send_data("db", "depts", [Dept("eng", 3), Dept("ops", 1), Dept("hr", 2)])
+    c.create_set("db", "out", EmpDept)
+    j = EmpJoinDept()
+    j.set_input(0, ScanSet("db", "emps", Employee))
+    j.set_input(1, ScanSet("db", "depts", Dept))
+    c.execute_computations(WriteSet("db", "out").set_input(j))
+    got = sorted((o.emp, o.dept, o.floor) for o in c.get_set_iterator("db", "out"))
+    floors = {"eng": 3, "ops": 1, "hr": 2}
+    exp = sorted((e.name, e.department, floors[e.department]) for e in _emps() if e.department in floors)
+    assert got == exp
+
+
+def test_aggregate(tmp_path):
+    c = _client(tmp_path)
+    c.create_set("db", "totals", DepartmentTotal)
+    a = SalaryByDept()
+    a.set_input(ScanSet("db", "emps", Employee))
+    c.execute_computations(WriteSet("db", "totals").set_input(a))
+    got = {o.department: o.total for o in c.get_set_iterator("db", "totals")}
+    exp = {}
+    for e in _emps():
+        exp[e.department] = exp.get(e.department, 0.0) + e.salary
+    assert got.keys() == exp.keys()
+    for k in exp:
+        assert abs(got[k] - exp[k]) < 1e-6
+
+
+def test_multiselection_and_topk(tmp_path):
+    c = _client(tmp_path)
+    c.create_set("db", "flat", StringIntPair)
+    m = Explode()
+    m.set_input(ScanSet("db", "emps", Employee))
+    c.execute_computations(WriteSet("db", "flat").set_input(m))
+    assert sum(1 for _ in c.get_set_iterator("db", "flat")) == sum(e.age % 3 for e in _emps())
+    c.create_set("db", "top", Employee)
+    t = TopSalary(5)
+    t.set_input(ScanSet("db", "emps", Employee))
+    c.execute_computations(WriteSet("db", "top").set_input(t))
+    got = sorted(o.salary for o in c.get_set_iterator("db", "top"))
+    assert got == sorted(e.salary for e in _emps())[-5:]
+
+
+def test_tcap_roundtrip(tmp_path):
+    c = _client(tmp_path)
+    j = EmpJoinDept()
+    j.set_input(0, ScanSet("db", "emps", Employee))
+    j.set_input(1, ScanSet("db", "emps", Employee))
+    text = c.explain(WriteSet("db", "x").set_input(j))
+    assert "HASHLEFT" in text and "JOIN" in text and "OUTPUT" in text and "stage" in text
+
+
+def test_chained_selection_join_aggregate(tmp_path):
+    """selection -> join -> aggregate -> write in ONE job (multi-stage pipeline with breakers)."""
+    c = _client(tmp_path)
+    c.create_set("db", "depts", Dept)
+    c.send_data("db", "depts", [Dept("eng", 3), Dept("ops", 1), Dept("sales", 2), Dept("hr", 9)])
+
+    class FloorSum(AggregateComp):
+        def get_key_projection(self, r):
+            return make_lambda_from_member(r, "dept")
+
+        def get_value_projection(self, r):
+            return make_lambda_from_member(r, "floor")
+
+    s = OlderThan(30).set_input(ScanSet("db", "emps", Employee))
+    j = EmpJoinDept()
+    j.set_input(0, s)
+    j.set_input(1, ScanSet("db", "depts", Dept))
+    a = FloorSum().set_input(j)
+    c.create_set("db", "res", None)
+    c.execute_computations(WriteSet("db", "res").set_input(a))
+    got = {}
+    for b in c.get_set_batches("db", "res"):
+        for k, v in zip(b.columns["key"], b.columns["value"].tolist()):
+            got[k] = v
+    floors = {"eng": 3, "ops": 1, "sales": 2, "hr": 9}
+    exp = {}
+    for e in _emps():
+        if e.age > 30:
+            exp[e.department] = exp.get(e.department, 0) + floors[e.department]
+    assert got == exp
+    _ = torch
