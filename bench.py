@@ -1,0 +1,123 @@
+"""Headline benchmark: whole-node inference rows/sec for netsDB's FF-NN + conv2d block.
+
+One step (per GPU, weak scaling; every rank holds its own partition of the inference inputs and
+the model is replicated — netsDB's broadcast join of the weight sets, "materializeModel"):
+  1. FF-NN inference_unit on AmazonCat-14k dims (reference src/tests/source/FFTestWithDeduplication.cc:
+     batch 1000, features 597540, hidden 1000, labels 14588; blocks 50x10000; dropout 0.5 as FFTest.cc)
+     = 2 jobs through the engine: W1·Xᵀ -> +b1, relu, dropout -> Wo·Y -> +bo, exp, ᵀ  |  row softmax
+  2. conv2d_memory_fusion block (reference src/tests/source/PipelinedConv2dMemFuseTest.cc: 100 images
+     3x112x112, 64 filters 7x7x3, stride 1, no padding) = 1 job, fused implicit-GEMM conv + bias.
+rows/step/GPU = FF input rows + images.  Synthetic data, random-init weights, bf16 compute.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+FULL = dict(batch=1000, features=597540, hidden=1000, labels=14588, block_x=50, block_y=10000,
+            images=100, channels=3, height=112, width=112, filters=64, ksize=7)
+SMALL = dict(batch=64, features=4096, hidden=256, labels=512, block_x=32, block_y=512,
+             images=4, channels=3, height=32, width=32, filters=16, ksize=7)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--small", action="store_true", help="tiny shapes (CPU smoke only; not a valid measurement)")
+    ap.add_argument("--dropout", type=float, default=0.5)
+    ap.add_argument("--profile-json", default=None)
+    args = ap.parse_args()
+
+    from netsdb_amd.client import PDBClient
+    from netsdb_amd.models import conv2d as cv
+    from netsdb_amd.models import ff
+    from netsdb_amd.parallel.comm import ClusterContext
+
+    cfg = SMALL if args.small else FULL
+    ctx = ClusterContext.from_env()
+    if ctx.world_size != args.gpus and ctx.rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={ctx.world_size}", file=sys.stderr)
+    root = tempfile.mkdtemp(prefix=f"nsdb_bench_r{ctx.rank}_")
+    client = PDBClient(ctx=ctx, root=root, device=ctx.device)
+    dev = ctx.device
+
+    # ---- data (per-rank partition of the inputs, replicated model) ----
+    ff.load_model(client, "ff", cfg["batch"] * ctx.world_size, cfg["features"], cfg["hidden"], cfg["labels"],
+                  cfg["block_x"], cfg["block_y"], seed=1234, partition_inputs=True)
+    client.create_database("conv2d")
+    cv.load_images(client, "conv2d", "img", cfg["images"], cfg["channels"], cfg["height"], cfg["width"], seed=99)
+    w, b = cv.random_kernel(cfg["filters"], cfg["channels"], cfg["ksize"], cfg["ksize"], seed=7, device=dev)
+    local_rows = client.storage.get_set("ff", "inputs").local_rows
+
+    def step(i):
+        ff.inference_unit(client, "ff", "w1", "wo", "inputs", "b1", "bo", "output", dropout_rate=args.dropout,
+                          seed=i)
+        cv.conv2d_memfuse_inference(client, "conv2d", "img", "conv_out", w, b)
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        ctx.barrier()
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    for i in range(args.warmup):
+        step(i)
+    sync()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    sync()
+    dt = time.perf_counter() - t0
+    dt = ctx.all_reduce_scalar(dt, "max")
+    rows_local = local_rows + cfg["images"]
+    rows_total = ctx.all_reduce_scalar(float(rows_local), "sum") * args.steps
+    value = rows_total / dt
+    # sanity: softmax rows sum to 1
+    out = client.storage.get_set("ff", "output")
+    ok = bool(torch.allclose(out.matrix()[:4].float().sum(-1), torch.ones(min(4, out.local_rows), device=dev),
+                             atol=1e-2)) if out.panel is not None else False
+    if ctx.rank == 0:
+        res = {
+            "metric": "inference rows/sec (whole node), FF-NN + conv2d block",
+            "value": round(value, 2),
+            "unit": "rows/s",
+            "n_gpus": ctx.world_size,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random inputs/images, random-init weights)",
+            "config": {
+                "model": "FF-NN AmazonCat-14k (597540-1000-14588, relu+dropout0.5, softmax) + conv2d 7x7x3->64 block",
+                "global_batch": int(rows_total / args.steps),
+                "ff_rows_per_gpu": local_rows,
+                "conv_images_per_gpu": cfg["images"],
+                "image": [cfg["channels"], cfg["height"], cfg["width"]],
+                "seq_len": None,
+                "parallelism": f"dp{ctx.world_size} (row-partitioned inputs, broadcast model)",
+                "small": bool(args.small),
+                "softmax_rows_sum_to_1": ok,
+            },
+        }
+        print(json.dumps(res), flush=True)
+    if ctx.distributed:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -144,7 +144,7 @@ torch::Tensor im2col(torch::Tensor X, int64_t KH, int64_t KW, int64_t stride, in
   return out;
 }
 
-torch::Tensor softmax_rows(torch::Tensor X, c10::optional<torch::Tensor> bias, bool out_f32, bool log_out) {
+torch::Tensor softmax_rows(torch::Tensor X, c10::optional<torch::Tensor> bias, bool out_f32, int64_t mode) {
   check_cuda(X, "X");
   TORCH_CHECK(X.dim() == 2 && X.stride(-1) == 1, "X must be 2-D row-contiguous");
   const bool xf = is_f32(X, "X");
@@ -155,7 +155,7 @@ torch::Tensor softmax_rows(torch::Tensor X, c10::optional<torch::Tensor> bias, b
   }
   auto Y = torch::empty({X.size(0), X.size(1)}, X.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16));
   check_rc(nsdb_softmax_rows(X.data_ptr(), xf, bptr, Y.data_ptr(), out_f32, (int)X.size(0), (int)X.size(1),
-                             X.stride(0), Y.stride(0), log_out ? 1 : 0, cur_stream()),
+                             X.stride(0), Y.stride(0), (int)mode, cur_stream()),
            "softmax_rows");
   return Y;
 }
@@ -231,7 +231,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("nchw_out") = false, py::arg("out_f32") = false);
   m.def("im2col", &im2col);
   m.def("softmax_rows", &softmax_rows, py::arg("X"), py::arg("bias") = py::none(), py::arg("out_f32") = true,
-        py::arg("log_out") = false);
+        py::arg("mode") = 0);
   m.def("bias_act", &bias_act, py::arg("X"), py::arg("bias") = py::none(), py::arg("bias_mode") = 2,
         py::arg("act") = 0, py::arg("dropout") = 0.0, py::arg("seed") = 0, py::arg("out_f32") = false);
   m.def("lstm_cell", &lstm_cell, py::arg("gates"), py::arg("c_prev") = py::none(), py::arg("h_f32") = true);

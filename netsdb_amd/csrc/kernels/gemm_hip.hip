@@ -74,11 +74,15 @@ __device__ __forceinline__ bf16x8 read_frag(const char* lds_tile, int row, int c
 __global__ void __launch_bounds__(NTHREADS, 2) gemm_nt_bf16_kernel(GemmParams p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
 
+  // 1-D grid over (split, tile); the bijective XCD remap hands every XCD a contiguous run of
+  // work ids, split-major: with splits a multiple of 8 each XCD owns whole K-slices, so the A and
+  // B panels of a slice are re-read out of ONE XCD's L2 (the M=N=1000, K=600k FF layer-1 shape).
   const int ntiles = p.tiles_m * p.tiles_n;
-  const int tile = xcd_remap(blockIdx.x, ntiles);
+  const int wg = xcd_remap(blockIdx.x, ntiles * p.splits);
+  const int split = wg / ntiles, tile = wg % ntiles;
   // column-major tile walk: consecutive tiles (same XCD after the remap) share the B panel
   const int tm = tile % p.tiles_m, tn = tile / p.tiles_m;
-  const int split = blockIdx.y, batch = blockIdx.z;
+  const int batch = blockIdx.z;
   const int m0 = tm * BM, n0 = tn * BN;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -254,7 +258,7 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
   p.alpha = alpha; p.dropout = dropout; p.seed = seed;
   p.tiles_m = (M + nsdb::BM - 1) / nsdb::BM;
   p.tiles_n = (N + nsdb::BN - 1) / nsdb::BN;
-  dim3 grid(p.tiles_m * p.tiles_n, p.splits, batch);
+  dim3 grid(p.tiles_m * p.tiles_n * p.splits, 1, batch);
   hipLaunchKernelGGL(nsdb::gemm_nt_bf16_kernel, grid, dim3(nsdb::NTHREADS), 0, stream, p);
   if (p.splits > 1) {
     const long long MN = (long long)M * N;

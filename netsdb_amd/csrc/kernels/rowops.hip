@@ -54,6 +54,21 @@ __global__ void __launch_bounds__(256) softmax_rows_kernel(const TI* X, const fl
   }
 }
 
+// y = x / rowsum(x): FFOutputLayer applied to exp'd scores (FFTransposeBiasSum wrote exp(z)).
+template <typename TI, typename TO>
+__global__ void __launch_bounds__(256) row_normalize_kernel(const TI* X, TO* Y, int R, int N, long long ldx,
+                                                            long long ldy) {
+  __shared__ float red[8];
+  const int row = blockIdx.x;
+  if (row >= R) return;
+  const TI* x = X + (long long)row * ldx;
+  float s = 0.f;
+  for (int j = threadIdx.x; j < N; j += blockDim.x) s += ld(x, j);
+  const float inv = 1.f / block_reduce(s, red, false);
+  TO* y = Y + (long long)row * ldy;
+  for (int j = threadIdx.x; j < N; j += blockDim.x) st(y, j, ld(x, j) * inv);
+}
+
 // y = dropout(act(x + bias[row|col])) elementwise over [R][N]
 template <typename TI, typename TO>
 __global__ void __launch_bounds__(256) bias_act_kernel(const TI* X, const float* bias, TO* Y, int R, int N,
@@ -127,6 +142,16 @@ extern "C" {
 int nsdb_softmax_rows(const void* X, int x_f32, const float* bias, void* Y, int y_f32, int R, int N,
                       long long ldx, long long ldy, int log_out, hipStream_t st) {
   if (R <= 0) return 0;
+  if (log_out == 2) {   // row normalise
+#define NSDB_RN(TI, TO) \
+  hipLaunchKernelGGL((nsdb::row_normalize_kernel<TI, TO>), dim3(R), dim3(256), 0, st, (const TI*)X, (TO*)Y, R, N, ldx, ldy)
+    if (x_f32 && y_f32) NSDB_RN(float, float);
+    else if (x_f32) NSDB_RN(float, unsigned short);
+    else if (y_f32) NSDB_RN(unsigned short, float);
+    else NSDB_RN(unsigned short, unsigned short);
+#undef NSDB_RN
+    return (int)hipGetLastError();
+  }
 #define NSDB_SM(TI, TO) \
   hipLaunchKernelGGL((nsdb::softmax_rows_kernel<TI, TO>), dim3(R), dim3(256), 0, st, (const TI*)X, bias, (TO*)Y, R, N, ldx, ldy, log_out)
   if (x_f32 && y_f32) NSDB_SM(float, float);

@@ -129,10 +129,18 @@ def im2col(X, KH, KW, stride=1, pad=0, dil=1, ldk=None):
 
 def softmax_rows(X, bias=None, out_dtype=torch.float32, log=False):
     if _use_hip(X):
-        return _ext.hip().softmax_rows(X, bias, out_dtype == torch.float32, bool(log))
+        return _ext.hip().softmax_rows(X, bias, out_dtype == torch.float32, 1 if log else 0)
     v = X.float() + (bias.float() if bias is not None else 0.0)
     r = torch.log_softmax(v, dim=-1) if log else torch.softmax(v, dim=-1)
     return r.to(out_dtype)
+
+
+def row_normalize(X, out_dtype=torch.float32):
+    """x / rowsum(x) (FFOutputLayer over exp'd scores)."""
+    if _use_hip(X):
+        return _ext.hip().softmax_rows(X, None, out_dtype == torch.float32, 2)
+    v = X.float()
+    return (v / v.sum(-1, keepdim=True)).to(out_dtype)
 
 
 def bias_act(X, bias=None, bias_mode=BIAS_COL, act=ACT_NONE, dropout=0.0, seed=0, out_dtype=torch.bfloat16):

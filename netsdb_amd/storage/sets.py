@@ -177,6 +177,8 @@ class DenseMatrixSet(UserSet):
         self.block_cols = 0
         self.row_offset = 0                           # first global row held by this node
         self.local_rows = 0
+        self.transposed = False                       # panel holds the logical matrix transposed
+        self.replicated = False                       # every rank holds the full matrix
 
     # geometry -------------------------------------------------------
     def define(self, total_rows: int, total_cols: int, block_rows: int, block_cols: int, row_offset: int = 0,
@@ -195,17 +197,22 @@ class DenseMatrixSet(UserSet):
         return self
 
     def set_panel(self, panel: torch.Tensor, total_rows: int, total_cols: int, block_rows: int, block_cols: int,
-                  row_offset: int = 0):
+                  row_offset: int = 0, transposed: bool = False, replicated: bool = False):
+        """Install a physical panel. ``transposed``: panel is [cols, rows] of the logical matrix."""
         self.panel = panel
         self.total_rows, self.total_cols = total_rows, total_cols
         self.block_rows, self.block_cols = block_rows, block_cols
         self.row_offset = row_offset
-        self.local_rows = panel.shape[0]
+        self.transposed = transposed
+        self.replicated = replicated
+        self.local_rows = panel.shape[1] if transposed else panel.shape[0]
         self.stats = {"records": self.num_blocks(), "bytes": panel.numel() * panel.element_size()}
         return self
 
     def matrix(self) -> torch.Tensor:
-        """[local_rows, total_cols] view (row stride = padded ld)."""
+        """Logical [local_rows, total_cols] view (a transposed view when the panel is transposed)."""
+        if self.transposed:
+            return self.panel[: self.total_cols, : self.local_rows].t()
         return self.panel[:, : self.total_cols]
 
     def num_blocks(self) -> int:
