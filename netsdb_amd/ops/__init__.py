@@ -68,6 +68,20 @@ def gemm_nt(A, B, bias=None, bias_mode=BIAS_NONE, act=ACT_NONE, out_dtype=torch.
     if _use_hip(A, B):
         if bias is not None and bias.dtype != torch.float32:
             bias = bias.float()
+        # compute dtype is bf16 on the matrix cores (f32 operands are rounded once here)
+        if A.dtype != torch.bfloat16:
+            A = A.to(torch.bfloat16)
+        if B.dtype != torch.bfloat16:
+            B = B.to(torch.bfloat16)
+        if A.stride(-1) != 1 or A.stride(-2) % 8:
+            A = pad_k(A.contiguous())
+        if B.stride(-1) != 1 or B.stride(-2) % 8:
+            B = pad_k(B.contiguous())
+        if A.shape[-1] != B.shape[-1] or A.shape[-1] % 8:
+            k = max(A.shape[-1], B.shape[-1])
+            k = (k + 7) // 8 * 8
+            A = torch.nn.functional.pad(A, (0, k - A.shape[-1])) if A.shape[-1] < k else A
+            B = torch.nn.functional.pad(B, (0, k - B.shape[-1])) if B.shape[-1] < k else B
         return _ext.hip().gemm_nt(A, B, bias, int(bias_mode if bias is not None else 0), act,
                                   out_dtype == torch.float32, float(alpha), float(dropout), int(seed),
                                   int(splits), out)
