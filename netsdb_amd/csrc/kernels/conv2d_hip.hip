@@ -17,7 +17,7 @@
 
 namespace nsdb {
 
-constexpr int CV_BM = 128, CV_BN = 64, CV_KC = 512;      // K staged in LDS in chunks of 512
+constexpr int CV_BM = 128, CV_BN = 64, CV_KC = 256;      // K staged in LDS in chunks of 256 (36 KB LDS -> 4 blocks/CU)
 constexpr int CV_WROW = CV_KC * 2 + 16;                   // padded LDS row (bytes) of the filter panel
 
 struct ConvParams {
@@ -31,7 +31,7 @@ struct ConvParams {
   int act, nchw_out, out_f32;
 };
 
-__global__ void __launch_bounds__(256, 2) conv2d_igemm_kernel(ConvParams p) {
+__global__ void __launch_bounds__(256, 4) conv2d_igemm_kernel(ConvParams p) {
   __shared__ __attribute__((aligned(16))) char smem[CV_BN * CV_WROW + CV_KC * 8];
   char* wpanel = smem;
   int* koff = reinterpret_cast<int*>(smem + CV_BN * CV_WROW);          // per-k image offset
@@ -65,6 +65,8 @@ __global__ void __launch_bounds__(256, 2) conv2d_igemm_kernel(ConvParams p) {
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned short*>(p.X), (short)0, (int)((long long)p.N * p.C * HW * 2), 0x00020000);
 
   for (int kc = 0; kc < p.K; kc += CV_KC) {
     const int klen = min(CV_KC, p.K - kc);
@@ -92,54 +94,104 @@ __global__ void __launch_bounds__(256, 2) conv2d_igemm_kernel(ConvParams p) {
     }
     __syncthreads();
 
-    for (int ks = 0; ks < klen32; ks += 32) {
+    // software-pipelined gather: the 16 loads of k-step t+1 are issued before step t's MFMAs and
+    // only packed into the bf16x8 fragment after them (sched_barrier keeps the pack below)
+    auto gather = [&](int ks, unsigned (&raw)[2][8]) {
       const int kb = ks + 8 * (lane >> 4);
-      bf16x8 af[2];
+      // (kh, kw) and image offsets of this lane's 8 k values: 4 x ds_read_b128 (16 lanes share them)
+      const int4 ko0 = *reinterpret_cast<const int4*>(koff + kb), ko1 = *reinterpret_cast<const int4*>(koff + kb + 4);
+      const int4 hw0 = *reinterpret_cast<const int4*>(khw + kb), hw1 = *reinterpret_cast<const int4*>(khw + kb + 4);
+      const int ko[8] = {ko0.x, ko0.y, ko0.z, ko0.w, ko1.x, ko1.y, ko1.z, ko1.w};
+      const int hw[8] = {hw0.x, hw0.y, hw0.z, hw0.w, hw1.x, hw1.y, hw1.z, hw1.w};
+      // buffer loads: a masked lane gets an out-of-range offset and the descriptor's range check
+      // returns 0 -> no select after the load and no branch around it
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
+        const int base = pix_base[i] + ih0[i] * p.W + iw0[i];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const int hw = khw[kb + j];
-          const int ih = ih0[i] + (hw >> 16), iw = iw0[i] + (hw & 0xffff);
-          unsigned short v = 0;
-          if (pix_ok[i] && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W)
-            v = p.X[(long long)pix_base[i] + koff[kb + j] + ih0[i] * p.W + iw0[i]];
-          af[i][j] = (short)v;
+          const int ih = ih0[i] + (hw[j] >> 16), iw = iw0[i] + (hw[j] & 0xffff);
+          const bool ok = pix_ok[i] & ((unsigned)ih < (unsigned)p.H) & ((unsigned)iw < (unsigned)p.W);
+          const int off = ok ? (base + ko[j]) * 2 : 0x7ffffff0;
+          raw[i][j] = __builtin_amdgcn_raw_buffer_load_b16(xr, off, 0, 0);
         }
       }
+    };
+    auto pack = [&](const unsigned (&raw)[2][8], bf16x8 (&af)[2]) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) af[i][j] = (short)raw[i][j];
+    };
+    unsigned raw[2][8];
+    bf16x8 cur[2];
+    gather(0, raw);
+    pack(raw, cur);
+    for (int ks = 0; ks < klen32; ks += 32) {
+      const bool more = ks + 32 < klen32;
+      if (more) gather(ks + 32, raw);
+      __builtin_amdgcn_sched_barrier(0);
+      const int kb = ks + 8 * (lane >> 4);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(wpanel + (j * 16 + (lane & 15)) * CV_WROW + kb * 2);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[i], bfr, acc[i][j], 0, 0, 0);
       }
+      __builtin_amdgcn_sched_barrier(0);
+      if (more) pack(raw, cur);
     }
   }
 
-  // epilogue: col (oc) = lane&15, row (pixel) = (lane>>4)*4 + r
+  // epilogue: col (oc) = lane&15, row (pixel) = (lane>>4)*4 + r. NCHW: the lane's 4 pixels are
+  // consecutive in one output plane -> one 8-byte (bf16) / 16-byte (f32) store when they share an image.
+  const long long OHW = (long long)p.OH * p.OW;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int oc = oc0 + j * 16 + (lane & 15);
     if (oc >= p.OC) continue;
     const float b = p.bias ? p.bias[oc] : 0.f;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i) {
+      const long long pp0 = p0 + wave * 32 + i * 16 + (lane >> 4) * 4;
+      float vv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) vv[r] = apply_act(acc[i][j][r] + b, p.act);
+      if (p.nchw_out) {
+        const long long n0 = pp0 / OHW, rem0 = pp0 % OHW;
+        if (pp0 + 3 < P && rem0 + 3 < OHW) {
+          const long long off = (n0 * p.OC + oc) * OHW + rem0;
+          if (p.out_f32) {
+            float* o = reinterpret_cast<float*>(p.out) + off;
+            if ((off & 3) == 0) *reinterpret_cast<float4*>(o) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+            else { o[0] = vv[0]; o[1] = vv[1]; o[2] = vv[2]; o[3] = vv[3]; }
+          } else {
+            unsigned short* o = reinterpret_cast<unsigned short*>(p.out) + off;
+            const unsigned lo = f32_to_bf16(vv[0]) | ((unsigned)f32_to_bf16(vv[1]) << 16);
+            const unsigned hi = f32_to_bf16(vv[2]) | ((unsigned)f32_to_bf16(vv[3]) << 16);
+            if ((off & 3) == 0) *reinterpret_cast<uint2*>(o) = make_uint2(lo, hi);
+            else if ((off & 1) == 0) { reinterpret_cast<unsigned*>(o)[0] = lo; reinterpret_cast<unsigned*>(o)[1] = hi; }
+            else { o[0] = (unsigned short)lo; o[1] = (unsigned short)(lo >> 16); o[2] = (unsigned short)hi; o[3] = (unsigned short)(hi >> 16); }
+          }
+          continue;
+        }
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const long long pp = p0 + wave * 32 + i * 16 + (lane >> 4) * 4 + r;
+        const long long pp = pp0 + r;
         if (pp >= P) continue;
-        const float v = apply_act(acc[i][j][r] + b, p.act);
         long long off;
         if (p.nchw_out) {
-          const long long n = pp / (p.OH * p.OW), rem = pp % (p.OH * p.OW);
-          off = (n * p.OC + oc) * (long long)(p.OH * p.OW) + rem;
+          const long long n = pp / OHW, rem = pp % OHW;
+          off = (n * p.OC + oc) * OHW + rem;
         } else {
           off = pp * p.OC + oc;
         }
-        if (p.out_f32) reinterpret_cast<float*>(p.out)[off] = v;
-        else reinterpret_cast<unsigned short*>(p.out)[off] = f32_to_bf16(v);
+        if (p.out_f32) reinterpret_cast<float*>(p.out)[off] = vv[r];
+        else reinterpret_cast<unsigned short*>(p.out)[off] = f32_to_bf16(vv[r]);
       }
+    }
   }
 }
 
