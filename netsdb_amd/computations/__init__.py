@@ -270,12 +270,45 @@ class RowSoftmax:
 
 @dataclass
 class Elementwise:
+    """join(A.key == B.key) projecting op(A.data, B.data) blockwise (LASillyAddJoin, ...Substract,
+    ...ScaleMultiply)."""
+
     op: str = "add"
     extra: dict = field(default_factory=dict)
 
 
+@dataclass
+class Transpose:
+    """selection swapping block indices and transposing payloads (LASillyTransposeSelection)."""
+
+
+@dataclass
+class Reduce:
+    """aggregate reducing a matrix along rows ('row' -> column vector), columns ('col' -> row vector)
+    or everything ('all' -> 1x1) with max/min/sum (LASillyRow/Col/Max/MinElement/...Aggregate)."""
+
+    axis: str = "row"
+    op: str = "sum"
+
+
+@dataclass
+class Inverse:
+    """matrix inverse (LASillyInverse1Aggregate + Inverse2Selection + Inverse3MultiSelection)."""
+
+
+@dataclass
+class Duplicate:
+    """multi-selection repeating a row vector down ('row') or a column vector across ('col')
+    (LASillyDuplicateRowMultiSelection / DuplicateColMultiSelection)."""
+
+    axis: str = "row"
+    block_size: int = 1
+    num_blocks: int = 1
+
+
 __all__ = ["Computation", "ScanSet", "ScanUserSet", "WriteSet", "WriteUserSet", "SelectionComp",
            "MultiSelectionComp", "JoinComp", "AggregateComp", "ClusterAggregateComp", "PartitionComp", "TopKComp",
-           "BlockMatmul", "BlockSum", "BiasAct", "RowSoftmax", "Elementwise"]
+           "BlockMatmul", "BlockSum", "BiasAct", "RowSoftmax", "Elementwise", "Transpose", "Reduce", "Inverse",
+           "Duplicate"]
 
 _ = (Any, Callable, Sequence, torch)

@@ -10,7 +10,7 @@ int nsdb_gemm_splits(int M, int N, int K, int batch);
 int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const float* bias, int M, int N, int K,
                       long long lda, long long ldb, long long ldc, long long sA, long long sB, long long sC,
                       long long sBias, int batch, int splits, int act, int bias_mode, int out_f32, float alpha,
-                      float dropout, unsigned long long seed, hipStream_t stream);
+                      float dropout, unsigned long long seed, int accumulate, hipStream_t stream);
 int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* out, int N, int C, int H, int W,
                       int OC, int KH, int KW, int stride, int pad, int dil, int ldw, int act, int nchw_out,
                       int out_f32, hipStream_t stream);
@@ -47,7 +47,7 @@ bool is_f32(const torch::Tensor& t, const char* name) {
 // C = epi(alpha * A @ B^T); A [b?,M,K] bf16, B [b?,N,K] bf16 (row stride may exceed K), bias f32.
 torch::Tensor gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Tensor> bias, int64_t bias_mode,
                       int64_t act, bool out_f32, double alpha, double dropout, int64_t seed, int64_t splits,
-                      c10::optional<torch::Tensor> out) {
+                      c10::optional<torch::Tensor> out, bool accumulate) {
   check_cuda(A, "A");
   check_cuda(B, "B");
   TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && B.scalar_type() == torch::kBFloat16, "A,B must be bf16");
@@ -80,8 +80,10 @@ torch::Tensor gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Ten
     TORCH_CHECK(C.scalar_type() == opts.dtype(), "out dtype mismatch");
     TORCH_CHECK(C.size(-2) == M && C.size(-1) == N && C.stride(-1) == 1, "out shape mismatch");
   } else {
+    TORCH_CHECK(!accumulate, "accumulate=True needs an existing f32 out tensor");
     C = batched ? torch::empty({batch, M, N}, opts) : torch::empty({M, N}, opts);
   }
+  TORCH_CHECK(!accumulate || out_f32, "accumulate=True needs out_f32");
   int s = splits > 0 ? (int)splits : nsdb_gemm_splits((int)M, (int)N, (int)K, (int)batch);
   torch::Tensor ws;
   float* wsp = nullptr;
@@ -93,7 +95,7 @@ torch::Tensor gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Ten
       A.data_ptr(), B.data_ptr(), C.data_ptr(), wsp, bptr, (int)M, (int)N, (int)K, A.stride(-2), B.stride(-2),
       C.stride(-2), batched ? A.stride(0) : 0, batched ? B.stride(0) : 0, batched ? C.stride(0) : 0, sBias,
       (int)batch, s, (int)act, (int)bias_mode, out_f32 ? 1 : 0, (float)alpha, (float)dropout,
-      (unsigned long long)seed, cur_stream());
+      (unsigned long long)seed, accumulate ? 1 : 0, cur_stream());
   check_rc(rc, "gemm_nt");
   return C;
 }
@@ -224,7 +226,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "netsdb_amd CDNA4 (gfx950) HIP kernels";
   m.def("gemm_nt", &gemm_nt, "epi(alpha*A@B^T) on MFMA", py::arg("A"), py::arg("B"), py::arg("bias") = py::none(),
         py::arg("bias_mode") = 0, py::arg("act") = 0, py::arg("out_f32") = false, py::arg("alpha") = 1.0,
-        py::arg("dropout") = 0.0, py::arg("seed") = 0, py::arg("splits") = 0, py::arg("out") = py::none());
+        py::arg("dropout") = 0.0, py::arg("seed") = 0, py::arg("splits") = 0, py::arg("out") = py::none(),
+        py::arg("accumulate") = false);
   m.def("gemm_splits", &gemm_splits);
   m.def("conv2d", &conv2d, py::arg("X"), py::arg("W"), py::arg("bias") = py::none(), py::arg("KH") = 1,
         py::arg("KW") = 1, py::arg("stride") = 1, py::arg("pad") = 0, py::arg("dil") = 1, py::arg("act") = 0,

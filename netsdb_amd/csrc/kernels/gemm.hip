@@ -39,7 +39,7 @@ struct GemmParams {
   long long sA, sB, sC, sBias;
   int M, N, K;
   int splits, kchunk;
-  int act, bias_mode, out_f32;
+  int act, bias_mode, out_f32, accumulate;
   float alpha, dropout;
   unsigned long long seed;
   int tiles_m, tiles_n;
@@ -178,6 +178,7 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_nt_bf16_kernel(GemmParams p)
           v = hash_uniform(p.seed, idx) < p.dropout ? 0.f : v * keep_scale;
         }
         const long long off = batch * p.sC + (long long)row * p.ldc + col;
+        if (p.accumulate) v += reinterpret_cast<float*>(p.C)[off];
         if (p.out_f32) reinterpret_cast<float*>(p.C)[off] = v;
         else reinterpret_cast<unsigned short*>(p.C)[off] = f32_to_bf16(v);
       }
@@ -206,6 +207,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(GemmParams p) {
       v = hash_uniform(p.seed, idx) < p.dropout ? 0.f : v * keep_scale;
     }
     const long long off = batch * p.sC + (long long)row * p.ldc + col;
+    if (p.accumulate) v += reinterpret_cast<float*>(p.C)[off];
     if (p.out_f32) reinterpret_cast<float*>(p.C)[off] = v;
     else reinterpret_cast<unsigned short*>(p.C)[off] = f32_to_bf16(v);
   }
@@ -237,12 +239,13 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
                       int M, int N, int K, long long lda, long long ldb, long long ldc,
                       long long sA, long long sB, long long sC, long long sBias, int batch,
                       int splits, int act, int bias_mode, int out_f32, float alpha, float dropout,
-                      unsigned long long seed, hipStream_t stream) {
+                      unsigned long long seed, int accumulate, hipStream_t stream) {
   if (M <= 0 || N <= 0 || batch <= 0) return 0;
   if (K % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0) return -1;        // 16-B rows for the LDS-DMA
   if ((long long)nsdb::BM * lda * 2 >= 0x7ffffff0LL || (long long)nsdb::BN * ldb * 2 >= 0x7ffffff0LL)
     return -2;                                                         // per-tile buffer range
   if (splits > 1 && ws == nullptr) return -3;
+  if (accumulate && !out_f32) return -4;                                // C += A.B^T only into f32
   nsdb::GemmParams p;
   p.A = (const unsigned short*)A; p.B = (const unsigned short*)B; p.C = C; p.ws = ws; p.bias = bias;
   p.lda = lda; p.ldb = ldb; p.ldc = ldc; p.sA = sA; p.sB = sB; p.sC = sC; p.sBias = sBias;
@@ -253,7 +256,7 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
   p.kchunk = std::max(1, kchunk_steps) * nsdb::BK;
   p.splits = (K + p.kchunk - 1) / p.kchunk;
   if (p.splits < 1) p.splits = 1;
-  p.act = act; p.bias_mode = bias ? bias_mode : 0; p.out_f32 = out_f32;
+  p.act = act; p.bias_mode = bias ? bias_mode : 0; p.out_f32 = out_f32; p.accumulate = accumulate;
   p.alpha = alpha; p.dropout = dropout; p.seed = seed;
   p.tiles_m = (M + nsdb::BM - 1) / nsdb::BM;
   p.tiles_n = (N + nsdb::BN - 1) / nsdb::BN;

@@ -62,8 +62,9 @@ def _use_hip(*ts) -> bool:
 
 
 def gemm_nt(A, B, bias=None, bias_mode=BIAS_NONE, act=ACT_NONE, out_dtype=torch.bfloat16, alpha=1.0,
-            dropout=0.0, seed=0, splits=0, out=None):
-    """epilogue(alpha * A @ B^T): A [..,M,K], B [..,N,K] (K-contiguous), bias f32 per row/col."""
+            dropout=0.0, seed=0, splits=0, out=None, accumulate=False):
+    """epilogue(alpha * A @ B^T) [+ out when accumulate]: A [..,M,K], B [..,N,K] (K-contiguous),
+    bias f32 per row/col. ``accumulate`` adds into an existing f32 ``out`` (C += A.B^T)."""
     act = act_code(act)
     if _use_hip(A, B):
         if bias is not None and bias.dtype != torch.float32:
@@ -84,13 +85,16 @@ def gemm_nt(A, B, bias=None, bias_mode=BIAS_NONE, act=ACT_NONE, out_dtype=torch.
             B = torch.nn.functional.pad(B, (0, k - B.shape[-1])) if B.shape[-1] < k else B
         return _ext.hip().gemm_nt(A, B, bias, int(bias_mode if bias is not None else 0), act,
                                   out_dtype == torch.float32, float(alpha), float(dropout), int(seed),
-                                  int(splits), out)
+                                  int(splits), out, bool(accumulate))
     v = torch.matmul(A.float(), B.float().transpose(-1, -2)) * alpha
     if bias is not None:
         b = bias.float()
         v = v + (b.unsqueeze(-1) if bias_mode == BIAS_ROW else b.unsqueeze(-2))
     v = _apply_act(v, act)
     v = _dropout_ref(v, dropout, seed)
+    if accumulate:
+        out.add_(v.to(out.dtype))
+        return out
     v = v.to(out_dtype)
     if out is not None:
         out.copy_(v)

@@ -142,11 +142,19 @@ class ClusterContext:
 
     # -------------------------------------------------------------- record batch shuffles
     def exchange(self, parts: Sequence[Optional[RecordBatch]], template: Optional[RecordBatch] = None) -> List[RecordBatch]:
-        """Shuffle: ``parts[d]`` goes to rank d; returns the batches received (one per source)."""
+        """Shuffle: ``parts[d]`` goes to rank d; returns the batches received (one per source).
+        Nested columns (RecordBatch object columns, tuple key columns) are flattened for the wire."""
         ws = self.world_size
         assert len(parts) == ws
         if not self.distributed:
             return [parts[0]] if parts[0] is not None else []
+        flat = [_flatten(p) if p is not None else None for p in parts]
+        tflat = _flatten(template) if template is not None else None
+        got = self._exchange_flat(flat, tflat)
+        return [_unflatten(g) for g in got]
+
+    def _exchange_flat(self, parts, template=None) -> List[RecordBatch]:
+        ws = self.world_size
         ref = template or next((p for p in parts if p is not None), None)
         meta = _batch_meta(ref)
         metas = [None] * ws
@@ -203,6 +211,60 @@ class ClusterContext:
         if not self.distributed:
             return [b] if b is not None else []
         return self.exchange([b] * self.world_size)
+
+
+_SEP = "\x1f"
+
+
+def _flatten(b: RecordBatch, prefix: str = "") -> RecordBatch:
+    """Nested RecordBatch / tuple columns -> flat columns named prefix+SEP-paths."""
+    cols = {}
+    for k, c in b.columns.items():
+        name = prefix + k
+        if isinstance(c, RecordBatch):
+            tn = c.type.type_name() if c.type is not None else ""
+            inner = _flatten(c, name + _SEP + "R" + tn + _SEP)
+            cols.update(inner.columns)
+            if not inner.columns:
+                cols[name + _SEP + "R" + tn + _SEP + "__empty__"] = torch.zeros(c.n, dtype=torch.int8)
+        elif isinstance(c, tuple):
+            for i, x in enumerate(c):
+                cols[name + _SEP + f"T{i}"] = x
+        else:
+            cols[name] = c
+    return RecordBatch(cols, b.n, b.type)
+
+
+def _unflatten(b: RecordBatch) -> RecordBatch:
+    if not any(_SEP in k for k in b.columns):
+        return b
+    tree: dict = {}
+    for k, c in b.columns.items():
+        parts = k.split(_SEP)
+        node = tree
+        for p in parts[:-1]:
+            node = node.setdefault(p, {})
+        node[parts[-1]] = c
+
+    def build(node, n, type_):
+        cols = {}
+        for k, v in node.items():
+            if isinstance(v, dict):
+                sub_keys = list(v)
+                if all(s.startswith("T") and s[1:].isdigit() for s in sub_keys) and not any(
+                        isinstance(x, dict) for x in v.values()):
+                    cols[k] = tuple(v[f"T{i}"] for i in range(len(sub_keys)))
+                else:
+                    (rk,) = sub_keys
+                    tn = rk[1:]
+                    inner = v[rk]
+                    inner.pop("__empty__", None)
+                    cols[k] = build(inner, n, lookup_type(tn) if tn else None)
+            else:
+                cols[k] = v
+        return RecordBatch(cols, n, type_)
+
+    return build(tree, b.n, b.type)
 
 
 def _batch_meta(b: Optional[RecordBatch]):

@@ -8,12 +8,20 @@ literally that is one small GEMM per block pair, a hash aggregation of partial b
 more pass per epilogue.
 
 When the computations declare their tensor pattern (``tensor_pattern()``) and the operands are
-dense matrix sets, this pass rewrites the chain into :class:`MatmulNode` s that run as ONE split-K
-MFMA GEMM each (the split-K slab reducer *is* the block aggregate) with bias/act/dropout fused in
-the epilogue, and :class:`SoftmaxNode` s for RowAggregate+OutputLayer.  Operand orientation is
-chosen per node so that every GEMM reads both operands K-contiguous with no transposes
-(``physical flag`` bookkeeping below).  Everything not matched runs through the generic TCAP
-pipeline; fused results feeding generic computations are materialised into temp dense sets.
+dense matrix sets, this pass rewrites the chain into nodes evaluated on the dense HBM panels:
+:class:`MatmulNode` = ONE split-K MFMA GEMM (the split-K slab reducer *is* the block aggregate)
+with bias/act/dropout fused in the epilogue; softmax/row-normalise, elementwise, transpose
+(a layout flag flip, no data movement), reductions, inverse and duplication nodes.  Operand
+orientation is chosen per node so every GEMM reads both operands K-contiguous with no transposes.
+
+Distribution (one rank per GPU): a matrix value is replicated or partitioned by logical rows or
+columns.  A matmul whose K dimension is partitioned runs as a ring: each rank multiplies its A
+column-slab with the B slab it holds while the next slab arrives from its neighbour over xGMI
+(``batch_isend_irecv`` on RCCL), accumulating into an f32 C with the GEMM's accumulate epilogue —
+netsDB's hash-partitioned join + shuffle-aggregate, overlapped with the block GEMMs.
+
+Everything not matched runs through the generic TCAP pipeline; fused results feeding generic
+computations are materialised into temp dense sets.
 """
 from __future__ import annotations
 
@@ -21,31 +29,39 @@ import itertools
 from typing import Dict, List, Optional, Tuple
 
 import torch
+import torch.distributed as dist
 
 from .. import ops
-from ..computations import (AggregateComp, BiasAct, BlockMatmul, BlockSum, Computation, JoinComp, RowSoftmax,
-                            ScanSet, WriteSet)
+from ..computations import (AggregateComp, BiasAct, BlockMatmul, BlockSum, Computation, Duplicate, Elementwise,
+                            Inverse, JoinComp, MultiSelectionComp, Reduce, RowSoftmax, ScanSet, SelectionComp,
+                            Transpose, WriteSet)
 from ..storage.sets import DenseMatrixSet
 
 _tmp_ids = itertools.count()
 
 
 class Dense:
-    """A logical matrix value: physical 2-D tensor + 'transposed' flag (+ block geometry)."""
+    """A logical matrix value: physical 2-D tensor + 'transposed' flag + distribution.
 
-    def __init__(self, phys: torch.Tensor, rows: int, cols: int, transposed: bool, br: int, bc: int):
+    ``rows``/``cols`` are the LOCAL logical extents; ``part`` is None (replicated), 'rows' or 'cols'
+    (the logical dimension split over ranks, ``offset`` = first global index held here,
+    ``total`` = global extent of that dimension)."""
+
+    def __init__(self, phys: torch.Tensor, rows: int, cols: int, transposed: bool, br: int, bc: int,
+                 part: Optional[str] = None, offset: int = 0, total: Optional[int] = None):
         self.phys, self.rows, self.cols, self.transposed = phys, rows, cols, transposed
         self.br, self.bc = br, bc
+        self.part, self.offset = part, offset
+        self.total = total if total is not None else (rows if part == "rows" else cols if part == "cols" else 0)
 
     def physical(self, want_transposed: bool) -> torch.Tensor:
         """K-contiguous physical layout in the wanted orientation (copy only on mismatch)."""
         if want_transposed == self.transposed:
             p = self.phys
         else:
-            # logical L: phys = L if not transposed else L^T; materialise the other orientation
             r, c = (self.cols, self.rows) if self.transposed else (self.rows, self.cols)
             p = self.phys[:r, :c].t().contiguous()
-        if p.shape[1] % 8 or p.stride(0) % 8:
+        if p.shape[1] % 8 or p.stride(0) % 8 or p.stride(1) != 1:
             p = ops.pad_k(p.contiguous())
         return p
 
@@ -54,6 +70,16 @@ class Dense:
             return self.phys[: self.cols, : self.rows].t()
         return self.phys[: self.rows, : self.cols]
 
+    def t(self) -> "Dense":
+        part = {"rows": "cols", "cols": "rows"}.get(self.part) if self.part else None
+        return Dense(self.phys, self.cols, self.rows, not self.transposed, self.bc, self.br, part, self.offset,
+                     self.total)
+
+    @staticmethod
+    def of(t: torch.Tensor, br: int, bc: int, part=None, offset=0, total=None) -> "Dense":
+        phys = t if (t.shape[1] % 8 == 0 and t.stride(1) == 1) else ops.pad_k(t.contiguous())
+        return Dense(phys, t.shape[0], t.shape[1], False, br, bc, part, offset, total)
+
 
 def _kslice(t: torch.Tensor, rows: int, k8: int) -> torch.Tensor:
     """[rows, k8] view of a zero-padded physical panel (pads with zeros when it is narrower)."""
@@ -61,6 +87,19 @@ def _kslice(t: torch.Tensor, rows: int, k8: int) -> torch.Tensor:
     if t.shape[1] < k8:
         t = torch.nn.functional.pad(t, (0, k8 - t.shape[1]))
     return t[:, :k8]
+
+
+def _replicate(engine, d: Dense) -> Dense:
+    """All-gather a partitioned value along its split dimension (broadcast-join build side)."""
+    ctx = engine.ctx
+    if d.part is None or not ctx.distributed:
+        return d
+    L = d.logical()
+    if d.part == "rows":
+        full = torch.cat(ctx.all_gather_tensor(L.contiguous()))
+    else:
+        full = torch.cat(ctx.all_gather_tensor(L.t().contiguous())).t()
+    return Dense.of(full.contiguous(), d.br, d.bc)
 
 
 class Node:
@@ -75,11 +114,9 @@ class SourceNode(Node):
     def eval(self, engine) -> Dense:
         s = self.set
         if self.value is None:
-            phys = s.panel
-            rows, cols = (s.local_rows, s.total_cols)
-            if s.transposed:
-                phys = s.panel
-            self.value = Dense(phys, rows, cols, s.transposed, s.block_rows, s.block_cols)
+            part = None if (s.replicated or not engine.ctx.distributed) else "rows"
+            self.value = Dense(s.panel, s.local_rows, s.total_cols, s.transposed, s.block_rows, s.block_cols,
+                               part, s.row_offset, s.total_rows)
         return self.value
 
 
@@ -97,47 +134,101 @@ class MatmulNode(Node):
         if self.value is not None:
             return self.value
         A, B = self.a.eval(engine), self.b.eval(engine)
-        # effective logical operands: C = opA(A) . opB(B)
-        M = A.cols if self.p.transpose_a else A.rows
-        K = A.rows if self.p.transpose_a else A.cols
-        N = B.rows if self.p.transpose_b else B.cols
-        Kb = B.cols if self.p.transpose_b else B.rows
-        if K != Kb:
-            raise ValueError(f"fused matmul K mismatch {K} vs {Kb}")
-        # X = opA(A) as [M,K] K-contig <=> physical(A) with flag == transpose_a
-        # Y = opB(B)^T as [N,K] K-contig <=> physical(B) with flag == (not transpose_b)
-        K8 = (K + 7) // 8 * 8
-        X = _kslice(A.physical(self.p.transpose_a), M, K8)
-        Y = _kslice(B.physical(not self.p.transpose_b), N, K8)
-        # logical output L = C (or C^T with transpose_out); the consumer asks for a physical
-        # orientation relative to L; compute C = X.Y^T or C^T = Y.X^T accordingly (no copies)
+        opA = A.t() if self.p.transpose_a else A           # [M, K]
+        opB = B.t() if self.p.transpose_b else B           # [K, N]
+        # distribution: M-split A and N-split B are local; a K-split needs the ring
+        if opA.part == "rows" and opB.part == "cols":
+            opB = _replicate(engine, opB)
+        ring = opA.part == "cols" and opB.part == "rows"
+        if opA.part == "cols" and not ring:
+            opA = _replicate(engine, opA)
+        if opB.part == "rows" and not ring:
+            opB = _replicate(engine, opB)
+        M, K, N = opA.rows, opA.cols, opB.cols
+        if not ring and K != opB.rows:
+            raise ValueError(f"fused matmul K mismatch {K} vs {opB.rows}")
         want_t = bool(self.consumers_want_t)
         phys_is_c = self.transpose_out == want_t
-        bias_t = None
-        mode = ops.BIAS_NONE
+        bias_t, mode = None, ops.BIAS_NONE
         if self.bias is not None:
-            bias_t = self.bias.eval(engine).logical().reshape(-1).float().contiguous()
+            bias_t = _replicate(engine, self.bias.eval(engine)).logical().reshape(-1).float().contiguous()
             along_c_rows = self.bias_along == "row"
+            if opA.part == "rows" and along_c_rows:
+                bias_t = bias_t[opA.offset: opA.offset + M]
+            if opB.part == "cols" and not along_c_rows:
+                bias_t = bias_t[opB.offset: opB.offset + N]
             mode = (ops.BIAS_ROW if along_c_rows else ops.BIAS_COL) if phys_is_c else \
                 (ops.BIAS_COL if along_c_rows else ops.BIAS_ROW)
         act = ops.act_code(self.act)
-        # exp'd scores (FFTransposeBiasSum) keep f32 so the later row normalisation is exact
-        odt = torch.float32 if act == ops.ACT_EXP else torch.bfloat16
-        if phys_is_c:
-            phys = ops.gemm_nt(X, Y, bias_t, mode, act, out_dtype=odt, dropout=self.dropout, seed=self.seed)
+        # exp'd scores keep f32 (exact row normalisation); f32 operands keep an f32 result
+        odt = torch.float32 if (act == ops.ACT_EXP or opA.phys.dtype == torch.float32
+                                or opB.phys.dtype == torch.float32) else torch.bfloat16
+        if ring:
+            phys = self._ring(engine, opA, opB, M, N, phys_is_c, bias_t, mode, act, odt)
         else:
-            phys = ops.gemm_nt(Y, X, bias_t, mode, act, out_dtype=odt, dropout=self.dropout, seed=self.seed)
-        lr, lc = (M, N) if not self.transpose_out else (N, M)
-        transposed = want_t
-        br = A.bc if self.p.transpose_a else A.br
-        bc = B.br if self.p.transpose_b else B.bc
+            K8 = (K + 7) // 8 * 8
+            # X = opA as [M,K] K-contig <=> opA physical not transposed; Y = opB^T as [N,K]
+            X = _kslice(opA.physical(False), M, K8)
+            Y = _kslice(opB.physical(True), N, K8)
+            if phys_is_c:
+                phys = ops.gemm_nt(X, Y, bias_t, mode, act, out_dtype=odt, dropout=self.dropout, seed=self.seed)
+            else:
+                phys = ops.gemm_nt(Y, X, bias_t, mode, act, out_dtype=odt, dropout=self.dropout, seed=self.seed)
+        part, offset, total = None, 0, None
+        if opA.part == "rows":
+            part, offset, total = "rows", opA.offset, opA.total
+        elif opB.part == "cols":
+            part, offset, total = "cols", opB.offset, opB.total
+        br, bc = opA.br, opB.bc
         if self.transpose_out:
-            br, bc = bc, br
-        self.value = Dense(phys, lr, lc, transposed, br, bc)
-        return self.value
+            value = Dense(phys, N, M, want_t, bc, br, {"rows": "cols", "cols": "rows"}.get(part), offset, total)
+        else:
+            value = Dense(phys, M, N, want_t, br, bc, part, offset, total)
+        self.value = value
+        return value
+
+    def _ring(self, engine, opA: Dense, opB: Dense, M, N, phys_is_c, bias_t, mode, act, odt):
+        """K-partitioned matmul: C_r = sum_s A_r[:, K_s] . B_s with B slabs circulating on a ring."""
+        ctx = engine.ctx
+        ws, r = ctx.world_size, ctx.rank
+        kr = torch.tensor([[opB.offset, opB.rows]], dtype=torch.int64, device=ctx.device)
+        allk = ctx.all_gather_tensor(kr)
+        ranges = [(int(x[0, 0]), int(x[0, 1])) for x in allk]
+        kmax = max(k for _, k in ranges)
+        kmax8 = (kmax + 7) // 8 * 8
+        # local slab of B^T [N, Ks] (K-contiguous), padded to the largest slab for the ring buffers
+        bt = opB.physical(True)[:N, :opB.rows]
+        buf = [torch.zeros(N, kmax8, dtype=torch.bfloat16, device=bt.device) for _ in range(2)]
+        buf[0][:, :opB.rows].copy_(bt)
+        A_full = opA.physical(False)   # [M, K_total] local rows, all columns
+        C = torch.zeros(M, N, dtype=torch.float32, device=bt.device)
+        cur = 0
+        for t in range(ws):
+            s = (r - t) % ws
+            reqs = []
+            if t + 1 < ws:
+                p2p = [dist.P2POp(dist.isend, buf[cur], (r + 1) % ws),
+                       dist.P2POp(dist.irecv, buf[cur ^ 1], (r - 1) % ws)]
+                reqs = dist.batch_isend_irecv(p2p)
+            k0, ks = ranges[s]
+            k8 = (ks + 7) // 8 * 8
+            if k0 % 8 == 0 and k0 + k8 <= A_full.shape[1]:
+                Xs = A_full[:M, k0:k0 + k8]
+            else:
+                Xs = ops.pad_k(A_full[:M, k0:k0 + ks].contiguous())
+            Ys = buf[cur][:, :k8]
+            ops.gemm_nt(Xs, Ys, out=C, out_dtype=torch.float32, accumulate=True)
+            for q in reqs:
+                q.wait()
+            cur ^= 1
+        # epilogue (bias/act/dropout) on the summed f32 C
+        src = C if phys_is_c else C.t().contiguous()
+        return ops.bias_act(src, bias_t, mode if mode else ops.BIAS_COL, act, self.dropout, self.seed, out_dtype=odt)
 
 
 class SoftmaxNode(Node):
+    """RowAggregate(sum) + OutputLayer(divide) over exp'd scores == row normalisation."""
+
     def __init__(self, x: Node):
         self.x = x
 
@@ -145,12 +236,13 @@ class SoftmaxNode(Node):
         if self.value is None:
             self.x.consumers_want_t = False
             X = self.x.eval(engine)
-            phys = X.physical(False)[:, : X.cols]
+            if X.part == "cols":
+                X = _replicate(engine, X)
+            phys = X.physical(False)[: X.rows, : X.cols]
             if phys.stride(-1) != 1:
                 phys = phys.contiguous()
-            # RowAggregate(sum) + OutputLayer(divide) over exp'd scores == row normalisation
             y = ops.row_normalize(phys, out_dtype=torch.float32)
-            self.value = Dense(y, X.rows, X.cols, False, X.br, X.bc)
+            self.value = Dense(y, X.rows, X.cols, False, X.br, X.bc, X.part, X.offset, X.total)
         return self.value
 
 
@@ -164,14 +256,105 @@ class BiasActNode(Node):
         if self.value is None:
             self.x.consumers_want_t = False
             X = self.x.eval(engine)
-            b = self.bias.eval(engine).logical().reshape(-1).float().contiguous()
-            phys = X.physical(False)[:, : X.cols].contiguous()
+            b = _replicate(engine, self.bias.eval(engine)).logical().reshape(-1).float().contiguous()
+            if X.part == "rows" and self.p.bias_along == "row":
+                b = b[X.offset: X.offset + X.rows]
+            if X.part == "cols" and self.p.bias_along != "row":
+                b = b[X.offset: X.offset + X.cols]
+            phys = X.physical(False)[: X.rows, : X.cols].contiguous()
             mode = ops.BIAS_ROW if self.p.bias_along == "row" else ops.BIAS_COL
             y = ops.bias_act(phys, b, mode, ops.act_code(self.p.act), self.p.dropout, self.p.seed)
-            if self.p.transpose_out:
-                self.value = Dense(ops.pad_k(y), X.cols, X.rows, True, X.bc, X.br)
+            v = Dense.of(y, X.br, X.bc, X.part, X.offset, X.total)
+            self.value = v.t() if self.p.transpose_out else v
+        return self.value
+
+
+class EwiseNode(Node):
+    _OPS = {"add": torch.add, "sub": torch.sub, "mul": torch.mul, "div": torch.div}
+
+    def __init__(self, a: Node, b: Node, op: str):
+        self.a, self.b, self.op = a, b, op
+
+    def eval(self, engine) -> Dense:
+        if self.value is None:
+            A, B = self.a.eval(engine), self.b.eval(engine)
+            if A.part != B.part or A.offset != B.offset:
+                A, B = _replicate(engine, A), _replicate(engine, B)
+            y = self._OPS[self.op](A.logical().float(), B.logical().float()).to(torch.bfloat16)
+            self.value = Dense.of(y.contiguous(), A.br, A.bc, A.part, A.offset, A.total)
+        return self.value
+
+
+class TransposeNode(Node):
+    def __init__(self, x: Node):
+        self.x = x
+
+    def eval(self, engine) -> Dense:
+        if self.value is None:
+            self.value = self.x.eval(engine).t()      # metadata only: flip the layout flag
+        return self.value
+
+
+def _dop(op):
+    return {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
+
+
+class ReduceNode(Node):
+    def __init__(self, x: Node, axis: str, op: str):
+        self.x, self.axis, self.op = x, axis, op
+
+    def eval(self, engine) -> Dense:
+        if self.value is None:
+            X = self.x.eval(engine)
+            L = X.logical().float()
+            red = {"sum": torch.sum, "max": torch.amax, "min": torch.amin}[self.op]
+            ctx = engine.ctx
+            if self.axis == "row":          # -> column vector [rows, 1]
+                y = red(L, dim=1, keepdim=True)
+                if X.part == "cols":
+                    y = ctx.all_reduce(y.contiguous(), _dop(self.op))
+                v = Dense.of(y, X.br, 1, "rows" if X.part == "rows" else None, X.offset, X.total)
+            elif self.axis == "col":        # -> row vector [1, cols]
+                y = red(L, dim=0, keepdim=True)
+                if X.part == "rows":
+                    y = ctx.all_reduce(y.contiguous(), _dop(self.op))
+                v = Dense.of(y, 1, X.bc, "cols" if X.part == "cols" else None, X.offset, X.total)
             else:
-                self.value = Dense(ops.pad_k(y), X.rows, X.cols, False, X.br, X.bc)
+                y = red(L).reshape(1, 1)
+                if X.part is not None:
+                    y = ctx.all_reduce(y.contiguous(), _dop(self.op))
+                v = Dense.of(y, 1, 1)
+            self.value = v
+        return self.value
+
+
+class InverseNode(Node):
+    def __init__(self, x: Node):
+        self.x = x
+
+    def eval(self, engine) -> Dense:
+        if self.value is None:
+            X = _replicate(engine, self.x.eval(engine))
+            inv = torch.linalg.inv(X.logical().double()).float()
+            self.value = Dense.of(inv.contiguous(), X.br, X.bc)
+        return self.value
+
+
+class DuplicateNode(Node):
+    def __init__(self, x: Node, pat: Duplicate):
+        self.x, self.p = x, pat
+
+    def eval(self, engine) -> Dense:
+        if self.value is None:
+            X = _replicate(engine, self.x.eval(engine))
+            L = X.logical()
+            n = self.p.block_size * self.p.num_blocks
+            if self.p.axis == "row":
+                y = L[:1].expand(n, L.shape[1]).contiguous()
+                self.value = Dense.of(y, self.p.block_size, X.bc)
+            else:
+                y = L[:, :1].expand(L.shape[0], n).contiguous()
+                self.value = Dense.of(y, X.br, self.p.block_size)
         return self.value
 
 
@@ -202,6 +385,9 @@ class Fuser:
         if src is not None:
             return src
         pat = c.tensor_pattern()
+        if pat is None:
+            return None
+        name = type(c).__name__
         if isinstance(c, AggregateComp) and isinstance(pat, BlockSum):
             j = c.inputs[0]
             jp = j.tensor_pattern() if j is not None else None
@@ -210,32 +396,62 @@ class Fuser:
                 b = self.match(j.inputs[jp.b_input])
                 if a is not None and b is not None:
                     node = MatmulNode(a, b, jp)
-                    # operand orientation requests flow to producers
-                    if isinstance(a, (MatmulNode, BiasActNode)):
+                    if isinstance(a, MatmulNode):
                         a.consumers_want_t = jp.transpose_a
-                    if isinstance(b, (MatmulNode, BiasActNode)):
+                    if isinstance(b, MatmulNode):
                         b.consumers_want_t = not jp.transpose_b
-                    self.fused.append(f"matmul[{type(j).__name__}+{type(c).__name__}]")
+                    self.fused.append(f"matmul[{type(j).__name__}+{name}]")
                     return node
             return None
         if isinstance(c, JoinComp) and isinstance(pat, BiasAct):
             x = self.match(c.inputs[pat.data_input])
             b = self.match(c.inputs[pat.bias_input])
-            if x is None or not isinstance(b, SourceNode):
+            if x is None or b is None:
                 return None
-            if isinstance(x, MatmulNode) and x.bias is None and x.act == "none" and not x.transpose_out:
+            if isinstance(x, MatmulNode) and x.bias is None and x.act == "none" and not x.transpose_out \
+                    and x.value is None:
                 x.bias, x.bias_along, x.act, x.dropout, x.seed = b, pat.bias_along, pat.act, pat.dropout, pat.seed
                 x.transpose_out = pat.transpose_out
-                self.fused.append(f"epilogue[{type(c).__name__}]")
+                self.fused.append(f"epilogue[{name}]")
                 return x
-            self.fused.append(f"bias_act[{type(c).__name__}]")
+            self.fused.append(f"bias_act[{name}]")
             return BiasActNode(x, b, pat)
         if isinstance(c, JoinComp) and isinstance(pat, RowSoftmax):
             x = self.match(c.inputs[0])
             if x is None:
                 return None
-            self.fused.append(f"softmax[{type(c).__name__}]")
+            self.fused.append(f"softmax[{name}]")
             return SoftmaxNode(x)
+        if isinstance(c, JoinComp) and isinstance(pat, Elementwise):
+            a, b = self.match(c.inputs[0]), self.match(c.inputs[1])
+            if a is None or b is None:
+                return None
+            self.fused.append(f"ewise_{pat.op}[{name}]")
+            return EwiseNode(a, b, pat.op)
+        if isinstance(c, SelectionComp) and isinstance(pat, Transpose):
+            x = self.match(c.inputs[0])
+            if x is None:
+                return None
+            self.fused.append(f"transpose[{name}]")
+            return TransposeNode(x)
+        if isinstance(c, AggregateComp) and isinstance(pat, Reduce):
+            x = self.match(c.inputs[0])
+            if x is None:
+                return None
+            self.fused.append(f"reduce_{pat.axis}_{pat.op}[{name}]")
+            return ReduceNode(x, pat.axis, pat.op)
+        if isinstance(pat, Inverse):
+            x = self.match(c.inputs[0])
+            if x is None:
+                return None
+            self.fused.append(f"inverse[{name}]")
+            return InverseNode(x)
+        if isinstance(c, MultiSelectionComp) and isinstance(pat, Duplicate):
+            x = self.match(c.inputs[0])
+            if x is None:
+                return None
+            self.fused.append(f"duplicate_{pat.axis}[{name}]")
+            return DuplicateNode(x, pat)
         return None
 
     # ------------------------------------------------------------------ rewrite
@@ -269,18 +485,24 @@ class Fuser:
 
     def _write(self, n: Node, db: str, name: str, create: bool = False):
         v = n.eval(self.engine)
+        ctx = self.engine.ctx
+        if v.part == "cols":
+            v = _replicate(self.engine, v)
         st = self.engine.storage
         if create or not st.has_set(db, name):
             st.create_set(db, name, None, dense=True, persistent=False)
         s = st.get_set(db, name)
+        replicated = v.part is None
+        row_off = v.offset if v.part == "rows" else 0
+        total_rows = v.total if v.part == "rows" else v.rows
         if isinstance(s, DenseMatrixSet):
-            s.set_panel(v.phys, v.rows if not v.transposed else v.rows, v.cols, max(1, v.br), max(1, v.bc),
-                        transposed=v.transposed)
-            s.total_rows = v.rows
+            s.set_panel(v.phys, total_rows, v.cols, max(1, v.br), max(1, v.bc), row_offset=row_off,
+                        transposed=v.transposed, replicated=replicated or not ctx.distributed)
             s.local_rows = v.rows
         else:
             tmp = DenseMatrixSet(st, db, name, s.type, -1, s.page_size, s.device)
-            tmp.set_panel(v.phys, v.rows, v.cols, max(1, v.br), max(1, v.bc), transposed=v.transposed)
+            tmp.set_panel(v.phys, total_rows, v.cols, max(1, v.br), max(1, v.bc), row_offset=row_off,
+                          transposed=v.transposed)
             tmp.local_rows = v.rows
             s.add_batch(tmp.to_blocks())
 
@@ -291,4 +513,5 @@ def fuse_tensor_patterns(sinks: List[Computation], engine) -> Tuple[List[Computa
     return rest, f.fused
 
 
-__all__ = ["fuse_tensor_patterns", "Fuser", "MatmulNode", "SoftmaxNode", "BiasActNode", "SourceNode", "Dense"]
+__all__ = ["fuse_tensor_patterns", "Fuser", "MatmulNode", "SoftmaxNode", "BiasActNode", "SourceNode", "Dense",
+           "EwiseNode", "TransposeNode", "ReduceNode", "InverseNode", "DuplicateNode"]

@@ -1,0 +1,134 @@
+"""Multi-process (gloo, world_size 2, 127.0.0.1) tests of the distributed paths: dispatcher
+send_data, broadcast and hash-partitioned joins, shuffle aggregation, partitioned FF inference and
+the ring (K-partitioned) LA matmul.  The same code runs over RCCL on GPUs."""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, ws, port, fn_name, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(ws),
+                      LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        from netsdb_amd.parallel.comm import ClusterContext
+
+        ctx = ClusterContext(rank, ws, torch.device("cpu"), "gloo")
+        res = globals()[fn_name](ctx, out_dir)
+        torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(fn_name, ws=2):
+    out = tempfile.mkdtemp()
+    mp.spawn(_worker, args=(ws, _free_port(), fn_name, out), nprocs=ws, join=True)
+    return [torch.load(os.path.join(out, f"r{r}.pt"), weights_only=False) for r in range(ws)]
+
+
+# ------------------------------------------------------------------ scenarios (run inside ranks)
+def _engine_scenario(ctx, out_dir):
+    from netsdb_amd.client import PDBClient
+    from netsdb_amd.computations import ScanSet, WriteSet
+    from tests.test_engine import Dept, EmpDept, EmpJoinDept, SalaryByDept, _emps
+    from netsdb_amd.objects.builtin import DepartmentTotal, Employee
+
+    res = {}
+    for thr, tag in ((2 << 30, "broadcast"), (0, "partitioned")):
+        c = PDBClient(ctx=ctx, root=tempfile.mkdtemp(), page_size=1 << 12, broadcast_threshold=thr)
+        c.create_database("db")
+        c.create_set("db", "emps", Employee)
+        c.send_data("db", "emps", _emps(60) if ctx.rank == 0 else None)
+        c.create_set("db", "depts", Dept)
+        c.send_data("db", "depts", [Dept("eng", 3), Dept("ops", 1), Dept("hr", 2)] if ctx.rank == 0 else None)
+        c.create_set("db", "out", EmpDept)
+        j = EmpJoinDept()
+        j.set_input(0, ScanSet("db", "emps", Employee))
+        j.set_input(1, ScanSet("db", "depts", Dept))
+        c.execute_computations(WriteSet("db", "out").set_input(j))
+        res[f"join_{tag}"] = sorted((o.emp, o.dept, o.floor) for o in c.get_set_iterator("db", "out", gather=True))
+        res[f"local_emps_{tag}"] = c.get_set("db", "emps").num_records()
+        c.create_set("db", "totals", DepartmentTotal)
+        c.execute_computations(WriteSet("db", "totals").set_input(SalaryByDept().set_input(ScanSet("db", "emps", Employee))))
+        res[f"agg_{tag}"] = sorted((o.department, round(o.total, 6)) for o in c.get_set_iterator("db", "totals", gather=True))
+    return res
+
+
+def _ff_scenario(ctx, out_dir):
+    from netsdb_amd.client import PDBClient
+    from netsdb_amd.models import ff
+    from netsdb_amd.models.blocks import to_tensor
+
+    c = PDBClient(ctx=ctx, root=tempfile.mkdtemp())
+    ff.load_model(c, "ff", 48, 64, 32, 16, 8, 16, dtype=torch.float32, partition_inputs=True)
+    ff.inference_unit(c, "ff", "w1", "wo", "inputs", "b1", "bo", "output")
+    out = to_tensor(c, "ff", "output")
+    g = lambda n: to_tensor(c, "ff", n)  # noqa: E731
+    ref = ff.reference_inference(g("inputs"), g("w1"), g("b1"), g("wo"), g("bo"))
+    return {"err": (out.float() - ref).abs().max().item(), "local": c.get_set("ff", "inputs").local_rows}
+
+
+def _la_ring_scenario(ctx, out_dir):
+    from netsdb_amd.client import PDBClient
+    from netsdb_amd.computations import ScanSet, WriteSet
+    from netsdb_amd.la import computations as L
+    from netsdb_amd.models import blocks as B
+
+    c = PDBClient(ctx=ctx, root=tempfile.mkdtemp())
+    c.create_database("LA_db")
+    g = torch.Generator().manual_seed(5)
+    A = torch.rand(48, 40, generator=g)
+    Bm = torch.rand(40, 24, generator=g)
+    B.load_tensor(c, "LA_db", "A", A, 8, 8, dtype=torch.float32, partition_rows=True)
+    B.load_tensor(c, "LA_db", "B", Bm, 8, 8, dtype=torch.float32, partition_rows=True)
+    c.create_set("LA_db", "C", None, dense=True)
+    j = L.LAMultiply1Join()
+    j.set_input(0, ScanSet("LA_db", "A"))
+    j.set_input(1, ScanSet("LA_db", "B"))
+    st = c.execute_computations(WriteSet("LA_db", "C").set_input(L.LAMultiply2Aggregate().set_input(j)))
+    C = B.to_tensor(c, "LA_db", "C")
+    return {"err": (C.float() - A @ Bm).abs().max().item(), "fused": st.get("fused_ops")}
+
+
+@pytest.mark.timeout(300)
+def test_distributed_engine_join_aggregate():
+    r0, r1 = _run("_engine_scenario")
+    from tests.test_engine import _emps
+
+    floors = {"eng": 3, "ops": 1, "hr": 2}
+    exp = sorted((e.name, e.department, floors[e.department]) for e in _emps(60) if e.department in floors)
+    tot = {}
+    for e in _emps(60):
+        tot[e.department] = tot.get(e.department, 0.0) + e.salary
+    for tag in ("broadcast", "partitioned"):
+        assert r0[f"join_{tag}"] == exp == r1[f"join_{tag}"]
+        assert r0[f"local_emps_{tag}"] + r1[f"local_emps_{tag}"] == 60
+        assert r0[f"local_emps_{tag}"] > 0 and r1[f"local_emps_{tag}"] > 0
+        assert r0[f"agg_{tag}"] == sorted((k, round(v, 6)) for k, v in tot.items())
+
+
+@pytest.mark.timeout(300)
+def test_distributed_ff_partitioned_inputs():
+    r0, r1 = _run("_ff_scenario")
+    assert r0["local"] + r1["local"] == 48
+    assert r0["err"] < 1e-4 and r1["err"] < 1e-4
+
+
+@pytest.mark.timeout(300)
+def test_distributed_la_ring_matmul():
+    r0, r1 = _run("_la_ring_scenario")
+    assert r0["err"] < 1e-4 and r1["err"] < 1e-4
+    assert any("matmul" in f for f in r0["fused"])
