@@ -1,0 +1,168 @@
+"""Model deduplication: share identical / near-identical tensor blocks across models.
+
+Reference: src/deduplication (TensorBlockIndex — map persisted deduplicated source blocks to the
+runtime blocks of each target set; SharedFFMatrixBlockSet / SharedTensorBlockSet — sets whose pages
+are shared; PartitionTensorBlockSharedPageIterator), PDBClient::addSharedMapping / addSharedPage,
+model-inference/deduplication (LSH block matching in indexing/, page packing in page-packing/),
+drivers FFTestWithDeduplication.cc, TestWord2VecWithDeduplication.cc, TextClassifierDeduplication.cc.
+
+MI355X-native design: all models' blocks live ONCE in an HBM block pool [n_unique, br, bc]; each
+model is a block-index table (TensorBlockIndex).  Dedup detection hashes blocks on the GPU
+(exact) or compares random-projection LSH signatures + an L-inf tolerance (approximate).  A model
+is materialised for inference by one gather (index_select) into its dense panel, or page-packed:
+blocks are ordered so models that share blocks share pages (greedy packing, page_packing.py's
+bin-packing idea).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from ..execution.kernels import mix64
+
+
+@dataclass
+class TensorBlockIndex:
+    """model name -> [nbr, nbc] table of pool block ids (+ geometry)."""
+
+    block_rows: int
+    block_cols: int
+    tables: Dict[str, torch.Tensor] = field(default_factory=dict)
+    shapes: Dict[str, Tuple[int, int]] = field(default_factory=dict)
+
+    def to_json(self) -> dict:
+        return {"block_rows": self.block_rows, "block_cols": self.block_cols,
+                "tables": {k: v.cpu().tolist() for k, v in self.tables.items()},
+                "shapes": {k: list(v) for k, v in self.shapes.items()}}
+
+    @staticmethod
+    def from_json(d: dict) -> "TensorBlockIndex":
+        idx = TensorBlockIndex(d["block_rows"], d["block_cols"])
+        idx.tables = {k: torch.tensor(v, dtype=torch.int64) for k, v in d["tables"].items()}
+        idx.shapes = {k: tuple(v) for k, v in d["shapes"].items()}
+        return idx
+
+
+def to_blocks(m: torch.Tensor, br: int, bc: int) -> torch.Tensor:
+    R, C = m.shape
+    nbr, nbc = math.ceil(R / br), math.ceil(C / bc)
+    m = torch.nn.functional.pad(m, (0, nbc * bc - C, 0, nbr * br - R))
+    return m.reshape(nbr, br, nbc, bc).permute(0, 2, 1, 3).reshape(nbr * nbc, br, bc)
+
+
+def from_blocks(blocks: torch.Tensor, nbr: int, nbc: int, R: int, C: int) -> torch.Tensor:
+    br, bc = blocks.shape[1], blocks.shape[2]
+    return blocks.reshape(nbr, nbc, br, bc).permute(0, 2, 1, 3).reshape(nbr * br, nbc * bc)[:R, :C]
+
+
+def block_hashes(blocks: torch.Tensor) -> torch.Tensor:
+    """Exact content hash per block (on device): mix64 over the raw 16-bit/32-bit words."""
+    flat = blocks.reshape(blocks.shape[0], -1)
+    if flat.dtype in (torch.bfloat16, torch.float16):
+        words = flat.view(torch.int16).to(torch.int64) & 0xFFFF
+    else:
+        words = flat.float().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    pos = torch.arange(words.shape[1], device=words.device, dtype=torch.int64)
+    h = mix64(words * 0x100000001B3 + pos)
+    return mix64(h.sum(1))   # order-aware (pos mixed in), commutative sum is fine after mixing
+
+
+def lsh_signatures(blocks: torch.Tensor, bits: int = 64, seed: int = 0) -> torch.Tensor:
+    """Random-hyperplane LSH signature per block (similar blocks -> equal signatures)."""
+    flat = blocks.reshape(blocks.shape[0], -1).float()
+    g = torch.Generator(device=flat.device).manual_seed(seed)
+    planes = torch.randn(flat.shape[1], bits, generator=g, device=flat.device)
+    s = (flat @ planes) > 0
+    w = (1 << torch.arange(bits - 1, device=flat.device, dtype=torch.int64))
+    return (s[:, : bits - 1].long() * w).sum(1)
+
+
+class BlockPool:
+    """Deduplicated block storage shared by many models (SharedFFMatrixBlockSet analogue)."""
+
+    def __init__(self, block_rows: int, block_cols: int, device="cpu", dtype=torch.bfloat16, tolerance: float = 0.0):
+        self.br, self.bc = block_rows, block_cols
+        self.device, self.dtype = device, dtype
+        self.tolerance = tolerance
+        self.blocks = torch.empty(0, block_rows, block_cols, dtype=dtype, device=device)
+        self.keys = torch.empty(0, dtype=torch.int64, device=device)
+        self.index = TensorBlockIndex(block_rows, block_cols)
+        self.stats = {"blocks_in": 0, "blocks_stored": 0}
+
+    def add_model(self, name: str, m: torch.Tensor) -> torch.Tensor:
+        m = m.to(self.device, self.dtype)
+        R, C = m.shape
+        nbr, nbc = math.ceil(R / self.br), math.ceil(C / self.bc)
+        blks = to_blocks(m, self.br, self.bc)
+        keys = block_hashes(blks) if self.tolerance == 0 else lsh_signatures(blks)
+        ids = torch.empty(blks.shape[0], dtype=torch.int64, device=self.device)
+        # match against the pool (sorted-key binary search), verify content within tolerance
+        if self.keys.numel():
+            order = torch.argsort(self.keys)
+            sk = self.keys[order]
+            pos = torch.searchsorted(sk, keys).clamp(max=sk.numel() - 1)
+            cand = order[pos]
+            hit = sk[pos] == keys
+            if hit.any():
+                diff = (self.blocks[cand].float() - blks.float()).abs().amax(dim=(1, 2))
+                hit &= diff <= self.tolerance
+        else:
+            cand = torch.zeros_like(ids)
+            hit = torch.zeros(blks.shape[0], dtype=torch.bool, device=self.device)
+        ids[hit] = cand[hit]
+        new = (~hit).nonzero().flatten()
+        if new.numel():
+            # dedup within the model itself
+            nk = keys[new]
+            uk, inv = torch.unique(nk, return_inverse=True)
+            first = torch.full((uk.numel(),), new.numel(), dtype=torch.int64, device=self.device)
+            first.scatter_reduce_(0, inv, torch.arange(new.numel(), device=self.device), reduce="amin")
+            base = self.blocks.shape[0]
+            self.blocks = torch.cat([self.blocks, blks[new[first]]])
+            self.keys = torch.cat([self.keys, uk if self.tolerance == 0 else nk[first]])
+            ids[new] = base + inv
+        self.index.tables[name] = ids.reshape(nbr, nbc)
+        self.index.shapes[name] = (R, C)
+        self.stats["blocks_in"] += blks.shape[0]
+        self.stats["blocks_stored"] = self.blocks.shape[0]
+        return ids
+
+    def materialize(self, name: str) -> torch.Tensor:
+        t = self.index.tables[name]
+        R, C = self.index.shapes[name]
+        blks = self.blocks.index_select(0, t.flatten().to(self.blocks.device))
+        return from_blocks(blks, t.shape[0], t.shape[1], R, C)
+
+    def dedup_ratio(self) -> float:
+        return self.stats["blocks_stored"] / max(1, self.stats["blocks_in"])
+
+    def pack_pages(self, blocks_per_page: int) -> List[List[int]]:
+        """Greedy page packing: blocks shared by the same set of models go to the same pages, so a
+        model touches as few pages as possible (model-inference/deduplication/page-packing)."""
+        owners: Dict[int, set] = {}
+        for name, t in self.index.tables.items():
+            for b in t.flatten().tolist():
+                owners.setdefault(b, set()).add(name)
+        groups: Dict[frozenset, List[int]] = {}
+        for b, o in owners.items():
+            groups.setdefault(frozenset(o), []).append(b)
+        pages: List[List[int]] = []
+        for key in sorted(groups, key=lambda k: (-len(k), sorted(k))):
+            blks = sorted(groups[key])
+            for s in range(0, len(blks), blocks_per_page):
+                pages.append(blks[s:s + blocks_per_page])
+        return pages
+
+
+def pages_touched(pool: BlockPool, pages: List[List[int]], name: str) -> int:
+    page_of = {b: i for i, p in enumerate(pages) for b in p}
+    return len({page_of[b] for b in pool.index.tables[name].flatten().tolist()})
+
+
+__all__ = ["TensorBlockIndex", "BlockPool", "block_hashes", "lsh_signatures", "to_blocks", "from_blocks",
+           "pages_touched"]
+
+_ = Optional

@@ -1,0 +1,131 @@
+"""LSTM, logistic regression, FF_proj, word2vec (3 plans), semantic classifier and deduplication
+against fp32/fp64 torch references (reference tests: LSTMTest.cc, LogisticRegressionTest.cc,
+FCProjTest.cc, Word2Vec.cc, TestSemanticClassifier.cc, TestDeduplication.cc)."""
+import pytest
+import torch
+
+from netsdb_amd.client import PDBClient
+from netsdb_amd.models import blocks as B
+from netsdb_amd.models import dedup, logreg, lstm, word2vec
+
+DEVS = ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)]
+
+
+@pytest.mark.parametrize("dev", DEVS)
+def test_lstm(dev):
+    torch.manual_seed(0)
+    xs = torch.randn(5, 7, 24, device=dev)
+    r = lstm.lstm_inference(xs, 32)
+    h_ref, c_ref = r["model"].reference(xs)
+    torch.testing.assert_close(r["h"].double().cpu(), h_ref, atol=3e-2, rtol=3e-2)
+    torch.testing.assert_close(r["c"].double().cpu(), c_ref, atol=3e-2, rtol=3e-2)
+
+
+def test_lstm_udfs_generic(tmp_path):
+    from netsdb_amd.computations import ScanSet, WriteSet
+    from netsdb_amd.models.ff import mk_blocks
+    from netsdb_amd.objects.builtin import FFMatrixBlock
+
+    c = PDBClient(root=str(tmp_path))
+    c.create_database("l")
+    mats = [torch.randn(2, 4, 4) for _ in range(3)]
+    for i, m in enumerate(mats):
+        c.create_set("l", f"m{i}", FFMatrixBlock)
+        c.add_local_data("l", f"m{i}", mk_blocks(torch.tensor([0, 1]), torch.tensor([0, 0]), m, 8, 4))
+    j = lstm.LSTMThreeWaySum("tanh")
+    for i in range(3):
+        j.set_input(i, ScanSet("l", f"m{i}", FFMatrixBlock))
+    c.create_set("l", "out", FFMatrixBlock)
+    c.execute_computations(WriteSet("l", "out").set_input(j))
+    got = sorted(c.get_set_iterator("l", "out"), key=lambda o: o.block_row)
+    exp = torch.tanh(mats[0] + mats[1] + mats[2])
+    for k in range(2):
+        torch.testing.assert_close(got[k].data.float(), exp[k], atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("dev", DEVS)
+def test_logreg(tmp_path, dev):
+    c = PDBClient(root=str(tmp_path), device=dev)
+    logreg.load_logreg(c, "lr", 50, 24, 10, 8, dtype=torch.float32)
+    logreg.inference_unit_log_reg(c, "lr")
+    out = B.to_tensor(c, "lr", "output").float().cpu()
+    X, w, b = (B.to_tensor(c, "lr", n).float().cpu() for n in ("inputs", "w", "b"))
+    ref = torch.sigmoid(X @ w + b)
+    torch.testing.assert_close(out.reshape(-1), ref.reshape(-1), atol=1e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("dev", DEVS)
+def test_fc_network_projection(tmp_path, dev):
+    from netsdb_amd.computations import ScanSet, WriteSet
+    from netsdb_amd.objects.record import RecordBatch
+
+    torch.manual_seed(1)
+    Ws = [torch.randn(32, 40, device=dev) * 0.2, torch.randn(10, 32, device=dev) * 0.2]
+    bs = [torch.randn(32, device=dev) * 0.1, torch.randn(10, device=dev) * 0.1]
+    fcn = logreg.FullyConnectedNetwork(Ws, bs)
+    c = PDBClient(root=str(tmp_path), device=dev)
+    c.create_database("fc")
+    c.create_set("fc", "rows", None)
+    x = torch.randn(30, 40, device=dev)
+    c.add_local_data("fc", "rows", RecordBatch({"data": x}, 30))
+    c.create_set("fc", "out", None)
+    c.execute_computations(WriteSet("fc", "out").set_input(fcn.set_input(ScanSet("fc", "rows"))))
+    y = RecordBatch.concat(c.get_set_batches("fc", "out")).columns["data"].float().cpu()
+    ref = torch.softmax(torch.relu(x.cpu() @ Ws[0].cpu().t() + bs[0].cpu()) @ Ws[1].cpu().t() + bs[1].cpu(), -1)
+    torch.testing.assert_close(y, ref, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("dev", DEVS)
+def test_word2vec_three_plans(tmp_path, dev):
+    c = PDBClient(root=str(tmp_path), device=dev)
+    V, D = 200, 48
+    word2vec.load_embeddings(c, "w2v", "emb", V, D, 32, 16, dtype=torch.float32)
+    E = B.to_tensor(c, "w2v", "emb").float().cpu()
+    ids = torch.tensor([3, 77, 150, 3, 199])
+    word2vec.word2vec_matmul(c, "w2v", "emb", ids, V, 8, 32)
+    got = B.to_tensor(c, "w2v", "w2v_out").float().cpu()
+    torch.testing.assert_close(got, E[ids], atol=1e-2, rtol=1e-2)
+    look = word2vec.word2vec_lookup(c, "w2v", "emb", ids).cpu()
+    torch.testing.assert_close(look, E[ids], atol=1e-6, rtol=1e-6)
+    word2vec.word2vec_sparse(c, "w2v", "emb", ids.tolist())
+    segs = word2vec.assemble_segments(c, "w2v", "w2v_segments", D)
+    for i in set(ids.tolist()):
+        torch.testing.assert_close(segs[i], E[i], atol=1e-6, rtol=1e-6)
+
+
+@pytest.mark.parametrize("dev", DEVS)
+def test_semantic_classifier(dev):
+    torch.manual_seed(2)
+    E = torch.randn(500, 64, device=dev)
+    clf = word2vec.SemanticClassifier(E, 32, 5)
+    idx = torch.randint(0, 500, (40,), device=dev)
+    offs = torch.tensor([0, 10, 10, 25, 40], device=dev)
+    y = clf.forward(idx, offs).cpu()
+    torch.testing.assert_close(y, clf.reference(idx, offs), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("dev", DEVS)
+def test_dedup_exact_and_lsh(dev):
+    torch.manual_seed(3)
+    base = torch.randn(64, 96, device=dev)
+    m2 = base.clone()
+    m2[:16, :32] += 1.0                     # one block differs
+    m3 = torch.cat([base[:32], torch.randn(32, 96, device=dev)])
+    pool = dedup.BlockPool(16, 32, device=dev, dtype=torch.float32)
+    for n, m in (("a", base), ("b", m2), ("c", m3)):
+        pool.add_model(n, m)
+    assert pool.stats["blocks_in"] == 36
+    # a: 12 new; b: 1 new; c: 6 shared + 6 new
+    assert pool.stats["blocks_stored"] == 12 + 1 + 6
+    for n, m in (("a", base), ("b", m2), ("c", m3)):
+        torch.testing.assert_close(pool.materialize(n), m)
+    pages = pool.pack_pages(4)
+    assert sum(len(p) for p in pages) == pool.stats["blocks_stored"]
+    assert dedup.pages_touched(pool, pages, "a") <= 5
+    # approximate (LSH + tolerance): tiny perturbations dedup
+    pool2 = dedup.BlockPool(16, 32, device=dev, dtype=torch.float32, tolerance=1e-3)
+    pool2.add_model("x", base)
+    pool2.add_model("y", base + 1e-5)
+    assert pool2.stats["blocks_stored"] < 24
+    idx = dedup.TensorBlockIndex.from_json(pool.index.to_json())
+    assert torch.equal(idx.tables["b"], pool.index.tables["b"].cpu())
