@@ -31,7 +31,7 @@ class PDBClient:
     def __init__(self, ctx: Optional[ClusterContext] = None, root: Optional[str] = None, device=None,
                  page_size: int = DEFAULT_PAGE_SIZE, pool_pages: int = 16, catalog_path: Optional[str] = None,
                  trace: bool = False, broadcast_threshold: int = 2 << 30, fusion: bool = True,
-                 device_budget: Optional[int] = None):
+                 device_budget: Optional[int] = None, resume: bool = False):
         self.ctx = ctx or ClusterContext(device=torch.device(device) if device is not None else torch.device("cpu"))
         dev = device if device is not None else self.ctx.device
         self.device = torch.device(dev)
@@ -44,6 +44,28 @@ class PDBClient:
         self.catalog.register_node(self.ctx.rank, os.environ.get("MASTER_ADDR", "127.0.0.1"), str(self.device),
                                    torch.cuda.get_device_properties(self.device).total_memory
                                    if self.device.type == "cuda" else 0)
+        self.learning = None
+        if resume:
+            self._resume()
+
+    # ------------------------------------------------------------------ checkpoint / resume
+    def _resume(self):
+        """Re-open every set recorded in the catalog from its page files (after flush_data)."""
+        import itertools
+
+        max_id = 0
+        for meta in self.catalog.sets():
+            max_id = max(max_id, meta["set_id"])
+            t = self.catalog.resolve_type(meta["type"]) if meta["type"] else None
+            dense = meta["layout"] == "dense"
+            s = self.storage.create_set(meta["db"], meta["name"], t, meta["page_size"], dense=dense,
+                                        set_id=meta["set_id"])
+            m = meta.get("meta") or {}
+            if dense and m.get("dense"):
+                s.restore(m["dense"])
+            elif m.get("pages"):
+                s.restore(m["pages"])
+        self.storage._ids = itertools.count(max_id + 1)
 
     # ------------------------------------------------------------------ catalog
     def register_type(self, cls: type) -> bool:
@@ -163,7 +185,20 @@ class PDBClient:
     getSetIterator = get_set_iterator
 
     def flush_data(self) -> bool:
+        """Persist every set (pages -> native page pool -> page files) and record the layout in the
+        catalog so a new PDBClient(root=..., resume=True) can reopen them (checkpoint)."""
+        from .storage.sets import DenseMatrixSet
+
         self.storage.flush()
+        for (db, name), s in self.storage.sets.items():
+            if not s.persistent or self.catalog.get_set(db, name) is None:
+                continue
+            meta = dict(self.catalog.get_set(db, name)["meta"])
+            if isinstance(s, DenseMatrixSet):
+                meta["dense"] = s.geometry()
+            else:
+                meta["pages"] = s.page_meta()
+            self.catalog.update_set_meta(db, name, meta)
         return True
 
     flushData = flush_data

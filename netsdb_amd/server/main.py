@@ -1,0 +1,51 @@
+"""Start a netsdb_amd cluster: ``python -m netsdb_amd.server.main --port 8108`` (one process) or
+``torchrun --nproc-per-node N --master-addr 127.0.0.1 -m netsdb_amd.server.main --port 8108``
+(one process per GPU; rank 0 serves clients, all ranks execute).  Mirrors the reference's
+startPseudoCluster.py / startMaster.sh + startWorkers.sh."""
+from __future__ import annotations
+
+import argparse
+import os
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--port", type=int, default=8108)
+    ap.add_argument("--root", default=None, help="data directory (catalog + page files)")
+    ap.add_argument("--page-size-mb", type=int, default=64)
+    ap.add_argument("--resume", action="store_true", help="reopen the sets persisted in --root")
+    ap.add_argument("--heartbeat-port", type=int, default=0)
+    ap.add_argument("--jobs", action="append", default=[],
+                    help="operator-chosen module exposing a JOBS dict {name: fn(client, **kw)} to clients")
+    a = ap.parse_args(argv)
+
+    from ..client import PDBClient
+    from ..parallel.comm import ClusterContext
+    from ..utils.health import HeartbeatMonitor
+    from .frontend import PDBFrontend, serve_worker
+
+    import importlib
+
+    jobs = {}
+    for mod in a.jobs:
+        jobs.update(getattr(importlib.import_module(mod), "JOBS"))
+    ctx = ClusterContext.from_env()
+    root = a.root or os.path.join(os.getcwd(), "netsdb_data")
+    client = PDBClient(ctx=ctx, root=os.path.join(root, f"rank{ctx.rank}"), page_size=a.page_size_mb << 20,
+                       resume=a.resume)
+    health = None
+    if a.heartbeat_port:
+        health = HeartbeatMonitor.standalone(a.host, a.heartbeat_port, ctx.rank, ctx.world_size).start()
+    if ctx.rank == 0:
+        fe = PDBFrontend(client, a.host, a.port, health, jobs=jobs)
+        print(f"[netsdb_amd] master listening on {a.host}:{fe.start().port} (world {ctx.world_size})", flush=True)
+        fe.stopped.wait()
+    else:
+        serve_worker(client, jobs, health)
+    if health:
+        health.stop()
+
+
+if __name__ == "__main__":
+    main()

@@ -161,6 +161,20 @@ class UserSet:
             p.persist()
         self.manager.buffer_manager.flush_set(self.set_id)
 
+    def page_meta(self) -> list:
+        return [[p.page_no, p.n, p.nbytes] for p in self.pages]
+
+    def restore(self, pages: list):
+        """Re-attach persisted pages lazily (they load from the page file on first scan)."""
+        for page_no, n, nbytes in pages:
+            p = Page.__new__(Page)
+            p.set, p.page_no, p.batch, p.nbytes, p.n = self, page_no, None, nbytes, n
+            p.pins, p.location, p.dirty, p.last_use = 0, "pool", False, 0
+            self.pages.append(p)
+            self.stats["records"] += n
+            self.stats["bytes"] += nbytes
+        return self
+
     def __repr__(self):
         return f"UserSet({self.db}.{self.name}, pages={len(self.pages)}, records={self.num_records()})"
 
@@ -282,6 +296,7 @@ class DenseMatrixSet(UserSet):
         self.stats = {"records": 0, "bytes": 0}
 
     def flush(self):
+        """Persist the panel (as its MatrixBlock records) through the page pool into the set's page file."""
         if self.panel is None:
             return
         b = self.to_blocks("cpu")
@@ -296,6 +311,32 @@ class DenseMatrixSet(UserSet):
             bm.unpin(self.set_id, page, True, len(chunk))
             page += 1
         bm.flush_set(self.set_id)
+        self.flushed_chunks = page
+
+    def geometry(self) -> dict:
+        return {"total_rows": self.total_rows, "total_cols": self.total_cols, "block_rows": self.block_rows,
+                "block_cols": self.block_cols, "row_offset": self.row_offset, "local_rows": self.local_rows,
+                "replicated": self.replicated, "dtype": str(self.panel.dtype).replace("torch.", "")
+                if self.panel is not None else "bfloat16", "chunks": getattr(self, "flushed_chunks", 0)}
+
+    def restore(self, geo: dict):
+        """Rebuild the panel from the chunks written by :meth:`flush` (checkpoint/resume)."""
+        bm = self.manager.buffer_manager
+        data = bytearray()
+        for page in range(int(geo.get("chunks", 0))):
+            slot = bm.pin(self.set_id, page, False)
+            n = bm.bytes_used(self.set_id, page)
+            data += bytes(bm.slot_view(slot)[:n])
+            bm.unpin(self.set_id, page, False, 0)
+        if not data:
+            return self
+        b = deserialize_batch(bytes(data))
+        self.define(geo["total_rows"], geo["total_cols"], geo["block_rows"], geo["block_cols"],
+                    row_offset=geo["row_offset"], local_rows=geo["local_rows"], dtype=getattr(torch, geo["dtype"]))
+        self.replicated = geo.get("replicated", True)
+        self.add_batch(b)
+        self.flushed_chunks = int(geo.get("chunks", 0))
+        return self
 
 
 __all__ = ["Page", "UserSet", "DenseMatrixSet"]

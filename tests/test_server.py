@@ -1,0 +1,70 @@
+"""Socket front end + remote client + heartbeat failure detection (reference: master/worker
+servers driven by PDBClient over sockets)."""
+import socket
+import time
+
+from netsdb_amd.client import PDBClient
+from netsdb_amd.objects.builtin import Employee
+from netsdb_amd.server import PDBFrontend, RemotePDBClient
+from netsdb_amd.utils.health import HeartbeatMonitor, NodeFailure
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_remote_client_roundtrip(tmp_path):
+    from netsdb_amd.examples import employee_jobs
+
+    fe = PDBFrontend(PDBClient(root=str(tmp_path)), port=0, jobs=employee_jobs.JOBS).start()
+    rc = RemotePDBClient("127.0.0.1", fe.port)
+    assert rc.ping()["world_size"] == 1
+    assert rc.create_database("db")
+    rc.create_set("db", "emps", "Employee")
+    emps = [Employee(f"e{i}", 20 + i, "eng" if i % 2 else "ops", 100.0 * i) for i in range(30)]
+    assert rc.send_data("db", "emps", emps) == 30
+    assert "select_older" in rc.ping()["jobs"]
+    rc.run("select_older", db="db", src="emps", dst="old", age=40)
+    old = rc.get_set("db", "old")
+    assert sorted(o.name for o in old) == sorted(e.name for e in emps if e.age > 40)
+    rc.run("totals", db="db", src="emps", dst="tot")
+    tot = {o.department: o.total for o in rc.get_set("db", "tot")}
+    assert abs(tot["eng"] - sum(e.salary for e in emps if e.department == "eng")) < 1e-6
+    assert "SCAN" in rc.explain("plan", db="db", src="emps", age=3)
+    assert any(s["name"] == "emps" for s in rc.list_sets("db"))
+    assert "Employee" in rc.print_catalog()
+    try:
+        rc._call(op="bogus")
+        raise AssertionError("expected error")
+    except RuntimeError as e:
+        assert "unknown request" in str(e)
+    try:
+        rc.run("os.system", cmd="true")
+        raise AssertionError("unregistered job must be refused")
+    except RuntimeError as e:
+        assert "not registered" in str(e)
+    rc.shutdown()
+    fe.stopped.wait(5)
+
+
+def test_heartbeat_failure_detection():
+    port = _port()
+    m0 = HeartbeatMonitor.standalone("127.0.0.1", port, 0, 2, interval=0.05, timeout=0.3)
+    m1 = HeartbeatMonitor.standalone("127.0.0.1", port, 1, 2, interval=0.05, timeout=0.3)
+    m0.start()
+    m1.start()
+    time.sleep(0.2)
+    assert all(s["state"] == "alive" for s in m0.status().values())
+    m1.stop()                        # rank 1 "dies"
+    time.sleep(0.8)
+    assert 1 in m0.dead_ranks()
+    try:
+        m0.check()
+        raise AssertionError("expected NodeFailure")
+    except NodeFailure:
+        pass
+    m0.stop()
