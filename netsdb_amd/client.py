@@ -90,6 +90,9 @@ class PDBClient:
                    policy=None, device="default") -> bool:
         if not self.catalog.has_database(db):
             self.catalog.create_database(db)
+        if policy == "auto":
+            # Lachesis: ask the self-learning advisor for the partition key of this set
+            policy = self.learning.advise(db, name) if self.learning is not None else None
         if type_ is not None:
             self.catalog.register_type(type_)
         sid = self.catalog.create_set(db, name, type_.type_name() if type_ else None, page_size or self.storage.page_size,
@@ -232,6 +235,12 @@ class PDBClient:
         return True
 
     addSharedMapping = add_shared_mapping
+
+    def enable_self_learning(self, path: str = ":memory:", learned: bool = False):
+        """Record job history and let create_set(..., policy='auto') pick partition keys."""
+        from .selflearning import SelfLearningHook
+
+        return SelfLearningHook(self, path, learned)
 
     def barrier(self):
         self.ctx.barrier()

@@ -87,6 +87,7 @@ class QueryEngine:
         self.fusion = fusion
         self.last_plan = None
         self.last_tcap = None
+        self._last_comps = None
 
     # ------------------------------------------------------------------ entry
     def execute(self, sinks: List[Computation], job_name: str = "job") -> JobStats:
@@ -100,9 +101,11 @@ class QueryEngine:
             stats["fused_ops"] = fused
             if not sinks:
                 stats["seconds"] = time.perf_counter() - t0
+                self.last_plan = self.last_tcap = self._last_comps = None
                 return stats
         plan = compile_tcap(sinks)
         self.last_tcap = plan.tcap
+        self._last_comps = plan.computations
         with self.tracer.span("parse_tcap", job=job_name):
             atoms = _ext.native().parse_tcap(plan.tcap)
         planner = Planner(self._scan_size, self.ctx.world_size, self.broadcast_threshold)

@@ -1,1 +1,252 @@
+"""Self-learning data placement (Lachesis) — reference: src/selfLearning (SelfLearningDB,
+SelfLearningServer, RuleBasedDataPlacementOptimizerForLoadJob, DRLBasedDataPlacementOptimizerForLoadJob,
+JobStageSelfLearningInfo, LambdaContext; docs/selfLearning-database-schema-full.pdf).
 
+Every executed job is recorded into a sqlite history: for each scanned set, which stages consumed
+it, what they ended in (hash-partitioned join build/probe, aggregation shuffle, partition, user set)
+and the key lambda they hashed it by (attribute/method name — native lambdas cannot be used to
+place data and are skipped, as in the reference).  When a set is (re)loaded, the advisor picks the
+partition key:
+
+* :class:`RuleBasedAdvisor` — the reference rule: the key of the most frequent shuffle/repartition
+  consumer of that set (following one level of indirection through sets derived from it);
+* :class:`LearnedAdvisor`  — epsilon-greedy bandit over the candidate keys, rewarded by the observed
+  job time of consumers when the set was placed with that key (a lightweight stand-in for the
+  reference's DRL agent; the state/reward plumbing is the same).
+
+The chosen key becomes a dispatcher :class:`LambdaPolicy`, so co-partitioned joins run without a
+shuffle (the planner sees both sides partitioned by the join key).
+"""
+from __future__ import annotations
+
+import json
+import random
+import sqlite3
+import threading
+import time
+from typing import Dict, List, Optional, Tuple
+
+from ..lambdas import AttAccess, MethodCall
+from ..parallel.dispatcher import LambdaPolicy
+
+_SCHEMA = """
+CREATE TABLE IF NOT EXISTS jobs (id INTEGER PRIMARY KEY AUTOINCREMENT, name TEXT, started REAL, seconds REAL);
+CREATE TABLE IF NOT EXISTS stage_use (job_id INTEGER, db TEXT, set_name TEXT, sink TEXT, comp TEXT,
+                                      key_kind TEXT, key_name TEXT, input_index INTEGER, seconds REAL);
+CREATE TABLE IF NOT EXISTS lineage (job_id INTEGER, src_db TEXT, src_set TEXT, dst_db TEXT, dst_set TEXT);
+CREATE TABLE IF NOT EXISTS placements (db TEXT, set_name TEXT, key_kind TEXT, key_name TEXT, t REAL);
+CREATE TABLE IF NOT EXISTS rewards (db TEXT, set_name TEXT, key_name TEXT, seconds REAL);
+"""
+
+
+def _producer_map(atoms) -> Dict[str, dict]:
+    return {a["output"]["name"]: a for a in atoms}
+
+
+def _source_scan(atoms_by_out, ts: str) -> Optional[dict]:
+    """Follow producers back from tuple set ``ts`` to the SCAN feeding it (single-input chains)."""
+    seen = set()
+    while ts and ts not in seen:
+        seen.add(ts)
+        a = atoms_by_out.get(ts)
+        if a is None:
+            return None
+        if a["type"] == "SCAN":
+            return a
+        if a["type"] == "JOIN":
+            return None
+        ts = a["input"]["name"]
+    return None
+
+
+def _key_of(comp, atoms_by_out, key_col_ts: str, key_att: str):
+    """The lambda node that produced column ``key_att`` (APPLY atom) -> (kind, name) or None."""
+    ts = key_col_ts
+    seen = set()
+    while ts and ts not in seen:
+        seen.add(ts)
+        a = atoms_by_out.get(ts)
+        if a is None:
+            return None
+        if a["type"] == "APPLY" and a["output"]["atts"] and a["output"]["atts"][-1] == key_att:
+            node = comp.extract_lambdas().get(a["lambda"])
+            if isinstance(node, AttAccess):
+                return ("att", node.field)
+            if isinstance(node, MethodCall):
+                return ("method", node.method)
+            return ("native", a["lambda"])
+        ts = a["input"]["name"]
+    return None
+
+
+def extract_uses(atoms, comps, plan) -> List[dict]:
+    """Partition-relevant uses of every scanned set in one job."""
+    by_out = _producer_map(atoms)
+    uses = []
+    strat = plan.join_strategy if plan is not None else {}
+    for a in atoms:
+        if a["type"] in ("HASHLEFT", "HASHRIGHT"):
+            scan = _source_scan(by_out, a["input"]["name"])
+            if scan is None:
+                continue
+            comp = comps.get(a["comp"])
+            key = _key_of(comp, by_out, a["input"]["name"], a["input"]["atts"][0]) if comp else None
+            join_out = next((j["output"]["name"] for j in atoms if j["type"] == "JOIN" and
+                             a["output"]["name"] in (j["input"]["name"], j["input2"]["name"])), None)
+            # a broadcast join never moves this set; partitioned (or single-node 'local', which would be
+            # partitioned at scale) joins hash it by this key -> a placement candidate
+            sink = "Broadcast" if strat.get(join_out, {}).get("strategy") == "broadcast" else "Shuffle"
+            uses.append({"db": scan["db"], "set": scan["set"], "sink": sink, "comp": a["comp"],
+                         "key": key, "index": 0 if a["type"] == "HASHLEFT" else 1})
+        elif a["type"] in ("AGGREGATE", "PARTITION"):
+            scan = _source_scan(by_out, a["input"]["name"])
+            if scan is None:
+                continue
+            comp = comps.get(a["comp"])
+            key = _key_of(comp, by_out, a["input"]["name"], a["input"]["atts"][0]) if comp else None
+            uses.append({"db": scan["db"], "set": scan["set"], "sink": "Repartition" if a["type"] == "PARTITION"
+                         else "Shuffle", "comp": a["comp"], "key": key, "index": 0})
+        elif a["type"] == "OUTPUT":
+            scan = _source_scan(by_out, a["input"]["name"])
+            if scan is not None:
+                uses.append({"db": scan["db"], "set": scan["set"], "sink": "UserSet", "comp": a["comp"], "key": None,
+                             "index": 0, "dst": (a["db"], a["set"])})
+    return uses
+
+
+class SelfLearningDB:
+    def __init__(self, path: str = ":memory:"):
+        self.conn = sqlite3.connect(path, check_same_thread=False)
+        self.conn.executescript(_SCHEMA)
+        self.lock = threading.Lock()
+
+    def record_job(self, name: str, seconds: float, uses: List[dict]) -> int:
+        with self.lock, self.conn:
+            cur = self.conn.execute("INSERT INTO jobs(name, started, seconds) VALUES (?,?,?)", (name, time.time(), seconds))
+            jid = cur.lastrowid
+            for u in uses:
+                k = u.get("key") or (None, None)
+                self.conn.execute("INSERT INTO stage_use VALUES (?,?,?,?,?,?,?,?,?)",
+                                  (jid, u["db"], u["set"], u["sink"], u["comp"], k[0], k[1], u["index"], seconds))
+                if u.get("dst"):
+                    self.conn.execute("INSERT INTO lineage VALUES (?,?,?,?,?)", (jid, u["db"], u["set"], *u["dst"]))
+            # reward the current placement of every set this job read
+            for u in uses:
+                p = self.current_placement(u["db"], u["set"])
+                if p is not None:
+                    self.conn.execute("INSERT INTO rewards VALUES (?,?,?,?)", (u["db"], u["set"], p[1], seconds))
+            return jid
+
+    def record_placement(self, db: str, set_name: str, key: Tuple[str, str]):
+        with self.lock, self.conn:
+            self.conn.execute("INSERT INTO placements VALUES (?,?,?,?,?)", (db, set_name, key[0], key[1], time.time()))
+
+    def current_placement(self, db, set_name) -> Optional[Tuple[str, str]]:
+        r = self.conn.execute("SELECT key_kind, key_name FROM placements WHERE db=? AND set_name=? ORDER BY t DESC LIMIT 1",
+                              (db, set_name)).fetchone()
+        return tuple(r) if r else None
+
+    def candidates(self, db: str, set_name: str, sinks=("Shuffle", "Repartition")) -> List[Tuple[str, str, int]]:
+        q = ("SELECT key_kind, key_name, COUNT(*) FROM stage_use WHERE db=? AND set_name=? AND key_kind IN ('att','method') "
+             f"AND sink IN ({','.join('?' * len(sinks))}) GROUP BY key_kind, key_name ORDER BY COUNT(*) DESC, SUM(seconds) DESC")
+        return [tuple(r) for r in self.conn.execute(q, (db, set_name, *sinks))]
+
+    def derived_sets(self, db: str, set_name: str) -> List[Tuple[str, str]]:
+        return [tuple(r) for r in self.conn.execute(
+            "SELECT DISTINCT dst_db, dst_set FROM lineage WHERE src_db=? AND src_set=?", (db, set_name))]
+
+    def mean_reward(self, db, set_name, key_name) -> Optional[float]:
+        r = self.conn.execute("SELECT AVG(seconds), COUNT(*) FROM rewards WHERE db=? AND set_name=? AND key_name=?",
+                              (db, set_name, key_name)).fetchone()
+        return None if not r or not r[1] else float(r[0])
+
+    def export(self) -> dict:
+        return {t: [list(r) for r in self.conn.execute(f"SELECT * FROM {t}")]
+                for t in ("jobs", "stage_use", "lineage", "placements", "rewards")}
+
+
+def key_policy(kind: str, name: str, type_=None) -> LambdaPolicy:
+    """Dispatcher policy hashing records by an attribute or (vectorised) method."""
+    if kind == "att":
+        fn = lambda b: b.columns[name]  # noqa: E731
+    else:
+        def fn(b):
+            m = getattr(b.type, name)
+            vec = getattr(m, "__vectorized__", None)
+            return vec(b) if vec is not None else [m(v) for v in __import__(
+                "netsdb_amd.lambdas", fromlist=["SelfRef"]).SelfRef(b).views()]
+    return LambdaPolicy(fn, description=f"{kind}:{name}")
+
+
+class RuleBasedAdvisor:
+    def __init__(self, db: SelfLearningDB):
+        self.db = db
+
+    def best_key(self, dbname: str, set_name: str) -> Optional[Tuple[str, str]]:
+        c = self.db.candidates(dbname, set_name)
+        if c:
+            return (c[0][0], c[0][1])
+        for d, s in self.db.derived_sets(dbname, set_name):        # one level of indirection
+            c = self.db.candidates(d, s)
+            if c:
+                return (c[0][0], c[0][1])
+        return None
+
+    def policy(self, dbname: str, set_name: str) -> Optional[LambdaPolicy]:
+        k = self.best_key(dbname, set_name)
+        return key_policy(*k) if k else None
+
+
+class LearnedAdvisor(RuleBasedAdvisor):
+    """Epsilon-greedy bandit over the candidate keys (reward = -mean consumer job time)."""
+
+    def __init__(self, db: SelfLearningDB, epsilon: float = 0.1, seed: int = 0):
+        super().__init__(db)
+        self.epsilon = epsilon
+        self.rng = random.Random(seed)
+
+    def best_key(self, dbname, set_name):
+        cands = [(k, n) for k, n, _ in self.db.candidates(dbname, set_name)]
+        if not cands:
+            return super().best_key(dbname, set_name)
+        untried = [c for c in cands if self.db.mean_reward(dbname, set_name, c[1]) is None]
+        if untried:
+            return untried[0]
+        if self.rng.random() < self.epsilon:
+            return self.rng.choice(cands)
+        return min(cands, key=lambda c: self.db.mean_reward(dbname, set_name, c[1]))
+
+
+class SelfLearningHook:
+    """Attach to a PDBClient: records every job; ``advise(db, set)`` returns a partition policy."""
+
+    def __init__(self, client, path: str = ":memory:", learned: bool = False):
+        self.client = client
+        self.db = SelfLearningDB(path)
+        self.advisor = LearnedAdvisor(self.db) if learned else RuleBasedAdvisor(self.db)
+        eng = client.engine
+        orig = eng.execute
+
+        def execute(sinks, job_name="job"):
+            st = orig(sinks, job_name)
+            if eng.last_tcap is not None and eng.last_plan is not None and eng._last_comps is not None:
+                atoms = eng.last_plan.atoms
+                uses = extract_uses(atoms, eng._last_comps, eng.last_plan)
+                self.db.record_job(job_name, st.get("seconds", 0.0), uses)
+            return st
+
+        eng.execute = execute
+        client.learning = self
+
+    def advise(self, dbname: str, set_name: str) -> Optional[LambdaPolicy]:
+        k = self.advisor.best_key(dbname, set_name)
+        if k is None:
+            return None
+        self.db.record_placement(dbname, set_name, k)
+        return key_policy(*k)
+
+    def report(self) -> str:
+        return json.dumps(self.db.export(), default=str)[:10000]
+
+
+__all__ = ["SelfLearningDB", "RuleBasedAdvisor", "LearnedAdvisor", "SelfLearningHook", "extract_uses", "key_policy"]
