@@ -7,6 +7,7 @@
 
 extern "C" {
 int nsdb_gemm_splits(int M, int N, int K, int batch);
+void nsdb_gemm_force_config(int cfg);
 int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const float* bias, int M, int N, int K,
                       long long lda, long long ldb, long long ldc, long long sA, long long sB, long long sC,
                       long long sBias, int batch, int splits, int act, int bias_mode, int out_f32, float alpha,
@@ -229,6 +230,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dropout") = 0.0, py::arg("seed") = 0, py::arg("splits") = 0, py::arg("out") = py::none(),
         py::arg("accumulate") = false);
   m.def("gemm_splits", &gemm_splits);
+  m.def("gemm_force_config", [](int64_t cfg) { nsdb_gemm_force_config((int)cfg); },
+        "-1 auto, 0 = 128x128 tile, 1 = 256x256 tile (A/B testing)");
   m.def("conv2d", &conv2d, py::arg("X"), py::arg("W"), py::arg("bias") = py::none(), py::arg("KH") = 1,
         py::arg("KW") = 1, py::arg("stride") = 1, py::arg("pad") = 0, py::arg("dil") = 1, py::arg("act") = 0,
         py::arg("nchw_out") = false, py::arg("out_f32") = false);

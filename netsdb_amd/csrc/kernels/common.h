@@ -34,6 +34,19 @@ __device__ __forceinline__ float apply_act(float v, int act) {
   }
 }
 
+// Compact activation for unrolled MFMA epilogues: exp / sigmoid / tanh share ONE __expf
+// (t = exp(a*v): exp -> t, sigmoid -> 1/(1+t) with a=-1, tanh -> 2/(1+t)-1 with a=-2), so a
+// 128-element unrolled epilogue stays small enough to be fully unrolled (no acc spill to scratch).
+__device__ __forceinline__ float apply_act_compact(float v, int act) {
+  if (act == ACT_NONE) return v;
+  if (act == ACT_RELU) return fmaxf(v, 0.f);
+  const float a = act == ACT_EXP ? 1.f : (act == ACT_SIGMOID ? -1.f : -2.f);
+  const float t = __expf(a * v);
+  if (act == ACT_EXP) return t;
+  const float s = __frcp_rn(1.f + t);
+  return act == ACT_SIGMOID ? s : 2.f * s - 1.f;
+}
+
 // Counter-based hash RNG (stateless; identical on every launch for a given seed).
 __device__ __forceinline__ float hash_uniform(uint64_t seed, uint64_t idx) {
   uint64_t z = seed + idx * 0x9E3779B97F4A7C15ull;

@@ -36,7 +36,7 @@ def main():
     dev = "cuda:0"
     res = []
     shapes = [
-        ("ff_layer1_amazoncat14k_b1000", 1000, 1000, 597536),   # X[1000,597540->pad] . W1[1000,..]^T
+        ("ff_layer1_amazoncat14k_b1000", 1000, 1000, 597568),   # X[1000,597540->pad64] . W1[1000,..]^T
         ("ff_layer2_amazoncat14k_b1000", 1000, 14588, 1000),
         ("square_4096", 4096, 4096, 4096),
         ("square_8192", 8192, 8192, 8192),
@@ -48,10 +48,18 @@ def main():
         Kp = (K + 7) // 8 * 8
         A = torch.empty(M, Kp, device=dev, dtype=torch.bfloat16).uniform_(-1, 1)
         B = torch.empty(N, Kp, device=dev, dtype=torch.bfloat16).uniform_(-1, 1)
+        from netsdb_amd import _ext
+
+        cfg_ms = {}
+        for cfg in (0, 1):
+            _ext.hip().gemm_force_config(cfg)
+            cfg_ms[cfg] = timeit(lambda: ops.gemm_nt(A, B))
+        _ext.hip().gemm_force_config(-1)
         t_ours = timeit(lambda: ops.gemm_nt(A, B))
         t_lib = timeit(lambda: torch.matmul(A, B.t()))
         fl = 2.0 * M * N * Kp
         r = dict(op="gemm_nt", shape=name, M=M, N=N, K=Kp, ms=t_ours, tflops=fl / t_ours / 1e9,
+                 tile128_tflops=fl / cfg_ms[0] / 1e9, tile256_tflops=fl / cfg_ms[1] / 1e9,
                  lib_ms=t_lib, lib_tflops=fl / t_lib / 1e9, splits=ops.gemm_splits(M, N, Kp))
         print(json.dumps(r), flush=True)
         res.append(r)

@@ -30,9 +30,19 @@ def test_gemm_identity_asymmetric():
     torch.testing.assert_close(C, B.float().t().contiguous(), rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (1000, 1000, 4096), (77, 300, 520), (513, 129, 8), (2048, 64, 1024)])
+@pytest.fixture(params=[-1, 0, 1], ids=["auto", "tile128", "tile256"])
+def gemm_cfg(request):
+    from netsdb_amd import _ext
+
+    _ext.hip().gemm_force_config(request.param)
+    yield request.param
+    _ext.hip().gemm_force_config(-1)
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (1000, 1000, 4096), (77, 300, 520), (513, 129, 8), (2048, 64, 1024),
+                                   (600, 520, 2056)])
 @pytest.mark.parametrize("splits", [0, 1, 3])
-def test_gemm_shapes(M, N, K, splits):
+def test_gemm_shapes(M, N, K, splits, gemm_cfg):
     torch.manual_seed(0)
     A = torch.randn(M, K, device=DEV).to(torch.bfloat16)
     B = torch.randn(N, K, device=DEV).to(torch.bfloat16)
@@ -42,7 +52,7 @@ def test_gemm_shapes(M, N, K, splits):
 
 @pytest.mark.parametrize("mode,act", [(1, ops.ACT_RELU), (2, ops.ACT_SIGMOID), (2, ops.ACT_NONE), (1, ops.ACT_EXP)])
 @pytest.mark.parametrize("splits", [1, 4])
-def test_gemm_epilogue(mode, act, splits):
+def test_gemm_epilogue(mode, act, splits, gemm_cfg):
     torch.manual_seed(1)
     M, N, K = 300, 200, 640
     A = (torch.randn(M, K, device=DEV) * 0.05).to(torch.bfloat16)
@@ -60,6 +70,16 @@ def test_gemm_batched_strided():
     B = torch.randn(3, 70, 192, device=DEV).to(torch.bfloat16)
     C = ops.gemm_nt(A, B, out_dtype=torch.float32)
     _close(C, _ref_gemm(A, B), tol=1e-2)
+
+
+def test_gemm_accumulate(gemm_cfg):
+    torch.manual_seed(5)
+    A = torch.randn(300, 256, device=DEV).to(torch.bfloat16)
+    B = torch.randn(280, 256, device=DEV).to(torch.bfloat16)
+    C = torch.randn(300, 280, device=DEV)
+    ref = C + _ref_gemm(A, B)
+    ops.gemm_nt(A, B, out=C, out_dtype=torch.float32, accumulate=True)
+    _close(C, ref, tol=1e-2)
 
 
 def test_gemm_dropout_matches_host_rng():
