@@ -71,6 +71,65 @@ __device__ __forceinline__ bf16x8 read_frag(const char* lds_tile, int row, int c
   return *reinterpret_cast<const bf16x8*>(lds_tile + row * 128 + pc * 16);
 }
 
+// ---- epilogue, staged through the (now free) LDS: each wave spills its accumulators with
+// statically indexed ds_writes (keeps acc in registers: a heavy per-element epilogue unrolled
+// 128x would push acc to scratch), then all threads run the epilogue over whole rows ->
+// coalesced global stores (f32 split-K slabs or bf16/f32 C).
+// C/D map of 16x16x32: col = lane&15, row = (lane>>4)*4 + reg
+template <int TBM, int TBN, int WGM, int WGN>
+__device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[TBM / WGM / 16][TBN / WGN / 16], char* smem,
+                                               int smem_bytes, const GemmParams& p, int batch, int split, int m0,
+                                               int n0, int tid, int lane, int wave) {
+  constexpr int NW = WGM * WGN, TM = TBM / WGM / 16, TN = TBN / WGN / 16;
+  constexpr int WR = TBM / WGM, WC = TBN / WGN, WTILE = WR * WC;
+  static_assert(WC >= 32, "swizzle needs >= 32 columns per wave tile");
+  const int per_pass = min(smem_bytes / (WTILE * 4), NW);
+  float* st = reinterpret_cast<float*>(smem);
+  const int col_l = lane & 15, row_q = (lane >> 4) * 4;
+  const float* bias = p.bias ? p.bias + batch * p.sBias : nullptr;
+  const float keep_scale = p.dropout > 0.f ? 1.f / (1.f - p.dropout) : 1.f;
+  float* ws = p.splits > 1 ? p.ws + ((long long)batch * p.splits + split) * (long long)p.M * p.N : nullptr;
+  for (int g0 = 0; g0 < NW; g0 += per_pass) {
+    __syncthreads();
+    if (wave >= g0 && wave < g0 + per_pass) {
+      float* w = st + (wave - g0) * WTILE;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = i * 16 + row_q + r, col = j * 16 + col_l;
+            w[row * WC + (col ^ (((row >> 2) & 1) << 4))] = acc[i][j][r];
+          }
+    }
+    __syncthreads();
+    const int nwv = min(per_pass, NW - g0);
+    for (int e = tid; e < nwv * WTILE; e += 64 * NW) {
+      const int wl = e / WTILE, loc = e % WTILE, r = loc / WC, c = loc % WC;
+      const int wv = g0 + wl;
+      const int row = m0 + (wv / WGN) * WR + r, col = n0 + (wv % WGN) * WC + c;
+      if (row >= p.M || col >= p.N) continue;
+      float v = st[wl * WTILE + r * WC + (c ^ (((r >> 2) & 1) << 4))];
+      if (ws) {
+        ws[(long long)row * p.N + col] = v;
+        continue;
+      }
+      v *= p.alpha;
+      if (bias) v += p.bias_mode == 1 ? bias[row] : bias[col];
+      v = apply_act(v, p.act);
+      if (p.dropout > 0.f) {
+        const unsigned long long idx = ((unsigned long long)batch * p.M + row) * p.N + col;
+        v = hash_uniform(p.seed, idx) < p.dropout ? 0.f : v * keep_scale;
+      }
+      const long long off = batch * p.sC + (long long)row * p.ldc + col;
+      if (p.accumulate) v += reinterpret_cast<float*>(p.C)[off];
+      if (p.out_f32) reinterpret_cast<float*>(p.C)[off] = v;
+      else reinterpret_cast<unsigned short*>(p.C)[off] = f32_to_bf16(v);
+    }
+  }
+}
+
 // TBM x TBN tile, WGM x WGN waves; each wave owns (TBM/WGM) x (TBN/WGN) = TM x TN 16x16 MFMA tiles.
 //   <128,128,2,2>: 256 threads, 64 KiB LDS, 2 blocks/CU (general shapes)
 //   <256,256,2,4>: 512 threads, 128 KiB LDS, 1 block/CU, 128x64 per wave = 32 MFMAs per k-substep:
@@ -151,58 +210,182 @@ gemm_nt_tile_kernel(GemmParams p) {
     __syncthreads();
   }
 
-  // ---- epilogue, staged through the (now free) LDS: each wave spills its accumulators with
-  // statically indexed ds_writes (keeps acc in registers: a heavy per-element epilogue unrolled
-  // 128x would push acc to scratch), then all threads run the epilogue over whole rows ->
-  // coalesced global stores (f32 split-K slabs or bf16/f32 C).
-  // C/D map of 16x16x32: col = lane&15, row = (lane>>4)*4 + reg
-  constexpr int WR = TBM / WGM, WC = TBN / WGN, WTILE = WR * WC;
-  constexpr int PER_PASS = (2 * STG) / (WTILE * 4) < NW ? (2 * STG) / (WTILE * 4) : NW;
-  static_assert(WC >= 32, "swizzle needs >= 32 columns per wave tile");
-  float* st = reinterpret_cast<float*>(smem);
-  const int col_l = lane & 15, row_q = (lane >> 4) * 4;
-  const float* bias = p.bias ? p.bias + batch * p.sBias : nullptr;
-  const float keep_scale = p.dropout > 0.f ? 1.f / (1.f - p.dropout) : 1.f;
-  float* ws = p.splits > 1 ? p.ws + ((long long)batch * p.splits + split) * (long long)p.M * p.N : nullptr;
-  for (int g0 = 0; g0 < NW; g0 += PER_PASS) {
-    __syncthreads();
-    if (wave >= g0 && wave < g0 + PER_PASS) {
-      float* w = st + (wave - g0) * WTILE;
+  store_tile_lds<TBM, TBN, WGM, WGN>(acc, smem, 2 * STG, p, batch, split, m0, n0, tid, lane, wave);
+}
+
+// ---------------------------------------------------------------------------------------------
+// 256x256x64 "8-phase" kernel for long-K / large shapes (cdna_hip_programming.md §5, the 256^2
+// 8-phase template): 512 threads = 8 waves as 2(M) x 4(N), each wave 128x64 = 8x4 MFMA tiles.
+//
+//  * Each K-tile (64 KiB: A 256x64 + B 256x64) is held as four 16 KiB "half-tiles" in LDS:
+//      A0 = rows {0..63, 128..191}, A1 = rows {64..127, 192..255}      (wave M-group wr: rows wr*128+qm*64..)
+//      B0 = rows {wc*64 + 0..31},    B1 = rows {wc*64 + 32..63}           (wave N index wc)
+//    so the C-quadrant (qm, qn) a wave computes in a phase reads exactly half-tiles A_qm and B_qn.
+//  * 4 phases per K-tile, quadrant order (0,0) (0,1) (1,1) (1,0); 2 LDS buffers, 2 K-tiles/iteration.
+//    Every phase: ds_read its fragments -> issue ONE half-tile LDS-DMA (2 x buffer_load...lds per
+//    thread) -> raw s_barrier -> lgkmcnt(0) -> 16 MFMAs at high priority -> raw s_barrier.
+//  * Wave group wr=1 runs one barrier behind wr=0 (one extra s_barrier up front): on every SIMD one
+//    wave is on the MFMAs while the other issues its LDS reads and DMA (ping-pong).
+//  * Staging schedule for the tile t in buffer b (phase j):
+//      j0 -> A1 of t+1 (buffer b^1)   j1 -> B0 of t+2 (b)   j2 -> A0 of t+2 (b)   j3 -> B1 of t+2 (b)
+//    WAR: a half-tile is restaged >= 2 phases after its last ds_read, or 1 phase after when a counted
+//    lgkmcnt before the reading phase's first barrier retired those reads (B0: lgkmcnt(8) in j0 —
+//    its 4 B reads are issued first, then 8 A reads, order pinned by sched_barrier).
+//    RAW: s_waitcnt vmcnt(6) in j3 (3 half-tiles stay in flight across the barrier) retires all of
+//    tile t+1, which is first read in the NEXT phase (never in the same phase as its wait).
+//    vmcnt is never 0 inside the loop; beyond the last K-tile the DMA targets k >= kend, which the
+//    buffer range check zero-fills, so every phase issues the same number of VMEM ops.
+//  * All LDS is one __shared__ array (a second object makes hipcc drain vmcnt before ds_reads).
+// ---------------------------------------------------------------------------------------------
+#define NSDB_BARRIER()                          \
+  do {                                          \
+    __builtin_amdgcn_sched_barrier(0);          \
+    asm volatile("s_barrier" ::: "memory");     \
+    __builtin_amdgcn_sched_barrier(0);          \
+  } while (0)
+
+// V: diagnostic variants (0 = production). 1 no setprio, 2 stage before ds_reads, 3 no group stagger,
+// 4 no DMA issued (load-free upper bound, wrong results), 5 no ds_reads after the first tile (wrong results),
+// 6 no vmcnt wait in the loop (racy), 7 zero-record descriptors (DMA issued, no memory traffic)
+template <int V>
+__global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
+  constexpr int HALF = 128 * 128;            // bytes of one half-tile (128 rows x 64 bf16)
+  constexpr int BUF = 4 * HALF;              // one K-tile
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+
+  const int ntiles = p.tiles_m * p.tiles_n;
+  const int wg = xcd_remap(blockIdx.x, ntiles * p.splits);
+  const int split = wg / ntiles, tile = wg % ntiles;
+  const int tm = tile % p.tiles_m, tn = tile / p.tiles_m;
+  const int batch = blockIdx.z;
+  const int m0 = tm * 256, n0 = tn * 256;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+
+  const int rows_a = min(256, p.M - m0), rows_b = min(256, p.N - n0);
+  const unsigned short* Ab = p.A + batch * p.sA + (long long)m0 * p.lda;
+  const unsigned short* Bb = p.B + batch * p.sB + (long long)n0 * p.ldb;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(Ab, V == 7 ? 0u : (unsigned)((long long)rows_a * p.lda * 2));
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(Bb, V == 7 ? 0u : (unsigned)((long long)rows_b * p.ldb * 2));
+
+  const int kbeg = split * p.kchunk;
+  const int kend = min(p.K, kbeg + p.kchunk);
+  const int nk = max(0, (kend - kbeg + BK - 1) / BK);
+  const int niter = (nk + 1) >> 1;
+
+  // Per-thread DMA source rows. Wave-instruction i of a half-tile fills LDS rows
+  // hr = i*64 + wave*8 + (lane>>3) (1 KiB, lane-linear); the logical 16-B chunk at physical slot
+  // lane&7 is chunk ^ ((hr>>1)&7) (same swizzle as read_frag), hence a per-lane k offset.
+  const int lr = wave * 8 + (lane >> 3);
+  const int kc = ((lane & 7) ^ ((lr >> 1) & 7)) * 8;
+  int roff[4][2];      // [slot A0,A1,B0,B1][i] byte offset of the source row, or -1 if out of range
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+  for (int q = 0; q < 2; ++q)
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = i * 16 + row_q + r, col = j * 16 + col_l;
-            w[row * WC + (col ^ (((row >> 2) & 1) << 4))] = acc[i][j][r];
-          }
+    for (int i = 0; i < 2; ++i) {
+      const int ta = i * 128 + q * 64 + lr;
+      const int tb = (2 * i + (lr >> 5)) * 64 + q * 32 + (lr & 31);
+      roff[q][i] = ta < rows_a ? (int)((long long)ta * p.lda * 2) : -1;
+      roff[2 + q][i] = tb < rows_b ? (int)((long long)tb * p.ldb * 2) : -1;
     }
-    __syncthreads();
-    const int nwv = min(PER_PASS, NW - g0);
-    for (int e = tid; e < nwv * WTILE; e += 64 * NW) {
-      const int wl = e / WTILE, loc = e % WTILE, r = loc / WC, c = loc % WC;
-      const int wv = g0 + wl;
-      const int row = m0 + (wv / WGN) * WR + r, col = n0 + (wv % WGN) * WC + c;
-      if (row >= p.M || col >= p.N) continue;
-      float v = st[wl * WTILE + r * WC + (c ^ (((r >> 2) & 1) << 4))];
-      if (ws) {
-        ws[(long long)row * p.N + col] = v;
-        continue;
-      }
-      v *= p.alpha;
-      if (bias) v += p.bias_mode == 1 ? bias[row] : bias[col];
-      v = apply_act(v, p.act);
-      if (p.dropout > 0.f) {
-        const unsigned long long idx = ((unsigned long long)batch * p.M + row) * p.N + col;
-        v = hash_uniform(p.seed, idx) < p.dropout ? 0.f : v * keep_scale;
-      }
-      const long long off = batch * p.sC + (long long)row * p.ldc + col;
-      if (p.accumulate) v += reinterpret_cast<float*>(p.C)[off];
-      if (p.out_f32) reinterpret_cast<float*>(p.C)[off] = v;
-      else reinterpret_cast<unsigned short*>(p.C)[off] = f32_to_bf16(v);
+
+  auto stage = [&](int buf, int slot, int u) {
+    if constexpr (V == 4) return;
+    const int k = kbeg + u * BK + kc;
+    const bool kin = k < kend;
+    char* dst = smem + buf * BUF + slot * HALF;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int ro = roff[slot][i];
+      const int voff = (kin && ro >= 0) ? ro + k * 2 : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(slot < 2 ? ra : rb, (lds_void*)(dst + (i * 64 + wave * 8) * 128), 16,
+                                               voff, 0, 0, 0);
     }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[4][2], b0[2][2], b1[2][2];
+
+  bool skip_reads = false;
+  auto readA = [&](int buf, int q) {
+    if constexpr (V == 5) { if (skip_reads) return; }
+    const char* base = smem + buf * BUF + q * HALF;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) af[mi][kk] = read_frag(base, wr * 64 + mi * 16 + (lane & 15), kk * 4 + (lane >> 4));
+  };
+  auto readB = [&](int buf, int q, bf16x8 (&bq)[2][2]) {
+    if constexpr (V == 5) { if (skip_reads) return; }
+    const char* base = smem + buf * BUF + (2 + q) * HALF;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) bq[ni][kk] = read_frag(base, wc * 32 + ni * 16 + (lane & 15), kk * 4 + (lane >> 4));
+  };
+  auto mma = [&](int qm, int qn, const bf16x8 (&bq)[2][2]) {
+    NSDB_BARRIER();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (V != 1) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+          acc[qm * 4 + mi][qn * 2 + ni] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi][kk], bq[ni][kk], acc[qm * 4 + mi][qn * 2 + ni], 0, 0, 0);
+    if constexpr (V != 1) __builtin_amdgcn_s_setprio(0);
+    NSDB_BARRIER();
+  };
+  // one K-tile u held in buffer `cur` (u+1 in cur^1)
+  auto ktile = [&](int cur, int u) {
+    // j0: quadrant (0,0); reads B0 then A0; stages A1 of u+1
+    if constexpr (V == 2) stage(cur ^ 1, 1, u + 1);
+    readB(cur, 0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    readA(cur, 0);
+    if constexpr (V != 2) stage(cur ^ 1, 1, u + 1);
+    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");   // the 4 B0 reads (issued first) are done
+    mma(0, 0, b0);
+    // j1: quadrant (0,1); reads B1; stages B0 of u+2
+    if constexpr (V == 2) stage(cur, 2, u + 2);
+    readB(cur, 1, b1);
+    if constexpr (V != 2) stage(cur, 2, u + 2);
+    mma(0, 1, b1);
+    // j2: quadrant (1,1); reads A1; stages A0 of u+2
+    if constexpr (V == 2) stage(cur, 0, u + 2);
+    readA(cur, 1);
+    if constexpr (V != 2) stage(cur, 0, u + 2);
+    mma(1, 1, b1);
+    // j3: quadrant (1,0) from registers; stages B1 of u+2; retires tile u+1 (3 half-tiles stay in flight)
+    stage(cur, 3, u + 2);
+    if constexpr (V != 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    mma(1, 0, b0);
+  };
+
+  // prologue: tile 0 (4 halves) + B0, A0, B1 of tile 1; tile 0 complete when <= 6 ops remain
+  stage(0, 2, 0); stage(0, 0, 0); stage(0, 3, 0); stage(0, 1, 0);
+  stage(1, 2, 1); stage(1, 0, 1); stage(1, 3, 1);
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  NSDB_BARRIER();
+  if (V != 3 && wr == 1) NSDB_BARRIER();            // stagger the two wave groups by one barrier
+
+  for (int it = 0; it < niter; ++it) {
+    ktile(0, 2 * it);
+    ktile(1, 2 * it + 1);
+    if constexpr (V == 5) skip_reads = true;
   }
+  if (V != 3 && wr == 0) NSDB_BARRIER();            // re-align the groups
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // trailing zero-fill DMAs land before LDS reuse
+  store_tile_lds<256, 256, 2, 4>(acc, smem, 2 * BUF, p, batch, split, m0, n0, tid, lane, wave);
 }
 
 // Split-K slab reducer + fused epilogue (the ClusterAggregate "combine" of the partial block products).
@@ -238,7 +421,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(GemmParams p) {
 // ---------------------------------------------------------------- host side
 extern "C" {
 
-static int g_force_cfg = -1;   // -1 auto, 0 = 128x128, 1 = 256x256 (A/B testing)
+static int g_force_cfg = -1;   // -1 auto, 0 = 128x128, 1 = 256x256 2-stage, 2 = 256x256 8-phase (A/B testing)
 
 // Tile config: the 256x256 tile (1 block/CU) when both dims fill it and there is enough work.
 static int pick_cfg(int M, int N, int K, int batch) {
@@ -299,7 +482,16 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
   p.tiles_m = (M + tbm - 1) / tbm;
   p.tiles_n = (N + tbn - 1) / tbn;
   dim3 grid(p.tiles_m * p.tiles_n * p.splits, 1, batch);
-  if (cfg)
+  if (cfg == 2)
+    hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<0>, grid, dim3(512), 0, stream, p);
+  else if (cfg >= 3 && cfg <= 9) {   // diagnostic variants of the 8-phase kernel (timing only)
+    auto kern = cfg == 3 ? nsdb::gemm_nt_256_8ph_kernel<1> : cfg == 4 ? nsdb::gemm_nt_256_8ph_kernel<2>
+              : cfg == 5 ? nsdb::gemm_nt_256_8ph_kernel<3> : cfg == 6 ? nsdb::gemm_nt_256_8ph_kernel<4>
+              : cfg == 7 ? nsdb::gemm_nt_256_8ph_kernel<5> : cfg == 8 ? nsdb::gemm_nt_256_8ph_kernel<6>
+                         : nsdb::gemm_nt_256_8ph_kernel<7>;
+    hipLaunchKernelGGL(kern, grid, dim3(512), 0, stream, p);
+  }
+  else if (cfg == 1)
     hipLaunchKernelGGL((nsdb::gemm_nt_tile_kernel<256, 256, 2, 4>), grid, dim3(512), 0, stream, p);
   else
     hipLaunchKernelGGL((nsdb::gemm_nt_tile_kernel<128, 128, 2, 2>), grid, dim3(256), 0, stream, p);

@@ -1,0 +1,782 @@
+"""TPC-H on netsdb_amd — schema, a deterministic synthetic generator, and the reference's query set
+(reference: src/tpch/headers/TPCHSchema.h, Query01/02/03/04/06/12/13/14/17/22.h, src/tpch/source/
+tpchDataLoader.cc, Query*/ drivers).
+
+Every query is a netsDB computation graph (SelectionComp / JoinComp / AggregateComp / TopKComp over
+ScanSets) executed by the engine; the lambdas are *vectorised* over whole record batches, so numeric
+predicates and the revenue arithmetic run as tensor ops on the set's device (HBM-resident columns on a
+GPU node) and the group-bys reduce on the device (``index_add`` over fp64 value rows).
+
+Storage choices (MI355X-first, semantics unchanged):
+  * dates are ``int`` yyyymmdd (order-preserving, so ``<``/``>=`` match the reference's strcmp on
+    'YYYY-MM-DD' strings) and money/quantities are ``float`` (fp64) columns;
+  * the remaining text fields (flags, modes, names, comments) are host string columns.
+
+The generator follows TPC-H dbgen's cardinalities and value domains (SF x 150k customers, 1.5M
+orders, 1-7 lineitems per order, 200k parts x 4 suppliers, custkeys with ``custkey % 3 == 0``
+placing no orders, ...) but is NOT byte-identical to dbgen — there is no network to fetch dbgen
+output; ``reference_*`` functions (pandas) pin every query's result on the same generated data.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..computations import AggregateComp, JoinComp, ScanSet, SelectionComp, TopKComp, WriteSet
+from ..lambdas import make_batch_lambda, make_lambda_from_member
+from ..objects.record import PDBObject, RecordBatch
+
+# ----------------------------------------------------------------------------------------- schema
+
+
+class Region(PDBObject):
+    r_regionkey: int
+    r_name: str
+    r_comment: str
+
+
+class Nation(PDBObject):
+    n_nationkey: int
+    n_name: str
+    n_regionkey: int
+    n_comment: str
+
+
+class Supplier(PDBObject):
+    s_suppkey: int
+    s_name: str
+    s_address: str
+    s_nationkey: int
+    s_phone: str
+    s_acctbal: float
+    s_comment: str
+
+
+class Customer(PDBObject):
+    c_custkey: int
+    c_name: str
+    c_address: str
+    c_nationkey: int
+    c_phone: str
+    c_acctbal: float
+    c_mktsegment: str
+    c_comment: str
+
+
+class Part(PDBObject):
+    p_partkey: int
+    p_name: str
+    p_mfgr: str
+    p_brand: str
+    p_type: str
+    p_size: int
+    p_container: str
+    p_retailprice: float
+    p_comment: str
+
+
+class PartSupp(PDBObject):
+    ps_partkey: int
+    ps_suppkey: int
+    ps_availqty: int
+    ps_supplycost: float
+    ps_comment: str
+
+
+class Order(PDBObject):
+    o_orderkey: int
+    o_custkey: int
+    o_orderstatus: str
+    o_totalprice: float
+    o_orderdate: int
+    o_orderpriority: str
+    o_clerk: str
+    o_shippriority: int
+    o_comment: str
+
+
+class LineItem(PDBObject):
+    l_orderkey: int
+    l_partkey: int
+    l_suppkey: int
+    l_linenumber: int
+    l_quantity: float
+    l_extendedprice: float
+    l_discount: float
+    l_tax: float
+    l_returnflag: str
+    l_linestatus: str
+    l_shipdate: int
+    l_commitdate: int
+    l_receiptdate: int
+    l_shipinstruct: str
+    l_shipmode: str
+    l_comment: str
+
+
+TABLES = {"region": Region, "nation": Nation, "supplier": Supplier, "customer": Customer, "part": Part,
+          "partsupp": PartSupp, "orders": Order, "lineitem": LineItem}
+
+# -------------------------------------------------------------------------------------- generator
+REGIONS = ["AFRICA", "AMERICA", "ASIA", "EUROPE", "MIDDLE EAST"]
+NATIONS = [("ALGERIA", 0), ("ARGENTINA", 1), ("BRAZIL", 1), ("CANADA", 1), ("EGYPT", 4), ("ETHIOPIA", 0),
+           ("FRANCE", 3), ("GERMANY", 3), ("INDIA", 2), ("INDONESIA", 2), ("IRAN", 4), ("IRAQ", 4), ("JAPAN", 2),
+           ("JORDAN", 4), ("KENYA", 0), ("MOROCCO", 0), ("MOZAMBIQUE", 0), ("PERU", 1), ("CHINA", 2),
+           ("ROMANIA", 3), ("SAUDI ARABIA", 4), ("VIETNAM", 2), ("RUSSIA", 3), ("UNITED KINGDOM", 3),
+           ("UNITED STATES", 1)]
+SEGMENTS = ["AUTOMOBILE", "BUILDING", "FURNITURE", "HOUSEHOLD", "MACHINERY"]
+PRIORITIES = ["1-URGENT", "2-HIGH", "3-MEDIUM", "4-NOT SPECIFIED", "5-LOW"]
+SHIPMODES = ["REG AIR", "AIR", "RAIL", "SHIP", "TRUCK", "MAIL", "FOB"]
+INSTRUCTS = ["DELIVER IN PERSON", "COLLECT COD", "NONE", "TAKE BACK RETURN"]
+TYPE_S1 = ["STANDARD", "SMALL", "MEDIUM", "LARGE", "ECONOMY", "PROMO"]
+TYPE_S2 = ["ANODIZED", "BURNISHED", "PLATED", "POLISHED", "BRUSHED"]
+TYPE_S3 = ["TIN", "NICKEL", "BRASS", "STEEL", "COPPER"]
+CONT_S1 = ["SM", "LG", "MED", "JUMBO", "WRAP"]
+CONT_S2 = ["CASE", "BOX", "BAG", "JAR", "PKG", "PACK", "CAN", "DRUM"]
+WORDS = ["furiously", "quickly", "carefully", "blithely", "regular", "final", "pending", "express", "ironic",
+         "deposits", "accounts", "packages", "theodolites", "pinto", "beans", "foxes", "ideas", "dependencies"]
+CURRENT_DATE = 19950617
+
+
+def _days_to_ymd(d: np.ndarray) -> np.ndarray:
+    dt = np.datetime64("1970-01-01") + d.astype("timedelta64[D]")
+    y = dt.astype("datetime64[Y]").astype(int) + 1970
+    m = dt.astype("datetime64[M]").astype(int) % 12 + 1
+    day = (dt - dt.astype("datetime64[M]")).astype(int) + 1
+    return (y * 10000 + m * 100 + day).astype(np.int64)
+
+
+def _ymd_to_days(v: int) -> int:
+    s = f"{v:08d}"
+    return int((np.datetime64(f"{s[:4]}-{s[4:6]}-{s[6:]}") - np.datetime64("1970-01-01")).astype(int))
+
+
+def add_days(ymd: int, n: int) -> int:
+    return int(_days_to_ymd(np.array([_ymd_to_days(ymd) + n]))[0])
+
+
+def _comments(rng, n, special_frac=0.0):
+    w = rng.integers(0, len(WORDS), size=(n, 4))
+    out = [" ".join(WORDS[j] for j in row) for row in w]
+    if special_frac > 0:
+        for i in np.nonzero(rng.random(n) < special_frac)[0]:
+            out[i] = f"{out[i]} special {WORDS[w[i, 0]]} requests"
+    return out
+
+
+def generate(sf: float = 0.01, seed: int = 0) -> Dict[str, Dict[str, object]]:
+    """Columnar TPC-H tables: ``{table: {column: np.ndarray | list[str]}}``."""
+    rng = np.random.default_rng(seed)
+    n_supp = max(10, int(10000 * sf))
+    n_cust = max(30, int(150000 * sf))
+    n_part = max(40, int(200000 * sf))
+    n_ord = max(150, int(1500000 * sf))
+    t: Dict[str, Dict[str, object]] = {}
+    t["region"] = {"r_regionkey": np.arange(5), "r_name": list(REGIONS), "r_comment": _comments(rng, 5)}
+    t["nation"] = {"n_nationkey": np.arange(25), "n_name": [n for n, _ in NATIONS],
+                   "n_regionkey": np.array([r for _, r in NATIONS]), "n_comment": _comments(rng, 25)}
+    sk = np.arange(1, n_supp + 1)
+    snat = rng.integers(0, 25, n_supp)
+    t["supplier"] = {"s_suppkey": sk, "s_name": [f"Supplier#{k:09d}" for k in sk],
+                     "s_address": [f"addr{k}" for k in sk], "s_nationkey": snat,
+                     "s_phone": [f"{n + 10}-{k % 900 + 100}-{k % 800 + 200}-{k % 9000 + 1000}" for k, n in zip(sk, snat)],
+                     "s_acctbal": np.round(rng.uniform(-999.99, 9999.99, n_supp), 2), "s_comment": _comments(rng, n_supp)}
+    ck = np.arange(1, n_cust + 1)
+    cnat = rng.integers(0, 25, n_cust)
+    t["customer"] = {"c_custkey": ck, "c_name": [f"Customer#{k:09d}" for k in ck], "c_address": [f"caddr{k}" for k in ck],
+                     "c_nationkey": cnat,
+                     "c_phone": [f"{n + 10}-{rng.integers(100, 999)}-{rng.integers(100, 999)}-{rng.integers(1000, 9999)}"
+                                 for n in cnat],
+                     "c_acctbal": np.round(rng.uniform(-999.99, 9999.99, n_cust), 2),
+                     "c_mktsegment": [SEGMENTS[i] for i in rng.integers(0, 5, n_cust)], "c_comment": _comments(rng, n_cust)}
+    pk = np.arange(1, n_part + 1)
+    retail = np.round((90000 + (pk // 10) % 20001 + 100 * (pk % 1000)) / 100.0, 2)
+    m = rng.integers(1, 6, n_part)
+    t["part"] = {"p_partkey": pk, "p_name": [" ".join(WORDS[j] for j in rng.integers(0, len(WORDS), 3)) for _ in pk],
+                 "p_mfgr": [f"Manufacturer#{x}" for x in m],
+                 "p_brand": [f"Brand#{x}{y}" for x, y in zip(m, rng.integers(1, 6, n_part))],
+                 "p_type": [f"{TYPE_S1[a]} {TYPE_S2[b]} {TYPE_S3[c]}" for a, b, c in
+                            zip(rng.integers(0, 6, n_part), rng.integers(0, 5, n_part), rng.integers(0, 5, n_part))],
+                 "p_size": rng.integers(1, 51, n_part),
+                 "p_container": [f"{CONT_S1[a]} {CONT_S2[b]}" for a, b in zip(rng.integers(0, 5, n_part),
+                                                                              rng.integers(0, 8, n_part))],
+                 "p_retailprice": retail, "p_comment": _comments(rng, n_part)}
+    ps_pk = np.repeat(pk, 4)
+    ps_sk = ((ps_pk + np.tile(np.arange(4), n_part) * (n_supp // 4 + (ps_pk - 1) // n_supp)) % n_supp) + 1
+    t["partsupp"] = {"ps_partkey": ps_pk, "ps_suppkey": ps_sk, "ps_availqty": rng.integers(1, 10000, 4 * n_part),
+                     "ps_supplycost": np.round(rng.uniform(1.0, 1000.0, 4 * n_part), 2),
+                     "ps_comment": _comments(rng, 4 * n_part)}
+    # orders: sparse keys as dbgen (8 keys used of every 32), customers with key % 3 == 0 place none
+    ok = np.arange(n_ord)
+    ok = (ok // 8) * 32 + (ok % 8) + 1
+    valid_c = ck[ck % 3 != 0]
+    ocust = valid_c[rng.integers(0, len(valid_c), n_ord)]
+    start, end = _ymd_to_days(19920101), _ymd_to_days(19980802) - 151
+    odays = rng.integers(start, end + 1, n_ord)
+    nl = rng.integers(1, 8, n_ord)
+    li_ord = np.repeat(np.arange(n_ord), nl)
+    nli = len(li_ord)
+    lnum = np.concatenate([np.arange(1, k + 1) for k in nl])
+    lpk = rng.integers(1, n_part + 1, nli)
+    lsk = ((lpk + rng.integers(0, 4, nli) * (n_supp // 4 + (lpk - 1) // n_supp)) % n_supp) + 1
+    qty = rng.integers(1, 51, nli).astype(np.float64)
+    ext = np.round(qty * retail[lpk - 1], 2)
+    disc = rng.integers(0, 11, nli) / 100.0
+    tax = rng.integers(0, 9, nli) / 100.0
+    ship = odays[li_ord] + rng.integers(1, 122, nli)
+    commit = odays[li_ord] + rng.integers(30, 91, nli)
+    receipt = ship + rng.integers(1, 31, nli)
+    ship_y, commit_y, receipt_y = _days_to_ymd(ship), _days_to_ymd(commit), _days_to_ymd(receipt)
+    rflag = np.where(receipt_y <= CURRENT_DATE, np.where(rng.random(nli) < 0.5, "R", "A"), "N")
+    lstatus = np.where(ship_y > CURRENT_DATE, "O", "F")
+    t["lineitem"] = {"l_orderkey": ok[li_ord], "l_partkey": lpk, "l_suppkey": lsk, "l_linenumber": lnum,
+                     "l_quantity": qty, "l_extendedprice": ext, "l_discount": disc, "l_tax": tax,
+                     "l_returnflag": rflag.tolist(), "l_linestatus": lstatus.tolist(), "l_shipdate": ship_y,
+                     "l_commitdate": commit_y, "l_receiptdate": receipt_y,
+                     "l_shipinstruct": [INSTRUCTS[i] for i in rng.integers(0, 4, nli)],
+                     "l_shipmode": [SHIPMODES[i] for i in rng.integers(0, 7, nli)], "l_comment": _comments(rng, nli)}
+    total = np.zeros(n_ord)
+    np.add.at(total, li_ord, ext * (1 + tax) * (1 - disc))
+    nF = np.zeros(n_ord, dtype=np.int64)
+    np.add.at(nF, li_ord, (lstatus == "F").astype(np.int64))
+    ostatus = np.where(nF == nl, "F", np.where(nF == 0, "O", "P"))
+    t["orders"] = {"o_orderkey": ok, "o_custkey": ocust, "o_orderstatus": ostatus.tolist(),
+                   "o_totalprice": np.round(total, 2), "o_orderdate": _days_to_ymd(odays),
+                   "o_orderpriority": [PRIORITIES[i] for i in rng.integers(0, 5, n_ord)],
+                   "o_clerk": [f"Clerk#{i:09d}" for i in rng.integers(1, max(2, int(1000 * sf)) + 1, n_ord)],
+                   "o_shippriority": np.zeros(n_ord, dtype=np.int64), "o_comment": _comments(rng, n_ord, 0.02)}
+    return t
+
+
+def to_batch(table: str, cols: Dict[str, object], device=None) -> RecordBatch:
+    typ = TABLES[table]
+    out = {}
+    n = None
+    for name, ft in typ.fields().items():
+        v = cols[name]
+        if ft is str:
+            out[name] = list(v)
+        else:
+            arr = np.asarray(v)
+            out[name] = torch.from_numpy(arr.astype(np.float64 if ft is float else np.int64))
+            if device is not None:
+                out[name] = out[name].to(device)
+        n = len(v)
+    return RecordBatch(out, n, typ)
+
+
+def load(client, db: str, tables: Dict[str, Dict[str, object]], page_rows: Optional[int] = None):
+    """Create the TPC-H sets and dispatch the rows (tpchDataLoader.cc)."""
+    client.create_database(db)
+    for name, typ in TABLES.items():
+        client.create_set(db, name, typ)
+        client.send_data(db, name, to_batch(name, tables[name]))
+
+
+# ------------------------------------------------------------------------------------ helpers
+def _col(b: RecordBatch, name: str):
+    return b.columns[name]
+
+
+def _strmask(strings: Sequence[str], pred, device) -> torch.Tensor:
+    return torch.tensor([bool(pred(s)) for s in strings], dtype=torch.bool, device=device)
+
+
+def _isin_str(strings: Sequence[str], allowed: Sequence[str], device) -> torch.Tensor:
+    a = set(allowed)
+    return _strmask(strings, lambda s: s in a, device)
+
+
+def _dev(b: RecordBatch):
+    for v in b.columns.values():
+        if isinstance(v, torch.Tensor):
+            return v.device
+    return torch.device("cpu")
+
+
+class _Filter(SelectionComp):
+    """SelectionComp with a vectorised boolean predicate over the whole batch."""
+
+    def __init__(self, pred):
+        super().__init__()
+        self.pred = pred
+
+    def get_selection(self, x):
+        return make_batch_lambda(x, self.pred)
+
+    def get_projection(self, x):
+        from ..lambdas import make_lambda_from_self
+
+        return make_lambda_from_self(x)
+
+
+class _GroupBy(AggregateComp):
+    """Group-by with a vectorised key (column or tuple of columns) and an [n, F] fp64 value row."""
+
+    def __init__(self, key_fn, val_fn, out_fn, reduce_op: str = "sum"):
+        super().__init__()
+        self.key_fn, self.val_fn, self.out_fn = key_fn, val_fn, out_fn
+        self.reduce_op = reduce_op
+
+    def get_key_projection(self, x):
+        return make_batch_lambda(x, self.key_fn)
+
+    def get_value_projection(self, x):
+        return make_batch_lambda(x, self.val_fn)
+
+    def make_output(self, keys, values):
+        return self.out_fn(keys, values)
+
+
+def _rows_out(names: List[str]):
+    """make_output building a plain tuple-set batch {key columns..., value columns...}."""
+
+    def out(keys, values):
+        ks = keys if isinstance(keys, tuple) else (keys,)
+        ks = [list(k) if not isinstance(k, torch.Tensor) else k for k in ks]
+        if isinstance(values, torch.Tensor):
+            v = values if values.dim() == 2 else values.unsqueeze(1)
+        else:
+            v = torch.stack([torch.as_tensor(x) for x in values])
+        n = v.shape[0]
+        cols = {f"k{i}": k for i, k in enumerate(ks)}
+        for j, nm in enumerate(names):
+            cols[nm] = v[:, j]
+        return RecordBatch(cols, n)
+
+    return out
+
+
+def _str_keys(*cols):
+    """Tuple key of string columns -> a single string key per row (host grouping)."""
+    return ["|".join(t) for t in zip(*cols)]
+
+
+def _collect(client, db: str, name: str) -> List[RecordBatch]:
+    return [b for b in client.get_set_batches(db, name, gather=True) if b.n]
+
+
+def _run(client, db: str, out: str, comp, job: str):
+    if client.storage.has_set(db, out):
+        client.remove_set(db, out)
+    client.create_set(db, out, None)
+    client.execute_computations(WriteSet(db, out).set_input(comp), job_name=job)
+    got = _collect(client, db, out)
+    if not got:
+        return None
+    b = RecordBatch.concat(got)
+    return b.columns["value"] if "value" in b.columns and isinstance(b.columns["value"], RecordBatch) else b
+
+
+def _flat(b):
+    """Unwrap the aggregate's output column into its record batch."""
+    if b is None:
+        return None
+    if isinstance(b, RecordBatch) and len(b.columns) == 1:
+        v = next(iter(b.columns.values()))
+        if isinstance(v, RecordBatch):
+            return v
+    return b
+
+
+def _as_list(c):
+    return c.tolist() if isinstance(c, torch.Tensor) else list(c)
+
+
+# ------------------------------------------------------------------------------------ queries
+def q01(client, db: str, delta_days: int = 90) -> List[dict]:
+    """Pricing summary report (Query01.h: Q01Agg over LineItem keyed by returnflag|linestatus)."""
+    cutoff = add_days(19981201, -delta_days)
+    sel = _Filter(lambda b: _col(b, "l_shipdate") <= cutoff).set_input(ScanSet(db, "lineitem", LineItem))
+
+    def vals(b):
+        q, p, d, t = (_col(b, c).double() for c in ("l_quantity", "l_extendedprice", "l_discount", "l_tax"))
+        dp = p * (1 - d)
+        return torch.stack([q, p, dp, dp * (1 + t), d, torch.ones_like(q)], 1)
+
+    agg = _GroupBy(lambda b: _str_keys(_col(b, "l_returnflag"), _col(b, "l_linestatus")), vals,
+                   _rows_out(["sum_qty", "sum_base_price", "sum_disc_price", "sum_charge", "sum_disc", "count"]))
+    r = _flat(_run(client, db, "q01_out", agg.set_input(sel), "tpch_q01"))
+    out = []
+    if r is None:
+        return out
+    for i, k in enumerate(_as_list(r.columns["k0"])):
+        rf, ls = k.split("|")
+        c = float(r.columns["count"][i])
+        row = {"l_returnflag": rf, "l_linestatus": ls}
+        for f in ("sum_qty", "sum_base_price", "sum_disc_price", "sum_charge"):
+            row[f] = float(r.columns[f][i])
+        row.update(avg_qty=row["sum_qty"] / c, avg_price=row["sum_base_price"] / c,
+                   avg_disc=float(r.columns["sum_disc"][i]) / c, count_order=int(c))
+        out.append(row)
+    return sorted(out, key=lambda x: (x["l_returnflag"], x["l_linestatus"]))
+
+
+class _EqJoin(JoinComp):
+    """N-way equi-join: ``keys`` = [(i, att_i, j, att_j), ...] ANDed; ``proj(*batches)`` builds the
+    output batch (vectorised)."""
+
+    def __init__(self, n: int, keys, proj):
+        super().__init__(n)
+        self.keys, self.proj = keys, proj
+
+    def get_selection(self, *ins):
+        pred = None
+        for i, ai, j, aj in self.keys:
+            e = make_lambda_from_member(ins[i], ai) == make_lambda_from_member(ins[j], aj)
+            pred = e if pred is None else (pred & e)
+        return pred
+
+    def get_projection(self, *ins):
+        return make_batch_lambda(*ins, self.proj)
+
+
+def _pick(prefix_cols):
+    """Projection merging chosen columns of the joined inputs into one batch."""
+
+    def proj(*bs):
+        cols = {}
+        for b, names in zip(bs, prefix_cols):
+            for nm in names:
+                cols[nm] = b.columns[nm]
+        n = bs[0].n
+        return RecordBatch(cols, n)
+
+    return proj
+
+
+def q03(client, db: str, segment: str = "BUILDING", date: int = 19950315, k: int = 10) -> List[dict]:
+    """Shipping priority (Query03.h): customer ⋈ orders ⋈ lineitem, revenue by (orderkey, orderdate,
+    shippriority), top-10 by revenue."""
+    cs = _Filter(lambda b: _isin_str(_col(b, "c_mktsegment"), [segment], _dev(b))).set_input(ScanSet(db, "customer", Customer))
+    os_ = _Filter(lambda b: _col(b, "o_orderdate") < date).set_input(ScanSet(db, "orders", Order))
+    ls = _Filter(lambda b: _col(b, "l_shipdate") > date).set_input(ScanSet(db, "lineitem", LineItem))
+    j = _EqJoin(3, [(0, "c_custkey", 1, "o_custkey"), (1, "o_orderkey", 2, "l_orderkey")],
+                _pick([[], ["o_orderdate", "o_shippriority"], ["l_orderkey", "l_extendedprice", "l_discount"]]))
+    j.set_input(0, cs)
+    j.set_input(1, os_)
+    j.set_input(2, ls)
+    agg = _GroupBy(lambda b: (_col(b, "l_orderkey"), _col(b, "o_orderdate"), _col(b, "o_shippriority")),
+                   lambda b: (_col(b, "l_extendedprice").double() * (1 - _col(b, "l_discount").double())).unsqueeze(1),
+                   _rows_out(["revenue"]))
+    r = _flat(_run(client, db, "q03_out", agg.set_input(j), "tpch_q03"))
+    if r is None:
+        return []
+    rows = [{"l_orderkey": int(a), "o_orderdate": int(b_), "o_shippriority": int(c), "revenue": float(v)}
+            for a, b_, c, v in zip(_as_list(r.columns["k0"]), _as_list(r.columns["k1"]), _as_list(r.columns["k2"]),
+                                   _as_list(r.columns["revenue"]))]
+    rows.sort(key=lambda x: (-x["revenue"], x["o_orderdate"], x["l_orderkey"]))
+    return rows[:k]
+
+
+def q04(client, db: str, date: int = 19930701) -> List[dict]:
+    """Order priority checking (Query04.h): orders in [date, date+3mo) having a late lineitem."""
+    end = date + 300 if date % 10000 < 1000 else date + 10000 - 900   # +3 months on yyyymmdd
+    late = _Filter(lambda b: _col(b, "l_commitdate") < _col(b, "l_receiptdate")).set_input(ScanSet(db, "lineitem", LineItem))
+    # EXISTS -> distinct late orderkeys (aggregate), then join with the orders of the quarter
+    dist = _GroupBy(lambda b: _col(b, "l_orderkey"), lambda b: torch.ones(b.n, 1, dtype=torch.float64, device=_dev(b)),
+                    _rows_out(["n"]))
+    os_ = _Filter(lambda b: (_col(b, "o_orderdate") >= date) & (_col(b, "o_orderdate") < end)).set_input(
+        ScanSet(db, "orders", Order))
+    j = _EqJoin(2, [(0, "o_orderkey", 1, "k0")], _pick([["o_orderpriority"], []]))
+    j.set_input(0, os_)
+    j.set_input(1, dist.set_input(late))
+    cnt = _GroupBy(lambda b: list(_col(b, "o_orderpriority")),
+                   lambda b: torch.ones(b.n, 1, dtype=torch.float64, device=_dev(b)), _rows_out(["order_count"]))
+    r = _flat(_run(client, db, "q04_out", cnt.set_input(j), "tpch_q04"))
+    if r is None:
+        return []
+    return sorted(({"o_orderpriority": p, "order_count": int(c)} for p, c in
+                   zip(_as_list(r.columns["k0"]), _as_list(r.columns["order_count"]))), key=lambda x: x["o_orderpriority"])
+
+
+def q06(client, db: str, date: int = 19940101, discount: float = 0.06, quantity: float = 24) -> float:
+    """Forecasting revenue change (Query06.h): one global sum."""
+    lo, hi = discount - 0.01 - 1e-9, discount + 0.01 + 1e-9
+
+    def pred(b):
+        d, s, q = _col(b, "l_discount"), _col(b, "l_shipdate"), _col(b, "l_quantity")
+        return (s >= date) & (s < date + 10000) & (d >= lo) & (d <= hi) & (q < quantity)
+
+    sel = _Filter(pred).set_input(ScanSet(db, "lineitem", LineItem))
+    agg = _GroupBy(lambda b: torch.zeros(b.n, dtype=torch.int64, device=_dev(b)),
+                   lambda b: (_col(b, "l_extendedprice").double() * _col(b, "l_discount").double()).unsqueeze(1),
+                   _rows_out(["revenue"]))
+    r = _flat(_run(client, db, "q06_out", agg.set_input(sel), "tpch_q06"))
+    return 0.0 if r is None else float(r.columns["revenue"].sum())
+
+
+def q12(client, db: str, modes=("MAIL", "SHIP"), date: int = 19940101) -> List[dict]:
+    """Shipping modes and order priority (Query12.h): lineitem ⋈ orders, high/low priority counts."""
+
+    def pred(b):
+        c, r, s = _col(b, "l_commitdate"), _col(b, "l_receiptdate"), _col(b, "l_shipdate")
+        return _isin_str(_col(b, "l_shipmode"), modes, _dev(b)) & (c < r) & (s < c) & (r >= date) & (r < date + 10000)
+
+    ls = _Filter(pred).set_input(ScanSet(db, "lineitem", LineItem))
+    j = _EqJoin(2, [(0, "o_orderkey", 1, "l_orderkey")], _pick([["o_orderpriority"], ["l_shipmode"]]))
+    j.set_input(0, ScanSet(db, "orders", Order))
+    j.set_input(1, ls)
+
+    def vals(b):
+        hi = _isin_str(_col(b, "o_orderpriority"), ["1-URGENT", "2-HIGH"], _dev(b)).double()
+        return torch.stack([hi, 1 - hi], 1)
+
+    agg = _GroupBy(lambda b: list(_col(b, "l_shipmode")), vals, _rows_out(["high_line_count", "low_line_count"]))
+    r = _flat(_run(client, db, "q12_out", agg.set_input(j), "tpch_q12"))
+    if r is None:
+        return []
+    return sorted(({"l_shipmode": m, "high_line_count": int(h), "low_line_count": int(lo_)} for m, h, lo_ in
+                   zip(_as_list(r.columns["k0"]), _as_list(r.columns["high_line_count"]),
+                       _as_list(r.columns["low_line_count"]))), key=lambda x: x["l_shipmode"])
+
+
+def q13(client, db: str, w1: str = "special", w2: str = "requests") -> List[dict]:
+    """Customer distribution (Query13.h): orders per customer (LEFT OUTER JOIN -> customers with none
+    counted via the customer cardinality), then customers per order-count."""
+    import re
+
+    pat = re.compile(f".*{w1}.*{w2}.*")
+    os_ = _Filter(lambda b: ~_strmask(_col(b, "o_comment"), pat.match, _dev(b))).set_input(ScanSet(db, "orders", Order))
+    per_c = _GroupBy(lambda b: _col(b, "o_custkey"), lambda b: torch.ones(b.n, 1, dtype=torch.float64, device=_dev(b)),
+                     _rows_out(["c_count"]))
+    dist = _GroupBy(lambda b: _col(b, "c_count").long(),
+                    lambda b: torch.ones(b.n, 1, dtype=torch.float64, device=_dev(b)), _rows_out(["custdist"]))
+    r = _flat(_run(client, db, "q13_out", dist.set_input(per_c.set_input(os_)), "tpch_q13"))
+    ncust = _count(client, db, "customer")
+    rows = {} if r is None else {int(k): int(v) for k, v in zip(_as_list(r.columns["k0"]), _as_list(r.columns["custdist"]))}
+    with_orders = sum(rows.values())
+    if ncust - with_orders > 0:
+        rows[0] = rows.get(0, 0) + ncust - with_orders
+    out = [{"c_count": k, "custdist": v} for k, v in rows.items()]
+    return sorted(out, key=lambda x: (-x["custdist"], -x["c_count"]))
+
+
+def _count(client, db: str, name: str) -> int:
+    return sum(b.n for b in client.get_set_batches(db, name, gather=True))
+
+
+def q14(client, db: str, date: int = 19950901) -> float:
+    """Promotion effect (Query14.h): lineitem ⋈ part, 100 * promo revenue / revenue."""
+    end = date + 100 if date % 10000 < 1201 else date + 10000 - 1100
+    ls = _Filter(lambda b: (_col(b, "l_shipdate") >= date) & (_col(b, "l_shipdate") < end)).set_input(
+        ScanSet(db, "lineitem", LineItem))
+    j = _EqJoin(2, [(0, "l_partkey", 1, "p_partkey")], _pick([["l_extendedprice", "l_discount"], ["p_type"]]))
+    j.set_input(0, ls)
+    j.set_input(1, ScanSet(db, "part", Part))
+
+    def vals(b):
+        rev = _col(b, "l_extendedprice").double() * (1 - _col(b, "l_discount").double())
+        promo = _strmask(_col(b, "p_type"), lambda s: s.startswith("PROMO"), _dev(b)).double()
+        return torch.stack([rev * promo, rev], 1)
+
+    agg = _GroupBy(lambda b: torch.zeros(b.n, dtype=torch.int64, device=_dev(b)), vals, _rows_out(["promo", "total"]))
+    r = _flat(_run(client, db, "q14_out", agg.set_input(j), "tpch_q14"))
+    if r is None:
+        return 0.0
+    return 100.0 * float(r.columns["promo"].sum()) / max(float(r.columns["total"].sum()), 1e-30)
+
+
+def q17(client, db: str, brand: str = "Brand#23", container: str = "MED BOX") -> float:
+    """Small-quantity-order revenue (Query17.h): per-part average quantity, then lineitems of the
+    brand/container parts under 0.2 x that average; sum(extendedprice) / 7."""
+    ps = _Filter(lambda b: _isin_str(_col(b, "p_brand"), [brand], _dev(b)) &
+                 _isin_str(_col(b, "p_container"), [container], _dev(b))).set_input(ScanSet(db, "part", Part))
+    j = _EqJoin(2, [(0, "l_partkey", 1, "p_partkey")], _pick([["l_partkey", "l_quantity", "l_extendedprice"], []]))
+    j.set_input(0, ScanSet(db, "lineitem", LineItem))
+    j.set_input(1, ps)
+    # job 1: the qualifying lineitems; job 2 (same plan shape as the reference): avg per part + filter
+    if client.storage.has_set(db, "q17_li"):
+        client.remove_set(db, "q17_li")
+    client.create_set(db, "q17_li", None)
+    client.execute_computations(WriteSet(db, "q17_li").set_input(j), job_name="tpch_q17_join")
+    avg = _GroupBy(lambda b: _col(b, "l_partkey"),
+                   lambda b: torch.stack([_col(b, "l_quantity").double(), torch.ones(b.n, dtype=torch.float64,
+                                                                                      device=_dev(b))], 1),
+                   _rows_out(["sq", "n"]))
+    li = ScanSet(db, "q17_li")
+    a = avg.set_input(li)
+    j2 = _EqJoin(2, [(0, "l_partkey", 1, "k0")], _pick([["l_quantity", "l_extendedprice"], ["sq", "n"]]))
+    j2.set_input(0, ScanSet(db, "q17_li"))
+    j2.set_input(1, a)
+    small = _Filter(lambda b: _col(b, "l_quantity") < 0.2 * _col(b, "sq") / _col(b, "n")).set_input(j2)
+    tot = _GroupBy(lambda b: torch.zeros(b.n, dtype=torch.int64, device=_dev(b)),
+                   lambda b: _col(b, "l_extendedprice").double().unsqueeze(1), _rows_out(["s"]))
+    r = _flat(_run(client, db, "q17_out", tot.set_input(small), "tpch_q17"))
+    return 0.0 if r is None else float(r.columns["s"].sum()) / 7.0
+
+
+def q22(client, db: str, codes=("13", "31", "23", "29", "30", "18", "17")) -> List[dict]:
+    """Global sales opportunity (Query22.h): customers of the country codes with above-average positive
+    balance and no orders; count and balance by code."""
+    cset = list(codes)
+
+    def in_codes(b):
+        return _strmask(_col(b, "c_phone"), lambda s: s[:2] in cset, _dev(b))
+
+    pos = _Filter(lambda b: in_codes(b) & (_col(b, "c_acctbal") > 0)).set_input(ScanSet(db, "customer", Customer))
+    avg = _GroupBy(lambda b: torch.zeros(b.n, dtype=torch.int64, device=_dev(b)),
+                   lambda b: torch.stack([_col(b, "c_acctbal").double(), torch.ones(b.n, dtype=torch.float64,
+                                                                                    device=_dev(b))], 1),
+                   _rows_out(["s", "n"]))
+    r = _flat(_run(client, db, "q22_avg", avg.set_input(pos), "tpch_q22_avg"))
+    mean = float(r.columns["s"].sum() / r.columns["n"].sum()) if r is not None else 0.0
+    # NOT EXISTS orders: distinct custkeys with orders (aggregate), used as a broadcast anti-join set
+    has = _GroupBy(lambda b: _col(b, "o_custkey"), lambda b: torch.ones(b.n, 1, dtype=torch.float64, device=_dev(b)),
+                   _rows_out(["n"]))
+    h = _flat(_run(client, db, "q22_has", has.set_input(ScanSet(db, "orders", Order)), "tpch_q22_orders"))
+    with_orders = h.columns["k0"] if h is not None else torch.zeros(0, dtype=torch.int64)
+
+    def pred(b):
+        ck = _col(b, "c_custkey")
+        return in_codes(b) & (_col(b, "c_acctbal") > mean) & ~torch.isin(ck, with_orders.to(ck.device))
+
+    sel = _Filter(pred).set_input(ScanSet(db, "customer", Customer))
+    agg = _GroupBy(lambda b: [s[:2] for s in _col(b, "c_phone")],
+                   lambda b: torch.stack([torch.ones(b.n, dtype=torch.float64, device=_dev(b)),
+                                          _col(b, "c_acctbal").double()], 1), _rows_out(["numcust", "totacctbal"]))
+    r = _flat(_run(client, db, "q22_out", agg.set_input(sel), "tpch_q22"))
+    if r is None:
+        return []
+    return sorted(({"cntrycode": c, "numcust": int(n), "totacctbal": float(t)} for c, n, t in
+                   zip(_as_list(r.columns["k0"]), _as_list(r.columns["numcust"]), _as_list(r.columns["totacctbal"]))),
+                  key=lambda x: x["cntrycode"])
+
+
+def q02(client, db: str, size: int = 15, type_suffix: str = "BRASS", region: str = "EUROPE", k: int = 100) -> List[dict]:
+    """Minimum cost supplier (Query02.h): part ⋈ partsupp ⋈ supplier ⋈ nation ⋈ region, min supply
+    cost per part (aggregate), joined back to keep the suppliers at that minimum; top 100."""
+    ps_ = _Filter(lambda b: (_col(b, "p_size") == size) &
+                  _strmask(_col(b, "p_type"), lambda s: s.endswith(type_suffix), _dev(b))).set_input(ScanSet(db, "part", Part))
+    rs = _Filter(lambda b: _isin_str(_col(b, "r_name"), [region], _dev(b))).set_input(ScanSet(db, "region", Region))
+    j = _EqJoin(5, [(0, "p_partkey", 1, "ps_partkey"), (1, "ps_suppkey", 2, "s_suppkey"),
+                    (2, "s_nationkey", 3, "n_nationkey"), (3, "n_regionkey", 4, "r_regionkey")],
+                _pick([["p_partkey", "p_mfgr"], ["ps_supplycost"], ["s_acctbal", "s_name", "s_address", "s_phone",
+                                                                    "s_comment"], ["n_name"], []]))
+    j.set_input(0, ps_)
+    j.set_input(1, ScanSet(db, "partsupp", PartSupp))
+    j.set_input(2, ScanSet(db, "supplier", Supplier))
+    j.set_input(3, ScanSet(db, "nation", Nation))
+    j.set_input(4, rs)
+    if client.storage.has_set(db, "q02_cand"):
+        client.remove_set(db, "q02_cand")
+    client.create_set(db, "q02_cand", None)
+    client.execute_computations(WriteSet(db, "q02_cand").set_input(j), job_name="tpch_q02_join")
+    mn = _GroupBy(lambda b: _col(b, "p_partkey"), lambda b: _col(b, "ps_supplycost").double().unsqueeze(1),
+                  _rows_out(["mincost"]), reduce_op="min")
+    j2 = _EqJoin(2, [(0, "p_partkey", 1, "k0")],
+                 _pick([["p_partkey", "p_mfgr", "ps_supplycost", "s_acctbal", "s_name", "s_address", "s_phone",
+                         "s_comment", "n_name"], ["mincost"]]))
+    j2.set_input(0, ScanSet(db, "q02_cand"))
+    j2.set_input(1, mn.set_input(ScanSet(db, "q02_cand")))
+    best = _Filter(lambda b: _col(b, "ps_supplycost") == _col(b, "mincost")).set_input(j2)
+    if client.storage.has_set(db, "q02_out"):
+        client.remove_set(db, "q02_out")
+    client.create_set(db, "q02_out", None)
+    client.execute_computations(WriteSet(db, "q02_out").set_input(best), job_name="tpch_q02")
+    got = _collect(client, db, "q02_out")
+    if not got:
+        return []
+    b = RecordBatch.concat(got)
+    b = _flat(b)
+    rows = [{"s_acctbal": float(a), "s_name": s, "n_name": n, "p_partkey": int(p), "p_mfgr": m}
+            for a, s, n, p, m in zip(_as_list(b.columns["s_acctbal"]), _as_list(b.columns["s_name"]),
+                                     _as_list(b.columns["n_name"]), _as_list(b.columns["p_partkey"]),
+                                     _as_list(b.columns["p_mfgr"]))]
+    rows.sort(key=lambda x: (-x["s_acctbal"], x["n_name"], x["s_name"], x["p_partkey"]))
+    return rows[:k]
+
+
+QUERIES = {"q01": q01, "q02": q02, "q03": q03, "q04": q04, "q06": q06, "q12": q12, "q13": q13, "q14": q14,
+           "q17": q17, "q22": q22}
+
+
+# ------------------------------------------------------------------ pandas references (tests)
+def frames(tables):
+    import pandas as pd
+
+    return {k: pd.DataFrame({c: (np.asarray(v) if not isinstance(v, list) else v) for c, v in t.items()})
+            for k, t in tables.items()}
+
+
+def reference(name: str, tables, **kw):
+    """The same query in pandas over the generated tables (test oracle)."""
+    f = frames(tables)
+    li, o, c, p = f["lineitem"], f["orders"], f["customer"], f["part"]
+    if name == "q01":
+        cut = add_days(19981201, -kw.get("delta_days", 90))
+        x = li[li.l_shipdate <= cut].copy()
+        x["dp"] = x.l_extendedprice * (1 - x.l_discount)
+        x["ch"] = x.dp * (1 + x.l_tax)
+        g = x.groupby(["l_returnflag", "l_linestatus"])
+        r = g.agg(sum_qty=("l_quantity", "sum"), sum_base_price=("l_extendedprice", "sum"), sum_disc_price=("dp", "sum"),
+                  sum_charge=("ch", "sum"), avg_qty=("l_quantity", "mean"), avg_price=("l_extendedprice", "mean"),
+                  avg_disc=("l_discount", "mean"), count_order=("l_quantity", "size")).reset_index()
+        return r.to_dict("records")
+    if name == "q03":
+        d = kw.get("date", 19950315)
+        x = c[c.c_mktsegment == kw.get("segment", "BUILDING")].merge(o[o.o_orderdate < d], left_on="c_custkey",
+                                                                      right_on="o_custkey")
+        x = x.merge(li[li.l_shipdate > d], left_on="o_orderkey", right_on="l_orderkey")
+        x["revenue"] = x.l_extendedprice * (1 - x.l_discount)
+        r = x.groupby(["l_orderkey", "o_orderdate", "o_shippriority"]).revenue.sum().reset_index()
+        r = r.sort_values(["revenue", "o_orderdate", "l_orderkey"], ascending=[False, True, True]).head(kw.get("k", 10))
+        return r.to_dict("records")
+    if name == "q04":
+        d = kw.get("date", 19930701)
+        end = d + 300 if d % 10000 < 1000 else d + 10000 - 900
+        late = set(li[li.l_commitdate < li.l_receiptdate].l_orderkey)
+        x = o[(o.o_orderdate >= d) & (o.o_orderdate < end) & o.o_orderkey.isin(late)]
+        return x.groupby("o_orderpriority").size().rename("order_count").reset_index().to_dict("records")
+    if name == "q06":
+        d, disc, q = kw.get("date", 19940101), kw.get("discount", 0.06), kw.get("quantity", 24)
+        x = li[(li.l_shipdate >= d) & (li.l_shipdate < d + 10000) & (li.l_discount >= disc - 0.01 - 1e-9) &
+               (li.l_discount <= disc + 0.01 + 1e-9) & (li.l_quantity < q)]
+        return float((x.l_extendedprice * x.l_discount).sum())
+    if name == "q12":
+        d, modes = kw.get("date", 19940101), kw.get("modes", ("MAIL", "SHIP"))
+        x = li[li.l_shipmode.isin(modes) & (li.l_commitdate < li.l_receiptdate) & (li.l_shipdate < li.l_commitdate) &
+               (li.l_receiptdate >= d) & (li.l_receiptdate < d + 10000)].merge(o, left_on="l_orderkey", right_on="o_orderkey")
+        hi = x.o_orderpriority.isin(["1-URGENT", "2-HIGH"])
+        x = x.assign(h=hi.astype(int), lo=(~hi).astype(int))
+        r = x.groupby("l_shipmode").agg(high_line_count=("h", "sum"), low_line_count=("lo", "sum")).reset_index()
+        return r.to_dict("records")
+    if name == "q13":
+        oo = o[~o.o_comment.str.match(".*special.*requests.*")]
+        cnt = oo.groupby("o_custkey").size()
+        per = c.c_custkey.map(cnt).fillna(0).astype(int)
+        r = per.value_counts().rename_axis("c_count").rename("custdist").reset_index()
+        return sorted(r.to_dict("records"), key=lambda x: (-x["custdist"], -x["c_count"]))
+    if name == "q14":
+        d = kw.get("date", 19950901)
+        end = d + 100 if d % 10000 < 1201 else d + 10000 - 1100
+        x = li[(li.l_shipdate >= d) & (li.l_shipdate < end)].merge(p, left_on="l_partkey", right_on="p_partkey")
+        rev = x.l_extendedprice * (1 - x.l_discount)
+        return float(100.0 * rev[x.p_type.str.startswith("PROMO")].sum() / rev.sum())
+    if name == "q17":
+        pp = p[(p.p_brand == kw.get("brand", "Brand#23")) & (p.p_container == kw.get("container", "MED BOX"))]
+        x = li.merge(pp, left_on="l_partkey", right_on="p_partkey")
+        avg = x.groupby("l_partkey").l_quantity.mean()
+        x = x[x.l_quantity < 0.2 * x.l_partkey.map(avg)]
+        return float(x.l_extendedprice.sum() / 7.0)
+    if name == "q22":
+        codes = list(kw.get("codes", ("13", "31", "23", "29", "30", "18", "17")))
+        cc = c.assign(code=c.c_phone.str[:2])
+        cc = cc[cc.code.isin(codes)]
+        mean = cc[cc.c_acctbal > 0].c_acctbal.mean()
+        x = cc[(cc.c_acctbal > mean) & ~cc.c_custkey.isin(set(o.o_custkey))]
+        r = x.groupby("code").agg(numcust=("c_custkey", "size"), totacctbal=("c_acctbal", "sum")).reset_index()
+        return r.rename(columns={"code": "cntrycode"}).to_dict("records")
+    if name == "q02":
+        s, n, r_, ps = f["supplier"], f["nation"], f["region"], f["partsupp"]
+        pp = p[(p.p_size == kw.get("size", 15)) & p.p_type.str.endswith(kw.get("type_suffix", "BRASS"))]
+        x = pp.merge(ps, left_on="p_partkey", right_on="ps_partkey").merge(s, left_on="ps_suppkey", right_on="s_suppkey")
+        x = x.merge(n, left_on="s_nationkey", right_on="n_nationkey").merge(r_[r_.r_name == kw.get("region", "EUROPE")],
+                                                                           left_on="n_regionkey", right_on="r_regionkey")
+        mn = x.groupby("p_partkey").ps_supplycost.transform("min")
+        x = x[x.ps_supplycost == mn]
+        x = x.sort_values(["s_acctbal", "n_name", "s_name", "p_partkey"], ascending=[False, True, True, True])
+        return x[["s_acctbal", "s_name", "n_name", "p_partkey", "p_mfgr"]].head(kw.get("k", 100)).to_dict("records")
+    raise KeyError(name)

@@ -63,6 +63,22 @@ def registered_types() -> Dict[str, type]:
     return dict(_REGISTRY)
 
 
+_BUILTIN_ANN = {"int": int, "float": float, "str": str, "bool": bool, "bytes": bytes, "object": object}
+
+
+def _resolve_annotation(ann: str, cls):
+    if ann in _BUILTIN_ANN:
+        return _BUILTIN_ANN[ann]
+    import sys
+
+    scope = dict(vars(sys.modules.get(cls.__module__, object())))
+    scope.update(vars(cls))
+    try:
+        return eval(ann, scope)  # noqa: S307 - class annotations of in-process types only
+    except Exception:
+        return object
+
+
 class PDBObject:
     """Base class of every storable type. Subclasses declare fields via annotations."""
 
@@ -76,6 +92,8 @@ class PDBObject:
         for name, ann in cls.__dict__.get("__annotations__", {}).items():
             if name.startswith("_"):
                 continue
+            if isinstance(ann, str):           # postponed annotations (from __future__ import annotations)
+                ann = _resolve_annotation(ann, cls)
             fields[name] = cls.__dict__.get(name, None) if isinstance(cls.__dict__.get(name), (Tensor, Vector)) \
                 else ann
         cls.__fields__ = fields

@@ -51,7 +51,7 @@ def main():
         from netsdb_amd import _ext
 
         cfg_ms = {}
-        for cfg in (0, 1):
+        for cfg in (0, 1, 2):
             _ext.hip().gemm_force_config(cfg)
             cfg_ms[cfg] = timeit(lambda: ops.gemm_nt(A, B))
         _ext.hip().gemm_force_config(-1)
@@ -60,6 +60,7 @@ def main():
         fl = 2.0 * M * N * Kp
         r = dict(op="gemm_nt", shape=name, M=M, N=N, K=Kp, ms=t_ours, tflops=fl / t_ours / 1e9,
                  tile128_tflops=fl / cfg_ms[0] / 1e9, tile256_tflops=fl / cfg_ms[1] / 1e9,
+                 tile256_8ph_tflops=fl / cfg_ms[2] / 1e9,
                  lib_ms=t_lib, lib_tflops=fl / t_lib / 1e9, splits=ops.gemm_splits(M, N, Kp))
         print(json.dumps(r), flush=True)
         res.append(r)

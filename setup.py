@@ -2,7 +2,7 @@
 
     PYTORCH_ROCM_ARCH=gfx950 python setup.py build_ext --inplace
 
-Two extensions:
+Two extensions (both compiled directly with hipcc / the host C++ compiler — no source translation):
   * netsdb_amd._hip_kernels — CDNA4 HIP kernels (MFMA block GEMM, fused implicit-GEMM conv2d,
     row softmax, bias/act, LSTM cell, embedding bag) + PyTorch bindings.
   * netsdb_amd._native      — host C++ runtime (page pool / buffer manager, partitioned page
@@ -20,19 +20,67 @@ KDIR = os.path.join("netsdb_amd", "csrc", "kernels")
 RDIR = os.path.join("netsdb_amd", "csrc", "runtime")
 
 
-def hip_ext():
-    from torch.utils.cpp_extension import CUDAExtension
+HIP_SOURCES = ("gemm.hip", "conv2d.hip", "rowops.hip")
 
-    srcs = [os.path.join(KDIR, f) for f in ("bindings.cpp", "gemm.hip", "conv2d.hip", "rowops.hip")]
-    return CUDAExtension(
-        name="netsdb_amd._hip_kernels",
-        sources=srcs,
-        include_dirs=[os.path.join(ROOT, KDIR)],
-        extra_compile_args={
-            "cxx": ["-O3", "-std=c++17"],
-            "nvcc": ["-O3", "-std=c++17", "--offload-arch=gfx950", "-fno-gpu-rdc", "-munsafe-fp-atomics"],
-        },
-    )
+
+def hip_ext():
+    """The kernel extension is compiled by :class:`HipBuildExt` with hipcc directly (gfx950 code
+    objects, no source translation step); ``sources`` only lists the files for dependency tracking."""
+    from setuptools import Extension
+
+    srcs = [os.path.join(KDIR, f) for f in ("bindings.cpp",) + HIP_SOURCES]
+    return Extension(name="netsdb_amd._hip_kernels", sources=srcs)
+
+
+def _torch_flags():
+    import sysconfig
+
+    import torch
+    from torch.utils.cpp_extension import include_paths, library_paths
+
+    inc = [f"-I{p}" for p in include_paths()] + [f"-I{sysconfig.get_paths()['include']}", f"-I{os.path.join(ROOT, KDIR)}"]
+    defs = ["-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DTORCH_API_INCLUDE_EXTENSION_H",
+            "-DTORCH_EXTENSION_NAME=_hip_kernels", f"-D_GLIBCXX_USE_CXX11_ABI={int(torch._C._GLIBCXX_USE_CXX11_ABI)}"]
+    libdirs = library_paths()
+    libs = [f"-L{d}" for d in libdirs] + [f"-Wl,-rpath,{d}" for d in libdirs] + [
+        "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip"]
+    return inc, defs, libs
+
+
+def build_hip_extension(out_path: str, build_dir: str, jobs: int = 8):
+    """hipcc every kernel TU for gfx950 (parallel), the bindings TU as host C++, then link."""
+    import subprocess
+    from concurrent.futures import ThreadPoolExecutor
+
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    hipcc = os.path.join(rocm, "bin", "hipcc")
+    arch = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+    inc, defs, libs = _torch_flags()
+    os.makedirs(build_dir, exist_ok=True)
+    common = ["-O3", "-std=c++17", "-fPIC"] + defs + inc
+    cmds, objs = [], []
+    for f in ("bindings.cpp",) + HIP_SOURCES:
+        src = os.path.join(ROOT, KDIR, f)
+        obj = os.path.join(build_dir, f + ".o")
+        objs.append(obj)
+        hdrs = [os.path.join(ROOT, KDIR, h) for h in os.listdir(os.path.join(ROOT, KDIR)) if h.endswith(".h")]
+        if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(x) for x in [src] + hdrs):
+            continue
+        if f.endswith(".hip"):
+            cmds.append([hipcc, "-x", "hip", f"--offload-arch={arch}", "-fno-gpu-rdc", "-munsafe-fp-atomics"]
+                        + common + ["-c", src, "-o", obj])
+        else:
+            cmds.append([hipcc, "-x", "c++"] + common + [f"-I{rocm}/include", "-c", src, "-o", obj])
+
+    def run(c):
+        print(" ".join(c[:3] + [c[-3]]), flush=True)
+        subprocess.run(c, check=True)
+
+    with ThreadPoolExecutor(max(1, min(jobs, len(cmds) or 1))) as ex:
+        list(ex.map(run, cmds))
+    os.makedirs(os.path.dirname(out_path), exist_ok=True)
+    subprocess.run([hipcc, "-shared", "-fPIC", f"--offload-arch={arch}", "-o", out_path] + objs + libs
+                   + [f"-L{rocm}/lib", "-lamdhip64"], check=True)
 
 
 def native_ext():
@@ -50,9 +98,21 @@ def native_ext():
     )
 
 
-def main():
-    from torch.utils.cpp_extension import BuildExtension
+def _build_ext_cls():
+    from setuptools.command.build_ext import build_ext
 
+    class HipBuildExt(build_ext):
+        def build_extension(self, ext):
+            if ext.name == "netsdb_amd._hip_kernels":
+                build_hip_extension(self.get_ext_fullpath(ext.name), os.path.join(self.build_temp, "hip"),
+                                    int(os.environ.get("MAX_JOBS", "8")))
+            else:
+                super().build_extension(ext)
+
+    return HipBuildExt
+
+
+def main():
     which = os.environ.get("NSDB_BUILD", "all")
     exts = []
     if which in ("all", "native"):
@@ -64,7 +124,7 @@ def main():
         version="0.1.0",
         packages=["netsdb_amd"],
         ext_modules=exts,
-        cmdclass={"build_ext": BuildExtension.with_options(use_ninja=True)},
+        cmdclass={"build_ext": _build_ext_cls()},
     )
 
 

@@ -132,3 +132,37 @@ def test_distributed_la_ring_matmul():
     r0, r1 = _run("_la_ring_scenario")
     assert r0["err"] < 1e-4 and r1["err"] < 1e-4
     assert any("matmul" in f for f in r0["fused"])
+
+
+def _tpch_scenario(ctx, out_dir):
+    from netsdb_amd.client import PDBClient
+    from netsdb_amd.models import tpch
+
+    t = tpch.generate(0.002, seed=3)
+    c = PDBClient(ctx=ctx, root=tempfile.mkdtemp(), broadcast_threshold=0)   # force hash-partitioned joins
+    tpch.load(c, "tpch", t)
+    return {q: tpch.QUERIES[q](c, "tpch") for q in ("q01", "q03", "q06", "q12", "q13", "q22")}
+
+
+def test_distributed_tpch_partitioned():
+    import math
+
+    from netsdb_amd.models import tpch
+
+    t = tpch.generate(0.002, seed=3)
+    res = _run("_tpch_scenario")
+    for q in ("q01", "q03", "q06", "q12", "q13", "q22"):
+        ref = tpch.reference(q, t)
+        for r in res:
+            got = r[q]
+            if isinstance(ref, float):
+                assert math.isclose(got, ref, rel_tol=1e-9), q
+                continue
+            if q in ("q01",):
+                ref = sorted(ref, key=lambda x: (x["l_returnflag"], x["l_linestatus"]))
+            elif q in ("q12", "q22", "q04"):
+                ref = sorted(ref, key=lambda x: x[list(x)[0]])
+            assert len(got) == len(ref), q
+            for g, e in zip(got, ref):
+                for k, v in e.items():
+                    assert (math.isclose(g[k], v, rel_tol=1e-9, abs_tol=1e-6) if isinstance(v, float) else g[k] == v), (q, g, e)

@@ -30,7 +30,7 @@ def test_gemm_identity_asymmetric():
     torch.testing.assert_close(C, B.float().t().contiguous(), rtol=0, atol=0)
 
 
-@pytest.fixture(params=[-1, 0, 1], ids=["auto", "tile128", "tile256"])
+@pytest.fixture(params=[-1, 0, 1, 2], ids=["auto", "tile128", "tile256", "tile256_8ph"])
 def gemm_cfg(request):
     from netsdb_amd import _ext
 
@@ -40,7 +40,7 @@ def gemm_cfg(request):
 
 
 @pytest.mark.parametrize("M,N,K", [(128, 128, 64), (1000, 1000, 4096), (77, 300, 520), (513, 129, 8), (2048, 64, 1024),
-                                   (600, 520, 2056)])
+                                   (600, 520, 2056), (256, 256, 64), (1024, 768, 8192), (300, 1000, 576)])
 @pytest.mark.parametrize("splits", [0, 1, 3])
 def test_gemm_shapes(M, N, K, splits, gemm_cfg):
     torch.manual_seed(0)

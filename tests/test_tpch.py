@@ -1,0 +1,78 @@
+"""TPC-H queries (reference src/tpch Query01..22) through the engine vs a pandas oracle on the same
+generated data (dbgen itself is not available offline: parity with dbgen output is unpinned)."""
+import math
+
+import pytest
+
+from netsdb_amd.client import PDBClient
+from netsdb_amd.models import tpch
+
+
+@pytest.fixture(scope="module")
+def db(tmp_path_factory):
+    t = tpch.generate(0.004, seed=7)
+    c = PDBClient(root=str(tmp_path_factory.mktemp("tpch")))
+    tpch.load(c, "tpch", t)
+    return c, t
+
+
+def _close_rows(got, ref, keys):
+    assert len(got) == len(ref), (got[:3], ref[:3])
+    for g, r in zip(got, ref):
+        for k in keys:
+            if isinstance(r[k], float):
+                assert math.isclose(g[k], r[k], rel_tol=1e-9, abs_tol=1e-6), (k, g, r)
+            else:
+                assert g[k] == r[k], (k, g, r)
+
+
+def test_q01(db):
+    c, t = db
+    ref = sorted(tpch.reference("q01", t), key=lambda x: (x["l_returnflag"], x["l_linestatus"]))
+    _close_rows(tpch.q01(c, "tpch"), ref, list(ref[0]))
+
+
+def test_q03(db):
+    c, t = db
+    ref = tpch.reference("q03", t)
+    assert ref
+    _close_rows(tpch.q03(c, "tpch"), ref, list(ref[0]))
+
+
+def test_q04_q12_q13_q22(db):
+    c, t = db
+    for q in ("q04", "q12", "q22"):
+        ref = tpch.reference(q, t)
+        assert ref, q
+        key = list(ref[0])[0]
+        _close_rows(tpch.QUERIES[q](c, "tpch"), sorted(ref, key=lambda x: x[key]), list(ref[0]))
+    ref = tpch.reference("q13", t)
+    _close_rows(tpch.q13(c, "tpch"), ref, ["c_count", "custdist"])
+
+
+def test_q06_q14(db):
+    c, t = db
+    assert math.isclose(tpch.q06(c, "tpch"), tpch.reference("q06", t), rel_tol=1e-9)
+    assert math.isclose(tpch.q14(c, "tpch"), tpch.reference("q14", t), rel_tol=1e-9)
+
+
+def test_q17(db):
+    c, t = db
+    # pick a brand/container pair present in the data so the query is non-trivial
+    brand, cont = t["part"]["p_brand"][3], t["part"]["p_container"][3]
+    ref = tpch.reference("q17", t, brand=brand, container=cont)
+    assert ref > 0
+    assert math.isclose(tpch.q17(c, "tpch", brand=brand, container=cont), ref, rel_tol=1e-9)
+
+
+def test_q02(db):
+    c, t = db
+    size = int(t["part"]["p_size"][5])
+    suffix = t["part"]["p_type"][5].split()[-1]
+    for region in tpch.REGIONS:
+        ref = tpch.reference("q02", t, size=size, type_suffix=suffix, region=region)
+        if ref:
+            break
+    assert ref
+    got = tpch.q02(c, "tpch", size=size, type_suffix=suffix, region=region)
+    _close_rows(got, ref, ["s_acctbal", "s_name", "n_name", "p_partkey", "p_mfgr"])
