@@ -49,6 +49,21 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, un
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
 
+// Grouped tile walk: each XCD owns a contiguous run of tile ids (xcd_remap); walking them in groups of
+// GROUP_M row-tiles makes the ~32 tiles an XCD runs at once a GROUP_M x 4 block, so every A row-panel is
+// re-read by 4 column tiles and every B panel by GROUP_M row tiles out of that XCD's L2 (instead of one
+// column of tiles pulling every A panel through each XCD).
+constexpr int GROUP_M = 8;
+__device__ __forceinline__ void grouped_tile(int tile, int tiles_m, int tiles_n, int& tm, int& tn) {
+  const int per_group = GROUP_M * tiles_n;
+  const int g = tile / per_group;
+  const int first_m = g * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int r = tile - g * per_group;
+  tm = first_m + r % gsize;
+  tn = r / gsize;
+}
+
 // Stage one ROWSx64 bf16 operand tile with NW waves: ROWS/(8*NW) wave-instructions of 1 KiB per wave.
 template <int ROWS, int NW>
 __device__ __forceinline__ void stage_tile(__amdgpu_buffer_rsrc_t rsrc, char* lds_tile, long long ld,
@@ -149,7 +164,8 @@ gemm_nt_tile_kernel(GemmParams p) {
   const int wg = xcd_remap(blockIdx.x, ntiles * p.splits);
   const int split = wg / ntiles, tile = wg % ntiles;
   // column-major tile walk: consecutive tiles (same XCD after the remap) share the B panel
-  const int tm = tile % p.tiles_m, tn = tile / p.tiles_m;
+  int tm, tn;
+  grouped_tile(tile, p.tiles_m, p.tiles_n, tm, tn);
   const int batch = blockIdx.z;
   const int m0 = tm * TBM, n0 = tn * TBN;
 
@@ -246,7 +262,8 @@ gemm_nt_tile_kernel(GemmParams p) {
 
 // V: diagnostic variants (0 = production). 1 no setprio, 2 stage before ds_reads, 3 no group stagger,
 // 4 no DMA issued (load-free upper bound, wrong results), 5 no ds_reads after the first tile (wrong results),
-// 6 no vmcnt wait in the loop (racy), 7 zero-record descriptors (DMA issued, no memory traffic)
+// 6 no vmcnt wait in the loop (racy), 7 zero-record descriptors (DMA issued, no memory traffic),
+// 8 vmcnt(2) instead of 6 (1 half-tile in flight: latency sensitivity)
 template <int V>
 __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   constexpr int HALF = 128 * 128;            // bytes of one half-tile (128 rows x 64 bf16)
@@ -256,7 +273,8 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   const int ntiles = p.tiles_m * p.tiles_n;
   const int wg = xcd_remap(blockIdx.x, ntiles * p.splits);
   const int split = wg / ntiles, tile = wg % ntiles;
-  const int tm = tile % p.tiles_m, tn = tile / p.tiles_m;
+  int tm, tn;
+  grouped_tile(tile, p.tiles_m, p.tiles_n, tm, tn);
   const int batch = blockIdx.z;
   const int m0 = tm * 256, n0 = tn * 256;
 
@@ -367,7 +385,8 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
     mma(1, 1, b1);
     // j3: quadrant (1,0) from registers; stages B1 of u+2; retires tile u+1 (3 half-tiles stay in flight)
     stage(cur, 3, u + 2);
-    if constexpr (V != 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    if constexpr (V == 8) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if constexpr (V != 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     mma(1, 0, b0);
   };
 
@@ -484,6 +503,8 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
   dim3 grid(p.tiles_m * p.tiles_n * p.splits, 1, batch);
   if (cfg == 2)
     hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<0>, grid, dim3(512), 0, stream, p);
+  else if (cfg == 10)
+    hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<8>, grid, dim3(512), 0, stream, p);
   else if (cfg >= 3 && cfg <= 9) {   // diagnostic variants of the 8-phase kernel (timing only)
     auto kern = cfg == 3 ? nsdb::gemm_nt_256_8ph_kernel<1> : cfg == 4 ? nsdb::gemm_nt_256_8ph_kernel<2>
               : cfg == 5 ? nsdb::gemm_nt_256_8ph_kernel<3> : cfg == 6 ? nsdb::gemm_nt_256_8ph_kernel<4>
