@@ -448,7 +448,7 @@ static int pick_cfg(int M, int N, int K, int batch) {
   const long long big_tiles = (long long)((M + 255) / 256) * ((N + 255) / 256) * batch;
   const bool fills = M >= 192 && N >= 192;
   const long long ksteps = (K + nsdb::BK - 1) / nsdb::BK;
-  return (fills && big_tiles * ksteps >= 256LL * 32) ? 1 : 0;
+  return (fills && big_tiles * ksteps >= 256LL * 32) ? 2 : 0;
 }
 
 void nsdb_gemm_force_config(int cfg) { g_force_cfg = cfg; }
