@@ -34,17 +34,33 @@ from .ff import FFAggMatrix, FFTransposeMult
 
 
 def flatten_kernel(weight: torch.Tensor) -> torch.Tensor:
-    """[OC, C, KH, KW] -> [OC, ldk] in im2col (c, kh, kw) order, zero-padded to a multiple of 8."""
+    """[OC, C, KH, KW] -> [OC, ldk] bf16 in im2col (c, kh, kw) order, zero-padded to a multiple of 8
+    (KernelToChunks/KernelBiasJoin's kernel_flat; built once per weight tensor, then reused)."""
     oc = weight.shape[0]
-    return ops.pad_k(weight.reshape(oc, -1)).contiguous()
+    return ops.derived(weight, "conv_wflat",
+                       lambda w: ops.pad_k(w.reshape(oc, -1).to(torch.bfloat16)).contiguous())
 
 
-def images_batch(data: torch.Tensor, first_key: int = 0) -> RecordBatch:
+_CONST_COLS = {}
+
+
+def _const_col(v: int, n: int, dev) -> torch.Tensor:
+    """A length-n int64 column of value v (slice of a cached device buffer: no kernel per call)."""
+    key = (v, str(dev))
+    buf = _CONST_COLS.get(key)
+    if buf is None or buf.numel() < n:
+        buf = torch.full((max(n, 1024),), v, dtype=torch.int64, device=dev)
+        _CONST_COLS[key] = buf
+    return buf[:n]
+
+
+def images_batch(data: torch.Tensor, first_key: int = 0, keys: Optional[torch.Tensor] = None) -> RecordBatch:
     n, c, h, w = data.shape
     dev = data.device
-    full = lambda v: torch.full((n,), v, dtype=torch.int64, device=dev)  # noqa: E731
-    return RecordBatch({"key": torch.arange(first_key, first_key + n, device=dev), "channels": full(c),
-                        "height": full(h), "width": full(w), "data": data}, n, Image)
+    if keys is None:
+        keys = torch.arange(first_key, first_key + n, device=dev)
+    return RecordBatch({"key": keys, "channels": _const_col(c, n, dev), "height": _const_col(h, n, dev),
+                        "width": _const_col(w, n, dev), "data": data}, n, Image)
 
 
 class Conv2DMemFuse(SelectionComp):
@@ -54,8 +70,8 @@ class Conv2DMemFuse(SelectionComp):
                  dilation: int = 1, act: str = "none", nchw_out: bool = True):
         super().__init__()
         self.kh, self.kw = weight.shape[2], weight.shape[3]
-        self.wflat = flatten_kernel(weight.to(torch.bfloat16))
-        self.bias = bias.float() if bias is not None else None
+        self.wflat = flatten_kernel(weight)
+        self.bias = ops.derived(bias, "bias_f32", lambda t: t.float()) if bias is not None else None
         self.stride, self.padding, self.dilation, self.act, self.nchw_out = stride, padding, dilation, act, nchw_out
 
     def get_selection(self, img):
@@ -70,9 +86,7 @@ class Conv2DMemFuse(SelectionComp):
             bias = self.bias.to(x.device) if self.bias is not None else None
             y = ops.conv2d(x.contiguous(), w, bias, self.kh, self.kw, self.stride, self.padding, self.dilation,
                            ops.act_code(self.act), nchw_out=True)
-            out = images_batch(y)
-            out.columns["key"] = b.columns["key"]
-            return out
+            return images_batch(y, keys=b.columns["key"])
 
         return make_batch_lambda(img, proj, tag="conv2d_igemm")
 

@@ -106,6 +106,30 @@ def gemm_splits(M, N, K, batch=1) -> int:
     return int(_ext.hip().gemm_splits(M, N, K, batch))
 
 
+_DERIVED: "OrderedDict" = None
+
+
+def derived(t: torch.Tensor, tag: str, fn):
+    """Memoise a tensor derived from an unchanged source tensor (model weights / biases converted or
+    re-laid-out once, not on every inference call). Keyed by storage pointer, in-place version
+    counter, shape, dtype and device, so any write to the source invalidates the entry."""
+    global _DERIVED
+    from collections import OrderedDict
+
+    if _DERIVED is None:
+        _DERIVED = OrderedDict()
+    key = (tag, t.data_ptr(), t._version, tuple(t.shape), tuple(t.stride()), t.dtype, str(t.device))
+    hit = _DERIVED.get(key)
+    if hit is not None:
+        _DERIVED.move_to_end(key)
+        return hit[1]
+    val = fn(t)
+    _DERIVED[key] = (t, val)           # keep the source alive so its pointer is not reused
+    if len(_DERIVED) > 256:
+        _DERIVED.popitem(last=False)
+    return val
+
+
 def pad_k(t: torch.Tensor, mult: int = 8) -> torch.Tensor:
     """Zero-pad the last dim to a multiple of ``mult`` (block storage keeps rows 16-B aligned)."""
     k = t.shape[-1]

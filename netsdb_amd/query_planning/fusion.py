@@ -151,7 +151,8 @@ class MatmulNode(Node):
         phys_is_c = self.transpose_out == want_t
         bias_t, mode = None, ops.BIAS_NONE
         if self.bias is not None:
-            bias_t = _replicate(engine, self.bias.eval(engine)).logical().reshape(-1).float().contiguous()
+            bias_t = ops.derived(_replicate(engine, self.bias.eval(engine)).logical(), "bias_f32",
+                                 lambda t: t.reshape(-1).float().contiguous())
             along_c_rows = self.bias_along == "row"
             if opA.part == "rows" and along_c_rows:
                 bias_t = bias_t[opA.offset: opA.offset + M]
@@ -238,7 +239,8 @@ class SoftmaxNode(Node):
             X = self.x.eval(engine)
             if X.part == "cols":
                 X = _replicate(engine, X)
-            phys = X.physical(False)[: X.rows, : X.cols]
+            # row-normalise reads any row stride: no K-padding copy of the [rows, labels] scores
+            phys = X.phys[: X.rows, : X.cols] if not X.transposed else X.logical().contiguous()
             if phys.stride(-1) != 1:
                 phys = phys.contiguous()
             y = ops.row_normalize(phys, out_dtype=torch.float32)
