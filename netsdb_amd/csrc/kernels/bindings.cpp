@@ -15,6 +15,8 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
 int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* out, int N, int C, int H, int W,
                       int OC, int KH, int KW, int stride, int pad, int dil, int ldw, int act, int nchw_out,
                       int out_f32, hipStream_t stream);
+extern int nsdb_conv2d_force_generic;
+extern int nsdb_conv2d_variant;
 int nsdb_im2col(const void* X, void* out, int N, int C, int H, int W, int KH, int KW, int stride, int pad, int dil,
                 int ldk, hipStream_t stream);
 int nsdb_softmax_rows(const void* X, int x_f32, const float* bias, void* Y, int y_f32, int R, int N,
@@ -232,6 +234,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_splits", &gemm_splits);
   m.def("gemm_force_config", [](int64_t cfg) { nsdb_gemm_force_config((int)cfg); },
         "-1 auto, 0 = 128x128 tile, 1 = 256x256 tile (A/B testing)");
+  m.def("conv2d_force_generic", [](int64_t v) { nsdb_conv2d_force_generic = (int)v; },
+        "1: route every conv2d to the generic gather kernel (A/B testing)");
+  m.def("conv2d_variant", [](int64_t v) { nsdb_conv2d_variant = (int)v; }, "row-kernel diagnostic variant");
   m.def("conv2d", &conv2d, py::arg("X"), py::arg("W"), py::arg("bias") = py::none(), py::arg("KH") = 1,
         py::arg("KW") = 1, py::arg("stride") = 1, py::arg("pad") = 0, py::arg("dil") = 1, py::arg("act") = 0,
         py::arg("nchw_out") = false, py::arg("out_f32") = false);

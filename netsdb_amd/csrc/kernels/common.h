@@ -16,12 +16,26 @@ __device__ __forceinline__ float bf16_to_f32(unsigned short h) {
   return __uint_as_float(((unsigned)h) << 16);
 }
 
-// Round-to-nearest-even f32 -> bf16 (NaN kept NaN: see MI355X_MICROARCH correctness table).
+// Round-to-nearest-even f32 -> bf16 with NaN kept NaN: a plain conversion to __bf16 compiles to the
+// hardware v_cvt_pk_bf16_f32 on gfx950 (MI355X_MICROARCH correctness table) — branch-free, unlike an
+// integer-rounding version with a NaN test (a divergent branch per element in unrolled epilogues).
 __device__ __forceinline__ unsigned short f32_to_bf16(float f) {
-  unsigned u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (unsigned short)((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (unsigned short)(u >> 16);
+  const __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(unsigned short, b);
+}
+
+__device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
+  return (unsigned)f32_to_bf16(lo) | ((unsigned)f32_to_bf16(hi) << 16);
+}
+
+// Compile-time activation (kernels templated on ACT: no per-element switch in unrolled epilogues).
+template <int ACT>
+__device__ __forceinline__ float act_t(float v) {
+  if constexpr (ACT == ACT_RELU) return v > 0.f ? v : 0.f;
+  else if constexpr (ACT == ACT_SIGMOID) return 1.f / (1.f + __expf(-v));
+  else if constexpr (ACT == ACT_EXP) return __expf(v);
+  else if constexpr (ACT == ACT_TANH) return tanhf(v);
+  else return v;
 }
 
 __device__ __forceinline__ float apply_act(float v, int act) {

@@ -194,6 +194,286 @@ __global__ void __launch_bounds__(256, 4) conv2d_igemm_kernel(ConvParams p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Row-tiled direct conv for small-C / wide-image layers (the memfuse headline: 3 -> 64, 7x7,
+// stride 1, pad 0 on 112x112). The generic kernel above gathers one bf16 per lane per k (TA-bound:
+// ~2.8M scalar-gather wave instructions for the headline shape). Here:
+//  * a block owns TR=4 consecutive output rows of one image (one per wave) and stages the
+//    C x (TR+KH-1) input rows it needs into LDS ONCE, as 4 copies shifted by 0..3 elements, so the
+//    8 taps (kw = 0..7, KW <= 8 zero-padded) of a (c, kh) filter row at any output column are one
+//    8-byte-aligned pair of ds_read_b64 — the MFMA A fragment comes straight out of LDS;
+//  * K is re-ordered to (c, kh, kw8): k-step = 4 (c, kh) rows x 8 taps = 32 = one
+//    mfma_f32_16x16x32_bf16; the re-ordered filter (4 n-tiles x NKS k-steps) lives in VGPRs for the
+//    whole (persistent) block;
+//  * copy stride 288 B and the 4-copy interleave make a wave's ds_read_b64 bank-conflict free
+//    (16 lanes of one (c,kh) row cover 128 B, the next row is +128 B mod 256);
+//  * the block's [64 oc][4 rows][OW] bf16 output tile is staged through LDS and written as one contiguous run per oc (the 4
+//    output rows of a plane are adjacent in NCHW) with coalesced dword stores — per-lane 8-byte
+//    fragment stores into 64 different planes were the limit of the gather kernel (~1 TB/s).
+// Preconditions (host-checked): stride 1, dil 1, pad 0, KW <= 8, W % 8 == 0, OW <= 112,
+// C*KH <= 4*CVR_NKS, C*(4+KH-1) <= CVR_ROWS.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+constexpr int CVR_TR = 4, CVR_NKS = 6, CVR_CP = 288;                 // rows/block, max k-steps, copy stride (B)
+constexpr int CVR_ROWS = 30;                                           // max (c, r) input rows per group
+constexpr int CVR_ZERO = CVR_ROWS * 4 * CVR_CP;                        // zero block (A source past C*KH)
+constexpr int CVR_BUF = CVR_ZERO + 4 * CVR_CP;
+constexpr int CVR_MAXT = 7;                                            // output tiles of 16 per row (OW <= 112)
+constexpr int CVR_OSTAGE = 32 * CVR_TR * (16 * CVR_MAXT + 4) * 2;      // [TR][32 oc][OWS] bf16 (one half)
+constexpr int CVR_WROW = CVR_NKS * 4 * 16 + 16;                       // staged filter row (B)
+
+struct ConvRowParams {
+  const unsigned short* X;
+  const unsigned short* Wt;
+  const float* bias;
+  void* out;
+  int N, C, H, W, OC, KH, KW, OH, OW, ldw;
+  int rin, ckh, nks, ntiles, chunks, groups_per_img, ngroups;
+  int act, nchw_out, out_f32;
+  int variant;   // diagnostics (bit flags, timing only): 1 no global stores, 2 no MFMA, 4 no LDS output
+                 // staging, 8 prologue only, 16 no compute, 32 s_memtime stamps over the output
+};
+
+template <int ACT>
+__global__ void __launch_bounds__(256, 2) conv2d_rows_kernel(ConvRowParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[CVR_BUF + CVR_OSTAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int oc0 = blockIdx.y * 64;
+
+  // ---- filter -> VGPRs (B fragments in (c*KH+kh, kw8) k order): raw [64][ldw] rows staged into LDS with
+  // independent 16-B loads (<= 6 per thread, all in flight together), then each lane picks its taps
+  {
+    const int cpr = p.ldw / 8, nch = 64 * cpr;
+    uint4 v[6];
+#pragma unroll
+    for (int u = 0; u < 6; ++u) {
+      const int e = tid + u * 256;
+      const int r = e / cpr, ch = e - (e / cpr) * cpr;
+      v[u] = make_uint4(0, 0, 0, 0);
+      if (e < nch && oc0 + r < p.OC) v[u] = *reinterpret_cast<const uint4*>(p.Wt + (long long)(oc0 + r) * p.ldw + ch * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < 6; ++u) {
+      const int e = tid + u * 256;
+      if (e < nch) reinterpret_cast<uint4*>(smem)[e] = v[u];
+    }
+  }
+  __syncthreads();
+  bf16x8 bw[4][CVR_NKS];
+  {
+    const unsigned short* raw = reinterpret_cast<const unsigned short*>(smem);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int ks = 0; ks < CVR_NKS; ++ks) {
+        const int ocl = nt * 16 + (lane & 15), q = ks * 4 + (lane >> 4);
+#pragma unroll
+        for (int kw = 0; kw < 8; ++kw)
+          bw[nt][ks][kw] = (q < p.ckh && kw < p.KW) ? (short)raw[ocl * p.ldw + q * p.KW + kw] : (short)0;
+      }
+  }
+  float bias_v[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const int oc = oc0 + nt * 16 + (lane & 15);
+    bias_v[nt] = (p.bias && oc < p.OC) ? p.bias[oc] : 0.f;
+  }
+  __syncthreads();
+
+  // zero block at the end of both buffers (the A source of k-steps past C*KH)
+  for (int e = tid; e < 4 * CVR_CP / 16; e += 256)
+    reinterpret_cast<uint4*>(smem + CVR_ZERO)[e] = make_uint4(0, 0, 0, 0);
+
+  // per-lane A base offsets for each k-step (relative to a buffer), wave row folded in
+  int abase[CVR_NKS];
+#pragma unroll
+  for (int ks = 0; ks < CVR_NKS; ++ks) {
+    const int q = ks * 4 + (lane >> 4);
+    if (q < p.ckh) {
+      const int c = q / p.KH, kh = q % p.KH;
+      abase[ks] = ((c * p.rin + wave + kh) * 4 + (lane & 3)) * CVR_CP + (lane & 12) * 2;
+    } else {
+      abase[ks] = CVR_ZERO + (lane & 3) * 16 + (lane & 12) * 2;   // inside the zero block
+    }
+  }
+
+  // input staging work items: (c, r, chunk j); each thread handles <= 2 items per group
+  const int items = p.C * p.rin * p.chunks;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned short*>(p.X), (short)0, (int)((long long)p.N * p.C * p.H * p.W * 2), 0x00020000);
+  u32x4 lo[2], hi[2];
+  // branch-free: an invalid chunk gets an out-of-range offset and the buffer range check returns
+  // zeros (a branch around each load makes hipcc wait vmcnt(0) right after it — no prefetch)
+  auto fetch = [&](int g) {
+    const int n = g / p.groups_per_img, oh0 = (g % p.groups_per_img) * CVR_TR;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int it = min(tid + u * 256, items - 1);
+      const int j = it % p.chunks, cr = it / p.chunks, r = cr % p.rin, c = cr / p.rin;
+      const int ih = oh0 + r;
+      const int rowoff = (((n * p.C + c) * p.H + ih) * p.W) * 2;
+      const bool rok = ih < p.H;
+      lo[u] = __builtin_amdgcn_raw_buffer_load_b128(xr, (rok && 8 * j < p.W) ? rowoff + 16 * j : 0x7ffffff0, 0, 0);
+      hi[u] = __builtin_amdgcn_raw_buffer_load_b128(xr, (rok && 8 * (j + 1) < p.W) ? rowoff + 16 * (j + 1) : 0x7ffffff0,
+                                                   0, 0);
+    }
+  };
+  auto store_rows = [&](char* buf) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int it = tid + u * 256;
+      if (it >= items) continue;
+      const int j = it % p.chunks, cr = it / p.chunks;
+      char* row = buf + cr * 4 * CVR_CP + j * 16;
+      const unsigned w[6] = {lo[u].x, lo[u].y, lo[u].z, lo[u].w, hi[u].x, hi[u].y};
+      // shift s (elements) = 2s bytes: copy s holds in[e + s] at entry e
+      *reinterpret_cast<u32x4*>(row) = lo[u];
+      *reinterpret_cast<u32x4*>(row + CVR_CP) =
+          u32x4{__builtin_amdgcn_alignbyte(w[1], w[0], 2), __builtin_amdgcn_alignbyte(w[2], w[1], 2),
+                     __builtin_amdgcn_alignbyte(w[3], w[2], 2), __builtin_amdgcn_alignbyte(w[4], w[3], 2)};
+      *reinterpret_cast<u32x4*>(row + 2 * CVR_CP) = u32x4{w[1], w[2], w[3], w[4]};
+      *reinterpret_cast<u32x4*>(row + 3 * CVR_CP) =
+          u32x4{__builtin_amdgcn_alignbyte(w[2], w[1], 2), __builtin_amdgcn_alignbyte(w[3], w[2], 2),
+                     __builtin_amdgcn_alignbyte(w[4], w[3], 2), __builtin_amdgcn_alignbyte(w[5], w[4], 2)};
+    }
+  };
+
+  const long long OHW = (long long)p.OH * p.OW;
+  unsigned short* ostage = reinterpret_cast<unsigned short*>(smem + CVR_BUF);   // [64 oc][TR rows][OW] bf16
+  const bool staged = p.nchw_out && !p.out_f32 && (p.OW & 1) == 0;
+  // stage layout [row][32 oc][ows], ows = 16*ntiles + 4: the 16 oc rows a ds_write_b64 lane group
+  // touches are 58 dwords apart -> 16 distinct bank pairs (a 112-element stride put all 16 on one bank)
+  const int ows = p.ntiles * 16 + 4;
+  int g = blockIdx.x;
+  if (p.variant & 8) return;          // diagnostics: prologue only
+  // variant 7: s_memtime stamps (diagnostic build: written over the start of the output)
+  unsigned long long st_t0 = 0, st_stage = 0, st_work = 0, st_tmp = 0, st_comp = 0, st_bar = 0;
+  auto stamp = [&]() -> unsigned long long {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+  };
+  if (p.variant & 32) st_t0 = stamp();
+  if (g < p.ngroups) fetch(g);
+  for (; g < p.ngroups; g += gridDim.x) {
+    const int n = g / p.groups_per_img, oh0 = (g % p.groups_per_img) * CVR_TR, oh = oh0 + wave;
+    if (p.variant & 32) st_tmp = stamp();
+    __syncthreads();                                   // previous group's readers of both buffers are done
+    store_rows(smem);
+    __syncthreads();
+    if (p.variant & 32) { const unsigned long long t = stamp(); st_stage += t - st_tmp; st_tmp = t; }
+    if (g + (int)gridDim.x < p.ngroups) fetch(g + gridDim.x);   // next group's rows in flight during compute
+    // two passes over the row, 32 output channels each: the [32 oc][TR][OWS] bf16 stage is 28 KB, so
+    // two blocks fit a CU (the A fragments are re-read from LDS for the second half — cheap)
+    const int rows_valid = min(CVR_TR, p.OH - oh0);
+    const int dwpr = p.OW >> 1;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      if (!staged && half == 1) break;
+      if (oh < p.OH && !(p.variant & 16)) {
+        auto load_a = [&](int t, bf16x8 (&af)[CVR_NKS]) {
+#pragma unroll
+          for (int ks = 0; ks < CVR_NKS; ++ks) {
+            const uint2* a = reinterpret_cast<const uint2*>(__builtin_assume_aligned(smem + abase[ks] + t * 32, 8));
+            const uint2 a0 = a[0], a1 = a[1];
+            af[ks][0] = (short)a0.x; af[ks][1] = (short)(a0.x >> 16); af[ks][2] = (short)a0.y; af[ks][3] = (short)(a0.y >> 16);
+            af[ks][4] = (short)a1.x; af[ks][5] = (short)(a1.x >> 16); af[ks][6] = (short)a1.y; af[ks][7] = (short)(a1.y >> 16);
+          }
+        };
+        for (int t = 0; t < p.ntiles; ++t) {
+          f32x4 acc[4];
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+          bf16x8 af[CVR_NKS];
+          load_a(t, af);
+          // staged: this half's 2 n-tiles; direct: all 4. Even and odd k-steps accumulate into separate
+          // registers (two independent MFMA chains per n-tile, summed after the loop)
+          if (!(p.variant & 2)) {
+            f32x4 acc2[4];
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) acc2[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < CVR_NKS; ++ks)
+#pragma unroll
+              for (int nt = 0; nt < 4; ++nt)
+                if (!staged || (nt >> 1) == half) {
+                  if (ks & 1) acc2[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks], bw[nt][ks], acc2[nt], 0, 0, 0);
+                  else acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks], bw[nt][ks], acc[nt], 0, 0, 0);
+                }
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) acc[nt] += acc2[nt];
+          } else {
+#pragma unroll
+            for (int ks = 0; ks < CVR_NKS; ++ks) acc[0][0] += (float)af[ks][0];
+          }
+          const int owb = t * 16 + (lane >> 4) * 4;
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) {
+            if (staged && (nt >> 1) != half) continue;
+            const int ocl = nt * 16 + (lane & 15);
+            const int oc = oc0 + ocl;
+            float vv[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) vv[r] = act_t<ACT>(acc[nt][r] + bias_v[nt]);
+            if (staged) {
+              if (!(p.variant & 4))   // [ocl - 32*half][row][OWS]: 4 pixels = one 8-byte write
+                *reinterpret_cast<uint2*>(ostage + (wave * 32 + (ocl - 32 * half)) * ows + owb) =
+                    make_uint2(pack_bf16x2(vv[0], vv[1]), pack_bf16x2(vv[2], vv[3]));
+              else
+                acc[0][0] += vv[1];
+            } else if (oc < p.OC) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                if (owb + r >= p.OW) continue;
+                const long long off = p.nchw_out ? ((long long)n * p.OC + oc) * OHW + (long long)oh * p.OW + owb + r
+                                                 : (((long long)n * p.OH + oh) * p.OW + owb + r) * p.OC + oc;
+                if (p.out_f32) reinterpret_cast<float*>(p.out)[off] = vv[r];
+                else reinterpret_cast<unsigned short*>(p.out)[off] = f32_to_bf16(vv[r]);
+              }
+            }
+          }
+        }
+      }
+      if (!staged) break;
+      if (p.variant & 32) { const unsigned long long t = stamp(); st_comp += t - st_tmp; st_tmp = t; }
+      __syncthreads();
+      if (p.variant & 32) { const unsigned long long t = stamp(); st_bar += t - st_tmp; st_tmp = t; }
+      if (!(p.variant & 1)) {
+        // each (oc, output row) is a 2*OW-byte contiguous segment of the NCHW output (the TR rows of a
+        // plane are adjacent): one wave writes one segment per instruction (lane = dword)
+        const int noc = min(32, p.OC - (oc0 + 32 * half));
+        unsigned short* obase = reinterpret_cast<unsigned short*>(p.out) +
+                                ((long long)n * p.OC + oc0 + 32 * half) * OHW + (long long)oh0 * p.OW;
+        // all of this wave's LDS reads first, then the stores (a read->store pair per iteration would
+        // expose the LDS latency 32 times per half)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          unsigned v[16];
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            const int pr = wave + 4 * (16 * b + j), ocl = pr >> 2, row = pr & 3;
+            v[j] = *reinterpret_cast<const unsigned*>(ostage + (row * 32 + ocl) * ows + 2 * min(lane, 55));
+          }
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            const int pr = wave + 4 * (16 * b + j), ocl = pr >> 2, row = pr & 3;
+            if (ocl < noc && row < rows_valid && lane < dwpr)
+              reinterpret_cast<unsigned*>(obase + ocl * OHW + row * p.OW)[lane] = v[j];
+          }
+        }
+      }
+      __syncthreads();
+    }
+    if (p.variant & 32) st_work += stamp() - st_tmp;
+  }
+  if ((p.variant & 32) && lane == 0) {
+    unsigned long long* d = reinterpret_cast<unsigned long long*>(p.out) + (blockIdx.x * 4 + wave) * 4;
+    d[0] = stamp() - st_t0; d[1] = st_stage; d[2] = st_comp; d[3] = st_bar;
+  }
+}
+
 // Explicit im2col (the reference's materialised ImageToChunks/ImageBlockToMatrix path, kept for the
 // "materialise" plan and for testing). out[p][k] bf16 with ld = ldk (>= K, zero padded).
 __global__ void im2col_kernel(const unsigned short* X, unsigned short* out, int N, int C, int H, int W,
@@ -222,6 +502,9 @@ __global__ void im2col_kernel(const unsigned short* X, unsigned short* out, int 
 
 extern "C" {
 
+int nsdb_conv2d_force_generic = 0;   // 1: always use the generic gather kernel (A/B, tests)
+int nsdb_conv2d_variant = 0;         // row-kernel diagnostics (timing only)
+
 int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* out, int N, int C, int H,
                       int W, int OC, int KH, int KW, int stride, int pad, int dil, int ldw, int act,
                       int nchw_out, int out_f32, hipStream_t stream) {
@@ -235,6 +518,34 @@ int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* ou
   if (ldw % 8 != 0 || ldw < p.K || p.OH <= 0 || p.OW <= 0) return -1;
   if ((long long)N * C * H * W >= 0x7fffffffLL) return -2;   // 32-bit image offsets
   p.act = act; p.nchw_out = nchw_out; p.out_f32 = out_f32;
+  // row-tiled LDS kernel for small-C, wide-row layers (see conv2d_rows_kernel)
+  const int rin = nsdb::CVR_TR + KH - 1;
+  if (nsdb_conv2d_force_generic == 0 && stride == 1 && dil == 1 && pad == 0 && KW <= 8 && W % 8 == 0 &&
+      C * KH <= 4 * nsdb::CVR_NKS && C * rin <= nsdb::CVR_ROWS && p.OW <= 16 * nsdb::CVR_MAXT) {
+    nsdb::ConvRowParams q;
+    q.X = p.X; q.Wt = p.Wt; q.bias = bias; q.out = out;
+    q.N = N; q.C = C; q.H = H; q.W = W; q.OC = OC; q.KH = KH; q.KW = KW; q.OH = p.OH; q.OW = p.OW; q.ldw = ldw;
+    q.rin = rin; q.ckh = C * KH; q.nks = (C * KH + 3) / 4;
+    q.ntiles = (p.OW + 15) / 16;
+    q.chunks = std::min((16 * q.ntiles + 4 + 7) / 8, nsdb::CVR_CP / 16);
+    q.groups_per_img = (p.OH + nsdb::CVR_TR - 1) / nsdb::CVR_TR;
+    q.ngroups = N * q.groups_per_img;
+    q.act = act; q.nchw_out = nchw_out; q.out_f32 = out_f32; q.variant = nsdb_conv2d_variant;
+    if (C * rin * q.chunks > 512 || 64 * ldw / 8 > 6 * 256 || 64 * ldw * 2 > nsdb::CVR_BUF) goto generic;
+    {
+      const int blocks = std::min(q.ngroups, 256 * 2);     // persistent: two blocks per CU
+      const dim3 grid(blocks, (OC + 63) / 64);
+      switch (act) {
+        case nsdb::ACT_RELU: hipLaunchKernelGGL(nsdb::conv2d_rows_kernel<nsdb::ACT_RELU>, grid, dim3(256), 0, stream, q); break;
+        case nsdb::ACT_SIGMOID: hipLaunchKernelGGL(nsdb::conv2d_rows_kernel<nsdb::ACT_SIGMOID>, grid, dim3(256), 0, stream, q); break;
+        case nsdb::ACT_EXP: hipLaunchKernelGGL(nsdb::conv2d_rows_kernel<nsdb::ACT_EXP>, grid, dim3(256), 0, stream, q); break;
+        case nsdb::ACT_TANH: hipLaunchKernelGGL(nsdb::conv2d_rows_kernel<nsdb::ACT_TANH>, grid, dim3(256), 0, stream, q); break;
+        default: hipLaunchKernelGGL(nsdb::conv2d_rows_kernel<nsdb::ACT_NONE>, grid, dim3(256), 0, stream, q); break;
+      }
+      return (int)hipGetLastError();
+    }
+  }
+generic:
   const long long P = (long long)N * p.OH * p.OW;
   dim3 grid((unsigned)((P + nsdb::CV_BM - 1) / nsdb::CV_BM), (OC + nsdb::CV_BN - 1) / nsdb::CV_BN);
   hipLaunchKernelGGL(nsdb::conv2d_igemm_kernel, grid, dim3(256), 0, stream, p);

@@ -70,11 +70,17 @@ def main():
     Wf = ops.pad_k(torch.empty(64, 147, device=dev).uniform_(-0.1, 0.1)).to(torch.bfloat16).contiguous()
     bias = torch.randn(64, device=dev)
     t_ours = timeit(lambda: ops.conv2d(X, Wf, bias, 7, 7, 1, 0))
+    from netsdb_amd import _ext as _e
+
+    _e.hip().conv2d_force_generic(1)
+    t_generic = timeit(lambda: ops.conv2d(X, Wf, bias, 7, 7, 1, 0))
+    _e.hip().conv2d_force_generic(0)
     w4 = Wf[:, :147].reshape(64, 3, 7, 7).contiguous()
     t_lib = timeit(lambda: torch.nn.functional.conv2d(X, w4, bias.to(torch.bfloat16)))
     t_mat = timeit(lambda: ops.gemm_nt(ops.im2col(X, 7, 7, 1, 0), Wf, bias, ops.BIAS_COL))
     fl = 2.0 * 100 * 106 * 106 * 64 * 147
-    r = dict(op="conv2d_7x7x3_64_100img", ms=t_ours, tflops=fl / t_ours / 1e9, lib_ms=t_lib,
+    r = dict(op="conv2d_7x7x3_64_100img", ms=t_ours, tflops=fl / t_ours / 1e9, generic_gather_ms=t_generic,
+             lib_ms=t_lib,
              materialized_im2col_gemm_ms=t_mat, out_GBps=100 * 106 * 106 * 64 * 2 / t_ours / 1e6)
     print(json.dumps(r), flush=True)
     res.append(r)

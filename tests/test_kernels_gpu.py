@@ -92,13 +92,25 @@ def test_gemm_dropout_matches_host_rng():
     _close(C.cpu(), ref, tol=1e-2)
 
 
+@pytest.fixture(params=[0, 1], ids=["auto", "generic"])
+def conv_generic(request):
+    from netsdb_amd import _ext
+
+    _ext.hip().conv2d_force_generic(request.param)
+    yield request.param
+    _ext.hip().conv2d_force_generic(0)
+
+
 @pytest.mark.parametrize("cfg", [
     dict(N=2, C=3, H=20, W=20, OC=8, KH=7, KW=7, stride=1, pad=0),     # the memfuse 7x7x3 shape, small
+    dict(N=3, C=3, H=30, W=112, OC=64, KH=7, KW=7, stride=1, pad=0),   # row kernel: headline geometry
+    dict(N=2, C=2, H=13, W=16, OC=70, KH=5, KW=3, stride=1, pad=0),    # row kernel: 2 oc tiles, OH % 4 != 0
+    dict(N=1, C=1, H=9, W=128, OC=16, KH=8, KW=8, stride=1, pad=0),    # row kernel: KW = 8, OW = 121
     dict(N=1, C=64, H=14, W=14, OC=70, KH=3, KW=3, stride=2, pad=1),   # K=576 > one LDS K chunk, OC edge
     dict(N=3, C=16, H=9, W=11, OC=64, KH=1, KW=1, stride=1, pad=0),
 ])
 @pytest.mark.parametrize("nchw", [False, True])
-def test_conv2d(cfg, nchw):
+def test_conv2d(cfg, nchw, conv_generic):
     torch.manual_seed(4)
     X = torch.randn(cfg["N"], cfg["C"], cfg["H"], cfg["W"], device=DEV).to(torch.bfloat16)
     K = cfg["C"] * cfg["KH"] * cfg["KW"]
