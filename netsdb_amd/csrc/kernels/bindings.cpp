@@ -103,6 +103,33 @@ torch::Tensor gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Ten
   return C;
 }
 
+// Study path: A/B as K-tiled panels [K/64][ldt][64] bf16 (ldt >= rows, multiple of 256 not required);
+// runs the 8-phase kernel's K-tiled variant. C [M,N] f32|bf16.
+torch::Tensor gemm_nt_ktiled(torch::Tensor Ap, torch::Tensor Bp, int64_t M, int64_t N, int64_t K, bool out_f32) {
+  check_cuda(Ap, "A");
+  check_cuda(Bp, "B");
+  TORCH_CHECK(Ap.scalar_type() == torch::kBFloat16 && Bp.scalar_type() == torch::kBFloat16, "A,B must be bf16");
+  TORCH_CHECK(Ap.dim() == 3 && Bp.dim() == 3 && Ap.is_contiguous() && Bp.is_contiguous(), "A,B [K/64][ld][64]");
+  TORCH_CHECK(Ap.size(2) == 64 && Bp.size(2) == 64 && K % 64 == 0 && Ap.size(0) == K / 64 && Bp.size(0) == K / 64,
+              "K-tiled panels must hold K/64 slabs of 64");
+  TORCH_CHECK(Ap.size(1) >= M && Bp.size(1) >= N, "panel rows < M/N");
+  auto C = torch::empty({M, N}, Ap.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16));
+  nsdb_gemm_force_config(11);
+  const int s = nsdb_gemm_splits((int)M, (int)N, (int)K, 1);
+  torch::Tensor ws;
+  float* wsp = nullptr;
+  if (s > 1) {
+    ws = torch::empty({s * M * N}, Ap.options().dtype(torch::kFloat32));
+    wsp = ws.data_ptr<float>();
+  }
+  const int rc = nsdb_gemm_nt_bf16(Ap.data_ptr(), Bp.data_ptr(), C.data_ptr(), wsp, nullptr, (int)M, (int)N, (int)K,
+                                   Ap.size(1), Bp.size(1), N, 0, 0, 0, 0, 1, s, 0, 0, out_f32 ? 1 : 0, 1.f, 0.f, 0, 0,
+                                   cur_stream());
+  nsdb_gemm_force_config(-1);
+  check_rc(rc, "gemm_nt_ktiled");
+  return C;
+}
+
 int64_t gemm_splits(int64_t M, int64_t N, int64_t K, int64_t batch) {
   return nsdb_gemm_splits((int)M, (int)N, (int)K, (int)batch);
 }
@@ -232,6 +259,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dropout") = 0.0, py::arg("seed") = 0, py::arg("splits") = 0, py::arg("out") = py::none(),
         py::arg("accumulate") = false);
   m.def("gemm_splits", &gemm_splits);
+  m.def("gemm_nt_ktiled", &gemm_nt_ktiled, "study: 8-phase GEMM over K-tiled [K/64][ld][64] operand panels");
   m.def("gemm_force_config", [](int64_t cfg) { nsdb_gemm_force_config((int)cfg); },
         "-1 auto, 0 = 128x128 tile, 1 = 256x256 tile (A/B testing)");
   m.def("conv2d_force_generic", [](int64_t v) { nsdb_conv2d_force_generic = (int)v; },

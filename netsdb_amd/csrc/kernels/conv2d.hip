@@ -207,8 +207,9 @@ __global__ void __launch_bounds__(256, 4) conv2d_igemm_kernel(ConvParams p) {
 //    whole (persistent) block;
 //  * copy stride 288 B and the 4-copy interleave make a wave's ds_read_b64 bank-conflict free
 //    (16 lanes of one (c,kh) row cover 128 B, the next row is +128 B mod 256);
-//  * the block's [64 oc][4 rows][OW] bf16 output tile is staged through LDS and written as one contiguous run per oc (the 4
-//    output rows of a plane are adjacent in NCHW) with coalesced dword stores — per-lane 8-byte
+//  * the block's [64 oc][4 rows][OW] bf16 output tile is staged through LDS segment-major and written as one
+//    contiguous run per oc (the 4 output rows of a plane are adjacent in NCHW) with coalesced 8-byte stores
+//    (the store tail is issue-bound: 8 B/lane halves the instructions of dword stores); per-lane
 //    fragment stores into 64 different planes were the limit of the gather kernel (~1 TB/s).
 // Preconditions (host-checked): stride 1, dil 1, pad 0, KW <= 8, W % 8 == 0, OW <= 112,
 // C*KH <= 4*CVR_NKS, C*(4+KH-1) <= CVR_ROWS.
@@ -229,6 +230,7 @@ struct ConvRowParams {
   int N, C, H, W, OC, KH, KW, OH, OW, ldw;
   int rin, ckh, nks, ntiles, chunks, groups_per_img, ngroups;
   int act, nchw_out, out_f32;
+  int segs, vec8;  // staged output: LDS run stride per oc (elements); 8-B output chunks allowed
   int variant;   // diagnostics (bit flags, timing only): 1 no global stores, 2 no MFMA, 4 no LDS output
                  // staging, 8 prologue only, 16 no compute, 32 s_memtime stamps over the output
 };
@@ -339,11 +341,13 @@ __global__ void __launch_bounds__(256, 2) conv2d_rows_kernel(ConvRowParams p) {
   };
 
   const long long OHW = (long long)p.OH * p.OW;
-  unsigned short* ostage = reinterpret_cast<unsigned short*>(smem + CVR_BUF);   // [64 oc][TR rows][OW] bf16
+  unsigned short* ostage = reinterpret_cast<unsigned short*>(smem + CVR_BUF);   // [32 oc][segs] bf16
   const bool staged = p.nchw_out && !p.out_f32 && (p.OW & 1) == 0;
-  // stage layout [row][32 oc][ows], ows = 16*ntiles + 4: the 16 oc rows a ds_write_b64 lane group
-  // touches are 58 dwords apart -> 16 distinct bank pairs (a 112-element stride put all 16 on one bank)
-  const int ows = p.ntiles * 16 + 4;
+  // stage layout "segment-major" [32 oc][segs]: the TR output rows of one oc plane are adjacent in
+  // NCHW, so each oc's rows_valid*OW outputs are ONE contiguous run both in LDS and in HBM and a
+  // wave moves it with 8-B (4-pixel) loads/stores. segs = 4*OW rounded so that segs/2 dwords is
+  // 2 mod 4: the 16 oc a ds_write lane group touches land on 16 distinct banks.
+  const int segs = p.segs;
   int g = blockIdx.x;
   if (p.variant & 8) return;          // diagnostics: prologue only
   // variant 7: s_memtime stamps (diagnostic build: written over the start of the output)
@@ -368,7 +372,6 @@ __global__ void __launch_bounds__(256, 2) conv2d_rows_kernel(ConvRowParams p) {
     // two passes over the row, 32 output channels each: the [32 oc][TR][OWS] bf16 stage is 28 KB, so
     // two blocks fit a CU (the A fragments are re-read from LDS for the second half — cheap)
     const int rows_valid = min(CVR_TR, p.OH - oh0);
-    const int dwpr = p.OW >> 1;
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       if (!staged && half == 1) break;
@@ -418,11 +421,13 @@ __global__ void __launch_bounds__(256, 2) conv2d_rows_kernel(ConvRowParams p) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) vv[r] = act_t<ACT>(acc[nt][r] + bias_v[nt]);
             if (staged) {
-              if (!(p.variant & 4))   // [ocl - 32*half][row][OWS]: 4 pixels = one 8-byte write
-                *reinterpret_cast<uint2*>(ostage + (wave * 32 + (ocl - 32 * half)) * ows + owb) =
-                    make_uint2(pack_bf16x2(vv[0], vv[1]), pack_bf16x2(vv[2], vv[3]));
-              else
+              if (!(p.variant & 4)) {   // [ocl - 32*half][row*OW + ow]: 2 dword writes (OW even -> 4-B aligned)
+                unsigned* dst = reinterpret_cast<unsigned*>(ostage + (ocl - 32 * half) * segs + wave * p.OW + owb);
+                if (owb + 1 < p.OW) dst[0] = pack_bf16x2(vv[0], vv[1]);
+                if (owb + 3 < p.OW) dst[1] = pack_bf16x2(vv[2], vv[3]);
+              } else {
                 acc[0][0] += vv[1];
+              }
             } else if (oc < p.OC) {
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
@@ -441,26 +446,46 @@ __global__ void __launch_bounds__(256, 2) conv2d_rows_kernel(ConvRowParams p) {
       __syncthreads();
       if (p.variant & 32) { const unsigned long long t = stamp(); st_bar += t - st_tmp; st_tmp = t; }
       if (!(p.variant & 1)) {
-        // each (oc, output row) is a 2*OW-byte contiguous segment of the NCHW output (the TR rows of a
-        // plane are adjacent): one wave writes one segment per instruction (lane = dword)
+        // one contiguous run of seg = rows_valid*OW outputs per oc plane; wave w stores oc w, w+4, ..
+        // (all LDS reads first, then the stores: a read->store pair per oc would expose the LDS latency)
         const int noc = min(32, p.OC - (oc0 + 32 * half));
+        const int seg = rows_valid * p.OW;
         unsigned short* obase = reinterpret_cast<unsigned short*>(p.out) +
                                 ((long long)n * p.OC + oc0 + 32 * half) * OHW + (long long)oh0 * p.OW;
-        // all of this wave's LDS reads first, then the stores (a read->store pair per iteration would
-        // expose the LDS latency 32 times per half)
+        if (p.vec8 && (seg & 3) == 0) {
+          // 8-B chunks (plane and row offsets are 8-B aligned: host checked OH*OW % 4 == 0)
+          const int n4 = seg >> 2;
+          uint2 v[8][2];
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          unsigned v[16];
+          for (int j = 0; j < 8; ++j)
 #pragma unroll
-          for (int j = 0; j < 16; ++j) {
-            const int pr = wave + 4 * (16 * b + j), ocl = pr >> 2, row = pr & 3;
-            v[j] = *reinterpret_cast<const unsigned*>(ostage + (row * 32 + ocl) * ows + 2 * min(lane, 55));
-          }
+            for (int h = 0; h < 2; ++h)
+              v[j][h] = *reinterpret_cast<const uint2*>(ostage + (wave + 4 * j) * segs + 4 * min(lane + 64 * h, n4 - 1));
 #pragma unroll
-          for (int j = 0; j < 16; ++j) {
-            const int pr = wave + 4 * (16 * b + j), ocl = pr >> 2, row = pr & 3;
-            if (ocl < noc && row < rows_valid && lane < dwpr)
-              reinterpret_cast<unsigned*>(obase + ocl * OHW + row * p.OW)[lane] = v[j];
+          for (int j = 0; j < 8; ++j)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int ocl = wave + 4 * j, q = lane + 64 * h;
+              if (ocl < noc && q < n4) *reinterpret_cast<uint2*>(obase + ocl * OHW + 4 * q) = v[j][h];
+            }
+        } else {
+          const int n2 = seg >> 1;   // OW even -> dword chunks, 4-B aligned
+#pragma unroll
+          for (int b2 = 0; b2 < 2; ++b2) {
+            unsigned v[4][4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+              for (int h = 0; h < 4; ++h)
+                v[j][h] = *reinterpret_cast<const unsigned*>(ostage + (wave + 4 * (4 * b2 + j)) * segs +
+                                                             2 * min(lane + 64 * h, n2 - 1));
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+              for (int h = 0; h < 4; ++h) {
+                const int ocl = wave + 4 * (4 * b2 + j), q = lane + 64 * h;
+                if (ocl < noc && q < n2) reinterpret_cast<unsigned*>(obase + ocl * OHW)[q] = v[j][h];
+              }
           }
         }
       }
@@ -531,6 +556,10 @@ int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* ou
     q.groups_per_img = (p.OH + nsdb::CVR_TR - 1) / nsdb::CVR_TR;
     q.ngroups = N * q.groups_per_img;
     q.act = act; q.nchw_out = nchw_out; q.out_f32 = out_f32; q.variant = nsdb_conv2d_variant;
+    q.segs = (4 * p.OW + 3) & ~3;
+    if ((q.segs / 2) % 4 == 0) q.segs += 4;
+    q.vec8 = ((long long)p.OH * p.OW) % 4 == 0 && (reinterpret_cast<uintptr_t>(out) & 7) == 0;
+    if (32 * q.segs * 2 > nsdb::CVR_OSTAGE) goto generic;
     if (C * rin * q.chunks > 512 || 64 * ldw / 8 > 6 * 256 || 64 * ldw * 2 > nsdb::CVR_BUF) goto generic;
     {
       const int blocks = std::min(q.ngroups, 256 * 2);     // persistent: two blocks per CU

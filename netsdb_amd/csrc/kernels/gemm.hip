@@ -43,6 +43,8 @@ struct GemmParams {
   float alpha, dropout;
   unsigned long long seed;
   int tiles_m, tiles_n;
+  int vec_ws;               // N % 4 == 0: 4-column groups of the split-K slabs are 16-B aligned
+  int vec_c;                // C rows/base aligned for 4-column vector stores (16 B f32, 8 B bf16)
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
@@ -120,27 +122,71 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[TBM / WGM / 16
     }
     __syncthreads();
     const int nwv = min(per_pass, NW - g0);
-    for (int e = tid; e < nwv * WTILE; e += 64 * NW) {
+    // 4 consecutive columns per thread: one 16-B LDS read and one 16-B (f32) / 8-B (bf16) global
+    // store — the tail of a short-K tile is store-ISSUE bound, so 4x fewer store instructions than
+    // an element per lane (the XOR-16 swizzle keeps aligned groups of 4 columns contiguous).
+    for (int e = tid * 4; e < nwv * WTILE; e += 64 * NW * 4) {
       const int wl = e / WTILE, loc = e % WTILE, r = loc / WC, c = loc % WC;
       const int wv = g0 + wl;
       const int row = m0 + (wv / WGN) * WR + r, col = n0 + (wv % WGN) * WC + c;
       if (row >= p.M || col >= p.N) continue;
-      float v = st[wl * WTILE + r * WC + (c ^ (((r >> 2) & 1) << 4))];
+      const f32x4 v4 = *reinterpret_cast<const f32x4*>(st + wl * WTILE + r * WC + (c ^ (((r >> 2) & 1) << 4)));
+      const int nv = min(4, p.N - col);
       if (ws) {
-        ws[(long long)row * p.N + col] = v;
+        float* d = ws + (long long)row * p.N + col;
+        if (nv == 4 && p.vec_ws) {
+          *reinterpret_cast<f32x4*>(d) = v4;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (j < nv) d[j] = v4[j];
+        }
         continue;
       }
-      v *= p.alpha;
-      if (bias) v += p.bias_mode == 1 ? bias[row] : bias[col];
-      v = apply_act(v, p.act);
-      if (p.dropout > 0.f) {
-        const unsigned long long idx = ((unsigned long long)batch * p.M + row) * p.N + col;
-        v = hash_uniform(p.seed, idx) < p.dropout ? 0.f : v * keep_scale;
-      }
       const long long off = batch * p.sC + (long long)row * p.ldc + col;
-      if (p.accumulate) v += reinterpret_cast<float*>(p.C)[off];
-      if (p.out_f32) reinterpret_cast<float*>(p.C)[off] = v;
-      else reinterpret_cast<unsigned short*>(p.C)[off] = f32_to_bf16(v);
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float x = v4[j] * p.alpha;
+        if (bias) x += p.bias_mode == 1 ? bias[row] : bias[min(col + j, p.N - 1)];
+        x = apply_act(x, p.act);
+        if (p.dropout > 0.f) {
+          const unsigned long long idx = ((unsigned long long)batch * p.M + row) * p.N + col + j;
+          x = hash_uniform(p.seed, idx) < p.dropout ? 0.f : x * keep_scale;
+        }
+        v[j] = x;
+      }
+      const bool vec = nv == 4 && p.vec_c;
+      if (p.accumulate) {
+        const float* cf = reinterpret_cast<const float*>(p.C) + off;
+        if (vec) {
+          const f32x4 o = *reinterpret_cast<const f32x4*>(cf);
+          v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (j < nv) v[j] += cf[j];
+        }
+      }
+      if (p.out_f32) {
+        float* d = reinterpret_cast<float*>(p.C) + off;
+        if (vec) {
+          *reinterpret_cast<f32x4*>(d) = f32x4{v[0], v[1], v[2], v[3]};
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (j < nv) d[j] = v[j];
+        }
+      } else {
+        unsigned short* d = reinterpret_cast<unsigned short*>(p.C) + off;
+        if (vec) {
+          *reinterpret_cast<uint2*>(d) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (j < nv) d[j] = f32_to_bf16(v[j]);
+        }
+      }
     }
   }
 }
@@ -283,15 +329,24 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   const int wr = wave >> 2, wc = wave & 3;
 
   const int rows_a = min(256, p.M - m0), rows_b = min(256, p.N - n0);
-  const unsigned short* Ab = p.A + batch * p.sA + (long long)m0 * p.lda;
-  const unsigned short* Bb = p.B + batch * p.sB + (long long)n0 * p.ldb;
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(Ab, V == 7 ? 0u : (unsigned)((long long)rows_a * p.lda * 2));
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(Bb, V == 7 ? 0u : (unsigned)((long long)rows_b * p.ldb * 2));
-
   const int kbeg = split * p.kchunk;
   const int kend = min(p.K, kbeg + p.kchunk);
   const int nk = max(0, (kend - kbeg + BK - 1) / BK);
   const int niter = (nk + 1) >> 1;
+
+  // KT (variant 9): K-tiled operands [K/64][ld rows][64] — every (tile, k-step) half-tile is one
+  // contiguous 16 KiB run instead of 128 rows x 128 B strided by the row length (DRAM page locality
+  // study). lda/ldb are then the padded row counts; the descriptor base sits at this split's first slab.
+  constexpr bool KT = (V == 9);
+  const unsigned short* Ab = KT ? p.A + batch * p.sA + ((long long)(kbeg / BK) * p.lda + m0) * BK
+                                : p.A + batch * p.sA + (long long)m0 * p.lda;
+  const unsigned short* Bb = KT ? p.B + batch * p.sB + ((long long)(kbeg / BK) * p.ldb + n0) * BK
+                                : p.B + batch * p.sB + (long long)n0 * p.ldb;
+  const long long bytes_a = KT ? std::min<long long>(0x7fffffffLL, (long long)nk * p.lda * BK * 2) : (long long)rows_a * p.lda * 2;
+  const long long bytes_b = KT ? std::min<long long>(0x7fffffffLL, (long long)nk * p.ldb * BK * 2) : (long long)rows_b * p.ldb * 2;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(Ab, V == 7 ? 0u : (unsigned)bytes_a);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(Bb, V == 7 ? 0u : (unsigned)bytes_b);
+  const int slab_a = KT ? p.lda * BK * 2 : 0, slab_b = KT ? p.ldb * BK * 2 : 0;
 
   // Per-thread DMA source rows. Wave-instruction i of a half-tile fills LDS rows
   // hr = i*64 + wave*8 + (lane>>3) (1 KiB, lane-linear); the logical 16-B chunk at physical slot
@@ -305,8 +360,8 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
     for (int i = 0; i < 2; ++i) {
       const int ta = i * 128 + q * 64 + lr;
       const int tb = (2 * i + (lr >> 5)) * 64 + q * 32 + (lr & 31);
-      roff[q][i] = ta < rows_a ? (int)((long long)ta * p.lda * 2) : -1;
-      roff[2 + q][i] = tb < rows_b ? (int)((long long)tb * p.ldb * 2) : -1;
+      roff[q][i] = ta < rows_a ? (KT ? ta * BK * 2 : (int)((long long)ta * p.lda * 2)) : -1;
+      roff[2 + q][i] = tb < rows_b ? (KT ? tb * BK * 2 : (int)((long long)tb * p.ldb * 2)) : -1;
     }
 
   auto stage = [&](int buf, int slot, int u) {
@@ -317,7 +372,7 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int ro = roff[slot][i];
-      const int voff = (kin && ro >= 0) ? ro + k * 2 : OOB;
+      const int voff = (kin && ro >= 0) ? (KT ? u * (slot < 2 ? slab_a : slab_b) + ro + kc * 2 : ro + k * 2) : OOB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(slot < 2 ? ra : rb, (lds_void*)(dst + (i * 64 + wave * 8) * 128), 16,
                                                voff, 0, 0, 0);
     }
@@ -415,6 +470,45 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(GemmParams p) {
   const float* bias = p.bias ? p.bias + batch * p.sBias : nullptr;
   const float keep_scale = p.dropout > 0.f ? 1.f / (1.f - p.dropout) : 1.f;
   (void)total;
+  if (p.vec_ws) {
+    // N % 4 == 0: 4 consecutive columns of one row per thread, 16-B slab loads (splits in flight together)
+    for (long long e = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4; e < MN;
+         e += (long long)gridDim.x * blockDim.x * 4) {
+      const float* w = p.ws + (long long)batch * p.splits * MN + e;
+      f32x4 s = *reinterpret_cast<const f32x4*>(w);
+#pragma unroll 4
+      for (int k = 1; k < p.splits; ++k) s += *reinterpret_cast<const f32x4*>(w + k * MN);
+      const int row = (int)(e / p.N), col = (int)(e % p.N);
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float x = s[j] * p.alpha;
+        if (bias) x += (p.bias_mode == 1) ? bias[row] : bias[col + j];
+        x = apply_act_compact(x, p.act);
+        if (p.dropout > 0.f) {
+          const unsigned long long idx = (unsigned long long)batch * MN + e + j;
+          x = hash_uniform(p.seed, idx) < p.dropout ? 0.f : x * keep_scale;
+        }
+        v[j] = x;
+      }
+      const long long off = batch * p.sC + (long long)row * p.ldc + col;
+      if (p.accumulate) {
+        const float* cf = reinterpret_cast<const float*>(p.C) + off;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] += cf[j];
+      }
+      if (p.out_f32) {
+        float* d = reinterpret_cast<float*>(p.C) + off;
+        if (p.vec_c) *reinterpret_cast<f32x4*>(d) = f32x4{v[0], v[1], v[2], v[3]};
+        else { d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3]; }
+      } else {
+        unsigned short* d = reinterpret_cast<unsigned short*>(p.C) + off;
+        if (p.vec_c) *reinterpret_cast<uint2*>(d) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+        else { d[0] = f32_to_bf16(v[0]); d[1] = f32_to_bf16(v[1]); d[2] = f32_to_bf16(v[2]); d[3] = f32_to_bf16(v[3]); }
+      }
+    }
+    return;
+  }
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < MN;
        e += (long long)gridDim.x * blockDim.x) {
     const float* w = p.ws + (long long)batch * p.splits * MN + e;
@@ -500,11 +594,16 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
   const int tbm = cfg ? 256 : nsdb::BM, tbn = cfg ? 256 : nsdb::BN;
   p.tiles_m = (M + tbm - 1) / tbm;
   p.tiles_n = (N + tbn - 1) / tbn;
+  p.vec_ws = (N % 4 == 0) ? 1 : 0;
+  p.vec_c = (ldc % 4 == 0 && sC % 4 == 0 &&
+             (reinterpret_cast<uintptr_t>(C) & (out_f32 ? 15 : 7)) == 0) ? 1 : 0;
   dim3 grid(p.tiles_m * p.tiles_n * p.splits, 1, batch);
   if (cfg == 2)
     hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<0>, grid, dim3(512), 0, stream, p);
   else if (cfg == 10)
     hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<8>, grid, dim3(512), 0, stream, p);
+  else if (cfg == 11)   // K-tiled operands (caller passes [K/64][ld][64] panels, lda/ldb = padded rows)
+    hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<9>, grid, dim3(512), 0, stream, p);
   else if (cfg >= 3 && cfg <= 9) {   // diagnostic variants of the 8-phase kernel (timing only)
     auto kern = cfg == 3 ? nsdb::gemm_nt_256_8ph_kernel<1> : cfg == 4 ? nsdb::gemm_nt_256_8ph_kernel<2>
               : cfg == 5 ? nsdb::gemm_nt_256_8ph_kernel<3> : cfg == 6 ? nsdb::gemm_nt_256_8ph_kernel<4>
@@ -518,7 +617,7 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
     hipLaunchKernelGGL((nsdb::gemm_nt_tile_kernel<128, 128, 2, 2>), grid, dim3(256), 0, stream, p);
   if (p.splits > 1) {
     const long long MN = (long long)M * N;
-    int blocks = (int)std::min<long long>((MN + 255) / 256, 4096);
+    int blocks = (int)std::min<long long>(((p.vec_ws ? MN / 4 : MN) + 255) / 256, 4096);
     hipLaunchKernelGGL(nsdb::splitk_reduce_kernel, dim3(blocks, batch), dim3(256), 0, stream, p);
   }
   return (int)hipGetLastError();

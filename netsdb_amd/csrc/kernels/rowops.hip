@@ -69,6 +69,41 @@ __global__ void __launch_bounds__(256) row_normalize_kernel(const TI* X, TO* Y, 
   for (int j = threadIdx.x; j < N; j += blockDim.x) st(y, j, ld(x, j) * inv);
 }
 
+// Register-resident variant for f32 rows with 16-B aligned rows (the [batch, labels] exp'd scores of
+// the FF output layer, 58 KB/row): 512 threads each hold NV float4 of the row, so the row is read
+// from HBM once (the two-pass kernel above re-reads it) — 1 read + 1 write per element.
+template <typename TO, int NV>
+__global__ void __launch_bounds__(512) row_normalize_vec_kernel(const float* X, TO* Y, int R, int N, long long ldx,
+                                                                long long ldy) {
+  __shared__ float red[8];
+  const int row = blockIdx.x;
+  if (row >= R) return;
+  const int n4 = N >> 2;
+  const f32x4* x = reinterpret_cast<const f32x4*>(X + (long long)row * ldx);
+  f32x4 v[NV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int j = threadIdx.x + i * 512;
+    v[i] = j < n4 ? __builtin_nontemporal_load(x + j) : f32x4{0.f, 0.f, 0.f, 0.f};
+    s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
+  }
+  const float inv = 1.f / block_reduce(s, red, false);
+  TO* y = Y + (long long)row * ldy;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int j = threadIdx.x + i * 512;
+    if (j >= n4) break;
+    const f32x4 o = v[i] * inv;
+    if constexpr (sizeof(TO) == 4) {
+      __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(y) + j);
+    } else {
+      uint2 pk{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
+      reinterpret_cast<uint2*>(y)[j] = pk;
+    }
+  }
+}
+
 // y = dropout(act(x + bias[row|col])) elementwise over [R][N]
 template <typename TI, typename TO>
 __global__ void __launch_bounds__(256) bias_act_kernel(const TI* X, const float* bias, TO* Y, int R, int N,
@@ -143,6 +178,17 @@ int nsdb_softmax_rows(const void* X, int x_f32, const float* bias, void* Y, int 
                       long long ldx, long long ldy, int log_out, hipStream_t st) {
   if (R <= 0) return 0;
   if (log_out == 2) {   // row normalise
+    const bool vec = x_f32 && (N % 4 == 0) && (ldx % 4 == 0) && (ldy % 4 == 0) &&
+                     ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(Y)) & 15) == 0;
+    if (vec && N <= 512 * 4 * 8) {
+#define NSDB_RNV(TO, NV) \
+  hipLaunchKernelGGL((nsdb::row_normalize_vec_kernel<TO, NV>), dim3(R), dim3(512), 0, st, (const float*)X, (TO*)Y, R, N, ldx, ldy)
+      const int nv = (N / 4 + 511) / 512;
+      if (y_f32) { if (nv <= 2) NSDB_RNV(float, 2); else if (nv <= 4) NSDB_RNV(float, 4); else NSDB_RNV(float, 8); }
+      else { if (nv <= 2) NSDB_RNV(unsigned short, 2); else if (nv <= 4) NSDB_RNV(unsigned short, 4); else NSDB_RNV(unsigned short, 8); }
+#undef NSDB_RNV
+      return (int)hipGetLastError();
+    }
 #define NSDB_RN(TI, TO) \
   hipLaunchKernelGGL((nsdb::row_normalize_kernel<TI, TO>), dim3(R), dim3(256), 0, st, (const TI*)X, (TO*)Y, R, N, ldx, ldy)
     if (x_f32 && y_f32) NSDB_RN(float, float);

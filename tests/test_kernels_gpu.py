@@ -139,6 +139,30 @@ def test_softmax_rows(dt):
     assert torch.allclose(y.sum(-1), torch.ones(37, device=DEV), atol=1e-4)
 
 
+@pytest.mark.parametrize("R,N", [(37, 14588), (5, 1000), (3, 130), (4, 50000), (2, 7)])
+@pytest.mark.parametrize("out_f32", [True, False])
+def test_row_normalize(R, N, out_f32):
+    X = torch.rand(R, N, device=DEV) + 0.1
+    y = ops.row_normalize(X, out_dtype=torch.float32 if out_f32 else torch.bfloat16)
+    _close(y, X / X.sum(-1, keepdim=True), tol=1e-2 if not out_f32 else 1e-5)
+
+
+@pytest.mark.parametrize("n0,n1", [(0, 256), (3, 301), (128, 1000), (1, 2)])
+def test_gemm_out_column_slice(n0, n1):
+    # C[:, n0:n1] views (ldc != N, unaligned base): the distributed N-chunk pipeline writes these
+    torch.manual_seed(6)
+    A = torch.randn(200, 320, device=DEV).to(torch.bfloat16)
+    B = torch.randn(1000, 320, device=DEV).to(torch.bfloat16)
+    bias = torch.randn(1000, device=DEV)
+    for dt in (torch.float32, torch.bfloat16):
+        C = torch.zeros(200, 1000, device=DEV, dtype=dt)
+        ops.gemm_nt(A, B[n0:n1], bias[n0:n1], ops.BIAS_COL, ops.ACT_RELU, out_dtype=dt, out=C[:, n0:n1])
+        ref = torch.zeros(200, 1000, device=DEV)
+        ref[:, n0:n1] = _ref_gemm(A, B[n0:n1], bias[n0:n1], 2, ops.ACT_RELU)
+        _close(C, ref, tol=2e-2)
+        assert C[:, :n0].abs().sum() == 0 and C[:, n1:].abs().sum() == 0
+
+
 def test_bias_act_and_lstm_and_embedding():
     X = torch.randn(33, 65, device=DEV)
     b = torch.randn(33, device=DEV)
