@@ -15,10 +15,11 @@ with bias/act/dropout fused in the epilogue; softmax/row-normalise, elementwise,
 orientation is chosen per node so every GEMM reads both operands K-contiguous with no transposes.
 
 Distribution (one rank per GPU): a matrix value is replicated or partitioned by logical rows or
-columns.  A matmul whose K dimension is partitioned runs as a ring: each rank multiplies its A
-column-slab with the B slab it holds while the next slab arrives from its neighbour over xGMI
-(``batch_isend_irecv`` on RCCL), accumulating into an f32 C with the GEMM's accumulate epilogue —
-netsDB's hash-partitioned join + shuffle-aggregate, overlapped with the block GEMMs.
+columns.  Row-split A against K-split B (both sets row-partitioned, the LA DSL's ``A %*% B``) runs
+as an N-chunked pipeline: B^T chunks are all-gathered over RCCL (all xGMI links) while the previous
+chunk's full-K GEMM writes its column block of C in place.  A K-split product (``A '* B``, or one
+side replicated) multiplies each rank's K range into an f32 partial and reduce-scatters it —
+netsDB's hash-partitioned join + shuffle-aggregate of partial blocks, as collectives.
 
 Everything not matched runs through the generic TCAP pipeline; fused results feeding generic
 computations are materialised into temp dense sets.
@@ -136,16 +137,21 @@ class MatmulNode(Node):
         A, B = self.a.eval(engine), self.b.eval(engine)
         opA = A.t() if self.p.transpose_a else A           # [M, K]
         opB = B.t() if self.p.transpose_b else B           # [K, N]
-        # distribution: M-split A and N-split B are local; a K-split needs the ring
-        if opA.part == "rows" and opB.part == "cols":
-            opB = _replicate(engine, opB)
-        ring = opA.part == "cols" and opB.part == "rows"
-        if opA.part == "cols" and not ring:
-            opA = _replicate(engine, opA)
-        if opB.part == "rows" and not ring:
-            opB = _replicate(engine, opB)
+        # distribution (one rank per GPU): M-split A / N-split B are local; a K-split of B against
+        # row-split A runs the N-chunked all-gather pipeline; K-split partial products are
+        # reduce-scattered (netsDB's shuffle aggregation of partial blocks)
+        dist_mode = "local"
+        if engine.ctx.distributed:
+            if opA.part == "cols" and opB.part == "cols":
+                opA = _replicate(engine, opA)
+            if opA.part == "rows" and opB.part == "cols":
+                opB = _replicate(engine, opB)
+            if opA.part == "rows" and opB.part == "rows":
+                dist_mode = "allgather_n"
+            elif opA.part == "cols" or opB.part == "rows":
+                dist_mode = "kpartial"
         M, K, N = opA.rows, opA.cols, opB.cols
-        if not ring and K != opB.rows:
+        if dist_mode == "local" and K != opB.rows:
             raise ValueError(f"fused matmul K mismatch {K} vs {opB.rows}")
         want_t = bool(self.consumers_want_t)
         phys_is_c = self.transpose_out == want_t
@@ -164,8 +170,12 @@ class MatmulNode(Node):
         # exp'd scores keep f32 (exact row normalisation); f32 operands keep an f32 result
         odt = torch.float32 if (act == ops.ACT_EXP or opA.phys.dtype == torch.float32
                                 or opB.phys.dtype == torch.float32) else torch.bfloat16
-        if ring:
-            phys = self._ring(engine, opA, opB, M, N, phys_is_c, bias_t, mode, act, odt)
+        if dist_mode == "allgather_n":
+            phys = self._allgather_n(engine, opA, opB, M, N, phys_is_c, bias_t, mode, act, odt)
+        elif dist_mode == "kpartial":
+            value = self._kpartial(engine, opA, opB, M, N, phys_is_c, bias_t, act, odt)
+            self.value = value
+            return value
         else:
             K8 = (K + 7) // 8 * 8
             # X = opA as [M,K] K-contig <=> opA physical not transposed; Y = opB^T as [N,K]
@@ -188,43 +198,130 @@ class MatmulNode(Node):
         self.value = value
         return value
 
-    def _ring(self, engine, opA: Dense, opB: Dense, M, N, phys_is_c, bias_t, mode, act, odt):
-        """K-partitioned matmul: C_r = sum_s A_r[:, K_s] . B_s with B slabs circulating on a ring."""
+    def _allgather_n(self, engine, opA: Dense, opB: Dense, M, N, phys_is_c, bias_t, mode, act, odt):
+        """Row-split A [M_r, K] x K-split B (rank s holds rows K_s of B): every rank needs all of B.
+
+        B^T is all-gathered in N-chunks over RCCL (one collective per chunk uses every xGMI link of
+        the node, unlike a neighbour ring that is bound by one link) on the communication stream while
+        the previous chunk's full-K MFMA GEMM runs: C_r[:, n0:n1] = epi(A_r . B[:, n0:n1]) written in
+        place, so there is no f32 partial and no accumulation pass.  Chunks of rank slabs
+        [ws, nc, k_s] are laid side by side along K, matching A's columns (A is re-laid out once only
+        when the K partition is uneven)."""
+        ctx = engine.ctx
+        ws = ctx.world_size
+        cd = ctx._comm_device()
+        kr = torch.tensor([[opB.offset, opB.rows]], dtype=torch.int64, device=cd)
+        ranges = [(int(x[0, 0]), int(x[0, 1])) for x in ctx.all_gather_tensor(kr)]
+        kmax8 = (max(k for _, k in ranges) + 7) // 8 * 8
+        A_full = opA.physical(False)                         # [M, >= K_total]: local rows, all K
+        dev = A_full.device
+        uniform = all(off == s * kmax8 and k == kmax8 for s, (off, k) in enumerate(ranges)) and \
+            A_full.shape[1] >= ws * kmax8
+        if uniform:
+            A_use = A_full[:M, : ws * kmax8]
+        else:
+            A_use = torch.zeros(M, ws * kmax8, dtype=A_full.dtype, device=dev)
+            for s_, (off, k) in enumerate(ranges):
+                A_use[:, s_ * kmax8: s_ * kmax8 + k] = A_full[:M, off: off + k]
+        Bt = opB.physical(True)[:N, : opB.rows]               # [N, K_r] K-contiguous
+        if Bt.shape[1] != kmax8 or not Bt.is_contiguous():
+            Bt = torch.nn.functional.pad(Bt, (0, kmax8 - Bt.shape[1])).contiguous()
+        # chunk N: ~8 chunks of >= 1024 columns (multiples of 256 = whole GEMM tiles)
+        nchunks = max(1, min(8, N // 1024))
+        step = (N + nchunks - 1) // nchunks
+        step = (step + 255) // 256 * 256
+        bounds = [(n0, min(N, n0 + step)) for n0 in range(0, N, step)]
+        out = torch.empty((M, N) if phys_is_c else (N, M), dtype=odt, device=dev)
+        nccl = ctx.backend == "nccl"
+
+        def start(c):
+            n0, n1 = bounds[c]
+            src = Bt[n0:n1].to(cd).contiguous()
+            if nccl:
+                dst = torch.empty(ws * (n1 - n0), kmax8, dtype=src.dtype, device=cd)
+                return dst, dist.all_gather_into_tensor(dst, src, async_op=True)
+            parts = [torch.empty_like(src) for _ in range(ws)]
+            return parts, dist.all_gather(parts, src, async_op=True)
+
+        pending = start(0)
+        for c, (n0, n1) in enumerate(bounds):
+            got, work = pending
+            if c + 1 < len(bounds):
+                pending = start(c + 1)        # next chunk's collective overlaps this chunk's GEMM
+            work.wait()
+            nc = n1 - n0
+            g = got.view(ws, nc, kmax8) if nccl else torch.stack(got)
+            Y = g.permute(1, 0, 2).reshape(nc, ws * kmax8).to(dev)
+            b = None
+            if bias_t is not None:
+                b = bias_t[n0:n1] if (mode == ops.BIAS_COL) == phys_is_c else bias_t
+            seed = self.seed + c * 0x9E3779B1
+            if phys_is_c:
+                ops.gemm_nt(A_use, Y, b, mode, act, out_dtype=odt, dropout=self.dropout, seed=seed, out=out[:, n0:n1])
+            else:
+                ops.gemm_nt(Y, A_use, b, mode, act, out_dtype=odt, dropout=self.dropout, seed=seed, out=out[n0:n1])
+        return out
+
+    def _kpartial(self, engine, opA: Dense, opB: Dense, M, N, phys_is_c, bias_t, act, odt) -> Dense:
+        """K-split product: each rank multiplies the K range it holds (A's column slab and/or B's row
+        slab, slicing the replicated operand to that range) into an f32 partial of the whole output,
+        then reduce-scatter sums the partials and leaves each rank its block-row range of C (C^T when
+        the consumer wants the transposed layout) — then the epilogue runs on the local slice."""
         ctx = engine.ctx
         ws, r = ctx.world_size, ctx.rank
-        kr = torch.tensor([[opB.offset, opB.rows]], dtype=torch.int64, device=ctx.device)
-        allk = ctx.all_gather_tensor(kr)
-        ranges = [(int(x[0, 0]), int(x[0, 1])) for x in allk]
-        kmax = max(k for _, k in ranges)
-        kmax8 = (kmax + 7) // 8 * 8
-        # local slab of B^T [N, Ks] (K-contiguous), padded to the largest slab for the ring buffers
-        bt = opB.physical(True)[:N, :opB.rows]
-        buf = [torch.zeros(N, kmax8, dtype=torch.bfloat16, device=bt.device) for _ in range(2)]
-        buf[0][:, :opB.rows].copy_(bt)
-        A_full = opA.physical(False)   # [M, K_total] local rows, all columns
-        C = torch.zeros(M, N, dtype=torch.float32, device=bt.device)
-        cur = 0
-        for t in range(ws):
-            s = (r - t) % ws
-            reqs = []
-            if t + 1 < ws:
-                p2p = [dist.P2POp(dist.isend, buf[cur], (r + 1) % ws),
-                       dist.P2POp(dist.irecv, buf[cur ^ 1], (r - 1) % ws)]
-                reqs = dist.batch_isend_irecv(p2p)
-            k0, ks = ranges[s]
-            k8 = (ks + 7) // 8 * 8
-            if k0 % 8 == 0 and k0 + k8 <= A_full.shape[1]:
-                Xs = A_full[:M, k0:k0 + k8]
-            else:
-                Xs = ops.pad_k(A_full[:M, k0:k0 + ks].contiguous())
-            Ys = buf[cur][:, :k8]
-            ops.gemm_nt(Xs, Ys, out=C, out_dtype=torch.float32, accumulate=True)
-            for q in reqs:
-                q.wait()
-            cur ^= 1
-        # epilogue (bias/act/dropout) on the summed f32 C
-        src = C if phys_is_c else C.t().contiguous()
-        return ops.bias_act(src, bias_t, mode if mode else ops.BIAS_COL, act, self.dropout, self.seed, out_dtype=odt)
+        cd = ctx._comm_device()
+        if opA.part == "cols" and opB.part == "rows":
+            ka = torch.tensor([[opA.offset, opA.cols, opB.offset, opB.rows]], dtype=torch.int64, device=cd)
+            same = all(int(x[0, 0]) == int(x[0, 2]) and int(x[0, 1]) == int(x[0, 3]) for x in ctx.all_gather_tensor(ka))
+            if not same:
+                opA = _replicate(engine, opA)
+        if opA.part == "cols":
+            k0, kn = opA.offset, opA.cols
+        else:
+            k0, kn = opB.offset, opB.rows
+        kn8 = (kn + 7) // 8 * 8
+        A_loc = opA.physical(False)
+        Bt_loc = opB.physical(True)
+        a0 = 0 if opA.part == "cols" else k0
+        b0 = 0 if opB.part == "rows" else k0
+        X = A_loc[:M, a0: a0 + kn]
+        Y = Bt_loc[:N, b0: b0 + kn]
+        if kn8 != kn or a0 % 8 or b0 % 8:
+            X = torch.nn.functional.pad(X, (0, kn8 - kn)).contiguous()
+            Y = torch.nn.functional.pad(Y, (0, kn8 - kn)).contiguous()
+        P = ops.gemm_nt(X, Y, out_dtype=torch.float32) if phys_is_c else ops.gemm_nt(Y, X, out_dtype=torch.float32)
+        R = P.shape[0]
+        blk = max(1, opA.br if phys_is_c else opB.bc)
+        nb = (R + blk - 1) // blk
+        per = (nb + ws - 1) // ws
+        counts = [max(0, min(R, (s + 1) * per * blk) - min(R, s * per * blk)) for s in range(ws)]
+        off = min(R, r * per * blk)
+        if ctx.backend == "nccl" and len(set(counts)) > 1:
+            # RCCL reduce_scatter wants equal slices: pad the partial to ws equal slices
+            eq = per * blk
+            Pp = torch.zeros(eq * ws, P.shape[1], dtype=P.dtype, device=P.device)
+            Pp[:R] = P
+            loc = ctx.reduce_scatter_rows(Pp, [eq] * ws)[: counts[r]]
+        else:
+            loc = ctx.reduce_scatter_rows(P, counts)
+        # epilogue on the local rows: bias along C rows (phys rows when phys_is_c) is sliced by offset
+        along_phys_rows = (self.bias_along == "row") == phys_is_c
+        b = None
+        if bias_t is not None:
+            b = bias_t[off: off + counts[r]] if along_phys_rows else bias_t
+        y = ops.bias_act(loc.contiguous(), b, ops.BIAS_ROW if along_phys_rows else ops.BIAS_COL, act, self.dropout,
+                         self.seed + r, out_dtype=odt)
+        br, bc = opA.br, opB.bc
+        total = R
+        if phys_is_c:      # phys = C rows [off, off+cnt) -> logical C row-partitioned
+            part = "rows"
+            if self.transpose_out:
+                return Dense(y, N, counts[r], True, bc, br, "cols", off, total)
+            return Dense(y, counts[r], N, False, br, bc, part, off, total)
+        # phys = C^T rows = C columns [off, off+cnt)
+        if self.transpose_out:
+            return Dense(y, counts[r], M, False, bc, br, "rows", off, total)
+        return Dense(y, M, counts[r], True, br, bc, "cols", off, total)
 
 
 class SoftmaxNode(Node):

@@ -103,6 +103,45 @@ def _la_ring_scenario(ctx, out_dir):
     return {"err": (C.float() - A @ Bm).abs().max().item(), "fused": st.get("fused_ops")}
 
 
+def _la_dist_scenario(ctx, out_dir):
+    """Uneven row partitions (40 rows / block 8 over 2 ranks = 24 + 16): A %*% B (row x K split,
+    all-gather pipeline), A '* B (K x K split -> reduce-scatter), and a fused bias+relu epilogue."""
+    from netsdb_amd.client import PDBClient
+    from netsdb_amd.computations import ScanSet, WriteSet
+    from netsdb_amd.la import computations as L
+    from netsdb_amd.models import blocks as B
+
+    c = PDBClient(ctx=ctx, root=tempfile.mkdtemp())
+    c.create_database("LA_db")
+    g = torch.Generator().manual_seed(7)
+    A = torch.rand(40, 40, generator=g) - 0.5
+    Bm = torch.rand(40, 24, generator=g) - 0.5
+    B.load_tensor(c, "LA_db", "A", A, 8, 8, dtype=torch.float32, partition_rows=True)
+    B.load_tensor(c, "LA_db", "B", Bm, 8, 8, dtype=torch.float32, partition_rows=True)
+    res = {"local_rows": c.get_set("LA_db", "A").local_rows}
+    for tag, jcls, ref in (("mul", L.LAMultiply1Join, A @ Bm), ("tmul", L.LATransposeMultiply1Join, A.t() @ Bm)):
+        c.create_set("LA_db", f"C_{tag}", None, dense=True)
+        j = jcls()
+        j.set_input(0, ScanSet("LA_db", "A"))
+        j.set_input(1, ScanSet("LA_db", "B"))
+        st = c.execute_computations(WriteSet("LA_db", f"C_{tag}").set_input(L.LAMultiply2Aggregate().set_input(j)))
+        C = B.to_tensor(c, "LA_db", f"C_{tag}")
+        res[tag] = (C.float() - ref).abs().max().item()
+        res[f"{tag}_shape"] = tuple(C.shape)
+        res[f"{tag}_fused"] = st.get("fused_ops")
+    return res
+
+
+@pytest.mark.timeout(300)
+def test_distributed_la_partitioned_matmuls():
+    r0, r1 = _run("_la_dist_scenario")
+    assert r0["local_rows"] == 24 and r1["local_rows"] == 16
+    for r in (r0, r1):
+        assert r["mul"] < 1e-4 and r["tmul"] < 1e-4, r
+        assert r["mul_shape"] == (40, 24) and r["tmul_shape"] == (40, 24)
+        assert any("matmul" in f for f in r["tmul_fused"])
+
+
 @pytest.mark.timeout(300)
 def test_distributed_engine_join_aggregate():
     r0, r1 = _run("_engine_scenario")
