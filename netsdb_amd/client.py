@@ -230,11 +230,158 @@ class PDBClient:
         return plan.tcap + "\n" + pp.explain()
 
     # ------------------------------------------------------------------ dedup / shared pages
-    def add_shared_mapping(self, db, set_name, shared_db, shared_set, meta=None):
-        self.catalog.add_shared_mapping(db, set_name, shared_db, shared_set, meta)
+    def add_shared_page(self, sharing_db: str, sharing_set: str, sharing_type, shared_db: str, shared_set: str,
+                        shared_type, page_id: int, partition_id: int = 0, page_seq_id: Optional[int] = None,
+                        add_shared_set: bool = False, node_id: int = -1) -> bool:
+        """Link page ``page_seq_id`` (default ``page_id``) of the shared set into the sharing set on node
+        ``node_id`` (-1: every rank).  PDBClient::addSharedPage; ``add_shared_set`` mirrors
+        whetherToAddSharedSet (records the shared set in the catalog on first link)."""
+        if node_id >= 0 and node_id != self.ctx.rank:
+            return True
+        sharing = self.storage.get_set(sharing_db, sharing_set)
+        shared = self.storage.get_set(shared_db, shared_set)
+        sharing.add_shared_page(shared, int(page_seq_id if page_seq_id is not None else page_id))
+        if add_shared_set:
+            self.catalog.add_shared_mapping(sharing_db, sharing_set, shared_db, shared_set,
+                                            {"kind": "pages", "partition": partition_id})
+        return True
+
+    addSharedPage = add_shared_page
+
+    def add_shared_mapping(self, sharing_db: str, sharing_set: str, sharing_type, shared_db: str, shared_set: str,
+                           shared_type, file_name: Optional[str] = None, total_rows: int = 0, total_cols: int = 0,
+                           transpose: bool = False, mapping: Optional[dict] = None) -> bool:
+        """Remap the shared set's blocks (by distinct block id) to their place in the sharing set:
+        PDBClient::addSharedMapping -> SharedFFMatrixBlockSet::loadIndexFromFile.  ``file_name``
+        holds 'blockKey,blockRow,blockCol' lines; ``mapping`` may give {key: (row, col)} directly."""
+        from .models.dedup import TensorBlockIndex
+
+        sharing = self.storage.get_set(sharing_db, sharing_set)
+        shared = self.storage.get_set(shared_db, shared_set)
+        idx = TensorBlockIndex(0, 0)
+        key = TensorBlockIndex.set_key(0, 0, sharing.set_id)
+        if file_name is not None:
+            idx.load_index_file(key, file_name, total_rows, total_cols, transpose)
+        for k, (r, c) in (mapping or {}).items():
+            idx.insert_index(key, k, (c, r, total_rows, total_cols) if transpose else (r, c, total_rows, total_cols))
+        targets = idx.targets.get(key, {})
+        sharing.set_shared_mapping(shared, targets)
+        if not sharing.link(shared).pages:
+            # a mapping alone shares every page of the shared set (the reference links pages first)
+            for p in range(max(1, len(shared.pages))):
+                sharing.add_shared_page(shared, p)
+        self.catalog.add_shared_mapping(sharing_db, sharing_set, shared_db, shared_set,
+                                        {"kind": "mapping", "file": file_name, "entries": len(targets),
+                                         "total_rows": total_rows, "total_cols": total_cols, "transpose": transpose})
         return True
 
     addSharedMapping = add_shared_mapping
+
+    # ------------------------------------------------------------------ remaining PDBClient surface
+    def create_temp_set(self, db: str, name: str, type_=None, page_size: Optional[int] = None) -> bool:
+        """createTempSet: a storage-only set (not in the catalog, never flushed)."""
+        self.storage.create_set(db, name, type_, page_size, persistent=False)
+        return True
+
+    createTempSet = create_temp_set
+
+    def remove_temp_set(self, db: str, name: str, type_=None) -> bool:
+        self.storage.remove_set(db, name)
+        return True
+
+    removeTempSet = remove_temp_set
+
+    def remove_hash_set(self, name: str) -> bool:
+        """removeHashSet: join/aggregation hash tables live only inside one job here (device tensors
+        freed with the job), so there is no persistent hash set to drop."""
+        return True
+
+    removeHashSet = remove_hash_set
+
+    def delete_set(self, db: str, name: str) -> bool:
+        return self.remove_set(db, name)
+
+    deleteSet = delete_set
+
+    def export_set(self, db: str, name: str, path: str, fmt: str = "csv") -> bool:
+        """exportSet: schema line + one value line per object (ExportableObject::toSchemaString /
+        toValueString; objects may define ``to_schema_string(fmt)`` / ``to_value_string(fmt)``)."""
+        import json as _json
+
+        head = False
+        with open(path, "w") as f:
+            for b in self.get_set_batches(db, name):
+                for o in b.to_objects():
+                    fields = list(type(o).fields()) if hasattr(type(o), "fields") else []
+                    if not head:
+                        hs = o.to_schema_string(fmt) if hasattr(o, "to_schema_string") else \
+                            (",".join(fields) + "\n" if fmt == "csv" else "")
+                        f.write(hs)
+                        head = True
+                    if hasattr(o, "to_value_string"):
+                        f.write(o.to_value_string(fmt))
+                        continue
+                    vals = {k: getattr(o, k) for k in fields}
+                    vals = {k: (v.tolist() if isinstance(v, torch.Tensor) else v) for k, v in vals.items()}
+                    if fmt == "json":
+                        f.write(_json.dumps(vals, default=str) + "\n")
+                    else:
+                        f.write(",".join(str(vals[k]) for k in fields) + "\n")
+        return True
+
+    exportSet = export_set
+
+    def register_node(self, address: str, port: int = 0, name: str = "", node_type: str = "worker",
+                      status: int = 0) -> bool:
+        self.catalog.register_node(self.ctx.rank, f"{address}:{port}", name or node_type, 0)
+        return True
+
+    registerNode = register_node
+
+    def register_set(self, set_and_db, policy) -> bool:
+        """registerSet(pair(set, db), policy): the dispatcher partition policy of a set."""
+        name, db = set_and_db
+        self.policies[(db, name)] = make_policy(policy)
+        return True
+
+    registerSet = register_set
+
+    def send_bytes(self, set_and_db, data: bytes) -> int:
+        """sendBytes: a serialised page image (storage.serde) appended to this rank's partition."""
+        from .storage.serde import deserialize_batch
+
+        name, db = set_and_db
+        b = deserialize_batch(data)
+        self.storage.get_set(db, name).add_batch(b)
+        return b.n
+
+    sendBytes = send_bytes
+
+    def list_registered_databases(self) -> str:
+        return "\n".join(self.catalog.databases())
+
+    listRegisteredDatabases = list_registered_databases
+
+    def list_registered_sets_for_database(self, db: str) -> str:
+        return "\n".join(f"{s['db']}.{s['name']} ({s['type']})" for s in self.catalog.sets(db))
+
+    listRegisteredSetsForADatabase = list_registered_sets_for_database
+
+    def list_nodes_in_cluster(self) -> str:
+        return "\n".join(str(n) for n in self.catalog.nodes())
+
+    listNodesInCluster = list_nodes_in_cluster
+
+    def list_user_defined_types(self) -> str:
+        return "\n".join(sorted(self.catalog.types()))
+
+    listUserDefinedTypes = list_user_defined_types
+
+    def list_all_registered_metadata(self) -> str:
+        return self.catalog.print_catalog()
+
+    listAllRegisteredMetadata = list_all_registered_metadata
+    printCatalogMetadata = list_all_registered_metadata
 
     def enable_self_learning(self, path: str = ":memory:", learned: bool = False):
         """Record job history and let create_set(..., policy='auto') pick partition keys."""

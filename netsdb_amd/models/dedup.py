@@ -33,16 +33,55 @@ class TensorBlockIndex:
     tables: Dict[str, torch.Tensor] = field(default_factory=dict)
     shapes: Dict[str, Tuple[int, int]] = field(default_factory=dict)
 
+    # --- FFMatrixBlockIndex parity (src/deduplication/headers/FFMatrixBlockIndex.h): per target set,
+    # distinct (shared) block id -> target block metadata (block_row, block_col, total_rows, total_cols)
+    targets: Dict[int, Dict[int, Tuple[int, int, int, int]]] = field(default_factory=dict)
+
+    @staticmethod
+    def set_key(db_id: int, type_id: int, set_id: int) -> int:
+        return int(type_id) + int(set_id) * 100000 + int(db_id) * 100000000
+
+    def insert_index(self, set_key: int, block_key: int, meta: Tuple[int, int, int, int]) -> bool:
+        self.targets.setdefault(int(set_key), {})[int(block_key)] = tuple(int(x) for x in meta)
+        return True
+
+    def remove_index(self, set_key: int, block_key: int) -> bool:
+        m = self.targets.get(int(set_key))
+        if m is None:
+            return False
+        m.pop(int(block_key), None)
+        return True
+
+    def get_target_metadata(self, set_key: int, block_key: int) -> Optional[Tuple[int, int, int, int]]:
+        return self.targets.get(int(set_key), {}).get(int(block_key))
+
+    def load_index_file(self, set_key: int, path: str, total_rows: int, total_cols: int,
+                        transpose: bool = False) -> Dict[int, Tuple[int, int, int, int]]:
+        """SharedFFMatrixBlockSet::loadIndexFromFile: lines 'blockKey,blockRow,blockCol' (transpose swaps
+        the target row/col), every target sized total_rows x total_cols."""
+        with open(path) as f:
+            for line in f:
+                parts = [x.strip() for x in line.replace(",", " ").split()]
+                if len(parts) < 3:
+                    continue
+                key, r, c = int(parts[0]), int(parts[1]), int(parts[2])
+                if transpose:
+                    r, c = c, r
+                self.insert_index(set_key, key, (r, c, total_rows, total_cols))
+        return dict(self.targets.get(int(set_key), {}))
+
     def to_json(self) -> dict:
         return {"block_rows": self.block_rows, "block_cols": self.block_cols,
                 "tables": {k: v.cpu().tolist() for k, v in self.tables.items()},
-                "shapes": {k: list(v) for k, v in self.shapes.items()}}
+                "shapes": {k: list(v) for k, v in self.shapes.items()},
+                "targets": {str(k): {str(b): list(m) for b, m in v.items()} for k, v in self.targets.items()}}
 
     @staticmethod
     def from_json(d: dict) -> "TensorBlockIndex":
         idx = TensorBlockIndex(d["block_rows"], d["block_cols"])
         idx.tables = {k: torch.tensor(v, dtype=torch.int64) for k, v in d["tables"].items()}
         idx.shapes = {k: tuple(v) for k, v in d["shapes"].items()}
+        idx.targets = {int(k): {int(b): tuple(m) for b, m in v.items()} for k, v in d.get("targets", {}).items()}
         return idx
 
 

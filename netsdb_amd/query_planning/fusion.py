@@ -475,6 +475,8 @@ class Fuser:
             st = self.engine.storage
             if st.has_set(c.db, c.set_name):
                 s = st.get_set(c.db, c.set_name)
+                if isinstance(s, DenseMatrixSet):
+                    s.resolve_shared()         # dedup: linked shared blocks -> the dense panel
                 if isinstance(s, DenseMatrixSet) and s.panel is not None:
                     return SourceNode(s)
         return None

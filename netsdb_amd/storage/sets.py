@@ -17,7 +17,7 @@ from __future__ import annotations
 import itertools
 import math
 import threading
-from typing import Iterator, List, Optional, Tuple
+from typing import Dict, Iterator, List, Optional, Tuple
 
 import torch
 
@@ -92,6 +92,68 @@ class Page:
         self.dirty = False
 
 
+class SharedLink:
+    """Pages of a shared set linked into a sharing set (reference: PDBClient::addSharedPage /
+    addSharedMapping, src/deduplication SharedFFMatrixBlockSet + PartitionTensorBlockSharedPageIterator).
+
+    The sharing set scans its own pages, then the linked pages of the shared set.  With a block
+    mapping (distinct block id -> target (block_row, block_col, total_rows, total_cols)) the shared
+    blocks' metadata is rewritten on the fly, exactly as the reference's shared-page iterator does;
+    a block without an entry gets block_row = block_col = -1 (the reference's "not found" marker)."""
+
+    def __init__(self, shared: "UserSet"):
+        self.shared = shared
+        self.pages: List[int] = []
+        self.keys: Optional[torch.Tensor] = None      # sorted distinct block ids
+        self.targets: Optional[torch.Tensor] = None   # [n, 4] int64 (block_row, block_col, total_rows, total_cols)
+
+    def set_mapping(self, mapping: dict):
+        items = sorted(mapping.items())
+        self.keys = torch.tensor([k for k, _ in items], dtype=torch.int64)
+        self.targets = torch.tensor([list(v) for _, v in items], dtype=torch.int64).reshape(-1, 4)
+
+    def batches(self, device=None) -> Iterator[RecordBatch]:
+        sh = self.shared
+        if isinstance(sh, DenseMatrixSet):
+            src = [sh.to_blocks(device)] if sh.panel is not None and (not self.pages or 0 in self.pages) else []
+        else:
+            src = []
+            for pno in self.pages:
+                if 0 <= pno < len(sh.pages):
+                    pg = sh.pages[pno]
+                    pg.pins += 1
+                    try:
+                        src.append(pg.load(device if device is not None else sh.device))
+                    finally:
+                        pg.pins -= 1
+        for b in src:
+            yield self._remap(b) if self.keys is not None else b
+
+    def _remap(self, b: RecordBatch) -> RecordBatch:
+        if b.n == 0 or "distinct_block_id" not in b.columns:
+            return b
+        ids = b.columns["distinct_block_id"]
+        dev = ids.device
+        keys, tg = self.keys.to(dev), self.targets.to(dev)
+        if keys.numel() == 0:
+            found = torch.zeros(b.n, dtype=torch.bool, device=dev)
+            pos = torch.zeros(b.n, dtype=torch.int64, device=dev)
+        else:
+            pos = torch.searchsorted(keys, ids).clamp(max=keys.numel() - 1)
+            found = keys[pos] == ids
+        cols = dict(b.columns)
+        for j, name in enumerate(("block_row", "block_col", "total_rows", "total_cols")):
+            miss = -1 if j < 2 else 0
+            cols[name] = torch.where(found, tg[pos, j], torch.full_like(ids, miss))
+        return RecordBatch(cols, b.n, b.type)
+
+    def num_records(self) -> int:
+        sh = self.shared
+        if isinstance(sh, DenseMatrixSet):
+            return sh.num_blocks() if sh.panel is not None else 0
+        return sum(sh.pages[p].n for p in self.pages if 0 <= p < len(sh.pages))
+
+
 class UserSet:
     """One node's partition of a stored set."""
 
@@ -108,6 +170,28 @@ class UserSet:
         self.lock = threading.RLock()
         self.partition_key = None       # (computation, lambda) describing how the set is partitioned
         self.stats = {"records": 0, "bytes": 0}
+        self.shared_links: Dict[Tuple[str, str], SharedLink] = {}   # dedup: pages linked from shared sets
+
+    # -------------------------------------------------------------- dedup page sharing
+    def link(self, shared: "UserSet") -> SharedLink:
+        key = (shared.db, shared.name)
+        if key not in self.shared_links:
+            self.shared_links[key] = SharedLink(shared)
+        return self.shared_links[key]
+
+    def add_shared_page(self, shared: "UserSet", page_no: int):
+        ln = self.link(shared)
+        if page_no not in ln.pages:
+            ln.pages.append(page_no)
+        self._shared_dirty = True
+
+    def set_shared_mapping(self, shared: "UserSet", mapping: dict):
+        self.link(shared).set_mapping(mapping)
+        self._shared_dirty = True
+
+    def shared_batches(self, device=None) -> Iterator[RecordBatch]:
+        for ln in list(self.shared_links.values()):
+            yield from ln.batches(device)
 
     # -------------------------------------------------------------- writes
     def add_batch(self, batch: RecordBatch):
@@ -143,6 +227,7 @@ class UserSet:
                 yield b
             finally:
                 p.pins -= 1
+        yield from self.shared_batches(device)
 
     def all(self, device=None) -> Optional[RecordBatch]:
         bs = list(self.scan(device))
@@ -151,7 +236,7 @@ class UserSet:
         return RecordBatch.concat(bs)
 
     def num_records(self) -> int:
-        return self.stats["records"]
+        return self.stats["records"] + sum(ln.num_records() for ln in self.shared_links.values())
 
     def nbytes(self) -> int:
         return self.stats["bytes"]
@@ -225,6 +310,8 @@ class DenseMatrixSet(UserSet):
 
     def matrix(self) -> torch.Tensor:
         """Logical [local_rows, total_cols] view (a transposed view when the panel is transposed)."""
+        if self.shared_links:
+            self.resolve_shared()
         if self.transposed:
             return self.panel[: self.total_cols, : self.local_rows].t()
         return self.panel[:, : self.total_cols]
@@ -259,10 +346,34 @@ class DenseMatrixSet(UserSet):
             if h > 0 and w > 0:
                 self.panel[r0:r0 + h, c0:c0 + w] = blk[:h, :w].to(self.panel.device, self.panel.dtype)
 
+    def resolve_shared(self):
+        """Scatter the linked shared blocks (metadata remapped) into this set's dense panel — the
+        HBM-resident form the MFMA kernels read.  Done once per change of the links."""
+        if not self.shared_links or not getattr(self, "_shared_dirty", False):
+            return self
+        for b in self.shared_batches():
+            if b.n == 0:
+                continue
+            keep = b.columns["block_row"] >= 0
+            if self.panel is not None and self.block_rows:
+                r0 = b.columns["block_row"] * self.block_rows
+                keep &= (r0 >= self.row_offset) & (r0 < self.row_offset + self.local_rows)
+            if not bool(keep.all()):
+                b = b.take(keep.nonzero().flatten())
+            if b.n:
+                self.add_batch(b)
+        self._shared_dirty = False
+        return self
+
     def scan(self, device=None) -> Iterator[RecordBatch]:
+        self.resolve_shared()
         if self.panel is None:
             return
         yield self.to_blocks(device)
+
+    def num_records(self) -> int:
+        self.resolve_shared()
+        return self.num_blocks()
 
     def to_blocks(self, device=None) -> RecordBatch:
         from ..objects.builtin import MatrixBlock

@@ -129,3 +129,50 @@ def test_dedup_exact_and_lsh(dev):
     assert pool2.stats["blocks_stored"] < 24
     idx = dedup.TensorBlockIndex.from_json(pool.index.to_json())
     assert torch.equal(idx.tables["b"], pool.index.tables["b"].cpu())
+
+
+def test_shared_pages_and_mapping(tmp_path):
+    """addSharedPage / addSharedMapping: a model set reads deduplicated blocks of a shared set, with
+    the block metadata remapped from an index file (FFTestWithDeduplication.cc flow)."""
+    from netsdb_amd.client import PDBClient
+    from netsdb_amd.models import blocks
+    from netsdb_amd.objects.builtin import FFMatrixBlock
+    from netsdb_amd.objects.record import RecordBatch
+
+    c = PDBClient(root=str(tmp_path), page_size=1 << 12)
+    br, bc = 4, 8
+    shared_blocks = torch.randn(3, br, bc)
+    n = 3
+    cols = {"block_row": torch.zeros(n, dtype=torch.int64), "block_col": torch.zeros(n, dtype=torch.int64),
+            "row_nums": torch.full((n,), br, dtype=torch.int64), "col_nums": torch.full((n,), bc, dtype=torch.int64),
+            "total_rows": torch.zeros(n, dtype=torch.int64), "total_cols": torch.zeros(n, dtype=torch.int64),
+            "distinct_block_id": torch.tensor([10, 11, 12]), "partition_by_col": torch.zeros(n, dtype=torch.bool),
+            "data": shared_blocks}
+    c.create_set("db", "shared", FFMatrixBlock)
+    c.add_local_data("db", "shared", RecordBatch(cols, n, FFMatrixBlock))
+    # the sharing model: an 8x16 matrix (2x2 blocks), block (1,1) private, the rest from the shared set
+    s = blocks.create_matrix_set(c, "db", "model", 8, 16, br, bc, dtype=torch.float32)
+    private = torch.randn(br, bc)
+    s.panel[br:, bc:16] = private
+    idx_file = tmp_path / "index.txt"
+    idx_file.write_text("10,0,0\n11,0,1\n12,1,0\n")
+    c.add_shared_page("db", "model", FFMatrixBlock, "db", "shared", FFMatrixBlock, 0, add_shared_set=True)
+    c.add_shared_mapping("db", "model", FFMatrixBlock, "db", "shared", FFMatrixBlock,
+                         file_name=str(idx_file), total_rows=8, total_cols=16)
+    m = blocks.to_tensor(c, "db", "model")
+    expect = torch.zeros(8, 16)
+    expect[:br, :bc], expect[:br, bc:] = shared_blocks[0], shared_blocks[1]
+    expect[br:, :bc], expect[br:, bc:] = shared_blocks[2], private
+    torch.testing.assert_close(m, expect)
+    # a transposed mapping swaps block row/col; unmapped ids get the (-1, -1) "not found" marker
+    c.create_set("db", "model2", FFMatrixBlock)
+    c.add_shared_mapping("db", "model2", FFMatrixBlock, "db", "shared", FFMatrixBlock,
+                         mapping={10: (0, 1)}, total_rows=16, total_cols=8, transpose=True)
+    got = RecordBatch.concat(list(c.get_set("db", "model2").scan()))
+    rows, cols_ = got.columns["block_row"].tolist(), got.columns["block_col"].tolist()
+    assert (rows[0], cols_[0]) == (1, 0) and rows[1:] == [-1, -1] and cols_[1:] == [-1, -1]
+    ti = dedup.TensorBlockIndex(br, bc)
+    key = dedup.TensorBlockIndex.set_key(0, 1, 2)
+    ti.load_index_file(key, str(idx_file), 8, 16)
+    assert ti.get_target_metadata(key, 12) == (1, 0, 8, 16)
+    assert ti.remove_index(key, 12) and ti.get_target_metadata(key, 12) is None
