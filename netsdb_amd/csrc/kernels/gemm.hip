@@ -45,6 +45,7 @@ struct GemmParams {
   int tiles_m, tiles_n;
   int vec_ws;               // N % 4 == 0: 4-column groups of the split-K slabs are 16-B aligned
   int vec_c;                // C rows/base aligned for 4-column vector stores (16 B f32, 8 B bf16)
+  int diag;                 // timing diagnostics (wrong results): 1 no epilogue global stores, 2 no operand loads
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
@@ -129,7 +130,7 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[TBM / WGM / 16
       const int wl = e / WTILE, loc = e % WTILE, r = loc / WC, c = loc % WC;
       const int wv = g0 + wl;
       const int row = m0 + (wv / WGN) * WR + r, col = n0 + (wv % WGN) * WC + c;
-      if (row >= p.M || col >= p.N) continue;
+      if (row >= p.M || col >= p.N || (p.diag & 1)) continue;
       const f32x4 v4 = *reinterpret_cast<const f32x4*>(st + wl * WTILE + r * WC + (c ^ (((r >> 2) & 1) << 4)));
       const int nv = min(4, p.N - col);
       if (ws) {
@@ -235,7 +236,7 @@ gemm_nt_tile_kernel(GemmParams p) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (nk > 0) {
+  if (nk > 0 && !(p.diag & 2)) {
     stage_tile<TBM, NW>(ra, smem, p.lda, rows_a, kbeg, kend, wave, lane);
     stage_tile<TBN, NW>(rb, smem + A_BYTES, p.ldb, rows_b, kbeg, kend, wave, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -244,7 +245,7 @@ gemm_nt_tile_kernel(GemmParams p) {
 
   for (int t = 0; t < nk; ++t) {
     char* cur = smem + (t & 1) * STG;
-    if (t + 1 < nk) {
+    if (t + 1 < nk && !(p.diag & 2)) {
       char* nxt = smem + ((t + 1) & 1) * STG;
       const int k1 = kbeg + (t + 1) * BK;
       stage_tile<TBM, NW>(ra, nxt, p.lda, rows_a, k1, kend, wave, lane);
@@ -534,7 +535,8 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(GemmParams p) {
 // ---------------------------------------------------------------- host side
 extern "C" {
 
-static int g_force_cfg = -1;   // -1 auto, 0 = 128x128, 1 = 256x256 2-stage, 2 = 256x256 8-phase (A/B testing)
+static int g_force_cfg = -1;  // -1 auto, 0 = 128x128, 1 = 256x256 2-stage, 2 = 256x256 8-phase (A/B testing)
+static int g_diag = 0;        // force_config / 100: kernel timing diagnostics (GemmParams::diag)
 
 // Tile config: the 256x256 tile (1 block/CU) when both dims fill it and there is enough work.
 static int pick_cfg(int M, int N, int K, int batch) {
@@ -545,7 +547,10 @@ static int pick_cfg(int M, int N, int K, int batch) {
   return (fills && big_tiles * ksteps >= 256LL * 32) ? 2 : 0;
 }
 
-void nsdb_gemm_force_config(int cfg) { g_force_cfg = cfg; }
+void nsdb_gemm_force_config(int cfg) {
+  g_force_cfg = cfg < 0 ? cfg : cfg % 100;
+  g_diag = cfg < 0 ? 0 : cfg / 100;
+}
 
 // Number of split-K slices the launcher will use; the caller sizes the workspace with it.
 int nsdb_gemm_splits(int M, int N, int K, int batch) {
@@ -590,6 +595,7 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
   if (p.splits < 1) p.splits = 1;
   p.act = act; p.bias_mode = bias ? bias_mode : 0; p.out_f32 = out_f32; p.accumulate = accumulate;
   p.alpha = alpha; p.dropout = dropout; p.seed = seed;
+  p.diag = g_diag;
   const int cfg = pick_cfg(M, N, K, batch);
   const int tbm = cfg ? 256 : nsdb::BM, tbn = cfg ? 256 : nsdb::BN;
   p.tiles_m = (M + tbm - 1) / tbm;

@@ -81,6 +81,7 @@ PYBIND11_MODULE(_native, m) {
       .def("drop_set", &BufferManager::drop_set)
       .def("flush_set", &BufferManager::flush_set, py::call_guard<py::gil_scoped_release>())
       .def("flush_all", &BufferManager::flush_all, py::call_guard<py::gil_scoped_release>())
+      .def("prefetch", &BufferManager::prefetch, py::call_guard<py::gil_scoped_release>())
       .def("bytes_used", &BufferManager::bytes_used)
       .def("set_pages", &BufferManager::set_pages)
       .def_property_readonly("page_size", &BufferManager::page_size)
@@ -89,6 +90,26 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("evictions", &BufferManager::evictions)
       .def_property_readonly("loads", &BufferManager::loads)
       .def_property_readonly("spill_dir", &BufferManager::spill_dir);
+
+  py::class_<Buzzer, std::shared_ptr<Buzzer>>(m, "Buzzer")
+      .def("wait", &Buzzer::wait, py::arg("timeout") = -1.0, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("done", &Buzzer::done)
+      .def_property_readonly("error", &Buzzer::error);
+
+  py::class_<WorkerQueue>(m, "WorkerQueue")
+      .def(py::init<int>(), py::arg("num_workers") = 4)
+      .def("submit_flush", [](WorkerQueue& q, BufferManager& bm, int64_t set_id) {
+        return q.submit([&bm, set_id] { bm.flush_set(set_id); });
+      }, py::keep_alive<0, 2>())
+      .def("submit_prefetch", [](WorkerQueue& q, BufferManager& bm, int64_t set_id, std::vector<int64_t> pages) {
+        return q.submit([&bm, set_id, pages] {
+          for (int64_t p : pages) bm.prefetch(set_id, p);
+        });
+      }, py::keep_alive<0, 2>())
+      .def("drain", &WorkerQueue::drain, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("num_workers", &WorkerQueue::num_workers)
+      .def_property_readonly("completed", &WorkerQueue::completed)
+      .def_property_readonly("pending", &WorkerQueue::pending);
 
   m.def("hash_columns", [](std::vector<py::array_t<int64_t, py::array::c_style | py::array::forcecast>> cols) {
     if (cols.empty()) throw std::runtime_error("hash_columns: no columns");

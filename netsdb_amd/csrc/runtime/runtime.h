@@ -5,10 +5,18 @@
 //   SlabAllocator    <- src/memory/{SlabAllocator,tlsf}.cc (here: best-fit with coalescing, used for
 //                       the HBM arena offsets of device-resident pages)
 //   hashing          <- src/lambdas/LambdaCreationFunctions.cc mapToPartitionId, HashPartitionSink
+//   WorkerQueue      <- src/work (PDBWorkerQueue, PDBWorker, PDBWork, PDBBuzzer): a fixed pool of
+//                       native threads running storage work (page prefetch / flush) off the Python thread
 #pragma once
+#include <atomic>
+#include <condition_variable>
 #include <cstddef>
 #include <cstdint>
+#include <deque>
+#include <functional>
 #include <list>
+#include <memory>
+#include <thread>
 #include <map>
 #include <mutex>
 #include <string>
@@ -100,6 +108,7 @@ class BufferManager {
   void drop_set(int64_t set_id);
   void flush_set(int64_t set_id);
   void flush_all();
+  bool prefetch(int64_t set_id, int64_t page_no);   // load an evicted page into a slot (stays unpinned)
   uint8_t* slot_ptr(int64_t slot);
   uint64_t bytes_used(int64_t set_id, int64_t page_no) const;
   int64_t resident_pages() const;
@@ -131,6 +140,48 @@ class BufferManager {
   PageFile* file_for(int64_t set_id);
   int64_t grab_slot();
   void write_back(int64_t slot);
+};
+
+// ------------------------------------------------------------------ work queue
+// PDBBuzzer: completion handle of one submitted work item.
+class Buzzer {
+ public:
+  void buzz(const std::string& error = "");
+  bool wait(double timeout_s);             // true when done (timeout_s < 0: wait forever)
+  bool done() const;
+  std::string error() const;
+
+ private:
+  mutable std::mutex mu_;
+  std::condition_variable cv_;
+  bool done_ = false;
+  std::string error_;
+};
+
+// PDBWorkerQueue: N worker threads draining a FIFO of work items.
+class WorkerQueue {
+ public:
+  explicit WorkerQueue(int num_workers);
+  ~WorkerQueue();
+  std::shared_ptr<Buzzer> submit(std::function<void()> work);
+  void drain();                            // wait until every submitted item finished
+  int num_workers() const { return (int)threads_.size(); }
+  int64_t completed() const { return completed_.load(); }
+  int64_t pending() const;
+
+ private:
+  struct Item {
+    std::function<void()> fn;
+    std::shared_ptr<Buzzer> buzzer;
+  };
+  void loop();
+  std::vector<std::thread> threads_;
+  std::deque<Item> q_;
+  mutable std::mutex mu_;
+  std::condition_variable cv_, idle_cv_;
+  bool stop_ = false;
+  int active_ = 0;
+  std::atomic<int64_t> completed_{0};
 };
 
 // ------------------------------------------------------------------ hashing

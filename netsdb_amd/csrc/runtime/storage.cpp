@@ -296,6 +296,18 @@ void BufferManager::flush_set(int64_t set_id) {
   if (files_.count(set_id)) files_[set_id]->sync();
 }
 
+bool BufferManager::prefetch(int64_t set_id, int64_t page_no) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (table_.count(PageKey{set_id, page_no})) return false;       // already resident
+    PageFile* f = file_for(set_id);
+    if (!f->has_page((uint64_t)page_no)) return false;
+  }
+  pin(set_id, page_no, false);
+  unpin(set_id, page_no, false, 0);
+  return true;
+}
+
 void BufferManager::flush_all() {
   std::lock_guard<std::mutex> g(mu_);
   for (auto& kv : table_) write_back(kv.second);

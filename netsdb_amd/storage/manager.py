@@ -23,7 +23,8 @@ DEFAULT_PAGE_SIZE = 64 << 20
 
 class StorageManager:
     def __init__(self, root: Optional[str] = None, device=None, page_size: int = DEFAULT_PAGE_SIZE,
-                 pool_pages: int = 16, device_budget: Optional[int] = None, rank: int = 0):
+                 pool_pages: int = 16, device_budget: Optional[int] = None, rank: int = 0, io_workers: int = 2,
+                 read_ahead: int = 4):
         self.root = root or tempfile.mkdtemp(prefix="netsdb_amd_")
         os.makedirs(self.root, exist_ok=True)
         self.device = torch.device(device) if device is not None else None
@@ -32,6 +33,9 @@ class StorageManager:
         spill = os.path.join(self.root, f"node{rank}")
         os.makedirs(spill, exist_ok=True)
         self.buffer_manager = _ext.native().BufferManager(page_size, pool_pages, spill)
+        # native I/O workers (src/work PDBWorkerQueue): page read-ahead for scans, background flushes
+        self.workers = _ext.native().WorkerQueue(io_workers)
+        self.read_ahead = max(0, min(read_ahead, pool_pages // 2))
         if device_budget is None and self.device is not None and self.device.type == "cuda":
             total = torch.cuda.get_device_properties(self.device).total_memory
             device_budget = int(total * 0.85)
@@ -121,10 +125,33 @@ class StorageManager:
         return freed
 
     def flush(self):
+        """Write every persistent page image to the pool, then let the native workers write the pool's
+        dirty frames to the page files (set by set) and wait for them (checkpoint barrier)."""
+        buzzers = []
         for s in self.sets.values():
             if s.persistent:
-                s.flush()
+                s.persist_pages()
+                buzzers.append(self.workers.submit_flush(self.buffer_manager, s.set_id))
+        for b in buzzers:
+            b.wait()
+            if b.error:
+                raise RuntimeError(f"page flush failed: {b.error}")
         self.buffer_manager.flush_all()
+
+    def flush_async(self):
+        """Background checkpoint: persist page images now, return the buzzers of the file writes."""
+        out = []
+        for s in self.sets.values():
+            if s.persistent:
+                s.persist_pages()
+                out.append(self.workers.submit_flush(self.buffer_manager, s.set_id))
+        return out
+
+    def prefetch(self, uset, page_nos):
+        """Queue native read-ahead of evicted pages (page file -> pool slot) for an upcoming scan."""
+        if page_nos:
+            return self.workers.submit_prefetch(self.buffer_manager, uset.set_id, list(page_nos))
+        return None
 
     def summary(self) -> dict:
         return {
@@ -134,6 +161,8 @@ class StorageManager:
             "device_budget": self.device_budget,
             "pool_resident_pages": self.buffer_manager.resident_pages,
             "pool_evictions": self.buffer_manager.evictions,
+            "pool_loads": self.buffer_manager.loads,
+            "io_work_completed": self.workers.completed,
             **self.stats,
         }
 

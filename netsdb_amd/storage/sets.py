@@ -219,7 +219,17 @@ class UserSet:
     # -------------------------------------------------------------- reads
     def scan(self, device=None) -> Iterator[RecordBatch]:
         device = device if device is not None else self.device
-        for p in list(self.pages):
+        pages = list(self.pages)
+        ra = getattr(self.manager, "read_ahead", 0)
+        queued = 0
+        for i, p in enumerate(pages):
+            if ra and i >= queued:
+                # native read-ahead: evicted pages among the next `ra` are pulled from the page file into
+                # pool slots by the I/O workers while this page is deserialised / consumed
+                nxt = [q.page_no for q in pages[i: i + ra] if q.batch is None]
+                if nxt:
+                    self.manager.prefetch(self, nxt)
+                queued = i + ra
             p.pins += 1
             try:
                 b = p.load(device)
@@ -241,9 +251,12 @@ class UserSet:
     def nbytes(self) -> int:
         return self.stats["bytes"]
 
-    def flush(self):
+    def persist_pages(self):
         for p in self.pages:
             p.persist()
+
+    def flush(self):
+        self.persist_pages()
         self.manager.buffer_manager.flush_set(self.set_id)
 
     def page_meta(self) -> list:
@@ -410,6 +423,12 @@ class DenseMatrixSet(UserSet):
         """Persist the panel (as its MatrixBlock records) through the page pool into the set's page file."""
         if self.panel is None:
             return
+        self.persist_pages()
+        self.manager.buffer_manager.flush_set(self.set_id)
+
+    def persist_pages(self):
+        if self.panel is None:
+            return
         b = self.to_blocks("cpu")
         bm = self.manager.buffer_manager
         data = serialize_batch(b)
@@ -421,7 +440,6 @@ class DenseMatrixSet(UserSet):
             bm.slot_view(slot)[: len(chunk)] = chunk
             bm.unpin(self.set_id, page, True, len(chunk))
             page += 1
-        bm.flush_set(self.set_id)
         self.flushed_chunks = page
 
     def geometry(self) -> dict:

@@ -105,3 +105,48 @@ def test_checkpoint_resume(tmp_path):
     torch.testing.assert_close(B.to_tensor(c2, "d", "m"), m)
     c2.create_set("d", "new", Employee)      # fresh ids do not collide with resumed sets
     assert c2.get_set("d", "new").set_id > c2.get_set("d", "m").set_id
+
+
+def test_native_worker_queue_flush_and_read_ahead(tmp_path):
+    """src/work parity: native WorkerQueue + Buzzer drive background page flushes and scan read-ahead."""
+    from netsdb_amd import _ext
+    from netsdb_amd.client import PDBClient
+    from netsdb_amd.objects.builtin import Employee
+
+    nat = _ext.native()
+    q = nat.WorkerQueue(3)
+    bm = nat.BufferManager(1 << 12, 4, str(tmp_path / "pool"))
+    for p in range(8):                       # 8 pages through a 4-slot pool: half are evicted to the file
+        slot = bm.pin(7, p, True)
+        bm.slot_view(slot)[:4] = bytes([p, p, p, p])
+        bm.unpin(7, p, True, 4)
+    assert bm.evictions >= 4
+    b = q.submit_flush(bm, 7)
+    assert b.wait(30.0) and b.done and b.error == ""
+    loads0 = bm.loads
+    b = q.submit_prefetch(bm, 7, [0, 1])     # evicted pages come back into pool slots
+    assert b.wait(30.0) and b.error == ""
+    assert bm.loads >= loads0 + 1
+    slot = bm.pin(7, 0, False)
+    assert bytes(bm.slot_view(slot)[:4]) == bytes([0, 0, 0, 0])
+    bm.unpin(7, 0, False, 0)
+    q.drain()
+    assert q.pending == 0 and q.completed == 2
+
+    # through the client: a set larger than the device budget is spilled, then scanned with read-ahead
+    c = PDBClient(root=str(tmp_path / "db"), page_size=1 << 12, pool_pages=4)
+    c.create_database("d")
+    c.create_set("d", "e", Employee)
+    emps = [Employee(f"e{i}", i % 60, "eng", float(i)) for i in range(600)]
+    c.send_data("d", "e", emps)
+    pages = c.get_set("d", "e").pages
+    assert len(pages) > 4
+    for p in pages:                          # spill every page: the 4-slot pool pushes most to the file
+        p.spill()
+    assert all(p.batch is None for p in pages)
+    loads0 = c.storage.buffer_manager.loads
+    got = sorted(o.name for o in c.get_set_iterator("d", "e"))
+    assert got == sorted(e.name for e in emps)
+    assert c.storage.buffer_manager.loads > loads0
+    c.flush_data()
+    assert c.storage.summary()["io_work_completed"] >= 1
