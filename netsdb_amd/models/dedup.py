@@ -178,9 +178,15 @@ class BlockPool:
     def dedup_ratio(self) -> float:
         return self.stats["blocks_stored"] / max(1, self.stats["blocks_in"])
 
-    def pack_pages(self, blocks_per_page: int) -> List[List[int]]:
-        """Greedy page packing: blocks shared by the same set of models go to the same pages, so a
-        model touches as few pages as possible (model-inference/deduplication/page-packing)."""
+    def pack_pages(self, blocks_per_page: int, algorithm: str = "greedy1") -> List[List[int]]:
+        """Page packing: blocks shared by the same set of models go to the same pages, so a model
+        touches as few pages as possible (model-inference/deduplication/page-packing).  ``algorithm``:
+        greedy1 (equivalence classes, default), two_stage, greedy2, baseline (models/page_packing.py)."""
+        if algorithm != "greedy1":
+            from .page_packing import pack
+
+            models = [set(t.flatten().tolist()) for t in self.index.tables.values()]
+            return pack(models, blocks_per_page, algorithm).pages
         owners: Dict[int, set] = {}
         for name, t in self.index.tables.items():
             for b in t.flatten().tolist():
