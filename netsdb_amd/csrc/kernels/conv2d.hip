@@ -235,8 +235,12 @@ struct ConvRowParams {
                  // staging, 8 prologue only, 16 no compute, 32 s_memtime stamps over the output
 };
 
-template <int ACT>
+// STAGED (LDS-staged NCHW bf16 output) and the diagnostics switch are template parameters: a runtime
+// flag here made hipcc wrap every MFMA of the inner loop in its own branch (+ s_nop padding).
+// DIAG = false compiles every diagnostic test to a constant.
+template <int ACT, bool STAGED, bool DIAG>
 __global__ void __launch_bounds__(256, 2) conv2d_rows_kernel(ConvRowParams p) {
+  const int var = DIAG ? p.variant : 0;
   __shared__ __attribute__((aligned(16))) char smem[CVR_BUF + CVR_OSTAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -342,14 +346,14 @@ __global__ void __launch_bounds__(256, 2) conv2d_rows_kernel(ConvRowParams p) {
 
   const long long OHW = (long long)p.OH * p.OW;
   unsigned short* ostage = reinterpret_cast<unsigned short*>(smem + CVR_BUF);   // [32 oc][segs] bf16
-  const bool staged = p.nchw_out && !p.out_f32 && (p.OW & 1) == 0;
+  constexpr bool staged = STAGED;
   // stage layout "segment-major" [32 oc][segs]: the TR output rows of one oc plane are adjacent in
   // NCHW, so each oc's rows_valid*OW outputs are ONE contiguous run both in LDS and in HBM and a
   // wave moves it with 8-B (4-pixel) loads/stores. segs = 4*OW rounded so that segs/2 dwords is
   // 2 mod 4: the 16 oc a ds_write lane group touches land on 16 distinct banks.
   const int segs = p.segs;
   int g = blockIdx.x;
-  if (p.variant & 8) return;          // diagnostics: prologue only
+  if (var & 8) return;          // diagnostics: prologue only
   // variant 7: s_memtime stamps (diagnostic build: written over the start of the output)
   unsigned long long st_t0 = 0, st_stage = 0, st_work = 0, st_tmp = 0, st_comp = 0, st_bar = 0;
   auto stamp = [&]() -> unsigned long long {
@@ -359,15 +363,15 @@ __global__ void __launch_bounds__(256, 2) conv2d_rows_kernel(ConvRowParams p) {
     __builtin_amdgcn_sched_barrier(0);
     return t;
   };
-  if (p.variant & 32) st_t0 = stamp();
+  if (var & 32) st_t0 = stamp();
   if (g < p.ngroups) fetch(g);
   for (; g < p.ngroups; g += gridDim.x) {
     const int n = g / p.groups_per_img, oh0 = (g % p.groups_per_img) * CVR_TR, oh = oh0 + wave;
-    if (p.variant & 32) st_tmp = stamp();
+    if (var & 32) st_tmp = stamp();
     __syncthreads();                                   // previous group's readers of both buffers are done
     store_rows(smem);
     __syncthreads();
-    if (p.variant & 32) { const unsigned long long t = stamp(); st_stage += t - st_tmp; st_tmp = t; }
+    if (var & 32) { const unsigned long long t = stamp(); st_stage += t - st_tmp; st_tmp = t; }
     if (g + (int)gridDim.x < p.ngroups) fetch(g + gridDim.x);   // next group's rows in flight during compute
     // two passes over the row, 32 output channels each: the [32 oc][TR][OWS] bf16 stage is 28 KB, so
     // two blocks fit a CU (the A fragments are re-read from LDS for the second half — cheap)
@@ -375,7 +379,7 @@ __global__ void __launch_bounds__(256, 2) conv2d_rows_kernel(ConvRowParams p) {
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       if (!staged && half == 1) break;
-      if (oh < p.OH && !(p.variant & 16)) {
+      if (oh < p.OH && !(var & 16)) {
         auto load_a = [&](int t, bf16x8 (&af)[CVR_NKS]) {
 #pragma unroll
           for (int ks = 0; ks < CVR_NKS; ++ks) {
@@ -385,32 +389,26 @@ __global__ void __launch_bounds__(256, 2) conv2d_rows_kernel(ConvRowParams p) {
             af[ks][4] = (short)a1.x; af[ks][5] = (short)(a1.x >> 16); af[ks][6] = (short)a1.y; af[ks][7] = (short)(a1.y >> 16);
           }
         };
+        // A fragments of tile t+1 are read from LDS while tile t's MFMAs run (software pipeline; the
+        // 16x16x32 MFMA issues back to back on one accumulator chain, so one chain per n-tile)
+        bf16x8 af[CVR_NKS];
+        load_a(0, af);
         for (int t = 0; t < p.ntiles; ++t) {
           f32x4 acc[4];
 #pragma unroll
           for (int nt = 0; nt < 4; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-          bf16x8 af[CVR_NKS];
-          load_a(t, af);
-          // staged: this half's 2 n-tiles; direct: all 4. Even and odd k-steps accumulate into separate
-          // registers (two independent MFMA chains per n-tile, summed after the loop)
-          if (!(p.variant & 2)) {
-            f32x4 acc2[4];
-#pragma unroll
-            for (int nt = 0; nt < 4; ++nt) acc2[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (!(var & 2)) {
 #pragma unroll
             for (int ks = 0; ks < CVR_NKS; ++ks)
 #pragma unroll
               for (int nt = 0; nt < 4; ++nt)
-                if (!staged || (nt >> 1) == half) {
-                  if (ks & 1) acc2[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks], bw[nt][ks], acc2[nt], 0, 0, 0);
-                  else acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks], bw[nt][ks], acc[nt], 0, 0, 0);
-                }
-#pragma unroll
-            for (int nt = 0; nt < 4; ++nt) acc[nt] += acc2[nt];
+                if (!staged || (nt >> 1) == half)
+                  acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks], bw[nt][ks], acc[nt], 0, 0, 0);
           } else {
 #pragma unroll
             for (int ks = 0; ks < CVR_NKS; ++ks) acc[0][0] += (float)af[ks][0];
           }
+          if (t + 1 < p.ntiles) load_a(t + 1, af);
           const int owb = t * 16 + (lane >> 4) * 4;
 #pragma unroll
           for (int nt = 0; nt < 4; ++nt) {
@@ -421,7 +419,7 @@ __global__ void __launch_bounds__(256, 2) conv2d_rows_kernel(ConvRowParams p) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) vv[r] = act_t<ACT>(acc[nt][r] + bias_v[nt]);
             if (staged) {
-              if (!(p.variant & 4)) {   // [ocl - 32*half][row*OW + ow]: 2 dword writes (OW even -> 4-B aligned)
+              if (!(var & 4)) {   // [ocl - 32*half][row*OW + ow]: 2 dword writes (OW even -> 4-B aligned)
                 unsigned* dst = reinterpret_cast<unsigned*>(ostage + (ocl - 32 * half) * segs + wave * p.OW + owb);
                 if (owb + 1 < p.OW) dst[0] = pack_bf16x2(vv[0], vv[1]);
                 if (owb + 3 < p.OW) dst[1] = pack_bf16x2(vv[2], vv[3]);
@@ -442,10 +440,10 @@ __global__ void __launch_bounds__(256, 2) conv2d_rows_kernel(ConvRowParams p) {
         }
       }
       if (!staged) break;
-      if (p.variant & 32) { const unsigned long long t = stamp(); st_comp += t - st_tmp; st_tmp = t; }
+      if (var & 32) { const unsigned long long t = stamp(); st_comp += t - st_tmp; st_tmp = t; }
       __syncthreads();
-      if (p.variant & 32) { const unsigned long long t = stamp(); st_bar += t - st_tmp; st_tmp = t; }
-      if (!(p.variant & 1)) {
+      if (var & 32) { const unsigned long long t = stamp(); st_bar += t - st_tmp; st_tmp = t; }
+      if (!(var & 1)) {
         // one contiguous run of seg = rows_valid*OW outputs per oc plane; wave w stores oc w, w+4, ..
         // (all LDS reads first, then the stores: a read->store pair per oc would expose the LDS latency)
         const int noc = min(32, p.OC - (oc0 + 32 * half));
@@ -491,9 +489,9 @@ __global__ void __launch_bounds__(256, 2) conv2d_rows_kernel(ConvRowParams p) {
       }
       __syncthreads();
     }
-    if (p.variant & 32) st_work += stamp() - st_tmp;
+    if (var & 32) st_work += stamp() - st_tmp;
   }
-  if ((p.variant & 32) && lane == 0) {
+  if ((var & 32) && lane == 0) {
     unsigned long long* d = reinterpret_cast<unsigned long long*>(p.out) + (blockIdx.x * 4 + wave) * 4;
     d[0] = stamp() - st_t0; d[1] = st_stage; d[2] = st_comp; d[3] = st_bar;
   }
@@ -564,13 +562,25 @@ int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* ou
     {
       const int blocks = std::min(q.ngroups, 256 * 2);     // persistent: two blocks per CU
       const dim3 grid(blocks, (OC + 63) / 64);
-      switch (act) {
-        case nsdb::ACT_RELU: hipLaunchKernelGGL(nsdb::conv2d_rows_kernel<nsdb::ACT_RELU>, grid, dim3(256), 0, stream, q); break;
-        case nsdb::ACT_SIGMOID: hipLaunchKernelGGL(nsdb::conv2d_rows_kernel<nsdb::ACT_SIGMOID>, grid, dim3(256), 0, stream, q); break;
-        case nsdb::ACT_EXP: hipLaunchKernelGGL(nsdb::conv2d_rows_kernel<nsdb::ACT_EXP>, grid, dim3(256), 0, stream, q); break;
-        case nsdb::ACT_TANH: hipLaunchKernelGGL(nsdb::conv2d_rows_kernel<nsdb::ACT_TANH>, grid, dim3(256), 0, stream, q); break;
-        default: hipLaunchKernelGGL(nsdb::conv2d_rows_kernel<nsdb::ACT_NONE>, grid, dim3(256), 0, stream, q); break;
+      const bool staged = nchw_out && !out_f32 && (p.OW & 1) == 0;
+      if (q.variant != 0) {   // diagnostics build (timing only): runtime variant bits, no activation
+        if (staged) hipLaunchKernelGGL((nsdb::conv2d_rows_kernel<nsdb::ACT_NONE, true, true>), grid, dim3(256), 0, stream, q);
+        else hipLaunchKernelGGL((nsdb::conv2d_rows_kernel<nsdb::ACT_NONE, false, true>), grid, dim3(256), 0, stream, q);
+        return (int)hipGetLastError();
       }
+#define NSDB_CVR_LAUNCH(A)                                                                                      \
+  do {                                                                                                        \
+    if (staged) hipLaunchKernelGGL((nsdb::conv2d_rows_kernel<A, true, false>), grid, dim3(256), 0, stream, q); \
+    else hipLaunchKernelGGL((nsdb::conv2d_rows_kernel<A, false, false>), grid, dim3(256), 0, stream, q);       \
+  } while (0)
+      switch (act) {
+        case nsdb::ACT_RELU: NSDB_CVR_LAUNCH(nsdb::ACT_RELU); break;
+        case nsdb::ACT_SIGMOID: NSDB_CVR_LAUNCH(nsdb::ACT_SIGMOID); break;
+        case nsdb::ACT_EXP: NSDB_CVR_LAUNCH(nsdb::ACT_EXP); break;
+        case nsdb::ACT_TANH: NSDB_CVR_LAUNCH(nsdb::ACT_TANH); break;
+        default: NSDB_CVR_LAUNCH(nsdb::ACT_NONE); break;
+      }
+#undef NSDB_CVR_LAUNCH
       return (int)hipGetLastError();
     }
   }
