@@ -544,7 +544,9 @@ static int pick_cfg(int M, int N, int K, int batch) {
   const long long big_tiles = (long long)((M + 255) / 256) * ((N + 255) / 256) * batch;
   const bool fills = M >= 192 && N >= 192;
   const long long ksteps = (K + nsdb::BK - 1) / nsdb::BK;
-  return (fills && big_tiles * ksteps >= 256LL * 32) ? 2 : 0;
+  // 8-phase 256^2 when there is a long mainloop, or when >= 3/4 of the CUs get a tile and K spans at
+  // least 16 k-tiles (the FF output layer 1000x14588x1000: 60 us vs 75 us for 128^2, kernel trace)
+  return (fills && (big_tiles * ksteps >= 256LL * 32 || (big_tiles >= 192 && ksteps >= 16))) ? 2 : 0;
 }
 
 void nsdb_gemm_force_config(int cfg) {
@@ -561,7 +563,9 @@ int nsdb_gemm_splits(int M, int N, int K, int batch) {
   // fill the chip: 256 CUs x (2 blocks of 128^2 | 1 block of 256^2); keep >= 8 k-steps per split
   const int target = cfg ? 256 : 512;
   int splits = 1;
-  if (tiles < target) {
+  // >= 3/4 of the chip busy: a split's f32 slabs + reduce pass cost more than the idle CUs (1000x14588x1024:
+  // 51 us + 24 us reduce with 2 splits vs 60 us unsplit)
+  if (tiles < target && !(cfg && tiles >= 192)) {
     splits = (target + tiles - 1) / tiles;
     splits = std::min(splits, std::max(1, ksteps / 8));
   }

@@ -181,10 +181,19 @@ class MatmulNode(Node):
             # X = opA as [M,K] K-contig <=> opA physical not transposed; Y = opB^T as [N,K]
             X = _kslice(opA.physical(False), M, K8)
             Y = _kslice(opB.physical(True), N, K8)
+            # result rows padded to 64 elements (128-B aligned for bf16): a consumer GEMM's LDS-DMA then
+            # moves whole cache lines per row segment (1000-wide bf16 rows straddle lines: +12% on the FF
+            # output layer); consumers read the [rows, cols] view, the padding is never touched
+            pr, pc = (M, N) if phys_is_c else (N, M)
+            out = None
+            if X.is_cuda and pc % 64 and pc >= 64:
+                out = torch.empty(pr, (pc + 63) // 64 * 64, dtype=odt, device=X.device)[:, :pc]
             if phys_is_c:
-                phys = ops.gemm_nt(X, Y, bias_t, mode, act, out_dtype=odt, dropout=self.dropout, seed=self.seed)
+                phys = ops.gemm_nt(X, Y, bias_t, mode, act, out_dtype=odt, dropout=self.dropout, seed=self.seed,
+                                   out=out)
             else:
-                phys = ops.gemm_nt(Y, X, bias_t, mode, act, out_dtype=odt, dropout=self.dropout, seed=self.seed)
+                phys = ops.gemm_nt(Y, X, bias_t, mode, act, out_dtype=odt, dropout=self.dropout, seed=self.seed,
+                                   out=out)
         part, offset, total = None, 0, None
         if opA.part == "rows":
             part, offset, total = "rows", opA.offset, opA.total

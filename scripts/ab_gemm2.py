@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--out-ld-align", type=int, default=1, help="C row stride alignment (elements)")
+    ap.add_argument("--splits", type=int, default=0, help="force split-K (0 = launcher's choice)")
     ap.add_argument("--epis", default="plain_bf16,bias_exp_f32")
     ap.add_argument("--ld-align", type=int, default=8, help="operand row stride alignment (elements)")
     a = ap.parse_args()
@@ -62,9 +63,10 @@ def main():
             _ext.hip().gemm_force_config(c)
             for epi in a.epis.split(","):
                 if epi == "plain_bf16":
-                    fn = lambda: ops.gemm_nt(A, B, out=Cb)  # noqa: E731
+                    fn = lambda: ops.gemm_nt(A, B, out=Cb, splits=a.splits)  # noqa: E731
                 else:
-                    fn = lambda: ops.gemm_nt(A, B, bias, ops.BIAS_COL, ops.ACT_EXP, out_dtype=torch.float32, out=Cf)  # noqa: E731
+                    fn = lambda: ops.gemm_nt(A, B, bias, ops.BIAS_COL, ops.ACT_EXP, out_dtype=torch.float32, out=Cf,
+                                               splits=a.splits)  # noqa: E731
                 ms = timeit(fn, a.iters, a.rounds)
                 res[f"cfg{c}_{epi}_us"] = round(ms * 1e3, 1)
                 res[f"cfg{c}_{epi}_tflops"] = round(2.0 * M * N * K / ms / 1e9, 1)
