@@ -13,7 +13,7 @@ simply an embedded database.  (A socket front end for remote clients lives in
 from __future__ import annotations
 
 import os
-from typing import Iterable, Iterator, List, Optional, Sequence
+from typing import Iterator, List, Optional
 
 import torch
 
@@ -383,8 +383,9 @@ class PDBClient:
     listAllRegisteredMetadata = list_all_registered_metadata
     printCatalogMetadata = list_all_registered_metadata
 
-    def enable_self_learning(self, path: str = ":memory:", learned: bool = False):
-        """Record job history and let create_set(..., policy='auto') pick partition keys."""
+    def enable_self_learning(self, path: str = ":memory:", learned=False):
+        """Record job history and let create_set(..., policy='auto') pick partition keys.
+        ``learned``: False rule-based, True bandit, "drl" the Q-network agent (selflearning.DRLAdvisor)."""
         from .selflearning import SelfLearningHook
 
         return SelfLearningHook(self, path, learned)
@@ -394,5 +395,3 @@ class PDBClient:
 
 
 __all__ = ["PDBClient"]
-
-_ = (Iterable, Sequence)

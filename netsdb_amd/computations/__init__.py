@@ -18,9 +18,7 @@ from __future__ import annotations
 
 import itertools
 from dataclasses import dataclass, field
-from typing import Any, Callable, List, Optional, Sequence
-
-import torch
+from typing import List, Optional
 
 from ..lambdas import Arg, Lambda, Literal
 
@@ -310,5 +308,3 @@ __all__ = ["Computation", "ScanSet", "ScanUserSet", "WriteSet", "WriteUserSet", 
            "MultiSelectionComp", "JoinComp", "AggregateComp", "ClusterAggregateComp", "PartitionComp", "TopKComp",
            "BlockMatmul", "BlockSum", "BiasAct", "RowSoftmax", "Elementwise", "Transpose", "Reduce", "Inverse",
            "Duplicate"]
-
-_ = (Any, Callable, Sequence, torch)

@@ -11,7 +11,7 @@ happen exactly once per sink on every rank, so ranks stay in lock-step.
 from __future__ import annotations
 
 import time
-from typing import Any, Dict, List, Optional
+from typing import Dict, List, Optional
 
 import torch
 
@@ -410,5 +410,3 @@ class _JobState:
 
 
 __all__ = ["QueryEngine", "JobStats"]
-
-_ = Any

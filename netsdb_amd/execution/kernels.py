@@ -8,7 +8,7 @@ on the GPU for device-resident columns.
 """
 from __future__ import annotations
 
-from typing import Any, List, Sequence, Tuple
+from typing import Any, List, Tuple
 
 import torch
 import xxhash
@@ -201,5 +201,3 @@ def split_by_dest(batch: RecordBatch, dest: torch.Tensor, nparts: int) -> List[R
 
 __all__ = ["mix64", "hash_keys", "column_to_int64", "join_match", "group_ids", "segment_reduce", "take_reps",
            "partition_of", "split_by_dest"]
-
-_ = Sequence

@@ -10,8 +10,7 @@ from __future__ import annotations
 
 import torch
 
-from ..computations import (AggregateComp, BlockMatmul, BlockSum, Duplicate, Elementwise, Inverse, JoinComp,
-                            MultiSelectionComp, Reduce, SelectionComp, Transpose)
+from ..computations import (AggregateComp, BlockMatmul, Duplicate, Elementwise, Inverse, JoinComp, MultiSelectionComp, Reduce, SelectionComp, Transpose)
 from ..lambdas import make_batch_lambda, make_lambda_from_method
 from ..models.ff import FFAggMatrix, _bmm_nt, mk_blocks
 from ..objects.builtin import MatrixBlock
@@ -215,5 +214,3 @@ class LADuplicateColMultiSelection(_DupSel):
 
 
 __all__ = [n for n in dir() if n.startswith("LA")]
-
-_ = BlockSum

@@ -12,7 +12,7 @@ from __future__ import annotations
 
 import itertools
 from dataclasses import dataclass
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Dict, List, Sequence, Tuple
 
 from ..computations import (AggregateComp, Computation, JoinComp, MultiSelectionComp, PartitionComp, ScanSet,
                             SelectionComp, TopKComp, WriteSet)
@@ -256,5 +256,3 @@ def compile_tcap(sinks: Sequence[Computation]) -> CompiledPlan:
 
 
 __all__ = ["TupleSpec", "CompiledPlan", "TCAPCompiler", "compile_tcap", "compile_lambda"]
-
-_ = Optional

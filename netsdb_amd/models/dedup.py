@@ -209,5 +209,3 @@ def pages_touched(pool: BlockPool, pages: List[List[int]], name: str) -> int:
 
 __all__ = ["TensorBlockIndex", "BlockPool", "block_hashes", "lsh_signatures", "to_blocks", "from_blocks",
            "pages_touched"]
-
-_ = Optional

@@ -18,7 +18,7 @@ from .. import ops
 from ..computations import SelectionComp
 from ..lambdas import make_batch_lambda
 from ..objects.record import RecordBatch
-from .ff import (FFAggMatrix, FFInputLayerJoin, FFMatrixBlockScanner, FFMatrixWriter, FFTransposeBiasSumSigmoid,
+from .ff import (FFAggMatrix, FFMatrixBlockScanner, FFMatrixWriter, FFTransposeBiasSumSigmoid,
                  create_output_set)
 from . import blocks as B
 
@@ -86,5 +86,3 @@ class FullyConnectedNetwork(SelectionComp):
 
 
 __all__ = ["load_logreg", "inference_unit_log_reg", "FullyConnectedNetwork"]
-
-_ = FFInputLayerJoin

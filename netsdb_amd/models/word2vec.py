@@ -12,9 +12,8 @@ Three plans over an embedding set (vocab x dim, block-partitioned):
 """
 from __future__ import annotations
 
-import math
 import time
-from typing import List, Optional
+from typing import List
 
 import torch
 
@@ -160,5 +159,3 @@ class SemanticClassifier:
 
 __all__ = ["EmbeddingSegment", "EmbeddingLookupSparse", "load_embeddings", "word2vec_matmul", "word2vec_lookup",
            "word2vec_sparse", "assemble_segments", "SemanticClassifier"]
-
-_ = (math, Optional)

@@ -16,7 +16,6 @@ UDF lambdas operate on whole columns (vectorised, GPU) or, for opaque Python lam
 """
 from __future__ import annotations
 
-import dataclasses
 from typing import Any, Dict, Iterable, List, Optional, Sequence
 
 import torch
@@ -428,5 +427,3 @@ def batch_of(records: Iterable[Any], type_=None, device=None) -> RecordBatch:
 __all__ = ["PDBObject", "Tensor", "Vector", "RecordBatch", "RecordView", "register_type", "lookup_type",
            "registered_types", "batch_of", "make_column", "column_item", "column_take", "column_concat",
            "column_kind", "column_slice", "column_len"]
-
-_ = dataclasses  # kept for users defining dataclass-style helpers

@@ -14,7 +14,7 @@ BroadcastJoinBuildHTJobStage and HashPartitionedJoinBuildHTJobStage).
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import Callable, Dict, List, Optional
+from typing import Callable, Dict, List
 
 STREAMING = {"APPLY", "FILTER", "FLATTEN", "HASHLEFT", "HASHRIGHT", "HASHONE"}
 
@@ -185,5 +185,3 @@ class Planner:
 
 
 __all__ = ["Planner", "PhysicalPlan", "Stage"]
-
-_ = Optional

@@ -11,8 +11,9 @@ partition key:
 * :class:`RuleBasedAdvisor` — the reference rule: the key of the most frequent shuffle/repartition
   consumer of that set (following one level of indirection through sets derived from it);
 * :class:`LearnedAdvisor`  — epsilon-greedy bandit over the candidate keys, rewarded by the observed
-  job time of consumers when the set was placed with that key (a lightweight stand-in for the
-  reference's DRL agent; the state/reward plumbing is the same).
+  job time of consumers when the set was placed with that key;
+* :class:`DRLAdvisor`      — the reference's deep-RL agent: a Q-network over an RLState-style vector
+  (candidate-key features + cluster/environment features), trained online from the same rewards.
 
 The chosen key becomes a dispatcher :class:`LambdaPolicy`, so co-partitioned joins run without a
 shuffle (the planner sees both sides partitioned by the join key).
@@ -20,6 +21,8 @@ shuffle (the planner sees both sides partitioned by the join key).
 from __future__ import annotations
 
 import json
+import math
+import os
 import random
 import sqlite3
 import threading
@@ -217,13 +220,119 @@ class LearnedAdvisor(RuleBasedAdvisor):
         return min(cands, key=lambda c: self.db.mean_reward(dbname, set_name, c[1]))
 
 
-class SelfLearningHook:
-    """Attach to a PDBClient: records every job; ``advise(db, set)`` returns a partition policy."""
+class DRLAdvisor(RuleBasedAdvisor):
+    """Deep-RL placement agent (reference: DRLBasedDataPlacementOptimizerForLoadJob + RLClient/RLState,
+    whose state vector goes to an external RL server that answers with the best lambda index).
 
-    def __init__(self, client, path: str = ":memory:", learned: bool = False):
+    Here the agent is in-process: a Q-network (MLP) maps the RLState-style vector — per candidate key
+    slot: use frequency, mean consumer-job time, last observed reward and an untried flag; plus input
+    size, number of nodes/GPUs, number of candidates, host cores and device memory — to one value per
+    candidate slot.  A placement is a one-step episode (its reward, minus the consumer job time, arrives
+    when the jobs reading the set run), so the update is a contextual-bandit Q regression over a replay
+    buffer (gamma = 0) with epsilon-greedy exploration over the valid slots."""
+
+    SLOTS = 4
+
+    def __init__(self, db: SelfLearningDB, epsilon: float = 0.2, seed: int = 0, hidden: int = 64, lr: float = 3e-3,
+                 env: Optional[dict] = None):
+        super().__init__(db)
+        import torch
+
+        self.torch = torch
+        self.rng = random.Random(seed)
+        self.epsilon = epsilon
+        self.env = dict(env or {})
+        g = torch.Generator().manual_seed(seed)
+        dim = self.SLOTS * 4 + 6
+        self.q = torch.nn.Sequential(torch.nn.Linear(dim, hidden), torch.nn.ReLU(), torch.nn.Linear(hidden, hidden),
+                                     torch.nn.ReLU(), torch.nn.Linear(hidden, self.SLOTS))
+        with torch.no_grad():
+            for p in self.q.parameters():
+                p.copy_(torch.empty_like(p).uniform_(-0.1, 0.1, generator=g))
+        self.opt = torch.optim.Adam(self.q.parameters(), lr=lr)
+        self.replay: List[Tuple[list, int, float]] = []
+        self.pending: Dict[Tuple[str, str], Tuple[list, int, List[Tuple[str, str]]]] = {}
+        self.scale: Optional[float] = None      # running reward scale (seconds)
+
+    def state(self, dbname: str, set_name: str, cands: List[Tuple[str, str, int]]) -> list:
+        """RLState.toVector analogue."""
+        total = max(1, sum(c[2] for c in cands))
+        s = self.scale or 1.0
+        feats: list = []
+        for i in range(self.SLOTS):
+            if i < len(cands):
+                _, n, cnt = cands[i]
+                r = self.db.mean_reward(dbname, set_name, n)
+                sec = self.db.conn.execute("SELECT AVG(seconds) FROM stage_use WHERE db=? AND set_name=? AND key_name=?",
+                                           (dbname, set_name, n)).fetchone()[0] or 0.0
+                feats += [cnt / total, sec / s, (r / s) if r is not None else 0.0, 1.0 if r is None else 0.0]
+            else:
+                feats += [0.0, 0.0, 0.0, 0.0]
+        e = self.env
+        feats += [math.log1p(e.get("input_records", 0)) / 20.0, e.get("num_nodes", 1) / 8.0, len(cands) / self.SLOTS,
+                  (os.cpu_count() or 1) / 256.0, e.get("mem_gb", 0.0) / 288.0, e.get("num_gpus", 1) / 8.0]
+        return feats
+
+    def best_key(self, dbname, set_name):
+        cands = self.db.candidates(dbname, set_name)[: self.SLOTS]
+        if not cands:
+            return super().best_key(dbname, set_name)
+        torch = self.torch
+        s = self.state(dbname, set_name, cands)
+        if self.rng.random() < self.epsilon:
+            a = self.rng.randrange(len(cands))
+        else:
+            with torch.no_grad():
+                q = self.q(torch.tensor([s], dtype=torch.float32))[0, : len(cands)]
+            a = int(q.argmax())
+        self.pending[(dbname, set_name)] = (s, a, [(k, n) for k, n, _ in cands])
+        return (cands[a][0], cands[a][1])
+
+    def observe(self, dbname: str, set_name: str, key_name: str, seconds: float, steps: int = 20):
+        """Reward of the placement last chosen for (db, set): minus the time of a job that read it."""
+        p = self.pending.get((dbname, set_name))
+        if p is None:
+            return
+        s, a, cands = p
+        if cands[a][1] != key_name:
+            return
+        self.scale = seconds if self.scale is None else 0.9 * self.scale + 0.1 * seconds
+        self.replay.append((s, a, -seconds / max(self.scale, 1e-9)))
+        self.replay = self.replay[-512:]
+        torch = self.torch
+        for _ in range(steps):
+            batch = [self.replay[self.rng.randrange(len(self.replay))] for _ in range(min(32, len(self.replay)))]
+            S = torch.tensor([b[0] for b in batch], dtype=torch.float32)
+            A = torch.tensor([b[1] for b in batch])
+            R = torch.tensor([b[2] for b in batch], dtype=torch.float32)
+            loss = torch.nn.functional.mse_loss(self.q(S).gather(1, A[:, None])[:, 0], R)
+            self.opt.zero_grad()
+            loss.backward()
+            self.opt.step()
+
+    def save(self, path: str):
+        self.torch.save({"q": self.q.state_dict(), "scale": self.scale}, path)
+
+    def load(self, path: str):
+        st = self.torch.load(path, weights_only=True)
+        self.q.load_state_dict(st["q"])
+        self.scale = st["scale"]
+
+
+class SelfLearningHook:
+    """Attach to a PDBClient: records every job; ``advise(db, set)`` returns a partition policy.
+    ``learned``: False = rule-based, True / "bandit" = epsilon-greedy bandit, "drl" = :class:`DRLAdvisor`."""
+
+    def __init__(self, client, path: str = ":memory:", learned=False):
         self.client = client
         self.db = SelfLearningDB(path)
-        self.advisor = LearnedAdvisor(self.db) if learned else RuleBasedAdvisor(self.db)
+        if learned == "drl":
+            budget = client.storage.device_budget
+            env = {"num_nodes": client.ctx.world_size, "num_gpus": client.ctx.world_size,
+                   "mem_gb": budget / 2 ** 30 if budget < 1 << 60 else 0.0}
+            self.advisor = DRLAdvisor(self.db, env=env)
+        else:
+            self.advisor = LearnedAdvisor(self.db) if learned else RuleBasedAdvisor(self.db)
         eng = client.engine
         orig = eng.execute
 
@@ -232,7 +341,13 @@ class SelfLearningHook:
             if eng.last_tcap is not None and eng.last_plan is not None and eng._last_comps is not None:
                 atoms = eng.last_plan.atoms
                 uses = extract_uses(atoms, eng._last_comps, eng.last_plan)
-                self.db.record_job(job_name, st.get("seconds", 0.0), uses)
+                secs = st.get("seconds", 0.0)
+                self.db.record_job(job_name, secs, uses)
+                if isinstance(self.advisor, DRLAdvisor):
+                    for u in uses:
+                        p = self.db.current_placement(u["db"], u["set"])
+                        if p is not None:
+                            self.advisor.observe(u["db"], u["set"], p[1], secs)
             return st
 
         eng.execute = execute
@@ -249,4 +364,5 @@ class SelfLearningHook:
         return json.dumps(self.db.export(), default=str)[:10000]
 
 
-__all__ = ["SelfLearningDB", "RuleBasedAdvisor", "LearnedAdvisor", "SelfLearningHook", "extract_uses", "key_policy"]
+__all__ = ["SelfLearningDB", "RuleBasedAdvisor", "LearnedAdvisor", "DRLAdvisor", "SelfLearningHook", "extract_uses",
+           "key_policy"]

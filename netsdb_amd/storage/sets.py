@@ -14,7 +14,6 @@ assembling blocks before every block GEMM.
 """
 from __future__ import annotations
 
-import itertools
 import math
 import threading
 from typing import Dict, Iterator, List, Optional, Tuple
@@ -23,9 +22,6 @@ import torch
 
 from ..objects.record import RecordBatch
 from .serde import deserialize_batch, serialize_batch
-
-_page_ids = itertools.count()
-
 
 class Page:
     __slots__ = ("set", "page_no", "batch", "nbytes", "pins", "location", "dirty", "last_use", "n")
@@ -469,5 +465,3 @@ class DenseMatrixSet(UserSet):
 
 
 __all__ = ["Page", "UserSet", "DenseMatrixSet"]
-
-_ = _page_ids

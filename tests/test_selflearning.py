@@ -52,4 +52,54 @@ def test_learned_advisor_prefers_faster_key():
                                    {"db": "d", "set": "s", "sink": "Shuffle", "comp": "C", "key": ("att", "b"), "index": 0}])
     adv = LearnedAdvisor(db, epsilon=0.0)
     assert adv.best_key("d", "s") == ("att", "b")
-    _ = torch
+
+
+def test_drl_advisor_learns_faster_placement(tmp_path):
+    """DRLBasedDataPlacementOptimizer parity: the Q-network agent, fed the consumer-job time of each
+    placement it chooses, converges to the placement under which the consumers run faster."""
+    from netsdb_amd.selflearning import DRLAdvisor
+
+    db = SelfLearningDB()
+    uses = [{"db": "d", "set": "s", "sink": "Shuffle", "comp": "J", "key": ("att", k), "index": 0} for k in ("a", "b")]
+    db.record_job("warm", 1.0, uses)                          # both keys are candidates
+    adv = DRLAdvisor(db, epsilon=0.2, seed=3)
+    rnd = torch.Generator().manual_seed(0)
+    picks = []
+    for _ in range(80):
+        k = adv.best_key("d", "s")
+        db.record_placement("d", "s", k)
+        # environment: co-partitioning on 'b' makes the consumer job ~3x faster
+        secs = (1.0 if k[1] == "b" else 3.0) + 0.1 * float(torch.rand(1, generator=rnd))
+        db.record_job("consumer", secs, uses)
+        adv.observe("d", "s", k[1], secs)
+        picks.append(k[1])
+    adv.epsilon = 0.0
+    assert adv.best_key("d", "s") == ("att", "b")
+    assert picks[-30:].count("b") >= 20
+    path = str(tmp_path / "q.pt")
+    adv.save(path)
+    adv2 = DRLAdvisor(db, epsilon=0.0, seed=9)
+    adv2.load(path)
+    assert adv2.best_key("d", "s") == ("att", "b")
+
+
+def test_drl_hook_through_engine(tmp_path):
+    """enable_self_learning(learned="drl"): jobs feed the agent, policy='auto' asks it for the key."""
+    c = PDBClient(root=str(tmp_path), broadcast_threshold=0)
+    hook = c.enable_self_learning(learned="drl")
+    c.create_database("db")
+    c.create_set("db", "emps", Employee)
+    c.send_data("db", "emps", _emps())
+    c.create_set("db", "depts", Dept)
+    c.send_data("db", "depts", [Dept("eng", 1)])
+    for _ in range(3):
+        j = EmpJoinDept()
+        j.set_input(0, ScanSet("db", "emps", Employee))
+        j.set_input(1, ScanSet("db", "depts", Dept))
+        c.create_set("db", "out", EmpDept)
+        c.execute_computations(WriteSet("db", "out").set_input(j))
+        c.remove_set("db", "depts")
+        c.create_set("db", "depts", Dept, policy="auto")      # placement chosen by the agent, then rewarded
+        c.send_data("db", "depts", [Dept("eng", 1)])
+    assert c.policies[("db", "depts")] is not None
+    assert len(hook.advisor.replay) >= 1
