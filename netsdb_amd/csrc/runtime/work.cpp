@@ -23,7 +23,11 @@ bool Buzzer::wait(double timeout_s) {
     cv_.wait(g, [&] { return done_; });
     return true;
   }
-  return cv_.wait_for(g, std::chrono::duration<double>(timeout_s), [&] { return done_; });
+  // system_clock deadline: libstdc++ maps it to pthread_cond_timedwait, which ThreadSanitizer intercepts
+  // (steady_clock waits use pthread_cond_clockwait, invisible to TSan -> false "double lock" reports)
+  const auto deadline = std::chrono::system_clock::now() +
+                        std::chrono::duration_cast<std::chrono::system_clock::duration>(std::chrono::duration<double>(timeout_s));
+  return cv_.wait_until(g, deadline, [&] { return done_; });
 }
 
 bool Buzzer::done() const {
