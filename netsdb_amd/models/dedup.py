@@ -11,7 +11,8 @@ model is a block-index table (TensorBlockIndex).  Dedup detection hashes blocks 
 (exact) or compares random-projection LSH signatures + an L-inf tolerance (approximate).  A model
 is materialised for inference by one gather (index_select) into its dense panel, or page-packed:
 blocks are ordered so models that share blocks share pages (greedy packing, page_packing.py's
-bin-packing idea).
+bin-packing idea).  Across GPUs, :class:`DistributedBlockPool` stores every distinct block once in the
+cluster (hash-owner placement, RCCL all-to-all).
 """
 from __future__ import annotations
 
@@ -135,8 +136,17 @@ class BlockPool:
         m = m.to(self.device, self.dtype)
         R, C = m.shape
         nbr, nbc = math.ceil(R / self.br), math.ceil(C / self.bc)
-        blks = to_blocks(m, self.br, self.bc)
-        keys = block_hashes(blks) if self.tolerance == 0 else lsh_signatures(blks)
+        ids = self.insert_blocks(to_blocks(m, self.br, self.bc))
+        self.index.tables[name] = ids.reshape(nbr, nbc)
+        self.index.shapes[name] = (R, C)
+        return ids
+
+    def insert_blocks(self, blks: torch.Tensor, keys: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Pool ids of ``blks`` [n, br, bc]: a block equal (within tolerance) to a stored one reuses its
+        id; new distinct blocks are appended (deduplicated among themselves too)."""
+        blks = blks.to(self.device, self.dtype)
+        if keys is None:
+            keys = block_hashes(blks) if self.tolerance == 0 else lsh_signatures(blks)
         ids = torch.empty(blks.shape[0], dtype=torch.int64, device=self.device)
         # match against the pool (sorted-key binary search), verify content within tolerance
         if self.keys.numel():
@@ -154,7 +164,7 @@ class BlockPool:
         ids[hit] = cand[hit]
         new = (~hit).nonzero().flatten()
         if new.numel():
-            # dedup within the model itself
+            # dedup within the incoming blocks themselves
             nk = keys[new]
             uk, inv = torch.unique(nk, return_inverse=True)
             first = torch.full((uk.numel(),), new.numel(), dtype=torch.int64, device=self.device)
@@ -163,8 +173,6 @@ class BlockPool:
             self.blocks = torch.cat([self.blocks, blks[new[first]]])
             self.keys = torch.cat([self.keys, uk if self.tolerance == 0 else nk[first]])
             ids[new] = base + inv
-        self.index.tables[name] = ids.reshape(nbr, nbc)
-        self.index.shapes[name] = (R, C)
         self.stats["blocks_in"] += blks.shape[0]
         self.stats["blocks_stored"] = self.blocks.shape[0]
         return ids
@@ -202,10 +210,94 @@ class BlockPool:
         return pages
 
 
+class DistributedBlockPool:
+    """Cluster-wide model deduplication (one process per GPU): every distinct block is stored ONCE in
+    the cluster, on the rank that owns its content hash, so identical blocks of models held by
+    different GPUs (fine-tuned word2vec / classifier embedding tables) share one copy.
+
+    ``add_model`` (collective): block hashes on the device -> RCCL all-to-all of (hash, payload) to the
+    hash owners -> owners deduplicate against their pool (content-verified, :meth:`BlockPool.insert_blocks`)
+    -> global ids (owner << 40 | owner-local id) all-to-all'd back.  ``materialize`` (collective) fetches
+    a model's blocks from their owners with a second all-to-all pair.  The reference shares blocks through
+    TensorBlockIndex + SharedFFMatrixBlockSet pages over its socket dispatcher (src/deduplication,
+    TestWord2VecWithDeduplication.cc)."""
+
+    SHIFT = 40
+
+    def __init__(self, ctx, block_rows: int, block_cols: int, device=None, dtype=torch.bfloat16,
+                 tolerance: float = 0.0):
+        self.ctx = ctx
+        self.br, self.bc = block_rows, block_cols
+        self.device = torch.device(device) if device is not None else ctx.device
+        self.dtype = dtype
+        self.local = BlockPool(block_rows, block_cols, device=self.device, dtype=dtype, tolerance=tolerance)
+        self.tables: Dict[str, torch.Tensor] = {}
+        self.shapes: Dict[str, Tuple[int, int]] = {}
+        self.stats = {"blocks_in": 0}
+
+    def _ship(self, rows: torch.Tensor, dest: torch.Tensor):
+        """Group rows by destination rank and all-to-all them: (received rows, recv counts, send order)."""
+        order = torch.argsort(dest, stable=True)
+        counts = torch.bincount(dest, minlength=self.ctx.world_size).tolist()
+        got, recv = self.ctx.all_to_all_rows(rows[order], counts)
+        return got, recv, order
+
+    def _payload(self, blks: torch.Tensor) -> torch.Tensor:
+        return blks.reshape(blks.shape[0], self.br * self.bc).contiguous().view(torch.uint8)
+
+    def add_model(self, name: str, m: Optional[torch.Tensor]) -> torch.Tensor:
+        ws, rank = self.ctx.world_size, self.ctx.rank
+        m = torch.empty(0, self.bc, dtype=self.dtype, device=self.device) if m is None else m.to(self.device, self.dtype)
+        R, C = m.shape
+        nbr, nbc = math.ceil(R / self.br), math.ceil(C / self.bc)
+        if m.numel():
+            blks = to_blocks(m, self.br, self.bc)
+            h = block_hashes(blks)
+        else:
+            blks = torch.empty(0, self.br, self.bc, dtype=self.dtype, device=self.device)
+            h = torch.empty(0, dtype=torch.int64, device=self.device)
+        owner = (mix64(h) & 0x7FFFFFFFFFFFFFFF) % ws
+        got_h, recv, order = self._ship(h, owner)
+        got_b, _, _ = self._ship(self._payload(blks), owner)
+        got_b = got_b.to(self.device).view(self.dtype).reshape(-1, self.br, self.bc)
+        if got_b.shape[0]:
+            local_ids = self.local.insert_blocks(got_b, got_h.to(self.device))
+        else:
+            local_ids = torch.empty(0, dtype=torch.int64, device=self.device)
+        back, _ = self.ctx.all_to_all_rows((rank << self.SHIFT) | local_ids, recv)
+        ids = torch.empty_like(h)
+        ids[order] = back.to(ids.device)
+        self.tables[name] = ids.reshape(nbr, nbc)
+        self.shapes[name] = (R, C)
+        self.stats["blocks_in"] += int(blks.shape[0])
+        return ids
+
+    def materialize(self, name: Optional[str]) -> Optional[torch.Tensor]:
+        """Collective: rebuild this rank's model ``name`` (None: only serve the other ranks' requests)."""
+        if name is not None:
+            ids = self.tables[name].flatten()
+        else:
+            ids = torch.empty(0, dtype=torch.int64, device=self.device)
+        req, recv, order = self._ship(ids & ((1 << self.SHIFT) - 1), ids >> self.SHIFT)
+        payload = self._payload(self.local.blocks.index_select(0, req.to(self.device)))
+        got, _ = self.ctx.all_to_all_rows(payload, recv)
+        if name is None:
+            return None
+        blks = torch.empty(ids.numel(), self.br, self.bc, dtype=self.dtype, device=self.device)
+        blks[order] = got.to(self.device).view(self.dtype).reshape(-1, self.br, self.bc)
+        t = self.tables[name]
+        R, C = self.shapes[name]
+        return from_blocks(blks, t.shape[0], t.shape[1], R, C)
+
+    def stored_blocks(self) -> int:
+        """Distinct blocks stored on this rank (the sum over ranks = cluster-wide distinct blocks)."""
+        return int(self.local.blocks.shape[0])
+
+
 def pages_touched(pool: BlockPool, pages: List[List[int]], name: str) -> int:
     page_of = {b: i for i, p in enumerate(pages) for b in p}
     return len({page_of[b] for b in pool.index.tables[name].flatten().tolist()})
 
 
-__all__ = ["TensorBlockIndex", "BlockPool", "block_hashes", "lsh_signatures", "to_blocks", "from_blocks",
+__all__ = ["TensorBlockIndex", "BlockPool", "DistributedBlockPool", "block_hashes", "lsh_signatures", "to_blocks", "from_blocks",
            "pages_touched"]

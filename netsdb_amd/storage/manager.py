@@ -24,7 +24,7 @@ DEFAULT_PAGE_SIZE = 64 << 20
 class StorageManager:
     def __init__(self, root: Optional[str] = None, device=None, page_size: int = DEFAULT_PAGE_SIZE,
                  pool_pages: int = 16, device_budget: Optional[int] = None, rank: int = 0, io_workers: int = 2,
-                 read_ahead: int = 4):
+                 read_ahead: int = 4, pinned_budget: Optional[int] = None):
         self.root = root or tempfile.mkdtemp(prefix="netsdb_amd_")
         os.makedirs(self.root, exist_ok=True)
         self.device = torch.device(device) if device is not None else None
@@ -40,6 +40,17 @@ class StorageManager:
             total = torch.cuda.get_device_properties(self.device).total_memory
             device_budget = int(total * 0.85)
         self.device_budget = device_budget or (1 << 62)
+        # warm tier: evicted device pages go to pinned host memory by async DMA (hosttier.py)
+        self.host_tier = None
+        if self.device is not None and self.device.type == "cuda" and pinned_budget != 0:
+            from .hosttier import PinnedHostTier
+
+            if pinned_budget is None:
+                try:
+                    pinned_budget = min(64 << 30, os.sysconf("SC_PAGE_SIZE") * os.sysconf("SC_PHYS_PAGES") // 8)
+                except (ValueError, OSError):
+                    pinned_budget = 8 << 30
+            self.host_tier = PinnedHostTier(self.device, pinned_budget)
         self.device_bytes = 0
         self.sets: Dict[Tuple[str, str], UserSet] = {}
         self._ids = itertools.count(1)
@@ -74,9 +85,7 @@ class StorageManager:
         with self.lock:
             s = self.sets.pop((db, name), None)
             if s is not None:
-                for p in s.pages:
-                    if p.location == "device" and p.batch is not None:
-                        self.device_bytes -= p.nbytes
+                self._release_pages(s)
                 s.clear()
 
     def remove_database(self, db: str):
@@ -86,10 +95,15 @@ class StorageManager:
 
     def clear_set(self, db: str, name: str):
         s = self.get_set(db, name)
+        self._release_pages(s)
+        s.clear()
+
+    def _release_pages(self, s: UserSet):
         for p in s.pages:
             if p.location == "device" and p.batch is not None:
                 self.device_bytes -= p.nbytes
-        s.clear()
+            elif p.location == "pinned" and self.host_tier is not None:
+                self.host_tier.release(p.nbytes)
 
     # ----------------------------------------------------------- memory accounting / eviction
     def account(self, page: Page):
@@ -163,6 +177,7 @@ class StorageManager:
             "pool_evictions": self.buffer_manager.evictions,
             "pool_loads": self.buffer_manager.loads,
             "io_work_completed": self.workers.completed,
+            "pinned_tier": dict(self.host_tier.stats, used=self.host_tier.used) if self.host_tier is not None else None,
             **self.stats,
         }
 

@@ -24,7 +24,7 @@ from ..objects.record import RecordBatch
 from .serde import deserialize_batch, serialize_batch
 
 class Page:
-    __slots__ = ("set", "page_no", "batch", "nbytes", "pins", "location", "dirty", "last_use", "n")
+    __slots__ = ("set", "page_no", "batch", "nbytes", "pins", "location", "dirty", "last_use", "n", "event")
 
     def __init__(self, uset: "UserSet", page_no: int, batch: RecordBatch):
         self.set = uset
@@ -36,14 +36,25 @@ class Page:
         self.location = "device" if batch.device.type == "cuda" else "host"
         self.dirty = True
         self.last_use = 0
+        self.event = None      # pinned tier: completion event of the page's D2H copy
 
     def is_resident(self) -> bool:
         return self.batch is not None
 
     def spill(self):
-        """Serialise into the native page pool (LRU -> disk) and drop the in-memory batch."""
+        """Evict from HBM: to the pinned host tier (async DMA) when it has room, else serialise into the
+        native page pool (LRU -> disk) and drop the in-memory batch."""
         if self.batch is None or self.pins > 0:
             return 0
+        tier = getattr(self.set.manager, "host_tier", None)
+        if self.location == "device" and tier is not None and tier.admit(self.nbytes):
+            self.batch, self.event = tier.offload(self.batch, self.nbytes)
+            self.location = "pinned"
+            return self.nbytes
+        if self.location == "pinned":
+            self.batch = tier.host_view(self.batch, self.event)
+            tier.release(self.nbytes)
+            self.event = None
         bm = self.set.manager.buffer_manager
         data = serialize_batch(self.batch)
         if len(data) > bm.page_size:
@@ -59,6 +70,16 @@ class Page:
         return freed
 
     def load(self, device) -> RecordBatch:
+        if self.location == "pinned":
+            tier = self.set.manager.host_tier
+            if device is not None and torch.device(device).type == "cuda":
+                self.batch = tier.fetch(self.batch, self.event, self.nbytes)   # async H2D, stream-ordered
+                self.event = None
+                self.location = "device"
+                self.set.manager.account_bytes(self.nbytes, device)
+            else:
+                self.batch = tier.host_view(self.batch, self.event)
+            return self.batch
         if self.batch is not None:
             return self.batch
         bm = self.set.manager.buffer_manager
@@ -81,6 +102,8 @@ class Page:
         if self.batch is None or not self.dirty:
             return
         bm = self.set.manager.buffer_manager
+        if self.location == "pinned":
+            self.set.manager.host_tier.host_view(self.batch, self.event)
         data = serialize_batch(self.batch)
         slot = bm.pin(self.set.set_id, self.page_no, True)
         bm.slot_view(slot)[: len(data)] = data

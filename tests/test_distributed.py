@@ -205,3 +205,32 @@ def test_distributed_tpch_partitioned():
             for g, e in zip(got, ref):
                 for k, v in e.items():
                     assert (math.isclose(g[k], v, rel_tol=1e-9, abs_tol=1e-6) if isinstance(v, float) else g[k] == v), (q, g, e)
+
+
+def _dedup_scenario(ctx, out_dir):
+    """Cross-GPU model dedup (BASELINE config 'model-deduplication over word2vec embedding tables across
+    8 GPUs'): rank 0 and rank 1 hold embedding tables sharing 3 of 4 block rows."""
+    from netsdb_amd.models.dedup import DistributedBlockPool
+
+    base = torch.randn(64, 96, generator=torch.Generator().manual_seed(11))
+    m = base.clone()
+    if ctx.rank == 1:
+        m[:16] = torch.randn(16, 96, generator=torch.Generator().manual_seed(99))   # private block row
+    pool = DistributedBlockPool(ctx, 16, 32, device="cpu", dtype=torch.float32)
+    pool.add_model("emb", m)
+    pool.add_model("emb_copy", m)                 # an identical model adds no blocks
+    back = pool.materialize("emb")
+    back2 = pool.materialize("emb_copy")
+    pool.add_model("nothing", None)               # a rank without a model still takes part
+    stored = ctx.all_reduce_scalar(float(pool.stored_blocks()), "sum")
+    return {"err": float((back - m).abs().max()), "err2": float((back2 - m).abs().max()), "stored": stored,
+            "blocks_in": pool.stats["blocks_in"]}
+
+
+@pytest.mark.timeout(300)
+def test_distributed_block_dedup():
+    r0, r1 = _run("_dedup_scenario")
+    for r in (r0, r1):
+        assert r["err"] == 0.0 and r["err2"] == 0.0
+        assert r["stored"] == 12 + 3          # 12 blocks per table, rank 1 adds 3 private ones
+        assert r["blocks_in"] == 24

@@ -1,5 +1,6 @@
 """Storage layer: serde round trips, native buffer manager LRU/spill, page files, slab allocator,
 HBM-budget eviction, catalog, checkpoint/resume (reference: src/storage, src/bufferMgr, src/catalog tests)."""
+import pytest
 import torch
 
 from netsdb_amd import _ext
@@ -150,3 +151,32 @@ def test_native_worker_queue_flush_and_read_ahead(tmp_path):
     assert c.storage.buffer_manager.loads > loads0
     c.flush_data()
     assert c.storage.summary()["io_work_completed"] >= 1
+
+
+@pytest.mark.gpu
+def test_pinned_host_tier_spill_and_reload(tmp_path):
+    """HBM pressure evicts device pages to pinned host memory with async D2H copies on the copy stream;
+    a scan brings them back with async H2D copies ordered before the consumer (no serialisation)."""
+    import torch
+
+    from netsdb_amd.client import PDBClient
+    from netsdb_amd.objects.record import RecordBatch
+
+    c = PDBClient(root=str(tmp_path), device="cuda:0", page_size=1 << 16, device_budget=1 << 18)
+    c.create_database("d")
+    c.create_set("d", "x", None)
+    g = torch.Generator(device="cuda:0").manual_seed(0)
+    data = torch.randn(4096, 64, device="cuda:0", generator=g)          # 1 MiB in 64 KiB pages, budget 256 KiB
+    c.add_local_data("d", "x", RecordBatch({"v": data, "k": torch.arange(4096, device="cuda:0")}, 4096))
+    tier = c.storage.host_tier
+    assert tier is not None and tier.stats["offloads"] > 0
+    pages = c.get_set("d", "x").pages
+    assert any(p.location == "pinned" for p in pages)
+    assert all(p.batch.columns["v"].is_pinned() for p in pages if p.location == "pinned")
+    got = torch.cat([b.columns["v"] for b in c.get_set("d", "x").scan()])
+    keys = torch.cat([b.columns["k"] for b in c.get_set("d", "x").scan()])
+    assert got.is_cuda and torch.equal(got[keys.argsort()], data)
+    assert tier.stats["fetches"] > 0
+    assert c.storage.device_bytes <= c.storage.device_budget + (1 << 16)
+    c.remove_set("d", "x")
+    assert tier.used == 0
