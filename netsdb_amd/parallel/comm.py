@@ -35,6 +35,10 @@ class ClusterContext:
         self.device = device if device is not None else torch.device("cpu")
         self.backend = backend
         self.group = group
+        # host-side metadata collectives (plan sizes, batch schemas, scalars) run on a gloo group when the
+        # data backend is RCCL: a RCCL scalar all-reduce + .item() would block the host on the GPU stream
+        # and stall kernel enqueueing mid-step
+        self.meta_group = None
 
     @property
     def distributed(self) -> bool:
@@ -58,7 +62,18 @@ class ClusterContext:
                 kw["device_id"] = dev
             dist.init_process_group(be, rank=rank, world_size=ws, **kw)
         be = dist.get_backend() if dist.is_initialized() else None
-        return ClusterContext(rank, ws, dev, be)
+        ctx = ClusterContext(rank, ws, dev, be)
+        ctx.attach_meta_group()
+        return ctx
+
+    def attach_meta_group(self):
+        """Collective: create the gloo metadata group next to a RCCL data group."""
+        if self.backend == "nccl" and self.world_size > 1 and self.meta_group is None:
+            try:
+                self.meta_group = dist.new_group(backend="gloo")
+            except (RuntimeError, ValueError):      # no gloo transport: metadata stays on RCCL
+                self.meta_group = None
+        return self
 
     # -------------------------------------------------------------- primitives
     def barrier(self):
@@ -79,9 +94,13 @@ class ClusterContext:
     def all_reduce_scalar(self, v: float, op="sum") -> float:
         if not self.distributed:
             return v
+        rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
+        if self.meta_group is not None:
+            t = torch.tensor([float(v)], dtype=torch.float64)
+            dist.all_reduce(t, op=rop, group=self.meta_group)
+            return float(t.item())
         t = torch.tensor([float(v)], dtype=torch.float64, device=self._comm_device())
-        dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
-                               "min": dist.ReduceOp.MIN}[op])
+        dist.all_reduce(t, op=rop)
         return float(t.item())
 
     def all_gather_tensor(self, t: torch.Tensor) -> List[torch.Tensor]:
@@ -137,7 +156,10 @@ class ClusterContext:
         if not self.distributed:
             return obj
         box = [obj]
-        dist.broadcast_object_list(box, src=src, device=self._comm_device() if self.backend == "nccl" else None)
+        if self.meta_group is not None:
+            dist.broadcast_object_list(box, src=src, group=self.meta_group)
+        else:
+            dist.broadcast_object_list(box, src=src, device=self._comm_device() if self.backend == "nccl" else None)
         return box[0]
 
     # -------------------------------------------------------------- record batch shuffles
@@ -158,7 +180,7 @@ class ClusterContext:
         ref = template or next((p for p in parts if p is not None), None)
         meta = _batch_meta(ref)
         metas = [None] * ws
-        dist.all_gather_object(metas, meta)
+        dist.all_gather_object(metas, meta, group=self.meta_group)
         ref_meta = next((m for m in metas if m is not None), None)
         if ref_meta is None:
             return []
