@@ -27,6 +27,12 @@ int nsdb_lstm_cell(const void* gates, int g_f32, const float* c_prev, void* h_ou
                    int H, hipStream_t st);
 int nsdb_embedding_bag(const void* table, int t_f32, const long long* idx, const long long* offsets,
                        const float* weights, float* out, int Bn, int D, int mode, hipStream_t st);
+int nsdb_str_hash(const void* bytes, const int64_t* off, int64_t n, uint64_t* out, hipStream_t st);
+int nsdb_str_like(const void* bytes, const int64_t* off, int64_t n, const uint8_t* pat, int pat_len,
+                  const int* seg_start, const int* seg_len, int nseg, int anchor_start, int anchor_end, int negate,
+                  uint8_t* out, hipStream_t st);
+int nsdb_str_gather(const void* src, const int64_t* off, const int64_t* idx, const int64_t* out_off, int64_t m,
+                    void* dst, hipStream_t st);
 }
 
 namespace {
@@ -250,6 +256,61 @@ torch::Tensor embedding_bag(torch::Tensor table, torch::Tensor idx, torch::Tenso
   return out;
 }
 
+// String columns: bytes u8 [>= offsets[-1] + 16] (padding read by the dword loads), offsets i64 [n+1].
+void check_strings(const torch::Tensor& bytes, const torch::Tensor& off) {
+  check_cuda(bytes, "bytes");
+  check_cuda(off, "offsets");
+  TORCH_CHECK(bytes.scalar_type() == torch::kUInt8 && bytes.dim() == 1 && bytes.is_contiguous(), "bytes u8 1-D");
+  TORCH_CHECK(off.scalar_type() == torch::kInt64 && off.dim() == 1 && off.is_contiguous() && off.numel() >= 1,
+              "offsets i64 [n+1]");
+  TORCH_CHECK(bytes.numel() % 4 == 0 && bytes.numel() >= 16, "bytes must be padded to a multiple of 4, >= 16");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(bytes.data_ptr()) % 4 == 0, "bytes must be 4-byte aligned");
+}
+
+torch::Tensor str_hash(torch::Tensor bytes, torch::Tensor off, int64_t payload_end) {
+  check_strings(bytes, off);
+  TORCH_CHECK(payload_end + 16 <= bytes.numel(), "string payload must be followed by >= 16 pad bytes");
+  const int64_t n = off.numel() - 1;
+  auto out = torch::empty({n}, off.options());
+  check_rc(nsdb_str_hash(bytes.data_ptr(), off.data_ptr<int64_t>(), n, (uint64_t*)out.data_ptr<int64_t>(),
+                         cur_stream()),
+           "str_hash");
+  return out;
+}
+
+torch::Tensor str_like(torch::Tensor bytes, torch::Tensor off, int64_t payload_end, const std::string& pat,
+                       std::vector<int64_t> seg_start, std::vector<int64_t> seg_len, bool anchor_start,
+                       bool anchor_end, bool negate) {
+  check_strings(bytes, off);
+  TORCH_CHECK(payload_end + 16 <= bytes.numel(), "string payload must be followed by >= 16 pad bytes");
+  TORCH_CHECK(seg_start.size() == seg_len.size(), "segment lists differ in length");
+  TORCH_CHECK(pat.size() <= 224 && seg_start.size() <= 16, "pattern too long for the kernarg pattern (224 B, 16 segs)");
+  std::vector<int> ss(seg_start.begin(), seg_start.end()), sl(seg_len.begin(), seg_len.end());
+  const int64_t n = off.numel() - 1;
+  auto out = torch::empty({n}, bytes.options());
+  check_rc(nsdb_str_like(bytes.data_ptr(), off.data_ptr<int64_t>(), n, (const uint8_t*)pat.data(), (int)pat.size(),
+                         ss.data(), sl.data(), (int)ss.size(), anchor_start, anchor_end, negate,
+                         out.data_ptr<uint8_t>(), cur_stream()),
+           "str_like");
+  return out.view(torch::kBool);
+}
+
+// idx must index rows of off (0 <= idx < n): checked by the caller on the device before launch.
+torch::Tensor str_gather(torch::Tensor bytes, torch::Tensor off, torch::Tensor idx, torch::Tensor out_off,
+                         int64_t out_bytes) {
+  check_strings(bytes, off);
+  check_cuda(idx, "idx");
+  check_cuda(out_off, "out_off");
+  TORCH_CHECK(idx.scalar_type() == torch::kInt64 && idx.is_contiguous() && idx.dim() == 1, "idx i64 1-D");
+  TORCH_CHECK(out_off.scalar_type() == torch::kInt64 && out_off.numel() == idx.numel() + 1, "out_off [m+1]");
+  const int64_t padded = ((out_bytes + 16 + 3) / 4) * 4;
+  auto dst = torch::zeros({padded}, bytes.options());
+  check_rc(nsdb_str_gather(bytes.data_ptr(), off.data_ptr<int64_t>(), idx.data_ptr<int64_t>(),
+                           out_off.data_ptr<int64_t>(), idx.numel(), dst.data_ptr(), cur_stream()),
+           "str_gather");
+  return dst;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -276,4 +337,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_cell", &lstm_cell, py::arg("gates"), py::arg("c_prev") = py::none(), py::arg("h_f32") = true);
   m.def("embedding_bag", &embedding_bag, py::arg("table"), py::arg("idx"), py::arg("offsets"),
         py::arg("weights") = py::none(), py::arg("mode") = 0);
+  m.def("str_hash", &str_hash, "64-bit hash per string of a device string column");
+  m.def("str_like", &str_like, "SQL LIKE over a device string column (segments of the pattern bytes)");
+  m.def("str_gather", &str_gather, "take() of a device string column into a new padded byte buffer");
 }

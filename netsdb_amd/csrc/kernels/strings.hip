@@ -1,0 +1,168 @@
+// Device-resident string columns (objects/strings.py StringColumn): UTF-8 bytes in one HBM buffer +
+// int64 offsets[n+1]. The reference keeps pdb::String objects inside pages and runs string predicates
+// and hash-map probes on the CPU per object (src/objectModel String.h, tpchBench Q12/Q13/Q14 selections,
+// StringIntPair hash maps); here a whole column is one launch:
+//
+//  * nsdb_str_hash   — 64-bit hash per string (group-by / join keys, IN-lists),
+//  * nsdb_str_like   — SQL LIKE with '%' and single-byte '_' (=, prefix, suffix, contains are the
+//                      1-segment special cases), pattern in the kernarg segment (scalar loads),
+//  * nsdb_str_gather — take(): copy selected strings into a new packed buffer.
+//
+// One lane per string: TPC-H / Reddit strings are 1-120 bytes, so 64 neighbouring strings of a wave
+// are a few contiguous KB that the L1/L2 serve from a handful of lines. Bytes are read as aligned
+// dwords from a buffer the host pads by >= 16 bytes, so an 8-byte chunk at any offset is two 64-bit
+// halves funnel-shifted together (no byte loads, no unaligned access).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+constexpr int kPatBytes = 224;
+constexpr int kPatSegs = 16;
+constexpr uint8_t kAnyByte = 0xFF;   // '_' (never a byte of valid UTF-8)
+
+struct LikePattern {               // passed by value: lives in the kernarg segment, read by s_load
+  uint8_t bytes[kPatBytes];
+  uint8_t seg_start[kPatSegs];
+  uint8_t seg_len[kPatSegs];
+  int nseg;
+  int anchor_start;
+  int anchor_end;
+  int negate;
+};
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  x ^= x >> 30;
+  x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 27;
+  x *= 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return x;
+}
+
+// 8 bytes starting at byte offset p (little endian), from a dword view of the padded buffer.
+__device__ __forceinline__ uint64_t load8(const uint32_t* __restrict__ w, int64_t p) {
+  const int64_t q = p >> 2;
+  const uint32_t sh = (uint32_t)(p & 3) * 8u;
+  const uint64_t a = (uint64_t)w[q] | ((uint64_t)w[q + 1] << 32);
+  const uint64_t b = (uint64_t)w[q + 2];
+  return sh ? (a >> sh) | (b << (64u - sh)) : a;
+}
+
+__device__ __forceinline__ uint32_t byte_at(const uint32_t* __restrict__ w, int64_t p) {
+  return (w[p >> 2] >> ((uint32_t)(p & 3) * 8u)) & 0xFFu;
+}
+
+__global__ __launch_bounds__(256) void str_hash_kernel(const uint32_t* __restrict__ w,
+                                                      const int64_t* __restrict__ off, int64_t n,
+                                                      uint64_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t s = off[i], e = off[i + 1];
+  const int64_t len = e - s;
+  uint64_t h = mix64((uint64_t)len ^ 0x9E3779B97F4A7C15ull);
+  for (int64_t p = s; p < e; p += 8) {
+    uint64_t c = load8(w, p);
+    const int64_t rem = e - p;
+    if (rem < 8) c &= (1ull << (8 * rem)) - 1ull;
+    h = mix64(h ^ c);
+  }
+  out[i] = h;
+}
+
+__device__ __forceinline__ bool seg_match_at(const uint32_t* __restrict__ w, int64_t p, const LikePattern& pt,
+                                             int sg) {
+  const int st = pt.seg_start[sg], ln = pt.seg_len[sg];
+  for (int k = 0; k < ln; ++k) {
+    const uint32_t pc = pt.bytes[st + k];
+    if (pc != kAnyByte && byte_at(w, p + k) != pc) return false;
+  }
+  return true;
+}
+
+__global__ __launch_bounds__(256) void str_like_kernel(const uint32_t* __restrict__ w,
+                                                      const int64_t* __restrict__ off, int64_t n,
+                                                      LikePattern pt, uint8_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t s = off[i], e = off[i + 1];
+  bool ok = true;
+  int64_t pos = s;
+  for (int sg = 0; sg < pt.nseg && ok; ++sg) {
+    const int ln = pt.seg_len[sg];
+    const bool first = sg == 0, last = sg == pt.nseg - 1;
+    if (first && pt.anchor_start) {
+      ok = (e - pos >= ln) && seg_match_at(w, pos, pt, sg);
+      pos += ln;
+      if (ok && last && pt.anchor_end) ok = pos == e;
+    } else if (last && pt.anchor_end) {
+      const int64_t p = e - ln;
+      ok = (p >= pos) && seg_match_at(w, p, pt, sg);
+      pos = e;
+    } else {   // leftmost occurrence at or after pos (greedy is exact for '%'-separated fixed segments)
+      int64_t p = pos;
+      bool found = false;
+      for (; p + ln <= e; ++p)
+        if (seg_match_at(w, p, pt, sg)) { found = true; break; }
+      ok = found;
+      pos = p + ln;
+    }
+  }
+  if (pt.nseg == 0 && pt.anchor_start && pt.anchor_end) ok = (e == s);   // pattern '' matches only ''
+  out[i] = (uint8_t)(ok != (pt.negate != 0));
+}
+
+// out_off[j] = exclusive prefix of the selected lengths (computed on the device by the caller).
+__global__ __launch_bounds__(256) void str_gather_kernel(const uint8_t* __restrict__ src,
+                                                        const int64_t* __restrict__ off,
+                                                        const int64_t* __restrict__ idx,
+                                                        const int64_t* __restrict__ out_off, int64_t m,
+                                                        uint8_t* __restrict__ dst) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const int64_t r = idx[j];
+  const int64_t s = off[r], len = off[r + 1] - s, d = out_off[j];
+  for (int64_t k = 0; k < len; ++k) dst[d + k] = src[s + k];
+}
+
+inline int grid_for(int64_t n) { return (int)((n + 255) / 256); }
+
+}  // namespace
+
+extern "C" {
+
+int nsdb_str_hash(const void* bytes, const int64_t* off, int64_t n, uint64_t* out, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(str_hash_kernel, dim3(grid_for(n)), dim3(256), 0, st, (const uint32_t*)bytes, off, n, out);
+  return (int)hipGetLastError();
+}
+
+int nsdb_str_like(const void* bytes, const int64_t* off, int64_t n, const uint8_t* pat, int pat_len,
+                  const int* seg_start, const int* seg_len, int nseg, int anchor_start, int anchor_end, int negate,
+                  uint8_t* out, hipStream_t st) {
+  if (pat_len > kPatBytes || nseg > kPatSegs || pat_len < 0 || nseg < 0) return -2;
+  LikePattern pt{};
+  for (int k = 0; k < pat_len; ++k) pt.bytes[k] = pat[k];
+  for (int k = 0; k < nseg; ++k) {
+    if (seg_start[k] < 0 || seg_len[k] < 0 || seg_start[k] + seg_len[k] > pat_len) return -3;
+    pt.seg_start[k] = (uint8_t)seg_start[k];
+    pt.seg_len[k] = (uint8_t)seg_len[k];
+  }
+  pt.nseg = nseg;
+  pt.anchor_start = anchor_start;
+  pt.anchor_end = anchor_end;
+  pt.negate = negate;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(str_like_kernel, dim3(grid_for(n)), dim3(256), 0, st, (const uint32_t*)bytes, off, n, pt, out);
+  return (int)hipGetLastError();
+}
+
+int nsdb_str_gather(const void* src, const int64_t* off, const int64_t* idx, const int64_t* out_off, int64_t m,
+                    void* dst, hipStream_t st) {
+  if (m <= 0) return 0;
+  hipLaunchKernelGGL(str_gather_kernel, dim3(grid_for(m)), dim3(256), 0, st, (const uint8_t*)src, off, idx,
+                     out_off, m, (uint8_t*)dst);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

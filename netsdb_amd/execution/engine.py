@@ -20,6 +20,7 @@ from ..computations import AggregateComp, Computation, TopKComp
 from ..lambdas import Literal, SelfRef
 from ..logical_plan.tcap import compile_tcap
 from ..objects.record import PDBObject, RecordBatch, RecordView, batch_of, column_concat
+from ..objects.strings import StringColumn
 from ..parallel.comm import ClusterContext
 from ..query_planning.planner import Planner
 from ..utils.trace import Tracer
@@ -41,7 +42,7 @@ class _One:
 def _normalize(val, n: int, device):
     if isinstance(val, SelfRef):
         return val.batch
-    if isinstance(val, (RecordBatch, torch.Tensor, tuple)):
+    if isinstance(val, (RecordBatch, torch.Tensor, tuple, StringColumn)):
         return val
     if isinstance(val, list):
         if val and isinstance(val[0], PDBObject):

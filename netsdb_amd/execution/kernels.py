@@ -14,6 +14,7 @@ import torch
 import xxhash
 
 from ..objects.record import RecordBatch, RecordView
+from ..objects.strings import StringColumn, hash_str, is_string_list
 
 _M1 = -0x40A7B892E31B1A47   # 0xBF58476D1CE4E5B9 as signed int64
 _M2 = -0x6B2FB644ECCEEE15   # 0x94D049BB133111EB as signed int64
@@ -36,6 +37,8 @@ def mix64(x: torch.Tensor) -> torch.Tensor:
 def _obj_key(v) -> int:
     if isinstance(v, RecordView):
         v = v.as_tuple()
+    if isinstance(v, str):
+        return hash_str(v)               # same key as a StringColumn row (device hash kernel)
     if isinstance(v, torch.Tensor):
         v = v.tolist()
     h = xxhash.xxh64_intdigest(repr(v).encode())
@@ -65,6 +68,10 @@ def column_to_int64(c, device=None) -> torch.Tensor:
     if isinstance(c, RecordBatch):
         cols = tuple(v for v in c.columns.values())
         return column_to_int64(cols, device)
+    if isinstance(c, StringColumn):
+        return c.hash64()
+    if is_string_list(c):               # vectorised: pack once, hash on the device (or numpy on CPU)
+        return StringColumn.from_list(c, device).hash64()
     vals = [_obj_key(v) for v in c]
     return torch.tensor(vals, dtype=torch.int64, device=device)
 
@@ -97,6 +104,20 @@ def join_match(build_h: torch.Tensor, probe_h: torch.Tensor) -> Tuple[torch.Tens
 
 def group_ids(keys) -> Tuple[torch.Tensor, Any, int]:
     """Exact group-by: returns (inverse index per row, representative key column, #groups)."""
+    if isinstance(keys, StringColumn):
+        inv, first, n = _unique_first(keys.hash64())
+        return inv, keys.take(first), n
+    if isinstance(keys, tuple) and any(isinstance(k, StringColumn) for k in keys) and all(
+            isinstance(k, StringColumn) or (isinstance(k, torch.Tensor) and k.dim() == 1) for k in keys):
+        dev = keys[0].device
+        cols = [k.hash64() if isinstance(k, StringColumn) else
+                (k.to(dev).long() if not k.is_floating_point() else k.double().view(torch.int64).to(dev)) for k in keys]
+        uniq, inv = torch.unique(torch.stack([c.to(dev) for c in cols], 1), dim=0, return_inverse=True)
+        first = torch.full((uniq.shape[0],), inv.numel(), dtype=torch.long, device=dev)
+        first.scatter_reduce_(0, inv, torch.arange(inv.numel(), device=dev), "amin")
+        reps = tuple(k.take(first) if isinstance(k, StringColumn) else k.index_select(0, first.to(k.device))
+                     for k in keys)
+        return inv, reps, uniq.shape[0]
     if isinstance(keys, tuple) and all(isinstance(k, torch.Tensor) and k.dim() == 1 for k in keys):
         dev = keys[0].device
         stacked = torch.stack([k.to(dev).long() if not k.is_floating_point() else k.double().view(torch.int64).to(dev)
@@ -122,6 +143,14 @@ def group_ids(keys) -> Tuple[torch.Tensor, Any, int]:
             reps.append(v)
         inv.append(g)
     return torch.tensor(inv, dtype=torch.int64), reps, len(reps)
+
+
+def _unique_first(h: torch.Tensor):
+    """(inverse, first row of each group, #groups) for a 1-D key tensor."""
+    uniq, inv = torch.unique(h, return_inverse=True)
+    first = torch.full((uniq.numel(),), h.numel(), dtype=torch.long, device=h.device)
+    first.scatter_reduce_(0, inv, torch.arange(h.numel(), device=h.device), "amin")
+    return inv, first, uniq.numel()
 
 
 def _hashable(v):

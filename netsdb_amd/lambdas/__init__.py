@@ -17,6 +17,7 @@ from typing import Any, Callable, List, Optional, Sequence
 import torch
 
 from ..objects.record import RecordBatch, RecordView, column_item
+from ..objects.strings import StringColumn
 
 
 class Arg:
@@ -239,7 +240,7 @@ class Native(Lambda):
             if isinstance(v, RecordBatch):
                 n = v.n
                 break
-            if isinstance(v, (list, torch.Tensor)):
+            if isinstance(v, (list, StringColumn, torch.Tensor)):
                 n = len(v)
                 break
         if n is None:
@@ -256,7 +257,10 @@ def _row_accessor(v):
         return lambda i: RecordView(v, i)
     if isinstance(v, tuple):
         return lambda i: tuple(column_item(c, i) for c in v)
-    if isinstance(v, (list, torch.Tensor)):
+    if isinstance(v, StringColumn):
+        lst = v.tolist()                  # one D2H for a row-at-a-time (non-vectorised) lambda
+        return lambda i: lst[i]
+    if isinstance(v, (list, StringColumn, torch.Tensor)):
         return lambda i: column_item(v, i)
     return lambda i: v
 
@@ -314,8 +318,14 @@ def _equals(a, b):
             e = _equals(x, y)
             out = e if out is None else _logic("&&", out, e)
         return out
+    if isinstance(a, str) and isinstance(b, StringColumn):
+        a, b = b, a
+    if isinstance(a, StringColumn) and isinstance(b, str):
+        return a.eq(b)                                   # one device pattern-match launch
+    if isinstance(a, StringColumn) and isinstance(b, StringColumn) and len(a) == len(b):
+        return a.hash64() == b.to(a.device).hash64()     # row-wise equality by 64-bit hash
     ta, tb = _to_tensor_col(a), _to_tensor_col(b)
-    if ta is not None and (tb is not None or not isinstance(b, (list, SelfRef))):
+    if ta is not None and (tb is not None or not isinstance(b, (list, StringColumn, SelfRef))):
         other = tb if tb is not None else b
         if isinstance(other, torch.Tensor):
             other = other.to(ta.device)
@@ -337,18 +347,20 @@ def _not(a):
     t = _to_tensor_col(a)
     if t is not None:
         return ~t.bool()
+    if isinstance(a, StringColumn):
+        a = a.tolist()
     return [not x for x in a]
 
 
 def _elementwise(f, a, b):
     if isinstance(a, torch.Tensor) and isinstance(b, torch.Tensor):
         return f(a, b.to(a.device))
-    if isinstance(a, torch.Tensor) and not isinstance(b, (list, SelfRef)):
+    if isinstance(a, torch.Tensor) and not isinstance(b, (list, StringColumn, SelfRef)):
         return f(a, b)
-    if isinstance(b, torch.Tensor) and not isinstance(a, (list, SelfRef)):
+    if isinstance(b, torch.Tensor) and not isinstance(a, (list, StringColumn, SelfRef)):
         return f(a, b)
-    if isinstance(a, (list, torch.Tensor)) or isinstance(b, (list, torch.Tensor)):
-        n = len(a) if isinstance(a, (list, torch.Tensor)) else len(b)
+    if isinstance(a, (list, StringColumn, torch.Tensor)) or isinstance(b, (list, StringColumn, torch.Tensor)):
+        n = len(a) if isinstance(a, (list, StringColumn, torch.Tensor)) else len(b)
         ga, gb = _row_accessor(a), _row_accessor(b)
         return [f(ga(i), gb(i)) for i in range(n)]
     return f(a, b)

@@ -27,6 +27,7 @@ import torch
 from ..computations import AggregateComp, JoinComp, ScanSet, SelectionComp, TopKComp, WriteSet
 from ..lambdas import make_batch_lambda, make_lambda_from_member
 from ..objects.record import PDBObject, RecordBatch
+from ..objects.strings import StringColumn, use_device_strings
 
 # ----------------------------------------------------------------------------------------- schema
 
@@ -257,7 +258,7 @@ def to_batch(table: str, cols: Dict[str, object], device=None) -> RecordBatch:
     for name, ft in typ.fields().items():
         v = cols[name]
         if ft is str:
-            out[name] = list(v)
+            out[name] = StringColumn.from_list(v, device) if use_device_strings(device or "cpu") else list(v)
         else:
             arr = np.asarray(v)
             out[name] = torch.from_numpy(arr.astype(np.float64 if ft is float else np.int64))
@@ -281,12 +282,23 @@ def _col(b: RecordBatch, name: str):
 
 
 def _strmask(strings: Sequence[str], pred, device) -> torch.Tensor:
+    if isinstance(strings, StringColumn):
+        strings = strings.tolist()
     return torch.tensor([bool(pred(s)) for s in strings], dtype=torch.bool, device=device)
 
 
 def _isin_str(strings: Sequence[str], allowed: Sequence[str], device) -> torch.Tensor:
+    if isinstance(strings, StringColumn):          # device column: hash kernel + isin, no host strings
+        return strings.isin(list(allowed)).to(device)
     a = set(allowed)
     return _strmask(strings, lambda s: s in a, device)
+
+
+def _like(strings, pattern: str, device, negate: bool = False) -> torch.Tensor:
+    """SQL LIKE over a string column: one HIP launch for a device column, a regex on host lists."""
+    if isinstance(strings, StringColumn):
+        return strings.like(pattern, negate).to(device)
+    return StringColumn.from_list(strings).like(pattern, negate).to(device)
 
 
 def _dev(b: RecordBatch):
@@ -350,7 +362,10 @@ def _rows_out(names: List[str]):
 
 
 def _str_keys(*cols):
-    """Tuple key of string columns -> a single string key per row (host grouping)."""
+    """Tuple key of string columns: device columns stay a tuple (hash-kernel group-by on the GPU), host
+    lists become one joined string per row (host grouping)."""
+    if all(isinstance(c, StringColumn) for c in cols):
+        return tuple(cols)
     return ["|".join(t) for t in zip(*cols)]
 
 
@@ -402,8 +417,9 @@ def q01(client, db: str, delta_days: int = 90) -> List[dict]:
     out = []
     if r is None:
         return out
+    k1 = _as_list(r.columns["k1"]) if "k1" in r.columns else None
     for i, k in enumerate(_as_list(r.columns["k0"])):
-        rf, ls = k.split("|")
+        rf, ls = (k, k1[i]) if k1 is not None else k.split("|")
         c = float(r.columns["count"][i])
         row = {"l_returnflag": rf, "l_linestatus": ls}
         for f in ("sum_qty", "sum_base_price", "sum_disc_price", "sum_charge"):
@@ -483,7 +499,7 @@ def q04(client, db: str, date: int = 19930701) -> List[dict]:
     j = _EqJoin(2, [(0, "o_orderkey", 1, "k0")], _pick([["o_orderpriority"], []]))
     j.set_input(0, os_)
     j.set_input(1, dist.set_input(late))
-    cnt = _GroupBy(lambda b: list(_col(b, "o_orderpriority")),
+    cnt = _GroupBy(lambda b: _col(b, "o_orderpriority"),
                    lambda b: torch.ones(b.n, 1, dtype=torch.float64, device=_dev(b)), _rows_out(["order_count"]))
     r = _flat(_run(client, db, "q04_out", cnt.set_input(j), "tpch_q04"))
     if r is None:
@@ -524,7 +540,7 @@ def q12(client, db: str, modes=("MAIL", "SHIP"), date: int = 19940101) -> List[d
         hi = _isin_str(_col(b, "o_orderpriority"), ["1-URGENT", "2-HIGH"], _dev(b)).double()
         return torch.stack([hi, 1 - hi], 1)
 
-    agg = _GroupBy(lambda b: list(_col(b, "l_shipmode")), vals, _rows_out(["high_line_count", "low_line_count"]))
+    agg = _GroupBy(lambda b: _col(b, "l_shipmode"), vals, _rows_out(["high_line_count", "low_line_count"]))
     r = _flat(_run(client, db, "q12_out", agg.set_input(j), "tpch_q12"))
     if r is None:
         return []
@@ -536,10 +552,8 @@ def q12(client, db: str, modes=("MAIL", "SHIP"), date: int = 19940101) -> List[d
 def q13(client, db: str, w1: str = "special", w2: str = "requests") -> List[dict]:
     """Customer distribution (Query13.h): orders per customer (LEFT OUTER JOIN -> customers with none
     counted via the customer cardinality), then customers per order-count."""
-    import re
-
-    pat = re.compile(f".*{w1}.*{w2}.*")
-    os_ = _Filter(lambda b: ~_strmask(_col(b, "o_comment"), pat.match, _dev(b))).set_input(ScanSet(db, "orders", Order))
+    os_ = _Filter(lambda b: _like(_col(b, "o_comment"), f"%{w1}%{w2}%", _dev(b), negate=True)).set_input(
+        ScanSet(db, "orders", Order))
     per_c = _GroupBy(lambda b: _col(b, "o_custkey"), lambda b: torch.ones(b.n, 1, dtype=torch.float64, device=_dev(b)),
                      _rows_out(["c_count"]))
     dist = _GroupBy(lambda b: _col(b, "c_count").long(),
@@ -569,7 +583,7 @@ def q14(client, db: str, date: int = 19950901) -> float:
 
     def vals(b):
         rev = _col(b, "l_extendedprice").double() * (1 - _col(b, "l_discount").double())
-        promo = _strmask(_col(b, "p_type"), lambda s: s.startswith("PROMO"), _dev(b)).double()
+        promo = _like(_col(b, "p_type"), "PROMO%", _dev(b)).double()
         return torch.stack([rev * promo, rev], 1)
 
     agg = _GroupBy(lambda b: torch.zeros(b.n, dtype=torch.int64, device=_dev(b)), vals, _rows_out(["promo", "total"]))
@@ -614,7 +628,13 @@ def q22(client, db: str, codes=("13", "31", "23", "29", "30", "18", "17")) -> Li
     cset = list(codes)
 
     def in_codes(b):
-        return _strmask(_col(b, "c_phone"), lambda s: s[:2] in cset, _dev(b))
+        c = _col(b, "c_phone")
+        if not isinstance(c, StringColumn):
+            return _strmask(c, lambda s: s[:2] in cset, _dev(b))
+        m = torch.zeros(len(c), dtype=torch.bool, device=_dev(b))
+        for code in cset:                      # country-code prefix: one LIKE launch per code
+            m |= c.startswith(code).to(m.device)
+        return m
 
     pos = _Filter(lambda b: in_codes(b) & (_col(b, "c_acctbal") > 0)).set_input(ScanSet(db, "customer", Customer))
     avg = _GroupBy(lambda b: torch.zeros(b.n, dtype=torch.int64, device=_dev(b)),
@@ -649,7 +669,7 @@ def q02(client, db: str, size: int = 15, type_suffix: str = "BRASS", region: str
     """Minimum cost supplier (Query02.h): part ⋈ partsupp ⋈ supplier ⋈ nation ⋈ region, min supply
     cost per part (aggregate), joined back to keep the suppliers at that minimum; top 100."""
     ps_ = _Filter(lambda b: (_col(b, "p_size") == size) &
-                  _strmask(_col(b, "p_type"), lambda s: s.endswith(type_suffix), _dev(b))).set_input(ScanSet(db, "part", Part))
+                  _like(_col(b, "p_type"), "%" + type_suffix, _dev(b))).set_input(ScanSet(db, "part", Part))
     rs = _Filter(lambda b: _isin_str(_col(b, "r_name"), [region], _dev(b))).set_input(ScanSet(db, "region", Region))
     j = _EqJoin(5, [(0, "p_partkey", 1, "ps_partkey"), (1, "ps_suppkey", 2, "s_suppkey"),
                     (2, "s_nationkey", 3, "n_nationkey"), (3, "n_regionkey", 4, "r_regionkey")],

@@ -20,6 +20,8 @@ from typing import Any, Dict, Iterable, List, Optional, Sequence
 
 import torch
 
+from .strings import StringColumn, is_string_list, use_device_strings
+
 
 class Tensor:
     """Field type for fixed-shape tensor payloads (e.g. a MatrixBlock's rawData)."""
@@ -197,7 +199,7 @@ class RecordBatch:
     @property
     def device(self) -> torch.device:
         for c in self.columns.values():
-            if isinstance(c, torch.Tensor):
+            if isinstance(c, (torch.Tensor, StringColumn)):
                 return c.device
         return torch.device("cpu")
 
@@ -253,6 +255,8 @@ class RecordBatch:
                 total += c.numel() * c.element_size()
             elif isinstance(c, RecordBatch):
                 total += c.nbytes()
+            elif isinstance(c, StringColumn):
+                total += c.nbytes
             elif isinstance(c, tuple):
                 total += sum(x.numel() * x.element_size() if isinstance(x, torch.Tensor) else 16 * len(x) for x in c)
             else:
@@ -280,6 +284,10 @@ class RecordBatch:
 def _col_to(c, device):
     if isinstance(c, torch.Tensor):
         return c.to(device, non_blocking=True)
+    if isinstance(c, StringColumn):
+        return c.to(device)
+    if is_string_list(c) and use_device_strings(device):
+        return StringColumn.from_list(c, device)
     if isinstance(c, RecordBatch):
         return c.to(device)
     if isinstance(c, tuple):
@@ -343,7 +351,7 @@ def column_item(c, i):
 
 
 def column_take(c, idx):
-    if isinstance(c, RecordBatch):
+    if isinstance(c, (RecordBatch, StringColumn)):
         return c.take(idx)
     if isinstance(c, tuple):
         return tuple(column_take(x, idx) for x in c)
@@ -361,6 +369,10 @@ def column_concat(parts):
         return RecordBatch.concat(parts)
     if parts and all(isinstance(p, tuple) for p in parts):
         return tuple(column_concat([p[i] for p in parts]) for i in range(len(parts[0])))
+    if parts and any(isinstance(p, StringColumn) for p in parts):
+        sc = next(p for p in parts if isinstance(p, StringColumn))
+        return StringColumn.concat([p if isinstance(p, StringColumn) else StringColumn.from_list(p, sc.device)
+                                    for p in parts])
     if all(isinstance(p, torch.Tensor) for p in parts):
         if len(parts) == 1:
             return parts[0]

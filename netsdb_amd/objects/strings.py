@@ -1,0 +1,337 @@
+"""Device-resident string columns.
+
+The reference stores ``pdb::String`` objects inside pages (src/objectModel/headers/PDBString.h) and
+evaluates string predicates, hash-map keys and joins on them one object at a time on the CPU
+(tpchBench selections, StringIntPair maps in serviceBenchmarks/StringHashMapTest). Here a ``str`` column
+that lives on a GPU is one :class:`StringColumn`: the UTF-8 bytes of every row packed into one uint8
+buffer plus int64 ``offsets[n+1]``, both in HBM. Predicates (=, IN, LIKE, prefix/suffix/contains),
+hashing for group-by/join keys and gathers are single HIP launches over the whole column
+(``csrc/kernels/strings.hip``); Python strings appear only when a caller iterates the column.
+
+The same class runs on CPU tensors (numpy paths with identical results) so the CPU test-suite covers the
+logic; on a GPU box the HIP path is mandatory (``_ext.hip()`` raises if the kernels are missing).
+
+Policy: :func:`use_device_strings` decides whether ``RecordBatch.to(device)`` packs ``list[str]`` columns
+into a StringColumn — by default only for GPU devices; ``NSDB_DEVICE_STRINGS=1`` forces it everywhere
+(used to run the CPU suite through this path), ``=0`` disables it.
+"""
+from __future__ import annotations
+
+import os
+import re
+from typing import Iterable, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .. import _ext
+
+_PAD = 16                        # bytes after the payload that the kernels' dword loads may touch
+_ANY = 0xFF                      # '_' wildcard byte in a compiled LIKE pattern (never valid UTF-8)
+_M1, _M2, _SEED = 0xBF58476D1CE4E5B9, 0x94D049BB133111EB, 0x9E3779B97F4A7C15
+_MASK = (1 << 64) - 1
+
+
+def use_device_strings(device) -> bool:
+    flag = os.environ.get("NSDB_DEVICE_STRINGS")
+    if flag is not None:
+        return flag == "1"
+    return device is not None and torch.device(device).type == "cuda"
+
+
+def _mix_py(x: int) -> int:
+    x ^= x >> 30
+    x = (x * _M1) & _MASK
+    x ^= x >> 27
+    x = (x * _M2) & _MASK
+    x ^= x >> 31
+    return x
+
+
+def hash_str(s) -> int:
+    """Host twin of the kernel's string hash (signed int64, as stored in hash columns)."""
+    b = s.encode() if isinstance(s, str) else bytes(s)
+    h = _mix_py(len(b) ^ _SEED)
+    for p in range(0, len(b), 8):
+        h = _mix_py(h ^ int.from_bytes(b[p:p + 8], "little"))
+    return h - (1 << 64) if h >= (1 << 63) else h
+
+
+def _mix_np(x: np.ndarray) -> np.ndarray:
+    x = x ^ (x >> np.uint64(30))
+    x = x * np.uint64(_M1)
+    x = x ^ (x >> np.uint64(27))
+    x = x * np.uint64(_M2)
+    return x ^ (x >> np.uint64(31))
+
+
+def _hash_np(buf: np.ndarray, off: np.ndarray) -> np.ndarray:
+    starts, lens = off[:-1], off[1:] - off[:-1]
+    with np.errstate(over="ignore"):
+        h = _mix_np(lens.astype(np.uint64) ^ np.uint64(_SEED))
+        nch = int((lens.max() + 7) // 8) if lens.size else 0
+        j = np.arange(8)
+        for k in range(nch):
+            active = lens > 8 * k
+            if not active.any():
+                break
+            rem = lens - 8 * k
+            idx = np.minimum(starts[:, None] + 8 * k + j[None, :], buf.size - 1)
+            byts = buf[idx].astype(np.uint64)
+            byts[j[None, :] >= rem[:, None]] = 0
+            c = (byts << (np.uint64(8) * j.astype(np.uint64))[None, :]).sum(1, dtype=np.uint64)
+            h = np.where(active, _mix_np(h ^ c), h)
+    return h.view(np.int64)
+
+
+def _compile_like(pattern: str):
+    """LIKE pattern -> (pattern bytes, segment starts, segment lengths, anchor_start, anchor_end)."""
+    parts = pattern.split("%")
+    anchor_start, anchor_end = not pattern.startswith("%"), not pattern.endswith("%")
+    if pattern == "":
+        return b"", [], [], True, True
+    segs = [p for p in parts if p]
+    buf, st, ln = bytearray(), [], []
+    for p in segs:
+        b = bytes(_ANY if ch == ord("_") else ch for ch in p.encode())
+        st.append(len(buf))
+        ln.append(len(b))
+        buf += b
+    return bytes(buf), st, ln, anchor_start, anchor_end
+
+
+def _literal(segs: Sequence[str], anchor_start: bool, anchor_end: bool):
+    buf, st, ln = bytearray(), [], []
+    for p in segs:
+        b = p.encode()
+        if _ANY in b:
+            raise ValueError("literal contains byte 0xFF")
+        st.append(len(buf))
+        ln.append(len(b))
+        buf += b
+    return bytes(buf), st, ln, anchor_start, anchor_end
+
+
+def _like_regex(pat, st, ln, a0, a1) -> "re.Pattern[bytes]":
+    pieces = [re.escape(pat[s:s + n]).replace(re.escape(bytes([_ANY])), b".") for s, n in zip(st, ln)]
+    body = b".*".join(pieces)
+    if not pieces:
+        return re.compile(rb"\A\Z" if (a0 and a1) else rb"", re.S)
+    return re.compile((rb"\A" if a0 else b"") + (body if a0 else b".*" + body) + (rb"\Z" if a1 else b""), re.S)
+
+
+class StringColumn:
+    """n strings: ``data`` uint8 [>= payload + 16] (4-byte multiple), ``offsets`` int64 [n+1] into data."""
+
+    __slots__ = ("data", "offsets", "payload", "buf_rows")
+
+    def __init__(self, data: torch.Tensor, offsets: torch.Tensor, payload: int, buf_rows: Optional[int] = None):
+        self.data, self.offsets, self.payload = data, offsets, int(payload)
+        self.buf_rows = max(1, offsets.numel() - 1) if buf_rows is None else buf_rows   # rows sharing data
+
+    # ------------------------------------------------------------------ construction
+    @staticmethod
+    def _alloc_size(payload: int) -> int:
+        return ((payload + _PAD + 3) // 4) * 4
+
+    @staticmethod
+    def from_list(strs: Iterable, device=None) -> "StringColumn":
+        enc = [s.encode() if isinstance(s, str) else bytes(s) for s in strs]
+        lens = np.fromiter((len(b) for b in enc), dtype=np.int64, count=len(enc))
+        off = np.zeros(len(enc) + 1, dtype=np.int64)
+        np.cumsum(lens, out=off[1:])
+        payload = int(off[-1])
+        buf = np.zeros(StringColumn._alloc_size(payload), dtype=np.uint8)
+        if payload:
+            buf[:payload] = np.frombuffer(b"".join(enc), dtype=np.uint8)
+        data, offs = torch.from_numpy(buf), torch.from_numpy(off)
+        if device is not None and torch.device(device).type != "cpu":
+            data, offs = data.pin_memory().to(device, non_blocking=True), offs.pin_memory().to(device, non_blocking=True)
+        return StringColumn(data, offs, payload)
+
+    @staticmethod
+    def empty(device=None) -> "StringColumn":
+        return StringColumn.from_list([], device)
+
+    # ------------------------------------------------------------------ sequence protocol
+    @property
+    def device(self) -> torch.device:
+        return self.data.device
+
+    def __len__(self) -> int:
+        return self.offsets.numel() - 1
+
+    def _host(self):
+        return self.data[: self.payload].cpu().numpy(), self.offsets.cpu().numpy()
+
+    def tolist(self) -> List[str]:
+        buf, off = self._host()
+        raw = buf.tobytes()
+        return [raw[s:e].decode() for s, e in zip(off[:-1].tolist(), off[1:].tolist())]
+
+    def __iter__(self):
+        return iter(self.tolist())
+
+    def __array__(self, dtype=None, copy=None):
+        return np.array(self.tolist(), dtype=object)
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            s, e, step = i.indices(len(self))
+            if step != 1:
+                return self.take(torch.arange(s, e, step, dtype=torch.long))
+            e = max(e, s)
+            return StringColumn(self.data, self.offsets[s:e + 1], self.payload, self.buf_rows)
+        if isinstance(i, (torch.Tensor, list, np.ndarray)):
+            return self.take(i)
+        n = len(self)
+        if i < 0:
+            i += n
+        if not 0 <= i < n:
+            raise IndexError(i)
+        s, e = self.offsets[i:i + 2].tolist()
+        return bytes(self.data[s:e].cpu().numpy()).decode()
+
+    def __repr__(self):
+        return f"StringColumn(n={len(self)}, bytes={self.payload}, device={self.device})"
+
+    @property
+    def nbytes(self) -> int:
+        """Bytes this column accounts for: a slice (page) of a shared buffer is charged its row share,
+        estimated without reading the device offsets."""
+        return self.data.numel() * len(self) // self.buf_rows + 8 * self.offsets.numel()
+
+    def to(self, device) -> "StringColumn":
+        device = torch.device(device)
+        if device == self.device:
+            return self
+        return StringColumn(self.data.to(device, non_blocking=True), self.offsets.to(device, non_blocking=True),
+                            self.payload, self.buf_rows)
+
+    def compact(self) -> "StringColumn":
+        """Own buffer holding exactly these rows (after slicing a shared buffer)."""
+        return self.take(torch.arange(len(self), dtype=torch.long, device=self.device))
+
+    # ------------------------------------------------------------------ relational ops
+    def take(self, idx) -> "StringColumn":
+        dev = self.device
+        if not isinstance(idx, torch.Tensor):
+            idx = torch.as_tensor(np.asarray(idx, dtype=np.int64) if len(idx) else np.zeros(0, np.int64))
+        idx = idx.to(dev)
+        if idx.dtype == torch.bool:
+            idx = idx.nonzero().flatten()
+        idx = idx.long().contiguous()
+        n, m = len(self), idx.numel()
+        lens = (self.offsets[1:] - self.offsets[:-1]).index_select(0, idx) if m else idx
+        out_off = torch.zeros(m + 1, dtype=torch.int64, device=dev)
+        if m:
+            torch.cumsum(lens, 0, out=out_off[1:])
+        total = int(out_off[-1]) if m else 0
+        if dev.type == "cuda":
+            if m:   # host-side bound check before the launch (a bad index must never reach the GPU)
+                lo, hi = torch.aminmax(idx)
+                if int(lo) < 0 or int(hi) >= n:
+                    raise IndexError("string take index out of range")
+            data = _ext.hip().str_gather(self.data, self.offsets, idx, out_off, total)
+        else:
+            ii = idx.numpy()
+            if m and (ii.min() < 0 or ii.max() >= n):
+                raise IndexError("string take index out of range")
+            src = self.data.numpy()
+            off = self.offsets.numpy()
+            data_np = np.zeros(self._alloc_size(total), dtype=np.uint8)
+            if total:
+                starts, ln = off[:-1][ii], (off[1:] - off[:-1])[ii]
+                pos = np.repeat(starts - out_off[:-1].numpy(), ln) + np.arange(total)
+                data_np[:total] = src[pos]
+            data = torch.from_numpy(data_np)
+        return StringColumn(data, out_off, total)
+
+    @staticmethod
+    def concat(parts: Sequence["StringColumn"]) -> "StringColumn":
+        parts = list(parts)
+        dev = parts[0].device
+        datas, offs, base = [], [torch.zeros(1, dtype=torch.int64, device=dev)], 0
+        for p in parts:
+            p = p.to(dev)
+            o0 = p.offsets[:1]
+            k = len(p)
+            if k == 0:
+                continue
+            o = p.offsets - o0
+            datas.append((p.data, o0, p.offsets[-1:]))
+            offs.append(o[1:] + base)
+            base = base + (o[-1])
+        # byte ranges: each part's rows are contiguous in its buffer from offsets[0] to offsets[-1]
+        if not datas:
+            return StringColumn.empty(dev)
+        bounds = torch.stack([torch.cat([s, e]) for _, s, e in datas]).cpu().tolist()
+        total = sum(e - s for s, e in bounds)
+        data = torch.zeros(StringColumn._alloc_size(total), dtype=torch.uint8, device=dev)
+        pos = 0
+        for (d, _, _), (s, e) in zip(datas, bounds):
+            data[pos:pos + e - s] = d[s:e]
+            pos += e - s
+        return StringColumn(data, torch.cat(offs), total)
+
+    def hash64(self) -> torch.Tensor:
+        """int64 hash per row (== :func:`hash_str` of the row)."""
+        if self.device.type == "cuda":
+            return _ext.hip().str_hash(self.data, self.offsets, self.payload)
+        return torch.from_numpy(_hash_np(self.data.numpy(), self.offsets.numpy()).copy())
+
+    def _match(self, compiled, negate=False) -> torch.Tensor:
+        pat, st, ln, a0, a1 = compiled
+        if self.device.type == "cuda":
+            return _ext.hip().str_like(self.data, self.offsets, self.payload, pat, st, ln, a0, a1, negate)
+        rx = _like_regex(pat, st, ln, a0, a1)
+        buf, off = self._host()
+        raw = buf.tobytes()
+        out = np.fromiter((rx.search(raw[s:e]) is not None for s, e in zip(off[:-1].tolist(), off[1:].tolist())),
+                          dtype=bool, count=len(self))
+        return torch.from_numpy(out != negate)
+
+    def like(self, pattern: str, negate: bool = False) -> torch.Tensor:
+        """SQL ``LIKE`` ('%' any run, '_' any single byte) -> bool mask on the column's device."""
+        c = _compile_like(pattern)
+        if len(c[0]) > 224 or len(c[1]) > 16:
+            raise ValueError("LIKE pattern longer than 224 bytes / 16 segments")
+        return self._match(c, negate)
+
+    def eq(self, s: str) -> torch.Tensor:
+        return self._match(_literal([s], True, True))
+
+    def startswith(self, s: str) -> torch.Tensor:
+        return self._match(_literal([s], True, False))
+
+    def endswith(self, s: str) -> torch.Tensor:
+        return self._match(_literal([s], False, True))
+
+    def contains(self, s: str) -> torch.Tensor:
+        return self._match(_literal([s], False, False))
+
+    def isin(self, values: Sequence[str]) -> torch.Tensor:
+        """Membership by 64-bit hash (one launch + torch.isin); collisions are ~2^-64 per pair."""
+        h = self.hash64()
+        ref = torch.tensor([hash_str(v) for v in values], dtype=torch.int64, device=self.device)
+        return torch.isin(h, ref)
+
+    def dict_encode(self):
+        """(codes int64 [n], dictionary list[str]): device unique over the hashes; only the distinct
+        strings cross to the host."""
+        h = self.hash64()
+        uniq, inv = torch.unique(h, return_inverse=True)
+        first = torch.full((uniq.numel(),), len(self), dtype=torch.long, device=self.device)
+        first.scatter_reduce_(0, inv, torch.arange(len(self), device=self.device), "amin")
+        return inv, self.take(first).tolist()
+
+
+def is_string_list(c) -> bool:
+    return isinstance(c, list) and len(c) > 0 and all(isinstance(x, str) for x in c)
+
+
+def as_strings(c, device=None) -> StringColumn:
+    return c if isinstance(c, StringColumn) else StringColumn.from_list(c, device)
+
+
+__all__ = ["StringColumn", "hash_str", "use_device_strings", "is_string_list", "as_strings"]

@@ -22,6 +22,7 @@ import torch
 import torch.distributed as dist
 
 from ..objects.record import RecordBatch, lookup_type
+from ..objects.strings import StringColumn
 from ..storage.serde import _enc_obj, _dec_obj  # noqa: F401  (shared object codec)
 
 
@@ -194,6 +195,9 @@ class ClusterContext:
                 t = torch.cat([_as_tensor(p.columns[name], cm, self.device) for p in parts])
                 out, recv_counts = self.all_to_all_rows(t, counts)
                 recv_cols[name] = out
+            elif cm["kind"] == "string":
+                recv_cols[name] = self._exchange_strings([p.columns[name] for p in parts], counts)
+                recv_counts = recv_cols[name][1]
             else:
                 payloads = [json.dumps([_enc_plain(v) for v in p.columns[name]]).encode() for p in parts]
                 data = torch.frombuffer(bytearray(b"".join(payloads)) or bytearray(b"\0"), dtype=torch.uint8)
@@ -222,11 +226,35 @@ class ClusterContext:
                 name = cm["name"]
                 if cm["kind"] == "tensor":
                     cols[name] = recv_cols[name][off: off + k]
+                elif cm["kind"] == "string":
+                    cols[name] = recv_cols[name][0][src]
                 else:
                     cols[name] = [_dec_plain(v) for v in recv_cols[name][src]]
             out_batches.append(RecordBatch(cols, k, t))
             off += k
         return out_batches
+
+    def _exchange_strings(self, cols, counts):
+        """Device string columns on the wire: row lengths + packed bytes, two all-to-alls, no host
+        decode. Returns (one StringColumn per source rank, received row counts)."""
+        dev = self.device
+        cols = [c if isinstance(c, StringColumn) else StringColumn.from_list(list(c), dev) for c in cols]
+        cols = [c.to(dev) for c in cols]
+        lens = torch.cat([c.offsets[1:] - c.offsets[:-1] for c in cols])
+        rlens, rcounts = self.all_to_all_rows(lens, counts)
+        bounds = torch.stack([torch.stack([c.offsets[0], c.offsets[-1]]) for c in cols]).cpu().tolist()
+        data = torch.cat([c.data[s:e] for c, (s, e) in zip(cols, bounds)])
+        rdata, rbytes = self.all_to_all_rows(data, [e - s for s, e in bounds])
+        out, ro, rb = [], 0, 0
+        for k, nb in zip(rcounts, rbytes):
+            offs = torch.zeros(k + 1, dtype=torch.int64, device=rlens.device)
+            if k:
+                torch.cumsum(rlens[ro: ro + k], 0, out=offs[1:])
+            buf = torch.zeros(StringColumn._alloc_size(nb), dtype=torch.uint8, device=rdata.device)
+            buf[:nb] = rdata[rb: rb + nb]
+            out.append(StringColumn(buf, offs, nb))
+            ro, rb = ro + k, rb + nb
+        return out, rcounts
 
     def broadcast_batch_all(self, b: Optional[RecordBatch]) -> List[RecordBatch]:
         """All-gather: every rank receives every rank's batch (broadcast join build side)."""
@@ -297,6 +325,8 @@ def _batch_meta(b: Optional[RecordBatch]):
         if isinstance(c, torch.Tensor):
             cols.append({"name": k, "kind": "tensor", "dtype": str(c.dtype).replace("torch.", ""),
                          "shape": list(c.shape[1:])})
+        elif isinstance(c, StringColumn):
+            cols.append({"name": k, "kind": "string"})
         else:
             cols.append({"name": k, "kind": "object"})
     return {"type": b.type.type_name() if b.type is not None else None, "columns": cols}
@@ -313,6 +343,8 @@ def _empty_like_meta(meta, device):
     for cm in meta["columns"]:
         if cm["kind"] == "tensor":
             cols[cm["name"]] = torch.empty((0,) + tuple(cm["shape"]), dtype=getattr(torch, cm["dtype"]), device=device)
+        elif cm["kind"] == "string":
+            cols[cm["name"]] = StringColumn.empty(device)
         else:
             cols[cm["name"]] = []
     t = lookup_type(meta["type"]) if meta["type"] else None

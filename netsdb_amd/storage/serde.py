@@ -18,6 +18,7 @@ import numpy as np
 import torch
 
 from ..objects.record import PDBObject, RecordBatch, lookup_type
+from ..objects.strings import StringColumn
 
 _ALIGN = 64
 _DT = {torch.float32: "f32", torch.float64: "f64", torch.float16: "f16", torch.bfloat16: "bf16", torch.int64: "i64",
@@ -97,6 +98,13 @@ def serialize_batch(batch: RecordBatch) -> bytes:
             b = _tensor_bytes(c)
             cols_meta.append({"name": name, "kind": "tensor", "dtype": _DT[c.dtype], "shape": list(c.shape),
                               "off": add(b), "len": len(b)})
+        elif isinstance(c, StringColumn):       # packed UTF-8 + offsets: no per-string JSON
+            o = c.offsets.cpu()
+            base = int(o[0]) if o.numel() else 0
+            ob = _tensor_bytes(o - base)
+            db = c.data[base: base + int(o[-1]) - base].cpu().numpy().tobytes() if o.numel() > 1 else b""
+            cols_meta.append({"name": name, "kind": "string", "n": o.numel() - 1, "off": add(ob), "len": len(ob),
+                              "doff": add(db), "dlen": len(db)})
         else:
             blobs: List[bytes] = []
             enc = [_enc_obj(v, blobs) for v in c]
@@ -121,6 +129,12 @@ def deserialize_batch(data) -> RecordBatch:
         seg = mv[base + cm["off"]: base + cm["off"] + cm["len"]]
         if cm["kind"] == "tensor":
             cols[cm["name"]] = _tensor_from(seg, cm["dtype"], cm["shape"])
+        elif cm["kind"] == "string":
+            offs = _tensor_from(seg, "i64", [cm["n"] + 1])
+            raw = np.frombuffer(mv[base + cm["doff"]: base + cm["doff"] + cm["dlen"]], dtype=np.uint8)
+            buf = np.zeros(StringColumn._alloc_size(cm["dlen"]), dtype=np.uint8)
+            buf[: cm["dlen"]] = raw
+            cols[cm["name"]] = StringColumn(torch.from_numpy(buf), offs, cm["dlen"])
         else:
             enc = json.loads(bytes(seg).decode())
             raw_blobs = [mv[base + o: base + o + ln] for o, ln in cm.get("blobs", [])]

@@ -1,5 +1,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 180 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29631 scripts/rehearse_meta_group.py > gpurun_out/meta_group.log 2>&1; rc=$?
-grep "rank" gpurun_out/meta_group.log | tail -4; tail -5 gpurun_out/meta_group.log; exit $rc
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+tail -3 gpurun_out/pytest_gpu.log
+timeout -k 10 300 python scripts/bench_services.py --device cuda:0 > gpurun_out/bench_services.log 2>&1 || { tail -20 gpurun_out/bench_services.log; exit 1; }
+grep primitive gpurun_out/bench_services.log

@@ -207,6 +207,20 @@ def test_distributed_tpch_partitioned():
                     assert (math.isclose(g[k], v, rel_tol=1e-9, abs_tol=1e-6) if isinstance(v, float) else g[k] == v), (q, g, e)
 
 
+def _string_shuffle_scenario(ctx, out_dir):
+    """Packed device-string columns on the wire (tests/test_strings.py)."""
+    from netsdb_amd.objects.record import RecordBatch
+    from netsdb_amd.objects.strings import StringColumn
+
+    strs = [f"r{ctx.rank}-{i}-" + "z" * (i % 11) for i in range(40)]
+    col = StringColumn.from_list(strs)
+    b = RecordBatch({"s": col, "i": torch.arange(40)}, 40)
+    dest = torch.arange(40) % 2
+    parts = [b.take(torch.nonzero(dest == d).flatten()) for d in range(2)]
+    got = ctx.exchange(parts)
+    return [(g["s"].tolist(), g["i"].tolist(), type(g["s"]).__name__) for g in got]
+
+
 def _dedup_scenario(ctx, out_dir):
     """Cross-GPU model dedup (BASELINE config 'model-deduplication over word2vec embedding tables across
     8 GPUs'): rank 0 and rank 1 hold embedding tables sharing 3 of 4 block rows."""
