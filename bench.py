@@ -7,6 +7,9 @@ the model is replicated — netsDB's broadcast join of the weight sets, "materia
      = 2 jobs through the engine: W1·Xᵀ -> +b1, relu, dropout -> Wo·Y -> +bo, exp, ᵀ  |  row softmax
   2. conv2d_memory_fusion block (reference src/tests/source/PipelinedConv2dMemFuseTest.cc: 100 images
      3x112x112, 64 filters 7x7x3, stride 1, no padding) = 1 job, fused implicit-GEMM conv + bias.
+The conv2d job is independent of the FF jobs (resident images, own weights), so it is submitted on a
+second HIP stream (PDBClient.submit_job) and its kernels run concurrently with the FF kernels; the step
+ends with a stream-ordered join of both (--overlap none runs it serially after the FF jobs).
 rows/step/GPU = FF input rows + images.  Synthetic data, random-init weights, bf16 compute.
 
     python bench.py [--gpus N --steps K --warmup W]
@@ -37,6 +40,9 @@ def main():
     ap.add_argument("--small", action="store_true", help="tiny shapes (CPU smoke only; not a valid measurement)")
     ap.add_argument("--dropout", type=float, default=0.5)
     ap.add_argument("--profile-json", default=None)
+    ap.add_argument("--overlap", choices=["none", "after", "before"], default="before",
+                    help="conv2d job on its own HIP stream, submitted after/before the FF jobs (independent inputs)")
+    ap.add_argument("--job-priority", type=int, default=0, help="HIP stream priority of the conv2d job stream")
     args = ap.parse_args()
 
     from netsdb_amd.client import PDBClient
@@ -59,11 +65,22 @@ def main():
     cv.load_images(client, "conv2d", "img", cfg["images"], cfg["channels"], cfg["height"], cfg["width"], seed=99)
     w, b = cv.random_kernel(cfg["filters"], cfg["channels"], cfg["ksize"], cfg["ksize"], seed=7, device=dev)
     local_rows = client.storage.get_set("ff", "inputs").local_rows
+    client.job_stream_priority = args.job_priority
+
+    def conv():
+        cv.conv2d_memfuse_inference(client, "conv2d", "img", "conv_out", w, b)
 
     def step(i):
+        if args.overlap == "before":
+            client.submit_job(conv, independent=True)
         ff.inference_unit(client, "ff", "w1", "wo", "inputs", "b1", "bo", "output", dropout_rate=args.dropout,
                           seed=i)
-        cv.conv2d_memfuse_inference(client, "conv2d", "img", "conv_out", w, b)
+        if args.overlap == "none":
+            conv()
+        elif args.overlap == "after":
+            client.submit_job(conv, independent=True)
+        if args.overlap != "none":
+            client.wait_jobs()   # the step ends when both jobs have (stream-ordered join)
 
     def sync():
         if dev.type == "cuda":
@@ -112,6 +129,7 @@ def main():
                 "parallelism": f"dp{ctx.world_size} (row-partitioned inputs, broadcast model)",
                 "small": bool(args.small),
                 "softmax_rows_sum_to_1": ok,
+                "conv_overlap": args.overlap,
             },
         }
         print(json.dumps(res), flush=True)

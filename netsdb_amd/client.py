@@ -45,6 +45,8 @@ class PDBClient:
                                    torch.cuda.get_device_properties(self.device).total_memory
                                    if self.device.type == "cuda" else 0)
         self.learning = None
+        self.job_streams = None
+        self.job_stream_priority = 0
         if resume:
             self._resume()
 
@@ -392,6 +394,23 @@ class PDBClient:
 
     def barrier(self):
         self.ctx.barrier()
+
+    # ------------------------------------------------------------------ concurrent jobs
+    def submit_job(self, fn, *args, lane: int = 0, independent: bool = False, **kwargs):
+        """Run ``fn(*args, **kwargs)`` (any job-issuing callable, e.g. a model's inference entry point)
+        with its kernels enqueued on a job stream, concurrently with work on the caller's stream.
+        Returns a :class:`~netsdb_amd.execution.streams.JobHandle`; see that module for the ordering
+        contract (QuerySchedulerServer's concurrent job scheduling, on HIP queues)."""
+        if self.job_streams is None:
+            from .execution.streams import JobStreams
+
+            self.job_streams = JobStreams(self.device, lanes=2, priority=self.job_stream_priority)
+        return self.job_streams.submit(fn, *args, lane=lane, independent=independent, **kwargs)
+
+    def wait_jobs(self):
+        """The caller's stream waits (stream-ordered) for every submitted job."""
+        if self.job_streams is not None:
+            self.job_streams.wait_all()
 
 
 __all__ = ["PDBClient"]
