@@ -42,7 +42,7 @@ def main():
     ap.add_argument("--profile-json", default=None)
     ap.add_argument("--overlap", choices=["none", "after", "before"], default="before",
                     help="conv2d job on its own HIP stream, submitted after/before the FF jobs (independent inputs)")
-    ap.add_argument("--job-priority", type=int, default=0, help="HIP stream priority of the conv2d job stream")
+    ap.add_argument("--job-priority", type=int, default=-1, help="HIP stream priority of the conv2d job stream")
     args = ap.parse_args()
 
     from netsdb_amd.client import PDBClient
