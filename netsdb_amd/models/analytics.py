@@ -27,6 +27,7 @@ from ..computations import AggregateComp, JoinComp, MultiSelectionComp, ScanSet,
 from ..lambdas import make_batch_lambda, make_lambda_from_member, make_lambda_from_self
 from ..objects.builtin import DoubleVector
 from ..objects.record import PDBObject, RecordBatch, Tensor
+from ..utils.sampler import fraction_for_sample_size, randomize_in_place
 
 
 def _dev(b: RecordBatch):
@@ -126,11 +127,16 @@ def kmeans(client, db: str, name: str, k: int, iters: int = 10, init: Optional[t
            seed: int = 0, tol: float = 0.0):
     """Lloyd iterations (KMeansQuery): returns (centroids [k, d], per-iteration shift list)."""
     if init is None:
+        # sample size as the reference driver: Sampler::computeFractionForSampleSize(k, total, false)
+        total = sum(b.n for b in client.get_set_batches(db, name))
+        total = int(client.ctx.all_reduce_scalar(float(total), "sum")) if client.ctx.distributed else total
+        frac = fraction_for_sample_size(k, total, with_replacement=False)
         s = _run_to_batch(client, db, f"{name}_kmeans_sample",
-                          KMeansSampleSelection(0.05, seed).set_input(ScanSet(db, name, DoubleVector)), "kmeans_sample")
+                          KMeansSampleSelection(frac, seed).set_input(ScanSet(db, name, DoubleVector)), "kmeans_sample")
         pts = s.columns["data"] if s is not None and s.n >= k else None
         if pts is None:
             pts = RecordBatch.concat(client.get_set_batches(db, name, gather=True)).columns["data"]
+        pts = randomize_in_place(pts.clone(), torch.Generator().manual_seed(seed))
         init = pts[:k].clone()
     C = init.clone()
     shifts = []
