@@ -43,6 +43,9 @@ def main():
     ap.add_argument("--overlap", choices=["none", "after", "before"], default="before",
                     help="conv2d job on its own HIP stream, submitted after/before the FF jobs (independent inputs)")
     ap.add_argument("--job-priority", type=int, default=-1, help="HIP stream priority of the conv2d job stream")
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="FF steps in flight: step i's FF jobs go to job lane i %% inflight (>1 pipelines "
+                         "consecutive batches: step i+1's layer-1 GEMM starts while step i's tail kernels run)")
     args = ap.parse_args()
 
     from netsdb_amd.client import PDBClient
@@ -65,22 +68,33 @@ def main():
     cv.load_images(client, "conv2d", "img", cfg["images"], cfg["channels"], cfg["height"], cfg["width"], seed=99)
     w, b = cv.random_kernel(cfg["filters"], cfg["channels"], cfg["ksize"], cfg["ksize"], seed=7, device=dev)
     local_rows = client.storage.get_set("ff", "inputs").local_rows
-    client.job_stream_priority = args.job_priority
+    inflight = max(1, args.inflight)
+    conv_lane = inflight if inflight > 1 else 0
+    client.job_lanes = conv_lane + 1
+    client.job_lane_priority = {conv_lane: args.job_priority}
 
     def conv():
         cv.conv2d_memfuse_inference(client, "conv2d", "img", "conv_out", w, b)
 
-    def step(i):
-        if args.overlap == "before":
-            client.submit_job(conv, independent=True)
+    def ffjobs(i):
         ff.inference_unit(client, "ff", "w1", "wo", "inputs", "b1", "bo", "output", dropout_rate=args.dropout,
                           seed=i)
+
+    def step(i):
+        if args.overlap == "before":
+            client.submit_job(conv, lane=conv_lane, independent=True)
+        if inflight > 1:
+            # batches are independent (own inputs/outputs; weights read-only and materialised in warmup)
+            client.submit_job(ffjobs, i, lane=i % inflight, independent=True)
+        else:
+            ffjobs(i)
         if args.overlap == "none":
             conv()
         elif args.overlap == "after":
-            client.submit_job(conv, independent=True)
-        if args.overlap != "none":
+            client.submit_job(conv, lane=conv_lane, independent=True)
+        if args.overlap != "none" and inflight == 1:
             client.wait_jobs()   # the step ends when both jobs have (stream-ordered join)
+
 
     def sync():
         if dev.type == "cuda":
@@ -89,12 +103,19 @@ def main():
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
 
-    for i in range(args.warmup):
+    if args.warmup > 0:
+        # first step serially: derived weights / plans are materialised once, before any lane reads them
+        ffjobs(0)
+        conv()
+        sync()
+    for i in range(1, args.warmup):
         step(i)
+    client.wait_jobs()
     sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
+    client.wait_jobs()
     sync()
     dt = time.perf_counter() - t0
     dt = ctx.all_reduce_scalar(dt, "max")
@@ -130,6 +151,7 @@ def main():
                 "small": bool(args.small),
                 "softmax_rows_sum_to_1": ok,
                 "conv_overlap": args.overlap,
+                "ff_steps_in_flight": inflight,
             },
         }
         print(json.dumps(res), flush=True)

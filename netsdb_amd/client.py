@@ -47,6 +47,8 @@ class PDBClient:
         self.learning = None
         self.job_streams = None
         self.job_stream_priority = 0
+        self.job_lanes = 2               # job streams (in-order job queues) created on first submit_job
+        self.job_lane_priority = {}      # lane -> HIP stream priority (default job_stream_priority)
         if resume:
             self._resume()
 
@@ -404,7 +406,8 @@ class PDBClient:
         if self.job_streams is None:
             from .execution.streams import JobStreams
 
-            self.job_streams = JobStreams(self.device, lanes=2, priority=self.job_stream_priority)
+            self.job_streams = JobStreams(self.device, lanes=self.job_lanes, priority=self.job_stream_priority,
+                                          lane_priority=self.job_lane_priority)
         return self.job_streams.submit(fn, *args, lane=lane, independent=independent, **kwargs)
 
     def wait_jobs(self):

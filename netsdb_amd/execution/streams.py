@@ -55,10 +55,11 @@ class JobStreams:
     ``lanes`` streams are created lazily; jobs submitted with the same ``lane`` are serialised on
     that stream (a lane is an in-order job queue, like one reference worker's job queue)."""
 
-    def __init__(self, device, lanes: int = 2, priority: int = 0):
+    def __init__(self, device, lanes: int = 2, priority: int = 0, lane_priority: Optional[dict] = None):
         self.device = torch.device(device)
         self.lanes = max(1, int(lanes))
         self.priority = priority
+        self.lane_priority = dict(lane_priority or {})
         self._streams: List[Optional[torch.cuda.Stream]] = [None] * self.lanes
         self.submitted = 0
 
@@ -69,7 +70,7 @@ class JobStreams:
     def stream(self, lane: int = 0) -> "torch.cuda.Stream":
         lane %= self.lanes
         if self._streams[lane] is None:
-            self._streams[lane] = torch.cuda.Stream(self.device, priority=self.priority)
+            self._streams[lane] = torch.cuda.Stream(self.device, priority=self.lane_priority.get(lane, self.priority))
         return self._streams[lane]
 
     def submit(self, fn: Callable, *args, lane: int = 0, independent: bool = False, **kwargs) -> JobHandle:
