@@ -7,9 +7,11 @@ the model is replicated — netsDB's broadcast join of the weight sets, "materia
      = 2 jobs through the engine: W1·Xᵀ -> +b1, relu, dropout -> Wo·Y -> +bo, exp, ᵀ  |  row softmax
   2. conv2d_memory_fusion block (reference src/tests/source/PipelinedConv2dMemFuseTest.cc: 100 images
      3x112x112, 64 filters 7x7x3, stride 1, no padding) = 1 job, fused implicit-GEMM conv + bias.
-The conv2d job is independent of the FF jobs (resident images, own weights), so it is submitted on a
-second HIP stream (PDBClient.submit_job) and its kernels run concurrently with the FF kernels; the step
-ends with a stream-ordered join of both (--overlap none runs it serially after the FF jobs).
+The conv2d job is independent of the FF jobs (resident images, own weights); --overlap before|after submits
+it on a second HIP stream (PDBClient.submit_job) next to the FF kernels.  Default: serial — once the clocks
+have ramped (warmup 10) the overlap measures no gain (1.037-1.043M vs 1.034-1.045M rows/s, profiles/r1_overlap).
+The default warmup of 10 steps keeps the GPU clock ramp out of the timed window (10 timed steps after 2
+warmups measured 0.85-0.89M rows/s on the same box that gives 1.03-1.07M after 10).
 rows/step/GPU = FF input rows + images.  Synthetic data, random-init weights, bf16 compute.
 
     python bench.py [--gpus N --steps K --warmup W]
@@ -35,12 +37,12 @@ SMALL = dict(batch=64, features=4096, hidden=256, labels=512, block_x=32, block_
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--small", action="store_true", help="tiny shapes (CPU smoke only; not a valid measurement)")
     ap.add_argument("--dropout", type=float, default=0.5)
     ap.add_argument("--profile-json", default=None)
-    ap.add_argument("--overlap", choices=["none", "after", "before"], default="before",
+    ap.add_argument("--overlap", choices=["none", "after", "before"], default="none",
                     help="conv2d job on its own HIP stream, submitted after/before the FF jobs (independent inputs)")
     ap.add_argument("--job-priority", type=int, default=-1, help="HIP stream priority of the conv2d job stream")
     ap.add_argument("--inflight", type=int, default=1,
