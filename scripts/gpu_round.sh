@@ -9,11 +9,11 @@ echo "[gpu_round] tests" && timeout -k 10 600 python -m pytest tests -m gpu -x -
 rc=$?; tail -5 gpurun_out/pytest_gpu.log; [ $rc -ne 0 ] && exit $rc
 echo "[gpu_round] smoke" && timeout -k 10 300 python __graft_entry__.py > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
 tail -2 gpurun_out/smoke.log
-echo "[gpu_round] bench" && timeout -k 10 600 python bench.py --steps ${STEPS:-10} --warmup ${WARMUP:-2} > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -30 gpurun_out/bench.err; exit 1; }
+echo "[gpu_round] bench" && timeout -k 10 600 python bench.py --steps ${STEPS:-50} --warmup ${WARMUP:-10} > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -30 gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.json
 if [ "${PROFILE:-1}" = "1" ]; then
   echo "[gpu_round] rocprofv3"
   export TMPDIR=/tmp
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 3 --warmup 1 > gpurun_out/prof.log 2>&1 || { tail -20 gpurun_out/prof.log; exit 1; }
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 10 --warmup 10 > gpurun_out/prof.log 2>&1 || { tail -20 gpurun_out/prof.log; exit 1; }
   find gpurun_out/prof -name "*stats*" | head
 fi
