@@ -476,9 +476,17 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(GemmParams p) {
     for (long long e = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4; e < MN;
          e += (long long)gridDim.x * blockDim.x * 4) {
       const float* w = p.ws + (long long)batch * p.splits * MN + e;
-      f32x4 s = *reinterpret_cast<const f32x4*>(w);
-#pragma unroll 4
-      for (int k = 1; k < p.splits; ++k) s += *reinterpret_cast<const f32x4*>(w + k * MN);
+      // up to 16 slab loads in flight per thread (uniform predicates, one wait before the adds): the
+      // reducer is HBM/MALL-latency bound with 4 outstanding loads
+      f32x4 part[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (k < p.splits) part[k] = *reinterpret_cast<const f32x4*>(w + k * MN);
+      f32x4 s = part[0];
+#pragma unroll
+      for (int k = 1; k < 16; ++k)
+        if (k < p.splits) s += part[k];
+      for (int k = 16; k < p.splits; ++k) s += *reinterpret_cast<const f32x4*>(w + k * MN);
       const int row = (int)(e / p.N), col = (int)(e % p.N);
       float v[4];
 #pragma unroll
