@@ -14,6 +14,7 @@ collective.  ``backend='gloo'`` runs the identical code path on CPU (tests, pseu
 """
 from __future__ import annotations
 
+import base64
 import json
 import os
 from typing import Any, Dict, List, Optional, Sequence
@@ -354,7 +355,11 @@ def _empty_like_meta(meta, device):
 def _enc_plain(v):
     blobs: List[bytes] = []
     if isinstance(v, torch.Tensor):
-        return {"__tt__": [v.detach().cpu().float().tolist(), str(v.dtype).replace("torch.", "")]}
+        # exact bytes + dtype + shape (a float round trip would change int64 > 2^24 and every float64)
+        t = v.detach().cpu().contiguous()
+        raw = t.view(torch.uint8).numpy().tobytes() if t.numel() else b""
+        return {"__tt__": [base64.b64encode(raw).decode("ascii"), str(t.dtype).replace("torch.", ""),
+                           list(t.shape)]}
     enc = _enc_obj(v, blobs)
     if blobs:
         raise TypeError("tensors nested in object columns cannot be shuffled; use a tensor column")
@@ -363,8 +368,12 @@ def _enc_plain(v):
 
 def _dec_plain(v):
     if isinstance(v, dict) and "__tt__" in v:
-        data, dt = v["__tt__"]
-        return torch.tensor(data, dtype=getattr(torch, dt))
+        data, dt, shape = v["__tt__"]
+        raw = bytearray(base64.b64decode(data))
+        dtype = getattr(torch, dt)
+        if not raw:
+            return torch.empty(shape, dtype=dtype)
+        return torch.frombuffer(raw, dtype=torch.uint8).view(dtype).reshape(shape).clone()
     return _dec_obj(v, [])
 
 

@@ -67,10 +67,19 @@ class PinnedHostTier:
     def fetch(self, host: RecordBatch, ev: Optional[torch.cuda.Event], nbytes: int) -> RecordBatch:
         """Pinned host batch -> device batch (async H2D), ordered before the consumer stream's next work."""
         consumer = torch.cuda.current_stream(self.device)
+
+        def h2d(t: torch.Tensor) -> torch.Tensor:
+            d = t.to(self.device, non_blocking=True)
+            # d is allocated on the copy stream's pool; the consumer reads it, so a free must wait for the
+            # consumer's queued kernels too (else the next fetch's H2D may overwrite it under them)
+            if d.device.type == "cuda":
+                d.record_stream(consumer)
+            return d
+
         with torch.cuda.stream(self.stream):
             if ev is not None:
                 self.stream.wait_event(ev)
-            dev = _map_tensors(host, lambda t: t.to(self.device, non_blocking=True))
+            dev = _map_tensors(host, h2d)
         consumer.wait_stream(self.stream)
         self.used = max(0, self.used - nbytes)
         self.stats["fetches"] += 1

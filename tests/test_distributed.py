@@ -248,3 +248,27 @@ def test_distributed_block_dedup():
         assert r["err"] == 0.0 and r["err2"] == 0.0
         assert r["stored"] == 12 + 3          # 12 blocks per table, rank 1 adds 3 private ones
         assert r["blocks_in"] == 24
+
+
+def _object_tensor_shuffle_scenario(ctx, out_dir):
+    """Tensors inside object columns keep their exact bytes on the wire (int64 near 2^40, float64)."""
+    from netsdb_amd.objects.record import RecordBatch
+
+    vals = [torch.tensor([(1 << 40) + 7 * i + ctx.rank, -(1 << 41) - i], dtype=torch.int64) for i in range(6)]
+    fl = [torch.tensor([1.0 / 3.0 + i, 1e-300], dtype=torch.float64) for i in range(6)]
+    b = RecordBatch({"v": vals, "f": fl, "i": torch.arange(6)}, 6)
+    dest = torch.arange(6) % 2
+    parts = [b.take(torch.nonzero(dest == d).flatten()) for d in range(2)]
+    got = ctx.exchange(parts)
+    return [([x.tolist() for x in g["v"]], [x.tolist() for x in g["f"]], [x.dtype for x in g["v"]]) for g in got]
+
+
+@pytest.mark.timeout(300)
+def test_distributed_object_tensor_exact_bytes():
+    res = _run("_object_tensor_shuffle_scenario")
+    for rank, got in enumerate(res):
+        for src, (v, f, dts) in enumerate(got):
+            idx = [i for i in range(6) if i % 2 == rank]
+            assert v == [[(1 << 40) + 7 * i + src, -(1 << 41) - i] for i in idx]
+            assert f == [[1.0 / 3.0 + i, 1e-300] for i in idx]
+            assert all(d == torch.int64 for d in dts)

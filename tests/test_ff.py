@@ -14,9 +14,10 @@ def _run(tmp_path, fusion, device="cpu", two_layers=False):
     ff.load_model(c, "ff", batch, feats, hid, labels, block_x=16, block_y=32, hidden2=32 if two_layers else None,
                   dtype=torch.float32)
     if two_layers:
-        ff.inference(c, "ff", "w1", "w2", "wo", "inputs", "b1", "b2", "bo", "output")
+        res = ff.inference(c, "ff", "w1", "w2", "wo", "inputs", "b1", "b2", "bo", "output")
     else:
-        ff.inference_unit(c, "ff", "w1", "wo", "inputs", "b1", "bo", "output")
+        res = ff.inference_unit(c, "ff", "w1", "wo", "inputs", "b1", "bo", "output")
+    c.last_jobs = res["jobs"]
     out = to_tensor(c, "ff", "output")
     g = lambda n: to_tensor(c, "ff", n)  # noqa: E731
     ref = ff.reference_inference(g("inputs"), g("w1"), g("b1"), g("wo"), g("bo"),
@@ -29,8 +30,16 @@ def test_ff_inference_unit_cpu(tmp_path, fusion):
     out, ref, c = _run(tmp_path, fusion)
     assert out.shape == ref.shape
     torch.testing.assert_close(out, ref, atol=2e-3, rtol=2e-2)
+    fused = [op for j in c.last_jobs for op in j.get("fused_ops", [])]
     if fusion:
-        assert c.engine.last_plan is None or True
+        # the whole graph lowers onto MFMA GEMMs with fused epilogues: no TCAP pipeline runs
+        assert any(op.startswith("matmul[FFTransposeMult") for op in fused), fused
+        assert any(op.startswith("epilogue[FFReluBiasSum") for op in fused), fused
+        assert any(op.startswith("softmax[FFOutputLayer") for op in fused), fused
+        assert c.engine.last_plan is None
+    else:
+        assert fused == []
+        assert c.engine.last_plan is not None and len(c.engine.last_plan.stages) > 0
 
 
 @pytest.mark.parametrize("fusion", [True, False])
