@@ -214,6 +214,7 @@ __global__ void __launch_bounds__(256, 4) conv2d_igemm_kernel(ConvParams p) {
 // Preconditions (host-checked): stride 1, dil 1, pad 0, KW <= 8, W % 8 == 0, OW <= 112,
 // C*KH <= 4*CVR_NKS, C*(4+KH-1) <= CVR_ROWS.
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 constexpr int CVR_TR = 4, CVR_NKS = 6, CVR_CP = 288;                 // rows/block, max k-steps, copy stride (B)
 constexpr int CVR_ROWS = 30;                                           // max (c, r) input rows per group
 constexpr int CVR_ZERO = CVR_ROWS * 4 * CVR_CP;                        // zero block (A source past C*KH)
@@ -221,6 +222,7 @@ constexpr int CVR_BUF = CVR_ZERO + 4 * CVR_CP;
 constexpr int CVR_MAXT = 7;                                            // output tiles of 16 per row (OW <= 112)
 constexpr int CVR_OSTAGE = 32 * CVR_TR * (16 * CVR_MAXT + 4) * 2;      // [TR][32 oc][OWS] bf16 (one half)
 constexpr int CVR_WROW = CVR_NKS * 4 * 16 + 16;                       // staged filter row (B)
+constexpr int CVR_TRASH = 64;                                          // sink for masked epilogue LDS writes
 
 struct ConvRowParams {
   const unsigned short* X;
@@ -241,7 +243,7 @@ struct ConvRowParams {
 template <int ACT, bool STAGED, bool DIAG>
 __global__ void __launch_bounds__(256, 2) conv2d_rows_kernel(ConvRowParams p) {
   const int var = DIAG ? p.variant : 0;
-  __shared__ __attribute__((aligned(16))) char smem[CVR_BUF + CVR_OSTAGE];
+  __shared__ __attribute__((aligned(16))) char smem[CVR_BUF + CVR_OSTAGE + CVR_TRASH];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int oc0 = blockIdx.y * 64;
@@ -307,21 +309,34 @@ __global__ void __launch_bounds__(256, 2) conv2d_rows_kernel(ConvRowParams p) {
   const int items = p.C * p.rin * p.chunks;
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<unsigned short*>(p.X), (short)0, (int)((long long)p.N * p.C * p.H * p.W * 2), 0x00020000);
-  u32x4 lo[2], hi[2];
+  u32x4 lo[2];
+  u32x2 hi[2];
+  // per-thread staging items are the same for every group: precompute their image-relative byte offsets
+  // and validity once (a per-group div/mod + 64-bit mad chain here sat between the prefetch loads and made
+  // hipcc wait for them in place)
+  int it_off[2], it_r[2];
+  bool it_lo[2], it_hi[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int it = min(tid + u * 256, items - 1);
+    const int j = it % p.chunks, cr = it / p.chunks, r = cr % p.rin, c = cr / p.rin;
+    it_off[u] = ((c * p.H + r) * p.W + 8 * j) * 2;
+    it_r[u] = r;
+    it_lo[u] = 8 * j < p.W;
+    it_hi[u] = 8 * (j + 1) < p.W;
+  }
   // branch-free: an invalid chunk gets an out-of-range offset and the buffer range check returns
   // zeros (a branch around each load makes hipcc wait vmcnt(0) right after it — no prefetch)
   auto fetch = [&](int g) {
+    const bool gok = g < p.ngroups;
     const int n = g / p.groups_per_img, oh0 = (g % p.groups_per_img) * CVR_TR;
+    const int gbase = ((n * p.C * p.H) + oh0) * p.W * 2;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int it = min(tid + u * 256, items - 1);
-      const int j = it % p.chunks, cr = it / p.chunks, r = cr % p.rin, c = cr / p.rin;
-      const int ih = oh0 + r;
-      const int rowoff = (((n * p.C + c) * p.H + ih) * p.W) * 2;
-      const bool rok = ih < p.H;
-      lo[u] = __builtin_amdgcn_raw_buffer_load_b128(xr, (rok && 8 * j < p.W) ? rowoff + 16 * j : 0x7ffffff0, 0, 0);
-      hi[u] = __builtin_amdgcn_raw_buffer_load_b128(xr, (rok && 8 * (j + 1) < p.W) ? rowoff + 16 * (j + 1) : 0x7ffffff0,
-                                                   0, 0);
+      const bool rok = gok && oh0 + it_r[u] < p.H;
+      const int o = gbase + it_off[u];
+      lo[u] = __builtin_amdgcn_raw_buffer_load_b128(xr, (rok && it_lo[u]) ? o : 0x7ffffff0, 0, 0);
+      hi[u] = __builtin_amdgcn_raw_buffer_load_b64(xr, (rok && it_hi[u]) ? o + 16 : 0x7ffffff0, 0, 0);
     }
   };
   auto store_rows = [&](char* buf) {
@@ -345,6 +360,9 @@ __global__ void __launch_bounds__(256, 2) conv2d_rows_kernel(ConvRowParams p) {
   };
 
   const long long OHW = (long long)p.OH * p.OW;
+  const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+      p.out, (short)0, (int)std::min<long long>((long long)p.N * p.OC * OHW * (p.out_f32 ? 4 : 2), 0x7fffffffLL),
+      0x00020000);
   unsigned short* ostage = reinterpret_cast<unsigned short*>(smem + CVR_BUF);   // [32 oc][segs] bf16
   constexpr bool staged = STAGED;
   // stage layout "segment-major" [32 oc][segs]: the TR output rows of one oc plane are adjacent in
@@ -364,15 +382,20 @@ __global__ void __launch_bounds__(256, 2) conv2d_rows_kernel(ConvRowParams p) {
     return t;
   };
   if (var & 32) st_t0 = stamp();
-  if (g < p.ngroups) fetch(g);
+  if (g < p.ngroups) {
+    fetch(g);
+    store_rows(smem);                                  // first group staged before the loop (one drain)
+  }
   for (; g < p.ngroups; g += gridDim.x) {
     const int n = g / p.groups_per_img, oh0 = (g % p.groups_per_img) * CVR_TR, oh = oh0 + wave;
     if (var & 32) st_tmp = stamp();
-    __syncthreads();                                   // previous group's readers of both buffers are done
-    store_rows(smem);
-    __syncthreads();
+    __syncthreads();                                   // this group's staged input rows are visible
     if (var & 32) { const unsigned long long t = stamp(); st_stage += t - st_tmp; st_tmp = t; }
-    if (g + (int)gridDim.x < p.ngroups) fetch(g + gridDim.x);   // next group's rows in flight during compute
+    // next group's rows in flight during compute and the output stores; staged into LDS at the END of
+    // this iteration. Issued unconditionally (past the last group every offset is out of range), so the
+    // loads consumed in an iteration are always the ones issued at its top, followed by exactly the
+    // group's output stores: hipcc waits vmcnt(<stores>) for them instead of draining the output stores
+    fetch(g + gridDim.x);
     // two passes over the row, 32 output channels each: the [32 oc][TR][OWS] bf16 stage is 28 KB, so
     // two blocks fit a CU (the A fragments are re-read from LDS for the second half — cheap)
     const int rows_valid = min(CVR_TR, p.OH - oh0);
@@ -420,9 +443,12 @@ __global__ void __launch_bounds__(256, 2) conv2d_rows_kernel(ConvRowParams p) {
             for (int r = 0; r < 4; ++r) vv[r] = act_t<ACT>(acc[nt][r] + bias_v[nt]);
             if (staged) {
               if (!(var & 4)) {   // [ocl - 32*half][row*OW + ow]: 2 dword writes (OW even -> 4-B aligned)
+                // branch-free: a pixel pair past OW is written to the trash word (a branch per write made
+                // hipcc split the tile epilogue into 8 exec-masked blocks)
                 unsigned* dst = reinterpret_cast<unsigned*>(ostage + (ocl - 32 * half) * segs + wave * p.OW + owb);
-                if (owb + 1 < p.OW) dst[0] = pack_bf16x2(vv[0], vv[1]);
-                if (owb + 3 < p.OW) dst[1] = pack_bf16x2(vv[2], vv[3]);
+                unsigned* trash = reinterpret_cast<unsigned*>(smem + CVR_BUF + CVR_OSTAGE);
+                *(owb + 1 < p.OW ? dst : trash) = pack_bf16x2(vv[0], vv[1]);
+                *(owb + 3 < p.OW ? dst + 1 : trash) = pack_bf16x2(vv[2], vv[3]);
               } else {
                 acc[0][0] += vv[1];
               }
@@ -448,10 +474,10 @@ __global__ void __launch_bounds__(256, 2) conv2d_rows_kernel(ConvRowParams p) {
         // (all LDS reads first, then the stores: a read->store pair per oc would expose the LDS latency)
         const int noc = min(32, p.OC - (oc0 + 32 * half));
         const int seg = rows_valid * p.OW;
-        unsigned short* obase = reinterpret_cast<unsigned short*>(p.out) +
-                                ((long long)n * p.OC + oc0 + 32 * half) * OHW + (long long)oh0 * p.OW;
-        if (p.vec8 && (seg & 3) == 0) {
-          // 8-B chunks (plane and row offsets are 8-B aligned: host checked OH*OW % 4 == 0)
+        const int obase = (int)((((long long)n * p.OC + oc0 + 32 * half) * OHW + (long long)oh0 * p.OW) * 2);
+        {
+          // 8-B chunks (plane and row offsets are 8-B aligned and every run is a multiple of 4 pixels:
+          // host checked OH*OW % 4 == 0 and (OH % 4) * OW % 4 == 0)
           const int n4 = seg >> 2;
           uint2 v[8][2];
 #pragma unroll
@@ -464,31 +490,15 @@ __global__ void __launch_bounds__(256, 2) conv2d_rows_kernel(ConvRowParams p) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
               const int ocl = wave + 4 * j, q = lane + 64 * h;
-              if (ocl < noc && q < n4) *reinterpret_cast<uint2*>(obase + ocl * OHW + 4 * q) = v[j][h];
+              const int off = (ocl < noc && q < n4) ? obase + (int)(ocl * OHW * 2) + 8 * q : 0x7ffffff0;
+              __builtin_amdgcn_raw_buffer_store_b64(u32x2{v[j][h].x, v[j][h].y}, orsrc, off, 0, 0);
             }
-        } else {
-          const int n2 = seg >> 1;   // OW even -> dword chunks, 4-B aligned
-#pragma unroll
-          for (int b2 = 0; b2 < 2; ++b2) {
-            unsigned v[4][4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-#pragma unroll
-              for (int h = 0; h < 4; ++h)
-                v[j][h] = *reinterpret_cast<const unsigned*>(ostage + (wave + 4 * (4 * b2 + j)) * segs +
-                                                             2 * min(lane + 64 * h, n2 - 1));
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-#pragma unroll
-              for (int h = 0; h < 4; ++h) {
-                const int ocl = wave + 4 * (4 * b2 + j), q = lane + 64 * h;
-                if (ocl < noc && q < n2) reinterpret_cast<unsigned*>(obase + ocl * OHW)[q] = v[j][h];
-              }
-          }
         }
       }
       __syncthreads();
     }
+    if (!staged) __syncthreads();                      // (the staged half loop ends with a barrier)
+    store_rows(smem);
     if (var & 32) st_work += stamp() - st_tmp;
   }
   if ((var & 32) && lane == 0) {
@@ -558,11 +568,12 @@ int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* ou
     if ((q.segs / 2) % 4 == 0) q.segs += 4;
     q.vec8 = ((long long)p.OH * p.OW) % 4 == 0 && (reinterpret_cast<uintptr_t>(out) & 7) == 0;
     if (32 * q.segs * 2 > nsdb::CVR_OSTAGE) goto generic;
+    if ((long long)N * OC * p.OH * p.OW * 2 >= 0x7ffffff0LL) goto generic;    // 31-bit buffer offsets
     if (C * rin * q.chunks > 512 || 64 * ldw / 8 > 6 * 256 || 64 * ldw * 2 > nsdb::CVR_BUF) goto generic;
     {
       const int blocks = std::min(q.ngroups, 256 * 2);     // persistent: two blocks per CU
       const dim3 grid(blocks, (OC + 63) / 64);
-      const bool staged = nchw_out && !out_f32 && (p.OW & 1) == 0;
+      const bool staged = nchw_out && !out_f32 && (p.OW & 1) == 0 && q.vec8 && ((p.OH % 4) * p.OW) % 4 == 0;
       if (q.variant != 0) {   // diagnostics build (timing only): runtime variant bits, no activation
         if (staged) hipLaunchKernelGGL((nsdb::conv2d_rows_kernel<nsdb::ACT_NONE, true, true>), grid, dim3(256), 0, stream, q);
         else hipLaunchKernelGGL((nsdb::conv2d_rows_kernel<nsdb::ACT_NONE, false, true>), grid, dim3(256), 0, stream, q);
