@@ -79,6 +79,7 @@ PYBIND11_MODULE(_native, m) {
         return py::memoryview::from_memory(b.slot_ptr(slot), (ssize_t)b.page_size(), false);
       })
       .def("drop_set", &BufferManager::drop_set)
+      .def("drop_page", &BufferManager::drop_page)
       .def("flush_set", &BufferManager::flush_set, py::call_guard<py::gil_scoped_release>())
       .def("flush_all", &BufferManager::flush_all, py::call_guard<py::gil_scoped_release>())
       .def("prefetch", &BufferManager::prefetch, py::call_guard<py::gil_scoped_release>())

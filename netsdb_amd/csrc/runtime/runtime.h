@@ -106,6 +106,7 @@ class BufferManager {
   int64_t pin(int64_t set_id, int64_t page_no, bool create);
   void unpin(int64_t set_id, int64_t page_no, bool dirty, uint64_t bytes_used);
   void drop_set(int64_t set_id);
+  bool drop_page(int64_t set_id, int64_t page_no);   // forget one page (frame freed; file bytes left unreferenced)
   void flush_set(int64_t set_id);
   void flush_all();
   bool prefetch(int64_t set_id, int64_t page_no);   // load an evicted page into a slot (stays unpinned)

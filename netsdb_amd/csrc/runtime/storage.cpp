@@ -264,6 +264,22 @@ void BufferManager::unpin(int64_t set_id, int64_t page_no, bool dirty, uint64_t 
   }
 }
 
+bool BufferManager::drop_page(int64_t set_id, int64_t page_no) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = table_.find(PageKey{set_id, page_no});
+  if (it != table_.end()) {
+    Frame& fr = frames_[it->second];
+    if (fr.pins > 0) return false;
+    if (fr.in_lru) lru_.erase(fr.lru_it);
+    fr = Frame();
+    free_slots_.push_back(it->second);
+    table_.erase(it);
+  }
+  auto k = known_.find(set_id);
+  if (k != known_.end()) k->second.erase(page_no);
+  return true;
+}
+
 void BufferManager::drop_set(int64_t set_id) {
   std::lock_guard<std::mutex> g(mu_);
   for (auto it = table_.begin(); it != table_.end();) {

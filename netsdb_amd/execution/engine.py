@@ -73,6 +73,14 @@ class BuildTable:
         self.h = batch.columns[hash_col] if batch is not None and batch.n else torch.empty(0, dtype=torch.int64)
 
 
+class PartitionedBuild:
+    """An out-of-core join build side: hash partitions in spillable spools (PartitionedHashSet)."""
+
+    def __init__(self, parts, hash_col: str):
+        self.parts = parts
+        self.hash_col = hash_col
+
+
 class JobStats(dict):
     pass
 
@@ -87,6 +95,9 @@ class QueryEngine:
         self.broadcast_threshold = broadcast_threshold
         self.fusion = fusion
         self.last_plan = None
+        self.ooc_stats = {}
+        self.ooc_fraction = 0.25          # of the device budget: in-memory build / group-by / tuple-set limit
+        self._spools = []
         self.last_tcap = None
         self._last_comps = None
 
@@ -98,8 +109,12 @@ class QueryEngine:
         if self.fusion:
             from ..query_planning.fusion import fuse_tensor_patterns
 
+            ooc0 = dict(self.ooc_stats)
             sinks, fused = fuse_tensor_patterns(sinks, self)
             stats["fused_ops"] = fused
+            ooc = {k: v - ooc0.get(k, 0) for k, v in self.ooc_stats.items() if v - ooc0.get(k, 0)}
+            if ooc:
+                stats["out_of_core"] = ooc
             if not sinks:
                 stats["seconds"] = time.perf_counter() - t0
                 self.last_plan = self.last_tcap = self._last_comps = None
@@ -113,12 +128,21 @@ class QueryEngine:
         pplan = planner.plan(atoms)
         self.last_plan = pplan
         state = _JobState(plan.computations)
-        for st in pplan.stages:
-            ts = time.perf_counter()
-            with self.tracer.span(f"stage{st.id}", job=job_name, sink=st.sink.get("kind")):
-                n = self._run_stage(st, state)
-            stats["stages"].append({"id": st.id, "desc": st.describe(), "rows_in": n,
-                                    "seconds": time.perf_counter() - ts})
+        ooc0 = dict(self.ooc_stats)
+        try:
+            for st in pplan.stages:
+                ts = time.perf_counter()
+                with self.tracer.span(f"stage{st.id}", job=job_name, sink=st.sink.get("kind")):
+                    n = self._run_stage(st, state)
+                stats["stages"].append({"id": st.id, "desc": st.describe(), "rows_in": n,
+                                        "seconds": time.perf_counter() - ts})
+        finally:
+            for sp in self._spools:        # job-scoped spills (builds, spooled tuple sets) end with the job
+                sp.drop()
+            self._spools = []
+        ooc = {k: v - ooc0.get(k, 0) for k, v in self.ooc_stats.items() if v - ooc0.get(k, 0)}
+        if ooc:
+            stats["out_of_core"] = dict(stats.get("out_of_core", {}), **ooc)
         stats["seconds"] = time.perf_counter() - t0
         stats["tcap_atoms"] = len(atoms)
         return stats
@@ -143,35 +167,78 @@ class QueryEngine:
             for b in state.materialized.get(src["ts"], []):
                 yield b
 
+    def _ooc_limit(self) -> int:
+        """Bytes an in-memory join build / group-by / materialised tuple set may take before it is
+        hash-partitioned into spillable spools (a fraction of the node's device budget)."""
+        return max(1 << 14, int(self.storage.device_budget * self.ooc_fraction))
+
     def _run_stage(self, st, state) -> int:
-        # split ops at partitioned-join probes: their inputs must be shuffled collectively first
+        # split ops at partitioned-join probes (inputs shuffled collectively first) and at probes of
+        # out-of-core (partitioned) builds (probe side hash-partitioned into spools, Grace join)
         segments: List[List[dict]] = [[]]
         for o in st.ops:
-            if o["type"] == "JOIN" and o.get("_strategy") == "partitioned":
+            if o["type"] == "JOIN" and (o.get("_strategy") == "partitioned" or
+                                        isinstance(state.builds.get(o["output"]["name"]), PartitionedBuild)):
                 segments.append([o])
             else:
                 segments[-1].append(o)
-        batches = self._source_batches(st, state)
-        rows = 0
+        rows = [0]
+
+        def source():
+            for b in self._source_batches(st, state):
+                rows[0] += b.n
+                yield b
+
+        it = source()
         for si, seg in enumerate(segments):
+            ops = seg
             if si > 0:
-                # collective repartition of the probe side by its join hash
                 probe = seg[0]
                 hcol = probe["input"]["atts"][0] if probe["_probe_side"] == "left" else probe["input2"]["atts"][0]
-                collected = [b for b in batches if b.n]
-                batches = iter(self._shuffle_by(collected, hcol))
-            out = []
-            for b in batches:
-                if si == 0:
-                    rows += b.n
-                for o in seg:
-                    if b.n == 0 and o["type"] != "JOIN":
-                        break
-                    b = self._apply_atom(o, b, state)
-                out.append(b)
-            batches = iter(out)
-        self._sink(st, list(batches), state)
-        return rows
+                if probe.get("_strategy") == "partitioned":
+                    # collective repartition of the probe side by its join hash
+                    collected = [b for b in it if b.n]
+                    it = iter(self._shuffle_by(collected, hcol))
+                pb = state.builds.get(probe["output"]["name"])
+                if isinstance(pb, PartitionedBuild):
+                    it = self._grace_probe(probe, it, pb, hcol, state)
+                    ops = seg[1:]
+            it = self._apply_ops(ops, it, state)
+        self._sink(st, it, state)
+        return rows[0]
+
+    def _apply_ops(self, ops, it, state):
+        """Stream batches through a segment's atoms (generator: one page in flight per stage)."""
+        for b in it:
+            for o in ops:
+                if b.n == 0 and o["type"] != "JOIN":
+                    break
+                b = self._apply_atom(o, b, state)
+            yield b
+
+    def _grace_probe(self, a, it, pb: "PartitionedBuild", hcol: str, state):
+        """Out-of-core hash join (PartitionedHashSet): the probe side is hash-partitioned into spools with
+        the build side's partition function, then each partition's build table is built alone and probed."""
+        from .spool import PartitionedSpool
+
+        name = a["output"]["name"]
+        probe_parts = PartitionedSpool(self.storage, pb.parts.nparts, "probe")
+        try:
+            for b in it:
+                if b.n:
+                    probe_parts.add(b, b.columns[hcol])
+            self.ooc_stats["grace_joins"] = self.ooc_stats.get("grace_joins", 0) + 1
+            for p in range(pb.parts.nparts):
+                if probe_parts.parts[p].n == 0 or pb.parts.parts[p].n == 0:
+                    continue
+                state.builds[name] = BuildTable(pb.parts.parts[p].concat(), pb.hash_col)
+                self.ooc_stats["grace_partitions"] = self.ooc_stats.get("grace_partitions", 0) + 1
+                for b in probe_parts.parts[p]:
+                    yield self._probe(a, b, state)
+                state.builds[name] = pb
+        finally:
+            state.builds[name] = pb
+            probe_parts.drop()
 
     def _shuffle_by(self, batches: List[RecordBatch], hcol: str) -> List[RecordBatch]:
         ws = self.ctx.world_size
@@ -268,21 +335,22 @@ class QueryEngine:
         return RecordBatch(cols, int(pi.numel()))
 
     # ------------------------------------------------------------------ sinks
-    def _sink(self, st, batches: List[RecordBatch], state):
+    def _sink(self, st, batches, state):
         sk = st.sink
         kind = sk["kind"]
-        batches = [x for x in batches if x is not None]
         if kind == "discard":
+            for _ in batches:
+                pass
             return
         if kind == "materialize":
-            state.materialized[sk["ts"]] = batches
+            state.materialized[sk["ts"]] = self._collect(batches, "mat")
             return
         if kind == "output":
             a = sk["atom"]
             col = a["input"]["atts"][0]
             uset = self.storage.get_set(a["db"], a["set"])
             for x in batches:
-                if x.n == 0:
+                if x is None or x.n == 0:
                     continue
                 v = x.columns[col]
                 if not isinstance(v, RecordBatch):
@@ -294,42 +362,139 @@ class QueryEngine:
             side = sk["side"]
             hcol = a["input"]["atts"][0] if side == "left" else a["input2"]["atts"][0]
             cols = (a["projection"]["atts"] if side == "left" else a["projection2"]["atts"]) + [hcol]
-            parts = [RecordBatch({c: x.columns[c] for c in cols}, x.n) for x in batches if x.n]
-            local = RecordBatch.concat(parts) if parts else None
+            parts = (RecordBatch({c: x.columns[c] for c in cols}, x.n) for x in batches if x is not None and x.n)
             strat = sk["strategy"]
-            if strat == "broadcast":
-                got = self.ctx.broadcast_batch_all(local)
+            name = a["output"]["name"]
+            if self.ctx.distributed and strat in ("broadcast", "partitioned"):
+                parts = list(parts)
+                local = RecordBatch.concat(parts) if parts else None
+                if strat == "broadcast":
+                    got = self.ctx.broadcast_batch_all(local)
+                else:
+                    got = self._shuffle_by([local] if local is not None else [], hcol)
                 got = [g for g in got if g is not None and g.n]
-                local = RecordBatch.concat(got) if got else None
-            elif strat == "partitioned":
-                got = self._shuffle_by([local] if local is not None else [], hcol)
-                got = [g for g in got if g.n]
-                local = RecordBatch.concat(got) if got else None
-            state.builds[a["output"]["name"]] = BuildTable(local, hcol)
+                parts = iter(got)
+            state.builds[name] = self._build_table(parts, hcol, st)
             return
         if kind == "aggregate":
             self._aggregate(sk["atom"], batches, state)
             return
         if kind == "partition":
-            self._partition(sk["atom"], batches, state)
+            self._partition(sk["atom"], [x for x in batches if x is not None], state)
             return
         raise ValueError(kind)
 
+    def _collect(self, batches, tag: str):
+        """Keep a tuple set in memory while it is small; past the out-of-core limit continue it in a
+        spillable spool (pages charged to the budget, LRU-spilled, re-read page by page)."""
+        from .spool import Spool
+
+        limit = self._ooc_limit()
+        held, size, spool = [], 0, None
+        for b in batches:
+            if b is None:
+                continue
+            if spool is not None:
+                spool.add(b)
+                continue
+            held.append(b)
+            size += b.nbytes()
+            if size > limit:
+                spool = Spool(self.storage, tag)
+                for h in held:
+                    spool.add(h)
+                held = []
+                self.ooc_stats["spooled_sets"] = self.ooc_stats.get("spooled_sets", 0) + 1
+        if spool is not None:
+            self._spools.append(spool)
+            return spool
+        return held
+
+    def _build_table(self, parts, hcol: str, st) -> "BuildTable":
+        """In-memory build table, or — past the out-of-core limit — a hash-partitioned build whose
+        partitions live in spillable spools (probed partition by partition: Grace hash join)."""
+        from .spool import PartitionedSpool
+
+        limit = self._ooc_limit()
+        held, size, pspool = [], 0, None
+        for b in parts:
+            if pspool is not None:
+                pspool.add(b, b.columns[hcol])
+                continue
+            held.append(b)
+            size += b.nbytes()
+            if size > limit:
+                est = max(size, self._stage_source_bytes(st))
+                nparts = int(min(256, max(2, -(-2 * est // limit))))
+                pspool = PartitionedSpool(self.storage, nparts, "build")
+                for h in held:
+                    pspool.add(h, h.columns[hcol])
+                held = []
+        if pspool is not None:
+            self._spools.append(pspool)
+            self.ooc_stats["partitioned_builds"] = self.ooc_stats.get("partitioned_builds", 0) + 1
+            return PartitionedBuild(pspool, hcol)
+        return BuildTable(RecordBatch.concat(held) if held else None, hcol)
+
+    def _stage_source_bytes(self, st) -> int:
+        src = st.source
+        if src["kind"] == "scan":
+            try:
+                return self.storage.get_set(src["atom"]["db"], src["atom"]["set"]).nbytes()
+            except KeyError:
+                return 0
+        return 0
+
     def _aggregate(self, a, batches, state):
+        from .spool import PartitionedSpool
+
         comp: AggregateComp = state.comps[a["comp"]]
         kcol, vcol = a["input"]["atts"]
         out_ts, out_col = a["output"]["name"], a["output"]["atts"][0]
-        nonempty = [x for x in batches if x.n]
         if isinstance(comp, TopKComp):
-            self._topk(comp, nonempty, kcol, vcol, out_ts, out_col, state)
+            self._topk(comp, [x for x in batches if x is not None and x.n], kcol, vcol, out_ts, out_col, state)
             return
-        keys = column_concat([x.columns[kcol] for x in nonempty]) if nonempty else None
-        vals = column_concat([x.columns[vcol] for x in nonempty]) if nonempty else None
         op = getattr(comp, "reduce_op", "sum")
         combine = comp.combine
-        if keys is not None:
-            inv, reps, g = K.group_ids(keys)
-            agg = K.segment_reduce(vals, inv, g, op if isinstance(vals, torch.Tensor) else None, combine)
+        # stream (key, value) pairs; past the out-of-core limit hash-partition them by key into spools
+        # and reduce each partition alone (its groups are disjoint from every other partition's)
+        limit = self._ooc_limit()
+        held, size, pspool = [], 0, None
+        for x in batches:
+            if x is None or x.n == 0:
+                continue
+            kv = RecordBatch({"k": x.columns[kcol], "v": x.columns[vcol]}, x.n)
+            if pspool is not None:
+                pspool.add(kv, K.hash_keys(kv.columns["k"], kv.device))
+                continue
+            held.append(kv)
+            size += kv.nbytes()
+            if size > limit:
+                nparts = int(min(256, max(2, -(-2 * size // limit))))
+                pspool = PartitionedSpool(self.storage, nparts, "agg")
+                for h in held:
+                    pspool.add(h, K.hash_keys(h.columns["k"], h.device))
+                held = []
+        groups = [held] if pspool is None else [p for p in pspool.parts if p.n]
+        reps_parts, agg_parts = [], []
+        try:
+            for grp in groups:
+                bs = [b for b in grp if b.n]
+                if not bs:
+                    continue
+                keys = column_concat([b.columns["k"] for b in bs])
+                vals = column_concat([b.columns["v"] for b in bs])
+                inv, reps, g = K.group_ids(keys)
+                reps_parts.append(reps)
+                agg_parts.append(K.segment_reduce(vals, inv, g, op if isinstance(vals, torch.Tensor) else None,
+                                                  combine))
+        finally:
+            if pspool is not None:
+                pspool.drop()
+                self.ooc_stats["partitioned_aggregations"] = self.ooc_stats.get("partitioned_aggregations", 0) + 1
+        if reps_parts:
+            reps = reps_parts[0] if len(reps_parts) == 1 else column_concat(reps_parts)
+            agg = agg_parts[0] if len(agg_parts) == 1 else column_concat(agg_parts)
         else:
             reps, agg = None, None
         if self.ctx.distributed:

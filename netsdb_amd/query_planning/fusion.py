@@ -48,12 +48,23 @@ class Dense:
     (the logical dimension split over ranks, ``offset`` = first global index held here,
     ``total`` = global extent of that dimension)."""
 
-    def __init__(self, phys: torch.Tensor, rows: int, cols: int, transposed: bool, br: int, bc: int,
-                 part: Optional[str] = None, offset: int = 0, total: Optional[int] = None):
-        self.phys, self.rows, self.cols, self.transposed = phys, rows, cols, transposed
+    def __init__(self, phys: Optional[torch.Tensor], rows: int, cols: int, transposed: bool, br: int, bc: int,
+                 part: Optional[str] = None, offset: int = 0, total: Optional[int] = None, src=None):
+        self._phys, self.rows, self.cols, self.transposed = phys, rows, cols, transposed
         self.br, self.bc = br, bc
         self.part, self.offset = part, offset
         self.total = total if total is not None else (rows if part == "rows" else cols if part == "cols" else 0)
+        self.src = src            # the DenseMatrixSet behind a scanned value (panel fetched on first use)
+
+    @property
+    def phys(self) -> torch.Tensor:
+        if self._phys is None and self.src is not None:
+            return self.src.panel          # reloads a spilled panel; not cached: the set may evict it again
+        return self._phys
+
+    @phys.setter
+    def phys(self, t):
+        self._phys = t
 
     def physical(self, want_transposed: bool) -> torch.Tensor:
         """K-contiguous physical layout in the wanted orientation (copy only on mismatch)."""
@@ -73,8 +84,8 @@ class Dense:
 
     def t(self) -> "Dense":
         part = {"rows": "cols", "cols": "rows"}.get(self.part) if self.part else None
-        return Dense(self.phys, self.cols, self.rows, not self.transposed, self.bc, self.br, part, self.offset,
-                     self.total)
+        return Dense(self._phys, self.cols, self.rows, not self.transposed, self.bc, self.br, part, self.offset,
+                     self.total, self.src)
 
     @staticmethod
     def of(t: torch.Tensor, br: int, bc: int, part=None, offset=0, total=None) -> "Dense":
@@ -116,8 +127,8 @@ class SourceNode(Node):
         s = self.set
         if self.value is None:
             part = None if (s.replicated or not engine.ctx.distributed) else "rows"
-            self.value = Dense(s.panel, s.local_rows, s.total_cols, s.transposed, s.block_rows, s.block_cols,
-                               part, s.row_offset, s.total_rows)
+            self.value = Dense(None, s.local_rows, s.total_cols, s.transposed, s.block_rows, s.block_cols,
+                               part, s.row_offset, s.total_rows, src=s)
         return self.value
 
 
@@ -176,6 +187,8 @@ class MatmulNode(Node):
             value = self._kpartial(engine, opA, opB, M, N, phys_is_c, bias_t, act, odt)
             self.value = value
             return value
+        elif self._out_of_core(engine, opA, opB, M, N, K, odt):
+            phys = self._ooc_matmul(engine, opA, opB, M, N, K, phys_is_c, bias_t, mode, act, odt)
         else:
             K8 = (K + 7) // 8 * 8
             # X = opA as [M,K] K-contig <=> opA physical not transposed; Y = opB^T as [N,K]
@@ -206,6 +219,74 @@ class MatmulNode(Node):
             value = Dense(phys, M, N, want_t, br, bc, part, offset, total)
         self.value = value
         return value
+
+    # ---------------------------------------------------------------- out-of-core block GEMM
+    @staticmethod
+    def _out_of_core(engine, opA: Dense, opB: Dense, M, N, K, odt) -> bool:
+        """Both operands are stored dense sets whose panels are the GEMM's [rows, K] operands and they do
+        not fit the device budget together with the result: run the block GEMM slab by slab."""
+        sa, sb = opA.src, opB.src
+        if sa is None or sb is None or opA.transposed or not opB.transposed or sa is sb:
+            return False
+        mgr = engine.storage
+        out_b = M * N * torch.empty(0, dtype=odt).element_size()
+        return sa.panel_nbytes() + sb.panel_nbytes() + out_b > mgr.device_budget
+
+    def _ooc_matmul(self, engine, opA: Dense, opB: Dense, M, N, K, phys_is_c, bias_t, mode, act, odt):
+        """netsDB's block-matmul join executed out of core: row slabs of the two operand panels are loaded
+        (from HBM when resident, else from the pinned host tier / page pool they were evicted to) so that
+        two slabs + the result stay within the device budget; each slab pair is one fused MFMA GEMM
+        writing its block of C in place (PipelineStage over spilled pages, PartitionedHashSet-style
+        bounded working set). Dropout masks are drawn per slab pair (seeded by its position)."""
+        sa, sb = opA.src, opB.src
+        mgr = engine.storage
+        dev = mgr.home
+        K8 = (K + 7) // 8 * 8
+        pr, pc = (M, N) if phys_is_c else (N, M)
+        out = torch.empty(pr, pc, dtype=odt, device=dev)
+        out_b = out.numel() * out.element_size()
+        mgr.account_bytes(out_b, dev)
+        # make room: spill every evictable panel/page (the operands included: their slabs stream back)
+        mgr.evict(mgr.device_bytes)
+        row_b = max(sa.row_bytes(), sb.row_bytes())
+        avail = max(mgr.available(), 2 * 16 * row_b)
+        slab = max(16, min(max(M, N), avail // (2 * row_b)))
+        slab = slab // 16 * 16 if slab >= 32 else slab
+        sa_rows = min(M, slab)
+        sb_rows = min(N, slab)
+        nblk = 0
+        for a0 in range(0, M, sa_rows):
+            a1 = min(M, a0 + sa_rows)
+            Xa = sa.load_rows(a0, a1, dev)
+            xb = Xa.numel() * Xa.element_size()
+            mgr.account_bytes(xb, dev)
+            Xa = _kslice(Xa, a1 - a0, K8)
+            for b0 in range(0, N, sb_rows):
+                b1 = min(N, b0 + sb_rows)
+                Yb = sb.load_rows(b0, b1, dev)
+                yb = Yb.numel() * Yb.element_size()
+                mgr.account_bytes(yb, dev)
+                Yb = _kslice(Yb, b1 - b0, K8)
+                seed = self.seed + 0x9E3779B1 * (nblk + 1)
+                if phys_is_c:
+                    b = None if bias_t is None else (bias_t[a0:a1] if mode == ops.BIAS_ROW else bias_t[b0:b1])
+                    ops.gemm_nt(Xa, Yb, b, mode, act, out_dtype=odt, dropout=self.dropout, seed=seed,
+                                out=out[a0:a1, b0:b1])
+                else:
+                    b = None if bias_t is None else (bias_t[b0:b1] if mode == ops.BIAS_ROW else bias_t[a0:a1])
+                    ops.gemm_nt(Yb, Xa, b, mode, act, out_dtype=odt, dropout=self.dropout, seed=seed,
+                                out=out[b0:b1, a0:a1])
+                del Yb
+                mgr.release_bytes(yb, dev)
+                nblk += 1
+            del Xa
+            mgr.release_bytes(xb, dev)
+        mgr.release_bytes(out_b, dev)          # re-charged when the result is installed in its set
+        st = getattr(engine, "ooc_stats", None)
+        if st is not None:
+            st["ooc_matmuls"] = st.get("ooc_matmuls", 0) + 1
+            st["ooc_slab_pairs"] = st.get("ooc_slab_pairs", 0) + nblk
+        return out
 
     def _allgather_n(self, engine, opA: Dense, opB: Dense, M, N, phys_is_c, bias_t, mode, act, odt):
         """Row-split A [M_r, K] x K-split B (rank s holds rows K_s of B): every rank needs all of B.
@@ -486,7 +567,7 @@ class Fuser:
                 s = st.get_set(c.db, c.set_name)
                 if isinstance(s, DenseMatrixSet):
                     s.resolve_shared()         # dedup: linked shared blocks -> the dense panel
-                if isinstance(s, DenseMatrixSet) and s.panel is not None:
+                if isinstance(s, DenseMatrixSet) and s.has_data():
                     return SourceNode(s)
         return None
 

@@ -11,6 +11,7 @@ import itertools
 import os
 import tempfile
 import threading
+from collections import OrderedDict
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -28,6 +29,9 @@ class StorageManager:
         self.root = root or tempfile.mkdtemp(prefix="netsdb_amd_")
         os.makedirs(self.root, exist_ok=True)
         self.device = torch.device(device) if device is not None else None
+        # the "device tier" whose bytes the budget governs: the GPU, or the CPU for a CPU pseudo-cluster
+        # node (out-of-core tests run the same spill/reload code with a CPU home device)
+        self.home = self.device if self.device is not None else torch.device("cpu")
         self.page_size = page_size
         self.rank = rank
         spill = os.path.join(self.root, f"node{rank}")
@@ -52,8 +56,14 @@ class StorageManager:
                     pinned_budget = 8 << 30
             self.host_tier = PinnedHostTier(self.device, pinned_budget)
         self.device_bytes = 0
+        # LRU of everything resident on the device tier (pages and dense panels), oldest first: eviction
+        # pops from the front instead of scanning every page of every set (PageCache's LRU list)
+        self._lru: "OrderedDict[int, object]" = OrderedDict()
         self.sets: Dict[Tuple[str, str], UserSet] = {}
         self._ids = itertools.count(1)
+        # sets created without a catalog id (temp sets, spools) draw from a disjoint range: their pool pages
+        # are keyed by set id and must never alias a catalog set's pages
+        self._temp_ids = itertools.count(1 << 32)
         self._clock = itertools.count()
         self.lock = threading.RLock()
         self.stats = {"evicted_pages": 0, "evicted_bytes": 0}
@@ -66,7 +76,7 @@ class StorageManager:
             if key in self.sets:
                 return self.sets[key]
             dev = self.device if device == "default" else device
-            sid = set_id if set_id is not None else next(self._ids)
+            sid = set_id if set_id is not None else (next(self._ids) if persistent else next(self._temp_ids))
             cls = DenseMatrixSet if dense else UserSet
             s = cls(self, db, name, type_, sid, page_size or self.page_size, dev, persistent)
             self.sets[key] = s
@@ -99,41 +109,99 @@ class StorageManager:
         s.clear()
 
     def _release_pages(self, s: UserSet):
+        if isinstance(s, DenseMatrixSet):
+            s.release_storage()
+            self.untrack(s)
         for p in s.pages:
+            self.untrack(p)
             if p.location == "device" and p.batch is not None:
                 self.device_bytes -= p.nbytes
             elif p.location == "pinned" and self.host_tier is not None:
                 self.host_tier.release(p.nbytes)
 
     # ----------------------------------------------------------- memory accounting / eviction
+    def on_home(self, device) -> bool:
+        """True when ``device`` is the budgeted device tier of this node."""
+        if device is None:
+            return False
+        d, h = torch.device(device), self.home
+        if d.type != h.type:
+            return False
+        return d.type != "cuda" or (d.index or 0) == (h.index or 0)
+
+    def track(self, obj):
+        """``obj`` (a page or dense set) is resident on the device tier: most recently used."""
+        obj.last_use = next(self._clock)
+        self._lru[id(obj)] = obj
+        self._lru.move_to_end(id(obj))
+
+    def untrack(self, obj):
+        self._lru.pop(id(obj), None)
+
     def account(self, page: Page):
         page.last_use = next(self._clock)
         if page.location == "device":
-            self.account_bytes(page.nbytes, self.device)
+            self.track(page)
+            self.account_bytes(page.nbytes, self.home, keep=page)
 
-    def account_bytes(self, nbytes: int, device=None):
-        if device is None or torch.device(device).type != "cuda":
+    def account_bytes(self, nbytes: int, device=None, keep=None):
+        """Charge ``nbytes`` on ``device``; over budget, spill LRU pages / dense panels (never ``keep``)."""
+        if not self.on_home(device):
             return
         with self.lock:
             self.device_bytes += nbytes
             if self.device_bytes > self.device_budget:
-                self.evict(self.device_bytes - self.device_budget)
+                self.evict(self.device_bytes - self.device_budget, keep=keep)
 
-    def touch(self, page: Page):
+    def release_bytes(self, nbytes: int, device=None):
+        if self.on_home(device):
+            with self.lock:
+                self.device_bytes = max(0, self.device_bytes - nbytes)
+
+    def available(self) -> int:
+        """Bytes the budget still admits on the device tier."""
+        return max(0, self.device_budget - self.device_bytes)
+
+    def touch(self, page):
         page.last_use = next(self._clock)
+        if id(page) in self._lru:
+            self._lru.move_to_end(id(page))
 
-    def evict(self, need: int) -> int:
-        """Spill least-recently-used unpinned device pages to the host page pool."""
-        cands = [p for s in self.sets.values() for p in s.pages
-                 if p.location == "device" and p.batch is not None and p.pins == 0]
-        cands.sort(key=lambda p: p.last_use)
+    def evict(self, need: int, keep=None) -> int:
+        """Spill least-recently-used unpinned device pages (to the pinned tier / page pool) and dense
+        panels (in block-row slabs, PageCache/PDBEvictWork style) until ``need`` bytes are free."""
         freed = 0
-        for p in cands:
-            if freed >= need:
+        kept = 0                     # pinned / kept entries stay at the front of the LRU
+        while freed < need:
+            chunk = list(itertools.islice(self._lru.items(), kept, kept + 32))
+            if not chunk:
                 break
-            f = p.spill()
-            freed += f
-            self.stats["evicted_pages"] += 1
+            for key, p in chunk:
+                if freed >= need:
+                    break
+                if p is keep:
+                    kept += 1
+                    continue
+                if isinstance(p, DenseMatrixSet):
+                    if not p.resident_on_home():
+                        self.untrack(p)
+                        continue
+                elif p.location != "device" or p.batch is None:
+                    self.untrack(p)
+                    continue
+                if p.pins:
+                    kept += 1
+                    continue
+                f = p.spill()
+                if f or not (p.resident_on_home() if isinstance(p, DenseMatrixSet) else p.location == "device"):
+                    self.untrack(p)
+                else:
+                    kept += 1
+                freed += f
+                if isinstance(p, DenseMatrixSet):
+                    self.stats["evicted_panels"] = self.stats.get("evicted_panels", 0) + 1
+                else:
+                    self.stats["evicted_pages"] += 1
         self.device_bytes -= freed
         self.stats["evicted_bytes"] += freed
         return freed

@@ -98,6 +98,12 @@ def serialize_batch(batch: RecordBatch) -> bytes:
             b = _tensor_bytes(c)
             cols_meta.append({"name": name, "kind": "tensor", "dtype": _DT[c.dtype], "shape": list(c.shape),
                               "off": add(b), "len": len(b)})
+        elif isinstance(c, RecordBatch):        # nested record column (an engine tuple set's object column)
+            b = serialize_batch(c)
+            cols_meta.append({"name": name, "kind": "batch", "off": add(b), "len": len(b)})
+        elif isinstance(c, tuple):              # tuple column (multi-attribute keys): a nested batch of its parts
+            b = serialize_batch(RecordBatch({f"t{i}": x for i, x in enumerate(c)}, batch.n))
+            cols_meta.append({"name": name, "kind": "tuple", "k": len(c), "off": add(b), "len": len(b)})
         elif isinstance(c, StringColumn):       # packed UTF-8 + offsets: no per-string JSON
             o = c.offsets.cpu()
             base = int(o[0]) if o.numel() else 0
@@ -129,6 +135,11 @@ def deserialize_batch(data) -> RecordBatch:
         seg = mv[base + cm["off"]: base + cm["off"] + cm["len"]]
         if cm["kind"] == "tensor":
             cols[cm["name"]] = _tensor_from(seg, cm["dtype"], cm["shape"])
+        elif cm["kind"] == "batch":
+            cols[cm["name"]] = deserialize_batch(seg)
+        elif cm["kind"] == "tuple":
+            inner = deserialize_batch(seg)
+            cols[cm["name"]] = tuple(inner.columns[f"t{i}"] for i in range(cm["k"]))
         elif cm["kind"] == "string":
             offs = _tensor_from(seg, "i64", [cm["n"] + 1])
             raw = np.frombuffer(mv[base + cm["doff"]: base + cm["doff"] + cm["dlen"]], dtype=np.uint8)

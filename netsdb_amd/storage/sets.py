@@ -33,7 +33,9 @@ class Page:
         self.nbytes = batch.nbytes()
         self.n = batch.n
         self.pins = 0
-        self.location = "device" if batch.device.type == "cuda" else "host"
+        mgr = getattr(uset, "manager", None)
+        home = mgr.on_home(batch.device) if mgr is not None and hasattr(mgr, "on_home") else batch.device.type == "cuda"
+        self.location = "device" if home else "host"
         self.dirty = True
         self.last_use = 0
         self.event = None      # pinned tier: completion event of the page's D2H copy
@@ -76,7 +78,12 @@ class Page:
                 self.batch = tier.fetch(self.batch, self.event, self.nbytes)   # async H2D, stream-ordered
                 self.event = None
                 self.location = "device"
-                self.set.manager.account_bytes(self.nbytes, device)
+                self.set.manager.track(self)
+                self.pins += 1
+                try:
+                    self.set.manager.account_bytes(self.nbytes, device, keep=self)
+                finally:
+                    self.pins -= 1
             else:
                 self.batch = tier.host_view(self.batch, self.event)
             return self.batch
@@ -93,8 +100,16 @@ class Page:
         if device is not None and torch.device(device).type == "cuda":
             b = b.to(device)
         self.batch = b
-        self.location = "device" if b.device.type == "cuda" else "host"
+        mgr = self.set.manager
+        self.location = "device" if mgr.on_home(b.device) else "host"
         self.dirty = False
+        if self.location == "device":
+            mgr.track(self)
+            self.pins += 1            # the reload is charged to the budget; never evict the page being loaded
+            try:
+                mgr.account_bytes(self.nbytes, mgr.home, keep=self)
+            finally:
+                self.pins -= 1
         return b
 
     def persist(self):
@@ -134,7 +149,7 @@ class SharedLink:
     def batches(self, device=None) -> Iterator[RecordBatch]:
         sh = self.shared
         if isinstance(sh, DenseMatrixSet):
-            src = [sh.to_blocks(device)] if sh.panel is not None and (not self.pages or 0 in self.pages) else []
+            src = [sh.to_blocks(device)] if sh.has_data() and (not self.pages or 0 in self.pages) else []
         else:
             src = []
             for pno in self.pages:
@@ -169,7 +184,7 @@ class SharedLink:
     def num_records(self) -> int:
         sh = self.shared
         if isinstance(sh, DenseMatrixSet):
-            return sh.num_blocks() if sh.panel is not None else 0
+            return sh.num_blocks() if sh.has_data() else 0
         return sum(sh.pages[p].n for p in self.pages if 0 <= p < len(sh.pages))
 
 
@@ -220,7 +235,9 @@ class UserSet:
             batch = batch.to(self.device)
         with self.lock:
             per_row = max(1, batch.nbytes() // max(1, batch.n))
-            rows_per_page = max(1, self.page_size // per_row)
+            # leave room for the serialised page header/column directory when the page spills to the pool
+            usable = max(per_row, self.page_size - max(2048, self.page_size // 16))
+            rows_per_page = max(1, usable // per_row)
             for s in range(0, batch.n, rows_per_page):
                 part = batch.slice(s, min(batch.n, s + rows_per_page)) if batch.n > rows_per_page else batch
                 p = Page(self, len(self.pages), part)
@@ -231,6 +248,8 @@ class UserSet:
 
     def clear(self):
         with self.lock:
+            for p in self.pages:
+                self.manager.untrack(p)
             self.pages = []
             self.stats = {"records": 0, "bytes": 0}
             self.manager.buffer_manager.drop_set(self.set_id)
@@ -297,11 +316,25 @@ class UserSet:
 
 
 class DenseMatrixSet(UserSet):
-    """A block-partitioned matrix stored as one dense row-slab panel per node."""
+    """A block-partitioned matrix stored as one dense row-slab panel per node.
+
+    The panel is charged to the node's device budget and is evictable like any page
+    (PageCache.cc / PDBEvictWork): under HBM pressure the storage manager spills it in block-row
+    slabs of about one page — to the pinned host tier by async D2H copies when the panel is on a GPU,
+    else serialised into the native page pool — and the next access of :attr:`panel` brings it back
+    (H2D copies on the copy stream, ordered before the consumer by a stream wait).  Out-of-core
+    consumers read row ranges with :meth:`load_rows` without making the whole panel resident."""
+
+    SPILL_BASE = 1 << 20        # pool page numbers of spilled slabs (persisted chunks use 0..)
 
     def __init__(self, manager, db, name, type_, set_id, page_size, device=None, persistent=True):
         super().__init__(manager, db, name, type_, set_id, page_size, device, persistent)
-        self.panel: Optional[torch.Tensor] = None     # [local_rows_padded, ld]
+        self._panel: Optional[torch.Tensor] = None    # [local_rows_padded, ld] when resident
+        self._spilled: Optional[list] = None          # [(row0, rows, where, handle, event)] when evicted
+        self._shape = None                            # (rows, ld, dtype, device) of the spilled panel
+        self._charged = 0                             # bytes charged to the device budget
+        self.pins = 0
+        self.last_use = 0
         self.total_rows = 0
         self.total_cols = 0
         self.block_rows = 0
@@ -310,6 +343,194 @@ class DenseMatrixSet(UserSet):
         self.local_rows = 0
         self.transposed = False                       # panel holds the logical matrix transposed
         self.replicated = False                       # every rank holds the full matrix
+        self.stats_io = {"spills": 0, "reloads": 0, "slab_loads": 0}
+
+    # residency -------------------------------------------------------
+    @property
+    def panel(self) -> Optional[torch.Tensor]:
+        if self._panel is None and self._spilled is not None:
+            self.reload()
+        if self._panel is not None:
+            self.manager.touch(self)
+        return self._panel
+
+    @panel.setter
+    def panel(self, t: Optional[torch.Tensor]):
+        self._install(t)
+
+    def _install(self, t: Optional[torch.Tensor]):
+        self._drop_spilled()
+        old = self._charged
+        self._panel = t
+        self._charged = 0
+        if old:
+            self.manager.release_bytes(old, self.manager.home)
+        if t is None or not self.manager.on_home(t.device):
+            self.manager.untrack(self)
+        if t is not None and self.manager.on_home(t.device):
+            self._charged = t.numel() * t.element_size()
+            self.manager.track(self)
+            self.pins += 1
+            try:
+                self.manager.account_bytes(self._charged, self.manager.home, keep=self)
+            finally:
+                self.pins -= 1
+
+    def is_resident(self) -> bool:
+        return self._panel is not None
+
+    def is_spilled(self) -> bool:
+        return self._spilled is not None
+
+    def resident_on_home(self) -> bool:
+        return self._panel is not None and self._charged > 0
+
+    def has_data(self) -> bool:
+        return self._panel is not None or self._spilled is not None
+
+    def panel_nbytes(self) -> int:
+        if self._panel is not None:
+            return self._panel.numel() * self._panel.element_size()
+        if self._shape is not None:
+            r, ld, dt, _ = self._shape
+            return r * ld * torch.empty(0, dtype=dt).element_size()
+        return 0
+
+    def row_bytes(self) -> int:
+        if self._panel is not None:
+            return self._panel.shape[1] * self._panel.element_size()
+        if self._shape is not None:
+            return self._shape[1] * torch.empty(0, dtype=self._shape[2]).element_size()
+        return 0
+
+    def _slab_rows(self, ld: int, esize: int) -> int:
+        per = max(1, self.page_size // max(1, ld * esize))
+        if self.block_rows:
+            per = max(self.block_rows, per // self.block_rows * self.block_rows)
+        return per
+
+    def spill(self) -> int:
+        """Evict the panel in block-row slabs; returns the device bytes freed (0 if pinned/absent)."""
+        t = self._panel
+        if t is None or self.pins > 0:
+            return 0
+        tier = getattr(self.manager, "host_tier", None)
+        rows, ld = t.shape
+        es = t.element_size()
+        step = self._slab_rows(ld, es)
+        slabs = []
+        bm = self.manager.buffer_manager
+        for i, r0 in enumerate(range(0, rows, step)):
+            part = t[r0: r0 + step]
+            nb = part.numel() * es
+            if t.is_cuda and tier is not None and tier.admit(nb):
+                from ..objects.record import RecordBatch
+
+                host, ev = tier.offload(RecordBatch({"x": part}, part.shape[0]), nb)
+                slabs.append((r0, part.shape[0], "pinned", host.columns["x"], ev))
+                continue
+            data = part.contiguous().cpu().view(torch.uint8).numpy().tobytes()
+            if len(data) > bm.page_size:
+                raise RuntimeError(f"dense slab {len(data)} B exceeds the pool page size {bm.page_size}")
+            pno = self.SPILL_BASE + i
+            slot = bm.pin(self.set_id, pno, True)
+            bm.slot_view(slot)[: len(data)] = data
+            bm.unpin(self.set_id, pno, True, len(data))
+            slabs.append((r0, part.shape[0], "pool", pno, None))
+        self._shape = (rows, ld, t.dtype, t.device)
+        self._spilled = slabs
+        freed = self._charged
+        self._charged = 0
+        self._panel = None
+        self.stats_io["spills"] += 1
+        return freed
+
+    def _slab_tensor(self, slab, device) -> torch.Tensor:
+        r0, n, where, h, ev = slab
+        _, ld, dt, _ = self._shape
+        if where == "pinned":
+            tier = self.manager.host_tier
+            if device is not None and torch.device(device).type == "cuda":
+                from ..objects.record import RecordBatch
+
+                return tier.fetch(RecordBatch({"x": h}, n), ev, 0).columns["x"]
+            if ev is not None:
+                ev.synchronize()
+            return h
+        bm = self.manager.buffer_manager
+        slot = bm.pin(self.set_id, h, False)
+        try:
+            nb = bm.bytes_used(self.set_id, h)
+            raw = bytearray(bm.slot_view(slot)[:nb])
+        finally:
+            bm.unpin(self.set_id, h, False, 0)
+        x = torch.frombuffer(raw, dtype=torch.uint8).view(dt).reshape(n, ld)
+        return x.to(device) if device is not None else x
+
+    def reload(self):
+        """Bring a spilled panel back to its device (charged to the budget, may evict others)."""
+        if self._spilled is None:
+            return self._panel
+        rows, ld, dt, dev = self._shape
+        self.pins += 1
+        try:
+            if self.manager.on_home(dev):
+                self.manager.track(self)
+                self.manager.account_bytes(rows * ld * torch.empty(0, dtype=dt).element_size(), self.manager.home,
+                                           keep=self)
+                self._charged = rows * ld * torch.empty(0, dtype=dt).element_size()
+            t = torch.empty(rows, ld, dtype=dt, device=dev)
+            for sl in self._spilled:
+                t[sl[0]: sl[0] + sl[1]].copy_(self._slab_tensor(sl, dev), non_blocking=True)
+        finally:
+            self.pins -= 1
+        self._drop_spilled(keep_charge=True)
+        self._panel = t
+        self.stats_io["reloads"] += 1
+        return t
+
+    def load_rows(self, r0: int, r1: int, device=None) -> torch.Tensor:
+        """Rows [r0, r1) of the panel on ``device`` (a view when resident, else assembled from the spilled
+        slabs without reloading the rest): the out-of-core block GEMM's operand slabs."""
+        if self._panel is not None:
+            v = self._panel[r0:r1]
+            return v if device is None or v.device == torch.device(device) else v.to(device)
+        if self._spilled is None:
+            raise RuntimeError(f"set {self.db}.{self.name} holds no panel")
+        rows, ld, dt, dev = self._shape
+        device = dev if device is None else device
+        out = torch.empty(r1 - r0, ld, dtype=dt, device=device)
+        for sl in self._spilled:
+            a, b = max(r0, sl[0]), min(r1, sl[0] + sl[1])
+            if a < b:
+                out[a - r0: b - r0].copy_(self._slab_tensor(sl, device)[a - sl[0]: b - sl[0]], non_blocking=True)
+        self.stats_io["slab_loads"] += 1
+        return out
+
+    def _drop_spilled(self, keep_charge: bool = False):
+        if self._spilled is None:
+            return
+        tier = getattr(self.manager, "host_tier", None)
+        for r0, n, where, h, ev in self._spilled:
+            if where == "pinned" and tier is not None:
+                tier.release(h.numel() * h.element_size())
+        if any(sl[2] == "pool" for sl in self._spilled):
+            bm = self.manager.buffer_manager
+            if hasattr(bm, "drop_page"):
+                for sl in self._spilled:
+                    if sl[2] == "pool":
+                        bm.drop_page(self.set_id, sl[3])
+        self._spilled = None
+        if not keep_charge:
+            self._shape = None
+
+    def release_storage(self):
+        """Return the panel's device bytes and spilled slabs (set removed or cleared)."""
+        self._drop_spilled()
+        if self._charged:
+            self.manager.release_bytes(self._charged, self.manager.home)
+        self._charged = 0
+        self._panel = None
 
     # geometry -------------------------------------------------------
     def define(self, total_rows: int, total_cols: int, block_rows: int, block_cols: int, row_offset: int = 0,
@@ -323,8 +544,7 @@ class DenseMatrixSet(UserSet):
         dev = device if device is not None else self.device
         alloc = torch.zeros if zero else torch.empty
         self.panel = alloc(self.local_rows, ld, dtype=dtype, device=dev)
-        self.stats = {"records": self.num_blocks(), "bytes": self.panel.numel() * self.panel.element_size()}
-        self.manager.account_bytes(self.stats["bytes"], dev)
+        self.stats = {"records": self.num_blocks(), "bytes": self._panel.numel() * self._panel.element_size()}
         return self
 
     def set_panel(self, panel: torch.Tensor, total_rows: int, total_cols: int, block_rows: int, block_cols: int,
@@ -361,7 +581,7 @@ class DenseMatrixSet(UserSet):
         """Scatter MatrixBlock records into the panel."""
         if batch.n == 0:
             return
-        if self.panel is None:
+        if not self.has_data():
             b0 = batch.columns
             self.define(int(b0["total_rows"][0]), int(b0["total_cols"][0]), int(b0["row_nums"][0]),
                         int(b0["col_nums"][0]), dtype=batch.columns["data"].dtype if isinstance(
@@ -387,7 +607,7 @@ class DenseMatrixSet(UserSet):
             if b.n == 0:
                 continue
             keep = b.columns["block_row"] >= 0
-            if self.panel is not None and self.block_rows:
+            if self.has_data() and self.block_rows:
                 r0 = b.columns["block_row"] * self.block_rows
                 keep &= (r0 >= self.row_offset) & (r0 < self.row_offset + self.local_rows)
             if not bool(keep.all()):
@@ -399,7 +619,7 @@ class DenseMatrixSet(UserSet):
 
     def scan(self, device=None) -> Iterator[RecordBatch]:
         self.resolve_shared()
-        if self.panel is None:
+        if not self.has_data():
             return
         yield self.to_blocks(device)
 
@@ -435,18 +655,18 @@ class DenseMatrixSet(UserSet):
         return RecordBatch(cols, n, t)
 
     def clear(self):
-        self.panel = None
+        self.release_storage()
         self.stats = {"records": 0, "bytes": 0}
 
     def flush(self):
         """Persist the panel (as its MatrixBlock records) through the page pool into the set's page file."""
-        if self.panel is None:
+        if not self.has_data():
             return
         self.persist_pages()
         self.manager.buffer_manager.flush_set(self.set_id)
 
     def persist_pages(self):
-        if self.panel is None:
+        if not self.has_data():
             return
         b = self.to_blocks("cpu")
         bm = self.manager.buffer_manager
@@ -464,8 +684,13 @@ class DenseMatrixSet(UserSet):
     def geometry(self) -> dict:
         return {"total_rows": self.total_rows, "total_cols": self.total_cols, "block_rows": self.block_rows,
                 "block_cols": self.block_cols, "row_offset": self.row_offset, "local_rows": self.local_rows,
-                "replicated": self.replicated, "dtype": str(self.panel.dtype).replace("torch.", "")
-                if self.panel is not None else "bfloat16", "chunks": getattr(self, "flushed_chunks", 0)}
+                "replicated": self.replicated, "dtype": str(self._dtype()).replace("torch.", ""),
+                "chunks": getattr(self, "flushed_chunks", 0)}
+
+    def _dtype(self):
+        if self._panel is not None:
+            return self._panel.dtype
+        return self._shape[2] if self._shape is not None else torch.bfloat16
 
     def restore(self, geo: dict):
         """Rebuild the panel from the chunks written by :meth:`flush` (checkpoint/resume)."""

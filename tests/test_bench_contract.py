@@ -27,7 +27,7 @@ def test_bench_single_process(extra):
     d = _last_json(r.stdout)
     assert KEYS <= set(d) and d["n_gpus"] == 1 and d["steps"] == 2 and d["value"] > 0
     assert d["higher_is_better"] is True and d["scaling"] == "weak" and d["dtype"] == "bf16"
-    assert d["config"]["softmax_rows_sum_to_1"] is True
+    assert d["config"]["check"]["ok"] is True and d["config"]["check"]["ff_max_rel_err"] < 1e-2
 
 
 def test_bench_two_ranks_gloo():
@@ -38,3 +38,4 @@ def test_bench_two_ranks_gloo():
     assert r.returncode == 0, r.stderr[-2000:]
     d = _last_json(r.stdout)
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 * (64 + 4)
+    assert d["config"]["check"]["ok"] is True
