@@ -211,17 +211,20 @@ class PDBClient:
     flushData = flush_data
 
     # ------------------------------------------------------------------ queries
-    def execute_computations(self, *sinks, job_name: str = "job"):
+    def execute_computations(self, *sinks, job_name: str = "job", pre_compile: bool = False):
+        """Run the computation graph ending in ``sinks``. ``pre_compile``: only compile + parse it into the
+        engine's pre-compiled workload cache (PDBClient::executeComputations(preCompile=true)); later
+        executions of a structurally identical graph skip TCAP compilation and parsing."""
         flat: List = []
         for s in sinks:
             if isinstance(s, (list, tuple)):
                 flat.extend(s)
             else:
                 flat.append(s)
-        return self.engine.execute(flat, job_name)
+        return self.engine.execute(flat, job_name, pre_compile=pre_compile)
 
-    def executeComputations(self, *sinks, job_name: str = "job"):
-        return self.execute_computations(*sinks, job_name=job_name)
+    def executeComputations(self, *sinks, job_name: str = "job", pre_compile: bool = False):
+        return self.execute_computations(*sinks, job_name=job_name, pre_compile=pre_compile)
 
     def explain(self, *sinks) -> str:
         from .logical_plan.tcap import compile_tcap

@@ -18,11 +18,11 @@ import torch
 from .. import _ext
 from ..computations import AggregateComp, Computation, TopKComp
 from ..lambdas import Literal, SelfRef
-from ..logical_plan.tcap import compile_tcap
+from ..logical_plan.tcap import bind_atoms, compile_tcap, graph_signature
 from ..objects.record import PDBObject, RecordBatch, RecordView, batch_of, column_concat
 from ..objects.strings import StringColumn
 from ..parallel.comm import ClusterContext
-from ..query_planning.planner import Planner
+from ..query_planning.planner import AdaptivePlanner, PhysicalPlan, Planner
 from ..utils.trace import Tracer
 from . import kernels as K
 
@@ -95,6 +95,10 @@ class QueryEngine:
         self.broadcast_threshold = broadcast_threshold
         self.fusion = fusion
         self.last_plan = None
+        self.adaptive = True              # statistics-driven stage selection (AdaptivePlanner)
+        self.plan_cache_enabled = True
+        self._plan_cache = {}
+        self.cache_stats = {"tcap_compiles": 0, "tcap_cache_hits": 0}
         self.ooc_stats = {}
         self.ooc_fraction = 0.25          # of the device budget: in-memory build / group-by / tuple-set limit
         self._spools = []
@@ -102,11 +106,71 @@ class QueryEngine:
         self._last_comps = None
 
     # ------------------------------------------------------------------ entry
-    def execute(self, sinks: List[Computation], job_name: str = "job") -> JobStats:
+    def _compile(self, sinks, job_name, stats):
+        """TCAP for the graph: from the pre-compiled workload cache when a structurally identical graph
+        ran (or was pre-compiled) before — no TCAP emission, no parse — else compile + native parse."""
+        sig, comps, sets = (None, None, None)
+        if self.plan_cache_enabled:
+            try:
+                sig, comps, sets = graph_signature(sinks)
+            except Exception:          # a graph the signature walk cannot key: always compile
+                sig = None
+        hit = self._plan_cache.get(sig) if sig is not None else None
+        if hit is not None:
+            self.cache_stats["tcap_cache_hits"] += 1
+            stats["tcap_cached"] = True
+            tcap, atoms = hit
+            return bind_atoms(atoms, sets), comps, tcap
+        plan = compile_tcap(sinks)
+        with self.tracer.span("parse_tcap", job=job_name):
+            atoms = _ext.native().parse_tcap(plan.tcap)
+        self.cache_stats["tcap_compiles"] += 1
+        stats["tcap_cached"] = False
+        if sig is not None:
+            self._plan_cache[sig] = (plan.tcap, atoms)
+            while len(self._plan_cache) > 256:
+                self._plan_cache.pop(next(iter(self._plan_cache)))
+        return atoms, plan.computations, plan.tcap
+
+    def _timed_stage(self, st, state, stats, job_name):
+        ts = time.perf_counter()
+        with self.tracer.span(f"stage{st.id}", job=job_name, sink=st.sink.get("kind")):
+            n = self._run_stage(st, state)
+        stats["stages"].append({"id": st.id, "desc": st.describe(), "rows_in": n,
+                                "seconds": time.perf_counter() - ts})
+        return n
+
+    def _run_adaptive(self, atoms, state, stats, job_name):
+        """Stage-at-a-time execution driven by measured statistics (AdaptivePlanner): each finished
+        stage's materialised output is measured (bytes, summed over ranks so every rank takes the same
+        decisions) and costed for the next source selection."""
+        ap = AdaptivePlanner(atoms, self._scan_size, self.ctx.world_size, self.broadcast_threshold)
+        stages = []
+        while ap.has_work():
+            st = ap.next_stage()
+            if st is None:
+                break
+            self._timed_stage(st, state, stats, job_name)
+            stages.append(st)
+            measured = None
+            sk = st.sink.get("kind")
+            if sk in ("materialize", "aggregate", "partition"):
+                out = st.sink["ts"] if sk == "materialize" else st.sink["atom"]["output"]["name"]
+                m = state.materialized.get(out, [])
+                measured = m.bytes if hasattr(m, "bytes") else sum(b.nbytes() for b in m if b is not None)
+                if self.ctx.distributed:
+                    measured = int(self.ctx.all_reduce_scalar(float(measured), "sum"))
+                stats.setdefault("measured_bytes", {})[out] = measured
+            ap.complete(st, measured)
+        if ap.decisions:
+            stats["join_decisions"] = ap.decisions
+        return PhysicalPlan(stages, atoms, {d["join"]: d for d in ap.decisions})
+
+    def execute(self, sinks: List[Computation], job_name: str = "job", pre_compile: bool = False) -> JobStats:
         t0 = time.perf_counter()
         stats = JobStats(job=job_name, stages=[])
         sinks = list(sinks)
-        if self.fusion:
+        if self.fusion and not pre_compile:       # (fusion executes the matched kernels: not on pre-compile)
             from ..query_planning.fusion import fuse_tensor_patterns
 
             ooc0 = dict(self.ooc_stats)
@@ -119,23 +183,24 @@ class QueryEngine:
                 stats["seconds"] = time.perf_counter() - t0
                 self.last_plan = self.last_tcap = self._last_comps = None
                 return stats
-        plan = compile_tcap(sinks)
-        self.last_tcap = plan.tcap
-        self._last_comps = plan.computations
-        with self.tracer.span("parse_tcap", job=job_name):
-            atoms = _ext.native().parse_tcap(plan.tcap)
-        planner = Planner(self._scan_size, self.ctx.world_size, self.broadcast_threshold)
-        pplan = planner.plan(atoms)
-        self.last_plan = pplan
-        state = _JobState(plan.computations)
+        atoms, comps, tcap = self._compile(sinks, job_name, stats)
+        self.last_tcap = tcap
+        self._last_comps = comps
+        if pre_compile:
+            stats["pre_compiled"] = True
+            stats["seconds"] = time.perf_counter() - t0
+            return stats
+        state = _JobState(comps)
         ooc0 = dict(self.ooc_stats)
         try:
-            for st in pplan.stages:
-                ts = time.perf_counter()
-                with self.tracer.span(f"stage{st.id}", job=job_name, sink=st.sink.get("kind")):
-                    n = self._run_stage(st, state)
-                stats["stages"].append({"id": st.id, "desc": st.describe(), "rows_in": n,
-                                        "seconds": time.perf_counter() - ts})
+            if self.adaptive:
+                pplan = self._run_adaptive(atoms, state, stats, job_name)
+            else:
+                planner = Planner(self._scan_size, self.ctx.world_size, self.broadcast_threshold)
+                pplan = planner.plan(atoms)
+                for st in pplan.stages:
+                    self._timed_stage(st, state, stats, job_name)
+            self.last_plan = pplan
         finally:
             for sp in self._spools:        # job-scoped spills (builds, spooled tuple sets) end with the job
                 sp.drop()

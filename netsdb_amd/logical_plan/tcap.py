@@ -255,4 +255,81 @@ def compile_tcap(sinks: Sequence[Computation]) -> CompiledPlan:
     return TCAPCompiler().compile(list(sinks))
 
 
-__all__ = ["TupleSpec", "CompiledPlan", "TCAPCompiler", "compile_tcap", "compile_lambda"]
+def _lam_tokens(lam: Lambda) -> tuple:
+    return tuple((type(n).__name__, n.kind, n.name, getattr(n, "field", None), getattr(n, "method", None),
+                  getattr(n, "op", None), tuple(n.input_indices()) if not n.children else len(n.children))
+                 for n in lam.nodes_postorder())
+
+
+def graph_signature(sinks: Sequence[Computation]) -> Tuple[tuple, Dict[str, Computation], Dict[str, Tuple[str, str]]]:
+    """Structural key of a computation graph + its TCAP name bindings, WITHOUT emitting TCAP.
+
+    Walks the graph in exactly the compiler's order and binds every computation's name and lambda
+    names the same way (so a cached TCAP / parsed atom list can execute against this graph instance):
+    two graphs with the same signature compile to the same TCAP text.  Lambda literal values and native
+    lambda bodies are looked up on the live objects at run time, so they are not part of the key
+    (QuerySchedulerServer's pre-compiled workloads, src/queryPlanning/headers/PreCompiledWorkload.h)."""
+    comps: Dict[str, Computation] = {}
+    names: Dict[int, str] = {}
+    sets: Dict[str, Tuple[str, str]] = {}
+    counter = itertools.count()
+    toks: List[tuple] = []
+
+    def reg(comp, lam, lc):
+        lam.assign_names(lc)
+        for n in lam.nodes_postorder():
+            comp._lambdas[n.name] = n
+        return _lam_tokens(lam)
+
+    def visit(comp) -> str:
+        if id(comp) in names:
+            return names[id(comp)]
+        ins = []
+        for i, c in enumerate(comp.inputs):
+            if c is None:
+                raise ValueError(f"{comp!r}: input {i} not set")
+            ins.append(visit(c))
+            if comp.input_types[i] is None:
+                comp.input_types[i] = c.output_type
+        name = f"{comp.comp_type}_{next(counter)}"
+        names[id(comp)] = name
+        comps[name] = comp
+        comp._tcap_name = name
+        comp._lambdas = {}
+        lc = itertools.count()
+        args = [Arg(i, t) for i, t in enumerate(comp.input_types)]
+        tok: list = [type(comp).__module__ + "." + type(comp).__qualname__, comp.comp_type, tuple(ins)]
+        if isinstance(comp, (ScanSet, WriteSet)):
+            sets[name] = (comp.db, comp.set_name)     # parameters of the workload, not part of its shape
+        elif isinstance(comp, SelectionComp):
+            tok.append(reg(comp, comp.get_selection(args[0]), lc))
+            tok.append(reg(comp, comp.get_projection(args[0]), lc))
+        elif isinstance(comp, JoinComp):
+            tok.append(reg(comp, comp.get_selection(*args), lc))
+            tok.append(reg(comp, comp.get_projection(*args), lc))
+        elif isinstance(comp, (AggregateComp, TopKComp)):
+            tok.append(reg(comp, comp.get_key_projection(args[0]), lc))
+            tok.append(reg(comp, comp.get_value_projection(args[0]), lc))
+        elif isinstance(comp, PartitionComp):
+            tok.append(reg(comp, comp.get_key_projection(args[0]), lc))
+        toks.append(tuple(tok))
+        return name
+
+    for s in sinks:
+        toks.append(("sink", visit(s)))
+    return tuple(toks), comps, sets
+
+
+def bind_atoms(atoms: List[dict], sets: Dict[str, Tuple[str, str]]) -> List[dict]:
+    """A cached (pre-compiled) atom list re-bound to this instance's scanned / written sets."""
+    out = []
+    for a in atoms:
+        if a["type"] in ("SCAN", "OUTPUT") and a.get("comp") in sets:
+            db, st = sets[a["comp"]]
+            if (a.get("db"), a.get("set")) != (db, st):
+                a = dict(a, db=db, set=st)
+        out.append(a)
+    return out
+
+
+__all__ = ["TupleSpec", "CompiledPlan", "TCAPCompiler", "compile_tcap", "compile_lambda", "graph_signature", "bind_atoms"]

@@ -14,7 +14,7 @@ BroadcastJoinBuildHTJobStage and HashPartitionedJoinBuildHTJobStage).
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import Callable, Dict, List
+from typing import Callable, Dict, List, Optional
 
 STREAMING = {"APPLY", "FILTER", "FLATTEN", "HASHLEFT", "HASHRIGHT", "HASHONE"}
 
@@ -184,4 +184,155 @@ class Planner:
         return order
 
 
-__all__ = ["Planner", "PhysicalPlan", "Stage"]
+# ---------------------------------------------------------------------------------------------------
+class AdaptivePlanner:
+    """Statistics-driven, incremental stage planning (reference: TCAPAnalyzer::getBestSource /
+    penalizedSourceSets, TCAPAnalyzer.cc:1233-1300, and QuerySchedulerServer's dynamic planning loop,
+    QuerySchedulerServer.cc:1033-1260, which materialises intermediate sets and re-analyses the
+    remaining TCAP with their measured statistics).
+
+    Stages are emitted one at a time from the sources available now: scans (catalogued set sizes) and
+    tuple sets materialised by finished stages (their MEASURED sizes).  Policy:
+      1. a source whose pipeline completes without building a join (it ends in an aggregation,
+         partition, materialisation or output, probing only built tables) runs first, cheapest first —
+         these stages produce the statistics the join decisions need;
+      2. otherwise the cheapest source runs and builds the first unbuilt join it reaches (the smaller
+         side builds, judged on measured sizes where known);
+      3. a pipeline that has already probed a join and would build another is abandoned and its
+         source penalised (cost x1000), so the huge post-join table is not built (the reference's
+         "met a join sink with probing" rule).
+    """
+
+    PENALTY = 1000.0
+
+    def __init__(self, atoms: List[dict], size_of_scan: Callable[[dict], int], world_size: int = 1,
+                 broadcast_threshold: int = 2 << 30):
+        self.atoms = atoms
+        self.world_size = world_size
+        self.broadcast_threshold = broadcast_threshold
+        self.producer: Dict[str, dict] = {}
+        self.consumers: Dict[str, List[dict]] = {}
+        for a in atoms:
+            self.producer[a["output"]["name"]] = a
+            for key in ("input", "input2"):
+                nm = a[key]["name"]
+                if nm:
+                    lst = self.consumers.setdefault(nm, [])
+                    if not any(x is a for x in lst):
+                        lst.append(a)
+        # pending sources: [ts, first consumer (None = all via consumers map), cost, kind]
+        self.pending: List[list] = []
+        for a in atoms:
+            if a["type"] == "SCAN":
+                self.pending.append([a["output"]["name"], None, float(size_of_scan(a)), "scan", a])
+        self.built: Dict[str, dict] = {}
+        self.penalized: Dict[str, float] = {}
+        self.decisions: List[dict] = []
+        self.next_id = 0
+        self.measured: Dict[str, int] = {}
+
+    def has_work(self) -> bool:
+        return bool(self.pending)
+
+    def _cost(self, entry) -> float:
+        key = f"{entry[0]}|{id(entry[1])}"
+        c = max(1.0, entry[2])
+        return c * self.penalized.get(key, 1.0)
+
+    def next_stage(self) -> Optional[Stage]:
+        if not self.pending:
+            return None
+        order = sorted(self.pending, key=self._cost)
+        # 1. statistics-producing / join-free pipelines first
+        for e in order:
+            st, info = self._walk(e, allow_build=False)
+            if st is not None:
+                return self._take(e, st, info)
+        # 2. cheapest source builds; 3. probe-then-build pipelines are abandoned + penalised
+        for e in order:
+            st, info = self._walk(e, allow_build=True)
+            if st is not None:
+                return self._take(e, st, info)
+            self.penalized[f"{e[0]}|{id(e[1])}"] = self.penalized.get(f"{e[0]}|{id(e[1])}", 1.0) * self.PENALTY
+        e = order[0]                      # everything penalised: build anyway (forced)
+        st, info = self._walk(e, allow_build=True, force=True)
+        return self._take(e, st, info)
+
+    def _take(self, e, st: Stage, info: dict) -> Stage:
+        self.pending.remove(e)
+        st.id = self.next_id
+        self.next_id += 1
+        if info.get("build"):
+            name, side, strat = info["build"]
+            self.built[name] = {"build": side, "strategy": strat}
+            self.decisions.append({"join": name, "build_side": side, "strategy": strat, "source": e[0],
+                                   "cost": e[2], "measured": e[3] == "materialized"})
+        return st
+
+    def _walk(self, e, allow_build: bool, force: bool = False):
+        ts0, first, cost, kind = e[0], e[1], e[2], e[3]
+        src = {"kind": "scan", "atom": e[4], "ts": ts0} if kind == "scan" else {"kind": "materialized", "ts": ts0}
+        st = Stage(0, src)
+        ts, c = ts0, first
+        probed = False
+        info: dict = {}
+        while True:
+            if c is None:
+                cons = self.consumers.get(ts, [])
+                if not cons:
+                    st.sink = {"kind": "discard", "ts": ts}
+                    return st, info
+                if len(cons) > 1:
+                    st.sink = {"kind": "materialize", "ts": ts}
+                    info["then"] = [(ts, cc) for cc in cons]
+                    return st, info
+                c = cons[0]
+            t = c["type"]
+            if t in STREAMING:
+                st.ops.append(c)
+                ts, c = c["output"]["name"], None
+                continue
+            if t == "JOIN":
+                name = c["output"]["name"]
+                side = "left" if c["input"]["name"] == ts else "right"
+                if name in self.built:
+                    js = self.built[name]
+                    st.ops.append(dict(c, _probe_side=side, _strategy=js["strategy"], _build=js["build"]))
+                    probed = True
+                    ts, c = name, None
+                    continue
+                if not allow_build or (probed and not force):
+                    return None, info
+                if self.world_size == 1:
+                    strat = "local"
+                elif cost <= self.broadcast_threshold:
+                    strat = "broadcast"
+                else:
+                    strat = "partitioned"
+                st.sink = {"kind": "join_build", "atom": c, "side": side, "strategy": strat, "ts": ts}
+                info["build"] = (name, side, strat)
+                return st, info
+            if t in ("AGGREGATE", "PARTITION"):
+                st.sink = {"kind": t.lower(), "atom": c, "ts": ts}
+                info["then"] = [(c["output"]["name"], None)]
+                return st, info
+            if t == "OUTPUT":
+                st.sink = {"kind": "output", "atom": c, "ts": ts}
+                return st, info
+            raise ValueError(f"unexpected atom {t}")
+
+    def complete(self, st: Stage, measured_bytes: Optional[int]):
+        """A stage finished: its materialised output becomes a new source, costed by its measured size."""
+        sk = st.sink.get("kind")
+        if sk in ("materialize", "aggregate", "partition"):
+            out = st.sink["ts"] if sk == "materialize" else st.sink["atom"]["output"]["name"]
+            size = int(measured_bytes or 0)
+            self.measured[out] = size
+            if sk == "materialize":
+                for cc in self.consumers.get(out, []):
+                    self.pending.append([out, cc, float(size), "materialized", None])
+            else:
+                self.pending.append([out, None, float(size), "materialized", None])
+
+
+__all__ = ["Planner", "PhysicalPlan", "Stage", "AdaptivePlanner"]

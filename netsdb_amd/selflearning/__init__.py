@@ -336,8 +336,10 @@ class SelfLearningHook:
         eng = client.engine
         orig = eng.execute
 
-        def execute(sinks, job_name="job"):
-            st = orig(sinks, job_name)
+        def execute(sinks, job_name="job", **kw):
+            st = orig(sinks, job_name, **kw)
+            if st.get("pre_compiled"):
+                return st
             if eng.last_tcap is not None and eng.last_plan is not None and eng._last_comps is not None:
                 atoms = eng.last_plan.atoms
                 uses = extract_uses(atoms, eng._last_comps, eng.last_plan)

@@ -1,0 +1,120 @@
+"""Statistics-driven planning and pre-compiled workloads (reference: TCAPAnalyzer::getBestSource with
+penalised sources, TCAPAnalyzer.cc:1233-1300; QuerySchedulerServer dynamic planning / preCompile,
+QuerySchedulerServer.cc:1033-1260; PreCompiledWorkload.h)."""
+import torch
+
+from netsdb_amd.client import PDBClient
+from netsdb_amd.computations import AggregateComp, JoinComp, ScanSet, WriteSet
+from netsdb_amd.lambdas import make_lambda, make_lambda_from_member, make_lambda_from_method
+from netsdb_amd.objects import PDBObject, RecordBatch
+from netsdb_amd.objects.builtin import DepartmentTotal, Employee
+
+
+class Dept(PDBObject):
+    name: str
+    floor: int
+
+
+class TotalFloor(PDBObject):
+    dept: str
+    floor: int
+    total: float
+
+
+class SalaryByDept(AggregateComp):
+    def get_key_projection(self, e):
+        return make_lambda_from_method(e, "getDepartment")
+
+    def get_value_projection(self, e):
+        return make_lambda_from_method(e, "getSalary")
+
+    def make_output(self, keys, values):
+        return RecordBatch.from_objects([DepartmentTotal(k, float(v)) for k, v in zip(keys, values.tolist())],
+                                        DepartmentTotal)
+
+
+class TotalJoinDept(JoinComp):
+    def get_selection(self, t, d):
+        return make_lambda_from_member(t, "department") == make_lambda_from_member(d, "name")
+
+    def get_projection(self, t, d):
+        return make_lambda(t, d, lambda a, b: TotalFloor(a.department, b.floor, a.total))
+
+
+def _client(tmp_path, adaptive=True):
+    c = PDBClient(root=str(tmp_path))
+    c.engine.adaptive = adaptive
+    c.create_database("db")
+    c.create_set("db", "emps", Employee)
+    c.send_data("db", "emps", [Employee(f"e{i}", 20 + i % 40, f"d{i % 8}", 100.0 + i) for i in range(4000)])
+    c.create_set("db", "depts", Dept)
+    c.send_data("db", "depts", [Dept(f"d{i}", i % 13) for i in range(500)])
+    return c
+
+
+def _job(c, out):
+    c.create_set("db", out, TotalFloor)
+    j = TotalJoinDept()
+    j.set_input(0, SalaryByDept().set_input(ScanSet("db", "emps", Employee)))
+    j.set_input(1, ScanSet("db", "depts", Dept))
+    return c.execute_computations(WriteSet("db", out, TotalFloor).set_input(j), job_name="totals-by-floor")
+
+
+def _rows(c, name):
+    return sorted((o.dept, o.floor, round(o.total, 6)) for o in c.get_set_iterator("db", name))
+
+
+def test_stats_driven_plan_builds_the_measured_smaller_side(tmp_path):
+    # static estimate of the aggregation output (input/4 of 4000 employees) > the 500-row dept set, so the
+    # static planner builds on depts; measured, the aggregation has 8 rows and the adaptive plan builds there
+    c_static = _client(tmp_path / "s", adaptive=False)
+    st_s = _job(c_static, "out")
+    (js,) = c_static.engine.last_plan.join_strategy.values()
+    assert js["build"] == "right"
+
+    c = _client(tmp_path / "a", adaptive=True)
+    st = _job(c, "out")
+    (d,) = st["join_decisions"]
+    assert d["build_side"] == "left" and d["measured"] is True       # the aggregation result builds
+    assert list(st["measured_bytes"].values())[0] < c.storage.get_set("db", "depts").nbytes()
+    # the statistics-producing stage (scan emps -> aggregate) ran before any join decision
+    assert st["stages"][0]["desc"].endswith("=> aggregate")
+    exp = sorted((f"d{k}", k % 13, round(sum(100.0 + i for i in range(4000) if i % 8 == k), 6)) for k in range(8))
+    assert _rows(c, "out") == exp == _rows(c_static, "out")
+
+
+def test_repeated_job_skips_tcap_compile_and_parse(tmp_path):
+    c = _client(tmp_path)
+    cs = c.engine.cache_stats
+    st1 = _job(c, "o1")
+    assert st1["tcap_cached"] is False and cs["tcap_compiles"] == 1
+    st2 = _job(c, "o2")                      # new computation objects, same graph shape
+    assert st2["tcap_cached"] is True and cs["tcap_compiles"] == 1 and cs["tcap_cache_hits"] == 1
+    assert _rows(c, "o1") == _rows(c, "o2")
+
+
+def test_pre_compile_then_execute(tmp_path):
+    c = _client(tmp_path)
+    c.create_set("db", "pc", TotalFloor)
+    j = TotalJoinDept()
+    j.set_input(0, SalaryByDept().set_input(ScanSet("db", "emps", Employee)))
+    j.set_input(1, ScanSet("db", "depts", Dept))
+    st = c.execute_computations(WriteSet("db", "pc", TotalFloor).set_input(j), pre_compile=True)
+    assert st["pre_compiled"] and c.get_set("db", "pc").num_records() == 0      # compiled, not run
+    assert c.engine.cache_stats["tcap_compiles"] == 1
+    st2 = _job(c, "o3")
+    assert st2["tcap_cached"] is True and c.engine.cache_stats["tcap_compiles"] == 1
+    assert len(_rows(c, "o3")) == 8
+
+
+def test_penalised_probe_then_build_pipeline(tmp_path):
+    """A pipeline that probed one join and reaches an unbuilt second join is abandoned and penalised:
+    the 3-way chain still runs, each join building on its smaller input."""
+    from netsdb_amd.models import tpch
+
+    t = tpch.generate(0.002, seed=3)
+    c = PDBClient(root=str(tmp_path))
+    tpch.load(c, "tpch", t)
+    got = tpch.QUERIES["q03"](c, "tpch")
+    ref = tpch.reference("q03", t)
+    assert len(got) == len(ref)
