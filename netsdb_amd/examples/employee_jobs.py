@@ -47,3 +47,46 @@ def plan(client, db, src, age):
 
 
 JOBS = {"select_older": select_older, "totals": totals, "plan": plan}
+
+
+# --------------------------------------------------------------------------- a UDF library for remote graphs
+# (computation classes + record types a remote client references BY NAME in a declarative graph, after
+# register_type("netsdb_amd.examples.employee_jobs"); the server imports only allow-listed modules)
+from netsdb_amd.computations import JoinComp  # noqa: E402
+from netsdb_amd.lambdas import make_lambda  # noqa: E402
+from netsdb_amd.objects.record import PDBObject  # noqa: E402
+
+
+class Department(PDBObject):
+    name: str
+    floor: int
+
+
+class EmpFloor(PDBObject):
+    name: str
+    department: str
+    floor: int
+    salary: float
+
+
+class EmpJoinDepartment(JoinComp):
+    """Employee.department == Department.name -> EmpFloor."""
+
+    def get_selection(self, e, d):
+        return make_lambda_from_member(e, "department") == make_lambda_from_member(d, "name")
+
+    def get_projection(self, e, d):
+        return make_lambda(e, d, lambda a, b: EmpFloor(a.name, a.department, b.floor, a.salary))
+
+
+class SalaryByFloor(AggregateComp):
+    def get_key_projection(self, e):
+        return make_lambda_from_member(e, "floor")
+
+    def get_value_projection(self, e):
+        return make_lambda_from_member(e, "salary")
+
+    def make_output(self, keys, values):
+        ks = keys.tolist() if hasattr(keys, "tolist") else list(keys)
+        return RecordBatch.from_objects([DepartmentTotal(f"floor{k}", float(v)) for k, v in zip(ks, values.tolist())],
+                                        DepartmentTotal)

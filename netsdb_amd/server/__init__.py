@@ -14,6 +14,6 @@ Wire format: 4-byte big-endian length + UTF-8 JSON; tensors travel as {"__tensor
 shape, base64]}.  No pickle anywhere.
 """
 from .protocol import recv_msg, send_msg
-from .frontend import PDBFrontend, RemotePDBClient, serve_worker
+from .frontend import PDBFrontend, RemoteComp, RemotePDBClient, UDFRegistry, serve_worker
 
-__all__ = ["PDBFrontend", "RemotePDBClient", "serve_worker", "send_msg", "recv_msg"]
+__all__ = ["PDBFrontend", "RemotePDBClient", "RemoteComp", "UDFRegistry", "serve_worker", "send_msg", "recv_msg"]

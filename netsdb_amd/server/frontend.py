@@ -1,30 +1,116 @@
 """Master front end (rank 0) + SPMD worker loop + remote client.
 
-Security model: the wire protocol never imports code or names arbitrary functions.  The server
-operator registers UDF jobs up front (``PDBFrontend.register_job(name, fn)`` or the
-``--jobs module`` flag of server/main.py, resolved on the server at start-up); remote clients can
-only invoke those jobs by name with JSON arguments, and can only refer to record types that are
-already registered server-side.  The listener binds to 127.0.0.1 unless told otherwise.
+Security model: the wire protocol never ships code.  Remote clients can
+  * invoke jobs the operator registered up front (``PDBFrontend.register_job`` / ``--jobs module``);
+  * ``register_type(module)`` (PDBClient::registerType): the server imports the module ONLY if it lies
+    under one of the operator's allow-listed module prefixes (``--udf-modules``) and registers the
+    record types and computation (UDF) classes it defines;
+  * ``execute_computations(graph)`` (PDBClient::executeComputations): a DECLARATIVE computation graph —
+    nodes naming registered computation classes with JSON constructor arguments, scan/write nodes
+    naming sets — which the server rebuilds and runs through its engine (``pre_compile`` supported).
+The listener binds to 127.0.0.1 unless told otherwise.
 """
 from __future__ import annotations
 
+import importlib
+import inspect
 import socket
 import socketserver
 import threading
 import traceback
-from typing import Any, Callable, Dict, List, Optional
+from typing import Any, Callable, Dict, List, Optional, Sequence
 
 from ..objects.record import PDBObject, lookup_type
 from .protocol import recv_msg, send_msg
 
 
+class UDFRegistry:
+    """Computation classes remote graphs may instantiate, by name (server-side allow-list)."""
+
+    def __init__(self, allowed_modules: Sequence[str] = ()):
+        from ..computations import Computation
+
+        self.base = Computation
+        self.allowed = tuple(allowed_modules)
+        self.classes: Dict[str, type] = {}
+        self.modules: List[str] = []
+
+    def allowed_module(self, mod: str) -> bool:
+        return any(mod == p or mod.startswith(p.rstrip(".") + ".") for p in self.allowed)
+
+    def register_module(self, mod: str) -> dict:
+        """registerType: import an allow-listed module; register its record types and UDF classes."""
+        if not isinstance(mod, str) or not mod.replace("_", "").replace(".", "").isalnum():
+            raise ValueError("module path must be a dotted identifier")
+        if not self.allowed_module(mod):
+            raise PermissionError(f"module '{mod}' is not under an allow-listed UDF module prefix")
+        m = importlib.import_module(mod)
+        types, comps = [], []
+        for name, obj in vars(m).items():
+            if not inspect.isclass(obj) or obj.__module__ != m.__name__:
+                continue
+            if issubclass(obj, PDBObject):
+                types.append(obj.type_name())
+            elif issubclass(obj, self.base):
+                self.classes[name] = obj
+                comps.append(name)
+        if mod not in self.modules:
+            self.modules.append(mod)
+        return {"module": mod, "types": sorted(types), "computations": sorted(comps)}
+
+    def get(self, name: str) -> type:
+        if name not in self.classes:
+            raise KeyError(f"computation class '{name}' is not registered on this server")
+        return self.classes[name]
+
+
+def _json_args(v):
+    if isinstance(v, (str, int, float, bool)) or v is None:
+        return v
+    if isinstance(v, list):
+        return [_json_args(x) for x in v]
+    if isinstance(v, dict) and all(isinstance(k, str) for k in v):
+        return {k: _json_args(x) for k, x in v.items()}
+    raise ValueError("constructor arguments must be JSON values")
+
+
+def build_graph(spec: dict, registry: UDFRegistry):
+    """Rebuild a declarative graph: {"nodes": [{"id", "kind": "scan"|"write"|"comp", ...}], "sinks": [ids]}."""
+    from ..computations import ScanSet, WriteSet
+
+    nodes = spec.get("nodes")
+    if not isinstance(nodes, list) or len(nodes) > 10000:
+        raise ValueError("graph.nodes must be a list")
+    built: Dict[int, Any] = {}
+    for n in nodes:
+        kind, nid = n.get("kind"), n.get("id")
+        if not isinstance(nid, int) or nid in built:
+            raise ValueError("every node needs a unique integer id")
+        if kind in ("scan", "write"):
+            t = lookup_type(n["type"]) if n.get("type") else None
+            c = (ScanSet if kind == "scan" else WriteSet)(str(n["db"]), str(n["set"]), t)
+        elif kind == "comp":
+            cls = registry.get(str(n["class"]))
+            c = cls(*_json_args(n.get("args") or []), **_json_args(n.get("kwargs") or {}))
+        else:
+            raise ValueError(f"unknown node kind {kind!r}")
+        built[nid] = c
+    for n in nodes:
+        for i, src in enumerate(n.get("inputs") or []):
+            if src not in built:
+                raise ValueError(f"node {n['id']}: unknown input {src}")
+            built[n["id"]].set_input(i, built[src])
+    return [built[s] for s in spec.get("sinks", [])]
+
+
 class Dispatcher:
     """Executes one request against a PDBClient (runs on every rank)."""
 
-    def __init__(self, client, jobs: Dict[str, Callable], health=None):
+    def __init__(self, client, jobs: Dict[str, Callable], health=None, registry: Optional[UDFRegistry] = None):
         self.client = client
         self.jobs = jobs
         self.health = health
+        self.registry = registry or UDFRegistry()
 
     def handle(self, req: dict):
         op = req["op"]
@@ -77,6 +163,20 @@ class Dispatcher:
         if op == "explain":
             sinks = self._job(req["job"])(c, **_kwargs(req))
             return c.explain(*(sinks if isinstance(sinks, (list, tuple)) else [sinks]))
+        if op == "register_type":
+            info = self.registry.register_module(req["module"])
+            for tn in info["types"]:
+                t = lookup_type(tn)
+                if t is not None:
+                    c.register_type(t)
+            return info
+        if op == "execute":
+            sinks = build_graph(req["graph"], self.registry)
+            st = c.execute_computations(*sinks, job_name=str(req.get("job_name", "remote-job")),
+                                        pre_compile=bool(req.get("pre_compile", False)))
+            return _jsonable({k: v for k, v in st.items() if k != "stages"} | {"stages": len(st.get("stages", []))})
+        if op == "explain_graph":
+            return c.explain(*build_graph(req["graph"], self.registry))
         raise ValueError(f"unknown request {op}")
 
     def _job(self, name: str) -> Callable:
@@ -116,10 +216,11 @@ class PDBFrontend:
     """Rank-0 socket server. ``serve_forever()`` blocks; ``start()`` runs it in a thread."""
 
     def __init__(self, client, host: str = "127.0.0.1", port: int = 8108, health=None,
-                 jobs: Optional[Dict[str, Callable]] = None):
+                 jobs: Optional[Dict[str, Callable]] = None, udf_modules: Sequence[str] = ()):
         self.client = client
         self.jobs: Dict[str, Callable] = dict(jobs or {})
-        self.dispatcher = Dispatcher(client, self.jobs, health)
+        self.registry = UDFRegistry(udf_modules)
+        self.dispatcher = Dispatcher(client, self.jobs, health, self.registry)
         self.host, self.port = host, port
         self.lock = threading.Lock()
         self._server: Optional[socketserver.ThreadingTCPServer] = None
@@ -178,9 +279,9 @@ class PDBFrontend:
         self.stopped.set()
 
 
-def serve_worker(client, jobs: Optional[Dict[str, Callable]] = None, health=None):
+def serve_worker(client, jobs: Optional[Dict[str, Callable]] = None, health=None, udf_modules: Sequence[str] = ()):
     """Non-zero ranks: execute every broadcast request until shutdown (WorkerMain)."""
-    d = Dispatcher(client, dict(jobs or {}), health)
+    d = Dispatcher(client, dict(jobs or {}), health, UDFRegistry(udf_modules))
     while True:
         req = client.ctx.broadcast_object(None, src=0)
         if req.get("op") == "shutdown":
@@ -247,6 +348,21 @@ class RemotePDBClient:
     def explain(self, job: str, **kwargs):
         return self._call(op="explain", job=job, kwargs=kwargs)
 
+    def register_type(self, module: str) -> dict:
+        """PDBClient::registerType: the server imports an allow-listed UDF module (no code is sent)."""
+        return self._call(op="register_type", module=module)
+
+    registerType = register_type
+
+    def execute_computations(self, *sinks, job_name: str = "remote-job", pre_compile: bool = False) -> dict:
+        """PDBClient::executeComputations on a graph of :class:`RemoteComp` nodes, shipped declaratively."""
+        return self._call(op="execute", graph=RemoteComp.graph(sinks), job_name=job_name, pre_compile=pre_compile)
+
+    executeComputations = execute_computations
+
+    def explain_graph(self, *sinks) -> str:
+        return self._call(op="explain_graph", graph=RemoteComp.graph(sinks))
+
     def shutdown(self):
         try:
             return self._call(op="shutdown")
@@ -257,4 +373,65 @@ class RemotePDBClient:
         self.sock.close()
 
 
-__all__ = ["PDBFrontend", "RemotePDBClient", "serve_worker", "Dispatcher"]
+class RemoteComp:
+    """Client-side node of a declarative computation graph: a server-registered computation class name
+    + JSON constructor arguments, or a scan / write of a named set.
+
+        scan = RemoteComp.scan("db", "emps", "Employee")
+        agg = RemoteComp("SalaryByDept").set_input(RemoteComp("OlderThan", 40).set_input(scan))
+        rc.execute_computations(RemoteComp.write("db", "out", "DepartmentTotal").set_input(agg))
+    """
+
+    def __init__(self, cls_name: str, *args, **kwargs):
+        self.kind = "comp"
+        self.cls_name = cls_name
+        self.args, self.kwargs = list(args), dict(kwargs)
+        self.inputs: Dict[int, "RemoteComp"] = {}
+        self.db = self.set_name = self.type_name = None
+
+    @staticmethod
+    def scan(db: str, set_name: str, type_name: Optional[str] = None) -> "RemoteComp":
+        n = RemoteComp("ScanSet")
+        n.kind, n.db, n.set_name, n.type_name = "scan", db, set_name, type_name
+        return n
+
+    @staticmethod
+    def write(db: str, set_name: str, type_name: Optional[str] = None) -> "RemoteComp":
+        n = RemoteComp("WriteSet")
+        n.kind, n.db, n.set_name, n.type_name = "write", db, set_name, type_name
+        return n
+
+    def set_input(self, *a) -> "RemoteComp":
+        i, comp = (0, a[0]) if len(a) == 1 else a
+        self.inputs[int(i)] = comp
+        return self
+
+    setInput = set_input
+
+    @staticmethod
+    def graph(sinks) -> dict:
+        ids: Dict[int, int] = {}
+        nodes: List[dict] = []
+
+        def visit(n: "RemoteComp") -> int:
+            if id(n) in ids:
+                return ids[id(n)]
+            ins = [visit(n.inputs[i]) for i in sorted(n.inputs)]
+            nid = len(nodes)
+            ids[id(n)] = nid
+            d = {"id": nid, "kind": n.kind, "inputs": ins}
+            if n.kind == "comp":
+                d.update({"class": n.cls_name, "args": n.args, "kwargs": n.kwargs})
+            else:
+                d.update({"db": n.db, "set": n.set_name, "type": n.type_name})
+            nodes.append(d)
+            return nid
+
+        flat = []
+        for s in sinks:
+            flat.extend(s if isinstance(s, (list, tuple)) else [s])
+        return {"nodes": nodes, "sinks": [visit(s) for s in flat]}
+
+
+__all__ = ["PDBFrontend", "RemotePDBClient", "RemoteComp", "UDFRegistry", "build_graph", "serve_worker",
+           "Dispatcher"]

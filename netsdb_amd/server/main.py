@@ -18,6 +18,8 @@ def main(argv=None):
     ap.add_argument("--heartbeat-port", type=int, default=0)
     ap.add_argument("--jobs", action="append", default=[],
                     help="operator-chosen module exposing a JOBS dict {name: fn(client, **kw)} to clients")
+    ap.add_argument("--udf-modules", action="append", default=[],
+                    help="module prefix remote clients may register_type() (UDF classes + record types)")
     a = ap.parse_args(argv)
 
     from ..client import PDBClient
@@ -38,11 +40,11 @@ def main(argv=None):
     if a.heartbeat_port:
         health = HeartbeatMonitor.standalone(a.host, a.heartbeat_port, ctx.rank, ctx.world_size).start()
     if ctx.rank == 0:
-        fe = PDBFrontend(client, a.host, a.port, health, jobs=jobs)
+        fe = PDBFrontend(client, a.host, a.port, health, jobs=jobs, udf_modules=a.udf_modules)
         print(f"[netsdb_amd] master listening on {a.host}:{fe.start().port} (world {ctx.world_size})", flush=True)
         fe.stopped.wait()
     else:
-        serve_worker(client, jobs, health)
+        serve_worker(client, jobs, health, a.udf_modules)
     if health:
         health.stop()
 

@@ -68,3 +68,59 @@ def test_heartbeat_failure_detection():
     except NodeFailure:
         pass
     m0.stop()
+
+
+def test_remote_declarative_graph_select_join_aggregate(tmp_path):
+    """A Selection -> Join -> Aggregate graph built CLIENT-side and shipped declaratively (class names +
+    JSON args), after register_type() of an allow-listed UDF module; no job is pre-registered."""
+    from netsdb_amd.server import RemoteComp as RC
+
+    fe = PDBFrontend(PDBClient(root=str(tmp_path)), port=0, udf_modules=["netsdb_amd.examples"]).start()
+    rc = RemotePDBClient("127.0.0.1", fe.port)
+    try:
+        assert rc.ping()["jobs"] == []
+        info = rc.register_type("netsdb_amd.examples.employee_jobs")
+        assert {"OlderThan", "EmpJoinDepartment", "SalaryByFloor"} <= set(info["computations"])
+        assert "Department" in info["types"]
+        for bad in ("os", "subprocess", "netsdb_amd.examplesX.mod", "netsdb_amd.server.frontend"):
+            try:
+                rc.register_type(bad)
+                raise AssertionError(f"{bad} must be refused")
+            except RuntimeError as e:
+                assert "allow-listed" in str(e) or "No module" in str(e)
+        rc.create_database("db")
+        rc.create_set("db", "emps", "Employee")
+        rc.create_set("db", "depts", "Department")
+        emps = [Employee(f"e{i}", 20 + i, ["eng", "ops", "hr"][i % 3], 100.0 * i) for i in range(40)]
+        rc.send_data("db", "emps", emps)
+        rc.send_data("db", "depts", [{"name": "eng", "floor": 3}, {"name": "ops", "floor": 1}])
+        rc.create_set("db", "by_floor", "DepartmentTotal")
+        old = RC("OlderThan", 30).set_input(RC.scan("db", "emps", "Employee"))
+        j = RC("EmpJoinDepartment").set_input(0, old).set_input(1, RC.scan("db", "depts", "Department"))
+        sink = RC.write("db", "by_floor", "DepartmentTotal").set_input(RC("SalaryByFloor").set_input(j))
+        assert "JOIN" in rc.explain_graph(sink)
+        st = rc.execute_computations(sink, job_name="remote-graph")
+        assert st["stages"] >= 3
+        got = {o.department: o.total for o in rc.get_set("db", "by_floor")}
+        floors = {"eng": 3, "ops": 1}
+        exp = {}
+        for e in emps:
+            if e.age > 30 and e.department in floors:
+                k = f"floor{floors[e.department]}"
+                exp[k] = exp.get(k, 0.0) + e.salary
+        assert got.keys() == exp.keys() and all(abs(got[k] - exp[k]) < 1e-6 for k in exp)
+        try:
+            rc.execute_computations(RC.write("db", "x").set_input(RC("Unregistered").set_input(
+                RC.scan("db", "emps", "Employee"))))
+            raise AssertionError("unregistered class must be refused")
+        except RuntimeError as e:
+            assert "not registered" in str(e)
+        # pre-compile then run the same graph shape again: no TCAP compile the second time
+        rc.create_set("db", "by_floor2", "DepartmentTotal")
+        sink2 = RC.write("db", "by_floor2", "DepartmentTotal").set_input(RC("SalaryByFloor").set_input(
+            RC("EmpJoinDepartment").set_input(0, RC("OlderThan", 30).set_input(RC.scan("db", "emps", "Employee")))
+            .set_input(1, RC.scan("db", "depts", "Department"))))
+        assert rc.execute_computations(sink2)["tcap_cached"] is True
+    finally:
+        rc.shutdown()
+        fe.stopped.wait(5)
