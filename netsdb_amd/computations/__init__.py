@@ -276,6 +276,23 @@ class Elementwise:
 
 
 @dataclass
+class GateSum:
+    """N-way join(equal block keys) projecting act(in_0 + ... + in_{n-1}) (LSTMThreeWaySum)."""
+
+    act: str = "sigmoid"
+
+
+@dataclass
+class CellUpdate:
+    """4-way join projecting f * c_prev + i * g (LSTMTwoSum; inputs f, c_prev, i, g)."""
+
+
+@dataclass
+class HiddenOut:
+    """2-way join projecting o * tanh(c) (LSTMHiddenState; inputs o, c)."""
+
+
+@dataclass
 class Transpose:
     """selection swapping block indices and transposing payloads (LASillyTransposeSelection)."""
 

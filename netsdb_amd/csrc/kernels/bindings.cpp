@@ -23,6 +23,8 @@ int nsdb_softmax_rows(const void* X, int x_f32, const float* bias, void* Y, int 
                       long long ldx, long long ldy, int log_out, hipStream_t st);
 int nsdb_bias_act(const void* X, int x_f32, const float* bias, void* Y, int y_f32, int R, int N, int bias_mode,
                   int act, float dropout, unsigned long long seed, hipStream_t st);
+int nsdb_lstm_ew(int mode, const float* a, const float* b, const float* c, const float* d, float* out, long long n,
+                 hipStream_t st);
 int nsdb_lstm_cell(const void* gates, int g_f32, const float* c_prev, void* h_out, int h_f32, float* c_out, int B,
                    int H, hipStream_t st);
 int nsdb_embedding_bag(const void* table, int t_f32, const long long* idx, const long long* offsets,
@@ -75,11 +77,17 @@ torch::Tensor gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Ten
   if (bias.has_value() && bias->defined()) {
     check_cuda(*bias, "bias");
     TORCH_CHECK(bias->scalar_type() == torch::kFloat32 && bias->is_contiguous(), "bias must be contiguous f32");
-    TORCH_CHECK(bias_mode == 1 || bias_mode == 2, "bias_mode must be 1 (per row) or 2 (per col)");
-    const int64_t blen = bias->size(-1);
-    TORCH_CHECK(blen == (bias_mode == 1 ? M : N), "bias length mismatch");
-    sBias = (bias->dim() == 2) ? blen : 0;
-    TORCH_CHECK(bias->dim() == 1 || bias->size(0) == batch, "bias batch mismatch");
+    TORCH_CHECK(bias_mode >= 1 && bias_mode <= 3, "bias_mode must be 1 (per row), 2 (per col) or 3 (matrix)");
+    if (bias_mode == 3) {   // full [.., M, N] f32 matrix added in the epilogue (LSTM gate biases)
+      TORCH_CHECK(bias->size(-1) == N && bias->size(-2) == M, "bias matrix must be [M, N]");
+      TORCH_CHECK(bias->dim() == 2 || bias->size(0) == batch, "bias batch mismatch");
+      sBias = (bias->dim() == 3) ? M * N : 0;
+    } else {
+      const int64_t blen = bias->size(-1);
+      TORCH_CHECK(blen == (bias_mode == 1 ? M : N), "bias length mismatch");
+      sBias = (bias->dim() == 2) ? blen : 0;
+      TORCH_CHECK(bias->dim() == 1 || bias->size(0) == batch, "bias batch mismatch");
+    }
     bptr = bias->data_ptr<float>();
   }
   auto opts = A.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16);
@@ -235,6 +243,31 @@ std::vector<torch::Tensor> lstm_cell(torch::Tensor gates, c10::optional<torch::T
   return {h, c};
 }
 
+torch::Tensor lstm_ew(int64_t mode, torch::Tensor a, torch::Tensor b, c10::optional<torch::Tensor> c,
+                      c10::optional<torch::Tensor> d) {
+  auto chk = [&](const torch::Tensor& t, const char* n) {
+    check_cuda(t, n);
+    TORCH_CHECK(t.scalar_type() == torch::kFloat32 && t.is_contiguous() && t.numel() == a.numel(),
+                n, " must be contiguous f32 of the same size");
+  };
+  chk(a, "a");
+  chk(b, "b");
+  const float* cp = nullptr;
+  const float* dp = nullptr;
+  if (mode == 0) {
+    TORCH_CHECK(c.has_value() && d.has_value(), "mode 0 needs 4 inputs");
+    chk(*c, "c");
+    chk(*d, "d");
+    cp = c->data_ptr<float>();
+    dp = d->data_ptr<float>();
+  }
+  auto out = torch::empty_like(a);
+  check_rc(nsdb_lstm_ew((int)mode, a.data_ptr<float>(), b.data_ptr<float>(), cp, dp, out.data_ptr<float>(),
+                        (long long)a.numel(), cur_stream()),
+           "lstm_ew");
+  return out;
+}
+
 torch::Tensor embedding_bag(torch::Tensor table, torch::Tensor idx, torch::Tensor offsets,
                             c10::optional<torch::Tensor> weights, int64_t mode) {
   check_cuda(table, "table");
@@ -334,6 +367,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("mode") = 0);
   m.def("bias_act", &bias_act, py::arg("X"), py::arg("bias") = py::none(), py::arg("bias_mode") = 2,
         py::arg("act") = 0, py::arg("dropout") = 0.0, py::arg("seed") = 0, py::arg("out_f32") = false);
+  m.def("lstm_ew", &lstm_ew, py::arg("mode"), py::arg("a"), py::arg("b"), py::arg("c") = py::none(),
+        py::arg("d") = py::none());
   m.def("lstm_cell", &lstm_cell, py::arg("gates"), py::arg("c_prev") = py::none(), py::arg("h_f32") = true);
   m.def("embedding_bag", &embedding_bag, py::arg("table"), py::arg("idx"), py::arg("offsets"),
         py::arg("weights") = py::none(), py::arg("mode") = 0);

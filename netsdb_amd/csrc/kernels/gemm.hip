@@ -149,7 +149,10 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[TBM / WGM / 16
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float x = v4[j] * p.alpha;
-        if (bias) x += p.bias_mode == 1 ? bias[row] : bias[min(col + j, p.N - 1)];
+        if (bias)
+          x += p.bias_mode == 1 ? bias[row]
+             : p.bias_mode == 3 ? bias[(long long)row * p.N + min(col + j, p.N - 1)]   // full f32 [M][N] matrix
+                                : bias[min(col + j, p.N - 1)];
         x = apply_act(x, p.act);
         if (p.dropout > 0.f) {
           const unsigned long long idx = ((unsigned long long)batch * p.M + row) * p.N + col + j;
@@ -492,7 +495,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(GemmParams p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float x = s[j] * p.alpha;
-        if (bias) x += (p.bias_mode == 1) ? bias[row] : bias[col + j];
+        if (bias) x += (p.bias_mode == 1) ? bias[row] : (p.bias_mode == 3) ? bias[e + j] : bias[col + j];
         x = apply_act_compact(x, p.act);
         if (p.dropout > 0.f) {
           const unsigned long long idx = (unsigned long long)batch * MN + e + j;
@@ -525,7 +528,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(GemmParams p) {
     for (int k = 0; k < p.splits; ++k) s += w[k * MN];
     const int row = (int)(e / p.N), col = (int)(e % p.N);
     float v = s * p.alpha;
-    if (bias) v += (p.bias_mode == 1) ? bias[row] : bias[col];
+    if (bias) v += (p.bias_mode == 1) ? bias[row] : (p.bias_mode == 3) ? bias[e] : bias[col];
     v = apply_act_compact(v, p.act);
     if (p.dropout > 0.f) {
       const unsigned long long idx = (unsigned long long)batch * MN + e;

@@ -140,6 +140,28 @@ __global__ void __launch_bounds__(256) lstm_cell_kernel(const TG* gates, const f
   }
 }
 
+// LSTM cell elementwise steps over [n] f32 (row-major matrices of equal shape):
+//   mode 0 (LSTMTwoSum):      out = a * b + c * d      (f * c_prev + i * g)
+//   mode 1 (LSTMHiddenState): out = a * tanh(b)         (o * tanh(c))
+// 16-B loads/stores (4 floats per thread), scalar tail
+__global__ void __launch_bounds__(256) lstm_ew_kernel(int mode, const float* a, const float* b, const float* c,
+                                                      const float* d, float* out, long long n) {
+  const long long n4 = n / 4;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n4; e += (long long)gridDim.x * blockDim.x) {
+    const f32x4 x = reinterpret_cast<const f32x4*>(a)[e], y = reinterpret_cast<const f32x4*>(b)[e];
+    f32x4 r;
+    if (mode == 0) {
+      const f32x4 z = reinterpret_cast<const f32x4*>(c)[e], w = reinterpret_cast<const f32x4*>(d)[e];
+      r = x * y + z * w;
+    } else {
+      r = f32x4{x[0] * tanhf(y[0]), x[1] * tanhf(y[1]), x[2] * tanhf(y[2]), x[3] * tanhf(y[3])};
+    }
+    reinterpret_cast<f32x4*>(out)[e] = r;
+  }
+  for (long long e = n4 * 4 + (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x)
+    out[e] = mode == 0 ? a[e] * b[e] + c[e] * d[e] : a[e] * tanhf(b[e]);
+}
+
 // out[b][:] = reduce_{i in [offsets[b], offsets[b+1])} w_i * table[idx[i]][:]   (mode 0 sum, 1 mean)
 template <typename TT>
 __global__ void __launch_bounds__(256) embedding_bag_kernel(const TT* table, const long long* idx,
@@ -219,6 +241,14 @@ int nsdb_bias_act(const void* X, int x_f32, const float* bias, void* Y, int y_f3
   else if (y_f32) NSDB_BA(unsigned short, float);
   else NSDB_BA(unsigned short, unsigned short);
 #undef NSDB_BA
+  return (int)hipGetLastError();
+}
+
+int nsdb_lstm_ew(int mode, const float* a, const float* b, const float* c, const float* d, float* out, long long n,
+                 hipStream_t st) {
+  const long long n4 = (n + 3) / 4;
+  const int grid = (int)std::min<long long>((n4 + 255) / 256, 4096);
+  hipLaunchKernelGGL(nsdb::lstm_ew_kernel, dim3(grid > 0 ? grid : 1), dim3(256), 0, st, mode, a, b, c, d, out, n);
   return (int)hipGetLastError();
 }
 

@@ -15,7 +15,7 @@ from .. import _ext
 ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_EXP, ACT_TANH = 0, 1, 2, 3, 4
 _ACT_NAMES = {"none": 0, None: 0, "relu": 1, "sigmoid": 2, "exp": 3, "tanh": 4}
 
-BIAS_NONE, BIAS_ROW, BIAS_COL = 0, 1, 2
+BIAS_NONE, BIAS_ROW, BIAS_COL, BIAS_MAT = 0, 1, 2, 3
 
 
 def act_code(act) -> int:
@@ -89,7 +89,7 @@ def gemm_nt(A, B, bias=None, bias_mode=BIAS_NONE, act=ACT_NONE, out_dtype=torch.
     v = torch.matmul(A.float(), B.float().transpose(-1, -2)) * alpha
     if bias is not None:
         b = bias.float()
-        v = v + (b.unsqueeze(-1) if bias_mode == BIAS_ROW else b.unsqueeze(-2))
+        v = v + (b if bias_mode == BIAS_MAT else b.unsqueeze(-1) if bias_mode == BIAS_ROW else b.unsqueeze(-2))
     v = _apply_act(v, act)
     v = _dropout_ref(v, dropout, seed)
     if accumulate:
@@ -209,6 +209,21 @@ def lstm_cell(gates, c_prev=None, h_dtype=torch.float32):
     c = f * (c_prev.float() if c_prev is not None else 0.0) + i * gg
     h = o * torch.tanh(c)
     return h.to(h_dtype), c
+
+
+def lstm_two_sum(f, cp, i, g):
+    """LSTMTwoSum: f * c_prev + i * g (f32, elementwise HIP kernel on the GPU)."""
+    if _use_hip(f):
+        t = [x.float().contiguous() for x in (f, cp, i, g)]
+        return _ext.hip().lstm_ew(0, t[0], t[1], t[2], t[3])
+    return f.float() * cp.float() + i.float() * g.float()
+
+
+def lstm_hidden(o, c):
+    """LSTMHiddenState: o * tanh(c)."""
+    if _use_hip(o):
+        return _ext.hip().lstm_ew(1, o.float().contiguous(), c.float().contiguous())
+    return o.float() * torch.tanh(c.float())
 
 
 def embedding_bag(table, idx, offsets, weights=None, mode="sum"):

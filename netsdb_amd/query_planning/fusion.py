@@ -33,9 +33,9 @@ import torch
 import torch.distributed as dist
 
 from .. import ops
-from ..computations import (AggregateComp, BiasAct, BlockMatmul, BlockSum, Computation, Duplicate, Elementwise,
-                            Inverse, JoinComp, MultiSelectionComp, Reduce, RowSoftmax, ScanSet, SelectionComp,
-                            Transpose, WriteSet)
+from ..computations import (AggregateComp, BiasAct, BlockMatmul, BlockSum, CellUpdate, Computation, Duplicate,
+                            Elementwise, GateSum, HiddenOut, Inverse, JoinComp, MultiSelectionComp, Reduce, RowSoftmax,
+                            ScanSet, SelectionComp, Transpose, WriteSet)
 from ..storage.sets import DenseMatrixSet
 
 _tmp_ids = itertools.count()
@@ -474,6 +474,191 @@ class EwiseNode(Node):
         return self.value
 
 
+# --------------------------------------------------------------------------------------- LSTM (src/LSTM)
+_KCAT: Dict[tuple, torch.Tensor] = {}
+
+
+def _kcat(parts: List[torch.Tensor], cache: bool) -> torch.Tensor:
+    """Concatenate K-contiguous [rows, K_i] operands along K (each K_i padded to 8). Weight panels are
+    concatenated once and reused while none of them is written (keyed by storage + version)."""
+    key = tuple((p.data_ptr(), p._version, tuple(p.shape), tuple(p.stride())) for p in parts) if cache else None
+    if key is not None and key in _KCAT:
+        return _KCAT[key]
+    out = torch.cat([ops.pad_k(p) for p in parts], 1).contiguous()
+    if key is not None:
+        if len(_KCAT) > 64:
+            _KCAT.clear()
+        _KCAT[key] = out
+    return out
+
+
+def _is_plain_matmul(n) -> bool:
+    return isinstance(n, MatmulNode) and n.bias is None and n.act == "none" and not n.transpose_out \
+        and n.value is None
+
+
+def _local(engine, node) -> Dense:
+    v = node.eval(engine)
+    return _replicate(engine, v) if v.part is not None and engine.ctx.distributed else v
+
+
+class GateSumNode(Node):
+    """LSTMThreeWaySum: act(W.x + U.h + B).  The block-matmul inputs become ONE GEMM over the
+    K-concatenation [W | U] . [x ; h] (the sum of the products IS the product of the concatenations),
+    the remaining (dense) inputs are summed into a full-matrix bias added in the GEMM epilogue, and the
+    sigmoid/tanh is applied there too (no separate elementwise passes)."""
+
+    def __init__(self, ins: List[Node], act: str):
+        self.ins, self.act = ins, act
+
+    def parts(self, engine):
+        mms = [n for n in self.ins if _is_plain_matmul(n)]
+        rest = [n for n in self.ins if not _is_plain_matmul(n)]
+        ops_ = []
+        for m in mms:
+            A, B = _local(engine, m.a), _local(engine, m.b)
+            opA = A.t() if m.p.transpose_a else A
+            opB = B.t() if m.p.transpose_b else B
+            ops_.append((opA, opB))
+        return ops_, rest
+
+    def eval(self, engine) -> Dense:
+        if self.value is not None:
+            return self.value
+        ops_, rest = self.parts(engine)
+        bias = None
+        for n in rest:
+            t = _local(engine, n).logical().float()
+            bias = t.clone() if bias is None else bias + t
+        act = ops.act_code(self.act)
+        if ops_:
+            M, N = ops_[0][0].rows, ops_[0][1].cols
+            if any(a.rows != M or b.cols != N or a.cols != b.rows for a, b in ops_):
+                raise ValueError("LSTM gate products of different shapes")
+            X = _kcat([_kslice(a.physical(False), M, a.cols) for a, _ in ops_], cache=True)
+            Y = _kcat([_kslice(b.physical(True), N, b.rows) for _, b in ops_], cache=False)
+            if X.shape[1] != Y.shape[1]:
+                raise ValueError("K mismatch in the gate GEMM")
+            b = bias.contiguous() if bias is not None else None
+            y = ops.gemm_nt(X, Y, b, ops.BIAS_MAT if b is not None else ops.BIAS_NONE, act,
+                            out_dtype=torch.float32)
+        else:
+            y = ops.bias_act(bias.contiguous(), None, ops.BIAS_NONE, act, out_dtype=torch.float32)
+        first = ops_[0][0] if ops_ else _local(engine, rest[0])
+        self.value = Dense.of(y, first.br, (ops_[0][1].bc if ops_ else first.bc))
+        return self.value
+
+
+class CellUpdateNode(Node):
+    """LSTMTwoSum: c = f * c_prev + i * g (one elementwise HIP pass)."""
+
+    def __init__(self, f, cp, i, g):
+        self.f, self.cp, self.i, self.g = f, cp, i, g
+        self.fused_step = None       # set when HiddenOutNode lowered the whole step
+
+    def eval(self, engine) -> Dense:
+        if self.value is None:
+            vs = [_local(engine, n) for n in (self.f, self.cp, self.i, self.g)]
+            t = [v.logical().float().contiguous() for v in vs]
+            y = ops.lstm_two_sum(*t)
+            self.value = Dense.of(y, vs[0].br, vs[0].bc)
+        return self.value
+
+
+class HiddenOutNode(Node):
+    """LSTMHiddenState: h = o * tanh(c).
+
+    When the whole time step is in the graph — h = HiddenState(o, TwoSum(f, c_prev, i, g)) with the four
+    gates ThreeWaySums of W.x + U.h + B over the SAME x and h — it lowers to ONE stacked gate GEMM
+    (all four gates' [W | U] rows, bias matrices in the epilogue, gates laid out [batch, 4H]) followed by
+    the fused ``lstm_cell`` kernel, which also yields c_t for the TwoSum's writer."""
+
+    def __init__(self, o, c):
+        self.o, self.c = o, c
+
+    def _step_pattern(self):
+        c = self.c
+        if not isinstance(c, CellUpdateNode):
+            return None
+        gates = {"i": c.i, "f": c.f, "g": c.g, "o": self.o}
+        want = {"i": "sigmoid", "f": "sigmoid", "g": "tanh", "o": "sigmoid"}
+        for k, n in gates.items():
+            if not isinstance(n, GateSumNode) or n.act != want[k] or n.value is not None:
+                return None
+            mms = [x for x in n.ins if _is_plain_matmul(x)]
+            if len(mms) != 2 or len(n.ins) != 3:
+                return None
+        return gates
+
+    def eval(self, engine) -> Dense:
+        if self.value is not None:
+            return self.value
+        gates = self._step_pattern()
+        if gates is not None:
+            try:
+                self.value = self._fused_step(engine, gates)
+                return self.value
+            except ValueError:
+                pass
+        O, C = _local(engine, self.o), _local(engine, self.c)
+        y = ops.lstm_hidden(O.logical().float().contiguous(), C.logical().float().contiguous())
+        self.value = Dense.of(y, O.br, O.bc)
+        return self.value
+
+    def _fused_step(self, engine, gates) -> Dense:
+        order = ("i", "f", "g", "o")            # lstm_cell's gate layout
+        xs, ys, biases = [], None, []
+        shape = None
+        for k in order:
+            ops_, rest = gates[k].parts(engine)
+            (a0, b0), (a1, b1) = ops_
+            M, N = a0.rows, b0.cols
+            if shape is None:
+                shape = (M, N, a0.br, b0.bc)
+                ys = [b0, b1]
+            elif (M, N) != shape[:2] or b0.src is not ys[0].src or b1.src is not ys[1].src:
+                raise ValueError("gates do not share x / h")
+            if (b0.src is None and b0._phys is not ys[0]._phys) or (b1.src is None and b1._phys is not ys[1]._phys):
+                raise ValueError("gates do not share x / h")
+            xs.append(_kcat([_kslice(a0.physical(False), M, a0.cols), _kslice(a1.physical(False), M, a1.cols)],
+                            cache=True))
+            bm = None
+            for n in rest:
+                t = _local(engine, n).logical().float()
+                bm = t if bm is None else bm + t
+            biases.append(bm)
+        M, N, br, bc = shape
+        W = _kcat_rows(xs)                                   # [4H, D + H]  (cached while weights unchanged)
+        Y = _kcat([_kslice(ys[0].physical(True), N, ys[0].rows), _kslice(ys[1].physical(True), N, ys[1].rows)],
+                  cache=False)                              # [batch, D + H] = [x ; h]^T
+        bias_t = torch.cat([(b if b is not None else torch.zeros(M, N, device=W.device)).t() for b in biases],
+                           1).contiguous()                  # [batch, 4H]
+        g = ops.gemm_nt(Y, W, bias_t, ops.BIAS_MAT, ops.ACT_NONE, out_dtype=torch.float32)   # [batch, 4H]
+        cprev = _local(engine, self.c.cp).logical().float().t().contiguous()               # [batch, H]
+        h, c = ops.lstm_cell(g, cprev)
+        self.c.value = Dense.of(c.t().contiguous(), br, bc)
+        self.c.fused_step = True
+        st = getattr(engine, "ooc_stats", None)
+        if st is not None:
+            st["lstm_fused_steps"] = st.get("lstm_fused_steps", 0) + 1
+        return Dense.of(h.t().contiguous(), br, bc)
+
+
+_ROWCAT: Dict[tuple, torch.Tensor] = {}
+
+
+def _kcat_rows(parts: List[torch.Tensor]) -> torch.Tensor:
+    key = tuple((p.data_ptr(), tuple(p.shape)) for p in parts)
+    hit = _ROWCAT.get(key)
+    if hit is not None and hit[1] == tuple(p._version for p in parts):
+        return hit[0]
+    out = torch.cat(parts, 0).contiguous()
+    if len(_ROWCAT) > 32:
+        _ROWCAT.clear()
+    _ROWCAT[key] = (out, tuple(p._version for p in parts))
+    return out
+
+
 class TransposeNode(Node):
     def __init__(self, x: Node):
         self.x = x
@@ -613,6 +798,26 @@ class Fuser:
                 return None
             self.fused.append(f"softmax[{name}]")
             return SoftmaxNode(x)
+        if isinstance(c, JoinComp) and isinstance(pat, GateSum):
+            ins = [self.match(x) for x in c.inputs]
+            if any(x is None for x in ins):
+                return None
+            self.fused.append(f"gate_gemm[{name}:{sum(_is_plain_matmul(x) for x in ins)}x]")
+            return GateSumNode(ins, pat.act)
+        if isinstance(c, JoinComp) and isinstance(pat, CellUpdate):
+            ins = [self.match(x) for x in c.inputs]
+            if any(x is None for x in ins):
+                return None
+            self.fused.append(f"lstm_two_sum[{name}]")
+            return CellUpdateNode(*ins)
+        if isinstance(c, JoinComp) and isinstance(pat, HiddenOut):
+            ins = [self.match(x) for x in c.inputs]
+            if any(x is None for x in ins):
+                return None
+            node = HiddenOutNode(*ins)
+            self.fused.append("lstm_step[stacked gate GEMM + lstm_cell]" if node._step_pattern() is not None
+                              else f"lstm_hidden[{name}]")
+            return node
         if isinstance(c, JoinComp) and isinstance(pat, Elementwise):
             a, b = self.match(c.inputs[0]), self.match(c.inputs[1])
             if a is None or b is None:
@@ -648,6 +853,9 @@ class Fuser:
     # ------------------------------------------------------------------ rewrite
     def run(self, sinks: List[Computation]) -> List[Computation]:
         remaining: List[Computation] = []
+        # writers of a whole LSTM step (h_t) first: their stacked-gate lowering also produces c_t
+        sinks = sorted(sinks, key=lambda s: 0 if (isinstance(s, WriteSet) and s.inputs and
+                                                  isinstance(self.match(s.inputs[0]), HiddenOutNode)) else 1)
         for s in sinks:
             if isinstance(s, WriteSet):
                 n = self.match(s.inputs[0])
@@ -705,4 +913,5 @@ def fuse_tensor_patterns(sinks: List[Computation], engine) -> Tuple[List[Computa
 
 
 __all__ = ["fuse_tensor_patterns", "Fuser", "MatmulNode", "SoftmaxNode", "BiasActNode", "SourceNode", "Dense",
-           "EwiseNode", "TransposeNode", "ReduceNode", "InverseNode", "DuplicateNode"]
+           "EwiseNode", "TransposeNode", "ReduceNode", "InverseNode", "DuplicateNode", "GateSumNode", "CellUpdateNode",
+           "HiddenOutNode"]
