@@ -11,7 +11,7 @@ void nsdb_gemm_force_config(int cfg);
 int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const float* bias, int M, int N, int K,
                       long long lda, long long ldb, long long ldc, long long sA, long long sB, long long sC,
                       long long sBias, int batch, int splits, int act, int bias_mode, int out_f32, float alpha,
-                      float dropout, unsigned long long seed, int accumulate, hipStream_t stream);
+                      float dropout, unsigned long long seed, int accumulate, long long seg_k, long long seg_stride_b, hipStream_t stream);
 int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* out, int N, int C, int H, int W,
                       int OC, int KH, int KW, int stride, int pad, int dil, int ldw, int act, int nchw_out,
                       int out_f32, hipStream_t stream);
@@ -112,8 +112,57 @@ torch::Tensor gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Ten
       A.data_ptr(), B.data_ptr(), C.data_ptr(), wsp, bptr, (int)M, (int)N, (int)K, A.stride(-2), B.stride(-2),
       C.stride(-2), batched ? A.stride(0) : 0, batched ? B.stride(0) : 0, batched ? C.stride(0) : 0, sBias,
       (int)batch, s, (int)act, (int)bias_mode, out_f32 ? 1 : 0, (float)alpha, (float)dropout,
-      (unsigned long long)seed, accumulate ? 1 : 0, cur_stream());
+      (unsigned long long)seed, accumulate ? 1 : 0, 0, 0, cur_stream());
   check_rc(rc, "gemm_nt");
+  return C;
+}
+
+// C = epilogue(A . Bcat^T) where Bcat [N, S*seg_k] is an all-gathered chunk held as [S][N][seg_k] (rank s's
+// K slab of every row): the kernel reads each K segment in place (split-K, one or more splits per
+// segment), so the gathered buffer needs no permute/reshape copy into a K-contiguous panel.
+torch::Tensor gemm_nt_bseg(torch::Tensor A, torch::Tensor Bg, c10::optional<torch::Tensor> bias, int64_t bias_mode,
+                           int64_t act, bool out_f32, double alpha, double dropout, int64_t seed,
+                           c10::optional<torch::Tensor> out) {
+  check_cuda(A, "A");
+  check_cuda(Bg, "B");
+  TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && Bg.scalar_type() == torch::kBFloat16, "A,B must be bf16");
+  TORCH_CHECK(A.dim() == 2 && A.stride(1) == 1 && A.stride(0) % 8 == 0, "A [M, K] K-contiguous");
+  TORCH_CHECK(Bg.dim() == 3 && Bg.is_contiguous(), "B must be a contiguous [S, N, seg_k] gathered chunk");
+  const int64_t S = Bg.size(0), N = Bg.size(1), segk = Bg.size(2), M = A.size(0), K = S * segk;
+  TORCH_CHECK(segk % 64 == 0, "seg_k must be a multiple of 64");
+  TORCH_CHECK(A.size(1) == K, "A K must equal S*seg_k");
+  const float* bptr = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->scalar_type() == torch::kFloat32 && bias->is_contiguous() && bias->dim() == 1, "bias f32 1-D");
+    TORCH_CHECK(bias->numel() == (bias_mode == 1 ? M : N), "bias length mismatch");
+    bptr = bias->data_ptr<float>();
+  }
+  auto opts = A.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16);
+  torch::Tensor C;
+  if (out.has_value() && out->defined()) {
+    C = *out;
+    TORCH_CHECK(C.scalar_type() == opts.dtype() && C.size(0) == M && C.size(1) == N && C.stride(1) == 1, "out");
+  } else {
+    C = torch::empty({M, N}, opts);
+  }
+  // splits: S segments x d splits per segment (d | seg_k/64), close to the launcher's own choice
+  const int auto_s = std::max<int>(1, nsdb_gemm_splits((int)M, (int)N, (int)K, 1));
+  const int steps = (int)(segk / 64);
+  int d = 1;
+  for (int c = 1; c <= steps; ++c)
+    if (steps % c == 0 && S * c <= std::max<int64_t>(auto_s, S)) d = c;
+  const int s = (int)(S * d);
+  torch::Tensor ws;
+  float* wsp = nullptr;
+  if (s > 1) {
+    ws = torch::empty({(int64_t)s * M * N}, A.options().dtype(torch::kFloat32));
+    wsp = ws.data_ptr<float>();
+  }
+  const int rc = nsdb_gemm_nt_bf16(A.data_ptr(), Bg.data_ptr(), C.data_ptr(), wsp, bptr, (int)M, (int)N, (int)K,
+                                   A.stride(0), segk, C.stride(0), 0, 0, 0, 0, 1, s, (int)act,
+                                   bptr ? (int)bias_mode : 0, out_f32 ? 1 : 0, (float)alpha, (float)dropout,
+                                   (unsigned long long)seed, 0, segk, N * segk, cur_stream());
+  check_rc(rc, "gemm_nt_bseg");
   return C;
 }
 
@@ -138,7 +187,7 @@ torch::Tensor gemm_nt_ktiled(torch::Tensor Ap, torch::Tensor Bp, int64_t M, int6
   }
   const int rc = nsdb_gemm_nt_bf16(Ap.data_ptr(), Bp.data_ptr(), C.data_ptr(), wsp, nullptr, (int)M, (int)N, (int)K,
                                    Ap.size(1), Bp.size(1), N, 0, 0, 0, 0, 1, s, 0, 0, out_f32 ? 1 : 0, 1.f, 0.f, 0, 0,
-                                   cur_stream());
+                                   0, 0, cur_stream());
   nsdb_gemm_force_config(-1);
   check_rc(rc, "gemm_nt_ktiled");
   return C;
@@ -367,6 +416,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("mode") = 0);
   m.def("bias_act", &bias_act, py::arg("X"), py::arg("bias") = py::none(), py::arg("bias_mode") = 2,
         py::arg("act") = 0, py::arg("dropout") = 0.0, py::arg("seed") = 0, py::arg("out_f32") = false);
+  m.def("gemm_nt_bseg", &gemm_nt_bseg, py::arg("A"), py::arg("Bg"), py::arg("bias") = py::none(),
+        py::arg("bias_mode") = 0, py::arg("act") = 0, py::arg("out_f32") = true, py::arg("alpha") = 1.0,
+        py::arg("dropout") = 0.0, py::arg("seed") = 0, py::arg("out") = py::none());
   m.def("lstm_ew", &lstm_ew, py::arg("mode"), py::arg("a"), py::arg("b"), py::arg("c") = py::none(),
         py::arg("d") = py::none());
   m.def("lstm_cell", &lstm_cell, py::arg("gates"), py::arg("c_prev") = py::none(), py::arg("h_f32") = true);

@@ -46,6 +46,10 @@ struct GemmParams {
   int vec_ws;               // N % 4 == 0: 4-column groups of the split-K slabs are 16-B aligned
   int vec_c;                // C rows/base aligned for 4-column vector stores (16 B f32, 8 B bf16)
   int diag;                 // timing diagnostics (wrong results): 1 no epilogue global stores, 2 no operand loads
+  // K-segmented B (an all-gathered [S][N][seg_k] chunk consumed in place, no permute copy): the B rows of
+  // K segment s start at B + s * seg_stride_b (elements) with k taken relative to s * seg_k; every split
+  // lies inside one segment (host forces kchunk | seg_k). seg_k = 0: plain B.
+  long long seg_k, seg_stride_b;
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
@@ -225,13 +229,14 @@ gemm_nt_tile_kernel(GemmParams p) {
 
   const int rows_a = min(TBM, p.M - m0), rows_b = min(TBN, p.N - n0);
   const unsigned short* Ab = p.A + batch * p.sA + (long long)m0 * p.lda;
-  const unsigned short* Bb = p.B + batch * p.sB + (long long)n0 * p.ldb;
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(Ab, (unsigned)((long long)rows_a * p.lda * 2));
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(Bb, (unsigned)((long long)rows_b * p.ldb * 2));
-
   const int kbeg = split * p.kchunk;
   const int kend = min(p.K, kbeg + p.kchunk);
   const int nk = (kend - kbeg + BK - 1) / BK;
+  const long long kseg = p.seg_k ? kbeg / p.seg_k : 0;
+  const int kb0 = (int)(kseg * p.seg_k);      // B's k origin (segmented B)
+  const unsigned short* Bb = p.B + batch * p.sB + (long long)n0 * p.ldb + kseg * p.seg_stride_b;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(Ab, (unsigned)((long long)rows_a * p.lda * 2));
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(Bb, (unsigned)((long long)rows_b * p.ldb * 2));
 
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -241,7 +246,7 @@ gemm_nt_tile_kernel(GemmParams p) {
 
   if (nk > 0 && !(p.diag & 2)) {
     stage_tile<TBM, NW>(ra, smem, p.lda, rows_a, kbeg, kend, wave, lane);
-    stage_tile<TBN, NW>(rb, smem + A_BYTES, p.ldb, rows_b, kbeg, kend, wave, lane);
+    stage_tile<TBN, NW>(rb, smem + A_BYTES, p.ldb, rows_b, kbeg - kb0, kend - kb0, wave, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
@@ -252,7 +257,7 @@ gemm_nt_tile_kernel(GemmParams p) {
       char* nxt = smem + ((t + 1) & 1) * STG;
       const int k1 = kbeg + (t + 1) * BK;
       stage_tile<TBM, NW>(ra, nxt, p.lda, rows_a, k1, kend, wave, lane);
-      stage_tile<TBN, NW>(rb, nxt + A_BYTES, p.ldb, rows_b, k1, kend, wave, lane);
+      stage_tile<TBN, NW>(rb, nxt + A_BYTES, p.ldb, rows_b, k1 - kb0, kend - kb0, wave, lane);
     }
     const char* la = cur;
     const char* lb = cur + A_BYTES;
@@ -344,8 +349,10 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   constexpr bool KT = (V == 9);
   const unsigned short* Ab = KT ? p.A + batch * p.sA + ((long long)(kbeg / BK) * p.lda + m0) * BK
                                 : p.A + batch * p.sA + (long long)m0 * p.lda;
+  const long long kseg = (!KT && p.seg_k) ? kbeg / p.seg_k : 0;
+  const int kb0 = (int)(kseg * p.seg_k);      // B's k origin (segmented B)
   const unsigned short* Bb = KT ? p.B + batch * p.sB + ((long long)(kbeg / BK) * p.ldb + n0) * BK
-                                : p.B + batch * p.sB + (long long)n0 * p.ldb;
+                                : p.B + batch * p.sB + (long long)n0 * p.ldb + kseg * p.seg_stride_b;
   const long long bytes_a = KT ? std::min<long long>(0x7fffffffLL, (long long)nk * p.lda * BK * 2) : (long long)rows_a * p.lda * 2;
   const long long bytes_b = KT ? std::min<long long>(0x7fffffffLL, (long long)nk * p.ldb * BK * 2) : (long long)rows_b * p.ldb * 2;
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(Ab, V == 7 ? 0u : (unsigned)bytes_a);
@@ -376,7 +383,8 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int ro = roff[slot][i];
-      const int voff = (kin && ro >= 0) ? (KT ? u * (slot < 2 ? slab_a : slab_b) + ro + kc * 2 : ro + k * 2) : OOB;
+      const int voff = (kin && ro >= 0) ? (KT ? u * (slot < 2 ? slab_a : slab_b) + ro + kc * 2
+                                              : ro + (slot < 2 ? k : k - kb0) * 2) : OOB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(slot < 2 ? ra : rb, (lds_void*)(dst + (i * 64 + wave * 8) * 128), 16,
                                                voff, 0, 0, 0);
     }
@@ -591,7 +599,8 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
                       int M, int N, int K, long long lda, long long ldb, long long ldc,
                       long long sA, long long sB, long long sC, long long sBias, int batch,
                       int splits, int act, int bias_mode, int out_f32, float alpha, float dropout,
-                      unsigned long long seed, int accumulate, hipStream_t stream) {
+                      unsigned long long seed, int accumulate, long long seg_k, long long seg_stride_b,
+                      hipStream_t stream) {
   if (M <= 0 || N <= 0 || batch <= 0) return 0;
   if (K % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0) return -1;        // 16-B rows for the LDS-DMA
   if (256LL * lda * 2 >= 0x7ffffff0LL || 256LL * ldb * 2 >= 0x7ffffff0LL)
@@ -611,6 +620,9 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
   p.act = act; p.bias_mode = bias ? bias_mode : 0; p.out_f32 = out_f32; p.accumulate = accumulate;
   p.alpha = alpha; p.dropout = dropout; p.seed = seed;
   p.diag = g_diag;
+  p.seg_k = seg_k;
+  p.seg_stride_b = seg_stride_b;
+  if (seg_k > 0 && (seg_k % p.kchunk != 0 || seg_k % nsdb::BK != 0)) return -5;   // a split must not cross a segment
   const int cfg = pick_cfg(M, N, K, batch);
   const int tbm = cfg ? 256 : nsdb::BM, tbn = cfg ? 256 : nsdb::BN;
   p.tiles_m = (M + tbm - 1) / tbm;

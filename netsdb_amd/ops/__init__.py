@@ -102,6 +102,22 @@ def gemm_nt(A, B, bias=None, bias_mode=BIAS_NONE, act=ACT_NONE, out_dtype=torch.
     return v
 
 
+def gemm_nt_segmented(A, Bg, bias=None, bias_mode=BIAS_NONE, act=ACT_NONE, out_dtype=torch.bfloat16, dropout=0.0,
+                      seed=0, out=None):
+    """epilogue(A . Bcat^T) with Bcat [N, S*seg_k] held as an all-gathered [S, N, seg_k] chunk (rank s's K slab
+    of every row): the GPU kernel walks the K segments in place (no permute copy); seg_k % 64 == 0."""
+    act = act_code(act)
+    if _use_hip(A, Bg):
+        if bias is not None and bias.dtype != torch.float32:
+            bias = bias.float()
+        return _ext.hip().gemm_nt_bseg(A.to(torch.bfloat16), Bg.to(torch.bfloat16).contiguous(), bias,
+                                       int(bias_mode if bias is not None else 0), act, out_dtype == torch.float32,
+                                       1.0, float(dropout), int(seed), out)
+    S, N, sk = Bg.shape
+    Bcat = Bg.permute(1, 0, 2).reshape(N, S * sk)     # the CPU oracle may copy
+    return gemm_nt(A, Bcat, bias, bias_mode, act, out_dtype, dropout=dropout, seed=seed, out=out)
+
+
 def gemm_splits(M, N, K, batch=1) -> int:
     return int(_ext.hip().gemm_splits(M, N, K, batch))
 

@@ -17,6 +17,7 @@ from __future__ import annotations
 import base64
 import json
 import os
+import time
 from typing import Any, Dict, List, Optional, Sequence
 
 import torch
@@ -41,6 +42,11 @@ class ClusterContext:
         # data backend is RCCL: a RCCL scalar all-reduce + .item() would block the host on the GPU stream
         # and stall kernel enqueueing mid-step
         self.meta_group = None
+        # failure detection (utils/health.HeartbeatMonitor): every collective is issued async and waited
+        # for under a watchdog that raises NodeFailure when a peer stops heartbeating, instead of hanging
+        self.health = None
+        self._schema_cache: Dict[int, dict] = {}
+        self.stats = {"collectives": 0, "schema_cache_hits": 0, "schema_exchanges": 0}
 
     @property
     def distributed(self) -> bool:
@@ -77,20 +83,54 @@ class ClusterContext:
                 self.meta_group = None
         return self
 
+    # -------------------------------------------------------------- failure-aware collective issue
+    def attach_health(self, monitor):
+        """Guard every collective with a heartbeat monitor (a dead rank raises NodeFailure, no hang)."""
+        self.health = monitor
+        return self
+
+    def _wait(self, work):
+        if work is None:
+            return
+        if self.health is None:
+            work.wait()
+            return
+        while not work.is_completed():
+            self.health.check()
+            time.sleep(0.001)
+        try:
+            work.wait()
+        except RuntimeError as e:
+            # a transport error (peer socket reset, RCCL abort): report it as the node failure it is once
+            # the heartbeats confirm which rank stopped
+            deadline = time.time() + 2.5 * getattr(self.health, "timeout", 1.0)
+            while time.time() < deadline:
+                self.health.check()
+                time.sleep(0.01)
+            raise
+
+    def _coll(self, fn, *args, **kw):
+        """Issue a torch.distributed collective asynchronously and wait under the heartbeat watchdog."""
+        self.stats["collectives"] += 1
+        if self.health is not None:
+            self.health.check()
+            self.health.mark_progress()
+        self._wait(fn(*args, async_op=True, **kw))
+
     # -------------------------------------------------------------- primitives
     def barrier(self):
         if self.distributed:
             if self.device.type == "cuda":
-                dist.barrier(device_ids=[self.device.index])
+                self._coll(dist.barrier, device_ids=[self.device.index])
             else:
-                dist.barrier()
+                self._coll(dist.barrier)
 
     def _comm_device(self):
         return self.device if self.backend == "nccl" else torch.device("cpu")
 
     def all_reduce(self, t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
         if self.distributed:
-            dist.all_reduce(t, op=op)
+            self._coll(dist.all_reduce, t, op=op)
         return t
 
     def all_reduce_scalar(self, v: float, op="sum") -> float:
@@ -99,27 +139,37 @@ class ClusterContext:
         rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
         if self.meta_group is not None:
             t = torch.tensor([float(v)], dtype=torch.float64)
-            dist.all_reduce(t, op=rop, group=self.meta_group)
+            self._coll(dist.all_reduce, t, op=rop, group=self.meta_group)
             return float(t.item())
         t = torch.tensor([float(v)], dtype=torch.float64, device=self._comm_device())
-        dist.all_reduce(t, op=rop)
+        self._coll(dist.all_reduce, t, op=rop)
         return float(t.item())
 
-    def all_gather_tensor(self, t: torch.Tensor) -> List[torch.Tensor]:
-        """Variable-first-dim all_gather (rows)."""
+    def all_gather_ints(self, vals: Sequence[int]) -> List[List[int]]:
+        """Small host-side integer metadata from every rank (sizes, ranges, schema hashes): over the gloo
+        metadata group next to RCCL, so no device tensor and no host sync on the GPU stream."""
+        if not self.distributed:
+            return [list(vals)]
+        on_meta = self.meta_group is not None
+        dev = torch.device("cpu") if on_meta else self._comm_device()
+        t = torch.tensor(list(vals), dtype=torch.int64, device=dev)
+        outs = [torch.empty_like(t) for _ in range(self.world_size)]
+        self._coll(dist.all_gather, outs, t, group=self.meta_group) if on_meta else self._coll(dist.all_gather, outs, t)
+        return [o.cpu().tolist() for o in outs]
+
+    def all_gather_tensor(self, t: torch.Tensor, sizes: Optional[Sequence[int]] = None) -> List[torch.Tensor]:
+        """Variable-first-dim all_gather (rows). ``sizes`` (rows per rank) skips the size exchange when the
+        caller knows them (cached plan metadata)."""
         if not self.distributed:
             return [t]
         cd = self._comm_device()
-        n = torch.tensor([t.shape[0]], dtype=torch.int64, device=cd)
-        ns = [torch.zeros_like(n) for _ in range(self.world_size)]
-        dist.all_gather(ns, n)
-        ns = [int(x.item()) for x in ns]
+        ns = list(sizes) if sizes is not None else [x[0] for x in self.all_gather_ints([t.shape[0]])]
         mx = max(ns)
         src = t.to(cd)
         if src.shape[0] < mx:
             src = torch.cat([src, src.new_zeros((mx - src.shape[0],) + tuple(src.shape[1:]))])
         outs = [torch.empty_like(src) for _ in range(self.world_size)]
-        dist.all_gather(outs, src.contiguous())
+        self._coll(dist.all_gather, outs, src.contiguous())
         return [o[:k].to(t.device) for o, k in zip(outs, ns)]
 
     def all_to_all_rows(self, t: torch.Tensor, send_counts: Sequence[int]) -> (torch.Tensor, List[int]):
@@ -127,17 +177,14 @@ class ClusterContext:
         if not self.distributed:
             return t, list(send_counts)
         cd = self._comm_device()
-        sc = torch.tensor(list(send_counts), dtype=torch.int64, device=cd)
-        rc = torch.empty_like(sc)
-        dist.all_to_all_single(rc, sc)
-        recv = [int(x) for x in rc.tolist()]
+        recv = [row[self.rank] for row in self.all_gather_ints(list(send_counts))]   # host metadata, no sync
         src = t.to(cd).contiguous()
         out = src.new_empty((sum(recv),) + tuple(src.shape[1:]))
         if src.dtype == torch.bool:
             s8, o8 = src.view(torch.uint8), out.view(torch.uint8)
-            dist.all_to_all_single(o8, s8, recv, list(send_counts))
+            self._coll(dist.all_to_all_single, o8, s8, recv, list(send_counts))
         else:
-            dist.all_to_all_single(out, src, recv, list(send_counts))
+            self._coll(dist.all_to_all_single, out, src, recv, list(send_counts))
         return out.to(t.device), recv
 
     def reduce_scatter_rows(self, t: torch.Tensor, counts: Sequence[int]) -> torch.Tensor:
@@ -147,16 +194,18 @@ class ClusterContext:
         cd = self._comm_device()
         if self.backend == "nccl" and len(set(counts)) == 1:
             out = t.new_empty((counts[self.rank],) + tuple(t.shape[1:]))
-            dist.reduce_scatter_tensor(out, t.contiguous(), op=dist.ReduceOp.SUM)
+            self._coll(dist.reduce_scatter_tensor, out, t.contiguous(), op=dist.ReduceOp.SUM)
             return out
         full = t.to(cd).contiguous().clone()
-        dist.all_reduce(full)
+        self._coll(dist.all_reduce, full)
         s = sum(counts[: self.rank])
         return full[s: s + counts[self.rank]].to(t.device)
 
     def broadcast_object(self, obj: Any, src: int = 0) -> Any:
         if not self.distributed:
             return obj
+        if self.health is not None:
+            self.health.check()
         box = [obj]
         if self.meta_group is not None:
             dist.broadcast_object_list(box, src=src, group=self.meta_group)
@@ -181,9 +230,7 @@ class ClusterContext:
         ws = self.world_size
         ref = template or next((p for p in parts if p is not None), None)
         meta = _batch_meta(ref)
-        metas = [None] * ws
-        dist.all_gather_object(metas, meta, group=self.meta_group)
-        ref_meta = next((m for m in metas if m is not None), None)
+        ref_meta = self._agree_schema(meta)
         if ref_meta is None:
             return []
         parts = [p if p is not None else _empty_like_meta(ref_meta, self.device) for p in parts]
@@ -213,11 +260,7 @@ class ClusterContext:
                     off += k
                 recv_cols[name] = vals
         if recv_counts is None:
-            cd = self._comm_device()
-            sc = torch.tensor(counts, dtype=torch.int64, device=cd)
-            rc = torch.empty_like(sc)
-            dist.all_to_all_single(rc, sc)
-            recv_counts = [int(x) for x in rc.tolist()]
+            recv_counts = [row[self.rank] for row in self.all_gather_ints(counts)]
         t = lookup_type(ref_meta["type"]) if ref_meta["type"] else None
         out_batches = []
         off = 0
@@ -235,6 +278,44 @@ class ClusterContext:
             off += k
         return out_batches
 
+    def _agree_schema(self, meta: Optional[dict]) -> Optional[dict]:
+        """Every rank learns the batch schema of the shuffle (ranks with no rows send none): a 63-bit hash
+        per rank over the metadata group; the JSON schema itself travels (as a byte tensor, never pickled)
+        only the first time a schema hash is seen, after that it comes from the cache."""
+        import xxhash
+
+        blob = json.dumps(meta, sort_keys=True).encode() if meta is not None else b""
+        h = (xxhash.xxh64_intdigest(blob) >> 1) if meta is not None else -1
+        if meta is not None:
+            self._schema_cache.setdefault(h, meta)
+        hs = [x[0] for x in self.all_gather_ints([h])]
+        known = [x for x in hs if x >= 0]
+        if not known:
+            return None
+        # the exchange decision must be identical on every rank: agree on "anyone missing a schema"
+        missing = int(not all(x in self._schema_cache for x in known))
+        if not any(x[0] for x in self.all_gather_ints([missing])):
+            self.stats["schema_cache_hits"] += 1
+            return self._schema_cache[known[0]]
+        self.stats["schema_exchanges"] += 1
+        lens = [x[0] for x in self.all_gather_ints([len(blob)])]
+        mx = max(lens)
+        buf = torch.zeros(mx, dtype=torch.uint8)
+        if blob:
+            buf[: len(blob)] = torch.frombuffer(bytearray(blob), dtype=torch.uint8)
+        on_meta = self.meta_group is not None
+        dev = torch.device("cpu") if on_meta else self._comm_device()
+        buf = buf.to(dev)
+        outs = [torch.empty_like(buf) for _ in range(self.world_size)]
+        self._coll(dist.all_gather, outs, buf, group=self.meta_group) if on_meta else self._coll(dist.all_gather, outs, buf)
+        got = None
+        for o, n, hh in zip(outs, lens, hs):
+            if hh >= 0 and n:
+                m = json.loads(o[:n].cpu().numpy().tobytes().decode())
+                self._schema_cache.setdefault(hh, m)
+                got = got or m
+        return got
+
     def _exchange_strings(self, cols, counts):
         """Device string columns on the wire: row lengths + packed bytes, two all-to-alls, no host
         decode. Returns (one StringColumn per source rank, received row counts)."""
@@ -243,7 +324,7 @@ class ClusterContext:
         cols = [c.to(dev) for c in cols]
         lens = torch.cat([c.offsets[1:] - c.offsets[:-1] for c in cols])
         rlens, rcounts = self.all_to_all_rows(lens, counts)
-        bounds = torch.stack([torch.stack([c.offsets[0], c.offsets[-1]]) for c in cols]).cpu().tolist()
+        bounds = torch.stack([torch.stack([c.offsets[0], c.offsets[-1]]) for c in cols]).cpu().tolist()   # one host read
         data = torch.cat([c.data[s:e] for c, (s, e) in zip(cols, bounds)])
         rdata, rbytes = self.all_to_all_rows(data, [e - s for s, e in bounds])
         out, ro, rb = [], 0, 0

@@ -294,28 +294,35 @@ class MatmulNode(Node):
         B^T is all-gathered in N-chunks over RCCL (one collective per chunk uses every xGMI link of
         the node, unlike a neighbour ring that is bound by one link) on the communication stream while
         the previous chunk's full-K MFMA GEMM runs: C_r[:, n0:n1] = epi(A_r . B[:, n0:n1]) written in
-        place, so there is no f32 partial and no accumulation pass.  Chunks of rank slabs
-        [ws, nc, k_s] are laid side by side along K, matching A's columns (A is re-laid out once only
-        when the K partition is uneven)."""
+        place.  The gathered chunk [ws, nc, kseg] is consumed IN PLACE by the K-segmented GEMM (each
+        rank's K slab is one segment; no permute/reshape copy), and A's columns are laid out once as
+        the matching [M, ws * kseg] panel (cached).  The ranks' K ranges are plan metadata: gathered
+        once per (set, geometry) over the host metadata group and cached — no per-call collective and
+        no device->host sync."""
         ctx = engine.ctx
         ws = ctx.world_size
         cd = ctx._comm_device()
-        kr = torch.tensor([[opB.offset, opB.rows]], dtype=torch.int64, device=cd)
-        ranges = [(int(x[0, 0]), int(x[0, 1])) for x in ctx.all_gather_tensor(kr)]
-        kmax8 = (max(k for _, k in ranges) + 7) // 8 * 8
+        key = ("kranges", id(opB.src) if opB.src is not None else None, opB.offset, opB.rows, ws)
+        cache = engine.__dict__.setdefault("meta_cache", {})
+        ranges = cache.get(key) if opB.src is not None else None
+        if ranges is None:
+            ranges = [tuple(r) for r in ctx.all_gather_ints([opB.offset, opB.rows])]
+            if opB.src is not None:
+                cache[key] = ranges
+        kseg = max(64, (max(k for _, k in ranges) + 63) // 64 * 64)
         A_full = opA.physical(False)                         # [M, >= K_total]: local rows, all K
         dev = A_full.device
-        uniform = all(off == s * kmax8 and k == kmax8 for s, (off, k) in enumerate(ranges)) and \
-            A_full.shape[1] >= ws * kmax8
-        if uniform:
-            A_use = A_full[:M, : ws * kmax8]
-        else:
-            A_use = torch.zeros(M, ws * kmax8, dtype=A_full.dtype, device=dev)
+
+        def lay_out(a):
+            out = torch.zeros(M, ws * kseg, dtype=a.dtype, device=a.device)
             for s_, (off, k) in enumerate(ranges):
-                A_use[:, s_ * kmax8: s_ * kmax8 + k] = A_full[:M, off: off + k]
+                out[:, s_ * kseg: s_ * kseg + k] = a[:M, off: off + k]
+            return out
+
+        A_use = ops.derived(A_full, f"kseg_layout:{kseg}:{ranges}", lay_out)
         Bt = opB.physical(True)[:N, : opB.rows]               # [N, K_r] K-contiguous
-        if Bt.shape[1] != kmax8 or not Bt.is_contiguous():
-            Bt = torch.nn.functional.pad(Bt, (0, kmax8 - Bt.shape[1])).contiguous()
+        if Bt.shape[1] != kseg or not Bt.is_contiguous():
+            Bt = torch.nn.functional.pad(Bt, (0, kseg - Bt.shape[1])).contiguous()
         # chunk N: ~8 chunks of >= 1024 columns (multiples of 256 = whole GEMM tiles)
         nchunks = max(1, min(8, N // 1024))
         step = (N + nchunks - 1) // nchunks
@@ -327,8 +334,11 @@ class MatmulNode(Node):
         def start(c):
             n0, n1 = bounds[c]
             src = Bt[n0:n1].to(cd).contiguous()
+            if ctx.health is not None:
+                ctx.health.check()
+            ctx.stats["collectives"] += 1
             if nccl:
-                dst = torch.empty(ws * (n1 - n0), kmax8, dtype=src.dtype, device=cd)
+                dst = torch.empty(ws, n1 - n0, kseg, dtype=src.dtype, device=cd)
                 return dst, dist.all_gather_into_tensor(dst, src, async_op=True)
             parts = [torch.empty_like(src) for _ in range(ws)]
             return parts, dist.all_gather(parts, src, async_op=True)
@@ -338,31 +348,41 @@ class MatmulNode(Node):
             got, work = pending
             if c + 1 < len(bounds):
                 pending = start(c + 1)        # next chunk's collective overlaps this chunk's GEMM
-            work.wait()
-            nc = n1 - n0
-            g = got.view(ws, nc, kmax8) if nccl else torch.stack(got)
-            Y = g.permute(1, 0, 2).reshape(nc, ws * kmax8).to(dev)
+            ctx._wait(work)
+            g = got if nccl else torch.stack(got)             # [ws, nc, kseg]: rank s's K slab of each row
+            g = g.to(dev)
             b = None
             if bias_t is not None:
                 b = bias_t[n0:n1] if (mode == ops.BIAS_COL) == phys_is_c else bias_t
             seed = self.seed + c * 0x9E3779B1
             if phys_is_c:
-                ops.gemm_nt(A_use, Y, b, mode, act, out_dtype=odt, dropout=self.dropout, seed=seed, out=out[:, n0:n1])
+                ops.gemm_nt_segmented(A_use, g, b, mode, act, out_dtype=odt, dropout=self.dropout, seed=seed,
+                                      out=out[:, n0:n1])
             else:
-                ops.gemm_nt(Y, A_use, b, mode, act, out_dtype=odt, dropout=self.dropout, seed=seed, out=out[n0:n1])
+                # C^T chunk = (A . Bchunk^T)^T: the segmented operand must be B, so transpose the small result
+                mode_t = {ops.BIAS_ROW: ops.BIAS_COL, ops.BIAS_COL: ops.BIAS_ROW}.get(mode, mode)
+                r = ops.gemm_nt_segmented(A_use, g, b, mode_t, act, out_dtype=odt, dropout=self.dropout, seed=seed)
+                out[n0:n1].copy_(r.t())
         return out
 
     def _kpartial(self, engine, opA: Dense, opB: Dense, M, N, phys_is_c, bias_t, act, odt) -> Dense:
         """K-split product: each rank multiplies the K range it holds (A's column slab and/or B's row
         slab, slicing the replicated operand to that range) into an f32 partial of the whole output,
         then reduce-scatter sums the partials and leaves each rank its block-row range of C (C^T when
-        the consumer wants the transposed layout) — then the epilogue runs on the local slice."""
+        the consumer wants the transposed layout) — then the epilogue runs on the local slice.  The
+        K-range agreement is cached plan metadata; for RCCL's equal-slice reduce-scatter the GEMM writes
+        straight into the padded send buffer (no zero-pad copy of the partial)."""
         ctx = engine.ctx
         ws, r = ctx.world_size, ctx.rank
-        cd = ctx._comm_device()
         if opA.part == "cols" and opB.part == "rows":
-            ka = torch.tensor([[opA.offset, opA.cols, opB.offset, opB.rows]], dtype=torch.int64, device=cd)
-            same = all(int(x[0, 0]) == int(x[0, 2]) and int(x[0, 1]) == int(x[0, 3]) for x in ctx.all_gather_tensor(ka))
+            cache = engine.__dict__.setdefault("meta_cache", {})
+            key = ("kpart", id(opA.src), id(opB.src), opA.offset, opA.cols, opB.offset, opB.rows, ws)
+            same = cache.get(key) if (opA.src is not None and opB.src is not None) else None
+            if same is None:
+                rows = ctx.all_gather_ints([opA.offset, opA.cols, opB.offset, opB.rows])
+                same = all(x[0] == x[2] and x[1] == x[3] for x in rows)
+                if opA.src is not None and opB.src is not None:
+                    cache[key] = same
             if not same:
                 opA = _replicate(engine, opA)
         if opA.part == "cols":
@@ -379,20 +399,21 @@ class MatmulNode(Node):
         if kn8 != kn or a0 % 8 or b0 % 8:
             X = torch.nn.functional.pad(X, (0, kn8 - kn)).contiguous()
             Y = torch.nn.functional.pad(Y, (0, kn8 - kn)).contiguous()
-        P = ops.gemm_nt(X, Y, out_dtype=torch.float32) if phys_is_c else ops.gemm_nt(Y, X, out_dtype=torch.float32)
-        R = P.shape[0]
+        R, Ccols = (M, N) if phys_is_c else (N, M)
         blk = max(1, opA.br if phys_is_c else opB.bc)
         nb = (R + blk - 1) // blk
         per = (nb + ws - 1) // ws
         counts = [max(0, min(R, (s + 1) * per * blk) - min(R, s * per * blk)) for s in range(ws)]
         off = min(R, r * per * blk)
         if ctx.backend == "nccl" and len(set(counts)) > 1:
-            # RCCL reduce_scatter wants equal slices: pad the partial to ws equal slices
             eq = per * blk
-            Pp = torch.zeros(eq * ws, P.shape[1], dtype=P.dtype, device=P.device)
-            Pp[:R] = P
+            Pp = torch.empty(eq * ws, Ccols, dtype=torch.float32, device=X.device)
+            Pp[R:].zero_()
+            (ops.gemm_nt(X, Y, out_dtype=torch.float32, out=Pp[:R]) if phys_is_c else
+             ops.gemm_nt(Y, X, out_dtype=torch.float32, out=Pp[:R]))
             loc = ctx.reduce_scatter_rows(Pp, [eq] * ws)[: counts[r]]
         else:
+            P = ops.gemm_nt(X, Y, out_dtype=torch.float32) if phys_is_c else ops.gemm_nt(Y, X, out_dtype=torch.float32)
             loc = ctx.reduce_scatter_rows(P, counts)
         # epilogue on the local rows: bias along C rows (phys rows when phys_is_c) is sliced by offset
         along_phys_rows = (self.bias_along == "row") == phys_is_c

@@ -39,6 +39,7 @@ def main(argv=None):
     health = None
     if a.heartbeat_port:
         health = HeartbeatMonitor.standalone(a.host, a.heartbeat_port, ctx.rank, ctx.world_size).start()
+        ctx.attach_health(health)      # every engine collective waits under the heartbeat watchdog
     if ctx.rank == 0:
         fe = PDBFrontend(client, a.host, a.port, health, jobs=jobs, udf_modules=a.udf_modules)
         print(f"[netsdb_amd] master listening on {a.host}:{fe.start().port} (world {ctx.world_size})", flush=True)

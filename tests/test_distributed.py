@@ -272,3 +272,128 @@ def test_distributed_object_tensor_exact_bytes():
             assert v == [[(1 << 40) + 7 * i + src, -(1 << 41) - i] for i in idx]
             assert f == [[1.0 / 3.0 + i, 1e-300] for i in idx]
             assert all(d == torch.int64 for d in dts)
+
+
+# ------------------------------------------------------------------ 4 ranks, uneven partitions
+def _la_dist4_scenario(ctx, out_dir):
+    res = _la_dist_scenario(ctx, out_dir)
+    return res
+
+
+@pytest.mark.timeout(600)
+def test_distributed_4ranks_uneven_la_join_agg_dedup():
+    """world_size 4: 40 rows in blocks of 8 split 16/16/8/0 (one rank holds nothing) for the all-gather
+    N-chunk pipeline (A %*% B) and the K-split reduce-scatter (A '* B); partitioned and broadcast joins,
+    shuffle aggregation, and the cross-GPU dedup pool, on 4 gloo ranks."""
+    res = _run("_la_dist4_scenario", ws=4)
+    assert [r["local_rows"] for r in res] == [16, 16, 8, 0]
+    for r in res:
+        assert r["mul"] < 1e-4 and r["tmul"] < 1e-4, r
+        assert r["mul_shape"] == (40, 24) and r["tmul_shape"] == (40, 24)
+    from tests.test_engine import _emps
+
+    eng = _run("_engine_scenario", ws=4)
+    floors = {"eng": 3, "ops": 1, "hr": 2}
+    exp = sorted((e.name, e.department, floors[e.department]) for e in _emps(60) if e.department in floors)
+    for tag in ("broadcast", "partitioned"):
+        assert all(r[f"join_{tag}"] == exp for r in eng)
+        assert sum(r[f"local_emps_{tag}"] for r in eng) == 60
+    ded = _run("_dedup_scenario", ws=4)
+    for r in ded:
+        assert r["err"] == 0.0 and r["err2"] == 0.0 and r["stored"] == 12 + 3
+
+
+def _no_sync_scenario(ctx, out_dir):
+    """The fused distributed matmul issues no .item()/.tolist() host reads once its plan metadata is
+    cached (second run): the K ranges and sizes come from the per-plan cache, collectives run async."""
+    from netsdb_amd.client import PDBClient
+    from netsdb_amd.computations import ScanSet, WriteSet
+    from netsdb_amd.la import computations as L
+    from netsdb_amd.models import blocks as B
+
+    c = PDBClient(ctx=ctx, root=tempfile.mkdtemp())
+    c.create_database("LA_db")
+    g = torch.Generator().manual_seed(7)
+    A = torch.rand(40, 40, generator=g) - 0.5
+    Bm = torch.rand(40, 24, generator=g) - 0.5
+    B.load_tensor(c, "LA_db", "A", A, 8, 8, dtype=torch.float32, partition_rows=True)
+    B.load_tensor(c, "LA_db", "B", Bm, 8, 8, dtype=torch.float32, partition_rows=True)
+
+    def job(name):
+        c.create_set("LA_db", name, None, dense=True)
+        j = L.LAMultiply1Join()
+        j.set_input(0, ScanSet("LA_db", "A"))
+        j.set_input(1, ScanSet("LA_db", "B"))
+        return c.execute_computations(WriteSet("LA_db", name).set_input(L.LAMultiply2Aggregate().set_input(j)))
+
+    job("C1")
+    calls = []
+    orig_item, orig_tolist = torch.Tensor.item, torch.Tensor.tolist
+
+    def guard(name, fn):
+        def w(self, *a, **k):
+            calls.append(name)
+            return fn(self, *a, **k)
+        return w
+
+    torch.Tensor.item, torch.Tensor.tolist = guard("item", orig_item), guard("tolist", orig_tolist)
+    try:
+        n0 = ctx.stats["collectives"]
+        st = job("C2")
+        ncoll = ctx.stats["collectives"] - n0
+    finally:
+        torch.Tensor.item, torch.Tensor.tolist = orig_item, orig_tolist
+    C = B.to_tensor(c, "LA_db", "C2")
+    return {"calls": calls, "fused": st.get("fused_ops"), "err": (C.float() - A @ Bm).abs().max().item(),
+            "collectives": ncoll}
+
+
+@pytest.mark.timeout(300)
+def test_distributed_fused_step_has_no_host_sync():
+    for r in _run("_no_sync_scenario"):
+        assert any("matmul" in f for f in r["fused"])
+        assert r["calls"] == [], r["calls"]
+        assert r["err"] < 1e-4
+        assert r["collectives"] >= 1          # the B chunks' all-gathers (no metadata collectives)
+
+
+def _killed_rank_worker(rank, ws, port, hb_port, out_dir, mode):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(ws))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    from netsdb_amd.parallel.comm import ClusterContext
+    from netsdb_amd.utils.health import HeartbeatMonitor, NodeFailure
+
+    ctx = ClusterContext(rank, ws, torch.device("cpu"), "gloo")
+    hb = HeartbeatMonitor.standalone("127.0.0.1", hb_port, rank, ws, interval=0.05, timeout=0.25).start()
+    ctx.attach_health(hb)
+    ctx.all_reduce(torch.ones(1))                 # both alive: a normal collective
+    if rank == 1:
+        hb.stop()
+        if mode == "hang":                        # alive process, stuck outside the collective: no socket error
+            import time as _t
+
+            _t.sleep(15)
+        os._exit(0)                               # rank 1 dies without entering the next collective
+    import time
+
+    t0 = time.time()
+    outcome = "completed"
+    try:
+        ctx.all_reduce(torch.ones(4))             # would hang forever on a dead peer
+    except NodeFailure as e:
+        outcome = f"NodeFailure: {e}"
+    with open(os.path.join(out_dir, "r0.txt"), "w") as f:
+        f.write(f"{outcome}\n{time.time() - t0:.3f}\n")
+    os._exit(0)                                   # the abandoned gloo work cannot be torn down cleanly
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("mode", ["exit", "hang"])
+def test_killed_rank_raises_node_failure_instead_of_hanging(mode):
+    """A peer that dies (socket reset) or hangs outside the collective (heartbeat stops, no transport
+    error: the case that would block forever) makes the survivor's collective raise NodeFailure."""
+    out = tempfile.mkdtemp()
+    mp.spawn(_killed_rank_worker, args=(2, _free_port(), _free_port(), out, mode), nprocs=2, join=True)
+    outcome, secs = open(os.path.join(out, "r0.txt")).read().split("\n")[:2]
+    assert outcome.startswith("NodeFailure"), outcome
+    assert float(secs) < 10.0

@@ -179,3 +179,34 @@ def test_bias_act_and_lstm_and_embedding():
     e = ops.embedding_bag(table, idx, offs, mode="mean")
     er = ops.embedding_bag(table.cpu(), idx.cpu(), offs.cpu(), mode="mean")
     _close(e.cpu(), er, 1e-5)
+
+
+@pytest.mark.parametrize("S,N,segk,M", [(2, 300, 128, 200), (4, 1000, 320, 256), (8, 777, 64, 130)])
+@pytest.mark.parametrize("out_f32", [True, False])
+def test_gemm_segmented_b_in_place(S, N, segk, M, out_f32):
+    """The all-gathered [S, N, seg_k] chunk consumed in place (K segment s at B + s*N*seg_k) vs the
+    permuted K-contiguous panel: the distributed all-gather pipeline's GEMM."""
+    torch.manual_seed(9)
+    A = torch.randn(M, S * segk, device=DEV).to(torch.bfloat16)
+    Bg = torch.randn(S, N, segk, device=DEV).to(torch.bfloat16)
+    bias = torch.randn(N, device=DEV)
+    dt = torch.float32 if out_f32 else torch.bfloat16
+    C = ops.gemm_nt_segmented(A, Bg, bias, ops.BIAS_COL, ops.ACT_RELU, out_dtype=dt)
+    ref = _ref_gemm(A, Bg.permute(1, 0, 2).reshape(N, S * segk), bias, 2, ops.ACT_RELU)
+    _close(C, ref, tol=1e-2 if out_f32 else 2e-2)
+
+
+def test_gemm_bias_matrix_epilogue():
+    torch.manual_seed(10)
+    A = torch.randn(300, 256, device=DEV).to(torch.bfloat16)
+    B = torch.randn(500, 256, device=DEV).to(torch.bfloat16)
+    bm = torch.randn(300, 500, device=DEV)
+    for splits in (1, 3):
+        C = ops.gemm_nt(A, B, bm, ops.BIAS_MAT, ops.ACT_SIGMOID, out_dtype=torch.float32, splits=splits)
+        _close(C, torch.sigmoid(A.float() @ B.float().t() + bm), tol=1e-2)
+
+
+def test_lstm_elementwise_kernels():
+    f, cp, i, g = (torch.randn(130, 77, device=DEV) for _ in range(4))
+    _close(ops.lstm_two_sum(f, cp, i, g), f * cp + i * g, 1e-6)
+    _close(ops.lstm_hidden(f, cp), f * torch.tanh(cp), 1e-6)
