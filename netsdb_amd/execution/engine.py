@@ -19,7 +19,8 @@ from .. import _ext
 from ..computations import AggregateComp, Computation, TopKComp
 from ..lambdas import Literal, SelfRef
 from ..logical_plan.tcap import bind_atoms, compile_tcap, graph_signature
-from ..objects.record import PDBObject, RecordBatch, RecordView, batch_of, column_concat
+from ..objects.nested import NestedColumn
+from ..objects.record import PDBObject, RecordBatch, RecordView, batch_of, column_concat, column_take
 from ..objects.strings import StringColumn
 from ..parallel.comm import ClusterContext
 from ..query_planning.planner import AdaptivePlanner, PhysicalPlan, Planner
@@ -42,7 +43,7 @@ class _One:
 def _normalize(val, n: int, device):
     if isinstance(val, SelfRef):
         return val.batch
-    if isinstance(val, (RecordBatch, torch.Tensor, tuple, StringColumn)):
+    if isinstance(val, (RecordBatch, torch.Tensor, tuple, StringColumn, NestedColumn)):
         return val
     if isinstance(val, list):
         if val and isinstance(val[0], PDBObject):
@@ -360,6 +361,12 @@ class QueryEngine:
         if t == "FLATTEN":
             vcol = b.columns[a["input"]["atts"][0]]
             carry = a["projection"]["atts"]
+            if isinstance(vcol, NestedColumn):
+                # device FLATTEN: the element column as rows, carried columns gathered by parent index
+                vals, parent = vcol.flatten()
+                cols = {c: column_take(b.columns[c], parent) for c in carry}
+                cols[a["output"]["atts"][-1]] = vals
+                return RecordBatch(cols, int(parent.numel()))
             lens, flat = [], []
             for v in (vcol if not isinstance(vcol, RecordBatch) else [vcol]):
                 items = list(v) if not isinstance(v, RecordBatch) else [RecordView(v, i) for i in range(v.n)]

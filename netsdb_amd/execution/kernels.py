@@ -169,6 +169,18 @@ def _hashable(v):
 
 def segment_reduce(values, inv: torch.Tensor, ngroups: int, op: str = "sum", combine=None):
     """Combine values of rows sharing a group id."""
+    from ..objects.nested import MapColumn, NestedColumn
+
+    if isinstance(values, MapColumn):       # PDBMap merge per group, on the device
+        return MapColumn.merge(values, inv, ngroups)
+    if isinstance(values, NestedColumn):    # Vector concatenation per group (stable order)
+        order = torch.argsort(inv.to(values.device), stable=True)
+        ent = values.take(order)
+        glens = torch.zeros(ngroups, dtype=torch.int64, device=values.device).index_add_(
+            0, inv.to(values.device), values.lengths())
+        off = torch.zeros(ngroups + 1, dtype=torch.int64, device=values.device)
+        torch.cumsum(glens, 0, out=off[1:])
+        return NestedColumn(off, ent.values)
     if isinstance(values, torch.Tensor):
         inv = inv.to(values.device)
         shape = (ngroups,) + tuple(values.shape[1:])

@@ -9,7 +9,10 @@ one column per field:
 * ``int``/``float``/``bool`` -> 1-D torch tensor (int64 / float64 / bool)
 * ``Tensor(shape, dtype)``  -> one stacked tensor ``[n, *shape]`` (lives in HBM when the set is
   device-resident: the MatrixBlock payloads of the linear-algebra sets)
-* ``str`` / ``object`` / ``Vector`` -> Python list (host)
+* ``Vector(int|float|str|SomePDBObject)`` -> :class:`~netsdb_amd.objects.nested.NestedColumn` (offsets +
+  element column, device-resident, recursively nested); ``Map(K, V)`` -> ``MapColumn``
+* a field annotated with a PDBObject subclass (a ``Handle<T>``) -> a nested RecordBatch (struct column)
+* ``str`` / ``object`` / ``Vector(object)`` -> Python list (host)
 
 UDF lambdas operate on whole columns (vectorised, GPU) or, for opaque Python lambdas, on
 :class:`RecordView` objects (the analogue of dereferencing a ``Handle<T>``).
@@ -35,13 +38,27 @@ class Tensor:
 
 
 class Vector:
-    """Variable-length vector field (pdb::Vector<T>); stored as a list column."""
+    """Variable-length vector field (pdb::Vector<T>): a device NestedColumn when the element type is a
+    scalar, ``str`` or a PDBObject type; ``Vector(object)`` stays a host list column."""
 
     def __init__(self, elem=float):
         self.elem = elem
 
+    def nested(self) -> bool:
+        return self.elem in (int, float, bool, str) or (isinstance(self.elem, type) and issubclass(self.elem, PDBObject))
+
     def __repr__(self):
         return f"Vector({getattr(self.elem, '__name__', self.elem)})"
+
+
+class Map:
+    """Map field (pdb::Map<K, V>): a device MapColumn (keys + values children)."""
+
+    def __init__(self, key=str, value=float):
+        self.key, self.value = key, value
+
+    def __repr__(self):
+        return f"Map({getattr(self.key, '__name__', self.key)}, {getattr(self.value, '__name__', self.value)})"
 
 
 SCALAR_TYPES = {int: torch.int64, float: torch.float64, bool: torch.bool}
@@ -95,7 +112,7 @@ class PDBObject:
                 continue
             if isinstance(ann, str):           # postponed annotations (from __future__ import annotations)
                 ann = _resolve_annotation(ann, cls)
-            fields[name] = cls.__dict__.get(name, None) if isinstance(cls.__dict__.get(name), (Tensor, Vector)) \
+            fields[name] = cls.__dict__.get(name, None) if isinstance(cls.__dict__.get(name), (Tensor, Vector, Map)) \
                 else ann
         cls.__fields__ = fields
         register_type(cls)
@@ -111,7 +128,7 @@ class PDBObject:
                 raise TypeError(f"unknown field {n} for {type(self).__name__}")
             setattr(self, n, v)
         for n in names:
-            if not hasattr(self, n) or isinstance(getattr(self, n), (Tensor, Vector)):
+            if not hasattr(self, n) or isinstance(getattr(self, n), (Tensor, Vector, Map)):
                 setattr(self, n, _default_for(self.__fields__[n]))
 
     @classmethod
@@ -161,10 +178,18 @@ def _default_for(ft):
         return ""
     if isinstance(ft, Vector):
         return []
+    if isinstance(ft, Map):
+        return {}
     return None
 
 
 def column_kind(ft) -> str:
+    if isinstance(ft, Vector):
+        return "nested" if ft.nested() else "object"
+    if isinstance(ft, Map):
+        return "map"
+    if isinstance(ft, type) and issubclass(ft, PDBObject):
+        return "struct"
     if ft in SCALAR_TYPES:
         return "scalar"
     if isinstance(ft, Tensor) or ft is torch.Tensor:
@@ -198,8 +223,10 @@ class RecordBatch:
 
     @property
     def device(self) -> torch.device:
+        from .nested import NestedColumn
+
         for c in self.columns.values():
-            if isinstance(c, (torch.Tensor, StringColumn)):
+            if isinstance(c, (torch.Tensor, StringColumn, NestedColumn)):
                 return c.device
         return torch.device("cpu")
 
@@ -255,7 +282,7 @@ class RecordBatch:
                 total += c.numel() * c.element_size()
             elif isinstance(c, RecordBatch):
                 total += c.nbytes()
-            elif isinstance(c, StringColumn):
+            elif isinstance(c, StringColumn) or hasattr(c, "offsets"):
                 total += c.nbytes
             elif isinstance(c, tuple):
                 total += sum(x.numel() * x.element_size() if isinstance(x, torch.Tensor) else 16 * len(x) for x in c)
@@ -292,6 +319,8 @@ def _col_to(c, device):
         return c.to(device)
     if isinstance(c, tuple):
         return tuple(_col_to(x, device) for x in c)
+    if hasattr(c, "offsets") and hasattr(c, "to"):        # NestedColumn / MapColumn
+        return c.to(device)
     return c
 
 
@@ -322,6 +351,19 @@ def make_column(vals: List[Any], ft, device=None):
                 out = out.to(ft.dtype)
             return out.to(device) if device is not None else out
         return [t.to(device) if device is not None else t for t in ts]
+    if kind == "nested":
+        from .nested import NestedColumn
+
+        return NestedColumn.from_lists([list(v) if v is not None else [] for v in vals], ft.elem, device)
+    if kind == "map":
+        from .nested import MapColumn
+
+        return MapColumn.from_dicts([dict(v) if v is not None else {} for v in vals], device)
+    if kind == "struct":
+        objs = [v.materialize() if isinstance(v, RecordView) else v for v in vals]
+        return RecordBatch.from_objects(objs, ft, device)
+    if ft is str or (vals and all(isinstance(v, str) for v in vals) and ft is not object):
+        return list(vals)
     return list(vals)
 
 
@@ -351,7 +393,9 @@ def column_item(c, i):
 
 
 def column_take(c, idx):
-    if isinstance(c, (RecordBatch, StringColumn)):
+    from .nested import NestedColumn
+
+    if isinstance(c, (RecordBatch, StringColumn, NestedColumn)):
         return c.take(idx)
     if isinstance(c, tuple):
         return tuple(column_take(x, idx) for x in c)
@@ -365,8 +409,14 @@ def column_take(c, idx):
 
 
 def column_concat(parts):
+    from .nested import MapColumn, NestedColumn
+
     if parts and all(isinstance(p, RecordBatch) for p in parts):
         return RecordBatch.concat(parts)
+    if parts and all(isinstance(p, MapColumn) for p in parts):
+        return MapColumn.concat(parts)
+    if parts and all(isinstance(p, NestedColumn) for p in parts):
+        return NestedColumn.concat(parts)
     if parts and all(isinstance(p, tuple) for p in parts):
         return tuple(column_concat([p[i] for p in parts]) for i in range(len(parts[0])))
     if parts and any(isinstance(p, StringColumn) for p in parts):
@@ -436,6 +486,6 @@ def batch_of(records: Iterable[Any], type_=None, device=None) -> RecordBatch:
     return RecordBatch.from_objects(objs, type_, device)
 
 
-__all__ = ["PDBObject", "Tensor", "Vector", "RecordBatch", "RecordView", "register_type", "lookup_type",
+__all__ = ["PDBObject", "Tensor", "Vector", "Map", "RecordBatch", "RecordView", "register_type", "lookup_type",
            "registered_types", "batch_of", "make_column", "column_item", "column_take", "column_concat",
            "column_kind", "column_slice", "column_len"]

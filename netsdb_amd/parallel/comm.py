@@ -23,7 +23,8 @@ from typing import Any, Dict, List, Optional, Sequence
 import torch
 import torch.distributed as dist
 
-from ..objects.record import RecordBatch, lookup_type
+from ..objects.nested import MapColumn, NestedColumn
+from ..objects.record import RecordBatch, column_slice, lookup_type
 from ..objects.strings import StringColumn
 from ..storage.serde import _enc_obj, _dec_obj  # noqa: F401  (shared object codec)
 
@@ -246,6 +247,8 @@ class ClusterContext:
             elif cm["kind"] == "string":
                 recv_cols[name] = self._exchange_strings([p.columns[name] for p in parts], counts)
                 recv_counts = recv_cols[name][1]
+            elif cm["kind"] in ("nested", "map"):
+                recv_cols[name], recv_counts = self._exchange_nested([p.columns[name] for p in parts], counts, cm)
             else:
                 payloads = [json.dumps([_enc_plain(v) for v in p.columns[name]]).encode() for p in parts]
                 data = torch.frombuffer(bytearray(b"".join(payloads)) or bytearray(b"\0"), dtype=torch.uint8)
@@ -272,6 +275,8 @@ class ClusterContext:
                     cols[name] = recv_cols[name][off: off + k]
                 elif cm["kind"] == "string":
                     cols[name] = recv_cols[name][0][src]
+                elif cm["kind"] in ("nested", "map"):
+                    cols[name] = recv_cols[name][src]
                 else:
                     cols[name] = [_dec_plain(v) for v in recv_cols[name][src]]
             out_batches.append(RecordBatch(cols, k, t))
@@ -336,6 +341,27 @@ class ClusterContext:
             buf[:nb] = rdata[rb: rb + nb]
             out.append(StringColumn(buf, offs, nb))
             ro, rb = ro + k, rb + nb
+        return out, rcounts
+
+    def _exchange_nested(self, cols, counts, cm):
+        """Vector / Map columns on the wire: per-row lengths in one all-to-all, then the element child
+        (itself a batch, possibly nested again) shuffled recursively with per-destination element counts.
+        Every rank runs the same collectives: the schema (and so this branch) was agreed beforehand."""
+        dev = self.device
+        cols = [_nested_rebase(c) for c in cols]
+        lens = torch.cat([c.lengths().to(dev) for c in cols])
+        rlens, rcounts = self.all_to_all_rows(lens, counts)
+        child_parts = [_flatten(_nested_child(c)) for c in cols]
+        got = self._exchange_flat(child_parts)
+        out, ro = [], 0
+        for src, k in enumerate(rcounts):
+            offs = torch.zeros(k + 1, dtype=torch.int64, device=rlens.device)
+            if k:
+                torch.cumsum(rlens[ro: ro + k], 0, out=offs[1:])
+            ch = _unflatten(got[src]) if got else _unflatten(_empty_like_meta(cm["child"], dev))
+            out.append(MapColumn(offs, ch.columns["k"], ch.columns["v"]) if cm["kind"] == "map"
+                       else NestedColumn(offs, ch.columns["v"]))
+            ro += k
         return out, rcounts
 
     def broadcast_batch_all(self, b: Optional[RecordBatch]) -> List[RecordBatch]:
@@ -409,9 +435,27 @@ def _batch_meta(b: Optional[RecordBatch]):
                          "shape": list(c.shape[1:])})
         elif isinstance(c, StringColumn):
             cols.append({"name": k, "kind": "string"})
+        elif isinstance(c, NestedColumn):
+            cols.append({"name": k, "kind": "map" if isinstance(c, MapColumn) else "nested",
+                         "child": _batch_meta(_flatten(_nested_child(_nested_rebase(c))))})
         else:
             cols.append({"name": k, "kind": "object"})
     return {"type": b.type.type_name() if b.type is not None else None, "columns": cols}
+
+
+def _nested_rebase(c):
+    """A nested column whose offsets start at 0 and whose children hold exactly its elements."""
+    if c.offsets.numel() and int(c.offsets[0]) != 0:
+        return c.slice(0, len(c))
+    return c
+
+
+def _nested_child(c) -> RecordBatch:
+    n = int(c.offsets[-1]) if c.offsets.numel() else 0
+    cols = {"v": column_slice(c.values, 0, n)}
+    if isinstance(c, MapColumn):
+        cols["k"] = column_slice(c.keys, 0, n)
+    return RecordBatch(cols, n)
 
 
 def _as_tensor(c, cm, device):
@@ -427,6 +471,11 @@ def _empty_like_meta(meta, device):
             cols[cm["name"]] = torch.empty((0,) + tuple(cm["shape"]), dtype=getattr(torch, cm["dtype"]), device=device)
         elif cm["kind"] == "string":
             cols[cm["name"]] = StringColumn.empty(device)
+        elif cm["kind"] in ("nested", "map"):
+            ch = _unflatten(_empty_like_meta(cm["child"], device))
+            off = torch.zeros(1, dtype=torch.int64, device=device)
+            cols[cm["name"]] = MapColumn(off, ch.columns["k"], ch.columns["v"]) if cm["kind"] == "map" \
+                else NestedColumn(off, ch.columns["v"])
         else:
             cols[cm["name"]] = []
     t = lookup_type(meta["type"]) if meta["type"] else None

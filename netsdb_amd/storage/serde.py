@@ -18,6 +18,7 @@ import numpy as np
 import torch
 
 from ..objects.record import PDBObject, RecordBatch, lookup_type
+from ..objects.nested import MapColumn, NestedColumn
 from ..objects.strings import StringColumn
 
 _ALIGN = 64
@@ -98,6 +99,17 @@ def serialize_batch(batch: RecordBatch) -> bytes:
             b = _tensor_bytes(c)
             cols_meta.append({"name": name, "kind": "tensor", "dtype": _DT[c.dtype], "shape": list(c.shape),
                               "off": add(b), "len": len(b)})
+        elif isinstance(c, NestedColumn):       # Vector / Map field: offsets + element (and key) children
+            if c.offsets.numel() and int(c.offsets[0]) != 0:
+                c = c.slice(0, len(c))
+            ob = _tensor_bytes(c.offsets.cpu() - c.offsets[0].cpu())
+            ch = {"v": c.values}
+            if isinstance(c, MapColumn):
+                ch["k"] = c.keys
+            b = serialize_batch(RecordBatch(ch, int(c.offsets[-1] - c.offsets[0]) if c.offsets.numel() else 0))
+            cols_meta.append({"name": name, "kind": "map" if isinstance(c, MapColumn) else "nested",
+                              "n": c.offsets.numel() - 1, "off": add(ob), "len": len(ob), "boff": add(b),
+                              "blen": len(b)})
         elif isinstance(c, RecordBatch):        # nested record column (an engine tuple set's object column)
             b = serialize_batch(c)
             cols_meta.append({"name": name, "kind": "batch", "off": add(b), "len": len(b)})
@@ -137,6 +149,11 @@ def deserialize_batch(data) -> RecordBatch:
             cols[cm["name"]] = _tensor_from(seg, cm["dtype"], cm["shape"])
         elif cm["kind"] == "batch":
             cols[cm["name"]] = deserialize_batch(seg)
+        elif cm["kind"] in ("nested", "map"):
+            offs = _tensor_from(seg, "i64", [cm["n"] + 1])
+            inner = deserialize_batch(mv[base + cm["boff"]: base + cm["boff"] + cm["blen"]])
+            cols[cm["name"]] = (MapColumn(offs, inner.columns["k"], inner.columns["v"]) if cm["kind"] == "map"
+                                else NestedColumn(offs, inner.columns["v"]))
         elif cm["kind"] == "tuple":
             inner = deserialize_batch(seg)
             cols[cm["name"]] = tuple(inner.columns[f"t{i}"] for i in range(cm["k"]))

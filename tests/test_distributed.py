@@ -397,3 +397,33 @@ def test_killed_rank_raises_node_failure_instead_of_hanging(mode):
     outcome, secs = open(os.path.join(out, "r0.txt")).read().split("\n")[:2]
     assert outcome.startswith("NodeFailure"), outcome
     assert float(secs) < 10.0
+
+
+def _nested_scenario(ctx, out_dir):
+    """Vector / Map columns on the wire: customers dispatched across ranks (nested exchange), the
+    vectorized FLATTEN + map-merge group-by with its shuffle, and top-k Jaccard."""
+    from netsdb_amd.client import PDBClient
+    from netsdb_amd.models import tpch_nested as T
+
+    cs = T.generate(80, seed=7)
+    c = PDBClient(ctx=ctx, root=tempfile.mkdtemp(), page_size=1 << 14)
+    c.create_database("bench")
+    c.create_set("bench", "customers", T.BCustomer)
+    c.send_data("bench", "customers", cs if ctx.rank == 0 else None)
+    local = c.get_set("bench", "customers").num_records()
+    q = [2, 4, 6, 8]
+    return {"local": local, "gb": T.supplier_groupby(c, "bench"), "gb_obj": T.supplier_groupby(c, "bench", False),
+            "top": T.top_jaccard(c, "bench", 5, q)}
+
+
+@pytest.mark.timeout(300)
+def test_distributed_nested_columns():
+    from netsdb_amd.models import tpch_nested as T
+
+    cs = T.generate(80, seed=7)
+    res = _run("_nested_scenario")
+    assert sum(r["local"] for r in res) == 80 and all(r["local"] < 80 for r in res)
+    ref = T.reference_groupby(cs)
+    for r in res:
+        assert r["gb"] == ref and r["gb_obj"] == ref
+        assert r["top"] == T.reference_jaccard(cs, [2, 4, 6, 8], 5)
