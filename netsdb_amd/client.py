@@ -269,9 +269,16 @@ class PDBClient:
         key = TensorBlockIndex.set_key(0, 0, sharing.set_id)
         if file_name is not None:
             idx.load_index_file(key, file_name, total_rows, total_cols, transpose)
-        for k, (r, c) in (mapping or {}).items():
+        multi = {}
+        for k, v in (mapping or {}).items():
+            if isinstance(v, list):       # one stored block at several places of the sharing model
+                multi[int(k)] = [(c, r, total_rows, total_cols) if transpose else (r, c, total_rows, total_cols)
+                                 for r, c in v]
+                continue
+            r, c = v
             idx.insert_index(key, k, (c, r, total_rows, total_cols) if transpose else (r, c, total_rows, total_cols))
-        targets = idx.targets.get(key, {})
+        targets = dict(idx.targets.get(key, {}))
+        targets.update(multi)
         sharing.set_shared_mapping(shared, targets)
         if not sharing.link(shared).pages:
             # a mapping alone shares every page of the shared set (the reference links pages first)

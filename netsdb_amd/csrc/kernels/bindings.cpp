@@ -29,6 +29,11 @@ int nsdb_lstm_cell(const void* gates, int g_f32, const float* c_prev, void* h_ou
                    int H, hipStream_t st);
 int nsdb_embedding_bag(const void* table, int t_f32, const long long* idx, const long long* offsets,
                        const float* weights, float* out, int Bn, int D, int mode, hipStream_t st);
+int nsdb_dedup_splits(long long nblocks, long long bytes_per_block);
+int nsdb_block_hash(const void* data, long long nblocks, long long words, int S, unsigned long long* partial,
+                    hipStream_t st);
+int nsdb_block_maxdiff(const void* pool, const long long* cand, const void* blks, long long nblocks, long long elems,
+                       int is_f32, int S, float* partial, hipStream_t st);
 int nsdb_str_hash(const void* bytes, const int64_t* off, int64_t n, uint64_t* out, hipStream_t st);
 int nsdb_str_like(const void* bytes, const int64_t* off, int64_t n, const uint8_t* pat, int pat_len,
                   const int* seg_start, const int* seg_len, int nseg, int anchor_start, int anchor_end, int negate,
@@ -393,6 +398,52 @@ torch::Tensor str_gather(torch::Tensor bytes, torch::Tensor off, torch::Tensor i
   return dst;
 }
 
+// Dedup: blocks [n, ...] contiguous (any dtype; bytes per block % 16 == 0) -> [n, S] i64 partial sums.
+torch::Tensor block_hash_partial(torch::Tensor blocks) {
+  check_cuda(blocks, "blocks");
+  TORCH_CHECK(blocks.is_contiguous() && blocks.dim() >= 1, "blocks must be contiguous [n, ...]");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(blocks.data_ptr()) % 16 == 0, "blocks must be 16-B aligned");
+  const int64_t n = blocks.size(0);
+  const int64_t bytes = n ? blocks.numel() / n * blocks.element_size() : 0;
+  TORCH_CHECK(bytes % 16 == 0, "bytes per block must be a multiple of 16");
+  const int S = nsdb_dedup_splits(n, bytes);
+  auto out = torch::empty({n, S}, blocks.options().dtype(torch::kInt64));
+  const char* base = (const char*)blocks.data_ptr();
+  for (int64_t b0 = 0; b0 < n; b0 += 65535) {           // grid.y limit
+    const int64_t nb = std::min<int64_t>(65535, n - b0);
+    check_rc(nsdb_block_hash(base + b0 * bytes, nb, bytes / 4, S,
+                             (unsigned long long*)out.data_ptr<int64_t>() + b0 * S, cur_stream()),
+             "block_hash");
+  }
+  return out;
+}
+
+// max |pool[cand[b]] - blks[b]| per block, [n, S] f32 partials. cand must index rows of pool (the
+// caller derives it from a searchsorted over the pool's own keys, so 0 <= cand < pool.size(0)).
+torch::Tensor block_maxdiff_partial(torch::Tensor pool, torch::Tensor cand, torch::Tensor blks) {
+  check_cuda(pool, "pool");
+  check_cuda(cand, "cand");
+  check_cuda(blks, "blks");
+  TORCH_CHECK(pool.scalar_type() == blks.scalar_type(), "pool/blks dtype mismatch");
+  const bool f32 = is_f32(pool, "pool");
+  TORCH_CHECK(pool.is_contiguous() && blks.is_contiguous() && cand.is_contiguous(), "contiguous inputs");
+  TORCH_CHECK(cand.scalar_type() == torch::kInt64 && cand.dim() == 1 && cand.numel() == blks.size(0), "cand i64 [n]");
+  const int64_t n = blks.size(0);
+  TORCH_CHECK(pool.size(0) > 0 || n == 0, "empty pool");
+  const int64_t elems = n ? blks.numel() / n : 0;
+  TORCH_CHECK(pool.numel() == pool.size(0) * elems, "pool/blks block size mismatch");
+  const int S = nsdb_dedup_splits(n, elems * blks.element_size());
+  auto out = torch::empty({n, S}, blks.options().dtype(torch::kFloat32));
+  for (int64_t b0 = 0; b0 < n; b0 += 65535) {
+    const int64_t nb = std::min<int64_t>(65535, n - b0);
+    check_rc(nsdb_block_maxdiff(pool.data_ptr(), (const long long*)cand.data_ptr<int64_t>() + b0,
+                                (const char*)blks.data_ptr() + b0 * elems * blks.element_size(), nb, elems, f32, S,
+                                out.data_ptr<float>() + b0 * S, cur_stream()),
+             "block_maxdiff");
+  }
+  return out;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -424,6 +475,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_cell", &lstm_cell, py::arg("gates"), py::arg("c_prev") = py::none(), py::arg("h_f32") = true);
   m.def("embedding_bag", &embedding_bag, py::arg("table"), py::arg("idx"), py::arg("offsets"),
         py::arg("weights") = py::none(), py::arg("mode") = 0);
+  m.def("block_hash_partial", &block_hash_partial, "dedup: per-(block, split) partial content-hash sums");
+  m.def("block_maxdiff_partial", &block_maxdiff_partial, "dedup: per-(block, split) max |pool[cand] - blk|");
   m.def("str_hash", &str_hash, "64-bit hash per string of a device string column");
   m.def("str_like", &str_like, "SQL LIKE over a device string column (segments of the pattern bytes)");
   m.def("str_gather", &str_gather, "take() of a device string column into a new padded byte buffer");

@@ -474,14 +474,47 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   store_tile_lds<256, 256, 2, 4>(acc, smem, 2 * BUF, p, batch, split, m0, n0, tid, lane, wave);
 }
 
+// Epilogue of 4 consecutive reduced columns of one row (alpha, bias, activation, dropout, accumulate,
+// f32 / bf16 store) shared by the split-K reducers.
+__device__ __forceinline__ void reduce_epilogue4(const GemmParams& p, int batch, long long MN, long long e, f32x4 s) {
+  const float* bias = p.bias ? p.bias + batch * p.sBias : nullptr;
+  const float keep_scale = p.dropout > 0.f ? 1.f / (1.f - p.dropout) : 1.f;
+  const int row = (int)(e / p.N), col = (int)(e % p.N);
+  float v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float x = s[j] * p.alpha;
+    if (bias) x += (p.bias_mode == 1) ? bias[row] : (p.bias_mode == 3) ? bias[e + j] : bias[col + j];
+    x = apply_act_compact(x, p.act);
+    if (p.dropout > 0.f) {
+      const unsigned long long idx = (unsigned long long)batch * MN + e + j;
+      x = hash_uniform(p.seed, idx) < p.dropout ? 0.f : x * keep_scale;
+    }
+    v[j] = x;
+  }
+  const long long off = batch * p.sC + (long long)row * p.ldc + col;
+  if (p.accumulate) {
+    const float* cf = reinterpret_cast<const float*>(p.C) + off;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] += cf[j];
+  }
+  if (p.out_f32) {
+    float* d = reinterpret_cast<float*>(p.C) + off;
+    if (p.vec_c) *reinterpret_cast<f32x4*>(d) = f32x4{v[0], v[1], v[2], v[3]};
+    else { d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3]; }
+  } else {
+    unsigned short* d = reinterpret_cast<unsigned short*>(p.C) + off;
+    if (p.vec_c) *reinterpret_cast<uint2*>(d) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+    else { d[0] = f32_to_bf16(v[0]); d[1] = f32_to_bf16(v[1]); d[2] = f32_to_bf16(v[2]); d[3] = f32_to_bf16(v[3]); }
+  }
+}
+
 // Split-K slab reducer + fused epilogue (the ClusterAggregate "combine" of the partial block products).
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(GemmParams p) {
   const long long MN = (long long)p.M * p.N;
-  const long long total = MN * gridDim.y;
   const int batch = blockIdx.y;
   const float* bias = p.bias ? p.bias + batch * p.sBias : nullptr;
   const float keep_scale = p.dropout > 0.f ? 1.f / (1.f - p.dropout) : 1.f;
-  (void)total;
   if (p.vec_ws) {
     // N % 4 == 0: 4 consecutive columns of one row per thread, 16-B slab loads (splits in flight together)
     for (long long e = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4; e < MN;
@@ -498,34 +531,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(GemmParams p) {
       for (int k = 1; k < 16; ++k)
         if (k < p.splits) s += part[k];
       for (int k = 16; k < p.splits; ++k) s += *reinterpret_cast<const f32x4*>(w + k * MN);
-      const int row = (int)(e / p.N), col = (int)(e % p.N);
-      float v[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float x = s[j] * p.alpha;
-        if (bias) x += (p.bias_mode == 1) ? bias[row] : (p.bias_mode == 3) ? bias[e + j] : bias[col + j];
-        x = apply_act_compact(x, p.act);
-        if (p.dropout > 0.f) {
-          const unsigned long long idx = (unsigned long long)batch * MN + e + j;
-          x = hash_uniform(p.seed, idx) < p.dropout ? 0.f : x * keep_scale;
-        }
-        v[j] = x;
-      }
-      const long long off = batch * p.sC + (long long)row * p.ldc + col;
-      if (p.accumulate) {
-        const float* cf = reinterpret_cast<const float*>(p.C) + off;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] += cf[j];
-      }
-      if (p.out_f32) {
-        float* d = reinterpret_cast<float*>(p.C) + off;
-        if (p.vec_c) *reinterpret_cast<f32x4*>(d) = f32x4{v[0], v[1], v[2], v[3]};
-        else { d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3]; }
-      } else {
-        unsigned short* d = reinterpret_cast<unsigned short*>(p.C) + off;
-        if (p.vec_c) *reinterpret_cast<uint2*>(d) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-        else { d[0] = f32_to_bf16(v[0]); d[1] = f32_to_bf16(v[1]); d[2] = f32_to_bf16(v[2]); d[3] = f32_to_bf16(v[3]); }
-      }
+      reduce_epilogue4(p, batch, MN, e, s);
     }
     return;
   }
@@ -546,6 +552,39 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(GemmParams p) {
     if (p.accumulate) v += reinterpret_cast<float*>(p.C)[off];
     if (p.out_f32) reinterpret_cast<float*>(p.C)[off] = v;
     else reinterpret_cast<unsigned short*>(p.C)[off] = f32_to_bf16(v);
+  }
+}
+
+// Narrow outputs with many splits (M x N small, K huge: dedup / word2vec scoring 500 x 100 x 1e6): the
+// plain reducer has too few workgroups and walks every slab serially per thread.  Here 8 groups of 64
+// lanes share 64 output vec4s; group g sums slabs g, g+8, ... with 4 loads in flight, then the 8
+// partials meet in LDS.  Deterministic (fixed summation tree).
+__global__ void __launch_bounds__(512) splitk_reduce_wide_kernel(GemmParams p) {
+  const long long MN = (long long)p.M * p.N;
+  const int batch = blockIdx.y;
+  const int v = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const long long e = ((long long)blockIdx.x * 64 + v) * 4;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (e < MN) {
+    const float* w = p.ws + (long long)batch * p.splits * MN + e;
+    for (int k = g; k < p.splits; k += 32) {
+      f32x4 a[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (k + 8 * q < p.splits) a[q] = *reinterpret_cast<const f32x4*>(w + (long long)(k + 8 * q) * MN);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (k + 8 * q < p.splits) s += a[q];
+    }
+  }
+  __shared__ f32x4 red[8][64];
+  red[g][v] = s;
+  __syncthreads();
+  if (g == 0 && e < MN) {
+    f32x4 t = red[0][v];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) t += red[q][v];
+    reduce_epilogue4(p, batch, MN, e, t);
   }
 }
 
@@ -650,8 +689,14 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
     hipLaunchKernelGGL((nsdb::gemm_nt_tile_kernel<128, 128, 2, 2>), grid, dim3(256), 0, stream, p);
   if (p.splits > 1) {
     const long long MN = (long long)M * N;
-    int blocks = (int)std::min<long long>(((p.vec_ws ? MN / 4 : MN) + 255) / 256, 4096);
-    hipLaunchKernelGGL(nsdb::splitk_reduce_kernel, dim3(blocks, batch), dim3(256), 0, stream, p);
+    const long long plain_blocks = ((p.vec_ws ? MN / 4 : MN) + 255) / 256;
+    if (p.vec_ws && p.splits >= 8 && plain_blocks * batch < 512) {
+      hipLaunchKernelGGL(nsdb::splitk_reduce_wide_kernel, dim3((unsigned)((MN / 4 + 63) / 64), batch), dim3(512), 0,
+                         stream, p);
+    } else {
+      int blocks = (int)std::min<long long>(plain_blocks, 4096);
+      hipLaunchKernelGGL(nsdb::splitk_reduce_kernel, dim3(blocks, batch), dim3(256), 0, stream, p);
+    }
   }
   return (int)hipGetLastError();
 }

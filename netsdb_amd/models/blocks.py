@@ -105,16 +105,21 @@ def to_tensor(client, db: str, name: str, gather: bool = True) -> torch.Tensor:
     from ..objects.record import RecordBatch
 
     b = RecordBatch.concat(batches)
+    keep = (b.columns["block_row"] >= 0) & (b.columns["block_col"] >= 0)     # unmapped shared blocks
+    if not bool(keep.all()):
+        b = b.take(keep.nonzero().flatten())
+    if b.n == 0:
+        return torch.empty(0)
     tr, tc = int(b.columns["total_rows"][0]), int(b.columns["total_cols"][0])
     data = b.columns["data"]
     br, bc = data.shape[1], data.shape[2]
-    out = torch.zeros(tr, tc, dtype=torch.float32, device=data.device)
-    for k in range(b.n):
-        i, j = int(b.columns["block_row"][k]), int(b.columns["block_col"][k])
-        r0, c0 = i * br, j * bc
-        h, w = min(br, tr - r0), min(bc, tc - c0)
-        out[r0:r0 + h, c0:c0 + w] = data[k, :h, :w].float()
-    return out
+    nbr, nbc = -(-tr // br), -(-tc // bc)
+    # one scatter of every block into the padded [nbr, br, nbc, bc] view (no per-block host loop)
+    out = torch.zeros(nbr, br, nbc, bc, dtype=torch.float32, device=data.device)
+    r = b.columns["block_row"].to(data.device)
+    c = b.columns["block_col"].to(data.device)
+    out[r, :, c, :] = data.float()
+    return out.reshape(nbr * br, nbc * bc)[:tr, :tc]
 
 
 __all__ = ["create_matrix_set", "fill_random", "load_matrix", "load_tensor", "load_block_file", "to_tensor"]

@@ -98,16 +98,63 @@ def from_blocks(blocks: torch.Tensor, nbr: int, nbc: int, R: int, C: int) -> tor
     return blocks.reshape(nbr, nbc, br, bc).permute(0, 2, 1, 3).reshape(nbr * br, nbc * bc)[:R, :C]
 
 
+_FNV = 0x100000001B3
+
+
+def _words32(blocks: torch.Tensor) -> torch.Tensor:
+    """Each block's raw bytes as u32 words (int64 holding 0..2^32-1), zero-padded to a whole word."""
+    flat = blocks.reshape(blocks.shape[0], -1).contiguous()
+    raw = flat.view(torch.uint8)
+    pad = (-raw.shape[1]) % 4
+    if pad:
+        raw = torch.nn.functional.pad(raw, (0, pad))
+    return raw.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+
+
+def block_hashes_reference(blocks: torch.Tensor, chunk_words: int = 1 << 24) -> torch.Tensor:
+    """Canonical block content hash in torch (any device):
+    ``mix64(sum_j mix64(w_j * 0x100000001B3 + j))`` over the block's 32-bit words, wrapping int64.
+    Processed in bounded chunks of blocks so a 2-MB-block model never materialises 8 B per element."""
+    n = blocks.shape[0]
+    out = torch.empty(n, dtype=torch.int64, device=blocks.device)
+    if n == 0:
+        return out
+    per = max(1, (blocks[0].numel() * blocks.element_size() + 3) // 4)
+    step = max(1, chunk_words // per)
+    for b0 in range(0, n, step):
+        w = _words32(blocks[b0: b0 + step])
+        pos = torch.arange(w.shape[1], device=w.device, dtype=torch.int64)
+        out[b0: b0 + step] = mix64(mix64(w * _FNV + pos).sum(1))
+    return out
+
+
+def _native_ok(blocks: torch.Tensor) -> bool:
+    if not blocks.is_cuda or blocks.shape[0] == 0:
+        return False
+    return (blocks[0].numel() * blocks.element_size()) % 16 == 0 and blocks.is_contiguous() and \
+        blocks.data_ptr() % 16 == 0
+
+
 def block_hashes(blocks: torch.Tensor) -> torch.Tensor:
-    """Exact content hash per block (on device): mix64 over the raw 16-bit/32-bit words."""
-    flat = blocks.reshape(blocks.shape[0], -1)
-    if flat.dtype in (torch.bfloat16, torch.float16):
-        words = flat.view(torch.int16).to(torch.int64) & 0xFFFF
-    else:
-        words = flat.float().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
-    pos = torch.arange(words.shape[1], device=words.device, dtype=torch.int64)
-    h = mix64(words * 0x100000001B3 + pos)
-    return mix64(h.sum(1))   # order-aware (pos mixed in), commutative sum is fine after mixing
+    """Exact content hash per block: one HBM pass of the ``block_hash`` HIP kernel on a GPU (partial sums
+    per split, finished here), the chunked torch reference elsewhere — bit-identical results."""
+    if _native_ok(blocks):
+        from .. import _ext
+
+        return mix64(_ext.hip().block_hash_partial(blocks).sum(1))
+    return block_hashes_reference(blocks)
+
+
+def block_maxdiff(pool: torch.Tensor, cand: torch.Tensor, blks: torch.Tensor) -> torch.Tensor:
+    """max |pool[cand[i]] - blks[i]| per block (content verification of hash hits); the HIP kernel reads
+    both operands once without gathering the candidates."""
+    if blks.shape[0] == 0:
+        return torch.empty(0, dtype=torch.float32, device=blks.device)
+    if _native_ok(blks) and pool.is_contiguous() and pool.dtype in (torch.float32, torch.bfloat16):
+        from .. import _ext
+
+        return _ext.hip().block_maxdiff_partial(pool, cand.contiguous(), blks).amax(1)
+    return (pool.index_select(0, cand).float() - blks.float()).abs().flatten(1).amax(1)
 
 
 def lsh_signatures(blocks: torch.Tensor, bits: int = 64, seed: int = 0) -> torch.Tensor:
@@ -121,16 +168,37 @@ def lsh_signatures(blocks: torch.Tensor, bits: int = 64, seed: int = 0) -> torch
 
 
 class BlockPool:
-    """Deduplicated block storage shared by many models (SharedFFMatrixBlockSet analogue)."""
+    """Deduplicated block storage shared by many models (SharedFFMatrixBlockSet analogue).
+
+    The pool is one capacity-doubling device buffer [cap, br, bc] (amortised O(1) appends, no
+    re-concatenation of the whole pool per insert) plus its keys kept sorted for the hash-hit
+    search; stored blocks never move, so pool ids stay valid."""
 
     def __init__(self, block_rows: int, block_cols: int, device="cpu", dtype=torch.bfloat16, tolerance: float = 0.0):
         self.br, self.bc = block_rows, block_cols
         self.device, self.dtype = device, dtype
         self.tolerance = tolerance
-        self.blocks = torch.empty(0, block_rows, block_cols, dtype=dtype, device=device)
-        self.keys = torch.empty(0, dtype=torch.int64, device=device)
+        self._buf = torch.empty(0, block_rows, block_cols, dtype=dtype, device=device)
+        self._n = 0
+        self.keys = torch.empty(0, dtype=torch.int64, device=device)        # key of pool id i
+        self._sorted_keys = self.keys
+        self._sorted_ids = torch.empty(0, dtype=torch.int64, device=device)
         self.index = TensorBlockIndex(block_rows, block_cols)
-        self.stats = {"blocks_in": 0, "blocks_stored": 0}
+        self.stats = {"blocks_in": 0, "blocks_stored": 0, "grows": 0}
+
+    @property
+    def blocks(self) -> torch.Tensor:
+        return self._buf[: self._n]
+
+    def _reserve(self, n: int):
+        if n <= self._buf.shape[0]:
+            return
+        cap = max(n, 2 * self._buf.shape[0], 16)
+        buf = torch.empty(cap, self.br, self.bc, dtype=self.dtype, device=self.device)
+        if self._n:
+            buf[: self._n].copy_(self._buf[: self._n])
+        self._buf = buf
+        self.stats["grows"] += 1
 
     def add_model(self, name: str, m: torch.Tensor) -> torch.Tensor:
         m = m.to(self.device, self.dtype)
@@ -144,37 +212,45 @@ class BlockPool:
     def insert_blocks(self, blks: torch.Tensor, keys: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Pool ids of ``blks`` [n, br, bc]: a block equal (within tolerance) to a stored one reuses its
         id; new distinct blocks are appended (deduplicated among themselves too)."""
-        blks = blks.to(self.device, self.dtype)
+        blks = blks.to(self.device, self.dtype).contiguous()
         if keys is None:
             keys = block_hashes(blks) if self.tolerance == 0 else lsh_signatures(blks)
+        keys = keys.to(self.device)
         ids = torch.empty(blks.shape[0], dtype=torch.int64, device=self.device)
-        # match against the pool (sorted-key binary search), verify content within tolerance
-        if self.keys.numel():
-            order = torch.argsort(self.keys)
-            sk = self.keys[order]
+        # match against the pool (binary search in the sorted keys), verify content within tolerance
+        if self._n:
+            sk = self._sorted_keys
             pos = torch.searchsorted(sk, keys).clamp(max=sk.numel() - 1)
-            cand = order[pos]
+            cand = self._sorted_ids[pos]
             hit = sk[pos] == keys
-            if hit.any():
-                diff = (self.blocks[cand].float() - blks.float()).abs().amax(dim=(1, 2))
-                hit &= diff <= self.tolerance
+            if bool(hit.any()):
+                hi = hit.nonzero().flatten()
+                ok = block_maxdiff(self.blocks, cand[hi], blks[hi]) <= self.tolerance
+                hit[hi] = ok
         else:
             cand = torch.zeros_like(ids)
             hit = torch.zeros(blks.shape[0], dtype=torch.bool, device=self.device)
         ids[hit] = cand[hit]
         new = (~hit).nonzero().flatten()
         if new.numel():
-            # dedup within the incoming blocks themselves
+            # dedup within the incoming blocks themselves (equal keys -> the first occurrence)
             nk = keys[new]
             uk, inv = torch.unique(nk, return_inverse=True)
             first = torch.full((uk.numel(),), new.numel(), dtype=torch.int64, device=self.device)
             first.scatter_reduce_(0, inv, torch.arange(new.numel(), device=self.device), reduce="amin")
-            base = self.blocks.shape[0]
-            self.blocks = torch.cat([self.blocks, blks[new[first]]])
-            self.keys = torch.cat([self.keys, uk if self.tolerance == 0 else nk[first]])
+            base, k = self._n, uk.numel()
+            self._reserve(base + k)
+            self._buf[base: base + k].copy_(blks[new[first]])
+            self._n = base + k
+            new_keys = uk if self.tolerance == 0 else nk[first]
+            self.keys = torch.cat([self.keys, new_keys])
+            sk, order = torch.sort(torch.cat([self._sorted_keys, new_keys]), stable=True)
+            self._sorted_keys = sk
+            self._sorted_ids = torch.cat([self._sorted_ids,
+                                          torch.arange(base, base + k, device=self.device)])[order]
             ids[new] = base + inv
         self.stats["blocks_in"] += blks.shape[0]
-        self.stats["blocks_stored"] = self.blocks.shape[0]
+        self.stats["blocks_stored"] = self._n
         return ids
 
     def materialize(self, name: str) -> torch.Tensor:
@@ -182,6 +258,64 @@ class BlockPool:
         R, C = self.index.shapes[name]
         blks = self.blocks.index_select(0, t.flatten().to(self.blocks.device))
         return from_blocks(blks, t.shape[0], t.shape[1], R, C)
+
+    # ------------------------------------------------------------------ storage integration
+    def store(self, client, db: str, set_name: str, blocks_per_page: int = 64, algorithm: str = "greedy1") -> Dict[int, int]:
+        """Persist the distinct blocks as an FFMatrixBlock set whose pages follow the page packing (blocks
+        shared by the same models land on the same pages), so each model links only the pages it uses.
+        Returns {pool block id: page number}.  The set's pages go through the node's buffer pool like any
+        other set (budgeted, spillable, flushed)."""
+        from ..objects.builtin import FFMatrixBlock
+        from ..objects.record import RecordBatch
+
+        pages = self.pack_pages(blocks_per_page, algorithm)
+        blk_bytes = self.br * self.bc * torch.empty(0, dtype=self.dtype).element_size() + 80
+        big = max((len(p) for p in pages), default=1)
+        page_size = int(big * blk_bytes * 16 // 15) + 8192
+        if client.storage.has_set(db, set_name):
+            client.remove_set(db, set_name)
+        client.create_database(db)
+        client.create_set(db, set_name, FFMatrixBlock, page_size=page_size)
+        st = client.storage.get_set(db, set_name)
+        page_of: Dict[int, int] = {}
+        for pg in pages:
+            ids = torch.tensor(pg, dtype=torch.int64, device=self.blocks.device)
+            n = ids.numel()
+            z = torch.zeros(n, dtype=torch.int64, device=ids.device)
+            cols = {"block_row": z, "block_col": z.clone(),
+                    "row_nums": torch.full((n,), self.br, dtype=torch.int64, device=ids.device),
+                    "col_nums": torch.full((n,), self.bc, dtype=torch.int64, device=ids.device),
+                    "total_rows": z.clone(), "total_cols": z.clone(), "data": self.blocks.index_select(0, ids),
+                    "distinct_block_id": ids, "partition_by_col": torch.zeros(n, dtype=torch.bool, device=ids.device)}
+            before = len(st.pages)
+            st.add_batch(RecordBatch(cols, n, FFMatrixBlock))
+            assert len(st.pages) == before + 1, "a packed page must map to exactly one storage page"
+            for b in pg:
+                page_of[int(b)] = before
+        self.stored_pages = page_of
+        return page_of
+
+    def link_model(self, client, db: str, model_set: str, pool_set: str, name: str) -> int:
+        """Make ``model_set`` read model ``name`` from the stored pool set: link exactly the pages holding
+        its blocks (addSharedPage) and map each distinct block to its place(s) in the model
+        (addSharedMapping).  Returns the number of pages linked."""
+        from ..objects.builtin import FFMatrixBlock
+
+        t = self.index.tables[name].cpu()
+        R, C = self.index.shapes[name]
+        if not client.storage.has_set(db, model_set):
+            client.create_set(db, model_set, FFMatrixBlock)
+        places: Dict[int, list] = {}
+        for (r, c), b in zip(torch.cartesian_prod(torch.arange(t.shape[0]), torch.arange(t.shape[1])).tolist(),
+                             t.flatten().tolist()):
+            places.setdefault(int(b), []).append((r, c))
+        pages = sorted({self.stored_pages[b] for b in places})
+        for p in pages:
+            client.add_shared_page(db, model_set, FFMatrixBlock, db, pool_set, FFMatrixBlock, p)
+        client.add_shared_mapping(db, model_set, FFMatrixBlock, db, pool_set, FFMatrixBlock,
+                                  mapping={b: v if len(v) > 1 else v[0] for b, v in places.items()},
+                                  total_rows=R, total_cols=C)
+        return len(pages)
 
     def dedup_ratio(self) -> float:
         return self.stats["blocks_stored"] / max(1, self.stats["blocks_in"])
@@ -294,10 +428,96 @@ class DistributedBlockPool:
         return int(self.local.blocks.shape[0])
 
 
+class SharedInference:
+    """Batched inference of many deduplicated models, computing each shared column block ONCE:
+    ``y_m = W_m @ X^T`` for models m with identical geometry.  Column blocks whose pool ids agree across
+    every model (the word2vec/text-classifier case: fine-tuned copies of one embedding table) form one
+    common panel; ``P = W_common @ X_common^T`` is one MFMA GEMM for all models, and each model adds only
+    its private columns' GEMM on top (``accumulate`` epilogue), so the work and the HBM traffic scale with
+    the DISTINCT bytes, not with models x model size.  The reference runs FFTransposeMult + FFAggMatrix
+    per model over shared pages (TestWord2VecWithDeduplication.cc:96-152) and re-reads the shared blocks
+    every time."""
+
+    def __init__(self, tables: Dict[str, torch.Tensor], shapes: Dict[str, Tuple[int, int]], fetch, br: int, bc: int):
+        self.names = list(tables)
+        T = torch.stack([tables[n].cpu() for n in self.names])          # [M, nbr, nbc]
+        assert len({shapes[n] for n in self.names}) == 1, "SharedInference needs models of one shape"
+        self.R, self.C = shapes[self.names[0]]
+        self.br, self.bc = br, bc
+        self.nbr, self.nbc = T.shape[1], T.shape[2]
+        common = (T == T[0:1]).all(0).all(0)                              # [nbc]
+        self.common_cols = common.nonzero().flatten()
+        self.priv_cols = (~common).nonzero().flatten()
+
+        def panel(t: torch.Tensor, cols: torch.Tensor) -> torch.Tensor:
+            ids = t[:, cols].flatten()
+            blks = fetch(ids)                                              # [nbr*len(cols), br, bc]
+            return from_blocks(blks, self.nbr, cols.numel(), self.nbr * br, cols.numel() * bc).contiguous()
+
+        self.w_common = panel(T[0], self.common_cols) if self.common_cols.numel() else None
+        # private panels stacked [M, R, kp]: every model's private columns scored by ONE batched GEMM
+        self.w_priv = torch.stack([panel(T[i], self.priv_cols) for i in range(len(self.names))]) \
+            if self.priv_cols.numel() else None
+        dev = (self.w_common if self.w_common is not None else self.w_priv).device
+        self.common_runs = _runs(self.common_cols.tolist())
+        self.priv_runs = _runs(self.priv_cols.tolist())
+        self.common_cols, self.priv_cols = self.common_cols.to(dev), self.priv_cols.to(dev)
+
+    def panel_bytes(self) -> int:
+        ps = [p for p in (self.w_common, self.w_priv) if p is not None]
+        return sum(p.numel() * p.element_size() for p in ps)
+
+    def _xpart(self, X: torch.Tensor, cols: torch.Tensor, runs) -> list:
+        """(panel column offset, X column block view) per contiguous run of column blocks: zero-copy strided
+        views of X (the GEMM takes any K-contiguous row stride); many short runs fall back to one gather."""
+        if len(runs) <= 4:
+            out, off = [], 0
+            for c0, c1 in runs:
+                out.append((off, X[:, c0 * self.bc: c1 * self.bc]))
+                off += (c1 - c0) * self.bc
+            return out
+        g = X.reshape(X.shape[0], self.nbc, self.bc).index_select(1, cols).reshape(X.shape[0], -1).contiguous()
+        return [(0, g)]
+
+    def run(self, X: torch.Tensor) -> Dict[str, torch.Tensor]:
+        """X [B, C] -> {model: [R, B] f32} (rows beyond R of the padded row blocks dropped)."""
+        from .. import ops
+
+        ref = self.w_common if self.w_common is not None else self.w_priv
+        X = X.to(ref.dtype)
+        if X.shape[1] != self.nbc * self.bc:
+            X = torch.nn.functional.pad(X, (0, self.nbc * self.bc - X.shape[1]))
+        P = None
+        if self.w_common is not None:
+            for off, xv in self._xpart(X, self.common_cols, self.common_runs):
+                wv = self.w_common[:, off: off + xv.shape[1]]
+                P = ops.gemm_nt(wv, xv, P, ops.BIAS_MAT if P is not None else ops.BIAS_NONE, out_dtype=torch.float32)
+        if self.w_priv is None:
+            return {n: P[: self.R] for n in self.names}
+        M = self.w_priv.shape[0]
+        Y = P
+        for off, xv in self._xpart(X, self.priv_cols, self.priv_runs):
+            wv = self.w_priv[:, :, off: off + xv.shape[1]]
+            xb = xv.unsqueeze(0).expand(M, -1, -1)            # batch stride 0: one X panel for every model
+            Y = ops.gemm_nt(wv, xb, Y, ops.BIAS_MAT if Y is not None else ops.BIAS_NONE, out_dtype=torch.float32)
+        return {n: Y[i, : self.R] for i, n in enumerate(self.names)}
+
+
+def _runs(cols) -> list:
+    """Sorted column-block ids -> [(start, end)) contiguous runs."""
+    out = []
+    for c in cols:
+        if out and out[-1][1] == c:
+            out[-1][1] = c + 1
+        else:
+            out.append([c, c + 1])
+    return [tuple(r) for r in out]
+
+
 def pages_touched(pool: BlockPool, pages: List[List[int]], name: str) -> int:
     page_of = {b: i for i, p in enumerate(pages) for b in p}
     return len({page_of[b] for b in pool.index.tables[name].flatten().tolist()})
 
 
-__all__ = ["TensorBlockIndex", "BlockPool", "DistributedBlockPool", "block_hashes", "lsh_signatures", "to_blocks", "from_blocks",
-           "pages_touched"]
+__all__ = ["TensorBlockIndex", "BlockPool", "DistributedBlockPool", "block_hashes", "block_hashes_reference",
+           "block_maxdiff", "SharedInference", "lsh_signatures", "to_blocks", "from_blocks", "pages_touched"]

@@ -142,9 +142,16 @@ class SharedLink:
         self.targets: Optional[torch.Tensor] = None   # [n, 4] int64 (block_row, block_col, total_rows, total_cols)
 
     def set_mapping(self, mapping: dict):
-        items = sorted(mapping.items())
-        self.keys = torch.tensor([k for k, _ in items], dtype=torch.int64)
-        self.targets = torch.tensor([list(v) for _, v in items], dtype=torch.int64).reshape(-1, 4)
+        """distinct block id -> target (block_row, block_col, total_rows, total_cols), or a list of targets
+        when one stored block appears at several places of the sharing model (exact dedup of repeated
+        blocks inside one model); keys are kept sorted with repeats."""
+        rows = []
+        for k, v in mapping.items():
+            for t in (v if v and isinstance(v, list) else [v]):
+                rows.append((int(k), *[int(x) for x in t]))
+        rows.sort()
+        self.keys = torch.tensor([r[0] for r in rows], dtype=torch.int64)
+        self.targets = torch.tensor([list(r[1:]) for r in rows], dtype=torch.int64).reshape(-1, 4)
 
     def batches(self, device=None) -> Iterator[RecordBatch]:
         sh = self.shared
@@ -170,16 +177,25 @@ class SharedLink:
         dev = ids.device
         keys, tg = self.keys.to(dev), self.targets.to(dev)
         if keys.numel() == 0:
-            found = torch.zeros(b.n, dtype=torch.bool, device=dev)
-            pos = torch.zeros(b.n, dtype=torch.int64, device=dev)
+            lo = torch.zeros(b.n, dtype=torch.int64, device=dev)
+            cnt = torch.zeros(b.n, dtype=torch.int64, device=dev)
         else:
-            pos = torch.searchsorted(keys, ids).clamp(max=keys.numel() - 1)
-            found = keys[pos] == ids
-        cols = dict(b.columns)
+            lo = torch.searchsorted(keys, ids, right=False)
+            cnt = torch.searchsorted(keys, ids, right=True) - lo
+        # a block with k targets becomes k rows; a block without one keeps a single (-1, -1) row
+        rep = cnt.clamp_min(1)
+        row = torch.repeat_interleave(torch.arange(b.n, device=dev), rep)
+        start = torch.cumsum(rep, 0) - rep
+        within = torch.arange(row.numel(), device=dev) - start.index_select(0, row)
+        found = cnt.index_select(0, row) > 0
+        tpos = (lo.index_select(0, row) + within).clamp(max=max(0, keys.numel() - 1))
+        out = b.take(row) if row.numel() != b.n or bool((cnt > 1).any()) else b
+        cols = dict(out.columns)
         for j, name in enumerate(("block_row", "block_col", "total_rows", "total_cols")):
             miss = -1 if j < 2 else 0
-            cols[name] = torch.where(found, tg[pos, j], torch.full_like(ids, miss))
-        return RecordBatch(cols, b.n, b.type)
+            val = tg[tpos, j] if keys.numel() else torch.zeros_like(row)
+            cols[name] = torch.where(found, val, torch.full_like(row, miss))
+        return RecordBatch(cols, int(row.numel()), b.type)
 
     def num_records(self) -> int:
         sh = self.shared

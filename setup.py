@@ -20,7 +20,7 @@ KDIR = os.path.join("netsdb_amd", "csrc", "kernels")
 RDIR = os.path.join("netsdb_amd", "csrc", "runtime")
 
 
-HIP_SOURCES = ("gemm.hip", "conv2d.hip", "rowops.hip", "strings.hip")
+HIP_SOURCES = ("gemm.hip", "conv2d.hip", "rowops.hip", "strings.hip", "dedup.hip")
 
 
 def hip_ext():

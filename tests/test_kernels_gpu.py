@@ -210,3 +210,29 @@ def test_lstm_elementwise_kernels():
     f, cp, i, g = (torch.randn(130, 77, device=DEV) for _ in range(4))
     _close(ops.lstm_two_sum(f, cp, i, g), f * cp + i * g, 1e-6)
     _close(ops.lstm_hidden(f, cp), f * torch.tanh(cp), 1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(500, 100, 100000), (500, 100, 900000), (64, 48, 65536)])
+def test_gemm_narrow_many_splits_wide_reducer(M, N, K):
+    """Small M x N with huge K (dedup scoring): many split-K slices reduced by the wide reducer."""
+    g = torch.Generator(device="cuda:0").manual_seed(5)
+    A = (torch.randn(M, K, device="cuda:0", generator=g) * 0.05).to(torch.bfloat16)
+    B = (torch.randn(N, K, device="cuda:0", generator=g) * 0.05).to(torch.bfloat16)
+    assert ops.gemm_splits(M, N, K) >= 8
+    bias = torch.randn(M, N, device="cuda:0")
+    C = ops.gemm_nt(A, B, bias, ops.BIAS_MAT, out_dtype=torch.float32)
+    ref = A.float() @ B.float().t() + bias
+    assert (C - ref).abs().max().item() / ref.abs().max().item() < 1e-4
+
+
+@pytest.mark.gpu
+def test_gemm_batched_broadcast_b_and_bias_matrix():
+    """Batched private-column scoring: B broadcast over the batch (stride 0), 2-D bias matrix broadcast."""
+    g = torch.Generator(device="cuda:0").manual_seed(6)
+    A = (torch.randn(5, 300, 20000, device="cuda:0", generator=g) * 0.05).to(torch.bfloat16)
+    X = (torch.randn(100, 20000, device="cuda:0", generator=g) * 0.05).to(torch.bfloat16)
+    P = torch.randn(300, 100, device="cuda:0")
+    Y = ops.gemm_nt(A, X.unsqueeze(0).expand(5, -1, -1), P, ops.BIAS_MAT, out_dtype=torch.float32)
+    ref = A.float() @ X.float().t() + P
+    assert (Y - ref).abs().max().item() / ref.abs().max().item() < 1e-4

@@ -209,3 +209,32 @@ def test_page_packing_algorithms():
     pool.add_model("b", m)
     pages = pool.pack_pages(2, algorithm="two_stage")
     assert sum(len(p) for p in pages) == pool.stats["blocks_stored"]
+
+
+def test_block_pool_growth_and_storage_link(tmp_path):
+    """BlockPool appends are amortised (capacity doubling, not a cat per insert), hashes match the
+    canonical reference, and a stored pool backs model sets through shared pages + block mappings
+    (a repeated block inside one model maps to all its places)."""
+    from netsdb_amd.client import PDBClient
+    from netsdb_amd.models import blocks
+
+    g = torch.Generator().manual_seed(4)
+    pool = dedup.BlockPool(8, 16, dtype=torch.float32)
+    shared = torch.randn(32, 64, generator=g)
+    models = {}
+    for i in range(6):
+        m = shared.clone()
+        m[:8, :16] = torch.randn(8, 16, generator=g)      # private block (0,0)
+        m[8:16, 16:32] = m[:8, 16:32]                     # block (1,1) repeats block (0,1)
+        models[f"m{i}"] = m
+        pool.add_model(f"m{i}", m)
+    assert pool.stats["grows"] <= 4
+    assert pool.stats["blocks_stored"] == 16 - 1 + 6 - 1 + 0  # 15 shared-distinct + 6 private, minus (0,0)
+    assert torch.equal(dedup.block_hashes(pool.blocks), dedup.block_hashes_reference(pool.blocks))
+    c = PDBClient(root=str(tmp_path))
+    page_of = pool.store(c, "dd", "pool", blocks_per_page=4)
+    assert len(page_of) == pool.stats["blocks_stored"]
+    for name, m in models.items():
+        npages = pool.link_model(c, "dd", f"set_{name}", "pool", name)
+        assert npages < len(set(page_of.values()))         # only the pages this model uses
+        torch.testing.assert_close(blocks.to_tensor(c, "dd", f"set_{name}"), m)
