@@ -624,7 +624,10 @@ int nsdb_gemm_splits(int M, int N, int K, int batch) {
   // >= 3/4 of the chip busy: a split's f32 slabs + reduce pass cost more than the idle CUs (1000x14588x1024:
   // 51 us + 24 us reduce with 2 splits vs 60 us unsplit)
   if (tiles < target && !(cfg && tiles >= 192)) {
-    splits = (target + tiles - 1) / tiles;
+    // round DOWN: tiles * splits stays within one wave of resident workgroups. Rounding up left a
+    // handful of workgroups for a second, nearly empty wave (6000x100x100k: 47 tiles x 11 splits =
+    // 517 WGs ran 456 us; x 10 = 470 WGs fit one wave)
+    splits = std::max(1, target / tiles);
     splits = std::min(splits, std::max(1, ksteps / 8));
   }
   if (splits > 1) {

@@ -498,6 +498,9 @@ class SharedInference:
         Y = P
         for off, xv in self._xpart(X, self.priv_cols, self.priv_runs):
             wv = self.w_priv[:, :, off: off + xv.shape[1]]
+            # a narrow private slice of X is compacted first (a 20 MB copy; the GEMM then streams B
+            # rows 200 KB apart instead of 2 MB apart: 266 vs 296 us at 12 x 500 x 100 x 100k)
+            xv = xv.contiguous() if xv.stride(0) > 2 * xv.shape[1] else xv
             xb = xv.unsqueeze(0).expand(M, -1, -1)            # batch stride 0: one X panel for every model
             Y = ops.gemm_nt(wv, xb, Y, ops.BIAS_MAT if Y is not None else ops.BIAS_NONE, out_dtype=torch.float32)
         return {n: Y[i, : self.R] for i, n in enumerate(self.names)}
