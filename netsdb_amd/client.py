@@ -27,6 +27,16 @@ from .storage.manager import DEFAULT_PAGE_SIZE, StorageManager
 from .utils.trace import Tracer
 
 
+def _placement_of(policy, world_size: int):
+    """(key kind, key name, world size) of a key-hash dispatch policy (Lachesis LambdaPolicy built by
+    selflearning.key_policy, description 'att:<field>' / 'method:<name>'), else None."""
+    desc = getattr(policy, "description", "") or ""
+    kind, _, name = desc.partition(":")
+    if getattr(policy, "name", None) == "lambda" and kind in ("att", "method") and name:
+        return (kind, name, int(world_size))
+    return None
+
+
 class PDBClient:
     def __init__(self, ctx: Optional[ClusterContext] = None, root: Optional[str] = None, device=None,
                  page_size: int = DEFAULT_PAGE_SIZE, pool_pages: int = 16, catalog_path: Optional[str] = None,
@@ -160,10 +170,16 @@ class PDBClient:
         else:
             parts = [None] * ws
         got = self.ctx.exchange(parts, template=batch)
+        placement = _placement_of(pol, ws)
+        if hasattr(uset, "note_placement"):
+            uset.note_placement(placement)
         n = 0
         for g in got:
             if g is not None and g.n:
-                uset.add_batch(g)
+                if hasattr(uset, "note_placement"):
+                    uset.add_batch(g, placement=placement)
+                else:
+                    uset.add_batch(g)
                 n += g.n
         return n
 

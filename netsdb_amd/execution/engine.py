@@ -101,6 +101,8 @@ class QueryEngine:
         self._plan_cache = {}
         self.cache_stats = {"tcap_compiles": 0, "tcap_cache_hits": 0}
         self.ooc_stats = {}
+        self.shuffle_count = 0            # all-to-all repartitions of join inputs (per job: stats["shuffles"])
+        self._copart = set()
         self.ooc_fraction = 0.25          # of the device budget: in-memory build / group-by / tuple-set limit
         self._spools = []
         self.last_tcap = None
@@ -145,7 +147,7 @@ class QueryEngine:
         """Stage-at-a-time execution driven by measured statistics (AdaptivePlanner): each finished
         stage's materialised output is measured (bytes, summed over ranks so every rank takes the same
         decisions) and costed for the next source selection."""
-        ap = AdaptivePlanner(atoms, self._scan_size, self.ctx.world_size, self.broadcast_threshold)
+        ap = AdaptivePlanner(atoms, self._scan_size, self.ctx.world_size, self.broadcast_threshold, self._copart)
         stages = []
         while ap.has_work():
             st = ap.next_stage()
@@ -193,11 +195,15 @@ class QueryEngine:
             return stats
         state = _JobState(comps)
         ooc0 = dict(self.ooc_stats)
+        self._copart = self._copartitioned_joins(atoms, comps) if self.ctx.distributed else set()
+        if self._copart:
+            stats["copartitioned_joins"] = sorted(self._copart)
+        shuffles0 = self.shuffle_count
         try:
             if self.adaptive:
                 pplan = self._run_adaptive(atoms, state, stats, job_name)
             else:
-                planner = Planner(self._scan_size, self.ctx.world_size, self.broadcast_threshold)
+                planner = Planner(self._scan_size, self.ctx.world_size, self.broadcast_threshold, self._copart)
                 pplan = planner.plan(atoms)
                 for st in pplan.stages:
                     self._timed_stage(st, state, stats, job_name)
@@ -211,7 +217,45 @@ class QueryEngine:
             stats["out_of_core"] = dict(stats.get("out_of_core", {}), **ooc)
         stats["seconds"] = time.perf_counter() - t0
         stats["tcap_atoms"] = len(atoms)
+        stats["shuffles"] = self.shuffle_count - shuffles0
         return stats
+
+    def _copartitioned_joins(self, atoms, comps) -> set:
+        """Joins whose two inputs are scans of sets already hash-placed by exactly the join key of their
+        side (Lachesis placement, ``UserSet.placement``) with this world size: the hash atom's key lambda
+        reads a field / method of the scanned object itself and the dispatcher hashed the same column
+        with the same function, so matching rows already share a rank.  The decision is agreed over all
+        ranks (min of the local flags) because a set's placement is tracked per rank."""
+        from ..selflearning import _key_of, _producer_map, _source_scan
+
+        by_out = _producer_map(atoms)
+        cands = []
+        for a in atoms:
+            if a["type"] != "JOIN":
+                continue
+            ok = True
+            for key in ("input", "input2"):
+                h = by_out.get(a[key]["name"])
+                if h is None or h["type"] not in ("HASHLEFT", "HASHRIGHT") or len(h["input"]["atts"]) != 1:
+                    ok = False
+                    break
+                scan = _source_scan(by_out, h["input"]["name"])
+                comp = comps.get(h["comp"])
+                k = _key_of(comp, by_out, h["input"]["name"], h["input"]["atts"][0], scan) if (scan and comp) else None
+                try:
+                    s = self.storage.get_set(scan["db"], scan["set"]) if scan else None
+                except KeyError:
+                    s = None
+                pl = getattr(s, "placement", None)
+                if k is None or k[0] not in ("att", "method") or pl is None or \
+                        (pl[0], pl[1], pl[2]) != (k[0], k[1], self.ctx.world_size):
+                    ok = False
+                    break
+            cands.append((a["output"]["name"], ok))
+        if not cands:
+            return set()
+        flags = [self.ctx.all_reduce_scalar(1.0 if ok else 0.0, "min") for _, ok in cands]
+        return {name for (name, _), f in zip(cands, flags) if f > 0.5}
 
     def _scan_size(self, atom) -> int:
         try:
@@ -310,6 +354,7 @@ class QueryEngine:
         ws = self.ctx.world_size
         if ws == 1:
             return batches
+        self.shuffle_count += 1
         merged = RecordBatch.concat(batches) if batches else None
         if merged is None:
             parts = [None] * ws

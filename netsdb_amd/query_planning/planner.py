@@ -49,10 +49,13 @@ class PhysicalPlan:
 
 class Planner:
     def __init__(self, size_of_scan: Callable[[dict], int], world_size: int = 1,
-                 broadcast_threshold: int = 2 << 30):
+                 broadcast_threshold: int = 2 << 30, copartitioned=()):
         self.size_of_scan = size_of_scan
         self.world_size = world_size
         self.broadcast_threshold = broadcast_threshold
+        # joins whose two inputs are already hash-placed by their join keys on every rank (Lachesis
+        # co-partitioning): built and probed where the rows are, no shuffle of either side
+        self.copartitioned = set(copartitioned)
 
     def plan(self, atoms: List[dict]) -> PhysicalPlan:
         producer: Dict[str, dict] = {}
@@ -87,6 +90,8 @@ class Planner:
                 bsz = right_sz if build == "right" else left_sz
                 if self.world_size == 1:
                     strat = "local"
+                elif a["output"]["name"] in self.copartitioned:
+                    strat = "copartitioned"
                 elif bsz <= self.broadcast_threshold:
                     strat = "broadcast"
                 else:
@@ -206,8 +211,9 @@ class AdaptivePlanner:
     PENALTY = 1000.0
 
     def __init__(self, atoms: List[dict], size_of_scan: Callable[[dict], int], world_size: int = 1,
-                 broadcast_threshold: int = 2 << 30):
+                 broadcast_threshold: int = 2 << 30, copartitioned=()):
         self.atoms = atoms
+        self.copartitioned = set(copartitioned)
         self.world_size = world_size
         self.broadcast_threshold = broadcast_threshold
         self.producer: Dict[str, dict] = {}
@@ -305,6 +311,8 @@ class AdaptivePlanner:
                     return None, info
                 if self.world_size == 1:
                     strat = "local"
+                elif name in self.copartitioned:
+                    strat = "copartitioned"
                 elif cost <= self.broadcast_threshold:
                     strat = "broadcast"
                 else:

@@ -39,6 +39,27 @@ CREATE TABLE IF NOT EXISTS stage_use (job_id INTEGER, db TEXT, set_name TEXT, si
 CREATE TABLE IF NOT EXISTS lineage (job_id INTEGER, src_db TEXT, src_set TEXT, dst_db TEXT, dst_set TEXT);
 CREATE TABLE IF NOT EXISTS placements (db TEXT, set_name TEXT, key_kind TEXT, key_name TEXT, t REAL);
 CREATE TABLE IF NOT EXISTS rewards (db TEXT, set_name TEXT, key_name TEXT, seconds REAL);
+-- job / stage / lambda / data history (the reference SelfLearningDB.cc schema, docs/selfLearning-database-schema)
+CREATE TABLE IF NOT EXISTS data (id INTEGER PRIMARY KEY AUTOINCREMENT, db TEXT, set_name TEXT, created_job_id INTEGER,
+                                 is_removed INTEGER DEFAULT 0, set_type TEXT, class_name TEXT, size INTEGER,
+                                 page_size INTEGER, placement_kind TEXT, placement_key TEXT, modification_time REAL,
+                                 UNIQUE(db, set_name));
+CREATE TABLE IF NOT EXISTS job (id INTEGER PRIMARY KEY AUTOINCREMENT, name TEXT UNIQUE, tcap TEXT, signature TEXT,
+                                initial_latency REAL, initial_job_instance_id INTEGER);
+CREATE TABLE IF NOT EXISTS job_instance (id INTEGER PRIMARY KEY AUTOINCREMENT, job_id INTEGER, status TEXT,
+                                         submit_time REAL, finish_time REAL, shuffles INTEGER, seconds REAL);
+CREATE TABLE IF NOT EXISTS job_stage (id INTEGER PRIMARY KEY AUTOINCREMENT, job_instance_id INTEGER, stage_id INTEGER,
+                                      source_type TEXT, sink_type TEXT, strategy TEXT, num_ops INTEGER,
+                                      rows_in INTEGER, seconds REAL, description TEXT);
+CREATE TABLE IF NOT EXISTS lambda (id INTEGER PRIMARY KEY AUTOINCREMENT, job_id INTEGER, lambda_type TEXT,
+                                   lambda_identifier TEXT, computation_name TEXT, lambda_name TEXT,
+                                   input_index INTEGER, UNIQUE(job_id, computation_name, lambda_identifier));
+CREATE TABLE IF NOT EXISTS data_job_stage (data_id INTEGER, job_stage_id INTEGER, index_in_inputs INTEGER,
+                                           data_type TEXT);
+-- trace workloads (tpchGenTrace.cc): partition schemes and the measured runs under each
+CREATE TABLE IF NOT EXISTS partition_scheme_stat (id INTEGER PRIMARY KEY, scheme TEXT);
+CREATE TABLE IF NOT EXISTS run_stat (id INTEGER PRIMARY KEY AUTOINCREMENT, job_name TEXT, partition_scheme_id INTEGER,
+                                     environment_id INTEGER, latency REAL, shuffles INTEGER);
 """
 
 
@@ -62,8 +83,31 @@ def _source_scan(atoms_by_out, ts: str) -> Optional[dict]:
     return None
 
 
-def _key_of(comp, atoms_by_out, key_col_ts: str, key_att: str):
-    """The lambda node that produced column ``key_att`` (APPLY atom) -> (kind, name) or None."""
+def _scan_origin(atoms_by_out, ts: str, col: str) -> Optional[dict]:
+    """The SCAN whose object column ``col`` of tuple set ``ts`` IS (carried unchanged, or renamed by
+    identity ``self`` lambdas of selections/joins), else None (a derived or joined value)."""
+    seen = set()
+    while ts and (ts, col) not in seen:
+        seen.add((ts, col))
+        a = atoms_by_out.get(ts)
+        if a is None or a["type"] == "JOIN":
+            return None
+        if a["type"] == "SCAN":
+            return a if a["output"]["atts"] and col == a["output"]["atts"][0] else None
+        outs = a["output"]["atts"]
+        if col not in outs:
+            return None
+        if a["type"] == "APPLY" and outs[-1] == col and col not in a["projection"]["atts"]:
+            if not str(a.get("lambda", "")).startswith("self") or len(a["input"]["atts"]) != 1:
+                return None
+            col = a["input"]["atts"][0]
+        ts = a["input"]["name"]
+    return None
+
+
+def _key_of(comp, atoms_by_out, key_col_ts: str, key_att: str, scan: Optional[dict] = None):
+    """The lambda node that produced column ``key_att`` (APPLY atom) -> (kind, name) or None.  With
+    ``scan``, the lambda must read the scanned object column itself (not a derived object)."""
     ts = key_col_ts
     seen = set()
     while ts and ts not in seen:
@@ -72,6 +116,9 @@ def _key_of(comp, atoms_by_out, key_col_ts: str, key_att: str):
         if a is None:
             return None
         if a["type"] == "APPLY" and a["output"]["atts"] and a["output"]["atts"][-1] == key_att:
+            if scan is not None and (len(a["input"]["atts"]) != 1 or
+                                     _scan_origin(atoms_by_out, a["input"]["name"], a["input"]["atts"][0]) is not scan):
+                return None
             node = comp.extract_lambdas().get(a["lambda"])
             if isinstance(node, AttAccess):
                 return ("att", node.field)
@@ -140,6 +187,88 @@ class SelfLearningDB:
                     self.conn.execute("INSERT INTO rewards VALUES (?,?,?,?)", (u["db"], u["set"], p[1], seconds))
             return jid
 
+    # ------------------------------------------------------------------ full job history
+    def upsert_data(self, db: str, set_name: str, uset=None, job_id: Optional[int] = None) -> int:
+        pl = getattr(uset, "placement", None) if uset is not None else None
+        typ = getattr(uset, "type", None)
+        with self.lock, self.conn:
+            self.conn.execute(
+                "INSERT INTO data(db, set_name, created_job_id, set_type, class_name, size, page_size, placement_kind,"
+                " placement_key, modification_time) VALUES (?,?,?,?,?,?,?,?,?,?) ON CONFLICT(db, set_name) DO UPDATE SET"
+                " size=excluded.size, placement_kind=excluded.placement_kind, placement_key=excluded.placement_key,"
+                " modification_time=excluded.modification_time, is_removed=0",
+                (db, set_name, job_id, type(uset).__name__ if uset is not None else None,
+                 typ.type_name() if typ is not None else None,
+                 int(uset.nbytes()) if uset is not None and hasattr(uset, "nbytes") else None,
+                 getattr(uset, "page_size", None), pl[0] if pl else None, pl[1] if pl else None, time.time()))
+            return self.conn.execute("SELECT id FROM data WHERE db=? AND set_name=?", (db, set_name)).fetchone()[0]
+
+    def record_instance(self, name: str, tcap: Optional[str], stats: dict, plan, comps, storage=None) -> int:
+        """One executed job: job (first latency), job_instance, job_stage per physical stage (with the
+        measured rows/seconds), lambda per computation lambda, data + data_job_stage for every scanned
+        and written set."""
+        import hashlib
+
+        secs = float(stats.get("seconds", 0.0))
+        sig = hashlib.sha1((tcap or "").encode()).hexdigest()[:16]
+        with self.lock, self.conn:
+            self.conn.execute("INSERT OR IGNORE INTO job(name, tcap, signature, initial_latency) VALUES (?,?,?,?)",
+                              (name, (tcap or "")[:20000], sig, secs))
+            jid = self.conn.execute("SELECT id FROM job WHERE name=?", (name,)).fetchone()[0]
+            cur = self.conn.execute("INSERT INTO job_instance(job_id, status, submit_time, finish_time, shuffles, seconds)"
+                                    " VALUES (?,?,?,?,?,?)", (jid, "finished", time.time() - secs, time.time(),
+                                                              int(stats.get("shuffles", 0)), secs))
+            iid = cur.lastrowid
+            self.conn.execute("UPDATE job SET initial_job_instance_id=COALESCE(initial_job_instance_id, ?) WHERE id=?",
+                              (iid, jid))
+            for cname, comp in (comps or {}).items():
+                try:
+                    lams = comp.extract_lambdas()
+                except Exception:
+                    continue
+                for lname, node in lams.items():
+                    field = getattr(node, "field", None) or getattr(node, "method", None)
+                    self.conn.execute("INSERT OR IGNORE INTO lambda(job_id, lambda_type, lambda_identifier,"
+                                      " computation_name, lambda_name, input_index) VALUES (?,?,?,?,?,?)",
+                                      (jid, type(node).__name__, lname, cname, field,
+                                       getattr(node, "input_index", None)))
+        timing = {st["id"]: st for st in stats.get("stages", [])}
+        for st in (plan.stages if plan is not None else []):
+            sink = st.sink or {}
+            t = timing.get(st.id, {})
+            with self.lock, self.conn:
+                sid = self.conn.execute(
+                    "INSERT INTO job_stage(job_instance_id, stage_id, source_type, sink_type, strategy, num_ops,"
+                    " rows_in, seconds, description) VALUES (?,?,?,?,?,?,?,?,?)",
+                    (iid, st.id, st.source.get("kind"), sink.get("kind"), sink.get("strategy"), len(st.ops),
+                     t.get("rows_in"), t.get("seconds"), st.describe())).lastrowid
+            ios = []
+            if st.source.get("kind") == "scan":
+                ios.append((st.source["atom"]["db"], st.source["atom"]["set"], 0, "in"))
+            if sink.get("kind") == "output":
+                ios.append((sink["atom"]["db"], sink["atom"]["set"], 0, "out"))
+            for d, sname, idx, kind in ios:
+                uset = None
+                if storage is not None:
+                    try:
+                        uset = storage.get_set(d, sname)
+                    except KeyError:
+                        uset = None
+                did = self.upsert_data(d, sname, uset, jid)
+                with self.lock, self.conn:
+                    self.conn.execute("INSERT INTO data_job_stage VALUES (?,?,?,?)", (did, sid, idx, kind))
+        return iid
+
+    def record_scheme(self, scheme_id: int, scheme: dict):
+        with self.lock, self.conn:
+            self.conn.execute("INSERT OR REPLACE INTO partition_scheme_stat VALUES (?,?)",
+                              (scheme_id, json.dumps(scheme, sort_keys=True)))
+
+    def record_run(self, job_name: str, scheme_id: int, env_id: int, latency: float, shuffles: int):
+        with self.lock, self.conn:
+            self.conn.execute("INSERT INTO run_stat(job_name, partition_scheme_id, environment_id, latency, shuffles)"
+                              " VALUES (?,?,?,?,?)", (job_name, scheme_id, env_id, latency, shuffles))
+
     def record_placement(self, db: str, set_name: str, key: Tuple[str, str]):
         with self.lock, self.conn:
             self.conn.execute("INSERT INTO placements VALUES (?,?,?,?,?)", (db, set_name, key[0], key[1], time.time()))
@@ -165,7 +294,8 @@ class SelfLearningDB:
 
     def export(self) -> dict:
         return {t: [list(r) for r in self.conn.execute(f"SELECT * FROM {t}")]
-                for t in ("jobs", "stage_use", "lineage", "placements", "rewards")}
+                for t in ("jobs", "stage_use", "lineage", "placements", "rewards", "data", "job", "job_instance",
+                          "job_stage", "lambda", "data_job_stage", "partition_scheme_stat", "run_stat")}
 
 
 def key_policy(kind: str, name: str, type_=None) -> LambdaPolicy:
@@ -310,6 +440,35 @@ class DRLAdvisor(RuleBasedAdvisor):
             loss.backward()
             self.opt.step()
 
+    def fit_offline(self, samples: List[Tuple[str, str, str, float]], epochs: int = 200, batch: int = 32):
+        """Train from a recorded trace (tpchTraining.cc): ``samples`` = (db, set, key_name, cost) runs, cost
+        = the consumer jobs' latency (or any measured cost such as shuffles) under that placement.  Each
+        sample becomes (state of the set's candidate list, index of the key, -cost/scale)."""
+        torch = self.torch
+        costs = [c for *_, c in samples]
+        if not costs:
+            return 0
+        self.scale = max(1e-9, sum(costs) / len(costs))
+        for dbname, set_name, key_name, cost in samples:
+            cands = self.db.candidates(dbname, set_name)[: self.SLOTS]
+            names = [n for _, n, _ in cands]
+            if key_name not in names:
+                continue
+            self.replay.append((self.state(dbname, set_name, cands), names.index(key_name), -cost / self.scale))
+        self.replay = self.replay[-4096:]
+        if not self.replay:
+            return 0
+        for _ in range(epochs):
+            bt = [self.replay[self.rng.randrange(len(self.replay))] for _ in range(min(batch, len(self.replay)))]
+            S = torch.tensor([b[0] for b in bt], dtype=torch.float32)
+            A = torch.tensor([b[1] for b in bt])
+            R = torch.tensor([b[2] for b in bt], dtype=torch.float32)
+            loss = torch.nn.functional.mse_loss(self.q(S).gather(1, A[:, None])[:, 0], R)
+            self.opt.zero_grad()
+            loss.backward()
+            self.opt.step()
+        return len(self.replay)
+
     def save(self, path: str):
         self.torch.save({"q": self.q.state_dict(), "scale": self.scale}, path)
 
@@ -345,6 +504,8 @@ class SelfLearningHook:
                 uses = extract_uses(atoms, eng._last_comps, eng.last_plan)
                 secs = st.get("seconds", 0.0)
                 self.db.record_job(job_name, secs, uses)
+                self.db.record_instance(job_name, eng.last_tcap, st, eng.last_plan, eng._last_comps, client.storage)
+                self.last_stats = st
                 if isinstance(self.advisor, DRLAdvisor):
                     for u in uses:
                         p = self.db.current_placement(u["db"], u["set"])

@@ -219,6 +219,10 @@ class UserSet:
         self.persistent = persistent
         self.lock = threading.RLock()
         self.partition_key = None       # (computation, lambda) describing how the set is partitioned
+        # hash placement of the rows across ranks: (key kind, key name, world size) when every row came
+        # through a dispatch by that key (send_data with a key LambdaPolicy); None once anything else
+        # (round-robin dispatch, local adds, engine outputs) put rows here
+        self.placement = None
         self.stats = {"records": 0, "bytes": 0}
         self.shared_links: Dict[Tuple[str, str], SharedLink] = {}   # dedup: pages linked from shared sets
 
@@ -244,7 +248,19 @@ class UserSet:
             yield from ln.batches(device)
 
     # -------------------------------------------------------------- writes
-    def add_batch(self, batch: RecordBatch):
+    def note_placement(self, placement):
+        """A collective dispatch into this set (called on every rank, rows or not): an empty set takes the
+        dispatch's placement; a different placement on a non-empty set makes it unknown."""
+        if self.stats["records"] == 0 and not getattr(self, "_placed", False):
+            self.placement = placement
+        elif placement != self.placement:
+            self.placement = None
+        self._placed = True
+
+    def add_batch(self, batch: RecordBatch, placement="unknown"):
+        if placement == "unknown":
+            self.placement = None
+            self._placed = True
         if batch.n == 0:
             return
         if self.device is not None and batch.device != torch.device(self.device):
@@ -268,6 +284,8 @@ class UserSet:
                 self.manager.untrack(p)
             self.pages = []
             self.stats = {"records": 0, "bytes": 0}
+            self.placement = None
+            self._placed = False
             self.manager.buffer_manager.drop_set(self.set_id)
 
     # -------------------------------------------------------------- reads

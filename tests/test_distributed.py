@@ -427,3 +427,53 @@ def test_distributed_nested_columns():
     for r in res:
         assert r["gb"] == ref and r["gb_obj"] == ref
         assert r["top"] == T.reference_jaccard(cs, [2, 4, 6, 8], 5)
+
+
+def _lachesis_scenario(ctx, out_dir):
+    """tpchGenTrace -> tpchTraining -> placement: the trace runs Q12/Q03 under 4 partition schemes of
+    orders x lineitem, the DRL agent is fitted on the measured data movement, and the tables it then
+    places make Q12's orders-lineitem join co-partitioned (no shuffle of either side)."""
+    from netsdb_amd.client import PDBClient
+    from netsdb_amd.models import tpch, tpch_trace
+
+    data = tpch.generate(0.002, seed=3)
+    c = PDBClient(ctx=ctx, root=tempfile.mkdtemp(), broadcast_threshold=0)
+    tpch.load(c, "tpch", data)
+    c.enable_self_learning(learned="drl")
+    keys = {"orders": [("att", "o_orderkey"), ("att", "o_custkey")],
+            "lineitem": [("att", "l_orderkey"), ("att", "l_partkey")]}
+    schemes = tpch_trace.partition_schemes(["orders", "lineitem"], keys)
+    runs = tpch_trace.gen_trace(c, "tpch", data, schemes, queries=("q12", "q03"))
+    adv, samples = tpch_trace.train_advisor(c, "tpch", cost="shuffles")
+    picks = {}
+    for t in ("orders", "lineitem"):
+        c.remove_set("tpch", t)
+        c.create_set("tpch", t, tpch.TABLES[t], policy="auto")
+        picks[t] = c.policies[("tpch", t)].description
+        c.send_data("tpch", t, tpch.to_batch(t, data[t]))
+    got = tpch.q12(c, "tpch")
+    st = c.learning.last_stats
+    hist = {tb: c.learning.db.conn.execute(f"SELECT COUNT(*) FROM {tb}").fetchone()[0]
+            for tb in ("job", "job_instance", "job_stage", "lambda", "data", "data_job_stage", "run_stat")}
+    return {"runs": runs, "picks": picks, "q12": got, "copart": st.get("copartitioned_joins", []),
+            "shuffles": st.get("shuffles"), "hist": hist}
+
+
+@pytest.mark.timeout(600)
+def test_distributed_learned_placement_skips_join_shuffle():
+    from netsdb_amd.models import tpch
+
+    data = tpch.generate(0.002, seed=3)
+    ref = sorted(tpch.reference("q12", data), key=lambda x: x["l_shipmode"])
+    for r in _run("_lachesis_scenario"):
+        by = {}
+        for row in r["runs"]:
+            by.setdefault(row["scheme"], {})[row["job"]] = row
+        # scheme 0 = (o_orderkey, l_orderkey): Q12's join is co-partitioned, the others shuffle both sides
+        assert by[0]["q12"]["shuffles"] == 0 and by[0]["q12"]["copartitioned"]
+        assert all(by[s]["q12"]["shuffles"] == 2 for s in (1, 2, 3))
+        assert r["picks"] == {"orders": "att:o_orderkey", "lineitem": "att:l_orderkey"}
+        assert r["copart"] and r["shuffles"] == 0
+        assert [(x["l_shipmode"], x["high_line_count"], x["low_line_count"]) for x in r["q12"]] == \
+            [(x["l_shipmode"], x["high_line_count"], x["low_line_count"]) for x in ref]
+        assert all(v > 0 for v in r["hist"].values()), r["hist"]
