@@ -323,7 +323,13 @@ template <int V>
 __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   constexpr int HALF = 128 * 128;            // bytes of one half-tile (128 rows x 64 bf16)
   constexpr int BUF = 4 * HALF;              // one K-tile
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  // RING (variant 10): the 160 KiB LDS as a ring of 10 half-tile slots. Half-tile h = 4u + q (staging
+  // order q: B0, A0, B1, A1 of k-tile u) lives in slot h % 10 and is staged at phase P = h - 9 (P = 4u' + j
+  // counts phases), so 5 half-tiles (80 KiB) stay in flight across the barriers instead of 3: the
+  // slot restaged at phase P held half-tile P - 1, the same WAR distance as the 2-buffer schedule.
+  constexpr bool RING = (V == 10);
+  constexpr int NRING = 10;
+  __shared__ __attribute__((aligned(16))) char smem[RING ? NRING * HALF : 2 * BUF];
 
   const int ntiles = p.tiles_m * p.tiles_n;
   const int wg = xcd_remap(blockIdx.x, ntiles * p.splits);
@@ -379,7 +385,7 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
     if constexpr (V == 4) return;
     const int k = kbeg + u * BK + kc;
     const bool kin = k < kend;
-    char* dst = smem + buf * BUF + slot * HALF;
+    char* dst = RING ? smem + buf * HALF : smem + buf * BUF + slot * HALF;   // RING: buf = ring slot
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int ro = roff[slot][i];
@@ -430,6 +436,45 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
     if constexpr (V != 1) __builtin_amdgcn_s_setprio(0);
     NSDB_BARRIER();
   };
+  // RING: half-tile h = 4u + q, q = 0 B0, 1 A0, 2 B1, 3 A1 (slot ids A0=0, A1=1, B0=2, B1=3)
+  auto stage_h = [&](int h) {
+    constexpr int slot_of[4] = {2, 0, 3, 1};
+    stage(h % NRING, slot_of[h & 3], h >> 2);
+  };
+  auto ring_base = [&](int u, int q) { return smem + ((4 * u + q) % NRING) * HALF; };
+  auto readA_r = [&](const char* base) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) af[mi][kk] = read_frag(base, wr * 64 + mi * 16 + (lane & 15), kk * 4 + (lane >> 4));
+  };
+  auto readB_r = [&](const char* base, bf16x8 (&bq)[2][2]) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) bq[ni][kk] = read_frag(base, wc * 32 + ni * 16 + (lane & 15), kk * 4 + (lane >> 4));
+  };
+  auto ktile_ring = [&](int u) {
+    // j0: (0,0) reads B0, A0 of u; stages h = 4u+9 (A0 of u+2)
+    readB_r(ring_base(u, 0), b0);
+    __builtin_amdgcn_sched_barrier(0);
+    readA_r(ring_base(u, 1));
+    stage_h(4 * u + 9);
+    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");   // B0 reads retired before the barrier
+    mma(0, 0, b0);
+    // j1: (0,1) reads B1; stages B1 of u+2 (into B0(u)'s slot, read in j0)
+    readB_r(ring_base(u, 2), b1);
+    stage_h(4 * u + 10);
+    mma(0, 1, b1);
+    // j2: (1,1) reads A1; stages A1 of u+2
+    readA_r(ring_base(u, 3));
+    stage_h(4 * u + 11);
+    mma(1, 1, b1);
+    // j3: (1,0) from registers; stages B0 of u+3; retires k-tile u+1 (5 half-tiles stay in flight)
+    stage_h(4 * u + 12);
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    mma(1, 0, b0);
+  };
   // one K-tile u held in buffer `cur` (u+1 in cur^1)
   auto ktile = [&](int cur, int u) {
     // j0: quadrant (0,0); reads B0 then A0; stages A1 of u+1
@@ -457,6 +502,15 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
     mma(1, 0, b0);
   };
 
+  if constexpr (RING) {
+    // prologue: half-tiles 0..8 (tile 0, tile 1, B0 of tile 2); tile 0 complete when <= 10 ops remain
+#pragma unroll
+    for (int h = 0; h < 9; ++h) stage_h(h);
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    NSDB_BARRIER();
+    if (wr == 1) NSDB_BARRIER();
+    for (int u = 0; u < nk; ++u) ktile_ring(u);
+  } else {
   // prologue: tile 0 (4 halves) + B0, A0, B1 of tile 1; tile 0 complete when <= 6 ops remain
   stage(0, 2, 0); stage(0, 0, 0); stage(0, 3, 0); stage(0, 1, 0);
   stage(1, 2, 1); stage(1, 0, 1); stage(1, 3, 1);
@@ -469,9 +523,165 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
     ktile(1, 2 * it + 1);
     if constexpr (V == 5) skip_reads = true;
   }
+  }
   if (V != 3 && wr == 0) NSDB_BARRIER();            // re-align the groups
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // trailing zero-fill DMAs land before LDS reuse
-  store_tile_lds<256, 256, 2, 4>(acc, smem, 2 * BUF, p, batch, split, m0, n0, tid, lane, wave);
+  store_tile_lds<256, 256, 2, 4>(acc, smem, (int)sizeof(smem), p, batch, split, m0, n0, tid, lane, wave);
+}
+
+// ---------------------------------------------------------------------------------------------
+// 256x256x64 "w4" kernel: 4 waves (256 threads, ONE wave per SIMD), 2(M) x 2(N), each wave owns a
+// 128x128 output block = 8x8 mfma_f32_16x16x32_bf16 tiles, 256 f32 accumulators per lane (AGPRs;
+// 512-register budget at one wave/SIMD).
+//
+//  * LDS per MFMA: each k32 sub-step a wave reads 8 A + 8 B fragments (16 ds_read_b128) for 64 MFMAs,
+//    2/3 of the LDS bytes per FLOP of the 8-wave 128x64-per-wave 8-phase kernel (24 reads / 64 MFMAs).
+//  * Register double buffer: fragment sets R0 (k32 sub-step s0) and R1 (s1). The reads of the next
+//    sub-step are issued between the MFMAs of the current one (sched_group_barrier interleave), so the
+//    MFMA stream never waits on an LDS round trip; one wave per SIMD hides its own latencies.
+//  * LDS ring of 5 operand slots (32 KiB = 256 rows x 64 bf16 each; 160 KiB): k-tile u's A in slot
+//    (2u)%5, its B in slot (2u+1)%5. One barrier per k-tile, between the two sub-steps' MFMA blocks:
+//        [s0 MFMAs on R0 | ds_read s1 -> R1]  lgkmcnt(0) vmcnt(8) s_barrier  (tile t+1 landed, every
+//        read of tile t retired)  stage B of t+2 and A of t+3 into tile t's two slots
+//        [s1 MFMAs on R1 | ds_read s0 of tile t+1 -> R0 | 16 LDS-DMA issues]
+//    so A is fetched 2 k-tiles ahead and B 1 k-tile ahead (64-96 KiB in flight per CU); vmcnt is never
+//    0 inside the loop (the youngest half-tile, A of t+2, stays in flight across the barrier).
+//  * DMA rows are 128 B (full cache lines); LDS image lane-linear per wave-instruction with the same
+//    XOR swizzle as read_frag applied to the per-lane SOURCE k (rule 21). Rows past M/N are zero-filled
+//    by the descriptor's range check; k past the split is redirected out of range.
+// ---------------------------------------------------------------------------------------------
+template <int V>
+__global__ void __launch_bounds__(256, 1) gemm_nt_256_w4_kernel(GemmParams p) {
+  constexpr int SLOT = 256 * 128;             // one operand's 256 rows x 64 bf16
+  constexpr int NSLOT = 5;
+  __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT];
+
+  const int ntiles = p.tiles_m * p.tiles_n;
+  const int wg = xcd_remap(blockIdx.x, ntiles * p.splits);
+  const int split = wg / ntiles, tile = wg % ntiles;
+  int tm, tn;
+  grouped_tile(tile, p.tiles_m, p.tiles_n, tm, tn);
+  const int batch = blockIdx.z;
+  const int m0 = tm * 256, n0 = tn * 256;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+
+  const int rows_a = min(256, p.M - m0), rows_b = min(256, p.N - n0);
+  const int kbeg = split * p.kchunk;
+  const int kend = min(p.K, kbeg + p.kchunk);
+  const int nk = max(0, (kend - kbeg + BK - 1) / BK);
+  const long long kseg = p.seg_k ? kbeg / p.seg_k : 0;
+  const int kb0 = (int)(kseg * p.seg_k);
+  const unsigned short* Ab = p.A + batch * p.sA + (long long)m0 * p.lda;
+  const unsigned short* Bb = p.B + batch * p.sB + (long long)n0 * p.ldb + kseg * p.seg_stride_b;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(Ab, (unsigned)((long long)rows_a * p.lda * 2));
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(Bb, (unsigned)((long long)rows_b * p.ldb * 2));
+
+  // DMA: wave-instruction i (0..7) of a slot fills rows i*32 + wave*8 + (lane>>3); physical 16-B slot
+  // lane&7 holds logical chunk (lane&7) ^ ((row>>1)&7), and (row>>1)&7 does not depend on i.
+  const int hr0 = wave * 8 + (lane >> 3);
+  const int kc = ((lane & 7) ^ ((hr0 >> 1) & 7)) * 8;
+  const unsigned a_lane = (unsigned)(hr0 * p.lda * 2 + kc * 2), b_lane = (unsigned)(hr0 * p.ldb * 2 + kc * 2);
+  const unsigned a_step = (unsigned)(32 * p.lda * 2), b_step = (unsigned)(32 * p.ldb * 2);
+
+  auto stage = [&](int op, int u) {
+    if constexpr (V == 4) return;
+    const int slot = (2 * u + op) % NSLOT;
+    char* dst = smem + slot * SLOT + wave * 8 * 128;
+    const int k = kbeg + u * BK;                        // this k-tile's first k (absolute)
+    const bool kin = k + kc < kend;
+    const unsigned base = op == 0 ? a_lane + (unsigned)k * 2 : b_lane + (unsigned)(k - kb0) * 2;
+    const unsigned step = op == 0 ? a_step : b_step;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const unsigned voff = kin ? base + i * step : (unsigned)OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(op == 0 ? ra : rb, (lds_void*)(dst + i * 32 * 128), 16, (int)voff, 0, 0, 0);
+    }
+  };
+
+  auto stage_one = [&](int op, int u, int i) {
+    if constexpr (V == 4) return;
+    const int slot = (2 * u + op) % NSLOT;
+    char* dst = smem + slot * SLOT + wave * 8 * 128 + i * 32 * 128;
+    const int k = kbeg + u * BK;
+    const bool kin = k + kc < kend;
+    const unsigned voff = kin ? (op == 0 ? a_lane + (unsigned)k * 2 + i * a_step : b_lane + (unsigned)(k - kb0) * 2 + i * b_step)
+                              : (unsigned)OOB;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(op == 0 ? ra : rb, (lds_void*)dst, 16, (int)voff, 0, 0, 0);
+  };
+
+  // Fragment reads: row = w*128 + f*16 + (lane&15), (row>>1)&7 = ((lane&15)>>1); f adds 2 KiB (imm offset).
+  const int rl = lane & 15, sw = (rl >> 1) & 7;
+  const int off_s0 = rl * 128 + (((lane >> 4)) ^ sw) * 16;
+  const int off_s1 = rl * 128 + ((4 + (lane >> 4)) ^ sw) * 16;
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 a0[8], b0[8], a1[8], b1[8];
+
+  auto read_set = [&](int u, int off, bf16x8 (&af)[8], bf16x8 (&bq)[8]) {
+    const char* sa = smem + ((2 * u) % NSLOT) * SLOT + wr * 128 * 128 + off;
+    const char* sb = smem + ((2 * u + 1) % NSLOT) * SLOT + wc * 128 * 128 + off;
+#pragma unroll
+    for (int f = 0; f < 8; ++f) {
+      af[f] = *reinterpret_cast<const bf16x8*>(sa + f * 2048);
+      bq[f] = *reinterpret_cast<const bf16x8*>(sb + f * 2048);
+    }
+  };
+  // 64 MFMAs on (af, bq) with the 16 fragment reads of the next sub-step (B first: the next block's
+  // first row of MFMAs needs every B fragment) interleaved 1 per 2 MFMAs over the first 32, and, with
+  // DMA, 16 LDS-DMA issues interleaved 1 per 4 MFMAs. The MFMAs are inline asm with the accumulator pinned to AGPRs ("+a", in place): the
+  // builtin's register-class heuristics at 512 registers copy every accumulator AGPR<->VGPR per
+  // iteration. Source order is the issue order (the asm is volatile); hipcc still inserts the
+  // counted lgkmcnt waits for the fragment registers the asm reads.
+  auto mma_rd = [&](const bf16x8 (&af)[8], const bf16x8 (&bq)[8], int u_next, int off_next, bf16x8 (&an)[8],
+                    bf16x8 (&bn)[8], bool dma, int t) {
+    const char* sa = smem + ((2 * u_next) % NSLOT) * SLOT + wr * 128 * 128 + off_next;
+    const char* sb = smem + ((2 * u_next + 1) % NSLOT) * SLOT + wc * 128 * 128 + off_next;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(af[i]), "v"(bq[j]));
+        // reads in the first half of the block (1 per 2 MFMAs): they retire long before the next
+        // block's first MFMA / the barrier's lgkmcnt(0)
+        if (i < 4 && (j & 1) == 1) {
+          const int r = i * 4 + (j >> 1);        // 0..15
+          if (r < 8) bn[r] = *reinterpret_cast<const bf16x8*>(sb + r * 2048);
+          else an[r - 8] = *reinterpret_cast<const bf16x8*>(sa + (r - 8) * 2048);
+        }
+        if (dma && (j & 3) == 3) {
+          const int g = i * 2 + (j >> 2);        // 0..15
+          if (g < 8) stage_one(1, t + 2, g);
+          else stage_one(0, t + 3, g - 8);
+        }
+      }
+  };
+
+  // prologue: A0 B0 A1 B1 A2 in flight; tile 0 complete when <= 3 half-tiles (24 ops) remain
+  stage(0, 0); stage(1, 0); stage(0, 1); stage(1, 1); stage(0, 2);
+  asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  NSDB_BARRIER();
+  read_set(0, off_s0, a0, b0);
+
+  for (int t = 0; t < nk; ++t) {
+    // s0: 64 MFMAs on R0 | the s1 reads of tile t -> R1
+    mma_rd(a0, b0, t, off_s1, a1, b1, false, t);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr (V != 6) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    NSDB_BARRIER();
+    // s1: 64 MFMAs on R1 | tile t+1's s0 reads -> R0 | DMA of B(t+2), A(t+3) into tile t's slots
+    mma_rd(a1, b1, t + 1, off_s0, a0, b0, true, t);
+  }
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");   // MFMA results -> AGPR reads (asm: no hazard padding)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // trailing zero-fill DMAs land before LDS reuse
+  __syncthreads();
+  store_tile_lds<256, 256, 2, 2>(acc, smem, NSLOT * SLOT, p, batch, split, m0, n0, tid, lane, wave);
 }
 
 // Epilogue of 4 consecutive reduced columns of one row (alpha, bias, activation, dropout, accumulate,
@@ -677,6 +887,12 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
     hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<0>, grid, dim3(512), 0, stream, p);
   else if (cfg == 10)
     hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<8>, grid, dim3(512), 0, stream, p);
+  else if (cfg == 14)   // 8-phase with a 10-slot half-tile LDS ring (5 half-tiles in flight)
+    hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<10>, grid, dim3(512), 0, stream, p);
+  else if (cfg == 12)   // 4-wave 128x128-per-wave kernel (one wave per SIMD)
+    hipLaunchKernelGGL(nsdb::gemm_nt_256_w4_kernel<0>, grid, dim3(256), 0, stream, p);
+  else if (cfg == 13)   // w4 diagnostic: no DMA issued (load-free upper bound, wrong results)
+    hipLaunchKernelGGL(nsdb::gemm_nt_256_w4_kernel<4>, grid, dim3(256), 0, stream, p);
   else if (cfg == 11)   // K-tiled operands (caller passes [K/64][ld][64] panels, lda/ldb = padded rows)
     hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<9>, grid, dim3(512), 0, stream, p);
   else if (cfg >= 3 && cfg <= 9) {   // diagnostic variants of the 8-phase kernel (timing only)
