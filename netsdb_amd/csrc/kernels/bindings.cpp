@@ -5,6 +5,10 @@
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
+#include <map>
+#include <mutex>
+#include <utility>
+
 extern "C" {
 int nsdb_gemm_splits(int M, int N, int K, int batch);
 void nsdb_gemm_force_config(int cfg);
@@ -12,6 +16,9 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
                       long long lda, long long ldb, long long ldc, long long sA, long long sB, long long sC,
                       long long sBias, int batch, int splits, int act, int bias_mode, int out_f32, float alpha,
                       float dropout, unsigned long long seed, int accumulate, long long seg_k, long long seg_stride_b, hipStream_t stream);
+int nsdb_gemm_nt_softmax(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, long long lda,
+                         long long ldb, long long ldc, int bias_mode, float alpha, int axis, void* part, int* cnt,
+                         int* flag, hipStream_t stream);
 int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* out, int N, int C, int H, int W,
                       int OC, int KH, int KW, int stride, int pad, int dil, int ldw, int act, int nchw_out,
                       int out_f32, hipStream_t stream);
@@ -119,6 +126,65 @@ torch::Tensor gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Ten
       (int)batch, s, (int)act, (int)bias_mode, out_f32 ? 1 : 0, (float)alpha, (float)dropout,
       (unsigned long long)seed, accumulate ? 1 : 0, 0, 0, cur_stream());
   check_rc(rc, "gemm_nt");
+  return C;
+}
+
+// Arrival counters + fallback flags of the fused softmax: zero between launches (the fix-up kernel re-zeroes
+// what a launch used), so one persistent buffer per (device, stream) — launches on one stream are ordered.
+std::mutex g_sm_mu;
+std::map<std::pair<int, hipStream_t>, torch::Tensor> g_sm_state;
+
+torch::Tensor softmax_state(const torch::Tensor& like, int64_t need, hipStream_t st) {
+  std::lock_guard<std::mutex> lk(g_sm_mu);
+  auto key = std::make_pair((int)like.get_device(), st);
+  auto it = g_sm_state.find(key);
+  if (it == g_sm_state.end() || it->second.numel() < need) {
+    auto t = torch::zeros({std::max<int64_t>(need, 4096)}, like.options().dtype(torch::kInt32));
+    g_sm_state[key] = t;
+    return t;
+  }
+  return it->second;
+}
+
+// C (f32 [M, N]) = softmax(alpha * A . B^T + bias) along axis 1 (every row of C) or 2 (every column), fused
+// into the GEMM epilogue (max-subtracted; cross-workgroup partials, see gemm.hip softmax_epilogue_8ph).
+torch::Tensor gemm_nt_softmax(torch::Tensor A, torch::Tensor B, c10::optional<torch::Tensor> bias, int64_t bias_mode,
+                              int64_t axis, c10::optional<torch::Tensor> out, double alpha) {
+  check_cuda(A, "A");
+  check_cuda(B, "B");
+  TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && B.scalar_type() == torch::kBFloat16, "A,B must be bf16");
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2, "A,B must be 2-D");
+  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1, "A,B must be K-contiguous");
+  TORCH_CHECK(axis == 1 || axis == 2, "axis must be 1 (rows) or 2 (columns)");
+  const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
+  TORCH_CHECK(B.size(1) == K && K % 8 == 0, "K mismatch or K % 8 != 0");
+  TORCH_CHECK(A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0, "row strides must be multiples of 8");
+  TORCH_CHECK(M < (1LL << 31) && N < (1LL << 31), "dims too large");
+  const float* bptr = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    check_cuda(*bias, "bias");
+    TORCH_CHECK(bias->scalar_type() == torch::kFloat32 && bias->is_contiguous() && bias->dim() == 1, "bias f32 1-D");
+    TORCH_CHECK(bias_mode == 1 || bias_mode == 2, "fused softmax takes a per-row (1) or per-column (2) bias");
+    TORCH_CHECK(bias->numel() == (bias_mode == 1 ? M : N), "bias length mismatch");
+    bptr = bias->data_ptr<float>();
+  }
+  torch::Tensor C;
+  if (out.has_value() && out->defined()) {
+    C = *out;
+    TORCH_CHECK(C.scalar_type() == torch::kFloat32 && C.dim() == 2 && C.size(0) == M && C.size(1) == N &&
+                C.stride(1) == 1, "out must be f32 [M, N] with unit column stride");
+  } else {
+    C = torch::empty({M, N}, A.options().dtype(torch::kFloat32));
+  }
+  const int64_t tm = (M + 255) / 256, tn = (N + 255) / 256;
+  auto part = torch::empty({tm * tn * 256 * 2}, A.options().dtype(torch::kFloat32));
+  const hipStream_t st = cur_stream();
+  auto state = softmax_state(A, std::max(tm, tn) + tm * tn, st);
+  int* cnt = state.data_ptr<int>();
+  const int rc = nsdb_gemm_nt_softmax(A.data_ptr(), B.data_ptr(), C.data_ptr<float>(), bptr, (int)M, (int)N, (int)K,
+                                      A.stride(0), B.stride(0), C.stride(0), (int)bias_mode, (float)alpha, (int)axis,
+                                      part.data_ptr(), cnt, cnt + std::max(tm, tn), st);
+  check_rc(rc, "gemm_nt_softmax");
   return C;
 }
 
@@ -453,6 +519,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dropout") = 0.0, py::arg("seed") = 0, py::arg("splits") = 0, py::arg("out") = py::none(),
         py::arg("accumulate") = false);
   m.def("gemm_splits", &gemm_splits);
+  m.def("gemm_nt_softmax", &gemm_nt_softmax, "softmax(alpha A.B^T + bias) fused into the GEMM epilogue");
   m.def("gemm_nt_ktiled", &gemm_nt_ktiled, "study: 8-phase GEMM over K-tiled [K/64][ld][64] operand panels");
   m.def("gemm_force_config", [](int64_t cfg) { nsdb_gemm_force_config((int)cfg); },
         "-1 auto, 0 = 128x128 tile, 1 = 256x256 tile (A/B testing)");

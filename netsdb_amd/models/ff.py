@@ -236,9 +236,15 @@ def create_output_set(client, db: str, name: str):
 
 
 def inference_unit(client, db: str, w1: str, wo: str, inputs: str, b1: str, bo: str, output: str,
-                   dropout_rate: float = 0.0, seed: int = 0) -> dict:
-    """SimpleFF.cc inference_unit: one hidden layer + softmax output (two jobs)."""
-    create_output_set(client, db, "yo")
+                   dropout_rate: float = 0.0, seed: int = 0, single_job: bool = False) -> dict:
+    """SimpleFF.cc inference_unit: one hidden layer + softmax output (two jobs, the exp'd scores materialised
+    in the intermediate set "yo" between them, as the reference does).
+
+    ``single_job=True`` submits the whole graph as ONE job with no "yo" set (FFOutputLayer and FFRowAggregate
+    read the FFTransposeBiasSum result directly): the fuser then lowers the output layer to one GEMM whose
+    epilogue computes the max-subtracted softmax (ops.gemm_nt_softmax), with no exp'd round trip through HBM."""
+    if not single_job:
+        create_output_set(client, db, "yo")
     create_output_set(client, db, output)
     t0 = time.perf_counter()
     readA, readB = FFMatrixBlockScanner(db, w1), FFMatrixBlockScanner(db, inputs)
@@ -256,6 +262,12 @@ def inference_unit(client, db: str, w1: str, wo: str, inputs: str, b1: str, bo: 
     bsum = FFTransposeBiasSum()
     bsum.set_input(0, agg1)
     bsum.set_input(1, FFMatrixBlockScanner(db, bo))
+    if single_job:
+        soft = FFOutputLayer()
+        soft.set_input(0, bsum)
+        soft.set_input(1, FFRowAggregate().set_input(bsum))
+        s = client.execute_computations(FFMatrixWriter(db, output).set_input(soft), job_name="inference-unit-fused")
+        return {"seconds": time.perf_counter() - t0, "jobs": [s]}
     s1 = client.execute_computations(FFMatrixWriter(db, "yo").set_input(bsum), job_name="inference-unit-intermediate")
     readF = FFMatrixBlockScanner(db, "yo")
     expsum = FFRowAggregate().set_input(readF)

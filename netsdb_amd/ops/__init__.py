@@ -102,6 +102,36 @@ def gemm_nt(A, B, bias=None, bias_mode=BIAS_NONE, act=ACT_NONE, out_dtype=torch.
     return v
 
 
+def gemm_nt_softmax(A, B, bias=None, bias_mode=BIAS_NONE, axis=1, alpha=1.0, out=None):
+    """softmax(alpha * A @ B^T + bias) along ``axis`` 1 (each row of the [M, N] result) or 2 (each column), f32.
+    On the GPU the normalisation is fused into the GEMM epilogue (max-subtracted, no exp'd round trip through
+    HBM); the CPU oracle is the same max-subtracted softmax in fp32."""
+    if _use_hip(A, B):
+        if bias is not None and bias.dtype != torch.float32:
+            bias = bias.float()
+        A = A.to(torch.bfloat16) if A.dtype != torch.bfloat16 else A
+        B = B.to(torch.bfloat16) if B.dtype != torch.bfloat16 else B
+        if A.stride(-1) != 1 or A.stride(-2) % 8 or A.shape[-1] % 8:
+            A = pad_k(A.contiguous())
+        if B.stride(-1) != 1 or B.stride(-2) % 8 or B.shape[-1] % 8:
+            B = pad_k(B.contiguous())
+        if A.shape[-1] != B.shape[-1]:
+            k = max(A.shape[-1], B.shape[-1])
+            A = torch.nn.functional.pad(A, (0, k - A.shape[-1])) if A.shape[-1] < k else A
+            B = torch.nn.functional.pad(B, (0, k - B.shape[-1])) if B.shape[-1] < k else B
+        return _ext.hip().gemm_nt_softmax(A, B, bias, int(bias_mode if bias is not None else 0), int(axis), out,
+                                          float(alpha))
+    v = torch.matmul(A.float(), B.float().transpose(-1, -2)) * alpha
+    if bias is not None:
+        b = bias.float()
+        v = v + (b.unsqueeze(-1) if bias_mode == BIAS_ROW else b.unsqueeze(-2))
+    y = torch.softmax(v, dim=-1 if axis == 1 else -2)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
 def gemm_nt_segmented(A, Bg, bias=None, bias_mode=BIAS_NONE, act=ACT_NONE, out_dtype=torch.bfloat16, dropout=0.0,
                       seed=0, out=None):
     """epilogue(A . Bcat^T) with Bcat [N, S*seg_k] held as an all-gathered [S, N, seg_k] chunk (rank s's K slab

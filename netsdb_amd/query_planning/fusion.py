@@ -117,6 +117,7 @@ def _replicate(engine, d: Dense) -> Dense:
 class Node:
     consumers_want_t: Optional[bool] = None
     value: Optional[Dense] = None
+    uses: int = 0              # graph consumers (the fused softmax needs its GEMM to have exactly one)
 
 
 class SourceNode(Node):
@@ -141,6 +142,8 @@ class MatmulNode(Node):
         self.dropout = 0.0
         self.seed = 0
         self.transpose_out = False
+        self.fuse_softmax = False      # set by the only consumer, a SoftmaxNode: normalise in the epilogue
+        self.softmax_fused = False     # the value holds softmax(scores), not exp(scores)
 
     def eval(self, engine) -> Dense:
         if self.value is not None:
@@ -201,7 +204,15 @@ class MatmulNode(Node):
             out = None
             if X.is_cuda and pc % 64 and pc >= 64:
                 out = torch.empty(pr, (pc + 63) // 64 * 64, dtype=odt, device=X.device)[:, :pc]
-            if phys_is_c:
+            if self.fuse_softmax and act == ops.ACT_EXP and self.dropout == 0.0 and mode != ops.BIAS_MAT \
+                    and X.is_cuda:
+                # exp(scores + b) / rowsum over the rows of this node's LOGICAL value (C, or C^T when
+                # transpose_out): the rows of phys when phys holds that value, else its columns
+                axis = 1 if phys_is_c != self.transpose_out else 2
+                phys = ops.gemm_nt_softmax(X, Y, bias_t, mode, axis=axis, out=out) if phys_is_c else \
+                    ops.gemm_nt_softmax(Y, X, bias_t, mode, axis=axis, out=out)
+                self.softmax_fused = True
+            elif phys_is_c:
                 phys = ops.gemm_nt(X, Y, bias_t, mode, act, out_dtype=odt, dropout=self.dropout, seed=self.seed,
                                    out=out)
             else:
@@ -440,11 +451,19 @@ class SoftmaxNode(Node):
 
     def __init__(self, x: Node):
         self.x = x
+        self.notes: Optional[List[str]] = None     # the fuser's fused-op list (records the epilogue fusion)
 
     def eval(self, engine) -> Dense:
         if self.value is None:
             self.x.consumers_want_t = False
+            if isinstance(self.x, MatmulNode) and self.x.value is None and self.x.uses == 1 and self.x.act == "exp":
+                self.x.fuse_softmax = True
             X = self.x.eval(engine)
+            if getattr(self.x, "softmax_fused", False):
+                self.value = X                      # normalised inside the GEMM epilogue
+                if self.notes is not None:
+                    self.notes.append("softmax_epilogue[gemm]")
+                return self.value
             if X.part == "cols":
                 X = _replicate(engine, X)
             # row-normalise reads any row stride: no K-padding copy of the [rows, labels] scores
@@ -761,8 +780,13 @@ class Fuser:
 
     def match(self, c: Computation) -> Optional[Node]:
         if id(c) in self.memo:
-            return self.memo[id(c)]
+            n = self.memo[id(c)]
+            if n is not None:
+                n.uses += 1
+            return n
         n = self._match(c)
+        if n is not None:
+            n.uses += 1
         self.memo[id(c)] = n
         return n
 
@@ -809,6 +833,7 @@ class Fuser:
                     and x.value is None:
                 x.bias, x.bias_along, x.act, x.dropout, x.seed = b, pat.bias_along, pat.act, pat.dropout, pat.seed
                 x.transpose_out = pat.transpose_out
+                x.uses -= 1                     # the epilogue join is absorbed into the GEMM, not a consumer
                 self.fused.append(f"epilogue[{name}]")
                 return x
             self.fused.append(f"bias_act[{name}]")
@@ -818,7 +843,9 @@ class Fuser:
             if x is None:
                 return None
             self.fused.append(f"softmax[{name}]")
-            return SoftmaxNode(x)
+            node = SoftmaxNode(x)
+            node.notes = self.fused
+            return node
         if isinstance(c, JoinComp) and isinstance(pat, GateSum):
             ins = [self.match(x) for x in c.inputs]
             if any(x is None for x in ins):
@@ -877,6 +904,13 @@ class Fuser:
         # writers of a whole LSTM step (h_t) first: their stacked-gate lowering also produces c_t
         sinks = sorted(sinks, key=lambda s: 0 if (isinstance(s, WriteSet) and s.inputs and
                                                   isinstance(self.match(s.inputs[0]), HiddenOutNode)) else 1)
+        # match every sink's inputs before anything is evaluated, so Node.uses counts all consumers (a GEMM
+        # whose exp'd scores are also read elsewhere must not normalise them in its epilogue)
+        for s in sinks:
+            if not isinstance(s, WriteSet):
+                for inp in s.inputs:
+                    if inp is not None:
+                        self.match(inp)
         for s in sinks:
             if isinstance(s, WriteSet):
                 n = self.match(s.inputs[0])

@@ -1,6 +1,7 @@
 """FF output-layer GEMM (1000 x 14588 x 1000) epilogue cost breakdown, interleaved rounds in one process:
 bf16 out / f32 out / f32 + bias + exp (the in-bench softmax numerator, 64-padded ldc) / the same with the
-epilogue's global stores skipped (diag 1) and the row normaliser that follows it.
+epilogue's global stores skipped (diag 1), the row normaliser that follows it, the two together, and the
+softmax fused into the GEMM epilogue (ops.gemm_nt_softmax).
 
     python scripts/ab_gemm2_epi.py [--rounds 5] [--cfg 2]
 """
@@ -37,6 +38,9 @@ def main():
         "f32_bias_exp": lambda: ops.gemm_nt(X, W, bias, ops.BIAS_COL, ops.ACT_EXP, out_dtype=torch.float32, out=outp),
         "f32_bias_exp_nostore": "diag",
         "rownorm": lambda: ops.row_normalize(outp, out_dtype=torch.float32),
+        "exp_then_rownorm": lambda: ops.row_normalize(
+            ops.gemm_nt(X, W, bias, ops.BIAS_COL, ops.ACT_EXP, out_dtype=torch.float32, out=outp), out_dtype=torch.float32),
+        "fused_softmax": lambda: ops.gemm_nt_softmax(X, W, bias, ops.BIAS_COL, axis=1, out=outp),
     }
     res = {k: [] for k in variants}
     for _ in range(a.rounds):
