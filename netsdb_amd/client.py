@@ -222,6 +222,7 @@ class PDBClient:
             else:
                 meta["pages"] = s.page_meta()
             self.catalog.update_set_meta(db, name, meta)
+        self.catalog.checkpoint()
         return True
 
     flushData = flush_data

@@ -25,7 +25,7 @@ DEFAULT_PAGE_SIZE = 64 << 20
 class StorageManager:
     def __init__(self, root: Optional[str] = None, device=None, page_size: int = DEFAULT_PAGE_SIZE,
                  pool_pages: int = 16, device_budget: Optional[int] = None, rank: int = 0, io_workers: int = 2,
-                 read_ahead: int = 4, pinned_budget: Optional[int] = None):
+                 read_ahead: int = 4, pinned_budget: Optional[int] = None, page_pool_chunk: Optional[int] = None):
         self.root = root or tempfile.mkdtemp(prefix="netsdb_amd_")
         os.makedirs(self.root, exist_ok=True)
         self.device = torch.device(device) if device is not None else None
@@ -55,6 +55,14 @@ class StorageManager:
                 except (ValueError, OSError):
                     pinned_budget = 8 << 30
             self.host_tier = PinnedHostTier(self.device, pinned_budget)
+        # home-tier page arena: page columns are carved out of arena chunks by the native slab allocator
+        # (src/memory + bufferMgr page pool); page_pool_chunk=0 disables it
+        self.page_pool = None
+        if page_pool_chunk != 0:
+            from .devpool import DevicePagePool
+
+            chunk = page_pool_chunk or ((256 << 20) if self.home.type == "cuda" else (16 << 20))
+            self.page_pool = DevicePagePool(self.home, chunk, max_bytes=self.device_budget)
         self.device_bytes = 0
         # LRU of everything resident on the device tier (pages and dense panels), oldest first: eviction
         # pops from the front instead of scanning every page of every set (PageCache's LRU list)
@@ -118,6 +126,7 @@ class StorageManager:
                 self.device_bytes -= p.nbytes
             elif p.location == "pinned" and self.host_tier is not None:
                 self.host_tier.release(p.nbytes)
+            p.release_regions()
 
     # ----------------------------------------------------------- memory accounting / eviction
     def on_home(self, device) -> bool:
@@ -246,6 +255,7 @@ class StorageManager:
             "pool_loads": self.buffer_manager.loads,
             "io_work_completed": self.workers.completed,
             "pinned_tier": dict(self.host_tier.stats, used=self.host_tier.used) if self.host_tier is not None else None,
+            "page_pool": self.page_pool.summary() if self.page_pool is not None else None,
             **self.stats,
         }
 

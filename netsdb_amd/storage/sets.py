@@ -24,21 +24,38 @@ from ..objects.record import RecordBatch
 from .serde import deserialize_batch, serialize_batch
 
 class Page:
-    __slots__ = ("set", "page_no", "batch", "nbytes", "pins", "location", "dirty", "last_use", "n", "event")
+    __slots__ = ("set", "page_no", "batch", "nbytes", "pins", "location", "dirty", "last_use", "n", "event", "regions")
 
-    def __init__(self, uset: "UserSet", page_no: int, batch: RecordBatch):
+    def __init__(self, uset: "UserSet", page_no: int, batch: RecordBatch, to_pool: bool = False):
         self.set = uset
         self.page_no = page_no
-        self.batch: Optional[RecordBatch] = batch
         self.nbytes = batch.nbytes()
         self.n = batch.n
         self.pins = 0
         mgr = getattr(uset, "manager", None)
+        pool = getattr(mgr, "page_pool", None)
+        # pages arriving from the host (sendData / add_batch of host records, page reloads) are copied straight
+        # into slab-allocated regions of the manager's HBM page arena (storage/devpool.py); a page a device
+        # kernel just produced keeps its tensors (no extra device copy); on a CPU node every page is in the
+        # host arena
+        self.regions = []
+        if to_pool and pool is not None:
+            batch, self.regions = pool.adopt(batch, move=True)
+            batch = batch.to(uset.device)        # string / nested column objects (tensor columns: no-op)
         home = mgr.on_home(batch.device) if mgr is not None and hasattr(mgr, "on_home") else batch.device.type == "cuda"
+        if home and pool is not None and not self.regions and not pool.is_cuda:
+            batch, self.regions = pool.adopt(batch)
         self.location = "device" if home else "host"
         self.dirty = True
         self.last_use = 0
         self.event = None      # pinned tier: completion event of the page's D2H copy
+        self.batch: Optional[RecordBatch] = batch
+
+    def release_regions(self, events=()):
+        """Hand the page's arena regions back to the slab allocator (stream-ordered)."""
+        if self.regions:
+            self.set.manager.page_pool.release(self.regions, events)
+            self.regions = []
 
     def is_resident(self) -> bool:
         return self.batch is not None
@@ -51,6 +68,7 @@ class Page:
         tier = getattr(self.set.manager, "host_tier", None)
         if self.location == "device" and tier is not None and tier.admit(self.nbytes):
             self.batch, self.event = tier.offload(self.batch, self.nbytes)
+            self.release_regions((self.event,))          # reusable once the D2H copy has read them
             self.location = "pinned"
             return self.nbytes
         if self.location == "pinned":
@@ -66,6 +84,7 @@ class Page:
         view[: len(data)] = data
         bm.unpin(self.set.set_id, self.page_no, True, len(data))
         freed = self.nbytes if self.location == "device" else 0
+        self.release_regions()
         self.batch = None
         self.location = "pool"
         self.dirty = False
@@ -75,7 +94,8 @@ class Page:
         if self.location == "pinned":
             tier = self.set.manager.host_tier
             if device is not None and torch.device(device).type == "cuda":
-                self.batch = tier.fetch(self.batch, self.event, self.nbytes)   # async H2D, stream-ordered
+                pool = getattr(self.set.manager, "page_pool", None)
+                self.batch, self.regions = tier.fetch(self.batch, self.event, self.nbytes, pool=pool)
                 self.event = None
                 self.location = "device"
                 self.set.manager.track(self)
@@ -97,10 +117,15 @@ class Page:
         finally:
             bm.unpin(self.set.set_id, self.page_no, False, 0)
         b = deserialize_batch(data)
-        if device is not None and torch.device(device).type == "cuda":
-            b = b.to(device)
-        self.batch = b
         mgr = self.set.manager
+        if device is not None and torch.device(device).type == "cuda":
+            pool = getattr(mgr, "page_pool", None)
+            if pool is not None and mgr.on_home(device):
+                b, self.regions = pool.adopt(b, move=True)     # H2D straight into the page arena
+            b = b.to(device)
+        elif mgr.on_home(b.device) and getattr(mgr, "page_pool", None) is not None:
+            b, self.regions = mgr.page_pool.adopt(b)
+        self.batch = b
         self.location = "device" if mgr.on_home(b.device) else "host"
         self.dirty = False
         if self.location == "device":
@@ -263,7 +288,10 @@ class UserSet:
             self._placed = True
         if batch.n == 0:
             return
-        if self.device is not None and batch.device != torch.device(self.device):
+        pool = getattr(self.manager, "page_pool", None)
+        to_pool = (pool is not None and pool.is_cuda and self.device is not None and batch.device.type == "cpu"
+                   and self.manager.on_home(self.device))
+        if self.device is not None and batch.device != torch.device(self.device) and not to_pool:
             batch = batch.to(self.device)
         with self.lock:
             per_row = max(1, batch.nbytes() // max(1, batch.n))
@@ -272,7 +300,7 @@ class UserSet:
             rows_per_page = max(1, usable // per_row)
             for s in range(0, batch.n, rows_per_page):
                 part = batch.slice(s, min(batch.n, s + rows_per_page)) if batch.n > rows_per_page else batch
-                p = Page(self, len(self.pages), part)
+                p = Page(self, len(self.pages), part, to_pool=to_pool)
                 self.pages.append(p)
                 self.stats["records"] += part.n
                 self.stats["bytes"] += p.nbytes
@@ -340,6 +368,7 @@ class UserSet:
             p = Page.__new__(Page)
             p.set, p.page_no, p.batch, p.nbytes, p.n = self, page_no, None, nbytes, n
             p.pins, p.location, p.dirty, p.last_use = 0, "pool", False, 0
+            p.event, p.regions = None, []
             self.pages.append(p)
             self.stats["records"] += n
             self.stats["bytes"] += nbytes
