@@ -9,6 +9,8 @@ namespace nsdb {
 typedef __attribute__((ext_vector_type(8))) short bf16x8;   // 4 VGPRs, one MFMA A/B fragment
 typedef __attribute__((ext_vector_type(4))) float f32x4;    // 16x16 accumulator (4 regs)
 typedef __attribute__((address_space(3))) void lds_void;
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));   // 16-B raw buffer load / LDS store
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_SIGMOID = 2, ACT_EXP = 3, ACT_TANH = 4 };
 

@@ -213,8 +213,6 @@ __global__ void __launch_bounds__(256, 4) conv2d_igemm_kernel(ConvParams p) {
 //    fragment stores into 64 different planes were the limit of the gather kernel (~1 TB/s).
 // Preconditions (host-checked): stride 1, dil 1, pad 0, KW <= 8, W % 8 == 0, OW <= 112,
 // C*KH <= 4*CVR_NKS, C*(4+KH-1) <= CVR_ROWS.
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 constexpr int CVR_TR = 4, CVR_NKS = 6, CVR_CP = 288;                 // rows/block, max k-steps, copy stride (B)
 constexpr int CVR_ROWS = 30;                                           // max (c, r) input rows per group
 constexpr int CVR_ZERO = CVR_ROWS * 4 * CVR_CP;                        // zero block (A source past C*KH)

@@ -126,7 +126,7 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[TBM / WGM / 16
     if (wave >= g0 && wave < g0 + per_pass) {
       float* w = st + (wave - g0) * WTILE;
       if constexpr (TSL) {
-        static_assert(WC == 64, "TSL image: 16 chunks of 4 floats per row");
+        static_assert(WC % 64 == 0, "TSL image: 16-chunk swizzle groups of 4 floats");
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -965,6 +965,143 @@ __global__ void __launch_bounds__(256, 1) gemm_nt_256_w4_kernel(GemmParams p) {
   store_tile_lds<256, 256, 2, 2>(acc, smem, NSLOT * SLOT, p, batch, split, m0, n0, tid, lane, wave);
 }
 
+// ---------------------------------------------------------------------------------------------
+// "w4r": the 4-wave / 128x128-per-wave 256x256x64 tile (one wave per SIMD, 256 AGPR accumulators — the
+// structure hipBLASLt's Tensile kernel uses on gfx950: MT256x256x64, 256 threads, ~130 KiB LDS) with
+// REGISTER-staged global loads instead of LDS-DMA. The LDS-DMA variant (w4 above) paid ~60+ issue cycles per
+// buffer_load...lds (MI355X_MICROARCH 'LDS-DMA piece issue cost'): 16 per wave per k-tile next to 128 MFMAs
+// left the MFMA pipe idle; a global_load_dwordx4 + ds_write_b128 pair costs a fraction of that.
+//  * per k-tile t (k64 = sub-steps s0, s1, 64 MFMAs each on fragment sets R0 / R1):
+//      [s0: MFMAs(R0) | ds_read (t,s1) -> R1 | ds_write G (= tile t+1) -> L[(t+1)&1] | global_load t+2 -> G]
+//      lgkmcnt(0) + s_barrier   (tile t+1 in LDS; every read of tile t's s1 retired)
+//      [s1: MFMAs(R1) | ds_read (t+1,s0) -> R0 from L[(t+1)&1]]
+//    G = 16 x 16 B per thread (one k-tile of A and B: 512 rows x 128 B); its loads are issued one k-tile
+//    before their ds_write; L = 2 LDS buffers x 64 KiB. (Splitting G into k-halves written in both blocks —
+//    to spread the ~830 LDS write cycles — measured slower: 8192^3 1152 vs 1204 TF, FF layer 1 -20 %.)
+//  * global loads: 8 consecutive lanes read one row's 128 B (full cache line); the ds_write puts chunk c of
+//    row r at slot c ^ ((r >> 1) & 7) — the read_frag swizzle — so both the 8-lane write groups and the
+//    fragment reads are bank-conflict free.
+//  * MFMA operands swapped (transposed accumulator tiles, TSL store) — in-place asm MFMAs keep the
+//    accumulators in AGPRs (see w4).
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256, 1) gemm_nt_256_w4r_kernel(GemmParams p) {
+  constexpr int OPB = 256 * 128;             // one operand's 256 rows x 64 bf16
+  constexpr int BUFB = 2 * OPB;              // A + B of one k-tile
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUFB];
+
+  const int ntiles = p.tiles_m * p.tiles_n;
+  const int wg = xcd_remap(blockIdx.x, ntiles * p.splits);
+  const int split = wg / ntiles, tile = wg % ntiles;
+  int tm, tn;
+  grouped_tile(tile, p.tiles_m, p.tiles_n, tm, tn);
+  const int batch = blockIdx.z;
+  const int m0 = tm * 256, n0 = tn * 256;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+
+  const int rows_a = min(256, p.M - m0), rows_b = min(256, p.N - n0);
+  const int kbeg = split * p.kchunk;
+  const int kend = min(p.K, kbeg + p.kchunk);
+  const int nk = max(0, (kend - kbeg + BK - 1) / BK);
+  const long long kseg = p.seg_k ? kbeg / p.seg_k : 0;
+  const int kb0 = (int)(kseg * p.seg_k);
+  const unsigned short* Ab = p.A + batch * p.sA + (long long)m0 * p.lda;
+  const unsigned short* Bb = p.B + batch * p.sB + (long long)n0 * p.ldb + kseg * p.seg_stride_b;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(Ab, (unsigned)((long long)rows_a * p.lda * 2));
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(Bb, (unsigned)((long long)rows_b * p.ldb * 2));
+
+  // load i (0..15) of this thread: rows (i & 7) * 32 + tid / 8 of A (i < 8) or B, 16-B chunk tid % 8
+  const int lrow = tid >> 3, lch = tid & 7;
+  const unsigned a_off = (unsigned)(lrow * p.lda * 2 + lch * 16), b_off = (unsigned)(lrow * p.ldb * 2 + lch * 16);
+  const unsigned a_step = (unsigned)(32 * p.lda * 2), b_step = (unsigned)(32 * p.ldb * 2);
+  const int kcl = lch * 8;                   // this lane's k within the k-tile
+  // LDS image byte offset of load i: row r = (i & 7) * 32 + lrow, chunk lch -> r*128 + (lch ^ ((r>>1)&7))*16
+  const int w_off = lrow * 128 + ((lch ^ ((lrow >> 1) & 7)) * 16);    // (i & 7) * 32 rows add 4096 B, same swizzle
+
+  u32x4 g[16];
+  auto gload_one = [&](int u, int i) {
+    const int k = kbeg + u * BK;
+    const bool kin = k + kcl < kend;
+    const bool isa = i < 8;
+    const unsigned off = isa ? a_off + (unsigned)k * 2 + (i & 7) * a_step
+                             : b_off + (unsigned)(k - kb0) * 2 + (i & 7) * b_step;
+    g[i] = __builtin_amdgcn_raw_buffer_load_b128(isa ? ra : rb, kin ? (int)off : OOB, 0, 0);
+  };
+  auto gwrite_one = [&](int buf, int i) {
+    char* base = smem + buf * BUFB + (i < 8 ? 0 : OPB) + (i & 7) * 4096 + w_off;
+    *reinterpret_cast<u32x4*>(base) = g[i];
+  };
+
+  // fragment reads: row = w*128 + f*16 + (lane&15); (row>>1)&7 = ((lane&15)>>1)
+  const int rl = lane & 15, sw = (rl >> 1) & 7;
+  const int off_s0 = rl * 128 + (((lane >> 4)) ^ sw) * 16;
+  const int off_s1 = rl * 128 + ((4 + (lane >> 4)) ^ sw) * 16;
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 a0[8], b0[8], a1[8], b1[8];
+
+  auto read_set = [&](int buf, int off, bf16x8 (&af)[8], bf16x8 (&bq)[8]) {
+    const char* sa = smem + buf * BUFB + wr * 128 * 128 + off;
+    const char* sb = smem + buf * BUFB + OPB + wc * 128 * 128 + off;
+#pragma unroll
+    for (int f = 0; f < 8; ++f) {
+      af[f] = *reinterpret_cast<const bf16x8*>(sa + f * 2048);
+      bq[f] = *reinterpret_cast<const bf16x8*>(sb + f * 2048);
+    }
+  };
+  // 64 MFMAs (transposed tiles: B fragment first) with the next sub-step's 16 fragment reads (1 per 2 MFMAs
+  // over the first 32) and, in s0 blocks, the 16 ds_writes of the staged tile each followed by its refill load
+  auto block = [&](const bf16x8 (&af)[8], const bf16x8 (&bq)[8], int rbuf, int roff, bf16x8 (&an)[8], bf16x8 (&bn)[8],
+                   bool stage, int wbuf, int u_load) {
+    const char* sa = smem + rbuf * BUFB + wr * 128 * 128 + roff;
+    const char* sb = smem + rbuf * BUFB + OPB + wc * 128 * 128 + roff;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(bq[j]), "v"(af[i]));
+        if (i < 4 && (j & 1) == 1) {
+          const int r = i * 4 + (j >> 1);
+          if (r < 8) bn[r] = *reinterpret_cast<const bf16x8*>(sb + r * 2048);
+          else an[r - 8] = *reinterpret_cast<const bf16x8*>(sa + (r - 8) * 2048);
+        }
+        if (stage && (j & 3) == 3) {
+          const int q = i * 2 + (j >> 2);        // 0..15: write staged chunk q, then refill it
+          gwrite_one(wbuf, q);
+          gload_one(u_load, q);
+        }
+      }
+  };
+
+  // prologue: tile 0 -> L[0]; tile 1 in flight in G; tile 0's s0 fragments
+#pragma unroll
+  for (int i = 0; i < 16; ++i) gload_one(0, i);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) gwrite_one(0, i);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) gload_one(1, i);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  read_set(0, off_s0, a0, b0);
+
+  for (int t = 0; t < nk; ++t) {
+    const int cur = t & 1;
+    block(a0, b0, cur, off_s1, a1, b1, true, cur ^ 1, t + 2);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    NSDB_BARRIER();
+    block(a1, b1, cur ^ 1, off_s0, a0, b0, false, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  __syncthreads();
+  store_tile_lds<256, 256, 2, 2, true>(acc, smem, (int)sizeof(smem), p, batch, split, m0, n0, tid, lane, wave);
+}
+
 // Epilogue of 4 consecutive reduced columns of one row (alpha, bias, activation, dropout, accumulate,
 // f32 / bf16 store) shared by the split-K reducers.
 __device__ __forceinline__ void reduce_epilogue4(const GemmParams& p, int batch, long long MN, long long e, f32x4 s) {
@@ -1205,6 +1342,8 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
     hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<10>, grid, dim3(512), 0, stream, p);
   else if (cfg == 12)   // 4-wave 128x128-per-wave kernel (one wave per SIMD)
     hipLaunchKernelGGL(nsdb::gemm_nt_256_w4_kernel<0>, grid, dim3(256), 0, stream, p);
+  else if (cfg == 16)   // w4r: 4-wave 128x128-per-wave kernel, register-staged global loads
+    hipLaunchKernelGGL(nsdb::gemm_nt_256_w4r_kernel, grid, dim3(256), 0, stream, p);
   else if (cfg == 13)   // w4 diagnostic: no DMA issued (load-free upper bound, wrong results)
     hipLaunchKernelGGL(nsdb::gemm_nt_256_w4_kernel<4>, grid, dim3(256), 0, stream, p);
   else if (cfg == 11)   // K-tiled operands (caller passes [K/64][ld][64] panels, lda/ldb = padded rows)

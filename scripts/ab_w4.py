@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--check-only", action="store_true")
+    ap.add_argument("--scale-b", type=float, default=1.0, help="B ~ U(-1,1) * scale (FF W1 init: sqrt(3/features))")
     a = ap.parse_args()
     h = _ext.hip()
     cfgs = [int(c) for c in a.cfgs.split(",")]
@@ -29,7 +30,7 @@ def main():
         M, N, K = (int(x) for x in sh.split("x"))
         g = torch.Generator(device="cuda:0").manual_seed(0)
         A = torch.empty(M, K, device="cuda:0", dtype=torch.bfloat16).uniform_(-1, 1, generator=g)
-        B = torch.empty(N, K, device="cuda:0", dtype=torch.bfloat16).uniform_(-1, 1, generator=g)
+        B = (torch.empty(N, K, device="cuda:0").uniform_(-1, 1, generator=g) * a.scale_b).to(torch.bfloat16)
         rows = torch.randperm(M, device="cuda:0", generator=g)[:24].sort().values
         rows[-1] = M - 1
         ref = A[rows].float() @ B.float().t()
