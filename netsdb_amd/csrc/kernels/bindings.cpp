@@ -12,6 +12,7 @@
 extern "C" {
 int nsdb_gemm_splits(int M, int N, int K, int batch);
 void nsdb_gemm_force_config(int cfg);
+void nsdb_gemm_set_stamps(void* ptr);
 int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const float* bias, int M, int N, int K,
                       long long lda, long long ldb, long long ldc, long long sA, long long sB, long long sC,
                       long long sBias, int batch, int splits, int act, int bias_mode, int out_f32, float alpha,
@@ -519,6 +520,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dropout") = 0.0, py::arg("seed") = 0, py::arg("splits") = 0, py::arg("out") = py::none(),
         py::arg("accumulate") = false);
   m.def("gemm_splits", &gemm_splits);
+  m.def("gemm_set_stamps", [](int64_t ptr) { nsdb_gemm_set_stamps(reinterpret_cast<void*>(ptr)); },
+        "diagnostic: u64 [workgroups][64] buffer for the cfg-17 progress stamps (0 to unset)");
   m.def("gemm_nt_softmax", &gemm_nt_softmax, "softmax(alpha A.B^T + bias) fused into the GEMM epilogue");
   m.def("gemm_nt_ktiled", &gemm_nt_ktiled, "study: 8-phase GEMM over K-tiled [K/64][ld][64] operand panels");
   m.def("gemm_force_config", [](int64_t cfg) { nsdb_gemm_force_config((int)cfg); },

@@ -57,6 +57,7 @@ struct GemmParams {
   float2* sm_part;
   int* sm_cnt;
   int* sm_flag;
+  unsigned long long* stamps;   // diagnostic variant 12: per-workgroup real-time stamps every 32 k-tiles
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
@@ -792,7 +793,14 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
     ktile(0, 2 * it);
     ktile(1, 2 * it + 1);
     if constexpr (V == 5) skip_reads = true;
+    if constexpr (V == 12) {     // progress stamps (100 MHz real-time clock, comparable across CUs)
+      if (tid == 0 && (it & 15) == 0) p.stamps[(long long)wg * 64 + min(it >> 4, 62)] = __builtin_amdgcn_s_memrealtime();
+    }
   }
+  }
+  if constexpr (V == 12) {      // slot 63: the XCD this workgroup ran on (HW_REG_XCC_ID) and its CU id
+    if (tid == 0) p.stamps[(long long)wg * 64 + 63] =
+        ((unsigned long long)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 32) | (unsigned)__builtin_amdgcn_s_getreg((15 << 11) | 4);
   }
   if (V != 3 && wr == 0) NSDB_BARRIER();            // re-align the groups
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // trailing zero-fill DMAs land before LDS reuse
@@ -1223,6 +1231,10 @@ extern "C" {
 
 static int g_force_cfg = -1;  // -1 auto, 0 = 128x128, 1 = 256x256 2-stage, 2 = 256x256 8-phase (A/B testing)
 static int g_diag = 0;        // force_config / 100: kernel timing diagnostics (GemmParams::diag)
+static unsigned long long* g_stamps = nullptr;   // cfg 17 progress-stamp buffer ([wg][64] u64)
+
+
+void nsdb_gemm_set_stamps(void* ptr) { g_stamps = (unsigned long long*)ptr; }
 
 // Tile config: the 256x256 tile (1 block/CU) when both dims fill it and there is enough work.
 static int pick_cfg(int M, int N, int K, int batch) {
@@ -1287,7 +1299,7 @@ int nsdb_gemm_nt_softmax(const void* A, const void* B, float* C, const float* bi
   p.tiles_n = (N + 255) / 256;
   p.vec_ws = 0;
   p.vec_c = (ldc % 4 == 0 && (reinterpret_cast<uintptr_t>(C) & 15) == 0) ? 1 : 0;
-  p.softmax = axis; p.sm_part = (float2*)part; p.sm_cnt = cnt; p.sm_flag = flag;
+  p.softmax = axis; p.sm_part = (float2*)part; p.sm_cnt = cnt; p.sm_flag = flag; p.stamps = nullptr;
   const int tiles = p.tiles_m * p.tiles_n;
   if (axis == 1) hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<20>, dim3(tiles), dim3(512), 0, stream, p);
   else hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<21>, dim3(tiles), dim3(512), 0, stream, p);
@@ -1323,6 +1335,8 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
   p.seg_k = seg_k;
   p.seg_stride_b = seg_stride_b;
   p.softmax = 0; p.sm_part = nullptr; p.sm_cnt = nullptr; p.sm_flag = nullptr;
+  p.stamps = g_stamps;
+  if (g_force_cfg == 17 && g_stamps == nullptr) return -6;
   if (seg_k > 0 && (seg_k % p.kchunk != 0 || seg_k % nsdb::BK != 0)) return -5;   // a split must not cross a segment
   const int cfg = pick_cfg(M, N, K, batch);
   const int tbm = cfg ? 256 : nsdb::BM, tbn = cfg ? 256 : nsdb::BN;
@@ -1336,6 +1350,8 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
     hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<0>, grid, dim3(512), 0, stream, p);
   else if (cfg == 10)
     hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<8>, grid, dim3(512), 0, stream, p);
+  else if (cfg == 17)   // 8-phase with progress stamps (diagnostic: workgroup drift within a split)
+    hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<12>, grid, dim3(512), 0, stream, p);
   else if (cfg == 15)   // 8-phase, untransposed accumulators + LDS-staged epilogue store (A/B of the direct store)
     hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<11>, grid, dim3(512), 0, stream, p);
   else if (cfg == 14)   // 8-phase with a 10-slot half-tile LDS ring (5 half-tiles in flight)
