@@ -1,0 +1,59 @@
+"""The GEMM study kernels behind profiles/r2_gemm1_study and profiles/r2_epilogue are kept runnable and must
+stay bit-exact with the production 8-phase kernel (same k order, same fp32 accumulation): 4-wave 128x128
+per-wave kernels (LDS-DMA cfg 12, register-staged cfg 16), the 10-slot LDS ring (cfg 14), the untransposed
+LDS-staged epilogue (cfg 15) — plus the cfg-17 drift diagnostic (real-time stamps + XCD ids)."""
+import pytest
+import torch
+
+from netsdb_amd import _ext, ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(autouse=True)
+def _reset():
+    yield
+    _ext.hip().gemm_force_config(-1)
+
+
+@pytest.mark.parametrize("shape", [(777, 555, 4104), (300, 2000, 100000), (512, 512, 640)])
+@pytest.mark.parametrize("cfg", [12, 14, 15, 16])
+def test_study_kernels_bit_exact(shape, cfg):
+    M, N, K = shape
+    g = torch.Generator(device=DEV).manual_seed(5)
+    A = torch.empty(M, K, device=DEV).uniform_(-1, 1, generator=g).to(torch.bfloat16)
+    B = torch.empty(N, K, device=DEV).uniform_(-1, 1, generator=g).to(torch.bfloat16)
+    bias = torch.randn(N, device=DEV, generator=g)
+    h = _ext.hip()
+    h.gemm_force_config(2)
+    ref = ops.gemm_nt(A, B, bias, ops.BIAS_COL, ops.ACT_RELU, out_dtype=torch.float32)
+    h.gemm_force_config(cfg)
+    out = ops.gemm_nt(A, B, bias, ops.BIAS_COL, ops.ACT_RELU, out_dtype=torch.float32)
+    torch.testing.assert_close(out, ref, atol=0, rtol=0)
+
+
+def test_drift_diagnostic_stamps():
+    M, N, K = 1000, 1000, 64 * 16 * 40          # split-K 16, 40 k-tiles per split
+    A = torch.empty(M, K, device=DEV, dtype=torch.bfloat16).uniform_(-1, 1)
+    B = torch.empty(N, K, device=DEV, dtype=torch.bfloat16).uniform_(-1, 1)
+    h = _ext.hip()
+    st = torch.zeros(256 * 64, dtype=torch.int64, device=DEV)
+    h.gemm_set_stamps(st.data_ptr())
+    try:
+        h.gemm_force_config(2)
+        ref = ops.gemm_nt(A, B, out_dtype=torch.float32)
+        h.gemm_force_config(17)
+        out = ops.gemm_nt(A, B, out_dtype=torch.float32)
+        torch.cuda.synchronize()
+    finally:
+        h.gemm_set_stamps(0)
+    torch.testing.assert_close(out, ref, atol=0, rtol=0)
+    s = st.view(256, 64).cpu()
+    assert (s[:, 0] > 0).all()                          # every workgroup stamped its first iteration
+    xcc = (s[:, 63] >> 32).tolist()
+    assert all(0 <= x < 8 for x in xcc)
+    # the bijective XCD remap: workgroups of one split share an XCD id label (placement is observed, not
+    # guaranteed by contract — only check that the ids are consistent within most splits)
+    same = sum(len(set(xcc[g * 16:(g + 1) * 16])) == 1 for g in range(16))
+    assert same >= 12, xcc
