@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <map>
+#include <vector>
 #include <mutex>
 #include <utility>
 
@@ -13,6 +14,8 @@ extern "C" {
 int nsdb_gemm_splits(int M, int N, int K, int batch);
 void nsdb_gemm_force_config(int cfg);
 void nsdb_gemm_set_stamps(void* ptr);
+void nsdb_gemm_set_adapt(int on);
+int nsdb_gemm_adapt_state(int M, int N, int K, float* out);
 int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const float* bias, int M, int N, int K,
                       long long lda, long long ldb, long long ldc, long long sA, long long sB, long long sC,
                       long long sBias, int batch, int splits, int act, int bias_mode, int out_f32, float alpha,
@@ -520,6 +523,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dropout") = 0.0, py::arg("seed") = 0, py::arg("splits") = 0, py::arg("out") = py::none(),
         py::arg("accumulate") = false);
   m.def("gemm_splits", &gemm_splits);
+  m.def("gemm_set_adapt", [](int64_t on) { nsdb_gemm_set_adapt((int)on); },
+        "adaptive split-K K-partition across XCDs on/off (A/B)");
+  m.def("gemm_adapt_state", [](int64_t M, int64_t N, int64_t K) {
+        std::vector<float> buf(128, 0.f);
+        const int n = nsdb_gemm_adapt_state((int)M, (int)N, (int)K, buf.data());
+        TORCH_CHECK(n >= 0, "gemm_adapt_state: device copy failed");
+        std::vector<float> share(buf.begin(), buf.begin() + n), rate(buf.begin() + 64, buf.begin() + 64 + n);
+        return std::make_pair(share, rate);
+      }, "learned (shares, rates) of the adaptive split-K state for an (M, N, K) GEMM (empty if none)");
   m.def("gemm_set_stamps", [](int64_t ptr) { nsdb_gemm_set_stamps(reinterpret_cast<void*>(ptr)); },
         "diagnostic: u64 [workgroups][64] buffer for the cfg-17 progress stamps (0 to unset)");
   m.def("gemm_nt_softmax", &gemm_nt_softmax, "softmax(alpha A.B^T + bias) fused into the GEMM epilogue");

@@ -20,6 +20,8 @@
 //  * XCD-aware bijective workgroup remap (T1)
 #include "common.h"
 #include <algorithm>
+#include <map>
+#include <tuple>
 
 namespace nsdb {
 
@@ -58,7 +60,28 @@ struct GemmParams {
   int* sm_cnt;
   int* sm_flag;
   unsigned long long* stamps;   // diagnostic variant 12: per-workgroup real-time stamps every 32 k-tiles
+  struct AdaptState* adapt;     // split-K: launch-to-launch adaptive K partition (see AdaptState)
 };
+
+// Adaptive split-K partition (8-phase kernel, split-K launches). The splits of one GEMM run on different XCDs
+// (the bijective remap puts a split's tiles on one XCD) and the XCDs of one MI355X stream at persistently
+// different rates: per-split finish times of the FF layer-1 GEMM rank-correlate 0.76-0.94 from one launch to
+// the next and spread over ~40 k-tiles (~80 us) — a tail of idle CUs (profiles/r2_gemm1_study, drift and
+// persistence logs). Each launch reads the K share of every split from this state (equal shares on the first
+// launch), times its workgroups, and the last workgroup to finish turns the measured per-split rates
+// (median workgroup of the split; EMA over launches, shares clamped to [0.6, 1.4] of equal) into the shares
+// of the NEXT launch, which is stream-ordered after it. Every workgroup of a launch derives the same
+// contiguous K ranges from the same floats, so any shares give an exact partition of K: only the speed
+// depends on them. Release/acquire hand-off per cdna_hip_programming.md §6 G16.
+struct AdaptState {
+  float share[64];
+  float rate[64];
+  unsigned cnt;
+  unsigned pad[15];
+  unsigned long long t0[4096];
+  unsigned long long t1[4096];
+};
+constexpr int ADAPT_MAX_SPLITS = 64, ADAPT_MAX_WG = 4096;
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
@@ -614,8 +637,29 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   const int wr = wave >> 2, wc = wave & 3;
 
   const int rows_a = min(256, p.M - m0), rows_b = min(256, p.N - n0);
-  const int kbeg = split * p.kchunk;
-  const int kend = min(p.K, kbeg + p.kchunk);
+  AdaptState* const ad = (V == 0 && p.adapt != nullptr) ? p.adapt : nullptr;
+  int kbeg = split * p.kchunk;
+  int kend = min(p.K, kbeg + p.kchunk);
+  if (ad != nullptr) {
+    // this split's K range from the shares (identical arithmetic in every workgroup)
+    const int total = (p.K + BK - 1) / BK;
+    float acc_s = 0.f, tot_s = 0.f;
+    for (int g = 0; g < p.splits; ++g) {
+      const float sh = ad->share[g];
+      tot_s += sh;
+      if (g < split) acc_s += sh;
+    }
+    const float my_s = ad->share[split];
+    if (tot_s > 0.f) {
+      const int b0 = (int)((float)total * (acc_s / tot_s) + 0.5f);
+      const int b1 = split == p.splits - 1 ? total : (int)((float)total * ((acc_s + my_s) / tot_s) + 0.5f);
+      kbeg = min(b0, total) * BK;
+      kend = min(p.K, min(b1, total) * BK);
+    }
+  }
+  // start time kept in a register and stored with the finish time: a vector store (or load) pending at the
+  // loop entry would make the compiler's wait-count pass put vmcnt(0) waits into the counted-vmcnt loop
+  const unsigned long long t_begin = ad != nullptr ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const int nk = max(0, (kend - kbeg + BK - 1) / BK);
   const int niter = (nk + 1) >> 1;
 
@@ -804,6 +848,75 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   }
   if (V != 3 && wr == 0) NSDB_BARRIER();            // re-align the groups
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // trailing zero-fill DMAs land before LDS reuse
+  if (ad != nullptr) {
+    // finish time; the last workgroup of the launch derives the next launch's shares (the groups are
+    // re-aligned here, so the block-wide barriers below pair up)
+    // (the flag lives in the tile buffer, free here: a second __shared__ object makes the wait-count pass
+    // assume the loop's LDS-DMA writes may alias its ds_reads and put vmcnt(0) before every one of them)
+    int& adapt_last = reinterpret_cast<int*>(smem)[64 * 65];
+    if (tid == 0) {
+      ad->t0[wg] = t_begin;
+      ad->t1[wg] = __builtin_amdgcn_s_memrealtime();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      const unsigned c = __hip_atomic_fetch_add(&ad->cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      adapt_last = (c + 1 == (unsigned)(ntiles * p.splits)) ? 1 : 0;
+    }
+    __syncthreads();
+    if (adapt_last && wave == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      const int total = (p.K + BK - 1) / BK;
+      float acc_s = 0.f, tot_s = 0.f, my_s = 0.f;
+      for (int g = 0; g < p.splits; ++g) {
+        const float sh = ad->share[g];
+        tot_s += sh;
+        if (g < lane) acc_s += sh;
+        if (g == lane) my_s = sh;
+      }
+      float rate = 0.f;
+      if (lane < p.splits) {
+        int kt = (total + p.splits - 1) / p.splits;
+        if (tot_s > 0.f) {
+          const int b0 = (int)((float)total * (acc_s / tot_s) + 0.5f);
+          const int b1 = lane == p.splits - 1 ? total : (int)((float)total * ((acc_s + my_s) / tot_s) + 0.5f);
+          kt = b1 - b0;
+        } else {
+          kt = min(total, (lane + 1) * kt) - min(total, lane * kt);
+        }
+        // median duration of the split's workgroups: durations staged in LDS (row per split), rank select
+        float* dl = reinterpret_cast<float*>(smem) + lane * 65;
+        const int n = ntiles;          // <= 64 (host guard)
+        for (int i = 0; i < n; ++i) {
+          const int w = lane * ntiles + i;
+          dl[i] = (float)(long long)(__hip_atomic_load(&ad->t1[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
+                                     __hip_atomic_load(&ad->t0[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        }
+        float med = 1.f;
+        for (int i = 0; i < n; ++i) {
+          const float di = dl[i];
+          int rank = 0;
+          for (int j = 0; j < n; ++j) {
+            const float dj = dl[j];
+            rank += (dj < di || (dj == di && j < i)) ? 1 : 0;
+          }
+          if (rank == n / 2) med = fmaxf(di, 1.f);
+        }
+        const float r = (float)max(kt, 1) / med;
+        const float prev = ad->rate[lane];
+        rate = prev > 0.f ? 0.5f * prev + 0.5f * r : r;
+      }
+      float sum = rate;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+      if (lane < p.splits && sum > 0.f) {
+        const float eq = 1.f / (float)p.splits;
+        ad->rate[lane] = rate;
+        ad->share[lane] = fminf(fmaxf(rate / sum, 0.6f * eq), 1.4f * eq);   // readers renormalise
+      }
+      if (lane == 0) ad->cnt = 0u;     // ready for the next launch (stream-ordered after this one)
+    }
+    __syncthreads();                   // LDS scratch above is reused by the epilogue
+  }
   // the fused softmax turns acc into the final values in place; the common store then runs with a plain
   // (alpha 1, no bias/act/dropout, f32) epilogue
   // (variants 20 / 21: softmax along axis 1 / 2 — separate instantiations, one epilogue each: both in one
@@ -1232,6 +1345,27 @@ extern "C" {
 static int g_force_cfg = -1;  // -1 auto, 0 = 128x128, 1 = 256x256 2-stage, 2 = 256x256 8-phase (A/B testing)
 static int g_diag = 0;        // force_config / 100: kernel timing diagnostics (GemmParams::diag)
 static unsigned long long* g_stamps = nullptr;   // cfg 17 progress-stamp buffer ([wg][64] u64)
+static int g_adapt = 0;   // adaptive split-K partition: opt-in (measured neutral, profiles/r2_gemm1_study)
+
+void nsdb_gemm_set_adapt(int on) { g_adapt = on; }
+
+static std::map<std::tuple<int, void*, int, int, int, int>, nsdb::AdaptState*>& adapt_states() {
+  static std::map<std::tuple<int, void*, int, int, int, int>, nsdb::AdaptState*> states;
+  return states;
+}
+
+// Inspection: copy the learned shares and rates (splits floats each) of the first state matching
+// (M, N, K) into out[0:2*64]; returns the split count, 0 if there is none. Synchronises the device.
+int nsdb_gemm_adapt_state(int M, int N, int K, float* out) {
+  for (auto& kv : adapt_states()) {
+    if (std::get<2>(kv.first) == M && std::get<3>(kv.first) == N && std::get<4>(kv.first) == K && kv.second) {
+      if (hipDeviceSynchronize() != hipSuccess) return -1;
+      if (hipMemcpy(out, kv.second, 2 * 64 * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+      return std::get<5>(kv.first);
+    }
+  }
+  return 0;
+}
 
 
 void nsdb_gemm_set_stamps(void* ptr) { g_stamps = (unsigned long long*)ptr; }
@@ -1299,7 +1433,7 @@ int nsdb_gemm_nt_softmax(const void* A, const void* B, float* C, const float* bi
   p.tiles_n = (N + 255) / 256;
   p.vec_ws = 0;
   p.vec_c = (ldc % 4 == 0 && (reinterpret_cast<uintptr_t>(C) & 15) == 0) ? 1 : 0;
-  p.softmax = axis; p.sm_part = (float2*)part; p.sm_cnt = cnt; p.sm_flag = flag; p.stamps = nullptr;
+  p.softmax = axis; p.sm_part = (float2*)part; p.sm_cnt = cnt; p.sm_flag = flag; p.stamps = nullptr; p.adapt = nullptr;
   const int tiles = p.tiles_m * p.tiles_n;
   if (axis == 1) hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<20>, dim3(tiles), dim3(512), 0, stream, p);
   else hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<21>, dim3(tiles), dim3(512), 0, stream, p);
@@ -1336,6 +1470,7 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
   p.seg_stride_b = seg_stride_b;
   p.softmax = 0; p.sm_part = nullptr; p.sm_cnt = nullptr; p.sm_flag = nullptr;
   p.stamps = g_stamps;
+  p.adapt = nullptr;
   if (g_force_cfg == 17 && g_stamps == nullptr) return -6;
   if (seg_k > 0 && (seg_k % p.kchunk != 0 || seg_k % nsdb::BK != 0)) return -5;   // a split must not cross a segment
   const int cfg = pick_cfg(M, N, K, batch);
@@ -1346,6 +1481,27 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
   p.vec_c = (ldc % 4 == 0 && sC % 4 == 0 &&
              (reinterpret_cast<uintptr_t>(C) & (out_f32 ? 15 : 7)) == 0) ? 1 : 0;
   dim3 grid(p.tiles_m * p.tiles_n * p.splits, 1, batch);
+  // only long split-K GEMMs (>= 8 splits of >= 16 k-tiles: the XCD tail is worth it); the rest keep the
+  // static partition, bit-reproducible from run to run (the adaptive one is exact but moves the summation
+  // grouping between launches; nsdb_gemm_set_adapt(0) restores full reproducibility)
+  if (cfg == 2 && g_adapt && p.splits >= 8 && (K / nsdb::BK) / p.splits >= 16 && batch == 1 && seg_k == 0 && p.splits <= nsdb::ADAPT_MAX_SPLITS &&
+      (long long)p.tiles_m * p.tiles_n * p.splits <= nsdb::ADAPT_MAX_WG && p.tiles_m * p.tiles_n <= 64) {
+    // one persistent state per (shape, splits) — the measured rates belong to that workload
+    // (per stream: launches on one stream are ordered, so every workgroup of a launch reads the same shares)
+    auto& states = adapt_states();
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const auto key = std::make_tuple(dev, (void*)stream, M, N, K, p.splits);
+    auto it = states.find(key);
+    nsdb::AdaptState* st = nullptr;
+    if (it != states.end()) {
+      st = it->second;
+    } else if (hipMalloc((void**)&st, sizeof(nsdb::AdaptState)) == hipSuccess) {
+      if (hipMemset(st, 0, sizeof(nsdb::AdaptState)) != hipSuccess) st = nullptr;
+      states[key] = st;
+    }
+    p.adapt = st;
+  }
   if (cfg == 2)
     hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<0>, grid, dim3(512), 0, stream, p);
   else if (cfg == 10)

@@ -1,7 +1,8 @@
 """The GEMM study kernels behind profiles/r2_gemm1_study and profiles/r2_epilogue are kept runnable and must
 stay bit-exact with the production 8-phase kernel (same k order, same fp32 accumulation): 4-wave 128x128
 per-wave kernels (LDS-DMA cfg 12, register-staged cfg 16), the 10-slot LDS ring (cfg 14), the untransposed
-LDS-staged epilogue (cfg 15) — plus the cfg-17 drift diagnostic (real-time stamps + XCD ids)."""
+LDS-staged epilogue (cfg 15) — plus the cfg-17 drift diagnostic (real-time stamps + XCD ids) and the opt-in
+adaptive split-K K partition (gemm_set_adapt)."""
 import pytest
 import torch
 
@@ -13,8 +14,11 @@ DEV = "cuda:0"
 
 @pytest.fixture(autouse=True)
 def _reset():
+    # the bit-exact comparisons need cfg 2's static K partition (the adaptive one moves between launches)
+    _ext.hip().gemm_set_adapt(0)
     yield
     _ext.hip().gemm_force_config(-1)
+    _ext.hip().gemm_set_adapt(0)
 
 
 @pytest.mark.parametrize("shape", [(777, 555, 4104), (300, 2000, 100000), (512, 512, 640)])
@@ -57,3 +61,26 @@ def test_drift_diagnostic_stamps():
     # guaranteed by contract — only check that the ids are consistent within most splits)
     same = sum(len(set(xcc[g * 16:(g + 1) * 16])) == 1 for g in range(16))
     assert same >= 12, xcc
+
+
+@pytest.mark.parametrize("shape", [(1000, 1000, 64 * 16 * 40 + 40), (300, 700, 100000)])
+def test_adaptive_splitk_partition_exact(shape):
+    """The adaptive split-K K partition (cfg 2, split-K launches) is an exact partition of K whatever shares
+    the state has learned: several launches in a row (the shares move after each) all match fp32, and
+    match the non-adaptive partition to summation-order rounding."""
+    M, N, K = shape
+    g = torch.Generator(device=DEV).manual_seed(7)
+    A = torch.empty(M, K, device=DEV).uniform_(-1, 1, generator=g).to(torch.bfloat16)
+    B = torch.empty(N, K, device=DEV).uniform_(-1, 1, generator=g).to(torch.bfloat16)
+    assert ops.gemm_splits(M, N, K) > 1
+    h = _ext.hip()
+    h.gemm_force_config(2)
+    rows = torch.arange(0, M, 97, device=DEV)
+    ref = A[rows].float() @ B.float().t()
+    h.gemm_set_adapt(0)
+    base = ops.gemm_nt(A, B, out_dtype=torch.float32)
+    h.gemm_set_adapt(1)
+    for _ in range(6):
+        out = ops.gemm_nt(A, B, out_dtype=torch.float32)
+        assert ((out[rows] - ref).abs().max() / ref.abs().max()).item() < 1e-5
+        assert ((out - base).abs().max() / base.abs().max()).item() < 1e-5
