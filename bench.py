@@ -73,9 +73,16 @@ def main():
                          "the chip's clock dips for ~10-20 ms after the GEMMs start and then settles "
                          "(profiles/r2_clock_settle); the timed window should see the settled clock")
     ap.add_argument("--profile-json", default=None)
-    ap.add_argument("--overlap", choices=["none", "after", "before"], default="none",
-                    help="conv2d job on its own HIP stream, submitted after/before the FF jobs (independent inputs)")
-    ap.add_argument("--job-priority", type=int, default=-1, help="HIP stream priority of the conv2d job stream")
+    ap.add_argument("--overlap", choices=["none", "after", "before", "tail"], default="none",
+                    help="conv2d job on its own HIP stream, submitted after/before the FF jobs (independent inputs); "
+                         "tail: gated on the GPU to start when the first workgroup of the FF layer-1 GEMM finishes "
+                         "(fills the CUs that GEMM's tail leaves idle)")
+    ap.add_argument("--job-priority", type=int, default=None,
+                    help="HIP stream priority of the conv2d job stream (default -1 = high; 0 in tail mode, where the "
+                         "FF jobs run on a high-priority stream instead)")
+    ap.add_argument("--conv-blocks", type=int, default=None,
+                    help="conv2d row-kernel grid cap (default 512 persistent blocks; tail mode: 0 = one short block "
+                         "per row group, so the FF kernels after the GEMM are not held behind persistent conv blocks)")
     ap.add_argument("--inflight", type=int, default=1,
                     help="FF steps in flight: step i's FF jobs go to job lane i %% inflight (>1 pipelines "
                          "consecutive batches: step i+1's layer-1 GEMM starts while step i's tail kernels run)")
@@ -104,7 +111,21 @@ def main():
     inflight = max(1, args.inflight)
     conv_lane = inflight if inflight > 1 else 0
     client.job_lanes = conv_lane + 1
-    client.job_lane_priority = {conv_lane: args.job_priority}
+    tail = args.overlap == "tail"
+    prio = args.job_priority if args.job_priority is not None else (0 if tail else -1)
+    client.job_lane_priority = {conv_lane: prio}
+    conv_blocks = args.conv_blocks if args.conv_blocks is not None else (0 if tail else None)
+    if conv_blocks is not None and dev.type == "cuda":
+        from netsdb_amd import _ext
+
+        _ext.hip().conv2d_max_blocks(conv_blocks)
+    main_stream = None
+    if tail and dev.type == "cuda":
+        # FF jobs on a high-priority stream: when conv blocks and the FF tail kernels both wait for CUs, the
+        # dispatcher takes the FF kernels' workgroups first
+        main_stream = torch.cuda.Stream(dev, priority=-1)
+        main_stream.wait_stream(torch.cuda.current_stream(dev))
+        torch.cuda.set_stream(main_stream)
 
     def conv():
         cv.conv2d_memfuse_inference(client, "conv2d", "img", "conv_out", w, b)
@@ -114,6 +135,7 @@ def main():
                           seed=i)
 
     def step(i):
+        trig = client.arm_tail_trigger() if args.overlap == "tail" else None
         if args.overlap == "before":
             client.submit_job(conv, lane=conv_lane, independent=True)
         if inflight > 1:
@@ -125,6 +147,8 @@ def main():
             conv()
         elif args.overlap == "after":
             client.submit_job(conv, lane=conv_lane, independent=True)
+        elif args.overlap == "tail":
+            client.submit_job(conv, lane=conv_lane, independent=True, start_on=trig)
         if args.overlap != "none" and inflight == 1:
             client.wait_jobs()   # the step ends when both jobs have (stream-ordered join)
 

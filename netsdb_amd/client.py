@@ -59,6 +59,7 @@ class PDBClient:
         self.job_stream_priority = 0
         self.job_lanes = 2               # job streams (in-order job queues) created on first submit_job
         self.job_lane_priority = {}      # lane -> HIP stream priority (default job_stream_priority)
+        self.tail_trigger = None         # TailTrigger (arm_tail_trigger)
         if resume:
             self._resume()
 
@@ -425,7 +426,17 @@ class PDBClient:
         self.ctx.barrier()
 
     # ------------------------------------------------------------------ concurrent jobs
-    def submit_job(self, fn, *args, lane: int = 0, independent: bool = False, **kwargs):
+    def arm_tail_trigger(self):
+        """Arm the tail trigger of the next long GEMM this client enqueues; pass the returned trigger as
+        ``submit_job(..., start_on=trigger)`` to start an independent job in that GEMM's tail (see
+        :class:`~netsdb_amd.execution.streams.TailTrigger`)."""
+        if self.tail_trigger is None:
+            from .execution.streams import TailTrigger
+
+            self.tail_trigger = TailTrigger(self.device)
+        return self.tail_trigger.arm()
+
+    def submit_job(self, fn, *args, lane: int = 0, independent: bool = False, start_on=None, **kwargs):
         """Run ``fn(*args, **kwargs)`` (any job-issuing callable, e.g. a model's inference entry point)
         with its kernels enqueued on a job stream, concurrently with work on the caller's stream.
         Returns a :class:`~netsdb_amd.execution.streams.JobHandle`; see that module for the ordering
@@ -435,7 +446,7 @@ class PDBClient:
 
             self.job_streams = JobStreams(self.device, lanes=self.job_lanes, priority=self.job_stream_priority,
                                           lane_priority=self.job_lane_priority)
-        return self.job_streams.submit(fn, *args, lane=lane, independent=independent, **kwargs)
+        return self.job_streams.submit(fn, *args, lane=lane, independent=independent, start_on=start_on, **kwargs)
 
     def wait_jobs(self):
         """The caller's stream waits (stream-ordered) for every submitted job."""

@@ -15,6 +15,10 @@ int nsdb_gemm_splits(int M, int N, int K, int batch);
 void nsdb_gemm_force_config(int cfg);
 void nsdb_gemm_set_stamps(void* ptr);
 void nsdb_gemm_set_adapt(int on);
+void nsdb_tail_trigger_arm(void* flag, unsigned value);
+int nsdb_tail_trigger_consumed();
+void nsdb_tail_trigger_disarm();
+int nsdb_stream_wait_value(hipStream_t stream, void* flag, unsigned value);
 int nsdb_gemm_adapt_state(int M, int N, int K, float* out);
 int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const float* bias, int M, int N, int K,
                       long long lda, long long ldb, long long ldc, long long sA, long long sB, long long sC,
@@ -28,6 +32,7 @@ int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* ou
                       int out_f32, hipStream_t stream);
 extern int nsdb_conv2d_force_generic;
 extern int nsdb_conv2d_variant;
+extern int nsdb_conv2d_max_blocks;
 int nsdb_im2col(const void* X, void* out, int N, int C, int H, int W, int KH, int KW, int stride, int pad, int dil,
                 int ldk, hipStream_t stream);
 int nsdb_softmax_rows(const void* X, int x_f32, const float* bias, void* Y, int y_f32, int R, int N,
@@ -523,6 +528,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dropout") = 0.0, py::arg("seed") = 0, py::arg("splits") = 0, py::arg("out") = py::none(),
         py::arg("accumulate") = false);
   m.def("gemm_splits", &gemm_splits);
+  m.def("tail_trigger_arm", [](torch::Tensor flag, int64_t value) {
+          TORCH_CHECK(flag.is_cuda() && flag.scalar_type() == torch::kInt32 && flag.numel() >= 1, "flag: int32 device tensor");
+          nsdb_tail_trigger_arm(flag.data_ptr(), (unsigned)value);
+        }, "arm the tail trigger of the next long 8-phase GEMM launch");
+  m.def("tail_trigger_consumed", []() { return (bool)nsdb_tail_trigger_consumed(); },
+        "whether a launch took the armed trigger (clears it)");
+  m.def("tail_trigger_disarm", []() { nsdb_tail_trigger_disarm(); });
+  m.def("stream_wait_value", [](torch::Tensor flag, int64_t value) {
+          TORCH_CHECK(flag.is_cuda() && flag.scalar_type() == torch::kInt32 && flag.numel() >= 1, "flag: int32 device tensor");
+          check_rc(nsdb_stream_wait_value(cur_stream(), flag.data_ptr(), (unsigned)value), "stream_wait_value");
+        }, "current stream waits on the GPU until flag >= value (unsigned)");
   m.def("gemm_set_adapt", [](int64_t on) { nsdb_gemm_set_adapt((int)on); },
         "adaptive split-K K-partition across XCDs on/off (A/B)");
   m.def("gemm_adapt_state", [](int64_t M, int64_t N, int64_t K) {
@@ -540,6 +556,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "-1 auto, 0 = 128x128 tile, 1 = 256x256 tile (A/B testing)");
   m.def("conv2d_force_generic", [](int64_t v) { nsdb_conv2d_force_generic = (int)v; },
         "1: route every conv2d to the generic gather kernel (A/B testing)");
+  m.def("conv2d_max_blocks", [](int64_t v) { const int old = nsdb_conv2d_max_blocks; nsdb_conv2d_max_blocks = (int)v; return old; },
+        "row-kernel grid cap (0 = one block per row group); returns the previous value");
   m.def("conv2d_variant", [](int64_t v) { nsdb_conv2d_variant = (int)v; }, "row-kernel diagnostic variant");
   m.def("conv2d", &conv2d, py::arg("X"), py::arg("W"), py::arg("bias") = py::none(), py::arg("KH") = 1,
         py::arg("KW") = 1, py::arg("stride") = 1, py::arg("pad") = 0, py::arg("dil") = 1, py::arg("act") = 0,

@@ -535,6 +535,10 @@ extern "C" {
 
 int nsdb_conv2d_force_generic = 0;   // 1: always use the generic gather kernel (A/B, tests)
 int nsdb_conv2d_variant = 0;         // row-kernel diagnostics (timing only)
+// row kernel grid cap: > 0 persistent blocks (default 2 per CU: the filter prologue is paid once per block);
+// 0 = one block per row group (short-lived blocks that the dispatcher can interleave with higher-priority
+// kernels when the conv shares the GPU with another job, e.g. gated into a GEMM's tail)
+int nsdb_conv2d_max_blocks = 512;
 
 int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* out, int N, int C, int H,
                       int W, int OC, int KH, int KW, int stride, int pad, int dil, int ldw, int act,
@@ -569,7 +573,7 @@ int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* ou
     if ((long long)N * OC * p.OH * p.OW * 2 >= 0x7ffffff0LL) goto generic;    // 31-bit buffer offsets
     if (C * rin * q.chunks > 512 || 64 * ldw / 8 > 6 * 256 || 64 * ldw * 2 > nsdb::CVR_BUF) goto generic;
     {
-      const int blocks = std::min(q.ngroups, 256 * 2);     // persistent: two blocks per CU
+      const int blocks = nsdb_conv2d_max_blocks > 0 ? std::min(q.ngroups, nsdb_conv2d_max_blocks) : q.ngroups;
       const dim3 grid(blocks, (OC + 63) / 64);
       const bool staged = nchw_out && !out_f32 && (p.OW & 1) == 0 && q.vec8 && ((p.OH % 4) * p.OW) % 4 == 0;
       if (q.variant != 0) {   // diagnostics build (timing only): runtime variant bits, no activation

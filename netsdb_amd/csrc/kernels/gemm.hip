@@ -61,6 +61,11 @@ struct GemmParams {
   int* sm_flag;
   unsigned long long* stamps;   // diagnostic variant 12: per-workgroup real-time stamps every 32 k-tiles
   struct AdaptState* adapt;     // split-K: launch-to-launch adaptive K partition (see AdaptState)
+  // tail trigger (8-phase kernel): every workgroup raises *signal to signal_value (atomic max) when its main
+  // loop is done, so a job stream gated on it (hipStreamWaitValue32 >= value) launches while this GEMM's
+  // tail leaves CUs idle (see nsdb_tail_trigger_arm)
+  unsigned* signal;
+  unsigned signal_value;
 };
 
 // Adaptive split-K partition (8-phase kernel, split-K launches). The splits of one GEMM run on different XCDs
@@ -699,14 +704,20 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
     if constexpr (V == 4) return;
     const int k = kbeg + u * BK + kc;
     const bool kin = k < kend;
+    // memory-side diagnostics (timing only, wrong results): 13 every split streams the SAME K window
+    // [0, kchunk) (unique bytes / splits: Infinity-Cache resident); 14 every workgroup cycles over 2 k-tiles
+    // (L2/L1 resident: the L2 -> CU path alone)
+    const int ks = V == 13 ? k - kbeg : V == 14 ? (u & 1) * BK + kc : k;
     char* dst = RING ? smem + buf * HALF : smem + buf * BUF + slot * HALF;   // RING: buf = ring slot
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int ro = roff[slot][i];
       const int voff = (kin && ro >= 0) ? (KT ? u * (slot < 2 ? slab_a : slab_b) + ro + kc * 2
-                                              : ro + (slot < 2 ? k : k - kb0) * 2) : OOB;
+                                              : ro + (slot < 2 ? ks : ks - kb0) * 2) : OOB;
+      // V15: non-temporal operand stream (aux nt): the once-streamed panels do not displace the split-K slabs
+      // (and other resident sets) from the Infinity Cache
       __builtin_amdgcn_raw_ptr_buffer_load_lds(slot < 2 ? ra : rb, (lds_void*)(dst + (i * 64 + wave * 8) * 128), 16,
-                                               voff, 0, 0, 0);
+                                               voff, 0, 0, V == 15 ? 2 : 0);
     }
   };
 
@@ -848,6 +859,8 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   }
   if (V != 3 && wr == 0) NSDB_BARRIER();            // re-align the groups
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // trailing zero-fill DMAs land before LDS reuse
+  if (V == 0 && p.signal != nullptr && tid == 0)     // tail trigger: this workgroup's CU frees up soon
+    __hip_atomic_fetch_max(p.signal, p.signal_value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (ad != nullptr) {
     // finish time; the last workgroup of the launch derives the next launch's shares (the groups are
     // re-aligned here, so the block-wide barriers below pair up)
@@ -1349,6 +1362,33 @@ static int g_adapt = 0;   // adaptive split-K partition: opt-in (measured neutra
 
 void nsdb_gemm_set_adapt(int on) { g_adapt = on; }
 
+// Tail trigger: start an independent job in the tail of the next long GEMM instead of after it.
+// arm(flag, v): the next 8-phase launch with >= 128 workgroups and >= 64 k-tiles per workgroup makes each
+// workgroup raise *flag to v when its main loop ends (the grid is one resident wave, so by then every
+// workgroup of it has been dispatched and the CUs that finish first are idle until the launch drains).
+// consumed() tells the caller whether a launch took it (only then may a stream wait on the flag: the value is
+// written unconditionally by every workgroup of that launch, so the wait always ends).
+static struct { unsigned* flag; unsigned value; int consumed; } g_trig = {nullptr, 0u, 0};
+
+void nsdb_tail_trigger_arm(void* flag, unsigned value) {
+  g_trig.flag = (unsigned*)flag;
+  g_trig.value = value;
+  g_trig.consumed = 0;
+}
+
+int nsdb_tail_trigger_consumed() {
+  const int c = g_trig.flag != nullptr && g_trig.consumed;
+  if (c) g_trig.flag = nullptr;         // one launch per arm
+  return c;
+}
+
+void nsdb_tail_trigger_disarm() { g_trig.flag = nullptr; g_trig.consumed = 0; }
+
+// Make `stream` wait (on the GPU command processor, no host involvement) until *flag >= value.
+int nsdb_stream_wait_value(hipStream_t stream, void* flag, unsigned value) {
+  return (int)hipStreamWaitValue32(stream, flag, value, hipStreamWaitValueGte, 0xffffffffu);
+}
+
 static std::map<std::tuple<int, void*, int, int, int, int>, nsdb::AdaptState*>& adapt_states() {
   static std::map<std::tuple<int, void*, int, int, int, int>, nsdb::AdaptState*> states;
   return states;
@@ -1434,6 +1474,7 @@ int nsdb_gemm_nt_softmax(const void* A, const void* B, float* C, const float* bi
   p.vec_ws = 0;
   p.vec_c = (ldc % 4 == 0 && (reinterpret_cast<uintptr_t>(C) & 15) == 0) ? 1 : 0;
   p.softmax = axis; p.sm_part = (float2*)part; p.sm_cnt = cnt; p.sm_flag = flag; p.stamps = nullptr; p.adapt = nullptr;
+  p.signal = nullptr; p.signal_value = 0;
   const int tiles = p.tiles_m * p.tiles_n;
   if (axis == 1) hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<20>, dim3(tiles), dim3(512), 0, stream, p);
   else hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<21>, dim3(tiles), dim3(512), 0, stream, p);
@@ -1471,6 +1512,7 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
   p.softmax = 0; p.sm_part = nullptr; p.sm_cnt = nullptr; p.sm_flag = nullptr;
   p.stamps = g_stamps;
   p.adapt = nullptr;
+  p.signal = nullptr; p.signal_value = 0;
   if (g_force_cfg == 17 && g_stamps == nullptr) return -6;
   if (seg_k > 0 && (seg_k % p.kchunk != 0 || seg_k % nsdb::BK != 0)) return -5;   // a split must not cross a segment
   const int cfg = pick_cfg(M, N, K, batch);
@@ -1502,6 +1544,12 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
     }
     p.adapt = st;
   }
+  if (cfg == 2 && g_trig.flag != nullptr && !g_trig.consumed && (long long)grid.x * batch >= 128 &&
+      (long long)((p.kchunk + nsdb::BK - 1) / nsdb::BK) >= 64) {
+    p.signal = g_trig.flag;               // the armed tail trigger goes to this long GEMM
+    p.signal_value = g_trig.value;
+    g_trig.consumed = 1;
+  }
   if (cfg == 2)
     hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<0>, grid, dim3(512), 0, stream, p);
   else if (cfg == 10)
@@ -1518,6 +1566,12 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
     hipLaunchKernelGGL(nsdb::gemm_nt_256_w4r_kernel, grid, dim3(256), 0, stream, p);
   else if (cfg == 13)   // w4 diagnostic: no DMA issued (load-free upper bound, wrong results)
     hipLaunchKernelGGL(nsdb::gemm_nt_256_w4_kernel<4>, grid, dim3(256), 0, stream, p);
+  else if (cfg == 20)   // 8-phase with non-temporal operand loads
+    hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<15>, grid, dim3(512), 0, stream, p);
+  else if (cfg == 18)   // diagnostic: all splits stream one shared K window (MALL-resident operands)
+    hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<13>, grid, dim3(512), 0, stream, p);
+  else if (cfg == 19)   // diagnostic: every workgroup cycles over 2 k-tiles (L2-resident operands)
+    hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<14>, grid, dim3(512), 0, stream, p);
   else if (cfg == 11)   // K-tiled operands (caller passes [K/64][ld][64] panels, lda/ldb = padded rows)
     hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<9>, grid, dim3(512), 0, stream, p);
   else if (cfg >= 3 && cfg <= 9) {   // diagnostic variants of the 8-phase kernel (timing only)

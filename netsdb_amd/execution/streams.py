@@ -18,6 +18,14 @@ Ordering contract:
     stream, ``submit`` of that later job orders it after the consumer by default (drop
     ``independent`` for jobs that replace outputs another stream has read).
 On CPU every job runs inline and handles are already complete.
+
+Tail-gated jobs (``TailTrigger``): a long split-K GEMM (the FF layer-1 product) runs as ONE resident wave of
+256 workgroups whose finish times spread over tens of microseconds (XCD rate differences and stragglers,
+profiles/r2_gemm1_study) — CUs that finish first sit idle until the launch drains. An independent job submitted
+with ``start_on=trigger.arm()`` (armed BEFORE the GEMM is enqueued) is held on its stream by the GPU command
+processor (hipStreamWaitValue32) until the first workgroup of that GEMM finishes its main loop, so its kernels
+fill exactly those idle CUs: it can neither start early and take CUs the GEMM's wave needs, nor wait for
+the GEMM's whole tail.
 """
 from __future__ import annotations
 
@@ -49,6 +57,50 @@ class JobHandle:
         return self.result
 
 
+class TailTrigger:
+    """Device flag raised by the workgroups of the next long 8-phase GEMM launch (see module doc).
+
+    ``arm()`` before enqueuing the job whose GEMM tail should be filled; ``JobStreams.submit(...,
+    start_on=trigger)`` then gates the submitted job on it. The gate is only installed when a launch actually
+    took the armed trigger (every workgroup of that launch writes the flag, so the wait always ends);
+    otherwise the job starts ungated."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.flag = torch.zeros(1, dtype=torch.int32, device=self.device) if self.device.type == "cuda" else None
+        self.epoch = 0
+        self.armed = False
+        self.gated = 0       # jobs that were actually gated (stats / tests)
+
+    def arm(self) -> "TailTrigger":
+        if self.flag is None:
+            return self
+        from .. import _ext
+
+        self.epoch = self.epoch % 0x7FFFFFFF + 1     # flag values only grow (atomic max), never wrap to 0
+        if self.epoch == 1 and self.gated:           # wrapped: restart from a zero flag
+            self.flag.zero_()
+        _ext.hip().tail_trigger_arm(self.flag, self.epoch)
+        self.armed = True
+        return self
+
+    def gate(self, stream) -> bool:
+        """Make ``stream`` wait on the GPU for the armed launch's first finished workgroup."""
+        if not self.armed or self.flag is None:
+            return False
+        from .. import _ext
+
+        h = _ext.hip()
+        self.armed = False
+        if not h.tail_trigger_consumed():
+            h.tail_trigger_disarm()
+            return False
+        with torch.cuda.stream(stream):
+            h.stream_wait_value(self.flag, self.epoch)
+        self.gated += 1
+        return True
+
+
 class JobStreams:
     """A small pool of HIP streams for concurrently executing independent jobs on one device.
 
@@ -73,7 +125,8 @@ class JobStreams:
             self._streams[lane] = torch.cuda.Stream(self.device, priority=self.lane_priority.get(lane, self.priority))
         return self._streams[lane]
 
-    def submit(self, fn: Callable, *args, lane: int = 0, independent: bool = False, **kwargs) -> JobHandle:
+    def submit(self, fn: Callable, *args, lane: int = 0, independent: bool = False,
+               start_on: Optional[TailTrigger] = None, **kwargs) -> JobHandle:
         self.submitted += 1
         if not self.on_gpu:
             return JobHandle(fn(*args, **kwargs), None, None)
@@ -81,6 +134,8 @@ class JobStreams:
         caller = torch.cuda.current_stream(self.device)
         if not independent:
             s.wait_stream(caller)
+        if start_on is not None:
+            start_on.gate(s)
         with torch.cuda.stream(s):
             res = fn(*args, **kwargs)
             ev = torch.cuda.Event()

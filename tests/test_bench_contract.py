@@ -18,7 +18,8 @@ def _last_json(out: str) -> dict:
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("extra", [[], ["--overlap", "before"], ["--overlap", "after", "--inflight", "2"]])
+@pytest.mark.parametrize("extra", [[], ["--overlap", "before"], ["--overlap", "after", "--inflight", "2"],
+                                   ["--overlap", "tail"]])
 def test_bench_single_process(extra):
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
     r = subprocess.run([sys.executable, "bench.py", "--small", "--steps", "2", "--warmup", "2"] + extra, cwd=ROOT,

@@ -67,3 +67,60 @@ def test_submit_orders_after_caller_stream_gpu():
     out = h.wait()
     torch.cuda.synchronize()
     assert torch.all(out == 2)
+
+
+def test_tail_trigger_cpu_is_inert():
+    from netsdb_amd.execution.streams import TailTrigger
+
+    t = TailTrigger("cpu").arm()
+    assert t.flag is None and not t.gate(None)
+    js = JobStreams("cpu")
+    assert js.submit(lambda: 7, start_on=t).wait() == 7
+
+
+def _long_splitk_operands(dev):
+    # 1024 x 1024 x 65536: 16 tiles x 16 splits = 256 workgroups of 64 k-tiles (a tail-trigger launch)
+    g = torch.Generator(device=dev).manual_seed(0)
+    A = torch.empty(1024, 65536, device=dev).uniform_(-1, 1, generator=g).to(torch.bfloat16)
+    B = (torch.empty(1024, 65536, device=dev).uniform_(-1, 1, generator=g) * 0.01).to(torch.bfloat16)
+    return A, B
+
+
+@pytest.mark.gpu
+def test_tail_gated_job_gpu():
+    """A job gated on the tail trigger of a long split-K GEMM runs after the GEMM's first workgroup finishes:
+    results of both are exact vs ungated runs, the gate was installed and the flag carries the epoch."""
+    from netsdb_amd import ops
+    from netsdb_amd.execution.streams import TailTrigger
+
+    dev = "cuda:0"
+    A, B = _long_splitk_operands(dev)
+    assert ops.gemm_splits(1024, 1024, 65536) == 16
+    ref = ops.gemm_nt(A, B, out_dtype=torch.float32)
+    x = torch.arange(1 << 20, device=dev, dtype=torch.float32)
+    js = JobStreams(dev, lanes=1)
+    trig = TailTrigger(dev)
+    for it in range(3):
+        trig.arm()
+        C = ops.gemm_nt(A, B, out_dtype=torch.float32)
+        h = js.submit(lambda: x * 2 + it, independent=True, start_on=trig)
+        y = h.wait()
+        torch.cuda.synchronize()
+        assert torch.equal(C, ref)
+        assert torch.equal(y, x * 2 + it)
+        assert trig.gated == it + 1 and int(trig.flag.item()) == trig.epoch
+
+
+@pytest.mark.gpu
+def test_tail_trigger_unconsumed_does_not_gate_gpu():
+    """Armed but no qualifying GEMM launched (short K): the job runs ungated (no wait that could never end)."""
+    from netsdb_amd import ops
+    from netsdb_amd.execution.streams import TailTrigger
+
+    dev = "cuda:0"
+    trig = TailTrigger(dev).arm()
+    a = torch.randn(512, 512, device=dev).to(torch.bfloat16)
+    ops.gemm_nt(a, a)
+    js = JobStreams(dev, lanes=1)
+    y = js.submit(lambda: a.float().sum(), independent=True, start_on=trig).synchronize()
+    assert trig.gated == 0 and torch.isfinite(y)
