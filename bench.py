@@ -80,6 +80,9 @@ def main():
     ap.add_argument("--job-priority", type=int, default=None,
                     help="HIP stream priority of the conv2d job stream (default -1 = high; 0 in tail mode, where the "
                          "FF jobs run on a high-priority stream instead)")
+    ap.add_argument("--conv-kernel", choices=["rows", "rowfull"], default=None,
+                    help="conv2d row kernel: two-pass 2-waves/SIMD (rows) or full-row 1-wave/SIMD with stores "
+                         "pipelined under the MFMAs (rowfull); default: the library default")
     ap.add_argument("--conv-blocks", type=int, default=None,
                     help="conv2d row-kernel grid cap (default 512 persistent blocks; tail mode: 0 = one short block "
                          "per row group, so the FF kernels after the GEMM are not held behind persistent conv blocks)")
@@ -119,6 +122,10 @@ def main():
         from netsdb_amd import _ext
 
         _ext.hip().conv2d_max_blocks(conv_blocks)
+    if args.conv_kernel is not None and dev.type == "cuda":
+        from netsdb_amd import _ext
+
+        _ext.hip().conv2d_rowfull(1 if args.conv_kernel == "rowfull" else 0)
     main_stream = None
     if tail and dev.type == "cuda":
         # FF jobs on a high-priority stream: when conv blocks and the FF tail kernels both wait for CUs, the

@@ -33,6 +33,7 @@ int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* ou
 extern int nsdb_conv2d_force_generic;
 extern int nsdb_conv2d_variant;
 extern int nsdb_conv2d_max_blocks;
+extern int nsdb_conv2d_rowfull;
 int nsdb_im2col(const void* X, void* out, int N, int C, int H, int W, int KH, int KW, int stride, int pad, int dil,
                 int ldk, hipStream_t stream);
 int nsdb_softmax_rows(const void* X, int x_f32, const float* bias, void* Y, int y_f32, int R, int N,
@@ -558,6 +559,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "1: route every conv2d to the generic gather kernel (A/B testing)");
   m.def("conv2d_max_blocks", [](int64_t v) { const int old = nsdb_conv2d_max_blocks; nsdb_conv2d_max_blocks = (int)v; return old; },
         "row-kernel grid cap (0 = one block per row group); returns the previous value");
+  m.def("conv2d_rowfull", [](int64_t v) { const int old = nsdb_conv2d_rowfull; nsdb_conv2d_rowfull = (int)v; return old; },
+        "full-row conv kernel on/off (A/B); returns the previous value");
   m.def("conv2d_variant", [](int64_t v) { nsdb_conv2d_variant = (int)v; }, "row-kernel diagnostic variant");
   m.def("conv2d", &conv2d, py::arg("X"), py::arg("W"), py::arg("bias") = py::none(), py::arg("KH") = 1,
         py::arg("KW") = 1, py::arg("stride") = 1, py::arg("pad") = 0, py::arg("dil") = 1, py::arg("act") = 0,

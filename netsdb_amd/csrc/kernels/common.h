@@ -26,8 +26,12 @@ __device__ __forceinline__ unsigned short f32_to_bf16(float f) {
   return __builtin_bit_cast(unsigned short, b);
 }
 
+// Two f32 -> one packed bf16x2 dword in ONE v_cvt_pk_bf16_f32 (same RNE / NaN semantics as f32_to_bf16); the
+// element-wise form compiled to two converts + shift + or per dword in every epilogue.
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
-  return (unsigned)f32_to_bf16(lo) | ((unsigned)f32_to_bf16(hi) << 16);
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2_t){lo, hi}, bf16x2_t));
 }
 
 // Compile-time activation (kernels templated on ACT: no per-element switch in unrolled epilogues).

@@ -13,6 +13,7 @@
 // 32 pixels x 64 channels = 2 x 4 mfma_f32_16x16x32_bf16 accumulators.
 #include "common.h"
 #include <algorithm>
+#include <type_traits>
 
 namespace nsdb {
 
@@ -505,6 +506,307 @@ __global__ void __launch_bounds__(256, 2) conv2d_rows_kernel(ConvRowParams p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Full-row variant of the row-tiled conv (the headline 3 -> 64, 7x7 on 112^2: 7 pixel tiles per output row).
+// conv2d_rows_kernel above computes each 16-pixel tile as two 6-deep dependent MFMA chains (32 oc per pass,
+// two passes) with the epilogue right behind the last MFMA, at 2 waves/SIMD: its inner loop is latency-bound
+// (~30 % MFMA issue). Here ONE wave per SIMD (1 block of 4 waves per CU, 512 registers per lane):
+//  * a wave owns one output row x all 64 oc: 7 tiles x 4 n-tiles = 28 independent accumulator chains, so the
+//    6 k-steps issue 28 back-to-back MFMAs each; the A fragments of k-step ks+1 (7 ds_read pairs) are read
+//    while k-step ks's MFMAs run (register double buffer);
+//  * epilogue (bias + act -> bf16) into ONE [64 oc][segs] LDS image of the block's 4 rows, then every oc's
+//    4-row run (contiguous in NCHW) leaves as 8-B coalesced stores. The stores of group g drain while group
+//    g+1's MFMAs run: the next group's input rows are fetched BEFORE them (the wait for that fetch never
+//    waits for the stores), and only two barriers per group separate the LDS phases;
+//  * segs = 2 x (64k + 36) bf16: the ds_write_b32 lane groups (16 oc rows x {+0, +2 dwords}) hit 32 distinct
+//    banks.
+// Input staging (4 shifted copies per (c, r) row) and the filter-in-VGPRs layout are the row kernel's.
+constexpr int CVF_NT = 7;                                            // pixel tiles per row (OW 97..112)
+constexpr int CVF_SEGS = 2 * (64 * 3 + 36);                          // 456 >= 4 * 112 - pad
+constexpr int CVF_STAGE = 2 * 64 * CVF_SEGS * 2;                     // 2 x [64 oc][segs] bf16 (PIPE: double)
+template <int ACT, bool DIAG, bool PIPE>
+__global__ void __launch_bounds__(256, 1) conv2d_rowfull_kernel(ConvRowParams p) {
+  // DIAG: s_memtime phase stamps per wave (timing build, written over the output): total, MFMA, epilogue,
+  // mid barrier, stores, input staging
+  unsigned long long tt[6] = {0, 0, 0, 0, 0, 0}, t_prev = 0;
+  auto stamp = [&](int slot) {
+    if constexpr (DIAG) {
+      unsigned long long t;
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if (slot >= 0) tt[slot] += t - t_prev;
+      t_prev = t;
+    }
+  };
+  stamp(-1);
+  const unsigned long long t_start = t_prev;
+  __shared__ __attribute__((aligned(16))) char smem[CVR_BUF + CVF_STAGE + CVR_TRASH];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int oc0 = blockIdx.y * 64;
+
+  // ---- filter -> VGPRs (as conv2d_rows_kernel)
+  {
+    const int cpr = p.ldw / 8, nch = 64 * cpr;
+    uint4 v[6];
+#pragma unroll
+    for (int u = 0; u < 6; ++u) {
+      const int e = tid + u * 256;
+      const int r = e / cpr, ch = e - (e / cpr) * cpr;
+      v[u] = make_uint4(0, 0, 0, 0);
+      if (e < nch && oc0 + r < p.OC) v[u] = *reinterpret_cast<const uint4*>(p.Wt + (long long)(oc0 + r) * p.ldw + ch * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < 6; ++u) {
+      const int e = tid + u * 256;
+      if (e < nch) reinterpret_cast<uint4*>(smem)[e] = v[u];
+    }
+  }
+  __syncthreads();
+  bf16x8 bw[4][CVR_NKS];
+  {
+    const unsigned short* raw = reinterpret_cast<const unsigned short*>(smem);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int ks = 0; ks < CVR_NKS; ++ks) {
+        const int ocl = nt * 16 + (lane & 15), q = ks * 4 + (lane >> 4);
+#pragma unroll
+        for (int kw = 0; kw < 8; ++kw)
+          bw[nt][ks][kw] = (q < p.ckh && kw < p.KW) ? (short)raw[ocl * p.ldw + q * p.KW + kw] : (short)0;
+      }
+  }
+  float bias_v[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const int oc = oc0 + nt * 16 + (lane & 15);
+    bias_v[nt] = (p.bias && oc < p.OC) ? p.bias[oc] : 0.f;
+  }
+  __syncthreads();
+  for (int e = tid; e < 4 * CVR_CP / 16; e += 256)
+    reinterpret_cast<uint4*>(smem + CVR_ZERO)[e] = make_uint4(0, 0, 0, 0);
+
+  int abase[CVR_NKS];
+#pragma unroll
+  for (int ks = 0; ks < CVR_NKS; ++ks) {
+    const int q = ks * 4 + (lane >> 4);
+    if (q < p.ckh) {
+      const int c = q / p.KH, kh = q % p.KH;
+      abase[ks] = ((c * p.rin + wave + kh) * 4 + (lane & 3)) * CVR_CP + (lane & 12) * 2;
+    } else {
+      abase[ks] = CVR_ZERO + (lane & 3) * 16 + (lane & 12) * 2;
+    }
+  }
+
+  // input staging work items (c, r, chunk j), <= 2 per thread, identical for every group
+  const int items = p.C * p.rin * p.chunks;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned short*>(p.X), (short)0, (int)((long long)p.N * p.C * p.H * p.W * 2), 0x00020000);
+  u32x4 lo[2][2];      // [fetch slot][item]: two groups' rows in flight (slot = group parity)
+  u32x2 hi[2][2];
+  int it_off[2], it_r[2];
+  bool it_lo[2], it_hi[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int it = min(tid + u * 256, items - 1);
+    const int j = it % p.chunks, cr = it / p.chunks, r = cr % p.rin, c = cr / p.rin;
+    it_off[u] = ((c * p.H + r) * p.W + 8 * j) * 2;
+    it_r[u] = r;
+    it_lo[u] = 8 * j < p.W;
+    it_hi[u] = 8 * (j + 1) < p.W;
+  }
+  auto fetch = [&](int g, auto SLOT) {
+    constexpr int sl = decltype(SLOT)::value;
+    const bool gok = g < p.ngroups;
+    const int n = g / p.groups_per_img, oh0 = (g % p.groups_per_img) * CVR_TR;
+    const int gbase = ((n * p.C * p.H) + oh0) * p.W * 2;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bool rok = gok && oh0 + it_r[u] < p.H;
+      const int o = gbase + it_off[u];
+      lo[sl][u] = __builtin_amdgcn_raw_buffer_load_b128(xr, (rok && it_lo[u]) ? o : 0x7ffffff0, 0, 0);
+      hi[sl][u] = __builtin_amdgcn_raw_buffer_load_b64(xr, (rok && it_hi[u]) ? o + 16 : 0x7ffffff0, 0, 0);
+    }
+  };
+  auto store_rows = [&](auto SLOT) {
+    constexpr int sl = decltype(SLOT)::value;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int it = tid + u * 256;
+      if (it >= items) continue;
+      const int j = it % p.chunks, cr = it / p.chunks;
+      char* row = smem + cr * 4 * CVR_CP + j * 16;
+      const unsigned w[6] = {lo[sl][u].x, lo[sl][u].y, lo[sl][u].z, lo[sl][u].w, hi[sl][u].x, hi[sl][u].y};
+      *reinterpret_cast<u32x4*>(row) = lo[sl][u];
+      *reinterpret_cast<u32x4*>(row + CVR_CP) =
+          u32x4{__builtin_amdgcn_alignbyte(w[1], w[0], 2), __builtin_amdgcn_alignbyte(w[2], w[1], 2),
+                __builtin_amdgcn_alignbyte(w[3], w[2], 2), __builtin_amdgcn_alignbyte(w[4], w[3], 2)};
+      *reinterpret_cast<u32x4*>(row + 2 * CVR_CP) = u32x4{w[1], w[2], w[3], w[4]};
+      *reinterpret_cast<u32x4*>(row + 3 * CVR_CP) =
+          u32x4{__builtin_amdgcn_alignbyte(w[2], w[1], 2), __builtin_amdgcn_alignbyte(w[3], w[2], 2),
+                __builtin_amdgcn_alignbyte(w[4], w[3], 2), __builtin_amdgcn_alignbyte(w[5], w[4], 2)};
+    }
+  };
+
+  const long long OHW = (long long)p.OH * p.OW;
+  const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+      p.out, (short)0, (int)std::min<long long>((long long)p.N * p.OC * OHW * 2, 0x7fffffffLL), 0x00020000);
+  unsigned short* ostage = reinterpret_cast<unsigned short*>(smem + CVR_BUF);
+  unsigned* const trash = reinterpret_cast<unsigned*>(smem + CVR_BUF + CVF_STAGE);
+
+  // one output chunk of the group held in stage `st`: oc (wave + 4 j), 8-byte piece q = lane + 64 h of its
+  // rows_valid * OW run (c = 2 j + h); pieces past the run / oc past OC go to an out-of-range offset (dropped)
+  auto chunk_read = [&](const unsigned short* st, int c, int n4) -> uint2 {
+    const int j = c >> 1, h = c & 1;
+    return *reinterpret_cast<const uint2*>(st + (wave + 4 * j) * CVF_SEGS + 4 * min(lane + 64 * h, n4 - 1));
+  };
+  auto chunk_store = [&](uint2 v, int c, int obase, int n4, int noc) {
+    const int j = c >> 1, h = c & 1;
+    const int ocl = wave + 4 * j, q = lane + 64 * h;
+    const int off = (ocl < noc && q < n4) ? obase + (int)(ocl * OHW * 2) + 8 * q : 0x7ffffff0;
+    __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, orsrc, off, 0, 0);
+  };
+  const int noc = min(64, p.OC - oc0);
+  // the previous group's stores (PIPE: issued between this group's MFMA blocks; n4 = 0 before the first group)
+  int prev_obase = 0, prev_n4 = 0;
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  int g = blockIdx.x;
+  // input rows are fetched TWO groups ahead (slot = group parity): a load queues behind the stores issued
+  // before it on the CU, so the rows consumed at the end of group g were requested before group g-1's stores
+  // (one group ahead, the wait for them was a wait for the previous group's store drain)
+  fetch(g, I0{});
+  store_rows(I0{});
+  fetch(g + gridDim.x, I1{});
+  // 32 dropped stores (out-of-range offset) after it, as after every loop body: the first group's wait for
+  // slot 1 then counts past 32 stores like every later one (hipcc merges the entry path into the loop's count)
+#pragma unroll
+  for (int c = 0; c < 32; ++c) __builtin_amdgcn_raw_buffer_store_b64(u32x2{0u, 0u}, orsrc, 0x7ffffff0, 0, 0);
+  auto body = [&](auto PAR) {
+    constexpr int par = decltype(PAR)::value;
+    const int n = g / p.groups_per_img, oh0 = (g % p.groups_per_img) * CVR_TR, oh = oh0 + wave;
+    __syncthreads();                                   // input rows of g visible; stage reads of g-1 done
+    fetch(g + 2 * gridDim.x, PAR);                     // into the slot group g's rows were staged from
+    stamp(5);
+    unsigned short* const st_cur = ostage + (PIPE ? par * (64 * CVF_SEGS) : 0);
+    const unsigned short* const st_prev = ostage + (PIPE ? (par ^ 1) * (64 * CVF_SEGS) : 0);
+    f32x4 acc[CVF_NT][4];          // the bias rides in as the accumulators' initial value
+#pragma unroll
+    for (int t = 0; t < CVF_NT; ++t)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) acc[t][nt] = f32x4{bias_v[nt], bias_v[nt], bias_v[nt], bias_v[nt]};
+    bf16x8 af[2][CVF_NT];
+    auto load_a = [&](int ks, bf16x8 (&a)[CVF_NT]) {
+#pragma unroll
+      for (int t = 0; t < CVF_NT; ++t) {
+        const uint2* src = reinterpret_cast<const uint2*>(__builtin_assume_aligned(smem + abase[ks] + t * 32, 8));
+        const uint2 a0 = src[0], a1 = src[1];
+        a[t] = __builtin_bit_cast(bf16x8, u32x4{a0.x, a0.y, a1.x, a1.y});
+      }
+    };
+    // the order is pinned (sched_barrier): left to itself hipcc funnels every A fragment through one register
+    // quad (read -> lgkmcnt(0) -> 4 MFMAs -> read ...), which exposes the LDS latency 42 times per group.
+    // PIPE: each k-step also carries 6 of the previous group's 32 output chunks per wave (LDS read before the
+    // MFMAs, global store after them), so the store stream drains under the MFMAs instead of after them
+    constexpr int CPK = 6;
+    load_a(0, af[0]);
+#pragma unroll
+    for (int ks = 0; ks < CVR_NKS; ++ks) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (ks + 1 < CVR_NKS) load_a(ks + 1, af[(ks + 1) & 1]);
+      uint2 sv[CPK];
+      if constexpr (PIPE) {
+#pragma unroll
+        for (int i = 0; i < CPK; ++i)
+          if (ks * CPK + i < 32) sv[i] = chunk_read(st_prev, ks * CPK + i, max(prev_n4, 1));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < CVF_NT; ++t)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          acc[t][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks & 1][t], bw[nt][ks], acc[t][nt], 0, 0, 0);
+      if constexpr (PIPE) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < CPK; ++i)
+          if (ks * CPK + i < 32) chunk_store(sv[i], ks * CPK + i, prev_obase, prev_n4, noc);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    stamp(1);
+    // epilogue -> [oc][row * OW + ow] bf16 (4 consecutive pixels per lane: two dword writes, branch-free:
+    // pixel pairs past OW go to the trash word)
+#pragma unroll
+    for (int t = 0; t < CVF_NT; ++t) {
+      const int owb = t * 16 + (lane >> 4) * 4;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        float vv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) vv[r] = act_t<ACT>(acc[t][nt][r]);
+        unsigned* dst = reinterpret_cast<unsigned*>(st_cur + (nt * 16 + (lane & 15)) * CVF_SEGS + wave * p.OW + owb);
+        if (t + 1 < CVF_NT) {        // tiles 0..5 lie inside every row (OW > 96): constant LDS offsets
+          dst[0] = pack_bf16x2(vv[0], vv[1]);
+          dst[1] = pack_bf16x2(vv[2], vv[3]);
+        } else {
+          *(owb + 1 < p.OW ? dst : trash) = pack_bf16x2(vv[0], vv[1]);
+          *(owb + 3 < p.OW ? dst + 1 : trash) = pack_bf16x2(vv[2], vv[3]);
+        }
+      }
+    }
+    stamp(2);
+    __syncthreads();                                   // stage complete; every input-row read of g retired
+    stamp(3);
+    const int rows_valid = min(CVR_TR, p.OH - oh0);
+    prev_n4 = (rows_valid * p.OW) >> 2;
+    prev_obase = (int)((((long long)n * p.OC + oc0) * OHW + (long long)oh0 * p.OW) * 2);
+    if constexpr (!PIPE) {
+      uint2 v[32];
+#pragma unroll
+      for (int c = 0; c < 32; ++c) v[c] = chunk_read(st_cur, c, prev_n4);
+#pragma unroll
+      for (int c = 0; c < 32; ++c) chunk_store(v[c], c, prev_obase, prev_n4, noc);
+    }
+    stamp(4);
+    // rows of g + grid into the (now free) input buffer
+    if constexpr (par == 0) store_rows(I1{});
+    else store_rows(I0{});
+    (void)oh;
+  };
+  int it = 0;
+  while (g < p.ngroups) {
+    body(I0{});
+    g += gridDim.x;
+    ++it;
+    if (g >= p.ngroups) break;
+    body(I1{});
+    g += gridDim.x;
+    ++it;
+  }
+  if constexpr (PIPE) {
+    // the last group's chunks (its stage was completed before the loop's last barrier)
+    if (it > 0) {
+      const unsigned short* st_last = ostage + ((it + 1) & 1) * (64 * CVF_SEGS);
+      uint2 v[32];
+#pragma unroll
+      for (int c = 0; c < 32; ++c) v[c] = chunk_read(st_last, c, prev_n4);
+#pragma unroll
+      for (int c = 0; c < 32; ++c) chunk_store(v[c], c, prev_obase, prev_n4, noc);
+    }
+  }
+  if constexpr (DIAG) {
+    stamp(5);
+    tt[0] = t_prev - t_start;
+    if (lane == 0) {
+      unsigned long long* d = reinterpret_cast<unsigned long long*>(p.out) + (blockIdx.x * 4 + wave) * 8;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) d[i] = tt[i];
+    }
+  }
+}
+
 // Explicit im2col (the reference's materialised ImageToChunks/ImageBlockToMatrix path, kept for the
 // "materialise" plan and for testing). out[p][k] bf16 with ld = ldk (>= K, zero padded).
 __global__ void im2col_kernel(const unsigned short* X, unsigned short* out, int N, int C, int H, int W,
@@ -539,6 +841,7 @@ int nsdb_conv2d_variant = 0;         // row-kernel diagnostics (timing only)
 // 0 = one block per row group (short-lived blocks that the dispatcher can interleave with higher-priority
 // kernels when the conv shares the GPU with another job, e.g. gated into a GEMM's tail)
 int nsdb_conv2d_max_blocks = 512;
+int nsdb_conv2d_rowfull = 1;         // full-row kernel for 97 <= OW <= 112 (0: the two-pass row kernel, A/B)
 
 int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* out, int N, int C, int H,
                       int W, int OC, int KH, int KW, int stride, int pad, int dil, int ldw, int act,
@@ -576,6 +879,32 @@ int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* ou
       const int blocks = nsdb_conv2d_max_blocks > 0 ? std::min(q.ngroups, nsdb_conv2d_max_blocks) : q.ngroups;
       const dim3 grid(blocks, (OC + 63) / 64);
       const bool staged = nchw_out && !out_f32 && (p.OW & 1) == 0 && q.vec8 && ((p.OH % 4) * p.OW) % 4 == 0;
+      if (staged && q.variant == 0 && nsdb_conv2d_rowfull && q.ntiles == nsdb::CVF_NT && 4 * p.OW <= nsdb::CVF_SEGS) {
+        // one block of 4 waves per CU (one wave per SIMD), persistent over the row groups
+        const dim3 gridf(std::min(q.ngroups, nsdb_conv2d_max_blocks > 0 ? std::min(nsdb_conv2d_max_blocks, 256) : q.ngroups),
+                         (OC + 63) / 64);
+#define NSDB_CVF_LAUNCH(A) hipLaunchKernelGGL((nsdb::conv2d_rowfull_kernel<A, false, true>), gridf, dim3(256), 0, stream, q)
+        if (nsdb_conv2d_rowfull == 2 || nsdb_conv2d_rowfull == 3) {   // phase-stamp timing builds (diagnostic)
+          if (nsdb_conv2d_rowfull == 2)
+            hipLaunchKernelGGL((nsdb::conv2d_rowfull_kernel<nsdb::ACT_NONE, true, true>), gridf, dim3(256), 0, stream, q);
+          else
+            hipLaunchKernelGGL((nsdb::conv2d_rowfull_kernel<nsdb::ACT_NONE, true, false>), gridf, dim3(256), 0, stream, q);
+          return (int)hipGetLastError();
+        }
+        if (nsdb_conv2d_rowfull == 4) {   // unpipelined stores (A/B)
+          hipLaunchKernelGGL((nsdb::conv2d_rowfull_kernel<nsdb::ACT_NONE, false, false>), gridf, dim3(256), 0, stream, q);
+          return (int)hipGetLastError();
+        }
+        switch (act) {
+          case nsdb::ACT_RELU: NSDB_CVF_LAUNCH(nsdb::ACT_RELU); break;
+          case nsdb::ACT_SIGMOID: NSDB_CVF_LAUNCH(nsdb::ACT_SIGMOID); break;
+          case nsdb::ACT_EXP: NSDB_CVF_LAUNCH(nsdb::ACT_EXP); break;
+          case nsdb::ACT_TANH: NSDB_CVF_LAUNCH(nsdb::ACT_TANH); break;
+          default: NSDB_CVF_LAUNCH(nsdb::ACT_NONE); break;
+        }
+#undef NSDB_CVF_LAUNCH
+        return (int)hipGetLastError();
+      }
       if (q.variant != 0) {   // diagnostics build (timing only): runtime variant bits, no activation
         if (staged) hipLaunchKernelGGL((nsdb::conv2d_rows_kernel<nsdb::ACT_NONE, true, true>), grid, dim3(256), 0, stream, q);
         else hipLaunchKernelGGL((nsdb::conv2d_rows_kernel<nsdb::ACT_NONE, false, true>), grid, dim3(256), 0, stream, q);

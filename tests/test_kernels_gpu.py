@@ -236,3 +236,31 @@ def test_gemm_batched_broadcast_b_and_bias_matrix():
     Y = ops.gemm_nt(A, X.unsqueeze(0).expand(5, -1, -1), P, ops.BIAS_MAT, out_dtype=torch.float32)
     ref = A.float() @ X.float().t() + P
     assert (Y - ref).abs().max().item() / ref.abs().max().item() < 1e-4
+
+
+@pytest.mark.parametrize("rowfull", [0, 1], ids=["rows", "rowfull"])
+@pytest.mark.parametrize("cfg", [
+    dict(N=3, C=3, H=30, W=112, OC=64, KH=7, KW=7),    # headline geometry (7 pixel tiles per row)
+    dict(N=2, C=2, H=14, W=104, OC=70, KH=5, KW=3),    # OW = 102, partial second oc tile, OH % 4 == 2
+    dict(N=1, C=3, H=21, W=104, OC=16, KH=7, KW=7),    # OW = 98, one partial oc tile
+])
+def test_conv2d_rows_bf16_nchw(cfg, rowfull):
+    """The LDS-staged bf16 NCHW output path (what the conv2d job runs): the two-pass row kernel and the full-row
+    kernel (1 wave/SIMD, stores pipelined under the MFMAs) vs the fp32 reference, with a relu epilogue."""
+    from netsdb_amd import _ext
+
+    torch.manual_seed(5)
+    X = torch.randn(cfg["N"], cfg["C"], cfg["H"], cfg["W"], device=DEV).to(torch.bfloat16)
+    K = cfg["C"] * cfg["KH"] * cfg["KW"]
+    Wt = ops.pad_k(torch.randn(cfg["OC"], K, device=DEV) * 0.1).to(torch.bfloat16).contiguous()
+    bias = torch.randn(cfg["OC"], device=DEV)
+    old = _ext.hip().conv2d_rowfull(rowfull)
+    try:
+        y = ops.conv2d(X, Wt, bias, cfg["KH"], cfg["KW"], 1, 0, act=ops.ACT_RELU, nchw_out=True)
+        torch.cuda.synchronize()
+    finally:
+        _ext.hip().conv2d_rowfull(old)
+    assert y.dtype == torch.bfloat16
+    ref = ops.conv2d(X.cpu(), Wt.cpu(), bias.cpu(), cfg["KH"], cfg["KW"], 1, 0, act=ops.ACT_RELU, nchw_out=True,
+                     out_dtype=torch.float32)
+    _close(y.float().cpu(), ref, tol=1e-2)
