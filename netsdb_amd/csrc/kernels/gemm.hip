@@ -700,6 +700,11 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
       roff[2 + q][i] = tb < rows_b ? (KT ? tb * BK * 2 : (int)((long long)tb * p.ldb * 2)) : -1;
     }
 
+  // cache-policy bits of the operand DMAs (gfx950 CPol: sc0 1, nt 2, sc1 16): V15 nt on both; V16 sc1 (L1
+  // bypass) on both; V17 nt+sc1 on B only; V18 nt+sc1 on A only (hipBLASLt's MT256x256x64 streams one operand
+  // with `nt sc1`)
+  constexpr int AUX_A = V == 15 ? 2 : V == 16 ? 16 : V == 18 ? 18 : 0;
+  constexpr int AUX_B = V == 15 ? 2 : V == 16 ? 16 : V == 17 ? 18 : 0;
   auto stage = [&](int buf, int slot, int u) {
     if constexpr (V == 4) return;
     const int k = kbeg + u * BK + kc;
@@ -716,8 +721,10 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
                                               : ro + (slot < 2 ? ks : ks - kb0) * 2) : OOB;
       // V15: non-temporal operand stream (aux nt): the once-streamed panels do not displace the split-K slabs
       // (and other resident sets) from the Infinity Cache
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(slot < 2 ? ra : rb, (lds_void*)(dst + (i * 64 + wave * 8) * 128), 16,
-                                               voff, 0, 0, V == 15 ? 2 : 0);
+      if (slot < 2)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)(dst + (i * 64 + wave * 8) * 128), 16, voff, 0, 0, AUX_A);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(dst + (i * 64 + wave * 8) * 128), 16, voff, 0, 0, AUX_B);
     }
   };
 
@@ -1568,6 +1575,12 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
     hipLaunchKernelGGL(nsdb::gemm_nt_256_w4_kernel<4>, grid, dim3(256), 0, stream, p);
   else if (cfg == 20)   // 8-phase with non-temporal operand loads
     hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<15>, grid, dim3(512), 0, stream, p);
+  else if (cfg == 21)   // 8-phase, sc1 (L1 bypass) operand loads
+    hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<16>, grid, dim3(512), 0, stream, p);
+  else if (cfg == 22)   // 8-phase, nt sc1 on B
+    hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<17>, grid, dim3(512), 0, stream, p);
+  else if (cfg == 23)   // 8-phase, nt sc1 on A
+    hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<18>, grid, dim3(512), 0, stream, p);
   else if (cfg == 18)   // diagnostic: all splits stream one shared K window (MALL-resident operands)
     hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<13>, grid, dim3(512), 0, stream, p);
   else if (cfg == 19)   // diagnostic: every workgroup cycles over 2 k-tiles (L2-resident operands)

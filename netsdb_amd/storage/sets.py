@@ -649,9 +649,12 @@ class DenseMatrixSet(UserSet):
             self.define(int(b0["total_rows"][0]), int(b0["total_cols"][0]), int(b0["row_nums"][0]),
                         int(b0["col_nums"][0]), dtype=batch.columns["data"].dtype if isinstance(
                             batch.columns["data"], torch.Tensor) else torch.float32)
-        rows = batch.columns["block_row"].tolist()
-        cols = batch.columns["block_col"].tolist()
         data = batch.columns["data"]
+        todo = self._scatter_full_blocks(batch) if isinstance(data, torch.Tensor) else None
+        rows = batch.columns["block_row"].tolist() if todo is None else batch.columns["block_row"][todo].tolist()
+        cols = batch.columns["block_col"].tolist() if todo is None else batch.columns["block_col"][todo].tolist()
+        if todo is not None:
+            data = data[todo]
         for i, (r, c) in enumerate(zip(rows, cols)):
             r0 = r * self.block_rows - self.row_offset
             c0 = c * self.block_cols
@@ -660,6 +663,29 @@ class DenseMatrixSet(UserSet):
             w = min(blk.shape[1], self.total_cols - c0)
             if h > 0 and w > 0:
                 self.panel[r0:r0 + h, c0:c0 + w] = blk[:h, :w].to(self.panel.device, self.panel.dtype)
+
+    def _scatter_full_blocks(self, batch: RecordBatch):
+        """Vectorised part of add_batch: every block that lies wholly inside the panel and on the block grid is
+        written by ONE index_put over a [block-rows, br, block-cols, bc] strided view of the panel (no per-block
+        host loop). Returns the indices of the remaining (edge / off-grid) blocks for the element-wise path, or
+        None when the batch does not have the uniform [n, br, bc] form (everything goes element-wise)."""
+        data = batch.columns["data"]
+        br, bc = self.block_rows, self.block_cols
+        if data.dim() != 3 or data.shape[1] != br or data.shape[2] != bc or self.row_offset % br != 0 or \
+                self.panel.dim() != 2 or self.panel.stride(1) != 1:
+            return None
+        dev = self.panel.device
+        r = batch.columns["block_row"].to(dev, torch.long) - self.row_offset // br
+        c = batch.columns["block_col"].to(dev, torch.long)
+        nfr, nfc = self.local_rows // br, self.total_cols // bc
+        full = (r >= 0) & (r < nfr) & (c >= 0) & (c < nfc)
+        if nfr > 0 and nfc > 0:
+            ld = self.panel.stride(0)
+            grid = self.panel.as_strided((nfr, br, nfc, bc), (br * ld, ld, bc, 1))
+            sel = full.nonzero().flatten()
+            if sel.numel():
+                grid[r[sel], :, c[sel], :] = data[sel.to(data.device)].to(dev, self.panel.dtype)
+        return (~full).nonzero().flatten().to(batch.columns["block_row"].device)
 
     def resolve_shared(self):
         """Scatter the linked shared blocks (metadata remapped) into this set's dense panel — the

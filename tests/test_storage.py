@@ -180,3 +180,27 @@ def test_pinned_host_tier_spill_and_reload(tmp_path):
     assert c.storage.device_bytes <= c.storage.device_budget + (1 << 16)
     c.remove_set("d", "x")
     assert tier.used == 0
+
+
+def test_dense_add_batch_vectorised_matches_elementwise():
+    """DenseMatrixSet.add_batch scatters whole interior blocks with one index_put over a strided block view and
+    only the ragged edge blocks element-wise: same panel as the per-block loop, blocks in any order."""
+    import tempfile
+
+    from netsdb_amd.client import PDBClient
+    from netsdb_amd.models.blocks import load_tensor, to_tensor
+
+    c = PDBClient(root=tempfile.mkdtemp(), device="cpu")
+    c.create_database("db")
+    g = torch.Generator().manual_seed(3)
+    for rows, cols, br, bc in ((300, 500, 10, 100), (97, 130, 16, 32), (64, 64, 64, 64), (5, 7, 8, 8)):
+        a = torch.randn(rows, cols, generator=g)
+        load_tensor(c, "db", "src", a, br, bc, dtype=torch.float32)
+        blocks = c.storage.get_set("db", "src").to_blocks()
+        perm = torch.randperm(blocks.n, generator=g)
+        load_tensor(c, "db", "dst", torch.zeros(rows, cols), br, bc, dtype=torch.float32)
+        dst = c.storage.get_set("db", "dst")
+        dst.add_batch(blocks.take(perm))
+        torch.testing.assert_close(to_tensor(c, "db", "dst"), a, rtol=0, atol=0)
+        c.remove_set("db", "src")
+        c.remove_set("db", "dst")
