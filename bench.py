@@ -187,12 +187,14 @@ def main():
         step(i)
     client.wait_jobs()
     sync()
+    coll0 = ctx.stats.get("collectives", 0)
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
     client.wait_jobs()
     sync()
     dt = time.perf_counter() - t0
+    coll_per_step = (ctx.stats.get("collectives", 0) - coll0 - 1) / max(1, args.steps)   # minus sync()'s barrier
     dt = ctx.all_reduce_scalar(dt, "max")
     rows_local = local_rows + cfg["images"]
     rows_total = ctx.all_reduce_scalar(float(rows_local), "sum") * args.steps
@@ -225,6 +227,7 @@ def main():
                 "settle_steps_untimed": settle_steps,
                 "conv_overlap": args.overlap,
                 "ff_steps_in_flight": inflight,
+                "collectives_per_step": round(coll_per_step, 2),
             },
         }
         print(json.dumps(res), flush=True)

@@ -228,9 +228,13 @@ class AdaptivePlanner:
                         lst.append(a)
         # pending sources: [ts, first consumer (None = all via consumers map), cost, kind]
         self.pending: List[list] = []
-        for a in atoms:
-            if a["type"] == "SCAN":
-                self.pending.append([a["output"]["name"], None, float(size_of_scan(a)), "scan", a])
+        # source costs only matter when there is a choice to make (several sources, or a join whose side /
+        # broadcast decision reads them): a single-source pipeline skips the sizing, which on a cluster is a
+        # collective per job (every rank sees the same atoms, so every rank skips it)
+        scans = [a for a in atoms if a["type"] == "SCAN"]
+        costed = len(scans) > 1 or any(a["type"] in ("JOIN", "HASHLEFT", "HASHRIGHT", "HASHONE") for a in atoms)
+        for a in scans:
+            self.pending.append([a["output"]["name"], None, float(size_of_scan(a)) if costed else 0.0, "scan", a])
         self.built: Dict[str, dict] = {}
         self.penalized: Dict[str, float] = {}
         self.decisions: List[dict] = []

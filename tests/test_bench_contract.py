@@ -40,3 +40,6 @@ def test_bench_two_ranks_gloo():
     d = _last_json(r.stdout)
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 * (64 + 4)
     assert d["config"]["check"]["ok"] is True
+    # weak scaling with a replicated model: the timed steps are rank-local (no collective inside a step; the
+    # conv job's single-source plan skips the cluster-wide source sizing)
+    assert d["config"]["collectives_per_step"] == 0
