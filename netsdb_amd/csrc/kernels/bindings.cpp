@@ -49,6 +49,8 @@ int nsdb_embedding_bag(const void* table, int t_f32, const long long* idx, const
 int nsdb_dedup_splits(long long nblocks, long long bytes_per_block);
 int nsdb_block_hash(const void* data, long long nblocks, long long words, int S, unsigned long long* partial,
                     hipStream_t st);
+int nsdb_block_simcount(const void* pool, const long long* cand, const void* query, long long nblocks, long long elems,
+                        int bc, int h, int w, float fp, int is_f32, int S, unsigned* partial, hipStream_t st);
 int nsdb_block_maxdiff(const void* pool, const long long* cand, const void* blks, long long nblocks, long long elems,
                        int is_f32, int S, float* partial, hipStream_t st);
 int nsdb_str_hash(const void* bytes, const int64_t* off, int64_t n, uint64_t* out, hipStream_t st);
@@ -520,6 +522,30 @@ torch::Tensor block_maxdiff_partial(torch::Tensor pool, torch::Tensor cand, torc
   return out;
 }
 
+// approximate dedup: per-(candidate, split) counts of elements within fp of one query block over its h x w corner
+torch::Tensor block_simcount_partial(torch::Tensor pool, torch::Tensor cand, torch::Tensor query, int64_t bc, int64_t h,
+                                     int64_t w, double fp) {
+  TORCH_CHECK(pool.is_cuda() && pool.is_contiguous() && query.is_contiguous() && cand.is_contiguous(), "device, contiguous");
+  TORCH_CHECK(pool.scalar_type() == query.scalar_type(), "pool/query dtype");
+  TORCH_CHECK(pool.scalar_type() == torch::kBFloat16 || pool.scalar_type() == torch::kFloat32, "bf16 or f32");
+  TORCH_CHECK(cand.scalar_type() == torch::kInt64 && cand.dim() == 1, "cand i64 [n]");
+  const int64_t elems = query.numel();
+  TORCH_CHECK(pool.dim() >= 1 && pool.size(0) > 0 && pool.numel() == pool.size(0) * elems, "pool rows of query size");
+  TORCH_CHECK(elems % bc == 0 && h >= 0 && w >= 0 && h * bc <= elems && w <= bc, "block geometry");
+  const int64_t n = cand.size(0);
+  const bool f32 = pool.scalar_type() == torch::kFloat32;
+  const int S = nsdb_dedup_splits(std::max<int64_t>(n, 1), elems * pool.element_size());
+  auto out = torch::empty({n, S}, cand.options().dtype(torch::kInt32));
+  for (int64_t b0 = 0; b0 < n; b0 += 65535) {
+    const int64_t nb = std::min<int64_t>(65535, n - b0);
+    check_rc(nsdb_block_simcount(pool.data_ptr(), (const long long*)cand.data_ptr<int64_t>() + b0, query.data_ptr(), nb,
+                                 elems, (int)bc, (int)h, (int)w, (float)fp, f32, S,
+                                 reinterpret_cast<unsigned*>(out.data_ptr<int>()) + b0 * S, cur_stream()),
+             "block_simcount");
+  }
+  return out;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -579,6 +605,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embedding_bag", &embedding_bag, py::arg("table"), py::arg("idx"), py::arg("offsets"),
         py::arg("weights") = py::none(), py::arg("mode") = 0);
   m.def("block_hash_partial", &block_hash_partial, "dedup: per-(block, split) partial content-hash sums");
+  m.def("block_simcount_partial", &block_simcount_partial,
+        "approximate dedup: per-(candidate, split) counts of elements within fp of a query block");
   m.def("block_maxdiff_partial", &block_maxdiff_partial, "dedup: per-(block, split) max |pool[cand] - blk|");
   m.def("str_hash", &str_hash, "64-bit hash per string of a device string column");
   m.def("str_like", &str_like, "SQL LIKE over a device string column (segments of the pattern bytes)");

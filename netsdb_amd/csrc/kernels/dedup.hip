@@ -7,6 +7,9 @@
 //                    wrap mod 2^64, so the result is bit-identical to the torch reference on any device).
 //  * block_maxdiff — max |pool[cand[b]] - blks[b]| per block without gathering the candidate blocks
 //                    (content verification of a hash hit); per-(block, split) partials again.
+//  * block_simcount — approximate-dedup similarity (indexing/deduplicator.py): the number of elements of
+//                    candidate pool[cand[b]] within fp of ONE query block, over the valid h x w corner of
+//                    the br x bc blocks (padded edge blocks compare only their real part).
 // Blocks are streamed with 16-B loads; S workgroups per block so a launch has >> 256 workgroups even
 // for a few hundred 2-MB word2vec blocks.
 #include "common.h"
@@ -82,6 +85,43 @@ __global__ void __launch_bounds__(256) block_maxdiff_kernel(const T* __restrict_
   if (threadIdx.x == 0) partial[(long long)b * S + s] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 }
 
+// pool: [*, elems] T, cand: [nblocks] i64, query: [elems] T; elems = br * bc; counts the elements e of the
+// h x w corner (row e / bc < h, column e % bc < w) with |pool[cand[b]][e] - query[e]| <= fp.
+// grid (S, nblocks); elems * sizeof(T) % 16 == 0.
+template <typename T>
+__global__ void __launch_bounds__(256) block_simcount_kernel(const T* __restrict__ pool, const long long* __restrict__ cand,
+                                                             const T* __restrict__ query, long long elems, int bc,
+                                                             long long valid_end, int w, float fp,
+                                                             unsigned* __restrict__ partial) {
+  constexpr int V = 16 / sizeof(T);
+  const int b = blockIdx.y, s = blockIdx.x, S = gridDim.x;
+  const long long q = elems / V, per = (q + S - 1) / S;
+  const long long q0 = (long long)s * per, q1 = q0 + per < q ? q0 + per : q;
+  const u32x4v* pa = reinterpret_cast<const u32x4v*>(pool + cand[b] * elems);
+  const u32x4v* pq = reinterpret_cast<const u32x4v*>(query);
+  unsigned cnt = 0;
+  for (long long i = q0 + threadIdx.x; i < q1; i += blockDim.x) {
+    const u32x4v va = __builtin_nontemporal_load(pa + i), vq = pq[i];
+    const T* ea = reinterpret_cast<const T*>(&va);
+    const T* eq = reinterpret_cast<const T*>(&vq);
+    const long long e0 = i * V;
+    int col = (int)(e0 % bc);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const bool valid = (e0 + k) < valid_end && col < w;
+      cnt += (valid && fabsf(to_f<T>(ea[k]) - to_f<T>(eq[k])) <= fp) ? 1u : 0u;
+      col = col + 1 == bc ? 0 : col + 1;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+  __shared__ unsigned red[4];
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[wv] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[(long long)b * S + s] = red[0] + red[1] + red[2] + red[3];
+}
+
 }  // namespace nsdb
 
 extern "C" {
@@ -112,6 +152,21 @@ int nsdb_block_maxdiff(const void* pool, const long long* cand, const void* blks
   else
     hipLaunchKernelGGL(nsdb::block_maxdiff_kernel<unsigned short>, dim3(S, (unsigned)nblocks), dim3(256), 0, st,
                        (const unsigned short*)pool, cand, (const unsigned short*)blks, elems, partial);
+  return (int)hipGetLastError();
+}
+
+int nsdb_block_simcount(const void* pool, const long long* cand, const void* query, long long nblocks, long long elems,
+                        int bc, int h, int w, float fp, int is_f32, int S, unsigned* partial, hipStream_t st) {
+  if (nblocks <= 0) return 0;
+  if ((elems * (is_f32 ? 4 : 2)) % 16 || nblocks > 65535 || S <= 0 || bc <= 0) return -1;
+  const long long valid_end = (long long)h * bc;
+  if (is_f32)
+    hipLaunchKernelGGL(nsdb::block_simcount_kernel<float>, dim3(S, (unsigned)nblocks), dim3(256), 0, st,
+                       (const float*)pool, cand, (const float*)query, elems, bc, valid_end, w, fp, partial);
+  else
+    hipLaunchKernelGGL(nsdb::block_simcount_kernel<unsigned short>, dim3(S, (unsigned)nblocks), dim3(256), 0, st,
+                       (const unsigned short*)pool, cand, (const unsigned short*)query, elems, bc, valid_end, w, fp,
+                       partial);
   return (int)hipGetLastError();
 }
 
