@@ -68,6 +68,10 @@ class TailTrigger:
     def __init__(self, device):
         self.device = torch.device(device)
         self.flag = torch.zeros(1, dtype=torch.int32, device=self.device) if self.device.type == "cuda" else None
+        if self.flag is not None:
+            # the command processor may evaluate a gate on another stream before a stream-ordered zero-fill has
+            # run: a recycled allocation still holding a stale value >= the first epoch would open the gate early
+            torch.cuda.synchronize(self.device)
         self.epoch = 0
         self.armed = False
         self.gated = 0       # jobs that were actually gated (stats / tests)
@@ -80,6 +84,7 @@ class TailTrigger:
         self.epoch = self.epoch % 0x7FFFFFFF + 1     # flag values only grow (atomic max), never wrap to 0
         if self.epoch == 1 and self.gated:           # wrapped: restart from a zero flag
             self.flag.zero_()
+            torch.cuda.synchronize(self.device)
         _ext.hip().tail_trigger_arm(self.flag, self.epoch)
         self.armed = True
         return self
