@@ -48,6 +48,11 @@ class ClusterContext:
         self.health = None
         self._schema_cache: Dict[int, dict] = {}
         self.stats = {"collectives": 0, "schema_cache_hits": 0, "schema_exchanges": 0}
+        # single-tensor collectives (all_gather_into_tensor / reduce_scatter_tensor into one contiguous buffer):
+        # RCCL's native form; gloo implements them too in this torch, so the CPU multi-rank tests run the SAME
+        # branches the GPUs take. NSDB_TENSOR_COLLECTIVES=0 selects the list-based fallback (tested as well).
+        env = os.environ.get("NSDB_TENSOR_COLLECTIVES")
+        self.tensor_collectives = (env != "0") if env is not None else backend in ("nccl", "gloo")
 
     @property
     def distributed(self) -> bool:
@@ -193,10 +198,11 @@ class ClusterContext:
         if not self.distributed:
             return t
         cd = self._comm_device()
-        if self.backend == "nccl" and len(set(counts)) == 1:
-            out = t.new_empty((counts[self.rank],) + tuple(t.shape[1:]))
-            self._coll(dist.reduce_scatter_tensor, out, t.contiguous(), op=dist.ReduceOp.SUM)
-            return out
+        if self.tensor_collectives and len(set(counts)) == 1:
+            src = t.to(cd).contiguous()
+            out = src.new_empty((counts[self.rank],) + tuple(t.shape[1:]))
+            self._coll(dist.reduce_scatter_tensor, out, src, op=dist.ReduceOp.SUM)
+            return out.to(t.device)
         full = t.to(cd).contiguous().clone()
         self._coll(dist.all_reduce, full)
         s = sum(counts[: self.rank])

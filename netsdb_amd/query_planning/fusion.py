@@ -340,7 +340,7 @@ class MatmulNode(Node):
         step = (step + 255) // 256 * 256
         bounds = [(n0, min(N, n0 + step)) for n0 in range(0, N, step)]
         out = torch.empty((M, N) if phys_is_c else (N, M), dtype=odt, device=dev)
-        nccl = ctx.backend == "nccl"
+        nccl = ctx.tensor_collectives            # one [ws, nc, kseg] buffer (RCCL's form; gloo too)
 
         def start(c):
             n0, n1 = bounds[c]
@@ -349,7 +349,8 @@ class MatmulNode(Node):
                 ctx.health.check()
             ctx.stats["collectives"] += 1
             if nccl:
-                dst = torch.empty(ws, n1 - n0, kseg, dtype=src.dtype, device=cd)
+                # concatenated form [ws * nc, kseg] (every backend accepts it; viewed as [ws, nc, kseg] below)
+                dst = torch.empty(ws * (n1 - n0), kseg, dtype=src.dtype, device=cd)
                 return dst, dist.all_gather_into_tensor(dst, src, async_op=True)
             parts = [torch.empty_like(src) for _ in range(ws)]
             return parts, dist.all_gather(parts, src, async_op=True)
@@ -360,7 +361,7 @@ class MatmulNode(Node):
             if c + 1 < len(bounds):
                 pending = start(c + 1)        # next chunk's collective overlaps this chunk's GEMM
             ctx._wait(work)
-            g = got if nccl else torch.stack(got)             # [ws, nc, kseg]: rank s's K slab of each row
+            g = got.view(ws, n1 - n0, kseg) if nccl else torch.stack(got)   # [ws, nc, kseg]: rank s's K slab
             g = g.to(dev)
             b = None
             if bias_t is not None:
@@ -416,7 +417,7 @@ class MatmulNode(Node):
         per = (nb + ws - 1) // ws
         counts = [max(0, min(R, (s + 1) * per * blk) - min(R, s * per * blk)) for s in range(ws)]
         off = min(R, r * per * blk)
-        if ctx.backend == "nccl" and len(set(counts)) > 1:
+        if ctx.tensor_collectives and len(set(counts)) > 1:
             eq = per * blk
             Pp = torch.empty(eq * ws, Ccols, dtype=torch.float32, device=X.device)
             Pp[R:].zero_()

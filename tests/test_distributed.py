@@ -118,7 +118,7 @@ def _la_dist_scenario(ctx, out_dir):
     Bm = torch.rand(40, 24, generator=g) - 0.5
     B.load_tensor(c, "LA_db", "A", A, 8, 8, dtype=torch.float32, partition_rows=True)
     B.load_tensor(c, "LA_db", "B", Bm, 8, 8, dtype=torch.float32, partition_rows=True)
-    res = {"local_rows": c.get_set("LA_db", "A").local_rows}
+    res = {"local_rows": c.get_set("LA_db", "A").local_rows, "tensor_collectives": ctx.tensor_collectives}
     for tag, jcls, ref in (("mul", L.LAMultiply1Join, A @ Bm), ("tmul", L.LATransposeMultiply1Join, A.t() @ Bm)):
         c.create_set("LA_db", f"C_{tag}", None, dense=True)
         j = jcls()
@@ -133,8 +133,14 @@ def _la_dist_scenario(ctx, out_dir):
 
 
 @pytest.mark.timeout(300)
-def test_distributed_la_partitioned_matmuls():
+@pytest.mark.parametrize("tensor_coll", ["1", "0"], ids=["tensor-collectives", "list-collectives"])
+def test_distributed_la_partitioned_matmuls(tensor_coll, monkeypatch):
+    """A %*% B over the all-gathered N-chunk pipeline and A '* B over the K-split reduce-scatter, with the
+    single-tensor collectives (all_gather_into_tensor / reduce_scatter_tensor: the branches RCCL runs) and with
+    the list-based fallback."""
+    monkeypatch.setenv("NSDB_TENSOR_COLLECTIVES", tensor_coll)
     r0, r1 = _run("_la_dist_scenario")
+    assert r0["tensor_collectives"] == (tensor_coll == "1")
     assert r0["local_rows"] == 24 and r1["local_rows"] == 16
     for r in (r0, r1):
         assert r["mul"] < 1e-4 and r["tmul"] < 1e-4, r
