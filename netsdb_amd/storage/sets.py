@@ -678,6 +678,8 @@ class DenseMatrixSet(UserSet):
         r = batch.columns["block_row"].to(dev, torch.long) - self.row_offset // br
         c = batch.columns["block_col"].to(dev, torch.long)
         nfr, nfc = self.local_rows // br, self.total_cols // bc
+        if r.numel() > 1 and torch.unique(r * max(1, nfc + 1) + c).numel() < r.numel():
+            return None      # a block written twice: keep the element-wise path's last-writer-wins order
         full = (r >= 0) & (r < nfr) & (c >= 0) & (c < nfc)
         if nfr > 0 and nfc > 0:
             ld = self.panel.stride(0)
