@@ -80,6 +80,10 @@ def main():
     ap.add_argument("--job-priority", type=int, default=None,
                     help="HIP stream priority of the conv2d job stream (default -1 = high; 0 in tail mode, where the "
                          "FF jobs run on a high-priority stream instead)")
+    ap.add_argument("--graph", action="store_true",
+                    help="record one whole step (FF jobs + conv2d job) into a HIP graph after the warmup and time its "
+                         "replays (PDBClient.capture_job: no host work per step; the dropout seed of the recorded "
+                         "step is reused)")
     ap.add_argument("--conv-kernel", choices=["rows", "rowfull"], default=None,
                     help="conv2d row kernel: two-pass 2-waves/SIMD (rows) or full-row 1-wave/SIMD with stores "
                          "pipelined under the MFMAs (rowfull); default: the library default")
@@ -187,10 +191,19 @@ def main():
         step(i)
     client.wait_jobs()
     sync()
+    captured = None
+    if args.graph and dev.type == "cuda":
+        captured = client.capture_job(step, args.warmup, inputs=[("ff", "inputs"), ("conv2d", "img")])
+        for _ in range(3):
+            captured.replay()
+        sync()
     coll0 = ctx.stats.get("collectives", 0)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(args.warmup + i)
+        if captured is not None:
+            captured.replay()
+        else:
+            step(args.warmup + i)
     client.wait_jobs()
     sync()
     dt = time.perf_counter() - t0
@@ -228,6 +241,7 @@ def main():
                 "conv_overlap": args.overlap,
                 "ff_steps_in_flight": inflight,
                 "collectives_per_step": round(coll_per_step, 2),
+                "graph_replay": captured is not None,
             },
         }
         print(json.dumps(res), flush=True)

@@ -426,6 +426,14 @@ class PDBClient:
         self.ctx.barrier()
 
     # ------------------------------------------------------------------ concurrent jobs
+    def capture_job(self, fn, *args, warmup: int = 1, inputs=(), **kwargs):
+        """Record ``fn(*args, **kwargs)`` (a job-issuing callable) into a HIP graph and return a
+        :class:`~netsdb_amd.execution.graphs.CapturedJob` whose ``replay()`` re-runs its kernels with no host
+        work (pre-compiled workloads, taken to the kernel-launch level; see that module for the contract)."""
+        from .execution.graphs import CapturedJob
+
+        return CapturedJob(self, fn, *args, warmup=warmup, inputs=inputs, **kwargs)
+
     def arm_tail_trigger(self):
         """Arm the tail trigger of the next long GEMM this client enqueues; pass the returned trigger as
         ``submit_job(..., start_on=trigger)`` to start an independent job in that GEMM's tail (see

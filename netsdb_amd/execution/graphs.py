@@ -1,0 +1,70 @@
+"""Captured jobs: a job's whole kernel sequence recorded once into a HIP graph and replayed.
+
+Reference: src/queryPlanning/headers/PreCompiledWorkload.h + QuerySchedulerServer's pre-compiled
+workloads (plan once, re-run many times). ``execute_computations(pre_compile=True)`` already caches the
+compiled TCAP / physical plan; a captured job goes one step further on the MI355X: the engine's host work
+(planning, fusion pattern matching, catalog bookkeeping, Python dispatch of every kernel) runs ONCE under
+stream capture, and every later run is a single ``hipGraphLaunch`` of the recorded kernels — the launch-bound
+inner loop of small-batch serving (a few 10-us kernels per request) no longer waits on the host.
+
+Contract (as for any HIP graph):
+  * the job must be host-sync free (the fused engine paths are: no ``.item()`` / ``.tolist()`` on device
+    tensors, tested by tests/test_distributed.py's guard and tests/test_graphs.py);
+  * a replay re-runs the captured kernels on the SAME device buffers: new inputs are written in place into the
+    input sets' tensors (``CapturedJob.input(db, set)`` returns the panel to ``copy_`` into; declare those sets
+    with ``inputs=[(db, set), ...]`` so that their memoised derivations are recorded too), outputs appear in
+    the output sets' tensors captured by the recording run; host-side values baked into kernel arguments
+    (e.g. a dropout seed) are those of the recording run;
+  * the catalog / set metadata reflect the recording run (a replay changes only device memory).
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import torch
+
+
+class CapturedJob:
+    def __init__(self, client, fn: Callable, *args, warmup: int = 1, inputs=(), **kwargs):
+        self.client = client
+        self.device = torch.device(client.device)
+        if self.device.type != "cuda":
+            raise RuntimeError("CapturedJob needs a GPU device (HIP graph capture)")
+        self.fn, self.args, self.kwargs = fn, args, kwargs
+        self.stream = torch.cuda.Stream(self.device)
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.stream):
+            for _ in range(max(1, warmup)):          # materialise derived weights / plans / workspaces first
+                fn(*args, **kwargs)
+        torch.cuda.synchronize(self.device)
+        # derivations (re-layouts / casts memoised by ops.derived) of the declared input sets are recomputed
+        # inside the graph, so a replay sees new inputs written into the input panels; the model's weights
+        # keep their cached derivations (recorded as plain reads)
+        from .. import ops
+
+        self.inputs = [tuple(x) for x in inputs]
+        keys = {self.input(db, name).untyped_storage().data_ptr() for db, name in self.inputs}
+        ops._NO_CACHE_STORAGES.update(keys)
+        try:
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph, stream=self.stream):
+                self.result = fn(*args, **kwargs)
+        finally:
+            ops._NO_CACHE_STORAGES.difference_update(keys)
+        torch.cuda.synchronize(self.device)
+        self.replays = 0
+
+    def input(self, db: str, set_name: str) -> torch.Tensor:
+        """The device tensor a replay reads for a dense input set (write new inputs into it in place)."""
+        s = self.client.storage.get_set(db, set_name)
+        return s.panel
+
+    def replay(self, stream: Optional["torch.cuda.Stream"] = None):
+        """Launch the recorded kernels (stream-ordered after the caller's stream; returns immediately)."""
+        cur = stream or torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            self.graph.replay()
+        cur.wait_stream(self.stream)
+        self.replays += 1
+        return self.result

@@ -155,6 +155,9 @@ def gemm_splits(M, N, K, batch=1) -> int:
 _DERIVED: "OrderedDict" = None
 
 
+_NO_CACHE_STORAGES: set = set()      # storages whose derivations are recomputed (execution/graphs.py inputs)
+
+
 def derived(t: torch.Tensor, tag: str, fn):
     """Memoise a tensor derived from an unchanged source tensor (model weights / biases converted or
     re-laid-out once, not on every inference call). Keyed by storage pointer, in-place version
@@ -162,6 +165,8 @@ def derived(t: torch.Tensor, tag: str, fn):
     global _DERIVED
     from collections import OrderedDict
 
+    if _NO_CACHE_STORAGES and t.untyped_storage().data_ptr() in _NO_CACHE_STORAGES:
+        return fn(t)        # a captured job's input: the derivation must be part of the recorded kernels
     if _DERIVED is None:
         _DERIVED = OrderedDict()
     key = (tag, t.data_ptr(), t._version, tuple(t.shape), tuple(t.stride()), t.dtype, str(t.device))
