@@ -43,7 +43,7 @@ class CapturedJob:
         from .. import ops
 
         self.inputs = [tuple(x) for x in inputs]
-        keys = {self.input(db, name).untyped_storage().data_ptr() for db, name in self.inputs}
+        keys = {t.untyped_storage().data_ptr() for db, name in self.inputs for t in self.input_tensors(db, name)}
         ops._NO_CACHE_STORAGES.update(keys)
         try:
             self.graph = torch.cuda.CUDAGraph()
@@ -54,17 +54,31 @@ class CapturedJob:
         torch.cuda.synchronize(self.device)
         self.replays = 0
 
+    def input_tensors(self, db: str, set_name: str):
+        """Every device tensor a replay reads for an input set: a dense set's panel, or the tensor columns of
+        a paged set's resident pages (write new inputs into them in place)."""
+        s = self.client.storage.get_set(db, set_name)
+        if hasattr(s, "panel") and s.panel is not None:
+            return [s.panel]
+        out = []
+        for pg in getattr(s, "pages", []):
+            if pg.batch is not None:
+                out.extend(v for v in pg.batch.columns.values() if isinstance(v, torch.Tensor))
+        return out
+
     def input(self, db: str, set_name: str) -> torch.Tensor:
         """The device tensor a replay reads for a dense input set (write new inputs into it in place)."""
-        s = self.client.storage.get_set(db, set_name)
-        return s.panel
+        ts = self.input_tensors(db, set_name)
+        if len(ts) != 1:
+            raise ValueError(f"{db}.{set_name} is held in {len(ts)} tensors; use input_tensors()")
+        return ts[0]
 
     def replay(self, stream: Optional["torch.cuda.Stream"] = None):
         """Launch the recorded kernels (stream-ordered after the caller's stream; returns immediately)."""
+        # launched straight onto the caller's stream (a graph is not tied to its capture stream): no cross-stream
+        # event pair per replay, so back-to-back replays queue like eagerly enqueued kernels
         cur = stream or torch.cuda.current_stream(self.device)
-        self.stream.wait_stream(cur)
-        with torch.cuda.stream(self.stream):
+        with torch.cuda.stream(cur):
             self.graph.replay()
-        cur.wait_stream(self.stream)
         self.replays += 1
         return self.result
