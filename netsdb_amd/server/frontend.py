@@ -20,6 +20,8 @@ import threading
 import traceback
 from typing import Any, Callable, Dict, List, Optional, Sequence
 
+import torch
+
 from ..objects.record import PDBObject, lookup_type
 from .protocol import recv_msg, send_msg
 
@@ -111,6 +113,48 @@ class Dispatcher:
         self.jobs = jobs
         self.health = health
         self.registry = registry or UDFRegistry()
+        self.prepared: Dict[int, Any] = {}      # handle -> (CapturedJob | eager closure, input sets)
+
+    def _prepare(self, req: dict):
+        """Prepared (captured) job: the registered job's kernels recorded into a HIP graph on a GPU server
+        (execution/graphs.py), a plain closure on a CPU server; run_prepared then only feeds inputs + replays."""
+        c = self.client
+        fn = self._job(req["job"])
+        kw = _kwargs(req)
+        inputs = [tuple(x) for x in (req.get("inputs") or [])]
+        if not all(len(x) == 2 and all(isinstance(v, str) for v in x) for x in inputs):
+            raise ValueError("inputs must be [db, set] pairs")
+        if torch.device(c.device).type == "cuda":
+            runner = c.capture_job(fn, c, inputs=inputs, **kw)
+        else:
+            fn(c, **kw)
+            runner = (lambda: fn(c, **kw))
+        h = len(self.prepared) + 1
+        self.prepared[h] = (runner, inputs)
+        return {"handle": h, "graph": not callable(runner)}
+
+    def _run_prepared(self, req: dict):
+        c = self.client
+        h = int(req["handle"])
+        if h not in self.prepared:
+            raise KeyError(f"no prepared job {h}")
+        runner, inputs = self.prepared[h]
+        for f in req.get("feeds") or []:
+            key = (f["db"], f["set"])
+            if key not in inputs:
+                raise ValueError(f"{key} is not an input of prepared job {h}")
+            t = _dec_tensor(f)
+            s = c.storage.get_set(*key)
+            dst = s.panel
+            if t.dim() != 2 or t.shape[0] > dst.shape[0] or t.shape[1] > dst.shape[1]:
+                raise ValueError(f"feed {tuple(t.shape)} does not fit the input panel {tuple(dst.shape)}")
+            dst[: t.shape[0], : t.shape[1]].copy_(t.to(dst.device, dst.dtype))
+        if callable(runner):
+            runner()
+        else:
+            runner.replay()
+            torch.cuda.synchronize(runner.device)
+        return {"ok": True}
 
     def handle(self, req: dict):
         op = req["op"]
@@ -177,12 +221,37 @@ class Dispatcher:
             return _jsonable({k: v for k, v in st.items() if k != "stages"} | {"stages": len(st.get("stages", []))})
         if op == "explain_graph":
             return c.explain(*build_graph(req["graph"], self.registry))
+        if op == "prepare":
+            return self._prepare(req)
+        if op == "run_prepared":
+            return self._run_prepared(req)
         raise ValueError(f"unknown request {op}")
 
     def _job(self, name: str) -> Callable:
         if name not in self.jobs:
             raise KeyError(f"job '{name}' is not registered on this server")
         return self.jobs[name]
+
+
+def _enc_tensor(t) -> dict:
+    """Exact-bytes tensor encoding for prepared-job feeds (raw bytes base64 + dtype + shape; no pickle)."""
+    import base64
+
+    t = t.detach().cpu().contiguous()
+    return {"data": base64.b64encode(t.view(torch.uint8).numpy().tobytes()).decode("ascii"),
+            "dtype": str(t.dtype).replace("torch.", ""), "shape": list(t.shape)}
+
+
+def _dec_tensor(f: dict):
+    import base64
+
+    dt = getattr(torch, str(f["dtype"]), None)
+    if not isinstance(dt, torch.dtype):
+        raise ValueError(f"bad dtype {f.get('dtype')!r}")
+    raw = bytearray(base64.b64decode(f["data"]))
+    shape = [int(x) for x in f["shape"]]
+    t = torch.frombuffer(raw, dtype=torch.uint8) if raw else torch.empty(0, dtype=torch.uint8)
+    return t.view(dt).reshape(shape)
 
 
 def _kwargs(req) -> dict:
@@ -359,6 +428,17 @@ class RemotePDBClient:
         return self._call(op="execute", graph=RemoteComp.graph(sinks), job_name=job_name, pre_compile=pre_compile)
 
     executeComputations = execute_computations
+
+    def prepare_job(self, job: str, inputs=(), **kwargs) -> dict:
+        """Prepare a registered job for repeated runs: on a GPU server its kernels are captured into a HIP
+        graph once; returns {"handle", "graph"}."""
+        return self._call(op="prepare", job=job, kwargs=kwargs, inputs=[list(x) for x in inputs])
+
+    def run_prepared(self, handle: int, feeds: Optional[dict] = None) -> dict:
+        """Write ``feeds`` ({(db, set): 2-D tensor}) into the prepared job's input sets and run it (a graph
+        replay on a GPU server)."""
+        fs = [dict(db=k[0], set=k[1], **_enc_tensor(v)) for k, v in (feeds or {}).items()]
+        return self._call(op="run_prepared", handle=handle, feeds=fs)
 
     def explain_graph(self, *sinks) -> str:
         return self._call(op="explain_graph", graph=RemoteComp.graph(sinks))

@@ -3,6 +3,8 @@ servers driven by PDBClient over sockets)."""
 import socket
 import time
 
+import pytest
+
 from netsdb_amd.client import PDBClient
 from netsdb_amd.objects.builtin import Employee
 from netsdb_amd.server import PDBFrontend, RemotePDBClient
@@ -124,3 +126,59 @@ def test_remote_declarative_graph_select_join_aggregate(tmp_path):
     finally:
         rc.shutdown()
         fe.stopped.wait(5)
+
+
+def _ff_jobs():
+    from netsdb_amd.models import ff
+
+    def load(c, seed=0):
+        ff.load_model(c, "ff", 64, 1024, 128, 100, 32, 256, seed=seed)
+        return {"ok": True}
+
+    def unit(c):
+        ff.inference_unit(c, "ff", "w1", "wo", "inputs", "b1", "bo", "output", dropout_rate=0.0, seed=0)
+        return {"ok": True}
+
+    return {"ff_load": load, "ff_unit": unit}
+
+
+def _prepared_roundtrip(tmp_path, device):
+    import torch
+
+    from netsdb_amd.models import ff
+    from netsdb_amd.models.blocks import to_tensor
+
+    srv = PDBClient(root=str(tmp_path / "srv"), device=device)
+    fe = PDBFrontend(srv, port=0, jobs=_ff_jobs()).start()
+    rc = RemotePDBClient("127.0.0.1", fe.port)
+    try:
+        rc.run("ff_load", seed=0)
+        h = rc.prepare_job("ff_unit", inputs=[("ff", "inputs")])
+        assert h["graph"] == (device != "cpu")
+        local = PDBClient(root=str(tmp_path / "loc"), device=device)
+        ff.load_model(local, "ff", 64, 1024, 128, 100, 32, 256, seed=0)
+        for k in range(2):
+            x = (torch.rand(64, 1024, generator=torch.Generator().manual_seed(10 + k)) - 0.5)
+            assert rc.run_prepared(h["handle"], {("ff", "inputs"): x})["ok"]
+            p = local.storage.get_set("ff", "inputs").panel
+            p[:64, :1024].copy_(x.to(p.device, p.dtype))
+            ff.inference_unit(local, "ff", "w1", "wo", "inputs", "b1", "bo", "output", dropout_rate=0.0, seed=0)
+            assert torch.equal(to_tensor(srv, "ff", "output").float().cpu(), to_tensor(local, "ff", "output").float().cpu())
+        try:
+            rc.run_prepared(h["handle"], {("ff", "w1"): torch.zeros(2, 2)})
+            raise AssertionError("a non-input set must be refused")
+        except RuntimeError as e:
+            assert "not an input" in str(e)
+    finally:
+        rc.shutdown()
+
+
+def test_remote_prepared_job_cpu(tmp_path):
+    """Prepared job over the wire: feeds written into the declared input set, then the job re-run
+    (a HIP-graph replay on a GPU server; eager on a CPU server) — same output as a local run."""
+    _prepared_roundtrip(tmp_path, "cpu")
+
+
+@pytest.mark.gpu
+def test_remote_prepared_job_gpu_graph(tmp_path):
+    _prepared_roundtrip(tmp_path, "cuda:0")
