@@ -84,6 +84,8 @@ def main():
                     help="record one whole step (FF jobs + conv2d job) into a HIP graph after the warmup and time its "
                          "replays (PDBClient.capture_job: no host work per step; the dropout seed of the recorded "
                          "step is reused)")
+    ap.add_argument("--rownorm-loads", choices=["nt", "plain"], default=None,
+                    help="row-normalise row loads: non-temporal (library default) or cache-allocating")
     ap.add_argument("--conv-kernel", choices=["rows", "rowfull"], default=None,
                     help="conv2d row kernel: two-pass 2-waves/SIMD (rows) or full-row 1-wave/SIMD with stores "
                          "pipelined under the MFMAs (rowfull); default: the library default")
@@ -130,6 +132,10 @@ def main():
         from netsdb_amd import _ext
 
         _ext.hip().conv2d_rowfull(1 if args.conv_kernel == "rowfull" else 0)
+    if args.rownorm_loads is not None and dev.type == "cuda":
+        from netsdb_amd import _ext
+
+        _ext.hip().rownorm_plain_loads(1 if args.rownorm_loads == "plain" else 0)
     main_stream = None
     if tail and dev.type == "cuda":
         # FF jobs on a high-priority stream: when conv blocks and the FF tail kernels both wait for CUs, the

@@ -34,6 +34,7 @@ extern int nsdb_conv2d_force_generic;
 extern int nsdb_conv2d_variant;
 extern int nsdb_conv2d_max_blocks;
 extern int nsdb_conv2d_rowfull;
+extern int nsdb_rownorm_plain_loads;
 int nsdb_im2col(const void* X, void* out, int N, int C, int H, int W, int KH, int KW, int stride, int pad, int dil,
                 int ldk, hipStream_t stream);
 int nsdb_softmax_rows(const void* X, int x_f32, const float* bias, void* Y, int y_f32, int R, int N,
@@ -585,6 +586,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "1: route every conv2d to the generic gather kernel (A/B testing)");
   m.def("conv2d_max_blocks", [](int64_t v) { const int old = nsdb_conv2d_max_blocks; nsdb_conv2d_max_blocks = (int)v; return old; },
         "row-kernel grid cap (0 = one block per row group); returns the previous value");
+  m.def("rownorm_plain_loads", [](int64_t v) { const int o = nsdb_rownorm_plain_loads; nsdb_rownorm_plain_loads = (int)v; return o; },
+        "row normalise: cache-allocating (1) or non-temporal (0) row loads; returns the previous value");
   m.def("conv2d_rowfull", [](int64_t v) { const int old = nsdb_conv2d_rowfull; nsdb_conv2d_rowfull = (int)v; return old; },
         "full-row conv kernel on/off (A/B); returns the previous value");
   m.def("conv2d_variant", [](int64_t v) { nsdb_conv2d_variant = (int)v; }, "row-kernel diagnostic variant");

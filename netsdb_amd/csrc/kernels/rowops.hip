@@ -74,7 +74,9 @@ __global__ void __launch_bounds__(256) row_normalize_kernel(const TI* X, TO* Y, 
 // from HBM once (the two-pass kernel above re-reads it) — 1 read + 1 write per element.
 template <typename TO, int NV>
 __global__ void __launch_bounds__(512) row_normalize_vec_kernel(const float* X, TO* Y, int R, int N, long long ldx,
-                                                                long long ldy) {
+                                                                long long ldy, int plain_loads) {
+  // plain_loads: cache-allocating instead of non-temporal row loads (the rows were usually just written by the
+  // producing GEMM and may still sit in the Infinity Cache; A/B knob nsdb_rownorm_plain_loads)
   __shared__ float red[8];
   const int row = blockIdx.x;
   if (row >= R) return;
@@ -85,7 +87,7 @@ __global__ void __launch_bounds__(512) row_normalize_vec_kernel(const float* X, 
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int j = threadIdx.x + i * 512;
-    v[i] = j < n4 ? __builtin_nontemporal_load(x + j) : f32x4{0.f, 0.f, 0.f, 0.f};
+    v[i] = j < n4 ? (plain_loads ? x[j] : __builtin_nontemporal_load(x + j)) : f32x4{0.f, 0.f, 0.f, 0.f};
     s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
   }
   const float inv = 1.f / block_reduce(s, red, false);
@@ -196,6 +198,8 @@ static int grid_for(long long n) { return (int)std::min<long long>((n + 255) / 2
 
 extern "C" {
 
+int nsdb_rownorm_plain_loads = 0;   // A/B knob of row_normalize_vec_kernel's row load policy
+
 int nsdb_softmax_rows(const void* X, int x_f32, const float* bias, void* Y, int y_f32, int R, int N,
                       long long ldx, long long ldy, int log_out, hipStream_t st) {
   if (R <= 0) return 0;
@@ -204,7 +208,7 @@ int nsdb_softmax_rows(const void* X, int x_f32, const float* bias, void* Y, int 
                      ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(Y)) & 15) == 0;
     if (vec && N <= 512 * 4 * 8) {
 #define NSDB_RNV(TO, NV) \
-  hipLaunchKernelGGL((nsdb::row_normalize_vec_kernel<TO, NV>), dim3(R), dim3(512), 0, st, (const float*)X, (TO*)Y, R, N, ldx, ldy)
+  hipLaunchKernelGGL((nsdb::row_normalize_vec_kernel<TO, NV>), dim3(R), dim3(512), 0, st, (const float*)X, (TO*)Y, R, N, ldx, ldy, nsdb_rownorm_plain_loads)
       const int nv = (N / 4 + 511) / 512;
       if (y_f32) { if (nv <= 2) NSDB_RNV(float, 2); else if (nv <= 4) NSDB_RNV(float, 4); else NSDB_RNV(float, 8); }
       else { if (nv <= 2) NSDB_RNV(unsigned short, 2); else if (nv <= 4) NSDB_RNV(unsigned short, 4); else NSDB_RNV(unsigned short, 8); }
