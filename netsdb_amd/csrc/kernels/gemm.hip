@@ -66,7 +66,11 @@ struct GemmParams {
   // tail leaves CUs idle (see nsdb_tail_trigger_arm)
   unsigned* signal;
   unsigned signal_value;
+  // K-tail stealing (variant 19, split-K): per-tile claim counters (zero at launch; the split-K reducer re-zeroes
+  // them) for the STEAL_TQ tail chunks of STEAL_CH k-tiles at the end of every split's K range
+  int* steal_cnt;
 };
+constexpr int STEAL_TQ = 4, STEAL_CH = 16;
 
 // Adaptive split-K partition (8-phase kernel, split-K launches). The splits of one GEMM run on different XCDs
 // (the bijective remap puts a split's tiles on one XCD) and the XCDs of one MI355X stream at persistently
@@ -665,8 +669,11 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   // start time kept in a register and stored with the finish time: a vector store (or load) pending at the
   // loop entry would make the compiler's wait-count pass put vmcnt(0) waits into the counted-vmcnt loop
   const unsigned long long t_begin = ad != nullptr ? __builtin_amdgcn_s_memrealtime() : 0ull;
-  const int nk = max(0, (kend - kbeg + BK - 1) / BK);
-  const int niter = (nk + 1) >> 1;
+  // V19: this workgroup's static part stops STEAL_TQ * STEAL_CH k-tiles short of its split's end; those tail
+  // chunks (of every split of the tile) are claimed afterwards by whichever workgroup of the tile is free first
+  if constexpr (V == 19) kend = max(kbeg, min(kend, kbeg + p.kchunk - STEAL_TQ * STEAL_CH * BK));
+  int nk = max(0, (kend - kbeg + BK - 1) / BK);
+  int niter = (nk + 1) >> 1;
 
   // KT (variant 9): K-tiled operands [K/64][ld rows][64] — every (tile, k-step) half-tile is one
   // contiguous 16 KiB run instead of 128 rows x 128 B strided by the row length (DRAM page locality
@@ -844,6 +851,7 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
     if (wr == 1) NSDB_BARRIER();
     for (int u = 0; u < nk; ++u) ktile_ring(u);
   } else {
+  for (int seg = 0;; ++seg) {      // V19: the static part, then claimed tail chunks (one segment otherwise)
   // prologue: tile 0 (4 halves) + B0, A0, B1 of tile 1; tile 0 complete when <= 6 ops remain
   stage(0, 2, 0); stage(0, 0, 0); stage(0, 3, 0); stage(0, 1, 0);
   stage(1, 2, 1); stage(1, 0, 1); stage(1, 3, 1);
@@ -859,12 +867,47 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
       if (tid == 0 && (it & 15) == 0) p.stamps[(long long)wg * 64 + min(it >> 4, 62)] = __builtin_amdgcn_s_memrealtime();
     }
   }
+  if constexpr (V != 19) {
+    break;
+  } else {
+    // segment done: re-align the wave groups, drain every wave's trailing DMAs, then claim the tile's next tail
+    // chunk (one returning vector atomic by thread 0, broadcast through LDS between two full barriers)
+    if (wr == 0) NSDB_BARRIER();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* slot = reinterpret_cast<int*>(smem);
+    const int nchunks = p.splits * STEAL_TQ;
+    if (tid == 0) {
+      int c = nchunks, kb = 0, ke = 0;
+      while (true) {                                  // skip empty chunks (short last split); bounded by nchunks
+        c = __hip_atomic_fetch_add(&p.steal_cnt[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (c >= nchunks) break;
+        const int v = c % p.splits, j = c / p.splits;
+        const int vend = min(p.K, (v + 1) * p.kchunk);
+        const int tail0 = max(v * p.kchunk, v * p.kchunk + p.kchunk - STEAL_TQ * STEAL_CH * BK);
+        kb = tail0 + j * STEAL_CH * BK;
+        ke = min(vend, kb + STEAL_CH * BK);
+        if (kb < ke) break;
+      }
+      slot[0] = c < nchunks ? kb : -1;
+      slot[1] = ke;
+    }
+    __syncthreads();
+    const int nkb = slot[0], nke = slot[1];
+    __syncthreads();                                  // slot read before the next prologue's DMAs land
+    if (nkb < 0) break;
+    kbeg = nkb;
+    kend = nke;
+    nk = (kend - kbeg + BK - 1) / BK;
+    niter = (nk + 1) >> 1;
+  }
+  }
   }
   if constexpr (V == 12) {      // slot 63: the XCD this workgroup ran on (HW_REG_XCC_ID) and its CU id
     if (tid == 0) p.stamps[(long long)wg * 64 + 63] =
         ((unsigned long long)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 32) | (unsigned)__builtin_amdgcn_s_getreg((15 << 11) | 4);
   }
-  if (V != 3 && wr == 0) NSDB_BARRIER();            // re-align the groups
+  if (V != 3 && V != 19 && wr == 0) NSDB_BARRIER();  // re-align the groups (V19 re-aligned per segment)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // trailing zero-fill DMAs land before LDS reuse
   if (V == 0 && p.signal != nullptr && tid == 0)     // tail trigger: this workgroup's CU frees up soon
     __hip_atomic_fetch_max(p.signal, p.signal_value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1279,7 +1322,14 @@ __device__ __forceinline__ void reduce_epilogue4(const GemmParams& p, int batch,
 }
 
 // Split-K slab reducer + fused epilogue (the ClusterAggregate "combine" of the partial block products).
+// the K-tail stealing counters of the GEMM this reducer follows go back to zero for the next launch
+__device__ __forceinline__ void reset_steal_counters(const GemmParams& p) {
+  if (p.steal_cnt != nullptr && blockIdx.x == 0 && blockIdx.y == 0)
+    for (int i = threadIdx.x; i < p.tiles_m * p.tiles_n; i += blockDim.x) p.steal_cnt[i] = 0;
+}
+
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(GemmParams p) {
+  reset_steal_counters(p);
   const long long MN = (long long)p.M * p.N;
   const int batch = blockIdx.y;
   const float* bias = p.bias ? p.bias + batch * p.sBias : nullptr;
@@ -1329,6 +1379,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(GemmParams p) {
 // lanes share 64 output vec4s; group g sums slabs g, g+8, ... with 4 loads in flight, then the 8
 // partials meet in LDS.  Deterministic (fixed summation tree).
 __global__ void __launch_bounds__(512) splitk_reduce_wide_kernel(GemmParams p) {
+  reset_steal_counters(p);
   const long long MN = (long long)p.M * p.N;
   const int batch = blockIdx.y;
   const int v = threadIdx.x & 63, g = threadIdx.x >> 6;
@@ -1481,7 +1532,7 @@ int nsdb_gemm_nt_softmax(const void* A, const void* B, float* C, const float* bi
   p.vec_ws = 0;
   p.vec_c = (ldc % 4 == 0 && (reinterpret_cast<uintptr_t>(C) & 15) == 0) ? 1 : 0;
   p.softmax = axis; p.sm_part = (float2*)part; p.sm_cnt = cnt; p.sm_flag = flag; p.stamps = nullptr; p.adapt = nullptr;
-  p.signal = nullptr; p.signal_value = 0;
+  p.signal = nullptr; p.signal_value = 0; p.steal_cnt = nullptr;
   const int tiles = p.tiles_m * p.tiles_n;
   if (axis == 1) hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<20>, dim3(tiles), dim3(512), 0, stream, p);
   else hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<21>, dim3(tiles), dim3(512), 0, stream, p);
@@ -1519,7 +1570,7 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
   p.softmax = 0; p.sm_part = nullptr; p.sm_cnt = nullptr; p.sm_flag = nullptr;
   p.stamps = g_stamps;
   p.adapt = nullptr;
-  p.signal = nullptr; p.signal_value = 0;
+  p.signal = nullptr; p.signal_value = 0; p.steal_cnt = nullptr;
   if (g_force_cfg == 17 && g_stamps == nullptr) return -6;
   if (seg_k > 0 && (seg_k % p.kchunk != 0 || seg_k % nsdb::BK != 0)) return -5;   // a split must not cross a segment
   const int cfg = pick_cfg(M, N, K, batch);
@@ -1573,6 +1624,20 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
     hipLaunchKernelGGL(nsdb::gemm_nt_256_w4r_kernel, grid, dim3(256), 0, stream, p);
   else if (cfg == 13)   // w4 diagnostic: no DMA issued (load-free upper bound, wrong results)
     hipLaunchKernelGGL(nsdb::gemm_nt_256_w4_kernel<4>, grid, dim3(256), 0, stream, p);
+  else if (cfg == 24 && p.splits > 1 && batch == 1 && seg_k == 0 && p.tiles_m * p.tiles_n <= 4096) {
+    // 8-phase with K-tail stealing: per-(device, stream) claim counters, zeroed once here and re-zeroed by the
+    // split-K reducer that follows every launch
+    static std::map<std::pair<int, void*>, int*> bufs;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    int*& cnt = bufs[{dev, (void*)stream}];
+    if (cnt == nullptr) {
+      if (hipMalloc((void**)&cnt, 4096 * sizeof(int)) != hipSuccess) return -7;
+      if (hipMemset(cnt, 0, 4096 * sizeof(int)) != hipSuccess) return -7;
+    }
+    p.steal_cnt = cnt;
+    hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<19>, grid, dim3(512), 0, stream, p);
+  }
   else if (cfg == 20)   // 8-phase with non-temporal operand loads
     hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<15>, grid, dim3(512), 0, stream, p);
   else if (cfg == 21)   // 8-phase, sc1 (L1 bypass) operand loads

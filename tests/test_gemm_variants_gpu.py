@@ -84,3 +84,30 @@ def test_adaptive_splitk_partition_exact(shape):
         out = ops.gemm_nt(A, B, out_dtype=torch.float32)
         assert ((out[rows] - ref).abs().max() / ref.abs().max()).item() < 1e-5
         assert ((out - base).abs().max() / base.abs().max()).item() < 1e-5
+
+
+@pytest.mark.parametrize("shape", [(1000, 1000, 597568), (1024, 768, 65536 + 8 * 64), (512, 512, 40960)])
+def test_ksteal_variant_vs_fp32(shape):
+    """K-tail stealing (cfg 24): every split's last 4 x 16 k-tiles are claimed by whichever workgroup of the
+    tile is free first (summation order differs from cfg 2, the sum does not); three launches in a row check
+    that the reducer re-zeroes the claim counters."""
+    from netsdb_amd import _ext, ops
+
+    M, N, K = shape
+    g = torch.Generator(device="cuda:0").manual_seed(1)
+    A = torch.empty(M, K, device="cuda:0").uniform_(-1, 1, generator=g).to(torch.bfloat16)
+    B = (torch.empty(N, K, device="cuda:0").uniform_(-1, 1, generator=g) * (3.0 / K) ** 0.5).to(torch.bfloat16)
+    rows = torch.linspace(0, M - 1, 16, device="cuda:0").long()
+    ref = A[rows].float() @ B.float().t()
+    h = _ext.hip()
+    try:
+        h.gemm_force_config(24)
+        outs = [ops.gemm_nt(A, B, out_dtype=torch.float32) for _ in range(3)]
+        torch.cuda.synchronize()
+    finally:
+        h.gemm_force_config(-1)
+    base = ops.gemm_nt(A, B, out_dtype=torch.float32)
+    for o in outs:
+        err = ((o[rows] - ref).abs().max() / ref.abs().max()).item()
+        assert err < 1e-4, err
+        assert ((o - base).abs().max() / base.abs().max()).item() < 1e-5
