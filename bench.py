@@ -84,6 +84,9 @@ def main():
                     help="record one whole step (FF jobs + conv2d job) into a HIP graph after the warmup and time its "
                          "replays (PDBClient.capture_job: no host work per step; the dropout seed of the recorded "
                          "step is reused)")
+    ap.add_argument("--ksteal", action="store_true",
+                    help="FF layer-1 split-K GEMM with K-tail stealing (opt-in: ~1 %% faster in isolation, summation "
+                         "order varies run to run)")
     ap.add_argument("--rownorm-loads", choices=["nt", "plain"], default=None,
                     help="row-normalise row loads: non-temporal (library default) or cache-allocating")
     ap.add_argument("--conv-kernel", choices=["rows", "rowfull"], default=None,
@@ -132,6 +135,10 @@ def main():
         from netsdb_amd import _ext
 
         _ext.hip().conv2d_rowfull(1 if args.conv_kernel == "rowfull" else 0)
+    if args.ksteal and dev.type == "cuda":
+        from netsdb_amd import _ext
+
+        _ext.hip().gemm_set_steal(1)
     if args.rownorm_loads is not None and dev.type == "cuda":
         from netsdb_amd import _ext
 
@@ -248,6 +255,7 @@ def main():
                 "ff_steps_in_flight": inflight,
                 "collectives_per_step": round(coll_per_step, 2),
                 "graph_replay": captured is not None,
+                "ksteal": bool(args.ksteal),
             },
         }
         print(json.dumps(res), flush=True)

@@ -15,6 +15,8 @@ int nsdb_gemm_splits(int M, int N, int K, int batch);
 void nsdb_gemm_force_config(int cfg);
 void nsdb_gemm_set_stamps(void* ptr);
 void nsdb_gemm_set_adapt(int on);
+void nsdb_gemm_steal(int tq, int ch);
+void nsdb_gemm_set_steal(int on);
 void nsdb_tail_trigger_arm(void* flag, unsigned value);
 int nsdb_tail_trigger_consumed();
 void nsdb_tail_trigger_disarm();
@@ -567,6 +569,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           TORCH_CHECK(flag.is_cuda() && flag.scalar_type() == torch::kInt32 && flag.numel() >= 1, "flag: int32 device tensor");
           check_rc(nsdb_stream_wait_value(cur_stream(), flag.data_ptr(), (unsigned)value), "stream_wait_value");
         }, "current stream waits on the GPU until flag >= value (unsigned)");
+  m.def("gemm_set_steal", [](int64_t on) { nsdb_gemm_set_steal((int)on); },
+        "opt-in: long split-K GEMMs use K-tail stealing (summation order varies run to run)");
+  m.def("gemm_steal", [](int64_t tq, int64_t ch) { nsdb_gemm_steal((int)tq, (int)ch); },
+        "K-tail stealing geometry of cfg 24: tail chunks per split, k-tiles per chunk");
   m.def("gemm_set_adapt", [](int64_t on) { nsdb_gemm_set_adapt((int)on); },
         "adaptive split-K K-partition across XCDs on/off (A/B)");
   m.def("gemm_adapt_state", [](int64_t M, int64_t N, int64_t K) {

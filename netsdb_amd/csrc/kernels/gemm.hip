@@ -67,10 +67,10 @@ struct GemmParams {
   unsigned* signal;
   unsigned signal_value;
   // K-tail stealing (variant 19, split-K): per-tile claim counters (zero at launch; the split-K reducer re-zeroes
-  // them) for the STEAL_TQ tail chunks of STEAL_CH k-tiles at the end of every split's K range
+  // them) for the steal_tq tail chunks of steal_ch k-tiles at the end of every split's K range
   int* steal_cnt;
+  int steal_tq, steal_ch;       // tail chunks per split, k-tiles per chunk (nsdb_gemm_steal)
 };
-constexpr int STEAL_TQ = 4, STEAL_CH = 16;
 
 // Adaptive split-K partition (8-phase kernel, split-K launches). The splits of one GEMM run on different XCDs
 // (the bijective remap puts a split's tiles on one XCD) and the XCDs of one MI355X stream at persistently
@@ -669,9 +669,9 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   // start time kept in a register and stored with the finish time: a vector store (or load) pending at the
   // loop entry would make the compiler's wait-count pass put vmcnt(0) waits into the counted-vmcnt loop
   const unsigned long long t_begin = ad != nullptr ? __builtin_amdgcn_s_memrealtime() : 0ull;
-  // V19: this workgroup's static part stops STEAL_TQ * STEAL_CH k-tiles short of its split's end; those tail
+  // V19: this workgroup's static part stops steal_tq * steal_ch k-tiles short of its split's end; those tail
   // chunks (of every split of the tile) are claimed afterwards by whichever workgroup of the tile is free first
-  if constexpr (V == 19) kend = max(kbeg, min(kend, kbeg + p.kchunk - STEAL_TQ * STEAL_CH * BK));
+  if constexpr (V == 19) kend = max(kbeg, min(kend, kbeg + p.kchunk - p.steal_tq * p.steal_ch * BK));
   int nk = max(0, (kend - kbeg + BK - 1) / BK);
   int niter = (nk + 1) >> 1;
 
@@ -876,7 +876,7 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int* slot = reinterpret_cast<int*>(smem);
-    const int nchunks = p.splits * STEAL_TQ;
+    const int nchunks = p.splits * p.steal_tq;
     if (tid == 0) {
       int c = nchunks, kb = 0, ke = 0;
       while (true) {                                  // skip empty chunks (short last split); bounded by nchunks
@@ -884,9 +884,9 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
         if (c >= nchunks) break;
         const int v = c % p.splits, j = c / p.splits;
         const int vend = min(p.K, (v + 1) * p.kchunk);
-        const int tail0 = max(v * p.kchunk, v * p.kchunk + p.kchunk - STEAL_TQ * STEAL_CH * BK);
-        kb = tail0 + j * STEAL_CH * BK;
-        ke = min(vend, kb + STEAL_CH * BK);
+        const int tail0 = max(v * p.kchunk, v * p.kchunk + p.kchunk - p.steal_tq * p.steal_ch * BK);
+        kb = tail0 + j * p.steal_ch * BK;
+        ke = min(vend, kb + p.steal_ch * BK);
         if (kb < ke) break;
       }
       slot[0] = c < nchunks ? kb : -1;
@@ -909,7 +909,7 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   }
   if (V != 3 && V != 19 && wr == 0) NSDB_BARRIER();  // re-align the groups (V19 re-aligned per segment)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // trailing zero-fill DMAs land before LDS reuse
-  if (V == 0 && p.signal != nullptr && tid == 0)     // tail trigger: this workgroup's CU frees up soon
+  if ((V == 0 || V == 19) && p.signal != nullptr && tid == 0)   // tail trigger: this CU frees up soon
     __hip_atomic_fetch_max(p.signal, p.signal_value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (ad != nullptr) {
     // finish time; the last workgroup of the launch derives the next launch's shares (the groups are
@@ -1420,6 +1420,15 @@ static int g_adapt = 0;   // adaptive split-K partition: opt-in (measured neutra
 
 void nsdb_gemm_set_adapt(int on) { g_adapt = on; }
 
+// K-tail stealing geometry (cfg 24): tail chunks per split and k-tiles per chunk (even)
+static int g_steal_tq = 4, g_steal_ch = 16;
+static int g_steal_on = 0;   // opt-in: long split-K launches of cfg 2 take the stealing variant (not bit-reproducible)
+void nsdb_gemm_set_steal(int on) { g_steal_on = on; }
+void nsdb_gemm_steal(int tq, int ch) {
+  g_steal_tq = tq < 1 ? 1 : tq;
+  g_steal_ch = ch < 2 ? 2 : (ch & ~1);
+}
+
 // Tail trigger: start an independent job in the tail of the next long GEMM instead of after it.
 // arm(flag, v): the next 8-phase launch with >= 128 workgroups and >= 64 k-tiles per workgroup makes each
 // workgroup raise *flag to v when its main loop ends (the grid is one resident wave, so by then every
@@ -1532,7 +1541,7 @@ int nsdb_gemm_nt_softmax(const void* A, const void* B, float* C, const float* bi
   p.vec_ws = 0;
   p.vec_c = (ldc % 4 == 0 && (reinterpret_cast<uintptr_t>(C) & 15) == 0) ? 1 : 0;
   p.softmax = axis; p.sm_part = (float2*)part; p.sm_cnt = cnt; p.sm_flag = flag; p.stamps = nullptr; p.adapt = nullptr;
-  p.signal = nullptr; p.signal_value = 0; p.steal_cnt = nullptr;
+  p.signal = nullptr; p.signal_value = 0; p.steal_cnt = nullptr; p.steal_tq = 0; p.steal_ch = 2;
   const int tiles = p.tiles_m * p.tiles_n;
   if (axis == 1) hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<20>, dim3(tiles), dim3(512), 0, stream, p);
   else hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<21>, dim3(tiles), dim3(512), 0, stream, p);
@@ -1570,7 +1579,7 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
   p.softmax = 0; p.sm_part = nullptr; p.sm_cnt = nullptr; p.sm_flag = nullptr;
   p.stamps = g_stamps;
   p.adapt = nullptr;
-  p.signal = nullptr; p.signal_value = 0; p.steal_cnt = nullptr;
+  p.signal = nullptr; p.signal_value = 0; p.steal_cnt = nullptr; p.steal_tq = 0; p.steal_ch = 2;
   if (g_force_cfg == 17 && g_stamps == nullptr) return -6;
   if (seg_k > 0 && (seg_k % p.kchunk != 0 || seg_k % nsdb::BK != 0)) return -5;   // a split must not cross a segment
   const int cfg = pick_cfg(M, N, K, batch);
@@ -1608,7 +1617,9 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
     p.signal_value = g_trig.value;
     g_trig.consumed = 1;
   }
-  if (cfg == 2)
+  const bool steal = g_steal_on && cfg == 2 && p.splits > 1 && batch == 1 && seg_k == 0 &&
+                     p.tiles_m * p.tiles_n <= 4096 && (K / nsdb::BK) / p.splits >= 4 * g_steal_tq * g_steal_ch;
+  if (cfg == 2 && !steal)
     hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<0>, grid, dim3(512), 0, stream, p);
   else if (cfg == 10)
     hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<8>, grid, dim3(512), 0, stream, p);
@@ -1624,7 +1635,8 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
     hipLaunchKernelGGL(nsdb::gemm_nt_256_w4r_kernel, grid, dim3(256), 0, stream, p);
   else if (cfg == 13)   // w4 diagnostic: no DMA issued (load-free upper bound, wrong results)
     hipLaunchKernelGGL(nsdb::gemm_nt_256_w4_kernel<4>, grid, dim3(256), 0, stream, p);
-  else if (cfg == 24 && p.splits > 1 && batch == 1 && seg_k == 0 && p.tiles_m * p.tiles_n <= 4096) {
+  else if ((cfg == 24 || (cfg == 2 && g_steal_on && (K / nsdb::BK) / p.splits >= 4 * g_steal_tq * g_steal_ch)) &&
+           p.splits > 1 && batch == 1 && seg_k == 0 && p.tiles_m * p.tiles_n <= 4096) {
     // 8-phase with K-tail stealing: per-(device, stream) claim counters, zeroed once here and re-zeroed by the
     // split-K reducer that follows every launch
     static std::map<std::pair<int, void*>, int*> bufs;
@@ -1636,6 +1648,8 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
       if (hipMemset(cnt, 0, 4096 * sizeof(int)) != hipSuccess) return -7;
     }
     p.steal_cnt = cnt;
+    p.steal_tq = g_steal_tq;
+    p.steal_ch = g_steal_ch;
     hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<19>, grid, dim3(512), 0, stream, p);
   }
   else if (cfg == 20)   // 8-phase with non-temporal operand loads
