@@ -36,6 +36,7 @@ extern int nsdb_conv2d_force_generic;
 extern int nsdb_conv2d_variant;
 extern int nsdb_conv2d_max_blocks;
 extern int nsdb_conv2d_rowfull;
+extern int nsdb_conv2d_contig;
 extern int nsdb_rownorm_plain_loads;
 int nsdb_im2col(const void* X, void* out, int N, int C, int H, int W, int KH, int KW, int stride, int pad, int dil,
                 int ldk, hipStream_t stream);
@@ -594,6 +595,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "row-kernel grid cap (0 = one block per row group); returns the previous value");
   m.def("rownorm_plain_loads", [](int64_t v) { const int o = nsdb_rownorm_plain_loads; nsdb_rownorm_plain_loads = (int)v; return o; },
         "row normalise: cache-allocating (1) or non-temporal (0) row loads; returns the previous value");
+  m.def("conv2d_contig", [](int64_t v) { const int o = nsdb_conv2d_contig; nsdb_conv2d_contig = (int)v; return o; },
+        "full-row conv: contiguous row-group runs per block (1) or grid stride (0); returns the previous value");
   m.def("conv2d_rowfull", [](int64_t v) { const int old = nsdb_conv2d_rowfull; nsdb_conv2d_rowfull = (int)v; return old; },
         "full-row conv kernel on/off (A/B); returns the previous value");
   m.def("conv2d_variant", [](int64_t v) { nsdb_conv2d_variant = (int)v; }, "row-kernel diagnostic variant");

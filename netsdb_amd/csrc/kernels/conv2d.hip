@@ -232,6 +232,8 @@ struct ConvRowParams {
   int rin, ckh, nks, ntiles, chunks, groups_per_img, ngroups;
   int act, nchw_out, out_f32;
   int segs, vec8;  // staged output: LDS run stride per oc (elements); 8-B output chunks allowed
+  int contig;      // full-row kernel: each block walks a contiguous run of row groups (same image, consecutive
+                   // rows: every plane's output grows as one sequential stream) instead of a grid stride
   int variant;   // diagnostics (bit flags, timing only): 1 no global stores, 2 no MFMA, 4 no LDS output
                  // staging, 8 prologue only, 16 no compute, 32 s_memtime stamps over the output
 };
@@ -616,9 +618,14 @@ __global__ void __launch_bounds__(256, 1) conv2d_rowfull_kernel(ConvRowParams p)
     it_lo[u] = 8 * j < p.W;
     it_hi[u] = 8 * (j + 1) < p.W;
   }
+  // group walk: grid stride, or (contig) one contiguous run of row groups per block
+  const int per = p.contig ? (p.ngroups + gridDim.x - 1) / gridDim.x : 0;
+  int g0 = p.contig ? blockIdx.x * per : blockIdx.x;
+  const int gstep = p.contig ? 1 : gridDim.x;
+  const int gend = p.contig ? min(p.ngroups, g0 + per) : p.ngroups;
   auto fetch = [&](int g, auto SLOT) {
     constexpr int sl = decltype(SLOT)::value;
-    const bool gok = g < p.ngroups;
+    const bool gok = g < gend;
     const int n = g / p.groups_per_img, oh0 = (g % p.groups_per_img) * CVR_TR;
     const int gbase = ((n * p.C * p.H) + oh0) * p.W * 2;
 #pragma unroll
@@ -672,13 +679,13 @@ __global__ void __launch_bounds__(256, 1) conv2d_rowfull_kernel(ConvRowParams p)
   int prev_obase = 0, prev_n4 = 0;
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
-  int g = blockIdx.x;
+  int g = g0;
   // input rows are fetched TWO groups ahead (slot = group parity): a load queues behind the stores issued
   // before it on the CU, so the rows consumed at the end of group g were requested before group g-1's stores
   // (one group ahead, the wait for them was a wait for the previous group's store drain)
   fetch(g, I0{});
   store_rows(I0{});
-  fetch(g + gridDim.x, I1{});
+  fetch(g + gstep, I1{});
   // 32 dropped stores (out-of-range offset) after it, as after every loop body: the first group's wait for
   // slot 1 then counts past 32 stores like every later one (hipcc merges the entry path into the loop's count)
 #pragma unroll
@@ -687,7 +694,7 @@ __global__ void __launch_bounds__(256, 1) conv2d_rowfull_kernel(ConvRowParams p)
     constexpr int par = decltype(PAR)::value;
     const int n = g / p.groups_per_img, oh0 = (g % p.groups_per_img) * CVR_TR, oh = oh0 + wave;
     __syncthreads();                                   // input rows of g visible; stage reads of g-1 done
-    fetch(g + 2 * gridDim.x, PAR);                     // into the slot group g's rows were staged from
+    fetch(g + 2 * gstep, PAR);                     // into the slot group g's rows were staged from
     stamp(5);
     unsigned short* const st_cur = ostage + (PIPE ? par * (64 * CVF_SEGS) : 0);
     const unsigned short* const st_prev = ostage + (PIPE ? (par ^ 1) * (64 * CVF_SEGS) : 0);
@@ -776,13 +783,13 @@ __global__ void __launch_bounds__(256, 1) conv2d_rowfull_kernel(ConvRowParams p)
     (void)oh;
   };
   int it = 0;
-  while (g < p.ngroups) {
+  while (g < gend) {
     body(I0{});
-    g += gridDim.x;
+    g += gstep;
     ++it;
-    if (g >= p.ngroups) break;
+    if (g >= gend) break;
     body(I1{});
-    g += gridDim.x;
+    g += gstep;
     ++it;
   }
   if constexpr (PIPE) {
@@ -841,7 +848,8 @@ int nsdb_conv2d_variant = 0;         // row-kernel diagnostics (timing only)
 // 0 = one block per row group (short-lived blocks that the dispatcher can interleave with higher-priority
 // kernels when the conv shares the GPU with another job, e.g. gated into a GEMM's tail)
 int nsdb_conv2d_max_blocks = 512;
-int nsdb_conv2d_rowfull = 1;         // full-row kernel for 97 <= OW <= 112 (0: the two-pass row kernel, A/B)
+int nsdb_conv2d_rowfull = 1;
+int nsdb_conv2d_contig = 0;          // full-row kernel: contiguous row-group runs per block (A/B)         // full-row kernel for 97 <= OW <= 112 (0: the two-pass row kernel, A/B)
 
 int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* out, int N, int C, int H,
                       int W, int OC, int KH, int KW, int stride, int pad, int dil, int ldw, int act,
@@ -869,6 +877,7 @@ int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* ou
     q.groups_per_img = (p.OH + nsdb::CVR_TR - 1) / nsdb::CVR_TR;
     q.ngroups = N * q.groups_per_img;
     q.act = act; q.nchw_out = nchw_out; q.out_f32 = out_f32; q.variant = nsdb_conv2d_variant;
+    q.contig = nsdb_conv2d_contig;
     q.segs = (4 * p.OW + 3) & ~3;
     if ((q.segs / 2) % 4 == 0) q.segs += 4;
     q.vec8 = ((long long)p.OH * p.OW) % 4 == 0 && (reinterpret_cast<uintptr_t>(out) & 7) == 0;

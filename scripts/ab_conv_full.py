@@ -29,26 +29,30 @@ def main():
     Wf = ops.pad_k(W.reshape(64, 147)).to(torch.bfloat16).contiguous()
     bias = torch.randn(64, device=dev, generator=g)
     ref = F.conv2d(X.float(), W.to(torch.bfloat16).float(), bias)
-    variants = {"rowfull": 1, "rowfull_nopipe": 4, "rows": 0}
+    variants = {"rowfull": 1, "rowfull_nopipe": 4, "rows": 0, "rowfull_contig": 1}
     out = {}
     for name, v in variants.items():
         h.conv2d_rowfull(v)
+        h.conv2d_contig(1 if name == "rowfull_contig" else 0)
         for act, fn in ((ops.ACT_NONE, lambda t: t), (ops.ACT_RELU, torch.relu)):
             y = ops.conv2d(X, Wf, bias, 7, 7, 1, 0, act=act, nchw_out=True).float()
             out[f"{name}_act{act}_rel_err"] = ((y - fn(ref)).abs().max() / ref.abs().max()).item()
     h.conv2d_rowfull(1)
+    h.conv2d_contig(0)
     print(json.dumps(out), flush=True)
     Xm, Wm = X.clone(), W.to(torch.bfloat16)
     fns = {
         "rowfull": lambda: ops.conv2d(X, Wf, bias, 7, 7, 1, 0, nchw_out=True),
         "rowfull_nopipe": lambda: ops.conv2d(X, Wf, bias, 7, 7, 1, 0, nchw_out=True),
+        "rowfull_contig": lambda: ops.conv2d(X, Wf, bias, 7, 7, 1, 0, nchw_out=True),
         "rows": lambda: ops.conv2d(X, Wf, bias, 7, 7, 1, 0, nchw_out=True),
         "miopen": lambda: F.conv2d(Xm, Wm, bias.to(torch.bfloat16)),
     }
     ts = {k: [] for k in fns}
     for _ in range(a.rounds):
         for k, fn in fns.items():
-            h.conv2d_rowfull({"rowfull": 1, "rowfull_nopipe": 4}.get(k, 0))
+            h.conv2d_rowfull({"rowfull": 1, "rowfull_nopipe": 4, "rowfull_contig": 1}.get(k, 0))
+            h.conv2d_contig(1 if k == "rowfull_contig" else 0)
             for _ in range(3):
                 fn()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -59,6 +63,7 @@ def main():
             torch.cuda.synchronize()
             ts[k].append(e0.elapsed_time(e1) / a.iters * 1000)
     h.conv2d_rowfull(1)
+    h.conv2d_contig(0)
     print(json.dumps({f"{k}_us_min": round(min(v), 1) for k, v in ts.items()} |
                      {f"{k}_us_med": round(sorted(v)[len(v) // 2], 1) for k, v in ts.items()}), flush=True)
 
