@@ -99,6 +99,8 @@ def main():
                     help="FF steps in flight: step i's FF jobs go to job lane i %% inflight (>1 pipelines "
                          "consecutive batches: step i+1's layer-1 GEMM starts while step i's tail kernels run)")
     args = ap.parse_args()
+    if args.graph and (args.overlap != "none" or args.inflight > 1):
+        ap.error("--graph records the serial step (no --overlap / --inflight job streams)")
 
     from netsdb_amd.client import PDBClient
     from netsdb_amd.models import conv2d as cv
