@@ -41,13 +41,13 @@ class PDBClient:
     def __init__(self, ctx: Optional[ClusterContext] = None, root: Optional[str] = None, device=None,
                  page_size: int = DEFAULT_PAGE_SIZE, pool_pages: int = 16, catalog_path: Optional[str] = None,
                  trace: bool = False, broadcast_threshold: int = 2 << 30, fusion: bool = True,
-                 device_budget: Optional[int] = None, resume: bool = False):
+                 device_budget: Optional[int] = None, resume: bool = False, pinned_budget: Optional[int] = None):
         self.ctx = ctx or ClusterContext(device=torch.device(device) if device is not None else torch.device("cpu"))
         dev = device if device is not None else self.ctx.device
         self.device = torch.device(dev)
         self.tracer = Tracer(enabled=trace, rank=self.ctx.rank)
         self.storage = StorageManager(root=root, device=self.device, page_size=page_size, pool_pages=pool_pages,
-                                      rank=self.ctx.rank, device_budget=device_budget)
+                                      rank=self.ctx.rank, device_budget=device_budget, pinned_budget=pinned_budget)
         self.catalog = Catalog(catalog_path or os.path.join(self.storage.root, f"catalog_r{self.ctx.rank}.db"))
         self.engine = QueryEngine(self.storage, self.ctx, self.catalog, self.tracer, broadcast_threshold, fusion)
         self.policies = {}
@@ -62,6 +62,19 @@ class PDBClient:
         self.tail_trigger = None         # TailTrigger (arm_tail_trigger)
         if resume:
             self._resume()
+
+    @classmethod
+    def from_config(cls, conf, **kwargs) -> "PDBClient":
+        """A client built from a :class:`~netsdb_amd.utils.config.Configuration` (or a settings-file path);
+        keyword arguments override the file."""
+        from .utils.config import Configuration
+
+        if isinstance(conf, str):
+            conf = Configuration.load(conf)
+        kw = conf.client_kwargs()
+        kw.setdefault("root", conf.root_directory)
+        kw.update(kwargs)
+        return cls(**kw)
 
     # ------------------------------------------------------------------ checkpoint / resume
     def _resume(self):
