@@ -672,7 +672,11 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   // V19: this workgroup's static part stops steal_tq * steal_ch k-tiles short of its split's end; those tail
   // chunks (of every split of the tile) are claimed afterwards by whichever workgroup of the tile is free first
   if constexpr (V == 19) kend = max(kbeg, min(kend, kbeg + p.kchunk - p.steal_tq * p.steal_ch * BK));
-  int nk = max(0, (kend - kbeg + BK - 1) / BK);
+  if constexpr (V == 22) {   // pair range [2 * (split / 2) * kchunk, ...): this split takes every other k-tile
+    kbeg = (split & ~1) * p.kchunk;
+    kend = min(p.K, kbeg + 2 * p.kchunk);
+  }
+  int nk = V == 22 ? max(0, ((kend - kbeg + BK - 1) / BK - (split & 1) + 1) / 2) : max(0, (kend - kbeg + BK - 1) / BK);
   int niter = (nk + 1) >> 1;
 
   // KT (variant 9): K-tiled operands [K/64][ld rows][64] — every (tile, k-step) half-tile is one
@@ -715,11 +719,13 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   auto stage = [&](int buf, int slot, int u) {
     if constexpr (V == 4) return;
     const int k = kbeg + u * BK + kc;
-    const bool kin = k < kend;
+    const bool kin = (V == 22 ? kbeg + (2 * u + (split & 1)) * BK + kc : k) < kend;
     // memory-side diagnostics (timing only, wrong results): 13 every split streams the SAME K window
     // [0, kchunk) (unique bytes / splits: Infinity-Cache resident); 14 every workgroup cycles over 2 k-tiles
     // (L2/L1 resident: the L2 -> CU path alone)
-    const int ks = V == 13 ? k - kbeg : V == 14 ? (u & 1) * BK + kc : k;
+    // V22: the two splits an XCD runs interleave their k-tiles over the pair's joint K range (split parity p
+    // takes k-tiles 2u + p), so both stream the same DRAM pages at the same time
+    const int ks = V == 13 ? k - kbeg : V == 14 ? (u & 1) * BK + kc : V == 22 ? kbeg + (2 * u + (split & 1)) * BK + kc : k;
     char* dst = RING ? smem + buf * HALF : smem + buf * BUF + slot * HALF;   // RING: buf = ring slot
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -1652,6 +1658,8 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
     p.steal_ch = g_steal_ch;
     hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<19>, grid, dim3(512), 0, stream, p);
   }
+  else if (cfg == 25 && p.splits % 2 == 0)   // 8-phase, XCD split pairs interleave their k-tiles
+    hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<22>, grid, dim3(512), 0, stream, p);
   else if (cfg == 20)   // 8-phase with non-temporal operand loads
     hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<15>, grid, dim3(512), 0, stream, p);
   else if (cfg == 21)   // 8-phase, sc1 (L1 bypass) operand loads
