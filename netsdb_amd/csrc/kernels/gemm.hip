@@ -615,6 +615,8 @@ gemm_nt_tile_kernel(GemmParams p) {
 // 4 no DMA issued (load-free upper bound, wrong results), 5 no ds_reads after the first tile (wrong results),
 // 6 no vmcnt wait in the loop (racy), 7 zero-record descriptors (DMA issued, no memory traffic),
 // 8 vmcnt(2) instead of 6 (1 half-tile in flight: latency sensitivity)
+__device__ __forceinline__ void reduce_epilogue4(const GemmParams& p, int batch, long long MN, long long e, f32x4 s);
+
 template <int V>
 __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   constexpr int HALF = 128 * 128;            // bytes of one half-tile (128 rows x 64 bf16)
@@ -998,6 +1000,43 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
     return;
   }
   store_tile_lds<256, 256, 2, 4, TS>(acc, smem, (int)sizeof(smem), p, batch, split, m0, n0, tid, lane, wave);
+  if constexpr (V == 23) {
+    // split-K fix-up in the GEMM launch (no reducer kernel): every workgroup releases its slab and counts itself
+    // in on the tile's arrival counter; the last one to arrive sums the tile's slabs in split order (the
+    // reducer's order: bit-identical results) and runs the reducer's epilogue, then re-zeroes the counter.
+    // No workgroup waits on another (host guard: vec_ws, batch 1, no segmented B).
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();                                   // every wave's slab stores released; LDS image consumed
+    int* last = reinterpret_cast<int*>(smem);
+    if (tid == 0) {
+      const int c = __hip_atomic_fetch_add(&p.steal_cnt[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last[0] = (c == p.splits - 1) ? 1 : 0;
+    }
+    __syncthreads();
+    if (last[0] == 0) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const long long MN = (long long)p.M * p.N;
+    const int cq = tid & 63;                           // column quad of the tile (64 x 4 columns)
+    const int col = n0 + cq * 4;
+    if (col < p.N) {
+      for (int r = tid >> 6; r < 256 && m0 + r < p.M; r += 8) {
+        const long long e = (long long)(m0 + r) * p.N + col;
+        const float* w = p.ws + e;
+        f32x4 part[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+          if (k < p.splits) part[k] = *reinterpret_cast<const f32x4*>(w + k * MN);
+        f32x4 s = part[0];
+#pragma unroll
+        for (int k = 1; k < 16; ++k)
+          if (k < p.splits) s += part[k];
+        for (int k = 16; k < p.splits; ++k) s += *reinterpret_cast<const f32x4*>(w + k * MN);
+        reduce_epilogue4(p, 0, MN, e, s);
+      }
+    }
+    if (tid == 0) p.steal_cnt[tile] = 0;               // next launch is stream-ordered after this one
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1657,6 +1696,21 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
     p.steal_tq = g_steal_tq;
     p.steal_ch = g_steal_ch;
     hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<19>, grid, dim3(512), 0, stream, p);
+  }
+  else if (cfg == 26 && p.splits > 1 && batch == 1 && seg_k == 0 && p.vec_ws && p.tiles_m * p.tiles_n <= 4096) {
+    // 8-phase with the split-K fix-up by each tile's last-arriving workgroup (no reducer launch below):
+    // per-(device, stream) arrival counters, zeroed once here and re-zeroed by the fixing workgroup
+    static std::map<std::pair<int, void*>, int*> fix_bufs;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    int*& cnt = fix_bufs[{dev, (void*)stream}];
+    if (cnt == nullptr) {
+      if (hipMalloc((void**)&cnt, 4096 * sizeof(int)) != hipSuccess) return -7;
+      if (hipMemset(cnt, 0, 4096 * sizeof(int)) != hipSuccess) return -7;
+    }
+    p.steal_cnt = cnt;
+    hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<23>, grid, dim3(512), 0, stream, p);
+    return (int)hipGetLastError();
   }
   else if (cfg == 25 && p.splits % 2 == 0)   // 8-phase, XCD split pairs interleave their k-tiles
     hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<22>, grid, dim3(512), 0, stream, p);

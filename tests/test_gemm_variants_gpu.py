@@ -112,3 +112,28 @@ def test_ksteal_variant_vs_fp32(shape):
         err = ((o[rows] - ref).abs().max() / ref.abs().max()).item()
         assert err < 1e-4, err
         assert ((o - base).abs().max() / base.abs().max()).item() < 1e-5
+
+
+@pytest.mark.parametrize("shape", [(1000, 1000, 597568), (777, 1236, 40960), (300, 2000, 100000)])
+def test_fixup_variant_bit_exact(shape):
+    """Split-K fix-up by each tile's last-arriving workgroup (cfg 26, no reducer launch) sums the slabs in the
+    reducer's split order and runs its epilogue: bit-identical to cfg 2 + reducer, bias/relu/dropout/bf16 out
+    included; three launches in a row check that the fixing workgroups re-zero the arrival counters."""
+    M, N, K = shape
+    g = torch.Generator(device=DEV).manual_seed(3)
+    A = torch.empty(M, K, device=DEV).uniform_(-1, 1, generator=g).to(torch.bfloat16)
+    B = (torch.empty(N, K, device=DEV).uniform_(-1, 1, generator=g) * (3.0 / K) ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(M, device=DEV, generator=g) * 0.1
+    assert ops.gemm_splits(M, N, K) > 1
+    h = _ext.hip()
+
+    def run():
+        return ops.gemm_nt(A, B, bias, ops.BIAS_ROW, ops.ACT_RELU, dropout=0.5, seed=11)
+
+    h.gemm_force_config(2)
+    ref = run()
+    h.gemm_force_config(26)
+    outs = [run() for _ in range(3)]
+    torch.cuda.synchronize()
+    for o in outs:
+        assert torch.equal(o, ref)
