@@ -2,8 +2,8 @@
 stay bit-exact with the production 8-phase kernel (same k order, same fp32 accumulation): 4-wave 128x128
 per-wave kernels (LDS-DMA cfg 12, register-staged cfg 16), the 10-slot LDS ring (cfg 14), the untransposed
 LDS-staged epilogue (cfg 15) — plus the cfg-17 drift diagnostic (real-time stamps + XCD ids), the opt-in
-adaptive split-K K partition (gemm_set_adapt) and the opt-in K-tail stealing variant (cfg 24, exact but not
-bit-reproducible: checked against fp32 and cfg 2 instead)."""
+adaptive split-K K partition (gemm_set_adapt), the opt-in K-tail stealing variant (cfg 24, exact but not
+bit-reproducible: checked against fp32 and cfg 2 instead) and the in-launch split-K fix-up (cfg 26, bit-exact)."""
 import pytest
 import torch
 
