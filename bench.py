@@ -222,7 +222,7 @@ def main():
     client.wait_jobs()
     sync()
     dt = time.perf_counter() - t0
-    coll_per_step = (ctx.stats.get("collectives", 0) - coll0 - 1) / max(1, args.steps)   # minus sync()'s barrier
+    coll_per_step = (ctx.stats.get("collectives", 0) - coll0 - (1 if ctx.distributed else 0)) / max(1, args.steps)  # minus sync()'s barrier
     dt = ctx.all_reduce_scalar(dt, "max")
     rows_local = local_rows + cfg["images"]
     rows_total = ctx.all_reduce_scalar(float(rows_local), "sum") * args.steps
