@@ -34,13 +34,14 @@ SMALL = dict(batch=64, features=4096, hidden=256, labels=512, block_x=32, block_
              images=4, channels=3, height=32, width=32, filters=16, ksize=7)
 
 
-def verify(client, cv, ff, w, b, dev, nrows=16, nimg=2):
+def verify(client, cv, ff, w, b, dev, nrows=16, nimg=2, single_job=False):
     """Untimed correctness check after the timed steps: one more FF inference_unit with dropout 0,
     sampled output rows vs the fp32 network (hidden activations rounded to bf16 as the plan stores
     them), and sampled conv2d images vs F.conv2d in fp32. Returns max relative errors."""
     from netsdb_amd.models.blocks import to_tensor
 
-    ff.inference_unit(client, "ff", "w1", "wo", "inputs", "b1", "bo", "output", dropout_rate=0.0, seed=0)
+    ff.inference_unit(client, "ff", "w1", "wo", "inputs", "b1", "bo", "output", dropout_rate=0.0, seed=0,
+                      single_job=single_job)
     out = to_tensor(client, "ff", "output", gather=False).float()
     x_all = to_tensor(client, "ff", "inputs", gather=False)
     n = min(nrows, out.shape[0])
@@ -84,6 +85,9 @@ def main():
                     help="record one whole step (FF jobs + conv2d job) into a HIP graph after the warmup and time its "
                          "replays (PDBClient.capture_job: no host work per step; the dropout seed of the recorded "
                          "step is reused)")
+    ap.add_argument("--single-job", action="store_true",
+                    help="submit inference_unit as ONE job (no materialised 'yo' set: the output layer runs as one GEMM "
+                         "with the max-subtracted softmax in its epilogue); default: the reference's two jobs")
     ap.add_argument("--ksteal", action="store_true",
                     help="FF layer-1 split-K GEMM with K-tail stealing (opt-in: ~1 %% faster in isolation, summation "
                          "order varies run to run)")
@@ -158,7 +162,7 @@ def main():
 
     def ffjobs(i):
         ff.inference_unit(client, "ff", "w1", "wo", "inputs", "b1", "bo", "output", dropout_rate=args.dropout,
-                          seed=i)
+                          seed=i, single_job=args.single_job)
 
     def step(i):
         trig = client.arm_tail_trigger() if args.overlap == "tail" else None
@@ -227,7 +231,7 @@ def main():
     rows_local = local_rows + cfg["images"]
     rows_total = ctx.all_reduce_scalar(float(rows_local), "sum") * args.steps
     value = rows_total / dt
-    check = verify(client, cv, ff, w, b, dev)
+    check = verify(client, cv, ff, w, b, dev, single_job=args.single_job)
     if ctx.rank == 0:
         res = {
             "metric": "inference rows/sec (whole node), FF-NN + conv2d block",
@@ -258,6 +262,7 @@ def main():
                 "collectives_per_step": round(coll_per_step, 2),
                 "graph_replay": captured is not None,
                 "ksteal": bool(args.ksteal),
+                "single_job": bool(args.single_job),
             },
         }
         print(json.dumps(res), flush=True)
