@@ -58,8 +58,8 @@ static unsigned short f2bf(float f) {
   return (unsigned short)((u + 0x7fff + ((u >> 16) & 1)) >> 16);
 }
 
-int main() {
-  const int blocks = 512, n_ops = 8 * 64 * 8;   // 8 operand regs x 64 lanes x 8 bf16
+int main(int argc, char** argv) {
+  const int blocks = argc > 1 ? atoi(argv[1]) : 512, n_ops = 8 * 64 * 8;   // 8 operand regs x 64 lanes x 8 bf16
   std::vector<unsigned short> rnd(n_ops), zero(n_ops, 0);
   srand(1);
   for (auto& v : rnd) v = f2bf((float)rand() / (float)RAND_MAX * 2.f - 1.f);
@@ -91,7 +91,7 @@ int main() {
         float ms = 0.f;
         (void)hipEventElapsedTime(&ms, e0, e1);
         ms /= 10;
-        printf("rep %d %s %s: %.3f ms  %.0f TFLOP/s\n", rep, big ? "32x32x16" : "16x16x32", z ? "zeros " : "random",
+        printf("blocks %d rep %d %s %s: %.3f ms  %.0f TFLOP/s\n", blocks, rep, big ? "32x32x16" : "16x16x32", z ? "zeros " : "random",
                ms, 2 * macs / (ms * 1e-3) / 1e12);
       }
   return hipGetLastError() == hipSuccess ? 0 : 2;
