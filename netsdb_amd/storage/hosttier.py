@@ -66,18 +66,18 @@ class PinnedHostTier:
 
     def fetch(self, host: RecordBatch, ev: Optional[torch.cuda.Event], nbytes: int, pool=None):
         """Pinned host batch -> device batch (async H2D), ordered before the consumer stream's next work.
-        With the manager's page arena (``pool``) the copies land in slab-allocated regions: returns
-        (batch, regions)."""
+        With the manager's page arena (``pool``) the copies land in slab-allocated regions. Returns
+        (batch, regions); regions is empty without a pool."""
         consumer = torch.cuda.current_stream(self.device)
         regions = []
 
         def h2d(t: torch.Tensor) -> torch.Tensor:
             if pool is not None and t.device.type == "cpu" and t.numel() > 0:
-                h = pool.alloc(t.numel() * t.element_size())
-                if h is not None:
-                    d = pool.view(h, t.dtype, t.shape)
+                r = pool.alloc_region(t.numel() * t.element_size())
+                if r is not None:
+                    d = r.tensor().view(t.dtype).view(tuple(t.shape))
                     d.copy_(t, non_blocking=True)
-                    regions.append(h)
+                    regions.append(r)
                     return d
             d = t.to(self.device, non_blocking=True)
             # d is allocated on the copy stream's pool; the consumer reads it, so a free must wait for the
@@ -94,7 +94,7 @@ class PinnedHostTier:
         self.used = max(0, self.used - nbytes)
         self.stats["fetches"] += 1
         self.stats["bytes_in"] += nbytes
-        return (dev, regions) if pool is not None else dev
+        return dev, regions
 
     def release(self, nbytes: int):
         self.used = max(0, self.used - nbytes)

@@ -127,6 +127,7 @@ class StorageManager:
             elif p.location == "pinned" and self.host_tier is not None:
                 self.host_tier.release(p.nbytes)
             p.release_regions()
+            p.batch = None          # the region returns once no held batch views it any more
 
     # ----------------------------------------------------------- memory accounting / eviction
     def on_home(self, device) -> bool:

@@ -52,10 +52,13 @@ class Page:
         self.batch: Optional[RecordBatch] = batch
 
     def release_regions(self, events=()):
-        """Hand the page's arena regions back to the slab allocator (stream-ordered)."""
-        if self.regions:
-            self.set.manager.page_pool.release(self.regions, events)
-            self.regions = []
+        """Drop the page's hold on its arena regions. A region returns to the slab allocator when the last
+        tensor viewing it is gone (batches a scan yielded earlier stay valid) and every event in ``events``
+        (e.g. the eviction's D2H copy) has completed (storage/devpool.py)."""
+        for r in self.regions:
+            for e in events:
+                r.attach_event(e)
+        self.regions = []
 
     def is_resident(self) -> bool:
         return self.batch is not None
@@ -388,8 +391,6 @@ class DenseMatrixSet(UserSet):
     (H2D copies on the copy stream, ordered before the consumer by a stream wait).  Out-of-core
     consumers read row ranges with :meth:`load_rows` without making the whole panel resident."""
 
-    SPILL_BASE = 1 << 20        # pool page numbers of spilled slabs (persisted chunks use 0..)
-
     def __init__(self, manager, db, name, type_, set_id, page_size, device=None, persistent=True):
         super().__init__(manager, db, name, type_, set_id, page_size, device, persistent)
         self._panel: Optional[torch.Tensor] = None    # [local_rows_padded, ld] when resident
@@ -407,6 +408,10 @@ class DenseMatrixSet(UserSet):
         self.transposed = False                       # panel holds the logical matrix transposed
         self.replicated = False                       # every rank holds the full matrix
         self.stats_io = {"spills": 0, "reloads": 0, "slab_loads": 0}
+        # spilled slabs go to the page pool under a temp set id of their own with page numbers from 0 (the
+        # persisted chunks use this set's id): the page file offset is page_no * page_size, so the slabs must
+        # not sit at large page numbers of the set's own file
+        self._spill_id: Optional[int] = None
 
     # residency -------------------------------------------------------
     @property
@@ -495,10 +500,12 @@ class DenseMatrixSet(UserSet):
             data = part.contiguous().cpu().view(torch.uint8).numpy().tobytes()
             if len(data) > bm.page_size:
                 raise RuntimeError(f"dense slab {len(data)} B exceeds the pool page size {bm.page_size}")
-            pno = self.SPILL_BASE + i
-            slot = bm.pin(self.set_id, pno, True)
+            pno = i
+            if self._spill_id is None:
+                self._spill_id = next(self.manager._temp_ids)
+            slot = bm.pin(self._spill_id, pno, True)
             bm.slot_view(slot)[: len(data)] = data
-            bm.unpin(self.set_id, pno, True, len(data))
+            bm.unpin(self._spill_id, pno, True, len(data))
             slabs.append((r0, part.shape[0], "pool", pno, None))
         self._shape = (rows, ld, t.dtype, t.device)
         self._spilled = slabs
@@ -516,17 +523,17 @@ class DenseMatrixSet(UserSet):
             if device is not None and torch.device(device).type == "cuda":
                 from ..objects.record import RecordBatch
 
-                return tier.fetch(RecordBatch({"x": h}, n), ev, 0).columns["x"]
+                return tier.fetch(RecordBatch({"x": h}, n), ev, 0)[0].columns["x"]
             if ev is not None:
                 ev.synchronize()
             return h
         bm = self.manager.buffer_manager
-        slot = bm.pin(self.set_id, h, False)
+        slot = bm.pin(self._spill_id, h, False)
         try:
-            nb = bm.bytes_used(self.set_id, h)
+            nb = bm.bytes_used(self._spill_id, h)
             raw = bytearray(bm.slot_view(slot)[:nb])
         finally:
-            bm.unpin(self.set_id, h, False, 0)
+            bm.unpin(self._spill_id, h, False, 0)
         x = torch.frombuffer(raw, dtype=torch.uint8).view(dt).reshape(n, ld)
         return x.to(device) if device is not None else x
 
@@ -577,12 +584,8 @@ class DenseMatrixSet(UserSet):
         for r0, n, where, h, ev in self._spilled:
             if where == "pinned" and tier is not None:
                 tier.release(h.numel() * h.element_size())
-        if any(sl[2] == "pool" for sl in self._spilled):
-            bm = self.manager.buffer_manager
-            if hasattr(bm, "drop_page"):
-                for sl in self._spilled:
-                    if sl[2] == "pool":
-                        bm.drop_page(self.set_id, sl[3])
+        if any(sl[2] == "pool" for sl in self._spilled) and self._spill_id is not None:
+            self.manager.buffer_manager.drop_set(self._spill_id)
         self._spilled = None
         if not keep_charge:
             self._shape = None

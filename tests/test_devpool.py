@@ -43,6 +43,8 @@ def test_pages_live_in_the_arena_and_return_on_remove(tmp_path):
     got = torch.cat([b.columns["x"] for b in st.get_set("db", "s").scan()])
     torch.testing.assert_close(got, x)
     st.remove_set("db", "s")
+    assert pool.used() > 0            # `col` and `got`'s sources: a held view keeps its region
+    del col, pages
     assert pool.used() == 0 and pool.stats["frees"] >= pool.stats["allocs"] - 0
 
 
@@ -92,3 +94,50 @@ def test_gpu_pages_in_hbm_arena_with_eviction(tmp_path):
     torch.cuda.synchronize()
     st.page_pool._reclaim(block=True)
     assert st.page_pool.used() == 0
+
+
+def test_held_batches_survive_spill_and_region_reuse(tmp_path):
+    """A batch yielded by scan() stays valid after its page is spilled and the arena region is reused by the
+    next page load (the region is freed with the last tensor viewing it, not with page residency)."""
+    c = PDBClient(root=str(tmp_path), device="cpu")
+    st = c.storage
+    st.device_budget = 17 << 20
+    c.create_database("db")
+    s = st.create_set("db", "s", page_size=4 << 20)
+    x = torch.arange(10_000_000, dtype=torch.float32)
+    s.add_batch(RecordBatch({"x": x}, x.numel()))
+    assert st.stats["evicted_pages"] > 0
+    held = [b.columns["x"][1:] for b in s.scan()]     # derived views only: the page batches themselves are dropped
+    got = torch.cat([torch.cat([x[:1] * 0, h]) for h in held])
+    starts = torch.tensor([0] + [h.numel() + 1 for h in held]).cumsum(0)[:-1]
+    ref = x.clone()
+    ref[starts] = 0
+    torch.testing.assert_close(got, ref)
+    torch.testing.assert_close(s.all().columns["x"], x)
+
+
+def test_chunks_without_live_regions_go_back(tmp_path):
+    pool = DevicePagePool("cpu", chunk_bytes=1 << 20)
+    regs = [pool.alloc_region(600_000) for _ in range(4)]     # one region per chunk
+    assert pool.stats["chunks"] == 4
+    keep = regs[0].tensor()[:10]                               # a view keeps region 0 (and chunk 0) alive
+    del regs
+    assert pool.used() >= 600_000 and len(pool.slabs) == 1
+    assert pool.stats["chunks_released"] == 3
+    del keep
+    assert pool.used() == 0
+
+
+def test_dense_panel_spill_with_large_pool_pages(tmp_path):
+    """Dense spill slabs use a spill set of their own with page numbers from 0: a panel larger than the pool
+    spills with 64 MiB pages (page_no * page_size stays far below the file-size limit)."""
+    from netsdb_amd.storage.manager import StorageManager
+
+    st = StorageManager(root=str(tmp_path), device=None, page_size=64 << 20, pool_pages=2)
+    d = st.create_set("db", "m", dense=True)
+    panel = torch.randn(3 * 1024, 8192 * 2)                   # 192 MiB f32 > 2 pool pages of 64 MiB
+    d.set_panel(panel.clone(), 3 * 1024, 8192 * 2, 1024, 1024)
+    freed = d.spill()
+    assert freed > 0 and d.is_spilled()
+    torch.testing.assert_close(d.panel, panel)
+    st.remove_set("db", "m")
