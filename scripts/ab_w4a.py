@@ -1,0 +1,92 @@
+"""A/B of the asm-scheduled 4-wave GEMM (cfg 30/31/32 = schedules V0/V1/V2, gemm_w4a.hip) against the
+8-phase production kernel (cfg 2): correctness vs an fp32 reference on ragged / split / square shapes, then
+interleaved timing rounds in one process (CUDA events) on the FF layer-1 shape with the bench's operand data
+(inputs U(-1,1), W1 scaled by sqrt(3/K)) and on 8192^3 / 4096^3 with U(-1,1) operands.
+
+    python scripts/ab_w4a.py [--cfgs 2,30,31,32] [--rounds 5] [--check-only]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from netsdb_amd import _ext, ops  # noqa: E402
+
+
+def check(h, cfgs):
+    g = torch.Generator(device="cuda:0").manual_seed(1)
+    out = {}
+    for (M, N, K) in [(1000, 1000, 64 * 160), (300, 520, 4096), (256, 256, 64), (1000, 14588, 1024),
+                      (777, 1000, 64 * 37), (2048, 2048, 2048)]:
+        A = torch.empty(M, K, device="cuda:0").uniform_(-1, 1, generator=g).to(torch.bfloat16)
+        B = torch.empty(N, K, device="cuda:0").uniform_(-1, 1, generator=g).to(torch.bfloat16)
+        ref = A.float() @ B.float().t()
+        for c in cfgs:
+            h.gemm_force_config(c)
+            C = ops.gemm_nt(A, B, out_dtype=torch.float32)
+            torch.cuda.synchronize()
+            err = ((C - ref).abs().max() / ref.abs().max()).item()
+            out[f"{M}x{N}x{K}/cfg{c}"] = round(err, 7)
+            assert err < 1e-3 or c >= 33, (M, N, K, c, err)   # 33+: timing diagnostics (wrong results)
+    h.gemm_force_config(-1)
+    return out
+
+
+def timed(h, cfgs, A, B, rounds, iters):
+    ts = {c: [] for c in cfgs}
+    for _ in range(rounds):
+        for c in cfgs:
+            h.gemm_force_config(c)
+            for _ in range(3):
+                ops.gemm_nt(A, B)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(iters):
+                ops.gemm_nt(A, B)
+            e1.record()
+            torch.cuda.synchronize()
+            ts[c].append(e0.elapsed_time(e1) / iters)
+    h.gemm_force_config(-1)
+    return {f"cfg{c}": {"ms_min": round(min(v), 4), "ms_med": round(sorted(v)[len(v) // 2], 4)} for c, v in ts.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cfgs", default="2,30,31,32")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--check-only", action="store_true")
+    ap.add_argument("--shapes", default="ff,8192,4096")
+    a = ap.parse_args()
+    h = _ext.hip()
+    cfgs = [int(c) for c in a.cfgs.split(",")]
+    print(json.dumps({"check": check(h, cfgs)}), flush=True)
+    if a.check_only:
+        return
+    g = torch.Generator(device="cuda:0").manual_seed(0)
+    for shp in a.shapes.split(","):
+        if shp == "ff":
+            M, N, K = 1000, 1000, 597568
+            X = torch.empty(M, K, device="cuda:0").uniform_(-1, 1, generator=g).to(torch.bfloat16)
+            W = (torch.empty(N, K, device="cuda:0").uniform_(-1, 1, generator=g) * (3.0 / K) ** 0.5).to(torch.bfloat16)
+            r = timed(h, cfgs, W, X, a.rounds, a.iters)
+            flop = 2.0 * M * N * K
+            del X, W
+        else:
+            n = int(shp)
+            A = torch.empty(n, n, device="cuda:0").uniform_(-1, 1, generator=g).to(torch.bfloat16)
+            B = torch.empty(n, n, device="cuda:0").uniform_(-1, 1, generator=g).to(torch.bfloat16)
+            r = timed(h, cfgs, A, B, a.rounds, a.iters)
+            flop = 2.0 * n ** 3
+            del A, B
+        for v in r.values():
+            v["tflops_med"] = round(flop / (v["ms_med"] * 1e-3) / 1e12, 1)
+        print(json.dumps({shp: r}), flush=True)
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

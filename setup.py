@@ -20,7 +20,7 @@ KDIR = os.path.join("netsdb_amd", "csrc", "kernels")
 RDIR = os.path.join("netsdb_amd", "csrc", "runtime")
 
 
-HIP_SOURCES = ("gemm.hip", "conv2d.hip", "rowops.hip", "strings.hip", "dedup.hip")
+HIP_SOURCES = ("gemm.hip", "gemm_w4a.hip", "conv2d.hip", "rowops.hip", "strings.hip", "dedup.hip")
 
 
 def hip_ext():
@@ -63,7 +63,7 @@ def build_hip_extension(out_path: str, build_dir: str, jobs: int = 8):
         src = os.path.join(ROOT, KDIR, f)
         obj = os.path.join(build_dir, f + ".o")
         objs.append(obj)
-        hdrs = [os.path.join(ROOT, KDIR, h) for h in os.listdir(os.path.join(ROOT, KDIR)) if h.endswith(".h")]
+        hdrs = [os.path.join(ROOT, KDIR, h) for h in os.listdir(os.path.join(ROOT, KDIR)) if h.endswith((".h", ".inc"))]
         if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(x) for x in [src] + hdrs):
             continue
         if f.endswith(".hip"):
