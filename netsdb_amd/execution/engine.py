@@ -105,6 +105,9 @@ class QueryEngine:
         self._copart = set()
         self.ooc_fraction = 0.25          # of the device budget: in-memory build / group-by / tuple-set limit
         self._spools = []
+        # streaming shuffle (execution/shuffle.py): chunk size per round and cumulative round statistics
+        self.shuffle_chunk_bytes = 64 << 20
+        self.shuffle_stats = {}
         self.last_tcap = None
         self._last_comps = None
 
@@ -306,9 +309,9 @@ class QueryEngine:
                 probe = seg[0]
                 hcol = probe["input"]["atts"][0] if probe["_probe_side"] == "left" else probe["input2"]["atts"][0]
                 if probe.get("_strategy") == "partitioned":
-                    # collective repartition of the probe side by its join hash
-                    collected = [b for b in it if b.n]
-                    it = iter(self._shuffle_by(collected, hcol))
+                    # streaming repartition of the probe side by its join hash: chunks leave while the
+                    # source pipeline still runs, received batches flow into the probe
+                    it = self._stream_shuffle(it, hcol, "probe")
                 pb = state.builds.get(probe["output"]["name"])
                 if isinstance(pb, PartitionedBuild):
                     it = self._grace_probe(probe, it, pb, hcol, state)
@@ -349,6 +352,26 @@ class QueryEngine:
         finally:
             state.builds[name] = pb
             probe_parts.drop()
+
+    def _stream_shuffle(self, batches, hcol: Optional[str], tag: str, combine=None, key=None):
+        """Hash-shuffle a batch stream across ranks in chunk rounds (StreamingShuffle); yields received batches."""
+        from .shuffle import shuffle_stream
+
+        if self.ctx.world_size == 1:
+            yield from (b for b in batches if b is not None and b.n)
+            return
+        if tag in ("probe", "build"):
+            self.shuffle_count += 1         # repartitions of join inputs (JobStats["shuffles"])
+        keyf = key if key is not None else (lambda b: b.columns[hcol])
+        st = {}
+        try:
+            yield from shuffle_stream(self.ctx, batches, keyf, self.shuffle_chunk_bytes, stats=st, combine=combine)
+        finally:
+            st["shuffles"] = 1
+            for k, v in st.items():
+                self.shuffle_stats[k] = self.shuffle_stats.get(k, 0) + v
+            self.shuffle_stats.setdefault("by_tag", {})
+            self.shuffle_stats["by_tag"][tag] = self.shuffle_stats["by_tag"].get(tag, 0) + 1
 
     def _shuffle_by(self, batches: List[RecordBatch], hcol: str) -> List[RecordBatch]:
         ws = self.ctx.world_size
@@ -482,22 +505,21 @@ class QueryEngine:
             parts = (RecordBatch({c: x.columns[c] for c in cols}, x.n) for x in batches if x is not None and x.n)
             strat = sk["strategy"]
             name = a["output"]["name"]
-            if self.ctx.distributed and strat in ("broadcast", "partitioned"):
+            if self.ctx.distributed and strat == "broadcast":
                 parts = list(parts)
                 local = RecordBatch.concat(parts) if parts else None
-                if strat == "broadcast":
-                    got = self.ctx.broadcast_batch_all(local)
-                else:
-                    got = self._shuffle_by([local] if local is not None else [], hcol)
-                got = [g for g in got if g is not None and g.n]
-                parts = iter(got)
+                got = self.ctx.broadcast_batch_all(local)
+                parts = iter([g for g in got if g is not None and g.n])
+            elif self.ctx.distributed and strat == "partitioned":
+                # streaming shuffle straight into the (spillable) build table
+                parts = self._stream_shuffle(parts, hcol, "build")
             state.builds[name] = self._build_table(parts, hcol, st)
             return
         if kind == "aggregate":
             self._aggregate(sk["atom"], batches, state)
             return
         if kind == "partition":
-            self._partition(sk["atom"], [x for x in batches if x is not None], state)
+            self._partition(sk["atom"], batches, state)
             return
         raise ValueError(kind)
 
@@ -573,14 +595,42 @@ class QueryEngine:
             return
         op = getattr(comp, "reduce_op", "sum")
         combine = comp.combine
-        # stream (key, value) pairs; past the out-of-core limit hash-partition them by key into spools
-        # and reduce each partition alone (its groups are disjoint from every other partition's)
+        kv = (RecordBatch({"k": x.columns[kcol], "v": x.columns[vcol]}, x.n) for x in batches if x is not None and x.n)
+        if not self.ctx.distributed:
+            reps, agg = self._reduce_kv(kv, op, combine)
+        else:
+            # CombinerProcessor -> streaming shuffle by key hash -> AggregationProcessor: every chunk of (key,
+            # value) pairs is combined locally before it is sent (CombinedShuffleSink), the shuffle rounds leave
+            # while the pipeline runs, and the receiving side merges what arrives with the out-of-core
+            # (hash-partitioned) reduction
+            merge_op = "sum" if op == "count" else op
+
+            def combiner(batch):
+                inv, reps_c, g = K.group_ids(batch.columns["k"])
+                vals = batch.columns["v"]
+                agg_c = K.segment_reduce(vals, inv, g, op if isinstance(vals, torch.Tensor) else None, combine)
+                loc = RecordBatch({"k": reps_c, "v": _normalize(agg_c, len(agg_c), None)}, len(agg_c))
+                return loc, K.hash_keys(reps_c, loc.device)
+
+            recv = self._stream_shuffle(kv, None, "aggregate", combine=combiner, key=lambda b: None)
+            reps, agg = self._reduce_kv(recv, merge_op, combine)
+        if reps is None:
+            state.materialized[out_ts] = []
+            return
+        out = comp.make_output(reps, agg)
+        state.materialized[out_ts] = [RecordBatch({out_col: out}, out.n)]
+
+    def _reduce_kv(self, kv_batches, op, combine):
+        """(key, value) batches -> (representative keys, aggregates). Streamed; past the out-of-core limit the
+        pairs are hash-partitioned by key into spools and each partition is reduced alone (its groups are
+        disjoint from every other partition's)."""
+        from .spool import PartitionedSpool
+
         limit = self._ooc_limit()
         held, size, pspool = [], 0, None
-        for x in batches:
-            if x is None or x.n == 0:
+        for kv in kv_batches:
+            if kv is None or kv.n == 0:
                 continue
-            kv = RecordBatch({"k": x.columns[kcol], "v": x.columns[vcol]}, x.n)
             if pspool is not None:
                 pspool.add(kv, K.hash_keys(kv.columns["k"], kv.device))
                 continue
@@ -609,33 +659,11 @@ class QueryEngine:
             if pspool is not None:
                 pspool.drop()
                 self.ooc_stats["partitioned_aggregations"] = self.ooc_stats.get("partitioned_aggregations", 0) + 1
-        if reps_parts:
-            reps = reps_parts[0] if len(reps_parts) == 1 else column_concat(reps_parts)
-            agg = agg_parts[0] if len(agg_parts) == 1 else column_concat(agg_parts)
-        else:
-            reps, agg = None, None
-        if self.ctx.distributed:
-            # combiner output -> shuffle by key hash -> final merge (netsDB CombinerProcessor/AggregationProcessor)
-            if reps is not None:
-                kc = reps if isinstance(reps, (tuple, torch.Tensor)) else reps
-                local = RecordBatch({"k": kc, "v": _normalize(agg, len(agg), None)}, len(agg))
-                dest = K.partition_of(K.hash_keys(kc, local.device), self.ctx.world_size)
-                parts = K.split_by_dest(local, dest, self.ctx.world_size)
-            else:
-                parts = [None] * self.ctx.world_size
-            got = [x for x in self.ctx.exchange(parts) if x is not None and x.n]
-            if got:
-                merged = RecordBatch.concat(got)
-                inv, reps, g = K.group_ids(merged.columns["k"])
-                vv = merged.columns["v"]
-                agg = K.segment_reduce(vv, inv, g, op if isinstance(vv, torch.Tensor) else None, combine)
-            else:
-                reps, agg = None, None
-        if reps is None:
-            state.materialized[out_ts] = []
-            return
-        out = comp.make_output(reps, agg)
-        state.materialized[out_ts] = [RecordBatch({out_col: out}, out.n)]
+        if not reps_parts:
+            return None, None
+        reps = reps_parts[0] if len(reps_parts) == 1 else column_concat(reps_parts)
+        agg = agg_parts[0] if len(agg_parts) == 1 else column_concat(agg_parts)
+        return reps, agg
 
     def _topk(self, comp, batches, kcol, vcol, out_ts, out_col, state):
         objs, scores = [], []
@@ -667,22 +695,23 @@ class QueryEngine:
         state.materialized[out_ts] = [RecordBatch({out_col: local.columns["o"]}, local.n)]
 
     def _partition(self, a, batches, state):
+        """PartitionComp: rows go to the rank owning their key hash in streaming shuffle rounds; what arrives is
+        appended to the target set (if any) as it comes, never concatenated whole."""
         comp = state.comps[a["comp"]]
         kcol, ocol = a["input"]["atts"]
-        nonempty = [RecordBatch({"k": x.columns[kcol], "o": x.columns[ocol]}, x.n) for x in batches if x.n]
-        local = RecordBatch.concat(nonempty) if nonempty else None
-        ws = self.ctx.world_size
-        if local is not None:
-            dest = K.partition_of(K.hash_keys(local.columns["k"], local.device), ws)
-            parts = K.split_by_dest(local, dest, ws)
-        else:
-            parts = [None] * ws
-        got = [g for g in self.ctx.exchange(parts) if g is not None and g.n]
+        kb = (RecordBatch({"k": x.columns[kcol], "o": x.columns[ocol]}, x.n) for x in batches if x is not None and x.n)
+        recv = self._stream_shuffle(kb, None, "partition", key=lambda b: K.hash_keys(b.columns["k"], b.device))
         out_ts, out_col = a["output"]["name"], a["output"]["atts"][0]
-        objs = RecordBatch.concat([g for g in got]).columns["o"] if got else None
-        if objs is not None and getattr(comp, "set_name", "") and self.storage.has_set(comp.db, comp.set_name):
-            self.storage.get_set(comp.db, comp.set_name).add_batch(objs)
-        state.materialized[out_ts] = [RecordBatch({out_col: objs}, objs.n)] if objs is not None else []
+        target = None
+        if getattr(comp, "set_name", "") and self.storage.has_set(comp.db, comp.set_name):
+            target = self.storage.get_set(comp.db, comp.set_name)
+        outs = []
+        for g in recv:
+            objs = g.columns["o"]
+            if target is not None:
+                target.add_batch(objs)
+            outs.append(RecordBatch({out_col: objs}, g.n))
+        state.materialized[out_ts] = outs
 
 
 class _JobState:

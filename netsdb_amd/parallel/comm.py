@@ -193,6 +193,17 @@ class ClusterContext:
             self._coll(dist.all_to_all_single, out, src, recv, list(send_counts))
         return out.to(t.device), recv
 
+    def all_to_all_bytes_async(self, out: torch.Tensor, inp: torch.Tensor, out_splits: Sequence[int],
+                               in_splits: Sequence[int]):
+        """Issue one variable-split all-to-all of byte buffers WITHOUT waiting (the streaming shuffle's data
+        round); wait for the returned work with :meth:`_wait` (heartbeat-checked). On RCCL the transfer runs on
+        the communicator's stream, ordered after the work already queued on the current stream."""
+        self.stats["collectives"] += 1
+        if self.health is not None:
+            self.health.check()
+            self.health.mark_progress()
+        return dist.all_to_all_single(out, inp, list(out_splits), list(in_splits), async_op=True)
+
     def reduce_scatter_rows(self, t: torch.Tensor, counts: Sequence[int]) -> torch.Tensor:
         """Sum ``t`` over ranks and return this rank's row slice (counts[r] rows per rank)."""
         if not self.distributed:
@@ -244,13 +255,24 @@ class ClusterContext:
         counts = [p.n for p in parts]
         recv_cols: Dict[str, Any] = {}
         recv_counts = None
+        # every fixed-width tensor column rides ONE all-to-all as a packed row image (one count exchange for
+        # the whole batch instead of one per column); strings / nested / objects follow column by column
+        from ..execution.shuffle import PackedSchema
+
+        tcols = [cm for cm in ref_meta["columns"] if cm["kind"] == "tensor"]
+        if tcols:
+            ps = PackedSchema({"type": ref_meta["type"], "columns": tcols})
+            t = torch.cat([ps.pack(RecordBatch({cm["name"]: _as_tensor(p.columns[cm["name"]], cm, self.device)
+                                                for cm in tcols}, p.n)) for p in parts])
+            out, recv_counts = self.all_to_all_rows(t, counts)
+            got = ps.unpack(out)
+            for cm in tcols:
+                recv_cols[cm["name"]] = got.columns[cm["name"]]
         for cm in ref_meta["columns"]:
             name = cm["name"]
             if cm["kind"] == "tensor":
-                t = torch.cat([_as_tensor(p.columns[name], cm, self.device) for p in parts])
-                out, recv_counts = self.all_to_all_rows(t, counts)
-                recv_cols[name] = out
-            elif cm["kind"] == "string":
+                continue
+            if cm["kind"] == "string":
                 recv_cols[name] = self._exchange_strings([p.columns[name] for p in parts], counts)
                 recv_counts = recv_cols[name][1]
             elif cm["kind"] in ("nested", "map"):
@@ -371,10 +393,41 @@ class ClusterContext:
         return out, rcounts
 
     def broadcast_batch_all(self, b: Optional[RecordBatch]) -> List[RecordBatch]:
-        """All-gather: every rank receives every rank's batch (broadcast join build side)."""
+        """All-gather: every rank receives every rank's batch (broadcast join build side). Fixed-width tensor
+        batches go as ONE packed row image through all_gather(_into_tensor) (one copy of the local batch on
+        the wire, not world_size copies through an all-to-all); other batches use the record exchange."""
         if not self.distributed:
             return [b] if b is not None else []
-        return self.exchange([b] * self.world_size)
+        from ..execution.shuffle import PackedSchema
+
+        flat = _flatten(b) if b is not None else None
+        meta = self._agree_schema(_batch_meta(flat))
+        if meta is None:
+            return []
+        if not PackedSchema.supports(meta):
+            return self.exchange([b] * self.world_size)
+        ps = PackedSchema(meta)
+        if flat is not None and _batch_meta(flat) != meta:
+            raise RuntimeError(f"broadcast schema mismatch: {_batch_meta(flat)} vs {meta}")
+        rows = ps.pack(flat) if flat is not None else torch.empty(0, ps.row_bytes, dtype=torch.uint8, device=self.device)
+        ns = [x[0] for x in self.all_gather_ints([rows.shape[0]])]
+        mx = max(ns)
+        if mx == 0:
+            return []
+        cd = self._comm_device()
+        src = rows.to(cd)
+        if src.shape[0] < mx:
+            src = torch.cat([src, src.new_zeros((mx - src.shape[0], ps.row_bytes))])
+        src = src.contiguous()
+        if self.tensor_collectives:
+            out = src.new_empty((self.world_size * mx, ps.row_bytes))
+            self._coll(dist.all_gather_into_tensor, out, src)
+            outs = [out[i * mx:(i + 1) * mx] for i in range(self.world_size)]
+        else:
+            outs = [torch.empty_like(src) for _ in range(self.world_size)]
+            self._coll(dist.all_gather, outs, src)
+        t = lookup_type(meta["type"]) if meta["type"] else None
+        return [_unflatten(ps.unpack(o[:k].to(self.device), t)) for o, k in zip(outs, ns) if k]
 
 
 _SEP = "\x1f"

@@ -377,13 +377,77 @@ class MatmulNode(Node):
                 out[n0:n1].copy_(r.t())
         return out
 
+    def _kpartial_overlapped(self, engine, X, Y, phys_is_c, R, Ccols, counts, eq):
+        """Σ_ranks (X . Y^T) (or Y . X^T), reduce-scattered by rows, in column chunks: the chunk-c partial
+        [ws * eq, cw] f32 is written by the MFMA GEMM straight into the collective's send buffer (rows past R
+        zeroed once), its reduce-scatter is issued asynchronously (RCCL runs it on its own stream) and the
+        GEMM of chunk c+1 runs meanwhile. At most two chunk partials are alive at any time (the one reducing
+        and the one being computed) instead of one f32 partial of the whole [R, Ccols] output (the LA
+        DSL's 64k x 64k K-split product: 16 GiB per rank before). Reference pattern:
+        src/sharedLibraries/headers/LASillyMultiply1Join.h + LASillyMultiply2Aggregate.h (per-block partial
+        products aggregated by key), realised as GEMM + reduce-scatter on the node's xGMI links."""
+        ctx = engine.ctx
+        ws, r = ctx.world_size, ctx.rank
+        dev = X.device
+        cd = ctx._comm_device()
+        loc = torch.empty(counts[r], Ccols, dtype=torch.float32, device=dev)
+        chunks = _kpartial_chunks(Ccols)
+        st = engine.__dict__.setdefault("ooc_stats", {})
+        live = {"bytes": 0, "peak": 0}
+
+        def alloc(nbytes):
+            live["bytes"] += nbytes
+            live["peak"] = max(live["peak"], live["bytes"])
+
+        def start(c0, c1):
+            cw = c1 - c0
+            P = torch.empty(ws * eq, cw, dtype=torch.float32, device=dev)
+            alloc(P.numel() * 4)
+            if ws * eq > R:
+                P[R:].zero_()
+            if phys_is_c:
+                ops.gemm_nt(X, Y[c0:c1], out_dtype=torch.float32, out=P[:R])
+            else:
+                ops.gemm_nt(Y, X[c0:c1], out_dtype=torch.float32, out=P[:R])
+            src = P.to(cd)
+            if ctx.health is not None:
+                ctx.health.check()
+                ctx.health.mark_progress()
+            ctx.stats["collectives"] += 1
+            if ctx.tensor_collectives:
+                out = torch.empty(eq, cw, dtype=torch.float32, device=cd)
+                work = dist.reduce_scatter_tensor(out, src, op=dist.ReduceOp.SUM, async_op=True)
+            else:
+                out = src
+                work = dist.all_reduce(src, async_op=True)
+            return P, out, work
+
+        def finish(c0, c1, P, out, work):
+            ctx._wait(work)
+            got = out[: counts[r]] if ctx.tensor_collectives else out[r * eq: r * eq + counts[r]]
+            loc[:, c0:c1].copy_(got.to(dev))
+            live["bytes"] -= P.numel() * 4
+
+        pending = None
+        for c0, c1 in chunks:
+            nxt = (c0, c1) + start(c0, c1)          # this chunk's GEMM overlaps the previous reduce-scatter
+            if pending is not None:
+                finish(*pending)
+            pending = nxt
+        if pending is not None:
+            finish(*pending)
+        st["kpartial_chunks"] = st.get("kpartial_chunks", 0) + len(chunks)
+        st["kpartial_peak_partial_bytes"] = max(st.get("kpartial_peak_partial_bytes", 0), live["peak"])
+        st["kpartial_full_partial_bytes"] = max(st.get("kpartial_full_partial_bytes", 0), ws * eq * Ccols * 4)
+        return loc
+
     def _kpartial(self, engine, opA: Dense, opB: Dense, M, N, phys_is_c, bias_t, act, odt) -> Dense:
         """K-split product: each rank multiplies the K range it holds (A's column slab and/or B's row
-        slab, slicing the replicated operand to that range) into an f32 partial of the whole output,
-        then reduce-scatter sums the partials and leaves each rank its block-row range of C (C^T when
-        the consumer wants the transposed layout) — then the epilogue runs on the local slice.  The
-        K-range agreement is cached plan metadata; for RCCL's equal-slice reduce-scatter the GEMM writes
-        straight into the padded send buffer (no zero-pad copy of the partial)."""
+        slab, slicing the replicated operand to that range) into f32 partials of the output, and
+        reduce-scatter sums them so each rank keeps its block-row range of C (C^T when the consumer wants
+        the transposed layout) — then the epilogue runs on the local slice. The partial is produced and
+        reduced in column chunks, pipelined (:meth:`_kpartial_overlapped`). The K-range agreement is cached
+        plan metadata."""
         ctx = engine.ctx
         ws, r = ctx.world_size, ctx.rank
         if opA.part == "cols" and opB.part == "rows":
@@ -417,16 +481,7 @@ class MatmulNode(Node):
         per = (nb + ws - 1) // ws
         counts = [max(0, min(R, (s + 1) * per * blk) - min(R, s * per * blk)) for s in range(ws)]
         off = min(R, r * per * blk)
-        if ctx.tensor_collectives and len(set(counts)) > 1:
-            eq = per * blk
-            Pp = torch.empty(eq * ws, Ccols, dtype=torch.float32, device=X.device)
-            Pp[R:].zero_()
-            (ops.gemm_nt(X, Y, out_dtype=torch.float32, out=Pp[:R]) if phys_is_c else
-             ops.gemm_nt(Y, X, out_dtype=torch.float32, out=Pp[:R]))
-            loc = ctx.reduce_scatter_rows(Pp, [eq] * ws)[: counts[r]]
-        else:
-            P = ops.gemm_nt(X, Y, out_dtype=torch.float32) if phys_is_c else ops.gemm_nt(Y, X, out_dtype=torch.float32)
-            loc = ctx.reduce_scatter_rows(P, counts)
+        loc = self._kpartial_overlapped(engine, X, Y, phys_is_c, R, Ccols, counts, per * blk)
         # epilogue on the local rows: bias along C rows (phys rows when phys_is_c) is sliced by offset
         along_phys_rows = (self.bias_along == "row") == phys_is_c
         b = None
@@ -445,6 +500,14 @@ class MatmulNode(Node):
         if self.transpose_out:
             return Dense(y, counts[r], M, False, bc, br, "rows", off, total)
         return Dense(y, M, counts[r], True, br, bc, "cols", off, total)
+
+
+def _kpartial_chunks(ccols: int, target: int = 8):
+    """Column chunks of the K-split partial: ~``target`` chunks of whole 256-column GEMM tiles."""
+    if ccols <= 256:
+        return [(0, ccols)]
+    step = max(256, ((ccols + target - 1) // target + 255) // 256 * 256)
+    return [(c0, min(ccols, c0 + step)) for c0 in range(0, ccols, step)]
 
 
 class SoftmaxNode(Node):

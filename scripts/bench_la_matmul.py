@@ -30,7 +30,13 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--check", type=int, default=32, help="output rows checked against an fp32 reference")
+    ap.add_argument("--op", choices=["mul", "tmul"], default="mul",
+                    help="mul: C = A %%*%% B (row x K split, all-gather pipeline); tmul: C = A '* B (K x K split, "
+                         "overlapped chunked reduce-scatter)")
+    ap.add_argument("--small", action="store_true", help="CPU/contract size: 320 x 320 in blocks of 64, 1 step")
     a = ap.parse_args()
+    if a.small:
+        a.size, a.block, a.steps, a.warmup = 320, 64, 1, 0
 
     from netsdb_amd.client import PDBClient
     from netsdb_amd.la import LAInstance
@@ -46,7 +52,7 @@ def main():
     B.load_matrix(c, "LA_db", "A_in", n, n, bs, bs, seed=11, partition_rows=True)
     B.load_matrix(c, "LA_db", "B_in", n, n, bs, bs, seed=12, partition_rows=True)
     la.vars.update({"A": "A_in", "B": "B_in"})
-    prog = "C = A %*% B"
+    prog = "C = A %*% B" if a.op == "mul" else "C = A '* B"
 
     def sync():
         if ctx.device.type == "cuda":
@@ -78,24 +84,35 @@ def main():
         Al = sa.matrix()[:rows, :n].float()
         ref = torch.zeros_like(Cl)
         rng = torch.tensor([[sb.row_offset, sb.local_rows]], device=ctx.device)
-        for s, pr in enumerate(ctx.all_gather_tensor(rng)):
-            k0, kn = int(pr[0, 0]), int(pr[0, 1])
-            Bs = sb.matrix()[:kn, :n].contiguous() if s == ctx.rank else torch.empty(kn, n, dtype=sb.panel.dtype,
-                                                                                        device=ctx.device)
+        ranges = [(int(pr[0, 0]), int(pr[0, 1])) for pr in ctx.all_gather_tensor(rng)]
+
+        def full(st, s, k0, kn):
+            M = st.matrix()[:kn, :n].contiguous() if s == ctx.rank else torch.empty(kn, n, dtype=st.panel.dtype,
+                                                                                    device=ctx.device)
             if ctx.distributed:
-                torch.distributed.broadcast(Bs, src=s)
-            ref += Al[:, k0:k0 + kn] @ Bs.float()
-        err = float((Cl - ref).abs().max() / ref.abs().max().clamp(min=1e-6))
+                torch.distributed.broadcast(M, src=s)
+            return M.float()
+
+        if a.op == "mul":
+            for s, (k0, kn) in enumerate(ranges):
+                ref += Al[:, k0:k0 + kn] @ full(sb, s, k0, kn)
+        else:
+            # C = A^T B: this rank's output rows are columns [c0, c0 + rows) of A
+            c0 = sc.row_offset
+            for s, (k0, kn) in enumerate(ranges):
+                As = full(sa, s, k0, kn)
+                ref += As[:, c0:c0 + rows].t() @ full(sb, s, k0, kn)
+        err = float((Cl - ref).abs().max() / ref.abs().max().clamp(min=1e-6)) if Cl.numel() else 0.0   # empty rank
         err = ctx.all_reduce_scalar(err, "max")
     flops = 2.0 * n * n * n
     if ctx.rank == 0:
         st = la.job_stats[-1] if la.job_stats else {}
-        print(json.dumps({"metric": "LA DSL C = A %*% B dense matmul", "n": n, "block": bs, "blocks_per_dim": nb,
+        print(json.dumps({"metric": f"LA DSL {prog} dense matmul", "n": n, "block": bs, "blocks_per_dim": nb,
                           "n_gpus": ctx.world_size, "ms_per_multiply": round(dt * 1e3, 3),
                           "tflops_total": round(flops / dt / 1e12, 1),
                           "tflops_per_gpu": round(flops / dt / 1e12 / ctx.world_size, 1), "dtype": "bf16",
                           "data": "synthetic random", "rel_err_sampled": err,
-                          "fused": st.get("fused_ops")}), flush=True)
+                          "fused": st.get("fused_ops"), "out_of_core": st.get("out_of_core")}), flush=True)
     if ctx.distributed:
         torch.distributed.destroy_process_group()
 

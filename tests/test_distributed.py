@@ -483,3 +483,91 @@ def test_distributed_learned_placement_skips_join_shuffle():
         assert [(x["l_shipmode"], x["high_line_count"], x["low_line_count"]) for x in r["q12"]] == \
             [(x["l_shipmode"], x["high_line_count"], x["low_line_count"]) for x in ref]
         assert all(v > 0 for v in r["hist"].values()), r["hist"]
+
+
+# ------------------------------------------------------------------ 8 ranks (the whole MI355X node), uneven
+def _kpartial_wide_scenario(ctx, out_dir):
+    """A '* B with a 1280-column output: the K-split partial is produced and reduce-scattered in 256-column
+    chunks, pipelined; at most two chunk partials are alive (fusion.MatmulNode._kpartial_overlapped)."""
+    from netsdb_amd.client import PDBClient
+    from netsdb_amd.computations import ScanSet, WriteSet
+    from netsdb_amd.la import computations as L
+    from netsdb_amd.models import blocks as B
+
+    c = PDBClient(ctx=ctx, root=tempfile.mkdtemp())
+    c.create_database("LA_db")
+    g = torch.Generator().manual_seed(5)
+    A = torch.rand(40, 72, generator=g) - 0.5
+    Bm = torch.rand(40, 1280, generator=g) - 0.5
+    B.load_tensor(c, "LA_db", "A", A, 8, 8, dtype=torch.float32, partition_rows=True)
+    B.load_tensor(c, "LA_db", "B", Bm, 8, 64, dtype=torch.float32, partition_rows=True)
+    c.create_set("LA_db", "C", None, dense=True)
+    j = L.LATransposeMultiply1Join()
+    j.set_input(0, ScanSet("LA_db", "A"))
+    j.set_input(1, ScanSet("LA_db", "B"))
+    st = c.execute_computations(WriteSet("LA_db", "C").set_input(L.LAMultiply2Aggregate().set_input(j)))
+    C = B.to_tensor(c, "LA_db", "C")
+    return {"err": (C.float() - A.t() @ Bm).abs().max().item(), "ooc": st.get("out_of_core", {}),
+            "local_rows": c.get_set("LA_db", "A").local_rows}
+
+
+@pytest.mark.timeout(900)
+def test_distributed_8ranks_uneven_la_ff_dedup_engine():
+    """world_size 8 (one rank per GPU of an MI355X node) on gloo: 40 rows in blocks of 8 put 8 rows on ranks
+    0-4 and none on ranks 5-7. The all-gather N-chunk pipeline (A %*% B), the K-split reduce-scatter
+    (A '* B, narrow and chunked-wide), partitioned FF inference, the cross-GPU dedup pool and the engine's
+    broadcast / partitioned joins + shuffle aggregation all run and match their references."""
+    res = _run("_la_dist4_scenario", ws=8)
+    assert [r["local_rows"] for r in res] == [8, 8, 8, 8, 8, 0, 0, 0]
+    for r in res:
+        assert r["mul"] < 1e-4 and r["tmul"] < 1e-4, r
+        assert r["mul_shape"] == (40, 24) and r["tmul_shape"] == (40, 24)
+    wide = _run("_kpartial_wide_scenario", ws=8)
+    for r in wide:
+        assert r["err"] < 1e-4, r
+        o = r["ooc"]
+        assert o["kpartial_chunks"] == 5, o
+        # peak extra memory of the K-split partial: two chunk partials, not the whole output's
+        assert o["kpartial_peak_partial_bytes"] <= 2 * (o["kpartial_full_partial_bytes"] // 5) + 4096, o
+        assert o["kpartial_peak_partial_bytes"] < o["kpartial_full_partial_bytes"]
+    for r in _run("_ff_scenario", ws=8):
+        assert r["err"] < 1e-4, r
+    for r in _run("_dedup_scenario", ws=8):
+        assert r["err"] == 0.0 and r["err2"] == 0.0 and r["stored"] == 12 + 3
+    from tests.test_engine import _emps
+
+    eng = _run("_engine_scenario", ws=8)
+    floors = {"eng": 3, "ops": 1, "hr": 2}
+    exp = sorted((e.name, e.department, floors[e.department]) for e in _emps(60) if e.department in floors)
+    tot = {}
+    for e in _emps(60):
+        tot[e.department] = tot.get(e.department, 0.0) + e.salary
+    for tag in ("broadcast", "partitioned"):
+        assert all(r[f"join_{tag}"] == exp for r in eng)
+        assert sum(r[f"local_emps_{tag}"] for r in eng) == 60
+        assert all(r[f"agg_{tag}"] == sorted((k, round(v, 6)) for k, v in tot.items()) for r in eng)
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("op", ["mul", "tmul"])
+def test_bench_la_matmul_small_8ranks_contract(op):
+    """scripts/bench_la_matmul.py --small under torchrun with 8 CPU ranks (gloo): one JSON line from rank 0,
+    the sampled output rows match the fp32 reference, and the fused distributed matmul ran."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(root, "scripts", "bench_la_matmul.py"), "--small", "--op", op]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=tempfile.gettempdir(), env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 8 and r["rel_err_sampled"] < 1e-2, r
+    assert any("matmul" in f for f in r["fused"]), r
+    if op == "tmul":
+        assert r["out_of_core"]["kpartial_chunks"] >= 2, r
