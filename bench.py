@@ -88,9 +88,6 @@ def main():
     ap.add_argument("--single-job", action="store_true",
                     help="submit inference_unit as ONE job (no materialised 'yo' set: the output layer runs as one GEMM "
                          "with the max-subtracted softmax in its epilogue); default: the reference's two jobs")
-    ap.add_argument("--ksteal", action="store_true",
-                    help="FF layer-1 split-K GEMM with K-tail stealing (opt-in: ~1 %% faster in isolation, summation "
-                         "order varies run to run)")
     ap.add_argument("--rownorm-loads", choices=["nt", "plain"], default=None,
                     help="row-normalise row loads: non-temporal (library default) or cache-allocating")
     ap.add_argument("--conv-kernel", choices=["rows", "rowfull"], default=None,
@@ -141,10 +138,6 @@ def main():
         from netsdb_amd import _ext
 
         _ext.hip().conv2d_rowfull(1 if args.conv_kernel == "rowfull" else 0)
-    if args.ksteal and dev.type == "cuda":
-        from netsdb_amd import _ext
-
-        _ext.hip().gemm_set_steal(1)
     if args.rownorm_loads is not None and dev.type == "cuda":
         from netsdb_amd import _ext
 
@@ -261,7 +254,6 @@ def main():
                 "ff_steps_in_flight": inflight,
                 "collectives_per_step": round(coll_per_step, 2),
                 "graph_replay": captured is not None,
-                "ksteal": bool(args.ksteal),
                 "single_job": bool(args.single_job),
             },
         }

@@ -11,24 +11,17 @@
 #include <utility>
 
 extern "C" {
-int nsdb_gemm_splits(int M, int N, int K, int batch);
-void nsdb_gemm_force_config(int cfg);
-void nsdb_gemm_set_stamps(void* ptr);
-void nsdb_gemm_set_adapt(int on);
-void nsdb_gemm_steal(int tq, int ch);
-void nsdb_gemm_set_steal(int on);
-void nsdb_tail_trigger_arm(void* flag, unsigned value);
-int nsdb_tail_trigger_consumed();
-void nsdb_tail_trigger_disarm();
+int nsdb_gemm_splits(int M, int N, int K, int batch, int cfg);
+int nsdb_gemm_tail_eligible(int M, int N, int K, int batch, int splits, int cfg);
 int nsdb_stream_wait_value(hipStream_t stream, void* flag, unsigned value);
-int nsdb_gemm_adapt_state(int M, int N, int K, float* out);
 int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const float* bias, int M, int N, int K,
                       long long lda, long long ldb, long long ldc, long long sA, long long sB, long long sC,
                       long long sBias, int batch, int splits, int act, int bias_mode, int out_f32, float alpha,
-                      float dropout, unsigned long long seed, int accumulate, long long seg_k, long long seg_stride_b, hipStream_t stream);
+                      float dropout, unsigned long long seed, int accumulate, long long seg_k, long long seg_stride_b,
+                      const void* opts, hipStream_t stream);
 int nsdb_gemm_nt_softmax(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, long long lda,
                          long long ldb, long long ldc, int bias_mode, float alpha, int axis, void* part, int* cnt,
-                         int* flag, hipStream_t stream);
+                         int* flag, int force_fallback, hipStream_t stream);
 int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* out, int N, int C, int H, int W,
                       int OC, int KH, int KW, int stride, int pad, int dil, int ldw, int act, int nchw_out,
                       int out_f32, hipStream_t stream);
@@ -69,6 +62,14 @@ namespace {
 
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
+// Per-call launch options of the block GEMM (gemm.hip GemmOpts): a forced config or a tail trigger belongs to
+// the one call that passes it.
+struct GemmOpts {
+  int cfg;
+  unsigned* signal;
+  unsigned signal_value;
+};
+
 void check_rc(int rc, const char* what) {
   TORCH_CHECK(rc == 0, what, " failed with code ", rc, " (", hipGetErrorString((hipError_t)(rc > 0 ? rc : 0)), ")");
 }
@@ -84,9 +85,12 @@ bool is_f32(const torch::Tensor& t, const char* name) {
 }
 
 // C = epi(alpha * A @ B^T); A [b?,M,K] bf16, B [b?,N,K] bf16 (row stride may exceed K), bias f32.
+// cfg: -1 auto, 0 (128x128 tile kernel), 2 (256x256 8-phase). signal: int32 device flag of a tail trigger that
+// this launch raises to signal_value (execution/streams.py TailTrigger; the caller checked gemm_tail_eligible).
 torch::Tensor gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Tensor> bias, int64_t bias_mode,
                       int64_t act, bool out_f32, double alpha, double dropout, int64_t seed, int64_t splits,
-                      c10::optional<torch::Tensor> out, bool accumulate) {
+                      c10::optional<torch::Tensor> out, bool accumulate, int64_t cfg,
+                      c10::optional<torch::Tensor> signal, int64_t signal_value) {
   check_cuda(A, "A");
   check_cuda(B, "B");
   TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && B.scalar_type() == torch::kBFloat16, "A,B must be bf16");
@@ -129,18 +133,26 @@ torch::Tensor gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Ten
     C = batched ? torch::empty({batch, M, N}, opts) : torch::empty({M, N}, opts);
   }
   TORCH_CHECK(!accumulate || out_f32, "accumulate=True needs out_f32");
-  int s = splits > 0 ? (int)splits : nsdb_gemm_splits((int)M, (int)N, (int)K, (int)batch);
+  TORCH_CHECK(cfg == -1 || cfg == 0 || cfg == 2, "gemm_nt: cfg must be -1 (auto), 0 or 2 (study configs: _hip_study)");
+  int s = splits > 0 ? (int)splits : nsdb_gemm_splits((int)M, (int)N, (int)K, (int)batch, (int)cfg);
   torch::Tensor ws;
   float* wsp = nullptr;
   if (s > 1) {
     ws = torch::empty({batch * s * M * N}, A.options().dtype(torch::kFloat32));
     wsp = ws.data_ptr<float>();
   }
+  GemmOpts o{(int)cfg, nullptr, 0u};
+  if (signal.has_value() && signal->defined()) {
+    check_cuda(*signal, "signal");
+    TORCH_CHECK(signal->scalar_type() == torch::kInt32 && signal->numel() >= 1, "signal must be an int32 flag");
+    o.signal = reinterpret_cast<unsigned*>(signal->data_ptr());
+    o.signal_value = (unsigned)signal_value;
+  }
   const int rc = nsdb_gemm_nt_bf16(
       A.data_ptr(), B.data_ptr(), C.data_ptr(), wsp, bptr, (int)M, (int)N, (int)K, A.stride(-2), B.stride(-2),
       C.stride(-2), batched ? A.stride(0) : 0, batched ? B.stride(0) : 0, batched ? C.stride(0) : 0, sBias,
       (int)batch, s, (int)act, (int)bias_mode, out_f32 ? 1 : 0, (float)alpha, (float)dropout,
-      (unsigned long long)seed, accumulate ? 1 : 0, 0, 0, cur_stream());
+      (unsigned long long)seed, accumulate ? 1 : 0, 0, 0, &o, cur_stream());
   check_rc(rc, "gemm_nt");
   return C;
 }
@@ -165,7 +177,7 @@ torch::Tensor softmax_state(const torch::Tensor& like, int64_t need, hipStream_t
 // C (f32 [M, N]) = softmax(alpha * A . B^T + bias) along axis 1 (every row of C) or 2 (every column), fused
 // into the GEMM epilogue (max-subtracted; cross-workgroup partials, see gemm.hip softmax_epilogue_8ph).
 torch::Tensor gemm_nt_softmax(torch::Tensor A, torch::Tensor B, c10::optional<torch::Tensor> bias, int64_t bias_mode,
-                              int64_t axis, c10::optional<torch::Tensor> out, double alpha) {
+                              int64_t axis, c10::optional<torch::Tensor> out, double alpha, bool force_fallback) {
   check_cuda(A, "A");
   check_cuda(B, "B");
   TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && B.scalar_type() == torch::kBFloat16, "A,B must be bf16");
@@ -199,7 +211,7 @@ torch::Tensor gemm_nt_softmax(torch::Tensor A, torch::Tensor B, c10::optional<to
   int* cnt = state.data_ptr<int>();
   const int rc = nsdb_gemm_nt_softmax(A.data_ptr(), B.data_ptr(), C.data_ptr<float>(), bptr, (int)M, (int)N, (int)K,
                                       A.stride(0), B.stride(0), C.stride(0), (int)bias_mode, (float)alpha, (int)axis,
-                                      part.data_ptr(), cnt, cnt + std::max(tm, tn), st);
+                                      part.data_ptr(), cnt, cnt + std::max(tm, tn), force_fallback ? 1 : 0, st);
   check_rc(rc, "gemm_nt_softmax");
   return C;
 }
@@ -233,7 +245,7 @@ torch::Tensor gemm_nt_bseg(torch::Tensor A, torch::Tensor Bg, c10::optional<torc
     C = torch::empty({M, N}, opts);
   }
   // splits: S segments x d splits per segment (d | seg_k/64), close to the launcher's own choice
-  const int auto_s = std::max<int>(1, nsdb_gemm_splits((int)M, (int)N, (int)K, 1));
+  const int auto_s = std::max<int>(1, nsdb_gemm_splits((int)M, (int)N, (int)K, 1, -1));
   const int steps = (int)(segk / 64);
   int d = 1;
   for (int c = 1; c <= steps; ++c)
@@ -248,40 +260,13 @@ torch::Tensor gemm_nt_bseg(torch::Tensor A, torch::Tensor Bg, c10::optional<torc
   const int rc = nsdb_gemm_nt_bf16(A.data_ptr(), Bg.data_ptr(), C.data_ptr(), wsp, bptr, (int)M, (int)N, (int)K,
                                    A.stride(0), segk, C.stride(0), 0, 0, 0, 0, 1, s, (int)act,
                                    bptr ? (int)bias_mode : 0, out_f32 ? 1 : 0, (float)alpha, (float)dropout,
-                                   (unsigned long long)seed, 0, segk, N * segk, cur_stream());
+                                   (unsigned long long)seed, 0, segk, N * segk, nullptr, cur_stream());
   check_rc(rc, "gemm_nt_bseg");
   return C;
 }
 
-// Study path: A/B as K-tiled panels [K/64][ldt][64] bf16 (ldt >= rows, multiple of 256 not required);
-// runs the 8-phase kernel's K-tiled variant. C [M,N] f32|bf16.
-torch::Tensor gemm_nt_ktiled(torch::Tensor Ap, torch::Tensor Bp, int64_t M, int64_t N, int64_t K, bool out_f32) {
-  check_cuda(Ap, "A");
-  check_cuda(Bp, "B");
-  TORCH_CHECK(Ap.scalar_type() == torch::kBFloat16 && Bp.scalar_type() == torch::kBFloat16, "A,B must be bf16");
-  TORCH_CHECK(Ap.dim() == 3 && Bp.dim() == 3 && Ap.is_contiguous() && Bp.is_contiguous(), "A,B [K/64][ld][64]");
-  TORCH_CHECK(Ap.size(2) == 64 && Bp.size(2) == 64 && K % 64 == 0 && Ap.size(0) == K / 64 && Bp.size(0) == K / 64,
-              "K-tiled panels must hold K/64 slabs of 64");
-  TORCH_CHECK(Ap.size(1) >= M && Bp.size(1) >= N, "panel rows < M/N");
-  auto C = torch::empty({M, N}, Ap.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16));
-  nsdb_gemm_force_config(11);
-  const int s = nsdb_gemm_splits((int)M, (int)N, (int)K, 1);
-  torch::Tensor ws;
-  float* wsp = nullptr;
-  if (s > 1) {
-    ws = torch::empty({s * M * N}, Ap.options().dtype(torch::kFloat32));
-    wsp = ws.data_ptr<float>();
-  }
-  const int rc = nsdb_gemm_nt_bf16(Ap.data_ptr(), Bp.data_ptr(), C.data_ptr(), wsp, nullptr, (int)M, (int)N, (int)K,
-                                   Ap.size(1), Bp.size(1), N, 0, 0, 0, 0, 1, s, 0, 0, out_f32 ? 1 : 0, 1.f, 0.f, 0, 0,
-                                   0, 0, cur_stream());
-  nsdb_gemm_force_config(-1);
-  check_rc(rc, "gemm_nt_ktiled");
-  return C;
-}
-
-int64_t gemm_splits(int64_t M, int64_t N, int64_t K, int64_t batch) {
-  return nsdb_gemm_splits((int)M, (int)N, (int)K, (int)batch);
+int64_t gemm_splits(int64_t M, int64_t N, int64_t K, int64_t batch, int64_t cfg) {
+  return nsdb_gemm_splits((int)M, (int)N, (int)K, (int)batch, (int)cfg);
 }
 
 torch::Tensor conv2d(torch::Tensor X, torch::Tensor Wt, c10::optional<torch::Tensor> bias, int64_t KH, int64_t KW,
@@ -557,38 +542,21 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nt", &gemm_nt, "epi(alpha*A@B^T) on MFMA", py::arg("A"), py::arg("B"), py::arg("bias") = py::none(),
         py::arg("bias_mode") = 0, py::arg("act") = 0, py::arg("out_f32") = false, py::arg("alpha") = 1.0,
         py::arg("dropout") = 0.0, py::arg("seed") = 0, py::arg("splits") = 0, py::arg("out") = py::none(),
-        py::arg("accumulate") = false);
-  m.def("gemm_splits", &gemm_splits);
-  m.def("tail_trigger_arm", [](torch::Tensor flag, int64_t value) {
-          TORCH_CHECK(flag.is_cuda() && flag.scalar_type() == torch::kInt32 && flag.numel() >= 1, "flag: int32 device tensor");
-          nsdb_tail_trigger_arm(flag.data_ptr(), (unsigned)value);
-        }, "arm the tail trigger of the next long 8-phase GEMM launch");
-  m.def("tail_trigger_consumed", []() { return (bool)nsdb_tail_trigger_consumed(); },
-        "whether a launch took the armed trigger (clears it)");
-  m.def("tail_trigger_disarm", []() { nsdb_tail_trigger_disarm(); });
+        py::arg("accumulate") = false, py::arg("cfg") = -1, py::arg("signal") = py::none(),
+        py::arg("signal_value") = 0);
+  m.def("gemm_splits", &gemm_splits, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("batch") = 1,
+        py::arg("cfg") = -1);
+  m.def("gemm_tail_eligible", [](int64_t M, int64_t N, int64_t K, int64_t batch, int64_t splits, int64_t cfg) {
+          return (bool)nsdb_gemm_tail_eligible((int)M, (int)N, (int)K, (int)batch, (int)splits, (int)cfg);
+        }, "whether a launch of this shape raises a tail trigger passed to it (long, one-wave 8-phase GEMM)",
+        py::arg("M"), py::arg("N"), py::arg("K"), py::arg("batch") = 1, py::arg("splits") = 0, py::arg("cfg") = -1);
   m.def("stream_wait_value", [](torch::Tensor flag, int64_t value) {
           TORCH_CHECK(flag.is_cuda() && flag.scalar_type() == torch::kInt32 && flag.numel() >= 1, "flag: int32 device tensor");
           check_rc(nsdb_stream_wait_value(cur_stream(), flag.data_ptr(), (unsigned)value), "stream_wait_value");
         }, "current stream waits on the GPU until flag >= value (unsigned)");
-  m.def("gemm_set_steal", [](int64_t on) { nsdb_gemm_set_steal((int)on); },
-        "opt-in: long split-K GEMMs use K-tail stealing (summation order varies run to run)");
-  m.def("gemm_steal", [](int64_t tq, int64_t ch) { nsdb_gemm_steal((int)tq, (int)ch); },
-        "K-tail stealing geometry of cfg 24: tail chunks per split, k-tiles per chunk");
-  m.def("gemm_set_adapt", [](int64_t on) { nsdb_gemm_set_adapt((int)on); },
-        "adaptive split-K K-partition across XCDs on/off (A/B)");
-  m.def("gemm_adapt_state", [](int64_t M, int64_t N, int64_t K) {
-        std::vector<float> buf(128, 0.f);
-        const int n = nsdb_gemm_adapt_state((int)M, (int)N, (int)K, buf.data());
-        TORCH_CHECK(n >= 0, "gemm_adapt_state: device copy failed");
-        std::vector<float> share(buf.begin(), buf.begin() + n), rate(buf.begin() + 64, buf.begin() + 64 + n);
-        return std::make_pair(share, rate);
-      }, "learned (shares, rates) of the adaptive split-K state for an (M, N, K) GEMM (empty if none)");
-  m.def("gemm_set_stamps", [](int64_t ptr) { nsdb_gemm_set_stamps(reinterpret_cast<void*>(ptr)); },
-        "diagnostic: u64 [workgroups][64] buffer for the cfg-17 progress stamps (0 to unset)");
-  m.def("gemm_nt_softmax", &gemm_nt_softmax, "softmax(alpha A.B^T + bias) fused into the GEMM epilogue");
-  m.def("gemm_nt_ktiled", &gemm_nt_ktiled, "study: 8-phase GEMM over K-tiled [K/64][ld][64] operand panels");
-  m.def("gemm_force_config", [](int64_t cfg) { nsdb_gemm_force_config((int)cfg); },
-        "-1 auto, 0 = 128x128 tile, 1 = 256x256 tile (A/B testing)");
+  m.def("gemm_nt_softmax", &gemm_nt_softmax, "softmax(alpha A.B^T + bias) fused into the GEMM epilogue",
+        py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("bias_mode") = 0, py::arg("axis") = 1,
+        py::arg("out") = py::none(), py::arg("alpha") = 1.0, py::arg("force_fallback") = false);
   m.def("conv2d_force_generic", [](int64_t v) { nsdb_conv2d_force_generic = (int)v; },
         "1: route every conv2d to the generic gather kernel (A/B testing)");
   m.def("conv2d_max_blocks", [](int64_t v) { const int old = nsdb_conv2d_max_blocks; nsdb_conv2d_max_blocks = (int)v; return old; },

@@ -18,7 +18,7 @@
 // (cdna_hip_programming.md §5.7): every asynchronously written register (ds_read / buffer_load
 // destinations) is named "+v" by the wait statement that retires it, so no compiler copy can read it
 // early; the accumulators are "+a" operands of the MFMA statements only.
-#include "gemm_common.h"
+#include "../kernels/gemm_common.h"
 
 namespace nsdb {
 
@@ -165,7 +165,7 @@ extern "C" {
 
 // Launch the w4a kernel (variant v) for a split-K GEMM whose parameters the caller prepared (gemm.hip's
 // launcher): K and every split's K range are multiples of 64; lda/ldb rows fit the 32-bit buffer range.
-int nsdb_gemm_w4a_launch(const nsdb::GemmParams* p, int batch, int v, hipStream_t stream) {
+int nsdb_study_gemm_w4a_launch(const nsdb::GemmParams* p, int batch, int v, hipStream_t stream) {
   if (p->K % nsdb::BK != 0 || p->kchunk % nsdb::BK != 0) return -1;
   dim3 grid(p->tiles_m * p->tiles_n * p->splits, 1, batch);
   if (v == 1) hipLaunchKernelGGL(nsdb::gemm_nt_256_w4a_kernel<1>, grid, dim3(256), 0, stream, *p);

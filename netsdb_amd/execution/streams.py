@@ -29,9 +29,28 @@ the GEMM's whole tail.
 """
 from __future__ import annotations
 
-from typing import Callable, List, Optional
+import threading
+from typing import Callable, Dict, List, Optional, Tuple
 
 import torch
+
+# tail triggers armed per (device, stream): ops.gemm_nt hands the trigger to the first eligible GEMM enqueued on
+# THAT stream (no process-wide state in the kernel library; GEMMs on other streams never take it)
+_armed: Dict[Tuple[int, int], "TailTrigger"] = {}
+_armed_lock = threading.Lock()
+
+
+def _stream_key(device) -> Tuple[int, int]:
+    dev = torch.device(device)
+    return (dev.index or 0, torch.cuda.current_stream(dev).cuda_stream)
+
+
+def armed_trigger(device) -> Optional["TailTrigger"]:
+    """The tail trigger armed on the current stream of ``device``, if any (ops.gemm_nt's per-call lookup)."""
+    if not _armed or torch.device(device).type != "cuda":
+        return None
+    with _armed_lock:
+        return _armed.get(_stream_key(device))
 
 
 class JobHandle:
@@ -58,12 +77,14 @@ class JobHandle:
 
 
 class TailTrigger:
-    """Device flag raised by the workgroups of the next long 8-phase GEMM launch (see module doc).
+    """Device flag raised by the workgroups of the next long 8-phase GEMM launch enqueued on the stream that
+    armed it (see module doc).
 
-    ``arm()`` before enqueuing the job whose GEMM tail should be filled; ``JobStreams.submit(...,
-    start_on=trigger)`` then gates the submitted job on it. The gate is only installed when a launch actually
-    took the armed trigger (every workgroup of that launch writes the flag, so the wait always ends);
-    otherwise the job starts ungated."""
+    ``arm()`` (on the stream that will run the GEMM) before enqueuing the job whose GEMM tail should be filled;
+    ``JobStreams.submit(..., start_on=trigger)`` then gates the submitted job on it. The gate is only installed
+    when a launch actually took the armed trigger (every workgroup of that launch writes the flag, so the wait
+    always ends); otherwise the job starts ungated. Arming is per stream: a GEMM enqueued on another stream
+    (another job lane, another thread's stream) never takes it."""
 
     def __init__(self, device):
         self.device = torch.device(device)
@@ -74,6 +95,8 @@ class TailTrigger:
             torch.cuda.synchronize(self.device)
         self.epoch = 0
         self.armed = False
+        self.consumed = False
+        self._key = None
         self.gated = 0       # jobs that were actually gated (stats / tests)
 
     def arm(self) -> "TailTrigger":
@@ -85,9 +108,26 @@ class TailTrigger:
         if self.epoch == 1 and self.gated:           # wrapped: restart from a zero flag
             self.flag.zero_()
             torch.cuda.synchronize(self.device)
-        _ext.hip().tail_trigger_arm(self.flag, self.epoch)
+        _ext.hip()                                   # the GEMM that takes it runs on the HIP kernels
+        self.disarm()
+        self._key = _stream_key(self.device)
+        with _armed_lock:
+            _armed[self._key] = self
         self.armed = True
+        self.consumed = False
         return self
+
+    def take(self) -> Tuple[torch.Tensor, int]:
+        """Called by the GEMM launch that takes the trigger: (flag, value) for that launch only."""
+        self.consumed = True
+        self.disarm()
+        return self.flag, self.epoch
+
+    def disarm(self):
+        with _armed_lock:
+            if self._key is not None and _armed.get(self._key) is self:
+                del _armed[self._key]
+        self._key = None
 
     def gate(self, stream) -> bool:
         """Make ``stream`` wait on the GPU for the armed launch's first finished workgroup."""
@@ -97,9 +137,10 @@ class TailTrigger:
 
         h = _ext.hip()
         self.armed = False
-        if not h.tail_trigger_consumed():
-            h.tail_trigger_disarm()
+        if not self.consumed:
+            self.disarm()
             return False
+        self.consumed = False
         with torch.cuda.stream(stream):
             h.stream_wait_value(self.flag, self.epoch)
         self.gated += 1

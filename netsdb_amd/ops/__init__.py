@@ -61,31 +61,51 @@ def _use_hip(*ts) -> bool:
     return on_gpu
 
 
+def gemm_operands(A, B):
+    """bf16, K-contiguous operands with 16-B rows and equal (multiple-of-8) K, as the MFMA kernels read them."""
+    # compute dtype is bf16 on the matrix cores (f32 operands are rounded once here)
+    if A.dtype != torch.bfloat16:
+        A = A.to(torch.bfloat16)
+    if B.dtype != torch.bfloat16:
+        B = B.to(torch.bfloat16)
+    if A.stride(-1) != 1 or A.stride(-2) % 8:
+        A = pad_k(A.contiguous())
+    if B.stride(-1) != 1 or B.stride(-2) % 8:
+        B = pad_k(B.contiguous())
+    if A.shape[-1] != B.shape[-1] or A.shape[-1] % 8:
+        k = max(A.shape[-1], B.shape[-1])
+        k = (k + 7) // 8 * 8
+        A = torch.nn.functional.pad(A, (0, k - A.shape[-1])) if A.shape[-1] < k else A
+        B = torch.nn.functional.pad(B, (0, k - B.shape[-1])) if B.shape[-1] < k else B
+    return A, B
+
+
 def gemm_nt(A, B, bias=None, bias_mode=BIAS_NONE, act=ACT_NONE, out_dtype=torch.bfloat16, alpha=1.0,
-            dropout=0.0, seed=0, splits=0, out=None, accumulate=False):
+            dropout=0.0, seed=0, splits=0, out=None, accumulate=False, cfg=None):
     """epilogue(alpha * A @ B^T) [+ out when accumulate]: A [..,M,K], B [..,N,K] (K-contiguous),
-    bias f32 per row/col. ``accumulate`` adds into an existing f32 ``out`` (C += A.B^T)."""
+    bias f32 per row/col. ``accumulate`` adds into an existing f32 ``out`` (C += A.B^T). ``cfg`` forces the
+    tile config of THIS call (0 = 128x128, 2 = 256x256 8-phase; None = auto). A tail trigger armed on the
+    current stream (execution/streams.TailTrigger) is handed to this launch when the launch is long enough to
+    take it — per call and per stream, so GEMMs on other lanes or threads never see it."""
     act = act_code(act)
     if _use_hip(A, B):
         if bias is not None and bias.dtype != torch.float32:
             bias = bias.float()
-        # compute dtype is bf16 on the matrix cores (f32 operands are rounded once here)
-        if A.dtype != torch.bfloat16:
-            A = A.to(torch.bfloat16)
-        if B.dtype != torch.bfloat16:
-            B = B.to(torch.bfloat16)
-        if A.stride(-1) != 1 or A.stride(-2) % 8:
-            A = pad_k(A.contiguous())
-        if B.stride(-1) != 1 or B.stride(-2) % 8:
-            B = pad_k(B.contiguous())
-        if A.shape[-1] != B.shape[-1] or A.shape[-1] % 8:
-            k = max(A.shape[-1], B.shape[-1])
-            k = (k + 7) // 8 * 8
-            A = torch.nn.functional.pad(A, (0, k - A.shape[-1])) if A.shape[-1] < k else A
-            B = torch.nn.functional.pad(B, (0, k - B.shape[-1])) if B.shape[-1] < k else B
-        return _ext.hip().gemm_nt(A, B, bias, int(bias_mode if bias is not None else 0), act,
-                                  out_dtype == torch.float32, float(alpha), float(dropout), int(seed),
-                                  int(splits), out, bool(accumulate))
+        A, B = gemm_operands(A, B)
+        h = _ext.hip()
+        c = -1 if cfg is None else int(cfg)
+        sig, sval = None, 0
+        from ..execution.streams import armed_trigger
+
+        trig = armed_trigger(A.device)
+        if trig is not None:
+            M, N, K = A.shape[-2], B.shape[-2], A.shape[-1]
+            batch = A.shape[0] if A.dim() == 3 else 1
+            if h.gemm_tail_eligible(M, N, K, batch, int(splits), c):
+                sig, sval = trig.take()
+        return h.gemm_nt(A, B, bias, int(bias_mode if bias is not None else 0), act,
+                         out_dtype == torch.float32, float(alpha), float(dropout), int(seed),
+                         int(splits), out, bool(accumulate), c, sig, int(sval))
     v = torch.matmul(A.float(), B.float().transpose(-1, -2)) * alpha
     if bias is not None:
         b = bias.float()
@@ -102,7 +122,7 @@ def gemm_nt(A, B, bias=None, bias_mode=BIAS_NONE, act=ACT_NONE, out_dtype=torch.
     return v
 
 
-def gemm_nt_softmax(A, B, bias=None, bias_mode=BIAS_NONE, axis=1, alpha=1.0, out=None):
+def gemm_nt_softmax(A, B, bias=None, bias_mode=BIAS_NONE, axis=1, alpha=1.0, out=None, force_fallback=False):
     """softmax(alpha * A @ B^T + bias) along ``axis`` 1 (each row of the [M, N] result) or 2 (each column), f32.
     On the GPU the normalisation is fused into the GEMM epilogue (max-subtracted, no exp'd round trip through
     HBM); the CPU oracle is the same max-subtracted softmax in fp32."""
@@ -120,7 +140,7 @@ def gemm_nt_softmax(A, B, bias=None, bias_mode=BIAS_NONE, axis=1, alpha=1.0, out
             A = torch.nn.functional.pad(A, (0, k - A.shape[-1])) if A.shape[-1] < k else A
             B = torch.nn.functional.pad(B, (0, k - B.shape[-1])) if B.shape[-1] < k else B
         return _ext.hip().gemm_nt_softmax(A, B, bias, int(bias_mode if bias is not None else 0), int(axis), out,
-                                          float(alpha))
+                                          float(alpha), bool(force_fallback))
     v = torch.matmul(A.float(), B.float().transpose(-1, -2)) * alpha
     if bias is not None:
         b = bias.float()

@@ -14,14 +14,14 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from netsdb_amd import _ext, ops  # noqa: E402
+from netsdb_amd import study, _ext, ops  # noqa: E402
 
 
 def timed(A, B, n):
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(n + 1)]
     evs[0].record()
     for i in range(n):
-        ops.gemm_nt(A, B)
+        study.gemm_nt(A, B)
         evs[i + 1].record()
     torch.cuda.synchronize()
     return [evs[i].elapsed_time(evs[i + 1]) for i in range(n)]
@@ -35,7 +35,7 @@ def main():
     ap.add_argument("--scale-b", type=float, default=1.0)
     ap.add_argument("--trace", type=int, default=12, help="launches timed one by one from a fresh state")
     a = ap.parse_args()
-    h = _ext.hip()
+    h = study.ext()
     h.gemm_force_config(-1)
     for sh in a.shapes.split(","):
         M, N, K = (int(x) for x in sh.split("x"))
@@ -52,7 +52,7 @@ def main():
         res["rates"] = [round(x, 4) for x in rt_]
         for on in (0, 1):
             h.gemm_set_adapt(on)
-            out = ops.gemm_nt(A, B, out_dtype=torch.float32)
+            out = study.gemm_nt(A, B, out_dtype=torch.float32)
             torch.cuda.synchronize()
             res[f"adapt{on}_rel_err"] = ((out[rows] - ref).abs().max() / ref.abs().max()).item()
             del out

@@ -12,7 +12,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from netsdb_amd import _ext, ops  # noqa: E402
+from netsdb_amd import study, _ext, ops  # noqa: E402
 
 
 def main():
@@ -21,7 +21,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     a = ap.parse_args()
-    h = _ext.hip()
+    h = study.ext()
     h.gemm_set_adapt(0)
     M, N, K = 1000, 1000, 597568
     g = torch.Generator(device="cuda:0").manual_seed(0)
@@ -33,11 +33,11 @@ def main():
         for c in cfgs:
             h.gemm_force_config(c)
             for _ in range(3):
-                ops.gemm_nt(W, X)
+                study.gemm_nt(W, X)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(a.iters):
-                ops.gemm_nt(W, X)
+                study.gemm_nt(W, X)
             e1.record()
             torch.cuda.synchronize()
             ts[c].append(e0.elapsed_time(e1) / a.iters)

@@ -5,7 +5,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from netsdb_amd import _ext, ops  # noqa: E402
+from netsdb_amd import study, _ext, ops  # noqa: E402
 from scripts.ab_dedup_gemm import t  # noqa: E402
 
 
@@ -17,13 +17,13 @@ def main():
     Wm = (torch.randn(500, 1_000_000, device=dev, generator=g) * 0.05).to(torch.bfloat16)
     Xp = X[:, 900_000:]
     for cfg in (0, 1, 2):
-        _ext.hip().gemm_force_config(cfg)
+        study.ext().gemm_force_config(cfg)
         for sp in (0, 8, 16, 32, 64, 128, 256):
-            a = t(lambda: ops.gemm_nt(Wp, Xp, out_dtype=torch.float32, splits=sp))
-            b = t(lambda: ops.gemm_nt(Wm, X, out_dtype=torch.float32, splits=sp))
+            a = t(lambda: study.gemm_nt(Wp, Xp, out_dtype=torch.float32, splits=sp))
+            b = t(lambda: study.gemm_nt(Wm, X, out_dtype=torch.float32, splits=sp))
             print(f"cfg={cfg} splits={sp:3d}  6000x100x100k {a:7.1f} us ({1.2e9 / a / 1e6:5.2f} TB/s)   "
                   f"500x100x1M {b:7.1f} us ({1.0e9 / b / 1e6:5.2f} TB/s)", flush=True)
-    _ext.hip().gemm_force_config(-1)
+    study.ext().gemm_force_config(-1)
 
 
 if __name__ == "__main__":

@@ -12,7 +12,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from netsdb_amd import _ext, ops  # noqa: E402
+from netsdb_amd import study, _ext, ops  # noqa: E402
 
 
 def main():
@@ -21,7 +21,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     a = ap.parse_args()
-    h = _ext.hip()
+    h = study.ext()
     h.gemm_set_adapt(0)
     M, N, K = (int(x) for x in a.shape.split("x"))
     g = torch.Generator(device="cuda:0").manual_seed(0)
@@ -30,7 +30,7 @@ def main():
     bias = torch.randn(M, device="cuda:0", generator=g) * 0.1
 
     def run():
-        return ops.gemm_nt(A, B, bias, ops.BIAS_ROW, ops.ACT_RELU, dropout=0.5, seed=7)
+        return study.gemm_nt(A, B, bias, ops.BIAS_ROW, ops.ACT_RELU, dropout=0.5, seed=7)
 
     outs = {}
     for cfg in (2, 26, 26):

@@ -10,7 +10,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from netsdb_amd import _ext, ops  # noqa: E402
+from netsdb_amd import study, _ext, ops  # noqa: E402
 
 
 def main():
@@ -28,17 +28,17 @@ def main():
         best = {c: 1e9 for c in cfgs}
         for _ in range(a.rounds):
             for c in cfgs:
-                _ext.hip().gemm_force_config(c)
+                study.ext().gemm_force_config(c)
                 for _ in range(3):
-                    ops.gemm_nt(A, B)
+                    study.gemm_nt(A, B)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(a.iters):
-                    ops.gemm_nt(A, B)
+                    study.gemm_nt(A, B)
                 e1.record()
                 torch.cuda.synchronize()
                 best[c] = min(best[c], e0.elapsed_time(e1) / a.iters)
-        _ext.hip().gemm_force_config(-1)
+        study.ext().gemm_force_config(-1)
         fl = 2.0 * M * N * K
         print(json.dumps({"shape": sh, **{f"cfg{c}_tflops": round(fl / best[c] / 1e9, 1) for c in cfgs}}), flush=True)
         del A, B

@@ -13,7 +13,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from netsdb_amd import _ext, ops  # noqa: E402
+from netsdb_amd import study, _ext, ops  # noqa: E402
 
 
 def timeit(fn, iters, rounds):
@@ -60,22 +60,22 @@ def main():
                 ms = timeit(lambda: torch.matmul(A, B.t()), a.iters, a.rounds)
                 res["hipblaslt_bf16_us"] = round(ms * 1e3, 1)
                 continue
-            _ext.hip().gemm_force_config(c)
+            study.ext().gemm_force_config(c)
             for epi in a.epis.split(","):
                 if epi == "plain_bf16":
-                    fn = lambda: ops.gemm_nt(A, B, out=Cb, splits=a.splits)  # noqa: E731
+                    fn = lambda: study.gemm_nt(A, B, out=Cb, splits=a.splits)  # noqa: E731
                 else:
-                    fn = lambda: ops.gemm_nt(A, B, bias, ops.BIAS_COL, ops.ACT_EXP, out_dtype=torch.float32, out=Cf,
+                    fn = lambda: study.gemm_nt(A, B, bias, ops.BIAS_COL, ops.ACT_EXP, out_dtype=torch.float32, out=Cf,
                                                splits=a.splits)  # noqa: E731
                 ms = timeit(fn, a.iters, a.rounds)
                 res[f"cfg{c}_{epi}_us"] = round(ms * 1e3, 1)
                 res[f"cfg{c}_{epi}_tflops"] = round(2.0 * M * N * K / ms / 1e9, 1)
-            out = ops.gemm_nt(A, B, bias, ops.BIAS_COL, ops.ACT_EXP, out_dtype=torch.float32)
+            out = study.gemm_nt(A, B, bias, ops.BIAS_COL, ops.ACT_EXP, out_dtype=torch.float32)
             if ref is None and M * N * K < 2e11:
                 ref = torch.exp(A.float() @ B.float().t())
             if ref is not None:
                 res[f"cfg{c}_maxrel"] = float(((out - ref).abs() / ref.abs().clamp_min(1e-3)).max())
-        _ext.hip().gemm_force_config(-1)
+        study.ext().gemm_force_config(-1)
         print(json.dumps(res), flush=True)
         del A, B
 

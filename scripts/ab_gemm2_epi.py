@@ -13,7 +13,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from netsdb_amd import _ext, ops  # noqa: E402
+from netsdb_amd import study, _ext, ops  # noqa: E402
 
 
 def main():
@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--N", type=int, default=14588)
     ap.add_argument("--K", type=int, default=1000)
     a = ap.parse_args()
-    h = _ext.hip()
+    h = study.ext()
     M, N, K = a.M, a.N, a.K
     dev = "cuda:0"
     X = (torch.rand(M, K, device=dev) * 0.1).to(torch.bfloat16)
@@ -33,13 +33,13 @@ def main():
     bias = torch.randn(N, device=dev) * 0.1
     outp = torch.empty(M, (N + 63) // 64 * 64, device=dev)[:, :N]
     variants = {
-        "bf16_noepi": lambda: ops.gemm_nt(X, W),
-        "f32_noepi": lambda: ops.gemm_nt(X, W, out_dtype=torch.float32, out=outp),
-        "f32_bias_exp": lambda: ops.gemm_nt(X, W, bias, ops.BIAS_COL, ops.ACT_EXP, out_dtype=torch.float32, out=outp),
+        "bf16_noepi": lambda: study.gemm_nt(X, W),
+        "f32_noepi": lambda: study.gemm_nt(X, W, out_dtype=torch.float32, out=outp),
+        "f32_bias_exp": lambda: study.gemm_nt(X, W, bias, ops.BIAS_COL, ops.ACT_EXP, out_dtype=torch.float32, out=outp),
         "f32_bias_exp_nostore": "diag",
         "rownorm": lambda: ops.row_normalize(outp, out_dtype=torch.float32),
         "exp_then_rownorm": lambda: ops.row_normalize(
-            ops.gemm_nt(X, W, bias, ops.BIAS_COL, ops.ACT_EXP, out_dtype=torch.float32, out=outp), out_dtype=torch.float32),
+            study.gemm_nt(X, W, bias, ops.BIAS_COL, ops.ACT_EXP, out_dtype=torch.float32, out=outp), out_dtype=torch.float32),
         "fused_softmax": lambda: ops.gemm_nt_softmax(X, W, bias, ops.BIAS_COL, axis=1, out=outp),
     }
     res = {k: [] for k in variants}

@@ -11,7 +11,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from netsdb_amd import _ext, ops  # noqa: E402
+from netsdb_amd import study, _ext, ops  # noqa: E402
 
 
 def ktile(t: torch.Tensor, ld: int) -> torch.Tensor:
@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--scale-b", type=float, default=1.0, help="scale of B (FF W1 init: sqrt(3/features))")
     a = ap.parse_args()
-    h = _ext.hip()
+    h = study.ext()
     for sh in a.shapes.split(","):
         M, N, K = (int(x) for x in sh.split("x"))
         A = torch.empty(M, K, device="cuda:0", dtype=torch.bfloat16).uniform_(-1, 1)
@@ -36,11 +36,11 @@ def main():
         ldA, ldB = (M + 255) // 256 * 256, (N + 255) // 256 * 256
         Ap, Bp = ktile(A, ldA), ktile(B, ldB)
         h.gemm_force_config(2)
-        ref = ops.gemm_nt(A, B, out_dtype=torch.float32)
+        ref = study.gemm_nt(A, B, out_dtype=torch.float32)
         h.gemm_force_config(-1)
         got = h.gemm_nt_ktiled(Ap, Bp, M, N, K, True)
         err = ((got - ref).abs().max() / ref.abs().max().clamp(min=1e-6)).item()
-        fns = {"rowmajor_8ph": lambda: ops.gemm_nt(A, B), "ktiled_8ph": lambda: h.gemm_nt_ktiled(Ap, Bp, M, N, K, False)}
+        fns = {"rowmajor_8ph": lambda: study.gemm_nt(A, B), "ktiled_8ph": lambda: h.gemm_nt_ktiled(Ap, Bp, M, N, K, False)}
         best = {k: 1e9 for k in fns}
         for _ in range(a.rounds):
             for k, fn in fns.items():

@@ -11,7 +11,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from netsdb_amd import _ext, ops  # noqa: E402
+from netsdb_amd import study, _ext, ops  # noqa: E402
 
 
 def main():
@@ -21,7 +21,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     a = ap.parse_args()
-    h = _ext.hip()
+    h = study.ext()
     M, N, K = (int(x) for x in a.shape.split("x"))
     g = torch.Generator(device="cuda:0").manual_seed(0)
     A = torch.empty(M, K, device="cuda:0").uniform_(-1, 1, generator=g).to(torch.bfloat16)
@@ -35,11 +35,11 @@ def main():
             if geom:
                 h.gemm_steal(*geom)
             for _ in range(3):
-                ops.gemm_nt(A, B)
+                study.gemm_nt(A, B)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(a.iters):
-                ops.gemm_nt(A, B)
+                study.gemm_nt(A, B)
             e1.record()
             torch.cuda.synchronize()
             ts[n].append(e0.elapsed_time(e1) / a.iters)

@@ -12,7 +12,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from netsdb_amd import _ext, ops  # noqa: E402
+from netsdb_amd import study, _ext, ops  # noqa: E402
 
 
 def main():
@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--check-only", action="store_true")
     ap.add_argument("--scale-b", type=float, default=1.0, help="B ~ U(-1,1) * scale (FF W1 init: sqrt(3/features))")
     a = ap.parse_args()
-    h = _ext.hip()
+    h = study.ext()
     cfgs = [int(c) for c in a.cfgs.split(",")]
     for sh in a.shapes.split(","):
         M, N, K = (int(x) for x in sh.split("x"))
@@ -37,7 +37,7 @@ def main():
         res = {"shape": sh, "splits": ops.gemm_splits(M, N, K)}
         for c in cfgs:
             h.gemm_force_config(c)
-            out = ops.gemm_nt(A, B, out_dtype=torch.float32)
+            out = study.gemm_nt(A, B, out_dtype=torch.float32)
             torch.cuda.synchronize()
             err = ((out[rows] - ref).abs().max() / ref.abs().max()).item()
             res[f"cfg{c}_rel_err"] = err
@@ -51,11 +51,11 @@ def main():
             for c in cfgs:
                 h.gemm_force_config(c)
                 for _ in range(3):
-                    ops.gemm_nt(A, B)
+                    study.gemm_nt(A, B)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(a.iters):
-                    ops.gemm_nt(A, B)
+                    study.gemm_nt(A, B)
                 e1.record()
                 torch.cuda.synchronize()
                 best[c].append(e0.elapsed_time(e1) / a.iters)

@@ -13,7 +13,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from netsdb_amd import _ext, ops  # noqa: E402
+from netsdb_amd import study, _ext, ops  # noqa: E402
 
 
 def check(h, cfgs):
@@ -26,7 +26,7 @@ def check(h, cfgs):
         ref = A.float() @ B.float().t()
         for c in cfgs:
             h.gemm_force_config(c)
-            C = ops.gemm_nt(A, B, out_dtype=torch.float32)
+            C = study.gemm_nt(A, B, out_dtype=torch.float32)
             torch.cuda.synchronize()
             err = ((C - ref).abs().max() / ref.abs().max()).item()
             out[f"{M}x{N}x{K}/cfg{c}"] = round(err, 7)
@@ -41,11 +41,11 @@ def timed(h, cfgs, A, B, rounds, iters):
         for c in cfgs:
             h.gemm_force_config(c)
             for _ in range(3):
-                ops.gemm_nt(A, B)
+                study.gemm_nt(A, B)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(iters):
-                ops.gemm_nt(A, B)
+                study.gemm_nt(A, B)
             e1.record()
             torch.cuda.synchronize()
             ts[c].append(e0.elapsed_time(e1) / iters)
@@ -61,7 +61,7 @@ def main():
     ap.add_argument("--check-only", action="store_true")
     ap.add_argument("--shapes", default="ff,8192,4096")
     a = ap.parse_args()
-    h = _ext.hip()
+    h = study.ext()
     cfgs = [int(c) for c in a.cfgs.split(",")]
     print(json.dumps({"check": check(h, cfgs)}), flush=True)
     if a.check_only:

@@ -12,7 +12,7 @@ import time
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from netsdb_amd import ops  # noqa: E402
+from netsdb_amd import study, ops  # noqa: E402
 
 
 def timeit(fn, iters=20, warmup=5):
@@ -52,10 +52,10 @@ def main():
 
         cfg_ms = {}
         for cfg in (0, 1, 2):
-            _ext.hip().gemm_force_config(cfg)
-            cfg_ms[cfg] = timeit(lambda: ops.gemm_nt(A, B))
-        _ext.hip().gemm_force_config(-1)
-        t_ours = timeit(lambda: ops.gemm_nt(A, B))
+            study.ext().gemm_force_config(cfg)
+            cfg_ms[cfg] = timeit(lambda: study.gemm_nt(A, B))
+        study.ext().gemm_force_config(-1)
+        t_ours = timeit(lambda: study.gemm_nt(A, B))
         t_lib = timeit(lambda: torch.matmul(A, B.t()))
         fl = 2.0 * M * N * Kp
         r = dict(op="gemm_nt", shape=name, M=M, N=N, K=Kp, ms=t_ours, tflops=fl / t_ours / 1e9,
@@ -77,7 +77,7 @@ def main():
     _e.hip().conv2d_force_generic(0)
     w4 = Wf[:, :147].reshape(64, 3, 7, 7).contiguous()
     t_lib = timeit(lambda: torch.nn.functional.conv2d(X, w4, bias.to(torch.bfloat16)))
-    t_mat = timeit(lambda: ops.gemm_nt(ops.im2col(X, 7, 7, 1, 0), Wf, bias, ops.BIAS_COL))
+    t_mat = timeit(lambda: study.gemm_nt(ops.im2col(X, 7, 7, 1, 0), Wf, bias, ops.BIAS_COL))
     fl = 2.0 * 100 * 106 * 106 * 64 * 147
     r = dict(op="conv2d_7x7x3_64_100img", ms=t_ours, tflops=fl / t_ours / 1e9, generic_gather_ms=t_generic,
              lib_ms=t_lib,

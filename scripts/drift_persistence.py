@@ -13,7 +13,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from netsdb_amd import _ext, ops  # noqa: E402
+from netsdb_amd import study, _ext, ops  # noqa: E402
 
 
 def main():
@@ -22,18 +22,18 @@ def main():
     ap.add_argument("--scale-b", type=float, default=0.0022)
     a = ap.parse_args()
     M, N, K = 1000, 1000, 597568
-    h = _ext.hip()
+    h = study.ext()
     A = torch.empty(M, K, device="cuda:0", dtype=torch.bfloat16).uniform_(-1, 1)
     B = (torch.empty(N, K, device="cuda:0").uniform_(-1, 1) * a.scale_b).to(torch.bfloat16)
     st = torch.zeros(256 * 64, dtype=torch.int64, device="cuda:0")
     h.gemm_set_stamps(st.data_ptr())
     h.gemm_force_config(17)
     for _ in range(3):
-        ops.gemm_nt(A, B)
+        study.gemm_nt(A, B)
     lags = []
     for _ in range(a.launches):
         st.zero_()
-        ops.gemm_nt(A, B)
+        study.gemm_nt(A, B)
         torch.cuda.synchronize()
         s = st.view(256, 64).cpu().double()
         last = s[:, 18]

@@ -20,7 +20,16 @@ KDIR = os.path.join("netsdb_amd", "csrc", "kernels")
 RDIR = os.path.join("netsdb_amd", "csrc", "runtime")
 
 
-HIP_SOURCES = ("gemm.hip", "gemm_w4a.hip", "conv2d.hip", "rowops.hip", "strings.hip", "dedup.hip")
+HIP_SOURCES = ("gemm.hip", "conv2d.hip", "rowops.hip", "strings.hip", "dedup.hip")
+SDIR = os.path.join("netsdb_amd", "csrc", "study")
+STUDY_SOURCES = ("gemm_study.hip", "gemm_w4a.hip")
+
+
+def study_ext():
+    from setuptools import Extension
+
+    srcs = [os.path.join(SDIR, f) for f in ("study_bindings.cpp",) + STUDY_SOURCES]
+    return Extension(name="netsdb_amd._hip_study", sources=srcs)
 
 
 def hip_ext():
@@ -32,7 +41,7 @@ def hip_ext():
     return Extension(name="netsdb_amd._hip_kernels", sources=srcs)
 
 
-def _torch_flags():
+def _torch_flags(study: bool = False):
     import sysconfig
 
     import torch
@@ -40,30 +49,33 @@ def _torch_flags():
 
     inc = [f"-I{p}" for p in include_paths()] + [f"-I{sysconfig.get_paths()['include']}", f"-I{os.path.join(ROOT, KDIR)}"]
     defs = ["-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DTORCH_API_INCLUDE_EXTENSION_H",
-            "-DTORCH_EXTENSION_NAME=_hip_kernels", f"-D_GLIBCXX_USE_CXX11_ABI={int(torch._C._GLIBCXX_USE_CXX11_ABI)}"]
+            "-DTORCH_EXTENSION_NAME=" + ("_hip_study" if study else "_hip_kernels"), f"-D_GLIBCXX_USE_CXX11_ABI={int(torch._C._GLIBCXX_USE_CXX11_ABI)}"]
     libdirs = library_paths()
     libs = [f"-L{d}" for d in libdirs] + [f"-Wl,-rpath,{d}" for d in libdirs] + [
         "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip"]
     return inc, defs, libs
 
 
-def build_hip_extension(out_path: str, build_dir: str, jobs: int = 8):
-    """hipcc every kernel TU for gfx950 (parallel), the bindings TU as host C++, then link."""
+def build_hip_extension(out_path: str, build_dir: str, jobs: int = 8, study: bool = False):
+    """hipcc every kernel TU for gfx950 (parallel), the bindings TU as host C++, then link. ``study`` builds the
+    separate diagnostic extension (_hip_study: the GEMM study variants) instead of the product one."""
     import subprocess
     from concurrent.futures import ThreadPoolExecutor
 
     rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
     hipcc = os.path.join(rocm, "bin", "hipcc")
     arch = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
-    inc, defs, libs = _torch_flags()
+    inc, defs, libs = _torch_flags(study)
     os.makedirs(build_dir, exist_ok=True)
     common = ["-O3", "-std=c++17", "-fPIC"] + defs + inc
     cmds, objs = [], []
-    for f in ("bindings.cpp",) + HIP_SOURCES:
-        src = os.path.join(ROOT, KDIR, f)
+    srcdir = SDIR if study else KDIR
+    for f in (("study_bindings.cpp",) + STUDY_SOURCES) if study else (("bindings.cpp",) + HIP_SOURCES):
+        src = os.path.join(ROOT, srcdir, f)
         obj = os.path.join(build_dir, f + ".o")
         objs.append(obj)
-        hdrs = [os.path.join(ROOT, KDIR, h) for h in os.listdir(os.path.join(ROOT, KDIR)) if h.endswith((".h", ".inc"))]
+        hdrs = [os.path.join(ROOT, d, h) for d in (KDIR, srcdir) for h in os.listdir(os.path.join(ROOT, d))
+                if h.endswith((".h", ".inc"))]
         if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(x) for x in [src] + hdrs):
             continue
         if f.endswith(".hip"):
@@ -103,9 +115,11 @@ def _build_ext_cls():
 
     class HipBuildExt(build_ext):
         def build_extension(self, ext):
-            if ext.name == "netsdb_amd._hip_kernels":
-                build_hip_extension(self.get_ext_fullpath(ext.name), os.path.join(self.build_temp, "hip"),
-                                    int(os.environ.get("MAX_JOBS", "8")))
+            if ext.name in ("netsdb_amd._hip_kernels", "netsdb_amd._hip_study"):
+                study = ext.name.endswith("_study")
+                build_hip_extension(self.get_ext_fullpath(ext.name),
+                                    os.path.join(self.build_temp, "hip_study" if study else "hip"),
+                                    int(os.environ.get("MAX_JOBS", "8")), study=study)
             else:
                 super().build_extension(ext)
 
@@ -119,6 +133,8 @@ def main():
         exts.append(native_ext())
     if which in ("all", "hip"):
         exts.append(hip_ext())
+    if which in ("all", "study"):
+        exts.append(study_ext())
     setup(
         name="netsdb_amd",
         version="0.1.0",

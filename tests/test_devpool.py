@@ -93,6 +93,10 @@ def test_gpu_pages_in_hbm_arena_with_eviction(tmp_path):
     st.remove_set("db", "s")
     torch.cuda.synchronize()
     st.page_pool._reclaim(block=True)
+    assert st.page_pool.used() > 0            # `got` still views reloaded pages: their regions stay
+    del got, g
+    torch.cuda.synchronize()
+    st.page_pool._reclaim(block=True)
     assert st.page_pool.used() == 0
 
 

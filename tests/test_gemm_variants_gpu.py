@@ -3,11 +3,14 @@ stay bit-exact with the production 8-phase kernel (same k order, same fp32 accum
 per-wave kernels (LDS-DMA cfg 12, register-staged cfg 16), the 10-slot LDS ring (cfg 14), the untransposed
 LDS-staged epilogue (cfg 15) — plus the cfg-17 drift diagnostic (real-time stamps + XCD ids), the opt-in
 adaptive split-K K partition (gemm_set_adapt), the opt-in K-tail stealing variant (cfg 24, exact but not
-bit-reproducible: checked against fp32 and cfg 2 instead) and the in-launch split-K fix-up (cfg 26, bit-exact)."""
+bit-reproducible: checked against fp32 and cfg 2 instead) and the in-launch split-K fix-up (cfg 26, bit-exact).
+They live in the separate study extension (netsdb_amd.study / _hip_study); the reference side of every
+bit-exact check is the PRODUCT kernel (ops.gemm_nt, cfg 2), so the lean production 8-phase kernel is also
+checked bit-identical to the study copy it was cut from."""
 import pytest
 import torch
 
-from netsdb_amd import _ext, ops
+from netsdb_amd import ops, study
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -16,25 +19,22 @@ DEV = "cuda:0"
 @pytest.fixture(autouse=True)
 def _reset():
     # the bit-exact comparisons need cfg 2's static K partition (the adaptive one moves between launches)
-    _ext.hip().gemm_set_adapt(0)
+    study.ext().gemm_set_adapt(0)
     yield
-    _ext.hip().gemm_force_config(-1)
-    _ext.hip().gemm_set_adapt(0)
+    study.ext().gemm_force_config(-1)
+    study.ext().gemm_set_adapt(0)
 
 
 @pytest.mark.parametrize("shape", [(777, 555, 4104), (300, 2000, 100000), (512, 512, 640)])
-@pytest.mark.parametrize("cfg", [12, 14, 15, 16])
+@pytest.mark.parametrize("cfg", [2, 12, 14, 15, 16, 30])
 def test_study_kernels_bit_exact(shape, cfg):
     M, N, K = shape
     g = torch.Generator(device=DEV).manual_seed(5)
     A = torch.empty(M, K, device=DEV).uniform_(-1, 1, generator=g).to(torch.bfloat16)
     B = torch.empty(N, K, device=DEV).uniform_(-1, 1, generator=g).to(torch.bfloat16)
     bias = torch.randn(N, device=DEV, generator=g)
-    h = _ext.hip()
-    h.gemm_force_config(2)
-    ref = ops.gemm_nt(A, B, bias, ops.BIAS_COL, ops.ACT_RELU, out_dtype=torch.float32)
-    h.gemm_force_config(cfg)
-    out = ops.gemm_nt(A, B, bias, ops.BIAS_COL, ops.ACT_RELU, out_dtype=torch.float32)
+    ref = ops.gemm_nt(A, B, bias, ops.BIAS_COL, ops.ACT_RELU, out_dtype=torch.float32, cfg=2)   # product kernel
+    out = study.gemm_nt(A, B, bias, ops.BIAS_COL, ops.ACT_RELU, out_dtype=torch.float32, cfg=cfg)
     torch.testing.assert_close(out, ref, atol=0, rtol=0)
 
 
@@ -42,14 +42,12 @@ def test_drift_diagnostic_stamps():
     M, N, K = 1000, 1000, 64 * 16 * 40          # split-K 16, 40 k-tiles per split
     A = torch.empty(M, K, device=DEV, dtype=torch.bfloat16).uniform_(-1, 1)
     B = torch.empty(N, K, device=DEV, dtype=torch.bfloat16).uniform_(-1, 1)
-    h = _ext.hip()
+    h = study.ext()
     st = torch.zeros(256 * 64, dtype=torch.int64, device=DEV)
     h.gemm_set_stamps(st.data_ptr())
     try:
-        h.gemm_force_config(2)
-        ref = ops.gemm_nt(A, B, out_dtype=torch.float32)
-        h.gemm_force_config(17)
-        out = ops.gemm_nt(A, B, out_dtype=torch.float32)
+        ref = ops.gemm_nt(A, B, out_dtype=torch.float32, cfg=2)
+        out = study.gemm_nt(A, B, out_dtype=torch.float32, cfg=17)
         torch.cuda.synchronize()
     finally:
         h.gemm_set_stamps(0)
@@ -74,15 +72,14 @@ def test_adaptive_splitk_partition_exact(shape):
     A = torch.empty(M, K, device=DEV).uniform_(-1, 1, generator=g).to(torch.bfloat16)
     B = torch.empty(N, K, device=DEV).uniform_(-1, 1, generator=g).to(torch.bfloat16)
     assert ops.gemm_splits(M, N, K) > 1
-    h = _ext.hip()
-    h.gemm_force_config(2)
+    h = study.ext()
     rows = torch.arange(0, M, 97, device=DEV)
     ref = A[rows].float() @ B.float().t()
     h.gemm_set_adapt(0)
-    base = ops.gemm_nt(A, B, out_dtype=torch.float32)
+    base = study.gemm_nt(A, B, out_dtype=torch.float32, cfg=2)
     h.gemm_set_adapt(1)
     for _ in range(6):
-        out = ops.gemm_nt(A, B, out_dtype=torch.float32)
+        out = study.gemm_nt(A, B, out_dtype=torch.float32, cfg=2)
         assert ((out[rows] - ref).abs().max() / ref.abs().max()).item() < 1e-5
         assert ((out - base).abs().max() / base.abs().max()).item() < 1e-5
 
@@ -92,7 +89,7 @@ def test_ksteal_variant_vs_fp32(shape):
     """K-tail stealing (cfg 24): every split's last 4 x 16 k-tiles are claimed by whichever workgroup of the
     tile is free first (summation order differs from cfg 2, the sum does not); three launches in a row check
     that the reducer re-zeroes the claim counters."""
-    from netsdb_amd import _ext, ops
+    from netsdb_amd import ops, study
 
     M, N, K = shape
     g = torch.Generator(device="cuda:0").manual_seed(1)
@@ -100,13 +97,8 @@ def test_ksteal_variant_vs_fp32(shape):
     B = (torch.empty(N, K, device="cuda:0").uniform_(-1, 1, generator=g) * (3.0 / K) ** 0.5).to(torch.bfloat16)
     rows = torch.linspace(0, M - 1, 16, device="cuda:0").long()
     ref = A[rows].float() @ B.float().t()
-    h = _ext.hip()
-    try:
-        h.gemm_force_config(24)
-        outs = [ops.gemm_nt(A, B, out_dtype=torch.float32) for _ in range(3)]
-        torch.cuda.synchronize()
-    finally:
-        h.gemm_force_config(-1)
+    outs = [study.gemm_nt(A, B, out_dtype=torch.float32, cfg=24) for _ in range(3)]
+    torch.cuda.synchronize()
     base = ops.gemm_nt(A, B, out_dtype=torch.float32)
     for o in outs:
         err = ((o[rows] - ref).abs().max() / ref.abs().max()).item()
@@ -125,15 +117,8 @@ def test_fixup_variant_bit_exact(shape):
     B = (torch.empty(N, K, device=DEV).uniform_(-1, 1, generator=g) * (3.0 / K) ** 0.5).to(torch.bfloat16)
     bias = torch.randn(M, device=DEV, generator=g) * 0.1
     assert ops.gemm_splits(M, N, K) > 1
-    h = _ext.hip()
-
-    def run():
-        return ops.gemm_nt(A, B, bias, ops.BIAS_ROW, ops.ACT_RELU, dropout=0.5, seed=11)
-
-    h.gemm_force_config(2)
-    ref = run()
-    h.gemm_force_config(26)
-    outs = [run() for _ in range(3)]
+    ref = ops.gemm_nt(A, B, bias, ops.BIAS_ROW, ops.ACT_RELU, dropout=0.5, seed=11, cfg=2)
+    outs = [study.gemm_nt(A, B, bias, ops.BIAS_ROW, ops.ACT_RELU, dropout=0.5, seed=11, cfg=26) for _ in range(3)]
     torch.cuda.synchronize()
     for o in outs:
         assert torch.equal(o, ref)

@@ -124,3 +124,33 @@ def test_tail_trigger_unconsumed_does_not_gate_gpu():
     js = JobStreams(dev, lanes=1)
     y = js.submit(lambda: a.float().sum(), independent=True, start_on=trig).synchronize()
     assert trig.gated == 0 and torch.isfinite(y)
+
+
+@pytest.mark.gpu
+def test_tail_trigger_is_per_stream_gpu():
+    """A trigger armed on one job lane (its HIP stream) is invisible to a long GEMM enqueued on ANOTHER lane at
+    the same time: that GEMM neither takes it nor raises its flag; the armed lane's own GEMM then does. (The
+    kernel library holds no process-wide launch state: a forced config or a trigger belongs to one call.)"""
+    from netsdb_amd import ops
+    from netsdb_amd.execution.streams import TailTrigger
+
+    dev = "cuda:0"
+    A, B = _long_splitk_operands(dev)
+    ref = ops.gemm_nt(A, B, out_dtype=torch.float32)
+    js = JobStreams(dev, lanes=2)
+    s_armed, s_other = js.stream(0), js.stream(1)
+    trig = TailTrigger(dev)
+    with torch.cuda.stream(s_armed):
+        trig.arm()
+    other = js.submit(lambda: ops.gemm_nt(A, B, out_dtype=torch.float32), lane=1, independent=True)
+    C_other = other.synchronize()
+    assert not trig.consumed and int(trig.flag.item()) == 0
+    assert torch.equal(C_other, ref)
+    # a forced config on the other lane's calls does not change this lane's choice either
+    C_forced = js.submit(lambda: ops.gemm_nt(A, B, out_dtype=torch.float32, cfg=0), lane=1, independent=True)
+    with torch.cuda.stream(s_armed):
+        C_armed = ops.gemm_nt(A, B, out_dtype=torch.float32)
+    torch.cuda.synchronize()
+    assert trig.consumed and int(trig.flag.item()) == trig.epoch
+    assert torch.equal(C_armed, ref)
+    assert (C_forced.synchronize() - ref).abs().max().item() <= 1e-3 * ref.abs().max().item()

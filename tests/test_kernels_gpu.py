@@ -30,13 +30,10 @@ def test_gemm_identity_asymmetric():
     torch.testing.assert_close(C, B.float().t().contiguous(), rtol=0, atol=0)
 
 
-@pytest.fixture(params=[-1, 0, 1, 2], ids=["auto", "tile128", "tile256", "tile256_8ph"])
+@pytest.fixture(params=[None, 0, 2], ids=["auto", "tile128", "tile256_8ph"])
 def gemm_cfg(request):
-    from netsdb_amd import _ext
-
-    _ext.hip().gemm_force_config(request.param)
-    yield request.param
-    _ext.hip().gemm_force_config(-1)
+    """Per-call tile config (ops.gemm_nt(cfg=...)): the production configs of the kernel library."""
+    return request.param
 
 
 @pytest.mark.parametrize("M,N,K", [(128, 128, 64), (1000, 1000, 4096), (77, 300, 520), (513, 129, 8), (2048, 64, 1024),
@@ -46,7 +43,7 @@ def test_gemm_shapes(M, N, K, splits, gemm_cfg):
     torch.manual_seed(0)
     A = torch.randn(M, K, device=DEV).to(torch.bfloat16)
     B = torch.randn(N, K, device=DEV).to(torch.bfloat16)
-    C = ops.gemm_nt(A, B, out_dtype=torch.float32, splits=splits)
+    C = ops.gemm_nt(A, B, out_dtype=torch.float32, splits=splits, cfg=gemm_cfg)
     _close(C, _ref_gemm(A, B), tol=1e-2)
 
 
@@ -58,9 +55,9 @@ def test_gemm_epilogue(mode, act, splits, gemm_cfg):
     A = (torch.randn(M, K, device=DEV) * 0.05).to(torch.bfloat16)
     B = (torch.randn(N, K, device=DEV) * 0.05).to(torch.bfloat16)
     bias = torch.randn(M if mode == 1 else N, device=DEV)
-    C = ops.gemm_nt(A, B, bias=bias, bias_mode=mode, act=act, out_dtype=torch.float32, splits=splits)
+    C = ops.gemm_nt(A, B, bias=bias, bias_mode=mode, act=act, out_dtype=torch.float32, splits=splits, cfg=gemm_cfg)
     _close(C, _ref_gemm(A, B, bias, mode, act), tol=1e-2)
-    Cb = ops.gemm_nt(A, B, bias=bias, bias_mode=mode, act=act, out_dtype=torch.bfloat16, splits=splits)
+    Cb = ops.gemm_nt(A, B, bias=bias, bias_mode=mode, act=act, out_dtype=torch.bfloat16, splits=splits, cfg=gemm_cfg)
     _close(Cb, _ref_gemm(A, B, bias, mode, act), tol=2e-2)
 
 
@@ -78,7 +75,7 @@ def test_gemm_accumulate(gemm_cfg):
     B = torch.randn(280, 256, device=DEV).to(torch.bfloat16)
     C = torch.randn(300, 280, device=DEV)
     ref = C + _ref_gemm(A, B)
-    ops.gemm_nt(A, B, out=C, out_dtype=torch.float32, accumulate=True)
+    ops.gemm_nt(A, B, out=C, out_dtype=torch.float32, accumulate=True, cfg=gemm_cfg)
     _close(C, ref, tol=1e-2)
 
 

@@ -109,12 +109,7 @@ def test_softmax_gemm_fallback_fixup(axis):
     A = torch.randn(M, K, device="cuda:0", generator=g).to(torch.bfloat16)
     B = (torch.randn(N, K, device="cuda:0", generator=g) * 0.1).to(torch.bfloat16)
     bias = torch.randn(N, device="cuda:0", generator=g)
-    h = _ext.hip()
-    h.gemm_force_config(400)
-    try:
-        y = ops.gemm_nt_softmax(A, B, bias, ops.BIAS_COL, axis=axis)
-    finally:
-        h.gemm_force_config(-1)
+    y = ops.gemm_nt_softmax(A, B, bias, ops.BIAS_COL, axis=axis, force_fallback=True)
     ref = _ref(A, B, bias, ops.BIAS_COL, axis)
     assert (y - ref).abs().max().item() / ref.abs().max().item() < 2e-5
     y2 = ops.gemm_nt_softmax(A, B, bias, ops.BIAS_COL, axis=axis)
