@@ -653,6 +653,7 @@ int nsdb_gemm_splits(int M, int N, int K, int batch, int cfg) {
 int nsdb_gemm_tail_eligible(int M, int N, int K, int batch, int splits, int cfg) {
   if (resolve_cfg(cfg, M, N, K, batch) != 2) return 0;
   const int ksteps = (K + nsdb::BK - 1) / nsdb::BK;
+  if (splits <= 0) splits = nsdb_gemm_splits(M, N, K, batch, cfg);    // the launcher's own choice
   splits = std::max(1, splits);
   const int kchunk_steps = (ksteps + splits - 1) / splits;
   const long long wgs = (long long)((M + 255) / 256) * ((N + 255) / 256) * ((ksteps + kchunk_steps - 1) / kchunk_steps) * batch;
