@@ -115,7 +115,9 @@ class PDBClient:
     removeDatabase = remove_database
 
     def create_set(self, db: str, name: str, type_=None, page_size: Optional[int] = None, dense: bool = False,
-                   policy=None, device="default") -> bool:
+                   policy=None, device="default", locality: Optional[str] = None) -> bool:
+        """Create a set. ``locality`` tells the page cache how the set is used (storage/manager.py LOCALITY:
+        "model" for weights every step re-reads, "job" (default), "shuffle", "partition", "temp")."""
         if not self.catalog.has_database(db):
             self.catalog.create_database(db)
         if policy == "auto":
@@ -126,12 +128,17 @@ class PDBClient:
         sid = self.catalog.create_set(db, name, type_.type_name() if type_ else None, page_size or self.storage.page_size,
                                       "dense" if dense else "pages",
                                       {"policy": getattr(policy, "name", policy) if policy is not None else "roundrobin"})
-        self.storage.create_set(db, name, type_, page_size, device=device, dense=dense, set_id=sid)
+        self.storage.create_set(db, name, type_, page_size, device=device, dense=dense, set_id=sid, locality=locality)
         if policy is not None:
             self.policies[(db, name)] = make_policy(policy)
         return True
 
     createSet = create_set
+
+    def set_locality(self, db: str, name: str, locality: str):
+        """Declare how an existing set is used (see create_set): the cost-based page cache keeps "model" sets
+        resident under pressure from one-pass job data."""
+        self.storage.set_locality(db, name, locality)
 
     def remove_set(self, db: str, name: str) -> bool:
         self.storage.remove_set(db, name)

@@ -31,10 +31,12 @@ def grace_partition(h: torch.Tensor, nparts: int) -> torch.Tensor:
 
 
 class Spool:
-    def __init__(self, storage, tag: str = "spool", page_size: Optional[int] = None):
+    def __init__(self, storage, tag: str = "spool", page_size: Optional[int] = None, locality: str = "temp"):
         self.storage = storage
         self.name = f"{tag}_{next(_ids)}"
-        self.set = storage.create_set(SPOOL_DB, self.name, None, page_size=page_size, persistent=False)
+        # temp / partition locality: MRU replacement and a low reuse prior in the cost-based page cache
+        self.set = storage.create_set(SPOOL_DB, self.name, None, page_size=page_size, persistent=False,
+                                      locality=locality)
         self.n = 0
         self.bytes = 0
 
@@ -67,7 +69,7 @@ class PartitionedSpool:
 
     def __init__(self, storage, nparts: int, tag: str = "part", page_size: Optional[int] = None):
         self.nparts = nparts
-        self.parts = [Spool(storage, f"{tag}{i}", page_size) for i in range(nparts)]
+        self.parts = [Spool(storage, f"{tag}{i}", page_size, locality="partition") for i in range(nparts)]
 
     def add(self, b: RecordBatch, h: torch.Tensor):
         if b is None or b.n == 0:

@@ -326,6 +326,10 @@ def load_model(client, db: str, batch: int, features: int, hidden: int, labels: 
     B.load_matrix(client, db, "wo", labels, last_in, block_x, block_x, seed=seed + 6, scale=(3.0 / last_in) ** 0.5,
                   dtype=dtype)
     B.load_matrix(client, db, "bo", labels, 1, block_x, 1, seed=seed + 7, scale=0.1, dtype=dtype)
+    # the weights are re-read by every inference step: "model" locality in the cost-based page cache
+    for name in ("w1", "b1", "wo", "bo") + (("w2", "b2") if hidden2 else ()):
+        if client.storage.has_set(db, name):
+            client.set_locality(db, name, "model")
 
 
 def reference_inference(x, w1, b1, wo, bo, w2=None, b2=None):

@@ -4,6 +4,21 @@ src/storage/source/PageCache.cc, PDBEvictWork.cc, src/bufferMgr/*).
 Owns the node's sets, the HBM budget (288 GB per MI355X: the default budget is 85 % of device
 memory), the native :class:`BufferManager` page pool (host memory, LRU-spills to disk), and the
 device->host eviction of unpinned pages when the HBM budget is exceeded.
+
+Eviction is cost-based per locality set (reference: src/storage/headers/PageCache.h:28-38 cost-based
+policy and CompareLocalitySets, LocalitySet.h:158-210 locality / replacement / durability types). Every
+set has a locality type (``LOCALITY``): model weights reused every step, job inputs/outputs, shuffle
+data, hash-partition spools and temp data. Within a set the replacement policy picks the candidate —
+LRU for reused sets, MRU for sequential one-pass data (a spool page just written is the one read last).
+Across sets the victim is the candidate with the lowest eviction cost per byte
+
+    cost = write_cost + reuse_prob * read_cost,    reuse_prob = prior(locality) / (1 + distance / n)
+
+(write_cost: moving the page out, 1 per byte for every tier; read_cost: bringing it back if it is reused,
+1 per byte; distance: accesses since the candidate was last touched — the reference's reference distance —
+normalised by the number of resident objects n). A spool-heavy job under a tight budget thus spills its own
+spool pages before it touches an FF weight panel that every step re-reads, which a single global LRU would
+evict first because the panel was touched longest ago.
 """
 from __future__ import annotations
 
@@ -20,6 +35,15 @@ from .. import _ext
 from .sets import DenseMatrixSet, Page, UserSet
 
 DEFAULT_PAGE_SIZE = 64 << 20
+
+# locality type -> (reuse prior, replacement policy within the set)
+LOCALITY = {
+    "model": (8.0, "lru"),        # weights / lookup tables re-read by every job step
+    "job": (1.0, "lru"),          # job inputs and outputs
+    "shuffle": (0.1, "mru"),      # shuffle data (read once by the receiving stage)
+    "partition": (0.1, "mru"),    # hash-partition spools (Grace join / partitioned aggregation)
+    "temp": (0.05, "mru"),        # spooled tuple sets and other job-scoped temp data
+}
 
 
 class StorageManager:
@@ -64,9 +88,10 @@ class StorageManager:
             chunk = page_pool_chunk or ((256 << 20) if self.home.type == "cuda" else (16 << 20))
             self.page_pool = DevicePagePool(self.home, chunk, max_bytes=self.device_budget)
         self.device_bytes = 0
-        # LRU of everything resident on the device tier (pages and dense panels), oldest first: eviction
-        # pops from the front instead of scanning every page of every set (PageCache's LRU list)
-        self._lru: "OrderedDict[int, object]" = OrderedDict()
+        # per locality set: everything of it resident on the device tier (pages and dense panels) in recency
+        # order, oldest first (LocalitySet::cachedPages: pop_front for LRU, pop_back for MRU)
+        self._resident: Dict[int, Tuple[object, "OrderedDict[int, object]"]] = {}
+        self.eviction_policy = "cost"     # "cost" (per-locality-set costs) or "lru" (one global LRU, A/B tests)
         self.sets: Dict[Tuple[str, str], UserSet] = {}
         self._ids = itertools.count(1)
         # sets created without a catalog id (temp sets, spools) draw from a disjoint range: their pool pages
@@ -78,7 +103,8 @@ class StorageManager:
 
     # ----------------------------------------------------------- sets
     def create_set(self, db: str, name: str, type_=None, page_size: Optional[int] = None, device="default",
-                   dense: bool = False, set_id: Optional[int] = None, persistent: bool = True) -> UserSet:
+                   dense: bool = False, set_id: Optional[int] = None, persistent: bool = True,
+                   locality: Optional[str] = None) -> UserSet:
         with self.lock:
             key = (db, name)
             if key in self.sets:
@@ -87,8 +113,15 @@ class StorageManager:
             sid = set_id if set_id is not None else (next(self._ids) if persistent else next(self._temp_ids))
             cls = DenseMatrixSet if dense else UserSet
             s = cls(self, db, name, type_, sid, page_size or self.page_size, dev, persistent)
+            s.locality = locality or ("job" if persistent else "temp")
             self.sets[key] = s
             return s
+
+    def set_locality(self, db: str, name: str, locality: str):
+        """Declare how a set is used (``LOCALITY`` keys): e.g. ``model`` for weights every step re-reads."""
+        if locality not in LOCALITY:
+            raise ValueError(f"unknown locality {locality!r}: one of {sorted(LOCALITY)}")
+        self.get_set(db, name).locality = locality
 
     def get_set(self, db: str, name: str) -> UserSet:
         try:
@@ -139,14 +172,30 @@ class StorageManager:
             return False
         return d.type != "cuda" or (d.index or 0) == (h.index or 0)
 
+    @staticmethod
+    def _set_of(obj):
+        return obj if isinstance(obj, DenseMatrixSet) else obj.set
+
     def track(self, obj):
         """``obj`` (a page or dense set) is resident on the device tier: most recently used."""
         obj.last_use = next(self._clock)
-        self._lru[id(obj)] = obj
-        self._lru.move_to_end(id(obj))
+        s = self._set_of(obj)
+        ent = self._resident.get(id(s))
+        if ent is None:
+            ent = self._resident[id(s)] = (s, OrderedDict())
+        ent[1][id(obj)] = obj
+        ent[1].move_to_end(id(obj))
 
     def untrack(self, obj):
-        self._lru.pop(id(obj), None)
+        s = self._set_of(obj)
+        ent = self._resident.get(id(s))
+        if ent is not None:
+            ent[1].pop(id(obj), None)
+            if not ent[1]:
+                del self._resident[id(s)]
+
+    def resident_objects(self) -> int:
+        return sum(len(od) for _, od in self._resident.values())
 
     def account(self, page: Page):
         page.last_use = next(self._clock)
@@ -174,44 +223,86 @@ class StorageManager:
 
     def touch(self, page):
         page.last_use = next(self._clock)
-        if id(page) in self._lru:
-            self._lru.move_to_end(id(page))
+        ent = self._resident.get(id(self._set_of(page)))
+        if ent is not None and id(page) in ent[1]:
+            ent[1].move_to_end(id(page))
+
+    @staticmethod
+    def _resident_on_device(p) -> bool:
+        return p.resident_on_home() if isinstance(p, DenseMatrixSet) else (p.location == "device" and p.batch is not None)
+
+    @staticmethod
+    def _nbytes(p) -> int:
+        return max(1, p._charged if isinstance(p, DenseMatrixSet) else p.nbytes)
+
+    def _candidate(self, s, od: "OrderedDict[int, object]", keep, skip: set):
+        """The set's replacement candidate (LRU: oldest; MRU: newest) that may be evicted now."""
+        policy = LOCALITY.get(getattr(s, "locality", "job"), LOCALITY["job"])[1]
+        seq = reversed(od.values()) if policy == "mru" else od.values()
+        for p in seq:
+            if p is keep or p.pins or id(p) in skip:
+                continue
+            return p
+        return None
+
+    def evict_cost(self, s, p) -> float:
+        """Eviction cost per byte of candidate ``p`` of locality set ``s`` (module doc)."""
+        prior = LOCALITY.get(getattr(s, "locality", "job"), LOCALITY["job"])[0]
+        n = max(1, self.resident_objects())
+        distance = max(0, self._clock_now() - p.last_use)
+        reuse_prob = prior / (1.0 + distance / n)
+        return 1.0 + reuse_prob * 1.0
+
+    def _clock_now(self) -> int:
+        return getattr(self, "_last_clock", 0)
+
+    def _pick_victim(self, keep, skip: set):
+        if self.eviction_policy == "lru":
+            best = None
+            for s, od in self._resident.values():
+                for p in od.values():
+                    if p is keep or p.pins or id(p) in skip:
+                        continue
+                    if best is None or p.last_use < best.last_use:
+                        best = p
+                    break                      # the set's oldest unpinned object
+            return best
+        best, best_cost = None, None
+        for s, od in self._resident.values():
+            p = self._candidate(s, od, keep, skip)
+            if p is None:
+                continue
+            c = self.evict_cost(s, p)
+            if best is None or c < best_cost or (c == best_cost and p.last_use < best.last_use):
+                best, best_cost = p, c
+        return best
 
     def evict(self, need: int, keep=None) -> int:
-        """Spill least-recently-used unpinned device pages (to the pinned tier / page pool) and dense
-        panels (in block-row slabs, PageCache/PDBEvictWork style) until ``need`` bytes are free."""
+        """Spill device pages (to the pinned tier / page pool) and dense panels (in block-row slabs,
+        PageCache/PDBEvictWork style) until ``need`` bytes are free: victims by per-locality-set cost."""
         freed = 0
-        kept = 0                     # pinned / kept entries stay at the front of the LRU
+        skip = set()                 # objects that could not be spilled this round
+        self._last_clock = next(self._clock)
         while freed < need:
-            chunk = list(itertools.islice(self._lru.items(), kept, kept + 32))
-            if not chunk:
+            p = self._pick_victim(keep, skip)
+            if p is None:
                 break
-            for key, p in chunk:
-                if freed >= need:
-                    break
-                if p is keep:
-                    kept += 1
-                    continue
-                if isinstance(p, DenseMatrixSet):
-                    if not p.resident_on_home():
-                        self.untrack(p)
-                        continue
-                elif p.location != "device" or p.batch is None:
-                    self.untrack(p)
-                    continue
-                if p.pins:
-                    kept += 1
-                    continue
-                f = p.spill()
-                if f or not (p.resident_on_home() if isinstance(p, DenseMatrixSet) else p.location == "device"):
-                    self.untrack(p)
-                else:
-                    kept += 1
-                freed += f
-                if isinstance(p, DenseMatrixSet):
-                    self.stats["evicted_panels"] = self.stats.get("evicted_panels", 0) + 1
-                else:
-                    self.stats["evicted_pages"] += 1
+            if not self._resident_on_device(p):
+                self.untrack(p)
+                continue
+            f = p.spill()
+            if f or not self._resident_on_device(p):
+                self.untrack(p)
+                self.stats.setdefault("evicted_by_locality", {})
+                loc = getattr(self._set_of(p), "locality", "job")
+                self.stats["evicted_by_locality"][loc] = self.stats["evicted_by_locality"].get(loc, 0) + 1
+            else:
+                skip.add(id(p))
+            freed += f
+            if isinstance(p, DenseMatrixSet):
+                self.stats["evicted_panels"] = self.stats.get("evicted_panels", 0) + 1
+            else:
+                self.stats["evicted_pages"] += 1
         self.device_bytes -= freed
         self.stats["evicted_bytes"] += freed
         return freed
@@ -247,7 +338,8 @@ class StorageManager:
 
     def summary(self) -> dict:
         return {
-            "sets": {f"{d}.{n}": {"records": s.num_records(), "bytes": s.nbytes(), "pages": len(s.pages)}
+            "sets": {f"{d}.{n}": {"records": s.num_records(), "bytes": s.nbytes(), "pages": len(s.pages),
+                                  "locality": getattr(s, "locality", "job")}
                      for (d, n), s in self.sets.items()},
             "device_bytes": self.device_bytes,
             "device_budget": self.device_budget,
@@ -261,4 +353,4 @@ class StorageManager:
         }
 
 
-__all__ = ["StorageManager", "DEFAULT_PAGE_SIZE"]
+__all__ = ["StorageManager", "DEFAULT_PAGE_SIZE", "LOCALITY"]

@@ -472,9 +472,11 @@ class DenseMatrixSet(UserSet):
         return 0
 
     def _slab_rows(self, ld: int, esize: int) -> int:
+        """Rows per spill slab: whole block rows when a block row fits a page, else as many rows as fit (a slab
+        must fit one pool page; load_rows assembles any row range from slabs of any height)."""
         per = max(1, self.page_size // max(1, ld * esize))
-        if self.block_rows:
-            per = max(self.block_rows, per // self.block_rows * self.block_rows)
+        if self.block_rows and per >= self.block_rows:
+            per = per // self.block_rows * self.block_rows
         return per
 
     def spill(self) -> int:

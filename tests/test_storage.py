@@ -204,3 +204,41 @@ def test_dense_add_batch_vectorised_matches_elementwise():
         torch.testing.assert_close(to_tensor(c, "db", "dst"), a, rtol=0, atol=0)
         c.remove_set("db", "src")
         c.remove_set("db", "dst")
+
+
+@pytest.mark.parametrize("policy", ["cost", "lru"])
+def test_spool_pressure_keeps_model_panel_resident(tmp_path, policy):
+    """Cost-based page cache (storage/manager.py; reference PageCache.h cost policy + LocalitySet types): a
+    spool-heavy job under a tight budget spills its own MRU spool pages and never the "model" weight panel
+    every step re-reads; the single global LRU (A/B) evicts the panel first because it was touched longest ago."""
+    import torch
+
+    from netsdb_amd.client import PDBClient
+    from netsdb_amd.execution.spool import Spool
+    from netsdb_amd.models.blocks import load_tensor, to_tensor
+    from netsdb_amd.objects.record import RecordBatch
+
+    c = PDBClient(root=str(tmp_path), device="cpu", device_budget=3 << 20, page_size=128 << 10)
+    st = c.storage
+    st.eviction_policy = policy
+    c.create_database("ff")
+    w1 = torch.randn(512, 1024)                                # 2 MiB f32 panel
+    load_tensor(c, "ff", "w1", w1, 64, 256, dtype=torch.float32)
+    c.set_locality("ff", "w1", "model")
+    panel = st.get_set("ff", "w1")
+    assert panel.is_resident()
+    sp = Spool(st, "job")
+    for i in range(24):                                        # 24 x 128 KiB of one-pass spool pages
+        x = torch.full((32 * 1024,), float(i))
+        sp.add(RecordBatch({"x": x}, x.numel()))
+    ev = st.stats.get("evicted_by_locality", {})
+    if policy == "cost":
+        assert panel.is_resident() and not panel.is_spilled(), ev
+        assert ev.get("temp", 0) > 0 and ev.get("model", 0) == 0, ev
+    else:
+        assert panel.is_spilled(), ev                          # the plain LRU takes the oldest object: the panel
+    assert st.device_bytes <= st.device_budget
+    got = torch.cat([b.columns["x"] for b in sp])              # spilled spool pages read back in order
+    assert torch.equal(got, torch.arange(24).repeat_interleave(32 * 1024).float())
+    torch.testing.assert_close(to_tensor(c, "ff", "w1"), w1)
+    sp.drop()
