@@ -22,6 +22,8 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
 int nsdb_gemm_nt_softmax(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, long long lda,
                          long long ldb, long long ldc, int bias_mode, float alpha, int axis, void* part, int* cnt,
                          int* flag, int force_fallback, hipStream_t stream);
+int nsdb_gemm_nt_f32(const float* A, const float* B, float* C, int M, int N, int K, long long lda, long long ldb,
+                     long long ldc, float alpha, int accumulate, hipStream_t stream);
 int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* out, int N, int C, int H, int W,
                       int OC, int KH, int KW, int stride, int pad, int dil, int ldw, int act, int nchw_out,
                       int out_f32, hipStream_t stream);
@@ -54,6 +56,8 @@ int nsdb_str_hash(const void* bytes, const int64_t* off, int64_t n, uint64_t* ou
 int nsdb_str_like(const void* bytes, const int64_t* off, int64_t n, const uint8_t* pat, int pat_len,
                   const int* seg_start, const int* seg_len, int nseg, int anchor_start, int anchor_end, int negate,
                   uint8_t* out, hipStream_t st);
+int nsdb_str_slice(const void* src, const int64_t* off, int64_t start, const int64_t* out_off, int64_t n, void* dst,
+                   hipStream_t st);
 int nsdb_str_gather(const void* src, const int64_t* off, const int64_t* idx, const int64_t* out_off, int64_t m,
                     void* dst, hipStream_t st);
 }
@@ -265,6 +269,32 @@ torch::Tensor gemm_nt_bseg(torch::Tensor A, torch::Tensor Bg, c10::optional<torc
   return C;
 }
 
+// C (f32 [M, N]) = alpha * A . B^T (+ C): exact-f32 MFMA (v_mfma_f32_16x16x4_f32) for the analytics libraries.
+torch::Tensor gemm_nt_f32(torch::Tensor A, torch::Tensor B, double alpha, c10::optional<torch::Tensor> out,
+                          bool accumulate) {
+  check_cuda(A, "A");
+  check_cuda(B, "B");
+  TORCH_CHECK(A.scalar_type() == torch::kFloat32 && B.scalar_type() == torch::kFloat32, "A,B must be f32");
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1, "A,B [rows, K] K-contiguous");
+  const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
+  TORCH_CHECK(B.size(1) == K && K % 4 == 0, "K mismatch or K % 4 != 0");
+  TORCH_CHECK(A.stride(0) % 4 == 0 && B.stride(0) % 4 == 0, "row strides must be multiples of 4");
+  TORCH_CHECK(M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31), "dims too large");
+  torch::Tensor C;
+  if (out.has_value() && out->defined()) {
+    C = *out;
+    TORCH_CHECK(C.scalar_type() == torch::kFloat32 && C.dim() == 2 && C.size(0) == M && C.size(1) == N &&
+                C.stride(1) == 1, "out must be f32 [M, N] with unit column stride");
+  } else {
+    TORCH_CHECK(!accumulate, "accumulate=True needs an existing out tensor");
+    C = torch::empty({M, N}, A.options());
+  }
+  check_rc(nsdb_gemm_nt_f32(A.data_ptr<float>(), B.data_ptr<float>(), C.data_ptr<float>(), (int)M, (int)N, (int)K,
+                            A.stride(0), B.stride(0), C.stride(0), (float)alpha, accumulate ? 1 : 0, cur_stream()),
+           "gemm_nt_f32");
+  return C;
+}
+
 int64_t gemm_splits(int64_t M, int64_t N, int64_t K, int64_t batch, int64_t cfg) {
   return nsdb_gemm_splits((int)M, (int)N, (int)K, (int)batch, (int)cfg);
 }
@@ -465,6 +495,21 @@ torch::Tensor str_gather(torch::Tensor bytes, torch::Tensor off, torch::Tensor i
   return dst;
 }
 
+// SUBSTRING of every row: out_off [n+1] (device prefix sums of the clamped lengths), cap = an upper bound of the
+// output bytes known on the host (n * length): no device read to size the buffer.
+torch::Tensor str_slice(torch::Tensor bytes, torch::Tensor off, int64_t start, torch::Tensor out_off, int64_t cap) {
+  check_strings(bytes, off);
+  check_cuda(out_off, "out_off");
+  TORCH_CHECK(start >= 0, "start must be >= 0");
+  TORCH_CHECK(out_off.scalar_type() == torch::kInt64 && out_off.numel() == off.numel(), "out_off [n+1]");
+  const int64_t padded = ((cap + 16 + 3) / 4) * 4;
+  auto dst = torch::zeros({padded}, bytes.options());
+  check_rc(nsdb_str_slice(bytes.data_ptr(), off.data_ptr<int64_t>(), start, out_off.data_ptr<int64_t>(),
+                          off.numel() - 1, dst.data_ptr(), cur_stream()),
+           "str_slice");
+  return dst;
+}
+
 // Dedup: blocks [n, ...] contiguous (any dtype; bytes per block % 16 == 0) -> [n, S] i64 partial sums.
 torch::Tensor block_hash_partial(torch::Tensor blocks) {
   check_cuda(blocks, "blocks");
@@ -544,6 +589,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dropout") = 0.0, py::arg("seed") = 0, py::arg("splits") = 0, py::arg("out") = py::none(),
         py::arg("accumulate") = false, py::arg("cfg") = -1, py::arg("signal") = py::none(),
         py::arg("signal_value") = 0);
+  m.def("gemm_nt_f32", &gemm_nt_f32, "alpha * A.B^T (+C) on the exact-f32 MFMA (16x16x4)", py::arg("A"),
+        py::arg("B"), py::arg("alpha") = 1.0, py::arg("out") = py::none(), py::arg("accumulate") = false);
   m.def("gemm_splits", &gemm_splits, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("batch") = 1,
         py::arg("cfg") = -1);
   m.def("gemm_tail_eligible", [](int64_t M, int64_t N, int64_t K, int64_t batch, int64_t splits, int64_t cfg) {
@@ -590,5 +637,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("block_maxdiff_partial", &block_maxdiff_partial, "dedup: per-(block, split) max |pool[cand] - blk|");
   m.def("str_hash", &str_hash, "64-bit hash per string of a device string column");
   m.def("str_like", &str_like, "SQL LIKE over a device string column (segments of the pattern bytes)");
+  m.def("str_slice", &str_slice, "SUBSTRING of every row of a device string column (no host read)");
   m.def("str_gather", &str_gather, "take() of a device string column into a new padded byte buffer");
 }

@@ -125,6 +125,18 @@ __global__ __launch_bounds__(256) void str_gather_kernel(const uint8_t* __restri
   for (int64_t k = 0; k < len; ++k) dst[d + k] = src[s + k];
 }
 
+// SUBSTRING: row j's bytes [start, start + len_j) (len_j = out_off[j+1] - out_off[j], computed on the device by the
+// caller as clamp(row length - start, 0, length)) copied to out_off[j].
+__global__ __launch_bounds__(256) void str_slice_kernel(const uint8_t* __restrict__ src,
+                                                       const int64_t* __restrict__ off, int64_t start,
+                                                       const int64_t* __restrict__ out_off, int64_t n,
+                                                       uint8_t* __restrict__ dst) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const int64_t s = off[j] + start, d = out_off[j], len = out_off[j + 1] - d;
+  for (int64_t k = 0; k < len; ++k) dst[d + k] = src[s + k];
+}
+
 inline int grid_for(int64_t n) { return (int)((n + 255) / 256); }
 
 }  // namespace
@@ -162,6 +174,15 @@ int nsdb_str_gather(const void* src, const int64_t* off, const int64_t* idx, con
   if (m <= 0) return 0;
   hipLaunchKernelGGL(str_gather_kernel, dim3(grid_for(m)), dim3(256), 0, st, (const uint8_t*)src, off, idx,
                      out_off, m, (uint8_t*)dst);
+  return (int)hipGetLastError();
+}
+
+int nsdb_str_slice(const void* src, const int64_t* off, int64_t start, const int64_t* out_off, int64_t n, void* dst,
+                   hipStream_t st) {
+  if (n <= 0) return 0;
+  if (start < 0) return -2;
+  hipLaunchKernelGGL(str_slice_kernel, dim3(grid_for(n)), dim3(256), 0, st, (const uint8_t*)src, off, start, out_off, n,
+                     (uint8_t*)dst);
   return (int)hipGetLastError();
 }
 

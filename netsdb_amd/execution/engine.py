@@ -666,21 +666,24 @@ class QueryEngine:
         return reps, agg
 
     def _topk(self, comp, batches, kcol, vcol, out_ts, out_col, state):
+        """TopKComp: per-rank top k by score on the device (torch.topk over the device score column; objects
+        gathered with a device take), then the ranks' candidates meet through one packed all-gather and the
+        global top k is selected on the device again. No host copy of the scores."""
         objs, scores = [], []
         for x in batches:
-            o = x.columns[kcol]
+            objs.append(x.columns[kcol])
             s = x.columns[vcol]
-            objs.append(o)
             scores.append(s if isinstance(s, torch.Tensor) else torch.tensor(s, dtype=torch.float64))
+        local = None
         if objs:
             ob = column_concat(objs)
-            sc = torch.cat([s.double().cpu() for s in scores])
+            dev = scores[0].device
+            sc = torch.cat([s.to(dev) for s in scores])
+            if not sc.is_floating_point():
+                sc = sc.double()
             k = min(comp.k, sc.numel())
             top = torch.topk(sc, k).indices
-            local = RecordBatch({"o": ob.take(top) if isinstance(ob, RecordBatch) else [ob[i] for i in top.tolist()],
-                                 "s": sc[top]}, k)
-        else:
-            local = None
+            local = RecordBatch({"o": column_take(ob, top), "s": sc.index_select(0, top)}, k)
         if self.ctx.distributed:
             got = [g for g in self.ctx.broadcast_batch_all(local) if g is not None and g.n]
             local = RecordBatch.concat(got) if got else None

@@ -23,6 +23,8 @@ from typing import Optional
 
 import torch
 
+from .. import ops
+
 from ..computations import AggregateComp, JoinComp, MultiSelectionComp, ScanSet, SelectionComp, WriteSet
 from ..lambdas import make_batch_lambda, make_lambda_from_member, make_lambda_from_self
 from ..objects.builtin import DoubleVector
@@ -79,9 +81,11 @@ class _KeyedSum(AggregateComp):
 
 # ---------------------------------------------------------------------------------------- k-means
 def _sq_dists(X: torch.Tensor, C: torch.Tensor) -> torch.Tensor:
-    """|x - c|^2 for all pairs via one GEMM (the norm expansion of KMeansNormVectorMap)."""
+    """|x - c|^2 for all pairs via one GEMM (the norm expansion of KMeansNormVectorMap): -2 X.C^T runs on the
+    exact-f32 MFMA kernel on the GPU (ops.gemm_nt_f32), in the data's dtype on the CPU."""
     C = C.to(X.device, X.dtype)
-    return (X * X).sum(1, keepdim=True) - 2.0 * (X @ C.t()) + (C * C).sum(1).unsqueeze(0)
+    xc = ops.gemm_nt_f32(X, C, alpha=-2.0)
+    return (X * X).sum(1, keepdim=True).to(xc.dtype) + xc + (C * C).sum(1).unsqueeze(0).to(xc.dtype)
 
 
 class KMeansSampleSelection(SelectionComp):
@@ -179,13 +183,20 @@ class GmmModel:
     def update(self):
         self.chol = torch.linalg.cholesky(self.covars)
         self.logdet = 2.0 * torch.log(torch.diagonal(self.chol, dim1=-2, dim2=-1)).sum(-1)
+        # whitening L^-1 per component: Mahalanobis terms of all components become ONE GEMM per batch
+        eye = torch.eye(self.chol.shape[-1], dtype=self.chol.dtype, device=self.chol.device)
+        self.chol_inv = torch.linalg.solve_triangular(self.chol, eye.expand_as(self.chol), upper=False)
 
     def log_resp(self, X: torch.Tensor):
-        """log(w_k N(x | mu_k, S_k)) for every row and component, and the row log-likelihood."""
+        """log(w_k N(x | mu_k, S_k)) for every row and component, and the row log-likelihood.
+        z_k = L_k^-1 (x - mu_k) for every component at once: [k*d, d] x X^T on the matrix cores (ops.gemm_nt_f32)
+        minus L_k^-1 mu_k."""
         d = X.shape[1]
+        k = self.means.shape[0]
         dev, dt = X.device, X.dtype
-        diff = X.unsqueeze(0) - self.means.to(dev, dt).unsqueeze(1)                     # [k, n, d]
-        z = torch.linalg.solve_triangular(self.chol.to(dev, dt), diff.transpose(1, 2), upper=False)  # [k, d, n]
+        Li = self.chol_inv.to(dev, dt)                                                  # [k, d, d]
+        z = ops.gemm_nt_f32(Li.reshape(k * d, d), X).to(dt).reshape(k, d, -1)          # [k, d, n]
+        z = z - torch.bmm(Li, self.means.to(dev, dt).unsqueeze(2))                      # - L^-1 mu
         maha = (z * z).sum(1)                                                           # [k, n]
         lp = (torch.log(self.weights.to(dev, dt)).unsqueeze(1) - 0.5 * (d * torch.log(torch.tensor(2 * torch.pi, dtype=dt))
                                                                         + self.logdet.to(dev, dt).unsqueeze(1) + maha))
@@ -215,8 +226,11 @@ class GmmPartialStats(MultiSelectionComp):
             R = lr.exp()                                                   # [k, n]
             k, d = R.shape[0], X.shape[1]
             s0 = R.sum(1, keepdim=True)                                    # [k, 1]
-            s1 = R @ X                                                     # [k, d]
-            s2 = torch.einsum("kn,ni,nj->kij", R, X, X).reshape(k, d * d)  # [k, d*d]
+            Xt = X.t().contiguous()                                        # [d, n]: K = n contiguous
+            s1 = ops.gemm_nt_f32(R, Xt).to(X.dtype)                        # [k, d] = R . X
+            # second moments sum_n r_kn x_n x_n^T: (r_k * X^T) . X as one [k*d, n] x [d, n]^T GEMM
+            s2 = ops.gemm_nt_f32((R.unsqueeze(1) * Xt.unsqueeze(0)).reshape(k * d, -1), Xt).to(X.dtype)
+            s2 = s2.reshape(k, d * d)                                      # [k, d*d]
             llc = torch.zeros(k, 1, dtype=X.dtype, device=X.device)
             llc[0, 0] = ll.sum()
             return RecordBatch({"comp": torch.arange(k, device=X.device), "stats": torch.cat([s0, s1, s2, llc], 1)}, k,

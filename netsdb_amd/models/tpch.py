@@ -654,7 +654,11 @@ def q22(client, db: str, codes=("13", "31", "23", "29", "30", "18", "17")) -> Li
         return in_codes(b) & (_col(b, "c_acctbal") > mean) & ~torch.isin(ck, with_orders.to(ck.device))
 
     sel = _Filter(pred).set_input(ScanSet(db, "customer", Customer))
-    agg = _GroupBy(lambda b: [s[:2] for s in _col(b, "c_phone")],
+    def cntrycode(b):
+        c = _col(b, "c_phone")        # SUBSTRING(c_phone, 1, 2): a device string column stays one
+        return c.substr(0, 2) if isinstance(c, StringColumn) else [s[:2] for s in c]
+
+    agg = _GroupBy(cntrycode,
                    lambda b: torch.stack([torch.ones(b.n, dtype=torch.float64, device=_dev(b)),
                                           _col(b, "c_acctbal").double()], 1), _rows_out(["numcust", "totacctbal"]))
     r = _flat(_run(client, db, "q22_out", agg.set_input(sel), "tpch_q22"))

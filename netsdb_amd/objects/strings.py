@@ -247,6 +247,32 @@ class StringColumn:
             data = torch.from_numpy(data_np)
         return StringColumn(data, out_off, total)
 
+    def substr(self, start: int, length: int) -> "StringColumn":
+        """SQL SUBSTRING(s FROM start + 1 FOR length) of every row, on bytes (0-based ``start``): lengths clamped
+        and prefix-summed on the device, one copy launch, no device->host read (the output buffer is sized by the
+        host-known bound n * length)."""
+        if start < 0 or length < 0:
+            raise ValueError("substr: start and length must be >= 0")
+        dev, n = self.device, len(self)
+        lens = self.offsets[1:] - self.offsets[:-1]
+        new = (lens - start).clamp(min=0, max=length)
+        out_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        if n:
+            torch.cumsum(new, 0, out=out_off[1:])
+        cap = n * length
+        if dev.type == "cuda":
+            data = _ext.hip().str_slice(self.data, self.offsets.contiguous(), int(start), out_off, cap)
+        else:
+            src, off, oo = self.data.numpy(), self.offsets.numpy(), out_off.numpy()
+            data_np = np.zeros(self._alloc_size(cap), dtype=np.uint8)
+            total = int(oo[-1])
+            if total:
+                ln = oo[1:] - oo[:-1]
+                pos = np.repeat(off[:-1] + start - oo[:-1], ln) + np.arange(total)
+                data_np[:total] = src[pos]
+            data = torch.from_numpy(data_np)
+        return StringColumn(data, out_off, cap)
+
     @staticmethod
     def concat(parts: Sequence["StringColumn"]) -> "StringColumn":
         parts = list(parts)

@@ -122,6 +122,43 @@ def gemm_nt(A, B, bias=None, bias_mode=BIAS_NONE, act=ACT_NONE, out_dtype=torch.
     return v
 
 
+def gemm_nt_f32(A, B, alpha=1.0, out=None, accumulate=False):
+    """alpha * A @ B^T (+ out) at fp32 precision: A [M, K], B [N, K]. GPU tensors run the exact-f32 MFMA kernel
+    (csrc/kernels/gemm_f32.hip; f64 inputs are computed in f32 there); CPU tensors keep their dtype (the
+    reference analytics run in double)."""
+    if _use_hip(A, B):
+        A = A.float()
+        B = B.float()
+        if A.stride(-1) != 1 or A.stride(-2) % 4 or A.shape[-1] % 4:
+            A = _pad_k4(A)
+        if B.stride(-1) != 1 or B.stride(-2) % 4 or B.shape[-1] % 4:
+            B = _pad_k4(B)
+        if out is not None and (out.dtype != torch.float32 or out.stride(-1) != 1):
+            r = _ext.hip().gemm_nt_f32(A, B, float(alpha))
+            if accumulate:
+                out.add_(r.to(out.dtype))
+            else:
+                out.copy_(r)
+            return out
+        return _ext.hip().gemm_nt_f32(A, B, float(alpha), out, bool(accumulate))
+    dt = torch.promote_types(A.dtype, B.dtype)
+    v = (A.to(dt) @ B.to(dt).transpose(-1, -2)) * alpha
+    if out is not None:
+        if accumulate:
+            out.add_(v.to(out.dtype))
+        else:
+            out.copy_(v)
+        return out
+    return v
+
+
+def _pad_k4(X):
+    k = (X.shape[-1] + 3) // 4 * 4
+    Y = torch.zeros(X.shape[:-1] + (k,), dtype=X.dtype, device=X.device)
+    Y[..., : X.shape[-1]] = X
+    return Y
+
+
 def gemm_nt_softmax(A, B, bias=None, bias_mode=BIAS_NONE, axis=1, alpha=1.0, out=None, force_fallback=False):
     """softmax(alpha * A @ B^T + bias) along ``axis`` 1 (each row of the [M, N] result) or 2 (each column), f32.
     On the GPU the normalisation is fused into the GEMM epilogue (max-subtracted, no exp'd round trip through

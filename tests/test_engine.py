@@ -1,5 +1,6 @@
 """End-to-end query tests on the CPU pseudo-cluster path (reference test strategy: src/tests/source
 Test*.cc selection/join/aggregation programs checked against expected outputs)."""
+import pytest
 import torch
 
 from netsdb_amd.client import PDBClient
@@ -192,3 +193,45 @@ def test_chained_selection_join_aggregate(tmp_path):
             exp[e.department] = exp.get(e.department, 0) + floors[e.department]
     assert got == exp
     _ = torch
+
+
+@pytest.mark.gpu
+def test_topk_on_device_gpu(tmp_path):
+    """TopKComp on a device set: scores never leave the GPU (no .cpu()/.tolist()/.item() inside the TopK sink),
+    result matches the host top 5."""
+    from netsdb_amd.execution.engine import QueryEngine
+
+    c = PDBClient(root=str(tmp_path), page_size=1 << 12, device="cuda:0")
+    c.create_database("db")
+    c.create_set("db", "emps", Employee)
+    c.send_data("db", "emps", _emps(300))
+    c.create_set("db", "top", Employee)
+    calls = []
+    orig_topk = QueryEngine._topk
+    orig = {k: getattr(torch.Tensor, k) for k in ("cpu", "tolist", "item")}
+
+    def guard(name):
+        def w(self, *a, **kw):
+            calls.append(name)
+            return orig[name](self, *a, **kw)
+        return w
+
+    def guarded_topk(self, *a, **kw):
+        for k in orig:
+            setattr(torch.Tensor, k, guard(k))
+        try:
+            return orig_topk(self, *a, **kw)
+        finally:
+            for k, f in orig.items():
+                setattr(torch.Tensor, k, f)
+
+    QueryEngine._topk = guarded_topk
+    try:
+        t = TopSalary(5)
+        t.set_input(ScanSet("db", "emps", Employee))
+        c.execute_computations(WriteSet("db", "top").set_input(t))
+    finally:
+        QueryEngine._topk = orig_topk
+    assert calls == [], calls
+    got = sorted(o.salary for o in c.get_set_iterator("db", "top"))
+    assert got == sorted(e.salary for e in _emps(300))[-5:]

@@ -175,3 +175,45 @@ def test_tpch_string_queries_gpu(tmp_path):
     finally:
         tpch._like = orig
     assert seen and all(t is StringColumn and d.type == "cuda" for t, d in seen)
+
+
+def test_substr_cpu():
+    """SUBSTRING on bytes: clamped at both ends, empty rows, lengths 0, a start past every row."""
+    strs = ["", "a", "ab", "13-555-0199", "27-1", "xyz" * 20, "é-x"]
+    col = StringColumn.from_list(strs)
+    for start, length in ((0, 2), (1, 3), (5, 0), (40, 10), (0, 100)):
+        got = col.substr(start, length)
+        raw = [bytes(got.data[got.offsets[i]:got.offsets[i + 1]].numpy()) for i in range(len(strs))]
+        assert raw == [x.encode()[start:start + length] for x in strs]
+    ascii_col = StringColumn.from_list(strs[:6])
+    sub = ascii_col.substr(0, 2)
+    assert sub.tolist() == [x[:2] for x in strs[:6]]
+    assert sub.hash64().tolist() == [hash_str(x[:2]) for x in strs[:6]]     # group-by keys of the substrings
+
+
+@pytest.mark.gpu
+def test_substr_gpu_matches_cpu_without_host_reads():
+    strs = _strings(4000, seed=9)
+    cpu = StringColumn.from_list(strs).substr(1, 3)
+    col = StringColumn.from_list(strs, "cuda:0")
+    calls = []
+    orig = {k: getattr(torch.Tensor, k) for k in ("cpu", "tolist", "item")}
+
+    def guard(name):
+        def w(self, *a, **kw):
+            calls.append(name)
+            return orig[name](self, *a, **kw)
+        return w
+
+    for k in orig:
+        setattr(torch.Tensor, k, guard(k))
+    try:
+        sub = col.substr(1, 3)
+        h = sub.hash64()
+    finally:
+        for k, f in orig.items():
+            setattr(torch.Tensor, k, f)
+    assert calls == [], calls
+    assert sub.device.type == "cuda"
+    assert sub.tolist() == cpu.tolist()
+    assert h.cpu().tolist() == cpu.hash64().tolist()
