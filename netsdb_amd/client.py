@@ -12,6 +12,9 @@ simply an embedded database.  (A socket front end for remote clients lives in
 """
 from __future__ import annotations
 
+import contextlib
+import threading
+
 import os
 from typing import Iterator, List, Optional
 
@@ -49,7 +52,8 @@ class PDBClient:
         self.storage = StorageManager(root=root, device=self.device, page_size=page_size, pool_pages=pool_pages,
                                       rank=self.ctx.rank, device_budget=device_budget, pinned_budget=pinned_budget)
         self.catalog = Catalog(catalog_path or os.path.join(self.storage.root, f"catalog_r{self.ctx.rank}.db"))
-        self.engine = QueryEngine(self.storage, self.ctx, self.catalog, self.tracer, broadcast_threshold, fusion)
+        self._engine = QueryEngine(self.storage, self.ctx, self.catalog, self.tracer, broadcast_threshold, fusion)
+        self._lane = threading.local()    # per-thread job lane (server requests running concurrently)
         self.policies = {}
         self.catalog.register_node(self.ctx.rank, os.environ.get("MASTER_ADDR", "127.0.0.1"), str(self.device),
                                    torch.cuda.get_device_properties(self.device).total_memory
@@ -62,6 +66,41 @@ class PDBClient:
         self.tail_trigger = None         # TailTrigger (arm_tail_trigger)
         if resume:
             self._resume()
+
+    @property
+    def engine(self):
+        """The query engine of the calling thread's job lane (``job_lane``), else the client's engine."""
+        e = getattr(self._lane, "engine", None)
+        return e if e is not None else self._engine
+
+    @engine.setter
+    def engine(self, e):
+        self._engine = e
+
+    @contextlib.contextmanager
+    def job_lane(self, lane: int):
+        """Run this thread's jobs on lane ``lane``: an engine of its own (same storage / catalog / plan cache and
+        configuration) and, on a GPU, a HIP stream of its own (JobStreams lane), so requests touching disjoint
+        sets execute concurrently (the reference's QuerySchedulerServer running independent jobs)."""
+        prev = getattr(self._lane, "engine", None)
+        self._lane.engine = self._engine.clone()
+        try:
+            if self.device is not None and torch.device(self.device).type == "cuda":
+                if self.job_streams is None:
+                    from .execution.streams import JobStreams
+
+                    self.job_streams = JobStreams(self.device, lanes=max(self.job_lanes, 4),
+                                                  priority=self.job_stream_priority,
+                                                  lane_priority=self.job_lane_priority)
+                s = self.job_streams.stream(lane)
+                s.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(s):
+                    yield
+                    s.synchronize()
+            else:
+                yield
+        finally:
+            self._lane.engine = prev
 
     @classmethod
     def from_config(cls, conf, **kwargs) -> "PDBClient":

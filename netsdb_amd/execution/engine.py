@@ -111,6 +111,16 @@ class QueryEngine:
         self.last_tcap = None
         self._last_comps = None
 
+    def clone(self) -> "QueryEngine":
+        """An engine for another job lane: same storage, context, catalog, tracer, configuration and plan cache
+        (dict access under the GIL); its own per-job state (spools, statistics)."""
+        e = QueryEngine(self.storage, self.ctx, self.catalog, self.tracer, self.broadcast_threshold, self.fusion)
+        for k in ("adaptive", "plan_cache_enabled", "ooc_fraction", "shuffle_chunk_bytes"):
+            setattr(e, k, getattr(self, k))
+        e._plan_cache = self._plan_cache
+        e.__dict__["meta_cache"] = self.__dict__.setdefault("meta_cache", {})
+        return e
+
     # ------------------------------------------------------------------ entry
     def _compile(self, sinks, job_name, stats):
         """TCAP for the graph: from the pre-compiled workload cache when a structurally identical graph

@@ -16,6 +16,7 @@ import importlib
 import inspect
 import socket
 import socketserver
+import itertools
 import threading
 import traceback
 from typing import Any, Callable, Dict, List, Optional, Sequence
@@ -281,8 +282,76 @@ def _jsonable(v):
     return repr(v)
 
 
+class _RWLock:
+    """Readers-writer lock (writers preferred)."""
+
+    def __init__(self):
+        self._c = threading.Condition()
+        self._readers = 0
+        self._writer = False
+        self._waiting_writers = 0
+
+    def acquire(self, write: bool):
+        with self._c:
+            if write:
+                self._waiting_writers += 1
+                while self._writer or self._readers:
+                    self._c.wait()
+                self._waiting_writers -= 1
+                self._writer = True
+            else:
+                while self._writer or self._waiting_writers:
+                    self._c.wait()
+                self._readers += 1
+
+    def release(self, write: bool):
+        with self._c:
+            if write:
+                self._writer = False
+            else:
+                self._readers -= 1
+            self._c.notify_all()
+
+
+# Requests answered by rank 0 alone from its catalog / plan state: no data, no collectives, never broadcast, so
+# they run at any time, concurrently with jobs.
+LOCAL_OPS = frozenset({"ping", "list_sets", "list_nodes", "print_catalog", "explain", "explain_graph"})
+
+
+def _graph_sets(sinks):
+    """(read sets, written sets) of a computation graph: its ScanSets and WriteSets."""
+    from ..computations import ScanSet, WriteSet
+
+    reads, writes, seen, todo = set(), set(), set(), list(sinks)
+    while todo:
+        c = todo.pop()
+        if c is None or id(c) in seen:
+            continue
+        seen.add(id(c))
+        if isinstance(c, WriteSet):
+            writes.add((c.db, c.set_name))
+        elif isinstance(c, ScanSet):
+            reads.add((c.db, c.set_name))
+        todo.extend(getattr(c, "inputs", []) or [])
+    return reads, writes
+
+
 class PDBFrontend:
-    """Rank-0 socket server. ``serve_forever()`` blocks; ``start()`` runs it in a thread."""
+    """Rank-0 socket server. ``serve_forever()`` blocks; ``start()`` runs it in a thread.
+
+    Concurrency (reference: QuerySchedulerServer running independent jobs at once). Every connection has a
+    handler thread; a request runs under locks of exactly what it touches instead of one global lock:
+      * catalog / planning requests (``LOCAL_OPS``) take no lock and are never broadcast;
+      * set-scoped requests take a readers-writer lock per (db, set) (ScanSets read, WriteSets write for
+        declarative graphs; jobs registered with ``sets=(reads, writes)``), plus the database lock shared;
+        requests of unknown footprint (registered jobs without declared sets, flush, prepared jobs) take the
+        global lock exclusively. Locks are acquired in one sorted order (no lock-order deadlock);
+      * a job runs on a job lane of its own (``PDBClient.job_lane``: its own engine and, on a GPU, its own HIP
+        stream), so jobs on disjoint sets overlap;
+      * with several ranks, every request that runs on all ranks is broadcast and executed in ONE global
+        order (a ticket taken when it is broadcast; such requests run one at a time on every rank), so the
+        collectives of different requests never interleave.
+    """
 
     def __init__(self, client, host: str = "127.0.0.1", port: int = 8108, health=None,
                  jobs: Optional[Dict[str, Callable]] = None, udf_modules: Sequence[str] = ()):
@@ -291,7 +360,14 @@ class PDBFrontend:
         self.registry = UDFRegistry(udf_modules)
         self.dispatcher = Dispatcher(client, self.jobs, health, self.registry)
         self.host, self.port = host, port
-        self.lock = threading.Lock()
+        self.set_locks: Dict[tuple, _RWLock] = {}
+        self._locks_guard = threading.Lock()
+        self.coll_lock = threading.Lock()     # multi-rank: broadcast requests execute one at a time, in order
+        self.set_footprints: Dict[str, tuple] = {}     # registered job -> (reads, writes)
+        self._lanes = itertools.count()
+        self.active = 0
+        self.max_active = 0                   # most requests executing at once (stats / tests)
+        self._active_guard = threading.Lock()
         self._server: Optional[socketserver.ThreadingTCPServer] = None
         self.stopped = threading.Event()
         fe = self
@@ -311,24 +387,98 @@ class PDBFrontend:
 
         self._handler = Handler
 
-    def register_job(self, name: str, fn: Callable):
-        """Expose ``fn(client, **kwargs)`` to remote clients under ``name`` (server-side only)."""
+    def register_job(self, name: str, fn: Callable, sets: Optional[tuple] = None):
+        """Expose ``fn(client, **kwargs)`` to remote clients under ``name`` (server-side only). ``sets`` =
+        (reads, writes), each an iterable of (db, set): the job then runs concurrently with requests on other
+        sets; without it the job takes the global lock."""
         self.jobs[name] = fn
+        if sets is not None:
+            r, w = sets
+            self.set_footprints[name] = (frozenset(map(tuple, r)), frozenset(map(tuple, w)))
         return self
+
+    # ------------------------------------------------------------------ locking
+    def _lock_of(self, key) -> _RWLock:
+        with self._locks_guard:
+            lk = self.set_locks.get(key)
+            if lk is None:
+                lk = self.set_locks[key] = _RWLock()
+            return lk
+
+    def _footprint(self, req) -> List[tuple]:
+        """[(lock key, write)] of a request, sorted: ("*",) global, ("db", name) database, ("set", db, set)."""
+        op = req["op"]
+        if op in LOCAL_OPS or op == "shutdown":
+            return []
+        reads, writes, glob = set(), set(), False
+        if op in ("create_set", "remove_set", "clear_set", "send_data"):
+            writes.add((req.get("db"), req.get("set")))
+        elif op == "get_set":
+            reads.add((req.get("db"), req.get("set")))
+        elif op in ("create_database", "remove_database"):
+            return [(("*",), False), (("db", str(req.get("name"))), True)]
+        elif op == "execute":
+            try:
+                reads, writes = _graph_sets(build_graph(req["graph"], self.registry))
+            except Exception:
+                glob = True
+        elif op == "run" and req.get("job") in self.set_footprints:
+            reads, writes = (set(x) for x in self.set_footprints[req["job"]])
+        else:
+            glob = True
+        if glob:
+            return [(("*",), True)]
+        keys = {("*",): False}
+        for db, st in reads | writes:
+            keys[("db", str(db))] = False
+        for db, st in reads:
+            keys[("set", str(db), str(st))] = keys.get(("set", str(db), str(st)), False)
+        for db, st in writes:
+            keys[("set", str(db), str(st))] = True
+        return sorted(keys.items())
 
     def execute(self, req) -> dict:
         if not isinstance(req, dict) or not isinstance(req.get("op"), str):
             return {"ok": False, "error": "malformed request"}
-        with self.lock:  # requests are serialised: every rank executes them in the same order
-            ctx = self.client.ctx
-            if ctx.distributed:
-                ctx.broadcast_object(req, src=0)
-            if req["op"] == "shutdown":
-                return {"ok": True, "result": True}
+        ctx = self.client.ctx
+        op = req["op"]
+        if op == "shutdown":
+            with self.coll_lock:
+                if ctx.distributed:
+                    ctx.broadcast_object(req, src=0)
+            return {"ok": True, "result": True}
+        fp = self._footprint(req)
+        held = []
+        try:
+            for key, write in fp:
+                lk = self._lock_of(key)
+                lk.acquire(write)
+                held.append((lk, write))
+            broadcast = ctx.distributed and op not in LOCAL_OPS
+            with self._active_guard:
+                self.active += 1
+                self.max_active = max(self.max_active, self.active)
             try:
-                return {"ok": True, "result": self.dispatcher.handle(req)}
-            except Exception as e:
-                return {"ok": False, "error": f"{type(e).__name__}: {e}", "trace": traceback.format_exc()}
+                if broadcast:
+                    # one global order for everything every rank executes: broadcast and run under the same lock
+                    with self.coll_lock:
+                        ctx.broadcast_object(req, src=0)
+                        return {"ok": True, "result": self._run(req)}
+                return {"ok": True, "result": self._run(req)}
+            finally:
+                with self._active_guard:
+                    self.active -= 1
+        except Exception as e:
+            return {"ok": False, "error": f"{type(e).__name__}: {e}", "trace": traceback.format_exc()}
+        finally:
+            for lk, write in reversed(held):
+                lk.release(write)
+
+    def _run(self, req):
+        if req["op"] in LOCAL_OPS:
+            return self.dispatcher.handle(req)
+        with self.client.job_lane(next(self._lanes) % 4):
+            return self.dispatcher.handle(req)
 
     def start(self):
         socketserver.ThreadingTCPServer.allow_reuse_address = True

@@ -182,3 +182,63 @@ def test_remote_prepared_job_cpu(tmp_path):
 @pytest.mark.gpu
 def test_remote_prepared_job_gpu_graph(tmp_path):
     _prepared_roundtrip(tmp_path, "cuda:0")
+
+
+def test_concurrent_requests_long_job_and_catalog_call(tmp_path):
+    """A long job from one client and catalog calls / a job on a disjoint set from a second client overlap in
+    time: requests hold locks of what they touch, not one global lock (reference: QuerySchedulerServer)."""
+    import threading
+
+    from netsdb_amd.examples import employee_jobs
+
+    started, release = threading.Event(), threading.Event()
+    log = []
+
+    def long_job(client, db, seconds=5.0):
+        log.append(("long_start", time.monotonic()))
+        started.set()
+        release.wait(seconds)
+        log.append(("long_end", time.monotonic()))
+        return "done"
+
+    fe = PDBFrontend(PDBClient(root=str(tmp_path)), port=0, jobs=employee_jobs.JOBS).start()
+    fe.register_job("long", long_job, sets=([("db", "emps")], []))
+    rc1 = RemotePDBClient("127.0.0.1", fe.port)
+    rc2 = RemotePDBClient("127.0.0.1", fe.port)
+    rc1.create_database("db")
+    rc1.create_set("db", "emps", "Employee")
+    rc1.create_set("db", "other", "Employee")
+    emps = [Employee(f"e{i}", 20 + i, "eng", 10.0 * i) for i in range(20)]
+    rc1.send_data("db", "emps", emps)
+    out = {}
+    t = threading.Thread(target=lambda: out.setdefault("r", rc1.run("long", db="db")))
+    t.start()
+    assert started.wait(10)
+    t0 = time.monotonic()
+    sets = rc2.list_sets("db")                                   # catalog call while the job runs
+    cat = rc2.print_catalog()
+    rc2.send_data("db", "other", emps[:3])                       # a write to a disjoint set
+    got = rc2.get_set("db", "other")
+    t1 = time.monotonic()
+    assert not release.is_set() and t.is_alive()                 # all of it answered while the job was running
+    release.set()
+    t.join(10)
+    assert out["r"] == "done"
+    assert any(s["name"] == "emps" for s in sets) and "Employee" in cat and len(got) == 3
+    start = dict(log)["long_start"]
+    end = dict(log)["long_end"]
+    assert start < t0 and t1 < end                               # overlap in time
+    assert fe.max_active >= 2
+    # a write to the job's own set waits for the job (per-set writer lock)
+    release.clear()
+    started.clear()
+    t = threading.Thread(target=lambda: rc1.run("long", db="db", seconds=0.5))
+    t.start()
+    assert started.wait(10)
+    tw0 = time.monotonic()
+    rc2.send_data("db", "emps", emps[:1])
+    tw1 = time.monotonic()
+    t.join(10)
+    assert tw1 - tw0 >= 0.3                                      # blocked behind the job that reads emps
+    rc1.shutdown()
+    fe.stopped.wait(5)
