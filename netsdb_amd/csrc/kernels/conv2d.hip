@@ -814,6 +814,306 @@ __global__ void __launch_bounds__(256, 1) conv2d_rowfull_kernel(ConvRowParams p)
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Warp-specialised full-row conv (the default for the headline layer). The phase stamps of
+// conv2d_rowfull_kernel (profiles/r2_s3, r2_write_bw) show its ONE wave per SIMD stalling the MFMAs queued
+// behind a store that finds the CU's memory queue full: 25 K cycles of store issue + 27 K of waiting per wave,
+// on top of 33 K of MFMA and 15 K of epilogue — serialised, not overlapped. Here 8 waves = 2 per SIMD in two roles:
+//  * compute waves 0-3 (one output row x 64 oc each, filter in VGPRs as before) run the 7 pixel tiles one after
+//    the other: 24 MFMAs per tile on 4 accumulator chains (a 16x16x32 bf16 chain issues every 16 cycles even on
+//    one accumulator, so the 28-chain interleave is not needed). The 42 (tile, k-step) A fragments stream from
+//    LDS through a 4-deep register ring, and tile t-2's epilogue (bias seeded in the accumulators, act, bf16
+//    pack, LDS stage) is slotted between tile t's k-steps. 3 x 16 accumulator registers instead of 112: the
+//    wave fits the 256 registers of 2 waves per SIMD;
+//  * store waves 4-7 own every vector-memory instruction: they read the previous group's staged
+//    [64 oc][4 rows x OW] image into registers, release the stage, send it as 8-B stores (each oc's 4-row run
+//    is contiguous in NCHW), then write the next group's input rows (fetched one group earlier) into the other
+//    row buffer as the 4 shifted copies. A store waiting for queue space stalls only its own wave; the MFMAs of
+//    the compute wave on the same SIMD keep issuing.
+// LDS: 2 input-row buffers (double-buffered, so row staging never sits between two compute phases) + ONE output
+// stage. Two barriers per group: top (rows of g staged, stage of g-1 complete) and S (the store waves hold
+// stage g-1 in registers; the compute waves reach it after tile 1, before their first epilogue write).
+constexpr int CVW_STAGE = 64 * CVF_SEGS * 2;                          // [64 oc][segs] bf16
+constexpr int CVW_LDS = 2 * CVR_BUF + CVW_STAGE + CVR_TRASH;
+template <int ACT, bool DIAG>
+__global__ void __launch_bounds__(512, 1) conv2d_ws_kernel(ConvRowParams p) {
+  // DIAG: s_memtime phase stamps per wave (timing build, written over the output). Compute waves: [1] tiles 0-1,
+  // [2] wait at S, [3] tiles 2-6 + epilogues, [4] -, [5] wait at the top barrier. Store waves: [1] stage reads,
+  // [2] wait at S, [3] store issue, [4] row staging (incl. the wait for the fetched rows) + next fetch, [5] wait
+  // at the top barrier.
+  unsigned long long tt[6] = {0, 0, 0, 0, 0, 0}, t_prev = 0;
+  auto stamp = [&](int slot) {
+    if constexpr (DIAG) {
+      unsigned long long t;
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if (slot >= 0) tt[slot] += t - t_prev;
+      t_prev = t;
+    }
+  };
+  stamp(-1);
+  const unsigned long long t_start = t_prev;
+  __shared__ __attribute__((aligned(16))) char smem[CVW_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool is_compute = wave < 4;
+  const int oc0 = blockIdx.y * 64;
+
+  // ---- filter -> LDS (all 512 threads) -> compute waves' VGPRs
+  {
+    const int cpr = p.ldw / 8, nch = 64 * cpr;
+    uint4 v[3];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int e = tid + u * 512;
+      const int r = e / cpr, ch = e - (e / cpr) * cpr;
+      v[u] = make_uint4(0, 0, 0, 0);
+      if (e < nch && oc0 + r < p.OC) v[u] = *reinterpret_cast<const uint4*>(p.Wt + (long long)(oc0 + r) * p.ldw + ch * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int e = tid + u * 512;
+      if (e < nch) reinterpret_cast<uint4*>(smem)[e] = v[u];
+    }
+  }
+  __syncthreads();
+  bf16x8 bw[4][CVR_NKS];
+  float bias_v[4];
+  int abase[CVR_NKS];          // byte offset of k-step ks's A fragment (tile 0) inside a row buffer
+  if (is_compute) {
+    const unsigned short* raw = reinterpret_cast<const unsigned short*>(smem);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int ks = 0; ks < CVR_NKS; ++ks) {
+        const int ocl = nt * 16 + (lane & 15), q = ks * 4 + (lane >> 4);
+#pragma unroll
+        for (int kw = 0; kw < 8; ++kw)
+          bw[nt][ks][kw] = (q < p.ckh && kw < p.KW) ? (short)raw[ocl * p.ldw + q * p.KW + kw] : (short)0;
+      }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int oc = oc0 + nt * 16 + (lane & 15);
+      bias_v[nt] = (p.bias && oc < p.OC) ? p.bias[oc] : 0.f;
+    }
+#pragma unroll
+    for (int ks = 0; ks < CVR_NKS; ++ks) {
+      const int q = ks * 4 + (lane >> 4);
+      if (q < p.ckh) {
+        const int c = q / p.KH, kh = q % p.KH;
+        abase[ks] = ((c * p.rin + wave + kh) * 4 + (lane & 3)) * CVR_CP + (lane & 12) * 2;
+      } else {
+        abase[ks] = CVR_ZERO + (lane & 3) * 16 + (lane & 12) * 2;
+      }
+    }
+  }
+  __syncthreads();                                     // filter reads done: the rows area is free
+  for (int e = tid; e < 2 * (4 * CVR_CP / 16); e += 512) {
+    const int b = e / (4 * CVR_CP / 16), i = e - b * (4 * CVR_CP / 16);
+    reinterpret_cast<uint4*>(smem + b * CVR_BUF + CVR_ZERO)[i] = make_uint4(0, 0, 0, 0);
+  }
+
+  // store waves: input staging work items (c, r, chunk j), <= 2 per store lane, identical for every group
+  const int sl_id = tid - 256;
+  const int items = p.C * p.rin * p.chunks;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned short*>(p.X), (short)0, (int)((long long)p.N * p.C * p.H * p.W * 2), 0x00020000);
+  u32x4 lo[2];         // [item]: the next group's rows, fetched one group ahead
+  u32x2 hi[2];
+  int it_off[2], it_r[2];
+  bool it_lo[2], it_hi[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int it = max(0, min(sl_id + u * 256, items - 1));
+    const int j = it % p.chunks, cr = it / p.chunks, r = cr % p.rin, c = cr / p.rin;
+    it_off[u] = ((c * p.H + r) * p.W + 8 * j) * 2;
+    it_r[u] = r;
+    it_lo[u] = 8 * j < p.W;
+    it_hi[u] = 8 * (j + 1) < p.W;
+  }
+  const int gstep = gridDim.x, gend = p.ngroups;
+  auto fetch = [&](int g) {
+    const bool gok = g < gend;
+    const int n = g / p.groups_per_img, oh0 = (g % p.groups_per_img) * CVR_TR;
+    const int gbase = ((n * p.C * p.H) + oh0) * p.W * 2;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bool rok = gok && oh0 + it_r[u] < p.H;
+      const int o = gbase + it_off[u];
+      lo[u] = __builtin_amdgcn_raw_buffer_load_b128(xr, (rok && it_lo[u]) ? o : 0x7ffffff0, 0, 0);
+      hi[u] = __builtin_amdgcn_raw_buffer_load_b64(xr, (rok && it_hi[u]) ? o + 16 : 0x7ffffff0, 0, 0);
+    }
+  };
+  auto store_rows = [&](char* rb) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int it = sl_id + u * 256;
+      if (it >= items) continue;
+      const int j = it % p.chunks, cr = it / p.chunks;
+      char* row = rb + cr * 4 * CVR_CP + j * 16;
+      const unsigned w[6] = {lo[u].x, lo[u].y, lo[u].z, lo[u].w, hi[u].x, hi[u].y};
+      *reinterpret_cast<u32x4*>(row) = lo[u];
+      *reinterpret_cast<u32x4*>(row + CVR_CP) =
+          u32x4{__builtin_amdgcn_alignbyte(w[1], w[0], 2), __builtin_amdgcn_alignbyte(w[2], w[1], 2),
+                __builtin_amdgcn_alignbyte(w[3], w[2], 2), __builtin_amdgcn_alignbyte(w[4], w[3], 2)};
+      *reinterpret_cast<u32x4*>(row + 2 * CVR_CP) = u32x4{w[1], w[2], w[3], w[4]};
+      *reinterpret_cast<u32x4*>(row + 3 * CVR_CP) =
+          u32x4{__builtin_amdgcn_alignbyte(w[2], w[1], 2), __builtin_amdgcn_alignbyte(w[3], w[2], 2),
+                __builtin_amdgcn_alignbyte(w[4], w[3], 2), __builtin_amdgcn_alignbyte(w[5], w[4], 2)};
+    }
+  };
+
+  const long long OHW = (long long)p.OH * p.OW;
+  const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+      p.out, (short)0, (int)std::min<long long>((long long)p.N * p.OC * OHW * 2, 0x7fffffffLL), 0x00020000);
+  unsigned short* const stage = reinterpret_cast<unsigned short*>(smem + 2 * CVR_BUF);
+  unsigned* const trash = reinterpret_cast<unsigned*>(smem + 2 * CVR_BUF + CVW_STAGE);
+  const int sw = wave - 4;          // store wave index: oc rows sw + 4 j of the stage
+
+  // one output chunk of the staged group: oc (sw + 4 j), 8-byte piece q = lane + 64 h of its rows_valid * OW
+  // run (c = 2 j + h). The per-lane part of the LDS address / global offset is one register per h (rd[h] /
+  // vo[h], set per group); the oc part is an immediate / a scalar offset. Pieces past the run / oc past OC go
+  // to an out-of-range offset (dropped).
+  auto chunk_read = [&](int c, const int (&rd)[2]) -> uint2 {
+    const int j = c >> 1, h = c & 1;
+    return *reinterpret_cast<const uint2*>(stage + (sw + 4 * j) * CVF_SEGS + rd[h]);
+  };
+  auto chunk_store = [&](uint2 v, int c, int obase, const int (&vo)[2], int noc) {
+    const int j = c >> 1, h = c & 1;
+    const int ocl = sw + 4 * j;
+    const int soff = ocl < noc ? obase + (int)(ocl * OHW * 2) : 0x7ffffff0;
+    __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, orsrc, vo[h], soff, 0);
+  };
+  auto lane_offsets = [&](int n4, int (&rd)[2], int (&vo)[2]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int q = lane + 64 * h;
+      rd[h] = 4 * min(q, max(n4, 1) - 1);
+      vo[h] = q < n4 ? 8 * q : 0x7ffffff0;
+    }
+  };
+  // tile t's epilogue for n-tile nt: act -> bf16 pairs -> [oc][row * OW + ow] of the stage (pixel pairs past
+  // OW in the last tile go to the trash word)
+  auto epi = [&](int t, int nt, const f32x4& a) {
+    const int owb = t * 16 + (lane >> 4) * 4;
+    float vv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) vv[r] = act_t<ACT>(a[r]);
+    unsigned* dst = reinterpret_cast<unsigned*>(stage + (nt * 16 + (lane & 15)) * CVF_SEGS + wave * p.OW + owb);
+    if (t + 1 < CVF_NT) {
+      dst[0] = pack_bf16x2(vv[0], vv[1]);
+      dst[1] = pack_bf16x2(vv[2], vv[3]);
+    } else {
+      *(owb + 1 < p.OW ? dst : trash) = pack_bf16x2(vv[0], vv[1]);
+      *(owb + 3 < p.OW ? dst + 1 : trash) = pack_bf16x2(vv[2], vv[3]);
+    }
+  };
+  auto load_frag = [&](const char* rb, int t, int ks) -> bf16x8 {
+    const uint2* src = reinterpret_cast<const uint2*>(__builtin_assume_aligned(rb + abase[ks] + t * 32, 8));
+    const uint2 a0 = src[0], a1 = src[1];
+    return __builtin_bit_cast(bf16x8, u32x4{a0.x, a0.y, a1.x, a1.y});
+  };
+
+  const int noc = min(64, p.OC - oc0);
+  // The two roles run separate loops with the same barrier sequence (top, S per group; one final barrier):
+  // is_compute is wave-uniform, and one loop with role branches inside made hipcc merge the two roles' wait
+  // counters at the joins (the store waves then waited for their own stores to drain before writing rows).
+  if (is_compute) {
+    int par = 0;
+    for (int g = blockIdx.x; g < gend; g += gstep, par ^= 1) {
+      stamp(4);
+      __syncthreads();                                 // top: rows of g staged, stage of g-1 complete
+      stamp(5);
+      const char* const rb = smem + par * CVR_BUF;
+      constexpr int NF = CVF_NT * CVR_NKS, AHEAD = 3, LAG = 2;
+      f32x4 acc[LAG + 1][4];
+      bf16x8 ring[4];
+#pragma unroll
+      for (int f = 0; f < AHEAD; ++f) ring[f] = load_frag(rb, f / CVR_NKS, f % CVR_NKS);
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        const int t = f / CVR_NKS, ks = f % CVR_NKS;
+        __builtin_amdgcn_sched_barrier(0);
+        if (f + AHEAD < NF) ring[(f + AHEAD) & 3] = load_frag(rb, (f + AHEAD) / CVR_NKS, (f + AHEAD) % CVR_NKS);
+        if (ks == 0) {
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) acc[t % (LAG + 1)][nt] = f32x4{bias_v[nt], bias_v[nt], bias_v[nt], bias_v[nt]};
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          acc[t % (LAG + 1)][nt] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring[f & 3], bw[nt][ks], acc[t % (LAG + 1)][nt], 0, 0, 0);
+        if (f == LAG * CVR_NKS - 1) {
+          __builtin_amdgcn_sched_barrier(0);
+          stamp(1);
+          __syncthreads();                             // S: the store waves hold stage g-1 in registers
+          stamp(2);
+        }
+        if (t >= LAG && ks < 4) {
+          __builtin_amdgcn_sched_barrier(0);
+          epi(t - LAG, ks, acc[(t - LAG) % (LAG + 1)][ks]);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = CVF_NT - LAG; t < CVF_NT; ++t)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) epi(t, nt, acc[t % (LAG + 1)][nt]);
+      stamp(3);
+    }
+    __syncthreads();
+  } else {
+    int prev_obase = 0, prev_n4 = 0, par = 0;
+    int g = blockIdx.x;
+    fetch(g);
+    store_rows(smem);
+    fetch(g + gstep);
+    for (; g < gend; g += gstep, par ^= 1) {
+      stamp(4);
+      __syncthreads();                                 // top
+      stamp(5);
+      int rd[2], vo[2];
+      lane_offsets(prev_n4, rd, vo);                   // the stage holds g-1 (first group: every store dropped)
+      uint2 v[32];
+#pragma unroll
+      for (int c = 0; c < 32; ++c) v[c] = chunk_read(c, rd);
+      stamp(1);
+      __syncthreads();                                 // S: stage free for g's epilogues
+      stamp(2);
+#pragma unroll
+      for (int c = 0; c < 32; ++c) chunk_store(v[c], c, prev_obase, vo, noc);
+      stamp(3);
+      store_rows(smem + (par ^ 1) * CVR_BUF);          // rows of g + grid (fetched one group ago)
+      fetch(g + 2 * gstep);                            // behind this group's stores: a whole group to arrive
+      stamp(4);
+      const int n = g / p.groups_per_img, oh0 = (g % p.groups_per_img) * CVR_TR;
+      prev_n4 = (min(CVR_TR, p.OH - oh0) * p.OW) >> 2;
+      prev_obase = (int)((((long long)n * p.OC + oc0) * OHW + (long long)oh0 * p.OW) * 2);
+    }
+    __syncthreads();                                   // the last group's stage is complete
+    if (g != (int)blockIdx.x) {
+      int rd[2], vo[2];
+      lane_offsets(prev_n4, rd, vo);
+      uint2 v[32];
+#pragma unroll
+      for (int c = 0; c < 32; ++c) v[c] = chunk_read(c, rd);
+#pragma unroll
+      for (int c = 0; c < 32; ++c) chunk_store(v[c], c, prev_obase, vo, noc);
+    }
+  }
+  if constexpr (DIAG) {
+    stamp(-1);
+    tt[0] = t_prev - t_start;
+    if (lane == 0) {
+      unsigned long long* d = reinterpret_cast<unsigned long long*>(p.out) + (blockIdx.x * 8 + wave) * 8;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) d[i] = tt[i];
+    }
+  }
+}
+
 // Explicit im2col (the reference's materialised ImageToChunks/ImageBlockToMatrix path, kept for the
 // "materialise" plan and for testing). out[p][k] bf16 with ld = ldk (>= K, zero padded).
 __global__ void im2col_kernel(const unsigned short* X, unsigned short* out, int N, int C, int H, int W,
@@ -902,6 +1202,22 @@ int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* ou
         }
         if (nsdb_conv2d_rowfull == 4) {   // unpipelined stores (A/B)
           hipLaunchKernelGGL((nsdb::conv2d_rowfull_kernel<nsdb::ACT_NONE, false, false>), gridf, dim3(256), 0, stream, q);
+          return (int)hipGetLastError();
+        }
+        if (nsdb_conv2d_rowfull == 6) {   // warp-specialised, phase-stamp timing build (diagnostic)
+          hipLaunchKernelGGL((nsdb::conv2d_ws_kernel<nsdb::ACT_NONE, true>), gridf, dim3(512), 0, stream, q);
+          return (int)hipGetLastError();
+        }
+        if (nsdb_conv2d_rowfull == 5) {   // warp-specialised: 4 compute + 4 store waves per CU
+#define NSDB_CVW_LAUNCH(A) hipLaunchKernelGGL((nsdb::conv2d_ws_kernel<A, false>), gridf, dim3(512), 0, stream, q)
+          switch (act) {
+            case nsdb::ACT_RELU: NSDB_CVW_LAUNCH(nsdb::ACT_RELU); break;
+            case nsdb::ACT_SIGMOID: NSDB_CVW_LAUNCH(nsdb::ACT_SIGMOID); break;
+            case nsdb::ACT_EXP: NSDB_CVW_LAUNCH(nsdb::ACT_EXP); break;
+            case nsdb::ACT_TANH: NSDB_CVW_LAUNCH(nsdb::ACT_TANH); break;
+            default: NSDB_CVW_LAUNCH(nsdb::ACT_NONE); break;
+          }
+#undef NSDB_CVW_LAUNCH
           return (int)hipGetLastError();
         }
         switch (act) {

@@ -245,8 +245,9 @@ def gmm(client, db: str, name: str, k: int, iters: int = 10, init_means: Optiona
     data = RecordBatch.concat(client.get_set_batches(db, name, gather=True)).columns["data"]
     d = data.shape[1]
     dt = data.dtype
-    means = init_means.clone().to(dt) if init_means is not None else data[:k].clone()
-    cov0 = torch.cov(data.T.double()).to(dt) + reg * torch.eye(d, dtype=dt)
+    # model parameters (k x d x d) live on the host; log_resp / the stats UDF move them to the set's device
+    means = (init_means if init_means is not None else data[:k]).detach().cpu().clone().to(dt)
+    cov0 = torch.cov(data.T.double()).cpu().to(dt) + reg * torch.eye(d, dtype=dt)
     model = GmmModel(torch.full((k,), 1.0 / k, dtype=dt), means, cov0.unsqueeze(0).repeat(k, 1, 1).clone())
     lls = []
     for it in range(iters):

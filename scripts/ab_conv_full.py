@@ -1,4 +1,5 @@
-"""A/B of the full-row conv kernel (conv2d_rowfull_kernel) vs the two-pass row kernel and MIOpen on the
+"""A/B of the conv row kernels — warp-specialised (conv2d_ws_kernel, mode 5), full-row (conv2d_rowfull_kernel,
+mode 1), two-pass row kernel (mode 0) — and MIOpen on the
 memfuse headline shape (100 x 3 x 112 x 112, 64 filters 7x7): correctness vs fp32 F.conv2d, then interleaved
 event timing.
 
@@ -20,6 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--stamps", action="store_true", help="also the full-row kernel's phase stamps")
     a = ap.parse_args()
     h = _ext.hip()
     dev = "cuda:0"
@@ -29,11 +31,10 @@ def main():
     Wf = ops.pad_k(W.reshape(64, 147)).to(torch.bfloat16).contiguous()
     bias = torch.randn(64, device=dev, generator=g)
     ref = F.conv2d(X.float(), W.to(torch.bfloat16).float(), bias)
-    variants = {"rowfull": 1, "rowfull_nopipe": 4, "rows": 0, "rowfull_contig": 1}
+    variants = {"warpspec": 5, "rowfull": 1, "rows": 0}
     out = {}
     for name, v in variants.items():
         h.conv2d_rowfull(v)
-        h.conv2d_contig(1 if name == "rowfull_contig" else 0)
         for act, fn in ((ops.ACT_NONE, lambda t: t), (ops.ACT_RELU, torch.relu)):
             y = ops.conv2d(X, Wf, bias, 7, 7, 1, 0, act=act, nchw_out=True).float()
             out[f"{name}_act{act}_rel_err"] = ((y - fn(ref)).abs().max() / ref.abs().max()).item()
@@ -41,18 +42,12 @@ def main():
     h.conv2d_contig(0)
     print(json.dumps(out), flush=True)
     Xm, Wm = X.clone(), W.to(torch.bfloat16)
-    fns = {
-        "rowfull": lambda: ops.conv2d(X, Wf, bias, 7, 7, 1, 0, nchw_out=True),
-        "rowfull_nopipe": lambda: ops.conv2d(X, Wf, bias, 7, 7, 1, 0, nchw_out=True),
-        "rowfull_contig": lambda: ops.conv2d(X, Wf, bias, 7, 7, 1, 0, nchw_out=True),
-        "rows": lambda: ops.conv2d(X, Wf, bias, 7, 7, 1, 0, nchw_out=True),
-        "miopen": lambda: F.conv2d(Xm, Wm, bias.to(torch.bfloat16)),
-    }
+    ours = lambda: ops.conv2d(X, Wf, bias, 7, 7, 1, 0, nchw_out=True)  # noqa: E731
+    fns = {k: ours for k in variants} | {"miopen": lambda: F.conv2d(Xm, Wm, bias.to(torch.bfloat16))}
     ts = {k: [] for k in fns}
     for _ in range(a.rounds):
         for k, fn in fns.items():
-            h.conv2d_rowfull({"rowfull": 1, "rowfull_nopipe": 4, "rowfull_contig": 1}.get(k, 0))
-            h.conv2d_contig(1 if k == "rowfull_contig" else 0)
+            h.conv2d_rowfull(variants.get(k, 1))
             for _ in range(3):
                 fn()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -88,7 +83,33 @@ def stamps(mode=2):
                       "stamps_max": dict(zip(names, [round(float(v)) for v in st.max(0).values]))}), flush=True)
 
 
+def stamps_ws():
+    """Phase stamps of the warp-specialised kernel (conv2d_rowfull(6)): s_memtime cycles per wave, compute waves
+    (0-3) and store waves (4-7) separately."""
+    h = _ext.hip()
+    dev = "cuda:0"
+    X = torch.empty(100, 3, 112, 112, device=dev).uniform_(-1, 1).to(torch.bfloat16)
+    Wf = ops.pad_k(torch.empty(64, 147, device=dev).uniform_(-0.1, 0.1)).to(torch.bfloat16).contiguous()
+    bias = torch.randn(64, device=dev)
+    h.conv2d_rowfull(6)
+    for _ in range(3):
+        y = ops.conv2d(X, Wf, bias, 7, 7, 1, 0, nchw_out=True)
+    torch.cuda.synchronize()
+    st = y.reshape(-1).view(torch.int64)[: 256 * 8 * 8].reshape(256, 8, 8)[:, :, :6].double()
+    h.conv2d_rowfull(5)
+    names = {"compute": ["total", "mfma_loop", "wait_A", "epilogue_t6", "wait_top", "-"],
+             "store": ["total", "stores", "wait_A", "row_staging", "wait_top", "-"]}
+    out = {}
+    for role, sl in (("compute", slice(0, 4)), ("store", slice(4, 8))):
+        r = st[:, sl].reshape(-1, 6)
+        out[role] = {"mean": dict(zip(names[role], [round(float(v)) for v in r.mean(0)])),
+                     "max": dict(zip(names[role], [round(float(v)) for v in r.max(0).values]))}
+    print(json.dumps({"ws_stamps": out}), flush=True)
+
+
 if __name__ == "__main__":
     main()
-    stamps(2)
-    stamps(3)
+    stamps_ws()
+    if "--stamps" in sys.argv:
+        stamps(2)
+        stamps(3)

@@ -235,15 +235,17 @@ def test_gemm_batched_broadcast_b_and_bias_matrix():
     assert (Y - ref).abs().max().item() / ref.abs().max().item() < 1e-4
 
 
-@pytest.mark.parametrize("rowfull", [0, 1], ids=["rows", "rowfull"])
+@pytest.mark.parametrize("rowfull,blocks", [(0, 512), (1, 512), (5, 512), (5, 3)],
+                         ids=["rows", "rowfull", "warpspec", "warpspec-persistent"])
 @pytest.mark.parametrize("cfg", [
     dict(N=3, C=3, H=30, W=112, OC=64, KH=7, KW=7),    # headline geometry (7 pixel tiles per row)
     dict(N=2, C=2, H=14, W=104, OC=70, KH=5, KW=3),    # OW = 102, partial second oc tile, OH % 4 == 2
     dict(N=1, C=3, H=21, W=104, OC=16, KH=7, KW=7),    # OW = 98, one partial oc tile
 ])
-def test_conv2d_rows_bf16_nchw(cfg, rowfull):
-    """The LDS-staged bf16 NCHW output path (what the conv2d job runs): the two-pass row kernel and the full-row
-    kernel (1 wave/SIMD, stores pipelined under the MFMAs) vs the fp32 reference, with a relu epilogue."""
+def test_conv2d_rows_bf16_nchw(cfg, rowfull, blocks):
+    """The LDS-staged bf16 NCHW output path (what the conv2d job runs): the two-pass row kernel, the full-row
+    kernel (1 wave/SIMD, stores pipelined under the MFMAs) and the warp-specialised kernel (compute + store waves;
+    with 3 persistent blocks every block walks several row groups) vs the fp32 reference, with a relu epilogue."""
     from netsdb_amd import _ext
 
     torch.manual_seed(5)
@@ -252,11 +254,13 @@ def test_conv2d_rows_bf16_nchw(cfg, rowfull):
     Wt = ops.pad_k(torch.randn(cfg["OC"], K, device=DEV) * 0.1).to(torch.bfloat16).contiguous()
     bias = torch.randn(cfg["OC"], device=DEV)
     old = _ext.hip().conv2d_rowfull(rowfull)
+    old_b = _ext.hip().conv2d_max_blocks(blocks)
     try:
         y = ops.conv2d(X, Wt, bias, cfg["KH"], cfg["KW"], 1, 0, act=ops.ACT_RELU, nchw_out=True)
         torch.cuda.synchronize()
     finally:
         _ext.hip().conv2d_rowfull(old)
+        _ext.hip().conv2d_max_blocks(old_b)
     assert y.dtype == torch.bfloat16
     ref = ops.conv2d(X.cpu(), Wt.cpu(), bias.cpu(), cfg["KH"], cfg["KW"], 1, 0, act=ops.ACT_RELU, nchw_out=True,
                      out_dtype=torch.float32)
