@@ -90,9 +90,10 @@ def main():
                          "with the max-subtracted softmax in its epilogue); default: the reference's two jobs")
     ap.add_argument("--rownorm-loads", choices=["nt", "plain"], default=None,
                     help="row-normalise row loads: non-temporal (library default) or cache-allocating")
-    ap.add_argument("--conv-kernel", choices=["rows", "rowfull"], default=None,
-                    help="conv2d row kernel: two-pass 2-waves/SIMD (rows) or full-row 1-wave/SIMD with stores "
-                         "pipelined under the MFMAs (rowfull); default: the library default")
+    ap.add_argument("--conv-kernel", choices=["rows", "rowfull", "warpspec"], default=None,
+                    help="conv2d row kernel: two-pass 2-waves/SIMD (rows), full-row 1-wave/SIMD with stores "
+                         "pipelined under the MFMAs (rowfull), or compute + store waves (warpspec); default: the "
+                         "library default")
     ap.add_argument("--conv-blocks", type=int, default=None,
                     help="conv2d row-kernel grid cap (default 512 persistent blocks; tail mode: 0 = one short block "
                          "per row group, so the FF kernels after the GEMM are not held behind persistent conv blocks)")
@@ -137,7 +138,7 @@ def main():
     if args.conv_kernel is not None and dev.type == "cuda":
         from netsdb_amd import _ext
 
-        _ext.hip().conv2d_rowfull(1 if args.conv_kernel == "rowfull" else 0)
+        _ext.hip().conv2d_rowfull({"rows": 0, "rowfull": 1, "warpspec": 5}[args.conv_kernel])
     if args.rownorm_loads is not None and dev.type == "cuda":
         from netsdb_amd import _ext
 

@@ -72,6 +72,7 @@ struct GemmOpts {
   int cfg;
   unsigned* signal;
   unsigned signal_value;
+  int epi;
 };
 
 void check_rc(int rc, const char* what) {
@@ -94,7 +95,7 @@ bool is_f32(const torch::Tensor& t, const char* name) {
 torch::Tensor gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Tensor> bias, int64_t bias_mode,
                       int64_t act, bool out_f32, double alpha, double dropout, int64_t seed, int64_t splits,
                       c10::optional<torch::Tensor> out, bool accumulate, int64_t cfg,
-                      c10::optional<torch::Tensor> signal, int64_t signal_value) {
+                      c10::optional<torch::Tensor> signal, int64_t signal_value, int64_t epi) {
   check_cuda(A, "A");
   check_cuda(B, "B");
   TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && B.scalar_type() == torch::kBFloat16, "A,B must be bf16");
@@ -145,7 +146,8 @@ torch::Tensor gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Ten
     ws = torch::empty({batch * s * M * N}, A.options().dtype(torch::kFloat32));
     wsp = ws.data_ptr<float>();
   }
-  GemmOpts o{(int)cfg, nullptr, 0u};
+  TORCH_CHECK(epi >= -1 && epi <= 1, "gemm_nt: epi must be -1 (auto), 0 (LDS-staged) or 1 (direct)");
+  GemmOpts o{(int)cfg, nullptr, 0u, (int)epi};
   if (signal.has_value() && signal->defined()) {
     check_cuda(*signal, "signal");
     TORCH_CHECK(signal->scalar_type() == torch::kInt32 && signal->numel() >= 1, "signal must be an int32 flag");
@@ -588,7 +590,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bias_mode") = 0, py::arg("act") = 0, py::arg("out_f32") = false, py::arg("alpha") = 1.0,
         py::arg("dropout") = 0.0, py::arg("seed") = 0, py::arg("splits") = 0, py::arg("out") = py::none(),
         py::arg("accumulate") = false, py::arg("cfg") = -1, py::arg("signal") = py::none(),
-        py::arg("signal_value") = 0);
+        py::arg("signal_value") = 0, py::arg("epi") = -1);
   m.def("gemm_nt_f32", &gemm_nt_f32, "alpha * A.B^T (+C) on the exact-f32 MFMA (16x16x4)", py::arg("A"),
         py::arg("B"), py::arg("alpha") = 1.0, py::arg("out") = py::none(), py::arg("accumulate") = false);
   m.def("gemm_splits", &gemm_splits, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("batch") = 1,

@@ -860,60 +860,6 @@ __global__ void __launch_bounds__(512, 1) conv2d_ws_kernel(ConvRowParams p) {
   const bool is_compute = wave < 4;
   const int oc0 = blockIdx.y * 64;
 
-  // ---- filter -> LDS (all 512 threads) -> compute waves' VGPRs
-  {
-    const int cpr = p.ldw / 8, nch = 64 * cpr;
-    uint4 v[3];
-#pragma unroll
-    for (int u = 0; u < 3; ++u) {
-      const int e = tid + u * 512;
-      const int r = e / cpr, ch = e - (e / cpr) * cpr;
-      v[u] = make_uint4(0, 0, 0, 0);
-      if (e < nch && oc0 + r < p.OC) v[u] = *reinterpret_cast<const uint4*>(p.Wt + (long long)(oc0 + r) * p.ldw + ch * 8);
-    }
-#pragma unroll
-    for (int u = 0; u < 3; ++u) {
-      const int e = tid + u * 512;
-      if (e < nch) reinterpret_cast<uint4*>(smem)[e] = v[u];
-    }
-  }
-  __syncthreads();
-  bf16x8 bw[4][CVR_NKS];
-  float bias_v[4];
-  int abase[CVR_NKS];          // byte offset of k-step ks's A fragment (tile 0) inside a row buffer
-  if (is_compute) {
-    const unsigned short* raw = reinterpret_cast<const unsigned short*>(smem);
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-      for (int ks = 0; ks < CVR_NKS; ++ks) {
-        const int ocl = nt * 16 + (lane & 15), q = ks * 4 + (lane >> 4);
-#pragma unroll
-        for (int kw = 0; kw < 8; ++kw)
-          bw[nt][ks][kw] = (q < p.ckh && kw < p.KW) ? (short)raw[ocl * p.ldw + q * p.KW + kw] : (short)0;
-      }
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      const int oc = oc0 + nt * 16 + (lane & 15);
-      bias_v[nt] = (p.bias && oc < p.OC) ? p.bias[oc] : 0.f;
-    }
-#pragma unroll
-    for (int ks = 0; ks < CVR_NKS; ++ks) {
-      const int q = ks * 4 + (lane >> 4);
-      if (q < p.ckh) {
-        const int c = q / p.KH, kh = q % p.KH;
-        abase[ks] = ((c * p.rin + wave + kh) * 4 + (lane & 3)) * CVR_CP + (lane & 12) * 2;
-      } else {
-        abase[ks] = CVR_ZERO + (lane & 3) * 16 + (lane & 12) * 2;
-      }
-    }
-  }
-  __syncthreads();                                     // filter reads done: the rows area is free
-  for (int e = tid; e < 2 * (4 * CVR_CP / 16); e += 512) {
-    const int b = e / (4 * CVR_CP / 16), i = e - b * (4 * CVR_CP / 16);
-    reinterpret_cast<uint4*>(smem + b * CVR_BUF + CVR_ZERO)[i] = make_uint4(0, 0, 0, 0);
-  }
-
   // store waves: input staging work items (c, r, chunk j), <= 2 per store lane, identical for every group
   const int sl_id = tid - 256;
   const int items = p.C * p.rin * p.chunks;
@@ -963,6 +909,74 @@ __global__ void __launch_bounds__(512, 1) conv2d_ws_kernel(ConvRowParams p) {
                 __builtin_amdgcn_alignbyte(w[4], w[3], 2), __builtin_amdgcn_alignbyte(w[5], w[4], 2)};
     }
   };
+
+  // ---- prologue. The store waves request group 0's input rows first; meanwhile every thread copies the filter
+  // panel into the (still unused) output stage and the compute waves pick their fragments out of it, while the
+  // store waves write the rows into row buffer 0 and request group 1's (the loop's first top barrier joins them).
+  if (!is_compute) fetch(blockIdx.x);
+  char* const fstage = smem + 2 * CVR_BUF;
+  {
+    const int cpr = p.ldw / 8, nch = 64 * cpr;
+    uint4 v[3];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int e = tid + u * 512;
+      const int r = e / cpr, ch = e - (e / cpr) * cpr;
+      v[u] = make_uint4(0, 0, 0, 0);
+      if (e < nch && oc0 + r < p.OC) v[u] = *reinterpret_cast<const uint4*>(p.Wt + (long long)(oc0 + r) * p.ldw + ch * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int e = tid + u * 512;
+      if (e < nch) reinterpret_cast<uint4*>(fstage)[e] = v[u];
+    }
+  }
+  __syncthreads();
+  bf16x8 bw[4][CVR_NKS];
+  float bias_v[4];
+  int abase[CVR_NKS];          // byte offset of k-step ks's A fragment (tile 0) inside a row buffer
+  if (is_compute) {
+    // branch-free: every read is issued (clamped inside the oc's row) and out-of-range taps are selected to
+    // zero afterwards — a conditional read per element made hipcc wrap each in its own exec-masked branch with
+    // its own wait (~190 serialised LDS round trips, ~6 us of prologue)
+    const unsigned short* raw = reinterpret_cast<const unsigned short*>(fstage);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int ks = 0; ks < CVR_NKS; ++ks) {
+        const int ocl = nt * 16 + (lane & 15), q = ks * 4 + (lane >> 4);
+        const bool qok = q < p.ckh;
+        const int rbase = ocl * p.ldw + min(q, p.ckh - 1) * p.KW;
+        short v[8];
+#pragma unroll
+        for (int kw = 0; kw < 8; ++kw) v[kw] = (short)raw[rbase + min(kw, p.KW - 1)];
+#pragma unroll
+        for (int kw = 0; kw < 8; ++kw) bw[nt][ks][kw] = (qok && kw < p.KW) ? v[kw] : (short)0;
+      }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int oc = oc0 + nt * 16 + (lane & 15);
+      bias_v[nt] = (p.bias && oc < p.OC) ? p.bias[oc] : 0.f;
+    }
+#pragma unroll
+    for (int ks = 0; ks < CVR_NKS; ++ks) {
+      const int q = ks * 4 + (lane >> 4);
+      if (q < p.ckh) {
+        const int c = q / p.KH, kh = q % p.KH;
+        abase[ks] = ((c * p.rin + wave + kh) * 4 + (lane & 3)) * CVR_CP + (lane & 12) * 2;
+      } else {
+        abase[ks] = CVR_ZERO + (lane & 3) * 16 + (lane & 12) * 2;
+      }
+    }
+  }
+  if (!is_compute) {
+    for (int e = sl_id; e < 2 * (4 * CVR_CP / 16); e += 256) {
+      const int b = e / (4 * CVR_CP / 16), i = e - b * (4 * CVR_CP / 16);
+      reinterpret_cast<uint4*>(smem + b * CVR_BUF + CVR_ZERO)[i] = make_uint4(0, 0, 0, 0);
+    }
+    store_rows(smem);
+    fetch(blockIdx.x + gstep);
+  }
 
   const long long OHW = (long long)p.OH * p.OW;
   const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
@@ -1067,9 +1081,6 @@ __global__ void __launch_bounds__(512, 1) conv2d_ws_kernel(ConvRowParams p) {
   } else {
     int prev_obase = 0, prev_n4 = 0, par = 0;
     int g = blockIdx.x;
-    fetch(g);
-    store_rows(smem);
-    fetch(g + gstep);
     for (; g < gend; g += gstep, par ^= 1) {
       stamp(4);
       __syncthreads();                                 // top
@@ -1148,8 +1159,10 @@ int nsdb_conv2d_variant = 0;         // row-kernel diagnostics (timing only)
 // 0 = one block per row group (short-lived blocks that the dispatcher can interleave with higher-priority
 // kernels when the conv shares the GPU with another job, e.g. gated into a GEMM's tail)
 int nsdb_conv2d_max_blocks = 512;
-int nsdb_conv2d_rowfull = 1;
-int nsdb_conv2d_contig = 0;          // full-row kernel: contiguous row-group runs per block (A/B)         // full-row kernel for 97 <= OW <= 112 (0: the two-pass row kernel, A/B)
+// row-kernel choice for 97 <= OW <= 112: 5 = warp-specialised (default), 1 = full-row, 0 = two-pass; 2/3/4/6 are
+// diagnostics (phase stamps, unpipelined stores)
+int nsdb_conv2d_rowfull = 5;
+int nsdb_conv2d_contig = 0;          // full-row kernel: contiguous row-group runs per block (A/B)
 
 int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* out, int N, int C, int H,
                       int W, int OC, int KH, int KW, int stride, int pad, int dil, int ldw, int act,

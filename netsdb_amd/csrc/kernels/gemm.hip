@@ -237,6 +237,81 @@ __global__ void __launch_bounds__(256) softmax_fixup_kernel(GemmParams p) {
   if (tid == 0) p.sm_flag[tile] = 0;
 }
 
+// Direct epilogue of the unsplit 8-phase tile: every lane stores its own accumulators, 4 consecutive columns
+// of one row per (i, j) (the transposed TS layout: acc[i][j][r] = C[wr*128 + i*16 + rl][wc*64 + j*16 + cq + r]),
+// i.e. one 16-B (f32) / 8-B (bf16) store per lane and a wave instruction of 16 rows x 64 B. No LDS image, no
+// barrier, no per-pass wait: the store_tile_lds path spends two LDS passes (4 of the 8 waves' f32 tiles fit
+// its 128 KiB) with a barrier and an LDS-read -> store dependency per iteration, and the FF output layer's
+// all-at-once tail (228 tiles ending together) paid ~2x the bare store stream for it (scripts/native/
+// store_gemm2: 10-12 us for the 58 MB stream either way). Bias (per row / per column) is loaded into
+// registers before the first store (a load behind stores waits for them: vmcnt is in order).
+__device__ __forceinline__ void store_direct_8ph(const f32x4 (&acc)[8][4], const GemmParams& p, int batch, int m0,
+                                                 int n0, int lane, int wave) {
+  const int wr = wave >> 2, wc = wave & 3;
+  const int rl = lane & 15, cq = (lane >> 4) * 4;
+  const float* bias = p.bias ? p.bias + batch * p.sBias : nullptr;
+  const float keep_scale = p.dropout > 0.f ? 1.f / (1.f - p.dropout) : 1.f;
+  f32x4 bc[4];
+  float br[8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    bc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int col = n0 + wc * 64 + j * 16 + cq;
+    if (bias && p.bias_mode == 2 && col < p.N) {
+      const float* bp = bias + col;
+      if (col + 3 < p.N && ((reinterpret_cast<uintptr_t>(bp) & 15) == 0)) bc[j] = *reinterpret_cast<const f32x4*>(bp);
+      else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bc[j][r] = bp[min(r, p.N - 1 - col)];
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = m0 + wr * 128 + i * 16 + rl;
+    br[i] = (bias && p.bias_mode == 1 && row < p.M) ? bias[row] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = m0 + wr * 128 + i * 16 + rl;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n0 + wc * 64 + j * 16 + cq;
+      f32x4 w;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float x = apply_act_compact(acc[i][j][r] * p.alpha + br[i] + bc[j][r], p.act);
+        if (p.dropout > 0.f) {
+          const unsigned long long idx = ((unsigned long long)batch * p.M + row) * p.N + col + r;
+          x = hash_uniform(p.seed, idx) < p.dropout ? 0.f : x * keep_scale;
+        }
+        w[r] = x;
+      }
+      if (row < p.M && col < p.N) {
+        const long long off = batch * p.sC + (long long)row * p.ldc + col;
+        const int nv = min(4, p.N - col);
+        if (p.out_f32) {
+          float* d = reinterpret_cast<float*>(p.C) + off;
+          if (nv == 4) *reinterpret_cast<f32x4*>(d) = w;
+          else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (r < nv) d[r] = w[r];
+          }
+        } else {
+          unsigned short* d = reinterpret_cast<unsigned short*>(p.C) + off;
+          if (nv == 4) *reinterpret_cast<uint2*>(d) = make_uint2(pack_bf16x2(w[0], w[1]), pack_bf16x2(w[2], w[3]));
+          else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (r < nv) d[r] = f32_to_bf16(w[r]);
+          }
+        }
+      }
+    }
+  }
+}
+
 // TBM x TBN tile, WGM x WGN waves; each wave owns (TBM/WGM) x (TBN/WGN) = TM x TN 16x16 MFMA tiles.
 //   <128,128,2,2>: 256 threads, 64 KiB LDS, 2 blocks/CU (general shapes)
 //   <256,256,2,4>: 512 threads, 128 KiB LDS, 1 block/CU, 128x64 per wave = 32 MFMAs per k-substep:
@@ -247,7 +322,7 @@ gemm_nt_tile_kernel(GemmParams p) {
   constexpr int NW = WGM * WGN;
   constexpr int TM = TBM / WGM / 16, TN = TBN / WGN / 16;
   constexpr int A_BYTES = TBM * BK * 2, B_BYTES = TBN * BK * 2, STG = A_BYTES + B_BYTES;
-  __shared__ __attribute__((aligned(16))) char smem[2 * STG];
+  __shared__ __attribute__((aligned(16))) char smem[2 * STG + 1024];   // + the epilogue's bias (store_tile_lds)
 
   // 1-D grid over (split, tile); the bijective XCD remap hands every XCD a contiguous run of
   // work ids, split-major: with splits a multiple of 8 each XCD owns whole K-slices, so the A and
@@ -319,7 +394,8 @@ gemm_nt_tile_kernel(GemmParams p) {
     __syncthreads();
   }
 
-  store_tile_lds<TBM, TBN, WGM, WGN>(acc, smem, 2 * STG, p, batch, split, m0, n0, tid, lane, wave);
+  store_tile_lds<TBM, TBN, WGM, WGN>(acc, smem, 2 * STG, p, batch, split, m0, n0, tid, lane, wave,
+                                     reinterpret_cast<float*>(smem + 2 * STG));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -368,7 +444,7 @@ template <int EPI>
 __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   constexpr int HALF = 128 * 128;            // bytes of one half-tile (128 rows x 64 bf16)
   constexpr int BUF = 4 * HALF;              // one K-tile
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF + 1024];   // + the epilogue's bias (store_tile_lds)
 
   const int ntiles = p.tiles_m * p.tiles_n;
   const int wg = xcd_remap(blockIdx.x, ntiles * p.splits);
@@ -506,10 +582,15 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
     softmax_epilogue_8ph<EPI>(acc, smem, (int)sizeof(smem), p, m0, n0, tm, tn, tid, lane, wave);
     GemmParams q = p;
     q.alpha = 1.f; q.bias = nullptr; q.act = 0; q.dropout = 0.f; q.accumulate = 0; q.out_f32 = 1; q.splits = 1;
-    store_tile_lds<256, 256, 2, 4, true>(acc, smem, (int)sizeof(smem), q, 0, 0, m0, n0, tid, lane, wave);
+    store_tile_lds<256, 256, 2, 4, true>(acc, smem, 2 * BUF, q, 0, 0, m0, n0, tid, lane, wave);
     return;
   }
-  store_tile_lds<256, 256, 2, 4, true>(acc, smem, (int)sizeof(smem), p, batch, split, m0, n0, tid, lane, wave);
+  if (p.direct_epi) {
+    store_direct_8ph(acc, p, batch, m0, n0, lane, wave);
+    return;
+  }
+  store_tile_lds<256, 256, 2, 4, true>(acc, smem, 2 * BUF, p, batch, split, m0, n0, tid, lane, wave,
+                                       reinterpret_cast<float*>(smem + 2 * BUF));
 }
 
 
@@ -602,6 +683,7 @@ struct GemmOpts {
   int cfg;                  // -1 auto, 0 = 128x128 tile kernel, 2 = 256x256 8-phase kernel
   unsigned* signal;         // tail trigger of this launch (8-phase only), or nullptr
   unsigned signal_value;
+  int epi;                  // 8-phase unsplit epilogue: -1 auto (direct), 0 LDS-staged, 1 direct register stores
 };
 
 extern "C" {
@@ -685,6 +767,7 @@ int nsdb_gemm_nt_softmax(const void* A, const void* B, float* C, const float* bi
   p.vec_c = (ldc % 4 == 0 && (reinterpret_cast<uintptr_t>(C) & 15) == 0) ? 1 : 0;
   p.softmax = axis; p.sm_part = (float2*)part; p.sm_cnt = cnt; p.sm_flag = flag; p.stamps = nullptr; p.adapt = nullptr;
   p.signal = nullptr; p.signal_value = 0; p.steal_cnt = nullptr; p.steal_tq = 0; p.steal_ch = 2;
+  p.direct_epi = 0;
   const int tiles = p.tiles_m * p.tiles_n;
   if (axis == 1) hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<1>, dim3(tiles), dim3(512), 0, stream, p);
   else hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<2>, dim3(tiles), dim3(512), 0, stream, p);
@@ -731,6 +814,10 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
   p.vec_ws = (N % 4 == 0) ? 1 : 0;
   p.vec_c = (ldc % 4 == 0 && sC % 4 == 0 &&
              (reinterpret_cast<uintptr_t>(C) & (out_f32 ? 15 : 7)) == 0) ? 1 : 0;
+  // the direct register epilogue for unsplit 8-phase launches with aligned C rows (opts->epi: -1 auto = direct,
+  // 0 = LDS-staged, 1 = direct); split-K slabs, C += A.B^T and per-element bias keep the LDS-staged epilogue
+  const int epi_pref = opts ? opts->epi : -1;
+  p.direct_epi = (cfg == 2 && p.splits == 1 && !accumulate && p.vec_c && p.bias_mode != 3 && epi_pref != 0) ? 1 : 0;
   dim3 grid(p.tiles_m * p.tiles_n * p.splits, 1, batch);
   if (cfg == 2) {
     if (opts && opts->signal) {            // this launch's tail trigger (the caller checked eligibility)

@@ -52,6 +52,9 @@ struct GemmParams {
   // them) for the steal_tq tail chunks of steal_ch k-tiles at the end of every split's K range
   int* steal_cnt;
   int steal_tq, steal_ch;       // tail chunks per split, k-tiles per chunk (nsdb_gemm_steal)
+  // 8-phase kernel, unsplit launches: store C straight from the accumulator registers (no LDS round trip;
+  // see store_direct_8ph in gemm.hip). 0: the LDS-staged store_tile_lds epilogue.
+  int direct_epi;
 };
 
 // Adaptive split-K partition (8-phase kernel, split-K launches). The splits of one GEMM run on different XCDs
@@ -126,7 +129,7 @@ __device__ __forceinline__ bf16x8 read_frag(const char* lds_tile, int row, int c
 template <int TBM, int TBN, int WGM, int WGN, bool TSL = false>
 __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[TBM / WGM / 16][TBN / WGN / 16], char* smem,
                                                int smem_bytes, const GemmParams& p, int batch, int split, int m0,
-                                               int n0, int tid, int lane, int wave) {
+                                               int n0, int tid, int lane, int wave, float* lds_bias = nullptr) {
   constexpr int NW = WGM * WGN, TM = TBM / WGM / 16, TN = TBN / WGN / 16;
   constexpr int WR = TBM / WGM, WC = TBN / WGN, WTILE = WR * WC;
   static_assert(WC >= 32, "swizzle needs >= 32 columns per wave tile");
@@ -136,6 +139,14 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[TBM / WGM / 16
   const float* bias = p.bias ? p.bias + batch * p.sBias : nullptr;
   const float keep_scale = p.dropout > 0.f ? 1.f / (1.f - p.dropout) : 1.f;
   float* ws = p.splits > 1 ? p.ws + ((long long)batch * p.splits + split) * (long long)p.M * p.N : nullptr;
+  // Per-row / per-column bias of the tile staged in LDS (lds_bias: >= max(TBM, TBN) floats, 16-B aligned) before
+  // any store is issued. A global bias load inside the store loop waits on vmcnt, which also counts the stores
+  // issued before it (in-order counter): the output stream then drained once per iteration.
+  const bool lbias = lds_bias && bias && !ws && (p.bias_mode == 1 || p.bias_mode == 2);
+  if (lbias) {
+    const int nb = p.bias_mode == 1 ? TBM : TBN, base = p.bias_mode == 1 ? m0 : n0, lim = p.bias_mode == 1 ? p.M : p.N;
+    for (int i = tid; i < nb; i += 64 * NW) lds_bias[i] = base + i < lim ? bias[base + i] : 0.f;
+  }
   for (int g0 = 0; g0 < NW; g0 += per_pass) {
     __syncthreads();
     if (wave >= g0 && wave < g0 + per_pass) {
@@ -190,7 +201,14 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[TBM / WGM / 16
         cc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
         if (ws || !okk[k]) continue;
         const int nv = min(4, p.N - col);
-        if (bias) {
+        if (lbias) {
+          if (p.bias_mode == 1) {
+            const float b = lds_bias[(wv / WGN) * WR + r];
+            bb[k] = f32x4{b, b, b, b};
+          } else {
+            bb[k] = *reinterpret_cast<const f32x4*>(lds_bias + (wv % WGN) * WC + c);
+          }
+        } else if (bias) {
           if (p.bias_mode == 1) {
             const float b = bias[row];
             bb[k] = f32x4{b, b, b, b};

@@ -81,10 +81,11 @@ def gemm_operands(A, B):
 
 
 def gemm_nt(A, B, bias=None, bias_mode=BIAS_NONE, act=ACT_NONE, out_dtype=torch.bfloat16, alpha=1.0,
-            dropout=0.0, seed=0, splits=0, out=None, accumulate=False, cfg=None):
+            dropout=0.0, seed=0, splits=0, out=None, accumulate=False, cfg=None, epi=None):
     """epilogue(alpha * A @ B^T) [+ out when accumulate]: A [..,M,K], B [..,N,K] (K-contiguous),
     bias f32 per row/col. ``accumulate`` adds into an existing f32 ``out`` (C += A.B^T). ``cfg`` forces the
-    tile config of THIS call (0 = 128x128, 2 = 256x256 8-phase; None = auto). A tail trigger armed on the
+    tile config of THIS call (0 = 128x128, 2 = 256x256 8-phase; None = auto); ``epi`` the 8-phase kernel's
+    unsplit epilogue (0 = LDS-staged, 1 = direct register stores; None = auto: direct). A tail trigger armed on the
     current stream (execution/streams.TailTrigger) is handed to this launch when the launch is long enough to
     take it — per call and per stream, so GEMMs on other lanes or threads never see it."""
     act = act_code(act)
@@ -105,7 +106,7 @@ def gemm_nt(A, B, bias=None, bias_mode=BIAS_NONE, act=ACT_NONE, out_dtype=torch.
                 sig, sval = trig.take()
         return h.gemm_nt(A, B, bias, int(bias_mode if bias is not None else 0), act,
                          out_dtype == torch.float32, float(alpha), float(dropout), int(seed),
-                         int(splits), out, bool(accumulate), c, sig, int(sval))
+                         int(splits), out, bool(accumulate), c, sig, int(sval), -1 if epi is None else int(epi))
     v = torch.matmul(A.float(), B.float().transpose(-1, -2)) * alpha
     if bias is not None:
         b = bias.float()

@@ -38,7 +38,7 @@ def main():
         for act, fn in ((ops.ACT_NONE, lambda t: t), (ops.ACT_RELU, torch.relu)):
             y = ops.conv2d(X, Wf, bias, 7, 7, 1, 0, act=act, nchw_out=True).float()
             out[f"{name}_act{act}_rel_err"] = ((y - fn(ref)).abs().max() / ref.abs().max()).item()
-    h.conv2d_rowfull(1)
+    h.conv2d_rowfull(5)
     h.conv2d_contig(0)
     print(json.dumps(out), flush=True)
     Xm, Wm = X.clone(), W.to(torch.bfloat16)
@@ -47,7 +47,7 @@ def main():
     ts = {k: [] for k in fns}
     for _ in range(a.rounds):
         for k, fn in fns.items():
-            h.conv2d_rowfull(variants.get(k, 1))
+            h.conv2d_rowfull(variants.get(k, 5))
             for _ in range(3):
                 fn()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -57,7 +57,7 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             ts[k].append(e0.elapsed_time(e1) / a.iters * 1000)
-    h.conv2d_rowfull(1)
+    h.conv2d_rowfull(5)
     h.conv2d_contig(0)
     print(json.dumps({f"{k}_us_min": round(min(v), 1) for k, v in ts.items()} |
                      {f"{k}_us_med": round(sorted(v)[len(v) // 2], 1) for k, v in ts.items()}), flush=True)
@@ -77,7 +77,7 @@ def stamps(mode=2):
         y = ops.conv2d(X, Wf, bias, 7, 7, 1, 0, nchw_out=True)
     torch.cuda.synchronize()
     st = y.reshape(-1).view(torch.int64)[: 256 * 4 * 8].reshape(256 * 4, 8)[:, :6].double()
-    h.conv2d_rowfull(1)
+    h.conv2d_rowfull(5)
     names = ["total", "mfma", "epilogue", "mid_barrier", "stores", "rows+top_barrier"]
     print(json.dumps({"mode": mode, "stamps_mean": dict(zip(names, [round(float(v)) for v in st.mean(0)])),
                       "stamps_max": dict(zip(names, [round(float(v)) for v in st.max(0).values]))}), flush=True)
@@ -97,8 +97,8 @@ def stamps_ws():
     torch.cuda.synchronize()
     st = y.reshape(-1).view(torch.int64)[: 256 * 8 * 8].reshape(256, 8, 8)[:, :, :6].double()
     h.conv2d_rowfull(5)
-    names = {"compute": ["total", "mfma_loop", "wait_A", "epilogue_t6", "wait_top", "-"],
-             "store": ["total", "stores", "wait_A", "row_staging", "wait_top", "-"]}
+    names = {"compute": ["total", "tiles_0_1", "wait_S", "tiles_2_6_epilogues", "prologue", "wait_top"],
+             "store": ["total", "stage_reads", "wait_S", "store_issue", "row_staging_and_prologue", "wait_top"]}
     out = {}
     for role, sl in (("compute", slice(0, 4)), ("store", slice(4, 8))):
         r = st[:, sl].reshape(-1, 6)

@@ -61,6 +61,32 @@ def test_gemm_epilogue(mode, act, splits, gemm_cfg):
     _close(Cb, _ref_gemm(A, B, bias, mode, act), tol=2e-2)
 
 
+@pytest.mark.parametrize("M,N,K", [(300, 200, 640), (1000, 1030, 1000), (257, 514, 64)])
+@pytest.mark.parametrize("mode,act,dropout", [(0, ops.ACT_NONE, 0.0), (1, ops.ACT_RELU, 0.0), (2, ops.ACT_EXP, 0.0),
+                                              (2, ops.ACT_SIGMOID, 0.3)])
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+def test_gemm_8ph_direct_epilogue_matches_lds_staged(M, N, K, mode, act, dropout, out_dtype):
+    """The 8-phase kernel's direct register epilogue (epi=1, default for unsplit launches) and its LDS-staged
+    epilogue (epi=0) write the same values (same fp32 math, same dropout hash), ragged edges included; both
+    against the fp32 reference."""
+    torch.manual_seed(7)
+    A = (torch.randn(M, K, device=DEV) * 0.05).to(torch.bfloat16)
+    B = (torch.randn(N, K, device=DEV) * 0.05).to(torch.bfloat16)
+    bias = torch.randn(M if mode == 1 else N, device=DEV) if mode else None
+    kw = dict(bias=bias, bias_mode=mode, act=act, out_dtype=out_dtype, dropout=dropout, seed=99, splits=1, cfg=2)
+    Cd = ops.gemm_nt(A, B, epi=1, **kw)
+    Cl = ops.gemm_nt(A, B, epi=0, **kw)
+    torch.testing.assert_close(Cd, Cl, rtol=0, atol=0)
+    if dropout == 0.0:
+        _close(Cd, _ref_gemm(A, B, bias, mode, act), tol=2e-2)
+    # ldc-padded output (a column slice of a wider buffer), as the FF output layer writes it
+    wide = torch.full((M, (N + 63) // 64 * 64), -7.0, device=DEV, dtype=out_dtype)
+    view = wide[:, :N]
+    ops.gemm_nt(A, B, out=view, epi=1, **kw)
+    torch.testing.assert_close(view, Cl, rtol=0, atol=0)
+    assert (wide[:, N:] == -7.0).all()
+
+
 def test_gemm_batched_strided():
     torch.manual_seed(2)
     A = torch.randn(3, 130, 200, device=DEV).to(torch.bfloat16)[:, :, :192]   # row stride 200 > K
