@@ -169,17 +169,20 @@ __device__ __forceinline__ void softmax_epilogue_8ph(f32x4 (&acc)[8][4], char* s
   // loads batched 8 deep), or this tile's own max on the fallback path
   float* fin = st;                                     // [256][2] (the wave stats are consumed)
   if (ok) {
+    // 16 partials in flight per thread (two threads per row, every other tile each): the partials were written
+    // by other XCDs, so each batch is a full round trip past L2 — one batch covers a row-block of up to 32 tiles
+    // (the FF output layer: 57 tiles -> 2 round trips instead of 4 with 8 in flight)
     const int e = tid & 255, half = tid >> 8;
     float m = -INFINITY, s = 0.f;
-    for (int t0 = half; t0 < need; t0 += 16) {
-      float2 v[8];
+    for (int t0 = half; t0 < need; t0 += 32) {
+      float2 v[16];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
+      for (int q = 0; q < 16; ++q) {
         const int t = t0 + 2 * q;
         v[q] = t < need ? part[t * 256 + e] : make_float2(-INFINITY, 0.f);
       }
 #pragma unroll
-      for (int q = 0; q < 8; ++q) sm_combine(m, s, v[q].x, v[q].y);
+      for (int q = 0; q < 16; ++q) sm_combine(m, s, v[q].x, v[q].y);
     }
     float* h2 = st + 1024;
     if (half == 1) { h2[e * 2] = m; h2[e * 2 + 1] = s; }
@@ -582,7 +585,8 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
     softmax_epilogue_8ph<EPI>(acc, smem, (int)sizeof(smem), p, m0, n0, tm, tn, tid, lane, wave);
     GemmParams q = p;
     q.alpha = 1.f; q.bias = nullptr; q.act = 0; q.dropout = 0.f; q.accumulate = 0; q.out_f32 = 1; q.splits = 1;
-    store_tile_lds<256, 256, 2, 4, true>(acc, smem, 2 * BUF, q, 0, 0, m0, n0, tid, lane, wave);
+    if (p.direct_epi) store_direct_8ph(acc, q, 0, m0, n0, lane, wave);
+    else store_tile_lds<256, 256, 2, 4, true>(acc, smem, 2 * BUF, q, 0, 0, m0, n0, tid, lane, wave);
     return;
   }
   if (p.direct_epi) {
@@ -748,7 +752,7 @@ int nsdb_gemm_tail_eligible(int M, int N, int K, int batch, int splits, int cfg)
 // every tile takes the non-co-resident fallback path.
 int nsdb_gemm_nt_softmax(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, long long lda,
                          long long ldb, long long ldc, int bias_mode, float alpha, int axis, void* part, int* cnt,
-                         int* flag, int force_fallback, hipStream_t stream) {
+                         int* flag, int force_fallback, int epi, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
   if (K % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0 || (axis != 1 && axis != 2)) return -1;
   if (256LL * lda * 2 >= 0x7ffffff0LL || 256LL * ldb * 2 >= 0x7ffffff0LL) return -2;
@@ -767,7 +771,7 @@ int nsdb_gemm_nt_softmax(const void* A, const void* B, float* C, const float* bi
   p.vec_c = (ldc % 4 == 0 && (reinterpret_cast<uintptr_t>(C) & 15) == 0) ? 1 : 0;
   p.softmax = axis; p.sm_part = (float2*)part; p.sm_cnt = cnt; p.sm_flag = flag; p.stamps = nullptr; p.adapt = nullptr;
   p.signal = nullptr; p.signal_value = 0; p.steal_cnt = nullptr; p.steal_tq = 0; p.steal_ch = 2;
-  p.direct_epi = 0;
+  p.direct_epi = p.vec_c && epi != 0 ? 1 : 0;      // final values straight from registers (store_direct_8ph)
   const int tiles = p.tiles_m * p.tiles_n;
   if (axis == 1) hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<1>, dim3(tiles), dim3(512), 0, stream, p);
   else hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<2>, dim3(tiles), dim3(512), 0, stream, p);

@@ -160,10 +160,12 @@ def _pad_k4(X):
     return Y
 
 
-def gemm_nt_softmax(A, B, bias=None, bias_mode=BIAS_NONE, axis=1, alpha=1.0, out=None, force_fallback=False):
+def gemm_nt_softmax(A, B, bias=None, bias_mode=BIAS_NONE, axis=1, alpha=1.0, out=None, force_fallback=False,
+                    epi=None):
     """softmax(alpha * A @ B^T + bias) along ``axis`` 1 (each row of the [M, N] result) or 2 (each column), f32.
     On the GPU the normalisation is fused into the GEMM epilogue (max-subtracted, no exp'd round trip through
-    HBM); the CPU oracle is the same max-subtracted softmax in fp32."""
+    HBM; ``epi`` 0 = LDS-staged final store, 1 / None = direct register stores when C rows are 16-B aligned);
+    the CPU oracle is the same max-subtracted softmax in fp32."""
     if _use_hip(A, B):
         if bias is not None and bias.dtype != torch.float32:
             bias = bias.float()
@@ -178,7 +180,7 @@ def gemm_nt_softmax(A, B, bias=None, bias_mode=BIAS_NONE, axis=1, alpha=1.0, out
             A = torch.nn.functional.pad(A, (0, k - A.shape[-1])) if A.shape[-1] < k else A
             B = torch.nn.functional.pad(B, (0, k - B.shape[-1])) if B.shape[-1] < k else B
         return _ext.hip().gemm_nt_softmax(A, B, bias, int(bias_mode if bias is not None else 0), int(axis), out,
-                                          float(alpha), bool(force_fallback))
+                                          float(alpha), bool(force_fallback), -1 if epi is None else int(epi))
     v = torch.matmul(A.float(), B.float().transpose(-1, -2)) * alpha
     if bias is not None:
         b = bias.float()

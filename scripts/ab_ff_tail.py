@@ -50,6 +50,7 @@ def main():
         "two_job_total": lambda: ops.row_normalize(
             ops.gemm_nt(H, W, bias, ops.BIAS_COL, ops.ACT_EXP, out_dtype=torch.float32, out=outp), out_dtype=torch.float32),
         "fused_softmax_gemm": lambda: ops.gemm_nt_softmax(H, W, bias, ops.BIAS_COL, axis=1, out=sm_out),
+        "fused_softmax_gemm_ldsepi": lambda: ops.gemm_nt_softmax(H, W, bias, ops.BIAS_COL, axis=1, out=sm_out, epi=0),
         "gemm2_bf16_nobias": lambda: ops.gemm_nt(H, W),
     }
     ts = {k: [] for k in fns}

@@ -65,16 +65,20 @@ def test_softmax_gemm_cpu_oracle_is_safe():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("epi", [None, 0], ids=["direct", "lds"])
 @pytest.mark.parametrize("axis", [1, 2])
 @pytest.mark.parametrize("shape,mode", [((300, 700, 96), ops.BIAS_COL), ((777, 555, 4104), ops.BIAS_ROW),
-                                        ((256, 256, 64), None), ((1000, 14588, 1000), ops.BIAS_COL)])
-def test_softmax_gemm_vs_fp32(shape, mode, axis):
+                                        ((256, 256, 64), None), ((1000, 14588, 1000), ops.BIAS_COL),
+                                        ((300, 701, 64), ops.BIAS_COL)])
+def test_softmax_gemm_vs_fp32(shape, mode, axis, epi):
+    """Direct register stores (C rows 16-B aligned; N = 701 falls back to the LDS-staged store) and the
+    LDS-staged final store."""
     M, N, K = shape
     g = torch.Generator(device="cuda:0").manual_seed(1)
     A = (torch.rand(M, K, device="cuda:0", generator=g) * 0.2).to(torch.bfloat16)
     B = (torch.randn(N, K, device="cuda:0", generator=g) / K ** 0.5).to(torch.bfloat16)
     bias = None if mode is None else torch.randn(M if mode == ops.BIAS_ROW else N, device="cuda:0", generator=g)
-    y = ops.gemm_nt_softmax(A, B, bias, mode or ops.BIAS_NONE, axis=axis)
+    y = ops.gemm_nt_softmax(A, B, bias, mode or ops.BIAS_NONE, axis=axis, epi=epi)
     ref = _ref(A, B, bias, mode, axis)
     assert y.shape == (M, N) and y.dtype == torch.float32
     err = ((y - ref).abs().max() / ref.abs().max()).item()
