@@ -97,6 +97,9 @@ def main():
     ap.add_argument("--conv-blocks", type=int, default=None,
                     help="conv2d row-kernel grid cap (default 512 persistent blocks; tail mode: 0 = one short block "
                          "per row group, so the FF kernels after the GEMM are not held behind persistent conv blocks)")
+    ap.add_argument("--tail-prefetch", action="store_true",
+                    help="read the output layer's weight into the Infinity Cache during layer 1's tail "
+                         "(execution/streams.TailPrefetch; measured slower, off by default)")
     ap.add_argument("--inflight", type=int, default=1,
                     help="FF steps in flight: step i's FF jobs go to job lane i %% inflight (>1 pipelines "
                          "consecutive batches: step i+1's layer-1 GEMM starts while step i's tail kernels run)")
@@ -116,6 +119,7 @@ def main():
     root = tempfile.mkdtemp(prefix=f"nsdb_bench_r{ctx.rank}_")
     client = PDBClient(ctx=ctx, root=root, device=ctx.device)
     dev = ctx.device
+    client.engine.tail_prefetch = bool(args.tail_prefetch)
 
     # ---- data (per-rank partition of the inputs, replicated model) ----
     ff.load_model(client, "ff", cfg["batch"] * ctx.world_size, cfg["features"], cfg["hidden"], cfg["labels"],
@@ -256,6 +260,7 @@ def main():
                 "collectives_per_step": round(coll_per_step, 2),
                 "graph_replay": captured is not None,
                 "single_job": bool(args.single_job),
+                "tail_prefetch": bool(args.tail_prefetch),
             },
         }
         print(json.dumps(res), flush=True)

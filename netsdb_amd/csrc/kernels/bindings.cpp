@@ -33,6 +33,7 @@ extern int nsdb_conv2d_max_blocks;
 extern int nsdb_conv2d_rowfull;
 extern int nsdb_conv2d_contig;
 extern int nsdb_rownorm_plain_loads;
+int nsdb_prefetch(const void* ptr, long long bytes, unsigned* sink, int blocks, hipStream_t stream);
 int nsdb_im2col(const void* X, void* out, int N, int C, int H, int W, int KH, int KW, int stride, int pad, int dil,
                 int ldk, hipStream_t stream);
 int nsdb_softmax_rows(const void* X, int x_f32, const float* bias, void* Y, int y_f32, int R, int N,
@@ -344,6 +345,20 @@ torch::Tensor im2col(torch::Tensor X, int64_t KH, int64_t KW, int64_t stride, in
   return out;
 }
 
+// Cache warm-up read of each tensor's storage bytes on the current stream (ops.prefetch).
+void prefetch(std::vector<torch::Tensor> ts, torch::Tensor sink, int64_t blocks) {
+  check_cuda(sink, "sink");
+  TORCH_CHECK(sink.scalar_type() == torch::kInt32 && sink.numel() >= 1, "sink must be an int32 scratch word");
+  for (auto& t : ts) {
+    if (!t.defined() || t.numel() == 0) continue;
+    check_cuda(t, "prefetch tensor");
+    long long span = 1;                  // elements from the first to the last one the view addresses
+    for (int64_t d = 0; d < t.dim(); ++d) span += (t.size(d) - 1) * std::abs(t.stride(d));
+    check_rc(nsdb_prefetch(t.data_ptr(), span * (long long)t.element_size(),
+                           reinterpret_cast<unsigned*>(sink.data_ptr()), (int)blocks, cur_stream()), "prefetch");
+  }
+}
+
 torch::Tensor softmax_rows(torch::Tensor X, c10::optional<torch::Tensor> bias, bool out_f32, int64_t mode) {
   check_cuda(X, "X");
   TORCH_CHECK(X.dim() == 2 && X.stride(-1) == 1, "X must be 2-D row-contiguous");
@@ -592,6 +607,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dropout") = 0.0, py::arg("seed") = 0, py::arg("splits") = 0, py::arg("out") = py::none(),
         py::arg("accumulate") = false, py::arg("cfg") = -1, py::arg("signal") = py::none(),
         py::arg("signal_value") = 0, py::arg("epi") = -1);
+  m.def("prefetch", &prefetch, "warm the caches with a read of each tensor", py::arg("tensors"), py::arg("sink"),
+        py::arg("blocks") = 64);
   m.def("gemm_nt_f32", &gemm_nt_f32, "alpha * A.B^T (+C) on the exact-f32 MFMA (16x16x4)", py::arg("A"),
         py::arg("B"), py::arg("alpha") = 1.0, py::arg("out") = py::none(), py::arg("accumulate") = false);
   m.def("gemm_splits", &gemm_splits, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("batch") = 1,

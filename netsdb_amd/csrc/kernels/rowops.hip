@@ -196,6 +196,26 @@ __global__ void __launch_bounds__(256) embedding_bag_kernel(const TT* table, con
 
 static int grid_for(long long n) { return (int)std::min<long long>((n + 255) / 256, 8192); }
 
+namespace nsdb {
+
+// Cache warm-up read: every 128-B line of [base, base + bytes) is loaded once (16 B per lane, a 2 KiB stride
+// per wave instruction keeps each load on its own line group) so a consumer launched later finds it in the
+// Infinity Cache (MALL) instead of HBM. The loaded words are folded into one value that is stored to a scratch
+// word only when it equals a host-chosen key (keeps the loads live; the store almost never happens and only
+// touches the scratch word). Few workgroups: it runs in CUs another kernel's tail leaves idle.
+__global__ void __launch_bounds__(256) prefetch_kernel(const char* base, long long bytes, unsigned* sink,
+                                                       unsigned key) {
+  const long long lines = bytes >> 7;
+  unsigned acc = 0;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long l = (long long)blockIdx.x * blockDim.x + threadIdx.x; l < lines; l += stride) {
+    const uint4 v = *reinterpret_cast<const uint4*>(base + (l << 7));
+    acc ^= v.x ^ v.w;
+  }
+  if (acc == key) sink[0] = acc;
+}
+}  // namespace nsdb
+
 extern "C" {
 
 int nsdb_rownorm_plain_loads = 0;   // A/B knob of row_normalize_vec_kernel's row load policy
@@ -280,6 +300,14 @@ int nsdb_embedding_bag(const void* table, int t_f32, const long long* idx, const
   else
     hipLaunchKernelGGL((nsdb::embedding_bag_kernel<unsigned short>), dim3(blocks), dim3(256), 0, st,
                        (const unsigned short*)table, idx, offsets, weights, out, Bn, D, mode);
+  return (int)hipGetLastError();
+}
+
+// Warm the caches with a read of [ptr, ptr + bytes) (prefetch_kernel) on `stream`; blocks <= 0: 64.
+int nsdb_prefetch(const void* ptr, long long bytes, unsigned* sink, int blocks, hipStream_t stream) {
+  if (bytes <= 0) return 0;
+  hipLaunchKernelGGL(nsdb::prefetch_kernel, dim3(blocks > 0 ? blocks : 64), dim3(256), 0, stream,
+                     reinterpret_cast<const char*>(ptr), bytes, sink, 0x9e3779b9u);
   return (int)hipGetLastError();
 }
 

@@ -108,6 +108,10 @@ class QueryEngine:
         # streaming shuffle (execution/shuffle.py): chunk size per round and cumulative round statistics
         self.shuffle_chunk_bytes = 64 << 20
         self.shuffle_stats = {}
+        # fused GEMM chains: read a later GEMM's stored weight into the Infinity Cache during the tail of the GEMM
+        # evaluated before it (query_planning/fusion.py MatmulNode._tail_prefetch). Off by default: measured
+        # slower in the bench (profiles/r3_s2: 1.021 vs 0.992 ms per step)
+        self.tail_prefetch = False
         self.last_tcap = None
         self._last_comps = None
 
@@ -115,7 +119,7 @@ class QueryEngine:
         """An engine for another job lane: same storage, context, catalog, tracer, configuration and plan cache
         (dict access under the GIL); its own per-job state (spools, statistics)."""
         e = QueryEngine(self.storage, self.ctx, self.catalog, self.tracer, self.broadcast_threshold, self.fusion)
-        for k in ("adaptive", "plan_cache_enabled", "ooc_fraction", "shuffle_chunk_bytes"):
+        for k in ("adaptive", "plan_cache_enabled", "ooc_fraction", "shuffle_chunk_bytes", "tail_prefetch"):
             setattr(e, k, getattr(self, k))
         e._plan_cache = self._plan_cache
         e.__dict__["meta_cache"] = self.__dict__.setdefault("meta_cache", {})

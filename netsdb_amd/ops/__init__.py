@@ -280,6 +280,23 @@ def im2col(X, KH, KW, stride=1, pad=0, dil=1, ldk=None):
     return torch.nn.functional.pad(cols, (0, ldk - K)).to(X.dtype)
 
 
+_PREFETCH_SINK = {}
+
+
+def prefetch(tensors, blocks=64):
+    """Warm the GPU caches (Infinity Cache) with a read of each tensor on the current stream (HIP prefetch_kernel:
+    one 16-B load per 128-B line, nothing written). For operands a later kernel reads after a cache-flushing
+    one (the FF output weights after layer 1's 2.4 GB stream). CPU tensors: no-op."""
+    ts = [t for t in tensors if isinstance(t, torch.Tensor) and t.is_cuda and t.numel()]
+    if not ts:
+        return
+    dev = ts[0].device
+    sink = _PREFETCH_SINK.get(dev)
+    if sink is None:
+        sink = _PREFETCH_SINK[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
+    _ext.hip().prefetch(ts, sink, int(blocks))
+
+
 def softmax_rows(X, bias=None, out_dtype=torch.float32, log=False):
     if _use_hip(X):
         return _ext.hip().softmax_rows(X, bias, out_dtype == torch.float32, 1 if log else 0)

@@ -148,7 +148,41 @@ class MatmulNode(Node):
     def eval(self, engine) -> Dense:
         if self.value is not None:
             return self.value
+        pf = self._tail_prefetch(engine)
         A, B = self.a.eval(engine), self.b.eval(engine)
+        if pf is not None:
+            pf.launched()
+        try:
+            return self._eval(engine, A, B)
+        finally:
+            if pf is not None:
+                pf.end()
+
+    def _tail_prefetch(self, engine):
+        """One operand is a stored weight set and the other comes out of a GEMM evaluated first (the FF output
+        layer after layer 1): warm the weight into the Infinity Cache during that GEMM's tail
+        (streams.TailPrefetch). Engine option ``tail_prefetch`` (default off: measured slower in the bench)."""
+        if not getattr(engine, "tail_prefetch", False) or engine.ctx.distributed:
+            return None
+        srcs = [c for c in (self.a, self.b) if isinstance(c, SourceNode)]
+        heavy = [c for c in (self.a, self.b) if isinstance(c, (MatmulNode, BiasActNode, EwiseNode))]
+        if len(srcs) != 1 or len(heavy) != 1:
+            return None
+        try:
+            w = srcs[0].eval(engine).phys
+        except Exception:
+            return None
+        if not isinstance(w, torch.Tensor) or not w.is_cuda or w.numel() * w.element_size() < (4 << 20):
+            return None
+        pf = engine.__dict__.get("_tail_prefetch")
+        if pf is None:
+            from ..execution.streams import TailPrefetch
+
+            pf = engine.__dict__["_tail_prefetch"] = TailPrefetch(w.device)
+        extra = [self.bias.eval(engine).phys] if self.bias is not None and isinstance(self.bias, SourceNode) else []
+        return pf if pf.begin([w] + [t for t in extra if isinstance(t, torch.Tensor)]) else None
+
+    def _eval(self, engine, A: Dense, B: Dense) -> Dense:
         opA = A.t() if self.p.transpose_a else A           # [M, K]
         opB = B.t() if self.p.transpose_b else B           # [K, N]
         # distribution (one rank per GPU): M-split A / N-split B are local; a K-split of B against

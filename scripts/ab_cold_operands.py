@@ -2,7 +2,7 @@
 (100 x 3 x 112^2, 64 filters 7x7): in the bench both run right after the layer-1 GEMM has streamed 2.4 GB
 through the Infinity Cache, so their operands come from HBM; in isolated A/B loops they are cache-hot. Each
 timed call here follows (a) a 1 GiB read that evicts the cache ('cold'), (b) the same read and then a plain
-read of just the call's operands ('prefetched'), (c) nothing ('hot'). Event timing of the call alone.
+ops.prefetch of just the call's operands ('prefetched'), (c) nothing ('hot'). Event timing of the call alone.
 
     python scripts/ab_cold_operands.py [--rounds 5]
 """
@@ -32,12 +32,11 @@ def main():
     Wf = ops.pad_k(torch.empty(64, 147, device=dev).uniform_(-0.1, 0.1, generator=g)).to(torch.bfloat16).contiguous()
     cb = torch.randn(64, device=dev, generator=g)
     big = torch.empty(512 << 20, device=dev, dtype=torch.bfloat16).uniform_(-1, 1, generator=g)   # 1 GiB
-    sink = torch.empty(4, device=dev)
 
     calls = {
         "gemm2": (lambda: ops.gemm_nt(H, W, bias, ops.BIAS_COL, ops.ACT_EXP, out_dtype=torch.float32, out=outp),
-                  lambda: (torch.sum(W, out=sink[0]), torch.sum(H, out=sink[1]))),
-        "conv": (lambda: ops.conv2d(X, Wf, cb, 7, 7, 1, 0, nchw_out=True), lambda: torch.sum(X, out=sink[2])),
+                  lambda: ops.prefetch([W, H, bias])),
+        "conv": (lambda: ops.conv2d(X, Wf, cb, 7, 7, 1, 0, nchw_out=True), lambda: ops.prefetch([X])),
     }
     res = {f"{k}_{m}": [] for k in calls for m in ("cold", "prefetched", "hot")}
     for _ in range(a.rounds):
@@ -48,7 +47,7 @@ def main():
                 ts = []
                 for _ in range(5):
                     if mode != "hot":
-                        torch.sum(big, out=sink[3])
+                        big.sum()          # result discarded: the read is the point
                     if mode == "prefetched":
                         pre()
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
