@@ -26,7 +26,7 @@ int nsdb_gemm_nt_f32(const float* A, const float* B, float* C, int M, int N, int
                      long long ldc, float alpha, int accumulate, hipStream_t stream);
 int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* out, int N, int C, int H, int W,
                       int OC, int KH, int KW, int stride, int pad, int dil, int ldw, int act, int nchw_out,
-                      int out_f32, hipStream_t stream);
+                      int out_f32, const void* wfrag, hipStream_t stream);
 extern int nsdb_conv2d_force_generic;
 extern int nsdb_conv2d_variant;
 extern int nsdb_conv2d_max_blocks;
@@ -304,7 +304,8 @@ int64_t gemm_splits(int64_t M, int64_t N, int64_t K, int64_t batch, int64_t cfg)
 }
 
 torch::Tensor conv2d(torch::Tensor X, torch::Tensor Wt, c10::optional<torch::Tensor> bias, int64_t KH, int64_t KW,
-                     int64_t stride, int64_t pad, int64_t dil, int64_t act, bool nchw_out, bool out_f32) {
+                     int64_t stride, int64_t pad, int64_t dil, int64_t act, bool nchw_out, bool out_f32,
+                     c10::optional<torch::Tensor> wfrag) {
   check_cuda(X, "X");
   check_cuda(Wt, "W");
   TORCH_CHECK(X.scalar_type() == torch::kBFloat16 && Wt.scalar_type() == torch::kBFloat16, "X,W must be bf16");
@@ -322,11 +323,18 @@ torch::Tensor conv2d(torch::Tensor X, torch::Tensor Wt, c10::optional<torch::Ten
     check_cuda(*bias, "bias");
     bptr = bias->data_ptr<float>();
   }
+  const void* fptr = nullptr;      // MFMA B-fragment packed filter (ops.conv_filter_fragments): [ceil(OC/64)][4][6][64][8]
+  if (wfrag.has_value() && wfrag->defined()) {
+    check_cuda(*wfrag, "wfrag");
+    TORCH_CHECK(wfrag->scalar_type() == torch::kBFloat16 && wfrag->is_contiguous() &&
+                    wfrag->numel() == ((OC + 63) / 64) * 4 * 6 * 64 * 8, "wfrag must be the packed [OC/64][4][6][64][8] filter");
+    fptr = wfrag->data_ptr();
+  }
   auto opts = X.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16);
   torch::Tensor out = nchw_out ? torch::empty({N, OC, OH, OW}, opts) : torch::empty({N * OH * OW, OC}, opts);
   check_rc(nsdb_conv2d_igemm(X.data_ptr(), Wt.data_ptr(), bptr, out.data_ptr(), (int)N, (int)C, (int)H, (int)W,
                              (int)OC, (int)KH, (int)KW, (int)stride, (int)pad, (int)dil, (int)ldw, (int)act,
-                             nchw_out ? 1 : 0, out_f32 ? 1 : 0, cur_stream()),
+                             nchw_out ? 1 : 0, out_f32 ? 1 : 0, fptr, cur_stream()),
            "conv2d");
   return out;
 }
@@ -637,7 +645,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv2d_variant", [](int64_t v) { nsdb_conv2d_variant = (int)v; }, "row-kernel diagnostic variant");
   m.def("conv2d", &conv2d, py::arg("X"), py::arg("W"), py::arg("bias") = py::none(), py::arg("KH") = 1,
         py::arg("KW") = 1, py::arg("stride") = 1, py::arg("pad") = 0, py::arg("dil") = 1, py::arg("act") = 0,
-        py::arg("nchw_out") = false, py::arg("out_f32") = false);
+        py::arg("nchw_out") = false, py::arg("out_f32") = false, py::arg("wfrag") = py::none());
   m.def("im2col", &im2col);
   m.def("softmax_rows", &softmax_rows, py::arg("X"), py::arg("bias") = py::none(), py::arg("out_f32") = true,
         py::arg("mode") = 0);

@@ -234,6 +234,8 @@ struct ConvRowParams {
   int segs, vec8;  // staged output: LDS run stride per oc (elements); 8-B output chunks allowed
   int contig;      // full-row kernel: each block walks a contiguous run of row groups (same image, consecutive
                    // rows: every plane's output grows as one sequential stream) instead of a grid stride
+  const unsigned short* Wfrag;   // warp-specialised kernel: the filter pre-packed in MFMA B-fragment order
+                                 // [OC/64][4 n-tiles][6 k-steps][64 lanes][8] bf16 (ops.conv_filter_fragments)
   int variant;   // diagnostics (bit flags, timing only): 1 no global stores, 2 no MFMA, 4 no LDS output
                  // staging, 8 prologue only, 16 no compute, 32 s_memtime stamps over the output
 };
@@ -910,49 +912,21 @@ __global__ void __launch_bounds__(512, 1) conv2d_ws_kernel(ConvRowParams p) {
     }
   };
 
-  // ---- prologue. The store waves request group 0's input rows first; meanwhile every thread copies the filter
-  // panel into the (still unused) output stage and the compute waves pick their fragments out of it, while the
-  // store waves write the rows into row buffer 0 and request group 1's (the loop's first top barrier joins them).
+  // ---- prologue. The store waves request group 0's input rows first and write them into row buffer 0 while the
+  // compute waves load their filter fragments; the loop's first top barrier joins them.
   if (!is_compute) fetch(blockIdx.x);
-  char* const fstage = smem + 2 * CVR_BUF;
-  {
-    const int cpr = p.ldw / 8, nch = 64 * cpr;
-    uint4 v[3];
-#pragma unroll
-    for (int u = 0; u < 3; ++u) {
-      const int e = tid + u * 512;
-      const int r = e / cpr, ch = e - (e / cpr) * cpr;
-      v[u] = make_uint4(0, 0, 0, 0);
-      if (e < nch && oc0 + r < p.OC) v[u] = *reinterpret_cast<const uint4*>(p.Wt + (long long)(oc0 + r) * p.ldw + ch * 8);
-    }
-#pragma unroll
-    for (int u = 0; u < 3; ++u) {
-      const int e = tid + u * 512;
-      if (e < nch) reinterpret_cast<uint4*>(fstage)[e] = v[u];
-    }
-  }
-  __syncthreads();
+  // filter fragments straight from the pre-packed tensor: one 16-B load per (n-tile, k-step) and lane (no LDS
+  // staging, no per-element extraction: a few dozen instructions of prologue instead of ~700 — on a cold
+  // instruction cache the prologue's code size, not its work, was its cost)
   bf16x8 bw[4][CVR_NKS];
   float bias_v[4];
   int abase[CVR_NKS];          // byte offset of k-step ks's A fragment (tile 0) inside a row buffer
   if (is_compute) {
-    // branch-free: every read is issued (clamped inside the oc's row) and out-of-range taps are selected to
-    // zero afterwards — a conditional read per element made hipcc wrap each in its own exec-masked branch with
-    // its own wait (~190 serialised LDS round trips, ~6 us of prologue)
-    const unsigned short* raw = reinterpret_cast<const unsigned short*>(fstage);
+    const uint4* wf = reinterpret_cast<const uint4*>(p.Wfrag) + (long long)blockIdx.y * 4 * CVR_NKS * 64 + lane;
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
-      for (int ks = 0; ks < CVR_NKS; ++ks) {
-        const int ocl = nt * 16 + (lane & 15), q = ks * 4 + (lane >> 4);
-        const bool qok = q < p.ckh;
-        const int rbase = ocl * p.ldw + min(q, p.ckh - 1) * p.KW;
-        short v[8];
-#pragma unroll
-        for (int kw = 0; kw < 8; ++kw) v[kw] = (short)raw[rbase + min(kw, p.KW - 1)];
-#pragma unroll
-        for (int kw = 0; kw < 8; ++kw) bw[nt][ks][kw] = (qok && kw < p.KW) ? v[kw] : (short)0;
-      }
+      for (int ks = 0; ks < CVR_NKS; ++ks) bw[nt][ks] = __builtin_bit_cast(bf16x8, wf[(nt * CVR_NKS + ks) * 64]);
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       const int oc = oc0 + nt * 16 + (lane & 15);
@@ -1166,7 +1140,7 @@ int nsdb_conv2d_contig = 0;          // full-row kernel: contiguous row-group ru
 
 int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* out, int N, int C, int H,
                       int W, int OC, int KH, int KW, int stride, int pad, int dil, int ldw, int act,
-                      int nchw_out, int out_f32, hipStream_t stream) {
+                      int nchw_out, int out_f32, const void* wfrag, hipStream_t stream) {
   nsdb::ConvParams p;
   p.X = (const unsigned short*)X; p.Wt = (const unsigned short*)Wt; p.bias = bias; p.out = out;
   p.N = N; p.C = C; p.H = H; p.W = W; p.OC = OC; p.KH = KH; p.KW = KW;
@@ -1191,6 +1165,7 @@ int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* ou
     q.ngroups = N * q.groups_per_img;
     q.act = act; q.nchw_out = nchw_out; q.out_f32 = out_f32; q.variant = nsdb_conv2d_variant;
     q.contig = nsdb_conv2d_contig;
+    q.Wfrag = (const unsigned short*)wfrag;
     q.segs = (4 * p.OW + 3) & ~3;
     if ((q.segs / 2) % 4 == 0) q.segs += 4;
     q.vec8 = ((long long)p.OH * p.OW) % 4 == 0 && (reinterpret_cast<uintptr_t>(out) & 7) == 0;
@@ -1217,11 +1192,11 @@ int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* ou
           hipLaunchKernelGGL((nsdb::conv2d_rowfull_kernel<nsdb::ACT_NONE, false, false>), gridf, dim3(256), 0, stream, q);
           return (int)hipGetLastError();
         }
-        if (nsdb_conv2d_rowfull == 6) {   // warp-specialised, phase-stamp timing build (diagnostic)
+        if (nsdb_conv2d_rowfull == 6 && wfrag != nullptr) {   // warp-specialised, phase-stamp timing build (diagnostic)
           hipLaunchKernelGGL((nsdb::conv2d_ws_kernel<nsdb::ACT_NONE, true>), gridf, dim3(512), 0, stream, q);
           return (int)hipGetLastError();
         }
-        if (nsdb_conv2d_rowfull == 5) {   // warp-specialised: 4 compute + 4 store waves per CU
+        if (nsdb_conv2d_rowfull == 5 && wfrag != nullptr) {   // warp-specialised: 4 compute + 4 store waves per CU
 #define NSDB_CVW_LAUNCH(A) hipLaunchKernelGGL((nsdb::conv2d_ws_kernel<A, false>), gridf, dim3(512), 0, stream, q)
           switch (act) {
             case nsdb::ACT_RELU: NSDB_CVW_LAUNCH(nsdb::ACT_RELU); break;

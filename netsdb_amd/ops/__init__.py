@@ -250,6 +250,32 @@ def pad_k(t: torch.Tensor, mult: int = 8) -> torch.Tensor:
     return torch.nn.functional.pad(t, (0, kp - k))
 
 
+def conv_filter_fragments(Wflat, C, KH, KW):
+    """The filter [OC, >=C*KH*KW] (im2col (c, kh, kw) order) re-laid in the warp-specialised conv kernel's MFMA
+    B-fragment order: [ceil(OC/64)][4 n-tiles][6 k-steps][64 lanes][8] bf16, lane l of n-tile nt / k-step ks
+    holding oc = 64 t + 16 nt + (l & 15), taps kw = 0..7 of filter row q = 4 ks + (l >> 4) (q = c * KH + kh),
+    zero past KW / C*KH / OC. The kernel then loads each fragment with one 16-B read (conv2d.hip conv2d_ws_kernel)."""
+    OC = Wflat.shape[0]
+    ckh = C * KH
+    oct_ = (OC + 63) // 64
+    dev = Wflat.device
+    nt = torch.arange(4, device=dev).view(4, 1, 1, 1)
+    ks = torch.arange(6, device=dev).view(1, 6, 1, 1)
+    ln = torch.arange(64, device=dev).view(1, 1, 64, 1)
+    kw = torch.arange(8, device=dev).view(1, 1, 1, 8)
+    ocl = nt * 16 + (ln & 15)
+    q = ks * 4 + (ln >> 4)
+    kidx = (q.clamp(max=max(ckh - 1, 0)) * KW + kw.clamp(max=KW - 1)).expand(4, 6, 64, 8)
+    valid = ((q < ckh) & (kw < KW)).expand(4, 6, 64, 8)
+    Wp = torch.zeros(oct_ * 64, Wflat.shape[1], dtype=torch.bfloat16, device=dev)
+    Wp[:OC] = Wflat.to(torch.bfloat16)
+    out = []
+    for t in range(oct_):
+        rows = (t * 64 + ocl).expand(4, 6, 64, 8)
+        out.append(torch.where(valid, Wp[rows, kidx], torch.zeros((), dtype=torch.bfloat16, device=dev)))
+    return torch.stack(out).contiguous()
+
+
 def conv2d(X, Wflat, bias=None, KH=1, KW=1, stride=1, pad=0, dil=1, act=ACT_NONE, nchw_out=False,
            out_dtype=torch.bfloat16):
     """Fused implicit-GEMM conv. X [N,C,H,W]; Wflat [OC, >=C*KH*KW] in (c,kh,kw) im2col order."""
@@ -257,8 +283,13 @@ def conv2d(X, Wflat, bias=None, KH=1, KW=1, stride=1, pad=0, dil=1, act=ACT_NONE
     if _use_hip(X, Wflat):
         if bias is not None and bias.dtype != torch.float32:
             bias = bias.float()
+        C = X.shape[1]
+        wfrag = None
+        if stride == 1 and dil == 1 and pad == 0 and KW <= 8 and C * KH <= 24:
+            # small-C row-kernel shapes: the packed B fragments (cached per filter tensor and version)
+            wfrag = derived(Wflat, f"conv_frag_{C}_{KH}_{KW}", lambda t: conv_filter_fragments(t, C, KH, KW))
         return _ext.hip().conv2d(X, Wflat, bias, KH, KW, stride, pad, dil, act, bool(nchw_out),
-                                 out_dtype == torch.float32)
+                                 out_dtype == torch.float32, wfrag)
     N, C = X.shape[0], X.shape[1]
     OC = Wflat.shape[0]
     w = Wflat[:, : C * KH * KW].float().reshape(OC, C, KH, KW)

@@ -38,16 +38,19 @@ def main():
                   lambda: ops.prefetch([W, H, bias])),
         "conv": (lambda: ops.conv2d(X, Wf, cb, 7, 7, 1, 0, nchw_out=True), lambda: ops.prefetch([X])),
     }
-    res = {f"{k}_{m}": [] for k in calls for m in ("cold", "prefetched", "hot")}
+    modes = ("cold", "prefetched", "hot", "after_write")
+    res = {f"{k}_{m}": [] for k in calls for m in modes}
     for _ in range(a.rounds):
         for k, (fn, pre) in calls.items():
-            for mode in ("cold", "prefetched", "hot"):
+            for mode in modes:
                 for _ in range(3):
                     fn()
                 ts = []
                 for _ in range(5):
-                    if mode != "hot":
+                    if mode in ("cold", "prefetched"):
                         big.sum()          # result discarded: the read is the point
+                    if mode == "after_write":
+                        ops.row_normalize(outp, out_dtype=torch.float32)   # 58 MB read + 58 MB written just before
                     if mode == "prefetched":
                         pre()
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
