@@ -21,7 +21,7 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
                       const void* opts, hipStream_t stream);
 int nsdb_gemm_nt_softmax(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, long long lda,
                          long long ldb, long long ldc, int bias_mode, float alpha, int axis, void* part, int* cnt,
-                         int* flag, int force_fallback, int epi, hipStream_t stream);
+                         int* flag, int force_fallback, int epi, unsigned long long* stamps, hipStream_t stream);
 int nsdb_gemm_nt_f32(const float* A, const float* B, float* C, int M, int N, int K, long long lda, long long ldb,
                      long long ldc, float alpha, int accumulate, hipStream_t stream);
 int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* out, int N, int C, int H, int W,
@@ -185,7 +185,7 @@ torch::Tensor softmax_state(const torch::Tensor& like, int64_t need, hipStream_t
 // into the GEMM epilogue (max-subtracted; cross-workgroup partials, see gemm.hip softmax_epilogue_8ph).
 torch::Tensor gemm_nt_softmax(torch::Tensor A, torch::Tensor B, c10::optional<torch::Tensor> bias, int64_t bias_mode,
                               int64_t axis, c10::optional<torch::Tensor> out, double alpha, bool force_fallback,
-                              int64_t epi) {
+                              int64_t epi, c10::optional<torch::Tensor> stamps) {
   check_cuda(A, "A");
   check_cuda(B, "B");
   TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && B.scalar_type() == torch::kBFloat16, "A,B must be bf16");
@@ -217,9 +217,16 @@ torch::Tensor gemm_nt_softmax(torch::Tensor A, torch::Tensor B, c10::optional<to
   const hipStream_t st = cur_stream();
   auto state = softmax_state(A, std::max(tm, tn) + tm * tn, st);
   int* cnt = state.data_ptr<int>();
+  unsigned long long* sp = nullptr;
+  if (stamps.has_value() && stamps->defined()) {     // diagnostic phase stamps: int64 [tiles * 8]
+    check_cuda(*stamps, "stamps");
+    TORCH_CHECK(stamps->scalar_type() == torch::kInt64 && stamps->is_contiguous() && stamps->numel() >= tm * tn * 8,
+                "stamps must be int64 with >= tiles * 8 entries");
+    sp = reinterpret_cast<unsigned long long*>(stamps->data_ptr<int64_t>());
+  }
   const int rc = nsdb_gemm_nt_softmax(A.data_ptr(), B.data_ptr(), C.data_ptr<float>(), bptr, (int)M, (int)N, (int)K,
                                       A.stride(0), B.stride(0), C.stride(0), (int)bias_mode, (float)alpha, (int)axis,
-                                      part.data_ptr(), cnt, cnt + std::max(tm, tn), force_fallback ? 1 : 0, (int)epi, st);
+                                      part.data_ptr(), cnt, cnt + std::max(tm, tn), force_fallback ? 1 : 0, (int)epi, sp, st);
   check_rc(rc, "gemm_nt_softmax");
   return C;
 }
@@ -631,7 +638,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         }, "current stream waits on the GPU until flag >= value (unsigned)");
   m.def("gemm_nt_softmax", &gemm_nt_softmax, "softmax(alpha A.B^T + bias) fused into the GEMM epilogue",
         py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("bias_mode") = 0, py::arg("axis") = 1,
-        py::arg("out") = py::none(), py::arg("alpha") = 1.0, py::arg("force_fallback") = false, py::arg("epi") = -1);
+        py::arg("out") = py::none(), py::arg("alpha") = 1.0, py::arg("force_fallback") = false, py::arg("epi") = -1,
+        py::arg("stamps") = py::none());
   m.def("conv2d_force_generic", [](int64_t v) { nsdb_conv2d_force_generic = (int)v; },
         "1: route every conv2d to the generic gather kernel (A/B testing)");
   m.def("conv2d_max_blocks", [](int64_t v) { const int old = nsdb_conv2d_max_blocks; nsdb_conv2d_max_blocks = (int)v; return old; },

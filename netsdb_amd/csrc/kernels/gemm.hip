@@ -124,6 +124,7 @@ __device__ __forceinline__ void softmax_epilogue_8ph(f32x4 (&acc)[8][4], char* s
       }
   }
   __syncthreads();
+  unsigned long long* stamp = p.stamps ? p.stamps + (long long)(tm * p.tiles_n + tn) * 8 : nullptr;
   const int grp = AXIS == 1 ? tm : tn, need = AXIS == 1 ? p.tiles_n : p.tiles_m;
   const int my = AXIS == 1 ? tn : tm;
   float2* part = p.sm_part + (long long)grp * need * 256;
@@ -152,6 +153,7 @@ __device__ __forceinline__ void softmax_epilogue_8ph(f32x4 (&acc)[8][4], char* s
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int c = __hip_atomic_fetch_add(p.sm_cnt + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    if (stamp) stamp[2] = t0;                          // diagnostic stamps: partial published, arrived
     while (c < need) {
       __builtin_amdgcn_s_sleep(4);
       c = __hip_atomic_load(p.sm_cnt + grp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -160,6 +162,7 @@ __device__ __forceinline__ void softmax_epilogue_8ph(f32x4 (&acc)[8][4], char* s
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const bool ok = c >= need && !(p.diag & 4);        // diag 4: take the fallback path (tests)
+    if (stamp) stamp[3] = __builtin_amdgcn_s_memrealtime();   // the row-block complete
     *okslot = ok ? 1 : 0;
     if (!ok) p.sm_flag[tm * p.tiles_n + tn] = 1;
   }
@@ -197,6 +200,7 @@ __device__ __forceinline__ void softmax_epilogue_8ph(f32x4 (&acc)[8][4], char* s
     fin[tid * 2 + 1] = 1.f;
   }
   __syncthreads();
+  if (stamp && tid == 0) stamp[4] = __builtin_amdgcn_s_memrealtime();   // row statistics combined
   // 5. normalised values in place (the caller's common LDS-staged store writes them)
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -445,6 +449,8 @@ gemm_nt_tile_kernel(GemmParams p) {
 
 template <int EPI>
 __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
+  // fused-softmax launches may carry diagnostic phase stamps (p.stamps: [tile][8] on the 100 MHz real-time clock)
+  const unsigned long long t_entry = EPI != 0 ? __builtin_amdgcn_s_memrealtime() : 0ull;
   constexpr int HALF = 128 * 128;            // bytes of one half-tile (128 rows x 64 bf16)
   constexpr int BUF = 4 * HALF;              // one K-tile
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF + 1024];   // + the epilogue's bias (store_tile_lds)
@@ -582,11 +588,26 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   if constexpr (EPI != 0) {
     // the fused softmax turns acc into the final values in place; the common store then runs with a plain
     // (alpha 1, no bias/act/dropout, f32) epilogue
+    unsigned long long* stamp = p.stamps ? p.stamps + (long long)(tm * p.tiles_n + tn) * 8 : nullptr;
+    if (stamp && tid == 0) {
+      stamp[0] = t_entry;
+      stamp[1] = __builtin_amdgcn_s_memrealtime();     // main loop done
+    }
     softmax_epilogue_8ph<EPI>(acc, smem, (int)sizeof(smem), p, m0, n0, tm, tn, tid, lane, wave);
     GemmParams q = p;
     q.alpha = 1.f; q.bias = nullptr; q.act = 0; q.dropout = 0.f; q.accumulate = 0; q.out_f32 = 1; q.splits = 1;
     if (p.direct_epi) store_direct_8ph(acc, q, 0, m0, n0, lane, wave);
     else store_tile_lds<256, 256, 2, 4, true>(acc, smem, 2 * BUF, q, 0, 0, m0, n0, tid, lane, wave);
+    if (stamp) {
+      if (tid == 0) stamp[5] = __builtin_amdgcn_s_memrealtime();   // stores issued (wave 0)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        stamp[6] = __builtin_amdgcn_s_memrealtime();                 // every wave's stores complete
+        stamp[7] = ((unsigned long long)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 32) |
+                   (unsigned)__builtin_amdgcn_s_getreg((15 << 11) | 4);   // XCC id, HW_ID (CU / SE)
+      }
+    }
     return;
   }
   if (p.direct_epi) {
@@ -752,7 +773,7 @@ int nsdb_gemm_tail_eligible(int M, int N, int K, int batch, int splits, int cfg)
 // every tile takes the non-co-resident fallback path.
 int nsdb_gemm_nt_softmax(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, long long lda,
                          long long ldb, long long ldc, int bias_mode, float alpha, int axis, void* part, int* cnt,
-                         int* flag, int force_fallback, int epi, hipStream_t stream) {
+                         int* flag, int force_fallback, int epi, unsigned long long* stamps, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
   if (K % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0 || (axis != 1 && axis != 2)) return -1;
   if (256LL * lda * 2 >= 0x7ffffff0LL || 256LL * ldb * 2 >= 0x7ffffff0LL) return -2;
@@ -769,7 +790,7 @@ int nsdb_gemm_nt_softmax(const void* A, const void* B, float* C, const float* bi
   p.tiles_n = (N + 255) / 256;
   p.vec_ws = 0;
   p.vec_c = (ldc % 4 == 0 && (reinterpret_cast<uintptr_t>(C) & 15) == 0) ? 1 : 0;
-  p.softmax = axis; p.sm_part = (float2*)part; p.sm_cnt = cnt; p.sm_flag = flag; p.stamps = nullptr; p.adapt = nullptr;
+  p.softmax = axis; p.sm_part = (float2*)part; p.sm_cnt = cnt; p.sm_flag = flag; p.stamps = stamps; p.adapt = nullptr;
   p.signal = nullptr; p.signal_value = 0; p.steal_cnt = nullptr; p.steal_tq = 0; p.steal_ch = 2;
   p.direct_epi = p.vec_c && epi != 0 ? 1 : 0;      // final values straight from registers (store_direct_8ph)
   const int tiles = p.tiles_m * p.tiles_n;
