@@ -4,7 +4,9 @@ One step (per GPU, weak scaling; every rank holds its own partition of the infer
 the model is replicated — netsDB's broadcast join of the weight sets, "materializeModel"):
   1. FF-NN inference_unit on AmazonCat-14k dims (reference src/tests/source/FFTestWithDeduplication.cc:
      batch 1000, features 597540, hidden 1000, labels 14588; blocks 50x10000; dropout 0.5 as FFTest.cc)
-     = 2 jobs through the engine: W1·Xᵀ -> +b1, relu, dropout -> Wo·Y -> +bo, exp, ᵀ  |  row softmax
+     = the reference's 2 jobs (W1·Xᵀ -> +b1, relu, dropout -> Wo·Y -> +bo, exp, ᵀ  |  row softmax) submitted as ONE
+     engine job: the planner lowers the output layer + row softmax to one GEMM with the normalisation in its
+     epilogue (--two-job keeps the materialised "yo" set and the separate row-normalise job)
   2. conv2d_memory_fusion block (reference src/tests/source/PipelinedConv2dMemFuseTest.cc: 100 images
      3x112x112, 64 filters 7x7x3, stride 1, no padding) = 1 job, fused implicit-GEMM conv + bias.
 The conv2d job is independent of the FF jobs (resident images, own weights); --overlap before|after submits
@@ -85,9 +87,11 @@ def main():
                     help="record one whole step (FF jobs + conv2d job) into a HIP graph after the warmup and time its "
                          "replays (PDBClient.capture_job: no host work per step; the dropout seed of the recorded "
                          "step is reused)")
-    ap.add_argument("--single-job", action="store_true",
-                    help="submit inference_unit as ONE job (no materialised 'yo' set: the output layer runs as one GEMM "
-                         "with the max-subtracted softmax in its epilogue); default: the reference's two jobs")
+    ap.add_argument("--two-job", action="store_true",
+                    help="submit inference_unit as the reference's two jobs (output layer exp -> 'yo' set, then the row "
+                         "normalise); default: ONE job, whose output layer is one GEMM with the max-subtracted softmax "
+                         "in its epilogue (55-59 us vs 66-70 + 18 us in-bench, profiles/r3_s3/softmax)")
+    ap.add_argument("--single-job", action="store_true", help=argparse.SUPPRESS)   # the default; kept for old scripts
     ap.add_argument("--rownorm-loads", choices=["nt", "plain"], default=None,
                     help="row-normalise row loads: non-temporal (library default) or cache-allocating")
     ap.add_argument("--conv-kernel", choices=["rows", "rowfull", "warpspec"], default=None,
@@ -104,6 +108,7 @@ def main():
                     help="FF steps in flight: step i's FF jobs go to job lane i %% inflight (>1 pipelines "
                          "consecutive batches: step i+1's layer-1 GEMM starts while step i's tail kernels run)")
     args = ap.parse_args()
+    args.single_job = not args.two_job
     if args.graph and (args.overlap != "none" or args.inflight > 1):
         ap.error("--graph records the serial step (no --overlap / --inflight job streams)")
 

@@ -21,7 +21,8 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
                       const void* opts, hipStream_t stream);
 int nsdb_gemm_nt_softmax(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, long long lda,
                          long long ldb, long long ldc, int bias_mode, float alpha, int axis, void* part, int* cnt,
-                         int* flag, int force_fallback, int epi, unsigned long long* stamps, hipStream_t stream);
+                         int* flag, int* dep, int force_fallback, int epi, unsigned long long* stamps,
+                         hipStream_t stream);
 int nsdb_gemm_nt_f32(const float* A, const float* B, float* C, int M, int N, int K, long long lda, long long ldb,
                      long long ldc, float alpha, int accumulate, hipStream_t stream);
 int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* out, int N, int C, int H, int W,
@@ -213,9 +214,13 @@ torch::Tensor gemm_nt_softmax(torch::Tensor A, torch::Tensor B, c10::optional<to
     C = torch::empty({M, N}, A.options().dtype(torch::kFloat32));
   }
   const int64_t tm = (M + 255) / 256, tn = (N + 255) / 256;
-  auto part = torch::empty({tm * tn * 256 * 2}, A.options().dtype(torch::kFloat32));
+  // per-group partials [group][256 lines][need rounded up to even] float2 (gemm.hip sm_need_pad)
+  const int64_t groups = axis == 1 ? tm : tn, need = axis == 1 ? tn : tm;
+  auto part = torch::empty({groups * 256 * ((need + 1) & ~1LL) * 2}, A.options().dtype(torch::kFloat32));
   const hipStream_t st = cur_stream();
-  auto state = softmax_state(A, std::max(tm, tn) + tm * tn, st);
+  // arrival [max(tm, tn)] | departure [max(tm, tn)] | timed-out flags [tm * tn]: zero on entry, zero on exit
+  const int64_t maxg = std::max(tm, tn);
+  auto state = softmax_state(A, 2 * maxg + tm * tn, st);
   int* cnt = state.data_ptr<int>();
   unsigned long long* sp = nullptr;
   if (stamps.has_value() && stamps->defined()) {     // diagnostic phase stamps: int64 [tiles * 8]
@@ -226,7 +231,7 @@ torch::Tensor gemm_nt_softmax(torch::Tensor A, torch::Tensor B, c10::optional<to
   }
   const int rc = nsdb_gemm_nt_softmax(A.data_ptr(), B.data_ptr(), C.data_ptr<float>(), bptr, (int)M, (int)N, (int)K,
                                       A.stride(0), B.stride(0), C.stride(0), (int)bias_mode, (float)alpha, (int)axis,
-                                      part.data_ptr(), cnt, cnt + std::max(tm, tn), force_fallback ? 1 : 0, (int)epi, sp, st);
+                                      part.data_ptr(), cnt, cnt + 2 * maxg, cnt + maxg, force_fallback ? 1 : 0, (int)epi, sp, st);
   check_rc(rc, "gemm_nt_softmax");
   return C;
 }

@@ -45,8 +45,74 @@ __device__ __forceinline__ void sm_combine(float& m, float& s, float m2, float s
   m = mn;
 }
 
+// Partials of one softmax group (row-block for AXIS 1, column-block for AXIS 2): float2 (max, sum exp)
+// [group][256 lines][need_pad] with need_pad = need rounded up to even, so the partials of one line are
+// contiguous and 16-B aligned: the combine reads a line's partials with 16-B loads, all in flight at once.
+__host__ __device__ __forceinline__ int sm_need_pad(int need) { return (need + 1) & ~1; }
+
+// LDS map of the epilogue. Bytes [0, 128 KiB): the tile buffers, which the main loop no longer needs, become the
+// landing zone of the group's partials (LDS-DMA, [256 lines][32 16-B slots], slot = pair ^ (line & 31)).
+// From SM_ST = 128 KiB, floats:
+//   [0, 2048)      per-wave line partials [8 waves][128 | 64][2]
+//   [2048, 2560)   this tile's own partial per line [256][2]    (fallback scale)
+//   [2560, 3072)   second half of the combine [256][2]
+//   [3072, 3584)   final (max, 1/sum) per line [256][2]
+//   [3584]         poll verdict
+constexpr int SM_ST = 131072;
+constexpr int SM_LDS = SM_ST + 3600 * 4;              // LDS bytes of a fused-softmax launch
+
+// Final (max M, 1/sum S) per line of a softmax group into fin[256][2]: the group's partials ([256 lines][npad]
+// float2, contiguous) come into LDS by LDS-DMA (no VGPRs: the tile's logits hold 128 of them), 64 partials per
+// line per chunk, every wave-instruction moving 1 KiB and a whole chunk in flight at once (one round trip for up
+// to 64 tiles per group). Device-scope (sc1) loads: never served from a stale line of this XCD's L2, so no
+// acquire fence (which would invalidate the L2 under the tiles still in their main loops). Two threads per
+// line then reduce from LDS: the max first, then the rescaled sums (independent exps, no serial chain).
+// Every thread of the workgroup calls it (barriers inside).
+__device__ __forceinline__ void sm_group_stats(const float2* part, int npad, char* smem, float* fin, float* h2,
+                                               int tid, int lane, int wave) {
+  const int e = tid & 255, half = tid >> 8;
+  const int npairs = npad >> 1;
+  const __amdgpu_buffer_rsrc_t rp = make_rsrc(part, (unsigned)(256 * npad * 8));
+  float m = -INFINITY, s = 0.f;
+  for (int c0 = 0; c0 < npairs; c0 += 32) {
+#pragma unroll 4
+    for (int w = wave; w < 128; w += 8) {              // 256 lines x 32 slots = 128 wave-instructions
+      const int piece = w * 64 + lane;
+      const int line = piece >> 5, pr = c0 + ((piece & 31) ^ (line & 31));
+      const int voff = pr < npairs ? (line * npad + pr * 2) * 8 : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rp, (lds_void*)(smem + w * 1024), 16, voff, 0, 0, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int q0 = half * 16, qe = min(min(32, npairs - c0), q0 + 16);
+    const char* row = smem + e * 512;
+    float cm = -INFINITY;
+    for (int q = q0; q < qe; ++q) {
+      const float4 v = *reinterpret_cast<const float4*>(row + ((q ^ (e & 31)) * 16));
+      cm = fmaxf(cm, fmaxf(v.x, v.z));
+    }
+    if (cm != -INFINITY) {
+      float cs = 0.f;
+      for (int q = q0; q < qe; ++q) {
+        const float4 v = *reinterpret_cast<const float4*>(row + ((q ^ (e & 31)) * 16));
+        cs += v.y * __expf(v.x - cm) + v.w * __expf(v.z - cm);   // exp(-inf - cm) = 0 for empty partials
+      }
+      sm_combine(m, s, cm, cs);
+    }
+    __syncthreads();                                   // the zone is refilled by the next chunk
+  }
+  if (half == 1) { h2[e * 2] = m; h2[e * 2 + 1] = s; }
+  __syncthreads();
+  if (half == 0) {
+    sm_combine(m, s, h2[e * 2], h2[e * 2 + 1]);
+    fin[e * 2] = m;
+    fin[e * 2 + 1] = s > 0.f ? 1.f / s : 0.f;
+  }
+  __syncthreads();
+}
+
 template <int AXIS>
-__device__ __forceinline__ void softmax_epilogue_8ph(f32x4 (&acc)[8][4], char* smem, int /*smem_bytes*/, const GemmParams& p,
+__device__ __forceinline__ bool softmax_epilogue_8ph(f32x4 (&acc)[8][4], char* smem, int /*smem_bytes*/, const GemmParams& p,
                                                      int m0, int n0, int tm, int tn, int tid, int lane, int wave) {
   // transposed accumulator layout (TS): acc[i][j][r] = C[wr*128 + i*16 + rl][wc*64 + j*16 + cq + r]
   const int wr = wave >> 2, wc = wave & 3;
@@ -72,8 +138,10 @@ __device__ __forceinline__ void softmax_epilogue_8ph(f32x4 (&acc)[8][4], char* s
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[i][j][r] = acc[i][j][r] * p.alpha + brow + bcol[j][r];
   }
-  // 2. tile partial per row (AXIS 1) / column (AXIS 2): registers + wave shuffles, then across waves in LDS
-  float* st = reinterpret_cast<float*>(smem);          // [8 waves][128 | 64][2]
+  // 2. per-wave line max m_w (registers + wave shuffles); acc becomes exp(x - m_w) — the ONLY exp per element:
+  // the final value is that times exp(m_w - M) / S, one factor per line and wave; wave sums of the exps, then
+  // across the waves of a line in LDS
+  float* st = reinterpret_cast<float*>(smem + SM_ST);  // [8 waves][128 | 64][2]
   if constexpr (AXIS == 1) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -85,12 +153,15 @@ __device__ __forceinline__ void softmax_epilogue_8ph(f32x4 (&acc)[8][4], char* s
       m = fmaxf(m, __shfl_xor(m, 16, 64));
       m = fmaxf(m, __shfl_xor(m, 32, 64));
       float sum = 0.f;
-      if (m != -INFINITY) {
+      const float ms = m == -INFINITY ? 0.f : m;        // an all-invalid line: exp(-inf) = 0 everywhere
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) sum += __expf(acc[i][j][r] - m);
-      }
+        for (int r = 0; r < 4; ++r) {
+          const float e = __expf(acc[i][j][r] - ms);
+          acc[i][j][r] = e;
+          sum += e;
+        }
       sum += __shfl_xor(sum, 16, 64);
       sum += __shfl_xor(sum, 32, 64);
       if (lane < 16) {
@@ -110,9 +181,12 @@ __device__ __forceinline__ void softmax_epilogue_8ph(f32x4 (&acc)[8][4], char* s
 #pragma unroll
         for (int o = 1; o < 16; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
         float sum = 0.f;
-        if (m != -INFINITY) {
+        const float ms = m == -INFINITY ? 0.f : m;
 #pragma unroll
-          for (int i = 0; i < 8; ++i) sum += __expf(acc[i][j][r] - m);
+        for (int i = 0; i < 8; ++i) {
+          const float e = __expf(acc[i][j][r] - ms);
+          acc[i][j][r] = e;
+          sum += e;
         }
 #pragma unroll
         for (int o = 1; o < 16; o <<= 1) sum += __shfl_xor(sum, o, 64);
@@ -127,7 +201,8 @@ __device__ __forceinline__ void softmax_epilogue_8ph(f32x4 (&acc)[8][4], char* s
   unsigned long long* stamp = p.stamps ? p.stamps + (long long)(tm * p.tiles_n + tn) * 8 : nullptr;
   const int grp = AXIS == 1 ? tm : tn, need = AXIS == 1 ? p.tiles_n : p.tiles_m;
   const int my = AXIS == 1 ? tn : tm;
-  float2* part = p.sm_part + (long long)grp * need * 256;
+  const int npad = sm_need_pad(need);
+  float2* part = p.sm_part + (long long)grp * 256 * npad;
   float* tstat = st + 2048;                           // [256][2] this tile's own partial (fallback scale)
   if (tid < 256) {
     float m = -INFINITY, s = 0.f;
@@ -140,108 +215,150 @@ __device__ __forceinline__ void softmax_epilogue_8ph(f32x4 (&acc)[8][4], char* s
 #pragma unroll
       for (int w = 0; w < 2; ++w) sm_combine(m, s, st[((wcc * 2 + w) * 64 + c2) * 2], st[((wcc * 2 + w) * 64 + c2) * 2 + 1]);
     }
-    part[my * 256 + tid] = make_float2(m, s);
+    // device-scope (sc1) stores: written through this XCD's L2, so no L2 write-back fence is needed before the
+    // arrival (a release fence writes back the whole L2 and measured 5-14 us per tile)
+    auto put = [&](int idx, float a, float b) {
+      const unsigned long long v = ((unsigned long long)__float_as_uint(b) << 32) | __float_as_uint(a);
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(part + idx), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    put(tid * npad + my, m, s);
+    if (npad != need && my == 0) put(tid * npad + need, -INFINITY, 0.f);   // the pad slot
     tstat[tid * 2] = m;
     tstat[tid * 2 + 1] = s;
   }
-  // 3. publish the partial, arrive, poll (bounded) for the whole row-block
+  // 3. publish the partial, arrive, poll (bounded) for the whole group
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  int* okslot = reinterpret_cast<int*>(st + 2048 + 512);
+  int* okslot = reinterpret_cast<int*>(st + 3584);
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // every wave's partial stores were acknowledged (vmcnt(0) + barrier above) before the arrival
     int c = __hip_atomic_fetch_add(p.sm_cnt + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     if (stamp) stamp[2] = t0;                          // diagnostic stamps: partial published, arrived
     while (c < need) {
-      __builtin_amdgcn_s_sleep(4);
+      __builtin_amdgcn_s_sleep(1);
       c = __hip_atomic_load(p.sm_cnt + grp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (__builtin_amdgcn_s_memrealtime() - t0 > 20000ull) break;   // 200 us at 100 MHz
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const bool ok = c >= need && !(p.diag & 4);        // diag 4: take the fallback path (tests)
-    if (stamp) stamp[3] = __builtin_amdgcn_s_memrealtime();   // the row-block complete
+    if (stamp) stamp[3] = __builtin_amdgcn_s_memrealtime();   // the group complete
     *okslot = ok ? 1 : 0;
-    if (!ok) p.sm_flag[tm * p.tiles_n + tn] = 1;
   }
   __syncthreads();
   const bool ok = *okslot != 0;
-  // 4. final (max, 1/sum) per row/column of the tile: all partials of the row-block (2 threads per row,
-  // loads batched 8 deep), or this tile's own max on the fallback path
-  float* fin = st;                                     // [256][2] (the wave stats are consumed)
+  // 4. final (max, 1/sum) per line of the tile from the group's partials, or this tile's own on the fallback path
+  float* fin = st + 3072;                              // [256][2]
   if (ok) {
-    // 16 partials in flight per thread (two threads per row, every other tile each): the partials were written
-    // by other XCDs, so each batch is a full round trip past L2 — one batch covers a row-block of up to 32 tiles
-    // (the FF output layer: 57 tiles -> 2 round trips instead of 4 with 8 in flight)
-    const int e = tid & 255, half = tid >> 8;
-    float m = -INFINITY, s = 0.f;
-    for (int t0 = half; t0 < need; t0 += 32) {
-      float2 v[16];
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int t = t0 + 2 * q;
-        v[q] = t < need ? part[t * 256 + e] : make_float2(-INFINITY, 0.f);
-      }
-#pragma unroll
-      for (int q = 0; q < 16; ++q) sm_combine(m, s, v[q].x, v[q].y);
+    sm_group_stats(part, npad, smem, fin, st + 2560, tid, lane, wave);
+  } else {
+    if (tid < 256) {
+      fin[tid * 2] = tstat[tid * 2];
+      fin[tid * 2 + 1] = 1.f;
     }
-    float* h2 = st + 1024;
-    if (half == 1) { h2[e * 2] = m; h2[e * 2 + 1] = s; }
     __syncthreads();
-    if (half == 0) {
-      sm_combine(m, s, h2[e * 2], h2[e * 2 + 1]);
-      fin[e * 2] = m;
-      fin[e * 2 + 1] = s > 0.f ? 1.f / s : 0.f;
-    }
-  } else if (tid < 256) {
-    fin[tid * 2] = tstat[tid * 2];
-    fin[tid * 2 + 1] = 1.f;
   }
-  __syncthreads();
-  if (stamp && tid == 0) stamp[4] = __builtin_amdgcn_s_memrealtime();   // row statistics combined
-  // 5. normalised values in place (the caller's common LDS-staged store writes them)
+  if (stamp && tid == 0) stamp[4] = __builtin_amdgcn_s_memrealtime();   // group statistics combined
+  // 5. final values in place: acc (= exp(x - m_w)) times exp(m_w - M) / S, one factor per line of the wave
+  // (the caller's store writes them)
+  if constexpr (AXIS == 1) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 8; ++i) {
+      const int e = wr * 128 + i * 16 + rl;
+      const float mw = st[((wr * 4 + wc) * 128 + i * 16 + rl) * 2];
+      const float M = fin[e * 2];
+      const float f = mw == -INFINITY ? 0.f : __expf(mw - M) * fin[e * 2 + 1];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] *= f;
+    }
+  } else {
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int e = AXIS == 1 ? wr * 128 + i * 16 + rl : wc * 64 + j * 16 + cq + r;
-        const float x = acc[i][j][r];
-        acc[i][j][r] = x == -INFINITY ? 0.f : __expf(x - fin[e * 2]) * fin[e * 2 + 1];
+        const int e = wc * 64 + j * 16 + cq + r;
+        const float mw = st[((wc * 2 + wr) * 64 + j * 16 + cq + r) * 2];
+        const float M = fin[e * 2];
+        const float f = mw == -INFINITY ? 0.f : __expf(mw - M) * fin[e * 2 + 1];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i][j][r] *= f;
       }
+  }
+  return ok;
 }
 
-// Fix-up after a fused-softmax launch: re-zeroes the arrival counters and rescales the tiles whose poll
-// timed out (normally none: every block returns after reading its flag).
-__global__ void __launch_bounds__(256) softmax_fixup_kernel(GemmParams p) {
-  const int tile = blockIdx.x, tid = threadIdx.x;
-  const int AX = p.softmax;
-  if (tile == 0)
-    for (int i = tid; i < max(p.tiles_m, p.tiles_n); i += 256) p.sm_cnt[i] = 0;
-  if (p.sm_flag[tile] == 0) return;
-  const int tm = tile / p.tiles_n, tn = tile % p.tiles_n;
-  const int grp = AX == 1 ? tm : tn, need = AX == 1 ? p.tiles_n : p.tiles_m, my = AX == 1 ? tn : tm;
-  const float2* part = p.sm_part + (long long)grp * need * 256;
-  __shared__ float fac[256];
-  {
-    float m = -INFINITY, s = 0.f;
-    for (int t = 0; t < need; ++t) sm_combine(m, s, part[t * 256 + tid].x, part[t * 256 + tid].y);
-    const float mt = part[my * 256 + tid].x;
-    fac[tid] = (s > 0.f && mt != -INFINITY) ? __expf(mt - m) / s : 0.f;
-  }
-  __syncthreads();
+// Late rescale (the rare fallback path): run by the last tile of a group to depart when some tiles of the group
+// timed out. Every partial is published and every timed-out tile's exp(x - m_tile) is written back (they depart
+// after their stores and an L2 write-back); each gets the factor exp(m_tile - M) / S per line.
+template <int AXIS>
+__device__ __forceinline__ void sm_late_rescale(const GemmParams& p, char* smem, int grp, int need, int tid, int lane,
+                                             int wave) {
+  const int npad = sm_need_pad(need);
+  float* st = reinterpret_cast<float*>(smem + SM_ST);
+  int* slot = reinterpret_cast<int*>(st + 3592);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  const float2* part = p.sm_part + (long long)grp * 256 * npad;
+  float* fin = st + 3072;
+  sm_group_stats(part, npad, smem, fin, st + 2560, tid, lane, wave);
+  float* fac = st + 2048;                             // [256]
   float* C = reinterpret_cast<float*>(p.C);
-  const int m0 = tm * 256, n0 = tn * 256;
-  for (int e = tid; e < 256 * 256; e += 256) {
-    const int r = e >> 8, c = e & 255;
-    const int row = m0 + r, col = n0 + c;
-    if (row < p.M && col < p.N) C[(long long)row * p.ldc + col] *= fac[AX == 1 ? r : c];
+  for (int t = 0; t < need; ++t) {
+    const int ttm = AXIS == 1 ? grp : t, ttn = AXIS == 1 ? t : grp;
+    int* fl = p.sm_flag + ttm * p.tiles_n + ttn;
+    if (tid == 0) *slot = __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const bool flagged = *slot != 0;
+    if (flagged && tid < 256) {
+      const float mt = part[tid * npad + t].x;
+      fac[tid] = (fin[tid * 2 + 1] > 0.f && mt != -INFINITY) ? __expf(mt - fin[tid * 2]) * fin[tid * 2 + 1] : 0.f;
+    }
+    __syncthreads();
+    if (flagged) {
+      const int m0 = ttm * 256, n0 = ttn * 256;
+      for (int e = tid; e < 256 * 256; e += 512) {
+        const int r = e >> 8, c = e & 255;
+        const int row = m0 + r, col = n0 + c;
+        if (row < p.M && col < p.N) C[(long long)row * p.ldc + col] *= fac[AXIS == 1 ? r : c];
+      }
+      if (tid == 0) __hip_atomic_store(fl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();                                   // slot / fac reused
+  }
+}
+
+// Departure of a fused-softmax tile (no fix-up launch). One word per group counts departures (low 16 bits) and
+// timed-out tiles (high 16 bits). A tile on the normal path departs as soon as it has the group's statistics
+// (before its stores); a timed-out tile departs after its exp(x - m_tile) stores are complete and written back,
+// with its flag set. The last tile to depart re-zeroes the group's counters for the next launch (every tile has
+// passed its poll by then) and, if some tiles timed out, rescales them (sm_late_rescale). Every thread calls it.
+template <int AXIS>
+__device__ __forceinline__ void sm_depart(const GemmParams& p, char* smem, bool ok, int tm, int tn, int tid, int lane,
+                                          int wave) {
+  const int grp = AXIS == 1 ? tm : tn, need = AXIS == 1 ? p.tiles_n : p.tiles_m;
+  int* slot = reinterpret_cast<int*>(smem + SM_ST) + 3588;
+  if (!ok) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (tid == 0) {
+    if (!ok) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // this tile's outputs written back from its L2
+      __hip_atomic_store(p.sm_flag + tm * p.tiles_n + tn, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const int inc = ok ? 1 : 0x10001;
+    const int d = __hip_atomic_fetch_add(p.sm_dep + grp, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + inc;
+    int verdict = 0;
+    if ((d & 0xffff) == need) {
+      verdict = (d >> 16) > 0 ? 2 : 1;
+      __hip_atomic_store(p.sm_cnt + grp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p.sm_dep + grp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *slot = verdict;
   }
   __syncthreads();
-  if (tid == 0) p.sm_flag[tile] = 0;
+  if (*slot == 2) sm_late_rescale<AXIS>(p, smem, grp, need, tid, lane, wave);
 }
 
 // Direct epilogue of the unsplit 8-phase tile: every lane stores its own accumulators, 4 consecutive columns
@@ -453,7 +570,8 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   const unsigned long long t_entry = EPI != 0 ? __builtin_amdgcn_s_memrealtime() : 0ull;
   constexpr int HALF = 128 * 128;            // bytes of one half-tile (128 rows x 64 bf16)
   constexpr int BUF = 4 * HALF;              // one K-tile
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF + 1024];   // + the epilogue's bias (store_tile_lds)
+  // + the epilogue's bias (store_tile_lds), or the fused softmax's line statistics (SM_LDS)
+  __shared__ __attribute__((aligned(16))) char smem[EPI != 0 ? SM_LDS : 2 * BUF + 1024];
 
   const int ntiles = p.tiles_m * p.tiles_n;
   const int wg = xcd_remap(blockIdx.x, ntiles * p.splits);
@@ -593,11 +711,13 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
       stamp[0] = t_entry;
       stamp[1] = __builtin_amdgcn_s_memrealtime();     // main loop done
     }
-    softmax_epilogue_8ph<EPI>(acc, smem, (int)sizeof(smem), p, m0, n0, tm, tn, tid, lane, wave);
+    const bool ok = softmax_epilogue_8ph<EPI>(acc, smem, (int)sizeof(smem), p, m0, n0, tm, tn, tid, lane, wave);
+    if (ok) sm_depart<EPI>(p, smem, true, tm, tn, tid, lane, wave);
     GemmParams q = p;
     q.alpha = 1.f; q.bias = nullptr; q.act = 0; q.dropout = 0.f; q.accumulate = 0; q.out_f32 = 1; q.splits = 1;
     if (p.direct_epi) store_direct_8ph(acc, q, 0, m0, n0, lane, wave);
     else store_tile_lds<256, 256, 2, 4, true>(acc, smem, 2 * BUF, q, 0, 0, m0, n0, tid, lane, wave);
+    if (!ok) sm_depart<EPI>(p, smem, false, tm, tn, tid, lane, wave);
     if (stamp) {
       if (tid == 0) stamp[5] = __builtin_amdgcn_s_memrealtime();   // stores issued (wave 0)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -773,7 +893,8 @@ int nsdb_gemm_tail_eligible(int M, int N, int K, int batch, int splits, int cfg)
 // every tile takes the non-co-resident fallback path.
 int nsdb_gemm_nt_softmax(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, long long lda,
                          long long ldb, long long ldc, int bias_mode, float alpha, int axis, void* part, int* cnt,
-                         int* flag, int force_fallback, int epi, unsigned long long* stamps, hipStream_t stream) {
+                         int* flag, int* dep, int force_fallback, int epi, unsigned long long* stamps,
+                         hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
   if (K % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0 || (axis != 1 && axis != 2)) return -1;
   if (256LL * lda * 2 >= 0x7ffffff0LL || 256LL * ldb * 2 >= 0x7ffffff0LL) return -2;
@@ -790,13 +911,13 @@ int nsdb_gemm_nt_softmax(const void* A, const void* B, float* C, const float* bi
   p.tiles_n = (N + 255) / 256;
   p.vec_ws = 0;
   p.vec_c = (ldc % 4 == 0 && (reinterpret_cast<uintptr_t>(C) & 15) == 0) ? 1 : 0;
-  p.softmax = axis; p.sm_part = (float2*)part; p.sm_cnt = cnt; p.sm_flag = flag; p.stamps = stamps; p.adapt = nullptr;
+  p.softmax = axis; p.sm_part = (float2*)part; p.sm_cnt = cnt; p.sm_flag = flag; p.sm_dep = dep; p.stamps = stamps;
+  p.adapt = nullptr;
   p.signal = nullptr; p.signal_value = 0; p.steal_cnt = nullptr; p.steal_tq = 0; p.steal_ch = 2;
   p.direct_epi = p.vec_c && epi != 0 ? 1 : 0;      // final values straight from registers (store_direct_8ph)
   const int tiles = p.tiles_m * p.tiles_n;
   if (axis == 1) hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<1>, dim3(tiles), dim3(512), 0, stream, p);
   else hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<2>, dim3(tiles), dim3(512), 0, stream, p);
-  hipLaunchKernelGGL(nsdb::softmax_fixup_kernel, dim3(tiles), dim3(256), 0, stream, p);
   return (int)hipGetLastError();
 }
 

@@ -41,6 +41,7 @@ struct GemmParams {
   float2* sm_part;
   int* sm_cnt;
   int* sm_flag;
+  int* sm_dep;               // fused softmax: departures (low 16 bits) + timed-out tiles (high 16) per group
   unsigned long long* stamps;   // diagnostic variant 12: per-workgroup real-time stamps every 32 k-tiles
   struct AdaptState* adapt;     // split-K: launch-to-launch adaptive K partition (see AdaptState)
   // tail trigger (8-phase kernel): every workgroup raises *signal to signal_value (atomic max) when its main

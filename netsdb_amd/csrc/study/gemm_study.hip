@@ -25,217 +25,7 @@
 namespace nsdb {
 
 
-// ---- fused, max-subtracted softmax epilogue of the 256x256 8-wave tile (FFOutputLayer: the reference's
-// exp(x + b) / rowsum without its overflow at x > 88; src/FF/headers/FFOutputLayer.h + FFRowAggregate.h).
-// The softmax row (AXIS 1) spans tiles_n workgroups, so the tile's logits stay in registers while the
-// workgroups of one row-block exchange per-row (max, sum exp) partials through global memory:
-//   logits -> per-row tile partial (wave shuffles + LDS across the 4 column waves) -> store partial ->
-//   agent-scope release + arrival counter -> bounded poll until every tile of the row-block arrived ->
-//   acquire -> combine all partials of the row -> exp(x - M) / S written once (no exp'd f32 round trip
-//   through HBM and no separate row-normalise pass).
-// Placement-independent (cdna_hip_programming.md §6 G16 release/acquire): correct on any XCD mapping. The
-// poll is bounded (~200 us on the 100 MHz real-time clock): if the row-block's workgroups are not
-// co-resident (the GPU shared with another job), a timed-out tile writes exp(x - m_tile), flags itself and
-// the fix-up kernel rescales it by exp(m_tile - M) / S after the launch — slow but never wrong or hung.
-// AXIS 2 is the same over the rows of C (the planner computed C^T).
-__device__ __forceinline__ void sm_combine(float& m, float& s, float m2, float s2) {
-  const float mn = fmaxf(m, m2);
-  if (mn == -INFINITY) return;
-  s = s * __expf(m - mn) + s2 * __expf(m2 - mn);
-  m = mn;
-}
-
-template <int AXIS>
-__device__ __forceinline__ void softmax_epilogue_8ph(f32x4 (&acc)[8][4], char* smem, int /*smem_bytes*/, const GemmParams& p,
-                                                     int m0, int n0, int tm, int tn, int tid, int lane, int wave) {
-  // transposed accumulator layout (TS): acc[i][j][r] = C[wr*128 + i*16 + rl][wc*64 + j*16 + cq + r]
-  const int wr = wave >> 2, wc = wave & 3;
-  const int rl = lane & 15, cq = (lane >> 4) * 4;
-  // 1. logits in registers (invalid rows / columns -> -inf: they never win a max and exp to 0). Per-row or
-  // per-column bias only (host-checked)
-  float bcol[4][4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int col = n0 + wc * 64 + j * 16 + cq + r;
-      bcol[j][r] = (p.bias && p.bias_mode == 2) ? p.bias[min(col, p.N - 1)] : 0.f;
-      if (col >= p.N) bcol[j][r] = -INFINITY;
-    }
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int row = m0 + wr * 128 + i * 16 + rl;
-    float brow = (p.bias && p.bias_mode == 1) ? p.bias[min(row, p.M - 1)] : 0.f;
-    if (row >= p.M) brow = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[i][j][r] = acc[i][j][r] * p.alpha + brow + bcol[j][r];
-  }
-  // 2. tile partial per row (AXIS 1) / column (AXIS 2): registers + wave shuffles, then across waves in LDS
-  float* st = reinterpret_cast<float*>(smem);          // [8 waves][128 | 64][2]
-  if constexpr (AXIS == 1) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float m = -INFINITY;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) m = fmaxf(m, acc[i][j][r]);
-      m = fmaxf(m, __shfl_xor(m, 16, 64));
-      m = fmaxf(m, __shfl_xor(m, 32, 64));
-      float sum = 0.f;
-      if (m != -INFINITY) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) sum += __expf(acc[i][j][r] - m);
-      }
-      sum += __shfl_xor(sum, 16, 64);
-      sum += __shfl_xor(sum, 32, 64);
-      if (lane < 16) {
-        const int idx = ((wr * 4 + wc) * 128 + i * 16 + rl) * 2;
-        st[idx] = m;
-        st[idx + 1] = sum;
-      }
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float m = -INFINITY;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) m = fmaxf(m, acc[i][j][r]);
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-        float sum = 0.f;
-        if (m != -INFINITY) {
-#pragma unroll
-          for (int i = 0; i < 8; ++i) sum += __expf(acc[i][j][r] - m);
-        }
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) sum += __shfl_xor(sum, o, 64);
-        if (rl == 0) {
-          const int idx = ((wc * 2 + wr) * 64 + j * 16 + cq + r) * 2;
-          st[idx] = m;
-          st[idx + 1] = sum;
-        }
-      }
-  }
-  __syncthreads();
-  const int grp = AXIS == 1 ? tm : tn, need = AXIS == 1 ? p.tiles_n : p.tiles_m;
-  const int my = AXIS == 1 ? tn : tm;
-  float2* part = p.sm_part + (long long)grp * need * 256;
-  float* tstat = st + 2048;                           // [256][2] this tile's own partial (fallback scale)
-  if (tid < 256) {
-    float m = -INFINITY, s = 0.f;
-    if constexpr (AXIS == 1) {
-      const int wrr = tid >> 7, rl = tid & 127;
-#pragma unroll
-      for (int w = 0; w < 4; ++w) sm_combine(m, s, st[((wrr * 4 + w) * 128 + rl) * 2], st[((wrr * 4 + w) * 128 + rl) * 2 + 1]);
-    } else {
-      const int wcc = tid >> 6, c2 = tid & 63;
-#pragma unroll
-      for (int w = 0; w < 2; ++w) sm_combine(m, s, st[((wcc * 2 + w) * 64 + c2) * 2], st[((wcc * 2 + w) * 64 + c2) * 2 + 1]);
-    }
-    part[my * 256 + tid] = make_float2(m, s);
-    tstat[tid * 2] = m;
-    tstat[tid * 2 + 1] = s;
-  }
-  // 3. publish the partial, arrive, poll (bounded) for the whole row-block
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int* okslot = reinterpret_cast<int*>(st + 2048 + 512);
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int c = __hip_atomic_fetch_add(p.sm_cnt + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (c < need) {
-      __builtin_amdgcn_s_sleep(4);
-      c = __hip_atomic_load(p.sm_cnt + grp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 20000ull) break;   // 200 us at 100 MHz
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const bool ok = c >= need && !(p.diag & 4);        // diag 4: take the fallback path (tests)
-    *okslot = ok ? 1 : 0;
-    if (!ok) p.sm_flag[tm * p.tiles_n + tn] = 1;
-  }
-  __syncthreads();
-  const bool ok = *okslot != 0;
-  // 4. final (max, 1/sum) per row/column of the tile: all partials of the row-block (2 threads per row,
-  // loads batched 8 deep), or this tile's own max on the fallback path
-  float* fin = st;                                     // [256][2] (the wave stats are consumed)
-  if (ok) {
-    const int e = tid & 255, half = tid >> 8;
-    float m = -INFINITY, s = 0.f;
-    for (int t0 = half; t0 < need; t0 += 16) {
-      float2 v[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int t = t0 + 2 * q;
-        v[q] = t < need ? part[t * 256 + e] : make_float2(-INFINITY, 0.f);
-      }
-#pragma unroll
-      for (int q = 0; q < 8; ++q) sm_combine(m, s, v[q].x, v[q].y);
-    }
-    float* h2 = st + 1024;
-    if (half == 1) { h2[e * 2] = m; h2[e * 2 + 1] = s; }
-    __syncthreads();
-    if (half == 0) {
-      sm_combine(m, s, h2[e * 2], h2[e * 2 + 1]);
-      fin[e * 2] = m;
-      fin[e * 2 + 1] = s > 0.f ? 1.f / s : 0.f;
-    }
-  } else if (tid < 256) {
-    fin[tid * 2] = tstat[tid * 2];
-    fin[tid * 2 + 1] = 1.f;
-  }
-  __syncthreads();
-  // 5. normalised values in place (the caller's common LDS-staged store writes them)
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int e = AXIS == 1 ? wr * 128 + i * 16 + rl : wc * 64 + j * 16 + cq + r;
-        const float x = acc[i][j][r];
-        acc[i][j][r] = x == -INFINITY ? 0.f : __expf(x - fin[e * 2]) * fin[e * 2 + 1];
-      }
-}
-
-// Fix-up after a fused-softmax launch: re-zeroes the arrival counters and rescales the tiles whose poll
-// timed out (normally none: every block returns after reading its flag).
-__global__ void __launch_bounds__(256) softmax_fixup_kernel(GemmParams p) {
-  const int tile = blockIdx.x, tid = threadIdx.x;
-  const int AX = p.softmax;
-  if (tile == 0)
-    for (int i = tid; i < max(p.tiles_m, p.tiles_n); i += 256) p.sm_cnt[i] = 0;
-  if (p.sm_flag[tile] == 0) return;
-  const int tm = tile / p.tiles_n, tn = tile % p.tiles_n;
-  const int grp = AX == 1 ? tm : tn, need = AX == 1 ? p.tiles_n : p.tiles_m, my = AX == 1 ? tn : tm;
-  const float2* part = p.sm_part + (long long)grp * need * 256;
-  __shared__ float fac[256];
-  {
-    float m = -INFINITY, s = 0.f;
-    for (int t = 0; t < need; ++t) sm_combine(m, s, part[t * 256 + tid].x, part[t * 256 + tid].y);
-    const float mt = part[my * 256 + tid].x;
-    fac[tid] = (s > 0.f && mt != -INFINITY) ? __expf(mt - m) / s : 0.f;
-  }
-  __syncthreads();
-  float* C = reinterpret_cast<float*>(p.C);
-  const int m0 = tm * 256, n0 = tn * 256;
-  for (int e = tid; e < 256 * 256; e += 256) {
-    const int r = e >> 8, c = e & 255;
-    const int row = m0 + r, col = n0 + c;
-    if (row < p.M && col < p.N) C[(long long)row * p.ldc + col] *= fac[AX == 1 ? r : c];
-  }
-  __syncthreads();
-  if (tid == 0) p.sm_flag[tile] = 0;
-}
+// (the fused softmax GEMM epilogue lives only in the product build, csrc/kernels/gemm.hip)
 
 // TBM x TBN tile, WGM x WGN waves; each wave owns (TBM/WGM) x (TBN/WGN) = TM x TN 16x16 MFMA tiles.
 //   <128,128,2,2>: 256 threads, 64 KiB LDS, 2 blocks/CU (general shapes)
@@ -728,17 +518,6 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
       if (lane == 0) ad->cnt = 0u;     // ready for the next launch (stream-ordered after this one)
     }
     __syncthreads();                   // LDS scratch above is reused by the epilogue
-  }
-  // the fused softmax turns acc into the final values in place; the common store then runs with a plain
-  // (alpha 1, no bias/act/dropout, f32) epilogue
-  // (variants 20 / 21: softmax along axis 1 / 2 — separate instantiations, one epilogue each: both in one
-  // kernel pushed the epilogue past 256 VGPRs into scratch)
-  if constexpr (V == 20 || V == 21) {
-    softmax_epilogue_8ph<V == 20 ? 1 : 2>(acc, smem, (int)sizeof(smem), p, m0, n0, tm, tn, tid, lane, wave);
-    GemmParams q = p;
-    q.alpha = 1.f; q.bias = nullptr; q.act = 0; q.dropout = 0.f; q.accumulate = 0; q.out_f32 = 1; q.splits = 1;
-    store_tile_lds<256, 256, 2, 4, true>(acc, smem, (int)sizeof(smem), q, 0, 0, m0, n0, tid, lane, wave);
-    return;
   }
   store_tile_lds<256, 256, 2, 4, TS>(acc, smem, (int)sizeof(smem), p, batch, split, m0, n0, tid, lane, wave);
   if constexpr (V == 23) {
@@ -1272,36 +1051,6 @@ int nsdb_study_gemm_splits(int M, int N, int K, int batch) {
   return splits;
 }
 
-// C (f32) = softmax(alpha * A . B^T + bias) along axis 1 (each row of C) or 2 (each column of C), fused into
-// the 8-phase GEMM's epilogue (one launch + the fix-up). part: f32x2 [tiles][256]; cnt: int [max(tiles_m,
-// tiles_n)] and flag: int [tiles], both zero on entry (the fix-up leaves them zero).
-int nsdb_study_gemm_nt_softmax(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, long long lda,
-                         long long ldb, long long ldc, int bias_mode, float alpha, int axis, void* part, int* cnt,
-                         int* flag, hipStream_t stream) {
-  if (M <= 0 || N <= 0) return 0;
-  if (K % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0 || (axis != 1 && axis != 2)) return -1;
-  if (256LL * lda * 2 >= 0x7ffffff0LL || 256LL * ldb * 2 >= 0x7ffffff0LL) return -2;
-  nsdb::GemmParams p;
-  p.A = (const unsigned short*)A; p.B = (const unsigned short*)B; p.C = C; p.ws = nullptr; p.bias = bias;
-  p.lda = lda; p.ldb = ldb; p.ldc = ldc; p.sA = p.sB = p.sC = p.sBias = 0;
-  p.M = M; p.N = N; p.K = K;
-  p.kchunk = std::max(1, (K + nsdb::BK - 1) / nsdb::BK) * nsdb::BK;
-  p.splits = 1;
-  p.act = 0; p.bias_mode = bias ? bias_mode : 0; p.out_f32 = 1; p.accumulate = 0;
-  p.alpha = alpha; p.dropout = 0.f; p.seed = 0; p.diag = g_diag & 4;
-  p.seg_k = 0; p.seg_stride_b = 0;
-  p.tiles_m = (M + 255) / 256;
-  p.tiles_n = (N + 255) / 256;
-  p.vec_ws = 0;
-  p.vec_c = (ldc % 4 == 0 && (reinterpret_cast<uintptr_t>(C) & 15) == 0) ? 1 : 0;
-  p.softmax = axis; p.sm_part = (float2*)part; p.sm_cnt = cnt; p.sm_flag = flag; p.stamps = nullptr; p.adapt = nullptr;
-  p.signal = nullptr; p.signal_value = 0; p.steal_cnt = nullptr; p.steal_tq = 0; p.steal_ch = 2;
-  const int tiles = p.tiles_m * p.tiles_n;
-  if (axis == 1) hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<20>, dim3(tiles), dim3(512), 0, stream, p);
-  else hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<21>, dim3(tiles), dim3(512), 0, stream, p);
-  hipLaunchKernelGGL(nsdb::softmax_fixup_kernel, dim3(tiles), dim3(256), 0, stream, p);
-  return (int)hipGetLastError();
-}
 
 int nsdb_study_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const float* bias,
                       int M, int N, int K, long long lda, long long ldb, long long ldc,

@@ -28,9 +28,6 @@ int nsdb_study_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, co
                       long long lda, long long ldb, long long ldc, long long sA, long long sB, long long sC,
                       long long sBias, int batch, int splits, int act, int bias_mode, int out_f32, float alpha,
                       float dropout, unsigned long long seed, int accumulate, long long seg_k, long long seg_stride_b, hipStream_t stream);
-int nsdb_study_gemm_nt_softmax(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, long long lda,
-                         long long ldb, long long ldc, int bias_mode, float alpha, int axis, void* part, int* cnt,
-                         int* flag, hipStream_t stream);
 }
 
 namespace {

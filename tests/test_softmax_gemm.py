@@ -69,7 +69,8 @@ def test_softmax_gemm_cpu_oracle_is_safe():
 @pytest.mark.parametrize("axis", [1, 2])
 @pytest.mark.parametrize("shape,mode", [((300, 700, 96), ops.BIAS_COL), ((777, 555, 4104), ops.BIAS_ROW),
                                         ((256, 256, 64), None), ((1000, 14588, 1000), ops.BIAS_COL),
-                                        ((300, 701, 64), ops.BIAS_COL)])
+                                        ((300, 701, 64), ops.BIAS_COL), ((300, 16700, 64), ops.BIAS_COL),
+                                        ((16700, 300, 64), ops.BIAS_ROW)])
 def test_softmax_gemm_vs_fp32(shape, mode, axis, epi):
     """Direct register stores (C rows 16-B aligned; N = 701 falls back to the LDS-staged store) and the
     LDS-staged final store."""
@@ -105,9 +106,9 @@ def test_softmax_gemm_large_logits_stay_finite():
 @pytest.mark.gpu
 @pytest.mark.parametrize("axis", [1, 2])
 def test_softmax_gemm_fallback_fixup(axis):
-    """Every tile takes the timed-out path (diag 4): it writes exp(x - m_tile) and the fix-up kernel rescales
-    it by exp(m_tile - M) / S; the result must still match, and the next (normal) launch must see zeroed
-    counters / flags."""
+    """Every tile takes the timed-out path (diag 4): it writes exp(x - m_tile), and the last tile of its group to
+    depart rescales it by exp(m_tile - M) / S inside the same launch (no fix-up kernel); the result must still
+    match, and the following launches (normal and timed-out, alternating) must see zeroed counters / flags."""
     M, N, K = 600, 1100, 320
     g = torch.Generator(device="cuda:0").manual_seed(3)
     A = torch.randn(M, K, device="cuda:0", generator=g).to(torch.bfloat16)
@@ -116,8 +117,9 @@ def test_softmax_gemm_fallback_fixup(axis):
     y = ops.gemm_nt_softmax(A, B, bias, ops.BIAS_COL, axis=axis, force_fallback=True)
     ref = _ref(A, B, bias, ops.BIAS_COL, axis)
     assert (y - ref).abs().max().item() / ref.abs().max().item() < 2e-5
-    y2 = ops.gemm_nt_softmax(A, B, bias, ops.BIAS_COL, axis=axis)
-    torch.testing.assert_close(y2, y, atol=1e-6, rtol=1e-5)
+    for fb in (False, True, False):
+        y2 = ops.gemm_nt_softmax(A, B, bias, ops.BIAS_COL, axis=axis, force_fallback=fb)
+        torch.testing.assert_close(y2, y, atol=1e-6, rtol=1e-5)
 
 
 @pytest.mark.gpu
