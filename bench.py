@@ -104,6 +104,9 @@ def main():
     ap.add_argument("--tail-prefetch", action="store_true",
                     help="read the output layer's weight into the Infinity Cache during layer 1's tail "
                          "(execution/streams.TailPrefetch; measured slower, off by default)")
+    ap.add_argument("--no-operand-prefetch", action="store_true",
+                    help="disable the in-kernel operand prefetch (the output layer's weight read into the Infinity "
+                         "Cache by the layer-1 GEMM's workgroups as they finish)")
     ap.add_argument("--inflight", type=int, default=1,
                     help="FF steps in flight: step i's FF jobs go to job lane i %% inflight (>1 pipelines "
                          "consecutive batches: step i+1's layer-1 GEMM starts while step i's tail kernels run)")
@@ -125,6 +128,7 @@ def main():
     client = PDBClient(ctx=ctx, root=root, device=ctx.device)
     dev = ctx.device
     client.engine.tail_prefetch = bool(args.tail_prefetch)
+    client.engine.operand_prefetch = not args.no_operand_prefetch
 
     # ---- data (per-rank partition of the inputs, replicated model) ----
     ff.load_model(client, "ff", cfg["batch"] * ctx.world_size, cfg["features"], cfg["hidden"], cfg["labels"],
@@ -266,6 +270,7 @@ def main():
                 "graph_replay": captured is not None,
                 "single_job": bool(args.single_job),
                 "tail_prefetch": bool(args.tail_prefetch),
+                "operand_prefetch": not args.no_operand_prefetch,
             },
         }
         print(json.dumps(res), flush=True)

@@ -75,6 +75,8 @@ struct GemmOpts {
   unsigned* signal;
   unsigned signal_value;
   int epi;
+  const void* pf_ptr;
+  long long pf_bytes;
 };
 
 void check_rc(int rc, const char* what) {
@@ -97,7 +99,8 @@ bool is_f32(const torch::Tensor& t, const char* name) {
 torch::Tensor gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Tensor> bias, int64_t bias_mode,
                       int64_t act, bool out_f32, double alpha, double dropout, int64_t seed, int64_t splits,
                       c10::optional<torch::Tensor> out, bool accumulate, int64_t cfg,
-                      c10::optional<torch::Tensor> signal, int64_t signal_value, int64_t epi) {
+                      c10::optional<torch::Tensor> signal, int64_t signal_value, int64_t epi,
+                      c10::optional<torch::Tensor> prefetch) {
   check_cuda(A, "A");
   check_cuda(B, "B");
   TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && B.scalar_type() == torch::kBFloat16, "A,B must be bf16");
@@ -149,12 +152,20 @@ torch::Tensor gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Ten
     wsp = ws.data_ptr<float>();
   }
   TORCH_CHECK(epi >= -1 && epi <= 1, "gemm_nt: epi must be -1 (auto), 0 (LDS-staged) or 1 (direct)");
-  GemmOpts o{(int)cfg, nullptr, 0u, (int)epi};
+  GemmOpts o{(int)cfg, nullptr, 0u, (int)epi, nullptr, 0};
   if (signal.has_value() && signal->defined()) {
     check_cuda(*signal, "signal");
     TORCH_CHECK(signal->scalar_type() == torch::kInt32 && signal->numel() >= 1, "signal must be an int32 flag");
     o.signal = reinterpret_cast<unsigned*>(signal->data_ptr());
     o.signal_value = (unsigned)signal_value;
+  }
+  if (prefetch.has_value() && prefetch->defined() && prefetch->numel() > 0) {
+    // the byte span of the tensor's elements (a strided view reads its whole span)
+    check_cuda(*prefetch, "prefetch");
+    int64_t last = 0;
+    for (int64_t d = 0; d < prefetch->dim(); ++d) last += (prefetch->size(d) - 1) * prefetch->stride(d);
+    o.pf_ptr = prefetch->data_ptr();
+    o.pf_bytes = (last + 1) * (long long)prefetch->element_size();
   }
   const int rc = nsdb_gemm_nt_bf16(
       A.data_ptr(), B.data_ptr(), C.data_ptr(), wsp, bptr, (int)M, (int)N, (int)K, A.stride(-2), B.stride(-2),
@@ -626,7 +637,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bias_mode") = 0, py::arg("act") = 0, py::arg("out_f32") = false, py::arg("alpha") = 1.0,
         py::arg("dropout") = 0.0, py::arg("seed") = 0, py::arg("splits") = 0, py::arg("out") = py::none(),
         py::arg("accumulate") = false, py::arg("cfg") = -1, py::arg("signal") = py::none(),
-        py::arg("signal_value") = 0, py::arg("epi") = -1);
+        py::arg("signal_value") = 0, py::arg("epi") = -1, py::arg("prefetch") = py::none());
   m.def("prefetch", &prefetch, "warm the caches with a read of each tensor", py::arg("tensors"), py::arg("sink"),
         py::arg("blocks") = 64);
   m.def("gemm_nt_f32", &gemm_nt_f32, "alpha * A.B^T (+C) on the exact-f32 MFMA (16x16x4)", py::arg("A"),

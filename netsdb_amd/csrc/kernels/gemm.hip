@@ -58,8 +58,11 @@ __host__ __device__ __forceinline__ int sm_need_pad(int need) { return (need + 1
 //   [2560, 3072)   second half of the combine [256][2]
 //   [3072, 3584)   final (max, 1/sum) per line [256][2]
 //   [3584]         poll verdict
+//   [SM_BIAS, +2 KiB)   the tile's column bias [256] and row bias [256], staged at launch (before the main loop's
+//                       first barrier), so the epilogue does not wait on global loads
 constexpr int SM_ST = 131072;
-constexpr int SM_LDS = SM_ST + 3600 * 4;              // LDS bytes of a fused-softmax launch
+constexpr int SM_BIAS = SM_ST + 3600 * 4;
+constexpr int SM_LDS = SM_BIAS + 2048;                // LDS bytes of a fused-softmax launch
 
 // Final (max M, 1/sum S) per line of a softmax group into fin[256][2]: the group's partials ([256 lines][npad]
 // float2, contiguous) come into LDS by LDS-DMA (no VGPRs: the tile's logits hold 128 of them), 64 partials per
@@ -117,6 +120,7 @@ __device__ __forceinline__ bool softmax_epilogue_8ph(f32x4 (&acc)[8][4], char* s
   // transposed accumulator layout (TS): acc[i][j][r] = C[wr*128 + i*16 + rl][wc*64 + j*16 + cq + r]
   const int wr = wave >> 2, wc = wave & 3;
   const int rl = lane & 15, cq = (lane >> 4) * 4;
+  const float* sbias = reinterpret_cast<const float*>(smem + SM_BIAS);   // [256 column | 256 row] bias of the tile
   // 1. logits in registers (invalid rows / columns -> -inf: they never win a max and exp to 0). Per-row or
   // per-column bias only (host-checked)
   float bcol[4][4];
@@ -125,13 +129,13 @@ __device__ __forceinline__ bool softmax_epilogue_8ph(f32x4 (&acc)[8][4], char* s
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int col = n0 + wc * 64 + j * 16 + cq + r;
-      bcol[j][r] = (p.bias && p.bias_mode == 2) ? p.bias[min(col, p.N - 1)] : 0.f;
+      bcol[j][r] = sbias[wc * 64 + j * 16 + cq + r];     // staged in LDS at launch (0 without a column bias)
       if (col >= p.N) bcol[j][r] = -INFINITY;
     }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int row = m0 + wr * 128 + i * 16 + rl;
-    float brow = (p.bias && p.bias_mode == 1) ? p.bias[min(row, p.M - 1)] : 0.f;
+    float brow = sbias[256 + wr * 128 + i * 16 + rl];
     if (row >= p.M) brow = -INFINITY;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -369,10 +373,34 @@ __device__ __forceinline__ void sm_depart(const GemmParams& p, char* smem, bool 
 // all-at-once tail (228 tiles ending together) paid ~2x the bare store stream for it (scripts/native/
 // store_gemm2: 10-12 us for the 58 MB stream either way). Bias (per row / per column) is loaded into
 // registers before the first store (a load behind stores waits for them: vmcnt is in order).
-__device__ __forceinline__ void store_direct_8ph(const f32x4 (&acc)[8][4], const GemmParams& p, int batch, int m0,
-                                                 int n0, int lane, int wave) {
+// Split-K launches store their raw f32 slab the same way (the reducer applies the epilogue): no LDS image, so no
+// compiler-inserted vmcnt drain before each LDS read of the staged store loop (which also made that loop wait for
+// its own earlier stores and for anything else in flight, e.g. an operand prefetch).
+__device__ __forceinline__ void store_direct_8ph(const f32x4 (&acc)[8][4], const GemmParams& p, int batch, int split,
+                                                 int m0, int n0, int lane, int wave) {
   const int wr = wave >> 2, wc = wave & 3;
   const int rl = lane & 15, cq = (lane >> 4) * 4;
+  if (p.splits > 1) {
+    float* ws = p.ws + ((long long)batch * p.splits + split) * (long long)p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = m0 + wr * 128 + i * 16 + rl;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = n0 + wc * 64 + j * 16 + cq;
+        if (row < p.M && col < p.N) {
+          float* d = ws + (long long)row * p.N + col;
+          if (col + 4 <= p.N) *reinterpret_cast<f32x4*>(d) = acc[i][j];   // N % 4 == 0 (host: vec_ws)
+          else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (col + r < p.N) d[r] = acc[i][j][r];
+          }
+        }
+      }
+    }
+    return;
+  }
   const float* bias = p.bias ? p.bias + batch * p.sBias : nullptr;
   const float keep_scale = p.dropout > 0.f ? 1.f / (1.f - p.dropout) : 1.f;
   f32x4 bc[4];
@@ -570,8 +598,9 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   const unsigned long long t_entry = EPI != 0 ? __builtin_amdgcn_s_memrealtime() : 0ull;
   constexpr int HALF = 128 * 128;            // bytes of one half-tile (128 rows x 64 bf16)
   constexpr int BUF = 4 * HALF;              // one K-tile
-  // + the epilogue's bias (store_tile_lds), or the fused softmax's line statistics (SM_LDS)
-  __shared__ __attribute__((aligned(16))) char smem[EPI != 0 ? SM_LDS : 2 * BUF + 1024];
+  // + the epilogue's bias (store_tile_lds) and the operand-prefetch sink (1 KiB per wave), or the fused softmax's
+  // line statistics (SM_LDS)
+  __shared__ __attribute__((aligned(16))) char smem[EPI != 0 ? SM_LDS : 2 * BUF + 1024 + 8 * 1024];
 
   const int ntiles = p.tiles_m * p.tiles_n;
   const int wg = xcd_remap(blockIdx.x, ntiles * p.splits);
@@ -614,6 +643,15 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
       roff[2 + q][i] = tb < rows_b ? (int)((long long)tb * p.ldb * 2) : -1;
     }
 
+  // fused softmax: the tile's per-column (threads 0-255) / per-row (256-511) bias, loaded before the prologue's DMAs
+  // and written to LDS after its wait (read by the epilogue, after the main loop's barriers)
+  float bias_v = 0.f;
+  if constexpr (EPI != 0) {
+    const int c = tid & 255;
+    const int idx = tid < 256 ? n0 + c : m0 + c;
+    const bool use = p.bias && (tid < 256 ? (p.bias_mode == 2 && idx < p.N) : (p.bias_mode == 1 && idx < p.M));
+    if (use) bias_v = p.bias[idx];
+  }
   auto stage = [&](int buf, int slot, int u) {
     const int k = kbeg + u * BK + kc;
     const bool kin = k < kend;
@@ -693,6 +731,7 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   stage(0, 2, 0); stage(0, 0, 0); stage(0, 3, 0); stage(0, 1, 0);
   stage(1, 2, 1); stage(1, 0, 1); stage(1, 3, 1);
   asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  if constexpr (EPI != 0) reinterpret_cast<float*>(smem + SM_BIAS)[tid] = bias_v;   // [256 col | 256 row]
   NSDB_BARRIER();
   if (wr == 1) NSDB_BARRIER();            // stagger the two wave groups by one barrier
   for (int it = 0; it < niter; ++it) {
@@ -703,6 +742,26 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // trailing zero-fill DMAs land before LDS reuse
   if (p.signal != nullptr && tid == 0)    // tail trigger: this CU frees up soon
     __hip_atomic_fetch_max(p.signal, p.signal_value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if constexpr (EPI == 0) {
+    // Operand prefetch (per launch, GemmParams::pf_ptr): the next kernel's operand (the FF output weight after
+    // layer 1, whose 2.4 GB stream evicts it) is read into the Infinity Cache by this launch's workgroups as each
+    // finishes its main loop, spread over the launch's tail. 1/nwg of the bytes per workgroup, LDS-DMA into a
+    // 1 KiB sink per wave (no VGPRs; the sink is disjoint from the epilogue's LDS image); the loads stay in
+    // flight under the epilogue's stores and retire before the wave ends.
+    if (p.pf_ptr != nullptr) {
+      const long long nwg = (long long)gridDim.x * gridDim.z;
+      const long long wid = (long long)blockIdx.z * gridDim.x + blockIdx.x;
+      const long long chunk = ((p.pf_bytes + nwg - 1) / nwg + 1023) & ~1023LL;
+      const long long beg = wid * chunk;
+      if (beg < p.pf_bytes) {
+        const int len = (int)min(chunk, p.pf_bytes - beg);
+        const __amdgpu_buffer_rsrc_t rf = make_rsrc(p.pf_ptr + beg, (unsigned)len);
+        char* sink = smem + 2 * BUF + 1024 + wave * 1024;
+        for (int off = wave * 1024; off < len; off += 8 * 1024)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rf, (lds_void*)sink, 16, off + lane * 16, 0, 0, 0);
+      }
+    }
+  }
   if constexpr (EPI != 0) {
     // the fused softmax turns acc into the final values in place; the common store then runs with a plain
     // (alpha 1, no bias/act/dropout, f32) epilogue
@@ -715,7 +774,7 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
     if (ok) sm_depart<EPI>(p, smem, true, tm, tn, tid, lane, wave);
     GemmParams q = p;
     q.alpha = 1.f; q.bias = nullptr; q.act = 0; q.dropout = 0.f; q.accumulate = 0; q.out_f32 = 1; q.splits = 1;
-    if (p.direct_epi) store_direct_8ph(acc, q, 0, m0, n0, lane, wave);
+    if (p.direct_epi) store_direct_8ph(acc, q, 0, 0, m0, n0, lane, wave);
     else store_tile_lds<256, 256, 2, 4, true>(acc, smem, 2 * BUF, q, 0, 0, m0, n0, tid, lane, wave);
     if (!ok) sm_depart<EPI>(p, smem, false, tm, tn, tid, lane, wave);
     if (stamp) {
@@ -731,11 +790,12 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
     return;
   }
   if (p.direct_epi) {
-    store_direct_8ph(acc, p, batch, m0, n0, lane, wave);
-    return;
+    store_direct_8ph(acc, p, batch, split, m0, n0, lane, wave);
+  } else {
+    store_tile_lds<256, 256, 2, 4, true>(acc, smem, 2 * BUF, p, batch, split, m0, n0, tid, lane, wave,
+                                         reinterpret_cast<float*>(smem + 2 * BUF));
   }
-  store_tile_lds<256, 256, 2, 4, true>(acc, smem, 2 * BUF, p, batch, split, m0, n0, tid, lane, wave,
-                                       reinterpret_cast<float*>(smem + 2 * BUF));
+  if (p.pf_ptr != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // prefetch DMAs retired
 }
 
 
@@ -829,6 +889,8 @@ struct GemmOpts {
   unsigned* signal;         // tail trigger of this launch (8-phase only), or nullptr
   unsigned signal_value;
   int epi;                  // 8-phase unsplit epilogue: -1 auto (direct), 0 LDS-staged, 1 direct register stores
+  const void* pf_ptr;       // operand prefetch of this launch (8-phase only): pf_bytes at pf_ptr, or nullptr
+  long long pf_bytes;
 };
 
 extern "C" {
@@ -960,15 +1022,21 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
   p.vec_ws = (N % 4 == 0) ? 1 : 0;
   p.vec_c = (ldc % 4 == 0 && sC % 4 == 0 &&
              (reinterpret_cast<uintptr_t>(C) & (out_f32 ? 15 : 7)) == 0) ? 1 : 0;
-  // the direct register epilogue for unsplit 8-phase launches with aligned C rows (opts->epi: -1 auto = direct,
-  // 0 = LDS-staged, 1 = direct); split-K slabs, C += A.B^T and per-element bias keep the LDS-staged epilogue
+  // the direct register epilogue for unsplit 8-phase launches with aligned C rows and for split-K slabs (opts->epi:
+  // -1 auto = direct, 0 = LDS-staged, 1 = direct); C += A.B^T and per-element bias keep the LDS-staged epilogue
   const int epi_pref = opts ? opts->epi : -1;
-  p.direct_epi = (cfg == 2 && p.splits == 1 && !accumulate && p.vec_c && p.bias_mode != 3 && epi_pref != 0) ? 1 : 0;
+  // split-K slabs (N % 4 == 0) take the direct stores too
+  p.direct_epi = (cfg == 2 && epi_pref != 0 &&
+                  ((p.splits == 1 && !accumulate && p.vec_c && p.bias_mode != 3) || (p.splits > 1 && p.vec_ws))) ? 1 : 0;
   dim3 grid(p.tiles_m * p.tiles_n * p.splits, 1, batch);
   if (cfg == 2) {
     if (opts && opts->signal) {            // this launch's tail trigger (the caller checked eligibility)
       p.signal = opts->signal;
       p.signal_value = opts->signal_value;
+    }
+    if (opts && opts->pf_ptr && opts->pf_bytes > 0) {   // this launch's operand prefetch
+      p.pf_ptr = (const char*)opts->pf_ptr;
+      p.pf_bytes = opts->pf_bytes;
     }
     hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<0>, grid, dim3(512), 0, stream, p);
   } else {

@@ -41,7 +41,9 @@ struct GemmParams {
   float2* sm_part;
   int* sm_cnt;
   int* sm_flag;
-  int* sm_dep;               // fused softmax: departures (low 16 bits) + timed-out tiles (high 16) per group
+  int* sm_dep = nullptr;     // fused softmax: departures (low 16 bits) + timed-out tiles (high 16) per group
+  const char* pf_ptr = nullptr;   // operand prefetch for the NEXT kernel (8-phase, EPI 0): bytes read into the
+  long long pf_bytes = 0;         // Infinity Cache by the workgroups after their main loops
   unsigned long long* stamps;   // diagnostic variant 12: per-workgroup real-time stamps every 32 k-tiles
   struct AdaptState* adapt;     // split-K: launch-to-launch adaptive K partition (see AdaptState)
   // tail trigger (8-phase kernel): every workgroup raises *signal to signal_value (atomic max) when its main

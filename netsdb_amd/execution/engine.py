@@ -112,6 +112,9 @@ class QueryEngine:
         # evaluated before it (query_planning/fusion.py MatmulNode._tail_prefetch). Off by default: measured
         # slower in the bench (profiles/r3_s2: 1.021 vs 0.992 ms per step)
         self.tail_prefetch = False
+        # in-kernel operand prefetch: the weight of such a later GEMM is read into the Infinity Cache by the
+        # workgroups of the long GEMM before it as they finish (ops.gemm_nt / gemm.hip GemmParams::pf_ptr)
+        self.operand_prefetch = True
         self.last_tcap = None
         self._last_comps = None
 
@@ -119,7 +122,8 @@ class QueryEngine:
         """An engine for another job lane: same storage, context, catalog, tracer, configuration and plan cache
         (dict access under the GIL); its own per-job state (spools, statistics)."""
         e = QueryEngine(self.storage, self.ctx, self.catalog, self.tracer, self.broadcast_threshold, self.fusion)
-        for k in ("adaptive", "plan_cache_enabled", "ooc_fraction", "shuffle_chunk_bytes", "tail_prefetch"):
+        for k in ("adaptive", "plan_cache_enabled", "ooc_fraction", "shuffle_chunk_bytes", "tail_prefetch",
+                  "operand_prefetch"):
             setattr(e, k, getattr(self, k))
         e._plan_cache = self._plan_cache
         e.__dict__["meta_cache"] = self.__dict__.setdefault("meta_cache", {})

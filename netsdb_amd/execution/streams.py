@@ -53,6 +53,34 @@ def armed_trigger(device) -> Optional["TailTrigger"]:
         return _armed.get(_stream_key(device))
 
 
+# operand prefetches armed per (device, stream): ops.gemm_nt hands the tensor to the first long 8-phase GEMM enqueued
+# on THAT stream, whose workgroups read it into the Infinity Cache as they finish (gemm.hip GemmParams::pf_ptr)
+_armed_pf: Dict[Tuple[int, int], torch.Tensor] = {}
+
+
+def arm_operand_prefetch(tensor: torch.Tensor):
+    """Arm ``tensor`` (a later kernel's operand on the current stream) for the next long GEMM on this stream."""
+    if not isinstance(tensor, torch.Tensor) or not tensor.is_cuda:
+        return False
+    with _armed_lock:
+        _armed_pf[_stream_key(tensor.device)] = tensor
+    return True
+
+
+def disarm_operand_prefetch(device):
+    if _armed_pf and torch.device(device).type == "cuda":
+        with _armed_lock:
+            _armed_pf.pop(_stream_key(device), None)
+
+
+def take_operand_prefetch(device) -> Optional[torch.Tensor]:
+    """The operand prefetch armed on the current stream of ``device`` (removed: one launch takes it)."""
+    if not _armed_pf or torch.device(device).type != "cuda":
+        return None
+    with _armed_lock:
+        return _armed_pf.pop(_stream_key(device), None)
+
+
 class JobHandle:
     def __init__(self, result, event: Optional["torch.cuda.Event"], stream: Optional["torch.cuda.Stream"],
                  device=None):

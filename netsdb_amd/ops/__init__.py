@@ -86,8 +86,10 @@ def gemm_nt(A, B, bias=None, bias_mode=BIAS_NONE, act=ACT_NONE, out_dtype=torch.
     bias f32 per row/col. ``accumulate`` adds into an existing f32 ``out`` (C += A.B^T). ``cfg`` forces the
     tile config of THIS call (0 = 128x128, 2 = 256x256 8-phase; None = auto); ``epi`` the 8-phase kernel's
     unsplit epilogue (0 = LDS-staged, 1 = direct register stores; None = auto: direct). A tail trigger armed on the
-    current stream (execution/streams.TailTrigger) is handed to this launch when the launch is long enough to
-    take it — per call and per stream, so GEMMs on other lanes or threads never see it."""
+    current stream (execution/streams.TailTrigger) and an armed operand prefetch (streams.arm_operand_prefetch: a
+    later kernel's operand read into the Infinity Cache by this launch's workgroups as they finish) are handed to
+    this launch when it is long enough to take them — per call and per stream, so GEMMs on other lanes or threads
+    never see them."""
     act = act_code(act)
     if _use_hip(A, B):
         if bias is not None and bias.dtype != torch.float32:
@@ -95,18 +97,22 @@ def gemm_nt(A, B, bias=None, bias_mode=BIAS_NONE, act=ACT_NONE, out_dtype=torch.
         A, B = gemm_operands(A, B)
         h = _ext.hip()
         c = -1 if cfg is None else int(cfg)
-        sig, sval = None, 0
-        from ..execution.streams import armed_trigger
+        sig, sval, pf = None, 0, None
+        from ..execution import streams
 
-        trig = armed_trigger(A.device)
-        if trig is not None:
+        trig = streams.armed_trigger(A.device)
+        pf_armed = bool(streams._armed_pf)
+        if trig is not None or pf_armed:
             M, N, K = A.shape[-2], B.shape[-2], A.shape[-1]
             batch = A.shape[0] if A.dim() == 3 else 1
             if h.gemm_tail_eligible(M, N, K, batch, int(splits), c):
-                sig, sval = trig.take()
+                if trig is not None:
+                    sig, sval = trig.take()
+                if pf_armed:
+                    pf = streams.take_operand_prefetch(A.device)
         return h.gemm_nt(A, B, bias, int(bias_mode if bias is not None else 0), act,
                          out_dtype == torch.float32, float(alpha), float(dropout), int(seed),
-                         int(splits), out, bool(accumulate), c, sig, int(sval), -1 if epi is None else int(epi))
+                         int(splits), out, bool(accumulate), c, sig, int(sval), -1 if epi is None else int(epi), pf)
     v = torch.matmul(A.float(), B.float().transpose(-1, -2)) * alpha
     if bias is not None:
         b = bias.float()

@@ -149,7 +149,14 @@ class MatmulNode(Node):
         if self.value is not None:
             return self.value
         pf = self._tail_prefetch(engine)
-        A, B = self.a.eval(engine), self.b.eval(engine)
+        armed = self._arm_operand_prefetch(engine) if pf is None else None
+        try:
+            A, B = self.a.eval(engine), self.b.eval(engine)
+        finally:
+            if armed is not None:
+                from ..execution.streams import disarm_operand_prefetch
+
+                disarm_operand_prefetch(armed)
         if pf is not None:
             pf.launched()
         try:
@@ -158,21 +165,43 @@ class MatmulNode(Node):
             if pf is not None:
                 pf.end()
 
-    def _tail_prefetch(self, engine):
-        """One operand is a stored weight set and the other comes out of a GEMM evaluated first (the FF output
-        layer after layer 1): warm the weight into the Infinity Cache during that GEMM's tail
-        (streams.TailPrefetch). Engine option ``tail_prefetch`` (default off: measured slower in the bench)."""
-        if not getattr(engine, "tail_prefetch", False) or engine.ctx.distributed:
-            return None
+    def _prefetch_weight(self, engine):
+        """The stored weight operand of a GEMM whose other operand comes out of a GEMM evaluated first (the FF
+        output layer after layer 1), when it is worth warming (on the GPU, >= 4 MiB); else None."""
         srcs = [c for c in (self.a, self.b) if isinstance(c, SourceNode)]
         heavy = [c for c in (self.a, self.b) if isinstance(c, (MatmulNode, BiasActNode, EwiseNode))]
-        if len(srcs) != 1 or len(heavy) != 1:
+        if len(srcs) != 1 or len(heavy) != 1 or heavy[0].value is not None:
             return None
         try:
             w = srcs[0].eval(engine).phys
         except Exception:
             return None
         if not isinstance(w, torch.Tensor) or not w.is_cuda or w.numel() * w.element_size() < (4 << 20):
+            return None
+        return w
+
+    def _arm_operand_prefetch(self, engine):
+        """In-kernel operand prefetch (engine option ``operand_prefetch``, default on): the weight is armed on the
+        current stream, and the first long 8-phase GEMM launched while the children are evaluated (layer 1)
+        reads it into the Infinity Cache with its workgroups as they finish (ops.gemm_nt). Returns the device to
+        disarm, or None."""
+        if not getattr(engine, "operand_prefetch", False):
+            return None
+        w = self._prefetch_weight(engine)
+        if w is None:
+            return None
+        from ..execution.streams import arm_operand_prefetch
+
+        return w.device if arm_operand_prefetch(w) else None
+
+    def _tail_prefetch(self, engine):
+        """One operand is a stored weight set and the other comes out of a GEMM evaluated first (the FF output
+        layer after layer 1): warm the weight into the Infinity Cache during that GEMM's tail
+        (streams.TailPrefetch). Engine option ``tail_prefetch`` (default off: measured slower in the bench)."""
+        if not getattr(engine, "tail_prefetch", False) or engine.ctx.distributed:
+            return None
+        w = self._prefetch_weight(engine)
+        if w is None:
             return None
         pf = engine.__dict__.get("_tail_prefetch")
         if pf is None:
