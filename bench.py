@@ -144,18 +144,14 @@ def main():
     prio = args.job_priority if args.job_priority is not None else (0 if tail else -1)
     client.job_lane_priority = {conv_lane: prio}
     conv_blocks = args.conv_blocks if args.conv_blocks is not None else (0 if tail else None)
-    if conv_blocks is not None and dev.type == "cuda":
-        from netsdb_amd import _ext
+    # kernel launch options: a per-call scope for this (the only) host thread; the library keeps no global state
+    from netsdb_amd import ops
 
-        _ext.hip().conv2d_max_blocks(conv_blocks)
-    if args.conv_kernel is not None and dev.type == "cuda":
-        from netsdb_amd import _ext
-
-        _ext.hip().conv2d_rowfull({"rows": 0, "rowfull": 1, "warpspec": 5}[args.conv_kernel])
-    if args.rownorm_loads is not None and dev.type == "cuda":
-        from netsdb_amd import _ext
-
-        _ext.hip().rownorm_plain_loads(1 if args.rownorm_loads == "plain" else 0)
+    kscope = ops.kernel_options(
+        conv_blocks=conv_blocks,
+        conv_kernel=None if args.conv_kernel is None else {"rows": 0, "rowfull": 1, "warpspec": 5}[args.conv_kernel],
+        rownorm_plain_loads=None if args.rownorm_loads is None else args.rownorm_loads == "plain")
+    kscope.__enter__()
     main_stream = None
     if tail and dev.type == "cuda":
         # FF jobs on a high-priority stream: when conv blocks and the FF tail kernels both wait for CUs, the

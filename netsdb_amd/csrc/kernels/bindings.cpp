@@ -25,20 +25,17 @@ int nsdb_gemm_nt_softmax(const void* A, const void* B, float* C, const float* bi
                          hipStream_t stream);
 int nsdb_gemm_nt_f32(const float* A, const float* B, float* C, int M, int N, int K, long long lda, long long ldb,
                      long long ldc, float alpha, int accumulate, hipStream_t stream);
+struct ConvOpts {
+  int force_generic, variant, max_blocks, kernel, contig;
+};
 int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* out, int N, int C, int H, int W,
                       int OC, int KH, int KW, int stride, int pad, int dil, int ldw, int act, int nchw_out,
-                      int out_f32, const void* wfrag, hipStream_t stream);
-extern int nsdb_conv2d_force_generic;
-extern int nsdb_conv2d_variant;
-extern int nsdb_conv2d_max_blocks;
-extern int nsdb_conv2d_rowfull;
-extern int nsdb_conv2d_contig;
-extern int nsdb_rownorm_plain_loads;
+                      int out_f32, const void* wfrag, const struct ConvOpts* opts, hipStream_t stream);
 int nsdb_prefetch(const void* ptr, long long bytes, unsigned* sink, int blocks, hipStream_t stream);
 int nsdb_im2col(const void* X, void* out, int N, int C, int H, int W, int KH, int KW, int stride, int pad, int dil,
                 int ldk, hipStream_t stream);
 int nsdb_softmax_rows(const void* X, int x_f32, const float* bias, void* Y, int y_f32, int R, int N,
-                      long long ldx, long long ldy, int log_out, hipStream_t st);
+                      long long ldx, long long ldy, int log_out, int plain_loads, hipStream_t st);
 int nsdb_bias_act(const void* X, int x_f32, const float* bias, void* Y, int y_f32, int R, int N, int bias_mode,
                   int act, float dropout, unsigned long long seed, hipStream_t st);
 int nsdb_lstm_ew(int mode, const float* a, const float* b, const float* c, const float* d, float* out, long long n,
@@ -328,7 +325,8 @@ int64_t gemm_splits(int64_t M, int64_t N, int64_t K, int64_t batch, int64_t cfg)
 
 torch::Tensor conv2d(torch::Tensor X, torch::Tensor Wt, c10::optional<torch::Tensor> bias, int64_t KH, int64_t KW,
                      int64_t stride, int64_t pad, int64_t dil, int64_t act, bool nchw_out, bool out_f32,
-                     c10::optional<torch::Tensor> wfrag) {
+                     c10::optional<torch::Tensor> wfrag, int64_t kernel, int64_t max_blocks, bool force_generic,
+                     int64_t variant, int64_t contig) {
   check_cuda(X, "X");
   check_cuda(Wt, "W");
   TORCH_CHECK(X.scalar_type() == torch::kBFloat16 && Wt.scalar_type() == torch::kBFloat16, "X,W must be bf16");
@@ -353,11 +351,14 @@ torch::Tensor conv2d(torch::Tensor X, torch::Tensor Wt, c10::optional<torch::Ten
                     wfrag->numel() == ((OC + 63) / 64) * 4 * 6 * 64 * 8, "wfrag must be the packed [OC/64][4][6][64][8] filter");
     fptr = wfrag->data_ptr();
   }
+  // per-call kernel options (-1: the library default)
+  const ConvOpts o{force_generic ? 1 : 0, (int)variant, max_blocks < 0 ? 512 : (int)max_blocks, kernel < 0 ? 5 : (int)kernel,
+                   (int)contig};
   auto opts = X.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16);
   torch::Tensor out = nchw_out ? torch::empty({N, OC, OH, OW}, opts) : torch::empty({N * OH * OW, OC}, opts);
   check_rc(nsdb_conv2d_igemm(X.data_ptr(), Wt.data_ptr(), bptr, out.data_ptr(), (int)N, (int)C, (int)H, (int)W,
                              (int)OC, (int)KH, (int)KW, (int)stride, (int)pad, (int)dil, (int)ldw, (int)act,
-                             nchw_out ? 1 : 0, out_f32 ? 1 : 0, fptr, cur_stream()),
+                             nchw_out ? 1 : 0, out_f32 ? 1 : 0, fptr, &o, cur_stream()),
            "conv2d");
   return out;
 }
@@ -390,7 +391,8 @@ void prefetch(std::vector<torch::Tensor> ts, torch::Tensor sink, int64_t blocks)
   }
 }
 
-torch::Tensor softmax_rows(torch::Tensor X, c10::optional<torch::Tensor> bias, bool out_f32, int64_t mode) {
+torch::Tensor softmax_rows(torch::Tensor X, c10::optional<torch::Tensor> bias, bool out_f32, int64_t mode,
+                           bool plain_loads) {
   check_cuda(X, "X");
   TORCH_CHECK(X.dim() == 2 && X.stride(-1) == 1, "X must be 2-D row-contiguous");
   const bool xf = is_f32(X, "X");
@@ -401,7 +403,7 @@ torch::Tensor softmax_rows(torch::Tensor X, c10::optional<torch::Tensor> bias, b
   }
   auto Y = torch::empty({X.size(0), X.size(1)}, X.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16));
   check_rc(nsdb_softmax_rows(X.data_ptr(), xf, bptr, Y.data_ptr(), out_f32, (int)X.size(0), (int)X.size(1),
-                             X.stride(0), Y.stride(0), (int)mode, cur_stream()),
+                             X.stride(0), Y.stride(0), (int)mode, plain_loads ? 1 : 0, cur_stream()),
            "softmax_rows");
   return Y;
 }
@@ -656,23 +658,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("bias_mode") = 0, py::arg("axis") = 1,
         py::arg("out") = py::none(), py::arg("alpha") = 1.0, py::arg("force_fallback") = false, py::arg("epi") = -1,
         py::arg("stamps") = py::none());
-  m.def("conv2d_force_generic", [](int64_t v) { nsdb_conv2d_force_generic = (int)v; },
-        "1: route every conv2d to the generic gather kernel (A/B testing)");
-  m.def("conv2d_max_blocks", [](int64_t v) { const int old = nsdb_conv2d_max_blocks; nsdb_conv2d_max_blocks = (int)v; return old; },
-        "row-kernel grid cap (0 = one block per row group); returns the previous value");
-  m.def("rownorm_plain_loads", [](int64_t v) { const int o = nsdb_rownorm_plain_loads; nsdb_rownorm_plain_loads = (int)v; return o; },
-        "row normalise: cache-allocating (1) or non-temporal (0) row loads; returns the previous value");
-  m.def("conv2d_contig", [](int64_t v) { const int o = nsdb_conv2d_contig; nsdb_conv2d_contig = (int)v; return o; },
-        "full-row conv: contiguous row-group runs per block (1) or grid stride (0); returns the previous value");
-  m.def("conv2d_rowfull", [](int64_t v) { const int old = nsdb_conv2d_rowfull; nsdb_conv2d_rowfull = (int)v; return old; },
-        "full-row conv kernel on/off (A/B); returns the previous value");
-  m.def("conv2d_variant", [](int64_t v) { nsdb_conv2d_variant = (int)v; }, "row-kernel diagnostic variant");
   m.def("conv2d", &conv2d, py::arg("X"), py::arg("W"), py::arg("bias") = py::none(), py::arg("KH") = 1,
         py::arg("KW") = 1, py::arg("stride") = 1, py::arg("pad") = 0, py::arg("dil") = 1, py::arg("act") = 0,
-        py::arg("nchw_out") = false, py::arg("out_f32") = false, py::arg("wfrag") = py::none());
+        py::arg("nchw_out") = false, py::arg("out_f32") = false, py::arg("wfrag") = py::none(), py::arg("kernel") = -1,
+        py::arg("max_blocks") = -1, py::arg("force_generic") = false, py::arg("variant") = 0, py::arg("contig") = 0);
   m.def("im2col", &im2col);
   m.def("softmax_rows", &softmax_rows, py::arg("X"), py::arg("bias") = py::none(), py::arg("out_f32") = true,
-        py::arg("mode") = 0);
+        py::arg("mode") = 0, py::arg("plain_loads") = false);
   m.def("bias_act", &bias_act, py::arg("X"), py::arg("bias") = py::none(), py::arg("bias_mode") = 2,
         py::arg("act") = 0, py::arg("dropout") = 0.0, py::arg("seed") = 0, py::arg("out_f32") = false);
   m.def("gemm_nt_bseg", &gemm_nt_bseg, py::arg("A"), py::arg("Bg"), py::arg("bias") = py::none(),

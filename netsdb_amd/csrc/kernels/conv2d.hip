@@ -1127,20 +1127,24 @@ __global__ void im2col_kernel(const unsigned short* X, unsigned short* out, int 
 
 extern "C" {
 
-int nsdb_conv2d_force_generic = 0;   // 1: always use the generic gather kernel (A/B, tests)
-int nsdb_conv2d_variant = 0;         // row-kernel diagnostics (timing only)
-// row kernel grid cap: > 0 persistent blocks (default 2 per CU: the filter prologue is paid once per block);
-// 0 = one block per row group (short-lived blocks that the dispatcher can interleave with higher-priority
-// kernels when the conv shares the GPU with another job, e.g. gated into a GEMM's tail)
-int nsdb_conv2d_max_blocks = 512;
-// row-kernel choice for 97 <= OW <= 112: 5 = warp-specialised (default), 1 = full-row, 0 = two-pass; 2/3/4/6 are
-// diagnostics (phase stamps, unpipelined stores)
-int nsdb_conv2d_rowfull = 5;
-int nsdb_conv2d_contig = 0;          // full-row kernel: contiguous row-group runs per block (A/B)
+// Per-call launch options (no process-wide state: a choice applies to exactly the call that passes it).
+struct ConvOpts {
+  int force_generic;   // 1: the generic gather kernel (A/B, tests)
+  int variant;         // row-kernel diagnostics (timing only)
+  // row kernel grid cap: > 0 persistent blocks (default 512 = 2 per CU: the filter prologue is paid once per block);
+  // 0 = one block per row group (short-lived blocks that the dispatcher can interleave with higher-priority
+  // kernels when the conv shares the GPU with another job, e.g. gated into a GEMM's tail)
+  int max_blocks;
+  // row-kernel choice for 97 <= OW <= 112: 5 = warp-specialised (default), 1 = full-row, 0 = two-pass; 2/3/4/6 are
+  // diagnostics (phase stamps, unpipelined stores)
+  int kernel;
+  int contig;          // full-row kernel: contiguous row-group runs per block (A/B)
+};
 
 int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* out, int N, int C, int H,
                       int W, int OC, int KH, int KW, int stride, int pad, int dil, int ldw, int act,
-                      int nchw_out, int out_f32, const void* wfrag, hipStream_t stream) {
+                      int nchw_out, int out_f32, const void* wfrag, const ConvOpts* opts, hipStream_t stream) {
+  const ConvOpts o = opts ? *opts : ConvOpts{0, 0, 512, 5, 0};
   nsdb::ConvParams p;
   p.X = (const unsigned short*)X; p.Wt = (const unsigned short*)Wt; p.bias = bias; p.out = out;
   p.N = N; p.C = C; p.H = H; p.W = W; p.OC = OC; p.KH = KH; p.KW = KW;
@@ -1153,7 +1157,7 @@ int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* ou
   p.act = act; p.nchw_out = nchw_out; p.out_f32 = out_f32;
   // row-tiled LDS kernel for small-C, wide-row layers (see conv2d_rows_kernel)
   const int rin = nsdb::CVR_TR + KH - 1;
-  if (nsdb_conv2d_force_generic == 0 && stride == 1 && dil == 1 && pad == 0 && KW <= 8 && W % 8 == 0 &&
+  if (o.force_generic == 0 && stride == 1 && dil == 1 && pad == 0 && KW <= 8 && W % 8 == 0 &&
       C * KH <= 4 * nsdb::CVR_NKS && C * rin <= nsdb::CVR_ROWS && p.OW <= 16 * nsdb::CVR_MAXT) {
     nsdb::ConvRowParams q;
     q.X = p.X; q.Wt = p.Wt; q.bias = bias; q.out = out;
@@ -1163,8 +1167,8 @@ int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* ou
     q.chunks = std::min((16 * q.ntiles + 4 + 7) / 8, nsdb::CVR_CP / 16);
     q.groups_per_img = (p.OH + nsdb::CVR_TR - 1) / nsdb::CVR_TR;
     q.ngroups = N * q.groups_per_img;
-    q.act = act; q.nchw_out = nchw_out; q.out_f32 = out_f32; q.variant = nsdb_conv2d_variant;
-    q.contig = nsdb_conv2d_contig;
+    q.act = act; q.nchw_out = nchw_out; q.out_f32 = out_f32; q.variant = o.variant;
+    q.contig = o.contig;
     q.Wfrag = (const unsigned short*)wfrag;
     q.segs = (4 * p.OW + 3) & ~3;
     if ((q.segs / 2) % 4 == 0) q.segs += 4;
@@ -1173,30 +1177,30 @@ int nsdb_conv2d_igemm(const void* X, const void* Wt, const float* bias, void* ou
     if ((long long)N * OC * p.OH * p.OW * 2 >= 0x7ffffff0LL) goto generic;    // 31-bit buffer offsets
     if (C * rin * q.chunks > 512 || 64 * ldw / 8 > 6 * 256 || 64 * ldw * 2 > nsdb::CVR_BUF) goto generic;
     {
-      const int blocks = nsdb_conv2d_max_blocks > 0 ? std::min(q.ngroups, nsdb_conv2d_max_blocks) : q.ngroups;
+      const int blocks = o.max_blocks > 0 ? std::min(q.ngroups, o.max_blocks) : q.ngroups;
       const dim3 grid(blocks, (OC + 63) / 64);
       const bool staged = nchw_out && !out_f32 && (p.OW & 1) == 0 && q.vec8 && ((p.OH % 4) * p.OW) % 4 == 0;
-      if (staged && q.variant == 0 && nsdb_conv2d_rowfull && q.ntiles == nsdb::CVF_NT && 4 * p.OW <= nsdb::CVF_SEGS) {
+      if (staged && q.variant == 0 && o.kernel && q.ntiles == nsdb::CVF_NT && 4 * p.OW <= nsdb::CVF_SEGS) {
         // one block of 4 waves per CU (one wave per SIMD), persistent over the row groups
-        const dim3 gridf(std::min(q.ngroups, nsdb_conv2d_max_blocks > 0 ? std::min(nsdb_conv2d_max_blocks, 256) : q.ngroups),
+        const dim3 gridf(std::min(q.ngroups, o.max_blocks > 0 ? std::min(o.max_blocks, 256) : q.ngroups),
                          (OC + 63) / 64);
 #define NSDB_CVF_LAUNCH(A) hipLaunchKernelGGL((nsdb::conv2d_rowfull_kernel<A, false, true>), gridf, dim3(256), 0, stream, q)
-        if (nsdb_conv2d_rowfull == 2 || nsdb_conv2d_rowfull == 3) {   // phase-stamp timing builds (diagnostic)
-          if (nsdb_conv2d_rowfull == 2)
+        if (o.kernel == 2 || o.kernel == 3) {   // phase-stamp timing builds (diagnostic)
+          if (o.kernel == 2)
             hipLaunchKernelGGL((nsdb::conv2d_rowfull_kernel<nsdb::ACT_NONE, true, true>), gridf, dim3(256), 0, stream, q);
           else
             hipLaunchKernelGGL((nsdb::conv2d_rowfull_kernel<nsdb::ACT_NONE, true, false>), gridf, dim3(256), 0, stream, q);
           return (int)hipGetLastError();
         }
-        if (nsdb_conv2d_rowfull == 4) {   // unpipelined stores (A/B)
+        if (o.kernel == 4) {   // unpipelined stores (A/B)
           hipLaunchKernelGGL((nsdb::conv2d_rowfull_kernel<nsdb::ACT_NONE, false, false>), gridf, dim3(256), 0, stream, q);
           return (int)hipGetLastError();
         }
-        if (nsdb_conv2d_rowfull == 6 && wfrag != nullptr) {   // warp-specialised, phase-stamp timing build (diagnostic)
+        if (o.kernel == 6 && wfrag != nullptr) {   // warp-specialised, phase-stamp timing build (diagnostic)
           hipLaunchKernelGGL((nsdb::conv2d_ws_kernel<nsdb::ACT_NONE, true>), gridf, dim3(512), 0, stream, q);
           return (int)hipGetLastError();
         }
-        if (nsdb_conv2d_rowfull == 5 && wfrag != nullptr) {   // warp-specialised: 4 compute + 4 store waves per CU
+        if (o.kernel == 5 && wfrag != nullptr) {   // warp-specialised: 4 compute + 4 store waves per CU
 #define NSDB_CVW_LAUNCH(A) hipLaunchKernelGGL((nsdb::conv2d_ws_kernel<A, false>), gridf, dim3(512), 0, stream, q)
           switch (act) {
             case nsdb::ACT_RELU: NSDB_CVW_LAUNCH(nsdb::ACT_RELU); break;

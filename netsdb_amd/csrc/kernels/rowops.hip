@@ -76,7 +76,7 @@ template <typename TO, int NV>
 __global__ void __launch_bounds__(512) row_normalize_vec_kernel(const float* X, TO* Y, int R, int N, long long ldx,
                                                                 long long ldy, int plain_loads) {
   // plain_loads: cache-allocating instead of non-temporal row loads (the rows were usually just written by the
-  // producing GEMM and may still sit in the Infinity Cache; A/B knob nsdb_rownorm_plain_loads)
+  // producing GEMM and may still sit in the Infinity Cache; per-call option plain_loads)
   __shared__ float red[8];
   const int row = blockIdx.x;
   if (row >= R) return;
@@ -218,17 +218,16 @@ __global__ void __launch_bounds__(256) prefetch_kernel(const char* base, long lo
 
 extern "C" {
 
-int nsdb_rownorm_plain_loads = 0;   // A/B knob of row_normalize_vec_kernel's row load policy
-
+// plain_loads (per call): row_normalize_vec_kernel's row load policy (0 = non-temporal, the default; 1 = plain)
 int nsdb_softmax_rows(const void* X, int x_f32, const float* bias, void* Y, int y_f32, int R, int N,
-                      long long ldx, long long ldy, int log_out, hipStream_t st) {
+                      long long ldx, long long ldy, int log_out, int plain_loads, hipStream_t st) {
   if (R <= 0) return 0;
   if (log_out == 2) {   // row normalise
     const bool vec = x_f32 && (N % 4 == 0) && (ldx % 4 == 0) && (ldy % 4 == 0) &&
                      ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(Y)) & 15) == 0;
     if (vec && N <= 512 * 4 * 8) {
 #define NSDB_RNV(TO, NV) \
-  hipLaunchKernelGGL((nsdb::row_normalize_vec_kernel<TO, NV>), dim3(R), dim3(512), 0, st, (const float*)X, (TO*)Y, R, N, ldx, ldy, nsdb_rownorm_plain_loads)
+  hipLaunchKernelGGL((nsdb::row_normalize_vec_kernel<TO, NV>), dim3(R), dim3(512), 0, st, (const float*)X, (TO*)Y, R, N, ldx, ldy, plain_loads)
       const int nv = (N / 4 + 511) / 512;
       if (y_f32) { if (nv <= 2) NSDB_RNV(float, 2); else if (nv <= 4) NSDB_RNV(float, 4); else NSDB_RNV(float, 8); }
       else { if (nv <= 2) NSDB_RNV(unsigned short, 2); else if (nv <= 4) NSDB_RNV(unsigned short, 4); else NSDB_RNV(unsigned short, 8); }

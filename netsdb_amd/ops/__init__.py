@@ -7,6 +7,9 @@ CPU system) and the numerics oracle of the kernel tests.
 """
 from __future__ import annotations
 
+import contextlib
+import threading
+
 import numpy as np
 import torch
 
@@ -282,9 +285,58 @@ def conv_filter_fragments(Wflat, C, KH, KW):
     return torch.stack(out).contiguous()
 
 
+_KOPTS = threading.local()
+_KOPT_KEYS = {"conv_kernel", "conv_blocks", "conv_generic", "conv_variant", "conv_contig", "rownorm_plain_loads"}
+
+
+@contextlib.contextmanager
+def kernel_options(**kw):
+    """Kernel launch options for the HIP calls made by THIS thread inside the block (nested blocks override):
+    conv_kernel (conv2d row kernel: 5 warp-specialised = default, 1 full-row, 0 two-pass; 2/3/4/6 diagnostics),
+    conv_blocks (row-kernel grid cap, default 512; 0 = one block per row group), conv_generic (bool: the generic
+    gather kernel), conv_variant / conv_contig (row-kernel diagnostics), rownorm_plain_loads (bool: row normalise
+    with cache-allocating loads). Every option is passed per call to the kernel library, which keeps no
+    process-wide launch state: other threads (server requests, job lanes on their own threads) never see them."""
+    bad = set(kw) - _KOPT_KEYS
+    if bad:
+        raise ValueError(f"unknown kernel options {sorted(bad)}")
+    prev = getattr(_KOPTS, "d", {})
+    _KOPTS.d = {**prev, **{k: v for k, v in kw.items() if v is not None}}
+    try:
+        yield
+    finally:
+        _KOPTS.d = prev
+
+
+def set_kernel_options(**kw) -> dict:
+    """Set kernel launch options for the calling THREAD until changed (study scripts; ``kernel_options`` is the
+    scoped form). A value of None removes the option. Returns the previous options (restore_kernel_options)."""
+    bad = set(kw) - _KOPT_KEYS
+    if bad:
+        raise ValueError(f"unknown kernel options {sorted(bad)}")
+    prev = getattr(_KOPTS, "d", {})
+    d = dict(prev)
+    for k, v in kw.items():
+        if v is None:
+            d.pop(k, None)
+        else:
+            d[k] = v
+    _KOPTS.d = d
+    return prev
+
+
+def restore_kernel_options(prev: dict):
+    _KOPTS.d = dict(prev)
+
+
+def _kopt(name, default):
+    return getattr(_KOPTS, "d", {}).get(name, default)
+
+
 def conv2d(X, Wflat, bias=None, KH=1, KW=1, stride=1, pad=0, dil=1, act=ACT_NONE, nchw_out=False,
            out_dtype=torch.bfloat16):
-    """Fused implicit-GEMM conv. X [N,C,H,W]; Wflat [OC, >=C*KH*KW] in (c,kh,kw) im2col order."""
+    """Fused implicit-GEMM conv. X [N,C,H,W]; Wflat [OC, >=C*KH*KW] in (c,kh,kw) im2col order. Launch options
+    come from the calling thread's ``kernel_options`` scope."""
     act = act_code(act)
     if _use_hip(X, Wflat):
         if bias is not None and bias.dtype != torch.float32:
@@ -295,7 +347,9 @@ def conv2d(X, Wflat, bias=None, KH=1, KW=1, stride=1, pad=0, dil=1, act=ACT_NONE
             # small-C row-kernel shapes: the packed B fragments (cached per filter tensor and version)
             wfrag = derived(Wflat, f"conv_frag_{C}_{KH}_{KW}", lambda t: conv_filter_fragments(t, C, KH, KW))
         return _ext.hip().conv2d(X, Wflat, bias, KH, KW, stride, pad, dil, act, bool(nchw_out),
-                                 out_dtype == torch.float32, wfrag)
+                                 out_dtype == torch.float32, wfrag, int(_kopt("conv_kernel", -1)),
+                                 int(_kopt("conv_blocks", -1)), bool(_kopt("conv_generic", False)),
+                                 int(_kopt("conv_variant", 0)), int(_kopt("conv_contig", 0)))
     N, C = X.shape[0], X.shape[1]
     OC = Wflat.shape[0]
     w = Wflat[:, : C * KH * KW].float().reshape(OC, C, KH, KW)
@@ -345,7 +399,8 @@ def softmax_rows(X, bias=None, out_dtype=torch.float32, log=False):
 def row_normalize(X, out_dtype=torch.float32):
     """x / rowsum(x) (FFOutputLayer over exp'd scores)."""
     if _use_hip(X):
-        return _ext.hip().softmax_rows(X, None, out_dtype == torch.float32, 2)
+        return _ext.hip().softmax_rows(X, None, out_dtype == torch.float32, 2,
+                                       bool(_kopt("rownorm_plain_loads", False)))
     v = X.float()
     return (v / v.sum(-1, keepdim=True)).to(out_dtype)
 

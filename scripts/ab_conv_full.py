@@ -34,12 +34,12 @@ def main():
     variants = {"warpspec": 5, "rowfull": 1, "rows": 0}
     out = {}
     for name, v in variants.items():
-        h.conv2d_rowfull(v)
+        ops.set_kernel_options(conv_kernel=v)
         for act, fn in ((ops.ACT_NONE, lambda t: t), (ops.ACT_RELU, torch.relu)):
             y = ops.conv2d(X, Wf, bias, 7, 7, 1, 0, act=act, nchw_out=True).float()
             out[f"{name}_act{act}_rel_err"] = ((y - fn(ref)).abs().max() / ref.abs().max()).item()
-    h.conv2d_rowfull(5)
-    h.conv2d_contig(0)
+    ops.set_kernel_options(conv_kernel=5)
+    ops.set_kernel_options(conv_contig=0)
     print(json.dumps(out), flush=True)
     Xm, Wm = X.clone(), W.to(torch.bfloat16)
     ours = lambda: ops.conv2d(X, Wf, bias, 7, 7, 1, 0, nchw_out=True)  # noqa: E731
@@ -47,7 +47,7 @@ def main():
     ts = {k: [] for k in fns}
     for _ in range(a.rounds):
         for k, fn in fns.items():
-            h.conv2d_rowfull(variants.get(k, 5))
+            ops.set_kernel_options(conv_kernel=variants.get(k, 5))
             for _ in range(3):
                 fn()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -57,8 +57,8 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             ts[k].append(e0.elapsed_time(e1) / a.iters * 1000)
-    h.conv2d_rowfull(5)
-    h.conv2d_contig(0)
+    ops.set_kernel_options(conv_kernel=5)
+    ops.set_kernel_options(conv_contig=0)
     print(json.dumps({f"{k}_us_min": round(min(v), 1) for k, v in ts.items()} |
                      {f"{k}_us_med": round(sorted(v)[len(v) // 2], 1) for k, v in ts.items()}), flush=True)
 
@@ -66,37 +66,37 @@ def main():
 
 
 def stamps(mode=2):
-    """Phase stamps of the full-row kernel (conv2d_rowfull(2)): s_memtime cycles per wave."""
+    """Phase stamps of the full-row kernel (kernel option conv_kernel=2): s_memtime cycles per wave."""
     h = _ext.hip()
     dev = "cuda:0"
     X = torch.empty(100, 3, 112, 112, device=dev).uniform_(-1, 1).to(torch.bfloat16)
     Wf = ops.pad_k(torch.empty(64, 147, device=dev).uniform_(-0.1, 0.1)).to(torch.bfloat16).contiguous()
     bias = torch.randn(64, device=dev)
-    h.conv2d_rowfull(mode)
+    ops.set_kernel_options(conv_kernel=mode)
     for _ in range(3):
         y = ops.conv2d(X, Wf, bias, 7, 7, 1, 0, nchw_out=True)
     torch.cuda.synchronize()
     st = y.reshape(-1).view(torch.int64)[: 256 * 4 * 8].reshape(256 * 4, 8)[:, :6].double()
-    h.conv2d_rowfull(5)
+    ops.set_kernel_options(conv_kernel=5)
     names = ["total", "mfma", "epilogue", "mid_barrier", "stores", "rows+top_barrier"]
     print(json.dumps({"mode": mode, "stamps_mean": dict(zip(names, [round(float(v)) for v in st.mean(0)])),
                       "stamps_max": dict(zip(names, [round(float(v)) for v in st.max(0).values]))}), flush=True)
 
 
 def stamps_ws():
-    """Phase stamps of the warp-specialised kernel (conv2d_rowfull(6)): s_memtime cycles per wave, compute waves
+    """Phase stamps of the warp-specialised kernel (kernel option conv_kernel=6): s_memtime cycles per wave, compute waves
     (0-3) and store waves (4-7) separately."""
     h = _ext.hip()
     dev = "cuda:0"
     X = torch.empty(100, 3, 112, 112, device=dev).uniform_(-1, 1).to(torch.bfloat16)
     Wf = ops.pad_k(torch.empty(64, 147, device=dev).uniform_(-0.1, 0.1)).to(torch.bfloat16).contiguous()
     bias = torch.randn(64, device=dev)
-    h.conv2d_rowfull(6)
+    ops.set_kernel_options(conv_kernel=6)
     for _ in range(3):
         y = ops.conv2d(X, Wf, bias, 7, 7, 1, 0, nchw_out=True)
     torch.cuda.synchronize()
     st = y.reshape(-1).view(torch.int64)[: 256 * 8 * 8].reshape(256, 8, 8)[:, :, :6].double()
-    h.conv2d_rowfull(5)
+    ops.set_kernel_options(conv_kernel=5)
     names = {"compute": ["total", "tiles_0_1", "wait_S", "tiles_2_6_epilogues", "prologue", "wait_top"],
              "store": ["total", "stage_reads", "wait_S", "store_issue", "row_staging_and_prologue", "wait_top"]}
     out = {}

@@ -72,9 +72,9 @@ def main():
     t_ours = timeit(lambda: ops.conv2d(X, Wf, bias, 7, 7, 1, 0))
     from netsdb_amd import _ext as _e
 
-    _e.hip().conv2d_force_generic(1)
+    ops.set_kernel_options(conv_generic=bool(1))
     t_generic = timeit(lambda: ops.conv2d(X, Wf, bias, 7, 7, 1, 0))
-    _e.hip().conv2d_force_generic(0)
+    ops.set_kernel_options(conv_generic=bool(0))
     w4 = Wf[:, :147].reshape(64, 3, 7, 7).contiguous()
     t_lib = timeit(lambda: torch.nn.functional.conv2d(X, w4, bias.to(torch.bfloat16)))
     t_mat = timeit(lambda: study.gemm_nt(ops.im2col(X, 7, 7, 1, 0), Wf, bias, ops.BIAS_COL))

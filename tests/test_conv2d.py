@@ -59,3 +59,41 @@ def test_spatial_rewriting_plan(tmp_path, device):
     ref = torch.nn.functional.conv2d(x, w.cpu().to(torch.bfloat16).float(), b.cpu())
     ref = ref.permute(0, 2, 3, 1).reshape(-1, w.shape[0])
     torch.testing.assert_close(res, ref, atol=5e-2, rtol=5e-2)
+
+
+def test_kernel_options_are_per_thread_and_scoped():
+    """Kernel launch options (conv row kernel, grid cap, ...) live in the calling thread's scope and are passed per
+    call: another thread (a server request, a job lane on its own thread) never sees them, and they end with the
+    block. Unknown options are rejected."""
+    import threading
+
+    from netsdb_amd import ops
+
+    seen = {}
+    go, done = threading.Event(), threading.Event()
+
+    def other():
+        go.wait(10)
+        seen["other"] = ops._kopt("conv_kernel", -1)
+        done.set()
+
+    t = threading.Thread(target=other)
+    t.start()
+    with ops.kernel_options(conv_kernel=1, conv_blocks=0):
+        with ops.kernel_options(conv_kernel=0):
+            seen["nested"] = (ops._kopt("conv_kernel", -1), ops._kopt("conv_blocks", -1))
+        seen["outer"] = ops._kopt("conv_kernel", -1)
+        go.set()
+        done.wait(10)
+    t.join(10)
+    seen["after"] = ops._kopt("conv_kernel", -1)
+    assert seen == {"nested": (0, 0), "outer": 1, "other": -1, "after": -1}
+    prev = ops.set_kernel_options(conv_generic=True)
+    assert ops._kopt("conv_generic", False) is True
+    ops.restore_kernel_options(prev)
+    assert ops._kopt("conv_generic", False) is False
+    import pytest
+
+    with pytest.raises(ValueError):
+        with ops.kernel_options(conv_kernal=5):
+            pass

@@ -117,11 +117,8 @@ def test_gemm_dropout_matches_host_rng():
 
 @pytest.fixture(params=[0, 1], ids=["auto", "generic"])
 def conv_generic(request):
-    from netsdb_amd import _ext
-
-    _ext.hip().conv2d_force_generic(request.param)
-    yield request.param
-    _ext.hip().conv2d_force_generic(0)
+    with ops.kernel_options(conv_generic=bool(request.param)):
+        yield request.param
 
 
 @pytest.mark.parametrize("cfg", [
@@ -272,21 +269,14 @@ def test_conv2d_rows_bf16_nchw(cfg, rowfull, blocks):
     """The LDS-staged bf16 NCHW output path (what the conv2d job runs): the two-pass row kernel, the full-row
     kernel (1 wave/SIMD, stores pipelined under the MFMAs) and the warp-specialised kernel (compute + store waves;
     with 3 persistent blocks every block walks several row groups) vs the fp32 reference, with a relu epilogue."""
-    from netsdb_amd import _ext
-
     torch.manual_seed(5)
     X = torch.randn(cfg["N"], cfg["C"], cfg["H"], cfg["W"], device=DEV).to(torch.bfloat16)
     K = cfg["C"] * cfg["KH"] * cfg["KW"]
     Wt = ops.pad_k(torch.randn(cfg["OC"], K, device=DEV) * 0.1).to(torch.bfloat16).contiguous()
     bias = torch.randn(cfg["OC"], device=DEV)
-    old = _ext.hip().conv2d_rowfull(rowfull)
-    old_b = _ext.hip().conv2d_max_blocks(blocks)
-    try:
+    with ops.kernel_options(conv_kernel=rowfull, conv_blocks=blocks):
         y = ops.conv2d(X, Wt, bias, cfg["KH"], cfg["KW"], 1, 0, act=ops.ACT_RELU, nchw_out=True)
         torch.cuda.synchronize()
-    finally:
-        _ext.hip().conv2d_rowfull(old)
-        _ext.hip().conv2d_max_blocks(old_b)
     assert y.dtype == torch.bfloat16
     ref = ops.conv2d(X.cpu(), Wt.cpu(), bias.cpu(), cfg["KH"], cfg["KW"], 1, 0, act=ops.ACT_RELU, nchw_out=True,
                      out_dtype=torch.float32)
