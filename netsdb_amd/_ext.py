@@ -7,7 +7,6 @@
 from __future__ import annotations
 
 import importlib
-import os
 
 _hip_mod = None
 _hip_err: Exception | None = None
@@ -74,7 +73,3 @@ def native_available() -> bool:
     except RuntimeError:
         return False
 
-
-def strict_gpu() -> bool:
-    """On a GPU box ops must run on the HIP path (NSDB_ALLOW_EAGER=1 relaxes this for debugging)."""
-    return os.environ.get("NSDB_ALLOW_EAGER", "0") != "1"
