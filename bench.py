@@ -76,10 +76,13 @@ def main():
                          "the chip's clock dips for ~10-20 ms after the GEMMs start and then settles "
                          "(profiles/r2_clock_settle); the timed window should see the settled clock")
     ap.add_argument("--profile-json", default=None)
-    ap.add_argument("--overlap", choices=["none", "after", "before", "tail"], default="none",
+    ap.add_argument("--overlap", choices=["none", "after", "before", "tail", "beside"], default="none",
                     help="conv2d job on its own HIP stream, submitted after/before the FF jobs (independent inputs); "
                          "tail: gated on the GPU to start when the first workgroup of the FF layer-1 GEMM finishes "
-                         "(fills the CUs that GEMM's tail leaves idle)")
+                         "(fills the CUs that GEMM's tail leaves idle); beside: the layer-1 GEMM leaves "
+                         "--reserve-cus CUs free and the conv2d job runs on them next to it (start gate)")
+    ap.add_argument("--reserve-cus", type=int, default=16,
+                    help="--overlap beside: CUs the layer-1 GEMM leaves to the conv2d job (its grid)")
     ap.add_argument("--job-priority", type=int, default=None,
                     help="HIP stream priority of the conv2d job stream (default -1 = high; 0 in tail mode, where the "
                          "FF jobs run on a high-priority stream instead)")
@@ -160,15 +163,23 @@ def main():
         main_stream.wait_stream(torch.cuda.current_stream(dev))
         torch.cuda.set_stream(main_stream)
 
+    beside = args.overlap == "beside"
+
     def conv():
-        cv.conv2d_memfuse_inference(client, "conv2d", "img", "conv_out", w, b)
+        if beside:
+            # persistent conv blocks sized to the CUs the layer-1 GEMM leaves free
+            with ops.kernel_options(conv_blocks=args.reserve_cus):
+                cv.conv2d_memfuse_inference(client, "conv2d", "img", "conv_out", w, b)
+        else:
+            cv.conv2d_memfuse_inference(client, "conv2d", "img", "conv_out", w, b)
 
     def ffjobs(i):
         ff.inference_unit(client, "ff", "w1", "wo", "inputs", "b1", "bo", "output", dropout_rate=args.dropout,
                           seed=i, single_job=args.single_job)
 
     def step(i):
-        trig = client.arm_tail_trigger() if args.overlap == "tail" else None
+        trig = client.arm_tail_trigger() if args.overlap == "tail" else \
+            client.arm_start_gate(args.reserve_cus) if beside else None
         if args.overlap == "before":
             client.submit_job(conv, lane=conv_lane, independent=True)
         if inflight > 1:
@@ -180,7 +191,7 @@ def main():
             conv()
         elif args.overlap == "after":
             client.submit_job(conv, lane=conv_lane, independent=True)
-        elif args.overlap == "tail":
+        elif args.overlap in ("tail", "beside"):
             client.submit_job(conv, lane=conv_lane, independent=True, start_on=trig)
         if args.overlap != "none" and inflight == 1:
             client.wait_jobs()   # the step ends when both jobs have (stream-ordered join)

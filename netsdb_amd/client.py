@@ -64,6 +64,7 @@ class PDBClient:
         self.job_lanes = 2               # job streams (in-order job queues) created on first submit_job
         self.job_lane_priority = {}      # lane -> HIP stream priority (default job_stream_priority)
         self.tail_trigger = None         # TailTrigger (arm_tail_trigger)
+        self.start_gate = None           # TailTrigger in start mode (arm_start_gate)
         if resume:
             self._resume()
 
@@ -502,6 +503,18 @@ class PDBClient:
 
             self.tail_trigger = TailTrigger(self.device)
         return self.tail_trigger.arm()
+
+    def arm_start_gate(self, reserve_cus: int = 16):
+        """Arm a START gate on the next long GEMM this client enqueues: that GEMM leaves ``reserve_cus`` CUs free,
+        and a job submitted with ``submit_job(..., start_on=gate)`` starts once the GEMM holds all of its CUs, so
+        it runs beside the GEMM on the reserved CUs (see :class:`~netsdb_amd.execution.streams.TailTrigger`).
+        Size the gated job's grid to the reserved CUs (e.g. ``ops.kernel_options(conv_blocks=reserve_cus)``)."""
+        g = self.start_gate
+        if g is None or g.reserve_cus != int(reserve_cus):
+            from .execution.streams import TailTrigger
+
+            g = self.start_gate = TailTrigger(self.device, mode="start", reserve_cus=reserve_cus)
+        return g.arm()
 
     def submit_job(self, fn, *args, lane: int = 0, independent: bool = False, start_on=None, **kwargs):
         """Run ``fn(*args, **kwargs)`` (any job-issuing callable, e.g. a model's inference entry point)

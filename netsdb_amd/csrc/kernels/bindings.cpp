@@ -13,6 +13,7 @@
 extern "C" {
 int nsdb_gemm_splits(int M, int N, int K, int batch, int cfg);
 int nsdb_gemm_tail_eligible(int M, int N, int K, int batch, int splits, int cfg);
+int nsdb_gemm_launch_wgs(int M, int N, int K, int batch, int splits, int cfg);
 int nsdb_stream_wait_value(hipStream_t stream, void* flag, unsigned value);
 int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const float* bias, int M, int N, int K,
                       long long lda, long long ldb, long long ldc, long long sA, long long sB, long long sC,
@@ -74,6 +75,7 @@ struct GemmOpts {
   int epi;
   const void* pf_ptr;
   long long pf_bytes;
+  unsigned* start_signal;
 };
 
 void check_rc(int rc, const char* what) {
@@ -97,7 +99,7 @@ torch::Tensor gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Ten
                       int64_t act, bool out_f32, double alpha, double dropout, int64_t seed, int64_t splits,
                       c10::optional<torch::Tensor> out, bool accumulate, int64_t cfg,
                       c10::optional<torch::Tensor> signal, int64_t signal_value, int64_t epi,
-                      c10::optional<torch::Tensor> prefetch) {
+                      c10::optional<torch::Tensor> prefetch, c10::optional<torch::Tensor> start_signal) {
   check_cuda(A, "A");
   check_cuda(B, "B");
   TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && B.scalar_type() == torch::kBFloat16, "A,B must be bf16");
@@ -149,7 +151,13 @@ torch::Tensor gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Ten
     wsp = ws.data_ptr<float>();
   }
   TORCH_CHECK(epi >= -1 && epi <= 1, "gemm_nt: epi must be -1 (auto), 0 (LDS-staged) or 1 (direct)");
-  GemmOpts o{(int)cfg, nullptr, 0u, (int)epi, nullptr, 0};
+  GemmOpts o{(int)cfg, nullptr, 0u, (int)epi, nullptr, 0, nullptr};
+  if (start_signal.has_value() && start_signal->defined()) {
+    check_cuda(*start_signal, "start_signal");
+    TORCH_CHECK(start_signal->scalar_type() == torch::kInt32 && start_signal->numel() >= 1,
+                "start_signal must be an int32 flag");
+    o.start_signal = reinterpret_cast<unsigned*>(start_signal->data_ptr());
+  }
   if (signal.has_value() && signal->defined()) {
     check_cuda(*signal, "signal");
     TORCH_CHECK(signal->scalar_type() == torch::kInt32 && signal->numel() >= 1, "signal must be an int32 flag");
@@ -639,7 +647,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bias_mode") = 0, py::arg("act") = 0, py::arg("out_f32") = false, py::arg("alpha") = 1.0,
         py::arg("dropout") = 0.0, py::arg("seed") = 0, py::arg("splits") = 0, py::arg("out") = py::none(),
         py::arg("accumulate") = false, py::arg("cfg") = -1, py::arg("signal") = py::none(),
-        py::arg("signal_value") = 0, py::arg("epi") = -1, py::arg("prefetch") = py::none());
+        py::arg("signal_value") = 0, py::arg("epi") = -1, py::arg("prefetch") = py::none(),
+        py::arg("start_signal") = py::none());
+  m.def("gemm_launch_wgs", [](int64_t M, int64_t N, int64_t K, int64_t batch, int64_t splits, int64_t cfg) {
+          return (int64_t)nsdb_gemm_launch_wgs((int)M, (int)N, (int)K, (int)batch, (int)splits, (int)cfg);
+        }, "workgroups of the GEMM launch for this shape (splits <= 0: the launcher's choice)",
+        py::arg("M"), py::arg("N"), py::arg("K"), py::arg("batch") = 1, py::arg("splits") = 0, py::arg("cfg") = -1);
   m.def("prefetch", &prefetch, "warm the caches with a read of each tensor", py::arg("tensors"), py::arg("sink"),
         py::arg("blocks") = 64);
   m.def("gemm_nt_f32", &gemm_nt_f32, "alpha * A.B^T (+C) on the exact-f32 MFMA (16x16x4)", py::arg("A"),

@@ -732,6 +732,12 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   stage(1, 2, 1); stage(1, 0, 1); stage(1, 3, 1);
   asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   if constexpr (EPI != 0) reinterpret_cast<float*>(smem + SM_BIAS)[tid] = bias_v;   // [256 col | 256 row]
+  // start gate (per launch): a job gated on flag >= base + workgroups (hipStreamWaitValue32) is dispatched only
+  // once every workgroup of this launch holds its CU, so it can only take the CUs this launch leaves free. Issued
+  // after the prologue's wait: the in-order vmcnt retires it at the first k-tile's counted wait, not before the
+  // prologue's DMAs.
+  if (p.start_signal != nullptr && tid == 0)
+    __hip_atomic_fetch_add(p.start_signal, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   NSDB_BARRIER();
   if (wr == 1) NSDB_BARRIER();            // stagger the two wave groups by one barrier
   for (int it = 0; it < niter; ++it) {
@@ -891,6 +897,7 @@ struct GemmOpts {
   int epi;                  // 8-phase unsplit epilogue: -1 auto (direct), 0 LDS-staged, 1 direct register stores
   const void* pf_ptr;       // operand prefetch of this launch (8-phase only): pf_bytes at pf_ptr, or nullptr
   long long pf_bytes;
+  unsigned* start_signal;   // start gate of this launch (8-phase only): +1 per workgroup at its start, or nullptr
 };
 
 extern "C" {
@@ -935,6 +942,18 @@ int nsdb_gemm_splits(int M, int N, int K, int batch, int cfg) {
     splits = (ksteps + kchunk_steps - 1) / kchunk_steps;
   }
   return splits;
+}
+
+// Workgroups of the launch nsdb_gemm_nt_bf16 makes for this shape (splits <= 0: the launcher's own choice).
+int nsdb_gemm_launch_wgs(int M, int N, int K, int batch, int splits, int cfg) {
+  cfg = resolve_cfg(cfg, M, N, K, batch);
+  const int tbm = cfg ? 256 : nsdb::BM, tbn = cfg ? 256 : nsdb::BN;
+  const int ksteps = (K + nsdb::BK - 1) / nsdb::BK;
+  if (splits <= 0) splits = nsdb_gemm_splits(M, N, K, batch, cfg);
+  splits = std::max(1, splits);
+  const int kchunk_steps = std::max(1, (ksteps + splits - 1) / splits);
+  const int s = std::max(1, (ksteps + kchunk_steps - 1) / kchunk_steps);
+  return ((M + tbm - 1) / tbm) * ((N + tbn - 1) / tbn) * s * batch;
 }
 
 // Would a launch of this shape take a tail trigger (an 8-phase launch of >= 128 workgroups with >= 64 k-tiles
@@ -1034,6 +1053,7 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
       p.signal = opts->signal;
       p.signal_value = opts->signal_value;
     }
+    if (opts && opts->start_signal) p.start_signal = opts->start_signal;   // this launch's start gate
     if (opts && opts->pf_ptr && opts->pf_bytes > 0) {   // this launch's operand prefetch
       p.pf_ptr = (const char*)opts->pf_ptr;
       p.pf_bytes = opts->pf_bytes;

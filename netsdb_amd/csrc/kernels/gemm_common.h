@@ -42,6 +42,7 @@ struct GemmParams {
   int* sm_cnt;
   int* sm_flag;
   int* sm_dep = nullptr;     // fused softmax: departures (low 16 bits) + timed-out tiles (high 16) per group
+  unsigned* start_signal = nullptr;   // start gate (8-phase): every workgroup adds 1 when it starts (system scope)
   const char* pf_ptr = nullptr;   // operand prefetch for the NEXT kernel (8-phase, EPI 0): bytes read into the
   long long pf_bytes = 0;         // Infinity Cache by the workgroups after their main loops
   unsigned long long* stamps;   // diagnostic variant 12: per-workgroup real-time stamps every 32 k-tiles

@@ -108,13 +108,24 @@ class TailTrigger:
     """Device flag raised by the workgroups of the next long 8-phase GEMM launch enqueued on the stream that
     armed it (see module doc).
 
+    ``mode="start"`` (a START gate, :meth:`PDBClient.arm_start_gate`): the launch that takes it leaves
+    ``reserve_cus`` CUs free (fewer split-K slices: the layer-1 GEMM is power-limited, so 240 instead of 256
+    workgroups cost it ~2 %), every workgroup adds 1 to the flag when it starts, and the gated job waits for
+    flag >= base + workgroups — it is dispatched only once the whole GEMM holds its CUs, so it runs on exactly
+    the reserved ones, beside the GEMM, instead of in its tail.
+
     ``arm()`` (on the stream that will run the GEMM) before enqueuing the job whose GEMM tail should be filled;
     ``JobStreams.submit(..., start_on=trigger)`` then gates the submitted job on it. The gate is only installed
     when a launch actually took the armed trigger (every workgroup of that launch writes the flag, so the wait
     always ends); otherwise the job starts ungated. Arming is per stream: a GEMM enqueued on another stream
     (another job lane, another thread's stream) never takes it."""
 
-    def __init__(self, device):
+    def __init__(self, device, mode: str = "tail", reserve_cus: int = 0):
+        if mode not in ("tail", "start"):
+            raise ValueError(f"trigger mode {mode!r}: 'tail' or 'start'")
+        self.mode = mode
+        self.reserve_cus = int(reserve_cus)
+        self.count = 0       # start mode: workgroups counted into the flag so far (the gate's wait value)
         self.device = torch.device(device)
         self.flag = torch.zeros(1, dtype=torch.int32, device=self.device) if self.device.type == "cuda" else None
         if self.flag is not None:
@@ -133,9 +144,11 @@ class TailTrigger:
         from .. import _ext
 
         self.epoch = self.epoch % 0x7FFFFFFF + 1     # flag values only grow (atomic max), never wrap to 0
-        if self.epoch == 1 and self.gated:           # wrapped: restart from a zero flag
+        if (self.epoch == 1 and self.gated) or self.count > 0x7FFF0000:   # wrapped: restart from a zero flag
+            torch.cuda.synchronize(self.device)
             self.flag.zero_()
             torch.cuda.synchronize(self.device)
+            self.count = 0
         _ext.hip()                                   # the GEMM that takes it runs on the HIP kernels
         self.disarm()
         self._key = _stream_key(self.device)
@@ -145,10 +158,14 @@ class TailTrigger:
         self.consumed = False
         return self
 
-    def take(self) -> Tuple[torch.Tensor, int]:
-        """Called by the GEMM launch that takes the trigger: (flag, value) for that launch only."""
+    def take(self, workgroups: int = 0) -> Tuple[torch.Tensor, int]:
+        """Called by the GEMM launch that takes the trigger: (flag, value) for that launch only (start mode: the
+        launch's ``workgroups`` each add 1; the value is the flag once all have started)."""
         self.consumed = True
         self.disarm()
+        if self.mode == "start":
+            self.count += int(workgroups)
+            return self.flag, self.count
         return self.flag, self.epoch
 
     def disarm(self):
@@ -170,7 +187,7 @@ class TailTrigger:
             return False
         self.consumed = False
         with torch.cuda.stream(stream):
-            h.stream_wait_value(self.flag, self.epoch)
+            h.stream_wait_value(self.flag, self.count if self.mode == "start" else self.epoch)
         self.gated += 1
         return True
 

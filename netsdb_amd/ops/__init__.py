@@ -105,17 +105,22 @@ def gemm_nt(A, B, bias=None, bias_mode=BIAS_NONE, act=ACT_NONE, out_dtype=torch.
 
         trig = streams.armed_trigger(A.device)
         pf_armed = bool(streams._armed_pf)
+        start_sig = None
         if trig is not None or pf_armed:
             M, N, K = A.shape[-2], B.shape[-2], A.shape[-1]
             batch = A.shape[0] if A.dim() == 3 else 1
             if h.gemm_tail_eligible(M, N, K, batch, int(splits), c):
-                if trig is not None:
+                if trig is not None and trig.mode == "start":
+                    splits = _reserve_cus_splits(h, A.device, M, N, K, batch, int(splits), c, trig.reserve_cus)
+                    start_sig, _ = trig.take(h.gemm_launch_wgs(M, N, K, batch, int(splits), c))
+                elif trig is not None:
                     sig, sval = trig.take()
                 if pf_armed:
                     pf = streams.take_operand_prefetch(A.device)
         return h.gemm_nt(A, B, bias, int(bias_mode if bias is not None else 0), act,
                          out_dtype == torch.float32, float(alpha), float(dropout), int(seed),
-                         int(splits), out, bool(accumulate), c, sig, int(sval), -1 if epi is None else int(epi), pf)
+                         int(splits), out, bool(accumulate), c, sig, int(sval), -1 if epi is None else int(epi), pf,
+                         start_sig)
     v = torch.matmul(A.float(), B.float().transpose(-1, -2)) * alpha
     if bias is not None:
         b = bias.float()
@@ -130,6 +135,16 @@ def gemm_nt(A, B, bias=None, bias_mode=BIAS_NONE, act=ACT_NONE, out_dtype=torch.
         out.copy_(v)
         return out
     return v
+
+
+def _reserve_cus_splits(h, device, M, N, K, batch, splits, cfg, reserve):
+    """Split-K slices for a one-wave launch that leaves ``reserve`` of the device's CUs free (start gates)."""
+    cus = torch.cuda.get_device_properties(device).multi_processor_count
+    cap = max(1, cus - int(reserve))
+    s = splits if splits > 0 else h.gemm_splits(M, N, K, batch, cfg)
+    while s > 1 and h.gemm_launch_wgs(M, N, K, batch, s, cfg) > cap:
+        s -= 1
+    return s
 
 
 def gemm_nt_f32(A, B, alpha=1.0, out=None, accumulate=False):

@@ -19,7 +19,8 @@ def _last_json(out: str) -> dict:
 
 
 @pytest.mark.parametrize("extra", [[], ["--overlap", "before"], ["--overlap", "after", "--inflight", "2"],
-                                   ["--overlap", "tail"], ["--graph"], ["--two-job"], ["--single-job"]])
+                                   ["--overlap", "tail"], ["--overlap", "beside"], ["--graph"], ["--two-job"],
+                                   ["--single-job"]])
 def test_bench_single_process(extra):
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
     r = subprocess.run([sys.executable, "bench.py", "--small", "--steps", "2", "--warmup", "2"] + extra, cwd=ROOT,

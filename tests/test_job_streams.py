@@ -154,3 +154,41 @@ def test_tail_trigger_is_per_stream_gpu():
     assert trig.consumed and int(trig.flag.item()) == trig.epoch
     assert torch.equal(C_armed, ref)
     assert (C_forced.synchronize() - ref).abs().max().item() <= 1e-3 * ref.abs().max().item()
+
+
+@pytest.mark.gpu
+def test_start_gate_reserves_cus_and_gates_job_gpu():
+    """A START gate: the long split-K GEMM that takes it leaves reserve_cus CUs free (fewer split-K slices, exact
+    result vs an ungated launch with the same splits), every workgroup adds 1 to the flag when it starts, and the
+    gated job (sized to the reserved CUs) runs once all have started; over repeated launches the flag carries the
+    running workgroup count. Conv2d with a 16-block grid (what bench.py --overlap beside runs) stays exact."""
+    from netsdb_amd import _ext, ops
+    from netsdb_amd.execution.streams import TailTrigger
+
+    dev = "cuda:0"
+    A, B = _long_splitk_operands(dev)
+    h = _ext.hip()
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    s_res = ops._reserve_cus_splits(h, dev, 1024, 1024, 65536, 1, 0, -1, 16)
+    wgs = h.gemm_launch_wgs(1024, 1024, 65536, 1, s_res, -1)
+    assert wgs <= cus - 16 and s_res < ops.gemm_splits(1024, 1024, 65536)
+    ref = ops.gemm_nt(A, B, out_dtype=torch.float32, splits=s_res)
+    X = torch.empty(6, 3, 112, 112, device=dev).uniform_(-1, 1).to(torch.bfloat16)
+    Wf = ops.pad_k(torch.empty(64, 147, device=dev).uniform_(-0.1, 0.1)).to(torch.bfloat16).contiguous()
+    bias = torch.randn(64, device=dev)
+    yref = ops.conv2d(X, Wf, bias, 7, 7, 1, 0, nchw_out=True)
+    js = JobStreams(dev, lanes=1)
+    gate = TailTrigger(dev, mode="start", reserve_cus=16)
+
+    def conv_job():
+        with ops.kernel_options(conv_blocks=16):
+            return ops.conv2d(X, Wf, bias, 7, 7, 1, 0, nchw_out=True)
+
+    for it in range(3):
+        gate.arm()
+        C = ops.gemm_nt(A, B, out_dtype=torch.float32)
+        y = js.submit(conv_job, independent=True, start_on=gate).wait()
+        torch.cuda.synchronize()
+        assert torch.equal(C, ref)
+        assert torch.equal(y, yref)
+        assert gate.gated == it + 1 and int(gate.flag.item()) == gate.count == wgs * (it + 1)
