@@ -192,3 +192,26 @@ def test_start_gate_reserves_cus_and_gates_job_gpu():
         assert torch.equal(C, ref)
         assert torch.equal(y, yref)
         assert gate.gated == it + 1 and int(gate.flag.item()) == gate.count == wgs * (it + 1)
+
+
+@pytest.mark.gpu
+def test_operand_prefetch_is_taken_once_and_exact_gpu():
+    """An operand prefetch armed on the stream is taken by the next long 8-phase GEMM only (results bitwise equal
+    to an unarmed launch), not by a short GEMM before it, and never by a GEMM on another lane."""
+    from netsdb_amd import ops
+    from netsdb_amd.execution import streams
+
+    dev = "cuda:0"
+    A, B = _long_splitk_operands(dev)
+    W2 = torch.randn(14588, 1000, device=dev).to(torch.bfloat16)
+    ref = ops.gemm_nt(A, B, out_dtype=torch.float32)
+    js = JobStreams(dev, lanes=1)
+    assert streams.arm_operand_prefetch(W2)
+    a = torch.randn(256, 256, device=dev).to(torch.bfloat16)
+    ops.gemm_nt(a, a)                                     # short: does not take it
+    other = js.submit(lambda: ops.gemm_nt(A, B, out_dtype=torch.float32), independent=True).synchronize()
+    assert streams._armed_pf, "a GEMM on another stream took the prefetch"
+    C = ops.gemm_nt(A, B, out_dtype=torch.float32)        # long split-K: takes it
+    torch.cuda.synchronize()
+    assert not streams._armed_pf
+    assert torch.equal(C, ref) and torch.equal(other, ref)
