@@ -168,6 +168,13 @@ class TailTrigger:
             return self.flag, self.count
         return self.flag, self.epoch
 
+    def untake(self, workgroups: int = 0):
+        """The launch that took the trigger failed to enqueue: nothing will raise the flag, so no job may be gated
+        on it (a gate on a value that never comes would stall its stream forever)."""
+        self.consumed = False
+        if self.mode == "start":
+            self.count -= int(workgroups)
+
     def disarm(self):
         with _armed_lock:
             if self._key is not None and _armed.get(self._key) is self:

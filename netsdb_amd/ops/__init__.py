@@ -105,22 +105,30 @@ def gemm_nt(A, B, bias=None, bias_mode=BIAS_NONE, act=ACT_NONE, out_dtype=torch.
 
         trig = streams.armed_trigger(A.device)
         pf_armed = bool(streams._armed_pf)
-        start_sig = None
+        start_sig, taken, nwg = None, None, 0
         if trig is not None or pf_armed:
             M, N, K = A.shape[-2], B.shape[-2], A.shape[-1]
             batch = A.shape[0] if A.dim() == 3 else 1
             if h.gemm_tail_eligible(M, N, K, batch, int(splits), c):
                 if trig is not None and trig.mode == "start":
                     splits = _reserve_cus_splits(h, A.device, M, N, K, batch, int(splits), c, trig.reserve_cus)
-                    start_sig, _ = trig.take(h.gemm_launch_wgs(M, N, K, batch, int(splits), c))
+                    nwg = h.gemm_launch_wgs(M, N, K, batch, int(splits), c)
+                    start_sig, _ = trig.take(nwg)
+                    taken = trig
                 elif trig is not None:
                     sig, sval = trig.take()
+                    taken = trig
                 if pf_armed:
                     pf = streams.take_operand_prefetch(A.device)
-        return h.gemm_nt(A, B, bias, int(bias_mode if bias is not None else 0), act,
-                         out_dtype == torch.float32, float(alpha), float(dropout), int(seed),
-                         int(splits), out, bool(accumulate), c, sig, int(sval), -1 if epi is None else int(epi), pf,
-                         start_sig)
+        try:
+            return h.gemm_nt(A, B, bias, int(bias_mode if bias is not None else 0), act,
+                             out_dtype == torch.float32, float(alpha), float(dropout), int(seed),
+                             int(splits), out, bool(accumulate), c, sig, int(sval), -1 if epi is None else int(epi),
+                             pf, start_sig)
+        except Exception:
+            if taken is not None:
+                taken.untake(nwg)
+            raise
     v = torch.matmul(A.float(), B.float().transpose(-1, -2)) * alpha
     if bias is not None:
         b = bias.float()

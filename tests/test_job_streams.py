@@ -215,3 +215,22 @@ def test_operand_prefetch_is_taken_once_and_exact_gpu():
     torch.cuda.synchronize()
     assert not streams._armed_pf
     assert torch.equal(C, ref) and torch.equal(other, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["tail", "start"])
+def test_trigger_taken_by_failed_launch_does_not_gate_gpu(mode):
+    """A long GEMM takes the armed trigger but its launch is rejected (bad output tensor): the trigger is handed
+    back, so the job submitted on it runs ungated instead of waiting on the GPU for a flag no kernel raises."""
+    from netsdb_amd import ops
+    from netsdb_amd.execution.streams import TailTrigger
+
+    dev = "cuda:0"
+    A, B = _long_splitk_operands(dev)
+    trig = TailTrigger(dev, mode=mode, reserve_cus=16).arm()
+    bad = torch.empty(3, 3, device=dev, dtype=torch.float16)
+    with pytest.raises(RuntimeError):
+        ops.gemm_nt(A, B, out_dtype=torch.float32, out=bad)
+    js = JobStreams(dev, lanes=1)
+    y = js.submit(lambda: A[:4, :4].float().sum(), independent=True, start_on=trig).synchronize()
+    assert trig.gated == 0 and torch.isfinite(y) and trig.count == 0
