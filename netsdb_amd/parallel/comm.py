@@ -60,10 +60,14 @@ class ClusterContext:
 
     @staticmethod
     def from_env(device: Optional[str] = None, backend: Optional[str] = None) -> "ClusterContext":
-        """torchrun-style init (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_ADDR/MASTER_PORT)."""
+        """torchrun-style init (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_ADDR/MASTER_PORT). Rehearsal overrides:
+        NSDB_DEVICE (e.g. every rank on cuda:0 of a one-GPU box) and NSDB_DIST_BACKEND (gloo: RCCL refuses two
+        ranks on one GPU)."""
         ws = int(os.environ.get("WORLD_SIZE", "1"))
         rank = int(os.environ.get("RANK", "0"))
         local = int(os.environ.get("LOCAL_RANK", "0"))
+        device = device or os.environ.get("NSDB_DEVICE") or None
+        backend = backend or os.environ.get("NSDB_DIST_BACKEND") or None
         if device is None:
             device = f"cuda:{local}" if torch.cuda.device_count() > 0 else "cpu"
         dev = torch.device(device)
@@ -72,7 +76,7 @@ class ClusterContext:
         if ws > 1 and not dist.is_initialized():
             be = backend or ("nccl" if dev.type == "cuda" else "gloo")
             kw = {}
-            if dev.type == "cuda":
+            if dev.type == "cuda" and be == "nccl":
                 kw["device_id"] = dev
             dist.init_process_group(be, rank=rank, world_size=ws, **kw)
         be = dist.get_backend() if dist.is_initialized() else None
