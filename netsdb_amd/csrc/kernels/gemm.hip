@@ -45,6 +45,29 @@ __device__ __forceinline__ void sm_combine(float& m, float& s, float m2, float s
   m = mn;
 }
 
+// Cross-half wave reductions on the gfx950 lane-swap VALU ops (v_permlane32_swap / v_permlane16_swap: lanes l and
+// l ^ 32 / l ^ 16 exchange in one instruction, no LDS round trip like ds_bpermute)
+__device__ __forceinline__ float2 swap_pair32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return make_float2(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float2 swap_pair16(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return make_float2(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float max_xor16_32(float x) {          // max over lanes {l, l^16, l^32, l^48}
+  float2 a = swap_pair16(x);
+  x = fmaxf(a.x, a.y);
+  a = swap_pair32(x);
+  return fmaxf(a.x, a.y);
+}
+__device__ __forceinline__ float sum_xor16_32(float x) {
+  float2 a = swap_pair16(x);
+  x = a.x + a.y;
+  a = swap_pair32(x);
+  return a.x + a.y;
+}
+
 // Partials of one softmax group (row-block for AXIS 1, column-block for AXIS 2): float2 (max, sum exp)
 // [group][256 lines][need_pad] with need_pad = need rounded up to even, so the partials of one line are
 // contiguous and 16-B aligned: the combine reads a line's partials with 16-B loads, all in flight at once.
@@ -154,8 +177,7 @@ __device__ __forceinline__ bool softmax_epilogue_8ph(f32x4 (&acc)[8][4], char* s
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) m = fmaxf(m, acc[i][j][r]);
-      m = fmaxf(m, __shfl_xor(m, 16, 64));
-      m = fmaxf(m, __shfl_xor(m, 32, 64));
+      m = max_xor16_32(m);
       float sum = 0.f;
       const float ms = m == -INFINITY ? 0.f : m;        // an all-invalid line: exp(-inf) = 0 everywhere
 #pragma unroll
@@ -166,8 +188,7 @@ __device__ __forceinline__ bool softmax_epilogue_8ph(f32x4 (&acc)[8][4], char* s
           acc[i][j][r] = e;
           sum += e;
         }
-      sum += __shfl_xor(sum, 16, 64);
-      sum += __shfl_xor(sum, 32, 64);
+      sum = sum_xor16_32(sum);
       if (lane < 16) {
         const int idx = ((wr * 4 + wc) * 128 + i * 16 + rl) * 2;
         st[idx] = m;
