@@ -83,6 +83,19 @@ def gemm_operands(A, B):
     return A, B
 
 
+_STREAMS = None
+
+
+def _streams():
+    """execution.streams, imported once (it imports this module lazily: no import cycle at load time)."""
+    global _STREAMS
+    if _STREAMS is None:
+        from ..execution import streams
+
+        _STREAMS = streams
+    return _STREAMS
+
+
 def gemm_nt(A, B, bias=None, bias_mode=BIAS_NONE, act=ACT_NONE, out_dtype=torch.bfloat16, alpha=1.0,
             dropout=0.0, seed=0, splits=0, out=None, accumulate=False, cfg=None, epi=None):
     """epilogue(alpha * A @ B^T) [+ out when accumulate]: A [..,M,K], B [..,N,K] (K-contiguous),
@@ -101,9 +114,8 @@ def gemm_nt(A, B, bias=None, bias_mode=BIAS_NONE, act=ACT_NONE, out_dtype=torch.
         h = _ext.hip()
         c = -1 if cfg is None else int(cfg)
         sig, sval, pf = None, 0, None
-        from ..execution import streams
-
-        trig = streams.armed_trigger(A.device)
+        streams = _streams()
+        trig = streams.armed_trigger(A.device) if streams._armed else None
         pf_armed = bool(streams._armed_pf)
         start_sig, taken, nwg = None, None, 0
         if trig is not None or pf_armed:
