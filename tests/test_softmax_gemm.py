@@ -140,3 +140,48 @@ def test_ff_engine_fuses_softmax_into_gemm_epilogue():
     ref = ff.reference_inference(gt("inputs"), gt("w1"), gt("b1"), gt("wo"), gt("bo"))
     assert (out - ref).abs().max().item() < 2e-3
     torch.testing.assert_close(out.sum(1), torch.ones(out.shape[0], device=out.device), atol=1e-4, rtol=0)
+
+
+@pytest.mark.gpu
+def test_softmax_gemm_not_co_resident_gpu():
+    """The fused softmax needs every tile of a row-block resident at once. Here a long split-K GEMM takes a START
+    gate that leaves 64 CUs free, and the fused softmax of the FF output shape (228 tiles) is gated on it from
+    another stream: 64 tiles get CUs, the rest only when the GEMM's workgroups finish. The resident tiles' bounded
+    poll runs out, they write exp(x - m_tile) and depart flagged; the late ones find their row-block complete and
+    finish normally; the last tile to depart rescales the flagged ones. Slow, but exact and never hung."""
+    from netsdb_amd import _ext
+    from netsdb_amd.execution.streams import JobStreams, TailTrigger
+
+    dev = "cuda:0"
+    g = torch.Generator(device=dev).manual_seed(11)
+    M, N, K = 1000, 14588, 1000
+    A = torch.empty(M, K, device=dev).uniform_(0, 1, generator=g).to(torch.bfloat16)
+    B = (torch.empty(N, K, device=dev).uniform_(-1, 1, generator=g) * 0.055).to(torch.bfloat16)
+    bias = torch.empty(N, device=dev).uniform_(-0.1, 0.1, generator=g)
+    GA = torch.empty(1024, 1 << 20, device=dev).uniform_(-1, 1, generator=g).to(torch.bfloat16)
+    GB = (torch.empty(1024, 1 << 20, device=dev).uniform_(-1, 1, generator=g) * 1e-3).to(torch.bfloat16)
+    ref = _ref(A, B, bias, ops.BIAS_COL, 1)
+    torch.cuda.synchronize()
+    tiles = ((M + 255) // 256) * ((N + 255) // 256)
+    st = torch.zeros(tiles * 8, dtype=torch.int64, device=dev)
+    js = JobStreams(dev, lanes=1)
+    gate = TailTrigger(dev, mode="start", reserve_cus=64)
+    for rep in range(2):          # the first GEMM launch of a process is slow to start (the softmax then runs after it)
+        gate.arm()
+        C = ops.gemm_nt(GA, GB, out_dtype=torch.float32)          # ~4 ms, 192 workgroups
+        h = js.submit(lambda: _ext.hip().gemm_nt_softmax(A, B, bias, ops.BIAS_COL, 1, None, 1.0, False, -1, st),
+                      independent=True, start_on=gate)
+        y = h.synchronize()
+        torch.cuda.synchronize()
+        assert gate.gated == rep + 1 and torch.isfinite(C).all()
+        assert (y - ref).abs().max().item() / ref.abs().max().item() < 2e-5
+    assert (y - ref).abs().max().item() / ref.abs().max().item() < 2e-5
+    torch.testing.assert_close(y.sum(1), torch.ones(M, device=dev), atol=1e-4, rtol=0)
+    # the scenario happened: some tiles' bounded poll ran out (>= ~200 us on the 100 MHz clock) and some tiles
+    # started only after those timeouts
+    s8 = st.view(tiles, 8).cpu()
+    poll = s8[:, 3] - s8[:, 2]
+    assert int((poll >= 19000).sum()) > 0, poll.max()
+    assert int(s8[:, 0].max()) > int(s8[:, 3][poll >= 19000].min())
+    y2 = ops.gemm_nt_softmax(A, B, bias, ops.BIAS_COL, axis=1)      # counters / flags left clean
+    torch.testing.assert_close(y2, y, atol=1e-6, rtol=1e-5)
