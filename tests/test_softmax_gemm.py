@@ -166,7 +166,8 @@ def test_softmax_gemm_not_co_resident_gpu():
     st = torch.zeros(tiles * 8, dtype=torch.int64, device=dev)
     js = JobStreams(dev, lanes=1)
     gate = TailTrigger(dev, mode="start", reserve_cus=64)
-    for rep in range(2):          # the first GEMM launch of a process is slow to start (the softmax then runs after it)
+    exercised = []
+    for rep in range(3):          # the first GEMM launch of a process is slow to start (the softmax then runs after it)
         gate.arm()
         C = ops.gemm_nt(GA, GB, out_dtype=torch.float32)          # ~4 ms, 192 workgroups
         h = js.submit(lambda: _ext.hip().gemm_nt_softmax(A, B, bias, ops.BIAS_COL, 1, None, 1.0, False, -1, st),
@@ -175,13 +176,12 @@ def test_softmax_gemm_not_co_resident_gpu():
         torch.cuda.synchronize()
         assert gate.gated == rep + 1 and torch.isfinite(C).all()
         assert (y - ref).abs().max().item() / ref.abs().max().item() < 2e-5
-    assert (y - ref).abs().max().item() / ref.abs().max().item() < 2e-5
-    torch.testing.assert_close(y.sum(1), torch.ones(M, device=dev), atol=1e-4, rtol=0)
-    # the scenario happened: some tiles' bounded poll ran out (>= ~200 us on the 100 MHz clock) and some tiles
-    # started only after those timeouts
-    s8 = st.view(tiles, 8).cpu()
-    poll = s8[:, 3] - s8[:, 2]
-    assert int((poll >= 19000).sum()) > 0, poll.max()
-    assert int(s8[:, 0].max()) > int(s8[:, 3][poll >= 19000].min())
+        torch.testing.assert_close(y.sum(1), torch.ones(M, device=dev), atol=1e-4, rtol=0)
+        # did the scenario happen: some tiles' bounded poll ran out (>= ~200 us on the 100 MHz clock) and some
+        # tiles started only after those timeouts?
+        s8 = st.view(tiles, 8).cpu()
+        timed_out = (s8[:, 3] - s8[:, 2]) >= 19000
+        exercised.append(bool(timed_out.any()) and int(s8[:, 0].max()) > int(s8[:, 3][timed_out].min()))
+    assert any(exercised), exercised
     y2 = ops.gemm_nt_softmax(A, B, bias, ops.BIAS_COL, axis=1)      # counters / flags left clean
     torch.testing.assert_close(y2, y, atol=1e-6, rtol=1e-5)
