@@ -234,3 +234,17 @@ def test_trigger_taken_by_failed_launch_does_not_gate_gpu(mode):
     js = JobStreams(dev, lanes=1)
     y = js.submit(lambda: A[:4, :4].float().sum(), independent=True, start_on=trig).synchronize()
     assert trig.gated == 0 and torch.isfinite(y) and trig.count == 0
+
+
+def test_start_gate_and_prefetch_api_cpu():
+    """CPU: a start gate is inert (no flag, nothing gated), an operand prefetch of a host tensor is refused, and
+    an unknown trigger mode is rejected."""
+    from netsdb_amd.execution import streams
+    from netsdb_amd.execution.streams import TailTrigger
+
+    g = TailTrigger("cpu", mode="start", reserve_cus=16).arm()
+    assert g.flag is None and g.gate(None) is False and g.count == 0
+    assert streams.arm_operand_prefetch(torch.zeros(4)) is False
+    assert streams.take_operand_prefetch("cpu") is None
+    with pytest.raises(ValueError):
+        TailTrigger("cpu", mode="middle")
