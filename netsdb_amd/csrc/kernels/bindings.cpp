@@ -5,6 +5,7 @@
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
+#include <limits>
 #include <map>
 #include <vector>
 #include <mutex>
@@ -53,6 +54,8 @@ int nsdb_block_simcount(const void* pool, const long long* cand, const void* que
 int nsdb_block_maxdiff(const void* pool, const long long* cand, const void* blks, long long nblocks, long long elems,
                        int is_f32, int S, float* partial, hipStream_t st);
 int nsdb_str_hash(const void* bytes, const int64_t* off, int64_t n, uint64_t* out, hipStream_t st);
+int nsdb_hash_group_insert(const void* keys, long long n, void* table, long long cap, int* slot_of, int* occ,
+                           hipStream_t st);
 int nsdb_str_like(const void* bytes, const int64_t* off, int64_t n, const uint8_t* pat, int pat_len,
                   const int* seg_start, const int* seg_len, int nseg, int anchor_start, int anchor_end, int negate,
                   uint8_t* out, hipStream_t st);
@@ -569,6 +572,33 @@ torch::Tensor str_slice(torch::Tensor bytes, torch::Tensor off, int64_t start, t
   return dst;
 }
 
+// Exact group-by of a device int64 key column (hashagg.hip): one insert launch into an open-addressing table,
+// then only the g distinct keys are sorted. Returns (inverse [n] i64, sorted distinct keys [g] i64) — the same
+// result as torch.unique(keys, sorted=True, return_inverse=True).
+std::vector<torch::Tensor> hash_group_ids(torch::Tensor keys) {
+  check_cuda(keys, "keys");
+  TORCH_CHECK(keys.scalar_type() == torch::kInt64 && keys.dim() == 1, "keys must be a 1-D int64 tensor");
+  keys = keys.contiguous();
+  const int64_t n = keys.numel();
+  if (n == 0) return {torch::empty({0}, keys.options()), torch::empty({0}, keys.options())};
+  TORCH_CHECK(n < (int64_t(1) << 29), "hash_group_ids: at most 2^29 rows per call (int32 slots)");
+  int64_t cap = 1024;
+  while (cap < 2 * n) cap <<= 1;
+  auto table = torch::full({cap + 1}, std::numeric_limits<int64_t>::min(), keys.options());
+  auto occ = torch::zeros({cap + 1}, keys.options().dtype(torch::kInt32));
+  auto slot_of = torch::empty({n}, keys.options().dtype(torch::kInt32));
+  check_rc(nsdb_hash_group_insert(keys.data_ptr(), n, table.data_ptr(), cap, slot_of.data_ptr<int>(),
+                                  occ.data_ptr<int>(), cur_stream()),
+           "hash_group_insert");
+  auto slots = occ.nonzero().squeeze(1);                      // occupied slots (one host read: the count g)
+  auto sorted = table.index_select(0, slots).sort();
+  auto uniq = std::get<0>(sorted);
+  auto rank = torch::empty({cap + 1}, keys.options());
+  rank.index_put_({slots.index_select(0, std::get<1>(sorted))},
+                  torch::arange(uniq.numel(), keys.options()));
+  return {rank.index_select(0, slot_of.to(torch::kInt64)), uniq};
+}
+
 // Dedup: blocks [n, ...] contiguous (any dtype; bytes per block % 16 == 0) -> [n, S] i64 partial sums.
 torch::Tensor block_hash_partial(torch::Tensor blocks) {
   check_cuda(blocks, "blocks");
@@ -692,6 +722,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("block_simcount_partial", &block_simcount_partial,
         "approximate dedup: per-(candidate, split) counts of elements within fp of a query block");
   m.def("block_maxdiff_partial", &block_maxdiff_partial, "dedup: per-(block, split) max |pool[cand] - blk|");
+  m.def("hash_group_ids", &hash_group_ids, "exact group-by of a device int64 column: (inverse, sorted keys)");
   m.def("str_hash", &str_hash, "64-bit hash per string of a device string column");
   m.def("str_like", &str_like, "SQL LIKE over a device string column (segments of the pattern bytes)");
   m.def("str_slice", &str_slice, "SUBSTRING of every row of a device string column (no host read)");

@@ -13,6 +13,7 @@ from typing import Any, List, Tuple
 import torch
 import xxhash
 
+from .. import _ext
 from ..objects.record import RecordBatch, RecordView
 from ..objects.strings import StringColumn, hash_str, is_string_list
 
@@ -127,6 +128,10 @@ def group_ids(keys) -> Tuple[torch.Tensor, Any, int]:
                      for j, k in enumerate(keys))
         return inv, reps, uniq.shape[0]
     if isinstance(keys, torch.Tensor) and keys.dim() == 1:
+        if keys.is_cuda and not keys.is_floating_point() and keys.dtype != torch.bool:
+            # device hash table (hashagg.hip): O(n) insert, only the distinct keys are sorted
+            inv, uniq = _ext.hip().hash_group_ids(keys.long())
+            return inv, uniq.to(keys.dtype), uniq.numel()
         uniq, inv = torch.unique(keys, return_inverse=True)
         return inv, uniq, uniq.numel()
     # host objects: dict grouping preserving first-seen order
@@ -147,7 +152,10 @@ def group_ids(keys) -> Tuple[torch.Tensor, Any, int]:
 
 def _unique_first(h: torch.Tensor):
     """(inverse, first row of each group, #groups) for a 1-D key tensor."""
-    uniq, inv = torch.unique(h, return_inverse=True)
+    if h.is_cuda:
+        inv, uniq = _ext.hip().hash_group_ids(h)
+    else:
+        uniq, inv = torch.unique(h, return_inverse=True)
     first = torch.full((uniq.numel(),), h.numel(), dtype=torch.long, device=h.device)
     first.scatter_reduce_(0, inv, torch.arange(h.numel(), device=h.device), "amin")
     return inv, first, uniq.numel()
