@@ -128,7 +128,7 @@ def group_ids(keys) -> Tuple[torch.Tensor, Any, int]:
                      for j, k in enumerate(keys))
         return inv, reps, uniq.shape[0]
     if isinstance(keys, torch.Tensor) and keys.dim() == 1:
-        if keys.is_cuda and not keys.is_floating_point() and keys.dtype != torch.bool:
+        if keys.is_cuda and not keys.is_floating_point() and keys.dtype != torch.bool and _hash_groupby():
             # device hash table (hashagg.hip): O(n) insert, only the distinct keys are sorted
             inv, uniq = _ext.hip().hash_group_ids(keys.long())
             return inv, uniq.to(keys.dtype), uniq.numel()
@@ -150,9 +150,18 @@ def group_ids(keys) -> Tuple[torch.Tensor, Any, int]:
     return torch.tensor(inv, dtype=torch.int64), reps, len(reps)
 
 
+def _hash_groupby() -> bool:
+    """Device hash-table group ids (hashagg.hip) instead of torch.unique; ops.kernel_options(hash_groupby=...)."""
+    from .. import ops
+    return bool(ops._kopt("hash_groupby", HASH_GROUPBY_DEFAULT))
+
+
+HASH_GROUPBY_DEFAULT = False
+
+
 def _unique_first(h: torch.Tensor):
     """(inverse, first row of each group, #groups) for a 1-D key tensor."""
-    if h.is_cuda:
+    if h.is_cuda and _hash_groupby():
         inv, uniq = _ext.hip().hash_group_ids(h)
     else:
         uniq, inv = torch.unique(h, return_inverse=True)

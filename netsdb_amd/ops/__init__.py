@@ -321,7 +321,8 @@ def conv_filter_fragments(Wflat, C, KH, KW):
 
 
 _KOPTS = threading.local()
-_KOPT_KEYS = {"conv_kernel", "conv_blocks", "conv_generic", "conv_variant", "conv_contig", "rownorm_plain_loads"}
+_KOPT_KEYS = {"conv_kernel", "conv_blocks", "conv_generic", "conv_variant", "conv_contig", "rownorm_plain_loads",
+              "hash_groupby"}
 
 
 @contextlib.contextmanager
@@ -330,8 +331,8 @@ def kernel_options(**kw):
     conv_kernel (conv2d row kernel: 5 warp-specialised = default, 1 full-row, 0 two-pass; 2/3/4/6 diagnostics),
     conv_blocks (row-kernel grid cap, default 512; 0 = one block per row group), conv_generic (bool: the generic
     gather kernel), conv_variant / conv_contig (row-kernel diagnostics), rownorm_plain_loads (bool: row normalise
-    with cache-allocating loads). Every option is passed per call to the kernel library, which keeps no
-    process-wide launch state: other threads (server requests, job lanes on their own threads) never see them."""
+    with cache-allocating loads), hash_groupby (bool: device hash-table group ids, default off). Every option is
+    passed per call to the kernel library, which keeps no process-wide launch state: other threads (server requests, job lanes on their own threads) never see them."""
     bad = set(kw) - _KOPT_KEYS
     if bad:
         raise ValueError(f"unknown kernel options {sorted(bad)}")

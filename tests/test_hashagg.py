@@ -37,18 +37,24 @@ def test_hash_group_ids_matches_unique_gpu():
 @pytest.mark.gpu
 def test_group_ids_uses_hash_table_gpu():
     dev = "cuda:0"
+    from netsdb_amd import ops
     keys32 = torch.randint(-100, 100, (100_000,), device=dev, dtype=torch.int32)
-    inv, reps, n = K.group_ids(keys32)
+    with ops.kernel_options(hash_groupby=True):
+        inv, reps, n = K.group_ids(keys32)
     ru, ri = torch.unique(keys32, return_inverse=True)
     assert n == ru.numel() and reps.dtype == torch.int32 and torch.equal(reps, ru) and torch.equal(inv, ri)
     # string keys group by their device hash through the same table
     from netsdb_amd.objects.strings import StringColumn
     words = ["ab", "c", "ab", "", "xyz", "c", "ab"] * 1000
     col = StringColumn.from_list(words, dev)
-    inv, reps, n = K.group_ids(col)
+    with ops.kernel_options(hash_groupby=True):
+        inv, reps, n = K.group_ids(col)
     assert n == 4 and sorted(reps.tolist()) == sorted(set(words))
     back = [reps.tolist()[i] for i in inv.tolist()]
     assert back == words
+    with ops.kernel_options(hash_groupby=False):          # torch.unique path, same result
+        inv2, reps2, n2 = K.group_ids(keys32)
+    assert n2 == n and torch.equal(reps2, ru) and torch.equal(inv2, ri)
 
 
 def test_hash_group_ids_rejects_bad_input_cpu():
