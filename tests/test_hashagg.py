@@ -54,7 +54,7 @@ def test_group_ids_uses_hash_table_gpu():
     assert back == words
     with ops.kernel_options(hash_groupby=False):          # torch.unique path, same result
         inv2, reps2, n2 = K.group_ids(keys32)
-    assert n2 == n and torch.equal(reps2, ru) and torch.equal(inv2, ri)
+    assert n2 == ru.numel() and torch.equal(reps2, ru) and torch.equal(inv2, ri)
 
 
 def test_hash_group_ids_rejects_bad_input_cpu():
