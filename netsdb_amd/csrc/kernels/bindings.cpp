@@ -54,16 +54,20 @@ int nsdb_block_simcount(const void* pool, const long long* cand, const void* que
 int nsdb_block_maxdiff(const void* pool, const long long* cand, const void* blks, long long nblocks, long long elems,
                        int is_f32, int S, float* partial, hipStream_t st);
 int nsdb_str_hash(const void* bytes, const int64_t* off, int64_t n, uint64_t* out, hipStream_t st);
-int nsdb_hash_group_insert(const void* keys, long long n, void* table, long long cap, int* slot_of, int* occ,
-                           hipStream_t st);
 int nsdb_str_like(const void* bytes, const int64_t* off, int64_t n, const uint8_t* pat, int pat_len,
                   const int* seg_start, const int* seg_len, int nseg, int anchor_start, int anchor_end, int negate,
                   uint8_t* out, hipStream_t st);
 int nsdb_str_slice(const void* src, const int64_t* off, int64_t start, const int64_t* out_off, int64_t n, void* dst,
                    hipStream_t st);
+int nsdb_str_eq_pairs(const void* a, const int64_t* offa, const int64_t* ia, const void* b, const int64_t* offb,
+                      const int64_t* ib, int64_t m, uint8_t* out, hipStream_t st);
 int nsdb_str_gather(const void* src, const int64_t* off, const int64_t* idx, const int64_t* out_off, int64_t m,
                     void* dst, hipStream_t st);
 }
+
+void register_relops(pybind11::module& m);
+std::vector<torch::Tensor> hash_aggregate_impl(torch::Tensor keys, c10::optional<torch::Tensor> vals,
+                                               const std::string& op, bool want_inv, int64_t low_threshold);
 
 namespace {
 
@@ -557,6 +561,35 @@ torch::Tensor str_gather(torch::Tensor bytes, torch::Tensor off, torch::Tensor i
   return dst;
 }
 
+// out[i] = (a[ia[i]] == b[ib[i]]) byte-exact; ia / ib may be None (identity). Indices are checked on the device
+// by the caller (they come from the same grouping / join that produced them).
+torch::Tensor str_eq_pairs(torch::Tensor a, torch::Tensor offa, c10::optional<torch::Tensor> ia, torch::Tensor b,
+                           torch::Tensor offb, c10::optional<torch::Tensor> ib, int64_t m) {
+  check_strings(a, offa);
+  check_strings(b, offb);
+  const int64_t* pa = nullptr;
+  const int64_t* pb = nullptr;
+  if (ia.has_value() && ia->defined()) {
+    check_cuda(*ia, "ia");
+    TORCH_CHECK(ia->scalar_type() == torch::kInt64 && ia->is_contiguous() && ia->numel() == m, "ia i64 [m]");
+    pa = ia->data_ptr<int64_t>();
+  } else {
+    TORCH_CHECK(offa.numel() - 1 >= m, "a has fewer than m rows");
+  }
+  if (ib.has_value() && ib->defined()) {
+    check_cuda(*ib, "ib");
+    TORCH_CHECK(ib->scalar_type() == torch::kInt64 && ib->is_contiguous() && ib->numel() == m, "ib i64 [m]");
+    pb = ib->data_ptr<int64_t>();
+  } else {
+    TORCH_CHECK(offb.numel() - 1 >= m, "b has fewer than m rows");
+  }
+  auto out = torch::empty({m}, a.options());
+  check_rc(nsdb_str_eq_pairs(a.data_ptr(), offa.data_ptr<int64_t>(), pa, b.data_ptr(), offb.data_ptr<int64_t>(), pb, m,
+                             out.data_ptr<uint8_t>(), cur_stream()),
+           "str_eq_pairs");
+  return out.view(torch::kBool);
+}
+
 // SUBSTRING of every row: out_off [n+1] (device prefix sums of the clamped lengths), cap = an upper bound of the
 // output bytes known on the host (n * length): no device read to size the buffer.
 torch::Tensor str_slice(torch::Tensor bytes, torch::Tensor off, int64_t start, torch::Tensor out_off, int64_t cap) {
@@ -572,31 +605,20 @@ torch::Tensor str_slice(torch::Tensor bytes, torch::Tensor off, int64_t start, t
   return dst;
 }
 
-// Exact group-by of a device int64 key column (hashagg.hip): one insert launch into an open-addressing table,
-// then only the g distinct keys are sorted. Returns (inverse [n] i64, sorted distinct keys [g] i64) — the same
-// result as torch.unique(keys, sorted=True, return_inverse=True).
+// Exact group-by of a device int64 key column on the device hash aggregation (relops.hip), returned as
+// torch.unique(keys, sorted=True, return_inverse=True) would: (inverse [n] i64, sorted distinct keys [g] i64).
+// Only the g distinct keys are sorted.
 std::vector<torch::Tensor> hash_group_ids(torch::Tensor keys) {
   check_cuda(keys, "keys");
   TORCH_CHECK(keys.scalar_type() == torch::kInt64 && keys.dim() == 1, "keys must be a 1-D int64 tensor");
-  keys = keys.contiguous();
   const int64_t n = keys.numel();
   if (n == 0) return {torch::empty({0}, keys.options()), torch::empty({0}, keys.options())};
-  TORCH_CHECK(n < (int64_t(1) << 29), "hash_group_ids: at most 2^29 rows per call (int32 slots)");
-  int64_t cap = 1024;
-  while (cap < 2 * n) cap <<= 1;
-  auto table = torch::full({cap + 1}, std::numeric_limits<int64_t>::min(), keys.options());
-  auto occ = torch::zeros({cap + 1}, keys.options().dtype(torch::kInt32));
-  auto slot_of = torch::empty({n}, keys.options().dtype(torch::kInt32));
-  check_rc(nsdb_hash_group_insert(keys.data_ptr(), n, table.data_ptr(), cap, slot_of.data_ptr<int>(),
-                                  occ.data_ptr<int>(), cur_stream()),
-           "hash_group_insert");
-  auto slots = occ.nonzero().squeeze(1);                      // occupied slots (one host read: the count g)
-  auto sorted = table.index_select(0, slots).sort();
-  auto uniq = std::get<0>(sorted);
-  auto rank = torch::empty({cap + 1}, keys.options());
-  rank.index_put_({slots.index_select(0, std::get<1>(sorted))},
-                  torch::arange(uniq.numel(), keys.options()));
-  return {rank.index_select(0, slot_of.to(torch::kInt64)), uniq};
+  auto r = hash_aggregate_impl(keys, c10::nullopt, "sum", true, 0);
+  TORCH_CHECK(r[5][2].item<int64_t>() == 1, "hash_group_ids: device table overflow");
+  auto sorted = r[0].sort();
+  auto rank = torch::empty_like(r[0]);
+  rank.index_put_({std::get<1>(sorted)}, torch::arange(r[0].numel(), keys.options()));
+  return {rank.index_select(0, r[4]), std::get<0>(sorted)};
 }
 
 // Dedup: blocks [n, ...] contiguous (any dtype; bytes per block % 16 == 0) -> [n, S] i64 partial sums.
@@ -673,6 +695,7 @@ torch::Tensor block_simcount_partial(torch::Tensor pool, torch::Tensor cand, tor
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "netsdb_amd CDNA4 (gfx950) HIP kernels";
+  register_relops(m);
   m.def("gemm_nt", &gemm_nt, "epi(alpha*A@B^T) on MFMA", py::arg("A"), py::arg("B"), py::arg("bias") = py::none(),
         py::arg("bias_mode") = 0, py::arg("act") = 0, py::arg("out_f32") = false, py::arg("alpha") = 1.0,
         py::arg("dropout") = 0.0, py::arg("seed") = 0, py::arg("splits") = 0, py::arg("out") = py::none(),
@@ -726,5 +749,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("str_hash", &str_hash, "64-bit hash per string of a device string column");
   m.def("str_like", &str_like, "SQL LIKE over a device string column (segments of the pattern bytes)");
   m.def("str_slice", &str_slice, "SUBSTRING of every row of a device string column (no host read)");
+  m.def("str_eq_pairs", &str_eq_pairs, "byte-exact equality of string row pairs a[ia[i]] == b[ib[i]]",
+        py::arg("a"), py::arg("offa"), py::arg("ia"), py::arg("b"), py::arg("offb"), py::arg("ib"), py::arg("m"));
   m.def("str_gather", &str_gather, "take() of a device string column into a new padded byte buffer");
 }

@@ -1,0 +1,900 @@
+// Device relational operators: hash aggregation, hash join (build / probe / expand) and the partition+pack
+// permutation of the shuffle sink. Reference: netsDB aggregates through C++ hash maps per page
+// (src/queryExecution/headers/AggregationProcessor.h:16, CombinerProcessor, PartitionedHashSet.h:20), joins
+// through JoinMap / PairArray (src/lambdas/headers/JoinTuple.h:434 JoinProbe, :1243 PartitionedJoinSink,
+// HashSink.h:14) and partitions with HashPartitionSink. Here each is a few device launches over whole columns.
+//
+// Hash aggregation of n rows (one int64 key per row; multi-column keys are packed or hashed by the caller,
+// execution/kernels.py) with F value columns (8-byte: double or int64; op sum / min / max; a row count always):
+//
+//  * agg_sample: ONE workgroup counts the distinct keys of 4096 evenly spaced rows into a device word. Every
+//    later kernel reads that word and returns at once when its path is not the one taken, so the choice costs
+//    no host round trip (the only host read of the whole aggregation is the final group count).
+//  * LOW path (few groups): agg_low — each workgroup pre-aggregates its rows in an LDS hash table (claim by LDS
+//    CAS, f64 / u64 LDS atomics), rows whose key does not fit go straight to a small global table, and at the
+//    end each workgroup flushes its LDS entries ONCE into the global table (agent-scope atomics). Millions of
+//    rows on a handful of keys therefore cost one global atomic per (workgroup, key), not per row. If the
+//    global table overflows (the sample under-estimated the groups) a device flag routes the work to:
+//  * PART path (many groups): radix partition by the top hash bits (agg_hist: per-workgroup LDS histograms;
+//    agg_scan_rows / agg_scan_tot: bucket-major exclusive scans + a work list of <= CH-row chunks; agg_scatter:
+//    keys, values and row ids packed bucket-contiguous), then agg_part: persistent workgroups dequeue chunks
+//    (one returning atomic on a device word), aggregate a chunk in an LDS table sized so a whole bucket fits,
+//    and write a bucket that is one chunk straight to the dense output (its groups occur nowhere else).
+//    Buckets of several chunks (hot keys) flush through a global table instead.
+//  * agg_emit copies the global-table groups to the dense output; agg_fix_inv turns per-row global-slot
+//    references into dense group ids (only when the caller wants the per-row inverse).
+// Dense group ids come from one device counter bumped by whoever creates a group, so there is no compaction
+// pass over the tables and no nonzero()/sort.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+namespace nsdb_rel {
+
+typedef unsigned long long u64;
+typedef long long i64;
+constexpr u64 kEmpty = 0x8000000000000000ull;   // empty-slot marker (rows whose key is this value get a slot of their own)
+
+__device__ __forceinline__ u64 mix64(u64 x) {
+  x ^= x >> 30;
+  x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 27;
+  x *= 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return x;
+}
+
+// ---------------------------------------------------------------- accumulators (8-byte words)
+enum AggOp : int { OP_SUM = 0, OP_MIN = 1, OP_MAX = 2 };
+
+// order-preserving u64 image of a double / int64, so min / max are unsigned integer atomics
+__device__ __forceinline__ u64 ord_of(double v) {
+  const u64 b = __double_as_longlong(v);
+  return (b & kEmpty) ? ~b : (b | kEmpty);
+}
+__device__ __forceinline__ u64 ord_of(i64 v) { return (u64)v ^ kEmpty; }
+__device__ __forceinline__ double ord_to_f64(u64 o) {
+  return __longlong_as_double((o & kEmpty) ? (i64)(o & ~kEmpty) : (i64)~o);
+}
+__device__ __forceinline__ i64 ord_to_i64(u64 o) { return (i64)(o ^ kEmpty); }
+
+template <typename VT, int OP>
+__host__ __device__ __forceinline__ u64 acc_identity() {
+  if constexpr (OP == OP_MIN) return ~0ull;
+  else if constexpr (OP == OP_MAX) return 0ull;
+  else return 0ull;   // +0.0 and integer 0 are both all-zero bits
+}
+
+template <typename VT, int OP, int SCOPE>
+__device__ __forceinline__ void acc_add(u64* p, VT v) {
+  if constexpr (OP == OP_SUM) {
+    if constexpr (sizeof(VT) == 8 && __is_same(VT, double))
+      __hip_atomic_fetch_add(reinterpret_cast<double*>(p), v, __ATOMIC_RELAXED, SCOPE);
+    else
+      __hip_atomic_fetch_add(p, (u64)v, __ATOMIC_RELAXED, SCOPE);
+  } else if constexpr (OP == OP_MIN) {
+    __hip_atomic_fetch_min(p, ord_of(v), __ATOMIC_RELAXED, SCOPE);
+  } else {
+    __hip_atomic_fetch_max(p, ord_of(v), __ATOMIC_RELAXED, SCOPE);
+  }
+}
+
+// merge an already-accumulated word (an LDS partial) into a global accumulator
+template <typename VT, int OP>
+__device__ __forceinline__ void acc_merge_global(u64* p, u64 w) {
+  if constexpr (OP == OP_SUM) {
+    if constexpr (__is_same(VT, double))
+      __hip_atomic_fetch_add(reinterpret_cast<double*>(p), __longlong_as_double((i64)w), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    else
+      __hip_atomic_fetch_add(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if constexpr (OP == OP_MIN) {
+    __hip_atomic_fetch_min(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    __hip_atomic_fetch_max(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// accumulator word -> output value bits
+template <typename VT, int OP>
+__device__ __forceinline__ u64 acc_out(u64 w) {
+  if constexpr (OP == OP_SUM) return w;
+  else if constexpr (__is_same(VT, double)) return (u64)__double_as_longlong(ord_to_f64(w));
+  else return (u64)ord_to_i64(w);
+}
+
+// ---------------------------------------------------------------- shared state of one aggregation
+// One int64 word array zeroed by the host per call.
+struct AggMeta {
+  i64 est;            // distinct keys in the sample
+  i64 low;            // 1: the sample says few groups -> LOW path first
+  i64 ng_low;         // groups created by the LOW path
+  i64 ng_part;        // groups created by the PART path
+  i64 fail_low;       // LOW global table overflowed -> PART path runs
+  i64 fail_part;      // PART global table overflowed -> the caller falls back
+  i64 sentinel_low;   // the kEmpty key's group was created (LOW / PART)
+  i64 sentinel_part;
+  i64 nwork;          // PART work items (chunks)
+  i64 wnext;          // PART dequeue counter
+  i64 pad[6];
+};
+
+struct GTable {                     // open-addressing global table: cap slots + one slot (cap) for the kEmpty key
+  u64* key;                         // [cap + 1], preset kEmpty
+  u64* acc;                         // [(cap + 1) * F], preset to the op identity
+  u64* cnt;                         // [cap + 1], preset 0
+  u64* rmin;                        // [cap + 1], preset ~0: smallest row index of the group
+  i64* gid_of_slot;                 // [cap + 1]
+  u64 mask;                         // cap - 1
+};
+
+struct AggOut {
+  i64* reps;        // [n] dense group keys
+  u64* aggs;        // [n * F]
+  i64* cnt;         // [n]
+  i64* slot_of_gid; // [n] global slot of a group, or -1 when the group was written directly
+  i64* first;       // [n] smallest row index of each group (its representative row)
+  i64* inv;         // [n] or null
+};
+
+__device__ __forceinline__ bool take_low(const AggMeta* m) { return m->low != 0; }
+__device__ __forceinline__ bool take_part(const AggMeta* m) { return m->low == 0 || m->fail_low != 0; }
+
+constexpr int kLdsProbe = 64;     // LDS probe window: a row whose window is full goes to the global table
+constexpr u64 kGlobalProbe = 1024;  // global probe window: beyond it the table counts as full (fail flag)
+
+// Global slot of key k (created on first sight). Returns -1 when the table is full (fail flag set).
+__device__ __forceinline__ i64 gtable_slot(GTable t, u64 k, i64* ngroups, i64* sentinel, i64* fail, AggOut o) {
+  if (k == kEmpty) {
+    const u64 s = t.mask + 1;
+    i64 exp0 = 0;
+    if (__hip_atomic_compare_exchange_strong(sentinel, &exp0, (i64)1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT)) {
+      const i64 gid = __hip_atomic_fetch_add(ngroups, (i64)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      t.gid_of_slot[s] = gid;
+      o.reps[gid] = (i64)k;
+      o.slot_of_gid[gid] = (i64)s;
+    }
+    return (i64)s;
+  }
+  u64 s = mix64(k) & t.mask;
+  const u64 window = t.mask < kGlobalProbe ? t.mask + 1 : kGlobalProbe;
+  for (u64 p = 0; p < window; ++p) {
+    u64 cur = __hip_atomic_load(t.key + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == kEmpty) {
+      if (__hip_atomic_compare_exchange_strong(t.key + s, &cur, k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)) {
+        const i64 gid = __hip_atomic_fetch_add(ngroups, (i64)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // more groups than half the table: probe windows grow long -> give up on this table
+        if ((u64)gid > (t.mask >> 1)) __hip_atomic_store(fail, (i64)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        t.gid_of_slot[s] = gid;
+        o.reps[gid] = (i64)k;
+        o.slot_of_gid[gid] = (i64)s;
+        return (i64)s;
+      }
+      // cur now holds the key another row claimed this slot with
+    }
+    if (cur == k) return (i64)s;
+    s = (s + 1) & t.mask;
+  }
+  __hip_atomic_store(fail, (i64)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return -1;
+}
+
+// LDS table of one workgroup: key words, F accumulators, counts, and the global slot / group id each entry
+// ends up in. Laid out as [key | acc | cnt | ref] in one dynamic LDS array.
+struct LTable {
+  u64* key;
+  u64* acc;
+  unsigned* cnt;
+  i64* ref;
+  u64* rmin;
+  int cap;   // power of two
+};
+
+// [key | acc | ref | rmin | cnt]: 28 + 8F bytes per entry
+__device__ __forceinline__ LTable ltable_at(char* base, int cap, int F) {
+  LTable t;
+  t.key = reinterpret_cast<u64*>(base);
+  t.acc = t.key + cap;
+  t.ref = reinterpret_cast<i64*>(t.acc + (size_t)cap * F);
+  t.rmin = reinterpret_cast<u64*>(t.ref + cap);
+  t.cnt = reinterpret_cast<unsigned*>(t.rmin + cap);
+  t.cap = cap;
+  return t;
+}
+
+template <typename VT, int OP>
+__device__ __forceinline__ void ltable_clear(LTable t, int F) {
+  for (int i = threadIdx.x; i < t.cap; i += blockDim.x) {
+    t.key[i] = kEmpty;
+    t.cnt[i] = 0;
+    t.ref[i] = 0;
+    t.rmin[i] = ~0ull;
+  }
+  for (int i = threadIdx.x; i < t.cap * F; i += blockDim.x) t.acc[i] = acc_identity<VT, OP>();
+}
+
+// LDS slot of k (inserted if absent), or -1 if its probe window is full.
+__device__ __forceinline__ int ltable_slot(LTable t, u64 k, u64 h) {
+  const int mask = t.cap - 1;
+  int s = (int)(h & (u64)mask);
+  const int window = t.cap < kLdsProbe ? t.cap : kLdsProbe;
+  for (int p = 0; p < window; ++p) {
+    u64 cur = t.key[s];
+    if (cur == kEmpty) {
+      u64 e = kEmpty;
+      __hip_atomic_compare_exchange_strong(t.key + s, &e, k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+      cur = e;   // kEmpty if this row claimed the slot, else the key that did
+      if (cur == kEmpty) return s;
+    }
+    if (cur == k) return s;
+    s = (s + 1) & mask;
+  }
+  return -1;
+}
+
+// lookup only (the key is known to be present when this is called for a row that hit the LDS table)
+__device__ __forceinline__ int ltable_find(LTable t, u64 k, u64 h) {
+  const int mask = t.cap - 1;
+  int s = (int)(h & (u64)mask);
+  const int window = t.cap < kLdsProbe ? t.cap : kLdsProbe;
+  for (int p = 0; p < window; ++p) {
+    const u64 cur = t.key[s];
+    if (cur == k) return s;
+    if (cur == kEmpty) return -1;
+    s = (s + 1) & mask;
+  }
+  return -1;
+}
+
+template <typename VT, int OP>
+__device__ __forceinline__ void row_into_global(GTable g, u64 k, const VT* v, int F, i64* ngroups, i64* sentinel,
+                                                i64* fail, AggOut o, i64 row) {
+  const i64 s = gtable_slot(g, k, ngroups, sentinel, fail, o);
+  if (s < 0) return;
+  for (int f = 0; f < F; ++f) acc_add<VT, OP, __HIP_MEMORY_SCOPE_AGENT>(g.acc + s * F + f, v[f]);
+  __hip_atomic_fetch_add(g.cnt + s, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_min(g.rmin + s, (u64)row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (o.inv) o.inv[row] = -(s + 1);
+}
+
+// ---------------------------------------------------------------- sample estimate
+__global__ __launch_bounds__(1024) void agg_sample_kernel(const u64* __restrict__ keys, i64 n, int low_thr,
+                                                          AggMeta* meta) {
+  constexpr int S = 4096, CAP = 8192;
+  __shared__ u64 tab[CAP];
+  __shared__ int count;
+  for (int i = threadIdx.x; i < CAP; i += blockDim.x) tab[i] = kEmpty;
+  if (threadIdx.x == 0) count = 0;
+  __syncthreads();
+  const int ns = (int)std::min<i64>(S, n);
+  for (int i = threadIdx.x; i < ns; i += blockDim.x) {
+    const i64 r = (n <= S) ? i : ((i64)i * n) / S;   // n < 2^31: no overflow
+    const u64 k = keys[r];
+    if (k == kEmpty) continue;
+    int s = (int)(mix64(k) & (CAP - 1));
+    for (;;) {
+      u64 e = kEmpty;
+      if (__hip_atomic_compare_exchange_strong(tab + s, &e, k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP)) {
+        atomicAdd(&count, 1);
+        break;
+      }
+      if (e == k) break;
+      s = (s + 1) & (CAP - 1);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    meta->est = count;
+    meta->low = count <= low_thr ? 1 : 0;
+  }
+}
+
+// One launch presets both global tables ([key | acc | cnt | gid] words) and zeroes the meta words.
+__global__ __launch_bounds__(256) void agg_init_kernel(u64* glow, i64 cap_low, u64* gpart, i64 cap_part, int F,
+                                                       u64 ident, AggMeta* meta) {
+  const i64 stride = (i64)gridDim.x * blockDim.x;
+  const i64 t0 = (i64)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int which = 0; which < 2; ++which) {
+    u64* base = which ? gpart : glow;
+    const i64 c1 = (which ? cap_part : cap_low) + 1;
+    for (i64 i = t0; i < c1 * (3 + F); i += stride) {
+      // key: kEmpty; acc: the op identity; cnt: 0; rmin: ~0 (the gid region is written on claim)
+      base[i] = i < c1 ? kEmpty : (i < c1 * (1 + F) ? ident : (i < c1 * (2 + F) ? 0ull : ~0ull));
+    }
+  }
+  if (t0 < (i64)(sizeof(AggMeta) / 8)) reinterpret_cast<i64*>(meta)[t0] = 0;
+}
+
+// ---------------------------------------------------------------- LOW path
+template <typename VT, int OP>
+__global__ __launch_bounds__(256) void agg_low_kernel(const u64* __restrict__ keys, const VT* __restrict__ vals, i64 n,
+                                                      int F, int lcap, GTable g, AggMeta* meta, AggOut o) {
+  if (!take_low(meta)) return;
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  LTable t = ltable_at(lds_raw, lcap, F);
+  ltable_clear<VT, OP>(t, F);
+  __syncthreads();
+  const i64 stride = (i64)gridDim.x * blockDim.x;
+  int it = 0;
+  for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride, ++it) {
+    if ((it & 63) == 63 && __hip_atomic_load(&meta->fail_low, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+    const u64 k = keys[i];
+    const VT* v = vals + i * F;
+    int s = -1;
+    if (k != kEmpty) s = ltable_slot(t, k, mix64(k));
+    if (s >= 0) {
+      for (int f = 0; f < F; ++f) acc_add<VT, OP, __HIP_MEMORY_SCOPE_WORKGROUP>(t.acc + s * F + f, v[f]);
+      __hip_atomic_fetch_add(t.cnt + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_min(t.rmin + s, (u64)i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+      row_into_global<VT, OP>(g, k, v, F, &meta->ng_low, &meta->sentinel_low, &meta->fail_low, o, i);
+    }
+  }
+  __syncthreads();
+  // one flush per (workgroup, key)
+  for (int e = threadIdx.x; e < lcap; e += blockDim.x) {
+    const u64 k = t.key[e];
+    if (k == kEmpty) continue;
+    const i64 s = gtable_slot(g, k, &meta->ng_low, &meta->sentinel_low, &meta->fail_low, o);
+    t.ref[e] = -(s + 1);
+    if (s < 0) continue;
+    for (int f = 0; f < F; ++f) acc_merge_global<VT, OP>(g.acc + s * F + f, t.acc[e * F + f]);
+    __hip_atomic_fetch_add(g.cnt + s, (u64)t.cnt[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_min(g.rmin + s, t.rmin[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (o.inv == nullptr) return;
+  __syncthreads();
+  for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const u64 k = keys[i];
+    if (k == kEmpty) continue;
+    const int s = ltable_find(t, k, mix64(k));
+    if (s >= 0) o.inv[i] = t.ref[s];
+  }
+}
+
+// ---------------------------------------------------------------- PART path
+// bucket of a key: the top pbits of its hash (the LDS slot uses the low bits)
+__device__ __forceinline__ int bucket_of(u64 k, int pbits) {
+  return pbits == 0 ? 0 : (int)(mix64(k) >> (64 - pbits));
+}
+
+// rows [wg * rpw, min(n, (wg + 1) * rpw)) per workgroup; hist is bucket-major [P][G]
+__global__ __launch_bounds__(1024) void agg_hist_kernel(const u64* __restrict__ keys, i64 n, i64 rpw, int pbits,
+                                                        unsigned* __restrict__ hist, const AggMeta* meta) {
+  if (!take_part(meta)) return;
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  unsigned* h = reinterpret_cast<unsigned*>(lds_raw);
+  const int P = 1 << pbits;
+  for (int i = threadIdx.x; i < P; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  const i64 r0 = (i64)blockIdx.x * rpw, r1 = std::min<i64>(n, r0 + rpw);
+  for (i64 i = r0 + threadIdx.x; i < r1; i += blockDim.x) atomicAdd(h + bucket_of(keys[i], pbits), 1u);
+  __syncthreads();
+  for (int b = threadIdx.x; b < P; b += blockDim.x) hist[(size_t)b * gridDim.x + blockIdx.x] = h[b];
+}
+
+// workgroup b: exclusive scan of hist[b][0..G) in place, tot[b] = its sum
+__global__ __launch_bounds__(256) void scan_rows_kernel(unsigned* __restrict__ hist, int G, i64* __restrict__ tot,
+                                                        const AggMeta* meta, int guard) {
+  if (guard && !take_part(meta)) return;
+  __shared__ unsigned part[256];
+  unsigned* row = hist + (size_t)blockIdx.x * G;
+  const int per = (G + 255) / 256;
+  const int c0 = threadIdx.x * per, c1 = std::min(G, c0 + per);
+  unsigned s = 0;
+  for (int c = c0; c < c1; ++c) s += row[c];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned run = 0;
+    for (int j = 0; j < 256; ++j) {
+      const unsigned x = part[j];
+      part[j] = run;
+      run += x;
+    }
+    tot[blockIdx.x] = run;
+  }
+  __syncthreads();
+  unsigned run = part[threadIdx.x];
+  for (int c = c0; c < c1; ++c) {
+    const unsigned x = row[c];
+    row[c] = run;
+    run += x;
+  }
+}
+
+// one workgroup: bstart = exclusive scan of tot[P] (+ total at P); work list: wstart[b] = first chunk of bucket b
+// (chunks of at most ch rows), nwork = total chunks
+__global__ __launch_bounds__(1024) void scan_tot_kernel(const i64* __restrict__ tot, int P, i64 ch,
+                                                        i64* __restrict__ bstart, i64* __restrict__ wstart,
+                                                        AggMeta* meta, int guard) {
+  if (guard && !take_part(meta)) return;
+  __shared__ i64 pr[1024], pw[1024];
+  const int per = (P + 1023) / 1024;
+  const int c0 = threadIdx.x * per, c1 = std::min(P, c0 + per);
+  i64 sr = 0, sw = 0;
+  for (int c = c0; c < c1; ++c) {
+    sr += tot[c];
+    if (wstart) sw += (tot[c] + ch - 1) / ch;
+  }
+  pr[threadIdx.x] = sr;
+  pw[threadIdx.x] = sw;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    i64 a = 0, b = 0;
+    for (int j = 0; j < 1024; ++j) {
+      const i64 x = pr[j], y = pw[j];
+      pr[j] = a;
+      pw[j] = b;
+      a += x;
+      b += y;
+    }
+    bstart[P] = a;
+    if (wstart) {
+      wstart[P] = b;
+      meta->nwork = b;
+    }
+  }
+  __syncthreads();
+  i64 a = pr[threadIdx.x], b = pw[threadIdx.x];
+  for (int c = c0; c < c1; ++c) {
+    bstart[c] = a;
+    a += tot[c];
+    if (wstart) {
+      wstart[c] = b;
+      b += (tot[c] + ch - 1) / ch;
+    }
+  }
+}
+
+// pack rows bucket-contiguous: pkey[pos], pval[pos * F + f], prow[pos]
+template <typename VT>
+__global__ __launch_bounds__(1024) void agg_scatter_kernel(const u64* __restrict__ keys, const VT* __restrict__ vals,
+                                                           i64 n, int F, i64 rpw, int pbits,
+                                                           const unsigned* __restrict__ hist,
+                                                           const i64* __restrict__ bstart, u64* __restrict__ pkey,
+                                                           VT* __restrict__ pval, int* __restrict__ prow,
+                                                           const AggMeta* meta) {
+  if (!take_part(meta)) return;
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  unsigned* c = reinterpret_cast<unsigned*>(lds_raw);
+  const int P = 1 << pbits;
+  for (int b = threadIdx.x; b < P; b += blockDim.x) c[b] = 0;
+  __syncthreads();
+  const i64 r0 = (i64)blockIdx.x * rpw, r1 = std::min<i64>(n, r0 + rpw);
+  for (i64 i = r0 + threadIdx.x; i < r1; i += blockDim.x) {
+    const u64 k = keys[i];
+    const int b = bucket_of(k, pbits);
+    const i64 pos = bstart[b] + hist[(size_t)b * gridDim.x + blockIdx.x] + atomicAdd(c + b, 1u);
+    pkey[pos] = k;
+    for (int f = 0; f < F; ++f) pval[pos * F + f] = vals[i * F + f];
+    prow[pos] = (int)i;
+  }
+}
+
+template <typename VT, int OP>
+__global__ __launch_bounds__(256) void agg_part_kernel(const u64* __restrict__ pkey, const VT* __restrict__ pval,
+                                                       const int* __restrict__ prow, int F, int lcap, int P, i64 ch,
+                                                       const i64* __restrict__ bstart, const i64* __restrict__ wstart,
+                                                       GTable g, AggMeta* meta, AggOut o) {
+  if (!take_part(meta)) return;
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  LTable t = ltable_at(lds_raw, lcap, F);
+  __shared__ i64 w_sh;
+  __shared__ int nocc;
+  __shared__ i64 base_sh;
+  const i64 nwork = meta->nwork;
+  for (;;) {
+    if (threadIdx.x == 0) w_sh = __hip_atomic_fetch_add(&meta->wnext, (i64)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ltable_clear<VT, OP>(t, F);
+    if (threadIdx.x == 0) nocc = 0;
+    __syncthreads();
+    const i64 w = w_sh;
+    if (w >= nwork) return;   // every workgroup reaches this once the list is drained
+    // bucket of work item w: last b with wstart[b] <= w
+    int lo = 0, hi = P - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (wstart[mid] <= w) lo = mid;
+      else hi = mid - 1;
+    }
+    const int b = lo;
+    const i64 chunks = wstart[b + 1] - wstart[b];
+    const i64 r0 = bstart[b] + (w - wstart[b]) * ch, r1 = std::min(bstart[b + 1], r0 + ch);
+    for (i64 r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
+      const u64 k = pkey[r];
+      const VT* v = pval + r * F;
+      int s = -1;
+      if (k != kEmpty) s = ltable_slot(t, k, mix64(k));
+      const int row = prow[r];
+      if (s >= 0) {
+        for (int f = 0; f < F; ++f) acc_add<VT, OP, __HIP_MEMORY_SCOPE_WORKGROUP>(t.acc + s * F + f, v[f]);
+        __hip_atomic_fetch_add(t.cnt + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_min(t.rmin + s, (u64)row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else {
+        row_into_global<VT, OP>(g, k, v, F, &meta->ng_part, &meta->sentinel_part, &meta->fail_part, o, row);
+      }
+    }
+    __syncthreads();
+    if (chunks == 1) {
+      // the bucket is this chunk: its groups occur nowhere else -> dense output directly
+      for (int e = threadIdx.x; e < lcap; e += blockDim.x)
+        if (t.key[e] != kEmpty) t.ref[e] = atomicAdd(&nocc, 1);   // local id (any order)
+      __syncthreads();
+      if (threadIdx.x == 0) base_sh = __hip_atomic_fetch_add(&meta->ng_part, (i64)nocc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const i64 base = base_sh;
+      for (int e = threadIdx.x; e < lcap; e += blockDim.x) {
+        const u64 k = t.key[e];
+        if (k == kEmpty) continue;
+        const i64 gid = base + t.ref[e];
+        t.ref[e] = gid;
+        o.reps[gid] = (i64)k;
+        o.cnt[gid] = (i64)t.cnt[e];
+        o.first[gid] = (i64)t.rmin[e];
+        o.slot_of_gid[gid] = -1;
+        for (int f = 0; f < F; ++f) o.aggs[gid * F + f] = acc_out<VT, OP>(t.acc[e * F + f]);
+      }
+    } else {
+      for (int e = threadIdx.x; e < lcap; e += blockDim.x) {
+        const u64 k = t.key[e];
+        if (k == kEmpty) continue;
+        const i64 s = gtable_slot(g, k, &meta->ng_part, &meta->sentinel_part, &meta->fail_part, o);
+        t.ref[e] = -(s + 1);
+        if (s < 0) continue;
+        for (int f = 0; f < F; ++f) acc_merge_global<VT, OP>(g.acc + s * F + f, t.acc[e * F + f]);
+        __hip_atomic_fetch_add(g.cnt + s, (u64)t.cnt[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_min(g.rmin + s, t.rmin[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (o.inv != nullptr) {
+      __syncthreads();
+      for (i64 r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
+        const u64 k = pkey[r];
+        if (k == kEmpty) continue;
+        const int s = ltable_find(t, k, mix64(k));
+        if (s >= 0) o.inv[prow[r]] = t.ref[s];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// global-table groups -> dense output (grid-stride over the groups of the path that was taken)
+template <typename VT, int OP>
+__global__ __launch_bounds__(256) void agg_emit_kernel(GTable glow, GTable gpart, int F, const AggMeta* meta,
+                                                       AggOut o) {
+  const bool low = !take_part(meta);
+  const GTable g = low ? glow : gpart;
+  const i64 ng = low ? meta->ng_low : meta->ng_part;
+  for (i64 gid = (i64)blockIdx.x * blockDim.x + threadIdx.x; gid < ng; gid += (i64)gridDim.x * blockDim.x) {
+    const i64 s = o.slot_of_gid[gid];
+    if (s < 0) continue;
+    o.cnt[gid] = (i64)g.cnt[s];
+    o.first[gid] = (i64)g.rmin[s];
+    for (int f = 0; f < F; ++f) o.aggs[gid * F + f] = acc_out<VT, OP>(g.acc[s * F + f]);
+  }
+}
+
+// per-row global-slot references (-(slot + 1)) -> dense group ids
+__global__ __launch_bounds__(256) void agg_fix_inv_kernel(i64* __restrict__ inv, i64 n, const i64* __restrict__ gid_low,
+                                                          const i64* __restrict__ gid_part, const AggMeta* meta) {
+  const i64* gos = take_part(meta) ? gid_part : gid_low;
+  for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) {
+    const i64 v = inv[i];
+    if (v < 0) inv[i] = gos[-v - 1];
+  }
+}
+
+// ---------------------------------------------------------------- hash join
+// build: tkey[cap + 1] preset kEmpty, tcnt[cap + 1] preset 0; row_slot / row_rank per build row
+__global__ __launch_bounds__(256) void join_insert_kernel(const u64* __restrict__ keys, i64 n, u64* tkey,
+                                                          unsigned* tcnt, u64 mask, int* __restrict__ row_slot,
+                                                          unsigned* __restrict__ row_rank) {
+  for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) {
+    const u64 k = keys[i];
+    u64 s;
+    if (k == kEmpty) {
+      s = mask + 1;
+    } else {
+      s = mix64(k) & mask;
+      for (;;) {   // the table has >= 2 slots per build row: the key or an empty slot is always met
+        u64 cur = __hip_atomic_load(tkey + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == kEmpty) {
+          if (__hip_atomic_compare_exchange_strong(tkey + s, &cur, k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT))
+            break;
+        }
+        if (cur == k) break;
+        s = (s + 1) & mask;
+      }
+    }
+    row_slot[i] = (int)s;
+    row_rank[i] = __hip_atomic_fetch_add(tcnt + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// perm[toff[slot] + rank] = row: build rows grouped by key (CSR over the slots)
+__global__ __launch_bounds__(256) void join_perm_kernel(const int* __restrict__ row_slot,
+                                                        const unsigned* __restrict__ row_rank, i64 n,
+                                                        const i64* __restrict__ toff, i64* __restrict__ perm) {
+  for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x)
+    perm[toff[row_slot[i]] + row_rank[i]] = i;
+}
+
+// probe: matches per probe row (cnt) and the slot they sit in
+__global__ __launch_bounds__(256) void join_probe_kernel(const u64* __restrict__ keys, i64 m, const u64* __restrict__ tkey,
+                                                         const unsigned* __restrict__ tcnt, u64 mask,
+                                                         i64* __restrict__ cnt, int* __restrict__ slot) {
+  for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (i64)gridDim.x * blockDim.x) {
+    const u64 k = keys[i];
+    i64 c = 0;
+    int sl = -1;
+    if (k == kEmpty) {
+      sl = (int)(mask + 1);
+      c = tcnt[sl];
+    } else {
+      u64 s = mix64(k) & mask;
+      for (;;) {
+        const u64 cur = tkey[s];
+        if (cur == k) {
+          sl = (int)s;
+          c = tcnt[s];
+          break;
+        }
+        if (cur == kEmpty) break;
+        s = (s + 1) & mask;
+      }
+    }
+    cnt[i] = c;
+    slot[i] = sl;
+  }
+}
+
+// expand: probe row i owns output rows [ooff[i] - cnt[i], ooff[i]) (ooff = inclusive scan of cnt)
+__global__ __launch_bounds__(256) void join_expand_kernel(const i64* __restrict__ cnt, const i64* __restrict__ ooff,
+                                                          const int* __restrict__ slot, i64 m,
+                                                          const i64* __restrict__ toff, const i64* __restrict__ perm,
+                                                          i64* __restrict__ bidx, i64* __restrict__ pidx) {
+  for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (i64)gridDim.x * blockDim.x) {
+    const i64 c = cnt[i];
+    if (c == 0) continue;
+    const i64 o = ooff[i] - c, b0 = toff[slot[i]];
+    for (i64 j = 0; j < c; ++j) {
+      bidx[o + j] = perm[b0 + j];
+      pidx[o + j] = i;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- partition + pack (shuffle sink)
+// dest[i] in [0, P): per-workgroup histograms (bucket-major), then a stable-within-chunk scatter of row ids
+__global__ __launch_bounds__(1024) void part_hist_kernel(const i64* __restrict__ dest, i64 n, i64 rpw, int P,
+                                                         unsigned* __restrict__ hist) {
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  unsigned* h = reinterpret_cast<unsigned*>(lds_raw);
+  for (int i = threadIdx.x; i < P; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  const i64 r0 = (i64)blockIdx.x * rpw, r1 = std::min<i64>(n, r0 + rpw);
+  for (i64 i = r0 + threadIdx.x; i < r1; i += blockDim.x) atomicAdd(h + dest[i], 1u);
+  __syncthreads();
+  for (int b = threadIdx.x; b < P; b += blockDim.x) hist[(size_t)b * gridDim.x + blockIdx.x] = h[b];
+}
+
+// Rows are placed in input order within each destination: the chunk is walked in 1024-row tiles; inside a tile
+// each wave ranks its lanes per destination with ballots (lanes of one destination, in lane order), the waves'
+// counts are prefix-summed in LDS, and a running per-destination base carries over to the next tile.
+__global__ __launch_bounds__(1024) void part_scatter_kernel(const i64* __restrict__ dest, i64 n, i64 rpw, int P,
+                                                            const unsigned* __restrict__ hist,
+                                                            const i64* __restrict__ bstart, i64* __restrict__ perm) {
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  unsigned* base = reinterpret_cast<unsigned*>(lds_raw);   // [P] running base within this chunk
+  unsigned* wc = base + P;                                  // [16][P] per-wave counts of the current tile
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int b = threadIdx.x; b < P; b += blockDim.x) base[b] = 0;
+  const i64 r0 = (i64)blockIdx.x * rpw, r1 = std::min<i64>(n, r0 + rpw);
+  for (i64 t0 = r0; t0 < r1; t0 += 1024) {
+    for (int j = threadIdx.x; j < 16 * P; j += blockDim.x) wc[j] = 0;
+    __syncthreads();
+    const i64 i = t0 + threadIdx.x;
+    const bool valid = i < r1;
+    const int d = valid ? (int)dest[i] : -1;
+    // rank among this wave's lanes of the same destination
+    u64 todo = __ballot(valid);
+    int rank = 0;
+    while (todo) {
+      const int leader = __ffsll((long long)todo) - 1;
+      const int dl = __shfl(d, leader, 64);
+      const u64 m = __ballot(valid && d == dl);
+      if (d == dl && valid) rank = __popcll(m & ((1ull << lane) - 1));
+      if (lane == leader) wc[wave * P + dl] = __popcll(m);
+      todo &= ~m;
+    }
+    __syncthreads();
+    if (valid) {
+      unsigned before = 0;
+      for (int w = 0; w < wave; ++w) before += wc[w * P + d];
+      perm[bstart[d] + hist[(size_t)d * gridDim.x + blockIdx.x] + base[d] + before + rank] = i;
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < P; b += blockDim.x) {
+      unsigned s = 0;
+      for (int w = 0; w < 16; ++w) s += wc[w * P + b];
+      base[b] += s;
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------- host launchers
+template <typename VT, int OP>
+int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv, void* meta_v, void* glow_v,
+                 i64 gcap_low, void* gpart_v, i64 gcap_part, void* out_v, void* work_v, int pbits, int lcap_low,
+                 int lcap_part, int low_thr, hipStream_t st) {
+  AggMeta* meta = reinterpret_cast<AggMeta*>(meta_v);
+  // glow / gpart: [key (cap+1) | acc (cap+1)*F | cnt (cap+1) | gid (cap+1)] u64 words, preset by the caller
+  auto mk = [&](void* base, i64 cap) {
+    GTable t;
+    u64* p = reinterpret_cast<u64*>(base);
+    t.key = p;
+    t.acc = p + (cap + 1);
+    t.cnt = t.acc + (cap + 1) * F;
+    t.rmin = t.cnt + (cap + 1);
+    t.gid_of_slot = reinterpret_cast<i64*>(t.rmin + (cap + 1));
+    t.mask = (u64)(cap - 1);
+    return t;
+  };
+  const GTable glow = mk(glow_v, gcap_low), gpart = mk(gpart_v, gcap_part);
+  i64* ob = reinterpret_cast<i64*>(out_v);   // [reps n | aggs n*F | cnt n | slot_of_gid n | first n | inv n]
+  AggOut o;
+  o.reps = ob;
+  o.aggs = reinterpret_cast<u64*>(ob + n);
+  o.cnt = ob + n + n * F;
+  o.slot_of_gid = o.cnt + n;
+  o.first = o.slot_of_gid + n;
+  o.inv = want_inv ? o.first + n : nullptr;
+  const u64* k = reinterpret_cast<const u64*>(keys);
+  const VT* v = reinterpret_cast<const VT*>(vals);
+  const size_t lbytes_low = (size_t)lcap_low * (28 + 8 * F);
+  const size_t lbytes_part = (size_t)lcap_part * (28 + 8 * F);
+
+  hipLaunchKernelGGL(agg_init_kernel, dim3(512), dim3(256), 0, st, reinterpret_cast<u64*>(glow_v), gcap_low,
+                     reinterpret_cast<u64*>(gpart_v), gcap_part, F, acc_identity<VT, OP>(), meta);
+  hipLaunchKernelGGL(agg_sample_kernel, dim3(1), dim3(1024), 0, st, k, n, low_thr, meta);
+  const int gl = (int)std::min<i64>(1024, std::max<i64>(1, (n + 2047) / 2048));
+  hipLaunchKernelGGL((agg_low_kernel<VT, OP>), dim3(gl), dim3(256), lbytes_low, st, k, v, n, F, lcap_low, glow, meta, o);
+  // PART: work buffers [hist P*G u32 | tot P | bstart P+1 | wstart P+1 | pkey n | pval n*F | prow n (i32)]
+  const int P = 1 << pbits;
+  const int G = (int)std::min<i64>(256, std::max<i64>(1, (n + 16383) / 16384));
+  const i64 rpw = (n + G - 1) / G;
+  char* w = reinterpret_cast<char*>(work_v);
+  unsigned* hist = reinterpret_cast<unsigned*>(w);
+  i64* tot = reinterpret_cast<i64*>(w + (((size_t)P * G * 4 + 15) & ~(size_t)15));
+  i64* bstart = tot + P;
+  i64* wstart = bstart + P + 1;
+  u64* pkey = reinterpret_cast<u64*>(wstart + P + 1);
+  VT* pval = reinterpret_cast<VT*>(pkey + n);
+  int* prow = reinterpret_cast<int*>(pval + n * F);
+  const i64 ch = (3 * (i64)lcap_part) / 4;   // rows per work item: the LDS table stays <= 3/4 full
+  hipLaunchKernelGGL(agg_hist_kernel, dim3(G), dim3(1024), (size_t)P * 4, st, k, n, rpw, pbits, hist, meta);
+  hipLaunchKernelGGL(scan_rows_kernel, dim3(P), dim3(256), 0, st, hist, G, tot, meta, 1);
+  hipLaunchKernelGGL(scan_tot_kernel, dim3(1), dim3(1024), 0, st, tot, P, ch, bstart, wstart, meta, 1);
+  hipLaunchKernelGGL((agg_scatter_kernel<VT>), dim3(G), dim3(1024), (size_t)P * 4, st, k, v, n, F, rpw, pbits, hist,
+                     bstart, pkey, pval, prow, meta);
+  hipLaunchKernelGGL((agg_part_kernel<VT, OP>), dim3(1024), dim3(256), lbytes_part, st, pkey, pval, prow, F, lcap_part,
+                     P, ch, bstart, wstart, gpart, meta, o);
+  hipLaunchKernelGGL((agg_emit_kernel<VT, OP>), dim3(512), dim3(256), 0, st, glow, gpart, F, meta, o);
+  if (want_inv)
+    hipLaunchKernelGGL(agg_fix_inv_kernel, dim3((unsigned)std::min<i64>(2048, (n + 255) / 256)), dim3(256), 0, st,
+                       o.inv, n, glow.gid_of_slot, gpart.gid_of_slot, meta);
+  return (int)hipGetLastError();
+}
+
+}  // namespace nsdb_rel
+
+using namespace nsdb_rel;
+
+extern "C" {
+
+// Byte size of the PART work buffer for (n, F, pbits).
+long long nsdb_agg_work_bytes(long long n, int F, int pbits, int want_inv) {
+  const long long P = 1LL << pbits;
+  const long long G = std::min<long long>(256, std::max<long long>(1, (n + 16383) / 16384));
+  (void)want_inv;
+  return ((P * G * 4 + 15) & ~15LL) + 8 * (P + 2 * (P + 1)) + 8 * n + 8 * n * F + 4 * n + 64;
+}
+
+// vt: 0 double, 1 int64; op: 0 sum, 1 min, 2 max
+int nsdb_hash_aggregate(const void* keys, const void* vals, long long n, int F, int vt, int op, int want_inv,
+                        void* meta, void* glow, long long gcap_low, void* gpart, long long gcap_part, void* out,
+                        void* work, int pbits, int lcap_low, int lcap_part, int low_thr, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (n >= (1LL << 31)) return (int)hipErrorInvalidValue;
+  if (F < 0 || F > 16 || pbits < 0 || pbits > 14) return (int)hipErrorInvalidValue;
+  auto pow2 = [](long long x) { return x > 0 && (x & (x - 1)) == 0; };
+  if (!pow2(gcap_low) || !pow2(gcap_part) || !pow2(lcap_low) || !pow2(lcap_part)) return (int)hipErrorInvalidValue;
+  if ((size_t)lcap_low * (28 + 8 * F) > 65536 || (size_t)lcap_part * (28 + 8 * F) > 131072) return (int)hipErrorInvalidValue;
+#define NSDB_AGG(VT, OP) agg_launch_t<VT, OP>(keys, vals, n, F, want_inv, meta, glow, gcap_low, gpart, gcap_part, out, work, pbits, lcap_low, lcap_part, low_thr, st)
+  if (vt == 0) {
+    if (op == 0) return NSDB_AGG(double, OP_SUM);
+    if (op == 1) return NSDB_AGG(double, OP_MIN);
+    if (op == 2) return NSDB_AGG(double, OP_MAX);
+  } else if (vt == 1) {
+    if (op == 0) return NSDB_AGG(i64, OP_SUM);
+    if (op == 1) return NSDB_AGG(i64, OP_MIN);
+    if (op == 2) return NSDB_AGG(i64, OP_MAX);
+  }
+#undef NSDB_AGG
+  return (int)hipErrorInvalidValue;
+}
+
+// Join build over n int64 keys: tkey [cap + 1] preset kEmpty, tcnt [cap + 1] preset 0 (cap a power of two >= 2n).
+int nsdb_join_insert(const void* keys, long long n, void* tkey, unsigned* tcnt, long long cap, int* row_slot,
+                     unsigned* row_rank, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (cap <= 0 || (cap & (cap - 1)) != 0 || cap < 2 * n || cap >= (1LL << 31)) return (int)hipErrorInvalidValue;
+  const unsigned g = (unsigned)std::min<long long>(4096, (n + 255) / 256);
+  hipLaunchKernelGGL(join_insert_kernel, dim3(g), dim3(256), 0, st, (const u64*)keys, n, (u64*)tkey, tcnt,
+                     (u64)(cap - 1), row_slot, row_rank);
+  return (int)hipGetLastError();
+}
+
+int nsdb_join_perm(const int* row_slot, const unsigned* row_rank, long long n, const long long* toff, long long* perm,
+                   hipStream_t st) {
+  if (n <= 0) return 0;
+  const unsigned g = (unsigned)std::min<long long>(4096, (n + 255) / 256);
+  hipLaunchKernelGGL(join_perm_kernel, dim3(g), dim3(256), 0, st, row_slot, row_rank, n, toff, perm);
+  return (int)hipGetLastError();
+}
+
+int nsdb_join_probe(const void* keys, long long m, const void* tkey, const unsigned* tcnt, long long cap,
+                    long long* cnt, int* slot, hipStream_t st) {
+  if (m <= 0) return 0;
+  if (cap <= 0 || (cap & (cap - 1)) != 0) return (int)hipErrorInvalidValue;
+  const unsigned g = (unsigned)std::min<long long>(4096, (m + 255) / 256);
+  hipLaunchKernelGGL(join_probe_kernel, dim3(g), dim3(256), 0, st, (const u64*)keys, m, (const u64*)tkey, tcnt,
+                     (u64)(cap - 1), cnt, slot);
+  return (int)hipGetLastError();
+}
+
+int nsdb_join_expand(const long long* cnt, const long long* ooff, const int* slot, long long m, const long long* toff,
+                     const long long* perm, long long* bidx, long long* pidx, hipStream_t st) {
+  if (m <= 0) return 0;
+  const unsigned g = (unsigned)std::min<long long>(4096, (m + 255) / 256);
+  hipLaunchKernelGGL(join_expand_kernel, dim3(g), dim3(256), 0, st, cnt, ooff, slot, m, toff, perm, bidx, pidx);
+  return (int)hipGetLastError();
+}
+
+// Stable partition permutation: dest [n] in [0, P), P <= 2048. work: hist P*G u32 + tot P i64 + bstart P+1 i64.
+long long nsdb_part_work_bytes(long long n, int P) {
+  const long long G = std::min<long long>(256, std::max<long long>(1, (n + 16383) / 16384));
+  return ((P * G * 4 + 15) & ~15LL) + 8 * (2 * P + 1) + 64;
+}
+
+int nsdb_partition_perm(const long long* dest, long long n, int P, void* work, long long* perm, long long* counts,
+                        hipStream_t st) {
+  if (n <= 0) return 0;
+  if (P <= 0 || P > 2048 || n >= (1LL << 31)) return (int)hipErrorInvalidValue;
+  const int G = (int)std::min<long long>(256, std::max<long long>(1, (n + 16383) / 16384));
+  const long long rpw = (n + G - 1) / G;
+  const size_t lds = (size_t)P * 4 * 17;
+  if (lds > 163840) return (int)hipErrorInvalidValue;
+  char* w = reinterpret_cast<char*>(work);
+  unsigned* hist = reinterpret_cast<unsigned*>(w);
+  long long* tot = reinterpret_cast<long long*>(w + (((size_t)P * G * 4 + 15) & ~(size_t)15));
+  long long* bstart = tot + P;
+  hipLaunchKernelGGL(part_hist_kernel, dim3(G), dim3(1024), (size_t)P * 4, st, dest, n, rpw, P, hist);
+  hipLaunchKernelGGL(scan_rows_kernel, dim3(P), dim3(256), 0, st, hist, G, tot, (const AggMeta*)nullptr, 0);
+  hipLaunchKernelGGL(scan_tot_kernel, dim3(1), dim3(1024), 0, st, tot, P, (long long)1, bstart, (long long*)nullptr,
+                     (AggMeta*)nullptr, 0);
+  hipLaunchKernelGGL(part_scatter_kernel, dim3(G), dim3(1024), lds, st, dest, n, rpw, P, hist, bstart, perm);
+  if (counts) (void)hipMemcpyAsync(counts, tot, sizeof(long long) * P, hipMemcpyDeviceToDevice, st);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,224 @@
+// PyTorch bindings of the device relational operators (relops.hip): hash aggregation, hash join build /
+// probe, and the stable partition permutation of the shuffle sink. Every entry checks device / dtype / shape
+// on the host before anything is launched, and launches on the current HIP stream.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+#include <limits>
+#include <string>
+#include <tuple>
+#include <vector>
+
+typedef long long ll;
+template <typename T> ll* LL(T* p) { return reinterpret_cast<ll*>(p); }
+
+extern "C" {
+long long nsdb_agg_work_bytes(long long n, int F, int pbits, int want_inv);
+int nsdb_hash_aggregate(const void* keys, const void* vals, long long n, int F, int vt, int op, int want_inv,
+                        void* meta, void* glow, long long gcap_low, void* gpart, long long gcap_part, void* out,
+                        void* work, int pbits, int lcap_low, int lcap_part, int low_thr, hipStream_t st);
+int nsdb_join_insert(const void* keys, long long n, void* tkey, unsigned* tcnt, long long cap, int* row_slot,
+                     unsigned* row_rank, hipStream_t st);
+int nsdb_join_perm(const int* row_slot, const unsigned* row_rank, long long n, const long long* toff, long long* perm,
+                   hipStream_t st);
+int nsdb_join_probe(const void* keys, long long m, const void* tkey, const unsigned* tcnt, long long cap,
+                    long long* cnt, int* slot, hipStream_t st);
+int nsdb_join_expand(const long long* cnt, const long long* ooff, const int* slot, long long m, const long long* toff,
+                     const long long* perm, long long* bidx, long long* pidx, hipStream_t st);
+long long nsdb_part_work_bytes(long long n, int P);
+int nsdb_partition_perm(const long long* dest, long long n, int P, void* work, long long* perm, long long* counts,
+                        hipStream_t st);
+}
+
+namespace {
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void rc_ok(int rc, const char* what) {
+  TORCH_CHECK(rc == 0, what, " failed with code ", rc, " (", hipGetErrorString((hipError_t)(rc > 0 ? rc : 0)), ")");
+}
+
+int64_t pow2_at_least(int64_t x) {
+  int64_t c = 1;
+  while (c < x) c <<= 1;
+  return c;
+}
+int64_t pow2_at_most(int64_t x) {
+  int64_t c = 1;
+  while (c * 2 <= x) c <<= 1;
+  return c;
+}
+
+// Word offsets of the AggMeta fields (relops.hip): est, low, ng_low, ng_part, fail_low, fail_part, ...
+constexpr int kMetaWords = 16;
+
+// Group n int64 keys and reduce F value columns per group on the device.
+//   vals: [n, F] float64 or int64 (or None / F == 0: counts only); op: "sum" | "min" | "max".
+// Returns (reps [g] i64, aggs [g, F] (vals dtype), counts [g] i64, first [g] i64 (smallest row of each group),
+// inv [n] i64 (or empty), status): status = [g, path (0 LOW, 1 PART), ok (0: the PART table overflowed; outputs
+// invalid, fall back), distinct keys in the 4096-row sample].
+std::vector<torch::Tensor> hash_aggregate(torch::Tensor keys, c10::optional<torch::Tensor> vals, const std::string& op,
+                                          bool want_inv, int64_t low_threshold) {
+  TORCH_CHECK(keys.is_cuda(), "keys must be a GPU tensor");
+  TORCH_CHECK(keys.scalar_type() == torch::kInt64 && keys.dim() == 1, "keys must be 1-D int64");
+  keys = keys.contiguous();
+  const int64_t n = keys.numel();
+  TORCH_CHECK(n < (int64_t(1) << 31), "hash_aggregate: at most 2^31 - 1 rows per call");
+  int opc = op == "sum" ? 0 : op == "min" ? 1 : op == "max" ? 2 : -1;
+  TORCH_CHECK(opc >= 0, "op must be sum, min or max");
+  int F = 0, vt = 0;
+  torch::Tensor v;
+  auto vdtype = torch::kFloat64;
+  if (vals.has_value() && vals->defined() && vals->numel() > 0) {
+    v = *vals;
+    TORCH_CHECK(v.is_cuda() && v.device() == keys.device(), "vals must be on the keys' device");
+    TORCH_CHECK(v.scalar_type() == torch::kFloat64 || v.scalar_type() == torch::kInt64, "vals must be float64 or int64");
+    if (v.dim() == 1) v = v.unsqueeze(1);
+    TORCH_CHECK(v.dim() == 2 && v.size(0) == n, "vals must be [n] or [n, F]");
+    v = v.contiguous();
+    F = (int)v.size(1);
+    TORCH_CHECK(F <= 16, "at most 16 value columns");
+    vt = v.scalar_type() == torch::kInt64 ? 1 : 0;
+    vdtype = v.scalar_type();
+  }
+  auto i64 = keys.options().dtype(torch::kInt64);
+  if (n == 0) {
+    return {torch::empty({0}, i64), torch::empty({0, F}, keys.options().dtype(vdtype)), torch::empty({0}, i64),
+            torch::empty({0}, i64), torch::empty({0}, i64), torch::tensor({0, 0, 1, 0}, torch::kInt64)};
+  }
+  // LDS tables: LOW <= 64 KiB (two workgroups per CU), PART <= 128 KiB; buckets average <= ch / 2 rows (hash
+  // partitions are tightly binomial, so nearly every bucket is a single work item)
+  const int64_t entry = 28 + 8 * F;
+  const int64_t lcap_low = std::min<int64_t>(2048, pow2_at_most(65536 / entry));
+  const int64_t lcap_part = std::min<int64_t>(4096, pow2_at_most(131072 / entry));
+  const int64_t ch = (3 * lcap_part) / 4;   // rows per PART work item (relops.hip agg_launch_t)
+  int64_t P = std::min<int64_t>(16384, pow2_at_least(std::max<int64_t>(1, (2 * n + ch - 1) / ch)));
+  int pbits = 0;
+  while ((int64_t(1) << pbits) < P) ++pbits;
+  const int64_t gcap_low = 4 * lcap_low;
+  const int64_t gcap_part = std::max<int64_t>(4096, std::min<int64_t>(pow2_at_least(2 * n), int64_t(1) << 20));
+  const int64_t thr = low_threshold > 0 ? low_threshold : lcap_low / 4;
+
+  auto meta = torch::empty({kMetaWords}, i64);
+  auto glow = torch::empty({(gcap_low + 1) * (4 + F)}, i64);
+  auto gpart = torch::empty({(gcap_part + 1) * (4 + F)}, i64);
+  auto out = torch::empty({n * (5 + F) + (want_inv ? n : 0)}, i64);
+  const int64_t wbytes = nsdb_agg_work_bytes(n, F, pbits, want_inv ? 1 : 0);
+  auto work = torch::empty({(wbytes + 7) / 8}, i64);
+  rc_ok(nsdb_hash_aggregate(keys.data_ptr(), F ? v.data_ptr() : nullptr, n, F, vt, opc, want_inv ? 1 : 0,
+                            meta.data_ptr(), glow.data_ptr(), gcap_low, gpart.data_ptr(), gcap_part, out.data_ptr(),
+                            work.data_ptr(), pbits, (int)lcap_low, (int)lcap_part, (int)thr, stream()),
+        "hash_aggregate");
+  auto m = meta.cpu();   // the one host read: group count and path flags
+  const ll* mp = LL(m.data_ptr<int64_t>());
+  const bool low_ok = mp[1] != 0 && mp[4] == 0;
+  const int64_t g = (int64_t)(low_ok ? mp[2] : mp[3]);
+  const bool ok = low_ok || mp[5] == 0;
+  auto status = torch::tensor({(int64_t)g, (int64_t)(low_ok ? 0 : 1), (int64_t)(ok ? 1 : 0), (int64_t)mp[0]}, torch::kInt64);
+  if (!ok) return {torch::Tensor(), torch::Tensor(), torch::Tensor(), torch::Tensor(), torch::Tensor(), status};
+  auto reps = out.narrow(0, 0, g);
+  auto aggs = out.narrow(0, n, g * F).view({g, F});
+  if (vt == 0) aggs = aggs.view(torch::kFloat64);
+  auto cnt = out.narrow(0, n + n * F, g);
+  auto first = out.narrow(0, n * (4 + F), g);
+  torch::Tensor inv = want_inv ? out.narrow(0, n * (5 + F), n) : torch::empty({0}, i64);
+  // the views keep the whole n-row buffer alive: copy small results out of it
+  if (g * 4 < n) {
+    reps = reps.clone();
+    aggs = aggs.clone();
+    cnt = cnt.clone();
+    first = first.clone();
+  }
+  return {reps, aggs, cnt, first, inv, status};
+}
+
+// Join build: returns (tkey [cap+1] i64, tcnt [cap+1] i32, toff [cap+1] i64 (exclusive offsets), perm [n] i64).
+std::vector<torch::Tensor> join_build(torch::Tensor keys) {
+  TORCH_CHECK(keys.is_cuda() && keys.scalar_type() == torch::kInt64 && keys.dim() == 1, "keys: 1-D int64 GPU tensor");
+  keys = keys.contiguous();
+  const int64_t n = keys.numel();
+  TORCH_CHECK(n < (int64_t(1) << 29), "join_build: at most 2^29 build rows per table");
+  const int64_t cap = pow2_at_least(std::max<int64_t>(1024, 2 * n));
+  auto i64 = keys.options().dtype(torch::kInt64);
+  auto tkey = torch::full({cap + 1}, std::numeric_limits<int64_t>::min(), i64);
+  auto tcnt = torch::zeros({cap + 1}, keys.options().dtype(torch::kInt32));
+  auto row_slot = torch::empty({n}, keys.options().dtype(torch::kInt32));
+  auto row_rank = torch::empty({n}, keys.options().dtype(torch::kInt32));
+  rc_ok(nsdb_join_insert(keys.data_ptr(), n, tkey.data_ptr(), reinterpret_cast<unsigned*>(tcnt.data_ptr<int>()), cap,
+                         row_slot.data_ptr<int>(), reinterpret_cast<unsigned*>(row_rank.data_ptr<int>()), stream()),
+        "join_insert");
+  auto toff = torch::cumsum(tcnt, 0, torch::kInt64).sub_(tcnt);
+  auto perm = torch::empty({n}, i64);
+  rc_ok(nsdb_join_perm(row_slot.data_ptr<int>(), reinterpret_cast<const unsigned*>(row_rank.data_ptr<int>()), n,
+                       LL(toff.data_ptr<int64_t>()), LL(perm.data_ptr<int64_t>()), stream()),
+        "join_perm");
+  return {tkey, tcnt, toff, perm};
+}
+
+// Probe a built table with m int64 keys: all (build row, probe row) pairs with equal keys, probe-major.
+std::vector<torch::Tensor> join_probe(torch::Tensor tkey, torch::Tensor tcnt, torch::Tensor toff, torch::Tensor perm,
+                                      torch::Tensor keys) {
+  TORCH_CHECK(keys.is_cuda() && keys.scalar_type() == torch::kInt64 && keys.dim() == 1, "keys: 1-D int64 GPU tensor");
+  TORCH_CHECK(tkey.is_cuda() && tkey.scalar_type() == torch::kInt64 && tcnt.scalar_type() == torch::kInt32 &&
+                  toff.scalar_type() == torch::kInt64 && perm.scalar_type() == torch::kInt64,
+              "join table tensors (from join_build) expected");
+  const int64_t cap = tkey.numel() - 1;
+  TORCH_CHECK(cap >= 1024 && (cap & (cap - 1)) == 0 && tcnt.numel() == cap + 1 && toff.numel() == cap + 1,
+              "malformed join table");
+  TORCH_CHECK(keys.device() == tkey.device(), "probe keys must be on the table's device");
+  keys = keys.contiguous();
+  const int64_t m = keys.numel();
+  auto i64 = keys.options().dtype(torch::kInt64);
+  if (m == 0 || perm.numel() == 0) return {torch::empty({0}, i64), torch::empty({0}, i64)};
+  auto cnt = torch::empty({m}, i64);
+  auto slot = torch::empty({m}, keys.options().dtype(torch::kInt32));
+  rc_ok(nsdb_join_probe(keys.data_ptr(), m, tkey.data_ptr(), reinterpret_cast<const unsigned*>(tcnt.data_ptr<int>()),
+                        cap, LL(cnt.data_ptr<int64_t>()), slot.data_ptr<int>(), stream()),
+        "join_probe");
+  auto ooff = torch::cumsum(cnt, 0);
+  const int64_t total = ooff[m - 1].item<int64_t>();   // sizes the output (one host read)
+  auto bidx = torch::empty({total}, i64);
+  auto pidx = torch::empty({total}, i64);
+  if (total > 0)
+    rc_ok(nsdb_join_expand(LL(cnt.data_ptr<int64_t>()), LL(ooff.data_ptr<int64_t>()), slot.data_ptr<int>(), m,
+                           LL(toff.data_ptr<int64_t>()), LL(perm.data_ptr<int64_t>()), LL(bidx.data_ptr<int64_t>()),
+                           LL(pidx.data_ptr<int64_t>()), stream()),
+          "join_expand");
+  return {bidx, pidx};
+}
+
+// Stable partition permutation of dest (values in [0, P)): rows of partition 0 first (input order), then 1, ...
+std::vector<torch::Tensor> partition_perm(torch::Tensor dest, int64_t P) {
+  TORCH_CHECK(dest.is_cuda() && dest.scalar_type() == torch::kInt64 && dest.dim() == 1, "dest: 1-D int64 GPU tensor");
+  TORCH_CHECK(P >= 1 && P <= 2048, "partition_perm: 1 <= P <= 2048");
+  dest = dest.contiguous();
+  const int64_t n = dest.numel();
+  TORCH_CHECK(n < (int64_t(1) << 31), "partition_perm: at most 2^31 - 1 rows");
+  auto i64 = dest.options().dtype(torch::kInt64);
+  auto counts = torch::zeros({P}, i64);
+  auto perm = torch::empty({n}, i64);
+  if (n == 0) return {perm, counts};
+  auto work = torch::empty({(nsdb_part_work_bytes(n, (int)P) + 7) / 8}, i64);
+  rc_ok(nsdb_partition_perm(LL(dest.data_ptr<int64_t>()), n, (int)P, work.data_ptr(), LL(perm.data_ptr<int64_t>()),
+                            LL(counts.data_ptr<int64_t>()), stream()),
+        "partition_perm");
+  return {perm, counts};
+}
+
+}  // namespace
+
+std::vector<torch::Tensor> hash_aggregate_impl(torch::Tensor keys, c10::optional<torch::Tensor> vals,
+                                               const std::string& op, bool want_inv, int64_t low_threshold) {
+  return hash_aggregate(keys, vals, op, want_inv, low_threshold);
+}
+
+void register_relops(pybind11::module& m) {
+  m.def("hash_aggregate", &hash_aggregate,
+        "device hash group-by + aggregate: (reps, aggs, counts, first, inv, status[g, path, ok, sample_distinct])",
+        pybind11::arg("keys"), pybind11::arg("vals") = pybind11::none(), pybind11::arg("op") = "sum",
+        pybind11::arg("want_inv") = false, pybind11::arg("low_threshold") = 0);
+  m.def("join_build", &join_build, "device hash-join build: (tkey, tcnt, toff, perm)");
+  m.def("join_probe", &join_probe, "device hash-join probe: (build_idx, probe_idx)");
+  m.def("partition_perm", &partition_perm, "stable device partition permutation: (perm, counts)");
+}

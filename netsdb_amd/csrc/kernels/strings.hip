@@ -139,9 +139,34 @@ __global__ __launch_bounds__(256) void str_slice_kernel(const uint8_t* __restric
 
 inline int grid_for(int64_t n) { return (int)((n + 255) / 256); }
 
+
+// Exact equality of row pairs (a[ia[i]] == b[ib[i]]) for value-exact string keys: group-by / join / IN decide by
+// 64-bit hash first, then every row is byte-compared with its group's or match's representative
+// (reference pdb::String equality, src/objectModel/headers/PDBString.h:46-48).
+__global__ __launch_bounds__(256) void str_eq_pairs_kernel(const uint32_t* __restrict__ wa, const int64_t* __restrict__ offa,
+                                                           const int64_t* __restrict__ ia,
+                                                           const uint32_t* __restrict__ wb, const int64_t* __restrict__ offb,
+                                                           const int64_t* __restrict__ ib, int64_t m,
+                                                           uint8_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const int64_t ra = ia ? ia[i] : i, rb = ib ? ib[i] : i;
+  const int64_t sa = offa[ra], la = offa[ra + 1] - sa;
+  const int64_t sb = offb[rb], lb = offb[rb + 1] - sb;
+  bool eq = la == lb;
+  for (int64_t p = 0; eq && p < la; p += 8) {
+    uint64_t x = load8(wa, sa + p) ^ load8(wb, sb + p);
+    const int64_t rem = la - p;
+    if (rem < 8) x &= (1ull << (8 * rem)) - 1ull;
+    eq = x == 0;
+  }
+  out[i] = eq ? 1 : 0;
+}
+
 }  // namespace
 
 extern "C" {
+
 
 int nsdb_str_hash(const void* bytes, const int64_t* off, int64_t n, uint64_t* out, hipStream_t st) {
   if (n <= 0) return 0;
@@ -183,6 +208,14 @@ int nsdb_str_slice(const void* src, const int64_t* off, int64_t start, const int
   if (start < 0) return -2;
   hipLaunchKernelGGL(str_slice_kernel, dim3(grid_for(n)), dim3(256), 0, st, (const uint8_t*)src, off, start, out_off, n,
                      (uint8_t*)dst);
+  return (int)hipGetLastError();
+}
+
+int nsdb_str_eq_pairs(const void* a, const int64_t* offa, const int64_t* ia, const void* b, const int64_t* offb,
+                      const int64_t* ib, int64_t m, uint8_t* out, hipStream_t st) {
+  if (m <= 0) return 0;
+  hipLaunchKernelGGL(str_eq_pairs_kernel, dim3(grid_for(m)), dim3(256), 0, st, (const uint32_t*)a, offa, ia,
+                     (const uint32_t*)b, offb, ib, m, out);
   return (int)hipGetLastError();
 }
 

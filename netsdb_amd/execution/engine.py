@@ -68,10 +68,19 @@ def _normalize(val, n: int, device):
 
 
 class BuildTable:
+    """An in-memory join build side: its tuple set plus a hash table over the join-hash column, built on the
+    first probe and reused by every later probe batch (device table on the GPU, kernels.JoinTable)."""
+
     def __init__(self, batch: Optional[RecordBatch], hash_col: str):
         self.batch = batch
         self.hash_col = hash_col
         self.h = batch.columns[hash_col] if batch is not None and batch.n else torch.empty(0, dtype=torch.int64)
+        self._table = None
+
+    def table(self, device) -> "K.JoinTable":
+        if self._table is None:
+            self._table = K.JoinTable(self.h.to(device))
+        return self._table
 
 
 class PartitionedBuild:
@@ -477,7 +486,7 @@ class QueryEngine:
         if bt.batch is None or bt.batch.n == 0 or b.n == 0:
             bi = pi = torch.empty(0, dtype=torch.int64, device=b.device)
         else:
-            bi, pi = K.join_match(bt.h, probe_h)
+            bi, pi = bt.table(probe_h.device).probe(probe_h)
         pb = RecordBatch({c: b.columns[c] for c in (lcols if side == "left" else rcols)}, b.n).take(pi)
         if bt.batch is None:
             bb_cols = {c: [] for c in (rcols if side == "left" else lcols)}
@@ -621,17 +630,29 @@ class QueryEngine:
             # value) pairs is combined locally before it is sent (CombinedShuffleSink), the shuffle rounds leave
             # while the pipeline runs, and the receiving side merges what arrives with the out-of-core
             # (hash-partitioned) reduction
-            merge_op = "sum" if op == "count" else op
+            # 'mean' travels as (sum, count) columns and is divided after the final merge
+            mean = op == "mean"
+            local_op = "sum" if mean else op
+            merge_op = "sum" if op in ("count", "mean") else op
 
             def combiner(batch):
-                inv, reps_c, g = K.group_ids(batch.columns["k"])
                 vals = batch.columns["v"]
-                agg_c = K.segment_reduce(vals, inv, g, op if isinstance(vals, torch.Tensor) else None, combine)
+                if mean:
+                    vals = _sum_count(vals)
+                fused = K.group_reduce(batch.columns["k"], vals, local_op)
+                if fused is not None:
+                    reps_c, agg_c = fused
+                else:
+                    inv, reps_c, g = K.group_ids(batch.columns["k"])
+                    agg_c = K.segment_reduce(vals, inv, g, local_op if isinstance(vals, torch.Tensor) else None,
+                                             combine)
                 loc = RecordBatch({"k": reps_c, "v": _normalize(agg_c, len(agg_c), None)}, len(agg_c))
                 return loc, K.hash_keys(reps_c, loc.device)
 
             recv = self._stream_shuffle(kv, None, "aggregate", combine=combiner, key=lambda b: None)
             reps, agg = self._reduce_kv(recv, merge_op, combine)
+            if mean and agg is not None:
+                agg = _mean_of(agg)
         if reps is None:
             state.materialized[out_ts] = []
             return
@@ -669,10 +690,14 @@ class QueryEngine:
                     continue
                 keys = column_concat([b.columns["k"] for b in bs])
                 vals = column_concat([b.columns["v"] for b in bs])
-                inv, reps, g = K.group_ids(keys)
+                fused = K.group_reduce(keys, vals, op)   # device hash aggregation (relops.hip), or None
+                if fused is not None:
+                    reps, agg = fused
+                else:
+                    inv, reps, g = K.group_ids(keys)
+                    agg = K.segment_reduce(vals, inv, g, op if isinstance(vals, torch.Tensor) else None, combine)
                 reps_parts.append(reps)
-                agg_parts.append(K.segment_reduce(vals, inv, g, op if isinstance(vals, torch.Tensor) else None,
-                                                  combine))
+                agg_parts.append(agg)
         finally:
             if pspool is not None:
                 pspool.drop()
@@ -733,6 +758,20 @@ class QueryEngine:
                 target.add_batch(objs)
             outs.append(RecordBatch({out_col: objs}, g.n))
         state.materialized[out_ts] = outs
+
+
+def _sum_count(vals):
+    """[n, ...] numeric values -> [n, F + 1] float64 (the values, then a count column of ones)."""
+    if not isinstance(vals, torch.Tensor):
+        vals = torch.as_tensor(vals, dtype=torch.float64)
+    flat = vals.reshape(vals.shape[0], -1).double()
+    return torch.cat([flat, torch.ones(flat.shape[0], 1, dtype=torch.float64, device=flat.device)], 1)
+
+
+def _mean_of(sc):
+    """Merged (sum, count) columns -> the mean per group (1-D for a single value column)."""
+    m = sc[:, :-1] / sc[:, -1:]
+    return m.squeeze(1) if m.shape[1] == 1 else m
 
 
 class _JobState:

@@ -2,9 +2,13 @@
 
 Reference: src/queryExecution + src/lambdas/headers (HashSink, JoinTuple, JoinMap/PairArray,
 AggregationMap, FilterExecutor, FlattenExecutor, HashPartitionSink).  netsDB uses per-record
-C++ hash maps; here hashing, join matching and group-by run as whole-column tensor ops
-(sort + searchsorted joins, unique/inverse group ids, index_add segment sums) so they execute
-on the GPU for device-resident columns.
+C++ hash maps; here every operator runs over whole columns. On the GPU the hot ones are device hash
+tables (csrc/kernels/relops.hip): the join build/probe (JoinTable), the fused group-by + aggregate
+(group_reduce; group_ids for the inverse) and the partition permutation of the shuffle sink
+(partition_order). Keys are value-exact: several int columns pack into one int64 when their ranges allow,
+otherwise (and for strings) a 64-bit hash groups and every row is then compared with its group's
+representative row (strings byte by byte), so colliding keys are never merged. On the CPU the same
+operators are sort / unique / searchsorted tensor ops.
 """
 from __future__ import annotations
 
@@ -81,38 +85,241 @@ def hash_keys(c, device=None) -> torch.Tensor:
     return mix64(column_to_int64(c, device))
 
 
+class JoinTable:
+    """A join build side keyed by its int64 join-hash column, built ONCE and probed by every probe batch
+    (reference JoinMap / JoinProbe, src/lambdas/headers/JoinTuple.h:434, HashSink.h:14).
+
+    On the GPU: a device open-addressing table (relops.hip join_insert) whose slots hold a key's build rows as
+    a CSR run (join_perm), probed by one lookup per probe row (join_probe) and expanded into the (build, probe)
+    pairs (join_expand). On the CPU: the build hashes sorted once, probes binary-searched."""
+
+    def __init__(self, build_h: torch.Tensor):
+        self.h = build_h
+        self.n = int(build_h.numel())
+        self._dev = None
+        self._sorted = None
+        if self.n and build_h.is_cuda:
+            self._dev = _ext.hip().join_build(build_h.long().contiguous())
+        elif self.n:
+            self._sorted = torch.sort(build_h)
+
+    def probe(self, probe_h: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """All (build_idx, probe_idx) pairs with equal keys, probe-major."""
+        dev = probe_h.device
+        if self.n == 0 or probe_h.numel() == 0:
+            e = torch.empty(0, dtype=torch.int64, device=dev)
+            return e, e
+        if self._dev is not None:
+            tkey, tcnt, toff, perm = self._dev
+            return tuple(_ext.hip().join_probe(tkey, tcnt, toff, perm, probe_h.to(tkey.device).long().contiguous()))
+        sh, order = self._sorted
+        sh, order = sh.to(dev), order.to(dev)
+        lo = torch.searchsorted(sh, probe_h, right=False)
+        hi = torch.searchsorted(sh, probe_h, right=True)
+        cnt = hi - lo
+        probe_idx = torch.repeat_interleave(torch.arange(probe_h.numel(), device=dev), cnt)
+        if probe_idx.numel() == 0:
+            e = torch.empty(0, dtype=torch.int64, device=dev)
+            return e, e
+        starts = torch.repeat_interleave(lo, cnt)
+        csum = torch.cumsum(cnt, 0)
+        offs = torch.arange(probe_idx.numel(), device=dev) - torch.repeat_interleave(csum - cnt, cnt)
+        build_idx = order[starts + offs]
+        return build_idx, probe_idx
+
+
 def join_match(build_h: torch.Tensor, probe_h: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-    """All (build_idx, probe_idx) pairs with equal hashes: sort build side, binary-search probes."""
-    dev = probe_h.device
-    build_h = build_h.to(dev)
-    if build_h.numel() == 0 or probe_h.numel() == 0:
-        e = torch.empty(0, dtype=torch.int64, device=dev)
-        return e, e
-    sh, order = torch.sort(build_h)
-    lo = torch.searchsorted(sh, probe_h, right=False)
-    hi = torch.searchsorted(sh, probe_h, right=True)
-    cnt = hi - lo
-    probe_idx = torch.repeat_interleave(torch.arange(probe_h.numel(), device=dev), cnt)
-    if probe_idx.numel() == 0:
-        e = torch.empty(0, dtype=torch.int64, device=dev)
-        return e, e
-    starts = torch.repeat_interleave(lo, cnt)
-    csum = torch.cumsum(cnt, 0)
-    offs = torch.arange(probe_idx.numel(), device=dev) - torch.repeat_interleave(csum - cnt, cnt)
-    build_idx = order[starts + offs]
-    return build_idx, probe_idx
+    """All (build_idx, probe_idx) pairs with equal hashes (one-shot JoinTable)."""
+    return JoinTable(build_h.to(probe_h.device)).probe(probe_h)
+
+
+# ------------------------------------------------------------------------------ exact grouping on the device
+def _norm_col(c: torch.Tensor) -> torch.Tensor:
+    """1-D key column -> int64 words with value equality (floats by bits, -0.0 folded into +0.0)."""
+    if c.dtype == torch.int64:
+        return c.contiguous()
+    if c.is_floating_point():
+        return (c.double() + 0.0).view(torch.int64)
+    return c.long()
+
+
+def _pack_exact(words: List[torch.Tensor]):
+    """Several int64 key columns -> ONE int64 with the same equality and lexicographic order, when their value
+    ranges fit in 62 bits together (one host read of the column minima / maxima): (packed, layout) or None."""
+    if len(words) == 1:
+        return words[0], None
+    mm = torch.stack([torch.stack(list(torch.aminmax(w))) for w in words]).cpu().tolist()
+    bits = [int(hi - lo).bit_length() for lo, hi in mm]
+    if sum(bits) > 62:
+        return None
+    shifts, sh = [], sum(bits)
+    for b in bits:
+        sh -= b
+        shifts.append(sh)
+    packed = None
+    for w, (lo, _), s in zip(words, mm, shifts):
+        t = (w - lo) << s if s else (w - lo)
+        packed = t if packed is None else packed | t
+    return packed, [(lo, s, b) for (lo, _), s, b in zip(mm, shifts, bits)]
+
+
+def _unpack(packed: torch.Tensor, layout) -> List[torch.Tensor]:
+    out = []
+    for lo, s, b in layout:
+        v = _lsr(packed, s) if s else packed
+        out.append((v & ((1 << b) - 1) if b < 63 else v) + lo)
+    return out
+
+
+def _combine_words(words: List[torch.Tensor]) -> torch.Tensor:
+    out = None
+    for h in words:
+        out = h if out is None else mix64(out ^ h)
+    return out
+
+
+def _device_cols(keys):
+    """The key as a list of device columns (StringColumn or 1-D tensor), or None if it is not device-groupable."""
+    cols = list(keys) if isinstance(keys, tuple) else [keys]
+    if not cols:
+        return None
+    for c in cols:
+        if isinstance(c, StringColumn):
+            if c.device.type != "cuda":
+                return None
+        elif not (isinstance(c, torch.Tensor) and c.is_cuda and c.dim() == 1 and c.dtype != torch.bool
+                  or isinstance(c, torch.Tensor) and c.is_cuda and c.dim() == 1 and c.dtype == torch.bool):
+            return None
+    n = len(cols[0])
+    if any(len(c) != n for c in cols):
+        return None
+    return cols
+
+
+def _rows_match_rep(cols, words, ref: torch.Tensor) -> bool:
+    """Every row's key equals the key of its group's representative row ``ref`` (exactness check of a
+    hash-decided grouping)."""
+    ok = None
+    for c, w in zip(cols, words):
+        eq = c.eq_rows(None, c, ref) if isinstance(c, StringColumn) else (w == w.index_select(0, ref))
+        ok = eq if ok is None else ok & eq
+    return bool(ok.all())
+
+
+def _hash_aggregate(key64: torch.Tensor, vals, op: str, want_inv: bool):
+    r = _ext.hip().hash_aggregate(key64.contiguous(), vals, op, want_inv, 0)
+    status = r[5].tolist()
+    if status[2] != 1:
+        return None
+    return r[0], r[1], r[2], r[3], r[4]
+
+
+def _sort_groups(key_reps: torch.Tensor):
+    """Order of the groups by key value (the order torch.unique(sorted=True) gives) and its inverse rank."""
+    order = torch.argsort(key_reps)
+    rank = torch.empty_like(order)
+    rank[order] = torch.arange(order.numel(), device=order.device)
+    return order, rank
+
+
+def _take_col(c, idx):
+    return c.take(idx) if isinstance(c, StringColumn) else c.index_select(0, idx)
+
+
+def _group_ids_device(keys):
+    """Exact group ids of device key columns: packed ints, or a 64-bit hash + a check of every row against its
+    group's representative (strings byte-compared). None when the caller must take the generic path."""
+    cols = _device_cols(keys)
+    if cols is None or len(cols[0]) == 0:
+        return None
+    words = [c.hash64() if isinstance(c, StringColumn) else _norm_col(c) for c in cols]
+    packed = None if any(isinstance(c, StringColumn) for c in cols) else _pack_exact(words)
+    key = packed[0] if packed is not None else _combine_words(words)
+    r = _hash_aggregate(key, None, "sum", True)
+    if r is None:
+        return None
+    reps_k, _, _, first, inv = r
+    if packed is None and not _rows_match_rep(cols, words, first.index_select(0, inv)):
+        return None          # two different keys share a hash: the exact generic path decides
+    order, rank = _sort_groups(reps_k)
+    first = first.index_select(0, order)
+    inv = rank.index_select(0, inv)
+    reps = tuple(_take_col(c, first) for c in cols)
+    return inv, (reps if isinstance(keys, tuple) else reps[0]), int(first.numel())
+
+
+def group_reduce(keys, values, op: str = "sum"):
+    """Fused device group-by + aggregation (relops.hip hash_aggregate: LDS pre-aggregation for few groups, radix
+    partitioning for many): ``(representative keys, aggregates)`` ordered like :func:`group_ids`, or None when
+    the inputs need the generic path (host objects, non-numeric values, unsupported op).
+    Reference: AggregationProcessor.h:16 / CombinerProcessor over PDBMap hash tables."""
+    if op not in ("sum", "count", "min", "max", "mean") or not isinstance(values, torch.Tensor) or not values.is_cuda:
+        return None
+    cols = _device_cols(keys)
+    if cols is None or len(cols[0]) != values.shape[0] or values.shape[0] == 0:
+        return None
+    if values.dtype == torch.bool or values.is_complex():
+        return None
+    n = values.shape[0]
+    flat = values.reshape(n, -1)
+    if flat.shape[1] > 16:
+        return None
+    is_float = values.is_floating_point()
+    vals = None
+    if op != "count":
+        vals = flat.double() if is_float else flat.long()
+    kop = {"sum": "sum", "mean": "sum", "count": "sum", "min": "min", "max": "max"}[op]
+    words = [c.hash64() if isinstance(c, StringColumn) else _norm_col(c) for c in cols]
+    packed = None if any(isinstance(c, StringColumn) for c in cols) else _pack_exact(words)
+    key = packed[0] if packed is not None else _combine_words(words)
+    r = _hash_aggregate(key, vals, kop, packed is None)
+    if r is None:
+        return None
+    reps_k, aggs, cnt, first, inv = r
+    if packed is None and not _rows_match_rep(cols, words, first.index_select(0, inv)):
+        return None
+    order, _ = _sort_groups(reps_k)
+    g = int(order.numel())
+    cnt = cnt.index_select(0, order)
+    if op == "count":
+        agg = cnt
+    else:
+        agg = aggs.index_select(0, order)
+        if op == "mean":
+            agg = agg / cnt.unsqueeze(1).to(agg.dtype)
+        out_dtype = values.dtype if (is_float or op != "mean") else torch.float64
+        agg = agg.to(out_dtype).reshape((g,) + tuple(values.shape[1:]))
+    if packed is not None and packed[1] is not None:
+        unp = _unpack(reps_k.index_select(0, order), packed[1])
+        reps = tuple(u.to(c.dtype) if not c.is_floating_point() else u.view(torch.float64).to(c.dtype)
+                     for u, c in zip(unp, cols))
+    elif packed is not None:
+        rk = reps_k.index_select(0, order)
+        c = cols[0]
+        reps = (rk.to(c.dtype) if not c.is_floating_point() else rk.view(torch.float64).to(c.dtype),)
+    else:
+        fo = first.index_select(0, order)
+        reps = tuple(_take_col(c, fo) for c in cols)
+    return (reps if isinstance(keys, tuple) else reps[0]), agg
 
 
 def group_ids(keys) -> Tuple[torch.Tensor, Any, int]:
-    """Exact group-by: returns (inverse index per row, representative key column, #groups)."""
+    """Exact group-by: returns (inverse index per row, representative key column, #groups), groups in key order
+    (hash order for string keys). Device columns group on the device hash tables (values compared exactly);
+    host data groups with torch.unique / a dict."""
+    if _device_cols(keys) is not None and _hip_groupby():
+        r = _group_ids_device(keys)
+        if r is not None:
+            return r
     if isinstance(keys, StringColumn):
-        inv, first, n = _unique_first(keys.hash64())
-        return inv, keys.take(first), n
+        return _group_strings_exact(keys)
     if isinstance(keys, tuple) and any(isinstance(k, StringColumn) for k in keys) and all(
             isinstance(k, StringColumn) or (isinstance(k, torch.Tensor) and k.dim() == 1) for k in keys):
         dev = keys[0].device
-        cols = [k.hash64() if isinstance(k, StringColumn) else
-                (k.to(dev).long() if not k.is_floating_point() else k.double().view(torch.int64).to(dev)) for k in keys]
+        strs = [k for k in keys if isinstance(k, StringColumn)]
+        # exact: string columns by their dictionary codes (hash + byte re-check), then a lexicographic unique
+        cols = [_group_strings_exact(k)[0] if isinstance(k, StringColumn) else _norm_col(k.to(dev)) for k in keys]
+        del strs
         uniq, inv = torch.unique(torch.stack([c.to(dev) for c in cols], 1), dim=0, return_inverse=True)
         first = torch.full((uniq.shape[0],), inv.numel(), dtype=torch.long, device=dev)
         first.scatter_reduce_(0, inv, torch.arange(inv.numel(), device=dev), "amin")
@@ -128,10 +335,6 @@ def group_ids(keys) -> Tuple[torch.Tensor, Any, int]:
                      for j, k in enumerate(keys))
         return inv, reps, uniq.shape[0]
     if isinstance(keys, torch.Tensor) and keys.dim() == 1:
-        if keys.is_cuda and not keys.is_floating_point() and keys.dtype != torch.bool and _hash_groupby():
-            # device hash table (hashagg.hip): O(n) insert, only the distinct keys are sorted
-            inv, uniq = _ext.hip().hash_group_ids(keys.long())
-            return inv, uniq.to(keys.dtype), uniq.numel()
         uniq, inv = torch.unique(keys, return_inverse=True)
         return inv, uniq, uniq.numel()
     # host objects: dict grouping preserving first-seen order
@@ -150,21 +353,48 @@ def group_ids(keys) -> Tuple[torch.Tensor, Any, int]:
     return torch.tensor(inv, dtype=torch.int64), reps, len(reps)
 
 
-def _hash_groupby() -> bool:
-    """Device hash-table group ids (hashagg.hip) instead of torch.unique; ops.kernel_options(hash_groupby=...)."""
+def _group_strings_exact(col: StringColumn):
+    """(inverse, representative strings, #groups) of a string column: group by 64-bit hash, then byte-compare
+    every row with its group's first row; rows of a hash shared by different strings are regrouped by value."""
+    h = col.hash64()
+    inv, first, g = _unique_first(h)
+    ok = col.eq_rows(None, col, first.index_select(0, inv))
+    if bool(ok.all()):
+        return inv, col.take(first), g
+    # hash collision(s): split exactly by value (host dict over the distinct strings of the colliding groups)
+    strs = col.tolist()
+    seen, inv_l, firsts = {}, [], []
+    for i, s in enumerate(strs):
+        gi = seen.get(s)
+        if gi is None:
+            gi = len(firsts)
+            seen[s] = gi
+            firsts.append(i)
+        inv_l.append(gi)
+    dev = col.device
+    return (torch.tensor(inv_l, dtype=torch.int64, device=dev),
+            col.take(torch.tensor(firsts, dtype=torch.int64, device=dev)), len(firsts))
+
+
+def _hip_groupby() -> bool:
+    """Device hash tables for group-by (relops.hip) instead of torch.unique; ops.kernel_options(hash_groupby=...)."""
     from .. import ops
     return bool(ops._kopt("hash_groupby", HASH_GROUPBY_DEFAULT))
 
 
-HASH_GROUPBY_DEFAULT = False
+_hash_groupby = _hip_groupby
+HASH_GROUPBY_DEFAULT = True
 
 
 def _unique_first(h: torch.Tensor):
-    """(inverse, first row of each group, #groups) for a 1-D key tensor."""
-    if h.is_cuda and _hash_groupby():
-        inv, uniq = _ext.hip().hash_group_ids(h)
-    else:
-        uniq, inv = torch.unique(h, return_inverse=True)
+    """(inverse, first row of each group, #groups) for a 1-D int64 key tensor."""
+    if h.is_cuda and _hip_groupby() and h.numel():
+        r = _hash_aggregate(h.long(), None, "sum", True)
+        if r is not None:
+            reps_k, _, _, first, inv = r
+            order, rank = _sort_groups(reps_k)
+            return rank.index_select(0, inv), first.index_select(0, order), int(order.numel())
+    uniq, inv = torch.unique(h, return_inverse=True)
     first = torch.full((uniq.numel(),), h.numel(), dtype=torch.long, device=h.device)
     first.scatter_reduce_(0, inv, torch.arange(h.numel(), device=h.device), "amin")
     return inv, first, uniq.numel()
@@ -246,9 +476,17 @@ def partition_of(h: torch.Tensor, nparts: int) -> torch.Tensor:
     return torch.remainder(h, nparts)
 
 
+def partition_order(dest: torch.Tensor, nparts: int) -> Tuple[torch.Tensor, List[int]]:
+    """Stable permutation grouping rows by destination + per-destination counts (HashPartitionSink): one
+    device pass of per-workgroup histograms + ballot-ranked scatter (relops.hip partition_perm) on the GPU."""
+    if dest.is_cuda and 0 < nparts <= 2048 and dest.numel():
+        perm, counts = _ext.hip().partition_perm(dest.long().contiguous(), nparts)
+        return perm, counts.tolist()
+    return torch.argsort(dest, stable=True), torch.bincount(dest, minlength=nparts).tolist()
+
+
 def split_by_dest(batch: RecordBatch, dest: torch.Tensor, nparts: int) -> List[RecordBatch]:
-    order = torch.argsort(dest, stable=True)
-    counts = torch.bincount(dest, minlength=nparts).tolist()
+    order, counts = partition_order(dest, nparts)
     sorted_b = batch.take(order)
     out, s = [], 0
     for c in counts:
@@ -257,5 +495,5 @@ def split_by_dest(batch: RecordBatch, dest: torch.Tensor, nparts: int) -> List[R
     return out
 
 
-__all__ = ["mix64", "hash_keys", "column_to_int64", "join_match", "group_ids", "segment_reduce", "take_reps",
-           "partition_of", "split_by_dest"]
+__all__ = ["mix64", "hash_keys", "column_to_int64", "JoinTable", "join_match", "group_ids", "group_reduce",
+           "segment_reduce", "take_reps", "partition_of", "partition_order", "split_by_dest"]

@@ -323,7 +323,7 @@ def _equals(a, b):
     if isinstance(a, StringColumn) and isinstance(b, str):
         return a.eq(b)                                   # one device pattern-match launch
     if isinstance(a, StringColumn) and isinstance(b, StringColumn) and len(a) == len(b):
-        return a.hash64() == b.to(a.device).hash64()     # row-wise equality by 64-bit hash
+        return a.eq_rows(None, b, None)                  # row-wise byte-exact equality (one device launch)
     ta, tb = _to_tensor_col(a), _to_tensor_col(b)
     if ta is not None and (tb is not None or not isinstance(b, (list, StringColumn, SelfRef))):
         other = tb if tb is not None else b

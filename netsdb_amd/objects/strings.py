@@ -306,6 +306,41 @@ class StringColumn:
             return _ext.hip().str_hash(self.data, self.offsets, self.payload)
         return torch.from_numpy(_hash_np(self.data.numpy(), self.offsets.numpy()).copy())
 
+    def eq_rows(self, ia: Optional[torch.Tensor], other: "StringColumn", ib: Optional[torch.Tensor]) -> torch.Tensor:
+        """Byte-exact ``self[ia[i]] == other[ib[i]]`` for every i (ia / ib None: the identity), as a bool mask: the
+        exact check behind hash-decided group-by / join / IN (reference pdb::String equality, PDBString.h:46-48)."""
+        m = len(self) if ia is None else ia.numel()
+        dev = self.device
+        other = other.to(dev)
+        if m == 0:
+            return torch.zeros(0, dtype=torch.bool, device=dev)
+        for idx, col in ((ia, self), (ib, other)):
+            if idx is not None and idx.numel():
+                lo, hi = torch.aminmax(idx)
+                if int(lo) < 0 or int(hi) >= len(col):
+                    raise IndexError("eq_rows index out of range")
+        if dev.type == "cuda":
+            ia_ = None if ia is None else ia.to(dev).long().contiguous()
+            ib_ = None if ib is None else ib.to(dev).long().contiguous()
+            return _ext.hip().str_eq_pairs(self.data, self.offsets.contiguous(), ia_, other.data,
+                                           other.offsets.contiguous(), ib_, m)
+        ra = np.arange(m) if ia is None else ia.numpy()
+        rb = np.arange(m) if ib is None else ib.numpy()
+        oa, ob = self.offsets.numpy(), other.offsets.numpy()
+        sa, la = oa[:-1][ra], (oa[1:] - oa[:-1])[ra]
+        sb, lb = ob[:-1][rb], (ob[1:] - ob[:-1])[rb]
+        eq = la == lb
+        idx = np.nonzero(eq & (la > 0))[0]
+        if idx.size:
+            ln = la[idx]
+            tot = int(ln.sum())
+            rel = np.arange(tot) - np.repeat(np.cumsum(ln) - ln, ln)
+            da, db = self.data.numpy(), other.data.numpy()
+            same = da[np.repeat(sa[idx], ln) + rel] == db[np.repeat(sb[idx], ln) + rel]
+            ok = np.minimum.reduceat(same, np.cumsum(ln) - ln)
+            eq[idx] = ok.astype(bool)
+        return torch.from_numpy(eq)
+
     def _match(self, compiled, negate=False) -> torch.Tensor:
         pat, st, ln, a0, a1 = compiled
         if self.device.type == "cuda":
@@ -337,19 +372,31 @@ class StringColumn:
         return self._match(_literal([s], False, False))
 
     def isin(self, values: Sequence[str]) -> torch.Tensor:
-        """Membership by 64-bit hash (one launch + torch.isin); collisions are ~2^-64 per pair."""
+        """Exact membership: a 64-bit hash decides the candidate value (one launch + a sort/search of the
+        list's hashes), then every candidate row is byte-compared with that value (str_eq_pairs), so two strings
+        with equal hashes are never confused."""
+        values = list(dict.fromkeys(values))
+        n = len(self)
+        if n == 0 or not values:
+            return torch.zeros(n, dtype=torch.bool, device=self.device)
         h = self.hash64()
-        ref = torch.tensor([hash_str(v) for v in values], dtype=torch.int64, device=self.device)
-        return torch.isin(h, ref)
+        ref = StringColumn.from_list(values, self.device)
+        sh, order = torch.sort(ref.hash64())
+        pos = torch.searchsorted(sh, h).clamp_(max=len(values) - 1)
+        cand = sh.index_select(0, pos) == h
+        if bool(torch.unique(sh).numel() != sh.numel()):
+            # two listed values share a hash: decide on the host (exact, and never hit in practice)
+            allowed = set(values)
+            return torch.tensor([s in allowed for s in self.tolist()], dtype=torch.bool, device=self.device)
+        return cand & self.eq_rows(None, ref, order.index_select(0, pos))
 
     def dict_encode(self):
         """(codes int64 [n], dictionary list[str]): device unique over the hashes; only the distinct
         strings cross to the host."""
-        h = self.hash64()
-        uniq, inv = torch.unique(h, return_inverse=True)
-        first = torch.full((uniq.numel(),), len(self), dtype=torch.long, device=self.device)
-        first.scatter_reduce_(0, inv, torch.arange(len(self), device=self.device), "amin")
-        return inv, self.take(first).tolist()
+        from ..execution.kernels import group_ids   # exact (hash + byte re-check) grouping
+
+        inv, reps, _ = group_ids(self)
+        return inv, reps.tolist()
 
 
 def is_string_list(c) -> bool:

@@ -20,7 +20,8 @@ KDIR = os.path.join("netsdb_amd", "csrc", "kernels")
 RDIR = os.path.join("netsdb_amd", "csrc", "runtime")
 
 
-HIP_SOURCES = ("gemm.hip", "gemm_f32.hip", "conv2d.hip", "rowops.hip", "strings.hip", "dedup.hip", "hashagg.hip")
+HIP_SOURCES = ("gemm.hip", "gemm_f32.hip", "conv2d.hip", "rowops.hip", "strings.hip", "dedup.hip", "relops.hip",
+               "relops_bind.cpp")
 SDIR = os.path.join("netsdb_amd", "csrc", "study")
 STUDY_SOURCES = ("gemm_study.hip", "gemm_w4a.hip")
 

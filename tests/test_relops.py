@@ -1,0 +1,247 @@
+"""Device relational operators (csrc/kernels/relops.hip via execution/kernels.py): hash aggregation, hash join,
+partition permutation, and value-exact keys (strings byte-compared after the hash; packed int tuples).
+
+GPU tests compare every kernel against a plain PyTorch / Python reference of the same op; CPU tests cover the
+host paths and the collision handling with a deliberately weak string hash."""
+import pytest
+import torch
+
+from netsdb_amd import _ext
+from netsdb_amd.execution import kernels as K
+from netsdb_amd.objects.strings import StringColumn
+
+DEV = "cuda:0"
+
+
+def _ref_groupby(keys, vals, op):
+    """dict: key -> (agg row, count) in fp64 / int64 on the host."""
+    out = {}
+    k = keys.tolist()
+    v = vals.tolist() if vals is not None else [None] * len(k)
+    for kk, vv in zip(k, v):
+        vv = vv if isinstance(vv, list) else [vv]
+        if kk not in out:
+            out[kk] = [list(vv), 1]
+        else:
+            a, c = out[kk]
+            for j, x in enumerate(vv):
+                a[j] = a[j] + x if op == "sum" else (min(a[j], x) if op == "min" else max(a[j], x))
+            out[kk][1] = c + 1
+    return out
+
+
+def _check_agg(keys, vals, op, r, rtol=1e-9):
+    reps, aggs, cnt, first, inv, status = r
+    ref = _ref_groupby(keys.cpu(), None if vals is None else vals.cpu(), op)
+    g = int(status[0])
+    assert g == len(ref) == reps.numel()
+    assert sorted(reps.tolist()) == sorted(ref.keys())
+    kl = keys.cpu().tolist()
+    first_of = {}
+    for i, kk in enumerate(kl):
+        first_of.setdefault(kk, i)
+    cl, fl = cnt.cpu().tolist(), first.cpu().tolist()
+    al = aggs.cpu().tolist() if vals is not None else None
+    for i, kk in enumerate(reps.tolist()):
+        a, c = ref[kk]
+        assert cl[i] == c
+        assert fl[i] == first_of[kk]
+        if al is not None:
+            for x, y in zip(al[i], a):
+                assert abs(x - y) <= rtol * max(1.0, abs(y)), (kk, al[i], a)
+    if inv.numel():
+        assert torch.equal(reps.index_select(0, inv).cpu(), keys.cpu())
+
+
+# ------------------------------------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,distinct", [(1000, 8), (200_000, 10), (200_000, 5000), (300_000, 250_000),
+                                        (50_000, 1), (17, 17)])
+@pytest.mark.parametrize("op", ["sum", "min", "max"])
+def test_hash_aggregate_f64(n, distinct, op):
+    g = torch.Generator(device=DEV).manual_seed(n + distinct)
+    keys = torch.randint(0, distinct, (n,), device=DEV, generator=g) * 7919 - 3 * distinct
+    vals = torch.rand(n, 3, device=DEV, dtype=torch.float64, generator=g) - 0.5
+    r = _ext.hip().hash_aggregate(keys, vals, op, True, 0)
+    assert int(r[5][2]) == 1
+    _check_agg(keys, vals, op, r)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("op", ["sum", "min", "max"])
+def test_hash_aggregate_int64_and_sentinel(op):
+    g = torch.Generator(device=DEV).manual_seed(3)
+    keys = torch.randint(0, 300, (100_000,), device=DEV, generator=g)
+    keys[::97] = torch.iinfo(torch.int64).min            # the empty-slot marker as a real key
+    keys[5::101] = torch.iinfo(torch.int64).max
+    vals = torch.randint(-10**12, 10**12, (100_000,), device=DEV, generator=g)
+    for thr in (0, 1):                                      # LOW path and forced PART path
+        r = _ext.hip().hash_aggregate(keys, vals, op, True, thr if thr else 0)
+        _check_agg(keys, vals.unsqueeze(1), op, r, rtol=0)
+    r = _ext.hip().hash_aggregate(keys, None, "sum", False, 0)   # counts only, no inverse
+    reps, _, cnt, _, inv, _ = r
+    assert inv.numel() == 0
+    ref = torch.bincount(torch.unique(keys.cpu(), return_inverse=True)[1])
+    assert sorted(cnt.cpu().tolist()) == sorted(ref.tolist())
+
+
+@pytest.mark.gpu
+def test_hash_aggregate_paths_agree_on_skew():
+    """Zipf-like skew: hot keys span many PART chunks (global-table flush) next to singleton buckets."""
+    g = torch.Generator(device=DEV).manual_seed(11)
+    hot = torch.randint(0, 4, (400_000,), device=DEV, generator=g)
+    cold = torch.randint(1000, 10**9, (100_000,), device=DEV, generator=g)
+    keys = torch.cat([hot, cold])[torch.randperm(500_000, device=DEV, generator=g)]
+    vals = torch.ones(500_000, 1, device=DEV, dtype=torch.float64)
+    for thr in (0, 100_000):
+        r = _ext.hip().hash_aggregate(keys, vals, "sum", True, thr)
+        _check_agg(keys, vals, "sum", r)
+
+
+@pytest.mark.gpu
+def test_group_reduce_matches_segment_reduce():
+    g = torch.Generator(device=DEV).manual_seed(5)
+    n = 123_457
+    a = torch.randint(0, 50, (n,), device=DEV, generator=g)
+    b = torch.randint(-3, 3, (n,), device=DEV, generator=g).to(torch.int32)
+    v = torch.randn(n, 2, device=DEV, generator=g)
+    for op in ("sum", "min", "max", "count", "mean"):
+        reps, agg = K.group_reduce((a, b), v, op)
+        with K_opts(hash_groupby=False):
+            inv, reps2, g2 = K.group_ids((a.cpu(), b.cpu()))
+        ref = K.segment_reduce(v.cpu(), inv, g2, op) if op != "count" else torch.bincount(inv)
+        assert torch.equal(reps[0].cpu(), reps2[0]) and torch.equal(reps[1].cpu(), reps2[1])
+        assert reps[1].dtype == torch.int32
+        torch.testing.assert_close(agg.cpu().to(ref.dtype), ref, rtol=1e-5, atol=1e-4)
+
+
+def K_opts(**kw):
+    from netsdb_amd import ops
+    return ops.kernel_options(**kw)
+
+
+@pytest.mark.gpu
+def test_group_ids_device_tuple_unpackable_and_floats():
+    g = torch.Generator(device=DEV).manual_seed(9)
+    n = 50_000
+    a = torch.randint(-2**62, 2**62, (30,), device=DEV, generator=g)[torch.randint(0, 30, (n,), device=DEV, generator=g)]
+    b = torch.randint(-2**62, 2**62, (7,), device=DEV, generator=g)[torch.randint(0, 7, (n,), device=DEV, generator=g)]
+    f = torch.tensor([0.0, -0.0, 1.5, float("inf")], device=DEV)[torch.randint(0, 4, (n,), device=DEV, generator=g)]
+    inv, reps, ng = K.group_ids((a, b, f))
+    ref = {}
+    for t in zip(a.tolist(), b.tolist(), f.tolist()):
+        ref.setdefault(t, len(ref))
+    assert ng == len(ref)
+    got = list(zip(*(r.tolist() for r in reps)))
+    assert sorted(got) == sorted(ref.keys())
+    rows = list(zip(a.tolist(), b.tolist(), f.tolist()))
+    il = inv.tolist()
+    for i in range(0, n, 997):
+        assert got[il[i]] == rows[i]
+
+
+@pytest.mark.gpu
+def test_join_table_device_vs_host():
+    g = torch.Generator(device=DEV).manual_seed(2)
+    build = torch.randint(0, 5000, (40_000,), device=DEV, generator=g)
+    build[::13] = torch.iinfo(torch.int64).min
+    probe = torch.randint(-100, 6000, (70_000,), device=DEV, generator=g)
+    probe[::17] = torch.iinfo(torch.int64).min
+    jt = K.JoinTable(build)
+    bi, pi = jt.probe(probe)
+    bi2, pi2 = K.JoinTable(build.cpu()).probe(probe.cpu())
+    assert bi.numel() == bi2.numel() > 0
+    assert torch.equal(build[bi], probe[pi])
+    a = sorted(zip(pi.cpu().tolist(), bi.cpu().tolist()))
+    b = sorted(zip(pi2.tolist(), bi2.tolist()))
+    assert a == b
+    assert bool((pi[1:] >= pi[:-1]).all())                 # probe-major
+    e_b, e_p = jt.probe(torch.empty(0, dtype=torch.int64, device=DEV))
+    assert e_b.numel() == 0 and e_p.numel() == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P", [1, 2, 8, 255, 1024])
+def test_partition_order_stable(P):
+    g = torch.Generator(device=DEV).manual_seed(P)
+    dest = torch.randint(0, P, (200_003,), device=DEV, generator=g)
+    perm, counts = K.partition_order(dest, P)
+    assert torch.equal(perm.cpu(), torch.argsort(dest.cpu(), stable=True))
+    assert counts == torch.bincount(dest.cpu(), minlength=P).tolist()
+
+
+@pytest.mark.gpu
+def test_string_keys_exact_under_hash_collisions_gpu(monkeypatch):
+    strs = [f"key{i % 37}" for i in range(5000)]
+    col = StringColumn.from_list(strs, DEV)
+    orig = StringColumn.hash64
+    monkeypatch.setattr(StringColumn, "hash64", lambda self: orig(self) & 3)   # 4 hash values for 37 strings
+    inv, reps, ng = K.group_ids(col)
+    assert ng == 37 and sorted(reps.tolist()) == sorted(set(strs))
+    rl = reps.tolist()
+    assert [rl[i] for i in inv.tolist()] == strs
+    nums = torch.tensor([i % 2 for i in range(5000)], device=DEV)
+    inv2, reps2, ng2 = K.group_ids((col, nums))
+    assert ng2 == len(set(zip(strs, nums.tolist())))
+    vals = torch.ones(5000, device=DEV)
+    r = K.group_reduce(col, vals, "sum")
+    if r is not None:   # a hash-decided fused result must be exact too
+        assert sorted(zip(r[0].tolist(), r[1].tolist())) == sorted((s, float(strs.count(s))) for s in set(strs))
+    m = col.isin(["key1", "key5"])
+    assert m.tolist() == [s in ("key1", "key5") for s in strs]
+
+
+@pytest.mark.gpu
+def test_str_eq_pairs_kernel():
+    a = StringColumn.from_list(["", "a", "abcdefghij", "abcdefghiX", "same", "x" * 100], DEV)
+    b = StringColumn.from_list(["", "b", "abcdefghij", "abcdefghij", "same", "x" * 99 + "y"], DEV)
+    assert a.eq_rows(None, b, None).tolist() == [True, False, True, False, True, False]
+    ia = torch.tensor([4, 2, 0], device=DEV)
+    ib = torch.tensor([4, 3, 0], device=DEV)
+    assert a.eq_rows(ia, b, ib).tolist() == [True, True, True]
+
+
+# ------------------------------------------------------------------------------------------------ CPU
+def test_string_group_exact_under_collisions_cpu(monkeypatch):
+    strs = [f"k{i % 11}" for i in range(400)]
+    col = StringColumn.from_list(strs)
+    orig = StringColumn.hash64
+    monkeypatch.setattr(StringColumn, "hash64", lambda self: orig(self) & 1)
+    inv, reps, ng = K.group_ids(col)
+    assert ng == 11
+    rl = reps.tolist()
+    assert [rl[i] for i in inv.tolist()] == strs
+    assert col.isin(["k3"]).tolist() == [s == "k3" for s in strs]
+    assert col.eq_rows(None, StringColumn.from_list(["k0"] * 400), None).tolist() == [s == "k0" for s in strs]
+
+
+def test_isin_listed_values_sharing_a_hash(monkeypatch):
+    col = StringColumn.from_list(["a", "b", "c", "a"])
+    monkeypatch.setattr(StringColumn, "hash64", lambda self: torch.zeros(len(self), dtype=torch.int64))
+    assert col.isin(["a", "c"]).tolist() == [True, False, True, True]
+
+
+def test_join_table_host_path():
+    build = torch.tensor([5, 1, 5, 9, 1, 1])
+    probe = torch.tensor([1, 2, 5, 9, 9])
+    bi, pi = K.JoinTable(build).probe(probe)
+    pairs = sorted(zip(pi.tolist(), bi.tolist()))
+    assert pairs == [(0, 1), (0, 4), (0, 5), (2, 0), (2, 2), (3, 3), (4, 3)]
+
+
+def test_partition_order_host_path():
+    dest = torch.tensor([2, 0, 2, 1, 0])
+    perm, counts = K.partition_order(dest, 3)
+    assert perm.tolist() == [1, 4, 3, 0, 2] and counts == [2, 1, 2]
+
+
+def test_pack_exact_roundtrip():
+    a = torch.tensor([3, -5, 3, 100])
+    b = torch.tensor([7, 7, 8, 0])
+    packed, layout = K._pack_exact([a, b])
+    ua, ub = K._unpack(packed, layout)
+    assert torch.equal(ua, a) and torch.equal(ub, b)
+    # lexicographic order preserved
+    order = torch.argsort(packed)
+    assert [(int(a[i]), int(b[i])) for i in order] == sorted(zip(a.tolist(), b.tolist()))
+    assert K._pack_exact([torch.tensor([-2**62, 2**62]), torch.tensor([0, 1])]) is None
