@@ -180,6 +180,11 @@ class PDBClient:
         resident under pressure from one-pass job data."""
         self.storage.set_locality(db, name, locality)
 
+    def set_costs(self, db: str, name: str, write_cost: Optional[float] = None, read_cost: Optional[float] = None):
+        """Per-set multipliers of the page cache's eviction write / read costs (LocalitySet::setWriteCost /
+        setReadCost, src/storage/headers/LocalitySet.h:122-139)."""
+        self.storage.set_costs(db, name, write_cost=write_cost, read_cost=read_cost)
+
     def remove_set(self, db: str, name: str) -> bool:
         self.storage.remove_set(db, name)
         self.catalog.remove_set(db, name)

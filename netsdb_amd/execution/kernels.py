@@ -476,13 +476,19 @@ def partition_of(h: torch.Tensor, nparts: int) -> torch.Tensor:
     return torch.remainder(h, nparts)
 
 
-def partition_order(dest: torch.Tensor, nparts: int) -> Tuple[torch.Tensor, List[int]]:
-    """Stable permutation grouping rows by destination + per-destination counts (HashPartitionSink): one
-    device pass of per-workgroup histograms + ballot-ranked scatter (relops.hip partition_perm) on the GPU."""
+def partition_perm(dest: torch.Tensor, nparts: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Stable permutation grouping rows by destination + per-destination counts as a tensor (no host read):
+    on the GPU one pass of per-workgroup histograms + a ballot-ranked scatter (relops.hip partition_perm)."""
     if dest.is_cuda and 0 < nparts <= 2048 and dest.numel():
         perm, counts = _ext.hip().partition_perm(dest.long().contiguous(), nparts)
-        return perm, counts.tolist()
-    return torch.argsort(dest, stable=True), torch.bincount(dest, minlength=nparts).tolist()
+        return perm, counts
+    return torch.argsort(dest, stable=True), torch.bincount(dest, minlength=nparts)
+
+
+def partition_order(dest: torch.Tensor, nparts: int) -> Tuple[torch.Tensor, List[int]]:
+    """:func:`partition_perm` with the counts read back as a list (HashPartitionSink)."""
+    perm, counts = partition_perm(dest, nparts)
+    return perm, counts.tolist()
 
 
 def split_by_dest(batch: RecordBatch, dest: torch.Tensor, nparts: int) -> List[RecordBatch]:
@@ -496,4 +502,4 @@ def split_by_dest(batch: RecordBatch, dest: torch.Tensor, nparts: int) -> List[R
 
 
 __all__ = ["mix64", "hash_keys", "column_to_int64", "JoinTable", "join_match", "group_ids", "group_reduce",
-           "segment_reduce", "take_reps", "partition_of", "partition_order", "split_by_dest"]
+           "segment_reduce", "take_reps", "partition_of", "partition_perm", "partition_order", "split_by_dest"]

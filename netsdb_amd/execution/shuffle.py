@@ -140,8 +140,7 @@ class StreamingShuffle:
         dest = K.partition_of(h.to(flat.device), self.ws)
         ch = _Chunk()
         ch.rows = flat.n
-        ch.counts = torch.bincount(dest, minlength=self.ws)
-        order = torch.argsort(dest, stable=True)
+        order, ch.counts = K.partition_perm(dest, self.ws)   # device partition+pack permutation, counts stay on device
         sorted_b = flat.take(order)
         from ..parallel.comm import _batch_meta
 
@@ -183,19 +182,22 @@ class StreamingShuffle:
         if ch is not None and ch.event is not None:
             ch.event.synchronize()             # the chunk sealed one step ago: its counts have landed
         send = [int(x) for x in ch.host.tolist()] if ch is not None else [0] * ws
-        rows = ctx.all_gather_ints(send + [1 if more else 0])
+        # a chunk whose schema differs from the agreed one is flagged in the same all-gather, so every rank
+        # learns it together and takes the record-exchange path for this round (never a one-rank raise that
+        # leaves the peers blocked in the all-to-all)
+        odd = int(self.schema is not None and ch is not None and ch.meta != self.schema.meta)
+        rows = ctx.all_gather_ints(send + [1 if more else 0, odd])
         recv = [r[ctx.rank] for r in rows]
         any_more = any(r[ws] for r in rows)
+        any_odd = any(r[ws + 1] for r in rows)
         self.stats["rounds"] += 1
         if not self.input_done:
             self.stats["rounds_while_pipeline"] += 1
         self.stats["rows_sent"] += sum(send) - send[ctx.rank]
         self.stats["rows_received"] += sum(recv) - recv[ctx.rank]
-        if self.schema is not None:          # agreed on every rank: all columns fixed-width tensors
+        if self.schema is not None and not any_odd:   # every rank: all columns fixed-width tensors, same schema
             rb = self.schema.row_bytes
-            if ch is not None and (ch.packed is None or ch.meta != self.schema.meta):
-                if ch.meta != self.schema.meta:
-                    raise RuntimeError(f"shuffle {self.tag}: chunk schema {ch.meta} != agreed {self.schema.meta}")
+            if ch is not None and ch.packed is None:
                 ch.packed = self.schema.pack(ch.batch)
             src = ch.packed.reshape(-1) if ch is not None else torch.empty(0, dtype=torch.uint8, device=ctx.device)
             out = torch.empty(sum(recv) * rb, dtype=torch.uint8, device=src.device)
@@ -248,6 +250,22 @@ class StreamingShuffle:
                 if b is not None and b.n:
                     yield b
             return
+        # Two shuffles on one context must never have rounds in flight at once: their collectives share the
+        # metadata group, and rank A could enter this shuffle's round while rank B is still in the other's.
+        # A shuffle started while another one runs (an upstream shuffle feeding a shuffling sink: a partitioned
+        # probe under a distributed aggregate / partition / partitioned build) therefore seals its chunks
+        # locally and starts its rounds only once its input is exhausted, and yields only after its last
+        # round; the plan nests shuffles the same way on every rank, so every rank takes the same mode.
+        active = getattr(self.ctx, "_active_shuffles", 0)
+        deferred = active > 0
+        self.stats["deferred"] = int(deferred)
+        self.ctx._active_shuffles = active + 1
+        try:
+            yield from self._run(items, deferred)
+        finally:
+            self.ctx._active_shuffles = getattr(self.ctx, "_active_shuffles", 1) - 1
+
+    def _run(self, items, deferred: bool) -> Iterator[RecordBatch]:
         for b, h in items:
             if b is None or b.n == 0:
                 continue
@@ -255,6 +273,8 @@ class StreamingShuffle:
             self.pending_bytes += b.nbytes()
             if self.pending_bytes >= self.chunk_bytes:
                 self._seal()
+            if deferred:
+                continue
             # lag one sealed chunk: the host reads counts only of chunks whose copy was issued a step ago
             while len(self.sealed) > 1 and not self.done:
                 self._round(self.sealed.popleft(), more=True)
@@ -266,6 +286,12 @@ class StreamingShuffle:
             self._round(ch, more=bool(self.sealed))
         while not self.done:
             self._round(None, more=False)
+        if deferred:
+            # hold every received batch until the rounds are over (the outer shuffle may start rounds as soon
+            # as this one yields)
+            got = list(self._drain(block=True))
+            yield from got
+            return
         yield from self._drain(block=True)
 
 

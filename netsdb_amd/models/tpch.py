@@ -258,7 +258,10 @@ def to_batch(table: str, cols: Dict[str, object], device=None) -> RecordBatch:
     for name, ft in typ.fields().items():
         v = cols[name]
         if ft is str:
-            out[name] = StringColumn.from_list(v, device) if use_device_strings(device or "cpu") else list(v)
+            if hasattr(v, "to_column"):      # tpch_gen.GenStrings: one vocabulary gather on the device
+                out[name] = v.to_column(device) if use_device_strings(device or "cpu") else v.tolist()
+            else:
+                out[name] = StringColumn.from_list(v, device) if use_device_strings(device or "cpu") else list(v)
         else:
             arr = np.asarray(v)
             out[name] = torch.from_numpy(arr.astype(np.float64 if ft is float else np.int64))
@@ -268,12 +271,16 @@ def to_batch(table: str, cols: Dict[str, object], device=None) -> RecordBatch:
     return RecordBatch(out, n, typ)
 
 
-def load(client, db: str, tables: Dict[str, Dict[str, object]], page_rows: Optional[int] = None):
-    """Create the TPC-H sets and dispatch the rows (tpchDataLoader.cc)."""
+def load(client, db: str, tables: Dict[str, Dict[str, object]], page_rows: Optional[int] = None,
+         only: Optional[Sequence[str]] = None, device=None):
+    """Create the TPC-H sets and dispatch the rows (tpchDataLoader.cc). ``only``: a subset of the tables;
+    ``device``: build the batch there first (device string columns from generated vocabularies)."""
     client.create_database(db)
     for name, typ in TABLES.items():
+        if only is not None and name not in only:
+            continue
         client.create_set(db, name, typ)
-        client.send_data(db, name, to_batch(name, tables[name]))
+        client.send_data(db, name, to_batch(name, tables[name], device))
 
 
 # ------------------------------------------------------------------------------------ helpers
@@ -721,20 +728,24 @@ QUERIES = {"q01": q01, "q02": q02, "q03": q03, "q04": q04, "q06": q06, "q12": q1
 def frames(tables):
     import pandas as pd
 
-    return {k: pd.DataFrame({c: (np.asarray(v) if not isinstance(v, list) else v) for c, v in t.items()})
-            for k, t in tables.items()}
+    def col(v):
+        if hasattr(v, "to_pandas"):          # tpch_gen.GenStrings -> Categorical / fixed-width strings
+            return v.to_pandas()
+        return np.asarray(v) if not isinstance(v, list) else v
+
+    return {k: pd.DataFrame({c: col(v) for c, v in t.items()}) for k, t in tables.items()}
 
 
-def reference(name: str, tables, **kw):
-    """The same query in pandas over the generated tables (test oracle)."""
-    f = frames(tables)
+def reference(name: str, tables, f=None, **kw):
+    """The same query in pandas over the generated tables (test oracle); ``f``: prebuilt :func:`frames`."""
+    f = frames(tables) if f is None else f
     li, o, c, p = f["lineitem"], f["orders"], f["customer"], f["part"]
     if name == "q01":
         cut = add_days(19981201, -kw.get("delta_days", 90))
         x = li[li.l_shipdate <= cut].copy()
         x["dp"] = x.l_extendedprice * (1 - x.l_discount)
         x["ch"] = x.dp * (1 + x.l_tax)
-        g = x.groupby(["l_returnflag", "l_linestatus"])
+        g = x.groupby(["l_returnflag", "l_linestatus"], observed=True)
         r = g.agg(sum_qty=("l_quantity", "sum"), sum_base_price=("l_extendedprice", "sum"), sum_disc_price=("dp", "sum"),
                   sum_charge=("ch", "sum"), avg_qty=("l_quantity", "mean"), avg_price=("l_extendedprice", "mean"),
                   avg_disc=("l_discount", "mean"), count_order=("l_quantity", "size")).reset_index()
@@ -753,7 +764,7 @@ def reference(name: str, tables, **kw):
         end = d + 300 if d % 10000 < 1000 else d + 10000 - 900
         late = set(li[li.l_commitdate < li.l_receiptdate].l_orderkey)
         x = o[(o.o_orderdate >= d) & (o.o_orderdate < end) & o.o_orderkey.isin(late)]
-        return x.groupby("o_orderpriority").size().rename("order_count").reset_index().to_dict("records")
+        return x.groupby("o_orderpriority", observed=True).size().rename("order_count").reset_index().to_dict("records")
     if name == "q06":
         d, disc, q = kw.get("date", 19940101), kw.get("discount", 0.06), kw.get("quantity", 24)
         x = li[(li.l_shipdate >= d) & (li.l_shipdate < d + 10000) & (li.l_discount >= disc - 0.01 - 1e-9) &
@@ -765,10 +776,11 @@ def reference(name: str, tables, **kw):
                (li.l_receiptdate >= d) & (li.l_receiptdate < d + 10000)].merge(o, left_on="l_orderkey", right_on="o_orderkey")
         hi = x.o_orderpriority.isin(["1-URGENT", "2-HIGH"])
         x = x.assign(h=hi.astype(int), lo=(~hi).astype(int))
-        r = x.groupby("l_shipmode").agg(high_line_count=("h", "sum"), low_line_count=("lo", "sum")).reset_index()
+        r = x.groupby("l_shipmode", observed=True).agg(high_line_count=("h", "sum"),
+                                                       low_line_count=("lo", "sum")).reset_index()
         return r.to_dict("records")
     if name == "q13":
-        oo = o[~o.o_comment.str.match(".*special.*requests.*")]
+        oo = o[~np.asarray(o.o_comment.str.match(".*special.*requests.*"), dtype=bool)]
         cnt = oo.groupby("o_custkey").size()
         per = c.c_custkey.map(cnt).fillna(0).astype(int)
         r = per.value_counts().rename_axis("c_count").rename("custdist").reset_index()

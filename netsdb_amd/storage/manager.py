@@ -10,15 +10,26 @@ policy and CompareLocalitySets, LocalitySet.h:158-210 locality / replacement / d
 set has a locality type (``LOCALITY``): model weights reused every step, job inputs/outputs, shuffle
 data, hash-partition spools and temp data. Within a set the replacement policy picks the candidate —
 LRU for reused sets, MRU for sequential one-pass data (a spool page just written is the one read last).
-Across sets the victim is the candidate with the lowest eviction cost per byte
+Across sets the victim is the candidate with the lowest eviction cost per byte freed
 
-    cost = write_cost + reuse_prob * read_cost,    reuse_prob = prior(locality) / (1 + distance / n)
+    cost = (write_cost + reuse_prob * read_cost) / min(bytes, need),  reuse_prob = prior(locality) / (1 + distance / n)
 
-(write_cost: moving the page out, 1 per byte for every tier; read_cost: bringing it back if it is reused,
-1 per byte; distance: accesses since the candidate was last touched — the reference's reference distance —
-normalised by the number of resident objects n). A spool-heavy job under a tight budget thus spills its own
-spool pages before it touches an FF weight panel that every step re-reads, which a single global LRU would
-evict first because the panel was touched longest ago.
+in microseconds (reference LocalitySet::writeCost / readCost, PageCache.h:345-368):
+
+  * write_cost: moving the object out. 0 for a CLEAN object — a page whose serialised image is already in the
+    page pool / page file (loaded from it or persisted since its last change), or a "model" panel unchanged
+    since it was persisted: eviction just drops it. A dirty object pays its tier: an async D2H copy into the
+    pinned host tier when the tier admits it (~25 GB/s + 10 us), else serialisation into the native page pool
+    (~3 GB/s + 50 us, and the pool writes it to the page file).
+  * read_cost: bringing it back if it is reused, from the tier it will sit in (pinned: H2D ~25 GB/s; pool or
+    page file: ~3 GB/s + deserialisation), so a 64 MiB panel costs ~16000x a 4 KiB spool page to reload.
+  * per-set multipliers (``StorageManager.set_costs``, LocalitySet::setWriteCost / setReadCost) scale both;
+    distance is the number of accesses since the candidate was last touched (the reference distance),
+    normalised by the number n of resident objects.
+
+A spool-heavy job under a tight budget thus spills its own spool pages before it touches an FF weight panel
+that every step re-reads (which a single global LRU would evict first because it was touched longest ago),
+and among equally old objects a clean one goes before a dirty one.
 """
 from __future__ import annotations
 
@@ -35,6 +46,10 @@ from .. import _ext
 from .sets import DenseMatrixSet, Page, UserSet
 
 DEFAULT_PAGE_SIZE = 64 << 20
+
+# eviction tiers: bytes per microsecond and fixed microseconds per transfer (module doc)
+TIER_BW = {"pinned": 25e3, "pool": 3e3}
+TIER_T0 = {"pinned": 10.0, "pool": 50.0}
 
 # locality type -> (reuse prior, replacement policy within the set)
 LOCALITY = {
@@ -162,6 +177,14 @@ class StorageManager:
             p.release_regions()
             p.batch = None          # the region returns once no held batch views it any more
 
+    def set_costs(self, db: str, name: str, write_cost: Optional[float] = None, read_cost: Optional[float] = None):
+        """Per-set multipliers of the write / read cost (LocalitySet::setWriteCost / setReadCost)."""
+        st = self.get_set(db, name)
+        if write_cost is not None:
+            st.write_cost = float(write_cost)
+        if read_cost is not None:
+            st.read_cost = float(read_cost)
+
     # ----------------------------------------------------------- memory accounting / eviction
     def on_home(self, device) -> bool:
         """True when ``device`` is the budgeted device tier of this node."""
@@ -176,32 +199,38 @@ class StorageManager:
     def _set_of(obj):
         return obj if isinstance(obj, DenseMatrixSet) else obj.set
 
+    # The resident-set dicts are shared by every job lane (concurrent server requests): track / untrack / touch
+    # and the victim scan all hold self.lock (an RLock, re-entered by evict -> untrack).
     def track(self, obj):
         """``obj`` (a page or dense set) is resident on the device tier: most recently used."""
-        obj.last_use = next(self._clock)
-        s = self._set_of(obj)
-        ent = self._resident.get(id(s))
-        if ent is None:
-            ent = self._resident[id(s)] = (s, OrderedDict())
-        ent[1][id(obj)] = obj
-        ent[1].move_to_end(id(obj))
+        with self.lock:
+            obj.last_use = next(self._clock)
+            s = self._set_of(obj)
+            ent = self._resident.get(id(s))
+            if ent is None:
+                ent = self._resident[id(s)] = (s, OrderedDict())
+            ent[1][id(obj)] = obj
+            ent[1].move_to_end(id(obj))
 
     def untrack(self, obj):
-        s = self._set_of(obj)
-        ent = self._resident.get(id(s))
-        if ent is not None:
-            ent[1].pop(id(obj), None)
-            if not ent[1]:
-                del self._resident[id(s)]
+        with self.lock:
+            s = self._set_of(obj)
+            ent = self._resident.get(id(s))
+            if ent is not None:
+                ent[1].pop(id(obj), None)
+                if not ent[1]:
+                    del self._resident[id(s)]
 
     def resident_objects(self) -> int:
-        return sum(len(od) for _, od in self._resident.values())
+        with self.lock:
+            return sum(len(od) for _, od in self._resident.values())
 
     def account(self, page: Page):
-        page.last_use = next(self._clock)
-        if page.location == "device":
-            self.track(page)
-            self.account_bytes(page.nbytes, self.home, keep=page)
+        with self.lock:
+            page.last_use = next(self._clock)
+            if page.location == "device":
+                self.track(page)
+                self.account_bytes(page.nbytes, self.home, keep=page)
 
     def account_bytes(self, nbytes: int, device=None, keep=None):
         """Charge ``nbytes`` on ``device``; over budget, spill LRU pages / dense panels (never ``keep``)."""
@@ -222,10 +251,11 @@ class StorageManager:
         return max(0, self.device_budget - self.device_bytes)
 
     def touch(self, page):
-        page.last_use = next(self._clock)
-        ent = self._resident.get(id(self._set_of(page)))
-        if ent is not None and id(page) in ent[1]:
-            ent[1].move_to_end(id(page))
+        with self.lock:
+            page.last_use = next(self._clock)
+            ent = self._resident.get(id(self._set_of(page)))
+            if ent is not None and id(page) in ent[1]:
+                ent[1].move_to_end(id(page))
 
     @staticmethod
     def _resident_on_device(p) -> bool:
@@ -245,18 +275,45 @@ class StorageManager:
             return p
         return None
 
-    def evict_cost(self, s, p) -> float:
-        """Eviction cost per byte of candidate ``p`` of locality set ``s`` (module doc)."""
+    @staticmethod
+    def is_clean(p) -> bool:
+        """Evicting ``p`` needs no write: its image is already persisted (module doc)."""
+        if isinstance(p, DenseMatrixSet):
+            return p.is_clean()
+        return not p.dirty
+
+    def _spill_tier(self, p) -> str:
+        """Where a dirty ``p`` goes when evicted now: the pinned host tier if it admits the bytes, else the pool."""
+        tier = self.host_tier
+        if tier is not None and self.home.type == "cuda" and tier.used + self._nbytes(p) <= tier.budget:
+            return "pinned"
+        return "pool"
+
+    def write_cost(self, s, p) -> float:
+        """Microseconds to move ``p`` out of the device tier (0 when clean), times the set's multiplier."""
+        if self.is_clean(p):
+            return 0.0
+        t = self._spill_tier(p)
+        return (self._nbytes(p) / TIER_BW[t] + TIER_T0[t]) * getattr(s, "write_cost", 1.0)
+
+    def read_cost(self, s, p) -> float:
+        """Microseconds to bring ``p`` back from where eviction puts it, times the set's multiplier."""
+        t = "pool" if self.is_clean(p) else self._spill_tier(p)
+        return (self._nbytes(p) / TIER_BW[t] + TIER_T0[t]) * getattr(s, "read_cost", 1.0)
+
+    def evict_cost(self, s, p, need: Optional[int] = None) -> float:
+        """Eviction cost per byte freed of candidate ``p`` of locality set ``s`` (module doc)."""
         prior = LOCALITY.get(getattr(s, "locality", "job"), LOCALITY["job"])[0]
         n = max(1, self.resident_objects())
         distance = max(0, self._clock_now() - p.last_use)
         reuse_prob = prior / (1.0 + distance / n)
-        return 1.0 + reuse_prob * 1.0
+        freed = self._nbytes(p) if need is None else max(1, min(self._nbytes(p), need))
+        return (self.write_cost(s, p) + reuse_prob * self.read_cost(s, p)) / freed
 
     def _clock_now(self) -> int:
         return getattr(self, "_last_clock", 0)
 
-    def _pick_victim(self, keep, skip: set):
+    def _pick_victim(self, keep, skip: set, need: Optional[int] = None):
         if self.eviction_policy == "lru":
             best = None
             for s, od in self._resident.values():
@@ -272,7 +329,7 @@ class StorageManager:
             p = self._candidate(s, od, keep, skip)
             if p is None:
                 continue
-            c = self.evict_cost(s, p)
+            c = self.evict_cost(s, p, need)
             if best is None or c < best_cost or (c == best_cost and p.last_use < best.last_use):
                 best, best_cost = p, c
         return best
@@ -280,11 +337,15 @@ class StorageManager:
     def evict(self, need: int, keep=None) -> int:
         """Spill device pages (to the pinned tier / page pool) and dense panels (in block-row slabs,
         PageCache/PDBEvictWork style) until ``need`` bytes are free: victims by per-locality-set cost."""
+        with self.lock:
+            return self._evict(need, keep)
+
+    def _evict(self, need: int, keep=None) -> int:
         freed = 0
         skip = set()                 # objects that could not be spilled this round
         self._last_clock = next(self._clock)
         while freed < need:
-            p = self._pick_victim(keep, skip)
+            p = self._pick_victim(keep, skip, need - freed)
             if p is None:
                 break
             if not self._resident_on_device(p):
@@ -353,4 +414,4 @@ class StorageManager:
         }
 
 
-__all__ = ["StorageManager", "DEFAULT_PAGE_SIZE", "LOCALITY"]
+__all__ = ["StorageManager", "DEFAULT_PAGE_SIZE", "LOCALITY", "TIER_BW", "TIER_T0"]

@@ -68,6 +68,12 @@ class Page:
         native page pool (LRU -> disk) and drop the in-memory batch."""
         if self.batch is None or self.pins > 0:
             return 0
+        if self.location == "device" and not self.dirty:
+            # clean: the page's serialised image is already in the pool / page file (write cost 0) -> just drop it
+            self.release_regions()
+            self.batch = None
+            self.location = "pool"
+            return self.nbytes
         tier = getattr(self.set.manager, "host_tier", None)
         if self.location == "device" and tier is not None and tier.admit(self.nbytes):
             self.batch, self.event = tier.offload(self.batch, self.nbytes)
@@ -412,10 +418,25 @@ class DenseMatrixSet(UserSet):
         # persisted chunks use this set's id): the page file offset is page_no * page_size, so the slabs must
         # not sit at large page numbers of the set's own file
         self._spill_id: Optional[int] = None
+        self._clean_key = None                        # (panel id, version) persisted by persist_pages
+        self._clean_geo = None                        # geometry of a clean panel dropped by eviction
 
     # residency -------------------------------------------------------
+    def is_clean(self) -> bool:
+        """A "model" panel (read-only weights by contract) unchanged since persist_pages wrote its image: evicting
+        it needs no write (storage/manager.py cost model); its version counter catches in-place tensor writes."""
+        t = self._panel
+        return (t is not None and getattr(self, "locality", "job") == "model" and self._clean_key is not None
+                and self._clean_key == (id(t), t._version))
+
     @property
     def panel(self) -> Optional[torch.Tensor]:
+        if self._panel is None and self._clean_geo is not None:
+            geo, self._clean_geo = self._clean_geo, None
+            self.restore(geo)                          # clean drop: rebuild from the persisted chunks
+            self.stats_io["reloads"] += 1
+            if self._panel is not None:                # restored from the persisted image: clean again
+                self._clean_key = (id(self._panel), self._panel._version)
         if self._panel is None and self._spilled is not None:
             self.reload()
         if self._panel is not None:
@@ -448,13 +469,13 @@ class DenseMatrixSet(UserSet):
         return self._panel is not None
 
     def is_spilled(self) -> bool:
-        return self._spilled is not None
+        return self._spilled is not None or self._clean_geo is not None
 
     def resident_on_home(self) -> bool:
         return self._panel is not None and self._charged > 0
 
     def has_data(self) -> bool:
-        return self._panel is not None or self._spilled is not None
+        return self._panel is not None or self._spilled is not None or self._clean_geo is not None
 
     def panel_nbytes(self) -> int:
         if self._panel is not None:
@@ -484,6 +505,15 @@ class DenseMatrixSet(UserSet):
         t = self._panel
         if t is None or self.pins > 0:
             return 0
+        if self.is_clean():
+            # write cost 0: the image persisted by persist_pages is current -> drop, restore on next access
+            self._clean_geo = self.geometry()
+            freed = self._charged
+            self._charged = 0
+            self._panel = None
+            self._clean_key = None
+            self.stats_io["spills"] += 1
+            return freed
         tier = getattr(self.manager, "host_tier", None)
         rows, ld = t.shape
         es = t.element_size()
@@ -564,6 +594,8 @@ class DenseMatrixSet(UserSet):
     def load_rows(self, r0: int, r1: int, device=None) -> torch.Tensor:
         """Rows [r0, r1) of the panel on ``device`` (a view when resident, else assembled from the spilled
         slabs without reloading the rest): the out-of-core block GEMM's operand slabs."""
+        if self._panel is None and self._clean_geo is not None:
+            self.panel                                   # noqa: B018  (restore the dropped clean panel)
         if self._panel is not None:
             v = self._panel[r0:r1]
             return v if device is None or v.device == torch.device(device) else v.to(device)
@@ -595,6 +627,8 @@ class DenseMatrixSet(UserSet):
     def release_storage(self):
         """Return the panel's device bytes and spilled slabs (set removed or cleared)."""
         self._drop_spilled()
+        self._clean_geo = None
+        self._clean_key = None
         if self._charged:
             self.manager.release_bytes(self._charged, self.manager.home)
         self._charged = 0
@@ -776,6 +810,8 @@ class DenseMatrixSet(UserSet):
             bm.unpin(self.set_id, page, True, len(chunk))
             page += 1
         self.flushed_chunks = page
+        t = self._panel
+        self._clean_key = (id(t), t._version) if t is not None else None
 
     def geometry(self) -> dict:
         return {"total_rows": self.total_rows, "total_cols": self.total_cols, "block_rows": self.block_rows,

@@ -1,0 +1,116 @@
+"""TPC-H throughput on one MI355X: Q01, Q03, Q06, Q12, Q13 (+ optional others) at SF 1 and SF 10, through the
+engine on device-resident sets, each result checked against the pandas oracle on the same generated data.
+
+Reference: src/tpch/source/tpchDataLoader.cc (load), src/tpchBench + src/tpch/headers/Query*.h (queries).
+Data: models/tpch_gen.generate_fast (dbgen cardinalities and domains, vectorised; not byte-identical to dbgen).
+Timing: each query is run once untimed (plan compile, allocator warm-up), then ``--rounds`` times, each a full
+query including its result read-back, bracketed by torch.cuda.synchronize(); the median is reported.
+
+    python scripts/bench_tpch.py [--sf 1,10] [--queries q01,q03,q06,q12,q13] [--rounds 3] [--json out.json]
+"""
+import argparse
+import json
+import math
+import os
+import statistics
+import sys
+import tempfile
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from netsdb_amd.client import PDBClient  # noqa: E402
+from netsdb_amd.models import tpch, tpch_gen  # noqa: E402
+
+NEEDS = {"q01": ["lineitem"], "q03": ["customer", "orders", "lineitem"], "q04": ["orders", "lineitem"],
+         "q06": ["lineitem"], "q12": ["orders", "lineitem"], "q13": ["customer", "orders"],
+         "q14": ["lineitem", "part"], "q22": ["customer", "orders"]}
+
+
+def _close(got, ref):
+    if isinstance(ref, float):
+        return math.isclose(got, ref, rel_tol=1e-9, abs_tol=1e-6)
+    if len(got) != len(ref):
+        return False
+    for g, r in zip(got, ref):
+        for k, v in r.items():
+            if isinstance(v, float):
+                if not math.isclose(g[k], v, rel_tol=1e-9, abs_tol=1e-6):
+                    return False
+            elif g[k] != v:
+                return False
+    return True
+
+
+def _ref_sorted(q, ref):
+    if isinstance(ref, float) or q in ("q03", "q13"):
+        return ref
+    if q == "q01":
+        return sorted(ref, key=lambda x: (x["l_returnflag"], x["l_linestatus"]))
+    key = list(ref[0])[0]
+    return sorted(ref, key=lambda x: x[key])
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sf", default="1,10")
+    ap.add_argument("--queries", default="q01,q03,q06,q12,q13")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    queries = a.queries.split(",")
+    out = {"device": torch.cuda.get_device_name(0), "rounds": a.rounds, "results": []}
+    for sf in (float(x) for x in a.sf.split(",")):
+        t0 = time.perf_counter()
+        tables = tpch_gen.generate_fast(sf, seed=1)
+        t_gen = time.perf_counter() - t0
+        c = PDBClient(root=tempfile.mkdtemp(prefix="tpch_bench_"), device=dev)
+        need = sorted({t for q in queries for t in NEEDS.get(q, tpch.TABLES)})
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        tpch.load(c, "tpch", tables, only=need, device=dev)
+        torch.cuda.synchronize()
+        t_load = time.perf_counter() - t0
+        nli = len(tables["lineitem"]["l_orderkey"])
+        frames = None if a.no_check else tpch.frames(tables)
+        print(json.dumps({"sf": sf, "lineitem_rows": nli, "gen_s": round(t_gen, 2), "load_s": round(t_load, 2)}),
+              flush=True)
+        for q in queries:
+            fn = tpch.QUERIES[q]
+            got = fn(c, "tpch")                       # untimed first run
+            ts = []
+            for _ in range(a.rounds):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                got = fn(c, "tpch")
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t0)
+            ok = None
+            if frames is not None:
+                t0 = time.perf_counter()
+                ref = _ref_sorted(q, tpch.reference(q, tables, f=frames))
+                t_ref = time.perf_counter() - t0
+                ok = _close(got, ref)
+            med = statistics.median(ts)
+            row = {"sf": sf, "query": q, "ms_median": round(med * 1e3, 2), "ms_min": round(min(ts) * 1e3, 2),
+                   "lineitem_rows_per_s": round(nli / med, 1), "check_vs_pandas": ok,
+                   "pandas_s": None if frames is None else round(t_ref, 2)}
+            out["results"].append(row)
+            print(json.dumps(row), flush=True)
+            if ok is False:
+                print(json.dumps({"mismatch": q, "got": str(got)[:400], "ref": str(ref)[:400]}), flush=True)
+        del c, tables, frames
+        torch.cuda.empty_cache()
+    if a.json:
+        os.makedirs(os.path.dirname(a.json) or ".", exist_ok=True)
+        with open(a.json, "w") as f:
+            json.dump(out, f, indent=1)
+    if any(r["check_vs_pandas"] is False for r in out["results"]):
+        sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()

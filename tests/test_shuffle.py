@@ -182,3 +182,61 @@ def test_ooc_join_and_groupby_8_ranks_match_pandas():
     want = ref.assign(k=ref.okey % 90001).groupby("k").value.sum().to_dict()
     assert len(got) == agg.n == len(want)                     # every group on exactly one rank
     assert max(abs(got[k] - want[k]) for k in want) < 1e-9
+
+
+def _nested_scenario(ctx, out_dir):
+    """A partitioned in-memory join (its probe side streamed through one shuffle) feeding a distributed group-by
+    (a second shuffle), tiny chunks, skewed per-rank data: the downstream shuffle must not start rounds while
+    the upstream one still has rounds in flight (execution/shuffle.py deferred mode)."""
+    from netsdb_amd.client import PDBClient
+    from netsdb_amd.computations import ScanSet, WriteSet
+    from netsdb_amd.models.tpch import _EqJoin, _GroupBy
+    from tests.test_out_of_core import OocCust, OocOrder, _join_proj
+
+    c = PDBClient(ctx=ctx, root=tempfile.mkdtemp(), device="cpu", page_size=8 << 10, broadcast_threshold=0)
+    c.engine.shuffle_chunk_bytes = 4 << 10
+    c.create_database("db")
+    g = torch.Generator().manual_seed(100 + ctx.rank)
+    n_o = [0, 9000, 1500, 20000][ctx.rank % 4]                # skewed: one rank has no orders at all
+    n_c = [3000, 200, 0, 5000][ctx.rank % 4]
+    orders = RecordBatch({"okey": torch.arange(n_o) + 100000 * ctx.rank,
+                          "cust": torch.randint(0, 9000, (n_o,), generator=g),
+                          "amount": torch.rand(n_o, generator=g, dtype=torch.float64)}, n_o, OocOrder)
+    ck = torch.arange(ctx.rank, 9000, ctx.world_size)[: n_c]   # each customer key on exactly one rank
+    cust = RecordBatch({"ckey": ck, "region": ck % 13, "weight": torch.rand(ck.numel(), generator=g,
+                                                                              dtype=torch.float64)}, ck.numel(), OocCust)
+    for name, t, b in (("orders", OocOrder, orders), ("cust", OocCust, cust)):
+        c.create_set("db", name, t)
+        if b.n:
+            c.storage.get_set("db", name).add_batch(b)        # rank-local data (no dispatch): skewed sizes
+    c.create_set("db", "agg", None)
+    j = _EqJoin(2, [(0, "cust", 1, "ckey")], _join_proj)
+    j.set_input(0, ScanSet("db", "orders", OocOrder))
+    j.set_input(1, ScanSet("db", "cust", OocCust))
+    gb = _GroupBy(lambda b: b.columns["region"], lambda b: b.columns["value"],
+                  lambda k, v: RecordBatch({"k": k, "total": v}, k.numel()))
+    st = c.execute_computations(WriteSet("db", "agg").set_input(gb.set_input(j)), job_name="nested-shuffles")
+    tot = c.get_set_batches("db", "agg")
+    agg = RecordBatch.concat(tot) if tot else None
+    agg = None if agg is None else {"k": agg.columns["k"].tolist(), "total": agg.columns["total"].tolist()}
+    return {"agg": agg, "orders": orders, "cust": cust,
+            "shuffles": st.get("shuffles"), "deferred": c.engine.shuffle_stats.get("deferred", 0),
+            "rounds": c.engine.shuffle_stats.get("rounds", 0)}
+
+
+@pytest.mark.timeout(300)
+def test_nested_shuffles_join_then_groupby_4_ranks():
+    pd = pytest.importorskip("pandas")
+    res = _run("_nested_scenario", 4)
+    assert all(r["shuffles"] >= 1 for r in res)
+    assert all(r["deferred"] >= 1 for r in res)               # the upstream probe shuffle ran deferred
+    od = pd.concat([pd.DataFrame({k: r["orders"].columns[k].numpy() for k in ("okey", "cust", "amount")})
+                    for r in res])
+    cd = pd.concat([pd.DataFrame({k: r["cust"].columns[k].numpy() for k in ("ckey", "region", "weight")})
+                    for r in res])
+    ref = od.merge(cd, left_on="cust", right_on="ckey")
+    want = ref.assign(v=ref.amount * ref.weight).groupby("region").v.sum().to_dict()
+    ks = [k for r in res if r["agg"] is not None for k in r["agg"]["k"]]
+    got = dict(zip(ks, [t for r in res if r["agg"] is not None for t in r["agg"]["total"]]))
+    assert len(got) == len(ks) == len(want) > 0
+    assert max(abs(got[k] - want[k]) for k in want) < 1e-9
