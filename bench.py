@@ -75,48 +75,16 @@ def main():
                     help="untimed steps run before the W warmup steps until this much wall time has passed: "
                          "the chip's clock dips for ~10-20 ms after the GEMMs start and then settles "
                          "(profiles/r2_clock_settle); the timed window should see the settled clock")
-    ap.add_argument("--profile-json", default=None)
-    ap.add_argument("--overlap", choices=["none", "after", "before", "tail", "beside"], default="none",
-                    help="conv2d job on its own HIP stream, submitted after/before the FF jobs (independent inputs); "
-                         "tail: gated on the GPU to start when the first workgroup of the FF layer-1 GEMM finishes "
-                         "(fills the CUs that GEMM's tail leaves idle); beside: the layer-1 GEMM leaves "
-                         "--reserve-cus CUs free and the conv2d job runs on them next to it (start gate)")
-    ap.add_argument("--reserve-cus", type=int, default=16,
-                    help="--overlap beside: CUs the layer-1 GEMM leaves to the conv2d job (its grid)")
-    ap.add_argument("--job-priority", type=int, default=None,
-                    help="HIP stream priority of the conv2d job stream (default -1 = high; 0 in tail mode, where the "
-                         "FF jobs run on a high-priority stream instead)")
-    ap.add_argument("--graph", action="store_true",
-                    help="record one whole step (FF jobs + conv2d job) into a HIP graph after the warmup and time its "
-                         "replays (PDBClient.capture_job: no host work per step; the dropout seed of the recorded "
-                         "step is reused)")
+    ap.add_argument("--overlap", choices=["none", "after", "before"], default="none",
+                    help="conv2d job on its own HIP stream (PDBClient.submit_job), submitted after/before the FF jobs "
+                         "(independent inputs); default serial: no gain once the clocks have ramped (profiles/r1_overlap)")
     ap.add_argument("--two-job", action="store_true",
                     help="submit inference_unit as the reference's two jobs (output layer exp -> 'yo' set, then the row "
                          "normalise); default: ONE job, whose output layer is one GEMM with the max-subtracted softmax "
                          "in its epilogue (55-59 us vs 66-70 + 18 us in-bench, profiles/r3_s3/softmax)")
     ap.add_argument("--single-job", action="store_true", help=argparse.SUPPRESS)   # the default; kept for old scripts
-    ap.add_argument("--rownorm-loads", choices=["nt", "plain"], default=None,
-                    help="row-normalise row loads: non-temporal (library default) or cache-allocating")
-    ap.add_argument("--conv-kernel", choices=["rows", "rowfull", "warpspec"], default=None,
-                    help="conv2d row kernel: two-pass 2-waves/SIMD (rows), full-row 1-wave/SIMD with stores "
-                         "pipelined under the MFMAs (rowfull), or compute + store waves (warpspec); default: the "
-                         "library default")
-    ap.add_argument("--conv-blocks", type=int, default=None,
-                    help="conv2d row-kernel grid cap (default 512 persistent blocks; tail mode: 0 = one short block "
-                         "per row group, so the FF kernels after the GEMM are not held behind persistent conv blocks)")
-    ap.add_argument("--tail-prefetch", action="store_true",
-                    help="read the output layer's weight into the Infinity Cache during layer 1's tail "
-                         "(execution/streams.TailPrefetch; measured slower, off by default)")
-    ap.add_argument("--no-operand-prefetch", action="store_true",
-                    help="disable the in-kernel operand prefetch (the output layer's weight read into the Infinity "
-                         "Cache by the layer-1 GEMM's workgroups as they finish)")
-    ap.add_argument("--inflight", type=int, default=1,
-                    help="FF steps in flight: step i's FF jobs go to job lane i %% inflight (>1 pipelines "
-                         "consecutive batches: step i+1's layer-1 GEMM starts while step i's tail kernels run)")
     args = ap.parse_args()
     args.single_job = not args.two_job
-    if args.graph and (args.overlap != "none" or args.inflight > 1):
-        ap.error("--graph records the serial step (no --overlap / --inflight job streams)")
 
     from netsdb_amd.client import PDBClient
     from netsdb_amd.models import conv2d as cv
@@ -130,8 +98,6 @@ def main():
     root = tempfile.mkdtemp(prefix=f"nsdb_bench_r{ctx.rank}_")
     client = PDBClient(ctx=ctx, root=root, device=ctx.device)
     dev = ctx.device
-    client.engine.tail_prefetch = bool(args.tail_prefetch)
-    client.engine.operand_prefetch = not args.no_operand_prefetch
 
     # ---- data (per-rank partition of the inputs, replicated model) ----
     ff.load_model(client, "ff", cfg["batch"] * ctx.world_size, cfg["features"], cfg["hidden"], cfg["labels"],
@@ -140,62 +106,26 @@ def main():
     cv.load_images(client, "conv2d", "img", cfg["images"], cfg["channels"], cfg["height"], cfg["width"], seed=99)
     w, b = cv.random_kernel(cfg["filters"], cfg["channels"], cfg["ksize"], cfg["ksize"], seed=7, device=dev)
     local_rows = client.storage.get_set("ff", "inputs").local_rows
-    inflight = max(1, args.inflight)
-    conv_lane = inflight if inflight > 1 else 0
-    client.job_lanes = conv_lane + 1
-    tail = args.overlap == "tail"
-    prio = args.job_priority if args.job_priority is not None else (0 if tail else -1)
-    client.job_lane_priority = {conv_lane: prio}
-    conv_blocks = args.conv_blocks if args.conv_blocks is not None else (0 if tail else None)
-    # kernel launch options: a per-call scope for this (the only) host thread; the library keeps no global state
-    from netsdb_amd import ops
-
-    kscope = ops.kernel_options(
-        conv_blocks=conv_blocks,
-        conv_kernel=None if args.conv_kernel is None else {"rows": 0, "rowfull": 1, "warpspec": 5}[args.conv_kernel],
-        rownorm_plain_loads=None if args.rownorm_loads is None else args.rownorm_loads == "plain")
-    kscope.__enter__()
-    main_stream = None
-    if tail and dev.type == "cuda":
-        # FF jobs on a high-priority stream: when conv blocks and the FF tail kernels both wait for CUs, the
-        # dispatcher takes the FF kernels' workgroups first
-        main_stream = torch.cuda.Stream(dev, priority=-1)
-        main_stream.wait_stream(torch.cuda.current_stream(dev))
-        torch.cuda.set_stream(main_stream)
-
-    beside = args.overlap == "beside"
+    client.job_lanes = 1
+    client.job_lane_priority = {0: -1}
 
     def conv():
-        if beside:
-            # persistent conv blocks sized to the CUs the layer-1 GEMM leaves free
-            with ops.kernel_options(conv_blocks=args.reserve_cus):
-                cv.conv2d_memfuse_inference(client, "conv2d", "img", "conv_out", w, b)
-        else:
-            cv.conv2d_memfuse_inference(client, "conv2d", "img", "conv_out", w, b)
+        cv.conv2d_memfuse_inference(client, "conv2d", "img", "conv_out", w, b)
 
     def ffjobs(i):
         ff.inference_unit(client, "ff", "w1", "wo", "inputs", "b1", "bo", "output", dropout_rate=args.dropout,
                           seed=i, single_job=args.single_job)
 
     def step(i):
-        trig = client.arm_tail_trigger() if args.overlap == "tail" else \
-            client.arm_start_gate(args.reserve_cus) if beside else None
         if args.overlap == "before":
-            client.submit_job(conv, lane=conv_lane, independent=True)
-        if inflight > 1:
-            # batches are independent (own inputs/outputs; weights read-only and materialised in warmup)
-            client.submit_job(ffjobs, i, lane=i % inflight, independent=True)
-        else:
-            ffjobs(i)
+            client.submit_job(conv, independent=True)
+        ffjobs(i)
         if args.overlap == "none":
             conv()
         elif args.overlap == "after":
-            client.submit_job(conv, lane=conv_lane, independent=True)
-        elif args.overlap in ("tail", "beside"):
-            client.submit_job(conv, lane=conv_lane, independent=True, start_on=trig)
-        if args.overlap != "none" and inflight == 1:
+            client.submit_job(conv, independent=True)
+        if args.overlap != "none":
             client.wait_jobs()   # the step ends when both jobs have (stream-ordered join)
-
 
     def sync():
         if dev.type == "cuda":
@@ -224,19 +154,10 @@ def main():
         step(i)
     client.wait_jobs()
     sync()
-    captured = None
-    if args.graph and dev.type == "cuda":
-        captured = client.capture_job(step, args.warmup, inputs=[("ff", "inputs"), ("conv2d", "img")])
-        for _ in range(3):
-            captured.replay()
-        sync()
     coll0 = ctx.stats.get("collectives", 0)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        if captured is not None:
-            captured.replay()
-        else:
-            step(args.warmup + i)
+        step(args.warmup + i)
     client.wait_jobs()
     sync()
     dt = time.perf_counter() - t0
@@ -272,12 +193,8 @@ def main():
                 "check": check,
                 "settle_steps_untimed": settle_steps,
                 "conv_overlap": args.overlap,
-                "ff_steps_in_flight": inflight,
                 "collectives_per_step": round(coll_per_step, 2),
-                "graph_replay": captured is not None,
                 "single_job": bool(args.single_job),
-                "tail_prefetch": bool(args.tail_prefetch),
-                "operand_prefetch": not args.no_operand_prefetch,
             },
         }
         print(json.dumps(res), flush=True)

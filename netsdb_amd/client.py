@@ -51,6 +51,7 @@ class PDBClient:
         self.tracer = Tracer(enabled=trace, rank=self.ctx.rank)
         self.storage = StorageManager(root=root, device=self.device, page_size=page_size, pool_pages=pool_pages,
                                       rank=self.ctx.rank, device_budget=device_budget, pinned_budget=pinned_budget)
+        self.storage.world_size = self.ctx.world_size
         self.catalog = Catalog(catalog_path or os.path.join(self.storage.root, f"catalog_r{self.ctx.rank}.db"))
         self._engine = QueryEngine(self.storage, self.ctx, self.catalog, self.tracer, broadcast_threshold, fusion)
         self._lane = threading.local()    # per-thread job lane (server requests running concurrently)
@@ -63,8 +64,6 @@ class PDBClient:
         self.job_stream_priority = 0
         self.job_lanes = 2               # job streams (in-order job queues) created on first submit_job
         self.job_lane_priority = {}      # lane -> HIP stream priority (default job_stream_priority)
-        self.tail_trigger = None         # TailTrigger (arm_tail_trigger)
-        self.start_gate = None           # TailTrigger in start mode (arm_start_gate)
         if resume:
             self._resume()
 
@@ -499,29 +498,7 @@ class PDBClient:
 
         return CapturedJob(self, fn, *args, warmup=warmup, inputs=inputs, **kwargs)
 
-    def arm_tail_trigger(self):
-        """Arm the tail trigger of the next long GEMM this client enqueues; pass the returned trigger as
-        ``submit_job(..., start_on=trigger)`` to start an independent job in that GEMM's tail (see
-        :class:`~netsdb_amd.execution.streams.TailTrigger`)."""
-        if self.tail_trigger is None:
-            from .execution.streams import TailTrigger
-
-            self.tail_trigger = TailTrigger(self.device)
-        return self.tail_trigger.arm()
-
-    def arm_start_gate(self, reserve_cus: int = 16):
-        """Arm a START gate on the next long GEMM this client enqueues: that GEMM leaves ``reserve_cus`` CUs free,
-        and a job submitted with ``submit_job(..., start_on=gate)`` starts once the GEMM holds all of its CUs, so
-        it runs beside the GEMM on the reserved CUs (see :class:`~netsdb_amd.execution.streams.TailTrigger`).
-        Size the gated job's grid to the reserved CUs (e.g. ``ops.kernel_options(conv_blocks=reserve_cus)``)."""
-        g = self.start_gate
-        if g is None or g.reserve_cus != int(reserve_cus):
-            from .execution.streams import TailTrigger
-
-            g = self.start_gate = TailTrigger(self.device, mode="start", reserve_cus=reserve_cus)
-        return g.arm()
-
-    def submit_job(self, fn, *args, lane: int = 0, independent: bool = False, start_on=None, **kwargs):
+    def submit_job(self, fn, *args, lane: int = 0, independent: bool = False, **kwargs):
         """Run ``fn(*args, **kwargs)`` (any job-issuing callable, e.g. a model's inference entry point)
         with its kernels enqueued on a job stream, concurrently with work on the caller's stream.
         Returns a :class:`~netsdb_amd.execution.streams.JobHandle`; see that module for the ordering
@@ -531,7 +508,7 @@ class PDBClient:
 
             self.job_streams = JobStreams(self.device, lanes=self.job_lanes, priority=self.job_stream_priority,
                                           lane_priority=self.job_lane_priority)
-        return self.job_streams.submit(fn, *args, lane=lane, independent=independent, start_on=start_on, **kwargs)
+        return self.job_streams.submit(fn, *args, lane=lane, independent=independent, **kwargs)
 
     def wait_jobs(self):
         """The caller's stream waits (stream-ordered) for every submitted job."""

@@ -13,9 +13,8 @@
 
 extern "C" {
 int nsdb_gemm_splits(int M, int N, int K, int batch, int cfg);
-int nsdb_gemm_tail_eligible(int M, int N, int K, int batch, int splits, int cfg);
+int nsdb_gemm_prefetch_eligible(int M, int N, int K, int batch, int splits, int cfg);
 int nsdb_gemm_launch_wgs(int M, int N, int K, int batch, int splits, int cfg);
-int nsdb_stream_wait_value(hipStream_t stream, void* flag, unsigned value);
 int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const float* bias, int M, int N, int K,
                       long long lda, long long ldb, long long ldc, long long sA, long long sB, long long sC,
                       long long sBias, int batch, int splits, int act, int bias_mode, int out_f32, float alpha,
@@ -73,16 +72,13 @@ namespace {
 
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
-// Per-call launch options of the block GEMM (gemm.hip GemmOpts): a forced config or a tail trigger belongs to
-// the one call that passes it.
+// Per-call launch options of the block GEMM (gemm.hip GemmOpts): a forced config or an operand prefetch belongs
+// to the one call that passes it.
 struct GemmOpts {
   int cfg;
-  unsigned* signal;
-  unsigned signal_value;
   int epi;
   const void* pf_ptr;
   long long pf_bytes;
-  unsigned* start_signal;
 };
 
 void check_rc(int rc, const char* what) {
@@ -100,13 +96,12 @@ bool is_f32(const torch::Tensor& t, const char* name) {
 }
 
 // C = epi(alpha * A @ B^T); A [b?,M,K] bf16, B [b?,N,K] bf16 (row stride may exceed K), bias f32.
-// cfg: -1 auto, 0 (128x128 tile kernel), 2 (256x256 8-phase). signal: int32 device flag of a tail trigger that
-// this launch raises to signal_value (execution/streams.py TailTrigger; the caller checked gemm_tail_eligible).
+// cfg: -1 auto, 0 (128x128 tile kernel), 2 (256x256 8-phase). prefetch: a later kernel's operand that this
+// launch's workgroups read into the Infinity Cache as they finish (the caller checked gemm_prefetch_eligible).
 torch::Tensor gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Tensor> bias, int64_t bias_mode,
                       int64_t act, bool out_f32, double alpha, double dropout, int64_t seed, int64_t splits,
-                      c10::optional<torch::Tensor> out, bool accumulate, int64_t cfg,
-                      c10::optional<torch::Tensor> signal, int64_t signal_value, int64_t epi,
-                      c10::optional<torch::Tensor> prefetch, c10::optional<torch::Tensor> start_signal) {
+                      c10::optional<torch::Tensor> out, bool accumulate, int64_t cfg, int64_t epi,
+                      c10::optional<torch::Tensor> prefetch) {
   check_cuda(A, "A");
   check_cuda(B, "B");
   TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && B.scalar_type() == torch::kBFloat16, "A,B must be bf16");
@@ -158,19 +153,7 @@ torch::Tensor gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Ten
     wsp = ws.data_ptr<float>();
   }
   TORCH_CHECK(epi >= -1 && epi <= 1, "gemm_nt: epi must be -1 (auto), 0 (LDS-staged) or 1 (direct)");
-  GemmOpts o{(int)cfg, nullptr, 0u, (int)epi, nullptr, 0, nullptr};
-  if (start_signal.has_value() && start_signal->defined()) {
-    check_cuda(*start_signal, "start_signal");
-    TORCH_CHECK(start_signal->scalar_type() == torch::kInt32 && start_signal->numel() >= 1,
-                "start_signal must be an int32 flag");
-    o.start_signal = reinterpret_cast<unsigned*>(start_signal->data_ptr());
-  }
-  if (signal.has_value() && signal->defined()) {
-    check_cuda(*signal, "signal");
-    TORCH_CHECK(signal->scalar_type() == torch::kInt32 && signal->numel() >= 1, "signal must be an int32 flag");
-    o.signal = reinterpret_cast<unsigned*>(signal->data_ptr());
-    o.signal_value = (unsigned)signal_value;
-  }
+  GemmOpts o{(int)cfg, (int)epi, nullptr, 0};
   if (prefetch.has_value() && prefetch->defined() && prefetch->numel() > 0) {
     // the byte span of the tensor's elements (a strided view reads its whole span)
     check_cuda(*prefetch, "prefetch");
@@ -699,9 +682,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nt", &gemm_nt, "epi(alpha*A@B^T) on MFMA", py::arg("A"), py::arg("B"), py::arg("bias") = py::none(),
         py::arg("bias_mode") = 0, py::arg("act") = 0, py::arg("out_f32") = false, py::arg("alpha") = 1.0,
         py::arg("dropout") = 0.0, py::arg("seed") = 0, py::arg("splits") = 0, py::arg("out") = py::none(),
-        py::arg("accumulate") = false, py::arg("cfg") = -1, py::arg("signal") = py::none(),
-        py::arg("signal_value") = 0, py::arg("epi") = -1, py::arg("prefetch") = py::none(),
-        py::arg("start_signal") = py::none());
+        py::arg("accumulate") = false, py::arg("cfg") = -1, py::arg("epi") = -1, py::arg("prefetch") = py::none());
   m.def("gemm_launch_wgs", [](int64_t M, int64_t N, int64_t K, int64_t batch, int64_t splits, int64_t cfg) {
           return (int64_t)nsdb_gemm_launch_wgs((int)M, (int)N, (int)K, (int)batch, (int)splits, (int)cfg);
         }, "workgroups of the GEMM launch for this shape (splits <= 0: the launcher's choice)",
@@ -712,14 +693,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("B"), py::arg("alpha") = 1.0, py::arg("out") = py::none(), py::arg("accumulate") = false);
   m.def("gemm_splits", &gemm_splits, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("batch") = 1,
         py::arg("cfg") = -1);
-  m.def("gemm_tail_eligible", [](int64_t M, int64_t N, int64_t K, int64_t batch, int64_t splits, int64_t cfg) {
-          return (bool)nsdb_gemm_tail_eligible((int)M, (int)N, (int)K, (int)batch, (int)splits, (int)cfg);
-        }, "whether a launch of this shape raises a tail trigger passed to it (long, one-wave 8-phase GEMM)",
+  m.def("gemm_prefetch_eligible", [](int64_t M, int64_t N, int64_t K, int64_t batch, int64_t splits, int64_t cfg) {
+          return (bool)nsdb_gemm_prefetch_eligible((int)M, (int)N, (int)K, (int)batch, (int)splits, (int)cfg);
+        }, "whether a launch of this shape takes an operand prefetch passed to it (long, one-wave 8-phase GEMM)",
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("batch") = 1, py::arg("splits") = 0, py::arg("cfg") = -1);
-  m.def("stream_wait_value", [](torch::Tensor flag, int64_t value) {
-          TORCH_CHECK(flag.is_cuda() && flag.scalar_type() == torch::kInt32 && flag.numel() >= 1, "flag: int32 device tensor");
-          check_rc(nsdb_stream_wait_value(cur_stream(), flag.data_ptr(), (unsigned)value), "stream_wait_value");
-        }, "current stream waits on the GPU until flag >= value (unsigned)");
   m.def("gemm_nt_softmax", &gemm_nt_softmax, "softmax(alpha A.B^T + bias) fused into the GEMM epilogue",
         py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("bias_mode") = 0, py::arg("axis") = 1,
         py::arg("out") = py::none(), py::arg("alpha") = 1.0, py::arg("force_fallback") = false, py::arg("epi") = -1,

@@ -600,9 +600,6 @@ gemm_nt_tile_kernel(GemmParams p) {
 //  * EPI: 0 = the common epilogue (bias / activation / dropout / split-K slabs); 1 / 2 = fused max-subtracted
 //    softmax over the columns / rows of C (one instantiation each: both in one kernel pushed the epilogue
 //    past 256 VGPRs into scratch).
-//  * Tail trigger (per launch, GemmParams::signal): every workgroup raises *signal to signal_value when its
-//    main loop is done, so a job stream gated on it (hipStreamWaitValue32 >= value) starts in this GEMM's
-//    tail (execution/streams.py TailTrigger).
 //  Studies of this loop (diagnostic variants, K-tail stealing, adaptive split-K, in-launch fix-up, ring
 //  buffers, cache policies, the 4-wave structures) live in the separate study build (csrc/study).
 // ---------------------------------------------------------------------------------------------
@@ -753,12 +750,6 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   stage(1, 2, 1); stage(1, 0, 1); stage(1, 3, 1);
   asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   if constexpr (EPI != 0) reinterpret_cast<float*>(smem + SM_BIAS)[tid] = bias_v;   // [256 col | 256 row]
-  // start gate (per launch): a job gated on flag >= base + workgroups (hipStreamWaitValue32) is dispatched only
-  // once every workgroup of this launch holds its CU, so it can only take the CUs this launch leaves free. Issued
-  // after the prologue's wait: the in-order vmcnt retires it at the first k-tile's counted wait, not before the
-  // prologue's DMAs.
-  if (p.start_signal != nullptr && tid == 0)
-    __hip_atomic_fetch_add(p.start_signal, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   NSDB_BARRIER();
   if (wr == 1) NSDB_BARRIER();            // stagger the two wave groups by one barrier
   for (int it = 0; it < niter; ++it) {
@@ -767,8 +758,6 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   }
   if (wr == 0) NSDB_BARRIER();            // re-align the groups
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // trailing zero-fill DMAs land before LDS reuse
-  if (p.signal != nullptr && tid == 0)    // tail trigger: this CU frees up soon
-    __hip_atomic_fetch_max(p.signal, p.signal_value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if constexpr (EPI == 0) {
     // Operand prefetch (per launch, GemmParams::pf_ptr): the next kernel's operand (the FF output weight after
     // layer 1, whose 2.4 GB stream evicts it) is read into the Infinity Cache by this launch's workgroups as each
@@ -908,25 +897,17 @@ __global__ void __launch_bounds__(512) splitk_reduce_wide_kernel(GemmParams p) {
 }  // namespace nsdb
 
 // ---------------------------------------------------------------- host side
-// Every launch decision is a per-call parameter (GemmOpts): a forced config or a tail trigger applies to
+// Every launch decision is a per-call parameter (GemmOpts): a forced config or an operand prefetch applies to
 // exactly the call that passes it — no process-wide state, so lanes on other streams / threads are never
 // affected. The product build exports only the production configs; the study variants are in csrc/study.
 struct GemmOpts {
   int cfg;                  // -1 auto, 0 = 128x128 tile kernel, 2 = 256x256 8-phase kernel
-  unsigned* signal;         // tail trigger of this launch (8-phase only), or nullptr
-  unsigned signal_value;
   int epi;                  // 8-phase unsplit epilogue: -1 auto (direct), 0 LDS-staged, 1 direct register stores
   const void* pf_ptr;       // operand prefetch of this launch (8-phase only): pf_bytes at pf_ptr, or nullptr
   long long pf_bytes;
-  unsigned* start_signal;   // start gate of this launch (8-phase only): +1 per workgroup at its start, or nullptr
 };
 
 extern "C" {
-
-// Make `stream` wait (on the GPU command processor, no host involvement) until *flag >= value.
-int nsdb_stream_wait_value(hipStream_t stream, void* flag, unsigned value) {
-  return (int)hipStreamWaitValue32(stream, flag, value, hipStreamWaitValueGte, 0xffffffffu);
-}
 
 // Tile config: the 256x256 8-phase tile (1 block/CU) when both dims fill it and there is enough work.
 static int pick_cfg(int M, int N, int K, int batch) {
@@ -977,9 +958,9 @@ int nsdb_gemm_launch_wgs(int M, int N, int K, int batch, int splits, int cfg) {
   return ((M + tbm - 1) / tbm) * ((N + tbn - 1) / tbn) * s * batch;
 }
 
-// Would a launch of this shape take a tail trigger (an 8-phase launch of >= 128 workgroups with >= 64 k-tiles
-// per workgroup: a long, one-wave-resident GEMM whose tail leaves CUs idle)?
-int nsdb_gemm_tail_eligible(int M, int N, int K, int batch, int splits, int cfg) {
+// Would a launch of this shape take an operand prefetch (an 8-phase launch of >= 128 workgroups with >= 64
+// k-tiles per workgroup: a long, one-wave-resident GEMM whose finishing workgroups can warm the next operand)?
+int nsdb_gemm_prefetch_eligible(int M, int N, int K, int batch, int splits, int cfg) {
   if (resolve_cfg(cfg, M, N, K, batch) != 2) return 0;
   const int ksteps = (K + nsdb::BK - 1) / nsdb::BK;
   if (splits <= 0) splits = nsdb_gemm_splits(M, N, K, batch, cfg);    // the launcher's own choice
@@ -1070,11 +1051,6 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
                   ((p.splits == 1 && !accumulate && p.vec_c && p.bias_mode != 3) || (p.splits > 1 && p.vec_ws))) ? 1 : 0;
   dim3 grid(p.tiles_m * p.tiles_n * p.splits, 1, batch);
   if (cfg == 2) {
-    if (opts && opts->signal) {            // this launch's tail trigger (the caller checked eligibility)
-      p.signal = opts->signal;
-      p.signal_value = opts->signal_value;
-    }
-    if (opts && opts->start_signal) p.start_signal = opts->start_signal;   // this launch's start gate
     if (opts && opts->pf_ptr && opts->pf_bytes > 0) {   // this launch's operand prefetch
       p.pf_ptr = (const char*)opts->pf_ptr;
       p.pf_bytes = opts->pf_bytes;

@@ -42,14 +42,13 @@ struct GemmParams {
   int* sm_cnt;
   int* sm_flag;
   int* sm_dep = nullptr;     // fused softmax: departures (low 16 bits) + timed-out tiles (high 16) per group
-  unsigned* start_signal = nullptr;   // start gate (8-phase): every workgroup adds 1 when it starts (system scope)
+  unsigned* start_signal = nullptr;   // study build only (csrc/study): start-gate experiments
   const char* pf_ptr = nullptr;   // operand prefetch for the NEXT kernel (8-phase, EPI 0): bytes read into the
   long long pf_bytes = 0;         // Infinity Cache by the workgroups after their main loops
   unsigned long long* stamps;   // diagnostic variant 12: per-workgroup real-time stamps every 32 k-tiles
   struct AdaptState* adapt;     // split-K: launch-to-launch adaptive K partition (see AdaptState)
-  // tail trigger (8-phase kernel): every workgroup raises *signal to signal_value (atomic max) when its main
-  // loop is done, so a job stream gated on it (hipStreamWaitValue32 >= value) launches while this GEMM's
-  // tail leaves CUs idle (see nsdb_tail_trigger_arm)
+  // study build only (csrc/study, rejected in the product: profiles/r2_tail): a tail trigger raised by every
+  // workgroup when its main loop is done
   unsigned* signal;
   unsigned signal_value;
   // K-tail stealing (variant 19, split-K): per-tile claim counters (zero at launch; the split-K reducer re-zeroes

@@ -103,7 +103,8 @@ std::vector<torch::Tensor> hash_aggregate(torch::Tensor keys, c10::optional<torc
   auto meta = torch::empty({kMetaWords}, i64);
   auto glow = torch::empty({(gcap_low + 1) * (4 + F)}, i64);
   auto gpart = torch::empty({(gcap_part + 1) * (4 + F)}, i64);
-  auto out = torch::empty({n * (5 + F) + (want_inv ? n : 0)}, i64);
+  // [reps n | aggs n*F | cnt n | slot_of_gid n | first n | inv n] (relops.hip agg_launch_t AggOut)
+  auto out = torch::empty({n * (4 + F) + (want_inv ? n : 0)}, i64);
   const int64_t wbytes = nsdb_agg_work_bytes(n, F, pbits, want_inv ? 1 : 0);
   auto work = torch::empty({(wbytes + 7) / 8}, i64);
   rc_ok(nsdb_hash_aggregate(keys.data_ptr(), F ? v.data_ptr() : nullptr, n, F, vt, opc, want_inv ? 1 : 0,
@@ -121,8 +122,8 @@ std::vector<torch::Tensor> hash_aggregate(torch::Tensor keys, c10::optional<torc
   auto aggs = out.narrow(0, n, g * F).view({g, F});
   if (vt == 0) aggs = aggs.view(torch::kFloat64);
   auto cnt = out.narrow(0, n + n * F, g);
-  auto first = out.narrow(0, n * (4 + F), g);
-  torch::Tensor inv = want_inv ? out.narrow(0, n * (5 + F), n) : torch::empty({0}, i64);
+  auto first = out.narrow(0, n * (3 + F), g);
+  torch::Tensor inv = want_inv ? out.narrow(0, n * (4 + F), n) : torch::empty({0}, i64);
   // the views keep the whole n-row buffer alive: copy small results out of it
   if (g * 4 < n) {
     reps = reps.clone();

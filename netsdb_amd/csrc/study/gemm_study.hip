@@ -944,7 +944,6 @@ __global__ void __launch_bounds__(512) splitk_reduce_wide_kernel(GemmParams p) {
 // ---------------------------------------------------------------- host side
 extern "C" {
 
-int nsdb_study_gemm_w4a_launch(const nsdb::GemmParams* p, int batch, int v, hipStream_t stream);
 
 static int g_force_cfg = -1;  // -1 auto, 0 = 128x128, 1 = 256x256 2-stage, 2 = 256x256 8-phase (A/B testing)
 static int g_diag = 0;        // force_config / 100: kernel timing diagnostics (GemmParams::diag)
@@ -1184,12 +1183,7 @@ int nsdb_study_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, co
     hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<13>, grid, dim3(512), 0, stream, p);
   else if (cfg == 19)   // diagnostic: every workgroup cycles over 2 k-tiles (L2-resident operands)
     hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<14>, grid, dim3(512), 0, stream, p);
-  else if (cfg >= 30 && cfg <= 36 && K % nsdb::BK == 0) {   // asm-scheduled 4-wave kernel (gemm_w4a.hip)
-    const int rc = nsdb_study_gemm_w4a_launch(&p, batch, cfg - 30, stream);
-    if (rc != 0) return rc;
-  }
-  else if (cfg >= 30 && cfg <= 36)
-    hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<0>, grid, dim3(512), 0, stream, p);
+  // (cfg 30-36, the asm-scheduled 4-wave "w4a" kernel, was removed after profiles/r3_w4a: 1139 vs 1379 TF)
   else if (cfg == 11)   // K-tiled operands (caller passes [K/64][ld][64] panels, lda/ldb = padded rows)
     hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<9>, grid, dim3(512), 0, stream, p);
   else if (cfg >= 3 && cfg <= 9) {   // diagnostic variants of the 8-phase kernel (timing only)

@@ -1,5 +1,5 @@
 // PyTorch bindings of the GEMM STUDY build (module netsdb_amd._hip_study): the diagnostic / rejected
-// variants of the block GEMM (csrc/study/gemm_study.hip, gemm_w4a.hip), kept for A/B scripts; never loaded
+// variants of the block GEMM (csrc/study/gemm_study.hip), kept for A/B scripts; never loaded
 // by the product.
 // Every op checks device/dtype/shape on the host BEFORE launching (a bad shape must never reach
 // the GPU) and launches on the current HIP stream so ops compose with hipGraph capture.
@@ -151,7 +151,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out") = py::none(), py::arg("accumulate") = false);
   m.def("gemm_splits", &gemm_splits);
   m.def("gemm_force_config", [](int64_t cfg) { nsdb_study_gemm_force_config((int)cfg); },
-        "study config (-1 auto; 3-26 8-phase variants / w4 / w4r / steal / fix-up; 30-36 asm-scheduled w4a)");
+        "study config (-1 auto; 3-26 8-phase variants / w4 / w4r / steal / fix-up)");
   m.def("gemm_set_stamps", [](int64_t ptr) { nsdb_study_gemm_set_stamps(reinterpret_cast<void*>(ptr)); });
   m.def("gemm_set_adapt", [](int64_t on) { nsdb_study_gemm_set_adapt((int)on); });
   m.def("gemm_adapt_state", [](int64_t M, int64_t N, int64_t K) {

@@ -23,6 +23,7 @@ from ..objects.nested import NestedColumn
 from ..objects.record import PDBObject, RecordBatch, RecordView, batch_of, column_concat, column_take
 from ..objects.strings import StringColumn
 from ..parallel.comm import ClusterContext
+from ..storage.sets import DenseMatrixSet
 from ..query_planning.planner import AdaptivePlanner, PhysicalPlan, Planner
 from ..utils.trace import Tracer
 from . import kernels as K
@@ -117,10 +118,6 @@ class QueryEngine:
         # streaming shuffle (execution/shuffle.py): chunk size per round and cumulative round statistics
         self.shuffle_chunk_bytes = 64 << 20
         self.shuffle_stats = {}
-        # fused GEMM chains: read a later GEMM's stored weight into the Infinity Cache during the tail of the GEMM
-        # evaluated before it (query_planning/fusion.py MatmulNode._tail_prefetch). Off by default: measured
-        # slower in the bench (profiles/r3_s2: 1.021 vs 0.992 ms per step)
-        self.tail_prefetch = False
         # in-kernel operand prefetch: the weight of such a later GEMM is read into the Infinity Cache by the
         # workgroups of the long GEMM before it as they finish (ops.gemm_nt / gemm.hip GemmParams::pf_ptr)
         self.operand_prefetch = True
@@ -131,7 +128,7 @@ class QueryEngine:
         """An engine for another job lane: same storage, context, catalog, tracer, configuration and plan cache
         (dict access under the GIL); its own per-job state (spools, statistics)."""
         e = QueryEngine(self.storage, self.ctx, self.catalog, self.tracer, self.broadcast_threshold, self.fusion)
-        for k in ("adaptive", "plan_cache_enabled", "ooc_fraction", "shuffle_chunk_bytes", "tail_prefetch",
+        for k in ("adaptive", "plan_cache_enabled", "ooc_fraction", "shuffle_chunk_bytes",
                   "operand_prefetch"):
             setattr(e, k, getattr(self, k))
         e._plan_cache = self._plan_cache
@@ -523,6 +520,8 @@ class QueryEngine:
                 if not isinstance(v, RecordBatch):
                     v = RecordBatch({"value": v}, x.n)
                 uset.add_batch(v)
+            if self.ctx.distributed and isinstance(uset, DenseMatrixSet):
+                self._merge_dense_output(uset)
             return
         if kind == "join_build":
             a = sk["atom"]
@@ -549,6 +548,31 @@ class QueryEngine:
             self._partition(sk["atom"], batches, state)
             return
         raise ValueError(kind)
+
+    _DTYPES = (torch.float32, torch.bfloat16, torch.float16, torch.float64)
+
+    def _merge_dense_output(self, s):
+        """A dense matrix written block by block by an SPMD pipeline: every rank wrote the blocks it produced (a
+        disjoint share). Agree on the geometry, give ranks without blocks a zero panel, and sum the panels so
+        every rank holds the whole matrix (replicated), as a fused GEMM's output would be."""
+        from ..storage.sets import DenseMatrixSet  # noqa: F401
+
+        geo = [0] * 5
+        if s.has_data():
+            dt = s.panel.dtype
+            geo = [s.total_rows, s.total_cols, s.block_rows, s.block_cols,
+                   self._DTYPES.index(dt) + 1 if dt in self._DTYPES else 1]
+        rows = self.ctx.all_gather_ints(geo)
+        ref = next((r for r in rows if r[0] > 0), None)
+        if ref is None:
+            return
+        if not s.has_data():
+            s.define(ref[0], ref[1], ref[2], ref[3], dtype=self._DTYPES[ref[4] - 1])
+        panel = s.panel
+        if s.row_offset != 0 or s.local_rows != ref[0]:
+            raise RuntimeError(f"dense output {s.db}.{s.name}: a row-partitioned panel cannot be merged")
+        self.ctx.all_reduce(panel)
+        s.replicated = True
 
     def _collect(self, batches, tag: str):
         """Keep a tuple set in memory while it is small; past the out-of-core limit continue it in a
@@ -622,8 +646,15 @@ class QueryEngine:
             return
         op = getattr(comp, "reduce_op", "sum")
         combine = comp.combine
+        # a comp may reduce a whole group's values at once (group_values(values, inv, ngroups)), e.g.
+        # FFAggMatrixToOneMatrix assembling every block of a matrix into one
+        group_fn = getattr(comp, "group_values", None)
         kv = (RecordBatch({"k": x.columns[kcol], "v": x.columns[vcol]}, x.n) for x in batches if x is not None and x.n)
-        if not self.ctx.distributed:
+        if group_fn is not None:
+            if self.ctx.distributed:   # raw values travel to the key's owner; it reduces them whole
+                kv = self._stream_shuffle(kv, None, "aggregate", key=lambda b: K.hash_keys(b.columns["k"], b.device))
+            reps, agg = self._reduce_kv(kv, op, combine, group_fn)
+        elif not self.ctx.distributed:
             reps, agg = self._reduce_kv(kv, op, combine)
         else:
             # CombinerProcessor -> streaming shuffle by key hash -> AggregationProcessor: every chunk of (key,
@@ -659,7 +690,7 @@ class QueryEngine:
         out = comp.make_output(reps, agg)
         state.materialized[out_ts] = [RecordBatch({out_col: out}, out.n)]
 
-    def _reduce_kv(self, kv_batches, op, combine):
+    def _reduce_kv(self, kv_batches, op, combine, group_fn=None):
         """(key, value) batches -> (representative keys, aggregates). Streamed; past the out-of-core limit the
         pairs are hash-partitioned by key into spools and each partition is reduced alone (its groups are
         disjoint from every other partition's)."""
@@ -690,8 +721,11 @@ class QueryEngine:
                     continue
                 keys = column_concat([b.columns["k"] for b in bs])
                 vals = column_concat([b.columns["v"] for b in bs])
-                fused = K.group_reduce(keys, vals, op)   # device hash aggregation (relops.hip), or None
-                if fused is not None:
+                fused = None if group_fn is not None else K.group_reduce(keys, vals, op)   # relops.hip, or None
+                if group_fn is not None:
+                    inv, reps, g = K.group_ids(keys)
+                    agg = group_fn(vals, inv, g)
+                elif fused is not None:
                     reps, agg = fused
                 else:
                     inv, reps, g = K.group_ids(keys)

@@ -22,11 +22,12 @@ from typing import Optional
 import torch
 
 from .. import ops
-from ..computations import (AggregateComp, BiasAct, BlockMatmul, BlockSum, JoinComp, RowSoftmax, ScanSet,
-                            WriteSet)
-from ..lambdas import make_batch_lambda, make_lambda_from_method
-from ..objects.builtin import FFMatrixBlock
-from ..objects.record import RecordBatch
+from ..computations import (AggregateComp, BiasAct, BlockMatmul, BlockSum, JoinComp, MultiSelectionComp,
+                            PartitionComp, RowSoftmax, ScanSet, WriteSet)
+from ..lambdas import make_batch_lambda, make_lambda_from_method, make_lambda_from_self
+from ..objects.builtin import FFMatrixBlock, getter
+from ..objects.nested import NestedColumn
+from ..objects.record import PDBObject, RecordBatch, Tensor
 from . import blocks as B
 
 
@@ -215,6 +216,130 @@ class FFOutputLayer(JoinComp):
         return RowSoftmax()
 
 
+# ------------------------------------------------------------------------------------ helper UDFs
+class InferenceResult(PDBObject):
+    """One inference row: its global row index, its block row and the first two output scores
+    (src/FF/headers/InferenceResult.h; label = 1 if score0 > score1 else -1)."""
+
+    index: int
+    block_row_id: int
+    inference: Tensor()
+
+    getKey = getter("index")
+    getInference = getter("inference")
+
+    def getLabel(self):
+        return 1 if float(self.inference[0]) > float(self.inference[1]) else -1
+
+    getLabel.__vectorized__ = lambda b: torch.where(b.columns["inference"][:, 0] > b.columns["inference"][:, 1], 1, -1)
+
+
+class FFSingleMatrix(FFMatrixBlock):
+    """Every block of a matrix assembled into one (src/FF/headers/FFSingleMatrix.h: key 1 + the block)."""
+
+    key: int
+
+    def getKey(self):
+        return self.key
+
+    getKey.__vectorized__ = lambda b: b.columns["key"]
+
+
+class FFMatrixPartitioner(PartitionComp):
+    """Store FFMatrixBlocks hash-partitioned across nodes by block row index (src/FF/headers/
+    FFMatrixPartitioner.h; the ``enablePartition`` output writer of SimpleFF.cc inference)."""
+
+    def __init__(self, db: str = "", set_name: str = ""):
+        super().__init__(db, set_name)
+
+    def get_key_projection(self, blk):
+        return make_lambda_from_method(blk, "getBlockRowIndex")
+
+
+class InferenceResultPartition(PartitionComp):
+    """Store InferenceResults partitioned by their row index (src/FF/headers/InferenceResultPartition.h)."""
+
+    def __init__(self, db: str = "", set_name: str = ""):
+        super().__init__(db, set_name)
+
+    def get_key_projection(self, r):
+        return make_lambda_from_method(r, "getKey")
+
+
+class FFMatrixMultiSel(MultiSelectionComp):
+    """FFMatrixBlock -> one InferenceResult per row (index = blockRow * rowNums + i, the row's first two values;
+    src/FF/headers/FFMatrixMultiSel.h). Vectorised: one [rows, 2] slice of the stacked block data per batch."""
+
+    def get_selection(self, blk):
+        return make_batch_lambda(blk, lambda b: torch.ones(b.n, dtype=torch.bool, device=b.columns["data"].device))
+
+    def get_projection(self, blk):
+        def proj(b: RecordBatch):
+            d = b.columns["data"]
+            n, rows = b.n, d.shape[1]
+            dev = d.device
+            br = b.columns["block_row"].to(dev).long()
+            rn = b.columns["row_nums"].to(dev).long()
+            i = torch.arange(rows, device=dev)
+            res = RecordBatch({"index": (br * rn).unsqueeze(1).add(i).reshape(-1),
+                               "block_row_id": br.repeat_interleave(rows),
+                               "inference": d[:, :, :2].reshape(n * rows, -1).double()}, n * rows, InferenceResult)
+            return NestedColumn(torch.arange(n + 1, device=dev) * rows, res)
+
+        return make_batch_lambda(blk, proj, tag="ff_matrix_multisel")
+
+
+class FFAggMatrixToOneMatrix(AggregateComp):
+    """Merge every FFMatrixBlock into one FFSingleMatrix (key 1): each block lands at its (blockRow, blockCol)
+    position of the total_rows x total_cols matrix (src/FF/headers/FFAggMatrixToOneMatrix.h + the block-placing
+    FFMatrixBlock::operator+). Vectorised: the blocks of a group are scattered into the matrix in one indexed copy
+    (engine group_values hook), not merged pairwise."""
+
+    reduce_op = None
+
+    def get_key_projection(self, blk):
+        return make_batch_lambda(blk, lambda b: torch.ones(b.n, dtype=torch.int64, device=b.columns["data"].device))
+
+    def get_value_projection(self, blk):
+        return make_lambda_from_self(blk)
+
+    def group_values(self, values, inv, ngroups):
+        b = values if isinstance(values, RecordBatch) else RecordBatch.concat(values)
+        d = b.columns["data"]
+        dev = d.device
+        inv = inv.to(dev)
+        br, bc = d.shape[1], d.shape[2]
+        out = []
+        for g in range(ngroups):
+            sel = torch.nonzero(inv == g).flatten()
+            r = b.columns["block_row"].to(dev).index_select(0, sel)
+            c = b.columns["block_col"].to(dev).index_select(0, sel)
+            tr = int(b.columns["total_rows"][sel[0]])
+            tc = int(b.columns["total_cols"][sel[0]])
+            nbr, nbc = -(-tr // br), -(-tc // bc)
+            full = torch.zeros(nbr, nbc, br, bc, dtype=d.dtype, device=dev)
+            full[r, c] = d.index_select(0, sel)
+            out.append(full.permute(0, 2, 1, 3).reshape(nbr * br, nbc * bc)[:tr, :tc])
+        return out
+
+    def make_output(self, keys, values):
+        mats = values
+        n = len(mats)
+        dev = mats[0].device if n else None
+        R = max(m.shape[0] for m in mats) if n else 0
+        C = max(m.shape[1] for m in mats) if n else 0
+        data = torch.zeros(n, R, C, dtype=mats[0].dtype if n else torch.float32, device=dev)
+        for i, m in enumerate(mats):
+            data[i, : m.shape[0], : m.shape[1]] = m
+        rows = torch.tensor([m.shape[0] for m in mats], dtype=torch.int64, device=dev)
+        cols = torch.tensor([m.shape[1] for m in mats], dtype=torch.int64, device=dev)
+        blk = mk_blocks(0, 0, data, rows, cols, type_=FFSingleMatrix)
+        blk.columns["row_nums"], blk.columns["col_nums"] = rows, cols
+        blk.columns["key"] = keys.to(dev) if isinstance(keys, torch.Tensor) else torch.ones(n, dtype=torch.int64,
+                                                                                              device=dev)
+        return blk
+
+
 def FFMatrixBlockScanner(db: str, set_name: str):
     return ScanSet(db, set_name, FFMatrixBlock)
 
@@ -279,10 +404,19 @@ def inference_unit(client, db: str, w1: str, wo: str, inputs: str, b1: str, bo: 
 
 
 def inference(client, db: str, w1: str, w2: str, wo: str, inputs: str, b1: str, b2: str, bo: str, output: str,
-              dropout_rate: float = 0.0, seed: int = 0) -> dict:
-    """SimpleFF.cc inference / inference_compute: two hidden layers (y1, y2, yo) + softmax."""
-    for n in ("y1", "y2", "yo", output):
+              dropout_rate: float = 0.0, seed: int = 0, enable_partition: bool = False) -> dict:
+    """SimpleFF.cc inference / inference_compute: two hidden layers (y1, y2, yo) + softmax.
+
+    ``enable_partition`` (SimpleFF.cc:129-132,194-197): the hidden layers' outputs y1 / y2 are written by
+    :class:`FFMatrixPartitioner` — FFMatrixBlock records hash-partitioned across the nodes by block row — instead
+    of the dense FFMatrixWriter panels; the next layer reads them as block records (generic join path)."""
+    for n in ("yo", output) if enable_partition else ("y1", "y2", "yo", output):
         create_output_set(client, db, n)
+    if enable_partition:
+        for n in ("y1", "y2"):
+            if client.storage.has_set(db, n):
+                client.remove_set(db, n)
+            client.create_set(db, n, FFMatrixBlock)
     t0 = time.perf_counter()
     stats = []
 
@@ -294,7 +428,8 @@ def inference(client, db: str, w1: str, w2: str, wo: str, inputs: str, b1: str, 
         bj = FFTransposeBiasSum() if last else FFReluBiasSum(dropout_rate, seed)
         bj.set_input(0, a)
         bj.set_input(1, FFMatrixBlockScanner(db, b))
-        stats.append(client.execute_computations(FFMatrixWriter(db, out).set_input(bj), job_name=f"inference-{out}"))
+        writer = FFMatrixPartitioner(db, out) if (enable_partition and not last) else FFMatrixWriter(db, out)
+        stats.append(client.execute_computations(writer.set_input(bj), job_name=f"inference-{out}"))
 
     layer(w1, inputs, b1, "y1", True, False)
     layer(w2, "y1", b2, "y2", False, False)
@@ -343,4 +478,6 @@ def reference_inference(x, w1, b1, wo, bo, w2=None, b2=None):
 
 __all__ = ["FFTransposeMult", "FFInputLayerJoin", "FFAggMatrix", "FFReluBiasSum", "FFTransposeBiasSum",
            "FFTransposeBiasSumSigmoid", "FFRowAggregate", "FFOutputLayer", "FFMatrixBlockScanner", "FFMatrixWriter",
+           "InferenceResult", "FFSingleMatrix", "FFMatrixPartitioner", "InferenceResultPartition", "FFMatrixMultiSel",
+           "FFAggMatrixToOneMatrix",
            "inference_unit", "inference", "load_model", "reference_inference", "mk_blocks", "setup"]

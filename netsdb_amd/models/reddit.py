@@ -292,6 +292,37 @@ def infer_labels(client, db: str, n: int, hidden: int = 32, labels: int = 4, blo
     return out, lab, ref
 
 
+def infer_results(client, db: str, n: int, hidden: int = 32, labels: int = 4, block: int = 16, seed: int = 0,
+                  enable_partition: bool = False):
+    """RedditFeatureExtractor.cc's inference stage: FF inference over the comment feature blocks, then
+    FFMatrixMultiSel flattens the output blocks into one ff.InferenceResult per comment (row index + its first
+    two scores), written by InferenceResultPartition (partitioned by index) when ``enable_partition``, else by a
+    plain writer. Returns (results batch sorted by index, the fp32 reference scores [n, 2])."""
+    X = features_matrix(client, db, n)
+    mdb = f"{db}_ffr"
+    ff.setup(client, mdb)
+    B.load_tensor(client, mdb, "inputs", X.float(), block, block, dtype=torch.float32)
+    g = torch.Generator().manual_seed(seed)
+    w1 = torch.randn(hidden, NUM_FEATURES, generator=g) * (3.0 / NUM_FEATURES) ** 0.5
+    wo = torch.randn(labels, hidden, generator=g) * (3.0 / hidden) ** 0.5
+    b1, bo = torch.randn(hidden, 1, generator=g) * 0.1, torch.randn(labels, 1, generator=g) * 0.1
+    for nm, t in (("w1", w1), ("wo", wo), ("b1", b1), ("bo", bo)):
+        B.load_tensor(client, mdb, nm, t, block, block if t.shape[1] > 1 else 1, dtype=torch.float32)
+    ff.inference_unit(client, mdb, "w1", "wo", "inputs", "b1", "bo", "output")
+    if client.storage.has_set(mdb, "results"):
+        client.remove_set(mdb, "results")
+    client.create_set(mdb, "results", ff.InferenceResult)
+    sel = ff.FFMatrixMultiSel().set_input(ff.FFMatrixBlockScanner(mdb, "output"))
+    writer = ff.InferenceResultPartition(mdb, "results") if enable_partition else \
+        WriteSet(mdb, "results", ff.InferenceResult)
+    client.execute_computations(writer.set_input(sel), job_name="reddit_inference_results")
+    got = [b for b in client.get_set_batches(mdb, "results", gather=True) if b.n]
+    res = RecordBatch.concat(got)
+    res = res.take(torch.argsort(res.columns["index"]))
+    ref = ff.reference_inference(X.float(), w1, b1, wo, bo)[:, :2]
+    return res, ref
+
+
 def label_split(client, db: str, threshold: int) -> List[int]:
     pos = _run(client, db, "positives", LabelSelection(threshold, True).set_input(ScanSet(db, "labelled")),
                "reddit_label_pos")

@@ -18,7 +18,7 @@ from typing import List
 import torch
 
 from .. import ops
-from ..computations import MultiSelectionComp, ScanSet, WriteSet
+from ..computations import MultiSelectionComp, ScanSet, SelectionComp, WriteSet
 from ..lambdas import make_batch_lambda
 from ..objects.builtin import FFMatrixBlock
 from ..objects.record import PDBObject, RecordBatch, Tensor
@@ -157,5 +157,53 @@ class SemanticClassifier:
         return torch.softmax(h @ self.W2.float().cpu().t() + self.b2.cpu(), -1)
 
 
+class SemanticClassifierSingleBlock(SelectionComp):
+    """Text classifier over the whole embedded batch as ONE matrix (src/word2vec/headers/
+    SemanticClassifierSingleBlock.h): x0 [sizeEmbed x batch] (an FFSingleMatrix from FFAggMatrixToOneMatrix) ->
+    relu(W0 x0 + b0) [sizeDense0 x batch] -> sigmoid(W1 y0 + b1) [sizeDense1 x batch] -> label (> 0.5 -> 1 else 0),
+    written as one FFMatrixBlock. The reference's dense weights are placeholder constants; here they are
+    seeded random weights of the same geometry (``weights()``), evaluated with exact-f32 GEMMs."""
+
+    def __init__(self, size_embed: int = 500, size_dense0: int = 16, size_dense1: int = 1, seed: int = 0):
+        super().__init__()
+        self.size_embed, self.size_dense0, self.size_dense1, self.seed = size_embed, size_dense0, size_dense1, seed
+
+    def weights(self, device=None):
+        g = torch.Generator().manual_seed(self.seed)
+        w0 = (torch.rand(self.size_dense0, self.size_embed, generator=g) * 2 - 1) * (3.0 / self.size_embed) ** 0.5
+        b0 = (torch.rand(self.size_dense0, generator=g) * 2 - 1) * 0.1
+        w1 = (torch.rand(self.size_dense1, self.size_dense0, generator=g) * 2 - 1) * (3.0 / self.size_dense0) ** 0.5
+        b1 = (torch.rand(self.size_dense1, generator=g) * 2 - 1) * 0.1
+        return [t.to(device) for t in (w0, b0, w1, b1)]
+
+    def classify(self, x0: torch.Tensor) -> torch.Tensor:
+        """x0 [sizeEmbed, batch] -> labels [sizeDense1, batch] (float 0 / 1)."""
+        w0, b0, w1, b1 = self.weights(x0.device)
+        x0 = x0.float()
+        if x0.is_cuda:
+            y0 = torch.relu(ops.gemm_nt_f32(w0.contiguous(), x0.t().contiguous()) + b0[:, None])
+            y1 = torch.sigmoid(ops.gemm_nt_f32(w1.contiguous(), y0.t().contiguous()) + b1[:, None])
+        else:
+            y0 = torch.relu(w0 @ x0 + b0[:, None])
+            y1 = torch.sigmoid(w1 @ y0 + b1[:, None])
+        return (y1 > 0.5).float()
+
+    def get_selection(self, m):
+        return make_batch_lambda(m, lambda b: torch.ones(b.n, dtype=torch.bool, device=b.columns["data"].device))
+
+    def get_projection(self, m):
+        from .ff import mk_blocks
+
+        def proj(b: RecordBatch):
+            outs = []
+            for k in range(b.n):
+                r, c = int(b.columns["row_nums"][k]), int(b.columns["col_nums"][k])
+                outs.append(self.classify(b.columns["data"][k, :r, :c]))
+            d = torch.stack(outs)
+            return mk_blocks(b.columns["block_row"], b.columns["block_col"], d, self.size_dense1, d.shape[2])
+
+        return make_batch_lambda(m, proj, tag="semantic_classifier_single_block")
+
+
 __all__ = ["EmbeddingSegment", "EmbeddingLookupSparse", "load_embeddings", "word2vec_matmul", "word2vec_lookup",
-           "word2vec_sparse", "assemble_segments", "SemanticClassifier"]
+           "word2vec_sparse", "assemble_segments", "SemanticClassifier", "SemanticClassifierSingleBlock"]

@@ -101,11 +101,10 @@ def gemm_nt(A, B, bias=None, bias_mode=BIAS_NONE, act=ACT_NONE, out_dtype=torch.
     """epilogue(alpha * A @ B^T) [+ out when accumulate]: A [..,M,K], B [..,N,K] (K-contiguous),
     bias f32 per row/col. ``accumulate`` adds into an existing f32 ``out`` (C += A.B^T). ``cfg`` forces the
     tile config of THIS call (0 = 128x128, 2 = 256x256 8-phase; None = auto); ``epi`` the 8-phase kernel's
-    unsplit epilogue (0 = LDS-staged, 1 = direct register stores; None = auto: direct). A tail trigger armed on the
-    current stream (execution/streams.TailTrigger) and an armed operand prefetch (streams.arm_operand_prefetch: a
-    later kernel's operand read into the Infinity Cache by this launch's workgroups as they finish) are handed to
-    this launch when it is long enough to take them — per call and per stream, so GEMMs on other lanes or threads
-    never see them."""
+    unsplit epilogue (0 = LDS-staged, 1 = direct register stores; None = auto: direct). An operand prefetch armed on
+    the current stream (streams.arm_operand_prefetch: a later kernel's operand read into the Infinity Cache by this
+    launch's workgroups as they finish) is handed to this launch when it is long enough to take it — per call and
+    per stream, so GEMMs on other lanes or threads never see it."""
     act = act_code(act)
     if _use_hip(A, B):
         if bias is not None and bias.dtype != torch.float32:
@@ -113,34 +112,16 @@ def gemm_nt(A, B, bias=None, bias_mode=BIAS_NONE, act=ACT_NONE, out_dtype=torch.
         A, B = gemm_operands(A, B)
         h = _ext.hip()
         c = -1 if cfg is None else int(cfg)
-        sig, sval, pf = None, 0, None
+        pf = None
         streams = _streams()
-        trig = streams.armed_trigger(A.device) if streams._armed else None
-        pf_armed = bool(streams._armed_pf)
-        start_sig, taken, nwg = None, None, 0
-        if trig is not None or pf_armed:
+        if streams._armed_pf:
             M, N, K = A.shape[-2], B.shape[-2], A.shape[-1]
             batch = A.shape[0] if A.dim() == 3 else 1
-            if h.gemm_tail_eligible(M, N, K, batch, int(splits), c):
-                if trig is not None and trig.mode == "start":
-                    splits = _reserve_cus_splits(h, A.device, M, N, K, batch, int(splits), c, trig.reserve_cus)
-                    nwg = h.gemm_launch_wgs(M, N, K, batch, int(splits), c)
-                    start_sig, _ = trig.take(nwg)
-                    taken = trig
-                elif trig is not None:
-                    sig, sval = trig.take()
-                    taken = trig
-                if pf_armed:
-                    pf = streams.take_operand_prefetch(A.device)
-        try:
-            return h.gemm_nt(A, B, bias, int(bias_mode if bias is not None else 0), act,
-                             out_dtype == torch.float32, float(alpha), float(dropout), int(seed),
-                             int(splits), out, bool(accumulate), c, sig, int(sval), -1 if epi is None else int(epi),
-                             pf, start_sig)
-        except Exception:
-            if taken is not None:
-                taken.untake(nwg)
-            raise
+            if h.gemm_prefetch_eligible(M, N, K, batch, int(splits), c):
+                pf = streams.take_operand_prefetch(A.device)
+        return h.gemm_nt(A, B, bias, int(bias_mode if bias is not None else 0), act,
+                         out_dtype == torch.float32, float(alpha), float(dropout), int(seed),
+                         int(splits), out, bool(accumulate), c, -1 if epi is None else int(epi), pf)
     v = torch.matmul(A.float(), B.float().transpose(-1, -2)) * alpha
     if bias is not None:
         b = bias.float()
@@ -155,16 +136,6 @@ def gemm_nt(A, B, bias=None, bias_mode=BIAS_NONE, act=ACT_NONE, out_dtype=torch.
         out.copy_(v)
         return out
     return v
-
-
-def _reserve_cus_splits(h, device, M, N, K, batch, splits, cfg, reserve):
-    """Split-K slices for a one-wave launch that leaves ``reserve`` of the device's CUs free (start gates)."""
-    cus = torch.cuda.get_device_properties(device).multi_processor_count
-    cap = max(1, cus - int(reserve))
-    s = splits if splits > 0 else h.gemm_splits(M, N, K, batch, cfg)
-    while s > 1 and h.gemm_launch_wgs(M, N, K, batch, s, cfg) > cap:
-        s -= 1
-    return s
 
 
 def gemm_nt_f32(A, B, alpha=1.0, out=None, accumulate=False):

@@ -148,8 +148,7 @@ class MatmulNode(Node):
     def eval(self, engine) -> Dense:
         if self.value is not None:
             return self.value
-        pf = self._tail_prefetch(engine)
-        armed = self._arm_operand_prefetch(engine) if pf is None else None
+        armed = self._arm_operand_prefetch(engine)
         try:
             A, B = self.a.eval(engine), self.b.eval(engine)
         finally:
@@ -157,13 +156,7 @@ class MatmulNode(Node):
                 from ..execution.streams import disarm_operand_prefetch
 
                 disarm_operand_prefetch(armed)
-        if pf is not None:
-            pf.launched()
-        try:
-            return self._eval(engine, A, B)
-        finally:
-            if pf is not None:
-                pf.end()
+        return self._eval(engine, A, B)
 
     def _prefetch_weight(self, engine):
         """The stored weight operand of a GEMM whose other operand comes out of a GEMM evaluated first (the FF
@@ -193,23 +186,6 @@ class MatmulNode(Node):
         from ..execution.streams import arm_operand_prefetch
 
         return w.device if arm_operand_prefetch(w) else None
-
-    def _tail_prefetch(self, engine):
-        """One operand is a stored weight set and the other comes out of a GEMM evaluated first (the FF output
-        layer after layer 1): warm the weight into the Infinity Cache during that GEMM's tail
-        (streams.TailPrefetch). Engine option ``tail_prefetch`` (default off: measured slower in the bench)."""
-        if not getattr(engine, "tail_prefetch", False) or engine.ctx.distributed:
-            return None
-        w = self._prefetch_weight(engine)
-        if w is None:
-            return None
-        pf = engine.__dict__.get("_tail_prefetch")
-        if pf is None:
-            from ..execution.streams import TailPrefetch
-
-            pf = engine.__dict__["_tail_prefetch"] = TailPrefetch(w.device)
-        extra = [self.bias.eval(engine).phys] if self.bias is not None and isinstance(self.bias, SourceNode) else []
-        return pf if pf.begin([w] + [t for t in extra if isinstance(t, torch.Tensor)]) else None
 
     def _eval(self, engine, A: Dense, B: Dense) -> Dense:
         opA = A.t() if self.p.transpose_a else A           # [M, K]

@@ -73,6 +73,7 @@ class StorageManager:
         self.home = self.device if self.device is not None else torch.device("cpu")
         self.page_size = page_size
         self.rank = rank
+        self.world_size = 1            # set by the client from its cluster context
         spill = os.path.join(self.root, f"node{rank}")
         os.makedirs(spill, exist_ok=True)
         self.buffer_manager = _ext.native().BufferManager(page_size, pool_pages, spill)

@@ -748,10 +748,18 @@ class DenseMatrixSet(UserSet):
         return self
 
     def scan(self, device=None) -> Iterator[RecordBatch]:
+        """The panel as MatrixBlock records. A replicated panel (every rank holds the whole matrix) yields only this
+        rank's share of the blocks on a multi-rank node set, so an SPMD pipeline over it processes each block once
+        cluster-wide (and a gathered read returns each block once)."""
         self.resolve_shared()
         if not self.has_data():
             return
-        yield self.to_blocks(device)
+        b = self.to_blocks(device)
+        ws = getattr(self.manager, "world_size", 1)
+        if self.replicated and ws > 1:
+            rank = getattr(self.manager, "rank", 0)
+            b = b.take(torch.arange(rank, b.n, ws, device=b.columns["block_row"].device))
+        yield b
 
     def num_records(self) -> int:
         self.resolve_shared()

@@ -1,7 +1,7 @@
 """The GEMM STUDY build (module ``netsdb_amd._hip_study``, sources in ``csrc/study``): the diagnostic and rejected
 variants of the block GEMM behind profiles/r2_gemm1_study and profiles/r3_w4a — 8-phase ablations, ring buffers,
 cache policies, K-tail stealing, adaptive split-K, the in-launch split-K fix-up, the 4-wave structures and the
-asm-scheduled w4a kernel. The product never imports it (``netsdb_amd.ops`` runs ``_hip_kernels`` only, whose
+kernel studies. The product never imports it (``netsdb_amd.ops`` runs ``_hip_kernels`` only, whose
 launcher exports the production configs and takes every launch decision as a per-call argument); A/B scripts
 and the study tests use this module.
 """

@@ -9,5 +9,7 @@ timeout -k 10 300 python -u scripts/ab_conv_full.py --rounds 3 > gpurun_out/ab_c
 cat gpurun_out/ab_conv_ws.log
 timeout -k 10 300 python -u scripts/ab_ff_tail.py --rounds 5 > gpurun_out/ab_ff_tail.log 2>&1 || { cat gpurun_out/ab_ff_tail.log; exit 1; }
 cat gpurun_out/ab_ff_tail.log
+# the store-pattern microbenchmark is built here from its source (no committed binary)
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o scripts/native/store_gemm2 scripts/native/store_gemm2.hip || exit 1
 timeout -k 10 60 ./scripts/native/store_gemm2 > gpurun_out/store_gemm2.txt 2>&1 || exit 1
 cat gpurun_out/store_gemm2.txt

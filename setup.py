@@ -23,7 +23,7 @@ RDIR = os.path.join("netsdb_amd", "csrc", "runtime")
 HIP_SOURCES = ("gemm.hip", "gemm_f32.hip", "conv2d.hip", "rowops.hip", "strings.hip", "dedup.hip", "relops.hip",
                "relops_bind.cpp")
 SDIR = os.path.join("netsdb_amd", "csrc", "study")
-STUDY_SOURCES = ("gemm_study.hip", "gemm_w4a.hip")
+STUDY_SOURCES = ("gemm_study.hip",)
 
 
 def study_ext():

@@ -18,8 +18,7 @@ def _last_json(out: str) -> dict:
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("extra", [[], ["--overlap", "before"], ["--overlap", "after", "--inflight", "2"],
-                                   ["--overlap", "tail"], ["--overlap", "beside"], ["--graph"], ["--two-job"],
+@pytest.mark.parametrize("extra", [[], ["--overlap", "before"], ["--overlap", "after"], ["--two-job"],
                                    ["--single-job"]])
 def test_bench_single_process(extra):
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")

@@ -26,7 +26,7 @@ def _reset():
 
 
 @pytest.mark.parametrize("shape", [(777, 555, 4104), (300, 2000, 100000), (512, 512, 640)])
-@pytest.mark.parametrize("cfg", [2, 12, 14, 15, 16, 30])
+@pytest.mark.parametrize("cfg", [2, 12, 14, 15, 16])
 def test_study_kernels_bit_exact(shape, cfg):
     M, N, K = shape
     g = torch.Generator(device=DEV).manual_seed(5)

@@ -80,7 +80,6 @@ def test_ff_inference_unit_headline_vs_fp32():
     from netsdb_amd.models.blocks import to_tensor
 
     c = PDBClient(root=tempfile.mkdtemp(), device=DEV)
-    c.engine.tail_prefetch = True          # opt-in path checked below
     ff.load_model(c, "ff", 1000, 597540, 1000, 14588, 50, 10000, seed=1234)
     res = ff.inference_unit(c, "ff", "w1", "wo", "inputs", "b1", "bo", "output", dropout_rate=0.0)
     fused = [op for j in res["jobs"] for op in j.get("fused_ops", [])]
@@ -96,15 +95,10 @@ def test_ff_inference_unit_headline_vs_fp32():
     e = _err(out[rows], ref)
     assert e < 1e-3, e
     assert torch.allclose(out[rows].sum(-1), torch.ones(32, device=DEV), atol=1e-3)
-    # the output layer's weight was read into the cache during layer 1's tail (streams.TailPrefetch), and the
-    # prefetch changes nothing in the result: the same job without it is bit-identical
-    pf = c.engine.__dict__.get("_tail_prefetch")
-    assert pf is not None and pf.prefetches >= 1 and pf.trigger.gated >= 1
-    n_pf = pf.prefetches
-    c.engine.tail_prefetch = False
+    # the in-kernel operand prefetch changes nothing in the result: the same job without it is bit-identical
+    c.engine.operand_prefetch = False
     ff.inference_unit(c, "ff", "w1", "wo", "inputs", "b1", "bo", "output", dropout_rate=0.0)
     torch.testing.assert_close(to_tensor(c, "ff", "output").float(), out, rtol=0, atol=0)
-    assert pf.prefetches == n_pf
 
 
 def test_conv2d_headline_vs_fp32():
