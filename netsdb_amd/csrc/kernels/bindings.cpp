@@ -52,16 +52,18 @@ int nsdb_block_simcount(const void* pool, const long long* cand, const void* que
                         int bc, int h, int w, float fp, int is_f32, int S, unsigned* partial, hipStream_t st);
 int nsdb_block_maxdiff(const void* pool, const long long* cand, const void* blks, long long nblocks, long long elems,
                        int is_f32, int S, float* partial, hipStream_t st);
-int nsdb_str_hash(const void* bytes, const int64_t* off, int64_t n, uint64_t* out, hipStream_t st);
-int nsdb_str_like(const void* bytes, const int64_t* off, int64_t n, const uint8_t* pat, int pat_len,
-                  const int* seg_start, const int* seg_len, int nseg, int anchor_start, int anchor_end, int negate,
-                  uint8_t* out, hipStream_t st);
-int nsdb_str_slice(const void* src, const int64_t* off, int64_t start, const int64_t* out_off, int64_t n, void* dst,
-                   hipStream_t st);
-int nsdb_str_eq_pairs(const void* a, const int64_t* offa, const int64_t* ia, const void* b, const int64_t* offb,
-                      const int64_t* ib, int64_t m, uint8_t* out, hipStream_t st);
-int nsdb_str_gather(const void* src, const int64_t* off, const int64_t* idx, const int64_t* out_off, int64_t m,
-                    void* dst, hipStream_t st);
+int nsdb_str_hash(const void* bytes, const int64_t* starts, const int64_t* ends, int64_t n, uint64_t* out,
+                  hipStream_t st);
+int nsdb_str_like(const void* bytes, const int64_t* starts, const int64_t* ends, int64_t n, const uint8_t* pat,
+                  int pat_len, const int* seg_start, const int* seg_len, int nseg, int anchor_start, int anchor_end,
+                  int negate, uint8_t* out, hipStream_t st);
+int nsdb_str_slice(const void* src, const int64_t* starts, int64_t start, const int64_t* out_off, int64_t n,
+                   void* dst, hipStream_t st);
+int nsdb_str_eq_pairs(const void* a, const int64_t* sta, const int64_t* ena, const int64_t* ia, const void* b,
+                      const int64_t* stb, const int64_t* enb, const int64_t* ib, int64_t m, uint8_t* out,
+                      hipStream_t st);
+int nsdb_str_gather(const void* src, const int64_t* starts, const int64_t* ends, const int64_t* idx,
+                    const int64_t* out_off, int64_t m, void* dst, hipStream_t st);
 }
 
 void register_relops(pybind11::module& m);
@@ -489,67 +491,78 @@ torch::Tensor embedding_bag(torch::Tensor table, torch::Tensor idx, torch::Tenso
   return out;
 }
 
-// String columns: bytes u8 [>= offsets[-1] + 16] (padding read by the dword loads), offsets i64 [n+1].
-void check_strings(const torch::Tensor& bytes, const torch::Tensor& off) {
+// String columns: bytes u8 [>= payload + 16] (padding read by the dword loads), row bounds as starts / ends i64 [n]
+// (a packed column passes offsets[:-1] / offsets[1:]; a gathered view its own arrays).
+void check_strings(const torch::Tensor& bytes, const torch::Tensor& st, const torch::Tensor& en) {
   check_cuda(bytes, "bytes");
-  check_cuda(off, "offsets");
+  check_cuda(st, "starts");
+  check_cuda(en, "ends");
   TORCH_CHECK(bytes.scalar_type() == torch::kUInt8 && bytes.dim() == 1 && bytes.is_contiguous(), "bytes u8 1-D");
-  TORCH_CHECK(off.scalar_type() == torch::kInt64 && off.dim() == 1 && off.is_contiguous() && off.numel() >= 1,
-              "offsets i64 [n+1]");
+  for (const torch::Tensor* t : {&st, &en})
+    TORCH_CHECK(t->scalar_type() == torch::kInt64 && t->dim() == 1 && (t->numel() <= 1 || t->stride(0) == 1),
+                "starts / ends: unit-stride i64");
+  TORCH_CHECK(st.numel() == en.numel(), "starts / ends length mismatch");
   TORCH_CHECK(bytes.numel() % 4 == 0 && bytes.numel() >= 16, "bytes must be padded to a multiple of 4, >= 16");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(bytes.data_ptr()) % 4 == 0, "bytes must be 4-byte aligned");
 }
 
-torch::Tensor str_hash(torch::Tensor bytes, torch::Tensor off, int64_t payload_end) {
-  check_strings(bytes, off);
+torch::Tensor str_hash(torch::Tensor bytes, torch::Tensor st, torch::Tensor en, int64_t payload_end) {
+  check_strings(bytes, st, en);
   TORCH_CHECK(payload_end + 16 <= bytes.numel(), "string payload must be followed by >= 16 pad bytes");
-  const int64_t n = off.numel() - 1;
-  auto out = torch::empty({n}, off.options());
-  check_rc(nsdb_str_hash(bytes.data_ptr(), off.data_ptr<int64_t>(), n, (uint64_t*)out.data_ptr<int64_t>(),
-                         cur_stream()),
+  const int64_t n = st.numel();
+  auto out = torch::empty({n}, st.options());
+  check_rc(nsdb_str_hash(bytes.data_ptr(), st.data_ptr<int64_t>(), en.data_ptr<int64_t>(), n,
+                         (uint64_t*)out.data_ptr<int64_t>(), cur_stream()),
            "str_hash");
   return out;
 }
 
-torch::Tensor str_like(torch::Tensor bytes, torch::Tensor off, int64_t payload_end, const std::string& pat,
-                       std::vector<int64_t> seg_start, std::vector<int64_t> seg_len, bool anchor_start,
-                       bool anchor_end, bool negate) {
-  check_strings(bytes, off);
+torch::Tensor str_like(torch::Tensor bytes, torch::Tensor st, torch::Tensor en, int64_t payload_end,
+                       const std::string& pat, std::vector<int64_t> seg_start, std::vector<int64_t> seg_len,
+                       bool anchor_start, bool anchor_end, bool negate) {
+  check_strings(bytes, st, en);
   TORCH_CHECK(payload_end + 16 <= bytes.numel(), "string payload must be followed by >= 16 pad bytes");
   TORCH_CHECK(seg_start.size() == seg_len.size(), "segment lists differ in length");
   TORCH_CHECK(pat.size() <= 224 && seg_start.size() <= 16, "pattern too long for the kernarg pattern (224 B, 16 segs)");
   std::vector<int> ss(seg_start.begin(), seg_start.end()), sl(seg_len.begin(), seg_len.end());
-  const int64_t n = off.numel() - 1;
+  const int64_t n = st.numel();
   auto out = torch::empty({n}, bytes.options());
-  check_rc(nsdb_str_like(bytes.data_ptr(), off.data_ptr<int64_t>(), n, (const uint8_t*)pat.data(), (int)pat.size(),
-                         ss.data(), sl.data(), (int)ss.size(), anchor_start, anchor_end, negate,
+  check_rc(nsdb_str_like(bytes.data_ptr(), st.data_ptr<int64_t>(), en.data_ptr<int64_t>(), n, (const uint8_t*)pat.data(),
+                         (int)pat.size(), ss.data(), sl.data(), (int)ss.size(), anchor_start, anchor_end, negate,
                          out.data_ptr<uint8_t>(), cur_stream()),
            "str_like");
   return out.view(torch::kBool);
 }
 
-// idx must index rows of off (0 <= idx < n): checked by the caller on the device before launch.
-torch::Tensor str_gather(torch::Tensor bytes, torch::Tensor off, torch::Tensor idx, torch::Tensor out_off,
-                         int64_t out_bytes) {
-  check_strings(bytes, off);
-  check_cuda(idx, "idx");
+// Pack rows idx (or every row when idx is None) of a column into a new padded buffer at out_off. Indices come
+// from the column's own row space (the callers derive them on the device).
+torch::Tensor str_gather(torch::Tensor bytes, torch::Tensor st, torch::Tensor en, c10::optional<torch::Tensor> idx,
+                         torch::Tensor out_off, int64_t out_bytes) {
+  check_strings(bytes, st, en);
   check_cuda(out_off, "out_off");
-  TORCH_CHECK(idx.scalar_type() == torch::kInt64 && idx.is_contiguous() && idx.dim() == 1, "idx i64 1-D");
-  TORCH_CHECK(out_off.scalar_type() == torch::kInt64 && out_off.numel() == idx.numel() + 1, "out_off [m+1]");
+  const int64_t* ip = nullptr;
+  int64_t m = st.numel();
+  if (idx.has_value() && idx->defined()) {
+    check_cuda(*idx, "idx");
+    TORCH_CHECK(idx->scalar_type() == torch::kInt64 && idx->is_contiguous() && idx->dim() == 1, "idx i64 1-D");
+    ip = idx->data_ptr<int64_t>();
+    m = idx->numel();
+  }
+  TORCH_CHECK(out_off.scalar_type() == torch::kInt64 && out_off.numel() == m + 1, "out_off [m+1]");
   const int64_t padded = ((out_bytes + 16 + 3) / 4) * 4;
   auto dst = torch::zeros({padded}, bytes.options());
-  check_rc(nsdb_str_gather(bytes.data_ptr(), off.data_ptr<int64_t>(), idx.data_ptr<int64_t>(),
-                           out_off.data_ptr<int64_t>(), idx.numel(), dst.data_ptr(), cur_stream()),
+  check_rc(nsdb_str_gather(bytes.data_ptr(), st.data_ptr<int64_t>(), en.data_ptr<int64_t>(), ip,
+                           out_off.data_ptr<int64_t>(), m, dst.data_ptr(), cur_stream()),
            "str_gather");
   return dst;
 }
 
-// out[i] = (a[ia[i]] == b[ib[i]]) byte-exact; ia / ib may be None (identity). Indices are checked on the device
-// by the caller (they come from the same grouping / join that produced them).
-torch::Tensor str_eq_pairs(torch::Tensor a, torch::Tensor offa, c10::optional<torch::Tensor> ia, torch::Tensor b,
-                           torch::Tensor offb, c10::optional<torch::Tensor> ib, int64_t m) {
-  check_strings(a, offa);
-  check_strings(b, offb);
+// out[i] = (a[ia[i]] == b[ib[i]]) byte-exact; ia / ib may be None (identity).
+torch::Tensor str_eq_pairs(torch::Tensor a, torch::Tensor sta, torch::Tensor ena, c10::optional<torch::Tensor> ia,
+                           torch::Tensor b, torch::Tensor stb, torch::Tensor enb, c10::optional<torch::Tensor> ib,
+                           int64_t m) {
+  check_strings(a, sta, ena);
+  check_strings(b, stb, enb);
   const int64_t* pa = nullptr;
   const int64_t* pb = nullptr;
   if (ia.has_value() && ia->defined()) {
@@ -557,33 +570,35 @@ torch::Tensor str_eq_pairs(torch::Tensor a, torch::Tensor offa, c10::optional<to
     TORCH_CHECK(ia->scalar_type() == torch::kInt64 && ia->is_contiguous() && ia->numel() == m, "ia i64 [m]");
     pa = ia->data_ptr<int64_t>();
   } else {
-    TORCH_CHECK(offa.numel() - 1 >= m, "a has fewer than m rows");
+    TORCH_CHECK(sta.numel() >= m, "a has fewer than m rows");
   }
   if (ib.has_value() && ib->defined()) {
     check_cuda(*ib, "ib");
     TORCH_CHECK(ib->scalar_type() == torch::kInt64 && ib->is_contiguous() && ib->numel() == m, "ib i64 [m]");
     pb = ib->data_ptr<int64_t>();
   } else {
-    TORCH_CHECK(offb.numel() - 1 >= m, "b has fewer than m rows");
+    TORCH_CHECK(stb.numel() >= m, "b has fewer than m rows");
   }
   auto out = torch::empty({m}, a.options());
-  check_rc(nsdb_str_eq_pairs(a.data_ptr(), offa.data_ptr<int64_t>(), pa, b.data_ptr(), offb.data_ptr<int64_t>(), pb, m,
-                             out.data_ptr<uint8_t>(), cur_stream()),
+  check_rc(nsdb_str_eq_pairs(a.data_ptr(), sta.data_ptr<int64_t>(), ena.data_ptr<int64_t>(), pa, b.data_ptr(),
+                             stb.data_ptr<int64_t>(), enb.data_ptr<int64_t>(), pb, m, out.data_ptr<uint8_t>(),
+                             cur_stream()),
            "str_eq_pairs");
   return out.view(torch::kBool);
 }
 
 // SUBSTRING of every row: out_off [n+1] (device prefix sums of the clamped lengths), cap = an upper bound of the
 // output bytes known on the host (n * length): no device read to size the buffer.
-torch::Tensor str_slice(torch::Tensor bytes, torch::Tensor off, int64_t start, torch::Tensor out_off, int64_t cap) {
-  check_strings(bytes, off);
+torch::Tensor str_slice(torch::Tensor bytes, torch::Tensor st, torch::Tensor en, int64_t start, torch::Tensor out_off,
+                        int64_t cap) {
+  check_strings(bytes, st, en);
   check_cuda(out_off, "out_off");
   TORCH_CHECK(start >= 0, "start must be >= 0");
-  TORCH_CHECK(out_off.scalar_type() == torch::kInt64 && out_off.numel() == off.numel(), "out_off [n+1]");
+  TORCH_CHECK(out_off.scalar_type() == torch::kInt64 && out_off.numel() == st.numel() + 1, "out_off [n+1]");
   const int64_t padded = ((cap + 16 + 3) / 4) * 4;
   auto dst = torch::zeros({padded}, bytes.options());
-  check_rc(nsdb_str_slice(bytes.data_ptr(), off.data_ptr<int64_t>(), start, out_off.data_ptr<int64_t>(),
-                          off.numel() - 1, dst.data_ptr(), cur_stream()),
+  check_rc(nsdb_str_slice(bytes.data_ptr(), st.data_ptr<int64_t>(), start, out_off.data_ptr<int64_t>(), st.numel(),
+                          dst.data_ptr(), cur_stream()),
            "str_slice");
   return dst;
 }
@@ -727,6 +742,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("str_like", &str_like, "SQL LIKE over a device string column (segments of the pattern bytes)");
   m.def("str_slice", &str_slice, "SUBSTRING of every row of a device string column (no host read)");
   m.def("str_eq_pairs", &str_eq_pairs, "byte-exact equality of string row pairs a[ia[i]] == b[ib[i]]",
-        py::arg("a"), py::arg("offa"), py::arg("ia"), py::arg("b"), py::arg("offb"), py::arg("ib"), py::arg("m"));
-  m.def("str_gather", &str_gather, "take() of a device string column into a new padded byte buffer");
+        py::arg("a"), py::arg("sta"), py::arg("ena"), py::arg("ia"), py::arg("b"), py::arg("stb"), py::arg("enb"),
+        py::arg("ib"), py::arg("m"));
+  m.def("str_gather", &str_gather, "pack rows of a device string column into a new padded byte buffer",
+        py::arg("bytes"), py::arg("starts"), py::arg("ends"), py::arg("idx"), py::arg("out_off"), py::arg("out_bytes"));
 }

@@ -54,11 +54,11 @@ __device__ __forceinline__ uint32_t byte_at(const uint32_t* __restrict__ w, int6
 }
 
 __global__ __launch_bounds__(256) void str_hash_kernel(const uint32_t* __restrict__ w,
-                                                      const int64_t* __restrict__ off, int64_t n,
-                                                      uint64_t* __restrict__ out) {
+                                                      const int64_t* __restrict__ st, const int64_t* __restrict__ en,
+                                                      int64_t n, uint64_t* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const int64_t s = off[i], e = off[i + 1];
+  const int64_t s = st[i], e = en[i];
   const int64_t len = e - s;
   uint64_t h = mix64((uint64_t)len ^ 0x9E3779B97F4A7C15ull);
   for (int64_t p = s; p < e; p += 8) {
@@ -81,11 +81,11 @@ __device__ __forceinline__ bool seg_match_at(const uint32_t* __restrict__ w, int
 }
 
 __global__ __launch_bounds__(256) void str_like_kernel(const uint32_t* __restrict__ w,
-                                                      const int64_t* __restrict__ off, int64_t n,
-                                                      LikePattern pt, uint8_t* __restrict__ out) {
+                                                      const int64_t* __restrict__ st, const int64_t* __restrict__ en,
+                                                      int64_t n, LikePattern pt, uint8_t* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const int64_t s = off[i], e = off[i + 1];
+  const int64_t s = st[i], e = en[i];
   bool ok = true;
   int64_t pos = s;
   for (int sg = 0; sg < pt.nseg && ok; ++sg) {
@@ -114,26 +114,27 @@ __global__ __launch_bounds__(256) void str_like_kernel(const uint32_t* __restric
 
 // out_off[j] = exclusive prefix of the selected lengths (computed on the device by the caller).
 __global__ __launch_bounds__(256) void str_gather_kernel(const uint8_t* __restrict__ src,
-                                                        const int64_t* __restrict__ off,
+                                                        const int64_t* __restrict__ st,
+                                                        const int64_t* __restrict__ en,
                                                         const int64_t* __restrict__ idx,
                                                         const int64_t* __restrict__ out_off, int64_t m,
                                                         uint8_t* __restrict__ dst) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= m) return;
-  const int64_t r = idx[j];
-  const int64_t s = off[r], len = off[r + 1] - s, d = out_off[j];
+  const int64_t r = idx ? idx[j] : j;
+  const int64_t s = st[r], len = en[r] - s, d = out_off[j];
   for (int64_t k = 0; k < len; ++k) dst[d + k] = src[s + k];
 }
 
 // SUBSTRING: row j's bytes [start, start + len_j) (len_j = out_off[j+1] - out_off[j], computed on the device by the
 // caller as clamp(row length - start, 0, length)) copied to out_off[j].
 __global__ __launch_bounds__(256) void str_slice_kernel(const uint8_t* __restrict__ src,
-                                                       const int64_t* __restrict__ off, int64_t start,
+                                                       const int64_t* __restrict__ st, int64_t start,
                                                        const int64_t* __restrict__ out_off, int64_t n,
                                                        uint8_t* __restrict__ dst) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
-  const int64_t s = off[j] + start, d = out_off[j], len = out_off[j + 1] - d;
+  const int64_t s = st[j] + start, d = out_off[j], len = out_off[j + 1] - d;
   for (int64_t k = 0; k < len; ++k) dst[d + k] = src[s + k];
 }
 
@@ -143,16 +144,16 @@ inline int grid_for(int64_t n) { return (int)((n + 255) / 256); }
 // Exact equality of row pairs (a[ia[i]] == b[ib[i]]) for value-exact string keys: group-by / join / IN decide by
 // 64-bit hash first, then every row is byte-compared with its group's or match's representative
 // (reference pdb::String equality, src/objectModel/headers/PDBString.h:46-48).
-__global__ __launch_bounds__(256) void str_eq_pairs_kernel(const uint32_t* __restrict__ wa, const int64_t* __restrict__ offa,
-                                                           const int64_t* __restrict__ ia,
-                                                           const uint32_t* __restrict__ wb, const int64_t* __restrict__ offb,
-                                                           const int64_t* __restrict__ ib, int64_t m,
-                                                           uint8_t* __restrict__ out) {
+__global__ __launch_bounds__(256) void str_eq_pairs_kernel(const uint32_t* __restrict__ wa, const int64_t* __restrict__ sta,
+                                                           const int64_t* __restrict__ ena, const int64_t* __restrict__ ia,
+                                                           const uint32_t* __restrict__ wb, const int64_t* __restrict__ stb,
+                                                           const int64_t* __restrict__ enb, const int64_t* __restrict__ ib,
+                                                           int64_t m, uint8_t* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= m) return;
   const int64_t ra = ia ? ia[i] : i, rb = ib ? ib[i] : i;
-  const int64_t sa = offa[ra], la = offa[ra + 1] - sa;
-  const int64_t sb = offb[rb], lb = offb[rb + 1] - sb;
+  const int64_t sa = sta[ra], la = ena[ra] - sa;
+  const int64_t sb = stb[rb], lb = enb[rb] - sb;
   bool eq = la == lb;
   for (int64_t p = 0; eq && p < la; p += 8) {
     uint64_t x = load8(wa, sa + p) ^ load8(wb, sb + p);
@@ -168,13 +169,18 @@ __global__ __launch_bounds__(256) void str_eq_pairs_kernel(const uint32_t* __res
 extern "C" {
 
 
-int nsdb_str_hash(const void* bytes, const int64_t* off, int64_t n, uint64_t* out, hipStream_t st) {
+// Every string entry point takes row bounds as (starts [n], ends [n]): a packed column passes (off, off + 1) of its
+// offsets[n+1]; a gathered view (StringColumn.take without a byte copy) passes its own starts / ends.
+int nsdb_str_hash(const void* bytes, const int64_t* starts, const int64_t* ends, int64_t n, uint64_t* out,
+                  hipStream_t st) {
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(str_hash_kernel, dim3(grid_for(n)), dim3(256), 0, st, (const uint32_t*)bytes, off, n, out);
+  hipLaunchKernelGGL(str_hash_kernel, dim3(grid_for(n)), dim3(256), 0, st, (const uint32_t*)bytes, starts, ends, n,
+                     out);
   return (int)hipGetLastError();
 }
 
-int nsdb_str_like(const void* bytes, const int64_t* off, int64_t n, const uint8_t* pat, int pat_len,
+int nsdb_str_like(const void* bytes, const int64_t* starts, const int64_t* ends, int64_t n, const uint8_t* pat,
+                  int pat_len,
                   const int* seg_start, const int* seg_len, int nseg, int anchor_start, int anchor_end, int negate,
                   uint8_t* out, hipStream_t st) {
   if (pat_len > kPatBytes || nseg > kPatSegs || pat_len < 0 || nseg < 0) return -2;
@@ -190,32 +196,34 @@ int nsdb_str_like(const void* bytes, const int64_t* off, int64_t n, const uint8_
   pt.anchor_end = anchor_end;
   pt.negate = negate;
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(str_like_kernel, dim3(grid_for(n)), dim3(256), 0, st, (const uint32_t*)bytes, off, n, pt, out);
+  hipLaunchKernelGGL(str_like_kernel, dim3(grid_for(n)), dim3(256), 0, st, (const uint32_t*)bytes, starts, ends, n, pt,
+                     out);
   return (int)hipGetLastError();
 }
 
-int nsdb_str_gather(const void* src, const int64_t* off, const int64_t* idx, const int64_t* out_off, int64_t m,
-                    void* dst, hipStream_t st) {
+int nsdb_str_gather(const void* src, const int64_t* starts, const int64_t* ends, const int64_t* idx,
+                    const int64_t* out_off, int64_t m, void* dst, hipStream_t st) {
   if (m <= 0) return 0;
-  hipLaunchKernelGGL(str_gather_kernel, dim3(grid_for(m)), dim3(256), 0, st, (const uint8_t*)src, off, idx,
+  hipLaunchKernelGGL(str_gather_kernel, dim3(grid_for(m)), dim3(256), 0, st, (const uint8_t*)src, starts, ends, idx,
                      out_off, m, (uint8_t*)dst);
   return (int)hipGetLastError();
 }
 
-int nsdb_str_slice(const void* src, const int64_t* off, int64_t start, const int64_t* out_off, int64_t n, void* dst,
-                   hipStream_t st) {
+int nsdb_str_slice(const void* src, const int64_t* starts, int64_t start, const int64_t* out_off, int64_t n,
+                   void* dst, hipStream_t st) {
   if (n <= 0) return 0;
   if (start < 0) return -2;
-  hipLaunchKernelGGL(str_slice_kernel, dim3(grid_for(n)), dim3(256), 0, st, (const uint8_t*)src, off, start, out_off, n,
+  hipLaunchKernelGGL(str_slice_kernel, dim3(grid_for(n)), dim3(256), 0, st, (const uint8_t*)src, starts, start, out_off, n,
                      (uint8_t*)dst);
   return (int)hipGetLastError();
 }
 
-int nsdb_str_eq_pairs(const void* a, const int64_t* offa, const int64_t* ia, const void* b, const int64_t* offb,
-                      const int64_t* ib, int64_t m, uint8_t* out, hipStream_t st) {
+int nsdb_str_eq_pairs(const void* a, const int64_t* sta, const int64_t* ena, const int64_t* ia, const void* b,
+                      const int64_t* stb, const int64_t* enb, const int64_t* ib, int64_t m, uint8_t* out,
+                      hipStream_t st) {
   if (m <= 0) return 0;
-  hipLaunchKernelGGL(str_eq_pairs_kernel, dim3(grid_for(m)), dim3(256), 0, st, (const uint32_t*)a, offa, ia,
-                     (const uint32_t*)b, offb, ib, m, out);
+  hipLaunchKernelGGL(str_eq_pairs_kernel, dim3(grid_for(m)), dim3(256), 0, st, (const uint32_t*)a, sta, ena, ia,
+                     (const uint32_t*)b, stb, enb, ib, m, out);
   return (int)hipGetLastError();
 }
 

@@ -4,7 +4,8 @@ The reference stores ``pdb::String`` objects inside pages (src/objectModel/heade
 evaluates string predicates, hash-map keys and joins on them one object at a time on the CPU
 (tpchBench selections, StringIntPair maps in serviceBenchmarks/StringHashMapTest). Here a ``str`` column
 that lives on a GPU is one :class:`StringColumn`: the UTF-8 bytes of every row packed into one uint8
-buffer plus int64 ``offsets[n+1]``, both in HBM. Predicates (=, IN, LIKE, prefix/suffix/contains),
+buffer plus int64 row bounds, both in HBM (packed: ``offsets[n+1]``; a row selection is a view of
+starts / ends into the source buffer, see :class:`StringColumn`). Predicates (=, IN, LIKE, prefix/suffix/contains),
 hashing for group-by/join keys and gathers are single HIP launches over the whole column
 (``csrc/kernels/strings.hip``); Python strings appear only when a caller iterates the column.
 
@@ -65,8 +66,8 @@ def _mix_np(x: np.ndarray) -> np.ndarray:
     return x ^ (x >> np.uint64(31))
 
 
-def _hash_np(buf: np.ndarray, off: np.ndarray) -> np.ndarray:
-    starts, lens = off[:-1], off[1:] - off[:-1]
+def _hash_np(buf: np.ndarray, starts: np.ndarray, ends: np.ndarray) -> np.ndarray:
+    lens = ends - starts
     with np.errstate(over="ignore"):
         h = _mix_np(lens.astype(np.uint64) ^ np.uint64(_SEED))
         nch = int((lens.max() + 7) // 8) if lens.size else 0
@@ -121,13 +122,26 @@ def _like_regex(pat, st, ln, a0, a1) -> "re.Pattern[bytes]":
 
 
 class StringColumn:
-    """n strings: ``data`` uint8 [>= payload + 16] (4-byte multiple), ``offsets`` int64 [n+1] into data."""
+    """n strings over one uint8 buffer ``data`` [>= payload + 16] (4-byte multiple): row i is
+    ``data[starts[i]:ends[i]]``. A PACKED column (built from a list, gathered, read from a page) also keeps
+    ``offsets`` [n+1] with starts = offsets[:-1], ends = offsets[1:]; a VIEW (the result of :meth:`take`, a
+    filter, a join probe) keeps only the index_select'ed starts / ends into its source's buffer, so selecting
+    rows costs two device gathers and no device->host read. Kernels take (starts, ends) and so run on either
+    form; :attr:`offsets` (serialisation, shuffles) packs a view in place on first use."""
 
-    __slots__ = ("data", "offsets", "payload", "buf_rows")
+    __slots__ = ("data", "starts", "ends", "_off", "payload", "buf_rows")
 
     def __init__(self, data: torch.Tensor, offsets: torch.Tensor, payload: int, buf_rows: Optional[int] = None):
-        self.data, self.offsets, self.payload = data, offsets, int(payload)
+        self.data, self._off, self.payload = data, offsets, int(payload)
+        self.starts, self.ends = offsets[:-1], offsets[1:]
         self.buf_rows = max(1, offsets.numel() - 1) if buf_rows is None else buf_rows   # rows sharing data
+
+    @staticmethod
+    def view(data: torch.Tensor, starts: torch.Tensor, ends: torch.Tensor, payload: int,
+             buf_rows: int) -> "StringColumn":
+        c = StringColumn.__new__(StringColumn)
+        c.data, c.starts, c.ends, c._off, c.payload, c.buf_rows = data, starts, ends, None, int(payload), buf_rows
+        return c
 
     # ------------------------------------------------------------------ construction
     @staticmethod
@@ -159,15 +173,31 @@ class StringColumn:
         return self.data.device
 
     def __len__(self) -> int:
-        return self.offsets.numel() - 1
+        return self.starts.numel()
+
+    @property
+    def is_packed(self) -> bool:
+        return self._off is not None
+
+    @property
+    def offsets(self) -> torch.Tensor:
+        """[n+1] row offsets; a view is packed into its own buffer first (one device->host read of the size)."""
+        if self._off is None:
+            p = self.compact()
+            self.data, self.starts, self.ends, self._off, self.payload, self.buf_rows = (
+                p.data, p.starts, p.ends, p._off, p.payload, p.buf_rows)
+        return self._off
+
+    def lengths(self) -> torch.Tensor:
+        return self.ends - self.starts
 
     def _host(self):
-        return self.data[: self.payload].cpu().numpy(), self.offsets.cpu().numpy()
+        return self.data[: self.payload].cpu().numpy(), self.starts.cpu().numpy(), self.ends.cpu().numpy()
 
     def tolist(self) -> List[str]:
-        buf, off = self._host()
+        buf, st, en = self._host()
         raw = buf.tobytes()
-        return [raw[s:e].decode() for s, e in zip(off[:-1].tolist(), off[1:].tolist())]
+        return [raw[s:e].decode() for s, e in zip(st.tolist(), en.tolist())]
 
     def __iter__(self):
         return iter(self.tolist())
@@ -181,7 +211,9 @@ class StringColumn:
             if step != 1:
                 return self.take(torch.arange(s, e, step, dtype=torch.long))
             e = max(e, s)
-            return StringColumn(self.data, self.offsets[s:e + 1], self.payload, self.buf_rows)
+            if self._off is not None:
+                return StringColumn(self.data, self._off[s:e + 1], self.payload, self.buf_rows)
+            return StringColumn.view(self.data, self.starts[s:e], self.ends[s:e], self.payload, self.buf_rows)
         if isinstance(i, (torch.Tensor, list, np.ndarray)):
             return self.take(i)
         n = len(self)
@@ -189,63 +221,68 @@ class StringColumn:
             i += n
         if not 0 <= i < n:
             raise IndexError(i)
-        s, e = self.offsets[i:i + 2].tolist()
+        s, e = int(self.starts[i]), int(self.ends[i])
         return bytes(self.data[s:e].cpu().numpy()).decode()
 
     def __repr__(self):
-        return f"StringColumn(n={len(self)}, bytes={self.payload}, device={self.device})"
+        kind = "packed" if self.is_packed else "view"
+        return f"StringColumn(n={len(self)}, {kind}, buffer_bytes={self.payload}, device={self.device})"
 
     @property
     def nbytes(self) -> int:
-        """Bytes this column accounts for: a slice (page) of a shared buffer is charged its row share,
+        """Bytes this column accounts for: a slice / view of a shared buffer is charged its row share,
         estimated without reading the device offsets."""
-        return self.data.numel() * len(self) // self.buf_rows + 8 * self.offsets.numel()
+        return self.data.numel() * len(self) // max(1, self.buf_rows) + 16 * len(self)
 
     def to(self, device) -> "StringColumn":
         device = torch.device(device)
         if device == self.device:
             return self
-        return StringColumn(self.data.to(device, non_blocking=True), self.offsets.to(device, non_blocking=True),
-                            self.payload, self.buf_rows)
+        if self._off is None and len(self) < self.buf_rows // 2:
+            return self.compact().to(device)          # do not move a large shared buffer for a few rows
+        data = self.data.to(device, non_blocking=True)
+        if self._off is not None:
+            return StringColumn(data, self._off.to(device, non_blocking=True), self.payload, self.buf_rows)
+        return StringColumn.view(data, self.starts.to(device, non_blocking=True),
+                                 self.ends.to(device, non_blocking=True), self.payload, self.buf_rows)
 
     def compact(self) -> "StringColumn":
-        """Own buffer holding exactly these rows (after slicing a shared buffer)."""
-        return self.take(torch.arange(len(self), dtype=torch.long, device=self.device))
+        """Own packed buffer holding exactly these rows (one device->host read of the byte total)."""
+        dev, n = self.device, len(self)
+        lens = self.ends - self.starts
+        out_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        if n:
+            torch.cumsum(lens, 0, out=out_off[1:])
+        total = int(out_off[-1]) if n else 0
+        if dev.type == "cuda":
+            data = _ext.hip().str_gather(self.data, self.starts.contiguous(), self.ends.contiguous(), None,
+                                         out_off, total)
+        else:
+            data_np = np.zeros(self._alloc_size(total), dtype=np.uint8)
+            if total:
+                st, ln = self.starts.numpy(), lens.numpy()
+                pos = np.repeat(st - out_off[:-1].numpy(), ln) + np.arange(total)
+                data_np[:total] = self.data.numpy()[pos]
+            data = torch.from_numpy(data_np)
+        return StringColumn(data, out_off, total)
 
     # ------------------------------------------------------------------ relational ops
     def take(self, idx) -> "StringColumn":
+        """Rows ``idx`` (int positions or a bool mask) as a view over this buffer: two index_selects (bounds are
+        checked by index_select itself), no device->host read for int indices."""
         dev = self.device
         if not isinstance(idx, torch.Tensor):
             idx = torch.as_tensor(np.asarray(idx, dtype=np.int64) if len(idx) else np.zeros(0, np.int64))
         idx = idx.to(dev)
         if idx.dtype == torch.bool:
             idx = idx.nonzero().flatten()
-        idx = idx.long().contiguous()
-        n, m = len(self), idx.numel()
-        lens = (self.offsets[1:] - self.offsets[:-1]).index_select(0, idx) if m else idx
-        out_off = torch.zeros(m + 1, dtype=torch.int64, device=dev)
-        if m:
-            torch.cumsum(lens, 0, out=out_off[1:])
-        total = int(out_off[-1]) if m else 0
-        if dev.type == "cuda":
-            if m:   # host-side bound check before the launch (a bad index must never reach the GPU)
-                lo, hi = torch.aminmax(idx)
-                if int(lo) < 0 or int(hi) >= n:
-                    raise IndexError("string take index out of range")
-            data = _ext.hip().str_gather(self.data, self.offsets, idx, out_off, total)
-        else:
+        idx = idx.long()
+        if dev.type != "cuda" and idx.numel():
             ii = idx.numpy()
-            if m and (ii.min() < 0 or ii.max() >= n):
+            if ii.min() < -len(self) or ii.max() >= len(self):
                 raise IndexError("string take index out of range")
-            src = self.data.numpy()
-            off = self.offsets.numpy()
-            data_np = np.zeros(self._alloc_size(total), dtype=np.uint8)
-            if total:
-                starts, ln = off[:-1][ii], (off[1:] - off[:-1])[ii]
-                pos = np.repeat(starts - out_off[:-1].numpy(), ln) + np.arange(total)
-                data_np[:total] = src[pos]
-            data = torch.from_numpy(data_np)
-        return StringColumn(data, out_off, total)
+        return StringColumn.view(self.data, self.starts.index_select(0, idx), self.ends.index_select(0, idx),
+                                 self.payload, self.buf_rows)
 
     def substr(self, start: int, length: int) -> "StringColumn":
         """SQL SUBSTRING(s FROM start + 1 FOR length) of every row, on bytes (0-based ``start``): lengths clamped
@@ -254,43 +291,46 @@ class StringColumn:
         if start < 0 or length < 0:
             raise ValueError("substr: start and length must be >= 0")
         dev, n = self.device, len(self)
-        lens = self.offsets[1:] - self.offsets[:-1]
-        new = (lens - start).clamp(min=0, max=length)
+        new = (self.ends - self.starts - start).clamp(min=0, max=length)
         out_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
         if n:
             torch.cumsum(new, 0, out=out_off[1:])
         cap = n * length
         if dev.type == "cuda":
-            data = _ext.hip().str_slice(self.data, self.offsets.contiguous(), int(start), out_off, cap)
+            data = _ext.hip().str_slice(self.data, self.starts.contiguous(), self.ends.contiguous(), int(start),
+                                        out_off, cap)
         else:
-            src, off, oo = self.data.numpy(), self.offsets.numpy(), out_off.numpy()
+            src, st, oo = self.data.numpy(), self.starts.numpy(), out_off.numpy()
             data_np = np.zeros(self._alloc_size(cap), dtype=np.uint8)
             total = int(oo[-1])
             if total:
                 ln = oo[1:] - oo[:-1]
-                pos = np.repeat(off[:-1] + start - oo[:-1], ln) + np.arange(total)
+                pos = np.repeat(st + start - oo[:-1], ln) + np.arange(total)
                 data_np[:total] = src[pos]
             data = torch.from_numpy(data_np)
         return StringColumn(data, out_off, cap)
 
     @staticmethod
     def concat(parts: Sequence["StringColumn"]) -> "StringColumn":
-        parts = list(parts)
+        parts = [p for p in parts if len(p)] or list(parts[:1])
+        if not parts:
+            return StringColumn.empty()
         dev = parts[0].device
+        parts = [p.to(dev) for p in parts]
+        d0 = parts[0].data
+        if all(p.data is d0 for p in parts):
+            # rows of one buffer (the pages / filtered slices of one set): concatenate the row bounds only
+            return StringColumn.view(d0, torch.cat([p.starts for p in parts]), torch.cat([p.ends for p in parts]),
+                                     max(p.payload for p in parts), max(p.buf_rows for p in parts))
+        parts = [p if p.is_packed else p.compact() for p in parts]
         datas, offs, base = [], [torch.zeros(1, dtype=torch.int64, device=dev)], 0
         for p in parts:
-            p = p.to(dev)
-            o0 = p.offsets[:1]
-            k = len(p)
-            if k == 0:
-                continue
-            o = p.offsets - o0
-            datas.append((p.data, o0, p.offsets[-1:]))
+            o0 = p._off[:1]
+            o = p._off - o0
+            datas.append((p.data, o0, p._off[-1:]))
             offs.append(o[1:] + base)
             base = base + (o[-1])
-        # byte ranges: each part's rows are contiguous in its buffer from offsets[0] to offsets[-1]
-        if not datas:
-            return StringColumn.empty(dev)
+        # byte ranges: each packed part's rows are contiguous in its buffer from offsets[0] to offsets[-1]
         bounds = torch.stack([torch.cat([s, e]) for _, s, e in datas]).cpu().tolist()
         total = sum(e - s for s, e in bounds)
         data = torch.zeros(StringColumn._alloc_size(total), dtype=torch.uint8, device=dev)
@@ -303,8 +343,8 @@ class StringColumn:
     def hash64(self) -> torch.Tensor:
         """int64 hash per row (== :func:`hash_str` of the row)."""
         if self.device.type == "cuda":
-            return _ext.hip().str_hash(self.data, self.offsets, self.payload)
-        return torch.from_numpy(_hash_np(self.data.numpy(), self.offsets.numpy()).copy())
+            return _ext.hip().str_hash(self.data, self.starts.contiguous(), self.ends.contiguous(), self.payload)
+        return torch.from_numpy(_hash_np(self.data.numpy(), self.starts.numpy(), self.ends.numpy()).copy())
 
     def eq_rows(self, ia: Optional[torch.Tensor], other: "StringColumn", ib: Optional[torch.Tensor]) -> torch.Tensor:
         """Byte-exact ``self[ia[i]] == other[ib[i]]`` for every i (ia / ib None: the identity), as a bool mask: the
@@ -314,21 +354,18 @@ class StringColumn:
         other = other.to(dev)
         if m == 0:
             return torch.zeros(0, dtype=torch.bool, device=dev)
-        for idx, col in ((ia, self), (ib, other)):
-            if idx is not None and idx.numel():
-                lo, hi = torch.aminmax(idx)
-                if int(lo) < 0 or int(hi) >= len(col):
-                    raise IndexError("eq_rows index out of range")
+        # resolve the indices into row bounds with index_select (bounds-checked by torch, no host read)
+        sa, ea = (self.starts, self.ends) if ia is None else (self.starts.index_select(0, ia.to(dev).long()),
+                                                              self.ends.index_select(0, ia.to(dev).long()))
+        sb, eb = (other.starts, other.ends) if ib is None else (other.starts.index_select(0, ib.to(dev).long()),
+                                                                other.ends.index_select(0, ib.to(dev).long()))
+        if sb.numel() < m:
+            raise IndexError("eq_rows: other has fewer rows than compared")
         if dev.type == "cuda":
-            ia_ = None if ia is None else ia.to(dev).long().contiguous()
-            ib_ = None if ib is None else ib.to(dev).long().contiguous()
-            return _ext.hip().str_eq_pairs(self.data, self.offsets.contiguous(), ia_, other.data,
-                                           other.offsets.contiguous(), ib_, m)
-        ra = np.arange(m) if ia is None else ia.numpy()
-        rb = np.arange(m) if ib is None else ib.numpy()
-        oa, ob = self.offsets.numpy(), other.offsets.numpy()
-        sa, la = oa[:-1][ra], (oa[1:] - oa[:-1])[ra]
-        sb, lb = ob[:-1][rb], (ob[1:] - ob[:-1])[rb]
+            return _ext.hip().str_eq_pairs(self.data, sa.contiguous(), ea.contiguous(), None, other.data,
+                                           sb.contiguous(), eb.contiguous(), None, m)
+        sa, la = sa.numpy()[:m], (ea - sa).numpy()[:m]
+        sb, lb = sb.numpy()[:m], (eb - sb).numpy()[:m]
         eq = la == lb
         idx = np.nonzero(eq & (la > 0))[0]
         if idx.size:
@@ -344,11 +381,12 @@ class StringColumn:
     def _match(self, compiled, negate=False) -> torch.Tensor:
         pat, st, ln, a0, a1 = compiled
         if self.device.type == "cuda":
-            return _ext.hip().str_like(self.data, self.offsets, self.payload, pat, st, ln, a0, a1, negate)
+            return _ext.hip().str_like(self.data, self.starts.contiguous(), self.ends.contiguous(), self.payload,
+                                       pat, st, ln, a0, a1, negate)
         rx = _like_regex(pat, st, ln, a0, a1)
-        buf, off = self._host()
+        buf, ss, ee = self._host()
         raw = buf.tobytes()
-        out = np.fromiter((rx.search(raw[s:e]) is not None for s, e in zip(off[:-1].tolist(), off[1:].tolist())),
+        out = np.fromiter((rx.search(raw[s:e]) is not None for s, e in zip(ss.tolist(), ee.tolist())),
                           dtype=bool, count=len(self))
         return torch.from_numpy(out != negate)
 

@@ -69,6 +69,14 @@ def test_submit_orders_after_caller_stream_gpu():
     assert torch.all(out == 2)
 
 
+def _long_splitk_operands(dev):
+    # 1024 x 1024 x 65536: 16 tiles x 16 splits = 256 workgroups of 64 k-tiles (a prefetch-eligible launch)
+    g = torch.Generator(device=dev).manual_seed(0)
+    A = torch.empty(1024, 65536, device=dev).uniform_(-1, 1, generator=g).to(torch.bfloat16)
+    B = (torch.empty(1024, 65536, device=dev).uniform_(-1, 1, generator=g) * 0.01).to(torch.bfloat16)
+    return A, B
+
+
 @pytest.mark.gpu
 def test_operand_prefetch_is_taken_once_and_exact_gpu():
     """An operand prefetch armed on the stream is taken by the next long 8-phase GEMM only (results bitwise equal
