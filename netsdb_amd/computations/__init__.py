@@ -298,6 +298,14 @@ class Transpose:
 
 
 @dataclass
+class Scale:
+    """selection multiplying every block by a constant (the LA DSL's ``c * A``; LAParser.y numeric literals with
+    the block-wise pattern of LASillyScaleMultiplyJoin)."""
+
+    scalar: float = 1.0
+
+
+@dataclass
 class Reduce:
     """aggregate reducing a matrix along rows ('row' -> column vector), columns ('col' -> row vector)
     or everything ('all' -> 1x1) with max/min/sum (LASillyRow/Col/Max/MinElement/...Aggregate)."""
@@ -323,5 +331,5 @@ class Duplicate:
 
 __all__ = ["Computation", "ScanSet", "ScanUserSet", "WriteSet", "WriteUserSet", "SelectionComp",
            "MultiSelectionComp", "JoinComp", "AggregateComp", "ClusterAggregateComp", "PartitionComp", "TopKComp",
-           "BlockMatmul", "BlockSum", "BiasAct", "RowSoftmax", "Elementwise", "Transpose", "Reduce", "Inverse",
+           "BlockMatmul", "BlockSum", "BiasAct", "RowSoftmax", "Elementwise", "Transpose", "Scale", "Reduce", "Inverse",
            "Duplicate"]

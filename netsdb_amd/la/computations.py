@@ -10,7 +10,7 @@ from __future__ import annotations
 
 import torch
 
-from ..computations import (AggregateComp, BlockMatmul, Duplicate, Elementwise, Inverse, JoinComp, MultiSelectionComp, Reduce, SelectionComp, Transpose)
+from ..computations import (AggregateComp, BlockMatmul, Duplicate, Elementwise, Inverse, JoinComp, MultiSelectionComp, Reduce, Scale, SelectionComp, Transpose)
 from ..lambdas import make_batch_lambda, make_lambda_from_method
 from ..models.ff import FFAggMatrix, _bmm_nt, mk_blocks
 from ..objects.builtin import MatrixBlock
@@ -112,6 +112,28 @@ class LATransposeSelection(SelectionComp):
 
     def tensor_pattern(self):
         return Transpose()
+
+
+class LAScaleSelection(SelectionComp):
+    """c * A block by block: a selection, so every rank scales only the blocks (rows) it holds — on dense
+    panels the fused lowering keeps A's row partition (no gather), on block records the engine maps each page."""
+
+    def __init__(self, scalar: float):
+        super().__init__()
+        self.scalar = float(scalar)
+
+    def get_projection(self, a):
+        s = self.scalar
+
+        def proj(x: RecordBatch):
+            d = x.columns["data"]
+            return _mb(x.columns["block_row"], x.columns["block_col"], (d.float() * s).to(d.dtype),
+                       x.columns["total_rows"], x.columns["total_cols"])
+
+        return make_batch_lambda(a, proj, tag="scale")
+
+    def tensor_pattern(self):
+        return Scale(self.scalar)
 
 
 class _ReduceAgg(AggregateComp):

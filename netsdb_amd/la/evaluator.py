@@ -127,11 +127,8 @@ class LAInstance:
         return name
 
     def _scale(self, m: str, scalar: float) -> str:
-        name = self._new()
-        src = self.client.storage.get_set(DB, m)
-        t = B.to_tensor(self.client, DB, m, gather=True)
-        B.load_tensor(self.client, DB, name, (t.float() * scalar), src.block_rows, src.block_cols, dtype=self.dtype)
-        return name
+        """``c * A``: one distributed selection job (LAScaleSelection), each rank scaling the blocks it holds."""
+        return self._run(L.LAScaleSelection(scalar).set_input(self._scan(m)), "la_scale")
 
 
 __all__ = ["LAInstance", "DB"]

@@ -35,7 +35,7 @@ import torch.distributed as dist
 from .. import ops
 from ..computations import (AggregateComp, BiasAct, BlockMatmul, BlockSum, CellUpdate, Computation, Duplicate,
                             Elementwise, GateSum, HiddenOut, Inverse, JoinComp, MultiSelectionComp, Reduce, RowSoftmax,
-                            ScanSet, SelectionComp, Transpose, WriteSet)
+                            ScanSet, Scale, SelectionComp, Transpose, WriteSet)
 from ..storage.sets import DenseMatrixSet
 
 _tmp_ids = itertools.count()
@@ -812,6 +812,21 @@ class TransposeNode(Node):
         return self.value
 
 
+class ScaleNode(Node):
+    """c * X on the value as it is laid out and distributed: each rank scales its own rows / columns."""
+
+    def __init__(self, x: Node, scalar: float):
+        self.x, self.scalar = x, scalar
+
+    def eval(self, engine) -> Dense:
+        if self.value is None:
+            X = self.x.eval(engine)
+            p = X.phys
+            y = (p.float() * self.scalar).to(p.dtype)
+            self.value = Dense(y, X.rows, X.cols, X.transposed, X.br, X.bc, X.part, X.offset, X.total)
+        return self.value
+
+
 def _dop(op):
     return {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
 
@@ -981,6 +996,12 @@ class Fuser:
                 return None
             self.fused.append(f"transpose[{name}]")
             return TransposeNode(x)
+        if isinstance(c, SelectionComp) and isinstance(pat, Scale):
+            x = self.match(c.inputs[0])
+            if x is None:
+                return None
+            self.fused.append(f"scale[{name}]")
+            return ScaleNode(x, pat.scalar)
         if isinstance(c, AggregateComp) and isinstance(pat, Reduce):
             x = self.match(c.inputs[0])
             if x is None:

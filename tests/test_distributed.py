@@ -129,6 +129,13 @@ def _la_dist_scenario(ctx, out_dir):
         res[tag] = (C.float() - ref).abs().max().item()
         res[f"{tag}_shape"] = tuple(C.shape)
         res[f"{tag}_fused"] = st.get("fused_ops")
+    # 2 * A (LA DSL scalar multiply): a selection over A's own row partition, no gather
+    c.create_set("LA_db", "C_scale", None, dense=True)
+    st = c.execute_computations(WriteSet("LA_db", "C_scale").set_input(L.LAScaleSelection(2.0).set_input(
+        ScanSet("LA_db", "A"))))
+    res["scale_local_rows"] = c.get_set("LA_db", "C_scale").local_rows
+    res["scale"] = (B.to_tensor(c, "LA_db", "C_scale").float() - 2 * A).abs().max().item()
+    res["scale_fused"] = st.get("fused_ops")
     return res
 
 
@@ -144,6 +151,8 @@ def test_distributed_la_partitioned_matmuls(tensor_coll, monkeypatch):
     assert r0["local_rows"] == 24 and r1["local_rows"] == 16
     for r in (r0, r1):
         assert r["mul"] < 1e-4 and r["tmul"] < 1e-4, r
+        assert r["scale"] < 1e-6 and r["scale_local_rows"] == r["local_rows"], r
+        assert any("scale" in f for f in r["scale_fused"])
         assert r["mul_shape"] == (40, 24) and r["tmul_shape"] == (40, 24)
         assert any("matmul" in f for f in r["tmul_fused"])
 
@@ -521,6 +530,7 @@ def test_distributed_8ranks_uneven_la_ff_dedup_engine():
     assert [r["local_rows"] for r in res] == [8, 8, 8, 8, 8, 0, 0, 0]
     for r in res:
         assert r["mul"] < 1e-4 and r["tmul"] < 1e-4, r
+        assert r["scale"] < 1e-6 and r["scale_local_rows"] == r["local_rows"], r   # 2 * A stays row-partitioned
         assert r["mul_shape"] == (40, 24) and r["tmul_shape"] == (40, 24)
     wide = _run("_kpartial_wide_scenario", ws=8)
     for r in wide:
