@@ -262,35 +262,64 @@ __device__ __forceinline__ void row_into_global(GTable g, u64 k, const VT* v, in
 }
 
 // ---------------------------------------------------------------- sample estimate
+// One workgroup hashes 4096 evenly spaced rows into an LDS table with per-key counts and writes the Chao1
+// estimate of the distinct keys, d + f1^2 / (2 f2) (f1 / f2: keys seen once / twice in the sample; exact d when
+// every row was sampled), clamped to [d, n]. The PART path sizes its sub-partitions from it.
 __global__ __launch_bounds__(1024) void agg_sample_kernel(const u64* __restrict__ keys, i64 n, int low_thr,
                                                           AggMeta* meta) {
   constexpr int S = 4096, CAP = 8192;
   __shared__ u64 tab[CAP];
-  __shared__ int count;
-  for (int i = threadIdx.x; i < CAP; i += blockDim.x) tab[i] = kEmpty;
-  if (threadIdx.x == 0) count = 0;
+  __shared__ unsigned tcnt[CAP];
+  __shared__ unsigned fsum[3];
+  for (int i = threadIdx.x; i < CAP; i += blockDim.x) {
+    tab[i] = kEmpty;
+    tcnt[i] = 0;
+  }
+  if (threadIdx.x < 3) fsum[threadIdx.x] = 0;
   __syncthreads();
   const int ns = (int)std::min<i64>(S, n);
-  for (int i = threadIdx.x; i < ns; i += blockDim.x) {
+  u64 kk[S / 1024];
+#pragma unroll
+  for (int j = 0; j < S / 1024; ++j) {   // all four loads in flight before the first insert
+    const int i = threadIdx.x + j * 1024;
     const i64 r = (n <= S) ? i : ((i64)i * n) / S;   // n < 2^31: no overflow
-    const u64 k = keys[r];
+    kk[j] = i < ns ? keys[r] : kEmpty;
+  }
+#pragma unroll
+  for (int j = 0; j < S / 1024; ++j) {
+    const u64 k = kk[j];
     if (k == kEmpty) continue;
     int s = (int)(mix64(k) & (CAP - 1));
     for (;;) {
       u64 e = kEmpty;
-      if (__hip_atomic_compare_exchange_strong(tab + s, &e, k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP)) {
-        atomicAdd(&count, 1);
+      __hip_atomic_compare_exchange_strong(tab + s, &e, k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (e == kEmpty || e == k) {
+        atomicAdd(tcnt + s, 1u);
         break;
       }
-      if (e == k) break;
       s = (s + 1) & (CAP - 1);
     }
   }
   __syncthreads();
+  unsigned d = 0, f1 = 0, f2 = 0;
+  for (int i = threadIdx.x; i < CAP; i += blockDim.x) {
+    const unsigned c = tcnt[i];
+    d += c > 0;
+    f1 += c == 1;
+    f2 += c == 2;
+  }
+  atomicAdd(fsum, d);
+  atomicAdd(fsum + 1, f1);
+  atomicAdd(fsum + 2, f2);
+  __syncthreads();
   if (threadIdx.x == 0) {
-    meta->est = count;
-    meta->low = count <= low_thr ? 1 : 0;
+    const double dd = fsum[0], g1 = fsum[1], g2 = fsum[2];
+    double est = dd;
+    if (n > S) est = g2 > 0 ? dd + g1 * g1 / (2.0 * g2) : dd + g1 * (g1 - 1) / 2.0;
+    est = std::min(est, (double)n);
+    meta->est = (i64)est;
+    meta->low = est <= (double)low_thr ? 1 : 0;
   }
 }
 
@@ -330,7 +359,8 @@ __global__ __launch_bounds__(256) void agg_low_kernel(const u64* __restrict__ ke
     if (s >= 0) {
       for (int f = 0; f < F; ++f) acc_add<VT, OP, __HIP_MEMORY_SCOPE_WORKGROUP>(t.acc + s * F + f, v[f]);
       __hip_atomic_fetch_add(t.cnt + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      __hip_atomic_fetch_min(t.rmin + s, (u64)i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      // rows arrive in increasing order per thread: after a key's first stride the minimum is settled
+      if ((u64)i < t.rmin[s]) __hip_atomic_fetch_min(t.rmin + s, (u64)i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     } else {
       row_into_global<VT, OP>(g, k, v, F, &meta->ng_low, &meta->sentinel_low, &meta->fail_low, o, i);
     }
@@ -452,116 +482,246 @@ __global__ __launch_bounds__(1024) void scan_tot_kernel(const i64* __restrict__ 
   }
 }
 
-// pack rows bucket-contiguous: pkey[pos], pval[pos * F + f], prow[pos]
+// Exclusive scan over a block of 1024 threads (one value each); returns the prefix, *total the block sum.
+__device__ __forceinline__ unsigned block_scan_excl(unsigned v, unsigned* wsum, unsigned* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  unsigned x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) wsum[wave] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned run = 0;
+    for (int w = 0; w < nw; ++w) {
+      const unsigned t = wsum[w];
+      wsum[w] = run;
+      run += t;
+    }
+    *total = run;
+  }
+  __syncthreads();
+  return wsum[wave] + x - v;
+}
+
+// Tile-staged scatter of rows [r0, r1) (read through rows_of, or 0..: plain row ids) into bucket runs: each
+// 1024-thread pass stages up to T rows in LDS sorted by bucket (counting sort: LDS histogram, block scan,
+// ranks from the histogram atomics), then writes each bucket's run contiguously at run[b], so the global
+// stores are long coalesced runs instead of one random 8-byte store per row. run[] (LDS, i64 [P]) is
+// advanced by the tile's counts. Row order inside a bucket is not preserved (the aggregates keep min row ids).
+template <typename VT>
+__device__ __forceinline__ void staged_scatter(const u64* __restrict__ skey, const VT* __restrict__ sval,
+                                               const int* __restrict__ srow, i64 r0, i64 r1, int F, int shift,
+                                               int P, int T, char* lds, i64* run, unsigned* cnt, unsigned* off,
+                                               unsigned* wsum, u64* __restrict__ dkey, VT* __restrict__ dval,
+                                               int* __restrict__ drow) {
+  constexpr int R = 4;   // rows per thread per tile (T <= 4096)
+  u64* st_key = reinterpret_cast<u64*>(lds);
+  VT* st_val = reinterpret_cast<VT*>(st_key + T);
+  int* st_row = reinterpret_cast<int*>(st_val + (size_t)T * F);
+  unsigned short* st_b = reinterpret_cast<unsigned short*>(st_row + T);
+  __shared__ unsigned tot_sh;
+  const unsigned pmask = (unsigned)P - 1;
+  for (i64 t0 = r0; t0 < r1; t0 += T) {
+    const int tn = (int)std::min<i64>(T, r1 - t0);
+    for (int b = threadIdx.x; b < P; b += blockDim.x) cnt[b] = 0;
+    __syncthreads();
+    u64 k[R];
+    int bk[R];
+    unsigned rk[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int p = threadIdx.x + j * 1024;
+      k[j] = p < tn ? skey[t0 + p] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int p = threadIdx.x + j * 1024;
+      if (p < tn) {
+        bk[j] = P == 1 ? 0 : (int)((mix64(k[j]) >> shift) & pmask);
+        rk[j] = atomicAdd(cnt + bk[j], 1u);
+      }
+    }
+    __syncthreads();
+    // exclusive scan of cnt[0..P) (P <= 4096: up to 4 buckets per thread)
+    {
+      const int per = (P + 1023) / 1024;
+      const int c0 = threadIdx.x * per;
+      unsigned sum = 0;
+      for (int c = c0; c < c0 + per && c < P; ++c) sum += cnt[c];
+      unsigned pre = block_scan_excl(sum, wsum, &tot_sh);
+      for (int c = c0; c < c0 + per && c < P; ++c) {
+        off[c] = pre;
+        pre += cnt[c];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int p = threadIdx.x + j * 1024;
+      if (p < tn) {
+        const unsigned q = off[bk[j]] + rk[j];
+        const i64 i = t0 + p;
+        st_key[q] = k[j];
+        st_row[q] = srow ? srow[i] : (int)i;
+        st_b[q] = (unsigned short)bk[j];
+        for (int f = 0; f < F; ++f) st_val[(size_t)q * F + f] = sval[i * F + f];
+      }
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < tn; q += blockDim.x) {
+      const int b = st_b[q];
+      const i64 dst = run[b] + (q - (int)off[b]);
+      dkey[dst] = st_key[q];
+      drow[dst] = st_row[q];
+      for (int f = 0; f < F; ++f) dval[dst * F + f] = st_val[(size_t)q * F + f];
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < P; b += blockDim.x) run[b] += cnt[b];
+    __syncthreads();
+  }
+}
+
+// level-1 scatter: workgroup g packs its rows [g * rpw, ...) into the P1 buckets at bstart[b] + hist[b][g]
 template <typename VT>
 __global__ __launch_bounds__(1024) void agg_scatter_kernel(const u64* __restrict__ keys, const VT* __restrict__ vals,
-                                                           i64 n, int F, i64 rpw, int pbits,
+                                                           i64 n, int F, i64 rpw, int pbits, int T,
                                                            const unsigned* __restrict__ hist,
                                                            const i64* __restrict__ bstart, u64* __restrict__ pkey,
                                                            VT* __restrict__ pval, int* __restrict__ prow,
                                                            const AggMeta* meta) {
   if (!take_part(meta)) return;
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
-  unsigned* c = reinterpret_cast<unsigned*>(lds_raw);
+  __shared__ i64 run[1024];
+  __shared__ unsigned cnt[1024], off[1024], wsum[16];
   const int P = 1 << pbits;
-  for (int b = threadIdx.x; b < P; b += blockDim.x) c[b] = 0;
+  for (int b = threadIdx.x; b < P; b += blockDim.x) run[b] = bstart[b] + hist[(size_t)b * gridDim.x + blockIdx.x];
   __syncthreads();
   const i64 r0 = (i64)blockIdx.x * rpw, r1 = std::min<i64>(n, r0 + rpw);
-  for (i64 i = r0 + threadIdx.x; i < r1; i += blockDim.x) {
-    const u64 k = keys[i];
-    const int b = bucket_of(k, pbits);
-    const i64 pos = bstart[b] + hist[(size_t)b * gridDim.x + blockIdx.x] + atomicAdd(c + b, 1u);
-    pkey[pos] = k;
-    for (int f = 0; f < F; ++f) pval[pos * F + f] = vals[i * F + f];
-    prow[pos] = (int)i;
-  }
+  staged_scatter<VT>(keys, vals, nullptr, r0, r1, F, 64 - pbits, P, T, lds_raw, run, cnt, off, wsum, pkey, pval, prow);
 }
 
+// Aggregate rows [r0, r1) of (key, val, row) in the LDS table (clearing it to cap entries first), then write the
+// groups straight to the dense output: the caller guarantees the range holds every row of its keys. Rows whose
+// LDS probe window is full go to the global table (emitted later by agg_emit).
 template <typename VT, int OP>
-__global__ __launch_bounds__(256) void agg_part_kernel(const u64* __restrict__ pkey, const VT* __restrict__ pval,
-                                                       const int* __restrict__ prow, int F, int lcap, int P, i64 ch,
-                                                       const i64* __restrict__ bstart, const i64* __restrict__ wstart,
-                                                       GTable g, AggMeta* meta, AggOut o) {
-  if (!take_part(meta)) return;
-  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
-  LTable t = ltable_at(lds_raw, lcap, F);
-  __shared__ i64 w_sh;
+__device__ __forceinline__ void agg_range_dense(const u64* __restrict__ pkey, const VT* __restrict__ pval,
+                                                const int* __restrict__ prow, i64 r0, i64 r1, int F, LTable t,
+                                                GTable g, AggMeta* meta, AggOut o) {
   __shared__ int nocc;
   __shared__ i64 base_sh;
-  const i64 nwork = meta->nwork;
-  for (;;) {
-    if (threadIdx.x == 0) w_sh = __hip_atomic_fetch_add(&meta->wnext, (i64)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    ltable_clear<VT, OP>(t, F);
-    if (threadIdx.x == 0) nocc = 0;
-    __syncthreads();
-    const i64 w = w_sh;
-    if (w >= nwork) return;   // every workgroup reaches this once the list is drained
-    // bucket of work item w: last b with wstart[b] <= w
-    int lo = 0, hi = P - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (wstart[mid] <= w) lo = mid;
-      else hi = mid - 1;
+  ltable_clear<VT, OP>(t, F);
+  if (threadIdx.x == 0) nocc = 0;
+  __syncthreads();
+  for (i64 r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
+    const u64 k = pkey[r];
+    const VT* v = pval + r * F;
+    const int row = prow[r];
+    int s = -1;
+    if (k != kEmpty) s = ltable_slot(t, k, mix64(k));
+    if (s >= 0) {
+      for (int f = 0; f < F; ++f) acc_add<VT, OP, __HIP_MEMORY_SCOPE_WORKGROUP>(t.acc + s * F + f, v[f]);
+      __hip_atomic_fetch_add(t.cnt + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if ((u64)row < t.rmin[s]) __hip_atomic_fetch_min(t.rmin + s, (u64)row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+      row_into_global<VT, OP>(g, k, v, F, &meta->ng_part, &meta->sentinel_part, &meta->fail_part, o, row);
     }
-    const int b = lo;
-    const i64 chunks = wstart[b + 1] - wstart[b];
-    const i64 r0 = bstart[b] + (w - wstart[b]) * ch, r1 = std::min(bstart[b + 1], r0 + ch);
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < t.cap; e += blockDim.x)
+    if (t.key[e] != kEmpty) t.ref[e] = atomicAdd(&nocc, 1);   // local id (any order)
+  __syncthreads();
+  if (threadIdx.x == 0 && nocc)
+    base_sh = __hip_atomic_fetch_add(&meta->ng_part, (i64)nocc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const i64 base = base_sh;
+  for (int e = threadIdx.x; e < t.cap; e += blockDim.x) {
+    const u64 k = t.key[e];
+    if (k == kEmpty) continue;
+    const i64 gid = base + t.ref[e];
+    t.ref[e] = gid;
+    o.reps[gid] = (i64)k;
+    o.cnt[gid] = (i64)t.cnt[e];
+    o.first[gid] = (i64)t.rmin[e];
+    o.slot_of_gid[gid] = -1;
+    for (int f = 0; f < F; ++f) o.aggs[gid * F + f] = acc_out<VT, OP>(t.acc[e * F + f]);
+  }
+  if (o.inv != nullptr) {
+    __syncthreads();
     for (i64 r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
       const u64 k = pkey[r];
-      const VT* v = pval + r * F;
-      int s = -1;
-      if (k != kEmpty) s = ltable_slot(t, k, mix64(k));
-      const int row = prow[r];
-      if (s >= 0) {
-        for (int f = 0; f < F; ++f) acc_add<VT, OP, __HIP_MEMORY_SCOPE_WORKGROUP>(t.acc + s * F + f, v[f]);
-        __hip_atomic_fetch_add(t.cnt + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_fetch_min(t.rmin + s, (u64)row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      } else {
-        row_into_global<VT, OP>(g, k, v, F, &meta->ng_part, &meta->sentinel_part, &meta->fail_part, o, row);
-      }
+      if (k == kEmpty) continue;
+      const int s = ltable_find(t, k, mix64(k));
+      if (s >= 0) o.inv[prow[r]] = t.ref[s];
     }
-    __syncthreads();
-    if (chunks == 1) {
-      // the bucket is this chunk: its groups occur nowhere else -> dense output directly
-      for (int e = threadIdx.x; e < lcap; e += blockDim.x)
-        if (t.key[e] != kEmpty) t.ref[e] = atomicAdd(&nocc, 1);   // local id (any order)
-      __syncthreads();
-      if (threadIdx.x == 0) base_sh = __hip_atomic_fetch_add(&meta->ng_part, (i64)nocc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __syncthreads();
-      const i64 base = base_sh;
-      for (int e = threadIdx.x; e < lcap; e += blockDim.x) {
-        const u64 k = t.key[e];
-        if (k == kEmpty) continue;
-        const i64 gid = base + t.ref[e];
-        t.ref[e] = gid;
-        o.reps[gid] = (i64)k;
-        o.cnt[gid] = (i64)t.cnt[e];
-        o.first[gid] = (i64)t.rmin[e];
-        o.slot_of_gid[gid] = -1;
-        for (int f = 0; f < F; ++f) o.aggs[gid * F + f] = acc_out<VT, OP>(t.acc[e * F + f]);
-      }
-    } else {
-      for (int e = threadIdx.x; e < lcap; e += blockDim.x) {
-        const u64 k = t.key[e];
-        if (k == kEmpty) continue;
-        const i64 s = gtable_slot(g, k, &meta->ng_part, &meta->sentinel_part, &meta->fail_part, o);
-        t.ref[e] = -(s + 1);
-        if (s < 0) continue;
-        for (int f = 0; f < F; ++f) acc_merge_global<VT, OP>(g.acc + s * F + f, t.acc[e * F + f]);
-        __hip_atomic_fetch_add(g.cnt + s, (u64)t.cnt[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_min(g.rmin + s, t.rmin[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+  }
+  __syncthreads();
+}
+
+// Workgroup b owns level-1 bucket b whole (no other workgroup sees its keys). When the estimated distinct keys
+// of the bucket fit the LDS table at load <= 1/2 it aggregates the bucket directly; otherwise it first splits the
+// bucket into P2 sub-buckets by the next hash bits (its own histogram + staged scatter into the second buffer,
+// same positions) and aggregates them one after another. No global atomics per row, one per group run.
+template <typename VT, int OP>
+__global__ __launch_bounds__(1024) void agg_bucket_kernel(const u64* __restrict__ pkey, const VT* __restrict__ pval,
+                                                          const int* __restrict__ prow, int F, int lcap, int p1bits,
+                                                          int T, i64 n, const i64* __restrict__ bstart,
+                                                          u64* __restrict__ qkey, VT* __restrict__ qval,
+                                                          int* __restrict__ qrow, GTable g, AggMeta* meta, AggOut o) {
+  if (!take_part(meta)) return;
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  __shared__ i64 run[1024];
+  __shared__ unsigned cnt[1024], off[1024], wsum[16], sb[1025];
+  const int b = blockIdx.x;
+  const i64 r0 = bstart[b], r1 = bstart[b + 1], nb = r1 - r0;
+  if (nb == 0) return;
+  const int P1 = 1 << p1bits;
+  // expected distinct keys of this bucket: the estimate's share, with 2x slack, never above its rows
+  const i64 est = meta->est;
+  const i64 db = std::min<i64>(nb, 2 * ((est + P1 - 1) / P1) + 16);
+  int p2bits = 0;
+  while (p2bits < 10 && (db >> p2bits) * 2 > lcap) ++p2bits;
+  if (p2bits == 0) {
+    int cap = 64;
+    while (cap < lcap && cap < 2 * db) cap <<= 1;
+    agg_range_dense<VT, OP>(pkey, pval, prow, r0, r1, F, ltable_at(lds_raw, cap, F), g, meta, o);
+    return;
+  }
+  const int P2 = 1 << p2bits;
+  const int shift = 64 - p1bits - p2bits;
+  const unsigned pmask = (unsigned)P2 - 1;
+  // histogram of the sub-buckets
+  for (int c = threadIdx.x; c < P2; c += blockDim.x) cnt[c] = 0;
+  __syncthreads();
+  for (i64 r = r0 + threadIdx.x; r < r1; r += blockDim.x) atomicAdd(cnt + ((mix64(pkey[r]) >> shift) & pmask), 1u);
+  __syncthreads();
+  {
+    unsigned tot;
+    const unsigned v = threadIdx.x < P2 ? cnt[threadIdx.x] : 0u;
+    const unsigned pre = block_scan_excl(v, wsum, &tot);
+    if (threadIdx.x < P2) {
+      sb[threadIdx.x] = pre;
+      run[threadIdx.x] = r0 + pre;
     }
-    if (o.inv != nullptr) {
-      __syncthreads();
-      for (i64 r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
-        const u64 k = pkey[r];
-        if (k == kEmpty) continue;
-        const int s = ltable_find(t, k, mix64(k));
-        if (s >= 0) o.inv[prow[r]] = t.ref[s];
-      }
-    }
-    __syncthreads();
+    if (threadIdx.x == 0) sb[P2] = (unsigned)nb;
+  }
+  __syncthreads();
+  staged_scatter<VT>(pkey, pval, prow, r0, r1, F, shift, P2, T, lds_raw, run, cnt, off, wsum, qkey, qval, qrow);
+  // this workgroup reads back what its own waves stored: drain the stores, then drop this CU's L1 lines
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const i64 dsub = std::min<i64>(nb, (db >> p2bits) + 16);
+  int cap = 64;
+  while (cap < lcap && cap < 2 * dsub) cap <<= 1;
+  const LTable t = ltable_at(lds_raw, cap, F);
+  for (int s2 = 0; s2 < P2; ++s2) {
+    const i64 a = r0 + sb[s2], e = r0 + sb[s2 + 1];
+    if (a < e) agg_range_dense<VT, OP>(qkey, qval, qrow, a, e, F, t, g, meta, o);
   }
 }
 
@@ -592,10 +752,17 @@ __global__ __launch_bounds__(256) void agg_fix_inv_kernel(i64* __restrict__ inv,
 }
 
 // ---------------------------------------------------------------- hash join
-// build: tkey[cap + 1] preset kEmpty, tcnt[cap + 1] preset 0; row_slot / row_rank per build row
-__global__ __launch_bounds__(256) void join_insert_kernel(const u64* __restrict__ keys, i64 n, u64* tkey,
-                                                          unsigned* tcnt, u64 mask, int* __restrict__ row_slot,
-                                                          unsigned* __restrict__ row_rank) {
+// Table: cap + 1 16-byte slots {key, cnt | pay << 32} (slot cap: the kEmpty key). pay = the build row itself when
+// the key has one build row (the primary-key case), else the start of its CSR run in perm. A probe row is then
+// ONE 16-byte random read (key, count and row together) and, for unique build keys, no second lookup.
+struct JSlot {
+  u64 key;
+  unsigned cnt;
+  unsigned pay;
+};
+
+__global__ __launch_bounds__(256) void join_insert_kernel(const u64* __restrict__ keys, i64 n, JSlot* tab, u64 mask,
+                                                          int* __restrict__ row_slot, unsigned* __restrict__ row_rank) {
   for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) {
     const u64 k = keys[i];
     u64 s;
@@ -604,9 +771,9 @@ __global__ __launch_bounds__(256) void join_insert_kernel(const u64* __restrict_
     } else {
       s = mix64(k) & mask;
       for (;;) {   // the table has >= 2 slots per build row: the key or an empty slot is always met
-        u64 cur = __hip_atomic_load(tkey + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        u64 cur = __hip_atomic_load(&tab[s].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (cur == kEmpty) {
-          if (__hip_atomic_compare_exchange_strong(tkey + s, &cur, k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+          if (__hip_atomic_compare_exchange_strong(&tab[s].key, &cur, k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_AGENT))
             break;
         }
@@ -615,60 +782,118 @@ __global__ __launch_bounds__(256) void join_insert_kernel(const u64* __restrict_
       }
     }
     row_slot[i] = (int)s;
-    row_rank[i] = __hip_atomic_fetch_add(tcnt + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    row_rank[i] = __hip_atomic_fetch_add(&tab[s].cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
-// perm[toff[slot] + rank] = row: build rows grouped by key (CSR over the slots)
+// perm[toff[slot] + rank] = row (build rows grouped by key); the rank-0 row writes the slot's payload
 __global__ __launch_bounds__(256) void join_perm_kernel(const int* __restrict__ row_slot,
                                                         const unsigned* __restrict__ row_rank, i64 n,
-                                                        const i64* __restrict__ toff, i64* __restrict__ perm) {
-  for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x)
-    perm[toff[row_slot[i]] + row_rank[i]] = i;
-}
-
-// probe: matches per probe row (cnt) and the slot they sit in
-__global__ __launch_bounds__(256) void join_probe_kernel(const u64* __restrict__ keys, i64 m, const u64* __restrict__ tkey,
-                                                         const unsigned* __restrict__ tcnt, u64 mask,
-                                                         i64* __restrict__ cnt, int* __restrict__ slot) {
-  for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (i64)gridDim.x * blockDim.x) {
-    const u64 k = keys[i];
-    i64 c = 0;
-    int sl = -1;
-    if (k == kEmpty) {
-      sl = (int)(mask + 1);
-      c = tcnt[sl];
-    } else {
-      u64 s = mix64(k) & mask;
-      for (;;) {
-        const u64 cur = tkey[s];
-        if (cur == k) {
-          sl = (int)s;
-          c = tcnt[s];
-          break;
-        }
-        if (cur == kEmpty) break;
-        s = (s + 1) & mask;
-      }
-    }
-    cnt[i] = c;
-    slot[i] = sl;
+                                                        const i64* __restrict__ toff, JSlot* tab,
+                                                        i64* __restrict__ perm) {
+  for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) {
+    const int s = row_slot[i];
+    const unsigned r = row_rank[i];
+    const i64 o = toff[s];
+    perm[o + r] = i;
+    if (r == 0) tab[s].pay = tab[s].cnt == 1 ? (unsigned)i : (unsigned)o;
   }
 }
 
-// expand: probe row i owns output rows [ooff[i] - cnt[i], ooff[i]) (ooff = inclusive scan of cnt)
-__global__ __launch_bounds__(256) void join_expand_kernel(const i64* __restrict__ cnt, const i64* __restrict__ ooff,
-                                                          const int* __restrict__ slot, i64 m,
-                                                          const i64* __restrict__ toff, const i64* __restrict__ perm,
-                                                          i64* __restrict__ bidx, i64* __restrict__ pidx) {
-  for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (i64)gridDim.x * blockDim.x) {
-    const i64 c = cnt[i];
-    if (c == 0) continue;
-    const i64 o = ooff[i] - c, b0 = toff[slot[i]];
-    for (i64 j = 0; j < c; ++j) {
-      bidx[o + j] = perm[b0 + j];
-      pidx[o + j] = i;
+constexpr int kJTile = 4096;   // probe rows per workgroup tile (256 threads x 16)
+
+__device__ __forceinline__ void jslot_find(const JSlot* __restrict__ tab, u64 mask, u64 k, unsigned& c,
+                                           unsigned& pay) {
+  c = 0;
+  pay = 0;
+  u64 s = k == kEmpty ? mask + 1 : mix64(k) & mask;
+  for (;;) {
+    const JSlot e = tab[s];   // one 16-byte load
+    if (e.key == k) {
+      c = e.cnt;
+      pay = e.pay;
+      return;
     }
+    if (e.key == kEmpty || k == kEmpty) return;
+    s = (s + 1) & mask;
+  }
+}
+
+// probe: matches (cnt) and payload per probe row, and the match total of each 4096-row tile
+__global__ __launch_bounds__(256) void join_probe_kernel(const u64* __restrict__ keys, i64 m,
+                                                         const JSlot* __restrict__ tab, u64 mask,
+                                                         unsigned* __restrict__ cnt, unsigned* __restrict__ pay,
+                                                         i64* __restrict__ tile_sum) {
+  __shared__ unsigned ws[4];
+  const i64 t0 = (i64)blockIdx.x * kJTile;
+  unsigned local = 0;
+  u64 k[kJTile / 256];
+#pragma unroll
+  for (int j = 0; j < kJTile / 256; ++j) {
+    const i64 i = t0 + j * 256 + threadIdx.x;
+    k[j] = i < m ? keys[i] : 0;
+  }
+#pragma unroll
+  for (int j = 0; j < kJTile / 256; ++j) {
+    const i64 i = t0 + j * 256 + threadIdx.x;
+    if (i < m) {
+      unsigned c, p;
+      jslot_find(tab, mask, k[j], c, p);
+      cnt[i] = c;
+      pay[i] = p;
+      local += c;
+    }
+  }
+  // workgroup sum
+  for (int d = 32; d > 0; d >>= 1) local += __shfl_down(local, d, 64);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = local;
+  __syncthreads();
+  if (threadIdx.x == 0) tile_sum[blockIdx.x] = (i64)ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+// expand: tile bases = exclusive scan of tile_sum; inside a tile, a block scan per 256-row slab gives each probe
+// row its output offset, so pairs come out probe-major with no full-length scan pass
+__global__ __launch_bounds__(256) void join_expand_kernel(const unsigned* __restrict__ cnt,
+                                                          const unsigned* __restrict__ pay, i64 m,
+                                                          const i64* __restrict__ tile_base,
+                                                          const i64* __restrict__ perm, i64* __restrict__ bidx,
+                                                          i64* __restrict__ pidx) {
+  __shared__ unsigned wsum[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const i64 t0 = (i64)blockIdx.x * kJTile;
+  i64 base = tile_base[blockIdx.x];
+  for (int j = 0; j < kJTile / 256; ++j) {
+    const i64 i = t0 + j * 256 + threadIdx.x;
+    const unsigned c = i < m ? cnt[i] : 0u;
+    unsigned x = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const unsigned y = __shfl_up(x, d, 64);
+      if (lane >= d) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    unsigned before = 0, slab = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const unsigned t = wsum[w];
+      before += w < wave ? t : 0u;
+      slab += t;
+    }
+    const i64 o = base + before + x - c;
+    if (c == 1) {
+      const unsigned p = pay[i];
+      bidx[o] = (i64)p;
+      pidx[o] = i;
+    } else if (c > 1) {
+      const i64 b0 = (i64)pay[i];
+      for (unsigned q = 0; q < c; ++q) {
+        bidx[o + q] = perm[b0 + q];
+        pidx[o + q] = i;
+      }
+    }
+    base += slab;
+    __syncthreads();
   }
 }
 
@@ -732,6 +957,12 @@ __global__ __launch_bounds__(1024) void part_scatter_kernel(const i64* __restric
 }
 
 // ---------------------------------------------------------------- host launchers
+// rows staged per scatter pass: a multiple of 1024, <= 4096, staging <= 96 KB
+inline int stage_rows(int F) {
+  const int t = (int)((96 * 1024) / (14 + 8 * F)) / 1024 * 1024;
+  return std::max(1024, std::min(4096, t));
+}
+
 template <typename VT, int OP>
 int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv, void* meta_v, void* glow_v,
                  i64 gcap_low, void* gpart_v, i64 gcap_part, void* out_v, void* work_v, int pbits, int lcap_low,
@@ -768,7 +999,7 @@ int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv,
   hipLaunchKernelGGL(agg_sample_kernel, dim3(1), dim3(1024), 0, st, k, n, low_thr, meta);
   const int gl = (int)std::min<i64>(1024, std::max<i64>(1, (n + 2047) / 2048));
   hipLaunchKernelGGL((agg_low_kernel<VT, OP>), dim3(gl), dim3(256), lbytes_low, st, k, v, n, F, lcap_low, glow, meta, o);
-  // PART: work buffers [hist P*G u32 | tot P | bstart P+1 | wstart P+1 | pkey n | pval n*F | prow n (i32)]
+  // PART: work buffers [hist P*G u32 | tot P | bstart P+1 | pkey n | pval n*F | prow n (i32) | qkey | qval | qrow]
   const int P = 1 << pbits;
   const int G = (int)std::min<i64>(256, std::max<i64>(1, (n + 16383) / 16384));
   const i64 rpw = (n + G - 1) / G;
@@ -776,18 +1007,22 @@ int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv,
   unsigned* hist = reinterpret_cast<unsigned*>(w);
   i64* tot = reinterpret_cast<i64*>(w + (((size_t)P * G * 4 + 15) & ~(size_t)15));
   i64* bstart = tot + P;
-  i64* wstart = bstart + P + 1;
-  u64* pkey = reinterpret_cast<u64*>(wstart + P + 1);
+  u64* pkey = reinterpret_cast<u64*>(bstart + P + 2);
   VT* pval = reinterpret_cast<VT*>(pkey + n);
   int* prow = reinterpret_cast<int*>(pval + n * F);
-  const i64 ch = (3 * (i64)lcap_part) / 4;   // rows per work item: the LDS table stays <= 3/4 full
+  u64* qkey = reinterpret_cast<u64*>(prow + ((n + 1) & ~(i64)1));
+  VT* qval = reinterpret_cast<VT*>(qkey + n);
+  int* qrow = reinterpret_cast<int*>(qval + n * F);
+  const int T = stage_rows(F);
+  const size_t stage_bytes = (size_t)T * (14 + 8 * F);
+  const size_t lds_bucket = std::max(stage_bytes, lbytes_part);
   hipLaunchKernelGGL(agg_hist_kernel, dim3(G), dim3(1024), (size_t)P * 4, st, k, n, rpw, pbits, hist, meta);
   hipLaunchKernelGGL(scan_rows_kernel, dim3(P), dim3(256), 0, st, hist, G, tot, meta, 1);
-  hipLaunchKernelGGL(scan_tot_kernel, dim3(1), dim3(1024), 0, st, tot, P, ch, bstart, wstart, meta, 1);
-  hipLaunchKernelGGL((agg_scatter_kernel<VT>), dim3(G), dim3(1024), (size_t)P * 4, st, k, v, n, F, rpw, pbits, hist,
+  hipLaunchKernelGGL(scan_tot_kernel, dim3(1), dim3(1024), 0, st, tot, P, (i64)1, bstart, (i64*)nullptr, meta, 1);
+  hipLaunchKernelGGL((agg_scatter_kernel<VT>), dim3(G), dim3(1024), stage_bytes, st, k, v, n, F, rpw, pbits, T, hist,
                      bstart, pkey, pval, prow, meta);
-  hipLaunchKernelGGL((agg_part_kernel<VT, OP>), dim3(1024), dim3(256), lbytes_part, st, pkey, pval, prow, F, lcap_part,
-                     P, ch, bstart, wstart, gpart, meta, o);
+  hipLaunchKernelGGL((agg_bucket_kernel<VT, OP>), dim3(P), dim3(1024), lds_bucket, st, pkey, pval, prow, F, lcap_part,
+                     pbits, T, n, bstart, qkey, qval, qrow, gpart, meta, o);
   hipLaunchKernelGGL((agg_emit_kernel<VT, OP>), dim3(512), dim3(256), 0, st, glow, gpart, F, meta, o);
   if (want_inv)
     hipLaunchKernelGGL(agg_fix_inv_kernel, dim3((unsigned)std::min<i64>(2048, (n + 255) / 256)), dim3(256), 0, st,
@@ -806,7 +1041,7 @@ long long nsdb_agg_work_bytes(long long n, int F, int pbits, int want_inv) {
   const long long P = 1LL << pbits;
   const long long G = std::min<long long>(256, std::max<long long>(1, (n + 16383) / 16384));
   (void)want_inv;
-  return ((P * G * 4 + 15) & ~15LL) + 8 * (P + 2 * (P + 1)) + 8 * n + 8 * n * F + 4 * n + 64;
+  return ((P * G * 4 + 15) & ~15LL) + 8 * (2 * P + 2) + 2 * (8 * n + 8 * n * F + 4 * (n + 1)) + 64;
 }
 
 // vt: 0 double, 1 int64; op: 0 sum, 1 min, 2 max
@@ -815,10 +1050,11 @@ int nsdb_hash_aggregate(const void* keys, const void* vals, long long n, int F, 
                         void* work, int pbits, int lcap_low, int lcap_part, int low_thr, hipStream_t st) {
   if (n <= 0) return 0;
   if (n >= (1LL << 31)) return (int)hipErrorInvalidValue;
-  if (F < 0 || F > 16 || pbits < 0 || pbits > 14) return (int)hipErrorInvalidValue;
+  if (F < 0 || F > 16 || pbits < 0 || pbits > 10) return (int)hipErrorInvalidValue;
   auto pow2 = [](long long x) { return x > 0 && (x & (x - 1)) == 0; };
   if (!pow2(gcap_low) || !pow2(gcap_part) || !pow2(lcap_low) || !pow2(lcap_part)) return (int)hipErrorInvalidValue;
   if ((size_t)lcap_low * (28 + 8 * F) > 65536 || (size_t)lcap_part * (28 + 8 * F) > 131072) return (int)hipErrorInvalidValue;
+  if ((size_t)stage_rows(F) * (14 + 8 * F) > 131072) return (int)hipErrorInvalidValue;
 #define NSDB_AGG(VT, OP) agg_launch_t<VT, OP>(keys, vals, n, F, want_inv, meta, glow, gcap_low, gpart, gcap_part, out, work, pbits, lcap_low, lcap_part, low_thr, st)
   if (vt == 0) {
     if (op == 0) return NSDB_AGG(double, OP_SUM);
@@ -833,40 +1069,43 @@ int nsdb_hash_aggregate(const void* keys, const void* vals, long long n, int F, 
   return (int)hipErrorInvalidValue;
 }
 
-// Join build over n int64 keys: tkey [cap + 1] preset kEmpty, tcnt [cap + 1] preset 0 (cap a power of two >= 2n).
-int nsdb_join_insert(const void* keys, long long n, void* tkey, unsigned* tcnt, long long cap, int* row_slot,
-                     unsigned* row_rank, hipStream_t st) {
+// Join build over n int64 keys: tab [cap + 1] 16-byte slots preset {kEmpty, 0, 0} (cap a power of two >= 2n).
+int nsdb_join_insert(const void* keys, long long n, void* tab, long long cap, int* row_slot, unsigned* row_rank,
+                     hipStream_t st) {
   if (n <= 0) return 0;
   if (cap <= 0 || (cap & (cap - 1)) != 0 || cap < 2 * n || cap >= (1LL << 31)) return (int)hipErrorInvalidValue;
   const unsigned g = (unsigned)std::min<long long>(4096, (n + 255) / 256);
-  hipLaunchKernelGGL(join_insert_kernel, dim3(g), dim3(256), 0, st, (const u64*)keys, n, (u64*)tkey, tcnt,
-                     (u64)(cap - 1), row_slot, row_rank);
+  hipLaunchKernelGGL(join_insert_kernel, dim3(g), dim3(256), 0, st, (const u64*)keys, n, (JSlot*)tab, (u64)(cap - 1),
+                     row_slot, row_rank);
   return (int)hipGetLastError();
 }
 
-int nsdb_join_perm(const int* row_slot, const unsigned* row_rank, long long n, const long long* toff, long long* perm,
-                   hipStream_t st) {
+int nsdb_join_perm(const int* row_slot, const unsigned* row_rank, long long n, const long long* toff, void* tab,
+                   long long* perm, hipStream_t st) {
   if (n <= 0) return 0;
   const unsigned g = (unsigned)std::min<long long>(4096, (n + 255) / 256);
-  hipLaunchKernelGGL(join_perm_kernel, dim3(g), dim3(256), 0, st, row_slot, row_rank, n, toff, perm);
+  hipLaunchKernelGGL(join_perm_kernel, dim3(g), dim3(256), 0, st, row_slot, row_rank, n, toff, (JSlot*)tab, perm);
   return (int)hipGetLastError();
 }
 
-int nsdb_join_probe(const void* keys, long long m, const void* tkey, const unsigned* tcnt, long long cap,
-                    long long* cnt, int* slot, hipStream_t st) {
+long long nsdb_join_tiles(long long m) { return (m + kJTile - 1) / kJTile; }
+
+// cnt / pay [m] u32, tile_sum [nsdb_join_tiles(m)] i64
+int nsdb_join_probe(const void* keys, long long m, const void* tab, long long cap, unsigned* cnt, unsigned* pay,
+                    long long* tile_sum, hipStream_t st) {
   if (m <= 0) return 0;
   if (cap <= 0 || (cap & (cap - 1)) != 0) return (int)hipErrorInvalidValue;
-  const unsigned g = (unsigned)std::min<long long>(4096, (m + 255) / 256);
-  hipLaunchKernelGGL(join_probe_kernel, dim3(g), dim3(256), 0, st, (const u64*)keys, m, (const u64*)tkey, tcnt,
-                     (u64)(cap - 1), cnt, slot);
+  hipLaunchKernelGGL(join_probe_kernel, dim3((unsigned)nsdb_join_tiles(m)), dim3(256), 0, st, (const u64*)keys, m,
+                     (const JSlot*)tab, (u64)(cap - 1), cnt, pay, tile_sum);
   return (int)hipGetLastError();
 }
 
-int nsdb_join_expand(const long long* cnt, const long long* ooff, const int* slot, long long m, const long long* toff,
+// tile_base: exclusive scan of tile_sum
+int nsdb_join_expand(const unsigned* cnt, const unsigned* pay, long long m, const long long* tile_base,
                      const long long* perm, long long* bidx, long long* pidx, hipStream_t st) {
   if (m <= 0) return 0;
-  const unsigned g = (unsigned)std::min<long long>(4096, (m + 255) / 256);
-  hipLaunchKernelGGL(join_expand_kernel, dim3(g), dim3(256), 0, st, cnt, ooff, slot, m, toff, perm, bidx, pidx);
+  hipLaunchKernelGGL(join_expand_kernel, dim3((unsigned)nsdb_join_tiles(m)), dim3(256), 0, st, cnt, pay, m, tile_base,
+                     perm, bidx, pidx);
   return (int)hipGetLastError();
 }
 

@@ -18,13 +18,14 @@ long long nsdb_agg_work_bytes(long long n, int F, int pbits, int want_inv);
 int nsdb_hash_aggregate(const void* keys, const void* vals, long long n, int F, int vt, int op, int want_inv,
                         void* meta, void* glow, long long gcap_low, void* gpart, long long gcap_part, void* out,
                         void* work, int pbits, int lcap_low, int lcap_part, int low_thr, hipStream_t st);
-int nsdb_join_insert(const void* keys, long long n, void* tkey, unsigned* tcnt, long long cap, int* row_slot,
-                     unsigned* row_rank, hipStream_t st);
-int nsdb_join_perm(const int* row_slot, const unsigned* row_rank, long long n, const long long* toff, long long* perm,
-                   hipStream_t st);
-int nsdb_join_probe(const void* keys, long long m, const void* tkey, const unsigned* tcnt, long long cap,
-                    long long* cnt, int* slot, hipStream_t st);
-int nsdb_join_expand(const long long* cnt, const long long* ooff, const int* slot, long long m, const long long* toff,
+int nsdb_join_insert(const void* keys, long long n, void* tab, long long cap, int* row_slot, unsigned* row_rank,
+                     hipStream_t st);
+int nsdb_join_perm(const int* row_slot, const unsigned* row_rank, long long n, const long long* toff, void* tab,
+                   long long* perm, hipStream_t st);
+long long nsdb_join_tiles(long long m);
+int nsdb_join_probe(const void* keys, long long m, const void* tab, long long cap, unsigned* cnt, unsigned* pay,
+                    long long* tile_sum, hipStream_t st);
+int nsdb_join_expand(const unsigned* cnt, const unsigned* pay, long long m, const long long* tile_base,
                      const long long* perm, long long* bidx, long long* pidx, hipStream_t st);
 long long nsdb_part_work_bytes(long long n, int P);
 int nsdb_partition_perm(const long long* dest, long long n, int P, void* work, long long* perm, long long* counts,
@@ -87,17 +88,17 @@ std::vector<torch::Tensor> hash_aggregate(torch::Tensor keys, c10::optional<torc
     return {torch::empty({0}, i64), torch::empty({0, F}, keys.options().dtype(vdtype)), torch::empty({0}, i64),
             torch::empty({0}, i64), torch::empty({0}, i64), torch::tensor({0, 0, 1, 0}, torch::kInt64)};
   }
-  // LDS tables: LOW <= 64 KiB (two workgroups per CU), PART <= 128 KiB; buckets average <= ch / 2 rows (hash
-  // partitions are tightly binomial, so nearly every bucket is a single work item)
+  // LDS tables: LOW <= 64 KiB (two workgroups per CU), PART <= 128 KiB. PART: level-1 buckets = one per CU
+  // (256) once there are >= 2048 rows per bucket; each bucket workgroup splits its bucket further on the device
+  // from the sampled distinct-key estimate (relops.hip agg_bucket_kernel), so no host decision needs the data.
   const int64_t entry = 28 + 8 * F;
   const int64_t lcap_low = std::min<int64_t>(2048, pow2_at_most(65536 / entry));
   const int64_t lcap_part = std::min<int64_t>(4096, pow2_at_most(131072 / entry));
-  const int64_t ch = (3 * lcap_part) / 4;   // rows per PART work item (relops.hip agg_launch_t)
-  int64_t P = std::min<int64_t>(16384, pow2_at_least(std::max<int64_t>(1, (2 * n + ch - 1) / ch)));
   int pbits = 0;
-  while ((int64_t(1) << pbits) < P) ++pbits;
+  while (pbits < 8 && (n >> (pbits + 1)) >= 2048) ++pbits;
   const int64_t gcap_low = 4 * lcap_low;
-  const int64_t gcap_part = std::max<int64_t>(4096, std::min<int64_t>(pow2_at_least(2 * n), int64_t(1) << 20));
+  // overflow table of the PART path (keys whose LDS probe window filled): a miss-sized estimate only
+  const int64_t gcap_part = std::max<int64_t>(4096, std::min<int64_t>(pow2_at_least(2 * n), int64_t(1) << 17));
   const int64_t thr = low_threshold > 0 ? low_threshold : lcap_low / 4;
 
   auto meta = torch::empty({kMetaWords}, i64);
@@ -134,7 +135,7 @@ std::vector<torch::Tensor> hash_aggregate(torch::Tensor keys, c10::optional<torc
   return {reps, aggs, cnt, first, inv, status};
 }
 
-// Join build: returns (tkey [cap+1] i64, tcnt [cap+1] i32, toff [cap+1] i64 (exclusive offsets), perm [n] i64).
+// Join build: returns (table [cap+1, 2] i64 of 16-byte slots {key, cnt | pay << 32}, perm [n] i64).
 std::vector<torch::Tensor> join_build(torch::Tensor keys) {
   TORCH_CHECK(keys.is_cuda() && keys.scalar_type() == torch::kInt64 && keys.dim() == 1, "keys: 1-D int64 GPU tensor");
   keys = keys.contiguous();
@@ -142,49 +143,53 @@ std::vector<torch::Tensor> join_build(torch::Tensor keys) {
   TORCH_CHECK(n < (int64_t(1) << 29), "join_build: at most 2^29 build rows per table");
   const int64_t cap = pow2_at_least(std::max<int64_t>(1024, 2 * n));
   auto i64 = keys.options().dtype(torch::kInt64);
-  auto tkey = torch::full({cap + 1}, std::numeric_limits<int64_t>::min(), i64);
-  auto tcnt = torch::zeros({cap + 1}, keys.options().dtype(torch::kInt32));
+  auto tab = torch::zeros({cap + 1, 2}, i64);
+  tab.select(1, 0).fill_(std::numeric_limits<int64_t>::min());
   auto row_slot = torch::empty({n}, keys.options().dtype(torch::kInt32));
   auto row_rank = torch::empty({n}, keys.options().dtype(torch::kInt32));
-  rc_ok(nsdb_join_insert(keys.data_ptr(), n, tkey.data_ptr(), reinterpret_cast<unsigned*>(tcnt.data_ptr<int>()), cap,
-                         row_slot.data_ptr<int>(), reinterpret_cast<unsigned*>(row_rank.data_ptr<int>()), stream()),
+  rc_ok(nsdb_join_insert(keys.data_ptr(), n, tab.data_ptr(), cap, row_slot.data_ptr<int>(),
+                         reinterpret_cast<unsigned*>(row_rank.data_ptr<int>()), stream()),
         "join_insert");
+  auto tcnt = tab.view(torch::kInt32).select(1, 2);   // the cnt word of every slot (strided view)
   auto toff = torch::cumsum(tcnt, 0, torch::kInt64).sub_(tcnt);
   auto perm = torch::empty({n}, i64);
   rc_ok(nsdb_join_perm(row_slot.data_ptr<int>(), reinterpret_cast<const unsigned*>(row_rank.data_ptr<int>()), n,
-                       LL(toff.data_ptr<int64_t>()), LL(perm.data_ptr<int64_t>()), stream()),
+                       LL(toff.data_ptr<int64_t>()), tab.data_ptr(), LL(perm.data_ptr<int64_t>()), stream()),
         "join_perm");
-  return {tkey, tcnt, toff, perm};
+  return {tab, perm};
 }
 
 // Probe a built table with m int64 keys: all (build row, probe row) pairs with equal keys, probe-major.
-std::vector<torch::Tensor> join_probe(torch::Tensor tkey, torch::Tensor tcnt, torch::Tensor toff, torch::Tensor perm,
-                                      torch::Tensor keys) {
+std::vector<torch::Tensor> join_probe(torch::Tensor tab, torch::Tensor perm, torch::Tensor keys) {
   TORCH_CHECK(keys.is_cuda() && keys.scalar_type() == torch::kInt64 && keys.dim() == 1, "keys: 1-D int64 GPU tensor");
-  TORCH_CHECK(tkey.is_cuda() && tkey.scalar_type() == torch::kInt64 && tcnt.scalar_type() == torch::kInt32 &&
-                  toff.scalar_type() == torch::kInt64 && perm.scalar_type() == torch::kInt64,
+  TORCH_CHECK(tab.is_cuda() && tab.scalar_type() == torch::kInt64 && tab.dim() == 2 && tab.size(1) == 2 &&
+                  tab.is_contiguous() && perm.scalar_type() == torch::kInt64,
               "join table tensors (from join_build) expected");
-  const int64_t cap = tkey.numel() - 1;
-  TORCH_CHECK(cap >= 1024 && (cap & (cap - 1)) == 0 && tcnt.numel() == cap + 1 && toff.numel() == cap + 1,
-              "malformed join table");
-  TORCH_CHECK(keys.device() == tkey.device(), "probe keys must be on the table's device");
+  const int64_t cap = tab.size(0) - 1;
+  TORCH_CHECK(cap >= 1024 && (cap & (cap - 1)) == 0, "malformed join table");
+  TORCH_CHECK(keys.device() == tab.device(), "probe keys must be on the table's device");
   keys = keys.contiguous();
   const int64_t m = keys.numel();
   auto i64 = keys.options().dtype(torch::kInt64);
   if (m == 0 || perm.numel() == 0) return {torch::empty({0}, i64), torch::empty({0}, i64)};
-  auto cnt = torch::empty({m}, i64);
-  auto slot = torch::empty({m}, keys.options().dtype(torch::kInt32));
-  rc_ok(nsdb_join_probe(keys.data_ptr(), m, tkey.data_ptr(), reinterpret_cast<const unsigned*>(tcnt.data_ptr<int>()),
-                        cap, LL(cnt.data_ptr<int64_t>()), slot.data_ptr<int>(), stream()),
+  auto i32 = keys.options().dtype(torch::kInt32);
+  auto cnt = torch::empty({m}, i32);
+  auto pay = torch::empty({m}, i32);
+  const int64_t tiles = nsdb_join_tiles(m);
+  auto tsum = torch::empty({tiles + 1}, i64);
+  rc_ok(nsdb_join_probe(keys.data_ptr(), m, tab.data_ptr(), cap, reinterpret_cast<unsigned*>(cnt.data_ptr<int>()),
+                        reinterpret_cast<unsigned*>(pay.data_ptr<int>()), LL(tsum.data_ptr<int64_t>()), stream()),
         "join_probe");
-  auto ooff = torch::cumsum(cnt, 0);
-  const int64_t total = ooff[m - 1].item<int64_t>();   // sizes the output (one host read)
+  auto incl = torch::cumsum(tsum.narrow(0, 0, tiles), 0);
+  const int64_t total = incl[tiles - 1].item<int64_t>();   // sizes the output (one host read)
+  auto base = incl.sub_(tsum.narrow(0, 0, tiles));
   auto bidx = torch::empty({total}, i64);
   auto pidx = torch::empty({total}, i64);
   if (total > 0)
-    rc_ok(nsdb_join_expand(LL(cnt.data_ptr<int64_t>()), LL(ooff.data_ptr<int64_t>()), slot.data_ptr<int>(), m,
-                           LL(toff.data_ptr<int64_t>()), LL(perm.data_ptr<int64_t>()), LL(bidx.data_ptr<int64_t>()),
-                           LL(pidx.data_ptr<int64_t>()), stream()),
+    rc_ok(nsdb_join_expand(reinterpret_cast<const unsigned*>(cnt.data_ptr<int>()),
+                           reinterpret_cast<const unsigned*>(pay.data_ptr<int>()), m, LL(base.data_ptr<int64_t>()),
+                           LL(perm.data_ptr<int64_t>()), LL(bidx.data_ptr<int64_t>()), LL(pidx.data_ptr<int64_t>()),
+                           stream()),
           "join_expand");
   return {bidx, pidx};
 }
@@ -219,7 +224,7 @@ void register_relops(pybind11::module& m) {
         "device hash group-by + aggregate: (reps, aggs, counts, first, inv, status[g, path, ok, sample_distinct])",
         pybind11::arg("keys"), pybind11::arg("vals") = pybind11::none(), pybind11::arg("op") = "sum",
         pybind11::arg("want_inv") = false, pybind11::arg("low_threshold") = 0);
-  m.def("join_build", &join_build, "device hash-join build: (tkey, tcnt, toff, perm)");
+  m.def("join_build", &join_build, "device hash-join build: (table, perm)");
   m.def("join_probe", &join_probe, "device hash-join probe: (build_idx, probe_idx)");
   m.def("partition_perm", &partition_perm, "stable device partition permutation: (perm, counts)");
 }

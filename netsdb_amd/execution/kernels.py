@@ -89,9 +89,10 @@ class JoinTable:
     """A join build side keyed by its int64 join-hash column, built ONCE and probed by every probe batch
     (reference JoinMap / JoinProbe, src/lambdas/headers/JoinTuple.h:434, HashSink.h:14).
 
-    On the GPU: a device open-addressing table (relops.hip join_insert) whose slots hold a key's build rows as
-    a CSR run (join_perm), probed by one lookup per probe row (join_probe) and expanded into the (build, probe)
-    pairs (join_expand). On the CPU: the build hashes sorted once, probes binary-searched."""
+    On the GPU: a device open-addressing table of 16-byte slots {key, count, payload} (relops.hip join_insert /
+    join_perm; payload = the build row for a unique key, else the start of its CSR run), probed by ONE 16-byte
+    lookup per probe row (join_probe) and expanded into the (build, probe) pairs probe-major (join_expand).
+    On the CPU: the build hashes sorted once, probes binary-searched."""
 
     def __init__(self, build_h: torch.Tensor):
         self.h = build_h
@@ -110,8 +111,8 @@ class JoinTable:
             e = torch.empty(0, dtype=torch.int64, device=dev)
             return e, e
         if self._dev is not None:
-            tkey, tcnt, toff, perm = self._dev
-            return tuple(_ext.hip().join_probe(tkey, tcnt, toff, perm, probe_h.to(tkey.device).long().contiguous()))
+            tab, perm = self._dev
+            return tuple(_ext.hip().join_probe(tab, perm, probe_h.to(tab.device).long().contiguous()))
         sh, order = self._sorted
         sh, order = sh.to(dev), order.to(dev)
         lo = torch.searchsorted(sh, probe_h, right=False)

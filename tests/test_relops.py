@@ -68,6 +68,21 @@ def test_hash_aggregate_f64(n, distinct, op):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("F", [1, 3])
+def test_hash_aggregate_high_cardinality_subpartitions(F):
+    """Mostly-distinct keys: every level-1 bucket is split again on the device (agg_bucket_kernel's sub-partition
+    pass), then each sub-bucket is aggregated in LDS and written straight to the dense output."""
+    g = torch.Generator(device=DEV).manual_seed(17 + F)
+    n = 1_000_000
+    keys = torch.randint(0, 800_000, (n,), device=DEV, generator=g) * 1_000_003
+    vals = torch.rand(n, F, device=DEV, dtype=torch.float64, generator=g)
+    r = _ext.hip().hash_aggregate(keys, vals, "sum", True, 0)
+    assert int(r[5][2]) == 1 and int(r[5][1]) == 1                   # PART path
+    assert int(r[5][3]) > 200_000                                       # the sample saw a high-cardinality column
+    _check_agg(keys, vals, "sum", r)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("op", ["sum", "min", "max"])
 def test_hash_aggregate_int64_and_sentinel(op):
     g = torch.Generator(device=DEV).manual_seed(3)
@@ -87,7 +102,8 @@ def test_hash_aggregate_int64_and_sentinel(op):
 
 @pytest.mark.gpu
 def test_hash_aggregate_paths_agree_on_skew():
-    """Zipf-like skew: hot keys span many PART chunks (global-table flush) next to singleton buckets."""
+    """Skew: four hot keys make four oversized level-1 buckets (each still owned by one workgroup) next to
+    buckets of singletons; LOW (thr 100k) and PART must agree."""
     g = torch.Generator(device=DEV).manual_seed(11)
     hot = torch.randint(0, 4, (400_000,), device=DEV, generator=g)
     cold = torch.randint(1000, 10**9, (100_000,), device=DEV, generator=g)
