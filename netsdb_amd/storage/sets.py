@@ -20,7 +20,7 @@ from typing import Dict, Iterator, List, Optional, Tuple
 
 import torch
 
-from ..objects.record import RecordBatch
+from ..objects.record import RecordBatch, merge_adjacent_batches
 from .serde import deserialize_batch, serialize_batch
 
 class Page:
@@ -238,6 +238,10 @@ class SharedLink:
         return sum(sh.pages[p].n for p in self.pages if 0 <= p < len(sh.pages))
 
 
+def _same_device(a: torch.device, b: torch.device) -> bool:
+    return a.type == b.type and (a.index == b.index or a.index is None or b.index is None)
+
+
 class UserSet:
     """One node's partition of a stored set."""
 
@@ -329,6 +333,10 @@ class UserSet:
     def scan(self, device=None) -> Iterator[RecordBatch]:
         device = device if device is not None else self.device
         pages = list(self.pages)
+        if device is not None and (torch.device(device).type == "cuda" or self.COALESCE_ANY_DEVICE) and len(pages) > 1:
+            yield from self._scan_coalesced(pages, torch.device(device))
+            yield from self.shared_batches(device)
+            return
         ra = getattr(self.manager, "read_ahead", 0)
         queued = 0
         for i, p in enumerate(pages):
@@ -347,6 +355,53 @@ class UserSet:
             finally:
                 p.pins -= 1
         yield from self.shared_batches(device)
+
+    # resident device pages merged per scanned batch (bytes): 64 MiB pages are a storage / spill unit, not a good
+    # kernel size on a 288 GB GPU; pages cut from one loaded batch are merged back without a copy
+    SCAN_COALESCE_BYTES = 4 << 30
+    COALESCE_ANY_DEVICE = False      # tests: run the merge on CPU pages too
+
+    def _scan_coalesced(self, pages, device) -> Iterator[RecordBatch]:
+        """Runs of consecutive pages resident on ``device`` whose columns are adjacent slices of one buffer are
+        yielded as ONE batch (zero-copy views, up to SCAN_COALESCE_BYTES); any other page is yielded alone."""
+        i = 0
+        while i < len(pages):
+            run, nbytes = [], 0
+            j = i
+            while j < len(pages) and nbytes < self.SCAN_COALESCE_BYTES:
+                b = pages[j].batch
+                if b is None or not _same_device(b.device, device):
+                    break
+                if run and merge_adjacent_batches([run[-1].batch, b]) is None:
+                    break                          # not a continuation of the previous page's buffers
+                run.append(pages[j])
+                nbytes += pages[j].nbytes
+                j += 1
+            merged = None
+            if len(run) > 1:
+                for p in run:
+                    p.pins += 1
+                try:
+                    merged = merge_adjacent_batches([p.batch for p in run])
+                    if merged is not None:
+                        for p in run:
+                            self.manager.touch(p)
+                        yield merged
+                finally:
+                    for p in run:
+                        p.pins -= 1
+            if merged is not None:
+                i = j
+                continue
+            p = pages[i]
+            p.pins += 1
+            try:
+                b = p.load(device)
+                self.manager.touch(p)
+                yield b
+            finally:
+                p.pins -= 1
+            i += 1
 
     def all(self, device=None) -> Optional[RecordBatch]:
         bs = list(self.scan(device))

@@ -351,3 +351,34 @@ def test_eviction_is_thread_safe(tmp_path):
         t.join()
     assert not errors, errors
     assert st.device_bytes <= st.device_budget
+
+
+def test_scan_coalesces_adjacent_pages_zero_copy(monkeypatch, tmp_path):
+    """Pages cut from one loaded batch come back from a scan as ONE batch of views (no copy); a page from
+    another batch starts a new run; results equal the page-by-page scan."""
+    from netsdb_amd.client import PDBClient
+    from netsdb_amd.objects.record import RecordBatch
+    from netsdb_amd.objects.strings import StringColumn
+    from netsdb_amd.storage.sets import UserSet
+
+    c = PDBClient(root=str(tmp_path), page_size=1 << 16)
+    c.create_database("d")
+    c.create_set("d", "s", None)
+    n = 20000
+    b = RecordBatch({"x": torch.arange(n), "y": torch.rand(n, 3),
+                     "s": StringColumn.from_list([f"v{i % 97}" for i in range(n)])}, n)
+    s = c.storage.get_set("d", "s")
+    # pages of a batch already on the set's device keep views of it (a GPU node: device-built batches); the
+    # CPU node's host arena would copy them, so add without it here
+    monkeypatch.setattr(c.storage, "page_pool", None)
+    s.add_batch(b)
+    s.add_batch(RecordBatch({"x": torch.arange(5), "y": torch.rand(5, 3), "s": StringColumn.from_list(list("abcde"))}, 5))
+    assert len(s.pages) > 3
+    plain = list(s.scan("cpu"))
+    monkeypatch.setattr(UserSet, "COALESCE_ANY_DEVICE", True)
+    merged = list(s.scan("cpu"))
+    assert len(merged) == 2 and merged[0].n == n and merged[1].n == 5
+    assert merged[0].columns["x"].data_ptr() == b.columns["x"].data_ptr()      # a view, not a copy
+    assert torch.equal(merged[0].columns["x"], b.columns["x"]) and torch.equal(merged[0].columns["y"], b.columns["y"])
+    assert merged[0].columns["s"].tolist() == b.columns["s"].tolist()
+    assert sum(p.n for p in plain) == n + 5
