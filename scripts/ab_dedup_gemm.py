@@ -36,6 +36,9 @@ def main():
     gb = lambda b, us: f"{b / us / 1e3:.2f} TB/s"
     us = t(lambda: ops.gemm_nt(Wc, Xc, out_dtype=torch.float32))
     print(f"common 500x100x900k view      {us:8.1f} us  {gb(0.9e9, us)}  splits={ops.gemm_splits(500, 100, 900000)}")
+    for cfg, sp in ((0, 64), (0, 256), (2, 128), (2, 64)):
+        us = t(lambda: ops.gemm_nt(Wc, Xc, out_dtype=torch.float32, cfg=cfg, splits=sp))
+        print(f"common cfg={cfg} splits={sp:3d}         {us:8.1f} us  {gb(0.9e9, us)}")
     for sp in (0, 16, 24, 32, 48, 64):
         xb = Xp.unsqueeze(0).expand(12, -1, -1)
         us = t(lambda: ops.gemm_nt(Wp, xb, P, ops.BIAS_MAT, out_dtype=torch.float32, splits=sp))
