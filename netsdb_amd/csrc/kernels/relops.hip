@@ -206,14 +206,18 @@ __device__ __forceinline__ LTable ltable_at(char* base, int cap, int F) {
 }
 
 template <typename VT, int OP>
-__device__ __forceinline__ void ltable_clear(LTable t, int F) {
-  for (int i = threadIdx.x; i < t.cap; i += blockDim.x) {
+__device__ __forceinline__ void ltable_clear(LTable t, int F, int lt = -1, int gs = 0) {
+  if (lt < 0) {
+    lt = threadIdx.x;
+    gs = blockDim.x;
+  }
+  for (int i = lt; i < t.cap; i += gs) {
     t.key[i] = kEmpty;
     t.cnt[i] = 0;
     t.ref[i] = 0;
     t.rmin[i] = ~0ull;
   }
-  for (int i = threadIdx.x; i < t.cap * F; i += blockDim.x) t.acc[i] = acc_identity<VT, OP>();
+  for (int i = lt; i < t.cap * F; i += gs) t.acc[i] = acc_identity<VT, OP>();
 }
 
 // LDS slot of k (inserted if absent), or -1 if its probe window is full.
@@ -285,20 +289,31 @@ __global__ __launch_bounds__(1024) void agg_sample_kernel(const u64* __restrict_
     const i64 r = (n <= S) ? i : ((i64)i * n) / S;   // n < 2^31: no overflow
     kk[j] = i < ns ? keys[r] : kEmpty;
   }
+  const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int j = 0; j < S / 1024; ++j) {
     const u64 k = kk[j];
-    if (k == kEmpty) continue;
-    int s = (int)(mix64(k) & (CAP - 1));
-    for (;;) {
-      u64 e = kEmpty;
-      __hip_atomic_compare_exchange_strong(tab + s, &e, k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (e == kEmpty || e == k) {
-        atomicAdd(tcnt + s, 1u);
-        break;
+    const bool active = k != kEmpty;
+    int s = -1;
+    if (active) {
+      s = (int)(mix64(k) & (CAP - 1));
+      for (;;) {
+        u64 e = tab[s];   // plain read first: a key already present costs no atomic
+        if (e == kEmpty)
+          __hip_atomic_compare_exchange_strong(tab + s, &e, k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (e == kEmpty || e == k) break;
+        s = (s + 1) & (CAP - 1);
       }
-      s = (s + 1) & (CAP - 1);
+    }
+    // one LDS add per distinct slot of the wave (a few hot keys would serialise 64 lanes on one word)
+    u64 todo = __ballot(active);
+    while (todo) {
+      const int leader = __ffsll((long long)todo) - 1;
+      const int ls = __shfl(s, leader, 64);
+      const u64 m = __ballot(active && s == ls);
+      if (lane == leader) atomicAdd(tcnt + ls, (unsigned)__popcll(m));
+      todo &= ~m;
     }
   }
   __syncthreads();
@@ -309,9 +324,16 @@ __global__ __launch_bounds__(1024) void agg_sample_kernel(const u64* __restrict_
     f1 += c == 1;
     f2 += c == 2;
   }
-  atomicAdd(fsum, d);
-  atomicAdd(fsum + 1, f1);
-  atomicAdd(fsum + 2, f2);
+  for (int o = 32; o > 0; o >>= 1) {
+    d += __shfl_down(d, o, 64);
+    f1 += __shfl_down(f1, o, 64);
+    f2 += __shfl_down(f2, o, 64);
+  }
+  if (lane == 0) {
+    atomicAdd(fsum, d);
+    atomicAdd(fsum + 1, f1);
+    atomicAdd(fsum + 2, f2);
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     const double dd = fsum[0], g1 = fsum[1], g2 = fsum[2];
@@ -340,6 +362,35 @@ __global__ __launch_bounds__(256) void agg_init_kernel(u64* glow, i64 cap_low, u
 }
 
 // ---------------------------------------------------------------- LOW path
+constexpr int kU = 4;        // rows per thread loaded before any is processed (memory-level parallelism)
+constexpr int kPreF = 2;     // value columns loaded with the keys (the rest at use)
+
+// Row (key, values) batch of one thread: kU rows of a 256*kU-row tile, loaded together.
+template <typename VT>
+struct RowBatch {
+  u64 k[kU];
+  VT v[kU][kPreF];
+  __device__ __forceinline__ void load(const u64* __restrict__ keys, const VT* __restrict__ vals, i64 t0, i64 n,
+                                       int F, int nthr) {
+#pragma unroll
+    for (int j = 0; j < kU; ++j) {
+      const i64 i = t0 + (i64)j * nthr + threadIdx.x;
+      k[j] = i < n ? keys[i] : kEmpty;
+#pragma unroll
+      for (int f = 0; f < kPreF; ++f) v[j][f] = (i < n && f < F) ? vals[i * F + f] : VT(0);
+    }
+  }
+};
+
+template <typename VT, int OP>
+__device__ __forceinline__ void ltable_add_row(LTable t, int s, const VT* pre, const VT* __restrict__ vrow, int F,
+                                               u64 row) {
+  for (int f = 0; f < F; ++f)
+    acc_add<VT, OP, __HIP_MEMORY_SCOPE_WORKGROUP>(t.acc + s * F + f, f < kPreF ? pre[f] : vrow[f]);
+  __hip_atomic_fetch_add(t.cnt + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (row < t.rmin[s]) __hip_atomic_fetch_min(t.rmin + s, row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 template <typename VT, int OP>
 __global__ __launch_bounds__(256) void agg_low_kernel(const u64* __restrict__ keys, const VT* __restrict__ vals, i64 n,
                                                       int F, int lcap, GTable g, AggMeta* meta, AggOut o) {
@@ -348,21 +399,27 @@ __global__ __launch_bounds__(256) void agg_low_kernel(const u64* __restrict__ ke
   LTable t = ltable_at(lds_raw, lcap, F);
   ltable_clear<VT, OP>(t, F);
   __syncthreads();
-  const i64 stride = (i64)gridDim.x * blockDim.x;
+  constexpr int TILE = 256 * kU;
+  const i64 tstride = (i64)gridDim.x * TILE;
   int it = 0;
-  for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride, ++it) {
-    if ((it & 63) == 63 && __hip_atomic_load(&meta->fail_low, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
-    const u64 k = keys[i];
-    const VT* v = vals + i * F;
-    int s = -1;
-    if (k != kEmpty) s = ltable_slot(t, k, mix64(k));
-    if (s >= 0) {
-      for (int f = 0; f < F; ++f) acc_add<VT, OP, __HIP_MEMORY_SCOPE_WORKGROUP>(t.acc + s * F + f, v[f]);
-      __hip_atomic_fetch_add(t.cnt + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      // rows arrive in increasing order per thread: after a key's first stride the minimum is settled
-      if ((u64)i < t.rmin[s]) __hip_atomic_fetch_min(t.rmin + s, (u64)i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    } else {
-      row_into_global<VT, OP>(g, k, v, F, &meta->ng_low, &meta->sentinel_low, &meta->fail_low, o, i);
+  for (i64 t0 = (i64)blockIdx.x * TILE; t0 < n; t0 += tstride, ++it) {
+    if ((it & 15) == 15 && __hip_atomic_load(&meta->fail_low, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+    RowBatch<VT> rb;
+    rb.load(keys, vals, t0, n, F, 256);
+#pragma unroll
+    for (int j = 0; j < kU; ++j) {
+      const i64 i = t0 + j * 256 + threadIdx.x;
+      if (i >= n) break;
+      const u64 k = rb.k[j];
+      const VT* v = vals + i * F;
+      const int s = k != kEmpty ? ltable_slot(t, k, mix64(k)) : -1;
+      if (s >= 0) {
+        ltable_add_row<VT, OP>(t, s, rb.v[j], v, F, (u64)i);
+      } else {
+        VT tmp[16];
+        for (int f = 0; f < F; ++f) tmp[f] = f < kPreF ? rb.v[j][f] : v[f];
+        row_into_global<VT, OP>(g, k, tmp, F, &meta->ng_low, &meta->sentinel_low, &meta->fail_low, o, i);
+      }
     }
   }
   __syncthreads();
@@ -379,11 +436,20 @@ __global__ __launch_bounds__(256) void agg_low_kernel(const u64* __restrict__ ke
   }
   if (o.inv == nullptr) return;
   __syncthreads();
-  for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const u64 k = keys[i];
-    if (k == kEmpty) continue;
-    const int s = ltable_find(t, k, mix64(k));
-    if (s >= 0) o.inv[i] = t.ref[s];
+  for (i64 t0 = (i64)blockIdx.x * TILE; t0 < n; t0 += tstride) {
+    u64 k[kU];
+#pragma unroll
+    for (int j = 0; j < kU; ++j) {
+      const i64 i = t0 + j * 256 + threadIdx.x;
+      k[j] = i < n ? keys[i] : kEmpty;
+    }
+#pragma unroll
+    for (int j = 0; j < kU; ++j) {
+      const i64 i = t0 + j * 256 + threadIdx.x;
+      if (k[j] == kEmpty || i >= n) continue;
+      const int s = ltable_find(t, k[j], mix64(k[j]));
+      if (s >= 0) o.inv[i] = t.ref[s];
+    }
   }
 }
 
@@ -391,6 +457,36 @@ __global__ __launch_bounds__(256) void agg_low_kernel(const u64* __restrict__ ke
 // bucket of a key: the top pbits of its hash (the LDS slot uses the low bits)
 __device__ __forceinline__ int bucket_of(u64 k, int pbits) {
   return pbits == 0 ? 0 : (int)(mix64(k) >> (64 - pbits));
+}
+
+// Exclusive scan over a block (blockDim a multiple of 64, <= 1024; one value per thread); returns the
+// thread's prefix, *total (shared) the block sum.
+template <typename T>
+__device__ __forceinline__ T block_scan_excl_t(T v, T* wsum, T* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  T x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const T y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) wsum[wave] = x;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    T w = threadIdx.x < nw ? wsum[threadIdx.x] : T(0);
+    T z = w;
+#pragma unroll
+    for (int d = 1; d < 16; d <<= 1) {
+      const T y = __shfl_up(z, d, 64);
+      if (threadIdx.x >= d) z += y;
+    }
+    if (threadIdx.x < nw) wsum[threadIdx.x] = z - w;
+    if (threadIdx.x == nw - 1) *total = z;
+  }
+  __syncthreads();
+  const T r = wsum[wave] + x - v;
+  __syncthreads();   // wsum may be reused by the caller's next scan
+  return r;
 }
 
 // rows [wg * rpw, min(n, (wg + 1) * rpw)) per workgroup; hist is bucket-major [P][G]
@@ -403,107 +499,45 @@ __global__ __launch_bounds__(1024) void agg_hist_kernel(const u64* __restrict__ 
   for (int i = threadIdx.x; i < P; i += blockDim.x) h[i] = 0;
   __syncthreads();
   const i64 r0 = (i64)blockIdx.x * rpw, r1 = std::min<i64>(n, r0 + rpw);
-  for (i64 i = r0 + threadIdx.x; i < r1; i += blockDim.x) atomicAdd(h + bucket_of(keys[i], pbits), 1u);
+  constexpr int U = 8;
+  for (i64 b0 = r0; b0 < r1; b0 += (i64)U * 1024) {
+    u64 k[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const i64 i = b0 + j * 1024 + threadIdx.x;
+      k[j] = i < r1 ? keys[i] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      if (b0 + j * 1024 + threadIdx.x < r1) atomicAdd(h + bucket_of(k[j], pbits), 1u);
+  }
   __syncthreads();
   for (int b = threadIdx.x; b < P; b += blockDim.x) hist[(size_t)b * gridDim.x + blockIdx.x] = h[b];
 }
 
-// workgroup b: exclusive scan of hist[b][0..G) in place, tot[b] = its sum
-__global__ __launch_bounds__(256) void scan_rows_kernel(unsigned* __restrict__ hist, int G, i64* __restrict__ tot,
-                                                        const AggMeta* meta, int guard) {
+// workgroup b: exclusive scan of hist[b][0..G) in place (G <= 1024, one entry per thread), tot[b] = its sum
+__global__ __launch_bounds__(1024) void scan_rows_kernel(unsigned* __restrict__ hist, int G, i64* __restrict__ tot,
+                                                         const AggMeta* meta, int guard) {
   if (guard && !take_part(meta)) return;
-  __shared__ unsigned part[256];
+  __shared__ unsigned wsum[16], total;
   unsigned* row = hist + (size_t)blockIdx.x * G;
-  const int per = (G + 255) / 256;
-  const int c0 = threadIdx.x * per, c1 = std::min(G, c0 + per);
-  unsigned s = 0;
-  for (int c = c0; c < c1; ++c) s += row[c];
-  part[threadIdx.x] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned run = 0;
-    for (int j = 0; j < 256; ++j) {
-      const unsigned x = part[j];
-      part[j] = run;
-      run += x;
-    }
-    tot[blockIdx.x] = run;
-  }
-  __syncthreads();
-  unsigned run = part[threadIdx.x];
-  for (int c = c0; c < c1; ++c) {
-    const unsigned x = row[c];
-    row[c] = run;
-    run += x;
-  }
+  const unsigned v = (int)threadIdx.x < G ? row[threadIdx.x] : 0u;
+  const unsigned pre = block_scan_excl_t<unsigned>(v, wsum, &total);
+  if ((int)threadIdx.x < G) row[threadIdx.x] = pre;
+  if (threadIdx.x == 0) tot[blockIdx.x] = total;
 }
 
-// one workgroup: bstart = exclusive scan of tot[P] (+ total at P); work list: wstart[b] = first chunk of bucket b
-// (chunks of at most ch rows), nwork = total chunks
-__global__ __launch_bounds__(1024) void scan_tot_kernel(const i64* __restrict__ tot, int P, i64 ch,
-                                                        i64* __restrict__ bstart, i64* __restrict__ wstart,
+// one workgroup: bstart = exclusive scan of tot[P] (P <= 2048), bstart[P] = the total
+__global__ __launch_bounds__(1024) void scan_tot_kernel(const i64* __restrict__ tot, int P, i64* __restrict__ bstart,
                                                         AggMeta* meta, int guard) {
   if (guard && !take_part(meta)) return;
-  __shared__ i64 pr[1024], pw[1024];
-  const int per = (P + 1023) / 1024;
-  const int c0 = threadIdx.x * per, c1 = std::min(P, c0 + per);
-  i64 sr = 0, sw = 0;
-  for (int c = c0; c < c1; ++c) {
-    sr += tot[c];
-    if (wstart) sw += (tot[c] + ch - 1) / ch;
-  }
-  pr[threadIdx.x] = sr;
-  pw[threadIdx.x] = sw;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    i64 a = 0, b = 0;
-    for (int j = 0; j < 1024; ++j) {
-      const i64 x = pr[j], y = pw[j];
-      pr[j] = a;
-      pw[j] = b;
-      a += x;
-      b += y;
-    }
-    bstart[P] = a;
-    if (wstart) {
-      wstart[P] = b;
-      meta->nwork = b;
-    }
-  }
-  __syncthreads();
-  i64 a = pr[threadIdx.x], b = pw[threadIdx.x];
-  for (int c = c0; c < c1; ++c) {
-    bstart[c] = a;
-    a += tot[c];
-    if (wstart) {
-      wstart[c] = b;
-      b += (tot[c] + ch - 1) / ch;
-    }
-  }
-}
-
-// Exclusive scan over a block of 1024 threads (one value each); returns the prefix, *total the block sum.
-__device__ __forceinline__ unsigned block_scan_excl(unsigned v, unsigned* wsum, unsigned* total) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  unsigned x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const unsigned y = __shfl_up(x, d, 64);
-    if (lane >= d) x += y;
-  }
-  if (lane == 63) wsum[wave] = x;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned run = 0;
-    for (int w = 0; w < nw; ++w) {
-      const unsigned t = wsum[w];
-      wsum[w] = run;
-      run += t;
-    }
-    *total = run;
-  }
-  __syncthreads();
-  return wsum[wave] + x - v;
+  __shared__ i64 wsum[16], total;
+  const int c0 = threadIdx.x * 2;
+  const i64 a = c0 < P ? tot[c0] : 0, b = c0 + 1 < P ? tot[c0 + 1] : 0;
+  const i64 pre = block_scan_excl_t<i64>(a + b, wsum, &total);
+  if (c0 < P) bstart[c0] = pre;
+  if (c0 + 1 < P) bstart[c0 + 1] = pre + a;
+  if (threadIdx.x == 0) bstart[P] = total;
 }
 
 // Tile-staged scatter of rows [r0, r1) (read through rows_of, or 0..: plain row ids) into bucket runs: each
@@ -517,7 +551,8 @@ __device__ __forceinline__ void staged_scatter(const u64* __restrict__ skey, con
                                                int P, int T, char* lds, i64* run, unsigned* cnt, unsigned* off,
                                                unsigned* wsum, u64* __restrict__ dkey, VT* __restrict__ dval,
                                                int* __restrict__ drow) {
-  constexpr int R = 4;   // rows per thread per tile (T <= 4096)
+  constexpr int R = 4;   // rows per thread per tile (T <= 4 * blockDim)
+  const int nthr = blockDim.x;
   u64* st_key = reinterpret_cast<u64*>(lds);
   VT* st_val = reinterpret_cast<VT*>(st_key + T);
   int* st_row = reinterpret_cast<int*>(st_val + (size_t)T * F);
@@ -531,27 +566,38 @@ __device__ __forceinline__ void staged_scatter(const u64* __restrict__ skey, con
     u64 k[R];
     int bk[R];
     unsigned rk[R];
+    VT pv[R][kPreF];
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-      const int p = threadIdx.x + j * 1024;
-      k[j] = p < tn ? skey[t0 + p] : 0;
+      const int p = threadIdx.x + j * nthr;
+      const i64 i = t0 + p;
+      k[j] = p < tn ? skey[i] : 0;
+#pragma unroll
+      for (int f = 0; f < kPreF; ++f) pv[j][f] = (p < tn && f < F) ? sval[i * F + f] : VT(0);
+    }
+    const int rowsrc = srow != nullptr;
+    int rw[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int p = threadIdx.x + j * nthr;
+      rw[j] = p < tn ? (rowsrc ? srow[t0 + p] : (int)(t0 + p)) : 0;
     }
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-      const int p = threadIdx.x + j * 1024;
+      const int p = threadIdx.x + j * nthr;
       if (p < tn) {
         bk[j] = P == 1 ? 0 : (int)((mix64(k[j]) >> shift) & pmask);
         rk[j] = atomicAdd(cnt + bk[j], 1u);
       }
     }
     __syncthreads();
-    // exclusive scan of cnt[0..P) (P <= 4096: up to 4 buckets per thread)
+    // exclusive scan of cnt[0..P) (P <= 4 * blockDim buckets)
     {
-      const int per = (P + 1023) / 1024;
+      const int per = (P + nthr - 1) / nthr;
       const int c0 = threadIdx.x * per;
       unsigned sum = 0;
       for (int c = c0; c < c0 + per && c < P; ++c) sum += cnt[c];
-      unsigned pre = block_scan_excl(sum, wsum, &tot_sh);
+      unsigned pre = block_scan_excl_t<unsigned>(sum, wsum, &tot_sh);
       for (int c = c0; c < c0 + per && c < P; ++c) {
         off[c] = pre;
         pre += cnt[c];
@@ -560,14 +606,14 @@ __device__ __forceinline__ void staged_scatter(const u64* __restrict__ skey, con
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-      const int p = threadIdx.x + j * 1024;
+      const int p = threadIdx.x + j * nthr;
       if (p < tn) {
         const unsigned q = off[bk[j]] + rk[j];
         const i64 i = t0 + p;
         st_key[q] = k[j];
-        st_row[q] = srow ? srow[i] : (int)i;
+        st_row[q] = rw[j];
         st_b[q] = (unsigned short)bk[j];
-        for (int f = 0; f < F; ++f) st_val[(size_t)q * F + f] = sval[i * F + f];
+        for (int f = 0; f < F; ++f) st_val[(size_t)q * F + f] = f < kPreF ? pv[j][f] : sval[i * F + f];
       }
     }
     __syncthreads();
@@ -586,7 +632,7 @@ __device__ __forceinline__ void staged_scatter(const u64* __restrict__ skey, con
 
 // level-1 scatter: workgroup g packs its rows [g * rpw, ...) into the P1 buckets at bstart[b] + hist[b][g]
 template <typename VT>
-__global__ __launch_bounds__(1024) void agg_scatter_kernel(const u64* __restrict__ keys, const VT* __restrict__ vals,
+__global__ __launch_bounds__(512) void agg_scatter_kernel(const u64* __restrict__ keys, const VT* __restrict__ vals,
                                                            i64 n, int F, i64 rpw, int pbits, int T,
                                                            const unsigned* __restrict__ hist,
                                                            const i64* __restrict__ bstart, u64* __restrict__ pkey,
@@ -603,58 +649,82 @@ __global__ __launch_bounds__(1024) void agg_scatter_kernel(const u64* __restrict
   staged_scatter<VT>(keys, vals, nullptr, r0, r1, F, 64 - pbits, P, T, lds_raw, run, cnt, off, wsum, pkey, pval, prow);
 }
 
-// Aggregate rows [r0, r1) of (key, val, row) in the LDS table (clearing it to cap entries first), then write the
-// groups straight to the dense output: the caller guarantees the range holds every row of its keys. Rows whose
-// LDS probe window is full go to the global table (emitted later by agg_emit).
+// ngrp thread groups (blockDim / ngrp threads each, ngrp <= 4) each aggregate their rows [a, e) of (key, val,
+// row) in their own LDS table t (cleared first), then write the groups straight to the dense output: the caller
+// guarantees a range holds every row of its keys. Every thread of the block calls this (block-wide barriers);
+// rows whose LDS probe window is full go to the global table (emitted later by agg_emit). One global atomic per
+// call reserves the dense ids of all groups of all ranges.
 template <typename VT, int OP>
-__device__ __forceinline__ void agg_range_dense(const u64* __restrict__ pkey, const VT* __restrict__ pval,
-                                                const int* __restrict__ prow, i64 r0, i64 r1, int F, LTable t,
-                                                GTable g, AggMeta* meta, AggOut o) {
-  __shared__ int nocc;
-  __shared__ i64 base_sh;
-  ltable_clear<VT, OP>(t, F);
-  if (threadIdx.x == 0) nocc = 0;
+__device__ __forceinline__ void agg_ranges_dense(const u64* __restrict__ pkey, const VT* __restrict__ pval,
+                                                 const int* __restrict__ prow, i64 a, i64 e, int F, LTable t,
+                                                 int ngrp, GTable g, AggMeta* meta, AggOut o) {
+  __shared__ int nocc[4];
+  __shared__ i64 base_sh[4];
+  const int gs = blockDim.x / ngrp, gi = threadIdx.x / gs, lt = threadIdx.x % gs;
+  ltable_clear<VT, OP>(t, F, lt, gs);
+  if (threadIdx.x < 4) nocc[threadIdx.x] = 0;
   __syncthreads();
-  for (i64 r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
-    const u64 k = pkey[r];
-    const VT* v = pval + r * F;
-    const int row = prow[r];
-    int s = -1;
-    if (k != kEmpty) s = ltable_slot(t, k, mix64(k));
-    if (s >= 0) {
-      for (int f = 0; f < F; ++f) acc_add<VT, OP, __HIP_MEMORY_SCOPE_WORKGROUP>(t.acc + s * F + f, v[f]);
-      __hip_atomic_fetch_add(t.cnt + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if ((u64)row < t.rmin[s]) __hip_atomic_fetch_min(t.rmin + s, (u64)row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    } else {
-      row_into_global<VT, OP>(g, k, v, F, &meta->ng_part, &meta->sentinel_part, &meta->fail_part, o, row);
+  for (i64 b0 = a; b0 < e; b0 += (i64)gs * kU) {
+    u64 k[kU];
+    int rw[kU];
+    VT pv[kU][kPreF];
+#pragma unroll
+    for (int j = 0; j < kU; ++j) {
+      const i64 r = b0 + (i64)j * gs + lt;
+      const bool in = r < e;
+      k[j] = in ? pkey[r] : kEmpty;
+      rw[j] = in ? prow[r] : 0;
+#pragma unroll
+      for (int f = 0; f < kPreF; ++f) pv[j][f] = (in && f < F) ? pval[r * F + f] : VT(0);
+    }
+#pragma unroll
+    for (int j = 0; j < kU; ++j) {
+      const i64 r = b0 + (i64)j * gs + lt;
+      if (r >= e) break;
+      const VT* v = pval + r * F;
+      const int sl = k[j] != kEmpty ? ltable_slot(t, k[j], mix64(k[j])) : -1;
+      if (sl >= 0) {
+        ltable_add_row<VT, OP>(t, sl, pv[j], v, F, (u64)rw[j]);
+      } else {
+        VT tmp[16];
+        for (int f = 0; f < F; ++f) tmp[f] = f < kPreF ? pv[j][f] : v[f];
+        row_into_global<VT, OP>(g, k[j], tmp, F, &meta->ng_part, &meta->sentinel_part, &meta->fail_part, o, rw[j]);
+      }
     }
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < t.cap; e += blockDim.x)
-    if (t.key[e] != kEmpty) t.ref[e] = atomicAdd(&nocc, 1);   // local id (any order)
+  for (int x = lt; x < t.cap; x += gs)
+    if (t.key[x] != kEmpty) t.ref[x] = atomicAdd(&nocc[gi], 1);   // local id (any order)
   __syncthreads();
-  if (threadIdx.x == 0 && nocc)
-    base_sh = __hip_atomic_fetch_add(&meta->ng_part, (i64)nocc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) {
+    i64 tot = 0;
+    for (int q = 0; q < ngrp; ++q) tot += nocc[q];
+    i64 b = tot ? __hip_atomic_fetch_add(&meta->ng_part, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    for (int q = 0; q < ngrp; ++q) {
+      base_sh[q] = b;
+      b += nocc[q];
+    }
+  }
   __syncthreads();
-  const i64 base = base_sh;
-  for (int e = threadIdx.x; e < t.cap; e += blockDim.x) {
-    const u64 k = t.key[e];
+  const i64 base = base_sh[gi];
+  for (int x = lt; x < t.cap; x += gs) {
+    const u64 k = t.key[x];
     if (k == kEmpty) continue;
-    const i64 gid = base + t.ref[e];
-    t.ref[e] = gid;
+    const i64 gid = base + t.ref[x];
+    t.ref[x] = gid;
     o.reps[gid] = (i64)k;
-    o.cnt[gid] = (i64)t.cnt[e];
-    o.first[gid] = (i64)t.rmin[e];
+    o.cnt[gid] = (i64)t.cnt[x];
+    o.first[gid] = (i64)t.rmin[x];
     o.slot_of_gid[gid] = -1;
-    for (int f = 0; f < F; ++f) o.aggs[gid * F + f] = acc_out<VT, OP>(t.acc[e * F + f]);
+    for (int f = 0; f < F; ++f) o.aggs[gid * F + f] = acc_out<VT, OP>(t.acc[x * F + f]);
   }
   if (o.inv != nullptr) {
     __syncthreads();
-    for (i64 r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
+    for (i64 r = a + lt; r < e; r += gs) {
       const u64 k = pkey[r];
       if (k == kEmpty) continue;
-      const int s = ltable_find(t, k, mix64(k));
-      if (s >= 0) o.inv[prow[r]] = t.ref[s];
+      const int sl = ltable_find(t, k, mix64(k));
+      if (sl >= 0) o.inv[prow[r]] = t.ref[sl];
     }
   }
   __syncthreads();
@@ -663,7 +733,8 @@ __device__ __forceinline__ void agg_range_dense(const u64* __restrict__ pkey, co
 // Workgroup b owns level-1 bucket b whole (no other workgroup sees its keys). When the estimated distinct keys
 // of the bucket fit the LDS table at load <= 1/2 it aggregates the bucket directly; otherwise it first splits the
 // bucket into P2 sub-buckets by the next hash bits (its own histogram + staged scatter into the second buffer,
-// same positions) and aggregates them one after another. No global atomics per row, one per group run.
+// same positions) and aggregates them four at a time (four thread groups, four LDS tables of a quarter each).
+// No global atomics per row: one per group flush and one per round for the dense ids.
 template <typename VT, int OP>
 __global__ __launch_bounds__(1024) void agg_bucket_kernel(const u64* __restrict__ pkey, const VT* __restrict__ pval,
                                                           const int* __restrict__ prow, int F, int lcap, int p1bits,
@@ -681,26 +752,38 @@ __global__ __launch_bounds__(1024) void agg_bucket_kernel(const u64* __restrict_
   // expected distinct keys of this bucket: the estimate's share, with 2x slack, never above its rows
   const i64 est = meta->est;
   const i64 db = std::min<i64>(nb, 2 * ((est + P1 - 1) / P1) + 16);
-  int p2bits = 0;
-  while (p2bits < 10 && (db >> p2bits) * 2 > lcap) ++p2bits;
-  if (p2bits == 0) {
+  if (2 * db <= lcap) {
     int cap = 64;
     while (cap < lcap && cap < 2 * db) cap <<= 1;
-    agg_range_dense<VT, OP>(pkey, pval, prow, r0, r1, F, ltable_at(lds_raw, cap, F), g, meta, o);
+    agg_ranges_dense<VT, OP>(pkey, pval, prow, r0, r1, F, ltable_at(lds_raw, cap, F), 1, g, meta, o);
     return;
   }
+  constexpr int NG = 4;
+  const int qcap = lcap / NG;   // each group's table
+  int p2bits = 0;
+  while (p2bits < 10 && (db >> p2bits) * 2 > qcap) ++p2bits;
   const int P2 = 1 << p2bits;
   const int shift = 64 - p1bits - p2bits;
   const unsigned pmask = (unsigned)P2 - 1;
   // histogram of the sub-buckets
   for (int c = threadIdx.x; c < P2; c += blockDim.x) cnt[c] = 0;
   __syncthreads();
-  for (i64 r = r0 + threadIdx.x; r < r1; r += blockDim.x) atomicAdd(cnt + ((mix64(pkey[r]) >> shift) & pmask), 1u);
+  for (i64 b0 = r0; b0 < r1; b0 += 8 * 1024) {
+    u64 k[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const i64 r = b0 + j * 1024 + threadIdx.x;
+      k[j] = r < r1 ? pkey[r] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (b0 + j * 1024 + threadIdx.x < r1) atomicAdd(cnt + ((mix64(k[j]) >> shift) & pmask), 1u);
+  }
   __syncthreads();
   {
-    unsigned tot;
+    __shared__ unsigned tot_sh2;
     const unsigned v = threadIdx.x < P2 ? cnt[threadIdx.x] : 0u;
-    const unsigned pre = block_scan_excl(v, wsum, &tot);
+    const unsigned pre = block_scan_excl_t<unsigned>(v, wsum, &tot_sh2);
     if (threadIdx.x < P2) {
       sb[threadIdx.x] = pre;
       run[threadIdx.x] = r0 + pre;
@@ -717,11 +800,13 @@ __global__ __launch_bounds__(1024) void agg_bucket_kernel(const u64* __restrict_
   __syncthreads();
   const i64 dsub = std::min<i64>(nb, (db >> p2bits) + 16);
   int cap = 64;
-  while (cap < lcap && cap < 2 * dsub) cap <<= 1;
-  const LTable t = ltable_at(lds_raw, cap, F);
-  for (int s2 = 0; s2 < P2; ++s2) {
-    const i64 a = r0 + sb[s2], e = r0 + sb[s2 + 1];
-    if (a < e) agg_range_dense<VT, OP>(qkey, qval, qrow, a, e, F, t, g, meta, o);
+  while (cap < qcap && cap < 2 * dsub) cap <<= 1;
+  const int gi = threadIdx.x / (blockDim.x / NG);
+  const LTable t = ltable_at(lds_raw + (size_t)gi * cap * (28 + 8 * F), cap, F);
+  for (int s0 = 0; s0 < P2; s0 += NG) {
+    const int s2 = s0 + gi;
+    const i64 a = s2 < P2 ? r0 + sb[s2] : 0, e = s2 < P2 ? r0 + sb[s2 + 1] : 0;
+    agg_ranges_dense<VT, OP>(qkey, qval, qrow, a, e, F, t, NG, g, meta, o);
   }
 }
 
@@ -802,47 +887,55 @@ __global__ __launch_bounds__(256) void join_perm_kernel(const int* __restrict__ 
 
 constexpr int kJTile = 4096;   // probe rows per workgroup tile (256 threads x 16)
 
-__device__ __forceinline__ void jslot_find(const JSlot* __restrict__ tab, u64 mask, u64 k, unsigned& c,
-                                           unsigned& pay) {
-  c = 0;
-  pay = 0;
-  u64 s = k == kEmpty ? mask + 1 : mix64(k) & mask;
-  for (;;) {
-    const JSlot e = tab[s];   // one 16-byte load
-    if (e.key == k) {
-      c = e.cnt;
-      pay = e.pay;
-      return;
-    }
-    if (e.key == kEmpty || k == kEmpty) return;
-    s = (s + 1) & mask;
-  }
-}
 
-// probe: matches (cnt) and payload per probe row, and the match total of each 4096-row tile
+// probe: matches (cnt) and payload per probe row, and the match total of each 4096-row tile. The first-slot
+// reads of all 16 rows of a thread are issued together (16 independent 16-byte loads in flight); only rows
+// whose first slot holds another key walk the probe chain.
 __global__ __launch_bounds__(256) void join_probe_kernel(const u64* __restrict__ keys, i64 m,
                                                          const JSlot* __restrict__ tab, u64 mask,
                                                          unsigned* __restrict__ cnt, unsigned* __restrict__ pay,
                                                          i64* __restrict__ tile_sum) {
   __shared__ unsigned ws[4];
+  constexpr int J = kJTile / 256;
   const i64 t0 = (i64)blockIdx.x * kJTile;
   unsigned local = 0;
-  u64 k[kJTile / 256];
+  u64 k[J];
 #pragma unroll
-  for (int j = 0; j < kJTile / 256; ++j) {
+  for (int j = 0; j < J; ++j) {
     const i64 i = t0 + j * 256 + threadIdx.x;
     k[j] = i < m ? keys[i] : 0;
   }
+  u64 sl[J];
+  JSlot e[J];
 #pragma unroll
-  for (int j = 0; j < kJTile / 256; ++j) {
+  for (int j = 0; j < J; ++j) {
+    sl[j] = k[j] == kEmpty ? mask + 1 : (mix64(k[j]) & mask);
+    e[j] = tab[sl[j]];
+  }
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
     const i64 i = t0 + j * 256 + threadIdx.x;
-    if (i < m) {
-      unsigned c, p;
-      jslot_find(tab, mask, k[j], c, p);
-      cnt[i] = c;
-      pay[i] = p;
-      local += c;
+    if (i >= m) continue;
+    unsigned c = 0, p = 0;
+    if (e[j].key == k[j]) {
+      c = e[j].cnt;
+      p = e[j].pay;
+    } else if (e[j].key != kEmpty && k[j] != kEmpty) {
+      u64 s = (sl[j] + 1) & mask;
+      for (;;) {
+        const JSlot x = tab[s];
+        if (x.key == k[j]) {
+          c = x.cnt;
+          p = x.pay;
+          break;
+        }
+        if (x.key == kEmpty) break;
+        s = (s + 1) & mask;
+      }
     }
+    cnt[i] = c;
+    pay[i] = p;
+    local += c;
   }
   // workgroup sum
   for (int d = 32; d > 0; d >>= 1) local += __shfl_down(local, d, 64);
@@ -957,11 +1050,14 @@ __global__ __launch_bounds__(1024) void part_scatter_kernel(const i64* __restric
 }
 
 // ---------------------------------------------------------------- host launchers
-// rows staged per scatter pass: a multiple of 1024, <= 4096, staging <= 96 KB
-inline int stage_rows(int F) {
-  const int t = (int)((96 * 1024) / (14 + 8 * F)) / 1024 * 1024;
-  return std::max(1024, std::min(4096, t));
+// rows staged per scatter pass: a multiple of 1024, <= 4096, staging <= budget bytes
+inline int stage_rows(int F, int budget = 48 * 1024, int nthr = 512) {
+  const int t = (int)(budget / (14 + 8 * F)) / nthr * nthr;
+  return std::max(nthr, std::min(4 * nthr, t));
 }
+
+// level-1 histogram / scatter workgroups (two per CU), >= 16 Ki rows each
+inline int agg_groups(long long n) { return (int)std::min<long long>(512, std::max<long long>(1, (n + 16383) / 16384)); }
 
 template <typename VT, int OP>
 int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv, void* meta_v, void* glow_v,
@@ -1001,7 +1097,7 @@ int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv,
   hipLaunchKernelGGL((agg_low_kernel<VT, OP>), dim3(gl), dim3(256), lbytes_low, st, k, v, n, F, lcap_low, glow, meta, o);
   // PART: work buffers [hist P*G u32 | tot P | bstart P+1 | pkey n | pval n*F | prow n (i32) | qkey | qval | qrow]
   const int P = 1 << pbits;
-  const int G = (int)std::min<i64>(256, std::max<i64>(1, (n + 16383) / 16384));
+  const int G = agg_groups(n);
   const i64 rpw = (n + G - 1) / G;
   char* w = reinterpret_cast<char*>(work_v);
   unsigned* hist = reinterpret_cast<unsigned*>(w);
@@ -1013,16 +1109,17 @@ int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv,
   u64* qkey = reinterpret_cast<u64*>(prow + ((n + 1) & ~(i64)1));
   VT* qval = reinterpret_cast<VT*>(qkey + n);
   int* qrow = reinterpret_cast<int*>(qval + n * F);
-  const int T = stage_rows(F);
+  const int T = stage_rows(F);                 // level-1 scatter: two workgroups per CU
   const size_t stage_bytes = (size_t)T * (14 + 8 * F);
-  const size_t lds_bucket = std::max(stage_bytes, lbytes_part);
+  const int T2 = stage_rows(F, 96 * 1024, 1024);     // bucket kernel: one workgroup per CU, larger tiles
+  const size_t lds_bucket = std::max((size_t)T2 * (14 + 8 * F), lbytes_part);
   hipLaunchKernelGGL(agg_hist_kernel, dim3(G), dim3(1024), (size_t)P * 4, st, k, n, rpw, pbits, hist, meta);
-  hipLaunchKernelGGL(scan_rows_kernel, dim3(P), dim3(256), 0, st, hist, G, tot, meta, 1);
-  hipLaunchKernelGGL(scan_tot_kernel, dim3(1), dim3(1024), 0, st, tot, P, (i64)1, bstart, (i64*)nullptr, meta, 1);
-  hipLaunchKernelGGL((agg_scatter_kernel<VT>), dim3(G), dim3(1024), stage_bytes, st, k, v, n, F, rpw, pbits, T, hist,
+  hipLaunchKernelGGL(scan_rows_kernel, dim3(P), dim3(1024), 0, st, hist, G, tot, meta, 1);
+  hipLaunchKernelGGL(scan_tot_kernel, dim3(1), dim3(1024), 0, st, tot, P, bstart, meta, 1);
+  hipLaunchKernelGGL((agg_scatter_kernel<VT>), dim3(G), dim3(512), stage_bytes, st, k, v, n, F, rpw, pbits, T, hist,
                      bstart, pkey, pval, prow, meta);
   hipLaunchKernelGGL((agg_bucket_kernel<VT, OP>), dim3(P), dim3(1024), lds_bucket, st, pkey, pval, prow, F, lcap_part,
-                     pbits, T, n, bstart, qkey, qval, qrow, gpart, meta, o);
+                     pbits, T2, n, bstart, qkey, qval, qrow, gpart, meta, o);
   hipLaunchKernelGGL((agg_emit_kernel<VT, OP>), dim3(512), dim3(256), 0, st, glow, gpart, F, meta, o);
   if (want_inv)
     hipLaunchKernelGGL(agg_fix_inv_kernel, dim3((unsigned)std::min<i64>(2048, (n + 255) / 256)), dim3(256), 0, st,
@@ -1039,7 +1136,7 @@ extern "C" {
 // Byte size of the PART work buffer for (n, F, pbits).
 long long nsdb_agg_work_bytes(long long n, int F, int pbits, int want_inv) {
   const long long P = 1LL << pbits;
-  const long long G = std::min<long long>(256, std::max<long long>(1, (n + 16383) / 16384));
+  const long long G = agg_groups(n);
   (void)want_inv;
   return ((P * G * 4 + 15) & ~15LL) + 8 * (2 * P + 2) + 2 * (8 * n + 8 * n * F + 4 * (n + 1)) + 64;
 }
@@ -1054,7 +1151,7 @@ int nsdb_hash_aggregate(const void* keys, const void* vals, long long n, int F, 
   auto pow2 = [](long long x) { return x > 0 && (x & (x - 1)) == 0; };
   if (!pow2(gcap_low) || !pow2(gcap_part) || !pow2(lcap_low) || !pow2(lcap_part)) return (int)hipErrorInvalidValue;
   if ((size_t)lcap_low * (28 + 8 * F) > 65536 || (size_t)lcap_part * (28 + 8 * F) > 131072) return (int)hipErrorInvalidValue;
-  if ((size_t)stage_rows(F) * (14 + 8 * F) > 131072) return (int)hipErrorInvalidValue;
+  if ((size_t)stage_rows(F, 96 * 1024, 1024) * (14 + 8 * F) > 131072) return (int)hipErrorInvalidValue;
 #define NSDB_AGG(VT, OP) agg_launch_t<VT, OP>(keys, vals, n, F, want_inv, meta, glow, gcap_low, gpart, gcap_part, out, work, pbits, lcap_low, lcap_part, low_thr, st)
   if (vt == 0) {
     if (op == 0) return NSDB_AGG(double, OP_SUM);
@@ -1128,9 +1225,8 @@ int nsdb_partition_perm(const long long* dest, long long n, int P, void* work, l
   long long* tot = reinterpret_cast<long long*>(w + (((size_t)P * G * 4 + 15) & ~(size_t)15));
   long long* bstart = tot + P;
   hipLaunchKernelGGL(part_hist_kernel, dim3(G), dim3(1024), (size_t)P * 4, st, dest, n, rpw, P, hist);
-  hipLaunchKernelGGL(scan_rows_kernel, dim3(P), dim3(256), 0, st, hist, G, tot, (const AggMeta*)nullptr, 0);
-  hipLaunchKernelGGL(scan_tot_kernel, dim3(1), dim3(1024), 0, st, tot, P, (long long)1, bstart, (long long*)nullptr,
-                     (AggMeta*)nullptr, 0);
+  hipLaunchKernelGGL(scan_rows_kernel, dim3(P), dim3(1024), 0, st, hist, G, tot, (const AggMeta*)nullptr, 0);
+  hipLaunchKernelGGL(scan_tot_kernel, dim3(1), dim3(1024), 0, st, tot, P, bstart, (AggMeta*)nullptr, 0);
   hipLaunchKernelGGL(part_scatter_kernel, dim3(G), dim3(1024), lds, st, dest, n, rpw, P, hist, bstart, perm);
   if (counts) (void)hipMemcpyAsync(counts, tot, sizeof(long long) * P, hipMemcpyDeviceToDevice, st);
   return (int)hipGetLastError();
