@@ -306,15 +306,17 @@ __global__ __launch_bounds__(1024) void agg_sample_kernel(const u64* __restrict_
         s = (s + 1) & (CAP - 1);
       }
     }
-    // one LDS add per distinct slot of the wave (a few hot keys would serialise 64 lanes on one word)
+    // hot keys: one LDS add per distinct slot for up to 4 slots of the wave (a handful of keys would serialise
+    // 64 lanes on one word); the remaining lanes (many distinct keys) add one by one
     u64 todo = __ballot(active);
-    while (todo) {
+    for (int r = 0; r < 4 && todo; ++r) {
       const int leader = __ffsll((long long)todo) - 1;
       const int ls = __shfl(s, leader, 64);
       const u64 m = __ballot(active && s == ls);
       if (lane == leader) atomicAdd(tcnt + ls, (unsigned)__popcll(m));
       todo &= ~m;
     }
+    if ((todo >> lane) & 1ull) atomicAdd(tcnt + s, 1u);
   }
   __syncthreads();
   unsigned d = 0, f1 = 0, f2 = 0;
@@ -632,7 +634,7 @@ __device__ __forceinline__ void staged_scatter(const u64* __restrict__ skey, con
 
 // level-1 scatter: workgroup g packs its rows [g * rpw, ...) into the P1 buckets at bstart[b] + hist[b][g]
 template <typename VT>
-__global__ __launch_bounds__(512) void agg_scatter_kernel(const u64* __restrict__ keys, const VT* __restrict__ vals,
+__global__ __launch_bounds__(1024) void agg_scatter_kernel(const u64* __restrict__ keys, const VT* __restrict__ vals,
                                                            i64 n, int F, i64 rpw, int pbits, int T,
                                                            const unsigned* __restrict__ hist,
                                                            const i64* __restrict__ bstart, u64* __restrict__ pkey,
@@ -1056,8 +1058,8 @@ inline int stage_rows(int F, int budget = 48 * 1024, int nthr = 512) {
   return std::max(nthr, std::min(4 * nthr, t));
 }
 
-// level-1 histogram / scatter workgroups (two per CU), >= 16 Ki rows each
-inline int agg_groups(long long n) { return (int)std::min<long long>(512, std::max<long long>(1, (n + 16383) / 16384)); }
+// level-1 histogram / scatter workgroups (one per CU), >= 16 Ki rows each
+inline int agg_groups(long long n) { return (int)std::min<long long>(256, std::max<long long>(1, (n + 16383) / 16384)); }
 
 template <typename VT, int OP>
 int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv, void* meta_v, void* glow_v,
@@ -1109,14 +1111,14 @@ int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv,
   u64* qkey = reinterpret_cast<u64*>(prow + ((n + 1) & ~(i64)1));
   VT* qval = reinterpret_cast<VT*>(qkey + n);
   int* qrow = reinterpret_cast<int*>(qval + n * F);
-  const int T = stage_rows(F);                 // level-1 scatter: two workgroups per CU
+  const int T = stage_rows(F, 96 * 1024, 1024);   // level-1 scatter: one 1024-thread workgroup per CU
   const size_t stage_bytes = (size_t)T * (14 + 8 * F);
   const int T2 = stage_rows(F, 96 * 1024, 1024);     // bucket kernel: one workgroup per CU, larger tiles
   const size_t lds_bucket = std::max((size_t)T2 * (14 + 8 * F), lbytes_part);
   hipLaunchKernelGGL(agg_hist_kernel, dim3(G), dim3(1024), (size_t)P * 4, st, k, n, rpw, pbits, hist, meta);
   hipLaunchKernelGGL(scan_rows_kernel, dim3(P), dim3(1024), 0, st, hist, G, tot, meta, 1);
   hipLaunchKernelGGL(scan_tot_kernel, dim3(1), dim3(1024), 0, st, tot, P, bstart, meta, 1);
-  hipLaunchKernelGGL((agg_scatter_kernel<VT>), dim3(G), dim3(512), stage_bytes, st, k, v, n, F, rpw, pbits, T, hist,
+  hipLaunchKernelGGL((agg_scatter_kernel<VT>), dim3(G), dim3(1024), stage_bytes, st, k, v, n, F, rpw, pbits, T, hist,
                      bstart, pkey, pval, prow, meta);
   hipLaunchKernelGGL((agg_bucket_kernel<VT, OP>), dim3(P), dim3(1024), lds_bucket, st, pkey, pval, prow, F, lcap_part,
                      pbits, T2, n, bstart, qkey, qval, qrow, gpart, meta, o);

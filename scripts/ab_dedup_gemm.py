@@ -46,6 +46,9 @@ def main():
     xb = Xpc.unsqueeze(0).expand(12, -1, -1)
     us = t(lambda: ops.gemm_nt(Wp, xb, P, ops.BIAS_MAT, out_dtype=torch.float32))
     print(f"private batched contiguous X   {us:8.1f} us  {gb(1.2e9, us)}")
+    for cfg, sp in ((2, 0), (2, 10), (2, 16), (2, 21)):
+        us = t(lambda: ops.gemm_nt(Wp, xb, P, ops.BIAS_MAT, out_dtype=torch.float32, cfg=cfg, splits=sp))
+        print(f"private batched cfg={cfg} splits={sp:3d} {us:8.1f} us  {gb(1.2e9, us)}")
     us = t(lambda: [ops.gemm_nt(Wp[i], Xp, P, ops.BIAS_MAT, out_dtype=torch.float32) for i in range(12)])
     print(f"private loop of 12            {us:8.1f} us  {gb(1.2e9, us)}  splits={ops.gemm_splits(500, 100, 100000)}")
     Wflat = Wp.reshape(6000, 100_000)

@@ -59,6 +59,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--host-profile", default=None, help="directory: cProfile of one timed run per query")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     queries = a.queries.split(",")
@@ -88,6 +89,19 @@ def main():
                 got = fn(c, "tpch")
                 torch.cuda.synchronize()
                 ts.append(time.perf_counter() - t0)
+            if a.host_profile:
+                import cProfile
+                import pstats
+
+                os.makedirs(a.host_profile, exist_ok=True)
+                pr = cProfile.Profile()
+                torch.cuda.synchronize()
+                pr.enable()
+                fn(c, "tpch")
+                torch.cuda.synchronize()
+                pr.disable()
+                with open(os.path.join(a.host_profile, f"{q}_sf{sf:g}.txt"), "w") as f:
+                    pstats.Stats(pr, stream=f).sort_stats("tottime").print_stats(40)
             ok = None
             if frames is not None:
                 t0 = time.perf_counter()
