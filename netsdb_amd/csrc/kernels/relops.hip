@@ -365,7 +365,7 @@ __global__ __launch_bounds__(256) void agg_init_kernel(u64* glow, i64 cap_low, u
 
 // ---------------------------------------------------------------- LOW path
 constexpr int kU = 4;        // rows per thread loaded before any is processed (memory-level parallelism)
-constexpr int kPreF = 2;     // value columns loaded with the keys (the rest at use)
+constexpr int kPreF = 1;     // value columns loaded with the keys (the rest at use)
 
 // Row (key, values) batch of one thread: kU rows of a 256*kU-row tile, loaded together.
 template <typename VT>
@@ -385,10 +385,8 @@ struct RowBatch {
 };
 
 template <typename VT, int OP>
-__device__ __forceinline__ void ltable_add_row(LTable t, int s, const VT* pre, const VT* __restrict__ vrow, int F,
-                                               u64 row) {
-  for (int f = 0; f < F; ++f)
-    acc_add<VT, OP, __HIP_MEMORY_SCOPE_WORKGROUP>(t.acc + s * F + f, f < kPreF ? pre[f] : vrow[f]);
+__device__ __forceinline__ void ltable_add_row(LTable t, int s, VT v0, const VT* __restrict__ vrow, int F, u64 row) {
+  for (int f = 0; f < F; ++f) acc_add<VT, OP, __HIP_MEMORY_SCOPE_WORKGROUP>(t.acc + s * F + f, f == 0 ? v0 : vrow[f]);
   __hip_atomic_fetch_add(t.cnt + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   if (row < t.rmin[s]) __hip_atomic_fetch_min(t.rmin + s, row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -404,25 +402,26 @@ __global__ __launch_bounds__(256) void agg_low_kernel(const u64* __restrict__ ke
   constexpr int TILE = 256 * kU;
   const i64 tstride = (i64)gridDim.x * TILE;
   int it = 0;
-  for (i64 t0 = (i64)blockIdx.x * TILE; t0 < n; t0 += tstride, ++it) {
+  RowBatch<VT> cur, nxt;
+  i64 t0 = (i64)blockIdx.x * TILE;
+  if (t0 < n) cur.load(keys, vals, t0, n, F, 256);
+  for (; t0 < n; t0 += tstride, ++it) {
     if ((it & 15) == 15 && __hip_atomic_load(&meta->fail_low, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
-    RowBatch<VT> rb;
-    rb.load(keys, vals, t0, n, F, 256);
+    if (t0 + tstride < n) nxt.load(keys, vals, t0 + tstride, n, F, 256);   // in flight during this tile
 #pragma unroll
     for (int j = 0; j < kU; ++j) {
       const i64 i = t0 + j * 256 + threadIdx.x;
       if (i >= n) break;
-      const u64 k = rb.k[j];
+      const u64 k = cur.k[j];
       const VT* v = vals + i * F;
       const int s = k != kEmpty ? ltable_slot(t, k, mix64(k)) : -1;
       if (s >= 0) {
-        ltable_add_row<VT, OP>(t, s, rb.v[j], v, F, (u64)i);
-      } else {
-        VT tmp[16];
-        for (int f = 0; f < F; ++f) tmp[f] = f < kPreF ? rb.v[j][f] : v[f];
-        row_into_global<VT, OP>(g, k, tmp, F, &meta->ng_low, &meta->sentinel_low, &meta->fail_low, o, i);
+        ltable_add_row<VT, OP>(t, s, cur.v[j][0], v, F, (u64)i);
+      } else {   // rare: the values are re-read from memory
+        row_into_global<VT, OP>(g, k, v, F, &meta->ng_low, &meta->sentinel_low, &meta->fail_low, o, i);
       }
     }
+    cur = nxt;
   }
   __syncthreads();
   // one flush per (workgroup, key)
@@ -547,13 +546,13 @@ __global__ __launch_bounds__(1024) void scan_tot_kernel(const i64* __restrict__ 
 // ranks from the histogram atomics), then writes each bucket's run contiguously at run[b], so the global
 // stores are long coalesced runs instead of one random 8-byte store per row. run[] (LDS, i64 [P]) is
 // advanced by the tile's counts. Row order inside a bucket is not preserved (the aggregates keep min row ids).
-template <typename VT>
+template <typename VT, int R>
 __device__ __forceinline__ void staged_scatter(const u64* __restrict__ skey, const VT* __restrict__ sval,
                                                const int* __restrict__ srow, i64 r0, i64 r1, int F, int shift,
                                                int P, int T, char* lds, i64* run, unsigned* cnt, unsigned* off,
                                                unsigned* wsum, u64* __restrict__ dkey, VT* __restrict__ dval,
                                                int* __restrict__ drow) {
-  constexpr int R = 4;   // rows per thread per tile (T <= 4 * blockDim)
+  // R rows per thread per tile (T <= R * blockDim)
   const int nthr = blockDim.x;
   u64* st_key = reinterpret_cast<u64*>(lds);
   VT* st_val = reinterpret_cast<VT*>(st_key + T);
@@ -561,29 +560,29 @@ __device__ __forceinline__ void staged_scatter(const u64* __restrict__ skey, con
   unsigned short* st_b = reinterpret_cast<unsigned short*>(st_row + T);
   __shared__ unsigned tot_sh;
   const unsigned pmask = (unsigned)P - 1;
+  const int rowsrc = srow != nullptr;
+  // the next tile's keys / first value / row ids are loaded while this tile goes through its LDS phases
+  u64 k[R], nk[R];
+  VT v0[R], nv0[R];
+  int rw[R], nrw[R];
+  auto load_tile = [&](i64 tb, u64 (&kk)[R], VT (&vv)[R], int (&rr)[R]) {
+    const int tnn = (int)std::min<i64>(T, r1 - tb);
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int p = threadIdx.x + j * nthr;
+      const bool in = p < tnn;
+      kk[j] = in ? skey[tb + p] : 0;
+      vv[j] = (in && F > 0) ? sval[(tb + p) * F] : VT(0);
+      rr[j] = in ? (rowsrc ? srow[tb + p] : (int)(tb + p)) : 0;
+    }
+  };
+  if (r0 < r1) load_tile(r0, k, v0, rw);
   for (i64 t0 = r0; t0 < r1; t0 += T) {
     const int tn = (int)std::min<i64>(T, r1 - t0);
     for (int b = threadIdx.x; b < P; b += blockDim.x) cnt[b] = 0;
     __syncthreads();
-    u64 k[R];
     int bk[R];
     unsigned rk[R];
-    VT pv[R][kPreF];
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-      const int p = threadIdx.x + j * nthr;
-      const i64 i = t0 + p;
-      k[j] = p < tn ? skey[i] : 0;
-#pragma unroll
-      for (int f = 0; f < kPreF; ++f) pv[j][f] = (p < tn && f < F) ? sval[i * F + f] : VT(0);
-    }
-    const int rowsrc = srow != nullptr;
-    int rw[R];
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-      const int p = threadIdx.x + j * nthr;
-      rw[j] = p < tn ? (rowsrc ? srow[t0 + p] : (int)(t0 + p)) : 0;
-    }
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       const int p = threadIdx.x + j * nthr;
@@ -592,6 +591,7 @@ __device__ __forceinline__ void staged_scatter(const u64* __restrict__ skey, con
         rk[j] = atomicAdd(cnt + bk[j], 1u);
       }
     }
+    if (t0 + T < r1) load_tile(t0 + T, nk, nv0, nrw);
     __syncthreads();
     // exclusive scan of cnt[0..P) (P <= 4 * blockDim buckets)
     {
@@ -615,7 +615,7 @@ __device__ __forceinline__ void staged_scatter(const u64* __restrict__ skey, con
         st_key[q] = k[j];
         st_row[q] = rw[j];
         st_b[q] = (unsigned short)bk[j];
-        for (int f = 0; f < F; ++f) st_val[(size_t)q * F + f] = f < kPreF ? pv[j][f] : sval[i * F + f];
+        for (int f = 0; f < F; ++f) st_val[(size_t)q * F + f] = f == 0 ? v0[j] : sval[i * F + f];
       }
     }
     __syncthreads();
@@ -629,6 +629,12 @@ __device__ __forceinline__ void staged_scatter(const u64* __restrict__ skey, con
     __syncthreads();
     for (int b = threadIdx.x; b < P; b += blockDim.x) run[b] += cnt[b];
     __syncthreads();
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      k[j] = nk[j];
+      v0[j] = nv0[j];
+      rw[j] = nrw[j];
+    }
   }
 }
 
@@ -648,7 +654,7 @@ __global__ __launch_bounds__(1024) void agg_scatter_kernel(const u64* __restrict
   for (int b = threadIdx.x; b < P; b += blockDim.x) run[b] = bstart[b] + hist[(size_t)b * gridDim.x + blockIdx.x];
   __syncthreads();
   const i64 r0 = (i64)blockIdx.x * rpw, r1 = std::min<i64>(n, r0 + rpw);
-  staged_scatter<VT>(keys, vals, nullptr, r0, r1, F, 64 - pbits, P, T, lds_raw, run, cnt, off, wsum, pkey, pval, prow);
+  staged_scatter<VT, 4>(keys, vals, nullptr, r0, r1, F, 64 - pbits, P, T, lds_raw, run, cnt, off, wsum, pkey, pval, prow);
 }
 
 // ngrp thread groups (blockDim / ngrp threads each, ngrp <= 4) each aggregate their rows [a, e) of (key, val,
@@ -666,19 +672,24 @@ __device__ __forceinline__ void agg_ranges_dense(const u64* __restrict__ pkey, c
   ltable_clear<VT, OP>(t, F, lt, gs);
   if (threadIdx.x < 4) nocc[threadIdx.x] = 0;
   __syncthreads();
-  for (i64 b0 = a; b0 < e; b0 += (i64)gs * kU) {
-    u64 k[kU];
-    int rw[kU];
-    VT pv[kU][kPreF];
+  // double-buffered row batches: batch b+1 is in flight while batch b goes into the LDS table
+  const i64 step = (i64)gs * kU;
+  u64 k[kU], nk[kU];
+  int rw[kU], nrw[kU];
+  VT v0[kU], nv0[kU];
+  auto load_b = [&](i64 b0, u64 (&kk)[kU], int (&rr)[kU], VT (&vv)[kU]) {
 #pragma unroll
     for (int j = 0; j < kU; ++j) {
       const i64 r = b0 + (i64)j * gs + lt;
       const bool in = r < e;
-      k[j] = in ? pkey[r] : kEmpty;
-      rw[j] = in ? prow[r] : 0;
-#pragma unroll
-      for (int f = 0; f < kPreF; ++f) pv[j][f] = (in && f < F) ? pval[r * F + f] : VT(0);
+      kk[j] = in ? pkey[r] : kEmpty;
+      rr[j] = in ? prow[r] : 0;
+      vv[j] = (in && F > 0) ? pval[r * F] : VT(0);
     }
+  };
+  if (a < e) load_b(a, k, rw, v0);
+  for (i64 b0 = a; b0 < e; b0 += step) {
+    if (b0 + step < e) load_b(b0 + step, nk, nrw, nv0);
 #pragma unroll
     for (int j = 0; j < kU; ++j) {
       const i64 r = b0 + (i64)j * gs + lt;
@@ -686,12 +697,16 @@ __device__ __forceinline__ void agg_ranges_dense(const u64* __restrict__ pkey, c
       const VT* v = pval + r * F;
       const int sl = k[j] != kEmpty ? ltable_slot(t, k[j], mix64(k[j])) : -1;
       if (sl >= 0) {
-        ltable_add_row<VT, OP>(t, sl, pv[j], v, F, (u64)rw[j]);
-      } else {
-        VT tmp[16];
-        for (int f = 0; f < F; ++f) tmp[f] = f < kPreF ? pv[j][f] : v[f];
-        row_into_global<VT, OP>(g, k[j], tmp, F, &meta->ng_part, &meta->sentinel_part, &meta->fail_part, o, rw[j]);
+        ltable_add_row<VT, OP>(t, sl, v0[j], v, F, (u64)rw[j]);
+      } else {   // rare (the table's probe window is full): the values are re-read from memory
+        row_into_global<VT, OP>(g, k[j], v, F, &meta->ng_part, &meta->sentinel_part, &meta->fail_part, o, rw[j]);
       }
+    }
+#pragma unroll
+    for (int j = 0; j < kU; ++j) {
+      k[j] = nk[j];
+      rw[j] = nrw[j];
+      v0[j] = nv0[j];
     }
   }
   __syncthreads();
@@ -793,7 +808,7 @@ __global__ __launch_bounds__(1024) void agg_bucket_kernel(const u64* __restrict_
     if (threadIdx.x == 0) sb[P2] = (unsigned)nb;
   }
   __syncthreads();
-  staged_scatter<VT>(pkey, pval, prow, r0, r1, F, shift, P2, T, lds_raw, run, cnt, off, wsum, qkey, qval, qrow);
+  staged_scatter<VT, 2>(pkey, pval, prow, r0, r1, F, shift, P2, T, lds_raw, run, cnt, off, wsum, qkey, qval, qrow);
   // this workgroup reads back what its own waves stored: drain the stores, then drop this CU's L1 lines
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1113,7 +1128,7 @@ int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv,
   int* qrow = reinterpret_cast<int*>(qval + n * F);
   const int T = stage_rows(F, 96 * 1024, 1024);   // level-1 scatter: one 1024-thread workgroup per CU
   const size_t stage_bytes = (size_t)T * (14 + 8 * F);
-  const int T2 = stage_rows(F, 96 * 1024, 1024);     // bucket kernel: one workgroup per CU, larger tiles
+  const int T2 = std::min(2048, stage_rows(F, 96 * 1024, 1024));   // bucket kernel's sub-partition tiles (2 rows / thread)
   const size_t lds_bucket = std::max((size_t)T2 * (14 + 8 * F), lbytes_part);
   hipLaunchKernelGGL(agg_hist_kernel, dim3(G), dim3(1024), (size_t)P * 4, st, k, n, rpw, pbits, hist, meta);
   hipLaunchKernelGGL(scan_rows_kernel, dim3(P), dim3(1024), 0, st, hist, G, tot, meta, 1);
