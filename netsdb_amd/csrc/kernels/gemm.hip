@@ -916,7 +916,12 @@ static int pick_cfg(int M, int N, int K, int batch) {
   const long long ksteps = (K + nsdb::BK - 1) / nsdb::BK;
   // 8-phase 256^2 when there is a long mainloop, or when >= 3/4 of the CUs get a tile and K spans at
   // least 16 k-tiles (the FF output layer 1000x14588x1000: 60 us vs 75 us for 128^2, kernel trace)
-  return (fills && (big_tiles * ksteps >= 256LL * 32 || (big_tiles >= 192 && ksteps >= 16))) ? 2 : 0;
+  if (fills && (big_tiles * ksteps >= 256LL * 32 || (big_tiles >= 192 && ksteps >= 16))) return 2;
+  // skinny, very long K (the dedup scoring GEMMs 500 x 100 x 900k and 12 x 500 x 100 x 100k): memory-bound; the
+  // 8-phase kernel keeps three half-tiles of A in flight and zero-fills the missing B rows without reading them
+  // (common panel 205 vs 222 us, batched private panels 263 vs 285 us, profiles/r4_dedup)
+  if ((M >= 192 || N >= 192) && std::min(M, N) >= 64 && ksteps >= 1024) return 2;
+  return 0;
 }
 
 static int resolve_cfg(int cfg, int M, int N, int K, int batch) { return cfg < 0 ? pick_cfg(M, N, K, batch) : cfg; }

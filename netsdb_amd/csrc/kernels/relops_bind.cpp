@@ -91,8 +91,8 @@ std::vector<torch::Tensor> hash_aggregate(torch::Tensor keys, c10::optional<torc
   // LDS tables: LOW <= 64 KiB (two workgroups per CU), PART <= 128 KiB. PART: level-1 buckets = one per CU
   // (256) once there are >= 2048 rows per bucket; each bucket workgroup splits its bucket further on the device
   // from the sampled distinct-key estimate (relops.hip agg_bucket_kernel), so no host decision needs the data.
-  const int64_t entry = 28 + 8 * F;
-  const int64_t lcap_low = std::min<int64_t>(2048, pow2_at_most(65536 / entry));
+  const int64_t entry = 20 + 8 * F;
+  const int64_t lcap_low = std::min<int64_t>(1024, pow2_at_most(65536 / entry));   // <= 36 KB: 4+ LOW workgroups per CU
   const int64_t lcap_part = std::min<int64_t>(4096, pow2_at_most(131072 / entry));
   int pbits = 0;
   while (pbits < 8 && (n >> (pbits + 1)) >= 2048) ++pbits;
