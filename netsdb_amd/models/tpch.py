@@ -487,11 +487,13 @@ def q03(client, db: str, segment: str = "BUILDING", date: int = 19950315, k: int
     r = _flat(_run(client, db, "q03_out", agg.set_input(j), "tpch_q03"))
     if r is None:
         return []
-    rows = [{"l_orderkey": int(a), "o_orderdate": int(b_), "o_shippriority": int(c), "revenue": float(v)}
-            for a, b_, c, v in zip(_as_list(r.columns["k0"]), _as_list(r.columns["k1"]), _as_list(r.columns["k2"]),
-                                   _as_list(r.columns["revenue"]))]
-    rows.sort(key=lambda x: (-x["revenue"], x["o_orderdate"], x["l_orderkey"]))
-    return rows[:k]
+    # top-k on the device (revenue desc, orderdate, orderkey): three stable sorts, only k rows reach the host
+    ok_, od, sp, rev = (torch.as_tensor(r.columns[c]) for c in ("k0", "k1", "k2", "revenue"))
+    order = torch.argsort(ok_, stable=True)
+    order = order[torch.argsort(od[order], stable=True)]
+    order = order[torch.argsort(-rev[order].double(), stable=True)][:k]
+    return [{"l_orderkey": int(a), "o_orderdate": int(b_), "o_shippriority": int(c), "revenue": float(v)}
+            for a, b_, c, v in zip(ok_[order].tolist(), od[order].tolist(), sp[order].tolist(), rev[order].tolist())]
 
 
 def q04(client, db: str, date: int = 19930701) -> List[dict]:

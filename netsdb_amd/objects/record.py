@@ -367,58 +367,63 @@ def make_column(vals: List[Any], ft, device=None):
     return list(vals)
 
 
-def _adjacent_tensors(parts) -> Optional[torch.Tensor]:
-    """One view over row-slices that sit back to back in one storage (pages cut from one loaded batch), else None."""
+def _adjacent_tensors(parts, check: bool = True) -> Optional[torch.Tensor]:
+    """One view over row-slices that sit back to back in one storage (pages cut from one loaded batch), else None.
+    ``check=False``: the caller already verified the layout (a cached scan plan)."""
     p0 = parts[0]
     if p0.dim() == 0:
         return None
-    ptr, stride, inner = p0.untyped_storage().data_ptr(), p0.stride(), p0.shape[1:]
-    off = p0.storage_offset() + p0.shape[0] * stride[0]
-    for p in parts[1:]:
-        if (p.untyped_storage().data_ptr() != ptr or p.dtype != p0.dtype or p.stride() != stride
-                or p.shape[1:] != inner or p.storage_offset() != off):
-            return None
-        off += p.shape[0] * stride[0]
+    if check:
+        ptr, stride, inner = p0.untyped_storage().data_ptr(), p0.stride(), p0.shape[1:]
+        off = p0.storage_offset() + p0.shape[0] * stride[0]
+        for p in parts[1:]:
+            if (p.untyped_storage().data_ptr() != ptr or p.dtype != p0.dtype or p.stride() != stride
+                    or p.shape[1:] != inner or p.storage_offset() != off):
+                return None
+            off += p.shape[0] * stride[0]
     n = sum(p.shape[0] for p in parts)
-    return p0.as_strided((n,) + tuple(inner), stride, p0.storage_offset())
+    return p0.as_strided((n,) + tuple(p0.shape[1:]), p0.stride(), p0.storage_offset())
 
 
-def merge_adjacent_column(parts):
+def merge_adjacent_column(parts, check: bool = True):
     """Zero-copy merge of one column's page slices (None when they are not views of one buffer)."""
     c0 = parts[0]
     if isinstance(c0, torch.Tensor):
-        return _adjacent_tensors(parts) if all(isinstance(p, torch.Tensor) for p in parts) else None
+        return _adjacent_tensors(parts, check) if all(isinstance(p, torch.Tensor) for p in parts) else None
     if isinstance(c0, StringColumn):
         if not all(isinstance(p, StringColumn) and p.data is c0.data for p in parts):
             return None
         if all(p.is_packed for p in parts):
             offs = [p._off for p in parts]
             o0 = offs[0]
-            ptr, pos = o0.untyped_storage().data_ptr(), o0.storage_offset() + o0.numel() - 1
-            for o in offs[1:]:
-                if o.untyped_storage().data_ptr() != ptr or o.stride() != (1,) or o.storage_offset() != pos:
-                    break
-                pos += o.numel() - 1
-            else:
-                n = sum(len(p) for p in parts)
-                return StringColumn(c0.data, o0.as_strided((n + 1,), (1,), o0.storage_offset()),
-                                    max(p.payload for p in parts), c0.buf_rows)
-            return None
+            ok = True
+            if check:
+                ptr, pos = o0.untyped_storage().data_ptr(), o0.storage_offset() + o0.numel() - 1
+                for o in offs[1:]:
+                    if o.untyped_storage().data_ptr() != ptr or o.stride() != (1,) or o.storage_offset() != pos:
+                        ok = False
+                        break
+                    pos += o.numel() - 1
+            if not ok:
+                return None
+            n = sum(len(p) for p in parts)
+            return StringColumn(c0.data, o0.as_strided((n + 1,), (1,), o0.storage_offset()),
+                                max(p.payload for p in parts), c0.buf_rows)
         # views: their row-bound arrays must themselves be adjacent slices (no copy is ever made here)
-        st = _adjacent_tensors([p.starts for p in parts])
-        en = _adjacent_tensors([p.ends for p in parts]) if st is not None else None
+        st = _adjacent_tensors([p.starts for p in parts], check)
+        en = _adjacent_tensors([p.ends for p in parts], check) if st is not None else None
         if st is None or en is None:
             return None
         return StringColumn.view(c0.data, st, en, max(p.payload for p in parts), max(p.buf_rows for p in parts))
     if isinstance(c0, tuple):
-        subs = [merge_adjacent_column([p[i] for p in parts]) for i in range(len(c0))]
+        subs = [merge_adjacent_column([p[i] for p in parts], check) for i in range(len(c0))]
         return None if any(x is None for x in subs) else tuple(subs)
     if isinstance(c0, RecordBatch):
-        return merge_adjacent_batches(parts)
+        return merge_adjacent_batches(parts, check)
     return None
 
 
-def merge_adjacent_batches(batches: Sequence["RecordBatch"]) -> Optional["RecordBatch"]:
+def merge_adjacent_batches(batches: Sequence["RecordBatch"], check: bool = True) -> Optional["RecordBatch"]:
     """The batches as ONE batch without copying row data, when every column of each is a row-slice of the same
     buffer as the previous one's (device pages of one set loaded from one batch); None otherwise."""
     b0 = batches[0]
@@ -427,7 +432,7 @@ def merge_adjacent_batches(batches: Sequence["RecordBatch"]) -> Optional["Record
         parts = [b.columns.get(k) for b in batches]
         if any(x is None for x in parts):
             return None
-        m = merge_adjacent_column(parts)
+        m = merge_adjacent_column(parts, check)
         if m is None:
             return None
         cols[k] = m

@@ -361,47 +361,57 @@ class UserSet:
     SCAN_COALESCE_BYTES = 4 << 30
     COALESCE_ANY_DEVICE = False      # tests: run the merge on CPU pages too
 
-    def _scan_coalesced(self, pages, device) -> Iterator[RecordBatch]:
-        """Runs of consecutive pages resident on ``device`` whose columns are adjacent slices of one buffer are
-        yielded as ONE batch (zero-copy views, up to SCAN_COALESCE_BYTES); any other page is yielded alone."""
-        i = 0
+    def _coalesce_runs(self, pages, device) -> List[Tuple[int, int]]:
+        """[i, j) runs of consecutive resident pages whose columns are adjacent slices of one buffer (checked once;
+        the plan is cached while the pages and their resident batches stay the same objects)."""
+        key = tuple((id(p), id(p.batch), p.n) for p in pages) + (str(device),)
+        if getattr(self, "_coalesce_key", None) == key:
+            return self._coalesce_plan
+        runs, i = [], 0
         while i < len(pages):
-            run, nbytes = [], 0
-            j = i
+            j, nbytes = i, 0
             while j < len(pages) and nbytes < self.SCAN_COALESCE_BYTES:
                 b = pages[j].batch
                 if b is None or not _same_device(b.device, device):
                     break
-                if run and merge_adjacent_batches([run[-1].batch, b]) is None:
+                if j > i and merge_adjacent_batches([pages[j - 1].batch, b]) is None:
                     break                          # not a continuation of the previous page's buffers
-                run.append(pages[j])
                 nbytes += pages[j].nbytes
                 j += 1
-            merged = None
-            if len(run) > 1:
+            if j - i > 1 and merge_adjacent_batches([p.batch for p in pages[i:j]]) is not None:
+                runs.append((i, j))
+                i = j
+            else:
+                runs.append((i, i + 1))
+                i += 1
+        self._coalesce_key, self._coalesce_plan = key, runs
+        return runs
+
+    def _scan_coalesced(self, pages, device) -> Iterator[RecordBatch]:
+        """Runs of consecutive pages resident on ``device`` whose columns are adjacent slices of one buffer are
+        yielded as ONE batch (zero-copy views, up to SCAN_COALESCE_BYTES); any other page is yielded alone."""
+        for i, j in self._coalesce_runs(pages, device):
+            run = pages[i:j]
+            if j - i > 1 and all(p.batch is not None for p in run):
                 for p in run:
                     p.pins += 1
                 try:
-                    merged = merge_adjacent_batches([p.batch for p in run])
-                    if merged is not None:
-                        for p in run:
-                            self.manager.touch(p)
-                        yield merged
+                    merged = merge_adjacent_batches([p.batch for p in run], check=False)
+                    for p in run:
+                        self.manager.touch(p)
+                    yield merged
                 finally:
                     for p in run:
                         p.pins -= 1
-            if merged is not None:
-                i = j
                 continue
-            p = pages[i]
-            p.pins += 1
-            try:
-                b = p.load(device)
-                self.manager.touch(p)
-                yield b
-            finally:
-                p.pins -= 1
-            i += 1
+            for p in run:
+                p.pins += 1
+                try:
+                    b = p.load(device)
+                    self.manager.touch(p)
+                    yield b
+                finally:
+                    p.pins -= 1
 
     def all(self, device=None) -> Optional[RecordBatch]:
         bs = list(self.scan(device))
