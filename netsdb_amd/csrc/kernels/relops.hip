@@ -115,8 +115,8 @@ struct AggMeta {
   i64 fail_part;      // PART global table overflowed -> the caller falls back
   i64 sentinel_low;   // the kEmpty key's group was created (LOW / PART)
   i64 sentinel_part;
-  i64 nwork;          // PART work items (chunks)
-  i64 wnext;          // PART dequeue counter
+  i64 occ_low;        // slots claimed in the LOW global table (its fill, apart from the group count)
+  i64 occ_part;       // slots claimed in the PART overflow table
   i64 pad[6];
 };
 
@@ -127,6 +127,7 @@ struct GTable {                     // open-addressing global table: cap slots +
   u64* rmin;                        // [cap + 1], preset ~0: smallest row index of the group
   i64* gid_of_slot;                 // [cap + 1]
   u64 mask;                         // cap - 1
+  i64* occ;                         // claimed-slot counter (AggMeta::occ_*)
 };
 
 struct AggOut {
@@ -166,8 +167,9 @@ __device__ __forceinline__ i64 gtable_slot(GTable t, u64 k, i64* ngroups, i64* s
       if (__hip_atomic_compare_exchange_strong(t.key + s, &cur, k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT)) {
         const i64 gid = __hip_atomic_fetch_add(ngroups, (i64)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // more groups than half the table: probe windows grow long -> give up on this table
-        if ((u64)gid > (t.mask >> 1)) __hip_atomic_store(fail, (i64)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the table more than half full: probe windows grow long -> give up on this table
+        const i64 used = __hip_atomic_fetch_add(t.occ, (i64)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((u64)used > (t.mask >> 1)) __hip_atomic_store(fail, (i64)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         t.gid_of_slot[s] = gid;
         o.reps[gid] = (i64)k;
         o.slot_of_gid[gid] = (i64)s;
@@ -1096,7 +1098,9 @@ int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv,
     t.mask = (u64)(cap - 1);
     return t;
   };
-  const GTable glow = mk(glow_v, gcap_low), gpart = mk(gpart_v, gcap_part);
+  GTable glow = mk(glow_v, gcap_low), gpart = mk(gpart_v, gcap_part);
+  glow.occ = &meta->occ_low;
+  gpart.occ = &meta->occ_part;
   i64* ob = reinterpret_cast<i64*>(out_v);   // [reps n | aggs n*F | cnt n | slot_of_gid n | first n | inv n]
   AggOut o;
   o.reps = ob;
