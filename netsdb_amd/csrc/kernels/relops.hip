@@ -775,8 +775,8 @@ __global__ __launch_bounds__(1024) void agg_bucket_kernel(const u64* __restrict_
   const i64 est = meta->est;
   const i64 db = std::min<i64>(nb, (5 * ((est + P1 - 1) / P1)) / 4 + 16);
   if (4 * db <= 3 * lcap) {
-    int cap = 64;
-    while (cap < lcap && 3 * cap < 4 * db) cap <<= 1;
+    int cap = 256;   // direct path: LDS is plentiful, keep the load <= 1/4 (short probes; measured faster)
+    while (cap < lcap && cap < 4 * db) cap <<= 1;
     agg_ranges_dense<VT, OP>(pkey, pval, prow, r0, r1, F, ltable_at(lds_raw, cap, F), 1, g, meta, o);
     return;
   }
