@@ -564,6 +564,7 @@ __device__ __forceinline__ void staged_scatter(const u64* __restrict__ skey, con
   __shared__ unsigned tot_sh;
   const unsigned pmask = (unsigned)P - 1;
   const int rowsrc = srow != nullptr;
+  const bool rows = drow != nullptr;      // carry row ids (first-row / inverse outputs wanted)
   // the next tile's keys / first value / row ids are loaded while this tile goes through its LDS phases
   u64 k[R], nk[R];
   VT v0[R], nv0[R];
@@ -576,7 +577,7 @@ __device__ __forceinline__ void staged_scatter(const u64* __restrict__ skey, con
       const bool in = p < tnn;
       kk[j] = in ? skey[tb + p] : 0;
       vv[j] = (in && F > 0) ? sval[(tb + p) * F] : VT(0);
-      rr[j] = in ? (rowsrc ? srow[tb + p] : (int)(tb + p)) : 0;
+      rr[j] = (in && rows) ? (rowsrc ? srow[tb + p] : (int)(tb + p)) : 0;
     }
   };
   if (r0 < r1) load_tile(r0, k, v0, rw);
@@ -616,7 +617,7 @@ __device__ __forceinline__ void staged_scatter(const u64* __restrict__ skey, con
         const unsigned q = off[bk[j]] + rk[j];
         const i64 i = t0 + p;
         st_key[q] = k[j];
-        st_row[q] = rw[j];
+        if (rows) st_row[q] = rw[j];
         st_b[q] = (unsigned short)bk[j];
         for (int f = 0; f < F; ++f) st_val[(size_t)q * F + f] = f == 0 ? v0[j] : sval[i * F + f];
       }
@@ -626,7 +627,7 @@ __device__ __forceinline__ void staged_scatter(const u64* __restrict__ skey, con
       const int b = st_b[q];
       const i64 dst = run[b] + (q - (int)off[b]);
       dkey[dst] = st_key[q];
-      drow[dst] = st_row[q];
+      if (rows) drow[dst] = st_row[q];
       for (int f = 0; f < F; ++f) dval[dst * F + f] = st_val[(size_t)q * F + f];
     }
     __syncthreads();
@@ -686,7 +687,7 @@ __device__ __forceinline__ void agg_ranges_dense(const u64* __restrict__ pkey, c
       const i64 r = b0 + (i64)j * gs + lt;
       const bool in = r < e;
       kk[j] = in ? pkey[r] : kEmpty;
-      rr[j] = in ? prow[r] : 0;
+      rr[j] = (in && prow) ? prow[r] : 0;
       vv[j] = (in && F > 0) ? pval[r * F] : VT(0);
     }
   };
@@ -1082,7 +1083,7 @@ inline int stage_rows(int F, int budget = 48 * 1024, int nthr = 512) {
 inline int agg_groups(long long n) { return (int)std::min<long long>(256, std::max<long long>(1, (n + 16383) / 16384)); }
 
 template <typename VT, int OP>
-int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv, void* meta_v, void* glow_v,
+int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv, int want_first, void* meta_v, void* glow_v,
                  i64 gcap_low, void* gpart_v, i64 gcap_part, void* out_v, void* work_v, int pbits, int lcap_low,
                  int lcap_part, int low_thr, hipStream_t st) {
   AggMeta* meta = reinterpret_cast<AggMeta*>(meta_v);
@@ -1133,6 +1134,7 @@ int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv,
   u64* qkey = reinterpret_cast<u64*>(prow + ((n + 1) & ~(i64)1));
   VT* qval = reinterpret_cast<VT*>(qkey + n);
   int* qrow = reinterpret_cast<int*>(qval + n * F);
+  if (!want_inv && !want_first) prow = qrow = nullptr;   // no row ids through the partitions
   const int T = stage_rows(F, 96 * 1024, 1024);   // level-1 scatter: one 1024-thread workgroup per CU
   const size_t stage_bytes = (size_t)T * (14 + 8 * F);
   const int T2 = std::min(2048, stage_rows(F, 96 * 1024, 1024));   // bucket kernel's sub-partition tiles (2 rows / thread)
@@ -1167,7 +1169,7 @@ long long nsdb_agg_work_bytes(long long n, int F, int pbits, int want_inv) {
 
 // vt: 0 double, 1 int64; op: 0 sum, 1 min, 2 max
 int nsdb_hash_aggregate(const void* keys, const void* vals, long long n, int F, int vt, int op, int want_inv,
-                        void* meta, void* glow, long long gcap_low, void* gpart, long long gcap_part, void* out,
+                        int want_first, void* meta, void* glow, long long gcap_low, void* gpart, long long gcap_part, void* out,
                         void* work, int pbits, int lcap_low, int lcap_part, int low_thr, hipStream_t st) {
   if (n <= 0) return 0;
   if (n >= (1LL << 31)) return (int)hipErrorInvalidValue;
@@ -1176,7 +1178,7 @@ int nsdb_hash_aggregate(const void* keys, const void* vals, long long n, int F, 
   if (!pow2(gcap_low) || !pow2(gcap_part) || !pow2(lcap_low) || !pow2(lcap_part)) return (int)hipErrorInvalidValue;
   if ((size_t)lcap_low * (20 + 8 * F) > 65536 || (size_t)lcap_part * (20 + 8 * F) > 131072) return (int)hipErrorInvalidValue;
   if ((size_t)stage_rows(F, 96 * 1024, 1024) * (14 + 8 * F) > 131072) return (int)hipErrorInvalidValue;
-#define NSDB_AGG(VT, OP) agg_launch_t<VT, OP>(keys, vals, n, F, want_inv, meta, glow, gcap_low, gpart, gcap_part, out, work, pbits, lcap_low, lcap_part, low_thr, st)
+#define NSDB_AGG(VT, OP) agg_launch_t<VT, OP>(keys, vals, n, F, want_inv, want_first, meta, glow, gcap_low, gpart, gcap_part, out, work, pbits, lcap_low, lcap_part, low_thr, st)
   if (vt == 0) {
     if (op == 0) return NSDB_AGG(double, OP_SUM);
     if (op == 1) return NSDB_AGG(double, OP_MIN);

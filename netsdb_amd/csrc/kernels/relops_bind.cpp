@@ -16,7 +16,7 @@ template <typename T> ll* LL(T* p) { return reinterpret_cast<ll*>(p); }
 extern "C" {
 long long nsdb_agg_work_bytes(long long n, int F, int pbits, int want_inv);
 int nsdb_hash_aggregate(const void* keys, const void* vals, long long n, int F, int vt, int op, int want_inv,
-                        void* meta, void* glow, long long gcap_low, void* gpart, long long gcap_part, void* out,
+                        int want_first, void* meta, void* glow, long long gcap_low, void* gpart, long long gcap_part, void* out,
                         void* work, int pbits, int lcap_low, int lcap_part, int low_thr, hipStream_t st);
 int nsdb_join_insert(const void* keys, long long n, void* tab, long long cap, int* row_slot, unsigned* row_rank,
                      hipStream_t st);
@@ -56,11 +56,12 @@ constexpr int kMetaWords = 16;
 
 // Group n int64 keys and reduce F value columns per group on the device.
 //   vals: [n, F] float64 or int64 (or None / F == 0: counts only); op: "sum" | "min" | "max".
-// Returns (reps [g] i64, aggs [g, F] (vals dtype), counts [g] i64, first [g] i64 (smallest row of each group),
+// Returns (reps [g] i64, aggs [g, F] (vals dtype), counts [g] i64, first [g] i64 (smallest row of each group; only
+// meaningful with want_first, which otherwise lets the partition passes skip row ids),
 // inv [n] i64 (or empty), status): status = [g, path (0 LOW, 1 PART), ok (0: the PART table overflowed; outputs
 // invalid, fall back), distinct keys in the 4096-row sample].
 std::vector<torch::Tensor> hash_aggregate(torch::Tensor keys, c10::optional<torch::Tensor> vals, const std::string& op,
-                                          bool want_inv, int64_t low_threshold) {
+                                          bool want_inv, int64_t low_threshold, bool want_first) {
   TORCH_CHECK(keys.is_cuda(), "keys must be a GPU tensor");
   TORCH_CHECK(keys.scalar_type() == torch::kInt64 && keys.dim() == 1, "keys must be 1-D int64");
   keys = keys.contiguous();
@@ -108,7 +109,7 @@ std::vector<torch::Tensor> hash_aggregate(torch::Tensor keys, c10::optional<torc
   auto out = torch::empty({n * (4 + F) + (want_inv ? n : 0)}, i64);
   const int64_t wbytes = nsdb_agg_work_bytes(n, F, pbits, want_inv ? 1 : 0);
   auto work = torch::empty({(wbytes + 7) / 8}, i64);
-  rc_ok(nsdb_hash_aggregate(keys.data_ptr(), F ? v.data_ptr() : nullptr, n, F, vt, opc, want_inv ? 1 : 0,
+  rc_ok(nsdb_hash_aggregate(keys.data_ptr(), F ? v.data_ptr() : nullptr, n, F, vt, opc, want_inv ? 1 : 0, want_first ? 1 : 0,
                             meta.data_ptr(), glow.data_ptr(), gcap_low, gpart.data_ptr(), gcap_part, out.data_ptr(),
                             work.data_ptr(), pbits, (int)lcap_low, (int)lcap_part, (int)thr, stream()),
         "hash_aggregate");
@@ -216,14 +217,14 @@ std::vector<torch::Tensor> partition_perm(torch::Tensor dest, int64_t P) {
 
 std::vector<torch::Tensor> hash_aggregate_impl(torch::Tensor keys, c10::optional<torch::Tensor> vals,
                                                const std::string& op, bool want_inv, int64_t low_threshold) {
-  return hash_aggregate(keys, vals, op, want_inv, low_threshold);
+  return hash_aggregate(keys, vals, op, want_inv, low_threshold, true);
 }
 
 void register_relops(pybind11::module& m) {
   m.def("hash_aggregate", &hash_aggregate,
         "device hash group-by + aggregate: (reps, aggs, counts, first, inv, status[g, path, ok, sample_distinct])",
         pybind11::arg("keys"), pybind11::arg("vals") = pybind11::none(), pybind11::arg("op") = "sum",
-        pybind11::arg("want_inv") = false, pybind11::arg("low_threshold") = 0);
+        pybind11::arg("want_inv") = false, pybind11::arg("low_threshold") = 0, pybind11::arg("want_first") = true);
   m.def("join_build", &join_build, "device hash-join build: (table, perm)");
   m.def("join_probe", &join_probe, "device hash-join probe: (build_idx, probe_idx)");
   m.def("partition_perm", &partition_perm, "stable device partition permutation: (perm, counts)");

@@ -207,8 +207,8 @@ def _rows_match_rep(cols, words, ref: torch.Tensor) -> bool:
     return bool(ok.all())
 
 
-def _hash_aggregate(key64: torch.Tensor, vals, op: str, want_inv: bool):
-    r = _ext.hip().hash_aggregate(key64.contiguous(), vals, op, want_inv, 0)
+def _hash_aggregate(key64: torch.Tensor, vals, op: str, want_inv: bool, want_first: bool = True):
+    r = _ext.hip().hash_aggregate(key64.contiguous(), vals, op, want_inv, 0, want_first)
     status = r[5].tolist()
     if status[2] != 1:
         return None
@@ -273,7 +273,9 @@ def group_reduce(keys, values, op: str = "sum"):
     words = [c.hash64() if isinstance(c, StringColumn) else _norm_col(c) for c in cols]
     packed = None if any(isinstance(c, StringColumn) for c in cols) else _pack_exact(words)
     key = packed[0] if packed is not None else _combine_words(words)
-    r = _hash_aggregate(key, vals, kop, packed is None)
+    # packed keys are the values themselves: no representative row (first / inverse) is needed, so the
+    # partition passes carry no row ids
+    r = _hash_aggregate(key, vals, kop, packed is None, packed is None)
     if r is None:
         return None
     reps_k, aggs, cnt, first, inv = r

@@ -67,11 +67,19 @@ def main():
         def dev_agg_inv():
             return h.hash_aggregate(keys, vals, "sum", True, 0)
 
+        def dev_agg_nofirst():   # the engine's numeric-key group-by: no representative rows needed
+            return h.hash_aggregate(keys, vals, "sum", False, 0, False)
+
+        r2 = dev_agg_nofirst()
+        o2 = torch.argsort(r2[0])
+        assert torch.equal(r2[0][o2], ref_u) and torch.allclose(r2[1][o2, 0], ref, rtol=1e-9), "no-first path differs"
+
         def torch_agg():
             u, inv = torch.unique(keys, return_inverse=True)
             return torch.zeros(u.numel(), device=dev, dtype=torch.float64).index_add_(0, inv, vals)
 
-        t = run({"hash_aggregate": dev_agg, "hash_aggregate_with_inverse": dev_agg_inv,
+        t = run({"hash_aggregate": dev_agg, "hash_aggregate_no_first": dev_agg_nofirst,
+                 "hash_aggregate_with_inverse": dev_agg_inv,
                  "torch_unique_index_add": torch_agg}, a.rounds)
         t["groups"] = int(ref_u.numel())
         t["path"] = "LOW" if int(r[5][1]) == 0 else "PART"

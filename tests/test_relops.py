@@ -261,3 +261,19 @@ def test_pack_exact_roundtrip():
     order = torch.argsort(packed)
     assert [(int(a[i]), int(b[i])) for i in order] == sorted(zip(a.tolist(), b.tolist()))
     assert K._pack_exact([torch.tensor([-2**62, 2**62]), torch.tensor([0, 1])]) is None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("distinct", [8, 5000, 400_000])
+def test_hash_aggregate_without_first_rows(distinct):
+    """want_first=False (packed numeric keys): the partition passes carry no row ids; groups, sums and counts
+    are unchanged."""
+    g = torch.Generator(device=DEV).manual_seed(distinct)
+    n = 600_000
+    keys = torch.randint(0, distinct, (n,), device=DEV, generator=g) * 7 + 1
+    vals = torch.rand(n, 2, device=DEV, dtype=torch.float64, generator=g)
+    a = _ext.hip().hash_aggregate(keys, vals, "sum", False, 0, True)
+    b = _ext.hip().hash_aggregate(keys, vals, "sum", False, 0, False)
+    oa, ob = torch.argsort(a[0]), torch.argsort(b[0])
+    assert torch.equal(a[0][oa], b[0][ob]) and torch.equal(a[2][oa], b[2][ob])
+    torch.testing.assert_close(a[1][oa], b[1][ob], rtol=1e-12, atol=1e-9)
