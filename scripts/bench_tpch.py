@@ -23,7 +23,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from netsdb_amd.client import PDBClient  # noqa: E402
 from netsdb_amd.models import tpch, tpch_gen  # noqa: E402
 
-NEEDS = {"q01": ["lineitem"], "q03": ["customer", "orders", "lineitem"], "q04": ["orders", "lineitem"],
+NEEDS = {"q01": ["lineitem"], "q02": ["part", "supplier", "partsupp", "nation", "region"], "q17": ["lineitem", "part"], "q03": ["customer", "orders", "lineitem"], "q04": ["orders", "lineitem"],
          "q06": ["lineitem"], "q12": ["orders", "lineitem"], "q13": ["customer", "orders"],
          "q14": ["lineitem", "part"], "q22": ["customer", "orders"]}
 
@@ -44,7 +44,7 @@ def _close(got, ref):
 
 
 def _ref_sorted(q, ref):
-    if isinstance(ref, float) or q in ("q03", "q13"):
+    if isinstance(ref, float) or q in ("q02", "q03", "q13"):
         return ref
     if q == "q01":
         return sorted(ref, key=lambda x: (x["l_returnflag"], x["l_linestatus"]))
