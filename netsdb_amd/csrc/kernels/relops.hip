@@ -1075,8 +1075,8 @@ __global__ __launch_bounds__(1024) void part_scatter_kernel(const i64* __restric
 // ---------------------------------------------------------------- host launchers
 // rows staged per scatter pass: a multiple of 1024, <= 4096, staging <= budget bytes
 inline int stage_rows(int F, int budget = 48 * 1024, int nthr = 512) {
-  const int t = (int)(budget / (14 + 8 * F)) / nthr * nthr;
-  return std::max(nthr, std::min(4 * nthr, t));
+  const int t = (int)(budget / (14 + 8 * F)) / 256 * 256;   // wide rows (F up to 16): tiles below one row per thread
+  return std::max(256, std::min(4 * nthr, t));
 }
 
 // level-1 histogram / scatter workgroups (one per CU), >= 16 Ki rows each
