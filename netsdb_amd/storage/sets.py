@@ -15,6 +15,7 @@ assembling blocks before every block GEMM.
 from __future__ import annotations
 
 import math
+import itertools
 import threading
 from typing import Dict, Iterator, List, Optional, Tuple
 
@@ -23,8 +24,22 @@ import torch
 from ..objects.record import RecordBatch, merge_adjacent_batches
 from .serde import deserialize_batch, serialize_batch
 
+_BATCH_GEN = itertools.count(1)
+
+
 class Page:
-    __slots__ = ("set", "page_no", "batch", "nbytes", "pins", "location", "dirty", "last_use", "n", "event", "regions")
+    __slots__ = ("set", "page_no", "_batch", "gen", "nbytes", "pins", "location", "dirty", "last_use", "n", "event",
+                 "regions")
+
+    @property
+    def batch(self) -> Optional[RecordBatch]:
+        return self._batch
+
+    @batch.setter
+    def batch(self, b: Optional[RecordBatch]):
+        # every (re)assignment gets a new generation: cached scan plans key on it (object ids can be reused)
+        self._batch = b
+        self.gen = next(_BATCH_GEN)
 
     def __init__(self, uset: "UserSet", page_no: int, batch: RecordBatch, to_pool: bool = False):
         self.set = uset
@@ -364,7 +379,7 @@ class UserSet:
     def _coalesce_runs(self, pages, device) -> List[Tuple[int, int]]:
         """[i, j) runs of consecutive resident pages whose columns are adjacent slices of one buffer (checked once;
         the plan is cached while the pages and their resident batches stay the same objects)."""
-        key = tuple((id(p), id(p.batch), p.n) for p in pages) + (str(device),)
+        key = tuple((id(p), p.gen, p.n) for p in pages) + (str(device),)
         if getattr(self, "_coalesce_key", None) == key:
             return self._coalesce_plan
         runs, i = [], 0

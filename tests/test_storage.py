@@ -382,3 +382,27 @@ def test_scan_coalesces_adjacent_pages_zero_copy(monkeypatch, tmp_path):
     assert torch.equal(merged[0].columns["x"], b.columns["x"]) and torch.equal(merged[0].columns["y"], b.columns["y"])
     assert merged[0].columns["s"].tolist() == b.columns["s"].tolist()
     assert sum(p.n for p in plain) == n + 5
+
+
+def test_scan_coalescing_plan_follows_page_reloads(monkeypatch, tmp_path):
+    """A page whose batch is replaced (spill + reload gives new tensors) invalidates the cached coalescing plan:
+    the scan re-checks instead of viewing past the new, separate storage."""
+    from netsdb_amd.client import PDBClient
+    from netsdb_amd.objects.record import RecordBatch
+    from netsdb_amd.storage.sets import UserSet
+
+    c = PDBClient(root=str(tmp_path), page_size=1 << 14)
+    c.create_database("d")
+    c.create_set("d", "s", None)
+    monkeypatch.setattr(c.storage, "page_pool", None)
+    monkeypatch.setattr(UserSet, "COALESCE_ANY_DEVICE", True)
+    s = c.storage.get_set("d", "s")
+    x = torch.arange(6000, dtype=torch.float32).reshape(3000, 2)
+    s.add_batch(RecordBatch({"x": x}, 3000))
+    assert len(s.pages) > 2
+    assert len(list(s.scan("cpu"))) == 1                       # one merged run, plan cached
+    p = s.pages[1]
+    p.batch = RecordBatch({"x": p.batch.columns["x"].clone()}, p.n)   # "reloaded" into its own storage
+    got = list(s.scan("cpu"))
+    assert len(got) > 1
+    assert torch.equal(torch.cat([b.columns["x"] for b in got]), x)
