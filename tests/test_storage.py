@@ -397,8 +397,8 @@ def test_scan_coalescing_plan_follows_page_reloads(monkeypatch, tmp_path):
     monkeypatch.setattr(c.storage, "page_pool", None)
     monkeypatch.setattr(UserSet, "COALESCE_ANY_DEVICE", True)
     s = c.storage.get_set("d", "s")
-    x = torch.arange(6000, dtype=torch.float32).reshape(3000, 2)
-    s.add_batch(RecordBatch({"x": x}, 3000))
+    x = torch.arange(20000, dtype=torch.float32).reshape(10000, 2)
+    s.add_batch(RecordBatch({"x": x}, 10000))
     assert len(s.pages) > 2
     assert len(list(s.scan("cpu"))) == 1                       # one merged run, plan cached
     p = s.pages[1]
