@@ -7,24 +7,27 @@
 // Hash aggregation of n rows (one int64 key per row; multi-column keys are packed or hashed by the caller,
 // execution/kernels.py) with F value columns (8-byte: double or int64; op sum / min / max; a row count always):
 //
-//  * agg_sample: ONE workgroup counts the distinct keys of 4096 evenly spaced rows into a device word. Every
-//    later kernel reads that word and returns at once when its path is not the one taken, so the choice costs
-//    no host round trip (the only host read of the whole aggregation is the final group count).
+//  * agg_sample: ONE workgroup hashes 4096 evenly spaced rows into an LDS table with counts and writes the Chao1
+//    estimate of the distinct keys into a device word. Every later kernel reads it and returns at once when its
+//    path is not the one taken, so the choice costs no host round trip (the only host read of the whole
+//    aggregation is the final group count).
 //  * LOW path (few groups): agg_low — each workgroup pre-aggregates its rows in an LDS hash table (claim by LDS
-//    CAS, f64 / u64 LDS atomics), rows whose key does not fit go straight to a small global table, and at the
-//    end each workgroup flushes its LDS entries ONCE into the global table (agent-scope atomics). Millions of
-//    rows on a handful of keys therefore cost one global atomic per (workgroup, key), not per row. If the
-//    global table overflows (the sample under-estimated the groups) a device flag routes the work to:
-//  * PART path (many groups): radix partition by the top hash bits (agg_hist: per-workgroup LDS histograms;
-//    agg_scan_rows / agg_scan_tot: bucket-major exclusive scans + a work list of <= CH-row chunks; agg_scatter:
-//    keys, values and row ids packed bucket-contiguous), then agg_part: persistent workgroups dequeue chunks
-//    (one returning atomic on a device word), aggregate a chunk in an LDS table sized so a whole bucket fits,
-//    and write a bucket that is one chunk straight to the dense output (its groups occur nowhere else).
-//    Buckets of several chunks (hot keys) flush through a global table instead.
-//  * agg_emit copies the global-table groups to the dense output; agg_fix_inv turns per-row global-slot
-//    references into dense group ids (only when the caller wants the per-row inverse).
-// Dense group ids come from one device counter bumped by whoever creates a group, so there is no compaction
-// pass over the tables and no nonzero()/sort.
+//    CAS, f64 / u64 LDS atomics; rows loaded four per thread, the next batch in flight while one is inserted),
+//    rows whose key does not fit go straight to a small global table, and at the end each workgroup flushes its
+//    LDS entries ONCE into the global table (agent-scope atomics): one global atomic per (workgroup, key), not per
+//    row. If the global table overflows (the sample under-estimated the groups) a device flag routes the work to:
+//  * PART path (many groups): 256 level-1 buckets by the top hash bits (agg_hist: per-workgroup LDS histograms;
+//    scan_rows / scan_tot: block scans; agg_scatter: tile-staged counting sort in LDS, so each bucket's rows leave
+//    as one coalesced run per tile), then agg_bucket: workgroup b owns bucket b whole. If its share of the
+//    estimate fits the LDS table it aggregates the bucket there and writes the groups straight to the dense
+//    output (their keys occur in no other bucket); otherwise it splits the bucket again by the next hash bits
+//    (its own histogram + staged scatter into a second buffer) and aggregates four sub-buckets at a time in four
+//    quarter tables. Rows whose LDS probe window is full go to a small overflow table (agg_emit copies those).
+//    No global atomic per row anywhere: per-row atomics on global memory execute at the memory side.
+//  * agg_fix_inv turns per-row global-slot references into dense group ids (only when the caller wants the
+//    per-row inverse); want_first = 0 drops the row ids from the partition passes altogether.
+// Dense group ids come from one device counter bumped once per emitted run, so there is no compaction pass over
+// the tables and no nonzero()/sort.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
