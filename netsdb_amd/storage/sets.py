@@ -405,9 +405,12 @@ class UserSet:
     def _scan_coalesced(self, pages, device) -> Iterator[RecordBatch]:
         """Runs of consecutive pages resident on ``device`` whose columns are adjacent slices of one buffer are
         yielded as ONE batch (zero-copy views, up to SCAN_COALESCE_BYTES); any other page is yielded alone."""
-        for i, j in self._coalesce_runs(pages, device):
+        plan = self._coalesce_runs(pages, device)
+        gens = [p.gen for p in pages]          # the layout the plan was checked against
+        for i, j in plan:
             run = pages[i:j]
-            if j - i > 1 and all(p.batch is not None for p in run):
+            # a page spilled / reloaded while earlier runs were consumed no longer matches the plan: page by page
+            if j - i > 1 and all(p.batch is not None and p.gen == g for p, g in zip(run, gens[i:j])):
                 for p in run:
                     p.pins += 1
                 try:

@@ -406,3 +406,28 @@ def test_scan_coalescing_plan_follows_page_reloads(monkeypatch, tmp_path):
     got = list(s.scan("cpu"))
     assert len(got) > 1
     assert torch.equal(torch.cat([b.columns["x"] for b in got]), x)
+
+
+def test_scan_coalescing_survives_reload_during_scan(monkeypatch, tmp_path):
+    """A page replaced while an earlier run of the same scan is being consumed is yielded on its own."""
+    from netsdb_amd.client import PDBClient
+    from netsdb_amd.objects.record import RecordBatch
+    from netsdb_amd.storage.sets import UserSet
+
+    c = PDBClient(root=str(tmp_path), page_size=1 << 14)
+    c.create_database("d")
+    c.create_set("d", "s", None)
+    monkeypatch.setattr(c.storage, "page_pool", None)
+    monkeypatch.setattr(UserSet, "COALESCE_ANY_DEVICE", True)
+    monkeypatch.setattr(UserSet, "SCAN_COALESCE_BYTES", 3 << 14)    # several runs per scan
+    s = c.storage.get_set("d", "s")
+    x = torch.arange(40000, dtype=torch.float32).reshape(20000, 2)
+    s.add_batch(RecordBatch({"x": x}, 20000))
+    list(s.scan("cpu"))                                             # plan cached
+    out = []
+    for k, b in enumerate(s.scan("cpu")):
+        out.append(b.columns["x"].clone())
+        if k == 0:                                                  # "reload" every later page mid-scan
+            for p in s.pages[3:]:
+                p.batch = RecordBatch({"x": p.batch.columns["x"].clone()}, p.n)
+    assert torch.equal(torch.cat(out), x)
