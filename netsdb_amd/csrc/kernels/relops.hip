@@ -274,9 +274,21 @@ __device__ __forceinline__ void row_into_global(GTable g, u64 k, const VT* v, in
 // One workgroup hashes 4096 evenly spaced rows into an LDS table with per-key counts and writes the Chao1
 // estimate of the distinct keys, d + f1^2 / (2 f2) (f1 / f2: keys seen once / twice in the sample; exact d when
 // every row was sampled), clamped to [d, n]. The PART path sizes its sub-partitions from it.
-__global__ __launch_bounds__(1024) void agg_sample_kernel(const u64* __restrict__ keys, i64 n, int low_thr,
+constexpr int kSample = 4096;
+
+// The sampled rows' keys into sbuf[4096]: the random reads spread over 64 workgroups (one CU's outstanding-miss
+// budget made a single-workgroup sample latency-bound).
+__global__ __launch_bounds__(64) void agg_sample_gather_kernel(const u64* __restrict__ keys, i64 n,
+                                                               u64* __restrict__ sbuf) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  const int ns = (int)std::min<i64>(kSample, n);
+  const i64 r = (n <= kSample) ? i : ((i64)i * n) / kSample;   // n < 2^31: no overflow
+  sbuf[i] = i < ns ? keys[r] : kEmpty;
+}
+
+__global__ __launch_bounds__(1024) void agg_sample_kernel(const u64* __restrict__ sbuf, i64 n, int low_thr,
                                                           AggMeta* meta) {
-  constexpr int S = 4096, CAP = 8192;
+  constexpr int S = kSample, CAP = 8192;
   __shared__ u64 tab[CAP];
   __shared__ unsigned tcnt[CAP];
   __shared__ unsigned fsum[3];
@@ -286,14 +298,9 @@ __global__ __launch_bounds__(1024) void agg_sample_kernel(const u64* __restrict_
   }
   if (threadIdx.x < 3) fsum[threadIdx.x] = 0;
   __syncthreads();
-  const int ns = (int)std::min<i64>(S, n);
   u64 kk[S / 1024];
 #pragma unroll
-  for (int j = 0; j < S / 1024; ++j) {   // all four loads in flight before the first insert
-    const int i = threadIdx.x + j * 1024;
-    const i64 r = (n <= S) ? i : ((i64)i * n) / S;   // n < 2^31: no overflow
-    kk[j] = i < ns ? keys[r] : kEmpty;
-  }
+  for (int j = 0; j < S / 1024; ++j) kk[j] = sbuf[threadIdx.x + j * 1024];   // contiguous, gathered before
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int j = 0; j < S / 1024; ++j) {
@@ -1120,7 +1127,9 @@ int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv,
 
   hipLaunchKernelGGL(agg_init_kernel, dim3(512), dim3(256), 0, st, reinterpret_cast<u64*>(glow_v), gcap_low,
                      reinterpret_cast<u64*>(gpart_v), gcap_part, F, acc_identity<VT, OP>(), meta);
-  hipLaunchKernelGGL(agg_sample_kernel, dim3(1), dim3(1024), 0, st, k, n, low_thr, meta);
+  u64* sbuf = reinterpret_cast<u64*>(meta) + sizeof(AggMeta) / 8;   // [4096] after the meta words
+  hipLaunchKernelGGL(agg_sample_gather_kernel, dim3(kSample / 64), dim3(64), 0, st, k, n, sbuf);
+  hipLaunchKernelGGL(agg_sample_kernel, dim3(1), dim3(1024), 0, st, sbuf, n, low_thr, meta);
   const int gl = (int)std::min<i64>(1024, std::max<i64>(1, (n + 2047) / 2048));
   hipLaunchKernelGGL((agg_low_kernel<VT, OP>), dim3(gl), dim3(256), lbytes_low, st, k, v, n, F, lcap_low, glow, meta, o);
   // PART: work buffers [hist P*G u32 | tot P | bstart P+1 | pkey n | pval n*F | prow n (i32) | qkey | qval | qrow]

@@ -52,7 +52,7 @@ int64_t pow2_at_most(int64_t x) {
 }
 
 // Word offsets of the AggMeta fields (relops.hip): est, low, ng_low, ng_part, fail_low, fail_part, ...
-constexpr int kMetaWords = 16;
+constexpr int kMetaWords = 16 + 4096;   // AggMeta + the sampled keys (relops.hip agg_sample_*)
 
 // Group n int64 keys and reduce F value columns per group on the device.
 //   vals: [n, F] float64 or int64 (or None / F == 0: counts only); op: "sum" | "min" | "max".
@@ -113,7 +113,7 @@ std::vector<torch::Tensor> hash_aggregate(torch::Tensor keys, c10::optional<torc
                             meta.data_ptr(), glow.data_ptr(), gcap_low, gpart.data_ptr(), gcap_part, out.data_ptr(),
                             work.data_ptr(), pbits, (int)lcap_low, (int)lcap_part, (int)thr, stream()),
         "hash_aggregate");
-  auto m = meta.cpu();   // the one host read: group count and path flags
+  auto m = meta.narrow(0, 0, 16).cpu();   // the one host read: group count and path flags
   const ll* mp = LL(m.data_ptr<int64_t>());
   const bool low_ok = mp[1] != 0 && mp[4] == 0;
   const int64_t g = (int64_t)(low_ok ? mp[2] : mp[3]);
