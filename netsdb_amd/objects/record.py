@@ -21,6 +21,8 @@ from __future__ import annotations
 
 from typing import Any, Dict, Iterable, List, Optional, Sequence
 
+import os
+
 import torch
 
 from .strings import StringColumn, is_string_list, use_device_strings
@@ -197,6 +199,95 @@ def column_kind(ft) -> str:
     return "object"
 
 
+LAZY_TAKE_MIN_COLS = 4
+LAZY_TAKE_ANY_DEVICE = os.environ.get("NSDB_LAZY_TAKE") == "1"   # tests: the lazy path on CPU batches too
+
+
+class LazyTakeColumns(dict):
+    """The columns of a row selection, gathered from ``src`` on first access and cached. Behaves as the dict of
+    every column (iteration, items(), values(), dict(...) and ** materialise what they touch); columns set or
+    deleted on it shadow the source."""
+
+    __slots__ = ("_src", "_idx", "_gone")
+
+    def __init__(self, src: Dict[str, Any], idx: torch.Tensor):
+        super().__init__()
+        self._src, self._idx, self._gone = src, idx, set()
+
+    def _fetch(self, k):
+        v = column_take(self._src[k], self._idx)
+        dict.__setitem__(self, k, v)
+        return v
+
+    def __getitem__(self, k):
+        if dict.__contains__(self, k):
+            return dict.__getitem__(self, k)
+        if k in self._src and k not in self._gone:
+            return self._fetch(k)
+        raise KeyError(k)
+
+    def __setitem__(self, k, v):
+        self._gone.discard(k)
+        dict.__setitem__(self, k, v)
+
+    def __delitem__(self, k):
+        if k not in self:
+            raise KeyError(k)
+        if dict.__contains__(self, k):
+            dict.__delitem__(self, k)
+        if k in self._src:
+            self._gone.add(k)
+
+    def __contains__(self, k):
+        return dict.__contains__(self, k) or (k in self._src and k not in self._gone)
+
+    def keys(self):
+        ks = [k for k in self._src if k not in self._gone]
+        ks += [k for k in dict.keys(self) if k not in self._src]
+        return ks
+
+    def __iter__(self):
+        return iter(self.keys())
+
+    def __len__(self):
+        return len(self.keys())
+
+    def values(self):
+        return [self[k] for k in self.keys()]
+
+    def items(self):
+        return [(k, self[k]) for k in self.keys()]
+
+    def get(self, k, default=None):
+        return self[k] if k in self else default
+
+    def pop(self, k, *default):
+        if k in self:
+            v = self[k]
+            del self[k]
+            return v
+        if default:
+            return default[0]
+        raise KeyError(k)
+
+    def copy(self):
+        return dict(self.items())
+
+    def update(self, other=(), **kw):
+        for k, v in (other.items() if hasattr(other, "items") else other):
+            self[k] = v
+        for k, v in kw.items():
+            self[k] = v
+
+    def setdefault(self, k, default=None):
+        if k not in self:
+            self[k] = default
+        return self[k]
+
+    def __repr__(self):
+        return repr(dict(self.items()))
+
+
 class RecordBatch:
     """Columnar batch of records of one type (or an anonymous tuple set when type is None)."""
 
@@ -260,11 +351,15 @@ class RecordBatch:
         return out
 
     def take(self, idx) -> "RecordBatch":
-        """Gather rows (idx: int64 tensor or list)."""
+        """Gather rows (idx: int64 tensor or list). A wide batch on the GPU gathers lazily: each column on its first
+        access (a filter feeding a UDF that reads a few fields of a wide record gathers only those)."""
+        n = len(idx) if not isinstance(idx, torch.Tensor) else int(idx.numel())
+        if isinstance(idx, torch.Tensor) and len(self.columns) > LAZY_TAKE_MIN_COLS and \
+                (idx.is_cuda or LAZY_TAKE_ANY_DEVICE):
+            return RecordBatch(LazyTakeColumns(self.columns, idx), n, self.type)
         cols = {}
         for k, c in self.columns.items():
             cols[k] = column_take(c, idx)
-        n = len(idx) if not isinstance(idx, torch.Tensor) else int(idx.numel())
         return RecordBatch(cols, n, self.type)
 
     def slice(self, s: int, e: int) -> "RecordBatch":

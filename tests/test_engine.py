@@ -240,3 +240,28 @@ def test_topk_on_device_gpu(tmp_path):
     assert all(n <= 64 and "engine.py" not in site for _, n, site in calls), calls
     got = sorted(o.salary for o in c.get_set_iterator("db", "top"))
     assert got == sorted(e.salary for e in _emps(300))[-5:]
+
+
+def test_lazy_take_columns_behave_as_dict(monkeypatch):
+    """Row selections of wide batches gather each column on first access (objects/record.py LazyTakeColumns);
+    every dict operation the engine and UDFs use sees all columns, with the gathered values."""
+    from netsdb_amd.objects import record as R
+
+    monkeypatch.setattr(R, "LAZY_TAKE_ANY_DEVICE", True)
+    cols = {f"c{i}": torch.arange(10) * (i + 1) for i in range(6)}
+    b = R.RecordBatch(dict(cols), 10)
+    idx = torch.tensor([1, 4, 7])
+    t = b.take(idx)
+    assert isinstance(t.columns, R.LazyTakeColumns) and t.n == 3
+    assert dict.__len__(t.columns) == 0                       # nothing gathered yet
+    assert t.columns["c2"].tolist() == [3, 12, 21]
+    assert dict.__len__(t.columns) == 1
+    assert list(t.columns) == list(cols) and len(t.columns) == 6 and "c5" in t.columns
+    t.columns["new"] = torch.zeros(3)
+    del t.columns["c0"]
+    assert "c0" not in t.columns and list(t.columns)[-1] == "new"
+    d = dict(t.columns)
+    assert set(d) == {"c1", "c2", "c3", "c4", "c5", "new"} and d["c4"].tolist() == [10, 25, 40]
+    assert {**t.columns}.keys() == d.keys()
+    assert [k for k, _ in t.columns.items()] == list(d)
+    assert R.RecordBatch.concat([t, t]).columns["c1"].tolist() == [2, 8, 14] * 2
