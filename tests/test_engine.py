@@ -261,7 +261,7 @@ def test_lazy_take_columns_behave_as_dict(monkeypatch):
     del t.columns["c0"]
     assert "c0" not in t.columns and list(t.columns)[-1] == "new"
     d = dict(t.columns)
-    assert set(d) == {"c1", "c2", "c3", "c4", "c5", "new"} and d["c4"].tolist() == [10, 25, 40]
+    assert set(d) == {"c1", "c2", "c3", "c4", "c5", "new"} and d["c4"].tolist() == [5, 20, 35]
     assert {**t.columns}.keys() == d.keys()
     assert [k for k, _ in t.columns.items()] == list(d)
     assert R.RecordBatch.concat([t, t]).columns["c1"].tolist() == [2, 8, 14] * 2
