@@ -371,19 +371,24 @@ class RecordBatch:
         return RecordBatch(cols, self.n, self.type)
 
     def nbytes(self) -> int:
-        total = 0
-        for c in self.columns.values():
-            if isinstance(c, torch.Tensor):
-                total += c.numel() * c.element_size()
-            elif isinstance(c, RecordBatch):
-                total += c.nbytes()
-            elif isinstance(c, StringColumn) or hasattr(c, "offsets"):
-                total += c.nbytes
-            elif isinstance(c, tuple):
-                total += sum(x.numel() * x.element_size() if isinstance(x, torch.Tensor) else 16 * len(x) for x in c)
-            else:
-                total += 16 * len(c) + sum(_obj_size(x) for x in c[:64]) * max(1, len(c) // max(1, min(64, len(c))))
-        return total
+        cols = self.columns
+        if isinstance(cols, LazyTakeColumns):
+            # columns not gathered yet: their source's bytes scaled to the selected rows (no gather to measure)
+            total = 0
+            for k in cols.keys():
+                if dict.__contains__(cols, k):
+                    total += _col_nbytes(dict.__getitem__(cols, k))
+                else:
+                    src = cols._src[k]
+                    total += _col_nbytes(src) * self.n // max(1, column_len(src))
+            return total
+        return sum(_col_nbytes(c) for c in cols.values())
+
+    def materialize(self) -> "RecordBatch":
+        """This batch with every lazily gathered column gathered (drops the reference to the source columns)."""
+        if isinstance(self.columns, LazyTakeColumns):
+            return RecordBatch(dict(self.columns.items()), self.n, self.type)
+        return self
 
     @staticmethod
     def concat(batches: Sequence["RecordBatch"]) -> "RecordBatch":
@@ -401,6 +406,18 @@ class RecordBatch:
     def __repr__(self):
         t = self.type.type_name() if self.type else "tuple"
         return f"RecordBatch<{t}>(n={self.n}, cols={list(self.columns)})"
+
+
+def _col_nbytes(c) -> int:
+    if isinstance(c, torch.Tensor):
+        return c.numel() * c.element_size()
+    if isinstance(c, RecordBatch):
+        return c.nbytes()
+    if isinstance(c, StringColumn) or hasattr(c, "offsets"):
+        return c.nbytes
+    if isinstance(c, tuple):
+        return sum(x.numel() * x.element_size() if isinstance(x, torch.Tensor) else 16 * len(x) for x in c)
+    return 16 * len(c) + sum(_obj_size(x) for x in c[:64]) * max(1, len(c) // max(1, min(64, len(c))))
 
 
 def _col_to(c, device):

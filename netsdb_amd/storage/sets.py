@@ -316,6 +316,7 @@ class UserSet:
             self._placed = True
         if batch.n == 0:
             return
+        batch = batch.materialize()          # a stored page never holds a lazy selection's source columns
         pool = getattr(self.manager, "page_pool", None)
         to_pool = (pool is not None and pool.is_cuda and self.device is not None and batch.device.type == "cpu"
                    and self.manager.on_home(self.device))

@@ -265,3 +265,21 @@ def test_lazy_take_columns_behave_as_dict(monkeypatch):
     assert {**t.columns}.keys() == d.keys()
     assert [k for k, _ in t.columns.items()] == list(d)
     assert R.RecordBatch.concat([t, t]).columns["c1"].tolist() == [2, 8, 14] * 2
+
+
+def test_lazy_take_nbytes_and_storage_do_not_gather(monkeypatch, tmp_path):
+    from netsdb_amd.client import PDBClient
+    from netsdb_amd.objects import record as R
+
+    monkeypatch.setattr(R, "LAZY_TAKE_ANY_DEVICE", True)
+    b = R.RecordBatch({f"c{i}": torch.arange(100, dtype=torch.float64) for i in range(6)}, 100)
+    t = b.take(torch.arange(0, 100, 4))
+    assert t.nbytes() == 6 * 25 * 8 and dict.__len__(t.columns) == 0     # estimated, nothing gathered
+    m = t.materialize()
+    assert type(m.columns) is dict and m.columns["c3"].tolist() == list(range(0, 100, 4))
+    c = PDBClient(root=str(tmp_path))
+    c.create_database("d")
+    c.create_set("d", "s", None)
+    s = c.storage.get_set("d", "s")
+    s.add_batch(t)
+    assert all(type(p.batch.columns) is dict for p in s.pages)
