@@ -513,17 +513,44 @@ __global__ __launch_bounds__(1024) void agg_hist_kernel(const u64* __restrict__ 
   for (int i = threadIdx.x; i < P; i += blockDim.x) h[i] = 0;
   __syncthreads();
   const i64 r0 = (i64)blockIdx.x * rpw, r1 = std::min<i64>(n, r0 + rpw);
-  constexpr int U = 8;
-  for (i64 b0 = r0; b0 < r1; b0 += (i64)U * 1024) {
-    u64 k[U];
+  // 16-byte loads (two keys per lane), the next batch in flight while this one is counted
+  constexpr int U = 4;
+  const i64 step = (i64)U * 2 * 1024;
+  const i64 e2 = r0 + ((r1 - r0) & ~(i64)1);   // even part: pairs
+  u64 k[U][2], nk[U][2];
+  auto load = [&](i64 b0, u64 (&kk)[U][2]) {
 #pragma unroll
     for (int j = 0; j < U; ++j) {
-      const i64 i = b0 + j * 1024 + threadIdx.x;
-      k[j] = i < r1 ? keys[i] : 0;
+      const i64 i = b0 + (i64)(j * 1024 + threadIdx.x) * 2;
+      if (i < e2) {
+        const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(keys + i);
+        kk[j][0] = v.x;
+        kk[j][1] = v.y;
+      }
     }
+  };
+  const bool aligned = ((reinterpret_cast<uintptr_t>(keys + r0)) & 15) == 0;
+  if (aligned) {
+    if (r0 < e2) load(r0, k);
+    for (i64 b0 = r0; b0 < e2; b0 += step) {
+      if (b0 + step < e2) load(b0 + step, nk);
 #pragma unroll
-    for (int j = 0; j < U; ++j)
-      if (b0 + j * 1024 + threadIdx.x < r1) atomicAdd(h + bucket_of(k[j], pbits), 1u);
+      for (int j = 0; j < U; ++j) {
+        const i64 i = b0 + (i64)(j * 1024 + threadIdx.x) * 2;
+        if (i < e2) {
+          atomicAdd(h + bucket_of(k[j][0], pbits), 1u);
+          atomicAdd(h + bucket_of(k[j][1], pbits), 1u);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        k[j][0] = nk[j][0];
+        k[j][1] = nk[j][1];
+      }
+    }
+    if (threadIdx.x == 0 && e2 < r1) atomicAdd(h + bucket_of(keys[e2], pbits), 1u);   // odd tail row
+  } else {
+    for (i64 i = r0 + threadIdx.x; i < r1; i += blockDim.x) atomicAdd(h + bucket_of(keys[i], pbits), 1u);
   }
   __syncthreads();
   for (int b = threadIdx.x; b < P; b += blockDim.x) hist[(size_t)b * gridDim.x + blockIdx.x] = h[b];
@@ -1135,7 +1162,7 @@ int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv,
   // PART: work buffers [hist P*G u32 | tot P | bstart P+1 | pkey n | pval n*F | prow n (i32) | qkey | qval | qrow]
   const int P = 1 << pbits;
   const int G = agg_groups(n);
-  const i64 rpw = (n + G - 1) / G;
+  const i64 rpw = (((n + G - 1) / G) + 1) & ~(i64)1;   // even: every workgroup's range starts 16-byte aligned
   char* w = reinterpret_cast<char*>(work_v);
   unsigned* hist = reinterpret_cast<unsigned*>(w);
   i64* tot = reinterpret_cast<i64*>(w + (((size_t)P * G * 4 + 15) & ~(size_t)15));
