@@ -906,42 +906,58 @@ struct JSlot {
   unsigned pay;
 };
 
+// The row that claims a slot (CAS) is its key's rank 0 and stores itself as the payload; each further row of
+// the key takes the next rank with one atomic add on the slot's count of EXTRA rows (a unique-key build does one
+// atomic per row). join_build then turns the counts into totals (+1 per claimed slot) on the device.
 __global__ __launch_bounds__(256) void join_insert_kernel(const u64* __restrict__ keys, i64 n, JSlot* tab, u64 mask,
                                                           int* __restrict__ row_slot, unsigned* __restrict__ row_rank) {
   for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) {
     const u64 k = keys[i];
     u64 s;
+    bool claimed = false;
     if (k == kEmpty) {
-      s = mask + 1;
+      s = mask + 1;   // the kEmpty key's own slot: every row counts as an extra, ranks from 1 (fixed below)
     } else {
       s = mix64(k) & mask;
       for (;;) {   // the table has >= 2 slots per build row: the key or an empty slot is always met
         u64 cur = __hip_atomic_load(&tab[s].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (cur == kEmpty) {
           if (__hip_atomic_compare_exchange_strong(&tab[s].key, &cur, k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT))
+                                                   __HIP_MEMORY_SCOPE_AGENT)) {
+            claimed = true;
             break;
+          }
         }
         if (cur == k) break;
         s = (s + 1) & mask;
       }
     }
     row_slot[i] = (int)s;
-    row_rank[i] = __hip_atomic_fetch_add(&tab[s].cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (claimed) {
+      tab[s].pay = (unsigned)i;
+      row_rank[i] = 0;
+    } else {
+      const unsigned r = __hip_atomic_fetch_add(&tab[s].cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) +
+                         (k == kEmpty ? 0u : 1u);
+      if (r == 0) tab[s].pay = (unsigned)i;   // the kEmpty slot's first row
+      row_rank[i] = r;
+    }
   }
 }
 
-// perm[toff[slot] + rank] = row (build rows grouped by key); the rank-0 row writes the slot's payload
+// Keys with more than one build row: perm[toff[slot] + rank] = row (CSR over the slots) and the slot's payload
+// becomes its run start. Unique keys (the primary-key case) only read their slot's count.
 __global__ __launch_bounds__(256) void join_perm_kernel(const int* __restrict__ row_slot,
                                                         const unsigned* __restrict__ row_rank, i64 n,
                                                         const i64* __restrict__ toff, JSlot* tab,
                                                         i64* __restrict__ perm) {
   for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) {
     const int s = row_slot[i];
+    if (tab[s].cnt <= 1) continue;   // unique key: its payload is already the row
     const unsigned r = row_rank[i];
     const i64 o = toff[s];
     perm[o + r] = i;
-    if (r == 0) tab[s].pay = tab[s].cnt == 1 ? (unsigned)i : (unsigned)o;
+    if (r == 0) tab[s].pay = (unsigned)o;
   }
 }
 

@@ -152,6 +152,10 @@ std::vector<torch::Tensor> join_build(torch::Tensor keys) {
                          reinterpret_cast<unsigned*>(row_rank.data_ptr<int>()), stream()),
         "join_insert");
   auto tcnt = tab.view(torch::kInt32).select(1, 2);   // the cnt word of every slot (strided view)
+  // insert counted the EXTRA rows of each key: + 1 per claimed slot gives the totals (the kEmpty slot, cap,
+  // counted all its rows)
+  auto claimed = tab.select(1, 0).narrow(0, 0, cap).ne(std::numeric_limits<int64_t>::min());
+  tcnt.narrow(0, 0, cap).add_(claimed.to(torch::kInt32));
   auto toff = torch::cumsum(tcnt, 0, torch::kInt64).sub_(tcnt);
   auto perm = torch::empty({n}, i64);
   rc_ok(nsdb_join_perm(row_slot.data_ptr<int>(), reinterpret_cast<const unsigned*>(row_rank.data_ptr<int>()), n,
