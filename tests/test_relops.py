@@ -177,6 +177,19 @@ def test_join_table_device_vs_host():
 
 
 @pytest.mark.gpu
+def test_join_unique_build_keys_and_single_sentinel():
+    """Primary-key builds (every key once, one row with the empty-slot marker value): the claiming row is its
+    own payload, no CSR run; every probe row finds exactly its build row."""
+    g = torch.Generator(device=DEV).manual_seed(4)
+    build = torch.randperm(300_000, device=DEV, generator=g) * 3 + 1
+    build[123] = torch.iinfo(torch.int64).min
+    probe = build[torch.randint(0, 300_000, (1_000_000,), device=DEV, generator=g)]
+    bi, pi = K.JoinTable(build).probe(probe)
+    assert pi.numel() == probe.numel() and torch.equal(pi, torch.arange(probe.numel(), device=DEV))
+    assert torch.equal(build[bi], probe)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("P", [1, 2, 8, 255, 1024])
 def test_partition_order_stable(P):
     g = torch.Generator(device=DEV).manual_seed(P)
