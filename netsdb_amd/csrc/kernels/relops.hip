@@ -137,7 +137,7 @@ struct AggOut {
   i64* reps;        // [n] dense group keys
   u64* aggs;        // [n * F]
   i64* cnt;         // [n]
-  i64* slot_of_gid; // [n] global slot of a group, or -1 when the group was written directly
+  i64* slot_of_gid; // [n] (unused region of the output buffer: kept so the bindings' offsets stay put)
   i64* first;       // [n] smallest row index of each group (its representative row)
   i64* inv;         // [n] or null
 };
@@ -158,7 +158,6 @@ __device__ __forceinline__ i64 gtable_slot(GTable t, u64 k, i64* ngroups, i64* s
       const i64 gid = __hip_atomic_fetch_add(ngroups, (i64)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       t.gid_of_slot[s] = gid;
       o.reps[gid] = (i64)k;
-      o.slot_of_gid[gid] = (i64)s;
     }
     return (i64)s;
   }
@@ -175,7 +174,6 @@ __device__ __forceinline__ i64 gtable_slot(GTable t, u64 k, i64* ngroups, i64* s
         if ((u64)used > (t.mask >> 1)) __hip_atomic_store(fail, (i64)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         t.gid_of_slot[s] = gid;
         o.reps[gid] = (i64)k;
-        o.slot_of_gid[gid] = (i64)s;
         return (i64)s;
       }
       // cur now holds the key another row claimed this slot with
@@ -773,7 +771,6 @@ __device__ __forceinline__ void agg_ranges_dense(const u64* __restrict__ pkey, c
     o.reps[gid] = (i64)k;
     o.cnt[gid] = (i64)t.cnt[x];
     o.first[gid] = (i64)t.rmin[x];
-    o.slot_of_gid[gid] = -1;
     for (int f = 0; f < F; ++f) o.aggs[gid * F + f] = acc_out<VT, OP>(t.acc[x * F + f]);
   }
   if (o.inv != nullptr) {
@@ -870,16 +867,19 @@ __global__ __launch_bounds__(1024) void agg_bucket_kernel(const u64* __restrict_
   }
 }
 
-// global-table groups -> dense output (grid-stride over the groups of the path that was taken)
+// global-table groups -> dense output: a sweep over the slots of the taken path's table (at most 2^17 + 1;
+// the groups written straight from LDS are not visited at all)
 template <typename VT, int OP>
 __global__ __launch_bounds__(256) void agg_emit_kernel(GTable glow, GTable gpart, int F, const AggMeta* meta,
                                                        AggOut o) {
   const bool low = !take_part(meta);
   const GTable g = low ? glow : gpart;
-  const i64 ng = low ? meta->ng_low : meta->ng_part;
-  for (i64 gid = (i64)blockIdx.x * blockDim.x + threadIdx.x; gid < ng; gid += (i64)gridDim.x * blockDim.x) {
-    const i64 s = o.slot_of_gid[gid];
-    if (s < 0) continue;
+  const bool sentinel = (low ? meta->sentinel_low : meta->sentinel_part) != 0;
+  const i64 nslots = (i64)g.mask + 2;   // cap slots + the kEmpty key's slot
+  for (i64 s = (i64)blockIdx.x * blockDim.x + threadIdx.x; s < nslots; s += (i64)gridDim.x * blockDim.x) {
+    const bool used = s == nslots - 1 ? sentinel : g.key[s] != kEmpty;
+    if (!used) continue;
+    const i64 gid = g.gid_of_slot[s];
     o.cnt[gid] = (i64)g.cnt[s];
     o.first[gid] = (i64)g.rmin[s];
     for (int f = 0; f < F; ++f) o.aggs[gid * F + f] = acc_out<VT, OP>(g.acc[s * F + f]);
@@ -1201,7 +1201,8 @@ int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv,
                      bstart, pkey, pval, prow, meta);
   hipLaunchKernelGGL((agg_bucket_kernel<VT, OP>), dim3(P), dim3(1024), lds_bucket, st, pkey, pval, prow, F, lcap_part,
                      pbits, T2, n, bstart, qkey, qval, qrow, gpart, meta, o);
-  hipLaunchKernelGGL((agg_emit_kernel<VT, OP>), dim3(512), dim3(256), 0, st, glow, gpart, F, meta, o);
+  hipLaunchKernelGGL((agg_emit_kernel<VT, OP>), dim3((unsigned)((std::max(gcap_low, gcap_part) + 2 + 255) / 256)),
+                     dim3(256), 0, st, glow, gpart, F, meta, o);
   if (want_inv)
     hipLaunchKernelGGL(agg_fix_inv_kernel, dim3((unsigned)std::min<i64>(2048, (n + 255) / 256)), dim3(256), 0, st,
                        o.inv, n, glow.gid_of_slot, gpart.gid_of_slot, meta);
