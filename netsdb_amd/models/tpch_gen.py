@@ -38,6 +38,12 @@ class GenStrings:
             return self.vocab[int(self.codes[i])]
         return bytes(self.fixed[i]).decode()
 
+    def rows(self, sl) -> "GenStrings":
+        """A row subset (slice or index array), e.g. one rank's share of a generated table."""
+        if self.codes is not None:
+            return GenStrings(self.vocab, self.codes[sl])
+        return GenStrings(fixed=self.fixed[sl])
+
     def tolist(self) -> List[str]:
         if self.codes is not None:
             v = self.vocab
