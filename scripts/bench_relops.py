@@ -74,15 +74,18 @@ def main():
         o2 = torch.argsort(r2[0])
         assert torch.equal(r2[0][o2], ref_u) and torch.allclose(r2[1][o2, 0], ref, rtol=1e-9), "no-first path differs"
 
+        def dev_agg_part():   # MID path disabled (the LOW / PART choice alone)
+            return h.hash_aggregate(keys, vals, "sum", False, 0, True, -1)
+
         def torch_agg():
             u, inv = torch.unique(keys, return_inverse=True)
             return torch.zeros(u.numel(), device=dev, dtype=torch.float64).index_add_(0, inv, vals)
 
         t = run({"hash_aggregate": dev_agg, "hash_aggregate_no_first": dev_agg_nofirst,
-                 "hash_aggregate_with_inverse": dev_agg_inv,
+                 "hash_aggregate_with_inverse": dev_agg_inv, "hash_aggregate_without_mid": dev_agg_part,
                  "torch_unique_index_add": torch_agg}, a.rounds)
         t["groups"] = int(ref_u.numel())
-        t["path"] = "LOW" if int(r[5][1]) == 0 else "PART"
+        t["path"] = ("LOW", "PART", "MID")[int(r[5][1])]
         t["sample_distinct"] = int(r[5][3])
         t["max_rel_err"] = err
         out["groupby"][str(distinct)] = t
