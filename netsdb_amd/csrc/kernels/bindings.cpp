@@ -52,6 +52,8 @@ int nsdb_block_simcount(const void* pool, const long long* cand, const void* que
                         int bc, int h, int w, float fp, int is_f32, int S, unsigned* partial, hipStream_t st);
 int nsdb_block_maxdiff(const void* pool, const long long* cand, const void* blks, long long nblocks, long long elems,
                        int is_f32, int S, float* partial, hipStream_t st);
+int nsdb_str_pack(const void* bytes, const int64_t* starts, const int64_t* ends, int64_t n, int L, int64_t* out,
+                  hipStream_t st);
 int nsdb_str_hash(const void* bytes, const int64_t* starts, const int64_t* ends, int64_t n, uint64_t* out,
                   hipStream_t st);
 int nsdb_str_like(const void* bytes, const int64_t* starts, const int64_t* ends, int64_t n, const uint8_t* pat,
@@ -517,6 +519,18 @@ torch::Tensor str_hash(torch::Tensor bytes, torch::Tensor st, torch::Tensor en, 
   return out;
 }
 
+// Exact short-string codes (strings.hip str_pack_kernel); the caller guarantees every row is <= L <= 7 bytes.
+torch::Tensor str_pack(torch::Tensor bytes, torch::Tensor st, torch::Tensor en, int64_t L) {
+  check_strings(bytes, st, en);
+  TORCH_CHECK(L >= 0 && L <= 7, "str_pack: L must be in [0, 7]");
+  const int64_t n = st.numel();
+  auto out = torch::empty({n}, st.options());
+  check_rc(nsdb_str_pack(bytes.data_ptr(), st.data_ptr<int64_t>(), en.data_ptr<int64_t>(), n, (int)L,
+                         out.data_ptr<int64_t>(), cur_stream()),
+           "str_pack");
+  return out;
+}
+
 torch::Tensor str_like(torch::Tensor bytes, torch::Tensor st, torch::Tensor en, int64_t payload_end,
                        const std::string& pat, std::vector<int64_t> seg_start, std::vector<int64_t> seg_len,
                        bool anchor_start, bool anchor_end, bool negate) {
@@ -739,6 +753,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("block_maxdiff_partial", &block_maxdiff_partial, "dedup: per-(block, split) max |pool[cand] - blk|");
   m.def("hash_group_ids", &hash_group_ids, "exact group-by of a device int64 column: (inverse, sorted keys)");
   m.def("str_hash", &str_hash, "64-bit hash per string of a device string column");
+  m.def("str_pack", &str_pack, "exact order-preserving int64 code per string of <= 7 bytes");
   m.def("str_like", &str_like, "SQL LIKE over a device string column (segments of the pattern bytes)");
   m.def("str_slice", &str_slice, "SUBSTRING of every row of a device string column (no host read)");
   m.def("str_eq_pairs", &str_eq_pairs, "byte-exact equality of string row pairs a[ia[i]] == b[ib[i]]",

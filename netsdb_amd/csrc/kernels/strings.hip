@@ -140,6 +140,26 @@ __global__ __launch_bounds__(256) void str_slice_kernel(const uint8_t* __restric
 
 inline int grid_for(int64_t n) { return (int)((n + 255) / 256); }
 
+// Exact short-string code (every row <= L <= 7 bytes, L a bound the caller knows): the row's bytes big-endian in
+// the low 8L bits, shifted left by 3, OR its length. Equal codes <=> equal strings, and code order is the bytes'
+// lexicographic order, so short string keys (TPC-H flags, modes, priorities) group / sort as plain integers with
+// no hash and no byte re-check.
+__global__ __launch_bounds__(256) void str_pack_kernel(const uint32_t* __restrict__ w, const int64_t* __restrict__ st,
+                                                      const int64_t* __restrict__ en, int64_t n, int L,
+                                                      int64_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t s = st[i];
+  const int64_t len = en[i] - s;
+  uint64_t be = 0;
+  if (len > 0 && L > 0) {
+    uint64_t c = load8(w, s);
+    c &= len < 8 ? (1ull << (8 * len)) - 1ull : ~0ull;
+    be = __builtin_bswap64(c) >> (8 * (8 - L));   // byte 0 at bits [8(L-1), 8L)
+  }
+  out[i] = (int64_t)((be << 3) | (uint64_t)len);
+}
+
 
 // Exact equality of row pairs (a[ia[i]] == b[ib[i]]) for value-exact string keys: group-by / join / IN decide by
 // 64-bit hash first, then every row is byte-compared with its group's or match's representative
@@ -175,6 +195,15 @@ int nsdb_str_hash(const void* bytes, const int64_t* starts, const int64_t* ends,
                   hipStream_t st) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(str_hash_kernel, dim3(grid_for(n)), dim3(256), 0, st, (const uint32_t*)bytes, starts, ends, n,
+                     out);
+  return (int)hipGetLastError();
+}
+
+int nsdb_str_pack(const void* bytes, const int64_t* starts, const int64_t* ends, int64_t n, int L, int64_t* out,
+                  hipStream_t st) {
+  if (L < 0 || L > 7) return -2;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(str_pack_kernel, dim3(grid_for(n)), dim3(256), 0, st, (const uint32_t*)bytes, starts, ends, n, L,
                      out);
   return (int)hipGetLastError();
 }

@@ -197,6 +197,39 @@ def _device_cols(keys):
     return cols
 
 
+def _exact_words(cols):
+    """Value-exact int64 words of key columns (numbers by value, strings of <= 7 bytes by their order-preserving
+    short codes, StringColumn.short_codes), or None when a string column holds longer rows (hash + re-check)."""
+    out = []
+    for c in cols:
+        if isinstance(c, StringColumn):
+            w = c.short_codes()
+            if w is None:
+                return None
+            out.append(w)
+        else:
+            out.append(_norm_col(c))
+    return out
+
+
+def _key_words(cols):
+    """(words, packed): exact words packed into one int64 when they fit, else hash words (packed None)."""
+    exact = _exact_words(cols)
+    if exact is not None:
+        packed = _pack_exact(exact)
+        if packed is not None:
+            return exact, packed
+        return exact, None
+    return [c.hash64() if isinstance(c, StringColumn) else _norm_col(c) for c in cols], None
+
+
+def _rep_from_word(u: torch.Tensor, c):
+    """A group's key column from its exact int64 word (inverse of _exact_words for one column)."""
+    if isinstance(c, StringColumn):
+        return StringColumn.from_short_codes(u, c.max_len())
+    return u.to(c.dtype) if not c.is_floating_point() else u.view(torch.float64).to(c.dtype)
+
+
 def _rows_match_rep(cols, words, ref: torch.Tensor) -> bool:
     """Every row's key equals the key of its group's representative row ``ref`` (exactness check of a
     hash-decided grouping)."""
@@ -233,8 +266,7 @@ def _group_ids_device(keys):
     cols = _device_cols(keys)
     if cols is None or len(cols[0]) == 0:
         return None
-    words = [c.hash64() if isinstance(c, StringColumn) else _norm_col(c) for c in cols]
-    packed = None if any(isinstance(c, StringColumn) for c in cols) else _pack_exact(words)
+    words, packed = _key_words(cols)
     key = packed[0] if packed is not None else _combine_words(words)
     r = _hash_aggregate(key, None, "sum", True)
     if r is None:
@@ -270,8 +302,7 @@ def group_reduce(keys, values, op: str = "sum"):
     if op != "count":
         vals = flat.double() if is_float else flat.long()
     kop = {"sum": "sum", "mean": "sum", "count": "sum", "min": "min", "max": "max"}[op]
-    words = [c.hash64() if isinstance(c, StringColumn) else _norm_col(c) for c in cols]
-    packed = None if any(isinstance(c, StringColumn) for c in cols) else _pack_exact(words)
+    words, packed = _key_words(cols)
     key = packed[0] if packed is not None else _combine_words(words)
     # packed keys are the values themselves: no representative row (first / inverse) is needed, so the
     # partition passes carry no row ids
@@ -294,12 +325,9 @@ def group_reduce(keys, values, op: str = "sum"):
         agg = agg.to(out_dtype).reshape((g,) + tuple(values.shape[1:]))
     if packed is not None and packed[1] is not None:
         unp = _unpack(reps_k.index_select(0, order), packed[1])
-        reps = tuple(u.to(c.dtype) if not c.is_floating_point() else u.view(torch.float64).to(c.dtype)
-                     for u, c in zip(unp, cols))
+        reps = tuple(_rep_from_word(u, c) for u, c in zip(unp, cols))
     elif packed is not None:
-        rk = reps_k.index_select(0, order)
-        c = cols[0]
-        reps = (rk.to(c.dtype) if not c.is_floating_point() else rk.view(torch.float64).to(c.dtype),)
+        reps = (_rep_from_word(reps_k.index_select(0, order), cols[0]),)
     else:
         fo = first.index_select(0, order)
         reps = tuple(_take_col(c, fo) for c in cols)

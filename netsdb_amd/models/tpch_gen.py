@@ -60,7 +60,7 @@ class GenStrings:
         data = np.zeros(StringColumn._alloc_size(n * w), dtype=np.uint8)
         data[: n * w] = self.fixed.ravel()
         off = np.arange(n + 1, dtype=np.int64) * w
-        col = StringColumn(torch.from_numpy(data), torch.from_numpy(off), n * w)
+        col = StringColumn(torch.from_numpy(data), torch.from_numpy(off), n * w, maxlen=w)
         return col.to(device) if device is not None else col
 
     def to_pandas(self):

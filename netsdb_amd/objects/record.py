@@ -520,13 +520,14 @@ def merge_adjacent_column(parts, check: bool = True):
                 return None
             n = sum(len(p) for p in parts)
             return StringColumn(c0.data, o0.as_strided((n + 1,), (1,), o0.storage_offset()),
-                                max(p.payload for p in parts), c0.buf_rows)
+                                max(p.payload for p in parts), c0.buf_rows, StringColumn.max_bound(parts))
         # views: their row-bound arrays must themselves be adjacent slices (no copy is ever made here)
         st = _adjacent_tensors([p.starts for p in parts], check)
         en = _adjacent_tensors([p.ends for p in parts], check) if st is not None else None
         if st is None or en is None:
             return None
-        return StringColumn.view(c0.data, st, en, max(p.payload for p in parts), max(p.buf_rows for p in parts))
+        return StringColumn.view(c0.data, st, en, max(p.payload for p in parts), max(p.buf_rows for p in parts),
+                                 StringColumn.max_bound(parts))
     if isinstance(c0, tuple):
         subs = [merge_adjacent_column([p[i] for p in parts], check) for i in range(len(c0))]
         return None if any(x is None for x in subs) else tuple(subs)

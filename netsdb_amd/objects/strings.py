@@ -129,18 +129,23 @@ class StringColumn:
     rows costs two device gathers and no device->host read. Kernels take (starts, ends) and so run on either
     form; :attr:`offsets` (serialisation, shuffles) packs a view in place on first use."""
 
-    __slots__ = ("data", "starts", "ends", "_off", "payload", "buf_rows")
+    __slots__ = ("data", "starts", "ends", "_off", "payload", "buf_rows", "_maxlen")
 
-    def __init__(self, data: torch.Tensor, offsets: torch.Tensor, payload: int, buf_rows: Optional[int] = None):
+    def __init__(self, data: torch.Tensor, offsets: torch.Tensor, payload: int, buf_rows: Optional[int] = None,
+                 maxlen: Optional[int] = None):
         self.data, self._off, self.payload = data, offsets, int(payload)
         self.starts, self.ends = offsets[:-1], offsets[1:]
         self.buf_rows = max(1, offsets.numel() - 1) if buf_rows is None else buf_rows   # rows sharing data
+        if maxlen is None and offsets.device.type == "cpu" and offsets.numel() > 1:
+            maxlen = int(np.diff(offsets.numpy()).max())       # host offsets: free to bound here
+        self._maxlen = maxlen     # upper bound of the row lengths (None: not known yet, see max_len)
 
     @staticmethod
     def view(data: torch.Tensor, starts: torch.Tensor, ends: torch.Tensor, payload: int,
-             buf_rows: int) -> "StringColumn":
+             buf_rows: int, maxlen: Optional[int] = None) -> "StringColumn":
         c = StringColumn.__new__(StringColumn)
         c.data, c.starts, c.ends, c._off, c.payload, c.buf_rows = data, starts, ends, None, int(payload), buf_rows
+        c._maxlen = maxlen
         return c
 
     # ------------------------------------------------------------------ construction
@@ -161,7 +166,7 @@ class StringColumn:
         data, offs = torch.from_numpy(buf), torch.from_numpy(off)
         if device is not None and torch.device(device).type != "cpu":
             data, offs = data.pin_memory().to(device, non_blocking=True), offs.pin_memory().to(device, non_blocking=True)
-        return StringColumn(data, offs, payload)
+        return StringColumn(data, offs, payload, maxlen=int(lens.max()) if len(enc) else 0)
 
     @staticmethod
     def empty(device=None) -> "StringColumn":
@@ -212,8 +217,9 @@ class StringColumn:
                 return self.take(torch.arange(s, e, step, dtype=torch.long))
             e = max(e, s)
             if self._off is not None:
-                return StringColumn(self.data, self._off[s:e + 1], self.payload, self.buf_rows)
-            return StringColumn.view(self.data, self.starts[s:e], self.ends[s:e], self.payload, self.buf_rows)
+                return StringColumn(self.data, self._off[s:e + 1], self.payload, self.buf_rows, self._maxlen)
+            return StringColumn.view(self.data, self.starts[s:e], self.ends[s:e], self.payload, self.buf_rows,
+                                     self._maxlen)
         if isinstance(i, (torch.Tensor, list, np.ndarray)):
             return self.take(i)
         n = len(self)
@@ -242,9 +248,10 @@ class StringColumn:
             return self.compact().to(device)          # do not move a large shared buffer for a few rows
         data = self.data.to(device, non_blocking=True)
         if self._off is not None:
-            return StringColumn(data, self._off.to(device, non_blocking=True), self.payload, self.buf_rows)
+            return StringColumn(data, self._off.to(device, non_blocking=True), self.payload, self.buf_rows,
+                                self._maxlen)
         return StringColumn.view(data, self.starts.to(device, non_blocking=True),
-                                 self.ends.to(device, non_blocking=True), self.payload, self.buf_rows)
+                                 self.ends.to(device, non_blocking=True), self.payload, self.buf_rows, self._maxlen)
 
     def compact(self) -> "StringColumn":
         """Own packed buffer holding exactly these rows (one device->host read of the byte total)."""
@@ -264,7 +271,7 @@ class StringColumn:
                 pos = np.repeat(st - out_off[:-1].numpy(), ln) + np.arange(total)
                 data_np[:total] = self.data.numpy()[pos]
             data = torch.from_numpy(data_np)
-        return StringColumn(data, out_off, total)
+        return StringColumn(data, out_off, total, maxlen=self._maxlen)
 
     # ------------------------------------------------------------------ relational ops
     def take(self, idx) -> "StringColumn":
@@ -282,7 +289,7 @@ class StringColumn:
             if ii.min() < -len(self) or ii.max() >= len(self):
                 raise IndexError("string take index out of range")
         return StringColumn.view(self.data, self.starts.index_select(0, idx), self.ends.index_select(0, idx),
-                                 self.payload, self.buf_rows)
+                                 self.payload, self.buf_rows, self._maxlen)
 
     def substr(self, start: int, length: int) -> "StringColumn":
         """SQL SUBSTRING(s FROM start + 1 FOR length) of every row, on bytes (0-based ``start``): lengths clamped
@@ -308,7 +315,8 @@ class StringColumn:
                 pos = np.repeat(st + start - oo[:-1], ln) + np.arange(total)
                 data_np[:total] = src[pos]
             data = torch.from_numpy(data_np)
-        return StringColumn(data, out_off, cap)
+        bound = length if self._maxlen is None else max(0, min(length, self._maxlen - start))
+        return StringColumn(data, out_off, cap, maxlen=bound)
 
     @staticmethod
     def concat(parts: Sequence["StringColumn"]) -> "StringColumn":
@@ -321,7 +329,8 @@ class StringColumn:
         if all(p.data is d0 for p in parts):
             # rows of one buffer (the pages / filtered slices of one set): concatenate the row bounds only
             return StringColumn.view(d0, torch.cat([p.starts for p in parts]), torch.cat([p.ends for p in parts]),
-                                     max(p.payload for p in parts), max(p.buf_rows for p in parts))
+                                     max(p.payload for p in parts), max(p.buf_rows for p in parts),
+                                     StringColumn.max_bound(parts))
         parts = [p if p.is_packed else p.compact() for p in parts]
         datas, offs, base = [], [torch.zeros(1, dtype=torch.int64, device=dev)], 0
         for p in parts:
@@ -338,7 +347,52 @@ class StringColumn:
         for (d, _, _), (s, e) in zip(datas, bounds):
             data[pos:pos + e - s] = d[s:e]
             pos += e - s
-        return StringColumn(data, torch.cat(offs), total)
+        return StringColumn(data, torch.cat(offs), total, maxlen=StringColumn.max_bound(parts))
+
+    @staticmethod
+    def max_bound(parts: Sequence["StringColumn"]) -> Optional[int]:
+        """Largest row-length bound of several columns (None if any is unknown)."""
+        b = [p._maxlen for p in parts]
+        return None if any(x is None for x in b) else max(b, default=0)
+
+    def max_len(self) -> int:
+        """An upper bound of the row lengths (exact when computed here: one device reduction + host read, cached)."""
+        if self._maxlen is None:
+            self._maxlen = int((self.ends - self.starts).amax()) if len(self) else 0
+        return self._maxlen
+
+    def short_codes(self) -> Optional[torch.Tensor]:
+        """Exact int64 code per row when every row is <= 7 bytes, else None: bytes big-endian in the low 8L bits
+        (L = :meth:`max_len`), shifted left 3, OR the length. Equal codes <=> equal strings and code order = byte
+        order, so short string keys group, join and sort as integers (no hash, no byte re-check)."""
+        L = self.max_len()
+        if L > 7:
+            return None
+        if self.device.type == "cuda":
+            return _ext.hip().str_pack(self.data, self.starts.contiguous(), self.ends.contiguous(), L)
+        st, en, buf = self.starts.numpy(), self.ends.numpy(), self.data.numpy()
+        ln = en - st
+        be = np.zeros(len(st), dtype=np.int64)
+        for j in range(L):
+            b = buf[np.minimum(st + j, buf.size - 1)].astype(np.int64)
+            be |= np.where(ln > j, b, 0) << (8 * (L - 1 - j))
+        return torch.from_numpy((be << 3) | ln)
+
+    @staticmethod
+    def from_short_codes(codes: torch.Tensor, L: int) -> "StringColumn":
+        """Inverse of :meth:`short_codes` (codes made with bound ``L``), on the codes' device."""
+        dev, n = codes.device, codes.numel()
+        lens = codes & 7
+        off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        if n:
+            torch.cumsum(lens, 0, out=off[1:])
+        total = int(off[-1]) if n else 0
+        data = torch.zeros(StringColumn._alloc_size(total), dtype=torch.uint8, device=dev)
+        if total:
+            j = torch.arange(L, device=dev, dtype=torch.int64)
+            byts = (codes.unsqueeze(1) >> (3 + 8 * (L - 1 - j)).unsqueeze(0)) & 0xFF
+            data[:total] = byts[j.unsqueeze(0) < lens.unsqueeze(1)].to(torch.uint8)
+        return StringColumn(data, off, total, maxlen=L)
 
     def hash64(self) -> torch.Tensor:
         """int64 hash per row (== :func:`hash_str` of the row)."""

@@ -202,7 +202,7 @@ def test_partition_order_stable(P):
 
 @pytest.mark.gpu
 def test_string_keys_exact_under_hash_collisions_gpu(monkeypatch):
-    strs = [f"key{i % 37}" for i in range(5000)]
+    strs = [f"longer-key{i % 37}" for i in range(5000)]     # > 7 bytes: the hash + byte re-check path
     col = StringColumn.from_list(strs, DEV)
     orig = StringColumn.hash64
     monkeypatch.setattr(StringColumn, "hash64", lambda self: orig(self) & 3)   # 4 hash values for 37 strings
@@ -217,8 +217,8 @@ def test_string_keys_exact_under_hash_collisions_gpu(monkeypatch):
     r = K.group_reduce(col, vals, "sum")
     if r is not None:   # a hash-decided fused result must be exact too
         assert sorted(zip(r[0].tolist(), r[1].tolist())) == sorted((s, float(strs.count(s))) for s in set(strs))
-    m = col.isin(["key1", "key5"])
-    assert m.tolist() == [s in ("key1", "key5") for s in strs]
+    m = col.isin(["longer-key1", "longer-key5"])
+    assert m.tolist() == [s in ("longer-key1", "longer-key5") for s in strs]
 
 
 @pytest.mark.gpu
@@ -335,3 +335,46 @@ def test_hash_aggregate_mid_overflow_falls_back_to_part():
     assert int(r[5][2]) == 1 and int(r[5][1]) == 1, r[5]
     assert int(r[5][3]) < 10_000                              # the sample's estimate pointed at MID
     _check_agg(keys, vals, "sum", r)
+
+
+_SHORT = ["", "a", "ab", "a\x00", "b", "zz", "abcdefg", "\u00e9", "A", "ab"]
+
+
+def _check_short_codes(col, strs):
+    codes = col.short_codes().cpu()
+    enc = [x.encode() for x in strs]
+    assert len(set(codes.tolist())) == len(set(enc))
+    assert all((codes[i] == codes[j]).item() == (enc[i] == enc[j]) for i in range(len(enc)) for j in range(len(enc)))
+    order = sorted(range(len(enc)), key=lambda i: enc[i])          # byte-lexicographic
+    assert sorted(codes.tolist()) == [codes[i].item() for i in order]
+    back = StringColumn.from_short_codes(codes.to(col.device), col.max_len())
+    assert back.tolist() == strs
+
+
+def test_short_string_codes_cpu():
+    """Strings of <= 7 bytes as exact, order-preserving int64 codes (no hash, no byte re-check)."""
+    col = StringColumn.from_list(_SHORT)
+    assert col.max_len() == 7
+    _check_short_codes(col, _SHORT)
+    _check_short_codes(col.take(torch.tensor([1, 4, 4, 8])), [_SHORT[i] for i in (1, 4, 4, 8)])
+    assert StringColumn.from_list(["abcdefgh", "a"]).short_codes() is None       # 8 bytes: hash path
+
+
+@pytest.mark.gpu
+def test_short_string_codes_and_groupby_gpu():
+    col = StringColumn.from_list(_SHORT, DEV)
+    _check_short_codes(col, _SHORT)
+    assert torch.equal(col.short_codes().cpu(), StringColumn.from_list(_SHORT).short_codes())
+    # a two-column short string key (the TPC-H Q01 shape): packed into one exact int, groups in byte order
+    g = torch.Generator(device=DEV).manual_seed(2)
+    n = 300_000
+    f1 = StringColumn.from_list(["A", "N", "R"], DEV).take(torch.randint(0, 3, (n,), device=DEV, generator=g))
+    f2 = StringColumn.from_list(["F", "O"], DEV).take(torch.randint(0, 2, (n,), device=DEV, generator=g))
+    v = torch.rand(n, 2, device=DEV, dtype=torch.float64, generator=g)
+    reps, agg = K.group_reduce((f1, f2), v, "sum")
+    keys = list(zip(f1.tolist(), f2.tolist()))
+    assert list(zip(reps[0].tolist(), reps[1].tolist())) == sorted(set(keys))
+    uk = sorted(set(keys))
+    gid = torch.tensor([uk.index(k) for k in keys])
+    ref = torch.zeros(len(uk), 2, dtype=torch.float64).index_add_(0, gid, v.cpu())
+    torch.testing.assert_close(agg.cpu(), ref, rtol=1e-9, atol=1e-9)
