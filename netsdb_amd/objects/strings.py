@@ -361,12 +361,14 @@ class StringColumn:
             self._maxlen = int((self.ends - self.starts).amax()) if len(self) else 0
         return self._maxlen
 
-    def short_codes(self) -> Optional[torch.Tensor]:
+    def short_codes(self, L: Optional[int] = None) -> Optional[torch.Tensor]:
         """Exact int64 code per row when every row is <= 7 bytes, else None: bytes big-endian in the low 8L bits
-        (L = :meth:`max_len`), shifted left 3, OR the length. Equal codes <=> equal strings and code order = byte
-        order, so short string keys group, join and sort as integers (no hash, no byte re-check)."""
-        L = self.max_len()
-        if L > 7:
+        (L = :meth:`max_len`, or a larger given bound), shifted left 3, OR the length. Equal codes <=> equal
+        strings and code order = byte order, so short string keys group, join and sort as integers (no hash, no
+        byte re-check)."""
+        ml = self.max_len()
+        L = ml if L is None else L
+        if L > 7 or ml > L:
             return None
         if self.device.type == "cuda":
             return _ext.hip().str_pack(self.data, self.starts.contiguous(), self.ends.contiguous(), L)
@@ -471,6 +473,14 @@ class StringColumn:
         n = len(self)
         if n == 0 or not values:
             return torch.zeros(n, dtype=torch.bool, device=self.device)
+        codes = self.short_codes()
+        if codes is not None:       # short rows: exact integer membership (values longer than any row never match)
+            L = self.max_len()
+            fit = [v for v in values if len(v.encode() if isinstance(v, str) else bytes(v)) <= L]
+            if not fit:
+                return torch.zeros(n, dtype=torch.bool, device=self.device)
+            ref = StringColumn.from_list(fit, self.device).short_codes(L)
+            return torch.isin(codes, ref)
         h = self.hash64()
         ref = StringColumn.from_list(values, self.device)
         sh, order = torch.sort(ref.hash64())

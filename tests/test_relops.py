@@ -358,6 +358,8 @@ def test_short_string_codes_cpu():
     _check_short_codes(col, _SHORT)
     _check_short_codes(col.take(torch.tensor([1, 4, 4, 8])), [_SHORT[i] for i in (1, 4, 4, 8)])
     assert StringColumn.from_list(["abcdefgh", "a"]).short_codes() is None       # 8 bytes: hash path
+    assert col.isin(["ab", "zz", "much too long"]).tolist() == [x in ("ab", "zz") for x in _SHORT]
+    assert col.take(torch.tensor([1, 2])).isin(["abcdefg"]).tolist() == [False, False]
 
 
 @pytest.mark.gpu
