@@ -90,9 +90,9 @@ def test_hash_aggregate_int64_and_sentinel(op):
     keys[::97] = torch.iinfo(torch.int64).min            # the empty-slot marker as a real key
     keys[5::101] = torch.iinfo(torch.int64).max
     vals = torch.randint(-10**12, 10**12, (100_000,), device=DEV, generator=g)
-    for thr, mid in ((0, 0), (1, 0), (1, -1)):             # LOW path, MID path, forced PART path
+    for thr, mid, path in ((100_000, 0, 0), (1, 0, 2), (1, -1, 1)):   # forced LOW, MID, forced PART
         r = _ext.hip().hash_aggregate(keys, vals, op, True, thr, True, mid)
-        assert int(r[5][1]) == (0 if thr == 0 else (2 if mid == 0 else 1))
+        assert int(r[5][1]) == path
         _check_agg(keys, vals.unsqueeze(1), op, r, rtol=0)
     r = _ext.hip().hash_aggregate(keys, None, "sum", False, 0)   # counts only, no inverse
     reps, _, cnt, _, inv, _ = r
