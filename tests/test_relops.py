@@ -17,7 +17,7 @@ def _ref_groupby(keys, vals, op):
     """dict: key -> (agg row, count) in fp64 / int64 on the host."""
     out = {}
     k = keys.tolist()
-    v = vals.tolist() if vals is not None else [None] * len(k)
+    v = vals.tolist() if vals is not None else [[]] * len(k)
     for kk, vv in zip(k, v):
         vv = vv if isinstance(vv, list) else [vv]
         if kk not in out:
