@@ -16,6 +16,10 @@
 //    rows whose key does not fit go straight to a small global table, and at the end each workgroup flushes its
 //    LDS entries ONCE into the global table (agent-scope atomics): one global atomic per (workgroup, key), not per
 //    row. If the global table overflows (the sample under-estimated the groups) a device flag routes the work to:
+//  * MID path (up to ~10 K groups for one value column, what one workgroup's 160 KiB LDS holds as dense arrays):
+//    agg_mid — a global key -> dense-id dictionary (L2-resident, claimed by CAS, ids from one counter) and per
+//    workgroup LDS accumulators indexed by the id; agg_mid_reduce folds the workgroups' partials per id. One pass
+//    over the rows and no partition buffers. Ids beyond the LDS arrays set a flag that routes the work to:
 //  * PART path (many groups): 256 level-1 buckets by the top hash bits (agg_hist: per-workgroup LDS histograms;
 //    scan_rows / scan_tot: block scans; agg_scatter: tile-staged counting sort in LDS, so each bucket's rows leave
 //    as one coalesced run per tile), then agg_bucket: workgroup b owns bucket b whole. If its share of the
