@@ -44,6 +44,11 @@ def _worker(rank, ws, port, out_dir, device="cuda:0"):
         res = {q: tpch.QUERIES[q](c, "tpch") for q in QUERIES}
         res["_hip"] = _ext.hip() is not None
         torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
+    except BaseException:
+        import traceback
+        with open(os.path.join(out_dir, f"err{rank}.txt"), "w") as fh:   # every rank's own traceback
+            fh.write(traceback.format_exc())
+        raise
     finally:
         dist.destroy_process_group()
 
@@ -54,7 +59,11 @@ def test_tpch_two_ranks_on_one_gpu_vs_pandas():
     from netsdb_amd.models import tpch, tpch_gen
 
     out = tempfile.mkdtemp()
-    mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    try:
+        mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    except Exception:
+        errs = [open(os.path.join(out, f)).read() for f in sorted(os.listdir(out)) if f.startswith("err")]
+        raise AssertionError("rank failures:\n" + "\n".join(errs))
     res = [torch.load(os.path.join(out, f"r{r}.pt"), weights_only=False) for r in range(2)]
     t = tpch_gen.generate_fast(0.01, seed=5)
     f = tpch.frames(t)
