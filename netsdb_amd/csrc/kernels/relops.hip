@@ -535,6 +535,86 @@ __device__ __noinline__ i64 mid_id_slow(DSlot* d, u64 mask, u64 k, AggMeta* m, i
   }
 }
 
+// Claim k's dictionary slot (no id read): the CAS winner takes the next dense id and publishes it.
+__device__ __forceinline__ void mid_claim(DSlot* d, u64 mask, u64 k, AggMeta* m, i64 dcap, i64* reps) {
+  const bool sent = k == kEmpty;
+  const u64 want = sent ? 1ull : k, empty = sent ? 0ull : kEmpty;
+  u64 s = sent ? mask + 1 : (mix64(k) & mask);
+  const u64 window = mask < kGlobalProbe ? mask + 1 : kGlobalProbe;
+  for (u64 p = 0; p < window; ++p) {
+    u64 cur = empty;
+    if (__hip_atomic_compare_exchange_strong(&d[s].key, &cur, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT)) {
+      const i64 id = __hip_atomic_fetch_add(&m->ng_mid, (i64)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&d[s].id, id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (id < dcap) reps[id] = (i64)k;
+      else __hip_atomic_store(&m->fail_mid, (i64)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    if (cur == want) return;
+    if (sent) break;
+    s = (s + 1) & mask;
+  }
+  __hip_atomic_store(&m->fail_mid, (i64)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Dictionary build, a kernel of its own: the slots are claimed by device-scope CAS, which this XCD's L2 does not
+// see, so a lookup in the same kernel could read a stale "empty" line and fall to the slow path for every row.
+// After the launch boundary the accumulation kernel reads a complete dictionary from L2. Each workgroup first
+// dedups its keys in an LDS key set, so a key costs one global CAS per workgroup, not per row.
+__global__ __launch_bounds__(kMidThreads) void agg_mid_dict_kernel(const u64* __restrict__ keys, i64 n, int scap,
+                                                                   DSlot* dict, u64 dmask, AggMeta* meta, i64 dcap,
+                                                                   i64* __restrict__ reps) {
+  if (!take_mid(meta)) return;
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  u64* set = reinterpret_cast<u64*>(lds_raw);
+  for (int i = threadIdx.x; i < scap; i += kMidThreads) set[i] = kEmpty;
+  __syncthreads();
+  constexpr int TILE = kMidThreads * kU;
+  const i64 tstride = (i64)gridDim.x * TILE;
+  const int smask = scap - 1;
+  u64 cur[kU], nxt[kU];
+  auto load = [&](i64 b0, u64 (&kk)[kU]) {
+#pragma unroll
+    for (int j = 0; j < kU; ++j) {
+      const i64 i = b0 + (i64)j * kMidThreads + threadIdx.x;
+      kk[j] = i < n ? keys[i] : kEmpty;
+    }
+  };
+  i64 t0 = (i64)blockIdx.x * TILE;
+  if (t0 < n) load(t0, cur);
+  for (int it = 0; t0 < n; t0 += tstride, ++it) {
+    if ((it & 7) == 7 && __hip_atomic_load(&meta->fail_mid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+    if (t0 + tstride < n) load(t0 + tstride, nxt);
+#pragma unroll
+    for (int j = 0; j < kU; ++j) {
+      const i64 i = t0 + (i64)j * kMidThreads + threadIdx.x;
+      if (i >= n) break;
+      const u64 k = cur[j];
+      bool fresh = true;   // first sight of k in this workgroup (or its LDS window is full)
+      if (k != kEmpty) {
+        int s = (int)((mix64(k) >> 32) & (u64)smask);
+        for (int p = 0; p < kLdsProbe; ++p) {
+          u64 c = set[s];
+          if (c == kEmpty) {
+            __hip_atomic_compare_exchange_strong(set + s, &c, k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (c == kEmpty) break;   // claimed here: fresh
+          }
+          if (c == k) {
+            fresh = false;
+            break;
+          }
+          s = (s + 1) & smask;
+        }
+      }
+      if (fresh) mid_claim(dict, dmask, k, meta, dcap, reps);
+    }
+#pragma unroll
+    for (int j = 0; j < kU; ++j) cur[j] = nxt[j];
+  }
+}
+
 // rows [t0, ...) strided like agg_low; LDS: [acc dcap*F u64 | cnt dcap u32 | rmin dcap u32 (want_first)]
 template <typename VT, int OP>
 __global__ __launch_bounds__(kMidThreads) void agg_mid_kernel(const u64* __restrict__ keys,
@@ -1403,6 +1483,10 @@ int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv,
     unsigned* part_cnt = reinterpret_cast<unsigned*>(part_acc + (size_t)Gm * dcap * F);
     unsigned* part_rmin = part_cnt + (size_t)Gm * dcap;
     const size_t lbytes_mid = (size_t)dcap * (8 * F + 4 + (want_first ? 4 : 0)) + kMidReserve;
+    int scap = 1024;   // LDS key set of the dictionary build: <= 1/2 full at dcap keys, <= 128 KiB
+    while (scap < 16384 && scap < 2 * dcap) scap <<= 1;
+    hipLaunchKernelGGL(agg_mid_dict_kernel, dim3(Gm), dim3(kMidThreads), (size_t)scap * 8, st, k, n, scap,
+                       reinterpret_cast<DSlot*>(gmid_v), (u64)(gcap_mid - 1), meta, (i64)dcap, o.reps);
     hipLaunchKernelGGL((agg_mid_kernel<VT, OP>), dim3(Gm), dim3(kMidThreads), lbytes_mid, st, k, v, n, F, dcap,
                        want_first, reinterpret_cast<DSlot*>(gmid_v), (u64)(gcap_mid - 1), meta, o, part_nw, part_acc,
                        part_cnt, part_rmin);

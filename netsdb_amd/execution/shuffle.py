@@ -64,7 +64,10 @@ class PackedSchema:
             c = b.columns[name]
             if w == 0:
                 continue
-            parts.append(c.contiguous().reshape(n, w // c.element_size()).view(torch.uint8).reshape(n, w))
+            cc = c.contiguous().reshape(n, w // c.element_size())
+            if cc.stride(-1) != 1:     # one-row views count as contiguous whatever their stride
+                cc = cc.clone(memory_format=torch.contiguous_format)
+            parts.append(cc.view(torch.uint8).reshape(n, w))
         if not parts:
             return torch.zeros(n, self.row_bytes, dtype=torch.uint8, device=b.device)
         return parts[0] if len(parts) == 1 else torch.cat(parts, dim=1)

@@ -31,6 +31,16 @@ def test_packed_row_image_roundtrip():
     assert empty.shape == (0, ps.row_bytes) and ps.unpack(empty).n == 0
 
 
+def test_packed_row_image_of_one_row_strided_columns():
+    """A one-row batch of column views (stride 6, e.g. an aggregate's value row split into columns) packs too:
+    torch calls a one-element view contiguous whatever its stride."""
+    v = torch.rand(1, 6, dtype=torch.float64)
+    b = RecordBatch({f"c{j}": v[:, j] for j in range(6)}, 1)
+    ps = PackedSchema(_batch_meta(b))
+    back = ps.unpack(ps.pack(b))
+    assert torch.equal(torch.stack([back.columns[f"c{j}"] for j in range(6)], 1), v)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
