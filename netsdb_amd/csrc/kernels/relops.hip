@@ -275,11 +275,11 @@ __device__ __forceinline__ int ltable_find(LTable t, u64 k, u64 h) {
 }
 
 template <typename VT, int OP>
-__device__ __forceinline__ void row_into_global(GTable g, u64 k, const VT* v, int F, i64* ngroups, i64* sentinel,
-                                                i64* fail, AggOut o, i64 row) {
+__device__ __forceinline__ void row_into_global(GTable g, u64 k, const VT* v, int F, i64 cs, i64* ngroups,
+                                                i64* sentinel, i64* fail, AggOut o, i64 row) {
   const i64 s = gtable_slot(g, k, ngroups, sentinel, fail, o);
   if (s < 0) return;
-  for (int f = 0; f < F; ++f) acc_add<VT, OP, __HIP_MEMORY_SCOPE_AGENT>(g.acc + s * F + f, v[f]);
+  for (int f = 0; f < F; ++f) acc_add<VT, OP, __HIP_MEMORY_SCOPE_AGENT>(g.acc + s * F + f, v[f * cs]);
   __hip_atomic_fetch_add(g.cnt + s, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_fetch_min(g.rmin + s, (u64)row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (o.inv) o.inv[row] = -(s + 1);
@@ -397,26 +397,30 @@ __global__ __launch_bounds__(256) void agg_init_kernel(u64* glow, i64 cap_low, u
 constexpr int kU = 4;        // rows per thread loaded before any is processed (memory-level parallelism)
 constexpr int kPreF = 1;     // value columns loaded with the keys (the rest at use)
 
-// Row (key, values) batch of one thread: kU rows of a 256*kU-row tile, loaded together.
+// Row (key, values) batch of one thread: kU rows of a 256*kU-row tile, loaded together. Value (i, f) of the input
+// is vals[i * rs + f * cs]: row-major [n, F] (rs = F, cs = 1) or column-major (rs = 1, cs = column pitch), so a
+// caller's stacked columns are read in place.
 template <typename VT>
 struct RowBatch {
   u64 k[kU];
   VT v[kU][kPreF];
   __device__ __forceinline__ void load(const u64* __restrict__ keys, const VT* __restrict__ vals, i64 t0, i64 n,
-                                       int F, int nthr) {
+                                       int F, int nthr, i64 rs, i64 cs) {
 #pragma unroll
     for (int j = 0; j < kU; ++j) {
       const i64 i = t0 + (i64)j * nthr + threadIdx.x;
       k[j] = i < n ? keys[i] : kEmpty;
 #pragma unroll
-      for (int f = 0; f < kPreF; ++f) v[j][f] = (i < n && f < F) ? vals[i * F + f] : VT(0);
+      for (int f = 0; f < kPreF; ++f) v[j][f] = (i < n && f < F) ? vals[i * rs + f * cs] : VT(0);
     }
   }
 };
 
 template <typename VT, int OP>
-__device__ __forceinline__ void ltable_add_row(LTable t, int s, VT v0, const VT* __restrict__ vrow, int F, u64 row) {
-  for (int f = 0; f < F; ++f) acc_add<VT, OP, __HIP_MEMORY_SCOPE_WORKGROUP>(t.acc + s * F + f, f == 0 ? v0 : vrow[f]);
+__device__ __forceinline__ void ltable_add_row(LTable t, int s, VT v0, const VT* __restrict__ vrow, int F, i64 cs,
+                                               u64 row) {
+  for (int f = 0; f < F; ++f)
+    acc_add<VT, OP, __HIP_MEMORY_SCOPE_WORKGROUP>(t.acc + s * F + f, f == 0 ? v0 : vrow[f * cs]);
   __hip_atomic_fetch_add(t.cnt + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   const unsigned r32 = (unsigned)row;
   if (r32 < t.rmin[s]) __hip_atomic_fetch_min(t.rmin + s, r32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -424,7 +428,8 @@ __device__ __forceinline__ void ltable_add_row(LTable t, int s, VT v0, const VT*
 
 template <typename VT, int OP>
 __global__ __launch_bounds__(256) void agg_low_kernel(const u64* __restrict__ keys, const VT* __restrict__ vals, i64 n,
-                                                      int F, int lcap, GTable g, AggMeta* meta, AggOut o) {
+                                                      int F, i64 rs, i64 cs, int lcap, GTable g, AggMeta* meta,
+                                                      AggOut o) {
   if (!take_low(meta)) return;
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   LTable t = ltable_at(lds_raw, lcap, F);
@@ -435,21 +440,21 @@ __global__ __launch_bounds__(256) void agg_low_kernel(const u64* __restrict__ ke
   int it = 0;
   RowBatch<VT> cur, nxt;
   i64 t0 = (i64)blockIdx.x * TILE;
-  if (t0 < n) cur.load(keys, vals, t0, n, F, 256);
+  if (t0 < n) cur.load(keys, vals, t0, n, F, 256, rs, cs);
   for (; t0 < n; t0 += tstride, ++it) {
     if ((it & 15) == 15 && __hip_atomic_load(&meta->fail_low, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
-    if (t0 + tstride < n) nxt.load(keys, vals, t0 + tstride, n, F, 256);   // in flight during this tile
+    if (t0 + tstride < n) nxt.load(keys, vals, t0 + tstride, n, F, 256, rs, cs);   // in flight during this tile
 #pragma unroll
     for (int j = 0; j < kU; ++j) {
       const i64 i = t0 + j * 256 + threadIdx.x;
       if (i >= n) break;
       const u64 k = cur.k[j];
-      const VT* v = vals + i * F;
+      const VT* v = vals + i * rs;
       const int s = k != kEmpty ? ltable_slot(t, k, mix64(k)) : -1;
       if (s >= 0) {
-        ltable_add_row<VT, OP>(t, s, cur.v[j][0], v, F, (u64)i);
+        ltable_add_row<VT, OP>(t, s, cur.v[j][0], v, F, cs, (u64)i);
       } else {   // rare: the values are re-read from memory
-        row_into_global<VT, OP>(g, k, v, F, &meta->ng_low, &meta->sentinel_low, &meta->fail_low, o, i);
+        row_into_global<VT, OP>(g, k, v, F, cs, &meta->ng_low, &meta->sentinel_low, &meta->fail_low, o, i);
       }
     }
     cur = nxt;
@@ -618,7 +623,8 @@ __global__ __launch_bounds__(kMidThreads) void agg_mid_dict_kernel(const u64* __
 // rows [t0, ...) strided like agg_low; LDS: [acc dcap*F u64 | cnt dcap u32 | rmin dcap u32 (want_first)]
 template <typename VT, int OP>
 __global__ __launch_bounds__(kMidThreads) void agg_mid_kernel(const u64* __restrict__ keys,
-                                                              const VT* __restrict__ vals, i64 n, int F, int dcap,
+                                                              const VT* __restrict__ vals, i64 n, int F, i64 rs,
+                                                              i64 cs, int dcap,
                                                               int want_first, DSlot* dict, u64 dmask, AggMeta* meta,
                                                               AggOut o, i64* __restrict__ part_nw,
                                                               u64* __restrict__ part_acc, unsigned* __restrict__ part_cnt,
@@ -641,10 +647,10 @@ __global__ __launch_bounds__(kMidThreads) void agg_mid_kernel(const u64* __restr
   int maxid = -1, it = 0;
   RowBatch<VT> cur, nxt;
   i64 t0 = (i64)blockIdx.x * TILE;
-  if (t0 < n) cur.load(keys, vals, t0, n, F, kMidThreads);
+  if (t0 < n) cur.load(keys, vals, t0, n, F, kMidThreads, rs, cs);
   for (; t0 < n; t0 += tstride, ++it) {
     if ((it & 7) == 7 && __hip_atomic_load(&meta->fail_mid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
-    if (t0 + tstride < n) nxt.load(keys, vals, t0 + tstride, n, F, kMidThreads);   // in flight during this tile
+    if (t0 + tstride < n) nxt.load(keys, vals, t0 + tstride, n, F, kMidThreads, rs, cs);   // in flight during this tile
     DSlot e[kU];
 #pragma unroll
     for (int j = 0; j < kU; ++j) {   // all dictionary reads of the batch issued together
@@ -664,9 +670,9 @@ __global__ __launch_bounds__(kMidThreads) void agg_mid_kernel(const u64* __restr
       if (id < 0) continue;
       const int x = (int)id;
       maxid = max(maxid, x);
-      const VT* vrow = vals + i * F;
+      const VT* vrow = vals + i * rs;
       for (int f = 0; f < F; ++f)
-        acc_add<VT, OP, __HIP_MEMORY_SCOPE_WORKGROUP>(lacc + (size_t)x * F + f, f == 0 ? cur.v[j][0] : vrow[f]);
+        acc_add<VT, OP, __HIP_MEMORY_SCOPE_WORKGROUP>(lacc + (size_t)x * F + f, f == 0 ? cur.v[j][0] : vrow[f * cs]);
       __hip_atomic_fetch_add(lcnt + x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       if (want_first) {
         const unsigned r32 = (unsigned)i;
@@ -874,8 +880,8 @@ __global__ __launch_bounds__(1024) void scan_tot_kernel(const i64* __restrict__ 
 // stores are long coalesced runs instead of one random 8-byte store per row. run[] (LDS, i64 [P]) is
 // advanced by the tile's counts. Row order inside a bucket is not preserved (the aggregates keep min row ids).
 template <typename VT, int R>
-__device__ __forceinline__ void staged_scatter(const u64* __restrict__ skey, const VT* __restrict__ sval,
-                                               const int* __restrict__ srow, i64 r0, i64 r1, int F, int shift,
+__device__ __forceinline__ void staged_scatter(const u64* __restrict__ skey, const VT* __restrict__ sval, i64 rs,
+                                               i64 cs, const int* __restrict__ srow, i64 r0, i64 r1, int F, int shift,
                                                int P, int T, char* lds, i64* run, unsigned* cnt, unsigned* off,
                                                unsigned* wsum, u64* __restrict__ dkey, VT* __restrict__ dval,
                                                int* __restrict__ drow) {
@@ -900,7 +906,7 @@ __device__ __forceinline__ void staged_scatter(const u64* __restrict__ skey, con
       const int p = threadIdx.x + j * nthr;
       const bool in = p < tnn;
       kk[j] = in ? skey[tb + p] : 0;
-      vv[j] = (in && F > 0) ? sval[(tb + p) * F] : VT(0);
+      vv[j] = (in && F > 0) ? sval[(tb + p) * rs] : VT(0);
       rr[j] = (in && rows) ? (rowsrc ? srow[tb + p] : (int)(tb + p)) : 0;
     }
   };
@@ -943,7 +949,7 @@ __device__ __forceinline__ void staged_scatter(const u64* __restrict__ skey, con
         st_key[q] = k[j];
         if (rows) st_row[q] = rw[j];
         st_b[q] = (unsigned short)bk[j];
-        for (int f = 0; f < F; ++f) st_val[(size_t)q * F + f] = f == 0 ? v0[j] : sval[i * F + f];
+        for (int f = 0; f < F; ++f) st_val[(size_t)q * F + f] = f == 0 ? v0[j] : sval[i * rs + f * cs];
       }
     }
     __syncthreads();
@@ -969,7 +975,7 @@ __device__ __forceinline__ void staged_scatter(const u64* __restrict__ skey, con
 // level-1 scatter: workgroup g packs its rows [g * rpw, ...) into the P1 buckets at bstart[b] + hist[b][g]
 template <typename VT>
 __global__ __launch_bounds__(1024) void agg_scatter_kernel(const u64* __restrict__ keys, const VT* __restrict__ vals,
-                                                           i64 n, int F, i64 rpw, int pbits, int T,
+                                                           i64 rs, i64 cs, i64 n, int F, i64 rpw, int pbits, int T,
                                                            const unsigned* __restrict__ hist,
                                                            const i64* __restrict__ bstart, u64* __restrict__ pkey,
                                                            VT* __restrict__ pval, int* __restrict__ prow,
@@ -982,7 +988,8 @@ __global__ __launch_bounds__(1024) void agg_scatter_kernel(const u64* __restrict
   for (int b = threadIdx.x; b < P; b += blockDim.x) run[b] = bstart[b] + hist[(size_t)b * gridDim.x + blockIdx.x];
   __syncthreads();
   const i64 r0 = (i64)blockIdx.x * rpw, r1 = std::min<i64>(n, r0 + rpw);
-  staged_scatter<VT, 4>(keys, vals, nullptr, r0, r1, F, 64 - pbits, P, T, lds_raw, run, cnt, off, wsum, pkey, pval, prow);
+  staged_scatter<VT, 4>(keys, vals, rs, cs, nullptr, r0, r1, F, 64 - pbits, P, T, lds_raw, run, cnt, off, wsum, pkey, pval,
+                        prow);
 }
 
 // ngrp thread groups (blockDim / ngrp threads each, ngrp <= 4) each aggregate their rows [a, e) of (key, val,
@@ -1025,9 +1032,9 @@ __device__ __forceinline__ void agg_ranges_dense(const u64* __restrict__ pkey, c
       const VT* v = pval + r * F;
       const int sl = k[j] != kEmpty ? ltable_slot(t, k[j], mix64(k[j])) : -1;
       if (sl >= 0) {
-        ltable_add_row<VT, OP>(t, sl, v0[j], v, F, (u64)rw[j]);
+        ltable_add_row<VT, OP>(t, sl, v0[j], v, F, 1, (u64)rw[j]);
       } else {   // rare (the table's probe window is full): the values are re-read from memory
-        row_into_global<VT, OP>(g, k[j], v, F, &meta->ng_part, &meta->sentinel_part, &meta->fail_part, o, rw[j]);
+        row_into_global<VT, OP>(g, k[j], v, F, 1, &meta->ng_part, &meta->sentinel_part, &meta->fail_part, o, rw[j]);
       }
     }
 #pragma unroll
@@ -1137,7 +1144,7 @@ __global__ __launch_bounds__(1024) void agg_bucket_kernel(const u64* __restrict_
     if (threadIdx.x == 0) sb[P2] = (unsigned)nb;
   }
   __syncthreads();
-  staged_scatter<VT, 2>(pkey, pval, prow, r0, r1, F, shift, P2, T, lds_raw, run, cnt, off, wsum, qkey, qval, qrow);
+  staged_scatter<VT, 2>(pkey, pval, F, 1, prow, r0, r1, F, shift, P2, T, lds_raw, run, cnt, off, wsum, qkey, qval, qrow);
   // this workgroup reads back what its own waves stored: drain the stores, then drop this CU's L1 lines
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1438,7 +1445,8 @@ inline long long mid_work_bytes(long long n, int F, int dcap) {
 template <typename VT, int OP>
 int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv, int want_first, void* meta_v, void* glow_v,
                  i64 gcap_low, void* gpart_v, i64 gcap_part, void* gmid_v, i64 gcap_mid, int dcap, void* out_v,
-                 void* work_v, int pbits, int lcap_low, int lcap_part, int low_thr, int mid_thr, hipStream_t st) {
+                 void* work_v, int pbits, int lcap_low, int lcap_part, int low_thr, int mid_thr, i64 rs, i64 cs,
+                 hipStream_t st) {
   AggMeta* meta = reinterpret_cast<AggMeta*>(meta_v);
   // glow / gpart: [key (cap+1) | acc (cap+1)*F | cnt (cap+1) | gid (cap+1)] u64 words, preset by the caller
   auto mk = [&](void* base, i64 cap) {
@@ -1475,7 +1483,8 @@ int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv,
   hipLaunchKernelGGL(agg_sample_gather_kernel, dim3(kSample / 64), dim3(64), 0, st, k, n, sbuf);
   hipLaunchKernelGGL(agg_sample_kernel, dim3(1), dim3(1024), 0, st, sbuf, n, low_thr, mid_thr, meta);
   const int gl = (int)std::min<i64>(1024, std::max<i64>(1, (n + 2047) / 2048));
-  hipLaunchKernelGGL((agg_low_kernel<VT, OP>), dim3(gl), dim3(256), lbytes_low, st, k, v, n, F, lcap_low, glow, meta, o);
+  hipLaunchKernelGGL((agg_low_kernel<VT, OP>), dim3(gl), dim3(256), lbytes_low, st, k, v, n, F, rs, cs, lcap_low, glow,
+                     meta, o);
   if (dcap > 0) {
     const int Gm = mid_groups(n);
     i64* part_nw = reinterpret_cast<i64*>(work_v);
@@ -1487,7 +1496,7 @@ int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv,
     while (scap < 16384 && scap < 2 * dcap) scap <<= 1;
     hipLaunchKernelGGL(agg_mid_dict_kernel, dim3(Gm), dim3(kMidThreads), (size_t)scap * 8, st, k, n, scap,
                        reinterpret_cast<DSlot*>(gmid_v), (u64)(gcap_mid - 1), meta, (i64)dcap, o.reps);
-    hipLaunchKernelGGL((agg_mid_kernel<VT, OP>), dim3(Gm), dim3(kMidThreads), lbytes_mid, st, k, v, n, F, dcap,
+    hipLaunchKernelGGL((agg_mid_kernel<VT, OP>), dim3(Gm), dim3(kMidThreads), lbytes_mid, st, k, v, n, F, rs, cs, dcap,
                        want_first, reinterpret_cast<DSlot*>(gmid_v), (u64)(gcap_mid - 1), meta, o, part_nw, part_acc,
                        part_cnt, part_rmin);
     hipLaunchKernelGGL((agg_mid_reduce_kernel<VT, OP>), dim3((dcap + 63) / 64), dim3(1024), 0, st, Gm, F, dcap,
@@ -1515,7 +1524,7 @@ int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv,
   hipLaunchKernelGGL(agg_hist_kernel, dim3(G), dim3(1024), (size_t)P * 4, st, k, n, rpw, pbits, hist, meta);
   hipLaunchKernelGGL(scan_rows_kernel, dim3(P), dim3(1024), 0, st, hist, G, tot, meta, 1);
   hipLaunchKernelGGL(scan_tot_kernel, dim3(1), dim3(1024), 0, st, tot, P, bstart, meta, 1);
-  hipLaunchKernelGGL((agg_scatter_kernel<VT>), dim3(G), dim3(1024), stage_bytes, st, k, v, n, F, rpw, pbits, T, hist,
+  hipLaunchKernelGGL((agg_scatter_kernel<VT>), dim3(G), dim3(1024), stage_bytes, st, k, v, rs, cs, n, F, rpw, pbits, T, hist,
                      bstart, pkey, pval, prow, meta);
   hipLaunchKernelGGL((agg_bucket_kernel<VT, OP>), dim3(P), dim3(1024), lds_bucket, st, pkey, pval, prow, F, lcap_part,
                      pbits, T2, n, bstart, qkey, qval, qrow, gpart, meta, o);
@@ -1547,11 +1556,12 @@ int nsdb_agg_mid_cap(int F, int want_first) {
   return (163840 - kMidReserve) / (8 * F + 4 + (want_first ? 4 : 0));
 }
 
-// vt: 0 double, 1 int64; op: 0 sum, 1 min, 2 max. dcap 0 disables the MID path.
+// vt: 0 double, 1 int64; op: 0 sum, 1 min, 2 max. dcap 0 disables the MID path. Value (i, f) is vals[i * vrs + f * vcs]
+// (vrs = vcs = 0: row-major [n, F]).
 int nsdb_hash_aggregate(const void* keys, const void* vals, long long n, int F, int vt, int op, int want_inv,
                         int want_first, void* meta, void* glow, long long gcap_low, void* gpart, long long gcap_part,
                         void* gmid, long long gcap_mid, int dcap, void* out, void* work, int pbits, int lcap_low,
-                        int lcap_part, int low_thr, int mid_thr, hipStream_t st) {
+                        int lcap_part, int low_thr, int mid_thr, long long vrs, long long vcs, hipStream_t st) {
   if (n <= 0) return 0;
   if (n >= (1LL << 31)) return (int)hipErrorInvalidValue;
   if (F < 0 || F > 16 || pbits < 0 || pbits > 10) return (int)hipErrorInvalidValue;
@@ -1562,7 +1572,12 @@ int nsdb_hash_aggregate(const void* keys, const void* vals, long long n, int F, 
   if (dcap < 0 || dcap > nsdb_agg_mid_cap(F, want_first)) return (int)hipErrorInvalidValue;
   if (dcap > 0 && (!pow2(gcap_mid) || gcap_mid < 2LL * dcap)) return (int)hipErrorInvalidValue;
   if (dcap == 0) mid_thr = 0;
-#define NSDB_AGG(VT, OP) agg_launch_t<VT, OP>(keys, vals, n, F, want_inv, want_first, meta, glow, gcap_low, gpart, gcap_part, gmid, gcap_mid, dcap, out, work, pbits, lcap_low, lcap_part, low_thr, mid_thr, st)
+  if (F > 0 && (vrs < 0 || vcs < 0)) return (int)hipErrorInvalidValue;
+  if (vrs == 0 && vcs == 0) {   // default: row-major [n, F]
+    vrs = F;
+    vcs = 1;
+  }
+#define NSDB_AGG(VT, OP) agg_launch_t<VT, OP>(keys, vals, n, F, want_inv, want_first, meta, glow, gcap_low, gpart, gcap_part, gmid, gcap_mid, dcap, out, work, pbits, lcap_low, lcap_part, low_thr, mid_thr, vrs, vcs, st)
   if (vt == 0) {
     if (op == 0) return NSDB_AGG(double, OP_SUM);
     if (op == 1) return NSDB_AGG(double, OP_MIN);

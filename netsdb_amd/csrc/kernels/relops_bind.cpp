@@ -19,7 +19,7 @@ int nsdb_agg_mid_cap(int F, int want_first);
 int nsdb_hash_aggregate(const void* keys, const void* vals, long long n, int F, int vt, int op, int want_inv,
                         int want_first, void* meta, void* glow, long long gcap_low, void* gpart, long long gcap_part,
                         void* gmid, long long gcap_mid, int dcap, void* out, void* work, int pbits, int lcap_low,
-                        int lcap_part, int low_thr, int mid_thr, hipStream_t st);
+                        int lcap_part, int low_thr, int mid_thr, long long vrs, long long vcs, hipStream_t st);
 int nsdb_join_insert(const void* keys, long long n, void* tab, long long cap, int* row_slot, unsigned* row_rank,
                      hipStream_t st);
 int nsdb_join_perm(const int* row_slot, const unsigned* row_rank, long long n, const long long* toff, void* tab,
@@ -74,6 +74,7 @@ std::vector<torch::Tensor> hash_aggregate(torch::Tensor keys, c10::optional<torc
   int opc = op == "sum" ? 0 : op == "min" ? 1 : op == "max" ? 2 : -1;
   TORCH_CHECK(opc >= 0, "op must be sum, min or max");
   int F = 0, vt = 0;
+  int64_t vrs = 0, vcs = 0;
   torch::Tensor v;
   auto vdtype = torch::kFloat64;
   if (vals.has_value() && vals->defined() && vals->numel() > 0) {
@@ -82,7 +83,11 @@ std::vector<torch::Tensor> hash_aggregate(torch::Tensor keys, c10::optional<torc
     TORCH_CHECK(v.scalar_type() == torch::kFloat64 || v.scalar_type() == torch::kInt64, "vals must be float64 or int64");
     if (v.dim() == 1) v = v.unsqueeze(1);
     TORCH_CHECK(v.dim() == 2 && v.size(0) == n, "vals must be [n] or [n, F]");
-    v = v.contiguous();
+    // row-major [n, F] or column-major (the transpose of a contiguous [F, n] stack) are read in place
+    const bool colmajor = v.size(1) > 1 && v.stride(0) == 1 && v.stride(1) >= n;
+    if (!colmajor) v = v.contiguous();
+    vrs = v.size(1) > 1 ? v.stride(0) : 1;
+    vcs = v.size(1) > 1 ? v.stride(1) : 1;
     F = (int)v.size(1);
     TORCH_CHECK(F <= 16, "at most 16 value columns");
     vt = v.scalar_type() == torch::kInt64 ? 1 : 0;
@@ -122,7 +127,8 @@ std::vector<torch::Tensor> hash_aggregate(torch::Tensor keys, c10::optional<torc
   rc_ok(nsdb_hash_aggregate(keys.data_ptr(), F ? v.data_ptr() : nullptr, n, F, vt, opc, want_inv ? 1 : 0, want_first ? 1 : 0,
                             meta.data_ptr(), glow.data_ptr(), gcap_low, gpart.data_ptr(), gcap_part,
                             dcap > 0 ? gmid.data_ptr() : nullptr, gcap_mid, dcap, out.data_ptr(), work.data_ptr(), pbits,
-                            (int)lcap_low, (int)lcap_part, (int)thr, (int)mid_thr, stream()),
+                            (int)lcap_low, (int)lcap_part, (int)thr, (int)mid_thr, (long long)vrs, (long long)vcs,
+                            stream()),
         "hash_aggregate");
   auto m = meta.narrow(0, 0, 16).cpu();   // the one host read: group count and path flags
   const ll* mp = LL(m.data_ptr<int64_t>());

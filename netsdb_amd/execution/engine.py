@@ -698,9 +698,29 @@ class QueryEngine:
 
         limit = self._ooc_limit()
         held, size, pspool = [], 0, None
+        # several chunks (a scan split into coalesced batches): each held chunk is pre-reduced on the device when
+        # the next arrives (sum / min / max merge with the same op), so the final reduction concatenates a few
+        # partial groups instead of every row; stops as soon as a chunk does not shrink (high-cardinality keys)
+        prereduce = group_fn is None and op in ("sum", "min", "max")
+
+        def _pre(b):
+            nonlocal prereduce
+            v = b.columns["v"]
+            if not (prereduce and b.n >= (1 << 16) and isinstance(v, torch.Tensor) and v.is_cuda):
+                return b
+            fused = K.group_reduce(b.columns["k"], v, op)
+            if fused is None or len(fused[1]) * 2 > b.n:
+                prereduce = False
+                return b
+            return RecordBatch({"k": fused[0], "v": fused[1]}, len(fused[1]))
+
         for kv in kv_batches:
             if kv is None or kv.n == 0:
                 continue
+            if pspool is None and held and prereduce:
+                size -= held[-1].nbytes()
+                held[-1] = _pre(held[-1])
+                size += held[-1].nbytes()
             if pspool is not None:
                 pspool.add(kv, K.hash_keys(kv.columns["k"], kv.device))
                 continue

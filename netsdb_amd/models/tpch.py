@@ -368,6 +368,12 @@ def _rows_out(names: List[str]):
     return out
 
 
+def _vcols(*cols) -> torch.Tensor:
+    """[n, F] value row of F columns, laid out column-major (the transpose of a contiguous [F, n] stack): each column
+    is copied contiguously and the device group-by reads it in place (relops.hip value strides)."""
+    return torch.stack(cols, 0).t()
+
+
 def _str_keys(*cols):
     """Tuple key of string columns: device columns stay a tuple (hash-kernel group-by on the GPU), host
     lists become one joined string per row (host grouping)."""
@@ -416,7 +422,7 @@ def q01(client, db: str, delta_days: int = 90) -> List[dict]:
     def vals(b):
         q, p, d, t = (_col(b, c).double() for c in ("l_quantity", "l_extendedprice", "l_discount", "l_tax"))
         dp = p * (1 - d)
-        return torch.stack([q, p, dp, dp * (1 + t), d, torch.ones_like(q)], 1)
+        return _vcols(q, p, dp, dp * (1 + t), d, torch.ones_like(q))
 
     agg = _GroupBy(lambda b: _str_keys(_col(b, "l_returnflag"), _col(b, "l_linestatus")), vals,
                    _rows_out(["sum_qty", "sum_base_price", "sum_disc_price", "sum_charge", "sum_disc", "count"]))
@@ -547,7 +553,7 @@ def q12(client, db: str, modes=("MAIL", "SHIP"), date: int = 19940101) -> List[d
 
     def vals(b):
         hi = _isin_str(_col(b, "o_orderpriority"), ["1-URGENT", "2-HIGH"], _dev(b)).double()
-        return torch.stack([hi, 1 - hi], 1)
+        return _vcols(hi, 1 - hi)
 
     agg = _GroupBy(lambda b: _col(b, "l_shipmode"), vals, _rows_out(["high_line_count", "low_line_count"]))
     r = _flat(_run(client, db, "q12_out", agg.set_input(j), "tpch_q12"))
@@ -593,7 +599,7 @@ def q14(client, db: str, date: int = 19950901) -> float:
     def vals(b):
         rev = _col(b, "l_extendedprice").double() * (1 - _col(b, "l_discount").double())
         promo = _like(_col(b, "p_type"), "PROMO%", _dev(b)).double()
-        return torch.stack([rev * promo, rev], 1)
+        return _vcols(rev * promo, rev)
 
     agg = _GroupBy(lambda b: torch.zeros(b.n, dtype=torch.int64, device=_dev(b)), vals, _rows_out(["promo", "total"]))
     r = _flat(_run(client, db, "q14_out", agg.set_input(j), "tpch_q14"))
@@ -616,8 +622,8 @@ def q17(client, db: str, brand: str = "Brand#23", container: str = "MED BOX") ->
     client.create_set(db, "q17_li", None)
     client.execute_computations(WriteSet(db, "q17_li").set_input(j), job_name="tpch_q17_join")
     avg = _GroupBy(lambda b: _col(b, "l_partkey"),
-                   lambda b: torch.stack([_col(b, "l_quantity").double(), torch.ones(b.n, dtype=torch.float64,
-                                                                                      device=_dev(b))], 1),
+                   lambda b: _vcols(_col(b, "l_quantity").double(), torch.ones(b.n, dtype=torch.float64,
+                                                                               device=_dev(b))),
                    _rows_out(["sq", "n"]))
     li = ScanSet(db, "q17_li")
     a = avg.set_input(li)
@@ -647,8 +653,8 @@ def q22(client, db: str, codes=("13", "31", "23", "29", "30", "18", "17")) -> Li
 
     pos = _Filter(lambda b: in_codes(b) & (_col(b, "c_acctbal") > 0)).set_input(ScanSet(db, "customer", Customer))
     avg = _GroupBy(lambda b: torch.zeros(b.n, dtype=torch.int64, device=_dev(b)),
-                   lambda b: torch.stack([_col(b, "c_acctbal").double(), torch.ones(b.n, dtype=torch.float64,
-                                                                                    device=_dev(b))], 1),
+                   lambda b: _vcols(_col(b, "c_acctbal").double(), torch.ones(b.n, dtype=torch.float64,
+                                                                             device=_dev(b))),
                    _rows_out(["s", "n"]))
     r = _flat(_run(client, db, "q22_avg", avg.set_input(pos), "tpch_q22_avg"))
     mean = float(r.columns["s"].sum() / r.columns["n"].sum()) if r is not None else 0.0
@@ -668,8 +674,8 @@ def q22(client, db: str, codes=("13", "31", "23", "29", "30", "18", "17")) -> Li
         return c.substr(0, 2) if isinstance(c, StringColumn) else [s[:2] for s in c]
 
     agg = _GroupBy(cntrycode,
-                   lambda b: torch.stack([torch.ones(b.n, dtype=torch.float64, device=_dev(b)),
-                                          _col(b, "c_acctbal").double()], 1), _rows_out(["numcust", "totacctbal"]))
+                   lambda b: _vcols(torch.ones(b.n, dtype=torch.float64, device=_dev(b)),
+                                    _col(b, "c_acctbal").double()), _rows_out(["numcust", "totacctbal"]))
     r = _flat(_run(client, db, "q22_out", agg.set_input(sel), "tpch_q22"))
     if r is None:
         return []

@@ -20,6 +20,7 @@ tail -2 $O/pytest_dist.log
 echo "[tpch]"
 timeout -k 10 600 python -u scripts/bench_tpch.py --sf 1,10 --queries q01,q02,q03,q04,q06,q12,q13,q14,q17,q22 --json $O/tpch.json > $O/tpch.log 2>&1 || { tail -20 $O/tpch.log; exit 1; }
 grep "^{" $O/tpch.log
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt_tpch -o run --output-format csv -- python3 scripts/bench_tpch.py --sf 10 --queries q01,q12,q03 --rounds 1 --no-check > $O/kt_tpch.log 2>&1 || { tail -5 $O/kt_tpch.log; exit 1; }
 echo "[gpu suite]"
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread --deselect tests/test_distributed_gpu.py::test_tpch_two_ranks_on_one_gpu_vs_pandas > $O/pytest_gpu.log 2>&1 || { tail -60 $O/pytest_gpu.log; exit 1; }
 tail -3 $O/pytest_gpu.log

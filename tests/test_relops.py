@@ -380,3 +380,23 @@ def test_short_string_codes_and_groupby_gpu():
     gid = torch.tensor([uk.index(k) for k in keys])
     ref = torch.zeros(len(uk), 2, dtype=torch.float64).index_add_(0, gid, v.cpu())
     torch.testing.assert_close(agg.cpu(), ref, rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("distinct", [6, 3000, 300_000])
+def test_hash_aggregate_column_major_values(distinct):
+    """A [n, F] value row given column-major (the transpose of a contiguous [F, n] stack) is read in place by every
+    path (LOW / MID / PART) and aggregates exactly like the row-major copy."""
+    g = torch.Generator(device=DEV).manual_seed(distinct)
+    n = 500_000
+    keys = torch.randint(0, distinct, (n,), device=DEV, generator=g) * 3 + 1
+    cols = torch.rand(4, n, device=DEV, dtype=torch.float64, generator=g)
+    vc = cols.t()
+    assert vc.stride() == (1, n)
+    a = _ext.hip().hash_aggregate(keys, vc, "sum", True, 0)
+    b = _ext.hip().hash_aggregate(keys, vc.contiguous(), "sum", True, 0)
+    assert int(a[5][1]) == int(b[5][1]) and int(a[5][2]) == 1
+    oa, ob = torch.argsort(a[0]), torch.argsort(b[0])
+    assert torch.equal(a[0][oa], b[0][ob]) and torch.equal(a[2][oa], b[2][ob]) and torch.equal(a[3][oa], b[3][ob])
+    torch.testing.assert_close(a[1][oa], b[1][ob], rtol=1e-12, atol=1e-9)
+    _check_agg(keys[:50_000], vc[:50_000], "max", _ext.hip().hash_aggregate(keys[:50_000], vc[:50_000], "max", True, 0))
