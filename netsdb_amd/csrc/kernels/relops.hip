@@ -1194,9 +1194,10 @@ __global__ __launch_bounds__(256) void agg_fix_inv_kernel(i64* __restrict__ inv,
 }
 
 // ---------------------------------------------------------------- hash join
-// Table: cap + 1 16-byte slots {key, cnt | pay << 32} (slot cap: the kEmpty key). pay = the build row itself when
-// the key has one build row (the primary-key case), else the start of its CSR run in perm. A probe row is then
-// ONE 16-byte random read (key, count and row together) and, for unique build keys, no second lookup.
+// Table: cap + 1 16-byte slots {key, cnt | pay << 32} (slot cap: the kEmpty key). cnt counts the key's build rows
+// beyond the first (the kEmpty slot: all of them); pay = the build row itself when the key has one build row (the
+// primary-key case), else the start of its CSR run in perm. A probe row is then ONE 16-byte random read (key, count
+// and row together) and, for unique build keys, no second lookup; a build without repeated keys needs no CSR pass.
 struct JSlot {
   u64 key;
   unsigned cnt;
@@ -1205,9 +1206,10 @@ struct JSlot {
 
 // The row that claims a slot (CAS) is its key's rank 0 and stores itself as the payload; each further row of
 // the key takes the next rank with one atomic add on the slot's count of EXTRA rows (a unique-key build does one
-// atomic per row). join_build then turns the counts into totals (+1 per claimed slot) on the device.
+// atomic per row). *ndup counts the rows of rank > 0 (one add per wave): zero means the CSR pass is skipped.
 __global__ __launch_bounds__(256) void join_insert_kernel(const u64* __restrict__ keys, i64 n, JSlot* tab, u64 mask,
-                                                          int* __restrict__ row_slot, unsigned* __restrict__ row_rank) {
+                                                          int* __restrict__ row_slot, unsigned* __restrict__ row_rank,
+                                                          unsigned long long* ndup) {
   for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) {
     const u64 k = keys[i];
     u64 s;
@@ -1230,27 +1232,30 @@ __global__ __launch_bounds__(256) void join_insert_kernel(const u64* __restrict_
       }
     }
     row_slot[i] = (int)s;
+    unsigned r = 0;
     if (claimed) {
       tab[s].pay = (unsigned)i;
-      row_rank[i] = 0;
     } else {
-      const unsigned r = __hip_atomic_fetch_add(&tab[s].cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) +
-                         (k == kEmpty ? 0u : 1u);
+      r = __hip_atomic_fetch_add(&tab[s].cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + (k == kEmpty ? 0u : 1u);
       if (r == 0) tab[s].pay = (unsigned)i;   // the kEmpty slot's first row
-      row_rank[i] = r;
     }
+    row_rank[i] = r;
+    const u64 dups = __ballot(r != 0);
+    if (dups != 0 && (threadIdx.x & 63) == (unsigned)(__ffsll((long long)__ballot(1)) - 1))
+      __hip_atomic_fetch_add(ndup, (unsigned long long)__popcll(dups), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
 // Keys with more than one build row: perm[toff[slot] + rank] = row (CSR over the slots) and the slot's payload
-// becomes its run start. Unique keys (the primary-key case) only read their slot's count.
+// becomes its run start. Unique keys only read their slot's count. Launched only when the build repeated a key.
 __global__ __launch_bounds__(256) void join_perm_kernel(const int* __restrict__ row_slot,
                                                         const unsigned* __restrict__ row_rank, i64 n,
-                                                        const i64* __restrict__ toff, JSlot* tab,
+                                                        const i64* __restrict__ toff, JSlot* tab, u64 mask,
                                                         i64* __restrict__ perm) {
+  const u64 sent = mask + 1;
   for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) {
     const int s = row_slot[i];
-    if (tab[s].cnt <= 1) continue;   // unique key: its payload is already the row
+    if (tab[s].cnt + ((u64)s != sent ? 1u : 0u) <= 1) continue;   // one build row: its payload is already the row
     const unsigned r = row_rank[i];
     const i64 o = toff[s];
     perm[o + r] = i;
@@ -1290,15 +1295,15 @@ __global__ __launch_bounds__(256) void join_probe_kernel(const u64* __restrict__
     const i64 i = t0 + j * 256 + threadIdx.x;
     if (i >= m) continue;
     unsigned c = 0, p = 0;
-    if (e[j].key == k[j]) {
-      c = e[j].cnt;
+    if (e[j].key == k[j]) {   // total rows: the extras + the claiming row (the kEmpty slot counts all of its rows)
+      c = e[j].cnt + (k[j] != kEmpty ? 1u : 0u);
       p = e[j].pay;
     } else if (e[j].key != kEmpty && k[j] != kEmpty) {
       u64 s = (sl[j] + 1) & mask;
       for (;;) {
         const JSlot x = tab[s];
         if (x.key == k[j]) {
-          c = x.cnt;
+          c = x.cnt + 1u;
           p = x.pay;
           break;
         }
@@ -1593,20 +1598,21 @@ int nsdb_hash_aggregate(const void* keys, const void* vals, long long n, int F, 
 
 // Join build over n int64 keys: tab [cap + 1] 16-byte slots preset {kEmpty, 0, 0} (cap a power of two >= 2n).
 int nsdb_join_insert(const void* keys, long long n, void* tab, long long cap, int* row_slot, unsigned* row_rank,
-                     hipStream_t st) {
+                     unsigned long long* ndup, hipStream_t st) {
   if (n <= 0) return 0;
   if (cap <= 0 || (cap & (cap - 1)) != 0 || cap < 2 * n || cap >= (1LL << 31)) return (int)hipErrorInvalidValue;
   const unsigned g = (unsigned)std::min<long long>(4096, (n + 255) / 256);
   hipLaunchKernelGGL(join_insert_kernel, dim3(g), dim3(256), 0, st, (const u64*)keys, n, (JSlot*)tab, (u64)(cap - 1),
-                     row_slot, row_rank);
+                     row_slot, row_rank, ndup);
   return (int)hipGetLastError();
 }
 
 int nsdb_join_perm(const int* row_slot, const unsigned* row_rank, long long n, const long long* toff, void* tab,
-                   long long* perm, hipStream_t st) {
+                   long long cap, long long* perm, hipStream_t st) {
   if (n <= 0) return 0;
   const unsigned g = (unsigned)std::min<long long>(4096, (n + 255) / 256);
-  hipLaunchKernelGGL(join_perm_kernel, dim3(g), dim3(256), 0, st, row_slot, row_rank, n, toff, (JSlot*)tab, perm);
+  hipLaunchKernelGGL(join_perm_kernel, dim3(g), dim3(256), 0, st, row_slot, row_rank, n, toff, (JSlot*)tab,
+                     (u64)(cap - 1), perm);
   return (int)hipGetLastError();
 }
 
