@@ -400,7 +400,8 @@ constexpr int kPreF = 1;     // value columns loaded with the keys (the rest at 
 // Row (key, values) batch of one thread: kU rows of a 256*kU-row tile, loaded together. Value (i, f) of the input
 // is vals[i * rs + f * cs]: row-major [n, F] (rs = F, cs = 1) or column-major (rs = 1, cs = column pitch), so a
 // caller's stacked columns are read in place.
-template <typename VT>
+// NT: non-temporal loads (streamed once; they do not push a kernel's L2-resident lookup table out of the L2).
+template <typename VT, bool NT = false>
 struct RowBatch {
   u64 k[kU];
   VT v[kU][kPreF];
@@ -409,9 +410,16 @@ struct RowBatch {
 #pragma unroll
     for (int j = 0; j < kU; ++j) {
       const i64 i = t0 + (i64)j * nthr + threadIdx.x;
-      k[j] = i < n ? keys[i] : kEmpty;
+      if constexpr (NT) {
+        k[j] = i < n ? __builtin_nontemporal_load(keys + i) : kEmpty;
 #pragma unroll
-      for (int f = 0; f < kPreF; ++f) v[j][f] = (i < n && f < F) ? vals[i * rs + f * cs] : VT(0);
+        for (int f = 0; f < kPreF; ++f)
+          v[j][f] = (i < n && f < F) ? __builtin_nontemporal_load(vals + i * rs + f * cs) : VT(0);
+      } else {
+        k[j] = i < n ? keys[i] : kEmpty;
+#pragma unroll
+        for (int f = 0; f < kPreF; ++f) v[j][f] = (i < n && f < F) ? vals[i * rs + f * cs] : VT(0);
+      }
     }
   }
 };
@@ -583,7 +591,7 @@ __global__ __launch_bounds__(kMidThreads) void agg_mid_dict_kernel(const u64* __
 #pragma unroll
     for (int j = 0; j < kU; ++j) {
       const i64 i = b0 + (i64)j * kMidThreads + threadIdx.x;
-      kk[j] = i < n ? keys[i] : kEmpty;
+      kk[j] = i < n ? __builtin_nontemporal_load(keys + i) : kEmpty;
     }
   };
   i64 t0 = (i64)blockIdx.x * TILE;
@@ -645,7 +653,7 @@ __global__ __launch_bounds__(kMidThreads) void agg_mid_kernel(const u64* __restr
   constexpr int TILE = kMidThreads * kU;
   const i64 tstride = (i64)gridDim.x * TILE;
   int maxid = -1, it = 0;
-  RowBatch<VT> cur, nxt;
+  RowBatch<VT, true> cur, nxt;   // keys / values stream past the L2-resident dictionary
   i64 t0 = (i64)blockIdx.x * TILE;
   if (t0 < n) cur.load(keys, vals, t0, n, F, kMidThreads, rs, cs);
   for (; t0 < n; t0 += tstride, ++it) {
@@ -1499,7 +1507,9 @@ int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv,
     const size_t lbytes_mid = (size_t)dcap * (8 * F + 4 + (want_first ? 4 : 0)) + kMidReserve;
     int scap = 1024;   // LDS key set of the dictionary build: <= 1/2 full at dcap keys, <= 128 KiB
     while (scap < 16384 && scap < 2 * dcap) scap <<= 1;
-    hipLaunchKernelGGL(agg_mid_dict_kernel, dim3(Gm), dim3(kMidThreads), (size_t)scap * 8, st, k, n, scap,
+    // fewer, longer workgroups for the build: each costs one device-scope CAS per distinct key it sees (~7 G/s on
+    // this part), so 64 of them trade read parallelism for 4x fewer CAS than one per CU
+    hipLaunchKernelGGL(agg_mid_dict_kernel, dim3(std::min(Gm, 64)), dim3(kMidThreads), (size_t)scap * 8, st, k, n, scap,
                        reinterpret_cast<DSlot*>(gmid_v), (u64)(gcap_mid - 1), meta, (i64)dcap, o.reps);
     hipLaunchKernelGGL((agg_mid_kernel<VT, OP>), dim3(Gm), dim3(kMidThreads), lbytes_mid, st, k, v, n, F, rs, cs, dcap,
                        want_first, reinterpret_cast<DSlot*>(gmid_v), (u64)(gcap_mid - 1), meta, o, part_nw, part_acc,
