@@ -62,8 +62,9 @@ constexpr int kMetaWords = 16 + 4096;   // AggMeta + the sampled keys (relops.hi
 // meaningful with want_first, which otherwise lets the partition passes skip row ids),
 // inv [n] i64 (or empty), status): status = [g, path (0 LOW, 1 PART, 2 MID), ok (0: the PART table overflowed;
 // outputs invalid, fall back), distinct keys in the 4096-row sample].
-// low_threshold / mid_threshold: largest estimated group count for the LOW / MID path (0: automatic; a negative
-// mid_threshold disables MID).
+// low_threshold: largest estimated group count for the LOW path (0: automatic). mid_threshold > 0 opts in to the MID
+// path (dense LDS arrays + a global key dictionary) up to that many estimated groups (capped by what the LDS holds);
+// 0 (the default) leaves it off: measured slower than PART at 10 K keys / 16 M rows (profiles/r4_relops).
 std::vector<torch::Tensor> hash_aggregate(torch::Tensor keys, c10::optional<torch::Tensor> vals, const std::string& op,
                                           bool want_inv, int64_t low_threshold, bool want_first, int64_t mid_threshold) {
   TORCH_CHECK(keys.is_cuda(), "keys must be a GPU tensor");
@@ -110,10 +111,10 @@ std::vector<torch::Tensor> hash_aggregate(torch::Tensor keys, c10::optional<torc
   // overflow table of the PART path (keys whose LDS probe window filled): a miss-sized estimate only
   const int64_t gcap_part = std::max<int64_t>(4096, std::min<int64_t>(pow2_at_least(2 * n), int64_t(1) << 17));
   const int64_t thr = low_threshold > 0 ? low_threshold : lcap_low / 4;
-  // MID: dense LDS arrays of up to dcap groups (relops.hip agg_mid_kernel), dictionary <= 1/2 full; the automatic
-  // threshold is dcap itself (the ids are exact: only more real groups than dcap send the work to PART)
-  const int dcap = mid_threshold < 0 ? 0 : nsdb_agg_mid_cap(F, want_first ? 1 : 0);
-  const int64_t mid_thr = dcap == 0 ? 0 : (mid_threshold > 0 ? std::min<int64_t>(mid_threshold, dcap) : dcap);
+  // MID (opt-in): dense LDS arrays of up to dcap groups (relops.hip agg_mid_kernel), dictionary <= 1/2 full (the ids
+  // are exact: only more real groups than dcap send the work to PART)
+  const int dcap = mid_threshold <= 0 ? 0 : nsdb_agg_mid_cap(F, want_first ? 1 : 0);
+  const int64_t mid_thr = dcap == 0 ? 0 : std::min<int64_t>(mid_threshold, dcap);
   const int64_t gcap_mid = dcap > 0 ? pow2_at_least(2 * (int64_t)dcap) : 0;
 
   auto meta = torch::empty({kMetaWords}, i64);
