@@ -92,6 +92,11 @@ class PartitionedBuild:
         self.hash_col = hash_col
 
 
+# NSDB_STAGE_SYNC=1: every stage is bracketed by device syncs and logged here (scripts/bench_tpch.py --stage-times)
+STAGE_SYNC = bool(int(__import__("os").environ.get("NSDB_STAGE_SYNC", "0") or 0))
+STAGE_LOG: List[dict] = []
+
+
 class JobStats(dict):
     pass
 
@@ -163,11 +168,18 @@ class QueryEngine:
         return atoms, plan.computations, plan.tcap
 
     def _timed_stage(self, st, state, stats, job_name):
+        sync = STAGE_SYNC and torch.cuda.is_available() and self.device.type == "cuda"
+        if sync:   # profiling: device time per stage (serialises the stream at stage boundaries)
+            torch.cuda.synchronize(self.device)
         ts = time.perf_counter()
         with self.tracer.span(f"stage{st.id}", job=job_name, sink=st.sink.get("kind")):
             n = self._run_stage(st, state)
-        stats["stages"].append({"id": st.id, "desc": st.describe(), "rows_in": n,
-                                "seconds": time.perf_counter() - ts})
+        if sync:
+            torch.cuda.synchronize(self.device)
+        rec = {"id": st.id, "desc": st.describe(), "rows_in": n, "seconds": time.perf_counter() - ts}
+        stats["stages"].append(rec)
+        if sync:
+            STAGE_LOG.append(dict(rec, job=job_name))
         return n
 
     def _run_adaptive(self, atoms, state, stats, job_name):

@@ -60,6 +60,8 @@ def main():
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--json", default=None)
     ap.add_argument("--host-profile", default=None, help="directory: cProfile of one timed run per query")
+    ap.add_argument("--stage-times", action="store_true",
+                    help="one extra run per query with device syncs at stage boundaries: per-stage seconds in the JSON")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     queries = a.queries.split(",")
@@ -89,6 +91,16 @@ def main():
                 got = fn(c, "tpch")
                 torch.cuda.synchronize()
                 ts.append(time.perf_counter() - t0)
+            stage_times = None
+            if a.stage_times:
+                from netsdb_amd.execution import engine as E
+
+                E.STAGE_SYNC = True
+                del E.STAGE_LOG[:]
+                fn(c, "tpch")
+                E.STAGE_SYNC = False
+                stage_times = [{"job": r["job"], "stage": r["desc"][:160], "ms": round(1e3 * r["seconds"], 3)}
+                               for r in E.STAGE_LOG]
             if a.host_profile:
                 import cProfile
                 import pstats
@@ -114,6 +126,10 @@ def main():
                    "pandas_s": None if frames is None else round(t_ref, 2)}
             out["results"].append(row)
             print(json.dumps(row), flush=True)
+            if stage_times is not None:
+                out.setdefault("stage_times", {})[f"sf{sf:g}_{q}"] = stage_times
+                print(json.dumps({"stages": q, "sf": sf, "ms": [s["ms"] for s in stage_times],
+                                  "total_ms": round(sum(s["ms"] for s in stage_times), 2)}), flush=True)
             if ok is False:
                 print(json.dumps({"mismatch": q, "got": str(got)[:400], "ref": str(ref)[:400]}), flush=True)
         del c, tables, frames
