@@ -168,14 +168,14 @@ class QueryEngine:
         return atoms, plan.computations, plan.tcap
 
     def _timed_stage(self, st, state, stats, job_name):
-        sync = STAGE_SYNC and torch.cuda.is_available() and self.device.type == "cuda"
+        sync = STAGE_SYNC and torch.cuda.is_available()
         if sync:   # profiling: device time per stage (serialises the stream at stage boundaries)
-            torch.cuda.synchronize(self.device)
+            torch.cuda.synchronize()
         ts = time.perf_counter()
         with self.tracer.span(f"stage{st.id}", job=job_name, sink=st.sink.get("kind")):
             n = self._run_stage(st, state)
         if sync:
-            torch.cuda.synchronize(self.device)
+            torch.cuda.synchronize()
         rec = {"id": st.id, "desc": st.describe(), "rows_in": n, "seconds": time.perf_counter() - ts}
         stats["stages"].append(rec)
         if sync:
