@@ -373,8 +373,10 @@ class UserSet:
         yield from self.shared_batches(device)
 
     # resident device pages merged per scanned batch (bytes): 64 MiB pages are a storage / spill unit, not a good
-    # kernel size on a 288 GB GPU; pages cut from one loaded batch are merged back without a copy
-    SCAN_COALESCE_BYTES = 4 << 30
+    # kernel size on a 288 GB GPU; pages cut from one loaded batch are merged back without a copy. 16 GiB keeps a
+    # TPC-H SF 10 lineitem scan one batch (one launch per operator instead of three; its intermediates stay far
+    # below the engine's out-of-core limit, a quarter of the device budget)
+    SCAN_COALESCE_BYTES = 16 << 30
     COALESCE_ANY_DEVICE = False      # tests: run the merge on CPU pages too
 
     def _coalesce_runs(self, pages, device) -> List[Tuple[int, int]]:
