@@ -166,8 +166,9 @@ std::vector<torch::Tensor> join_build(torch::Tensor keys) {
   TORCH_CHECK(n < (int64_t(1) << 29), "join_build: at most 2^29 build rows per table");
   const int64_t cap = pow2_at_least(std::max<int64_t>(1024, 2 * n));
   auto i64 = keys.options().dtype(torch::kInt64);
-  // every slot {kEmpty, 0}: one broadcast copy
-  auto tab = torch::tensor({std::numeric_limits<int64_t>::min(), int64_t(0)}, i64).expand({cap + 1, 2}).contiguous();
+  // every slot {kEmpty, 0} (two fills: a device tensor built from host values would be a pageable, blocking copy)
+  auto tab = torch::zeros({cap + 1, 2}, i64);
+  tab.select(1, 0).fill_(std::numeric_limits<int64_t>::min());
   auto row_slot = torch::empty({n}, keys.options().dtype(torch::kInt32));
   auto row_rank = torch::empty({n}, keys.options().dtype(torch::kInt32));
   auto ndup = torch::zeros({1}, i64);
