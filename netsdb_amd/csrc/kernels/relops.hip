@@ -1254,20 +1254,53 @@ __global__ __launch_bounds__(256) void join_insert_kernel(const u64* __restrict_
   }
 }
 
-// Keys with more than one build row: perm[toff[slot] + rank] = row (CSR over the slots) and the slot's payload
-// becomes its run start. Unique keys only read their slot's count. Launched only when the build repeated a key.
+// Runs of the keys with more than one build row, with no scan over the slots and no host decision: every slot
+// whose key repeated takes a run of perm from one bump counter (one atomic per wave, lanes prefix-summed by
+// shuffles), moves its claiming row (the payload) to the run's first entry and makes the run start its payload.
+// Both kernels return at once when the insert saw no repeated key (*ndup == 0).
+__global__ __launch_bounds__(256) void join_runs_kernel(JSlot* tab, u64 mask, const unsigned long long* ndup,
+                                                        unsigned long long* bump, i64* __restrict__ perm) {
+  if (*ndup == 0) return;
+  const u64 sent = mask + 1;
+  const int lane = threadIdx.x & 63;
+  for (i64 b = (i64)blockIdx.x * blockDim.x; b <= (i64)sent; b += (i64)gridDim.x * blockDim.x) {
+    const i64 s = b + threadIdx.x;
+    unsigned tot = 0, pay = 0;
+    if (s <= (i64)sent) {
+      const JSlot e = tab[s];
+      tot = e.key == kEmpty && (u64)s != sent ? 0u : e.cnt + ((u64)s != sent ? 1u : 0u);
+      pay = e.pay;
+      if (tot <= 1) tot = 0;
+    }
+    unsigned x = tot;   // inclusive prefix over the wave
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const unsigned y = __shfl_up(x, d, 64);
+      if (lane >= d) x += y;
+    }
+    const unsigned wtot = __shfl(x, 63, 64);
+    unsigned long long base = 0;
+    if (lane == 63 && wtot) base = __hip_atomic_fetch_add(bump, (unsigned long long)wtot, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+    base = __shfl(base, 63, 64);
+    if (tot) {
+      const i64 o = (i64)base + (x - tot);
+      perm[o] = (i64)pay;              // the claiming row is rank 0
+      tab[s].pay = (unsigned)o;
+    }
+  }
+}
+
+// rows of rank > 0: perm[run start + rank] = row
 __global__ __launch_bounds__(256) void join_perm_kernel(const int* __restrict__ row_slot,
                                                         const unsigned* __restrict__ row_rank, i64 n,
-                                                        const i64* __restrict__ toff, JSlot* tab, u64 mask,
+                                                        const unsigned long long* ndup, const JSlot* tab,
                                                         i64* __restrict__ perm) {
-  const u64 sent = mask + 1;
+  if (*ndup == 0) return;
   for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) {
-    const int s = row_slot[i];
-    if (tab[s].cnt + ((u64)s != sent ? 1u : 0u) <= 1) continue;   // one build row: its payload is already the row
     const unsigned r = row_rank[i];
-    const i64 o = toff[s];
-    perm[o + r] = i;
-    if (r == 0) tab[s].pay = (unsigned)o;
+    if (r == 0) continue;
+    perm[(i64)tab[row_slot[i]].pay + r] = i;
   }
 }
 
@@ -1617,12 +1650,15 @@ int nsdb_join_insert(const void* keys, long long n, void* tab, long long cap, in
   return (int)hipGetLastError();
 }
 
-int nsdb_join_perm(const int* row_slot, const unsigned* row_rank, long long n, const long long* toff, void* tab,
-                   long long cap, long long* perm, hipStream_t st) {
+// CSR runs of the repeated keys (device-guarded by *ndup; bump: one zeroed u64).
+int nsdb_join_perm(const int* row_slot, const unsigned* row_rank, long long n, const unsigned long long* ndup,
+                   unsigned long long* bump, void* tab, long long cap, long long* perm, hipStream_t st) {
   if (n <= 0) return 0;
+  const unsigned gs = (unsigned)std::min<long long>(4096, (cap + 1 + 255) / 256);
+  hipLaunchKernelGGL(join_runs_kernel, dim3(gs), dim3(256), 0, st, (JSlot*)tab, (u64)(cap - 1), ndup, bump, perm);
   const unsigned g = (unsigned)std::min<long long>(4096, (n + 255) / 256);
-  hipLaunchKernelGGL(join_perm_kernel, dim3(g), dim3(256), 0, st, row_slot, row_rank, n, toff, (JSlot*)tab,
-                     (u64)(cap - 1), perm);
+  hipLaunchKernelGGL(join_perm_kernel, dim3(g), dim3(256), 0, st, row_slot, row_rank, n, ndup, (const JSlot*)tab,
+                     perm);
   return (int)hipGetLastError();
 }
 

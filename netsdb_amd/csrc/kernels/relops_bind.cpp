@@ -22,8 +22,8 @@ int nsdb_hash_aggregate(const void* keys, const void* vals, long long n, int F, 
                         int lcap_part, int low_thr, int mid_thr, long long vrs, long long vcs, hipStream_t st);
 int nsdb_join_insert(const void* keys, long long n, void* tab, long long cap, int* row_slot, unsigned* row_rank,
                      unsigned long long* ndup, hipStream_t st);
-int nsdb_join_perm(const int* row_slot, const unsigned* row_rank, long long n, const long long* toff, void* tab,
-                   long long cap, long long* perm, hipStream_t st);
+int nsdb_join_perm(const int* row_slot, const unsigned* row_rank, long long n, const unsigned long long* ndup,
+                   unsigned long long* bump, void* tab, long long cap, long long* perm, hipStream_t st);
 long long nsdb_join_tiles(long long m);
 int nsdb_join_probe(const void* keys, long long m, const void* tab, long long cap, unsigned* cnt, unsigned* pay,
                     long long* tile_sum, hipStream_t st);
@@ -157,8 +157,8 @@ std::vector<torch::Tensor> hash_aggregate(torch::Tensor keys, c10::optional<torc
   return {reps, aggs, cnt, first, inv, status};
 }
 
-// Join build: returns (table [cap+1, 2] i64 of 16-byte slots {key, cnt | pay << 32}, perm [n] i64 — empty when no
-// build key repeats: every payload is then the build row itself).
+// Join build: returns (table [cap+1, 2] i64 of 16-byte slots {key, cnt | pay << 32}, perm [n] i64: the CSR runs of
+// repeated keys; untouched when no key repeats, every payload being the build row itself). No host read.
 std::vector<torch::Tensor> join_build(torch::Tensor keys) {
   TORCH_CHECK(keys.is_cuda() && keys.scalar_type() == torch::kInt64 && keys.dim() == 1, "keys: 1-D int64 GPU tensor");
   keys = keys.contiguous();
@@ -171,22 +171,16 @@ std::vector<torch::Tensor> join_build(torch::Tensor keys) {
   tab.select(1, 0).fill_(std::numeric_limits<int64_t>::min());
   auto row_slot = torch::empty({n}, keys.options().dtype(torch::kInt32));
   auto row_rank = torch::empty({n}, keys.options().dtype(torch::kInt32));
-  auto ndup = torch::zeros({1}, i64);
+  auto ctr = torch::zeros({2}, i64);   // [repeated-key rows, run bump counter]
   rc_ok(nsdb_join_insert(keys.data_ptr(), n, tab.data_ptr(), cap, row_slot.data_ptr<int>(),
                          reinterpret_cast<unsigned*>(row_rank.data_ptr<int>()),
-                         reinterpret_cast<unsigned long long*>(ndup.data_ptr<int64_t>()), stream()),
+                         reinterpret_cast<unsigned long long*>(ctr.data_ptr<int64_t>()), stream()),
         "join_insert");
-  if (ndup.item<int64_t>() == 0) return {tab, torch::empty({0}, i64)};   // unique build keys (one host read)
-  // insert counted the EXTRA rows of each key: + 1 per claimed slot gives the totals (the kEmpty slot, cap,
-  // counted all its rows); the table keeps the extras (join_probe adds the claiming row)
-  auto tcnt = tab.view(torch::kInt32).select(1, 2);   // the cnt word of every slot (strided view)
-  auto claimed = tab.select(1, 0).narrow(0, 0, cap).ne(std::numeric_limits<int64_t>::min());
-  auto tot = tcnt.to(torch::kInt64);
-  tot.narrow(0, 0, cap).add_(claimed);
-  auto toff = torch::cumsum(tot, 0).sub_(tot);
+  // the table keeps each key's EXTRA-row count (join_probe adds the claiming row)
   auto perm = torch::empty({n}, i64);
-  rc_ok(nsdb_join_perm(row_slot.data_ptr<int>(), reinterpret_cast<const unsigned*>(row_rank.data_ptr<int>()), n,
-                       LL(toff.data_ptr<int64_t>()), tab.data_ptr(), cap, LL(perm.data_ptr<int64_t>()), stream()),
+  auto* c = reinterpret_cast<unsigned long long*>(ctr.data_ptr<int64_t>());
+  rc_ok(nsdb_join_perm(row_slot.data_ptr<int>(), reinterpret_cast<const unsigned*>(row_rank.data_ptr<int>()), n, c,
+                       c + 1, tab.data_ptr(), cap, LL(perm.data_ptr<int64_t>()), stream()),
         "join_perm");
   return {tab, perm};
 }
