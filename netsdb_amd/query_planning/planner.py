@@ -203,9 +203,9 @@ class AdaptivePlanner:
          these stages produce the statistics the join decisions need;
       2. otherwise the cheapest source runs and builds the first unbuilt join it reaches (the smaller
          side builds, judged on measured sizes where known);
-      3. a pipeline that has already probed a join and would build another is abandoned and its
-         source penalised (cost x1000), so the huge post-join table is not built (the reference's
-         "met a join sink with probing" rule).
+      3. a pipeline that has already probed a join and would build another stops there and materialises
+         its output (the reference's "met a join sink with probing" rule abandons it instead): the next
+         decision sees that set's measured size and builds the join from the smaller side.
     """
 
     PENALTY = 1000.0
@@ -311,6 +311,15 @@ class AdaptivePlanner:
                     probed = True
                     ts, c = name, None
                     continue
+                if allow_build and probed and not force:
+                    # a probe-then-build pipeline stops at the join and materialises what it produced: the
+                    # post-probe set becomes a source with a MEASURED size, and the next decision builds this
+                    # join from whichever side is smaller (TPC-H Q03: 1.4 M orders x customer rows instead of
+                    # 32 M lineitem rows). The reference abandons such pipelines; measuring first keeps the
+                    # small-side choice without building a post-join table blind.
+                    st.sink = {"kind": "materialize", "ts": ts}
+                    info["then"] = [(ts, c)]
+                    return st, info
                 if not allow_build or (probed and not force):
                     return None, info
                 if self.world_size == 1:
