@@ -107,9 +107,10 @@ def test_pre_compile_then_execute(tmp_path):
     assert len(_rows(c, "o3")) == 8
 
 
-def test_penalised_probe_then_build_pipeline(tmp_path):
-    """A pipeline that probed one join and reaches an unbuilt second join is abandoned and penalised:
-    the 3-way chain still runs, each join building on its smaller input."""
+def test_probe_then_build_pipeline_materialises_and_builds_the_measured_side(tmp_path):
+    """Q03's chain customer -> orders -> lineitem: the orders pipeline probes the customer build and reaches the
+    unbuilt orders x lineitem join; it materialises its (small) output there, and that measured set builds the
+    join, so the large lineitem scan only probes."""
     from netsdb_amd.models import tpch
 
     t = tpch.generate(0.002, seed=3)
@@ -118,3 +119,6 @@ def test_penalised_probe_then_build_pipeline(tmp_path):
     got = tpch.QUERIES["q03"](c, "tpch")
     ref = tpch.reference("q03", t)
     assert len(got) == len(ref)
+    descs = [st.describe() for st in c.engine.last_plan.stages]
+    assert descs[1].endswith("=> materialize") and descs[2].startswith("stage 2: mat:")
+    assert descs[2].endswith("join_build (local)") and "JOIN" in descs[3] and "join_build" not in descs[3]
