@@ -502,30 +502,21 @@ def q03(client, db: str, segment: str = "BUILDING", date: int = 19950315, k: int
             for a, b_, c, v in zip(ok_[order].tolist(), od[order].tolist(), sp[order].tolist(), rev[order].tolist())]
 
 
-def _second_key(b):
-    """Second column of a two-column group key (device runs keep the columns; host runs group into (a, b) tuples)."""
-    return _col(b, "k1") if "k1" in b.columns else [k[1] for k in _col(b, "k0")]
-
-
 def q04(client, db: str, date: int = 19930701) -> List[dict]:
-    """Order priority checking (Query04.h): orders in [date, date+3mo) having a late lineitem.
-
-    EXISTS as a semi-join: the quarter's orders (the small side, built) are probed by the late lineitems, the
-    matching (order, priority) pairs are made distinct by a group-by, and the distinct orders are counted per
-    priority. (The first version grouped every late lineitem by order key before the join: a 38 M-row, 14 M-group
-    aggregation at SF 10.)"""
+    """Order priority checking (Query04.h): orders in [date, date+3mo) having a late lineitem."""
     end = date + 300 if date % 10000 < 1000 else date + 10000 - 900   # +3 months on yyyymmdd
     late = _Filter(lambda b: _col(b, "l_commitdate") < _col(b, "l_receiptdate")).set_input(ScanSet(db, "lineitem", LineItem))
+    # EXISTS -> distinct late orderkeys (aggregate), then join with the orders of the quarter
+    dist = _GroupBy(lambda b: _col(b, "l_orderkey"), lambda b: torch.ones(b.n, 1, dtype=torch.float64, device=_dev(b)),
+                    _rows_out(["n"]))
     os_ = _Filter(lambda b: (_col(b, "o_orderdate") >= date) & (_col(b, "o_orderdate") < end)).set_input(
         ScanSet(db, "orders", Order))
-    j = _EqJoin(2, [(0, "o_orderkey", 1, "l_orderkey")], _pick([["o_orderkey", "o_orderpriority"], []]))
+    j = _EqJoin(2, [(0, "o_orderkey", 1, "k0")], _pick([["o_orderpriority"], []]))
     j.set_input(0, os_)
-    j.set_input(1, late)
-    dist = _GroupBy(lambda b: (_col(b, "o_orderkey"), _col(b, "o_orderpriority")),
-                    lambda b: torch.ones(b.n, 1, dtype=torch.float64, device=_dev(b)), _rows_out(["n"]))
-    cnt = _GroupBy(_second_key,
+    j.set_input(1, dist.set_input(late))
+    cnt = _GroupBy(lambda b: _col(b, "o_orderpriority"),
                    lambda b: torch.ones(b.n, 1, dtype=torch.float64, device=_dev(b)), _rows_out(["order_count"]))
-    r = _flat(_run(client, db, "q04_out", cnt.set_input(dist.set_input(j)), "tpch_q04"))
+    r = _flat(_run(client, db, "q04_out", cnt.set_input(j), "tpch_q04"))
     if r is None:
         return []
     return sorted(({"o_orderpriority": p, "order_count": int(c)} for p, c in
