@@ -113,7 +113,7 @@ def main():
                 torch.cuda.synchronize()
                 pr.disable()
                 with open(os.path.join(a.host_profile, f"{q}_sf{sf:g}.txt"), "w") as f:
-                    pstats.Stats(pr, stream=f).sort_stats("tottime").print_stats(40)
+                    pstats.Stats(pr, stream=f).sort_stats("cumulative").print_stats(60)
             ok = None
             if frames is not None:
                 t0 = time.perf_counter()
