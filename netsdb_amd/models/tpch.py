@@ -309,10 +309,9 @@ def _like(strings, pattern: str, device, negate: bool = False) -> torch.Tensor:
 
 
 def _dev(b: RecordBatch):
-    for v in b.columns.values():
-        if isinstance(v, torch.Tensor):
-            return v.device
-    return torch.device("cpu")
+    """The batch's device (string and nested columns count: Q12's join output holds only string columns, and a
+    CPU answer here sent its value rows, and so its group-by, to the host)."""
+    return b.device
 
 
 class _Filter(SelectionComp):
