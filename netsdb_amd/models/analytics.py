@@ -33,10 +33,7 @@ from ..utils.sampler import fraction_for_sample_size, randomize_in_place
 
 
 def _dev(b: RecordBatch):
-    for v in b.columns.values():
-        if isinstance(v, torch.Tensor):
-            return v.device
-    return torch.device("cpu")
+    return b.device   # tensor, string and nested columns all count
 
 
 def _run_to_batch(client, db: str, out: str, comp, job: str) -> Optional[RecordBatch]:
