@@ -203,6 +203,22 @@ LAZY_TAKE_MIN_COLS = 4
 LAZY_TAKE_ANY_DEVICE = os.environ.get("NSDB_LAZY_TAKE") == "1"   # tests: the lazy path on CPU batches too
 
 
+class _LazyView:
+    """values() / items() of LazyTakeColumns: re-iterable, each column gathered when the iteration reaches it."""
+
+    __slots__ = ("_d", "_items")
+
+    def __init__(self, d, items: bool):
+        self._d, self._items = d, items
+
+    def __iter__(self):
+        d = self._d
+        return ((k, d[k]) for k in d.keys()) if self._items else (d[k] for k in d.keys())
+
+    def __len__(self):
+        return len(self._d.keys())
+
+
 class LazyTakeColumns(dict):
     """The columns of a row selection, gathered from ``src`` on first access and cached. Behaves as the dict of
     every column (iteration, items(), values(), dict(...) and ** materialise what they touch); columns set or
@@ -253,10 +269,10 @@ class LazyTakeColumns(dict):
         return len(self.keys())
 
     def values(self):
-        return [self[k] for k in self.keys()]
+        return _LazyView(self, False)     # gathers as it iterates (a loop that stops early gathers no more)
 
     def items(self):
-        return [(k, self[k]) for k in self.keys()]
+        return _LazyView(self, True)
 
     def get(self, k, default=None):
         return self[k] if k in self else default
@@ -316,7 +332,10 @@ class RecordBatch:
     def device(self) -> torch.device:
         from .nested import NestedColumn
 
-        for c in self.columns.values():
+        cols = self.columns
+        if isinstance(cols, LazyTakeColumns):
+            cols = cols._src                 # a row selection lives where its source does: nothing gathered to answer
+        for c in cols.values():
             if isinstance(c, (torch.Tensor, StringColumn, NestedColumn)):
                 return c.device
         return torch.device("cpu")

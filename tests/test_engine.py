@@ -283,3 +283,18 @@ def test_lazy_take_nbytes_and_storage_do_not_gather(monkeypatch, tmp_path):
     s = c.storage.get_set("d", "s")
     s.add_batch(t)
     assert all(type(p.batch.columns) is dict for p in s.pages)
+
+
+def test_lazy_take_device_and_values_gather_only_what_they_touch():
+    """RecordBatch.device of a lazy row selection reads its source (no gather); values() / items() gather as they
+    iterate, so a loop that stops at the first column gathers one."""
+    from netsdb_amd.objects import record as R
+
+    src = {f"c{i}": torch.arange(10) * i for i in range(8)}
+    lt = R.LazyTakeColumns(src, torch.tensor([1, 3, 5]))
+    b = RecordBatch(lt, 3)
+    assert b.device == torch.device("cpu") and not any(dict.__contains__(lt, k) for k in src)
+    first = next(iter(lt.values()))
+    assert first.tolist() == [0, 0, 0] and sum(dict.__contains__(lt, k) for k in src) == 1
+    assert len(lt.values()) == 8 and [k for k, _ in lt.items()] == [f"c{i}" for i in range(8)]
+    assert [v.tolist() for v in lt.values()][2] == [2, 6, 10]
