@@ -16,10 +16,6 @@
 //    rows whose key does not fit go straight to a small global table, and at the end each workgroup flushes its
 //    LDS entries ONCE into the global table (agent-scope atomics): one global atomic per (workgroup, key), not per
 //    row. If the global table overflows (the sample under-estimated the groups) a device flag routes the work to:
-//  * MID path (up to ~10 K groups for one value column, what one workgroup's 160 KiB LDS holds as dense arrays):
-//    agg_mid — a global key -> dense-id dictionary (L2-resident, claimed by CAS, ids from one counter) and per
-//    workgroup LDS accumulators indexed by the id; agg_mid_reduce folds the workgroups' partials per id. One pass
-//    over the rows and no partition buffers. Ids beyond the LDS arrays set a flag that routes the work to:
 //  * PART path (many groups): 256 level-1 buckets by the top hash bits (agg_hist: per-workgroup LDS histograms;
 //    scan_rows / scan_tot: block scans; agg_scatter: tile-staged counting sort in LDS, so each bucket's rows leave
 //    as one coalesced run per tile), then agg_bucket: workgroup b owns bucket b whole. If its share of the
@@ -124,10 +120,7 @@ struct AggMeta {
   i64 sentinel_part;
   i64 occ_low;        // slots claimed in the LOW global table (its fill, apart from the group count)
   i64 occ_part;       // slots claimed in the PART overflow table
-  i64 mid;            // 1: the sample says the groups fit one workgroup's LDS arrays -> MID path
-  i64 ng_mid;         // dense ids handed out by the MID dictionary
-  i64 fail_mid;       // MID dictionary or LDS arrays overflowed -> PART path runs
-  i64 pad[3];
+  i64 pad[6];
 };
 
 struct GTable {                     // open-addressing global table: cap slots + one slot (cap) for the kEmpty key
@@ -140,13 +133,6 @@ struct GTable {                     // open-addressing global table: cap slots +
   i64* occ;                         // claimed-slot counter (AggMeta::occ_*)
 };
 
-// MID dictionary slot: key -> dense group id (cap slots preset {kEmpty, -1}; slot cap, the kEmpty key's, preset
-// {0, -1} and claimed by writing 1). One 16-byte load resolves a row whose key is present.
-struct __attribute__((aligned(16))) DSlot {
-  u64 key;
-  i64 id;
-};
-
 struct AggOut {
   i64* reps;        // [n] dense group keys
   u64* aggs;        // [n * F]
@@ -157,10 +143,7 @@ struct AggOut {
 };
 
 __device__ __forceinline__ bool take_low(const AggMeta* m) { return m->low != 0; }
-__device__ __forceinline__ bool take_mid(const AggMeta* m) { return m->mid != 0 && m->fail_mid == 0; }
-__device__ __forceinline__ bool take_part(const AggMeta* m) {
-  return (m->low == 0 && m->mid == 0) || m->fail_low != 0 || m->fail_mid != 0;
-}
+__device__ __forceinline__ bool take_part(const AggMeta* m) { return m->low == 0 || m->fail_low != 0; }
 
 constexpr int kLdsProbe = 64;     // LDS probe window: a row whose window is full goes to the global table
 constexpr u64 kGlobalProbe = 1024;  // global probe window: beyond it the table counts as full (fail flag)
@@ -302,7 +285,7 @@ __global__ __launch_bounds__(64) void agg_sample_gather_kernel(const u64* __rest
 }
 
 __global__ __launch_bounds__(1024) void agg_sample_kernel(const u64* __restrict__ sbuf, i64 n, int low_thr,
-                                                          int mid_thr, AggMeta* meta) {
+                                                          AggMeta* meta) {
   constexpr int S = kSample, CAP = 8192;
   __shared__ u64 tab[CAP];
   __shared__ unsigned tcnt[CAP];
@@ -371,17 +354,14 @@ __global__ __launch_bounds__(1024) void agg_sample_kernel(const u64* __restrict_
     est = std::min(est, (double)n);
     meta->est = (i64)est;
     meta->low = est <= (double)low_thr ? 1 : 0;
-    meta->mid = (meta->low == 0 && est <= (double)mid_thr) ? 1 : 0;
   }
 }
 
 // One launch presets both global tables ([key | acc | cnt | gid] words) and zeroes the meta words.
 __global__ __launch_bounds__(256) void agg_init_kernel(u64* glow, i64 cap_low, u64* gpart, i64 cap_part, int F,
-                                                       u64 ident, AggMeta* meta, DSlot* dict, i64 cap_mid) {
+                                                       u64 ident, AggMeta* meta) {
   const i64 stride = (i64)gridDim.x * blockDim.x;
   const i64 t0 = (i64)blockIdx.x * blockDim.x + threadIdx.x;
-  if (dict != nullptr)
-    for (i64 i = t0; i <= cap_mid; i += stride) dict[i] = DSlot{i < cap_mid ? kEmpty : 0ull, -1};
   for (int which = 0; which < 2; ++which) {
     u64* base = which ? gpart : glow;
     const i64 c1 = (which ? cap_part : cap_low) + 1;
@@ -400,8 +380,7 @@ constexpr int kPreF = 1;     // value columns loaded with the keys (the rest at 
 // Row (key, values) batch of one thread: kU rows of a 256*kU-row tile, loaded together. Value (i, f) of the input
 // is vals[i * rs + f * cs]: row-major [n, F] (rs = F, cs = 1) or column-major (rs = 1, cs = column pitch), so a
 // caller's stacked columns are read in place.
-// NT: non-temporal loads (streamed once; they do not push a kernel's L2-resident lookup table out of the L2).
-template <typename VT, bool NT = false>
+template <typename VT>
 struct RowBatch {
   u64 k[kU];
   VT v[kU][kPreF];
@@ -410,16 +389,9 @@ struct RowBatch {
 #pragma unroll
     for (int j = 0; j < kU; ++j) {
       const i64 i = t0 + (i64)j * nthr + threadIdx.x;
-      if constexpr (NT) {
-        k[j] = i < n ? __builtin_nontemporal_load(keys + i) : kEmpty;
+      k[j] = i < n ? keys[i] : kEmpty;
 #pragma unroll
-        for (int f = 0; f < kPreF; ++f)
-          v[j][f] = (i < n && f < F) ? __builtin_nontemporal_load(vals + i * rs + f * cs) : VT(0);
-      } else {
-        k[j] = i < n ? keys[i] : kEmpty;
-#pragma unroll
-        for (int f = 0; f < kPreF; ++f) v[j][f] = (i < n && f < F) ? vals[i * rs + f * cs] : VT(0);
-      }
+      for (int f = 0; f < kPreF; ++f) v[j][f] = (i < n && f < F) ? vals[i * rs + f * cs] : VT(0);
     }
   }
 };
@@ -495,276 +467,6 @@ __global__ __launch_bounds__(256) void agg_low_kernel(const u64* __restrict__ ke
       const int s = ltable_find(t, k[j], mix64(k[j]));
       if (s >= 0) o.inv[i] = t.ref[s];
     }
-  }
-}
-
-// ---------------------------------------------------------------- MID path
-// Up to dcap groups (dcap = what one workgroup's LDS holds as dense arrays: 160 KiB / (8F + 4 [+ 4 with first]),
-// e.g. 10 K groups for one value column): a global dictionary (L2-resident, <= 1/2 full) maps each key to a dense
-// id, and every workgroup accumulates its rows into LDS arrays indexed by that id (no LDS hash probe, no key
-// compare in LDS). Each workgroup then writes its partial arrays once (only ids below the largest it touched) and
-// agg_mid_reduce folds the partials of all workgroups per id into the dense output. One pass over the rows, no
-// partition buffers: the 3-pass traffic of the PART path (read, scatter, read back) for group counts that do not
-// need it.
-constexpr int kMidThreads = 1024;
-constexpr int kMidReserve = 64;   // LDS bytes kept for the block's largest-id word
-
-// Slow path of the dictionary lookup, one probe step per loop iteration: a lane whose key another lane of its own
-// wave has just claimed never waits inside divergent code (the claimer publishes the id in the same iteration;
-// the waiter re-reads it in the next one). Returns the dense id, or -1 (dictionary full, or ids beyond dcap:
-// fail_mid set, the PART path redoes the aggregation).
-__device__ __noinline__ i64 mid_id_slow(DSlot* d, u64 mask, u64 k, AggMeta* m, i64 dcap, i64* reps) {
-  const bool sent = k == kEmpty;
-  const u64 want = sent ? 1ull : k, empty = sent ? 0ull : kEmpty;
-  u64 s = sent ? mask + 1 : (mix64(k) & mask);
-  const u64 window = mask < kGlobalProbe ? mask + 1 : kGlobalProbe;
-  u64 probes = 0;
-  for (;;) {
-    u64 cur = __hip_atomic_load(&d[s].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (cur == empty) {
-      if (__hip_atomic_compare_exchange_strong(&d[s].key, &cur, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT)) {
-        const i64 id = __hip_atomic_fetch_add(&m->ng_mid, (i64)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&d[s].id, id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (id < dcap) {
-          reps[id] = (i64)k;
-          return id;
-        }
-        __hip_atomic_store(&m->fail_mid, (i64)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return -1;
-      }
-    }
-    if (cur == want) {
-      const i64 id = __hip_atomic_load(&d[s].id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (id >= 0) return id < dcap ? id : -1;
-      __builtin_amdgcn_s_sleep(2);
-      continue;   // claimed, id not yet visible: read again next iteration
-    }
-    if (sent || ++probes >= window) {
-      __hip_atomic_store(&m->fail_mid, (i64)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return -1;
-    }
-    s = (s + 1) & mask;
-  }
-}
-
-// Claim k's dictionary slot (no id read): the CAS winner takes the next dense id and publishes it.
-__device__ __forceinline__ void mid_claim(DSlot* d, u64 mask, u64 k, AggMeta* m, i64 dcap, i64* reps) {
-  const bool sent = k == kEmpty;
-  const u64 want = sent ? 1ull : k, empty = sent ? 0ull : kEmpty;
-  u64 s = sent ? mask + 1 : (mix64(k) & mask);
-  const u64 window = mask < kGlobalProbe ? mask + 1 : kGlobalProbe;
-  for (u64 p = 0; p < window; ++p) {
-    u64 cur = empty;
-    if (__hip_atomic_compare_exchange_strong(&d[s].key, &cur, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT)) {
-      const i64 id = __hip_atomic_fetch_add(&m->ng_mid, (i64)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&d[s].id, id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (id < dcap) reps[id] = (i64)k;
-      else __hip_atomic_store(&m->fail_mid, (i64)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return;
-    }
-    if (cur == want) return;
-    if (sent) break;
-    s = (s + 1) & mask;
-  }
-  __hip_atomic_store(&m->fail_mid, (i64)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Dictionary build, a kernel of its own: the slots are claimed by device-scope CAS, which this XCD's L2 does not
-// see, so a lookup in the same kernel could read a stale "empty" line and fall to the slow path for every row.
-// After the launch boundary the accumulation kernel reads a complete dictionary from L2. Each workgroup first
-// dedups its keys in an LDS key set, so a key costs one global CAS per workgroup, not per row.
-__global__ __launch_bounds__(kMidThreads) void agg_mid_dict_kernel(const u64* __restrict__ keys, i64 n, int scap,
-                                                                   DSlot* dict, u64 dmask, AggMeta* meta, i64 dcap,
-                                                                   i64* __restrict__ reps) {
-  if (!take_mid(meta)) return;
-  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
-  u64* set = reinterpret_cast<u64*>(lds_raw);
-  for (int i = threadIdx.x; i < scap; i += kMidThreads) set[i] = kEmpty;
-  __syncthreads();
-  constexpr int TILE = kMidThreads * kU;
-  const i64 tstride = (i64)gridDim.x * TILE;
-  const int smask = scap - 1;
-  u64 cur[kU], nxt[kU];
-  auto load = [&](i64 b0, u64 (&kk)[kU]) {
-#pragma unroll
-    for (int j = 0; j < kU; ++j) {
-      const i64 i = b0 + (i64)j * kMidThreads + threadIdx.x;
-      kk[j] = i < n ? __builtin_nontemporal_load(keys + i) : kEmpty;
-    }
-  };
-  i64 t0 = (i64)blockIdx.x * TILE;
-  if (t0 < n) load(t0, cur);
-  for (int it = 0; t0 < n; t0 += tstride, ++it) {
-    if ((it & 7) == 7 && __hip_atomic_load(&meta->fail_mid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
-    if (t0 + tstride < n) load(t0 + tstride, nxt);
-#pragma unroll
-    for (int j = 0; j < kU; ++j) {
-      const i64 i = t0 + (i64)j * kMidThreads + threadIdx.x;
-      if (i >= n) break;
-      const u64 k = cur[j];
-      bool fresh = true;   // first sight of k in this workgroup (or its LDS window is full)
-      if (k != kEmpty) {
-        int s = (int)((mix64(k) >> 32) & (u64)smask);
-        for (int p = 0; p < kLdsProbe; ++p) {
-          u64 c = set[s];
-          if (c == kEmpty) {
-            __hip_atomic_compare_exchange_strong(set + s, &c, k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (c == kEmpty) break;   // claimed here: fresh
-          }
-          if (c == k) {
-            fresh = false;
-            break;
-          }
-          s = (s + 1) & smask;
-        }
-      }
-      if (fresh) mid_claim(dict, dmask, k, meta, dcap, reps);
-    }
-#pragma unroll
-    for (int j = 0; j < kU; ++j) cur[j] = nxt[j];
-  }
-}
-
-// rows [t0, ...) strided like agg_low; LDS: [acc dcap*F u64 | cnt dcap u32 | rmin dcap u32 (want_first)]
-template <typename VT, int OP>
-__global__ __launch_bounds__(kMidThreads) void agg_mid_kernel(const u64* __restrict__ keys,
-                                                              const VT* __restrict__ vals, i64 n, int F, i64 rs,
-                                                              i64 cs, int dcap,
-                                                              int want_first, DSlot* dict, u64 dmask, AggMeta* meta,
-                                                              AggOut o, i64* __restrict__ part_nw,
-                                                              u64* __restrict__ part_acc, unsigned* __restrict__ part_cnt,
-                                                              unsigned* __restrict__ part_rmin) {
-  if (!take_mid(meta)) return;
-  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
-  u64* lacc = reinterpret_cast<u64*>(lds_raw);
-  unsigned* lcnt = reinterpret_cast<unsigned*>(lacc + (size_t)dcap * F);
-  unsigned* lrmin = lcnt + dcap;
-  int* maxid_sh = reinterpret_cast<int*>(lrmin + (want_first ? dcap : 0));
-  for (int i = threadIdx.x; i < dcap * F; i += kMidThreads) lacc[i] = acc_identity<VT, OP>();
-  for (int i = threadIdx.x; i < dcap; i += kMidThreads) {
-    lcnt[i] = 0;
-    if (want_first) lrmin[i] = ~0u;
-  }
-  if (threadIdx.x == 0) *maxid_sh = -1;
-  __syncthreads();
-  constexpr int TILE = kMidThreads * kU;
-  const i64 tstride = (i64)gridDim.x * TILE;
-  int maxid = -1, it = 0;
-  RowBatch<VT, true> cur, nxt;   // keys / values stream past the L2-resident dictionary
-  i64 t0 = (i64)blockIdx.x * TILE;
-  if (t0 < n) cur.load(keys, vals, t0, n, F, kMidThreads, rs, cs);
-  for (; t0 < n; t0 += tstride, ++it) {
-    if ((it & 7) == 7 && __hip_atomic_load(&meta->fail_mid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
-    if (t0 + tstride < n) nxt.load(keys, vals, t0 + tstride, n, F, kMidThreads, rs, cs);   // in flight during this tile
-    DSlot e[kU];
-#pragma unroll
-    for (int j = 0; j < kU; ++j) {   // all dictionary reads of the batch issued together
-      const u64 k = cur.k[j];
-      const u64 s = k == kEmpty ? dmask + 1 : (mix64(k) & dmask);
-      e[j] = t0 + j * kMidThreads + threadIdx.x < n ? dict[s] : DSlot{0ull, -1};
-    }
-#pragma unroll
-    for (int j = 0; j < kU; ++j) {
-      const i64 i = t0 + j * kMidThreads + threadIdx.x;
-      if (i >= n) break;
-      const u64 k = cur.k[j];
-      const u64 want = k == kEmpty ? 1ull : k;
-      i64 id = (e[j].key == want && e[j].id >= 0) ? (e[j].id < dcap ? e[j].id : -1)
-                                                  : mid_id_slow(dict, dmask, k, meta, dcap, o.reps);
-      if (o.inv) o.inv[i] = id;
-      if (id < 0) continue;
-      const int x = (int)id;
-      maxid = max(maxid, x);
-      const VT* vrow = vals + i * rs;
-      for (int f = 0; f < F; ++f)
-        acc_add<VT, OP, __HIP_MEMORY_SCOPE_WORKGROUP>(lacc + (size_t)x * F + f, f == 0 ? cur.v[j][0] : vrow[f * cs]);
-      __hip_atomic_fetch_add(lcnt + x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (want_first) {
-        const unsigned r32 = (unsigned)i;
-        if (r32 < lrmin[x]) __hip_atomic_fetch_min(lrmin + x, r32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-    }
-    cur = nxt;
-  }
-  for (int d = 32; d > 0; d >>= 1) maxid = max(maxid, __shfl_xor(maxid, d, 64));
-  if ((threadIdx.x & 63) == 0) atomicMax(maxid_sh, maxid);
-  __syncthreads();
-  const int nw = *maxid_sh + 1;   // ids this workgroup touched are all below nw
-  const size_t wb = (size_t)blockIdx.x * dcap;
-  for (int i = threadIdx.x; i < nw * F; i += kMidThreads) part_acc[wb * F + i] = lacc[i];
-  for (int i = threadIdx.x; i < nw; i += kMidThreads) {
-    part_cnt[wb + i] = lcnt[i];
-    if (want_first) part_rmin[wb + i] = lrmin[i];
-  }
-  if (threadIdx.x == 0) part_nw[blockIdx.x] = nw;
-}
-
-template <typename VT, int OP>
-__device__ __forceinline__ u64 acc_combine(u64 a, u64 b) {
-  if constexpr (OP == OP_SUM) {
-    if constexpr (__is_same(VT, double))
-      return (u64)__double_as_longlong(__longlong_as_double((i64)a) + __longlong_as_double((i64)b));
-    else
-      return a + b;
-  } else if constexpr (OP == OP_MIN) {
-    return a < b ? a : b;
-  } else {
-    return a > b ? a : b;
-  }
-}
-
-// 64 ids per workgroup (lane = id), 16 waves over the G partials (wave q: partials q, q + 16, ...), LDS fold
-template <typename VT, int OP>
-__global__ __launch_bounds__(1024) void agg_mid_reduce_kernel(int G, int F, int dcap, int want_first,
-                                                              const AggMeta* meta, AggOut o,
-                                                              const i64* __restrict__ part_nw,
-                                                              const u64* __restrict__ part_acc,
-                                                              const unsigned* __restrict__ part_cnt,
-                                                              const unsigned* __restrict__ part_rmin) {
-  if (!take_mid(meta)) return;
-  const i64 ng = std::min<i64>(meta->ng_mid, dcap);
-  const int id0 = blockIdx.x * 64;
-  if (id0 >= ng) return;
-  __shared__ int nw[256];
-  __shared__ u64 red[16][64];
-  __shared__ unsigned redc[16][64], redr[16][64];
-  for (int w = threadIdx.x; w < G; w += 1024) nw[w] = (int)part_nw[w];
-  __syncthreads();
-  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
-  const int id = id0 + lane;
-  for (int f = 0; f < F; ++f) {
-    u64 a = acc_identity<VT, OP>();
-#pragma unroll 4
-    for (int w = q; w < G; w += 16)
-      if (id < nw[w]) a = acc_combine<VT, OP>(a, part_acc[((size_t)w * dcap + id) * F + f]);
-    red[q][lane] = a;
-    __syncthreads();
-    if (q == 0) {
-      for (int r = 1; r < 16; ++r) a = acc_combine<VT, OP>(a, red[r][lane]);
-      if (id < ng) o.aggs[(i64)id * F + f] = acc_out<VT, OP>(a);
-    }
-    __syncthreads();
-  }
-  unsigned c = 0, rm = ~0u;
-#pragma unroll 4
-  for (int w = q; w < G; w += 16)
-    if (id < nw[w]) {
-      c += part_cnt[(size_t)w * dcap + id];
-      if (want_first) rm = min(rm, part_rmin[(size_t)w * dcap + id]);
-    }
-  redc[q][lane] = c;
-  redr[q][lane] = rm;
-  __syncthreads();
-  if (q == 0 && id < ng) {
-    for (int r = 1; r < 16; ++r) {
-      c += redc[r][lane];
-      rm = min(rm, redr[r][lane]);
-    }
-    o.cnt[id] = (i64)c;
-    o.first[id] = want_first ? (i64)rm : 0;
   }
 }
 
@@ -1176,7 +878,6 @@ __global__ __launch_bounds__(1024) void agg_bucket_kernel(const u64* __restrict_
 template <typename VT, int OP>
 __global__ __launch_bounds__(256) void agg_emit_kernel(GTable glow, GTable gpart, int F, const AggMeta* meta,
                                                        AggOut o) {
-  if (take_mid(meta)) return;
   const bool low = !take_part(meta);
   const GTable g = low ? glow : gpart;
   const bool sentinel = (low ? meta->sentinel_low : meta->sentinel_part) != 0;
@@ -1491,21 +1192,10 @@ inline int stage_rows(int F, int budget = 48 * 1024, int nthr = 512) {
 // level-1 histogram / scatter workgroups (one per CU), >= 16 Ki rows each
 inline int agg_groups(long long n) { return (int)std::min<long long>(256, std::max<long long>(1, (n + 16383) / 16384)); }
 
-// MID workgroups: one per CU (the LDS arrays fill it), >= 16 Ki rows each
-inline int mid_groups(long long n) { return agg_groups(n); }
-
-// MID partial arrays [nw G | acc G*dcap*F | cnt G*dcap | rmin G*dcap] (aliases the PART work buffer: the PART
-// kernels only run when the MID path failed, after its reduce)
-inline long long mid_work_bytes(long long n, int F, int dcap) {
-  const long long G = mid_groups(n);
-  return 8 * G + G * (long long)dcap * (8LL * F + 8) + 64;
-}
-
 template <typename VT, int OP>
 int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv, int want_first, void* meta_v, void* glow_v,
-                 i64 gcap_low, void* gpart_v, i64 gcap_part, void* gmid_v, i64 gcap_mid, int dcap, void* out_v,
-                 void* work_v, int pbits, int lcap_low, int lcap_part, int low_thr, int mid_thr, i64 rs, i64 cs,
-                 hipStream_t st) {
+                 i64 gcap_low, void* gpart_v, i64 gcap_part, void* out_v, void* work_v, int pbits, int lcap_low,
+                 int lcap_part, int low_thr, i64 rs, i64 cs, hipStream_t st) {
   AggMeta* meta = reinterpret_cast<AggMeta*>(meta_v);
   // glow / gpart: [key (cap+1) | acc (cap+1)*F | cnt (cap+1) | gid (cap+1)] u64 words, preset by the caller
   auto mk = [&](void* base, i64 cap) {
@@ -1536,33 +1226,13 @@ int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv,
   const size_t lbytes_part = (size_t)lcap_part * (20 + 8 * F);
 
   hipLaunchKernelGGL(agg_init_kernel, dim3(512), dim3(256), 0, st, reinterpret_cast<u64*>(glow_v), gcap_low,
-                     reinterpret_cast<u64*>(gpart_v), gcap_part, F, acc_identity<VT, OP>(), meta,
-                     dcap > 0 ? reinterpret_cast<DSlot*>(gmid_v) : nullptr, gcap_mid);
+                     reinterpret_cast<u64*>(gpart_v), gcap_part, F, acc_identity<VT, OP>(), meta);
   u64* sbuf = reinterpret_cast<u64*>(meta) + sizeof(AggMeta) / 8;   // [4096] after the meta words
   hipLaunchKernelGGL(agg_sample_gather_kernel, dim3(kSample / 64), dim3(64), 0, st, k, n, sbuf);
-  hipLaunchKernelGGL(agg_sample_kernel, dim3(1), dim3(1024), 0, st, sbuf, n, low_thr, mid_thr, meta);
+  hipLaunchKernelGGL(agg_sample_kernel, dim3(1), dim3(1024), 0, st, sbuf, n, low_thr, meta);
   const int gl = (int)std::min<i64>(1024, std::max<i64>(1, (n + 2047) / 2048));
   hipLaunchKernelGGL((agg_low_kernel<VT, OP>), dim3(gl), dim3(256), lbytes_low, st, k, v, n, F, rs, cs, lcap_low, glow,
                      meta, o);
-  if (dcap > 0) {
-    const int Gm = mid_groups(n);
-    i64* part_nw = reinterpret_cast<i64*>(work_v);
-    u64* part_acc = reinterpret_cast<u64*>(part_nw + Gm);
-    unsigned* part_cnt = reinterpret_cast<unsigned*>(part_acc + (size_t)Gm * dcap * F);
-    unsigned* part_rmin = part_cnt + (size_t)Gm * dcap;
-    const size_t lbytes_mid = (size_t)dcap * (8 * F + 4 + (want_first ? 4 : 0)) + kMidReserve;
-    int scap = 1024;   // LDS key set of the dictionary build: <= 1/2 full at dcap keys, <= 128 KiB
-    while (scap < 16384 && scap < 2 * dcap) scap <<= 1;
-    // fewer, longer workgroups for the build: each costs one device-scope CAS per distinct key it sees (~7 G/s on
-    // this part), so 64 of them trade read parallelism for 4x fewer CAS than one per CU
-    hipLaunchKernelGGL(agg_mid_dict_kernel, dim3(std::min(Gm, 64)), dim3(kMidThreads), (size_t)scap * 8, st, k, n, scap,
-                       reinterpret_cast<DSlot*>(gmid_v), (u64)(gcap_mid - 1), meta, (i64)dcap, o.reps);
-    hipLaunchKernelGGL((agg_mid_kernel<VT, OP>), dim3(Gm), dim3(kMidThreads), lbytes_mid, st, k, v, n, F, rs, cs, dcap,
-                       want_first, reinterpret_cast<DSlot*>(gmid_v), (u64)(gcap_mid - 1), meta, o, part_nw, part_acc,
-                       part_cnt, part_rmin);
-    hipLaunchKernelGGL((agg_mid_reduce_kernel<VT, OP>), dim3((dcap + 63) / 64), dim3(1024), 0, st, Gm, F, dcap,
-                       want_first, meta, o, part_nw, part_acc, part_cnt, part_rmin);
-  }
   // PART: work buffers [hist P*G u32 | tot P | bstart P+1 | pkey n | pval n*F | prow n (i32) | qkey | qval | qrow]
   const int P = 1 << pbits;
   const int G = agg_groups(n);
@@ -1603,26 +1273,20 @@ using namespace nsdb_rel;
 
 extern "C" {
 
-// Byte size of the work buffer for (n, F, pbits, dcap): the PART partitions or the MID partials (aliased).
-long long nsdb_agg_work_bytes(long long n, int F, int pbits, int want_inv, int dcap) {
+// Byte size of the PART work buffer for (n, F, pbits).
+long long nsdb_agg_work_bytes(long long n, int F, int pbits, int want_inv) {
   const long long P = 1LL << pbits;
   const long long G = agg_groups(n);
   (void)want_inv;
-  const long long part = ((P * G * 4 + 15) & ~15LL) + 8 * (2 * P + 2) + 2 * (8 * n + 8 * n * F + 4 * (n + 1)) + 64;
-  return std::max(part, dcap > 0 ? mid_work_bytes(n, F, dcap) : 0LL);
+  return ((P * G * 4 + 15) & ~15LL) + 8 * (2 * P + 2) + 2 * (8 * n + 8 * n * F + 4 * (n + 1)) + 64;
 }
 
-// Largest MID group count for F value columns: dense LDS arrays of one 160 KiB workgroup.
-int nsdb_agg_mid_cap(int F, int want_first) {
-  return (163840 - kMidReserve) / (8 * F + 4 + (want_first ? 4 : 0));
-}
-
-// vt: 0 double, 1 int64; op: 0 sum, 1 min, 2 max. dcap 0 disables the MID path. Value (i, f) is vals[i * vrs + f * vcs]
-// (vrs = vcs = 0: row-major [n, F]).
+// vt: 0 double, 1 int64; op: 0 sum, 1 min, 2 max. Value (i, f) is vals[i * vrs + f * vcs] (vrs = vcs = 0: row-major
+// [n, F]).
 int nsdb_hash_aggregate(const void* keys, const void* vals, long long n, int F, int vt, int op, int want_inv,
                         int want_first, void* meta, void* glow, long long gcap_low, void* gpart, long long gcap_part,
-                        void* gmid, long long gcap_mid, int dcap, void* out, void* work, int pbits, int lcap_low,
-                        int lcap_part, int low_thr, int mid_thr, long long vrs, long long vcs, hipStream_t st) {
+                        void* out, void* work, int pbits, int lcap_low, int lcap_part, int low_thr, long long vrs,
+                        long long vcs, hipStream_t st) {
   if (n <= 0) return 0;
   if (n >= (1LL << 31)) return (int)hipErrorInvalidValue;
   if (F < 0 || F > 16 || pbits < 0 || pbits > 10) return (int)hipErrorInvalidValue;
@@ -1630,15 +1294,12 @@ int nsdb_hash_aggregate(const void* keys, const void* vals, long long n, int F, 
   if (!pow2(gcap_low) || !pow2(gcap_part) || !pow2(lcap_low) || !pow2(lcap_part)) return (int)hipErrorInvalidValue;
   if ((size_t)lcap_low * (20 + 8 * F) > 65536 || (size_t)lcap_part * (20 + 8 * F) > 131072) return (int)hipErrorInvalidValue;
   if ((size_t)stage_rows(F, 96 * 1024, 1024) * (14 + 8 * F) > 131072) return (int)hipErrorInvalidValue;
-  if (dcap < 0 || dcap > nsdb_agg_mid_cap(F, want_first)) return (int)hipErrorInvalidValue;
-  if (dcap > 0 && (!pow2(gcap_mid) || gcap_mid < 2LL * dcap)) return (int)hipErrorInvalidValue;
-  if (dcap == 0) mid_thr = 0;
   if (F > 0 && (vrs < 0 || vcs < 0)) return (int)hipErrorInvalidValue;
   if (vrs == 0 && vcs == 0) {   // default: row-major [n, F]
     vrs = F;
     vcs = 1;
   }
-#define NSDB_AGG(VT, OP) agg_launch_t<VT, OP>(keys, vals, n, F, want_inv, want_first, meta, glow, gcap_low, gpart, gcap_part, gmid, gcap_mid, dcap, out, work, pbits, lcap_low, lcap_part, low_thr, mid_thr, vrs, vcs, st)
+#define NSDB_AGG(VT, OP) agg_launch_t<VT, OP>(keys, vals, n, F, want_inv, want_first, meta, glow, gcap_low, gpart, gcap_part, out, work, pbits, lcap_low, lcap_part, low_thr, vrs, vcs, st)
   if (vt == 0) {
     if (op == 0) return NSDB_AGG(double, OP_SUM);
     if (op == 1) return NSDB_AGG(double, OP_MIN);

@@ -14,12 +14,11 @@ typedef long long ll;
 template <typename T> ll* LL(T* p) { return reinterpret_cast<ll*>(p); }
 
 extern "C" {
-long long nsdb_agg_work_bytes(long long n, int F, int pbits, int want_inv, int dcap);
-int nsdb_agg_mid_cap(int F, int want_first);
+long long nsdb_agg_work_bytes(long long n, int F, int pbits, int want_inv);
 int nsdb_hash_aggregate(const void* keys, const void* vals, long long n, int F, int vt, int op, int want_inv,
                         int want_first, void* meta, void* glow, long long gcap_low, void* gpart, long long gcap_part,
-                        void* gmid, long long gcap_mid, int dcap, void* out, void* work, int pbits, int lcap_low,
-                        int lcap_part, int low_thr, int mid_thr, long long vrs, long long vcs, hipStream_t st);
+                        void* out, void* work, int pbits, int lcap_low, int lcap_part, int low_thr, long long vrs,
+                        long long vcs, hipStream_t st);
 int nsdb_join_insert(const void* keys, long long n, void* tab, long long cap, int* row_slot, unsigned* row_rank,
                      unsigned long long* ndup, hipStream_t st);
 int nsdb_join_perm(const int* row_slot, const unsigned* row_rank, long long n, const unsigned long long* ndup,
@@ -60,13 +59,11 @@ constexpr int kMetaWords = 16 + 4096;   // AggMeta + the sampled keys (relops.hi
 //   vals: [n, F] float64 or int64 (or None / F == 0: counts only); op: "sum" | "min" | "max".
 // Returns (reps [g] i64, aggs [g, F] (vals dtype), counts [g] i64, first [g] i64 (smallest row of each group; only
 // meaningful with want_first, which otherwise lets the partition passes skip row ids),
-// inv [n] i64 (or empty), status): status = [g, path (0 LOW, 1 PART, 2 MID), ok (0: the PART table overflowed;
-// outputs invalid, fall back), distinct keys in the 4096-row sample].
-// low_threshold: largest estimated group count for the LOW path (0: automatic). mid_threshold > 0 opts in to the MID
-// path (dense LDS arrays + a global key dictionary) up to that many estimated groups (capped by what the LDS holds);
-// 0 (the default) leaves it off: measured slower than PART at 10 K keys / 16 M rows (profiles/r4_relops).
+// inv [n] i64 (or empty), status): status = [g, path (0 LOW, 1 PART), ok (0: the PART table overflowed; outputs
+// invalid, fall back), distinct keys in the 4096-row sample]. low_threshold: largest estimated group count for the
+// LOW path (0: automatic).
 std::vector<torch::Tensor> hash_aggregate(torch::Tensor keys, c10::optional<torch::Tensor> vals, const std::string& op,
-                                          bool want_inv, int64_t low_threshold, bool want_first, int64_t mid_threshold) {
+                                          bool want_inv, int64_t low_threshold, bool want_first) {
   TORCH_CHECK(keys.is_cuda(), "keys must be a GPU tensor");
   TORCH_CHECK(keys.scalar_type() == torch::kInt64 && keys.dim() == 1, "keys must be 1-D int64");
   keys = keys.contiguous();
@@ -111,35 +108,26 @@ std::vector<torch::Tensor> hash_aggregate(torch::Tensor keys, c10::optional<torc
   // overflow table of the PART path (keys whose LDS probe window filled): a miss-sized estimate only
   const int64_t gcap_part = std::max<int64_t>(4096, std::min<int64_t>(pow2_at_least(2 * n), int64_t(1) << 17));
   const int64_t thr = low_threshold > 0 ? low_threshold : lcap_low / 4;
-  // MID (opt-in): dense LDS arrays of up to dcap groups (relops.hip agg_mid_kernel), dictionary <= 1/2 full (the ids
-  // are exact: only more real groups than dcap send the work to PART)
-  const int dcap = mid_threshold <= 0 ? 0 : nsdb_agg_mid_cap(F, want_first ? 1 : 0);
-  const int64_t mid_thr = dcap == 0 ? 0 : std::min<int64_t>(mid_threshold, dcap);
-  const int64_t gcap_mid = dcap > 0 ? pow2_at_least(2 * (int64_t)dcap) : 0;
 
   auto meta = torch::empty({kMetaWords}, i64);
   auto glow = torch::empty({(gcap_low + 1) * (4 + F)}, i64);
   auto gpart = torch::empty({(gcap_part + 1) * (4 + F)}, i64);
-  auto gmid = torch::empty({dcap > 0 ? (gcap_mid + 1) * 2 : 0}, i64);
   // [reps n | aggs n*F | cnt n | slot_of_gid n | first n | inv n] (relops.hip agg_launch_t AggOut)
   auto out = torch::empty({n * (4 + F) + (want_inv ? n : 0)}, i64);
-  const int64_t wbytes = nsdb_agg_work_bytes(n, F, pbits, want_inv ? 1 : 0, dcap);
+  const int64_t wbytes = nsdb_agg_work_bytes(n, F, pbits, want_inv ? 1 : 0);
   auto work = torch::empty({(wbytes + 7) / 8}, i64);
   rc_ok(nsdb_hash_aggregate(keys.data_ptr(), F ? v.data_ptr() : nullptr, n, F, vt, opc, want_inv ? 1 : 0, want_first ? 1 : 0,
-                            meta.data_ptr(), glow.data_ptr(), gcap_low, gpart.data_ptr(), gcap_part,
-                            dcap > 0 ? gmid.data_ptr() : nullptr, gcap_mid, dcap, out.data_ptr(), work.data_ptr(), pbits,
-                            (int)lcap_low, (int)lcap_part, (int)thr, (int)mid_thr, (long long)vrs, (long long)vcs,
-                            stream()),
+                            meta.data_ptr(), glow.data_ptr(), gcap_low, gpart.data_ptr(), gcap_part, out.data_ptr(),
+                            work.data_ptr(), pbits, (int)lcap_low, (int)lcap_part, (int)thr, (long long)vrs,
+                            (long long)vcs, stream()),
         "hash_aggregate");
   auto m = meta.narrow(0, 0, 16).cpu();   // the one host read: group count and path flags
   const ll* mp = LL(m.data_ptr<int64_t>());
-  // AggMeta words: 0 est, 1 low, 2 ng_low, 3 ng_part, 4 fail_low, 5 fail_part, 10 mid, 11 ng_mid, 12 fail_mid
+  // AggMeta words: 0 est, 1 low, 2 ng_low, 3 ng_part, 4 fail_low, 5 fail_part
   const bool low_ok = mp[1] != 0 && mp[4] == 0;
-  const bool mid_ok = mp[10] != 0 && mp[12] == 0;
-  const int64_t g = (int64_t)(low_ok ? mp[2] : mid_ok ? mp[11] : mp[3]);
-  const bool ok = low_ok || mid_ok || mp[5] == 0;
-  const int64_t path = low_ok ? 0 : mid_ok ? 2 : 1;
-  auto status = torch::tensor({(int64_t)g, path, (int64_t)(ok ? 1 : 0), (int64_t)mp[0]}, torch::kInt64);
+  const int64_t g = (int64_t)(low_ok ? mp[2] : mp[3]);
+  const bool ok = low_ok || mp[5] == 0;
+  auto status = torch::tensor({(int64_t)g, (int64_t)(low_ok ? 0 : 1), (int64_t)(ok ? 1 : 0), (int64_t)mp[0]}, torch::kInt64);
   if (!ok) return {torch::Tensor(), torch::Tensor(), torch::Tensor(), torch::Tensor(), torch::Tensor(), status};
   auto reps = out.narrow(0, 0, g);
   auto aggs = out.narrow(0, n, g * F).view({g, F});
@@ -242,15 +230,14 @@ std::vector<torch::Tensor> partition_perm(torch::Tensor dest, int64_t P) {
 
 std::vector<torch::Tensor> hash_aggregate_impl(torch::Tensor keys, c10::optional<torch::Tensor> vals,
                                                const std::string& op, bool want_inv, int64_t low_threshold) {
-  return hash_aggregate(keys, vals, op, want_inv, low_threshold, true, 0);
+  return hash_aggregate(keys, vals, op, want_inv, low_threshold, true);
 }
 
 void register_relops(pybind11::module& m) {
   m.def("hash_aggregate", &hash_aggregate,
         "device hash group-by + aggregate: (reps, aggs, counts, first, inv, status[g, path, ok, sample_distinct])",
         pybind11::arg("keys"), pybind11::arg("vals") = pybind11::none(), pybind11::arg("op") = "sum",
-        pybind11::arg("want_inv") = false, pybind11::arg("low_threshold") = 0, pybind11::arg("want_first") = true,
-        pybind11::arg("mid_threshold") = 0);
+        pybind11::arg("want_inv") = false, pybind11::arg("low_threshold") = 0, pybind11::arg("want_first") = true);
   m.def("join_build", &join_build, "device hash-join build: (table, perm)");
   m.def("join_probe", &join_probe, "device hash-join probe: (build_idx, probe_idx)");
   m.def("partition_perm", &partition_perm, "stable device partition permutation: (perm, counts)");

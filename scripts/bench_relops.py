@@ -74,18 +74,15 @@ def main():
         o2 = torch.argsort(r2[0])
         assert torch.equal(r2[0][o2], ref_u) and torch.allclose(r2[1][o2, 0], ref, rtol=1e-9), "no-first path differs"
 
-        def dev_agg_mid():    # the opt-in MID path (dense LDS arrays + global dictionary)
-            return h.hash_aggregate(keys, vals, "sum", False, 0, True, 10**9)
-
         def torch_agg():
             u, inv = torch.unique(keys, return_inverse=True)
             return torch.zeros(u.numel(), device=dev, dtype=torch.float64).index_add_(0, inv, vals)
 
         t = run({"hash_aggregate": dev_agg, "hash_aggregate_no_first": dev_agg_nofirst,
-                 "hash_aggregate_with_inverse": dev_agg_inv, "hash_aggregate_mid_opt_in": dev_agg_mid,
+                 "hash_aggregate_with_inverse": dev_agg_inv, 
                  "torch_unique_index_add": torch_agg}, a.rounds)
         t["groups"] = int(ref_u.numel())
-        t["path"] = ("LOW", "PART", "MID")[int(r[5][1])]
+        t["path"] = ("LOW", "PART")[int(r[5][1])]
         t["sample_distinct"] = int(r[5][3])
         t["max_rel_err"] = err
         out["groupby"][str(distinct)] = t

@@ -90,8 +90,8 @@ def test_hash_aggregate_int64_and_sentinel(op):
     keys[::97] = torch.iinfo(torch.int64).min            # the empty-slot marker as a real key
     keys[5::101] = torch.iinfo(torch.int64).max
     vals = torch.randint(-10**12, 10**12, (100_000,), device=DEV, generator=g)
-    for thr, mid, path in ((100_000, 0, 0), (1, 10**9, 2), (1, 0, 1)):   # forced LOW, opt-in MID, PART
-        r = _ext.hip().hash_aggregate(keys, vals, op, True, thr, True, mid)
+    for thr, path in ((100_000, 0), (1, 1)):                # forced LOW, forced PART
+        r = _ext.hip().hash_aggregate(keys, vals, op, True, thr)
         assert int(r[5][1]) == path
         _check_agg(keys, vals.unsqueeze(1), op, r, rtol=0)
     r = _ext.hip().hash_aggregate(keys, None, "sum", False, 0)   # counts only, no inverse
@@ -302,50 +302,6 @@ def test_hash_aggregate_without_first_rows(distinct):
     torch.testing.assert_close(a[1][oa], b[1][ob], rtol=1e-12, atol=1e-9)
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("F,distinct", [(0, 3000), (1, 9000), (3, 4000)])
-@pytest.mark.parametrize("op", ["sum", "min", "max"])
-def test_hash_aggregate_mid_path(F, distinct, op):
-    """MID path (groups fit one workgroup's dense LDS arrays): global key -> id dictionary, per-workgroup LDS
-    accumulation by id, one reduce over the workgroups' partials. The kEmpty marker is a key like any other."""
-    g = torch.Generator(device=DEV).manual_seed(F * 7 + distinct)
-    n = 700_000
-    keys = torch.randint(0, distinct, (n,), device=DEV, generator=g) * 104_729 - 77
-    keys[3::1001] = torch.iinfo(torch.int64).min
-    vals = (torch.rand(n, F, device=DEV, dtype=torch.float64, generator=g) - 0.5) if F else None
-    r = _ext.hip().hash_aggregate(keys, vals, op, True, 0, True, 10**9)
-    assert int(r[5][2]) == 1 and int(r[5][1]) == 2, r[5]
-    _check_agg(keys, vals, op, r)
-
-
-@pytest.mark.gpu
-def test_hash_aggregate_mid_int64_without_first():
-    g = torch.Generator(device=DEV).manual_seed(23)
-    n = 1_000_000
-    keys = torch.randint(0, 12_000, (n,), device=DEV, generator=g)
-    vals = torch.randint(-10**9, 10**9, (n, 1), device=DEV, generator=g)
-    a = _ext.hip().hash_aggregate(keys, vals, "sum", False, 0, False, 10**9)
-    assert int(a[5][1]) == 2 and int(a[5][0]) == 12_000     # 12 K groups fit the 13.6 K-id arrays without first
-    b = _ext.hip().hash_aggregate(keys, vals, "sum", False, 0, True, -1)
-    oa, ob = torch.argsort(a[0]), torch.argsort(b[0])
-    assert torch.equal(a[0][oa], b[0][ob]) and torch.equal(a[1][oa], b[1][ob]) and torch.equal(a[2][oa], b[2][ob])
-
-
-@pytest.mark.gpu
-def test_hash_aggregate_mid_overflow_falls_back_to_part():
-    """The sampled rows (evenly spaced) see ~1000 keys but the column holds 30 K: MID is chosen, its dense ids run
-    past the LDS arrays, the device flag hands the work to PART, and the result is exact."""
-    n = 400_000
-    keys = (torch.arange(n, device=DEV, dtype=torch.int64) % 30_000) * 3
-    samp = (torch.arange(4096, device=DEV, dtype=torch.int64) * n) // 4096
-    keys[samp] = -(torch.arange(4096, device=DEV) % 1000) - 1
-    vals = torch.ones(n, 1, device=DEV, dtype=torch.float64)
-    r = _ext.hip().hash_aggregate(keys, vals, "sum", True, 0, True, 10**9)
-    assert int(r[5][2]) == 1 and int(r[5][1]) == 1, r[5]
-    assert int(r[5][3]) < 10_000                              # the sample's estimate pointed at MID
-    _check_agg(keys, vals, "sum", r)
-
-
 _SHORT = ["", "a", "ab", "a\x00", "b", "zz", "abcdefg", "\u00e9", "A", "ab"]
 
 
@@ -394,8 +350,8 @@ def test_short_string_codes_and_groupby_gpu():
 @pytest.mark.gpu
 @pytest.mark.parametrize("distinct", [6, 3000, 300_000])
 def test_hash_aggregate_column_major_values(distinct):
-    """A [n, F] value row given column-major (the transpose of a contiguous [F, n] stack) is read in place by every
-    path (LOW / MID / PART) and aggregates exactly like the row-major copy."""
+    """A [n, F] value row given column-major (the transpose of a contiguous [F, n] stack) is read in place by both
+    paths (LOW / PART) and aggregates exactly like the row-major copy."""
     g = torch.Generator(device=DEV).manual_seed(distinct)
     n = 500_000
     keys = torch.randint(0, distinct, (n,), device=DEV, generator=g) * 3 + 1
@@ -409,5 +365,3 @@ def test_hash_aggregate_column_major_values(distinct):
     assert torch.equal(a[0][oa], b[0][ob]) and torch.equal(a[2][oa], b[2][ob]) and torch.equal(a[3][oa], b[3][ob])
     torch.testing.assert_close(a[1][oa], b[1][ob], rtol=1e-12, atol=1e-9)
     _check_agg(keys[:50_000], vc[:50_000], "max", _ext.hip().hash_aggregate(keys[:50_000], vc[:50_000], "max", True, 0))
-    m = _ext.hip().hash_aggregate(keys[:50_000], vc[:50_000], "sum", True, 0, True, 10**9)   # the opt-in MID path
-    _check_agg(keys[:50_000], vc[:50_000], "sum", m)
