@@ -416,6 +416,15 @@ class RecordBatch:
             raise ValueError("nothing to concatenate")
         nonempty = [b for b in batches if b.n > 0] or batches[:1]
         first = nonempty[0]
+        if len(nonempty) == 1:               # nothing to join: a shallow copy (a lazy selection stays lazy)
+            c = first.columns
+            if isinstance(c, LazyTakeColumns):
+                cp = LazyTakeColumns(c._src, c._idx)
+                cp._gone = set(c._gone)
+                dict.update(cp, dict.items(c))
+            else:
+                cp = dict(c)
+            return RecordBatch(cp, first.n, first.type)
         cols = {}
         for k in first.columns:
             parts = [b.columns[k] for b in nonempty]

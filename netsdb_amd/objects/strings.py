@@ -323,6 +323,8 @@ class StringColumn:
         parts = [p for p in parts if len(p)] or list(parts[:1])
         if not parts:
             return StringColumn.empty()
+        if len(parts) == 1:
+            return parts[0]                  # nothing to join (a one-batch group-by used to copy its row bounds here)
         dev = parts[0].device
         parts = [p.to(dev) for p in parts]
         d0 = parts[0].data
