@@ -420,8 +420,14 @@ def q01(client, db: str, delta_days: int = 90) -> List[dict]:
 
     def vals(b):
         q, p, d, t = (_col(b, c).double() for c in ("l_quantity", "l_extendedprice", "l_discount", "l_tax"))
-        dp = p * (1 - d)
-        return _vcols(q, p, dp, dp * (1 + t), d, torch.ones_like(q))
+        out = torch.empty(6, b.n, dtype=torch.float64, device=q.device)   # column-major value row, filled in place
+        out[0].copy_(q)
+        out[1].copy_(p)
+        torch.mul(p, 1 - d, out=out[2])                 # disc_price
+        torch.mul(out[2], 1 + t, out=out[3])            # charge
+        out[4].copy_(d)
+        out[5].fill_(1.0)                               # count
+        return out.t()
 
     agg = _GroupBy(lambda b: _str_keys(_col(b, "l_returnflag"), _col(b, "l_linestatus")), vals,
                    _rows_out(["sum_qty", "sum_base_price", "sum_disc_price", "sum_charge", "sum_disc", "count"]))
