@@ -18,6 +18,10 @@ rows/step/GPU = FF input rows + images.  Synthetic data, random-init weights, bf
 
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
+
+Without torchrun (WORLD_SIZE unset) and N > 1, bench.py launches its own ranks: N child processes, one per GPU
+(LOCAL_RANK = GPU index, RCCL; gloo on a CPU-only host), started as ordinary subprocesses BEFORE this process makes
+any GPU call (it never re-execs itself), rendezvous on 127.0.0.1. Rank 0's JSON line is the result.
 """
 import argparse
 import json
@@ -64,6 +68,44 @@ def verify(client, cv, ff, w, b, dev, nrows=16, nimg=2, single_job=False):
             "conv_images": nimg, "conv_max_rel_err": conv_err, "ok": bool(ok)}
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv) -> int:
+    """Spawn ``n`` ranks of this script (one per GPU) and wait for them. Called before any GPU call in this
+    process: counting devices does not initialise the GPU; the children are separate processes (no exec)."""
+    import subprocess
+
+    ndev = torch.cuda.device_count()
+    if 0 < ndev < n:
+        print(f"[bench] --gpus {n} but only {ndev} GPUs visible", file=sys.stderr)
+        return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    try:
+        for p in procs:
+            rc = p.wait() or rc
+    finally:
+        for p in procs:                      # one rank failed: do not leave the others waiting in a collective
+            if p.poll() is None:
+                p.kill()
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -85,6 +127,8 @@ def main():
     ap.add_argument("--single-job", action="store_true", help=argparse.SUPPRESS)   # the default; kept for old scripts
     args = ap.parse_args()
     args.single_job = not args.two_job
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
     from netsdb_amd.client import PDBClient
     from netsdb_amd.models import conv2d as cv

@@ -315,7 +315,8 @@ class PDBClient:
 
         plan = compile_tcap(list(sinks))
         atoms = _ext.native().parse_tcap(plan.tcap)
-        pp = Planner(self.engine._scan_size, self.ctx.world_size, self.engine.broadcast_threshold).plan(atoms)
+        pp = Planner(self.engine._scan_size, self.ctx.world_size, self.engine.broadcast_threshold,
+                     distributed=self.ctx.distributed).plan(atoms)
         return plan.tcap + "\n" + pp.explain()
 
     # ------------------------------------------------------------------ dedup / shared pages

@@ -186,7 +186,8 @@ class QueryEngine:
         """Stage-at-a-time execution driven by measured statistics (AdaptivePlanner): each finished
         stage's materialised output is measured (bytes, summed over ranks so every rank takes the same
         decisions) and costed for the next source selection."""
-        ap = AdaptivePlanner(atoms, self._scan_size, self.ctx.world_size, self.broadcast_threshold, self._copart)
+        ap = AdaptivePlanner(atoms, self._scan_size, self.ctx.world_size, self.broadcast_threshold, self._copart,
+                             distributed=self.ctx.distributed)
         stages = []
         while ap.has_work():
             st = ap.next_stage()
@@ -242,7 +243,8 @@ class QueryEngine:
             if self.adaptive:
                 pplan = self._run_adaptive(atoms, state, stats, job_name)
             else:
-                planner = Planner(self._scan_size, self.ctx.world_size, self.broadcast_threshold, self._copart)
+                planner = Planner(self._scan_size, self.ctx.world_size, self.broadcast_threshold, self._copart,
+                                      distributed=self.ctx.distributed)
                 pplan = planner.plan(atoms)
                 for st in pplan.stages:
                     self._timed_stage(st, state, stats, job_name)
@@ -393,7 +395,7 @@ class QueryEngine:
         """Hash-shuffle a batch stream across ranks in chunk rounds (StreamingShuffle); yields received batches."""
         from .shuffle import shuffle_stream
 
-        if self.ctx.world_size == 1:
+        if not self.ctx.distributed:
             yield from (b for b in batches if b is not None and b.n)
             return
         if tag in ("probe", "build"):
@@ -411,7 +413,7 @@ class QueryEngine:
 
     def _shuffle_by(self, batches: List[RecordBatch], hcol: str) -> List[RecordBatch]:
         ws = self.ctx.world_size
-        if ws == 1:
+        if not self.ctx.distributed:
             return batches
         self.shuffle_count += 1
         merged = RecordBatch.concat(batches) if batches else None
@@ -525,6 +527,8 @@ class QueryEngine:
             a = sk["atom"]
             col = a["input"]["atts"][0]
             uset = self.storage.get_set(a["db"], a["set"])
+            dense = isinstance(uset, DenseMatrixSet)
+            written = []        # (block_row, block_col) this rank wrote into a dense set
             for x in batches:
                 if x is None or x.n == 0:
                     continue
@@ -532,8 +536,10 @@ class QueryEngine:
                 if not isinstance(v, RecordBatch):
                     v = RecordBatch({"value": v}, x.n)
                 uset.add_batch(v)
-            if self.ctx.distributed and isinstance(uset, DenseMatrixSet):
-                self._merge_dense_output(uset)
+                if dense and "block_row" in v.columns:
+                    written.append((v.columns["block_row"], v.columns["block_col"]))
+            if self.ctx.distributed and dense:
+                self._merge_dense_output(uset, written)
             return
         if kind == "join_build":
             a = sk["atom"]
@@ -563,12 +569,12 @@ class QueryEngine:
 
     _DTYPES = (torch.float32, torch.bfloat16, torch.float16, torch.float64)
 
-    def _merge_dense_output(self, s):
-        """A dense matrix written block by block by an SPMD pipeline: every rank wrote the blocks it produced (a
-        disjoint share). Agree on the geometry, give ranks without blocks a zero panel, and sum the panels so
-        every rank holds the whole matrix (replicated), as a fused GEMM's output would be."""
-        from ..storage.sets import DenseMatrixSet  # noqa: F401
-
+    def _merge_dense_output(self, s, written=()):
+        """A dense matrix written block by block by an SPMD pipeline: every rank wrote the blocks it produced. Agree
+        on the geometry, then merge by block OWNERSHIP: each block takes the value of the rank(s) that wrote it in
+        this job (averaged when several ranks emitted the same block), every other block keeps the panel's previous
+        value. A rerun into the same set, or a panel that already held a replicated matrix, is therefore not summed
+        across ranks. Afterwards every rank holds the whole matrix (replicated), as a fused GEMM's output would."""
         geo = [0] * 5
         if s.has_data():
             dt = s.panel.dtype
@@ -583,7 +589,25 @@ class QueryEngine:
         panel = s.panel
         if s.row_offset != 0 or s.local_rows != ref[0]:
             raise RuntimeError(f"dense output {s.db}.{s.name}: a row-partitioned panel cannot be merged")
-        self.ctx.all_reduce(panel)
+        tr, tc, br, bc = ref[0], ref[1], ref[2], ref[3]
+        nbr, nbc = -(-tr // br), -(-tc // bc)
+        dev = panel.device
+        mask = torch.zeros(nbr, nbc, dtype=torch.float32, device=dev)
+        for r, c in written:
+            r = torch.as_tensor(r, device=dev).long()
+            c = torch.as_tensor(c, device=dev).long()
+            ok = (r >= 0) & (r < nbr) & (c >= 0) & (c < nbc)
+            mask[r[ok], c[ok]] = 1.0
+        cnt = mask.clone()
+        self.ctx.all_reduce(cnt)
+        expand = lambda m: m.repeat_interleave(br, 0)[:tr].repeat_interleave(bc, 1)[:, :tc]  # noqa: E731
+        view = s.matrix()                                 # logical [rows, cols] (a transposed view if need be)
+        mine = expand(mask) > 0
+        contrib = torch.where(mine, view.float(), torch.zeros((), device=dev))
+        self.ctx.all_reduce(contrib)
+        c_el = expand(cnt)
+        merged = torch.where(c_el > 0, contrib / c_el.clamp(min=1.0), view.float())
+        view.copy_(merged.to(view.dtype))
         s.replicated = True
 
     def _collect(self, batches, tag: str):
@@ -677,10 +701,13 @@ class QueryEngine:
             mean = op == "mean"
             local_op = "sum" if mean else op
             merge_op = "sum" if op in ("count", "mean") else op
+            vmeta = {}                      # value dtype / trailing shape of a mean (the single-rank result's form)
 
             def combiner(batch):
                 vals = batch.columns["v"]
                 if mean:
+                    if isinstance(vals, torch.Tensor) and "dt" not in vmeta:
+                        vmeta["dt"], vmeta["shape"] = vals.dtype, tuple(vals.shape[1:])
                     vals = _sum_count(vals)
                 fused = K.group_reduce(batch.columns["k"], vals, local_op)
                 if fused is not None:
@@ -694,8 +721,18 @@ class QueryEngine:
 
             recv = self._stream_shuffle(kv, None, "aggregate", combine=combiner, key=lambda b: None)
             reps, agg = self._reduce_kv(recv, merge_op, combine)
-            if mean and agg is not None:
-                agg = _mean_of(agg)
+            if mean:
+                # every rank learns the value form (a rank may receive groups without having had rows of its own)
+                dts = (torch.float16, torch.bfloat16, torch.float32, torch.float64)
+                dt0 = vmeta.get("dt")
+                code = dts.index(dt0) if dt0 in dts else (-1 if dt0 is not None else -2)   # -2: no rows seen
+                shp = list(vmeta.get("shape", ()))[:4]
+                got = self.ctx.all_gather_ints([code, len(shp)] + shp + [0] * (4 - len(shp)))
+                ref = next((x for x in got if x[0] != -2), None)
+                if agg is not None:
+                    dt = dts[ref[0]] if ref is not None and ref[0] >= 0 else torch.float64
+                    shape = tuple(ref[2: 2 + ref[1]]) if ref is not None else None
+                    agg = _mean_of(agg, dt, shape)
         if reps is None:
             state.materialized[out_ts] = []
             return
@@ -834,9 +871,12 @@ def _sum_count(vals):
     return torch.cat([flat, torch.ones(flat.shape[0], 1, dtype=torch.float64, device=flat.device)], 1)
 
 
-def _mean_of(sc):
-    """Merged (sum, count) columns -> the mean per group (1-D for a single value column)."""
-    m = sc[:, :-1] / sc[:, -1:]
+def _mean_of(sc, dtype=torch.float64, shape=None):
+    """Merged (sum, count) columns -> the mean per group, in the form the single-rank group-by gives: float values
+    keep their dtype (integer values average to float64) and the values' trailing shape."""
+    m = (sc[:, :-1] / sc[:, -1:]).to(dtype)
+    if shape is not None and len(shape) and int(torch.Size(shape).numel()) == m.shape[1]:
+        return m.reshape((m.shape[0],) + tuple(shape))
     return m.squeeze(1) if m.shape[1] == 1 else m
 
 

@@ -135,12 +135,22 @@ def join_match(build_h: torch.Tensor, probe_h: torch.Tensor) -> Tuple[torch.Tens
 
 
 # ------------------------------------------------------------------------------ exact grouping on the device
+_MAG = 0x7FFFFFFFFFFFFFFF
+
+
+def _float_word(bits: torch.Tensor) -> torch.Tensor:
+    """IEEE-754 double bits -> an int64 with the same ORDER as the values (negative magnitudes flipped); an
+    involution, so it also maps such a word back to the bits."""
+    return bits ^ ((bits >> 63) & _MAG)
+
+
 def _norm_col(c: torch.Tensor) -> torch.Tensor:
-    """1-D key column -> int64 words with value equality (floats by bits, -0.0 folded into +0.0)."""
+    """1-D key column -> int64 words with value equality AND value order (floats by an order-preserving transform
+    of their bits, -0.0 folded into +0.0), so groups sort like torch.unique(sorted=True)."""
     if c.dtype == torch.int64:
         return c.contiguous()
     if c.is_floating_point():
-        return (c.double() + 0.0).view(torch.int64)
+        return _float_word((c.double() + 0.0).view(torch.int64))
     return c.long()
 
 
@@ -227,7 +237,7 @@ def _rep_from_word(u: torch.Tensor, c):
     """A group's key column from its exact int64 word (inverse of _exact_words for one column)."""
     if isinstance(c, StringColumn):
         return StringColumn.from_short_codes(u, c.max_len())
-    return u.to(c.dtype) if not c.is_floating_point() else u.view(torch.float64).to(c.dtype)
+    return u.to(c.dtype) if not c.is_floating_point() else _float_word(u).view(torch.float64).to(c.dtype)
 
 
 def _rows_match_rep(cols, words, ref: torch.Tensor) -> bool:

@@ -248,7 +248,7 @@ class StreamingShuffle:
     # ------------------------------------------------------------------ driver
     def run(self, items: Iterator[Tuple[RecordBatch, torch.Tensor]]) -> Iterator[RecordBatch]:
         """Consume (batch, hash) pairs; yield received batches as rounds complete."""
-        if self.ws == 1:
+        if not self.ctx.distributed:
             for b, _ in items:
                 if b is not None and b.n:
                     yield b

@@ -25,7 +25,7 @@ def create_matrix_set(client, db: str, name: str, rows: int, cols: int, block_ro
     client.create_set(db, name, type_, dense=True)
     s: DenseMatrixSet = client.storage.get_set(db, name)
     ws, rank = client.ctx.world_size, client.ctx.rank
-    if partition_rows and ws > 1:
+    if partition_rows and client.ctx.distributed:
         nbr = math.ceil(rows / block_rows)
         per = math.ceil(nbr / ws)
         r0 = min(rows, rank * per * block_rows)

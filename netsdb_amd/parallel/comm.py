@@ -33,9 +33,14 @@ class ClusterContext:
     """Rank/device information of this process (a netsDB 'worker node')."""
 
     def __init__(self, rank: int = 0, world_size: int = 1, device: Optional[torch.device] = None,
-                 backend: Optional[str] = None, group=None):
+                 backend: Optional[str] = None, group=None, force_collectives: bool = False):
         self.rank = rank
         self.world_size = world_size
+        # force_collectives: a one-rank process group (RCCL world_size 1 plus the gloo metadata group) runs the
+        # multi-rank branches — streaming shuffles, partitioned joins / aggregations, all-gathers and
+        # reduce-scatters on device buffers — instead of short-circuiting them (the hardware test of the RCCL
+        # path on a one-GPU box; results must equal the single-process run)
+        self.force_collectives = bool(force_collectives) and dist.is_initialized()
         self.device = device if device is not None else torch.device("cpu")
         self.backend = backend
         self.group = group
@@ -56,7 +61,7 @@ class ClusterContext:
 
     @property
     def distributed(self) -> bool:
-        return self.world_size > 1
+        return self.world_size > 1 or self.force_collectives
 
     @staticmethod
     def from_env(device: Optional[str] = None, backend: Optional[str] = None) -> "ClusterContext":
@@ -65,6 +70,7 @@ class ClusterContext:
         ranks on one GPU)."""
         ws = int(os.environ.get("WORLD_SIZE", "1"))
         rank = int(os.environ.get("RANK", "0"))
+        force = os.environ.get("NSDB_FORCE_COLLECTIVES", "0") == "1"
         local = int(os.environ.get("LOCAL_RANK", "0"))
         device = device or os.environ.get("NSDB_DEVICE") or None
         backend = backend or os.environ.get("NSDB_DIST_BACKEND") or None
@@ -73,20 +79,20 @@ class ClusterContext:
         dev = torch.device(device)
         if dev.type == "cuda":
             torch.cuda.set_device(dev)
-        if ws > 1 and not dist.is_initialized():
+        if (ws > 1 or force) and not dist.is_initialized():
             be = backend or ("nccl" if dev.type == "cuda" else "gloo")
             kw = {}
             if dev.type == "cuda" and be == "nccl":
                 kw["device_id"] = dev
             dist.init_process_group(be, rank=rank, world_size=ws, **kw)
         be = dist.get_backend() if dist.is_initialized() else None
-        ctx = ClusterContext(rank, ws, dev, be)
+        ctx = ClusterContext(rank, ws, dev, be, force_collectives=force)
         ctx.attach_meta_group()
         return ctx
 
     def attach_meta_group(self):
         """Collective: create the gloo metadata group next to a RCCL data group."""
-        if self.backend == "nccl" and self.world_size > 1 and self.meta_group is None:
+        if self.backend == "nccl" and self.distributed and self.meta_group is None:
             try:
                 self.meta_group = dist.new_group(backend="gloo")
             except (RuntimeError, ValueError):      # no gloo transport: metadata stays on RCCL

@@ -203,6 +203,9 @@ class MatmulNode(Node):
                 dist_mode = "allgather_n"
             elif opA.part == "cols" or opB.part == "rows":
                 dist_mode = "kpartial"
+        if dist_mode != "local":
+            ds = engine.__dict__.setdefault("dist_stats", {})
+            ds[dist_mode] = ds.get(dist_mode, 0) + 1
         M, K, N = opA.rows, opA.cols, opB.cols
         if dist_mode == "local" and K != opB.rows:
             raise ValueError(f"fused matmul K mismatch {K} vs {opB.rows}")

@@ -49,9 +49,11 @@ class PhysicalPlan:
 
 class Planner:
     def __init__(self, size_of_scan: Callable[[dict], int], world_size: int = 1,
-                 broadcast_threshold: int = 2 << 30, copartitioned=()):
+                 broadcast_threshold: int = 2 << 30, copartitioned=(), distributed: Optional[bool] = None):
         self.size_of_scan = size_of_scan
         self.world_size = world_size
+        # collectives on (a one-rank group with ClusterContext(force_collectives=True) included)
+        self.distributed = world_size > 1 if distributed is None else distributed
         self.broadcast_threshold = broadcast_threshold
         # joins whose two inputs are already hash-placed by their join keys on every rank (Lachesis
         # co-partitioning): built and probed where the rows are, no shuffle of either side
@@ -88,7 +90,7 @@ class Planner:
                 left_sz, right_sz = est.get(a["input"]["name"], 0), est.get(a["input2"]["name"], 0)
                 build = "right" if right_sz <= left_sz else "left"
                 bsz = right_sz if build == "right" else left_sz
-                if self.world_size == 1:
+                if not self.distributed:
                     strat = "local"
                 elif a["output"]["name"] in self.copartitioned:
                     strat = "copartitioned"
@@ -211,10 +213,11 @@ class AdaptivePlanner:
     PENALTY = 1000.0
 
     def __init__(self, atoms: List[dict], size_of_scan: Callable[[dict], int], world_size: int = 1,
-                 broadcast_threshold: int = 2 << 30, copartitioned=()):
+                 broadcast_threshold: int = 2 << 30, copartitioned=(), distributed: Optional[bool] = None):
         self.atoms = atoms
         self.copartitioned = set(copartitioned)
         self.world_size = world_size
+        self.distributed = world_size > 1 if distributed is None else distributed
         self.broadcast_threshold = broadcast_threshold
         self.producer: Dict[str, dict] = {}
         self.consumers: Dict[str, List[dict]] = {}
@@ -322,7 +325,7 @@ class AdaptivePlanner:
                     return st, info
                 if not allow_build or (probed and not force):
                     return None, info
-                if self.world_size == 1:
+                if not self.distributed:
                     strat = "local"
                 elif name in self.copartitioned:
                     strat = "copartitioned"

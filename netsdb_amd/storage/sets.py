@@ -17,6 +17,7 @@ from __future__ import annotations
 import math
 import itertools
 import threading
+import weakref
 from typing import Dict, Iterator, List, Optional, Tuple
 
 import torch
@@ -379,6 +380,14 @@ class UserSet:
     SCAN_COALESCE_BYTES = 16 << 30
     COALESCE_ANY_DEVICE = False      # tests: run the merge on CPU pages too
 
+    def coalesce_cap(self) -> int:
+        """Merged-batch cap: SCAN_COALESCE_BYTES, but never more than the engine's out-of-core share of the node's
+        device budget (``coalesce_fraction`` of it, default 1/8): per-batch intermediates (join expansion, gathers,
+        group-by work buffers) scale with the merged batch and must stay inside what the spill logic assumes free."""
+        budget = getattr(self.manager, "device_budget", None) or (1 << 62)
+        frac = getattr(self.manager, "coalesce_fraction", 0.125)
+        return int(max(self.page_size, min(self.SCAN_COALESCE_BYTES, budget * frac)))
+
     def _coalesce_runs(self, pages, device) -> List[Tuple[int, int]]:
         """[i, j) runs of consecutive resident pages whose columns are adjacent slices of one buffer (checked once;
         the plan is cached while the pages and their resident batches stay the same objects)."""
@@ -386,9 +395,10 @@ class UserSet:
         if getattr(self, "_coalesce_key", None) == key:
             return self._coalesce_plan
         runs, i = [], 0
+        cap = self.coalesce_cap()
         while i < len(pages):
             j, nbytes = i, 0
-            while j < len(pages) and nbytes < self.SCAN_COALESCE_BYTES:
+            while j < len(pages) and nbytes < cap:
                 b = pages[j].batch
                 if b is None or not _same_device(b.device, device):
                     break
@@ -512,8 +522,9 @@ class DenseMatrixSet(UserSet):
         """A "model" panel (read-only weights by contract) unchanged since persist_pages wrote its image: evicting
         it needs no write (storage/manager.py cost model); its version counter catches in-place tensor writes."""
         t = self._panel
-        return (t is not None and getattr(self, "locality", "job") == "model" and self._clean_key is not None
-                and self._clean_key == (id(t), t._version))
+        key = self._clean_key
+        return (t is not None and getattr(self, "locality", "job") == "model" and key is not None
+                and key[0]() is t and key[1] == t._version)
 
     @property
     def panel(self) -> Optional[torch.Tensor]:
@@ -522,7 +533,7 @@ class DenseMatrixSet(UserSet):
             self.restore(geo)                          # clean drop: rebuild from the persisted chunks
             self.stats_io["reloads"] += 1
             if self._panel is not None:                # restored from the persisted image: clean again
-                self._clean_key = (id(self._panel), self._panel._version)
+                self._clean_key = (weakref.ref(self._panel), self._panel._version)
         if self._panel is None and self._spilled is not None:
             self.reload()
         if self._panel is not None:
@@ -534,7 +545,10 @@ class DenseMatrixSet(UserSet):
         self._install(t)
 
     def _install(self, t: Optional[torch.Tensor]):
+        # a new panel invalidates any persisted clean image: a dropped clean panel must never come back over it
         self._drop_spilled()
+        self._clean_geo = None
+        self._clean_key = None
         old = self._charged
         self._panel = t
         self._charged = 0
@@ -905,7 +919,7 @@ class DenseMatrixSet(UserSet):
             page += 1
         self.flushed_chunks = page
         t = self._panel
-        self._clean_key = (id(t), t._version) if t is not None else None
+        self._clean_key = (weakref.ref(t), t._version) if t is not None else None
 
     def geometry(self) -> dict:
         return {"total_rows": self.total_rows, "total_cols": self.total_cols, "block_rows": self.block_rows,
@@ -933,6 +947,7 @@ class DenseMatrixSet(UserSet):
         self.define(geo["total_rows"], geo["total_cols"], geo["block_rows"], geo["block_cols"],
                     row_offset=geo["row_offset"], local_rows=geo["local_rows"], dtype=getattr(torch, geo["dtype"]))
         self.replicated = geo.get("replicated", True)
+        self.transposed = False          # the persisted blocks are logical: the rebuilt panel is row-major
         self.add_batch(b)
         self.flushed_chunks = int(geo.get("chunks", 0))
         return self

@@ -128,13 +128,15 @@ def _build_ext_cls():
 
 
 def main():
+    # the product build: the host runtime + the kernel extension. The GEMM study extension (_hip_study, the
+    # diagnostic variants behind profiles/r2_gemm1_study .. r4_vendor) is opt-in: NSDB_BUILD=study
     which = os.environ.get("NSDB_BUILD", "all")
     exts = []
     if which in ("all", "native"):
         exts.append(native_ext())
     if which in ("all", "hip"):
         exts.append(hip_ext())
-    if which in ("all", "study"):
+    if which == "study":
         exts.append(study_ext())
     setup(
         name="netsdb_amd",

@@ -43,3 +43,15 @@ def test_bench_two_ranks_gloo():
     # weak scaling with a replicated model: the timed steps are rank-local (no collective inside a step; the
     # conv job's single-source plan skips the cluster-wide source sizing)
     assert d["config"]["collectives_per_step"] == 0
+
+
+def test_bench_self_launches_ranks():
+    """``bench.py --gpus 2`` without torchrun spawns its own two ranks (gloo on this CPU host) and reports n_gpus 2."""
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--small", "--steps", "2", "--warmup", "1"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _last_json(r.stdout)
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 * (64 + 4)
+    assert d["config"]["check"]["ok"] is True

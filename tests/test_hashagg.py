@@ -1,4 +1,4 @@
-"""Device hash-table group-by (csrc/kernels/hashagg.hip, ops path execution/kernels.py group_ids) vs
+"""Device hash-table group-by (csrc/kernels/relops.hip hash_aggregate, ops path execution/kernels.py group_ids) vs
 torch.unique(sorted=True, return_inverse=True) — the reference groups through C++ hash maps
 (src/queryExecution aggregation processors); the result must be the exact sorted distinct keys and inverse."""
 import pytest

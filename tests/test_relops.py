@@ -223,9 +223,16 @@ def test_string_keys_exact_under_hash_collisions_gpu(monkeypatch):
     inv2, reps2, ng2 = K.group_ids((col, nums))
     assert ng2 == len(set(zip(strs, nums.tolist())))
     vals = torch.ones(5000, device=DEV)
+    # forced collisions: the fused hash aggregation must refuse (its per-row check against the group's
+    # representative fails) so the engine takes the exact generic path; that path must then be exact
+    assert K.group_reduce(col, vals, "sum") is None
+    inv3, reps3, g3 = K.group_ids(col)
+    agg3 = K.segment_reduce(vals, inv3, g3, "sum")
+    assert sorted(zip(reps3.tolist(), agg3.tolist())) == sorted((s, float(strs.count(s))) for s in set(strs))
+    monkeypatch.setattr(StringColumn, "hash64", orig)          # no collisions: the fused path runs and is exact
     r = K.group_reduce(col, vals, "sum")
-    if r is not None:   # a hash-decided fused result must be exact too
-        assert sorted(zip(r[0].tolist(), r[1].tolist())) == sorted((s, float(strs.count(s))) for s in set(strs))
+    assert r is not None
+    assert sorted(zip(r[0].tolist(), r[1].tolist())) == sorted((s, float(strs.count(s))) for s in set(strs))
     m = col.isin(["longer-key1", "longer-key5"])
     assert m.tolist() == [s in ("longer-key1", "longer-key5") for s in strs]
 
