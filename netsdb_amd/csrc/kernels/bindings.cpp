@@ -69,6 +69,7 @@ int nsdb_str_gather(const void* src, const int64_t* starts, const int64_t* ends,
 }
 
 void register_relops(pybind11::module& m);
+void register_pipeline(pybind11::module& m);
 std::vector<torch::Tensor> hash_aggregate_impl(torch::Tensor keys, c10::optional<torch::Tensor> vals,
                                                const std::string& op, bool want_inv, int64_t low_threshold);
 
@@ -708,6 +709,7 @@ torch::Tensor block_simcount_partial(torch::Tensor pool, torch::Tensor cand, tor
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "netsdb_amd CDNA4 (gfx950) HIP kernels";
   register_relops(m);
+  register_pipeline(m);
   m.def("gemm_nt", &gemm_nt, "epi(alpha*A@B^T) on MFMA", py::arg("A"), py::arg("B"), py::arg("bias") = py::none(),
         py::arg("bias_mode") = 0, py::arg("act") = 0, py::arg("out_f32") = false, py::arg("alpha") = 1.0,
         py::arg("dropout") = 0.0, py::arg("seed") = 0, py::arg("splits") = 0, py::arg("out") = py::none(),

@@ -1,0 +1,383 @@
+// Fused relational pipeline: scan -> filter -> project -> low-cardinality group-by + aggregate in ONE pass over the
+// input columns (reference: src/lambdas/headers/Pipeline.h:57,194, which pushes each page through the whole chain
+// of executors while it is cache-resident; the executors are FilterExecutor / ApplyExecutor / the aggregation
+// HashSink, src/queryExecution/headers/AggregationProcessor.h:16).
+//
+// The stage's lambda trees (the selection predicate, the group key and the value row: makeLambdaFromMember, ==, <,
+// &&, ||, +, -, *, /, IN, LIKE prefix/suffix, CASE) are compiled on the host (execution/pipeline.py) into a short
+// register program that this kernel INTERPRETS per row in registers: no intermediate column (filter mask, value row,
+// key) is ever materialised in HBM. The program is ahead-of-time code (no run-time compilation); its interpretation
+// cost is amortised over ROWS rows per thread and the opcode / register indices are wave-uniform (kernel arguments,
+// scalar branches only).
+//
+//  * Register file: NREG virtual 64-bit registers per row slot as ONE vector value in VGPRs; the wave-uniform register
+//    number indexes it with indirect register addressing (s_set_gpr_idx_on + v_mov): no scratch, no per-register
+//    branches.
+//  * Columns are loaded straight into their registers: registers [0, ncol) hold the loaded columns. "Late" columns
+//    (read only by the key / value row) are loaded after the predicate, for the kept rows only (a wave skips the
+//    cache lines none of its kept rows needs).
+//  * Aggregation: each thread keeps KSLOT (key, count, F values) slots in registers (few groups hit them every
+//    row); a row whose key is in no slot goes to the workgroup's LDS hash table (CAP slots, 64-bit CAS + LDS float
+//    atomics). At the end the slots are flushed into the LDS table, and the workgroup writes its occupied entries
+//    (compacted) to a per-workgroup partial; the host merges the partials (a few thousand rows). A workgroup whose
+//    table overflows raises status[0]: the stage then runs the unfused path (more groups than this kernel is for).
+#include "common.h"
+
+namespace nsdb_pipe {
+
+constexpr int NREG = 16, ROWS = 2, MAXINS = 48, MAXCOL = 10, FMAX = 8, KSLOT = 4, CAP = 256, NTHR = 256;
+constexpr long long EMPTY = (long long)0x8000000000000000ULL;
+constexpr int IMM_REG = -2;            // operand register meaning "the instruction's immediate"
+
+enum Op : int {
+  OP_NOP = 0, OP_CONST, OP_ADDF, OP_SUBF, OP_MULF, OP_DIVF, OP_ADDI, OP_SUBI, OP_MULI, OP_I2F,
+  OP_LTF, OP_LEF, OP_GTF, OP_GEF, OP_EQF, OP_NEF, OP_LTI, OP_LEI, OP_GTI, OP_GEI, OP_EQI, OP_NEI,
+  OP_AND, OP_OR, OP_NOT, OP_PACK, OP_SEQ, OP_SPRE, OP_SSUF, OP_SEL, OP_NEGF
+};
+enum ColKind : int { C_F64 = 0, C_I64, C_I32, C_F32, C_U8, C_SCODE, C_SREF };
+
+struct Ins {
+  int op, dst, a, b;
+  long long imm;
+};
+struct Col {
+  const void* p;                 // numeric column
+  const long long* st;           // string column: row starts / ends into dat
+  const long long* en;
+  const unsigned char* dat;
+  int kind, late, L, pad;
+};
+struct PipeArgs {
+  Ins ins[MAXINS];
+  Col col[MAXCOL];
+  const unsigned char* lit;      // literal pool of the string ops
+  long long n;
+  int nins_a, nins, ncol, keep_reg, key_reg, nval, agg_op, pad;
+  int val_reg[FMAX];
+  long long* out_key;            // [nwg][CAP]
+  unsigned long long* out_cnt;   // [nwg][CAP]
+  double* out_val;               // [nwg][CAP][FMAX]
+  int* out_occ;                  // [nwg]
+  int* status;                   // [0] overflow
+};
+
+typedef unsigned long long u64;
+// The register file of one row slot: NREG 64-bit registers as ONE vector value (NREG VGPR pairs).
+typedef unsigned long long regfile __attribute__((ext_vector_type(NREG)));
+
+__device__ __forceinline__ double u2f(u64 x) { return __longlong_as_double((long long)x); }
+__device__ __forceinline__ u64 f2u(double x) { return (u64)__double_as_longlong(x); }
+
+// Short-string code exactly as StringColumn.short_codes / str_pack (bytes big-endian in the low 8L bits, << 3 | len)
+__device__ __forceinline__ u64 short_code(const unsigned char* d, long long s, long long e, int L) {
+  const long long len = e - s;
+  if (len > L) return (u64)-1;
+  u64 c = 0;
+  for (int b = 0; b < L; ++b) c |= (b < len ? (u64)d[s + b] : 0ull) << (8 * (L - 1 - b));
+  return (c << 3) | (u64)len;
+}
+
+// Column c into register c of every row slot (masked: rows not in `m` load nothing).
+__device__ __forceinline__ void load_col(const Col& c, int reg, const long long (&row)[ROWS], const bool (&m)[ROWS],
+                                         regfile (&R)[ROWS]) {
+  u64 x[ROWS];
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j) {
+    x[j] = 0;
+    if (m[j]) {
+      const long long i = row[j];
+      switch (c.kind) {
+        case C_F64: x[j] = reinterpret_cast<const u64*>(c.p)[i]; break;
+        case C_I64: x[j] = reinterpret_cast<const u64*>(c.p)[i]; break;
+        case C_I32: x[j] = (u64)(long long)reinterpret_cast<const int*>(c.p)[i]; break;
+        case C_F32: x[j] = f2u((double)reinterpret_cast<const float*>(c.p)[i]); break;
+        case C_U8: x[j] = (u64)reinterpret_cast<const unsigned char*>(c.p)[i]; break;
+        case C_SCODE: x[j] = short_code(c.dat, c.st[i], c.en[i], c.L); break;
+        default: {                          // C_SREF: (start << 24) | length
+          const long long s = c.st[i], e = c.en[i];
+          x[j] = ((u64)s << 24) | (u64)min(e - s, (long long)0xFFFFFF);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j) R[j][reg] = x[j];
+}
+
+__device__ __forceinline__ bool str_match(const unsigned char* d, u64 ref, const unsigned char* lit, long long imm,
+                                          int mode) {
+  const long long s = (long long)(ref >> 24);
+  const int len = (int)(ref & 0xFFFFFF);
+  const unsigned char* l = lit + (imm >> 16);
+  const int ll = (int)(imm & 0xFFFF);
+  if (mode == 0 ? len != ll : len < ll) return false;
+  const long long o = mode == 2 ? s + len - ll : s;     // suffix: compare the last ll bytes
+  for (int b = 0; b < ll; ++b)
+    if (d[o + b] != l[b]) return false;
+  return true;
+}
+
+__device__ __forceinline__ u64 operand(const regfile& R, int k, long long imm) {
+  return k == IMM_REG ? (u64)imm : (k >= 0 ? R[k] : 0ull);
+}
+
+// Instructions [lo, hi) of the program over every row slot. The opcode and register numbers are kernel arguments
+// (SGPRs): one scalar dispatch per instruction, indirect register reads / writes.
+__device__ __forceinline__ void run(const PipeArgs& a, regfile (&R)[ROWS], int lo, int hi) {
+  for (int pc = lo; pc < hi; ++pc) {
+    const int op = a.ins[pc].op, dst = a.ins[pc].dst, ia = a.ins[pc].a, ib = a.ins[pc].b;
+    const long long imm = a.ins[pc].imm;
+    u64 x[ROWS], y[ROWS], z[ROWS];
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      x[j] = operand(R[j], ia, imm);
+      y[j] = operand(R[j], ib, imm);
+    }
+    switch (op) {
+#define NSDB_EACH(E)                                          \
+  _Pragma("unroll") for (int j = 0; j < ROWS; ++j) {          \
+    const double fx = u2f(x[j]), fy = u2f(y[j]);              \
+    const long long sx = (long long)x[j], sy = (long long)y[j]; \
+    (void)fx; (void)fy; (void)sx; (void)sy;                   \
+    z[j] = (E);                                               \
+  }                                                           \
+  break;
+      case OP_CONST: NSDB_EACH((u64)imm)
+      case OP_ADDF: NSDB_EACH(f2u(fx + fy))
+      case OP_SUBF: NSDB_EACH(f2u(fx - fy))
+      case OP_MULF: NSDB_EACH(f2u(fx * fy))
+      case OP_DIVF: NSDB_EACH(f2u(fx / fy))
+      case OP_NEGF: NSDB_EACH(f2u(-fx))
+      case OP_ADDI: NSDB_EACH((u64)(sx + sy))
+      case OP_SUBI: NSDB_EACH((u64)(sx - sy))
+      case OP_MULI: NSDB_EACH((u64)(sx * sy))
+      case OP_I2F: NSDB_EACH(f2u((double)sx))
+      case OP_LTF: NSDB_EACH((u64)(fx < fy))
+      case OP_LEF: NSDB_EACH((u64)(fx <= fy))
+      case OP_GTF: NSDB_EACH((u64)(fx > fy))
+      case OP_GEF: NSDB_EACH((u64)(fx >= fy))
+      case OP_EQF: NSDB_EACH((u64)(fx == fy))
+      case OP_NEF: NSDB_EACH((u64)(fx != fy))
+      case OP_LTI: NSDB_EACH((u64)(sx < sy))
+      case OP_LEI: NSDB_EACH((u64)(sx <= sy))
+      case OP_GTI: NSDB_EACH((u64)(sx > sy))
+      case OP_GEI: NSDB_EACH((u64)(sx >= sy))
+      case OP_EQI: NSDB_EACH((u64)(sx == sy))
+      case OP_NEI: NSDB_EACH((u64)(sx != sy))
+      case OP_AND: NSDB_EACH((u64)((x[j] != 0) & (y[j] != 0)))
+      case OP_OR: NSDB_EACH((u64)((x[j] != 0) | (y[j] != 0)))
+      case OP_NOT: NSDB_EACH((u64)(x[j] == 0))
+      case OP_PACK: NSDB_EACH((x[j] << (imm & 63)) | y[j])
+      case OP_SEL: NSDB_EACH(x[j] ? y[j] : R[j][(int)imm])                // z = x ? y : r[imm]
+      case OP_SEQ:
+      case OP_SPRE:
+      case OP_SSUF: {                                      // ib: the column whose bytes x refers to
+        const unsigned char* d = a.col[ib].dat;
+        const int mode = op == OP_SEQ ? 0 : (op == OP_SPRE ? 1 : 2);
+#pragma unroll
+        for (int j = 0; j < ROWS; ++j) z[j] = str_match(d, x[j], a.lit, imm, mode) ? 1ull : 0ull;
+        break;
+      }
+      default:
+#pragma unroll
+        for (int j = 0; j < ROWS; ++j) z[j] = 0;
+#undef NSDB_EACH
+    }
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) R[j][dst] = z[j];
+  }
+}
+
+__device__ __forceinline__ unsigned slot_hash(long long k) {
+  u64 z = (u64)k * 0x9E3779B97F4A7C15ull;
+  return (unsigned)(z >> 40);
+}
+
+__device__ __forceinline__ void lds_acc(double* p, double v, int op) {
+  if (op == 0) {
+    atomicAdd(p, v);
+    return;
+  }
+  unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+  unsigned long long old = *q;
+  while (true) {
+    const double cur = __longlong_as_double((long long)old);
+    const double nv = op == 1 ? fmin(cur, v) : fmax(cur, v);
+    if (nv == cur) return;
+    const unsigned long long got = atomicCAS(q, old, (unsigned long long)__double_as_longlong(nv));
+    if (got == old) return;
+    old = got;
+  }
+}
+
+template <int F>
+__device__ __forceinline__ void lds_insert(long long* tk, unsigned long long* tc, double* tv, int* ovf, long long key,
+                                           unsigned long long cnt, const double (&v)[F], int nval, int op) {
+  if (key == EMPTY) {
+    *ovf = 1;
+    return;
+  }
+  unsigned h = slot_hash(key) & (CAP - 1);
+  for (int p = 0; p < CAP; ++p) {
+    const long long prev = (long long)atomicCAS(reinterpret_cast<unsigned long long*>(tk + h), (unsigned long long)EMPTY,
+                                                (unsigned long long)key);
+    if (prev == EMPTY || prev == key) {
+      atomicAdd(tc + h, cnt);
+#pragma unroll
+      for (int f = 0; f < F; ++f)
+        if (f < nval) lds_acc(tv + h * FMAX + f, v[f], op);
+      return;
+    }
+    h = (h + 1) & (CAP - 1);
+  }
+  *ovf = 1;
+}
+
+__device__ __forceinline__ double acc_op(double a, double b, int op) {
+  return op == 0 ? a + b : (op == 1 ? fmin(a, b) : fmax(a, b));
+}
+
+template <int F>
+__global__ void __launch_bounds__(NTHR) pipe_agg_kernel(const PipeArgs a) {
+  __shared__ long long tk[CAP];
+  __shared__ unsigned long long tc[CAP];
+  __shared__ double tv[CAP * FMAX];
+  __shared__ int s_ovf, s_occ;
+  const int tid = threadIdx.x;
+  const double init = a.agg_op == 0 ? 0.0 : (a.agg_op == 1 ? __builtin_inf() : -__builtin_inf());
+  for (int i = tid; i < CAP; i += NTHR) {
+    tk[i] = EMPTY;
+    tc[i] = 0;
+  }
+  for (int i = tid; i < CAP * FMAX; i += NTHR) tv[i] = init;
+  if (tid == 0) {
+    s_ovf = 0;
+    s_occ = 0;
+  }
+  __syncthreads();
+
+  regfile R[ROWS];
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j) R[j] = (regfile)0;
+  long long sk[KSLOT];
+  unsigned long long sc[KSLOT];
+  double sv[KSLOT][F];
+  int used = 0;
+#pragma unroll
+  for (int s = 0; s < KSLOT; ++s) {
+    sk[s] = EMPTY;
+    sc[s] = 0;
+#pragma unroll
+    for (int f = 0; f < F; ++f) sv[s][f] = init;
+  }
+
+  const long long step = (long long)gridDim.x * NTHR * ROWS;
+  for (long long base = (long long)blockIdx.x * NTHR * ROWS; base < a.n; base += step) {
+    long long row[ROWS];
+    bool inr[ROWS], keep[ROWS];
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      row[j] = base + (long long)j * NTHR + tid;
+      inr[j] = row[j] < a.n;
+    }
+    // the predicate's ("early") columns, every load issued before any is used, then the predicate program
+    for (int c = 0; c < a.ncol; ++c)
+      if (!a.col[c].late) load_col(a.col[c], c, row, inr, R);
+    run(a, R, 0, a.nins_a);
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      keep[j] = inr[j] && (a.keep_reg < 0 || R[j][a.keep_reg] != 0);
+      any |= keep[j];
+    }
+    if (!__builtin_amdgcn_ballot_w64(any)) continue;           // no kept row in this wave
+    // late columns for the kept rows only, then the key / value program
+    for (int c = 0; c < a.ncol; ++c)
+      if (a.col[c].late) load_col(a.col[c], c, row, keep, R);
+    run(a, R, a.nins_a, a.nins);
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      if (!keep[j]) continue;
+      const long long key = a.key_reg < 0 ? 0 : (long long)R[j][a.key_reg];   // key_reg < 0: one global group
+      double v[F];
+#pragma unroll
+      for (int f = 0; f < F; ++f) v[f] = f < a.nval ? u2f(R[j][a.val_reg[f]]) : 0.0;
+      bool done = false;
+#pragma unroll
+      for (int s = 0; s < KSLOT; ++s) {
+        if (!done && s < used && sk[s] == key) {
+#pragma unroll
+          for (int f = 0; f < F; ++f) sv[s][f] = acc_op(sv[s][f], v[f], a.agg_op);
+          sc[s] += 1;
+          done = true;
+        }
+      }
+      if (!done && used < KSLOT) {
+#pragma unroll
+        for (int s = 0; s < KSLOT; ++s) {
+          if (!done && s == used) {
+            sk[s] = key;
+            sc[s] = 1;
+#pragma unroll
+            for (int f = 0; f < F; ++f) sv[s][f] = v[f];
+            done = true;
+          }
+        }
+        ++used;
+      }
+      if (!done) lds_insert<F>(tk, tc, tv, &s_ovf, key, 1, v, a.nval, a.agg_op);
+    }
+  }
+  // flush the register slots
+#pragma unroll
+  for (int s = 0; s < KSLOT; ++s)
+    if (s < used) lds_insert<F>(tk, tc, tv, &s_ovf, sk[s], sc[s], sv[s], a.nval, a.agg_op);
+  __syncthreads();
+  // occupied entries, compacted, to this workgroup's partial
+  const long long wg = blockIdx.x;
+  for (int i = tid; i < CAP; i += NTHR) {
+    if (tk[i] == EMPTY) continue;
+    const int pos = atomicAdd(&s_occ, 1);
+    const long long o = wg * CAP + pos;
+    a.out_key[o] = tk[i];
+    a.out_cnt[o] = tc[i];
+#pragma unroll
+    for (int f = 0; f < FMAX; ++f) a.out_val[o * FMAX + f] = tv[i * FMAX + f];
+  }
+  __syncthreads();
+  if (tid == 0) {
+    a.out_occ[wg] = s_occ;
+    if (s_ovf) atomicOr(a.status, 1);
+  }
+}
+
+}  // namespace nsdb_pipe
+
+extern "C" {
+
+int nsdb_pipe_sizes(int* out) {
+  out[0] = nsdb_pipe::MAXINS;
+  out[1] = nsdb_pipe::MAXCOL;
+  out[2] = nsdb_pipe::NREG;
+  out[3] = nsdb_pipe::FMAX;
+  out[4] = nsdb_pipe::CAP;
+  out[5] = (int)sizeof(nsdb_pipe::PipeArgs);
+  out[6] = nsdb_pipe::ROWS;
+  out[7] = nsdb_pipe::NTHR;
+  return 0;
+}
+
+// args: a host PipeArgs image (the binding fills it field by field); grid = number of workgroups.
+int nsdb_pipe_agg(const void* args, int grid, hipStream_t st) {
+  if (grid <= 0) return -1;
+  const nsdb_pipe::PipeArgs& a = *reinterpret_cast<const nsdb_pipe::PipeArgs*>(args);
+  if (a.nins > nsdb_pipe::MAXINS || a.ncol > nsdb_pipe::MAXCOL || a.nval > nsdb_pipe::FMAX || a.nins_a > a.nins)
+    return -2;
+  if (a.nval <= 2)
+    hipLaunchKernelGGL(nsdb_pipe::pipe_agg_kernel<2>, dim3(grid), dim3(nsdb_pipe::NTHR), 0, st, a);
+  else
+    hipLaunchKernelGGL(nsdb_pipe::pipe_agg_kernel<nsdb_pipe::FMAX>, dim3(grid), dim3(nsdb_pipe::NTHR), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

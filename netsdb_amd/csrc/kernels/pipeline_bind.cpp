@@ -1,0 +1,180 @@
+// PyTorch binding of the fused relational pipeline kernel (pipeline.hip). The program, the column table and the
+// aggregation are validated on the host — register / column / literal indices in range, every column on the
+// device with at least n rows and the dtype its kind reads — before the argument image is built and launched on
+// the current HIP stream.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+#include <tuple>
+#include <vector>
+
+extern "C" {
+int nsdb_pipe_sizes(int* out);
+int nsdb_pipe_agg(const void* args, int grid, hipStream_t st);
+}
+
+namespace {
+
+// host mirror of nsdb_pipe::PipeArgs (layout checked against the kernel's sizeof at first use)
+constexpr int MAXINS = 48, MAXCOL = 10, FMAX = 8;
+struct Ins {
+  int op, dst, a, b;
+  long long imm;
+};
+struct Col {
+  const void* p;
+  const long long* st;
+  const long long* en;
+  const unsigned char* dat;
+  int kind, late, L, pad;
+};
+struct PipeArgs {
+  Ins ins[MAXINS];
+  Col col[MAXCOL];
+  const unsigned char* lit;
+  long long n;
+  int nins_a, nins, ncol, keep_reg, key_reg, nval, agg_op, pad;
+  int val_reg[FMAX];
+  long long* out_key;
+  unsigned long long* out_cnt;
+  double* out_val;
+  int* out_occ;
+  int* status;
+};
+
+enum ColKind : int { C_F64 = 0, C_I64, C_I32, C_F32, C_U8, C_SCODE, C_SREF };
+enum : int { OP_SEQ = 26, OP_SPRE = 27, OP_SSUF = 28, OP_SEL = 29, OP_LAST = 30 };
+
+int sizes(int i) {
+  static int s[8] = {0};
+  static bool init = false;
+  if (!init) {
+    nsdb_pipe_sizes(s);
+    init = true;
+  }
+  return s[i];
+}
+
+void check_col(const torch::Tensor& t, int64_t n, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "pipe_agg: ", what, " must be a contiguous device tensor");
+  TORCH_CHECK(t.numel() >= n, "pipe_agg: ", what, " has fewer than n rows");
+}
+
+// prog: int64 [nins, 5] (op, dst, a, b, imm) on the CPU.
+// cols: per column (kind, late, L, data, starts, ends, bytes): data for numeric kinds, starts / ends / bytes for strings.
+std::vector<torch::Tensor> pipe_agg(torch::Tensor prog, int64_t nins_a,
+                                    std::vector<std::tuple<int64_t, int64_t, int64_t, c10::optional<torch::Tensor>,
+                                                           c10::optional<torch::Tensor>, c10::optional<torch::Tensor>,
+                                                           c10::optional<torch::Tensor>>> cols,
+                                    torch::Tensor lit, int64_t n, int64_t keep_reg, int64_t key_reg,
+                                    std::vector<int64_t> val_regs, int64_t agg_op, int64_t max_wg) {
+  TORCH_CHECK(sizes(0) == MAXINS && sizes(1) == MAXCOL && sizes(3) == FMAX && sizes(5) == (int)sizeof(PipeArgs),
+              "pipe_agg: host / kernel argument layout mismatch");
+  const int NREG = sizes(2), CAP = sizes(4), ROWS = sizes(6), NTHR = sizes(7);
+  TORCH_CHECK(prog.device().is_cpu() && prog.scalar_type() == torch::kInt64 && prog.dim() == 2 && prog.size(1) == 5,
+              "pipe_agg: prog must be a CPU int64 [nins, 5] tensor");
+  const int nins = (int)prog.size(0), ncol = (int)cols.size(), nval = (int)val_regs.size();
+  TORCH_CHECK(nins <= MAXINS && ncol <= MAXCOL && ncol <= NREG && nval <= FMAX && nval >= 0, "pipe_agg: too large");
+  TORCH_CHECK(nins_a >= 0 && nins_a <= nins, "pipe_agg: bad nins_a");
+  TORCH_CHECK(n >= 0, "pipe_agg: n < 0");
+  TORCH_CHECK(agg_op >= 0 && agg_op <= 2, "pipe_agg: agg_op is 0 sum, 1 min, 2 max");
+  TORCH_CHECK(keep_reg >= -1 && keep_reg < NREG && key_reg >= -1 && key_reg < NREG, "pipe_agg: bad keep/key reg");
+  TORCH_CHECK(lit.is_cuda() && lit.scalar_type() == torch::kUInt8 && lit.is_contiguous(), "pipe_agg: lit");
+  PipeArgs a;
+  std::memset(&a, 0, sizeof(a));
+  auto P = prog.accessor<int64_t, 2>();
+  for (int i = 0; i < nins; ++i) {
+    Ins& I = a.ins[i];
+    I.op = (int)P[i][0];
+    I.dst = (int)P[i][1];
+    I.a = (int)P[i][2];
+    I.b = (int)P[i][3];
+    I.imm = P[i][4];
+    TORCH_CHECK(I.op >= 0 && I.op <= OP_LAST, "pipe_agg: bad opcode at ", i);
+    TORCH_CHECK(I.dst >= 0 && I.dst < NREG && I.a >= -2 && I.a < NREG && I.b >= -2 && I.b < NREG,
+                "pipe_agg: register out of range at ", i);
+    if (I.op == OP_SEL) TORCH_CHECK(I.imm >= 0 && I.imm < NREG, "pipe_agg: select register at ", i);
+    if (I.op == OP_SEQ || I.op == OP_SPRE || I.op == OP_SSUF) {
+      TORCH_CHECK(I.b >= 0 && I.b < ncol && std::get<0>(cols[I.b]) == C_SREF, "pipe_agg: string op column at ", i);
+      const long long off = I.imm >> 16, len = I.imm & 0xFFFF;
+      TORCH_CHECK(off >= 0 && off + len <= lit.numel(), "pipe_agg: literal out of the pool at ", i);
+    }
+  }
+  a.nins = nins;
+  a.nins_a = (int)nins_a;
+  for (int c = 0; c < ncol; ++c) {
+    auto& t = cols[c];
+    Col& C = a.col[c];
+    C.kind = (int)std::get<0>(t);
+    C.late = (int)std::get<1>(t);
+    C.L = (int)std::get<2>(t);
+    TORCH_CHECK(C.kind >= C_F64 && C.kind <= C_SREF, "pipe_agg: bad column kind");
+    if (C.kind == C_SCODE || C.kind == C_SREF) {
+      TORCH_CHECK(std::get<4>(t).has_value() && std::get<5>(t).has_value() && std::get<6>(t).has_value(),
+                  "pipe_agg: string column needs starts / ends / bytes");
+      const auto &s = *std::get<4>(t), &e = *std::get<5>(t), &d = *std::get<6>(t);
+      check_col(s, n, "starts");
+      check_col(e, n, "ends");
+      TORCH_CHECK(s.scalar_type() == torch::kInt64 && e.scalar_type() == torch::kInt64, "pipe_agg: starts/ends int64");
+      TORCH_CHECK(d.is_cuda() && d.scalar_type() == torch::kUInt8, "pipe_agg: string bytes must be device uint8");
+      TORCH_CHECK(C.kind != C_SCODE || (C.L >= 0 && C.L <= 7), "pipe_agg: short code length bound 0..7");
+      C.st = reinterpret_cast<const long long*>(s.data_ptr<int64_t>());
+      C.en = reinterpret_cast<const long long*>(e.data_ptr<int64_t>());
+      C.dat = d.data_ptr<uint8_t>();
+    } else {
+      TORCH_CHECK(std::get<3>(t).has_value(), "pipe_agg: numeric column needs data");
+      const auto& x = *std::get<3>(t);
+      check_col(x, n, "column");
+      const auto st = x.scalar_type();
+      const bool ok = (C.kind == C_F64 && st == torch::kFloat64) || (C.kind == C_I64 && st == torch::kInt64) ||
+                      (C.kind == C_I32 && st == torch::kInt32) || (C.kind == C_F32 && st == torch::kFloat32) ||
+                      (C.kind == C_U8 && (st == torch::kUInt8 || st == torch::kBool));
+      TORCH_CHECK(ok, "pipe_agg: column dtype does not match its kind");
+      C.p = x.data_ptr();
+    }
+  }
+  a.ncol = ncol;
+  a.lit = lit.data_ptr<uint8_t>();
+  a.n = n;
+  a.keep_reg = (int)keep_reg;
+  a.key_reg = (int)key_reg;
+  a.nval = nval;
+  for (int f = 0; f < nval; ++f) {
+    TORCH_CHECK(val_regs[f] >= 0 && val_regs[f] < NREG, "pipe_agg: bad value register");
+    a.val_reg[f] = (int)val_regs[f];
+  }
+  a.agg_op = (int)agg_op;
+  const long long per = (long long)NTHR * ROWS * 4;
+  const int nwg = (int)std::max<long long>(1, std::min<long long>(max_wg > 0 ? max_wg : 2048, (n + per - 1) / per));
+  auto dev = lit.device();
+  auto i64 = torch::TensorOptions().dtype(torch::kInt64).device(dev);
+  auto out_key = torch::empty({(long long)nwg * CAP}, i64);
+  auto out_cnt = torch::empty({(long long)nwg * CAP}, i64);
+  auto out_val = torch::empty({(long long)nwg * CAP, FMAX}, i64.dtype(torch::kFloat64));
+  auto out_occ = torch::zeros({nwg}, i64.dtype(torch::kInt32));
+  auto status = torch::zeros({1}, i64.dtype(torch::kInt32));
+  a.out_key = reinterpret_cast<long long*>(out_key.data_ptr<int64_t>());
+  a.out_cnt = reinterpret_cast<unsigned long long*>(out_cnt.data_ptr<int64_t>());
+  a.out_val = out_val.data_ptr<double>();
+  a.out_occ = out_occ.data_ptr<int>();
+  a.status = status.data_ptr<int>();
+  if (n > 0) {
+    const int rc = nsdb_pipe_agg(&a, nwg, c10::hip::getCurrentHIPStream().stream());
+    TORCH_CHECK(rc == 0, "pipe_agg launch failed: ", rc);
+  }
+  return {out_key, out_cnt, out_val, out_occ, status};
+}
+
+}  // namespace
+
+void register_pipeline(pybind11::module& m) {
+  m.def("pipe_agg", &pipe_agg,
+        "fused scan -> filter -> project -> low-cardinality aggregate (pipeline.hip): per-workgroup partial "
+        "(keys, counts, values[.., 8], occupancy, status[overflow])",
+        pybind11::arg("prog"), pybind11::arg("nins_a"), pybind11::arg("cols"), pybind11::arg("lit"), pybind11::arg("n"),
+        pybind11::arg("keep_reg"), pybind11::arg("key_reg"), pybind11::arg("val_regs"), pybind11::arg("agg_op") = 0,
+        pybind11::arg("max_wg") = 0);
+}

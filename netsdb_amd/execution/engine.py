@@ -128,13 +128,16 @@ class QueryEngine:
         self.operand_prefetch = True
         self.last_tcap = None
         self._last_comps = None
+        # fused filter -> project -> aggregate stages (execution/pipeline.py, csrc/kernels/pipeline.hip)
+        self.fused_pipelines = True
+        self.pipeline_stats = {"fused_stages": 0, "fused_batches": 0, "fallback_batches": 0}
 
     def clone(self) -> "QueryEngine":
         """An engine for another job lane: same storage, context, catalog, tracer, configuration and plan cache
         (dict access under the GIL); its own per-job state (spools, statistics)."""
         e = QueryEngine(self.storage, self.ctx, self.catalog, self.tracer, self.broadcast_threshold, self.fusion)
         for k in ("adaptive", "plan_cache_enabled", "ooc_fraction", "shuffle_chunk_bytes",
-                  "operand_prefetch"):
+                  "operand_prefetch", "fused_pipelines"):
             setattr(e, k, getattr(self, k))
         e._plan_cache = self._plan_cache
         e.__dict__["meta_cache"] = self.__dict__.setdefault("meta_cache", {})
@@ -334,6 +337,15 @@ class QueryEngine:
             else:
                 segments[-1].append(o)
         rows = [0]
+        # a stage ending in an aggregation whose trailing atoms are lambda trees runs them as ONE fused launch per
+        # batch (filter -> key / value row -> per-workgroup pre-aggregation); the atoms before them run as usual
+        fplan = None
+        if self.fused_pipelines and st.sink.get("kind") == "aggregate":
+            from . import pipeline as PL
+
+            fplan = PL.plan_stage(segments[-1], state.comps, st.sink["atom"])
+            if fplan is not None:
+                segments[-1] = fplan.prefix
 
         def source():
             for b in self._source_batches(st, state):
@@ -355,8 +367,34 @@ class QueryEngine:
                     it = self._grace_probe(probe, it, pb, hcol, state)
                     ops = seg[1:]
             it = self._apply_ops(ops, it, state)
+        if fplan is not None:
+            it = self._fused_stream(fplan, it, state)
         self._sink(st, it, state)
         return rows[0]
+
+    def _fused_stream(self, fplan, it, state):
+        """Batches through a fused stage suffix: one pipeline launch each (pre-aggregated key / value batch out), or
+        the suffix's atoms eagerly for a batch the kernel does not take."""
+        from . import pipeline as PL
+
+        used = False
+        for b in it:
+            if b is None or b.n == 0:
+                continue
+            r = PL.run_batch(fplan, b)
+            if r is not None:
+                used = True
+                self.pipeline_stats["fused_batches"] += 1
+                yield r
+                continue
+            self.pipeline_stats["fallback_batches"] += 1
+            for o in fplan.suffix:
+                if b.n == 0:
+                    break
+                b = self._apply_atom(o, b, state)
+            yield b
+        if used:
+            self.pipeline_stats["fused_stages"] += 1
 
     def _apply_ops(self, ops, it, state):
         """Stream batches through a segment's atoms (generator: one page in flight per stage)."""

@@ -1,0 +1,794 @@
+"""Fused relational pipelines: a stage's filter -> project -> low-cardinality aggregate compiled into ONE device pass.
+
+Reference: src/lambdas/headers/Pipeline.h:57,194 (a page goes through the whole chain of executors while it is
+cache-resident) with the FilterExecutor / ApplyExecutor / aggregation HashSink of the chain
+(src/queryExecution/headers/AggregationProcessor.h:16); the TPC-H selections are lambda trees
+(src/tpch/headers/Query01.h, Query06.h: makeLambdaFromMember, ==, &&, arithmetic).
+
+The eager engine evaluates every APPLY atom of a stage as its own whole-column operation, so a scan-heavy stage
+materialises each intermediate (the filter mask, every comparison, every product of the value row) as a full-length
+column in HBM. When a stage ends in an aggregation and every atom after its last join is a lambda-tree node this
+module understands (member access, literals, + - * /, comparisons, && || !, string ==, IN, LIKE prefix / suffix,
+CASE, and the ``Values`` / ``KeyTuple`` rows of the aggregate), the atoms are compiled into a short register
+program for the device interpreter kernel ``pipe_agg`` (csrc/kernels/pipeline.hip): one launch reads each input
+column once, evaluates the predicate, key and value row per row in registers, pre-aggregates into per-workgroup
+tables, and only the per-workgroup partials (a few thousand rows) reach the merge. A batch whose groups overflow the
+kernel's tables, or whose columns are of a kind the kernel does not read, runs the eager atoms instead.
+
+Program (mirrors pipeline.hip): registers [0, ncol) hold the loaded columns (numeric: f64 / i64 / i32 / f32 / u8;
+strings: an exact short code for keys, or a (start, length) reference for byte comparisons), the temporaries follow.
+Segment A computes the keep mask from the predicate's ("early") columns; the key / value columns that only segment B
+reads are loaded for the kept rows only.
+"""
+from __future__ import annotations
+
+import struct
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from .. import _ext
+from ..lambdas import AttAccess, Binary, IsIn, KeyTuple, Like, Literal, Select, Unary, Values
+from ..objects.record import RecordBatch
+from ..objects.strings import StringColumn
+
+# ---- must match pipeline.hip ----------------------------------------------------------------------------------
+NREG, MAXINS, MAXCOL, FMAX = 16, 48, 10, 8
+IMM = -2                       # operand register number meaning "the instruction's immediate"
+(OP_NOP, OP_CONST, OP_ADDF, OP_SUBF, OP_MULF, OP_DIVF, OP_ADDI, OP_SUBI, OP_MULI, OP_I2F,
+ OP_LTF, OP_LEF, OP_GTF, OP_GEF, OP_EQF, OP_NEF, OP_LTI, OP_LEI, OP_GTI, OP_GEI, OP_EQI, OP_NEI,
+ OP_AND, OP_OR, OP_NOT, OP_PACK, OP_SEQ, OP_SPRE, OP_SSUF, OP_SEL, OP_NEGF) = range(31)
+C_F64, C_I64, C_I32, C_F32, C_U8, C_SCODE, C_SREF = range(7)
+AGG_OPS = {"sum": 0, "min": 1, "max": 2}
+
+_ARITH = {"+": (OP_ADDF, OP_ADDI), "-": (OP_SUBF, OP_SUBI), "*": (OP_MULF, OP_MULI), "/": (OP_DIVF, None)}
+_CMP = {"<": (OP_LTF, OP_LTI), "<=": (OP_LEF, OP_LEI), ">": (OP_GTF, OP_GTI), ">=": (OP_GEF, OP_GEI),
+        "==": (OP_EQF, OP_EQI), "!=": (OP_NEF, OP_NEI)}
+
+# test hook: run the compiled program with the torch interpreter on CPU batches too (validates the compiler where
+# there is no GPU); the engine never takes the fused path on CPU otherwise
+CPU_INTERPRETER = False
+# the torch interpreter's model of the kernel's per-workgroup table: more distinct kept keys than this -> overflow
+INTERP_CAP = 1 << 30
+
+
+class Unfusable(Exception):
+    pass
+
+
+# ---------------------------------------------------------------------------------------------- expression IR
+class E:
+    """Symbolic column expression of a stage (built from the TCAP atoms' lambda nodes)."""
+
+    __slots__ = ("kind", "args", "val")
+
+    def __init__(self, kind: str, args=(), val=None):
+        self.kind, self.args, self.val = kind, tuple(args), val
+
+    def __repr__(self):
+        return f"{self.kind}{self.args if self.args else ''}{'' if self.val is None else '=' + repr(self.val)}"
+
+
+def _node_expr(node, argx: List[E]) -> E:
+    if isinstance(node, Literal):
+        v = node.value
+        if not isinstance(v, (bool, int, float, str)):
+            raise Unfusable(f"literal {type(v).__name__}")
+        return E("const", (), v)
+    if isinstance(node, AttAccess):
+        return E("field", argx, node.field)
+    if isinstance(node, Values):
+        return E("vals", argx)
+    if isinstance(node, KeyTuple):
+        return E("keys", argx)
+    if isinstance(node, Like):
+        return E("like", argx, (node.pattern, node.negate))
+    if isinstance(node, IsIn):
+        return E("isin", argx, tuple(node.values))
+    if isinstance(node, Select):
+        return E("sel", argx)
+    if isinstance(node, Unary):
+        return E("not", argx)
+    if isinstance(node, Binary):
+        return E("bin", argx, node.op)
+    raise Unfusable(type(node).__name__)
+
+
+class StagePlan:
+    """The fusable suffix of a stage: ``prefix`` atoms run eagerly, the rest is one fused launch per batch."""
+
+    def __init__(self, prefix, suffix, conj: List[E], key: Optional[E], val: E, op: str, kcol: str, vcol: str):
+        self.prefix, self.suffix = prefix, suffix
+        self.conj, self.key, self.val, self.op = conj, key, val, op
+        self.kcol, self.vcol = kcol, vcol
+        self.disabled = False
+        self.reason = None
+        self.stats = {"fused_batches": 0, "fallback_batches": 0}
+
+
+def plan_stage(ops: List[dict], comps: dict, sink_atom: dict) -> Optional[StagePlan]:
+    """The fusable suffix of ``ops`` feeding the aggregation ``sink_atom``, or None."""
+    from ..computations import AggregateComp, TopKComp
+
+    comp = comps.get(sink_atom["comp"])
+    if not isinstance(comp, AggregateComp) or isinstance(comp, TopKComp) or getattr(comp, "group_values", None):
+        return None
+    op = getattr(comp, "reduce_op", "sum")
+    if op not in AGG_OPS:
+        return None
+    # the suffix: the longest run of trailing atoms that are all lambda-tree APPLYs / FILTERs (a join's projection is
+    # an opaque native lambda: the suffix starts after it and reads its output columns)
+    def fusable(o) -> bool:
+        if o["type"] == "FILTER":
+            return True
+        if o["type"] != "APPLY":
+            return False
+        if o["lambda"].startswith("self_"):
+            return True
+        node = comps[o["comp"]].extract_lambdas().get(o["lambda"])
+        try:
+            _node_expr(node, [E("src", (), a) for a in o["input"]["atts"]])
+        except Unfusable:
+            return False
+        return node is not None
+
+    start = len(ops)
+    while start > 0 and fusable(ops[start - 1]):
+        start -= 1
+    suffix = ops[start:]
+    env: Dict[str, E] = {}
+
+    def col(name: str) -> E:
+        return env[name] if name in env else E("src", (), name)
+
+    conj: List[E] = []
+    try:
+        for o in suffix:
+            if o["type"] == "FILTER":
+                conj.append(col(o["input"]["atts"][0]))
+                continue
+            args = o["input"]["atts"]
+            out = o["output"]["atts"][-1]
+            lname = o["lambda"]
+            if lname.startswith("self_"):
+                env[out] = col(args[0])
+                continue
+            node = comps[o["comp"]].extract_lambdas().get(lname)
+            if node is None:
+                raise Unfusable(lname)
+            env[out] = _node_expr(node, [col(a) for a in args])
+        kcol, vcol = sink_atom["input"]["atts"]
+        key, val = col(kcol), col(vcol)
+    except Unfusable:
+        return None
+    if key.kind == "src" or val.kind == "src":
+        return None                                  # computed before the suffix: nothing to fuse
+    if not suffix:
+        return None
+    return StagePlan(ops[:start], suffix, conj, key, val, op, kcol, vcol)
+
+
+# ---------------------------------------------------------------------------------------------- binding + codegen
+def _resolve(e: E, batch: RecordBatch):
+    """The runtime column of a 'field' / 'src' expression."""
+    if e.kind == "src":
+        c = batch.columns.get(e.val)
+        if c is None:
+            raise Unfusable(f"column {e.val}")
+        return c
+    if e.kind == "field":
+        base = _resolve(e.args[0], batch)
+        if isinstance(base, RecordBatch) and e.val in base.columns:
+            return base.columns[e.val]
+        raise Unfusable(f"field {e.val}")
+    raise Unfusable(e.kind)
+
+
+def _num_kind(t: torch.Tensor) -> Tuple[int, str]:
+    if t.dim() != 1:
+        raise Unfusable("non-scalar column")
+    return {torch.float64: (C_F64, "f"), torch.int64: (C_I64, "i"), torch.int32: (C_I32, "i"),
+            torch.float32: (C_F32, "f"), torch.uint8: (C_U8, "i"), torch.bool: (C_U8, "i")}.get(t.dtype) or \
+        (_ for _ in ()).throw(Unfusable(str(t.dtype)))
+
+
+class Program:
+    """A compiled program + the column table it reads."""
+
+    def __init__(self):
+        self.ins: List[Tuple[int, int, int, int, int]] = []
+        self.cols: List[dict] = []            # {"key": (path, usage), "kind", "late", "L", "obj": column}
+        self.col_index: Dict[tuple, int] = {}
+        self.lit = bytearray()
+        self.lit_index: Dict[bytes, int] = {}
+        self.free: List[int] = []
+        self.pinned = set()                   # common subexpressions kept for their later uses
+        self.nins_a = 0
+        self.keep_reg = -1
+        self.key_reg = -1
+        self.val_regs: List[int] = []
+        self.key_layout = None                # how to turn the packed key back into columns
+        self.nval = 0
+        self.val_shape = None
+
+    # registers
+    def temp(self) -> int:
+        if not self.free:
+            raise Unfusable("registers")
+        return self.free.pop()
+
+    def release(self, r: int):
+        if r >= len(self.cols) and r not in self.free and r not in self.pinned:
+            self.free.append(r)
+
+    def emit(self, op, dst, a=-1, b=-1, imm=0):
+        """a / b == IMM: that operand is the 64-bit immediate."""
+        if len(self.ins) >= MAXINS:
+            raise Unfusable("program too long")
+        self.ins.append((op, dst, a, b, int(imm)))
+
+    def literal(self, s: str) -> int:
+        b = s.encode()
+        if len(b) > 0xFFFF:
+            raise Unfusable("literal")
+        if b not in self.lit_index:
+            self.lit_index[b] = len(self.lit)
+            self.lit += b
+        return (self.lit_index[b] << 16) | len(b)
+
+
+def _fbits(v: float) -> int:
+    return struct.unpack("<q", struct.pack("<d", v))[0]
+
+
+def _path(e: E) -> tuple:
+    return (e.kind, e.val) + tuple(_path(a) for a in e.args)
+
+
+class _Compiler:
+    def __init__(self, plan: StagePlan, batch: RecordBatch):
+        self.plan, self.batch = plan, batch
+        self.p = Program()
+        self.cse: Dict[tuple, tuple] = {}
+        self.counts: Dict[tuple, int] = {}
+
+    def _count(self, e: E):
+        if e.kind in ("bin", "sel", "not", "like", "isin"):
+            k = _path(e)
+            self.counts[k] = self.counts.get(k, 0) + 1
+            if self.counts[k] > 1:
+                return
+        for a in e.args:
+            self._count(a)
+
+    # -- column slots (registers [0, ncol)) are assigned before any temporary
+    def _collect(self, e: E, usage: str, seg: str, out: list):
+        if e.kind in ("src", "field"):
+            out.append((e, usage, seg))
+            return
+        if e.kind == "bin" and e.val in ("==", "!=") and any(a.kind == "const" and isinstance(a.val, str) for a in e.args):
+            for a in e.args:
+                if a.kind != "const":
+                    self._collect(a, "sref", seg, out)
+            return
+        if e.kind in ("like", "isin"):
+            self._collect(e.args[0], "sref" if e.kind == "like" else "isin", seg, out)
+            return
+        for a in e.args:
+            self._collect(a, usage, seg, out)
+
+    def _slot(self, e: E, usage: str, late: bool) -> int:
+        obj = _resolve(e, self.batch)
+        if isinstance(obj, StringColumn):
+            if usage == "isin":
+                usage = "sref"
+            if usage == "key":
+                L = obj.max_len()
+                if L > 7:
+                    raise Unfusable("long string key")
+                kind, u = C_SCODE, ("scode", L)
+            elif usage == "sref":
+                kind, u, L = C_SREF, ("sref",), 0
+            else:
+                raise Unfusable("string in arithmetic")
+        elif isinstance(obj, torch.Tensor):
+            kind, _ = _num_kind(obj)
+            u, L = ("num",), 0
+        else:
+            raise Unfusable(type(obj).__name__)
+        key = (_path(e), u)
+        if key in self.p.col_index:
+            i = self.p.col_index[key]
+            if not late:
+                self.p.cols[i]["late"] = 0
+            return i
+        if len(self.p.cols) >= MAXCOL:
+            raise Unfusable("columns")
+        self.p.col_index[key] = len(self.p.cols)
+        self.p.cols.append({"kind": kind, "late": int(late), "L": L, "obj": obj})
+        return len(self.p.cols) - 1
+
+    def compile(self) -> Program:
+        plan, p = self.plan, self.p
+        uses = []
+        for c in plan.conj:
+            self._collect(c, "num", "A", uses)
+        keys = self._key_fields()
+        for k in keys:
+            uses.append((k, "key", "B"))
+        vals = plan.val.args if plan.val.kind == "vals" else (plan.val,)
+        for v in vals:
+            self._collect(v, "num", "B", uses)
+        for e, usage, seg in [u for u in uses if u[2] == "A"] + [u for u in uses if u[2] == "B"]:
+            self._slot(e, usage, late=seg == "B")
+        ncol = len(p.cols)
+        if ncol > NREG:
+            raise Unfusable("registers")
+        p.free = list(range(NREG - 1, ncol - 1, -1))
+        # segment A: the predicate
+        if plan.conj:
+            r = None
+            for c in plan.conj:
+                rc, t = self.gen(c)
+                if t not in ("i", "b"):
+                    rc = self._truthy(rc, t)
+                if r is None:
+                    r = rc
+                else:
+                    d = p.temp()
+                    p.emit(OP_AND, d, r, rc)
+                    p.release(r)
+                    p.release(rc)
+                    r = d
+            p.keep_reg = r
+        p.nins_a = len(p.ins)
+        self.cse, self.counts = {}, {}
+        for v in vals:
+            self._count(v)
+        # segment B: key, then the value row
+        p.key_reg = self._gen_key(keys)
+        if len(vals) > FMAX:
+            raise Unfusable("values")
+        for v in vals:
+            r, t = self.gen(v)
+            if t == "s":
+                raise Unfusable("string value")
+            if t != "f":
+                d = p.temp()
+                p.emit(OP_I2F, d, r)
+                p.release(r)
+                r = d
+            p.val_regs.append(r)
+        p.nval = len(vals)
+        p.val_shape = "row" if plan.val.kind == "vals" else "scalar"
+        if p.val_shape == "scalar" and self._static_type(plan.val) != "f":
+            raise Unfusable("integer value (the eager path sums it exactly as int64)")
+        return p
+
+    def _truthy(self, r, t):
+        p = self.p
+        z = p.temp()
+        p.emit(OP_CONST, z, imm=0)
+        d = p.temp()
+        p.emit(OP_NEF if t == "f" else OP_NEI, d, r, z)
+        p.release(z)
+        p.release(r)
+        return d
+
+    # -- keys
+    def _key_fields(self) -> List[E]:
+        k = self.plan.key
+        if k.kind == "const":
+            return []
+        items = list(k.args) if k.kind == "keys" else [k]
+        for it in items:
+            if it.kind not in ("src", "field"):
+                raise Unfusable("computed key")
+        return items
+
+    def _gen_key(self, items: List[E]) -> int:
+        p = self.p
+        k = self.plan.key
+        if not items:
+            p.key_layout = ("const", k.val)
+            return -1
+        slots = [p.col_index[(_path(e), self._key_usage(e))] for e in items]
+        objs = [p.cols[s]["obj"] for s in slots]
+        if len(items) == 1 and isinstance(objs[0], torch.Tensor):
+            if objs[0].is_floating_point():
+                raise Unfusable("float key")
+            p.key_layout = ("int", objs[0].dtype, k.kind == "keys")
+            return slots[0]
+        if not all(isinstance(o, StringColumn) for o in objs):
+            raise Unfusable("mixed key")
+        bits = [8 * p.cols[s]["L"] + 3 for s in slots]
+        if sum(bits) > 63:
+            raise Unfusable("key too wide")
+        p.key_layout = ("strings", [p.cols[s]["L"] for s in slots], k.kind == "keys")
+        r = slots[0]
+        for s, b in zip(slots[1:], bits[1:]):
+            d = p.temp()
+            p.emit(OP_PACK, d, r, s, b)
+            p.release(r)
+            r = d
+        return r
+
+    def _key_usage(self, e: E):
+        obj = _resolve(e, self.batch)
+        return ("scode", obj.max_len()) if isinstance(obj, StringColumn) else ("num",)
+
+    # -- expressions: (register, type) with type f / i / b / s
+    def gen(self, e: E):
+        key = _path(e) if e.kind in ("bin", "sel", "not", "like", "isin") else None
+        if key is not None and key in self.cse:
+            return self.cse[key]
+        r = self._gen(e)
+        if key is not None and self.counts.get(key, 0) > 1:
+            self.cse[key] = r
+            self.p.pinned.add(r[0])
+        return r
+
+    def _gen(self, e: E):
+        p = self.p
+        if e.kind in ("src", "field"):
+            obj = _resolve(e, self.batch)
+            if isinstance(obj, StringColumn):
+                return p.col_index[(_path(e), ("sref",))], "s"
+            i = p.col_index[(_path(e), ("num",))]
+            return i, _num_kind(obj)[1]
+        if e.kind == "const":
+            v = e.val
+            if isinstance(v, str):
+                raise Unfusable("bare string literal")
+            d = p.temp()
+            if isinstance(v, float):
+                p.emit(OP_CONST, d, imm=_fbits(v))
+                return d, "f"
+            p.emit(OP_CONST, d, imm=int(v))
+            return d, "i"
+        if e.kind == "not":
+            r, t = self.gen(e.args[0])
+            d = p.temp()
+            p.emit(OP_NOT, d, r)
+            p.release(r)
+            return d, "b"
+        if e.kind == "bin":
+            return self._bin(e)
+        if e.kind == "like":
+            pat, neg = e.val
+            r, t = self.gen(e.args[0])
+            if t != "s":
+                raise Unfusable("LIKE on a non-string")
+            body = pat.strip("%")
+            if "%" in body or "_" in pat:
+                raise Unfusable("LIKE pattern")
+            if pat.endswith("%") and not pat.startswith("%"):
+                opc = OP_SPRE
+            elif pat.startswith("%") and not pat.endswith("%"):
+                opc = OP_SSUF
+            elif "%" not in pat:
+                opc = OP_SEQ
+            else:
+                raise Unfusable("LIKE %x%")
+            d = p.temp()
+            p.emit(opc, d, r, r, p.literal(body))
+            if neg:
+                p.emit(OP_NOT, d, d)
+            return d, "b"
+        if e.kind == "isin":
+            r, t = self.gen(e.args[0])
+            acc = None
+            for v in e.val:
+                d = p.temp()
+                if t == "s":
+                    if not isinstance(v, str):
+                        raise Unfusable("IN types")
+                    p.emit(OP_SEQ, d, r, r, p.literal(v))
+                else:
+                    z = p.temp()
+                    if t == "f":
+                        p.emit(OP_CONST, z, imm=_fbits(float(v)))
+                        p.emit(OP_EQF, d, r, z)
+                    else:
+                        if isinstance(v, float):
+                            raise Unfusable("IN types")
+                        p.emit(OP_CONST, z, imm=int(v))
+                        p.emit(OP_EQI, d, r, z)
+                    p.release(z)
+                if acc is None:
+                    acc = d
+                else:
+                    p.emit(OP_OR, acc, acc, d)
+                    p.release(d)
+            p.release(r)
+            if acc is None:
+                acc = p.temp()
+                p.emit(OP_CONST, acc, imm=0)
+            return acc, "b"
+        if e.kind == "sel":
+            rc, tc = self.gen(e.args[0])
+            ra, ta = self.gen(e.args[1])
+            rb, tb = self.gen(e.args[2])
+            if "s" in (ta, tb):
+                raise Unfusable("string CASE")
+            if ta != tb:
+                ra, rb = self._promote(ra, ta), self._promote(rb, tb)
+                ta = "f"
+            d = p.temp()
+            p.emit(OP_SEL, d, rc, ra, rb)
+            for r in (rc, ra, rb):
+                p.release(r)
+            return d, ta
+        raise Unfusable(e.kind)
+
+    def _promote(self, r, t):
+        if t == "f":
+            return r
+        p = self.p
+        d = p.temp()
+        p.emit(OP_I2F, d, r)
+        p.release(r)
+        return d
+
+    def _bin(self, e: E):
+        p = self.p
+        op = e.val
+        a, b = e.args
+        if op in ("==", "!=") and (a.kind == "const" and isinstance(a.val, str) or b.kind == "const" and isinstance(b.val, str)):
+            s, lit = (b, a.val) if a.kind == "const" else (a, b.val)
+            r, t = self.gen(s)
+            if t != "s":
+                raise Unfusable("string compare")
+            d = p.temp()
+            p.emit(OP_SEQ, d, r, r, p.literal(lit))
+            if op == "!=":
+                p.emit(OP_NOT, d, d)
+            p.release(r)
+            return d, "b"
+        if op in ("&&", "||"):
+            ra, _ = self.gen(a)
+            rb, _ = self.gen(b)
+            d = p.temp()
+            p.emit(OP_AND if op == "&&" else OP_OR, d, ra, rb)
+            p.release(ra)
+            p.release(rb)
+            return d, "b"
+        # numeric: a literal operand rides in the instruction's immediate and takes the other side's type (an int
+        # literal against a float column compares as a float)
+        ra, ta, ia = self._operand(a, b, allow_imm=True)
+        rb, tb, ib = self._operand(b, a, allow_imm=ra != IMM)
+        imm = ia if ra == IMM else ib
+        if "s" in (ta, tb):
+            raise Unfusable("string arithmetic")
+        fl = "f" in (ta, tb) or op == "/"
+        if fl:
+            if ra == IMM and ta == "i":
+                imm = _fbits(float(imm))
+            if rb == IMM and tb == "i":
+                imm = _fbits(float(imm))
+            ra = ra if ra == IMM else self._promote(ra, ta)
+            rb = rb if rb == IMM else self._promote(rb, tb)
+        d = p.temp()
+        if op in _ARITH:
+            opc = _ARITH[op][0 if fl else 1]
+            if opc is None:
+                raise Unfusable(op)
+            p.emit(opc, d, ra, rb, imm)
+            res = "f" if fl else "i"
+        elif op in _CMP:
+            p.emit(_CMP[op][0 if fl else 1], d, ra, rb, imm)
+            res = "b"
+        else:
+            raise Unfusable(op)
+        p.release(ra)
+        p.release(rb)
+        return d, res
+
+    def _operand(self, e: E, other: E, allow_imm: bool):
+        """(register, type, immediate): a numeric literal becomes the immediate (register IMM) when allowed."""
+        if allow_imm and e.kind == "const" and isinstance(e.val, (int, float)) and not isinstance(e.val, bool):
+            ot = self._static_type(other)
+            if ot == "f" or isinstance(e.val, float):
+                return IMM, "f", _fbits(float(e.val))
+            return IMM, "i", int(e.val)
+        r, t = self._gen_as(e, other)
+        return r, t, 0
+
+    def _gen_as(self, e: E, other: E):
+        if e.kind == "const" and isinstance(e.val, (int, float)) and not isinstance(e.val, bool):
+            ot = self._static_type(other)
+            if ot == "f" or isinstance(e.val, float):
+                d = self.p.temp()
+                self.p.emit(OP_CONST, d, imm=_fbits(float(e.val)))
+                return d, "f"
+        return self.gen(e)
+
+    def _static_type(self, e: E) -> str:
+        if e.kind in ("src", "field"):
+            obj = _resolve(e, self.batch)
+            return "s" if isinstance(obj, StringColumn) else _num_kind(obj)[1]
+        if e.kind == "const":
+            return "f" if isinstance(e.val, float) else "i"
+        if e.kind == "bin" and e.val in _ARITH:
+            ts = [self._static_type(a) for a in e.args]
+            return "f" if "f" in ts or e.val == "/" else "i"
+        if e.kind == "sel":
+            ts = [self._static_type(a) for a in e.args[1:]]
+            return "f" if "f" in ts else "i"
+        return "b"
+
+
+# ---------------------------------------------------------------------------------------------- execution
+def run_batch(plan: StagePlan, batch: RecordBatch) -> Optional[RecordBatch]:
+    """One fused launch over ``batch``: the pre-aggregated {kcol: keys, vcol: values} batch, or None when this batch
+    must take the eager atoms (columns the kernel cannot read, more groups than its tables)."""
+    if plan.disabled or batch.n == 0:
+        return None
+    dev = batch.device
+    on_gpu = dev.type == "cuda" and _ext.hip() is not None and hasattr(_ext.hip(), "pipe_agg")
+    if not on_gpu and not (CPU_INTERPRETER and dev.type == "cpu"):
+        return None
+    try:
+        prog = _Compiler(plan, batch).compile()
+    except Unfusable as e:
+        plan.disabled = True
+        plan.reason = str(e)
+        return None
+    if on_gpu:
+        parts = _launch(prog, batch.n, dev, plan.op)
+    else:
+        parts = interpret(prog, batch.n, plan.op)
+    if parts is None:
+        plan.disabled = True            # more groups than the per-workgroup tables hold: this stage runs eagerly
+        return None
+    keys, vals = parts
+    plan.stats["fused_batches"] += 1
+    return RecordBatch({plan.kcol: _key_columns(prog, keys), plan.vcol: _value_column(prog, vals)}, int(keys.numel()))
+
+
+def _col_args(prog: Program, dev):
+    out = []
+    for c in prog.cols:
+        o = c["obj"]
+        if isinstance(o, StringColumn):
+            out.append((c["kind"], c["late"], c["L"], None, o.starts.contiguous(), o.ends.contiguous(), o.data))
+        else:
+            t = o.contiguous()
+            out.append((c["kind"], c["late"], c["L"], t, None, None, None))
+    return out
+
+
+def _launch(prog: Program, n: int, dev, op: str):
+    h = _ext.hip()
+    ins = torch.tensor(prog.ins if prog.ins else [[0, 0, -1, -1, 0]], dtype=torch.int64).reshape(-1, 5)
+    nins = len(prog.ins)
+    if not prog.ins:
+        ins = ins[:0]
+    lit = torch.frombuffer(bytearray(prog.lit or b"\0"), dtype=torch.uint8).to(dev, non_blocking=True)
+    key, cnt, val, occ, status = h.pipe_agg(ins[:nins], prog.nins_a, _col_args(prog, dev), lit, n, prog.keep_reg,
+                                            prog.key_reg, prog.val_regs, AGG_OPS[op])
+    cap = key.numel() // occ.numel()
+    mask = (torch.arange(cap, device=dev).unsqueeze(0) < occ.unsqueeze(1)).flatten()
+    k = key[mask]
+    v = val[mask][:, : prog.nval]
+    if int(status[0]) != 0:                      # the one host read of the launch
+        return None
+    return _merge(k, v, op)
+
+
+def _merge(k: torch.Tensor, v: torch.Tensor, op: str):
+    uniq, inv = torch.unique(k, return_inverse=True)
+    g = int(uniq.numel())
+    if op == "sum":
+        out = torch.zeros(g, v.shape[1], dtype=torch.float64, device=v.device).index_add_(0, inv, v)
+    else:
+        out = torch.zeros(g, v.shape[1], dtype=torch.float64, device=v.device).scatter_reduce_(
+            0, inv.unsqueeze(1).expand_as(v), v, "amin" if op == "min" else "amax", include_self=False)
+    return uniq, out
+
+
+def _key_columns(prog: Program, keys: torch.Tensor):
+    lay = prog.key_layout
+    if lay[0] == "const":
+        v = lay[1]
+        dt = torch.float64 if isinstance(v, float) else torch.int64
+        return torch.full((keys.numel(),), v, dtype=dt, device=keys.device)
+    if lay[0] == "int":
+        col = keys.to(lay[1])
+        return (col,) if lay[2] else col
+    Ls = lay[1]
+    bits = [8 * L + 3 for L in Ls]
+    cols, shift = [], sum(bits)
+    for L, b in zip(Ls, bits):
+        shift -= b
+        code = (keys >> shift) & ((1 << b) - 1)
+        cols.append(StringColumn.from_short_codes(code, L))
+    return tuple(cols) if lay[2] else cols[0]
+
+
+def _value_column(prog: Program, vals: torch.Tensor):
+    return vals.contiguous() if prog.val_shape == "row" else vals[:, 0].contiguous()
+
+
+# ---------------------------------------------------------------------------------------------- torch interpreter
+def _col_values(c: dict) -> torch.Tensor:
+    o, kind = c["obj"], c["kind"]
+    if kind == C_SCODE:
+        return o.short_codes(c["L"])
+    if kind == C_SREF:
+        return torch.stack([o.starts, o.ends], 1)                 # kept as (start, end); string ops read bytes
+    if kind in (C_F64, C_F32):
+        return o.double().view(torch.int64) if kind == C_F64 else o.double().view(torch.int64)
+    return o.long()
+
+
+def interpret(prog: Program, n: int, op: str):
+    """The program evaluated with whole-column torch ops (same semantics as pipeline.hip; the CPU check of the
+    compiler). Returns the merged (keys, values)."""
+    regs: List[Optional[torch.Tensor]] = [None] * NREG
+    for i, c in enumerate(prog.cols):
+        regs[i] = _col_values(c)
+    f = lambda t: t.view(torch.float64)  # noqa: E731
+    u = lambda t: t.view(torch.int64)    # noqa: E731
+
+    def strmatch(ref, col, imm, mode):
+        o = prog.cols[col]["obj"]
+        off, ll = imm >> 16, imm & 0xFFFF
+        lit = bytes(prog.lit[off: off + ll])
+        s = o.tolist()
+        if mode == 0:
+            m = [x.encode() == lit for x in s]
+        elif mode == 1:
+            m = [x.encode().startswith(lit) for x in s]
+        else:
+            m = [x.encode().endswith(lit) for x in s]
+        return torch.tensor(m, dtype=torch.int64)
+
+    def run(lo, hi):
+        for opc, d, a, b, imm in prog.ins[lo:hi]:
+            x = regs[a] if a >= 0 else (torch.full((n,), imm, dtype=torch.int64) if a == IMM else None)
+            y = regs[b] if b >= 0 else (torch.full((n,), imm, dtype=torch.int64) if b == IMM else None)
+            if opc == OP_CONST:
+                z = torch.full((n,), imm, dtype=torch.int64)
+            elif opc in (OP_ADDF, OP_SUBF, OP_MULF, OP_DIVF):
+                fx, fy = f(x), f(y)
+                z = u({OP_ADDF: fx + fy, OP_SUBF: fx - fy, OP_MULF: fx * fy, OP_DIVF: fx / fy}[opc].contiguous())
+            elif opc == OP_NEGF:
+                z = u((-f(x)).contiguous())
+            elif opc in (OP_ADDI, OP_SUBI, OP_MULI):
+                z = {OP_ADDI: x + y, OP_SUBI: x - y, OP_MULI: x * y}[opc]
+            elif opc == OP_I2F:
+                z = u(x.double())
+            elif OP_LTF <= opc <= OP_NEF:
+                fx, fy = f(x), f(y)
+                z = [fx < fy, fx <= fy, fx > fy, fx >= fy, fx == fy, fx != fy][opc - OP_LTF].long()
+            elif OP_LTI <= opc <= OP_NEI:
+                z = [x < y, x <= y, x > y, x >= y, x == y, x != y][opc - OP_LTI].long()
+            elif opc == OP_AND:
+                z = ((x != 0) & (y != 0)).long()
+            elif opc == OP_OR:
+                z = ((x != 0) | (y != 0)).long()
+            elif opc == OP_NOT:
+                z = (x == 0).long()
+            elif opc == OP_PACK:
+                z = (x << (imm & 63)) | y
+            elif opc in (OP_SEQ, OP_SPRE, OP_SSUF):
+                z = strmatch(x, b, imm, {OP_SEQ: 0, OP_SPRE: 1, OP_SSUF: 2}[opc])
+            elif opc == OP_SEL:
+                z = torch.where(x != 0, y, regs[imm])
+            else:
+                z = torch.zeros(n, dtype=torch.int64)
+            regs[d] = z
+
+    run(0, prog.nins_a)
+    keep = torch.ones(n, dtype=torch.bool) if prog.keep_reg < 0 else regs[prog.keep_reg] != 0
+    run(prog.nins_a, len(prog.ins))
+    key = torch.zeros(n, dtype=torch.int64) if prog.key_reg < 0 else regs[prog.key_reg]
+    vals = torch.stack([f(regs[r]) for r in prog.val_regs], 1) if prog.val_regs else torch.zeros(n, 0, dtype=torch.float64)
+    idx = keep.nonzero().flatten()
+    if torch.unique(key[idx]).numel() > INTERP_CAP:
+        return None
+    return _merge(key[idx], vals[idx], op)
+
+
+__all__ = ["plan_stage", "run_batch", "StagePlan", "Unfusable", "interpret"]

@@ -116,6 +116,22 @@ class Lambda:
     def __truediv__(self, other):
         return Binary("/", self, _lift(other))
 
+    # literal on the left (``1 - in.l_discount``)
+    def __radd__(self, other):
+        return Binary("+", _lift(other), self)
+
+    def __rsub__(self, other):
+        return Binary("-", _lift(other), self)
+
+    def __rmul__(self, other):
+        return Binary("*", _lift(other), self)
+
+    def __rtruediv__(self, other):
+        return Binary("/", _lift(other), self)
+
+    def __neg__(self):
+        return Binary("-", Literal(0.0), self)
+
     __hash__ = object.__hash__
 
     def __repr__(self):
@@ -366,6 +382,97 @@ def _elementwise(f, a, b):
     return f(a, b)
 
 
+class Values(Lambda):
+    """The [n, F] float64 value row of an aggregation from F scalar lambdas (column-major: each column is
+    contiguous, as the device group-by reads it). Tree-built value rows compile into the fused pipeline kernel
+    (execution/pipeline.py); the eager path stacks the columns."""
+
+    kind = "values"
+
+    def __init__(self, *items):
+        super().__init__(children=[_lift(x) for x in items])
+
+    def eval_node(self, inputs, child_vals):
+        n, dev = _len_dev(child_vals)
+        cols = []
+        for v in child_vals:
+            t = v if isinstance(v, torch.Tensor) else torch.as_tensor(v)
+            t = t.to(dev, torch.float64)
+            cols.append(t.expand(n) if t.dim() == 0 else t)
+        return torch.stack(cols, 0).t()
+
+
+class KeyTuple(Lambda):
+    """A composite group / join key: a tuple of key columns (exact multi-column equality)."""
+
+    kind = "keys"
+
+    def __init__(self, *items):
+        super().__init__(children=[_lift(x) for x in items])
+
+    def eval_node(self, inputs, child_vals):
+        return tuple(child_vals)
+
+
+class Like(Lambda):
+    """SQL ``LIKE`` of a string lambda against a pattern ('%' = any run, '_' = any byte)."""
+
+    kind = "like"
+
+    def __init__(self, x, pattern: str, negate: bool = False):
+        super().__init__(children=[_lift(x)])
+        self.pattern, self.negate = pattern, negate
+
+    def eval_node(self, inputs, child_vals):
+        v = child_vals[0]
+        col = v if isinstance(v, StringColumn) else StringColumn.from_list(list(v))
+        return col.like(self.pattern, self.negate)
+
+
+class IsIn(Lambda):
+    """``x IN (v1, v2, ...)`` over a string or numeric lambda."""
+
+    kind = "isin"
+
+    def __init__(self, x, values):
+        super().__init__(children=[_lift(x)])
+        self.values = list(values)
+
+    def eval_node(self, inputs, child_vals):
+        v = child_vals[0]
+        if isinstance(v, StringColumn):
+            return v.isin(self.values)
+        if isinstance(v, torch.Tensor):
+            return torch.isin(v, torch.tensor(self.values, dtype=v.dtype, device=v.device))
+        s = set(self.values)
+        return torch.tensor([x in s for x in v], dtype=torch.bool)
+
+
+class Select(Lambda):
+    """``cond ? a : b`` (SQL CASE WHEN cond THEN a ELSE b END)."""
+
+    kind = "select"
+
+    def __init__(self, cond, a, b):
+        super().__init__(children=[_lift(cond), _lift(a), _lift(b)])
+
+    def eval_node(self, inputs, child_vals):
+        c, a, b = child_vals
+        c = c if isinstance(c, torch.Tensor) else torch.as_tensor(c)
+        a = a if isinstance(a, torch.Tensor) else torch.as_tensor(a, dtype=torch.float64)
+        b = b if isinstance(b, torch.Tensor) else torch.as_tensor(b, dtype=torch.float64)
+        return torch.where(c.bool(), a.to(c.device), b.to(c.device))
+
+
+def _len_dev(vals):
+    for v in vals:
+        if isinstance(v, torch.Tensor) and v.dim() >= 1:
+            return v.shape[0], v.device
+        if isinstance(v, (list, StringColumn)):
+            return len(v), getattr(v, "device", torch.device("cpu"))
+    return 1, torch.device("cpu")
+
+
 # --------------------------------------------------------------------- creation functions
 def make_lambda_from_member(arg: Arg, member: str) -> Lambda:
     return AttAccess(arg, member)
@@ -399,6 +506,6 @@ makeLambdaFromMethod = make_lambda_from_method
 makeLambdaFromSelf = make_lambda_from_self
 
 __all__ = ["Arg", "Lambda", "Literal", "SelfLambda", "SelfRef", "AttAccess", "MethodCall", "Native", "Binary",
-           "Unary", "make_lambda", "make_batch_lambda", "make_lambda_from_member", "make_lambda_from_method",
+           "Unary", "Values", "KeyTuple", "Like", "IsIn", "Select", "make_lambda", "make_batch_lambda", "make_lambda_from_member", "make_lambda_from_method",
            "make_lambda_from_self", "makeLambda", "makeLambdaFromMember", "makeLambdaFromMethod",
            "makeLambdaFromSelf"]

@@ -25,7 +25,7 @@ import numpy as np
 import torch
 
 from ..computations import AggregateComp, JoinComp, ScanSet, SelectionComp, TopKComp, WriteSet
-from ..lambdas import make_batch_lambda, make_lambda_from_member
+from ..lambdas import IsIn, KeyTuple, Like, Literal, Select, Values, make_batch_lambda, make_lambda_from_member
 from ..objects.record import PDBObject, RecordBatch
 from ..objects.strings import StringColumn, use_device_strings
 
@@ -330,6 +330,41 @@ class _Filter(SelectionComp):
         return make_lambda_from_self(x)
 
 
+class _TreeFilter(SelectionComp):
+    """SelectionComp whose predicate is a lambda TREE (members, literals, comparisons, &&): compiled into the fused
+    pipeline kernel when its stage ends in an aggregation (execution/pipeline.py), evaluated column-wise otherwise."""
+
+    def __init__(self, pred):
+        super().__init__()
+        self.pred = pred
+
+    def get_selection(self, x):
+        return self.pred(x)
+
+    def get_projection(self, x):
+        from ..lambdas import make_lambda_from_self
+
+        return make_lambda_from_self(x)
+
+
+class _TreeGroupBy(AggregateComp):
+    """Group-by whose key (``KeyTuple`` / member / literal) and value row (``Values``) are lambda trees."""
+
+    def __init__(self, key_fn, val_fn, out_fn, reduce_op: str = "sum"):
+        super().__init__()
+        self.key_fn, self.val_fn, self.out_fn = key_fn, val_fn, out_fn
+        self.reduce_op = reduce_op
+
+    def get_key_projection(self, x):
+        return self.key_fn(x)
+
+    def get_value_projection(self, x):
+        return self.val_fn(x)
+
+    def make_output(self, keys, values):
+        return self.out_fn(keys, values)
+
+
 class _GroupBy(AggregateComp):
     """Group-by with a vectorised key (column or tuple of columns) and an [n, F] fp64 value row."""
 
@@ -352,6 +387,8 @@ def _rows_out(names: List[str]):
     """make_output building a plain tuple-set batch {key columns..., value columns...}."""
 
     def out(keys, values):
+        if isinstance(keys, list) and keys and isinstance(keys[0], tuple):   # host-grouped composite keys
+            keys = tuple(list(c) for c in zip(*keys))
         ks = keys if isinstance(keys, tuple) else (keys,)
         ks = [list(k) if not isinstance(k, torch.Tensor) else k for k in ks]
         if isinstance(values, torch.Tensor):
@@ -416,21 +453,16 @@ def _as_list(c):
 def q01(client, db: str, delta_days: int = 90) -> List[dict]:
     """Pricing summary report (Query01.h: Q01Agg over LineItem keyed by returnflag|linestatus)."""
     cutoff = add_days(19981201, -delta_days)
-    sel = _Filter(lambda b: _col(b, "l_shipdate") <= cutoff).set_input(ScanSet(db, "lineitem", LineItem))
+    # lambda trees (Query01.h's makeLambdaFromMember + comparison + arithmetic): ONE fused scan-filter-aggregate
+    # launch on the GPU (execution/pipeline.py), column-wise tensor ops elsewhere
+    sel = _TreeFilter(lambda x: x.l_shipdate <= cutoff).set_input(ScanSet(db, "lineitem", LineItem))
 
-    def vals(b):
-        q, p, d, t = (_col(b, c).double() for c in ("l_quantity", "l_extendedprice", "l_discount", "l_tax"))
-        out = torch.empty(6, b.n, dtype=torch.float64, device=q.device)   # column-major value row, filled in place
-        out[0].copy_(q)
-        out[1].copy_(p)
-        torch.mul(p, 1 - d, out=out[2])                 # disc_price
-        torch.mul(out[2], 1 + t, out=out[3])            # charge
-        out[4].copy_(d)
-        out[5].fill_(1.0)                               # count
-        return out.t()
+    def vals(x):
+        disc_price = x.l_extendedprice * (1 - x.l_discount)
+        return Values(x.l_quantity, x.l_extendedprice, disc_price, disc_price * (1 + x.l_tax), x.l_discount, 1.0)
 
-    agg = _GroupBy(lambda b: _str_keys(_col(b, "l_returnflag"), _col(b, "l_linestatus")), vals,
-                   _rows_out(["sum_qty", "sum_base_price", "sum_disc_price", "sum_charge", "sum_disc", "count"]))
+    agg = _TreeGroupBy(lambda x: KeyTuple(x.l_returnflag, x.l_linestatus), vals,
+                       _rows_out(["sum_qty", "sum_base_price", "sum_disc_price", "sum_charge", "sum_disc", "count"]))
     r = _flat(_run(client, db, "q01_out", agg.set_input(sel), "tpch_q01"))
     out = []
     if r is None:
@@ -532,14 +564,12 @@ def q06(client, db: str, date: int = 19940101, discount: float = 0.06, quantity:
     """Forecasting revenue change (Query06.h): one global sum."""
     lo, hi = discount - 0.01 - 1e-9, discount + 0.01 + 1e-9
 
-    def pred(b):
-        d, s, q = _col(b, "l_discount"), _col(b, "l_shipdate"), _col(b, "l_quantity")
-        return (s >= date) & (s < date + 10000) & (d >= lo) & (d <= hi) & (q < quantity)
+    def pred(x):
+        return (x.l_shipdate >= date) & (x.l_shipdate < date + 10000) & (x.l_discount >= lo) & (x.l_discount <= hi) & \
+            (x.l_quantity < quantity)
 
-    sel = _Filter(pred).set_input(ScanSet(db, "lineitem", LineItem))
-    agg = _GroupBy(lambda b: torch.zeros(b.n, dtype=torch.int64, device=_dev(b)),
-                   lambda b: (_col(b, "l_extendedprice").double() * _col(b, "l_discount").double()).unsqueeze(1),
-                   _rows_out(["revenue"]))
+    sel = _TreeFilter(pred).set_input(ScanSet(db, "lineitem", LineItem))
+    agg = _TreeGroupBy(lambda x: Literal(0), lambda x: Values(x.l_extendedprice * x.l_discount), _rows_out(["revenue"]))
     r = _flat(_run(client, db, "q06_out", agg.set_input(sel), "tpch_q06"))
     return 0.0 if r is None else float(r.columns["revenue"].sum())
 
@@ -556,11 +586,11 @@ def q12(client, db: str, modes=("MAIL", "SHIP"), date: int = 19940101) -> List[d
     j.set_input(0, ScanSet(db, "orders", Order))
     j.set_input(1, ls)
 
-    def vals(b):
-        hi = _isin_str(_col(b, "o_orderpriority"), ["1-URGENT", "2-HIGH"], _dev(b)).double()
-        return _vcols(hi, 1 - hi)
+    def vals(x):
+        hi = IsIn(x.o_orderpriority, ["1-URGENT", "2-HIGH"])
+        return Values(Select(hi, 1.0, 0.0), Select(hi, 0.0, 1.0))
 
-    agg = _GroupBy(lambda b: _col(b, "l_shipmode"), vals, _rows_out(["high_line_count", "low_line_count"]))
+    agg = _TreeGroupBy(lambda x: x.l_shipmode, vals, _rows_out(["high_line_count", "low_line_count"]))
     r = _flat(_run(client, db, "q12_out", agg.set_input(j), "tpch_q12"))
     if r is None:
         return []
@@ -601,12 +631,11 @@ def q14(client, db: str, date: int = 19950901) -> float:
     j.set_input(0, ls)
     j.set_input(1, ScanSet(db, "part", Part))
 
-    def vals(b):
-        rev = _col(b, "l_extendedprice").double() * (1 - _col(b, "l_discount").double())
-        promo = _like(_col(b, "p_type"), "PROMO%", _dev(b)).double()
-        return _vcols(rev * promo, rev)
+    def vals(x):
+        rev = x.l_extendedprice * (1 - x.l_discount)
+        return Values(Select(Like(x.p_type, "PROMO%"), rev, 0.0), rev)
 
-    agg = _GroupBy(lambda b: torch.zeros(b.n, dtype=torch.int64, device=_dev(b)), vals, _rows_out(["promo", "total"]))
+    agg = _TreeGroupBy(lambda x: Literal(0), vals, _rows_out(["promo", "total"]))
     r = _flat(_run(client, db, "q14_out", agg.set_input(j), "tpch_q14"))
     if r is None:
         return 0.0

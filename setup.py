@@ -21,7 +21,8 @@ RDIR = os.path.join("netsdb_amd", "csrc", "runtime")
 
 
 HIP_SOURCES = ("gemm.hip", "gemm_f32.hip", "conv2d.hip", "rowops.hip", "strings.hip", "dedup.hip", "relops.hip",
-               "relops_bind.cpp")
+               "relops_bind.cpp", "pipeline.hip", "pipeline_bind.cpp")
+PER_FILE_FLAGS = {}          # per-source extra hipcc flags
 SDIR = os.path.join("netsdb_amd", "csrc", "study")
 STUDY_SOURCES = ("gemm_study.hip",)
 
@@ -81,7 +82,7 @@ def build_hip_extension(out_path: str, build_dir: str, jobs: int = 8, study: boo
             continue
         if f.endswith(".hip"):
             cmds.append([hipcc, "-x", "hip", f"--offload-arch={arch}", "-fno-gpu-rdc", "-munsafe-fp-atomics"]
-                        + common + ["-c", src, "-o", obj])
+                        + common + PER_FILE_FLAGS.get(f, []) + ["-c", src, "-o", obj])
         else:
             cmds.append([hipcc, "-x", "c++"] + common + [f"-I{rocm}/include", "-c", src, "-o", obj])
 

@@ -1,0 +1,187 @@
+"""Fused filter -> project -> aggregate stages (execution/pipeline.py + csrc/kernels/pipeline.hip): the TPC-H Q01 /
+Q06 / Q12 / Q14 lambda trees compiled into the device interpreter's register program. On CPU the compiled program
+runs on the torch interpreter of the same instruction set (the compiler's check); on the GPU the kernel runs and
+must match the eager per-atom path and the pandas oracle. Reference: src/lambdas/headers/Pipeline.h:57,194."""
+import math
+import tempfile
+
+import pytest
+import torch
+
+from netsdb_amd.client import PDBClient
+from netsdb_amd.computations import AggregateComp, ScanSet, SelectionComp, WriteSet
+from netsdb_amd.execution import pipeline as PL
+from netsdb_amd.lambdas import IsIn, KeyTuple, Like, Literal, Select, Values, make_lambda_from_self
+from netsdb_amd.models import tpch, tpch_gen
+
+QUERIES = ("q01", "q06", "q12", "q14")
+
+
+def _close(a, b):
+    if isinstance(a, float):
+        return math.isclose(a, b, rel_tol=1e-9, abs_tol=1e-6)
+    if isinstance(a, list):
+        return len(a) == len(b) and all(_close(x, y) for x, y in zip(a, b))
+    if isinstance(a, dict):
+        return all(_close(a[k], b[k]) for k in b)
+    return a == b
+
+
+def _ref(q, t, f):
+    ref = tpch.reference(q, t, f=f)
+    if q == "q01":
+        ref = sorted(ref, key=lambda x: (x["l_returnflag"], x["l_linestatus"]))
+    elif q == "q12":
+        ref = sorted(ref, key=lambda x: x["l_shipmode"])
+    return ref
+
+
+def _client(dev, t):
+    c = PDBClient(root=tempfile.mkdtemp(), device=dev)
+    tpch.load(c, "tpch", t, device=dev)
+    return c
+
+
+def test_fused_tpch_cpu_interpreter(monkeypatch):
+    monkeypatch.setenv("NSDB_DEVICE_STRINGS", "1")
+    monkeypatch.setattr(PL, "CPU_INTERPRETER", True)
+    t = tpch_gen.generate_fast(0.003, seed=4)
+    f = tpch.frames(t)
+    c = _client("cpu", t)
+    for q in QUERIES:
+        got = tpch.QUERIES[q](c, "tpch")
+        assert _close(got, _ref(q, t, f)), (q, got)
+    st = c.engine.pipeline_stats
+    assert st["fused_stages"] >= len(QUERIES) and st["fallback_batches"] == 0, st
+
+
+class _Sel(SelectionComp):
+    def __init__(self, pred):
+        super().__init__()
+        self.pred = pred
+
+    def get_selection(self, x):
+        return self.pred(x)
+
+    def get_projection(self, x):
+        return make_lambda_from_self(x)
+
+
+class _Agg(AggregateComp):
+    def __init__(self, key, val, op="sum"):
+        super().__init__()
+        self.key, self.val, self.reduce_op = key, val, op
+
+    def get_key_projection(self, x):
+        return self.key(x)
+
+    def get_value_projection(self, x):
+        return self.val(x)
+
+
+_JOBS = [0]
+
+
+def _agg_job(c, pred, key, val, op="sum"):
+    _JOBS[0] += 1
+    out = f"o{_JOBS[0]}"
+    c.create_set("tpch", out, None)
+    comp = _Agg(key, val, op).set_input(_Sel(pred).set_input(ScanSet("tpch", "lineitem", tpch.LineItem)))
+    c.execute_computations(WriteSet("tpch", out).set_input(comp))
+    b = [x for x in c.get_set_batches("tpch", out) if x.n]
+    assert len(b) == 1
+    b = b[0]
+    keys = [b.columns[k] for k in sorted(k for k in b.columns if k.startswith("key"))]
+    keys = [k.tolist() if hasattr(k, "tolist") else list(k) for k in keys]
+    vals = b.columns["value"]
+    order = sorted(range(b.n), key=lambda i: tuple(k[i] for k in keys))
+    return [tuple(k[i] for k in keys) for i in order], vals[torch.tensor(order)].double().cpu()
+
+
+CASES = {
+    "min_max_int_key": (lambda x: (x.l_quantity > 10) | (x.l_tax == 0.0), lambda x: x.l_linenumber,
+                        lambda x: Values(x.l_extendedprice, x.l_discount * 2.0 - x.l_tax), "max"),
+    "min": (lambda x: ~(x.l_shipmode == "AIR"), lambda x: KeyTuple(x.l_linestatus, x.l_returnflag),
+            lambda x: Values(x.l_quantity / 3, -x.l_tax), "min"),
+    "isin_like_select": (lambda x: IsIn(x.l_shipmode, ["MAIL", "TRUCK", "REG AIR"]) & Like(x.l_shipinstruct, "%PERSON"),
+                         lambda x: x.l_linestatus,
+                         lambda x: Values(Select(x.l_discount < 0.05, x.l_quantity, 0), 1.0),
+                         "sum"),
+}
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_fused_operators_cpu_interpreter(case, monkeypatch):
+    """Each operator class (or, not, string ==, IN, LIKE suffix, CASE, min / max, int keys, composite string keys)
+    through the compiler: fused (torch interpreter) == eager."""
+    monkeypatch.setenv("NSDB_DEVICE_STRINGS", "1")
+    pred, key, val, op = CASES[case]
+    t = tpch_gen.generate_fast(0.002, seed=9)
+    c = _client("cpu", t)
+    eager = _agg_job(c, pred, key, val, op)
+    monkeypatch.setattr(PL, "CPU_INTERPRETER", True)
+    n0 = c.engine.pipeline_stats["fused_batches"]
+    fused = _agg_job(c, pred, key, val, op)
+    assert c.engine.pipeline_stats["fused_batches"] > n0
+    assert eager[0] == fused[0]
+    assert torch.allclose(eager[1], fused[1], rtol=1e-12, atol=1e-9)
+
+
+def test_fused_overflow_falls_back(monkeypatch):
+    """More groups than the kernel's per-workgroup tables: the batch takes the eager atoms, same result."""
+    monkeypatch.setenv("NSDB_DEVICE_STRINGS", "1")
+    t = tpch_gen.generate_fast(0.002, seed=9)
+    c = _client("cpu", t)
+    args = (lambda x: x.l_quantity > 1, lambda x: x.l_orderkey, lambda x: Values(x.l_extendedprice), "sum")
+    eager = _agg_job(c, *args)
+    monkeypatch.setattr(PL, "CPU_INTERPRETER", True)
+    monkeypatch.setattr(PL, "INTERP_CAP", 64)      # the interpreter models the kernel's table capacity
+    fused = _agg_job(c, *args)
+    assert c.engine.pipeline_stats["fallback_batches"] >= 1
+    assert eager[0] == fused[0] and torch.allclose(eager[1], fused[1])
+
+
+@pytest.mark.gpu
+def test_fused_tpch_gpu_vs_eager_and_pandas():
+    t = tpch_gen.generate_fast(0.05, seed=4)
+    f = tpch.frames(t)
+    c = _client("cuda:0", t)
+    for q in QUERIES:
+        c.engine.fused_pipelines = True
+        got = tpch.QUERIES[q](c, "tpch")
+        c.engine.fused_pipelines = False
+        eager = tpch.QUERIES[q](c, "tpch")
+        ref = _ref(q, t, f)
+        assert _close(got, ref), (q, got, ref)
+        assert _close(eager, ref), q
+    st = c.engine.pipeline_stats
+    assert st["fused_stages"] >= len(QUERIES) and st["fallback_batches"] == 0, st
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_fused_operators_gpu(case):
+    pred, key, val, op = CASES[case]
+    t = tpch_gen.generate_fast(0.01, seed=9)
+    c = _client("cuda:0", t)
+    c.engine.fused_pipelines = False
+    eager = _agg_job(c, pred, key, val, op)
+    c.engine.fused_pipelines = True
+    n0 = c.engine.pipeline_stats["fused_batches"]
+    fused = _agg_job(c, pred, key, val, op)
+    assert c.engine.pipeline_stats["fused_batches"] > n0
+    assert eager[0] == fused[0]
+    assert torch.allclose(eager[1], fused[1], rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.gpu
+def test_fused_overflow_gpu():
+    t = tpch_gen.generate_fast(0.01, seed=9)
+    c = _client("cuda:0", t)
+    args = (lambda x: x.l_quantity > 1, lambda x: x.l_orderkey, lambda x: Values(x.l_extendedprice), "sum")
+    c.engine.fused_pipelines = False
+    eager = _agg_job(c, *args)
+    c.engine.fused_pipelines = True
+    fused = _agg_job(c, *args)
+    assert c.engine.pipeline_stats["fallback_batches"] >= 1
+    assert eager[0] == fused[0] and torch.allclose(eager[1], fused[1])
