@@ -364,13 +364,14 @@ __global__ __launch_bounds__(256) void agg_init_kernel(u64* glow, i64 cap_low, u
   const i64 t0 = (i64)blockIdx.x * blockDim.x + threadIdx.x;
   for (int which = 0; which < 2; ++which) {
     u64* base = which ? gpart : glow;
+    if (base == nullptr) continue;               // phased launch: the PART table is set up in phase 2
     const i64 c1 = (which ? cap_part : cap_low) + 1;
     for (i64 i = t0; i < c1 * (3 + F); i += stride) {
       // key: kEmpty; acc: the op identity; cnt: 0; rmin: ~0 (the gid region is written on claim)
       base[i] = i < c1 ? kEmpty : (i < c1 * (1 + F) ? ident : (i < c1 * (2 + F) ? 0ull : ~0ull));
     }
   }
-  if (t0 < (i64)(sizeof(AggMeta) / 8)) reinterpret_cast<i64*>(meta)[t0] = 0;
+  if (meta != nullptr && t0 < (i64)(sizeof(AggMeta) / 8)) reinterpret_cast<i64*>(meta)[t0] = 0;
 }
 
 // ---------------------------------------------------------------- LOW path
@@ -1028,10 +1029,10 @@ __global__ __launch_bounds__(256) void join_probe_kernel(const u64* __restrict__
                                                          const JSlot* __restrict__ tab, u64 mask,
                                                          unsigned* __restrict__ cnt, unsigned* __restrict__ pay,
                                                          i64* __restrict__ tile_sum) {
-  __shared__ unsigned ws[4];
+  __shared__ u64 ws[4];   // match totals in 64 bits: a skewed many-to-many tile can exceed 2^32 pairs
   constexpr int J = kJTile / 256;
   const i64 t0 = (i64)blockIdx.x * kJTile;
-  unsigned local = 0;
+  u64 local = 0;
   u64 k[J];
 #pragma unroll
   for (int j = 0; j < J; ++j) {
@@ -1074,7 +1075,7 @@ __global__ __launch_bounds__(256) void join_probe_kernel(const u64* __restrict__
   for (int d = 32; d > 0; d >>= 1) local += __shfl_down(local, d, 64);
   if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = local;
   __syncthreads();
-  if (threadIdx.x == 0) tile_sum[blockIdx.x] = (i64)ws[0] + ws[1] + ws[2] + ws[3];
+  if (threadIdx.x == 0) tile_sum[blockIdx.x] = (i64)(ws[0] + ws[1] + ws[2] + ws[3]);
 }
 
 // expand: tile bases = exclusive scan of tile_sum; inside a tile, a block scan per 256-row slab gives each probe
@@ -1084,41 +1085,41 @@ __global__ __launch_bounds__(256) void join_expand_kernel(const unsigned* __rest
                                                           const i64* __restrict__ tile_base,
                                                           const i64* __restrict__ perm, i64* __restrict__ bidx,
                                                           i64* __restrict__ pidx) {
-  __shared__ unsigned wsum[4];
+  __shared__ u64 wsum[4];           // 64-bit prefixes (see join_probe_kernel)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const i64 t0 = (i64)blockIdx.x * kJTile;
   i64 base = tile_base[blockIdx.x];
   for (int j = 0; j < kJTile / 256; ++j) {
     const i64 i = t0 + j * 256 + threadIdx.x;
-    const unsigned c = i < m ? cnt[i] : 0u;
-    unsigned x = c;
+    const u64 c = i < m ? (u64)cnt[i] : 0ull;
+    u64 x = c;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-      const unsigned y = __shfl_up(x, d, 64);
+      const u64 y = __shfl_up(x, d, 64);
       if (lane >= d) x += y;
     }
     if (lane == 63) wsum[wave] = x;
     __syncthreads();
-    unsigned before = 0, slab = 0;
+    u64 before = 0, slab = 0;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-      const unsigned t = wsum[w];
+      const u64 t = wsum[w];
       before += w < wave ? t : 0u;
       slab += t;
     }
-    const i64 o = base + before + x - c;
+    const i64 o = base + (i64)(before + x - c);
     if (c == 1) {
       const unsigned p = pay[i];
       bidx[o] = (i64)p;
       pidx[o] = i;
     } else if (c > 1) {
       const i64 b0 = (i64)pay[i];
-      for (unsigned q = 0; q < c; ++q) {
+      for (u64 q = 0; q < c; ++q) {
         bidx[o + q] = perm[b0 + q];
         pidx[o + q] = i;
       }
     }
-    base += slab;
+    base += (i64)slab;
     __syncthreads();
   }
 }
@@ -1192,10 +1193,14 @@ inline int stage_rows(int F, int budget = 48 * 1024, int nthr = 512) {
 // level-1 histogram / scatter workgroups (one per CU), >= 16 Ki rows each
 inline int agg_groups(long long n) { return (int)std::min<long long>(256, std::max<long long>(1, (n + 16383) / 16384)); }
 
+// phase 0: every kernel (the device decides LOW / PART); phased launches let the host size the PART scratch only when
+// the PART path runs: 1 = init + sample + LOW, 2 = PART (its table initialised first), 3 = emit + inverse fix-up.
+// out: [reps ocap | aggs ocap*F | cnt ocap | slot_of_gid ocap | first ocap] (ocap: the groups the run may create);
+// inv_v: [n] per-row group ids (want_inv), shared by every phase.
 template <typename VT, int OP>
 int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv, int want_first, void* meta_v, void* glow_v,
-                 i64 gcap_low, void* gpart_v, i64 gcap_part, void* out_v, void* work_v, int pbits, int lcap_low,
-                 int lcap_part, int low_thr, i64 rs, i64 cs, hipStream_t st) {
+                 i64 gcap_low, void* gpart_v, i64 gcap_part, void* out_v, void* inv_v, i64 ocap, int phase, void* work_v,
+                 int pbits, int lcap_low, int lcap_part, int low_thr, i64 rs, i64 cs, hipStream_t st) {
   AggMeta* meta = reinterpret_cast<AggMeta*>(meta_v);
   // glow / gpart: [key (cap+1) | acc (cap+1)*F | cnt (cap+1) | gid (cap+1)] u64 words, preset by the caller
   auto mk = [&](void* base, i64 cap) {
@@ -1212,27 +1217,32 @@ int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv,
   GTable glow = mk(glow_v, gcap_low), gpart = mk(gpart_v, gcap_part);
   glow.occ = &meta->occ_low;
   gpart.occ = &meta->occ_part;
-  i64* ob = reinterpret_cast<i64*>(out_v);   // [reps n | aggs n*F | cnt n | slot_of_gid n | first n | inv n]
+  i64* ob = reinterpret_cast<i64*>(out_v);   // [reps ocap | aggs ocap*F | cnt ocap | slot_of_gid ocap | first ocap]
   AggOut o;
   o.reps = ob;
-  o.aggs = reinterpret_cast<u64*>(ob + n);
-  o.cnt = ob + n + n * F;
-  o.slot_of_gid = o.cnt + n;
-  o.first = o.slot_of_gid + n;
-  o.inv = want_inv ? o.first + n : nullptr;
+  o.aggs = reinterpret_cast<u64*>(ob + ocap);
+  o.cnt = ob + ocap + ocap * F;
+  o.slot_of_gid = o.cnt + ocap;
+  o.first = o.slot_of_gid + ocap;
+  o.inv = want_inv ? reinterpret_cast<i64*>(inv_v) : nullptr;
   const u64* k = reinterpret_cast<const u64*>(keys);
   const VT* v = reinterpret_cast<const VT*>(vals);
   const size_t lbytes_low = (size_t)lcap_low * (20 + 8 * F);
   const size_t lbytes_part = (size_t)lcap_part * (20 + 8 * F);
 
-  hipLaunchKernelGGL(agg_init_kernel, dim3(512), dim3(256), 0, st, reinterpret_cast<u64*>(glow_v), gcap_low,
-                     reinterpret_cast<u64*>(gpart_v), gcap_part, F, acc_identity<VT, OP>(), meta);
-  u64* sbuf = reinterpret_cast<u64*>(meta) + sizeof(AggMeta) / 8;   // [4096] after the meta words
-  hipLaunchKernelGGL(agg_sample_gather_kernel, dim3(kSample / 64), dim3(64), 0, st, k, n, sbuf);
-  hipLaunchKernelGGL(agg_sample_kernel, dim3(1), dim3(1024), 0, st, sbuf, n, low_thr, meta);
-  const int gl = (int)std::min<i64>(1024, std::max<i64>(1, (n + 2047) / 2048));
-  hipLaunchKernelGGL((agg_low_kernel<VT, OP>), dim3(gl), dim3(256), lbytes_low, st, k, v, n, F, rs, cs, lcap_low, glow,
-                     meta, o);
+  if (phase == 0 || phase == 1) {
+    hipLaunchKernelGGL(agg_init_kernel, dim3(512), dim3(256), 0, st, reinterpret_cast<u64*>(glow_v), gcap_low,
+                       phase == 0 ? reinterpret_cast<u64*>(gpart_v) : nullptr, gcap_part, F, acc_identity<VT, OP>(), meta);
+    u64* sbuf = reinterpret_cast<u64*>(meta) + sizeof(AggMeta) / 8;   // [4096] after the meta words
+    hipLaunchKernelGGL(agg_sample_gather_kernel, dim3(kSample / 64), dim3(64), 0, st, k, n, sbuf);
+    hipLaunchKernelGGL(agg_sample_kernel, dim3(1), dim3(1024), 0, st, sbuf, n, low_thr, meta);
+    const int gl = (int)std::min<i64>(1024, std::max<i64>(1, (n + 2047) / 2048));
+    hipLaunchKernelGGL((agg_low_kernel<VT, OP>), dim3(gl), dim3(256), lbytes_low, st, k, v, n, F, rs, cs, lcap_low, glow,
+                       meta, o);
+  }
+  if (phase == 2)
+    hipLaunchKernelGGL(agg_init_kernel, dim3(512), dim3(256), 0, st, (u64*)nullptr, gcap_low,
+                       reinterpret_cast<u64*>(gpart_v), gcap_part, F, acc_identity<VT, OP>(), (AggMeta*)nullptr);
   // PART: work buffers [hist P*G u32 | tot P | bstart P+1 | pkey n | pval n*F | prow n (i32) | qkey | qval | qrow]
   const int P = 1 << pbits;
   const int G = agg_groups(n);
@@ -1252,18 +1262,24 @@ int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv,
   const size_t stage_bytes = (size_t)T * (14 + 8 * F);
   const int T2 = std::min(2048, stage_rows(F, 96 * 1024, 1024));   // bucket kernel's sub-partition tiles (2 rows / thread)
   const size_t lds_bucket = std::max((size_t)T2 * (14 + 8 * F), lbytes_part);
-  hipLaunchKernelGGL(agg_hist_kernel, dim3(G), dim3(1024), (size_t)P * 4, st, k, n, rpw, pbits, hist, meta);
-  hipLaunchKernelGGL(scan_rows_kernel, dim3(P), dim3(1024), 0, st, hist, G, tot, meta, 1);
-  hipLaunchKernelGGL(scan_tot_kernel, dim3(1), dim3(1024), 0, st, tot, P, bstart, meta, 1);
-  hipLaunchKernelGGL((agg_scatter_kernel<VT>), dim3(G), dim3(1024), stage_bytes, st, k, v, rs, cs, n, F, rpw, pbits, T, hist,
-                     bstart, pkey, pval, prow, meta);
-  hipLaunchKernelGGL((agg_bucket_kernel<VT, OP>), dim3(P), dim3(1024), lds_bucket, st, pkey, pval, prow, F, lcap_part,
-                     pbits, T2, n, bstart, qkey, qval, qrow, gpart, meta, o);
-  hipLaunchKernelGGL((agg_emit_kernel<VT, OP>), dim3((unsigned)((std::max(gcap_low, gcap_part) + 2 + 255) / 256)),
-                     dim3(256), 0, st, glow, gpart, F, meta, o);
-  if (want_inv)
-    hipLaunchKernelGGL(agg_fix_inv_kernel, dim3((unsigned)std::min<i64>(2048, (n + 255) / 256)), dim3(256), 0, st,
-                       o.inv, n, glow.gid_of_slot, gpart.gid_of_slot, meta);
+  if (phase == 0 || phase == 2) {
+    hipLaunchKernelGGL(agg_hist_kernel, dim3(G), dim3(1024), (size_t)P * 4, st, k, n, rpw, pbits, hist, meta);
+    hipLaunchKernelGGL(scan_rows_kernel, dim3(P), dim3(1024), 0, st, hist, G, tot, meta, 1);
+    hipLaunchKernelGGL(scan_tot_kernel, dim3(1), dim3(1024), 0, st, tot, P, bstart, meta, 1);
+    hipLaunchKernelGGL((agg_scatter_kernel<VT>), dim3(G), dim3(1024), stage_bytes, st, k, v, rs, cs, n, F, rpw, pbits, T,
+                       hist, bstart, pkey, pval, prow, meta);
+    hipLaunchKernelGGL((agg_bucket_kernel<VT, OP>), dim3(P), dim3(1024), lds_bucket, st, pkey, pval, prow, F, lcap_part,
+                       pbits, T2, n, bstart, qkey, qval, qrow, gpart, meta, o);
+  }
+  if (phase == 0 || phase == 2 || phase == 3) {
+    // a phase-3 (LOW) emit never reads the PART table: take_part() is false there
+    hipLaunchKernelGGL((agg_emit_kernel<VT, OP>),
+                       dim3((unsigned)(((phase == 3 ? gcap_low : std::max(gcap_low, gcap_part)) + 2 + 255) / 256)),
+                       dim3(256), 0, st, glow, gpart, F, meta, o);
+    if (want_inv)
+      hipLaunchKernelGGL(agg_fix_inv_kernel, dim3((unsigned)std::min<i64>(2048, (n + 255) / 256)), dim3(256), 0, st,
+                         o.inv, n, glow.gid_of_slot, gpart.gid_of_slot, meta);
+  }
   return (int)hipGetLastError();
 }
 
@@ -1285,9 +1301,12 @@ long long nsdb_agg_work_bytes(long long n, int F, int pbits, int want_inv) {
 // [n, F]).
 int nsdb_hash_aggregate(const void* keys, const void* vals, long long n, int F, int vt, int op, int want_inv,
                         int want_first, void* meta, void* glow, long long gcap_low, void* gpart, long long gcap_part,
-                        void* out, void* work, int pbits, int lcap_low, int lcap_part, int low_thr, long long vrs,
-                        long long vcs, hipStream_t st) {
+                        void* out, void* inv, long long ocap, int phase, void* work, int pbits, int lcap_low,
+                        int lcap_part, int low_thr, long long vrs, long long vcs, hipStream_t st) {
   if (n <= 0) return 0;
+  if (phase < 0 || phase > 3 || ocap <= 0 || (want_inv && inv == nullptr)) return (int)hipErrorInvalidValue;
+  if ((phase == 0 || phase == 2) && (ocap < n || work == nullptr || gpart == nullptr)) return (int)hipErrorInvalidValue;
+  if (ocap < gcap_low + 1 && ocap < n) return (int)hipErrorInvalidValue;   // every LOW group needs an output row
   if (n >= (1LL << 31)) return (int)hipErrorInvalidValue;
   if (F < 0 || F > 16 || pbits < 0 || pbits > 10) return (int)hipErrorInvalidValue;
   auto pow2 = [](long long x) { return x > 0 && (x & (x - 1)) == 0; };
@@ -1299,7 +1318,7 @@ int nsdb_hash_aggregate(const void* keys, const void* vals, long long n, int F, 
     vrs = F;
     vcs = 1;
   }
-#define NSDB_AGG(VT, OP) agg_launch_t<VT, OP>(keys, vals, n, F, want_inv, want_first, meta, glow, gcap_low, gpart, gcap_part, out, work, pbits, lcap_low, lcap_part, low_thr, vrs, vcs, st)
+#define NSDB_AGG(VT, OP) agg_launch_t<VT, OP>(keys, vals, n, F, want_inv, want_first, meta, glow, gcap_low, gpart, gcap_part, out, inv, ocap, phase, work, pbits, lcap_low, lcap_part, low_thr, vrs, vcs, st)
   if (vt == 0) {
     if (op == 0) return NSDB_AGG(double, OP_SUM);
     if (op == 1) return NSDB_AGG(double, OP_MIN);

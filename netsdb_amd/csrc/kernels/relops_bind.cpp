@@ -5,6 +5,7 @@
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <limits>
 #include <string>
 #include <tuple>
@@ -17,8 +18,8 @@ extern "C" {
 long long nsdb_agg_work_bytes(long long n, int F, int pbits, int want_inv);
 int nsdb_hash_aggregate(const void* keys, const void* vals, long long n, int F, int vt, int op, int want_inv,
                         int want_first, void* meta, void* glow, long long gcap_low, void* gpart, long long gcap_part,
-                        void* out, void* work, int pbits, int lcap_low, int lcap_part, int low_thr, long long vrs,
-                        long long vcs, hipStream_t st);
+                        void* out, void* inv, long long ocap, int phase, void* work, int pbits, int lcap_low,
+                        int lcap_part, int low_thr, long long vrs, long long vcs, hipStream_t st);
 int nsdb_join_insert(const void* keys, long long n, void* tab, long long cap, int* row_slot, unsigned* row_rank,
                      unsigned long long* ndup, hipStream_t st);
 int nsdb_join_perm(const int* row_slot, const unsigned* row_rank, long long n, const unsigned long long* ndup,
@@ -60,15 +61,22 @@ constexpr int kMetaWords = 16 + 4096;   // AggMeta + the sampled keys (relops.hi
 // Returns (reps [g] i64, aggs [g, F] (vals dtype), counts [g] i64, first [g] i64 (smallest row of each group; only
 // meaningful with want_first, which otherwise lets the partition passes skip row ids),
 // inv [n] i64 (or empty), status): status = [g, path (0 LOW, 1 PART), ok (0: the PART table overflowed; outputs
-// invalid, fall back), distinct keys in the 4096-row sample]. low_threshold: largest estimated group count for the
-// LOW path (0: automatic).
+// invalid, fall back), distinct keys in the 4096-row sample, scratch bytes used]. low_threshold: largest estimated
+// group count for the LOW path (0: automatic).
+//
+// Scratch is sized for the path that runs. Phase 1 (sample + LOW) needs O(groups) words: the LOW global table and an
+// output of gcap_low + 1 groups. Only when the device reports that the LOW path did not take the rows (one host read,
+// which the LOW path needs anyway for its group count) are the PART buffers allocated — about 2 (12 + 8 F) n bytes of
+// partitioned rows plus an n-group output — and `scratch(+bytes)` / `scratch(-bytes)` (a Python callable, e.g. the
+// storage manager's device-budget accounting) is told before they are allocated and after they are released.
 std::vector<torch::Tensor> hash_aggregate(torch::Tensor keys, c10::optional<torch::Tensor> vals, const std::string& op,
-                                          bool want_inv, int64_t low_threshold, bool want_first) {
+                                          bool want_inv, int64_t low_threshold, bool want_first,
+                                          pybind11::object scratch) {
   TORCH_CHECK(keys.is_cuda(), "keys must be a GPU tensor");
   TORCH_CHECK(keys.scalar_type() == torch::kInt64 && keys.dim() == 1, "keys must be 1-D int64");
   keys = keys.contiguous();
   const int64_t n = keys.numel();
-  TORCH_CHECK(n < (int64_t(1) << 31), "hash_aggregate: at most 2^31 - 1 rows per call");
+  TORCH_CHECK(n < (int64_t(1) << 31), "hash_aggregate: at most 2^31 - 1 rows per call (the caller chunks)");
   int opc = op == "sum" ? 0 : op == "min" ? 1 : op == "max" ? 2 : -1;
   TORCH_CHECK(opc >= 0, "op must be sum, min or max");
   int F = 0, vt = 0;
@@ -94,14 +102,16 @@ std::vector<torch::Tensor> hash_aggregate(torch::Tensor keys, c10::optional<torc
   auto i64 = keys.options().dtype(torch::kInt64);
   if (n == 0) {
     return {torch::empty({0}, i64), torch::empty({0, F}, keys.options().dtype(vdtype)), torch::empty({0}, i64),
-            torch::empty({0}, i64), torch::empty({0}, i64), torch::tensor({0, 0, 1, 0}, torch::kInt64)};
+            torch::empty({0}, i64), torch::empty({0}, i64), torch::tensor({0, 0, 1, 0, 0}, torch::kInt64)};
   }
   // LDS tables: LOW <= 64 KiB (two workgroups per CU), PART <= 128 KiB. PART: level-1 buckets = one per CU
   // (256) once there are >= 2048 rows per bucket; each bucket workgroup splits its bucket further on the device
   // from the sampled distinct-key estimate (relops.hip agg_bucket_kernel), so no host decision needs the data.
   const int64_t entry = 20 + 8 * F;
   const int64_t lcap_low = std::min<int64_t>(1024, pow2_at_most(65536 / entry));   // <= 36 KB: 4+ LOW workgroups per CU
-  const int64_t lcap_part = std::min<int64_t>(4096, pow2_at_most(131072 / entry));
+  int64_t lcap_part = std::min<int64_t>(4096, pow2_at_most(131072 / entry));
+  // test hook: a tiny PART LDS table (power of two >= 64) makes the PART overflow table fill (status ok = 0)
+  if (const char* e = std::getenv("NSDB_AGG_TEST_LCAP_PART")) lcap_part = std::max<int64_t>(64, pow2_at_most(std::atoll(e)));
   int pbits = 0;
   while (pbits < 8 && (n >> (pbits + 1)) >= 2048) ++pbits;
   const int64_t gcap_low = 4 * lcap_low;
@@ -111,32 +121,59 @@ std::vector<torch::Tensor> hash_aggregate(torch::Tensor keys, c10::optional<torc
 
   auto meta = torch::empty({kMetaWords}, i64);
   auto glow = torch::empty({(gcap_low + 1) * (4 + F)}, i64);
-  auto gpart = torch::empty({(gcap_part + 1) * (4 + F)}, i64);
-  // [reps n | aggs n*F | cnt n | slot_of_gid n | first n | inv n] (relops.hip agg_launch_t AggOut)
-  auto out = torch::empty({n * (4 + F) + (want_inv ? n : 0)}, i64);
-  const int64_t wbytes = nsdb_agg_work_bytes(n, F, pbits, want_inv ? 1 : 0);
-  auto work = torch::empty({(wbytes + 7) / 8}, i64);
-  rc_ok(nsdb_hash_aggregate(keys.data_ptr(), F ? v.data_ptr() : nullptr, n, F, vt, opc, want_inv ? 1 : 0, want_first ? 1 : 0,
-                            meta.data_ptr(), glow.data_ptr(), gcap_low, gpart.data_ptr(), gcap_part, out.data_ptr(),
-                            work.data_ptr(), pbits, (int)lcap_low, (int)lcap_part, (int)thr, (long long)vrs,
-                            (long long)vcs, stream()),
-        "hash_aggregate");
-  auto m = meta.narrow(0, 0, 16).cpu();   // the one host read: group count and path flags
+  auto inv = want_inv ? torch::empty({n}, i64) : torch::empty({0}, i64);
+  const int64_t ocap_low = std::min<int64_t>(n, gcap_low + 1);
+  auto out = torch::empty({ocap_low * (4 + F)}, i64);
+  int64_t ocap = ocap_low;
+  auto launch = [&](int phase, void* gpart, void* work) {
+    rc_ok(nsdb_hash_aggregate(keys.data_ptr(), F ? v.data_ptr() : nullptr, n, F, vt, opc, want_inv ? 1 : 0,
+                              want_first ? 1 : 0, meta.data_ptr(), glow.data_ptr(), gcap_low, gpart, gcap_part,
+                              out.data_ptr(), want_inv ? inv.data_ptr() : nullptr, ocap, phase, work, pbits,
+                              (int)lcap_low, (int)lcap_part, (int)thr, (long long)vrs, (long long)vcs, stream()),
+          "hash_aggregate");
+  };
+  launch(1, nullptr, nullptr);
+  auto m = meta.narrow(0, 0, 16).cpu();   // the host read: group count and path flags
   const ll* mp = LL(m.data_ptr<int64_t>());
   // AggMeta words: 0 est, 1 low, 2 ng_low, 3 ng_part, 4 fail_low, 5 fail_part
   const bool low_ok = mp[1] != 0 && mp[4] == 0;
-  const int64_t g = (int64_t)(low_ok ? mp[2] : mp[3]);
-  const bool ok = low_ok || mp[5] == 0;
-  auto status = torch::tensor({(int64_t)g, (int64_t)(low_ok ? 0 : 1), (int64_t)(ok ? 1 : 0), (int64_t)mp[0]}, torch::kInt64);
+  int64_t scratch_bytes = (int64_t)(meta.numel() + glow.numel() + inv.numel() + out.numel()) * 8;
+  bool ok = true;
+  int64_t g = 0;
+  if (low_ok) {
+    launch(3, nullptr, nullptr);
+    g = (int64_t)mp[2];
+  } else {
+    const int64_t wbytes = nsdb_agg_work_bytes(n, F, pbits, want_inv ? 1 : 0);
+    const int64_t part_bytes = ((gcap_part + 1) * (4 + F) + n * (4 + F)) * 8 + wbytes;
+    if (!scratch.is_none()) scratch(part_bytes);
+    try {
+      auto gpart = torch::empty({(gcap_part + 1) * (4 + F)}, i64);
+      auto work = torch::empty({(wbytes + 7) / 8}, i64);
+      ocap = n;
+      out = torch::empty({n * (4 + F)}, i64);
+      launch(2, gpart.data_ptr(), work.data_ptr());
+      auto m2 = meta.narrow(0, 0, 16).cpu();
+      const ll* mp2 = LL(m2.data_ptr<int64_t>());
+      g = (int64_t)mp2[3];
+      ok = mp2[5] == 0;
+      scratch_bytes += part_bytes - (int64_t)ocap_low * (4 + F) * 8;
+    } catch (...) {
+      if (!scratch.is_none()) scratch(-part_bytes);
+      throw;
+    }
+    if (!scratch.is_none()) scratch(-part_bytes);
+  }
+  auto status = torch::tensor({(int64_t)g, (int64_t)(low_ok ? 0 : 1), (int64_t)(ok ? 1 : 0), (int64_t)mp[0],
+                               scratch_bytes}, torch::kInt64);
   if (!ok) return {torch::Tensor(), torch::Tensor(), torch::Tensor(), torch::Tensor(), torch::Tensor(), status};
   auto reps = out.narrow(0, 0, g);
-  auto aggs = out.narrow(0, n, g * F).view({g, F});
+  auto aggs = out.narrow(0, ocap, g * F).view({g, F});
   if (vt == 0) aggs = aggs.view(torch::kFloat64);
-  auto cnt = out.narrow(0, n + n * F, g);
-  auto first = out.narrow(0, n * (3 + F), g);
-  torch::Tensor inv = want_inv ? out.narrow(0, n * (4 + F), n) : torch::empty({0}, i64);
-  // the views keep the whole n-row buffer alive: copy small results out of it
-  if (g * 4 < n) {
+  auto cnt = out.narrow(0, ocap + ocap * F, g);
+  auto first = out.narrow(0, ocap * (3 + F), g);
+  // the views keep the whole ocap-row buffer alive: copy small results out of a large one
+  if (ocap > ocap_low && g * 4 < ocap) {
     reps = reps.clone();
     aggs = aggs.clone();
     cnt = cnt.clone();
@@ -230,14 +267,15 @@ std::vector<torch::Tensor> partition_perm(torch::Tensor dest, int64_t P) {
 
 std::vector<torch::Tensor> hash_aggregate_impl(torch::Tensor keys, c10::optional<torch::Tensor> vals,
                                                const std::string& op, bool want_inv, int64_t low_threshold) {
-  return hash_aggregate(keys, vals, op, want_inv, low_threshold, true);
+  return hash_aggregate(keys, vals, op, want_inv, low_threshold, true, pybind11::none());
 }
 
 void register_relops(pybind11::module& m) {
   m.def("hash_aggregate", &hash_aggregate,
-        "device hash group-by + aggregate: (reps, aggs, counts, first, inv, status[g, path, ok, sample_distinct])",
+        "device hash group-by + aggregate: (reps, aggs, counts, first, inv, status[g, path, ok, sample_distinct, scratch_bytes])",
         pybind11::arg("keys"), pybind11::arg("vals") = pybind11::none(), pybind11::arg("op") = "sum",
-        pybind11::arg("want_inv") = false, pybind11::arg("low_threshold") = 0, pybind11::arg("want_first") = true);
+        pybind11::arg("want_inv") = false, pybind11::arg("low_threshold") = 0, pybind11::arg("want_first") = true,
+        pybind11::arg("scratch") = pybind11::none());
   m.def("join_build", &join_build, "device hash-join build: (table, perm)");
   m.def("join_probe", &join_probe, "device hash-join probe: (build_idx, probe_idx)");
   m.def("partition_perm", &partition_perm, "stable device partition permutation: (perm, counts)");

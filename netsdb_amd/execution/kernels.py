@@ -12,6 +12,7 @@ operators are sort / unique / searchsorted tensor ops.
 """
 from __future__ import annotations
 
+import weakref
 from typing import Any, List, Tuple
 
 import torch
@@ -99,9 +100,10 @@ class JoinTable:
         self.n = int(build_h.numel())
         self._dev = None
         self._sorted = None
-        if self.n and build_h.is_cuda:
+        if self.n and build_h.is_cuda and self.n < JOIN_TABLE_MAX_ROWS:
             self._dev = _ext.hip().join_build(build_h.long().contiguous())
         elif self.n:
+            # builds past the device table's 2^29-row bound (32-bit payloads): sorted keys + binary search, on the device
             self._sorted = torch.sort(build_h)
 
     def probe(self, probe_h: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -127,6 +129,9 @@ class JoinTable:
         offs = torch.arange(probe_idx.numel(), device=dev) - torch.repeat_interleave(csum - cnt, cnt)
         build_idx = order[starts + offs]
         return build_idx, probe_idx
+
+
+JOIN_TABLE_MAX_ROWS = 1 << 29
 
 
 def join_match(build_h: torch.Tensor, probe_h: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -250,12 +255,90 @@ def _rows_match_rep(cols, words, ref: torch.Tensor) -> bool:
     return bool(ok.all())
 
 
+# ------------------------------------------------------------------------ relational scratch accounting
+# The device relational kernels' scratch (the PART path's partitioned rows and n-group output) is charged to the
+# storage manager that owns the device's HBM budget while it is allocated, so out-of-core accounting sees it (it may
+# evict pages to make room). One manager per device (the client's), registered by the StorageManager.
+_SCRATCH = {}
+SCRATCH_STATS = {"charged_bytes": 0, "peak_bytes": 0, "calls": 0}
+
+
+def register_scratch_accounting(manager) -> None:
+    dev = getattr(manager, "home", None)
+    if dev is not None and torch.device(dev).type == "cuda":
+        _SCRATCH[str(torch.device(dev))] = weakref.ref(manager)
+
+
+def _scratch_cb(dev):
+    ref = _SCRATCH.get(str(dev))
+    m = ref() if ref is not None else None
+
+    def cb(nbytes: int):
+        nbytes = int(nbytes)
+        if nbytes > 0:
+            SCRATCH_STATS["calls"] += 1
+            SCRATCH_STATS["charged_bytes"] += nbytes
+            SCRATCH_STATS["peak_bytes"] = max(SCRATCH_STATS["peak_bytes"], SCRATCH_STATS["charged_bytes"])
+            if m is not None:
+                m.account_bytes(nbytes, m.home)
+        else:
+            SCRATCH_STATS["charged_bytes"] += nbytes
+            if m is not None:
+                m.release_bytes(-nbytes, m.home)
+    return cb
+
+
+# rows per device aggregation call (the kernels index rows with 32-bit offsets): larger inputs are chunked and the
+# per-chunk groups merged
+AGG_CHUNK_ROWS = (1 << 31) - (1 << 20)
+LAST_AGG_STATUS = {}
+
+
 def _hash_aggregate(key64: torch.Tensor, vals, op: str, want_inv: bool, want_first: bool = True):
-    r = _ext.hip().hash_aggregate(key64.contiguous(), vals, op, want_inv, 0, want_first)
+    n = key64.numel()
+    if n > AGG_CHUNK_ROWS:
+        return _hash_aggregate_chunked(key64, vals, op, want_inv, want_first)
+    r = _ext.hip().hash_aggregate(key64.contiguous(), vals, op, want_inv, 0, want_first, _scratch_cb(key64.device))
     status = r[5].tolist()
+    LAST_AGG_STATUS.update(groups=status[0], path=("LOW", "PART")[status[1]], ok=status[2],
+                           sample_distinct=status[3], scratch_bytes=status[4] if len(status) > 4 else None)
     if status[2] != 1:
         return None
     return r[0], r[1], r[2], r[3], r[4]
+
+
+def _hash_aggregate_chunked(key64, vals, op, want_inv, want_first):
+    """> AGG_CHUNK_ROWS rows: aggregate each chunk, then merge the chunks' groups (sum of sums / counts, min of mins,
+    max of maxes); first rows and the per-row inverse are mapped through the merge."""
+    n = key64.numel()
+    parts = []
+    for s in range(0, n, AGG_CHUNK_ROWS):
+        e = min(n, s + AGG_CHUNK_ROWS)
+        r = _hash_aggregate(key64[s:e], None if vals is None else vals[s:e], op, want_inv, want_first)
+        if r is None:
+            return None
+        parts.append((s, r))
+    reps = torch.cat([r[0] for _, r in parts])
+    has_v = vals is not None and parts[0][1][1] is not None and parts[0][1][1].numel()
+    aggs = torch.cat([r[1] for _, r in parts]) if has_v else None
+    cnts = torch.cat([r[2] for _, r in parts])
+    firsts = torch.cat([r[3] + s for s, r in parts])
+    m = _hash_aggregate(reps, aggs, op, True, False)   # merge: the chunks' groups are few
+    if m is None:
+        return None
+    g_reps, g_aggs, _, _, ginv, = m
+    g = g_reps.numel()
+    g_cnt = torch.zeros(g, dtype=torch.int64, device=reps.device).index_add_(0, ginv, cnts)
+    g_first = torch.full((g,), n, dtype=torch.int64, device=reps.device).scatter_reduce_(0, ginv, firsts, "amin")
+    inv = None
+    if want_inv:
+        off, invs = 0, []
+        for s, r in parts:
+            k = r[0].numel()
+            invs.append(ginv[off: off + k].index_select(0, r[4]))
+            off += k
+        inv = torch.cat(invs)
+    return g_reps, g_aggs, g_cnt, g_first, inv
 
 
 def _sort_groups(key_reps: torch.Tensor):

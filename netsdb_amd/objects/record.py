@@ -338,6 +338,9 @@ class RecordBatch:
         for c in cols.values():
             if isinstance(c, (torch.Tensor, StringColumn, NestedColumn)):
                 return c.device
+        for c in cols.values():             # only object columns: where their records live (a scan's tuple set)
+            if isinstance(c, RecordBatch):
+                return c.device
         return torch.device("cpu")
 
     @staticmethod

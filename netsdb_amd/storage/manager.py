@@ -104,6 +104,10 @@ class StorageManager:
             chunk = page_pool_chunk or ((256 << 20) if self.home.type == "cuda" else (16 << 20))
             self.page_pool = DevicePagePool(self.home, chunk, max_bytes=self.device_budget)
         self.device_bytes = 0
+        # the device relational kernels charge their scratch to this manager's budget (execution/kernels.py)
+        from ..execution.kernels import register_scratch_accounting
+
+        register_scratch_accounting(self)
         # per locality set: everything of it resident on the device tier (pages and dense panels) in recency
         # order, oldest first (LocalitySet::cachedPages: pop_front for LRU, pop_back for MRU)
         self._resident: Dict[int, Tuple[object, "OrderedDict[int, object]"]] = {}

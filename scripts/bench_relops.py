@@ -3,6 +3,7 @@
   * group-by + sum of 16 M rows (int64 key, one f64 value) at 8, 10 k and 10 M distinct keys:
     hash_aggregate (relops.hip) vs torch.unique(return_inverse) + index_add_;
   * hash join: build 2 M rows, probe 16 M rows (PK-FK, ~1 match per probe) via JoinTable vs sort + searchsorted;
+    and a build-size sweep (2 / 16 / 64 M unique build keys, 16 M probes): build, probe, build + probe;
   * partition permutation of 16 M rows over 8 destinations: partition_perm vs argsort(stable) + bincount.
 
     python scripts/bench_relops.py [--rows 16000000] [--rounds 5] [--json out.json]
@@ -116,6 +117,22 @@ def main():
     t["build_rows"], t["probe_rows"], t["matches"] = nb, n, int(pi.numel())
     out["join"] = t
     print(json.dumps({"join": t}), flush=True)
+    del jt, bi, pi
+    # build-size sweep: unique-key builds of 2 / 16 / 64 M rows, each probed by 16 M keys (~90 % matching)
+    out["join_sweep"] = {}
+    for nb2 in (2_000_000, 16_000_000, 64_000_000):
+        b2 = torch.randperm(nb2, device=dev, generator=g) * 7 + 1
+        p2 = torch.randint(0, nb2, (n,), device=dev, generator=g) * 7 + 1
+        p2[::10] = -5
+        jt2 = K.JoinTable(b2)
+        bi2, pi2 = jt2.probe(p2)
+        assert torch.equal(b2[bi2], p2[pi2]) and pi2.numel() == int((p2 > 0).sum())
+        t = run({"build": lambda: K.JoinTable(b2), "probe": lambda: jt2.probe(p2),
+                 "build_probe": lambda: K.JoinTable(b2).probe(p2)}, a.rounds)
+        t["build_rows"], t["probe_rows"], t["matches"] = nb2, n, int(pi2.numel())
+        out["join_sweep"][str(nb2)] = t
+        print(json.dumps({"join_sweep": nb2, **t}), flush=True)
+        del b2, p2, jt2, bi2, pi2
     dest = torch.randint(0, 8, (n,), device=dev, generator=g)
     t = run({"partition_perm": lambda: K.partition_order(dest, 8),
              "torch_argsort_bincount": lambda: (torch.argsort(dest, stable=True),

@@ -372,3 +372,72 @@ def test_hash_aggregate_column_major_values(distinct):
     assert torch.equal(a[0][oa], b[0][ob]) and torch.equal(a[2][oa], b[2][ob]) and torch.equal(a[3][oa], b[3][ob])
     torch.testing.assert_close(a[1][oa], b[1][ob], rtol=1e-12, atol=1e-9)
     _check_agg(keys[:50_000], vc[:50_000], "max", _ext.hip().hash_aggregate(keys[:50_000], vc[:50_000], "max", True, 0))
+
+
+@pytest.mark.gpu
+def test_low_path_scratch_is_o_groups():
+    """LOW-path aggregation: scratch is the LOW table + an output of its capacity, whatever n (no n-sized buffers);
+    the PART path's buffers are allocated only when it runs, and are charged to the storage manager meanwhile."""
+    from netsdb_amd.execution import kernels as K
+
+    h = _ext.hip()
+    sizes = []
+    for n in (1 << 20, 1 << 24):
+        keys = torch.randint(0, 8, (n,), device=DEV) * 977
+        vals = torch.rand(n, device=DEV, dtype=torch.float64)
+        r = h.hash_aggregate(keys, vals, "sum", False, 0, False)
+        st = r[5].tolist()
+        assert st[1] == 0 and st[2] == 1 and st[0] == 8          # LOW path, ok, 8 groups
+        sizes.append(st[4])
+        ref = torch.zeros(8, dtype=torch.float64, device=DEV).index_add_(0, keys // 977, vals)
+        o = torch.argsort(r[0])
+        assert torch.allclose(r[1][o, 0], ref, rtol=1e-9)
+    assert sizes[0] == sizes[1] and sizes[1] < (1 << 20), sizes
+    # PART path: charged while allocated, released after
+    calls = []
+    n = 1 << 22
+    keys = torch.randperm(n, device=DEV)
+    r = h.hash_aggregate(keys, None, "sum", False, 0, False, lambda b: calls.append(b))
+    st = r[5].tolist()
+    assert st[1] == 1 and st[2] == 1 and st[0] == n
+    assert len(calls) == 2 and calls[0] > 0 and calls[0] == -calls[1] and st[4] > n * 8
+    K.SCRATCH_STATS["charged_bytes"] = 0
+
+
+@pytest.mark.gpu
+def test_part_overflow_falls_back_exactly(monkeypatch):
+    """A PART LDS table so small that its overflow table fills: hash_aggregate reports ok = 0, group_reduce returns
+    None, and the engine's generic path gives the exact result."""
+    from netsdb_amd.execution import kernels as K
+
+    monkeypatch.setenv("NSDB_AGG_TEST_LCAP_PART", "64")
+    n = 1 << 20
+    keys = torch.randint(0, 1 << 19, (n,), device=DEV) * 3 + 1
+    vals = torch.rand(n, device=DEV, dtype=torch.float64)
+    r = _ext.hip().hash_aggregate(keys, vals, "sum", False, 0, True)
+    assert r[5].tolist()[2] == 0                                   # the PART overflow table filled
+    assert K.group_reduce(keys, vals, "sum") is None               # the fused path refuses ...
+    inv, reps, g = K.group_ids(keys.cpu())                          # ... and the generic path is exact
+    agg = K.segment_reduce(vals.cpu(), inv, g, "sum")
+    u, ui = torch.unique(keys.cpu(), return_inverse=True)
+    assert torch.equal(reps, u) and torch.allclose(agg, torch.zeros(u.numel(), dtype=torch.float64).index_add_(0, ui, vals.cpu()))
+    monkeypatch.delenv("NSDB_AGG_TEST_LCAP_PART")
+    r2 = _ext.hip().hash_aggregate(keys, vals, "sum", False, 0, True)
+    assert r2[5].tolist()[2] == 1
+
+
+@pytest.mark.gpu
+def test_chunked_aggregation_matches_unchunked(monkeypatch):
+    """Inputs past the per-call row bound are aggregated chunk by chunk and merged (forced with a small bound)."""
+    from netsdb_amd.execution import kernels as K
+
+    n = 300_000
+    keys = torch.randint(0, 5000, (n,), device=DEV)
+    vals = torch.rand(n, 2, device=DEV, dtype=torch.float64)
+    full = K.group_reduce(keys, vals, "sum")
+    monkeypatch.setattr(K, "AGG_CHUNK_ROWS", 70_000)
+    part = K.group_reduce(keys, vals, "sum")
+    assert torch.equal(full[0], part[0]) and torch.allclose(full[1], part[1], rtol=1e-9)
+    inv, reps, g = K.group_ids(keys)
+    u, ui = torch.unique(keys, return_inverse=True)
+    assert torch.equal(reps, u) and torch.equal(inv, ui)
