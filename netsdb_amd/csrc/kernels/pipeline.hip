@@ -351,6 +351,31 @@ __global__ void __launch_bounds__(NTHR) pipe_agg_kernel(const PipeArgs a) {
   }
 }
 
+// Filter only: the predicate program over every row, the keep flag written as one byte per row (the FILTER of a
+// scan-filter stage that feeds a join / materialisation: no comparison column, literal column or AND of two masks is
+// materialised; the engine turns the mask into the stage's row selection).
+__global__ void __launch_bounds__(NTHR) pipe_mask_kernel(const PipeArgs a, unsigned char* __restrict__ mask) {
+  regfile R[ROWS];
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j) R[j] = (regfile)0;
+  const int tid = threadIdx.x;
+  const long long step = (long long)gridDim.x * NTHR * ROWS;
+  for (long long base = (long long)blockIdx.x * NTHR * ROWS; base < a.n; base += step) {
+    long long row[ROWS];
+    bool inr[ROWS];
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      row[j] = base + (long long)j * NTHR + tid;
+      inr[j] = row[j] < a.n;
+    }
+    for (int c = 0; c < a.ncol; ++c) load_col(a.col[c], c, row, inr, R);
+    run(a, R, 0, a.nins);
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j)
+      if (inr[j]) mask[row[j]] = (unsigned char)(a.keep_reg < 0 ? 1 : (R[j][a.keep_reg] != 0));
+  }
+}
+
 }  // namespace nsdb_pipe
 
 extern "C" {
@@ -377,6 +402,14 @@ int nsdb_pipe_agg(const void* args, int grid, hipStream_t st) {
     hipLaunchKernelGGL(nsdb_pipe::pipe_agg_kernel<2>, dim3(grid), dim3(nsdb_pipe::NTHR), 0, st, a);
   else
     hipLaunchKernelGGL(nsdb_pipe::pipe_agg_kernel<nsdb_pipe::FMAX>, dim3(grid), dim3(nsdb_pipe::NTHR), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+int nsdb_pipe_mask(const void* args, unsigned char* mask, int grid, hipStream_t st) {
+  if (grid <= 0) return -1;
+  const nsdb_pipe::PipeArgs& a = *reinterpret_cast<const nsdb_pipe::PipeArgs*>(args);
+  if (a.nins > nsdb_pipe::MAXINS || a.ncol > nsdb_pipe::MAXCOL) return -2;
+  hipLaunchKernelGGL(nsdb_pipe::pipe_mask_kernel, dim3(grid), dim3(nsdb_pipe::NTHR), 0, st, a, mask);
   return (int)hipGetLastError();
 }
 

@@ -14,6 +14,7 @@
 extern "C" {
 int nsdb_pipe_sizes(int* out);
 int nsdb_pipe_agg(const void* args, int grid, hipStream_t st);
+int nsdb_pipe_mask(const void* args, unsigned char* mask, int grid, hipStream_t st);
 }
 
 namespace {
@@ -65,15 +66,16 @@ void check_col(const torch::Tensor& t, int64_t n, const char* what) {
 
 // prog: int64 [nins, 5] (op, dst, a, b, imm) on the CPU.
 // cols: per column (kind, late, L, data, starts, ends, bytes): data for numeric kinds, starts / ends / bytes for strings.
-std::vector<torch::Tensor> pipe_agg(torch::Tensor prog, int64_t nins_a,
-                                    std::vector<std::tuple<int64_t, int64_t, int64_t, c10::optional<torch::Tensor>,
-                                                           c10::optional<torch::Tensor>, c10::optional<torch::Tensor>,
-                                                           c10::optional<torch::Tensor>>> cols,
-                                    torch::Tensor lit, int64_t n, int64_t keep_reg, int64_t key_reg,
-                                    std::vector<int64_t> val_regs, int64_t agg_op, int64_t max_wg) {
+typedef std::vector<std::tuple<int64_t, int64_t, int64_t, c10::optional<torch::Tensor>, c10::optional<torch::Tensor>,
+                               c10::optional<torch::Tensor>, c10::optional<torch::Tensor>>>
+    ColList;
+
+// Validate the program / columns / registers and fill the kernel's argument image.
+void fill_args(PipeArgs& a, const torch::Tensor& prog, int64_t nins_a, const ColList& cols, const torch::Tensor& lit,
+               int64_t n, int64_t keep_reg, int64_t key_reg, const std::vector<int64_t>& val_regs, int64_t agg_op) {
   TORCH_CHECK(sizes(0) == MAXINS && sizes(1) == MAXCOL && sizes(3) == FMAX && sizes(5) == (int)sizeof(PipeArgs),
               "pipe_agg: host / kernel argument layout mismatch");
-  const int NREG = sizes(2), CAP = sizes(4), ROWS = sizes(6), NTHR = sizes(7);
+  const int NREG = sizes(2);
   TORCH_CHECK(prog.device().is_cpu() && prog.scalar_type() == torch::kInt64 && prog.dim() == 2 && prog.size(1) == 5,
               "pipe_agg: prog must be a CPU int64 [nins, 5] tensor");
   const int nins = (int)prog.size(0), ncol = (int)cols.size(), nval = (int)val_regs.size();
@@ -83,7 +85,6 @@ std::vector<torch::Tensor> pipe_agg(torch::Tensor prog, int64_t nins_a,
   TORCH_CHECK(agg_op >= 0 && agg_op <= 2, "pipe_agg: agg_op is 0 sum, 1 min, 2 max");
   TORCH_CHECK(keep_reg >= -1 && keep_reg < NREG && key_reg >= -1 && key_reg < NREG, "pipe_agg: bad keep/key reg");
   TORCH_CHECK(lit.is_cuda() && lit.scalar_type() == torch::kUInt8 && lit.is_contiguous(), "pipe_agg: lit");
-  PipeArgs a;
   std::memset(&a, 0, sizeof(a));
   auto P = prog.accessor<int64_t, 2>();
   for (int i = 0; i < nins; ++i) {
@@ -106,7 +107,7 @@ std::vector<torch::Tensor> pipe_agg(torch::Tensor prog, int64_t nins_a,
   a.nins = nins;
   a.nins_a = (int)nins_a;
   for (int c = 0; c < ncol; ++c) {
-    auto& t = cols[c];
+    const auto& t = cols[c];
     Col& C = a.col[c];
     C.kind = (int)std::get<0>(t);
     C.late = (int)std::get<1>(t);
@@ -147,6 +148,14 @@ std::vector<torch::Tensor> pipe_agg(torch::Tensor prog, int64_t nins_a,
     a.val_reg[f] = (int)val_regs[f];
   }
   a.agg_op = (int)agg_op;
+}
+
+std::vector<torch::Tensor> pipe_agg(torch::Tensor prog, int64_t nins_a, ColList cols, torch::Tensor lit, int64_t n,
+                                    int64_t keep_reg, int64_t key_reg, std::vector<int64_t> val_regs, int64_t agg_op,
+                                    int64_t max_wg) {
+  const int CAP = sizes(4), ROWS = sizes(6), NTHR = sizes(7);
+  PipeArgs a;
+  fill_args(a, prog, nins_a, cols, lit, n, keep_reg, key_reg, val_regs, agg_op);
   const long long per = (long long)NTHR * ROWS * 4;
   const int nwg = (int)std::max<long long>(1, std::min<long long>(max_wg > 0 ? max_wg : 2048, (n + per - 1) / per));
   auto dev = lit.device();
@@ -168,9 +177,26 @@ std::vector<torch::Tensor> pipe_agg(torch::Tensor prog, int64_t nins_a,
   return {out_key, out_cnt, out_val, out_occ, status};
 }
 
+// The predicate program's keep flag per row (uint8 [n]); key / values unused.
+torch::Tensor pipe_mask(torch::Tensor prog, ColList cols, torch::Tensor lit, int64_t n, int64_t keep_reg) {
+  const int ROWS = sizes(6), NTHR = sizes(7);
+  PipeArgs a;
+  fill_args(a, prog, prog.size(0), cols, lit, n, keep_reg, -1, {}, 0);
+  auto mask = torch::empty({n}, lit.options().dtype(torch::kUInt8));
+  if (n > 0) {
+    const long long per = (long long)NTHR * ROWS * 4;
+    const int nwg = (int)std::max<long long>(1, std::min<long long>(4096, (n + per - 1) / per));
+    const int rc = nsdb_pipe_mask(&a, mask.data_ptr<uint8_t>(), nwg, c10::hip::getCurrentHIPStream().stream());
+    TORCH_CHECK(rc == 0, "pipe_mask launch failed: ", rc);
+  }
+  return mask;
+}
+
 }  // namespace
 
 void register_pipeline(pybind11::module& m) {
+  m.def("pipe_mask", &pipe_mask, "fused filter predicate (pipeline.hip): keep flag per row (uint8)",
+        pybind11::arg("prog"), pybind11::arg("cols"), pybind11::arg("lit"), pybind11::arg("n"), pybind11::arg("keep_reg"));
   m.def("pipe_agg", &pipe_agg,
         "fused scan -> filter -> project -> low-cardinality aggregate (pipeline.hip): per-workgroup partial "
         "(keys, counts, values[.., 8], occupancy, status[overflow])",

@@ -397,7 +397,12 @@ class QueryEngine:
             self.pipeline_stats["fused_stages"] += 1
 
     def _apply_ops(self, ops, it, state):
-        """Stream batches through a segment's atoms (generator: one page in flight per stage)."""
+        """Stream batches through a segment's atoms (generator: one page in flight per stage). Runs of lambda-tree
+        APPLYs ending in their FILTER execute as one fused predicate launch (execution/pipeline.py)."""
+        if self.fused_pipelines and any(o["type"] == "FILTER" for o in ops):
+            from . import pipeline as PL
+
+            ops = PL.fuse_filters(ops, state.comps)
         for b in it:
             for o in ops:
                 if b.n == 0 and o["type"] != "JOIN":
@@ -465,7 +470,7 @@ class QueryEngine:
     # ------------------------------------------------------------------ atoms
     def _apply_atom(self, a: dict, b: RecordBatch, state) -> RecordBatch:
         t = a["type"]
-        comp = state.comps.get(a["comp"])
+        comp = state.comps.get(a.get("comp"))
         if t == "APPLY":
             args = a["input"]["atts"]
             carry = a["projection"]["atts"]
@@ -524,6 +529,18 @@ class QueryEngine:
             return RecordBatch(cols, len(flat))
         if t == "JOIN":
             return self._probe(a, b, state)
+        if t == "FUSED_FILTER":
+            from . import pipeline as PL
+
+            r = PL.run_filter(a["plan"], b)
+            if r is not None:
+                self.pipeline_stats["fused_filters"] = self.pipeline_stats.get("fused_filters", 0) + 1
+                return r
+            for o in a["atoms"]:
+                if b.n == 0:
+                    break
+                b = self._apply_atom(o, b, state)
+            return b
         raise ValueError(f"atom {t} is not streaming")
 
     def _probe(self, a, b: RecordBatch, state) -> RecordBatch:

@@ -725,6 +725,19 @@ def _col_values(c: dict) -> torch.Tensor:
 def interpret(prog: Program, n: int, op: str):
     """The program evaluated with whole-column torch ops (same semantics as pipeline.hip; the CPU check of the
     compiler). Returns the merged (keys, values)."""
+    regs = _run_program(prog, n)
+    f = lambda t: t.view(torch.float64)  # noqa: E731
+    keep = torch.ones(n, dtype=torch.bool) if prog.keep_reg < 0 else regs[prog.keep_reg] != 0
+    key = torch.zeros(n, dtype=torch.int64) if prog.key_reg < 0 else regs[prog.key_reg]
+    vals = torch.stack([f(regs[r]) for r in prog.val_regs], 1) if prog.val_regs else torch.zeros(n, 0, dtype=torch.float64)
+    idx = keep.nonzero().flatten()
+    if torch.unique(key[idx]).numel() > INTERP_CAP:
+        return None
+    return _merge(key[idx], vals[idx], op)
+
+
+def _run_program(prog: Program, n: int) -> List[Optional[torch.Tensor]]:
+    """Every instruction of the program over whole columns: the final register values."""
     regs: List[Optional[torch.Tensor]] = [None] * NREG
     for i, c in enumerate(prog.cols):
         regs[i] = _col_values(c)
@@ -780,15 +793,102 @@ def interpret(prog: Program, n: int, op: str):
                 z = torch.zeros(n, dtype=torch.int64)
             regs[d] = z
 
-    run(0, prog.nins_a)
-    keep = torch.ones(n, dtype=torch.bool) if prog.keep_reg < 0 else regs[prog.keep_reg] != 0
-    run(prog.nins_a, len(prog.ins))
-    key = torch.zeros(n, dtype=torch.int64) if prog.key_reg < 0 else regs[prog.key_reg]
-    vals = torch.stack([f(regs[r]) for r in prog.val_regs], 1) if prog.val_regs else torch.zeros(n, 0, dtype=torch.float64)
-    idx = keep.nonzero().flatten()
-    if torch.unique(key[idx]).numel() > INTERP_CAP:
+    run(0, len(prog.ins))
+    return regs
+
+
+# ---------------------------------------------------------------------------------------------- fused FILTER
+class FilterPlan(StagePlan):
+    """A run of lambda-tree APPLY atoms ending in their FILTER: the predicate as one mask launch (pipe_mask)."""
+
+    def __init__(self, atoms, conj: E, proj: List[str]):
+        super().__init__([], atoms, [conj], E("const", (), 0), E("vals", ()), "sum", "", "")
+        self.proj = proj
+
+
+def fuse_filters(ops: List[dict], comps: dict) -> List[dict]:
+    """``ops`` with every maximal run [lambda-tree APPLYs..., FILTER] whose FILTER keeps only columns that existed
+    before the run replaced by one FUSED_FILTER op (its atoms kept for the eager fallback)."""
+    out, i = [], 0
+    while i < len(ops):
+        o = ops[i]
+        if o["type"] != "FILTER":
+            out.append(o)
+            i += 1
+            continue
+        j = len(out)                                    # walk back over the fusable APPLYs just before it
+        while j > 0 and out[j - 1]["type"] == "APPLY" and not out[j - 1]["lambda"].startswith("self_") and \
+                _apply_fusable(out[j - 1], comps):
+            j -= 1
+        run = out[j:]
+        fp = _filter_plan(run, o, comps) if run else None
+        if fp is None:
+            out.append(o)
+        else:
+            del out[j:]
+            out.append({"type": "FUSED_FILTER", "plan": fp, "atoms": run + [o]})
+        i += 1
+    return out
+
+
+def _apply_fusable(o, comps) -> bool:
+    node = comps[o["comp"]].extract_lambdas().get(o["lambda"])
+    if node is None:
+        return False
+    try:
+        _node_expr(node, [E("src", (), a) for a in o["input"]["atts"]])
+    except Unfusable:
+        return False
+    return True
+
+
+def _filter_plan(run, filt, comps) -> Optional[FilterPlan]:
+    env: Dict[str, E] = {}
+    col = lambda name: env[name] if name in env else E("src", (), name)  # noqa: E731
+    try:
+        for o in run:
+            node = comps[o["comp"]].extract_lambdas()[o["lambda"]]
+            env[o["output"]["atts"][-1]] = _node_expr(node, [col(a) for a in o["input"]["atts"]])
+    except (Unfusable, KeyError):
         return None
-    return _merge(key[idx], vals[idx], op)
+    conj = col(filt["input"]["atts"][0])
+    proj = list(filt["projection"]["atts"])
+    if conj.kind == "src" or any(c in env for c in proj):
+        return None
+    return FilterPlan(run + [filt], conj, proj)
 
 
-__all__ = ["plan_stage", "run_batch", "StagePlan", "Unfusable", "interpret"]
+def run_filter(plan: FilterPlan, batch: RecordBatch) -> Optional[RecordBatch]:
+    """The FILTER's output (its projection columns, the kept rows) from one mask launch, or None (eager atoms)."""
+    if plan.disabled or batch.n == 0:
+        return None
+    dev = batch.device
+    on_gpu = dev.type == "cuda" and _ext.hip() is not None and hasattr(_ext.hip(), "pipe_mask")
+    if not on_gpu and not (CPU_INTERPRETER and dev.type == "cpu"):
+        return None
+    try:
+        prog = _Compiler(plan, batch).compile()
+    except Unfusable as e:
+        plan.disabled = True
+        plan.reason = str(e)
+        return None
+    if on_gpu:
+        ins = torch.tensor(prog.ins, dtype=torch.int64).reshape(-1, 5)
+        lit = torch.frombuffer(bytearray(prog.lit or b"\0"), dtype=torch.uint8).to(dev, non_blocking=True)
+        mask = _ext.hip().pipe_mask(ins, _col_args(prog, dev), lit, batch.n, prog.keep_reg).bool()
+    else:
+        mask = interpret_mask(prog, batch.n)
+    plan.stats["fused_batches"] += 1
+    idx = torch.nonzero(mask, as_tuple=False).flatten()
+    keep = RecordBatch({c: batch.columns[c] for c in plan.proj}, batch.n)
+    return keep.take(idx)
+
+
+def interpret_mask(prog: Program, n: int) -> torch.Tensor:
+    """The predicate program's keep flags with the torch interpreter (CPU check of the compiler)."""
+    regs = _run_program(prog, n)
+    return torch.ones(n, dtype=torch.bool) if prog.keep_reg < 0 else regs[prog.keep_reg] != 0
+
+
+__all__ = ["plan_stage", "run_batch", "StagePlan", "Unfusable", "interpret", "fuse_filters", "run_filter",
+           "FilterPlan"]

@@ -516,9 +516,9 @@ def _pick(prefix_cols):
 def q03(client, db: str, segment: str = "BUILDING", date: int = 19950315, k: int = 10) -> List[dict]:
     """Shipping priority (Query03.h): customer ⋈ orders ⋈ lineitem, revenue by (orderkey, orderdate,
     shippriority), top-10 by revenue."""
-    cs = _Filter(lambda b: _isin_str(_col(b, "c_mktsegment"), [segment], _dev(b))).set_input(ScanSet(db, "customer", Customer))
-    os_ = _Filter(lambda b: _col(b, "o_orderdate") < date).set_input(ScanSet(db, "orders", Order))
-    ls = _Filter(lambda b: _col(b, "l_shipdate") > date).set_input(ScanSet(db, "lineitem", LineItem))
+    cs = _TreeFilter(lambda x: x.c_mktsegment == segment).set_input(ScanSet(db, "customer", Customer))
+    os_ = _TreeFilter(lambda x: x.o_orderdate < date).set_input(ScanSet(db, "orders", Order))
+    ls = _TreeFilter(lambda x: x.l_shipdate > date).set_input(ScanSet(db, "lineitem", LineItem))
     j = _EqJoin(3, [(0, "c_custkey", 1, "o_custkey"), (1, "o_orderkey", 2, "l_orderkey")],
                 _pick([[], ["o_orderdate", "o_shippriority"], ["l_orderkey", "l_extendedprice", "l_discount"]]))
     j.set_input(0, cs)
@@ -542,12 +542,11 @@ def q03(client, db: str, segment: str = "BUILDING", date: int = 19950315, k: int
 def q04(client, db: str, date: int = 19930701) -> List[dict]:
     """Order priority checking (Query04.h): orders in [date, date+3mo) having a late lineitem."""
     end = date + 300 if date % 10000 < 1000 else date + 10000 - 900   # +3 months on yyyymmdd
-    late = _Filter(lambda b: _col(b, "l_commitdate") < _col(b, "l_receiptdate")).set_input(ScanSet(db, "lineitem", LineItem))
+    late = _TreeFilter(lambda x: x.l_commitdate < x.l_receiptdate).set_input(ScanSet(db, "lineitem", LineItem))
     # EXISTS -> distinct late orderkeys (aggregate), then join with the orders of the quarter
     dist = _GroupBy(lambda b: _col(b, "l_orderkey"), lambda b: torch.ones(b.n, 1, dtype=torch.float64, device=_dev(b)),
                     _rows_out(["n"]))
-    os_ = _Filter(lambda b: (_col(b, "o_orderdate") >= date) & (_col(b, "o_orderdate") < end)).set_input(
-        ScanSet(db, "orders", Order))
+    os_ = _TreeFilter(lambda x: (x.o_orderdate >= date) & (x.o_orderdate < end)).set_input(ScanSet(db, "orders", Order))
     j = _EqJoin(2, [(0, "o_orderkey", 1, "k0")], _pick([["o_orderpriority"], []]))
     j.set_input(0, os_)
     j.set_input(1, dist.set_input(late))
@@ -577,11 +576,11 @@ def q06(client, db: str, date: int = 19940101, discount: float = 0.06, quantity:
 def q12(client, db: str, modes=("MAIL", "SHIP"), date: int = 19940101) -> List[dict]:
     """Shipping modes and order priority (Query12.h): lineitem ⋈ orders, high/low priority counts."""
 
-    def pred(b):
-        c, r, s = _col(b, "l_commitdate"), _col(b, "l_receiptdate"), _col(b, "l_shipdate")
-        return _isin_str(_col(b, "l_shipmode"), modes, _dev(b)) & (c < r) & (s < c) & (r >= date) & (r < date + 10000)
+    def pred(x):
+        c, r, s = x.l_commitdate, x.l_receiptdate, x.l_shipdate
+        return IsIn(x.l_shipmode, list(modes)) & (c < r) & (s < c) & (r >= date) & (r < date + 10000)
 
-    ls = _Filter(pred).set_input(ScanSet(db, "lineitem", LineItem))
+    ls = _TreeFilter(pred).set_input(ScanSet(db, "lineitem", LineItem))
     j = _EqJoin(2, [(0, "o_orderkey", 1, "l_orderkey")], _pick([["o_orderpriority"], ["l_shipmode"]]))
     j.set_input(0, ScanSet(db, "orders", Order))
     j.set_input(1, ls)
@@ -625,8 +624,7 @@ def _count(client, db: str, name: str) -> int:
 def q14(client, db: str, date: int = 19950901) -> float:
     """Promotion effect (Query14.h): lineitem ⋈ part, 100 * promo revenue / revenue."""
     end = date + 100 if date % 10000 < 1201 else date + 10000 - 1100
-    ls = _Filter(lambda b: (_col(b, "l_shipdate") >= date) & (_col(b, "l_shipdate") < end)).set_input(
-        ScanSet(db, "lineitem", LineItem))
+    ls = _TreeFilter(lambda x: (x.l_shipdate >= date) & (x.l_shipdate < end)).set_input(ScanSet(db, "lineitem", LineItem))
     j = _EqJoin(2, [(0, "l_partkey", 1, "p_partkey")], _pick([["l_extendedprice", "l_discount"], ["p_type"]]))
     j.set_input(0, ls)
     j.set_input(1, ScanSet(db, "part", Part))
@@ -645,8 +643,7 @@ def q14(client, db: str, date: int = 19950901) -> float:
 def q17(client, db: str, brand: str = "Brand#23", container: str = "MED BOX") -> float:
     """Small-quantity-order revenue (Query17.h): per-part average quantity, then lineitems of the
     brand/container parts under 0.2 x that average; sum(extendedprice) / 7."""
-    ps = _Filter(lambda b: _isin_str(_col(b, "p_brand"), [brand], _dev(b)) &
-                 _isin_str(_col(b, "p_container"), [container], _dev(b))).set_input(ScanSet(db, "part", Part))
+    ps = _TreeFilter(lambda x: (x.p_brand == brand) & (x.p_container == container)).set_input(ScanSet(db, "part", Part))
     j = _EqJoin(2, [(0, "l_partkey", 1, "p_partkey")], _pick([["l_partkey", "l_quantity", "l_extendedprice"], []]))
     j.set_input(0, ScanSet(db, "lineitem", LineItem))
     j.set_input(1, ps)

@@ -15,6 +15,7 @@ from netsdb_amd.lambdas import IsIn, KeyTuple, Like, Literal, Select, Values, ma
 from netsdb_amd.models import tpch, tpch_gen
 
 QUERIES = ("q01", "q06", "q12", "q14")
+FILTER_QUERIES = ("q03", "q04", "q17")      # tree-lambda FILTERs feeding joins: fused mask launches
 
 
 def _close(a, b):
@@ -31,8 +32,8 @@ def _ref(q, t, f):
     ref = tpch.reference(q, t, f=f)
     if q == "q01":
         ref = sorted(ref, key=lambda x: (x["l_returnflag"], x["l_linestatus"]))
-    elif q == "q12":
-        ref = sorted(ref, key=lambda x: x["l_shipmode"])
+    elif q in ("q04", "q12"):
+        ref = sorted(ref, key=lambda x: x[list(x)[0]])
     return ref
 
 
@@ -48,11 +49,12 @@ def test_fused_tpch_cpu_interpreter(monkeypatch):
     t = tpch_gen.generate_fast(0.003, seed=4)
     f = tpch.frames(t)
     c = _client("cpu", t)
-    for q in QUERIES:
+    for q in QUERIES + FILTER_QUERIES:
         got = tpch.QUERIES[q](c, "tpch")
         assert _close(got, _ref(q, t, f)), (q, got)
     st = c.engine.pipeline_stats
     assert st["fused_stages"] >= len(QUERIES) and st["fallback_batches"] == 0, st
+    assert st.get("fused_filters", 0) >= 5, st
 
 
 class _Sel(SelectionComp):
@@ -146,7 +148,7 @@ def test_fused_tpch_gpu_vs_eager_and_pandas():
     t = tpch_gen.generate_fast(0.05, seed=4)
     f = tpch.frames(t)
     c = _client("cuda:0", t)
-    for q in QUERIES:
+    for q in QUERIES + FILTER_QUERIES:
         c.engine.fused_pipelines = True
         got = tpch.QUERIES[q](c, "tpch")
         c.engine.fused_pipelines = False
