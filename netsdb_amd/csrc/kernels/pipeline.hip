@@ -16,16 +16,22 @@
 //  * Columns are loaded straight into their registers: registers [0, ncol) hold the loaded columns. "Late" columns
 //    (read only by the key / value row) are loaded after the predicate, for the kept rows only (a wave skips the
 //    cache lines none of its kept rows needs).
-//  * Aggregation: each thread keeps KSLOT (key, count, F values) slots in registers (few groups hit them every
-//    row); a row whose key is in no slot goes to the workgroup's LDS hash table (CAP slots, 64-bit CAS + LDS float
-//    atomics). At the end the slots are flushed into the LDS table, and the workgroup writes its occupied entries
-//    (compacted) to a per-workgroup partial; the host merges the partials (a few thousand rows). A workgroup whose
-//    table overflows raises status[0]: the stage then runs the unfused path (more groups than this kernel is for).
+//  * Column loads are unrolled over the MAXCOL column slots (compile-time register numbers): every row load of a pass
+//    is issued before the first one is used (the 2nd round only fetches the bytes of short-string columns), so a
+//    wave keeps all its columns' cache lines in flight instead of one column at a time.
+//  * Aggregation: each thread keeps KSLOT (key, F values) slots in registers (few groups hit them every row); a row
+//    whose key is in no slot goes to the workgroup's LDS hash table (CAP slots, 64-bit CAS + LDS float atomics). At
+//    the end every wave reduces its lanes' slots per distinct key (cross-lane butterflies, one LDS update per key per
+//    wave), and the workgroup merges its table into ONE global table of GCAP slots with device atomics: the host
+//    reads back a few KB, no per-workgroup partials and no second merge pass. A table overflow raises status[0]:
+//    the stage then runs the unfused path (more groups than this kernel is for). status[1] counts the kept rows
+//    (the host's selectivity estimate decides whether value columns load late, after the predicate).
 #include "common.h"
 
 namespace nsdb_pipe {
 
 constexpr int NREG = 16, ROWS = 2, MAXINS = 48, MAXCOL = 10, FMAX = 8, KSLOT = 4, CAP = 256, NTHR = 256;
+constexpr int GCAP = 2048;             // global table slots (power of two)
 constexpr long long EMPTY = (long long)0x8000000000000000ULL;
 constexpr int IMM_REG = -2;            // operand register meaning "the instruction's immediate"
 
@@ -54,11 +60,7 @@ struct PipeArgs {
   long long n;
   int nins_a, nins, ncol, keep_reg, key_reg, nval, agg_op, pad;
   int val_reg[FMAX];
-  long long* out_key;            // [nwg][CAP]
-  unsigned long long* out_cnt;   // [nwg][CAP]
-  double* out_val;               // [nwg][CAP][FMAX]
-  int* out_occ;                  // [nwg]
-  int* status;                   // [0] overflow
+  unsigned long long* table;     // [2 + GCAP + GCAP * FMAX]: status (overflow, kept rows), keys, values (f64 bits)
 };
 
 typedef unsigned long long u64;
@@ -77,31 +79,52 @@ __device__ __forceinline__ u64 short_code(const unsigned char* d, long long s, l
   return (c << 3) | (u64)len;
 }
 
-// Column c into register c of every row slot (masked: rows not in `m` load nothing).
-__device__ __forceinline__ void load_col(const Col& c, int reg, const long long (&row)[ROWS], const bool (&m)[ROWS],
-                                         regfile (&R)[ROWS]) {
-  u64 x[ROWS];
+// Pass 1 of a column's load: the row's value (numeric kinds) or its string start (x) and the low word of its end (y).
+__device__ __forceinline__ void fetch(const Col& c, const long long (&row)[ROWS], const bool (&m)[ROWS], u64 (&x)[ROWS],
+                                      unsigned (&y)[ROWS]) {
 #pragma unroll
   for (int j = 0; j < ROWS; ++j) {
     x[j] = 0;
+    y[j] = 0;
     if (m[j]) {
       const long long i = row[j];
       switch (c.kind) {
-        case C_F64: x[j] = reinterpret_cast<const u64*>(c.p)[i]; break;
+        case C_F64:
         case C_I64: x[j] = reinterpret_cast<const u64*>(c.p)[i]; break;
         case C_I32: x[j] = (u64)(long long)reinterpret_cast<const int*>(c.p)[i]; break;
         case C_F32: x[j] = f2u((double)reinterpret_cast<const float*>(c.p)[i]); break;
         case C_U8: x[j] = (u64)reinterpret_cast<const unsigned char*>(c.p)[i]; break;
-        case C_SCODE: x[j] = short_code(c.dat, c.st[i], c.en[i], c.L); break;
-        default: {                          // C_SREF: (start << 24) | length
-          const long long s = c.st[i], e = c.en[i];
-          x[j] = ((u64)s << 24) | (u64)min(e - s, (long long)0xFFFFFF);
-        }
+        default:
+          x[j] = (u64)c.st[i];
+          y[j] = (unsigned)c.en[i];
       }
     }
   }
+}
+
+// Pass 2: the register value (string kinds: the short code from the bytes / the (start << 24 | length) reference;
+// lengths fit 32 bits, so the end's low word suffices).
+__device__ __forceinline__ u64 finish(const Col& c, u64 x, unsigned y, bool m) {
+  if (c.kind == C_SCODE) return m ? short_code(c.dat, (long long)x, (long long)x + (long long)(unsigned)(y - (unsigned)x), c.L) : 0;
+  if (c.kind == C_SREF) return (x << 24) | (u64)min(y - (unsigned)x, 0xFFFFFFu);
+  return x;
+}
+
+// Every column of the pass (LATE: the late columns; else the early ones) into its register, all loads in flight at once.
+template <bool LATE>
+__device__ __forceinline__ void load_cols(const PipeArgs& a, const long long (&row)[ROWS], const bool (&m)[ROWS],
+                                          regfile (&R)[ROWS]) {
+  u64 x[MAXCOL][ROWS];
+  unsigned y[MAXCOL][ROWS];
 #pragma unroll
-  for (int j = 0; j < ROWS; ++j) R[j][reg] = x[j];
+  for (int c = 0; c < MAXCOL; ++c)
+    if (c < a.ncol && (a.col[c].late != 0) == LATE) fetch(a.col[c], row, m, x[c], y[c]);
+#pragma unroll
+  for (int c = 0; c < MAXCOL; ++c)
+    if (c < a.ncol && (a.col[c].late != 0) == LATE) {
+#pragma unroll
+      for (int j = 0; j < ROWS; ++j) R[j][c] = finish(a.col[c], x[c][j], y[c][j], m[j]);
+    }
 }
 
 __device__ __forceinline__ bool str_match(const unsigned char* d, u64 ref, const unsigned char* lit, long long imm,
@@ -193,66 +216,66 @@ __device__ __forceinline__ unsigned slot_hash(long long k) {
   return (unsigned)(z >> 40);
 }
 
-__device__ __forceinline__ void lds_acc(double* p, double v, int op) {
+__device__ __forceinline__ double acc_op(double a, double b, int op) {
+  return op == 0 ? a + b : (op == 1 ? fmin(a, b) : fmax(a, b));
+}
+
+// *p = op(*p, v) atomically (LDS or global: the pointer's address space is known after inlining). Sums use the
+// hardware f64 add atomic, min / max a 64-bit CAS loop.
+__device__ __forceinline__ void atomic_acc(double* p, double v, int op) {
   if (op == 0) {
     atomicAdd(p, v);
     return;
   }
-  unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
-  unsigned long long old = *q;
+  u64* q = reinterpret_cast<u64*>(p);
+  u64 old = *q;
   while (true) {
-    const double cur = __longlong_as_double((long long)old);
-    const double nv = op == 1 ? fmin(cur, v) : fmax(cur, v);
+    const double cur = u2f(old);
+    const double nv = acc_op(cur, v, op);
     if (nv == cur) return;
-    const unsigned long long got = atomicCAS(q, old, (unsigned long long)__double_as_longlong(nv));
+    const u64 got = atomicCAS(q, old, f2u(nv));
     if (got == old) return;
     old = got;
   }
 }
 
+// Linear-probing insert of (key, values) into a table of cap slots (LDS or global). False: the table is full.
 template <int F>
-__device__ __forceinline__ void lds_insert(long long* tk, unsigned long long* tc, double* tv, int* ovf, long long key,
-                                           unsigned long long cnt, const double (&v)[F], int nval, int op) {
-  if (key == EMPTY) {
-    *ovf = 1;
-    return;
-  }
-  unsigned h = slot_hash(key) & (CAP - 1);
-  for (int p = 0; p < CAP; ++p) {
-    const long long prev = (long long)atomicCAS(reinterpret_cast<unsigned long long*>(tk + h), (unsigned long long)EMPTY,
-                                                (unsigned long long)key);
+__device__ __forceinline__ bool table_insert(long long* tk, double* tv, unsigned cap, long long key, const double (&v)[F],
+                                             int nval, int op) {
+  unsigned h = slot_hash(key) & (cap - 1);
+  for (unsigned p = 0; p < cap; ++p) {
+    const long long prev = (long long)atomicCAS(reinterpret_cast<u64*>(tk + h), (u64)EMPTY, (u64)key);
     if (prev == EMPTY || prev == key) {
-      atomicAdd(tc + h, cnt);
 #pragma unroll
       for (int f = 0; f < F; ++f)
-        if (f < nval) lds_acc(tv + h * FMAX + f, v[f], op);
-      return;
+        if (f < nval) atomic_acc(tv + (size_t)h * FMAX + f, v[f], op);
+      return true;
     }
-    h = (h + 1) & (CAP - 1);
+    h = (h + 1) & (cap - 1);
   }
-  *ovf = 1;
+  return false;
 }
 
-__device__ __forceinline__ double acc_op(double a, double b, int op) {
-  return op == 0 ? a + b : (op == 1 ? fmin(a, b) : fmax(a, b));
+__device__ __forceinline__ double wave_reduce(double v, int op) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = acc_op(v, __shfl_xor(v, o), op);
+  return v;
 }
 
 template <int F>
 __global__ void __launch_bounds__(NTHR) pipe_agg_kernel(const PipeArgs a) {
   __shared__ long long tk[CAP];
-  __shared__ unsigned long long tc[CAP];
   __shared__ double tv[CAP * FMAX];
-  __shared__ int s_ovf, s_occ;
-  const int tid = threadIdx.x;
+  __shared__ int s_ovf;
+  __shared__ unsigned long long s_kept;
+  const int tid = threadIdx.x, lane = tid & 63;
   const double init = a.agg_op == 0 ? 0.0 : (a.agg_op == 1 ? __builtin_inf() : -__builtin_inf());
-  for (int i = tid; i < CAP; i += NTHR) {
-    tk[i] = EMPTY;
-    tc[i] = 0;
-  }
+  for (int i = tid; i < CAP; i += NTHR) tk[i] = EMPTY;
   for (int i = tid; i < CAP * FMAX; i += NTHR) tv[i] = init;
   if (tid == 0) {
     s_ovf = 0;
-    s_occ = 0;
+    s_kept = 0;
   }
   __syncthreads();
 
@@ -260,13 +283,13 @@ __global__ void __launch_bounds__(NTHR) pipe_agg_kernel(const PipeArgs a) {
 #pragma unroll
   for (int j = 0; j < ROWS; ++j) R[j] = (regfile)0;
   long long sk[KSLOT];
-  unsigned long long sc[KSLOT];
   double sv[KSLOT][F];
   int used = 0;
+  unsigned kept = 0;
+  bool ovf = false;
 #pragma unroll
   for (int s = 0; s < KSLOT; ++s) {
     sk[s] = EMPTY;
-    sc[s] = 0;
 #pragma unroll
     for (int f = 0; f < F; ++f) sv[s][f] = init;
   }
@@ -280,20 +303,17 @@ __global__ void __launch_bounds__(NTHR) pipe_agg_kernel(const PipeArgs a) {
       row[j] = base + (long long)j * NTHR + tid;
       inr[j] = row[j] < a.n;
     }
-    // the predicate's ("early") columns, every load issued before any is used, then the predicate program
-    for (int c = 0; c < a.ncol; ++c)
-      if (!a.col[c].late) load_col(a.col[c], c, row, inr, R);
+    load_cols<false>(a, row, inr, R);                          // the predicate's ("early") columns
     run(a, R, 0, a.nins_a);
     bool any = false;
 #pragma unroll
     for (int j = 0; j < ROWS; ++j) {
       keep[j] = inr[j] && (a.keep_reg < 0 || R[j][a.keep_reg] != 0);
       any |= keep[j];
+      kept += keep[j] ? 1u : 0u;
     }
     if (!__builtin_amdgcn_ballot_w64(any)) continue;           // no kept row in this wave
-    // late columns for the kept rows only, then the key / value program
-    for (int c = 0; c < a.ncol; ++c)
-      if (a.col[c].late) load_col(a.col[c], c, row, keep, R);
+    load_cols<true>(a, row, keep, R);                          // late columns: the kept rows only
     run(a, R, a.nins_a, a.nins);
 #pragma unroll
     for (int j = 0; j < ROWS; ++j) {
@@ -308,7 +328,6 @@ __global__ void __launch_bounds__(NTHR) pipe_agg_kernel(const PipeArgs a) {
         if (!done && s < used && sk[s] == key) {
 #pragma unroll
           for (int f = 0; f < F; ++f) sv[s][f] = acc_op(sv[s][f], v[f], a.agg_op);
-          sc[s] += 1;
           done = true;
         }
       }
@@ -317,7 +336,6 @@ __global__ void __launch_bounds__(NTHR) pipe_agg_kernel(const PipeArgs a) {
         for (int s = 0; s < KSLOT; ++s) {
           if (!done && s == used) {
             sk[s] = key;
-            sc[s] = 1;
 #pragma unroll
             for (int f = 0; f < F; ++f) sv[s][f] = v[f];
             done = true;
@@ -325,30 +343,55 @@ __global__ void __launch_bounds__(NTHR) pipe_agg_kernel(const PipeArgs a) {
         }
         ++used;
       }
-      if (!done) lds_insert<F>(tk, tc, tv, &s_ovf, key, 1, v, a.nval, a.agg_op);
+      if (!done) ovf |= (key == EMPTY) || !table_insert<F>(tk, tv, CAP, key, v, a.nval, a.agg_op);
     }
   }
-  // flush the register slots
+  // flush the register slots: per slot, the wave's lanes holding the leader's key are reduced across lanes and the
+  // leader lane makes the one LDS update for that key (no 64-way atomic contention on a few hot entries)
 #pragma unroll
-  for (int s = 0; s < KSLOT; ++s)
-    if (s < used) lds_insert<F>(tk, tc, tv, &s_ovf, sk[s], sc[s], sv[s], a.nval, a.agg_op);
+  for (int s = 0; s < KSLOT; ++s) {
+    bool act = s < used;
+    while (true) {
+      const u64 bal = __builtin_amdgcn_ballot_w64(act);
+      if (!bal) break;
+      const int leader = __builtin_ctzll(bal);
+      const long long kl = __shfl(sk[s], leader);
+      const bool mine = act && sk[s] == kl;
+      double v[F];
+#pragma unroll
+      for (int f = 0; f < F; ++f) v[f] = wave_reduce(mine ? sv[s][f] : init, a.agg_op);
+      if (lane == leader) ovf |= (kl == EMPTY) || !table_insert<F>(tk, tv, CAP, kl, v, a.nval, a.agg_op);
+      act = act && !mine;
+    }
+  }
+  atomicAdd(&s_kept, (unsigned long long)kept);
+  if (ovf) s_ovf = 1;
   __syncthreads();
-  // occupied entries, compacted, to this workgroup's partial
-  const long long wg = blockIdx.x;
+  // the workgroup's table into the global one
+  long long* gk = reinterpret_cast<long long*>(a.table + 2);
+  double* gv = reinterpret_cast<double*>(a.table + 2 + GCAP);
   for (int i = tid; i < CAP; i += NTHR) {
-    if (tk[i] == EMPTY) continue;
-    const int pos = atomicAdd(&s_occ, 1);
-    const long long o = wg * CAP + pos;
-    a.out_key[o] = tk[i];
-    a.out_cnt[o] = tc[i];
+    const long long k = tk[i];
+    if (k == EMPTY) continue;
+    double v[F];
 #pragma unroll
-    for (int f = 0; f < FMAX; ++f) a.out_val[o * FMAX + f] = tv[i * FMAX + f];
+    for (int f = 0; f < F; ++f) v[f] = tv[i * FMAX + f];
+    if (!table_insert<F>(gk, gv, GCAP, k, v, a.nval, a.agg_op)) s_ovf = 1;
   }
   __syncthreads();
   if (tid == 0) {
-    a.out_occ[wg] = s_occ;
-    if (s_ovf) atomicOr(a.status, 1);
+    if (s_ovf) atomicOr(a.table, 1ull);
+    atomicAdd(a.table + 1, s_kept);
   }
+}
+
+// The global table's initial state (status 0, keys EMPTY, values the aggregation's identity), one launch.
+__global__ void __launch_bounds__(NTHR) pipe_init_kernel(unsigned long long* table, int op) {
+  const double init = op == 0 ? 0.0 : (op == 1 ? __builtin_inf() : -__builtin_inf());
+  const int i = blockIdx.x * NTHR + threadIdx.x;
+  if (i < 2) table[i] = 0;
+  if (i < GCAP) table[2 + i] = (u64)EMPTY;
+  for (int k = i; k < GCAP * FMAX; k += gridDim.x * NTHR) table[2 + GCAP + k] = f2u(init);
 }
 
 // Filter only: the predicate program over every row, the keep flag written as one byte per row (the FILTER of a
@@ -368,7 +411,7 @@ __global__ void __launch_bounds__(NTHR) pipe_mask_kernel(const PipeArgs a, unsig
       row[j] = base + (long long)j * NTHR + tid;
       inr[j] = row[j] < a.n;
     }
-    for (int c = 0; c < a.ncol; ++c) load_col(a.col[c], c, row, inr, R);
+    load_cols<false>(a, row, inr, R);
     run(a, R, 0, a.nins);
 #pragma unroll
     for (int j = 0; j < ROWS; ++j)
@@ -389,17 +432,26 @@ int nsdb_pipe_sizes(int* out) {
   out[5] = (int)sizeof(nsdb_pipe::PipeArgs);
   out[6] = nsdb_pipe::ROWS;
   out[7] = nsdb_pipe::NTHR;
+  out[8] = nsdb_pipe::GCAP;
   return 0;
 }
 
-// args: a host PipeArgs image (the binding fills it field by field); grid = number of workgroups.
+// args: a host PipeArgs image (the binding fills it field by field, the mask pass marks every column early);
+// grid = number of workgroups. Initialises the global table, then the fused pass.
 int nsdb_pipe_agg(const void* args, int grid, hipStream_t st) {
   if (grid <= 0) return -1;
   const nsdb_pipe::PipeArgs& a = *reinterpret_cast<const nsdb_pipe::PipeArgs*>(args);
-  if (a.nins > nsdb_pipe::MAXINS || a.ncol > nsdb_pipe::MAXCOL || a.nval > nsdb_pipe::FMAX || a.nins_a > a.nins)
+  if (a.nins > nsdb_pipe::MAXINS || a.ncol > nsdb_pipe::MAXCOL || a.nval > nsdb_pipe::FMAX || a.nins_a > a.nins ||
+      a.table == nullptr)
     return -2;
+  hipLaunchKernelGGL(nsdb_pipe::pipe_init_kernel, dim3(nsdb_pipe::GCAP / nsdb_pipe::NTHR), dim3(nsdb_pipe::NTHR), 0, st,
+                     a.table, a.agg_op);
   if (a.nval <= 2)
     hipLaunchKernelGGL(nsdb_pipe::pipe_agg_kernel<2>, dim3(grid), dim3(nsdb_pipe::NTHR), 0, st, a);
+  else if (a.nval <= 4)
+    hipLaunchKernelGGL(nsdb_pipe::pipe_agg_kernel<4>, dim3(grid), dim3(nsdb_pipe::NTHR), 0, st, a);
+  else if (a.nval <= 6)
+    hipLaunchKernelGGL(nsdb_pipe::pipe_agg_kernel<6>, dim3(grid), dim3(nsdb_pipe::NTHR), 0, st, a);
   else
     hipLaunchKernelGGL(nsdb_pipe::pipe_agg_kernel<nsdb_pipe::FMAX>, dim3(grid), dim3(nsdb_pipe::NTHR), 0, st, a);
   return (int)hipGetLastError();

@@ -39,18 +39,14 @@ struct PipeArgs {
   long long n;
   int nins_a, nins, ncol, keep_reg, key_reg, nval, agg_op, pad;
   int val_reg[FMAX];
-  long long* out_key;
-  unsigned long long* out_cnt;
-  double* out_val;
-  int* out_occ;
-  int* status;
+  unsigned long long* table;
 };
 
 enum ColKind : int { C_F64 = 0, C_I64, C_I32, C_F32, C_U8, C_SCODE, C_SREF };
 enum : int { OP_SEQ = 26, OP_SPRE = 27, OP_SSUF = 28, OP_SEL = 29, OP_LAST = 30 };
 
 int sizes(int i) {
-  static int s[8] = {0};
+  static int s[9] = {0};
   static bool init = false;
   if (!init) {
     nsdb_pipe_sizes(s);
@@ -73,7 +69,8 @@ typedef std::vector<std::tuple<int64_t, int64_t, int64_t, c10::optional<torch::T
 // Validate the program / columns / registers and fill the kernel's argument image.
 void fill_args(PipeArgs& a, const torch::Tensor& prog, int64_t nins_a, const ColList& cols, const torch::Tensor& lit,
                int64_t n, int64_t keep_reg, int64_t key_reg, const std::vector<int64_t>& val_regs, int64_t agg_op) {
-  TORCH_CHECK(sizes(0) == MAXINS && sizes(1) == MAXCOL && sizes(3) == FMAX && sizes(5) == (int)sizeof(PipeArgs),
+  TORCH_CHECK(sizes(0) == MAXINS && sizes(1) == MAXCOL && sizes(3) == FMAX && sizes(5) == (int)sizeof(PipeArgs) &&
+                  sizes(8) > 0 && (sizes(8) & (sizes(8) - 1)) == 0,
               "pipe_agg: host / kernel argument layout mismatch");
   const int NREG = sizes(2);
   TORCH_CHECK(prog.device().is_cpu() && prog.scalar_type() == torch::kInt64 && prog.dim() == 2 && prog.size(1) == 5,
@@ -150,31 +147,21 @@ void fill_args(PipeArgs& a, const torch::Tensor& prog, int64_t nins_a, const Col
   a.agg_op = (int)agg_op;
 }
 
-std::vector<torch::Tensor> pipe_agg(torch::Tensor prog, int64_t nins_a, ColList cols, torch::Tensor lit, int64_t n,
-                                    int64_t keep_reg, int64_t key_reg, std::vector<int64_t> val_regs, int64_t agg_op,
-                                    int64_t max_wg) {
-  const int CAP = sizes(4), ROWS = sizes(6), NTHR = sizes(7);
+// Returns the global result table, int64 [2 + GCAP * (1 + FMAX)]: status (overflow flag, kept rows), GCAP keys
+// (INT64_MIN = free slot), then GCAP x FMAX f64 values (bit patterns). The host reads it back in one copy.
+torch::Tensor pipe_agg(torch::Tensor prog, int64_t nins_a, ColList cols, torch::Tensor lit, int64_t n, int64_t keep_reg,
+                       int64_t key_reg, std::vector<int64_t> val_regs, int64_t agg_op, int64_t max_wg) {
+  const int ROWS = sizes(6), NTHR = sizes(7), GCAP = sizes(8);
   PipeArgs a;
   fill_args(a, prog, nins_a, cols, lit, n, keep_reg, key_reg, val_regs, agg_op);
+  // enough workgroups to fill 256 CUs several times over, each thread still looping over a few row pairs
   const long long per = (long long)NTHR * ROWS * 4;
   const int nwg = (int)std::max<long long>(1, std::min<long long>(max_wg > 0 ? max_wg : 2048, (n + per - 1) / per));
-  auto dev = lit.device();
-  auto i64 = torch::TensorOptions().dtype(torch::kInt64).device(dev);
-  auto out_key = torch::empty({(long long)nwg * CAP}, i64);
-  auto out_cnt = torch::empty({(long long)nwg * CAP}, i64);
-  auto out_val = torch::empty({(long long)nwg * CAP, FMAX}, i64.dtype(torch::kFloat64));
-  auto out_occ = torch::zeros({nwg}, i64.dtype(torch::kInt32));
-  auto status = torch::zeros({1}, i64.dtype(torch::kInt32));
-  a.out_key = reinterpret_cast<long long*>(out_key.data_ptr<int64_t>());
-  a.out_cnt = reinterpret_cast<unsigned long long*>(out_cnt.data_ptr<int64_t>());
-  a.out_val = out_val.data_ptr<double>();
-  a.out_occ = out_occ.data_ptr<int>();
-  a.status = status.data_ptr<int>();
-  if (n > 0) {
-    const int rc = nsdb_pipe_agg(&a, nwg, c10::hip::getCurrentHIPStream().stream());
-    TORCH_CHECK(rc == 0, "pipe_agg launch failed: ", rc);
-  }
-  return {out_key, out_cnt, out_val, out_occ, status};
+  auto table = torch::empty({2 + (long long)GCAP * (1 + FMAX)}, lit.options().dtype(torch::kInt64));
+  a.table = reinterpret_cast<unsigned long long*>(table.data_ptr<int64_t>());
+  const int rc = nsdb_pipe_agg(&a, nwg, c10::hip::getCurrentHIPStream().stream());
+  TORCH_CHECK(rc == 0, "pipe_agg launch failed: ", rc);
+  return table;
 }
 
 // The predicate program's keep flag per row (uint8 [n]); key / values unused.
@@ -182,6 +169,7 @@ torch::Tensor pipe_mask(torch::Tensor prog, ColList cols, torch::Tensor lit, int
   const int ROWS = sizes(6), NTHR = sizes(7);
   PipeArgs a;
   fill_args(a, prog, prog.size(0), cols, lit, n, keep_reg, -1, {}, 0);
+  for (int c = 0; c < a.ncol; ++c) a.col[c].late = 0;      // the mask pass loads every column up front
   auto mask = torch::empty({n}, lit.options().dtype(torch::kUInt8));
   if (n > 0) {
     const long long per = (long long)NTHR * ROWS * 4;
@@ -198,8 +186,8 @@ void register_pipeline(pybind11::module& m) {
   m.def("pipe_mask", &pipe_mask, "fused filter predicate (pipeline.hip): keep flag per row (uint8)",
         pybind11::arg("prog"), pybind11::arg("cols"), pybind11::arg("lit"), pybind11::arg("n"), pybind11::arg("keep_reg"));
   m.def("pipe_agg", &pipe_agg,
-        "fused scan -> filter -> project -> low-cardinality aggregate (pipeline.hip): per-workgroup partial "
-        "(keys, counts, values[.., 8], occupancy, status[overflow])",
+        "fused scan -> filter -> project -> low-cardinality aggregate (pipeline.hip): the global result table "
+        "int64 [2 + GCAP * 9] = status (overflow, kept rows), keys, f64 values [GCAP, 8]",
         pybind11::arg("prog"), pybind11::arg("nins_a"), pybind11::arg("cols"), pybind11::arg("lit"), pybind11::arg("n"),
         pybind11::arg("keep_reg"), pybind11::arg("key_reg"), pybind11::arg("val_regs"), pybind11::arg("agg_op") = 0,
         pybind11::arg("max_wg") = 0);

@@ -5,7 +5,6 @@
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
-#include <cstdlib>
 #include <limits>
 #include <string>
 #include <tuple>
@@ -109,9 +108,7 @@ std::vector<torch::Tensor> hash_aggregate(torch::Tensor keys, c10::optional<torc
   // from the sampled distinct-key estimate (relops.hip agg_bucket_kernel), so no host decision needs the data.
   const int64_t entry = 20 + 8 * F;
   const int64_t lcap_low = std::min<int64_t>(1024, pow2_at_most(65536 / entry));   // <= 36 KB: 4+ LOW workgroups per CU
-  int64_t lcap_part = std::min<int64_t>(4096, pow2_at_most(131072 / entry));
-  // test hook: a tiny PART LDS table (power of two >= 64) makes the PART overflow table fill (status ok = 0)
-  if (const char* e = std::getenv("NSDB_AGG_TEST_LCAP_PART")) lcap_part = std::max<int64_t>(64, pow2_at_most(std::atoll(e)));
+  const int64_t lcap_part = std::min<int64_t>(4096, pow2_at_most(131072 / entry));
   int pbits = 0;
   while (pbits < 8 && (n >> (pbits + 1)) >= 2048) ++pbits;
   const int64_t gcap_low = 4 * lcap_low;

@@ -11,14 +11,17 @@ column in HBM. When a stage ends in an aggregation and every atom after its last
 module understands (member access, literals, + - * /, comparisons, && || !, string ==, IN, LIKE prefix / suffix,
 CASE, and the ``Values`` / ``KeyTuple`` rows of the aggregate), the atoms are compiled into a short register
 program for the device interpreter kernel ``pipe_agg`` (csrc/kernels/pipeline.hip): one launch reads each input
-column once, evaluates the predicate, key and value row per row in registers, pre-aggregates into per-workgroup
-tables, and only the per-workgroup partials (a few thousand rows) reach the merge. A batch whose groups overflow the
-kernel's tables, or whose columns are of a kind the kernel does not read, runs the eager atoms instead.
+column once, evaluates the predicate, key and value row per row in registers, pre-aggregates in registers / LDS and
+merges every workgroup into one small global table with device atomics; the host reads that table back in ONE copy
+(the launch's only synchronisation). A batch whose groups overflow the kernel's tables, or whose columns are of a
+kind the kernel does not read, runs the eager atoms instead.
 
 Program (mirrors pipeline.hip): registers [0, ncol) hold the loaded columns (numeric: f64 / i64 / i32 / f32 / u8;
 strings: an exact short code for keys, or a (start, length) reference for byte comparisons), the temporaries follow.
 Segment A computes the keep mask from the predicate's ("early") columns; the key / value columns that only segment B
-reads are loaded for the kept rows only.
+reads are loaded for the kept rows only — when the stage's measured selectivity (the kernel counts the kept rows)
+is low enough for that to save bandwidth; a non-selective predicate loads every column in one pass instead (one
+memory round trip per row block instead of two).
 """
 from __future__ import annotations
 
@@ -50,6 +53,10 @@ _CMP = {"<": (OP_LTF, OP_LTI), "<=": (OP_LEF, OP_LEI), ">": (OP_GTF, OP_GTI), ">
 CPU_INTERPRETER = False
 # the torch interpreter's model of the kernel's per-workgroup table: more distinct kept keys than this -> overflow
 INTERP_CAP = 1 << 30
+# late (post-predicate) loads of the key / value columns only when the stage keeps fewer rows than this fraction
+LATE_MAX_SEL = 0.25
+_SEL_EST: Dict[tuple, float] = {}          # stage signature -> kept fraction measured by its last launch
+_EMPTY = -(1 << 63)                        # free slot of the kernel's global table
 
 
 class Unfusable(Exception):
@@ -104,6 +111,14 @@ class StagePlan:
         self.disabled = False
         self.reason = None
         self.stats = {"fused_batches": 0, "fallback_batches": 0}
+        self._sig = None
+
+    @property
+    def sig(self) -> tuple:
+        """The stage's expressions (stable across executions of the same query): keys the selectivity estimate."""
+        if self._sig is None:
+            self._sig = (tuple(_path(c) for c in self.conj), _path(self.key), _path(self.val), self.op)
+        return self._sig
 
 
 def plan_stage(ops: List[dict], comps: dict, sink_atom: dict) -> Optional[StagePlan]:
@@ -251,6 +266,7 @@ class _Compiler:
         self.p = Program()
         self.cse: Dict[tuple, tuple] = {}
         self.counts: Dict[tuple, int] = {}
+        self.late_ok = _SEL_EST.get(plan.sig, 0.0) < LATE_MAX_SEL
 
     def _count(self, e: E):
         if e.kind in ("bin", "sel", "not", "like", "isin"):
@@ -320,7 +336,7 @@ class _Compiler:
         for v in vals:
             self._collect(v, "num", "B", uses)
         for e, usage, seg in [u for u in uses if u[2] == "A"] + [u for u in uses if u[2] == "B"]:
-            self._slot(e, usage, late=seg == "B")
+            self._slot(e, usage, late=seg == "B" and self.late_ok)
         ncol = len(p.cols)
         if ncol > NREG:
             raise Unfusable("registers")
@@ -635,15 +651,22 @@ def run_batch(plan: StagePlan, batch: RecordBatch) -> Optional[RecordBatch]:
         plan.reason = str(e)
         return None
     if on_gpu:
-        parts = _launch(prog, batch.n, dev, plan.op)
+        parts = _launch(prog, batch.n, dev, plan)
     else:
         parts = interpret(prog, batch.n, plan.op)
     if parts is None:
-        plan.disabled = True            # more groups than the per-workgroup tables hold: this stage runs eagerly
+        plan.disabled = True            # more groups than the kernel's tables hold: this stage runs eagerly
         return None
-    keys, vals = parts
+    keys, vals = parts                  # host tensors (a few rows): decoded on the host, then one upload each
     plan.stats["fused_batches"] += 1
-    return RecordBatch({plan.kcol: _key_columns(prog, keys), plan.vcol: _value_column(prog, vals)}, int(keys.numel()))
+    return RecordBatch({plan.kcol: _to_dev(_key_columns(prog, keys), dev),
+                        plan.vcol: _to_dev(_value_column(prog, vals), dev)}, int(keys.numel()))
+
+
+def _to_dev(x, dev):
+    if isinstance(x, tuple):
+        return tuple(_to_dev(c, dev) for c in x)
+    return x.to(dev) if x.device != dev else x
 
 
 def _col_args(prog: Program, dev):
@@ -658,22 +681,26 @@ def _col_args(prog: Program, dev):
     return out
 
 
-def _launch(prog: Program, n: int, dev, op: str):
+def _launch(prog: Program, n: int, dev, plan: StagePlan):
     h = _ext.hip()
     ins = torch.tensor(prog.ins if prog.ins else [[0, 0, -1, -1, 0]], dtype=torch.int64).reshape(-1, 5)
-    nins = len(prog.ins)
     if not prog.ins:
         ins = ins[:0]
     lit = torch.frombuffer(bytearray(prog.lit or b"\0"), dtype=torch.uint8).to(dev, non_blocking=True)
-    key, cnt, val, occ, status = h.pipe_agg(ins[:nins], prog.nins_a, _col_args(prog, dev), lit, n, prog.keep_reg,
-                                            prog.key_reg, prog.val_regs, AGG_OPS[op])
-    cap = key.numel() // occ.numel()
-    mask = (torch.arange(cap, device=dev).unsqueeze(0) < occ.unsqueeze(1)).flatten()
-    k = key[mask]
-    v = val[mask][:, : prog.nval]
-    if int(status[0]) != 0:                      # the one host read of the launch
+    table = h.pipe_agg(ins, prog.nins_a, _col_args(prog, dev), lit, n, prog.keep_reg, prog.key_reg, prog.val_regs,
+                       AGG_OPS[plan.op])
+    host = table.cpu()                           # the one device -> host read of the launch
+    if int(host[0]) != 0:
         return None
-    return _merge(k, v, op)
+    if n:
+        _SEL_EST[plan.sig] = int(host[1]) / n
+    gcap = (host.numel() - 2) // (1 + FMAX)
+    keys = host[2:2 + gcap]
+    occ = (keys != _EMPTY).nonzero().flatten()
+    k = keys[occ]
+    order = torch.argsort(k)
+    vals = host[2 + gcap:].view(torch.float64).reshape(gcap, FMAX)
+    return k[order], vals[occ[order], : prog.nval]
 
 
 def _merge(k: torch.Tensor, v: torch.Tensor, op: str):

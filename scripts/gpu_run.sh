@@ -15,6 +15,7 @@
 #   secondary    BASELINE.json secondary configs: LA 64k^2 %*%, config-5 dedup harness
 #   rccl         the one-rank RCCL test (force_collectives) under rocprofv3, to show the RCCL kernels
 #   py           python -u $PY_ARGS (a repo script; PY_LIMIT seconds, default 300)
+#   pyprof       the same under rocprofv3 --kernel-trace --stats (kernel summary copied to py_kernel_stats.csv)
 # Output under gpurun_out/$TAG (TAG defaults to "run").
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -92,6 +93,11 @@ run_task() {
     py)
       timeout -k 10 "${PY_LIMIT:-300}" python -u $PY_ARGS > "$O/py.log" 2>&1 || fail py $? "$O/py.log"
       tail -${PY_TAIL:-20} "$O/py.log" ;;
+    pyprof)
+      timeout -k 10 "${PY_LIMIT:-300}" rocprofv3 --kernel-trace --stats -d "$R/$O/pyprof" -o run --output-format csv -- \
+        python3 $PY_ARGS > "$O/pyprof.log" 2>&1 || fail pyprof $? "$O/pyprof.log"
+      f=$(ls "$O"/pyprof/*/run_kernel_stats.csv "$O"/pyprof/run_kernel_stats.csv 2>/dev/null | head -1)
+      [ -n "$f" ] && cp "$f" "$O/py_kernel_stats.csv" && head -${PY_TAIL:-20} "$O/py_kernel_stats.csv" ;;
     *) echo "[gpu_run] unknown task $1"; exit 2 ;;
   esac
 }

@@ -404,26 +404,57 @@ def test_low_path_scratch_is_o_groups():
     K.SCRATCH_STATS["charged_bytes"] = 0
 
 
+_C1, _C2, _M64 = 0xBF58476D1CE4E5B9, 0x94D049BB133111EB, (1 << 64) - 1
+
+
+def _unxorshift(y, s):
+    x, t = y, y
+    while t:
+        t >>= s
+        x ^= t
+    return x
+
+
+def _inv_mix64(h):
+    """Inverse of relops.hip mix64 (the splitmix64 finaliser): a key whose hash is h."""
+    x = _unxorshift(h, 31)
+    x = (x * pow(_C2, -1, 1 << 64)) & _M64
+    x = _unxorshift(x, 27)
+    x = (x * pow(_C1, -1, 1 << 64)) & _M64
+    return _unxorshift(x, 30)
+
+
+def _mix64(x):
+    x ^= x >> 30
+    x = (x * _C1) & _M64
+    x ^= x >> 27
+    x = (x * _C2) & _M64
+    return x ^ (x >> 31)
+
+
 @pytest.mark.gpu
-def test_part_overflow_falls_back_exactly(monkeypatch):
-    """A PART LDS table so small that its overflow table fills: hash_aggregate reports ok = 0, group_reduce returns
-    None, and the engine's generic path gives the exact result."""
+def test_part_overflow_falls_back_exactly():
+    """Keys crafted so that every one hashes to the same PART bucket, sub-bucket and LDS start slot: the LDS probe
+    windows fill, the overflow table fills, hash_aggregate reports ok = 0, group_reduce returns None, and the
+    engine's generic path gives the exact result."""
     from netsdb_amd.execution import kernels as K
 
-    monkeypatch.setenv("NSDB_AGG_TEST_LCAP_PART", "64")
-    n = 1 << 20
-    keys = torch.randint(0, 1 << 19, (n,), device=DEV) * 3 + 1
-    vals = torch.rand(n, device=DEV, dtype=torch.float64)
+    hs = [(0xA5C3F1 << 40) | (m << 16) | 0x1234 for m in range(1, 200_001)]
+    ks = [_inv_mix64(h) for h in hs]
+    assert all(_mix64(k) == h for k, h in zip(ks[:100], hs[:100]))
+    ks = [k - (1 << 64) if k >= (1 << 63) else k for k in ks]
+    distinct = torch.tensor(ks, dtype=torch.int64)
+    keys = distinct.repeat(5)[torch.randperm(1_000_000)].to(DEV)
+    vals = torch.rand(keys.numel(), device=DEV, dtype=torch.float64)
     r = _ext.hip().hash_aggregate(keys, vals, "sum", False, 0, True)
-    assert r[5].tolist()[2] == 0                                   # the PART overflow table filled
-    assert K.group_reduce(keys, vals, "sum") is None               # the fused path refuses ...
-    inv, reps, g = K.group_ids(keys.cpu())                          # ... and the generic path is exact
+    st = r[5].tolist()
+    assert st[1] == 1 and st[2] == 0, st                     # PART path, its overflow table filled
+    assert K.group_reduce(keys, vals, "sum") is None         # the fused path refuses ...
+    inv, reps, g = K.group_ids(keys.cpu())                    # ... and the generic path is exact
     agg = K.segment_reduce(vals.cpu(), inv, g, "sum")
     u, ui = torch.unique(keys.cpu(), return_inverse=True)
-    assert torch.equal(reps, u) and torch.allclose(agg, torch.zeros(u.numel(), dtype=torch.float64).index_add_(0, ui, vals.cpu()))
-    monkeypatch.delenv("NSDB_AGG_TEST_LCAP_PART")
-    r2 = _ext.hip().hash_aggregate(keys, vals, "sum", False, 0, True)
-    assert r2[5].tolist()[2] == 1
+    ref = torch.zeros(u.numel(), dtype=torch.float64).index_add_(0, ui, vals.cpu())
+    assert torch.equal(reps, u) and torch.allclose(agg, ref)
 
 
 @pytest.mark.gpu
