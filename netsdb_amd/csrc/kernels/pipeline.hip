@@ -6,32 +6,34 @@
 // The stage's lambda trees (the selection predicate, the group key and the value row: makeLambdaFromMember, ==, <,
 // &&, ||, +, -, *, /, IN, LIKE prefix/suffix, CASE) are compiled on the host (execution/pipeline.py) into a short
 // register program that this kernel INTERPRETS per row in registers: no intermediate column (filter mask, value row,
-// key) is ever materialised in HBM. The program is ahead-of-time code (no run-time compilation); its interpretation
-// cost is amortised over ROWS rows per thread and the opcode / register indices are wave-uniform (kernel arguments,
-// scalar branches only).
+// key) is ever materialised in HBM. The program is ahead-of-time code (no run-time compilation); the opcode and
+// register indices are wave-uniform (kernel arguments: scalar loads and scalar branches only).
 //
-//  * Register file: NREG virtual 64-bit registers per row slot as ONE vector value in VGPRs; the wave-uniform register
+//  * Register file: NR virtual 64-bit registers per row slot as ONE vector value in VGPRs; the wave-uniform register
 //    number indexes it with indirect register addressing (s_set_gpr_idx_on + v_mov): no scratch, no per-register
-//    branches.
-//  * Columns are loaded straight into their registers: registers [0, ncol) hold the loaded columns. "Late" columns
-//    (read only by the key / value row) are loaded after the predicate, for the kept rows only (a wave skips the
-//    cache lines none of its kept rows needs).
-//  * Column loads are unrolled over the MAXCOL column slots (compile-time register numbers): every row load of a pass
-//    is issued before the first one is used (the 2nd round only fetches the bytes of short-string columns), so a
-//    wave keeps all its columns' cache lines in flight instead of one column at a time.
+//    branches. Each interpreted instruction runs over ROWS rows per thread, so its dispatch (one scalar load of the
+//    next instruction, issued before the current one executes, and a scalar branch) is amortised over ROWS x 64
+//    rows. Two shapes are instantiated, NR x ROWS = 16 x 2 and 8 x 4: a program that fits in 8 registers (most
+//    predicates, Q06-like aggregates) runs twice as many rows per dispatch.
+//  * Compares carry an AND-with register (the host folds `x CMP y && r` into one instruction), so a conjunction of
+//    k range tests is k instructions, not 2k - 1.
+//  * Columns are loaded straight into their (compile-time) registers [0, ncol): every row load of a pass is issued
+//    before the first one is used (the 2nd round only fetches the bytes of short-string columns, which the host
+//    places in the first MAXSTR column slots). "Late" columns (read only by the key / value row) are loaded after the
+//    predicate, for the kept rows only, when the host's selectivity estimate says that saves bandwidth.
 //  * Aggregation: each thread keeps KSLOT (key, F values) slots in registers (few groups hit them every row); a row
 //    whose key is in no slot goes to the workgroup's LDS hash table (CAP slots, 64-bit CAS + LDS float atomics). At
 //    the end every wave reduces its lanes' slots per distinct key (cross-lane butterflies, one LDS update per key per
 //    wave), and the workgroup merges its table into ONE global table of GCAP slots with device atomics: the host
 //    reads back a few KB, no per-workgroup partials and no second merge pass. A table overflow raises status[0]:
-//    the stage then runs the unfused path (more groups than this kernel is for). status[1] counts the kept rows
-//    (the host's selectivity estimate decides whether value columns load late, after the predicate).
+//    the stage then runs the unfused path (more groups than this kernel is for). status[1] counts the kept rows.
 #include "common.h"
 
 namespace nsdb_pipe {
 
-constexpr int NREG = 16, ROWS = 2, MAXINS = 48, MAXCOL = 10, FMAX = 8, KSLOT = 4, CAP = 256, NTHR = 256;
+constexpr int NREG = 16, MAXINS = 48, MAXCOL = 10, MAXSTR = 4, FMAX = 8, KSLOT = 4, CAP = 256, NTHR = 256;
 constexpr int GCAP = 2048;             // global table slots (power of two)
+constexpr int NREG_SMALL = 8;          // the 8-register x 4-row shape
 constexpr long long EMPTY = (long long)0x8000000000000000ULL;
 constexpr int IMM_REG = -2;            // operand register meaning "the instruction's immediate"
 
@@ -44,6 +46,7 @@ enum ColKind : int { C_F64 = 0, C_I64, C_I32, C_F32, C_U8, C_SCODE, C_SREF };
 
 struct Ins {
   int op, dst, a, b;
+  int c, pad;                    // c >= 0: compares AND their result with register c
   long long imm;
 };
 struct Col {
@@ -51,80 +54,93 @@ struct Col {
   const long long* st;           // string column: row starts / ends into dat
   const long long* en;
   const unsigned char* dat;
-  int kind, late, L, pad;
+  int kind, late, L;
+  int raw_off, aux_off, pad;     // tile kernels: LDS byte offsets of the column's DMA image (string starts / ends)
 };
 struct PipeArgs {
-  Ins ins[MAXINS];
+  Ins ins[MAXINS + 1];           // + a NOP sentinel (the dispatch prefetches one instruction ahead)
   Col col[MAXCOL];
   const unsigned char* lit;      // literal pool of the string ops
   long long n;
-  int nins_a, nins, ncol, keep_reg, key_reg, nval, agg_op, pad;
+  int nins_a, nins, ncol, keep_reg, key_reg, nval, agg_op, nreg;
   int val_reg[FMAX];
+  int tile, lds_bytes;           // tile kernels: rows per tile, dynamic LDS bytes
   unsigned long long* table;     // [2 + GCAP + GCAP * FMAX]: status (overflow, kept rows), keys, values (f64 bits)
 };
 
 typedef unsigned long long u64;
-// The register file of one row slot: NREG 64-bit registers as ONE vector value (NREG VGPR pairs).
-typedef unsigned long long regfile __attribute__((ext_vector_type(NREG)));
+// The register file of one row slot: NR 64-bit registers as ONE vector value (NR VGPR pairs).
+template <int NR>
+struct RF {
+  typedef unsigned long long vec __attribute__((ext_vector_type(NR)));
+};
 
 __device__ __forceinline__ double u2f(u64 x) { return __longlong_as_double((long long)x); }
 __device__ __forceinline__ u64 f2u(double x) { return (u64)__double_as_longlong(x); }
 
 // Short-string code exactly as StringColumn.short_codes / str_pack (bytes big-endian in the low 8L bits, << 3 | len)
-__device__ __forceinline__ u64 short_code(const unsigned char* d, long long s, long long e, int L) {
-  const long long len = e - s;
+__device__ __forceinline__ u64 short_code(const unsigned char* d, long long s, long long len, int L) {
   if (len > L) return (u64)-1;
   u64 c = 0;
   for (int b = 0; b < L; ++b) c |= (b < len ? (u64)d[s + b] : 0ull) << (8 * (L - 1 - b));
   return (c << 3) | (u64)len;
 }
 
-// Pass 1 of a column's load: the row's value (numeric kinds) or its string start (x) and the low word of its end (y).
-__device__ __forceinline__ void fetch(const Col& c, const long long (&row)[ROWS], const bool (&m)[ROWS], u64 (&x)[ROWS],
-                                      unsigned (&y)[ROWS]) {
+// Every column of the pass (LATE: the late columns; else the early ones) into its register. Round 1 issues every
+// row load (numeric values; string starts and the low words of their ends) before any is used; round 2 turns the
+// string columns (slots < MAXSTR) into their register form: the short code from the bytes (keys), or the
+// (start << 24 | length) reference (byte comparisons). Lengths fit 32 bits, so the ends' low words suffice.
+template <bool LATE, int NR, int ROWS>
+__device__ __forceinline__ void load_cols(const PipeArgs& a, const long long (&row)[ROWS], const bool (&m)[ROWS],
+                                          typename RF<NR>::vec (&R)[ROWS]) {
+  unsigned y[MAXSTR][ROWS];
 #pragma unroll
-  for (int j = 0; j < ROWS; ++j) {
-    x[j] = 0;
-    y[j] = 0;
-    if (m[j]) {
-      const long long i = row[j];
-      switch (c.kind) {
-        case C_F64:
-        case C_I64: x[j] = reinterpret_cast<const u64*>(c.p)[i]; break;
-        case C_I32: x[j] = (u64)(long long)reinterpret_cast<const int*>(c.p)[i]; break;
-        case C_F32: x[j] = f2u((double)reinterpret_cast<const float*>(c.p)[i]); break;
-        case C_U8: x[j] = (u64)reinterpret_cast<const unsigned char*>(c.p)[i]; break;
-        default:
-          x[j] = (u64)c.st[i];
-          y[j] = (unsigned)c.en[i];
+  for (int c = 0; c < (NR < MAXCOL ? NR : MAXCOL); ++c) {
+    if (c >= a.ncol || (a.col[c].late != 0) != LATE) continue;
+    const Col& C = a.col[c];
+    const int kind = C.kind;
+    if (kind == C_F64 || kind == C_I64) {
+      const u64* p = reinterpret_cast<const u64*>(C.p);
+#pragma unroll
+      for (int j = 0; j < ROWS; ++j) R[j][c] = m[j] ? p[row[j]] : 0ull;
+    } else if (kind == C_I32) {
+      const int* p = reinterpret_cast<const int*>(C.p);
+#pragma unroll
+      for (int j = 0; j < ROWS; ++j) R[j][c] = m[j] ? (u64)(long long)p[row[j]] : 0ull;
+    } else if (kind == C_F32) {
+      const float* p = reinterpret_cast<const float*>(C.p);
+#pragma unroll
+      for (int j = 0; j < ROWS; ++j) R[j][c] = m[j] ? f2u((double)p[row[j]]) : 0ull;
+    } else if (kind == C_U8) {
+      const unsigned char* p = reinterpret_cast<const unsigned char*>(C.p);
+#pragma unroll
+      for (int j = 0; j < ROWS; ++j) R[j][c] = m[j] ? (u64)p[row[j]] : 0ull;
+    } else if (c < MAXSTR) {
+#pragma unroll
+      for (int j = 0; j < ROWS; ++j) {
+        R[j][c] = m[j] ? (u64)C.st[row[j]] : 0ull;
+        y[c < MAXSTR ? c : 0][j] = m[j] ? (unsigned)C.en[row[j]] : 0u;
       }
     }
   }
-}
-
-// Pass 2: the register value (string kinds: the short code from the bytes / the (start << 24 | length) reference;
-// lengths fit 32 bits, so the end's low word suffices).
-__device__ __forceinline__ u64 finish(const Col& c, u64 x, unsigned y, bool m) {
-  if (c.kind == C_SCODE) return m ? short_code(c.dat, (long long)x, (long long)x + (long long)(unsigned)(y - (unsigned)x), c.L) : 0;
-  if (c.kind == C_SREF) return (x << 24) | (u64)min(y - (unsigned)x, 0xFFFFFFu);
-  return x;
-}
-
-// Every column of the pass (LATE: the late columns; else the early ones) into its register, all loads in flight at once.
-template <bool LATE>
-__device__ __forceinline__ void load_cols(const PipeArgs& a, const long long (&row)[ROWS], const bool (&m)[ROWS],
-                                          regfile (&R)[ROWS]) {
-  u64 x[MAXCOL][ROWS];
-  unsigned y[MAXCOL][ROWS];
 #pragma unroll
-  for (int c = 0; c < MAXCOL; ++c)
-    if (c < a.ncol && (a.col[c].late != 0) == LATE) fetch(a.col[c], row, m, x[c], y[c]);
+  for (int c = 0; c < MAXSTR; ++c) {
+    if (c >= a.ncol || (a.col[c].late != 0) != LATE) continue;
+    const Col& C = a.col[c];
+    if (C.kind == C_SCODE) {
 #pragma unroll
-  for (int c = 0; c < MAXCOL; ++c)
-    if (c < a.ncol && (a.col[c].late != 0) == LATE) {
+      for (int j = 0; j < ROWS; ++j) {
+        const u64 s = R[j][c];
+        R[j][c] = m[j] ? short_code(C.dat, (long long)s, (long long)(unsigned)(y[c][j] - (unsigned)s), C.L) : 0ull;
+      }
+    } else if (C.kind == C_SREF) {
 #pragma unroll
-      for (int j = 0; j < ROWS; ++j) R[j][c] = finish(a.col[c], x[c][j], y[c][j], m[j]);
+      for (int j = 0; j < ROWS; ++j) {
+        const u64 s = R[j][c];
+        R[j][c] = (s << 24) | (u64)min(y[c][j] - (unsigned)s, 0xFFFFFFu);
+      }
     }
+  }
 }
 
 __device__ __forceinline__ bool str_match(const unsigned char* d, u64 ref, const unsigned char* lit, long long imm,
@@ -140,21 +156,27 @@ __device__ __forceinline__ bool str_match(const unsigned char* d, u64 ref, const
   return true;
 }
 
-__device__ __forceinline__ u64 operand(const regfile& R, int k, long long imm) {
+template <int NR>
+__device__ __forceinline__ u64 operand(const typename RF<NR>::vec& R, int k, long long imm) {
   return k == IMM_REG ? (u64)imm : (k >= 0 ? R[k] : 0ull);
 }
 
 // Instructions [lo, hi) of the program over every row slot. The opcode and register numbers are kernel arguments
-// (SGPRs): one scalar dispatch per instruction, indirect register reads / writes.
-__device__ __forceinline__ void run(const PipeArgs& a, regfile (&R)[ROWS], int lo, int hi) {
+// (SGPRs): one scalar dispatch per instruction (the next instruction's fields are loaded while this one runs),
+// indirect register reads / writes.
+template <int NR, int ROWS>
+__device__ __forceinline__ void run(const PipeArgs& a, typename RF<NR>::vec (&R)[ROWS], int lo, int hi) {
+  if (lo >= hi) return;
+  Ins cur = a.ins[lo];
   for (int pc = lo; pc < hi; ++pc) {
-    const int op = a.ins[pc].op, dst = a.ins[pc].dst, ia = a.ins[pc].a, ib = a.ins[pc].b;
-    const long long imm = a.ins[pc].imm;
+    const Ins nxt = a.ins[pc + 1];                     // in bounds: ins has a sentinel after MAXINS
+    const int op = cur.op, dst = cur.dst, ia = cur.a, ib = cur.b, ic = cur.c;
+    const long long imm = cur.imm;
     u64 x[ROWS], y[ROWS], z[ROWS];
 #pragma unroll
     for (int j = 0; j < ROWS; ++j) {
-      x[j] = operand(R[j], ia, imm);
-      y[j] = operand(R[j], ib, imm);
+      x[j] = operand<NR>(R[j], ia, imm);
+      y[j] = operand<NR>(R[j], ib, imm);
     }
     switch (op) {
 #define NSDB_EACH(E)                                          \
@@ -206,8 +228,13 @@ __device__ __forceinline__ void run(const PipeArgs& a, regfile (&R)[ROWS], int l
         for (int j = 0; j < ROWS; ++j) z[j] = 0;
 #undef NSDB_EACH
     }
+    if (ic >= 0) {                                     // compare folded with the AND of its conjunction
+#pragma unroll
+      for (int j = 0; j < ROWS; ++j) z[j] = (z[j] != 0 && R[j][ic] != 0) ? 1ull : 0ull;
+    }
 #pragma unroll
     for (int j = 0; j < ROWS; ++j) R[j][dst] = z[j];
+    cur = nxt;
   }
 }
 
@@ -263,7 +290,7 @@ __device__ __forceinline__ double wave_reduce(double v, int op) {
   return v;
 }
 
-template <int F>
+template <int F, int NR, int ROWS>
 __global__ void __launch_bounds__(NTHR) pipe_agg_kernel(const PipeArgs a) {
   __shared__ long long tk[CAP];
   __shared__ double tv[CAP * FMAX];
@@ -279,9 +306,9 @@ __global__ void __launch_bounds__(NTHR) pipe_agg_kernel(const PipeArgs a) {
   }
   __syncthreads();
 
-  regfile R[ROWS];
+  typename RF<NR>::vec R[ROWS];
 #pragma unroll
-  for (int j = 0; j < ROWS; ++j) R[j] = (regfile)0;
+  for (int j = 0; j < ROWS; ++j) R[j] = (typename RF<NR>::vec)0;
   long long sk[KSLOT];
   double sv[KSLOT][F];
   int used = 0;
@@ -303,8 +330,8 @@ __global__ void __launch_bounds__(NTHR) pipe_agg_kernel(const PipeArgs a) {
       row[j] = base + (long long)j * NTHR + tid;
       inr[j] = row[j] < a.n;
     }
-    load_cols<false>(a, row, inr, R);                          // the predicate's ("early") columns
-    run(a, R, 0, a.nins_a);
+    load_cols<false, NR, ROWS>(a, row, inr, R);              // the predicate's ("early") columns
+    run<NR, ROWS>(a, R, 0, a.nins_a);
     bool any = false;
 #pragma unroll
     for (int j = 0; j < ROWS; ++j) {
@@ -313,8 +340,8 @@ __global__ void __launch_bounds__(NTHR) pipe_agg_kernel(const PipeArgs a) {
       kept += keep[j] ? 1u : 0u;
     }
     if (!__builtin_amdgcn_ballot_w64(any)) continue;           // no kept row in this wave
-    load_cols<true>(a, row, keep, R);                          // late columns: the kept rows only
-    run(a, R, a.nins_a, a.nins);
+    load_cols<true, NR, ROWS>(a, row, keep, R);               // late columns: the kept rows only
+    run<NR, ROWS>(a, R, a.nins_a, a.nins);
 #pragma unroll
     for (int j = 0; j < ROWS; ++j) {
       if (!keep[j]) continue;
@@ -396,11 +423,12 @@ __global__ void __launch_bounds__(NTHR) pipe_init_kernel(unsigned long long* tab
 
 // Filter only: the predicate program over every row, the keep flag written as one byte per row (the FILTER of a
 // scan-filter stage that feeds a join / materialisation: no comparison column, literal column or AND of two masks is
-// materialised; the engine turns the mask into the stage's row selection).
+// materialised; the engine turns the mask into the stage's row selection). The binding marks every column early.
+template <int NR, int ROWS>
 __global__ void __launch_bounds__(NTHR) pipe_mask_kernel(const PipeArgs a, unsigned char* __restrict__ mask) {
-  regfile R[ROWS];
+  typename RF<NR>::vec R[ROWS];
 #pragma unroll
-  for (int j = 0; j < ROWS; ++j) R[j] = (regfile)0;
+  for (int j = 0; j < ROWS; ++j) R[j] = (typename RF<NR>::vec)0;
   const int tid = threadIdx.x;
   const long long step = (long long)gridDim.x * NTHR * ROWS;
   for (long long base = (long long)blockIdx.x * NTHR * ROWS; base < a.n; base += step) {
@@ -411,12 +439,367 @@ __global__ void __launch_bounds__(NTHR) pipe_mask_kernel(const PipeArgs a, unsig
       row[j] = base + (long long)j * NTHR + tid;
       inr[j] = row[j] < a.n;
     }
-    load_cols<false>(a, row, inr, R);
-    run(a, R, 0, a.nins);
+    load_cols<false, NR, ROWS>(a, row, inr, R);
+    run<NR, ROWS>(a, R, 0, a.nins);
 #pragma unroll
     for (int j = 0; j < ROWS; ++j)
       if (inr[j]) mask[row[j]] = (unsigned char)(a.keep_reg < 0 ? 1 : (R[j][a.keep_reg] != 0));
   }
+}
+
+// ------------------------------------------------------------------------------------------------ tile kernels
+// The same programs over LDS-resident column tiles. A workgroup owns tiles of T = 256 * RPT rows: every column's tile
+// is copied HBM -> LDS by LDS-DMA (buffer_load ... lds, 16 B per lane, no VGPR staging), so a wave has T x (column
+// bytes) in flight per tile instead of a few registers' worth, and the registers of the program live in LDS as
+// T-row vectors (register r = rows [r*T, (r+1)*T) of the tile image; 8-byte columns are DMA'd straight into their
+// register). Each thread owns rows tid + 256 i of the tile in every instruction, so the program runs with no barrier;
+// its operands are ds_read_b64 at the thread's row offsets (conflict-free), its dispatch is amortised over RPT rows
+// and it needs no indirect VGPR addressing. Narrow columns (i32 / f32 / u8) and strings are widened into their
+// register by the thread that owns the row (string codes gather their bytes from HBM). Several workgroups per CU
+// overlap one tile's DMA with another's interpretation.
+extern __shared__ __attribute__((aligned(16))) unsigned char tile_smem[];
+
+__device__ __forceinline__ int kind_width(int kind) {
+  return (kind == C_F64 || kind == C_I64) ? 8 : ((kind == C_I32 || kind == C_F32) ? 4 : (kind == C_U8 ? 1 : 8));
+}
+
+// `bytes` of the tile image from g to LDS l, wave `wave`'s share of the wave-instructions. A full tile uses 16-B
+// lanes (bytes is a multiple of 256; 1 KiB per instruction when it is a multiple of 1 KiB); the last, partial tile
+// uses lanes of the element width over exactly `valid` bytes of a bounds-checked buffer resource (lanes past the
+// column's end read zeros, never out of the column).
+__device__ __forceinline__ void dma_tile(const void* g, long long valid, unsigned char* l, int bytes, int w, bool full,
+                                         int wave, int lane) {
+  constexpr int NW = NTHR / 64;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(g), (short)0, (int)(valid < (long long)bytes ? valid : (long long)bytes), 0x00020000);
+  if (full && (bytes & 1023) == 0) {
+    for (int ch = wave; ch < (bytes >> 10); ch += NW)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (nsdb::lds_void*)(l + (ch << 10)), 16, (ch << 10) + lane * 16, 0, 0, 0);
+  } else if (w >= 4) {
+    for (int ch = wave; ch < (bytes >> 8); ch += NW)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (nsdb::lds_void*)(l + (ch << 8)), 4, (ch << 8) + lane * 4, 0, 0, 0);
+  } else {
+    for (int ch = wave; ch < (bytes >> 6); ch += NW)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (nsdb::lds_void*)(l + (ch << 6)), 1, (ch << 6) + lane, 0, 0, 0);
+  }
+}
+
+// Every column's tile (rows [row0, row0 + T)) into its LDS image, then the widening of narrow columns / strings into
+// their register for the rows this thread owns (after the barrier that makes every wave's DMA visible).
+template <int RPT>
+__device__ __forceinline__ void tile_load(const PipeArgs& a, long long row0, long long nrow, u64* regs) {
+  const int T = NTHR * RPT, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const bool full = nrow == T;
+  unsigned char* sm = tile_smem;
+  for (int c = 0; c < a.ncol; ++c) {
+    const Col& C = a.col[c];
+    if (C.kind == C_SCODE || C.kind == C_SREF) {
+      dma_tile(C.st + row0, nrow * 8, sm + C.raw_off, T * 8, 8, full, wave, lane);
+      dma_tile(C.en + row0, nrow * 8, sm + C.aux_off, T * 8, 8, full, wave, lane);
+    } else {
+      const int w = kind_width(C.kind);
+      dma_tile(reinterpret_cast<const unsigned char*>(C.p) + row0 * w, nrow * w, sm + C.raw_off, T * w, w, full, wave,
+               lane);
+    }
+  }
+  __syncthreads();                                     // waits for this wave's DMA; the barrier for everyone's
+  for (int c = 0; c < a.ncol; ++c) {
+    const Col& C = a.col[c];
+    u64* R = regs + (long long)c * T;
+    const unsigned char* raw = sm + C.raw_off;
+    switch (C.kind) {
+      case C_I32:
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) R[tid + i * NTHR] = (u64)(long long)reinterpret_cast<const int*>(raw)[tid + i * NTHR];
+        break;
+      case C_F32:
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) R[tid + i * NTHR] = f2u((double)reinterpret_cast<const float*>(raw)[tid + i * NTHR]);
+        break;
+      case C_U8:
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) R[tid + i * NTHR] = (u64)raw[tid + i * NTHR];
+        break;
+      case C_SCODE: {
+        const long long* en = reinterpret_cast<const long long*>(sm + C.aux_off);
+        u64 code[RPT];
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) {
+          const long long st = (long long)R[tid + i * NTHR];
+          code[i] = (tid + i * NTHR < nrow) ? short_code(C.dat, st, en[tid + i * NTHR] - st, C.L) : 0ull;
+        }
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) R[tid + i * NTHR] = code[i];
+        break;
+      }
+      case C_SREF: {
+        const long long* en = reinterpret_cast<const long long*>(sm + C.aux_off);
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) {
+          const u64 st = R[tid + i * NTHR];
+          R[tid + i * NTHR] = (st << 24) | (u64)min((long long)en[tid + i * NTHR] - (long long)st, 0xFFFFFFll);
+        }
+        break;
+      }
+      default:
+        break;                                         // 8-byte numeric: the DMA image is the register
+    }
+  }
+}
+
+// The program over the thread's RPT rows of the tile; registers are T-row vectors in LDS.
+template <int RPT>
+__device__ __forceinline__ void tile_run(const PipeArgs& a, u64* regs, int lo, int hi) {
+  const int T = NTHR * RPT, tid = threadIdx.x;
+  if (lo >= hi) return;
+  Ins cur = a.ins[lo];
+  for (int pc = lo; pc < hi; ++pc) {
+    const Ins nxt = a.ins[pc + 1];
+    const int op = cur.op, ia = cur.a, ib = cur.b, ic = cur.c;
+    const long long imm = cur.imm;
+    u64 x[RPT], y[RPT], z[RPT];
+    if (ia >= 0) {
+      const u64* A = regs + (long long)ia * T + tid;
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) x[i] = A[i * NTHR];
+    } else {
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) x[i] = ia == IMM_REG ? (u64)imm : 0ull;
+    }
+    if (ib >= 0) {
+      const u64* B = regs + (long long)ib * T + tid;
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) y[i] = B[i * NTHR];
+    } else {
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) y[i] = ib == IMM_REG ? (u64)imm : 0ull;
+    }
+    switch (op) {
+#define NSDB_EACH(E)                                          \
+  _Pragma("unroll") for (int j = 0; j < RPT; ++j) {           \
+    const double fx = u2f(x[j]), fy = u2f(y[j]);              \
+    const long long sx = (long long)x[j], sy = (long long)y[j]; \
+    (void)fx; (void)fy; (void)sx; (void)sy;                   \
+    z[j] = (E);                                               \
+  }                                                           \
+  break;
+      case OP_CONST: NSDB_EACH((u64)imm)
+      case OP_ADDF: NSDB_EACH(f2u(fx + fy))
+      case OP_SUBF: NSDB_EACH(f2u(fx - fy))
+      case OP_MULF: NSDB_EACH(f2u(fx * fy))
+      case OP_DIVF: NSDB_EACH(f2u(fx / fy))
+      case OP_NEGF: NSDB_EACH(f2u(-fx))
+      case OP_ADDI: NSDB_EACH((u64)(sx + sy))
+      case OP_SUBI: NSDB_EACH((u64)(sx - sy))
+      case OP_MULI: NSDB_EACH((u64)(sx * sy))
+      case OP_I2F: NSDB_EACH(f2u((double)sx))
+      case OP_LTF: NSDB_EACH((u64)(fx < fy))
+      case OP_LEF: NSDB_EACH((u64)(fx <= fy))
+      case OP_GTF: NSDB_EACH((u64)(fx > fy))
+      case OP_GEF: NSDB_EACH((u64)(fx >= fy))
+      case OP_EQF: NSDB_EACH((u64)(fx == fy))
+      case OP_NEF: NSDB_EACH((u64)(fx != fy))
+      case OP_LTI: NSDB_EACH((u64)(sx < sy))
+      case OP_LEI: NSDB_EACH((u64)(sx <= sy))
+      case OP_GTI: NSDB_EACH((u64)(sx > sy))
+      case OP_GEI: NSDB_EACH((u64)(sx >= sy))
+      case OP_EQI: NSDB_EACH((u64)(sx == sy))
+      case OP_NEI: NSDB_EACH((u64)(sx != sy))
+      case OP_AND: NSDB_EACH((u64)((x[j] != 0) & (y[j] != 0)))
+      case OP_OR: NSDB_EACH((u64)((x[j] != 0) | (y[j] != 0)))
+      case OP_NOT: NSDB_EACH((u64)(x[j] == 0))
+      case OP_PACK: NSDB_EACH((x[j] << (imm & 63)) | y[j])
+      case OP_SEL: {
+        const u64* S = regs + (long long)imm * T + tid;
+#pragma unroll
+        for (int j = 0; j < RPT; ++j) z[j] = x[j] ? y[j] : S[j * NTHR];
+        break;
+      }
+      case OP_SEQ:
+      case OP_SPRE:
+      case OP_SSUF: {
+        const unsigned char* d = a.col[ib].dat;
+        const int mode = op == OP_SEQ ? 0 : (op == OP_SPRE ? 1 : 2);
+#pragma unroll
+        for (int j = 0; j < RPT; ++j) z[j] = str_match(d, x[j], a.lit, imm, mode) ? 1ull : 0ull;
+        break;
+      }
+      default:
+#pragma unroll
+        for (int j = 0; j < RPT; ++j) z[j] = 0;
+#undef NSDB_EACH
+    }
+    if (ic >= 0) {
+      const u64* C = regs + (long long)ic * T + tid;
+#pragma unroll
+      for (int j = 0; j < RPT; ++j) z[j] = (z[j] != 0 && C[j * NTHR] != 0) ? 1ull : 0ull;
+    }
+    u64* D = regs + (long long)cur.dst * T + tid;
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) D[j * NTHR] = z[j];
+    cur = nxt;
+  }
+}
+
+template <int F, int RPT>
+__global__ void __launch_bounds__(NTHR) tile_agg_kernel(const PipeArgs a) {
+  __shared__ long long tk[CAP];
+  __shared__ double tv[CAP * FMAX];
+  __shared__ int s_ovf;
+  __shared__ unsigned long long s_kept;
+  constexpr int T = NTHR * RPT;
+  const int tid = threadIdx.x, lane = tid & 63;
+  u64* regs = reinterpret_cast<u64*>(tile_smem);
+  const double init = a.agg_op == 0 ? 0.0 : (a.agg_op == 1 ? __builtin_inf() : -__builtin_inf());
+  for (int i = tid; i < CAP; i += NTHR) tk[i] = EMPTY;
+  for (int i = tid; i < CAP * FMAX; i += NTHR) tv[i] = init;
+  if (tid == 0) {
+    s_ovf = 0;
+    s_kept = 0;
+  }
+  long long sk[KSLOT];
+  double sv[KSLOT][F];
+  int used = 0;
+  unsigned kept = 0;
+  bool ovf = false;
+#pragma unroll
+  for (int s = 0; s < KSLOT; ++s) {
+    sk[s] = EMPTY;
+#pragma unroll
+    for (int f = 0; f < F; ++f) sv[s][f] = init;
+  }
+  const long long ntiles = (a.n + T - 1) / T;
+  for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const long long row0 = t * T, nrow = min((long long)T, a.n - row0);
+    __syncthreads();                                   // the previous tile's registers are no longer read
+    tile_load<RPT>(a, row0, nrow, regs);
+    tile_run<RPT>(a, regs, 0, a.nins);
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int r = tid + i * NTHR;
+      if (r >= nrow) continue;
+      if (a.keep_reg >= 0 && regs[(long long)a.keep_reg * T + r] == 0) continue;
+      ++kept;
+      const long long key = a.key_reg < 0 ? 0 : (long long)regs[(long long)a.key_reg * T + r];
+      double v[F];
+#pragma unroll
+      for (int f = 0; f < F; ++f) v[f] = f < a.nval ? u2f(regs[(long long)a.val_reg[f] * T + r]) : 0.0;
+      bool done = false;
+#pragma unroll
+      for (int s = 0; s < KSLOT; ++s) {
+        if (!done && s < used && sk[s] == key) {
+#pragma unroll
+          for (int f = 0; f < F; ++f) sv[s][f] = acc_op(sv[s][f], v[f], a.agg_op);
+          done = true;
+        }
+      }
+      if (!done && used < KSLOT) {
+#pragma unroll
+        for (int s = 0; s < KSLOT; ++s) {
+          if (!done && s == used) {
+            sk[s] = key;
+#pragma unroll
+            for (int f = 0; f < F; ++f) sv[s][f] = v[f];
+            done = true;
+          }
+        }
+        ++used;
+      }
+      if (!done) ovf |= (key == EMPTY) || !table_insert<F>(tk, tv, CAP, key, v, a.nval, a.agg_op);
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < KSLOT; ++s) {
+    bool act = s < used;
+    while (true) {
+      const u64 bal = __builtin_amdgcn_ballot_w64(act);
+      if (!bal) break;
+      const int leader = __builtin_ctzll(bal);
+      const long long kl = __shfl(sk[s], leader);
+      const bool mine = act && sk[s] == kl;
+      double v[F];
+#pragma unroll
+      for (int f = 0; f < F; ++f) v[f] = wave_reduce(mine ? sv[s][f] : init, a.agg_op);
+      if (lane == leader) ovf |= (kl == EMPTY) || !table_insert<F>(tk, tv, CAP, kl, v, a.nval, a.agg_op);
+      act = act && !mine;
+    }
+  }
+  atomicAdd(&s_kept, (unsigned long long)kept);
+  if (ovf) s_ovf = 1;
+  __syncthreads();
+  long long* gk = reinterpret_cast<long long*>(a.table + 2);
+  double* gv = reinterpret_cast<double*>(a.table + 2 + GCAP);
+  for (int i = tid; i < CAP; i += NTHR) {
+    const long long k = tk[i];
+    if (k == EMPTY) continue;
+    double v[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) v[f] = tv[i * FMAX + f];
+    if (!table_insert<F>(gk, gv, GCAP, k, v, a.nval, a.agg_op)) s_ovf = 1;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    if (s_ovf) atomicOr(a.table, 1ull);
+    atomicAdd(a.table + 1, s_kept);
+  }
+}
+
+template <int RPT>
+__global__ void __launch_bounds__(NTHR) tile_mask_kernel(const PipeArgs a, unsigned char* __restrict__ mask) {
+  constexpr int T = NTHR * RPT;
+  const int tid = threadIdx.x;
+  u64* regs = reinterpret_cast<u64*>(tile_smem);
+  const long long ntiles = (a.n + T - 1) / T;
+  for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const long long row0 = t * T, nrow = min((long long)T, a.n - row0);
+    __syncthreads();
+    tile_load<RPT>(a, row0, nrow, regs);
+    tile_run<RPT>(a, regs, 0, a.nins);
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int r = tid + i * NTHR;
+      if (r < nrow) mask[row0 + r] = (unsigned char)(a.keep_reg < 0 ? 1 : (regs[(long long)a.keep_reg * T + r] != 0));
+    }
+  }
+}
+
+// Dynamic LDS above the 64 KiB default needs the kernel's attribute raised (once per shape is enough; it is cheap).
+template <int F>
+void launch_tile_agg(const PipeArgs& a, int grid, hipStream_t st) {
+  auto go = [&](auto kern) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              a.lds_bytes);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(NTHR), a.lds_bytes, st, a);
+  };
+  if (a.tile == 2048)
+    go(tile_agg_kernel<F, 8>);
+  else if (a.tile == 1024)
+    go(tile_agg_kernel<F, 4>);
+  else
+    go(tile_agg_kernel<F, 2>);
+}
+
+void launch_tile_mask(const PipeArgs& a, unsigned char* mask, int grid, hipStream_t st) {
+  auto go = [&](auto kern) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              a.lds_bytes);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(NTHR), a.lds_bytes, st, a, mask);
+  };
+  if (a.tile == 2048)
+    go(tile_mask_kernel<8>);
+  else if (a.tile == 1024)
+    go(tile_mask_kernel<4>);
+  else
+    go(tile_mask_kernel<2>);
+}
+
+
+template <int F>
+void launch_agg(const PipeArgs& a, int grid, hipStream_t st) {
+  if (a.nreg <= NREG_SMALL)
+    hipLaunchKernelGGL((pipe_agg_kernel<F, NREG_SMALL, 4>), dim3(grid), dim3(NTHR), 0, st, a);
+  else
+    hipLaunchKernelGGL((pipe_agg_kernel<F, NREG, 2>), dim3(grid), dim3(NTHR), 0, st, a);
 }
 
 }  // namespace nsdb_pipe
@@ -430,38 +813,59 @@ int nsdb_pipe_sizes(int* out) {
   out[3] = nsdb_pipe::FMAX;
   out[4] = nsdb_pipe::CAP;
   out[5] = (int)sizeof(nsdb_pipe::PipeArgs);
-  out[6] = nsdb_pipe::ROWS;
+  out[6] = nsdb_pipe::MAXSTR;
   out[7] = nsdb_pipe::NTHR;
   out[8] = nsdb_pipe::GCAP;
+  out[9] = nsdb_pipe::NREG_SMALL;
   return 0;
 }
 
-// args: a host PipeArgs image (the binding fills it field by field, the mask pass marks every column early);
-// grid = number of workgroups. Initialises the global table, then the fused pass.
+// args: a host PipeArgs image (the binding fills it field by field and sets nreg = 1 + the highest register the
+// program touches, which picks the register-file shape); grid = number of workgroups. Initialises the global
+// table, then the fused pass.
 int nsdb_pipe_agg(const void* args, int grid, hipStream_t st) {
   if (grid <= 0) return -1;
   const nsdb_pipe::PipeArgs& a = *reinterpret_cast<const nsdb_pipe::PipeArgs*>(args);
   if (a.nins > nsdb_pipe::MAXINS || a.ncol > nsdb_pipe::MAXCOL || a.nval > nsdb_pipe::FMAX || a.nins_a > a.nins ||
-      a.table == nullptr)
+      a.table == nullptr || a.nreg < 1 || a.nreg > nsdb_pipe::NREG)
     return -2;
+  if (a.tile != 0 && a.tile != 512 && a.tile != 1024 && a.tile != 2048) return -3;
   hipLaunchKernelGGL(nsdb_pipe::pipe_init_kernel, dim3(nsdb_pipe::GCAP / nsdb_pipe::NTHR), dim3(nsdb_pipe::NTHR), 0, st,
                      a.table, a.agg_op);
-  if (a.nval <= 2)
-    hipLaunchKernelGGL(nsdb_pipe::pipe_agg_kernel<2>, dim3(grid), dim3(nsdb_pipe::NTHR), 0, st, a);
-  else if (a.nval <= 4)
-    hipLaunchKernelGGL(nsdb_pipe::pipe_agg_kernel<4>, dim3(grid), dim3(nsdb_pipe::NTHR), 0, st, a);
-  else if (a.nval <= 6)
-    hipLaunchKernelGGL(nsdb_pipe::pipe_agg_kernel<6>, dim3(grid), dim3(nsdb_pipe::NTHR), 0, st, a);
-  else
-    hipLaunchKernelGGL(nsdb_pipe::pipe_agg_kernel<nsdb_pipe::FMAX>, dim3(grid), dim3(nsdb_pipe::NTHR), 0, st, a);
+  if (a.tile) {
+    if (a.nval <= 2)
+      nsdb_pipe::launch_tile_agg<2>(a, grid, st);
+    else if (a.nval <= 4)
+      nsdb_pipe::launch_tile_agg<4>(a, grid, st);
+    else if (a.nval <= 6)
+      nsdb_pipe::launch_tile_agg<6>(a, grid, st);
+    else
+      nsdb_pipe::launch_tile_agg<nsdb_pipe::FMAX>(a, grid, st);
+  } else if (a.nval <= 2) {
+    nsdb_pipe::launch_agg<2>(a, grid, st);
+  } else if (a.nval <= 4) {
+    nsdb_pipe::launch_agg<4>(a, grid, st);
+  } else if (a.nval <= 6) {
+    nsdb_pipe::launch_agg<6>(a, grid, st);
+  } else {
+    nsdb_pipe::launch_agg<nsdb_pipe::FMAX>(a, grid, st);
+  }
   return (int)hipGetLastError();
 }
 
 int nsdb_pipe_mask(const void* args, unsigned char* mask, int grid, hipStream_t st) {
   if (grid <= 0) return -1;
   const nsdb_pipe::PipeArgs& a = *reinterpret_cast<const nsdb_pipe::PipeArgs*>(args);
-  if (a.nins > nsdb_pipe::MAXINS || a.ncol > nsdb_pipe::MAXCOL) return -2;
-  hipLaunchKernelGGL(nsdb_pipe::pipe_mask_kernel, dim3(grid), dim3(nsdb_pipe::NTHR), 0, st, a, mask);
+  if (a.nins > nsdb_pipe::MAXINS || a.ncol > nsdb_pipe::MAXCOL || a.nreg < 1 || a.nreg > nsdb_pipe::NREG) return -2;
+  if (a.tile != 0 && a.tile != 512 && a.tile != 1024 && a.tile != 2048) return -3;
+  if (a.tile)
+    nsdb_pipe::launch_tile_mask(a, mask, grid, st);
+  else if (a.nreg <= nsdb_pipe::NREG_SMALL)
+    hipLaunchKernelGGL((nsdb_pipe::pipe_mask_kernel<nsdb_pipe::NREG_SMALL, 4>), dim3(grid), dim3(nsdb_pipe::NTHR), 0,
+                       st, a, mask);
+  else
+    hipLaunchKernelGGL((nsdb_pipe::pipe_mask_kernel<nsdb_pipe::NREG, 2>), dim3(grid), dim3(nsdb_pipe::NTHR), 0, st, a,
+                       mask);
   return (int)hipGetLastError();
 }
 

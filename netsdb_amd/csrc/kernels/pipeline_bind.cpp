@@ -23,6 +23,7 @@ namespace {
 constexpr int MAXINS = 48, MAXCOL = 10, FMAX = 8;
 struct Ins {
   int op, dst, a, b;
+  int c, pad;
   long long imm;
 };
 struct Col {
@@ -30,23 +31,25 @@ struct Col {
   const long long* st;
   const long long* en;
   const unsigned char* dat;
-  int kind, late, L, pad;
+  int kind, late, L;
+  int raw_off, aux_off, pad;
 };
 struct PipeArgs {
-  Ins ins[MAXINS];
+  Ins ins[MAXINS + 1];
   Col col[MAXCOL];
   const unsigned char* lit;
   long long n;
-  int nins_a, nins, ncol, keep_reg, key_reg, nval, agg_op, pad;
+  int nins_a, nins, ncol, keep_reg, key_reg, nval, agg_op, nreg;
   int val_reg[FMAX];
+  int tile, lds_bytes;
   unsigned long long* table;
 };
 
 enum ColKind : int { C_F64 = 0, C_I64, C_I32, C_F32, C_U8, C_SCODE, C_SREF };
-enum : int { OP_SEQ = 26, OP_SPRE = 27, OP_SSUF = 28, OP_SEL = 29, OP_LAST = 30 };
+enum : int { OP_LTF = 10, OP_NEI = 21, OP_SEQ = 26, OP_SPRE = 27, OP_SSUF = 28, OP_SEL = 29, OP_LAST = 30 };
 
 int sizes(int i) {
-  static int s[9] = {0};
+  static int s[10] = {0};
   static bool init = false;
   if (!init) {
     nsdb_pipe_sizes(s);
@@ -60,7 +63,7 @@ void check_col(const torch::Tensor& t, int64_t n, const char* what) {
   TORCH_CHECK(t.numel() >= n, "pipe_agg: ", what, " has fewer than n rows");
 }
 
-// prog: int64 [nins, 5] (op, dst, a, b, imm) on the CPU.
+// prog: int64 [nins, 6] (op, dst, a, b, c, imm) on the CPU; c >= 0 only on compares (AND with register c).
 // cols: per column (kind, late, L, data, starts, ends, bytes): data for numeric kinds, starts / ends / bytes for strings.
 typedef std::vector<std::tuple<int64_t, int64_t, int64_t, c10::optional<torch::Tensor>, c10::optional<torch::Tensor>,
                                c10::optional<torch::Tensor>, c10::optional<torch::Tensor>>>
@@ -73,10 +76,11 @@ void fill_args(PipeArgs& a, const torch::Tensor& prog, int64_t nins_a, const Col
                   sizes(8) > 0 && (sizes(8) & (sizes(8) - 1)) == 0,
               "pipe_agg: host / kernel argument layout mismatch");
   const int NREG = sizes(2);
-  TORCH_CHECK(prog.device().is_cpu() && prog.scalar_type() == torch::kInt64 && prog.dim() == 2 && prog.size(1) == 5,
-              "pipe_agg: prog must be a CPU int64 [nins, 5] tensor");
+  TORCH_CHECK(prog.device().is_cpu() && prog.scalar_type() == torch::kInt64 && prog.dim() == 2 && prog.size(1) == 6,
+              "pipe_agg: prog must be a CPU int64 [nins, 6] tensor");
   const int nins = (int)prog.size(0), ncol = (int)cols.size(), nval = (int)val_regs.size();
   TORCH_CHECK(nins <= MAXINS && ncol <= MAXCOL && ncol <= NREG && nval <= FMAX && nval >= 0, "pipe_agg: too large");
+  const int MAXSTR = sizes(6);
   TORCH_CHECK(nins_a >= 0 && nins_a <= nins, "pipe_agg: bad nins_a");
   TORCH_CHECK(n >= 0, "pipe_agg: n < 0");
   TORCH_CHECK(agg_op >= 0 && agg_op <= 2, "pipe_agg: agg_op is 0 sum, 1 min, 2 max");
@@ -90,11 +94,15 @@ void fill_args(PipeArgs& a, const torch::Tensor& prog, int64_t nins_a, const Col
     I.dst = (int)P[i][1];
     I.a = (int)P[i][2];
     I.b = (int)P[i][3];
-    I.imm = P[i][4];
+    I.c = (int)P[i][4];
+    I.imm = P[i][5];
     TORCH_CHECK(I.op >= 0 && I.op <= OP_LAST, "pipe_agg: bad opcode at ", i);
     TORCH_CHECK(I.dst >= 0 && I.dst < NREG && I.a >= -2 && I.a < NREG && I.b >= -2 && I.b < NREG,
                 "pipe_agg: register out of range at ", i);
+    TORCH_CHECK(I.c == -1 || (I.c >= 0 && I.c < NREG && I.op >= OP_LTF && I.op <= OP_NEI),
+                "pipe_agg: AND-with register only on compares, at ", i);
     if (I.op == OP_SEL) TORCH_CHECK(I.imm >= 0 && I.imm < NREG, "pipe_agg: select register at ", i);
+    a.nreg = std::max({a.nreg, I.dst + 1, I.a + 1, I.b + 1, I.c + 1, I.op == OP_SEL ? (int)I.imm + 1 : 0});
     if (I.op == OP_SEQ || I.op == OP_SPRE || I.op == OP_SSUF) {
       TORCH_CHECK(I.b >= 0 && I.b < ncol && std::get<0>(cols[I.b]) == C_SREF, "pipe_agg: string op column at ", i);
       const long long off = I.imm >> 16, len = I.imm & 0xFFFF;
@@ -111,6 +119,7 @@ void fill_args(PipeArgs& a, const torch::Tensor& prog, int64_t nins_a, const Col
     C.L = (int)std::get<2>(t);
     TORCH_CHECK(C.kind >= C_F64 && C.kind <= C_SREF, "pipe_agg: bad column kind");
     if (C.kind == C_SCODE || C.kind == C_SREF) {
+      TORCH_CHECK(c < MAXSTR, "pipe_agg: string columns must take the first ", MAXSTR, " column slots");
       TORCH_CHECK(std::get<4>(t).has_value() && std::get<5>(t).has_value() && std::get<6>(t).has_value(),
                   "pipe_agg: string column needs starts / ends / bytes");
       const auto &s = *std::get<4>(t), &e = *std::get<5>(t), &d = *std::get<6>(t);
@@ -135,6 +144,7 @@ void fill_args(PipeArgs& a, const torch::Tensor& prog, int64_t nins_a, const Col
     }
   }
   a.ncol = ncol;
+  a.nreg = std::max({a.nreg, ncol, (int)keep_reg + 1, (int)key_reg + 1, 1});
   a.lit = lit.data_ptr<uint8_t>();
   a.n = n;
   a.keep_reg = (int)keep_reg;
@@ -143,19 +153,67 @@ void fill_args(PipeArgs& a, const torch::Tensor& prog, int64_t nins_a, const Col
   for (int f = 0; f < nval; ++f) {
     TORCH_CHECK(val_regs[f] >= 0 && val_regs[f] < NREG, "pipe_agg: bad value register");
     a.val_reg[f] = (int)val_regs[f];
+    a.nreg = std::max(a.nreg, a.val_reg[f] + 1);
   }
   a.agg_op = (int)agg_op;
+}
+
+// LDS layout of the tile kernels for tile T: registers [0, nreg) as T x 8-byte vectors (8-byte columns are DMA'd
+// straight into theirs; string starts too), then the DMA images of narrow columns and the string ends. Returns the
+// dynamic LDS bytes.
+int tile_bytes(PipeArgs& a, int T) {
+  long long off = (long long)a.nreg * T * 8;
+  for (int c = 0; c < a.ncol; ++c) {
+    Col& C = a.col[c];
+    C.raw_off = c * T * 8;
+    C.aux_off = 0;
+    const int w = (C.kind == C_I32 || C.kind == C_F32) ? 4 : (C.kind == C_U8 ? 1 : 8);
+    if (C.kind == C_SCODE || C.kind == C_SREF) {
+      C.aux_off = (int)off;
+      off += (long long)T * 8;
+    } else if (w < 8) {
+      C.raw_off = (int)off;
+      off += ((long long)T * w + 15) / 16 * 16;
+    }
+  }
+  return (int)off;
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// Pick the tile kernels' tile size (0: the register kernels): the largest tile whose LDS lets several workgroups
+// share a CU, every column 16-byte aligned (the DMA's 16-byte lanes). `force` >= 0 overrides (0 = register kernels).
+void choose_tile(PipeArgs& a, int static_bytes, int64_t force) {
+  a.tile = 0;
+  a.lds_bytes = 0;
+  if (force == 0) return;
+  for (int c = 0; c < a.ncol; ++c) {
+    const Col& C = a.col[c];
+    if ((C.kind == C_SCODE || C.kind == C_SREF) ? !(aligned16(C.st) && aligned16(C.en)) : !aligned16(C.p)) return;
+  }
+  const int LDS = 160 * 1024;
+  const int cand[5][2] = {{2048, 3}, {1024, 3}, {1024, 2}, {512, 2}, {512, 1}};   // (tile, workgroups per CU)
+  for (const auto& tc : cand) {
+    if (force > 0 && tc[0] != force) continue;
+    const int b = tile_bytes(a, tc[0]);
+    if ((long long)(b + static_bytes) * tc[1] <= LDS) {
+      a.tile = tc[0];
+      a.lds_bytes = b;
+      return;
+    }
+  }
 }
 
 // Returns the global result table, int64 [2 + GCAP * (1 + FMAX)]: status (overflow flag, kept rows), GCAP keys
 // (INT64_MIN = free slot), then GCAP x FMAX f64 values (bit patterns). The host reads it back in one copy.
 torch::Tensor pipe_agg(torch::Tensor prog, int64_t nins_a, ColList cols, torch::Tensor lit, int64_t n, int64_t keep_reg,
-                       int64_t key_reg, std::vector<int64_t> val_regs, int64_t agg_op, int64_t max_wg) {
-  const int ROWS = sizes(6), NTHR = sizes(7), GCAP = sizes(8);
+                       int64_t key_reg, std::vector<int64_t> val_regs, int64_t agg_op, int64_t max_wg, int64_t tile) {
+  const int ROWS = 4, NTHR = sizes(7), GCAP = sizes(8), CAP = sizes(4);
   PipeArgs a;
   fill_args(a, prog, nins_a, cols, lit, n, keep_reg, key_reg, val_regs, agg_op);
-  // enough workgroups to fill 256 CUs several times over, each thread still looping over a few row pairs
-  const long long per = (long long)NTHR * ROWS * 4;
+  choose_tile(a, CAP * (8 + 8 * FMAX) + 16, tile);
+  // enough workgroups to fill 256 CUs several times over, each still looping over a few tiles / row blocks
+  const long long per = a.tile ? (long long)a.tile : (long long)NTHR * ROWS * 4;
   const int nwg = (int)std::max<long long>(1, std::min<long long>(max_wg > 0 ? max_wg : 2048, (n + per - 1) / per));
   auto table = torch::empty({2 + (long long)GCAP * (1 + FMAX)}, lit.options().dtype(torch::kInt64));
   a.table = reinterpret_cast<unsigned long long*>(table.data_ptr<int64_t>());
@@ -165,15 +223,16 @@ torch::Tensor pipe_agg(torch::Tensor prog, int64_t nins_a, ColList cols, torch::
 }
 
 // The predicate program's keep flag per row (uint8 [n]); key / values unused.
-torch::Tensor pipe_mask(torch::Tensor prog, ColList cols, torch::Tensor lit, int64_t n, int64_t keep_reg) {
-  const int ROWS = sizes(6), NTHR = sizes(7);
+torch::Tensor pipe_mask(torch::Tensor prog, ColList cols, torch::Tensor lit, int64_t n, int64_t keep_reg, int64_t tile) {
+  const int ROWS = 4, NTHR = sizes(7);
   PipeArgs a;
   fill_args(a, prog, prog.size(0), cols, lit, n, keep_reg, -1, {}, 0);
   for (int c = 0; c < a.ncol; ++c) a.col[c].late = 0;      // the mask pass loads every column up front
+  choose_tile(a, 0, tile);
   auto mask = torch::empty({n}, lit.options().dtype(torch::kUInt8));
   if (n > 0) {
-    const long long per = (long long)NTHR * ROWS * 4;
-    const int nwg = (int)std::max<long long>(1, std::min<long long>(4096, (n + per - 1) / per));
+    const long long per = a.tile ? (long long)a.tile : (long long)NTHR * ROWS * 4;
+    const int nwg = (int)std::max<long long>(1, std::min<long long>(a.tile ? 2048 : 4096, (n + per - 1) / per));
     const int rc = nsdb_pipe_mask(&a, mask.data_ptr<uint8_t>(), nwg, c10::hip::getCurrentHIPStream().stream());
     TORCH_CHECK(rc == 0, "pipe_mask launch failed: ", rc);
   }
@@ -184,11 +243,12 @@ torch::Tensor pipe_mask(torch::Tensor prog, ColList cols, torch::Tensor lit, int
 
 void register_pipeline(pybind11::module& m) {
   m.def("pipe_mask", &pipe_mask, "fused filter predicate (pipeline.hip): keep flag per row (uint8)",
-        pybind11::arg("prog"), pybind11::arg("cols"), pybind11::arg("lit"), pybind11::arg("n"), pybind11::arg("keep_reg"));
+        pybind11::arg("prog"), pybind11::arg("cols"), pybind11::arg("lit"), pybind11::arg("n"), pybind11::arg("keep_reg"),
+        pybind11::arg("tile") = -1);
   m.def("pipe_agg", &pipe_agg,
         "fused scan -> filter -> project -> low-cardinality aggregate (pipeline.hip): the global result table "
         "int64 [2 + GCAP * 9] = status (overflow, kept rows), keys, f64 values [GCAP, 8]",
         pybind11::arg("prog"), pybind11::arg("nins_a"), pybind11::arg("cols"), pybind11::arg("lit"), pybind11::arg("n"),
         pybind11::arg("keep_reg"), pybind11::arg("key_reg"), pybind11::arg("val_regs"), pybind11::arg("agg_op") = 0,
-        pybind11::arg("max_wg") = 0);
+        pybind11::arg("max_wg") = 0, pybind11::arg("tile") = -1);
 }

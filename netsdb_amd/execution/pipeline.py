@@ -36,7 +36,7 @@ from ..objects.record import RecordBatch
 from ..objects.strings import StringColumn
 
 # ---- must match pipeline.hip ----------------------------------------------------------------------------------
-NREG, MAXINS, MAXCOL, FMAX = 16, 48, 10, 8
+NREG, MAXINS, MAXCOL, FMAX, MAXSTR = 16, 48, 10, 8, 4
 IMM = -2                       # operand register number meaning "the instruction's immediate"
 (OP_NOP, OP_CONST, OP_ADDF, OP_SUBF, OP_MULF, OP_DIVF, OP_ADDI, OP_SUBI, OP_MULI, OP_I2F,
  OP_LTF, OP_LEF, OP_GTF, OP_GEF, OP_EQF, OP_NEF, OP_LTI, OP_LEI, OP_GTI, OP_GEI, OP_EQI, OP_NEI,
@@ -55,6 +55,9 @@ CPU_INTERPRETER = False
 INTERP_CAP = 1 << 30
 # late (post-predicate) loads of the key / value columns only when the stage keeps fewer rows than this fraction
 LATE_MAX_SEL = 0.25
+# kernel shape: -1 picks the LDS-tile kernels when their tile fits (else the register kernels), 0 forces the register
+# kernels, 512 / 1024 / 2048 force that tile
+TILE = -1
 _SEL_EST: Dict[tuple, float] = {}          # stage signature -> kept fraction measured by its last launch
 _EMPTY = -(1 << 63)                        # free slot of the kernel's global table
 
@@ -211,7 +214,7 @@ class Program:
     """A compiled program + the column table it reads."""
 
     def __init__(self):
-        self.ins: List[Tuple[int, int, int, int, int]] = []
+        self.ins: List[Tuple[int, int, int, int, int, int]] = []     # (op, dst, a, b, c, imm)
         self.cols: List[dict] = []            # {"key": (path, usage), "kind", "late", "L", "obj": column}
         self.col_index: Dict[tuple, int] = {}
         self.lit = bytearray()
@@ -237,10 +240,18 @@ class Program:
             self.free.append(r)
 
     def emit(self, op, dst, a=-1, b=-1, imm=0):
-        """a / b == IMM: that operand is the 64-bit immediate."""
+        """a / b == IMM: that operand is the 64-bit immediate. ``AND d, r, t`` right after the compare that wrote the
+        temporary t folds into that compare (its AND-with field c = r): one instruction per conjunct."""
+        if op == OP_AND and self.ins:
+            po, pd, pa, pb, pc, pimm = self.ins[-1]
+            if OP_LTF <= po <= OP_NEI and pc < 0:
+                other = a if pd == b else (b if pd == a else None)
+                if other is not None and other != pd and pd >= len(self.cols) and pd not in self.pinned:
+                    self.ins[-1] = (po, dst, pa, pb, other, pimm)
+                    return
         if len(self.ins) >= MAXINS:
             raise Unfusable("program too long")
-        self.ins.append((op, dst, a, b, int(imm)))
+        self.ins.append((op, dst, a, b, -1, int(imm)))
 
     def literal(self, s: str) -> int:
         b = s.encode()
@@ -337,6 +348,7 @@ class _Compiler:
             self._collect(v, "num", "B", uses)
         for e, usage, seg in [u for u in uses if u[2] == "A"] + [u for u in uses if u[2] == "B"]:
             self._slot(e, usage, late=seg == "B" and self.late_ok)
+        self._strings_first()
         ncol = len(p.cols)
         if ncol > NREG:
             raise Unfusable("registers")
@@ -380,6 +392,17 @@ class _Compiler:
         if p.val_shape == "scalar" and self._static_type(plan.val) != "f":
             raise Unfusable("integer value (the eager path sums it exactly as int64)")
         return p
+
+    def _strings_first(self):
+        """String columns take the first column slots (the kernel's 2nd load round only covers MAXSTR slots)."""
+        p = self.p
+        order = sorted(range(len(p.cols)), key=lambda i: (p.cols[i]["kind"] not in (C_SCODE, C_SREF), i))
+        if sum(c["kind"] in (C_SCODE, C_SREF) for c in p.cols) > MAXSTR:
+            raise Unfusable("string columns")
+        if order != list(range(len(order))):
+            where = {old: new for new, old in enumerate(order)}
+            p.cols = [p.cols[i] for i in order]
+            p.col_index = {k: where[i] for k, i in p.col_index.items()}
 
     def _truthy(self, r, t):
         p = self.p
@@ -683,12 +706,12 @@ def _col_args(prog: Program, dev):
 
 def _launch(prog: Program, n: int, dev, plan: StagePlan):
     h = _ext.hip()
-    ins = torch.tensor(prog.ins if prog.ins else [[0, 0, -1, -1, 0]], dtype=torch.int64).reshape(-1, 5)
+    ins = torch.tensor(prog.ins if prog.ins else [[0, 0, -1, -1, -1, 0]], dtype=torch.int64).reshape(-1, 6)
     if not prog.ins:
         ins = ins[:0]
     lit = torch.frombuffer(bytearray(prog.lit or b"\0"), dtype=torch.uint8).to(dev, non_blocking=True)
     table = h.pipe_agg(ins, prog.nins_a, _col_args(prog, dev), lit, n, prog.keep_reg, prog.key_reg, prog.val_regs,
-                       AGG_OPS[plan.op])
+                       AGG_OPS[plan.op], 0, TILE)
     host = table.cpu()                           # the one device -> host read of the launch
     if int(host[0]) != 0:
         return None
@@ -785,7 +808,7 @@ def _run_program(prog: Program, n: int) -> List[Optional[torch.Tensor]]:
         return torch.tensor(m, dtype=torch.int64)
 
     def run(lo, hi):
-        for opc, d, a, b, imm in prog.ins[lo:hi]:
+        for opc, d, a, b, c, imm in prog.ins[lo:hi]:
             x = regs[a] if a >= 0 else (torch.full((n,), imm, dtype=torch.int64) if a == IMM else None)
             y = regs[b] if b >= 0 else (torch.full((n,), imm, dtype=torch.int64) if b == IMM else None)
             if opc == OP_CONST:
@@ -818,6 +841,8 @@ def _run_program(prog: Program, n: int) -> List[Optional[torch.Tensor]]:
                 z = torch.where(x != 0, y, regs[imm])
             else:
                 z = torch.zeros(n, dtype=torch.int64)
+            if c >= 0:                          # compare folded with its conjunction's AND
+                z = ((z != 0) & (regs[c] != 0)).long()
             regs[d] = z
 
     run(0, len(prog.ins))
@@ -900,9 +925,9 @@ def run_filter(plan: FilterPlan, batch: RecordBatch) -> Optional[RecordBatch]:
         plan.reason = str(e)
         return None
     if on_gpu:
-        ins = torch.tensor(prog.ins, dtype=torch.int64).reshape(-1, 5)
+        ins = torch.tensor(prog.ins, dtype=torch.int64).reshape(-1, 6)
         lit = torch.frombuffer(bytearray(prog.lit or b"\0"), dtype=torch.uint8).to(dev, non_blocking=True)
-        mask = _ext.hip().pipe_mask(ins, _col_args(prog, dev), lit, batch.n, prog.keep_reg).bool()
+        mask = _ext.hip().pipe_mask(ins, _col_args(prog, dev), lit, batch.n, prog.keep_reg, TILE).bool()
     else:
         mask = interpret_mask(prog, batch.n)
     plan.stats["fused_batches"] += 1

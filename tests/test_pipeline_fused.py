@@ -144,7 +144,10 @@ def test_fused_overflow_falls_back(monkeypatch):
 
 
 @pytest.mark.gpu
-def test_fused_tpch_gpu_vs_eager_and_pandas():
+@pytest.mark.parametrize("tile", [-1, 0])
+def test_fused_tpch_gpu_vs_eager_and_pandas(tile, monkeypatch):
+    """Both kernel shapes (LDS-tile and register interpreters) against the eager path and pandas."""
+    monkeypatch.setattr(PL, "TILE", tile)
     t = tpch_gen.generate_fast(0.05, seed=4)
     f = tpch.frames(t)
     c = _client("cuda:0", t)
@@ -187,3 +190,58 @@ def test_fused_overflow_gpu():
     fused = _agg_job(c, *args)
     assert c.engine.pipeline_stats["fallback_batches"] >= 1
     assert eager[0] == fused[0] and torch.allclose(eager[1], fused[1])
+
+
+def _table_result(table: torch.Tensor, nval: int):
+    host = table.cpu()
+    gcap = (host.numel() - 2) // 9
+    keys = host[2:2 + gcap]
+    occ = (keys != -(1 << 63)).nonzero().flatten()
+    order = torch.argsort(keys[occ])
+    vals = host[2 + gcap:].view(torch.float64).reshape(gcap, 8)
+    return int(host[0]), int(host[1]), keys[occ][order], vals[occ[order], :nval]
+
+
+@pytest.mark.gpu
+def test_pipe_kernel_shapes_gpu():
+    """pipe_agg / pipe_mask directly: every tile size and the register kernels on the same program (all column kinds,
+    a partial last tile, string keys, compare-AND folding) give the torch interpreter's groups and sums."""
+    import struct
+
+    from netsdb_amd import _ext
+    from netsdb_amd.objects.strings import StringColumn
+
+    h = _ext.hip()
+    dev = torch.device("cuda:0")
+    n = 100_003
+    g = torch.Generator().manual_seed(3)
+    a = torch.randint(0, 100, (n,), generator=g, dtype=torch.int32)
+    b = torch.rand(n, generator=g, dtype=torch.float32)
+    u = torch.randint(0, 4, (n,), generator=g, dtype=torch.uint8)
+    d = torch.rand(n, generator=g, dtype=torch.float64) * 100
+    words = ["A", "BB", "CCC"]
+    s = StringColumn.from_list([words[i % 3] for i in torch.randint(0, 3, (n,), generator=g).tolist()])
+    fb = lambda v: struct.unpack("<q", struct.pack("<d", v))[0]  # noqa: E731
+    I = PL.IMM
+    # regs: 0 s (scode, L=3), 1 a, 2 b, 3 u, 4 d; keep 5 = a < 50 && b >= 0.25; key 6 = pack(s, u); values d, b*2
+    ins = [(PL.OP_LTI, 5, 1, I, -1, 50), (PL.OP_GEF, 5, 2, I, 5, fb(0.25)),
+           (PL.OP_PACK, 6, 0, 3, -1, 8), (PL.OP_MULF, 7, 2, I, -1, fb(2.0))]
+    prog = PL.Program()
+    prog.cols = [{"kind": PL.C_SCODE, "late": 0, "L": 3, "obj": s}, {"kind": PL.C_I32, "late": 0, "L": 0, "obj": a},
+                 {"kind": PL.C_F32, "late": 0, "L": 0, "obj": b}, {"kind": PL.C_U8, "late": 0, "L": 0, "obj": u},
+                 {"kind": PL.C_F64, "late": 0, "L": 0, "obj": d}]
+    prog.ins, prog.nins_a, prog.keep_reg, prog.key_reg, prog.val_regs = ins, 2, 5, 6, [4, 7]
+    ref_k, ref_v = PL.interpret(prog, n, "sum")
+    ref_mask = PL.interpret_mask(prog, n)
+    gprog = PL.Program()
+    gprog.cols = [dict(c, obj=c["obj"].to(dev)) for c in prog.cols]
+    cols = PL._col_args(gprog, dev)
+    lit = torch.zeros(1, dtype=torch.uint8, device=dev)
+    pt = torch.tensor(ins, dtype=torch.int64)
+    for tile in (0, 512, 1024, 2048):
+        st, kept, k, v = _table_result(h.pipe_agg(pt, 2, cols, lit, n, 5, 6, [4, 7], 0, 0, tile), 2)
+        assert st == 0 and kept == int(ref_mask.sum()), tile
+        assert torch.equal(k, ref_k), tile
+        assert torch.allclose(v, ref_v, rtol=1e-12, atol=1e-9), tile
+        m = h.pipe_mask(pt[:2], cols, lit, n, 5, tile).bool().cpu()
+        assert torch.equal(m, ref_mask), tile
