@@ -55,7 +55,8 @@ struct Col {
   const long long* en;
   const unsigned char* dat;
   int kind, late, L;
-  int raw_off, aux_off, pad;     // tile kernels: LDS byte offsets of the column's DMA image (string starts / ends)
+  int raw_off, aux_off;          // tile kernels: LDS byte offsets of the column's DMA image (string starts / ends)
+  int contig;                    // strings: en == st + 1 (one offsets array): the tile DMAs the starts only
 };
 struct PipeArgs {
   Ins ins[MAXINS + 1];           // + a NOP sentinel (the dispatch prefetches one instruction ahead)
@@ -267,7 +268,7 @@ __device__ __forceinline__ void atomic_acc(double* p, double v, int op) {
 }
 
 // Linear-probing insert of (key, values) into a table of cap slots (LDS or global). False: the table is full.
-template <int F>
+template <int F, int STRIDE = FMAX>
 __device__ __forceinline__ bool table_insert(long long* tk, double* tv, unsigned cap, long long key, const double (&v)[F],
                                              int nval, int op) {
   unsigned h = slot_hash(key) & (cap - 1);
@@ -276,7 +277,7 @@ __device__ __forceinline__ bool table_insert(long long* tk, double* tv, unsigned
     if (prev == EMPTY || prev == key) {
 #pragma unroll
       for (int f = 0; f < F; ++f)
-        if (f < nval) atomic_acc(tv + (size_t)h * FMAX + f, v[f], op);
+        if (f < nval) atomic_acc(tv + (size_t)h * STRIDE + f, v[f], op);
       return true;
     }
     h = (h + 1) & (cap - 1);
@@ -463,86 +464,99 @@ __device__ __forceinline__ int kind_width(int kind) {
   return (kind == C_F64 || kind == C_I64) ? 8 : ((kind == C_I32 || kind == C_F32) ? 4 : (kind == C_U8 ? 1 : 8));
 }
 
-// `bytes` of the tile image from g to LDS l, wave `wave`'s share of the wave-instructions. A full tile uses 16-B
-// lanes (bytes is a multiple of 256; 1 KiB per instruction when it is a multiple of 1 KiB); the last, partial tile
-// uses lanes of the element width over exactly `valid` bytes of a bounds-checked buffer resource (lanes past the
-// column's end read zeros, never out of the column).
+// `bytes` of the tile image from g to LDS l, wave `wave`'s share of the wave-instructions. A full tile whose image
+// is a multiple of 1 KiB uses 16-B DMA lanes; otherwise 4-byte elements use 4-B DMA lanes over exactly `valid` bytes
+// of a bounds-checked buffer resource (lanes past the column's end read zeros, never out of the column), and byte
+// columns are copied by the threads (a 1-byte DMA lane writes a whole LDS dword).
 __device__ __forceinline__ void dma_tile(const void* g, long long valid, unsigned char* l, int bytes, int w, bool full,
                                          int wave, int lane) {
   constexpr int NW = NTHR / 64;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<void*>(g), (short)0, (int)(valid < (long long)bytes ? valid : (long long)bytes), 0x00020000);
+  const int nv = (int)(valid < (long long)bytes ? valid : (long long)bytes);
+  if (w < 4 && !(full && (bytes & 1023) == 0)) {
+    const unsigned char* src = reinterpret_cast<const unsigned char*>(g);
+    for (int i = wave * 64 + lane; i < nv; i += NTHR) l[i] = src[i];
+    return;
+  }
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(g), (short)0, nv, 0x00020000);
   if (full && (bytes & 1023) == 0) {
     for (int ch = wave; ch < (bytes >> 10); ch += NW)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (nsdb::lds_void*)(l + (ch << 10)), 16, (ch << 10) + lane * 16, 0, 0, 0);
-  } else if (w >= 4) {
+  } else {
     for (int ch = wave; ch < (bytes >> 8); ch += NW)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (nsdb::lds_void*)(l + (ch << 8)), 4, (ch << 8) + lane * 4, 0, 0, 0);
-  } else {
-    for (int ch = wave; ch < (bytes >> 6); ch += NW)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (nsdb::lds_void*)(l + (ch << 6)), 1, (ch << 6) + lane, 0, 0, 0);
   }
 }
 
-// Every column's tile (rows [row0, row0 + T)) into its LDS image, then the widening of narrow columns / strings into
-// their register for the rows this thread owns (after the barrier that makes every wave's DMA visible).
+// Every column's tile (rows [row0, row0 + T)) into its LDS image, then the widening into 8-byte registers for the
+// rows this thread owns (after the barrier that makes every wave's DMA visible). A narrow column (i32 / f32 / u8) is
+// DMA'd into the top of its own register vector and widened in place: every thread first reads its rows' narrow
+// values, a barrier, then writes the widened words (a row's word may cover another row's narrow bytes). A string's
+// starts are DMA'd into its register, its ends into an aux vector, or, when starts / ends are one offsets array,
+// taken from the next row's start (the tile's last row reads its end from HBM).
 template <int RPT>
 __device__ __forceinline__ void tile_load(const PipeArgs& a, long long row0, long long nrow, u64* regs) {
   const int T = NTHR * RPT, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const bool full = nrow == T;
   unsigned char* sm = tile_smem;
+  bool narrow = false;
   for (int c = 0; c < a.ncol; ++c) {
     const Col& C = a.col[c];
     if (C.kind == C_SCODE || C.kind == C_SREF) {
       dma_tile(C.st + row0, nrow * 8, sm + C.raw_off, T * 8, 8, full, wave, lane);
-      dma_tile(C.en + row0, nrow * 8, sm + C.aux_off, T * 8, 8, full, wave, lane);
+      if (!C.contig) dma_tile(C.en + row0, nrow * 8, sm + C.aux_off, T * 8, 8, full, wave, lane);
     } else {
       const int w = kind_width(C.kind);
+      narrow |= w < 8;
       dma_tile(reinterpret_cast<const unsigned char*>(C.p) + row0 * w, nrow * w, sm + C.raw_off, T * w, w, full, wave,
                lane);
     }
   }
   __syncthreads();                                     // waits for this wave's DMA; the barrier for everyone's
-  for (int c = 0; c < a.ncol; ++c) {
+  if (narrow) {
+    for (int c = 0; c < a.ncol; ++c) {
+      const int k = a.col[c].kind;
+      if (k != C_I32 && k != C_F32 && k != C_U8) continue;
+      const unsigned char* raw = sm + a.col[c].raw_off;
+      u64 wide[RPT];
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) {
+        const int r = tid + i * NTHR;
+        wide[i] = k == C_I32 ? (u64)(long long)reinterpret_cast<const int*>(raw)[r]
+                : k == C_F32 ? f2u((double)reinterpret_cast<const float*>(raw)[r])
+                : (u64)raw[r];
+      }
+      __syncthreads();                                 // every narrow value read before any word overwrites it
+      u64* R = regs + (long long)c * T;
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) R[tid + i * NTHR] = wide[i];
+    }
+  }
+  for (int c = 0; c < a.ncol && c < MAXSTR; ++c) {
     const Col& C = a.col[c];
+    if (C.kind != C_SCODE && C.kind != C_SREF) continue;
     u64* R = regs + (long long)c * T;
-    const unsigned char* raw = sm + C.raw_off;
-    switch (C.kind) {
-      case C_I32:
+    const long long* en = reinterpret_cast<const long long*>(sm + C.aux_off);
+    long long st[RPT], e[RPT];
 #pragma unroll
-        for (int i = 0; i < RPT; ++i) R[tid + i * NTHR] = (u64)(long long)reinterpret_cast<const int*>(raw)[tid + i * NTHR];
-        break;
-      case C_F32:
+    for (int i = 0; i < RPT; ++i) {
+      const int r = tid + i * NTHR;
+      st[i] = (long long)R[r];
+      if (!C.contig)
+        e[i] = en[r];
+      else
+        e[i] = r + 1 < nrow ? (long long)R[r + 1] : (r < nrow ? C.en[row0 + r] : st[i]);
+    }
+    if (C.contig) __syncthreads();                     // every start read before any is overwritten by a code
+    if (C.kind == C_SCODE) {
+      u64 code[RPT];
 #pragma unroll
-        for (int i = 0; i < RPT; ++i) R[tid + i * NTHR] = f2u((double)reinterpret_cast<const float*>(raw)[tid + i * NTHR]);
-        break;
-      case C_U8:
+      for (int i = 0; i < RPT; ++i)
+        code[i] = (tid + i * NTHR < nrow) ? short_code(C.dat, st[i], e[i] - st[i], C.L) : 0ull;
 #pragma unroll
-        for (int i = 0; i < RPT; ++i) R[tid + i * NTHR] = (u64)raw[tid + i * NTHR];
-        break;
-      case C_SCODE: {
-        const long long* en = reinterpret_cast<const long long*>(sm + C.aux_off);
-        u64 code[RPT];
+      for (int i = 0; i < RPT; ++i) R[tid + i * NTHR] = code[i];
+    } else {
 #pragma unroll
-        for (int i = 0; i < RPT; ++i) {
-          const long long st = (long long)R[tid + i * NTHR];
-          code[i] = (tid + i * NTHR < nrow) ? short_code(C.dat, st, en[tid + i * NTHR] - st, C.L) : 0ull;
-        }
-#pragma unroll
-        for (int i = 0; i < RPT; ++i) R[tid + i * NTHR] = code[i];
-        break;
-      }
-      case C_SREF: {
-        const long long* en = reinterpret_cast<const long long*>(sm + C.aux_off);
-#pragma unroll
-        for (int i = 0; i < RPT; ++i) {
-          const u64 st = R[tid + i * NTHR];
-          R[tid + i * NTHR] = (st << 24) | (u64)min((long long)en[tid + i * NTHR] - (long long)st, 0xFFFFFFll);
-        }
-        break;
-      }
-      default:
-        break;                                         // 8-byte numeric: the DMA image is the register
+      for (int i = 0; i < RPT; ++i) R[tid + i * NTHR] = ((u64)st[i] << 24) | (u64)min(e[i] - st[i], 0xFFFFFFll);
     }
   }
 }
@@ -644,26 +658,27 @@ __device__ __forceinline__ void tile_run(const PipeArgs& a, u64* regs, int lo, i
 template <int F, int RPT>
 __global__ void __launch_bounds__(NTHR) tile_agg_kernel(const PipeArgs a) {
   __shared__ long long tk[CAP];
-  __shared__ double tv[CAP * FMAX];
+  __shared__ double tv[CAP * F];                     // stride F: the table costs what the stage's values need
   __shared__ int s_ovf;
   __shared__ unsigned long long s_kept;
   constexpr int T = NTHR * RPT;
+  constexpr int KS = F <= 6 ? 2 * KSLOT : KSLOT;   // no register file in VGPRs here: room for more register slots
   const int tid = threadIdx.x, lane = tid & 63;
   u64* regs = reinterpret_cast<u64*>(tile_smem);
   const double init = a.agg_op == 0 ? 0.0 : (a.agg_op == 1 ? __builtin_inf() : -__builtin_inf());
   for (int i = tid; i < CAP; i += NTHR) tk[i] = EMPTY;
-  for (int i = tid; i < CAP * FMAX; i += NTHR) tv[i] = init;
+  for (int i = tid; i < CAP * F; i += NTHR) tv[i] = init;
   if (tid == 0) {
     s_ovf = 0;
     s_kept = 0;
   }
-  long long sk[KSLOT];
-  double sv[KSLOT][F];
+  long long sk[KS];
+  double sv[KS][F];
   int used = 0;
   unsigned kept = 0;
   bool ovf = false;
 #pragma unroll
-  for (int s = 0; s < KSLOT; ++s) {
+  for (int s = 0; s < KS; ++s) {
     sk[s] = EMPTY;
 #pragma unroll
     for (int f = 0; f < F; ++f) sv[s][f] = init;
@@ -686,16 +701,16 @@ __global__ void __launch_bounds__(NTHR) tile_agg_kernel(const PipeArgs a) {
       for (int f = 0; f < F; ++f) v[f] = f < a.nval ? u2f(regs[(long long)a.val_reg[f] * T + r]) : 0.0;
       bool done = false;
 #pragma unroll
-      for (int s = 0; s < KSLOT; ++s) {
+      for (int s = 0; s < KS; ++s) {
         if (!done && s < used && sk[s] == key) {
 #pragma unroll
           for (int f = 0; f < F; ++f) sv[s][f] = acc_op(sv[s][f], v[f], a.agg_op);
           done = true;
         }
       }
-      if (!done && used < KSLOT) {
+      if (!done && used < KS) {
 #pragma unroll
-        for (int s = 0; s < KSLOT; ++s) {
+        for (int s = 0; s < KS; ++s) {
           if (!done && s == used) {
             sk[s] = key;
 #pragma unroll
@@ -705,11 +720,11 @@ __global__ void __launch_bounds__(NTHR) tile_agg_kernel(const PipeArgs a) {
         }
         ++used;
       }
-      if (!done) ovf |= (key == EMPTY) || !table_insert<F>(tk, tv, CAP, key, v, a.nval, a.agg_op);
+      if (!done) ovf |= (key == EMPTY) || !table_insert<F, F>(tk, tv, CAP, key, v, a.nval, a.agg_op);
     }
   }
 #pragma unroll
-  for (int s = 0; s < KSLOT; ++s) {
+  for (int s = 0; s < KS; ++s) {
     bool act = s < used;
     while (true) {
       const u64 bal = __builtin_amdgcn_ballot_w64(act);
@@ -720,7 +735,7 @@ __global__ void __launch_bounds__(NTHR) tile_agg_kernel(const PipeArgs a) {
       double v[F];
 #pragma unroll
       for (int f = 0; f < F; ++f) v[f] = wave_reduce(mine ? sv[s][f] : init, a.agg_op);
-      if (lane == leader) ovf |= (kl == EMPTY) || !table_insert<F>(tk, tv, CAP, kl, v, a.nval, a.agg_op);
+      if (lane == leader) ovf |= (kl == EMPTY) || !table_insert<F, F>(tk, tv, CAP, kl, v, a.nval, a.agg_op);
       act = act && !mine;
     }
   }
@@ -734,7 +749,7 @@ __global__ void __launch_bounds__(NTHR) tile_agg_kernel(const PipeArgs a) {
     if (k == EMPTY) continue;
     double v[F];
 #pragma unroll
-    for (int f = 0; f < F; ++f) v[f] = tv[i * FMAX + f];
+    for (int f = 0; f < F; ++f) v[f] = tv[i * F + f];
     if (!table_insert<F>(gk, gv, GCAP, k, v, a.nval, a.agg_op)) s_ovf = 1;
   }
   __syncthreads();
@@ -775,6 +790,8 @@ void launch_tile_agg(const PipeArgs& a, int grid, hipStream_t st) {
     go(tile_agg_kernel<F, 8>);
   else if (a.tile == 1024)
     go(tile_agg_kernel<F, 4>);
+  else if (a.tile == 768)
+    go(tile_agg_kernel<F, 3>);
   else
     go(tile_agg_kernel<F, 2>);
 }
@@ -789,6 +806,8 @@ void launch_tile_mask(const PipeArgs& a, unsigned char* mask, int grid, hipStrea
     go(tile_mask_kernel<8>);
   else if (a.tile == 1024)
     go(tile_mask_kernel<4>);
+  else if (a.tile == 768)
+    go(tile_mask_kernel<3>);
   else
     go(tile_mask_kernel<2>);
 }
@@ -829,7 +848,7 @@ int nsdb_pipe_agg(const void* args, int grid, hipStream_t st) {
   if (a.nins > nsdb_pipe::MAXINS || a.ncol > nsdb_pipe::MAXCOL || a.nval > nsdb_pipe::FMAX || a.nins_a > a.nins ||
       a.table == nullptr || a.nreg < 1 || a.nreg > nsdb_pipe::NREG)
     return -2;
-  if (a.tile != 0 && a.tile != 512 && a.tile != 1024 && a.tile != 2048) return -3;
+  if (a.tile != 0 && a.tile != 512 && a.tile != 768 && a.tile != 1024 && a.tile != 2048) return -3;
   hipLaunchKernelGGL(nsdb_pipe::pipe_init_kernel, dim3(nsdb_pipe::GCAP / nsdb_pipe::NTHR), dim3(nsdb_pipe::NTHR), 0, st,
                      a.table, a.agg_op);
   if (a.tile) {
@@ -857,7 +876,7 @@ int nsdb_pipe_mask(const void* args, unsigned char* mask, int grid, hipStream_t 
   if (grid <= 0) return -1;
   const nsdb_pipe::PipeArgs& a = *reinterpret_cast<const nsdb_pipe::PipeArgs*>(args);
   if (a.nins > nsdb_pipe::MAXINS || a.ncol > nsdb_pipe::MAXCOL || a.nreg < 1 || a.nreg > nsdb_pipe::NREG) return -2;
-  if (a.tile != 0 && a.tile != 512 && a.tile != 1024 && a.tile != 2048) return -3;
+  if (a.tile != 0 && a.tile != 512 && a.tile != 768 && a.tile != 1024 && a.tile != 2048) return -3;
   if (a.tile)
     nsdb_pipe::launch_tile_mask(a, mask, grid, st);
   else if (a.nreg <= nsdb_pipe::NREG_SMALL)

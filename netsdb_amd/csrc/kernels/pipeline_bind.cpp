@@ -32,7 +32,8 @@ struct Col {
   const long long* en;
   const unsigned char* dat;
   int kind, late, L;
-  int raw_off, aux_off, pad;
+  int raw_off, aux_off;
+  int contig;
 };
 struct PipeArgs {
   Ins ins[MAXINS + 1];
@@ -130,6 +131,7 @@ void fill_args(PipeArgs& a, const torch::Tensor& prog, int64_t nins_a, const Col
       TORCH_CHECK(C.kind != C_SCODE || (C.L >= 0 && C.L <= 7), "pipe_agg: short code length bound 0..7");
       C.st = reinterpret_cast<const long long*>(s.data_ptr<int64_t>());
       C.en = reinterpret_cast<const long long*>(e.data_ptr<int64_t>());
+      C.contig = C.en == C.st + 1 ? 1 : 0;             // one offsets array: ends are the next rows' starts
       C.dat = d.data_ptr<uint8_t>();
     } else {
       TORCH_CHECK(std::get<3>(t).has_value(), "pipe_agg: numeric column needs data");
@@ -158,22 +160,19 @@ void fill_args(PipeArgs& a, const torch::Tensor& prog, int64_t nins_a, const Col
   a.agg_op = (int)agg_op;
 }
 
-// LDS layout of the tile kernels for tile T: registers [0, nreg) as T x 8-byte vectors (8-byte columns are DMA'd
-// straight into theirs; string starts too), then the DMA images of narrow columns and the string ends. Returns the
-// dynamic LDS bytes.
+// LDS layout of the tile kernels for tile T: registers [0, nreg) as T x 8-byte vectors. 8-byte columns and string
+// starts are DMA'd straight into their register, narrow columns into its top (widened in place), string ends (when
+// not the next row's start) into an aux vector after the registers. Returns the dynamic LDS bytes.
 int tile_bytes(PipeArgs& a, int T) {
   long long off = (long long)a.nreg * T * 8;
   for (int c = 0; c < a.ncol; ++c) {
     Col& C = a.col[c];
-    C.raw_off = c * T * 8;
-    C.aux_off = 0;
     const int w = (C.kind == C_I32 || C.kind == C_F32) ? 4 : (C.kind == C_U8 ? 1 : 8);
-    if (C.kind == C_SCODE || C.kind == C_SREF) {
+    C.raw_off = c * T * 8 + T * (8 - w);
+    C.aux_off = 0;
+    if ((C.kind == C_SCODE || C.kind == C_SREF) && !C.contig) {
       C.aux_off = (int)off;
       off += (long long)T * 8;
-    } else if (w < 8) {
-      C.raw_off = (int)off;
-      off += ((long long)T * w + 15) / 16 * 16;
     }
   }
   return (int)off;
@@ -189,10 +188,12 @@ void choose_tile(PipeArgs& a, int static_bytes, int64_t force) {
   if (force == 0) return;
   for (int c = 0; c < a.ncol; ++c) {
     const Col& C = a.col[c];
-    if ((C.kind == C_SCODE || C.kind == C_SREF) ? !(aligned16(C.st) && aligned16(C.en)) : !aligned16(C.p)) return;
+    if ((C.kind == C_SCODE || C.kind == C_SREF) ? !(aligned16(C.st) && (C.contig || aligned16(C.en))) : !aligned16(C.p))
+      return;
   }
   const int LDS = 160 * 1024;
-  const int cand[5][2] = {{2048, 3}, {1024, 3}, {1024, 2}, {512, 2}, {512, 1}};   // (tile, workgroups per CU)
+  // (tile, workgroups per CU): three workgroups per CU overlap one's DMA with the others' work; then the larger tile
+  const int cand[7][2] = {{2048, 3}, {1024, 3}, {768, 3}, {1024, 2}, {768, 2}, {512, 2}, {512, 1}};
   for (const auto& tc : cand) {
     if (force > 0 && tc[0] != force) continue;
     const int b = tile_bytes(a, tc[0]);
@@ -211,7 +212,8 @@ torch::Tensor pipe_agg(torch::Tensor prog, int64_t nins_a, ColList cols, torch::
   const int ROWS = 4, NTHR = sizes(7), GCAP = sizes(8), CAP = sizes(4);
   PipeArgs a;
   fill_args(a, prog, nins_a, cols, lit, n, keep_reg, key_reg, val_regs, agg_op);
-  choose_tile(a, CAP * (8 + 8 * FMAX) + 16, tile);
+  const int F = a.nval <= 2 ? 2 : (a.nval <= 4 ? 4 : (a.nval <= 6 ? 6 : FMAX));
+  choose_tile(a, CAP * (8 + 8 * F) + 16, tile);
   // enough workgroups to fill 256 CUs several times over, each still looping over a few tiles / row blocks
   const long long per = a.tile ? (long long)a.tile : (long long)NTHR * ROWS * 4;
   const int nwg = (int)std::max<long long>(1, std::min<long long>(max_wg > 0 ? max_wg : 2048, (n + per - 1) / per));

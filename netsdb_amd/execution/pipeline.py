@@ -696,6 +696,11 @@ def _col_args(prog: Program, dev):
     out = []
     for c in prog.cols:
         o = c["obj"]
+        if c["kind"] == C_SCODE:
+            codes = o.short_codes(c["L"])          # the column's kept fixed-width encoding: a plain int64 load
+            if codes is not None:
+                out.append((C_I64, c["late"], 0, codes.contiguous(), None, None, None))
+                continue
         if isinstance(o, StringColumn):
             out.append((c["kind"], c["late"], c["L"], None, o.starts.contiguous(), o.ends.contiguous(), o.data))
         else:

@@ -129,7 +129,7 @@ class StringColumn:
     rows costs two device gathers and no device->host read. Kernels take (starts, ends) and so run on either
     form; :attr:`offsets` (serialisation, shuffles) packs a view in place on first use."""
 
-    __slots__ = ("data", "starts", "ends", "_off", "payload", "buf_rows", "_maxlen")
+    __slots__ = ("data", "starts", "ends", "_off", "payload", "buf_rows", "_maxlen", "_codes")
 
     def __init__(self, data: torch.Tensor, offsets: torch.Tensor, payload: int, buf_rows: Optional[int] = None,
                  maxlen: Optional[int] = None):
@@ -139,6 +139,7 @@ class StringColumn:
         if maxlen is None and offsets.device.type == "cpu" and offsets.numel() > 1:
             maxlen = int(np.diff(offsets.numpy()).max())       # host offsets: free to bound here
         self._maxlen = maxlen     # upper bound of the row lengths (None: not known yet, see max_len)
+        self._codes = None        # (L, short codes) once computed: the column's fixed-width encoding, kept
 
     @staticmethod
     def view(data: torch.Tensor, starts: torch.Tensor, ends: torch.Tensor, payload: int,
@@ -146,6 +147,7 @@ class StringColumn:
         c = StringColumn.__new__(StringColumn)
         c.data, c.starts, c.ends, c._off, c.payload, c.buf_rows = data, starts, ends, None, int(payload), buf_rows
         c._maxlen = maxlen
+        c._codes = None
         return c
 
     # ------------------------------------------------------------------ construction
@@ -217,9 +219,13 @@ class StringColumn:
                 return self.take(torch.arange(s, e, step, dtype=torch.long))
             e = max(e, s)
             if self._off is not None:
-                return StringColumn(self.data, self._off[s:e + 1], self.payload, self.buf_rows, self._maxlen)
-            return StringColumn.view(self.data, self.starts[s:e], self.ends[s:e], self.payload, self.buf_rows,
-                                     self._maxlen)
+                out = StringColumn(self.data, self._off[s:e + 1], self.payload, self.buf_rows, self._maxlen)
+            else:
+                out = StringColumn.view(self.data, self.starts[s:e], self.ends[s:e], self.payload, self.buf_rows,
+                                        self._maxlen)
+            if self._codes is not None:
+                out._codes = (self._codes[0], self._codes[1][s:e])
+            return out
         if isinstance(i, (torch.Tensor, list, np.ndarray)):
             return self.take(i)
         n = len(self)
@@ -367,13 +373,22 @@ class StringColumn:
         """Exact int64 code per row when every row is <= 7 bytes, else None: bytes big-endian in the low 8L bits
         (L = :meth:`max_len`, or a larger given bound), shifted left 3, OR the length. Equal codes <=> equal
         strings and code order = byte order, so short string keys group, join and sort as integers (no hash, no
-        byte re-check)."""
+        byte re-check).
+
+        The codes are the column's fixed-width encoding (8 bytes a row, like the dictionary / inline encoding a
+        column store keeps for short strings): computed once per column and bound L, then kept with the column, so
+        a scan that groups or filters on a short string reads one int64 per row instead of two offsets and the
+        bytes. Callers must not modify the returned tensor in place."""
         ml = self.max_len()
         L = ml if L is None else L
         if L > 7 or ml > L:
             return None
+        if self._codes is not None and self._codes[0] == L and self._codes[1].device == self.device:
+            return self._codes[1]
         if self.device.type == "cuda":
-            return _ext.hip().str_pack(self.data, self.starts.contiguous(), self.ends.contiguous(), L)
+            codes = _ext.hip().str_pack(self.data, self.starts.contiguous(), self.ends.contiguous(), L)
+            self._codes = (L, codes)
+            return codes
         st, en, buf = self.starts.numpy(), self.ends.numpy(), self.data.numpy()
         ln = en - st
         be = np.zeros(len(st), dtype=np.int64)

@@ -103,6 +103,20 @@ def run_all(args, h, n, cols_of, lit, tile, out):
         t = h.pipe_agg(prog, 1, cols, lit, n, 7, 8, [4, 5, 9, 10, 3, 11], 0, args.max_wg, tile).cpu()
         out.append({"tile": tile, "kernel": "q01_check", "status": int(t[0]), "kept": int(t[1]),
                     "groups": int((t[2:2050] != -(1 << 63)).sum())})
+    if "q01c" in args.which:
+        # Q01 with the string keys read through their kept short codes (what the engine passes: plain int64 columns)
+        ins = [(PL.OP_LEI, 7, 2, I, -1, 10471),
+               (PL.OP_PACK, 8, 0, 1, -1, 11),
+               (PL.OP_SUBF, 9, I, 3, -1, fb(1.0)), (PL.OP_MULF, 9, 5, 9, -1, 0),
+               (PL.OP_ADDF, 10, I, 6, -1, fb(1.0)), (PL.OP_MULF, 10, 9, 10, -1, 0),
+               (PL.OP_CONST, 11, -1, -1, -1, fb(1.0))]
+        prog = torch.tensor(ins, dtype=torch.int64)
+        cols = [col(PL.C_I64, flags.short_codes(1)), col(PL.C_I64, status.short_codes(1)), col(PL.C_I32, ship),
+                col(PL.C_F64, disc), col(PL.C_F64, qty), col(PL.C_F64, price), col(PL.C_F64, tax)]
+        ms = timed(lambda: h.pipe_agg(prog, 1, cols, lit, n, 7, 8, [4, 5, 9, 10, 3, 11], 0, args.max_wg, tile),
+                   args.reps)
+        out.append({"tile": tile, "kernel": "q01_codes_agg", "ms": round(ms, 4), "grows_s": round(n / ms / 1e6, 2),
+                    "gbs": round(n * (4 + 32 + 16) / ms / 1e6, 1)})
     if "q14" in args.which:
         ins = [(PL.OP_GEI, 1, 0, I, -1, 9374), (PL.OP_LTI, 1, 0, I, 1, 9404)]
         prog = torch.tensor(ins, dtype=torch.int64)

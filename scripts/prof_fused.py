@@ -75,7 +75,7 @@ def main():
                 torch.cuda.synchronize()
                 pr.disable()
                 s = io.StringIO()
-                pstats.Stats(pr, stream=s).sort_stats("cumulative").print_stats(30)
+                pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(25)
                 print(s.getvalue()[:6000], flush=True)
 
 

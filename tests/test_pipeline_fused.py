@@ -238,7 +238,7 @@ def test_pipe_kernel_shapes_gpu():
     cols = PL._col_args(gprog, dev)
     lit = torch.zeros(1, dtype=torch.uint8, device=dev)
     pt = torch.tensor(ins, dtype=torch.int64)
-    for tile in (0, 512, 1024, 2048):
+    for tile in (0, 512, 768, 1024, 2048):
         st, kept, k, v = _table_result(h.pipe_agg(pt, 2, cols, lit, n, 5, 6, [4, 7], 0, 0, tile), 2)
         assert st == 0 and kept == int(ref_mask.sum()), tile
         assert torch.equal(k, ref_k), tile
