@@ -689,16 +689,24 @@ __global__ void __launch_bounds__(NTHR) tile_agg_kernel(const PipeArgs a) {
     __syncthreads();                                   // the previous tile's registers are no longer read
     tile_load<RPT>(a, row0, nrow, regs);
     tile_run<RPT>(a, regs, 0, a.nins);
+    // every row's keep flag, key and values read first (all LDS reads in flight together), then the slots
+    bool kp[RPT];
+    long long kk[RPT];
+    double vv[RPT][F];
 #pragma unroll
     for (int i = 0; i < RPT; ++i) {
       const int r = tid + i * NTHR;
-      if (r >= nrow) continue;
-      if (a.keep_reg >= 0 && regs[(long long)a.keep_reg * T + r] == 0) continue;
-      ++kept;
-      const long long key = a.key_reg < 0 ? 0 : (long long)regs[(long long)a.key_reg * T + r];
-      double v[F];
+      kp[i] = r < nrow && (a.keep_reg < 0 || regs[(long long)a.keep_reg * T + r] != 0);
+      kk[i] = a.key_reg < 0 ? 0 : (long long)regs[(long long)a.key_reg * T + r];
 #pragma unroll
-      for (int f = 0; f < F; ++f) v[f] = f < a.nval ? u2f(regs[(long long)a.val_reg[f] * T + r]) : 0.0;
+      for (int f = 0; f < F; ++f) vv[i][f] = f < a.nval ? u2f(regs[(long long)a.val_reg[f] * T + r]) : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      if (!kp[i]) continue;
+      ++kept;
+      const long long key = kk[i];
+      const double (&v)[F] = vv[i];
       bool done = false;
 #pragma unroll
       for (int s = 0; s < KS; ++s) {

@@ -687,9 +687,14 @@ def run_batch(plan: StagePlan, batch: RecordBatch) -> Optional[RecordBatch]:
 
 
 def _to_dev(x, dev):
+    """Host result -> device without a synchronisation (pinned staging, asynchronous copy)."""
     if isinstance(x, tuple):
         return tuple(_to_dev(c, dev) for c in x)
-    return x.to(dev) if x.device != dev else x
+    if x.device == dev:
+        return x
+    if isinstance(x, StringColumn):
+        return x.to(dev)
+    return x.pin_memory().to(dev, non_blocking=True) if dev.type == "cuda" else x.to(dev)
 
 
 def _col_args(prog: Program, dev):

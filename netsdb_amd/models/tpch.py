@@ -27,7 +27,7 @@ import torch
 from ..computations import AggregateComp, JoinComp, ScanSet, SelectionComp, TopKComp, WriteSet
 from ..lambdas import IsIn, KeyTuple, Like, Literal, Select, Values, make_batch_lambda, make_lambda_from_member
 from ..objects.record import PDBObject, RecordBatch
-from ..objects.strings import StringColumn, use_device_strings
+from ..objects.strings import StringColumn, to_host, use_device_strings
 
 # ----------------------------------------------------------------------------------------- schema
 
@@ -468,14 +468,16 @@ def q01(client, db: str, delta_days: int = 90) -> List[dict]:
     if r is None:
         return out
     k1 = _as_list(r.columns["k1"]) if "k1" in r.columns else None
+    names = ("count", "sum_qty", "sum_base_price", "sum_disc_price", "sum_charge", "sum_disc")
+    hv = dict(zip(names, (t.tolist() for t in to_host(*(r.columns[f] for f in names)))))   # one device read
     for i, k in enumerate(_as_list(r.columns["k0"])):
         rf, ls = (k, k1[i]) if k1 is not None else k.split("|")
-        c = float(r.columns["count"][i])
+        c = float(hv["count"][i])
         row = {"l_returnflag": rf, "l_linestatus": ls}
         for f in ("sum_qty", "sum_base_price", "sum_disc_price", "sum_charge"):
-            row[f] = float(r.columns[f][i])
+            row[f] = float(hv[f][i])
         row.update(avg_qty=row["sum_qty"] / c, avg_price=row["sum_base_price"] / c,
-                   avg_disc=float(r.columns["sum_disc"][i]) / c, count_order=int(c))
+                   avg_disc=float(hv["sum_disc"][i]) / c, count_order=int(c))
         out.append(row)
     return sorted(out, key=lambda x: (x["l_returnflag"], x["l_linestatus"]))
 

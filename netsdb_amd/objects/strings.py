@@ -33,6 +33,16 @@ _M1, _M2, _SEED = 0xBF58476D1CE4E5B9, 0x94D049BB133111EB, 0x9E3779B97F4A7C15
 _MASK = (1 << 64) - 1
 
 
+def to_host(*ts: torch.Tensor) -> List[torch.Tensor]:
+    """Host copies of several tensors with ONE synchronisation: device tensors are copied asynchronously (into
+    pinned buffers) and the stream is synchronised once, instead of one blocking read per tensor."""
+    dev = [t for t in ts if t.device.type == "cuda"]
+    out = [t.to("cpu", non_blocking=True) if t.device.type == "cuda" else t for t in ts]
+    if dev:
+        torch.cuda.current_stream(dev[0].device).synchronize()
+    return out
+
+
 def use_device_strings(device) -> bool:
     flag = os.environ.get("NSDB_DEVICE_STRINGS")
     if flag is not None:
@@ -199,7 +209,8 @@ class StringColumn:
         return self.ends - self.starts
 
     def _host(self):
-        return self.data[: self.payload].cpu().numpy(), self.starts.cpu().numpy(), self.ends.cpu().numpy()
+        d, st, en = to_host(self.data[: self.payload], self.starts, self.ends)
+        return d.numpy(), st.numpy(), en.numpy()
 
     def tolist(self) -> List[str]:
         buf, st, en = self._host()
@@ -252,12 +263,13 @@ class StringColumn:
             return self
         if self._off is None and len(self) < self.buf_rows // 2:
             return self.compact().to(device)          # do not move a large shared buffer for a few rows
-        data = self.data.to(device, non_blocking=True)
+        # host sources are staged through pinned memory so the copies stay asynchronous (no stream sync)
+        mv = ((lambda t: t.pin_memory().to(device, non_blocking=True)) if self.device.type == "cpu"
+              and device.type == "cuda" else (lambda t: t.to(device, non_blocking=True)))
+        data = mv(self.data)
         if self._off is not None:
-            return StringColumn(data, self._off.to(device, non_blocking=True), self.payload, self.buf_rows,
-                                self._maxlen)
-        return StringColumn.view(data, self.starts.to(device, non_blocking=True),
-                                 self.ends.to(device, non_blocking=True), self.payload, self.buf_rows, self._maxlen)
+            return StringColumn(data, mv(self._off), self.payload, self.buf_rows, self._maxlen)
+        return StringColumn.view(data, mv(self.starts), mv(self.ends), self.payload, self.buf_rows, self._maxlen)
 
     def compact(self) -> "StringColumn":
         """Own packed buffer holding exactly these rows (one device->host read of the byte total)."""

@@ -173,6 +173,7 @@ class StorageManager:
         if isinstance(s, DenseMatrixSet):
             s.release_storage()
             self.untrack(s)
+        s.__dict__.pop("_merged_runs", None)
         for p in s.pages:
             self.untrack(p)
             if p.location == "device" and p.batch is not None:

@@ -84,6 +84,7 @@ class Page:
         native page pool (LRU -> disk) and drop the in-memory batch."""
         if self.batch is None or self.pins > 0:
             return 0
+        self.set.__dict__.pop("_merged_runs", None)      # kept scan views would hold this page's buffers alive
         if self.location == "device" and not self.dirty:
             # clean: the page's serialised image is already in the pool / page file (write cost 0) -> just drop it
             self.release_regions()
@@ -427,7 +428,16 @@ class UserSet:
                 for p in run:
                     p.pins += 1
                 try:
-                    merged = merge_adjacent_batches([p.batch for p in run], check=False)
+                    # the merged view of an unchanged run is kept: a re-scan costs no per-page work, and what a
+                    # query derives from its columns (a string column's short-code encoding) survives the scan
+                    ident = tuple((id(p.batch), p.gen) for p in run)
+                    cache = self.__dict__.setdefault("_merged_runs", {})
+                    hit = cache.get((i, j))
+                    if hit is not None and hit[0] == ident:
+                        merged = hit[1]
+                    else:
+                        merged = merge_adjacent_batches([p.batch for p in run], check=False)
+                        cache[(i, j)] = (ident, merged)
                     for p in run:
                         self.manager.touch(p)
                     yield merged
