@@ -346,6 +346,9 @@ class QueryEngine:
             fplan = PL.plan_stage(segments[-1], state.comps, st.sink["atom"])
             if fplan is not None:
                 segments[-1] = fplan.prefix
+                # one rank: the launches' few pre-aggregated rows stay on the host, the sink reduces them there
+                # and its result goes back to the device in one asynchronous upload (no device round trips)
+                fplan.host_out = not self.ctx.distributed
 
         def source():
             for b in self._source_batches(st, state):
@@ -383,6 +386,8 @@ class QueryEngine:
                 continue
             r = PL.run_batch(fplan, b)
             if r is not None:
+                if getattr(fplan, "host_out", False) and b.device.type == "cuda":
+                    state.fused_out_device = b.device
                 used = True
                 self.pipeline_stats["fused_batches"] += 1
                 yield r
@@ -747,6 +752,10 @@ class QueryEngine:
             reps, agg = self._reduce_kv(kv, op, combine, group_fn)
         elif not self.ctx.distributed:
             reps, agg = self._reduce_kv(kv, op, combine)
+            dev = state.fused_out_device
+            if dev is not None:
+                state.fused_out_device = None
+                reps, agg = _upload(reps, dev), _upload(agg, dev)
         else:
             # CombinerProcessor -> streaming shuffle by key hash -> AggregationProcessor: every chunk of (key,
             # value) pairs is combined locally before it is sent (CombinedShuffleSink), the shuffle rounds leave
@@ -843,6 +852,10 @@ class QueryEngine:
                 bs = [b for b in grp if b.n]
                 if not bs:
                     continue
+                devs = {b.device for b in bs}
+                if len(devs) > 1:                 # host-resident fused partials beside eager (device) batches
+                    dev = next(d for d in devs if d.type != "cpu")
+                    bs = [b.to(dev) if b.device.type == "cpu" else b for b in bs]
                 keys = column_concat([b.columns["k"] for b in bs])
                 vals = column_concat([b.columns["v"] for b in bs])
                 fused = None if group_fn is not None else K.group_reduce(keys, vals, op)   # relops.hip, or None
@@ -940,6 +953,21 @@ class _JobState:
         self.comps = comps
         self.materialized: Dict[str, List[RecordBatch]] = {}
         self.builds: Dict[str, BuildTable] = {}
+        self.fused_out_device = None     # a fused stage's host-resident partials: the device its result returns to
+
+
+def _upload(x, dev):
+    """A host aggregate result (tensor, StringColumn, tuple / list of them, RecordBatch) -> ``dev`` with pinned,
+    asynchronous copies (no stream synchronisation)."""
+    if isinstance(x, RecordBatch):
+        return RecordBatch({k: _upload(c, dev) for k, c in x.columns.items()}, x.n, x.type)
+    if isinstance(x, tuple):
+        return tuple(_upload(c, dev) for c in x)
+    if isinstance(x, torch.Tensor):
+        return x.pin_memory().to(dev, non_blocking=True) if x.device.type == "cpu" else x
+    if isinstance(x, StringColumn):
+        return x.to(dev)
+    return x
 
 
 __all__ = ["QueryEngine", "JobStats"]

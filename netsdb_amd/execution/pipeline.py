@@ -680,10 +680,12 @@ def run_batch(plan: StagePlan, batch: RecordBatch) -> Optional[RecordBatch]:
     if parts is None:
         plan.disabled = True            # more groups than the kernel's tables hold: this stage runs eagerly
         return None
-    keys, vals = parts                  # host tensors (a few rows): decoded on the host, then one upload each
+    keys, vals = parts                  # host tensors (a few rows): decoded on the host
     plan.stats["fused_batches"] += 1
-    return RecordBatch({plan.kcol: _to_dev(_key_columns(prog, keys), dev),
-                        plan.vcol: _to_dev(_value_column(prog, vals), dev)}, int(keys.numel()))
+    kc, vc = _key_columns(prog, keys), _value_column(prog, vals)
+    if getattr(plan, "host_out", False):
+        return RecordBatch({plan.kcol: kc, plan.vcol: vc}, int(keys.numel()))     # the sink reduces on the host
+    return RecordBatch({plan.kcol: _to_dev(kc, dev), plan.vcol: _to_dev(vc, dev)}, int(keys.numel()))
 
 
 def _to_dev(x, dev):

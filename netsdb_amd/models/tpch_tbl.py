@@ -137,11 +137,16 @@ def parse_tbl(buf: torch.Tensor, table: str, device=None) -> RecordBatch:
     fields = list(typ.fields().items())
     starts, ends = _field_bounds(buf, len(fields))
     n = starts.shape[0]
+    nb = int(buf.numel())
+    sbuf = buf                                 # the string kernels read whole words: a padded copy of the chunk
+    if StringColumn._alloc_size(nb) != nb:
+        sbuf = torch.zeros(StringColumn._alloc_size(nb), dtype=torch.uint8, device=buf.device)
+        sbuf[:nb] = buf
     cols = {}
     for j, (f, ft) in enumerate(fields):
         s, e = starts[:, j].contiguous(), ends[:, j].contiguous()
         if ft is str:
-            view = StringColumn.view(buf, s, e, int(buf.numel()), max(1, n))
+            view = StringColumn.view(sbuf, s, e, nb, max(1, n))
             col = view.compact()
             cols[f] = col if use_device_strings(device or buf.device) else col.tolist()
         else:
