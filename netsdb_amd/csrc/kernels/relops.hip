@@ -917,75 +917,42 @@ struct JSlot {
 // The row that claims a slot (CAS) is its key's rank 0 and stores itself as the payload; each further row of
 // the key takes the next rank with one atomic add on the slot's count of EXTRA rows (a unique-key build does one
 // atomic per row). *ndup counts the rows of rank > 0 (one add per wave): zero means the CSR pass is skipped.
-// Each thread takes kJIns rows at once and issues their first-slot claims together (returning CASes straight from
-// kEmpty, no load in front: the table is >= 2 slots per row, so the first slot is usually free): the atomics'
-// memory-side round trips overlap instead of running one dependent load + CAS per row; only a row whose first
-// slot holds another key walks the probe chain. row_slot is written only for rows of rank > 0 (the CSR pass reads
-// it for those alone).
-constexpr int kJIns = 4;
-
-__device__ __forceinline__ u64 cas_u64(u64* p, u64 expect, u64 val) {
-  u64 e = expect;
-  __hip_atomic_compare_exchange_strong(p, &e, val, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return e;   // the value found (== expect: claimed)
-}
-
 __global__ __launch_bounds__(256) void join_insert_kernel(const u64* __restrict__ keys, i64 n, JSlot* tab, u64 mask,
                                                           int* __restrict__ row_slot, unsigned* __restrict__ row_rank,
                                                           unsigned long long* ndup) {
-  const i64 stride = (i64)gridDim.x * blockDim.x * kJIns;
-  for (i64 base = (i64)blockIdx.x * blockDim.x * kJIns + threadIdx.x; base < n; base += stride) {
-    u64 k[kJIns], s[kJIns], got[kJIns];
-    bool valid[kJIns];
-#pragma unroll
-    for (int j = 0; j < kJIns; ++j) {
-      const i64 i = base + (i64)j * blockDim.x;
-      valid[j] = i < n;
-      k[j] = valid[j] ? keys[i] : kEmpty;
-      s[j] = k[j] == kEmpty ? mask + 1 : (mix64(k[j]) & mask);
-    }
-#pragma unroll
-    for (int j = 0; j < kJIns; ++j)   // independent first-slot claims, all in flight together
-      got[j] = (valid[j] && k[j] != kEmpty) ? cas_u64(&tab[s[j]].key, kEmpty, k[j]) : kEmpty;
-    unsigned rs[kJIns];
-#pragma unroll
-    for (int j = 0; j < kJIns; ++j) {
-      rs[j] = 0;
-      if (!valid[j]) continue;
-      const i64 i = base + (i64)j * blockDim.x;
-      bool claimed = false;
-      if (k[j] != kEmpty) {
-        claimed = got[j] == kEmpty;
-        if (!claimed && got[j] != k[j]) {   // another key holds the first slot: walk on
-          u64 q = (s[j] + 1) & mask;
-          for (;;) {
-            const u64 cur = cas_u64(&tab[q].key, kEmpty, k[j]);
-            if (cur == kEmpty) {
-              claimed = true;
-              break;
-            }
-            if (cur == k[j]) break;
-            q = (q + 1) & mask;
+  for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) {
+    const u64 k = keys[i];
+    u64 s;
+    bool claimed = false;
+    if (k == kEmpty) {
+      s = mask + 1;   // the kEmpty key's own slot: every row counts as an extra, ranks from 1 (fixed below)
+    } else {
+      s = mix64(k) & mask;
+      for (;;) {   // the table has >= 2 slots per build row: the key or an empty slot is always met
+        u64 cur = __hip_atomic_load(&tab[s].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == kEmpty) {
+          if (__hip_atomic_compare_exchange_strong(&tab[s].key, &cur, k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT)) {
+            claimed = true;
+            break;
           }
-          s[j] = q;
         }
+        if (cur == k) break;
+        s = (s + 1) & mask;
       }
-      unsigned r = 0;
-      if (claimed) {
-        tab[s[j]].pay = (unsigned)i;
-      } else {   // a further row of a key (or any row of the kEmpty key's own slot: ranks from 0)
-        r = __hip_atomic_fetch_add(&tab[s[j]].cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + (k[j] == kEmpty ? 0u : 1u);
-        if (r == 0) tab[s[j]].pay = (unsigned)i;   // the kEmpty slot's first row
-      }
-      row_rank[i] = r;
-      if (r != 0) row_slot[i] = (int)s[j];
-      rs[j] = r;
     }
-    unsigned nd = 0;
-#pragma unroll
-    for (int j = 0; j < kJIns; ++j) nd += __popcll(__ballot(rs[j] != 0));
-    if (nd != 0 && (threadIdx.x & 63) == (unsigned)(__ffsll((long long)__ballot(1)) - 1))
-      __hip_atomic_fetch_add(ndup, (unsigned long long)nd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    row_slot[i] = (int)s;
+    unsigned r = 0;
+    if (claimed) {
+      tab[s].pay = (unsigned)i;
+    } else {
+      r = __hip_atomic_fetch_add(&tab[s].cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + (k == kEmpty ? 0u : 1u);
+      if (r == 0) tab[s].pay = (unsigned)i;   // the kEmpty slot's first row
+    }
+    row_rank[i] = r;
+    const u64 dups = __ballot(r != 0);
+    if (dups != 0 && (threadIdx.x & 63) == (unsigned)(__ffsll((long long)__ballot(1)) - 1))
+      __hip_atomic_fetch_add(ndup, (unsigned long long)__popcll(dups), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -1370,7 +1337,7 @@ int nsdb_join_insert(const void* keys, long long n, void* tab, long long cap, in
                      unsigned long long* ndup, hipStream_t st) {
   if (n <= 0) return 0;
   if (cap <= 0 || (cap & (cap - 1)) != 0 || cap < 2 * n || cap >= (1LL << 31)) return (int)hipErrorInvalidValue;
-  const unsigned g = (unsigned)std::min<long long>(4096, (n + 256 * kJIns - 1) / (256 * kJIns));
+  const unsigned g = (unsigned)std::min<long long>(4096, (n + 255) / 256);
   hipLaunchKernelGGL(join_insert_kernel, dim3(g), dim3(256), 0, st, (const u64*)keys, n, (JSlot*)tab, (u64)(cap - 1),
                      row_slot, row_rank, ndup);
   return (int)hipGetLastError();
