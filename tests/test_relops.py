@@ -475,17 +475,16 @@ def test_chunked_aggregation_matches_unchunked(monkeypatch):
 
 
 @pytest.mark.gpu
-def test_partitioned_join_build_matches_global_insert():
-    """Builds of >= 1 M rows take the XCD-local path (each XCD inserts the rows of its table region with L2
-    atomics). With repeated keys, kEmpty-marker rows and a crafted cluster of keys sharing one home slot just before
-    a region's end (so rows run off their region and take the leftover device-scope insert), every (build, probe)
-    pair equals the host join's."""
+def test_large_join_build_with_clusters_matches_host():
+    """A build of >= 1 M rows with repeated keys, kEmpty-marker rows and a crafted cluster of 3000 keys sharing one
+    home slot (a 3000-slot probe chain that crosses an eighth of the table): every (build, probe) pair equals the
+    host join's."""
     g = torch.Generator(device=DEV).manual_seed(7)
     n = 1_200_000
     build = torch.randint(0, 500_000, (n,), device=DEV, generator=g) * 7 + 3
     build[::50_000] = torch.iinfo(torch.int64).min
     cap = 1 << 22                                   # pow2_at_least(2 n): the table the binding sizes
-    home = cap // 8 - 5                             # five slots before the end of region 0
+    home = cap // 8 - 5
     crafted = [_inv_mix64((j << 22) | home) for j in range(1, 3001)]
     crafted = torch.tensor([c - (1 << 64) if c >= 1 << 63 else c for c in crafted], dtype=torch.int64, device=DEV)
     assert all((_mix64(int(c) & _M64) & (cap - 1)) == home for c in crafted[:5].tolist())
