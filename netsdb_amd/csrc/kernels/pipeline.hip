@@ -36,6 +36,8 @@ constexpr int GCAP = 2048;             // global table slots (power of two)
 constexpr int NREG_SMALL = 8;          // the 8-register x 4-row shape
 constexpr long long EMPTY = (long long)0x8000000000000000ULL;
 constexpr int IMM_REG = -2;            // operand register meaning "the instruction's immediate"
+// tile-mode instruction flags (Ins.pad; the operand fields are then byte offsets of T-row register vectors)
+constexpr int TF_AIMM = 1, TF_ANONE = 2, TF_BIMM = 4, TF_BNONE = 8, TF_C = 16;
 
 enum Op : int {
   OP_NOP = 0, OP_CONST, OP_ADDF, OP_SUBF, OP_MULF, OP_DIVF, OP_ADDI, OP_SUBI, OP_MULI, OP_I2F,
@@ -65,7 +67,8 @@ struct PipeArgs {
   long long n;
   int nins_a, nins, ncol, keep_reg, key_reg, nval, agg_op, nreg;
   int val_reg[FMAX];
-  int tile, lds_bytes;           // tile kernels: rows per tile, dynamic LDS bytes
+  int tile, lds_bytes;           // tile / hybrid kernels: rows per tile, dynamic LDS bytes
+  int kmode, pad2;               // 0 register kernels, 1 LDS-tile kernels, 2 hybrid (LDS-DMA columns, VGPR registers)
   unsigned long long* table;     // [2 + GCAP + GCAP * FMAX]: status (overflow, kept rows), keys, values (f64 bits)
 };
 
@@ -140,6 +143,88 @@ __device__ __forceinline__ void load_cols(const PipeArgs& a, const long long (&r
         const u64 s = R[j][c];
         R[j][c] = (s << 24) | (u64)min(y[c][j] - (unsigned)s, 0xFFFFFFu);
       }
+    }
+  }
+}
+
+extern __shared__ __attribute__((aligned(16))) unsigned char tile_smem[];
+
+__device__ __forceinline__ int kind_width(int kind) {
+  return (kind == C_F64 || kind == C_I64) ? 8 : ((kind == C_I32 || kind == C_F32) ? 4 : (kind == C_U8 ? 1 : 8));
+}
+
+// `bytes` of the tile image from g to LDS l, wave `wave`'s share of the wave-instructions. A full tile whose image
+// is a multiple of 1 KiB uses 16-B DMA lanes; otherwise 4-byte elements use 4-B DMA lanes over exactly `valid` bytes
+// of a bounds-checked buffer resource (lanes past the column's end read zeros, never out of the column), and byte
+// columns are copied by the threads (a 1-byte DMA lane writes a whole LDS dword).
+__device__ __forceinline__ void dma_tile(const void* g, long long valid, unsigned char* l, int bytes, int w, bool full,
+                                         int wave, int lane) {
+  constexpr int NW = NTHR / 64;
+  const int nv = (int)(valid < (long long)bytes ? valid : (long long)bytes);
+  if (w < 4 && !(full && (bytes & 1023) == 0)) {
+    const unsigned char* src = reinterpret_cast<const unsigned char*>(g);
+    for (int i = wave * 64 + lane; i < nv; i += NTHR) l[i] = src[i];
+    return;
+  }
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(g), (short)0, nv, 0x00020000);
+  if (full && (bytes & 1023) == 0) {
+    for (int ch = wave; ch < (bytes >> 10); ch += NW)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (nsdb::lds_void*)(l + (ch << 10)), 16, (ch << 10) + lane * 16, 0, 0, 0);
+  } else {
+    for (int ch = wave; ch < (bytes >> 8); ch += NW)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (nsdb::lds_void*)(l + (ch << 8)), 4, (ch << 8) + lane * 4, 0, 0, 0);
+  }
+}
+
+// Hybrid kernels (HYB): the block's NTHR * ROWS rows of an iteration are first copied HBM -> LDS by LDS-DMA (every
+// column at its native width: many KB in flight per workgroup, no VGPRs), then each thread moves its rows' values
+// LDS -> its VGPR register file (one ds_read per column and row) and the register interpreter runs as usual. The
+// interpreter's operands never touch LDS, so LDS carries each column byte once.
+template <int NR, int ROWS>
+__device__ __forceinline__ void hyb_dma(const PipeArgs& a, long long row0, long long nrow) {
+  constexpr int T = NTHR * ROWS;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const bool full = nrow == T;
+  for (int c = 0; c < a.ncol; ++c) {
+    const Col& C = a.col[c];
+    if (C.kind == C_SCODE || C.kind == C_SREF) {
+      dma_tile(C.st + row0, nrow * 8, tile_smem + C.raw_off, T * 8, 8, full, wave, lane);
+      if (!C.contig) dma_tile(C.en + row0, nrow * 8, tile_smem + C.aux_off, T * 8, 8, full, wave, lane);
+    } else {
+      const int w = kind_width(C.kind);
+      dma_tile(reinterpret_cast<const unsigned char*>(C.p) + row0 * w, nrow * w, tile_smem + C.raw_off, T * w, w, full,
+               wave, lane);
+    }
+  }
+}
+
+template <int NR, int ROWS>
+__device__ __forceinline__ void hyb_load(const PipeArgs& a, long long row0, long long nrow, const bool (&m)[ROWS],
+                                         typename RF<NR>::vec (&R)[ROWS]) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int c = 0; c < (NR < MAXCOL ? NR : MAXCOL); ++c) {
+    if (c >= a.ncol) break;
+    const Col& C = a.col[c];
+    const unsigned char* raw = tile_smem + C.raw_off;
+    const int kind = C.kind;
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      const int r = j * NTHR + tid;
+      u64 v = 0;
+      if (kind == C_F64 || kind == C_I64) v = reinterpret_cast<const u64*>(raw)[r];
+      else if (kind == C_I32) v = (u64)(long long)reinterpret_cast<const int*>(raw)[r];
+      else if (kind == C_F32) v = f2u((double)reinterpret_cast<const float*>(raw)[r]);
+      else if (kind == C_U8) v = (u64)raw[r];
+      else {
+        const long long st = reinterpret_cast<const long long*>(raw)[r];
+        const long long en = C.contig ? (r + 1 < nrow ? reinterpret_cast<const long long*>(raw)[r + 1]
+                                                      : (m[j] ? C.en[row0 + r] : st))
+                                      : reinterpret_cast<const long long*>(tile_smem + C.aux_off)[r];
+        v = kind == C_SCODE ? (m[j] ? short_code(C.dat, st, en - st, C.L) : 0ull)
+                            : (((u64)st << 24) | (u64)min(en - st, 0xFFFFFFll));
+      }
+      R[j][c] = m[j] ? v : 0ull;
     }
   }
 }
@@ -291,7 +376,7 @@ __device__ __forceinline__ double wave_reduce(double v, int op) {
   return v;
 }
 
-template <int F, int NR, int ROWS>
+template <int F, int NR, int ROWS, bool HYB>
 __global__ void __launch_bounds__(NTHR) pipe_agg_kernel(const PipeArgs a) {
   __shared__ long long tk[CAP];
   __shared__ double tv[CAP * FMAX];
@@ -331,7 +416,15 @@ __global__ void __launch_bounds__(NTHR) pipe_agg_kernel(const PipeArgs a) {
       row[j] = base + (long long)j * NTHR + tid;
       inr[j] = row[j] < a.n;
     }
-    load_cols<false, NR, ROWS>(a, row, inr, R);              // the predicate's ("early") columns
+    if (HYB) {                                                 // the block's rows: HBM -> LDS -> registers
+      const long long nrow = min((long long)NTHR * ROWS, a.n - base);
+      __syncthreads();                                         // the previous rows' LDS reads are done
+      hyb_dma<NR, ROWS>(a, base, nrow);
+      __syncthreads();                                         // every wave's DMA has landed
+      hyb_load<NR, ROWS>(a, base, nrow, inr, R);
+    } else {
+      load_cols<false, NR, ROWS>(a, row, inr, R);              // the predicate's ("early") columns
+    }
     run<NR, ROWS>(a, R, 0, a.nins_a);
     bool any = false;
 #pragma unroll
@@ -341,7 +434,7 @@ __global__ void __launch_bounds__(NTHR) pipe_agg_kernel(const PipeArgs a) {
       kept += keep[j] ? 1u : 0u;
     }
     if (!__builtin_amdgcn_ballot_w64(any)) continue;           // no kept row in this wave
-    load_cols<true, NR, ROWS>(a, row, keep, R);               // late columns: the kept rows only
+    if (!HYB) load_cols<true, NR, ROWS>(a, row, keep, R);     // late columns: the kept rows only
     run<NR, ROWS>(a, R, a.nins_a, a.nins);
 #pragma unroll
     for (int j = 0; j < ROWS; ++j) {
@@ -425,7 +518,7 @@ __global__ void __launch_bounds__(NTHR) pipe_init_kernel(unsigned long long* tab
 // Filter only: the predicate program over every row, the keep flag written as one byte per row (the FILTER of a
 // scan-filter stage that feeds a join / materialisation: no comparison column, literal column or AND of two masks is
 // materialised; the engine turns the mask into the stage's row selection). The binding marks every column early.
-template <int NR, int ROWS>
+template <int NR, int ROWS, bool HYB>
 __global__ void __launch_bounds__(NTHR) pipe_mask_kernel(const PipeArgs a, unsigned char* __restrict__ mask) {
   typename RF<NR>::vec R[ROWS];
 #pragma unroll
@@ -440,7 +533,15 @@ __global__ void __launch_bounds__(NTHR) pipe_mask_kernel(const PipeArgs a, unsig
       row[j] = base + (long long)j * NTHR + tid;
       inr[j] = row[j] < a.n;
     }
-    load_cols<false, NR, ROWS>(a, row, inr, R);
+    if (HYB) {
+      const long long nrow = min((long long)NTHR * ROWS, a.n - base);
+      __syncthreads();
+      hyb_dma<NR, ROWS>(a, base, nrow);
+      __syncthreads();
+      hyb_load<NR, ROWS>(a, base, nrow, inr, R);
+    } else {
+      load_cols<false, NR, ROWS>(a, row, inr, R);
+    }
     run<NR, ROWS>(a, R, 0, a.nins);
 #pragma unroll
     for (int j = 0; j < ROWS; ++j)
@@ -458,35 +559,6 @@ __global__ void __launch_bounds__(NTHR) pipe_mask_kernel(const PipeArgs a, unsig
 // and it needs no indirect VGPR addressing. Narrow columns (i32 / f32 / u8) and strings are widened into their
 // register by the thread that owns the row (string codes gather their bytes from HBM). Several workgroups per CU
 // overlap one tile's DMA with another's interpretation.
-extern __shared__ __attribute__((aligned(16))) unsigned char tile_smem[];
-
-__device__ __forceinline__ int kind_width(int kind) {
-  return (kind == C_F64 || kind == C_I64) ? 8 : ((kind == C_I32 || kind == C_F32) ? 4 : (kind == C_U8 ? 1 : 8));
-}
-
-// `bytes` of the tile image from g to LDS l, wave `wave`'s share of the wave-instructions. A full tile whose image
-// is a multiple of 1 KiB uses 16-B DMA lanes; otherwise 4-byte elements use 4-B DMA lanes over exactly `valid` bytes
-// of a bounds-checked buffer resource (lanes past the column's end read zeros, never out of the column), and byte
-// columns are copied by the threads (a 1-byte DMA lane writes a whole LDS dword).
-__device__ __forceinline__ void dma_tile(const void* g, long long valid, unsigned char* l, int bytes, int w, bool full,
-                                         int wave, int lane) {
-  constexpr int NW = NTHR / 64;
-  const int nv = (int)(valid < (long long)bytes ? valid : (long long)bytes);
-  if (w < 4 && !(full && (bytes & 1023) == 0)) {
-    const unsigned char* src = reinterpret_cast<const unsigned char*>(g);
-    for (int i = wave * 64 + lane; i < nv; i += NTHR) l[i] = src[i];
-    return;
-  }
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(g), (short)0, nv, 0x00020000);
-  if (full && (bytes & 1023) == 0) {
-    for (int ch = wave; ch < (bytes >> 10); ch += NW)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (nsdb::lds_void*)(l + (ch << 10)), 16, (ch << 10) + lane * 16, 0, 0, 0);
-  } else {
-    for (int ch = wave; ch < (bytes >> 8); ch += NW)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (nsdb::lds_void*)(l + (ch << 8)), 4, (ch << 8) + lane * 4, 0, 0, 0);
-  }
-}
-
 // Every column's tile (rows [row0, row0 + T)) into its LDS image, then the widening into 8-byte registers for the
 // rows this thread owns (after the barrier that makes every wave's DMA visible). A narrow column (i32 / f32 / u8) is
 // DMA'd into the top of its own register vector and widened in place: every thread first reads its rows' narrow
@@ -566,27 +638,28 @@ template <int RPT>
 __device__ __forceinline__ void tile_run(const PipeArgs& a, u64* regs, int lo, int hi) {
   const int T = NTHR * RPT, tid = threadIdx.x;
   if (lo >= hi) return;
-  Ins cur = a.ins[lo];
+  // tile mode: the binding pre-decodes every operand into a byte offset of its T-row vector and a flag word
+  // (TF_*), so an instruction costs one scalar load of its record, its flag tests and the dispatch
+  const unsigned char* base = reinterpret_cast<const unsigned char*>(regs) + tid * 8;
+  (void)T;
   for (int pc = lo; pc < hi; ++pc) {
-    const Ins nxt = a.ins[pc + 1];
-    const int op = cur.op, ia = cur.a, ib = cur.b, ic = cur.c;
+    const Ins cur = a.ins[pc];
+    const int op = cur.op, fl = cur.pad;
     const long long imm = cur.imm;
     u64 x[RPT], y[RPT], z[RPT];
-    if (ia >= 0) {
-      const u64* A = regs + (long long)ia * T + tid;
+    if (fl & (TF_AIMM | TF_ANONE)) {
 #pragma unroll
-      for (int i = 0; i < RPT; ++i) x[i] = A[i * NTHR];
+      for (int i = 0; i < RPT; ++i) x[i] = (fl & TF_AIMM) ? (u64)imm : 0ull;
     } else {
 #pragma unroll
-      for (int i = 0; i < RPT; ++i) x[i] = ia == IMM_REG ? (u64)imm : 0ull;
+      for (int i = 0; i < RPT; ++i) x[i] = *reinterpret_cast<const u64*>(base + cur.a + i * NTHR * 8);
     }
-    if (ib >= 0) {
-      const u64* B = regs + (long long)ib * T + tid;
+    if (fl & (TF_BIMM | TF_BNONE)) {
 #pragma unroll
-      for (int i = 0; i < RPT; ++i) y[i] = B[i * NTHR];
+      for (int i = 0; i < RPT; ++i) y[i] = (fl & TF_BIMM) ? (u64)imm : 0ull;
     } else {
 #pragma unroll
-      for (int i = 0; i < RPT; ++i) y[i] = ib == IMM_REG ? (u64)imm : 0ull;
+      for (int i = 0; i < RPT; ++i) y[i] = *reinterpret_cast<const u64*>(base + cur.b + i * NTHR * 8);
     }
     switch (op) {
 #define NSDB_EACH(E)                                          \
@@ -623,16 +696,15 @@ __device__ __forceinline__ void tile_run(const PipeArgs& a, u64* regs, int lo, i
       case OP_OR: NSDB_EACH((u64)((x[j] != 0) | (y[j] != 0)))
       case OP_NOT: NSDB_EACH((u64)(x[j] == 0))
       case OP_PACK: NSDB_EACH((x[j] << (imm & 63)) | y[j])
-      case OP_SEL: {
-        const u64* S = regs + (long long)imm * T + tid;
+      case OP_SEL: {                                   // imm: the byte offset of the "else" register
 #pragma unroll
-        for (int j = 0; j < RPT; ++j) z[j] = x[j] ? y[j] : S[j * NTHR];
+        for (int j = 0; j < RPT; ++j) z[j] = x[j] ? y[j] : *reinterpret_cast<const u64*>(base + imm + j * NTHR * 8);
         break;
       }
       case OP_SEQ:
       case OP_SPRE:
-      case OP_SSUF: {
-        const unsigned char* d = a.col[ib].dat;
+      case OP_SSUF: {                                  // b: the column whose bytes x refers to
+        const unsigned char* d = a.col[cur.b].dat;
         const int mode = op == OP_SEQ ? 0 : (op == OP_SPRE ? 1 : 2);
 #pragma unroll
         for (int j = 0; j < RPT; ++j) z[j] = str_match(d, x[j], a.lit, imm, mode) ? 1ull : 0ull;
@@ -643,15 +715,13 @@ __device__ __forceinline__ void tile_run(const PipeArgs& a, u64* regs, int lo, i
         for (int j = 0; j < RPT; ++j) z[j] = 0;
 #undef NSDB_EACH
     }
-    if (ic >= 0) {
-      const u64* C = regs + (long long)ic * T + tid;
+    if (fl & TF_C) {
 #pragma unroll
-      for (int j = 0; j < RPT; ++j) z[j] = (z[j] != 0 && C[j * NTHR] != 0) ? 1ull : 0ull;
+      for (int j = 0; j < RPT; ++j)
+        z[j] = (z[j] != 0 && *reinterpret_cast<const u64*>(base + cur.c + j * NTHR * 8) != 0) ? 1ull : 0ull;
     }
-    u64* D = regs + (long long)cur.dst * T + tid;
 #pragma unroll
-    for (int j = 0; j < RPT; ++j) D[j * NTHR] = z[j];
-    cur = nxt;
+    for (int j = 0; j < RPT; ++j) *reinterpret_cast<u64*>(const_cast<unsigned char*>(base) + cur.dst + j * NTHR * 8) = z[j];
   }
 }
 
@@ -823,10 +893,22 @@ void launch_tile_mask(const PipeArgs& a, unsigned char* mask, int grid, hipStrea
 
 template <int F>
 void launch_agg(const PipeArgs& a, int grid, hipStream_t st) {
-  if (a.nreg <= NREG_SMALL)
-    hipLaunchKernelGGL((pipe_agg_kernel<F, NREG_SMALL, 4>), dim3(grid), dim3(NTHR), 0, st, a);
-  else
-    hipLaunchKernelGGL((pipe_agg_kernel<F, NREG, 2>), dim3(grid), dim3(NTHR), 0, st, a);
+  auto go = [&](auto kern) {
+    if (a.lds_bytes > 0)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                a.lds_bytes);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(NTHR), a.lds_bytes, st, a);
+  };
+  if (a.kmode == 2) {
+    if (a.nreg <= NREG_SMALL)
+      go(pipe_agg_kernel<F, NREG_SMALL, 4, true>);
+    else
+      go(pipe_agg_kernel<F, NREG, 2, true>);
+  } else if (a.nreg <= NREG_SMALL) {
+    go(pipe_agg_kernel<F, NREG_SMALL, 4, false>);
+  } else {
+    go(pipe_agg_kernel<F, NREG, 2, false>);
+  }
 }
 
 }  // namespace nsdb_pipe
@@ -856,10 +938,11 @@ int nsdb_pipe_agg(const void* args, int grid, hipStream_t st) {
   if (a.nins > nsdb_pipe::MAXINS || a.ncol > nsdb_pipe::MAXCOL || a.nval > nsdb_pipe::FMAX || a.nins_a > a.nins ||
       a.table == nullptr || a.nreg < 1 || a.nreg > nsdb_pipe::NREG)
     return -2;
-  if (a.tile != 0 && a.tile != 512 && a.tile != 768 && a.tile != 1024 && a.tile != 2048) return -3;
+  if (a.kmode == 1 && a.tile != 512 && a.tile != 768 && a.tile != 1024 && a.tile != 2048) return -3;
+  if (a.kmode == 2 && a.tile != nsdb_pipe::NTHR * (a.nreg <= nsdb_pipe::NREG_SMALL ? 4 : 2)) return -3;
   hipLaunchKernelGGL(nsdb_pipe::pipe_init_kernel, dim3(nsdb_pipe::GCAP / nsdb_pipe::NTHR), dim3(nsdb_pipe::NTHR), 0, st,
                      a.table, a.agg_op);
-  if (a.tile) {
+  if (a.kmode == 1) {
     if (a.nval <= 2)
       nsdb_pipe::launch_tile_agg<2>(a, grid, st);
     else if (a.nval <= 4)
@@ -884,15 +967,24 @@ int nsdb_pipe_mask(const void* args, unsigned char* mask, int grid, hipStream_t 
   if (grid <= 0) return -1;
   const nsdb_pipe::PipeArgs& a = *reinterpret_cast<const nsdb_pipe::PipeArgs*>(args);
   if (a.nins > nsdb_pipe::MAXINS || a.ncol > nsdb_pipe::MAXCOL || a.nreg < 1 || a.nreg > nsdb_pipe::NREG) return -2;
-  if (a.tile != 0 && a.tile != 512 && a.tile != 768 && a.tile != 1024 && a.tile != 2048) return -3;
-  if (a.tile)
+  if (a.kmode == 1 && a.tile != 512 && a.tile != 768 && a.tile != 1024 && a.tile != 2048) return -3;
+  if (a.kmode == 2 && a.tile != nsdb_pipe::NTHR * (a.nreg <= nsdb_pipe::NREG_SMALL ? 4 : 2)) return -3;
+  auto go = [&](auto kern) {
+    if (a.lds_bytes > 0)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                a.lds_bytes);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(nsdb_pipe::NTHR), a.lds_bytes, st, a, mask);
+  };
+  if (a.kmode == 1)
     nsdb_pipe::launch_tile_mask(a, mask, grid, st);
+  else if (a.kmode == 2 && a.nreg <= nsdb_pipe::NREG_SMALL)
+    go(nsdb_pipe::pipe_mask_kernel<nsdb_pipe::NREG_SMALL, 4, true>);
+  else if (a.kmode == 2)
+    go(nsdb_pipe::pipe_mask_kernel<nsdb_pipe::NREG, 2, true>);
   else if (a.nreg <= nsdb_pipe::NREG_SMALL)
-    hipLaunchKernelGGL((nsdb_pipe::pipe_mask_kernel<nsdb_pipe::NREG_SMALL, 4>), dim3(grid), dim3(nsdb_pipe::NTHR), 0,
-                       st, a, mask);
+    go(nsdb_pipe::pipe_mask_kernel<nsdb_pipe::NREG_SMALL, 4, false>);
   else
-    hipLaunchKernelGGL((nsdb_pipe::pipe_mask_kernel<nsdb_pipe::NREG, 2>), dim3(grid), dim3(nsdb_pipe::NTHR), 0, st, a,
-                       mask);
+    go(nsdb_pipe::pipe_mask_kernel<nsdb_pipe::NREG, 2, false>);
   return (int)hipGetLastError();
 }
 

@@ -43,6 +43,7 @@ struct PipeArgs {
   int nins_a, nins, ncol, keep_reg, key_reg, nval, agg_op, nreg;
   int val_reg[FMAX];
   int tile, lds_bytes;
+  int kmode, pad2;
   unsigned long long* table;
 };
 
@@ -180,16 +181,68 @@ int tile_bytes(PipeArgs& a, int T) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// Tile kernels take pre-decoded instructions: every register operand as the byte offset of its T-row vector in
+// LDS, immediates / absent operands as flags (pipeline.hip TF_*), the select's register as an offset too.
+void predecode_tile(PipeArgs& a) {
+  const long long T8 = (long long)a.tile * 8;
+  for (int i = 0; i < a.nins; ++i) {
+    Ins& I = a.ins[i];
+    const bool str = I.op == OP_SEQ || I.op == OP_SPRE || I.op == OP_SSUF;
+    int fl = 0;
+    if (I.a == -2) fl |= 1; else if (I.a < 0) fl |= 2; else I.a = (int)(I.a * T8);
+    if (str) fl |= 8;                                  // b: the column index of the bytes, not a register
+    else if (I.b == -2) fl |= 4; else if (I.b < 0) fl |= 8; else I.b = (int)(I.b * T8);
+    if (I.c >= 0) {
+      fl |= 16;
+      I.c = (int)(I.c * T8);
+    }
+    if (I.op == OP_SEL) I.imm = I.imm * T8;
+    I.dst = (int)(I.dst * T8);
+    I.pad = fl;
+  }
+}
+
+// Hybrid kernels: the block's NTHR * ROWS rows of every column DMA'd at native width (string ends only when they are
+// not the next row's start); registers stay in VGPRs. Returns the dynamic LDS bytes.
+int hyb_bytes(PipeArgs& a, int T) {
+  long long off = 0;
+  for (int c = 0; c < a.ncol; ++c) {
+    Col& C = a.col[c];
+    const int w = (C.kind == C_I32 || C.kind == C_F32) ? 4 : (C.kind == C_U8 ? 1 : 8);
+    C.raw_off = (int)off;
+    off += ((long long)T * w + 15) / 16 * 16;
+    C.aux_off = 0;
+    if ((C.kind == C_SCODE || C.kind == C_SREF) && !C.contig) {
+      C.aux_off = (int)off;
+      off += (long long)T * 8;
+    }
+  }
+  return (int)off;
+}
+
 // Pick the tile kernels' tile size (0: the register kernels): the largest tile whose LDS lets several workgroups
 // share a CU, every column 16-byte aligned (the DMA's 16-byte lanes). `force` >= 0 overrides (0 = register kernels).
-void choose_tile(PipeArgs& a, int static_bytes, int64_t force) {
+// mode: -1 hybrid (the default), -2 LDS-tile auto, 0 register kernels, > 0 LDS-tile kernels of that tile size.
+void choose_tile(PipeArgs& a, int static_bytes, int64_t force, int reg_static_bytes) {
   a.tile = 0;
   a.lds_bytes = 0;
+  a.kmode = 0;
   if (force == 0) return;
   for (int c = 0; c < a.ncol; ++c) {
     const Col& C = a.col[c];
     if ((C.kind == C_SCODE || C.kind == C_SREF) ? !(aligned16(C.st) && (C.contig || aligned16(C.en))) : !aligned16(C.p))
       return;
+  }
+  if (force == -1) {
+    const int T = 256 * (a.nreg <= sizes(9) ? 4 : 2);
+    const int b = hyb_bytes(a, T);
+    if ((long long)(b + reg_static_bytes) * 2 <= 160 * 1024) {
+      a.tile = T;
+      a.lds_bytes = b;
+      a.kmode = 2;
+      for (int c = 0; c < a.ncol; ++c) a.col[c].late = 0;   // every column arrives with the block's DMA
+    }
+    return;
   }
   const int LDS = 160 * 1024;
   // (tile, workgroups per CU): three workgroups per CU overlap one's DMA with the others' work; then the larger tile
@@ -200,6 +253,7 @@ void choose_tile(PipeArgs& a, int static_bytes, int64_t force) {
     if ((long long)(b + static_bytes) * tc[1] <= LDS) {
       a.tile = tc[0];
       a.lds_bytes = b;
+      a.kmode = 1;
       return;
     }
   }
@@ -213,7 +267,8 @@ torch::Tensor pipe_agg(torch::Tensor prog, int64_t nins_a, ColList cols, torch::
   PipeArgs a;
   fill_args(a, prog, nins_a, cols, lit, n, keep_reg, key_reg, val_regs, agg_op);
   const int F = a.nval <= 2 ? 2 : (a.nval <= 4 ? 4 : (a.nval <= 6 ? 6 : FMAX));
-  choose_tile(a, CAP * (8 + 8 * F) + 16, tile);
+  choose_tile(a, CAP * (8 + 8 * F) + 16, tile, CAP * (8 + 8 * FMAX) + 16);
+  if (a.kmode == 1) predecode_tile(a);
   // enough workgroups to fill 256 CUs several times over, each still looping over a few tiles / row blocks
   const long long per = a.tile ? (long long)a.tile : (long long)NTHR * ROWS * 4;
   const int nwg = (int)std::max<long long>(1, std::min<long long>(max_wg > 0 ? max_wg : 2048, (n + per - 1) / per));
@@ -230,7 +285,8 @@ torch::Tensor pipe_mask(torch::Tensor prog, ColList cols, torch::Tensor lit, int
   PipeArgs a;
   fill_args(a, prog, prog.size(0), cols, lit, n, keep_reg, -1, {}, 0);
   for (int c = 0; c < a.ncol; ++c) a.col[c].late = 0;      // the mask pass loads every column up front
-  choose_tile(a, 0, tile);
+  choose_tile(a, 0, tile, 0);
+  if (a.kmode == 1) predecode_tile(a);
   auto mask = torch::empty({n}, lit.options().dtype(torch::kUInt8));
   if (n > 0) {
     const long long per = a.tile ? (long long)a.tile : (long long)NTHR * ROWS * 4;

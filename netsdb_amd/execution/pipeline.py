@@ -55,9 +55,12 @@ CPU_INTERPRETER = False
 INTERP_CAP = 1 << 30
 # late (post-predicate) loads of the key / value columns only when the stage keeps fewer rows than this fraction
 LATE_MAX_SEL = 0.25
-# kernel shape: -1 picks the LDS-tile kernels when their tile fits (else the register kernels), 0 forces the register
-# kernels, 512 / 1024 / 2048 force that tile
-TILE = -1
+# kernel shape: -2 (default) the LDS-tile kernels (registers as LDS vectors) when their tile fits, -1 the hybrid kernels
+# (LDS-DMA column tiles, registers in VGPRs), 0 the register kernels (plain loads), 512 / 768 / 1024 / 2048 the
+# LDS-tile kernels of that tile; every mode falls back to the register kernels. Measured on 60 M rows
+# (profiles/r5_tpch/pipe_micro_modes.log): LDS-tile Q06 0.88 ms / Q14 mask 0.18 ms, hybrid 0.92 / 0.29, register
+# 1.22 / 0.34; an interpreted instruction costs 32-45 us of dispatch per 60 M rows in every mode.
+TILE = -2
 _SEL_EST: Dict[tuple, float] = {}          # stage signature -> kept fraction measured by its last launch
 _EMPTY = -(1 << 63)                        # free slot of the kernel's global table
 

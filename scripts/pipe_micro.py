@@ -103,6 +103,14 @@ def run_all(args, h, n, cols_of, lit, tile, out):
         t = h.pipe_agg(prog, 1, cols, lit, n, 7, 8, [4, 5, 9, 10, 3, 11], 0, args.max_wg, tile).cpu()
         out.append({"tile": tile, "kernel": "q01_check", "status": int(t[0]), "kept": int(t[1]),
                     "groups": int((t[2:2050] != -(1 << 63)).sum())})
+    if "disp" in args.which:
+        # dispatch cost: the Q06 columns with k no-op / AND instructions (k = 1, 6, 12)
+        cols = [col(PL.C_I32, ship), col(PL.C_F64, disc), col(PL.C_F64, qty), col(PL.C_F64, price)]
+        for name, ins1 in (("nop", (PL.OP_NOP, 4, -1, -1, -1, 0)), ("and", (PL.OP_AND, 4, 1, 2, -1, 0))):
+            for k in (1, 6, 12):
+                prog = torch.tensor([ins1] * k, dtype=torch.int64)
+                ms = timed(lambda: h.pipe_agg(prog, k, cols, lit, n, -1, -1, [3], 0, args.max_wg, tile), args.reps)
+                out.append({"tile": tile, "kernel": f"disp_{name}_{k}", "ms": round(ms, 4)})
     if "q01c" in args.which:
         # Q01 with the string keys read through their kept short codes (what the engine passes: plain int64 columns)
         ins = [(PL.OP_LEI, 7, 2, I, -1, 10471),

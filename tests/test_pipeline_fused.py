@@ -144,9 +144,9 @@ def test_fused_overflow_falls_back(monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tile", [-1, 0])
+@pytest.mark.parametrize("tile", [-2, -1, 0])
 def test_fused_tpch_gpu_vs_eager_and_pandas(tile, monkeypatch):
-    """Both kernel shapes (LDS-tile and register interpreters) against the eager path and pandas."""
+    """Every kernel shape (LDS-tile, hybrid and register interpreters) against the eager path and pandas."""
     monkeypatch.setattr(PL, "TILE", tile)
     t = tpch_gen.generate_fast(0.05, seed=4)
     f = tpch.frames(t)
@@ -238,7 +238,7 @@ def test_pipe_kernel_shapes_gpu():
     cols = PL._col_args(gprog, dev)
     lit = torch.zeros(1, dtype=torch.uint8, device=dev)
     pt = torch.tensor(ins, dtype=torch.int64)
-    for tile in (0, 512, 768, 1024, 2048):
+    for tile in (0, -1, -2, 512, 768, 1024, 2048):
         st, kept, k, v = _table_result(h.pipe_agg(pt, 2, cols, lit, n, 5, 6, [4, 7], 0, 0, tile), 2)
         assert st == 0 and kept == int(ref_mask.sum()), tile
         assert torch.equal(k, ref_k), tile
