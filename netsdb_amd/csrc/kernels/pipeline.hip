@@ -42,13 +42,15 @@ constexpr int TF_AIMM = 1, TF_ANONE = 2, TF_BIMM = 4, TF_BNONE = 8, TF_C = 16;
 enum Op : int {
   OP_NOP = 0, OP_CONST, OP_ADDF, OP_SUBF, OP_MULF, OP_DIVF, OP_ADDI, OP_SUBI, OP_MULI, OP_I2F,
   OP_LTF, OP_LEF, OP_GTF, OP_GEF, OP_EQF, OP_NEF, OP_LTI, OP_LEI, OP_GTI, OP_GEI, OP_EQI, OP_NEI,
-  OP_AND, OP_OR, OP_NOT, OP_PACK, OP_SEQ, OP_SPRE, OP_SSUF, OP_SEL, OP_NEGF
+  OP_AND, OP_OR, OP_NOT, OP_PACK, OP_SEQ, OP_SPRE, OP_SSUF, OP_SEL, OP_NEGF, OP_RNGF, OP_RNGI
 };
+constexpr int KPOOL = 16;              // second immediates: range upper bounds
 enum ColKind : int { C_F64 = 0, C_I64, C_I32, C_F32, C_U8, C_SCODE, C_SREF };
 
 struct Ins {
   int op, dst, a, b;
-  int c, pad;                    // c >= 0: compares AND their result with register c
+  int c;                         // c >= 0: compares AND their result with register c
+  int pad;                       // bits 0-7: tile-mode operand flags (TF_*); bits 8+: aux (range: kpool index | mode << 8)
   long long imm;
 };
 struct Col {
@@ -67,6 +69,7 @@ struct PipeArgs {
   long long n;
   int nins_a, nins, ncol, keep_reg, key_reg, nval, agg_op, nreg;
   int val_reg[FMAX];
+  long long kpool[KPOOL];        // range ops' upper bounds
   int tile, lds_bytes;           // tile / hybrid kernels: rows per tile, dynamic LDS bytes
   int kmode, pad2;               // 0 register kernels, 1 LDS-tile kernels, 2 hybrid (LDS-DMA columns, VGPR registers)
   unsigned long long* table;     // [2 + GCAP + GCAP * FMAX]: status (overflow, kept rows), keys, values (f64 bits)
@@ -300,6 +303,16 @@ __device__ __forceinline__ void run(const PipeArgs& a, typename RF<NR>::vec (&R)
       case OP_NOT: NSDB_EACH((u64)(x[j] == 0))
       case OP_PACK: NSDB_EACH((x[j] << (imm & 63)) | y[j])
       case OP_SEL: NSDB_EACH(x[j] ? y[j] : R[j][(int)imm])                // z = x ? y : r[imm]
+      case OP_RNGF: {                                      // lo <(=) x <(=) hi: imm = lo, kpool[aux] = hi
+        const int aux = cur.pad >> 8, mode = aux >> 8;
+        const double lo = u2f((u64)imm), hi = u2f((u64)a.kpool[aux & 0xFF]);
+        NSDB_EACH((u64)(((mode & 1) ? fx >= lo : fx > lo) && ((mode & 2) ? fx <= hi : fx < hi)))
+      }
+      case OP_RNGI: {
+        const int aux = cur.pad >> 8, mode = aux >> 8;
+        const long long lo = imm, hi = a.kpool[aux & 0xFF];
+        NSDB_EACH((u64)(((mode & 1) ? sx >= lo : sx > lo) && ((mode & 2) ? sx <= hi : sx < hi)))
+      }
       case OP_SEQ:
       case OP_SPRE:
       case OP_SSUF: {                                      // ib: the column whose bytes x refers to
@@ -700,6 +713,16 @@ __device__ __forceinline__ void tile_run(const PipeArgs& a, u64* regs, int lo, i
 #pragma unroll
         for (int j = 0; j < RPT; ++j) z[j] = x[j] ? y[j] : *reinterpret_cast<const u64*>(base + imm + j * NTHR * 8);
         break;
+      }
+      case OP_RNGF: {
+        const int aux = fl >> 8, mode = aux >> 8;
+        const double lo = u2f((u64)imm), hi = u2f((u64)a.kpool[aux & 0xFF]);
+        NSDB_EACH((u64)(((mode & 1) ? fx >= lo : fx > lo) && ((mode & 2) ? fx <= hi : fx < hi)))
+      }
+      case OP_RNGI: {
+        const int aux = fl >> 8, mode = aux >> 8;
+        const long long lo = imm, hi = a.kpool[aux & 0xFF];
+        NSDB_EACH((u64)(((mode & 1) ? sx >= lo : sx > lo) && ((mode & 2) ? sx <= hi : sx < hi)))
       }
       case OP_SEQ:
       case OP_SPRE:

@@ -20,7 +20,7 @@ int nsdb_pipe_mask(const void* args, unsigned char* mask, int grid, hipStream_t 
 namespace {
 
 // host mirror of nsdb_pipe::PipeArgs (layout checked against the kernel's sizeof at first use)
-constexpr int MAXINS = 48, MAXCOL = 10, FMAX = 8;
+constexpr int MAXINS = 48, MAXCOL = 10, FMAX = 8, KPOOL = 16;
 struct Ins {
   int op, dst, a, b;
   int c, pad;
@@ -42,13 +42,15 @@ struct PipeArgs {
   long long n;
   int nins_a, nins, ncol, keep_reg, key_reg, nval, agg_op, nreg;
   int val_reg[FMAX];
+  long long kpool[KPOOL];
   int tile, lds_bytes;
   int kmode, pad2;
   unsigned long long* table;
 };
 
 enum ColKind : int { C_F64 = 0, C_I64, C_I32, C_F32, C_U8, C_SCODE, C_SREF };
-enum : int { OP_LTF = 10, OP_NEI = 21, OP_SEQ = 26, OP_SPRE = 27, OP_SSUF = 28, OP_SEL = 29, OP_LAST = 30 };
+enum : int { OP_LTF = 10, OP_NEI = 21, OP_SEQ = 26, OP_SPRE = 27, OP_SSUF = 28, OP_SEL = 29, OP_RNGF = 31, OP_RNGI = 32,
+             OP_LAST = 32 };
 
 int sizes(int i) {
   static int s[10] = {0};
@@ -65,7 +67,8 @@ void check_col(const torch::Tensor& t, int64_t n, const char* what) {
   TORCH_CHECK(t.numel() >= n, "pipe_agg: ", what, " has fewer than n rows");
 }
 
-// prog: int64 [nins, 6] (op, dst, a, b, c, imm) on the CPU; c >= 0 only on compares (AND with register c).
+// prog: int64 [nins, 6 | 7] (op, dst, a, b, c, imm[, aux]) on the CPU; c >= 0 only on compares (AND with register c);
+// aux (range ops): kpool index | mode << 8.
 // cols: per column (kind, late, L, data, starts, ends, bytes): data for numeric kinds, starts / ends / bytes for strings.
 typedef std::vector<std::tuple<int64_t, int64_t, int64_t, c10::optional<torch::Tensor>, c10::optional<torch::Tensor>,
                                c10::optional<torch::Tensor>, c10::optional<torch::Tensor>>>
@@ -73,13 +76,16 @@ typedef std::vector<std::tuple<int64_t, int64_t, int64_t, c10::optional<torch::T
 
 // Validate the program / columns / registers and fill the kernel's argument image.
 void fill_args(PipeArgs& a, const torch::Tensor& prog, int64_t nins_a, const ColList& cols, const torch::Tensor& lit,
-               int64_t n, int64_t keep_reg, int64_t key_reg, const std::vector<int64_t>& val_regs, int64_t agg_op) {
+               int64_t n, int64_t keep_reg, int64_t key_reg, const std::vector<int64_t>& val_regs, int64_t agg_op,
+               const std::vector<int64_t>& kpool) {
   TORCH_CHECK(sizes(0) == MAXINS && sizes(1) == MAXCOL && sizes(3) == FMAX && sizes(5) == (int)sizeof(PipeArgs) &&
                   sizes(8) > 0 && (sizes(8) & (sizes(8) - 1)) == 0,
               "pipe_agg: host / kernel argument layout mismatch");
   const int NREG = sizes(2);
-  TORCH_CHECK(prog.device().is_cpu() && prog.scalar_type() == torch::kInt64 && prog.dim() == 2 && prog.size(1) == 6,
-              "pipe_agg: prog must be a CPU int64 [nins, 6] tensor");
+  TORCH_CHECK(prog.device().is_cpu() && prog.scalar_type() == torch::kInt64 && prog.dim() == 2 &&
+                  (prog.size(1) == 6 || prog.size(1) == 7),
+              "pipe_agg: prog must be a CPU int64 [nins, 6 | 7] tensor");
+  TORCH_CHECK(kpool.size() <= (size_t)KPOOL, "pipe_agg: at most ", KPOOL, " range bounds");
   const int nins = (int)prog.size(0), ncol = (int)cols.size(), nval = (int)val_regs.size();
   TORCH_CHECK(nins <= MAXINS && ncol <= MAXCOL && ncol <= NREG && nval <= FMAX && nval >= 0, "pipe_agg: too large");
   const int MAXSTR = sizes(6);
@@ -89,6 +95,8 @@ void fill_args(PipeArgs& a, const torch::Tensor& prog, int64_t nins_a, const Col
   TORCH_CHECK(keep_reg >= -1 && keep_reg < NREG && key_reg >= -1 && key_reg < NREG, "pipe_agg: bad keep/key reg");
   TORCH_CHECK(lit.is_cuda() && lit.scalar_type() == torch::kUInt8 && lit.is_contiguous(), "pipe_agg: lit");
   std::memset(&a, 0, sizeof(a));
+  for (size_t i = 0; i < kpool.size(); ++i) a.kpool[i] = kpool[i];
+  const bool has_aux = prog.size(1) == 7;
   auto P = prog.accessor<int64_t, 2>();
   for (int i = 0; i < nins; ++i) {
     Ins& I = a.ins[i];
@@ -98,10 +106,17 @@ void fill_args(PipeArgs& a, const torch::Tensor& prog, int64_t nins_a, const Col
     I.b = (int)P[i][3];
     I.c = (int)P[i][4];
     I.imm = P[i][5];
+    const int64_t aux = has_aux ? P[i][6] : 0;
+    TORCH_CHECK(aux >= 0 && aux < (int64_t(1) << 16), "pipe_agg: bad aux at ", i);
+    I.pad = (int)(aux << 8);
+    if (I.op == OP_RNGF || I.op == OP_RNGI)
+      TORCH_CHECK(I.b == -1 && (aux & 0xFF) < (int64_t)kpool.size() && (aux >> 8) <= 3,
+                  "pipe_agg: range op needs b = -1, a pool index and a mode, at ", i);
     TORCH_CHECK(I.op >= 0 && I.op <= OP_LAST, "pipe_agg: bad opcode at ", i);
     TORCH_CHECK(I.dst >= 0 && I.dst < NREG && I.a >= -2 && I.a < NREG && I.b >= -2 && I.b < NREG,
                 "pipe_agg: register out of range at ", i);
-    TORCH_CHECK(I.c == -1 || (I.c >= 0 && I.c < NREG && I.op >= OP_LTF && I.op <= OP_NEI),
+    TORCH_CHECK(I.c == -1 || (I.c >= 0 && I.c < NREG && ((I.op >= OP_LTF && I.op <= OP_NEI) || I.op == OP_RNGF ||
+                                                            I.op == OP_RNGI)),
                 "pipe_agg: AND-with register only on compares, at ", i);
     if (I.op == OP_SEL) TORCH_CHECK(I.imm >= 0 && I.imm < NREG, "pipe_agg: select register at ", i);
     a.nreg = std::max({a.nreg, I.dst + 1, I.a + 1, I.b + 1, I.c + 1, I.op == OP_SEL ? (int)I.imm + 1 : 0});
@@ -198,7 +213,7 @@ void predecode_tile(PipeArgs& a) {
     }
     if (I.op == OP_SEL) I.imm = I.imm * T8;
     I.dst = (int)(I.dst * T8);
-    I.pad = fl;
+    I.pad = fl | (I.pad & ~0xFF);
   }
 }
 
@@ -262,10 +277,11 @@ void choose_tile(PipeArgs& a, int static_bytes, int64_t force, int reg_static_by
 // Returns the global result table, int64 [2 + GCAP * (1 + FMAX)]: status (overflow flag, kept rows), GCAP keys
 // (INT64_MIN = free slot), then GCAP x FMAX f64 values (bit patterns). The host reads it back in one copy.
 torch::Tensor pipe_agg(torch::Tensor prog, int64_t nins_a, ColList cols, torch::Tensor lit, int64_t n, int64_t keep_reg,
-                       int64_t key_reg, std::vector<int64_t> val_regs, int64_t agg_op, int64_t max_wg, int64_t tile) {
+                       int64_t key_reg, std::vector<int64_t> val_regs, int64_t agg_op, int64_t max_wg, int64_t tile,
+                       std::vector<int64_t> kpool) {
   const int ROWS = 4, NTHR = sizes(7), GCAP = sizes(8), CAP = sizes(4);
   PipeArgs a;
-  fill_args(a, prog, nins_a, cols, lit, n, keep_reg, key_reg, val_regs, agg_op);
+  fill_args(a, prog, nins_a, cols, lit, n, keep_reg, key_reg, val_regs, agg_op, kpool);
   const int F = a.nval <= 2 ? 2 : (a.nval <= 4 ? 4 : (a.nval <= 6 ? 6 : FMAX));
   choose_tile(a, CAP * (8 + 8 * F) + 16, tile, CAP * (8 + 8 * FMAX) + 16);
   if (a.kmode == 1) predecode_tile(a);
@@ -280,10 +296,11 @@ torch::Tensor pipe_agg(torch::Tensor prog, int64_t nins_a, ColList cols, torch::
 }
 
 // The predicate program's keep flag per row (uint8 [n]); key / values unused.
-torch::Tensor pipe_mask(torch::Tensor prog, ColList cols, torch::Tensor lit, int64_t n, int64_t keep_reg, int64_t tile) {
+torch::Tensor pipe_mask(torch::Tensor prog, ColList cols, torch::Tensor lit, int64_t n, int64_t keep_reg, int64_t tile,
+                        std::vector<int64_t> kpool) {
   const int ROWS = 4, NTHR = sizes(7);
   PipeArgs a;
-  fill_args(a, prog, prog.size(0), cols, lit, n, keep_reg, -1, {}, 0);
+  fill_args(a, prog, prog.size(0), cols, lit, n, keep_reg, -1, {}, 0, kpool);
   for (int c = 0; c < a.ncol; ++c) a.col[c].late = 0;      // the mask pass loads every column up front
   choose_tile(a, 0, tile, 0);
   if (a.kmode == 1) predecode_tile(a);
@@ -302,11 +319,11 @@ torch::Tensor pipe_mask(torch::Tensor prog, ColList cols, torch::Tensor lit, int
 void register_pipeline(pybind11::module& m) {
   m.def("pipe_mask", &pipe_mask, "fused filter predicate (pipeline.hip): keep flag per row (uint8)",
         pybind11::arg("prog"), pybind11::arg("cols"), pybind11::arg("lit"), pybind11::arg("n"), pybind11::arg("keep_reg"),
-        pybind11::arg("tile") = -1);
+        pybind11::arg("tile") = -1, pybind11::arg("kpool") = std::vector<int64_t>());
   m.def("pipe_agg", &pipe_agg,
         "fused scan -> filter -> project -> low-cardinality aggregate (pipeline.hip): the global result table "
         "int64 [2 + GCAP * 9] = status (overflow, kept rows), keys, f64 values [GCAP, 8]",
         pybind11::arg("prog"), pybind11::arg("nins_a"), pybind11::arg("cols"), pybind11::arg("lit"), pybind11::arg("n"),
         pybind11::arg("keep_reg"), pybind11::arg("key_reg"), pybind11::arg("val_regs"), pybind11::arg("agg_op") = 0,
-        pybind11::arg("max_wg") = 0, pybind11::arg("tile") = -1);
+        pybind11::arg("max_wg") = 0, pybind11::arg("tile") = -1, pybind11::arg("kpool") = std::vector<int64_t>());
 }

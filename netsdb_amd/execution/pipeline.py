@@ -40,7 +40,8 @@ NREG, MAXINS, MAXCOL, FMAX, MAXSTR = 16, 48, 10, 8, 4
 IMM = -2                       # operand register number meaning "the instruction's immediate"
 (OP_NOP, OP_CONST, OP_ADDF, OP_SUBF, OP_MULF, OP_DIVF, OP_ADDI, OP_SUBI, OP_MULI, OP_I2F,
  OP_LTF, OP_LEF, OP_GTF, OP_GEF, OP_EQF, OP_NEF, OP_LTI, OP_LEI, OP_GTI, OP_GEI, OP_EQI, OP_NEI,
- OP_AND, OP_OR, OP_NOT, OP_PACK, OP_SEQ, OP_SPRE, OP_SSUF, OP_SEL, OP_NEGF) = range(31)
+ OP_AND, OP_OR, OP_NOT, OP_PACK, OP_SEQ, OP_SPRE, OP_SSUF, OP_SEL, OP_NEGF, OP_RNGF, OP_RNGI) = range(33)
+KPOOL = 16                     # second immediates (range upper bounds), pipeline.hip PipeArgs.kpool
 C_F64, C_I64, C_I32, C_F32, C_U8, C_SCODE, C_SREF = range(7)
 AGG_OPS = {"sum": 0, "min": 1, "max": 2}
 
@@ -217,7 +218,8 @@ class Program:
     """A compiled program + the column table it reads."""
 
     def __init__(self):
-        self.ins: List[Tuple[int, int, int, int, int, int]] = []     # (op, dst, a, b, c, imm)
+        self.ins: List[Tuple[int, int, int, int, int, int, int]] = []   # (op, dst, a, b, c, imm, aux)
+        self.kpool: List[int] = []            # range ops' upper bounds (aux = pool index | mode << 8)
         self.cols: List[dict] = []            # {"key": (path, usage), "kind", "late", "L", "obj": column}
         self.col_index: Dict[tuple, int] = {}
         self.lit = bytearray()
@@ -244,17 +246,46 @@ class Program:
 
     def emit(self, op, dst, a=-1, b=-1, imm=0):
         """a / b == IMM: that operand is the 64-bit immediate. ``AND d, r, t`` right after the compare that wrote the
-        temporary t folds into that compare (its AND-with field c = r): one instruction per conjunct."""
+        temporary t folds into that compare (its AND-with field c = r): one instruction per conjunct; and a lower and
+        an upper bound of the same register against immediates (``lo <= x`` folded with ``x < hi``) become ONE range
+        instruction (RNGF / RNGI)."""
         if op == OP_AND and self.ins:
-            po, pd, pa, pb, pc, pimm = self.ins[-1]
+            po, pd, pa, pb, pc, pimm, _ = self.ins[-1]
             if OP_LTF <= po <= OP_NEI and pc < 0:
                 other = a if pd == b else (b if pd == a else None)
                 if other is not None and other != pd and pd >= len(self.cols) and pd not in self.pinned:
-                    self.ins[-1] = (po, dst, pa, pb, other, pimm)
+                    self.ins[-1] = (po, dst, pa, pb, other, pimm, 0)
+                    self._range_fold()
                     return
         if len(self.ins) >= MAXINS:
             raise Unfusable("program too long")
-        self.ins.append((op, dst, a, b, -1, int(imm)))
+        self.ins.append((op, dst, a, b, -1, int(imm), 0))
+
+    _LOWER = {OP_GEF: 1, OP_GTF: 0, OP_GEI: 1, OP_GTI: 0}      # op -> lower bound inclusive?
+    _UPPER = {OP_LEF: 2, OP_LTF: 0, OP_LEI: 2, OP_LTI: 0}      # op -> upper bound inclusive (mode bit 1)?
+
+    def _range_fold(self):
+        """ins[-2] = (cmp1 r = x ? imm1), ins[-1] = (cmp2 d = (x ? imm2) & r): a lower + upper bound pair on one
+        register -> RNG d = lo <(=) x <(=) hi, AND-ed with ins[-2]'s own chain."""
+        if len(self.ins) < 2 or len(self.kpool) >= KPOOL:
+            return
+        o2, d, a2, b2, c2, imm2, _ = self.ins[-1]
+        o1, r, a1, b1, c1, imm1, _ = self.ins[-2]
+        if c2 != r or a1 != a2 or b1 != IMM or b2 != IMM or r < len(self.cols) or r in self.pinned or a1 < 0:
+            return
+        fam = lambda o: "f" if OP_LTF <= o <= OP_NEF else ("i" if OP_LTI <= o <= OP_NEI else None)  # noqa: E731
+        if fam(o1) is None or fam(o1) != fam(o2):
+            return
+        if o1 in self._LOWER and o2 in self._UPPER:
+            lo_op, lo, hi_op, hi = o1, imm1, o2, imm2
+        elif o2 in self._LOWER and o1 in self._UPPER:
+            lo_op, lo, hi_op, hi = o2, imm2, o1, imm1
+        else:
+            return
+        mode = self._LOWER[lo_op] | self._UPPER[hi_op]
+        self.kpool.append(int(hi))
+        aux = (len(self.kpool) - 1) | (mode << 8)
+        self.ins[-2:] = [(OP_RNGF if fam(o1) == "f" else OP_RNGI, d, a1, -1, c1, int(lo), aux)]
 
     def literal(self, s: str) -> int:
         b = s.encode()
@@ -721,12 +752,12 @@ def _col_args(prog: Program, dev):
 
 def _launch(prog: Program, n: int, dev, plan: StagePlan):
     h = _ext.hip()
-    ins = torch.tensor(prog.ins if prog.ins else [[0, 0, -1, -1, -1, 0]], dtype=torch.int64).reshape(-1, 6)
+    ins = torch.tensor(prog.ins if prog.ins else [[0, 0, -1, -1, -1, 0, 0]], dtype=torch.int64).reshape(-1, 7)
     if not prog.ins:
         ins = ins[:0]
     lit = torch.frombuffer(bytearray(prog.lit or b"\0"), dtype=torch.uint8).to(dev, non_blocking=True)
     table = h.pipe_agg(ins, prog.nins_a, _col_args(prog, dev), lit, n, prog.keep_reg, prog.key_reg, prog.val_regs,
-                       AGG_OPS[plan.op], 0, TILE)
+                       AGG_OPS[plan.op], 0, TILE, prog.kpool)
     host = table.cpu()                           # the one device -> host read of the launch
     if int(host[0]) != 0:
         return None
@@ -823,7 +854,7 @@ def _run_program(prog: Program, n: int) -> List[Optional[torch.Tensor]]:
         return torch.tensor(m, dtype=torch.int64)
 
     def run(lo, hi):
-        for opc, d, a, b, c, imm in prog.ins[lo:hi]:
+        for opc, d, a, b, c, imm, aux in prog.ins[lo:hi]:
             x = regs[a] if a >= 0 else (torch.full((n,), imm, dtype=torch.int64) if a == IMM else None)
             y = regs[b] if b >= 0 else (torch.full((n,), imm, dtype=torch.int64) if b == IMM else None)
             if opc == OP_CONST:
@@ -854,6 +885,11 @@ def _run_program(prog: Program, n: int) -> List[Optional[torch.Tensor]]:
                 z = strmatch(x, b, imm, {OP_SEQ: 0, OP_SPRE: 1, OP_SSUF: 2}[opc])
             elif opc == OP_SEL:
                 z = torch.where(x != 0, y, regs[imm])
+            elif opc in (OP_RNGF, OP_RNGI):
+                hi_v, mode = prog.kpool[aux & 0xFF], aux >> 8
+                xv, lo_t, hi_t = (f(x), f(torch.tensor([imm])), f(torch.tensor([hi_v]))) if opc == OP_RNGF else \
+                    (x, torch.tensor([imm]), torch.tensor([hi_v]))
+                z = (((xv >= lo_t) if mode & 1 else (xv > lo_t)) & ((xv <= hi_t) if mode & 2 else (xv < hi_t))).long()
             else:
                 z = torch.zeros(n, dtype=torch.int64)
             if c >= 0:                          # compare folded with its conjunction's AND
@@ -940,9 +976,9 @@ def run_filter(plan: FilterPlan, batch: RecordBatch) -> Optional[RecordBatch]:
         plan.reason = str(e)
         return None
     if on_gpu:
-        ins = torch.tensor(prog.ins, dtype=torch.int64).reshape(-1, 6)
+        ins = torch.tensor(prog.ins, dtype=torch.int64).reshape(-1, 7)
         lit = torch.frombuffer(bytearray(prog.lit or b"\0"), dtype=torch.uint8).to(dev, non_blocking=True)
-        mask = _ext.hip().pipe_mask(ins, _col_args(prog, dev), lit, batch.n, prog.keep_reg, TILE).bool()
+        mask = _ext.hip().pipe_mask(ins, _col_args(prog, dev), lit, batch.n, prog.keep_reg, TILE, prog.kpool).bool()
     else:
         mask = interpret_mask(prog, batch.n)
     plan.stats["fused_batches"] += 1

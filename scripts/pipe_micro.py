@@ -78,6 +78,13 @@ def run_all(args, h, n, cols_of, lit, tile, out):
                (PL.OP_LEF, 4, 1, I, 4, fb(0.07)), (PL.OP_LTF, 4, 2, I, 4, fb(24.0)),
                (PL.OP_MULF, 5, 3, 1, -1, 0)]
         prog = torch.tensor(ins, dtype=torch.int64)
+        # the same predicate with range instructions (what the compiler emits): 4 instructions
+        rins = [(PL.OP_RNGI, 4, 0, -1, -1, 8766, 0 | (1 << 8)), (PL.OP_RNGF, 4, 1, -1, 4, fb(0.05), 1 | (3 << 8)),
+                (PL.OP_LTF, 4, 2, I, 4, fb(24.0), 0), (PL.OP_MULF, 5, 3, 1, -1, 0, 0)]
+        rprog, kpool = torch.tensor(rins, dtype=torch.int64), [9131, fb(0.07)]
+        cols = [col(PL.C_I32, ship), col(PL.C_F64, disc), col(PL.C_F64, qty), col(PL.C_F64, price)]
+        ms = timed(lambda: h.pipe_agg(rprog, 3, cols, lit, n, 4, -1, [5], 0, args.max_wg, tile, kpool), args.reps)
+        out.append({"tile": tile, "kernel": "q06_range_agg", "ms": round(ms, 4), "grows_s": round(n / ms / 1e6, 2)})
         for late in (1, 0):
             cols = [col(PL.C_I32, ship), col(PL.C_F64, disc), col(PL.C_F64, qty), col(PL.C_F64, price, late)]
             ms = timed(lambda: h.pipe_agg(prog, 5, cols, lit, n, 4, -1, [5], 0, args.max_wg, tile), args.reps)
@@ -132,6 +139,9 @@ def run_all(args, h, n, cols_of, lit, tile, out):
         ms = timed(lambda: h.pipe_mask(prog, cols, lit, n, 1, tile), args.reps)
         out.append({"tile": tile, "kernel": "q14_mask", "ms": round(ms, 4), "grows_s": round(n / ms / 1e6, 2),
                     "gbs": round(n * 5 / ms / 1e6, 1)})
+        rprog = torch.tensor([(PL.OP_RNGI, 1, 0, -1, -1, 9374, 1 << 8)], dtype=torch.int64)
+        ms = timed(lambda: h.pipe_mask(rprog, cols, lit, n, 1, tile, [9404]), args.reps)
+        out.append({"tile": tile, "kernel": "q14_range_mask", "ms": round(ms, 4), "grows_s": round(n / ms / 1e6, 2)})
     if "floor" in args.which:
         # no instructions: the load / loop / store floor of each kernel on the same columns
         empty = torch.zeros(0, 6, dtype=torch.int64)

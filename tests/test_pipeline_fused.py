@@ -230,7 +230,7 @@ def test_pipe_kernel_shapes_gpu():
     prog.cols = [{"kind": PL.C_SCODE, "late": 0, "L": 3, "obj": s}, {"kind": PL.C_I32, "late": 0, "L": 0, "obj": a},
                  {"kind": PL.C_F32, "late": 0, "L": 0, "obj": b}, {"kind": PL.C_U8, "late": 0, "L": 0, "obj": u},
                  {"kind": PL.C_F64, "late": 0, "L": 0, "obj": d}]
-    prog.ins, prog.nins_a, prog.keep_reg, prog.key_reg, prog.val_regs = ins, 2, 5, 6, [4, 7]
+    prog.ins, prog.nins_a, prog.keep_reg, prog.key_reg, prog.val_regs = [t + (0,) for t in ins], 2, 5, 6, [4, 7]
     ref_k, ref_v = PL.interpret(prog, n, "sum")
     ref_mask = PL.interpret_mask(prog, n)
     gprog = PL.Program()
