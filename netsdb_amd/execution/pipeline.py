@@ -74,10 +74,11 @@ class Unfusable(Exception):
 class E:
     """Symbolic column expression of a stage (built from the TCAP atoms' lambda nodes)."""
 
-    __slots__ = ("kind", "args", "val")
+    __slots__ = ("kind", "args", "val", "_p")
 
     def __init__(self, kind: str, args=(), val=None):
         self.kind, self.args, self.val = kind, tuple(args), val
+        self._p = None
 
     def __repr__(self):
         return f"{self.kind}{self.args if self.args else ''}{'' if self.val is None else '=' + repr(self.val)}"
@@ -302,7 +303,10 @@ def _fbits(v: float) -> int:
 
 
 def _path(e: E) -> tuple:
-    return (e.kind, e.val) + tuple(_path(a) for a in e.args)
+    """Structural key of an expression (memoised on the node: the compiler asks for it many times)."""
+    if e._p is None:
+        e._p = (e.kind, e.val) + tuple(_path(a) for a in e.args)
+    return e._p
 
 
 class _Compiler:
@@ -366,7 +370,7 @@ class _Compiler:
         if len(self.p.cols) >= MAXCOL:
             raise Unfusable("columns")
         self.p.col_index[key] = len(self.p.cols)
-        self.p.cols.append({"kind": kind, "late": int(late), "L": L, "obj": obj})
+        self.p.cols.append({"kind": kind, "late": int(late), "L": L, "obj": obj, "expr": e})
         return len(self.p.cols) - 1
 
     def compile(self) -> Program:
@@ -692,6 +696,41 @@ class _Compiler:
 
 
 # ---------------------------------------------------------------------------------------------- execution
+_PROG_CACHE: Dict[tuple, Program] = {}
+_PROG_CACHE_MAX = 256
+
+
+def _schema_key(batch: RecordBatch) -> tuple:
+    """What a compiled program depends on besides the stage's expressions: each column's kind (dtype, or string with
+    its length bound), never its values."""
+    out = []
+    for k, c in batch.columns.items():
+        if isinstance(c, torch.Tensor):
+            out.append((k, str(c.dtype), c.dim()))
+        elif isinstance(c, StringColumn):
+            out.append((k, "s", c._maxlen))
+        else:
+            out.append((k, type(c).__name__))
+    return tuple(out)
+
+
+def _compile_cached(plan: StagePlan, batch: RecordBatch) -> Program:
+    """The stage's program for this batch: compiled once per (stage expressions, selectivity mode, column kinds) and
+    re-bound to the batch's columns afterwards (repeated queries skip the compiler)."""
+    key = (plan.sig, _SEL_EST.get(plan.sig, 0.0) < LATE_MAX_SEL, _schema_key(batch))
+    hit = _PROG_CACHE.get(key)
+    if hit is not None:
+        p = Program.__new__(Program)
+        p.__dict__.update(hit.__dict__)
+        p.cols = [dict(c, obj=_resolve(c["expr"], batch)) for c in hit.cols]
+        return p
+    p = _Compiler(plan, batch).compile()
+    if len(_PROG_CACHE) >= _PROG_CACHE_MAX:
+        _PROG_CACHE.pop(next(iter(_PROG_CACHE)))
+    _PROG_CACHE[key] = p
+    return p
+
+
 def run_batch(plan: StagePlan, batch: RecordBatch) -> Optional[RecordBatch]:
     """One fused launch over ``batch``: the pre-aggregated {kcol: keys, vcol: values} batch, or None when this batch
     must take the eager atoms (columns the kernel cannot read, more groups than its tables)."""
@@ -702,7 +741,7 @@ def run_batch(plan: StagePlan, batch: RecordBatch) -> Optional[RecordBatch]:
     if not on_gpu and not (CPU_INTERPRETER and dev.type == "cpu"):
         return None
     try:
-        prog = _Compiler(plan, batch).compile()
+        prog = _compile_cached(plan, batch)
     except Unfusable as e:
         plan.disabled = True
         plan.reason = str(e)
@@ -970,7 +1009,7 @@ def run_filter(plan: FilterPlan, batch: RecordBatch) -> Optional[RecordBatch]:
     if not on_gpu and not (CPU_INTERPRETER and dev.type == "cpu"):
         return None
     try:
-        prog = _Compiler(plan, batch).compile()
+        prog = _compile_cached(plan, batch)
     except Unfusable as e:
         plan.disabled = True
         plan.reason = str(e)
