@@ -84,6 +84,7 @@ struct GemmOpts {
   int epi;
   const void* pf_ptr;
   long long pf_bytes;
+  int kinter;
 };
 
 void check_rc(int rc, const char* what) {
@@ -101,7 +102,7 @@ bool is_f32(const torch::Tensor& t, const char* name) {
 }
 
 // C = epi(alpha * A @ B^T); A [b?,M,K] bf16, B [b?,N,K] bf16 (row stride may exceed K), bias f32.
-// cfg: -1 auto, 0 (128x128 tile kernel), 2 (256x256 8-phase). prefetch: a later kernel's operand that this
+// cfg: -1 auto, 0 (128x128 tile kernel), 2 (256x256 8-phase), 3 / 4 (256x128 / 128x256 skinny stream). prefetch: a later kernel's operand that this
 // launch's workgroups read into the Infinity Cache as they finish (the caller checked gemm_prefetch_eligible).
 torch::Tensor gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Tensor> bias, int64_t bias_mode,
                       int64_t act, bool out_f32, double alpha, double dropout, int64_t seed, int64_t splits,
@@ -149,7 +150,11 @@ torch::Tensor gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Ten
     C = batched ? torch::empty({batch, M, N}, opts) : torch::empty({M, N}, opts);
   }
   TORCH_CHECK(!accumulate || out_f32, "accumulate=True needs out_f32");
-  TORCH_CHECK(cfg == -1 || cfg == 0 || cfg == 2, "gemm_nt: cfg must be -1 (auto), 0 or 2 (study configs: _hip_study)");
+  TORCH_CHECK(cfg == -1 || cfg == 0 || (cfg >= 2 && cfg <= 6),
+              "gemm_nt: cfg must be -1 (auto), 0, 2, 3, 4, 5 or 6 (study configs: _hip_study)");
+  // 5 / 6: the stream tiles 3 / 4 with k-interleaved splits (split s takes k-tiles s, s + S, ...; an A/B arm)
+  const int kinter = cfg >= 5 ? 1 : 0;
+  if (cfg >= 5) cfg -= 2;
   int s = splits > 0 ? (int)splits : nsdb_gemm_splits((int)M, (int)N, (int)K, (int)batch, (int)cfg);
   torch::Tensor ws;
   float* wsp = nullptr;
@@ -158,7 +163,7 @@ torch::Tensor gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Ten
     wsp = ws.data_ptr<float>();
   }
   TORCH_CHECK(epi >= -1 && epi <= 1, "gemm_nt: epi must be -1 (auto), 0 (LDS-staged) or 1 (direct)");
-  GemmOpts o{(int)cfg, (int)epi, nullptr, 0};
+  GemmOpts o{(int)cfg, (int)epi, nullptr, 0, kinter};
   if (prefetch.has_value() && prefetch->defined() && prefetch->numel() > 0) {
     // the byte span of the tensor's elements (a strided view reads its whole span)
     check_cuda(*prefetch, "prefetch");

@@ -571,6 +571,109 @@ gemm_nt_tile_kernel(GemmParams p) {
                                      reinterpret_cast<float*>(smem + 2 * STG));
 }
 
+#define NSDB_BARRIER()                          \
+  do {                                          \
+    __builtin_amdgcn_sched_barrier(0);          \
+    asm volatile("s_barrier" ::: "memory");     \
+    __builtin_amdgcn_sched_barrier(0);          \
+  } while (0)
+
+// Skinny long-K streaming tile (cfg 3: 256 x 128, cfg 4: 128 x 256): one operand has <= 128 rows and K is long, so
+// the big operand streams from HBM exactly once and the GEMM is bound by that stream, not by the MFMAs (the dedup
+// scoring GEMMs 500 x 100 x 900k and 12 x 500 x 100 x 100k; DedupModels / FFMatrixBlockScanner-style inference,
+// reference src/FF/headers/FFTransposeMult.h:92). The 256x256 8-phase tile pads the 100-row operand to 256 rows,
+// i.e. 2.5x the MFMA work, which at ~6 TB/s of operand bytes lands at the power-capped MFMA ceiling; this tile pads
+// it to 128.
+//  * 8 waves as WGM x WGN, 64 x 64 per wave (4 x 4 MFMA tiles of 16x16x32), plain C layout (store_tile_lds).
+//  * An NS-slot LDS ring of whole k-tiles (TBM+TBN rows x 64 bf16, 48 KiB) with NS-1 tiles in flight: 96 KiB at
+//    NS = 3, twice the 8-phase kernel's 3 half-tiles, for the HBM latency at one workgroup per CU.
+//  * ONE barrier per k-tile: wait for this thread's DMAs of tile t (vmcnt = the DMAs of the NS-2 younger tiles) ->
+//    raw s_barrier (every wave's DMAs of t have landed, every wave's reads of t-1's slot are consumed by its MFMAs)
+//    -> DMA tile t+NS-1 into t-1's slot -> ds_read + MFMA tile t.
+//  * Past the last k-tile the DMAs target k >= kend and the buffer range check zero-fills them, so every iteration
+//    issues the same OPS VMEM instructions and the counted wait is a constant.
+//  * KI (k-interleaved splits, unsegmented B only): split s takes k-tiles s, s + S, s + 2S, ... instead of one
+//    contiguous chunk, so the S workgroups of a tile read S adjacent 128-B pieces of every operand row at about the
+//    same time (whole DRAM pages instead of one 128-B piece per page visit).
+template <int TBM, int TBN, int WGM, int WGN, int NS, bool KI>
+__global__ void __launch_bounds__(64 * WGM * WGN, 2) gemm_nt_stream_kernel(GemmParams p) {
+  constexpr int NW = WGM * WGN;
+  constexpr int TM = TBM / WGM / 16, TN = TBN / WGN / 16;
+  constexpr int A_BYTES = TBM * BK * 2, B_BYTES = TBN * BK * 2, STG = A_BYTES + B_BYTES;
+  constexpr int OPS = (TBM + TBN) / (8 * NW);      // 1 KiB wave-instructions per thread per k-tile
+  static_assert(TBM % (8 * NW) == 0 && TBN % (8 * NW) == 0 && NS >= 2, "stream tile geometry");
+  __shared__ __attribute__((aligned(16))) char smem[NS * STG + 1024];   // + the epilogue's bias (store_tile_lds)
+
+  const int ntiles = p.tiles_m * p.tiles_n;
+  const int wg = xcd_remap(blockIdx.x, ntiles * p.splits);
+  const int split = wg / ntiles, tile = wg % ntiles;
+  int tm, tn;
+  grouped_tile(tile, p.tiles_m, p.tiles_n, tm, tn);
+  const int batch = blockIdx.z;
+  const int m0 = tm * TBM, n0 = tn * TBN;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WGN, wn = wave % WGN;
+
+  const int rows_a = min(TBM, p.M - m0), rows_b = min(TBN, p.N - n0);
+  const unsigned short* Ab = p.A + batch * p.sA + (long long)m0 * p.lda;
+  const int ksteps = (p.K + BK - 1) / BK;
+  const int kbeg = KI ? split * BK : split * p.kchunk;
+  const int kend = KI ? p.K : min(p.K, kbeg + p.kchunk);
+  const int kstep = KI ? p.splits * BK : BK;            // k distance between consecutive k-tiles of this split
+  const int nk = KI ? max(0, (ksteps - split + p.splits - 1) / p.splits) : max(0, (kend - kbeg + BK - 1) / BK);
+  const long long kseg = (!KI && p.seg_k) ? kbeg / p.seg_k : 0;
+  const int kb0 = (int)(kseg * p.seg_k);
+  const unsigned short* Bb = p.B + batch * p.sB + (long long)n0 * p.ldb + kseg * p.seg_stride_b;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(Ab, (unsigned)((long long)rows_a * p.lda * 2));
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(Bb, (unsigned)((long long)rows_b * p.ldb * 2));
+
+  auto stage = [&](int slot, int t) {
+    char* dst = smem + slot * STG;
+    const int k = min(kbeg + t * kstep, kend);          // past the last k-tile: k = kend, zero-filled
+    stage_tile<TBM, NW>(ra, dst, p.lda, rows_a, k, kend, wave, lane);
+    stage_tile<TBN, NW>(rb, dst + A_BYTES, p.ldb, rows_b, k - kb0, kend - kb0, wave, lane);
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t) stage(t, t);
+  int slot = 0, wslot = NS - 1;
+  for (int t = 0; t < nk; ++t) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS * (NS - 2)) : "memory");
+    NSDB_BARRIER();
+    stage(wslot, t + NS - 1);
+    wslot = wslot + 1 == NS ? 0 : wslot + 1;
+    const char* la = smem + slot * STG;
+    const char* lb = la + A_BYTES;
+    slot = slot + 1 == NS ? 0 : slot + 1;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int chunk = kk * 4 + (lane >> 4);
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = read_frag(la, wm * (TBM / WGM) + i * 16 + (lane & 15), chunk);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = read_frag(lb, wn * (TBN / WGN) + j * 16 + (lane & 15), chunk);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the trailing zero-fill DMAs land before LDS reuse
+  __syncthreads();
+  store_tile_lds<TBM, TBN, WGM, WGN>(acc, smem, NS * STG, p, batch, split, m0, n0, tid, lane, wave,
+                                     reinterpret_cast<float*>(smem + NS * STG));
+}
+
 // ---------------------------------------------------------------------------------------------
 // 256x256x64 "8-phase" kernel for long-K / large shapes (cdna_hip_programming.md §5, the 256^2
 // 8-phase template): 512 threads = 8 waves as 2(M) x 4(N), each wave 128x64 = 8x4 MFMA tiles.
@@ -603,13 +706,6 @@ gemm_nt_tile_kernel(GemmParams p) {
 //  Studies of this loop (diagnostic variants, K-tail stealing, adaptive split-K, in-launch fix-up, ring
 //  buffers, cache policies, the 4-wave structures) live in the separate study build (csrc/study).
 // ---------------------------------------------------------------------------------------------
-#define NSDB_BARRIER()                          \
-  do {                                          \
-    __builtin_amdgcn_sched_barrier(0);          \
-    asm volatile("s_barrier" ::: "memory");     \
-    __builtin_amdgcn_sched_barrier(0);          \
-  } while (0)
-
 template <int EPI>
 __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   // fused-softmax launches may carry diagnostic phase stamps (p.stamps: [tile][8] on the 100 MHz real-time clock)
@@ -901,10 +997,11 @@ __global__ void __launch_bounds__(512) splitk_reduce_wide_kernel(GemmParams p) {
 // exactly the call that passes it — no process-wide state, so lanes on other streams / threads are never
 // affected. The product build exports only the production configs; the study variants are in csrc/study.
 struct GemmOpts {
-  int cfg;                  // -1 auto, 0 = 128x128 tile kernel, 2 = 256x256 8-phase kernel
+  int cfg;                  // -1 auto, 0 = 128x128 tile, 2 = 256x256 8-phase, 3 / 4 = 256x128 / 128x256 stream
   int epi;                  // 8-phase unsplit epilogue: -1 auto (direct), 0 LDS-staged, 1 direct register stores
   const void* pf_ptr;       // operand prefetch of this launch (8-phase only): pf_bytes at pf_ptr, or nullptr
   long long pf_bytes;
+  int kinter;               // stream tiles: 1 = k-interleaved splits (split s takes k-tiles s, s + S, ...)
 };
 
 extern "C" {
@@ -920,8 +1017,18 @@ static int pick_cfg(int M, int N, int K, int batch) {
   // skinny, very long K (the dedup scoring GEMMs 500 x 100 x 900k and 12 x 500 x 100 x 100k): memory-bound; the
   // 8-phase kernel keeps three half-tiles of A in flight and zero-fills the missing B rows without reading them
   // (common panel 205 vs 222 us, batched private panels 263 vs 285 us, profiles/r4_dedup)
+  // skinny (one side <= 128 rows) with a long K: the 256x128 / 128x256 stream tile (MFMA work padded to 128, not
+  // 256 rows; 2 k-tiles in flight per CU): 500x100x900k 208.7 vs 213.9 us, 12x500x100x100k 290.5 vs 292.9,
+  // 4096x128x16k 38.4 vs 40.7 (8-phase) / 43.8 (128^2) (profiles/r5_stream)
+  if (std::max(M, N) >= 192 && std::min(M, N) <= 128 && ksteps >= 256) return M >= N ? 3 : 4;
   if ((M >= 192 || N >= 192) && std::min(M, N) >= 64 && ksteps >= 1024) return 2;
   return 0;
+}
+
+// Macro tile of a config: 0 = 128x128, 2 = 256x256 8-phase, 3 = 256x128 stream, 4 = 128x256 stream.
+static void cfg_tile(int cfg, int& tbm, int& tbn) {
+  tbm = cfg == 2 || cfg == 3 ? 256 : nsdb::BM;
+  tbn = cfg == 2 || cfg == 4 ? 256 : nsdb::BN;
 }
 
 static int resolve_cfg(int cfg, int M, int N, int K, int batch) { return cfg < 0 ? pick_cfg(M, N, K, batch) : cfg; }
@@ -929,15 +1036,16 @@ static int resolve_cfg(int cfg, int M, int N, int K, int batch) { return cfg < 0
 // Number of split-K slices the launcher will use for config `cfg` (-1 auto); the caller sizes the workspace.
 int nsdb_gemm_splits(int M, int N, int K, int batch, int cfg) {
   cfg = resolve_cfg(cfg, M, N, K, batch);
-  const int tbm = cfg ? 256 : nsdb::BM, tbn = cfg ? 256 : nsdb::BN;
+  int tbm, tbn;
+  cfg_tile(cfg, tbm, tbn);
   const int tiles = ((M + tbm - 1) / tbm) * ((N + tbn - 1) / tbn) * batch;
   const int ksteps = (K + nsdb::BK - 1) / nsdb::BK;
   // fill the chip: 256 CUs x (2 blocks of 128^2 | 1 block of 256^2); keep >= 8 k-steps per split
-  const int target = cfg ? 256 : 512;
+  const int target = cfg ? 256 : 512;   // the 256^2 and stream tiles run one block per CU
   int splits = 1;
   // >= 3/4 of the chip busy: a split's f32 slabs + reduce pass cost more than the idle CUs (1000x14588x1024:
   // 51 us + 24 us reduce with 2 splits vs 60 us unsplit)
-  if (tiles < target && !(cfg && tiles >= 192)) {
+  if (tiles < target && !(cfg == 2 && tiles >= 192)) {
     // round DOWN: tiles * splits stays within one wave of resident workgroups. Rounding up left a
     // handful of workgroups for a second, nearly empty wave (6000x100x100k: 47 tiles x 11 splits =
     // 517 WGs ran 456 us; x 10 = 470 WGs fit one wave)
@@ -954,7 +1062,8 @@ int nsdb_gemm_splits(int M, int N, int K, int batch, int cfg) {
 // Workgroups of the launch nsdb_gemm_nt_bf16 makes for this shape (splits <= 0: the launcher's own choice).
 int nsdb_gemm_launch_wgs(int M, int N, int K, int batch, int splits, int cfg) {
   cfg = resolve_cfg(cfg, M, N, K, batch);
-  const int tbm = cfg ? 256 : nsdb::BM, tbn = cfg ? 256 : nsdb::BN;
+  int tbm, tbn;
+  cfg_tile(cfg, tbm, tbn);
   const int ksteps = (K + nsdb::BK - 1) / nsdb::BK;
   if (splits <= 0) splits = nsdb_gemm_splits(M, N, K, batch, cfg);
   splits = std::max(1, splits);
@@ -1022,7 +1131,7 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
   if (splits > 1 && ws == nullptr) return -3;
   if (accumulate && !out_f32) return -4;                                // C += A.B^T only into f32
   const int cfg = resolve_cfg(opts ? opts->cfg : -1, M, N, K, batch);
-  if (cfg != 0 && cfg != 2) return -8;                                  // not a production config
+  if (cfg < 0 || cfg > 4 || cfg == 1) return -8;                      // not a production config
   nsdb::GemmParams p;
   p.A = (const unsigned short*)A; p.B = (const unsigned short*)B; p.C = C; p.ws = ws; p.bias = bias;
   p.lda = lda; p.ldb = ldb; p.ldc = ldc; p.sA = sA; p.sB = sB; p.sC = sC; p.sBias = sBias;
@@ -1042,7 +1151,8 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
   p.stamps = nullptr; p.adapt = nullptr;
   p.signal = nullptr; p.signal_value = 0; p.steal_cnt = nullptr; p.steal_tq = 0; p.steal_ch = 2;
   if (seg_k > 0 && (seg_k % p.kchunk != 0 || seg_k % nsdb::BK != 0)) return -5;   // a split must not cross a segment
-  const int tbm = cfg ? 256 : nsdb::BM, tbn = cfg ? 256 : nsdb::BN;
+  int tbm, tbn;
+  cfg_tile(cfg, tbm, tbn);
   p.tiles_m = (M + tbm - 1) / tbm;
   p.tiles_n = (N + tbn - 1) / tbn;
   p.vec_ws = (N % 4 == 0) ? 1 : 0;
@@ -1061,6 +1171,18 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
       p.pf_bytes = opts->pf_bytes;
     }
     hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<0>, grid, dim3(512), 0, stream, p);
+  } else if (cfg == 3 || cfg == 4) {
+    // contiguous K chunks per split; k-interleaved splits on request (GemmOpts::kinter, unsegmented B only: a split
+    // must stay inside one segment). A/B in profiles/r5_stream: interleaving wins 3 % at M = 1000, N <= 128 and
+    // loses 4-5 % on the batched dedup panels, so it is not the default.
+    const bool ki = seg_k == 0 && p.splits > 1 && opts && opts->kinter;
+    if (cfg == 3) {
+      if (ki) hipLaunchKernelGGL((nsdb::gemm_nt_stream_kernel<256, 128, 4, 2, 3, true>), grid, dim3(512), 0, stream, p);
+      else hipLaunchKernelGGL((nsdb::gemm_nt_stream_kernel<256, 128, 4, 2, 3, false>), grid, dim3(512), 0, stream, p);
+    } else {
+      if (ki) hipLaunchKernelGGL((nsdb::gemm_nt_stream_kernel<128, 256, 2, 4, 3, true>), grid, dim3(512), 0, stream, p);
+      else hipLaunchKernelGGL((nsdb::gemm_nt_stream_kernel<128, 256, 2, 4, 3, false>), grid, dim3(512), 0, stream, p);
+    }
   } else {
     hipLaunchKernelGGL((nsdb::gemm_nt_tile_kernel<128, 128, 2, 2>), grid, dim3(256), 0, stream, p);
   }

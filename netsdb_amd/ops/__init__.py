@@ -100,7 +100,8 @@ def gemm_nt(A, B, bias=None, bias_mode=BIAS_NONE, act=ACT_NONE, out_dtype=torch.
             dropout=0.0, seed=0, splits=0, out=None, accumulate=False, cfg=None, epi=None):
     """epilogue(alpha * A @ B^T) [+ out when accumulate]: A [..,M,K], B [..,N,K] (K-contiguous),
     bias f32 per row/col. ``accumulate`` adds into an existing f32 ``out`` (C += A.B^T). ``cfg`` forces the
-    tile config of THIS call (0 = 128x128, 2 = 256x256 8-phase; None = auto); ``epi`` the 8-phase kernel's
+    tile config of THIS call (0 = 128x128, 2 = 256x256 8-phase, 3 / 4 = 256x128 / 128x256 skinny long-K stream;
+    None = auto); ``epi`` the 8-phase kernel's
     unsplit epilogue (0 = LDS-staged, 1 = direct register stores; None = auto: direct). An operand prefetch armed on
     the current stream (streams.arm_operand_prefetch: a later kernel's operand read into the Infinity Cache by this
     launch's workgroups as they finish) is handed to this launch when it is long enough to take it — per call and

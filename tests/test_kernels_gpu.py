@@ -30,7 +30,7 @@ def test_gemm_identity_asymmetric():
     torch.testing.assert_close(C, B.float().t().contiguous(), rtol=0, atol=0)
 
 
-@pytest.fixture(params=[None, 0, 2], ids=["auto", "tile128", "tile256_8ph"])
+@pytest.fixture(params=[None, 0, 2, 3, 4], ids=["auto", "tile128", "tile256_8ph", "stream256x128", "stream128x256"])
 def gemm_cfg(request):
     """Per-call tile config (ops.gemm_nt(cfg=...)): the production configs of the kernel library."""
     return request.param
@@ -87,12 +87,28 @@ def test_gemm_8ph_direct_epilogue_matches_lds_staged(M, N, K, mode, act, dropout
     assert (wide[:, N:] == -7.0).all()
 
 
-def test_gemm_batched_strided():
+def test_gemm_batched_strided(gemm_cfg):
     torch.manual_seed(2)
     A = torch.randn(3, 130, 200, device=DEV).to(torch.bfloat16)[:, :, :192]   # row stride 200 > K
     B = torch.randn(3, 70, 192, device=DEV).to(torch.bfloat16)
-    C = ops.gemm_nt(A, B, out_dtype=torch.float32)
+    C = ops.gemm_nt(A, B, out_dtype=torch.float32, cfg=gemm_cfg)
     _close(C, _ref_gemm(A, B), tol=1e-2)
+
+
+@pytest.mark.parametrize("M,N,K,batch", [(500, 100, 90000, 1), (100, 500, 40000, 1), (500, 100, 10000, 4),
+                                         (1000, 64, 60000, 1), (6000, 100, 20000, 1), (300, 8, 20000, 1),
+                                         (40, 2000, 17000, 1)])
+def test_gemm_stream_skinny_long_k(M, N, K, batch):
+    """The skinny long-K stream tiles (cfg 3: 256x128, cfg 4: 128x256; the dedup scoring shapes, scaled down)
+    against the fp32 reference and bit-exact against each other's split partition: same k-tiles, same order."""
+    torch.manual_seed(11)
+    shp = (batch,) if batch > 1 else ()
+    A = (torch.rand(*shp, M, K, device=DEV) - 0.5).to(torch.bfloat16)
+    B = (torch.rand(*shp, N, K, device=DEV) - 0.5).to(torch.bfloat16)
+    ref = _ref_gemm(A, B)
+    for cfg in (3, 4, 5, 6, None):
+        C = ops.gemm_nt(A, B, out_dtype=torch.float32, cfg=cfg)
+        _close(C, ref, tol=1e-2)
 
 
 def test_gemm_accumulate(gemm_cfg):
