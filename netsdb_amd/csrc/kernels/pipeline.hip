@@ -28,70 +28,9 @@
 //    reads back a few KB, no per-workgroup partials and no second merge pass. A table overflow raises status[0]:
 //    the stage then runs the unfused path (more groups than this kernel is for). status[1] counts the kept rows.
 #include "common.h"
+#include "pipeline_core.h"
 
 namespace nsdb_pipe {
-
-constexpr int NREG = 16, MAXINS = 48, MAXCOL = 10, MAXSTR = 4, FMAX = 8, KSLOT = 4, CAP = 256, NTHR = 256;
-constexpr int GCAP = 2048;             // global table slots (power of two)
-constexpr int NREG_SMALL = 8;          // the 8-register x 4-row shape
-constexpr long long EMPTY = (long long)0x8000000000000000ULL;
-constexpr int IMM_REG = -2;            // operand register meaning "the instruction's immediate"
-// tile-mode instruction flags (Ins.pad; the operand fields are then byte offsets of T-row register vectors)
-constexpr int TF_AIMM = 1, TF_ANONE = 2, TF_BIMM = 4, TF_BNONE = 8, TF_C = 16;
-
-enum Op : int {
-  OP_NOP = 0, OP_CONST, OP_ADDF, OP_SUBF, OP_MULF, OP_DIVF, OP_ADDI, OP_SUBI, OP_MULI, OP_I2F,
-  OP_LTF, OP_LEF, OP_GTF, OP_GEF, OP_EQF, OP_NEF, OP_LTI, OP_LEI, OP_GTI, OP_GEI, OP_EQI, OP_NEI,
-  OP_AND, OP_OR, OP_NOT, OP_PACK, OP_SEQ, OP_SPRE, OP_SSUF, OP_SEL, OP_NEGF, OP_RNGF, OP_RNGI
-};
-constexpr int KPOOL = 16;              // second immediates: range upper bounds
-enum ColKind : int { C_F64 = 0, C_I64, C_I32, C_F32, C_U8, C_SCODE, C_SREF };
-
-struct Ins {
-  int op, dst, a, b;
-  int c;                         // c >= 0: compares AND their result with register c
-  int pad;                       // bits 0-7: tile-mode operand flags (TF_*); bits 8+: aux (range: kpool index | mode << 8)
-  long long imm;
-};
-struct Col {
-  const void* p;                 // numeric column
-  const long long* st;           // string column: row starts / ends into dat
-  const long long* en;
-  const unsigned char* dat;
-  int kind, late, L;
-  int raw_off, aux_off;          // tile kernels: LDS byte offsets of the column's DMA image (string starts / ends)
-  int contig;                    // strings: en == st + 1 (one offsets array): the tile DMAs the starts only
-};
-struct PipeArgs {
-  Ins ins[MAXINS + 1];           // + a NOP sentinel (the dispatch prefetches one instruction ahead)
-  Col col[MAXCOL];
-  const unsigned char* lit;      // literal pool of the string ops
-  long long n;
-  int nins_a, nins, ncol, keep_reg, key_reg, nval, agg_op, nreg;
-  int val_reg[FMAX];
-  long long kpool[KPOOL];        // range ops' upper bounds
-  int tile, lds_bytes;           // tile / hybrid kernels: rows per tile, dynamic LDS bytes
-  int kmode, pad2;               // 0 register kernels, 1 LDS-tile kernels, 2 hybrid (LDS-DMA columns, VGPR registers)
-  unsigned long long* table;     // [2 + GCAP + GCAP * FMAX]: status (overflow, kept rows), keys, values (f64 bits)
-};
-
-typedef unsigned long long u64;
-// The register file of one row slot: NR 64-bit registers as ONE vector value (NR VGPR pairs).
-template <int NR>
-struct RF {
-  typedef unsigned long long vec __attribute__((ext_vector_type(NR)));
-};
-
-__device__ __forceinline__ double u2f(u64 x) { return __longlong_as_double((long long)x); }
-__device__ __forceinline__ u64 f2u(double x) { return (u64)__double_as_longlong(x); }
-
-// Short-string code exactly as StringColumn.short_codes / str_pack (bytes big-endian in the low 8L bits, << 3 | len)
-__device__ __forceinline__ u64 short_code(const unsigned char* d, long long s, long long len, int L) {
-  if (len > L) return (u64)-1;
-  u64 c = 0;
-  for (int b = 0; b < L; ++b) c |= (b < len ? (u64)d[s + b] : 0ull) << (8 * (L - 1 - b));
-  return (c << 3) | (u64)len;
-}
 
 // Every column of the pass (LATE: the late columns; else the early ones) into its register. Round 1 issues every
 // row load (numeric values; string starts and the low words of their ends) before any is used; round 2 turns the
@@ -232,19 +171,6 @@ __device__ __forceinline__ void hyb_load(const PipeArgs& a, long long row0, long
   }
 }
 
-__device__ __forceinline__ bool str_match(const unsigned char* d, u64 ref, const unsigned char* lit, long long imm,
-                                          int mode) {
-  const long long s = (long long)(ref >> 24);
-  const int len = (int)(ref & 0xFFFFFF);
-  const unsigned char* l = lit + (imm >> 16);
-  const int ll = (int)(imm & 0xFFFF);
-  if (mode == 0 ? len != ll : len < ll) return false;
-  const long long o = mode == 2 ? s + len - ll : s;     // suffix: compare the last ll bytes
-  for (int b = 0; b < ll; ++b)
-    if (d[o + b] != l[b]) return false;
-  return true;
-}
-
 template <int NR>
 __device__ __forceinline__ u64 operand(const typename RF<NR>::vec& R, int k, long long imm) {
   return k == IMM_REG ? (u64)imm : (k >= 0 ? R[k] : 0ull);
@@ -335,58 +261,6 @@ __device__ __forceinline__ void run(const PipeArgs& a, typename RF<NR>::vec (&R)
     for (int j = 0; j < ROWS; ++j) R[j][dst] = z[j];
     cur = nxt;
   }
-}
-
-__device__ __forceinline__ unsigned slot_hash(long long k) {
-  u64 z = (u64)k * 0x9E3779B97F4A7C15ull;
-  return (unsigned)(z >> 40);
-}
-
-__device__ __forceinline__ double acc_op(double a, double b, int op) {
-  return op == 0 ? a + b : (op == 1 ? fmin(a, b) : fmax(a, b));
-}
-
-// *p = op(*p, v) atomically (LDS or global: the pointer's address space is known after inlining). Sums use the
-// hardware f64 add atomic, min / max a 64-bit CAS loop.
-__device__ __forceinline__ void atomic_acc(double* p, double v, int op) {
-  if (op == 0) {
-    atomicAdd(p, v);
-    return;
-  }
-  u64* q = reinterpret_cast<u64*>(p);
-  u64 old = *q;
-  while (true) {
-    const double cur = u2f(old);
-    const double nv = acc_op(cur, v, op);
-    if (nv == cur) return;
-    const u64 got = atomicCAS(q, old, f2u(nv));
-    if (got == old) return;
-    old = got;
-  }
-}
-
-// Linear-probing insert of (key, values) into a table of cap slots (LDS or global). False: the table is full.
-template <int F, int STRIDE = FMAX>
-__device__ __forceinline__ bool table_insert(long long* tk, double* tv, unsigned cap, long long key, const double (&v)[F],
-                                             int nval, int op) {
-  unsigned h = slot_hash(key) & (cap - 1);
-  for (unsigned p = 0; p < cap; ++p) {
-    const long long prev = (long long)atomicCAS(reinterpret_cast<u64*>(tk + h), (u64)EMPTY, (u64)key);
-    if (prev == EMPTY || prev == key) {
-#pragma unroll
-      for (int f = 0; f < F; ++f)
-        if (f < nval) atomic_acc(tv + (size_t)h * STRIDE + f, v[f], op);
-      return true;
-    }
-    h = (h + 1) & (cap - 1);
-  }
-  return false;
-}
-
-__device__ __forceinline__ double wave_reduce(double v, int op) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = acc_op(v, __shfl_xor(v, o), op);
-  return v;
 }
 
 template <int F, int NR, int ROWS, bool HYB>
@@ -983,6 +857,14 @@ int nsdb_pipe_agg(const void* args, int grid, hipStream_t st) {
   } else {
     nsdb_pipe::launch_agg<nsdb_pipe::FMAX>(a, grid, st);
   }
+  return (int)hipGetLastError();
+}
+
+// The global result table's initial state (the run-time compiled aggregation kernels are launched by the binding).
+int nsdb_pipe_init(unsigned long long* table, int op, hipStream_t st) {
+  if (table == nullptr || op < 0 || op > 2) return -1;
+  hipLaunchKernelGGL(nsdb_pipe::pipe_init_kernel, dim3(nsdb_pipe::GCAP / nsdb_pipe::NTHR), dim3(nsdb_pipe::NTHR), 0, st,
+                     table, op);
   return (int)hipGetLastError();
 }
 

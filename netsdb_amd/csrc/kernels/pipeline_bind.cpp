@@ -5,8 +5,11 @@
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
 
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <tuple>
 #include <vector>
@@ -15,6 +18,7 @@ extern "C" {
 int nsdb_pipe_sizes(int* out);
 int nsdb_pipe_agg(const void* args, int grid, hipStream_t st);
 int nsdb_pipe_mask(const void* args, unsigned char* mask, int grid, hipStream_t st);
+int nsdb_pipe_init(unsigned long long* table, int op, hipStream_t st);
 }
 
 namespace {
@@ -274,14 +278,71 @@ void choose_tile(PipeArgs& a, int static_bytes, int64_t force, int reg_static_by
   }
 }
 
+// ---- run-time compiled kernels (pipeline_core.h jit_agg_body / jit_mask_body; sources from execution/pipeline.py)
+// hiprtc compile of one generated source whose only include is pipeline_core.h (passed as text): the gfx950 code
+// object, with the flags of the ahead-of-time kernels (-O3, hardware float atomics).
+pybind11::bytes jit_compile(const std::string& src, const std::string& header) {
+  hiprtcProgram prog;
+  const char* hdr[1] = {header.c_str()};
+  const char* names[1] = {"pipeline_core.h"};
+  TORCH_CHECK(hiprtcCreateProgram(&prog, src.c_str(), "nsdb_jit.hip", 1, hdr, names) == HIPRTC_SUCCESS,
+              "jit_compile: hiprtcCreateProgram failed");
+  const char* env = std::getenv("PYTORCH_ROCM_ARCH");
+  const std::string arch = std::string("--offload-arch=") + (env && *env ? env : "gfx950");
+  const char* opts[] = {arch.c_str(), "-O3", "-std=c++17", "-munsafe-fp-atomics"};
+  const hiprtcResult r = hiprtcCompileProgram(prog, 4, opts);
+  size_t ls = 0;
+  hiprtcGetProgramLogSize(prog, &ls);
+  std::string log(ls, '\0');
+  if (ls) hiprtcGetProgramLog(prog, &log[0]);
+  if (r != HIPRTC_SUCCESS) {
+    hiprtcDestroyProgram(&prog);
+    TORCH_CHECK(false, "jit_compile: ", hiprtcGetErrorString(r), "\n", log);
+  }
+  size_t n = 0;
+  hiprtcGetCodeSize(prog, &n);
+  std::string code(n, '\0');
+  hiprtcGetCode(prog, &code[0]);
+  hiprtcDestroyProgram(&prog);
+  return pybind11::bytes(code);
+}
+
+// Load a code object and return the kernel `name` as an opaque handle (modules stay loaded for the process).
+int64_t jit_load(const std::string& code, const std::string& name) {
+  static std::mutex mu;
+  static std::vector<hipModule_t> modules;
+  hipModule_t m;
+  TORCH_CHECK(hipModuleLoadData(&m, code.data()) == hipSuccess, "jit_load: hipModuleLoadData failed");
+  hipFunction_t f;
+  TORCH_CHECK(hipModuleGetFunction(&f, m, name.c_str()) == hipSuccess, "jit_load: no kernel ", name);
+  std::lock_guard<std::mutex> g(mu);
+  modules.push_back(m);
+  return reinterpret_cast<int64_t>(f);
+}
+
 // Returns the global result table, int64 [2 + GCAP * (1 + FMAX)]: status (overflow flag, kept rows), GCAP keys
 // (INT64_MIN = free slot), then GCAP x FMAX f64 values (bit patterns). The host reads it back in one copy.
 torch::Tensor pipe_agg(torch::Tensor prog, int64_t nins_a, ColList cols, torch::Tensor lit, int64_t n, int64_t keep_reg,
                        int64_t key_reg, std::vector<int64_t> val_regs, int64_t agg_op, int64_t max_wg, int64_t tile,
-                       std::vector<int64_t> kpool) {
+                       std::vector<int64_t> kpool, int64_t jit, int64_t jit_nreg, int64_t jit_rows) {
   const int ROWS = 4, NTHR = sizes(7), GCAP = sizes(8), CAP = sizes(4);
   PipeArgs a;
   fill_args(a, prog, nins_a, cols, lit, n, keep_reg, key_reg, val_regs, agg_op, kpool);
+  if (jit != 0) {                                   // the run-time compiled kernel of exactly this program shape
+    TORCH_CHECK(a.nreg == jit_nreg && jit_rows >= 1 && jit_rows <= 16,
+                "pipe_agg: compiled kernel for ", jit_nreg, " registers, the program uses ", a.nreg);
+    const long long per = (long long)NTHR * jit_rows * 4;
+    const int nwg = (int)std::max<long long>(1, std::min<long long>(max_wg > 0 ? max_wg : 2048, (n + per - 1) / per));
+    auto table = torch::empty({2 + (long long)GCAP * (1 + FMAX)}, lit.options().dtype(torch::kInt64));
+    a.table = reinterpret_cast<unsigned long long*>(table.data_ptr<int64_t>());
+    hipStream_t st = c10::hip::getCurrentHIPStream().stream();
+    TORCH_CHECK(nsdb_pipe_init(a.table, a.agg_op, st) == 0, "pipe_agg: table init failed");
+    void* params[] = {&a};
+    TORCH_CHECK(hipModuleLaunchKernel(reinterpret_cast<hipFunction_t>(jit), nwg, 1, 1, NTHR, 1, 1, 0, st, params,
+                                      nullptr) == hipSuccess,
+                "pipe_agg: compiled kernel launch failed");
+    return table;
+  }
   const int F = a.nval <= 2 ? 2 : (a.nval <= 4 ? 4 : (a.nval <= 6 ? 6 : FMAX));
   choose_tile(a, CAP * (8 + 8 * F) + 16, tile, CAP * (8 + 8 * FMAX) + 16);
   if (a.kmode == 1) predecode_tile(a);
@@ -297,11 +358,26 @@ torch::Tensor pipe_agg(torch::Tensor prog, int64_t nins_a, ColList cols, torch::
 
 // The predicate program's keep flag per row (uint8 [n]); key / values unused.
 torch::Tensor pipe_mask(torch::Tensor prog, ColList cols, torch::Tensor lit, int64_t n, int64_t keep_reg, int64_t tile,
-                        std::vector<int64_t> kpool) {
+                        std::vector<int64_t> kpool, int64_t jit, int64_t jit_nreg, int64_t jit_rows) {
   const int ROWS = 4, NTHR = sizes(7);
   PipeArgs a;
   fill_args(a, prog, prog.size(0), cols, lit, n, keep_reg, -1, {}, 0, kpool);
   for (int c = 0; c < a.ncol; ++c) a.col[c].late = 0;      // the mask pass loads every column up front
+  if (jit != 0) {
+    TORCH_CHECK(a.nreg == jit_nreg && jit_rows >= 1 && jit_rows <= 16,
+                "pipe_mask: compiled kernel for ", jit_nreg, " registers, the program uses ", a.nreg);
+    auto mask = torch::empty({n}, lit.options().dtype(torch::kUInt8));
+    if (n > 0) {
+      const long long per = (long long)NTHR * jit_rows * 4;
+      const int nwg = (int)std::max<long long>(1, std::min<long long>(4096, (n + per - 1) / per));
+      unsigned char* mp = mask.data_ptr<uint8_t>();
+      void* params[] = {&a, &mp};
+      TORCH_CHECK(hipModuleLaunchKernel(reinterpret_cast<hipFunction_t>(jit), nwg, 1, 1, NTHR, 1, 1, 0,
+                                        c10::hip::getCurrentHIPStream().stream(), params, nullptr) == hipSuccess,
+                  "pipe_mask: compiled kernel launch failed");
+    }
+    return mask;
+  }
   choose_tile(a, 0, tile, 0);
   if (a.kmode == 1) predecode_tile(a);
   auto mask = torch::empty({n}, lit.options().dtype(torch::kUInt8));
@@ -319,11 +395,17 @@ torch::Tensor pipe_mask(torch::Tensor prog, ColList cols, torch::Tensor lit, int
 void register_pipeline(pybind11::module& m) {
   m.def("pipe_mask", &pipe_mask, "fused filter predicate (pipeline.hip): keep flag per row (uint8)",
         pybind11::arg("prog"), pybind11::arg("cols"), pybind11::arg("lit"), pybind11::arg("n"), pybind11::arg("keep_reg"),
-        pybind11::arg("tile") = -1, pybind11::arg("kpool") = std::vector<int64_t>());
+        pybind11::arg("tile") = -1, pybind11::arg("kpool") = std::vector<int64_t>(), pybind11::arg("jit") = 0,
+        pybind11::arg("jit_nreg") = 0, pybind11::arg("jit_rows") = 0);
   m.def("pipe_agg", &pipe_agg,
         "fused scan -> filter -> project -> low-cardinality aggregate (pipeline.hip): the global result table "
         "int64 [2 + GCAP * 9] = status (overflow, kept rows), keys, f64 values [GCAP, 8]",
         pybind11::arg("prog"), pybind11::arg("nins_a"), pybind11::arg("cols"), pybind11::arg("lit"), pybind11::arg("n"),
         pybind11::arg("keep_reg"), pybind11::arg("key_reg"), pybind11::arg("val_regs"), pybind11::arg("agg_op") = 0,
-        pybind11::arg("max_wg") = 0, pybind11::arg("tile") = -1, pybind11::arg("kpool") = std::vector<int64_t>());
+        pybind11::arg("max_wg") = 0, pybind11::arg("tile") = -1, pybind11::arg("kpool") = std::vector<int64_t>(),
+        pybind11::arg("jit") = 0, pybind11::arg("jit_nreg") = 0, pybind11::arg("jit_rows") = 0);
+  m.def("jit_compile", &jit_compile, "hiprtc compile of a generated pipeline kernel source (gfx950 code object)",
+        pybind11::arg("src"), pybind11::arg("header"));
+  m.def("jit_load", &jit_load, "load a code object; the named kernel as an opaque handle for pipe_agg / pipe_mask(jit=)",
+        pybind11::arg("code"), pybind11::arg("name"));
 }

@@ -1,0 +1,302 @@
+// Shared definitions of the fused relational pipeline (pipeline.hip) and the bodies of its run-time compiled kernels.
+//
+// This header is compiled twice: into the ahead-of-time kernels (pipeline.hip, hipcc) and, as the only include of
+// every run-time generated kernel source (execution/pipeline.py jit_source), by hiprtc inside the process. It
+// therefore includes nothing and uses only HIP device built-ins.
+//
+// Run-time compiled kernels (jit_agg_body / jit_mask_body): the host turns a stage's register program into a
+// program policy P whose loads, instructions, keep flag, key and values are straight-line C++ on compile-time
+// register and column indices (immediates stay kernel arguments, so one compiled kernel serves every literal of a
+// query shape). The interpreter's per-instruction dispatch (a scalar load, a branch and an indirect register access
+// per instruction and row block: 32-45 us per instruction per 60 M rows, profiles/r5_tpch/pipe_micro_modes.log)
+// disappears, and the compiler schedules every row load of an iteration ahead of its first use.
+#pragma once
+
+namespace nsdb_pipe {
+
+constexpr int NREG = 16, MAXINS = 48, MAXCOL = 10, MAXSTR = 4, FMAX = 8, KSLOT = 4, CAP = 256, NTHR = 256;
+constexpr int GCAP = 2048;             // global table slots (power of two)
+constexpr int NREG_SMALL = 8;          // the 8-register x 4-row shape
+constexpr long long EMPTY = (long long)0x8000000000000000ULL;
+constexpr int IMM_REG = -2;            // operand register meaning "the instruction's immediate"
+// tile-mode instruction flags (Ins.pad; the operand fields are then byte offsets of T-row register vectors)
+constexpr int TF_AIMM = 1, TF_ANONE = 2, TF_BIMM = 4, TF_BNONE = 8, TF_C = 16;
+
+enum Op : int {
+  OP_NOP = 0, OP_CONST, OP_ADDF, OP_SUBF, OP_MULF, OP_DIVF, OP_ADDI, OP_SUBI, OP_MULI, OP_I2F,
+  OP_LTF, OP_LEF, OP_GTF, OP_GEF, OP_EQF, OP_NEF, OP_LTI, OP_LEI, OP_GTI, OP_GEI, OP_EQI, OP_NEI,
+  OP_AND, OP_OR, OP_NOT, OP_PACK, OP_SEQ, OP_SPRE, OP_SSUF, OP_SEL, OP_NEGF, OP_RNGF, OP_RNGI
+};
+constexpr int KPOOL = 16;              // second immediates: range upper bounds
+enum ColKind : int { C_F64 = 0, C_I64, C_I32, C_F32, C_U8, C_SCODE, C_SREF };
+
+struct Ins {
+  int op, dst, a, b;
+  int c;                         // c >= 0: compares AND their result with register c
+  int pad;                       // bits 0-7: tile-mode operand flags (TF_*); bits 8+: aux (range: kpool index | mode << 8)
+  long long imm;
+};
+struct Col {
+  const void* p;                 // numeric column
+  const long long* st;           // string column: row starts / ends into dat
+  const long long* en;
+  const unsigned char* dat;
+  int kind, late, L;
+  int raw_off, aux_off;          // tile kernels: LDS byte offsets of the column's DMA image (string starts / ends)
+  int contig;                    // strings: en == st + 1 (one offsets array): the tile DMAs the starts only
+};
+struct PipeArgs {
+  Ins ins[MAXINS + 1];           // + a NOP sentinel (the dispatch prefetches one instruction ahead)
+  Col col[MAXCOL];
+  const unsigned char* lit;      // literal pool of the string ops
+  long long n;
+  int nins_a, nins, ncol, keep_reg, key_reg, nval, agg_op, nreg;
+  int val_reg[FMAX];
+  long long kpool[KPOOL];        // range ops' upper bounds
+  int tile, lds_bytes;           // tile / hybrid kernels: rows per tile, dynamic LDS bytes
+  int kmode, pad2;               // 0 register kernels, 1 LDS-tile kernels, 2 hybrid (LDS-DMA columns, VGPR registers)
+  unsigned long long* table;     // [2 + GCAP + GCAP * FMAX]: status (overflow, kept rows), keys, values (f64 bits)
+};
+
+typedef unsigned long long u64;
+// The register file of one row slot: NR 64-bit registers as ONE vector value (NR VGPR pairs).
+template <int NR>
+struct RF {
+  typedef unsigned long long vec __attribute__((ext_vector_type(NR)));
+};
+
+__device__ __forceinline__ double u2f(u64 x) { return __longlong_as_double((long long)x); }
+__device__ __forceinline__ u64 f2u(double x) { return (u64)__double_as_longlong(x); }
+
+// Short-string code exactly as StringColumn.short_codes / str_pack (bytes big-endian in the low 8L bits, << 3 | len)
+__device__ __forceinline__ u64 short_code(const unsigned char* d, long long s, long long len, int L) {
+  if (len > L) return (u64)-1;
+  u64 c = 0;
+  for (int b = 0; b < L; ++b) c |= (b < len ? (u64)d[s + b] : 0ull) << (8 * (L - 1 - b));
+  return (c << 3) | (u64)len;
+}
+
+__device__ __forceinline__ bool str_match(const unsigned char* d, u64 ref, const unsigned char* lit, long long imm,
+                                          int mode) {
+  const long long s = (long long)(ref >> 24);
+  const int len = (int)(ref & 0xFFFFFF);
+  const unsigned char* l = lit + (imm >> 16);
+  const int ll = (int)(imm & 0xFFFF);
+  if (mode == 0 ? len != ll : len < ll) return false;
+  const long long o = mode == 2 ? s + len - ll : s;     // suffix: compare the last ll bytes
+  for (int b = 0; b < ll; ++b)
+    if (d[o + b] != l[b]) return false;
+  return true;
+}
+
+__device__ __forceinline__ unsigned slot_hash(long long k) {
+  u64 z = (u64)k * 0x9E3779B97F4A7C15ull;
+  return (unsigned)(z >> 40);
+}
+
+__device__ __forceinline__ double acc_op(double a, double b, int op) {
+  return op == 0 ? a + b : (op == 1 ? fmin(a, b) : fmax(a, b));
+}
+
+// *p = op(*p, v) atomically (LDS or global: the pointer's address space is known after inlining). Sums use the
+// hardware f64 add atomic, min / max a 64-bit CAS loop.
+__device__ __forceinline__ void atomic_acc(double* p, double v, int op) {
+  if (op == 0) {
+    atomicAdd(p, v);
+    return;
+  }
+  u64* q = reinterpret_cast<u64*>(p);
+  u64 old = *q;
+  while (true) {
+    const double cur = u2f(old);
+    const double nv = acc_op(cur, v, op);
+    if (nv == cur) return;
+    const u64 got = atomicCAS(q, old, f2u(nv));
+    if (got == old) return;
+    old = got;
+  }
+}
+
+// Linear-probing insert of (key, values) into a table of cap slots (LDS or global). False: the table is full.
+template <int F, int STRIDE = FMAX>
+__device__ __forceinline__ bool table_insert(long long* tk, double* tv, unsigned cap, long long key, const double (&v)[F],
+                                             int nval, int op) {
+  unsigned h = slot_hash(key) & (cap - 1);
+  for (unsigned p = 0; p < cap; ++p) {
+    const long long prev = (long long)atomicCAS(reinterpret_cast<u64*>(tk + h), (u64)EMPTY, (u64)key);
+    if (prev == EMPTY || prev == key) {
+#pragma unroll
+      for (int f = 0; f < F; ++f)
+        if (f < nval) atomic_acc(tv + (size_t)h * STRIDE + f, v[f], op);
+      return true;
+    }
+    h = (h + 1) & (cap - 1);
+  }
+  return false;
+}
+
+__device__ __forceinline__ double wave_reduce(double v, int op) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = acc_op(v, __shfl_xor(v, o), op);
+  return v;
+}
+
+
+// ---------------------------------------------------------------- run-time compiled (JIT) kernel bodies
+// P (generated): F, NR, ROWS; load<LATE, FULL>(a, row, m, R) (the columns of one pass into their registers, 0 where m
+// is false; FULL: every row of the block is in range and unmasked, so the loads carry no per-row exec mask); run_a / run_b (the predicate / key-and-value segments); keep(r), key(r), vals(r, v). Registers are a
+// plain u64 [ROWS][NR] array indexed by constants only, so every register lives in VGPRs.
+//
+// The aggregation is the register kernels' (pipe_agg_kernel): KSLOT register slots per thread, the workgroup's LDS
+// table, one merge into the global table; status[0] = overflow, status[1] = kept rows.
+template <typename P>
+__device__ __forceinline__ void jit_agg_body(const PipeArgs& a) {
+  constexpr int F = P::F, NR = P::NR, ROWS = P::ROWS;
+  __shared__ long long tk[CAP];
+  __shared__ double tv[CAP * FMAX];
+  __shared__ int s_ovf;
+  __shared__ unsigned long long s_kept;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const double init = a.agg_op == 0 ? 0.0 : (a.agg_op == 1 ? __builtin_inf() : -__builtin_inf());
+  for (int i = tid; i < CAP; i += NTHR) tk[i] = EMPTY;
+  for (int i = tid; i < CAP * FMAX; i += NTHR) tv[i] = init;
+  if (tid == 0) {
+    s_ovf = 0;
+    s_kept = 0;
+  }
+  __syncthreads();
+
+  u64 R[ROWS][NR];
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j)
+#pragma unroll
+    for (int r = 0; r < NR; ++r) R[j][r] = 0ull;
+  long long sk[KSLOT];
+  double sv[KSLOT][F];
+  int used = 0;
+  unsigned kept = 0;
+  bool ovf = false;
+#pragma unroll
+  for (int s = 0; s < KSLOT; ++s) {
+    sk[s] = EMPTY;
+#pragma unroll
+    for (int f = 0; f < F; ++f) sv[s][f] = init;
+  }
+
+  const long long step = (long long)gridDim.x * NTHR * ROWS;
+  for (long long base = (long long)blockIdx.x * NTHR * ROWS; base < a.n; base += step) {
+    long long row[ROWS];
+    bool inr[ROWS], keep[ROWS];
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      row[j] = base + (long long)j * NTHR + tid;
+      inr[j] = row[j] < a.n;
+    }
+    if (base + (long long)NTHR * ROWS <= a.n) P::template load<false, true>(a, row, inr, R);   // whole block: no masks
+    else P::template load<false, false>(a, row, inr, R);
+    P::run_a(a, R);
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      keep[j] = inr[j] && P::keep(R[j]);
+      any |= keep[j];
+      kept += keep[j] ? 1u : 0u;
+    }
+    if (!__builtin_amdgcn_ballot_w64(any)) continue;           // no kept row in this wave
+    P::template load<true, false>(a, row, keep, R);            // late columns: the kept rows only
+    P::run_b(a, R);
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      if (!keep[j]) continue;
+      const long long key = P::key(R[j]);
+      double v[F];
+      P::vals(R[j], v);
+      bool done = false;
+#pragma unroll
+      for (int s = 0; s < KSLOT; ++s) {
+        if (!done && s < used && sk[s] == key) {
+#pragma unroll
+          for (int f = 0; f < F; ++f) sv[s][f] = acc_op(sv[s][f], v[f], a.agg_op);
+          done = true;
+        }
+      }
+      if (!done && used < KSLOT) {
+#pragma unroll
+        for (int s = 0; s < KSLOT; ++s) {
+          if (!done && s == used) {
+            sk[s] = key;
+#pragma unroll
+            for (int f = 0; f < F; ++f) sv[s][f] = v[f];
+            done = true;
+          }
+        }
+        ++used;
+      }
+      if (!done) ovf |= (key == EMPTY) || !table_insert<F>(tk, tv, CAP, key, v, a.nval, a.agg_op);
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < KSLOT; ++s) {
+    bool act = s < used;
+    while (true) {
+      const u64 bal = __builtin_amdgcn_ballot_w64(act);
+      if (!bal) break;
+      const int leader = __builtin_ctzll(bal);
+      const long long kl = __shfl(sk[s], leader);
+      const bool mine = act && sk[s] == kl;
+      double v[F];
+#pragma unroll
+      for (int f = 0; f < F; ++f) v[f] = wave_reduce(mine ? sv[s][f] : init, a.agg_op);
+      if (lane == leader) ovf |= (kl == EMPTY) || !table_insert<F>(tk, tv, CAP, kl, v, a.nval, a.agg_op);
+      act = act && !mine;
+    }
+  }
+  atomicAdd(&s_kept, (unsigned long long)kept);
+  if (ovf) s_ovf = 1;
+  __syncthreads();
+  long long* gk = reinterpret_cast<long long*>(a.table + 2);
+  double* gv = reinterpret_cast<double*>(a.table + 2 + GCAP);
+  for (int i = tid; i < CAP; i += NTHR) {
+    const long long k = tk[i];
+    if (k == EMPTY) continue;
+    double v[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) v[f] = tv[i * FMAX + f];
+    if (!table_insert<F>(gk, gv, GCAP, k, v, a.nval, a.agg_op)) s_ovf = 1;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    if (s_ovf) atomicOr(a.table, 1ull);
+    atomicAdd(a.table + 1, s_kept);
+  }
+}
+
+// Filter only: keep flag per row (every column early, the whole program in run_a).
+template <typename P>
+__device__ __forceinline__ void jit_mask_body(const PipeArgs& a, unsigned char* __restrict__ mask) {
+  constexpr int NR = P::NR, ROWS = P::ROWS;
+  u64 R[ROWS][NR];
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j)
+#pragma unroll
+    for (int r = 0; r < NR; ++r) R[j][r] = 0ull;
+  const int tid = threadIdx.x;
+  const long long step = (long long)gridDim.x * NTHR * ROWS;
+  for (long long base = (long long)blockIdx.x * NTHR * ROWS; base < a.n; base += step) {
+    long long row[ROWS];
+    bool inr[ROWS];
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      row[j] = base + (long long)j * NTHR + tid;
+      inr[j] = row[j] < a.n;
+    }
+    if (base + (long long)NTHR * ROWS <= a.n) P::template load<false, true>(a, row, inr, R);
+    else P::template load<false, false>(a, row, inr, R);
+    P::run_a(a, R);
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j)
+      if (inr[j]) mask[row[j]] = P::keep(R[j]) ? 1 : 0;
+  }
+}
+
+}  // namespace nsdb_pipe

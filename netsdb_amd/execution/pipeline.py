@@ -25,7 +25,10 @@ memory round trip per row block instead of two).
 """
 from __future__ import annotations
 
+import hashlib
+import os
 import struct
+import warnings
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -789,14 +792,247 @@ def _col_args(prog: Program, dev):
     return out
 
 
+# ---------------------------------------------------------------------------------------------- compiled kernels
+# Run-time compilation (pipeline_core.h jit_agg_body / jit_mask_body): a program's loads, instructions, keep flag,
+# key and values become straight-line C++ on compile-time registers and column kinds, compiled once per program
+# shape by hiprtc inside the process (immediates stay kernel arguments: one kernel per query shape, not per literal)
+# and cached in memory and on disk. NSDB_PIPE_JIT=0 keeps the interpreter kernels (TILE) for every stage.
+JIT = os.environ.get("NSDB_PIPE_JIT", "1") != "0"
+JIT_ROWS = 4                                 # rows per thread per iteration of the compiled kernels (JIT_ROWS_SMALL
+JIT_ROWS_SMALL = 8                           # for programs of at most JIT_SMALL_NREG registers)
+JIT_SMALL_NREG = 8
+JIT_STATS = {"compiled": 0, "disk_hits": 0, "launches": 0, "failed": 0}
+_JIT_FN: Dict[str, Optional[int]] = {}       # generated source -> kernel handle (None: compile failed)
+_JIT_HEADER: Optional[str] = None
+_FOPS = {OP_ADDF: "+", OP_SUBF: "-", OP_MULF: "*", OP_DIVF: "/"}
+_IOPS = {OP_ADDI: "+", OP_SUBI: "-", OP_MULI: "*"}
+_FCMPS = {OP_LTF: "<", OP_LEF: "<=", OP_GTF: ">", OP_GEF: ">=", OP_EQF: "==", OP_NEF: "!="}
+_ICMPS = {OP_LTI: "<", OP_LEI: "<=", OP_GTI: ">", OP_GEI: ">=", OP_EQI: "==", OP_NEI: "!="}
+
+
+def _jit_header() -> str:
+    global _JIT_HEADER
+    if _JIT_HEADER is None:
+        path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc", "kernels",
+                            "pipeline_core.h")
+        with open(path) as f:
+            _JIT_HEADER = f.read()
+    return _JIT_HEADER
+
+
+def program_nreg(prog: Program, ncol: int, key_reg: int, val_regs) -> int:
+    """Registers the program touches, exactly as the binding's fill_args counts them (the compiled kernel's NR)."""
+    n = max(1, ncol, prog.keep_reg + 1, key_reg + 1, *(v + 1 for v in val_regs))
+    for (op, dst, a, b, c, imm, _aux) in prog.ins:
+        n = max(n, dst + 1, a + 1, b + 1, c + 1, imm + 1 if op == OP_SEL else 0)
+    return n
+
+
+def _jit_ins(pc: int, ins) -> Optional[str]:
+    """One instruction as a C++ statement on the register row r (the interpreter's semantics, pipeline.hip run)."""
+    op, dst, a, b, c, imm, aux = ins
+
+    def opnd(k):
+        return f"r[{k}]" if k >= 0 else (f"(u64)a.ins[{pc}].imm" if k == IMM else "0ull")
+
+    X, Y = opnd(a), opnd(b)
+    if op == OP_NOP:
+        return None
+    if op == OP_CONST:
+        z = f"(u64)a.ins[{pc}].imm"
+    elif op in _FOPS:
+        z = f"f2u(u2f({X}) {_FOPS[op]} u2f({Y}))"
+    elif op == OP_NEGF:
+        z = f"f2u(-u2f({X}))"
+    elif op in _IOPS:
+        z = f"(u64)((long long){X} {_IOPS[op]} (long long){Y})"
+    elif op == OP_I2F:
+        z = f"f2u((double)(long long){X})"
+    elif op in _FCMPS:
+        z = f"(u64)(u2f({X}) {_FCMPS[op]} u2f({Y}))"
+    elif op in _ICMPS:
+        z = f"(u64)((long long){X} {_ICMPS[op]} (long long){Y})"
+    elif op == OP_AND:
+        z = f"(u64)(({X} != 0ull) & ({Y} != 0ull))"
+    elif op == OP_OR:
+        z = f"(u64)(({X} != 0ull) | ({Y} != 0ull))"
+    elif op == OP_NOT:
+        z = f"(u64)({X} == 0ull)"
+    elif op == OP_PACK:
+        z = f"(({X} << (a.ins[{pc}].imm & 63)) | {Y})"
+    elif op == OP_SEL:
+        z = f"({X} ? {Y} : r[{int(imm)}])"
+    elif op in (OP_RNGF, OP_RNGI):
+        k, mode = aux & 0xFF, aux >> 8
+        lo_c, hi_c = (">=" if mode & 1 else ">"), ("<=" if mode & 2 else "<")
+        if op == OP_RNGF:
+            x, lo, hi = f"u2f({X})", f"u2f((u64)a.ins[{pc}].imm)", f"u2f((u64)a.kpool[{k}])"
+        else:
+            x, lo, hi = f"(long long){X}", f"a.ins[{pc}].imm", f"a.kpool[{k}]"
+        z = f"(u64)(({x} {lo_c} {lo}) && ({x} {hi_c} {hi}))"
+    elif op in (OP_SEQ, OP_SPRE, OP_SSUF):
+        mode = {OP_SEQ: 0, OP_SPRE: 1, OP_SSUF: 2}[op]
+        z = f"(u64)str_match(a.col[{b}].dat, {X}, a.lit, a.ins[{pc}].imm, {mode})"
+    else:
+        z = "0ull"
+    if c >= 0:
+        z = f"(u64)(({z}) != 0ull && r[{c}] != 0ull)"
+    return f"r[{dst}] = {z};"
+
+
+_LOADS = {C_F64: ("u64", "p[row[j]]"), C_I64: ("u64", "p[row[j]]"), C_I32: ("int", "(u64)(long long)p[row[j]]"),
+          C_F32: ("float", "f2u((double)p[row[j]])"), C_U8: ("unsigned char", "(u64)p[row[j]]")}
+
+
+def _jit_loads(kinds, lates, late: bool) -> List[str]:
+    out = []
+    for c, (kind, lt) in enumerate(zip(kinds, lates)):
+        if bool(lt) != late:
+            continue
+        if kind in _LOADS:
+            t, e = _LOADS[kind]
+            out.append(f"    {{ const {t}* p = reinterpret_cast<const {t}*>(a.col[{c}].p);\n"
+                       f"#pragma unroll\n      for (int j = 0; j < ROWS; ++j) R[j][{c}] = (FULL || m[j]) ? {e} : 0ull; }}")
+        elif kind in (C_SCODE, C_SREF):
+            v = (f"short_code(a.col[{c}].dat, s, e - s, a.col[{c}].L)" if kind == C_SCODE else
+                 "(((u64)s << 24) | (u64)(e - s < 0xFFFFFFll ? e - s : 0xFFFFFFll))")
+            out.append(f"    {{ const long long* st = a.col[{c}].st; const long long* en = a.col[{c}].en;\n"
+                       f"#pragma unroll\n      for (int j = 0; j < ROWS; ++j) {{\n"
+                       f"        const bool mj = FULL || m[j];\n"
+                       f"        const long long s = mj ? st[row[j]] : 0ll, e = mj ? en[row[j]] : 0ll;\n"
+                       f"        R[j][{c}] = mj ? {v} : 0ull;\n      }} }}")
+        else:
+            raise Unfusable(f"column kind {kind}")
+    return out
+
+
+def jit_source(prog: Program, kinds, lates, kind: str, key_reg: int = -1, val_regs=(), rows: int = JIT_ROWS) -> str:
+    """The C++ source of the compiled kernel of ``prog`` (``kind`` "agg" or "mask") over columns of these kinds."""
+    nreg = program_nreg(prog, len(kinds), key_reg, val_regs)
+    F = max(1, len(val_regs))
+    nins_a = prog.nins_a if kind == "agg" else len(prog.ins)
+
+    def seg(lo, hi):
+        body = [t for pc in range(lo, hi) if (t := _jit_ins(pc, prog.ins[pc])) is not None]
+        if not body:
+            return "    (void)a; (void)R;"
+        return ("#pragma unroll\n    for (int j = 0; j < ROWS; ++j) {\n      u64* r = R[j];\n"
+                + "".join(f"      {t}\n" for t in body) + "    }")
+
+    def loads(late):
+        ls = _jit_loads(kinds, [lt if kind == "agg" else 0 for lt in lates], late)
+        return "\n".join(ls) if ls else "    (void)a; (void)row; (void)m; (void)R;"
+
+    vals = "".join(f"    v[{f}] = u2f(r[{reg}]);\n" for f, reg in enumerate(val_regs)) or "    v[0] = 0.0; (void)r;\n"
+    keep = "true" if prog.keep_reg < 0 else f"r[{prog.keep_reg}] != 0ull"
+    key = "0ll" if key_reg < 0 else f"(long long)r[{key_reg}]"
+    entry = ("extern \"C\" __global__ void __launch_bounds__(nsdb_pipe::NTHR) nsdb_jit_agg(const nsdb_pipe::PipeArgs a) {\n"
+             "  nsdb_pipe::jit_agg_body<nsdb_pipe::JitProg>(a);\n}\n" if kind == "agg" else
+             "extern \"C\" __global__ void __launch_bounds__(nsdb_pipe::NTHR) nsdb_jit_mask(const nsdb_pipe::PipeArgs a, "
+             "unsigned char* mask) {\n  nsdb_pipe::jit_mask_body<nsdb_pipe::JitProg>(a, mask);\n}\n")
+    return f"""// generated by netsdb_amd.execution.pipeline.jit_source ({kind})
+#include "pipeline_core.h"
+namespace nsdb_pipe {{
+struct JitProg {{
+  static constexpr int F = {F}, NR = {nreg}, ROWS = {rows};
+  template <bool LATE, bool FULL>
+  __device__ static __forceinline__ void load(const PipeArgs& a, const long long (&row)[ROWS], const bool (&m)[ROWS],
+                                              u64 (&R)[ROWS][NR]) {{
+    if constexpr (!LATE) {{
+{loads(False)}
+    }} else {{
+{loads(True)}
+    }}
+  }}
+  __device__ static __forceinline__ void run_a(const PipeArgs& a, u64 (&R)[ROWS][NR]) {{
+{seg(0, nins_a)}
+  }}
+  __device__ static __forceinline__ void run_b(const PipeArgs& a, u64 (&R)[ROWS][NR]) {{
+{seg(nins_a, len(prog.ins))}
+  }}
+  __device__ static __forceinline__ bool keep(const u64 (&r)[NR]) {{ (void)r; return {keep}; }}
+  __device__ static __forceinline__ long long key(const u64 (&r)[NR]) {{ (void)r; return {key}; }}
+  __device__ static __forceinline__ void vals(const u64 (&r)[NR], double (&v)[F]) {{
+{vals}  }}
+}};
+}}  // namespace nsdb_pipe
+{entry}"""
+
+
+def _jit_cache_dir() -> Optional[str]:
+    d = os.environ.get("NSDB_JIT_CACHE") or os.path.join(os.path.expanduser("~"), ".cache", "netsdb_amd", "jit")
+    try:
+        os.makedirs(d, exist_ok=True)
+        return d
+    except OSError:
+        return None
+
+
+def jit_kernel(src: str, name: str) -> Optional[int]:
+    """The loaded kernel of a generated source (compiled once per process, code objects cached on disk), or None when
+    compilation fails (the interpreter kernels then run that stage)."""
+    if src in _JIT_FN:
+        return _JIT_FN[src]
+    h = _ext.hip()
+    fn = None
+    try:
+        hdr = _jit_header()
+        arch = os.environ.get("PYTORCH_ROCM_ARCH") or "gfx950"
+        digest = hashlib.sha256((arch + "\0" + hdr + "\0" + src).encode()).hexdigest()[:32]
+        d = _jit_cache_dir()
+        path = os.path.join(d, f"{digest}.hsaco") if d else None
+        code = None
+        if path and os.path.exists(path):
+            with open(path, "rb") as f:
+                code = f.read()
+            JIT_STATS["disk_hits"] += 1
+        if not code:
+            code = h.jit_compile(src, hdr)
+            JIT_STATS["compiled"] += 1
+            if path:
+                tmp = f"{path}.{os.getpid()}.tmp"
+                with open(tmp, "wb") as f:
+                    f.write(code)
+                os.replace(tmp, path)
+        fn = int(h.jit_load(code, name))
+    except Exception as e:          # noqa: BLE001 - any compiler / loader failure keeps the interpreter path
+        JIT_STATS["failed"] += 1
+        warnings.warn(f"pipeline kernel compilation failed, interpreting this stage: {e}")
+        fn = None
+    _JIT_FN[src] = fn
+    return fn
+
+
+def _jit_for(prog: Program, cargs, kind: str, key_reg: int = -1, val_regs=()):
+    """(kernel handle, nreg, rows) of the compiled kernel for this launch, or None (interpreter)."""
+    if not JIT or not hasattr(_ext.hip(), "jit_compile"):
+        return None
+    kinds = [c[0] for c in cargs]
+    lates = [c[1] for c in cargs]
+    nreg = program_nreg(prog, len(kinds), key_reg, val_regs)
+    rows = JIT_ROWS_SMALL if nreg <= JIT_SMALL_NREG else JIT_ROWS
+    try:
+        src = jit_source(prog, kinds, lates, kind, key_reg, val_regs, rows=rows)
+    except Unfusable:
+        return None
+    fn = jit_kernel(src, "nsdb_jit_agg" if kind == "agg" else "nsdb_jit_mask")
+    if fn is None:
+        return None
+    JIT_STATS["launches"] += 1
+    return fn, nreg, rows
+
+
 def _launch(prog: Program, n: int, dev, plan: StagePlan):
     h = _ext.hip()
     ins = torch.tensor(prog.ins if prog.ins else [[0, 0, -1, -1, -1, 0, 0]], dtype=torch.int64).reshape(-1, 7)
     if not prog.ins:
         ins = ins[:0]
     lit = torch.frombuffer(bytearray(prog.lit or b"\0"), dtype=torch.uint8).to(dev, non_blocking=True)
-    table = h.pipe_agg(ins, prog.nins_a, _col_args(prog, dev), lit, n, prog.keep_reg, prog.key_reg, prog.val_regs,
-                       AGG_OPS[plan.op], 0, TILE, prog.kpool)
+    cargs = _col_args(prog, dev)
+    jit = _jit_for(prog, cargs, "agg", prog.key_reg, prog.val_regs)
+    fn, jnreg, jrows = jit if jit else (0, 0, 0)
+    table = h.pipe_agg(ins, prog.nins_a, cargs, lit, n, prog.keep_reg, prog.key_reg, prog.val_regs,
+                       AGG_OPS[plan.op], 0, TILE, prog.kpool, fn, jnreg, jrows)
     host = table.cpu()                           # the one device -> host read of the launch
     if int(host[0]) != 0:
         return None
@@ -1017,7 +1253,11 @@ def run_filter(plan: FilterPlan, batch: RecordBatch) -> Optional[RecordBatch]:
     if on_gpu:
         ins = torch.tensor(prog.ins, dtype=torch.int64).reshape(-1, 7)
         lit = torch.frombuffer(bytearray(prog.lit or b"\0"), dtype=torch.uint8).to(dev, non_blocking=True)
-        mask = _ext.hip().pipe_mask(ins, _col_args(prog, dev), lit, batch.n, prog.keep_reg, TILE, prog.kpool).bool()
+        cargs = _col_args(prog, dev)
+        jit = _jit_for(prog, cargs, "mask")
+        fn, jnreg, jrows = jit if jit else (0, 0, 0)
+        mask = _ext.hip().pipe_mask(ins, cargs, lit, batch.n, prog.keep_reg, TILE, prog.kpool, fn, jnreg,
+                                    jrows).bool()
     else:
         mask = interpret_mask(prog, batch.n)
     plan.stats["fused_batches"] += 1

@@ -94,7 +94,7 @@ def build_hip_extension(out_path: str, build_dir: str, jobs: int = 8, study: boo
         list(ex.map(run, cmds))
     os.makedirs(os.path.dirname(out_path), exist_ok=True)
     subprocess.run([hipcc, "-shared", "-fPIC", f"--offload-arch={arch}", "-o", out_path] + objs + libs
-                   + [f"-L{rocm}/lib", "-lamdhip64"], check=True)
+                   + [f"-L{rocm}/lib", "-lamdhip64", "-lhiprtc"], check=True)
 
 
 def native_ext():

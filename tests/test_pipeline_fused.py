@@ -57,6 +57,37 @@ def test_fused_tpch_cpu_interpreter(monkeypatch):
     assert st.get("fused_filters", 0) >= 5, st
 
 
+def test_jit_sources_compile_cpu(monkeypatch):
+    """Every TPC-H stage program's run-time kernel source (aggregate and mask forms, early and late columns, both
+    string kinds) compiles with hiprtc for gfx950 — no GPU needed to compile; the GPU tests run the kernels."""
+    from netsdb_amd import _ext
+    if not _ext.hip_available() or not hasattr(_ext.hip(), "jit_compile"):
+        pytest.skip("kernel extension not built")
+    monkeypatch.setenv("NSDB_DEVICE_STRINGS", "1")
+    monkeypatch.setattr(PL, "CPU_INTERPRETER", True)
+    PL._PROG_CACHE.clear()
+    t = tpch_gen.generate_fast(0.002, seed=4)
+    c = _client("cpu", t)
+    for q in QUERIES + FILTER_QUERIES:
+        tpch.QUERIES[q](c, "tpch")
+    progs = list(PL._PROG_CACHE.values())
+    assert len(progs) >= len(QUERIES) + len(FILTER_QUERIES), len(progs)
+    h, hdr, seen = _ext.hip(), PL._jit_header(), set()
+    for p in progs:
+        kinds = [cc["kind"] for cc in p.cols]
+        lates = [cc["late"] for cc in p.cols]
+        srcs = [PL.jit_source(p, kinds, lates, "mask")]
+        if p.val_regs or p.key_reg >= 0:
+            srcs.append(PL.jit_source(p, kinds, lates, "agg", p.key_reg, p.val_regs))
+            srcs.append(PL.jit_source(p, [PL.C_I64 if k == PL.C_SCODE else k for k in kinds], [1] * len(kinds), "agg",
+                                      p.key_reg, p.val_regs))
+        for src in srcs:
+            if src not in seen:
+                seen.add(src)
+                assert len(h.jit_compile(src, hdr)) > 1000
+    assert len(seen) >= len(progs)
+
+
 class _Sel(SelectionComp):
     def __init__(self, pred):
         super().__init__()
@@ -144,10 +175,14 @@ def test_fused_overflow_falls_back(monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tile", [-2, -1, 0])
-def test_fused_tpch_gpu_vs_eager_and_pandas(tile, monkeypatch):
-    """Every kernel shape (LDS-tile, hybrid and register interpreters) against the eager path and pandas."""
+@pytest.mark.parametrize("tile,jit", [(-2, True), (-2, False), (-1, False), (0, False)],
+                         ids=["compiled", "lds_tile", "hybrid", "register"])
+def test_fused_tpch_gpu_vs_eager_and_pandas(tile, jit, monkeypatch):
+    """Every kernel shape (run-time compiled; LDS-tile, hybrid and register interpreters) against the eager path and
+    pandas."""
     monkeypatch.setattr(PL, "TILE", tile)
+    monkeypatch.setattr(PL, "JIT", jit)
+    j0 = dict(PL.JIT_STATS)
     t = tpch_gen.generate_fast(0.05, seed=4)
     f = tpch.frames(t)
     c = _client("cuda:0", t)
@@ -161,6 +196,11 @@ def test_fused_tpch_gpu_vs_eager_and_pandas(tile, monkeypatch):
         assert _close(eager, ref), q
     st = c.engine.pipeline_stats
     assert st["fused_stages"] >= len(QUERIES) and st["fallback_batches"] == 0, st
+    if jit:     # every fused launch took a compiled kernel
+        assert PL.JIT_STATS["failed"] == j0["failed"], PL.JIT_STATS
+        assert PL.JIT_STATS["launches"] - j0["launches"] >= len(QUERIES) + len(FILTER_QUERIES), PL.JIT_STATS
+    else:
+        assert PL.JIT_STATS["launches"] == j0["launches"]
 
 
 @pytest.mark.gpu
@@ -245,3 +285,22 @@ def test_pipe_kernel_shapes_gpu():
         assert torch.allclose(v, ref_v, rtol=1e-12, atol=1e-9), tile
         m = h.pipe_mask(pt[:2], cols, lit, n, 5, tile).bool().cpu()
         assert torch.equal(m, ref_mask), tile
+    # the run-time compiled kernels of the same program: all columns early, then d / b late (kept rows only)
+    kinds = [cc[0] for cc in cols]
+    for lates in ([0, 0, 0, 0, 0], [0, 0, 0, 1, 1]):
+        lcols = [(cc[0], lt) + tuple(cc[2:]) for cc, lt in zip(cols, lates)]
+        src = PL.jit_source(prog, kinds, lates, "agg", 6, [4, 7])
+        fn = PL.jit_kernel(src, "nsdb_jit_agg")
+        assert fn, "compiled aggregate kernel"
+        nreg = PL.program_nreg(prog, len(kinds), 6, [4, 7])
+        st, kept, k, v = _table_result(h.pipe_agg(pt, 2, lcols, lit, n, 5, 6, [4, 7], 0, 0, -2, [], fn, nreg,
+                                                  PL.JIT_ROWS), 2)
+        assert st == 0 and kept == int(ref_mask.sum()), lates
+        assert torch.equal(k, ref_k), lates
+        assert torch.allclose(v, ref_v, rtol=1e-12, atol=1e-9), lates
+    mprog = PL.Program()
+    mprog.cols, mprog.ins, mprog.nins_a, mprog.keep_reg = prog.cols, prog.ins[:2], 2, 5
+    fn = PL.jit_kernel(PL.jit_source(mprog, kinds, [0] * 5, "mask"), "nsdb_jit_mask")
+    assert fn, "compiled mask kernel"
+    m = h.pipe_mask(pt[:2], cols, lit, n, 5, -2, [], fn, PL.program_nreg(mprog, 5, -1, []), PL.JIT_ROWS).bool().cpu()
+    assert torch.equal(m, ref_mask)
