@@ -388,6 +388,7 @@ class QueryEngine:
             if r is not None:
                 if getattr(fplan, "host_out", False) and b.device.type == "cuda":
                     state.fused_out_device = b.device
+                state.unique_kv.append(r.columns[fplan.kcol])   # one row per key (the kernel's global table)
                 used = True
                 self.pipeline_stats["fused_batches"] += 1
                 yield r
@@ -751,7 +752,14 @@ class QueryEngine:
                 kv = self._stream_shuffle(kv, None, "aggregate", key=lambda b: K.hash_keys(b.columns["k"], b.device))
             reps, agg = self._reduce_kv(kv, op, combine, group_fn)
         elif not self.ctx.distributed:
-            reps, agg = self._reduce_kv(kv, op, combine)
+            kv = list(kv)
+            if len(kv) == 1 and any(kv[0].columns["k"] is u for u in state.unique_kv):
+                # the single batch is a fused launch's result: its keys are already unique (one global table per
+                # launch), so it IS the aggregate (no group-by pass over a handful of groups)
+                reps, agg = kv[0].columns["k"], kv[0].columns["v"]
+            else:
+                reps, agg = self._reduce_kv(kv, op, combine)
+            state.unique_kv.clear()
             dev = state.fused_out_device
             if dev is not None:
                 state.fused_out_device = None
@@ -954,6 +962,7 @@ class _JobState:
         self.materialized: Dict[str, List[RecordBatch]] = {}
         self.builds: Dict[str, BuildTable] = {}
         self.fused_out_device = None     # a fused stage's host-resident partials: the device its result returns to
+        self.unique_kv: List = []        # key columns of fused launch results (unique keys by construction)
 
 
 def _upload(x, dev):
