@@ -1183,6 +1183,29 @@ __global__ __launch_bounds__(1024) void part_scatter_kernel(const i64* __restric
   }
 }
 
+// ---------------------------------------------------------------- key hashing
+// out = mix64((x ^ y) + GOLD) over int64 columns (y optional): the engine's join / partition key hash
+// (execution/kernels.py mix64 / column_to_int64, = netsdb_amd._native.hash64) as ONE streaming pass, where the torch
+// expression is eleven elementwise kernels over the column. 2 rows per thread (16-B loads / stores).
+__global__ __launch_bounds__(256) void mix64_kernel(const u64* __restrict__ x, const u64* __restrict__ y, u64* out, i64 n) {
+  const i64 stride = (i64)gridDim.x * blockDim.x * 2;
+  for (i64 i = ((i64)blockIdx.x * blockDim.x + threadIdx.x) * 2; i < n; i += stride) {
+    if (i + 1 < n) {
+      ulonglong2 a = *reinterpret_cast<const ulonglong2*>(x + i);
+      if (y) {
+        const ulonglong2 b = *reinterpret_cast<const ulonglong2*>(y + i);
+        a.x ^= b.x;
+        a.y ^= b.y;
+      }
+      *reinterpret_cast<ulonglong2*>(out + i) = make_ulonglong2(mix64(a.x + 0x9E3779B97F4A7C15ull),
+                                                                mix64(a.y + 0x9E3779B97F4A7C15ull));
+    } else {
+      const u64 a = x[i] ^ (y ? y[i] : 0ull);
+      out[i] = mix64(a + 0x9E3779B97F4A7C15ull);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- host launchers
 // rows staged per scatter pass: a multiple of 1024, <= 4096, staging <= budget bytes
 inline int stage_rows(int F, int budget = 48 * 1024, int nthr = 512) {
@@ -1399,6 +1422,16 @@ int nsdb_partition_perm(const long long* dest, long long n, int P, void* work, l
   hipLaunchKernelGGL(scan_tot_kernel, dim3(1), dim3(1024), 0, st, tot, P, bstart, (AggMeta*)nullptr, 0);
   hipLaunchKernelGGL(part_scatter_kernel, dim3(G), dim3(1024), lds, st, dest, n, rpw, P, hist, bstart, perm);
   if (counts) (void)hipMemcpyAsync(counts, tot, sizeof(long long) * P, hipMemcpyDeviceToDevice, st);
+  return (int)hipGetLastError();
+}
+
+int nsdb_mix64(const void* x, const void* y, void* out, long long n, hipStream_t st) {
+  if (n <= 0) return 0;
+  if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(out)) & 15)
+    return (int)hipErrorInvalidValue;                  // 16-B row pairs
+  const long long blocks = std::min<long long>(8192, (n + 511) / 512);
+  hipLaunchKernelGGL(mix64_kernel, dim3((unsigned)blocks), dim3(256), 0, st, reinterpret_cast<const u64*>(x),
+                     reinterpret_cast<const u64*>(y), reinterpret_cast<u64*>(out), n);
   return (int)hipGetLastError();
 }
 

@@ -29,6 +29,7 @@ int nsdb_join_probe(const void* keys, long long m, const void* tab, long long ca
 int nsdb_join_expand(const unsigned* cnt, const unsigned* pay, long long m, const long long* tile_base,
                      const long long* perm, long long* bidx, long long* pidx, hipStream_t st);
 long long nsdb_part_work_bytes(long long n, int P);
+int nsdb_mix64(const void* x, const void* y, void* out, long long n, hipStream_t st);
 int nsdb_partition_perm(const long long* dest, long long n, int P, void* work, long long* perm, long long* counts,
                         hipStream_t st);
 }
@@ -260,6 +261,32 @@ std::vector<torch::Tensor> partition_perm(torch::Tensor dest, int64_t P) {
   return {perm, counts};
 }
 
+// mix64((x ^ y) + GOLD) per row (y optional), int64 in / out: the engine's key hash in one pass.
+torch::Tensor mix64(torch::Tensor x, c10::optional<torch::Tensor> y) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kInt64 && x.dim() == 1, "mix64: x must be a 1-D int64 GPU tensor");
+  x = x.contiguous();
+  const void* yp = nullptr;
+  torch::Tensor yc;
+  if (y.has_value() && y->defined()) {
+    TORCH_CHECK(y->is_cuda() && y->scalar_type() == torch::kInt64 && y->numel() == x.numel() && y->device() == x.device(),
+                "mix64: y must be an int64 GPU tensor like x");
+    yc = y->contiguous();
+    yp = yc.data_ptr();
+  }
+  auto out = torch::empty_like(x);
+  const bool aligned = ((reinterpret_cast<uintptr_t>(x.data_ptr()) | reinterpret_cast<uintptr_t>(yp) |
+                         reinterpret_cast<uintptr_t>(out.data_ptr())) & 15) == 0;
+  if (!aligned) {                                   // a view at an odd offset: realign first
+    x = x.clone();
+    if (yp) {
+      yc = yc.clone();
+      yp = yc.data_ptr();
+    }
+  }
+  rc_ok(nsdb_mix64(x.data_ptr(), yp, out.data_ptr(), x.numel(), stream()), "mix64");
+  return out;
+}
+
 }  // namespace
 
 std::vector<torch::Tensor> hash_aggregate_impl(torch::Tensor keys, c10::optional<torch::Tensor> vals,
@@ -276,4 +303,6 @@ void register_relops(pybind11::module& m) {
   m.def("join_build", &join_build, "device hash-join build: (table, perm)");
   m.def("join_probe", &join_probe, "device hash-join probe: (build_idx, probe_idx)");
   m.def("partition_perm", &partition_perm, "stable device partition permutation: (perm, counts)");
+  m.def("mix64", &mix64, "key hash mix64((x ^ y) + GOLD) per row, one pass", pybind11::arg("x"),
+        pybind11::arg("y") = pybind11::none());
 }

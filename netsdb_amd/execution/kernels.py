@@ -13,7 +13,7 @@ operators are sort / unique / searchsorted tensor ops.
 from __future__ import annotations
 
 import weakref
-from typing import Any, List, Tuple
+from typing import Any, List, Optional, Tuple
 
 import torch
 import xxhash
@@ -32,12 +32,21 @@ def _lsr(x: torch.Tensor, k: int) -> torch.Tensor:
     return (x >> k) & ((1 << (64 - k)) - 1)
 
 
-def mix64(x: torch.Tensor) -> torch.Tensor:
-    """splitmix64 finaliser in wrapping int64 arithmetic (matches netsdb_amd._native.hash64)."""
+def mix64(x: torch.Tensor, y: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """splitmix64 finaliser of (x ^ y) + GOLD in wrapping int64 arithmetic (matches netsdb_amd._native.hash64). On the
+    GPU one pass of relops.hip mix64_kernel; the torch expression below is the CPU path and the reference."""
+    if x.is_cuda and x.dim() == 1 and x.dtype == torch.int64 and x.numel() >= _MIX_MIN_ROWS and \
+            (y is None or (y.is_cuda and y.dtype == torch.int64 and y.shape == x.shape)):
+        return _ext.hip().mix64(x, y)
+    if y is not None:
+        x = x ^ y
     x = x + _GOLD
     x = (x ^ _lsr(x, 30)) * _M1
     x = (x ^ _lsr(x, 27)) * _M2
     return x ^ _lsr(x, 31)
+
+
+_MIX_MIN_ROWS = 1 << 14     # smaller columns: the torch expression (launch-bound either way)
 
 
 def _obj_key(v) -> int:
@@ -57,14 +66,14 @@ def column_to_int64(c, device=None) -> torch.Tensor:
         out = None
         for x in c:
             h = column_to_int64(x, device)
-            out = h if out is None else mix64(out ^ h)
+            out = h if out is None else mix64(out, h)
         return out
     if isinstance(c, torch.Tensor):
         if c.dim() > 1:
             c = c.reshape(c.shape[0], -1)
             out = torch.zeros(c.shape[0], dtype=torch.int64, device=c.device)
             for j in range(c.shape[1]):
-                out = mix64(out ^ column_to_int64(c[:, j]))
+                out = mix64(out, column_to_int64(c[:, j]))
             return out
         if c.dtype == torch.int64:
             return c
@@ -190,7 +199,7 @@ def _unpack(packed: torch.Tensor, layout) -> List[torch.Tensor]:
 def _combine_words(words: List[torch.Tensor]) -> torch.Tensor:
     out = None
     for h in words:
-        out = h if out is None else mix64(out ^ h)
+        out = h if out is None else mix64(out, h)
     return out
 
 

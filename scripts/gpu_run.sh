@@ -63,7 +63,7 @@ run_task() {
       grep '^{"sf"' "$O/tpch.log" | tail -12 ;;
     tpchprof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/$O/tpchprof" -o run --output-format csv -- \
-        python3 "$R/scripts/bench_tpch.py" ${TPCH_ARGS:---sf 10 --queries q01,q06 --runs 3} > "$O/tpchprof.log" 2>&1 \
+        python3 "$R/scripts/bench_tpch.py" ${TPCH_ARGS:---sf 10 --queries q01,q06 --rounds 3} > "$O/tpchprof.log" 2>&1 \
         || fail tpchprof $? "$O/tpchprof.log"
       f=$(ls "$O"/tpchprof/*/run_kernel_stats.csv "$O"/tpchprof/run_kernel_stats.csv 2>/dev/null | head -1)
       [ -n "$f" ] && cp "$f" "$O/tpch_kernel_stats.csv" && head -12 "$O/tpch_kernel_stats.csv" ;;

@@ -497,3 +497,31 @@ def test_large_join_build_with_clusters_matches_host():
     bi2, pi2 = K.JoinTable(build.cpu()).probe(probe.cpu())
     assert bi.numel() == bi2.numel()
     assert sorted(zip(pi.cpu().tolist(), bi.cpu().tolist())) == sorted(zip(pi2.tolist(), bi2.tolist()))
+
+
+@pytest.mark.gpu
+def test_mix64_kernel_matches_torch_expression():
+    """relops.hip mix64_kernel == the torch splitmix64 expression (wrapping int64), with and without the xor input,
+    odd lengths and a view at an odd offset (realigned by the binding)."""
+    from netsdb_amd import _ext
+    from netsdb_amd.execution import kernels as K
+
+    def ref(x, y=None):
+        if y is not None:
+            x = x ^ y
+        x = x + K._GOLD
+        x = (x ^ K._lsr(x, 30)) * K._M1
+        x = (x ^ K._lsr(x, 27)) * K._M2
+        return x ^ K._lsr(x, 31)
+
+    g = torch.Generator().manual_seed(5)
+    for n in (1, 2, 3, 1001, 1 << 20):
+        x = torch.randint(-(1 << 62), 1 << 62, (n,), generator=g, dtype=torch.int64)
+        y = torch.randint(-(1 << 62), 1 << 62, (n,), generator=g, dtype=torch.int64)
+        xd, yd = x.cuda(), y.cuda()
+        assert torch.equal(_ext.hip().mix64(xd).cpu(), ref(x))
+        assert torch.equal(_ext.hip().mix64(xd, yd).cpu(), ref(x, y))
+        if n > 2:
+            assert torch.equal(_ext.hip().mix64(xd[1:], yd[1:]).cpu(), ref(x[1:], y[1:]))
+    big = torch.randint(-(1 << 62), 1 << 62, (1 << 16,), generator=g, dtype=torch.int64)
+    assert torch.equal(K.mix64(big.cuda()).cpu(), ref(big))            # the engine entry takes the kernel
