@@ -385,7 +385,8 @@ def _group_ids_device(keys):
 
 def group_reduce(keys, values, op: str = "sum"):
     """Fused device group-by + aggregation (relops.hip hash_aggregate: LDS pre-aggregation for few groups, radix
-    partitioning for many): ``(representative keys, aggregates)`` ordered like :func:`group_ids`, or None when
+    partitioning for many): ``(representative keys, aggregates)`` ordered like :func:`group_ids` up to
+    SORTED_GROUPS_MAX groups (larger results in the table's order), or None when
     the inputs need the generic path (host objects, non-numeric values, unsupported op).
     Reference: AggregationProcessor.h:16 / CombinerProcessor over PDBMap hash tables."""
     if op not in ("sum", "count", "min", "max", "mean") or not isinstance(values, torch.Tensor) or not values.is_cuda:
@@ -414,26 +415,38 @@ def group_reduce(keys, values, op: str = "sum"):
     reps_k, aggs, cnt, first, inv = r
     if packed is None and not _rows_match_rep(cols, words, first.index_select(0, inv)):
         return None
-    order, _ = _sort_groups(reps_k)
-    g = int(order.numel())
-    cnt = cnt.index_select(0, order)
+    g = int(reps_k.numel())
+    if g > SORTED_GROUPS_MAX:
+        # an aggregation's output is a set: past this many groups they stay in the table's emit order (sorting 15 M
+        # group keys and gathering every output column by the permutation cost ~2 ms of TPC-H Q04's 8.6 at SF 10)
+        order = None
+    else:
+        order, _ = _sort_groups(reps_k)
+
+    def sel(t):
+        return t if order is None else t.index_select(0, order)
+
+    cnt = sel(cnt)
     if op == "count":
         agg = cnt
     else:
-        agg = aggs.index_select(0, order)
+        agg = sel(aggs)
         if op == "mean":
             agg = agg / cnt.unsqueeze(1).to(agg.dtype)
         out_dtype = values.dtype if (is_float or op != "mean") else torch.float64
         agg = agg.to(out_dtype).reshape((g,) + tuple(values.shape[1:]))
     if packed is not None and packed[1] is not None:
-        unp = _unpack(reps_k.index_select(0, order), packed[1])
+        unp = _unpack(sel(reps_k), packed[1])
         reps = tuple(_rep_from_word(u, c) for u, c in zip(unp, cols))
     elif packed is not None:
-        reps = (_rep_from_word(reps_k.index_select(0, order), cols[0]),)
+        reps = (_rep_from_word(sel(reps_k), cols[0]),)
     else:
-        fo = first.index_select(0, order)
+        fo = sel(first)
         reps = tuple(_take_col(c, fo) for c in cols)
     return (reps if isinstance(keys, tuple) else reps[0]), agg
+
+
+SORTED_GROUPS_MAX = 1 << 20     # group_reduce: results with more groups are not sorted by key
 
 
 def group_ids(keys) -> Tuple[torch.Tensor, Any, int]:

@@ -1257,7 +1257,7 @@ def run_filter(plan: FilterPlan, batch: RecordBatch) -> Optional[RecordBatch]:
         jit = _jit_for(prog, cargs, "mask")
         fn, jnreg, jrows = jit if jit else (0, 0, 0)
         mask = _ext.hip().pipe_mask(ins, cargs, lit, batch.n, prog.keep_reg, TILE, prog.kpool, fn, jnreg,
-                                    jrows).bool()
+                                    jrows).view(torch.bool)      # 0 / 1 bytes: a bool view, no conversion pass
     else:
         mask = interpret_mask(prog, batch.n)
     plan.stats["fused_batches"] += 1

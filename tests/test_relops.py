@@ -525,3 +525,21 @@ def test_mix64_kernel_matches_torch_expression():
             assert torch.equal(_ext.hip().mix64(xd[1:], yd[1:]).cpu(), ref(x[1:], y[1:]))
     big = torch.randint(-(1 << 62), 1 << 62, (1 << 16,), generator=g, dtype=torch.int64)
     assert torch.equal(K.mix64(big.cuda()).cpu(), ref(big))            # the engine entry takes the kernel
+
+
+@pytest.mark.gpu
+def test_group_reduce_many_groups_unsorted_is_exact():
+    """Past SORTED_GROUPS_MAX groups group_reduce returns the groups in the table's order (no key sort): the same
+    set of (key, aggregate) pairs as torch.unique + index_add."""
+    g = torch.Generator(device=DEV).manual_seed(8)
+    n = 3_000_000
+    keys = torch.randint(0, 1 << 40, (n,), device=DEV, generator=g)
+    keys[: n // 3] = keys[n // 3: 2 * (n // 3)]                       # repeats: ~2 M groups of 1-2 rows
+    vals = torch.rand(n, device=DEV, dtype=torch.float64, generator=g)
+    reps, agg = K.group_reduce(keys, vals, "sum")
+    assert reps.numel() > K.SORTED_GROUPS_MAX
+    o = torch.argsort(reps)
+    u, ui = torch.unique(keys, return_inverse=True)
+    ref = torch.zeros(u.numel(), dtype=torch.float64, device=DEV).index_add_(0, ui, vals)
+    assert torch.equal(reps[o], u)
+    torch.testing.assert_close(agg[o], ref, rtol=1e-12, atol=1e-12)
