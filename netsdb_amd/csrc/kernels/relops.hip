@@ -1206,6 +1206,83 @@ __global__ __launch_bounds__(256) void mix64_kernel(const u64* __restrict__ x, c
   }
 }
 
+// ---------------------------------------------------------------- stable stream compaction (mask -> row ids)
+// The row ids of the nonzero bytes of a 0/1 byte mask, in row order (a filter's selection): per-tile counts, one
+// scan, then every tile writes its ids at its offset, each wave a contiguous run per 64 rows (ballot + popcount).
+constexpr int CT_ROWS = 8192;   // rows per tile (one 256-thread workgroup)
+
+__global__ __launch_bounds__(256) void compact_count_kernel(const unsigned char* __restrict__ mask, i64 n,
+                                                            unsigned* __restrict__ cnt) {
+  const i64 t0 = (i64)blockIdx.x * CT_ROWS;
+  unsigned c = 0;
+  for (int r = threadIdx.x * 16; r < CT_ROWS; r += 256 * 16) {
+    const i64 i = t0 + r;
+    if (i + 16 <= n) {
+      const uint4 w = *reinterpret_cast<const uint4*>(mask + i);      // 16 bytes of 0 / 1
+      const u64 a = ((u64)w.y << 32) | w.x, b = ((u64)w.w << 32) | w.z;
+      // every nonzero byte -> 1, then the 16 bytes summed by one multiply
+      const u64 lo7 = 0x7F7F7F7F7F7F7F7Full, hi = 0x8080808080808080ull;
+      const u64 na = ((((a & lo7) + lo7) | a) & hi) >> 7, nb = ((((b & lo7) + lo7) | b) & hi) >> 7;
+      c += (unsigned)(((na + nb) * 0x0101010101010101ull) >> 56);
+    } else {
+      for (i64 k = i; k < n && k < i + 16; ++k) c += mask[k] != 0;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  __shared__ unsigned ws[4];
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) cnt[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+// exclusive scan of T tile counts (one workgroup): off[t], off[T] = total
+__global__ __launch_bounds__(1024) void compact_scan_kernel(const unsigned* __restrict__ cnt, int T, i64* __restrict__ off) {
+  __shared__ i64 part[1024];
+  const int per = (T + 1023) / 1024;
+  const int b = threadIdx.x * per;
+  i64 s = 0;
+  for (int k = b; k < b + per && k < T; ++k) s += cnt[k];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {
+    const i64 v = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  i64 run = part[threadIdx.x] - s;
+  for (int k = b; k < b + per && k < T; ++k) {
+    off[k] = run;
+    run += cnt[k];
+  }
+  if (threadIdx.x == 1023) off[T] = part[1023];
+}
+
+__global__ __launch_bounds__(256) void compact_write_kernel(const unsigned char* __restrict__ mask, i64 n,
+                                                            const i64* __restrict__ off, i64* __restrict__ out) {
+  __shared__ unsigned wc[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const i64 t0 = (i64)blockIdx.x * CT_ROWS;
+  i64 base = off[blockIdx.x];
+  const u64 lt = (1ull << lane) - 1;
+  for (int r = 0; r < CT_ROWS; r += 256) {
+    const i64 i = t0 + r + threadIdx.x;
+    const bool on = i < n && mask[i] != 0;
+    const u64 bal = __builtin_amdgcn_ballot_w64(on);
+    if (lane == 0) wc[wave] = (unsigned)__builtin_popcountll(bal);
+    __syncthreads();
+    unsigned before = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      before += w < wave ? wc[w] : 0u;
+      tot += wc[w];
+    }
+    if (on) out[base + before + __builtin_popcountll(bal & lt)] = i;
+    base += tot;
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------- host launchers
 // rows staged per scatter pass: a multiple of 1024, <= 4096, staging <= budget bytes
 inline int stage_rows(int F, int budget = 48 * 1024, int nthr = 512) {
@@ -1422,6 +1499,26 @@ int nsdb_partition_perm(const long long* dest, long long n, int P, void* work, l
   hipLaunchKernelGGL(scan_tot_kernel, dim3(1), dim3(1024), 0, st, tot, P, bstart, (AggMeta*)nullptr, 0);
   hipLaunchKernelGGL(part_scatter_kernel, dim3(G), dim3(1024), lds, st, dest, n, rpw, P, hist, bstart, perm);
   if (counts) (void)hipMemcpyAsync(counts, tot, sizeof(long long) * P, hipMemcpyDeviceToDevice, st);
+  return (int)hipGetLastError();
+}
+
+// Tiles of a compaction and its scratch (tile counts u32 + offsets i64 [T + 1]).
+long long nsdb_compact_tiles(long long n) { return (n + nsdb_rel::CT_ROWS - 1) / nsdb_rel::CT_ROWS; }
+
+// Phase 1: tile counts + offsets (off[T] = the number of set rows, which the caller reads to size the output).
+int nsdb_compact_count(const unsigned char* mask, long long n, unsigned* cnt, long long* off, hipStream_t st) {
+  const long long T = nsdb_compact_tiles(n);
+  if (T <= 0 || T > (1LL << 30) || (reinterpret_cast<uintptr_t>(mask) & 15)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(compact_count_kernel, dim3((unsigned)T), dim3(256), 0, st, mask, n, cnt);
+  hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, st, cnt, (int)T, off);
+  return (int)hipGetLastError();
+}
+
+// Phase 2: the row ids, in order, at out[0 .. off[T]).
+int nsdb_compact_write(const unsigned char* mask, long long n, const long long* off, long long* out, hipStream_t st) {
+  const long long T = nsdb_compact_tiles(n);
+  if (T <= 0) return 0;
+  hipLaunchKernelGGL(compact_write_kernel, dim3((unsigned)T), dim3(256), 0, st, mask, n, off, out);
   return (int)hipGetLastError();
 }
 

@@ -30,6 +30,9 @@ int nsdb_join_expand(const unsigned* cnt, const unsigned* pay, long long m, cons
                      const long long* perm, long long* bidx, long long* pidx, hipStream_t st);
 long long nsdb_part_work_bytes(long long n, int P);
 int nsdb_mix64(const void* x, const void* y, void* out, long long n, hipStream_t st);
+long long nsdb_compact_tiles(long long n);
+int nsdb_compact_count(const unsigned char* mask, long long n, unsigned* cnt, long long* off, hipStream_t st);
+int nsdb_compact_write(const unsigned char* mask, long long n, const long long* off, long long* out, hipStream_t st);
 int nsdb_partition_perm(const long long* dest, long long n, int P, void* work, long long* perm, long long* counts,
                         hipStream_t st);
 }
@@ -261,6 +264,35 @@ std::vector<torch::Tensor> partition_perm(torch::Tensor dest, int64_t P) {
   return {perm, counts};
 }
 
+// Row ids of the set rows of a 0/1 byte mask (bool or uint8), in order: torch.nonzero(mask).flatten() as three
+// streaming launches + one read of the total (the output size).
+torch::Tensor compact(torch::Tensor mask) {
+  TORCH_CHECK(mask.is_cuda() && mask.dim() == 1 && (mask.scalar_type() == torch::kBool ||
+                                                     mask.scalar_type() == torch::kUInt8),
+              "compact: 1-D bool / uint8 GPU mask");
+  mask = mask.contiguous();
+  const int64_t n = mask.numel();
+  auto i64 = mask.options().dtype(torch::kInt64);
+  if (n == 0) return torch::empty({0}, i64);
+  const unsigned char* mp = reinterpret_cast<const unsigned char*>(mask.data_ptr());
+  if (reinterpret_cast<uintptr_t>(mp) & 15) {
+    mask = mask.clone();
+    mp = reinterpret_cast<const unsigned char*>(mask.data_ptr());
+  }
+  const int64_t T = nsdb_compact_tiles(n);
+  auto cnt = torch::empty({T}, mask.options().dtype(torch::kInt32));
+  auto off = torch::empty({T + 1}, i64);
+  rc_ok(nsdb_compact_count(mp, n, reinterpret_cast<unsigned*>(cnt.data_ptr<int32_t>()), LL(off.data_ptr<int64_t>()),
+                           stream()),
+        "compact_count");
+  const int64_t total = off[T].item<int64_t>();
+  auto out = torch::empty({total}, i64);
+  if (total > 0)
+    rc_ok(nsdb_compact_write(mp, n, LL(off.data_ptr<int64_t>()), LL(out.data_ptr<int64_t>()), stream()),
+          "compact_write");
+  return out;
+}
+
 // mix64((x ^ y) + GOLD) per row (y optional), int64 in / out: the engine's key hash in one pass.
 torch::Tensor mix64(torch::Tensor x, c10::optional<torch::Tensor> y) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kInt64 && x.dim() == 1, "mix64: x must be a 1-D int64 GPU tensor");
@@ -303,6 +335,8 @@ void register_relops(pybind11::module& m) {
   m.def("join_build", &join_build, "device hash-join build: (table, perm)");
   m.def("join_probe", &join_probe, "device hash-join probe: (build_idx, probe_idx)");
   m.def("partition_perm", &partition_perm, "stable device partition permutation: (perm, counts)");
+  m.def("compact", &compact, "row ids of the set rows of a 0/1 byte mask, in order (stable stream compaction)",
+        pybind11::arg("mask"));
   m.def("mix64", &mix64, "key hash mix64((x ^ y) + GOLD) per row, one pass", pybind11::arg("x"),
         pybind11::arg("y") = pybind11::none());
 }

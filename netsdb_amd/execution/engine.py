@@ -500,7 +500,7 @@ class QueryEngine:
             mask = b.columns[a["input"]["atts"][0]]
             if not isinstance(mask, torch.Tensor):
                 mask = torch.tensor([bool(x) for x in mask], dtype=torch.bool)
-            idx = torch.nonzero(mask.bool(), as_tuple=False).flatten()
+            idx = K.selected_rows(mask.bool())
             keep = RecordBatch({c: b.columns[c] for c in a["projection"]["atts"]}, b.n)
             return keep.take(idx)
         if t in ("HASHLEFT", "HASHRIGHT"):

@@ -49,6 +49,19 @@ def mix64(x: torch.Tensor, y: Optional[torch.Tensor] = None) -> torch.Tensor:
 _MIX_MIN_ROWS = 1 << 14     # smaller columns: the torch expression (launch-bound either way)
 
 
+def selected_rows(mask: torch.Tensor) -> torch.Tensor:
+    """The row ids of a filter's kept rows, in order (torch.nonzero(mask).flatten()). On the GPU the relops.hip
+    stable compaction for large masks (per-tile counts, one scan, ordered id runs: a third of rocprim's partition
+    time on a 60 M-row mask)."""
+    if mask.is_cuda and mask.dim() == 1 and mask.numel() >= _COMPACT_MIN_ROWS and \
+            mask.dtype in (torch.bool, torch.uint8):
+        return _ext.hip().compact(mask)
+    return torch.nonzero(mask, as_tuple=False).flatten()
+
+
+_COMPACT_MIN_ROWS = 1 << 16
+
+
 def _obj_key(v) -> int:
     if isinstance(v, RecordView):
         v = v.as_tuple()

@@ -34,6 +34,7 @@ from typing import Dict, List, Optional, Tuple
 import torch
 
 from .. import _ext
+from . import kernels as K
 from ..lambdas import AttAccess, Binary, IsIn, KeyTuple, Like, Literal, Select, Unary, Values
 from ..objects.record import RecordBatch
 from ..objects.strings import StringColumn
@@ -1261,7 +1262,7 @@ def run_filter(plan: FilterPlan, batch: RecordBatch) -> Optional[RecordBatch]:
     else:
         mask = interpret_mask(prog, batch.n)
     plan.stats["fused_batches"] += 1
-    idx = torch.nonzero(mask, as_tuple=False).flatten()
+    idx = K.selected_rows(mask)
     keep = RecordBatch({c: batch.columns[c] for c in plan.proj}, batch.n)
     return keep.take(idx)
 

@@ -543,3 +543,20 @@ def test_group_reduce_many_groups_unsorted_is_exact():
     ref = torch.zeros(u.numel(), dtype=torch.float64, device=DEV).index_add_(0, ui, vals)
     assert torch.equal(reps[o], u)
     torch.testing.assert_close(agg[o], ref, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_compact_matches_nonzero():
+    """relops.hip stable compaction == torch.nonzero: bool and uint8 (bytes > 1 count as set) masks, dense / sparse /
+    empty / full, ragged tails, an unaligned view."""
+    g = torch.Generator(device=DEV).manual_seed(9)
+    for n in (1, 15, 16, 17, 8191, 8192, 8193, 100_003, 3_000_001):
+        for p in (0.0, 0.01, 0.5, 1.0):
+            m = torch.rand(n, device=DEV, generator=g) < p
+            assert torch.equal(_ext.hip().compact(m), torch.nonzero(m).flatten()), (n, p)
+        u = torch.randint(0, 4, (n,), device=DEV, generator=g).to(torch.uint8)
+        assert torch.equal(_ext.hip().compact(u), torch.nonzero(u).flatten()), n
+        if n > 3:
+            assert torch.equal(_ext.hip().compact(u[3:]), torch.nonzero(u[3:]).flatten()), n
+    big = torch.rand(1 << 20, device=DEV, generator=g) < 0.3
+    assert torch.equal(K.selected_rows(big), torch.nonzero(big).flatten())      # the engine entry
