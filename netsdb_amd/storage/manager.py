@@ -263,6 +263,22 @@ class StorageManager:
             if ent is not None and id(page) in ent[1]:
                 ent[1].move_to_end(id(page))
 
+    def touch_run(self, pages):
+        """touch() of consecutive pages of ONE set, oldest first, under one lock acquisition (a coalesced scan's run
+        of hundreds of pages)."""
+        if not pages:
+            return
+        with self.lock:
+            ent = self._resident.get(id(self._set_of(pages[0])))
+            od = ent[1] if ent is not None else None
+            clock = self._clock
+            for p in pages:
+                p.last_use = next(clock)
+                if od is not None:
+                    k = id(p)
+                    if k in od:
+                        od.move_to_end(k)
+
     @staticmethod
     def _resident_on_device(p) -> bool:
         return p.resident_on_home() if isinstance(p, DenseMatrixSet) else (p.location == "device" and p.batch is not None)

@@ -423,14 +423,17 @@ class UserSet:
         gens = [p.gen for p in pages]          # the layout the plan was checked against
         for i, j in plan:
             run = pages[i:j]
-            # a page spilled / reloaded while earlier runs were consumed no longer matches the plan: page by page
-            if j - i > 1 and all(p.batch is not None and p.gen == g for p, g in zip(run, gens[i:j])):
+            if j - i > 1:
+                # a page spilled / reloaded while earlier runs were consumed no longer matches the plan: page by page
+                # (one pass: the run's identity and its validity together)
+                ident = tuple((id(p.batch), p.gen) for p in run)
+                ok = all(p.batch is not None for p in run) and [g for _, g in ident] == gens[i:j]
+            if j - i > 1 and ok:
                 for p in run:
                     p.pins += 1
                 try:
                     # the merged view of an unchanged run is kept: a re-scan costs no per-page work, and what a
                     # query derives from its columns (a string column's short-code encoding) survives the scan
-                    ident = tuple((id(p.batch), p.gen) for p in run)
                     cache = self.__dict__.setdefault("_merged_runs", {})
                     hit = cache.get((i, j))
                     if hit is not None and hit[0] == ident:
@@ -438,8 +441,12 @@ class UserSet:
                     else:
                         merged = merge_adjacent_batches([p.batch for p in run], check=False)
                         cache[(i, j)] = (ident, merged)
-                    for p in run:
-                        self.manager.touch(p)
+                    touch_run = getattr(self.manager, "touch_run", None)
+                    if touch_run is not None:
+                        touch_run(run)
+                    else:
+                        for p in run:
+                            self.manager.touch(p)
                     yield merged
                 finally:
                     for p in run:

@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--queries", default="q01,q06")
     ap.add_argument("--runs", type=int, default=5)
     ap.add_argument("--profile", action="store_true")
+    ap.add_argument("--profile-runs", type=int, default=1)
+    ap.add_argument("--profile-sort", default="tottime")
+    ap.add_argument("--no-eager", action="store_true")
     a = ap.parse_args()
     from netsdb_amd.client import PDBClient
     from netsdb_amd.execution import pipeline as PL
@@ -49,7 +52,7 @@ def main():
         del t
         for q in a.queries.split(","):
             res = {"sf": sf, "query": q}
-            for fused in (True, False):
+            for fused in ((True,) if a.no_eager else (True, False)):
                 c.engine.fused_pipelines = fused
                 tpch.QUERIES[q](c, "tpch")
                 torch.cuda.synchronize()
@@ -71,12 +74,13 @@ def main():
             if a.profile:
                 pr = cProfile.Profile()
                 pr.enable()
-                tpch.QUERIES[q](c, "tpch")
-                torch.cuda.synchronize()
+                for _ in range(a.profile_runs):
+                    tpch.QUERIES[q](c, "tpch")
+                    torch.cuda.synchronize()
                 pr.disable()
                 s = io.StringIO()
-                pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(25)
-                print(s.getvalue()[:6000], flush=True)
+                pstats.Stats(pr, stream=s).sort_stats(a.profile_sort).print_stats(45)
+                print(s.getvalue()[:12000], flush=True)
 
 
 if __name__ == "__main__":
