@@ -38,9 +38,13 @@ class Page:
 
     @batch.setter
     def batch(self, b: Optional[RecordBatch]):
-        # every (re)assignment gets a new generation: cached scan plans key on it (object ids can be reused)
+        # every (re)assignment gets a new generation: cached scan plans key on it (object ids can be reused); the
+        # set's layout version follows, so a scan can tell in O(1) that none of its pages changed
         self._batch = b
         self.gen = next(_BATCH_GEN)
+        st = getattr(self, "set", None)
+        if st is not None:
+            st._layout_version = self.gen
 
     def __init__(self, uset: "UserSet", page_no: int, batch: RecordBatch, to_pool: bool = False):
         self.set = uset
@@ -342,6 +346,7 @@ class UserSet:
             for p in self.pages:
                 self.manager.untrack(p)
             self.pages = []
+            self._layout_version = next(_BATCH_GEN)
             self.stats = {"records": 0, "bytes": 0}
             self.placement = None
             self._placed = False
@@ -419,6 +424,23 @@ class UserSet:
     def _scan_coalesced(self, pages, device) -> Iterator[RecordBatch]:
         """Runs of consecutive pages resident on ``device`` whose columns are adjacent slices of one buffer are
         yielded as ONE batch (zero-copy views, up to SCAN_COALESCE_BYTES); any other page is yielded alone."""
+        # fast path: no page of the set changed since a scan that merged every page into cached runs
+        ver = (getattr(self, "_layout_version", None), len(pages), str(device))
+        fast = self.__dict__.get("_scan_fast")
+        if fast is not None and fast[0] == ver and ver[0] is not None:
+            touch_run = getattr(self.manager, "touch_run", None)
+            for run, merged in fast[1]:
+                for p in run:
+                    p.pins += 1
+                try:
+                    if touch_run is not None:
+                        touch_run(run)
+                    yield merged
+                finally:
+                    for p in run:
+                        p.pins -= 1
+            return
+        all_merged = []
         plan = self._coalesce_runs(pages, device)
         gens = [p.gen for p in pages]          # the layout the plan was checked against
         for i, j in plan:
@@ -447,11 +469,14 @@ class UserSet:
                     else:
                         for p in run:
                             self.manager.touch(p)
+                    if all_merged is not None:
+                        all_merged.append((run, merged))
                     yield merged
                 finally:
                     for p in run:
                         p.pins -= 1
                 continue
+            all_merged = None                  # a page-by-page run: no fast path for this layout
             for p in run:
                 p.pins += 1
                 try:
@@ -460,6 +485,8 @@ class UserSet:
                     yield b
                 finally:
                     p.pins -= 1
+        if all_merged is not None and ver[0] is not None and getattr(self, "_layout_version", None) == ver[0]:
+            self._scan_fast = (ver, all_merged)
 
     def all(self, device=None) -> Optional[RecordBatch]:
         bs = list(self.scan(device))
