@@ -120,7 +120,8 @@ struct AggMeta {
   i64 sentinel_part;
   i64 occ_low;        // slots claimed in the LOW global table (its fill, apart from the group count)
   i64 occ_part;       // slots claimed in the PART overflow table
-  i64 pad[6];
+  i64 lowp;           // key partitions of the MID path (low == 2)
+  i64 pad[5];
 };
 
 struct GTable {                     // open-addressing global table: cap slots + one slot (cap) for the kEmpty key
@@ -273,6 +274,10 @@ __device__ __forceinline__ void row_into_global(GTable g, u64 k, const VT* v, in
 // estimate of the distinct keys, d + f1^2 / (2 f2) (f1 / f2: keys seen once / twice in the sample; exact d when
 // every row was sampled), clamped to [d, n]. The PART path sizes its sub-partitions from it.
 constexpr int kSample = 4096;
+// MID path: at most this many key partitions. Every workgroup of a row group reads all of its rows' keys through its
+// own CU, so the per-CU load stream grows with P: measured (profiles/r5_relops) 16 M rows, 10 k keys at P = 5 took
+// 0.65 ms against the PART path's 0.47, so MID stops at P = 3 (~6 k groups).
+constexpr int kMidPMax = 3;
 
 // The sampled rows' keys into sbuf[4096]: the random reads spread over 64 workgroups (one CU's outstanding-miss
 // budget made a single-workgroup sample latency-bound).
@@ -285,7 +290,7 @@ __global__ __launch_bounds__(64) void agg_sample_gather_kernel(const u64* __rest
 }
 
 __global__ __launch_bounds__(1024) void agg_sample_kernel(const u64* __restrict__ sbuf, i64 n, int low_thr,
-                                                          AggMeta* meta) {
+                                                          int mid_keys, AggMeta* meta) {
   constexpr int S = kSample, CAP = 8192;
   __shared__ u64 tab[CAP];
   __shared__ unsigned tcnt[CAP];
@@ -353,7 +358,18 @@ __global__ __launch_bounds__(1024) void agg_sample_kernel(const u64* __restrict_
     if (n > S) est = g2 > 0 ? dd + g1 * g1 / (2.0 * g2) : dd + g1 * (g1 - 1) / 2.0;
     est = std::min(est, (double)n);
     meta->est = (i64)est;
-    meta->low = est <= (double)low_thr ? 1 : 0;
+    // LOW: one small LDS table per workgroup; MID: the key space split into lowp hash partitions, each a large LDS
+    // table, the partitions of one row range on one XCD (mid_keys: keys one MID table takes, 0 = no MID path)
+    const i64 p = mid_keys > 0 ? (i64)((est + mid_keys - 1) / mid_keys) : 0;
+    if (est <= (double)low_thr) {
+      meta->low = 1;
+      meta->lowp = 1;
+    } else if (mid_keys > 0 && p <= kMidPMax) {
+      meta->low = 2;
+      meta->lowp = p < 1 ? 1 : p;
+    } else {
+      meta->low = 0;
+    }
   }
 }
 
@@ -381,10 +397,11 @@ constexpr int kPreF = 1;     // value columns loaded with the keys (the rest at 
 // Row (key, values) batch of one thread: kU rows of a 256*kU-row tile, loaded together. Value (i, f) of the input
 // is vals[i * rs + f * cs]: row-major [n, F] (rs = F, cs = 1) or column-major (rs = 1, cs = column pitch), so a
 // caller's stacked columns are read in place.
-template <typename VT>
+template <typename VT, bool PRE = true>
 struct RowBatch {
   u64 k[kU];
   VT v[kU][kPreF];
+  // PRE = false (MID path): keys only; a row's values are read at use, by the one workgroup whose partition it is in
   __device__ __forceinline__ void load(const u64* __restrict__ keys, const VT* __restrict__ vals, i64 t0, i64 n,
                                        int F, int nthr, i64 rs, i64 cs) {
 #pragma unroll
@@ -392,7 +409,7 @@ struct RowBatch {
       const i64 i = t0 + (i64)j * nthr + threadIdx.x;
       k[j] = i < n ? keys[i] : kEmpty;
 #pragma unroll
-      for (int f = 0; f < kPreF; ++f) v[j][f] = (i < n && f < F) ? vals[i * rs + f * cs] : VT(0);
+      for (int f = 0; f < kPreF; ++f) v[j][f] = (PRE && i < n && f < F) ? vals[i * rs + f * cs] : VT(0);
     }
   }
 };
@@ -407,33 +424,52 @@ __device__ __forceinline__ void ltable_add_row(LTable t, int s, VT v0, const VT*
   if (r32 < t.rmin[s]) __hip_atomic_fetch_min(t.rmin + s, r32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-template <typename VT, int OP>
-__global__ __launch_bounds__(256) void agg_low_kernel(const u64* __restrict__ keys, const VT* __restrict__ vals, i64 n,
-                                                      int F, i64 rs, i64 cs, int lcap, GTable g, AggMeta* meta,
-                                                      AggOut o) {
-  if (!take_low(meta)) return;
+// MODE 1 (LOW): every workgroup aggregates its row tiles into one LDS table of lcap slots. MODE 2 (MID, 1024 threads,
+// one workgroup per CU, grid = 256): the key space is split into P = meta->lowp hash partitions; the 32 workgroups
+// of each XCD form floor(32 / P) row groups of P workgroups, workgroup (group, part) keeps only the keys of its
+// partition in its (large) LDS table, and the P workgroups of a row group share their rows through the XCD's L2
+// (HBM reads each row once). Many more groups than one LDS table holds are then aggregated in ONE pass over the
+// input, without the PART path's partitioned write + read of every row.
+__device__ __forceinline__ int mid_part(u64 k, int P) { return (int)((mix64(k) >> 40) % (u64)P); }
+
+template <typename VT, int OP, int NT, int MODE>
+__global__ __launch_bounds__(NT) void agg_low_kernel(const u64* __restrict__ keys, const VT* __restrict__ vals, i64 n,
+                                                     int F, i64 rs, i64 cs, int lcap, GTable g, AggMeta* meta,
+                                                     AggOut o) {
+  if (meta->low != MODE) return;
+  int P = 1, part = 0;
+  i64 gb = blockIdx.x, ngb = gridDim.x;
+  if constexpr (MODE == 2) {
+    P = (int)meta->lowp;
+    const int xcd = blockIdx.x & 7, m = blockIdx.x >> 3, q = (gridDim.x >> 3) / P;
+    if (m >= q * P) return;                      // the workgroups left over when P does not divide 32
+    part = m % P;
+    gb = xcd + 8 * (m / P);
+    ngb = 8 * q;
+  }
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   LTable t = ltable_at(lds_raw, lcap, F);
   ltable_clear<VT, OP>(t, F);
   __syncthreads();
-  constexpr int TILE = 256 * kU;
-  const i64 tstride = (i64)gridDim.x * TILE;
+  constexpr int TILE = NT * kU;
+  const i64 tstride = ngb * TILE;
   int it = 0;
-  RowBatch<VT> cur, nxt;
-  i64 t0 = (i64)blockIdx.x * TILE;
-  if (t0 < n) cur.load(keys, vals, t0, n, F, 256, rs, cs);
+  RowBatch<VT, MODE == 1> cur, nxt;
+  i64 t0 = gb * TILE;
+  if (t0 < n) cur.load(keys, vals, t0, n, F, NT, rs, cs);
   for (; t0 < n; t0 += tstride, ++it) {
     if ((it & 15) == 15 && __hip_atomic_load(&meta->fail_low, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
-    if (t0 + tstride < n) nxt.load(keys, vals, t0 + tstride, n, F, 256, rs, cs);   // in flight during this tile
+    if (t0 + tstride < n) nxt.load(keys, vals, t0 + tstride, n, F, NT, rs, cs);   // in flight during this tile
 #pragma unroll
     for (int j = 0; j < kU; ++j) {
-      const i64 i = t0 + j * 256 + threadIdx.x;
+      const i64 i = t0 + j * NT + threadIdx.x;
       if (i >= n) break;
       const u64 k = cur.k[j];
+      if (MODE == 2 && (k == kEmpty ? part != 0 : mid_part(k, P) != part)) continue;   // another partition's key
       const VT* v = vals + i * rs;
       const int s = k != kEmpty ? ltable_slot(t, k, mix64(k)) : -1;
       if (s >= 0) {
-        ltable_add_row<VT, OP>(t, s, cur.v[j][0], v, F, cs, (u64)i);
+        ltable_add_row<VT, OP>(t, s, MODE == 1 ? cur.v[j][0] : (F > 0 ? v[0] : VT(0)), v, F, cs, (u64)i);
       } else {   // rare: the values are re-read from memory
         row_into_global<VT, OP>(g, k, v, F, cs, &meta->ng_low, &meta->sentinel_low, &meta->fail_low, o, i);
       }
@@ -454,17 +490,18 @@ __global__ __launch_bounds__(256) void agg_low_kernel(const u64* __restrict__ ke
   }
   if (o.inv == nullptr) return;
   __syncthreads();
-  for (i64 t0 = (i64)blockIdx.x * TILE; t0 < n; t0 += tstride) {
+  for (i64 t0 = gb * TILE; t0 < n; t0 += tstride) {
     u64 k[kU];
 #pragma unroll
     for (int j = 0; j < kU; ++j) {
-      const i64 i = t0 + j * 256 + threadIdx.x;
+      const i64 i = t0 + j * NT + threadIdx.x;
       k[j] = i < n ? keys[i] : kEmpty;
     }
 #pragma unroll
     for (int j = 0; j < kU; ++j) {
-      const i64 i = t0 + j * 256 + threadIdx.x;
+      const i64 i = t0 + j * NT + threadIdx.x;
       if (k[j] == kEmpty || i >= n) continue;
+      if (MODE == 2 && mid_part(k[j], P) != part) continue;
       const int s = ltable_find(t, k[j], mix64(k[j]));
       if (s >= 0) o.inv[i] = t.ref[s];
     }
@@ -1300,7 +1337,7 @@ inline int agg_groups(long long n) { return (int)std::min<long long>(256, std::m
 template <typename VT, int OP>
 int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv, int want_first, void* meta_v, void* glow_v,
                  i64 gcap_low, void* gpart_v, i64 gcap_part, void* out_v, void* inv_v, i64 ocap, int phase, void* work_v,
-                 int pbits, int lcap_low, int lcap_part, int low_thr, i64 rs, i64 cs, hipStream_t st) {
+                 int pbits, int lcap_low, int lcap_part, int low_thr, int lcap_mid, i64 rs, i64 cs, hipStream_t st) {
   AggMeta* meta = reinterpret_cast<AggMeta*>(meta_v);
   // glow / gpart: [key (cap+1) | acc (cap+1)*F | cnt (cap+1) | gid (cap+1)] u64 words, preset by the caller
   auto mk = [&](void* base, i64 cap) {
@@ -1335,10 +1372,13 @@ int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv,
                        phase == 0 ? reinterpret_cast<u64*>(gpart_v) : nullptr, gcap_part, F, acc_identity<VT, OP>(), meta);
     u64* sbuf = reinterpret_cast<u64*>(meta) + sizeof(AggMeta) / 8;   // [4096] after the meta words
     hipLaunchKernelGGL(agg_sample_gather_kernel, dim3(kSample / 64), dim3(64), 0, st, k, n, sbuf);
-    hipLaunchKernelGGL(agg_sample_kernel, dim3(1), dim3(1024), 0, st, sbuf, n, low_thr, meta);
+    hipLaunchKernelGGL(agg_sample_kernel, dim3(1), dim3(1024), 0, st, sbuf, n, low_thr, lcap_mid / 2, meta);
     const int gl = (int)std::min<i64>(1024, std::max<i64>(1, (n + 2047) / 2048));
-    hipLaunchKernelGGL((agg_low_kernel<VT, OP>), dim3(gl), dim3(256), lbytes_low, st, k, v, n, F, rs, cs, lcap_low, glow,
-                       meta, o);
+    hipLaunchKernelGGL((agg_low_kernel<VT, OP, 256, 1>), dim3(gl), dim3(256), lbytes_low, st, k, v, n, F, rs, cs, lcap_low,
+                       glow, meta, o);
+    if (lcap_mid > 0)   // returns at once unless the sample chose the MID path
+      hipLaunchKernelGGL((agg_low_kernel<VT, OP, 1024, 2>), dim3(256), dim3(1024), (size_t)lcap_mid * (20 + 8 * F), st, k,
+                         v, n, F, rs, cs, lcap_mid, glow, meta, o);
   }
   if (phase == 2)
     hipLaunchKernelGGL(agg_init_kernel, dim3(512), dim3(256), 0, st, (u64*)nullptr, gcap_low,
@@ -1402,8 +1442,11 @@ long long nsdb_agg_work_bytes(long long n, int F, int pbits, int want_inv) {
 int nsdb_hash_aggregate(const void* keys, const void* vals, long long n, int F, int vt, int op, int want_inv,
                         int want_first, void* meta, void* glow, long long gcap_low, void* gpart, long long gcap_part,
                         void* out, void* inv, long long ocap, int phase, void* work, int pbits, int lcap_low,
-                        int lcap_part, int low_thr, long long vrs, long long vcs, hipStream_t st) {
+                        int lcap_part, int low_thr, int lcap_mid, long long vrs, long long vcs, hipStream_t st) {
   if (n <= 0) return 0;
+  if (lcap_mid < 0 || (lcap_mid > 0 && ((lcap_mid & (lcap_mid - 1)) || (size_t)lcap_mid * (20 + 8 * F) > 160 * 1024 ||
+                                        gcap_low < 2LL * kMidPMax * (lcap_mid / 2))))
+    return (int)hipErrorInvalidValue;   // the MID table fits one CU's LDS; the global table holds every MID group
   if (phase < 0 || phase > 3 || ocap <= 0 || (want_inv && inv == nullptr)) return (int)hipErrorInvalidValue;
   if ((phase == 0 || phase == 2) && (ocap < n || work == nullptr || gpart == nullptr)) return (int)hipErrorInvalidValue;
   if (ocap < gcap_low + 1 && ocap < n) return (int)hipErrorInvalidValue;   // every LOW group needs an output row
@@ -1418,7 +1461,7 @@ int nsdb_hash_aggregate(const void* keys, const void* vals, long long n, int F, 
     vrs = F;
     vcs = 1;
   }
-#define NSDB_AGG(VT, OP) agg_launch_t<VT, OP>(keys, vals, n, F, want_inv, want_first, meta, glow, gcap_low, gpart, gcap_part, out, inv, ocap, phase, work, pbits, lcap_low, lcap_part, low_thr, vrs, vcs, st)
+#define NSDB_AGG(VT, OP) agg_launch_t<VT, OP>(keys, vals, n, F, want_inv, want_first, meta, glow, gcap_low, gpart, gcap_part, out, inv, ocap, phase, work, pbits, lcap_low, lcap_part, low_thr, lcap_mid, vrs, vcs, st)
   if (vt == 0) {
     if (op == 0) return NSDB_AGG(double, OP_SUM);
     if (op == 1) return NSDB_AGG(double, OP_MIN);

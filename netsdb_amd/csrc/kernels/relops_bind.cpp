@@ -18,7 +18,7 @@ long long nsdb_agg_work_bytes(long long n, int F, int pbits, int want_inv);
 int nsdb_hash_aggregate(const void* keys, const void* vals, long long n, int F, int vt, int op, int want_inv,
                         int want_first, void* meta, void* glow, long long gcap_low, void* gpart, long long gcap_part,
                         void* out, void* inv, long long ocap, int phase, void* work, int pbits, int lcap_low,
-                        int lcap_part, int low_thr, long long vrs, long long vcs, hipStream_t st);
+                        int lcap_part, int low_thr, int lcap_mid, long long vrs, long long vcs, hipStream_t st);
 int nsdb_join_insert(const void* keys, long long n, void* tab, long long cap, int* row_slot, unsigned* row_rank,
                      unsigned long long* ndup, hipStream_t st);
 int nsdb_join_perm(const int* row_slot, const unsigned* row_rank, long long n, const unsigned long long* ndup,
@@ -40,6 +40,8 @@ int nsdb_partition_perm(const long long* dest, long long n, int P, void* work, l
 namespace {
 
 hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+bool g_agg_mid = true;   // the MID group-by path (agg_set_mid: A/B and tests)
 
 void rc_ok(int rc, const char* what) {
   TORCH_CHECK(rc == 0, what, " failed with code ", rc, " (", hipGetErrorString((hipError_t)(rc > 0 ? rc : 0)), ")");
@@ -115,7 +117,12 @@ std::vector<torch::Tensor> hash_aggregate(torch::Tensor keys, c10::optional<torc
   const int64_t lcap_part = std::min<int64_t>(4096, pow2_at_most(131072 / entry));
   int pbits = 0;
   while (pbits < 8 && (n >> (pbits + 1)) >= 2048) ++pbits;
-  const int64_t gcap_low = 4 * lcap_low;
+  // MID path (relops.hip agg_low_kernel MODE 2): up to 8 hash partitions of the key space, each one CU-sized LDS
+  // table of lcap_mid slots (half full at most); 0 disables it. The LOW global table then holds every MID group.
+  // (an explicit low_threshold pins the LOW / PART boundary: no MID path then)
+  const int64_t lcap_mid =
+      g_agg_mid && low_threshold <= 0 ? std::min<int64_t>(4096, pow2_at_most(160 * 1024 / entry)) : 0;
+  const int64_t gcap_low = std::max<int64_t>(4 * lcap_low, lcap_mid > 0 ? 2 * 8 * (lcap_mid / 2) : 0);
   // overflow table of the PART path (keys whose LDS probe window filled): a miss-sized estimate only
   const int64_t gcap_part = std::max<int64_t>(4096, std::min<int64_t>(pow2_at_least(2 * n), int64_t(1) << 17));
   const int64_t thr = low_threshold > 0 ? low_threshold : lcap_low / 4;
@@ -130,7 +137,8 @@ std::vector<torch::Tensor> hash_aggregate(torch::Tensor keys, c10::optional<torc
     rc_ok(nsdb_hash_aggregate(keys.data_ptr(), F ? v.data_ptr() : nullptr, n, F, vt, opc, want_inv ? 1 : 0,
                               want_first ? 1 : 0, meta.data_ptr(), glow.data_ptr(), gcap_low, gpart, gcap_part,
                               out.data_ptr(), want_inv ? inv.data_ptr() : nullptr, ocap, phase, work, pbits,
-                              (int)lcap_low, (int)lcap_part, (int)thr, (long long)vrs, (long long)vcs, stream()),
+                              (int)lcap_low, (int)lcap_part, (int)thr, (int)lcap_mid, (long long)vrs, (long long)vcs,
+                              stream()),
           "hash_aggregate");
   };
   launch(1, nullptr, nullptr);
@@ -335,6 +343,8 @@ void register_relops(pybind11::module& m) {
   m.def("join_build", &join_build, "device hash-join build: (table, perm)");
   m.def("join_probe", &join_probe, "device hash-join probe: (build_idx, probe_idx)");
   m.def("partition_perm", &partition_perm, "stable device partition permutation: (perm, counts)");
+  m.def("agg_set_mid", [](bool on) { g_agg_mid = on; }, "enable / disable the MID group-by path (hash-partitioned LDS "
+        "tables sharing their rows through L2); returns nothing", pybind11::arg("on"));
   m.def("compact", &compact, "row ids of the set rows of a 0/1 byte mask, in order (stable stream compaction)",
         pybind11::arg("mask"));
   m.def("mix64", &mix64, "key hash mix64((x ^ y) + GOLD) per row, one pass", pybind11::arg("x"),

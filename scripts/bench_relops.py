@@ -53,7 +53,7 @@ def main():
     h = _ext.hip()
     out = {"rows": n, "groupby": {}, "join": {}, "partition": {}}
     vals = torch.rand(n, device=dev, dtype=torch.float64, generator=g)
-    for distinct in (8, 10_000, 10_000_000):
+    for distinct in (8, 1000, 3000, 5000, 10_000, 10_000_000):
         keys = torch.randint(0, distinct, (n,), device=dev, generator=g) * 2654435761
         ref_u, ref_inv = torch.unique(keys, return_inverse=True)
         ref = torch.zeros(ref_u.numel(), device=dev, dtype=torch.float64).index_add_(0, ref_inv, vals)
@@ -79,11 +79,20 @@ def main():
             u, inv = torch.unique(keys, return_inverse=True)
             return torch.zeros(u.numel(), device=dev, dtype=torch.float64).index_add_(0, inv, vals)
 
-        t = run({"hash_aggregate": dev_agg, "hash_aggregate_no_first": dev_agg_nofirst,
-                 "hash_aggregate_with_inverse": dev_agg_inv, 
-                 "torch_unique_index_add": torch_agg}, a.rounds)
+        def dev_agg_part():      # the same call with the MID path off (A/B: MID vs PART)
+            h.agg_set_mid(False)
+            try:
+                return h.hash_aggregate(keys, vals, "sum", False, 0)
+            finally:
+                h.agg_set_mid(True)
+
+        arms = {"hash_aggregate": dev_agg, "hash_aggregate_no_first": dev_agg_nofirst,
+                "hash_aggregate_with_inverse": dev_agg_inv, "torch_unique_index_add": torch_agg}
+        if 8 < distinct < 1_000_000:
+            arms["hash_aggregate_mid_off"] = dev_agg_part
+        t = run(arms, a.rounds)
         t["groups"] = int(ref_u.numel())
-        t["path"] = ("LOW", "PART")[int(r[5][1])]
+        t["path"] = ("LOW/MID", "PART")[int(r[5][1])]
         t["sample_distinct"] = int(r[5][3])
         t["max_rel_err"] = err
         out["groupby"][str(distinct)] = t

@@ -392,7 +392,8 @@ def test_low_path_scratch_is_o_groups():
         ref = torch.zeros(8, dtype=torch.float64, device=DEV).index_add_(0, keys // 977, vals)
         o = torch.argsort(r[0])
         assert torch.allclose(r[1][o, 0], ref, rtol=1e-9)
-    assert sizes[0] == sizes[1] and sizes[1] < (1 << 20), sizes
+    # fixed-size tables (the LOW / MID global table holds up to 16 k MID groups: 2.6 MB at F = 1), never n-sized
+    assert sizes[0] == sizes[1] and sizes[1] < (4 << 20), sizes
     # PART path: charged while allocated, released after
     calls = []
     n = 1 << 22
@@ -560,3 +561,33 @@ def test_compact_matches_nonzero():
             assert torch.equal(_ext.hip().compact(u[3:]), torch.nonzero(u[3:]).flatten()), n
     big = torch.rand(1 << 20, device=DEV, generator=g) < 0.3
     assert torch.equal(K.selected_rows(big), torch.nonzero(big).flatten())      # the engine entry
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("distinct", [600, 1500, 3000, 5000])
+@pytest.mark.parametrize("op", ["sum", "min", "max"])
+def test_hash_aggregate_mid_path(distinct, op):
+    """The MID path (hash-partitioned LDS tables, one pass over the rows; relops.hip agg_low_kernel MODE 2) for
+    group counts between the LOW tables and the PART path: exact groups, aggregates, counts, first rows and inverse,
+    double and int64 values, and the same groups as with the MID path switched off (the PART path)."""
+    h = _ext.hip()
+    g = torch.Generator(device=DEV).manual_seed(distinct)
+    n = 400_003
+    keys = torch.randint(0, distinct, (n,), device=DEV, generator=g) * 7919 - 123456
+    keys[:5] = -(1 << 63)                                           # the kEmpty marker as a real key
+    vals = torch.rand(n, 2, device=DEV, dtype=torch.float64, generator=g)
+    r = h.hash_aggregate(keys, vals, op, True)
+    assert int(r[5][1]) == 0, "LOW / MID path expected"              # status path: 0 = the LDS-table paths
+    _check_agg(keys, vals, op, r)
+    ivals = torch.randint(-1000, 1000, (n, 1), device=DEV, generator=g)
+    ri = h.hash_aggregate(keys, ivals, op, False)
+    _check_agg(keys, ivals, op, ri)
+    h.agg_set_mid(False)
+    try:
+        rp = h.hash_aggregate(keys, vals, op, True)
+    finally:
+        h.agg_set_mid(True)
+    assert int(rp[5][1]) == 1                                        # the PART path ran
+    o1, o2 = torch.argsort(r[0]), torch.argsort(rp[0])
+    assert torch.equal(r[0][o1], rp[0][o2]) and torch.equal(r[2][o1], rp[2][o2])
+    torch.testing.assert_close(r[1][o1], rp[1][o2], rtol=1e-12, atol=1e-12)
