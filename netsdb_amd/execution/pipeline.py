@@ -113,6 +113,16 @@ def _node_expr(node, argx: List[E]) -> E:
     raise Unfusable(type(node).__name__)
 
 
+_FUSABLE_NODES = (AttAccess, Values, KeyTuple, Like, IsIn, Select, Unary, Binary)
+
+
+def _node_ok(node) -> bool:
+    """Whether _node_expr takes this lambda node (the same test, without building the expression)."""
+    if isinstance(node, Literal):
+        return isinstance(node.value, (bool, int, float, str))
+    return isinstance(node, _FUSABLE_NODES)
+
+
 class StagePlan:
     """The fusable suffix of a stage: ``prefix`` atoms run eagerly, the rest is one fused launch per batch."""
 
@@ -153,11 +163,7 @@ def plan_stage(ops: List[dict], comps: dict, sink_atom: dict) -> Optional[StageP
         if o["lambda"].startswith("self_"):
             return True
         node = comps[o["comp"]].extract_lambdas().get(o["lambda"])
-        try:
-            _node_expr(node, [E("src", (), a) for a in o["input"]["atts"]])
-        except Unfusable:
-            return False
-        return node is not None
+        return node is not None and _node_ok(node)
 
     start = len(ops)
     while start > 0 and fusable(ops[start - 1]):
