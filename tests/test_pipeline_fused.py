@@ -304,3 +304,37 @@ def test_pipe_kernel_shapes_gpu():
     assert fn, "compiled mask kernel"
     m = h.pipe_mask(pt[:2], cols, lit, n, 5, -2, [], fn, PL.program_nreg(mprog, 5, -1, []), PL.JIT_ROWS).bool().cpu()
     assert torch.equal(m, ref_mask)
+
+
+def test_jit_every_opcode_and_column_kind_compiles_cpu():
+    """One program touching every opcode and every column kind (early and late) through jit_source + hiprtc: the
+    generated C++ of each instruction form compiles for gfx950 (the GPU tests check the values)."""
+    from netsdb_amd import _ext
+    if not _ext.hip_available() or not hasattr(_ext.hip(), "jit_compile"):
+        pytest.skip("kernel extension not built")
+    I = PL.IMM
+    kinds = [PL.C_SCODE, PL.C_SREF, PL.C_F64, PL.C_I64, PL.C_I32, PL.C_F32, PL.C_U8]
+    p = PL.Program()
+    p.cols = [{"kind": k, "late": 0, "L": 3} for k in kinds]
+    p.kpool = [100, 7]
+    r = 7
+    ins = []
+    for op in range(PL.OP_RNGI + 1):
+        if op in (PL.OP_SEQ, PL.OP_SPRE, PL.OP_SSUF):
+            ins.append((op, r, 1, 1, -1, 3, 0))              # bytes of column 1 (SREF) against literal 0..3
+        elif op == PL.OP_SEL:
+            ins.append((op, r, 8, 2, -1, 9, 0))
+        elif op in (PL.OP_RNGF, PL.OP_RNGI):
+            ins.append((op, r, 2 if op == PL.OP_RNGF else 3, -1, 8, 5, (op - PL.OP_RNGF) | (3 << 8)))
+        elif PL.OP_LTF <= op <= PL.OP_NEI:
+            ins.append((op, r, 2, I, 8, 1, 0))               # compare folded with register 8
+        else:
+            ins.append((op, r, 3, 4 if op != PL.OP_NOT else -1, -1, 2, 0))
+        r = 8 + (len(ins) % 7)
+    p.ins, p.nins_a, p.keep_reg, p.key_reg, p.val_regs = ins, 20, 9, 10, [11, 12, 13]
+    h, hdr = _ext.hip(), PL._jit_header()
+    for lates in ([0] * 7, [0, 0, 1, 1, 1, 1, 1]):
+        for kind in ("agg", "mask"):
+            src = PL.jit_source(p, kinds, lates, kind, p.key_reg if kind == "agg" else -1,
+                                p.val_regs if kind == "agg" else ())
+            assert len(h.jit_compile(src, hdr)) > 1000, (kind, lates)
