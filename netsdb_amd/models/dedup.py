@@ -440,7 +440,6 @@ class SharedInference:
 
     def __init__(self, tables: Dict[str, torch.Tensor], shapes: Dict[str, Tuple[int, int]], fetch, br: int, bc: int):
         self.names = list(tables)
-        self._side = {}
         T = torch.stack([tables[n].cpu() for n in self.names])          # [M, nbr, nbc]
         assert len({shapes[n] for n in self.names}) == 1, "SharedInference needs models of one shape"
         self.R, self.C = shapes[self.names[0]]
@@ -463,8 +462,6 @@ class SharedInference:
         self.common_runs = _runs(self.common_cols.tolist())
         self.priv_runs = _runs(self.priv_cols.tolist())
         self.common_cols, self.priv_cols = self.common_cols.to(dev), self.priv_cols.to(dev)
-
-    OVERLAP = True           # private panels on a side stream beside the shared GEMM (bench_dedup.py --no-overlap: A/B)
 
     def panel_bytes(self) -> int:
         ps = [p for p in (self.w_common, self.w_priv) if p is not None]
@@ -490,17 +487,6 @@ class SharedInference:
         X = X.to(ref.dtype)
         if X.shape[1] != self.nbc * self.bc:
             X = torch.nn.functional.pad(X, (0, self.nbc * self.bc - X.shape[1]))
-        overlap = self.OVERLAP and X.is_cuda and self.w_common is not None and self.w_priv is not None
-        side = None
-        if overlap:
-            # the private panels do not need the shared product until their final add: they stream on a side
-            # stream beside the shared GEMM, filling its tail and its reducer's gap with their own HBM traffic
-            cur = torch.cuda.current_stream(X.device)
-            side = self._side.get(X.device)
-            if side is None:
-                side = self._side[X.device] = torch.cuda.Stream(X.device)
-            side.wait_stream(cur)
-            X.record_stream(side)
         P = None
         if self.w_common is not None:
             for off, xv in self._xpart(X, self.common_cols, self.common_runs):
@@ -509,28 +495,15 @@ class SharedInference:
         if self.w_priv is None:
             return {n: P[: self.R] for n in self.names}
         M = self.w_priv.shape[0]
-        Y = None if overlap else P
-        with torch.cuda.stream(side) if overlap else _nullctx():
-            for off, xv in self._xpart(X, self.priv_cols, self.priv_runs):
-                wv = self.w_priv[:, :, off: off + xv.shape[1]]
-                # a narrow private slice of X is compacted first (a 20 MB copy; the GEMM then streams B
-                # rows 200 KB apart instead of 2 MB apart: 266 vs 296 us at 12 x 500 x 100 x 100k)
-                xv = xv.contiguous() if xv.stride(0) > 2 * xv.shape[1] else xv
-                xb = xv.unsqueeze(0).expand(M, -1, -1)            # batch stride 0: one X panel for every model
-                Y = ops.gemm_nt(wv, xb, Y, ops.BIAS_MAT if Y is not None else ops.BIAS_NONE, out_dtype=torch.float32)
-        if overlap:
-            cur.wait_stream(side)
-            Y.record_stream(cur)
-            Y += P.unsqueeze(0)
+        Y = P
+        for off, xv in self._xpart(X, self.priv_cols, self.priv_runs):
+            wv = self.w_priv[:, :, off: off + xv.shape[1]]
+            # a narrow private slice of X is compacted first (a 20 MB copy; the GEMM then streams B
+            # rows 200 KB apart instead of 2 MB apart: 266 vs 296 us at 12 x 500 x 100 x 100k)
+            xv = xv.contiguous() if xv.stride(0) > 2 * xv.shape[1] else xv
+            xb = xv.unsqueeze(0).expand(M, -1, -1)            # batch stride 0: one X panel for every model
+            Y = ops.gemm_nt(wv, xb, Y, ops.BIAS_MAT if Y is not None else ops.BIAS_NONE, out_dtype=torch.float32)
         return {n: Y[i, : self.R] for i, n in enumerate(self.names)}
-
-
-class _nullctx:
-    def __enter__(self):
-        return None
-
-    def __exit__(self, *a):
-        return False
 
 
 def _runs(cols) -> list:

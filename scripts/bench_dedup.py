@@ -46,11 +46,9 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--check", type=int, default=1, help="compare model 0's scores with an fp32 reference")
-    ap.add_argument("--no-overlap", action="store_true", help="private panels after the shared GEMM (A/B)")
     a = ap.parse_args()
 
     from netsdb_amd.models.dedup import DistributedBlockPool, SharedInference
-    SharedInference.OVERLAP = not a.no_overlap
     from netsdb_amd import ops
     from netsdb_amd.parallel.comm import ClusterContext
 
