@@ -775,6 +775,12 @@ def q02(client, db: str, size: int = 15, type_suffix: str = "BRASS", region: str
         return []
     b = RecordBatch.concat(got)
     b = _flat(b)
+    acct = b.columns["s_acctbal"]
+    if isinstance(acct, torch.Tensor) and acct.numel() > k:
+        # ORDER BY s_acctbal DESC, ... LIMIT k: only rows at or above the k-th balance can be in the answer (ties at
+        # that balance are decided by the string keys below), so only those cross to the host and get decoded
+        a64 = acct.double()
+        b = b.take(torch.nonzero(a64 >= torch.topk(a64, k).values[-1]).flatten())
     rows = [{"s_acctbal": float(a), "s_name": s, "n_name": n, "p_partkey": int(p), "p_mfgr": m}
             for a, s, n, p, m in zip(_as_list(b.columns["s_acctbal"]), _as_list(b.columns["s_name"]),
                                      _as_list(b.columns["n_name"]), _as_list(b.columns["p_partkey"]),
