@@ -217,3 +217,20 @@ def test_substr_gpu_matches_cpu_without_host_reads():
     assert sub.device.type == "cuda"
     assert sub.tolist() == cpu.tolist()
     assert h.cpu().tolist() == cpu.hash64().tolist()
+
+
+@pytest.mark.gpu
+def test_like_contains_random_small_alphabet_gpu():
+    """Contains-segments of LIKE (the dword-at-a-time two-byte candidate scan in strings.hip find_seg) against the
+    regex reference on random strings over a 3-letter alphabet: overlapping and repeated candidates, matches at
+    every alignment and at the very end of a string, '_' inside and at the head of segments."""
+    g = torch.Generator().manual_seed(21)
+    strs = []
+    for _ in range(4000):
+        n = int(torch.randint(0, 40, (1,), generator=g))
+        strs.append("".join("abc"[int(i)] for i in torch.randint(0, 3, (n,), generator=g)))
+    col = StringColumn.from_list(strs, "cuda:0")
+    pats = ["%ab%", "%aab%", "%abc%ca%", "%ba%ab%cc%", "%a_c%", "%_b%", "%cc%", "%abcabc%", "a%bc%", "%ab%c",
+            "%aa%aa%aa%", "%c_a_b%", "%bb%"]
+    for p in pats:
+        assert col.like(p).cpu().tolist() == [_like_ref(s, p) for s in strs], p
