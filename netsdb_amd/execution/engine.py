@@ -410,8 +410,7 @@ class QueryEngine:
             from . import pipeline as PL
 
             ops = PL.fuse_filters(ops, state.comps)
-        if FOLD_HASH_PROBE:
-            ops = _fuse_hash_probe(ops)
+        ops = _fuse_hash_probe(ops)
         for b in it:
             for o in ops:
                 if b.n == 0 and o["type"] != "JOIN":
@@ -970,9 +969,6 @@ def _mean_of(sc, dtype=torch.float64, shape=None):
     if shape is not None and len(shape) and int(torch.Size(shape).numel()) == m.shape[1]:
         return m.reshape((m.shape[0],) + tuple(shape))
     return m.squeeze(1) if m.shape[1] == 1 else m
-
-
-FOLD_HASH_PROBE = True      # fold a probe's HASH atom into the probe kernel (scripts/ab_fold_probe.py: A/B)
 
 
 def _fuse_hash_probe(ops):
