@@ -1062,9 +1062,6 @@ constexpr int kJTile = 4096;   // probe rows per workgroup tile (256 threads x 1
 // probe: matches (cnt) and payload per probe row, and the match total of each 4096-row tile. The first-slot
 // reads of all 16 rows of a thread are issued together (16 independent 16-byte loads in flight); only rows
 // whose first slot holds another key walk the probe chain.
-// RAW: the probe column holds the raw int64 join keys; each is hashed here exactly as the engine's HASH atom would
-// (mix64(key + GOLD), execution/kernels.py hash_keys), so the hash column is never written and re-read.
-template <bool RAW>
 __global__ __launch_bounds__(256) void join_probe_kernel(const u64* __restrict__ keys, i64 m,
                                                          const JSlot* __restrict__ tab, u64 mask,
                                                          unsigned* __restrict__ cnt, unsigned* __restrict__ pay,
@@ -1078,7 +1075,6 @@ __global__ __launch_bounds__(256) void join_probe_kernel(const u64* __restrict__
   for (int j = 0; j < J; ++j) {
     const i64 i = t0 + j * 256 + threadIdx.x;
     k[j] = i < m ? keys[i] : 0;
-    if (RAW) k[j] = mix64(k[j] + 0x9E3779B97F4A7C15ull);
   }
   u64 sl[J];
   JSlot e[J];
@@ -1506,15 +1502,11 @@ long long nsdb_join_tiles(long long m) { return (m + kJTile - 1) / kJTile; }
 
 // cnt / pay [m] u32, tile_sum [nsdb_join_tiles(m)] i64
 int nsdb_join_probe(const void* keys, long long m, const void* tab, long long cap, unsigned* cnt, unsigned* pay,
-                    long long* tile_sum, int raw, hipStream_t st) {
+                    long long* tile_sum, hipStream_t st) {
   if (m <= 0) return 0;
   if (cap <= 0 || (cap & (cap - 1)) != 0) return (int)hipErrorInvalidValue;
-  if (raw)
-    hipLaunchKernelGGL(join_probe_kernel<true>, dim3((unsigned)nsdb_join_tiles(m)), dim3(256), 0, st, (const u64*)keys,
-                       m, (const JSlot*)tab, (u64)(cap - 1), cnt, pay, tile_sum);
-  else
-    hipLaunchKernelGGL(join_probe_kernel<false>, dim3((unsigned)nsdb_join_tiles(m)), dim3(256), 0, st, (const u64*)keys,
-                       m, (const JSlot*)tab, (u64)(cap - 1), cnt, pay, tile_sum);
+  hipLaunchKernelGGL(join_probe_kernel, dim3((unsigned)nsdb_join_tiles(m)), dim3(256), 0, st, (const u64*)keys, m,
+                     (const JSlot*)tab, (u64)(cap - 1), cnt, pay, tile_sum);
   return (int)hipGetLastError();
 }
 

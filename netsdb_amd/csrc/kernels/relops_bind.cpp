@@ -25,7 +25,7 @@ int nsdb_join_perm(const int* row_slot, const unsigned* row_rank, long long n, c
                    unsigned long long* bump, void* tab, long long cap, long long* perm, hipStream_t st);
 long long nsdb_join_tiles(long long m);
 int nsdb_join_probe(const void* keys, long long m, const void* tab, long long cap, unsigned* cnt, unsigned* pay,
-                    long long* tile_sum, int raw, hipStream_t st);
+                    long long* tile_sum, hipStream_t st);
 int nsdb_join_expand(const unsigned* cnt, const unsigned* pay, long long m, const long long* tile_base,
                      const long long* perm, long long* bidx, long long* pidx, hipStream_t st);
 long long nsdb_part_work_bytes(long long n, int P);
@@ -220,8 +220,7 @@ std::vector<torch::Tensor> join_build(torch::Tensor keys) {
 }
 
 // Probe a built table with m int64 keys: all (build row, probe row) pairs with equal keys, probe-major.
-// raw: keys are the raw int64 join keys (hashed in the probe kernel like the engine's HASH atom), else join hashes
-std::vector<torch::Tensor> join_probe(torch::Tensor tab, torch::Tensor perm, torch::Tensor keys, bool raw) {
+std::vector<torch::Tensor> join_probe(torch::Tensor tab, torch::Tensor perm, torch::Tensor keys) {
   TORCH_CHECK(keys.is_cuda() && keys.scalar_type() == torch::kInt64 && keys.dim() == 1, "keys: 1-D int64 GPU tensor");
   TORCH_CHECK(tab.is_cuda() && tab.scalar_type() == torch::kInt64 && tab.dim() == 2 && tab.size(1) == 2 &&
                   tab.is_contiguous() && perm.scalar_type() == torch::kInt64,
@@ -239,8 +238,7 @@ std::vector<torch::Tensor> join_probe(torch::Tensor tab, torch::Tensor perm, tor
   const int64_t tiles = nsdb_join_tiles(m);
   auto tsum = torch::empty({tiles + 1}, i64);
   rc_ok(nsdb_join_probe(keys.data_ptr(), m, tab.data_ptr(), cap, reinterpret_cast<unsigned*>(cnt.data_ptr<int>()),
-                        reinterpret_cast<unsigned*>(pay.data_ptr<int>()), LL(tsum.data_ptr<int64_t>()), raw ? 1 : 0,
-                        stream()),
+                        reinterpret_cast<unsigned*>(pay.data_ptr<int>()), LL(tsum.data_ptr<int64_t>()), stream()),
         "join_probe");
   auto incl = torch::cumsum(tsum.narrow(0, 0, tiles), 0);
   const int64_t total = incl[tiles - 1].item<int64_t>();   // sizes the output (one host read)
@@ -343,9 +341,7 @@ void register_relops(pybind11::module& m) {
         pybind11::arg("want_inv") = false, pybind11::arg("low_threshold") = 0, pybind11::arg("want_first") = true,
         pybind11::arg("scratch") = pybind11::none());
   m.def("join_build", &join_build, "device hash-join build: (table, perm)");
-  m.def("join_probe", &join_probe, "device hash-join probe: (build_idx, probe_idx); raw: the keys are raw int64 join "
-        "keys hashed in the kernel", pybind11::arg("tab"), pybind11::arg("perm"), pybind11::arg("keys"),
-        pybind11::arg("raw") = false);
+  m.def("join_probe", &join_probe, "device hash-join probe: (build_idx, probe_idx)");
   m.def("partition_perm", &partition_perm, "stable device partition permutation: (perm, counts)");
   m.def("agg_set_mid", [](bool on) { g_agg_mid = on; }, "enable / disable the MID group-by path (hash-partitioned LDS "
         "tables sharing their rows through L2); returns nothing", pybind11::arg("on"));

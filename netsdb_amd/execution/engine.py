@@ -404,13 +404,11 @@ class QueryEngine:
 
     def _apply_ops(self, ops, it, state):
         """Stream batches through a segment's atoms (generator: one page in flight per stage). Runs of lambda-tree
-        APPLYs ending in their FILTER execute as one fused predicate launch (execution/pipeline.py); a HASH atom
-        whose column only feeds the next atom's probe of a built join table is folded into that probe."""
+        APPLYs ending in their FILTER execute as one fused predicate launch (execution/pipeline.py)."""
         if self.fused_pipelines and any(o["type"] == "FILTER" for o in ops):
             from . import pipeline as PL
 
             ops = PL.fuse_filters(ops, state.comps)
-        ops = _fuse_hash_probe(ops)
         for b in it:
             for o in ops:
                 if b.n == 0 and o["type"] != "JOIN":
@@ -537,11 +535,6 @@ class QueryEngine:
             return RecordBatch(cols, len(flat))
         if t == "JOIN":
             return self._probe(a, b, state)
-        if t == "HASH_PROBE":
-            h = a["hash"]
-            raw = b.columns[h["input"]["atts"][0]]
-            hb = RecordBatch({c: b.columns[c] for c in h["projection"]["atts"]}, b.n)
-            return self._probe(a["join"], hb, state, raw_keys=raw)
         if t == "FUSED_FILTER":
             from . import pipeline as PL
 
@@ -556,23 +549,15 @@ class QueryEngine:
             return b
         raise ValueError(f"atom {t} is not streaming")
 
-    def _probe(self, a, b: RecordBatch, state, raw_keys=None) -> RecordBatch:
-        """raw_keys: the probe side's join key column (a folded HASH atom, `_fuse_hash_probe`): hashed inside the
-        probe kernel for an int64 device column, else hashed here first."""
+    def _probe(self, a, b: RecordBatch, state) -> RecordBatch:
         bt: BuildTable = state.builds[a["output"]["name"]]
         side = a["_probe_side"]
         lh, rh = a["input"]["atts"][0], a["input2"]["atts"][0]
         lcols, rcols = a["projection"]["atts"], a["projection2"]["atts"]
+        probe_h = b.columns[lh if side == "left" else rh]
         if bt.batch is None or bt.batch.n == 0 or b.n == 0:
             bi = pi = torch.empty(0, dtype=torch.int64, device=b.device)
-        elif raw_keys is not None:
-            dev = raw_keys.device if isinstance(raw_keys, torch.Tensor) else b.device
-            if isinstance(raw_keys, torch.Tensor) and raw_keys.dim() == 1 and raw_keys.dtype == torch.int64:
-                bi, pi = bt.table(dev).probe_raw(raw_keys)
-            else:
-                bi, pi = bt.table(dev).probe(K.hash_keys(raw_keys, b.device))
         else:
-            probe_h = b.columns[lh if side == "left" else rh]
             bi, pi = bt.table(probe_h.device).probe(probe_h)
         pb = RecordBatch({c: b.columns[c] for c in (lcols if side == "left" else rcols)}, b.n).take(pi)
         if bt.batch is None:
@@ -969,30 +954,6 @@ def _mean_of(sc, dtype=torch.float64, shape=None):
     if shape is not None and len(shape) and int(torch.Size(shape).numel()) == m.shape[1]:
         return m.reshape((m.shape[0],) + tuple(shape))
     return m.squeeze(1) if m.shape[1] == 1 else m
-
-
-def _fuse_hash_probe(ops):
-    """[HASHLEFT / HASHRIGHT of one key column, JOIN probing a built table with that hash] -> one HASH_PROBE atom
-    when the hash column is used by nothing but that probe (not in the join's projection): the probe then hashes
-    the raw key itself (kernels.JoinTable.probe_raw)."""
-    out, k = [], 0
-    while k < len(ops):
-        h = ops[k]
-        j = ops[k + 1] if k + 1 < len(ops) else None
-        if (j is not None and h["type"] in ("HASHLEFT", "HASHRIGHT") and len(h["input"]["atts"]) == 1 and
-                j["type"] == "JOIN" and "_probe_side" in j):
-            side = j["_probe_side"]
-            src = j["input"] if side == "left" else j["input2"]
-            hcol = h["output"]["atts"][-1]
-            proj = j["projection"]["atts"] if side == "left" else j["projection2"]["atts"]
-            if src["name"] == h["output"]["name"] and src["atts"] and src["atts"][0] == hcol and hcol not in proj \
-                    and all(c in h["projection"]["atts"] for c in proj):
-                out.append({"type": "HASH_PROBE", "hash": h, "join": j, "output": j["output"]})
-                k += 2
-                continue
-        out.append(h)
-        k += 1
-    return out
 
 
 class _JobState:

@@ -128,14 +128,6 @@ class JoinTable:
             # builds past the device table's 2^29-row bound (32-bit payloads): sorted keys + binary search, on the device
             self._sorted = torch.sort(build_h)
 
-    def probe_raw(self, keys: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-        """probe(hash_keys(keys)) for one int64 key column, with the hash computed inside the device probe kernel
-        (no hash column written and read back); other cases hash first."""
-        if self._dev is not None and keys.is_cuda and keys.dim() == 1 and keys.dtype == torch.int64 and self.n:
-            tab, perm = self._dev
-            return tuple(_ext.hip().join_probe(tab, perm, keys.to(tab.device).contiguous(), True))
-        return self.probe(hash_keys(keys, keys.device))
-
     def probe(self, probe_h: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """All (build_idx, probe_idx) pairs with equal keys, probe-major."""
         dev = probe_h.device

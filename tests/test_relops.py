@@ -591,17 +591,3 @@ def test_hash_aggregate_mid_path(distinct, op):
     o1, o2 = torch.argsort(r[0]), torch.argsort(rp[0])
     assert torch.equal(r[0][o1], rp[0][o2]) and torch.equal(r[2][o1], rp[2][o2])
     torch.testing.assert_close(r[1][o1], rp[1][o2], rtol=1e-12, atol=1e-12)
-
-
-@pytest.mark.gpu
-def test_join_probe_raw_keys_matches_hashed_probe():
-    """JoinTable.probe_raw (the key hashed inside the probe kernel, the engine's folded HASH atom) returns exactly the
-    pairs of probe(hash_keys(keys)): repeated build keys, misses, negative keys."""
-    g = torch.Generator(device=DEV).manual_seed(13)
-    build = torch.randint(-50_000, 50_000, (200_000,), device=DEV, generator=g)
-    probe = torch.randint(-80_000, 80_000, (1_000_003,), device=DEV, generator=g)
-    t = K.JoinTable(K.hash_keys(build, build.device))
-    b1, p1 = t.probe(K.hash_keys(probe, probe.device))
-    b2, p2 = t.probe_raw(probe)
-    assert torch.equal(b1, b2) and torch.equal(p1, p2)
-    assert torch.equal(build[b2], probe[p2])
