@@ -805,8 +805,11 @@ def _col_args(prog: Program, dev):
 # shape by hiprtc inside the process (immediates stay kernel arguments: one kernel per query shape, not per literal)
 # and cached in memory and on disk. NSDB_PIPE_JIT=0 keeps the interpreter kernels (TILE) for every stage.
 JIT = os.environ.get("NSDB_PIPE_JIT", "1") != "0"
-JIT_ROWS = 4                                 # rows per thread per iteration of the compiled kernels (JIT_ROWS_SMALL
-JIT_ROWS_SMALL = 8                           # for programs of at most JIT_SMALL_NREG registers)
+# rows per thread per iteration of the compiled kernels (JIT_ROWS_SMALL for programs of at most JIT_SMALL_NREG
+# registers); SF 10 launch times by rows 2 / 4 / 8 (profiles/r5_jit/ab_jit_rows.log): Q01 0.96 / 1.00 / 1.22 ms,
+# Q06 0.44 / 0.41 / 0.41, the Q14 mask 0.162 / 0.165 / 0.175
+JIT_ROWS = 2
+JIT_ROWS_SMALL = 4
 JIT_SMALL_NREG = 8
 JIT_STATS = {"compiled": 0, "disk_hits": 0, "launches": 0, "failed": 0}
 _JIT_FN: Dict[str, Optional[int]] = {}       # generated source -> kernel handle (None: compile failed)
