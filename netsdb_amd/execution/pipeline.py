@@ -787,7 +787,12 @@ def _col_args(prog: Program, dev):
     for c in prog.cols:
         o = c["obj"]
         if c["kind"] == C_SCODE:
-            codes = o.short_codes(c["L"])          # the column's kept fixed-width encoding: a plain int64 load
+            # the column's kept fixed-width encoding: a plain int32 (codes of <= 3 bytes) or int64 load
+            codes = o.short_codes32(c["L"]) if o.device.type == "cuda" else None
+            if codes is not None:
+                out.append((C_I32, c["late"], 0, codes.contiguous(), None, None, None))
+                continue
+            codes = o.short_codes(c["L"])
             if codes is not None:
                 out.append((C_I64, c["late"], 0, codes.contiguous(), None, None, None))
                 continue
