@@ -818,6 +818,7 @@ JIT_ROWS_SMALL = 4
 JIT_SMALL_NREG = 8
 JIT_STATS = {"compiled": 0, "disk_hits": 0, "launches": 0, "failed": 0}
 _JIT_FN: Dict[str, Optional[int]] = {}       # generated source -> kernel handle (None: compile failed)
+_JIT_SHAPES: Dict[tuple, tuple] = {}         # program shape -> (kernel handle or None, nreg, rows)
 _JIT_HEADER: Optional[str] = None
 _FOPS = {OP_ADDF: "+", OP_SUBF: "-", OP_MULF: "*", OP_DIVF: "/"}
 _IOPS = {OP_ADDI: "+", OP_SUBI: "-", OP_MULI: "*"}
@@ -1022,19 +1023,28 @@ def _jit_for(prog: Program, cargs, kind: str, key_reg: int = -1, val_regs=()):
     """(kernel handle, nreg, rows) of the compiled kernel for this launch, or None (interpreter)."""
     if not JIT or not hasattr(_ext.hip(), "jit_compile"):
         return None
-    kinds = [c[0] for c in cargs]
-    lates = [c[1] for c in cargs]
-    nreg = program_nreg(prog, len(kinds), key_reg, val_regs)
-    rows = JIT_ROWS_SMALL if nreg <= JIT_SMALL_NREG else JIT_ROWS
-    try:
-        src = jit_source(prog, kinds, lates, kind, key_reg, val_regs, rows=rows)
-    except Unfusable:
-        return None
-    fn = jit_kernel(src, "nsdb_jit_agg" if kind == "agg" else "nsdb_jit_mask")
-    if fn is None:
+    kinds = tuple(c[0] for c in cargs)
+    lates = tuple(c[1] for c in cargs) if kind == "agg" else ()
+    # the kernel of a program shape: generated + compiled once, then found by the shape alone (generating the source
+    # costs ~30 us of Python per launch)
+    shape = (kind, tuple(prog.ins), kinds, lates, key_reg, tuple(val_regs), prog.keep_reg, prog.nins_a, JIT_ROWS,
+             JIT_ROWS_SMALL, JIT_SMALL_NREG)
+    hit = _JIT_SHAPES.get(shape)
+    if hit is None:
+        nreg = program_nreg(prog, len(kinds), key_reg, val_regs)
+        rows = JIT_ROWS_SMALL if nreg <= JIT_SMALL_NREG else JIT_ROWS
+        try:
+            src = jit_source(prog, list(kinds), list(lates) or [0] * len(kinds), kind, key_reg, val_regs, rows=rows)
+        except Unfusable:
+            return None
+        fn = jit_kernel(src, "nsdb_jit_agg" if kind == "agg" else "nsdb_jit_mask")
+        if len(_JIT_SHAPES) >= 4096:          # the shape includes the immediates: bound it for varying literals
+            _JIT_SHAPES.clear()
+        hit = _JIT_SHAPES[shape] = (fn, nreg, rows)
+    if hit[0] is None:
         return None
     JIT_STATS["launches"] += 1
-    return fn, nreg, rows
+    return hit
 
 
 def _launch(prog: Program, n: int, dev, plan: StagePlan):
