@@ -146,19 +146,24 @@ class QueryEngine:
     # ------------------------------------------------------------------ entry
     def _compile(self, sinks, job_name, stats):
         """TCAP for the graph: from the pre-compiled workload cache when a structurally identical graph
-        ran (or was pre-compiled) before — no TCAP emission, no parse — else compile + native parse."""
+        ran (or was pre-compiled) before — no TCAP emission, no parse — else compile + native parse.  Also returns
+        the graph key (signature + lambda constants) later per-graph caches use, or None."""
         sig, comps, sets = (None, None, None)
+        gkey = None
         if self.plan_cache_enabled:
+            vals: list = []
             try:
-                sig, comps, sets = graph_signature(sinks)
+                sig, comps, sets = graph_signature(sinks, vals)
+                gkey = (sig, tuple(vals))
+                hash(gkey)
             except Exception:          # a graph the signature walk cannot key: always compile
-                sig = None
+                sig = gkey = None
         hit = self._plan_cache.get(sig) if sig is not None else None
         if hit is not None:
             self.cache_stats["tcap_cache_hits"] += 1
             stats["tcap_cached"] = True
             tcap, atoms = hit
-            return bind_atoms(atoms, sets), comps, tcap
+            return bind_atoms(atoms, sets), comps, tcap, gkey
         plan = compile_tcap(sinks)
         with self.tracer.span("parse_tcap", job=job_name):
             atoms = _ext.native().parse_tcap(plan.tcap)
@@ -168,7 +173,7 @@ class QueryEngine:
             self._plan_cache[sig] = (plan.tcap, atoms)
             while len(self._plan_cache) > 256:
                 self._plan_cache.pop(next(iter(self._plan_cache)))
-        return atoms, plan.computations, plan.tcap
+        return atoms, plan.computations, plan.tcap, gkey
 
     def _timed_stage(self, st, state, stats, job_name):
         sync = STAGE_SYNC and torch.cuda.is_available()
@@ -229,7 +234,7 @@ class QueryEngine:
                 stats["seconds"] = time.perf_counter() - t0
                 self.last_plan = self.last_tcap = self._last_comps = None
                 return stats
-        atoms, comps, tcap = self._compile(sinks, job_name, stats)
+        atoms, comps, tcap, gkey = self._compile(sinks, job_name, stats)
         self.last_tcap = tcap
         self._last_comps = comps
         if pre_compile:
@@ -237,6 +242,7 @@ class QueryEngine:
             stats["seconds"] = time.perf_counter() - t0
             return stats
         state = _JobState(comps)
+        state.graph_key = gkey
         ooc0 = dict(self.ooc_stats)
         self._copart = self._copartitioned_joins(atoms, comps) if self.ctx.distributed else set()
         if self._copart:
@@ -343,7 +349,7 @@ class QueryEngine:
         if self.fused_pipelines and st.sink.get("kind") == "aggregate":
             from . import pipeline as PL
 
-            fplan = PL.plan_stage(segments[-1], state.comps, st.sink["atom"])
+            fplan = PL.plan_stage(segments[-1], state.comps, st.sink["atom"], state.graph_key)
             if fplan is not None:
                 segments[-1] = fplan.prefix
                 # one rank: the launches' few pre-aggregated rows stay on the host, the sink reduces them there
@@ -963,6 +969,7 @@ class _JobState:
         self.builds: Dict[str, BuildTable] = {}
         self.fused_out_device = None     # a fused stage's host-resident partials: the device its result returns to
         self.unique_kv: List = []        # key columns of fused launch results (unique keys by construction)
+        self.graph_key = None            # (graph signature, lambda constants): keys per-graph plan caches
 
 
 def _upload(x, dev):
@@ -972,6 +979,8 @@ def _upload(x, dev):
         return RecordBatch({k: _upload(c, dev) for k, c in x.columns.items()}, x.n, x.type)
     if isinstance(x, tuple):
         return tuple(_upload(c, dev) for c in x)
+    if isinstance(x, torch.Tensor) and x.numel() <= 64 and x.device.type == "cpu":
+        return x.to(dev)                         # a few values: one small copy beats pinning a new host buffer
     if isinstance(x, torch.Tensor):
         return x.pin_memory().to(dev, non_blocking=True) if x.device.type == "cpu" else x
     if isinstance(x, StringColumn):

@@ -145,8 +145,34 @@ class StagePlan:
         return self._sig
 
 
-def plan_stage(ops: List[dict], comps: dict, sink_atom: dict) -> Optional[StagePlan]:
-    """The fusable suffix of ``ops`` feeding the aggregation ``sink_atom``, or None."""
+_STAGE_CACHE: Dict[tuple, Optional[tuple]] = {}    # (graph key, stage atoms, sink) -> plan_stage's expressions
+_STAGE_CACHE_MAX = 512
+_MISS = object()
+
+
+def plan_stage(ops: List[dict], comps: dict, sink_atom: dict, graph_key=None) -> Optional[StagePlan]:
+    """The fusable suffix of ``ops`` feeding the aggregation ``sink_atom``, or None.  With ``graph_key`` (the graph's
+    structural signature + every lambda constant, engine._compile) a repeated query re-uses the expressions built the
+    first time; the returned plan is always new and bound to this execution's atoms."""
+    ck = None
+    if graph_key is not None:
+        ck = (graph_key, tuple(o["output"]["name"] for o in ops), sink_atom["output"]["name"])
+        hit = _STAGE_CACHE.get(ck, _MISS)
+        if hit is not _MISS:
+            if hit is None:
+                return None
+            start, conj, key, val, op, kcol, vcol = hit
+            return StagePlan(ops[:start], ops[start:], conj, key, val, op, kcol, vcol)
+    plan = _plan_stage(ops, comps, sink_atom)
+    if ck is not None:
+        if len(_STAGE_CACHE) >= _STAGE_CACHE_MAX:
+            _STAGE_CACHE.pop(next(iter(_STAGE_CACHE)))
+        _STAGE_CACHE[ck] = None if plan is None else (
+            len(plan.prefix), plan.conj, plan.key, plan.val, plan.op, plan.kcol, plan.vcol)
+    return plan
+
+
+def _plan_stage(ops: List[dict], comps: dict, sink_atom: dict) -> Optional[StagePlan]:
     from ..computations import AggregateComp, TopKComp
 
     comp = comps.get(sink_atom["comp"])

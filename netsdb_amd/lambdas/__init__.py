@@ -56,10 +56,13 @@ class Lambda:
 
     def nodes_postorder(self) -> List["Lambda"]:
         out: List[Lambda] = []
-        for c in self.children:
-            out.extend(c.nodes_postorder())
-        out.append(self)
+        self._postorder(out)
         return out
+
+    def _postorder(self, out: List["Lambda"]) -> None:
+        for c in self.children:
+            c._postorder(out)
+        out.append(self)
 
     def assign_names(self, counter=None) -> "Lambda":
         counter = counter if counter is not None else itertools.count()

@@ -12,7 +12,7 @@ from __future__ import annotations
 
 import itertools
 from dataclasses import dataclass
-from typing import Dict, List, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 from ..computations import (AggregateComp, Computation, JoinComp, MultiSelectionComp, PartitionComp, ScanSet,
                             SelectionComp, TopKComp, WriteSet)
@@ -261,14 +261,34 @@ def _lam_tokens(lam: Lambda) -> tuple:
                  for n in lam.nodes_postorder())
 
 
-def graph_signature(sinks: Sequence[Computation]) -> Tuple[tuple, Dict[str, Computation], Dict[str, Tuple[str, str]]]:
+_PRIM = (bool, int, float, str, type(None))
+
+
+def _node_values(n) -> tuple:
+    """The constants a lambda node carries (literal value, LIKE pattern, IN list): not part of the graph signature
+    but of any plan decision made from the values (execution/pipeline.py's fused stage expressions)."""
+    out = []
+    for a in ("value", "pattern", "negate", "values"):
+        v = getattr(n, a, None)
+        if isinstance(v, list):
+            v = tuple(x if isinstance(x, _PRIM) else ("?", type(x).__name__) for x in v)
+        elif not isinstance(v, _PRIM):
+            v = ("?", type(v).__name__)          # not a fusable constant: its type decides the plan
+        out.append(v)
+    return tuple(out)
+
+
+def graph_signature(sinks: Sequence[Computation], values: Optional[list] = None
+                    ) -> Tuple[tuple, Dict[str, Computation], Dict[str, Tuple[str, str]]]:
     """Structural key of a computation graph + its TCAP name bindings, WITHOUT emitting TCAP.
 
     Walks the graph in exactly the compiler's order and binds every computation's name and lambda
     names the same way (so a cached TCAP / parsed atom list can execute against this graph instance):
     two graphs with the same signature compile to the same TCAP text.  Lambda literal values and native
     lambda bodies are looked up on the live objects at run time, so they are not part of the key
-    (QuerySchedulerServer's pre-compiled workloads, src/queryPlanning/headers/PreCompiledWorkload.h)."""
+    (QuerySchedulerServer's pre-compiled workloads, src/queryPlanning/headers/PreCompiledWorkload.h).
+    ``values``, when given, receives every lambda node's constants in the same walk (signature + values key plans
+    that depend on the constants)."""
     comps: Dict[str, Computation] = {}
     names: Dict[int, str] = {}
     sets: Dict[str, Tuple[str, str]] = {}
@@ -276,10 +296,20 @@ def graph_signature(sinks: Sequence[Computation]) -> Tuple[tuple, Dict[str, Comp
     toks: List[tuple] = []
 
     def reg(comp, lam, lc):
-        lam.assign_names(lc)
+        # assign_names + the name table + _lam_tokens in ONE walk of the tree (this runs on every execution)
+        d = comp._lambdas
+        out = []
         for n in lam.nodes_postorder():
-            comp._lambdas[n.name] = n
-        return _lam_tokens(lam)
+            if n.name is None:
+                n.name = f"{n.kind}_{next(lc)}"
+            d[n.name] = n
+            if values is not None:
+                nd = n.__dict__
+                if "value" in nd or "pattern" in nd or "values" in nd:
+                    values.append((n.name, _node_values(n)))
+            out.append((type(n).__name__, n.kind, n.name, getattr(n, "field", None), getattr(n, "method", None),
+                        getattr(n, "op", None), tuple(n.input_indices()) if not n.children else len(n.children)))
+        return tuple(out)
 
     def visit(comp) -> str:
         if id(comp) in names:

@@ -424,8 +424,9 @@ def _collect(client, db: str, name: str) -> List[RecordBatch]:
 
 def _run(client, db: str, out: str, comp, job: str):
     if client.storage.has_set(db, out):
-        client.remove_set(db, out)
-    client.create_set(db, out, None)
+        client.clear_set(db, out)                # a re-run: empty the result set (no catalog transactions)
+    else:
+        client.create_set(db, out, None)
     client.execute_computations(WriteSet(db, out).set_input(comp), job_name=job)
     got = _collect(client, db, out)
     if not got:

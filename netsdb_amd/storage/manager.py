@@ -271,13 +271,17 @@ class StorageManager:
         with self.lock:
             ent = self._resident.get(id(self._set_of(pages[0])))
             od = ent[1] if ent is not None else None
-            clock = self._clock
+            t = next(self._clock)                # one stamp for the run: ties inside it fall back to the set's order
             for p in pages:
-                p.last_use = next(clock)
-                if od is not None:
-                    k = id(p)
-                    if k in od:
-                        od.move_to_end(k)
+                p.last_use = t
+            if od is None:
+                return
+            ids = [id(p) for p in pages]
+            if len(od) >= len(ids) and list(itertools.islice(reversed(od), len(ids))) == ids[::-1]:
+                return                           # the run already is the set's most recent tail, in order
+            for k in ids:
+                if k in od:
+                    od.move_to_end(k)
 
     @staticmethod
     def _resident_on_device(p) -> bool:

@@ -109,9 +109,11 @@ def main():
                 pr = cProfile.Profile()
                 torch.cuda.synchronize()
                 pr.enable()
-                fn(c, "tpch")
-                torch.cuda.synchronize()
+                for _ in range(20):                   # 20 runs: per-call times resolve to microseconds
+                    fn(c, "tpch")
+                    torch.cuda.synchronize()
                 pr.disable()
+                pr.dump_stats(os.path.join(a.host_profile, f"{q}_sf{sf:g}.prof"))
                 with open(os.path.join(a.host_profile, f"{q}_sf{sf:g}.txt"), "w") as f:
                     pstats.Stats(pr, stream=f).sort_stats("cumulative").print_stats(60)
             ok = None

@@ -160,6 +160,28 @@ def test_fused_operators_cpu_interpreter(case, monkeypatch):
     assert torch.allclose(eager[1], fused[1], rtol=1e-12, atol=1e-9)
 
 
+def test_fused_stage_cache_keys_constants(monkeypatch):
+    """Repeated graphs re-use their fused stage expressions (plan_stage's cache), but a literal, IN list or LIKE
+    pattern that changes between runs of the same graph shape must change the plan: fused == eager for each."""
+    monkeypatch.setenv("NSDB_DEVICE_STRINGS", "1")
+    t = tpch_gen.generate_fast(0.002, seed=9)
+    c = _client("cpu", t)
+    variants = [(q, modes, pat) for q in (10, 30) for modes in (["MAIL"], ["TRUCK", "AIR"]) for pat in ("%PERSON", "%RN")]
+
+    def job(q, modes, pat):
+        return _agg_job(c, lambda x: (x.l_quantity > q) & IsIn(x.l_shipmode, modes) & Like(x.l_shipinstruct, pat),
+                        lambda x: x.l_linestatus, lambda x: Values(x.l_extendedprice), "sum")
+
+    eager = [job(*v) for v in variants]
+    monkeypatch.setattr(PL, "CPU_INTERPRETER", True)
+    PL._STAGE_CACHE.clear()
+    for _ in range(2):                               # the second pass hits the cache for every variant
+        for v, e in zip(variants, eager):
+            f = job(*v)
+            assert e[0] == f[0] and torch.allclose(e[1], f[1], rtol=1e-12, atol=1e-9), v
+    assert len(PL._STAGE_CACHE) == len(variants)
+
+
 def test_fused_overflow_falls_back(monkeypatch):
     """More groups than the kernel's per-workgroup tables: the batch takes the eager atoms, same result."""
     monkeypatch.setenv("NSDB_DEVICE_STRINGS", "1")
