@@ -979,8 +979,6 @@ def _upload(x, dev):
         return RecordBatch({k: _upload(c, dev) for k, c in x.columns.items()}, x.n, x.type)
     if isinstance(x, tuple):
         return tuple(_upload(c, dev) for c in x)
-    if isinstance(x, torch.Tensor) and x.numel() <= 64 and x.device.type == "cpu":
-        return x.to(dev)                         # a few values: one small copy beats pinning a new host buffer
     if isinstance(x, torch.Tensor):
         return x.pin_memory().to(dev, non_blocking=True) if x.device.type == "cpu" else x
     if isinstance(x, StringColumn):
