@@ -763,6 +763,7 @@ def _compile_cached(plan: StagePlan, batch: RecordBatch) -> Program:
         p.cols = [dict(c, obj=_resolve(c["expr"], batch)) for c in hit.cols]
         return p
     p = _Compiler(plan, batch).compile()
+    _prog_tensors(p, batch.device)              # built once here: every cached copy shares them
     if len(_PROG_CACHE) >= _PROG_CACHE_MAX:
         _PROG_CACHE.pop(next(iter(_PROG_CACHE)))
     _PROG_CACHE[key] = p
@@ -1075,12 +1076,30 @@ def _jit_for(prog: Program, cargs, kind: str, key_reg: int = -1, val_regs=()):
     return hit
 
 
+_LIT_DEV: Dict[tuple, torch.Tensor] = {}       # (literal bytes, device) -> the pool on the device (read-only)
+
+
+def _prog_tensors(prog: Program, dev):
+    """The program's instruction table (host int64 [nins, 7]) and its literal pool on ``dev``: built once per compiled
+    program / literal pool and shared by every launch of it (a cached program's copies share its ``_ins_t``)."""
+    ins = prog.__dict__.get("_ins_t")
+    if ins is None:
+        ins = torch.tensor(prog.ins if prog.ins else [[0, 0, -1, -1, -1, 0, 0]], dtype=torch.int64).reshape(-1, 7)
+        if not prog.ins:
+            ins = ins[:0]
+        prog._ins_t = ins
+    key = (bytes(prog.lit or b"\0"), dev)
+    lit = _LIT_DEV.get(key)
+    if lit is None:
+        if len(_LIT_DEV) >= 256:
+            _LIT_DEV.clear()
+        lit = _LIT_DEV[key] = torch.frombuffer(bytearray(key[0]), dtype=torch.uint8).to(dev)
+    return ins, lit
+
+
 def _launch(prog: Program, n: int, dev, plan: StagePlan):
     h = _ext.hip()
-    ins = torch.tensor(prog.ins if prog.ins else [[0, 0, -1, -1, -1, 0, 0]], dtype=torch.int64).reshape(-1, 7)
-    if not prog.ins:
-        ins = ins[:0]
-    lit = torch.frombuffer(bytearray(prog.lit or b"\0"), dtype=torch.uint8).to(dev, non_blocking=True)
+    ins, lit = _prog_tensors(prog, dev)
     cargs = _col_args(prog, dev)
     jit = _jit_for(prog, cargs, "agg", prog.key_reg, prog.val_regs)
     fn, jnreg, jrows = jit if jit else (0, 0, 0)
@@ -1322,8 +1341,7 @@ def run_filter(plan: FilterPlan, batch: RecordBatch) -> Optional[RecordBatch]:
         plan.reason = str(e)
         return None
     if on_gpu:
-        ins = torch.tensor(prog.ins, dtype=torch.int64).reshape(-1, 7)
-        lit = torch.frombuffer(bytearray(prog.lit or b"\0"), dtype=torch.uint8).to(dev, non_blocking=True)
+        ins, lit = _prog_tensors(prog, dev)
         cargs = _col_args(prog, dev)
         jit = _jit_for(prog, cargs, "mask")
         fn, jnreg, jrows = jit if jit else (0, 0, 0)
