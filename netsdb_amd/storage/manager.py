@@ -263,9 +263,9 @@ class StorageManager:
             if ent is not None and id(page) in ent[1]:
                 ent[1].move_to_end(id(page))
 
-    def touch_run(self, pages):
+    def touch_run(self, pages, ids=None):
         """touch() of consecutive pages of ONE set, oldest first, under one lock acquisition (a coalesced scan's run
-        of hundreds of pages)."""
+        of hundreds of pages). ``ids``: the pages' id()s, when the caller keeps them."""
         if not pages:
             return
         with self.lock:
@@ -276,7 +276,8 @@ class StorageManager:
                 p.last_use = t
             if od is None:
                 return
-            ids = [id(p) for p in pages]
+            if ids is None:
+                ids = [id(p) for p in pages]
             if len(od) >= len(ids) and list(itertools.islice(reversed(od), len(ids))) == ids[::-1]:
                 return                           # the run already is the set's most recent tail, in order
             for k in ids:

@@ -429,12 +429,12 @@ class UserSet:
         fast = self.__dict__.get("_scan_fast")
         if fast is not None and fast[0] == ver and ver[0] is not None:
             touch_run = getattr(self.manager, "touch_run", None)
-            for run, merged in fast[1]:
+            for run, merged, ids in fast[1]:
                 for p in run:
                     p.pins += 1
                 try:
                     if touch_run is not None:
-                        touch_run(run)
+                        touch_run(run, ids)
                     yield merged
                 finally:
                     for p in run:
@@ -486,7 +486,7 @@ class UserSet:
                 finally:
                     p.pins -= 1
         if all_merged is not None and ver[0] is not None and getattr(self, "_layout_version", None) == ver[0]:
-            self._scan_fast = (ver, all_merged)
+            self._scan_fast = (ver, [(run, merged, [id(p) for p in run]) for run, merged in all_merged])
 
     def all(self, device=None) -> Optional[RecordBatch]:
         bs = list(self.scan(device))
