@@ -446,6 +446,33 @@ def _flat(b):
     return b
 
 
+def _lists(cols: Dict[str, object]) -> Dict[str, list]:
+    """Python lists of several result columns (tensors, string columns) with ONE device read: every column's
+    buffers go through one to_host (asynchronous copies, one stream synchronisation)."""
+    parts: List[torch.Tensor] = []
+    plan = []
+    for nm, c in cols.items():
+        if isinstance(c, StringColumn):
+            plan.append((nm, "s", len(parts)))
+            parts += [c.data[: c.payload], c.starts, c.ends]
+        elif isinstance(c, torch.Tensor):
+            plan.append((nm, "t", len(parts)))
+            parts.append(c)
+        else:
+            plan.append((nm, "l", c))
+    hs = to_host(*parts)
+    out: Dict[str, list] = {}
+    for nm, kind, i in plan:
+        if kind == "s":
+            raw = hs[i].numpy().tobytes()
+            out[nm] = [raw[a:b].decode() for a, b in zip(hs[i + 1].tolist(), hs[i + 2].tolist())]
+        elif kind == "t":
+            out[nm] = hs[i].tolist()
+        else:
+            out[nm] = list(i)
+    return out
+
+
 def _as_list(c):
     return c.tolist() if isinstance(c, torch.Tensor) else list(c)
 
@@ -468,10 +495,10 @@ def q01(client, db: str, delta_days: int = 90) -> List[dict]:
     out = []
     if r is None:
         return out
-    k1 = _as_list(r.columns["k1"]) if "k1" in r.columns else None
     names = ("count", "sum_qty", "sum_base_price", "sum_disc_price", "sum_charge", "sum_disc")
-    hv = dict(zip(names, (t.tolist() for t in to_host(*(r.columns[f] for f in names)))))   # one device read
-    for i, k in enumerate(_as_list(r.columns["k0"])):
+    hv = _lists({f: r.columns[f] for f in names + tuple(k for k in ("k0", "k1") if k in r.columns)})  # one read
+    k1 = hv.get("k1")
+    for i, k in enumerate(hv["k0"]):
         rf, ls = (k, k1[i]) if k1 is not None else k.split("|")
         c = float(hv["count"][i])
         row = {"l_returnflag": rf, "l_linestatus": ls}
@@ -565,8 +592,8 @@ def q04(client, db: str, date: int = 19930701, join_first: bool = Q04_JOIN_FIRST
         r = _flat(_run(client, db, "q04_out", cnt.set_input(dist.set_input(j)), "tpch_q04"))
         if r is None:
             return []
-        return sorted(({"o_orderpriority": p, "order_count": int(c)} for p, c in
-                       zip(_as_list(r.columns["k0"]), _as_list(r.columns["order_count"]))),
+        hv = _lists({c: r.columns[c] for c in ("k0", "order_count")})
+        return sorted(({"o_orderpriority": p, "order_count": int(c)} for p, c in zip(hv["k0"], hv["order_count"])),
                       key=lambda x: x["o_orderpriority"])
     # EXISTS -> distinct late orderkeys (aggregate), then join with the orders of the quarter
     dist = _GroupBy(lambda b: _col(b, "l_orderkey"), lambda b: torch.ones(b.n, 1, dtype=torch.float64, device=_dev(b)),
@@ -580,8 +607,9 @@ def q04(client, db: str, date: int = 19930701, join_first: bool = Q04_JOIN_FIRST
     r = _flat(_run(client, db, "q04_out", cnt.set_input(j), "tpch_q04"))
     if r is None:
         return []
-    return sorted(({"o_orderpriority": p, "order_count": int(c)} for p, c in
-                   zip(_as_list(r.columns["k0"]), _as_list(r.columns["order_count"]))), key=lambda x: x["o_orderpriority"])
+    hv = _lists({c: r.columns[c] for c in ("k0", "order_count")})
+    return sorted(({"o_orderpriority": p, "order_count": int(c)} for p, c in zip(hv["k0"], hv["order_count"])),
+                  key=lambda x: x["o_orderpriority"])
 
 
 def q06(client, db: str, date: int = 19940101, discount: float = 0.06, quantity: float = 24) -> float:
@@ -618,9 +646,9 @@ def q12(client, db: str, modes=("MAIL", "SHIP"), date: int = 19940101) -> List[d
     r = _flat(_run(client, db, "q12_out", agg.set_input(j), "tpch_q12"))
     if r is None:
         return []
+    hv = _lists({c: r.columns[c] for c in ("k0", "high_line_count", "low_line_count")})
     return sorted(({"l_shipmode": m, "high_line_count": int(h), "low_line_count": int(lo_)} for m, h, lo_ in
-                   zip(_as_list(r.columns["k0"]), _as_list(r.columns["high_line_count"]),
-                       _as_list(r.columns["low_line_count"]))), key=lambda x: x["l_shipmode"])
+                   zip(hv["k0"], hv["high_line_count"], hv["low_line_count"])), key=lambda x: x["l_shipmode"])
 
 
 def q13(client, db: str, w1: str = "special", w2: str = "requests") -> List[dict]:
@@ -634,7 +662,8 @@ def q13(client, db: str, w1: str = "special", w2: str = "requests") -> List[dict
                     lambda b: torch.ones(b.n, 1, dtype=torch.float64, device=_dev(b)), _rows_out(["custdist"]))
     r = _flat(_run(client, db, "q13_out", dist.set_input(per_c.set_input(os_)), "tpch_q13"))
     ncust = _count(client, db, "customer")
-    rows = {} if r is None else {int(k): int(v) for k, v in zip(_as_list(r.columns["k0"]), _as_list(r.columns["custdist"]))}
+    hv = {} if r is None else _lists({c: r.columns[c] for c in ("k0", "custdist")})
+    rows = {} if r is None else {int(k): int(v) for k, v in zip(hv["k0"], hv["custdist"])}
     with_orders = sum(rows.values())
     if ncust - with_orders > 0:
         rows[0] = rows.get(0, 0) + ncust - with_orders
@@ -735,9 +764,9 @@ def q22(client, db: str, codes=("13", "31", "23", "29", "30", "18", "17")) -> Li
     r = _flat(_run(client, db, "q22_out", agg.set_input(sel), "tpch_q22"))
     if r is None:
         return []
+    hv = _lists({c: r.columns[c] for c in ("k0", "numcust", "totacctbal")})
     return sorted(({"cntrycode": c, "numcust": int(n), "totacctbal": float(t)} for c, n, t in
-                   zip(_as_list(r.columns["k0"]), _as_list(r.columns["numcust"]), _as_list(r.columns["totacctbal"]))),
-                  key=lambda x: x["cntrycode"])
+                   zip(hv["k0"], hv["numcust"], hv["totacctbal"])), key=lambda x: x["cntrycode"])
 
 
 def q02(client, db: str, size: int = 15, type_suffix: str = "BRASS", region: str = "EUROPE", k: int = 100) -> List[dict]:
@@ -782,10 +811,9 @@ def q02(client, db: str, size: int = 15, type_suffix: str = "BRASS", region: str
         # that balance are decided by the string keys below), so only those cross to the host and get decoded
         a64 = acct.double()
         b = b.take(torch.nonzero(a64 >= torch.topk(a64, k).values[-1]).flatten())
+    hv = _lists({c: b.columns[c] for c in ("s_acctbal", "s_name", "n_name", "p_partkey", "p_mfgr")})
     rows = [{"s_acctbal": float(a), "s_name": s, "n_name": n, "p_partkey": int(p), "p_mfgr": m}
-            for a, s, n, p, m in zip(_as_list(b.columns["s_acctbal"]), _as_list(b.columns["s_name"]),
-                                     _as_list(b.columns["n_name"]), _as_list(b.columns["p_partkey"]),
-                                     _as_list(b.columns["p_mfgr"]))]
+            for a, s, n, p, m in zip(hv["s_acctbal"], hv["s_name"], hv["n_name"], hv["p_partkey"], hv["p_mfgr"])]
     rows.sort(key=lambda x: (-x["s_acctbal"], x["n_name"], x["s_name"], x["p_partkey"]))
     return rows[:k]
 
