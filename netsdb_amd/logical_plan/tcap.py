@@ -267,12 +267,18 @@ _PRIM = (bool, int, float, str, type(None))
 def _node_values(n) -> tuple:
     """The constants a lambda node carries (literal value, LIKE pattern, IN list): not part of the graph signature
     but of any plan decision made from the values (execution/pipeline.py's fused stage expressions)."""
+    nd = n.__dict__
+    if "pattern" not in nd and "values" not in nd and type(nd.get("value")) in _PRIM:
+        v = nd.get("value")
+        return (type(v), v)                      # a plain literal (the common case); 1, 1.0 and True differ here
     out = []
     for a in ("value", "pattern", "negate", "values"):
         v = getattr(n, a, None)
         if isinstance(v, list):
-            v = tuple(x if isinstance(x, _PRIM) else ("?", type(x).__name__) for x in v)
-        elif not isinstance(v, _PRIM):
+            v = tuple((type(x), x) if isinstance(x, _PRIM) else ("?", type(x).__name__) for x in v)
+        elif isinstance(v, _PRIM):
+            v = (type(v), v)
+        else:
             v = ("?", type(v).__name__)          # not a fusable constant: its type decides the plan
         out.append(v)
     return tuple(out)
