@@ -330,9 +330,14 @@ class RecordBatch:
 
     @property
     def device(self) -> torch.device:
+        cols = self.columns
+        if type(cols) is dict:
+            for c in cols.values():              # fast path: the first column is a tensor (asked per batch and atom)
+                if isinstance(c, torch.Tensor):
+                    return c.device
+                break
         from .nested import NestedColumn
 
-        cols = self.columns
         if isinstance(cols, LazyTakeColumns):
             cols = cols._src                 # a row selection lives where its source does: nothing gathered to answer
         for c in cols.values():
