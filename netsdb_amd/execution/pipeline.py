@@ -28,6 +28,7 @@ from __future__ import annotations
 import hashlib
 import os
 import struct
+import threading
 import warnings
 
 import numpy as np
@@ -1128,9 +1129,11 @@ def _read_table(table: torch.Tensor):
     asynchronous copy + one stream sync instead of a pageable copy."""
     if not table.is_cuda:
         return table.numpy()
-    key = (table.device, table.numel())
+    key = (table.device, table.numel(), threading.get_ident())     # per thread: concurrent jobs never share one
     buf = _TABLE_HOST.get(key)
     if buf is None:
+        if len(_TABLE_HOST) >= 64:
+            _TABLE_HOST.clear()
         buf = _TABLE_HOST[key] = torch.empty(table.numel(), dtype=table.dtype, pin_memory=True)
     buf.copy_(table, non_blocking=True)
     torch.cuda.current_stream(table.device).synchronize()
