@@ -331,6 +331,8 @@ class RecordBatch:
     @property
     def device(self) -> torch.device:
         cols = self.columns
+        if isinstance(cols, LazyTakeColumns):
+            cols = cols._src                 # a row selection lives where its source does: nothing gathered to answer
         if type(cols) is dict:
             for c in cols.values():              # fast path: the first column is a tensor (asked per batch and atom)
                 if isinstance(c, torch.Tensor):
@@ -338,8 +340,6 @@ class RecordBatch:
                 break
         from .nested import NestedColumn
 
-        if isinstance(cols, LazyTakeColumns):
-            cols = cols._src                 # a row selection lives where its source does: nothing gathered to answer
         for c in cols.values():
             if isinstance(c, (torch.Tensor, StringColumn, NestedColumn)):
                 return c.device
