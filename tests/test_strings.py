@@ -234,3 +234,26 @@ def test_like_contains_random_small_alphabet_gpu():
             "%aa%aa%aa%", "%c_a_b%", "%bb%"]
     for p in pats:
         assert col.like(p).cpu().tolist() == [_like_ref(s, p) for s in strs], p
+
+
+def test_short_code_decode_host_paths_agree():
+    """from_short_codes: the numpy decode of a few host codes (fused aggregation keys) == the torch decode."""
+    import random
+
+    rng = random.Random(3)
+    for L in (1, 2, 3, 7):
+        words = ["".join(rng.choice("AB xyz|") for _ in range(rng.randint(0, L))) for _ in range(200)]
+        codes = StringColumn.from_list(words).short_codes(L)
+        small = StringColumn.from_short_codes(codes, L)                       # numpy path (n <= 65536)
+        big = StringColumn.from_short_codes(codes.repeat(400), L)             # torch path (80 000 rows)
+        assert list(small) == words
+        assert list(big)[:200] == words and len(big) == 80_000
+
+
+def test_tpch_result_lists_one_read():
+    """models/tpch.py _lists: tensors, string columns and plain lists of a result batch as Python lists."""
+    from netsdb_amd.models.tpch import _lists
+
+    sc = StringColumn.from_list(["R", "AF", "", "NO"])
+    got = _lists({"k": sc, "v": torch.tensor([1.5, 2.0, 0.0, -1.0]), "n": torch.tensor([1, 2, 3, 4]), "l": [9, 8, 7, 6]})
+    assert got == {"k": ["R", "AF", "", "NO"], "v": [1.5, 2.0, 0.0, -1.0], "n": [1, 2, 3, 4], "l": [9, 8, 7, 6]}
