@@ -78,12 +78,34 @@ def _free_port() -> int:
     return port
 
 
+def visible_gpus() -> int:
+    """GPUs this process would see, counted WITHOUT any torch.cuda / HIP call (the launching parent stays provably
+    GPU-free): HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES when set, else the KFD topology
+    nodes with a non-zero gpu_id. -1 when it cannot be told (then rank 0's own device check decides)."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([x for x in v.split(",") if x.strip() not in ("", "-1")])
+    topo = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        n = 0
+        for node in os.listdir(topo):
+            try:
+                with open(os.path.join(topo, node, "gpu_id")) as f:
+                    n += int(f.read().strip() or 0) != 0
+            except (OSError, ValueError):
+                continue
+        return n
+    except OSError:
+        return -1
+
+
 def launch_ranks(n: int, argv) -> int:
-    """Spawn ``n`` ranks of this script (one per GPU) and wait for them. Called before any GPU call in this
-    process: counting devices does not initialise the GPU; the children are separate processes (no exec)."""
+    """Spawn ``n`` ranks of this script (one per GPU) and wait for them. This process makes no GPU call at all
+    (visible_gpus reads the environment / KFD topology, not HIP); the children are separate processes (no exec)."""
     import subprocess
 
-    ndev = torch.cuda.device_count()
+    ndev = visible_gpus()
     if 0 < ndev < n:
         print(f"[bench] --gpus {n} but only {ndev} GPUs visible", file=sys.stderr)
         return 2
@@ -125,6 +147,8 @@ def main():
                          "normalise); default: ONE job, whose output layer is one GEMM with the max-subtracted softmax "
                          "in its epilogue (55-59 us vs 66-70 + 18 us in-bench, profiles/r3_s3/softmax)")
     ap.add_argument("--single-job", action="store_true", help=argparse.SUPPRESS)   # the default; kept for old scripts
+    ap.add_argument("--mfma", type=int, choices=[0, 16, 32], default=0,
+                    help="8-phase GEMM main-loop MFMA shape for this run (0 = the library default; A/B arm)")
     args = ap.parse_args()
     args.single_job = not args.two_job
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -135,6 +159,10 @@ def main():
     from netsdb_amd.models import ff
     from netsdb_amd.parallel.comm import ClusterContext
 
+    from netsdb_amd import ops
+
+    if args.mfma:
+        ops.set_kernel_options(gemm_mfma=args.mfma)
     cfg = SMALL if args.small else FULL
     ctx = ClusterContext.from_env()
     if ctx.world_size != args.gpus and ctx.rank == 0:
@@ -239,6 +267,7 @@ def main():
                 "conv_overlap": args.overlap,
                 "collectives_per_step": round(coll_per_step, 2),
                 "single_job": bool(args.single_job),
+                "gemm_mfma": args.mfma or "default",
             },
         }
         print(json.dumps(res), flush=True)

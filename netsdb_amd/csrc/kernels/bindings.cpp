@@ -85,6 +85,7 @@ struct GemmOpts {
   const void* pf_ptr;
   long long pf_bytes;
   int kinter;
+  int mfma;
 };
 
 void check_rc(int rc, const char* what) {
@@ -107,7 +108,7 @@ bool is_f32(const torch::Tensor& t, const char* name) {
 torch::Tensor gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Tensor> bias, int64_t bias_mode,
                       int64_t act, bool out_f32, double alpha, double dropout, int64_t seed, int64_t splits,
                       c10::optional<torch::Tensor> out, bool accumulate, int64_t cfg, int64_t epi,
-                      c10::optional<torch::Tensor> prefetch) {
+                      c10::optional<torch::Tensor> prefetch, int64_t mfma) {
   check_cuda(A, "A");
   check_cuda(B, "B");
   TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && B.scalar_type() == torch::kBFloat16, "A,B must be bf16");
@@ -163,7 +164,8 @@ torch::Tensor gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Ten
     wsp = ws.data_ptr<float>();
   }
   TORCH_CHECK(epi >= -1 && epi <= 1, "gemm_nt: epi must be -1 (auto), 0 (LDS-staged) or 1 (direct)");
-  GemmOpts o{(int)cfg, (int)epi, nullptr, 0, kinter};
+  TORCH_CHECK(mfma == 0 || mfma == 16 || mfma == 32, "gemm_nt: mfma must be 0 (auto), 16 or 32");
+  GemmOpts o{(int)cfg, (int)epi, nullptr, 0, kinter, (int)mfma};
   if (prefetch.has_value() && prefetch->defined() && prefetch->numel() > 0) {
     // the byte span of the tensor's elements (a strided view reads its whole span)
     check_cuda(*prefetch, "prefetch");
@@ -718,7 +720,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nt", &gemm_nt, "epi(alpha*A@B^T) on MFMA", py::arg("A"), py::arg("B"), py::arg("bias") = py::none(),
         py::arg("bias_mode") = 0, py::arg("act") = 0, py::arg("out_f32") = false, py::arg("alpha") = 1.0,
         py::arg("dropout") = 0.0, py::arg("seed") = 0, py::arg("splits") = 0, py::arg("out") = py::none(),
-        py::arg("accumulate") = false, py::arg("cfg") = -1, py::arg("epi") = -1, py::arg("prefetch") = py::none());
+        py::arg("accumulate") = false, py::arg("cfg") = -1, py::arg("epi") = -1, py::arg("prefetch") = py::none(),
+        py::arg("mfma") = 0);
   m.def("gemm_launch_wgs", [](int64_t M, int64_t N, int64_t K, int64_t batch, int64_t splits, int64_t cfg) {
           return (int64_t)nsdb_gemm_launch_wgs((int)M, (int)N, (int)K, (int)batch, (int)splits, (int)cfg);
         }, "workgroups of the GEMM launch for this shape (splits <= 0: the launcher's choice)",

@@ -910,6 +910,251 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   if (p.pf_ptr != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // prefetch DMAs retired
 }
 
+// ---------------------------------------------------------------------------------------------
+// The same 8-phase loop on v_mfma_f32_32x32x16_bf16 (GemmOpts::mfma = 32; common epilogue only).
+// Each MFMA does 2x the MACs of a 16x16x32 for the same 8 operand VGPRs, so the register-file operand reads per
+// MAC halve: the lever the power-limited layer-1 GEMM was measured to want (profiles/r2_gemm1_study/
+// mfma_power_waves.txt: 32x32x16 1,825-1,831 TF vs 16x16x32 1,672-1,753 TF at 2 waves/SIMD on random operands).
+// Unchanged: the half-tile LDS map and its DMA schedule, the ping-pong wave groups, the barrier/vmcnt/lgkmcnt
+// protocol (4 B reads, then 8 A reads, per phase — the same counts as the 16x16 loop). Changed:
+//  * fragments: lane l reads row l & 31 of a 32-row block, 16-B chunk 2s + (l >> 5) for k-step s (k 16s..16s+15)
+//    — the 32x32x16 operand map (A[row r][k = 8h + j]) with the same k permutation on both operands; the XOR
+//    swizzle of read_frag keeps these reads conflict-free (per 16-lane group: 16 distinct (row & 1, chunk ^ ...)
+//    slots);
+//  * per phase 2 (m) x 1 (n) 32x32 tiles x 4 k-steps = 8 MFMAs (the same 256 MFMA cycles as 16 of 16x16x32);
+//  * accumulators acc[mb][nb] (f32x16): the transposed product (B fragment as the A operand), so lane l holds
+//    C[m = wr*128 + mb*32 + (l & 31)][n = wc*64 + nb*32 + 8g + 4(l >> 5) + r] in register 4g + r: four runs of 4
+//    consecutive columns per lane, stored as 16-B (f32) / 8-B (bf16) pieces straight from the registers.
+// ---------------------------------------------------------------------------------------------
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+__device__ __forceinline__ void store_direct_8ph32(const f32x16 (&acc)[4][2], const GemmParams& p, int batch, int split,
+                                                   int m0, int n0, int lane, int wave) {
+  const int wr = wave >> 2, wc = wave & 3;
+  const int rl = lane & 31, ch = (lane >> 5) * 4;
+  if (p.splits > 1) {
+    float* ws = p.ws + ((long long)batch * p.splits + split) * (long long)p.M * p.N;
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) {
+      const int row = m0 + wr * 128 + mb * 32 + rl;
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int col = n0 + wc * 64 + nb * 32 + g * 8 + ch;
+          if (row < p.M && col < p.N) {
+            float* d = ws + (long long)row * p.N + col;
+            const f32x4 v = {acc[mb][nb][4 * g], acc[mb][nb][4 * g + 1], acc[mb][nb][4 * g + 2], acc[mb][nb][4 * g + 3]};
+            if (col + 4 <= p.N) *reinterpret_cast<f32x4*>(d) = v;          // N % 4 == 0 (host: vec_ws)
+            else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (col + r < p.N) d[r] = v[r];
+            }
+          }
+        }
+    }
+    return;
+  }
+  const float* bias = p.bias ? p.bias + batch * p.sBias : nullptr;
+  const float keep_scale = p.dropout > 0.f ? 1.f / (1.f - p.dropout) : 1.f;
+  float br[4];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) {
+    const int row = m0 + wr * 128 + mb * 32 + rl;
+    br[mb] = (bias && p.bias_mode == 1 && row < p.M) ? bias[row] : 0.f;
+  }
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int col = n0 + wc * 64 + nb * 32 + g * 8 + ch;
+      f32x4 bc = {0.f, 0.f, 0.f, 0.f};
+      if (bias && p.bias_mode == 2 && col < p.N) {
+        const float* bp = bias + col;
+        if (col + 3 < p.N && ((reinterpret_cast<uintptr_t>(bp) & 15) == 0)) bc = *reinterpret_cast<const f32x4*>(bp);
+        else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) bc[r] = bp[min(r, p.N - 1 - col)];
+        }
+      }
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) {
+        const int row = m0 + wr * 128 + mb * 32 + rl;
+        f32x4 w;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float x = apply_act_compact(acc[mb][nb][4 * g + r] * p.alpha + br[mb] + bc[r], p.act);
+          if (p.dropout > 0.f) {
+            const unsigned long long idx = ((unsigned long long)batch * p.M + row) * p.N + col + r;
+            x = hash_uniform(p.seed, idx) < p.dropout ? 0.f : x * keep_scale;
+          }
+          w[r] = x;
+        }
+        if (row < p.M && col < p.N) {
+          const long long off = batch * p.sC + (long long)row * p.ldc + col;
+          const int nv = min(4, p.N - col);
+          if (p.out_f32) {
+            float* d = reinterpret_cast<float*>(p.C) + off;
+            if (nv == 4) *reinterpret_cast<f32x4*>(d) = w;
+            else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (r < nv) d[r] = w[r];
+            }
+          } else {
+            unsigned short* d = reinterpret_cast<unsigned short*>(p.C) + off;
+            if (nv == 4) *reinterpret_cast<uint2*>(d) = make_uint2(pack_bf16x2(w[0], w[1]), pack_bf16x2(w[2], w[3]));
+            else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (r < nv) d[r] = f32_to_bf16(w[r]);
+            }
+          }
+        }
+      }
+    }
+}
+
+__global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph32_kernel(GemmParams p) {
+  constexpr int HALF = 128 * 128;
+  constexpr int BUF = 4 * HALF;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF + 1024 + 8 * 1024];
+
+  const int ntiles = p.tiles_m * p.tiles_n;
+  const int wg = xcd_remap(blockIdx.x, ntiles * p.splits);
+  const int split = wg / ntiles, tile = wg % ntiles;
+  int tm, tn;
+  grouped_tile(tile, p.tiles_m, p.tiles_n, tm, tn);
+  const int batch = blockIdx.z;
+  const int m0 = tm * 256, n0 = tn * 256;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+
+  const int rows_a = min(256, p.M - m0), rows_b = min(256, p.N - n0);
+  const int kbeg = split * p.kchunk;
+  const int kend = min(p.K, kbeg + p.kchunk);
+  const int nk = max(0, (kend - kbeg + BK - 1) / BK);
+  const int niter = (nk + 1) >> 1;
+
+  const unsigned short* Ab = p.A + batch * p.sA + (long long)m0 * p.lda;
+  const long long kseg = p.seg_k ? kbeg / p.seg_k : 0;
+  const int kb0 = (int)(kseg * p.seg_k);
+  const unsigned short* Bb = p.B + batch * p.sB + (long long)n0 * p.ldb + kseg * p.seg_stride_b;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(Ab, (unsigned)((long long)rows_a * p.lda * 2));
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(Bb, (unsigned)((long long)rows_b * p.ldb * 2));
+
+  // DMA source rows: identical half-tile map to gemm_nt_256_8ph_kernel
+  const int lr = wave * 8 + (lane >> 3);
+  const int kc = ((lane & 7) ^ ((lr >> 1) & 7)) * 8;
+  int roff[4][2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int ta = i * 128 + q * 64 + lr;
+      const int tb = (2 * i + (lr >> 5)) * 64 + q * 32 + (lr & 31);
+      roff[q][i] = ta < rows_a ? (int)((long long)ta * p.lda * 2) : -1;
+      roff[2 + q][i] = tb < rows_b ? (int)((long long)tb * p.ldb * 2) : -1;
+    }
+  auto stage = [&](int buf, int slot, int u) {
+    const int k = kbeg + u * BK + kc;
+    const bool kin = k < kend;
+    char* dst = smem + buf * BUF + slot * HALF;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int ro = roff[slot][i];
+      const int voff = (kin && ro >= 0) ? ro + (slot < 2 ? k : k - kb0) * 2 : OOB;
+      if (slot < 2)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)(dst + (i * 64 + wave * 8) * 128), 16, voff, 0, 0, 0);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(dst + (i * 64 + wave * 8) * 128), 16, voff, 0, 0, 0);
+    }
+  };
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  bf16x8 af[2][4], b0[4], b1[4];
+  const int frow = lane & 31, fch = lane >> 5;
+
+  auto readA = [&](int buf, int q) {
+    const char* base = smem + buf * BUF + q * HALF;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) af[mi][s] = read_frag(base, wr * 64 + mi * 32 + frow, 2 * s + fch);
+  };
+  auto readB = [&](int buf, int q, bf16x8 (&bq)[4]) {
+    const char* base = smem + buf * BUF + (2 + q) * HALF;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) bq[s] = read_frag(base, wc * 32 + frow, 2 * s + fch);
+  };
+  auto mma = [&](int qm, int qn, const bf16x8 (&bq)[4]) {
+    NSDB_BARRIER();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+        acc[qm * 2 + mi][qn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bq[s], af[mi][s], acc[qm * 2 + mi][qn], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    NSDB_BARRIER();
+  };
+  auto ktile = [&](int cur, int u) {
+    readB(cur, 0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    readA(cur, 0);
+    stage(cur ^ 1, 1, u + 1);
+    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");   // the 4 B0 reads (issued first) are done
+    mma(0, 0, b0);
+    readB(cur, 1, b1);
+    stage(cur, 2, u + 2);
+    mma(0, 1, b1);
+    readA(cur, 1);
+    stage(cur, 0, u + 2);
+    mma(1, 1, b1);
+    stage(cur, 3, u + 2);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    mma(1, 0, b0);
+  };
+
+  stage(0, 2, 0); stage(0, 0, 0); stage(0, 3, 0); stage(0, 1, 0);
+  stage(1, 2, 1); stage(1, 0, 1); stage(1, 3, 1);
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  NSDB_BARRIER();
+  if (wr == 1) NSDB_BARRIER();
+  for (int it = 0; it < niter; ++it) {
+    ktile(0, 2 * it);
+    ktile(1, 2 * it + 1);
+  }
+  if (wr == 0) NSDB_BARRIER();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (p.pf_ptr != nullptr) {           // operand prefetch of the next kernel (see gemm_nt_256_8ph_kernel)
+    const long long nwg = (long long)gridDim.x * gridDim.z;
+    const long long wid = (long long)blockIdx.z * gridDim.x + blockIdx.x;
+    const long long chunk = ((p.pf_bytes + nwg - 1) / nwg + 1023) & ~1023LL;
+    const long long beg = wid * chunk;
+    if (beg < p.pf_bytes) {
+      const int len = (int)min(chunk, p.pf_bytes - beg);
+      const __amdgpu_buffer_rsrc_t rf = make_rsrc(p.pf_ptr + beg, (unsigned)len);
+      char* sink = smem + 2 * BUF + 1024 + wave * 1024;
+      for (int off = wave * 1024; off < len; off += 8 * 1024)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rf, (lds_void*)sink, 16, off + lane * 16, 0, 0, 0);
+    }
+  }
+  store_direct_8ph32(acc, p, batch, split, m0, n0, lane, wave);
+  if (p.pf_ptr != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 
 // Split-K slab reducer + fused epilogue (the ClusterAggregate "combine" of the partial block products).
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(GemmParams p) {
@@ -1002,6 +1247,7 @@ struct GemmOpts {
   const void* pf_ptr;       // operand prefetch of this launch (8-phase only): pf_bytes at pf_ptr, or nullptr
   long long pf_bytes;
   int kinter;               // stream tiles: 1 = k-interleaved splits (split s takes k-tiles s, s + S, ...)
+  int mfma;                 // 8-phase main loop: 0 auto, 16 = 16x16x32, 32 = 32x32x16 (direct epilogue launches)
 };
 
 extern "C" {
@@ -1170,7 +1416,13 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
       p.pf_ptr = (const char*)opts->pf_ptr;
       p.pf_bytes = opts->pf_bytes;
     }
-    hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<0>, grid, dim3(512), 0, stream, p);
+    // the 32x32x16 main loop stores from registers only (store_direct_8ph32): launches that need the LDS-staged
+    // epilogue (C += A.B^T, a per-element bias, unaligned C) stay on the 16x16x32 loop
+    const int mf = opts ? opts->mfma : 0;
+    if (mf == 32 && p.direct_epi)
+      hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph32_kernel, grid, dim3(512), 0, stream, p);
+    else
+      hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<0>, grid, dim3(512), 0, stream, p);
   } else if (cfg == 3 || cfg == 4) {
     // contiguous K chunks per split; k-interleaved splits on request (GemmOpts::kinter, unsegmented B only: a split
     // must stay inside one segment). A/B in profiles/r5_stream: interleaving wins 3 % at M = 1000, N <= 128 and

@@ -762,7 +762,13 @@ def _compile_cached(plan: StagePlan, batch: RecordBatch) -> Program:
         p = Program.__new__(Program)
         p.__dict__.update(hit.__dict__)
         p.cols = [dict(c, obj=_resolve(c["expr"], batch)) for c in hit.cols]
-        return p
+        # A string key column's short-code bound L is fixed at compile time. The key above holds the column's
+        # length bound only when it was already known (no device read per batch), so a batch with an unknown bound
+        # can meet a program compiled for shorter strings: re-check the bound of every such column (one cached
+        # reduction per column) and compile afresh when a row is longer than L.
+        if all(c["kind"] != C_SCODE or c["obj"].max_len() <= c["L"] for c in p.cols):
+            return p
+        return _Compiler(plan, batch).compile()
     p = _Compiler(plan, batch).compile()
     _prog_tensors(p, batch.device)              # built once here: every cached copy shares them
     if len(_PROG_CACHE) >= _PROG_CACHE_MAX:
@@ -787,7 +793,12 @@ def run_batch(plan: StagePlan, batch: RecordBatch) -> Optional[RecordBatch]:
         plan.reason = str(e)
         return None
     if on_gpu:
-        parts = _launch(prog, batch.n, dev, plan)
+        try:
+            parts = _launch(prog, batch.n, dev, plan)
+        except Unfusable as e:
+            plan.disabled = True
+            plan.reason = str(e)
+            return None
     else:
         parts = interpret(prog, batch.n, plan.op)
     if parts is None:
@@ -826,6 +837,9 @@ def _col_args(prog: Program, dev):
             if codes is not None:
                 out.append((C_I64, c["late"], 0, codes.contiguous(), None, None, None))
                 continue
+            # a row longer than the program's bound L: the device short_code would map it to the same sentinel as
+            # every other long row and merge distinct groups — never launch that (the caller runs the eager atoms)
+            raise Unfusable(f"string key longer than the compiled bound {c['L']}")
         if isinstance(o, StringColumn):
             out.append((c["kind"], c["late"], c["L"], None, o.starts.contiguous(), o.ends.contiguous(), o.data))
         else:
@@ -1345,7 +1359,12 @@ def run_filter(plan: FilterPlan, batch: RecordBatch) -> Optional[RecordBatch]:
         return None
     if on_gpu:
         ins, lit = _prog_tensors(prog, dev)
-        cargs = _col_args(prog, dev)
+        try:
+            cargs = _col_args(prog, dev)
+        except Unfusable as e:
+            plan.disabled = True
+            plan.reason = str(e)
+            return None
         jit = _jit_for(prog, cargs, "mask")
         fn, jnreg, jrows = jit if jit else (0, 0, 0)
         mask = _ext.hip().pipe_mask(ins, cargs, lit, batch.n, prog.keep_reg, TILE, prog.kpool, fn, jnreg,

@@ -173,7 +173,10 @@ class StorageManager:
         if isinstance(s, DenseMatrixSet):
             s.release_storage()
             self.untrack(s)
-        s.__dict__.pop("_merged_runs", None)
+        if hasattr(s, "drop_scan_views"):
+            s.drop_scan_views()
+        else:
+            s.__dict__.pop("_merged_runs", None)
         for p in s.pages:
             self.untrack(p)
             if p.location == "device" and p.batch is not None:

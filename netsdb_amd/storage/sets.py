@@ -45,6 +45,9 @@ class Page:
         st = getattr(self, "set", None)
         if st is not None:
             st._layout_version = self.gen
+            # the scan fast path's merged views are stale now, and they would keep this page's old buffers (and the
+            # short-code encodings derived from them) alive after a spill credited their bytes back
+            st.__dict__.pop("_scan_fast", None)
 
     def __init__(self, uset: "UserSet", page_no: int, batch: RecordBatch, to_pool: bool = False):
         self.set = uset
@@ -88,7 +91,7 @@ class Page:
         native page pool (LRU -> disk) and drop the in-memory batch."""
         if self.batch is None or self.pins > 0:
             return 0
-        self.set.__dict__.pop("_merged_runs", None)      # kept scan views would hold this page's buffers alive
+        self.set.drop_scan_views()                       # kept scan views would hold this page's buffers alive
         if self.location == "device" and not self.dirty:
             # clean: the page's serialised image is already in the pool / page file (write cost 0) -> just drop it
             self.release_regions()
@@ -341,8 +344,15 @@ class UserSet:
                 self.stats["bytes"] += p.nbytes
                 self.manager.account(p)
 
+    def drop_scan_views(self):
+        """Forget the merged scan views (and the fast-path list holding them, with the string short-code encodings
+        cached on their columns): after a spill, drop or clear their HBM must actually be released."""
+        self.__dict__.pop("_merged_runs", None)
+        self.__dict__.pop("_scan_fast", None)
+
     def clear(self):
         with self.lock:
+            self.drop_scan_views()
             for p in self.pages:
                 self.manager.untrack(p)
             self.pages = []

@@ -6,6 +6,8 @@
 #   tests        pytest -m gpu (K=<-k filter> to narrow), per-test timeout, one process
 #   smoke        __graft_entry__.smoke()
 #   bench        bench.py --steps 20 --warmup 5 (the driver's arguments; BENCH_ARGS overrides)
+#   abbench      interleaved bench.py runs of AB_VARIANTS (';'-separated bench argument sets, default the two
+#                GEMM MFMA shapes) for AB_ROUNDS rounds (default 5), driver arguments; one JSON line per run
 #   prof         rocprofv3 --kernel-trace --stats of bench.py --steps 10 --warmup 10 + per-step timeline
 #   pmc          rocprofv3 --pmc pass(es) of bench.py, PMC="counter list" (one pass per ';'-separated list)
 #   tpch         scripts/bench_tpch.py at SF 1,10, all ten queries, pandas-checked, stage times (TPCH_ARGS)
@@ -40,9 +42,17 @@ run_task() {
       timeout -k 10 300 python -u bench.py ${BENCH_ARGS:---steps 20 --warmup 5} > "$O/bench.log" 2>&1 \
         || fail bench $? "$O/bench.log"
       grep "^{" "$O/bench.log" | tee "$O/bench.json" ;;
+    abbench)
+      IFS=';' read -ra vars <<< "${AB_VARIANTS:---mfma 16;--mfma 32}"
+      for r in $(seq 1 "${AB_ROUNDS:-5}"); do
+        for v in "${vars[@]}"; do
+          timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 $v > "$O/ab.log" 2>&1 || fail "abbench ($v)" $? "$O/ab.log"
+          echo "{\"round\": $r, \"args\": \"$v\", \"result\": $(grep '^{' "$O/ab.log")}" | tee -a "$O/abbench.jsonl"
+        done
+      done ;;
     prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/$O/prof" -o run --output-format csv -- \
-        python3 "$R/bench.py" --steps 10 --warmup 10 > "$O/prof.log" 2>&1 || fail prof $? "$O/prof.log"
+        python3 "$R/bench.py" --steps 10 --warmup 10 ${PROF_ARGS:-} > "$O/prof.log" 2>&1 || fail prof $? "$O/prof.log"
       f=$(ls "$O"/prof/*/run_kernel_stats.csv "$O"/prof/run_kernel_stats.csv 2>/dev/null | head -1)
       [ -n "$f" ] && cp "$f" "$O/bench_kernel_stats.csv" && head -8 "$O/bench_kernel_stats.csv"
       t=$(ls "$O"/prof/*/run_kernel_trace.csv "$O"/prof/run_kernel_trace.csv 2>/dev/null | head -1)

@@ -87,6 +87,64 @@ def test_gemm_8ph_direct_epilogue_matches_lds_staged(M, N, K, mode, act, dropout
     assert (wide[:, N:] == -7.0).all()
 
 
+def test_gemm_8ph_mfma32_identity_asymmetric():
+    """The 32x32x16 main loop (mfma=32): A = I with an asymmetric B catches a transposed C-write or a wrong k
+    permutation between the two operands' fragments."""
+    n = 512
+    A = torch.eye(n, device=DEV, dtype=torch.bfloat16)
+    B = (torch.arange(n * n, device=DEV, dtype=torch.float32).reshape(n, n) % 97 - 48).to(torch.bfloat16)
+    C = ops.gemm_nt(A, B, out_dtype=torch.float32, cfg=2, splits=1, mfma=32)
+    torch.testing.assert_close(C, B.float().t().contiguous(), rtol=0, atol=0)
+    Ct = ops.gemm_nt(B, A, out_dtype=torch.float32, cfg=2, splits=1, mfma=32)
+    torch.testing.assert_close(Ct, B.float(), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 1000, 6400), (300, 200, 640), (1000, 1030, 1000), (257, 514, 72),
+                                   (256, 256, 64), (513, 260, 8200)])
+@pytest.mark.parametrize("splits", [1, 3, 16])
+def test_gemm_8ph_mfma32_exact_vs_mfma16(M, N, K, splits):
+    """Small-integer operands make every partial sum exact in f32, so the 32x32x16 and 16x16x32 main loops must
+    agree bit for bit (split-K slabs + reducer, ragged M / N / K edges), and both equal the f32 reference."""
+    torch.manual_seed(21)
+    A = torch.randint(-3, 4, (M, K), device=DEV).to(torch.bfloat16)
+    B = torch.randint(-3, 4, (N, K), device=DEV).to(torch.bfloat16)
+    c32 = ops.gemm_nt(A, B, out_dtype=torch.float32, cfg=2, splits=splits, mfma=32)
+    c16 = ops.gemm_nt(A, B, out_dtype=torch.float32, cfg=2, splits=splits, mfma=16)
+    torch.testing.assert_close(c32, c16, rtol=0, atol=0)
+    torch.testing.assert_close(c32, _ref_gemm(A, B), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("mode,act,dropout", [(0, ops.ACT_NONE, 0.0), (1, ops.ACT_RELU, 0.0), (2, ops.ACT_EXP, 0.0),
+                                              (2, ops.ACT_SIGMOID, 0.3), (1, ops.ACT_RELU, 0.5)])
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("splits", [1, 4])
+def test_gemm_8ph_mfma32_epilogue(mode, act, dropout, out_dtype, splits):
+    """The 32x32x16 loop's register epilogue (bias per row / column, activations, dropout hash, bf16 packing) and
+    its split-K slabs against the fp32 reference, with the dropout mask equal to the 16x16x32 loop's."""
+    torch.manual_seed(8)
+    M, N, K = 1000, 1030, 1024
+    A = (torch.randn(M, K, device=DEV) * 0.05).to(torch.bfloat16)
+    B = (torch.randn(N, K, device=DEV) * 0.05).to(torch.bfloat16)
+    bias = torch.randn(M if mode == 1 else N, device=DEV) if mode else None
+    kw = dict(bias=bias, bias_mode=mode, act=act, out_dtype=out_dtype, dropout=dropout, seed=5, splits=splits, cfg=2)
+    c32 = ops.gemm_nt(A, B, mfma=32, **kw)
+    c16 = ops.gemm_nt(A, B, mfma=16, **kw)
+    assert torch.equal(c32 == 0, c16 == 0) or act == ops.ACT_RELU
+    if dropout == 0.0:
+        _close(c32, _ref_gemm(A, B, bias, mode, act), tol=2e-2)
+    _close(c32, c16.float(), tol=2e-2)
+
+
+def test_gemm_8ph_mfma32_ff_layer1_shape():
+    """The headline layer-1 shape class (M = N = 1000, K long, split-K 16) on the 32x32x16 loop vs fp32."""
+    torch.manual_seed(9)
+    M, N, K = 1000, 1000, 65536
+    A = (torch.rand(M, K, device=DEV) - 0.5).to(torch.bfloat16)
+    B = (torch.rand(N, K, device=DEV) - 0.5).to(torch.bfloat16)
+    C = ops.gemm_nt(A, B, out_dtype=torch.float32, cfg=2, mfma=32)
+    _close(C, _ref_gemm(A, B), tol=1e-2)
+
+
 def test_gemm_batched_strided(gemm_cfg):
     torch.manual_seed(2)
     A = torch.randn(3, 130, 200, device=DEV).to(torch.bfloat16)[:, :, :192]   # row stride 200 > K

@@ -182,6 +182,39 @@ def test_fused_stage_cache_keys_constants(monkeypatch):
     assert len(PL._STAGE_CACHE) == len(variants)
 
 
+def test_fused_program_cache_rechecks_string_key_bound(monkeypatch):
+    """A compiled program fixes a string key's short-code bound L. A later batch of the same stage whose string
+    lengths are not known yet (same program-cache key) but exceed L must not reuse that program: it recompiles
+    (or runs eagerly), and the groups stay distinct — fused == eager after the set's strings got longer."""
+    from netsdb_amd.objects.strings import StringColumn
+
+    monkeypatch.setenv("NSDB_DEVICE_STRINGS", "1")
+    t = tpch_gen.generate_fast(0.002, seed=9)
+    c = _client("cpu", t)
+    args = (lambda x: x.l_quantity > 1, lambda x: x.l_returnflag, lambda x: Values(x.l_extendedprice), "sum")
+    monkeypatch.setattr(PL, "CPU_INTERPRETER", True)
+    PL._PROG_CACHE.clear()
+    first = _agg_job(c, *args)
+    assert {k[0] for k in first[0]} <= {"A", "N", "R"}
+    # the same set, rewritten with longer flags ("A" -> "AX1", "N" -> "N", "R" -> "RYY2"): distinct 1-byte prefixes
+    # would merge if the 1-byte program were reused
+    b = [x for x in c.get_set_batches("tpch", "lineitem") if x.n]
+    rows = {k: v for k, v in b[0].columns.items()}
+    flags = rows["l_returnflag"].tolist() if isinstance(rows["l_returnflag"], StringColumn) else list(rows["l_returnflag"])
+    longer = {"A": "AX1", "N": "N", "R": "RYY2"}
+    new_flags = [longer[f] for f in flags]
+    newcol = StringColumn.from_list(new_flags)
+    newcol._maxlen = None                              # bound unknown: the cache key cannot tell it apart
+    rows["l_returnflag"] = newcol
+    c.clear_set("tpch", "lineitem")
+    c.send_data("tpch", "lineitem", type(b[0])(rows, b[0].n))
+    fused = _agg_job(c, *args)
+    monkeypatch.setattr(PL, "CPU_INTERPRETER", False)
+    eager = _agg_job(c, *args)
+    assert {k[0] for k in fused[0]} == {"AX1", "N", "RYY2"}
+    assert eager[0] == fused[0] and torch.allclose(eager[1], fused[1], rtol=1e-12, atol=1e-9)
+
+
 def test_fused_overflow_falls_back(monkeypatch):
     """More groups than the kernel's per-workgroup tables: the batch takes the eager atoms, same result."""
     monkeypatch.setenv("NSDB_DEVICE_STRINGS", "1")

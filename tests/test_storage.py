@@ -431,3 +431,41 @@ def test_scan_coalescing_survives_reload_during_scan(monkeypatch, tmp_path):
             for p in s.pages[3:]:
                 p.batch = RecordBatch({"x": p.batch.columns["x"].clone()}, p.n)
     assert torch.equal(torch.cat(out), x)
+
+
+def test_spill_and_clear_drop_scan_fast_views(monkeypatch, tmp_path):
+    """The scan fast path keeps merged zero-copy views of every run (and the string short-code encodings cached on
+    their columns). A spill, a clear or a set drop must let go of them, or the HBM credited back to the budget stays
+    referenced until the next scan."""
+    import weakref
+
+    from netsdb_amd.client import PDBClient
+    from netsdb_amd.objects.record import RecordBatch
+    from netsdb_amd.objects.strings import StringColumn
+    from netsdb_amd.storage.sets import UserSet
+
+    c = PDBClient(root=str(tmp_path), page_size=1 << 14)
+    c.create_database("d")
+    c.create_set("d", "s", None)
+    monkeypatch.setattr(c.storage, "page_pool", None)
+    monkeypatch.setattr(UserSet, "COALESCE_ANY_DEVICE", True)
+    s = c.storage.get_set("d", "s")
+    x = torch.arange(20000, dtype=torch.float32).reshape(10000, 2)
+    s.add_batch(RecordBatch({"x": x, "k": StringColumn.from_list([str(i % 7) for i in range(10000)])}, 10000))
+    assert len(list(s.scan("cpu"))) == 1
+    assert len(list(s.scan("cpu"))) == 1                  # fast path armed by the complete first scan
+    assert "_scan_fast" in s.__dict__ and "_merged_runs" in s.__dict__
+    merged = s._scan_fast[1][0][1]
+    codes = merged.columns["k"].short_codes()             # a derived encoding kept with the merged column
+    ref = weakref.ref(codes)
+    del merged, codes
+    s.pages[1].spill()
+    assert "_scan_fast" not in s.__dict__ and "_merged_runs" not in s.__dict__
+    import gc
+    gc.collect()
+    assert ref() is None                                  # nothing holds the merged views any more
+    got = list(s.scan("cpu"))                             # the spilled page reloads; contents unchanged
+    assert torch.equal(torch.cat([b.columns["x"] for b in got]), x)
+    list(s.scan("cpu"))
+    c.clear_set("d", "s")
+    assert "_scan_fast" not in s.__dict__ and "_merged_runs" not in s.__dict__
