@@ -68,66 +68,6 @@ def verify(client, cv, ff, w, b, dev, nrows=16, nimg=2, single_job=False):
             "conv_images": nimg, "conv_max_rel_err": conv_err, "ok": bool(ok)}
 
 
-def _free_port() -> int:
-    import socket
-
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
-
-
-def visible_gpus() -> int:
-    """GPUs this process would see, counted WITHOUT any torch.cuda / HIP call (the launching parent stays provably
-    GPU-free): HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES when set, else the KFD topology
-    nodes with a non-zero gpu_id. -1 when it cannot be told (then rank 0's own device check decides)."""
-    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
-        v = os.environ.get(var)
-        if v is not None:
-            return len([x for x in v.split(",") if x.strip() not in ("", "-1")])
-    topo = "/sys/class/kfd/kfd/topology/nodes"
-    try:
-        n = 0
-        for node in os.listdir(topo):
-            try:
-                with open(os.path.join(topo, node, "gpu_id")) as f:
-                    n += int(f.read().strip() or 0) != 0
-            except (OSError, ValueError):
-                continue
-        return n
-    except OSError:
-        return -1
-
-
-def launch_ranks(n: int, argv) -> int:
-    """Spawn ``n`` ranks of this script (one per GPU) and wait for them. This process makes no GPU call at all
-    (visible_gpus reads the environment / KFD topology, not HIP); the children are separate processes (no exec)."""
-    import subprocess
-
-    ndev = visible_gpus()
-    if 0 < ndev < n:
-        print(f"[bench] --gpus {n} but only {ndev} GPUs visible", file=sys.stderr)
-        return 2
-    port = _free_port()
-    procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
-                                      stdout=None if r == 0 else subprocess.DEVNULL))
-    rc = 0
-    try:
-        for p in procs:
-            rc = p.wait() or rc
-    finally:
-        for p in procs:                      # one rank failed: do not leave the others waiting in a collective
-            if p.poll() is None:
-                p.kill()
-    return rc
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -151,8 +91,10 @@ def main():
                     help="8-phase GEMM main-loop MFMA shape for this run (0 = the library default; A/B arm)")
     args = ap.parse_args()
     args.single_job = not args.two_job
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    from netsdb_amd.parallel import launch
+
+    if launch.should_launch(args.gpus):
+        sys.exit(launch.launch_ranks(__file__, args.gpus, sys.argv[1:]))
 
     from netsdb_amd.client import PDBClient
     from netsdb_amd.models import conv2d as cv

@@ -50,6 +50,10 @@ struct PipeArgs {
   int tile, lds_bytes;
   int kmode, pad2;
   unsigned long long* table;
+  const unsigned long long* jtab;
+  const long long* jperm;
+  unsigned long long jmask;
+  long long bn;
 };
 
 enum ColKind : int { C_F64 = 0, C_I64, C_I32, C_F32, C_U8, C_SCODE, C_SREF };
@@ -79,9 +83,10 @@ typedef std::vector<std::tuple<int64_t, int64_t, int64_t, c10::optional<torch::T
     ColList;
 
 // Validate the program / columns / registers and fill the kernel's argument image.
+// bn >= 0: a fused join (compiled kernels): columns with late == 2 are build-side columns of bn rows.
 void fill_args(PipeArgs& a, const torch::Tensor& prog, int64_t nins_a, const ColList& cols, const torch::Tensor& lit,
                int64_t n, int64_t keep_reg, int64_t key_reg, const std::vector<int64_t>& val_regs, int64_t agg_op,
-               const std::vector<int64_t>& kpool) {
+               const std::vector<int64_t>& kpool, int64_t bn = -1) {
   TORCH_CHECK(sizes(0) == MAXINS && sizes(1) == MAXCOL && sizes(3) == FMAX && sizes(5) == (int)sizeof(PipeArgs) &&
                   sizes(8) > 0 && (sizes(8) & (sizes(8) - 1)) == 0,
               "pipe_agg: host / kernel argument layout mismatch");
@@ -139,13 +144,15 @@ void fill_args(PipeArgs& a, const torch::Tensor& prog, int64_t nins_a, const Col
     C.late = (int)std::get<1>(t);
     C.L = (int)std::get<2>(t);
     TORCH_CHECK(C.kind >= C_F64 && C.kind <= C_SREF, "pipe_agg: bad column kind");
+    TORCH_CHECK(C.late >= 0 && C.late <= (bn >= 0 ? 2 : 1), "pipe_agg: bad column pass (2 = build side of a join)");
+    const int64_t rows = C.late == 2 ? bn : n;       // the rows this column is indexed by
     if (C.kind == C_SCODE || C.kind == C_SREF) {
       TORCH_CHECK(c < MAXSTR, "pipe_agg: string columns must take the first ", MAXSTR, " column slots");
       TORCH_CHECK(std::get<4>(t).has_value() && std::get<5>(t).has_value() && std::get<6>(t).has_value(),
                   "pipe_agg: string column needs starts / ends / bytes");
       const auto &s = *std::get<4>(t), &e = *std::get<5>(t), &d = *std::get<6>(t);
-      check_col(s, n, "starts");
-      check_col(e, n, "ends");
+      check_col(s, rows, "starts");
+      check_col(e, rows, "ends");
       TORCH_CHECK(s.scalar_type() == torch::kInt64 && e.scalar_type() == torch::kInt64, "pipe_agg: starts/ends int64");
       TORCH_CHECK(d.is_cuda() && d.scalar_type() == torch::kUInt8, "pipe_agg: string bytes must be device uint8");
       TORCH_CHECK(C.kind != C_SCODE || (C.L >= 0 && C.L <= 7), "pipe_agg: short code length bound 0..7");
@@ -156,7 +163,7 @@ void fill_args(PipeArgs& a, const torch::Tensor& prog, int64_t nins_a, const Col
     } else {
       TORCH_CHECK(std::get<3>(t).has_value(), "pipe_agg: numeric column needs data");
       const auto& x = *std::get<3>(t);
-      check_col(x, n, "column");
+      check_col(x, rows, "column");
       const auto st = x.scalar_type();
       const bool ok = (C.kind == C_F64 && st == torch::kFloat64) || (C.kind == C_I64 && st == torch::kInt64) ||
                       (C.kind == C_I32 && st == torch::kInt32) || (C.kind == C_F32 && st == torch::kFloat32) ||
@@ -307,6 +314,13 @@ pybind11::bytes jit_compile(const std::string& src, const std::string& header) {
   return pybind11::bytes(code);
 }
 
+// hiprtc version ("major.minor"): part of the on-disk code-object cache key, so a toolchain upgrade recompiles.
+std::string jit_version() {
+  int major = 0, minor = 0;
+  hiprtcVersion(&major, &minor);
+  return std::to_string(major) + "." + std::to_string(minor);
+}
+
 // Load a code object and return the kernel `name` as an opaque handle (modules stay loaded for the process).
 int64_t jit_load(const std::string& code, const std::string& name) {
   static std::mutex mu;
@@ -324,10 +338,29 @@ int64_t jit_load(const std::string& code, const std::string& name) {
 // (INT64_MIN = free slot), then GCAP x FMAX f64 values (bit patterns). The host reads it back in one copy.
 torch::Tensor pipe_agg(torch::Tensor prog, int64_t nins_a, ColList cols, torch::Tensor lit, int64_t n, int64_t keep_reg,
                        int64_t key_reg, std::vector<int64_t> val_regs, int64_t agg_op, int64_t max_wg, int64_t tile,
-                       std::vector<int64_t> kpool, int64_t jit, int64_t jit_nreg, int64_t jit_rows) {
+                       std::vector<int64_t> kpool, int64_t jit, int64_t jit_nreg, int64_t jit_rows,
+                       c10::optional<torch::Tensor> jtab, c10::optional<torch::Tensor> jperm, int64_t bn) {
   const int ROWS = 4, NTHR = sizes(7), GCAP = sizes(8), CAP = sizes(4);
   PipeArgs a;
-  fill_args(a, prog, nins_a, cols, lit, n, keep_reg, key_reg, val_regs, agg_op, kpool);
+  const bool join = jtab.has_value() && jtab->defined();
+  fill_args(a, prog, nins_a, cols, lit, n, keep_reg, key_reg, val_regs, agg_op, kpool, join ? bn : -1);
+  if (join) {
+    // the fused join probe exists in the compiled kernels only; the table is relops join_build's
+    TORCH_CHECK(jit != 0, "pipe_agg: a fused join needs its compiled kernel");
+    const auto& T = *jtab;
+    TORCH_CHECK(T.is_cuda() && T.scalar_type() == torch::kInt64 && T.dim() == 2 && T.size(1) == 2 && T.is_contiguous(),
+                "pipe_agg: join table must be join_build's int64 [cap + 1, 2] device tensor");
+    const int64_t cap = T.size(0) - 1;
+    TORCH_CHECK(cap >= 1024 && (cap & (cap - 1)) == 0, "pipe_agg: malformed join table");
+    TORCH_CHECK(jperm.has_value() && jperm->defined() && jperm->is_cuda() && jperm->scalar_type() == torch::kInt64 &&
+                    jperm->is_contiguous() && jperm->numel() >= bn && bn >= 0 && bn < (int64_t(1) << 29),
+                "pipe_agg: join permutation [build rows] int64 expected");
+    TORCH_CHECK(T.device() == lit.device() && jperm->device() == lit.device(), "pipe_agg: join table on another device");
+    a.jtab = reinterpret_cast<const unsigned long long*>(T.data_ptr<int64_t>());
+    a.jperm = reinterpret_cast<const long long*>(jperm->data_ptr<int64_t>());
+    a.jmask = (unsigned long long)(cap - 1);
+    a.bn = bn;
+  }
   if (jit != 0) {                                   // the run-time compiled kernel of exactly this program shape
     TORCH_CHECK(a.nreg == jit_nreg && jit_rows >= 1 && jit_rows <= 16,
                 "pipe_agg: compiled kernel for ", jit_nreg, " registers, the program uses ", a.nreg);
@@ -403,9 +436,11 @@ void register_pipeline(pybind11::module& m) {
         pybind11::arg("prog"), pybind11::arg("nins_a"), pybind11::arg("cols"), pybind11::arg("lit"), pybind11::arg("n"),
         pybind11::arg("keep_reg"), pybind11::arg("key_reg"), pybind11::arg("val_regs"), pybind11::arg("agg_op") = 0,
         pybind11::arg("max_wg") = 0, pybind11::arg("tile") = -1, pybind11::arg("kpool") = std::vector<int64_t>(),
-        pybind11::arg("jit") = 0, pybind11::arg("jit_nreg") = 0, pybind11::arg("jit_rows") = 0);
+        pybind11::arg("jit") = 0, pybind11::arg("jit_nreg") = 0, pybind11::arg("jit_rows") = 0,
+        pybind11::arg("jtab") = pybind11::none(), pybind11::arg("jperm") = pybind11::none(), pybind11::arg("bn") = -1);
   m.def("jit_compile", &jit_compile, "hiprtc compile of a generated pipeline kernel source (gfx950 code object)",
         pybind11::arg("src"), pybind11::arg("header"));
+  m.def("jit_version", &jit_version, "hiprtc version of the run-time compiler (code-object cache key)");
   m.def("jit_load", &jit_load, "load a code object; the named kernel as an opaque handle for pipe_agg / pipe_mask(jit=)",
         pybind11::arg("code"), pybind11::arg("name"));
 }

@@ -56,6 +56,13 @@ struct PipeArgs {
   int tile, lds_bytes;           // tile / hybrid kernels: rows per tile, dynamic LDS bytes
   int kmode, pad2;               // 0 register kernels, 1 LDS-tile kernels, 2 hybrid (LDS-DMA columns, VGPR registers)
   unsigned long long* table;     // [2 + GCAP + GCAP * FMAX]: status (overflow, kept rows), keys, values (f64 bits)
+  // fused join probe (compiled kernels only, jit_join_agg_body): the build side's table of 16-byte slots
+  // {join hash, extra rows | payload << 32} (relops.hip join_build: cap + 1 slots, slot cap = the kEmpty key's),
+  // its CSR runs of repeated keys, cap - 1, and the build rows (columns with late == 2 are build-side columns)
+  const unsigned long long* jtab;
+  const long long* jperm;
+  unsigned long long jmask;
+  long long bn;
 };
 
 typedef unsigned long long u64;
@@ -269,6 +276,206 @@ __device__ __forceinline__ void jit_agg_body(const PipeArgs& a) {
     if (s_ovf) atomicOr(a.table, 1ull);
     atomicAdd(a.table + 1, s_kept);
   }
+}
+
+// ---------------------------------------------------------------- fused join probe (reference JoinProbe inside the
+// pipeline chain: src/lambdas/headers/JoinTuple.h:434, Pipeline.h:194)
+// The probe side's join hash is the engine's (kernels.hash_keys of one integer key column: splitmix64's finaliser of
+// key + golden ratio), the slot the build's (relops.hip join_insert: the finaliser of the hash, masked; the kEmpty
+// hash has the extra slot cap). A slot is ONE 16-byte read; a key with one build row keeps that row as its payload,
+// a repeated key the start of its CSR run in jperm.
+constexpr u64 JEMPTY = 0x8000000000000000ull, JGOLD = 0x9E3779B97F4A7C15ull;
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ u64 fin64(u64 x) {
+  x ^= x >> 30;
+  x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 27;
+  x *= 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return x;
+}
+
+// build rows matching probe key k: cnt (0 = none) and the payload (the row when cnt == 1, else the run start)
+__device__ __forceinline__ void join_find(const PipeArgs& a, long long k, unsigned& cnt, unsigned& pay) {
+  const u64 h = fin64((u64)k + JGOLD);
+  u64 s = h == JEMPTY ? a.jmask + 1 : (fin64(h) & a.jmask);
+  cnt = 0;
+  pay = 0;
+  for (u64 it = 0; it <= a.jmask; ++it) {       // >= 2 slots per build row: an empty slot ends every chain
+    const u64x2 e = *reinterpret_cast<const u64x2*>(a.jtab + 2 * s);
+    if (e[0] == h) {
+      cnt = (unsigned)e[1] + (h != JEMPTY ? 1u : 0u);
+      pay = (unsigned)(e[1] >> 32);
+      return;
+    }
+    if (e[0] == JEMPTY || h == JEMPTY) return;
+    s = (s + 1) & a.jmask;
+  }
+}
+
+// One kept (key, values) row into the thread's KSLOT register slots, else the workgroup's LDS table.
+template <int F>
+__device__ __forceinline__ void agg_row(const PipeArgs& a, long long key, const double (&v)[F], long long (&sk)[KSLOT],
+                                        double (&sv)[KSLOT][F], int& used, bool& ovf, long long* tk, double* tv) {
+  bool done = false;
+#pragma unroll
+  for (int s = 0; s < KSLOT; ++s) {
+    if (!done && s < used && sk[s] == key) {
+#pragma unroll
+      for (int f = 0; f < F; ++f) sv[s][f] = acc_op(sv[s][f], v[f], a.agg_op);
+      done = true;
+    }
+  }
+  if (!done && used < KSLOT) {
+#pragma unroll
+    for (int s = 0; s < KSLOT; ++s) {
+      if (!done && s == used) {
+        sk[s] = key;
+#pragma unroll
+        for (int f = 0; f < F; ++f) sv[s][f] = v[f];
+        done = true;
+      }
+    }
+    ++used;
+  }
+  if (!done) ovf |= (key == EMPTY) || !table_insert<F>(tk, tv, CAP, key, v, a.nval, a.agg_op);
+}
+
+// register slots -> LDS table (wave-combined per key) -> the global table; status words
+template <int F>
+__device__ __forceinline__ void agg_flush(const PipeArgs& a, long long (&sk)[KSLOT], double (&sv)[KSLOT][F], int used,
+                                          bool ovf, unsigned long long kept, long long* tk, double* tv, int* s_ovf,
+                                          unsigned long long* s_kept, double init) {
+  const int tid = threadIdx.x, lane = tid & 63;
+#pragma unroll
+  for (int s = 0; s < KSLOT; ++s) {
+    bool act = s < used;
+    while (true) {
+      const u64 bal = __builtin_amdgcn_ballot_w64(act);
+      if (!bal) break;
+      const int leader = __builtin_ctzll(bal);
+      const long long kl = __shfl(sk[s], leader);
+      const bool mine = act && sk[s] == kl;
+      double v[F];
+#pragma unroll
+      for (int f = 0; f < F; ++f) v[f] = wave_reduce(mine ? sv[s][f] : init, a.agg_op);
+      if (lane == leader) ovf |= (kl == EMPTY) || !table_insert<F>(tk, tv, CAP, kl, v, a.nval, a.agg_op);
+      act = act && !mine;
+    }
+  }
+  atomicAdd(s_kept, kept);
+  if (ovf) *s_ovf = 1;
+  __syncthreads();
+  long long* gk = reinterpret_cast<long long*>(a.table + 2);
+  double* gv = reinterpret_cast<double*>(a.table + 2 + GCAP);
+  for (int i = tid; i < CAP; i += NTHR) {
+    const long long k = tk[i];
+    if (k == EMPTY) continue;
+    double v[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) v[f] = tv[i * FMAX + f];
+    if (!table_insert<F>(gk, gv, GCAP, k, v, a.nval, a.agg_op)) *s_ovf = 1;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    if (*s_ovf) atomicOr(a.table, 1ull);
+    atomicAdd(a.table + 1, *s_kept);
+  }
+}
+
+// scan -> predicate -> join probe -> [post-join predicate, key, values] per match -> aggregate, ONE launch. P adds to
+// the jit_agg_body policy: JK (the probe key's register), loadb(a, brow, m, R) (the build-side columns of the matched
+// build rows) and keep2(r) (the predicate after the join: the key re-check and any build-side condition). The
+// matches of a probe row (several for a repeated build key) are walked in lock step over the wave's rows: every
+// step loads one matched build row per active row and runs segment B on it. status[1] counts the rows that passed
+// segment A (the stage's selectivity estimate, as in jit_agg_body).
+template <typename P>
+__device__ __forceinline__ void jit_join_agg_body(const PipeArgs& a) {
+  constexpr int F = P::F, NR = P::NR, ROWS = P::ROWS;
+  __shared__ long long tk[CAP];
+  __shared__ double tv[CAP * FMAX];
+  __shared__ int s_ovf;
+  __shared__ unsigned long long s_kept;
+  const int tid = threadIdx.x;
+  const double init = a.agg_op == 0 ? 0.0 : (a.agg_op == 1 ? __builtin_inf() : -__builtin_inf());
+  for (int i = tid; i < CAP; i += NTHR) tk[i] = EMPTY;
+  for (int i = tid; i < CAP * FMAX; i += NTHR) tv[i] = init;
+  if (tid == 0) {
+    s_ovf = 0;
+    s_kept = 0;
+  }
+  __syncthreads();
+
+  u64 R[ROWS][NR];
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j)
+#pragma unroll
+    for (int r = 0; r < NR; ++r) R[j][r] = 0ull;
+  long long sk[KSLOT];
+  double sv[KSLOT][F];
+  int used = 0;
+  unsigned kept = 0;
+  bool ovf = false;
+#pragma unroll
+  for (int s = 0; s < KSLOT; ++s) {
+    sk[s] = EMPTY;
+#pragma unroll
+    for (int f = 0; f < F; ++f) sv[s][f] = init;
+  }
+
+  const long long step = (long long)gridDim.x * NTHR * ROWS;
+  for (long long base = (long long)blockIdx.x * NTHR * ROWS; base < a.n; base += step) {
+    long long row[ROWS], brow[ROWS];
+    bool inr[ROWS], keep[ROWS], act[ROWS];
+    unsigned cnt[ROWS], pay[ROWS];
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      row[j] = base + (long long)j * NTHR + tid;
+      inr[j] = row[j] < a.n;
+    }
+    if (base + (long long)NTHR * ROWS <= a.n) P::template load<false, true>(a, row, inr, R);
+    else P::template load<false, false>(a, row, inr, R);
+    P::run_a(a, R);
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      keep[j] = inr[j] && P::keep(R[j]);
+      kept += keep[j] ? 1u : 0u;
+    }
+    // probe: every kept row's first slot read issued together
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      cnt[j] = 0;
+      pay[j] = 0;
+      if (keep[j]) join_find(a, (long long)R[j][P::JK], cnt[j], pay[j]);
+      keep[j] = keep[j] && cnt[j] != 0;
+      any |= keep[j];
+    }
+    if (!__builtin_amdgcn_ballot_w64(any)) continue;
+    P::template load<true, false>(a, row, keep, R);            // late probe-side columns: the matched rows only
+    for (unsigned t = 0;; ++t) {
+      bool more = false;
+#pragma unroll
+      for (int j = 0; j < ROWS; ++j) {
+        act[j] = keep[j] && t < cnt[j];
+        brow[j] = !act[j] ? 0ll : (cnt[j] == 1u ? (long long)pay[j] : a.jperm[(long long)pay[j] + t]);
+        more |= act[j];
+      }
+      if (!__builtin_amdgcn_ballot_w64(more)) break;
+      P::loadb(a, brow, act, R);
+      P::run_b(a, R);
+#pragma unroll
+      for (int j = 0; j < ROWS; ++j) {
+        if (!act[j] || !P::keep2(R[j])) continue;
+        const long long key = P::key(R[j]);
+        double v[F];
+        P::vals(R[j], v);
+        agg_row<F>(a, key, v, sk, sv, used, ovf, tk, tv);
+      }
+    }
+  }
+  agg_flush<F>(a, sk, sv, used, ovf, (unsigned long long)kept, tk, tv, &s_ovf, &s_kept, init);
 }
 
 // Filter only: keep flag per row (every column early, the whole program in run_a).

@@ -25,7 +25,7 @@ from ..objects.strings import StringColumn
 from ..parallel.comm import ClusterContext
 from ..storage.sets import DenseMatrixSet
 from ..query_planning.planner import AdaptivePlanner, PhysicalPlan, Planner
-from ..utils.trace import Tracer
+from ..utils.trace import DeviceTimer, Tracer
 from . import kernels as K
 
 
@@ -98,7 +98,16 @@ STAGE_LOG: List[dict] = []
 
 
 class JobStats(dict):
-    pass
+    """Per-job statistics. On a GPU each stage record carries ``device_seconds``: the stage's time on the device
+    stream from a HIP event pair (utils/trace.DeviceTimer), None until resolved — :meth:`device_times` resolves
+    them (``block=False``: only pairs that already completed; the engine also resolves completed pairs at the start
+    of every later job), with no synchronisation inside the job."""
+
+    def device_times(self, block: bool = True) -> list:
+        timer = getattr(self, "_timer", None)
+        if timer is not None:
+            timer.resolve(block)
+        return [st.get("device_seconds") for st in self.get("stages", [])]
 
 
 class QueryEngine:
@@ -108,6 +117,9 @@ class QueryEngine:
         self.ctx = ctx or ClusterContext()
         self.catalog = catalog
         self.tracer = tracer or Tracer(enabled=False)
+        # per-stage device time from HIP event pairs (JobStats.device_times); no synchronisation inside a job
+        self.device_timing = True
+        self.device_timer = DeviceTimer()
         self.broadcast_threshold = broadcast_threshold
         self.fusion = fusion
         self.last_plan = None
@@ -137,7 +149,7 @@ class QueryEngine:
         (dict access under the GIL); its own per-job state (spools, statistics)."""
         e = QueryEngine(self.storage, self.ctx, self.catalog, self.tracer, self.broadcast_threshold, self.fusion)
         for k in ("adaptive", "plan_cache_enabled", "ooc_fraction", "shuffle_chunk_bytes",
-                  "operand_prefetch", "fused_pipelines"):
+                  "operand_prefetch", "fused_pipelines", "device_timing"):
             setattr(e, k, getattr(self, k))
         e._plan_cache = self._plan_cache
         e.__dict__["meta_cache"] = self.__dict__.setdefault("meta_cache", {})
@@ -175,16 +187,25 @@ class QueryEngine:
                 self._plan_cache.pop(next(iter(self._plan_cache)))
         return atoms, plan.computations, plan.tcap, gkey
 
+    def _device_timed(self) -> bool:
+        """Stage device timing on: a GPU engine outside a HIP-graph capture (a captured job replays no host code)."""
+        return (self.device_timing and self.ctx.device.type == "cuda" and torch.cuda.is_available()
+                and not torch.cuda.is_current_stream_capturing())
+
     def _timed_stage(self, st, state, stats, job_name):
         sync = STAGE_SYNC and torch.cuda.is_available()
         if sync:   # profiling: device time per stage (serialises the stream at stage boundaries)
             torch.cuda.synchronize()
+        dev_t = self._device_timed()
+        ev0 = self.device_timer.start() if dev_t else None
         ts = time.perf_counter()
         with self.tracer.span(f"stage{st.id}", job=job_name, sink=st.sink.get("kind")):
             n = self._run_stage(st, state)
         if sync:
             torch.cuda.synchronize()
         rec = {"id": st.id, "desc": st.describe(), "rows_in": n, "seconds": time.perf_counter() - ts}
+        if ev0 is not None:
+            self.device_timer.stop(ev0, rec, "device_seconds")
         stats["stages"].append(rec)
         if sync:
             STAGE_LOG.append(dict(rec, job=job_name))
@@ -220,6 +241,9 @@ class QueryEngine:
     def execute(self, sinks: List[Computation], job_name: str = "job", pre_compile: bool = False) -> JobStats:
         t0 = time.perf_counter()
         stats = JobStats(job=job_name, stages=[])
+        stats._timer = self.device_timer
+        if self.device_timer.pending:
+            self.device_timer.resolve(block=False)      # earlier jobs' stage times whose events have completed
         sinks = list(sinks)
         if self.fusion and not pre_compile:       # (fusion executes the matched kernels: not on pre-compile)
             from ..query_planning.fusion import fuse_tensor_patterns
@@ -351,10 +375,15 @@ class QueryEngine:
 
             fplan = PL.plan_stage(segments[-1], state.comps, st.sink["atom"], state.graph_key)
             if fplan is not None:
+                fplan.builds = state.builds          # a fused join probe reads its build table from the job state
+                if fplan.alt is not None:
+                    fplan.alt.builds = state.builds
                 segments[-1] = fplan.prefix
                 # one rank: the launches' few pre-aggregated rows stay on the host, the sink reduces them there
                 # and its result goes back to the device in one asynchronous upload (no device round trips)
                 fplan.host_out = not self.ctx.distributed
+                if fplan.alt is not None:
+                    fplan.alt.host_out = fplan.host_out
 
         def source():
             for b in self._source_batches(st, state):
@@ -391,7 +420,29 @@ class QueryEngine:
             if b is None or b.n == 0:
                 continue
             r = PL.run_batch(fplan, b)
+            if r is None and fplan.alt is not None and fplan.disabled:
+                # the fused probe could not run (no compiled kernel, an out-of-core build, ...): the atoms up to the
+                # alternative plan's suffix eagerly (the probe among them), then that plan's fused launch
+                alt = fplan.alt
+                head = fplan.suffix[: len(fplan.suffix) - len(alt.suffix)]
+                for o in head:
+                    if b.n == 0 and o["type"] != "JOIN":
+                        break
+                    b = self._apply_atom(o, b, state)
+                if b.n == 0:
+                    continue
+                r = PL.run_batch(alt, b)
+                if r is None:
+                    self.pipeline_stats["fallback_batches"] += 1
+                    for o in alt.suffix:
+                        if b.n == 0:
+                            break
+                        b = self._apply_atom(o, b, state)
+                    yield b
+                    continue
             if r is not None:
+                if fplan.join is not None and not fplan.disabled:
+                    self.pipeline_stats["fused_join_batches"] = self.pipeline_stats.get("fused_join_batches", 0) + 1
                 if getattr(fplan, "host_out", False) and b.device.type == "cuda":
                     state.fused_out_device = b.device
                 state.unique_kv.append(r.columns[fplan.kcol])   # one row per key (the kernel's global table)
@@ -635,6 +686,7 @@ class QueryEngine:
         raise ValueError(kind)
 
     _DTYPES = (torch.float32, torch.bfloat16, torch.float16, torch.float64)
+    MERGE_BAND_BYTES = 64 << 20        # _merge_dense_output: bytes of one band's contribution buffer
 
     def _merge_dense_output(self, s, written=()):
         """A dense matrix written block by block by an SPMD pipeline: every rank wrote the blocks it produced. Agree
@@ -667,14 +719,23 @@ class QueryEngine:
             mask[r[ok], c[ok]] = 1.0
         cnt = mask.clone()
         self.ctx.all_reduce(cnt)
-        expand = lambda m: m.repeat_interleave(br, 0)[:tr].repeat_interleave(bc, 1)[:, :tc]  # noqa: E731
         view = s.matrix()                                 # logical [rows, cols] (a transposed view if need be)
-        mine = expand(mask) > 0
-        contrib = torch.where(mine, view.float(), torch.zeros((), device=dev))
-        self.ctx.all_reduce(contrib)
-        c_el = expand(cnt)
-        merged = torch.where(c_el > 0, contrib / c_el.clamp(min=1.0), view.float())
-        view.copy_(merged.to(view.dtype))
+        # the masked all-reduce runs in the panel's own precision (float64 panels stay float64; bf16 / fp16 panels
+        # combine in f32 and round once), band by band of whole block rows (<= MERGE_BAND_BYTES per band, the same
+        # bands on every rank), so no full-size [rows, cols] mask / contribution / count temporaries are built
+        acc_dt = torch.float64 if view.dtype == torch.float64 else torch.float32
+        esz = torch.tensor([], dtype=acc_dt).element_size()
+        band_blocks = max(1, self.MERGE_BAND_BYTES // max(1, br * tc * esz))
+        for b0 in range(0, nbr, band_blocks):
+            b1 = min(nbr, b0 + band_blocks)
+            r0, r1 = b0 * br, min(tr, b1 * br)
+            rows_of = lambda m: m[b0:b1].repeat_interleave(br, 0)[: r1 - r0].repeat_interleave(bc, 1)[:, :tc]  # noqa: E731
+            band = view[r0:r1]
+            mine = rows_of(mask) > 0
+            contrib = torch.where(mine, band.to(acc_dt), torch.zeros((), dtype=acc_dt, device=dev))
+            self.ctx.all_reduce(contrib)
+            c_el = rows_of(cnt).to(acc_dt)
+            band.copy_(torch.where(c_el > 0, contrib / c_el.clamp(min=1.0), band.to(acc_dt)).to(view.dtype))
         s.replicated = True
 
     def _collect(self, batches, tag: str):

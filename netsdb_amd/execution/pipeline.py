@@ -127,12 +127,22 @@ def _node_ok(node) -> bool:
 
 
 class StagePlan:
-    """The fusable suffix of a stage: ``prefix`` atoms run eagerly, the rest is one fused launch per batch."""
+    """The fusable suffix of a stage: ``prefix`` atoms run eagerly, the rest is one fused launch per batch.
 
-    def __init__(self, prefix, suffix, conj: List[E], key: Optional[E], val: E, op: str, kcol: str, vcol: str):
+    ``join`` (a stage probing a build table inside the suffix): {"name": the JOIN's output tuple set (its BuildTable in
+    the job state), "key": the probe side's key expression}; ``post`` the predicate conjuncts after the join (the key
+    re-check and any condition on build-side columns); expressions rooted at an ``E("bsrc", name)`` read the build
+    side's columns at the matched build rows."""
+
+    def __init__(self, prefix, suffix, conj: List[E], key: Optional[E], val: E, op: str, kcol: str, vcol: str,
+                 join: Optional[dict] = None, post: Optional[List[E]] = None):
         self.prefix, self.suffix = prefix, suffix
         self.conj, self.key, self.val, self.op = conj, key, val, op
         self.kcol, self.vcol = kcol, vcol
+        self.join = join
+        self.post = list(post or [])
+        self.builds = None              # the job's build tables (engine state.builds), bound before the first batch
+        self.alt: Optional["StagePlan"] = None   # join plans: the same stage with the probe left to the eager atoms
         self.disabled = False
         self.reason = None
         self.stats = {"fused_batches": 0, "fallback_batches": 0}
@@ -142,8 +152,16 @@ class StagePlan:
     def sig(self) -> tuple:
         """The stage's expressions (stable across executions of the same query): keys the selectivity estimate."""
         if self._sig is None:
-            self._sig = (tuple(_path(c) for c in self.conj), _path(self.key), _path(self.val), self.op)
+            self._sig = (tuple(_path(c) for c in self.conj), _path(self.key), _path(self.val), self.op,
+                         _path(self.join["key"]) if self.join else None, tuple(_path(c) for c in self.post))
         return self._sig
+
+    def build_batch(self) -> Optional[RecordBatch]:
+        """The build side's tuple set of a fused join (None: no join, or its build is not an in-memory table)."""
+        if not self.join:
+            return None
+        bt = (self.builds or {}).get(self.join["name"])
+        return getattr(bt, "batch", None) if hasattr(bt, "table") else None
 
 
 _STAGE_CACHE: Dict[tuple, Optional[tuple]] = {}    # (graph key, stage atoms, sink) -> plan_stage's expressions
@@ -160,20 +178,36 @@ def plan_stage(ops: List[dict], comps: dict, sink_atom: dict, graph_key=None) ->
         ck = (graph_key, tuple(o["output"]["name"] for o in ops), sink_atom["output"]["name"])
         hit = _STAGE_CACHE.get(ck, _MISS)
         if hit is not _MISS:
-            if hit is None:
-                return None
-            start, conj, key, val, op, kcol, vcol = hit
-            return StagePlan(ops[:start], ops[start:], conj, key, val, op, kcol, vcol)
+            return _unfreeze(hit, ops)
     plan = _plan_stage(ops, comps, sink_atom)
+    if plan is not None and plan.join is not None:
+        # the same stage without the fused probe: what runs when the join cannot be fused at run time (no compiled
+        # kernels, an out-of-core or oversized build), its suffix starting after the join
+        plan.alt = _plan_stage(ops, comps, sink_atom, allow_join=False)
     if ck is not None:
         if len(_STAGE_CACHE) >= _STAGE_CACHE_MAX:
             _STAGE_CACHE.pop(next(iter(_STAGE_CACHE)))
-        _STAGE_CACHE[ck] = None if plan is None else (
-            len(plan.prefix), plan.conj, plan.key, plan.val, plan.op, plan.kcol, plan.vcol)
+        _STAGE_CACHE[ck] = _freeze(plan)
     return plan
 
 
-def _plan_stage(ops: List[dict], comps: dict, sink_atom: dict) -> Optional[StagePlan]:
+def _freeze(plan: Optional[StagePlan]):
+    if plan is None:
+        return None
+    return (len(plan.prefix), plan.conj, plan.key, plan.val, plan.op, plan.kcol, plan.vcol, plan.join, plan.post,
+            _freeze(getattr(plan, "alt", None)))
+
+
+def _unfreeze(hit, ops) -> Optional[StagePlan]:
+    if hit is None:
+        return None
+    start, conj, key, val, op, kcol, vcol, join, post, alt = hit
+    p = StagePlan(ops[:start], ops[start:], conj, key, val, op, kcol, vcol, join, post)
+    p.alt = _unfreeze(alt, ops)
+    return p
+
+
+def _plan_stage(ops: List[dict], comps: dict, sink_atom: dict, allow_join: bool = True) -> Optional[StagePlan]:
     from ..computations import AggregateComp, TopKComp
 
     comp = comps.get(sink_atom["comp"])
@@ -182,20 +216,31 @@ def _plan_stage(ops: List[dict], comps: dict, sink_atom: dict) -> Optional[Stage
     op = getattr(comp, "reduce_op", "sum")
     if op not in AGG_OPS:
         return None
-    # the suffix: the longest run of trailing atoms that are all lambda-tree APPLYs / FILTERs (a join's projection is
-    # an opaque native lambda: the suffix starts after it and reads its output columns)
+    # the suffix: the longest run of trailing atoms that are lambda-tree APPLYs / FILTERs, plus at most ONE join probe
+    # (its probe-side hash, the JOIN against an in-memory build table, the key re-check and a field-picking projection:
+    # reference JoinProbe in the pipeline chain, JoinTuple.h:434 / Pipeline.h:194). Other native lambdas (opaque UDFs)
+    # end the suffix: it starts after them and reads their output columns.
     def fusable(o) -> bool:
         if o["type"] == "FILTER":
             return True
+        if o["type"] in ("HASHLEFT", "HASHRIGHT"):
+            return len(o["input"]["atts"]) == 1
+        if o["type"] == "JOIN":
+            return allow_join and o.get("_probe_side") in ("left", "right") and o.get("_strategy") != "partitioned"
         if o["type"] != "APPLY":
             return False
         if o["lambda"].startswith("self_"):
             return True
         node = comps[o["comp"]].extract_lambdas().get(o["lambda"])
-        return node is not None and _node_ok(node)
+        return node is not None and (_node_ok(node) or _pick_spec(node) is not None)
 
     start = len(ops)
+    joins = 0
     while start > 0 and fusable(ops[start - 1]):
+        if ops[start - 1]["type"] == "JOIN":
+            if joins:
+                break                                 # one fused probe per stage: an earlier join stays eager
+            joins += 1
         start -= 1
     suffix = ops[start:]
     env: Dict[str, E] = {}
@@ -204,10 +249,27 @@ def _plan_stage(ops: List[dict], comps: dict, sink_atom: dict) -> Optional[Stage
         return env[name] if name in env else E("src", (), name)
 
     conj: List[E] = []
+    post: List[E] = []
+    join = None
+    hashes: Dict[str, E] = {}
     try:
         for o in suffix:
-            if o["type"] == "FILTER":
-                conj.append(col(o["input"]["atts"][0]))
+            t = o["type"]
+            if t == "FILTER":
+                (post if join else conj).append(col(o["input"]["atts"][0]))
+                continue
+            if t in ("HASHLEFT", "HASHRIGHT"):
+                hashes[o["output"]["atts"][-1]] = col(o["input"]["atts"][0])
+                continue
+            if t == "JOIN":
+                side = o["_probe_side"]
+                hatt = o["input"]["atts"][0] if side == "left" else o["input2"]["atts"][0]
+                if hatt not in hashes:
+                    raise Unfusable("join hash computed before the suffix")
+                bcols = o["projection2"]["atts"] if side == "left" else o["projection"]["atts"]
+                for c in bcols:
+                    env[c] = E("bsrc", (), c)
+                join = {"name": o["output"]["name"], "key": hashes[hatt]}
                 continue
             args = o["input"]["atts"]
             out = o["output"]["atts"][-1]
@@ -218,32 +280,67 @@ def _plan_stage(ops: List[dict], comps: dict, sink_atom: dict) -> Optional[Stage
             node = comps[o["comp"]].extract_lambdas().get(lname)
             if node is None:
                 raise Unfusable(lname)
-            env[out] = _node_expr(node, [col(a) for a in args])
+            spec = _pick_spec(node)
+            if spec is not None:
+                env[out] = E("pick", [col(a) for a in args], spec)
+                continue
+            env[out] = _simplify(_node_expr(node, [col(a) for a in args]))
         kcol, vcol = sink_atom["input"]["atts"]
         key, val = col(kcol), col(vcol)
     except Unfusable:
         return None
-    if key.kind == "src" or val.kind == "src":
+    if key.kind in ("src", "bsrc") or val.kind in ("src", "bsrc"):
         return None                                  # computed before the suffix: nothing to fuse
     if not suffix:
         return None
-    return StagePlan(ops[:start], suffix, conj, key, val, op, kcol, vcol)
+    return StagePlan(ops[:start], suffix, conj, key, val, op, kcol, vcol, join, post)
+
+
+def _pick_spec(node) -> Optional[tuple]:
+    """A join projection that only picks named fields of its inputs (models/tpch.py ``_pick``: the function carries
+    ``.pick`` = the field names taken from each input): ((names of input 0), (names of input 1), ...), else None."""
+    fn = getattr(node, "fn", None)
+    spec = getattr(fn, "pick", None)
+    if spec is None or not getattr(node, "vectorized", False):
+        return None
+    return tuple(tuple(x) for x in spec)
+
+
+def _simplify(e: E) -> E:
+    """field(pick(in_0, .., in_k), f) -> field(in_i, f) for the input i the projection took f from; recursively."""
+    if e.kind == "field" and e.args and e.args[0].kind == "pick":
+        pk = e.args[0]
+        for i, names in enumerate(pk.val):
+            if e.val in names:
+                return E("field", [pk.args[i]], e.val)
+        raise Unfusable(f"field {e.val} not in the join projection")
+    if any(a.kind == "pick" or a.args for a in e.args):
+        return E(e.kind, [_simplify(a) for a in e.args], e.val)
+    return e
 
 
 # ---------------------------------------------------------------------------------------------- binding + codegen
-def _resolve(e: E, batch: RecordBatch):
-    """The runtime column of a 'field' / 'src' expression."""
-    if e.kind == "src":
-        c = batch.columns.get(e.val)
+def _resolve(e: E, batch: RecordBatch, build: Optional[RecordBatch] = None):
+    """The runtime column of a 'field' / 'src' / 'bsrc' (build side of a fused join) expression."""
+    if e.kind in ("src", "bsrc"):
+        src = batch if e.kind == "src" else build
+        c = src.columns.get(e.val) if src is not None else None
         if c is None:
             raise Unfusable(f"column {e.val}")
         return c
     if e.kind == "field":
-        base = _resolve(e.args[0], batch)
+        base = _resolve(e.args[0], batch, build)
         if isinstance(base, RecordBatch) and e.val in base.columns:
             return base.columns[e.val]
         raise Unfusable(f"field {e.val}")
     raise Unfusable(e.kind)
+
+
+def _side(e: E) -> int:
+    """0: a probe-side (the stage's own) column; 1: a build-side column of the fused join."""
+    while e.kind == "field":
+        e = e.args[0]
+    return 1 if e.kind == "bsrc" else 0
 
 
 def _num_kind(t: torch.Tensor) -> Tuple[int, str]:
@@ -273,6 +370,8 @@ class Program:
         self.key_layout = None                # how to turn the packed key back into columns
         self.nval = 0
         self.val_shape = None
+        self.jk_reg = -1                      # fused join: the probe key's column register
+        self.keep2_reg = -1                   # fused join: the post-join predicate (per matched build row)
 
     # registers
     def temp(self) -> int:
@@ -349,8 +448,10 @@ def _path(e: E) -> tuple:
 
 
 class _Compiler:
-    def __init__(self, plan: StagePlan, batch: RecordBatch):
-        self.plan, self.batch = plan, batch
+    def __init__(self, plan: StagePlan, batch: RecordBatch, build: Optional[RecordBatch] = None):
+        self.plan, self.batch, self.build = plan, batch, build
+        if plan.join is not None and build is None:
+            raise Unfusable("join without a build table")
         self.p = Program()
         self.cse: Dict[tuple, tuple] = {}
         self.counts: Dict[tuple, int] = {}
@@ -381,8 +482,16 @@ class _Compiler:
         for a in e.args:
             self._collect(a, usage, seg, out)
 
+    def _res(self, e: E):
+        return _resolve(e, self.batch, self.build)
+
     def _slot(self, e: E, usage: str, late: bool) -> int:
-        obj = _resolve(e, self.batch)
+        obj = self._res(e)
+        side = _side(e)
+        if usage == "jkey":
+            if side or not isinstance(obj, torch.Tensor) or _num_kind(obj)[0] not in (C_I64, C_I32):
+                raise Unfusable("join key: a probe-side integer column")
+            usage = "num"
         if isinstance(obj, StringColumn):
             if usage == "isin":
                 usage = "sref"
@@ -409,7 +518,8 @@ class _Compiler:
         if len(self.p.cols) >= MAXCOL:
             raise Unfusable("columns")
         self.p.col_index[key] = len(self.p.cols)
-        self.p.cols.append({"kind": kind, "late": int(late), "L": L, "obj": obj, "expr": e})
+        # late: 0 first pass, 1 probe-side columns loaded for the kept rows, 2 build-side columns (matched build rows)
+        self.p.cols.append({"kind": kind, "late": 2 if side else int(late), "L": L, "obj": obj, "expr": e})
         return len(self.p.cols) - 1
 
     def compile(self) -> Program:
@@ -417,6 +527,12 @@ class _Compiler:
         uses = []
         for c in plan.conj:
             self._collect(c, "num", "A", uses)
+            if any(_side(u[0]) for u in uses):
+                raise Unfusable("build-side column before the join")
+        if plan.join is not None:
+            uses.append((plan.join["key"], "jkey", "A"))
+        for c in plan.post:
+            self._collect(c, "num", "B", uses)
         keys = self._key_fields()
         for k in keys:
             uses.append((k, "key", "B"))
@@ -447,10 +563,33 @@ class _Compiler:
                     r = d
             p.keep_reg = r
         p.nins_a = len(p.ins)
+        if plan.join is not None:
+            p.jk_reg = p.col_index[(_path(plan.join["key"]), ("num",))]
         self.cse, self.counts = {}, {}
         for v in vals:
             self._count(v)
-        # segment B: key, then the value row
+        # segment B: the predicate after the join (per matched build row), the key, then the value row
+        if plan.post:
+            r = None
+            for c in plan.post:
+                rc, t = self.gen(c)
+                if t not in ("i", "b"):
+                    rc = self._truthy(rc, t)
+                if r is None:
+                    r = rc
+                else:
+                    d = p.temp()
+                    p.emit(OP_AND, d, r, rc)
+                    p.release(r)
+                    p.release(rc)
+                    r = d
+            if r < len(p.cols):                        # a bare column as the condition: keep it in a temporary
+                d = p.temp()
+                p.emit(OP_CONST, d, imm=0)
+                p.emit(OP_NEI, d, r, d)
+                r = d
+            p.keep2_reg = r
+            p.pinned.add(r)                            # read after the key and values are computed
         p.key_reg = self._gen_key(keys)
         if len(vals) > FMAX:
             raise Unfusable("values")
@@ -530,7 +669,7 @@ class _Compiler:
         return r
 
     def _key_usage(self, e: E):
-        obj = _resolve(e, self.batch)
+        obj = self._res(e)
         return ("scode", obj.max_len()) if isinstance(obj, StringColumn) else ("num",)
 
     # -- expressions: (register, type) with type f / i / b / s
@@ -547,7 +686,7 @@ class _Compiler:
     def _gen(self, e: E):
         p = self.p
         if e.kind in ("src", "field"):
-            obj = _resolve(e, self.batch)
+            obj = self._res(e)
             if isinstance(obj, StringColumn):
                 return p.col_index[(_path(e), ("sref",))], "s"
             i = p.col_index[(_path(e), ("num",))]
@@ -721,7 +860,7 @@ class _Compiler:
 
     def _static_type(self, e: E) -> str:
         if e.kind in ("src", "field"):
-            obj = _resolve(e, self.batch)
+            obj = self._res(e)
             return "s" if isinstance(obj, StringColumn) else _num_kind(obj)[1]
         if e.kind == "const":
             return "f" if isinstance(e.val, float) else "i"
@@ -756,20 +895,24 @@ def _schema_key(batch: RecordBatch) -> tuple:
 def _compile_cached(plan: StagePlan, batch: RecordBatch) -> Program:
     """The stage's program for this batch: compiled once per (stage expressions, selectivity mode, column kinds) and
     re-bound to the batch's columns afterwards (repeated queries skip the compiler)."""
-    key = (plan.sig, _SEL_EST.get(plan.sig, 0.0) < LATE_MAX_SEL, _schema_key(batch))
+    build = plan.build_batch()
+    if plan.join is not None and build is None:
+        raise Unfusable("the join's build side is not an in-memory table")
+    key = (plan.sig, _SEL_EST.get(plan.sig, 0.0) < LATE_MAX_SEL, _schema_key(batch),
+           _schema_key(build) if build is not None else None)
     hit = _PROG_CACHE.get(key)
     if hit is not None:
         p = Program.__new__(Program)
         p.__dict__.update(hit.__dict__)
-        p.cols = [dict(c, obj=_resolve(c["expr"], batch)) for c in hit.cols]
+        p.cols = [dict(c, obj=_resolve(c["expr"], batch, build)) for c in hit.cols]
         # A string key column's short-code bound L is fixed at compile time. The key above holds the column's
         # length bound only when it was already known (no device read per batch), so a batch with an unknown bound
         # can meet a program compiled for shorter strings: re-check the bound of every such column (one cached
         # reduction per column) and compile afresh when a row is longer than L.
         if all(c["kind"] != C_SCODE or c["obj"].max_len() <= c["L"] for c in p.cols):
             return p
-        return _Compiler(plan, batch).compile()
-    p = _Compiler(plan, batch).compile()
+        return _Compiler(plan, batch, build).compile()
+    p = _Compiler(plan, batch, build).compile()
     _prog_tensors(p, batch.device)              # built once here: every cached copy shares them
     if len(_PROG_CACHE) >= _PROG_CACHE_MAX:
         _PROG_CACHE.pop(next(iter(_PROG_CACHE)))
@@ -799,6 +942,8 @@ def run_batch(plan: StagePlan, batch: RecordBatch) -> Optional[RecordBatch]:
             plan.disabled = True
             plan.reason = str(e)
             return None
+    elif plan.join is not None:
+        parts = interpret_join(prog, batch.n, plan)
     else:
         parts = interpret(prog, batch.n, plan.op)
     if parts is None:
@@ -827,6 +972,8 @@ def _col_args(prog: Program, dev):
     out = []
     for c in prog.cols:
         o = c["obj"]
+        if getattr(o, "device", dev) != dev:
+            raise Unfusable("a column on another device")
         if c["kind"] == C_SCODE:
             # the column's kept fixed-width encoding: a plain int32 (codes of <= 3 bytes) or int64 load
             codes = o.short_codes32(c["L"]) if o.device.type == "cuda" else None
@@ -861,7 +1008,7 @@ JIT_ROWS = 2
 JIT_ROWS_SMALL = 4
 JIT_SMALL_NREG = 8
 JIT_STATS = {"compiled": 0, "disk_hits": 0, "launches": 0, "failed": 0}
-_JIT_FN: Dict[str, Optional[int]] = {}       # generated source -> kernel handle (None: compile failed)
+_JIT_FN: Dict[tuple, Optional[int]] = {}     # (device, generated source) -> kernel handle (None: compile failed)
 _JIT_SHAPES: Dict[tuple, tuple] = {}         # program shape -> (kernel handle or None, nreg, rows)
 _JIT_HEADER: Optional[str] = None
 _FOPS = {OP_ADDF: "+", OP_SUBF: "-", OP_MULF: "*", OP_DIVF: "/"}
@@ -882,7 +1029,7 @@ def _jit_header() -> str:
 
 def program_nreg(prog: Program, ncol: int, key_reg: int, val_regs) -> int:
     """Registers the program touches, exactly as the binding's fill_args counts them (the compiled kernel's NR)."""
-    n = max(1, ncol, prog.keep_reg + 1, key_reg + 1, *(v + 1 for v in val_regs))
+    n = max(1, ncol, prog.keep_reg + 1, key_reg + 1, getattr(prog, "keep2_reg", -1) + 1, *(v + 1 for v in val_regs))
     for (op, dst, a, b, c, imm, _aux) in prog.ins:
         n = max(n, dst + 1, a + 1, b + 1, c + 1, imm + 1 if op == OP_SEL else 0)
     return n
@@ -944,22 +1091,28 @@ _LOADS = {C_F64: ("u64", "p[row[j]]"), C_I64: ("u64", "p[row[j]]"), C_I32: ("int
           C_F32: ("float", "f2u((double)p[row[j]])"), C_U8: ("unsigned char", "(u64)p[row[j]]")}
 
 
-def _jit_loads(kinds, lates, late: bool) -> List[str]:
+def _jit_loads(kinds, lates, late) -> List[str]:
+    """Load statements of the columns of one pass: ``late`` 0 / False = first pass, 1 / True = the kept rows' late
+    probe-side columns, 2 = a fused join's build-side columns at the matched build rows (index ``brow``)."""
     out = []
+    which = int(late)
     for c, (kind, lt) in enumerate(zip(kinds, lates)):
-        if bool(lt) != late:
+        if int(lt) != which:
             continue
+        ix = "brow[j]" if which == 2 else "row[j]"
+        full = "false" if which == 2 else "FULL"
         if kind in _LOADS:
             t, e = _LOADS[kind]
+            e = e.replace("row[j]", ix)
             out.append(f"    {{ const {t}* p = reinterpret_cast<const {t}*>(a.col[{c}].p);\n"
-                       f"#pragma unroll\n      for (int j = 0; j < ROWS; ++j) R[j][{c}] = (FULL || m[j]) ? {e} : 0ull; }}")
+                       f"#pragma unroll\n      for (int j = 0; j < ROWS; ++j) R[j][{c}] = ({full} || m[j]) ? {e} : 0ull; }}")
         elif kind in (C_SCODE, C_SREF):
             v = (f"short_code(a.col[{c}].dat, s, e - s, a.col[{c}].L)" if kind == C_SCODE else
                  "(((u64)s << 24) | (u64)(e - s < 0xFFFFFFll ? e - s : 0xFFFFFFll))")
             out.append(f"    {{ const long long* st = a.col[{c}].st; const long long* en = a.col[{c}].en;\n"
                        f"#pragma unroll\n      for (int j = 0; j < ROWS; ++j) {{\n"
-                       f"        const bool mj = FULL || m[j];\n"
-                       f"        const long long s = mj ? st[row[j]] : 0ll, e = mj ? en[row[j]] : 0ll;\n"
+                       f"        const bool mj = {full} || m[j];\n"
+                       f"        const long long s = mj ? st[{ix}] : 0ll, e = mj ? en[{ix}] : 0ll;\n"
                        f"        R[j][{c}] = mj ? {v} : 0ull;\n      }} }}")
         else:
             raise Unfusable(f"column kind {kind}")
@@ -979,22 +1132,27 @@ def jit_source(prog: Program, kinds, lates, kind: str, key_reg: int = -1, val_re
         return ("#pragma unroll\n    for (int j = 0; j < ROWS; ++j) {\n      u64* r = R[j];\n"
                 + "".join(f"      {t}\n" for t in body) + "    }")
 
+    join = kind == "agg" and getattr(prog, "jk_reg", -1) >= 0
+
     def loads(late):
         ls = _jit_loads(kinds, [lt if kind == "agg" else 0 for lt in lates], late)
-        return "\n".join(ls) if ls else "    (void)a; (void)row; (void)m; (void)R;"
+        idx = "brow" if late == 2 else "row"
+        return "\n".join(ls) if ls else f"    (void)a; (void){idx}; (void)m; (void)R;"
 
     vals = "".join(f"    v[{f}] = u2f(r[{reg}]);\n" for f, reg in enumerate(val_regs)) or "    v[0] = 0.0; (void)r;\n"
     keep = "true" if prog.keep_reg < 0 else f"r[{prog.keep_reg}] != 0ull"
+    keep2 = f"r[{prog.keep2_reg}] != 0ull" if join and getattr(prog, "keep2_reg", -1) >= 0 else "true"
     key = "0ll" if key_reg < 0 else f"(long long)r[{key_reg}]"
+    body = "jit_join_agg_body" if join else "jit_agg_body"
     entry = ("extern \"C\" __global__ void __launch_bounds__(nsdb_pipe::NTHR) nsdb_jit_agg(const nsdb_pipe::PipeArgs a) {\n"
-             "  nsdb_pipe::jit_agg_body<nsdb_pipe::JitProg>(a);\n}\n" if kind == "agg" else
+             f"  nsdb_pipe::{body}<nsdb_pipe::JitProg>(a);\n}}\n" if kind == "agg" else
              "extern \"C\" __global__ void __launch_bounds__(nsdb_pipe::NTHR) nsdb_jit_mask(const nsdb_pipe::PipeArgs a, "
              "unsigned char* mask) {\n  nsdb_pipe::jit_mask_body<nsdb_pipe::JitProg>(a, mask);\n}\n")
     return f"""// generated by netsdb_amd.execution.pipeline.jit_source ({kind})
 #include "pipeline_core.h"
 namespace nsdb_pipe {{
 struct JitProg {{
-  static constexpr int F = {F}, NR = {nreg}, ROWS = {rows};
+  static constexpr int F = {F}, NR = {nreg}, ROWS = {rows}, JK = {max(0, getattr(prog, "jk_reg", -1))};
   template <bool LATE, bool FULL>
   __device__ static __forceinline__ void load(const PipeArgs& a, const long long (&row)[ROWS], const bool (&m)[ROWS],
                                               u64 (&R)[ROWS][NR]) {{
@@ -1004,6 +1162,10 @@ struct JitProg {{
 {loads(True)}
     }}
   }}
+  __device__ static __forceinline__ void loadb(const PipeArgs& a, const long long (&brow)[ROWS], const bool (&m)[ROWS],
+                                               u64 (&R)[ROWS][NR]) {{
+{loads(2) if join else "    (void)a; (void)brow; (void)m; (void)R;"}
+  }}
   __device__ static __forceinline__ void run_a(const PipeArgs& a, u64 (&R)[ROWS][NR]) {{
 {seg(0, nins_a)}
   }}
@@ -1011,6 +1173,7 @@ struct JitProg {{
 {seg(nins_a, len(prog.ins))}
   }}
   __device__ static __forceinline__ bool keep(const u64 (&r)[NR]) {{ (void)r; return {keep}; }}
+  __device__ static __forceinline__ bool keep2(const u64 (&r)[NR]) {{ (void)r; return {keep2}; }}
   __device__ static __forceinline__ long long key(const u64 (&r)[NR]) {{ (void)r; return {key}; }}
   __device__ static __forceinline__ void vals(const u64 (&r)[NR], double (&v)[F]) {{
 {vals}  }}
@@ -1028,17 +1191,28 @@ def _jit_cache_dir() -> Optional[str]:
         return None
 
 
-def jit_kernel(src: str, name: str) -> Optional[int]:
-    """The loaded kernel of a generated source (compiled once per process, code objects cached on disk), or None when
-    compilation fails (the interpreter kernels then run that stage)."""
-    if src in _JIT_FN:
-        return _JIT_FN[src]
+def _dev_index(dev=None) -> int:
+    if dev is not None and torch.device(dev).type == "cuda":
+        d = torch.device(dev)
+        return d.index if d.index is not None else torch.cuda.current_device()
+    return torch.cuda.current_device() if torch.cuda.is_available() else -1
+
+
+def jit_kernel(src: str, name: str, dev=None) -> Optional[int]:
+    """The loaded kernel of a generated source on device ``dev`` (default: the current one), compiled once per process,
+    code objects cached on disk; or None when compilation fails (the interpreter kernels then run that stage). A
+    loaded module belongs to one device's context, so the handle cache is per device; the disk cache digest covers
+    the target, the header, the source and the hiprtc version."""
+    di = _dev_index(dev)
+    if (di, src) in _JIT_FN:
+        return _JIT_FN[(di, src)]
     h = _ext.hip()
     fn = None
     try:
         hdr = _jit_header()
         arch = os.environ.get("PYTORCH_ROCM_ARCH") or "gfx950"
-        digest = hashlib.sha256((arch + "\0" + hdr + "\0" + src).encode()).hexdigest()[:32]
+        rtc = h.jit_version() if hasattr(h, "jit_version") else "?"
+        digest = hashlib.sha256((arch + "\0" + rtc + "\0" + hdr + "\0" + src).encode()).hexdigest()[:32]
         d = _jit_cache_dir()
         path = os.path.join(d, f"{digest}.hsaco") if d else None
         code = None
@@ -1054,25 +1228,30 @@ def jit_kernel(src: str, name: str) -> Optional[int]:
                 with open(tmp, "wb") as f:
                     f.write(code)
                 os.replace(tmp, path)
-        fn = int(h.jit_load(code, name))
+        if di >= 0:
+            with torch.cuda.device(di):         # the module loads into this device's context
+                fn = int(h.jit_load(code, name))
+        else:
+            fn = int(h.jit_load(code, name))
     except Exception as e:          # noqa: BLE001 - any compiler / loader failure keeps the interpreter path
         JIT_STATS["failed"] += 1
         warnings.warn(f"pipeline kernel compilation failed, interpreting this stage: {e}")
         fn = None
-    _JIT_FN[src] = fn
+    _JIT_FN[(di, src)] = fn
     return fn
 
 
-def _jit_for(prog: Program, cargs, kind: str, key_reg: int = -1, val_regs=()):
-    """(kernel handle, nreg, rows) of the compiled kernel for this launch, or None (interpreter)."""
+def _jit_for(prog: Program, cargs, kind: str, key_reg: int = -1, val_regs=(), dev=None):
+    """(kernel handle, nreg, rows) of the compiled kernel for this launch on ``dev``, or None (interpreter)."""
     if not JIT or not hasattr(_ext.hip(), "jit_compile"):
         return None
     kinds = tuple(c[0] for c in cargs)
     lates = tuple(c[1] for c in cargs) if kind == "agg" else ()
     # the kernel of a program shape: generated + compiled once, then found by the shape alone (generating the source
     # costs ~30 us of Python per launch)
-    shape = (kind, tuple(prog.ins), kinds, lates, key_reg, tuple(val_regs), prog.keep_reg, prog.nins_a, JIT_ROWS,
-             JIT_ROWS_SMALL, JIT_SMALL_NREG)
+    shape = (_dev_index(dev), kind, tuple(prog.ins), kinds, lates, key_reg, tuple(val_regs), prog.keep_reg,
+             prog.nins_a, getattr(prog, "jk_reg", -1), getattr(prog, "keep2_reg", -1), JIT_ROWS, JIT_ROWS_SMALL,
+             JIT_SMALL_NREG)
     hit = _JIT_SHAPES.get(shape)
     if hit is None:
         nreg = program_nreg(prog, len(kinds), key_reg, val_regs)
@@ -1081,7 +1260,7 @@ def _jit_for(prog: Program, cargs, kind: str, key_reg: int = -1, val_regs=()):
             src = jit_source(prog, list(kinds), list(lates) or [0] * len(kinds), kind, key_reg, val_regs, rows=rows)
         except Unfusable:
             return None
-        fn = jit_kernel(src, "nsdb_jit_agg" if kind == "agg" else "nsdb_jit_mask")
+        fn = jit_kernel(src, "nsdb_jit_agg" if kind == "agg" else "nsdb_jit_mask", dev)
         if len(_JIT_SHAPES) >= 4096:          # the shape includes the immediates: bound it for varying literals
             _JIT_SHAPES.clear()
         hit = _JIT_SHAPES[shape] = (fn, nreg, rows)
@@ -1112,14 +1291,32 @@ def _prog_tensors(prog: Program, dev):
     return ins, lit
 
 
+def _join_table(plan: StagePlan, dev):
+    """(slots, perm, build rows) of the fused join's device hash table (relops join_build), built on first use."""
+    bt = plan.builds[plan.join["name"]]
+    if bt.batch is None or bt.batch.n == 0:
+        raise Unfusable("empty build side")
+    jt = bt.table(dev)
+    d = getattr(jt, "_dev", None)
+    if d is None:
+        raise Unfusable("build side without a device hash table")
+    return d[0], d[1], int(bt.batch.n)
+
+
 def _launch(prog: Program, n: int, dev, plan: StagePlan):
     h = _ext.hip()
     ins, lit = _prog_tensors(prog, dev)
     cargs = _col_args(prog, dev)
-    jit = _jit_for(prog, cargs, "agg", prog.key_reg, prog.val_regs)
+    jtab = jperm = None
+    bn = -1
+    if plan.join is not None:
+        jtab, jperm, bn = _join_table(plan, dev)
+    jit = _jit_for(prog, cargs, "agg", prog.key_reg, prog.val_regs, dev)
+    if jit is None and plan.join is not None:
+        raise Unfusable("the fused join probe needs the compiled kernels")
     fn, jnreg, jrows = jit if jit else (0, 0, 0)
     table = h.pipe_agg(ins, prog.nins_a, cargs, lit, n, prog.keep_reg, prog.key_reg, prog.val_regs,
-                       AGG_OPS[plan.op], 0, TILE, prog.kpool, fn, jnreg, jrows)
+                       AGG_OPS[plan.op], 0, TILE, prog.kpool, fn, jnreg, jrows, jtab, jperm, bn)
     host = _read_table(table)                    # the one device -> host read of the launch
     if int(host[0]) != 0:
         return None
@@ -1214,11 +1411,43 @@ def interpret(prog: Program, n: int, op: str):
     return _merge(key[idx], vals[idx], op)
 
 
-def _run_program(prog: Program, n: int) -> List[Optional[torch.Tensor]]:
-    """Every instruction of the program over whole columns: the final register values."""
+def interpret_join(prog: Program, n: int, plan: StagePlan):
+    """A fused join program with whole-column torch ops (the CPU model of jit_join_agg_body): segment A over the
+    probe rows, the probe against the build side's join hashes (kernels.JoinTable), segment B over every (build row,
+    probe row) pair, then the post-join keep flag, key and values merged."""
+    from . import kernels as KK
+
+    regs = _run_program(prog, n, hi=prog.nins_a, sides=(0,))
+    keep = torch.ones(n, dtype=torch.bool) if prog.keep_reg < 0 else regs[prog.keep_reg] != 0
+    kidx = keep.nonzero().flatten()
+    bt = plan.builds[plan.join["name"]]
+    h = KK.hash_keys(regs[prog.jk_reg][kidx])
+    bi, pi = bt.table(h.device).probe(h)
+    prow = kidx[pi]
+    m = int(prow.numel())
+    rowmap = {i: (bi if c["late"] == 2 else prow) for i, c in enumerate(prog.cols)}
+    regs = _run_program(prog, m, lo=prog.nins_a, rowmap=rowmap)
+    f = lambda t: t.view(torch.float64)  # noqa: E731
+    keep2 = torch.ones(m, dtype=torch.bool) if prog.keep2_reg < 0 else regs[prog.keep2_reg] != 0
+    key = torch.zeros(m, dtype=torch.int64) if prog.key_reg < 0 else regs[prog.key_reg]
+    vals = torch.stack([f(regs[r]) for r in prog.val_regs], 1) if prog.val_regs else torch.zeros(m, 0, dtype=torch.float64)
+    idx = keep2.nonzero().flatten()
+    if torch.unique(key[idx]).numel() > INTERP_CAP:
+        return None
+    return _merge(key[idx], vals[idx], plan.op)
+
+
+def _run_program(prog: Program, n: int, lo: int = 0, hi: Optional[int] = None, sides=(0, 1),
+                 rowmap: Optional[dict] = None) -> List[Optional[torch.Tensor]]:
+    """Instructions [lo, hi) of the program over whole columns: the final register values. ``rowmap``: column slot ->
+    the row of that column each of the n evaluated rows reads (a fused join's expanded pairs); ``sides``: which
+    columns to load (0 = the stage's own, build-side columns only with 1 in it)."""
     regs: List[Optional[torch.Tensor]] = [None] * NREG
     for i, c in enumerate(prog.cols):
-        regs[i] = _col_values(c)
+        if (1 if c["late"] == 2 else 0) not in sides:
+            continue
+        v = _col_values(c)
+        regs[i] = v if rowmap is None else v[rowmap[i]]
     f = lambda t: t.view(torch.float64)  # noqa: E731
     u = lambda t: t.view(torch.int64)    # noqa: E731
 
@@ -1227,6 +1456,8 @@ def _run_program(prog: Program, n: int) -> List[Optional[torch.Tensor]]:
         off, ll = imm >> 16, imm & 0xFFFF
         lit = bytes(prog.lit[off: off + ll])
         s = o.tolist()
+        if rowmap is not None:
+            s = [s[i] for i in rowmap[col].tolist()]
         if mode == 0:
             m = [x.encode() == lit for x in s]
         elif mode == 1:
@@ -1278,7 +1509,7 @@ def _run_program(prog: Program, n: int) -> List[Optional[torch.Tensor]]:
                 z = ((z != 0) & (regs[c] != 0)).long()
             regs[d] = z
 
-    run(0, len(prog.ins))
+    run(lo, len(prog.ins) if hi is None else hi)
     return regs
 
 
@@ -1365,7 +1596,7 @@ def run_filter(plan: FilterPlan, batch: RecordBatch) -> Optional[RecordBatch]:
             plan.disabled = True
             plan.reason = str(e)
             return None
-        jit = _jit_for(prog, cargs, "mask")
+        jit = _jit_for(prog, cargs, "mask", dev=dev)
         fn, jnreg, jrows = jit if jit else (0, 0, 0)
         mask = _ext.hip().pipe_mask(ins, cargs, lit, batch.n, prog.keep_reg, TILE, prog.kpool, fn, jnreg,
                                     jrows).view(torch.bool)      # 0 / 1 bytes: a bool view, no conversion pass
@@ -1383,5 +1614,5 @@ def interpret_mask(prog: Program, n: int) -> torch.Tensor:
     return torch.ones(n, dtype=torch.bool) if prog.keep_reg < 0 else regs[prog.keep_reg] != 0
 
 
-__all__ = ["plan_stage", "run_batch", "StagePlan", "Unfusable", "interpret", "fuse_filters", "run_filter",
+__all__ = ["plan_stage", "run_batch", "StagePlan", "Unfusable", "interpret", "interpret_join", "fuse_filters", "run_filter",
            "FilterPlan"]

@@ -540,6 +540,9 @@ def _pick(prefix_cols):
         n = bs[0].n
         return RecordBatch(cols, n)
 
+    # declarative form of this projection (field names per input): the fused pipeline compiler reads picked fields
+    # straight from the joined inputs instead of materialising the merged batch (execution/pipeline.py _pick_spec)
+    proj.pick = tuple(tuple(names) for names in prefix_cols)
     return proj
 
 

@@ -36,10 +36,9 @@ _MASK = (1 << 64) - 1
 def to_host(*ts: torch.Tensor) -> List[torch.Tensor]:
     """Host copies of several tensors with ONE synchronisation: device tensors are copied asynchronously (into
     pinned buffers) and the stream is synchronised once, instead of one blocking read per tensor."""
-    dev = [t for t in ts if t.device.type == "cuda"]
     out = [t.to("cpu", non_blocking=True) if t.device.type == "cuda" else t for t in ts]
-    if dev:
-        torch.cuda.current_stream(dev[0].device).synchronize()
+    for d in {t.device for t in ts if t.device.type == "cuda"}:     # every device the copies were queued on
+        torch.cuda.current_stream(d).synchronize()
     return out
 
 

@@ -52,7 +52,10 @@ class ClusterContext:
         # for under a watchdog that raises NodeFailure when a peer stops heartbeating, instead of hanging
         self.health = None
         self._schema_cache: Dict[int, dict] = {}
-        self.stats = {"collectives": 0, "schema_cache_hits": 0, "schema_exchanges": 0}
+        # coll_bytes: payload bytes this rank handed to data collectives (not the gloo metadata group);
+        # xgmi_pred_s: what those collectives would take on MI355X xGMI under xgmi_seconds' model
+        self.stats = {"collectives": 0, "schema_cache_hits": 0, "schema_exchanges": 0, "coll_bytes": 0,
+                      "xgmi_pred_s": 0.0, "data_collectives": 0}
         # single-tensor collectives (all_gather_into_tensor / reduce_scatter_tensor into one contiguous buffer):
         # RCCL's native form; gloo implements them too in this torch, so the CPU multi-rank tests run the SAME
         # branches the GPUs take. NSDB_TENSOR_COLLECTIVES=0 selects the list-based fallback (tested as well).
@@ -125,9 +128,21 @@ class ClusterContext:
                 time.sleep(0.01)
             raise
 
+    def _account(self, op: str, t: Optional[torch.Tensor], group=None):
+        """Per-collective traffic accounting (data group only): payload bytes and the modelled xGMI time."""
+        if t is None or (group is not None and group is self.meta_group):
+            return
+        nb = t.numel() * t.element_size()
+        self.stats["data_collectives"] += 1
+        self.stats["coll_bytes"] += nb
+        self.stats["xgmi_pred_s"] += xgmi_seconds(op, nb, self.world_size)
+
     def _coll(self, fn, *args, **kw):
         """Issue a torch.distributed collective asynchronously and wait under the heartbeat watchdog."""
         self.stats["collectives"] += 1
+        op = _COLL_OPS.get(fn)
+        if op is not None:
+            self._account(op[0], args[op[1]] if len(args) > op[1] else None, kw.get("group"))
         if self.health is not None:
             self.health.check()
             self.health.mark_progress()
@@ -209,6 +224,7 @@ class ClusterContext:
         round); wait for the returned work with :meth:`_wait` (heartbeat-checked). On RCCL the transfer runs on
         the communicator's stream, ordered after the work already queued on the current stream."""
         self.stats["collectives"] += 1
+        self._account("all_to_all", inp)
         if self.health is not None:
             self.health.check()
             self.health.mark_progress()
@@ -440,6 +456,40 @@ class ClusterContext:
         return [_unflatten(ps.unpack(o[:k].to(self.device), t)) for o, k in zip(outs, ns) if k]
 
 
+# ---------------------------------------------------------------------------------------------- xGMI model
+# MI355X node: 8 GPUs, every pair joined by one xGMI link (7 links per GPU, ~153 GB/s per link and direction), so a
+# collective over the full node is bound by the bytes ONE link carries, not by a ring's slowest hop. Model (no
+# congestion, alpha = fixed cost per collective):
+#   all_to_all (payload P per rank): each peer link carries P / n            -> alpha + (P / n) / B
+#   all_gather (P sent by each rank): every peer link carries P               -> alpha + P / B
+#   reduce_scatter (P input per rank): P / n per link                         -> alpha + (P / n) / B
+#   all_reduce (P per rank) = reduce_scatter + all_gather of P / n             -> 2 alpha + 2 (P / n) / B
+#   broadcast (P from the root): the root's links carry P each                -> alpha + P / B
+# With fewer ranks than 8 the same per-link rates hold (each rank still has a direct link to every peer).
+XGMI_LINK_BPS = 153e9
+XGMI_ALPHA_S = 10e-6
+
+
+def xgmi_seconds(op: str, nbytes: int, world: int, link_bps: float = XGMI_LINK_BPS, alpha: float = XGMI_ALPHA_S) -> float:
+    """Modelled wall time of one collective over ``world`` MI355X GPUs of one node (0 for a single rank)."""
+    if world <= 1 or nbytes <= 0:
+        return 0.0
+    per_peer = nbytes / world
+    if op == "all_reduce":
+        return 2 * alpha + 2 * per_peer / link_bps
+    if op in ("all_to_all", "reduce_scatter"):
+        return alpha + per_peer / link_bps
+    if op in ("all_gather", "broadcast"):
+        return alpha + nbytes / link_bps
+    return alpha
+
+
+# torch.distributed functions -> (model op, index of the payload tensor among the positional arguments)
+_COLL_OPS = {dist.all_reduce: ("all_reduce", 0), dist.all_gather: ("all_gather", 1),
+             dist.all_gather_into_tensor: ("all_gather", 1), dist.all_to_all_single: ("all_to_all", 1),
+             dist.reduce_scatter_tensor: ("reduce_scatter", 1), dist.broadcast: ("broadcast", 0)}
+
+
 _SEP = "\x1f"
 
 
@@ -578,4 +628,4 @@ def _dec_plain(v):
 
 LOCAL = ClusterContext()
 
-__all__ = ["ClusterContext", "LOCAL"]
+__all__ = ["ClusterContext", "LOCAL", "xgmi_seconds"]

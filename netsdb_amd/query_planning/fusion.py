@@ -390,6 +390,7 @@ class MatmulNode(Node):
             if ctx.health is not None:
                 ctx.health.check()
             ctx.stats["collectives"] += 1
+            ctx._account("all_gather", src)
             if nccl:
                 # concatenated form [ws * nc, kseg] (every backend accepts it; viewed as [ws, nc, kseg] below)
                 dst = torch.empty(ws * (n1 - n0), kseg, dtype=src.dtype, device=cd)
@@ -456,6 +457,7 @@ class MatmulNode(Node):
                 ctx.health.check()
                 ctx.health.mark_progress()
             ctx.stats["collectives"] += 1
+            ctx._account("reduce_scatter" if ctx.tensor_collectives else "all_reduce", src)
             if ctx.tensor_collectives:
                 out = torch.empty(eq, cw, dtype=torch.float32, device=cd)
                 work = dist.reduce_scatter_tensor(out, src, op=dist.ReduceOp.SUM, async_op=True)

@@ -50,7 +50,7 @@ CREATE TABLE IF NOT EXISTS job_instance (id INTEGER PRIMARY KEY AUTOINCREMENT, j
                                          submit_time REAL, finish_time REAL, shuffles INTEGER, seconds REAL);
 CREATE TABLE IF NOT EXISTS job_stage (id INTEGER PRIMARY KEY AUTOINCREMENT, job_instance_id INTEGER, stage_id INTEGER,
                                       source_type TEXT, sink_type TEXT, strategy TEXT, num_ops INTEGER,
-                                      rows_in INTEGER, seconds REAL, description TEXT);
+                                      rows_in INTEGER, seconds REAL, description TEXT, device_seconds REAL);
 CREATE TABLE IF NOT EXISTS lambda (id INTEGER PRIMARY KEY AUTOINCREMENT, job_id INTEGER, lambda_type TEXT,
                                    lambda_identifier TEXT, computation_name TEXT, lambda_name TEXT,
                                    input_index INTEGER, UNIQUE(job_id, computation_name, lambda_identifier));
@@ -168,7 +168,27 @@ class SelfLearningDB:
     def __init__(self, path: str = ":memory:"):
         self.conn = sqlite3.connect(path, check_same_thread=False)
         self.conn.executescript(_SCHEMA)
+        cols = {r[1] for r in self.conn.execute("PRAGMA table_info(job_stage)")}
+        if "device_seconds" not in cols:            # a history file written before stages had device times
+            self.conn.execute("ALTER TABLE job_stage ADD COLUMN device_seconds REAL")
         self.lock = threading.Lock()
+        # stage rows whose device time (HIP event pair, resolved asynchronously) was not known when recorded
+        self._pending_dev: List[tuple] = []
+
+    def flush_device_times(self, block: bool = False) -> int:
+        """Write the device times of recorded stages whose event pairs have resolved since (``block``: resolve them
+        now); returns how many stay pending."""
+        keep = []
+        for sid, stats, rec in self._pending_dev:
+            if rec.get("device_seconds") is None and hasattr(stats, "device_times"):
+                stats.device_times(block)
+            if rec.get("device_seconds") is None:
+                keep.append((sid, stats, rec))
+                continue
+            with self.lock, self.conn:
+                self.conn.execute("UPDATE job_stage SET device_seconds=? WHERE id=?", (rec["device_seconds"], sid))
+        self._pending_dev = keep
+        return len(keep)
 
     def record_job(self, name: str, seconds: float, uses: List[dict]) -> int:
         with self.lock, self.conn:
@@ -210,6 +230,10 @@ class SelfLearningDB:
         import hashlib
 
         secs = float(stats.get("seconds", 0.0))
+        if self._pending_dev:
+            self.flush_device_times(False)
+        if hasattr(stats, "device_times"):
+            stats.device_times(False)                 # whatever has completed already (no wait)
         sig = hashlib.sha1((tcap or "").encode()).hexdigest()[:16]
         with self.lock, self.conn:
             self.conn.execute("INSERT OR IGNORE INTO job(name, tcap, signature, initial_latency) VALUES (?,?,?,?)",
@@ -239,9 +263,11 @@ class SelfLearningDB:
             with self.lock, self.conn:
                 sid = self.conn.execute(
                     "INSERT INTO job_stage(job_instance_id, stage_id, source_type, sink_type, strategy, num_ops,"
-                    " rows_in, seconds, description) VALUES (?,?,?,?,?,?,?,?,?)",
+                    " rows_in, seconds, description, device_seconds) VALUES (?,?,?,?,?,?,?,?,?,?)",
                     (iid, st.id, st.source.get("kind"), sink.get("kind"), sink.get("strategy"), len(st.ops),
-                     t.get("rows_in"), t.get("seconds"), st.describe())).lastrowid
+                     t.get("rows_in"), t.get("seconds"), st.describe(), t.get("device_seconds"))).lastrowid
+            if "device_seconds" in t and t["device_seconds"] is None:
+                self._pending_dev.append((sid, stats, t))
             ios = []
             if st.source.get("kind") == "scan":
                 ios.append((st.source["atom"]["db"], st.source["atom"]["set"], 0, "in"))

@@ -6,8 +6,12 @@ blocks (90 of 100) are identical across models and whose remaining columns are p
 ``batch`` (100) one-hot-sized input rows is scored against every model (FFTransposeMult + FFAggMatrix:
 ``y = W @ X^T``).
 
-    python scripts/bench_dedup.py [--models 12] [--steps 5 --warmup 2]
+    python scripts/bench_dedup.py [--models 12] [--steps 5 --warmup 2] [--gpus N] [--small]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 scripts/bench_dedup.py
+
+``--gpus N`` without torchrun starts its own N ranks (netsdb_amd.parallel.launch: the parent makes no GPU call).
+The collective phases report the payload bytes each rank hands to RCCL and the xGMI time the node model predicts
+for them (parallel/comm.py xgmi_seconds) next to their measured time.
 
 Models are assigned round-robin to ranks; every phase is collective (ranks with no model that round take
 part with None).  Timed phases (each bracketed by barrier + synchronize, max over ranks):
@@ -46,7 +50,16 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--check", type=int, default=1, help="compare model 0's scores with an fp32 reference")
+    ap.add_argument("--gpus", type=int, default=1, help="ranks to start when not under torchrun (one per GPU)")
+    ap.add_argument("--small", action="store_true", help="CPU / contract size (8 models of 20 x 4000, blocks 10 x 400)")
     a = ap.parse_args()
+    if a.small:
+        a.models, a.rows, a.cols, a.block_rows, a.block_cols, a.shared_blocks, a.batch = 8, 20, 4000, 10, 400, 9, 16
+        a.steps, a.warmup = 1, 0
+    from netsdb_amd.parallel import launch
+
+    if launch.should_launch(a.gpus):
+        sys.exit(launch.launch_ranks(__file__, a.gpus, sys.argv[1:]))
 
     from netsdb_amd.models.dedup import DistributedBlockPool, SharedInference
     from netsdb_amd import ops
@@ -81,13 +94,28 @@ def main():
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
 
-    def timed(fn, steps):
+    comm = {}
+
+    def comm_mark():
+        return ctx.stats["coll_bytes"], ctx.stats["xgmi_pred_s"]
+
+    def comm_record(tag, mark, steps=1):
+        b = ctx.all_reduce_scalar(float(ctx.stats["coll_bytes"] - mark[0]), "max") / steps
+        x = ctx.all_reduce_scalar(ctx.stats["xgmi_pred_s"] - mark[1], "max") / steps
+        comm[f"{tag}_coll_MB_per_rank"] = round(b / 1e6, 3)
+        comm[f"{tag}_xgmi_pred_ms"] = round(x * 1e3, 3)
+
+    def timed(fn, steps, tag=None):
         sync()
+        mk = comm_mark()
         t0 = time.perf_counter()
         for _ in range(steps):
             fn()
         sync()
-        return ctx.all_reduce_scalar((time.perf_counter() - t0) / steps, "max")
+        dt = ctx.all_reduce_scalar((time.perf_counter() - t0) / steps, "max")
+        if tag:
+            comm_record(tag, mk, steps)
+        return dt
 
     # ---------------------------------------------------------------- add (timed once per pool build)
     def build_pool():
@@ -106,7 +134,9 @@ def main():
 
     for _ in range(max(1, a.warmup // 2)):
         build_pool()                                   # warm the hash / all-to-all paths
+    mk = comm_mark()
     pool, t_add = build_pool()
+    comm_record("add", mk)
     model_bytes = a.models * R * C * 2
     stored = ctx.all_reduce_scalar(float(pool.stored_blocks()), "sum")
     blocks_in = a.models * math.ceil(R / br) * nbc
@@ -123,7 +153,7 @@ def main():
 
     for _ in range(a.warmup):
         materialize()
-    t_mat = timed(materialize, a.steps)
+    t_mat = timed(materialize, a.steps, "materialize")
 
     # ---------------------------------------------------------------- inference
     def infer_naive():
@@ -183,7 +213,7 @@ def main():
             "infer_naive_rows_per_s": round(rows / t_naive, 1), "infer_naive_ms": round(t_naive * 1e3, 3),
             "infer_dedup_ms": round(t_dedup * 1e3, 3), "dedup_speedup": round(t_naive / t_dedup, 2),
             "panel_GB_dedup": round((si.panel_bytes() if si else 0) / 1e9, 3),
-            "panel_GB_naive": round(len(mine) * R * C * 2 / 1e9, 3), "rel_err_model0": err}), flush=True)
+            "panel_GB_naive": round(len(mine) * R * C * 2 / 1e9, 3), "rel_err_model0": err, **comm}), flush=True)
     if ctx.distributed:
         torch.distributed.destroy_process_group()
 

@@ -5,6 +5,10 @@ Reference: src/tpch/source/tpchDataLoader.cc (load), src/tpchBench + src/tpch/he
 Data: models/tpch_gen.generate_fast (dbgen cardinalities and domains, vectorised; not byte-identical to dbgen).
 Timing: each query is run once untimed (plan compile, allocator warm-up), then ``--rounds`` times, each a full
 query including its result read-back, bracketed by torch.cuda.synchronize(); the median is reported.
+First-run latency (``--cold``, default on): before the timed runs every query also runs twice from empty in-process
+caches (TCAP plans, stage expressions, compiled programs, loaded kernels): first with an EMPTY on-disk code-object
+cache (so its fused kernels are generated and compiled by hiprtc inside the measured run: ``first_ms_cold``), then
+with that cache warm (``first_ms_warm_disk``: the code objects are only loaded).
 
     python scripts/bench_tpch.py [--sf 1,10] [--queries q01,q03,q06,q12,q13] [--rounds 3] [--json out.json]
 """
@@ -52,6 +56,16 @@ def _ref_sorted(q, ref):
     return sorted(ref, key=lambda x: x[key])
 
 
+def _clear_process_caches(c):
+    """Forget every in-process cache a repeated query hits (a new process with the same data): TCAP plans, stage
+    expressions, compiled programs and their tensors, generated sources and loaded kernel handles."""
+    from netsdb_amd.execution import pipeline as PL
+
+    c.engine._plan_cache.clear()
+    for d in (PL._STAGE_CACHE, PL._PROG_CACHE, PL._JIT_FN, PL._JIT_SHAPES, PL._LIT_DEV):
+        d.clear()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sf", default="1,10")
@@ -60,6 +74,8 @@ def main():
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--json", default=None)
     ap.add_argument("--host-profile", default=None, help="directory: cProfile of one timed run per query")
+    ap.add_argument("--no-cold", dest="cold", action="store_false",
+                    help="skip the first-run latency measurement (cold / warm on-disk kernel cache)")
     ap.add_argument("--stage-times", action="store_true",
                     help="one extra run per query with device syncs at stage boundaries: per-stage seconds in the JSON")
     a = ap.parse_args()
@@ -83,6 +99,16 @@ def main():
               flush=True)
         for q in queries:
             fn = tpch.QUERIES[q]
+            first = {}
+            if a.cold:
+                os.environ["NSDB_JIT_CACHE"] = tempfile.mkdtemp(prefix=f"nsdb_jit_{q}_")   # an empty disk cache
+                for tag in ("first_ms_cold", "first_ms_warm_disk"):
+                    _clear_process_caches(c)
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                    fn(c, "tpch")
+                    torch.cuda.synchronize()
+                    first[tag] = round((time.perf_counter() - t0) * 1e3, 2)
             got = fn(c, "tpch")                       # untimed first run
             ts = []
             for _ in range(a.rounds):
@@ -125,7 +151,7 @@ def main():
             med = statistics.median(ts)
             row = {"sf": sf, "query": q, "ms_median": round(med * 1e3, 2), "ms_min": round(min(ts) * 1e3, 2),
                    "lineitem_rows_per_s": round(nli / med, 1), "check_vs_pandas": ok,
-                   "pandas_s": None if frames is None else round(t_ref, 2)}
+                   "pandas_s": None if frames is None else round(t_ref, 2), **first}
             out["results"].append(row)
             print(json.dumps(row), flush=True)
             if stage_times is not None:

@@ -298,3 +298,26 @@ def test_lazy_take_device_and_values_gather_only_what_they_touch():
     assert first.tolist() == [0, 0, 0] and sum(dict.__contains__(lt, k) for k in src) == 1
     assert len(lt.values()) == 8 and [k for k, _ in lt.items()] == [f"c{i}" for i in range(8)]
     assert [v.tolist() for v in lt.values()][2] == [2, 6, 10]
+
+
+def test_stage_records_and_history_device_time_cpu(tmp_path):
+    """On the CPU a stage record carries no device time (no event pair), the tracer's device mode is inert, and the
+    history's job_stage table has the device_seconds column (NULL here)."""
+    from netsdb_amd.client import PDBClient
+    from netsdb_amd.models import tpch, tpch_gen
+    from netsdb_amd.utils.trace import Tracer
+
+    c = PDBClient(root=str(tmp_path))
+    tpch.load(c, "tpch", tpch_gen.generate_fast(0.001, seed=3))
+    sl = c.enable_self_learning()
+    tpch.QUERIES["q06"](c, "tpch")
+    st = sl.last_stats
+    assert st["stages"] and all("device_seconds" not in s for s in st["stages"])
+    assert st.device_times() == [None] * len(st["stages"])
+    cols = {r[1] for r in sl.db.conn.execute("PRAGMA table_info(job_stage)")}
+    assert "device_seconds" in cols and sl.db.flush_device_times() == 0
+    tr = Tracer(device_time=True)
+    with tr.span("x"):
+        pass
+    assert tr.resolve() == 0 and "device_us" not in tr.events[0]["args"]
+    tr.export_chrome(str(tmp_path / "t.json"))

@@ -72,6 +72,20 @@ def _scenarios(ctx, dev):
         j.set_input(1, ScanSet("LA_db", "B"))
         c.execute_computations(WriteSet("LA_db", "C_twice").set_input(L.LAMultiply2Aggregate().set_input(j)))
     res["twice"] = (B.to_tensor(c, "LA_db", "C_twice").float().cpu() - A @ Bm).abs().max().item()
+    # the ownership merge keeps a float64 panel in float64 and works band by band (several bands here)
+    c.create_set("LA_db", "C_f64", None, dense=True)
+    s64 = c.storage.get_set("LA_db", "C_f64")
+    s64.define(70, 50, 16, 16, dtype=torch.float64, device=dev)
+    vals = (1.0 + torch.arange(70 * 50, dtype=torch.float64) * 1e-13).reshape(70, 50).to(dev)
+    s64.matrix().copy_(vals)
+    old_band = c.engine.MERGE_BAND_BYTES
+    c.engine.MERGE_BAND_BYTES = 16 * 50 * 8 * 2        # two block rows per band: 3 bands for 5 block rows
+    try:
+        c.engine._merge_dense_output(s64, written=[(torch.tensor([0, 2, 4]), torch.tensor([1, 3, 0]))])
+    finally:
+        c.engine.MERGE_BAND_BYTES = old_band
+    res["merge_f64"] = (s64.matrix().cpu() - vals.cpu()).abs().max().item()
+    res["merge_f64_dtype"] = str(s64.matrix().dtype)
     # FF inference with row-partitioned inputs
     c2 = PDBClient(ctx=ctx, root=tempfile.mkdtemp(), device=dev)
     ff.load_model(c2, "ff", 64, 96, 32, 24, 16, 32, dtype=torch.float32, partition_inputs=True)
@@ -143,6 +157,7 @@ def _check(r, tol=1e-4):
     assert r["distributed"] is True and r["single"]["distributed"] is False
     # vs fp64 (tol: bf16 MFMA on the GPU), and vs the single-process run of the same scenario
     assert r["mul"] < tol and r["tmul"] < tol and r["twice"] < tol and r["ff"] < tol, r
+    assert r["merge_f64"] == 0.0 and r["merge_f64_dtype"] == "torch.float64", r["merge_f64"]
     same = 1e-5 if tol <= 1e-4 else 1e-2     # the GPU's split / chunk order may round differently in bf16
     assert torch.allclose(r["C_mul"], r["single"]["C_mul"], rtol=same, atol=same)
     assert torch.allclose(r["ff_out"], r["single"]["ff_out"], rtol=same, atol=same * 0.1)

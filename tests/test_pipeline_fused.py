@@ -73,9 +73,18 @@ def test_jit_sources_compile_cpu(monkeypatch):
     progs = list(PL._PROG_CACHE.values())
     assert len(progs) >= len(QUERIES) + len(FILTER_QUERIES), len(progs)
     h, hdr, seen = _ext.hip(), PL._jit_header(), set()
+    joins = 0
     for p in progs:
         kinds = [cc["kind"] for cc in p.cols]
         lates = [cc["late"] for cc in p.cols]
+        if p.jk_reg >= 0:                      # a fused join probe: the aggregate kernel only (jit_join_agg_body)
+            joins += 1
+            src = PL.jit_source(p, kinds, lates, "agg", p.key_reg, p.val_regs)
+            assert "jit_join_agg_body" in src and "brow[j]" in src
+            if src not in seen:
+                seen.add(src)
+                assert len(h.jit_compile(src, hdr)) > 1000
+            continue
         srcs = [PL.jit_source(p, kinds, lates, "mask")]
         if p.val_regs or p.key_reg >= 0:
             srcs.append(PL.jit_source(p, kinds, lates, "agg", p.key_reg, p.val_regs))
@@ -86,6 +95,7 @@ def test_jit_sources_compile_cpu(monkeypatch):
                 seen.add(src)
                 assert len(h.jit_compile(src, hdr)) > 1000
     assert len(seen) >= len(progs)
+    assert joins >= 2, joins                   # q12 and q14 probe their build tables inside the fused kernel
 
 
 class _Sel(SelectionComp):
@@ -393,3 +403,90 @@ def test_jit_every_opcode_and_column_kind_compiles_cpu():
             src = PL.jit_source(p, kinds, lates, kind, p.key_reg if kind == "agg" else -1,
                                 p.val_regs if kind == "agg" else ())
             assert len(h.jit_compile(src, hdr)) > 1000, (kind, lates)
+
+
+# ---------------------------------------------------------------------------------------------- fused join probes
+def _join_agg(c, probe, build, keys, pick, key_fn, val_fn, out, op="sum"):
+    """probe ⋈ build (tpch _EqJoin + _pick) -> _TreeGroupBy(key, Values): rows sorted by key."""
+    j = tpch._EqJoin(2, keys, tpch._pick(pick))
+    j.set_input(0, probe)
+    j.set_input(1, build)
+    agg = tpch._TreeGroupBy(key_fn, val_fn, tpch._rows_out(["a", "b"]), reduce_op=op)
+    if c.storage.has_set("tpch", out):
+        c.remove_set("tpch", out)
+    c.create_set("tpch", out, None)
+    c.execute_computations(WriteSet("tpch", out).set_input(agg.set_input(j)))
+    b = [x for x in c.get_set_batches("tpch", out) if x.n][0]
+    ks = b.columns["k0"]
+    ks = ks.tolist() if hasattr(ks, "tolist") else list(ks)
+    order = sorted(range(b.n), key=lambda i: ks[i])
+    vals = torch.stack([b.columns["a"].double().cpu(), b.columns["b"].double().cpu()], 1)
+    return [ks[i] for i in order], vals[torch.tensor(order)]
+
+
+JOIN_CASES = {
+    # build = supplier (the smaller side) on its REPEATED s_nationkey (CSR runs: several suppliers per nation), probe
+    # = customer; a build-side integer key, values from both sides
+    "repeated_build_keys": (
+        lambda db: ScanSet(db, "customer", tpch.Customer),
+        lambda db: ScanSet(db, "supplier", tpch.Supplier),
+        [(0, "c_nationkey", 1, "s_nationkey")], [["c_custkey", "c_acctbal"], ["s_acctbal", "s_nationkey"]],
+        lambda x: x.s_nationkey,
+        lambda x: Values(Select(x.s_acctbal > 0.0, x.s_acctbal, 0.0) + x.c_acctbal * 0.5, 1.0), "sum"),
+    # build = orders, probe = one week of lineitems (fused predicate before the probe); a key and a value from the
+    # build side (string key at the matched build rows)
+    "build_side_string_key": (
+        lambda db: tpch._TreeFilter(lambda x: (x.l_shipdate >= 19960101) & (x.l_shipdate < 19960301)).set_input(
+            ScanSet(db, "lineitem", tpch.LineItem)),
+        lambda db: ScanSet(db, "orders", tpch.Order),
+        [(0, "l_orderkey", 1, "o_orderkey")], [["l_quantity"], ["o_orderstatus", "o_totalprice"]],
+        lambda x: x.o_orderstatus, lambda x: Values(x.l_quantity * 2.0, Select(x.o_totalprice > 100000.0, 1.0, 0.0)),
+        "sum"),
+    # build = part (unique p_partkey), probe = a quarter of lineitems; a probe-side key, min of a mixed expression
+    "unique_build_keys_min": (
+        lambda db: tpch._TreeFilter(lambda x: (x.l_shipdate >= 19950101) & (x.l_shipdate < 19950401)).set_input(
+            ScanSet(db, "lineitem", tpch.LineItem)),
+        lambda db: ScanSet(db, "part", tpch.Part),
+        [(0, "l_partkey", 1, "p_partkey")], [["l_linenumber", "l_extendedprice"], ["p_size", "p_retailprice"]],
+        lambda x: x.l_linenumber, lambda x: Values(x.l_extendedprice - x.p_retailprice, x.p_size * 1.0), "min"),
+}
+
+
+def _join_case(c, case):
+    probe, build, keys, pick, key_fn, val_fn, op = JOIN_CASES[case]
+    return _join_agg(c, probe("tpch"), build("tpch"), keys, pick, key_fn, val_fn, f"j_{case}", op)
+
+
+@pytest.mark.parametrize("case", sorted(JOIN_CASES))
+def test_fused_join_probe_cpu_interpreter(case, monkeypatch):
+    """A stage probing a build table inside the fused program (torch model of jit_join_agg_body): == the eager atoms."""
+    monkeypatch.setenv("NSDB_DEVICE_STRINGS", "1")
+    t = tpch_gen.generate_fast(0.003, seed=6)
+    c = _client("cpu", t)
+    eager = _join_case(c, case)
+    assert eager[0], "the case must produce groups"
+    monkeypatch.setattr(PL, "CPU_INTERPRETER", True)
+    j0 = c.engine.pipeline_stats.get("fused_join_batches", 0)
+    fused = _join_case(c, case)
+    assert c.engine.pipeline_stats.get("fused_join_batches", 0) > j0, c.engine.pipeline_stats
+    assert eager[0] == fused[0]
+    assert torch.allclose(eager[1], fused[1], rtol=1e-12, atol=1e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", sorted(JOIN_CASES))
+def test_fused_join_probe_gpu(case):
+    """The compiled join kernel (probe, CSR runs of repeated build keys, build-side gathers, post-join predicate)
+    against the eager probe / gather / group-by atoms on the same data."""
+    t = tpch_gen.generate_fast(0.05, seed=6)
+    c = _client("cuda:0", t)
+    c.engine.fused_pipelines = False
+    eager = _join_case(c, case)
+    c.engine.fused_pipelines = True
+    j0 = c.engine.pipeline_stats.get("fused_join_batches", 0)
+    f0 = PL.JIT_STATS["launches"]
+    fused = _join_case(c, case)
+    assert c.engine.pipeline_stats.get("fused_join_batches", 0) > j0, c.engine.pipeline_stats
+    assert PL.JIT_STATS["launches"] > f0
+    assert eager[0] == fused[0]
+    assert torch.allclose(eager[1], fused[1], rtol=1e-9, atol=1e-6)
