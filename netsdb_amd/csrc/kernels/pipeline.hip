@@ -810,7 +810,31 @@ void launch_agg(const PipeArgs& a, int grid, hipStream_t st) {
 
 }  // namespace nsdb_pipe
 
+namespace nsdb_pipe {
+// Emit regions (jit_emit_body) -> dense columns: workgroup w copies the cnt[w] rows its tile wrote, of every one of
+// the ne columns, to dst at off[w] (the exclusive scan of cnt). Reads and writes only the emitted rows.
+__global__ void __launch_bounds__(NTHR) emit_compact_kernel(const unsigned long long* __restrict__ src, int ne,
+                                                            long long ostride, long long cap,
+                                                            const unsigned* __restrict__ cnt,
+                                                            const long long* __restrict__ off,
+                                                            unsigned long long* __restrict__ dst, long long total) {
+  const long long w = blockIdx.x;
+  const long long c = cnt[w], o = off[w];
+  for (int e = 0; e < ne; ++e)
+    for (long long i = threadIdx.x; i < c; i += NTHR) dst[e * total + o + i] = src[e * ostride + w * cap + i];
+}
+}  // namespace nsdb_pipe
+
 extern "C" {
+
+int nsdb_pipe_emit_compact(const unsigned long long* src, int ne, long long ostride, long long cap, const unsigned* cnt,
+                           const long long* off, long long tiles, unsigned long long* dst, long long total,
+                           hipStream_t st) {
+  if (tiles <= 0 || ne <= 0 || total < 0) return total == 0 ? 0 : -1;
+  hipLaunchKernelGGL(nsdb_pipe::emit_compact_kernel, dim3((unsigned)tiles), dim3(nsdb_pipe::NTHR), 0, st, src, ne,
+                     ostride, cap, cnt, off, dst, total);
+  return (int)hipGetLastError();
+}
 
 int nsdb_pipe_sizes(int* out) {
   out[0] = nsdb_pipe::MAXINS;

@@ -19,6 +19,9 @@ int nsdb_pipe_sizes(int* out);
 int nsdb_pipe_agg(const void* args, int grid, hipStream_t st);
 int nsdb_pipe_mask(const void* args, unsigned char* mask, int grid, hipStream_t st);
 int nsdb_pipe_init(unsigned long long* table, int op, hipStream_t st);
+int nsdb_pipe_emit_compact(const unsigned long long* src, int ne, long long ostride, long long cap, const unsigned* cnt,
+                           const long long* off, long long tiles, unsigned long long* dst, long long total,
+                           hipStream_t st);
 }
 
 namespace {
@@ -389,6 +392,73 @@ torch::Tensor pipe_agg(torch::Tensor prog, int64_t nins_a, ColList cols, torch::
   return table;
 }
 
+// High-cardinality form of a fused stage (pipeline_core.h jit_emit_body, compiled kernels only): every kept (and
+// matched) row's ne emitted registers. Workgroup w writes the rows of input tile w into its region of `cap` rows;
+// the regions are then compacted into dense columns. Returns (dst int64 [ne, rows], status int64 [2] on the host:
+// overflow flag, rows that passed segment A). One host read (the status and the row total together).
+std::vector<torch::Tensor> pipe_emit(torch::Tensor prog, int64_t nins_a, ColList cols, torch::Tensor lit, int64_t n,
+                                     int64_t keep_reg, int64_t key_reg, std::vector<int64_t> val_regs,
+                                     std::vector<int64_t> kpool, int64_t jit, int64_t jit_nreg, int64_t jit_rows,
+                                     int64_t ne, int64_t tile_rows, int64_t cap, c10::optional<torch::Tensor> jtab,
+                                     c10::optional<torch::Tensor> jperm, int64_t bn) {
+  const int NTHR = sizes(7);
+  PipeArgs a;
+  const bool join = jtab.has_value() && jtab->defined();
+  fill_args(a, prog, nins_a, cols, lit, n, keep_reg, key_reg, val_regs, 0, kpool, join ? bn : -1);
+  TORCH_CHECK(jit != 0 && a.nreg == jit_nreg && jit_rows >= 1 && jit_rows <= 16,
+              "pipe_emit: needs its compiled kernel (", jit_nreg, " registers, the program uses ", a.nreg, ")");
+  TORCH_CHECK(ne >= 1 && ne <= 16, "pipe_emit: 1..16 emitted registers");
+  TORCH_CHECK(tile_rows >= NTHR * jit_rows && tile_rows % (NTHR * jit_rows) == 0 && cap >= 1 && cap <= tile_rows * 64,
+              "pipe_emit: tile rows must be whole row blocks, cap in [1, 64 * tile rows]");
+  if (join) {
+    const auto& T = *jtab;
+    TORCH_CHECK(T.is_cuda() && T.scalar_type() == torch::kInt64 && T.dim() == 2 && T.size(1) == 2 && T.is_contiguous(),
+                "pipe_emit: join table must be join_build's int64 [cap + 1, 2] device tensor");
+    const int64_t jcap = T.size(0) - 1;
+    TORCH_CHECK(jcap >= 1024 && (jcap & (jcap - 1)) == 0, "pipe_emit: malformed join table");
+    TORCH_CHECK(jperm.has_value() && jperm->defined() && jperm->is_cuda() && jperm->scalar_type() == torch::kInt64 &&
+                    jperm->is_contiguous() && jperm->numel() >= bn && bn >= 0 && bn < (int64_t(1) << 29),
+                "pipe_emit: join permutation [build rows] int64 expected");
+    a.jtab = reinterpret_cast<const unsigned long long*>(T.data_ptr<int64_t>());
+    a.jperm = reinterpret_cast<const long long*>(jperm->data_ptr<int64_t>());
+    a.jmask = (unsigned long long)(jcap - 1);
+    a.bn = bn;
+  }
+  auto i64 = lit.options().dtype(torch::kInt64);
+  const int64_t tiles = std::max<int64_t>(1, (n + tile_rows - 1) / tile_rows);
+  TORCH_CHECK(tiles < (int64_t(1) << 31), "pipe_emit: too many tiles");
+  const int64_t ostride = tiles * cap;
+  auto out = torch::empty({ne, ostride}, i64);
+  auto cnt = torch::empty({tiles}, lit.options().dtype(torch::kInt32));
+  auto status = torch::zeros({2}, i64);
+  a.table = reinterpret_cast<unsigned long long*>(status.data_ptr<int64_t>());
+  hipStream_t st = c10::hip::getCurrentHIPStream().stream();
+  unsigned long long* op = reinterpret_cast<unsigned long long*>(out.data_ptr<int64_t>());
+  long long tr = tile_rows, cp = cap, os = ostride;
+  unsigned* cp_cnt = reinterpret_cast<unsigned*>(cnt.data_ptr<int>());
+  void* params[] = {&a, &op, &tr, &cp, &os, &cp_cnt};
+  if (n > 0) {
+    TORCH_CHECK(hipModuleLaunchKernel(reinterpret_cast<hipFunction_t>(jit), (unsigned)tiles, 1, 1, NTHR, 1, 1, 0, st,
+                                      params, nullptr) == hipSuccess,
+                "pipe_emit: compiled kernel launch failed");
+  } else {
+    cnt.zero_();
+  }
+  auto incl = torch::cumsum(cnt, 0, torch::kInt64);
+  auto head = torch::cat({status, incl.narrow(0, tiles - 1, 1)}).to(torch::kCPU);   // the one host read
+  auto hv = head.accessor<int64_t, 1>();
+  const int64_t total = hv[2];
+  if (hv[0] != 0) return {torch::empty({ne, 0}, i64), head.narrow(0, 0, 2)};
+  auto off = incl.sub_(cnt.to(torch::kInt64));
+  auto dst = torch::empty({ne, total}, i64);
+  if (total > 0)
+    TORCH_CHECK(nsdb_pipe_emit_compact(op, (int)ne, ostride, cap, cp_cnt,
+                                       reinterpret_cast<const long long*>(off.data_ptr<int64_t>()), tiles,
+                                       reinterpret_cast<unsigned long long*>(dst.data_ptr<int64_t>()), total, st) == 0,
+                "pipe_emit: compaction launch failed");
+  return {dst, head.narrow(0, 0, 2)};
+}
+
 // The predicate program's keep flag per row (uint8 [n]); key / values unused.
 torch::Tensor pipe_mask(torch::Tensor prog, ColList cols, torch::Tensor lit, int64_t n, int64_t keep_reg, int64_t tile,
                         std::vector<int64_t> kpool, int64_t jit, int64_t jit_nreg, int64_t jit_rows) {
@@ -438,6 +508,14 @@ void register_pipeline(pybind11::module& m) {
         pybind11::arg("max_wg") = 0, pybind11::arg("tile") = -1, pybind11::arg("kpool") = std::vector<int64_t>(),
         pybind11::arg("jit") = 0, pybind11::arg("jit_nreg") = 0, pybind11::arg("jit_rows") = 0,
         pybind11::arg("jtab") = pybind11::none(), pybind11::arg("jperm") = pybind11::none(), pybind11::arg("bn") = -1);
+  m.def("pipe_emit", &pipe_emit,
+        "fused stage, high-cardinality form: every kept (matched) row's emitted registers as dense int64 columns "
+        "[ne, rows], and the host status (overflow, rows through segment A)",
+        pybind11::arg("prog"), pybind11::arg("nins_a"), pybind11::arg("cols"), pybind11::arg("lit"), pybind11::arg("n"),
+        pybind11::arg("keep_reg"), pybind11::arg("key_reg"), pybind11::arg("val_regs"), pybind11::arg("kpool"),
+        pybind11::arg("jit"), pybind11::arg("jit_nreg"), pybind11::arg("jit_rows"), pybind11::arg("ne"),
+        pybind11::arg("tile_rows"), pybind11::arg("cap"), pybind11::arg("jtab") = pybind11::none(),
+        pybind11::arg("jperm") = pybind11::none(), pybind11::arg("bn") = -1);
   m.def("jit_compile", &jit_compile, "hiprtc compile of a generated pipeline kernel source (gfx950 code object)",
         pybind11::arg("src"), pybind11::arg("header"));
   m.def("jit_version", &jit_version, "hiprtc version of the run-time compiler (code-object cache key)");

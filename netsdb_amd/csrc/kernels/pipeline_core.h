@@ -478,6 +478,147 @@ __device__ __forceinline__ void jit_join_agg_body(const PipeArgs& a) {
   agg_flush<F>(a, sk, sv, used, ovf, (unsigned long long)kept, tk, tv, &s_ovf, &s_kept, init);
 }
 
+// ---------------------------------------------------------------- emit: (key parts, values) rows for the sink
+// The high-cardinality form of a fused stage (more groups than GCAP): instead of pre-aggregating, every kept (and,
+// with a join, matched) row writes its P::NE emitted registers (key parts, then values) straight from registers —
+// no filter mask, compaction, key / value gathers or value-expression temporaries in HBM. The sink's device group-by
+// (relops) then reduces them. Workgroup w owns the rows [w * tile_rows, (w + 1) * tile_rows) and writes its rows
+// densely into ITS region [w * cap, (w + 1) * cap) of every output column (out + c * ostride): no global atomics,
+// deterministic placement; tile_cnt[w] = rows written, status[0] |= 1 when a region overflowed (the host then runs
+// the batch eagerly). Per block of NTHR * ROWS rows: a count pass, a workgroup exclusive scan in LDS, a write pass
+// (segment B is re-run for the write only when some lane of the wave walked more than one match).
+template <typename P>
+__device__ __forceinline__ void jit_emit_body(const PipeArgs& a, unsigned long long* __restrict__ out, long long tile_rows,
+                                              long long cap, long long ostride, unsigned* __restrict__ tile_cnt) {
+  constexpr int NR = P::NR, ROWS = P::ROWS, NE = P::NE;
+  __shared__ unsigned s_scan[NTHR / 64];
+  __shared__ unsigned long long s_kept;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const long long t0 = (long long)blockIdx.x * tile_rows;
+  const long long t1 = t0 + tile_rows < a.n ? t0 + tile_rows : a.n;
+  unsigned long long* region = out + (long long)blockIdx.x * cap;
+  if (tid == 0) s_kept = 0;
+  u64 R[ROWS][NR];
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j)
+#pragma unroll
+    for (int r = 0; r < NR; ++r) R[j][r] = 0ull;
+  long long written = 0;
+  unsigned kept = 0;
+  bool ovf = false;
+  for (long long base = t0; base < t1; base += (long long)NTHR * ROWS) {
+    long long row[ROWS], brow[ROWS];
+    bool inr[ROWS], keep[ROWS], act[ROWS];
+    unsigned cnt[ROWS], pay[ROWS];
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      row[j] = base + (long long)j * NTHR + tid;
+      inr[j] = row[j] < t1;
+    }
+    if (base + (long long)NTHR * ROWS <= t1) P::template load<false, true>(a, row, inr, R);
+    else P::template load<false, false>(a, row, inr, R);
+    P::run_a(a, R);
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      keep[j] = inr[j] && P::keep(R[j]);
+      kept += keep[j] ? 1u : 0u;
+      cnt[j] = keep[j] ? 1u : 0u;
+      pay[j] = 0;
+      if constexpr (P::JOIN) {
+        cnt[j] = 0;
+        if (keep[j]) join_find(a, (long long)R[j][P::JK], cnt[j], pay[j]);
+        keep[j] = keep[j] && cnt[j] != 0;
+      }
+      any |= keep[j];
+    }
+    const bool wave_any = __builtin_amdgcn_ballot_w64(any) != 0ull;
+    if (wave_any) P::template load<true, false>(a, row, keep, R);
+    // count pass
+    unsigned e = 0, trips = 0;
+    if (wave_any) {
+      for (unsigned t = 0;; ++t) {
+        bool more = false;
+#pragma unroll
+        for (int j = 0; j < ROWS; ++j) {
+          act[j] = keep[j] && t < cnt[j];
+          brow[j] = !act[j] ? 0ll : (!P::JOIN || cnt[j] == 1u ? (long long)pay[j] : a.jperm[(long long)pay[j] + t]);
+          more |= act[j];
+        }
+        if (!__builtin_amdgcn_ballot_w64(more)) break;
+        ++trips;
+        if constexpr (P::JOIN) P::loadb(a, brow, act, R);
+        P::run_b(a, R);
+#pragma unroll
+        for (int j = 0; j < ROWS; ++j) e += (act[j] && P::keep2(R[j])) ? 1u : 0u;
+      }
+    }
+    // workgroup exclusive scan of e
+    unsigned x = e;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const unsigned y = __shfl_up(x, d, 64);
+      if (lane >= d) x += y;
+    }
+    if (lane == 63) s_scan[wave] = x;
+    __syncthreads();
+    unsigned before = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < NTHR / 64; ++w) {
+      const unsigned v = s_scan[w];
+      before += w < wave ? v : 0u;
+      total += v;
+    }
+    long long o = written + before + x - e;
+    if (written + total > cap) ovf = true;
+    // write pass
+    if (e != 0 && !ovf) {
+      if (trips <= 1) {              // the registers still hold the single match's segment B
+#pragma unroll
+        for (int j = 0; j < ROWS; ++j) {
+          if (!keep[j] || !P::keep2(R[j])) continue;     // keep[j] => exactly one match (trips <= 1)
+          u64 w[NE];
+          P::emit(R[j], w);
+#pragma unroll
+          for (int c = 0; c < NE; ++c) region[c * ostride + o] = w[c];
+          ++o;
+        }
+      } else {
+        for (unsigned t = 0;; ++t) {
+          bool more = false;
+#pragma unroll
+          for (int j = 0; j < ROWS; ++j) {
+            act[j] = keep[j] && t < cnt[j];
+            brow[j] = !act[j] ? 0ll : (!P::JOIN || cnt[j] == 1u ? (long long)pay[j] : a.jperm[(long long)pay[j] + t]);
+            more |= act[j];
+          }
+          if (!__builtin_amdgcn_ballot_w64(more)) break;
+          if constexpr (P::JOIN) P::loadb(a, brow, act, R);
+          P::run_b(a, R);
+#pragma unroll
+          for (int j = 0; j < ROWS; ++j) {
+            if (!act[j] || !P::keep2(R[j])) continue;
+            u64 w[NE];
+            P::emit(R[j], w);
+#pragma unroll
+            for (int c = 0; c < NE; ++c) region[c * ostride + o] = w[c];
+            ++o;
+          }
+        }
+      }
+    }
+    written += total;
+    __syncthreads();                 // s_scan is rewritten by the next block
+  }
+  atomicAdd(&s_kept, (unsigned long long)kept);
+  __syncthreads();
+  if (tid == 0) {
+    tile_cnt[blockIdx.x] = ovf ? 0u : (unsigned)written;
+    if (ovf) atomicOr(a.table, 1ull);
+    atomicAdd(a.table + 1, s_kept);
+  }
+}
+
 // Filter only: keep flag per row (every column early, the whole program in run_a).
 template <typename P>
 __device__ __forceinline__ void jit_mask_body(const PipeArgs& a, unsigned char* __restrict__ mask) {

@@ -187,10 +187,14 @@ class QueryEngine:
                 self._plan_cache.pop(next(iter(self._plan_cache)))
         return atoms, plan.computations, plan.tcap, gkey
 
+    def _capturing(self) -> bool:
+        """A HIP-graph capture is recording on this thread's stream (event queries / timing records must wait)."""
+        return self.ctx.device.type == "cuda" and torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
     def _device_timed(self) -> bool:
         """Stage device timing on: a GPU engine outside a HIP-graph capture (a captured job replays no host code)."""
-        return (self.device_timing and self.ctx.device.type == "cuda" and torch.cuda.is_available()
-                and not torch.cuda.is_current_stream_capturing())
+        return self.device_timing and self.ctx.device.type == "cuda" and torch.cuda.is_available() and \
+            not self._capturing()
 
     def _timed_stage(self, st, state, stats, job_name):
         sync = STAGE_SYNC and torch.cuda.is_available()
@@ -242,7 +246,7 @@ class QueryEngine:
         t0 = time.perf_counter()
         stats = JobStats(job=job_name, stages=[])
         stats._timer = self.device_timer
-        if self.device_timer.pending:
+        if self.device_timer.pending and not self._capturing():
             self.device_timer.resolve(block=False)      # earlier jobs' stage times whose events have completed
         sinks = list(sinks)
         if self.fusion and not pre_compile:       # (fusion executes the matched kernels: not on pre-compile)
@@ -440,6 +444,15 @@ class QueryEngine:
                         b = self._apply_atom(o, b, state)
                     yield b
                     continue
+            if r is not None and getattr(r, "emitted", False):
+                # the stage's emitted (key parts, values) rows: device columns, reduced by the sink's group-by
+                if fplan.join is not None:
+                    self.pipeline_stats["fused_join_batches"] = self.pipeline_stats.get("fused_join_batches", 0) + 1
+                self.pipeline_stats["emitted_batches"] = self.pipeline_stats.get("emitted_batches", 0) + 1
+                used = True
+                self.pipeline_stats["fused_batches"] += 1
+                yield r
+                continue
             if r is not None:
                 if fplan.join is not None and not fplan.disabled:
                     self.pipeline_stats["fused_join_batches"] = self.pipeline_stats.get("fused_join_batches", 0) + 1

@@ -371,6 +371,10 @@ class Program:
         self.nval = 0
         self.val_shape = None
         self.jk_reg = -1                      # fused join: the probe key's column register
+        self.mode = "agg"                     # "emit": high-cardinality form (every row's key parts and values out)
+        self.emit_keys: List[tuple] = []      # emit: (register, "int" | "float" | "str", dtype | L) per key part
+        self.emit_keys_const = None           # emit: a literal key (no key registers)
+        self.key_tuple = False
         self.keep2_reg = -1                   # fused join: the post-join predicate (per matched build row)
 
     # registers
@@ -448,8 +452,9 @@ def _path(e: E) -> tuple:
 
 
 class _Compiler:
-    def __init__(self, plan: StagePlan, batch: RecordBatch, build: Optional[RecordBatch] = None):
+    def __init__(self, plan: StagePlan, batch: RecordBatch, build: Optional[RecordBatch] = None, mode: str = "agg"):
         self.plan, self.batch, self.build = plan, batch, build
+        self.mode = mode                  # "agg": pre-aggregate in the kernel's tables; "emit": every row out
         if plan.join is not None and build is None:
             raise Unfusable("join without a build table")
         self.p = Program()
@@ -590,7 +595,25 @@ class _Compiler:
                 r = d
             p.keep2_reg = r
             p.pinned.add(r)                            # read after the key and values are computed
-        p.key_reg = self._gen_key(keys)
+        p.mode = self.mode
+        if self.mode == "emit":
+            # key parts leave as they are in their column registers (any mix of integer, float and short-string
+            # columns: no packing into one 63-bit word), decoded on the host side of the launch
+            p.key_reg = -1
+            p.emit_keys = []
+            k = plan.key
+            if not keys:
+                p.emit_keys_const = k.val
+            for e in keys:
+                obj = self._res(e)
+                slot = p.col_index[(_path(e), self._key_usage(e))]
+                if isinstance(obj, StringColumn):
+                    p.emit_keys.append((slot, "str", p.cols[slot]["L"]))
+                else:
+                    p.emit_keys.append((slot, "float" if obj.is_floating_point() else "int", obj.dtype))
+            p.key_tuple = k.kind == "keys"
+        else:
+            p.key_reg = self._gen_key(keys)
         if len(vals) > FMAX:
             raise Unfusable("values")
         for v in vals:
@@ -892,14 +915,14 @@ def _schema_key(batch: RecordBatch) -> tuple:
     return tuple(out)
 
 
-def _compile_cached(plan: StagePlan, batch: RecordBatch) -> Program:
-    """The stage's program for this batch: compiled once per (stage expressions, selectivity mode, column kinds) and
-    re-bound to the batch's columns afterwards (repeated queries skip the compiler)."""
+def _compile_cached(plan: StagePlan, batch: RecordBatch, mode: str = "agg") -> Program:
+    """The stage's program for this batch: compiled once per (stage expressions, selectivity mode, column kinds, agg /
+    emit form) and re-bound to the batch's columns afterwards (repeated queries skip the compiler)."""
     build = plan.build_batch()
     if plan.join is not None and build is None:
         raise Unfusable("the join's build side is not an in-memory table")
     key = (plan.sig, _SEL_EST.get(plan.sig, 0.0) < LATE_MAX_SEL, _schema_key(batch),
-           _schema_key(build) if build is not None else None)
+           _schema_key(build) if build is not None else None, mode)
     hit = _PROG_CACHE.get(key)
     if hit is not None:
         p = Program.__new__(Program)
@@ -911,8 +934,8 @@ def _compile_cached(plan: StagePlan, batch: RecordBatch) -> Program:
         # reduction per column) and compile afresh when a row is longer than L.
         if all(c["kind"] != C_SCODE or c["obj"].max_len() <= c["L"] for c in p.cols):
             return p
-        return _Compiler(plan, batch, build).compile()
-    p = _Compiler(plan, batch, build).compile()
+        return _Compiler(plan, batch, build, mode).compile()
+    p = _Compiler(plan, batch, build, mode).compile()
     _prog_tensors(p, batch.device)              # built once here: every cached copy shares them
     if len(_PROG_CACHE) >= _PROG_CACHE_MAX:
         _PROG_CACHE.pop(next(iter(_PROG_CACHE)))
@@ -920,18 +943,31 @@ def _compile_cached(plan: StagePlan, batch: RecordBatch) -> Program:
     return p
 
 
+_EMIT_SIGS: Dict[tuple, bool] = {}           # stage signatures whose groups overflowed the kernel's tables
+_KEY_SHAPE = __import__("re").compile(r"float key|mixed key|key too wide")
+EMIT = os.environ.get("NSDB_PIPE_EMIT", "1") != "0"
+
+
 def run_batch(plan: StagePlan, batch: RecordBatch) -> Optional[RecordBatch]:
-    """One fused launch over ``batch``: the pre-aggregated {kcol: keys, vcol: values} batch, or None when this batch
-    must take the eager atoms (columns the kernel cannot read, more groups than its tables)."""
+    """One fused launch over ``batch``: the pre-aggregated {kcol: keys, vcol: values} batch; for a stage with more
+    groups than the kernel's tables (seen once, remembered per stage signature) the emitted, not yet aggregated
+    {kcol, vcol} rows of every kept row (``batch.emitted``, device columns for the sink's group-by); or None when this
+    batch must take the eager atoms (columns the kernel cannot read, no compiled kernels for the emitted form)."""
     if plan.disabled or batch.n == 0:
         return None
     dev = batch.device
     on_gpu = dev.type == "cuda" and _ext.hip() is not None and hasattr(_ext.hip(), "pipe_agg")
     if not on_gpu and not (CPU_INTERPRETER and dev.type == "cpu"):
         return None
+    if EMIT and _EMIT_SIGS.get(plan.sig):
+        return _run_emit(plan, batch, on_gpu)
     try:
         prog = _compile_cached(plan, batch)
     except Unfusable as e:
+        if EMIT and _KEY_SHAPE.search(str(e)):
+            # a key the kernel's one-word table cannot hold (float, mixed or too wide for one word): emitted form
+            _EMIT_SIGS[plan.sig] = True
+            return _run_emit(plan, batch, on_gpu)
         plan.disabled = True
         plan.reason = str(e)
         return None
@@ -947,7 +983,12 @@ def run_batch(plan: StagePlan, batch: RecordBatch) -> Optional[RecordBatch]:
     else:
         parts = interpret(prog, batch.n, plan.op)
     if parts is None:
-        plan.disabled = True            # more groups than the kernel's tables hold: this stage runs eagerly
+        # more groups than the kernel's tables hold: the emitted form (every row's key parts and values straight from
+        # registers into the sink's group-by) for this and every later run of the stage, else the eager atoms
+        if EMIT:
+            _EMIT_SIGS[plan.sig] = True
+            return _run_emit(plan, batch, on_gpu)
+        plan.disabled = True
         return None
     keys, vals = parts                  # host tensors (a few rows): decoded on the host
     plan.stats["fused_batches"] += 1
@@ -955,6 +996,80 @@ def run_batch(plan: StagePlan, batch: RecordBatch) -> Optional[RecordBatch]:
     if getattr(plan, "host_out", False):
         return RecordBatch({plan.kcol: kc, plan.vcol: vc}, int(keys.numel()))     # the sink reduces on the host
     return RecordBatch({plan.kcol: _to_dev(kc, dev), plan.vcol: _to_dev(vc, dev)}, int(keys.numel()))
+
+
+EMIT_TILE_BLOCKS = 16                         # row blocks (NTHR x ROWS rows) per emit tile
+
+
+class EmittedBatch(RecordBatch):
+    """A fused launch's emitted rows (key parts, values) — not pre-aggregated: the sink's group-by reduces them."""
+
+    __slots__ = ()
+    emitted = True
+
+
+def _run_emit(plan: StagePlan, batch: RecordBatch, on_gpu: bool) -> Optional[RecordBatch]:
+    try:
+        prog = _compile_cached(plan, batch, "emit")
+        if on_gpu:
+            got = _launch_emit(prog, batch.n, batch.device, plan)
+        else:
+            got = interpret_emit(prog, batch.n, plan)
+    except Unfusable as e:
+        plan.disabled = True
+        plan.reason = str(e)
+        return None
+    if got is None:
+        return None                     # an emit region overflowed (many matches per probe row): eager atoms
+    words, m = got
+    plan.stats["fused_batches"] += 1
+    plan.stats["emitted_rows"] = plan.stats.get("emitted_rows", 0) + m
+    nk = len(prog.emit_keys)
+    parts = []
+    for i, (_reg, kind, info) in enumerate(prog.emit_keys):
+        w = words[i]
+        if kind == "int":
+            parts.append(w.to(info) if info != torch.int64 else w)
+        elif kind == "float":
+            parts.append(w.view(torch.float64).to(info))
+        else:
+            parts.append(StringColumn.from_short_codes(w, info))
+    if nk == 0:
+        v = prog.emit_keys_const
+        key = torch.full((m,), v, dtype=torch.float64 if isinstance(v, float) else torch.int64, device=words.device)
+    else:
+        key = tuple(parts) if prog.key_tuple or nk > 1 else parts[0]
+    vals = words[nk:].view(torch.float64).t()        # [rows, F] column-major: the group-by reads it in place
+    if prog.val_shape != "row":
+        vals = vals[:, 0].contiguous()
+    return EmittedBatch({plan.kcol: key, plan.vcol: vals}, m)
+
+
+def _launch_emit(prog: Program, n: int, dev, plan: StagePlan):
+    """The emitted form's launch: (int64 words [ne, rows] on the device, rows), or None on a region overflow."""
+    h = _ext.hip()
+    if not hasattr(h, "pipe_emit"):
+        raise Unfusable("no emit kernels in this build")
+    ins, lit = _prog_tensors(prog, dev)
+    cargs = _col_args(prog, dev)
+    jtab = jperm = None
+    bn = -1
+    if plan.join is not None:
+        jtab, jperm, bn = _join_table(plan, dev)
+    jit = _jit_for(prog, cargs, "emit", -1, prog.val_regs, dev)
+    if jit is None:
+        raise Unfusable("the emitted form needs the compiled kernels")
+    fn, jnreg, jrows = jit
+    ne = len(prog.emit_keys) + len(prog.val_regs)
+    tile = 256 * jrows * EMIT_TILE_BLOCKS
+    cap = tile * (2 if plan.join is not None else 1)
+    words, status = h.pipe_emit(ins, prog.nins_a, cargs, lit, n, prog.keep_reg, -1, prog.val_regs, prog.kpool, fn,
+                                jnreg, jrows, max(1, ne), tile, cap, jtab, jperm, bn)
+    if int(status[0]) != 0:
+        return None
+    if n:
+        _SEL_EST[plan.sig] = int(status[1]) / n
+    return words, int(words.shape[1])
 
 
 def _to_dev(x, dev):
@@ -1120,10 +1235,13 @@ def _jit_loads(kinds, lates, late) -> List[str]:
 
 
 def jit_source(prog: Program, kinds, lates, kind: str, key_reg: int = -1, val_regs=(), rows: int = JIT_ROWS) -> str:
-    """The C++ source of the compiled kernel of ``prog`` (``kind`` "agg" or "mask") over columns of these kinds."""
+    """The C++ source of the compiled kernel of ``prog`` (``kind`` "agg", "emit" or "mask") over columns of these
+    kinds. "emit" writes every kept row's key-part registers (prog.emit_keys) and value registers."""
     nreg = program_nreg(prog, len(kinds), key_reg, val_regs)
     F = max(1, len(val_regs))
-    nins_a = prog.nins_a if kind == "agg" else len(prog.ins)
+    staged = kind in ("agg", "emit")                 # segment A / late columns / segment B split
+    nins_a = prog.nins_a if staged else len(prog.ins)
+    emit_regs = [k[0] for k in getattr(prog, "emit_keys", [])] + list(val_regs)
 
     def seg(lo, hi):
         body = [t for pc in range(lo, hi) if (t := _jit_ins(pc, prog.ins[pc])) is not None]
@@ -1132,10 +1250,10 @@ def jit_source(prog: Program, kinds, lates, kind: str, key_reg: int = -1, val_re
         return ("#pragma unroll\n    for (int j = 0; j < ROWS; ++j) {\n      u64* r = R[j];\n"
                 + "".join(f"      {t}\n" for t in body) + "    }")
 
-    join = kind == "agg" and getattr(prog, "jk_reg", -1) >= 0
+    join = staged and getattr(prog, "jk_reg", -1) >= 0
 
     def loads(late):
-        ls = _jit_loads(kinds, [lt if kind == "agg" else 0 for lt in lates], late)
+        ls = _jit_loads(kinds, [lt if staged else 0 for lt in lates], late)
         idx = "brow" if late == 2 else "row"
         return "\n".join(ls) if ls else f"    (void)a; (void){idx}; (void)m; (void)R;"
 
@@ -1144,15 +1262,24 @@ def jit_source(prog: Program, kinds, lates, kind: str, key_reg: int = -1, val_re
     keep2 = f"r[{prog.keep2_reg}] != 0ull" if join and getattr(prog, "keep2_reg", -1) >= 0 else "true"
     key = "0ll" if key_reg < 0 else f"(long long)r[{key_reg}]"
     body = "jit_join_agg_body" if join else "jit_agg_body"
-    entry = ("extern \"C\" __global__ void __launch_bounds__(nsdb_pipe::NTHR) nsdb_jit_agg(const nsdb_pipe::PipeArgs a) {\n"
-             f"  nsdb_pipe::{body}<nsdb_pipe::JitProg>(a);\n}}\n" if kind == "agg" else
-             "extern \"C\" __global__ void __launch_bounds__(nsdb_pipe::NTHR) nsdb_jit_mask(const nsdb_pipe::PipeArgs a, "
-             "unsigned char* mask) {\n  nsdb_pipe::jit_mask_body<nsdb_pipe::JitProg>(a, mask);\n}\n")
+    if kind == "agg":
+        entry = ("extern \"C\" __global__ void __launch_bounds__(nsdb_pipe::NTHR) nsdb_jit_agg(const nsdb_pipe::PipeArgs a) {\n"
+                 f"  nsdb_pipe::{body}<nsdb_pipe::JitProg>(a);\n}}\n")
+    elif kind == "emit":
+        entry = ("extern \"C\" __global__ void __launch_bounds__(nsdb_pipe::NTHR) nsdb_jit_emit(const nsdb_pipe::PipeArgs a, "
+                 "unsigned long long* out, long long tile_rows, long long cap, long long ostride, unsigned* tile_cnt) {\n"
+                 "  nsdb_pipe::jit_emit_body<nsdb_pipe::JitProg>(a, out, tile_rows, cap, ostride, tile_cnt);\n}\n")
+    else:
+        entry = ("extern \"C\" __global__ void __launch_bounds__(nsdb_pipe::NTHR) nsdb_jit_mask(const nsdb_pipe::PipeArgs a, "
+                 "unsigned char* mask) {\n  nsdb_pipe::jit_mask_body<nsdb_pipe::JitProg>(a, mask);\n}\n")
+    emit = "".join(f"    w[{i}] = r[{reg}];\n" for i, reg in enumerate(emit_regs)) or "    w[0] = 0ull; (void)r;\n"
     return f"""// generated by netsdb_amd.execution.pipeline.jit_source ({kind})
 #include "pipeline_core.h"
 namespace nsdb_pipe {{
 struct JitProg {{
   static constexpr int F = {F}, NR = {nreg}, ROWS = {rows}, JK = {max(0, getattr(prog, "jk_reg", -1))};
+  static constexpr int NE = {max(1, len(emit_regs))};
+  static constexpr bool JOIN = {"true" if join else "false"};
   template <bool LATE, bool FULL>
   __device__ static __forceinline__ void load(const PipeArgs& a, const long long (&row)[ROWS], const bool (&m)[ROWS],
                                               u64 (&R)[ROWS][NR]) {{
@@ -1177,6 +1304,8 @@ struct JitProg {{
   __device__ static __forceinline__ long long key(const u64 (&r)[NR]) {{ (void)r; return {key}; }}
   __device__ static __forceinline__ void vals(const u64 (&r)[NR], double (&v)[F]) {{
 {vals}  }}
+  __device__ static __forceinline__ void emit(const u64 (&r)[NR], u64 (&w)[NE]) {{
+{emit}  }}
 }};
 }}  // namespace nsdb_pipe
 {entry}"""
@@ -1246,11 +1375,12 @@ def _jit_for(prog: Program, cargs, kind: str, key_reg: int = -1, val_regs=(), de
     if not JIT or not hasattr(_ext.hip(), "jit_compile"):
         return None
     kinds = tuple(c[0] for c in cargs)
-    lates = tuple(c[1] for c in cargs) if kind == "agg" else ()
+    lates = tuple(c[1] for c in cargs) if kind in ("agg", "emit") else ()
     # the kernel of a program shape: generated + compiled once, then found by the shape alone (generating the source
     # costs ~30 us of Python per launch)
     shape = (_dev_index(dev), kind, tuple(prog.ins), kinds, lates, key_reg, tuple(val_regs), prog.keep_reg,
-             prog.nins_a, getattr(prog, "jk_reg", -1), getattr(prog, "keep2_reg", -1), JIT_ROWS, JIT_ROWS_SMALL,
+             prog.nins_a, getattr(prog, "jk_reg", -1), getattr(prog, "keep2_reg", -1),
+             tuple(k[0] for k in getattr(prog, "emit_keys", [])) if kind == "emit" else (), JIT_ROWS, JIT_ROWS_SMALL,
              JIT_SMALL_NREG)
     hit = _JIT_SHAPES.get(shape)
     if hit is None:
@@ -1260,7 +1390,7 @@ def _jit_for(prog: Program, cargs, kind: str, key_reg: int = -1, val_regs=(), de
             src = jit_source(prog, list(kinds), list(lates) or [0] * len(kinds), kind, key_reg, val_regs, rows=rows)
         except Unfusable:
             return None
-        fn = jit_kernel(src, "nsdb_jit_agg" if kind == "agg" else "nsdb_jit_mask", dev)
+        fn = jit_kernel(src, {"agg": "nsdb_jit_agg", "emit": "nsdb_jit_emit"}.get(kind, "nsdb_jit_mask"), dev)
         if len(_JIT_SHAPES) >= 4096:          # the shape includes the immediates: bound it for varying literals
             _JIT_SHAPES.clear()
         hit = _JIT_SHAPES[shape] = (fn, nreg, rows)
@@ -1409,6 +1539,31 @@ def interpret(prog: Program, n: int, op: str):
     if torch.unique(key[idx]).numel() > INTERP_CAP:
         return None
     return _merge(key[idx], vals[idx], op)
+
+
+def interpret_emit(prog: Program, n: int, plan: StagePlan):
+    """The emitted form with whole-column torch ops (the CPU model of jit_emit_body): (int64 words [ne, rows], rows)
+    of every kept (matched) row, key-part registers first, then the value registers."""
+    from . import kernels as KK
+
+    if plan.join is None:
+        regs = _run_program(prog, n)
+        keep = torch.ones(n, dtype=torch.bool) if prog.keep_reg < 0 else regs[prog.keep_reg] != 0
+    else:
+        regs = _run_program(prog, n, hi=prog.nins_a, sides=(0,))
+        keep = torch.ones(n, dtype=torch.bool) if prog.keep_reg < 0 else regs[prog.keep_reg] != 0
+        kidx = keep.nonzero().flatten()
+        bt = plan.builds[plan.join["name"]]
+        bi, pi = bt.table(kidx.device).probe(KK.hash_keys(regs[prog.jk_reg][kidx]))
+        prow = kidx[pi]
+        n = int(prow.numel())
+        regs = _run_program(prog, n, lo=prog.nins_a, rowmap={i: (bi if c["late"] == 2 else prow)
+                                                             for i, c in enumerate(prog.cols)})
+        keep = torch.ones(n, dtype=torch.bool) if prog.keep2_reg < 0 else regs[prog.keep2_reg] != 0
+    idx = keep.nonzero().flatten()
+    rs = [k[0] for k in prog.emit_keys] + list(prog.val_regs)
+    words = torch.stack([regs[r][idx] for r in rs]) if rs else torch.zeros(1, idx.numel(), dtype=torch.int64)
+    return words, int(idx.numel())
 
 
 def interpret_join(prog: Program, n: int, plan: StagePlan):

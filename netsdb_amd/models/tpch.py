@@ -557,9 +557,8 @@ def q03(client, db: str, segment: str = "BUILDING", date: int = 19950315, k: int
     j.set_input(0, cs)
     j.set_input(1, os_)
     j.set_input(2, ls)
-    agg = _GroupBy(lambda b: (_col(b, "l_orderkey"), _col(b, "o_orderdate"), _col(b, "o_shippriority")),
-                   lambda b: (_col(b, "l_extendedprice").double() * (1 - _col(b, "l_discount").double())).unsqueeze(1),
-                   _rows_out(["revenue"]))
+    agg = _TreeGroupBy(lambda x: KeyTuple(x.l_orderkey, x.o_orderdate, x.o_shippriority),
+                       lambda x: Values(x.l_extendedprice * (1 - x.l_discount)), _rows_out(["revenue"]))
     r = _flat(_run(client, db, "q03_out", agg.set_input(j), "tpch_q03"))
     if r is None:
         return []
@@ -599,8 +598,9 @@ def q04(client, db: str, date: int = 19930701, join_first: bool = Q04_JOIN_FIRST
         return sorted(({"o_orderpriority": p, "order_count": int(c)} for p, c in zip(hv["k0"], hv["order_count"])),
                       key=lambda x: x["o_orderpriority"])
     # EXISTS -> distinct late orderkeys (aggregate), then join with the orders of the quarter
-    dist = _GroupBy(lambda b: _col(b, "l_orderkey"), lambda b: torch.ones(b.n, 1, dtype=torch.float64, device=_dev(b)),
-                    _rows_out(["n"]))
+    # the distinct late order keys as a lambda-tree aggregation: late predicate + key straight from the scan registers
+    # (the compiled kernel's emitted form: 15 M groups at SF 10)
+    dist = _TreeGroupBy(lambda x: x.l_orderkey, lambda x: Values(1.0), _rows_out(["n"]))
     os_ = _TreeFilter(lambda x: (x.o_orderdate >= date) & (x.o_orderdate < end)).set_input(ScanSet(db, "orders", Order))
     j = _EqJoin(2, [(0, "o_orderkey", 1, "k0")], _pick([["o_orderpriority"], []]))
     j.set_input(0, os_)
@@ -698,29 +698,22 @@ def q14(client, db: str, date: int = 19950901) -> float:
 
 
 def q17(client, db: str, brand: str = "Brand#23", container: str = "MED BOX") -> float:
-    """Small-quantity-order revenue (Query17.h): per-part average quantity, then lineitems of the
-    brand/container parts under 0.2 x that average; sum(extendedprice) / 7."""
+    """Small-quantity-order revenue (Query17.h): per-part average quantity of the brand/container parts, then the
+    lineitems of those parts under 0.2 x that average; sum(extendedprice) / 7.
+
+    One job of two lineitem passes, each a join probe + aggregation compiled into one kernel (execution/pipeline.py):
+    (1) lineitem ⋈ the qualifying parts -> (sum quantity, count) per part; (2) lineitem ⋈ those per-part rows,
+    l_quantity < 0.2 * sq / n -> sum(l_extendedprice). Every lambda is a tree (members, arithmetic, comparisons)."""
     ps = _TreeFilter(lambda x: (x.p_brand == brand) & (x.p_container == container)).set_input(ScanSet(db, "part", Part))
-    j = _EqJoin(2, [(0, "l_partkey", 1, "p_partkey")], _pick([["l_partkey", "l_quantity", "l_extendedprice"], []]))
+    j = _EqJoin(2, [(0, "l_partkey", 1, "p_partkey")], _pick([["l_partkey", "l_quantity"], []]))
     j.set_input(0, ScanSet(db, "lineitem", LineItem))
     j.set_input(1, ps)
-    # job 1: the qualifying lineitems; job 2 (same plan shape as the reference): avg per part + filter
-    if client.storage.has_set(db, "q17_li"):
-        client.remove_set(db, "q17_li")
-    client.create_set(db, "q17_li", None)
-    client.execute_computations(WriteSet(db, "q17_li").set_input(j), job_name="tpch_q17_join")
-    avg = _GroupBy(lambda b: _col(b, "l_partkey"),
-                   lambda b: _vcols(_col(b, "l_quantity").double(), torch.ones(b.n, dtype=torch.float64,
-                                                                               device=_dev(b))),
-                   _rows_out(["sq", "n"]))
-    li = ScanSet(db, "q17_li")
-    a = avg.set_input(li)
+    avg = _TreeGroupBy(lambda x: x.l_partkey, lambda x: Values(x.l_quantity, 1.0), _rows_out(["sq", "n"]))
     j2 = _EqJoin(2, [(0, "l_partkey", 1, "k0")], _pick([["l_quantity", "l_extendedprice"], ["sq", "n"]]))
-    j2.set_input(0, ScanSet(db, "q17_li"))
-    j2.set_input(1, a)
-    small = _Filter(lambda b: _col(b, "l_quantity") < 0.2 * _col(b, "sq") / _col(b, "n")).set_input(j2)
-    tot = _GroupBy(lambda b: torch.zeros(b.n, dtype=torch.int64, device=_dev(b)),
-                   lambda b: _col(b, "l_extendedprice").double().unsqueeze(1), _rows_out(["s"]))
+    j2.set_input(0, ScanSet(db, "lineitem", LineItem))
+    j2.set_input(1, avg.set_input(j))
+    small = _TreeFilter(lambda x: x.l_quantity < 0.2 * x.sq / x.n).set_input(j2)
+    tot = _TreeGroupBy(lambda x: Literal(0), lambda x: Values(x.l_extendedprice), _rows_out(["s"]))
     r = _flat(_run(client, db, "q17_out", tot.set_input(small), "tpch_q17"))
     return 0.0 if r is None else float(r.columns["s"].sum()) / 7.0
 
@@ -739,16 +732,20 @@ def q22(client, db: str, codes=("13", "31", "23", "29", "30", "18", "17")) -> Li
             m |= c.startswith(code).to(m.device)
         return m
 
-    pos = _Filter(lambda b: in_codes(b) & (_col(b, "c_acctbal") > 0)).set_input(ScanSet(db, "customer", Customer))
-    avg = _GroupBy(lambda b: torch.zeros(b.n, dtype=torch.int64, device=_dev(b)),
-                   lambda b: _vcols(_col(b, "c_acctbal").double(), torch.ones(b.n, dtype=torch.float64,
-                                                                             device=_dev(b))),
-                   _rows_out(["s", "n"]))
+    def codes_pred(x):                         # SUBSTRING(c_phone, 1, 2) IN codes as prefix tests (lambda tree)
+        p = None
+        for code in cset:
+            t = Like(x.c_phone, code + "%")
+            p = t if p is None else (p | t)
+        return p
+
+    # the positive-balance average: predicate + one-group aggregation in one compiled kernel
+    pos = _TreeFilter(lambda x: codes_pred(x) & (x.c_acctbal > 0.0)).set_input(ScanSet(db, "customer", Customer))
+    avg = _TreeGroupBy(lambda x: Literal(0), lambda x: Values(x.c_acctbal, 1.0), _rows_out(["s", "n"]))
     r = _flat(_run(client, db, "q22_avg", avg.set_input(pos), "tpch_q22_avg"))
     mean = float(r.columns["s"].sum() / r.columns["n"].sum()) if r is not None else 0.0
     # NOT EXISTS orders: distinct custkeys with orders (aggregate), used as a broadcast anti-join set
-    has = _GroupBy(lambda b: _col(b, "o_custkey"), lambda b: torch.ones(b.n, 1, dtype=torch.float64, device=_dev(b)),
-                   _rows_out(["n"]))
+    has = _TreeGroupBy(lambda x: x.o_custkey, lambda x: Values(1.0), _rows_out(["n"]))
     h = _flat(_run(client, db, "q22_has", has.set_input(ScanSet(db, "orders", Order)), "tpch_q22_orders"))
     with_orders = h.columns["k0"] if h is not None else torch.zeros(0, dtype=torch.int64)
 
@@ -775,9 +772,9 @@ def q22(client, db: str, codes=("13", "31", "23", "29", "30", "18", "17")) -> Li
 def q02(client, db: str, size: int = 15, type_suffix: str = "BRASS", region: str = "EUROPE", k: int = 100) -> List[dict]:
     """Minimum cost supplier (Query02.h): part ⋈ partsupp ⋈ supplier ⋈ nation ⋈ region, min supply
     cost per part (aggregate), joined back to keep the suppliers at that minimum; top 100."""
-    ps_ = _Filter(lambda b: (_col(b, "p_size") == size) &
-                  _like(_col(b, "p_type"), "%" + type_suffix, _dev(b))).set_input(ScanSet(db, "part", Part))
-    rs = _Filter(lambda b: _isin_str(_col(b, "r_name"), [region], _dev(b))).set_input(ScanSet(db, "region", Region))
+    ps_ = _TreeFilter(lambda x: (x.p_size == size) & Like(x.p_type, "%" + type_suffix)).set_input(
+        ScanSet(db, "part", Part))
+    rs = _TreeFilter(lambda x: x.r_name == region).set_input(ScanSet(db, "region", Region))
     j = _EqJoin(5, [(0, "p_partkey", 1, "ps_partkey"), (1, "ps_suppkey", 2, "s_suppkey"),
                     (2, "s_nationkey", 3, "n_nationkey"), (3, "n_regionkey", 4, "r_regionkey")],
                 _pick([["p_partkey", "p_mfgr"], ["ps_supplycost"], ["s_acctbal", "s_name", "s_address", "s_phone",
@@ -791,14 +788,14 @@ def q02(client, db: str, size: int = 15, type_suffix: str = "BRASS", region: str
         client.remove_set(db, "q02_cand")
     client.create_set(db, "q02_cand", None)
     client.execute_computations(WriteSet(db, "q02_cand").set_input(j), job_name="tpch_q02_join")
-    mn = _GroupBy(lambda b: _col(b, "p_partkey"), lambda b: _col(b, "ps_supplycost").double().unsqueeze(1),
-                  _rows_out(["mincost"]), reduce_op="min")
+    mn = _TreeGroupBy(lambda x: x.p_partkey, lambda x: Values(x.ps_supplycost), _rows_out(["mincost"]),
+                      reduce_op="min")
     j2 = _EqJoin(2, [(0, "p_partkey", 1, "k0")],
                  _pick([["p_partkey", "p_mfgr", "ps_supplycost", "s_acctbal", "s_name", "s_address", "s_phone",
                          "s_comment", "n_name"], ["mincost"]]))
     j2.set_input(0, ScanSet(db, "q02_cand"))
     j2.set_input(1, mn.set_input(ScanSet(db, "q02_cand")))
-    best = _Filter(lambda b: _col(b, "ps_supplycost") == _col(b, "mincost")).set_input(j2)
+    best = _TreeFilter(lambda x: x.ps_supplycost == x.mincost).set_input(j2)
     if client.storage.has_set(db, "q02_out"):
         client.remove_set(db, "q02_out")
     client.create_set(db, "q02_out", None)

@@ -70,7 +70,13 @@ class DeviceTimer:
             self.pending.append((e0, e1, rec, key))
 
     def resolve(self, block: bool = False) -> int:
-        """Fill in the pairs that have completed (all of them when ``block``); returns how many are still pending."""
+        """Fill in the pairs that have completed (all of them when ``block``); returns how many are still pending.
+        A no-op while a HIP-graph capture records on this thread's stream (an event query would invalidate it)."""
+        if self.pending:
+            import torch
+
+            if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+                return len(self.pending)
         with self._lock:
             todo, self.pending = self.pending, []
         keep = []

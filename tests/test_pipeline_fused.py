@@ -96,6 +96,19 @@ def test_jit_sources_compile_cpu(monkeypatch):
                 assert len(h.jit_compile(src, hdr)) > 1000
     assert len(seen) >= len(progs)
     assert joins >= 2, joins                   # q12 and q14 probe their build tables inside the fused kernel
+    # the emitted (high-cardinality) form of every stage: tables capped so each stage overflows once
+    PL._PROG_CACHE.clear()
+    PL._EMIT_SIGS.clear()
+    monkeypatch.setattr(PL, "INTERP_CAP", 0)
+    for q in QUERIES:
+        tpch.QUERIES[q](c, "tpch")
+    emits = [p for p in PL._PROG_CACHE.values() if p.mode == "emit"]
+    assert len(emits) >= len(QUERIES), len(emits)
+    for p in emits:
+        kinds = [cc["kind"] for cc in p.cols]
+        src = PL.jit_source(p, kinds, [cc["late"] for cc in p.cols], "emit", -1, p.val_regs)
+        assert "jit_emit_body" in src
+        assert len(h.jit_compile(src, hdr)) > 1000
 
 
 class _Sel(SelectionComp):
@@ -234,9 +247,57 @@ def test_fused_overflow_falls_back(monkeypatch):
     eager = _agg_job(c, *args)
     monkeypatch.setattr(PL, "CPU_INTERPRETER", True)
     monkeypatch.setattr(PL, "INTERP_CAP", 64)      # the interpreter models the kernel's table capacity
+    monkeypatch.setattr(PL, "EMIT", False)         # without the emitted form: the eager atoms
     fused = _agg_job(c, *args)
     assert c.engine.pipeline_stats["fallback_batches"] >= 1
     assert eager[0] == fused[0] and torch.allclose(eager[1], fused[1])
+
+
+EMIT_CASES = {
+    # one integer key with more groups than the kernel's table: every kept row emitted, reduced by the group-by
+    "int_key": (lambda x: x.l_quantity > 1, lambda x: x.l_orderkey, lambda x: Values(x.l_extendedprice, 1.0), "sum"),
+    # a composite key of an integer, a float and a short string (not packable into one word), min
+    "composite_key": (lambda x: x.l_shipmode == "AIR", lambda x: KeyTuple(x.l_partkey, x.l_discount, x.l_returnflag),
+                      lambda x: Values(x.l_quantity * x.l_tax), "min"),
+}
+
+
+@pytest.mark.parametrize("case", sorted(EMIT_CASES))
+def test_fused_emit_cpu_interpreter(case, monkeypatch):
+    """High-cardinality stages: the emitted form (torch model of jit_emit_body) == the eager atoms."""
+    monkeypatch.setenv("NSDB_DEVICE_STRINGS", "1")
+    t = tpch_gen.generate_fast(0.002, seed=9)
+    c = _client("cpu", t)
+    eager = _agg_job(c, *EMIT_CASES[case])
+    monkeypatch.setattr(PL, "CPU_INTERPRETER", True)
+    monkeypatch.setattr(PL, "INTERP_CAP", 64)
+    PL._EMIT_SIGS.clear()
+    e0 = c.engine.pipeline_stats.get("emitted_batches", 0)
+    fused = _agg_job(c, *EMIT_CASES[case])
+    fused2 = _agg_job(c, *EMIT_CASES[case])        # the stage now starts in the emitted form
+    assert c.engine.pipeline_stats.get("emitted_batches", 0) >= e0 + 2, c.engine.pipeline_stats
+    for f in (fused, fused2):
+        assert eager[0] == f[0]
+        assert torch.allclose(eager[1], f[1], rtol=1e-12, atol=1e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", sorted(EMIT_CASES))
+def test_fused_emit_gpu(case):
+    """The compiled emit kernel (per-tile regions, workgroup scan, compaction) == the eager atoms, 10 k+ groups."""
+    t = tpch_gen.generate_fast(0.05, seed=9)
+    c = _client("cuda:0", t)
+    c.engine.fused_pipelines = False
+    eager = _agg_job(c, *EMIT_CASES[case])
+    c.engine.fused_pipelines = True
+    e0 = c.engine.pipeline_stats.get("emitted_batches", 0)
+    fused = _agg_job(c, *EMIT_CASES[case])
+    fused2 = _agg_job(c, *EMIT_CASES[case])
+    assert c.engine.pipeline_stats.get("emitted_batches", 0) >= e0 + 2, c.engine.pipeline_stats
+    assert len(eager[0]) > 2048
+    for f in (fused, fused2):
+        assert eager[0] == f[0]
+        assert torch.allclose(eager[1], f[1], rtol=1e-9, atol=1e-9)
 
 
 @pytest.mark.gpu
