@@ -1,7 +1,7 @@
 """A/B of the split-K count on the dedup harness's skinny long-K GEMMs (config 5: 12 models x 500 rows, batch 100):
 the launcher's one-wave choice against split counts that fill a second / third wave of workgroups.
 
-    python scripts/ab_splits.py [--iters 20]
+    python scripts/ab_dedup_splits.py [--iters 20]
 """
 import argparse
 import json

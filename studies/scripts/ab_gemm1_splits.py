@@ -1,6 +1,6 @@
 """Interleaved timing of the FF layer-1 GEMM (1000x1000x597568, 8-phase 256^2) over split-K factors:
 fewer splits = fewer busy CUs (16 tiles x splits workgroups) but less slab traffic; under the power cap the
-clock may rise.  python scripts/ab_splits.py [--splits 16,15,14,12] [--rounds 4] [--iters 10]"""
+clock may rise.  python studies/scripts/ab_gemm1_splits.py [--splits 16,15,14,12] [--rounds 4] [--iters 10]"""
 import argparse
 import json
 import os
