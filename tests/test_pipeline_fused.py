@@ -301,6 +301,23 @@ def test_fused_emit_gpu(case):
 
 
 @pytest.mark.gpu
+def test_fused_emit_gpu_million_groups():
+    """1 M+ groups (every order key of SF 0.7) through the emitted form: exact against the eager atoms."""
+    t = tpch_gen.generate_fast(0.7, seed=5)
+    c = _client("cuda:0", t)
+    args = (lambda x: x.l_quantity > 0, lambda x: x.l_orderkey, lambda x: Values(x.l_quantity, 1.0), "sum")
+    c.engine.fused_pipelines = False
+    eager = _agg_job(c, *args)
+    c.engine.fused_pipelines = True
+    e0 = c.engine.pipeline_stats.get("emitted_batches", 0)
+    fused = _agg_job(c, *args)
+    assert c.engine.pipeline_stats.get("emitted_batches", 0) > e0, c.engine.pipeline_stats
+    assert len(eager[0]) >= 1_000_000
+    assert eager[0] == fused[0]
+    assert torch.equal(eager[1], fused[1])         # integer-valued sums: exact whatever the order
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("tile,jit", [(-2, True), (-2, False), (-1, False), (0, False)],
                          ids=["compiled", "lds_tile", "hybrid", "register"])
 def test_fused_tpch_gpu_vs_eager_and_pandas(tile, jit, monkeypatch):
@@ -321,8 +338,10 @@ def test_fused_tpch_gpu_vs_eager_and_pandas(tile, jit, monkeypatch):
         assert _close(got, ref), (q, got, ref)
         assert _close(eager, ref), q
     st = c.engine.pipeline_stats
-    assert st["fused_stages"] >= len(QUERIES) and st["fallback_batches"] == 0, st
-    if jit:     # every fused launch took a compiled kernel
+    assert st["fused_stages"] >= len(QUERIES), st
+    if jit:     # every fused launch took a compiled kernel; the emitted form and join probes exist there only
+        assert st["fallback_batches"] == 0, st
+        assert st.get("fused_join_batches", 0) >= 3 and st.get("emitted_batches", 0) >= 1, st
         assert PL.JIT_STATS["failed"] == j0["failed"], PL.JIT_STATS
         assert PL.JIT_STATS["launches"] - j0["launches"] >= len(QUERIES) + len(FILTER_QUERIES), PL.JIT_STATS
     else:
@@ -346,7 +365,11 @@ def test_fused_operators_gpu(case):
 
 
 @pytest.mark.gpu
-def test_fused_overflow_gpu():
+@pytest.mark.parametrize("emit", [True, False], ids=["emitted", "eager"])
+def test_fused_overflow_gpu(emit, monkeypatch):
+    """A table overflow re-runs the batch in the emitted form, or (emitted form off) through the eager atoms."""
+    monkeypatch.setattr(PL, "EMIT", emit)
+    PL._EMIT_SIGS.clear()
     t = tpch_gen.generate_fast(0.01, seed=9)
     c = _client("cuda:0", t)
     args = (lambda x: x.l_quantity > 1, lambda x: x.l_orderkey, lambda x: Values(x.l_extendedprice), "sum")
@@ -354,7 +377,11 @@ def test_fused_overflow_gpu():
     eager = _agg_job(c, *args)
     c.engine.fused_pipelines = True
     fused = _agg_job(c, *args)
-    assert c.engine.pipeline_stats["fallback_batches"] >= 1
+    st = c.engine.pipeline_stats
+    if emit:
+        assert st.get("emitted_batches", 0) >= 1 and st["fallback_batches"] == 0, st
+    else:
+        assert st["fallback_batches"] >= 1, st
     assert eager[0] == fused[0] and torch.allclose(eager[1], fused[1])
 
 
