@@ -248,6 +248,12 @@ __device__ __forceinline__ void run(const PipeArgs& a, typename RF<NR>::vec (&R)
         for (int j = 0; j < ROWS; ++j) z[j] = str_match(d, x[j], a.lit, imm, mode) ? 1ull : 0ull;
         break;
       }
+      case OP_SLIKE: {
+        const unsigned char* d = a.col[ib].dat;
+#pragma unroll
+        for (int j = 0; j < ROWS; ++j) z[j] = str_like(d, x[j], a.lit, imm) ? 1ull : 0ull;
+        break;
+      }
       default:
 #pragma unroll
         for (int j = 0; j < ROWS; ++j) z[j] = 0;
@@ -605,6 +611,12 @@ __device__ __forceinline__ void tile_run(const PipeArgs& a, u64* regs, int lo, i
         const int mode = op == OP_SEQ ? 0 : (op == OP_SPRE ? 1 : 2);
 #pragma unroll
         for (int j = 0; j < RPT; ++j) z[j] = str_match(d, x[j], a.lit, imm, mode) ? 1ull : 0ull;
+        break;
+      }
+      case OP_SLIKE: {
+        const unsigned char* d = a.col[cur.b].dat;
+#pragma unroll
+        for (int j = 0; j < RPT; ++j) z[j] = str_like(d, x[j], a.lit, imm) ? 1ull : 0ull;
         break;
       }
       default:

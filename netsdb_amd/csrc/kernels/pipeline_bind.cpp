@@ -61,7 +61,8 @@ struct PipeArgs {
 
 enum ColKind : int { C_F64 = 0, C_I64, C_I32, C_F32, C_U8, C_SCODE, C_SREF };
 enum : int { OP_LTF = 10, OP_NEI = 21, OP_SEQ = 26, OP_SPRE = 27, OP_SSUF = 28, OP_SEL = 29, OP_RNGF = 31, OP_RNGI = 32,
-             OP_LAST = 32 };
+             OP_SLIKE = 33, OP_LAST = 33 };
+inline bool is_str_op(int op) { return op == OP_SEQ || op == OP_SPRE || op == OP_SSUF || op == OP_SLIKE; }
 
 int sizes(int i) {
   static int s[10] = {0};
@@ -132,10 +133,13 @@ void fill_args(PipeArgs& a, const torch::Tensor& prog, int64_t nins_a, const Col
                 "pipe_agg: AND-with register only on compares, at ", i);
     if (I.op == OP_SEL) TORCH_CHECK(I.imm >= 0 && I.imm < NREG, "pipe_agg: select register at ", i);
     a.nreg = std::max({a.nreg, I.dst + 1, I.a + 1, I.b + 1, I.c + 1, I.op == OP_SEL ? (int)I.imm + 1 : 0});
-    if (I.op == OP_SEQ || I.op == OP_SPRE || I.op == OP_SSUF) {
+    if (is_str_op(I.op)) {
       TORCH_CHECK(I.b >= 0 && I.b < ncol && std::get<0>(cols[I.b]) == C_SREF, "pipe_agg: string op column at ", i);
       const long long off = I.imm >> 16, len = I.imm & 0xFFFF;
       TORCH_CHECK(off >= 0 && off + len <= lit.numel(), "pipe_agg: literal out of the pool at ", i);
+      // [flags][nseg][lens][bytes]: built and checked by the host compiler (pipeline.py Program.like_literal); the
+      // pool lives on the device, so only its header size is checked here (no device read per launch)
+      if (I.op == OP_SLIKE) TORCH_CHECK(len >= 2, "pipe_agg: LIKE literal header at ", i);
     }
   }
   a.nins = nins;
@@ -163,6 +167,7 @@ void fill_args(PipeArgs& a, const torch::Tensor& prog, int64_t nins_a, const Col
       C.en = reinterpret_cast<const long long*>(e.data_ptr<int64_t>());
       C.contig = C.en == C.st + 1 ? 1 : 0;             // one offsets array: ends are the next rows' starts
       C.dat = d.data_ptr<uint8_t>();
+      TORCH_CHECK((reinterpret_cast<uintptr_t>(C.dat) & 3) == 0, "pipe_agg: string bytes must be 4-byte aligned");
     } else {
       TORCH_CHECK(std::get<3>(t).has_value(), "pipe_agg: numeric column needs data");
       const auto& x = *std::get<3>(t);
@@ -216,7 +221,7 @@ void predecode_tile(PipeArgs& a) {
   const long long T8 = (long long)a.tile * 8;
   for (int i = 0; i < a.nins; ++i) {
     Ins& I = a.ins[i];
-    const bool str = I.op == OP_SEQ || I.op == OP_SPRE || I.op == OP_SSUF;
+    const bool str = is_str_op(I.op);
     int fl = 0;
     if (I.a == -2) fl |= 1; else if (I.a < 0) fl |= 2; else I.a = (int)(I.a * T8);
     if (str) fl |= 8;                                  // b: the column index of the bytes, not a register

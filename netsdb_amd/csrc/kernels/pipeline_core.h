@@ -25,7 +25,7 @@ constexpr int TF_AIMM = 1, TF_ANONE = 2, TF_BIMM = 4, TF_BNONE = 8, TF_C = 16;
 enum Op : int {
   OP_NOP = 0, OP_CONST, OP_ADDF, OP_SUBF, OP_MULF, OP_DIVF, OP_ADDI, OP_SUBI, OP_MULI, OP_I2F,
   OP_LTF, OP_LEF, OP_GTF, OP_GEF, OP_EQF, OP_NEF, OP_LTI, OP_LEI, OP_GTI, OP_GEI, OP_EQI, OP_NEI,
-  OP_AND, OP_OR, OP_NOT, OP_PACK, OP_SEQ, OP_SPRE, OP_SSUF, OP_SEL, OP_NEGF, OP_RNGF, OP_RNGI
+  OP_AND, OP_OR, OP_NOT, OP_PACK, OP_SEQ, OP_SPRE, OP_SSUF, OP_SEL, OP_NEGF, OP_RNGF, OP_RNGI, OP_SLIKE
 };
 constexpr int KPOOL = 16;              // second immediates: range upper bounds
 enum ColKind : int { C_F64 = 0, C_I64, C_I32, C_F32, C_U8, C_SCODE, C_SREF };
@@ -93,6 +93,81 @@ __device__ __forceinline__ bool str_match(const unsigned char* d, u64 ref, const
   const long long o = mode == 2 ? s + len - ll : s;     // suffix: compare the last ll bytes
   for (int b = 0; b < ll; ++b)
     if (d[o + b] != l[b]) return false;
+  return true;
+}
+
+// General LIKE (OP_SLIKE: '%x%', '%a%b%', 'a%b', '_'): the literal is [flags: 1 anchored start, 2 anchored end]
+// [nseg][len_0 .. len_{nseg-1}][segment bytes], '_' = 0xFF (never a byte of UTF-8). The string buffer is read as
+// aligned dwords (StringColumn pads it by >= 16 bytes and keeps it a 4-byte multiple, as strings.hip str_like does);
+// a floating segment is searched 4 candidate starts per dword (SWAR compare of its first two bytes), and only those
+// candidates are verified byte by byte. Greedy leftmost matching is exact for '%'-separated fixed segments.
+__device__ __forceinline__ unsigned lk_byte(const unsigned* w, long long p) {
+  return (w[p >> 2] >> ((unsigned)(p & 3) * 8u)) & 0xFFu;
+}
+__device__ __forceinline__ bool lk_seg_at(const unsigned* w, long long p, const unsigned char* sb, int ln) {
+  for (int k = 0; k < ln; ++k) {
+    const unsigned c = sb[k];
+    if (c != 0xFFu && lk_byte(w, p + k) != c) return false;
+  }
+  return true;
+}
+__device__ __forceinline__ unsigned lk_zero_bytes(unsigned v) {   // 0x80 in every zero byte of v (exact)
+  return ~(((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v) & 0x80808080u;
+}
+__device__ __forceinline__ long long lk_find(const unsigned* w, long long pos, long long e, const unsigned char* sb,
+                                             int ln) {
+  const long long last = e - ln;
+  if (last < pos) return -1;
+  const unsigned b0 = sb[0], b1 = ln >= 2 ? sb[1] : 0xFFu;
+  if (ln < 2 || b0 == 0xFFu || b1 == 0xFFu) {
+    for (long long p = pos; p <= last; ++p)
+      if (lk_seg_at(w, p, sb, ln)) return p;
+    return -1;
+  }
+  const unsigned B0 = b0 * 0x01010101u, B1 = b1 * 0x01010101u;
+  long long base = pos & ~3ll;
+  unsigned x = w[base >> 2];
+  while (base <= last) {
+    const unsigned y = w[(base >> 2) + 1];
+    const unsigned x1 = (x >> 8) | (y << 24);           // the bytes at base + 1 .. base + 4
+    unsigned cand = lk_zero_bytes(x ^ B0) & lk_zero_bytes(x1 ^ B1);
+    while (cand) {
+      const long long p = base + (__builtin_ctz(cand) >> 3);
+      cand &= cand - 1;
+      if (p < pos || p > last) continue;
+      if (ln == 2 || lk_seg_at(w, p, sb, ln)) return p;
+    }
+    base += 4;
+    x = y;
+  }
+  return -1;
+}
+__device__ __forceinline__ bool str_like(const unsigned char* d, u64 ref, const unsigned char* lit, long long imm) {
+  const long long s = (long long)(ref >> 24), e = s + (long long)(ref & 0xFFFFFF);
+  const unsigned char* l = lit + (imm >> 16);
+  const int flags = l[0], nseg = l[1];
+  const unsigned* w = reinterpret_cast<const unsigned*>(d);
+  const unsigned char* sb = l + 2 + nseg;
+  if (nseg == 0) return (flags & 3) == 3 ? e == s : true;
+  long long pos = s;
+  for (int sg = 0; sg < nseg; ++sg) {
+    const int ln = l[2 + sg];
+    const bool last = sg == nseg - 1;
+    if (sg == 0 && (flags & 1)) {
+      if (e - pos < ln || !lk_seg_at(w, pos, sb, ln)) return false;
+      pos += ln;
+      if (last && (flags & 2) && pos != e) return false;
+    } else if (last && (flags & 2)) {
+      const long long p = e - ln;
+      if (p < pos || !lk_seg_at(w, p, sb, ln)) return false;
+      pos = e;
+    } else {
+      const long long p = lk_find(w, pos, e, sb, ln);
+      if (p < 0) return false;
+      pos = p + ln;
+    }
+    sb += ln;
+  }
   return true;
 }
 

@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import hashlib
 import os
+import re
 import struct
 import threading
 import warnings
@@ -47,7 +48,7 @@ NREG, MAXINS, MAXCOL, FMAX, MAXSTR = 16, 48, 10, 8, 4
 IMM = -2                       # operand register number meaning "the instruction's immediate"
 (OP_NOP, OP_CONST, OP_ADDF, OP_SUBF, OP_MULF, OP_DIVF, OP_ADDI, OP_SUBI, OP_MULI, OP_I2F,
  OP_LTF, OP_LEF, OP_GTF, OP_GEF, OP_EQF, OP_NEF, OP_LTI, OP_LEI, OP_GTI, OP_GEI, OP_EQI, OP_NEI,
- OP_AND, OP_OR, OP_NOT, OP_PACK, OP_SEQ, OP_SPRE, OP_SSUF, OP_SEL, OP_NEGF, OP_RNGF, OP_RNGI) = range(33)
+ OP_AND, OP_OR, OP_NOT, OP_PACK, OP_SEQ, OP_SPRE, OP_SSUF, OP_SEL, OP_NEGF, OP_RNGF, OP_RNGI, OP_SLIKE) = range(34)
 KPOOL = 16                     # second immediates (range upper bounds), pipeline.hip PipeArgs.kpool
 C_F64, C_I64, C_I32, C_F32, C_U8, C_SCODE, C_SREF = range(7)
 AGG_OPS = {"sum": 0, "min": 1, "max": 2}
@@ -430,8 +431,22 @@ class Program:
         aux = (len(self.kpool) - 1) | (mode << 8)
         self.ins[-2:] = [(OP_RNGF if fam(o1) == "f" else OP_RNGI, d, a1, -1, c1, int(lo), aux)]
 
+    def like_literal(self, pattern: str) -> int:
+        """A general LIKE pattern in the literal pool as pipeline_core.h str_like reads it: [flags: 1 anchored start,
+        2 anchored end][nseg][segment lengths][segment bytes, '_' = 0xFF]."""
+        from ..objects.strings import _compile_like
+
+        buf, _st, ln, a0, a1 = _compile_like(pattern)
+        if len(ln) > 32 or any(n > 255 for n in ln):
+            raise Unfusable("LIKE pattern size")
+        blob = bytes([int(a0) | (int(a1) << 1), len(ln)] + list(ln)) + bytes(buf)
+        assert len(blob) == 2 + len(ln) + sum(ln)
+        return self._pool(blob)
+
     def literal(self, s: str) -> int:
-        b = s.encode()
+        return self._pool(s.encode())
+
+    def _pool(self, b: bytes) -> int:
         if len(b) > 0xFFFF:
             raise Unfusable("literal")
         if b not in self.lit_index:
@@ -738,18 +753,18 @@ class _Compiler:
             if t != "s":
                 raise Unfusable("LIKE on a non-string")
             body = pat.strip("%")
-            if "%" in body or "_" in pat:
-                raise Unfusable("LIKE pattern")
-            if pat.endswith("%") and not pat.startswith("%"):
-                opc = OP_SPRE
-            elif pat.startswith("%") and not pat.endswith("%"):
-                opc = OP_SSUF
-            elif "%" not in pat:
-                opc = OP_SEQ
-            else:
-                raise Unfusable("LIKE %x%")
             d = p.temp()
-            p.emit(opc, d, r, r, p.literal(body))
+            if "%" in body or "_" in pat or (pat.startswith("%") and pat.endswith("%")):
+                # contains / several segments / '_': the general matcher (pipeline_core.h str_like)
+                p.emit(OP_SLIKE, d, r, r, p.like_literal(pat))
+            else:
+                if pat.endswith("%"):
+                    opc = OP_SPRE
+                elif pat.startswith("%"):
+                    opc = OP_SSUF
+                else:
+                    opc = OP_SEQ
+                p.emit(opc, d, r, r, p.literal(body))
             if neg:
                 p.emit(OP_NOT, d, d)
             return d, "b"
@@ -1195,6 +1210,8 @@ def _jit_ins(pc: int, ins) -> Optional[str]:
     elif op in (OP_SEQ, OP_SPRE, OP_SSUF):
         mode = {OP_SEQ: 0, OP_SPRE: 1, OP_SSUF: 2}[op]
         z = f"(u64)str_match(a.col[{b}].dat, {X}, a.lit, a.ins[{pc}].imm, {mode})"
+    elif op == OP_SLIKE:
+        z = f"(u64)str_like(a.col[{b}].dat, {X}, a.lit, a.ins[{pc}].imm)"
     else:
         z = "0ull"
     if c >= 0:
@@ -1613,7 +1630,20 @@ def _run_program(prog: Program, n: int, lo: int = 0, hi: Optional[int] = None, s
         s = o.tolist()
         if rowmap is not None:
             s = [s[i] for i in rowmap[col].tolist()]
-        if mode == 0:
+        if mode == 3:                          # general LIKE: decode the pool entry back into a regex
+            flags, nseg = lit[0], lit[1]
+            lens, body, segs, o = lit[2:2 + nseg], lit[2 + nseg:], [], 0
+            for ln_ in lens:
+                segs.append(body[o:o + ln_])
+                o += ln_
+            pieces = [re.escape(g).replace(re.escape(b"\xff"), b".") for g in segs]
+            if not pieces:
+                rx = re.compile(rb"\A\Z" if flags == 3 else rb"", re.S)
+            else:
+                rx = re.compile((rb"\A" if flags & 1 else rb".*") + b".*".join(pieces) + (rb"\Z" if flags & 2 else b""),
+                                re.S)
+            m = [rx.match(x.encode()) is not None for x in s]
+        elif mode == 0:
             m = [x.encode() == lit for x in s]
         elif mode == 1:
             m = [x.encode().startswith(lit) for x in s]
@@ -1649,8 +1679,8 @@ def _run_program(prog: Program, n: int, lo: int = 0, hi: Optional[int] = None, s
                 z = (x == 0).long()
             elif opc == OP_PACK:
                 z = (x << (imm & 63)) | y
-            elif opc in (OP_SEQ, OP_SPRE, OP_SSUF):
-                z = strmatch(x, b, imm, {OP_SEQ: 0, OP_SPRE: 1, OP_SSUF: 2}[opc])
+            elif opc in (OP_SEQ, OP_SPRE, OP_SSUF, OP_SLIKE):
+                z = strmatch(x, b, imm, {OP_SEQ: 0, OP_SPRE: 1, OP_SSUF: 2, OP_SLIKE: 3}[opc])
             elif opc == OP_SEL:
                 z = torch.where(x != 0, y, regs[imm])
             elif opc in (OP_RNGF, OP_RNGI):
