@@ -487,6 +487,18 @@ class SharedInference:
         X = X.to(ref.dtype)
         if X.shape[1] != self.nbc * self.bc:
             X = torch.nn.functional.pad(X, (0, self.nbc * self.bc - X.shape[1]))
+        side = None
+        if self.overlap and X.is_cuda and self.w_common is not None and self.w_priv is not None:
+            # private panels on a second HIP stream, launched first: it waits only for X (an event on the main
+            # stream), so it runs concurrently with the common panel's GEMM enqueued next on the main stream
+            main = torch.cuda.current_stream(X.device)
+            side = SharedInference._side.get(X.device)
+            if side is None:
+                side = SharedInference._side[X.device] = torch.cuda.Stream(X.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                Yp = self._private(X, None)
+            X.record_stream(side)
         P = None
         if self.w_common is not None:
             for off, xv in self._xpart(X, self.common_cols, self.common_runs):
@@ -494,8 +506,25 @@ class SharedInference:
                 P = ops.gemm_nt(wv, xv, P, ops.BIAS_MAT if P is not None else ops.BIAS_NONE, out_dtype=torch.float32)
         if self.w_priv is None:
             return {n: P[: self.R] for n in self.names}
+        if side is not None:
+            main.wait_stream(side)
+            Yp.record_stream(main)
+            Y = Yp.add_(P.unsqueeze(0))
+        else:
+            Y = self._private(X, P)
+        return {n: Y[i, : self.R] for i, n in enumerate(self.names)}
+
+    # Private panels concurrent with the common panel (run(): two HIP streams). Both GEMMs stream HBM at ~5 TB/s,
+    # but each drains its last wave of tiles and its split-K reduce alone; side by side, one kernel's tail overlaps
+    # the other's body. The private result then no longer accumulates onto P in its epilogue: one broadcast add
+    # (2.4 MB at config 5) joins them.
+    overlap = True
+    _side: Dict[torch.device, "torch.cuda.Stream"] = {}
+
+    def _private(self, X: torch.Tensor, Y: Optional[torch.Tensor]) -> torch.Tensor:
+        from .. import ops
+
         M = self.w_priv.shape[0]
-        Y = P
         for off, xv in self._xpart(X, self.priv_cols, self.priv_runs):
             wv = self.w_priv[:, :, off: off + xv.shape[1]]
             # a narrow private slice of X is compacted first (a 20 MB copy; the GEMM then streams B
@@ -503,7 +532,7 @@ class SharedInference:
             xv = xv.contiguous() if xv.stride(0) > 2 * xv.shape[1] else xv
             xb = xv.unsqueeze(0).expand(M, -1, -1)            # batch stride 0: one X panel for every model
             Y = ops.gemm_nt(wv, xb, Y, ops.BIAS_MAT if Y is not None else ops.BIAS_NONE, out_dtype=torch.float32)
-        return {n: Y[i, : self.R] for i, n in enumerate(self.names)}
+        return Y
 
 
 def _runs(cols) -> list:

@@ -784,17 +784,15 @@ def q02(client, db: str, size: int = 15, type_suffix: str = "BRASS", region: str
     j.set_input(2, ScanSet(db, "supplier", Supplier))
     j.set_input(3, ScanSet(db, "nation", Nation))
     j.set_input(4, rs)
-    if client.storage.has_set(db, "q02_cand"):
-        client.remove_set(db, "q02_cand")
-    client.create_set(db, "q02_cand", None)
-    client.execute_computations(WriteSet(db, "q02_cand").set_input(j), job_name="tpch_q02_join")
+    # ONE job: the 5-way join's candidates are an intermediate tuple set read by both the min-cost aggregation and
+    # the join back to it (no candidate set written and scanned twice, no second job)
     mn = _TreeGroupBy(lambda x: x.p_partkey, lambda x: Values(x.ps_supplycost), _rows_out(["mincost"]),
                       reduce_op="min")
     j2 = _EqJoin(2, [(0, "p_partkey", 1, "k0")],
                  _pick([["p_partkey", "p_mfgr", "ps_supplycost", "s_acctbal", "s_name", "s_address", "s_phone",
                          "s_comment", "n_name"], ["mincost"]]))
-    j2.set_input(0, ScanSet(db, "q02_cand"))
-    j2.set_input(1, mn.set_input(ScanSet(db, "q02_cand")))
+    j2.set_input(0, j)
+    j2.set_input(1, mn.set_input(j))
     best = _TreeFilter(lambda x: x.ps_supplycost == x.mincost).set_input(j2)
     if client.storage.has_set(db, "q02_out"):
         client.remove_set(db, "q02_out")

@@ -52,6 +52,10 @@ def main():
     ap.add_argument("--check", type=int, default=1, help="compare model 0's scores with an fp32 reference")
     ap.add_argument("--gpus", type=int, default=1, help="ranks to start when not under torchrun (one per GPU)")
     ap.add_argument("--small", action="store_true", help="CPU / contract size (8 models of 20 x 4000, blocks 10 x 400)")
+    ap.add_argument("--overlap", type=int, default=1,
+                    help="1: the private panels' GEMM on a second stream, concurrent with the common panel's")
+    ap.add_argument("--ab-overlap", type=int, default=0,
+                    help="N > 0: also time N interleaved rounds of overlap off / on (ab_overlap in the JSON)")
     a = ap.parse_args()
     if a.small:
         a.models, a.rows, a.cols, a.block_rows, a.block_cols, a.shared_blocks, a.batch = 8, 20, 4000, 10, 400, 9, 16
@@ -185,11 +189,22 @@ def main():
         if si is not None:
             si.run(X)
 
+    if si is not None:
+        si.overlap = bool(a.overlap)
     for _ in range(a.warmup):
         infer_naive()
         infer_dedup()
     t_naive = timed(infer_naive, a.steps)
     t_dedup = timed(infer_dedup, a.steps)
+    ab = None
+    if a.ab_overlap > 0 and si is not None:
+        ab = {"off_ms": [], "on_ms": []}
+        for _ in range(a.ab_overlap):
+            for flag, k in ((False, "off_ms"), (True, "on_ms")):
+                si.overlap = flag
+                infer_dedup()
+                ab[k].append(round(timed(infer_dedup, max(a.steps, 20)) * 1e3, 4))
+        si.overlap = bool(a.overlap)
 
     err = None
     if a.check and 0 in mine:
@@ -213,7 +228,8 @@ def main():
             "infer_naive_rows_per_s": round(rows / t_naive, 1), "infer_naive_ms": round(t_naive * 1e3, 3),
             "infer_dedup_ms": round(t_dedup * 1e3, 3), "dedup_speedup": round(t_naive / t_dedup, 2),
             "panel_GB_dedup": round((si.panel_bytes() if si else 0) / 1e9, 3),
-            "panel_GB_naive": round(len(mine) * R * C * 2 / 1e9, 3), "rel_err_model0": err, **comm}), flush=True)
+            "panel_GB_naive": round(len(mine) * R * C * 2 / 1e9, 3), "rel_err_model0": err,
+            "overlap": bool(a.overlap), "ab_overlap": ab, **comm}), flush=True)
     if ctx.distributed:
         torch.distributed.destroy_process_group()
 
