@@ -561,7 +561,8 @@ __device__ __forceinline__ void jit_join_agg_body(const PipeArgs& a) {
 // densely into ITS region [w * cap, (w + 1) * cap) of every output column (out + c * ostride): no global atomics,
 // deterministic placement; tile_cnt[w] = rows written, status[0] |= 1 when a region overflowed (the host then runs
 // the batch eagerly). Per block of NTHR * ROWS rows: a count pass, a workgroup exclusive scan in LDS, a write pass
-// (segment B is re-run for the write only when some lane of the wave walked more than one match).
+// (segment B is re-run for the write only when some lane of the wave walked more than one match). P::emit also gets
+// the row's index and its matched build row: the "pairs" form of a fused filter + join probe emits exactly those two.
 template <typename P>
 __device__ __forceinline__ void jit_emit_body(const PipeArgs& a, unsigned long long* __restrict__ out, long long tile_rows,
                                               long long cap, long long ostride, unsigned* __restrict__ tile_cnt) {
@@ -653,7 +654,7 @@ __device__ __forceinline__ void jit_emit_body(const PipeArgs& a, unsigned long l
         for (int j = 0; j < ROWS; ++j) {
           if (!keep[j] || !P::keep2(R[j])) continue;     // keep[j] => exactly one match (trips <= 1)
           u64 w[NE];
-          P::emit(R[j], w);
+          P::emit(R[j], w, row[j], P::JOIN ? (long long)pay[j] : 0ll);
 #pragma unroll
           for (int c = 0; c < NE; ++c) region[c * ostride + o] = w[c];
           ++o;
@@ -674,7 +675,7 @@ __device__ __forceinline__ void jit_emit_body(const PipeArgs& a, unsigned long l
           for (int j = 0; j < ROWS; ++j) {
             if (!act[j] || !P::keep2(R[j])) continue;
             u64 w[NE];
-            P::emit(R[j], w);
+            P::emit(R[j], w, row[j], brow[j]);
 #pragma unroll
             for (int c = 0; c < NE; ++c) region[c * ostride + o] = w[c];
             ++o;

@@ -10,6 +10,7 @@ happen exactly once per sink on every rank, so ranks stay in lock-step.
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import Dict, List, Optional
 
@@ -142,6 +143,8 @@ class QueryEngine:
         self._last_comps = None
         # fused filter -> project -> aggregate stages (execution/pipeline.py, csrc/kernels/pipeline.hip)
         self.fused_pipelines = True
+        # [filter ->] join probe runs outside aggregation stages as one compiled launch emitting (probe, build) rows
+        self.fused_probes = os.environ.get("NSDB_FUSED_PROBES", "1") != "0"
         self.pipeline_stats = {"fused_stages": 0, "fused_batches": 0, "fallback_batches": 0}
 
     def clone(self) -> "QueryEngine":
@@ -149,7 +152,7 @@ class QueryEngine:
         (dict access under the GIL); its own per-job state (spools, statistics)."""
         e = QueryEngine(self.storage, self.ctx, self.catalog, self.tracer, self.broadcast_threshold, self.fusion)
         for k in ("adaptive", "plan_cache_enabled", "ooc_fraction", "shuffle_chunk_bytes",
-                  "operand_prefetch", "fused_pipelines", "device_timing"):
+                  "operand_prefetch", "fused_pipelines", "fused_probes", "device_timing"):
             setattr(e, k, getattr(self, k))
         e._plan_cache = self._plan_cache
         e.__dict__["meta_cache"] = self.__dict__.setdefault("meta_cache", {})
@@ -475,10 +478,12 @@ class QueryEngine:
     def _apply_ops(self, ops, it, state):
         """Stream batches through a segment's atoms (generator: one page in flight per stage). Runs of lambda-tree
         APPLYs ending in their FILTER execute as one fused predicate launch (execution/pipeline.py)."""
-        if self.fused_pipelines and any(o["type"] == "FILTER" for o in ops):
+        if self.fused_pipelines and any(o["type"] in ("FILTER", "JOIN") for o in ops):
             from . import pipeline as PL
 
             ops = PL.fuse_filters(ops, state.comps)
+            if self.fused_probes:
+                ops = PL.fuse_probes(ops)
         for b in it:
             for o in ops:
                 if b.n == 0 and o["type"] != "JOIN":
@@ -605,6 +610,20 @@ class QueryEngine:
             return RecordBatch(cols, len(flat))
         if t == "JOIN":
             return self._probe(a, b, state)
+        if t == "FUSED_PROBE":
+            from . import pipeline as PL
+
+            plan = a["plan"]
+            plan.builds = state.builds
+            r = PL.run_probe(plan, b)
+            if r is not None:
+                self.pipeline_stats["fused_probes"] = self.pipeline_stats.get("fused_probes", 0) + 1
+                return self._join_output(a["join"], b, r[0], r[1], state.builds[a["join"]["output"]["name"]])
+            for o in a["atoms"]:
+                if b.n == 0 and o["type"] != "JOIN":
+                    break
+                b = self._apply_atom(o, b, state)
+            return b
         if t == "FUSED_FILTER":
             from . import pipeline as PL
 
@@ -629,6 +648,13 @@ class QueryEngine:
             bi = pi = torch.empty(0, dtype=torch.int64, device=b.device)
         else:
             bi, pi = bt.table(probe_h.device).probe(probe_h)
+        return self._join_output(a, b, pi, bi, bt)
+
+    def _join_output(self, a, b: RecordBatch, pi, bi, bt: "BuildTable") -> RecordBatch:
+        """The JOIN's output batch: its probe-side projection at probe rows ``pi`` of ``b`` next to its build-side
+        projection at build rows ``bi`` (row selections; columns materialise lazily)."""
+        side = a["_probe_side"]
+        lcols, rcols = a["projection"]["atts"], a["projection2"]["atts"]
         pb = RecordBatch({c: b.columns[c] for c in (lcols if side == "left" else rcols)}, b.n).take(pi)
         if bt.batch is None:
             bb_cols = {c: [] for c in (rcols if side == "left" else lcols)}

@@ -1060,8 +1060,9 @@ def _run_emit(plan: StagePlan, batch: RecordBatch, on_gpu: bool) -> Optional[Rec
     return EmittedBatch({plan.kcol: key, plan.vcol: vals}, m)
 
 
-def _launch_emit(prog: Program, n: int, dev, plan: StagePlan):
-    """The emitted form's launch: (int64 words [ne, rows] on the device, rows), or None on a region overflow."""
+def _launch_emit(prog: Program, n: int, dev, plan: StagePlan, kind: str = "emit"):
+    """The emitted form's launch: (int64 words [ne, rows] on the device, rows), or None on a region overflow. ``kind``
+    "pairs": the (probe row, build row) of every kept, matched row (a fused filter + join probe)."""
     h = _ext.hip()
     if not hasattr(h, "pipe_emit"):
         raise Unfusable("no emit kernels in this build")
@@ -1071,13 +1072,14 @@ def _launch_emit(prog: Program, n: int, dev, plan: StagePlan):
     bn = -1
     if plan.join is not None:
         jtab, jperm, bn = _join_table(plan, dev)
-    jit = _jit_for(prog, cargs, "emit", -1, prog.val_regs, dev)
+    jit = _jit_for(prog, cargs, kind, -1, prog.val_regs if kind == "emit" else (), dev)
     if jit is None:
         raise Unfusable("the emitted form needs the compiled kernels")
     fn, jnreg, jrows = jit
-    ne = len(prog.emit_keys) + len(prog.val_regs)
+    ne = 2 if kind == "pairs" else len(prog.emit_keys) + len(prog.val_regs)
     tile = 256 * jrows * EMIT_TILE_BLOCKS
-    cap = tile * (2 if plan.join is not None else 1)
+    # a tile's region: its rows times the plan's expected matches per row (joins: 2, raised after an overflow)
+    cap = tile * (getattr(plan, "cap_mult", 2) if plan.join is not None else 1)
     words, status = h.pipe_emit(ins, prog.nins_a, cargs, lit, n, prog.keep_reg, -1, prog.val_regs, prog.kpool, fn,
                                 jnreg, jrows, max(1, ne), tile, cap, jtab, jperm, bn)
     if int(status[0]) != 0:
@@ -1256,7 +1258,7 @@ def jit_source(prog: Program, kinds, lates, kind: str, key_reg: int = -1, val_re
     kinds. "emit" writes every kept row's key-part registers (prog.emit_keys) and value registers."""
     nreg = program_nreg(prog, len(kinds), key_reg, val_regs)
     F = max(1, len(val_regs))
-    staged = kind in ("agg", "emit")                 # segment A / late columns / segment B split
+    staged = kind in ("agg", "emit", "pairs")        # segment A / late columns / segment B split
     nins_a = prog.nins_a if staged else len(prog.ins)
     emit_regs = [k[0] for k in getattr(prog, "emit_keys", [])] + list(val_regs)
 
@@ -1282,7 +1284,7 @@ def jit_source(prog: Program, kinds, lates, kind: str, key_reg: int = -1, val_re
     if kind == "agg":
         entry = ("extern \"C\" __global__ void __launch_bounds__(nsdb_pipe::NTHR) nsdb_jit_agg(const nsdb_pipe::PipeArgs a) {\n"
                  f"  nsdb_pipe::{body}<nsdb_pipe::JitProg>(a);\n}}\n")
-    elif kind == "emit":
+    elif kind in ("emit", "pairs"):
         entry = ("extern \"C\" __global__ void __launch_bounds__(nsdb_pipe::NTHR) nsdb_jit_emit(const nsdb_pipe::PipeArgs a, "
                  "unsigned long long* out, long long tile_rows, long long cap, long long ostride, unsigned* tile_cnt) {\n"
                  "  nsdb_pipe::jit_emit_body<nsdb_pipe::JitProg>(a, out, tile_rows, cap, ostride, tile_cnt);\n}\n")
@@ -1290,12 +1292,15 @@ def jit_source(prog: Program, kinds, lates, kind: str, key_reg: int = -1, val_re
         entry = ("extern \"C\" __global__ void __launch_bounds__(nsdb_pipe::NTHR) nsdb_jit_mask(const nsdb_pipe::PipeArgs a, "
                  "unsigned char* mask) {\n  nsdb_pipe::jit_mask_body<nsdb_pipe::JitProg>(a, mask);\n}\n")
     emit = "".join(f"    w[{i}] = r[{reg}];\n" for i, reg in enumerate(emit_regs)) or "    w[0] = 0ull; (void)r;\n"
+    ne = max(1, len(emit_regs))
+    if kind == "pairs":                              # a fused filter + probe: (probe row, build row) per match
+        emit, ne = "    (void)r;\n    w[0] = (u64)row;\n    w[1] = (u64)brow;\n", 2
     return f"""// generated by netsdb_amd.execution.pipeline.jit_source ({kind})
 #include "pipeline_core.h"
 namespace nsdb_pipe {{
 struct JitProg {{
   static constexpr int F = {F}, NR = {nreg}, ROWS = {rows}, JK = {max(0, getattr(prog, "jk_reg", -1))};
-  static constexpr int NE = {max(1, len(emit_regs))};
+  static constexpr int NE = {ne};
   static constexpr bool JOIN = {"true" if join else "false"};
   template <bool LATE, bool FULL>
   __device__ static __forceinline__ void load(const PipeArgs& a, const long long (&row)[ROWS], const bool (&m)[ROWS],
@@ -1321,7 +1326,8 @@ struct JitProg {{
   __device__ static __forceinline__ long long key(const u64 (&r)[NR]) {{ (void)r; return {key}; }}
   __device__ static __forceinline__ void vals(const u64 (&r)[NR], double (&v)[F]) {{
 {vals}  }}
-  __device__ static __forceinline__ void emit(const u64 (&r)[NR], u64 (&w)[NE]) {{
+  __device__ static __forceinline__ void emit(const u64 (&r)[NR], u64 (&w)[NE], long long row, long long brow) {{
+    (void)row; (void)brow;
 {emit}  }}
 }};
 }}  // namespace nsdb_pipe
@@ -1392,7 +1398,7 @@ def _jit_for(prog: Program, cargs, kind: str, key_reg: int = -1, val_regs=(), de
     if not JIT or not hasattr(_ext.hip(), "jit_compile"):
         return None
     kinds = tuple(c[0] for c in cargs)
-    lates = tuple(c[1] for c in cargs) if kind in ("agg", "emit") else ()
+    lates = tuple(c[1] for c in cargs) if kind in ("agg", "emit", "pairs") else ()
     # the kernel of a program shape: generated + compiled once, then found by the shape alone (generating the source
     # costs ~30 us of Python per launch)
     shape = (_dev_index(dev), kind, tuple(prog.ins), kinds, lates, key_reg, tuple(val_regs), prog.keep_reg,
@@ -1407,7 +1413,8 @@ def _jit_for(prog: Program, cargs, kind: str, key_reg: int = -1, val_regs=(), de
             src = jit_source(prog, list(kinds), list(lates) or [0] * len(kinds), kind, key_reg, val_regs, rows=rows)
         except Unfusable:
             return None
-        fn = jit_kernel(src, {"agg": "nsdb_jit_agg", "emit": "nsdb_jit_emit"}.get(kind, "nsdb_jit_mask"), dev)
+        fn = jit_kernel(src, {"agg": "nsdb_jit_agg", "emit": "nsdb_jit_emit", "pairs": "nsdb_jit_emit"}.get(
+            kind, "nsdb_jit_mask"), dev)
         if len(_JIT_SHAPES) >= 4096:          # the shape includes the immediates: bound it for varying literals
             _JIT_SHAPES.clear()
         hit = _JIT_SHAPES[shape] = (fn, nreg, rows)
@@ -1698,6 +1705,94 @@ def _run_program(prog: Program, n: int, lo: int = 0, hi: Optional[int] = None, s
     return regs
 
 
+# ---------------------------------------------------------------------------------------------- fused probe
+class ProbePlan(StagePlan):
+    """[lambda-tree APPLYs + FILTER] -> HASH -> JOIN probe as ONE compiled launch (the "pairs" emit form): predicate,
+    probe of the build side's device hash table and the CSR walk of repeated keys in registers, writing the (probe
+    row, build row) of every kept, matched row. The join's output is then two row selections (lazy takes) — no mask,
+    compaction, key gather, hash column or probe / expand passes (reference JoinProbe in the pipeline chain,
+    src/lambdas/headers/JoinTuple.h:434)."""
+
+    def __init__(self, atoms, conj: List[E], join_atom: dict, key_col: str):
+        super().__init__([], atoms, conj, E("const", (), 0), E("vals", ()), "sum", "", "",
+                         join={"name": join_atom["output"]["name"], "key": E("src", (), key_col)})
+        self.jatom = join_atom
+        self.cap_mult = 2
+
+
+def fuse_probes(ops: List[dict]) -> List[dict]:
+    """``ops`` (after fuse_filters) with every [FUSED_FILTER]? HASHLEFT/RIGHT JOIN run whose probe key is one plain
+    column of the incoming batch replaced by one FUSED_PROBE op (its atoms kept for the eager fallback)."""
+    out: List[dict] = []
+    i = 0
+    while i < len(ops):
+        o = ops[i]
+        nxt = ops[i + 1] if i + 1 < len(ops) else None
+        if o["type"] in ("HASHLEFT", "HASHRIGHT") and nxt is not None and nxt["type"] == "JOIN" and \
+                len(o["input"]["atts"]) == 1 and nxt.get("_strategy") != "partitioned":
+            side = nxt.get("_probe_side")
+            probe_in = nxt["input"] if side == "left" else nxt["input2"] if side == "right" else None
+            if probe_in is not None and probe_in["name"] == o["output"]["name"] and \
+                    probe_in["atts"][0] == o["output"]["atts"][-1]:
+                key = o["input"]["atts"][0]
+                ff = out[-1] if out and out[-1]["type"] == "FUSED_FILTER" else None
+                if ff is not None and key not in ff["plan"].proj:
+                    ff = None
+                if ff is not None:
+                    out.pop()
+                    atoms, conj = ff["atoms"] + [o, nxt], list(ff["plan"].conj)
+                else:
+                    atoms, conj = [o, nxt], []
+                out.append({"type": "FUSED_PROBE", "plan": ProbePlan(atoms, conj, nxt, key), "atoms": atoms,
+                            "join": nxt})
+                i += 2
+                continue
+        out.append(o)
+        i += 1
+    return out
+
+
+def run_probe(plan: ProbePlan, batch: RecordBatch):
+    """(probe rows, build rows) of every kept, matched row of ``batch`` from one compiled launch, or None (eager atoms:
+    no compiled kernels, a column the kernel cannot read, an empty or out-of-core build side, a region overflow)."""
+    if plan.disabled or batch.n == 0:
+        return None
+    dev = batch.device
+    on_gpu = dev.type == "cuda" and _ext.hip() is not None and hasattr(_ext.hip(), "pipe_emit")
+    if not on_gpu and not (CPU_INTERPRETER and dev.type == "cpu"):
+        return None
+    try:
+        prog = _compile_cached(plan, batch, "pairs")
+        got = _launch_emit(prog, batch.n, dev, plan, "pairs") if on_gpu else interpret_pairs(prog, batch.n, plan)
+    except Unfusable as e:
+        plan.disabled = True
+        plan.reason = str(e)
+        return None
+    if got is None:                      # more matches per probe row than the tile regions hold: wider next time
+        plan.cap_mult *= 4
+        if plan.cap_mult > 32:
+            plan.disabled = True
+        return None
+    words, m = got
+    plan.stats["fused_batches"] += 1
+    return words[0], words[1]
+
+
+def interpret_pairs(prog: Program, n: int, plan: StagePlan):
+    """The "pairs" form with whole-column torch ops (CPU model): (int64 [2, m] probe rows / build rows, m)."""
+    from . import kernels as KK
+
+    regs = _run_program(prog, n, hi=prog.nins_a, sides=(0,))
+    keep = torch.ones(n, dtype=torch.bool) if prog.keep_reg < 0 else regs[prog.keep_reg] != 0
+    kidx = keep.nonzero().flatten()
+    bt = plan.builds[plan.join["name"]]
+    if bt.batch is None or bt.batch.n == 0:
+        raise Unfusable("empty build side")
+    bi, pi = bt.table(kidx.device).probe(KK.hash_keys(regs[prog.jk_reg][kidx]))
+    prow = kidx[pi]
+    return torch.stack([prow, bi.to(prow.dtype)]), int(prow.numel())
+
+
 # ---------------------------------------------------------------------------------------------- fused FILTER
 class FilterPlan(StagePlan):
     """A run of lambda-tree APPLY atoms ending in their FILTER: the predicate as one mask launch (pipe_mask)."""
@@ -1800,4 +1895,4 @@ def interpret_mask(prog: Program, n: int) -> torch.Tensor:
 
 
 __all__ = ["plan_stage", "run_batch", "StagePlan", "Unfusable", "interpret", "interpret_join", "fuse_filters", "run_filter",
-           "FilterPlan"]
+           "FilterPlan", "ProbePlan", "fuse_probes", "run_probe", "interpret_pairs"]

@@ -73,10 +73,18 @@ def test_jit_sources_compile_cpu(monkeypatch):
     progs = list(PL._PROG_CACHE.values())
     assert len(progs) >= len(QUERIES) + len(FILTER_QUERIES), len(progs)
     h, hdr, seen = _ext.hip(), PL._jit_header(), set()
-    joins = 0
+    joins = pairs = 0
     for p in progs:
         kinds = [cc["kind"] for cc in p.cols]
         lates = [cc["late"] for cc in p.cols]
+        if p.mode == "pairs":                  # a fused filter + probe outside an aggregation: (probe, build) rows
+            pairs += 1
+            src = PL.jit_source(p, kinds, lates, "pairs")
+            assert "jit_emit_body" in src and "w[1] = (u64)brow" in src
+            if src not in seen:
+                seen.add(src)
+                assert len(h.jit_compile(src, hdr)) > 1000
+            continue
         if p.jk_reg >= 0:                      # a fused join probe: the aggregate kernel only (jit_join_agg_body)
             joins += 1
             src = PL.jit_source(p, kinds, lates, "agg", p.key_reg, p.val_regs)
@@ -94,8 +102,9 @@ def test_jit_sources_compile_cpu(monkeypatch):
             if src not in seen:
                 seen.add(src)
                 assert len(h.jit_compile(src, hdr)) > 1000
-    assert len(seen) >= len(progs)
+    assert len(seen) >= len(progs) - pairs     # pairs programs of one shape share a source
     assert joins >= 2, joins                   # q12 and q14 probe their build tables inside the fused kernel
+    assert pairs >= 3, pairs                   # q02 / q03 / q04 filter + probe stages
     # the emitted (high-cardinality) form of every stage: tables capped so each stage overflows once
     PL._PROG_CACHE.clear()
     PL._EMIT_SIGS.clear()
@@ -582,3 +591,58 @@ def test_fused_join_probe_gpu(case):
     assert PL.JIT_STATS["launches"] > f0
     assert eager[0] == fused[0]
     assert torch.allclose(eager[1], fused[1], rtol=1e-9, atol=1e-6)
+
+
+def _join_rows(c, case, name):
+    """The JOIN_CASES join written to a set (no aggregation after it: the fused "pairs" probe or the eager atoms),
+    as sorted row tuples of the picked columns."""
+    probe, build, keys, pick, _k, _v, _op = JOIN_CASES[case]
+    j = tpch._EqJoin(2, keys, tpch._pick(pick))
+    j.set_input(0, probe("tpch"))
+    j.set_input(1, build("tpch"))
+    if c.storage.has_set("tpch", name):
+        c.remove_set("tpch", name)
+    c.create_set("tpch", name, None)
+    c.execute_computations(WriteSet("tpch", name).set_input(j))
+    cols = [x for side in pick for x in side]
+    rows = []
+    for b in c.get_set_batches("tpch", name):
+        b = tpch._flat(b)
+        if b is None or not b.n:
+            continue
+        vals = [b.columns[x] for x in cols]
+        vals = [v.tolist() if hasattr(v, "tolist") else list(v) for v in vals]
+        rows.extend(zip(*vals))
+    return sorted(rows)
+
+
+@pytest.mark.parametrize("case", sorted(JOIN_CASES))
+def test_fused_probe_pairs_cpu_interpreter(case, monkeypatch):
+    """[filter ->] probe with no aggregation after it (torch model of the "pairs" emit form) == the eager atoms,
+    repeated build keys included."""
+    monkeypatch.setenv("NSDB_DEVICE_STRINGS", "1")
+    t = tpch_gen.generate_fast(0.003, seed=6)
+    c = _client("cpu", t)
+    eager = _join_rows(c, case, "pe")
+    assert eager
+    monkeypatch.setattr(PL, "CPU_INTERPRETER", True)
+    p0 = c.engine.pipeline_stats.get("fused_probes", 0)
+    fused = _join_rows(c, case, "pf")
+    assert c.engine.pipeline_stats.get("fused_probes", 0) > p0, c.engine.pipeline_stats
+    assert eager == fused
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", sorted(JOIN_CASES))
+def test_fused_probe_pairs_gpu(case):
+    """The compiled "pairs" kernel (predicate, probe, CSR walk of repeated build keys, per-tile regions + compaction)
+    against the eager filter / hash / probe / expand atoms."""
+    t = tpch_gen.generate_fast(0.05, seed=6)
+    c = _client("cuda:0", t)
+    c.engine.fused_pipelines = False
+    eager = _join_rows(c, case, "pe")
+    c.engine.fused_pipelines = True
+    p0 = c.engine.pipeline_stats.get("fused_probes", 0)
+    fused = _join_rows(c, case, "pf")
+    assert c.engine.pipeline_stats.get("fused_probes", 0) > p0, c.engine.pipeline_stats
+    assert eager and eager == fused
