@@ -355,6 +355,7 @@ def test_fused_tpch_gpu_vs_eager_and_pandas(tile, jit, monkeypatch):
     if jit:     # every fused launch took a compiled kernel; the emitted form and join probes exist there only
         assert st["fallback_batches"] == 0, st
         assert st.get("fused_join_batches", 0) >= 3 and st.get("emitted_batches", 0) >= 1, st
+        assert st.get("fused_probes", 0) >= 3, st     # q02 / q03 / q04: filter + probe stages as "pairs" launches
         assert PL.JIT_STATS["failed"] == j0["failed"], PL.JIT_STATS
         assert PL.JIT_STATS["launches"] - j0["launches"] >= len(QUERIES) + len(FILTER_QUERIES), PL.JIT_STATS
     else:
