@@ -514,11 +514,11 @@ class SharedInference:
             Y = self._private(X, P)
         return {n: Y[i, : self.R] for i, n in enumerate(self.names)}
 
-    # Private panels concurrent with the common panel (run(): two HIP streams). Both GEMMs stream HBM at ~5 TB/s,
-    # but each drains its last wave of tiles and its split-K reduce alone; side by side, one kernel's tail overlaps
-    # the other's body. The private result then no longer accumulates onto P in its epilogue: one broadcast add
-    # (2.4 MB at config 5) joins them.
-    overlap = True
+    # Private panels concurrent with the common panel (run(): two HIP streams), the private result joined by one
+    # broadcast add instead of accumulating onto P in its epilogue. Measured slower at config 5 (interleaved, 5 x 20
+    # runs: 0.492 vs 0.480 ms, profiles/r6_dedup/dedup_overlap_ab.json: both GEMMs already stream HBM with the whole
+    # GPU, so running them side by side only splits the bandwidth), so it is off by default.
+    overlap = False
     _side: Dict[torch.device, "torch.cuda.Stream"] = {}
 
     def _private(self, X: torch.Tensor, Y: Optional[torch.Tensor]) -> torch.Tensor:

@@ -47,12 +47,12 @@ def main():
     ap.add_argument("--block-cols", type=int, default=10_000)
     ap.add_argument("--shared-blocks", type=int, default=90, help="column blocks shared by every model")
     ap.add_argument("--batch", type=int, default=100)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--check", type=int, default=1, help="compare model 0's scores with an fp32 reference")
     ap.add_argument("--gpus", type=int, default=1, help="ranks to start when not under torchrun (one per GPU)")
     ap.add_argument("--small", action="store_true", help="CPU / contract size (8 models of 20 x 4000, blocks 10 x 400)")
-    ap.add_argument("--overlap", type=int, default=1,
+    ap.add_argument("--overlap", type=int, default=0,
                     help="1: the private panels' GEMM on a second stream, concurrent with the common panel's")
     ap.add_argument("--ab-overlap", type=int, default=0,
                     help="N > 0: also time N interleaved rounds of overlap off / on (ab_overlap in the JSON)")
