@@ -89,6 +89,9 @@ def main():
     ap.add_argument("--single-job", action="store_true", help=argparse.SUPPRESS)   # the default; kept for old scripts
     ap.add_argument("--mfma", type=int, choices=[0, 16, 32], default=0,
                     help="8-phase GEMM main-loop MFMA shape for this run (0 = the library default; A/B arm)")
+    ap.add_argument("--fixup", type=int, choices=[-1, 0, 1], default=-1,
+                    help="layer-1 split-K reduction inside the GEMM launch (1) or the separate reducer (0); "
+                         "-1 = the library default")
     args = ap.parse_args()
     args.single_job = not args.two_job
     from netsdb_amd.parallel import launch
@@ -105,6 +108,8 @@ def main():
 
     if args.mfma:
         ops.set_kernel_options(gemm_mfma=args.mfma)
+    if args.fixup >= 0:
+        ops.set_kernel_options(gemm_fixup=args.fixup)
     cfg = SMALL if args.small else FULL
     ctx = ClusterContext.from_env()
     if ctx.world_size != args.gpus and ctx.rank == 0:
@@ -210,6 +215,7 @@ def main():
                 "collectives_per_step": round(coll_per_step, 2),
                 "single_job": bool(args.single_job),
                 "gemm_mfma": args.mfma or "default",
+                "gemm_fixup": args.fixup if args.fixup >= 0 else "default",
             },
         }
         print(json.dumps(res), flush=True)

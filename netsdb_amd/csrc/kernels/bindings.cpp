@@ -86,7 +86,11 @@ struct GemmOpts {
   long long pf_bytes;
   int kinter;
   int mfma;
+  int fixup;
+  int* fx_state;
 };
+
+torch::Tensor softmax_state(const torch::Tensor& like, int64_t need, hipStream_t st);
 
 void check_rc(int rc, const char* what) {
   TORCH_CHECK(rc == 0, what, " failed with code ", rc, " (", hipGetErrorString((hipError_t)(rc > 0 ? rc : 0)), ")");
@@ -108,7 +112,7 @@ bool is_f32(const torch::Tensor& t, const char* name) {
 torch::Tensor gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Tensor> bias, int64_t bias_mode,
                       int64_t act, bool out_f32, double alpha, double dropout, int64_t seed, int64_t splits,
                       c10::optional<torch::Tensor> out, bool accumulate, int64_t cfg, int64_t epi,
-                      c10::optional<torch::Tensor> prefetch, int64_t mfma) {
+                      c10::optional<torch::Tensor> prefetch, int64_t mfma, int64_t fixup) {
   check_cuda(A, "A");
   check_cuda(B, "B");
   TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && B.scalar_type() == torch::kBFloat16, "A,B must be bf16");
@@ -165,7 +169,14 @@ torch::Tensor gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Ten
   }
   TORCH_CHECK(epi >= -1 && epi <= 1, "gemm_nt: epi must be -1 (auto), 0 (LDS-staged) or 1 (direct)");
   TORCH_CHECK(mfma == 0 || mfma == 16 || mfma == 32, "gemm_nt: mfma must be 0 (auto), 16 or 32");
-  GemmOpts o{(int)cfg, (int)epi, nullptr, 0, kinter, (int)mfma};
+  GemmOpts o{(int)cfg, (int)epi, nullptr, 0, kinter, (int)mfma, 0, nullptr};
+  if (fixup && s > 1) {
+    // the in-launch split-K reduction's arrival / departure words: zero between launches on this stream (shared
+    // with the fused softmax's, which also leaves them zero)
+    const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
+    o.fixup = 1;
+    o.fx_state = softmax_state(A, 2 * tiles, cur_stream()).data_ptr<int>();
+  }
   if (prefetch.has_value() && prefetch->defined() && prefetch->numel() > 0) {
     // the byte span of the tensor's elements (a strided view reads its whole span)
     check_cuda(*prefetch, "prefetch");
@@ -721,7 +732,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bias_mode") = 0, py::arg("act") = 0, py::arg("out_f32") = false, py::arg("alpha") = 1.0,
         py::arg("dropout") = 0.0, py::arg("seed") = 0, py::arg("splits") = 0, py::arg("out") = py::none(),
         py::arg("accumulate") = false, py::arg("cfg") = -1, py::arg("epi") = -1, py::arg("prefetch") = py::none(),
-        py::arg("mfma") = 0);
+        py::arg("mfma") = 0, py::arg("fixup") = 0);
   m.def("gemm_launch_wgs", [](int64_t M, int64_t N, int64_t K, int64_t batch, int64_t splits, int64_t cfg) {
           return (int64_t)nsdb_gemm_launch_wgs((int)M, (int)N, (int)K, (int)batch, (int)splits, (int)cfg);
         }, "workgroups of the GEMM launch for this shape (splits <= 0: the launcher's choice)",

@@ -386,6 +386,78 @@ __device__ __forceinline__ void sm_depart(const GemmParams& p, char* smem, bool 
   if (*slot == 2) sm_late_rescale<AXIS>(p, smem, grp, need, tid, lane, wave);
 }
 
+// ---- split-K reduction inside the launch (GemmParams::fixup; the layer-1 GEMM's 14.6 us reducer launch + gap).
+// Every workgroup of a tile, after its slab is written through (store_direct_8ph) and acknowledged, counts in on the
+// tile's arrival word and waits (bounded poll) for the tile's other splits; then split s reduces rows
+// [s * R, s * R + R) of the tile (R = 256 / splits, 16 at 16 splits) over all slabs in split order — the separate
+// reducer's summation order, so the result is bit-identical — with the reducer's epilogue (bias, activation,
+// dropout, bf16 / f32 store). A single workgroup fixing a whole tile reads 4 MiB through one CU (~30 us; the
+// rejected cfg-26 last-arriver design, profiles/r2_gemm1_study); split 16 ways it is 256 KiB per CU, a few us after
+// the tile's last split lands. The wait relies on the tile's splits being co-resident (the launch is one workgroup
+// per CU); if the poll times out (the GPU shared with another job), the workgroup skips its rows, flags itself on
+// the departure word, and the tile's last workgroup to leave reduces the whole tile (slow, never wrong or hung).
+// Slabs of other splits are read with device-scope loads (never a stale line of this XCD's L2).
+__device__ __forceinline__ void fixup_rows_8ph(const GemmParams& p, int m0, int n0, int r0, int r1, int tid, int nthr) {
+  const long long MN = (long long)p.M * p.N;
+  const int cols = min(256, p.N - n0);
+  const int q4 = (cols + 3) >> 2;                  // 4-column groups per row (N % 4 == 0: no partial group)
+  const int rows = min(r1, p.M - m0) - r0;
+  for (int e4 = tid; e4 < rows * q4; e4 += nthr) {
+    const int r = r0 + e4 / q4, c = (e4 % q4) * 4;
+    const long long e = (long long)(m0 + r) * p.N + n0 + c;
+    const unsigned long long* w = reinterpret_cast<const unsigned long long*>(p.ws + e);
+    const long long step = MN / 2;                 // one slab in 8-byte words
+    unsigned long long lo[32], hi[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k)
+      if (k < p.splits) {
+        lo[k] = __hip_atomic_load(w + k * step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        hi[k] = __hip_atomic_load(w + k * step + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    f32x4 s = f32x4{__uint_as_float((unsigned)lo[0]), __uint_as_float((unsigned)(lo[0] >> 32)),
+                    __uint_as_float((unsigned)hi[0]), __uint_as_float((unsigned)(hi[0] >> 32))};
+#pragma unroll
+    for (int k = 1; k < 32; ++k)
+      if (k < p.splits)
+        s += f32x4{__uint_as_float((unsigned)lo[k]), __uint_as_float((unsigned)(lo[k] >> 32)),
+                   __uint_as_float((unsigned)hi[k]), __uint_as_float((unsigned)(hi[k] >> 32))};
+    reduce_epilogue4(p, 0, MN, e, s);
+  }
+}
+
+__device__ __noinline__ void splitk_fixup_8ph(const GemmParams& p, int* slot, int tile, int split, int m0, int n0,
+                                              int tid) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this workgroup's slab stores acknowledged
+  __syncthreads();
+  if (tid == 0) {
+    int c = __hip_atomic_fetch_add(p.fx_cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (c < p.splits) {
+      __builtin_amdgcn_s_sleep(2);
+      c = __hip_atomic_load(p.fx_cnt + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 20000ull) break;   // 200 us at 100 MHz
+    }
+    slot[0] = c >= p.splits ? 1 : 0;
+  }
+  __syncthreads();
+  const bool ok = slot[0] != 0;
+  const int R = (256 + p.splits - 1) / p.splits;
+  if (ok) fixup_rows_8ph(p, m0, n0, split * R, min(256, split * R + R), tid, 512);
+  if (tid == 0) {
+    const int inc = ok ? 1 : 0x10001;
+    const int d = __hip_atomic_fetch_add(p.fx_dep + tile, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + inc;
+    int verdict = 0;
+    if ((d & 0xffff) == p.splits) {                // the last to leave: every split has passed its poll
+      verdict = (d >> 16) > 0 ? 2 : 1;
+      __hip_atomic_store(p.fx_cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p.fx_dep + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    slot[1] = verdict;
+  }
+  __syncthreads();
+  if (slot[1] == 2) fixup_rows_8ph(p, m0, n0, 0, 256, tid, 512);   // some split timed out: the whole tile here
+}
+
 // Direct epilogue of the unsplit 8-phase tile: every lane stores its own accumulators, 4 consecutive columns
 // of one row per (i, j) (the transposed TS layout: acc[i][j][r] = C[wr*128 + i*16 + rl][wc*64 + j*16 + cq + r]),
 // i.e. one 16-B (f32) / 8-B (bf16) store per lane and a wave instruction of 16 rows x 64 B. No LDS image, no
@@ -411,7 +483,14 @@ __device__ __forceinline__ void store_direct_8ph(const f32x4 (&acc)[8][4], const
         const int col = n0 + wc * 64 + j * 16 + cq;
         if (row < p.M && col < p.N) {
           float* d = ws + (long long)row * p.N + col;
-          if (col + 4 <= p.N) *reinterpret_cast<f32x4*>(d) = acc[i][j];   // N % 4 == 0 (host: vec_ws)
+          if (p.fixup) {   // in-launch reduction: written through to the device-coherent level (vec_ws: N % 4 == 0)
+            unsigned long long* d2 = reinterpret_cast<unsigned long long*>(d);
+            const f32x4 a = acc[i][j];
+            __hip_atomic_store(d2, ((unsigned long long)__float_as_uint(a[1]) << 32) | __float_as_uint(a[0]),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(d2 + 1, ((unsigned long long)__float_as_uint(a[3]) << 32) | __float_as_uint(a[2]),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          } else if (col + 4 <= p.N) *reinterpret_cast<f32x4*>(d) = acc[i][j];   // N % 4 == 0 (host: vec_ws)
           else {
 #pragma unroll
             for (int r = 0; r < 4; ++r)
@@ -907,6 +986,10 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
     store_tile_lds<256, 256, 2, 4, true>(acc, smem, 2 * BUF, p, batch, split, m0, n0, tid, lane, wave,
                                          reinterpret_cast<float*>(smem + 2 * BUF));
   }
+  if (p.fixup) {   // host: split-K, direct epilogue, batch 1 — LDS words past the tile buffers (free after the loop)
+    splitk_fixup_8ph(p, reinterpret_cast<int*>(smem + 2 * BUF), tm * p.tiles_n + tn, split, m0, n0, tid);
+    return;
+  }
   if (p.pf_ptr != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // prefetch DMAs retired
 }
 
@@ -1248,6 +1331,8 @@ struct GemmOpts {
   long long pf_bytes;
   int kinter;               // stream tiles: 1 = k-interleaved splits (split s takes k-tiles s, s + S, ...)
   int mfma;                 // 8-phase main loop: 0 auto, 16 = 16x16x32, 32 = 32x32x16 (direct epilogue launches)
+  int fixup;                // 8-phase split-K: 1 = reduce inside the launch (splitk_fixup_8ph), no reducer launch
+  int* fx_state;            // its arrival / departure words ([2 * tiles] ints, zero between launches on a stream)
 };
 
 extern "C" {
@@ -1419,6 +1504,12 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
     // the 32x32x16 main loop stores from registers only (store_direct_8ph32): launches that need the LDS-staged
     // epilogue (C += A.B^T, a per-element bias, unaligned C) stay on the 16x16x32 loop
     const int mf = opts ? opts->mfma : 0;
+    if (opts && opts->fixup && opts->fx_state && p.splits > 1 && p.splits <= 32 && p.direct_epi && p.vec_ws &&
+        batch == 1 && !(mf == 32)) {
+      p.fixup = 1;
+      p.fx_cnt = opts->fx_state;
+      p.fx_dep = opts->fx_state + p.tiles_m * p.tiles_n;
+    }
     if (mf == 32 && p.direct_epi)
       hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph32_kernel, grid, dim3(512), 0, stream, p);
     else
@@ -1438,7 +1529,7 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
   } else {
     hipLaunchKernelGGL((nsdb::gemm_nt_tile_kernel<128, 128, 2, 2>), grid, dim3(256), 0, stream, p);
   }
-  if (p.splits > 1) {
+  if (p.splits > 1 && !p.fixup) {
     const long long MN = (long long)M * N;
     const long long plain_blocks = ((p.vec_ws ? MN / 4 : MN) + 255) / 256;
     if (p.vec_ws && p.splits >= 8 && plain_blocks * batch < 512) {

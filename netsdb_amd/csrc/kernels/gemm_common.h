@@ -58,6 +58,13 @@ struct GemmParams {
   // 8-phase kernel, unsplit launches: store C straight from the accumulator registers (no LDS round trip;
   // see store_direct_8ph in gemm.hip). 0: the LDS-staged store_tile_lds epilogue.
   int direct_epi;
+  // 8-phase split-K launches: the reduction inside the launch (gemm.hip splitk_fixup_8ph). Slabs are written through
+  // to the device-coherent level; the splits of a tile count in on fx_cnt[tile], wait for each other (bounded), and
+  // each reduces 1/splits of the tile's rows; fx_dep[tile] counts departures (low 16 bits) and timed-out workgroups
+  // (high 16): the last to leave re-zeroes both and, after a time-out, reduces the whole tile itself.
+  int fixup = 0;
+  int* fx_cnt = nullptr;
+  int* fx_dep = nullptr;
 };
 
 // Adaptive split-K partition (8-phase kernel, split-K launches). The splits of one GEMM run on different XCDs

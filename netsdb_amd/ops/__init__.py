@@ -97,14 +97,16 @@ def _streams():
 
 
 def gemm_nt(A, B, bias=None, bias_mode=BIAS_NONE, act=ACT_NONE, out_dtype=torch.bfloat16, alpha=1.0,
-            dropout=0.0, seed=0, splits=0, out=None, accumulate=False, cfg=None, epi=None, mfma=None):
+            dropout=0.0, seed=0, splits=0, out=None, accumulate=False, cfg=None, epi=None, mfma=None, fixup=None):
     """epilogue(alpha * A @ B^T) [+ out when accumulate]: A [..,M,K], B [..,N,K] (K-contiguous),
     bias f32 per row/col. ``accumulate`` adds into an existing f32 ``out`` (C += A.B^T). ``cfg`` forces the
     tile config of THIS call (0 = 128x128, 2 = 256x256 8-phase, 3 / 4 = 256x128 / 128x256 skinny long-K stream;
     None = auto); ``epi`` the 8-phase kernel's
     unsplit epilogue (0 = LDS-staged, 1 = direct register stores; None = auto: direct); ``mfma`` the 8-phase main
     loop's matrix instruction (16 = 16x16x32, 32 = 32x32x16; None = the thread's ``kernel_options(gemm_mfma=...)``,
-    else the library default). An operand prefetch armed on
+    else the library default); ``fixup`` (8-phase split-K launches) 1 = the split-K reduction inside the launch (each
+    split reduces 1/splits of its tile's rows after the tile's splits meet; no reducer launch), 0 = the separate
+    reducer (None = the thread's ``kernel_options(gemm_fixup=...)``, else 0). An operand prefetch armed on
     the current stream (streams.arm_operand_prefetch: a later kernel's operand read into the Infinity Cache by this
     launch's workgroups as they finish) is handed to this launch when it is long enough to take it — per call and
     per stream, so GEMMs on other lanes or threads never see it."""
@@ -125,7 +127,8 @@ def gemm_nt(A, B, bias=None, bias_mode=BIAS_NONE, act=ACT_NONE, out_dtype=torch.
         return h.gemm_nt(A, B, bias, int(bias_mode if bias is not None else 0), act,
                          out_dtype == torch.float32, float(alpha), float(dropout), int(seed),
                          int(splits), out, bool(accumulate), c, -1 if epi is None else int(epi), pf,
-                         int(mfma if mfma is not None else _kopt("gemm_mfma", 0)))
+                         int(mfma if mfma is not None else _kopt("gemm_mfma", 0)),
+                         int(fixup if fixup is not None else _kopt("gemm_fixup", 0)))
     v = torch.matmul(A.float(), B.float().transpose(-1, -2)) * alpha
     if bias is not None:
         b = bias.float()
@@ -297,7 +300,7 @@ def conv_filter_fragments(Wflat, C, KH, KW):
 
 _KOPTS = threading.local()
 _KOPT_KEYS = {"conv_kernel", "conv_blocks", "conv_generic", "conv_variant", "conv_contig", "rownorm_plain_loads",
-              "hash_groupby", "gemm_mfma"}
+              "hash_groupby", "gemm_mfma", "gemm_fixup"}
 
 
 @contextlib.contextmanager
@@ -307,7 +310,8 @@ def kernel_options(**kw):
     conv_blocks (row-kernel grid cap, default 512; 0 = one block per row group), conv_generic (bool: the generic
     gather kernel), conv_variant / conv_contig (row-kernel diagnostics), rownorm_plain_loads (bool: row normalise
     with cache-allocating loads), hash_groupby (bool: device hash-table group ids, default off), gemm_mfma (16 / 32:
-    the 8-phase GEMM main loop's MFMA shape; default the library's). Every option is
+    the 8-phase GEMM main loop's MFMA shape; default the library's), gemm_fixup (0 / 1: split-K reduction inside the
+    8-phase launch). Every option is
     passed per call to the kernel library, which keeps no process-wide launch state: other threads (server requests, job lanes on their own threads) never see them."""
     bad = set(kw) - _KOPT_KEYS
     if bad:

@@ -145,6 +145,26 @@ def test_gemm_8ph_mfma32_ff_layer1_shape():
     _close(C, _ref_gemm(A, B), tol=1e-2)
 
 
+@pytest.mark.parametrize("M,N,K,splits", [(1000, 1000, 65536, 16), (513, 260, 8200, 3), (300, 1028, 64000, 32),
+                                          (1000, 1000, 640, 5)])
+@pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
+def test_gemm_8ph_split_k_fixup_bit_exact(M, N, K, splits, out_dtype):
+    """The split-K reduction inside the 8-phase launch (splits of a tile meet, each reduces its rows) is bit-identical
+    to the separate reducer — the same slabs summed in split order, the same epilogue (bias, relu, dropout) — on
+    ragged M / N edges, three launches in a row (the arrival / departure words are re-zeroed by each launch)."""
+    torch.manual_seed(13)
+    A = (torch.rand(M, K, device=DEV) - 0.5).to(torch.bfloat16)
+    B = (torch.rand(N, K, device=DEV) - 0.5).to(torch.bfloat16)
+    bias = torch.rand(N, device=DEV) - 0.5
+    kw = dict(bias=bias, bias_mode=ops.BIAS_COL, act=ops.ACT_RELU, dropout=0.5, seed=3, out_dtype=out_dtype, cfg=2,
+              splits=splits)
+    ref = ops.gemm_nt(A, B, fixup=0, **kw)
+    for _ in range(3):
+        got = ops.gemm_nt(A, B, fixup=1, **kw)
+        assert torch.equal(got, ref)
+    _close(ops.gemm_nt(A, B, fixup=1, out_dtype=torch.float32, cfg=2, splits=splits), _ref_gemm(A, B), tol=1e-2)
+
+
 def test_gemm_batched_strided(gemm_cfg):
     torch.manual_seed(2)
     A = torch.randn(3, 130, 200, device=DEV).to(torch.bfloat16)[:, :, :192]   # row stride 200 > K
