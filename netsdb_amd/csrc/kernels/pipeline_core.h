@@ -224,6 +224,19 @@ __device__ __forceinline__ double wave_reduce(double v, int op) {
 }
 
 
+// Overflow of a fused aggregation (more groups than the tables hold): the launch's result is discarded and the host
+// re-runs the batch in the emitted form, so the scan stops as soon as any workgroup has overflowed — its own flag
+// every iteration (LDS), the launch's status word every 16 (a full LDS table otherwise costs every later row a probe
+// of all CAP slots: a 60 M-row scan that overflowed early measured 67-77 ms instead of ~0.5).
+__device__ __forceinline__ bool agg_overflowed(const PipeArgs& a, int* s_ovf, int it) {
+  if (__hip_atomic_load(s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return true;
+  return (it & 15) == 15 && (__hip_atomic_load(a.table, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1ull);
+}
+__device__ __forceinline__ void agg_mark_overflow(const PipeArgs& a, int* s_ovf) {
+  __hip_atomic_store(s_ovf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __hip_atomic_fetch_or(a.table, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ---------------------------------------------------------------- run-time compiled (JIT) kernel bodies
 // P (generated): F, NR, ROWS; load<LATE, FULL>(a, row, m, R) (the columns of one pass into their registers, 0 where m
 // is false; FULL: every row of the block is in range and unmasked, so the loads carry no per-row exec mask); run_a / run_b (the predicate / key-and-value segments); keep(r), key(r), vals(r, v). Registers are a
@@ -266,7 +279,9 @@ __device__ __forceinline__ void jit_agg_body(const PipeArgs& a) {
   }
 
   const long long step = (long long)gridDim.x * NTHR * ROWS;
-  for (long long base = (long long)blockIdx.x * NTHR * ROWS; base < a.n; base += step) {
+  int it = 0;
+  for (long long base = (long long)blockIdx.x * NTHR * ROWS; base < a.n; base += step, ++it) {
+    if (agg_overflowed(a, &s_ovf, it)) break;                 // the launch's result is discarded: stop scanning
     long long row[ROWS];
     bool inr[ROWS], keep[ROWS];
 #pragma unroll
@@ -314,8 +329,19 @@ __device__ __forceinline__ void jit_agg_body(const PipeArgs& a) {
         }
         ++used;
       }
-      if (!done) ovf |= (key == EMPTY) || !table_insert<F>(tk, tv, CAP, key, v, a.nval, a.agg_op);
+      if (!done && !ovf) {
+        ovf = (key == EMPTY) || !table_insert<F>(tk, tv, CAP, key, v, a.nval, a.agg_op);
+        if (ovf) agg_mark_overflow(a, &s_ovf);
+      }
     }
+  }
+  __syncthreads();
+  if (s_ovf) {                                               // no flush: the host re-runs the batch (emitted form)
+    if (tid == 0) {
+      atomicOr(a.table, 1ull);
+      atomicAdd(a.table + 1, (unsigned long long)kept);
+    }
+    return;
   }
 #pragma unroll
   for (int s = 0; s < KSLOT; ++s) {
@@ -414,7 +440,10 @@ __device__ __forceinline__ void agg_row(const PipeArgs& a, long long key, const 
     }
     ++used;
   }
-  if (!done) ovf |= (key == EMPTY) || !table_insert<F>(tk, tv, CAP, key, v, a.nval, a.agg_op);
+  if (!done && !ovf) {
+    ovf = (key == EMPTY) || !table_insert<F>(tk, tv, CAP, key, v, a.nval, a.agg_op);
+    if (ovf) __hip_atomic_fetch_or(a.table, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // seen by every loop
+  }
 }
 
 // register slots -> LDS table (wave-combined per key) -> the global table; status words
@@ -423,6 +452,17 @@ __device__ __forceinline__ void agg_flush(const PipeArgs& a, long long (&sk)[KSL
                                           bool ovf, unsigned long long kept, long long* tk, double* tv, int* s_ovf,
                                           unsigned long long* s_kept, double init) {
   const int tid = threadIdx.x, lane = tid & 63;
+  if (ovf) *s_ovf = 1;
+  __syncthreads();
+  if (*s_ovf || (__hip_atomic_load(a.table, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1ull)) {
+    atomicAdd(s_kept, kept);                       // the launch overflowed: no flush (the host re-runs the batch)
+    __syncthreads();
+    if (tid == 0) {
+      atomicOr(a.table, 1ull);
+      atomicAdd(a.table + 1, *s_kept);
+    }
+    return;
+  }
 #pragma unroll
   for (int s = 0; s < KSLOT; ++s) {
     bool act = s < used;
@@ -500,7 +540,9 @@ __device__ __forceinline__ void jit_join_agg_body(const PipeArgs& a) {
   }
 
   const long long step = (long long)gridDim.x * NTHR * ROWS;
-  for (long long base = (long long)blockIdx.x * NTHR * ROWS; base < a.n; base += step) {
+  int it = 0;
+  for (long long base = (long long)blockIdx.x * NTHR * ROWS; base < a.n; base += step, ++it) {
+    if (ovf || agg_overflowed(a, &s_ovf, it)) break;       // the launch's result is discarded: stop scanning
     long long row[ROWS], brow[ROWS];
     bool inr[ROWS], keep[ROWS], act[ROWS];
     unsigned cnt[ROWS], pay[ROWS];

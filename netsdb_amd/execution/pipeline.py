@@ -555,7 +555,8 @@ class _Compiler:
             self._collect(c, "num", "B", uses)
         keys = self._key_fields()
         for k in keys:
-            uses.append((k, "key", "B"))
+            if not self._row_key(k):
+                uses.append((k, "key", "B"))
         vals = plan.val.args if plan.val.kind == "vals" else (plan.val,)
         for v in vals:
             self._collect(v, "num", "B", uses)
@@ -621,6 +622,11 @@ class _Compiler:
                 p.emit_keys_const = k.val
             for e in keys:
                 obj = self._res(e)
+                if self._row_key(e):
+                    # a string longer than a short code: the row it comes from (probe row, or the matched build row);
+                    # the host takes the key strings by row afterwards (a view: two index gathers, no bytes copied)
+                    p.emit_keys.append((-2 if _side(e) else -1, "strrow", e))
+                    continue
                 slot = p.col_index[(_path(e), self._key_usage(e))]
                 if isinstance(obj, StringColumn):
                     p.emit_keys.append((slot, "str", p.cols[slot]["L"]))
@@ -705,6 +711,13 @@ class _Compiler:
             p.release(r)
             r = d
         return r
+
+    def _row_key(self, e: E) -> bool:
+        """Emit mode: a string key part too long for a short code is emitted as its row index instead."""
+        if self.mode != "emit":
+            return False
+        obj = self._res(e)
+        return isinstance(obj, StringColumn) and obj.max_len() > 7
 
     def _key_usage(self, e: E):
         obj = self._res(e)
@@ -959,7 +972,7 @@ def _compile_cached(plan: StagePlan, batch: RecordBatch, mode: str = "agg") -> P
 
 
 _EMIT_SIGS: Dict[tuple, bool] = {}           # stage signatures whose groups overflowed the kernel's tables
-_KEY_SHAPE = __import__("re").compile(r"float key|mixed key|key too wide")
+_KEY_SHAPE = __import__("re").compile(r"float key|mixed key|key too wide|long string key")
 EMIT = os.environ.get("NSDB_PIPE_EMIT", "1") != "0"
 
 
@@ -1043,6 +1056,9 @@ def _run_emit(plan: StagePlan, batch: RecordBatch, on_gpu: bool) -> Optional[Rec
     parts = []
     for i, (_reg, kind, info) in enumerate(prog.emit_keys):
         w = words[i]
+        if kind == "strrow":                          # the key strings at the emitted rows (probe or build side)
+            parts.append(_resolve(info, batch, plan.build_batch()).take(w))
+            continue
         if kind == "int":
             parts.append(w.to(info) if info != torch.int64 else w)
         elif kind == "float":
@@ -1260,7 +1276,7 @@ def jit_source(prog: Program, kinds, lates, kind: str, key_reg: int = -1, val_re
     F = max(1, len(val_regs))
     staged = kind in ("agg", "emit", "pairs")        # segment A / late columns / segment B split
     nins_a = prog.nins_a if staged else len(prog.ins)
-    emit_regs = [k[0] for k in getattr(prog, "emit_keys", [])] + list(val_regs)
+    emit_regs = [k[0] for k in getattr(prog, "emit_keys", [])] + list(val_regs)   # -1 / -2: the probe / build row
 
     def seg(lo, hi):
         body = [t for pc in range(lo, hi) if (t := _jit_ins(pc, prog.ins[pc])) is not None]
@@ -1291,7 +1307,8 @@ def jit_source(prog: Program, kinds, lates, kind: str, key_reg: int = -1, val_re
     else:
         entry = ("extern \"C\" __global__ void __launch_bounds__(nsdb_pipe::NTHR) nsdb_jit_mask(const nsdb_pipe::PipeArgs a, "
                  "unsigned char* mask) {\n  nsdb_pipe::jit_mask_body<nsdb_pipe::JitProg>(a, mask);\n}\n")
-    emit = "".join(f"    w[{i}] = r[{reg}];\n" for i, reg in enumerate(emit_regs)) or "    w[0] = 0ull; (void)r;\n"
+    emit = "".join(f"    w[{i}] = {'(u64)row' if reg == -1 else '(u64)brow' if reg == -2 else f'r[{reg}]'};\n"
+                   for i, reg in enumerate(emit_regs)) or "    w[0] = 0ull; (void)r;\n"
     ne = max(1, len(emit_regs))
     if kind == "pairs":                              # a fused filter + probe: (probe row, build row) per match
         emit, ne = "    (void)r;\n    w[0] = (u64)row;\n    w[1] = (u64)brow;\n", 2
@@ -1570,9 +1587,11 @@ def interpret_emit(prog: Program, n: int, plan: StagePlan):
     of every kept (matched) row, key-part registers first, then the value registers."""
     from . import kernels as KK
 
+    prow = brow = None
     if plan.join is None:
         regs = _run_program(prog, n)
         keep = torch.ones(n, dtype=torch.bool) if prog.keep_reg < 0 else regs[prog.keep_reg] != 0
+        prow = torch.arange(n)
     else:
         regs = _run_program(prog, n, hi=prog.nins_a, sides=(0,))
         keep = torch.ones(n, dtype=torch.bool) if prog.keep_reg < 0 else regs[prog.keep_reg] != 0
@@ -1584,9 +1603,11 @@ def interpret_emit(prog: Program, n: int, plan: StagePlan):
         regs = _run_program(prog, n, lo=prog.nins_a, rowmap={i: (bi if c["late"] == 2 else prow)
                                                              for i, c in enumerate(prog.cols)})
         keep = torch.ones(n, dtype=torch.bool) if prog.keep2_reg < 0 else regs[prog.keep2_reg] != 0
+        brow = bi
     idx = keep.nonzero().flatten()
     rs = [k[0] for k in prog.emit_keys] + list(prog.val_regs)
-    words = torch.stack([regs[r][idx] for r in rs]) if rs else torch.zeros(1, idx.numel(), dtype=torch.int64)
+    pick = lambda r: prow.to(torch.int64) if r == -1 else brow.to(torch.int64) if r == -2 else regs[r]  # noqa: E731
+    words = torch.stack([pick(r)[idx] for r in rs]) if rs else torch.zeros(1, idx.numel(), dtype=torch.int64)
     return words, int(idx.numel())
 
 

@@ -588,8 +588,11 @@ def q04(client, db: str, date: int = 19930701, join_first: bool = Q04_JOIN_FIRST
         j = _EqJoin(2, [(0, "o_orderkey", 1, "l_orderkey")], _pick([["o_orderkey", "o_orderpriority"], []]))
         j.set_input(0, os_)
         j.set_input(1, late)
+        # distinct (order, priority) of the matches as a lambda tree: the late-lineitem scan, its probe of the quarter's
+        # orders and the emitted (key, priority) rows are ONE compiled kernel (execution/pipeline.py emit form)
+        dist = _TreeGroupBy(lambda x: KeyTuple(x.o_orderkey, x.o_orderpriority), lambda x: Values(1.0),
+                            _rows_out(["n"]))
         ones = lambda b: torch.ones(b.n, 1, dtype=torch.float64, device=_dev(b))  # noqa: E731
-        dist = _GroupBy(lambda b: (_col(b, "o_orderkey"), _col(b, "o_orderpriority")), ones, _rows_out(["n"]))
         cnt = _GroupBy(lambda b: _col(b, "k1"), ones, _rows_out(["order_count"]))
         r = _flat(_run(client, db, "q04_out", cnt.set_input(dist.set_input(j)), "tpch_q04"))
         if r is None:

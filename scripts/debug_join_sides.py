@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--sf", type=float, default=0.05)
     ap.add_argument("--min-bytes", type=int, default=1)
     ap.add_argument("--queries", default="q14,q12,q03,q17,q04,q02")
+    ap.add_argument("--clear", action="store_true", help="clear the in-process caches before each query (cold runs)")
     a = ap.parse_args()
     P.AdaptivePlanner.MEASURE_BUILD_MIN = a.min_bytes
     orig = PL._launch
@@ -46,6 +47,10 @@ def main():
     c = PDBClient(root=tempfile.mkdtemp(), device="cuda:0")
     tpch.load(c, "tpch", t, device="cuda:0")
     for q in a.queries.split(","):
+        if a.clear:
+            c.engine._plan_cache.clear()
+            for d in (PL._STAGE_CACHE, PL._PROG_CACHE, PL._JIT_FN, PL._JIT_SHAPES, PL._LIT_DEV):
+                d.clear()
         try:
             got = tpch.QUERIES[q](c, "tpch")
         except RuntimeError as e:           # reported above with the columns; the next query still runs

@@ -272,6 +272,9 @@ EMIT_CASES = {
     # a composite key of an integer, a float and a short string (not packable into one word), min
     "composite_key": (lambda x: x.l_shipmode == "AIR", lambda x: KeyTuple(x.l_partkey, x.l_discount, x.l_returnflag),
                       lambda x: Values(x.l_quantity * x.l_tax), "min"),
+    # a string key part longer than a short code (17-byte ship instructions): emitted as its row, taken afterwards
+    "long_string_key": (lambda x: x.l_quantity > 30, lambda x: KeyTuple(x.l_partkey, x.l_shipinstruct),
+                        lambda x: Values(x.l_quantity), "sum"),
 }
 
 
