@@ -532,7 +532,7 @@ class _Compiler:
         key = (_path(e), u)
         if key in self.p.col_index:
             i = self.p.col_index[key]
-            if not late:
+            if not late and self.p.cols[i]["late"] != 2:   # an early use of a probe column; build columns stay 2
                 self.p.cols[i]["late"] = 0
             return i
         if len(self.p.cols) >= MAXCOL:

@@ -562,10 +562,15 @@ def _join_case(c, case):
     return _join_agg(c, probe("tpch"), build("tpch"), keys, pick, key_fn, val_fn, f"j_{case}", op)
 
 
+@pytest.mark.parametrize("late", [True, False], ids=["late_cols", "early_cols"])
 @pytest.mark.parametrize("case", sorted(JOIN_CASES))
-def test_fused_join_probe_cpu_interpreter(case, monkeypatch):
-    """A stage probing a build table inside the fused program (torch model of jit_join_agg_body): == the eager atoms."""
+def test_fused_join_probe_cpu_interpreter(case, late, monkeypatch):
+    """A stage probing a build table inside the fused program (torch model of jit_join_agg_body): == the eager atoms.
+    ``early_cols``: the selectivity estimate says "load every probe column in the first pass" (what a GPU run's
+    measured estimate does on repeats) — build-side columns must still be read at the matched build rows."""
     monkeypatch.setenv("NSDB_DEVICE_STRINGS", "1")
+    if not late:
+        monkeypatch.setattr(PL, "LATE_MAX_SEL", -1.0)
     t = tpch_gen.generate_fast(0.003, seed=6)
     c = _client("cpu", t)
     eager = _join_case(c, case)
