@@ -226,11 +226,13 @@ __device__ __forceinline__ double wave_reduce(double v, int op) {
 
 // Overflow of a fused aggregation (more groups than the tables hold): the launch's result is discarded and the host
 // re-runs the batch in the emitted form, so the scan stops as soon as any workgroup has overflowed — its own flag
-// every iteration (LDS), the launch's status word every 16 (a full LDS table otherwise costs every later row a probe
+// every iteration (LDS), the launch's status word every 64 (a full LDS table otherwise costs every later row a probe
 // of all CAP slots: a 60 M-row scan that overflowed early measured 67-77 ms instead of ~0.5).
 __device__ __forceinline__ bool agg_overflowed(const PipeArgs& a, int* s_ovf, int it) {
   if (__hip_atomic_load(s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return true;
-  return (it & 15) == 15 && (__hip_atomic_load(a.table, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1ull);
+  // the launch word (a device-scope load of one address by every thread) only every 64 iterations: a long scan
+  // with few groups never pays it more than a handful of times
+  return (it & 63) == 63 && (__hip_atomic_load(a.table, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1ull);
 }
 __device__ __forceinline__ void agg_mark_overflow(const PipeArgs& a, int* s_ovf) {
   __hip_atomic_store(s_ovf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);

@@ -32,6 +32,11 @@ from ..objects.strings import StringColumn, to_host, use_device_strings
 # ----------------------------------------------------------------------------------------- schema
 
 
+class Date32(int):
+    """A yyyymmdd date field (an ``int`` value) stored as an int32 column: half the bytes of an int64 column for every
+    date predicate a scan evaluates (Q01 / Q03 / Q04 / Q06 / Q12 / Q14 read 1-3 of them per lineitem row)."""
+
+
 class Region(PDBObject):
     r_regionkey: int
     r_name: str
@@ -91,7 +96,7 @@ class Order(PDBObject):
     o_custkey: int
     o_orderstatus: str
     o_totalprice: float
-    o_orderdate: int
+    o_orderdate: Date32
     o_orderpriority: str
     o_clerk: str
     o_shippriority: int
@@ -109,9 +114,9 @@ class LineItem(PDBObject):
     l_tax: float
     l_returnflag: str
     l_linestatus: str
-    l_shipdate: int
-    l_commitdate: int
-    l_receiptdate: int
+    l_shipdate: Date32
+    l_commitdate: Date32
+    l_receiptdate: Date32
     l_shipinstruct: str
     l_shipmode: str
     l_comment: str
@@ -264,7 +269,7 @@ def to_batch(table: str, cols: Dict[str, object], device=None) -> RecordBatch:
                 out[name] = StringColumn.from_list(v, device) if use_device_strings(device or "cpu") else list(v)
         else:
             arr = np.asarray(v)
-            out[name] = torch.from_numpy(arr.astype(np.float64 if ft is float else np.int64))
+            out[name] = torch.from_numpy(arr.astype(np.float64 if ft is float else np.int32 if ft is Date32 else np.int64))
             if device is not None:
                 out[name] = out[name].to(device)
         n = len(v)

@@ -151,6 +151,8 @@ def parse_tbl(buf: torch.Tensor, table: str, device=None) -> RecordBatch:
             cols[f] = col if use_device_strings(device or buf.device) else col.tolist()
         else:
             cols[f] = _parse_numeric(buf, s, e, ft is float)
+            if ft is T.Date32:
+                cols[f] = cols[f].to(torch.int32)
     return RecordBatch(cols, n, typ)
 
 

@@ -170,7 +170,7 @@ class PDBObject:
 
 
 def _default_for(ft):
-    if ft is int:
+    if ft is int or (isinstance(ft, type) and issubclass(ft, int) and ft is not bool):
         return 0
     if ft is float:
         return 0.0

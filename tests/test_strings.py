@@ -120,17 +120,17 @@ def test_tpch_string_queries_packed_cpu(device_strings, tmp_path):
     from netsdb_amd.models import tpch
 
     seen = []
-    orig = tpch._like
+    orig = StringColumn.like
 
-    def spy(strings, *a, **k):
-        seen.append(type(strings))
-        return orig(strings, *a, **k)
+    def spy(self, *a, **k):                      # Q13's NOT LIKE (a lambda tree) evaluated on the packed column
+        seen.append(type(self))
+        return orig(self, *a, **k)
 
-    tpch._like = spy
+    StringColumn.like = spy
     try:
         _tpch_strings("cpu", tmp_path)
     finally:
-        tpch._like = orig
+        StringColumn.like = orig
     assert seen and all(t is StringColumn for t in seen)
 
 
