@@ -494,10 +494,10 @@ class _Compiler:
         if e.kind == "bin" and e.val in ("==", "!=") and any(a.kind == "const" and isinstance(a.val, str) for a in e.args):
             for a in e.args:
                 if a.kind != "const":
-                    self._collect(a, "sref", seg, out)
+                    self._collect(a, "scmp", seg, out)
             return
         if e.kind in ("like", "isin"):
-            self._collect(e.args[0], "sref" if e.kind == "like" else "isin", seg, out)
+            self._collect(e.args[0], "sref" if e.kind == "like" else "scmp", seg, out)
             return
         for a in e.args:
             self._collect(a, usage, seg, out)
@@ -513,6 +513,10 @@ class _Compiler:
                 raise Unfusable("join key: a probe-side integer column")
             usage = "num"
         if isinstance(obj, StringColumn):
+            if usage == "scmp":
+                # == / IN against literals: a column of short strings is compared on its fixed-width code (one integer
+                # compare per literal, no offsets or bytes read); longer strings byte by byte
+                usage = "key" if obj.max_len() <= 7 else "sref"
             if usage == "isin":
                 usage = "sref"
             if usage == "key":
@@ -781,6 +785,22 @@ class _Compiler:
             if neg:
                 p.emit(OP_NOT, d, d)
             return d, "b"
+        if e.kind == "isin" and self._scode(e.args[0]) is not None:
+            r, L = self._scode(e.args[0])
+            acc = None
+            for v in e.val:
+                if not isinstance(v, str):
+                    raise Unfusable("IN types")
+                d = self._code_eq(r, L, v)
+                if acc is None:
+                    acc = d
+                else:
+                    p.emit(OP_OR, acc, acc, d)
+                    p.release(d)
+            if acc is None:
+                acc = p.temp()
+                p.emit(OP_CONST, acc, imm=0)
+            return acc, "b"
         if e.kind == "isin":
             r, t = self.gen(e.args[0])
             acc = None
@@ -827,6 +847,34 @@ class _Compiler:
             return d, ta
         raise Unfusable(e.kind)
 
+    def _scode(self, e: E):
+        """(slot, L) when string column ``e`` was registered by its short code (== / IN compares), else None."""
+        if e.kind not in ("src", "field"):
+            return None
+        obj = self._res(e)
+        if not isinstance(obj, StringColumn):
+            return None
+        L = obj.max_len()
+        i = self.p.col_index.get((_path(e), ("scode", L)))
+        return None if i is None else (i, L)
+
+    def _code_eq(self, r: int, L: int, lit: str) -> int:
+        """A temporary holding (code register r == the literal's short code); a literal longer than L never matches."""
+        p = self.p
+        b = lit.encode()
+        d = p.temp()
+        if len(b) > L:
+            p.emit(OP_CONST, d, imm=0)
+            return d
+        c = 0
+        for i in range(L):
+            c |= (b[i] if i < len(b) else 0) << (8 * (L - 1 - i))
+        z = p.temp()
+        p.emit(OP_CONST, z, imm=(c << 3) | len(b))
+        p.emit(OP_EQI, d, r, z)
+        p.release(z)
+        return d
+
     def _promote(self, r, t):
         if t == "f":
             return r
@@ -842,6 +890,12 @@ class _Compiler:
         a, b = e.args
         if op in ("==", "!=") and (a.kind == "const" and isinstance(a.val, str) or b.kind == "const" and isinstance(b.val, str)):
             s, lit = (b, a.val) if a.kind == "const" else (a, b.val)
+            sc = self._scode(s)
+            if sc is not None:                            # fixed-width code compare
+                d = self._code_eq(sc[0], sc[1], lit)
+                if op == "!=":
+                    p.emit(OP_NOT, d, d)
+                return d, "b"
             r, t = self.gen(s)
             if t != "s":
                 raise Unfusable("string compare")

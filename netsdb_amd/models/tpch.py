@@ -709,16 +709,17 @@ def q17(client, db: str, brand: str = "Brand#23", container: str = "MED BOX") ->
     """Small-quantity-order revenue (Query17.h): per-part average quantity of the brand/container parts, then the
     lineitems of those parts under 0.2 x that average; sum(extendedprice) / 7.
 
-    One job of two lineitem passes, each a join probe + aggregation compiled into one kernel (execution/pipeline.py):
-    (1) lineitem ⋈ the qualifying parts -> (sum quantity, count) per part; (2) lineitem ⋈ those per-part rows,
-    l_quantity < 0.2 * sq / n -> sum(l_extendedprice). Every lambda is a tree (members, arithmetic, comparisons)."""
+    ONE job and ONE lineitem pass: the scan's probe of the qualifying parts is one compiled launch emitting the
+    matched (lineitem, part) rows (execution/pipeline.py "pairs" form: ~0.1 % of the rows), an intermediate tuple set
+    read by both the per-part (sum quantity, count) aggregation and the join back to it; l_quantity < 0.2 * sq / n ->
+    sum(l_extendedprice) on those few rows. Every lambda is a tree (members, arithmetic, comparisons)."""
     ps = _TreeFilter(lambda x: (x.p_brand == brand) & (x.p_container == container)).set_input(ScanSet(db, "part", Part))
-    j = _EqJoin(2, [(0, "l_partkey", 1, "p_partkey")], _pick([["l_partkey", "l_quantity"], []]))
+    j = _EqJoin(2, [(0, "l_partkey", 1, "p_partkey")], _pick([["l_partkey", "l_quantity", "l_extendedprice"], []]))
     j.set_input(0, ScanSet(db, "lineitem", LineItem))
     j.set_input(1, ps)
     avg = _TreeGroupBy(lambda x: x.l_partkey, lambda x: Values(x.l_quantity, 1.0), _rows_out(["sq", "n"]))
     j2 = _EqJoin(2, [(0, "l_partkey", 1, "k0")], _pick([["l_quantity", "l_extendedprice"], ["sq", "n"]]))
-    j2.set_input(0, ScanSet(db, "lineitem", LineItem))
+    j2.set_input(0, j)
     j2.set_input(1, avg.set_input(j))
     small = _TreeFilter(lambda x: x.l_quantity < 0.2 * x.sq / x.n).set_input(j2)
     tot = _TreeGroupBy(lambda x: Literal(0), lambda x: Values(x.l_extendedprice), _rows_out(["s"]))

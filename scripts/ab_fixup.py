@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--n", type=int, default=1000)
     ap.add_argument("--k", type=int, default=597544)
     ap.add_argument("--settle-s", type=float, default=2.0)
+    ap.add_argument("--plain", action="store_true", help="f32 output, no bias / activation / dropout")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
@@ -34,6 +35,8 @@ def main():
     B = (torch.rand(a.n, a.k, device=dev, generator=g) - 0.5).to(torch.bfloat16)
     bias = torch.rand(a.n, device=dev, generator=g) - 0.5
     kw = dict(bias=bias, bias_mode=ops.BIAS_COL, act="relu", dropout=0.5, seed=7, cfg=2)
+    if a.plain:
+        kw = dict(out_dtype=torch.float32, cfg=2)
     ref = ops.gemm_nt(A, B, fixup=0, **kw)
     got = ops.gemm_nt(A, B, fixup=1, **kw)
     got2 = ops.gemm_nt(A, B, fixup=1, **kw)       # counters re-zeroed by the previous launch
