@@ -1504,8 +1504,11 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
     // the 32x32x16 main loop stores from registers only (store_direct_8ph32): launches that need the LDS-staged
     // epilogue (C += A.B^T, a per-element bias, unaligned C) stay on the 16x16x32 loop
     const int mf = opts ? opts->mfma : 0;
+    // only where the separate reducer would be the plain one (same summation order: bit-identical results); narrow
+    // outputs with many splits keep splitk_reduce_wide_kernel
+    const long long fx_blocks = ((long long)M * N / 4 + 255) / 256;
     if (opts && opts->fixup && opts->fx_state && p.splits > 1 && p.splits <= 32 && p.direct_epi && p.vec_ws &&
-        batch == 1 && !(mf == 32)) {
+        batch == 1 && !(mf == 32) && !(p.splits >= 8 && fx_blocks < 512)) {
       p.fixup = 1;
       p.fx_cnt = opts->fx_state;
       p.fx_dep = opts->fx_state + p.tiles_m * p.tiles_n;
