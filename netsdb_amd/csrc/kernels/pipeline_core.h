@@ -142,11 +142,122 @@ __device__ __forceinline__ long long lk_find(const unsigned* w, long long pos, l
   }
   return -1;
 }
+// The register-window form of str_like: the string's bytes come in as LKW16 16-byte loads from a 16-B aligned start
+// (all issued before any use: one memory latency per string instead of one per dword of a data-dependent scan loop),
+// then every segment is searched in registers — per dword, the SWAR test of the segment's first two bytes over its 4
+// candidate starts, and a candidate verified by comparing the (up to 16) bytes at that start, funnel-shifted out of
+// the window, against the segment under its '_' mask. All window indices are compile-time constants (no scratch).
+constexpr int LKW16 = 7;                  // 112-byte window
+constexpr int LKWD = LKW16 * 4;           // its dwords
+__device__ __forceinline__ u64 lk_bytes8(const unsigned (&w)[LKWD], int i, int o) {   // bytes 4i + o .. 4i + o + 7
+  const u64 lo = (u64)w[i] | ((u64)w[i + 1] << 32);
+  const u64 hi = (u64)w[i + 2];
+  return o ? (lo >> (8 * o)) | (hi << (64 - 8 * o)) : lo;
+}
+// pattern bytes [k, k + 8) of a segment (0xFF = any byte) as value / mask words
+__device__ __forceinline__ void lk_pat8(const unsigned char* sb, int ln, int k, u64& v, u64& m) {
+  v = 0;
+  m = 0;
+  for (int j = 0; j < 8 && k + j < ln; ++j) {
+    const u64 c = sb[k + j];
+    if (c != 0xFFu) {
+      v |= c << (8 * j);
+      m |= 0xFFull << (8 * j);
+    }
+  }
+}
+__device__ __forceinline__ bool lk_match_at(const unsigned (&w)[LKWD], int i, int o, int ln, u64 v0, u64 m0, u64 v1,
+                                            u64 m1) {
+  if (((lk_bytes8(w, i, o) ^ v0) & m0) != 0) return false;
+  return ln <= 8 || ((lk_bytes8(w, i + 2, o) ^ v1) & m1) == 0;
+}
+// leftmost start in [pos, last] of a segment (ln <= 16) inside the window, or -1
+__device__ __forceinline__ int lk_find_w(const unsigned (&w)[LKWD], int pos, int last, const unsigned char* sb, int ln) {
+  if (last < pos) return -1;
+  u64 v0, m0, v1 = 0, m1 = 0;
+  lk_pat8(sb, ln, 0, v0, m0);
+  if (ln > 8) lk_pat8(sb, ln, 8, v1, m1);
+  const unsigned b0 = sb[0], b1 = ln >= 2 ? sb[1] : 0xFFu;
+  const bool swar = ln >= 2 && b0 != 0xFFu && b1 != 0xFFu;
+  const unsigned B0 = b0 * 0x01010101u, B1 = b1 * 0x01010101u;
+  int found = -1;
+#pragma unroll
+  for (int i = 0; i < LKWD - 4; ++i) {
+    if (found < 0 && 4 * i + 3 >= pos && 4 * i <= last) {
+      unsigned cand = 0xFu;
+      if (swar) {
+        const unsigned x1 = (w[i] >> 8) | (w[i + 1] << 24);
+        const unsigned z = lk_zero_bytes(w[i] ^ B0) & lk_zero_bytes(x1 ^ B1);   // 0x80 per candidate byte
+        cand = ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+      }
+      while (cand) {
+        const int o = __builtin_ctz(cand);
+        cand &= cand - 1;
+        const int p = 4 * i + o;
+        if (p < pos || p > last) continue;
+        if (lk_match_at(w, i, o, ln, v0, m0, v1, m1)) {
+          found = p;
+          break;
+        }
+      }
+    }
+  }
+  return found;
+}
+
 __device__ __forceinline__ bool str_like(const unsigned char* d, u64 ref, const unsigned char* lit, long long imm) {
   const long long s = (long long)(ref >> 24), e = s + (long long)(ref & 0xFFFFFF);
   const unsigned char* l = lit + (imm >> 16);
   const int flags = l[0], nseg = l[1];
   const unsigned* w = reinterpret_cast<const unsigned*>(d);
+  {
+    // the register window: the string inside 112 bytes from a 16-B aligned start with >= 16 zero bytes after it (the
+    // funnel shifts' look-ahead: a candidate start p <= e - ln never compares a byte past e), every segment at most
+    // 16 bytes. Only the 16-B chunks holding the string are loaded: the last ends before e + 16, inside the buffer
+    // (StringColumn pads it by 16 bytes).
+    const long long a0 = s & ~15ll;
+    bool short_segs = true;
+    for (int sg = 0; sg < nseg; ++sg) short_segs &= l[2 + sg] <= 16;
+    if (short_segs && e - a0 + 16 <= 4 * LKWD) {
+      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+      unsigned win[LKWD];
+      const u32x4* src = reinterpret_cast<const u32x4*>(d + a0);
+      const int nload = (int)((e - a0 + 15) >> 4);
+#pragma unroll
+      for (int q = 0; q < LKW16; ++q) {
+        const u32x4 v = q < nload ? src[q] : u32x4{0u, 0u, 0u, 0u};
+        win[4 * q] = v.x;
+        win[4 * q + 1] = v.y;
+        win[4 * q + 2] = v.z;
+        win[4 * q + 3] = v.w;
+      }
+      const int ws = (int)(s - a0), we = (int)(e - a0);
+      if (nseg == 0) return (flags & 3) == 3 ? we == ws : true;
+      const unsigned char* sb = l + 2 + nseg;
+      int pos = ws;
+      for (int sg = 0; sg < nseg; ++sg) {
+        const int ln = l[2 + sg];
+        const bool last = sg == nseg - 1;
+        int p;
+        if (sg == 0 && (flags & 1)) {                  // anchored start: only at pos
+          p = lk_find_w(win, pos, pos, sb, ln);
+          if (p < 0 || we - pos < ln) return false;
+          pos += ln;
+          if (last && (flags & 2) && pos != we) return false;
+        } else if (last && (flags & 2)) {              // anchored end: only at we - ln
+          p = we - ln >= pos ? lk_find_w(win, we - ln, we - ln, sb, ln) : -1;
+          if (p < 0) return false;
+          pos = we;
+        } else {
+          p = lk_find_w(win, pos, we - ln, sb, ln);
+          if (p < 0) return false;
+          pos = p + ln;
+        }
+        sb += ln;
+      }
+      return true;
+    }
+  }
   const unsigned char* sb = l + 2 + nseg;
   if (nseg == 0) return (flags & 3) == 3 ? e == s : true;
   long long pos = s;

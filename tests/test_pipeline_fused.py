@@ -655,3 +655,24 @@ def test_fused_probe_pairs_gpu(case):
     fused = _join_rows(c, case, "pf")
     assert c.engine.pipeline_stats.get("fused_probes", 0) > p0, c.engine.pipeline_stats
     assert eager and eager == fused
+
+
+LIKE_PATTERNS = ["%ly%re%", "%e_s%", "care%", "%ts", "%furiously%", "%quickly%ideas%", "%s_ecial%r%",
+                 "%blithely regular pack%", "%", "furiously%deposits", "%a%b%c%d%e%"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pat", LIKE_PATTERNS)
+def test_fused_like_patterns_gpu(pat):
+    """The compiled general LIKE (register-window search for strings and segments that fit, the memory scan for the
+    rest: the 22-byte segment) against the eager column LIKE, as the count of matching rows per return flag."""
+    t = tpch_gen.generate_fast(0.02, seed=12)
+    c = _client("cuda:0", t)
+    args = (lambda x: Like(x.l_comment, pat), lambda x: x.l_returnflag, lambda x: Values(1.0), "sum")
+    c.engine.fused_pipelines = False
+    eager = _agg_job(c, *args)
+    c.engine.fused_pipelines = True
+    f0 = c.engine.pipeline_stats["fused_batches"]
+    fused = _agg_job(c, *args)
+    assert c.engine.pipeline_stats["fused_batches"] > f0
+    assert eager[0] == fused[0] and torch.equal(eager[1], fused[1]), (pat, eager, fused)
