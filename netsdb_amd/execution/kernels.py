@@ -128,6 +128,22 @@ class JoinTable:
             # builds past the device table's 2^29-row bound (32-bit payloads): sorted keys + binary search, on the device
             self._sorted = torch.sort(build_h)
 
+    _max_mult = None
+
+    def max_multiplicity(self) -> int:
+        """The most build rows any one key has (the fused probe kernels size their output regions by it): one device
+        reduction over the table's counts and one host read, once per table."""
+        if self._max_mult is None:
+            if self._dev is not None:
+                cnt = self._dev[0][:, 1] & 0xFFFFFFFF            # extra rows beyond the first, per slot
+                self._max_mult = int(cnt.max().item()) + 1 if self.n else 0
+            elif self.n:
+                _, c = torch.unique(self.h, return_counts=True)
+                self._max_mult = int(c.max().item())
+            else:
+                self._max_mult = 0
+        return self._max_mult
+
     def probe(self, probe_h: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """All (build_idx, probe_idx) pairs with equal keys, probe-major."""
         dev = probe_h.device

@@ -1140,16 +1140,21 @@ def _launch_emit(prog: Program, n: int, dev, plan: StagePlan, kind: str = "emit"
     cargs = _col_args(prog, dev)
     jtab = jperm = None
     bn = -1
+    mult = 1
     if plan.join is not None:
         jtab, jperm, bn = _join_table(plan, dev)
+        # every probe row emits at most the build side's largest key multiplicity: regions sized by it never overflow
+        mult = plan.builds[plan.join["name"]].table(dev).max_multiplicity()
+        if mult > 64:
+            raise Unfusable(f"a build key with {mult} rows (emit regions hold at most 64 per probe row)")
     jit = _jit_for(prog, cargs, kind, -1, prog.val_regs if kind == "emit" else (), dev)
     if jit is None:
         raise Unfusable("the emitted form needs the compiled kernels")
     fn, jnreg, jrows = jit
     ne = 2 if kind == "pairs" else len(prog.emit_keys) + len(prog.val_regs)
     tile = 256 * jrows * EMIT_TILE_BLOCKS
-    # a tile's region: its rows times the plan's expected matches per row (joins: 2, raised after an overflow)
-    cap = tile * (getattr(plan, "cap_mult", 2) if plan.join is not None else 1)
+    # a tile's region: its rows times the most matches one probe row can have
+    cap = tile * max(1, mult)
     words, status = h.pipe_emit(ins, prog.nins_a, cargs, lit, n, prog.keep_reg, -1, prog.val_regs, prog.kpool, fn,
                                 jnreg, jrows, max(1, ne), tile, cap, jtab, jperm, bn)
     if int(status[0]) != 0:
