@@ -425,7 +425,7 @@ __device__ __forceinline__ void fixup_rows_8ph(const GemmParams& p, int m0, int 
   }
 }
 
-__device__ __noinline__ void splitk_fixup_8ph(const GemmParams& p, int* slot, int tile, int split, int m0, int n0,
+__device__ __forceinline__ void splitk_fixup_8ph(const GemmParams& p, int* slot, int tile, int split, int m0, int n0,
                                               int tid) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this workgroup's slab stores acknowledged
   __syncthreads();
@@ -469,6 +469,7 @@ __device__ __noinline__ void splitk_fixup_8ph(const GemmParams& p, int* slot, in
 // Split-K launches store their raw f32 slab the same way (the reducer applies the epilogue): no LDS image, so no
 // compiler-inserted vmcnt drain before each LDS read of the staged store loop (which also made that loop wait for
 // its own earlier stores and for anything else in flight, e.g. an operand prefetch).
+template <bool WT = false>   // WT: split-K slabs written through to the device-coherent level (in-launch fix-up)
 __device__ __forceinline__ void store_direct_8ph(const f32x4 (&acc)[8][4], const GemmParams& p, int batch, int split,
                                                  int m0, int n0, int lane, int wave) {
   const int wr = wave >> 2, wc = wave & 3;
@@ -483,7 +484,7 @@ __device__ __forceinline__ void store_direct_8ph(const f32x4 (&acc)[8][4], const
         const int col = n0 + wc * 64 + j * 16 + cq;
         if (row < p.M && col < p.N) {
           float* d = ws + (long long)row * p.N + col;
-          if (p.fixup) {   // in-launch reduction: written through to the device-coherent level (vec_ws: N % 4 == 0)
+          if constexpr (WT) {   // in-launch reduction: written through to the device-coherent level (vec_ws)
             unsigned long long* d2 = reinterpret_cast<unsigned long long*>(d);
             const f32x4 a = acc[i][j];
             __hip_atomic_store(d2, ((unsigned long long)__float_as_uint(a[1]) << 32) | __float_as_uint(a[0]),
@@ -788,12 +789,13 @@ __global__ void __launch_bounds__(64 * WGM * WGN, 2) gemm_nt_stream_kernel(GemmP
 template <int EPI>
 __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   // fused-softmax launches may carry diagnostic phase stamps (p.stamps: [tile][8] on the 100 MHz real-time clock)
-  const unsigned long long t_entry = EPI != 0 ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  constexpr bool SMX = EPI == 1 || EPI == 2;   // the fused-softmax instantiations (EPI 3: split-K, reduced in-launch)
+  const unsigned long long t_entry = SMX ? __builtin_amdgcn_s_memrealtime() : 0ull;
   constexpr int HALF = 128 * 128;            // bytes of one half-tile (128 rows x 64 bf16)
   constexpr int BUF = 4 * HALF;              // one K-tile
   // + the epilogue's bias (store_tile_lds) and the operand-prefetch sink (1 KiB per wave), or the fused softmax's
   // line statistics (SM_LDS)
-  __shared__ __attribute__((aligned(16))) char smem[EPI != 0 ? SM_LDS : 2 * BUF + 1024 + 8 * 1024];
+  __shared__ __attribute__((aligned(16))) char smem[SMX ? SM_LDS : 2 * BUF + 1024 + 8 * 1024];
 
   const int ntiles = p.tiles_m * p.tiles_n;
   const int wg = xcd_remap(blockIdx.x, ntiles * p.splits);
@@ -839,7 +841,7 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   // fused softmax: the tile's per-column (threads 0-255) / per-row (256-511) bias, loaded before the prologue's DMAs
   // and written to LDS after its wait (read by the epilogue, after the main loop's barriers)
   float bias_v = 0.f;
-  if constexpr (EPI != 0) {
+  if constexpr (SMX) {
     const int c = tid & 255;
     const int idx = tid < 256 ? n0 + c : m0 + c;
     const bool use = p.bias && (tid < 256 ? (p.bias_mode == 2 && idx < p.N) : (p.bias_mode == 1 && idx < p.M));
@@ -924,7 +926,7 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   stage(0, 2, 0); stage(0, 0, 0); stage(0, 3, 0); stage(0, 1, 0);
   stage(1, 2, 1); stage(1, 0, 1); stage(1, 3, 1);
   asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  if constexpr (EPI != 0) reinterpret_cast<float*>(smem + SM_BIAS)[tid] = bias_v;   // [256 col | 256 row]
+  if constexpr (SMX) reinterpret_cast<float*>(smem + SM_BIAS)[tid] = bias_v;   // [256 col | 256 row]
   NSDB_BARRIER();
   if (wr == 1) NSDB_BARRIER();            // stagger the two wave groups by one barrier
   for (int it = 0; it < niter; ++it) {
@@ -933,7 +935,7 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
   }
   if (wr == 0) NSDB_BARRIER();            // re-align the groups
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // trailing zero-fill DMAs land before LDS reuse
-  if constexpr (EPI == 0) {
+  if constexpr (!SMX) {
     // Operand prefetch (per launch, GemmParams::pf_ptr): the next kernel's operand (the FF output weight after
     // layer 1, whose 2.4 GB stream evicts it) is read into the Infinity Cache by this launch's workgroups as each
     // finishes its main loop, spread over the launch's tail. 1/nwg of the bytes per workgroup, LDS-DMA into a
@@ -953,7 +955,7 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
       }
     }
   }
-  if constexpr (EPI != 0) {
+  if constexpr (SMX) {
     // the fused softmax turns acc into the final values in place; the common store then runs with a plain
     // (alpha 1, no bias/act/dropout, f32) epilogue
     unsigned long long* stamp = p.stamps ? p.stamps + (long long)(tm * p.tiles_n + tn) * 8 : nullptr;
@@ -980,15 +982,18 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_256_8ph_kernel(GemmParams p) {
     }
     return;
   }
+  if constexpr (EPI == 3) {
+    // split-K reduced inside the launch (host: direct epilogue, batch 1): write-through slabs, then the tile's splits
+    // meet; a separate instantiation, so the production EPI 0 kernel's registers are untouched by this code
+    store_direct_8ph<true>(acc, p, batch, split, m0, n0, lane, wave);
+    splitk_fixup_8ph(p, reinterpret_cast<int*>(smem + 2 * BUF), tm * p.tiles_n + tn, split, m0, n0, tid);
+    return;
+  }
   if (p.direct_epi) {
     store_direct_8ph(acc, p, batch, split, m0, n0, lane, wave);
   } else {
     store_tile_lds<256, 256, 2, 4, true>(acc, smem, 2 * BUF, p, batch, split, m0, n0, tid, lane, wave,
                                          reinterpret_cast<float*>(smem + 2 * BUF));
-  }
-  if (p.fixup) {   // host: split-K, direct epilogue, batch 1 — LDS words past the tile buffers (free after the loop)
-    splitk_fixup_8ph(p, reinterpret_cast<int*>(smem + 2 * BUF), tm * p.tiles_n + tn, split, m0, n0, tid);
-    return;
   }
   if (p.pf_ptr != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // prefetch DMAs retired
 }
@@ -1513,7 +1518,9 @@ int nsdb_gemm_nt_bf16(const void* A, const void* B, void* C, float* ws, const fl
       p.fx_cnt = opts->fx_state;
       p.fx_dep = opts->fx_state + p.tiles_m * p.tiles_n;
     }
-    if (mf == 32 && p.direct_epi)
+    if (p.fixup)
+      hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<3>, grid, dim3(512), 0, stream, p);
+    else if (mf == 32 && p.direct_epi)
       hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph32_kernel, grid, dim3(512), 0, stream, p);
     else
       hipLaunchKernelGGL(nsdb::gemm_nt_256_8ph_kernel<0>, grid, dim3(512), 0, stream, p);
