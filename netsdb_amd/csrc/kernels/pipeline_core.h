@@ -533,6 +533,37 @@ __device__ __forceinline__ void join_find(const PipeArgs& a, long long k, unsign
   }
 }
 
+// join_find for the ROWS rows of a thread at once: every kept row's first slot is read before any is compared (the
+// rows' probe latencies overlap instead of adding up), then each row walks its own collision chain.
+template <int ROWS>
+__device__ __forceinline__ void join_find_rows(const PipeArgs& a, const long long (&k)[ROWS], const bool (&keep)[ROWS],
+                                               unsigned (&cnt)[ROWS], unsigned (&pay)[ROWS]) {
+  u64 h[ROWS], s[ROWS];
+  u64x2 e[ROWS];
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j) {
+    cnt[j] = 0;
+    pay[j] = 0;
+    h[j] = fin64((u64)k[j] + JGOLD);
+    s[j] = h[j] == JEMPTY ? a.jmask + 1 : (fin64(h[j]) & a.jmask);
+    if (keep[j]) e[j] = *reinterpret_cast<const u64x2*>(a.jtab + 2 * s[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j) {
+    if (!keep[j]) continue;
+    for (u64 it = 0; it <= a.jmask; ++it) {       // >= 2 slots per build row: an empty slot ends every chain
+      if (e[j][0] == h[j]) {
+        cnt[j] = (unsigned)e[j][1] + (h[j] != JEMPTY ? 1u : 0u);
+        pay[j] = (unsigned)(e[j][1] >> 32);
+        break;
+      }
+      if (e[j][0] == JEMPTY || h[j] == JEMPTY) break;
+      s[j] = (s[j] + 1) & a.jmask;
+      e[j] = *reinterpret_cast<const u64x2*>(a.jtab + 2 * s[j]);
+    }
+  }
+}
+
 // One kept (key, values) row into the thread's KSLOT register slots, else the workgroup's LDS table.
 template <int F>
 __device__ __forceinline__ void agg_row(const PipeArgs& a, long long key, const double (&v)[F], long long (&sk)[KSLOT],
@@ -679,11 +710,14 @@ __device__ __forceinline__ void jit_join_agg_body(const PipeArgs& a) {
       kept += keep[j] ? 1u : 0u;
     }
     // probe: every kept row's first slot read issued together
+    {
+      long long k[ROWS];
+#pragma unroll
+      for (int j = 0; j < ROWS; ++j) k[j] = (long long)R[j][P::JK];
+      join_find_rows<ROWS>(a, k, keep, cnt, pay);
+    }
 #pragma unroll
     for (int j = 0; j < ROWS; ++j) {
-      cnt[j] = 0;
-      pay[j] = 0;
-      if (keep[j]) join_find(a, (long long)R[j][P::JK], cnt[j], pay[j]);
       keep[j] = keep[j] && cnt[j] != 0;
       any |= keep[j];
     }
@@ -761,11 +795,17 @@ __device__ __forceinline__ void jit_emit_body(const PipeArgs& a, unsigned long l
       kept += keep[j] ? 1u : 0u;
       cnt[j] = keep[j] ? 1u : 0u;
       pay[j] = 0;
-      if constexpr (P::JOIN) {
-        cnt[j] = 0;
-        if (keep[j]) join_find(a, (long long)R[j][P::JK], cnt[j], pay[j]);
-        keep[j] = keep[j] && cnt[j] != 0;
-      }
+    }
+    if constexpr (P::JOIN) {                       // every kept row's first slot read together
+      long long k[ROWS];
+#pragma unroll
+      for (int j = 0; j < ROWS; ++j) k[j] = (long long)R[j][P::JK];
+      join_find_rows<ROWS>(a, k, keep, cnt, pay);
+#pragma unroll
+      for (int j = 0; j < ROWS; ++j) keep[j] = keep[j] && cnt[j] != 0;
+    }
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
       any |= keep[j];
     }
     const bool wave_any = __builtin_amdgcn_ballot_w64(any) != 0ull;
