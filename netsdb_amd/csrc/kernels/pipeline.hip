@@ -348,12 +348,11 @@ __global__ void __launch_bounds__(NTHR) pipe_agg_kernel(const PipeArgs a) {
       if (!done && used < KSLOT) {
 #pragma unroll
         for (int s = 0; s < KSLOT; ++s) {
-          if (!done && s == used) {
-            sk[s] = key;
+          const bool ins = !done && s == used;   // selects, not a store at [used]: that form went to scratch
+          sk[s] = ins ? key : sk[s];
 #pragma unroll
-            for (int f = 0; f < F; ++f) sv[s][f] = v[f];
-            done = true;
-          }
+          for (int f = 0; f < F; ++f) sv[s][f] = ins ? v[f] : sv[s][f];
+          done = done || ins;
         }
         ++used;
       }
@@ -698,12 +697,11 @@ __global__ void __launch_bounds__(NTHR) tile_agg_kernel(const PipeArgs a) {
       if (!done && used < KS) {
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
-          if (!done && s == used) {
-            sk[s] = key;
+          const bool ins = !done && s == used;   // selects, not a store at [used]: that form went to scratch
+          sk[s] = ins ? key : sk[s];
 #pragma unroll
-            for (int f = 0; f < F; ++f) sv[s][f] = v[f];
-            done = true;
-          }
+          for (int f = 0; f < F; ++f) sv[s][f] = ins ? v[f] : sv[s][f];
+          done = done || ins;
         }
         ++used;
       }

@@ -438,12 +438,11 @@ __device__ __forceinline__ void jit_agg_body(const PipeArgs& a) {
       if (!done && used < KSLOT) {
 #pragma unroll
         for (int s = 0; s < KSLOT; ++s) {
-          if (!done && s == used) {
-            sk[s] = key;
+          const bool ins = !done && s == used;   // selects, not a store at [used]: that form went to scratch
+          sk[s] = ins ? key : sk[s];
 #pragma unroll
-            for (int f = 0; f < F; ++f) sv[s][f] = v[f];
-            done = true;
-          }
+          for (int f = 0; f < F; ++f) sv[s][f] = ins ? v[f] : sv[s][f];
+          done = done || ins;
         }
         ++used;
       }
@@ -580,12 +579,11 @@ __device__ __forceinline__ void agg_row(const PipeArgs& a, long long key, const 
   if (!done && used < KSLOT) {
 #pragma unroll
     for (int s = 0; s < KSLOT; ++s) {
-      if (!done && s == used) {
-        sk[s] = key;
+      const bool ins = !done && s == used;   // selects, not a store at [used]: that form went to scratch
+      sk[s] = ins ? key : sk[s];
 #pragma unroll
-        for (int f = 0; f < F; ++f) sv[s][f] = v[f];
-        done = true;
-      }
+      for (int f = 0; f < F; ++f) sv[s][f] = ins ? v[f] : sv[s][f];
+      done = done || ins;
     }
     ++used;
   }

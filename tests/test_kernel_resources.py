@@ -41,3 +41,84 @@ def test_gemm_8phase_kernels_do_not_spill():
     for name, r in hot.items():
         assert r.get("ScratchSize", 0) == 0, (name, r)
         assert r.get("Occupancy", 0) >= 2, (name, r)   # two waves per SIMD: the ping-pong wave groups
+
+
+def _tpch_jit_sources(queries):
+    """The generated sources of every fused kernel these TPC-H queries launch (agg / join agg / emit / pairs / mask),
+    captured from a CPU run through the interpreter: the same programs the GPU compiles with hiprtc."""
+    import tempfile
+
+    import torch
+
+    from netsdb_amd.client import PDBClient
+    from netsdb_amd.execution import pipeline as PL
+    from netsdb_amd.models import tpch
+
+    srcs = {}
+
+    def grab(prog, kind, plan=None):
+        cargs = PL._col_args(prog, torch.device("cpu"))
+        kinds, lates = [c[0] for c in cargs], [c[1] for c in cargs]
+        key_reg = prog.key_reg if kind == "agg" else -1
+        nreg = PL.program_nreg(prog, len(kinds), key_reg, prog.val_regs)
+        rows = PL.JIT_ROWS_SMALL if nreg <= PL.JIT_SMALL_NREG else PL.JIT_ROWS
+        if kind == "mask":
+            src = PL.jit_source(prog, kinds, [0] * len(kinds), "mask", rows=rows)
+        else:
+            src = PL.jit_source(prog, kinds, lates, kind, key_reg, prog.val_regs if kind != "pairs" else (), rows=rows)
+        srcs.setdefault(src, f"{kind}{len(srcs)}")
+
+    saved = {n: getattr(PL, n) for n in ("interpret", "interpret_join", "interpret_emit", "interpret_pairs",
+                                         "interpret_mask", "CPU_INTERPRETER")}
+
+    def hook(name, kind):
+        orig = saved[name]
+
+        def f(prog, n, *rest):
+            grab(prog, kind)
+            return orig(prog, n, *rest)
+        return f
+
+    PL.interpret, PL.interpret_join = hook("interpret", "agg"), hook("interpret_join", "agg")
+    PL.interpret_emit, PL.interpret_pairs = hook("interpret_emit", "emit"), hook("interpret_pairs", "pairs")
+    PL.interpret_mask = hook("interpret_mask", "mask")
+    PL.CPU_INTERPRETER = True
+    old_env = os.environ.get("NSDB_DEVICE_STRINGS")
+    os.environ["NSDB_DEVICE_STRINGS"] = "1"
+    try:
+        t = tpch.generate(0.004, seed=5)
+        c = PDBClient(root=tempfile.mkdtemp(), device="cpu")
+        tpch.load(c, "tpch", t)
+        for q in queries:
+            tpch.QUERIES[q](c, "tpch")
+    finally:
+        for n, v in saved.items():
+            setattr(PL, n, v)
+        if old_env is None:
+            os.environ.pop("NSDB_DEVICE_STRINGS", None)
+        else:
+            os.environ["NSDB_DEVICE_STRINGS"] = old_env
+    return srcs
+
+
+def test_fused_pipeline_kernels_do_not_spill(tmp_path):
+    """The run-time compiled scan kernels of the TPC-H queries (hiprtc on the GPU; hipcc here, same header) must not
+    use scratch: the fused join aggregation's register slots once compiled to a dynamically indexed private array
+    (112 bytes per lane) and Q12's fused probe ran ~0.7 ms instead of ~0.4."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    srcs = _tpch_jit_sources(["q01", "q03", "q04", "q12", "q13", "q14", "q17"])
+    assert any(k.startswith("agg") for k in srcs.values()) and any(k.startswith("emit") for k in srcs.values())
+    hdr = open(os.path.join(KDIR, "pipeline_core.h")).read()
+    for src, name in srcs.items():
+        # the hiprtc build sees the runtime header implicitly: include it, and the kernel header inline
+        with open(tmp_path / f"{name}.hip", "w") as f:
+            f.write("#include <hip/hip_runtime.h>\n" + src.replace('#include "pipeline_core.h"', hdr))
+
+    def one(name):
+        return name, _resources(str(tmp_path / f"{name}.hip"))
+
+    with ThreadPoolExecutor(4) as ex:
+        for name, res in ex.map(one, srcs.values()):
+            for fn, r in res.items():
+                assert r.get("ScratchSize", 0) == 0, (name, fn, r)
