@@ -205,12 +205,14 @@ __device__ __forceinline__ int lk_find_w(const unsigned (&w)[LKWD], int pos, int
   return found;
 }
 
+// WIN false: the memory scan only (the run-time kernels choose per program: pipeline.py JIT_LIKE_WINDOW)
+template <bool WIN = true>
 __device__ __forceinline__ bool str_like(const unsigned char* d, u64 ref, const unsigned char* lit, long long imm) {
   const long long s = (long long)(ref >> 24), e = s + (long long)(ref & 0xFFFFFF);
   const unsigned char* l = lit + (imm >> 16);
   const int flags = l[0], nseg = l[1];
   const unsigned* w = reinterpret_cast<const unsigned*>(d);
-  {
+  if constexpr (WIN) {
     // the register window: the string inside 112 bytes from a 16-B aligned start with >= 16 zero bytes after it (the
     // funnel shifts' look-ahead: a candidate start p <= e - ln never compares a byte past e), every segment at most
     // 16 bytes. Only the 16-B chunks holding the string are loaded: the last ends before e + 16, inside the buffer

@@ -1320,6 +1320,96 @@ __global__ __launch_bounds__(256) void compact_write_kernel(const unsigned char*
   }
 }
 
+// ---------------------------------------------------------------- clustered-key aggregation (runs of equal keys)
+// A group-by whose key column arrives ordered (TPC-H lineitem is stored by l_orderkey, so the late lineitems' order
+// keys of Q04 and the (orderkey, date, priority) keys of Q03's probe come out of a scan in runs) needs no hash table:
+// every run of equal consecutive keys is one group. Three passes, no atomics on data: run heads counted per tile
+// (with a flag for any descending step: unordered keys go to the hash path), the heads' row ids written in order
+// (the compaction's tile scan), and one thread per group reduces its run. A descending step anywhere means equal keys
+// may not be adjacent, so the caller falls back to hash aggregation; a non-descending column has each key in one run.
+__device__ __forceinline__ bool run_head(const u64* __restrict__ k, i64 i) { return i == 0 || k[i] != k[i - 1]; }
+
+__global__ __launch_bounds__(256) void run_count_kernel(const u64* __restrict__ k, i64 n, unsigned* __restrict__ cnt,
+                                                        unsigned long long* __restrict__ desc) {
+  const i64 t0 = (i64)blockIdx.x * CT_ROWS;
+  unsigned c = 0;
+  bool down = false;
+  for (int r = threadIdx.x; r < CT_ROWS; r += 256) {
+    const i64 i = t0 + r;
+    if (i >= n) break;
+    const u64 x = k[i];
+    const u64 p = i > 0 ? k[i - 1] : x;
+    c += (i == 0 || x != p) ? 1u : 0u;
+    down |= (long long)x < (long long)p;              // int64 order (a key column may hold negative values)
+  }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  __shared__ unsigned ws[4];
+  __shared__ int sdown;
+  if (threadIdx.x == 0) sdown = 0;
+  __syncthreads();
+  if (down) sdown = 1;
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    cnt[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+    if (sdown) atomicOr(desc, 1ull);
+  }
+}
+
+__global__ __launch_bounds__(256) void run_write_kernel(const u64* __restrict__ k, i64 n, const i64* __restrict__ off,
+                                                        const unsigned long long* __restrict__ desc,
+                                                        i64* __restrict__ heads) {
+  if (*desc) return;                                   // unordered: the caller takes the hash path
+  __shared__ unsigned wc[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const i64 t0 = (i64)blockIdx.x * CT_ROWS;
+  i64 base = off[blockIdx.x];
+  const u64 lt = (1ull << lane) - 1;
+  for (int r = 0; r < CT_ROWS; r += 256) {
+    const i64 i = t0 + r + threadIdx.x;
+    const bool on = i < n && run_head(k, i);
+    const u64 bal = __builtin_amdgcn_ballot_w64(on);
+    if (lane == 0) wc[wave] = (unsigned)__builtin_popcountll(bal);
+    __syncthreads();
+    unsigned before = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      before += w < wave ? wc[w] : 0u;
+      tot += wc[w];
+    }
+    if (on) heads[base + before + __builtin_popcountll(bal & lt)] = i;
+    base += tot;
+    __syncthreads();
+  }
+}
+
+// group g = rows [heads[g], heads[g + 1]) (the last ends at n): its key, row count and F reduced values (vals read in
+// place: element (row, f) at vals[row * rs + f * cs]); op 0 sum, 1 min, 2 max — in row order, as a sequential fold
+template <typename VT>
+__global__ __launch_bounds__(256) void run_reduce_kernel(const u64* __restrict__ k, const VT* __restrict__ vals,
+                                                         i64 rs, i64 cs, int F, int op, i64 n,
+                                                         const i64* __restrict__ heads, const i64* __restrict__ ng,
+                                                         const unsigned long long* __restrict__ desc,
+                                                         i64* __restrict__ okey, VT* __restrict__ oagg,
+                                                         i64* __restrict__ ocnt) {
+  if (*desc) return;
+  const i64 G = *ng;
+  for (i64 g = (i64)blockIdx.x * blockDim.x + threadIdx.x; g < G; g += (i64)gridDim.x * blockDim.x) {
+    const i64 lo = heads[g], hi = g + 1 < G ? heads[g + 1] : n;
+    okey[g] = (i64)k[lo];
+    ocnt[g] = hi - lo;
+    for (int f = 0; f < F; ++f) {
+      const VT* p = vals + f * cs;
+      VT acc = p[lo * rs];
+      for (i64 r = lo + 1; r < hi; ++r) {
+        const VT x = p[r * rs];
+        acc = op == 0 ? acc + x : (op == 1 ? (x < acc ? x : acc) : (x > acc ? x : acc));
+      }
+      oagg[g * F + f] = acc;
+    }
+  }
+}
+
 // ---------------------------------------------------------------- host launchers
 // rows staged per scatter pass: a multiple of 1024, <= 4096, staging <= budget bytes
 inline int stage_rows(int F, int budget = 48 * 1024, int nthr = 512) {
@@ -1562,6 +1652,39 @@ int nsdb_compact_write(const unsigned char* mask, long long n, const long long* 
   const long long T = nsdb_compact_tiles(n);
   if (T <= 0) return 0;
   hipLaunchKernelGGL(compact_write_kernel, dim3((unsigned)T), dim3(256), 0, st, mask, n, off, out);
+  return (int)hipGetLastError();
+}
+
+// Clustered-key aggregation, phase 1: run heads per tile and the descending-step flag. off has T + 2 words:
+// off[T] = the number of runs (groups), off[T + 1] = nonzero when the keys are not ordered (the caller reads both).
+int nsdb_run_count(const void* keys, long long n, unsigned* cnt, long long* off, hipStream_t st) {
+  const long long T = nsdb_compact_tiles(n);
+  if (T <= 0 || T > (1LL << 30)) return (int)hipErrorInvalidValue;
+  hipMemsetAsync(off + T + 1, 0, sizeof(long long), st);
+  hipLaunchKernelGGL(run_count_kernel, dim3((unsigned)T), dim3(256), 0, st, reinterpret_cast<const u64*>(keys), n, cnt,
+                     reinterpret_cast<unsigned long long*>(off + T + 1));
+  hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, st, cnt, (int)T, off);
+  return (int)hipGetLastError();
+}
+
+// phase 2: heads[G] and the groups (keys, counts, F values reduced with op 0 sum / 1 min / 2 max); vt 0 f64, 1 i64
+int nsdb_run_reduce(const void* keys, const void* vals, long long rs, long long cs, int F, int vt, int op, long long n,
+                    const long long* off, long long G, long long* heads, long long* okey, void* oagg, long long* ocnt,
+                    hipStream_t st) {
+  const long long T = nsdb_compact_tiles(n);
+  if (T <= 0) return 0;
+  const u64* k = reinterpret_cast<const u64*>(keys);
+  const unsigned long long* desc = reinterpret_cast<const unsigned long long*>(off + T + 1);
+  hipLaunchKernelGGL(run_write_kernel, dim3((unsigned)T), dim3(256), 0, st, k, n, off, desc, heads);
+  const unsigned blocks = (unsigned)std::max<long long>(1, std::min<long long>(16384, (G + 255) / 256));
+  if (vt == 1)
+    hipLaunchKernelGGL(run_reduce_kernel<long long>, dim3(blocks), dim3(256), 0, st, k,
+                       reinterpret_cast<const long long*>(vals), rs, cs, F, op, n, heads, off + T, desc, okey,
+                       reinterpret_cast<long long*>(oagg), ocnt);
+  else
+    hipLaunchKernelGGL(run_reduce_kernel<double>, dim3(blocks), dim3(256), 0, st, k,
+                       reinterpret_cast<const double*>(vals), rs, cs, F, op, n, heads, off + T, desc, okey,
+                       reinterpret_cast<double*>(oagg), ocnt);
   return (int)hipGetLastError();
 }
 

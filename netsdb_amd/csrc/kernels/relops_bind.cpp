@@ -35,6 +35,10 @@ int nsdb_compact_count(const unsigned char* mask, long long n, unsigned* cnt, lo
 int nsdb_compact_write(const unsigned char* mask, long long n, const long long* off, long long* out, hipStream_t st);
 int nsdb_partition_perm(const long long* dest, long long n, int P, void* work, long long* perm, long long* counts,
                         hipStream_t st);
+int nsdb_run_count(const void* keys, long long n, unsigned* cnt, long long* off, hipStream_t st);
+int nsdb_run_reduce(const void* keys, const void* vals, long long rs, long long cs, int F, int vt, int op, long long n,
+                    const long long* off, long long G, long long* heads, long long* okey, void* oagg, long long* ocnt,
+                    hipStream_t st);
 }
 
 namespace {
@@ -198,7 +202,11 @@ std::vector<torch::Tensor> join_build(torch::Tensor keys) {
   keys = keys.contiguous();
   const int64_t n = keys.numel();
   TORCH_CHECK(n < (int64_t(1) << 29), "join_build: at most 2^29 build rows per table");
-  const int64_t cap = pow2_at_least(std::max<int64_t>(1024, 2 * n));
+  // load factor: <= 1/8 for builds up to 256 k rows (a <= 64 MiB table: a probe of an ABSENT key — most probe rows of
+  // a selective join, TPC-H Q17's 60 M lineitems against ~2 k parts — expects ~1.1 slot reads instead of ~2.5 at 1/2),
+  // <= 1/4 up to 4 M rows, <= 1/2 beyond
+  const int64_t f = n <= (int64_t(1) << 18) ? 8 : (n <= (int64_t(1) << 22) ? 4 : 2);
+  const int64_t cap = pow2_at_least(std::max<int64_t>(1024, f * n));
   auto i64 = keys.options().dtype(torch::kInt64);
   // every slot {kEmpty, 0} (two fills: a device tensor built from host values would be a pageable, blocking copy)
   auto tab = torch::zeros({cap + 1, 2}, i64);
@@ -327,6 +335,50 @@ torch::Tensor mix64(torch::Tensor x, c10::optional<torch::Tensor> y) {
   return out;
 }
 
+// Group-by of keys that arrive in runs (relops.hip run_*_kernel): (reps [g], aggs [g, F], counts [g], first [g]) with
+// the groups in row order, or an empty list when the keys are not ordered (some key below its predecessor: equal
+// keys may then be apart) and the caller must take hash_aggregate. vals as in hash_aggregate; one host read (the
+// group count and the order flag together).
+std::vector<torch::Tensor> run_aggregate(torch::Tensor keys, c10::optional<torch::Tensor> vals, const std::string& op) {
+  TORCH_CHECK(keys.is_cuda() && keys.scalar_type() == torch::kInt64 && keys.dim() == 1, "keys must be 1-D int64 GPU");
+  keys = keys.contiguous();
+  const int64_t n = keys.numel();
+  const int opc = op == "sum" ? 0 : op == "min" ? 1 : op == "max" ? 2 : -1;
+  TORCH_CHECK(opc >= 0, "op must be sum, min or max");
+  int F = 0, vt = 0;
+  int64_t vrs = 0, vcs = 0;
+  torch::Tensor v;
+  auto vdtype = torch::kFloat64;
+  if (vals.has_value() && vals->defined() && vals->numel() > 0) {
+    v = *vals;
+    TORCH_CHECK(v.is_cuda() && v.device() == keys.device(), "vals must be on the keys' device");
+    TORCH_CHECK(v.scalar_type() == torch::kFloat64 || v.scalar_type() == torch::kInt64, "vals must be float64 or int64");
+    if (v.dim() == 1) v = v.unsqueeze(1);
+    TORCH_CHECK(v.dim() == 2 && v.size(0) == n, "vals must be [n] or [n, F]");
+    vrs = v.stride(0);
+    vcs = v.stride(1);
+    F = (int)v.size(1);
+    vt = v.scalar_type() == torch::kInt64 ? 1 : 0;
+    vdtype = v.scalar_type();
+  }
+  auto i64 = keys.options().dtype(torch::kInt64);
+  if (n == 0) return {};
+  const int64_t T = nsdb_compact_tiles(n);
+  auto cnt = torch::empty({T}, keys.options().dtype(torch::kInt32));
+  auto off = torch::empty({T + 2}, i64);
+  rc_ok(nsdb_run_count(keys.data_ptr(), n, reinterpret_cast<unsigned*>(cnt.data_ptr<int32_t>()),
+                       LL(off.data_ptr<int64_t>()), stream()), "run_count");
+  const auto st = off.slice(0, T, T + 2).cpu();          // [groups, descending step seen]
+  const int64_t G = st[0].item<int64_t>();
+  if (st[1].item<int64_t>() != 0) return {};
+  auto heads = torch::empty({G}, i64), okey = torch::empty({G}, i64), ocnt = torch::empty({G}, i64);
+  auto oagg = torch::empty({G, F}, keys.options().dtype(vdtype));
+  rc_ok(nsdb_run_reduce(keys.data_ptr(), F ? v.data_ptr() : nullptr, vrs, vcs, F, vt, opc, n, LL(off.data_ptr<int64_t>()),
+                        G, LL(heads.data_ptr<int64_t>()), LL(okey.data_ptr<int64_t>()), F ? oagg.data_ptr() : nullptr,
+                        LL(ocnt.data_ptr<int64_t>()), stream()), "run_reduce");
+  return {okey, oagg, ocnt, heads};
+}
+
 }  // namespace
 
 std::vector<torch::Tensor> hash_aggregate_impl(torch::Tensor keys, c10::optional<torch::Tensor> vals,
@@ -347,6 +399,9 @@ void register_relops(pybind11::module& m) {
         "tables sharing their rows through L2); returns nothing", pybind11::arg("on"));
   m.def("compact", &compact, "row ids of the set rows of a 0/1 byte mask, in order (stable stream compaction)",
         pybind11::arg("mask"));
+  m.def("run_aggregate", &run_aggregate, "group-by of keys arriving in runs: (reps, aggs, counts, first) or [] when "
+        "the keys are not ordered", pybind11::arg("keys"), pybind11::arg("vals") = pybind11::none(),
+        pybind11::arg("op") = "sum");
   m.def("mix64", &mix64, "key hash mix64((x ^ y) + GOLD) per row, one pass", pybind11::arg("x"),
         pybind11::arg("y") = pybind11::none());
 }

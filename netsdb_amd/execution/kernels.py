@@ -12,6 +12,7 @@ operators are sort / unique / searchsorted tensor ops.
 """
 from __future__ import annotations
 
+import os
 import weakref
 from typing import Any, List, Optional, Tuple
 
@@ -345,6 +346,27 @@ def _hash_aggregate(key64: torch.Tensor, vals, op: str, want_inv: bool, want_fir
     return r[0], r[1], r[2], r[3], r[4]
 
 
+RUN_AGG_MIN_ROWS = 1 << 18     # group_reduce tries the clustered-key path from this many rows
+RUN_AGG = os.environ.get("NSDB_RUN_AGG", "1") != "0"
+LAST_RUN_AGG = {"tried": 0, "used": 0}
+
+
+def _run_aggregate(key64: torch.Tensor, vals, op: str):
+    """Group-by of packed keys that arrive in runs of equal keys (relops.hip run_*_kernel: a scan of a table stored in
+    key order, e.g. TPC-H lineitem by l_orderkey): every run is one group, no hash table. None when the keys are not
+    ordered (checked on the device in the same pass that counts the runs), or too few rows to be worth the check."""
+    n = key64.numel()
+    h = _ext.hip()
+    if not RUN_AGG or n < RUN_AGG_MIN_ROWS or not hasattr(h, "run_aggregate"):
+        return None
+    LAST_RUN_AGG["tried"] += 1
+    r = h.run_aggregate(key64, vals, op)
+    if not r:
+        return None
+    LAST_RUN_AGG["used"] += 1
+    return r[0], r[1], r[2], r[3], None
+
+
 def _hash_aggregate_chunked(key64, vals, op, want_inv, want_first):
     """> AGG_CHUNK_ROWS rows: aggregate each chunk, then merge the chunks' groups (sum of sums / counts, min of mins,
     max of maxes); first rows and the per-row inverse are mapped through the merge."""
@@ -438,7 +460,9 @@ def group_reduce(keys, values, op: str = "sum"):
     key = packed[0] if packed is not None else _combine_words(words)
     # packed keys are the values themselves: no representative row (first / inverse) is needed, so the
     # partition passes carry no row ids
-    r = _hash_aggregate(key, vals, kop, packed is None, packed is None)
+    r = _run_aggregate(key, vals, kop) if packed is not None else None
+    if r is None:
+        r = _hash_aggregate(key, vals, kop, packed is None, packed is None)
     if r is None:
         return None
     reps_k, aggs, cnt, first, inv = r

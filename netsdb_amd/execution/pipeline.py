@@ -1214,6 +1214,11 @@ JIT = os.environ.get("NSDB_PIPE_JIT", "1") != "0"
 JIT_ROWS = 2
 JIT_ROWS_SMALL = 4
 JIT_SMALL_NREG = 8
+# general LIKE in the compiled kernels: the register-window matcher (True), the dword memory scan only (False), or per
+# pattern ("auto": the window for a pattern anchored at either end, the scan for floating segments only).
+# scripts/ab_like.py, SF 10 (profiles/r6_like): Q13's '%special%requests%' over every order comment 2.87 ms with the
+# window vs 2.62 with the scan; Q02's '%BRASS' 4.97 vs 5.11
+JIT_LIKE_WINDOW = {"0": False, "1": True}.get(os.environ.get("NSDB_JIT_LIKE_WINDOW", "auto"), "auto")
 JIT_STATS = {"compiled": 0, "disk_hits": 0, "launches": 0, "failed": 0}
 _JIT_FN: Dict[tuple, Optional[int]] = {}     # (device, generated source) -> kernel handle (None: compile failed)
 _JIT_SHAPES: Dict[tuple, tuple] = {}         # program shape -> (kernel handle or None, nreg, rows)
@@ -1242,7 +1247,14 @@ def program_nreg(prog: Program, ncol: int, key_reg: int, val_regs) -> int:
     return n
 
 
-def _jit_ins(pc: int, ins) -> Optional[str]:
+def _like_window(lit: bytes, imm: int) -> bool:
+    if JIT_LIKE_WINDOW != "auto":
+        return bool(JIT_LIKE_WINDOW)
+    off = int(imm) >> 16
+    return bool(lit) and off < len(lit) and (lit[off] & 3) != 0     # anchored start or end
+
+
+def _jit_ins(pc: int, ins, lit: bytes = b"") -> Optional[str]:
     """One instruction as a C++ statement on the register row r (the interpreter's semantics, pipeline.hip run)."""
     op, dst, a, b, c, imm, aux = ins
 
@@ -1288,7 +1300,7 @@ def _jit_ins(pc: int, ins) -> Optional[str]:
         mode = {OP_SEQ: 0, OP_SPRE: 1, OP_SSUF: 2}[op]
         z = f"(u64)str_match(a.col[{b}].dat, {X}, a.lit, a.ins[{pc}].imm, {mode})"
     elif op == OP_SLIKE:
-        z = f"(u64)str_like(a.col[{b}].dat, {X}, a.lit, a.ins[{pc}].imm)"
+        z = f"(u64)str_like<{'true' if _like_window(lit, imm) else 'false'}>(a.col[{b}].dat, {X}, a.lit, a.ins[{pc}].imm)"
     else:
         z = "0ull"
     if c >= 0:
@@ -1338,7 +1350,8 @@ def jit_source(prog: Program, kinds, lates, kind: str, key_reg: int = -1, val_re
     emit_regs = [k[0] for k in getattr(prog, "emit_keys", [])] + list(val_regs)   # -1 / -2: the probe / build row
 
     def seg(lo, hi):
-        body = [t for pc in range(lo, hi) if (t := _jit_ins(pc, prog.ins[pc])) is not None]
+        lit = bytes(prog.lit or b"")
+        body = [t for pc in range(lo, hi) if (t := _jit_ins(pc, prog.ins[pc], lit)) is not None]
         if not body:
             return "    (void)a; (void)R;"
         return ("#pragma unroll\n    for (int j = 0; j < ROWS; ++j) {\n      u64* r = R[j];\n"
@@ -1480,7 +1493,7 @@ def _jit_for(prog: Program, cargs, kind: str, key_reg: int = -1, val_regs=(), de
     shape = (_dev_index(dev), kind, tuple(prog.ins), kinds, lates, key_reg, tuple(val_regs), prog.keep_reg,
              prog.nins_a, getattr(prog, "jk_reg", -1), getattr(prog, "keep2_reg", -1),
              tuple(k[0] for k in getattr(prog, "emit_keys", [])) if kind == "emit" else (), JIT_ROWS, JIT_ROWS_SMALL,
-             JIT_SMALL_NREG)
+             JIT_SMALL_NREG, JIT_LIKE_WINDOW, bytes(prog.lit or b"") if JIT_LIKE_WINDOW == "auto" else b"")
     hit = _JIT_SHAPES.get(shape)
     if hit is None:
         nreg = program_nreg(prog, len(kinds), key_reg, val_regs)

@@ -277,6 +277,7 @@ class AdaptivePlanner:
 
     # A build side at least this large is not chosen blind against a FILTERed scan on the other side of its join.
     MEASURE_BUILD_MIN = 64 << 20
+    MEASURE_RATIO = 16
 
     def _measure_filtered_side(self, e, join: str):
         """About to build ``join`` from ``e`` (the cheapest source, costed by its size): if the join's other side is
@@ -288,6 +289,12 @@ class AdaptivePlanner:
             return None
         for e2 in self.pending:
             if e2 is e or e2[3] != "scan":
+                continue
+            if e[3] == "materialized" and e[2] * self.MEASURE_RATIO <= e2[2]:
+                # the build candidate's size is MEASURED and a small fraction of the scan's: the scan side stays the
+                # larger one unless its filter keeps less than 1 / MEASURE_RATIO, so it probes straight from the scan
+                # (TPC-H Q03: the 1.4 M orders x customer rows build, 32 M late lineitems probe in the fused scan
+                # instead of being materialised first)
                 continue
             ts, c, seen_filter = e2[0], e2[1], False
             st = Stage(0, {"kind": "scan", "atom": e2[4], "ts": ts})

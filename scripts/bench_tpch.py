@@ -109,7 +109,11 @@ def main():
                     fn(c, "tpch")
                     torch.cuda.synchronize()
                     first[tag] = round((time.perf_counter() - t0) * 1e3, 2)
+            from netsdb_amd.execution import kernels as K
+
+            run0 = dict(K.LAST_RUN_AGG)
             got = fn(c, "tpch")                       # untimed first run
+            run_agg = {k: K.LAST_RUN_AGG[k] - run0[k] for k in run0}   # clustered-key group-bys tried / used
             ts = []
             for _ in range(a.rounds):
                 torch.cuda.synchronize()
@@ -151,7 +155,7 @@ def main():
             med = statistics.median(ts)
             row = {"sf": sf, "query": q, "ms_median": round(med * 1e3, 2), "ms_min": round(min(ts) * 1e3, 2),
                    "lineitem_rows_per_s": round(nli / med, 1), "check_vs_pandas": ok,
-                   "pandas_s": None if frames is None else round(t_ref, 2), **first}
+                   "pandas_s": None if frames is None else round(t_ref, 2), "run_agg": run_agg, **first}
             out["results"].append(row)
             print(json.dumps(row), flush=True)
             if stage_times is not None:
