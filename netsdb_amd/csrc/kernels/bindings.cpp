@@ -61,6 +61,9 @@ int nsdb_str_like(const void* bytes, const int64_t* starts, const int64_t* ends,
                   int negate, uint8_t* out, hipStream_t st);
 int nsdb_str_slice(const void* src, const int64_t* starts, int64_t start, const int64_t* out_off, int64_t n,
                    void* dst, hipStream_t st);
+int nsdb_str_like_occ(const void* bytes, int64_t nbytes, int64_t payload_end, const int64_t* starts, const int64_t* ends,
+                      int64_t n, const uint8_t* pat, int pat_len, const int* seg_start, const int* seg_len, int nseg,
+                      int negate, uint64_t* occ, uint8_t* out, hipStream_t st);
 int nsdb_str_eq_pairs(const void* a, const int64_t* sta, const int64_t* ena, const int64_t* ia, const void* b,
                       const int64_t* stb, const int64_t* enb, const int64_t* ib, int64_t m, uint8_t* out,
                       hipStream_t st);
@@ -76,6 +79,8 @@ std::vector<torch::Tensor> hash_aggregate_impl(torch::Tensor keys, c10::optional
 namespace {
 
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+int64_t g_like_occ_min_rows = 1 << 16;   // str_like: rows from which the occurrence-bitmap form is used (0: off)
 
 // Per-call launch options of the block GEMM (gemm.hip GemmOpts): a forced config or an operand prefetch belongs
 // to the one call that passes it.
@@ -560,6 +565,20 @@ torch::Tensor str_like(torch::Tensor bytes, torch::Tensor st, torch::Tensor en, 
   std::vector<int> ss(seg_start.begin(), seg_start.end()), sl(seg_len.begin(), seg_len.end());
   const int64_t n = st.numel();
   auto out = torch::empty({n}, bytes.options());
+  // floating segments over many rows: the buffer-parallel occurrence-bitmap form (strings.hip like_occ_kernel) when
+  // the rows cover the buffer densely (a few rows viewing a large buffer keep the row search: the bitmaps cost the
+  // whole buffer)
+  const int64_t nseg = (int64_t)ss.size(), nwords = (payload_end + 63) / 64;
+  if (!anchor_start && !anchor_end && nseg >= 1 && nseg <= 4 && n >= g_like_occ_min_rows && payload_end <= 256 * n &&
+      (reinterpret_cast<uintptr_t>(bytes.data_ptr()) & 15) == 0) {
+    auto occ = torch::empty({nseg * nwords}, bytes.options().dtype(torch::kInt64));
+    const int rc = nsdb_str_like_occ(bytes.data_ptr(), bytes.numel(), payload_end, st.data_ptr<int64_t>(),
+                                     en.data_ptr<int64_t>(), n, (const uint8_t*)pat.data(), (int)pat.size(), ss.data(),
+                                     sl.data(), (int)nseg, negate, reinterpret_cast<uint64_t*>(occ.data_ptr<int64_t>()),
+                                     out.data_ptr<uint8_t>(), cur_stream());
+    if (rc == 0) return out.view(torch::kBool);
+    TORCH_CHECK(rc == -4, "str_like_occ failed with code ", rc);      // -4: pattern shape not eligible
+  }
   check_rc(nsdb_str_like(bytes.data_ptr(), st.data_ptr<int64_t>(), en.data_ptr<int64_t>(), n, (const uint8_t*)pat.data(),
                          (int)pat.size(), ss.data(), sl.data(), (int)ss.size(), anchor_start, anchor_end, negate,
                          out.data_ptr<uint8_t>(), cur_stream()),
@@ -775,6 +794,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("hash_group_ids", &hash_group_ids, "exact group-by of a device int64 column: (inverse, sorted keys)");
   m.def("str_hash", &str_hash, "64-bit hash per string of a device string column");
   m.def("str_pack", &str_pack, "exact order-preserving int64 code per string of <= 7 bytes");
+  m.def("str_like_occ_min_rows", [](int64_t v) { g_like_occ_min_rows = v <= 0 ? (int64_t(1) << 62) : v; },
+        "rows from which str_like takes the occurrence-bitmap form (<= 0: never; A/B and tests)");
   m.def("str_like", &str_like, "SQL LIKE over a device string column (segments of the pattern bytes)");
   m.def("str_slice", &str_slice, "SUBSTRING of every row of a device string column (no host read)");
   m.def("str_eq_pairs", &str_eq_pairs, "byte-exact equality of string row pairs a[ia[i]] == b[ib[i]]",

@@ -149,6 +149,108 @@ __global__ __launch_bounds__(256) void str_like_kernel(const uint32_t* __restric
   out[i] = (uint8_t)(ok != (pt.negate != 0));
 }
 
+// LIKE with floating segments only ('%a%b%': no anchored end), by occurrence bitmaps instead of a per-row search.
+// Pass 1 scans the WHOLE byte buffer once, buffer-parallel: thread t owns bytes [64 t, 64 t + 64) and writes, per
+// segment, the 64-bit word whose bit o says "the segment matches at byte 64 t + o" (80-byte register window: 5
+// aligned 16-B loads, candidates by the two-byte SWAR test, verified 8 bytes at a time under the '_' mask). Pass 2 is
+// per row: the leftmost set bit of segment 0 in [s, e - len0], then of segment 1 after it, ... — a few bitmap words
+// per row. Greedy leftmost placement is exact for '%'-separated fixed segments, and a bit only counts when the whole
+// occurrence lies inside the row, so matches across row boundaries never leak. Every row is then the same few word
+// reads, where the per-row search (str_like_kernel, and the compiled pipelines' matcher) costs a data-dependent
+// scan of every string: TPC-H Q13's NOT LIKE '%special%requests%' over 15 M order comments.
+constexpr int kOccSegs = 4;
+
+__global__ __launch_bounds__(256) void like_occ_kernel(const uint32_t* __restrict__ w, int64_t nwords, int64_t ndw,
+                                                       LikePattern pt, uint64_t* __restrict__ occ) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nwords) return;
+  uint32_t win[20];
+  const int64_t d0 = t * 16;
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    const int64_t d = d0 + 4 * q;
+    if (d + 4 <= ndw) {
+      const uint4 v = *reinterpret_cast<const uint4*>(w + d);
+      win[4 * q] = v.x;
+      win[4 * q + 1] = v.y;
+      win[4 * q + 2] = v.z;
+      win[4 * q + 3] = v.w;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) win[4 * q + k] = d + k < ndw ? w[d + k] : 0u;
+    }
+  }
+  for (int sg = 0; sg < pt.nseg; ++sg) {
+    const int ss = pt.seg_start[sg], ln = pt.seg_len[sg];
+    const uint32_t B0 = pt.bytes[ss] * 0x01010101u, B1 = pt.bytes[ss + 1] * 0x01010101u;
+    uint64_t v0 = 0, m0 = 0, v1 = 0, m1 = 0;
+    for (int k = 0; k < ln; ++k) {
+      const uint64_t c = pt.bytes[ss + k];
+      if (c == kAnyByte) continue;
+      if (k < 8) {
+        v0 |= c << (8 * k);
+        m0 |= 0xFFull << (8 * k);
+      } else {
+        v1 |= c << (8 * (k - 8));
+        m1 |= 0xFFull << (8 * (k - 8));
+      }
+    }
+    uint64_t bits = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t x1 = (win[i] >> 8) | (win[i + 1] << 24);
+      uint32_t z = zero_bytes(win[i] ^ B0) & zero_bytes(x1 ^ B1);
+      while (z) {
+        const uint32_t o = (uint32_t)__builtin_ctz(z) >> 3;
+        z &= z - 1;
+        const uint64_t lo = (uint64_t)win[i] | ((uint64_t)win[i + 1] << 32), hi = win[i + 2];
+        const uint64_t a = o ? (lo >> (8 * o)) | (hi << (64 - 8 * o)) : lo;
+        bool ok = ((a ^ v0) & m0) == 0;
+        if (ok && ln > 8) {
+          const uint64_t lo2 = (uint64_t)win[i + 2] | ((uint64_t)win[i + 3] << 32), hi2 = win[i + 4];
+          const uint64_t b = o ? (lo2 >> (8 * o)) | (hi2 << (64 - 8 * o)) : lo2;
+          ok = ((b ^ v1) & m1) == 0;
+        }
+        if (ok) bits |= 1ull << (4 * i + o);
+      }
+    }
+    occ[(int64_t)sg * nwords + t] = bits;
+  }
+}
+
+__global__ __launch_bounds__(256) void like_rows_kernel(const int64_t* __restrict__ st, const int64_t* __restrict__ en,
+                                                        int64_t n, const uint64_t* __restrict__ occ, int64_t nwords,
+                                                        LikePattern pt, uint8_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t e = en[i];
+  int64_t pos = st[i];
+  bool ok = true;
+  for (int sg = 0; sg < pt.nseg && ok; ++sg) {
+    const int ln = pt.seg_len[sg];
+    const int64_t last = e - ln;
+    if (last < pos) {
+      ok = false;
+      break;
+    }
+    const uint64_t* ob = occ + (int64_t)sg * nwords;
+    int64_t wi = pos >> 6;
+    uint64_t b = ob[wi] & (~0ull << (pos & 63));
+    int64_t p = -1;
+    while (true) {
+      if (b) {
+        p = wi * 64 + __builtin_ctzll(b);
+        break;
+      }
+      if (++wi * 64 > last) break;
+      b = ob[wi];
+    }
+    ok = p >= 0 && p <= last;
+    pos = p + ln;
+  }
+  out[i] = (uint8_t)(ok != (pt.negate != 0));
+}
+
 // out_off[j] = exclusive prefix of the selected lengths (computed on the device by the caller).
 __global__ __launch_bounds__(256) void str_gather_kernel(const uint8_t* __restrict__ src,
                                                         const int64_t* __restrict__ st,
@@ -264,6 +366,33 @@ int nsdb_str_like(const void* bytes, const int64_t* starts, const int64_t* ends,
   if (n <= 0) return 0;
   hipLaunchKernelGGL(str_like_kernel, dim3(grid_for(n)), dim3(256), 0, st, (const uint32_t*)bytes, starts, ends, n, pt,
                      out);
+  return (int)hipGetLastError();
+}
+
+// The bitmap form of nsdb_str_like: floating segments only (no anchors), 1..kOccSegs segments of 2..16 bytes whose
+// first two bytes are literal (else -4: the caller takes nsdb_str_like). occ: nseg * ceil(payload_end / 64) words of
+// scratch; nbytes: the readable buffer length (payload + pad).
+int nsdb_str_like_occ(const void* bytes, int64_t nbytes, int64_t payload_end, const int64_t* starts, const int64_t* ends,
+                      int64_t n, const uint8_t* pat, int pat_len, const int* seg_start, const int* seg_len, int nseg,
+                      int negate, uint64_t* occ, uint8_t* out, hipStream_t st) {
+  if (pat_len > kPatBytes || nseg < 1 || nseg > kOccSegs || pat_len < 0) return -4;
+  LikePattern pt{};
+  for (int k = 0; k < pat_len; ++k) pt.bytes[k] = pat[k];
+  for (int k = 0; k < nseg; ++k) {
+    if (seg_start[k] < 0 || seg_len[k] < 2 || seg_len[k] > 16 || seg_start[k] + seg_len[k] > pat_len) return -4;
+    if (pat[seg_start[k]] == kAnyByte || pat[seg_start[k] + 1] == kAnyByte) return -4;
+    pt.seg_start[k] = (uint8_t)seg_start[k];
+    pt.seg_len[k] = (uint8_t)seg_len[k];
+  }
+  pt.nseg = nseg;
+  pt.negate = negate;
+  if (n <= 0) return 0;
+  if (reinterpret_cast<uintptr_t>(bytes) & 15) return -4;
+  const int64_t nwords = (payload_end + 63) / 64;
+  if (nwords > 0)
+    hipLaunchKernelGGL(like_occ_kernel, dim3((unsigned)((nwords + 255) / 256)), dim3(256), 0, st,
+                       (const uint32_t*)bytes, nwords, nbytes / 4, pt, occ);
+  hipLaunchKernelGGL(like_rows_kernel, dim3(grid_for(n)), dim3(256), 0, st, starts, ends, n, occ, nwords, pt, out);
   return (int)hipGetLastError();
 }
 

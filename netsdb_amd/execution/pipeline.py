@@ -496,6 +496,9 @@ class _Compiler:
                 if a.kind != "const":
                     self._collect(a, "scmp", seg, out)
             return
+        if e.kind == "like" and _floating_like(e.val[0]):
+            out.append((e, "likemask", seg))           # precomputed per launch (occurrence bitmaps), read as a column
+            return
         if e.kind in ("like", "isin"):
             self._collect(e.args[0], "sref" if e.kind == "like" else "scmp", seg, out)
             return
@@ -506,6 +509,24 @@ class _Compiler:
         return _resolve(e, self.batch, self.build)
 
     def _slot(self, e: E, usage: str, late: bool) -> int:
+        if usage == "likemask":
+            pat = e.val[0]
+            e = e.args[0]
+            obj = self._res(e)
+            if not isinstance(obj, StringColumn):
+                raise Unfusable("LIKE on a non-string")
+            key = (_path(e), ("likemask", pat))
+            if key in self.p.col_index:
+                i = self.p.col_index[key]
+                if not late and self.p.cols[i]["late"] != 2:
+                    self.p.cols[i]["late"] = 0
+                return i
+            if len(self.p.cols) >= MAXCOL:
+                raise Unfusable("columns")
+            self.p.col_index[key] = len(self.p.cols)
+            self.p.cols.append({"kind": C_U8, "late": 2 if _side(e) else int(late), "L": 0, "obj": obj, "expr": e,
+                                "like": pat})
+            return len(self.p.cols) - 1
         obj = self._res(e)
         side = _side(e)
         if usage == "jkey":
@@ -766,6 +787,13 @@ class _Compiler:
             return self._bin(e)
         if e.kind == "like":
             pat, neg = e.val
+            m = p.col_index.get((_path(e.args[0]), ("likemask", pat)))
+            if m is not None:                          # the launch's precomputed match column
+                if not neg:
+                    return m, "b"
+                d = p.temp()
+                p.emit(OP_NOT, d, m)
+                return d, "b"
             r, t = self.gen(e.args[0])
             if t != "s":
                 raise Unfusable("LIKE on a non-string")
@@ -1181,6 +1209,9 @@ def _col_args(prog: Program, dev):
         o = c["obj"]
         if getattr(o, "device", dev) != dev:
             raise Unfusable("a column on another device")
+        if c.get("like") is not None:
+            out.append((C_U8, c["late"], 0, _like_mask(c), None, None, None))
+            continue
         if c["kind"] == C_SCODE:
             # the column's kept fixed-width encoding: a plain int32 (codes of <= 3 bytes) or int64 load
             codes = o.short_codes32(c["L"]) if o.device.type == "cuda" else None
@@ -1629,7 +1660,30 @@ def _value_column(prog: Program, vals: torch.Tensor):
 
 
 # ---------------------------------------------------------------------------------------------- torch interpreter
+def _floating_like(pattern) -> bool:
+    """A LIKE pattern of '%'-separated segments only ('%a%b%'), each 2-16 bytes starting with two literal bytes: the
+    launch precomputes its match column buffer-parallel (StringColumn.like -> strings.hip like_occ_kernel) instead of a
+    per-row search inside the fused kernel. JIT_LIKE_OCC = False keeps every LIKE in the kernel."""
+    if not JIT_LIKE_OCC or not isinstance(pattern, str) or not pattern.startswith("%") or not pattern.endswith("%"):
+        return False
+    from ..objects.strings import _ANY, _compile_like
+
+    buf, st, ln, a0, a1 = _compile_like(pattern)
+    return (not a0 and not a1 and 1 <= len(ln) <= 4 and all(2 <= n <= 16 for n in ln)
+            and all(buf[s] != _ANY and buf[s + 1] != _ANY for s in st))
+
+
+JIT_LIKE_OCC = os.environ.get("NSDB_JIT_LIKE_OCC", "1") != "0"
+
+
+def _like_mask(c: dict) -> torch.Tensor:
+    """The 0/1 match column of a precomputed LIKE (uint8, one per row of the string column)."""
+    return c["obj"].like(c["like"]).view(torch.uint8)
+
+
 def _col_values(c: dict) -> torch.Tensor:
+    if c.get("like") is not None:
+        return _like_mask(c).long()
     o, kind = c["obj"], c["kind"]
     if kind == C_SCODE:
         return o.short_codes(c["L"])

@@ -249,3 +249,44 @@ def test_tpch_result_lists_one_read():
     sc = StringColumn.from_list(["R", "AF", "", "NO"])
     got = _lists({"k": sc, "v": torch.tensor([1.5, 2.0, 0.0, -1.0]), "n": torch.tensor([1, 2, 3, 4]), "l": [9, 8, 7, 6]})
     assert got == {"k": ["R", "AF", "", "NO"], "v": [1.5, 2.0, 0.0, -1.0], "n": [1, 2, 3, 4], "l": [9, 8, 7, 6]}
+
+
+@pytest.mark.gpu
+def test_like_occurrence_bitmaps_gpu():
+    """The buffer-parallel LIKE (strings.hip like_occ_kernel + like_rows_kernel) for floating-segment patterns against
+    the per-row search and a Python regex: occurrences straddling row boundaries must not count, '_' inside a segment,
+    overlapping candidates ('aab' in 'aaab'), segments up to 16 bytes, a row selection viewing a larger buffer."""
+    from netsdb_amd import _ext
+
+    h = _ext.hip()
+    g = torch.Generator().manual_seed(11)
+    alpha = "abcs pecialrequstx"
+    n = 70_000
+    lens = torch.randint(0, 40, (n,), generator=g).tolist()
+    chars = torch.randint(0, len(alpha), (sum(lens),), generator=g).tolist()
+    strs, o = [], 0
+    for ln in lens:
+        strs.append("".join(alpha[c] for c in chars[o:o + ln]))
+        o += ln
+    strs[5] = "xx special yy requests zz"
+    strs[6], strs[7] = "...spec", "ial requests"                 # a match only across the row boundary
+    strs[8] = "aaab" * 3
+    col = StringColumn.from_list(strs, "cuda:0")
+    pats = ["%special%requests%", "%sp%", "%aab%", "%ec_al%", "%ab%ca%bs%", "%pecialrequstxabcs%",
+            "%special requests%"]
+    for pat in pats:
+        ref = [_like_ref(s, pat) for s in strs]
+        h.str_like_occ_min_rows(1 << 62)
+        slow = col.like(pat).cpu().tolist()
+        h.str_like_occ_min_rows(1)
+        fast = col.like(pat).cpu().tolist()
+        neg = col.like(pat, negate=True).cpu().tolist()
+        h.str_like_occ_min_rows(1 << 16)
+        assert slow == ref, pat
+        assert fast == ref, pat
+        assert neg == [not x for x in ref], pat
+    sel = col.take(torch.arange(3, n, 7, device="cuda:0"))
+    h.str_like_occ_min_rows(1)
+    got = sel.like("%special%requests%").cpu().tolist()
+    h.str_like_occ_min_rows(1 << 16)
+    assert got == [_like_ref(strs[i], "%special%requests%") for i in range(3, n, 7)]
