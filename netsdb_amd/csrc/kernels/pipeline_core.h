@@ -762,6 +762,8 @@ __device__ __forceinline__ void jit_emit_body(const PipeArgs& a, unsigned long l
                                               long long cap, long long ostride, unsigned* __restrict__ tile_cnt) {
   constexpr int NR = P::NR, ROWS = P::ROWS, NE = P::NE;
   __shared__ unsigned s_scan[NTHR / 64];
+  __shared__ unsigned s_jscan[ROWS][NTHR / 64];   // per row slot j: each wave's count of emitted rows
+  __shared__ int s_multi[NTHR / 64];              // a wave walked more than one match for some row
   __shared__ unsigned long long s_kept;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long long t0 = (long long)blockIdx.x * tile_rows;
@@ -829,7 +831,9 @@ __device__ __forceinline__ void jit_emit_body(const PipeArgs& a, unsigned long l
         for (int j = 0; j < ROWS; ++j) e += (act[j] && P::keep2(R[j])) ? 1u : 0u;
       }
     }
-    // workgroup exclusive scan of e
+    // workgroup exclusive scan of e (thread-major placement), and per row slot j (row-order placement: with at most
+    // one output per row the block's rows leave in row order — a scan of a table stored in key order then emits its
+    // keys in order, which the sink's clustered-key group-by (relops run_aggregate) needs)
     unsigned x = e;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -837,15 +841,47 @@ __device__ __forceinline__ void jit_emit_body(const PipeArgs& a, unsigned long l
       if (lane >= d) x += y;
     }
     if (lane == 63) s_scan[wave] = x;
+    unsigned cj[ROWS], xj[ROWS];
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      cj[j] = (trips == 1 && keep[j] && P::keep2(R[j])) ? 1u : 0u;
+      unsigned z = cj[j];
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const unsigned y = __shfl_up(z, d, 64);
+        if (lane >= d) z += y;
+      }
+      xj[j] = z;
+      if (lane == 63) s_jscan[j][wave] = z;
+    }
+    if (lane == 0) s_multi[wave] = trips > 1 ? 1 : 0;
     __syncthreads();
     unsigned before = 0, total = 0;
+    bool multi = false;
 #pragma unroll
     for (int w = 0; w < NTHR / 64; ++w) {
       const unsigned v = s_scan[w];
       before += w < wave ? v : 0u;
       total += v;
+      multi |= s_multi[w] != 0;
     }
     long long o = written + before + x - e;
+    long long oj[ROWS];
+    {
+      unsigned long long acc = 0;
+#pragma unroll
+      for (int j = 0; j < ROWS; ++j) {
+        unsigned bj = 0, tj = 0;
+#pragma unroll
+        for (int w = 0; w < NTHR / 64; ++w) {
+          const unsigned v = s_jscan[j][w];
+          bj += w < wave ? v : 0u;
+          tj += v;
+        }
+        oj[j] = written + (long long)acc + bj + xj[j] - cj[j];
+        acc += tj;
+      }
+    }
     if (written + total > cap) ovf = true;
     // write pass
     if (e != 0 && !ovf) {
@@ -855,8 +891,9 @@ __device__ __forceinline__ void jit_emit_body(const PipeArgs& a, unsigned long l
           if (!keep[j] || !P::keep2(R[j])) continue;     // keep[j] => exactly one match (trips <= 1)
           u64 w[NE];
           P::emit(R[j], w, row[j], P::JOIN ? (long long)pay[j] : 0ll);
+          const long long at = multi ? o : oj[j];
 #pragma unroll
-          for (int c = 0; c < NE; ++c) region[c * ostride + o] = w[c];
+          for (int c = 0; c < NE; ++c) region[c * ostride + at] = w[c];
           ++o;
         }
       } else {
