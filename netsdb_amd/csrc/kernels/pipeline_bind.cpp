@@ -57,9 +57,26 @@ struct PipeArgs {
   const long long* jperm;
   unsigned long long jmask;
   long long bn;
+  const unsigned long long* jbloom;
+  long long jbshift;
 };
 
 enum ColKind : int { C_F64 = 0, C_I64, C_I32, C_F32, C_U8, C_SCODE, C_SREF };
+
+// a join table's probe filter (relops join_build's third output; empty: none): W words, one per cap / W home slots
+void set_bloom(PipeArgs& a, int64_t cap, const c10::optional<torch::Tensor>& jbloom, const torch::Tensor& tab) {
+  a.jbloom = nullptr;
+  a.jbshift = 0;
+  if (!jbloom.has_value() || !jbloom->defined() || jbloom->numel() == 0) return;
+  const int64_t W = jbloom->numel();
+  TORCH_CHECK(jbloom->is_cuda() && jbloom->device() == tab.device() && jbloom->scalar_type() == torch::kInt64 &&
+                  jbloom->is_contiguous() && W <= cap && (W & (W - 1)) == 0,
+              "malformed join probe filter");
+  int sh = 0;
+  while ((W << sh) < cap) ++sh;
+  a.jbloom = reinterpret_cast<const unsigned long long*>(jbloom->data_ptr<int64_t>());
+  a.jbshift = sh;
+}
 enum : int { OP_LTF = 10, OP_NEI = 21, OP_SEQ = 26, OP_SPRE = 27, OP_SSUF = 28, OP_SEL = 29, OP_RNGF = 31, OP_RNGI = 32,
              OP_SLIKE = 33, OP_LAST = 33 };
 inline bool is_str_op(int op) { return op == OP_SEQ || op == OP_SPRE || op == OP_SSUF || op == OP_SLIKE; }
@@ -347,7 +364,8 @@ int64_t jit_load(const std::string& code, const std::string& name) {
 torch::Tensor pipe_agg(torch::Tensor prog, int64_t nins_a, ColList cols, torch::Tensor lit, int64_t n, int64_t keep_reg,
                        int64_t key_reg, std::vector<int64_t> val_regs, int64_t agg_op, int64_t max_wg, int64_t tile,
                        std::vector<int64_t> kpool, int64_t jit, int64_t jit_nreg, int64_t jit_rows,
-                       c10::optional<torch::Tensor> jtab, c10::optional<torch::Tensor> jperm, int64_t bn) {
+                       c10::optional<torch::Tensor> jtab, c10::optional<torch::Tensor> jperm, int64_t bn,
+                       c10::optional<torch::Tensor> jbloom) {
   const int ROWS = 4, NTHR = sizes(7), GCAP = sizes(8), CAP = sizes(4);
   PipeArgs a;
   const bool join = jtab.has_value() && jtab->defined();
@@ -368,6 +386,7 @@ torch::Tensor pipe_agg(torch::Tensor prog, int64_t nins_a, ColList cols, torch::
     a.jperm = reinterpret_cast<const long long*>(jperm->data_ptr<int64_t>());
     a.jmask = (unsigned long long)(cap - 1);
     a.bn = bn;
+    set_bloom(a, cap, jbloom, T);
   }
   if (jit != 0) {                                   // the run-time compiled kernel of exactly this program shape
     TORCH_CHECK(a.nreg == jit_nreg && jit_rows >= 1 && jit_rows <= 16,
@@ -405,7 +424,7 @@ std::vector<torch::Tensor> pipe_emit(torch::Tensor prog, int64_t nins_a, ColList
                                      int64_t keep_reg, int64_t key_reg, std::vector<int64_t> val_regs,
                                      std::vector<int64_t> kpool, int64_t jit, int64_t jit_nreg, int64_t jit_rows,
                                      int64_t ne, int64_t tile_rows, int64_t cap, c10::optional<torch::Tensor> jtab,
-                                     c10::optional<torch::Tensor> jperm, int64_t bn) {
+                                     c10::optional<torch::Tensor> jperm, int64_t bn, c10::optional<torch::Tensor> jbloom) {
   const int NTHR = sizes(7);
   PipeArgs a;
   const bool join = jtab.has_value() && jtab->defined();
@@ -428,6 +447,7 @@ std::vector<torch::Tensor> pipe_emit(torch::Tensor prog, int64_t nins_a, ColList
     a.jperm = reinterpret_cast<const long long*>(jperm->data_ptr<int64_t>());
     a.jmask = (unsigned long long)(jcap - 1);
     a.bn = bn;
+    set_bloom(a, jcap, jbloom, T);
   }
   auto i64 = lit.options().dtype(torch::kInt64);
   const int64_t tiles = std::max<int64_t>(1, (n + tile_rows - 1) / tile_rows);
@@ -512,7 +532,8 @@ void register_pipeline(pybind11::module& m) {
         pybind11::arg("keep_reg"), pybind11::arg("key_reg"), pybind11::arg("val_regs"), pybind11::arg("agg_op") = 0,
         pybind11::arg("max_wg") = 0, pybind11::arg("tile") = -1, pybind11::arg("kpool") = std::vector<int64_t>(),
         pybind11::arg("jit") = 0, pybind11::arg("jit_nreg") = 0, pybind11::arg("jit_rows") = 0,
-        pybind11::arg("jtab") = pybind11::none(), pybind11::arg("jperm") = pybind11::none(), pybind11::arg("bn") = -1);
+        pybind11::arg("jtab") = pybind11::none(), pybind11::arg("jperm") = pybind11::none(), pybind11::arg("bn") = -1,
+        pybind11::arg("jbloom") = pybind11::none());
   m.def("pipe_emit", &pipe_emit,
         "fused stage, high-cardinality form: every kept (matched) row's emitted registers as dense int64 columns "
         "[ne, rows], and the host status (overflow, rows through segment A)",
@@ -520,7 +541,7 @@ void register_pipeline(pybind11::module& m) {
         pybind11::arg("keep_reg"), pybind11::arg("key_reg"), pybind11::arg("val_regs"), pybind11::arg("kpool"),
         pybind11::arg("jit"), pybind11::arg("jit_nreg"), pybind11::arg("jit_rows"), pybind11::arg("ne"),
         pybind11::arg("tile_rows"), pybind11::arg("cap"), pybind11::arg("jtab") = pybind11::none(),
-        pybind11::arg("jperm") = pybind11::none(), pybind11::arg("bn") = -1);
+        pybind11::arg("jperm") = pybind11::none(), pybind11::arg("bn") = -1, pybind11::arg("jbloom") = pybind11::none());
   m.def("jit_compile", &jit_compile, "hiprtc compile of a generated pipeline kernel source (gfx950 code object)",
         pybind11::arg("src"), pybind11::arg("header"));
   m.def("jit_version", &jit_version, "hiprtc version of the run-time compiler (code-object cache key)");

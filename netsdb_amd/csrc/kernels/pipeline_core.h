@@ -63,6 +63,9 @@ struct PipeArgs {
   const long long* jperm;
   unsigned long long jmask;
   long long bn;
+  // the table's probe filter (relops.hip join_bloom_kernel; null: none): one word per 2^jbshift home slots
+  const unsigned long long* jbloom;
+  long long jbshift;
 };
 
 typedef unsigned long long u64;
@@ -372,7 +375,10 @@ __device__ __forceinline__ void jit_agg_body(const PipeArgs& a) {
   __shared__ int s_ovf;
   __shared__ unsigned long long s_kept;
   const int tid = threadIdx.x, lane = tid & 63;
-  const double init = a.agg_op == 0 ? 0.0 : (a.agg_op == 1 ? __builtin_inf() : -__builtin_inf());
+  // the aggregation op as a compile-time constant when the generated program fixes it (P::OP >= 0): a run-time op made
+  // every accumulate compute the sum, the min and the max and select (1,303 v_max / v_min_f64 in TPC-H Q01's kernel)
+  const int op = P::OP >= 0 ? P::OP : a.agg_op;
+  const double init = op == 0 ? 0.0 : (op == 1 ? __builtin_inf() : -__builtin_inf());
   for (int i = tid; i < CAP; i += NTHR) tk[i] = EMPTY;
   for (int i = tid; i < CAP * FMAX; i += NTHR) tv[i] = init;
   if (tid == 0) {
@@ -433,7 +439,7 @@ __device__ __forceinline__ void jit_agg_body(const PipeArgs& a) {
       for (int s = 0; s < KSLOT; ++s) {
         if (!done && s < used && sk[s] == key) {
 #pragma unroll
-          for (int f = 0; f < F; ++f) sv[s][f] = acc_op(sv[s][f], v[f], a.agg_op);
+          for (int f = 0; f < F; ++f) sv[s][f] = acc_op(sv[s][f], v[f], op);
           done = true;
         }
       }
@@ -449,7 +455,7 @@ __device__ __forceinline__ void jit_agg_body(const PipeArgs& a) {
         ++used;
       }
       if (!done && !ovf) {
-        ovf = (key == EMPTY) || !table_insert<F>(tk, tv, CAP, key, v, a.nval, a.agg_op);
+        ovf = (key == EMPTY) || !table_insert<F>(tk, tv, CAP, key, v, a.nval, op);
         if (ovf) agg_mark_overflow(a, &s_ovf);
       }
     }
@@ -473,8 +479,8 @@ __device__ __forceinline__ void jit_agg_body(const PipeArgs& a) {
       const bool mine = act && sk[s] == kl;
       double v[F];
 #pragma unroll
-      for (int f = 0; f < F; ++f) v[f] = wave_reduce(mine ? sv[s][f] : init, a.agg_op);
-      if (lane == leader) ovf |= (kl == EMPTY) || !table_insert<F>(tk, tv, CAP, kl, v, a.nval, a.agg_op);
+      for (int f = 0; f < F; ++f) v[f] = wave_reduce(mine ? sv[s][f] : init, op);
+      if (lane == leader) ovf |= (kl == EMPTY) || !table_insert<F>(tk, tv, CAP, kl, v, a.nval, op);
       act = act && !mine;
     }
   }
@@ -489,7 +495,7 @@ __device__ __forceinline__ void jit_agg_body(const PipeArgs& a) {
     double v[F];
 #pragma unroll
     for (int f = 0; f < F; ++f) v[f] = tv[i * FMAX + f];
-    if (!table_insert<F>(gk, gv, GCAP, k, v, a.nval, a.agg_op, GWIN)) s_ovf = 1;
+    if (!table_insert<F>(gk, gv, GCAP, k, v, a.nval, op, GWIN)) s_ovf = 1;
   }
   __syncthreads();
   if (tid == 0) {
@@ -541,17 +547,26 @@ __device__ __forceinline__ void join_find_rows(const PipeArgs& a, const long lon
                                                unsigned (&cnt)[ROWS], unsigned (&pay)[ROWS]) {
   u64 h[ROWS], s[ROWS];
   u64x2 e[ROWS];
+  bool may[ROWS];
 #pragma unroll
   for (int j = 0; j < ROWS; ++j) {
     cnt[j] = 0;
     pay[j] = 0;
     h[j] = fin64((u64)k[j] + JGOLD);
-    s[j] = h[j] == JEMPTY ? a.jmask + 1 : (fin64(h[j]) & a.jmask);
-    if (keep[j]) e[j] = *reinterpret_cast<const u64x2*>(a.jtab + 2 * s[j]);
+    const u64 f = fin64(h[j]);
+    s[j] = h[j] == JEMPTY ? a.jmask + 1 : (f & a.jmask);
+    may[j] = keep[j];
+    if (a.jbloom && keep[j] && h[j] != JEMPTY) {    // the table's probe filter first (L2-resident)
+      const u64 b = (1ull << ((f >> 40) & 63)) | (1ull << ((f >> 46) & 63));
+      may[j] = (a.jbloom[s[j] >> a.jbshift] & b) == b;
+    }
   }
 #pragma unroll
+  for (int j = 0; j < ROWS; ++j)
+    if (may[j]) e[j] = *reinterpret_cast<const u64x2*>(a.jtab + 2 * s[j]);
+#pragma unroll
   for (int j = 0; j < ROWS; ++j) {
-    if (!keep[j]) continue;
+    if (!may[j]) continue;
     for (u64 it = 0; it <= a.jmask; ++it) {       // >= 2 slots per build row: an empty slot ends every chain
       if (e[j][0] == h[j]) {
         cnt[j] = (unsigned)e[j][1] + (h[j] != JEMPTY ? 1u : 0u);
@@ -568,13 +583,14 @@ __device__ __forceinline__ void join_find_rows(const PipeArgs& a, const long lon
 // One kept (key, values) row into the thread's KSLOT register slots, else the workgroup's LDS table.
 template <int F>
 __device__ __forceinline__ void agg_row(const PipeArgs& a, long long key, const double (&v)[F], long long (&sk)[KSLOT],
-                                        double (&sv)[KSLOT][F], int& used, bool& ovf, long long* tk, double* tv) {
+                                        double (&sv)[KSLOT][F], int& used, bool& ovf, long long* tk, double* tv,
+                                        int op) {
   bool done = false;
 #pragma unroll
   for (int s = 0; s < KSLOT; ++s) {
     if (!done && s < used && sk[s] == key) {
 #pragma unroll
-      for (int f = 0; f < F; ++f) sv[s][f] = acc_op(sv[s][f], v[f], a.agg_op);
+      for (int f = 0; f < F; ++f) sv[s][f] = acc_op(sv[s][f], v[f], op);
       done = true;
     }
   }
@@ -590,7 +606,7 @@ __device__ __forceinline__ void agg_row(const PipeArgs& a, long long key, const 
     ++used;
   }
   if (!done && !ovf) {
-    ovf = (key == EMPTY) || !table_insert<F>(tk, tv, CAP, key, v, a.nval, a.agg_op);
+    ovf = (key == EMPTY) || !table_insert<F>(tk, tv, CAP, key, v, a.nval, op);
     if (ovf) __hip_atomic_fetch_or(a.table, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // seen by every loop
   }
 }
@@ -599,7 +615,7 @@ __device__ __forceinline__ void agg_row(const PipeArgs& a, long long key, const 
 template <int F>
 __device__ __forceinline__ void agg_flush(const PipeArgs& a, long long (&sk)[KSLOT], double (&sv)[KSLOT][F], int used,
                                           bool ovf, unsigned long long kept, long long* tk, double* tv, int* s_ovf,
-                                          unsigned long long* s_kept, double init) {
+                                          unsigned long long* s_kept, double init, int op) {
   const int tid = threadIdx.x, lane = tid & 63;
   if (ovf) *s_ovf = 1;
   __syncthreads();
@@ -623,8 +639,8 @@ __device__ __forceinline__ void agg_flush(const PipeArgs& a, long long (&sk)[KSL
       const bool mine = act && sk[s] == kl;
       double v[F];
 #pragma unroll
-      for (int f = 0; f < F; ++f) v[f] = wave_reduce(mine ? sv[s][f] : init, a.agg_op);
-      if (lane == leader) ovf |= (kl == EMPTY) || !table_insert<F>(tk, tv, CAP, kl, v, a.nval, a.agg_op);
+      for (int f = 0; f < F; ++f) v[f] = wave_reduce(mine ? sv[s][f] : init, op);
+      if (lane == leader) ovf |= (kl == EMPTY) || !table_insert<F>(tk, tv, CAP, kl, v, a.nval, op);
       act = act && !mine;
     }
   }
@@ -639,7 +655,7 @@ __device__ __forceinline__ void agg_flush(const PipeArgs& a, long long (&sk)[KSL
     double v[F];
 #pragma unroll
     for (int f = 0; f < F; ++f) v[f] = tv[i * FMAX + f];
-    if (!table_insert<F>(gk, gv, GCAP, k, v, a.nval, a.agg_op, GWIN)) *s_ovf = 1;
+    if (!table_insert<F>(gk, gv, GCAP, k, v, a.nval, op, GWIN)) *s_ovf = 1;
   }
   __syncthreads();
   if (tid == 0) {
@@ -662,7 +678,8 @@ __device__ __forceinline__ void jit_join_agg_body(const PipeArgs& a) {
   __shared__ int s_ovf;
   __shared__ unsigned long long s_kept;
   const int tid = threadIdx.x;
-  const double init = a.agg_op == 0 ? 0.0 : (a.agg_op == 1 ? __builtin_inf() : -__builtin_inf());
+  const int op = P::OP >= 0 ? P::OP : a.agg_op;     // compile-time when the program fixes it (see jit_agg_body)
+  const double init = op == 0 ? 0.0 : (op == 1 ? __builtin_inf() : -__builtin_inf());
   for (int i = tid; i < CAP; i += NTHR) tk[i] = EMPTY;
   for (int i = tid; i < CAP * FMAX; i += NTHR) tv[i] = init;
   if (tid == 0) {
@@ -740,11 +757,11 @@ __device__ __forceinline__ void jit_join_agg_body(const PipeArgs& a) {
         const long long key = P::key(R[j]);
         double v[F];
         P::vals(R[j], v);
-        agg_row<F>(a, key, v, sk, sv, used, ovf, tk, tv);
+        agg_row<F>(a, key, v, sk, sv, used, ovf, tk, tv, op);
       }
     }
   }
-  agg_flush<F>(a, sk, sv, used, ovf, (unsigned long long)kept, tk, tv, &s_ovf, &s_kept, init);
+  agg_flush<F>(a, sk, sv, used, ovf, (unsigned long long)kept, tk, tv, &s_ovf, &s_kept, init, op);
 }
 
 // ---------------------------------------------------------------- emit: (key parts, values) rows for the sink

@@ -25,7 +25,8 @@ int nsdb_join_perm(const int* row_slot, const unsigned* row_rank, long long n, c
                    unsigned long long* bump, void* tab, long long cap, long long* perm, hipStream_t st);
 long long nsdb_join_tiles(long long m);
 int nsdb_join_probe(const void* keys, long long m, const void* tab, long long cap, unsigned* cnt, unsigned* pay,
-                    long long* tile_sum, hipStream_t st);
+                    long long* tile_sum, const unsigned long long* bloom, int bshift, hipStream_t st);
+int nsdb_join_bloom(const void* tab, long long cap, long long W, unsigned long long* bloom, hipStream_t st);
 int nsdb_join_expand(const unsigned* cnt, const unsigned* pay, long long m, const long long* tile_base,
                      const long long* perm, long long* bidx, long long* pidx, hipStream_t st);
 long long nsdb_part_work_bytes(long long n, int P);
@@ -46,6 +47,8 @@ namespace {
 hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
 bool g_agg_mid = true;   // the MID group-by path (agg_set_mid: A/B and tests)
+bool g_join_bloom = true; // probe filters of large join tables (join_set_bloom: A/B and tests)
+int64_t g_join_bloom_min_bytes = int64_t(4) << 20;   // ... of tables with more slot bytes than this (past the L2)
 
 void rc_ok(int rc, const char* what) {
   TORCH_CHECK(rc == 0, what, " failed with code ", rc, " (", hipGetErrorString((hipError_t)(rc > 0 ? rc : 0)), ")");
@@ -224,11 +227,32 @@ std::vector<torch::Tensor> join_build(torch::Tensor keys) {
   rc_ok(nsdb_join_perm(row_slot.data_ptr<int>(), reinterpret_cast<const unsigned*>(row_rank.data_ptr<int>()), n, c,
                        c + 1, tab.data_ptr(), cap, LL(perm.data_ptr<int64_t>()), stream()),
         "join_perm");
-  return {tab, perm};
+  // probe filter for tables past the L2 (> 4 MiB of slots): ~16 filter bits per build row, one word per 2^shift slots
+  torch::Tensor bloom = torch::empty({0}, i64);
+  if (g_join_bloom && cap * 16 > g_join_bloom_min_bytes) {
+    const int64_t W = std::min<int64_t>(cap, pow2_at_least(std::max<int64_t>(64, (16 * n + 63) / 64)));
+    bloom = torch::zeros({W}, i64);
+    rc_ok(nsdb_join_bloom(tab.data_ptr(), cap, W, reinterpret_cast<unsigned long long*>(bloom.data_ptr<int64_t>()),
+                          stream()),
+          "join_bloom");
+  }
+  return {tab, perm, bloom};
+}
+
+// bloom: the table's probe filter from join_build (empty: none); shift = log2(slots per filter word)
+int bloom_shift(const torch::Tensor& tab, const c10::optional<torch::Tensor>& bloom) {
+  if (!bloom.has_value() || !bloom->defined() || bloom->numel() == 0) return -1;
+  const int64_t cap = tab.size(0) - 1, W = bloom->numel();
+  TORCH_CHECK(W <= cap && (W & (W - 1)) == 0 && bloom->is_contiguous() && bloom->scalar_type() == torch::kInt64 &&
+                  bloom->device() == tab.device(), "malformed join probe filter");
+  int sh = 0;
+  while ((W << sh) < cap) ++sh;
+  return sh;
 }
 
 // Probe a built table with m int64 keys: all (build row, probe row) pairs with equal keys, probe-major.
-std::vector<torch::Tensor> join_probe(torch::Tensor tab, torch::Tensor perm, torch::Tensor keys) {
+std::vector<torch::Tensor> join_probe(torch::Tensor tab, torch::Tensor perm, torch::Tensor keys,
+                                      c10::optional<torch::Tensor> bloom) {
   TORCH_CHECK(keys.is_cuda() && keys.scalar_type() == torch::kInt64 && keys.dim() == 1, "keys: 1-D int64 GPU tensor");
   TORCH_CHECK(tab.is_cuda() && tab.scalar_type() == torch::kInt64 && tab.dim() == 2 && tab.size(1) == 2 &&
                   tab.is_contiguous() && perm.scalar_type() == torch::kInt64,
@@ -245,8 +269,11 @@ std::vector<torch::Tensor> join_probe(torch::Tensor tab, torch::Tensor perm, tor
   auto pay = torch::empty({m}, i32);
   const int64_t tiles = nsdb_join_tiles(m);
   auto tsum = torch::empty({tiles + 1}, i64);
+  const int bsh = bloom_shift(tab, bloom);
   rc_ok(nsdb_join_probe(keys.data_ptr(), m, tab.data_ptr(), cap, reinterpret_cast<unsigned*>(cnt.data_ptr<int>()),
-                        reinterpret_cast<unsigned*>(pay.data_ptr<int>()), LL(tsum.data_ptr<int64_t>()), stream()),
+                        reinterpret_cast<unsigned*>(pay.data_ptr<int>()), LL(tsum.data_ptr<int64_t>()),
+                        bsh >= 0 ? reinterpret_cast<const unsigned long long*>(bloom->data_ptr<int64_t>()) : nullptr,
+                        bsh, stream()),
         "join_probe");
   auto incl = torch::cumsum(tsum.narrow(0, 0, tiles), 0);
   const int64_t total = incl[tiles - 1].item<int64_t>();   // sizes the output (one host read)
@@ -392,8 +419,14 @@ void register_relops(pybind11::module& m) {
         pybind11::arg("keys"), pybind11::arg("vals") = pybind11::none(), pybind11::arg("op") = "sum",
         pybind11::arg("want_inv") = false, pybind11::arg("low_threshold") = 0, pybind11::arg("want_first") = true,
         pybind11::arg("scratch") = pybind11::none());
-  m.def("join_build", &join_build, "device hash-join build: (table, perm)");
-  m.def("join_probe", &join_probe, "device hash-join probe: (build_idx, probe_idx)");
+  m.def("join_build", &join_build, "device hash-join build: (table, perm, probe filter (empty: none))");
+  m.def("join_probe", &join_probe, "device hash-join probe: (build_idx, probe_idx)", pybind11::arg("tab"),
+        pybind11::arg("perm"), pybind11::arg("keys"), pybind11::arg("bloom") = pybind11::none());
+  m.def("join_set_bloom", [](bool on, int64_t min_table_bytes) {
+          g_join_bloom = on;
+          g_join_bloom_min_bytes = min_table_bytes;
+        }, "build probe filters for join tables of more than min_table_bytes of slots (default on, 4 MiB)",
+        pybind11::arg("on"), pybind11::arg("min_table_bytes") = int64_t(4) << 20);
   m.def("partition_perm", &partition_perm, "stable device partition permutation: (perm, counts)");
   m.def("agg_set_mid", [](bool on) { g_agg_mid = on; }, "enable / disable the MID group-by path (hash-partitioned LDS "
         "tables sharing their rows through L2); returns nothing", pybind11::arg("on"));

@@ -152,8 +152,9 @@ class JoinTable:
             e = torch.empty(0, dtype=torch.int64, device=dev)
             return e, e
         if self._dev is not None:
-            tab, perm = self._dev
-            return tuple(_ext.hip().join_probe(tab, perm, probe_h.to(tab.device).long().contiguous()))
+            tab, perm = self._dev[0], self._dev[1]
+            bloom = self._dev[2] if len(self._dev) > 2 else None
+            return tuple(_ext.hip().join_probe(tab, perm, probe_h.to(tab.device).long().contiguous(), bloom))
         sh, order = self._sorted
         sh, order = sh.to(dev), order.to(dev)
         lo = torch.searchsorted(sh, probe_h, right=False)

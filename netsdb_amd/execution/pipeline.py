@@ -1166,11 +1166,11 @@ def _launch_emit(prog: Program, n: int, dev, plan: StagePlan, kind: str = "emit"
         raise Unfusable("no emit kernels in this build")
     ins, lit = _prog_tensors(prog, dev)
     cargs = _col_args(prog, dev)
-    jtab = jperm = None
+    jtab = jperm = jbloom = None
     bn = -1
     mult = 1
     if plan.join is not None:
-        jtab, jperm, bn = _join_table(plan, dev)
+        jtab, jperm, bn, jbloom = _join_table(plan, dev)
         # every probe row emits at most the build side's largest key multiplicity: regions sized by it never overflow
         mult = plan.builds[plan.join["name"]].table(dev).max_multiplicity()
         if mult > 64:
@@ -1184,7 +1184,7 @@ def _launch_emit(prog: Program, n: int, dev, plan: StagePlan, kind: str = "emit"
     # a tile's region: its rows times the most matches one probe row can have
     cap = tile * max(1, mult)
     words, status = h.pipe_emit(ins, prog.nins_a, cargs, lit, n, prog.keep_reg, -1, prog.val_regs, prog.kpool, fn,
-                                jnreg, jrows, max(1, ne), tile, cap, jtab, jperm, bn)
+                                jnreg, jrows, max(1, ne), tile, cap, jtab, jperm, bn, jbloom)
     if int(status[0]) != 0:
         return None
     if n:
@@ -1250,6 +1250,9 @@ JIT_SMALL_NREG = 8
 # scripts/ab_like.py, SF 10 (profiles/r6_like): Q13's '%special%requests%' over every order comment 2.87 ms with the
 # window vs 2.62 with the scan; Q02's '%BRASS' 4.97 vs 5.11
 JIT_LIKE_WINDOW = {"0": False, "1": True}.get(os.environ.get("NSDB_JIT_LIKE_WINDOW", "auto"), "auto")
+# the aggregation op compiled into the kernel (True) or read from the launch arguments (False: every accumulate then
+# computes sum, min and max and selects; scripts/ab_pipeline_flag.py --flag JIT_FIXED_OP measures both)
+JIT_FIXED_OP = os.environ.get("NSDB_JIT_FIXED_OP", "1") != "0"
 JIT_STATS = {"compiled": 0, "disk_hits": 0, "launches": 0, "failed": 0}
 _JIT_FN: Dict[tuple, Optional[int]] = {}     # (device, generated source) -> kernel handle (None: compile failed)
 _JIT_SHAPES: Dict[tuple, tuple] = {}         # program shape -> (kernel handle or None, nreg, rows)
@@ -1371,9 +1374,11 @@ def _jit_loads(kinds, lates, late) -> List[str]:
     return out
 
 
-def jit_source(prog: Program, kinds, lates, kind: str, key_reg: int = -1, val_regs=(), rows: int = JIT_ROWS) -> str:
+def jit_source(prog: Program, kinds, lates, kind: str, key_reg: int = -1, val_regs=(), rows: int = JIT_ROWS,
+               agg_op: int = -1) -> str:
     """The C++ source of the compiled kernel of ``prog`` (``kind`` "agg", "emit" or "mask") over columns of these
-    kinds. "emit" writes every kept row's key-part registers (prog.emit_keys) and value registers."""
+    kinds. "emit" writes every kept row's key-part registers (prog.emit_keys) and value registers. ``agg_op`` (0 sum,
+    1 min, 2 max; -1: the launch's argument) fixes the aggregation op at compile time."""
     nreg = program_nreg(prog, len(kinds), key_reg, val_regs)
     F = max(1, len(val_regs))
     staged = kind in ("agg", "emit", "pairs")        # segment A / late columns / segment B split
@@ -1420,7 +1425,7 @@ def jit_source(prog: Program, kinds, lates, kind: str, key_reg: int = -1, val_re
 namespace nsdb_pipe {{
 struct JitProg {{
   static constexpr int F = {F}, NR = {nreg}, ROWS = {rows}, JK = {max(0, getattr(prog, "jk_reg", -1))};
-  static constexpr int NE = {ne};
+  static constexpr int NE = {ne}, OP = {int(agg_op)};
   static constexpr bool JOIN = {"true" if join else "false"};
   template <bool LATE, bool FULL>
   __device__ static __forceinline__ void load(const PipeArgs& a, const long long (&row)[ROWS], const bool (&m)[ROWS],
@@ -1513,7 +1518,7 @@ def jit_kernel(src: str, name: str, dev=None) -> Optional[int]:
     return fn
 
 
-def _jit_for(prog: Program, cargs, kind: str, key_reg: int = -1, val_regs=(), dev=None):
+def _jit_for(prog: Program, cargs, kind: str, key_reg: int = -1, val_regs=(), dev=None, agg_op: int = -1):
     """(kernel handle, nreg, rows) of the compiled kernel for this launch on ``dev``, or None (interpreter)."""
     if not JIT or not hasattr(_ext.hip(), "jit_compile"):
         return None
@@ -1524,13 +1529,14 @@ def _jit_for(prog: Program, cargs, kind: str, key_reg: int = -1, val_regs=(), de
     shape = (_dev_index(dev), kind, tuple(prog.ins), kinds, lates, key_reg, tuple(val_regs), prog.keep_reg,
              prog.nins_a, getattr(prog, "jk_reg", -1), getattr(prog, "keep2_reg", -1),
              tuple(k[0] for k in getattr(prog, "emit_keys", [])) if kind == "emit" else (), JIT_ROWS, JIT_ROWS_SMALL,
-             JIT_SMALL_NREG, JIT_LIKE_WINDOW, bytes(prog.lit or b"") if JIT_LIKE_WINDOW == "auto" else b"")
+             JIT_SMALL_NREG, JIT_LIKE_WINDOW, bytes(prog.lit or b"") if JIT_LIKE_WINDOW == "auto" else b"", agg_op)
     hit = _JIT_SHAPES.get(shape)
     if hit is None:
         nreg = program_nreg(prog, len(kinds), key_reg, val_regs)
         rows = JIT_ROWS_SMALL if nreg <= JIT_SMALL_NREG else JIT_ROWS
         try:
-            src = jit_source(prog, list(kinds), list(lates) or [0] * len(kinds), kind, key_reg, val_regs, rows=rows)
+            src = jit_source(prog, list(kinds), list(lates) or [0] * len(kinds), kind, key_reg, val_regs, rows=rows,
+                             agg_op=agg_op)
         except Unfusable:
             return None
         fn = jit_kernel(src, {"agg": "nsdb_jit_agg", "emit": "nsdb_jit_emit", "pairs": "nsdb_jit_emit"}.get(
@@ -1566,7 +1572,8 @@ def _prog_tensors(prog: Program, dev):
 
 
 def _join_table(plan: StagePlan, dev):
-    """(slots, perm, build rows) of the fused join's device hash table (relops join_build), built on first use."""
+    """(slots, perm, build rows, probe filter or None) of the fused join's device hash table (relops join_build),
+    built on first use."""
     bt = plan.builds[plan.join["name"]]
     if bt.batch is None or bt.batch.n == 0:
         raise Unfusable("empty build side")
@@ -1574,23 +1581,24 @@ def _join_table(plan: StagePlan, dev):
     d = getattr(jt, "_dev", None)
     if d is None:
         raise Unfusable("build side without a device hash table")
-    return d[0], d[1], int(bt.batch.n)
+    return d[0], d[1], int(bt.batch.n), (d[2] if len(d) > 2 and d[2].numel() else None)
 
 
 def _launch(prog: Program, n: int, dev, plan: StagePlan):
     h = _ext.hip()
     ins, lit = _prog_tensors(prog, dev)
     cargs = _col_args(prog, dev)
-    jtab = jperm = None
+    jtab = jperm = jbloom = None
     bn = -1
     if plan.join is not None:
-        jtab, jperm, bn = _join_table(plan, dev)
-    jit = _jit_for(prog, cargs, "agg", prog.key_reg, prog.val_regs, dev)
+        jtab, jperm, bn, jbloom = _join_table(plan, dev)
+    jit = _jit_for(prog, cargs, "agg", prog.key_reg, prog.val_regs, dev,
+                   agg_op=AGG_OPS[plan.op] if JIT_FIXED_OP else -1)
     if jit is None and plan.join is not None:
         raise Unfusable("the fused join probe needs the compiled kernels")
     fn, jnreg, jrows = jit if jit else (0, 0, 0)
     table = h.pipe_agg(ins, prog.nins_a, cargs, lit, n, prog.keep_reg, prog.key_reg, prog.val_regs,
-                       AGG_OPS[plan.op], 0, TILE, prog.kpool, fn, jnreg, jrows, jtab, jperm, bn)
+                       AGG_OPS[plan.op], 0, TILE, prog.kpool, fn, jnreg, jrows, jtab, jperm, bn, jbloom)
     host = _read_table(table)                    # the one device -> host read of the launch
     if int(host[0]) != 0:
         return None
