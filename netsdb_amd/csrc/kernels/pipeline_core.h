@@ -437,11 +437,10 @@ __device__ __forceinline__ void jit_agg_body(const PipeArgs& a) {
       bool done = false;
 #pragma unroll
       for (int s = 0; s < KSLOT; ++s) {
-        if (!done && s < used && sk[s] == key) {
+        const bool hit = !done && s < used && sk[s] == key;   // selects (see the insert below)
 #pragma unroll
-          for (int f = 0; f < F; ++f) sv[s][f] = acc_op(sv[s][f], v[f], op);
-          done = true;
-        }
+        for (int f = 0; f < F; ++f) sv[s][f] = hit ? acc_op(sv[s][f], v[f], op) : sv[s][f];
+        done = done || hit;
       }
       if (!done && used < KSLOT) {
 #pragma unroll
@@ -588,11 +587,10 @@ __device__ __forceinline__ void agg_row(const PipeArgs& a, long long key, const 
   bool done = false;
 #pragma unroll
   for (int s = 0; s < KSLOT; ++s) {
-    if (!done && s < used && sk[s] == key) {
+    const bool hit = !done && s < used && sk[s] == key;   // selects (see the insert below)
 #pragma unroll
-      for (int f = 0; f < F; ++f) sv[s][f] = acc_op(sv[s][f], v[f], op);
-      done = true;
-    }
+    for (int f = 0; f < F; ++f) sv[s][f] = hit ? acc_op(sv[s][f], v[f], op) : sv[s][f];
+    done = done || hit;
   }
   if (!done && used < KSLOT) {
 #pragma unroll

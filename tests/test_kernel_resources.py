@@ -56,7 +56,7 @@ def _tpch_jit_sources(queries):
 
     srcs = {}
 
-    def grab(prog, kind, plan=None):
+    def grab(prog, kind, op="sum"):
         cargs = PL._col_args(prog, torch.device("cpu"))
         kinds, lates = [c[0] for c in cargs], [c[1] for c in cargs]
         key_reg = prog.key_reg if kind == "agg" else -1
@@ -65,7 +65,8 @@ def _tpch_jit_sources(queries):
         if kind == "mask":
             src = PL.jit_source(prog, kinds, [0] * len(kinds), "mask", rows=rows)
         else:
-            src = PL.jit_source(prog, kinds, lates, kind, key_reg, prog.val_regs if kind != "pairs" else (), rows=rows)
+            src = PL.jit_source(prog, kinds, lates, kind, key_reg, prog.val_regs if kind != "pairs" else (), rows=rows,
+                                agg_op=PL.AGG_OPS.get(op, -1) if kind == "agg" else -1)
         srcs.setdefault(src, f"{kind}{len(srcs)}")
 
     saved = {n: getattr(PL, n) for n in ("interpret", "interpret_join", "interpret_emit", "interpret_pairs",
@@ -75,7 +76,8 @@ def _tpch_jit_sources(queries):
         orig = saved[name]
 
         def f(prog, n, *rest):
-            grab(prog, kind)
+            op = rest[0] if rest and isinstance(rest[0], str) else getattr(rest[0], "op", "sum") if rest else "sum"
+            grab(prog, kind, op)
             return orig(prog, n, *rest)
         return f
 
@@ -101,24 +103,37 @@ def _tpch_jit_sources(queries):
     return srcs
 
 
-def test_fused_pipeline_kernels_do_not_spill(tmp_path):
-    """The run-time compiled scan kernels of the TPC-H queries (hiprtc on the GPU; hipcc here, same header) must not
-    use scratch: the fused join aggregation's register slots once compiled to a dynamically indexed private array
-    (112 bytes per lane) and Q12's fused probe ran ~0.7 ms instead of ~0.4."""
-    from concurrent.futures import ThreadPoolExecutor
+def _rtc_resources(src: str, hdr: str):
+    """(scratch bytes, VGPRs) per kernel of a generated source compiled exactly as the GPU run compiles it: hiprtc
+    (the extension's jit_compile, which needs no GPU) and the code object's metadata notes."""
+    from netsdb_amd import _ext
 
-    srcs = _tpch_jit_sources(["q01", "q03", "q04", "q12", "q13", "q14", "q17"])
+    h = _ext.hip()
+    if h is None or not hasattr(h, "jit_compile"):
+        pytest.skip("no hiprtc binding in this build")
+    code = bytes(h.jit_compile(src, hdr))
+    readelf = "/opt/rocm/lib/llvm/bin/llvm-readelf"
+    if not os.path.exists(readelf):
+        pytest.skip("llvm-readelf not available")
+    import tempfile
+
+    with tempfile.NamedTemporaryFile(suffix=".hsaco") as f:
+        f.write(code)
+        f.flush()
+        notes = subprocess.run([readelf, "--notes", f.name], capture_output=True, text=True, timeout=120).stdout
+    scratch = [int(x) for x in re.findall(r"private_segment_fixed_size:\s+(\d+)", notes)]
+    vgprs = [int(x) for x in re.findall(r"\.vgpr_count:\s+(\d+)", notes)]
+    return scratch, vgprs
+
+
+def test_fused_pipeline_kernels_do_not_spill():
+    """The run-time compiled scan kernels of the TPC-H queries must not use scratch, checked on what hiprtc itself
+    produces (it can differ from hipcc: the join-aggregation kernels spilled 80 B/lane under hiprtc and none under
+    hipcc). The fused join aggregation's register slots once compiled to a dynamically indexed private array and
+    Q12's fused probe ran ~0.6 ms instead of ~0.4 (profiles/r6_v6)."""
+    srcs = _tpch_jit_sources(["q01", "q02", "q03", "q04", "q12", "q13", "q14", "q17", "q22"])
     assert any(k.startswith("agg") for k in srcs.values()) and any(k.startswith("emit") for k in srcs.values())
     hdr = open(os.path.join(KDIR, "pipeline_core.h")).read()
     for src, name in srcs.items():
-        # the hiprtc build sees the runtime header implicitly: include it, and the kernel header inline
-        with open(tmp_path / f"{name}.hip", "w") as f:
-            f.write("#include <hip/hip_runtime.h>\n" + src.replace('#include "pipeline_core.h"', hdr))
-
-    def one(name):
-        return name, _resources(str(tmp_path / f"{name}.hip"))
-
-    with ThreadPoolExecutor(4) as ex:
-        for name, res in ex.map(one, srcs.values()):
-            for fn, r in res.items():
-                assert r.get("ScratchSize", 0) == 0, (name, fn, r)
+        scratch, vgprs = _rtc_resources(src, hdr)
+        assert scratch and all(x == 0 for x in scratch), (name, scratch, vgprs)
