@@ -21,7 +21,7 @@ from ..computations import AggregateComp, Computation, TopKComp
 from ..lambdas import Literal, SelfRef
 from ..logical_plan.tcap import bind_atoms, compile_tcap, graph_signature
 from ..objects.nested import NestedColumn
-from ..objects.record import PDBObject, RecordBatch, RecordView, batch_of, column_concat, column_take
+from ..objects.record import PDBObject, RecordBatch, RecordView, batch_of, column_concat, column_take, LazyTakeColumns
 from ..objects.strings import StringColumn
 from ..parallel.comm import ClusterContext
 from ..storage.sets import DenseMatrixSet
@@ -661,8 +661,12 @@ class QueryEngine:
             bbat = RecordBatch(bb_cols, 0)
         else:
             bbat = RecordBatch({c: bt.batch.columns[c] for c in (rcols if side == "left" else lcols)}, bt.batch.n).take(bi)
-        cols = {}
         left, right = (pb, bbat) if side == "left" else (bbat, pb)
+        if isinstance(pb.columns, LazyTakeColumns) or isinstance(bbat.columns, LazyTakeColumns):
+            # both sides stay row selections: a column is gathered when a later atom or sink reads it (a materialised
+            # join output used for one key and two fields gathers those three, not every projected column)
+            return RecordBatch(LazyTakeColumns.merged([(left, lcols), (right, rcols)]), int(pi.numel()))
+        cols = {}
         for c in lcols:
             cols[c] = left.columns[c]
         for c in rcols:

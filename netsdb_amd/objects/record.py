@@ -224,16 +224,37 @@ class LazyTakeColumns(dict):
     every column (iteration, items(), values(), dict(...) and ** materialise what they touch); columns set or
     deleted on it shadow the source."""
 
-    __slots__ = ("_src", "_idx", "_gone")
+    __slots__ = ("_src", "_idx", "_gone", "_idxs")
 
-    def __init__(self, src: Dict[str, Any], idx: torch.Tensor):
+    def __init__(self, src: Dict[str, Any], idx: Optional[torch.Tensor], idxs: Optional[Dict[str, Any]] = None):
         super().__init__()
-        self._src, self._idx, self._gone = src, idx, set()
+        self._src, self._idx, self._gone, self._idxs = src, idx, set(), idxs
 
     def _fetch(self, k):
-        v = column_take(self._src[k], self._idx)
+        idx = self._idx if self._idxs is None else self._idxs[k]
+        v = self._src[k] if idx is None else column_take(self._src[k], idx)
         dict.__setitem__(self, k, v)
         return v
+
+    def _source(self, k):
+        """(source column, row ids or None) of a column not gathered yet."""
+        return self._src[k], (self._idx if self._idxs is None else self._idxs[k])
+
+    @staticmethod
+    def merged(parts) -> "LazyTakeColumns":
+        """The columns of several row selections side by side (a join's output: the probe side's columns at the probe
+        rows next to the build side's at the build rows), each still gathered only when first read. ``parts``: (batch,
+        column names) in output order; a later part's column of the same name wins, as in a dict."""
+        src, idxs = {}, {}
+        for b, names in parts:
+            cols = b.columns
+            lazy = isinstance(cols, LazyTakeColumns)
+            for c in names:
+                if lazy and not dict.__contains__(cols, c) and c not in cols._gone and c in cols._src:
+                    src[c], idxs[c] = cols._source(c)
+                else:
+                    src[c], idxs[c] = cols[c], None
+        return LazyTakeColumns(src, None, idxs)
 
     def __getitem__(self, k):
         if dict.__contains__(self, k):
@@ -427,7 +448,7 @@ class RecordBatch:
         if len(nonempty) == 1:               # nothing to join: a shallow copy (a lazy selection stays lazy)
             c = first.columns
             if isinstance(c, LazyTakeColumns):
-                cp = LazyTakeColumns(c._src, c._idx)
+                cp = LazyTakeColumns(c._src, c._idx, c._idxs)
                 cp._gone = set(c._gone)
                 dict.update(cp, dict.items(c))
             else:
