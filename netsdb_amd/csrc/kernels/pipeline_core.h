@@ -522,6 +522,15 @@ __device__ __forceinline__ u64 fin64(u64 x) {
 }
 
 // build rows matching probe key k: cnt (0 = none) and the payload (the row when cnt == 1, else the run start)
+// Join tables of more than JWHOLE slots probe linearly INSIDE aligned regions of JREGION slots (wrapping at the
+// region's end, not the table's): relops.hip builds them region by region in LDS (kJRegion / kJWholeWrap there: the
+// values must be equal). Smaller tables: plain linear probing over the whole table.
+constexpr unsigned long long JREGION = 4096, JWHOLE = 1ull << 22;
+__device__ __forceinline__ unsigned long long jnext(unsigned long long s, unsigned long long mask) {
+  const unsigned long long rm = mask < JWHOLE ? mask : JREGION - 1;
+  return (s & ~rm) | ((s + 1) & rm);
+}
+
 __device__ __forceinline__ void join_find(const PipeArgs& a, long long k, unsigned& cnt, unsigned& pay) {
   const u64 h = fin64((u64)k + JGOLD);
   u64 s = h == JEMPTY ? a.jmask + 1 : (fin64(h) & a.jmask);
@@ -535,7 +544,7 @@ __device__ __forceinline__ void join_find(const PipeArgs& a, long long k, unsign
       return;
     }
     if (e[0] == JEMPTY || h == JEMPTY) return;
-    s = (s + 1) & a.jmask;
+    s = jnext(s, a.jmask);
   }
 }
 
@@ -573,7 +582,7 @@ __device__ __forceinline__ void join_find_rows(const PipeArgs& a, const long lon
         break;
       }
       if (e[j][0] == JEMPTY || h[j] == JEMPTY) break;
-      s[j] = (s[j] + 1) & a.jmask;
+      s[j] = jnext(s[j], a.jmask);
       e[j] = *reinterpret_cast<const u64x2*>(a.jtab + 2 * s[j]);
     }
   }

@@ -941,6 +941,20 @@ __global__ __launch_bounds__(256) void agg_fix_inv_kernel(i64* __restrict__ inv,
 }
 
 // ---------------------------------------------------------------- hash join
+// Tables of more than kJWholeWrap slots probe linearly inside aligned regions of kJRegion slots (a chain wraps at its
+// region's end) and are built region by region in LDS (join_region_build_kernel); smaller ones (builds up to ~1 M
+// rows, whose table fits the MALL) probe the whole table with plain linear probing and take the global-atomic insert
+// (no region can fill: no host check). Every probe (join_probe_kernel here, pipeline_core.h join_find /
+// join_find_rows, whose JREGION / JWHOLE must equal kJRegion / kJWholeWrap) walks the same order.
+constexpr int kJRegionBits = 12;
+constexpr u64 kJRegion = 1ull << kJRegionBits;
+constexpr u64 kJWholeWrap = 1ull << 22;   // tables of at most this many slots: chains wrap at the table's end
+__device__ __forceinline__ u64 jregion_mask(u64 mask) { return mask < kJWholeWrap ? mask : kJRegion - 1; }
+__device__ __forceinline__ u64 jnext(u64 s, u64 mask) {
+  const u64 rm = jregion_mask(mask);
+  return (s & ~rm) | ((s + 1) & rm);
+}
+
 // Table: cap + 1 16-byte slots {key, cnt | pay << 32} (slot cap: the kEmpty key). cnt counts the key's build rows
 // beyond the first (the kEmpty slot: all of them); pay = the build row itself when the key has one build row (the
 // primary-key case), else the start of its CSR run in perm. A probe row is then ONE 16-byte random read (key, count
@@ -956,7 +970,7 @@ struct JSlot {
 // atomic per row). *ndup counts the rows of rank > 0 (one add per wave): zero means the CSR pass is skipped.
 __global__ __launch_bounds__(256) void join_insert_kernel(const u64* __restrict__ keys, i64 n, JSlot* tab, u64 mask,
                                                           int* __restrict__ row_slot, unsigned* __restrict__ row_rank,
-                                                          unsigned long long* ndup) {
+                                                          unsigned long long* ndup, unsigned* fail) {
   for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) {
     const u64 k = keys[i];
     u64 s;
@@ -965,17 +979,29 @@ __global__ __launch_bounds__(256) void join_insert_kernel(const u64* __restrict_
       s = mask + 1;   // the kEmpty key's own slot: every row counts as an extra, ranks from 1 (fixed below)
     } else {
       s = mix64(k) & mask;
-      for (;;) {   // the table has >= 2 slots per build row: the key or an empty slot is always met
-        u64 cur = __hip_atomic_load(&tab[s].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (cur == kEmpty) {
-          if (__hip_atomic_compare_exchange_strong(&tab[s].key, &cur, k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT)) {
-            claimed = true;
-            break;
-          }
+      // CAS first (no separate load of the slot): a claim is ONE memory-side atomic, and a failed CAS returns the
+      // slot's key, which is all a load would have told (the key itself, or another key: next slot)
+      bool found = false;
+      const u64 rm = jregion_mask(mask);
+      for (u64 it = 0; it <= rm; ++it) {   // bounded: a full region (never at the table's load) raises *fail
+        u64 cur = kEmpty;
+        if (__hip_atomic_compare_exchange_strong(&tab[s].key, &cur, k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+          claimed = true;
+          found = true;
+          break;
         }
-        if (cur == k) break;
-        s = (s + 1) & mask;
+        if (cur == k) {
+          found = true;
+          break;
+        }
+        s = jnext(s, mask);
+      }
+      if (!found) {
+        __hip_atomic_store(fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        row_slot[i] = (int)(mask + 1);
+        row_rank[i] = 0;
+        continue;
       }
     }
     row_slot[i] = (int)s;
@@ -991,6 +1017,12 @@ __global__ __launch_bounds__(256) void join_insert_kernel(const u64* __restrict_
     if (dups != 0 && (threadIdx.x & 63) == (unsigned)(__ffsll((long long)__ballot(1)) - 1))
       __hip_atomic_fetch_add(ndup, (unsigned long long)__popcll(dups), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+}
+
+// Every slot {kEmpty, 0, 0} in one streaming pass of 16-B stores (two strided torch fills wrote each line twice).
+__global__ __launch_bounds__(256) void join_init_kernel(JSlot* tab, i64 nslots) {
+  for (i64 s = (i64)blockIdx.x * blockDim.x + threadIdx.x; s < nslots; s += (i64)gridDim.x * blockDim.x)
+    tab[s] = JSlot{kEmpty, 0u, 0u};
 }
 
 // Runs of the keys with more than one build row, with no host decision: every slot whose key repeated takes a run
@@ -1064,6 +1096,399 @@ __global__ __launch_bounds__(256) void join_perm_kernel(const int* __restrict__ 
 // OR into their home word atomically).
 __device__ __forceinline__ u64 bloom_bits(u64 f) { return (1ull << ((f >> 40) & 63)) | (1ull << ((f >> 46) & 63)); }
 
+// ---- partitioned build of a table of more than one region (cap > kJRegion): rows are partitioned by home region
+// (histogram per workgroup chunk, a bin-major scan, an LDS-ranked scatter of (key, row)), then ONE workgroup per
+// region inserts its rows into an LDS image of the region (LDS CAS / add: no memory-side atomics, which bound the
+// global insert at ~10 G claims/s once the table outgrows the MALL) and writes the region out in one coalesced
+// pass, with its probe-filter words. Bin P holds the rows whose key is kEmpty (the sentinel slot, global atomics).
+// Per row (in partition order) the build keeps its slot and rank for the CSR pass of repeated keys.
+constexpr int kJPartThreads = 512;
+
+// bin of a key: its home region >> sh (sh > 0: the coarse bins of a two-level partition), P for the kEmpty key
+__device__ __forceinline__ unsigned jbin_of(u64 k, u64 mask, unsigned P, int sh) {
+  return k == kEmpty ? P : (unsigned)((mix64(k) & mask) >> (kJRegionBits + sh));
+}
+
+// hist [G chunks][P + 1 bins] (chunk-major: each workgroup's row of counts is one coalesced store); chunk g = rows
+// [g * rpw, min(n, g * rpw + rpw))
+__global__ __launch_bounds__(kJPartThreads) void jpart_hist_kernel(const u64* __restrict__ keys, i64 n, i64 rpw,
+                                                                   u64 mask, unsigned P, int sh,
+                                                                   unsigned* __restrict__ hist,
+                                                                   JSlot* tab) {
+  extern __shared__ unsigned lh[];
+  const unsigned G = gridDim.x, g = blockIdx.x;
+  for (unsigned b = threadIdx.x; b <= P; b += blockDim.x) lh[b] = 0;
+  if (g == 0 && threadIdx.x == 0) tab[mask + 1] = JSlot{kEmpty, 0u, 0u};   // the sentinel slot (bin P uses it)
+  __syncthreads();
+  const i64 r0 = (i64)g * rpw, r1 = min(n, r0 + rpw);
+  constexpr int U = 8;                                  // 8 key loads in flight per thread
+  for (i64 c0 = r0; c0 < r1; c0 += (i64)U * blockDim.x) {
+    u64 k[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const i64 i = c0 + (i64)j * blockDim.x + threadIdx.x;
+      k[j] = i < r1 ? keys[i] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      if (c0 + (i64)j * blockDim.x + threadIdx.x < r1) atomicAdd(&lh[jbin_of(k[j], mask, P, sh)], 1u);
+  }
+  __syncthreads();
+  for (unsigned b = threadIdx.x; b <= P; b += blockDim.x) hist[(i64)g * (P + 1) + b] = lh[b];
+}
+
+// per bin (one thread each): exclusive scan over the G chunks' counts in place, down the column (for each chunk the
+// threads of a wave read adjacent bins: coalesced); the bin's total into btot[b]
+__global__ __launch_bounds__(256) void jpart_colscan_kernel(unsigned* __restrict__ hist, unsigned G, unsigned nb,
+                                                            i64* __restrict__ btot) {
+  const unsigned b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nb) return;
+  unsigned run = 0;
+  constexpr unsigned B = 16;            // 16 chunk counts loaded before any is rewritten: their latencies overlap
+  for (unsigned g0 = 0; g0 < G; g0 += B) {
+    unsigned v[B];
+#pragma unroll
+    for (unsigned j = 0; j < B; ++j) v[j] = g0 + j < G ? hist[(i64)(g0 + j) * nb + b] : 0u;
+#pragma unroll
+    for (unsigned j = 0; j < B; ++j) {
+      if (g0 + j < G) hist[(i64)(g0 + j) * nb + b] = run;
+      run += v[j];
+    }
+  }
+  btot[b] = run;
+}
+
+// one workgroup: bbase[b] = exclusive scan of btot over the P + 1 bins, bbase[P + 1] = n
+__global__ __launch_bounds__(1024) void jpart_totscan_kernel(const i64* __restrict__ btot, unsigned nb,
+                                                             i64* __restrict__ bbase) {
+  __shared__ i64 ws[16], tot;
+  const unsigned per = (nb + 1023) / 1024, b0 = threadIdx.x * per;
+  i64 mine = 0;
+  for (unsigned b = b0; b < min(nb, b0 + per); ++b) mine += btot[b];
+  // block exclusive scan of the 1024 thread sums (64-bit)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  i64 x = mine;
+  for (int d = 1; d < 64; d <<= 1) {
+    const i64 y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) ws[wave] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    i64 acc = 0;
+    for (int w = 0; w < 16; ++w) {
+      const i64 t = ws[w];
+      ws[w] = acc;
+      acc += t;
+    }
+    tot = acc;
+  }
+  __syncthreads();
+  i64 o = ws[wave] + x - mine;
+  for (unsigned b = b0; b < min(nb, b0 + per); ++b) {
+    bbase[b] = o;
+    o += btot[b];
+  }
+  if (threadIdx.x == 0) bbase[nb] = tot;
+}
+
+// scatter: chunk g's rows to bbase[bin] + hist[bin][g] + (LDS rank inside the chunk's share of the bin)
+__global__ __launch_bounds__(kJPartThreads) void jpart_scatter_kernel(const u64* __restrict__ keys, i64 n, i64 rpw,
+                                                                      u64 mask, unsigned P, int sh,
+                                                                      const unsigned* __restrict__ hist,
+                                                                      const i64* __restrict__ bbase,
+                                                                      u64* __restrict__ ikey, unsigned* __restrict__ irow) {
+  extern __shared__ unsigned lo[];     // [P + 1] running offset (relative to bbase) of this chunk in each bin
+  const unsigned G = gridDim.x, g = blockIdx.x;
+  for (unsigned b = threadIdx.x; b <= P; b += blockDim.x) lo[b] = hist[(i64)g * (P + 1) + b];
+  __syncthreads();
+  const i64 r0 = (i64)g * rpw, r1 = min(n, r0 + rpw);
+  constexpr int U = 8;
+  for (i64 c0 = r0; c0 < r1; c0 += (i64)U * blockDim.x) {
+    u64 k[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const i64 i = c0 + (i64)j * blockDim.x + threadIdx.x;
+      k[j] = i < r1 ? keys[i] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const i64 i = c0 + (i64)j * blockDim.x + threadIdx.x;
+      if (i >= r1) continue;
+      const unsigned b = jbin_of(k[j], mask, P, sh);
+      const i64 pos = bbase[b] + atomicAdd(&lo[b], 1u);
+      ikey[pos] = k[j];
+      irow[pos] = (unsigned)i;
+    }
+  }
+}
+
+// The coarse scatter of a two-level partition (<= kJStageBins bins), staged through LDS: each 4096-row tile is
+// counting-sorted by bin in LDS, then written out bin run by bin run (consecutive threads, consecutive addresses of
+// one run: ~16 rows = 128 B of keys per run at 257 bins) instead of every row to a line of its own.
+constexpr int kJStageBins = 1024, kJTileRows = 4096;
+__global__ __launch_bounds__(kJPartThreads) void jpart_scatter_staged_kernel(
+    const u64* __restrict__ keys, i64 n, i64 rpw, u64 mask, unsigned P, int sh, const unsigned* __restrict__ hist,
+    const i64* __restrict__ bbase, u64* __restrict__ ikey, unsigned* __restrict__ irow) {
+  __shared__ u64 lk[kJTileRows];
+  __shared__ unsigned lr[kJTileRows];
+  __shared__ unsigned short lb[kJTileRows];
+  __shared__ unsigned tcnt[kJStageBins], tst[kJStageBins], lo[kJStageBins];
+  __shared__ unsigned wsum[kJPartThreads / 64], tsum;
+  const unsigned G = gridDim.x, g = blockIdx.x, nb = P + 1;
+  for (unsigned b = threadIdx.x; b < nb; b += blockDim.x) lo[b] = (unsigned)(bbase[b] + hist[(i64)g * nb + b]);
+  const i64 r0 = (i64)g * rpw, r1 = min(n, r0 + rpw);
+  constexpr int U = kJTileRows / kJPartThreads;
+  const unsigned per = (nb + kJPartThreads - 1) / kJPartThreads;
+  for (i64 t0 = r0; t0 < r1; t0 += kJTileRows) {
+    u64 k[U];
+    unsigned bj[U], rk[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const i64 i = t0 + j * kJPartThreads + threadIdx.x;
+      k[j] = i < r1 ? keys[i] : 0;
+    }
+    for (unsigned b = threadIdx.x; b < nb; b += blockDim.x) tcnt[b] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const i64 i = t0 + j * kJPartThreads + threadIdx.x;
+      bj[j] = jbin_of(k[j], mask, P, sh);
+      if (i < r1) rk[j] = atomicAdd(&tcnt[bj[j]], 1u);
+    }
+    __syncthreads();
+    // tile-local bin starts: each thread sums `per` consecutive bins, one block scan
+    unsigned mine = 0;
+    for (unsigned q = 0; q < per; ++q) {
+      const unsigned b = threadIdx.x * per + q;
+      if (b < nb) mine += tcnt[b];
+    }
+    unsigned o = block_scan_excl_t<unsigned>(mine, wsum, &tsum);
+    for (unsigned q = 0; q < per; ++q) {
+      const unsigned b = threadIdx.x * per + q;
+      if (b < nb) {
+        tst[b] = o;
+        o += tcnt[b];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const i64 i = t0 + j * kJPartThreads + threadIdx.x;
+      if (i >= r1) continue;
+      const unsigned q = tst[bj[j]] + rk[j];
+      lk[q] = k[j];
+      lr[q] = (unsigned)i;
+      lb[q] = (unsigned short)bj[j];
+    }
+    __syncthreads();
+    const unsigned rows = (unsigned)min((i64)kJTileRows, r1 - t0);
+    for (unsigned q = threadIdx.x; q < rows; q += blockDim.x) {
+      const unsigned b = lb[q];
+      const i64 dst = (i64)lo[b] + (q - tst[b]);
+      ikey[dst] = lk[q];
+      irow[dst] = lr[q];
+    }
+    __syncthreads();
+    for (unsigned b = threadIdx.x; b < nb; b += blockDim.x) lo[b] += tcnt[b];
+    __syncthreads();
+  }
+}
+
+// Second level of a two-level partition (tables of many regions: one scatter over thousands of bins wrote every
+// row to its own cache line): one workgroup per coarse bin c splits its rows over the bin's 2^sh regions (an LDS
+// counting pass, then ranked writes to 2^sh growing runs) and publishes the regions' bases; workgroup Pc carries the
+// kEmpty rows to bin P.
+__global__ __launch_bounds__(1024) void jpart_sub_kernel(const u64* __restrict__ ikey1, const unsigned* __restrict__ irow1,
+                                                         const i64* __restrict__ cbase, u64 mask, int sh, unsigned Pc,
+                                                         unsigned P, i64* __restrict__ bbase, u64* __restrict__ ikey2,
+                                                         unsigned* __restrict__ irow2) {
+  __shared__ unsigned sc[1024], so[1024];
+  const unsigned c = blockIdx.x;
+  const i64 i0 = cbase[c], i1 = cbase[c + 1];
+  if (c == Pc) {
+    for (i64 p = i0 + threadIdx.x; p < i1; p += blockDim.x) {
+      ikey2[p] = ikey1[p];
+      irow2[p] = irow1[p];
+    }
+    if (threadIdx.x == 0) {
+      bbase[P] = i0;
+      bbase[P + 1] = i1;
+    }
+    return;
+  }
+  const unsigned S = 1u << sh, sm = S - 1;
+  for (unsigned j = threadIdx.x; j < S; j += blockDim.x) sc[j] = 0;
+  __syncthreads();
+  constexpr int U = 8;
+  for (i64 c0 = i0; c0 < i1; c0 += (i64)U * blockDim.x) {
+    u64 k[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const i64 p = c0 + (i64)j * blockDim.x + threadIdx.x;
+      k[j] = p < i1 ? ikey1[p] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      if (c0 + (i64)j * blockDim.x + threadIdx.x < i1)
+        atomicAdd(&sc[(unsigned)((mix64(k[j]) & mask) >> kJRegionBits) & sm], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned acc = 0;
+    for (unsigned j = 0; j < S; ++j) {
+      so[j] = acc;
+      bbase[((i64)c << sh) + j] = i0 + acc;
+      acc += sc[j];
+    }
+  }
+  __syncthreads();
+  for (i64 c0 = i0; c0 < i1; c0 += (i64)U * blockDim.x) {
+    u64 k[U];
+    unsigned r[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const i64 p = c0 + (i64)j * blockDim.x + threadIdx.x;
+      k[j] = p < i1 ? ikey1[p] : 0;
+      r[j] = p < i1 ? irow1[p] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (c0 + (i64)j * blockDim.x + threadIdx.x >= i1) continue;
+      const i64 pos = i0 + atomicAdd(&so[(unsigned)((mix64(k[j]) & mask) >> kJRegionBits) & sm], 1u);
+      ikey2[pos] = k[j];
+      irow2[pos] = r[j];
+    }
+  }
+}
+
+// one workgroup per region (blockIdx.x < P) builds it in LDS; workgroup P takes the kEmpty rows. islot / irank per
+// row in partition order; *fail when a region would be left without an empty slot (its chains could not end).
+// bloom: the table's probe filter (nullptr: none), 2^bshift slots per word, bshift <= kJRegionBits.
+__global__ __launch_bounds__(kJPartThreads) void join_region_build_kernel(
+    const u64* __restrict__ ikey, const unsigned* __restrict__ irow, const i64* __restrict__ bbase, u64 mask,
+    unsigned P, JSlot* __restrict__ tab, int* __restrict__ islot, unsigned* __restrict__ irank,
+    unsigned long long* ndup, unsigned* fail, unsigned long long* __restrict__ bloom, int bshift) {
+  __shared__ u64 lkey[kJRegion];
+  __shared__ unsigned lcnt[kJRegion], lpay[kJRegion];
+  __shared__ u64 lbl[kJRegion / 4];
+  __shared__ unsigned nclaim, ndl;
+  const unsigned b = blockIdx.x;
+  const i64 p0 = bbase[b], p1 = bbase[b + 1];
+  if (b == P) {                                  // rows whose key is the kEmpty marker: the sentinel slot
+    const u64 sent = mask + 1;
+    unsigned d = 0;
+    for (i64 p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
+      const unsigned r = __hip_atomic_fetch_add(&tab[sent].cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (r == 0) tab[sent].pay = irow[p];
+      islot[p] = (int)sent;
+      irank[p] = r;
+      d += r != 0;
+    }
+    if (d) __hip_atomic_fetch_add(ndup, (unsigned long long)d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  const u64 rm = kJRegion - 1;
+  const int wpr = bloom ? (int)(kJRegion >> bshift) : 0;   // filter words of this region
+  // the first IPT items of every thread are loaded before the LDS image is cleared (their latency overlaps it),
+  // and each later round's loads are all in flight before its inserts
+  constexpr int IPT = 8;
+  u64 kk[IPT];
+  unsigned rr[IPT];
+  auto load = [&](i64 c0) {
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+      const i64 p = c0 + j * kJPartThreads + threadIdx.x;
+      if (p < p1) {
+        kk[j] = ikey[p];
+        rr[j] = irow[p];
+      }
+    }
+  };
+  load(p0);
+  for (unsigned s = threadIdx.x; s < kJRegion; s += blockDim.x) {
+    lkey[s] = kEmpty;
+    lcnt[s] = 0;
+  }
+  for (int w = threadIdx.x; w < wpr; w += blockDim.x) lbl[w] = 0;
+  if (threadIdx.x == 0) {
+    nclaim = 0;
+    ndl = 0;
+  }
+  __syncthreads();
+  const i64 sbase = (i64)b << kJRegionBits;
+  unsigned d = 0, cl = 0;
+  bool bad = false;
+  for (i64 c0 = p0; c0 < p1; c0 += (i64)IPT * kJPartThreads) {
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+      const i64 p = c0 + j * kJPartThreads + threadIdx.x;
+      if (p >= p1) continue;
+      const u64 k = kk[j];
+      u64 s = mix64(k) & rm;
+      unsigned r = 0;
+      bool done = false;
+      for (u64 it = 0; it < kJRegion; ++it) {
+        const u64 prev = atomicCAS(&lkey[s], kEmpty, k);
+        if (prev == kEmpty) {
+          lpay[s] = rr[j];
+          ++cl;
+          done = true;
+          break;
+        }
+        if (prev == k) {
+          r = atomicAdd(&lcnt[s], 1u) + 1u;
+          done = true;
+          break;
+        }
+        s = (s + 1) & rm;
+      }
+      bad |= !done;
+      islot[p] = (int)(sbase + (i64)s);
+      irank[p] = r;
+      d += r != 0;
+    }
+    if (c0 + (i64)IPT * kJPartThreads < p1) load(c0 + (i64)IPT * kJPartThreads);
+  }
+  if (cl) atomicAdd(&nclaim, cl);
+  if (d) atomicAdd(&ndl, d);
+  if (bad) atomicOr(&ndl, 0x80000000u);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (nclaim >= kJRegion || (ndl & 0x80000000u))
+      __hip_atomic_store(fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned dd = ndl & 0x7fffffffu;
+    if (dd) __hip_atomic_fetch_add(ndup, (unsigned long long)dd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // the region out (16-B slot stores, coalesced), and its filter words from the LDS image
+  for (unsigned s = threadIdx.x; s < kJRegion; s += blockDim.x) {
+    const u64 k = lkey[s];
+    tab[sbase + s] = JSlot{k, lcnt[s], lpay[s]};
+    if (wpr && k != kEmpty) {
+      const u64 f = mix64(k);
+      atomicOr(&lbl[(f & rm) >> bshift], bloom_bits(f));
+    }
+  }
+  if (wpr) {
+    __syncthreads();
+    for (int w = threadIdx.x; w < wpr; w += blockDim.x) bloom[(i64)b * wpr + w] = lbl[w];
+  }
+}
+
+// rows of rank > 0 of a partitioned build: perm[run start + rank] = row (the rows in partition order)
+__global__ __launch_bounds__(256) void join_perm_items_kernel(const int* __restrict__ islot,
+                                                              const unsigned* __restrict__ irank,
+                                                              const unsigned* __restrict__ irow, i64 n,
+                                                              const unsigned long long* ndup, const JSlot* tab,
+                                                              i64* __restrict__ perm) {
+  if (*ndup == 0) return;
+  for (i64 p = (i64)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (i64)gridDim.x * blockDim.x) {
+    const unsigned r = irank[p];
+    if (r == 0) continue;
+    perm[(i64)tab[islot[p]].pay + r] = (i64)irow[p];
+  }
+}
+
 __global__ __launch_bounds__(256) void join_bloom_kernel(const JSlot* __restrict__ tab, u64 mask, int shift, i64 W,
                                                          unsigned long long* __restrict__ bloom) {
   const i64 w = (i64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1129,8 +1554,8 @@ __global__ __launch_bounds__(256) void join_probe_kernel(const u64* __restrict__
       c = e[j].cnt + (k[j] != kEmpty ? 1u : 0u);
       p = e[j].pay;
     } else if (e[j].key != kEmpty && k[j] != kEmpty) {
-      u64 s = (sl[j] + 1) & mask;
-      for (;;) {
+      u64 s = jnext(sl[j], mask);
+      for (u64 it = 0; it <= jregion_mask(mask); ++it) {   // a region always keeps an empty slot (the build checks it)
         const JSlot x = tab[s];
         if (x.key == k[j]) {
           c = x.cnt + 1u;
@@ -1138,7 +1563,7 @@ __global__ __launch_bounds__(256) void join_probe_kernel(const u64* __restrict__
           break;
         }
         if (x.key == kEmpty) break;
-        s = (s + 1) & mask;
+        s = jnext(s, mask);
       }
     }
     cnt[i] = c;
@@ -1550,6 +1975,53 @@ int agg_launch_t(const void* keys, const void* vals, i64 n, int F, int want_inv,
   return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------- multi-column gather
+// dst_c[i] = src_c[idx[i]] for up to kTakeCols columns of one row selection in ONE launch (a join output's columns
+// read together: Q02's lazily gathered columns were ~170 index_select launches per query, each ~6 us of host time).
+// Row width per column 1, 2, 4, 8 or 16 bytes (a column of wider rows is split by the host into 16-B words, a
+// multiple of them per row). blockIdx.y = column: the width switch is uniform per workgroup. Out-of-range ids write
+// zeros and raise *bad (the host checks it with the batch's other reads, never a fault).
+constexpr int kTakeCols = 48;
+struct TakeCol {
+  const char* src;
+  char* dst;
+  long long nsrc;    // rows of the source
+  int w;             // bytes per element: 1, 2, 4, 8, 16
+  int per;           // elements per row (row = per * w bytes)
+};
+struct TakeArgs {
+  TakeCol c[kTakeCols];
+};
+
+template <typename T>
+__device__ __forceinline__ void take_rows(const TakeCol& c, const i64* __restrict__ idx, i64 n, int* bad) {
+  const T* __restrict__ src = reinterpret_cast<const T*>(c.src);
+  T* __restrict__ dst = reinterpret_cast<T*>(c.dst);
+  const i64 tot = n * c.per;
+  for (i64 e = (i64)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (i64)gridDim.x * blockDim.x) {
+    const i64 i = c.per == 1 ? e : e / c.per;
+    const int q = c.per == 1 ? 0 : (int)(e - i * c.per);
+    const i64 r = idx[i];
+    if (r >= 0 && r < c.nsrc) {
+      dst[e] = src[r * c.per + q];
+    } else {
+      dst[e] = T{};
+      *bad = 1;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void take_many_kernel(TakeArgs a, const i64* __restrict__ idx, i64 n, int* bad) {
+  const TakeCol& c = a.c[blockIdx.y];
+  switch (c.w) {
+    case 1: take_rows<unsigned char>(c, idx, n, bad); break;
+    case 2: take_rows<unsigned short>(c, idx, n, bad); break;
+    case 4: take_rows<unsigned>(c, idx, n, bad); break;
+    case 8: take_rows<u64>(c, idx, n, bad); break;
+    default: take_rows<uint4>(c, idx, n, bad); break;
+  }
+}
+
 }  // namespace nsdb_rel
 
 using namespace nsdb_rel;
@@ -1602,14 +2074,121 @@ int nsdb_hash_aggregate(const void* keys, const void* vals, long long n, int F, 
   return (int)hipErrorInvalidValue;
 }
 
+int nsdb_take_many(const void* const* src, void* const* dst, const long long* nsrc, const int* w, const int* per,
+                   int ncols, const long long* idx, long long n, int* bad, hipStream_t st) {
+  if (ncols <= 0 || n <= 0) return 0;
+  if (ncols > kTakeCols) return (int)hipErrorInvalidValue;
+  TakeArgs a{};
+  long long maxe = 0;
+  for (int c = 0; c < ncols; ++c) {
+    if (!(w[c] == 1 || w[c] == 2 || w[c] == 4 || w[c] == 8 || w[c] == 16) || per[c] < 1) return (int)hipErrorInvalidValue;
+    a.c[c] = TakeCol{(const char*)src[c], (char*)dst[c], nsrc[c], w[c], per[c]};
+    maxe = std::max(maxe, n * (long long)per[c]);
+  }
+  const unsigned gx = (unsigned)std::max<long long>(1, std::min<long long>(2048, (maxe + 255) / 256));
+  hipLaunchKernelGGL(take_many_kernel, dim3(gx, (unsigned)ncols), dim3(256), 0, st, a, (const i64*)idx, (i64)n, bad);
+  return (int)hipGetLastError();
+}
+
+// Partitioned build (tables of 2..kJPartMaxRegions regions): bytes of its workspace. Up to kJPartOneLevel regions
+// the rows are partitioned straight into regions; beyond, into kJPartCoarse coarse bins first (sh = log2 of the
+// regions per coarse bin), then split per coarse bin (jpart_sub_kernel).
+constexpr long long kJPartMaxRegions = 8192;
+constexpr unsigned kJPartOneLevel = 2048, kJPartCoarse = 256;
+static void jpart_geometry(long long n, long long cap, unsigned& P, unsigned& G, long long& rpw, int& sh) {
+  P = (unsigned)(cap >> kJRegionBits);
+  G = (unsigned)std::max<long long>(1, std::min<long long>(1024, (n + 16383) / 16384));
+  rpw = (n + G - 1) / G;
+  sh = 0;
+  if (P > kJPartOneLevel)
+    while ((P >> sh) > kJPartCoarse) ++sh;
+}
+long long nsdb_jpart_work_bytes(long long n, long long cap) {
+  unsigned P, G;
+  long long rpw;
+  int sh;
+  jpart_geometry(n, cap, P, G, rpw, sh);
+  const unsigned Pc = P >> sh;
+  const long long hist = (((long long)(Pc + 1) * G * 4) + 15) & ~15LL;
+  return hist + (long long)(Pc + 1) * 8 + (long long)(Pc + 2) * 8 + (long long)(P + 2) * 8 +
+         n * (8 + 4 + 4 + 4) + (sh ? n * 12 : 0) + 64;
+}
+
+// tab: cap + 1 slots (any content: every region and the sentinel slot are written); ctr: 3 zeroed u64 {rows of rank
+// > 0, run bump, fail}; bloom: W = cap >> bshift zeroed-or-not words (every word is written), or nullptr.
+int nsdb_join_build_part(const void* keys, long long n, void* tab, long long cap, void* work,
+                         unsigned long long* ctr, unsigned long long* bloom, int bshift, long long* perm, hipStream_t st) {
+  if (n <= 0 || cap <= (long long)kJWholeWrap || (cap & (cap - 1)) != 0 || cap < 2 * n || cap >= (1LL << 31))
+    return (int)hipErrorInvalidValue;
+  unsigned P, G;
+  long long rpw;
+  int sh;
+  jpart_geometry(n, cap, P, G, rpw, sh);
+  if (P > kJPartMaxRegions || (bloom && (bshift < 2 || bshift > kJRegionBits))) return (int)hipErrorInvalidValue;
+  const unsigned Pc = P >> sh;
+  char* w = (char*)work;
+  unsigned* hist = (unsigned*)w;
+  w += (((long long)(Pc + 1) * G * 4) + 15) & ~15LL;
+  i64* btot = (i64*)w;
+  w += (long long)(Pc + 1) * 8;
+  i64* cbase = (i64*)w;
+  w += (long long)(Pc + 2) * 8;
+  i64* bbase = (i64*)w;
+  w += (long long)(P + 2) * 8;
+  u64* ikey = (u64*)w;
+  w += n * 8;
+  int* islot = (int*)w;
+  w += n * 4;
+  unsigned* irank = (unsigned*)w;
+  w += n * 4;
+  unsigned* irow = (unsigned*)w;
+  w += n * 4;
+  u64* ikey1 = sh ? (u64*)w : ikey;
+  unsigned* irow1 = sh ? (unsigned*)(w + n * 8) : irow;
+  const u64 mask = (u64)(cap - 1);
+  const size_t lds = (size_t)(Pc + 1) * 4;
+  hipLaunchKernelGGL(jpart_hist_kernel, dim3(G), dim3(kJPartThreads), lds, st, (const u64*)keys, (i64)n, (i64)rpw, mask,
+                     Pc, sh, hist, (JSlot*)tab);
+  hipLaunchKernelGGL(jpart_colscan_kernel, dim3((Pc + 1 + 255) / 256), dim3(256), 0, st, hist, G, Pc + 1, btot);
+  hipLaunchKernelGGL(jpart_totscan_kernel, dim3(1), dim3(1024), 0, st, (const i64*)btot, Pc + 1, sh ? cbase : bbase);
+  if (sh && Pc + 1 <= (unsigned)kJStageBins)
+    hipLaunchKernelGGL(jpart_scatter_staged_kernel, dim3(G), dim3(kJPartThreads), 0, st, (const u64*)keys, (i64)n,
+                       (i64)rpw, mask, Pc, sh, (const unsigned*)hist, (const i64*)cbase, ikey1, irow1);
+  else
+    hipLaunchKernelGGL(jpart_scatter_kernel, dim3(G), dim3(kJPartThreads), lds, st, (const u64*)keys, (i64)n, (i64)rpw,
+                       mask, Pc, sh, (const unsigned*)hist, (const i64*)(sh ? cbase : bbase), ikey1, irow1);
+  if (sh)
+    hipLaunchKernelGGL(jpart_sub_kernel, dim3(Pc + 1), dim3(1024), 0, st, (const u64*)ikey1, (const unsigned*)irow1,
+                       (const i64*)cbase, mask, sh, Pc, P, bbase, ikey, irow);
+  hipLaunchKernelGGL(join_region_build_kernel, dim3(P + 1), dim3(kJPartThreads), 0, st, (const u64*)ikey,
+                     (const unsigned*)irow, (const i64*)bbase, mask, P, (JSlot*)tab, islot, irank, ctr,
+                     (unsigned*)(ctr + 2), bloom, bshift);
+  const unsigned gs = (unsigned)std::min<long long>(4096, (cap + 1 + 255) / 256);
+  hipLaunchKernelGGL(join_runs_kernel, dim3(gs), dim3(256), 0, st, (JSlot*)tab, mask, (const unsigned long long*)ctr,
+                     ctr + 1, (i64*)perm);
+  const unsigned g = (unsigned)std::min<long long>(4096, (n + 255) / 256);
+  hipLaunchKernelGGL(join_perm_items_kernel, dim3(g), dim3(256), 0, st, (const int*)islot, (const unsigned*)irank,
+                     (const unsigned*)irow, (i64)n, (const unsigned long long*)ctr, (const JSlot*)tab, (i64*)perm);
+  return (int)hipGetLastError();
+}
+
+// Preset a join table's cap + 1 slots to {kEmpty, 0, 0}.
+int nsdb_join_init(void* tab, long long cap, hipStream_t st) {
+  if (cap <= 0) return (int)hipErrorInvalidValue;
+  const long long nslots = cap + 1;
+  const unsigned g = (unsigned)std::min<long long>(8192, (nslots + 255) / 256);
+  hipLaunchKernelGGL(join_init_kernel, dim3(g), dim3(256), 0, st, (JSlot*)tab, (i64)nslots);
+  return (int)hipGetLastError();
+}
+
 // Join build over n int64 keys: tab [cap + 1] 16-byte slots preset {kEmpty, 0, 0} (cap a power of two >= 2n).
 int nsdb_join_insert(const void* keys, long long n, void* tab, long long cap, int* row_slot, unsigned* row_rank,
-                     unsigned long long* ndup, hipStream_t st) {
+                     unsigned long long* ndup, unsigned* fail, hipStream_t st) {
   if (n <= 0) return 0;
   if (cap <= 0 || (cap & (cap - 1)) != 0 || cap < 2 * n || cap >= (1LL << 31)) return (int)hipErrorInvalidValue;
   const unsigned g = (unsigned)std::min<long long>(4096, (n + 255) / 256);
   hipLaunchKernelGGL(join_insert_kernel, dim3(g), dim3(256), 0, st, (const u64*)keys, n, (JSlot*)tab, (u64)(cap - 1),
-                     row_slot, row_rank, ndup);
+                     row_slot, row_rank, ndup, fail);
   return (int)hipGetLastError();
 }
 

@@ -20,13 +20,19 @@ int nsdb_hash_aggregate(const void* keys, const void* vals, long long n, int F, 
                         void* out, void* inv, long long ocap, int phase, void* work, int pbits, int lcap_low,
                         int lcap_part, int low_thr, int lcap_mid, long long vrs, long long vcs, hipStream_t st);
 int nsdb_join_insert(const void* keys, long long n, void* tab, long long cap, int* row_slot, unsigned* row_rank,
-                     unsigned long long* ndup, hipStream_t st);
+                     unsigned long long* ndup, unsigned* fail, hipStream_t st);
+long long nsdb_jpart_work_bytes(long long n, long long cap);
+int nsdb_join_build_part(const void* keys, long long n, void* tab, long long cap, void* work,
+                         unsigned long long* ctr, unsigned long long* bloom, int bshift, long long* perm, hipStream_t st);
 int nsdb_join_perm(const int* row_slot, const unsigned* row_rank, long long n, const unsigned long long* ndup,
                    unsigned long long* bump, void* tab, long long cap, long long* perm, hipStream_t st);
 long long nsdb_join_tiles(long long m);
 int nsdb_join_probe(const void* keys, long long m, const void* tab, long long cap, unsigned* cnt, unsigned* pay,
                     long long* tile_sum, const unsigned long long* bloom, int bshift, hipStream_t st);
 int nsdb_join_bloom(const void* tab, long long cap, long long W, unsigned long long* bloom, hipStream_t st);
+int nsdb_join_init(void* tab, long long cap, hipStream_t st);
+int nsdb_take_many(const void* const* src, void* const* dst, const long long* nsrc, const int* w, const int* per,
+                   int ncols, const long long* idx, long long n, int* bad, hipStream_t st);
 int nsdb_join_expand(const unsigned* cnt, const unsigned* pay, long long m, const long long* tile_base,
                      const long long* perm, long long* bidx, long long* pidx, hipStream_t st);
 long long nsdb_part_work_bytes(long long n, int P);
@@ -48,6 +54,7 @@ hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
 bool g_agg_mid = true;   // the MID group-by path (agg_set_mid: A/B and tests)
 bool g_join_bloom = true; // probe filters of large join tables (join_set_bloom: A/B and tests)
+bool g_join_part = true;  // partitioned (LDS region) build of multi-region join tables (join_set_part: A/B and tests)
 int64_t g_join_bloom_min_bytes = int64_t(4) << 20;   // ... of tables with more slot bytes than this (past the L2)
 
 void rc_ok(int rc, const char* what) {
@@ -209,34 +216,73 @@ std::vector<torch::Tensor> join_build(torch::Tensor keys) {
   // a selective join, TPC-H Q17's 60 M lineitems against ~2 k parts — expects ~1.1 slot reads instead of ~2.5 at 1/2),
   // <= 1/4 up to 4 M rows, <= 1/2 beyond
   const int64_t f = n <= (int64_t(1) << 18) ? 8 : (n <= (int64_t(1) << 22) ? 4 : 2);
-  const int64_t cap = pow2_at_least(std::max<int64_t>(1024, f * n));
+  int64_t cap = pow2_at_least(std::max<int64_t>(1024, f * n));
   auto i64 = keys.options().dtype(torch::kInt64);
-  // every slot {kEmpty, 0} (two fills: a device tensor built from host values would be a pageable, blocking copy)
-  auto tab = torch::zeros({cap + 1, 2}, i64);
-  tab.select(1, 0).fill_(std::numeric_limits<int64_t>::min());
-  auto row_slot = torch::empty({n}, keys.options().dtype(torch::kInt32));
-  auto row_rank = torch::empty({n}, keys.options().dtype(torch::kInt32));
-  auto ctr = torch::zeros({2}, i64);   // [repeated-key rows, run bump counter]
-  rc_ok(nsdb_join_insert(keys.data_ptr(), n, tab.data_ptr(), cap, row_slot.data_ptr<int>(),
-                         reinterpret_cast<unsigned*>(row_rank.data_ptr<int>()),
-                         reinterpret_cast<unsigned long long*>(ctr.data_ptr<int64_t>()), stream()),
-        "join_insert");
-  // the table keeps each key's EXTRA-row count (join_probe adds the claiming row)
-  auto perm = torch::empty({n}, i64);
-  auto* c = reinterpret_cast<unsigned long long*>(ctr.data_ptr<int64_t>());
-  rc_ok(nsdb_join_perm(row_slot.data_ptr<int>(), reinterpret_cast<const unsigned*>(row_rank.data_ptr<int>()), n, c,
-                       c + 1, tab.data_ptr(), cap, LL(perm.data_ptr<int64_t>()), stream()),
-        "join_perm");
-  // probe filter for tables past the L2 (> 4 MiB of slots): ~16 filter bits per build row, one word per 2^shift slots
-  torch::Tensor bloom = torch::empty({0}, i64);
-  if (g_join_bloom && cap * 16 > g_join_bloom_min_bytes) {
-    const int64_t W = std::min<int64_t>(cap, pow2_at_least(std::max<int64_t>(64, (16 * n + 63) / 64)));
-    bloom = torch::zeros({W}, i64);
-    rc_ok(nsdb_join_bloom(tab.data_ptr(), cap, W, reinterpret_cast<unsigned long long*>(bloom.data_ptr<int64_t>()),
-                          stream()),
-          "join_bloom");
+  // Tables of more than 2^22 slots: chains wrap inside regions of kJRegion = 4096 slots (relops.hip), the table is
+  // built region by region in LDS (join_build_part) and checked once on the host for a region left without an empty
+  // slot (a hash pile-up far outside the load's statistics), in which case it doubles and is rebuilt. Smaller ones:
+  // the global insert, whole-table linear probing.
+  constexpr int64_t R = 4096, kMaxRegions = 8192, kWhole = int64_t(1) << 22;   // relops.hip kJRegion, kJWholeWrap
+  for (int attempt = 0;; ++attempt) {
+    auto tab = torch::empty({cap + 1, 2}, i64);
+    auto ctr = torch::zeros({3}, i64);   // [repeated-key rows, run bump counter, fail]
+    auto* c = reinterpret_cast<unsigned long long*>(ctr.data_ptr<int64_t>());
+    auto perm = torch::empty({n}, i64);
+    // probe filter for tables past the L2 (> 4 MiB of slots): ~16 filter bits per build row, one word per 2^shift slots
+    torch::Tensor bloom = torch::empty({0}, i64);
+    int bshift = -1;
+    if (g_join_bloom && cap * 16 > g_join_bloom_min_bytes) {
+      const int64_t W = std::min<int64_t>(cap, pow2_at_least(std::max<int64_t>(64, (16 * n + 63) / 64)));
+      bshift = 0;
+      while ((W << bshift) < cap) ++bshift;
+      bloom = torch::empty({W}, i64);
+    }
+    const bool regions = cap > kWhole;                        // chains wrap inside 4096-slot regions
+    const bool part = regions && (cap / R) <= kMaxRegions && g_join_part;
+    bool bloom_done = false;
+    if (part) {
+      const bool fold = bshift >= 2 && bshift <= 12;          // filter words written with their region
+      auto work = torch::empty({(nsdb_jpart_work_bytes(n, cap) + 7) / 8}, i64);
+      rc_ok(nsdb_join_build_part(keys.data_ptr(), n, tab.data_ptr(), cap, work.data_ptr(), c,
+                                 fold ? reinterpret_cast<unsigned long long*>(bloom.data_ptr<int64_t>()) : nullptr,
+                                 bshift, LL(perm.data_ptr<int64_t>()), stream()),
+            "join_build_part");
+      bloom_done = fold;
+    } else {
+      rc_ok(nsdb_join_init(tab.data_ptr(), cap, stream()), "join_init");
+      auto row_slot = torch::empty({n}, keys.options().dtype(torch::kInt32));
+      auto row_rank = torch::empty({n}, keys.options().dtype(torch::kInt32));
+      rc_ok(nsdb_join_insert(keys.data_ptr(), n, tab.data_ptr(), cap, row_slot.data_ptr<int>(),
+                             reinterpret_cast<unsigned*>(row_rank.data_ptr<int>()), c,
+                             reinterpret_cast<unsigned*>(c + 2), stream()),
+            "join_insert");
+      // the table keeps each key's EXTRA-row count (join_probe adds the claiming row)
+      rc_ok(nsdb_join_perm(row_slot.data_ptr<int>(), reinterpret_cast<const unsigned*>(row_rank.data_ptr<int>()), n, c,
+                           c + 1, tab.data_ptr(), cap, LL(perm.data_ptr<int64_t>()), stream()),
+            "join_perm");
+    }
+    if (bshift >= 0 && !bloom_done) {
+      bloom.zero_();
+      rc_ok(nsdb_join_bloom(tab.data_ptr(), cap, bloom.numel(),
+                            reinterpret_cast<unsigned long long*>(bloom.data_ptr<int64_t>()), stream()),
+            "join_bloom");
+    }
+    // Region tables (builds past ~1 M rows) read {fail, largest extra-row count} in one transfer: a region left
+    // without an empty slot is rebuilt larger; the count is the table's max multiplicity - 1 (JoinTable
+    // .max_multiplicity, which sizes the fused probes' output regions, needs no read of its own). Whole-table tables
+    // cannot fill (load <= 1/2): no host read.
+    torch::Tensor stat = torch::empty({0}, i64);
+    if (regions) {
+      stat = torch::stack({ctr[2], tab.select(1, 1).bitwise_and(0xFFFFFFFFLL).max()}).cpu();
+      if (stat[0].item<int64_t>() != 0) {                    // a region without an empty slot: rebuild larger
+        TORCH_CHECK(attempt < 2 && cap * 2 < (int64_t(1) << 31),
+                    "join_build: hash regions overflow even at ", cap, " slots for ", n, " rows");
+        cap *= 2;
+        continue;
+      }
+    }
+    return {tab, perm, bloom, stat};
   }
-  return {tab, perm, bloom};
 }
 
 // bloom: the table's probe filter from join_build (empty: none); shift = log2(slots per filter word)
@@ -406,6 +452,54 @@ std::vector<torch::Tensor> run_aggregate(torch::Tensor keys, c10::optional<torch
   return {okey, oagg, ocnt, heads};
 }
 
+
+// Rows idx of several device columns in one launch (relops.hip take_many_kernel). Every column: a contiguous tensor
+// on idx's device whose rows (dim 0) are 1, 2, 4, 8 or a multiple of 16 bytes wide (narrower multi-byte rows are
+// copied element by element). Returns the gathered columns and a device flag word (1: an id was out of range).
+// bad: an int32 device word the kernel sets on an out-of-range id (kept by the caller across calls and checked with
+// its other reads: no per-call fill launch)
+std::vector<torch::Tensor> take_many(std::vector<torch::Tensor> cols, torch::Tensor idx, torch::Tensor bad) {
+  TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == torch::kInt64 && idx.dim() == 1, "take_many: idx 1-D int64 GPU");
+  TORCH_CHECK(bad.is_cuda() && bad.device() == idx.device() && bad.scalar_type() == torch::kInt32 && bad.numel() >= 1,
+              "take_many: bad must be an int32 word on idx's device");
+  idx = idx.contiguous();
+  const int64_t n = idx.numel();
+  std::vector<torch::Tensor> out;
+  out.reserve(cols.size());
+  std::vector<const void*> src;
+  std::vector<void*> dst;
+  std::vector<long long> nsrc;
+  std::vector<int> w, per;
+  auto flush = [&]() {
+    if (!src.empty())
+      rc_ok(nsdb_take_many(src.data(), dst.data(), nsrc.data(), w.data(), per.data(), (int)src.size(),
+                           LL(idx.data_ptr<int64_t>()), n, bad.data_ptr<int>(), stream()), "take_many");
+    src.clear(); dst.clear(); nsrc.clear(); w.clear(); per.clear();
+  };
+  for (auto& c : cols) {
+    TORCH_CHECK(c.is_cuda() && c.device() == idx.device() && c.dim() >= 1 && c.is_contiguous(),
+                "take_many: contiguous columns on idx's device expected");
+    auto sizes = c.sizes().vec();
+    sizes[0] = n;
+    auto o = torch::empty(sizes, c.options());
+    out.push_back(o);
+    TORCH_CHECK(n == 0 || c.size(0) > 0, "take_many: row ids into an empty column");
+    const int64_t rowb = c.numel() == 0 ? 0 : (int64_t)c.nbytes() / c.size(0);
+    if (n == 0 || rowb == 0) continue;
+    int ww, pp;
+    if (rowb == 1 || rowb == 2 || rowb == 4 || rowb == 8) { ww = (int)rowb; pp = 1; }
+    else if (rowb % 16 == 0) { ww = 16; pp = (int)(rowb / 16); }
+    else { ww = (int)c.element_size(); pp = (int)(rowb / ww); }
+    if (reinterpret_cast<uintptr_t>(c.data_ptr()) % ww != 0) {   // a view at an offset: element-wide copies
+      ww = (int)c.element_size();
+      pp = (int)(rowb / ww);
+    }
+    src.push_back(c.data_ptr()); dst.push_back(o.data_ptr()); nsrc.push_back(c.size(0)); w.push_back(ww); per.push_back(pp);
+    if ((int)src.size() == 48) flush();
+  }
+  flush();
+  return out;
+}
 }  // namespace
 
 std::vector<torch::Tensor> hash_aggregate_impl(torch::Tensor keys, c10::optional<torch::Tensor> vals,
@@ -419,7 +513,10 @@ void register_relops(pybind11::module& m) {
         pybind11::arg("keys"), pybind11::arg("vals") = pybind11::none(), pybind11::arg("op") = "sum",
         pybind11::arg("want_inv") = false, pybind11::arg("low_threshold") = 0, pybind11::arg("want_first") = true,
         pybind11::arg("scratch") = pybind11::none());
-  m.def("join_build", &join_build, "device hash-join build: (table, perm, probe filter (empty: none))");
+  m.def("take_many", &take_many, "rows idx of several device columns in one launch (bad: int32 device word set on "
+        "an out-of-range id)", pybind11::arg("cols"), pybind11::arg("idx"), pybind11::arg("bad"));
+  m.def("join_build", &join_build, "device hash-join build: (table, perm, probe filter (empty: none), host [fail, "
+        "largest extra-row count] (empty: not read))");
   m.def("join_probe", &join_probe, "device hash-join probe: (build_idx, probe_idx)", pybind11::arg("tab"),
         pybind11::arg("perm"), pybind11::arg("keys"), pybind11::arg("bloom") = pybind11::none());
   m.def("join_set_bloom", [](bool on, int64_t min_table_bytes) {
@@ -427,6 +524,8 @@ void register_relops(pybind11::module& m) {
           g_join_bloom_min_bytes = min_table_bytes;
         }, "build probe filters for join tables of more than min_table_bytes of slots (default on, 4 MiB)",
         pybind11::arg("on"), pybind11::arg("min_table_bytes") = int64_t(4) << 20);
+  m.def("join_set_part", [](bool on) { g_join_part = on; }, "partitioned LDS-region build of join tables of more than "
+        "one 4096-slot region (default on; off: the global-atomic insert)", pybind11::arg("on"));
   m.def("partition_perm", &partition_perm, "stable device partition permutation: (perm, counts)");
   m.def("agg_set_mid", [](bool on) { g_agg_mid = on; }, "enable / disable the MID group-by path (hash-partitioned LDS "
         "tables sharing their rows through L2); returns nothing", pybind11::arg("on"));

@@ -125,6 +125,9 @@ class JoinTable:
         self._sorted = None
         if self.n and build_h.is_cuda and self.n < JOIN_TABLE_MAX_ROWS:
             self._dev = _ext.hip().join_build(build_h.long().contiguous())
+            st = self._dev[3] if len(self._dev) > 3 else None
+            if st is not None and st.numel():                 # the build's own host read carried the max count
+                self._max_mult = int(st[1]) + 1
         elif self.n:
             # builds past the device table's 2^29-row bound (32-bit payloads): sorted keys + binary search, on the device
             self._sorted = torch.sort(build_h)

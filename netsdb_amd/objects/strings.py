@@ -37,8 +37,18 @@ def to_host(*ts: torch.Tensor) -> List[torch.Tensor]:
     """Host copies of several tensors with ONE synchronisation: device tensors are copied asynchronously (into
     pinned buffers) and the stream is synchronised once, instead of one blocking read per tensor."""
     out = [t.to("cpu", non_blocking=True) if t.device.type == "cuda" else t for t in ts]
-    for d in {t.device for t in ts if t.device.type == "cuda"}:     # every device the copies were queued on
+    devs = {t.device for t in ts if t.device.type == "cuda"}
+    # the multi-column gathers' out-of-range words ride along (record.take_many): a bad row id fails loudly at the
+    # next batched host read instead of leaving zeros behind, at no extra synchronisation
+    from .record import _TAKE_BAD
+
+    flags = [(d, _TAKE_BAD[d], _TAKE_BAD[d].to("cpu", non_blocking=True)) for d in devs if d in _TAKE_BAD]
+    for d in devs:                                              # every device the copies were queued on
         torch.cuda.current_stream(d).synchronize()
+    for d, dev_word, host_word in flags:
+        if int(host_word[0]) != 0:
+            dev_word.zero_()
+            raise IndexError(f"take_many: a row id was out of range on {d} (a lazily gathered column)")
     return out
 
 

@@ -1,7 +1,9 @@
 """A/B of a fused-pipeline switch (a module attribute of netsdb_amd.execution.pipeline, e.g. JIT_FIXED_OP,
-JIT_LIKE_WINDOW, JIT_ROWS) on TPC-H queries: interleaved rounds, every arm's answer checked equal to the first arm's.
+JIT_LIKE_WINDOW, JIT_ROWS; or hip:<setter> of the HIP extension, e.g. hip:join_set_part) on TPC-H queries:
+interleaved rounds, every arm's answer checked equal to the first arm's.
 
     python scripts/ab_pipeline_flag.py --flag JIT_FIXED_OP --values True,False [--sf 10] [--rounds 5] [--queries q01,q06]
+    python scripts/ab_pipeline_flag.py --flag hip:join_set_part --values True,False --queries q03,q22
 """
 import argparse
 import ast
@@ -34,18 +36,26 @@ def main():
     c = PDBClient(root=tempfile.mkdtemp(), device="cuda:0")
     tpch.load(c, "tpch", t, device="cuda:0")
     del t
-    orig = getattr(PL, a.flag)
+    from netsdb_amd import _ext
+
+    if a.flag.startswith("hip:"):                 # a setter of the HIP extension (its default is the first value)
+        setter = getattr(_ext.hip(), a.flag[4:])
+        setf = lambda v: setter(v)  # noqa: E731
+        orig = vals[0]
+    else:
+        setf = lambda v: setattr(PL, a.flag, v)  # noqa: E731
+        orig = getattr(PL, a.flag)
     out = {"flag": a.flag, "sf": a.sf}
     for q in a.queries.split(","):
         fn = tpch.QUERIES[q]
         res, ts = [], {str(v): [] for v in vals}
         for v in vals:
-            setattr(PL, a.flag, v)
+            setf(v)
             res.append(fn(c, "tpch"))
             fn(c, "tpch")
         for _ in range(a.rounds):
             for v in vals:
-                setattr(PL, a.flag, v)
+                setf(v)
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 fn(c, "tpch")
@@ -55,7 +65,7 @@ def main():
                   **{f"{k}_ms": round(statistics.median(x), 3) for k, x in ts.items()},
                   **{f"{k}_all": [round(y, 3) for y in x] for k, x in ts.items()}}
         print(json.dumps({q: out[q]}), flush=True)
-    setattr(PL, a.flag, orig)
+    setf(orig)
     print(json.dumps(out))
 
 

@@ -138,6 +138,15 @@ def main():
         assert torch.equal(b2[bi2], p2[pi2]) and pi2.numel() == int((p2 > 0).sum())
         t = run({"build": lambda: K.JoinTable(b2), "probe": lambda: jt2.probe(p2),
                  "build_probe": lambda: K.JoinTable(b2).probe(p2)}, a.rounds)
+        # the same probe against a table built without its probe filter (~90 % of the probes match: the filter
+        # word is a second dependent read for most rows)
+        _ext.hip().join_set_bloom(False)
+        try:
+            jt3 = K.JoinTable(b2)
+        finally:
+            _ext.hip().join_set_bloom(True)
+        t.update({"probe_no_filter": run({"p": lambda: jt3.probe(p2)}, a.rounds)["p"]})
+        del jt3
         t["build_rows"], t["probe_rows"], t["matches"] = nb2, n, int(pi2.numel())
         out["join_sweep"][str(nb2)] = t
         print(json.dumps({"join_sweep": nb2, **t}), flush=True)

@@ -644,3 +644,148 @@ def test_tpch_join_queries_with_probe_filters_gpu(tmp_path):
                     assert (a[k] == pytest.approx(v, rel=1e-9, abs=1e-6)) if isinstance(v, float) else a[k] == v, (q, k)
     finally:
         h.join_set_bloom(True)
+
+
+@pytest.mark.gpu
+def test_take_many_matches_index_select():
+    """relops take_many (one launch for many columns) equals index_select per column: every row width (1/2/4/8 B,
+    16-B multiples, odd multiples of the element), views at unaligned offsets, 2-D rows, and the bad-id word."""
+    from netsdb_amd.objects.record import take_many, take_many_check
+
+    dev = "cuda"
+    g = torch.Generator(device=dev).manual_seed(5)
+    n = 10_000
+    cols = [torch.randint(0, 255, (n,), device=dev, dtype=torch.uint8),
+            torch.randn(n, device=dev).to(torch.bfloat16),
+            torch.randn(n, device=dev),
+            torch.randint(-2**62, 2**62, (n,), device=dev, generator=g),
+            torch.randn(n, 4, device=dev),                       # 16-B rows
+            torch.randn(n, 3, device=dev, dtype=torch.float64),  # 24-B rows: 8-B elements
+            torch.randn(n, 3, device=dev),                       # 12-B rows
+            torch.randn(n + 1, device=dev, dtype=torch.float64)[1:],   # an 8-B-aligned view
+            torch.randn(n * 4 + 1, device=dev)[1:].view(n, 4)]         # 16-B rows at a 4-B offset
+    idx = torch.randint(0, n, (3000,), device=dev, generator=g)
+    got = take_many(cols, idx)
+    for c, o in zip(cols, got):
+        assert o.shape == (3000,) + tuple(c.shape[1:]) and torch.equal(o, c.index_select(0, idx))
+    assert take_many_check()
+    bad = idx.clone()
+    bad[7] = n + 5
+    take_many(cols[:2], bad)
+    assert not take_many_check() and take_many_check()
+    take_many(cols[:2], bad)
+    from netsdb_amd.objects.strings import to_host
+
+    with pytest.raises(IndexError):                      # surfaces at the next batched host read
+        to_host(idx)
+    assert take_many_check()
+    assert [o.numel() for o in take_many(cols[:3], idx[:0])] == [0, 0, 0]
+
+
+@pytest.mark.gpu
+def test_lazy_selection_group_gather(monkeypatch):
+    """A small lazy selection's first read gathers all of its pending columns (strings too) in one take_many launch;
+    the values are those of per-column takes, a large one still gathers column by column."""
+    from netsdb_amd.objects import record as R
+
+    dev = "cuda"
+    n = 5000
+    s = StringColumn.from_list([f"s{i % 97}" * (1 + i % 3) for i in range(n)], dev)
+    src = {"a": torch.arange(n, device=dev), "b": torch.randn(n, device=dev), "s": s,
+           "t": torch.randn(n, 2, device=dev)}
+    idx = torch.randint(0, n, (777,), device=dev)
+    calls = []
+    real = R.take_many
+    monkeypatch.setattr(R, "take_many", lambda c, i: calls.append(len(c)) or real(c, i))
+    lz = R.LazyTakeColumns(src, idx)
+    assert torch.equal(lz["b"], src["b"][idx])
+    assert calls == [5]                                   # a, b, t, s.starts, s.ends
+    assert torch.equal(lz["a"], idx) and torch.equal(lz["t"], src["t"][idx])
+    assert lz["s"].tolist() == s.take(idx).tolist() and calls == [5]
+    monkeypatch.setattr(R, "GROUP_TAKE_MAX_ROWS", 100)
+    lz2 = R.LazyTakeColumns(src, idx)
+    assert torch.equal(lz2["b"], src["b"][idx]) and calls == [5]
+
+
+def _unmix64(y: int) -> int:
+    """Inverse of relops.hip mix64 (splitmix64's finaliser): keys whose table home slots the test chooses."""
+    m = (1 << 64) - 1
+    y ^= (y >> 31) ^ (y >> 62)
+    y = (y * pow(0x94D049BB133111EB, -1, 1 << 64)) & m
+    y ^= (y >> 27) ^ (y >> 54)
+    y = (y * pow(0xBF58476D1CE4E5B9, -1, 1 << 64)) & m
+    y ^= (y >> 30) ^ (y >> 60)
+    return y
+
+
+def test_unmix64_inverts_mix64():
+    from netsdb_amd.objects.strings import _mix_py
+
+    for x in (0, 1, 12345, (1 << 64) - 1, 0x8000000000000001):
+        assert _unmix64(_mix_py(x)) == x
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,distinct", [(50_000, 50_000), (600_000, 150_000), (3_000_000, 3_000_000),
+                                        (6_000_000, 2_000_000)])   # the last: a two-level partition (4096 regions)
+def test_join_partitioned_build_matches_global_insert(n, distinct):
+    """The LDS region build (tables of more than one 4096-slot region) and the global-atomic insert give the same
+    pairs, with repeated keys (CSR runs), kEmpty-marker rows and the probe filter; the table's slot contents agree
+    as a set (claims may differ in which row of a repeated key is rank 0)."""
+    g = torch.Generator(device=DEV).manual_seed(11)
+    build = torch.randint(0, distinct, (n,), device=DEV, generator=g) * 7 + 3
+    build[::1001] = torch.iinfo(torch.int64).min
+    probe = torch.randint(0, distinct + distinct // 3, (200_000,), device=DEV, generator=g) * 7 + 3
+    probe[::37] = torch.iinfo(torch.int64).min
+    h = _ext.hip()
+    outs = []
+    for part in (True, False):
+        h.join_set_part(part)
+        try:
+            tab, perm, bloom, stat = h.join_build(build)
+            if tab.shape[0] - 1 > (1 << 22):              # region tables carry the build's host read
+                m = int(torch.unique(build, return_counts=True)[1].max())   # the kEmpty slot counts +1: a bound
+                assert stat.numel() == 2 and int(stat[0]) == 0 and m <= int(stat[1]) + 1 <= m + 1
+            else:
+                assert stat.numel() == 0                   # whole-table tables: no host read in the build
+            bi, pi = h.join_probe(tab, perm, probe, bloom)
+        finally:
+            h.join_set_part(True)
+        assert torch.equal(build[bi], probe[pi]) and bool((pi[1:] >= pi[:-1]).all())
+        keys = tab[:, 0].sort().values
+        outs.append((sorted(zip(pi.tolist(), bi.tolist())), keys, bloom))
+    assert outs[0][0] == outs[1][0]
+    assert torch.equal(outs[0][1], outs[1][1])
+    assert torch.equal(outs[0][2], outs[1][2])          # probe filters built in the region pass = the filter kernel's
+
+
+@pytest.mark.gpu
+def test_join_region_overflow_rebuilds_larger():
+    """A region table (past 2^22 slots): 6,000 distinct keys whose home slots all fall in ONE 4096-slot region of the
+    first 2^23-slot table, next to 1.1 M random keys. The build sees a region without an empty slot, doubles the table
+    (the crafted keys then split over two regions) and every key is found."""
+    rng = torch.Generator().manual_seed(3)
+    hi = torch.randint(0, 1 << 38, (6000,), generator=rng).tolist()
+    lo = torch.randint(0, 1 << 12, (6000,), generator=rng).tolist()
+    vals = {(int(a) << 24) | (int(a) & 1) << 23 | (int(b) & 0xFFF) for a, b in zip(hi, lo)}   # bits 12..22 zero
+    crafted = [(_unmix64(v) ^ (1 << 63)) - (1 << 63) for v in vals]    # as signed int64
+    crafted = torch.tensor([k for k in crafted if k != -(1 << 63)], dtype=torch.int64)
+    rnd = torch.randint(-(1 << 62), 1 << 62, (1_100_000,), generator=rng)
+    build = torch.unique(torch.cat([crafted, rnd]))
+    build = build[torch.randperm(build.numel(), generator=rng)].to(DEV)
+    tab, perm, bloom, stat = _ext.hip().join_build(build)
+    assert tab.shape[0] - 1 == 1 << 24 and int(stat[0]) == 0             # rebuilt once, larger
+    bi, pi = _ext.hip().join_probe(tab, perm, build, bloom)
+    assert torch.equal(pi, torch.arange(build.numel(), device=DEV)) and torch.equal(bi, pi)
+
+
+def test_join_region_constants_agree():
+    """relops.hip and pipeline_core.h (the fused probes) must walk the same probe order."""
+    import re
+    from pathlib import Path
+
+    kd = Path(__file__).resolve().parents[1] / "netsdb_amd" / "csrc" / "kernels"
+    r = (kd / "relops.hip").read_text()
+    c = (kd / "pipeline_core.h").read_text()
+    assert re.search(r"constexpr int kJRegionBits = 12;", r) and "constexpr u64 kJWholeWrap = 1ull << 22;" in r
+    assert "constexpr unsigned long long JREGION = 4096, JWHOLE = 1ull << 22;" in c
