@@ -56,6 +56,7 @@ bool g_agg_mid = true;   // the MID group-by path (agg_set_mid: A/B and tests)
 bool g_join_bloom = true; // probe filters of large join tables (join_set_bloom: A/B and tests)
 bool g_join_part = true;  // partitioned (LDS region) build of multi-region join tables (join_set_part: A/B and tests)
 int64_t g_join_bloom_min_bytes = int64_t(4) << 20;   // ... of tables with more slot bytes than this (past the L2)
+int64_t g_join_bloom_max_bytes = int64_t(4) << 20;   // ... whose filter has at most this many bytes
 
 void rc_ok(int rc, const char* what) {
   TORCH_CHECK(rc == 0, what, " failed with code ", rc, " (", hipGetErrorString((hipError_t)(rc > 0 ? rc : 0)), ")");
@@ -231,7 +232,11 @@ std::vector<torch::Tensor> join_build(torch::Tensor keys) {
     // probe filter for tables past the L2 (> 4 MiB of slots): ~16 filter bits per build row, one word per 2^shift slots
     torch::Tensor bloom = torch::empty({0}, i64);
     int bshift = -1;
-    if (g_join_bloom && cap * 16 > g_join_bloom_min_bytes) {
+    // ... while the filter itself stays L2-sized (<= 4 MiB: builds up to ~2 M rows). A larger one sits in the MALL
+    // next to the table, and its word is a second dependent far read for every probe that matches (16 M-row build,
+    // 90 % matching probes: 0.89 ms with the filter, 0.70 without, profiles/r6_join)
+    if (g_join_bloom && cap * 16 > g_join_bloom_min_bytes &&
+        std::min<int64_t>(cap, pow2_at_least(std::max<int64_t>(64, (16 * n + 63) / 64))) * 8 <= g_join_bloom_max_bytes) {
       const int64_t W = std::min<int64_t>(cap, pow2_at_least(std::max<int64_t>(64, (16 * n + 63) / 64)));
       bshift = 0;
       while ((W << bshift) < cap) ++bshift;
@@ -519,11 +524,14 @@ void register_relops(pybind11::module& m) {
         "largest extra-row count] (empty: not read))");
   m.def("join_probe", &join_probe, "device hash-join probe: (build_idx, probe_idx)", pybind11::arg("tab"),
         pybind11::arg("perm"), pybind11::arg("keys"), pybind11::arg("bloom") = pybind11::none());
-  m.def("join_set_bloom", [](bool on, int64_t min_table_bytes) {
+  m.def("join_set_bloom", [](bool on, int64_t min_table_bytes, int64_t max_filter_bytes) {
           g_join_bloom = on;
           g_join_bloom_min_bytes = min_table_bytes;
-        }, "build probe filters for join tables of more than min_table_bytes of slots (default on, 4 MiB)",
-        pybind11::arg("on"), pybind11::arg("min_table_bytes") = int64_t(4) << 20);
+          g_join_bloom_max_bytes = max_filter_bytes;
+        }, "build probe filters for join tables of more than min_table_bytes of slots whose filter has at most "
+        "max_filter_bytes (default on, 4 MiB, 4 MiB)",
+        pybind11::arg("on"), pybind11::arg("min_table_bytes") = int64_t(4) << 20,
+        pybind11::arg("max_filter_bytes") = int64_t(4) << 20);
   m.def("join_set_part", [](bool on) { g_join_part = on; }, "partitioned LDS-region build of join tables of more than "
         "one 4096-slot region (default on; off: the global-atomic insert)", pybind11::arg("on"));
   m.def("partition_perm", &partition_perm, "stable device partition permutation: (perm, counts)");

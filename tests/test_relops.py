@@ -741,6 +741,7 @@ def test_join_partitioned_build_matches_global_insert(n, distinct):
     outs = []
     for part in (True, False):
         h.join_set_part(part)
+        h.join_set_bloom(True, 4 << 20, 1 << 40)              # filters on every table past 4 MiB, however large
         try:
             tab, perm, bloom, stat = h.join_build(build)
             if tab.shape[0] - 1 > (1 << 22):              # region tables carry the build's host read
@@ -751,6 +752,7 @@ def test_join_partitioned_build_matches_global_insert(n, distinct):
             bi, pi = h.join_probe(tab, perm, probe, bloom)
         finally:
             h.join_set_part(True)
+            h.join_set_bloom(True)
         assert torch.equal(build[bi], probe[pi]) and bool((pi[1:] >= pi[:-1]).all())
         keys = tab[:, 0].sort().values
         outs.append((sorted(zip(pi.tolist(), bi.tolist())), keys, bloom))
