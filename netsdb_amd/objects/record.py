@@ -283,16 +283,19 @@ class LazyTakeColumns(dict):
             if ci is not idx:
                 continue
             v = self._src[c]
+            # contiguous sources only: a strided view (a column of a stacked value matrix) would be copied whole by
+            # .contiguous() for a small gather; it keeps its own index_select
             if isinstance(v, StringColumn):
-                if v.data.device != idx.device:
+                if v.data.device != idx.device or not (v.starts.is_contiguous() and v.ends.is_contiguous()):
                     continue
                 names.append((c, v))
                 parts.append(2)
-                srcs += [v.starts.contiguous(), v.ends.contiguous()]
-            elif isinstance(v, torch.Tensor) and v.device == idx.device and v.dim() >= 1 and v.dtype != torch.bool:
+                srcs += [v.starts, v.ends]
+            elif (isinstance(v, torch.Tensor) and v.device == idx.device and v.dim() >= 1 and v.dtype != torch.bool
+                  and v.is_contiguous()):
                 names.append((c, v))
                 parts.append(1)
-                srcs.append(v.contiguous())
+                srcs.append(v)
         if len(srcs) < 2:
             return
         out = take_many(srcs, idx)
