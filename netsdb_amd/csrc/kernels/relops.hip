@@ -1116,7 +1116,7 @@ __global__ __launch_bounds__(kJPartThreads) void jpart_hist_kernel(const u64* __
                                                                    unsigned* __restrict__ hist,
                                                                    JSlot* tab) {
   extern __shared__ unsigned lh[];
-  const unsigned G = gridDim.x, g = blockIdx.x;
+  const unsigned g = blockIdx.x;
   for (unsigned b = threadIdx.x; b <= P; b += blockDim.x) lh[b] = 0;
   if (g == 0 && threadIdx.x == 0) tab[mask + 1] = JSlot{kEmpty, 0u, 0u};   // the sentinel slot (bin P uses it)
   __syncthreads();
@@ -1199,7 +1199,7 @@ __global__ __launch_bounds__(kJPartThreads) void jpart_scatter_kernel(const u64*
                                                                       const i64* __restrict__ bbase,
                                                                       u64* __restrict__ ikey, unsigned* __restrict__ irow) {
   extern __shared__ unsigned lo[];     // [P + 1] running offset (relative to bbase) of this chunk in each bin
-  const unsigned G = gridDim.x, g = blockIdx.x;
+  const unsigned g = blockIdx.x;
   for (unsigned b = threadIdx.x; b <= P; b += blockDim.x) lo[b] = hist[(i64)g * (P + 1) + b];
   __syncthreads();
   const i64 r0 = (i64)g * rpw, r1 = min(n, r0 + rpw);
@@ -1235,7 +1235,7 @@ __global__ __launch_bounds__(kJPartThreads) void jpart_scatter_staged_kernel(
   __shared__ unsigned short lb[kJTileRows];
   __shared__ unsigned tcnt[kJStageBins], tst[kJStageBins], lo[kJStageBins];
   __shared__ unsigned wsum[kJPartThreads / 64], tsum;
-  const unsigned G = gridDim.x, g = blockIdx.x, nb = P + 1;
+  const unsigned g = blockIdx.x, nb = P + 1;
   for (unsigned b = threadIdx.x; b < nb; b += blockDim.x) lo[b] = (unsigned)(bbase[b] + hist[(i64)g * nb + b]);
   const i64 r0 = (i64)g * rpw, r1 = min(n, r0 + rpw);
   constexpr int U = kJTileRows / kJPartThreads;

@@ -4,6 +4,7 @@ interleaved rounds, every arm's answer checked equal to the first arm's.
 
     python scripts/ab_pipeline_flag.py --flag JIT_FIXED_OP --values True,False [--sf 10] [--rounds 5] [--queries q01,q06]
     python scripts/ab_pipeline_flag.py --flag hip:join_set_part --values True,False --queries q03,q22
+    python scripts/ab_pipeline_flag.py --flag objects.record:GROUP_TAKE_MAX_ROWS --values 262144,0 --queries q02
 """
 import argparse
 import ast
@@ -42,6 +43,13 @@ def main():
         setter = getattr(_ext.hip(), a.flag[4:])
         setf = lambda v: setter(v)  # noqa: E731
         orig = vals[0]
+    elif ":" in a.flag:                           # module:ATTR of another netsdb_amd module
+        import importlib
+
+        mname, attr = a.flag.split(":", 1)
+        mod = importlib.import_module(f"netsdb_amd.{mname}")
+        setf = lambda v: setattr(mod, attr, v)  # noqa: E731
+        orig = getattr(mod, attr)
     else:
         setf = lambda v: setattr(PL, a.flag, v)  # noqa: E731
         orig = getattr(PL, a.flag)
