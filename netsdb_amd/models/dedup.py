@@ -499,6 +499,19 @@ class SharedInference:
             with torch.cuda.stream(side):
                 Yp = self._private(X, None)
             X.record_stream(side)
+        xp = ps = None
+        if (side is None and self.prefetch_x and X.is_cuda and self.w_common is not None
+                and self.w_priv is not None):
+            # the private columns of X compacted on a second stream while the common panel's GEMM streams its
+            # weights on the main one (a 20 MB copy next to a 900 MB stream, instead of serialised between them)
+            main = torch.cuda.current_stream(X.device)
+            ps = SharedInference._side.get(X.device)
+            if ps is None:
+                ps = SharedInference._side[X.device] = torch.cuda.Stream(X.device)
+            ps.wait_stream(main)
+            with torch.cuda.stream(ps):
+                xp = [(off, self._compact(xv)) for off, xv in self._xpart(X, self.priv_cols, self.priv_runs)]
+            X.record_stream(ps)
         P = None
         if self.w_common is not None:
             for off, xv in self._xpart(X, self.common_cols, self.common_runs):
@@ -511,7 +524,11 @@ class SharedInference:
             Yp.record_stream(main)
             Y = Yp.add_(P.unsqueeze(0))
         else:
-            Y = self._private(X, P)
+            if xp is not None:
+                main.wait_stream(ps)
+                for _, xv in xp:
+                    xv.record_stream(main)
+            Y = self._private(X, P, xp)
         return {n: Y[i, : self.R] for i, n in enumerate(self.names)}
 
     # Private panels concurrent with the common panel (run(): two HIP streams), the private result joined by one
@@ -519,17 +536,22 @@ class SharedInference:
     # runs: 0.492 vs 0.480 ms, profiles/r6_dedup/dedup_overlap_ab.json: both GEMMs already stream HBM with the whole
     # GPU, so running them side by side only splits the bandwidth), so it is off by default.
     overlap = False
+    prefetch_x = False   # compact X's private columns on a second stream during the common GEMM (A/B: bench_dedup)
     _side: Dict[torch.device, "torch.cuda.Stream"] = {}
 
-    def _private(self, X: torch.Tensor, Y: Optional[torch.Tensor]) -> torch.Tensor:
+    @staticmethod
+    def _compact(xv: torch.Tensor) -> torch.Tensor:
+        # a narrow private slice of X is compacted first (a 20 MB copy; the GEMM then streams B rows 200 KB apart
+        # instead of 2 MB apart: 266 vs 296 us at 12 x 500 x 100 x 100k)
+        return xv.contiguous() if xv.stride(0) > 2 * xv.shape[1] else xv
+
+    def _private(self, X: torch.Tensor, Y: Optional[torch.Tensor], parts=None) -> torch.Tensor:
         from .. import ops
 
         M = self.w_priv.shape[0]
-        for off, xv in self._xpart(X, self.priv_cols, self.priv_runs):
+        for off, xv in (parts if parts is not None else self._xpart(X, self.priv_cols, self.priv_runs)):
             wv = self.w_priv[:, :, off: off + xv.shape[1]]
-            # a narrow private slice of X is compacted first (a 20 MB copy; the GEMM then streams B
-            # rows 200 KB apart instead of 2 MB apart: 266 vs 296 us at 12 x 500 x 100 x 100k)
-            xv = xv.contiguous() if xv.stride(0) > 2 * xv.shape[1] else xv
+            xv = self._compact(xv)
             xb = xv.unsqueeze(0).expand(M, -1, -1)            # batch stride 0: one X panel for every model
             Y = ops.gemm_nt(wv, xb, Y, ops.BIAS_MAT if Y is not None else ops.BIAS_NONE, out_dtype=torch.float32)
         return Y

@@ -54,6 +54,10 @@ def main():
     ap.add_argument("--small", action="store_true", help="CPU / contract size (8 models of 20 x 4000, blocks 10 x 400)")
     ap.add_argument("--overlap", type=int, default=0,
                     help="1: the private panels' GEMM on a second stream, concurrent with the common panel's")
+    ap.add_argument("--prefetch-x", type=int, default=-1,
+                    help="1 / 0: compact X's private columns on a second stream during the common GEMM (-1: default)")
+    ap.add_argument("--ab-prefetch", type=int, default=0,
+                    help="N > 0: also time N interleaved rounds of prefetch-x off / on (ab_prefetch in the JSON)")
     ap.add_argument("--ab-overlap", type=int, default=0,
                     help="N > 0: also time N interleaved rounds of overlap off / on (ab_overlap in the JSON)")
     a = ap.parse_args()
@@ -191,6 +195,8 @@ def main():
 
     if si is not None:
         si.overlap = bool(a.overlap)
+        if a.prefetch_x >= 0:
+            si.prefetch_x = bool(a.prefetch_x)
     for _ in range(a.warmup):
         infer_naive()
         infer_dedup()
@@ -205,6 +211,16 @@ def main():
                 infer_dedup()
                 ab[k].append(round(timed(infer_dedup, max(a.steps, 20)) * 1e3, 4))
         si.overlap = bool(a.overlap)
+    abp = None
+    if a.ab_prefetch > 0 and si is not None:
+        keep = si.prefetch_x
+        abp = {"off_ms": [], "on_ms": []}
+        for _ in range(a.ab_prefetch):
+            for flag, k in ((False, "off_ms"), (True, "on_ms")):
+                si.prefetch_x = flag
+                infer_dedup()
+                abp[k].append(round(timed(infer_dedup, max(a.steps, 20)) * 1e3, 4))
+        si.prefetch_x = keep
 
     err = None
     if a.check and 0 in mine:
@@ -229,7 +245,8 @@ def main():
             "infer_dedup_ms": round(t_dedup * 1e3, 3), "dedup_speedup": round(t_naive / t_dedup, 2),
             "panel_GB_dedup": round((si.panel_bytes() if si else 0) / 1e9, 3),
             "panel_GB_naive": round(len(mine) * R * C * 2 / 1e9, 3), "rel_err_model0": err,
-            "overlap": bool(a.overlap), "ab_overlap": ab, **comm}), flush=True)
+            "overlap": bool(a.overlap), "ab_overlap": ab,
+            "prefetch_x": bool(si.prefetch_x) if si is not None else None, "ab_prefetch": abp, **comm}), flush=True)
     if ctx.distributed:
         torch.distributed.destroy_process_group()
 
